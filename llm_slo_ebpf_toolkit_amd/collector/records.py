@@ -1,0 +1,181 @@
+"""Binary event/span record formats shared by the BPF probes, the native ring and the GPU.
+
+* ``REF_EVENT`` -- REF's packed 40-byte ``struct llm_slo_event``
+  (ebpf/c/llm_slo_event.h:32-42). Accepted for replay compatibility; decoded with REF's
+  exact rules (pkg/collector/ringbuf.go:152-243): type->(name, unit), count stays a count,
+  cpu_steal stays raw ns, everything else ns/1e6 -> ms, conn tuple only if a port != 0
+  (src_ip "0.0.0.0", protocol "tcp"), errno only if != 0, IPv4 little-endian bytes.
+* ``EVENT`` -- NEW 64-byte, 64-byte-aligned record (one cache line per event, 16-B
+  aligned fields for dwordx4 loads on gfx950). It keeps every REF field and adds
+  interned workload ids (pod/node/service), a 64-bit trace-id hash, a 64-bit
+  connection hash, a GPU id and flags. Layout is mirrored in
+  ``ops/csrc/mislo_records.h`` and ``ebpf/c/mislo_event.h``.
+* ``SPAN`` -- 64-byte span record for the correlation join.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from ..contracts.types import ConnTuple, ProbeEventV1
+from ..signals import catalog
+
+REF_EVENT = np.dtype([
+    ("pid", "<u4"), ("tid", "<u4"), ("timestamp_ns", "<u8"), ("signal_type", "<u4"),
+    ("value_ns", "<u8"), ("conn_src_port", "<u2"), ("conn_dst_port", "<u2"),
+    ("conn_dst_ip", "<u4"), ("errno_val", "<i4"),
+], align=False)
+assert REF_EVENT.itemsize == 40
+
+EVENT = np.dtype([
+    ("ts_ns", "<i8"),        # 0   CLOCK_REALTIME ns (probes convert ktime at the boundary)
+    ("value", "<u8"),        # 8   raw value in the signal's kernel unit (see catalog.decode_scale)
+    ("trace_h", "<u8"),      # 16  64-bit trace-id hash, 0 = none
+    ("pid", "<u4"),          # 24
+    ("tid", "<u4"),          # 28
+    ("pod_id", "<u4"),       # 32  interned pod id, 0 = unknown
+    ("dst_ip", "<u4"),       # 36  IPv4 (network order as read by the probe)
+    ("signal_type", "<u2"),  # 40
+    ("node_id", "<u2"),      # 42  interned node id
+    ("svc_id", "<u2"),       # 44  interned service id
+    ("flags", "<u2"),        # 46  bits 0-7 gpu id, bit 8 has_gpu, bit 9 synthetic
+    ("src_port", "<u2"),     # 48
+    ("dst_port", "<u2"),     # 50
+    ("errno", "<i4"),        # 52
+    ("conn_h", "<u8"),       # 56  connection hash (0 -> derived on device from ports/ip)
+])
+assert EVENT.itemsize == 64
+
+SPAN = np.dtype([
+    ("ts_ns", "<i8"),        # 0
+    ("trace_h", "<u8"),      # 8
+    ("conn_h", "<u8"),       # 16
+    ("pid", "<u4"),          # 24
+    ("pod_id", "<u4"),       # 28
+    ("node_id", "<u2"),      # 32
+    ("svc_id", "<u2"),       # 34
+    ("group_id", "<u4"),     # 36 incident group (service x window) for aggregation
+    ("ttft_ms", "<f4"),      # 40
+    ("latency_ms", "<f4"),   # 44
+    ("span_h", "<u8"),       # 48
+    ("reserved", "<u8"),     # 56
+])
+assert SPAN.itemsize == 64
+
+FLAG_HAS_GPU = 1 << 8
+FLAG_SYNTHETIC = 1 << 9
+
+# REF kernel type ids (ringbuf.go:29-39)
+REF_TYPE_CPU_STEAL = 6
+REF_TYPE_TCP_RETRANSMIT = 2
+
+
+def ipv4_from_u32(ip: int) -> str:
+    """REF ipFromU32 (ringbuf.go:240-243): little-endian byte order."""
+    ip = int(ip)
+    return f"{ip & 0xFF}.{(ip >> 8) & 0xFF}.{(ip >> 16) & 0xFF}.{(ip >> 24) & 0xFF}"
+
+
+def ref_convert_value(signal_type: int, value_ns: int) -> float:
+    """REF convertValue (ringbuf.go:229-238)."""
+    if signal_type in (REF_TYPE_TCP_RETRANSMIT, REF_TYPE_CPU_STEAL):
+        return float(value_ns)
+    return float(value_ns) / 1e6
+
+
+def ref_signal_from_type(signal_type: int):
+    """REF signalFromType (ringbuf.go:199-225): cpu_steal unit is "ns" at the kernel boundary."""
+    if signal_type == REF_TYPE_CPU_STEAL:
+        return "cpu_steal_pct", "ns"
+    if 1 <= signal_type <= 9:
+        return catalog.signal_from_type(signal_type)
+    return "unknown", "unknown"
+
+
+def decode_ref_record(buf: bytes, meta, ts_unix_nano: int) -> ProbeEventV1:
+    """Decode one 40-byte REF record exactly like REF toProbeEvent (ringbuf.go:161-197).
+
+    ``meta`` supplies node/namespace/pod/container/trace_id/span_id (EventMetadata);
+    REF stamps wall-clock ``time.Now()`` -- the caller passes it as ``ts_unix_nano``.
+    """
+    if len(buf) < REF_EVENT.itemsize:
+        raise ValueError("decode bpf event: short buffer")
+    r = np.frombuffer(buf[: REF_EVENT.itemsize], dtype=REF_EVENT)[0]
+    st = int(r["signal_type"])
+    name, unit = ref_signal_from_type(st)
+    ev = ProbeEventV1(
+        ts_unix_nano=int(ts_unix_nano), signal=name, node=meta.node, namespace=meta.namespace,
+        pod=meta.pod, container=meta.container, pid=int(r["pid"]), tid=int(r["tid"]),
+        value=ref_convert_value(st, int(r["value_ns"])), unit=unit, status="ok",
+        trace_id=meta.trace_id, span_id=meta.span_id)
+    sp, dp = int(r["conn_src_port"]), int(r["conn_dst_port"])
+    if sp != 0 or dp != 0:
+        ev.conn_tuple = ConnTuple("0.0.0.0", ipv4_from_u32(int(r["conn_dst_ip"])), sp, dp, "tcp")
+    if int(r["errno_val"]) != 0:
+        ev.errno = int(r["errno_val"])
+    return ev
+
+
+def encode_ref_record(pid, tid, ts_ns, signal_type, value_ns, sport=0, dport=0, dst_ip=0, errno=0) -> bytes:
+    a = np.zeros(1, dtype=REF_EVENT)
+    a[0] = (pid, tid, ts_ns, signal_type, value_ns, sport, dport, dst_ip, errno)
+    return a.tobytes()
+
+
+DECODE_SCALE = np.array([s.decode_scale for s in catalog.SIGNALS], dtype=np.float64)
+
+
+def type_to_slot_table(max_type: int = 128) -> np.ndarray:
+    """signal_type -> slot (or -1). Kernel-side constant table."""
+    t = np.full(max_type, -1, dtype=np.int32)
+    for spec in catalog.SIGNALS:
+        t[spec.kernel_type] = spec.slot
+    return t
+
+
+def conn_hash(src_port: int, dst_port: int, dst_ip: int) -> int:
+    """64-bit connection hash (splitmix64 over the packed tuple). 0 when no port is set
+    (REF builds a conn tuple only when a port != 0, ringbuf.go:181)."""
+    if src_port == 0 and dst_port == 0:
+        return 0
+    x = ((int(src_port) & 0xFFFF) << 48) | ((int(dst_port) & 0xFFFF) << 32) | (int(dst_ip) & 0xFFFFFFFF)
+    return splitmix64(x) or 1
+
+
+def splitmix64(x: int) -> int:
+    M = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & M
+    z = x
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def conn_hash_np(src_port: np.ndarray, dst_port: np.ndarray, dst_ip: np.ndarray) -> np.ndarray:
+    sp = src_port.astype(np.uint64)
+    dp = dst_port.astype(np.uint64)
+    ip = dst_ip.astype(np.uint64)
+    packed = (sp << np.uint64(48)) | (dp << np.uint64(32)) | ip
+    h = splitmix64_np(packed)
+    h = np.where(h == 0, np.uint64(1), h)
+    return np.where((sp == 0) & (dp == 0), np.uint64(0), h)
+
+
+def string_hash64(s: str) -> int:
+    """FNV-1a 64 of a string; 0 reserved for the empty string."""
+    if not s:
+        return 0
+    h = 0xCBF29CE484222325
+    for b in s.encode("utf-8"):
+        h ^= b
+        h = (h * 0x100000001B3) & ((1 << 64) - 1)
+    return h or 1

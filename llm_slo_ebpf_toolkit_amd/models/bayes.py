@@ -1,0 +1,320 @@
+"""Attribution models as linear-logit posteriors over the 16-slot feature layout.
+
+Every model here reduces to ``logits = X @ W + b`` followed by a log-sum-exp
+normalisation, which is exactly what the MFMA posterior kernel (``ops.posterior``)
+evaluates for a whole batch of incidents at once:
+
+* ``NaiveBayes.ref()`` -- REF-exact naive Bayes (pkg/attribution/bayesian.go:39-343):
+  uniform priors over the 8 REF domains, the 12x8 likelihood table, binary evidence
+  ``value >= threshold`` (bayesian.go:194-207), every table signal contributes
+  (absent = not elevated, bayesian.go:237-240), clamp [0.01, 0.99], LSE, evidence =
+  elevated signals with P(elevated|d) >= 0.5, stable sort by posterior, hypotheses
+  < 0.01 dropped, top-1 overrides the label map, empty ``signals`` -> rule fallback.
+  In linear form: X = e (0/1), W = log p - log(1-p), b = log prior + sum log(1-p).
+* ``NaiveBayes.learned(stats)`` -- the same model with priors/likelihoods re-estimated
+  from labelled sufficient statistics (Beta/Dirichlet smoothing towards a seeded
+  random-init table), the "random-init priors" north-star configuration.
+* ``LDA.fit(stats)`` -- the covariance-corrected model: shared-covariance Gaussian
+  class conditionals on log1p(signal) features; W = S^-1 mu_d,
+  b = -1/2 mu_d^T S^-1 mu_d + log pi_d. Its scatter matrix is the MFMA covariance step.
+
+All CPU math is float64 numpy (the oracle); the GPU path evaluates the same W/b.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..contracts.types import FaultHypothesis, IncidentAttribution
+from ..signals import catalog
+from .sample import FaultSample, build_attribution
+
+N_SLOTS = catalog.N_SLOTS
+N_DOMAINS = len(catalog.ALL_DOMAINS)       # 10 (8 REF + 2 GPU)
+N_REF_DOMAINS = len(catalog.REF_DOMAINS)   # 8
+THRESHOLDS = np.array([s.elevated for s in catalog.SIGNALS], dtype=np.float64)
+# Nominal ("healthy") values used to impute absent signals for continuous models:
+# REF base signal profile (pkg/signals/generator.go:244-259) + GPU nominals.
+NOMINAL = np.array([12, 0.2, 4, 18, 0, 22, 0, 0.6, 5, 0.5, 2, 5, 0.5, 40, 3, 1.0], dtype=np.float64)
+NEG_INF = -np.inf
+
+
+def clamp_likelihood(p):
+    return np.clip(p, 0.01, 0.99)
+
+
+@dataclass
+class Posterior:
+    domain: str
+    posterior: float
+    evidence: List[str]
+
+
+@dataclass
+class LinearPosteriorModel:
+    """logits[b, d] = X[b] @ W[:, d] + bias[d]; domains with bias -inf are inactive."""
+    name: str
+    weights: np.ndarray                 # [16, D] float64
+    bias: np.ndarray                    # [D]     float64 (-inf = inactive domain)
+    evidence_mask: np.ndarray           # [16, D] bool
+    feature_mode: str = "binary"        # "binary" (e = v >= thr) | "continuous"
+    thresholds: np.ndarray = field(default_factory=lambda: THRESHOLDS.copy())
+    mean: Optional[np.ndarray] = None   # continuous: feature centring
+    table_mask: Optional[np.ndarray] = None  # binary: which slots the model knows
+
+    def features(self, values: np.ndarray) -> np.ndarray:
+        """values: [B, 16] with NaN for absent signals -> model features X [B, 16]."""
+        values = np.asarray(values, dtype=np.float64)
+        if self.feature_mode == "binary":
+            with np.errstate(invalid="ignore"):
+                e = (values >= self.thresholds[None, :]) & ~np.isnan(values)
+            x = e.astype(np.float64)
+            if self.table_mask is not None:
+                x = x * self.table_mask[None, :]
+            return x
+        v = np.where(np.isnan(values), NOMINAL[None, :], values)
+        x = np.log1p(np.maximum(v, 0.0))
+        if self.mean is not None:
+            x = x - self.mean[None, :]
+        return x
+
+    def elevated(self, values: np.ndarray) -> np.ndarray:
+        values = np.asarray(values, dtype=np.float64)
+        with np.errstate(invalid="ignore"):
+            e = (values >= self.thresholds[None, :]) & ~np.isnan(values)
+        if self.table_mask is not None:
+            e &= self.table_mask[None, :].astype(bool)
+        return e
+
+    def logits(self, values: np.ndarray) -> np.ndarray:
+        return self.features(values) @ self.weights + self.bias[None, :]
+
+    def posteriors(self, values: np.ndarray) -> np.ndarray:
+        lg = self.logits(values)
+        m = np.max(lg, axis=1, keepdims=True)
+        with np.errstate(invalid="ignore"):
+            ex = np.exp(lg - m)
+        z = m + np.log(np.sum(ex, axis=1, keepdims=True))
+        return np.exp(lg - z)
+
+    def evidence_bits(self, values: np.ndarray) -> np.ndarray:
+        """[B, D] uint32 bitmask over slots: elevated & P(elevated|d) >= 0.5."""
+        e = self.elevated(values)
+        bits = np.zeros((e.shape[0], self.weights.shape[1]), dtype=np.uint32)
+        for s in range(N_SLOTS):
+            col = e[:, s:s + 1] & self.evidence_mask[s][None, :]
+            bits |= (col.astype(np.uint32) << np.uint32(s))
+        return bits
+
+    def attribute(self, signals: Dict[str, float]) -> List[Posterior]:
+        """Single-sample API with REF ordering semantics (stable sort, domain order ties)."""
+        vec = np.array([catalog.feature_vector(signals)], dtype=np.float64)
+        post = self.posteriors(vec)[0]
+        bits = self.evidence_bits(vec)[0]
+        out: List[Posterior] = []
+        for d, dom in enumerate(catalog.ALL_DOMAINS[: self.weights.shape[1]]):
+            if not np.isfinite(self.bias[d]):
+                continue
+            ev = sorted(catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if bits[d] >> s & 1)
+            out.append(Posterior(dom, float(post[d]), ev))
+        out.sort(key=lambda p: -p.posterior)  # Python sort is stable == sort.SliceStable
+        return out
+
+    def attribute_sample(self, sample: FaultSample) -> IncidentAttribution:
+        base = build_attribution(sample)
+        if not sample.signals:
+            return base
+        posts = self.attribute(sample.signals)
+        base.fault_hypotheses = [FaultHypothesis(p.domain, p.posterior, p.evidence)
+                                 for p in posts if p.posterior >= 0.01]
+        if posts:
+            base.predicted_fault_domain = posts[0].domain
+            base.confidence = posts[0].posterior
+        return base
+
+    def to_arrays(self) -> Dict[str, np.ndarray]:
+        return {"weights": self.weights, "bias": self.bias, "evidence_mask": self.evidence_mask,
+                "thresholds": self.thresholds,
+                "mean": self.mean if self.mean is not None else np.zeros(N_SLOTS),
+                "table_mask": self.table_mask if self.table_mask is not None else np.ones(N_SLOTS)}
+
+
+class NaiveBayes:
+    """Factory for binary-evidence naive Bayes in linear-logit form."""
+
+    @staticmethod
+    def from_tables(priors: Dict[str, float], likelihoods: Dict[str, Dict[str, float]],
+                    domains: Sequence[str] = catalog.REF_DOMAINS, name: str = "bayes") -> LinearPosteriorModel:
+        D = N_DOMAINS
+        W = np.zeros((N_SLOTS, D))
+        b = np.full(D, NEG_INF)
+        mask = np.zeros((N_SLOTS, D), dtype=bool)
+        table = np.zeros(N_SLOTS)
+        for dom in domains:
+            d = catalog.DOMAIN_INDEX[dom]
+            prior = priors.get(dom, 0.0)
+            if prior <= 0:
+                prior = 1e-10
+            b[d] = math.log(prior)
+        for sig, row in likelihoods.items():
+            spec = catalog.BY_NAME.get(sig)
+            if spec is None:
+                continue
+            s = spec.slot
+            table[s] = 1.0
+            for dom in domains:
+                d = catalog.DOMAIN_INDEX[dom]
+                p = row.get(dom)
+                if p is None:  # REF likelihoodFor: missing domain entry -> 0.5 uninformative
+                    pe = pn = 0.5
+                else:
+                    pe, pn = clamp_likelihood(p), clamp_likelihood(1.0 - p)
+                    mask[s, d] = p >= 0.5
+                W[s, d] = math.log(pe) - math.log(pn)
+                b[d] += math.log(pn)
+        return LinearPosteriorModel(name, W, b, mask, "binary", THRESHOLDS.copy(), None, table)
+
+    @staticmethod
+    def ref() -> LinearPosteriorModel:
+        doms = catalog.REF_DOMAINS
+        priors = {d: 1.0 / len(doms) for d in doms}
+        return NaiveBayes.from_tables(priors, catalog.ref_likelihoods(), doms, "bayes")
+
+    @staticmethod
+    def random_init_table(seed: int = 42, domains: Sequence[str] = catalog.ALL_DOMAINS) -> np.ndarray:
+        rng = np.random.default_rng(seed)
+        return rng.uniform(0.05, 0.95, size=(N_SLOTS, len(domains)))
+
+    @staticmethod
+    def learned(stats: "SufficientStats", alpha: float = 2.0, seed: int = 42,
+                init: Optional[np.ndarray] = None, domains: Sequence[str] = catalog.ALL_DOMAINS,
+                prior_pseudo: float = 1.0) -> LinearPosteriorModel:
+        """Posterior-mean estimates: p_sd = (c_sd + alpha*p0_sd) / (n_d + alpha), with p0 a
+        seeded random-init table (north star: random-init priors); pi_d ~ Dirichlet(1)."""
+        p0 = init if init is not None else NaiveBayes.random_init_table(seed, domains)
+        idx = [catalog.DOMAIN_INDEX[d] for d in domains]
+        n = stats.count[idx]
+        c = stats.elevated_sum[:, idx]
+        p = (c + alpha * p0) / (n[None, :] + alpha)
+        priors_arr = (n + prior_pseudo) / (n.sum() + prior_pseudo * len(idx))
+        priors = {d: float(priors_arr[i]) for i, d in enumerate(domains)}
+        lik = {catalog.SIGNAL_NAMES[s]: {d: float(p[s, i]) for i, d in enumerate(domains)}
+               for s in range(N_SLOTS)}
+        return NaiveBayes.from_tables(priors, lik, domains, "bayes_learned")
+
+
+class LDA:
+    @staticmethod
+    def fit(stats: "SufficientStats", shrinkage: float = 0.05, domains: Sequence[str] = catalog.ALL_DOMAINS,
+            prior_pseudo: float = 1.0) -> LinearPosteriorModel:
+        D = N_DOMAINS
+        idx = [catalog.DOMAIN_INDEX[d] for d in domains]
+        n = stats.count.astype(np.float64)
+        N = max(float(n[idx].sum()), 1.0)
+        mean_all = stats.x_sum.sum(axis=1) / N                  # [16]
+        mu = np.zeros((N_SLOTS, D))
+        for d in idx:
+            if n[d] > 0:
+                mu[:, d] = stats.x_sum[:, d] / n[d]
+            else:
+                mu[:, d] = mean_all
+        # pooled within-class scatter: S2 - sum_d n_d mu_d mu_d^T
+        within = stats.xx.copy()
+        for d in idx:
+            if n[d] > 0:
+                within -= n[d] * np.outer(mu[:, d], mu[:, d])
+        dof = max(N - len([d for d in idx if n[d] > 0]), 1.0)
+        cov = within / dof
+        cov = (1 - shrinkage) * cov + shrinkage * (np.trace(cov) / N_SLOTS + 1e-6) * np.eye(N_SLOTS)
+        prec = np.linalg.inv(cov)
+        muc = mu - mean_all[:, None]
+        W = np.zeros((N_SLOTS, D))
+        b = np.full(D, NEG_INF)
+        for d in idx:
+            W[:, d] = prec @ muc[:, d]
+            pi = (n[d] + prior_pseudo) / (N + prior_pseudo * len(idx))
+            b[d] = -0.5 * muc[:, d] @ prec @ muc[:, d] + math.log(pi)
+        # evidence: a slot supports d when the class mean sits above the elevated threshold
+        thr = np.log1p(THRESHOLDS) - mean_all
+        mask = muc >= thr[:, None]
+        return LinearPosteriorModel("lda", W, b, mask, "continuous", THRESHOLDS.copy(), mean_all, None)
+
+
+@dataclass
+class SufficientStats:
+    """Labelled sufficient statistics (CPU oracle of the MFMA statistics kernel).
+
+    count[d]            = #samples labelled d
+    elevated_sum[s, d]  = sum_b y_bd * e_bs        (E^T Y)
+    x_sum[s, d]         = sum_b y_bd * x_bs        (X^T Y, x = log1p(value), NOMINAL-imputed)
+    xx[s, t]            = sum_b x_bs x_bt          (X^T X, the covariance step)
+    """
+    count: np.ndarray = field(default_factory=lambda: np.zeros(N_DOMAINS))
+    elevated_sum: np.ndarray = field(default_factory=lambda: np.zeros((N_SLOTS, N_DOMAINS)))
+    x_sum: np.ndarray = field(default_factory=lambda: np.zeros((N_SLOTS, N_DOMAINS)))
+    xx: np.ndarray = field(default_factory=lambda: np.zeros((N_SLOTS, N_SLOTS)))
+
+    def add(self, values: np.ndarray, labels: np.ndarray, weights: Optional[np.ndarray] = None) -> None:
+        """values [B,16] (NaN = absent), labels [B] domain index (or [B,D] soft labels)."""
+        values = np.asarray(values, dtype=np.float64)
+        B = values.shape[0]
+        labels = np.asarray(labels)
+        if labels.ndim == 1:
+            Y = np.zeros((B, N_DOMAINS))
+            Y[np.arange(B), labels.astype(np.int64)] = 1.0
+        else:
+            Y = labels.astype(np.float64)
+        if weights is not None:
+            Y = Y * np.asarray(weights, dtype=np.float64)[:, None]
+        with np.errstate(invalid="ignore"):
+            E = ((values >= THRESHOLDS[None, :]) & ~np.isnan(values)).astype(np.float64)
+        X = np.log1p(np.maximum(np.where(np.isnan(values), NOMINAL[None, :], values), 0.0))
+        self.count += Y.sum(axis=0)
+        self.elevated_sum += E.T @ Y
+        self.x_sum += X.T @ Y
+        self.xx += X.T @ X
+
+    def merge(self, other: "SufficientStats") -> "SufficientStats":
+        return SufficientStats(self.count + other.count, self.elevated_sum + other.elevated_sum,
+                               self.x_sum + other.x_sum, self.xx + other.xx)
+
+    def pack(self) -> np.ndarray:
+        return np.concatenate([self.count.ravel(), self.elevated_sum.ravel(), self.x_sum.ravel(),
+                               self.xx.ravel()])
+
+    @classmethod
+    def unpack(cls, flat: np.ndarray) -> "SufficientStats":
+        flat = np.asarray(flat, dtype=np.float64)
+        o = 0
+        count = flat[o:o + N_DOMAINS]; o += N_DOMAINS
+        es = flat[o:o + N_SLOTS * N_DOMAINS].reshape(N_SLOTS, N_DOMAINS); o += N_SLOTS * N_DOMAINS
+        xs = flat[o:o + N_SLOTS * N_DOMAINS].reshape(N_SLOTS, N_DOMAINS); o += N_SLOTS * N_DOMAINS
+        xx = flat[o:o + N_SLOTS * N_SLOTS].reshape(N_SLOTS, N_SLOTS)
+        return cls(count.copy(), es.copy(), xs.copy(), xx.copy())
+
+    PACKED_LEN = N_DOMAINS + 2 * N_SLOTS * N_DOMAINS + N_SLOTS * N_SLOTS
+
+
+def samples_to_arrays(samples: Sequence[FaultSample]) -> Tuple[np.ndarray, np.ndarray]:
+    vals = np.array([catalog.feature_vector(s.signals) for s in samples], dtype=np.float64)
+    labels = np.array([catalog.DOMAIN_INDEX.get(s.actual_domain(), catalog.DOMAIN_INDEX["unknown"])
+                       for s in samples], dtype=np.int64)
+    return vals, labels
+
+
+def get_model(name: str, stats: Optional[SufficientStats] = None, seed: int = 42) -> LinearPosteriorModel:
+    if name in ("bayes", "", None):
+        return NaiveBayes.ref()
+    if name == "bayes_learned":
+        if stats is None:
+            raise ValueError("bayes_learned needs sufficient statistics")
+        return NaiveBayes.learned(stats, seed=seed)
+    if name == "lda":
+        if stats is None:
+            raise ValueError("lda needs sufficient statistics")
+        return LDA.fit(stats)
+    raise ValueError(f"unknown model {name!r}")

@@ -1,0 +1,357 @@
+// PyTorch bindings for the MI355X engine: a device-resident per-window Engine that owns
+// every buffer (allocated once through the caching allocator, sized for the window
+// capacity, so a window launches with no allocation and can be captured in a HIP graph)
+// and drives decode -> partition -> LDS join -> finalize -> MFMA posterior -> stats on the
+// caller's current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "mislo_launch.h"
+
+namespace py = pybind11;
+using namespace mislo;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define HIPCHECK(x)                                                                    \
+  do {                                                                                 \
+    hipError_t _e = (x);                                                               \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") +       \
+                                                   hipGetErrorString(_e) + " at " #x); \
+  } while (0)
+
+template <typename T>
+T* dptr(const torch::Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+void check_cuda(const torch::Tensor& t, const char* name) {
+  if (!t.is_cuda()) throw std::invalid_argument(std::string(name) + " must be a device tensor");
+  if (!t.is_contiguous()) throw std::invalid_argument(std::string(name) + " must be contiguous");
+}
+
+constexpr int kPacketHist = kSlots * kBuckets;            // 256
+constexpr int kPacketStatus = kSlots * 3;                 // 48
+constexpr int kPacketMisc = 2;
+constexpr int kPacketDbg = 8;
+constexpr int kPacketConf = kMaxDomains * kMaxDomains;    // 256
+constexpr int kPacketStats = 32 * 32;                     // 1024
+constexpr int kPacketCount = kMaxDomains;                 // 16
+constexpr int kPacketLen = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf + kPacketStats +
+                           kPacketCount;
+
+__global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsigned long long* misc,
+                       const unsigned long long* dbg, const uint32_t* confusion, const double* stats,
+                       const double* count, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int o = 0;
+  if (i < kPacketHist) { out[i] = hist[i]; return; }
+  o += kPacketHist;
+  if (i < o + kPacketStatus) { out[i] = status[i - o]; return; }
+  o += kPacketStatus;
+  if (i < o + kPacketMisc) { out[i] = (double)misc[i - o]; return; }
+  o += kPacketMisc;
+  if (i < o + kPacketDbg) { out[i] = (double)dbg[i - o]; return; }
+  o += kPacketDbg;
+  if (i < o + kPacketConf) { out[i] = confusion[i - o]; return; }
+  o += kPacketConf;
+  if (i < o + kPacketStats) { out[i] = stats[i - o]; return; }
+  o += kPacketStats;
+  if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
+}
+
+}  // namespace
+
+class Engine {
+ public:
+  Engine(int64_t sig_cap, int64_t span_cap, int64_t group_cap, int64_t device)
+      : sig_cap_((int)sig_cap), span_cap_((int)span_cap), group_cap_((int)group_cap) {
+    if (sig_cap <= 0 || span_cap <= 0 || group_cap <= 0) throw std::invalid_argument("capacities must be > 0");
+    if (sig_cap >= (1LL << 27)) throw std::invalid_argument("sig_cap must be < 2^27 (top-3 key packing)");
+    dev_ = torch::Device(torch::kCUDA, (c10::DeviceIndex)device);
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+    auto i64 = torch::TensorOptions().dtype(torch::kInt64).device(dev_);
+    auto i32 = torch::TensorOptions().dtype(torch::kInt32).device(dev_);
+    auto u8 = torch::TensorOptions().dtype(torch::kUInt8).device(dev_);
+    auto f32 = torch::TensorOptions().dtype(torch::kFloat32).device(dev_);
+    auto f64 = torch::TensorOptions().dtype(torch::kFloat64).device(dev_);
+    const int64_t N = sig_cap_, S = span_cap_, G = group_cap_;
+    nblk_sig_ = decode_grid(sig_cap_);
+    nblk_span_ = decode_grid(span_cap_);
+    counts = torch::zeros({4}, i32);
+    // signal columns
+    g_ts = torch::empty({N}, i64); g_val = torch::empty({N}, f32); g_slot = torch::empty({N}, u8);
+    g_status = torch::empty({N}, u8); g_pod = torch::empty({N}, i32); g_pid = torch::empty({N}, i32);
+    g_svcnode = torch::empty({N}, i32); g_trace = torch::empty({N}, i64); g_conn = torch::empty({N}, i64);
+    g_hash = torch::empty({kKeyTypes * N}, i64);
+    g_part_blk = torch::empty({(int64_t)nblk_sig_ * kKeyTypes * kParts}, i32);
+    g_part_off = torch::empty_like(g_part_blk);
+    g_part_tot = torch::empty({kKeyTypes * kParts}, i32);
+    g_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
+    g_items = torch::empty({kKeyTypes * N}, i32);
+    // span columns
+    s_ts = torch::empty({S}, i64); s_trace = torch::empty({S}, i64); s_conn = torch::empty({S}, i64);
+    s_pod = torch::empty({S}, i32); s_pid = torch::empty({S}, i32); s_svcnode = torch::empty({S}, i32);
+    s_group = torch::empty({S}, i32); s_hash = torch::empty({kKeyTypes * S}, i64);
+    s_part_blk = torch::empty({(int64_t)nblk_span_ * kKeyTypes * kParts}, i32);
+    s_part_off = torch::empty_like(s_part_blk);
+    s_part_tot = torch::empty({kKeyTypes * kParts}, i32);
+    s_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
+    s_items = torch::empty({kKeyTypes * S}, i32);
+    top3 = torch::empty({3 * S}, i64); cnt = torch::empty({S}, i32);
+    attrs = torch::empty({S, kSlots}, f32); conf = torch::empty({S}, f32); kernel_ms = torch::empty({S}, f32);
+    // groups / incidents
+    gsum = torch::empty({G, kSlots}, f32); gcnt = torch::empty({G, kSlots}, i32);
+    feat = torch::empty({G, kSlots}, f32); labels = torch::full({G}, -1, i32);
+    post = torch::empty({G, kMaxDomains}, f64); pred = torch::empty({G}, i32); gconf = torch::empty({G}, f64);
+    evbits = torch::empty({G, kMaxDomains}, i32);
+    // window accumulators
+    hist = torch::empty({kSlots, kBuckets}, i32); status_cnt = torch::empty({kSlots, 3}, i32);
+    misc = torch::empty({kPacketMisc}, i64); dbg = torch::empty({kPacketDbg}, i64);
+    confusion = torch::empty({kMaxDomains, kMaxDomains}, i32);
+    stats = torch::empty({32, 32}, f64); stats_count = torch::empty({kMaxDomains}, f64);
+    packet = torch::empty({kPacketLen}, f64);
+    model = torch::zeros({(int64_t)sizeof(PosteriorModel)}, u8);
+    join_defaults();
+  }
+
+  void join_defaults() { set_join_params(2000.0, 0.7, 3, 1); }
+
+  void set_join_params(double window_ms, double threshold, int64_t fanout, int64_t group_mode) {
+    const int64_t ms = 1000000;
+    int64_t outer = (int64_t)llround(window_ms * ms);
+    if (outer <= 0) outer = 2000 * ms;
+    if (outer >= (1LL << 35)) throw std::invalid_argument("window too large for top-3 key packing (< 34 s)");
+    jp_.outer_ns = outer;
+    const int64_t tw[4] = {outer, 100 * ms, 250 * ms, 500 * ms};
+    for (int k = 0; k < 4; ++k) jp_.win_ns[k] = std::min(outer, tw[k]);
+    const float cf[4] = {1.0f, 0.9f, 0.8f, 0.65f};
+    for (int k = 0; k < 4; ++k) jp_.conf[k] = cf[k];
+    jp_.threshold = threshold > 0 ? (float)threshold : 0.7f;
+    if (fanout <= 0) fanout = 3;
+    if (fanout > 3) throw std::invalid_argument("GPU join keeps at most 3 candidates per span");
+    jp_.fanout = (int)fanout;
+    jp_.group_mode = (int)group_mode;
+  }
+
+  // model: w[16,16] f64, bias[16], mean[16], nominal[16], thr[16] f32, dom_mask[16] i32
+  void set_model(torch::Tensor w, torch::Tensor bias, torch::Tensor mean, torch::Tensor nominal, torch::Tensor thr,
+                 torch::Tensor dom_mask, int64_t table_mask, int64_t mode) {
+    PosteriorModel pm;
+    std::memset(&pm, 0, sizeof(pm));
+    auto wc = w.to(torch::kCPU, torch::kFloat64).contiguous();
+    auto bc = bias.to(torch::kCPU, torch::kFloat64).contiguous();
+    auto mc = mean.to(torch::kCPU, torch::kFloat64).contiguous();
+    auto nc = nominal.to(torch::kCPU, torch::kFloat64).contiguous();
+    auto tc = thr.to(torch::kCPU, torch::kFloat32).contiguous();
+    auto dc = dom_mask.to(torch::kCPU, torch::kInt64).contiguous();
+    if (wc.numel() != kSlots * kMaxDomains || bc.numel() != kMaxDomains) throw std::invalid_argument("model shape");
+    std::memcpy(pm.w, wc.data_ptr<double>(), sizeof(pm.w));
+    std::memcpy(pm.bias, bc.data_ptr<double>(), sizeof(pm.bias));
+    std::memcpy(pm.mean, mc.data_ptr<double>(), sizeof(pm.mean));
+    std::memcpy(pm.nominal, nc.data_ptr<double>(), sizeof(pm.nominal));
+    std::memcpy(pm.thr, tc.data_ptr<float>(), sizeof(pm.thr));
+    for (int d = 0; d < kMaxDomains; ++d) pm.dom_mask[d] = (uint32_t)dc.data_ptr<int64_t>()[d];
+    pm.table_mask = (uint32_t)table_mask;
+    pm.mode = (int32_t)mode;
+    auto host = torch::from_blob(&pm, {(int64_t)sizeof(pm)}, torch::kUInt8).clone();
+    model.copy_(host, /*non_blocking=*/false);
+  }
+
+  // ---- stages --------------------------------------------------------------------------
+  void reset_window() {
+    hipStream_t st = cur_stream();
+    HIPCHECK(hipMemsetAsync(hist.data_ptr(), 0, hist.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(status_cnt.data_ptr(), 0, status_cnt.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(misc.data_ptr(), 0, misc.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(dbg.data_ptr(), 0, dbg.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(confusion.data_ptr(), 0, confusion.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(stats.data_ptr(), 0, stats.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(stats_count.data_ptr(), 0, stats_count.nbytes(), st));
+  }
+
+  SignalCols sig_cols() {
+    return SignalCols{dptr<int64_t>(g_ts), dptr<float>(g_val), dptr<uint8_t>(g_slot), dptr<uint8_t>(g_status),
+                      dptr<uint32_t>(g_pod), dptr<uint32_t>(g_pid), dptr<uint32_t>(g_svcnode),
+                      dptr<uint64_t>(g_trace), dptr<uint64_t>(g_conn), dptr<uint64_t>(g_hash)};
+  }
+  SpanCols span_cols() {
+    return SpanCols{dptr<int64_t>(s_ts), dptr<uint64_t>(s_trace), dptr<uint64_t>(s_conn), dptr<uint32_t>(s_pod),
+                    dptr<uint32_t>(s_pid), dptr<uint32_t>(s_svcnode), dptr<uint32_t>(s_group),
+                    dptr<uint64_t>(s_hash)};
+  }
+
+  // events: device uint8 tensor of 64-byte records (>= n*64 bytes); counts[0] must hold n.
+  void decode(torch::Tensor events) {
+    check_cuda(events, "events");
+    if (events.nbytes() < (size_t)sig_cap_ * 64)
+      throw std::invalid_argument("events buffer must hold sig_cap 64-byte records");
+    launch_decode_events(events.data_ptr(), dptr<int>(counts), sig_cap_, sig_cols(), dptr<uint32_t>(hist),
+                         dptr<uint32_t>(status_cnt), dptr<uint32_t>(g_part_blk),
+                         dptr<unsigned long long>(misc), cur_stream());
+    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
+                     dptr<uint32_t>(g_items), cur_stream());
+  }
+
+  void decode_ref(torch::Tensor events, int64_t pod, int64_t svcnode, int64_t trace_h) {
+    check_cuda(events, "events");
+    if (events.nbytes() < (size_t)sig_cap_ * 40)
+      throw std::invalid_argument("events buffer must hold sig_cap 40-byte REF records");
+    launch_decode_ref(events.data_ptr(), dptr<int>(counts), sig_cap_, (uint32_t)pod, (uint32_t)svcnode,
+                      (uint64_t)trace_h, sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
+                      dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
+    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
+                     dptr<uint32_t>(g_items), cur_stream());
+  }
+
+  // spans: device uint8 tensor of 64-byte span records; counts[1] = n spans, counts[2] = n groups
+  void join(torch::Tensor spans, int64_t n_groups, c10::optional<torch::Tensor> base_attrs) {
+    check_cuda(spans, "spans");
+    if (spans.nbytes() < (size_t)span_cap_ * 64)
+      throw std::invalid_argument("spans buffer must hold span_cap 64-byte records");
+    if (n_groups > group_cap_) throw std::invalid_argument("n_groups exceeds group capacity");
+    hipStream_t st = cur_stream();
+    launch_decode_spans(spans.data_ptr(), dptr<int>(counts) + 1, span_cap_, span_cols(), dptr<uint32_t>(s_part_blk), st);
+    launch_partition(dptr<uint64_t>(s_hash), dptr<int>(counts) + 1, span_cap_, nblk_span_,
+                     dptr<uint32_t>(s_part_blk), dptr<uint32_t>(s_part_off), dptr<uint32_t>(s_part_tot),
+                     dptr<uint32_t>(s_part_base), dptr<uint32_t>(s_items), st);
+    HIPCHECK(hipMemsetAsync(top3.data_ptr(), 0xFF, top3.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(cnt.data_ptr(), 0, cnt.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(gsum.data_ptr(), 0, gsum.nbytes(), st));
+    HIPCHECK(hipMemsetAsync(gcnt.data_ptr(), 0, gcnt.nbytes(), st));
+    launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(),
+                 dptr<uint32_t>(g_items), dptr<uint32_t>(g_part_base), sig_cap_, span_cap_, jp_,
+                 dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<float>(gsum),
+                 dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), st);
+    const float* base = nullptr;
+    if (base_attrs.has_value()) {
+      check_cuda(*base_attrs, "base_attrs");
+      if (base_attrs->numel() < (int64_t)span_cap_ * kSlots || base_attrs->scalar_type() != torch::kFloat32)
+        throw std::invalid_argument("base_attrs must be float32 [span_cap, 16]");
+      base = base_attrs->data_ptr<float>();
+    }
+    launch_finalize(dptr<int>(counts) + 1, span_cap_, dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), sig_cols(),
+                    span_cols(), jp_, base, dptr<float>(attrs), dptr<float>(conf), dptr<float>(kernel_ms),
+                    (int)n_groups, dptr<float>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat),
+                    dptr<unsigned long long>(dbg), st);
+  }
+
+  // Incident features -> posteriors (counts[2] = number of incident rows in `feat`).
+  void posterior(bool with_labels) {
+    launch_posterior(dptr<float>(feat), dptr<int>(counts) + 2, group_cap_,
+                     reinterpret_cast<const PosteriorModel*>(model.data_ptr()),
+                     with_labels ? dptr<int32_t>(labels) : nullptr, dptr<double>(post), dptr<int32_t>(pred),
+                     dptr<double>(gconf), dptr<uint32_t>(evbits), dptr<uint32_t>(confusion), cur_stream());
+  }
+
+  void accumulate_stats(c10::optional<torch::Tensor> weights) {
+    const float* w = nullptr;
+    if (weights.has_value()) {
+      check_cuda(*weights, "weights");
+      w = weights->data_ptr<float>();
+    }
+    launch_stats(dptr<float>(feat), dptr<int>(counts) + 2, group_cap_,
+                 reinterpret_cast<const PosteriorModel*>(model.data_ptr()), dptr<int32_t>(labels), w,
+                 dptr<double>(stats), dptr<double>(stats_count), cur_stream());
+  }
+
+  void pack() {
+    hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, cur_stream(), dptr<uint32_t>(hist),
+                       dptr<uint32_t>(status_cnt), dptr<unsigned long long>(misc), dptr<unsigned long long>(dbg),
+                       dptr<uint32_t>(confusion), dptr<double>(stats), dptr<double>(stats_count),
+                       dptr<double>(packet));
+  }
+
+  // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0].
+  void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn) {
+    reset_window();
+    decode(events);
+    join(spans, n_groups, c10::nullopt);
+    posterior(with_labels);
+    if (learn) accumulate_stats(c10::nullopt);
+    pack();
+  }
+
+  int64_t sig_cap() const { return sig_cap_; }
+  int64_t span_cap() const { return span_cap_; }
+  int64_t group_cap() const { return group_cap_; }
+  int64_t packet_len() const { return kPacketLen; }
+
+  torch::Tensor counts;
+  torch::Tensor g_ts, g_val, g_slot, g_status, g_pod, g_pid, g_svcnode, g_trace, g_conn, g_hash;
+  torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items;
+  torch::Tensor s_ts, s_trace, s_conn, s_pod, s_pid, s_svcnode, s_group, s_hash;
+  torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items;
+  torch::Tensor top3, cnt, attrs, conf, kernel_ms;
+  torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
+  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model;
+
+ private:
+  int sig_cap_, span_cap_, group_cap_;
+  int nblk_sig_ = 1, nblk_span_ = 1;
+  torch::Device dev_{torch::kCPU};
+  JoinParams jp_{};
+};
+
+void set_tables_py(torch::Tensor type_slot, torch::Tensor scale, torch::Tensor warn, torch::Tensor err,
+                   torch::Tensor edges) {
+  Tables t;
+  std::memset(&t, 0, sizeof(t));
+  auto ts = type_slot.to(torch::kCPU, torch::kInt8).contiguous();
+  auto sc = scale.to(torch::kCPU, torch::kFloat32).contiguous();
+  auto wa = warn.to(torch::kCPU, torch::kFloat32).contiguous();
+  auto er = err.to(torch::kCPU, torch::kFloat32).contiguous();
+  auto ed = edges.to(torch::kCPU, torch::kFloat32).contiguous();
+  if (ts.numel() != kMaxTypes || sc.numel() != kSlots || ed.numel() != kSlots * kBuckets)
+    throw std::invalid_argument("table shapes");
+  std::memcpy(t.type_slot, ts.data_ptr<int8_t>(), sizeof(t.type_slot));
+  std::memcpy(t.scale, sc.data_ptr<float>(), sizeof(t.scale));
+  std::memcpy(t.warn, wa.data_ptr<float>(), sizeof(t.warn));
+  std::memcpy(t.err, er.data_ptr<float>(), sizeof(t.err));
+  std::memcpy(t.edges, ed.data_ptr<float>(), sizeof(t.edges));
+  set_tables(&t);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) LLM-SLO engine kernels";
+  m.def("set_tables", &set_tables_py);
+  m.attr("PACKET_LEN") = kPacketLen;
+  m.attr("PACKET_LAYOUT") = py::make_tuple(kPacketHist, kPacketStatus, kPacketMisc, kPacketDbg, kPacketConf,
+                                           kPacketStats, kPacketCount);
+  m.attr("PARTS") = kParts;
+  m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("sig_cap"), py::arg("span_cap"),
+           py::arg("group_cap"), py::arg("device") = 0)
+      .def("set_join_params", &Engine::set_join_params, py::arg("window_ms") = 2000.0,
+           py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1)
+      .def("set_model", &Engine::set_model)
+      .def("reset_window", &Engine::reset_window)
+      .def("decode", &Engine::decode)
+      .def("decode_ref", &Engine::decode_ref)
+      .def("join", &Engine::join, py::arg("spans"), py::arg("n_groups"), py::arg("base_attrs") = py::none())
+      .def("posterior", &Engine::posterior)
+      .def("accumulate_stats", &Engine::accumulate_stats, py::arg("weights") = py::none())
+      .def("pack", &Engine::pack)
+      .def("run_window", &Engine::run_window)
+      .def_property_readonly("sig_cap", &Engine::sig_cap)
+      .def_property_readonly("span_cap", &Engine::span_cap)
+      .def_property_readonly("group_cap", &Engine::group_cap)
+      .def_property_readonly("packet_len", &Engine::packet_len)
+#define RO(name) .def_readonly(#name, &Engine::name)
+      RO(counts) RO(g_ts) RO(g_val) RO(g_slot) RO(g_status) RO(g_pod) RO(g_pid) RO(g_svcnode) RO(g_trace)
+      RO(g_conn) RO(g_hash) RO(g_part_base) RO(g_items) RO(s_ts) RO(s_hash) RO(s_part_base) RO(s_items)
+      RO(top3) RO(cnt) RO(attrs) RO(conf) RO(kernel_ms) RO(gsum) RO(gcnt) RO(feat) RO(labels) RO(post)
+      RO(pred) RO(gconf) RO(evbits) RO(hist) RO(status_cnt) RO(misc) RO(dbg) RO(confusion) RO(stats)
+      RO(stats_count) RO(packet) RO(model);
+#undef RO
+}

@@ -1,0 +1,233 @@
+// K1: batched record decode + status + per-signal histograms + join-partition counts.
+//
+// One pass over the window's 64-byte records (one cache line per event, read as
+// 4 x dwordx4 per lane, fully coalesced). Produces the structure-of-arrays columns the
+// join and posterior kernels consume, and -- fused into the same pass -- the per-signal
+// Prometheus-style histograms (REF agent histogram cmd/agent/main.go:190-194 generalised
+// to all 16 signals), per-signal status counters (REF generator.go:203-232 thresholds)
+// and the 4 x 1024 hash-partition histograms that size the join's partition buffers.
+// All histograms are LDS-privatised per workgroup: signal/status bins are merged with
+// one global atomic per non-zero bin (O(bins x workgroups), not O(N)); the partition
+// histogram is stored per workgroup for the atomic-free scatter (join.hip).
+//
+// The REF-compat variant decodes REF's packed 40-byte record with REF's exact unit
+// rules (pkg/collector/ringbuf.go:199-238) for replaying REF ring-buffer captures.
+#include "mislo_common.h"
+#include "mislo_launch.h"
+
+namespace mislo {
+
+__constant__ Tables c_tab;
+
+struct DecodeOut {
+  SignalCols cols;
+  uint32_t* hist;        // [kSlots * kBuckets]
+  uint32_t* status_cnt;  // [kSlots * 3]
+  uint32_t* part_cnt;    // [gridDim.x][kKeyTypes * kParts] per-block partition counts
+  unsigned long long* misc;  // [0] unsupported events, [1] zero-timestamp events
+};
+
+template <int NT>
+__device__ __forceinline__ void flush_counts(uint32_t* lds, uint32_t* global, int n) {
+  for (int i = threadIdx.x; i < n; i += NT) {
+    uint32_t v = lds[i];
+    if (v) atomicAdd(global + i, v);
+  }
+}
+
+// Per-block partition histogram, stored (not atomically merged): the scan kernel turns
+// the [blocks][4][1024] matrix into per-block scatter offsets, so the scatter pass needs
+// no global atomics and places each block's events contiguously.
+template <int NT>
+__device__ __forceinline__ void store_counts(const uint32_t* lds, uint32_t* dst) {
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) dst[i] = lds[i];
+}
+
+__device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val, int slot,
+                                           uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
+                                           uint64_t conn_h, const DecodeOut& o, uint32_t* s_hist,
+                                           uint32_t* s_status, uint32_t* s_part, int& unsupported,
+                                           int& zero_ts) {
+  uint8_t st = 0;
+  if (slot >= 0) {
+    st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
+    // bucket = number of finite edges strictly below val ("le" semantics: val <= edge[b])
+    int b = 0;
+#pragma unroll
+    for (int e = 0; e < kBuckets - 1; ++e) b += (val > c_tab.edges[slot][e]) ? 1 : 0;
+    atomicAdd(&s_hist[slot * kBuckets + b], 1u);
+    atomicAdd(&s_status[slot * 3 + st], 1u);
+  } else {
+    ++unsupported;
+  }
+  o.cols.ts[i] = ts;
+  o.cols.val[i] = val;
+  o.cols.slot[i] = slot >= 0 ? (uint8_t)slot : kNoSlot;
+  o.cols.status[i] = st;
+  o.cols.pod[i] = pod;
+  o.cols.pid[i] = pid;
+  o.cols.svcnode[i] = svcnode;
+  o.cols.trace_h[i] = trace_h;
+  o.cols.conn_h[i] = conn_h;
+  // Unsupported signal types never reach Match (REF correlator.go:73-77), and a zero
+  // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
+  const bool joinable = slot >= 0 && ts != 0;
+  if (ts == 0) ++zero_ts;
+#pragma unroll
+  for (int k = 0; k < kKeyTypes; ++k) {
+    uint64_t h = joinable ? key_hash(k, trace_h, pod, pid, conn_h, svcnode) : 0ull;
+    o.cols.hash[(size_t)k * cap + i] = h;
+    if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ ev, const int* __restrict__ n_ptr,
+                                                      int cap, DecodeOut o) {
+  __shared__ uint32_t s_hist[kSlots * kBuckets];
+  __shared__ uint32_t s_status[kSlots * 3];
+  __shared__ uint32_t s_part[kKeyTypes * kParts];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
+  __syncthreads();
+
+  const int n = min(*n_ptr, cap);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  int unsupported = 0, zero_ts = 0;
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const Event e = ev[i];
+    const int st = e.signal_type;
+    const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
+    const float val = slot >= 0 ? (float)((double)e.value * (double)c_tab.scale[slot]) : (float)e.value;
+    const uint64_t ch = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
+    const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
+    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status,
+               s_part, unsupported, zero_ts);
+  }
+  __syncthreads();
+  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
+  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
+  // wave-level reduction of the scalar counters, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    unsupported += __shfl_xor(unsupported, off);
+    zero_ts += __shfl_xor(zero_ts, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
+    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
+  }
+}
+
+// REF 40-byte records: REF units (count stays count, cpu_steal raw ns, else ns/1e6) and
+// workload identity supplied by the consumer (REF EventMetadata, ringbuf.go:19-26).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ ev, const int* __restrict__ n_ptr,
+                                                   int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,
+                                                   DecodeOut o) {
+  __shared__ uint32_t s_hist[kSlots * kBuckets];
+  __shared__ uint32_t s_status[kSlots * 3];
+  __shared__ uint32_t s_part[kKeyTypes * kParts];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
+  __syncthreads();
+  const int n = min(*n_ptr, cap);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  int unsupported = 0, zero_ts = 0;
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const RefEvent e = ev[i];
+    const uint32_t st = e.signal_type;
+    int slot = (st >= 1 && st <= 9) ? (int)c_tab.type_slot[st] : -1;
+    float val;
+    if (st == 2 || st == 6) val = (float)e.value_ns;           // tcp count, cpu_steal raw ns
+    else val = (float)((double)e.value_ns / 1e6);               // ns -> ms
+    const uint64_t ch = conn_hash(e.conn_src_port, e.conn_dst_port, e.conn_dst_ip);
+    decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, s_hist,
+               s_status, s_part, unsupported, zero_ts);
+  }
+  __syncthreads();
+  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
+  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
+  for (int off = 32; off > 0; off >>= 1) {
+    unsupported += __shfl_xor(unsupported, off);
+    zero_ts += __shfl_xor(zero_ts, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
+    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
+  }
+}
+
+// Span records -> span columns + span partition counts.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp, const int* __restrict__ n_ptr,
+                                                     int cap, SpanCols c, uint32_t* part_cnt) {
+  __shared__ uint32_t s_part[kKeyTypes * kParts];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  __syncthreads();
+  const int n = min(*n_ptr, cap);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const Span s = sp[i];
+    const uint32_t svcnode = ((uint32_t)s.svc_id << 16) | s.node_id;
+    c.ts[i] = s.ts_ns;
+    c.trace_h[i] = s.trace_h;
+    c.conn_h[i] = s.conn_h;
+    c.pod[i] = s.pod_id;
+    c.pid[i] = s.pid;
+    c.svcnode[i] = svcnode;
+    c.group[i] = s.group_id;
+#pragma unroll
+    for (int k = 0; k < kKeyTypes; ++k) {
+      uint64_t h = s.ts_ns != 0 ? key_hash(k, s.trace_h, s.pod_id, s.pid, s.conn_h, svcnode) : 0ull;
+      c.hash[(size_t)k * cap + i] = h;
+      if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
+    }
+  }
+  __syncthreads();
+  store_counts<NT>(s_part, part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
+}
+
+int decode_grid(int cap) {
+  // Fixed per-capacity grid (graph-replayable): ~4 events per thread, capped at kPartBlocks.
+  long long g = ((long long)cap + 1023) / 1024;
+  if (g < 1) g = 1;
+  if (g > kPartBlocks) g = kPartBlocks;
+  return (int)g;
+}
+
+void set_tables(const Tables* host_tables) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tab), host_tables, sizeof(Tables), 0, hipMemcpyHostToDevice);
+}
+
+void launch_decode_events(const void* ev, const int* n_dev, int cap, const SignalCols& cols, uint32_t* hist,
+                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream) {
+  DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
+  constexpr int NT = 256;
+  hipLaunchKernelGGL((k_decode_events<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                     (const Event*)ev, n_dev, cap, o);
+}
+
+void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,
+                       const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                       unsigned long long* misc, hipStream_t stream) {
+  DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
+  constexpr int NT = 256;
+  hipLaunchKernelGGL((k_decode_ref<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                     (const RefEvent*)ev, n_dev, cap, pod, svcnode, trace_h, o);
+}
+
+void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
+                         hipStream_t stream) {
+  constexpr int NT = 256;
+  hipLaunchKernelGGL((k_decode_spans<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                     (const Span*)sp, n_dev, cap, cols, part_cnt);
+}
+
+}  // namespace mislo

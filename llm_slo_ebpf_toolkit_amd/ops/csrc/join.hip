@@ -1,0 +1,446 @@
+// K2: radix-partitioned, LDS-staged span <-> signal hash join with REF's 4-tier rules.
+//
+// REF semantics (pkg/correlation/dns.go:50-113, ebpfcorrelator/correlator.go:50-125):
+// a (span, signal) pair matches at the FIRST tier it satisfies -- trace_id exact (1.0),
+// pod+pid within 100 ms (0.9), pod+conn within 250 ms (0.8), service+node within 500 ms
+// (0.65) -- all inside the outer window, windows compared as |dt| <= w on int64 ns,
+// zero timestamps never match. Per span the matches with conf >= threshold are ranked by
+// (conf desc, |dt| asc, input order), the best `fanout` (3) are kept and max-merged into
+// the span's attribute row; unmatched / low-confidence / fanout-dropped / unsupported
+// pairs are counted (DebugStats).
+//
+// GPU design (MI355X):
+//   1. decode (decode.hip) hashes every record's 4 join keys; the top 10 hash bits pick
+//      one of 1024 partitions per key type, counted per workgroup;
+//   2. k_part_scan / k_base_scan turn per-workgroup counts into scatter offsets;
+//   3. k_scatter writes record indices into partition lists (no global atomics);
+//   4. k_probe: one workgroup per (key type, partition) stages the partition's SPANS in
+//      LDS (bitonic-sorted by (key hash, ts)), then streams the partition's SIGNALS
+//      through it: binary search the key range, walk the |dt| window, drop pairs that
+//      satisfy a higher-precedence tier (each pair is found exactly once, at its own
+//      tier), and insert accepted candidates into the span's top-3 with a lock-free
+//      cascade of 64-bit atomicMin (key = tier | |dt| | signal index, so the numeric
+//      minimum IS REF's stable-sort order). The broad service+node tier, which REF can
+//      only ever count as low-confidence at the default threshold (0.65 < 0.7), is
+//      counted with two binary searches instead of enumerating O(S x N) pairs; pairs of
+//      higher tiers that also satisfy it are subtracted (overlap) to keep counts exact.
+//   5. k_finalize max-merges the kept candidates per span, writes the confidence and the
+//      retrieval decomposition. Incident-group features are the mean value per signal
+//      slot over either every accepted candidate pair (group_mode 1, accumulated in the
+//      probe) or the spans' merged top-3 attributes (group_mode 0, REF-style).
+#include "mislo_common.h"
+#include "mislo_launch.h"
+
+namespace mislo {
+
+constexpr int kSigBits = 27;  // top-3 key: [63:62] tier, [61:27] |dt| ns, [26:0] signal idx
+constexpr int kChunk = 1024;  // spans staged in LDS per pass
+
+// ---------------------------------------------------------------------------------------
+// partition scan + scatter
+// ---------------------------------------------------------------------------------------
+
+// part_blk[b][c] counts -> part_off[b][c] exclusive prefix over blocks, part_tot[c]
+__global__ __launch_bounds__(256) void k_part_scan(const uint32_t* __restrict__ part_blk, int nblk,
+                                                   uint32_t* __restrict__ part_off, uint32_t* __restrict__ part_tot) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= kKeyTypes * kParts) return;
+  uint32_t run = 0;
+  for (int b = 0; b < nblk; ++b) {
+    const size_t idx = (size_t)b * kKeyTypes * kParts + c;
+    const uint32_t v = part_blk[idx];
+    part_off[idx] = run;
+    run += v;
+  }
+  part_tot[c] = run;
+}
+
+// exclusive scan of the 4096 partition totals (one workgroup of 1024 threads, 4 each)
+__global__ __launch_bounds__(1024) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base) {
+  __shared__ uint32_t s[1024];
+  const int t = threadIdx.x;
+  uint32_t v[4];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = tot[t * 4 + j];
+    sum += v[j];
+  }
+  s[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    uint32_t x = t >= off ? s[t - off] : 0;
+    __syncthreads();
+    s[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = s[t] - sum;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    base[t * 4 + j] = run;
+    run += v[j];
+  }
+  if (t == 1023) base[kKeyTypes * kParts] = s[1023];
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scatter(const uint64_t* __restrict__ hash, const int* __restrict__ n_ptr,
+                                                int cap, const uint32_t* __restrict__ part_off,
+                                                const uint32_t* __restrict__ base, uint32_t* __restrict__ items) {
+  __shared__ uint32_t s_cnt[kKeyTypes * kParts];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_cnt[i] = 0;
+  __syncthreads();
+  const int n = min(*n_ptr, cap);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+#pragma unroll
+    for (int k = 0; k < kKeyTypes; ++k) {
+      const uint64_t h = hash[(size_t)k * cap + i];
+      if (!h) continue;
+      const int c = k * kParts + part_of(h);
+      const uint32_t r = atomicAdd(&s_cnt[c], 1u);
+      items[base[c] + my_off[c] + r] = (uint32_t)i;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// probe
+// ---------------------------------------------------------------------------------------
+
+__device__ __forceinline__ bool less_ht(uint64_t h1, int64_t t1, uint64_t h2, int64_t t2) {
+  return h1 < h2 || (h1 == h2 && t1 < t2);
+}
+
+__device__ __forceinline__ void top3_insert(unsigned long long* slot3, unsigned long long key) {
+  // Concurrent insertion into a sorted 3-slot array: each atomicMin keeps the smaller of
+  // (slot, key) in the slot and the larger continues down; the multiset is preserved and
+  // every slot only decreases, so the final slots are the 3 smallest keys in order.
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const unsigned long long old = atomicMin(slot3 + j, key);
+    if (old == kEmpty) return;
+    key = old > key ? old : key;
+  }
+}
+
+__device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
+
+// LDS budget per workgroup: kChunk x (hash 8 + ts 8 + idx 4 + top3 24 + count 4) B
+// + kLdsGroups x 16 x 8 B of incident accumulators = 48 KiB + 8 KiB at kChunk 1024,
+// i.e. two workgroups per CU. All per-pair updates (top-3 cascade, candidate count,
+// incident sums) hit LDS; global atomics are issued once per (span, chunk) on flush.
+constexpr int kLdsGroups = 64;
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
+                                              const uint32_t* __restrict__ span_base, SignalCols gc,
+                                              const uint32_t* __restrict__ sig_items,
+                                              const uint32_t* __restrict__ sig_base, int sig_cap, int span_cap,
+                                              JoinParams jp, unsigned long long* __restrict__ top3,
+                                              uint32_t* __restrict__ cnt, int n_groups, float* __restrict__ gsum,
+                                              uint32_t* __restrict__ gcnt, unsigned long long* __restrict__ dbg) {
+  __shared__ uint64_t s_h[kChunk];
+  __shared__ int64_t s_t[kChunk];
+  __shared__ uint32_t s_i[kChunk];
+  __shared__ unsigned long long s_top[kChunk * 3];
+  __shared__ uint32_t s_cnt[kChunk];
+  __shared__ float s_gsum[kLdsGroups * kSlots];
+  __shared__ uint32_t s_gcnt[kLdsGroups * kSlots];
+
+  const int k = blockIdx.y;
+  const int c = k * kParts + blockIdx.x;
+  const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
+  const uint32_t sg0 = sig_base[c], sg1 = sig_base[c + 1];
+  if (sp0 == sp1 || sg0 == sg1) return;
+
+  const int64_t w = jp.win_ns[k];
+  const bool cand_tier = jp.conf[k] >= jp.threshold;
+  const bool count_only = (k == 3) && !cand_tier;          // broad tier: count, never enumerate
+  const bool track_overlap = (k < 3) && (jp.conf[3] < jp.threshold);
+  const bool grp_lds = n_groups <= kLdsGroups;
+  const bool do_groups = cand_tier && jp.group_mode == 1 && n_groups > 0;
+  unsigned long long n_cand = 0, n_low = 0, n_overlap = 0;
+
+  if (do_groups && grp_lds) {
+    for (int i = threadIdx.x; i < kLdsGroups * kSlots; i += NT) {
+      s_gsum[i] = 0.f;
+      s_gcnt[i] = 0u;
+    }
+  }
+
+  for (uint32_t c0 = sp0; c0 < sp1; c0 += kChunk) {
+    const int m = (int)min((uint32_t)kChunk, sp1 - c0);
+    int M = 1;
+    while (M < m) M <<= 1;
+    __syncthreads();
+    for (int i = threadIdx.x; i < M; i += NT) {
+      if (i < m) {
+        const uint32_t s = span_items[c0 + i];
+        s_h[i] = sc.hash[(size_t)k * span_cap + s];
+        s_t[i] = sc.ts[s];
+        s_i[i] = s;
+      } else {
+        s_h[i] = ~0ull;
+        s_t[i] = INT64_MAX;
+        s_i[i] = 0xFFFFFFFFu;
+      }
+      s_top[3 * i] = kEmpty;
+      s_top[3 * i + 1] = kEmpty;
+      s_top[3 * i + 2] = kEmpty;
+      s_cnt[i] = 0u;
+    }
+    __syncthreads();
+    // bitonic sort of (hash, ts, idx) ascending
+    for (int size = 2; size <= M; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int t = threadIdx.x; t < (M >> 1); t += NT) {
+          const int i = 2 * t - (t & (stride - 1));
+          const int j = i + stride;
+          const bool up = (i & size) == 0;
+          const bool gt = less_ht(s_h[j], s_t[j], s_h[i], s_t[i]);
+          if (gt == up) {
+            uint64_t th = s_h[i]; s_h[i] = s_h[j]; s_h[j] = th;
+            int64_t tt = s_t[i]; s_t[i] = s_t[j]; s_t[j] = tt;
+            uint32_t ti = s_i[i]; s_i[i] = s_i[j]; s_i[j] = ti;
+          }
+        }
+        __syncthreads();
+      }
+    }
+
+    for (uint32_t q = sg0 + threadIdx.x; q < sg1; q += NT) {
+      const uint32_t g = sig_items[q];
+      const uint64_t h = gc.hash[(size_t)k * sig_cap + g];
+      const int64_t t = gc.ts[g];
+      // lower_bound (h, t - w)
+      int lo = 0, hi = m;
+      const int64_t tlo = t - w;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (less_ht(s_h[mid], s_t[mid], h, tlo)) lo = mid + 1; else hi = mid;
+      }
+      const int64_t thi = t + w;
+      if (count_only) {
+        // upper_bound (h, t + w): hash equality == key equality for this key type
+        int a = lo, b = m;
+        while (a < b) {
+          const int mid = (a + b) >> 1;
+          if (less_ht(h, thi, s_h[mid], s_t[mid])) b = mid; else a = mid + 1;
+        }
+        n_low += (unsigned long long)(a - lo);
+        continue;
+      }
+      if (lo >= m || s_h[lo] != h || s_t[lo] > thi) continue;
+      const uint32_t g_pod = gc.pod[g], g_pid = gc.pid[g], g_sn = gc.svcnode[g];
+      const uint64_t g_tr = gc.trace_h[g], g_cn = gc.conn_h[g];
+      const int g_slot = gc.slot[g];
+      const float g_val = gc.val[g];
+      for (int i = lo; i < m && s_h[i] == h && s_t[i] <= thi; ++i) {
+        const uint32_t s = s_i[i];
+        const int64_t dt = iabs64(t - s_t[i]);
+        const uint32_t s_pod = sc.pod[s];
+        const uint64_t s_cn = sc.conn_h[s];
+        if (k == 2 && !(s_pod == g_pod && s_cn == g_cn)) continue;  // hash collision guard
+        // higher-precedence tiers (REF Match order): skip pairs found at their own tier
+        const uint64_t s_tr = sc.trace_h[s];
+        const bool t0 = s_tr != 0 && s_tr == g_tr;  // |dt| <= outer holds for every pair here
+        if (k >= 1 && t0) continue;
+        if (k >= 2) {
+          const uint32_t s_pid = sc.pid[s];
+          const bool t1 = s_pod != 0 && s_pod == g_pod && s_pid != 0 && s_pid == g_pid && dt <= jp.win_ns[1];
+          if (t1) continue;
+        }
+        if (k >= 3) {
+          const bool t2 = s_pod != 0 && s_pod == g_pod && s_cn != 0 && s_cn == g_cn && dt <= jp.win_ns[2];
+          if (t2) continue;
+        }
+        if (cand_tier) {
+          unsigned long long key = ((unsigned long long)k << 62) | ((unsigned long long)dt << kSigBits) |
+                                   (unsigned long long)g;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {  // LDS top-3 cascade (see top3_insert)
+            const unsigned long long old = atomicMin(&s_top[3 * i + j], key);
+            if (old == kEmpty) break;
+            key = old > key ? old : key;
+          }
+          atomicAdd(&s_cnt[i], 1u);
+          ++n_cand;
+          if (do_groups) {
+            const uint32_t grp = sc.group[s];
+            if (grp < (uint32_t)n_groups) {
+              if (grp_lds) {
+                atomicAdd(&s_gsum[grp * kSlots + g_slot], g_val);
+                atomicAdd(&s_gcnt[grp * kSlots + g_slot], 1u);
+              } else {
+                atomicAdd(gsum + (size_t)grp * kSlots + g_slot, g_val);
+                atomicAdd(gcnt + (size_t)grp * kSlots + g_slot, 1u);
+              }
+            }
+          }
+        } else {
+          ++n_low;
+        }
+        if (track_overlap) {
+          const uint32_t s_sn = sc.svcnode[s];
+          if ((s_sn >> 16) != 0 && (s_sn & 0xFFFF) != 0 && s_sn == g_sn && dt <= jp.win_ns[3]) ++n_overlap;
+        }
+      }
+    }
+    // flush this chunk's per-span candidates to the global top-3 / counts
+    __syncthreads();
+    if (cand_tier) {
+      for (int i = threadIdx.x; i < m; i += NT) {
+        const uint32_t nc = s_cnt[i];
+        if (!nc) continue;
+        const uint32_t s = s_i[i];
+        atomicAdd(cnt + s, nc);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const unsigned long long key = s_top[3 * i + j];
+          if (key == kEmpty) break;
+          top3_insert(top3 + 3ull * s, key);
+        }
+      }
+    }
+  }
+  if (do_groups && grp_lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < n_groups * kSlots; i += NT) {
+      const uint32_t n = s_gcnt[i];
+      if (n) {
+        atomicAdd(gsum + i, s_gsum[i]);
+        atomicAdd(gcnt + i, n);
+      }
+    }
+  }
+  // wave reduce, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    n_cand += __shfl_xor(n_cand, off);
+    n_low += __shfl_xor(n_low, off);
+    n_overlap += __shfl_xor(n_overlap, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (n_cand) atomicAdd(&dbg[0], n_cand);
+    if (n_low) atomicAdd(&dbg[1], n_low);
+    if (n_overlap) atomicAdd(&dbg[2], n_overlap);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// finalize: top-3 -> attribute max-merge, confidence, retrieval decomposition, groups
+// ---------------------------------------------------------------------------------------
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr, int span_cap,
+                                                 const unsigned long long* __restrict__ top3,
+                                                 const uint32_t* __restrict__ cnt, SignalCols gc, SpanCols sc,
+                                                 JoinParams jp, const float* __restrict__ base_attrs,
+                                                 float* __restrict__ attrs, float* __restrict__ conf,
+                                                 float* __restrict__ kernel_ms, int n_groups,
+                                                 float* __restrict__ gsum, uint32_t* __restrict__ gcnt,
+                                                 unsigned long long* __restrict__ dbg) {
+  const int ns = min(*ns_ptr, span_cap);
+  const int s = blockIdx.x * NT + threadIdx.x;
+  unsigned long long dropped = 0, enriched = 0;
+  if (s < ns) {
+    float a[kSlots];
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) a[j] = base_attrs ? base_attrs[(size_t)s * kSlots + j] : __builtin_nanf("");
+    float mc = 0.f;
+    const int keep = jp.fanout;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const unsigned long long key = top3[3ull * s + j];
+      if (key == kEmpty || j >= keep) continue;
+      const int tier = (int)(key >> 62);
+      const uint32_t g = (uint32_t)(key & ((1ull << kSigBits) - 1));
+      const int slot = gc.slot[g];
+      const float v = gc.val[g];
+      // REF merge: attr = value if absent or value > existing
+      float cur = a[0];
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) if (q == slot) cur = a[q];
+      const bool take = (cur != cur) || v > cur;
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) if (q == slot && take) a[q] = v;
+      mc = fmaxf(mc, jp.conf[tier]);
+    }
+    const uint32_t c = cnt[s];
+    if ((int)c > keep) dropped = c - keep;
+    if (mc > 0.f) enriched = 1;
+    conf[s] = mc;
+    // retrieval decomposition (REF correlator.go:179-194): dns + connect + tls
+    float km = 0.f;
+    if (a[0] == a[0]) km += a[0];
+    if (a[3] == a[3]) km += a[3];
+    if (a[5] == a[5]) km += a[5];
+    kernel_ms[s] = km > 0.f ? km : __builtin_nanf("");
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) attrs[(size_t)s * kSlots + j] = a[j];
+    const uint32_t grp = sc.group[s];
+    if (jp.group_mode == 0 && n_groups > 0 && grp < (uint32_t)n_groups) {
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) {
+        if (a[j] == a[j]) {
+          atomicAdd(gsum + (size_t)grp * kSlots + j, a[j]);
+          atomicAdd(gcnt + (size_t)grp * kSlots + j, 1u);
+        }
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    dropped += __shfl_xor(dropped, off);
+    enriched += __shfl_xor(enriched, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (dropped) atomicAdd(&dbg[3], dropped);
+    if (enriched) atomicAdd(&dbg[4], enriched);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_group_features(int n, const float* __restrict__ gsum,
+                                                        const uint32_t* __restrict__ gcnt, float* __restrict__ feat) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = gcnt[i];
+  feat[i] = c ? gsum[i] / (float)c : __builtin_nanf("");
+}
+
+// ---------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------
+
+void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
+                      uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(k_part_scan, dim3((kKeyTypes * kParts + 255) / 256), dim3(256), 0, stream, part_blk, nblk,
+                     part_off, part_tot);
+  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(1024), 0, stream, part_tot, part_base);
+  hipLaunchKernelGGL((k_scatter<256>), dim3(nblk), dim3(256), 0, stream, hash, n_dev, cap, part_off, part_base,
+                     items);
+}
+
+void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
+                  const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
+                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, float* gsum,
+                  uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream) {
+  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes), dim3(256), 0, stream, sc, span_items, span_base, gc,
+                     sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg);
+}
+
+void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
+                     const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,
+                     float* attrs, float* conf, float* kernel_ms, int n_groups, float* gsum, uint32_t* gcnt,
+                     float* feat, unsigned long long* dbg, hipStream_t stream) {
+  hipLaunchKernelGGL((k_finalize<256>), dim3((span_cap + 255) / 256), dim3(256), 0, stream, ns_dev, span_cap, top3,
+                     cnt, gc, sc, jp, base_attrs, attrs, conf, kernel_ms, n_groups, gsum, gcnt, dbg);
+  if (n_groups > 0) {
+    const int n = n_groups * kSlots;
+    hipLaunchKernelGGL(k_group_features, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt, feat);
+  }
+}
+
+}  // namespace mislo

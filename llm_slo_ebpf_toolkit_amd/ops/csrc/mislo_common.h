@@ -1,0 +1,149 @@
+// Shared device/host definitions for the MI355X (gfx950) LLM-SLO engine kernels.
+//
+// Record layouts mirror llm_slo_ebpf_toolkit_amd/collector/records.py (EVENT, SPAN,
+// REF_EVENT). Signal slots / decode scales / thresholds / histogram edges mirror
+// signals/catalog.py and are uploaded once into __constant__ memory (mislo_set_tables).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mislo {
+
+constexpr int kSlots = 16;          // feature slots (12 REF + 4 GPU signals)
+constexpr int kBuckets = 16;        // histogram buckets per slot (15 edges + overflow)
+constexpr int kKeyTypes = 4;        // trace, pod+pid, pod+conn, svc+node
+constexpr int kPartBits = 10;       // 1024 hash partitions per key type
+constexpr int kParts = 1 << kPartBits;
+constexpr int kPartBlocks = 512;    // max decode/scatter workgroups (per-block partition counts)
+constexpr int kMaxDomains = 16;     // posterior columns (10 used, padded to the MFMA tile)
+constexpr int kMaxTypes = 128;      // signal_type lookup table size
+constexpr uint64_t kEmpty = ~0ull;  // empty top-3 slot
+constexpr uint8_t kNoSlot = 0xFF;
+
+// 64-byte event record (collector/records.py EVENT).
+struct alignas(64) Event {
+  int64_t ts_ns;
+  uint64_t value;
+  uint64_t trace_h;
+  uint32_t pid, tid, pod_id, dst_ip;
+  uint16_t signal_type, node_id, svc_id, flags, src_port, dst_port;
+  int32_t err;
+  uint64_t conn_h;
+};
+static_assert(sizeof(Event) == 64, "Event must be 64 bytes");
+
+// REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).
+struct __attribute__((packed)) RefEvent {
+  uint32_t pid, tid;
+  uint64_t timestamp_ns;
+  uint32_t signal_type;
+  uint64_t value_ns;
+  uint16_t conn_src_port, conn_dst_port;
+  uint32_t conn_dst_ip;
+  int32_t errno_val;
+};
+static_assert(sizeof(RefEvent) == 40, "RefEvent must be 40 bytes");
+
+// 64-byte span record (collector/records.py SPAN).
+struct alignas(64) Span {
+  int64_t ts_ns;
+  uint64_t trace_h, conn_h;
+  uint32_t pid, pod_id;
+  uint16_t node_id, svc_id;
+  uint32_t group_id;
+  float ttft_ms, latency_ms;
+  uint64_t span_h, reserved;
+};
+static_assert(sizeof(Span) == 64, "Span must be 64 bytes");
+
+// Decoded signal columns (structure of arrays, one entry per event).
+struct SignalCols {
+  int64_t* ts;
+  float* val;
+  uint8_t* slot;      // kNoSlot = unsupported / unknown type
+  uint8_t* status;    // 0 ok, 1 warning, 2 error
+  uint32_t* pod;
+  uint32_t* pid;
+  uint32_t* svcnode;  // (svc << 16) | node
+  uint64_t* trace_h;
+  uint64_t* conn_h;
+  uint64_t* hash;     // [kKeyTypes][n] partition hashes, 0 = key invalid
+};
+
+struct SpanCols {
+  int64_t* ts;
+  uint64_t* trace_h;
+  uint64_t* conn_h;
+  uint32_t* pod;
+  uint32_t* pid;
+  uint32_t* svcnode;
+  uint32_t* group;
+  uint64_t* hash;     // [kKeyTypes][n]
+};
+
+// Correlation tiers (REF pkg/correlation/dns.go:50-76).
+struct JoinParams {
+  int64_t outer_ns;       // outer window (default 2 s)
+  int64_t win_ns[4];      // effective per-tier window = min(outer, tier window)
+  float conf[4];          // 1.0, 0.9, 0.8, 0.65
+  float threshold;        // enrichment threshold (default 0.7)
+  int fanout;             // max join fanout (3)
+  int group_mode;         // incident features: 0 = mean of span top-3 attrs, 1 = mean of all candidates
+};
+
+struct Tables {
+  int8_t type_slot[kMaxTypes];
+  float scale[kSlots];
+  float warn[kSlots];
+  float err[kSlots];
+  float edges[kSlots][kBuckets];  // bucket b holds (edges[b-1], edges[b]]; last edge = +inf
+};
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Connection hash of (src_port, dst_port, dst_ip); 0 when no port is set
+// (REF builds a conn tuple only when a port != 0, pkg/collector/ringbuf.go:181).
+__host__ __device__ inline uint64_t conn_hash(uint32_t sport, uint32_t dport, uint32_t ip) {
+  if (sport == 0 && dport == 0) return 0;
+  uint64_t packed = ((uint64_t)(sport & 0xFFFF) << 48) | ((uint64_t)(dport & 0xFFFF) << 32) | ip;
+  uint64_t h = splitmix64(packed);
+  return h ? h : 1;
+}
+
+// Key hashes per key type; 0 = invalid key (empty field on this record). The top
+// kPartBits bits select the partition.
+__host__ __device__ inline uint64_t key_hash(int k, uint64_t trace_h, uint32_t pod, uint32_t pid,
+                                             uint64_t conn_h, uint32_t svcnode) {
+  uint64_t key;
+  switch (k) {
+    case 0:
+      if (trace_h == 0) return 0;
+      key = trace_h ^ 0x1111111111111111ull;
+      break;
+    case 1:
+      if (pod == 0 || pid == 0) return 0;
+      key = ((uint64_t)pod << 32 | pid) ^ 0x2222222222222222ull;
+      break;
+    case 2:
+      if (pod == 0 || conn_h == 0) return 0;
+      key = splitmix64(conn_h) ^ ((uint64_t)pod * 0x9E3779B97F4A7C15ull) ^ 0x3333333333333333ull;
+      break;
+    default:
+      if ((svcnode >> 16) == 0 || (svcnode & 0xFFFF) == 0) return 0;
+      key = (uint64_t)svcnode ^ 0x4444444444444444ull;
+      break;
+  }
+  uint64_t h = splitmix64(key);
+  return h ? h : 1;
+}
+
+__host__ __device__ inline int part_of(uint64_t h) { return (int)(h >> (64 - kPartBits)); }
+
+}  // namespace mislo

@@ -1,0 +1,56 @@
+// Host-side launch API of the MI355X engine kernels (plain pointers + hipStream_t), so the
+// torch bindings, the native agent runtime and the C++ tests can all drive them.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mislo_common.h"
+
+namespace mislo {
+
+// Attribution model in linear-logit form (models/bayes.py LinearPosteriorModel), resident
+// in device memory (too large for kernel arguments).
+struct PosteriorModel {
+  double w[kSlots][kMaxDomains];  // [slot][domain]
+  double bias[kMaxDomains];       // -inf = inactive domain
+  double mean[kSlots];            // continuous mode centring
+  double nominal[kSlots];         // continuous mode imputation for absent signals
+  float thr[kSlots];              // elevated thresholds
+  uint32_t dom_mask[kMaxDomains]; // per domain: slots with P(elevated|d) >= 0.5
+  uint32_t table_mask;            // slots known to the model (binary mode)
+  int32_t mode;                   // 0 binary evidence, 1 continuous (log1p) features
+};
+
+// decode.hip
+void set_tables(const Tables* host_tables);
+int decode_grid(int cap);
+void launch_decode_events(const void* ev, const int* n_dev, int cap, const SignalCols& cols, uint32_t* hist,
+                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream);
+void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,
+                       const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                       unsigned long long* misc, hipStream_t stream);
+void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
+                         hipStream_t stream);
+
+// join.hip
+void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
+                      uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
+                      hipStream_t stream);
+void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
+                  const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
+                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, float* gsum,
+                  uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream);
+void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
+                     const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,
+                     float* attrs, float* conf, float* kernel_ms, int n_groups, float* gsum, uint32_t* gcnt,
+                     float* feat, unsigned long long* dbg, hipStream_t stream);
+
+// posterior.hip
+void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
+                      double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
+                      hipStream_t stream);
+void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
+                  const float* weights, double* out, double* count, hipStream_t stream);
+
+}  // namespace mislo

@@ -1,0 +1,172 @@
+// K3: batched fault-domain posteriors and labelled sufficient statistics on matrix cores.
+//
+// Every attribution model (REF-exact naive Bayes, learned Bayes, covariance LDA; see
+// models/bayes.py) is a linear-logit model: logits[b, d] = X[b, :] @ W[:, d] + bias[d],
+// X = binary evidence (value >= elevated threshold, REF bayesian.go:194-243) or centred
+// log1p features. One wave computes a 16-incident x 16-domain logit tile with four
+// v_mfma_f64_16x16x4_f64 (K = 16 signal slots) -- float64 like REF's math.Log sums, so
+// the GPU posteriors match the CPU oracle to ~1e-15 -- then does the log-sum-exp,
+// argmax (ties -> lowest domain index == REF's stable sort), evidence bitmask
+// (elevated & P(elevated|d) >= 0.5) and the confusion-matrix update in registers.
+//
+// k_stats is the "MFMA covariance step": U^T V with U = [E | X], V = [Y | X] over a batch
+// of labelled incidents (K = incidents), giving E^T Y (likelihood counts), X^T Y (class
+// sums) and X^T X (scatter) in one 32x32 f64 product, reduced across waves with f64
+// atomics. These are the sufficient statistics the learned models are refit from.
+//
+// f64 MFMA C/D layout on gfx950: col = lane & 15, row = (lane >> 4) + 4 * reg
+// (cdna_hip_programming.md section 3 -- NOT the f32 row map).
+#include "mislo_common.h"
+#include "mislo_launch.h"
+
+namespace mislo {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double feature_x(float v, int s, const PosteriorModel& pm) {
+  if (pm.mode == 0) {
+    const bool e = (v == v) && v >= pm.thr[s] && ((pm.table_mask >> s) & 1u);
+    return e ? 1.0 : 0.0;
+  }
+  const double vv = (v == v) ? (double)v : pm.nominal[s];
+  return log1p(vv > 0.0 ? vv : 0.0) - pm.mean[s];
+}
+
+__device__ __forceinline__ uint32_t elevated_bits(const float* __restrict__ row, const PosteriorModel& pm) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) {
+    const float v = row[s];
+    if ((v == v) && v >= pm.thr[s]) b |= 1u << s;
+  }
+  return b & pm.table_mask;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_posterior(const float* __restrict__ feat, const int* __restrict__ ng_ptr,
+                                                  int cap, const PosteriorModel* __restrict__ pmp,
+                                                  const int32_t* __restrict__ labels,
+                                                  double* __restrict__ post, int32_t* __restrict__ pred,
+                                                  double* __restrict__ conf, uint32_t* __restrict__ evbits,
+                                                  uint32_t* __restrict__ confusion) {
+  const int G = min(*ng_ptr, cap);
+  const PosteriorModel& pm = *pmp;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row0 = (blockIdx.x * (NT / 64) + wave) * 16;
+  if (row0 >= G) return;  // whole wave exits together
+  const int i = lane & 15;
+  const int kq = lane >> 4;
+
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int s = 4 * kk + kq;
+    const int r = row0 + i;
+    const double a = r < G ? feature_x(feat[(size_t)r * kSlots + s], s, pm) : 0.0;
+    const double b = pm.w[s][i];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+
+  const double bias = pm.bias[i];
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int r = row0 + kq + 4 * reg;
+    const double lg = acc[reg] + bias;  // -inf for inactive domains
+    // max + argmax over the 16 domain lanes (ties -> lowest index)
+    double m = lg;
+    int am = i;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const double om = __shfl_xor(m, off, 16);
+      const int oa = __shfl_xor(am, off, 16);
+      if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+    }
+    const double ex = (lg == -INFINITY) ? 0.0 : exp(lg - m);
+    double sum = ex;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
+    const double logz = m + log(sum);
+    const double p = (lg == -INFINITY) ? 0.0 : exp(lg - logz);
+    if (r < G) {
+      post[(size_t)r * kMaxDomains + i] = p;
+      const uint32_t eb = elevated_bits(feat + (size_t)r * kSlots, pm);
+      evbits[(size_t)r * kMaxDomains + i] = eb & pm.dom_mask[i];
+      if (i == 0) {
+        pred[r] = am;
+        conf[r] = exp(m - logz);
+        if (labels != nullptr) {
+          const int y = labels[r];
+          if (y >= 0 && y < kMaxDomains) atomicAdd(confusion + y * kMaxDomains + am, 1u);
+        }
+      }
+    }
+  }
+}
+
+// U^T V over labelled incidents; out[32][32] f64, count[16] f64.
+template <int NT, int ROWS_PER_WAVE>
+__global__ __launch_bounds__(NT) void k_stats(const float* __restrict__ feat, const int* __restrict__ ng_ptr, int cap,
+                                              const PosteriorModel* __restrict__ pmp, const int32_t* __restrict__ labels,
+                                              const float* __restrict__ weights, double* __restrict__ out,
+                                              double* __restrict__ count) {
+  const int G = min(*ng_ptr, cap);
+  const PosteriorModel& pm = *pmp;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int base = (blockIdx.x * (NT / 64) + wave) * ROWS_PER_WAVE;
+  if (base >= G) return;
+  const int i = lane & 15;
+  const int kq = lane >> 4;
+  f64x4 t00 = {0, 0, 0, 0}, t01 = {0, 0, 0, 0}, t10 = {0, 0, 0, 0}, t11 = {0, 0, 0, 0};
+  for (int r0 = base; r0 < base + ROWS_PER_WAVE && r0 < G; r0 += 4) {
+    const int r = r0 + kq;
+    double e = 0.0, x = 0.0, y = 0.0;
+    if (r < G) {
+      const int lab = labels[r];
+      const double wgt = weights ? (double)weights[r] : 1.0;
+      if (lab >= 0) {
+        const float v = feat[(size_t)r * kSlots + i];
+        e = ((v == v) && v >= pm.thr[i]) ? 1.0 : 0.0;
+        const double vv = (v == v) ? (double)v : pm.nominal[i];
+        x = log1p(vv > 0.0 ? vv : 0.0);
+        y = (lab == i) ? wgt : 0.0;
+        if (i == 0) atomicAdd(count + (lab < kMaxDomains ? lab : 0), wgt);
+      }
+    }
+    // A = U^T (rows = U columns, k = incident), B = V (k = incident, cols = V columns)
+    t00 = __builtin_amdgcn_mfma_f64_16x16x4f64(e, y, t00, 0, 0, 0);  // E^T Y
+    t01 = __builtin_amdgcn_mfma_f64_16x16x4f64(e, x, t01, 0, 0, 0);  // E^T X
+    t10 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, t10, 0, 0, 0);  // X^T Y
+    t11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, t11, 0, 0, 0);  // X^T X
+  }
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int rr = kq + 4 * reg;
+    atomicAdd(out + (size_t)rr * 32 + i, t00[reg]);
+    atomicAdd(out + (size_t)rr * 32 + 16 + i, t01[reg]);
+    atomicAdd(out + (size_t)(16 + rr) * 32 + i, t10[reg]);
+    atomicAdd(out + (size_t)(16 + rr) * 32 + 16 + i, t11[reg]);
+  }
+}
+
+void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
+                      double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
+                      hipStream_t stream) {
+  constexpr int NT = 256;
+  const int rows_per_block = (NT / 64) * 16;
+  const int grid = (cap + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL((k_posterior<NT>), dim3(grid > 0 ? grid : 1), dim3(NT), 0, stream, feat, ng_dev, cap, pm, labels,
+                     post, pred, conf, evbits, confusion);
+}
+
+void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
+                  const float* weights, double* out, double* count, hipStream_t stream) {
+  constexpr int NT = 256, RPW = 256;
+  const int rows_per_block = (NT / 64) * RPW;
+  const int grid = (cap + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL((k_stats<NT, RPW>), dim3(grid > 0 ? grid : 1), dim3(NT), 0, stream, feat, ng_dev, cap, pm,
+                     labels, weights, out, count);
+}
+
+}  // namespace mislo

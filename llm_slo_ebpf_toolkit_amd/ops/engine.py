@@ -1,0 +1,148 @@
+"""Python driver of the device-resident window ``Engine`` (ops/csrc/bindings.cpp).
+
+``GpuEngine`` owns pinned host staging + device record buffers sized for the window
+capacity, uploads a window's records with async H2D copies on a copy stream, runs the
+whole kernel chain on the compute stream (optionally captured once into a HIP graph and
+replayed), and exposes the outputs. Debug-counter decoding reproduces REF's DebugStats
+from the kernel's pair counts (join.hip header).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+
+from ..collector import records
+from ..models.bayes import NOMINAL, LinearPosteriorModel
+from ..signals import catalog
+from . import load
+
+N_DOMAINS_PAD = 16
+
+
+def model_arrays(model: LinearPosteriorModel):
+    import torch
+
+    D = model.weights.shape[1]
+    w = np.zeros((16, N_DOMAINS_PAD), dtype=np.float64)
+    w[:, :D] = model.weights
+    bias = np.full(N_DOMAINS_PAD, -np.inf, dtype=np.float64)
+    bias[:D] = model.bias
+    mean = model.mean if model.mean is not None else np.zeros(16)
+    dom_mask = np.zeros(N_DOMAINS_PAD, dtype=np.int64)
+    for d in range(D):
+        dom_mask[d] = int(sum(1 << s for s in range(16) if model.evidence_mask[s, d]))
+    table_mask = 0xFFFF if model.table_mask is None else int(sum(1 << s for s in range(16) if model.table_mask[s] > 0))
+    mode = 0 if model.feature_mode == "binary" else 1
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
+    return (t(w, np.float64), t(bias, np.float64), t(mean, np.float64), t(NOMINAL, np.float64),
+            t(model.thresholds, np.float32), t(dom_mask, np.int64), table_mask, mode)
+
+
+def decode_debug(dbg: np.ndarray, misc: np.ndarray, n_spans: int, n_events: int) -> Dict[str, int]:
+    """Kernel pair counters -> REF DebugStats (correlator.go:20-25) + extras."""
+    cand, low_raw, overlap, dropped, enriched = (int(x) for x in dbg[:5])
+    unsupported_events = int(misc[0])
+    low = low_raw - overlap
+    n_sup = n_events - unsupported_events
+    return {
+        "candidates": cand, "low_confidence": low, "fanout_dropped": dropped,
+        "unmatched": n_spans * n_sup - (cand + low), "unsupported_type": n_spans * unsupported_events,
+        "spans_enriched": enriched,
+    }
+
+
+@dataclass
+class WindowOutputs:
+    hist: np.ndarray
+    status: np.ndarray
+    debug: Dict[str, int]
+    feat: np.ndarray
+    post: np.ndarray
+    pred: np.ndarray
+    conf: np.ndarray
+    evbits: np.ndarray
+    confusion: np.ndarray
+
+
+class GpuEngine:
+    def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, window_ms: float = 2000.0,
+                 threshold: float = 0.7, fanout: int = 3, group_mode: int = 1):
+        import torch
+
+        self.torch = torch
+        self.device = torch.device("cuda", device)
+        self.mod = load(device)
+        with torch.cuda.device(self.device):
+            self.eng = self.mod.Engine(sig_cap, span_cap, group_cap, device)
+            self.eng.set_join_params(window_ms, threshold, fanout, group_mode)
+            self.ev_dev = torch.zeros(sig_cap * 64, dtype=torch.uint8, device=self.device)
+            self.sp_dev = torch.zeros(span_cap * 64, dtype=torch.uint8, device=self.device)
+            self.ev_host = torch.empty(sig_cap * 64, dtype=torch.uint8, pin_memory=True)
+            self.sp_host = torch.empty(span_cap * 64, dtype=torch.uint8, pin_memory=True)
+            self.cnt_host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+            self.lab_host = torch.full((group_cap,), -1, dtype=torch.int32, pin_memory=True)
+            self.copy_stream = torch.cuda.Stream(self.device)
+        self.sig_cap, self.span_cap, self.group_cap = sig_cap, span_cap, group_cap
+        self.n_events = self.n_spans = self.n_groups = 0
+        self.graph = None
+
+    # ---------------------------------------------------------------------------------
+    def set_model(self, model: LinearPosteriorModel) -> None:
+        with self.torch.cuda.device(self.device):
+            self.eng.set_model(*model_arrays(model))
+
+    def set_join_params(self, window_ms=2000.0, threshold=0.7, fanout=3, group_mode=1):
+        self.eng.set_join_params(window_ms, threshold, fanout, group_mode)
+
+    def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None):
+        """Copy records into pinned staging (host memcpy, no GPU work)."""
+        n, s = events.shape[0], spans.shape[0]
+        if n > self.sig_cap or s > self.span_cap or n_groups > self.group_cap:
+            raise ValueError("window exceeds engine capacity")
+        if events.dtype != records.EVENT or spans.dtype != records.SPAN:
+            raise TypeError("events/spans must use the EVENT/SPAN record dtypes")
+        self.ev_host.numpy()[: n * 64] = events.view(np.uint8).reshape(-1)
+        self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)
+        c = self.cnt_host.numpy()
+        c[:] = (n, s, n_groups, 0)
+        lab = self.lab_host.numpy()
+        lab[:] = -1
+        if labels is not None:
+            lab[: len(labels)] = labels
+        self.n_events, self.n_spans, self.n_groups = n, s, n_groups
+
+    def upload(self, stream=None) -> None:
+        """Async H2D of the staged window on the copy stream; compute waits on an event."""
+        torch = self.torch
+        cs = self.copy_stream
+        with torch.cuda.stream(cs):
+            self.ev_dev[: self.n_events * 64].copy_(self.ev_host[: self.n_events * 64], non_blocking=True)
+            self.sp_dev[: self.n_spans * 64].copy_(self.sp_host[: self.n_spans * 64], non_blocking=True)
+            self.eng.counts.copy_(self.cnt_host, non_blocking=True)
+            self.eng.labels.copy_(self.lab_host, non_blocking=True)
+        (stream or torch.cuda.current_stream(self.device)).wait_stream(cs)
+
+    def run(self, with_labels: bool = True, learn: bool = False) -> None:
+        with self.torch.cuda.device(self.device):
+            self.eng.run_window(self.ev_dev, self.sp_dev, self.n_groups, with_labels, learn)
+
+    def process(self, events, spans, n_groups, labels=None, learn=False) -> "WindowOutputs":
+        self.stage(events, spans, n_groups, labels)
+        self.upload()
+        self.run(labels is not None, learn)
+        return self.outputs()
+
+    def outputs(self) -> WindowOutputs:
+        e = self.eng
+        self.torch.cuda.synchronize(self.device)
+        G = self.n_groups
+        dbg = e.dbg.cpu().numpy()
+        misc = e.misc.cpu().numpy()
+        return WindowOutputs(
+            hist=e.hist.cpu().numpy().astype(np.int64), status=e.status_cnt.cpu().numpy().astype(np.int64),
+            debug=decode_debug(dbg, misc, self.n_spans, self.n_events), feat=e.feat[:G].cpu().numpy(),
+            post=e.post[:G].cpu().numpy(), pred=e.pred[:G].cpu().numpy(), conf=e.gconf[:G].cpu().numpy(),
+            evbits=e.evbits[:G].cpu().numpy().view(np.uint32), confusion=e.confusion.cpu().numpy().astype(np.int64))

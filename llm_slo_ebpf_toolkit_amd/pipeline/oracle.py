@@ -1,0 +1,168 @@
+"""CPU reference ("oracle") of one GPU window, bit-faithful to the kernels' contracts.
+
+Given the same 64-byte EVENT/SPAN records the GPU consumes, recompute with plain numpy
+and REF's scalar semantics (correlation/match.py, correlation/correlator.py):
+decode (float32 values exactly as the kernel rounds them), per-span tiers, top-3
+candidate keys, merged attributes, confidence, debug counters, incident-group features,
+histograms and posteriors. Tests compare the GPU outputs against this (exact for keys,
+tiers, counts, predictions; tolerance for float sums whose order differs).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+
+from ..collector import records
+from ..signals import catalog
+from ..utils.timeutil import MS
+
+NO_SLOT = 255
+SIG_BITS = 27
+TIER_CONF = (1.0, 0.9, 0.8, 0.65)
+
+
+@dataclass
+class Decoded:
+    ts: np.ndarray
+    val: np.ndarray
+    slot: np.ndarray
+    status: np.ndarray
+    pod: np.ndarray
+    pid: np.ndarray
+    svcnode: np.ndarray
+    trace: np.ndarray
+    conn: np.ndarray
+
+
+def decode_events(ev: np.ndarray) -> Decoded:
+    type_slot = np.full(65536, NO_SLOT, dtype=np.uint8)
+    scale32 = np.zeros(16, dtype=np.float32)
+    for s in catalog.SIGNALS:
+        type_slot[s.kernel_type] = s.slot
+        scale32[s.slot] = np.float32(s.decode_scale)
+    st = ev["signal_type"].astype(np.int64)
+    slot = type_slot[st]
+    ok = slot != NO_SLOT
+    val = ev["value"].astype(np.float64).astype(np.float32)
+    sc = scale32[np.where(ok, slot, 0)].astype(np.float64)
+    val = np.where(ok, (ev["value"].astype(np.float64) * sc).astype(np.float32), val)
+    warn = np.array([s.warn for s in catalog.SIGNALS], dtype=np.float32)
+    err = np.array([s.error for s in catalog.SIGNALS], dtype=np.float32)
+    sl = np.where(ok, slot, 0)
+    status = np.where(val >= err[sl], 2, np.where(val >= warn[sl], 1, 0)).astype(np.uint8)
+    status = np.where(ok, status, 0).astype(np.uint8)
+    conn = ev["conn_h"].copy()
+    derived = records.conn_hash_np(ev["src_port"], ev["dst_port"], ev["dst_ip"])
+    conn = np.where(conn == 0, derived, conn)
+    svcnode = (ev["svc_id"].astype(np.uint32) << np.uint32(16)) | ev["node_id"].astype(np.uint32)
+    return Decoded(ev["ts_ns"].astype(np.int64), val, slot, status, ev["pod_id"].astype(np.uint32),
+                   ev["pid"].astype(np.uint32), svcnode, ev["trace_h"].astype(np.uint64), conn.astype(np.uint64))
+
+
+def histograms(d: Decoded) -> np.ndarray:
+    edges = np.array([list(s.buckets) for s in catalog.SIGNALS], dtype=np.float32)
+    h = np.zeros((16, 16), dtype=np.int64)
+    for s in range(16):
+        v = d.val[d.slot == s]
+        b = (v[:, None] > edges[s][None, :15]).sum(axis=1)
+        np.add.at(h[s], b, 1)
+    return h
+
+
+@dataclass
+class JoinResult:
+    top3: np.ndarray        # uint64 [S,3]
+    cnt: np.ndarray         # [S]
+    attrs: np.ndarray       # float32 [S,16]
+    conf: np.ndarray        # float32 [S]
+    gsum: np.ndarray        # float64 [G,16]
+    gcnt: np.ndarray        # int64 [G,16]
+    feat: np.ndarray        # float32 [G,16]
+    debug: Dict[str, int]
+
+
+def join(d: Decoded, spans: np.ndarray, n_groups: int, window_ms: float = 2000.0, threshold: float = 0.7,
+         fanout: int = 3, group_mode: int = 1) -> JoinResult:
+    outer = int(round(window_ms * MS))
+    if outer <= 0:
+        outer = 2000 * MS
+    win = [outer, min(outer, 100 * MS), min(outer, 250 * MS), min(outer, 500 * MS)]
+    thr = np.float32(threshold)
+    confs = np.array(TIER_CONF, dtype=np.float32)
+    S = spans.shape[0]
+    N = d.ts.shape[0]
+    supported = d.slot != NO_SLOT
+    n_sup = int(supported.sum())
+    idx_all = np.arange(N, dtype=np.uint64)
+    top3 = np.full((S, 3), np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+    cnt = np.zeros(S, dtype=np.int64)
+    attrs = np.full((S, 16), np.nan, dtype=np.float32)
+    conf = np.zeros(S, dtype=np.float32)
+    gsum = np.zeros((n_groups, 16), dtype=np.float64)
+    gcnt = np.zeros((n_groups, 16), dtype=np.int64)
+    matched_total = low_total = dropped_total = 0
+    sp_svcnode = (spans["svc_id"].astype(np.uint32) << np.uint32(16)) | spans["node_id"].astype(np.uint32)
+    for s in range(S):
+        t = int(spans["ts_ns"][s])
+        if t == 0:
+            continue
+        valid = supported & (d.ts != 0)
+        dt = np.abs(d.ts - t)
+        outer_ok = valid & (dt <= outer)
+        tr = np.uint64(spans["trace_h"][s])
+        pod = np.uint32(spans["pod_id"][s])
+        pid = np.uint32(spans["pid"][s])
+        cn = np.uint64(spans["conn_h"][s])
+        sn = sp_svcnode[s]
+        t1 = outer_ok & (tr != 0) & (d.trace == tr)
+        t2 = outer_ok & (pod != 0) & (d.pod == pod) & (pid != 0) & (d.pid == pid) & (dt <= win[1])
+        t3 = outer_ok & (pod != 0) & (d.pod == pod) & (cn != 0) & (d.conn == cn) & (dt <= win[2])
+        t4 = outer_ok & ((sn >> np.uint32(16)) != 0) & ((sn & np.uint32(0xFFFF)) != 0) & (d.svcnode == sn) & (dt <= win[3])
+        tier = np.where(t1, 1, np.where(t2, 2, np.where(t3, 3, np.where(t4, 4, 0))))
+        m = tier > 0
+        c = np.zeros(N, dtype=np.float32)
+        c[m] = confs[tier[m] - 1]
+        cand = m & (c >= thr)
+        low = m & (c < thr)
+        matched_total += int(m.sum())
+        low_total += int(low.sum())
+        ci = np.nonzero(cand)[0]
+        cnt[s] = ci.size
+        if ci.size:
+            keys = ((tier[ci].astype(np.uint64) - np.uint64(1)) << np.uint64(62)) | \
+                   (dt[ci].astype(np.uint64) << np.uint64(SIG_BITS)) | idx_all[ci]
+            keys.sort()
+            k3 = keys[:3]
+            top3[s, :k3.size] = k3
+            keep = keys[:min(fanout, 3)]
+            mc = np.float32(0)
+            for key in keep:
+                g = int(key & np.uint64((1 << SIG_BITS) - 1))
+                sl = int(d.slot[g])
+                v = d.val[g]
+                if np.isnan(attrs[s, sl]) or v > attrs[s, sl]:
+                    attrs[s, sl] = v
+                mc = max(mc, confs[int(key >> np.uint64(62))])
+            conf[s] = mc
+            dropped_total += max(0, ci.size - fanout)
+            grp = int(spans["group_id"][s])
+            if group_mode == 1 and grp < n_groups:
+                np.add.at(gsum[grp], d.slot[ci].astype(np.int64), d.val[ci].astype(np.float64))
+                np.add.at(gcnt[grp], d.slot[ci].astype(np.int64), 1)
+        grp = int(spans["group_id"][s])
+        if group_mode == 0 and grp < n_groups:
+            p = ~np.isnan(attrs[s])
+            gsum[grp][p] += attrs[s][p]
+            gcnt[grp][p] += 1
+    with np.errstate(invalid="ignore", divide="ignore"):
+        feat = np.where(gcnt > 0, gsum / np.maximum(gcnt, 1), np.nan).astype(np.float32)
+    n_uns = N - n_sup
+    debug = {
+        "candidates": int(cnt.sum()), "low_confidence": low_total, "fanout_dropped": dropped_total,
+        "unmatched": S * n_sup - matched_total, "unsupported_type": S * n_uns,
+        "spans_enriched": int((conf > 0).sum()),
+    }
+    return JoinResult(top3, cnt, attrs, conf, gsum, gcnt, feat, debug)

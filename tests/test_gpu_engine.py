@@ -1,0 +1,122 @@
+"""GPU engine vs the CPU oracle on small replay windows (exact keys/tiers/counts)."""
+
+import numpy as np
+import pytest
+
+from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, SufficientStats
+from llm_slo_ebpf_toolkit_amd.pipeline import oracle
+from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+
+pytestmark = pytest.mark.gpu
+
+
+def small_window(seed=1, n=4096, s=256, services=8, scenario="full"):
+    cfg = ReplayConfig(scenario=scenario, n_nodes=2, pods_per_node=8, n_services=services, events_per_window=n,
+                       spans_per_window=s, seed=seed)
+    return ReplayGenerator(cfg).next_window()
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from llm_slo_ebpf_toolkit_amd.ops.engine import GpuEngine
+
+    return GpuEngine(sig_cap=8192, span_cap=512, group_cap=64)
+
+
+def test_extension_is_native(engine):
+    import llm_slo_ebpf_toolkit_amd.ops as ops
+
+    assert ops.available()
+    assert engine.mod.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("group_mode", [1, 0])
+def test_decode_join_matches_oracle(engine, group_mode):
+    win = small_window()
+    engine.set_join_params(2000.0, 0.7, 3, group_mode)
+    engine.set_model(NaiveBayes.ref())
+    out = engine.process(win.events, win.spans, win.n_groups, win.group_labels)
+    e = engine.eng
+    d = oracle.decode_events(win.events)
+    N, S = win.n_events, win.n_spans
+    np.testing.assert_array_equal(e.g_slot[:N].cpu().numpy(), d.slot)
+    np.testing.assert_array_equal(e.g_val[:N].cpu().numpy(), d.val)
+    np.testing.assert_array_equal(out.hist, oracle.histograms(d))
+    ref = oracle.join(d, win.spans, win.n_groups, group_mode=group_mode)
+    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
+    np.testing.assert_array_equal(top3, ref.top3)
+    np.testing.assert_array_equal(e.cnt[:S].cpu().numpy(), ref.cnt)
+    np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
+    np.testing.assert_array_equal(e.conf[:S].cpu().numpy(), ref.conf)
+    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
+        assert out.debug[k] == ref.debug[k], k
+    np.testing.assert_allclose(out.feat, ref.feat, rtol=2e-5, equal_nan=True)
+
+
+def test_low_threshold_enumerates_service_node_tier(engine):
+    win = small_window(seed=3, n=2048, s=128)
+    engine.set_join_params(2000.0, 0.6, 3, 1)
+    engine.set_model(NaiveBayes.ref())
+    out = engine.process(win.events, win.spans, win.n_groups, win.group_labels)
+    d = oracle.decode_events(win.events)
+    ref = oracle.join(d, win.spans, win.n_groups, threshold=0.6)
+    S = win.n_spans
+    top3 = engine.eng.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
+    np.testing.assert_array_equal(top3, ref.top3)
+    for k in ("candidates", "low_confidence", "unmatched"):
+        assert out.debug[k] == ref.debug[k], k
+    engine.set_join_params(2000.0, 0.7, 3, 1)
+
+
+def test_posterior_matches_cpu_model(engine):
+    win = small_window(seed=5)
+    for model in (NaiveBayes.ref(),):
+        engine.set_model(model)
+        out = engine.process(win.events, win.spans, win.n_groups, win.group_labels)
+        post_cpu = model.posteriors(out.feat.astype(np.float64))
+        np.testing.assert_allclose(out.post[:, :10], post_cpu, rtol=1e-9, atol=1e-12)
+        np.testing.assert_array_equal(out.pred, np.argmax(model.logits(out.feat.astype(np.float64)), axis=1))
+        bits = model.evidence_bits(out.feat.astype(np.float64))
+        np.testing.assert_array_equal(out.evbits[:, :10], bits)
+        conf = np.zeros((16, 16), dtype=np.int64)
+        np.add.at(conf, (win.group_labels, out.pred), 1)
+        np.testing.assert_array_equal(out.confusion, conf)
+
+
+def test_stats_matches_cpu(engine):
+    win = small_window(seed=7)
+    model = NaiveBayes.ref()
+    engine.set_model(model)
+    engine.stage(win.events, win.spans, win.n_groups, win.group_labels)
+    engine.upload()
+    engine.run(True, learn=True)
+    out = engine.outputs()
+    st = SufficientStats()
+    st.add(out.feat.astype(np.float64), win.group_labels)
+    gpu = engine.eng.stats.cpu().numpy()
+    cnt = engine.eng.stats_count.cpu().numpy()
+    np.testing.assert_allclose(cnt[:10], st.count, rtol=1e-12)
+    np.testing.assert_allclose(gpu[:16, :10], st.elevated_sum, rtol=1e-12)
+    np.testing.assert_allclose(gpu[16:, :10], st.x_sum, rtol=1e-9)
+    np.testing.assert_allclose(gpu[16:, 16:], st.xx, rtol=1e-9)
+
+
+def test_ref_record_decode(engine):
+    import torch
+    from llm_slo_ebpf_toolkit_amd.collector import records
+
+    recs = [records.encode_ref_record(7, 8, 1_000_000_000 + i, t, v, 4000 if t in (1, 4) else 0, 53 if t == 1 else 0)
+            for i, (t, v) in enumerate([(1, 220_000_000), (2, 3), (6, 1500), (9, 51_000_000), (42, 1)])]
+    buf = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    dev = torch.zeros(engine.sig_cap * 40, dtype=torch.uint8, device="cuda")
+    dev[: buf.size] = torch.from_numpy(buf.copy()).cuda()
+    engine.eng.counts.copy_(torch.tensor([5, 0, 0, 0], dtype=torch.int32))
+    engine.eng.reset_window()
+    engine.eng.decode_ref(dev, 3, (1 << 16) | 2, 0)
+    torch.cuda.synchronize()
+    val = engine.eng.g_val[:5].cpu().numpy()
+    slot = engine.eng.g_slot[:5].cpu().numpy()
+    # REF convertValue (ringbuf.go:229-238): unknown types fall into the ns -> ms default
+    np.testing.assert_allclose(val, [220.0, 3.0, 1500.0, 51.0, 1e-6], rtol=1e-6)
+    assert list(slot) == [0, 1, 7, 11, 255]
+    assert int(engine.eng.misc[0].item()) == 1

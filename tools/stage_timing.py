@@ -1,0 +1,74 @@
+"""Per-stage GPU timing of one replay window (diagnostic; not the headline bench)."""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes  # noqa: E402
+from llm_slo_ebpf_toolkit_amd.ops.engine import GpuEngine  # noqa: E402
+from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--events", type=int, default=1 << 20)
+    ap.add_argument("--spans", type=int, default=16384)
+    ap.add_argument("--services", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    t = time.time()
+    cfg = ReplayConfig(events_per_window=a.events, spans_per_window=a.spans, n_services=a.services)
+    win = ReplayGenerator(cfg).next_window()
+    print(f"gen {time.time() - t:.2f}s", flush=True)
+    eng = GpuEngine(a.events, a.spans, a.services)
+    eng.set_model(NaiveBayes.ref())
+    eng.stage(win.events, win.spans, win.n_groups, win.group_labels)
+    eng.upload()
+    torch.cuda.synchronize()
+    e = eng.eng
+    stages = {
+        "reset": lambda: e.reset_window(),
+        "decode": lambda: e.decode(eng.ev_dev),
+        "join": lambda: e.join(eng.sp_dev, win.n_groups, None),
+        "posterior": lambda: e.posterior(True),
+        "stats": lambda: e.accumulate_stats(None),
+        "pack": lambda: e.pack(),
+    }
+    times = {k: [] for k in stages}
+    h2d = []
+    for it in range(a.iters + 3):
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record()
+        eng.upload()
+        s1.record()
+        torch.cuda.synchronize()
+        if it >= 3:
+            h2d.append(s0.elapsed_time(s1))
+        for k, fn in stages.items():
+            a0 = torch.cuda.Event(enable_timing=True)
+            a1 = torch.cuda.Event(enable_timing=True)
+            a0.record()
+            fn()
+            a1.record()
+            torch.cuda.synchronize()
+            if it >= 3:
+                times[k].append(a0.elapsed_time(a1))
+    res = {k: float(np.median(v)) for k, v in times.items()}
+    res["h2d"] = float(np.median(h2d))
+    tot = sum(v for k, v in res.items() if k != "h2d")
+    res["total_ms"] = tot
+    res["events_per_s_compute"] = a.events / (tot / 1e3)
+    res["debug"] = eng.outputs().debug
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
