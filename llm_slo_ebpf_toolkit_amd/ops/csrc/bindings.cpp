@@ -165,6 +165,28 @@ class Engine {
     model.copy_(host, /*non_blocking=*/false);
   }
 
+  // Retarget the per-window I/O buffers (counts int32[4], labels int32[group_cap],
+  // packet f64[PACKET_LEN]) so the caller can double-buffer them: the H2D of window i+1
+  // and the RCCL all-reduce of window i's packet then never race window i's kernels.
+  void bind_io(torch::Tensor c, torch::Tensor l, torch::Tensor p) {
+    check_cuda(c, "counts");
+    check_cuda(l, "labels");
+    check_cuda(p, "packet");
+    if (c.scalar_type() != torch::kInt32 || c.numel() < 4) throw std::invalid_argument("counts: int32[4]");
+    if (l.scalar_type() != torch::kInt32 || l.numel() < group_cap_) throw std::invalid_argument("labels: int32[G]");
+    if (p.scalar_type() != torch::kFloat64 || p.numel() < kPacketLen) throw std::invalid_argument("packet: f64[L]");
+    counts = c;
+    labels = l;
+    packet = p;
+  }
+
+  // Stream-ordered model update from a (pinned) host byte image of PosteriorModel.
+  void set_model_bytes(torch::Tensor host_bytes) {
+    if (host_bytes.scalar_type() != torch::kUInt8 || host_bytes.numel() != (int64_t)sizeof(PosteriorModel))
+      throw std::invalid_argument("model image must be uint8[POSTERIOR_MODEL_BYTES]");
+    model.copy_(host_bytes, /*non_blocking=*/true);
+  }
+
   // ---- stages --------------------------------------------------------------------------
   void reset_window() {
     hipStream_t st = cur_stream();
@@ -335,6 +357,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_join_params", &Engine::set_join_params, py::arg("window_ms") = 2000.0,
            py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1)
       .def("set_model", &Engine::set_model)
+      .def("set_model_bytes", &Engine::set_model_bytes)
+      .def("bind_io", &Engine::bind_io)
       .def("reset_window", &Engine::reset_window)
       .def("decode", &Engine::decode)
       .def("decode_ref", &Engine::decode_ref)

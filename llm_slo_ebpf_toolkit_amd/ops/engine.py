@@ -41,6 +41,28 @@ def model_arrays(model: LinearPosteriorModel):
             t(model.thresholds, np.float32), t(dom_mask, np.int64), table_mask, mode)
 
 
+MODEL_DTYPE = np.dtype([
+    ("w", "<f8", (16, 16)), ("bias", "<f8", (16,)), ("mean", "<f8", (16,)), ("nominal", "<f8", (16,)),
+    ("thr", "<f4", (16,)), ("dom_mask", "<u4", (16,)), ("table_mask", "<u4"), ("mode", "<i4"),
+])
+assert MODEL_DTYPE.itemsize == 2568  # == sizeof(mislo::PosteriorModel)
+
+
+def model_bytes(model: LinearPosteriorModel) -> np.ndarray:
+    """Byte image of ``mislo::PosteriorModel`` (ops/csrc/mislo_launch.h) for stream-ordered upload."""
+    w, bias, mean, nominal, thr, dom_mask, table_mask, mode = model_arrays(model)
+    rec = np.zeros(1, dtype=MODEL_DTYPE)
+    rec["w"][0] = w.numpy()
+    rec["bias"][0] = bias.numpy()
+    rec["mean"][0] = mean.numpy()
+    rec["nominal"][0] = nominal.numpy()
+    rec["thr"][0] = thr.numpy()
+    rec["dom_mask"][0] = dom_mask.numpy().astype(np.uint32)
+    rec["table_mask"][0] = table_mask
+    rec["mode"][0] = mode
+    return rec.view(np.uint8)
+
+
 def decode_debug(dbg: np.ndarray, misc: np.ndarray, n_spans: int, n_events: int) -> Dict[str, int]:
     """Kernel pair counters -> REF DebugStats (correlator.go:20-25) + extras."""
     cand, low_raw, overlap, dropped, enriched = (int(x) for x in dbg[:5])

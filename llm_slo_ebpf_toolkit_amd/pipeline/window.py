@@ -1,0 +1,208 @@
+"""Per-GPU window pipeline: copy stream || compute stream || RCCL side stream.
+
+One process drives one MI355X. For window i (double-buffered device I/O, b = i % 2):
+
+    copy stream    : H2D records(i) -> ev[b], sp[b], counts[b], labels[b]      (PCIe DMA)
+    compute stream : wait H2D(i); decode -> partition -> LDS join -> finalize ->
+                     MFMA posterior + confusion -> MFMA sufficient stats -> pack(packet[b])
+    comm stream    : wait compute(i); all_reduce(packet[b]) over RCCL/xGMI;
+                     totals += packet[b]; packet_host[b] <- packet[b] (async D2H)
+
+so the H2D of window i+1 and the node-wide all-reduce of window i run underneath the
+kernels of window i+1. The host then folds window i-1's all-reduced statistics into the
+online model (learned Bayes from random-init priors, or LDA) and uploads it with a
+stream-ordered copy, so window i+1 is scored by a model fitted on windows <= i-1
+(prequential, never on its own labels). Every rank refits from the same all-reduced
+totals, so the model stays identical across the node without a broadcast.
+
+The packet (see ops/csrc/bindings.cpp) packs signal histograms, status counters, debug
+pair counters, the confusion matrix and the 32x32 f64 sufficient statistics into one
+12.9 KB buffer: a single latency-bound collective per window instead of five.
+"""
+
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..models.bayes import LDA, N_DOMAINS, NaiveBayes, SufficientStats
+from ..models.metrics import macro_f1_from_confusion
+from ..ops.engine import GpuEngine, decode_debug, model_bytes
+from ..signals import catalog
+
+PACKET_LAYOUT = (256, 48, 2, 8, 256, 1024, 16)  # hist, status, misc, dbg, confusion, stats, count
+
+
+def unpack_packet(p: np.ndarray) -> Dict[str, np.ndarray]:
+    o = 0
+    out = {}
+    for name, n in zip(("hist", "status", "misc", "dbg", "confusion", "stats", "count"), PACKET_LAYOUT):
+        out[name] = p[o:o + n]
+        o += n
+    out["hist"] = out["hist"].reshape(16, 16)
+    out["status"] = out["status"].reshape(16, 3)
+    out["confusion"] = out["confusion"].reshape(16, 16)
+    out["stats"] = out["stats"].reshape(32, 32)
+    return out
+
+
+def stats_from_packet(p: Dict[str, np.ndarray]) -> SufficientStats:
+    st = p["stats"]
+    D = N_DOMAINS
+    return SufficientStats(count=p["count"][:D].copy(), elevated_sum=st[:16, :D].copy(),
+                           x_sum=st[16:, :D].copy(), xx=st[16:, 16:].copy())
+
+
+@dataclass
+class StagedWindow:
+    """A window's records in pinned host memory, ready for DMA."""
+    ev: "object"        # torch uint8 pinned [>= n_events*64]
+    sp: "object"        # torch uint8 pinned [>= n_spans*64]
+    counts: "object"    # torch int32 pinned [4]
+    labels: "object"    # torch int32 pinned [group_cap]
+    n_events: int
+    n_spans: int
+    n_groups: int
+    group_domains: List[List[str]] = field(default_factory=list)
+
+
+def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
+                 group_cap: int, group_domains=None) -> StagedWindow:
+    ev = torch.from_numpy(events.view(np.uint8).reshape(-1).copy()).pin_memory()
+    sp = torch.from_numpy(spans.view(np.uint8).reshape(-1).copy()).pin_memory()
+    counts = torch.tensor([events.shape[0], spans.shape[0], n_groups, 0], dtype=torch.int32).pin_memory()
+    lab = np.full(group_cap, -1, dtype=np.int32)
+    if labels is not None:
+        lab[: len(labels)] = labels
+    labels_t = torch.from_numpy(lab).pin_memory()
+    return StagedWindow(ev, sp, counts, labels_t, int(events.shape[0]), int(spans.shape[0]), n_groups,
+                        list(group_domains or []))
+
+
+class WindowPipeline:
+    def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, process_group=None,
+                 model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
+                 fanout: int = 3, group_mode: int = 1, learn: bool = True):
+        import torch
+
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.pg = process_group
+        self.model_name = model
+        self.seed = seed
+        self.learn = learn
+        self.engine = GpuEngine(sig_cap, span_cap, group_cap, device, window_ms, threshold, fanout, group_mode)
+        self.eng = self.engine.eng
+        L = int(self.engine.mod.PACKET_LEN)
+        self.packet_len = L
+        with torch.cuda.device(self.dev):
+            z8 = lambda n: torch.zeros(n, dtype=torch.uint8, device=self.dev)  # noqa: E731
+            self.ev_dev = [z8(sig_cap * 64), z8(sig_cap * 64)]
+            self.sp_dev = [z8(span_cap * 64), z8(span_cap * 64)]
+            self.counts_dev = [torch.zeros(4, dtype=torch.int32, device=self.dev) for _ in range(2)]
+            self.labels_dev = [torch.full((group_cap,), -1, dtype=torch.int32, device=self.dev) for _ in range(2)]
+            self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(2)]
+            self.totals = torch.zeros(L, dtype=torch.float64, device=self.dev)
+            self.packet_host = [torch.zeros(L, dtype=torch.float64).pin_memory() for _ in range(2)]
+            self.model_host = [torch.zeros(2568, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            self.copy_stream = torch.cuda.Stream(self.dev)
+            self.comm_stream = torch.cuda.Stream(self.dev)
+            self.compute_stream = torch.cuda.Stream(self.dev)
+            ev = lambda: torch.cuda.Event()  # noqa: E731
+            self.h2d_done = [ev(), ev()]
+            self.compute_done = [ev(), ev()]
+            self.comm_done = [ev(), ev()]
+        self.i = 0
+        self.cum_stats = SufficientStats()
+        self.windows_folded = 0
+        self.model = self._initial_model()
+        self._upload_model(self.model)
+        self.last_refit_s = 0.0
+
+    # ---------------------------------------------------------------------------------
+    def _initial_model(self):
+        if self.model_name == "bayes":
+            return NaiveBayes.ref()
+        if self.model_name == "lda":
+            return NaiveBayes.learned(SufficientStats(), seed=self.seed)  # until stats exist
+        return NaiveBayes.learned(SufficientStats(), seed=self.seed)
+
+    def _upload_model(self, model) -> None:
+        torch = self.torch
+        slot = self.i % 2
+        host = self.model_host[slot]
+        host.numpy()[:] = model_bytes(model)
+        with torch.cuda.stream(self.compute_stream):
+            self.eng.set_model_bytes(host)
+
+    def refit(self, stats: SufficientStats) -> None:
+        t = time.perf_counter()
+        if self.model_name == "lda" and stats.count.sum() > 32:
+            self.model = LDA.fit(stats)
+        elif self.model_name in ("bayes_learned", "lda"):
+            self.model = NaiveBayes.learned(stats, seed=self.seed)
+        self._upload_model(self.model)
+        self.last_refit_s = time.perf_counter() - t
+
+    # ---------------------------------------------------------------------------------
+    def submit(self, w: StagedWindow, with_labels: bool = True) -> None:
+        torch = self.torch
+        b = self.i % 2
+        cs, ks, ms = self.copy_stream, self.compute_stream, self.comm_stream
+        # H2D into buffer b once window i-2 (the last user of b) finished computing
+        cs.wait_event(self.compute_done[b])
+        with torch.cuda.stream(cs):
+            self.ev_dev[b][: w.n_events * 64].copy_(w.ev[: w.n_events * 64], non_blocking=True)
+            self.sp_dev[b][: w.n_spans * 64].copy_(w.sp[: w.n_spans * 64], non_blocking=True)
+            self.counts_dev[b].copy_(w.counts, non_blocking=True)
+            self.labels_dev[b].copy_(w.labels, non_blocking=True)
+            self.h2d_done[b].record(cs)
+        ks.wait_event(self.h2d_done[b])
+        ks.wait_event(self.comm_done[b])  # packet[b] no longer being reduced / read
+        with torch.cuda.stream(ks):
+            self.eng.bind_io(self.counts_dev[b], self.labels_dev[b], self.packet_dev[b])
+            self.eng.run_window(self.ev_dev[b], self.sp_dev[b], w.n_groups, with_labels,
+                                self.learn and with_labels)
+            self.compute_done[b].record(ks)
+        ms.wait_event(self.compute_done[b])
+        with torch.cuda.stream(ms):
+            if self.pg is not None:
+                torch.distributed.all_reduce(self.packet_dev[b], group=self.pg)
+            self.totals.add_(self.packet_dev[b])
+            self.packet_host[b].copy_(self.packet_dev[b], non_blocking=True)
+            self.comm_done[b].record(ms)
+        self.i += 1
+        # fold window i-2 (this call's predecessor's predecessor is certainly far along;
+        # folding i-1 would stall the host on the window just queued)
+        if self.i >= 2 and self.learn:
+            pb = (self.i - 2) % 2
+            self.comm_done[pb].synchronize()
+            pk = unpack_packet(self.packet_host[pb].numpy())
+            self.cum_stats = self.cum_stats.merge(stats_from_packet(pk))
+            self.windows_folded += 1
+            self.refit(self.cum_stats)
+
+    def drain(self) -> None:
+        self.torch.cuda.synchronize(self.dev)
+
+    def reset_totals(self) -> None:
+        self.drain()
+        self.totals.zero_()
+
+    def summary(self) -> Dict[str, object]:
+        self.drain()
+        p = unpack_packet(self.totals.cpu().numpy())
+        conf = p["confusion"][:N_DOMAINS, :N_DOMAINS].astype(np.int64)
+        return {
+            "confusion": conf,
+            "macro_f1": macro_f1_from_confusion(conf),
+            "accuracy": float(np.trace(conf) / conf.sum()) if conf.sum() else 0.0,
+            "hist": p["hist"].astype(np.int64),
+            "status": p["status"].astype(np.int64),
+            "dbg": p["dbg"].astype(np.int64),
+            "misc": p["misc"].astype(np.int64),
+            "stats": stats_from_packet(p),
+        }
