@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--paced-windows", type=int, default=3,
                     help="windows replayed at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--wire", type=int, default=32, choices=(32, 64),
+                    help="event record bytes on PCIe: 32 = compact (interned ids), 64 = full")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -86,8 +88,10 @@ def main() -> int:
                        n_services=a.services, seed=a.seed, shard=rank)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
-    staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, a.services, w.group_domains)
-              for w in wins]
+    from llm_slo_ebpf_toolkit_amd.collector.records import ConnInterner
+    interner = ConnInterner()
+    staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, a.services, w.group_domains,
+                           wire=a.wire, interner=interner) for w in wins]
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed)
@@ -196,6 +200,7 @@ def main() -> int:
             "spans_per_window_per_gpu": a.spans,
             "incidents_per_window_per_gpu": a.services,
             "scenario": a.scenario,
+            "wire_bytes_per_event": a.wire,
         },
         "macro_f1": round(summ["macro_f1"], 4),
         "vs_baseline_macro_f1": round(summ["macro_f1"] / BASELINE_MACRO_F1, 4),

@@ -46,6 +46,16 @@ EVENT = np.dtype([
 ])
 assert EVENT.itemsize == 64
 
+EVENT32 = np.dtype([
+    ("ts_ns", "<i8"),        # 0
+    ("trace_h", "<u8"),      # 8
+    ("value_milli", "<u4"),  # 16 value in 1/1000 of the signal's output unit
+    ("pid", "<u4"),          # 20
+    ("pod_id", "<u4"),       # 24 interned pod id (svc/node via the device pod table)
+    ("type_conn", "<u4"),    # 28 bits 0-7 signal_type, bits 8-31 interned connection id
+])
+assert EVENT32.itemsize == 32
+
 SPAN = np.dtype([
     ("ts_ns", "<i8"),        # 0
     ("trace_h", "<u8"),      # 8
@@ -168,6 +178,71 @@ def conn_hash_np(src_port: np.ndarray, dst_port: np.ndarray, dst_ip: np.ndarray)
     h = splitmix64_np(packed)
     h = np.where(h == 0, np.uint64(1), h)
     return np.where((sp == 0) & (dp == 0), np.uint64(0), h)
+
+
+def pod_table(events: np.ndarray, spans: np.ndarray = None) -> np.ndarray:
+    """pod_id -> (svc << 16 | node) lookup table (int32) from records that carry both."""
+    pods = [events["pod_id"]]
+    sn = [(events["svc_id"].astype(np.uint32) << np.uint32(16)) | events["node_id"].astype(np.uint32)]
+    if spans is not None and len(spans):
+        pods.append(spans["pod_id"])
+        sn.append((spans["svc_id"].astype(np.uint32) << np.uint32(16)) | spans["node_id"].astype(np.uint32))
+    p = np.concatenate(pods).astype(np.int64)
+    v = np.concatenate(sn)
+    table = np.zeros(int(p.max()) + 1 if p.size else 1, dtype=np.uint32)
+    table[p] = v
+    return table.view(np.int32)
+
+
+class ConnInterner:
+    """64-bit connection hash -> dense 24-bit connection id (0 = no connection); the
+    user-space side of the BPF probes' 5-tuple -> id map."""
+
+    def __init__(self):
+        self._ids = {}
+
+    def ids(self, conn_h: np.ndarray) -> np.ndarray:
+        uniq, inv = np.unique(conn_h, return_inverse=True)
+        out = np.zeros(uniq.shape[0], dtype=np.uint32)
+        for j, h in enumerate(uniq.tolist()):
+            if h == 0:
+                continue
+            i = self._ids.get(h)
+            if i is None:
+                i = len(self._ids) + 1
+                if i >= (1 << 24):
+                    raise OverflowError("connection id space exhausted")
+                self._ids[h] = i
+            out[j] = i
+        return out[inv]
+
+
+def to_compact(events: np.ndarray, interner: "ConnInterner") -> np.ndarray:
+    """EVENT (64 B) -> EVENT32 (32 B): milli-unit fixed point values, interned conn ids."""
+    out = np.zeros(events.shape[0], dtype=EVENT32)
+    out["ts_ns"] = events["ts_ns"]
+    out["trace_h"] = events["trace_h"]
+    scale = np.ones(65536, dtype=np.float64)
+    for s in catalog.SIGNALS:
+        scale[s.kernel_type] = s.decode_scale
+    st = events["signal_type"].astype(np.int64)
+    milli = np.rint(events["value"].astype(np.float64) * scale[st] * 1000.0)
+    out["value_milli"] = np.clip(milli, 0, 0xFFFFFFFF).astype(np.uint32)
+    out["pid"] = events["pid"]
+    out["pod_id"] = events["pod_id"]
+    conn = events["conn_h"].copy()
+    derived = conn_hash_np(events["src_port"], events["dst_port"], events["dst_ip"])
+    conn = np.where(conn == 0, derived, conn)
+    cid = interner.ids(conn)
+    out["type_conn"] = (st.astype(np.uint32) & np.uint32(0xFF)) | (cid << np.uint32(8))
+    return out
+
+
+def compact_spans(spans: np.ndarray, interner: "ConnInterner") -> np.ndarray:
+    """Spans keep the 64-byte layout; their conn key is rewritten to the same interned id."""
+    out = spans.copy()
+    out["conn_h"] = interner.ids(spans["conn_h"]).astype(np.uint64)
+    return out
 
 
 def string_hash64(s: str) -> int:

@@ -67,6 +67,26 @@ __global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsig
   if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
 }
 
+// One launch that zero/poison-fills every per-window accumulator (replaces eleven
+// hipMemsetAsync calls, each ~5 us of fill-kernel + launch overhead on gfx950).
+struct FillSeg {
+  uint32_t* ptr;
+  uint32_t n;      // 32-bit words
+  uint32_t value;
+};
+constexpr int kMaxFill = 12;
+struct FillList {
+  FillSeg seg[kMaxFill];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void k_fill_multi(FillList fl) {
+  for (int q = 0; q < fl.count; ++q) {
+    const FillSeg sg = fl.seg[q];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sg.n; i += gridDim.x * 256) sg.ptr[i] = sg.value;
+  }
+}
+
 }  // namespace
 
 class Engine {
@@ -118,6 +138,7 @@ class Engine {
     confusion = torch::empty({kMaxDomains, kMaxDomains}, i32);
     stats = torch::empty({32, 32}, f64); stats_count = torch::empty({kMaxDomains}, f64);
     packet = torch::empty({kPacketLen}, f64);
+    pod_table = torch::zeros({1}, i32);
     model = torch::zeros({(int64_t)sizeof(PosteriorModel)}, u8);
     join_defaults();
   }
@@ -189,14 +210,13 @@ class Engine {
 
   // ---- stages --------------------------------------------------------------------------
   void reset_window() {
-    hipStream_t st = cur_stream();
-    HIPCHECK(hipMemsetAsync(hist.data_ptr(), 0, hist.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(status_cnt.data_ptr(), 0, status_cnt.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(misc.data_ptr(), 0, misc.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(dbg.data_ptr(), 0, dbg.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(confusion.data_ptr(), 0, confusion.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(stats.data_ptr(), 0, stats.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(stats_count.data_ptr(), 0, stats_count.nbytes(), st));
+    FillList fl{};
+    auto add = [&](const torch::Tensor& t, uint32_t v) {
+      fl.seg[fl.count++] = FillSeg{reinterpret_cast<uint32_t*>(t.data_ptr()), (uint32_t)(t.nbytes() / 4), v};
+    };
+    add(hist, 0); add(status_cnt, 0); add(misc, 0); add(dbg, 0); add(confusion, 0); add(stats, 0);
+    add(stats_count, 0); add(top3, 0xFFFFFFFFu); add(cnt, 0); add(gsum, 0); add(gcnt, 0);
+    hipLaunchKernelGGL(k_fill_multi, dim3(256), dim3(256), 0, cur_stream(), fl);
   }
 
   SignalCols sig_cols() {
@@ -218,6 +238,26 @@ class Engine {
     launch_decode_events(events.data_ptr(), dptr<int>(counts), sig_cap_, sig_cols(), dptr<uint32_t>(hist),
                          dptr<uint32_t>(status_cnt), dptr<uint32_t>(g_part_blk),
                          dptr<unsigned long long>(misc), cur_stream());
+    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
+                     dptr<uint32_t>(g_items), cur_stream());
+  }
+
+  // pod id -> (svc << 16 | node) table for compact records (interned by the agent)
+  void set_pod_table(torch::Tensor table) {
+    check_cuda(table, "pod_table");
+    if (table.scalar_type() != torch::kInt32) throw std::invalid_argument("pod_table must be int32");
+    pod_table = table;
+  }
+
+  // events: device buffer of 32-byte compact records (>= sig_cap * 32 bytes)
+  void decode_compact(torch::Tensor events) {
+    check_cuda(events, "events");
+    if (events.nbytes() < (size_t)sig_cap_ * 32)
+      throw std::invalid_argument("events buffer must hold sig_cap 32-byte records");
+    launch_decode_compact(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(pod_table),
+                          (int)pod_table.numel(), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
+                          dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
     launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
                      dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
                      dptr<uint32_t>(g_items), cur_stream());
@@ -246,10 +286,7 @@ class Engine {
     launch_partition(dptr<uint64_t>(s_hash), dptr<int>(counts) + 1, span_cap_, nblk_span_,
                      dptr<uint32_t>(s_part_blk), dptr<uint32_t>(s_part_off), dptr<uint32_t>(s_part_tot),
                      dptr<uint32_t>(s_part_base), dptr<uint32_t>(s_items), st);
-    HIPCHECK(hipMemsetAsync(top3.data_ptr(), 0xFF, top3.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(cnt.data_ptr(), 0, cnt.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(gsum.data_ptr(), 0, gsum.nbytes(), st));
-    HIPCHECK(hipMemsetAsync(gcnt.data_ptr(), 0, gcnt.nbytes(), st));
+    // top3 / cnt / gsum / gcnt were reset by reset_window()
     launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(),
                  dptr<uint32_t>(g_items), dptr<uint32_t>(g_part_base), sig_cap_, span_cap_, jp_,
                  dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<float>(gsum),
@@ -294,9 +331,11 @@ class Engine {
   }
 
   // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0].
-  void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn) {
+  // wire: 64 = Event records, 32 = compact EventC32 records
+  void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn,
+                  int64_t wire) {
     reset_window();
-    decode(events);
+    if (wire == 32) decode_compact(events); else decode(events);
     join(spans, n_groups, c10::nullopt);
     posterior(with_labels);
     if (learn) accumulate_stats(c10::nullopt);
@@ -315,7 +354,7 @@ class Engine {
   torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
   torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
-  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model;
+  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, pod_table;
 
  private:
   int sig_cap_, span_cap_, group_cap_;
@@ -362,11 +401,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("reset_window", &Engine::reset_window)
       .def("decode", &Engine::decode)
       .def("decode_ref", &Engine::decode_ref)
+      .def("decode_compact", &Engine::decode_compact)
+      .def("set_pod_table", &Engine::set_pod_table)
       .def("join", &Engine::join, py::arg("spans"), py::arg("n_groups"), py::arg("base_attrs") = py::none())
       .def("posterior", &Engine::posterior)
       .def("accumulate_stats", &Engine::accumulate_stats, py::arg("weights") = py::none())
       .def("pack", &Engine::pack)
-      .def("run_window", &Engine::run_window)
+      .def("run_window", &Engine::run_window, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
+           py::arg("with_labels") = true, py::arg("learn") = false, py::arg("wire") = 64)
       .def_property_readonly("sig_cap", &Engine::sig_cap)
       .def_property_readonly("span_cap", &Engine::span_cap)
       .def_property_readonly("group_cap", &Engine::group_cap)
@@ -376,6 +418,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       RO(g_conn) RO(g_hash) RO(g_part_base) RO(g_items) RO(s_ts) RO(s_hash) RO(s_part_base) RO(s_items)
       RO(top3) RO(cnt) RO(attrs) RO(conf) RO(kernel_ms) RO(gsum) RO(gcnt) RO(feat) RO(labels) RO(post)
       RO(pred) RO(gconf) RO(evbits) RO(hist) RO(status_cnt) RO(misc) RO(dbg) RO(confusion) RO(stats)
-      RO(stats_count) RO(packet) RO(model);
+      RO(stats_count) RO(packet) RO(model) RO(pod_table);
 #undef RO
 }

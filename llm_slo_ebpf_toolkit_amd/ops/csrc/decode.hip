@@ -121,6 +121,49 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
   }
 }
 
+// 32-byte compact records: half the PCIe bytes of Event; service|node come from the
+// per-agent pod table (device resident), the connection id is already an exact key.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restrict__ ev,
+                                                       const int* __restrict__ n_ptr, int cap,
+                                                       const uint32_t* __restrict__ pod_svcnode, int n_pods,
+                                                       DecodeOut o) {
+  __shared__ uint32_t s_hist[kSlots * kBuckets];
+  __shared__ uint32_t s_status[kSlots * 3];
+  __shared__ uint32_t s_part[kKeyTypes * kParts];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
+  __syncthreads();
+
+  const int n = min(*n_ptr, cap);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  int unsupported = 0, zero_ts = 0;
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const EventC32 e = ev[i];
+    const int st = (int)(e.type_conn & 0xFFu);
+    const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
+    const float val = (float)((double)e.value_milli * 1e-3);
+    const uint64_t ch = (uint64_t)(e.type_conn >> 8);
+    const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
+    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status, s_part,
+               unsupported, zero_ts);
+  }
+  __syncthreads();
+  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
+  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
+  for (int off = 32; off > 0; off >>= 1) {
+    unsupported += __shfl_xor(unsupported, off);
+    zero_ts += __shfl_xor(zero_ts, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
+    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
+  }
+}
+
 // REF 40-byte records: REF units (count stays count, cpu_steal raw ns, else ns/1e6) and
 // workload identity supplied by the consumer (REF EventMetadata, ringbuf.go:19-26).
 template <int NT>
@@ -212,6 +255,15 @@ void launch_decode_events(const void* ev, const int* n_dev, int cap, const Signa
   constexpr int NT = 256;
   hipLaunchKernelGGL((k_decode_events<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                      (const Event*)ev, n_dev, cap, o);
+}
+
+void launch_decode_compact(const void* ev, const int* n_dev, int cap, const uint32_t* pod_svcnode, int n_pods,
+                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                           unsigned long long* misc, hipStream_t stream) {
+  DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
+  constexpr int NT = 256;
+  hipLaunchKernelGGL((k_decode_compact<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, (const EventC32*)ev, n_dev,
+                     cap, pod_svcnode, n_pods, o);
 }
 
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,

@@ -34,7 +34,7 @@
 namespace mislo {
 
 constexpr int kSigBits = 27;  // top-3 key: [63:62] tier, [61:27] |dt| ns, [26:0] signal idx
-constexpr int kChunk = 1024;  // spans staged in LDS per pass
+constexpr int kChunk = 512;   // spans staged in LDS per pass
 
 // ---------------------------------------------------------------------------------------
 // partition scan + scatter
@@ -46,7 +46,19 @@ __global__ __launch_bounds__(256) void k_part_scan(const uint32_t* __restrict__ 
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= kKeyTypes * kParts) return;
   uint32_t run = 0;
-  for (int b = 0; b < nblk; ++b) {
+  constexpr int U = 8;  // independent loads in flight per thread
+  int b = 0;
+  for (; b + U <= nblk; b += U) {
+    uint32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = part_blk[(size_t)(b + u) * kKeyTypes * kParts + c];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      part_off[(size_t)(b + u) * kKeyTypes * kParts + c] = run;
+      run += v[u];
+    }
+  }
+  for (; b < nblk; ++b) {
     const size_t idx = (size_t)b * kKeyTypes * kParts + c;
     const uint32_t v = part_blk[idx];
     part_off[idx] = run;
@@ -128,11 +140,19 @@ __device__ __forceinline__ void top3_insert(unsigned long long* slot3, unsigned 
 
 __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
 
-// LDS budget per workgroup: kChunk x (hash 8 + ts 8 + idx 4 + top3 24 + count 4) B
-// + kLdsGroups x 16 x 8 B of incident accumulators = 48 KiB + 8 KiB at kChunk 1024,
-// i.e. two workgroups per CU. All per-pair updates (top-3 cascade, candidate count,
-// incident sums) hit LDS; global atomics are issued once per (span, chunk) on flush.
+// Work decomposition: grid = (1024 partitions, 4 key types, kSplit signal slices). Keys of
+// the pod/service tiers are few and skewed (one serving pid per pod, one (svc, node) per
+// pod), so most partitions are empty and a handful carry thousands of signals; splitting
+// each partition's signal list over kSplit workgroups keeps ~8x more waves in flight for
+// this latency-bound walk. Each workgroup re-stages its (small) span partition.
+//
+// LDS budget per workgroup at kChunk 512: sorted keys (hash 8 + ts 8 + idx 4), the span
+// fields the tier tests need (pod 4, pid 4, conn 8, trace 8, svc|node 4, group 4), the
+// per-span top-3 (24) and candidate count (4) = 80 B x 512 = 40 KiB, plus 8 KiB of
+// incident accumulators -> three workgroups per CU. Every per-pair update is an LDS
+// atomic; global atomics happen once per (span, workgroup) on flush.
 constexpr int kLdsGroups = 64;
+constexpr int kSplit = 8;
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
@@ -145,6 +165,12 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
   __shared__ uint64_t s_h[kChunk];
   __shared__ int64_t s_t[kChunk];
   __shared__ uint32_t s_i[kChunk];
+  __shared__ uint64_t s_tr[kChunk];
+  __shared__ uint64_t s_cn[kChunk];
+  __shared__ uint32_t s_pod[kChunk];
+  __shared__ uint32_t s_pid[kChunk];
+  __shared__ uint32_t s_sn[kChunk];
+  __shared__ uint32_t s_grp[kChunk];
   __shared__ unsigned long long s_top[kChunk * 3];
   __shared__ uint32_t s_cnt[kChunk];
   __shared__ float s_gsum[kLdsGroups * kSlots];
@@ -153,8 +179,12 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
   const int k = blockIdx.y;
   const int c = k * kParts + blockIdx.x;
   const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
-  const uint32_t sg0 = sig_base[c], sg1 = sig_base[c + 1];
-  if (sp0 == sp1 || sg0 == sg1) return;
+  const uint32_t gb0 = sig_base[c], gb1 = sig_base[c + 1];
+  if (sp0 == sp1 || gb0 == gb1) return;
+  const uint32_t per = (gb1 - gb0 + kSplit - 1) / kSplit;
+  const uint32_t sg0 = gb0 + blockIdx.z * per;
+  const uint32_t sg1 = min(gb1, sg0 + per);
+  if (sg0 >= sg1) return;
 
   const int64_t w = jp.win_ns[k];
   const bool cand_tier = jp.conf[k] >= jp.threshold;
@@ -187,10 +217,6 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         s_t[i] = INT64_MAX;
         s_i[i] = 0xFFFFFFFFu;
       }
-      s_top[3 * i] = kEmpty;
-      s_top[3 * i + 1] = kEmpty;
-      s_top[3 * i + 2] = kEmpty;
-      s_cnt[i] = 0u;
     }
     __syncthreads();
     // bitonic sort of (hash, ts, idx) ascending
@@ -209,6 +235,23 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         }
         __syncthreads();
       }
+    }
+    // gather the tier-test fields in sorted order (only when pairs are enumerated)
+    if (!count_only) {
+      for (int i = threadIdx.x; i < m; i += NT) {
+        const uint32_t s = s_i[i];
+        s_tr[i] = sc.trace_h[s];
+        s_cn[i] = sc.conn_h[s];
+        s_pod[i] = sc.pod[s];
+        s_pid[i] = sc.pid[s];
+        s_sn[i] = sc.svcnode[s];
+        s_grp[i] = sc.group[s];
+        s_top[3 * i] = kEmpty;
+        s_top[3 * i + 1] = kEmpty;
+        s_top[3 * i + 2] = kEmpty;
+        s_cnt[i] = 0u;
+      }
+      __syncthreads();
     }
 
     for (uint32_t q = sg0 + threadIdx.x; q < sg1; q += NT) {
@@ -238,54 +281,71 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       const uint64_t g_tr = gc.trace_h[g], g_cn = gc.conn_h[g];
       const int g_slot = gc.slot[g];
       const float g_val = gc.val[g];
+      // incident sums: a signal's candidate spans share one key (pod / trace / svc+node),
+      // hence one incident group -- accumulate (group, pair count) in registers and add
+      // val x count once per run instead of once per pair (all lanes of a partition hit
+      // the same few LDS words, so per-pair atomics serialise).
+      uint32_t run_grp = 0xFFFFFFFFu, run_n = 0;
       for (int i = lo; i < m && s_h[i] == h && s_t[i] <= thi; ++i) {
-        const uint32_t s = s_i[i];
         const int64_t dt = iabs64(t - s_t[i]);
-        const uint32_t s_pod = sc.pod[s];
-        const uint64_t s_cn = sc.conn_h[s];
-        if (k == 2 && !(s_pod == g_pod && s_cn == g_cn)) continue;  // hash collision guard
+        const uint32_t p_pod = s_pod[i];
+        const uint64_t p_cn = s_cn[i];
+        if (k == 2 && !(p_pod == g_pod && p_cn == g_cn)) continue;  // hash collision guard
         // higher-precedence tiers (REF Match order): skip pairs found at their own tier
-        const uint64_t s_tr = sc.trace_h[s];
-        const bool t0 = s_tr != 0 && s_tr == g_tr;  // |dt| <= outer holds for every pair here
-        if (k >= 1 && t0) continue;
+        const uint64_t p_tr = s_tr[i];
+        if (k >= 1 && p_tr != 0 && p_tr == g_tr) continue;  // |dt| <= outer holds for every pair here
         if (k >= 2) {
-          const uint32_t s_pid = sc.pid[s];
-          const bool t1 = s_pod != 0 && s_pod == g_pod && s_pid != 0 && s_pid == g_pid && dt <= jp.win_ns[1];
-          if (t1) continue;
+          const uint32_t p_pid = s_pid[i];
+          if (p_pod != 0 && p_pod == g_pod && p_pid != 0 && p_pid == g_pid && dt <= jp.win_ns[1]) continue;
         }
-        if (k >= 3) {
-          const bool t2 = s_pod != 0 && s_pod == g_pod && s_cn != 0 && s_cn == g_cn && dt <= jp.win_ns[2];
-          if (t2) continue;
-        }
+        if (k >= 3 && p_pod != 0 && p_pod == g_pod && p_cn != 0 && p_cn == g_cn && dt <= jp.win_ns[2]) continue;
         if (cand_tier) {
           unsigned long long key = ((unsigned long long)k << 62) | ((unsigned long long)dt << kSigBits) |
                                    (unsigned long long)g;
+          // slots only ever decrease, so a key >= the current 3rd best can never enter the
+          // top-3: skip the atomic cascade (most pod+pid pairs are rejected here)
+          if (key < s_top[3 * i + 2]) {
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {  // LDS top-3 cascade (see top3_insert)
-            const unsigned long long old = atomicMin(&s_top[3 * i + j], key);
-            if (old == kEmpty) break;
-            key = old > key ? old : key;
+            for (int j = 0; j < 3; ++j) {  // LDS top-3 cascade (see top3_insert)
+              const unsigned long long old = atomicMin(&s_top[3 * i + j], key);
+              if (old == kEmpty) break;
+              key = old > key ? old : key;
+            }
           }
           atomicAdd(&s_cnt[i], 1u);
           ++n_cand;
           if (do_groups) {
-            const uint32_t grp = sc.group[s];
-            if (grp < (uint32_t)n_groups) {
-              if (grp_lds) {
-                atomicAdd(&s_gsum[grp * kSlots + g_slot], g_val);
-                atomicAdd(&s_gcnt[grp * kSlots + g_slot], 1u);
-              } else {
-                atomicAdd(gsum + (size_t)grp * kSlots + g_slot, g_val);
-                atomicAdd(gcnt + (size_t)grp * kSlots + g_slot, 1u);
+            const uint32_t grp = s_grp[i];
+            if (grp != run_grp) {
+              if (run_n && run_grp < (uint32_t)n_groups) {
+                if (grp_lds) {
+                  atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_val * (float)run_n);
+                  atomicAdd(&s_gcnt[run_grp * kSlots + g_slot], run_n);
+                } else {
+                  atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_val * (float)run_n);
+                  atomicAdd(gcnt + (size_t)run_grp * kSlots + g_slot, run_n);
+                }
               }
+              run_grp = grp;
+              run_n = 0;
             }
+            ++run_n;
           }
         } else {
           ++n_low;
         }
         if (track_overlap) {
-          const uint32_t s_sn = sc.svcnode[s];
-          if ((s_sn >> 16) != 0 && (s_sn & 0xFFFF) != 0 && s_sn == g_sn && dt <= jp.win_ns[3]) ++n_overlap;
+          const uint32_t p_sn = s_sn[i];
+          if ((p_sn >> 16) != 0 && (p_sn & 0xFFFF) != 0 && p_sn == g_sn && dt <= jp.win_ns[3]) ++n_overlap;
+        }
+      }
+      if (run_n && run_grp < (uint32_t)n_groups) {
+        if (grp_lds) {
+          atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_val * (float)run_n);
+          atomicAdd(&s_gcnt[run_grp * kSlots + g_slot], run_n);
+        } else {
+          atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_val * (float)run_n);
+          atomicAdd(gcnt + (size_t)run_grp * kSlots + g_slot, run_n);
         }
       }
     }
@@ -427,7 +487,7 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
                   const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, float* gsum,
                   uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream) {
-  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes), dim3(256), 0, stream, sc, span_items, span_base, gc,
+  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes, kSplit), dim3(256), 0, stream, sc, span_items, span_base, gc,
                      sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg);
 }
 

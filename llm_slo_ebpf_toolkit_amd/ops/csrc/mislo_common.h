@@ -15,7 +15,7 @@ constexpr int kBuckets = 16;        // histogram buckets per slot (15 edges + ov
 constexpr int kKeyTypes = 4;        // trace, pod+pid, pod+conn, svc+node
 constexpr int kPartBits = 10;       // 1024 hash partitions per key type
 constexpr int kParts = 1 << kPartBits;
-constexpr int kPartBlocks = 512;    // max decode/scatter workgroups (per-block partition counts)
+constexpr int kPartBlocks = 256;    // max decode/scatter workgroups (per-block partition counts)
 constexpr int kMaxDomains = 16;     // posterior columns (10 used, padded to the MFMA tile)
 constexpr int kMaxTypes = 128;      // signal_type lookup table size
 constexpr uint64_t kEmpty = ~0ull;  // empty top-3 slot
@@ -32,6 +32,21 @@ struct alignas(64) Event {
   uint64_t conn_h;
 };
 static_assert(sizeof(Event) == 64, "Event must be 64 bytes");
+
+// 32-byte compact wire record (collector/records.py EVENT32): what producers write into
+// the ring when PCIe bytes matter. Workload identity is interned at the source (the BPF
+// probes map cgroup -> pod id and the 5-tuple -> connection id in kernel maps that the
+// agent owns), service/node are looked up on the device from the pod id, and the value
+// is fixed-point in 1/1000 of the signal's output unit (1 us for ms latencies).
+struct alignas(32) EventC32 {
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli;
+  uint32_t pid;
+  uint32_t pod_id;
+  uint32_t type_conn;  // bits 0-7 signal_type, bits 8-31 interned connection id (0 = none)
+};
+static_assert(sizeof(EventC32) == 32, "EventC32 must be 32 bytes");
 
 // REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).
 struct __attribute__((packed)) RefEvent {

@@ -109,6 +109,7 @@ class GpuEngine:
             self.copy_stream = torch.cuda.Stream(self.device)
         self.sig_cap, self.span_cap, self.group_cap = sig_cap, span_cap, group_cap
         self.n_events = self.n_spans = self.n_groups = 0
+        self.wire = 64
         self.graph = None
 
     # ---------------------------------------------------------------------------------
@@ -119,14 +120,23 @@ class GpuEngine:
     def set_join_params(self, window_ms=2000.0, threshold=0.7, fanout=3, group_mode=1):
         self.eng.set_join_params(window_ms, threshold, fanout, group_mode)
 
+    def set_pod_table(self, table: np.ndarray) -> None:
+        """pod id -> (svc<<16|node) table used by 32-byte compact records."""
+        with self.torch.cuda.device(self.device):
+            t = self.torch.from_numpy(np.ascontiguousarray(table, dtype=np.int32)).to(self.device)
+            self.eng.set_pod_table(t)
+            self.torch.cuda.synchronize(self.device)
+
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None):
-        """Copy records into pinned staging (host memcpy, no GPU work)."""
+        """Copy records into pinned staging (host memcpy, no GPU work). ``events`` may be
+        64-byte EVENT or 32-byte EVENT32 records (the latter needs ``set_pod_table``)."""
         n, s = events.shape[0], spans.shape[0]
         if n > self.sig_cap or s > self.span_cap or n_groups > self.group_cap:
             raise ValueError("window exceeds engine capacity")
-        if events.dtype != records.EVENT or spans.dtype != records.SPAN:
-            raise TypeError("events/spans must use the EVENT/SPAN record dtypes")
-        self.ev_host.numpy()[: n * 64] = events.view(np.uint8).reshape(-1)
+        if events.dtype not in (records.EVENT, records.EVENT32) or spans.dtype != records.SPAN:
+            raise TypeError("events/spans must use the EVENT|EVENT32/SPAN record dtypes")
+        self.wire = events.dtype.itemsize
+        self.ev_host.numpy()[: n * self.wire] = events.view(np.uint8).reshape(-1)
         self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)
         c = self.cnt_host.numpy()
         c[:] = (n, s, n_groups, 0)
@@ -141,7 +151,8 @@ class GpuEngine:
         torch = self.torch
         cs = self.copy_stream
         with torch.cuda.stream(cs):
-            self.ev_dev[: self.n_events * 64].copy_(self.ev_host[: self.n_events * 64], non_blocking=True)
+            nb = self.n_events * self.wire
+            self.ev_dev[:nb].copy_(self.ev_host[:nb], non_blocking=True)
             self.sp_dev[: self.n_spans * 64].copy_(self.sp_host[: self.n_spans * 64], non_blocking=True)
             self.eng.counts.copy_(self.cnt_host, non_blocking=True)
             self.eng.labels.copy_(self.lab_host, non_blocking=True)
@@ -149,7 +160,7 @@ class GpuEngine:
 
     def run(self, with_labels: bool = True, learn: bool = False) -> None:
         with self.torch.cuda.device(self.device):
-            self.eng.run_window(self.ev_dev, self.sp_dev, self.n_groups, with_labels, learn)
+            self.eng.run_window(self.ev_dev, self.sp_dev, self.n_groups, with_labels, learn, self.wire)
 
     def process(self, events, spans, n_groups, labels=None, learn=False) -> "WindowOutputs":
         self.stage(events, spans, n_groups, labels)

@@ -62,6 +62,28 @@ def decode_events(ev: np.ndarray) -> Decoded:
                    ev["pid"].astype(np.uint32), svcnode, ev["trace_h"].astype(np.uint64), conn.astype(np.uint64))
 
 
+def decode_compact(ev: np.ndarray, pod_svcnode: np.ndarray) -> Decoded:
+    type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
+    for s in catalog.SIGNALS:
+        if s.kernel_type < 256:
+            type_slot[s.kernel_type] = s.slot
+    tc = ev["type_conn"].astype(np.uint32)
+    st = (tc & np.uint32(0xFF)).astype(np.int64)
+    slot = type_slot[st]
+    val = (ev["value_milli"].astype(np.float64) * 1e-3).astype(np.float32)
+    warn = np.array([s.warn for s in catalog.SIGNALS], dtype=np.float32)
+    err = np.array([s.error for s in catalog.SIGNALS], dtype=np.float32)
+    ok = slot != NO_SLOT
+    sl = np.where(ok, slot, 0)
+    status = np.where(ok, np.where(val >= err[sl], 2, np.where(val >= warn[sl], 1, 0)), 0).astype(np.uint8)
+    pods = ev["pod_id"].astype(np.int64)
+    table = pod_svcnode.view(np.uint32)
+    svcnode = np.where(pods < table.shape[0], table[np.minimum(pods, table.shape[0] - 1)], 0).astype(np.uint32)
+    return Decoded(ev["ts_ns"].astype(np.int64), val, slot, status, ev["pod_id"].astype(np.uint32),
+                   ev["pid"].astype(np.uint32), svcnode, ev["trace_h"].astype(np.uint64),
+                   (tc >> np.uint32(8)).astype(np.uint64))
+
+
 def histograms(d: Decoded) -> np.ndarray:
     edges = np.array([list(s.buckets) for s in catalog.SIGNALS], dtype=np.float32)
     h = np.zeros((16, 16), dtype=np.int64)

@@ -28,6 +28,7 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
+from ..collector import records
 from ..models.bayes import LDA, N_DOMAINS, NaiveBayes, SufficientStats
 from ..models.metrics import macro_f1_from_confusion
 from ..ops.engine import GpuEngine, decode_debug, model_bytes
@@ -59,7 +60,7 @@ def stats_from_packet(p: Dict[str, np.ndarray]) -> SufficientStats:
 @dataclass
 class StagedWindow:
     """A window's records in pinned host memory, ready for DMA."""
-    ev: "object"        # torch uint8 pinned [>= n_events*64]
+    ev: "object"        # torch uint8 pinned [>= n_events*wire]
     sp: "object"        # torch uint8 pinned [>= n_spans*64]
     counts: "object"    # torch int32 pinned [4]
     labels: "object"    # torch int32 pinned [group_cap]
@@ -67,10 +68,25 @@ class StagedWindow:
     n_spans: int
     n_groups: int
     group_domains: List[List[str]] = field(default_factory=list)
+    wire: int = 64                      # event record bytes: 64 (EVENT) or 32 (EVENT32)
+    pod_table: Optional[np.ndarray] = None  # int32 pod id -> svc<<16|node (wire 32)
 
 
 def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
-                 group_cap: int, group_domains=None) -> StagedWindow:
+                 group_cap: int, group_domains=None, wire: int = 64, interner=None) -> StagedWindow:
+    """Pin a window for DMA. ``wire=32`` converts 64-byte events to the compact 32-byte
+    record (interned conn ids, milli-unit values; collector/records.py EVENT32), halving
+    the PCIe bytes that bound the pipeline; spans get the same interned conn ids."""
+    pod_tab = None
+    if wire == 32:
+        if interner is None:
+            interner = records.ConnInterner()
+        if events.dtype == records.EVENT:
+            pod_tab = records.pod_table(events, spans)
+            events = records.to_compact(events, interner)
+        spans = records.compact_spans(spans, interner)
+    elif wire != 64:
+        raise ValueError("wire must be 64 or 32")
     ev = torch.from_numpy(events.view(np.uint8).reshape(-1).copy()).pin_memory()
     sp = torch.from_numpy(spans.view(np.uint8).reshape(-1).copy()).pin_memory()
     counts = torch.tensor([events.shape[0], spans.shape[0], n_groups, 0], dtype=torch.int32).pin_memory()
@@ -79,7 +95,7 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
         lab[: len(labels)] = labels
     labels_t = torch.from_numpy(lab).pin_memory()
     return StagedWindow(ev, sp, counts, labels_t, int(events.shape[0]), int(spans.shape[0]), n_groups,
-                        list(group_domains or []))
+                        list(group_domains or []), wire, pod_tab)
 
 
 class WindowPipeline:
@@ -115,6 +131,7 @@ class WindowPipeline:
             self.h2d_done = [ev(), ev()]
             self.compute_done = [ev(), ev()]
             self.comm_done = [ev(), ev()]
+        self.pod_key = None
         self.i = 0
         self.cum_stats = SufficientStats()
         self.windows_folded = 0
@@ -154,8 +171,15 @@ class WindowPipeline:
         cs, ks, ms = self.copy_stream, self.compute_stream, self.comm_stream
         # H2D into buffer b once window i-2 (the last user of b) finished computing
         cs.wait_event(self.compute_done[b])
+        if w.pod_table is not None:
+            key = (w.pod_table.shape[0], hash(w.pod_table.tobytes()))
+            if key != self.pod_key:  # interned pod table changed: re-upload (rare)
+                self.drain()
+                self.engine.set_pod_table(w.pod_table)
+                self.pod_key = key
         with torch.cuda.stream(cs):
-            self.ev_dev[b][: w.n_events * 64].copy_(w.ev[: w.n_events * 64], non_blocking=True)
+            nb = w.n_events * w.wire
+            self.ev_dev[b][:nb].copy_(w.ev[:nb], non_blocking=True)
             self.sp_dev[b][: w.n_spans * 64].copy_(w.sp[: w.n_spans * 64], non_blocking=True)
             self.counts_dev[b].copy_(w.counts, non_blocking=True)
             self.labels_dev[b].copy_(w.labels, non_blocking=True)
@@ -165,7 +189,7 @@ class WindowPipeline:
         with torch.cuda.stream(ks):
             self.eng.bind_io(self.counts_dev[b], self.labels_dev[b], self.packet_dev[b])
             self.eng.run_window(self.ev_dev[b], self.sp_dev[b], w.n_groups, with_labels,
-                                self.learn and with_labels)
+                                self.learn and with_labels, w.wire)
             self.compute_done[b].record(ks)
         ms.wait_event(self.compute_done[b])
         with torch.cuda.stream(ms):

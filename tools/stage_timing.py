@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--spans", type=int, default=16384)
     ap.add_argument("--services", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--wire", type=int, default=32, choices=(32, 64))
     a = ap.parse_args()
     t = time.time()
     cfg = ReplayConfig(events_per_window=a.events, spans_per_window=a.spans, n_services=a.services)
@@ -29,13 +30,20 @@ def main():
     print(f"gen {time.time() - t:.2f}s", flush=True)
     eng = GpuEngine(a.events, a.spans, a.services)
     eng.set_model(NaiveBayes.ref())
-    eng.stage(win.events, win.spans, win.n_groups, win.group_labels)
+    ev, sp = win.events, win.spans
+    if a.wire == 32:
+        from llm_slo_ebpf_toolkit_amd.collector import records
+
+        it = records.ConnInterner()
+        eng.set_pod_table(records.pod_table(ev, sp))
+        ev, sp = records.to_compact(ev, it), records.compact_spans(sp, it)
+    eng.stage(ev, sp, win.n_groups, win.group_labels)
     eng.upload()
     torch.cuda.synchronize()
     e = eng.eng
     stages = {
         "reset": lambda: e.reset_window(),
-        "decode": lambda: e.decode(eng.ev_dev),
+        "decode": (lambda: e.decode_compact(eng.ev_dev)) if a.wire == 32 else (lambda: e.decode(eng.ev_dev)),
         "join": lambda: e.join(eng.sp_dev, win.n_groups, None),
         "posterior": lambda: e.posterior(True),
         "stats": lambda: e.accumulate_stats(None),
