@@ -12,8 +12,9 @@ REF pkg/releasegate/gate.go:21-946, same defaults (3 % overhead, 10 % CV, >= 3 r
 Statistics: Mann-Whitney U with average tie ranks, tie-corrected variance and
 continuity correction (:816-891); Cliff's delta (:893-911); bootstrap CI of the p95
 difference (:917-946). Go's math/rand stream cannot be bit-reproduced in Python; the
-bootstrap is seeded (numpy PCG64, seed 42) and vectorised -- on a GPU it runs as the
-``ops.gatestats`` HIP kernel (all iterations x resamples in one launch).
+bootstrap uses a seeded counter-based stream (splitmix64, seed 42) that the numpy path
+and the ``ops.gatestats`` HIP kernel (K5: all iterations x resamples in one launch, LDS
+multiplicity histograms instead of per-resample sorts) evaluate identically.
 """
 
 from __future__ import annotations
@@ -142,34 +143,17 @@ def cliffs_delta(x: Sequence[float], y: Sequence[float]) -> float:
     return float(greater - lower) / float(len(xa) * len(ys))
 
 
-def _quantile_rows(a: np.ndarray, q: float) -> np.ndarray:
-    """Row-wise REF linear-interpolation quantile of an [iters, n] matrix."""
-    s = np.sort(a, axis=1)
-    n = s.shape[1]
-    if n == 1:
-        return s[:, 0]
-    pos = q * (n - 1)
-    lo, hi = math.floor(pos), math.ceil(pos)
-    if lo == hi:
-        return s[:, lo]
-    f = pos - lo
-    return s[:, lo] * (1 - f) + s[:, hi] * f
-
-
 def bootstrap_delta_ci(cand: Sequence[float], base: Sequence[float], quant: float, iterations: int,
                        seed: int = 42, use_gpu: bool = False) -> Tuple[float, float]:
     if len(cand) == 0 or len(base) == 0 or iterations < 10:
         return 0.0, 0.0
+    from ..ops import gatestats
+
     c = np.asarray(cand, dtype=np.float64)
     b = np.asarray(base, dtype=np.float64)
-    if use_gpu:
-        from ..ops import gatestats
-
-        deltas = gatestats.bootstrap_quantile_delta(c, b, quant, iterations, seed)
-    else:
-        rng = np.random.default_rng(seed)
-        deltas = (_quantile_rows(c[rng.integers(0, len(c), size=(iterations, len(c)))], quant)
-                  - _quantile_rows(b[rng.integers(0, len(b), size=(iterations, len(b)))], quant))
+    # counter-based resampling stream shared by the numpy path and the K5 HIP kernel, so
+    # the CPU and GPU gates agree bit for bit (ops/gatestats.py)
+    deltas = gatestats.bootstrap_quantile_delta(c, b, quant, iterations, seed, use_gpu=use_gpu)
     deltas = np.sort(deltas)
     lo = max(int(math.floor(0.025 * (len(deltas) - 1))), 0)
     hi = min(int(math.ceil(0.975 * (len(deltas) - 1))), len(deltas) - 1)
@@ -354,10 +338,14 @@ def evaluate_significance(c: Config) -> Dict[str, object]:
             out["pass"] = False
             out["scenarios"].append(r)
             continue
-        p = mann_whitney_p(ct, bt)
+        if c.use_gpu:  # K5 rank counts on the device: ranks, ties and Cliff's delta in one pass
+            from ..ops import gatestats
+
+            p, cd, _ = gatestats.stats_from_rank_counts(gatestats.rank_counts(ct, bt), len(ct), len(bt))
+        else:
+            p, cd = mann_whitney_p(ct, bt), cliffs_delta(ct, bt)
         sub_seed = c.bootstrap_seed + idx  # one deterministic stream per scenario
         lo, hi = bootstrap_delta_ci(ct, bt, 0.95, c.bootstrap_iterations, sub_seed, c.use_gpu)
-        cd = cliffs_delta(ct, bt)
         r.update({"mann_whitney_p_value": p, "bootstrap_delta_ci95": [lo, hi], "cliffs_delta": cd,
                   "practical_effect_pass": abs(cd) >= c.min_cliffs_delta_for_failure})
         is_reg = reg > c.regression_pct_limit and p < c.significance_alpha and lo > 0

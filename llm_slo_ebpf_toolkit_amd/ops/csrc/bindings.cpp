@@ -382,9 +382,64 @@ void set_tables_py(torch::Tensor type_slot, torch::Tensor scale, torch::Tensor w
   set_tables(&t);
 }
 
+// ---- K5 gate statistics / K6 storm counts (stand-alone device ops) -----------------------
+static void check_dev(const torch::Tensor& t, torch::ScalarType st, const char* name) {
+  check_cuda(t, name);
+  if (t.scalar_type() != st) throw std::invalid_argument(std::string(name) + ": wrong dtype");
+}
+
+// sorted_c / sorted_b: ascending f64 samples; returns [2, iters] bootstrap quantiles
+torch::Tensor boot_quantile_py(torch::Tensor sorted_c, torch::Tensor sorted_b, double q, int64_t iters,
+                               int64_t seed) {
+  check_dev(sorted_c, torch::kFloat64, "sorted_c");
+  check_dev(sorted_b, torch::kFloat64, "sorted_b");
+  const int64_t nc = sorted_c.numel(), nb = sorted_b.numel();
+  if (nc < 1 || nb < 1 || nc > boot_max_n() || nb > boot_max_n())
+    throw std::invalid_argument("bootstrap sample sizes must be in [1, boot_max_n]");
+  if (iters < 1 || iters >= (1LL << 31)) throw std::invalid_argument("iters out of range");
+  if (!(q >= 0.0 && q <= 1.0)) throw std::invalid_argument("q must be in [0, 1]");
+  c10::hip::HIPGuard guard(sorted_c.device());
+  auto out = torch::empty({2, iters}, sorted_c.options());
+  launch_boot_quantile(sorted_c.data_ptr<double>(), (int)nc, sorted_b.data_ptr<double>(), (int)nb, q, (int)iters,
+                       (uint64_t)seed, out.data_ptr<double>(), cur_stream());
+  return out;
+}
+
+// vals: [x..., y...] f64; returns uint32-as-int32 [4, n]: (all<v, all==v, y<v, y>v)
+torch::Tensor rank_counts_py(torch::Tensor vals, int64_t nx) {
+  check_dev(vals, torch::kFloat64, "vals");
+  const int64_t n = vals.numel();
+  if (nx < 0 || nx > n || n >= (1LL << 31)) throw std::invalid_argument("nx out of range");
+  c10::hip::HIPGuard guard(vals.device());
+  auto out = torch::empty({4, n}, vals.options().dtype(torch::kInt32));
+  if (n) launch_rank_counts(vals.data_ptr<double>(), (int)n, (int)nx, dptr<uint32_t>(out), cur_stream());
+  return out;
+}
+
+// keys (int64, sorted), ts (int64, sorted within key): per-event window counts + storm tally
+std::tuple<torch::Tensor, torch::Tensor> storm_counts_py(torch::Tensor keys, torch::Tensor ts, int64_t window_ns,
+                                                         int64_t threshold) {
+  check_dev(keys, torch::kInt64, "keys");
+  check_dev(ts, torch::kInt64, "ts");
+  const int64_t n = keys.numel();
+  if (ts.numel() != n || n >= (1LL << 31)) throw std::invalid_argument("keys/ts size mismatch");
+  c10::hip::HIPGuard guard(keys.device());
+  auto counts = torch::empty({n}, keys.options().dtype(torch::kInt32));
+  auto tally = torch::zeros({1}, keys.options());
+  launch_storm_counts(dptr<uint64_t>(keys), ts.data_ptr<int64_t>(), (int)n, window_ns, (uint32_t)threshold,
+                      dptr<uint32_t>(counts), dptr<unsigned long long>(tally), cur_stream());
+  return {counts, tally};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) LLM-SLO engine kernels";
   m.def("set_tables", &set_tables_py);
+  m.def("boot_quantile", &boot_quantile_py, py::arg("sorted_c"), py::arg("sorted_b"), py::arg("q"),
+        py::arg("iters"), py::arg("seed"));
+  m.def("rank_counts", &rank_counts_py, py::arg("vals"), py::arg("nx"));
+  m.def("storm_counts", &storm_counts_py, py::arg("keys"), py::arg("ts"), py::arg("window_ns"),
+        py::arg("threshold"));
+  m.attr("BOOT_MAX_N") = boot_max_n();
   m.attr("PACKET_LEN") = kPacketLen;
   m.attr("PACKET_LAYOUT") = py::make_tuple(kPacketHist, kPacketStatus, kPacketMisc, kPacketDbg, kPacketConf,
                                            kPacketStats, kPacketCount);

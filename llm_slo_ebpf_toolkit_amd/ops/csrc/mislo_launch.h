@@ -56,4 +56,14 @@ void launch_posterior(const float* feat, const int* ng_dev, int cap, const Poste
 void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                   const float* weights, double* out, double* count, hipStream_t stream);
 
+// gatestats.hip (K5)
+int boot_max_n();
+void launch_boot_quantile(const double* sorted_c, int nc, const double* sorted_b, int nb, double q, int iters,
+                          uint64_t seed, double* out, hipStream_t stream);
+void launch_rank_counts(const double* vals, int n_all, int nx, uint32_t* out, hipStream_t stream);
+
+// storm.hip (K6)
+void launch_storm_counts(const uint64_t* keys, const int64_t* ts, int n, int64_t window_ns, uint32_t threshold,
+                         uint32_t* counts, unsigned long long* n_storm, hipStream_t stream);
+
 }  // namespace mislo
