@@ -1,0 +1,118 @@
+"""Agent Prometheus surface: every REF metric name/type/label set (REF cmd/agent/main.go:137-302,
+SURVEY §2.8) plus the GPU window engine's metrics (additive, ``llm_slo_agent_gpu_*``).
+
+GPU histograms arrive as per-window bucket counts from the decode kernel (LDS-privatised,
+RCCL all-reduced across GPUs); ``observe_window_hist`` folds them into Prometheus
+histograms without re-observing events. The kernel's buckets are ``le`` buckets
+(v in (edge[b-1], edge[b]]) over the catalogue edges, of which REF's DNS edges
+{1..800} are a prefix, so the REF-named DNS histogram keeps exact ``le`` semantics.
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from ..contracts.types import ProbeEventV1
+from ..export.prometheus import Registry
+from ..signals import catalog
+
+EVENT_KINDS = ("slo", "probe", "both")
+DROP_REASONS = ("rate_limit", "schema", "emit")
+
+
+def _nz(v: str, fallback: str) -> str:
+    v = (v or "").strip()
+    return v if v else fallback
+
+
+class AgentMetrics:
+    def __init__(self, event_kind: str, capability_mode: str, supported: Sequence[str], enabled: Sequence[str]):
+        r = self.registry = Registry()
+        self.heartbeat = r.gauge("llm_slo_agent_heartbeat", "Unix timestamp of latest emitted sample.")
+        self.up = r.gauge("llm_slo_agent_up", "Agent process liveness.")
+        self.cpu = r.gauge("llm_slo_agent_cpu_overhead_pct", "Estimated agent CPU overhead percentage.")
+        self.kind = r.gauge("llm_slo_agent_event_kind", "Selected event-kind mode (one-hot gauge).", ("kind",))
+        self.mode = r.gauge("llm_slo_agent_capability_mode", "Detected capability mode (one-hot gauge).", ("mode",))
+        self.sig_enabled = r.gauge("llm_slo_agent_signal_enabled", "Signal enablement toggle by signal name.",
+                                   ("signal",))
+        self.dropped = r.counter("llm_slo_agent_dropped_events_total", "Dropped probe events by reason.", ("reason",))
+        self.hello = r.counter("llm_ebpf_hello_syscalls_total", "Hello tracer syscall events by comm.",
+                               ("node", "pod", "comm"))
+        self.dns = r.histogram("llm_ebpf_dns_latency_ms", "DNS latency observed from probe events.",
+                               catalog.REF_DNS_BUCKETS, ("node", "pod", "namespace"))
+        self.probe_events = r.counter("llm_ebpf_probe_events_total", "Probe events observed by signal and status.",
+                                      ("signal", "status"))
+        # ---- GPU window engine (additive) ----
+        self.win_events = r.counter("llm_slo_agent_gpu_window_events_total", "Events processed by the GPU engine.")
+        self.win_total = r.counter("llm_slo_agent_gpu_windows_total", "Windows processed by the GPU engine.")
+        self.win_latency = r.histogram("llm_slo_agent_gpu_window_latency_ms",
+                                       "Ring drain to attribution latency per window.",
+                                       (0.5, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000))
+        self.attr = r.counter("llm_slo_agent_attributions_total", "Incident attributions by predicted domain.",
+                              ("domain",))
+        self.corr = r.counter("llm_slo_agent_correlation_pairs_total",
+                              "Span/signal correlation outcomes (REF DebugStats) from the join kernel.", ("outcome",))
+        self.ring_dropped = r.gauge("llm_slo_agent_ring_dropped_events", "Events dropped by full producer rings.")
+        self.up.set(1)
+        for k in EVENT_KINDS:
+            self.kind.set(1 if k == event_kind else 0, k)
+        for m in catalog.CAPABILITY_MODES:
+            self.mode.set(1 if m == capability_mode else 0, m)
+        for reason in DROP_REASONS:
+            self.dropped.inc(0, reason)
+        self.set_enabled_signals(supported, enabled)
+
+    def set_heartbeat(self, ts_s: float = 0.0) -> None:
+        self.heartbeat.set(float(int(ts_s or time.time())))
+
+    def set_cpu_overhead(self, pct: float) -> None:
+        self.cpu.set(max(0.0, pct))
+
+    def set_enabled_signals(self, supported: Iterable[str], enabled: Iterable[str]) -> None:
+        en = set(enabled)
+        for s in supported:
+            self.sig_enabled.set(1 if s in en else 0, s)
+
+    def observe_probe_event(self, ev: ProbeEventV1, real_probe_metrics: bool = True) -> None:
+        self.probe_events.inc(1, ev.signal, ev.status)
+        if real_probe_metrics and ev.signal == "dns_latency_ms":
+            self.dns.observe(ev.value, _nz(ev.node, "unknown-node"), _nz(ev.pod, "unknown-pod"),
+                             _nz(ev.namespace, "default"))
+
+    def inc_dropped(self, reason: str) -> None:
+        self.dropped.inc(1, reason)
+
+    def inc_hello(self, node: str, pod: str, comm: str, count: int) -> None:
+        if count:
+            self.hello.inc(float(count), _nz(node, "unknown-node"), _nz(pod, "unknown-pod"), _nz(comm, "unknown"))
+
+    # ---- GPU window outputs -------------------------------------------------------------
+    def observe_window(self, hist: np.ndarray, status: np.ndarray, dbg, n_events: int, latency_ms: float,
+                       node: str, pod: str, namespace: str) -> None:
+        """hist [16 slots x 16 buckets], status [16 x 3] from the window packet."""
+        self.win_total.inc()
+        self.win_events.inc(float(n_events))
+        self.win_latency.observe(latency_ms)
+        dns = catalog.BY_NAME["dns_latency_ms"].slot
+        h = np.asarray(hist[dns], dtype=np.float64)
+        nref = len(catalog.REF_DNS_BUCKETS)
+        ref_counts = list(h[:nref]) + [float(h[nref:].sum())]  # buckets above 800 -> +Inf
+        self.dns.add_counts(ref_counts, 0.0, _nz(node, "unknown-node"), _nz(pod, "unknown-pod"),
+                            _nz(namespace, "default"))
+        names = ("ok", "warning", "error")
+        for s in catalog.SIGNALS:
+            row = status[s.slot]
+            for k in range(3):
+                if row[k]:
+                    self.probe_events.inc(float(row[k]), s.name, names[k])
+        cand, low, overlap, dropped, enriched = (int(x) for x in list(dbg)[:5])
+        self.corr.inc(float(cand), "candidate")
+        self.corr.inc(float(max(0, low - overlap)), "low_confidence")
+        self.corr.inc(float(dropped), "fanout_dropped")
+        self.corr.inc(float(enriched), "span_enriched")
+
+    def observe_attribution(self, domain: str) -> None:
+        self.attr.inc(1, domain)

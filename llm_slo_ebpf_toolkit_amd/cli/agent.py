@@ -1,0 +1,109 @@
+"""`agent`: node DaemonSet process (REF cmd/agent/main.go:269-633; flags :334-373).
+
+REF flags are all accepted with REF defaults. Additive flags select the MI355X window
+engine: ``--engine gpu --source replay|ring --window-ms --window-events --device
+--model --min-confidence --wire``; ``--count`` bounds the number of windows in GPU mode.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+from typing import List, Optional
+
+from ..agent.daemon import Agent, AgentOptions, run_forever
+from ..collector.probes import probe_smoke_check
+from ._common import GoFlags, eprint, is_version_request, print_version, split_csv
+
+
+def parse(argv: List[str]) -> (AgentOptions, bool):
+    d = AgentOptions()
+    p = GoFlags("agent", "LLM SLO node agent (MI355X window engine)")
+    for name, default, help_ in [
+        ("cluster", d.cluster, "cluster name"), ("namespace", d.namespace, "namespace"),
+        ("workload", d.workload, "workload"), ("service", d.service, "service"),
+        ("k8s-node", d.node, "node label"), ("pod", d.pod, "pod name"), ("container", d.container, "container name"),
+        ("scenario", d.scenario, "synthetic scenario name"), ("count", d.count, "sample count (0 = stream mode)"),
+        ("interval-ms", d.interval_ms, "emit interval for stream mode"),
+        ("event-kind", d.event_kind, "event kind: slo|probe|both"),
+        ("output", d.output, "output mode: stdout|jsonl|otlp"),
+        ("output-path", d.output_path, "output file when output=jsonl"),
+        ("otlp-endpoint", d.otlp_endpoint, "OTLP/HTTP logs endpoint when output=otlp"),
+        ("otlp-timeout-ms", d.otlp_timeout_ms, "OTLP export timeout in milliseconds"),
+        ("otlp-batch", d.otlp_batch, "log records per OTLP POST"),
+        ("webhook-url", d.webhook_url, "webhook endpoint URL (empty = disabled)"),
+        ("webhook-secret", d.webhook_secret, "HMAC-SHA256 secret for webhook signing"),
+        ("webhook-format", d.webhook_format, "webhook payload format: generic|pagerduty|opsgenie"),
+        ("webhook-timeout-ms", d.webhook_timeout_ms, "webhook HTTP timeout in milliseconds"),
+        ("capability-mode", d.capability_mode, "capability mode: auto|core_full|bcc_degraded|replay|gpu"),
+        ("disable-signals", "", "comma-separated signal names to disable"),
+        ("disable-overhead-guard", False, "disable overhead guard"),
+        ("config", d.config, "toolkit config path"),
+        ("enable-hello-tracer", False, "enable hello tracer metric path"),
+        ("hello-target-comm", ",".join(d.hello_target_comm), "comma-separated comm names for hello tracer"),
+        ("enable-real-probe-metrics", True, "enable probe-derived metrics on /metrics"),
+        ("metrics-bind", d.metrics_bind, "metrics and health bind address"),
+        ("probe-smoke", False, "run eBPF smoke check and exit"),
+        ("engine", d.engine, "attribution engine: synthetic (REF tick loop) | gpu (MI355X window engine)"),
+        ("source", d.source, "gpu engine record source: replay | ring"),
+        ("ring-name", d.ring_name, "shared-memory ring name prefix for --source ring"),
+        ("window-ms", d.window_ms, "gpu engine window length"),
+        ("window-events", d.window_events, "gpu engine events per window (capacity)"),
+        ("window-spans", d.window_spans, "gpu engine spans per window (capacity)"),
+        ("window-groups", d.window_groups, "gpu engine incident groups per window"),
+        ("device", d.device, "HIP device ordinal"),
+        ("model", d.model, "attribution model: bayes|bayes_learned|lda"),
+        ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
+        ("wire", d.wire, "event record bytes on PCIe: 32 (compact) | 64"),
+    ]:
+        p.flag(name, default, help_)
+    a = p.parse_args(argv)
+    o = AgentOptions(
+        cluster=a.cluster, namespace=a.namespace, workload=a.workload, service=a.service, node=a.k8s_node,
+        pod=a.pod, container=a.container, scenario=a.scenario, count=a.count, interval_ms=a.interval_ms,
+        event_kind=a.event_kind, output=a.output, output_path=a.output_path, otlp_endpoint=a.otlp_endpoint,
+        otlp_timeout_ms=a.otlp_timeout_ms, otlp_batch=a.otlp_batch, webhook_url=a.webhook_url,
+        webhook_secret=a.webhook_secret, webhook_format=a.webhook_format, webhook_timeout_ms=a.webhook_timeout_ms,
+        capability_mode=a.capability_mode, disable_signals=split_csv(a.disable_signals),
+        disable_overhead_guard=a.disable_overhead_guard, config=a.config, enable_hello_tracer=a.enable_hello_tracer,
+        hello_target_comm=split_csv(a.hello_target_comm), enable_real_probe_metrics=a.enable_real_probe_metrics,
+        metrics_bind=a.metrics_bind, engine=a.engine, source=a.source, ring_name=a.ring_name,
+        window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
+        window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence, wire=a.wire)
+    return o, a.probe_smoke
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    if is_version_request(argv):
+        return print_version()
+    opts, smoke = parse(argv)
+    if smoke:
+        try:
+            probe_smoke_check()
+        except Exception as exc:  # noqa: BLE001
+            eprint(f"probe smoke failed: {exc}")
+            return 1
+        print("probe smoke ok")
+        return 0
+    try:
+        agent = Agent(opts)
+    except Exception as exc:  # noqa: BLE001
+        eprint(str(exc))
+        return 1
+    agent.start_server()
+    agent.start_hello_tracer()
+    if opts.engine == "gpu":
+        from ..ops import require_gpu_extension
+
+        require_gpu_extension()
+        return run_forever(agent, lambda: agent.run_windows(max_windows=opts.count))
+    try:
+        return run_forever(agent, agent.run_synthetic)
+    except Exception as exc:  # noqa: BLE001 - REF: emit failures are fatal (exit 1)
+        eprint(f"emit sample failed: {exc}")
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

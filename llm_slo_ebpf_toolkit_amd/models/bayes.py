@@ -113,22 +113,33 @@ class LinearPosteriorModel:
     def attribute(self, signals: Dict[str, float]) -> List[Posterior]:
         """Single-sample API with REF ordering semantics (stable sort, domain order ties)."""
         vec = np.array([catalog.feature_vector(signals)], dtype=np.float64)
-        post = self.posteriors(vec)[0]
-        bits = self.evidence_bits(vec)[0]
+        return self.ranked(self.posteriors(vec)[0], self.evidence_bits(vec)[0])
+
+    def ranked(self, post: np.ndarray, bits: np.ndarray) -> List[Posterior]:
+        """Posterior row + evidence bitmask row (numpy or the GPU kernel's) -> sorted hypotheses."""
         out: List[Posterior] = []
         for d, dom in enumerate(catalog.ALL_DOMAINS[: self.weights.shape[1]]):
             if not np.isfinite(self.bias[d]):
                 continue
-            ev = sorted(catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if bits[d] >> s & 1)
+            ev = sorted(catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if int(bits[d]) >> s & 1)
             out.append(Posterior(dom, float(post[d]), ev))
         out.sort(key=lambda p: -p.posterior)  # Python sort is stable == sort.SliceStable
         return out
 
     def attribute_sample(self, sample: FaultSample) -> IncidentAttribution:
-        base = build_attribution(sample)
         if not sample.signals:
-            return base
-        posts = self.attribute(sample.signals)
+            return build_attribution(sample)
+        return self.attribution_from_ranked(sample, self.attribute(sample.signals))
+
+    def attribution_from_posterior(self, sample: FaultSample, post: np.ndarray,
+                                   bits: np.ndarray) -> IncidentAttribution:
+        if not sample.signals:
+            return build_attribution(sample)
+        return self.attribution_from_ranked(sample, self.ranked(post, bits))
+
+    @staticmethod
+    def attribution_from_ranked(sample: FaultSample, posts: List[Posterior]) -> IncidentAttribution:
+        base = build_attribution(sample)
         base.fault_hypotheses = [FaultHypothesis(p.domain, p.posterior, p.evidence)
                                  for p in posts if p.posterior >= 0.01]
         if posts:

@@ -39,7 +39,7 @@ void check_cuda(const torch::Tensor& t, const char* name) {
 
 constexpr int kPacketHist = kSlots * kBuckets;            // 256
 constexpr int kPacketStatus = kSlots * 3;                 // 48
-constexpr int kPacketMisc = 2;
+constexpr int kPacketMisc = 2 + kSlots;             // unsupported, zero-ts, per-slot value sums (milli)
 constexpr int kPacketDbg = 8;
 constexpr int kPacketConf = kMaxDomains * kMaxDomains;    // 256
 constexpr int kPacketStats = 32 * 32;                     // 1024

@@ -24,8 +24,11 @@ struct DecodeOut {
   uint32_t* hist;        // [kSlots * kBuckets]
   uint32_t* status_cnt;  // [kSlots * 3]
   uint32_t* part_cnt;    // [gridDim.x][kKeyTypes * kParts] per-block partition counts
-  unsigned long long* misc;  // [0] unsupported events, [1] zero-timestamp events
+  unsigned long long* misc;  // [0] unsupported events, [1] zero-timestamp events,
+                             // [2 + slot] per-signal value sum in 1/1000 units (Prometheus _sum)
 };
+
+constexpr int kMiscSums = 2;  // offset of the per-slot value sums in misc
 
 template <int NT>
 __device__ __forceinline__ void flush_counts(uint32_t* lds, uint32_t* global, int n) {
@@ -46,8 +49,8 @@ __device__ __forceinline__ void store_counts(const uint32_t* lds, uint32_t* dst)
 __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val, int slot,
                                            uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
                                            uint64_t conn_h, const DecodeOut& o, uint32_t* s_hist,
-                                           uint32_t* s_status, uint32_t* s_part, int& unsupported,
-                                           int& zero_ts) {
+                                           uint32_t* s_status, uint32_t* s_part, unsigned long long* s_sum,
+                                           int& unsupported, int& zero_ts) {
   uint8_t st = 0;
   if (slot >= 0) {
     st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
@@ -57,6 +60,9 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
     for (int e = 0; e < kBuckets - 1; ++e) b += (val > c_tab.edges[slot][e]) ? 1 : 0;
     atomicAdd(&s_hist[slot * kBuckets + b], 1u);
     atomicAdd(&s_status[slot * 3 + st], 1u);
+    // exact, order-independent integer sum (values are >= 0 by construction)
+    const double milli = rint((double)val * 1000.0);
+    if (milli > 0.0) atomicAdd(&s_sum[slot], (unsigned long long)milli);
   } else {
     ++unsupported;
   }
@@ -87,7 +93,9 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
   __shared__ uint32_t s_hist[kSlots * kBuckets];
   __shared__ uint32_t s_status[kSlots * 3];
   __shared__ uint32_t s_part[kKeyTypes * kParts];
+  __shared__ unsigned long long s_sum[kSlots];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
   for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
   for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
   __syncthreads();
@@ -104,11 +112,12 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
     const uint64_t ch = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
     const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
     decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status,
-               s_part, unsupported, zero_ts);
+               s_part, s_sum, unsupported, zero_ts);
   }
   __syncthreads();
   flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
   flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
   store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
   // wave-level reduction of the scalar counters, one atomic per wave
   for (int off = 32; off > 0; off >>= 1) {
@@ -131,7 +140,9 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
   __shared__ uint32_t s_hist[kSlots * kBuckets];
   __shared__ uint32_t s_status[kSlots * 3];
   __shared__ uint32_t s_part[kKeyTypes * kParts];
+  __shared__ unsigned long long s_sum[kSlots];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
   for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
   for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
   __syncthreads();
@@ -148,11 +159,12 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
     const uint64_t ch = (uint64_t)(e.type_conn >> 8);
     const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
     decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status, s_part,
-               unsupported, zero_ts);
+               s_sum, unsupported, zero_ts);
   }
   __syncthreads();
   flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
   flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
   store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
   for (int off = 32; off > 0; off >>= 1) {
     unsupported += __shfl_xor(unsupported, off);
@@ -173,7 +185,9 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
   __shared__ uint32_t s_hist[kSlots * kBuckets];
   __shared__ uint32_t s_status[kSlots * 3];
   __shared__ uint32_t s_part[kKeyTypes * kParts];
+  __shared__ unsigned long long s_sum[kSlots];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
   for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
   for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
   __syncthreads();
@@ -190,11 +204,12 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
     else val = (float)((double)e.value_ns / 1e6);               // ns -> ms
     const uint64_t ch = conn_hash(e.conn_src_port, e.conn_dst_port, e.conn_dst_ip);
     decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, s_hist,
-               s_status, s_part, unsupported, zero_ts);
+               s_status, s_part, s_sum, unsupported, zero_ts);
   }
   __syncthreads();
   flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
   flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
   store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
   for (int off = 32; off > 0; off >>= 1) {
     unsupported += __shfl_xor(unsupported, off);
@@ -211,7 +226,9 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp, const int* __restrict__ n_ptr,
                                                      int cap, SpanCols c, uint32_t* part_cnt) {
   __shared__ uint32_t s_part[kKeyTypes * kParts];
+  __shared__ unsigned long long s_sum[kSlots];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
   __syncthreads();
   const int n = min(*n_ptr, cap);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;

@@ -87,6 +87,7 @@ class WindowOutputs:
     conf: np.ndarray
     evbits: np.ndarray
     confusion: np.ndarray
+    value_sum: np.ndarray  # [16] per-slot sums of decoded values (exact milli-unit integer sums)
 
 
 class GpuEngine:
@@ -178,4 +179,5 @@ class GpuEngine:
             hist=e.hist.cpu().numpy().astype(np.int64), status=e.status_cnt.cpu().numpy().astype(np.int64),
             debug=decode_debug(dbg, misc, self.n_spans, self.n_events), feat=e.feat[:G].cpu().numpy(),
             post=e.post[:G].cpu().numpy(), pred=e.pred[:G].cpu().numpy(), conf=e.gconf[:G].cpu().numpy(),
-            evbits=e.evbits[:G].cpu().numpy().view(np.uint32), confusion=e.confusion.cpu().numpy().astype(np.int64))
+            evbits=e.evbits[:G].cpu().numpy().view(np.uint32), confusion=e.confusion.cpu().numpy().astype(np.int64),
+            value_sum=misc[2:18].astype(np.float64) * 1e-3)

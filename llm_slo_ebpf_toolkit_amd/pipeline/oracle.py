@@ -94,6 +94,16 @@ def histograms(d: Decoded) -> np.ndarray:
     return h
 
 
+def value_sums_milli(d: Decoded) -> np.ndarray:
+    """Per-slot exact integer sums of rint(val * 1000) (decode kernels' misc[2:18])."""
+    out = np.zeros(16, dtype=np.int64)
+    ok = d.slot != NO_SLOT
+    milli = np.rint(d.val[ok].astype(np.float64) * 1000.0)
+    milli = np.where(milli > 0, milli, 0).astype(np.int64)
+    np.add.at(out, d.slot[ok].astype(np.int64), milli)
+    return out
+
+
 @dataclass
 class JoinResult:
     top3: np.ndarray        # uint64 [S,3]

@@ -34,7 +34,7 @@ from ..models.metrics import macro_f1_from_confusion
 from ..ops.engine import GpuEngine, decode_debug, model_bytes
 from ..signals import catalog
 
-PACKET_LAYOUT = (256, 48, 2, 8, 256, 1024, 16)  # hist, status, misc, dbg, confusion, stats, count
+PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16)  # hist, status, misc(+16 value sums), dbg, confusion, stats, count
 
 
 def unpack_packet(p: np.ndarray) -> Dict[str, np.ndarray]:
@@ -47,6 +47,7 @@ def unpack_packet(p: np.ndarray) -> Dict[str, np.ndarray]:
     out["status"] = out["status"].reshape(16, 3)
     out["confusion"] = out["confusion"].reshape(16, 16)
     out["stats"] = out["stats"].reshape(32, 32)
+    out["value_sum"] = out["misc"][2:18] * 1e-3  # per-slot sums of decoded values (output units)
     return out
 
 
@@ -113,6 +114,8 @@ class WindowPipeline:
         self.engine = GpuEngine(sig_cap, span_cap, group_cap, device, window_ms, threshold, fanout, group_mode)
         self.eng = self.engine.eng
         L = int(self.engine.mod.PACKET_LEN)
+        if tuple(self.engine.mod.PACKET_LAYOUT) != PACKET_LAYOUT:
+            raise RuntimeError("stale _mislo_hip build: packet layout mismatch (rebuild with ops.build)")
         self.packet_len = L
         with torch.cuda.device(self.dev):
             z8 = lambda n: torch.zeros(n, dtype=torch.uint8, device=self.dev)  # noqa: E731
@@ -208,6 +211,12 @@ class WindowPipeline:
             self.cum_stats = self.cum_stats.merge(stats_from_packet(pk))
             self.windows_folded += 1
             self.refit(self.cum_stats)
+
+    def last_packet(self) -> Dict[str, np.ndarray]:
+        """Unpacked (all-reduced) packet of the most recently submitted window (after drain)."""
+        b = (self.i - 1) % 2
+        self.comm_done[b].synchronize()
+        return unpack_packet(self.packet_host[b].numpy().copy())
 
     def drain(self) -> None:
         self.torch.cuda.synchronize(self.dev)

@@ -175,6 +175,8 @@ uint64_t mislo_ring_push_batch(void* ring, const void* recs, uint64_t n) {
   return reinterpret_cast<ShmRing*>(ring)->ring->push_batch(recs, n);
 }
 
+void* mislo_ring_handle_ring(void* ring) { return ring ? reinterpret_cast<ShmRing*>(ring)->ring : nullptr; }
+
 uint64_t mislo_ring_size(void* ring) { return reinterpret_cast<ShmRing*>(ring)->ring->size(); }
 
 uint64_t mislo_ring_dropped(void* ring) {

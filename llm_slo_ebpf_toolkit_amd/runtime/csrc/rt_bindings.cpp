@@ -24,7 +24,7 @@ class HostRing {
     if (!shm_name.empty()) {
       shm_ = mislo_ring_create_shm(shm_name.c_str(), capacity, rec_size);
       if (!shm_) throw std::runtime_error("cannot create shared-memory ring " + shm_name);
-      ring_ = *reinterpret_cast<Ring**>(shm_);  // ShmRing's first member is the Ring*
+      ring_ = static_cast<Ring*>(mislo_ring_handle_ring(shm_));
     } else {
       bytes_ = Ring::bytes_for(capacity, rec_size);
       if (posix_memalign(&mem_, 4096, bytes_) != 0) throw std::bad_alloc();

@@ -42,6 +42,7 @@ def test_decode_join_matches_oracle(engine, group_mode):
     np.testing.assert_array_equal(e.g_slot[:N].cpu().numpy(), d.slot)
     np.testing.assert_array_equal(e.g_val[:N].cpu().numpy(), d.val)
     np.testing.assert_array_equal(out.hist, oracle.histograms(d))
+    np.testing.assert_array_equal(e.misc[2:18].cpu().numpy(), oracle.value_sums_milli(d))
     ref = oracle.join(d, win.spans, win.n_groups, group_mode=group_mode)
     top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
     np.testing.assert_array_equal(top3, ref.top3)
