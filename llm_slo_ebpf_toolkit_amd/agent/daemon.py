@@ -353,9 +353,15 @@ class Agent:
             gen = ReplayGenerator(ReplayConfig(scenario=o.scenario if o.scenario != "baseline" else "full",
                                                events_per_window=o.window_events, spans_per_window=o.window_spans,
                                                n_services=o.window_groups, window_ms=o.window_ms))
+            # The replay producer stands in for the BPF / rocprofiler producers, which run
+            # outside the agent: pre-generate a few windows and cycle them so the agent's
+            # overhead guard measures the agent, not the synthetic trace generator.
+            pool = [gen.next_window() for _ in range(4)]
+            i = 0
             while True:
-                w = gen.next_window()
-                yield w.events, w.spans, w.n_groups, [f"svc-{g + 1}" for g in range(w.n_groups)], w.t0_ns
+                w = pool[i % len(pool)]
+                i += 1
+                yield w.events, w.spans, w.n_groups, [f"svc-{g + 1}" for g in range(w.n_groups)], now_ns()
         elif o.source == "ring":
             yield from RingSource(o.ring_name, o.window_events, o.window_spans).windows(o.window_ms, self.stop_event,
                                                                                         o.window_groups)
@@ -394,10 +400,16 @@ class Agent:
         pipe = WindowPipeline(o.window_events, o.window_spans, o.window_groups, o.device, process_group,
                               model=o.model, learn=False)
         interner = ConnInterner()
+        source = self._window_source()
+        first = next(source)  # producer warm-up happens before the guard's first sample
+        if self.guard is not None:
+            self.guard.evaluate()
         self.ready = True
         period = o.window_ms / 1000.0
         nxt = time.monotonic()
-        for events, spans, n_groups, names, t0 in self._window_source():
+        import itertools
+
+        for events, spans, n_groups, names, t0 in itertools.chain([first], source):
             if self.stop_event.is_set():
                 break
             t_start = time.perf_counter()

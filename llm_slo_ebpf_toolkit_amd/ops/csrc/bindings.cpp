@@ -398,7 +398,7 @@ torch::Tensor boot_quantile_py(torch::Tensor sorted_c, torch::Tensor sorted_b, d
     throw std::invalid_argument("bootstrap sample sizes must be in [1, boot_max_n]");
   if (iters < 1 || iters >= (1LL << 31)) throw std::invalid_argument("iters out of range");
   if (!(q >= 0.0 && q <= 1.0)) throw std::invalid_argument("q must be in [0, 1]");
-  c10::hip::HIPGuard guard(sorted_c.device());
+  c10::hip::HIPGuard guard(sorted_c.device().index());
   auto out = torch::empty({2, iters}, sorted_c.options());
   launch_boot_quantile(sorted_c.data_ptr<double>(), (int)nc, sorted_b.data_ptr<double>(), (int)nb, q, (int)iters,
                        (uint64_t)seed, out.data_ptr<double>(), cur_stream());
@@ -410,7 +410,7 @@ torch::Tensor rank_counts_py(torch::Tensor vals, int64_t nx) {
   check_dev(vals, torch::kFloat64, "vals");
   const int64_t n = vals.numel();
   if (nx < 0 || nx > n || n >= (1LL << 31)) throw std::invalid_argument("nx out of range");
-  c10::hip::HIPGuard guard(vals.device());
+  c10::hip::HIPGuard guard(vals.device().index());
   auto out = torch::empty({4, n}, vals.options().dtype(torch::kInt32));
   if (n) launch_rank_counts(vals.data_ptr<double>(), (int)n, (int)nx, dptr<uint32_t>(out), cur_stream());
   return out;
@@ -423,7 +423,7 @@ std::tuple<torch::Tensor, torch::Tensor> storm_counts_py(torch::Tensor keys, tor
   check_dev(ts, torch::kInt64, "ts");
   const int64_t n = keys.numel();
   if (ts.numel() != n || n >= (1LL << 31)) throw std::invalid_argument("keys/ts size mismatch");
-  c10::hip::HIPGuard guard(keys.device());
+  c10::hip::HIPGuard guard(keys.device().index());
   auto counts = torch::empty({n}, keys.options().dtype(torch::kInt32));
   auto tally = torch::zeros({1}, keys.options());
   launch_storm_counts(dptr<uint64_t>(keys), ts.data_ptr<int64_t>(), (int)n, window_ns, (uint32_t)threshold,

@@ -33,3 +33,61 @@ def pytest_collection_modifyitems(config, items):
 @pytest.fixture
 def fixtures_dir():
     return FIXTURES
+
+
+class _Recorder:
+    """Tiny local HTTP server (REF tests use httptest.NewServer): records requests and
+    answers with a scripted sequence of (status, body) responses."""
+
+    def __init__(self, responses=None):
+        import http.server
+        import threading
+
+        self.requests = []
+        self.responses = list(responses or [])
+        rec = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            def _handle(self):
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(n) if n else b""
+                rec.requests.append({"method": self.command, "path": self.path, "headers": dict(self.headers),
+                                     "body": body})
+                status, payload = rec.responses.pop(0) if rec.responses else (200, b"{}")
+                if callable(payload):
+                    payload = payload(self.path)
+                if isinstance(payload, str):
+                    payload = payload.encode()
+                self.send_response(status)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(payload)))
+                self.end_headers()
+                self.wfile.write(payload)
+
+            do_GET = do_POST = _handle
+
+            def log_message(self, *a):
+                pass
+
+        self.httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        self.url = f"http://127.0.0.1:{self.httpd.server_address[1]}"
+        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
+        self.thread.start()
+
+    def close(self):
+        self.httpd.shutdown()
+        self.httpd.server_close()
+
+
+@pytest.fixture
+def http_recorder():
+    made = []
+
+    def make(responses=None):
+        r = _Recorder(responses)
+        made.append(r)
+        return r
+
+    yield make
+    for r in made:
+        r.close()

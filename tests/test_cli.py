@@ -1,0 +1,171 @@
+"""Every CLI (REF cmd/*, which REF leaves untested) run in-process with REF flags."""
+
+import csv
+import json
+import os
+
+import pytest
+
+from llm_slo_ebpf_toolkit_amd.cli import agent, attributor, benchgen, collector, correlationeval, faultinject, \
+    faultreplay, loadgen, m5gate, schemavalidate, sloctl
+from llm_slo_ebpf_toolkit_amd.contracts import validator
+
+from conftest import FIXTURES, ROOT
+
+
+def read_jsonl(path):
+    with open(path) as fh:
+        return [json.loads(x) for x in fh if x.strip()]
+
+
+@pytest.mark.parametrize("mod", [agent, attributor, benchgen, collector, correlationeval, faultinject, faultreplay,
+                                 loadgen, m5gate, schemavalidate, sloctl])
+def test_version(mod, capsys):
+    assert mod.main(["--version"]) == 0
+    assert capsys.readouterr().out.strip()
+
+
+def test_faultreplay_and_attributor(tmp_path):
+    fx = tmp_path / "fs.jsonl"
+    assert faultreplay.main(["--scenario", "mixed", "--count", "14", "--out", str(fx), "--with-signals"]) == 0
+    out, summ, conf = tmp_path / "a.jsonl", tmp_path / "s.json", tmp_path / "c.csv"
+    assert attributor.main(["-input", str(fx), "-out", str(out), "--summary-out", str(summ), "--confusion-out",
+                            str(conf), "--config", str(tmp_path / "missing.yaml")]) == 0
+    rows = read_jsonl(out)
+    assert len(rows) == 14
+    for r in rows:
+        validator.validate("incident-attribution", r)
+    s = json.load(open(summ))
+    # with profile signals REF's table confuses provider_throttle/provider_error (the mf-04 effect)
+    assert s["total_samples"] == 14 and s["attribution_mode"] == "bayes" and s["accuracy"] >= 0.8
+    with open(conf) as fh:
+        assert next(csv.reader(fh)) == ["actual", "predicted", "count"]
+
+
+def test_attributor_ref_dataset_macro_f1(tmp_path):
+    summ = tmp_path / "s.json"
+    assert attributor.main(["--input", os.path.join(FIXTURES, "ref_multi_fault_samples.jsonl"), "--out",
+                            str(tmp_path / "o.jsonl"), "--summary-out", str(summ)]) == 0
+    s = json.load(open(summ))
+    assert s["accuracy"] == pytest.approx(0.5273, abs=1e-4)
+    assert s["single_fault_macro_f1"] == pytest.approx(0.9818, abs=1e-4)
+    assert s["partial_accuracy"] == pytest.approx(0.9818, abs=1e-4)
+
+
+def test_attributor_default_sample_rule_mode(capsys):
+    assert attributor.main(["--attribution-mode", "rule"]) == 0
+    row = json.loads(capsys.readouterr().out.strip())
+    assert row["predicted_fault_domain"] == "provider_throttle"
+
+
+def test_attributor_webhook_strict_failure(tmp_path, http_recorder):
+    srv = http_recorder([(400, "no")])
+    rc = attributor.main(["--out", str(tmp_path / "o.jsonl"), "--webhook-enabled", "--webhook-url", srv.url,
+                          "--webhook-strict"])
+    assert rc == 1 and len(srv.requests) == 1
+    assert attributor.main(["--out", str(tmp_path / "o.jsonl"), "--webhook-enabled", "--webhook-url", srv.url,
+                            "--webhook-format", "bogus"]) == 2
+
+
+def test_faultinject_and_collector(tmp_path):
+    raw = tmp_path / "raw.jsonl"
+    assert faultinject.main(["--scenario", "mixed", "--count", "6", "--out", str(raw)]) == 0
+    assert len(read_jsonl(raw)) == 6
+    out = tmp_path / "ev.jsonl"
+    assert collector.main(["--input", str(raw), "--output", "jsonl", "--output-path", str(out)]) == 0
+    evs = read_jsonl(out)
+    assert len(evs) == 24
+    for e in evs:
+        validator.validate("slo-event", e)
+
+
+def test_collector_synthetic_otlp(http_recorder, tmp_path):
+    srv = http_recorder()
+    empty = tmp_path / "empty.jsonl"
+    empty.write_text("")
+    assert collector.main(["--input", str(empty), "--output", "otlp", "--otlp-endpoint", srv.url + "/v1/logs",
+                           "--count", "3", "--scenario", "dns_latency"]) == 0
+    n = sum(len(json.loads(r["body"])["resourceLogs"][0]["scopeLogs"][0]["logRecords"]) for r in srv.requests)
+    assert n == 12
+
+
+def test_collector_bad_output_mode(tmp_path):
+    empty = tmp_path / "empty.jsonl"
+    empty.write_text("")
+    assert collector.main(["--input", str(empty), "--output", "carrier"]) == 1
+
+
+def test_benchgen(tmp_path):
+    assert benchgen.main(["--out", str(tmp_path / "b"), "--scenario", "mixed_faults", "--measure-seconds", "0.2"]) == 0
+    files = set(os.listdir(tmp_path / "b"))
+    for f in ("attribution_summary.json", "collector_overhead.csv", "confusion-matrix.csv"):
+        assert f in files, files
+
+
+def test_correlationeval(tmp_path):
+    out, pred = tmp_path / "s.json", tmp_path / "p.csv"
+    assert correlationeval.main(["--input", os.path.join(FIXTURES, "ref_labeled_pairs.jsonl"), "--out", str(out),
+                                 "--predictions-out", str(pred)]) == 0
+    s = json.load(open(out))
+    assert s["precision"] == 1.0 and s["recall"] == 1.0 and s["sample_size"] == 55 and s["passed_gate"]
+    with open(pred) as fh:
+        rows = list(csv.reader(fh))
+    assert rows[0][0] == "case_id" and len(rows) == 56
+    assert correlationeval.main(["--input", os.path.join(FIXTURES, "ref_labeled_pairs.jsonl"), "--out", str(out),
+                                 "--predictions-out", str(pred), "--min-precision", "1.01"]) == 1
+
+
+def test_m5gate(tmp_path):
+    from test_releasegate import populate
+
+    cand, base = populate(tmp_path)
+    js, md = tmp_path / "g.json", tmp_path / "g.md"
+    assert m5gate.main(["--candidate-root", cand, "--baseline-root", base, "--scenarios", "dns_latency",
+                        "--out-json", str(js), "--out-md", str(md)]) == 0
+    assert json.load(open(js))["pass"] and "M5 Gate Summary" in md.read_text()
+    assert m5gate.main(["--candidate-root", cand, "--baseline-root", base, "--scenarios", "dns_latency",
+                        "--max-overhead-pct", "1", "--out-json", str(js), "--out-md", str(md)]) == 1
+
+
+def test_loadgen(tmp_path):
+    out = tmp_path / "req.jsonl"
+    assert loadgen.main(["--profile", "chat_short", "--duration-sec", "2", "--rps", "5", "--out", str(out)]) == 0
+    rows = read_jsonl(out)
+    assert len(rows) == 10 and rows[3]["request_id"] == "req-000003"
+    assert all(r["prompt_class"] == "chat_short" and 80 <= r["expected_ttft_ms"] < 150 for r in rows)
+    assert all(2 <= r["retrieval_docs"] <= 9 and 64 <= r["target_tokens"] < 576 for r in rows)
+    assert loadgen.main(["--rps", "0", "--out", str(out)]) == 1
+
+
+def test_schemavalidate(capsys, monkeypatch):
+    monkeypatch.chdir(ROOT)
+    assert schemavalidate.main([]) == 0
+    assert capsys.readouterr().out.count("ok:") == 4
+
+
+def test_sloctl(capsys, http_recorder):
+    assert sloctl.main([]) == 2
+    assert sloctl.main(["bogus"]) == 2
+    capsys.readouterr()
+    rc = sloctl.main(["prereq", "check", "--output", "json"])
+    rep = json.loads(capsys.readouterr().out)
+    assert rc in (0, 1) and {c["name"] for c in rep["checks"]} >= {"host_linux", "gpu_gfx950", "rccl_library"}
+    ok = json.dumps({"status": "success", "data": {"resultType": "vector", "result": [{"value": [1, "0.01"]}]}})
+    srv = http_recorder([(200, ok)] * 3)
+    assert sloctl.main(["cdgate", "check", "--prometheus-url", srv.url, "--output", "json"]) == 0
+    srv2 = http_recorder([(500, "x")])
+    assert sloctl.main(["cdgate", "check", "--prometheus-url", srv2.url, "--fail-open=false"]) == 1
+    srv3 = http_recorder([(500, "x")])
+    assert sloctl.main(["cdgate", "check", "--prometheus-url", srv3.url, "--fail-open"]) == 0
+
+
+def test_agent_synthetic_count(tmp_path):
+    out = tmp_path / "agent.jsonl"
+    assert agent.main(["--count", "3", "--event-kind", "both", "--output", "jsonl", "--output-path", str(out),
+                       "--metrics-bind", "", "--scenario", "dns_latency", "--config",
+                       os.path.join(ROOT, "config", "toolkit.yaml")]) == 0
+    rows = read_jsonl(out)
+    slo = [r for r in rows if "sli_name" in r]
+    probe = [r for r in rows if "signal" in r]
+    assert len(slo) == 12 and len(probe) == 3 * 9
+    assert agent.main(["--event-kind", "weird", "--metrics-bind", ""]) == 1

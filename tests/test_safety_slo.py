@@ -1,0 +1,103 @@
+"""Safety (REF pkg/safety/*_test.go), SLO math (REF pkg/slo/calculator_test.go), prereq."""
+
+import pytest
+
+from llm_slo_ebpf_toolkit_amd.evaluation import prereq, slo
+from llm_slo_ebpf_toolkit_amd.safety import CPUSample, OverheadGuard, RateLimiter, TokenBucket
+from llm_slo_ebpf_toolkit_amd.utils.timeutil import MS, SECOND
+
+
+def test_rate_limiter_allow():
+    lim = RateLimiter(2)
+    base = 100 * SECOND
+    assert lim.allow(base)
+    assert lim.allow(base + 100 * MS)
+    assert not lim.allow(base + 200 * MS)
+    assert lim.allow(base + 1200 * MS)
+
+
+class FakeSampler:
+    def __init__(self, samples):
+        self.samples, self.i = samples, 0
+
+    def sample(self):
+        s = self.samples[min(self.i, len(self.samples) - 1)]
+        self.i += 1
+        return s
+
+
+def test_overhead_guard_evaluate():
+    g = OverheadGuard(5, FakeSampler([CPUSample(100, 10_000), CPUSample(220, 10_800)]), ncpu=8)
+    assert g.evaluate() == (0.0, False)
+    pct, hit = g.evaluate()
+    assert pct == pytest.approx(120 / 800 * 100 * 8)
+    assert hit
+
+
+def test_token_bucket():
+    tb = TokenBucket(rate=10, burst=5)
+    t = 1000 * SECOND
+    assert all(tb.allow(1, t) for _ in range(5))
+    assert not tb.allow(1, t)
+    assert tb.allow(1, t + SECOND // 10)
+
+
+def test_ttft_and_tps():
+    assert slo.ttft_ms(1, 1 + 175 * MS) == 175
+    assert slo.tokens_per_second(SECOND, 3 * SECOND, 40) == pytest.approx(20)
+    with pytest.raises(ValueError):
+        slo.calculate(slo.Timing(), slo.RetrievalBreakdown())
+
+
+def test_aggregate():
+    items = [slo.Snapshot(100, 50, slo.RetrievalBreakdown(20, 10, 5)),
+             slo.Snapshot(200, 30, slo.RetrievalBreakdown(40, 15, 10)),
+             slo.Snapshot(300, 10, slo.RetrievalBreakdown(60, 25, 15))]
+    out = slo.aggregate(items)
+    assert out.ttft_p50 == 200 and out.tokens_per_s_p50 == 30 and out.retrieval_p95_ms > 0
+
+
+def test_histogram_quantile_le_semantics():
+    # 10 obs in (0,1], 10 in (1,2]: p50 at the first bucket's upper edge
+    q = slo.histogram_quantile(0.5, [1, 2, float("inf")], [10, 20, 20])
+    assert q == pytest.approx(1.0)
+
+
+@pytest.mark.parametrize("rel,exp", [("6.8.0-31-generic", (6, 8)), ("5.15.0", (5, 15)), ("4.19.112", (4, 19))])
+def test_parse_kernel_release(rel, exp):
+    assert prereq.parse_kernel_release(rel) == exp
+
+
+def test_parse_kernel_release_invalid():
+    with pytest.raises(ValueError):
+        prereq.parse_kernel_release("garbage")
+
+
+def _snap(**kw):
+    s = prereq.Snapshot(host_os="linux", host_arch="x86_64", kernel_release="6.8.0", has_btf=True,
+                        has_kernel_hdrs=True, has_bpftool=True, has_clang=True, has_kind=True, has_helm=True,
+                        is_root=True, has_hipcc=True, has_kfd=True, gfx_targets=["gfx950"], has_rccl=True,
+                        has_rocprofiler_sdk=True)
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def test_evaluate_blockers_and_strict():
+    assert prereq.evaluate(_snap()).pass_ and prereq.strict_pass(prereq.evaluate(_snap()))
+    r = prereq.evaluate(_snap(kernel_release="5.10.0"))
+    assert not r.pass_
+    r = prereq.evaluate(_snap(has_kind=False))  # warning only
+    assert r.pass_ and not prereq.strict_pass(r)
+    r = prereq.evaluate(_snap(has_kfd=False, gfx_targets=[]))
+    assert r.pass_
+    assert not prereq.evaluate(_snap(has_kfd=False), require_gpu=True).pass_
+
+
+def test_kfd_topology_parse(tmp_path):
+    d = tmp_path / "1"
+    d.mkdir()
+    (d / "properties").write_text("cpu_cores_count 0\ngfx_target_version 90500\n")
+    (tmp_path / "0").mkdir()
+    (tmp_path / "0" / "properties").write_text("cpu_cores_count 64\ngfx_target_version 0\n")
+    assert prereq.kfd_gfx_targets(str(tmp_path)) == ["gfx950"]
