@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--paced-windows", type=int, default=3,
                     help="windows replayed at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
+                    help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
     ap.add_argument("--wire", type=int, default=32, choices=(32, 64),
                     help="event record bytes on PCIe: 32 = compact (interned ids), 64 = full")
     ap.add_argument("--out", default="")
@@ -94,7 +96,8 @@ def main() -> int:
                            wire=a.wire, interner=interner) for w in wins]
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
-    pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed)
+    pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
+                          group_scope=a.group_scope)
 
     def run(n, start):
         for i in range(n):

@@ -345,7 +345,7 @@ class Agent:
 
     # ---- GPU window engine ----------------------------------------------------------------
     def _window_source(self) -> Iterator:
-        """Yields (events, spans, n_groups, group_names) per window."""
+        """Yields (StagedWindow, group_names, t0_ns) per window."""
         o = self.o
         if o.source == "replay":
             from ..pipeline.replay import ReplayConfig, ReplayGenerator
@@ -354,17 +354,33 @@ class Agent:
                                                events_per_window=o.window_events, spans_per_window=o.window_spans,
                                                n_services=o.window_groups, window_ms=o.window_ms))
             # The replay producer stands in for the BPF / rocprofiler producers, which run
-            # outside the agent: pre-generate a few windows and cycle them so the agent's
-            # overhead guard measures the agent, not the synthetic trace generator.
-            pool = [gen.next_window() for _ in range(4)]
+            # outside the agent and write records in the wire format: pre-generate and
+            # pre-stage a few windows and cycle them, so the agent's overhead guard
+            # measures the agent, not the synthetic trace generator.
+            import torch
+
+            from ..collector.records import ConnInterner
+            from ..pipeline.window import stage_window
+
+            it = ConnInterner()
+            pool = []
+            for _ in range(4):
+                w = gen.next_window()
+                pool.append(stage_window(torch, w.events, w.spans, min(w.n_groups, o.window_groups), None,
+                                         o.window_groups, None, wire=o.wire, interner=it))
+            names = [f"svc-{g + 1}" for g in range(o.window_groups)]
             i = 0
             while True:
-                w = pool[i % len(pool)]
+                yield pool[i % len(pool)], names, now_ns()
                 i += 1
-                yield w.events, w.spans, w.n_groups, [f"svc-{g + 1}" for g in range(w.n_groups)], now_ns()
         elif o.source == "ring":
-            yield from RingSource(o.ring_name, o.window_events, o.window_spans).windows(o.window_ms, self.stop_event,
-                                                                                        o.window_groups)
+            import torch
+
+            from ..pipeline.window import stage_window
+
+            src = RingSource(o.ring_name, o.window_events, o.window_spans)
+            for ev, sp, n_groups, names, t0 in src.windows(o.window_ms, self.stop_event, o.window_groups):
+                yield stage_window(torch, ev, sp, n_groups, None, o.window_groups, None, wire=64), names, t0
         else:
             raise ValueError(f"unknown window source {o.source!r}")
 
@@ -392,14 +408,12 @@ class Agent:
         """GPU engine main loop (one process per MI355X; ``process_group`` = RCCL node group)."""
         import torch
 
-        from ..pipeline.window import WindowPipeline, stage_window
-        from ..collector.records import ConnInterner
+        from ..pipeline.window import WindowPipeline
 
         o = self.o
         torch.cuda.set_device(o.device)
         pipe = WindowPipeline(o.window_events, o.window_spans, o.window_groups, o.device, process_group,
                               model=o.model, learn=False)
-        interner = ConnInterner()
         source = self._window_source()
         first = next(source)  # producer warm-up happens before the guard's first sample
         if self.guard is not None:
@@ -409,13 +423,10 @@ class Agent:
         nxt = time.monotonic()
         import itertools
 
-        for events, spans, n_groups, names, t0 in itertools.chain([first], source):
+        for w, names, t0 in itertools.chain([first], source):
             if self.stop_event.is_set():
                 break
             t_start = time.perf_counter()
-            n_groups = min(n_groups, o.window_groups)
-            w = stage_window(torch, events, spans, n_groups, None, o.window_groups, None, wire=o.wire,
-                             interner=interner)
             pipe.submit(w, with_labels=False)
             pipe.drain()
             e = pipe.eng
@@ -423,7 +434,7 @@ class Agent:
             lat_ms = 1e3 * (time.perf_counter() - t_start)
             self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], w.n_events, lat_ms, o.node, o.pod,
                                         o.namespace)
-            G = n_groups
+            G = w.n_groups
             post = e.post[:G].cpu().numpy()
             pred = e.pred[:G].cpu().numpy()
             bits = e.evbits[:G].cpu().numpy().view(np.uint32)

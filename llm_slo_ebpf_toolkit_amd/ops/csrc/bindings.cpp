@@ -342,6 +342,22 @@ class Engine {
     pack();
   }
 
+  // Global incident scope, split at the group-sum all-reduce (parallel/__init__.py):
+  //   run_window_pre -> all_reduce(gsum), all_reduce(gcnt) -> run_window_post
+  void run_window_pre(torch::Tensor events, torch::Tensor spans, int64_t n_groups, int64_t wire) {
+    reset_window();
+    if (wire == 32) decode_compact(events); else decode(events);
+    join(spans, n_groups, c10::nullopt);
+  }
+
+  void run_window_post(int64_t n_groups, bool with_labels, bool learn) {
+    if (n_groups > group_cap_) throw std::invalid_argument("n_groups exceeds group capacity");
+    launch_group_features((int)n_groups, dptr<float>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat), cur_stream());
+    posterior(with_labels);
+    if (learn) accumulate_stats(c10::nullopt);
+    pack();
+  }
+
   int64_t sig_cap() const { return sig_cap_; }
   int64_t span_cap() const { return span_cap_; }
   int64_t group_cap() const { return group_cap_; }
@@ -464,6 +480,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("pack", &Engine::pack)
       .def("run_window", &Engine::run_window, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
            py::arg("with_labels") = true, py::arg("learn") = false, py::arg("wire") = 64)
+      .def("run_window_pre", &Engine::run_window_pre, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
+           py::arg("wire") = 64)
+      .def("run_window_post", &Engine::run_window_post, py::arg("n_groups"), py::arg("with_labels") = true,
+           py::arg("learn") = false)
       .def_property_readonly("sig_cap", &Engine::sig_cap)
       .def_property_readonly("span_cap", &Engine::span_cap)
       .def_property_readonly("group_cap", &Engine::group_cap)

@@ -50,9 +50,9 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
                                            uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
                                            uint64_t conn_h, const DecodeOut& o, uint32_t* s_hist,
                                            uint32_t* s_status, uint32_t* s_part, unsigned long long* s_sum,
-                                           int& unsupported, int& zero_ts) {
+                                           int& unsupported, int& zero_ts, bool local) {
   uint8_t st = 0;
-  if (slot >= 0) {
+  if (slot >= 0 && local) {
     st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
     // bucket = number of finite edges strictly below val ("le" semantics: val <= edge[b])
     int b = 0;
@@ -63,7 +63,9 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
     // exact, order-independent integer sum (values are >= 0 by construction)
     const double milli = rint((double)val * 1000.0);
     if (milli > 0.0) atomicAdd(&s_sum[slot], (unsigned long long)milli);
-  } else {
+  } else if (slot >= 0) {
+    st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
+  } else if (local) {
     ++unsupported;
   }
   o.cols.ts[i] = ts;
@@ -78,7 +80,7 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
   // Unsupported signal types never reach Match (REF correlator.go:73-77), and a zero
   // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
   const bool joinable = slot >= 0 && ts != 0;
-  if (ts == 0) ++zero_ts;
+  if (ts == 0 && local) ++zero_ts;
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
     uint64_t h = joinable ? key_hash(k, trace_h, pod, pid, conn_h, svcnode) : 0ull;
@@ -101,6 +103,9 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
   __syncthreads();
 
   const int n = min(*n_ptr, cap);
+  // counts[3] = number of node-local events; events past it are imported halo / remote
+  // trace-tagged copies that take part in the join but not in the window's counters.
+  const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
     const uint64_t ch = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
     const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
     decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status,
-               s_part, s_sum, unsupported, zero_ts);
+               s_part, s_sum, unsupported, zero_ts, i < n_local);
   }
   __syncthreads();
   flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
@@ -148,6 +153,9 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
   __syncthreads();
 
   const int n = min(*n_ptr, cap);
+  // counts[3] = number of node-local events; events past it are imported halo / remote
+  // trace-tagged copies that take part in the join but not in the window's counters.
+  const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0;
@@ -159,7 +167,7 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
     const uint64_t ch = (uint64_t)(e.type_conn >> 8);
     const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
     decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status, s_part,
-               s_sum, unsupported, zero_ts);
+               s_sum, unsupported, zero_ts, i < n_local);
   }
   __syncthreads();
   flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
@@ -192,6 +200,9 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
   for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
   __syncthreads();
   const int n = min(*n_ptr, cap);
+  // counts[3] = number of node-local events; events past it are imported halo / remote
+  // trace-tagged copies that take part in the join but not in the window's counters.
+  const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0;
@@ -204,7 +215,7 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
     else val = (float)((double)e.value_ns / 1e6);               // ns -> ms
     const uint64_t ch = conn_hash(e.conn_src_port, e.conn_dst_port, e.conn_dst_ip);
     decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, s_hist,
-               s_status, s_part, s_sum, unsupported, zero_ts);
+               s_status, s_part, s_sum, unsupported, zero_ts, i < n_local);
   }
   __syncthreads();
   flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
@@ -226,9 +237,7 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp, const int* __restrict__ n_ptr,
                                                      int cap, SpanCols c, uint32_t* part_cnt) {
   __shared__ uint32_t s_part[kKeyTypes * kParts];
-  __shared__ unsigned long long s_sum[kSlots];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
-  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
   __syncthreads();
   const int n = min(*n_ptr, cap);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;

@@ -503,4 +503,12 @@ void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* 
   }
 }
 
+// Incident features from (possibly all-reduced) per-group sums: the second half of a
+// window in global incident scope (parallel/__init__.py).
+void launch_group_features(int n_groups, const float* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream) {
+  if (n_groups <= 0) return;
+  const int n = n_groups * kSlots;
+  hipLaunchKernelGGL(k_group_features, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt, feat);
+}
+
 }  // namespace mislo

@@ -49,6 +49,8 @@ void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* 
                      float* attrs, float* conf, float* kernel_ms, int n_groups, float* gsum, uint32_t* gcnt,
                      float* feat, unsigned long long* dbg, hipStream_t stream);
 
+void launch_group_features(int n_groups, const float* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream);
+
 // posterior.hip
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                       double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,

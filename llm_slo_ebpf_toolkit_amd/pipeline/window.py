@@ -74,7 +74,8 @@ class StagedWindow:
 
 
 def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
-                 group_cap: int, group_domains=None, wire: int = 64, interner=None) -> StagedWindow:
+                 group_cap: int, group_domains=None, wire: int = 64, interner=None,
+                 n_local: Optional[int] = None) -> StagedWindow:
     """Pin a window for DMA. ``wire=32`` converts 64-byte events to the compact 32-byte
     record (interned conn ids, milli-unit values; collector/records.py EVENT32), halving
     the PCIe bytes that bound the pipeline; spans get the same interned conn ids."""
@@ -90,7 +91,10 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
         raise ValueError("wire must be 64 or 32")
     ev = torch.from_numpy(events.view(np.uint8).reshape(-1).copy()).pin_memory()
     sp = torch.from_numpy(spans.view(np.uint8).reshape(-1).copy()).pin_memory()
-    counts = torch.tensor([events.shape[0], spans.shape[0], n_groups, 0], dtype=torch.int32).pin_memory()
+    # counts[3] = node-local events; events[n_local:] are imported halo / remote-trace
+    # records that join but are not counted (decode kernels, parallel/exchange.py)
+    nl = 0 if n_local is None or n_local >= events.shape[0] else int(n_local)
+    counts = torch.tensor([events.shape[0], spans.shape[0], n_groups, nl], dtype=torch.int32).pin_memory()
     lab = np.full(group_cap, -1, dtype=np.int32)
     if labels is not None:
         lab[: len(labels)] = labels
@@ -102,7 +106,7 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
 class WindowPipeline:
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, process_group=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
-                 fanout: int = 3, group_mode: int = 1, learn: bool = True):
+                 fanout: int = 3, group_mode: int = 1, learn: bool = True, group_scope: str = "rank"):
         import torch
 
         self.torch = torch
@@ -111,6 +115,11 @@ class WindowPipeline:
         self.model_name = model
         self.seed = seed
         self.learn = learn
+        if group_scope not in ("rank", "global"):
+            raise ValueError("group_scope must be 'rank' or 'global'")
+        # "rank": incident groups are per-GPU (each node's services); "global": groups span
+        # GPUs and are scored on all-reduced per-group sums (a second, G x 16 collective)
+        self.group_scope = group_scope
         self.engine = GpuEngine(sig_cap, span_cap, group_cap, device, window_ms, threshold, fanout, group_mode)
         self.eng = self.engine.eng
         L = int(self.engine.mod.PACKET_LEN)
@@ -134,6 +143,7 @@ class WindowPipeline:
             self.h2d_done = [ev(), ev()]
             self.compute_done = [ev(), ev()]
             self.comm_done = [ev(), ev()]
+            self.join_done, self.groups_done = ev(), ev()
         self.pod_key = None
         self.i = 0
         self.cum_stats = SufficientStats()
@@ -191,9 +201,25 @@ class WindowPipeline:
         ks.wait_event(self.comm_done[b])  # packet[b] no longer being reduced / read
         with torch.cuda.stream(ks):
             self.eng.bind_io(self.counts_dev[b], self.labels_dev[b], self.packet_dev[b])
-            self.eng.run_window(self.ev_dev[b], self.sp_dev[b], w.n_groups, with_labels,
-                                self.learn and with_labels, w.wire)
-            self.compute_done[b].record(ks)
+            if self.group_scope == "global" and self.pg is not None:
+                self.eng.run_window_pre(self.ev_dev[b], self.sp_dev[b], w.n_groups, w.wire)
+                self.join_done.record(ks)
+        if self.group_scope == "global" and self.pg is not None:
+            # group sums of this window across the node, then posterior on the global features
+            ms.wait_event(self.join_done)
+            with torch.cuda.stream(ms):
+                torch.distributed.all_reduce(self.eng.gsum[: w.n_groups], group=self.pg)
+                torch.distributed.all_reduce(self.eng.gcnt[: w.n_groups], group=self.pg)
+                self.groups_done.record(ms)
+            ks.wait_event(self.groups_done)
+            with torch.cuda.stream(ks):
+                self.eng.run_window_post(w.n_groups, with_labels, self.learn and with_labels)
+                self.compute_done[b].record(ks)
+        else:
+            with torch.cuda.stream(ks):
+                self.eng.run_window(self.ev_dev[b], self.sp_dev[b], w.n_groups, with_labels,
+                                    self.learn and with_labels, w.wire)
+                self.compute_done[b].record(ks)
         ms.wait_event(self.compute_done[b])
         with torch.cuda.stream(ms):
             if self.pg is not None:

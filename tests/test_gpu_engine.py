@@ -148,3 +148,34 @@ def test_compact_wire_matches_oracle(engine):
     for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
         assert out.debug[k] == ref.debug[k], k
     np.testing.assert_allclose(out.feat, ref.feat, rtol=2e-5, equal_nan=True)
+
+
+def test_split_pre_post_equals_run_window(engine):
+    """Global-incident-scope split (pre -> [group all-reduce] -> post) == one-shot window;
+    and n_local excludes imported records from the counters but not from the join."""
+    import torch
+
+    win = small_window(seed=13)
+    engine.set_join_params(2000.0, 0.7, 3, 1)
+    engine.set_model(NaiveBayes.ref())
+    out = engine.process(win.events, win.spans, win.n_groups, win.group_labels)
+    e = engine.eng
+    feat_a, post_a, pk_a = out.feat.copy(), out.post.copy(), e.packet.cpu().numpy().copy()
+    e.run_window_pre(engine.ev_dev, engine.sp_dev, win.n_groups, 64)
+    e.run_window_post(win.n_groups, True, False)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(e.feat[: win.n_groups].cpu().numpy(), feat_a)
+    np.testing.assert_array_equal(e.post[: win.n_groups].cpu().numpy(), post_a)
+    np.testing.assert_array_equal(e.packet.cpu().numpy(), pk_a)
+    # n_local: count only the first half of the events
+    half = win.n_events // 2
+    e.counts.copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, half], dtype=torch.int32))
+    e.run_window(engine.ev_dev, engine.sp_dev, win.n_groups, True, False, 64)
+    torch.cuda.synchronize()
+    d = oracle.decode_events(win.events[:half])
+    np.testing.assert_array_equal(e.hist.cpu().numpy().astype(np.int64), oracle.histograms(d))
+    np.testing.assert_array_equal(e.misc[2:18].cpu().numpy(), oracle.value_sums_milli(d))
+    top3 = e.top3[: 3 * win.n_spans].cpu().numpy().view(np.uint64).reshape(win.n_spans, 3)
+    ref = oracle.join(oracle.decode_events(win.events), win.spans, win.n_groups)
+    np.testing.assert_array_equal(top3, ref.top3)
+    e.counts.copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, 0], dtype=torch.int32))
