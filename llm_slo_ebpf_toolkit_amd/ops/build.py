@@ -4,6 +4,8 @@ Produces, next to the sources (so the .so travels with the repo snapshot to the 
 
 * ``ops/_mislo_hip<EXT_SUFFIX>``    -- torch extension: decode / join / posterior kernels
   and the ``Engine`` bindings (hipcc, --offload-arch=gfx950).
+* ``probes/rocprof/libmislo_rocprof.so`` -- rocprofiler-sdk tool library (GPU signals
+  from inside LLM workloads into the agent's shared-memory ring).
 * ``runtime/_mislo_rt<EXT_SUFFIX>`` -- native runtime (pinned MPSC ring, replay generator,
   gate statistics on the host) exposed through pybind11; also ``runtime/libmislo_rt.so``
   with a C ABI for external producers (BPF loader, rocprofiler-sdk tool).
@@ -129,9 +131,24 @@ def build_runtime(force: bool = False, jobs: int = 4) -> List[str]:
     return outs
 
 
+def build_rocprof_tool(force: bool = False) -> str:
+    """rocprofiler-sdk tool library (probes/rocprof): GPU signals -> shared-memory ring."""
+    src = os.path.join(PKG, "probes", "rocprof", "mislo_rocprof.cpp")
+    out = os.path.join(PKG, "probes", "rocprof", "libmislo_rocprof.so")
+    rt_dir = os.path.join(PKG, "runtime")
+    if force or _newer(out, [src, os.path.join(rt_dir, "libmislo_rt.so")]):
+        cxx = shutil.which("g++") or "c++"
+        _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", f"-I{ROCM}/include",
+              "-D__HIP_PLATFORM_AMD__=1", src, "-o", out,
+              f"-L{rt_dir}", "-lmislo_rt", "-Wl,-rpath,$ORIGIN/../../runtime", f"-L{ROCM}/lib", "-lrocprofiler-sdk",
+              f"-Wl,-rpath,{ROCM}/lib"])
+    return out
+
+
 def build_all(force: bool = False, jobs: int = 4) -> List[str]:
     outs = build_runtime(force, jobs)
     outs.append(build_hip_ext(force, jobs))
+    outs.append(build_rocprof_tool(force))
     return outs
 
 

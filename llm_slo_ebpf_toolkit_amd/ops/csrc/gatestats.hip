@@ -58,7 +58,8 @@ __global__ __launch_bounds__(NT) void k_boot_quantile(const double* __restrict__
   for (int w = 0; w < wave; ++w) base += s_wsum[w];
   uint32_t run = base + incl - local;  // exclusive prefix at chunk start
 
-  const double pos = __dmul_rn(q, (double)(n - 1));  // no FMA contraction into f below
+  double pos = q * (double)(n - 1);
+  asm volatile("" : "+v"(pos));  // keep the product rounded (no fma into pos - flo)
   const double flo = floor(pos), fhi = ceil(pos);
   const uint32_t r_lo = (uint32_t)flo, r_hi = (uint32_t)fhi;
   for (int i = beg; i < end; ++i) {
@@ -75,9 +76,12 @@ __global__ __launch_bounds__(NT) void k_boot_quantile(const double* __restrict__
     if (n == 1 || r_lo == r_hi) {
       r = s_val[0];
     } else {
-      const double f = __dsub_rn(pos, flo);
-      // no FMA contraction: matches numpy's  s_lo * (1 - f) + s_hi * f  bit for bit
-      r = __dadd_rn(__dmul_rn(s_val[0], __dsub_rn(1.0, f)), __dmul_rn(s_val[1], f));
+      const double f = pos - flo;
+      // Round each product separately (numpy's  s_lo * (1 - f) + s_hi * f): the empty asm
+      // makes the products opaque so the backend cannot fuse them into v_fmac_f64.
+      double a = s_val[0] * (1.0 - f), b = s_val[1] * f;
+      asm volatile("" : "+v"(a), "+v"(b));
+      r = a + b;
     }
     out[(size_t)set * iters + it] = r;
   }
