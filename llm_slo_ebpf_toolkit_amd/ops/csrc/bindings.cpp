@@ -128,7 +128,7 @@ class Engine {
     top3 = torch::empty({3 * S}, i64); cnt = torch::empty({S}, i32);
     attrs = torch::empty({S, kSlots}, f32); conf = torch::empty({S}, f32); kernel_ms = torch::empty({S}, f32);
     // groups / incidents
-    gsum = torch::empty({G, kSlots}, f32); gcnt = torch::empty({G, kSlots}, i32);
+    gsum = torch::empty({G, kSlots}, i64); gcnt = torch::empty({G, kSlots}, i32);
     feat = torch::empty({G, kSlots}, f32); labels = torch::full({G}, -1, i32);
     post = torch::empty({G, kMaxDomains}, f64); pred = torch::empty({G}, i32); gconf = torch::empty({G}, f64);
     evbits = torch::empty({G, kMaxDomains}, i32);
@@ -289,7 +289,7 @@ class Engine {
     // top3 / cnt / gsum / gcnt were reset by reset_window()
     launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(),
                  dptr<uint32_t>(g_items), dptr<uint32_t>(g_part_base), sig_cap_, span_cap_, jp_,
-                 dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<float>(gsum),
+                 dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<unsigned long long>(gsum),
                  dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), st);
     const float* base = nullptr;
     if (base_attrs.has_value()) {
@@ -300,7 +300,7 @@ class Engine {
     }
     launch_finalize(dptr<int>(counts) + 1, span_cap_, dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), sig_cols(),
                     span_cols(), jp_, base, dptr<float>(attrs), dptr<float>(conf), dptr<float>(kernel_ms),
-                    (int)n_groups, dptr<float>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat),
+                    (int)n_groups, dptr<unsigned long long>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat),
                     dptr<unsigned long long>(dbg), st);
   }
 
@@ -352,7 +352,7 @@ class Engine {
 
   void run_window_post(int64_t n_groups, bool with_labels, bool learn) {
     if (n_groups > group_cap_) throw std::invalid_argument("n_groups exceeds group capacity");
-    launch_group_features((int)n_groups, dptr<float>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat), cur_stream());
+    launch_group_features((int)n_groups, dptr<unsigned long long>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat), cur_stream());
     posterior(with_labels);
     if (learn) accumulate_stats(c10::nullopt);
     pack();

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
                                               const uint32_t* __restrict__ sig_items,
                                               const uint32_t* __restrict__ sig_base, int sig_cap, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
-                                              uint32_t* __restrict__ cnt, int n_groups, float* __restrict__ gsum,
+                                              uint32_t* __restrict__ cnt, int n_groups, unsigned long long* __restrict__ gsum,
                                               uint32_t* __restrict__ gcnt, unsigned long long* __restrict__ dbg) {
   __shared__ uint64_t s_h[kChunk];
   __shared__ int64_t s_t[kChunk];
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
   __shared__ uint32_t s_grp[kChunk];
   __shared__ unsigned long long s_top[kChunk * 3];
   __shared__ uint32_t s_cnt[kChunk];
-  __shared__ float s_gsum[kLdsGroups * kSlots];
+  __shared__ unsigned long long s_gsum[kLdsGroups * kSlots];
   __shared__ uint32_t s_gcnt[kLdsGroups * kSlots];
 
   const int k = blockIdx.y;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
 
   if (do_groups && grp_lds) {
     for (int i = threadIdx.x; i < kLdsGroups * kSlots; i += NT) {
-      s_gsum[i] = 0.f;
+      s_gsum[i] = 0ull;
       s_gcnt[i] = 0u;
     }
   }
@@ -281,6 +281,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       const uint64_t g_tr = gc.trace_h[g], g_cn = gc.conn_h[g];
       const int g_slot = gc.slot[g];
       const float g_val = gc.val[g];
+      const unsigned long long g_milli = milli_units(g_val);
       // incident sums: a signal's candidate spans share one key (pod / trace / svc+node),
       // hence one incident group -- accumulate (group, pair count) in registers and add
       // val x count once per run instead of once per pair (all lanes of a partition hit
@@ -319,10 +320,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
             if (grp != run_grp) {
               if (run_n && run_grp < (uint32_t)n_groups) {
                 if (grp_lds) {
-                  atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_val * (float)run_n);
+                  atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_milli * run_n);
                   atomicAdd(&s_gcnt[run_grp * kSlots + g_slot], run_n);
                 } else {
-                  atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_val * (float)run_n);
+                  atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_milli * run_n);
                   atomicAdd(gcnt + (size_t)run_grp * kSlots + g_slot, run_n);
                 }
               }
@@ -341,10 +342,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       }
       if (run_n && run_grp < (uint32_t)n_groups) {
         if (grp_lds) {
-          atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_val * (float)run_n);
+          atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_milli * run_n);
           atomicAdd(&s_gcnt[run_grp * kSlots + g_slot], run_n);
         } else {
-          atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_val * (float)run_n);
+          atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_milli * run_n);
           atomicAdd(gcnt + (size_t)run_grp * kSlots + g_slot, run_n);
         }
       }
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
                                                  JoinParams jp, const float* __restrict__ base_attrs,
                                                  float* __restrict__ attrs, float* __restrict__ conf,
                                                  float* __restrict__ kernel_ms, int n_groups,
-                                                 float* __restrict__ gsum, uint32_t* __restrict__ gcnt,
+                                                 unsigned long long* __restrict__ gsum, uint32_t* __restrict__ gcnt,
                                                  unsigned long long* __restrict__ dbg) {
   const int ns = min(*ns_ptr, span_cap);
   const int s = blockIdx.x * NT + threadIdx.x;
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
 #pragma unroll
       for (int j = 0; j < kSlots; ++j) {
         if (a[j] == a[j]) {
-          atomicAdd(gsum + (size_t)grp * kSlots + j, a[j]);
+          atomicAdd(gsum + (size_t)grp * kSlots + j, milli_units(a[j]));
           atomicAdd(gcnt + (size_t)grp * kSlots + j, 1u);
         }
       }
@@ -461,12 +462,14 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
   }
 }
 
-__global__ __launch_bounds__(256) void k_group_features(int n, const float* __restrict__ gsum,
+__global__ __launch_bounds__(256) void k_group_features(int n, const unsigned long long* __restrict__ gsum,
                                                         const uint32_t* __restrict__ gcnt, float* __restrict__ feat) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t c = gcnt[i];
-  feat[i] = c ? gsum[i] / (float)c : __builtin_nanf("");
+  // exact integer sums of milli-unit values: deterministic under any atomic order and
+  // associative across ranks (the group-sum all-reduce); oracle.join computes the same
+  feat[i] = c ? (float)(((double)gsum[i] * 1e-3) / (double)c) : __builtin_nanf("");
 }
 
 // ---------------------------------------------------------------------------------------
@@ -485,7 +488,7 @@ void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk,
 
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
-                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, float* gsum,
+                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
                   uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream) {
   hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes, kSplit), dim3(256), 0, stream, sc, span_items, span_base, gc,
                      sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg);
@@ -493,7 +496,7 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
                      const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,
-                     float* attrs, float* conf, float* kernel_ms, int n_groups, float* gsum, uint32_t* gcnt,
+                     float* attrs, float* conf, float* kernel_ms, int n_groups, unsigned long long* gsum, uint32_t* gcnt,
                      float* feat, unsigned long long* dbg, hipStream_t stream) {
   hipLaunchKernelGGL((k_finalize<256>), dim3((span_cap + 255) / 256), dim3(256), 0, stream, ns_dev, span_cap, top3,
                      cnt, gc, sc, jp, base_attrs, attrs, conf, kernel_ms, n_groups, gsum, gcnt, dbg);
@@ -505,7 +508,7 @@ void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* 
 
 // Incident features from (possibly all-reduced) per-group sums: the second half of a
 // window in global incident scope (parallel/__init__.py).
-void launch_group_features(int n_groups, const float* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream) {
+void launch_group_features(int n_groups, const unsigned long long* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream) {
   if (n_groups <= 0) return;
   const int n = n_groups * kSlots;
   hipLaunchKernelGGL(k_group_features, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt, feat);

@@ -159,6 +159,13 @@ __host__ __device__ inline uint64_t key_hash(int k, uint64_t trace_h, uint32_t p
   return h ? h : 1;
 }
 
+// Fixed-point (1/1000 unit) image of a non-negative value: incident-group sums are exact
+// integers, so they are deterministic and all-reduce associatively across GPUs.
+__host__ __device__ inline unsigned long long milli_units(float v) {
+  const double m = rint((double)v * 1000.0);
+  return m > 0.0 ? (unsigned long long)m : 0ull;
+}
+
 __host__ __device__ inline int part_of(uint64_t h) { return (int)(h >> (64 - kPartBits)); }
 
 }  // namespace mislo

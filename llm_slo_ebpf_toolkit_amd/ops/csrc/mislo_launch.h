@@ -42,14 +42,14 @@ void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk,
                       hipStream_t stream);
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
-                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, float* gsum,
+                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
                   uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream);
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
                      const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,
-                     float* attrs, float* conf, float* kernel_ms, int n_groups, float* gsum, uint32_t* gcnt,
+                     float* attrs, float* conf, float* kernel_ms, int n_groups, unsigned long long* gsum, uint32_t* gcnt,
                      float* feat, unsigned long long* dbg, hipStream_t stream);
 
-void launch_group_features(int n_groups, const float* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream);
+void launch_group_features(int n_groups, const unsigned long long* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream);
 
 // posterior.hip
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,

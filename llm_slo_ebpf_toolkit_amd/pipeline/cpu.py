@@ -91,8 +91,7 @@ class CpuWindowEngine:
         gsum, gcnt = j.gsum, j.gcnt
         if reduce_groups is not None:
             gsum, gcnt = reduce_groups(gsum, gcnt)
-        with np.errstate(invalid="ignore", divide="ignore"):
-            feat = np.where(gcnt > 0, gsum / np.maximum(gcnt, 1), np.nan)
+        feat = oracle.group_features(gsum, gcnt).astype(np.float64)
         post = self.model.posteriors(feat)
         pred = np.argmax(self.model.logits(feat), axis=1) if n_groups else np.zeros(0, dtype=np.int64)
         conf = np.zeros((16, 16), dtype=np.int64)

@@ -94,6 +94,18 @@ def histograms(d: Decoded) -> np.ndarray:
     return h
 
 
+def milli_units(v) -> np.ndarray:
+    """Fixed-point image used by the kernels for sums (mislo_common.h milli_units)."""
+    m = np.rint(np.asarray(v, dtype=np.float32).astype(np.float64) * 1000.0)
+    return np.where(m > 0, m, 0).astype(np.int64)
+
+
+def group_features(gsum: np.ndarray, gcnt: np.ndarray) -> np.ndarray:
+    """k_group_features: float((gsum * 1e-3) / gcnt) in double, NaN where no pairs."""
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return np.where(gcnt > 0, (gsum.astype(np.float64) * 1e-3) / np.maximum(gcnt, 1), np.nan).astype(np.float32)
+
+
 def value_sums_milli(d: Decoded) -> np.ndarray:
     """Per-slot exact integer sums of rint(val * 1000) (decode kernels' misc[2:18])."""
     out = np.zeros(16, dtype=np.int64)
@@ -110,7 +122,7 @@ class JoinResult:
     cnt: np.ndarray         # [S]
     attrs: np.ndarray       # float32 [S,16]
     conf: np.ndarray        # float32 [S]
-    gsum: np.ndarray        # float64 [G,16]
+    gsum: np.ndarray        # int64 [G,16] sums of milli-unit values (exact, order-free)
     gcnt: np.ndarray        # int64 [G,16]
     feat: np.ndarray        # float32 [G,16]
     debug: Dict[str, int]
@@ -133,7 +145,7 @@ def join(d: Decoded, spans: np.ndarray, n_groups: int, window_ms: float = 2000.0
     cnt = np.zeros(S, dtype=np.int64)
     attrs = np.full((S, 16), np.nan, dtype=np.float32)
     conf = np.zeros(S, dtype=np.float32)
-    gsum = np.zeros((n_groups, 16), dtype=np.float64)
+    gsum = np.zeros((n_groups, 16), dtype=np.int64)
     gcnt = np.zeros((n_groups, 16), dtype=np.int64)
     matched_total = low_total = dropped_total = 0
     sp_svcnode = (spans["svc_id"].astype(np.uint32) << np.uint32(16)) | spans["node_id"].astype(np.uint32)
@@ -182,15 +194,15 @@ def join(d: Decoded, spans: np.ndarray, n_groups: int, window_ms: float = 2000.0
             dropped_total += max(0, ci.size - fanout)
             grp = int(spans["group_id"][s])
             if group_mode == 1 and grp < n_groups:
-                np.add.at(gsum[grp], d.slot[ci].astype(np.int64), d.val[ci].astype(np.float64))
+                np.add.at(gsum[grp], d.slot[ci].astype(np.int64), milli_units(d.val[ci]))
                 np.add.at(gcnt[grp], d.slot[ci].astype(np.int64), 1)
         grp = int(spans["group_id"][s])
         if group_mode == 0 and grp < n_groups:
             p = ~np.isnan(attrs[s])
-            gsum[grp][p] += attrs[s][p]
+            gsum[grp][p] += milli_units(attrs[s][p])
             gcnt[grp][p] += 1
     with np.errstate(invalid="ignore", divide="ignore"):
-        feat = np.where(gcnt > 0, gsum / np.maximum(gcnt, 1), np.nan).astype(np.float32)
+        feat = group_features(gsum, gcnt)
     n_uns = N - n_sup
     debug = {
         "candidates": int(cnt.sum()), "low_confidence": low_total, "fanout_dropped": dropped_total,

@@ -51,7 +51,9 @@ def test_decode_join_matches_oracle(engine, group_mode):
     np.testing.assert_array_equal(e.conf[:S].cpu().numpy(), ref.conf)
     for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
         assert out.debug[k] == ref.debug[k], k
-    np.testing.assert_allclose(out.feat, ref.feat, rtol=2e-5, equal_nan=True)
+    np.testing.assert_array_equal(e.gsum[: win.n_groups].cpu().numpy(), ref.gsum)
+    np.testing.assert_array_equal(e.gcnt[: win.n_groups].cpu().numpy(), ref.gcnt)
+    np.testing.assert_array_equal(out.feat, ref.feat)
 
 
 def test_low_threshold_enumerates_service_node_tier(engine):
@@ -147,7 +149,9 @@ def test_compact_wire_matches_oracle(engine):
     np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
     for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
         assert out.debug[k] == ref.debug[k], k
-    np.testing.assert_allclose(out.feat, ref.feat, rtol=2e-5, equal_nan=True)
+    np.testing.assert_array_equal(e.gsum[: win.n_groups].cpu().numpy(), ref.gsum)
+    np.testing.assert_array_equal(e.gcnt[: win.n_groups].cpu().numpy(), ref.gcnt)
+    np.testing.assert_array_equal(out.feat, ref.feat)
 
 
 def test_split_pre_post_equals_run_window(engine):
