@@ -37,5 +37,5 @@ def test_every_signal_has_a_producer():
             continue
         src = open(os.path.join(EBPF_DIR, obj + ".bpf.c")).read()
         for p in progs:
-            assert re.search(rf"\b{p}\b\s*[(,]", src), (sig, obj, p)
+            assert re.search(rf"\b{p}\b\s*[(,)]", src), (sig, obj, p)
         assert 'SEC("license")' in src
