@@ -4,6 +4,8 @@
   sloctl cdgate check [--config PATH] [--prometheus-url URL] [--ttft-p95-ms N]
                       [--error-rate N] [--burn-rate N] [--fail-open] [--output text|json] [--timeout S]
   sloctl schema export [--root DIR]        (additive: regenerate the contract files)
+  sloctl lab run [--scenario NAME,...] [--dir DIR] [--device auto|cpu|gpu] [--out FILE]
+                                           (additive: execute incident-lab scenarios)
 """
 
 from __future__ import annotations
@@ -23,7 +25,8 @@ from ._common import GoFlags, eprint, is_version_request, print_version
 USAGE = """Usage:
   sloctl prereq check [--output text|json] [--strict] [--require-gpu]
   sloctl cdgate check [--config PATH] [--prometheus-url URL] [--ttft-p95-ms N] [--error-rate N] [--burn-rate N] [--fail-open] [--output text|json]
-  sloctl schema export [--root DIR]"""
+  sloctl schema export [--root DIR]
+  sloctl lab run [--scenario NAME,...] [--dir DIR] [--device auto|cpu|gpu] [--out FILE]"""
 
 CDGATE_USAGE = """Usage:
   sloctl cdgate check [flags]
@@ -116,6 +119,30 @@ def schema_export(args: List[str]) -> int:
     return 0
 
 
+def lab_run(args: List[str]) -> int:
+    from ..evaluation import incidentlab
+    from ._common import split_csv, write_json
+
+    p = GoFlags("sloctl lab run")
+    p.flag("scenario", "", "comma-separated scenario names (default: all)")
+    p.flag("dir", incidentlab.SCENARIO_DIR, "scenario directory")
+    p.flag("device", "auto", "engine device: auto|cpu|gpu")
+    p.flag("out", "", "write the JSON report here")
+    a = p.parse_args(args)
+    reports = incidentlab.run_all(a.dir, a.device, split_csv(a.scenario) or None)
+    if not reports:
+        eprint("no scenarios matched")
+        return 2
+    for r in reports:
+        print(f"[{'PASS' if r['pass'] else 'FAIL'}] {r['scenario']} (engine={r['engine']})")
+        for c in r["assertions"]:
+            act = "n/a" if c["actual"] is None else f"{c['actual']:.4f}"
+            print(f"    {'ok ' if c['pass'] else 'BAD'} {c['phase']}: {c['metric']} {c['op']} {c['value']} (actual {act})")
+    if a.out:
+        write_json(a.out, reports)
+    return 0 if all(r["pass"] for r in reports) else 1
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     if not argv:
@@ -127,7 +154,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     if cmd in ("help", "-h", "--help"):
         print(USAGE)
         return 0
-    table = {"prereq": {"check": prereq_check}, "cdgate": {"check": cdgate_check}, "schema": {"export": schema_export}}
+    table = {"prereq": {"check": prereq_check}, "cdgate": {"check": cdgate_check}, "schema": {"export": schema_export},
+             "lab": {"run": lab_run}}
     if cmd not in table:
         eprint(f'unknown command "{cmd}"')
         print(USAGE)
