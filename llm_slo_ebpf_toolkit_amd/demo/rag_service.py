@@ -1,0 +1,387 @@
+"""Demo RAG chat service (REF demo/rag-service/main.go, re-built in Python).
+
+``POST /chat`` {"prompt", "profile", "seed", "max_tokens", "stream", "request_id"}:
+
+1. a deterministic retrieval plan per (profile, prompt, seed) -- DNS, network and vector-DB
+   waits, documents from ``fixtures/corpus.json``;
+2. span ``chat.retrieval`` with ``llm.slo.retrieval.*`` attributes, DNS enrichment of the
+   request span through the correlator (tier + confidence -> ``llm_slo_correlation_total``);
+3. span ``chat.generation`` from the backend: ``stub`` (seeded token list, paced) or
+   ``llama`` (the random-init Llama on the local MI355X: real prefill + decode, so TTFT
+   carries GPU queueing / HBM / RCCL effects);
+4. streaming NDJSON (``{"token": ...}`` lines then a summary) or one JSON document.
+
+Prometheus on ``--metrics-bind``: ``llm_slo_ttft_ms``, ``llm_slo_tokens_per_sec``,
+``llm_slo_retrieval_{vectordb,network,dns}_ms`` histograms, ``llm_slo_requests_total``,
+``llm_slo_correlation_total`` -- and, closing a REF gap (the cdgate queries
+reference series nobody emitted), ``llm_slo_errors_total`` and ``llm_slo_burn_rate``
+(error-budget burn over a sliding window against a 99 % objective).
+Traces: OTLP/HTTP JSON (``/v1/traces``) when ``--otlp-endpoint`` is set, batched.
+"""
+
+from __future__ import annotations
+
+import argparse
+import collections
+import hashlib
+import http.server
+import json
+import os
+import random
+import sys
+import threading
+import time
+import urllib.request
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+from ..contracts import semconv
+from ..correlation.correlator import Correlator
+from ..correlation.match import SignalRef, SpanRef
+from ..export.prometheus import MetricsServer, Registry
+from ..utils.timeutil import MS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+VOCAB = ("reliability", "signal", "trace", "kernel", "latency", "attribution", "dns", "retrieval", "throughput",
+         "incident", "confidence", "evidence", "burn", "slo", "token", "scheduler", "gpu", "xgmi")
+
+
+@dataclass
+class Plan:
+    dns_ms: float
+    network_ms: float
+    vectordb_ms: float
+    warmup_ms: int
+    cadence_ms: int
+    docs: int
+
+
+def prompt_hash(prompt: str) -> int:
+    return int.from_bytes(hashlib.blake2b(prompt.encode(), digest_size=4).digest(), "little")
+
+
+def plan_for(profile: str, prompt: str, seed: int) -> Plan:
+    """Same ranges per profile as REF planForRequest (demo/rag-service/main.go:673-707)."""
+    r = random.Random(seed + prompt_hash(prompt))
+    if profile == "chat_short":
+        return Plan(2 + r.randrange(4), 4 + r.randrange(8), 10 + r.randrange(20), 25 + r.randrange(15),
+                    25 + r.randrange(10), 2 + r.randrange(2))
+    if profile == "context_long":
+        return Plan(8 + r.randrange(8), 15 + r.randrange(20), 70 + r.randrange(80), 50 + r.randrange(30),
+                    45 + r.randrange(20), 4 + r.randrange(2))
+    return Plan(5 + r.randrange(8), 10 + r.randrange(14), 35 + r.randrange(45), 30 + r.randrange(20),
+                30 + r.randrange(15), 3 + r.randrange(2))
+
+
+def stub_tokens(prompt: str, max_tokens: int, seed: int) -> List[str]:
+    max_tokens = min(max(1, max_tokens), 256)
+    r = random.Random(seed + prompt_hash(prompt))
+    out = [t for t in prompt.split() if t.strip()][:max_tokens]
+    while len(out) < max_tokens:
+        out.append(VOCAB[r.randrange(len(VOCAB))])
+    return out
+
+
+class StubBackend:
+    name = "stub"
+
+    def generate(self, prompt: str, max_tokens: int, seed: int, plan: Plan, emit) -> Dict[str, float]:
+        toks = stub_tokens(prompt, max_tokens, seed)
+        t0 = time.perf_counter()
+        time.sleep(plan.warmup_ms / 1000.0)
+        ttft = time.perf_counter() - t0
+        for i, t in enumerate(toks):
+            if i:
+                time.sleep(plan.cadence_ms / 1000.0)
+            emit(t)
+        total = time.perf_counter() - t0
+        return {"ttft_s": ttft, "total_s": total, "tokens": len(toks)}
+
+
+class LlamaBackend:
+    """Random-init Llama on the local GPU; token ids are rendered as vocabulary words."""
+    name = "llama"
+
+    def __init__(self, preset: str = "1b", device: str = "cuda"):
+        import torch
+
+        from ..models.llama import build
+
+        self.torch = torch
+        self.model = build(preset, device)
+        self.lock = threading.Lock()
+        self.device = device
+
+    def generate(self, prompt: str, max_tokens: int, seed: int, plan: Plan, emit) -> Dict[str, float]:
+        torch = self.torch
+        ids = [prompt_hash(w) % self.model.cfg.vocab for w in prompt.split()] or [1]
+        x = torch.tensor([ids], device=self.device)
+        with self.lock:  # one request on the GPU at a time (the demo is latency-oriented)
+            r = self.model.generate(x, max(1, min(max_tokens, 256)),
+                                    on_token=lambda t: emit(VOCAB[int(t.item()) % len(VOCAB)]))
+        return {"ttft_s": r["ttft_ms"] / 1e3, "total_s": r["total_ms"] / 1e3, "tokens": r["new_tokens"]}
+
+
+class SpanExporter:
+    """Batched OTLP/HTTP JSON trace export (chat.request / chat.retrieval / chat.generation)."""
+
+    def __init__(self, endpoint: str, service: str = "rag-service", max_batch: int = 64):
+        self.endpoint, self.service, self.max_batch = endpoint, service, max_batch
+        self.buf: List[dict] = []
+        self.lock = threading.Lock()
+
+    @staticmethod
+    def span(trace_id: str, span_id: str, parent: str, name: str, t0: int, t1: int, attrs: Dict[str, object]):
+        def val(v):
+            if isinstance(v, bool):
+                return {"boolValue": v}
+            if isinstance(v, int):
+                return {"intValue": str(v)}
+            if isinstance(v, float):
+                return {"doubleValue": v}
+            return {"stringValue": str(v)}
+
+        d = {"traceId": trace_id, "spanId": span_id, "name": name, "kind": 2, "startTimeUnixNano": str(t0),
+             "endTimeUnixNano": str(t1), "attributes": [{"key": k, "value": val(v)} for k, v in attrs.items()]}
+        if parent:
+            d["parentSpanId"] = parent
+        return d
+
+    def add(self, spans: List[dict]) -> None:
+        if not self.endpoint:
+            return
+        with self.lock:
+            self.buf += spans
+            if len(self.buf) < self.max_batch:
+                return
+            batch, self.buf = self.buf, []
+        self._post(batch)
+
+    def flush(self) -> None:
+        with self.lock:
+            batch, self.buf = self.buf, []
+        if batch:
+            self._post(batch)
+
+    def _post(self, spans: List[dict]) -> None:
+        body = {"resourceSpans": [{"resource": {"attributes": [{"key": "service.name",
+                                                                "value": {"stringValue": self.service}}]},
+                                   "scopeSpans": [{"scope": {"name": "rag-service"}, "spans": spans}]}]}
+        req = urllib.request.Request(self.endpoint, data=json.dumps(body).encode(), method="POST",
+                                     headers={"Content-Type": "application/json"})
+        try:
+            urllib.request.urlopen(req, timeout=5).read()
+        except Exception as exc:  # noqa: BLE001 - tracing must never fail a request
+            print(f"trace export failed: {exc}", file=sys.stderr)
+
+
+class BurnRate:
+    """Error-budget burn rate over a sliding window: error_ratio / (1 - objective)."""
+
+    def __init__(self, objective: float = 0.99, window_s: float = 300.0):
+        self.objective, self.window_s = objective, window_s
+        self.events = collections.deque()
+
+    def observe(self, ok: bool, now: Optional[float] = None) -> float:
+        now = time.monotonic() if now is None else now
+        self.events.append((now, ok))
+        while self.events and self.events[0][0] < now - self.window_s:
+            self.events.popleft()
+        n = len(self.events)
+        errs = sum(1 for _, o in self.events if not o)
+        return (errs / n) / (1.0 - self.objective) if n else 0.0
+
+
+class RagService:
+    def __init__(self, backend, corpus_path: str = os.path.join(HERE, "fixtures", "corpus.json"),
+                 otlp_endpoint: str = "", node: str = "demo-node", pod: str = "demo-rag-service"):
+        self.backend = backend
+        with open(corpus_path) as fh:
+            self.docs = json.load(fh)
+        self.corr = Correlator()
+        self.node, self.pod = node, pod
+        self.spans = SpanExporter(otlp_endpoint)
+        self.burn = BurnRate()
+        r = self.registry = Registry()
+        ms = (5, 10, 25, 50, 100, 200, 400, 800, 1600, 3200)
+        self.m_ttft = r.histogram("llm_slo_ttft_ms", "Time to first token (ms).", ms)
+        self.m_tps = r.histogram("llm_slo_tokens_per_sec", "Decode tokens per second.", (1, 5, 10, 20, 40, 80, 160, 320))
+        self.m_vdb = r.histogram("llm_slo_retrieval_vectordb_ms", "Vector DB time (ms).", ms)
+        self.m_net = r.histogram("llm_slo_retrieval_network_ms", "Retrieval network time (ms).", ms)
+        self.m_dns = r.histogram("llm_slo_retrieval_dns_ms", "Retrieval DNS time (ms).", ms)
+        self.m_req = r.counter("llm_slo_requests_total", "Chat requests by status and profile.", ("status", "profile"))
+        self.m_err = r.counter("llm_slo_errors_total", "Failed chat requests by profile.", ("profile",))
+        self.m_corr = r.counter("llm_slo_correlation_total", "DNS correlation decisions by tier and enrichment.",
+                                ("tier", "enriched"))
+        self.m_burn = r.gauge("llm_slo_burn_rate", "Error-budget burn rate (5 min window, 99% objective).")
+
+    def _fail(self, profile: str) -> None:
+        self.m_req.inc(1, "error", profile)
+        self.m_err.inc(1, profile)
+        self.m_burn.set(self.burn.observe(False))
+
+    def chat(self, req: dict, emit=None) -> dict:
+        prompt = (req.get("prompt") or "").strip()
+        if not prompt:
+            self.m_req.inc(1, "bad_request", "unknown")
+            raise ValueError("prompt is required")
+        profile = req.get("profile") or "rag_medium"
+        seed = int(req.get("seed") or 42)
+        max_tokens = int(req.get("max_tokens") or 64)
+        rid = req.get("request_id") or f"req-{time.time_ns()}"
+        trace_id = hashlib.blake2b(rid.encode(), digest_size=16).hexdigest()
+        root, rsp, gsp = (hashlib.blake2b(f"{rid}/{k}".encode(), digest_size=8).hexdigest() for k in "rxg")
+        t_req = time.time_ns()
+        plan = plan_for(profile, prompt, seed)
+        rnd = random.Random(seed + prompt_hash(prompt))
+        docs = sorted(d["title"] for d in rnd.sample(self.docs, min(plan.docs, len(self.docs))))
+        t_r0 = time.time_ns()
+        for wait in (plan.dns_ms, plan.network_ms, plan.vectordb_ms):
+            time.sleep(wait / 1000.0)
+        t_r1 = time.time_ns()
+        span = SpanRef(trace_id=trace_id, service="rag-service", node=self.node, pod=self.pod, pid=os.getpid(),
+                       timestamp=t_req)
+        sig = SignalRef(signal="dns_latency_ms", trace_id=trace_id, service="rag-service", node=self.node,
+                        pod=self.pod, pid=os.getpid(), timestamp=time.time_ns(), value=float(plan.dns_ms))
+        attrs, decision = self.corr.enrich_dns_attributes(None, span, sig)
+        if decision.matched:
+            enriched = "true" if decision.confidence >= self.corr.enrichment_threshold else "false"
+            self.m_corr.inc(1, decision.tier, enriched)
+        tokens: List[str] = []
+
+        def on_tok(t):
+            tokens.append(t)
+            if emit:
+                emit({"token": t, "index": len(tokens) - 1})
+
+        try:
+            g = self.backend.generate(prompt, max_tokens, seed, plan, on_tok)
+        except Exception:
+            self._fail(profile)
+            raise
+        t_end = time.time_ns()
+        ret_ms = (t_r1 - t_r0) / MS
+        ttft_ms = (t_r1 - t_req) / MS + g["ttft_s"] * 1e3
+        dec_s = max(g["total_s"] - g["ttft_s"], 1e-9)
+        tps = (g["tokens"] - 1) / dec_s if g["tokens"] > 1 else float(g["tokens"])
+        self.m_ttft.observe(ttft_ms)
+        self.m_tps.observe(tps)
+        self.m_vdb.observe(plan.vectordb_ms)
+        self.m_net.observe(plan.network_ms)
+        self.m_dns.observe(plan.dns_ms)
+        self.m_req.inc(1, "ok", profile)
+        self.m_burn.set(self.burn.observe(True))
+        root_attrs = {"request.id": rid, "llm.profile": profile, "llm.seed": seed, "llm.backend": self.backend.name,
+                      semconv.ATTR_SLO_TTFT_MS: ttft_ms, semconv.ATTR_SLO_TOKENS_PER_SEC: tps}
+        root_attrs.update({k: float(v) for k, v in (attrs or {}).items()})
+        if decision.tier:
+            root_attrs["llm.ebpf.correlation_tier"] = decision.tier
+        self.spans.add([
+            SpanExporter.span(trace_id, root, "", "chat.request", t_req, t_end, root_attrs),
+            SpanExporter.span(trace_id, rsp, root, "chat.retrieval", t_r0, t_r1, {
+                semconv.ATTR_RETRIEVAL_VECTORDB: float(plan.vectordb_ms),
+                semconv.ATTR_RETRIEVAL_NETWORK_MS: float(plan.network_ms),
+                semconv.ATTR_RETRIEVAL_DNS_MS: float(plan.dns_ms), "retrieval.selected_docs": len(docs)}),
+            SpanExporter.span(trace_id, gsp, root, "chat.generation", t_r1, t_end, {"llm.tokens.count": g["tokens"]}),
+        ])
+        return {"request_id": rid, "trace_id": trace_id, "profile": profile, "tokens": tokens, "documents": docs,
+                "ttft_ms": round(ttft_ms, 3), "tokens_per_sec": round(tps, 3), "retrieval_ms": round(ret_ms, 3),
+                "correlation": {"tier": decision.tier, "confidence": decision.confidence},
+                "attributes": attrs or {}}
+
+    def handler(self):
+        svc = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):
+                pass
+
+            def _json(self, code, obj):
+                b = json.dumps(obj).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(b)))
+                self.end_headers()
+                self.wfile.write(b)
+
+            def do_GET(self):
+                if self.path == "/healthz":
+                    self._json(200, {"status": "ok"})
+                else:
+                    self._json(404, {"error": "not found"})
+
+            def do_POST(self):
+                if self.path != "/chat":
+                    self._json(404, {"error": "not found"})
+                    return
+                n = int(self.headers.get("Content-Length") or 0)
+                try:
+                    req = json.loads(self.rfile.read(n) or b"{}")
+                except json.JSONDecodeError:
+                    svc.m_req.inc(1, "bad_request", "unknown")
+                    self._json(400, {"error": "invalid json body"})
+                    return
+                if req.get("stream"):
+                    self.send_response(200)
+                    self.send_header("Content-Type", "application/x-ndjson")
+                    self.send_header("Transfer-Encoding", "chunked")
+                    self.end_headers()
+
+                    def emit(d):
+                        line = (json.dumps(d) + "\n").encode()
+                        self.wfile.write(f"{len(line):x}\r\n".encode() + line + b"\r\n")
+                        self.wfile.flush()
+
+                    try:
+                        out = svc.chat(req, emit)
+                        out.pop("tokens", None)
+                        emit({"done": True, **out})
+                    except ValueError as exc:
+                        emit({"error": str(exc)})
+                    except Exception as exc:  # noqa: BLE001
+                        emit({"error": f"generation failed: {exc}"})
+                    self.wfile.write(b"0\r\n\r\n")
+                    return
+                try:
+                    self._json(200, svc.chat(req))
+                except ValueError as exc:
+                    self._json(400, {"error": str(exc)})
+                except Exception as exc:  # noqa: BLE001
+                    self._json(502, {"error": f"generation failed: {exc}"})
+
+        return H
+
+    def serve(self, bind: str = "127.0.0.1:8080", metrics_bind: str = "127.0.0.1:9464"):
+        host, port = bind.rsplit(":", 1)
+        httpd = http.server.ThreadingHTTPServer((host or "0.0.0.0", int(port)), self.handler())
+        metrics = MetricsServer(self.registry, metrics_bind).start() if metrics_bind else None
+        t = threading.Thread(target=httpd.serve_forever, daemon=True)
+        t.start()
+        return httpd, metrics
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="demo RAG chat service")
+    ap.add_argument("--bind", default="0.0.0.0:8080")
+    ap.add_argument("--metrics-bind", default="0.0.0.0:9464")
+    ap.add_argument("--backend", default=os.environ.get("LLM_BACKEND", "stub"), choices=("stub", "llama"))
+    ap.add_argument("--llama-preset", default="1b")
+    ap.add_argument("--otlp-endpoint", default=os.environ.get("OTEL_EXPORTER_OTLP_TRACES_ENDPOINT", ""))
+    a = ap.parse_args(argv)
+    backend = LlamaBackend(a.llama_preset) if a.backend == "llama" else StubBackend()
+    svc = RagService(backend, otlp_endpoint=a.otlp_endpoint)
+    httpd, _ = svc.serve(a.bind, a.metrics_bind)
+    print(f"rag-service listening on {a.bind} (backend={backend.name})", flush=True)
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        httpd.shutdown()
+        svc.spans.flush()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

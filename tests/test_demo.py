@@ -1,0 +1,78 @@
+"""Demo RAG service over real HTTP (stub backend): retrieval plan, DNS correlation,
+streaming NDJSON, Prometheus metrics incl. the errors / burn-rate series cdgate queries."""
+
+import json
+import urllib.request
+
+import pytest
+
+from llm_slo_ebpf_toolkit_amd.demo import rag_service as rs
+from llm_slo_ebpf_toolkit_amd.export.prometheus import parse_exposition
+
+
+@pytest.fixture
+def service(http_recorder):
+    traces = http_recorder()
+    svc = rs.RagService(rs.StubBackend(), otlp_endpoint=traces.url + "/v1/traces")
+    svc.spans.max_batch = 3
+    httpd, metrics = svc.serve("127.0.0.1:0", "127.0.0.1:0")
+    yield svc, f"http://127.0.0.1:{httpd.server_address[1]}", f"http://127.0.0.1:{metrics.port}", traces
+    httpd.shutdown()
+    metrics.stop()
+
+
+def post(url, body):
+    req = urllib.request.Request(url, data=json.dumps(body).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    return urllib.request.urlopen(req, timeout=30)
+
+
+def test_plan_is_deterministic_and_profile_shaped():
+    a, b = rs.plan_for("chat_short", "hi there", 42), rs.plan_for("chat_short", "hi there", 42)
+    assert a == b and 2 <= a.dns_ms < 6 and 10 <= a.vectordb_ms < 30
+    c = rs.plan_for("context_long", "hi there", 42)
+    assert 70 <= c.vectordb_ms < 150
+
+
+def test_chat_roundtrip_metrics_and_traces(service):
+    svc, api, metrics, traces = service
+    out = json.load(post(api + "/chat", {"prompt": "why is ttft high", "profile": "chat_short", "max_tokens": 5,
+                                         "request_id": "r1"}))
+    assert out["tokens"][:4] == ["why", "is", "ttft", "high"] and len(out["tokens"]) == 5
+    assert out["correlation"]["tier"] == "trace_id_exact" and out["correlation"]["confidence"] == 1.0
+    assert out["attributes"]["llm.ebpf.dns.latency_ms"] > 0
+    m = parse_exposition(urllib.request.urlopen(metrics + "/metrics").read().decode())
+    assert m['llm_slo_requests_total{status="ok",profile="chat_short"}'] == 1
+    assert m['llm_slo_correlation_total{tier="trace_id_exact",enriched="true"}'] == 1
+    assert m["llm_slo_ttft_ms_count"] == 1 and m["llm_slo_burn_rate"] == 0
+    spans = json.loads(traces.requests[0]["body"])["resourceSpans"][0]["scopeSpans"][0]["spans"]
+    assert [s["name"] for s in spans] == ["chat.request", "chat.retrieval", "chat.generation"]
+    assert len({s["traceId"] for s in spans}) == 1
+
+
+def test_streaming_and_errors(service):
+    svc, api, metrics, _ = service
+    lines = [json.loads(x) for x in post(api + "/chat", {"prompt": "stream me", "max_tokens": 3, "stream": True})
+             .read().decode().splitlines() if x.strip()]
+    assert [d.get("token") for d in lines[:3]] == ["stream", "me", lines[2]["token"]]
+    assert lines[-1]["done"] is True
+    with pytest.raises(urllib.error.HTTPError):
+        post(api + "/chat", {"prompt": "  "})
+
+    class Boom(rs.StubBackend):
+        def generate(self, *a, **k):
+            raise RuntimeError("backend down")
+
+    svc.backend = Boom()
+    with pytest.raises(urllib.error.HTTPError):
+        post(api + "/chat", {"prompt": "x", "max_tokens": 1})
+    m = parse_exposition(urllib.request.urlopen(metrics + "/metrics").read().decode())
+    assert m['llm_slo_errors_total{profile="rag_medium"}'] == 1 and m["llm_slo_burn_rate"] > 0
+
+
+def test_burn_rate_window():
+    b = rs.BurnRate(0.99, window_s=10)
+    for i in range(99):
+        b.observe(True, now=i * 0.01)
+    assert b.observe(False, now=1.0) == pytest.approx(1.0)
+    assert b.observe(True, now=100.0) == 0.0  # old events aged out
