@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--paced-windows", type=int, default=3,
                     help="windows replayed at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
     ap.add_argument("--wire", type=int, default=32, choices=(32, 64),
@@ -97,7 +98,7 @@ def main() -> int:
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
-                          group_scope=a.group_scope)
+                          group_scope=a.group_scope, use_graphs=not a.no_graphs)
 
     def run(n, start):
         for i in range(n):
@@ -170,7 +171,7 @@ def main() -> int:
         samples = [s for s in load_samples_jsonl(fx) if s.expected_domain]
         vals, labels = samples_to_arrays(samples)
         eng = pipe.engine
-        for name, model in (("bayes_ref", NaiveBayes.ref()), (a.model, pipe.model)):
+        for name, model in (("bayes_ref", NaiveBayes.ref()), (a.model, pipe.host_model())):
             eng.set_model(model)
             eng.eng.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
             eng.eng.counts.copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))

@@ -58,6 +58,9 @@ void launch_posterior(const float* feat, const int* ng_dev, int cap, const Poste
 void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                   const float* weights, double* out, double* count, hipStream_t stream);
 
+void launch_refit_nb(const double* stats, const double* p0, double alpha, double prior_pseudo, int n_dom,
+                     PosteriorModel* pm, hipStream_t stream);
+
 // gatestats.hip (K5)
 int boot_max_n();
 void launch_boot_quantile(const double* sorted_c, int nc, const double* sorted_b, int nb, double q, int iters,

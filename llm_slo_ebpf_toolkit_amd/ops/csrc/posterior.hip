@@ -150,6 +150,61 @@ __global__ __launch_bounds__(NT) void k_stats(const float* __restrict__ feat, co
   }
 }
 
+// On-device refit of the learned naive Bayes (models/bayes.py NaiveBayes.learned) from
+// the accumulated, all-reduced sufficient statistics: posterior-mean likelihoods
+//   p_sd = (c_sd + alpha * p0_sd) / (n_d + alpha),  pi_d = (n_d + pp) / (N + pp * D)
+// turned into the linear-logit model in place (w, bias, evidence masks). Runs on the
+// compute stream between windows, so online learning needs no host round trip.
+// stats: [32 x 32] f64 (rows 0-15 = E^T Y) followed by count[16]; p0: [16 x 16] f64.
+__global__ __launch_bounds__(256) void k_refit_nb(const double* __restrict__ stats, const double* __restrict__ p0,
+                                                  double alpha, double prior_pseudo, int n_dom,
+                                                  PosteriorModel* __restrict__ pm) {
+  __shared__ double s_logpn[kSlots][kMaxDomains];
+  __shared__ uint32_t s_mask[kMaxDomains];
+  const double* count = stats + 32 * 32;
+  const int t = threadIdx.x;
+  if (t < kMaxDomains) s_mask[t] = 0u;
+  __syncthreads();
+  {
+    const int sl = t >> 4, d = t & 15;  // 256 threads = 16 slots x 16 domain columns
+    if (d < n_dom) {
+      const double n = count[d];
+      const double c = stats[sl * 32 + d];
+      const double p = (c + alpha * p0[sl * 16 + d]) / (n + alpha);
+      const double pe = fmin(fmax(p, 0.01), 0.99), pn = fmin(fmax(1.0 - p, 0.01), 0.99);
+      pm->w[sl][d] = log(pe) - log(pn);
+      s_logpn[sl][d] = log(pn);
+      if (p >= 0.5) atomicOr(&s_mask[d], 1u << sl);
+    } else {
+      pm->w[sl][d] = 0.0;
+      s_logpn[sl][d] = 0.0;
+    }
+  }
+  __syncthreads();
+  if (t < kMaxDomains) {
+    if (t < n_dom) {
+      double N = 0.0;
+      for (int d = 0; d < n_dom; ++d) N += count[d];
+      double b = log((count[t] + prior_pseudo) / (N + prior_pseudo * (double)n_dom));
+      for (int sl = 0; sl < kSlots; ++sl) b += s_logpn[sl][t];
+      pm->bias[t] = b;
+      pm->dom_mask[t] = s_mask[t];
+    } else {
+      pm->bias[t] = -__builtin_inf();
+      pm->dom_mask[t] = 0u;
+    }
+  }
+  if (t == 0) {
+    pm->table_mask = 0xFFFFu;
+    pm->mode = 0;
+  }
+}
+
+void launch_refit_nb(const double* stats, const double* p0, double alpha, double prior_pseudo, int n_dom,
+                     PosteriorModel* pm, hipStream_t stream) {
+  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, p0, alpha, prior_pseudo, n_dom, pm);
+}
+
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                       double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
                       hipStream_t stream) {

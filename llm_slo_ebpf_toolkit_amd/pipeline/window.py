@@ -106,7 +106,8 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
 class WindowPipeline:
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, process_group=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
-                 fanout: int = 3, group_mode: int = 1, learn: bool = True, group_scope: str = "rank"):
+                 fanout: int = 3, group_mode: int = 1, learn: bool = True, group_scope: str = "rank",
+                 use_graphs: bool = True):
         import torch
 
         self.torch = torch
@@ -120,6 +121,14 @@ class WindowPipeline:
         # "rank": incident groups are per-GPU (each node's services); "global": groups span
         # GPUs and are scored on all-reduced per-group sums (a second, G x 16 collective)
         self.group_scope = group_scope
+        # learned naive Bayes refits on the device from accumulated all-reduced stats
+        # (ops k_refit_nb): no per-window host round trip; LDA refits on the host
+        self.device_refit = learn and model == "bayes_learned"
+        # the per-window kernel chain (reset, decode, partition, join, finalize, posterior,
+        # stats, pack: ~15 launches) is captured once per (buffer, shape) into a HIP graph
+        # and replayed: window launch cost becomes one graph launch
+        self.use_graphs = use_graphs
+        self.graphs: Dict[tuple, object] = {}
         self.engine = GpuEngine(sig_cap, span_cap, group_cap, device, window_ms, threshold, fanout, group_mode)
         self.eng = self.engine.eng
         L = int(self.engine.mod.PACKET_LEN)
@@ -134,6 +143,11 @@ class WindowPipeline:
             self.labels_dev = [torch.full((group_cap,), -1, dtype=torch.int32, device=self.dev) for _ in range(2)]
             self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(2)]
             self.totals = torch.zeros(L, dtype=torch.float64, device=self.dev)
+            self.stats_off = sum(PACKET_LAYOUT[:5])
+            self.stats_acc = torch.zeros(PACKET_LAYOUT[5] + PACKET_LAYOUT[6], dtype=torch.float64, device=self.dev)
+            p0 = np.zeros((16, 16), dtype=np.float64)
+            p0[:, :N_DOMAINS] = NaiveBayes.random_init_table(seed)
+            self.p0_dev = torch.from_numpy(p0.ravel()).to(self.dev)
             self.packet_host = [torch.zeros(L, dtype=torch.float64).pin_memory() for _ in range(2)]
             self.model_host = [torch.zeros(2568, dtype=torch.uint8).pin_memory() for _ in range(2)]
             self.copy_stream = torch.cuda.Stream(self.dev)
@@ -200,6 +214,13 @@ class WindowPipeline:
         ks.wait_event(self.h2d_done[b])
         ks.wait_event(self.comm_done[b])  # packet[b] no longer being reduced / read
         with torch.cuda.stream(ks):
+            if self.device_refit and self.i >= 2:
+                # fold window i-2's all-reduced statistics (packet[b], complete per the wait
+                # above) and refit before window i: deterministic prequential lag of 2
+                n = self.stats_acc.numel()
+                self.stats_acc.add_(self.packet_dev[b][self.stats_off:self.stats_off + n])
+                self.eng.refit_nb(self.stats_acc, self.p0_dev, 2.0, 1.0, N_DOMAINS)
+                self.windows_folded += 1
             self.eng.bind_io(self.counts_dev[b], self.labels_dev[b], self.packet_dev[b])
             if self.group_scope == "global" and self.pg is not None:
                 self.eng.run_window_pre(self.ev_dev[b], self.sp_dev[b], w.n_groups, w.wire)
@@ -217,8 +238,7 @@ class WindowPipeline:
                 self.compute_done[b].record(ks)
         else:
             with torch.cuda.stream(ks):
-                self.eng.run_window(self.ev_dev[b], self.sp_dev[b], w.n_groups, with_labels,
-                                    self.learn and with_labels, w.wire)
+                self._run_window(b, w, with_labels)
                 self.compute_done[b].record(ks)
         ms.wait_event(self.compute_done[b])
         with torch.cuda.stream(ms):
@@ -230,13 +250,46 @@ class WindowPipeline:
         self.i += 1
         # fold window i-2 (this call's predecessor's predecessor is certainly far along;
         # folding i-1 would stall the host on the window just queued)
-        if self.i >= 2 and self.learn:
+        if self.i >= 2 and self.learn and not self.device_refit:
             pb = (self.i - 2) % 2
             self.comm_done[pb].synchronize()
             pk = unpack_packet(self.packet_host[pb].numpy())
             self.cum_stats = self.cum_stats.merge(stats_from_packet(pk))
             self.windows_folded += 1
             self.refit(self.cum_stats)
+
+    def _run_window(self, b: int, w: StagedWindow, with_labels: bool) -> None:
+        learn = self.learn and with_labels
+        args = (self.ev_dev[b], self.sp_dev[b], w.n_groups, with_labels, learn, w.wire)
+        if not self.use_graphs:
+            self.eng.run_window(*args)
+            return
+        torch = self.torch
+        key = (b, w.n_groups, with_labels, learn, w.wire)
+        g = self.graphs.get(key)
+        if g is None:
+            if not self.graphs.get(("warm", b)):  # first use of the buffers: run eagerly once
+                self.eng.run_window(*args)
+                self.graphs[("warm", b)] = True
+                return
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=torch.cuda.current_stream(self.dev), capture_error_mode="thread_local"):
+                self.eng.run_window(*args)
+            self.graphs[key] = g
+        g.replay()
+
+    def host_model(self):
+        """The model currently on the device, as a host LinearPosteriorModel (reporting)."""
+        if not self.device_refit:
+            return self.model
+        self.drain()
+        st = self.stats_acc.cpu().numpy()
+        s = SufficientStats(count=st[1024:1024 + N_DOMAINS].copy(),
+                            elevated_sum=st[:1024].reshape(32, 32)[:16, :N_DOMAINS].copy(),
+                            x_sum=st[:1024].reshape(32, 32)[16:, :N_DOMAINS].copy(),
+                            xx=st[:1024].reshape(32, 32)[16:, 16:].copy())
+        self.model = NaiveBayes.learned(s, seed=self.seed)
+        return self.model
 
     def last_packet(self) -> Dict[str, np.ndarray]:
         """Unpacked (all-reduced) packet of the most recently submitted window (after drain)."""

@@ -183,3 +183,35 @@ def test_split_pre_post_equals_run_window(engine):
     ref = oracle.join(oracle.decode_events(win.events), win.spans, win.n_groups)
     np.testing.assert_array_equal(top3, ref.top3)
     e.counts.copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, 0], dtype=torch.int32))
+
+
+def test_device_refit_matches_host_learned_model(engine):
+    """k_refit_nb == NaiveBayes.learned on the same sufficient statistics."""
+    import torch
+
+    from llm_slo_ebpf_toolkit_amd.models.bayes import N_DOMAINS
+    from llm_slo_ebpf_toolkit_amd.ops.engine import MODEL_DTYPE, model_bytes
+
+    win = small_window(seed=17)
+    engine.set_model(NaiveBayes.ref())
+    out = engine.process(win.events, win.spans, win.n_groups, win.group_labels, learn=True)
+    st = SufficientStats()
+    st.add(out.feat.astype(np.float64), win.group_labels)
+    acc = np.zeros(1040)
+    S = np.zeros((32, 32))
+    S[:16, :N_DOMAINS] = st.elevated_sum
+    acc[:1024] = S.ravel()
+    acc[1024:1024 + N_DOMAINS] = st.count
+    p0 = np.zeros((16, 16))
+    p0[:, :N_DOMAINS] = NaiveBayes.random_init_table(42)
+    host = NaiveBayes.learned(st, seed=42)
+    engine.eng.set_model_bytes(torch.from_numpy(model_bytes(NaiveBayes.learned(SufficientStats(), seed=42))))
+    engine.eng.refit_nb(torch.from_numpy(acc).cuda(), torch.from_numpy(p0.ravel()).cuda(), 2.0, 1.0, N_DOMAINS)
+    torch.cuda.synchronize()
+    dev = np.frombuffer(engine.eng.model.cpu().numpy().tobytes(), dtype=MODEL_DTYPE)[0]
+    ref = np.frombuffer(model_bytes(host).tobytes(), dtype=MODEL_DTYPE)[0]
+    np.testing.assert_allclose(dev["w"], ref["w"], rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(dev["bias"][:N_DOMAINS], ref["bias"][:N_DOMAINS], rtol=1e-13)
+    assert np.isneginf(dev["bias"][N_DOMAINS:]).all()
+    np.testing.assert_array_equal(dev["dom_mask"], ref["dom_mask"])
+    assert dev["table_mask"] == ref["table_mask"] and dev["mode"] == 0
