@@ -128,7 +128,7 @@ class Engine {
     top3 = torch::empty({3 * S}, i64); cnt = torch::empty({S}, i32);
     attrs = torch::empty({S, kSlots}, f32); conf = torch::empty({S}, f32); kernel_ms = torch::empty({S}, f32);
     // groups / incidents
-    gsum = torch::empty({G, kSlots}, i64); gcnt = torch::empty({G, kSlots}, i32);
+    gsum = torch::empty({kGroupStripes * G, kSlots}, i64); gcnt = torch::empty({kGroupStripes * G, kSlots}, i32);
     feat = torch::empty({G, kSlots}, f32); labels = torch::full({G}, -1, i32);
     post = torch::empty({G, kMaxDomains}, f64); pred = torch::empty({G}, i32); gconf = torch::empty({G}, f64);
     evbits = torch::empty({G, kMaxDomains}, i32);

@@ -28,6 +28,8 @@
 //      retrieval decomposition. Incident-group features are the mean value per signal
 //      slot over either every accepted candidate pair (group_mode 1, accumulated in the
 //      probe) or the spans' merged top-3 attributes (group_mode 0, REF-style).
+#include <cstdlib>
+
 #include "mislo_common.h"
 #include "mislo_launch.h"
 
@@ -151,8 +153,21 @@ __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
 // per-span top-3 (24) and candidate count (4) = 80 B x 512 = 40 KiB, plus 8 KiB of
 // incident accumulators -> three workgroups per CU. Every per-pair update is an LDS
 // atomic; global atomics happen once per (span, workgroup) on flush.
+struct alignas(16) SpanKT {
+  uint64_t h;
+  int64_t t;
+};
+struct alignas(16) SpanTC {
+  uint64_t tr;
+  uint64_t cn;
+};
+struct alignas(16) SpanPP {
+  uint32_t pod, pid, sn, grp;
+};
+
 constexpr int kLdsGroups = 64;
 constexpr int kSplit = 8;
+constexpr int kMinPerSplit = 512;
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
@@ -161,27 +176,36 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
                                               const uint32_t* __restrict__ sig_base, int sig_cap, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups, unsigned long long* __restrict__ gsum,
-                                              uint32_t* __restrict__ gcnt, unsigned long long* __restrict__ dbg) {
-  __shared__ uint64_t s_h[kChunk];
-  __shared__ int64_t s_t[kChunk];
+                                              uint32_t* __restrict__ gcnt, unsigned long long* __restrict__ dbg,
+                                              int k_base) {
+  // span fields packed 16 B per entry so each pair costs three ds_read_b128 (key+time,
+  // trace+conn, pod|pid|svcnode|group) instead of nine scalar LDS reads
+  __shared__ SpanKT s_kt[kChunk];
+  __shared__ SpanTC s_tc[kChunk];
+  __shared__ SpanPP s_pp[kChunk];
   __shared__ uint32_t s_i[kChunk];
-  __shared__ uint64_t s_tr[kChunk];
-  __shared__ uint64_t s_cn[kChunk];
-  __shared__ uint32_t s_pod[kChunk];
-  __shared__ uint32_t s_pid[kChunk];
-  __shared__ uint32_t s_sn[kChunk];
-  __shared__ uint32_t s_grp[kChunk];
   __shared__ unsigned long long s_top[kChunk * 3];
+  __shared__ unsigned long long s_seed3[kChunk];  // global 3rd-best key after the trace phase
   __shared__ uint32_t s_cnt[kChunk];
   __shared__ unsigned long long s_gsum[kLdsGroups * kSlots];
   __shared__ uint32_t s_gcnt[kLdsGroups * kSlots];
 
-  const int k = blockIdx.y;
+  const int k = k_base + blockIdx.y;
+  // incident sums go to one of kGroupStripes copies (folded after the join): thousands of
+  // workgroups adding into the same G x 16 words would otherwise serialise in L2 atomics
+  {
+    const size_t stripe = (size_t)(blockIdx.x & (kGroupStripes - 1)) * (size_t)n_groups * kSlots;
+    gsum += stripe;
+    gcnt += stripe;
+  }
   const int c = k * kParts + blockIdx.x;
   const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
   const uint32_t gb0 = sig_base[c], gb1 = sig_base[c + 1];
   if (sp0 == sp1 || gb0 == gb1) return;
-  const uint32_t per = (gb1 - gb0 + kSplit - 1) / kSplit;
+  // split big signal lists over up to kSplit workgroups, but never below kMinPerSplit
+  // signals each: a workgroup has a fixed cost (staging, sort, accumulator init/flush)
+  // that would dominate sparse partitions (the trace tier: ~300 signals per partition)
+  const uint32_t per = max((gb1 - gb0 + kSplit - 1) / kSplit, (uint32_t)kMinPerSplit);
   const uint32_t sg0 = gb0 + blockIdx.z * per;
   const uint32_t sg1 = min(gb1, sg0 + per);
   if (sg0 >= sg1) return;
@@ -209,12 +233,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
     for (int i = threadIdx.x; i < M; i += NT) {
       if (i < m) {
         const uint32_t s = span_items[c0 + i];
-        s_h[i] = sc.hash[(size_t)k * span_cap + s];
-        s_t[i] = sc.ts[s];
+        s_kt[i] = SpanKT{sc.hash[(size_t)k * span_cap + s], sc.ts[s]};
         s_i[i] = s;
       } else {
-        s_h[i] = ~0ull;
-        s_t[i] = INT64_MAX;
+        s_kt[i] = SpanKT{~0ull, INT64_MAX};
         s_i[i] = 0xFFFFFFFFu;
       }
     }
@@ -226,10 +248,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           const int i = 2 * t - (t & (stride - 1));
           const int j = i + stride;
           const bool up = (i & size) == 0;
-          const bool gt = less_ht(s_h[j], s_t[j], s_h[i], s_t[i]);
+          const SpanKT ei = s_kt[i], ej = s_kt[j];
+          const bool gt = less_ht(ej.h, ej.t, ei.h, ei.t);
           if (gt == up) {
-            uint64_t th = s_h[i]; s_h[i] = s_h[j]; s_h[j] = th;
-            int64_t tt = s_t[i]; s_t[i] = s_t[j]; s_t[j] = tt;
+            s_kt[i] = ej; s_kt[j] = ei;
             uint32_t ti = s_i[i]; s_i[i] = s_i[j]; s_i[j] = ti;
           }
         }
@@ -240,15 +262,14 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
     if (!count_only) {
       for (int i = threadIdx.x; i < m; i += NT) {
         const uint32_t s = s_i[i];
-        s_tr[i] = sc.trace_h[s];
-        s_cn[i] = sc.conn_h[s];
-        s_pod[i] = sc.pod[s];
-        s_pid[i] = sc.pid[s];
-        s_sn[i] = sc.svcnode[s];
-        s_grp[i] = sc.group[s];
+        s_tc[i] = SpanTC{sc.trace_h[s], sc.conn_h[s]};
+        s_pp[i] = SpanPP{sc.pod[s], sc.pid[s], sc.svcnode[s], sc.group[s]};
         s_top[3 * i] = kEmpty;
         s_top[3 * i + 1] = kEmpty;
         s_top[3 * i + 2] = kEmpty;
+        // the trace tier ran to completion before this launch: a pair whose key is not
+        // below the span's current global 3rd best can never enter the final top-3
+        s_seed3[i] = k > 0 ? top3[3ull * s + 2] : kEmpty;
         s_cnt[i] = 0u;
       }
       __syncthreads();
@@ -263,7 +284,8 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       const int64_t tlo = t - w;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (less_ht(s_h[mid], s_t[mid], h, tlo)) lo = mid + 1; else hi = mid;
+        const SpanKT e = s_kt[mid];
+        if (less_ht(e.h, e.t, h, tlo)) lo = mid + 1; else hi = mid;
       }
       const int64_t thi = t + w;
       if (count_only) {
@@ -271,12 +293,13 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         int a = lo, b = m;
         while (a < b) {
           const int mid = (a + b) >> 1;
-          if (less_ht(h, thi, s_h[mid], s_t[mid])) b = mid; else a = mid + 1;
+          const SpanKT e = s_kt[mid];
+          if (less_ht(h, thi, e.h, e.t)) b = mid; else a = mid + 1;
         }
         n_low += (unsigned long long)(a - lo);
         continue;
       }
-      if (lo >= m || s_h[lo] != h || s_t[lo] > thi) continue;
+      if (lo >= m || s_kt[lo].h != h || s_kt[lo].t > thi) continue;
       const uint32_t g_pod = gc.pod[g], g_pid = gc.pid[g], g_sn = gc.svcnode[g];
       const uint64_t g_tr = gc.trace_h[g], g_cn = gc.conn_h[g];
       const int g_slot = gc.slot[g];
@@ -287,16 +310,20 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       // val x count once per run instead of once per pair (all lanes of a partition hit
       // the same few LDS words, so per-pair atomics serialise).
       uint32_t run_grp = 0xFFFFFFFFu, run_n = 0;
-      for (int i = lo; i < m && s_h[i] == h && s_t[i] <= thi; ++i) {
-        const int64_t dt = iabs64(t - s_t[i]);
-        const uint32_t p_pod = s_pod[i];
-        const uint64_t p_cn = s_cn[i];
+      for (int i = lo; i < m; ++i) {
+        const SpanKT e = s_kt[i];
+        if (e.h != h || e.t > thi) break;
+        const int64_t dt = iabs64(t - e.t);
+        const SpanTC tc = s_tc[i];
+        const SpanPP pp = s_pp[i];
+        const uint32_t p_pod = pp.pod;
+        const uint64_t p_cn = tc.cn;
         if (k == 2 && !(p_pod == g_pod && p_cn == g_cn)) continue;  // hash collision guard
         // higher-precedence tiers (REF Match order): skip pairs found at their own tier
-        const uint64_t p_tr = s_tr[i];
+        const uint64_t p_tr = tc.tr;
         if (k >= 1 && p_tr != 0 && p_tr == g_tr) continue;  // |dt| <= outer holds for every pair here
         if (k >= 2) {
-          const uint32_t p_pid = s_pid[i];
+          const uint32_t p_pid = pp.pid;
           if (p_pod != 0 && p_pod == g_pod && p_pid != 0 && p_pid == g_pid && dt <= jp.win_ns[1]) continue;
         }
         if (k >= 3 && p_pod != 0 && p_pod == g_pod && p_cn != 0 && p_cn == g_cn && dt <= jp.win_ns[2]) continue;
@@ -305,7 +332,8 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
                                    (unsigned long long)g;
           // slots only ever decrease, so a key >= the current 3rd best can never enter the
           // top-3: skip the atomic cascade (most pod+pid pairs are rejected here)
-          if (key < s_top[3 * i + 2]) {
+          // the seeded global bound rejects almost every lower-tier pair with one read
+          if (key < s_seed3[i] && key < s_top[3 * i + 2]) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) {  // LDS top-3 cascade (see top3_insert)
               const unsigned long long old = atomicMin(&s_top[3 * i + j], key);
@@ -316,7 +344,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           atomicAdd(&s_cnt[i], 1u);
           ++n_cand;
           if (do_groups) {
-            const uint32_t grp = s_grp[i];
+            const uint32_t grp = pp.grp;
             if (grp != run_grp) {
               if (run_n && run_grp < (uint32_t)n_groups) {
                 if (grp_lds) {
@@ -336,7 +364,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           ++n_low;
         }
         if (track_overlap) {
-          const uint32_t p_sn = s_sn[i];
+          const uint32_t p_sn = pp.sn;
           if ((p_sn >> 16) != 0 && (p_sn & 0xFFFF) != 0 && p_sn == g_sn && dt <= jp.win_ns[3]) ++n_overlap;
         }
       }
@@ -405,6 +433,11 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
                                                  unsigned long long* __restrict__ dbg) {
   const int ns = min(*ns_ptr, span_cap);
   const int s = blockIdx.x * NT + threadIdx.x;
+  {
+    const size_t stripe = (size_t)(blockIdx.x & (kGroupStripes - 1)) * (size_t)n_groups * kSlots;
+    gsum += stripe;
+    gcnt += stripe;
+  }
   unsigned long long dropped = 0, enriched = 0;
   if (s < ns) {
     float a[kSlots];
@@ -462,6 +495,22 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
   }
 }
 
+// Sum the incident-sum stripes into stripe 0 (exact integers: order-free).
+__global__ __launch_bounds__(256) void k_fold_groups(int n, unsigned long long* __restrict__ gsum,
+                                                     uint32_t* __restrict__ gcnt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  unsigned long long s = gsum[i];
+  uint32_t c = gcnt[i];
+#pragma unroll
+  for (int r = 1; r < kGroupStripes; ++r) {
+    s += gsum[(size_t)r * n + i];
+    c += gcnt[(size_t)r * n + i];
+  }
+  gsum[i] = s;
+  gcnt[i] = c;
+}
+
 __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned long long* __restrict__ gsum,
                                                         const uint32_t* __restrict__ gcnt, float* __restrict__ feat) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -490,8 +539,23 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
                   const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
                   uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream) {
-  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes, kSplit), dim3(256), 0, stream, sc, span_items, span_base, gc,
-                     sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg);
+  // phase 1: trace tier; phase 2: pod+pid, pod+conn, svc+node seeded with phase 1's top-3.
+  // MISLO_PROBE_PHASES=1 runs all four key types in one launch (diagnostic knob).
+  static const int phases = [] {
+    const char* v = getenv("MISLO_PROBE_PHASES");
+    return (v && v[0] == '1') ? 1 : 2;
+  }();
+  if (phases == 1) {
+    hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes, kSplit), dim3(256), 0, stream, sc, span_items,
+                       span_base, gc, sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg,
+                       0);
+    return;
+  }
+  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, 1, kSplit), dim3(256), 0, stream, sc, span_items, span_base, gc,
+                     sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg, 0);
+  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes - 1, kSplit), dim3(256), 0, stream, sc, span_items,
+                     span_base, gc, sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg,
+                     1);
 }
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
@@ -502,6 +566,7 @@ void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* 
                      cnt, gc, sc, jp, base_attrs, attrs, conf, kernel_ms, n_groups, gsum, gcnt, dbg);
   if (n_groups > 0) {
     const int n = n_groups * kSlots;
+    hipLaunchKernelGGL(k_fold_groups, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt);
     hipLaunchKernelGGL(k_group_features, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt, feat);
   }
 }

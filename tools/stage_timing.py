@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--services", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--wire", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--sort-ts", action="store_true", help="events in timestamp order (ring arrival order)")
     a = ap.parse_args()
     t = time.time()
     cfg = ReplayConfig(events_per_window=a.events, spans_per_window=a.spans, n_services=a.services)
@@ -31,6 +32,8 @@ def main():
     eng = GpuEngine(a.events, a.spans, a.services)
     eng.set_model(NaiveBayes.ref())
     ev, sp = win.events, win.spans
+    if a.sort_ts:
+        ev = ev[np.argsort(ev["ts_ns"], kind="stable")]
     if a.wire == 32:
         from llm_slo_ebpf_toolkit_amd.collector import records
 
