@@ -142,17 +142,26 @@ __device__ __forceinline__ void top3_insert(unsigned long long* slot3, unsigned 
 
 __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
 
-// Work decomposition: grid = (1024 partitions, 4 key types, kSplit signal slices). Keys of
-// the pod/service tiers are few and skewed (one serving pid per pod, one (svc, node) per
-// pod), so most partitions are empty and a handful carry thousands of signals; splitting
-// each partition's signal list over kSplit workgroups keeps ~8x more waves in flight for
-// this latency-bound walk. Each workgroup re-stages its (small) span partition.
+// Work decomposition: grid = (1024 partitions, key types, kSplit signal slices), launched
+// twice: the trace tier first, then pod+pid / pod+conn / svc+node. Keys of the pod and
+// service tiers are few and skewed, so most partitions are empty and a handful carry
+// thousands of signals; big signal lists are split over up to kSplit workgroups (never
+// below kMinPerSplit signals each: a workgroup has a fixed staging / sort / flush cost).
 //
-// LDS budget per workgroup at kChunk 512: sorted keys (hash 8 + ts 8 + idx 4), the span
-// fields the tier tests need (pod 4, pid 4, conn 8, trace 8, svc|node 4, group 4), the
-// per-span top-3 (24) and candidate count (4) = 80 B x 512 = 40 KiB, plus 8 KiB of
-// incident accumulators -> three workgroups per CU. Every per-pair update is an LDS
-// atomic; global atomics happen once per (span, workgroup) on flush.
+// Range accounting (why the pod tiers do not enumerate pairs). A signal's candidate spans
+// in a tier are one contiguous range of the partition's (hash, ts)-sorted spans. When the
+// hash run is uniform (same pod / pid / conn / svc|node / group) -- always, unless two keys
+// collide -- the tier's contribution is arithmetic on that range:
+//   pod+pid  (P2): all spans within 100 ms;
+//   pod+conn (P3): spans within 250 ms minus the 100 ms sub-range when the pid matches
+//                  (those pairs are P2's);
+// counts go into a difference array (two LDS atomics per signal), incident sums add
+// value x range length, the tier-4 overlap adds the range length. Pairs whose trace also
+// matches (T1) are counted by their pod tier; the trace pass, which enumerates T1 exactly,
+// skips counting those pairs and only contributes their (better) top-3 keys. Top-3 keys of
+// pod-tier pairs are only needed for spans whose third-best is not yet a trace key
+// ("needy" spans, usually none after the trace pass): those are visited through a compact
+// needy list. Non-uniform runs fall back to the exact per-pair walk.
 struct alignas(16) SpanKT {
   uint64_t h;
   int64_t t;
@@ -169,24 +178,78 @@ constexpr int kLdsGroups = 64;
 constexpr int kSplit = 8;
 constexpr int kMinPerSplit = 512;
 
+// In-place inclusive scan of v[0..n), n <= 2 * NT (each thread owns two adjacent entries).
+template <int NT>
+__device__ __forceinline__ void block_inclusive_scan(int* v, int n, int* wsum) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int i0 = 2 * t, i1 = 2 * t + 1;
+  const int a = i0 < n ? v[i0] : 0, b = i1 < n ? v[i1] : 0;
+  const int local = a + b;
+  int incl = local;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wave; ++w) base += wsum[w];
+  const int excl = base + incl - local;
+  if (i0 < n) v[i0] = excl + a;
+  if (i1 < n) v[i1] = excl + a + b;
+  __syncthreads();
+}
+
+// first index in [lo, hi) whose (h, t) is not less than (h0, t0)
+__device__ __forceinline__ int lower_ht(const SpanKT* kt, int lo, int hi, uint64_t h0, int64_t t0) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const SpanKT e = kt[mid];
+    if (less_ht(e.h, e.t, h0, t0)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+// first index in [lo, hi) whose (h, t) is greater than (h0, t0)
+__device__ __forceinline__ int upper_ht(const SpanKT* kt, int lo, int hi, uint64_t h0, int64_t t0) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const SpanKT e = kt[mid];
+    if (less_ht(h0, t0, e.h, e.t)) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+__device__ __forceinline__ int lower_u16(const uint16_t* v, int n, int x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int)v[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
                                               const uint32_t* __restrict__ span_base, SignalCols gc,
                                               const uint32_t* __restrict__ sig_items,
                                               const uint32_t* __restrict__ sig_base, int sig_cap, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
-                                              uint32_t* __restrict__ cnt, int n_groups, unsigned long long* __restrict__ gsum,
-                                              uint32_t* __restrict__ gcnt, unsigned long long* __restrict__ dbg,
-                                              int k_base) {
-  // span fields packed 16 B per entry so each pair costs three ds_read_b128 (key+time,
-  // trace+conn, pod|pid|svcnode|group) instead of nine scalar LDS reads
+                                              uint32_t* __restrict__ cnt, int n_groups,
+                                              unsigned long long* __restrict__ gsum, uint32_t* __restrict__ gcnt,
+                                              unsigned long long* __restrict__ dbg, int k_base) {
+  // span fields packed 16 B per entry (one ds_read_b128 each)
   __shared__ SpanKT s_kt[kChunk];
   __shared__ SpanTC s_tc[kChunk];
   __shared__ SpanPP s_pp[kChunk];
   __shared__ uint32_t s_i[kChunk];
   __shared__ unsigned long long s_top[kChunk * 3];
-  __shared__ unsigned long long s_seed3[kChunk];  // global 3rd-best key after the trace phase
-  __shared__ uint32_t s_cnt[kChunk];
+  __shared__ unsigned long long s_seed3[kChunk];  // global 3rd-best key after the trace pass
+  __shared__ int s_diff[kChunk + 1];              // candidate counts (difference array)
+  __shared__ int s_aux[kChunk];                   // scans: run ids, then needy positions
+  __shared__ uint16_t s_rid[kChunk];              // hash-run id per sorted position
+  __shared__ uint32_t s_runok[kChunk];            // hash run is uniform
+  __shared__ uint16_t s_needy[kChunk];            // sorted positions of needy spans
+  __shared__ int s_wsum[NT / 64];
+  __shared__ int s_nneedy;
   __shared__ unsigned long long s_gsum[kLdsGroups * kSlots];
   __shared__ uint32_t s_gcnt[kLdsGroups * kSlots];
 
@@ -202,9 +265,6 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
   const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
   const uint32_t gb0 = sig_base[c], gb1 = sig_base[c + 1];
   if (sp0 == sp1 || gb0 == gb1) return;
-  // split big signal lists over up to kSplit workgroups, but never below kMinPerSplit
-  // signals each: a workgroup has a fixed cost (staging, sort, accumulator init/flush)
-  // that would dominate sparse partitions (the trace tier: ~300 signals per partition)
   const uint32_t per = max((gb1 - gb0 + kSplit - 1) / kSplit, (uint32_t)kMinPerSplit);
   const uint32_t sg0 = gb0 + blockIdx.z * per;
   const uint32_t sg1 = min(gb1, sg0 + per);
@@ -216,9 +276,30 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
   const bool track_overlap = (k < 3) && (jp.conf[3] < jp.threshold);
   const bool grp_lds = n_groups <= kLdsGroups;
   const bool do_groups = cand_tier && jp.group_mode == 1 && n_groups > 0;
+  const bool ranged = (k == 1 || k == 2);                  // range accounting tiers
+  const bool cand1 = jp.conf[1] >= jp.threshold, cand2 = jp.conf[2] >= jp.threshold;
+  const bool groups1 = cand1 && jp.group_mode == 1 && n_groups > 0;
+  const bool groups2 = cand2 && jp.group_mode == 1 && n_groups > 0;
   unsigned long long n_cand = 0, n_low = 0, n_overlap = 0;
 
-  if (do_groups && grp_lds) {
+  auto add_group = [&](uint32_t grp, int slot, unsigned long long milli, uint32_t n) {
+    if (grp >= (uint32_t)n_groups || n == 0) return;
+    if (grp_lds) {
+      atomicAdd(&s_gsum[grp * kSlots + slot], milli * n);
+      atomicAdd(&s_gcnt[grp * kSlots + slot], n);
+    } else {
+      atomicAdd(gsum + (size_t)grp * kSlots + slot, milli * n);
+      atomicAdd(gcnt + (size_t)grp * kSlots + slot, n);
+    }
+  };
+  auto add_range = [&](int a, int b) {  // +1 candidate for every span of [a, b)
+    if (a < b) {
+      atomicAdd(&s_diff[a], 1);
+      atomicAdd(&s_diff[b], -1);
+    }
+  };
+
+  if (grp_lds && (do_groups || (k == 0 && (groups1 || groups2)))) {
     for (int i = threadIdx.x; i < kLdsGroups * kSlots; i += NT) {
       s_gsum[i] = 0ull;
       s_gcnt[i] = 0u;
@@ -258,7 +339,6 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         __syncthreads();
       }
     }
-    // gather the tier-test fields in sorted order (only when pairs are enumerated)
     if (!count_only) {
       for (int i = threadIdx.x; i < m; i += NT) {
         const uint32_t s = s_i[i];
@@ -267,48 +347,114 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         s_top[3 * i] = kEmpty;
         s_top[3 * i + 1] = kEmpty;
         s_top[3 * i + 2] = kEmpty;
-        // the trace tier ran to completion before this launch: a pair whose key is not
-        // below the span's current global 3rd best can never enter the final top-3
-        s_seed3[i] = k > 0 ? top3[3ull * s + 2] : kEmpty;
-        s_cnt[i] = 0u;
+        const unsigned long long seed = k > 0 ? top3[3ull * s + 2] : kEmpty;
+        s_seed3[i] = seed;
+        s_diff[i] = 0;
+        // hash-run heads, and (below) whether a pair key of this tier could still enter
+        // the span's top-3 (needy)
+        s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;
+        s_runok[i] = 1u;
       }
+      if (threadIdx.x == 0) s_diff[m] = 0;
       __syncthreads();
+      if (ranged) {
+        block_inclusive_scan<NT>(s_aux, m, s_wsum);  // run id = #heads up to i, minus one
+        for (int i = threadIdx.x; i < m; i += NT) {
+          s_rid[i] = (uint16_t)(s_aux[i] - 1);
+          if (i > 0 && s_kt[i].h == s_kt[i - 1].h) {
+            const SpanPP a = s_pp[i], b = s_pp[i - 1];
+            const SpanTC x = s_tc[i], y = s_tc[i - 1];
+            if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || x.cn != y.cn)
+              atomicAnd(&s_runok[s_aux[i] - 1], 0u);
+          }
+        }
+        __syncthreads();
+        // compact list of needy spans (sorted positions)
+        for (int i = threadIdx.x; i < m; i += NT) {
+          const unsigned long long seed = s_seed3[i];
+          s_aux[i] = (cand_tier && (seed == kEmpty || (int)(seed >> 62) >= k)) ? 1 : 0;
+        }
+        __syncthreads();
+        block_inclusive_scan<NT>(s_aux, m, s_wsum);
+        for (int i = threadIdx.x; i < m; i += NT) {
+          const int prev = i ? s_aux[i - 1] : 0;
+          if (s_aux[i] != prev) s_needy[prev] = (uint16_t)i;
+        }
+        if (threadIdx.x == 0) s_nneedy = s_aux[m - 1];
+        __syncthreads();
+      }
     }
+    const int n_needy = ranged && !count_only ? s_nneedy : 0;
 
     for (uint32_t q = sg0 + threadIdx.x; q < sg1; q += NT) {
       const uint32_t g = sig_items[q];
       const uint64_t h = gc.hash[(size_t)k * sig_cap + g];
       const int64_t t = gc.ts[g];
-      // lower_bound (h, t - w)
-      int lo = 0, hi = m;
-      const int64_t tlo = t - w;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const SpanKT e = s_kt[mid];
-        if (less_ht(e.h, e.t, h, tlo)) lo = mid + 1; else hi = mid;
-      }
+      const int lo = lower_ht(s_kt, 0, m, h, t - w);
       const int64_t thi = t + w;
       if (count_only) {
-        // upper_bound (h, t + w): hash equality == key equality for this key type
-        int a = lo, b = m;
-        while (a < b) {
-          const int mid = (a + b) >> 1;
-          const SpanKT e = s_kt[mid];
-          if (less_ht(h, thi, e.h, e.t)) b = mid; else a = mid + 1;
-        }
-        n_low += (unsigned long long)(a - lo);
+        n_low += (unsigned long long)(upper_ht(s_kt, lo, m, h, thi) - lo);
         continue;
       }
       if (lo >= m || s_kt[lo].h != h || s_kt[lo].t > thi) continue;
       const uint32_t g_pod = gc.pod[g], g_pid = gc.pid[g], g_sn = gc.svcnode[g];
       const uint64_t g_tr = gc.trace_h[g], g_cn = gc.conn_h[g];
       const int g_slot = gc.slot[g];
-      const float g_val = gc.val[g];
-      const unsigned long long g_milli = milli_units(g_val);
-      // incident sums: a signal's candidate spans share one key (pod / trace / svc+node),
-      // hence one incident group -- accumulate (group, pair count) in registers and add
-      // val x count once per run instead of once per pair (all lanes of a partition hit
-      // the same few LDS words, so per-pair atomics serialise).
+      const unsigned long long g_milli = milli_units(gc.val[g]);
+      const bool g_sn_ok = (g_sn >> 16) != 0 && (g_sn & 0xFFFF) != 0;
+
+      // ---- range accounting (pod tiers, uniform hash run) ----------------------------
+      if (ranged) {
+        const SpanPP p0 = s_pp[lo];
+        const SpanTC c0r = s_tc[lo];
+        const bool key_ok = s_runok[s_rid[lo]] && p0.pod != 0 && p0.pod == g_pod &&
+                            (k == 1 ? (p0.pid != 0 && p0.pid == g_pid) : (c0r.cn != 0 && c0r.cn == g_cn));
+        if (key_ok) {
+          const int hi = upper_ht(s_kt, lo, m, h, thi);
+          int a1 = hi, b1 = hi;  // P2 sub-range excluded from the pod+conn tier
+          if (k == 2 && p0.pid != 0 && p0.pid == g_pid) {
+            a1 = lower_ht(s_kt, lo, hi, h, t - jp.win_ns[1]);
+            b1 = upper_ht(s_kt, a1, hi, h, t + jp.win_ns[1]);
+          }
+          const int n_acc = (hi - lo) - (b1 - a1);
+          if (n_acc > 0) {
+            if (cand_tier) {
+              add_range(lo, a1);
+              add_range(b1, hi);
+              n_cand += (unsigned long long)n_acc;
+              if (do_groups) add_group(p0.grp, g_slot, g_milli, (uint32_t)n_acc);
+            } else {
+              n_low += (unsigned long long)n_acc;
+            }
+            if (track_overlap && g_sn_ok && p0.sn == g_sn && w <= jp.win_ns[3]) n_overlap += (unsigned long long)n_acc;
+            // top-3 keys only for needy spans in the accepted ranges
+            if (n_needy) {
+              for (int part = 0; part < 2; ++part) {
+                const int ra = part ? b1 : lo, rb = part ? hi : a1;
+                for (int j = lower_u16(s_needy, n_needy, ra); j < n_needy && (int)s_needy[j] < rb; ++j) {
+                  const int i = s_needy[j];
+                  const SpanTC tc = s_tc[i];
+                  if (tc.tr != 0 && tc.tr == g_tr) continue;  // a trace pair: its key is the trace pass's
+                  const int64_t dt = iabs64(t - s_kt[i].t);
+                  unsigned long long key = ((unsigned long long)k << 62) | ((unsigned long long)dt << kSigBits) |
+                                           (unsigned long long)g;
+                  if (key < s_seed3[i] && key < s_top[3 * i + 2]) {
+#pragma unroll
+                    for (int jj = 0; jj < 3; ++jj) {
+                      const unsigned long long old = atomicMin(&s_top[3 * i + jj], key);
+                      if (old == kEmpty) break;
+                      key = old > key ? old : key;
+                    }
+                  }
+                }
+              }
+            }
+          }
+          continue;
+        }
+      }
+
+      // ---- exact per-pair walk (trace tier, colliding / mixed runs, low threshold) ---
       uint32_t run_grp = 0xFFFFFFFFu, run_n = 0;
       for (int i = lo; i < m; ++i) {
         const SpanKT e = s_kt[i];
@@ -318,74 +464,80 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         const SpanPP pp = s_pp[i];
         const uint32_t p_pod = pp.pod;
         const uint64_t p_cn = tc.cn;
-        if (k == 2 && !(p_pod == g_pod && p_cn == g_cn)) continue;  // hash collision guard
-        // higher-precedence tiers (REF Match order): skip pairs found at their own tier
         const uint64_t p_tr = tc.tr;
-        if (k >= 1 && p_tr != 0 && p_tr == g_tr) continue;  // |dt| <= outer holds for every pair here
-        if (k >= 2) {
-          const uint32_t p_pid = pp.pid;
-          if (p_pod != 0 && p_pod == g_pod && p_pid != 0 && p_pid == g_pid && dt <= jp.win_ns[1]) continue;
-        }
-        if (k >= 3 && p_pod != 0 && p_pod == g_pod && p_cn != 0 && p_cn == g_cn && dt <= jp.win_ns[2]) continue;
-        if (cand_tier) {
+        // exact key equality (hash collision guard)
+        if (k == 0 && p_tr != g_tr) continue;
+        if (k == 1 && !(p_pod == g_pod && pp.pid == g_pid)) continue;
+        if (k == 2 && !(p_pod == g_pod && p_cn == g_cn)) continue;
+        const bool in_p2 = p_pod != 0 && p_pod == g_pod && pp.pid != 0 && pp.pid == g_pid && dt <= jp.win_ns[1];
+        const bool in_p3 = p_pod != 0 && p_pod == g_pod && p_cn != 0 && p_cn == g_cn && dt <= jp.win_ns[2];
+        const bool trace_eq = p_tr != 0 && p_tr == g_tr;
+        // REF tier precedence: a pair belongs to the first tier it satisfies
+        if (k == 2 && in_p2) continue;                        // P2's pair
+        if (k == 3 && (trace_eq || in_p2 || in_p3)) continue;  // higher tiers' pairs
+        // pod tiers count their trace pairs too (range accounting); the trace tier then
+        // leaves the counting of those pairs to them and only contributes the key
+        int owner = k;
+        if (k == 0) owner = in_p2 ? 1 : (in_p3 ? 2 : 0);
+        const bool tier_cand = jp.conf[k] >= jp.threshold;
+        const bool insert_key = tier_cand && !(k >= 1 && trace_eq);
+        if (insert_key) {
           unsigned long long key = ((unsigned long long)k << 62) | ((unsigned long long)dt << kSigBits) |
                                    (unsigned long long)g;
-          // slots only ever decrease, so a key >= the current 3rd best can never enter the
-          // top-3: skip the atomic cascade (most pod+pid pairs are rejected here)
-          // the seeded global bound rejects almost every lower-tier pair with one read
           if (key < s_seed3[i] && key < s_top[3 * i + 2]) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {  // LDS top-3 cascade (see top3_insert)
+            for (int j = 0; j < 3; ++j) {
               const unsigned long long old = atomicMin(&s_top[3 * i + j], key);
               if (old == kEmpty) break;
               key = old > key ? old : key;
             }
           }
-          atomicAdd(&s_cnt[i], 1u);
+        }
+        // counting: by the owning tier's accounting, fixed up when confidence classes differ
+        bool count_cand = false, count_low = false, fix_low = false, count_ovl = false;
+        if (owner == k) {
+          count_cand = tier_cand;
+          count_low = !tier_cand;
+          count_ovl = track_overlap;
+        } else {  // k == 0, pair already counted by pod tier `owner`
+          const bool owner_cand = owner == 1 ? cand1 : cand2;
+          if (tier_cand && !owner_cand) {
+            count_cand = true;
+            fix_low = true;
+          }
+        }
+        if (count_cand) {
+          atomicAdd(&s_diff[i], 1);
+          atomicAdd(&s_diff[i + 1], -1);
           ++n_cand;
-          if (do_groups) {
+          if (fix_low) --n_low;
+          if (do_groups || (k == 0 && jp.group_mode == 1 && n_groups > 0)) {
             const uint32_t grp = pp.grp;
             if (grp != run_grp) {
-              if (run_n && run_grp < (uint32_t)n_groups) {
-                if (grp_lds) {
-                  atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_milli * run_n);
-                  atomicAdd(&s_gcnt[run_grp * kSlots + g_slot], run_n);
-                } else {
-                  atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_milli * run_n);
-                  atomicAdd(gcnt + (size_t)run_grp * kSlots + g_slot, run_n);
-                }
-              }
+              add_group(run_grp, g_slot, g_milli, run_n);
               run_grp = grp;
               run_n = 0;
             }
             ++run_n;
           }
-        } else {
+        } else if (count_low) {
           ++n_low;
         }
-        if (track_overlap) {
+        if (count_ovl) {
           const uint32_t p_sn = pp.sn;
           if ((p_sn >> 16) != 0 && (p_sn & 0xFFFF) != 0 && p_sn == g_sn && dt <= jp.win_ns[3]) ++n_overlap;
         }
       }
-      if (run_n && run_grp < (uint32_t)n_groups) {
-        if (grp_lds) {
-          atomicAdd(&s_gsum[run_grp * kSlots + g_slot], g_milli * run_n);
-          atomicAdd(&s_gcnt[run_grp * kSlots + g_slot], run_n);
-        } else {
-          atomicAdd(gsum + (size_t)run_grp * kSlots + g_slot, g_milli * run_n);
-          atomicAdd(gcnt + (size_t)run_grp * kSlots + g_slot, run_n);
-        }
-      }
+      add_group(run_grp, g_slot, g_milli, run_n);
     }
     // flush this chunk's per-span candidates to the global top-3 / counts
     __syncthreads();
-    if (cand_tier) {
+    if (!count_only) {
+      block_inclusive_scan<NT>(s_diff, m, s_wsum);  // difference array -> per-span counts
       for (int i = threadIdx.x; i < m; i += NT) {
-        const uint32_t nc = s_cnt[i];
-        if (!nc) continue;
+        const int nc = s_diff[i];
         const uint32_t s = s_i[i];
-        atomicAdd(cnt + s, nc);
+        if (nc) atomicAdd(cnt + s, (uint32_t)nc);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const unsigned long long key = s_top[3 * i + j];
@@ -395,7 +547,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       }
     }
   }
-  if (do_groups && grp_lds) {
+  if (grp_lds && (do_groups || (k == 0 && (groups1 || groups2)))) {
     __syncthreads();
     for (int i = threadIdx.x; i < n_groups * kSlots; i += NT) {
       const uint32_t n = s_gcnt[i];
@@ -405,7 +557,8 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       }
     }
   }
-  // wave reduce, one atomic per wave
+  // wave reduce, one atomic per wave (n_low may go transiently negative per lane: two's
+  // complement wrap is exact in the final unsigned sum)
   for (int off = 32; off > 0; off >>= 1) {
     n_cand += __shfl_xor(n_cand, off);
     n_low += __shfl_xor(n_low, off);
