@@ -47,6 +47,8 @@ def parse():
                     help="windows replayed at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
+    ap.add_argument("--max-ahead", type=int, default=2, choices=(1, 2),
+                    help="windows the host may run ahead of the GPU (host back-pressure)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
     ap.add_argument("--wire", type=int, default=32, choices=(32, 64),
@@ -98,7 +100,7 @@ def main() -> int:
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
-                          group_scope=a.group_scope, use_graphs=not a.no_graphs)
+                          group_scope=a.group_scope, use_graphs=not a.no_graphs, max_ahead=a.max_ahead)
 
     def run(n, start):
         for i in range(n):
@@ -126,6 +128,7 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    host_us = pipe.host_issue_us()
     busy_cpu_pct, _, _ = meter.stop()
     if pg is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -216,6 +219,7 @@ def main() -> int:
         "window_latency_ms_p50": round(float(np.median(lat_ms)), 3) if lat_ms else None,
         "ref55_single_fault_macro_f1": {k: round(v, 4) for k, v in ref_f1.items()},
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
+        "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
     }
     if rank == 0:
         line = json.dumps(res)

@@ -87,6 +87,8 @@ def build_hip_ext(force: bool = False, jobs: int = 4) -> str:
     hdrs = _headers(CSRC)
     tflags, tld = torch_flags()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+    # extra -D flags for diagnostic builds (e.g. MISLO_HIP_DEFINES=-DMISLO_PROBE_PROFILE, with force)
+    common += os.environ.get("MISLO_HIP_DEFINES", "").split()
     jobs_list = []
     objs = []
     for src in HIP_SOURCES:

@@ -116,6 +116,7 @@ class Engine {
     g_part_tot = torch::empty({kKeyTypes * kParts}, i32);
     g_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
     g_items = torch::empty({kKeyTypes * N}, i32);
+    g_rec = torch::empty({(int64_t)N * (int64_t)sizeof(SigRec)}, u8);
     // span columns
     s_ts = torch::empty({S}, i64); s_trace = torch::empty({S}, i64); s_conn = torch::empty({S}, i64);
     s_pod = torch::empty({S}, i32); s_pid = torch::empty({S}, i32); s_svcnode = torch::empty({S}, i32);
@@ -125,6 +126,8 @@ class Engine {
     s_part_tot = torch::empty({kKeyTypes * kParts}, i32);
     s_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
     s_items = torch::empty({kKeyTypes * S}, i32);
+    s_rec = torch::empty({(int64_t)S * (int64_t)sizeof(SpanRec)}, u8);
+    probe_work = torch::zeros({kProbeWorkLen}, i32);
     top3 = torch::empty({3 * S}, i64); cnt = torch::empty({S}, i32);
     attrs = torch::empty({S, kSlots}, f32); conf = torch::empty({S}, f32); kernel_ms = torch::empty({S}, f32);
     // groups / incidents
@@ -220,12 +223,12 @@ class Engine {
   }
 
   SignalCols sig_cols() {
-    return SignalCols{dptr<int64_t>(g_ts), dptr<float>(g_val), dptr<uint8_t>(g_slot), dptr<uint8_t>(g_status),
+    return SignalCols{reinterpret_cast<SigRec*>(g_rec.data_ptr()), dptr<int64_t>(g_ts), dptr<float>(g_val), dptr<uint8_t>(g_slot), dptr<uint8_t>(g_status),
                       dptr<uint32_t>(g_pod), dptr<uint32_t>(g_pid), dptr<uint32_t>(g_svcnode),
                       dptr<uint64_t>(g_trace), dptr<uint64_t>(g_conn), dptr<uint64_t>(g_hash)};
   }
   SpanCols span_cols() {
-    return SpanCols{dptr<int64_t>(s_ts), dptr<uint64_t>(s_trace), dptr<uint64_t>(s_conn), dptr<uint32_t>(s_pod),
+    return SpanCols{reinterpret_cast<SpanRec*>(s_rec.data_ptr()), dptr<int64_t>(s_ts), dptr<uint64_t>(s_trace), dptr<uint64_t>(s_conn), dptr<uint32_t>(s_pod),
                     dptr<uint32_t>(s_pid), dptr<uint32_t>(s_svcnode), dptr<uint32_t>(s_group),
                     dptr<uint64_t>(s_hash)};
   }
@@ -290,7 +293,7 @@ class Engine {
     launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(),
                  dptr<uint32_t>(g_items), dptr<uint32_t>(g_part_base), sig_cap_, span_cap_, jp_,
                  dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<unsigned long long>(gsum),
-                 dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), st);
+                 dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), dptr<uint32_t>(probe_work), st);
     const float* base = nullptr;
     if (base_attrs.has_value()) {
       check_cuda(*base_attrs, "base_attrs");
@@ -378,9 +381,9 @@ class Engine {
 
   torch::Tensor counts;
   torch::Tensor g_ts, g_val, g_slot, g_status, g_pod, g_pid, g_svcnode, g_trace, g_conn, g_hash;
-  torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items;
+  torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items, g_rec, s_rec;
   torch::Tensor s_ts, s_trace, s_conn, s_pod, s_pid, s_svcnode, s_group, s_hash;
-  torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items;
+  torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, probe_work;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
   torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
   torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, pod_table;
@@ -505,7 +508,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("packet_len", &Engine::packet_len)
 #define RO(name) .def_readonly(#name, &Engine::name)
       RO(counts) RO(g_ts) RO(g_val) RO(g_slot) RO(g_status) RO(g_pod) RO(g_pid) RO(g_svcnode) RO(g_trace)
-      RO(g_conn) RO(g_hash) RO(g_part_base) RO(g_items) RO(s_ts) RO(s_hash) RO(s_part_base) RO(s_items)
+      RO(g_conn) RO(g_hash) RO(g_part_base) RO(g_items) RO(s_ts) RO(s_hash) RO(s_part_base) RO(s_items) RO(probe_work)
       RO(top3) RO(cnt) RO(attrs) RO(conf) RO(kernel_ms) RO(gsum) RO(gcnt) RO(feat) RO(labels) RO(post)
       RO(pred) RO(gconf) RO(evbits) RO(hist) RO(status_cnt) RO(misc) RO(dbg) RO(confusion) RO(stats)
       RO(stats_count) RO(packet) RO(model) RO(pod_table);

@@ -77,6 +77,18 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
   o.cols.svcnode[i] = svcnode;
   o.cols.trace_h[i] = trace_h;
   o.cols.conn_h[i] = conn_h;
+  {
+    SigRec r;
+    r.ts = ts;
+    r.tr = trace_h;
+    r.cn = conn_h;
+    r.pod = pod;
+    r.pid = pid;
+    r.sn = svcnode;
+    r.val = val;
+    r.slot = slot >= 0 ? (uint32_t)slot : kNoSlot;
+    o.cols.rec[i] = r;
+  }
   // Unsupported signal types never reach Match (REF correlator.go:73-77), and a zero
   // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
   const bool joinable = slot >= 0 && ts != 0;
@@ -252,6 +264,17 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp
     c.pid[i] = s.pid;
     c.svcnode[i] = svcnode;
     c.group[i] = s.group_id;
+    {
+      SpanRec r;
+      r.ts = s.ts_ns;
+      r.tr = s.trace_h;
+      r.cn = s.conn_h;
+      r.pod = s.pod_id;
+      r.pid = s.pid;
+      r.sn = svcnode;
+      r.grp = s.group_id;
+      c.rec[i] = r;
+    }
 #pragma unroll
     for (int k = 0; k < kKeyTypes; ++k) {
       uint64_t h = s.ts_ns != 0 ? key_hash(k, s.trace_h, s.pod_id, s.pid, s.conn_h, svcnode) : 0ull;

@@ -36,7 +36,7 @@
 namespace mislo {
 
 constexpr int kSigBits = 27;  // top-3 key: [63:62] tier, [61:27] |dt| ns, [26:0] signal idx
-constexpr int kChunk = 512;   // spans staged in LDS per pass
+constexpr int kChunk = 256;   // spans staged in LDS per pass
 
 // ---------------------------------------------------------------------------------------
 // partition scan + scatter
@@ -142,11 +142,11 @@ __device__ __forceinline__ void top3_insert(unsigned long long* slot3, unsigned 
 
 __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
 
-// Work decomposition: grid = (1024 partitions, key types, kSplit signal slices), launched
-// twice: the trace tier first, then pod+pid / pod+conn / svc+node. Keys of the pod and
-// service tiers are few and skewed, so most partitions are empty and a handful carry
-// thousands of signals; big signal lists are split over up to kSplit workgroups (never
-// below kMinPerSplit signals each: a workgroup has a fixed staging / sort / flush cost).
+// Work decomposition: two launches (the trace tier first, then pod+pid / pod+conn /
+// svc+node) of a fixed grid that dequeues items from a device-built work list (see
+// k_probe_work). Keys of the pod and service tiers are few and skewed: most of the 1024
+// partitions are empty and a handful carry thousands of signals. Empty partitions get no
+// item; a big signal list is sliced into items of kSigPerItem signals.
 //
 // Range accounting (why the pod tiers do not enumerate pairs). A signal's candidate spans
 // in a tier are one contiguous range of the partition's (hash, ts)-sorted spans. When the
@@ -175,8 +175,62 @@ struct alignas(16) SpanPP {
 };
 
 constexpr int kLdsGroups = 64;
-constexpr int kSplit = 8;
-constexpr int kMinPerSplit = 512;
+constexpr int kSigPerItem = 2048;  // signals per work item (a partition's list is sliced)
+
+// Work list for the two probe phases, rebuilt every window on the device (no host sync,
+// graph-capturable). One workgroup of 1024 threads, one partition per thread:
+//   work[0] / work[1]: item counts of phase 1 (trace) / phase 2 (pod+pid, pod+conn, svc+node)
+//   work[2] / work[3]: dequeue counters (zeroed here)
+//   items: code = key type << 28 | partition << 16 | slice << 8 | n slices.
+// Empty partitions get no item, so probe workgroups never wake for them; phase-2 items are
+// ordered by key type (enumerating tiers first, the count-only tier last).
+__global__ __launch_bounds__(1024) void k_probe_work(const uint32_t* __restrict__ span_base,
+                                                     const uint32_t* __restrict__ sig_base, int sig_per_item,
+                                                     uint32_t* __restrict__ work) {
+  __shared__ unsigned long long s[1024];
+  const int p = threadIdx.x;
+  uint32_t n[kKeyTypes];
+#pragma unroll
+  for (int k = 0; k < kKeyTypes; ++k) {
+    const int c = k * kParts + p;
+    const uint32_t ns = span_base[c + 1] - span_base[c], ng = sig_base[c + 1] - sig_base[c];
+    n[k] = (ns == 0 || ng == 0) ? 0u : min((ng + sig_per_item - 1) / (uint32_t)sig_per_item, (uint32_t)kProbeMaxSplit);
+  }
+  // packed inclusive scan: trace | pod+pid | pod+conn | svc+node counts, 16 bits each
+  const unsigned long long mine = (unsigned long long)n[0] | ((unsigned long long)n[1] << 16) |
+                                  ((unsigned long long)n[2] << 32) | ((unsigned long long)n[3] << 48);
+  s[p] = mine;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned long long x = p >= off ? s[p - off] : 0ull;
+    __syncthreads();
+    s[p] += x;
+    __syncthreads();
+  }
+  const unsigned long long tot = s[1023], excl = s[p] - mine;
+  uint32_t t[kKeyTypes], e[kKeyTypes];
+#pragma unroll
+  for (int k = 0; k < kKeyTypes; ++k) {
+    t[k] = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
+    e[k] = (uint32_t)((excl >> (16 * k)) & 0xFFFF);
+  }
+  uint32_t* items1 = work + 4;
+  uint32_t* items2 = work + 4 + kParts * kProbeMaxSplit;
+  for (uint32_t j = 0; j < n[0]; ++j) items1[e[0] + j] = (0u << 28) | ((uint32_t)p << 16) | (j << 8) | n[0];
+  uint32_t base = 0;
+#pragma unroll
+  for (int k = 1; k < kKeyTypes; ++k) {
+    for (uint32_t j = 0; j < n[k]; ++j)
+      items2[base + e[k] + j] = ((uint32_t)k << 28) | ((uint32_t)p << 16) | (j << 8) | n[k];
+    base += t[k];
+  }
+  if (p == 0) {
+    work[0] = t[0];
+    work[1] = t[1] + t[2] + t[3];
+    work[2] = 0u;
+    work[3] = 0u;
+  }
+}
 
 // In-place inclusive scan of v[0..n), n <= 2 * NT (each thread owns two adjacent entries).
 template <int NT>
@@ -235,8 +289,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups,
                                               unsigned long long* __restrict__ gsum, uint32_t* __restrict__ gcnt,
-                                              unsigned long long* __restrict__ dbg, int k_base) {
+                                              unsigned long long* __restrict__ dbg, uint32_t* __restrict__ work,
+                                              int phase) {
   // span fields packed 16 B per entry (one ds_read_b128 each)
+  static_assert(kChunk == NT, "staging keeps one span per thread");
   __shared__ SpanKT s_kt[kChunk];
   __shared__ SpanTC s_tc[kChunk];
   __shared__ SpanPP s_pp[kChunk];
@@ -250,10 +306,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
   __shared__ uint16_t s_needy[kChunk];            // sorted positions of needy spans
   __shared__ int s_wsum[NT / 64];
   __shared__ int s_nneedy;
+  __shared__ uint32_t s_item;
   __shared__ unsigned long long s_gsum[kLdsGroups * kSlots];
   __shared__ uint32_t s_gcnt[kLdsGroups * kSlots];
 
-  const int k = k_base + blockIdx.y;
   // incident sums go to one of kGroupStripes copies (folded after the join): thousands of
   // workgroups adding into the same G x 16 words would otherwise serialise in L2 atomics
   {
@@ -261,68 +317,87 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
     gsum += stripe;
     gcnt += stripe;
   }
-  const int c = k * kParts + blockIdx.x;
-  const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
-  const uint32_t gb0 = sig_base[c], gb1 = sig_base[c + 1];
-  if (sp0 == sp1 || gb0 == gb1) return;
-  const uint32_t per = max((gb1 - gb0 + kSplit - 1) / kSplit, (uint32_t)kMinPerSplit);
-  const uint32_t sg0 = gb0 + blockIdx.z * per;
-  const uint32_t sg1 = min(gb1, sg0 + per);
-  if (sg0 >= sg1) return;
-
-  const int64_t w = jp.win_ns[k];
-  const bool cand_tier = jp.conf[k] >= jp.threshold;
-  const bool count_only = (k == 3) && !cand_tier;          // broad tier: count, never enumerate
-  const bool track_overlap = (k < 3) && (jp.conf[3] < jp.threshold);
   const bool grp_lds = n_groups <= kLdsGroups;
-  const bool do_groups = cand_tier && jp.group_mode == 1 && n_groups > 0;
-  const bool ranged = (k == 1 || k == 2);                  // range accounting tiers
-  const bool cand1 = jp.conf[1] >= jp.threshold, cand2 = jp.conf[2] >= jp.threshold;
-  const bool groups1 = cand1 && jp.group_mode == 1 && n_groups > 0;
-  const bool groups2 = cand2 && jp.group_mode == 1 && n_groups > 0;
-  unsigned long long n_cand = 0, n_low = 0, n_overlap = 0;
-
-  auto add_group = [&](uint32_t grp, int slot, unsigned long long milli, uint32_t n) {
-    if (grp >= (uint32_t)n_groups || n == 0) return;
-    if (grp_lds) {
-      atomicAdd(&s_gsum[grp * kSlots + slot], milli * n);
-      atomicAdd(&s_gcnt[grp * kSlots + slot], n);
-    } else {
-      atomicAdd(gsum + (size_t)grp * kSlots + slot, milli * n);
-      atomicAdd(gcnt + (size_t)grp * kSlots + slot, n);
-    }
-  };
-  auto add_range = [&](int a, int b) {  // +1 candidate for every span of [a, b)
-    if (a < b) {
-      atomicAdd(&s_diff[a], 1);
-      atomicAdd(&s_diff[b], -1);
-    }
-  };
-
-  if (grp_lds && (do_groups || (k == 0 && (groups1 || groups2)))) {
+  const bool any_groups = jp.group_mode == 1 && n_groups > 0;
+  if (grp_lds && any_groups) {
     for (int i = threadIdx.x; i < kLdsGroups * kSlots; i += NT) {
       s_gsum[i] = 0ull;
       s_gcnt[i] = 0u;
     }
   }
+  const bool cand1 = jp.conf[1] >= jp.threshold, cand2 = jp.conf[2] >= jp.threshold;
+  unsigned long long n_cand = 0, n_low = 0, n_overlap = 0;
+  const uint32_t n_work = work[phase];
+  const uint32_t* items = work + 4 + (phase ? kParts * kProbeMaxSplit : 0);
+
+  // dynamic work queue: one item = (key type, partition, signal slice)
+  for (;;) {
+    __syncthreads();  // previous item's LDS reads are done before s_item / staging reuse
+    if (threadIdx.x == 0) s_item = atomicAdd(&work[2 + phase], 1u);
+    __syncthreads();
+    const uint32_t it = s_item;
+    if (it >= n_work) break;
+#ifdef MISLO_PROBE_PROFILE
+    unsigned long long pt = clock64(), p_stage = 0, p_sig = 0, p_flush = 0;
+#endif
+    const uint32_t code = items[it];
+    const int k = (int)(code >> 28);
+    const int part = (int)((code >> 16) & 0x3FF);
+    const uint32_t si = (code >> 8) & 0xFF, nsplit = code & 0xFF;
+    const int c = k * kParts + part;
+    const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
+    const uint32_t gb0 = sig_base[c], gb1 = sig_base[c + 1];
+    const uint32_t per = (gb1 - gb0 + nsplit - 1) / nsplit;
+    const uint32_t sg0 = gb0 + si * per;
+    const uint32_t sg1 = min(gb1, sg0 + per);
+
+    const int64_t w = jp.win_ns[k];
+    const bool cand_tier = jp.conf[k] >= jp.threshold;
+    const bool count_only = (k == 3) && !cand_tier;          // broad tier: count, never enumerate
+    const bool track_overlap = (k < 3) && (jp.conf[3] < jp.threshold);
+    const bool do_groups = cand_tier && any_groups;
+    const bool ranged = (k == 1 || k == 2);                  // range accounting tiers
+
+    auto add_group = [&](uint32_t grp, int slot, unsigned long long milli, uint32_t n) {
+      if (grp >= (uint32_t)n_groups || n == 0) return;
+      if (grp_lds) {
+        atomicAdd(&s_gsum[grp * kSlots + slot], milli * n);
+        atomicAdd(&s_gcnt[grp * kSlots + slot], n);
+      } else {
+        atomicAdd(gsum + (size_t)grp * kSlots + slot, milli * n);
+        atomicAdd(gcnt + (size_t)grp * kSlots + slot, n);
+      }
+    };
+    auto add_range = [&](int a, int b) {  // +1 candidate for every span of [a, b)
+      if (a < b) {
+        atomicAdd(&s_diff[a], 1);
+        atomicAdd(&s_diff[b], -1);
+      }
+    };
 
   for (uint32_t c0 = sp0; c0 < sp1; c0 += kChunk) {
     const int m = (int)min((uint32_t)kChunk, sp1 - c0);
     int M = 1;
     while (M < m) M <<= 1;
     __syncthreads();
-    for (int i = threadIdx.x; i < M; i += NT) {
-      if (i < m) {
-        const uint32_t s = span_items[c0 + i];
-        s_kt[i] = SpanKT{sc.hash[(size_t)k * span_cap + s], sc.ts[s]};
-        s_i[i] = s;
-      } else {
-        s_kt[i] = SpanKT{~0ull, INT64_MAX};
-        s_i[i] = 0xFFFFFFFFu;
-      }
+    // one span per thread (kChunk == NT): every global load of the chunk is issued up
+    // front and kept in registers across the sort, then written to its sorted slot
+    const int ti = threadIdx.x;
+    SpanRec rr{};
+    uint32_t my_s = 0xFFFFFFFFu;
+    unsigned long long my_seed = kEmpty;
+    if (ti < m) {
+      my_s = span_items[c0 + ti];
+      rr = sc.rec[my_s];
+      if (k > 0 && !count_only) my_seed = top3[3ull * my_s + 2];
+    }
+    if (ti < M) {
+      s_kt[ti] = ti < m ? SpanKT{key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn), rr.ts}
+                        : SpanKT{~0ull, INT64_MAX};
+      s_rid[ti] = (uint16_t)ti;  // pre-sort position, carried through the sort
     }
     __syncthreads();
-    // bitonic sort of (hash, ts, idx) ascending
+    // bitonic sort of (hash, ts, position) ascending
     for (int size = 2; size <= M; size <<= 1) {
       for (int stride = size >> 1; stride > 0; stride >>= 1) {
         for (int t = threadIdx.x; t < (M >> 1); t += NT) {
@@ -333,28 +408,32 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           const bool gt = less_ht(ej.h, ej.t, ei.h, ei.t);
           if (gt == up) {
             s_kt[i] = ej; s_kt[j] = ei;
-            uint32_t ti = s_i[i]; s_i[i] = s_i[j]; s_i[j] = ti;
+            const uint16_t tp = s_rid[i]; s_rid[i] = s_rid[j]; s_rid[j] = tp;
           }
         }
         __syncthreads();
       }
     }
-    if (!count_only) {
-      for (int i = threadIdx.x; i < m; i += NT) {
-        const uint32_t s = s_i[i];
-        s_tc[i] = SpanTC{sc.trace_h[s], sc.conn_h[s]};
-        s_pp[i] = SpanPP{sc.pod[s], sc.pid[s], sc.svcnode[s], sc.group[s]};
+    if (ti < m) s_needy[s_rid[ti]] = (uint16_t)ti;  // inverse permutation (scratch)
+    __syncthreads();
+    if (ti < m) {
+      const int i = s_needy[ti];  // this thread's span, sorted position
+      s_i[i] = my_s;
+      if (!count_only) {
+        s_tc[i] = SpanTC{rr.tr, rr.cn};
+        s_pp[i] = SpanPP{rr.pod, rr.pid, rr.sn, rr.grp};
         s_top[3 * i] = kEmpty;
         s_top[3 * i + 1] = kEmpty;
         s_top[3 * i + 2] = kEmpty;
-        const unsigned long long seed = k > 0 ? top3[3ull * s + 2] : kEmpty;
-        s_seed3[i] = seed;
+        s_seed3[i] = my_seed;
         s_diff[i] = 0;
-        // hash-run heads, and (below) whether a pair key of this tier could still enter
-        // the span's top-3 (needy)
-        s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;
         s_runok[i] = 1u;
       }
+    }
+    if (!count_only) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < m; i += NT)  // hash-run heads
+        s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;
       if (threadIdx.x == 0) s_diff[m] = 0;
       __syncthreads();
       if (ranged) {
@@ -364,7 +443,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           if (i > 0 && s_kt[i].h == s_kt[i - 1].h) {
             const SpanPP a = s_pp[i], b = s_pp[i - 1];
             const SpanTC x = s_tc[i], y = s_tc[i - 1];
-            if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || x.cn != y.cn)
+            if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || (k == 2 && x.cn != y.cn))
               atomicAnd(&s_runok[s_aux[i] - 1], 0u);
           }
         }
@@ -385,11 +464,25 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
       }
     }
     const int n_needy = ranged && !count_only ? s_nneedy : 0;
+#ifdef MISLO_PROBE_PROFILE
+    { const unsigned long long t = clock64(); p_stage += t - pt; pt = t; }
+#endif
 
-    for (uint32_t q = sg0 + threadIdx.x; q < sg1; q += NT) {
-      const uint32_t g = sig_items[q];
-      const uint64_t h = gc.hash[(size_t)k * sig_cap + g];
-      const int64_t t = gc.ts[g];
+    // signal records are prefetched one iteration ahead (their indices two ahead): each
+    // iteration's random 64-byte load overlaps the previous signal's LDS work
+    uint32_t q = sg0 + threadIdx.x;
+    uint32_t g_nx = q < sg1 ? sig_items[q] : 0u;
+    uint32_t g_nx2 = q + NT < sg1 ? sig_items[q + NT] : 0u;
+    SigRec r_nx{};
+    if (q < sg1) r_nx = gc.rec[g_nx];
+    for (; q < sg1; q += NT) {
+      const uint32_t g = g_nx;
+      const SigRec r = r_nx;
+      g_nx = g_nx2;
+      if (q + NT < sg1) r_nx = gc.rec[g_nx];
+      g_nx2 = q + 2 * NT < sg1 ? sig_items[q + 2 * NT] : 0u;
+      const uint64_t h = key_hash(k, r.tr, r.pod, r.pid, r.cn, r.sn);
+      const int64_t t = r.ts;
       const int lo = lower_ht(s_kt, 0, m, h, t - w);
       const int64_t thi = t + w;
       if (count_only) {
@@ -397,10 +490,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         continue;
       }
       if (lo >= m || s_kt[lo].h != h || s_kt[lo].t > thi) continue;
-      const uint32_t g_pod = gc.pod[g], g_pid = gc.pid[g], g_sn = gc.svcnode[g];
-      const uint64_t g_tr = gc.trace_h[g], g_cn = gc.conn_h[g];
-      const int g_slot = gc.slot[g];
-      const unsigned long long g_milli = milli_units(gc.val[g]);
+      const uint32_t g_pod = r.pod, g_pid = r.pid, g_sn = r.sn;
+      const uint64_t g_tr = r.tr, g_cn = r.cn;
+      const int g_slot = (int)r.slot;
+      const unsigned long long g_milli = milli_units(r.val);
       const bool g_sn_ok = (g_sn >> 16) != 0 && (g_sn & 0xFFFF) != 0;
 
       // ---- range accounting (pod tiers, uniform hash run) ----------------------------
@@ -511,7 +604,7 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           atomicAdd(&s_diff[i + 1], -1);
           ++n_cand;
           if (fix_low) --n_low;
-          if (do_groups || (k == 0 && jp.group_mode == 1 && n_groups > 0)) {
+          if (do_groups || (k == 0 && any_groups)) {
             const uint32_t grp = pp.grp;
             if (grp != run_grp) {
               add_group(run_grp, g_slot, g_milli, run_n);
@@ -532,11 +625,23 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
     }
     // flush this chunk's per-span candidates to the global top-3 / counts
     __syncthreads();
+#ifdef MISLO_PROBE_PROFILE
+    { const unsigned long long t = clock64(); p_sig += t - pt; pt = t; }
+#endif
     if (!count_only) {
       block_inclusive_scan<NT>(s_diff, m, s_wsum);  // difference array -> per-span counts
+      // phase 1, sole item of its partition: the only writer of these spans so far (a span
+      // has one trace key), so plain stores replace the atomic cascade
+      const bool sole = phase == 0 && nsplit == 1;
       for (int i = threadIdx.x; i < m; i += NT) {
         const int nc = s_diff[i];
         const uint32_t s = s_i[i];
+        if (sole) {
+          cnt[s] = (uint32_t)nc;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) top3[3ull * s + j] = s_top[3 * i + j];
+          continue;
+        }
         if (nc) atomicAdd(cnt + s, (uint32_t)nc);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -546,8 +651,25 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         }
       }
     }
+#ifdef MISLO_PROBE_PROFILE
+    __syncthreads();
+    { const unsigned long long t = clock64(); p_flush += t - pt; pt = t; }
+#endif
   }
-  if (grp_lds && (do_groups || (k == 0 && (groups1 || groups2)))) {
+#ifdef MISLO_PROBE_PROFILE
+  // per key type: items, signals, span chunks, stage / signal-loop / flush cycles
+  if (threadIdx.x == 0) {
+    unsigned long long* pr = reinterpret_cast<unsigned long long*>(work + kProbeProfOff) + 8 * k;
+    atomicAdd(pr + 0, 1ull);
+    atomicAdd(pr + 1, (unsigned long long)(sg1 - sg0));
+    atomicAdd(pr + 2, (unsigned long long)((sp1 - sp0 + kChunk - 1) / kChunk));
+    atomicAdd(pr + 3, p_stage);
+    atomicAdd(pr + 4, p_sig);
+    atomicAdd(pr + 5, p_flush);
+  }
+#endif
+  }  // work loop
+  if (grp_lds && any_groups) {
     __syncthreads();
     for (int i = threadIdx.x; i < n_groups * kSlots; i += NT) {
       const uint32_t n = s_gcnt[i];
@@ -691,24 +813,24 @@ void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk,
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
                   const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
-                  uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream) {
+                  uint32_t* gcnt, unsigned long long* dbg, uint32_t* work, hipStream_t stream) {
   // phase 1: trace tier; phase 2: pod+pid, pod+conn, svc+node seeded with phase 1's top-3.
-  // MISLO_PROBE_PHASES=1 runs all four key types in one launch (diagnostic knob).
-  static const int phases = [] {
-    const char* v = getenv("MISLO_PROBE_PHASES");
-    return (v && v[0] == '1') ? 1 : 2;
+  // Both phases pull items from the device-built work list. Diagnostic knobs (read once):
+  // MISLO_PROBE_GRID workgroups per phase, MISLO_PROBE_ITEM signals per work item.
+  static const int grid = [] {
+    const char* v = getenv("MISLO_PROBE_GRID");
+    const int x = v ? atoi(v) : 1024;
+    return x >= 1 && x <= 65536 ? x : 1024;
   }();
-  if (phases == 1) {
-    hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes, kSplit), dim3(256), 0, stream, sc, span_items,
-                       span_base, gc, sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg,
-                       0);
-    return;
-  }
-  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, 1, kSplit), dim3(256), 0, stream, sc, span_items, span_base, gc,
-                     sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg, 0);
-  hipLaunchKernelGGL((k_probe<256>), dim3(kParts, kKeyTypes - 1, kSplit), dim3(256), 0, stream, sc, span_items,
-                     span_base, gc, sig_items, sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg,
-                     1);
+  static const int per_item = [] {
+    const char* v = getenv("MISLO_PROBE_ITEM");
+    const int x = v ? atoi(v) : kSigPerItem;
+    return x >= 1 ? x : kSigPerItem;
+  }();
+  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(1024), 0, stream, span_base, sig_base, per_item, work);
+  for (int phase = 0; phase < 2; ++phase)
+    hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, sc, span_items, span_base, gc, sig_items,
+                       sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);
 }
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,

@@ -74,7 +74,28 @@ struct alignas(64) Span {
 static_assert(sizeof(Span) == 64, "Span must be 64 bytes");
 
 // Decoded signal columns (structure of arrays, one entry per event).
+// Row records of the fields the join reads per (signal, key type) visit: one 64-byte line
+// per random access instead of one line per column.
+struct alignas(64) SigRec {
+  int64_t ts;
+  uint64_t tr;
+  uint64_t cn;
+  uint32_t pod, pid, sn;
+  float val;
+  uint32_t slot;  // kNoSlot = unsupported
+  uint32_t pad[5];
+};
+struct alignas(64) SpanRec {
+  int64_t ts;
+  uint64_t tr;
+  uint64_t cn;
+  uint32_t pod, pid, sn, grp;
+  uint32_t pad[6];
+};
+static_assert(sizeof(SigRec) == 64 && sizeof(SpanRec) == 64, "row records are one cache line");
+
 struct SignalCols {
+  SigRec* rec;
   int64_t* ts;
   float* val;
   uint8_t* slot;      // kNoSlot = unsupported / unknown type
@@ -88,6 +109,7 @@ struct SignalCols {
 };
 
 struct SpanCols {
+  SpanRec* rec;
   int64_t* ts;
   uint64_t* trace_h;
   uint64_t* conn_h;

@@ -43,7 +43,11 @@ void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk,
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
                   const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
-                  uint32_t* gcnt, unsigned long long* dbg, hipStream_t stream);
+                  uint32_t* gcnt, unsigned long long* dbg, uint32_t* work, hipStream_t stream);
+// probe work list: 4 header words + one word per (key type, partition, signal slice)
+constexpr int kProbeMaxSplit = 16;
+constexpr int kProbeProfOff = 4 + 4 * 1024 * kProbeMaxSplit;  // MISLO_PROBE_PROFILE counters (u64 [4][8])
+constexpr int kProbeWorkLen = kProbeProfOff + 64;
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
                      const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,
                      float* attrs, float* conf, float* kernel_ms, int n_groups, unsigned long long* gsum, uint32_t* gcnt,

@@ -34,6 +34,8 @@ from ..models.metrics import macro_f1_from_confusion
 from ..ops.engine import GpuEngine, decode_debug, model_bytes
 from ..signals import catalog
 
+_HOST_TRACE = bool(__import__("os").environ.get("MISLO_HOST_TRACE"))
+
 PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16)  # hist, status, misc(+16 value sums), dbg, confusion, stats, count
 
 
@@ -107,7 +109,7 @@ class WindowPipeline:
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, process_group=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, group_scope: str = "rank",
-                 use_graphs: bool = True):
+                 use_graphs: bool = True, max_ahead: int = 2):
         import torch
 
         self.torch = torch
@@ -129,6 +131,10 @@ class WindowPipeline:
         # and replayed: window launch cost becomes one graph launch
         self.use_graphs = use_graphs
         self.graphs: Dict[tuple, object] = {}
+        # host back-pressure: submit(i) first waits until window i - max_ahead has computed.
+        # Stream-ordered waits alone let the host run arbitrarily far ahead; the runtime then
+        # stalls the host for milliseconds at a time once its command queues fill
+        self.max_ahead = min(2, max(1, int(max_ahead)))  # events exist for the last 2 windows
         self.engine = GpuEngine(sig_cap, span_cap, group_cap, device, window_ms, threshold, fanout, group_mode)
         self.eng = self.engine.eng
         L = int(self.engine.mod.PACKET_LEN)
@@ -143,6 +149,7 @@ class WindowPipeline:
             self.labels_dev = [torch.full((group_cap,), -1, dtype=torch.int32, device=self.dev) for _ in range(2)]
             self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(2)]
             self.totals = torch.zeros(L, dtype=torch.float64, device=self.dev)
+            self.host_s = [0.0, 0.0, 0.0, 0]
             self.stats_off = sum(PACKET_LAYOUT[:5])
             self.stats_acc = torch.zeros(PACKET_LAYOUT[5] + PACKET_LAYOUT[6], dtype=torch.float64, device=self.dev)
             p0 = np.zeros((16, 16), dtype=np.float64)
@@ -193,9 +200,12 @@ class WindowPipeline:
 
     # ---------------------------------------------------------------------------------
     def submit(self, w: StagedWindow, with_labels: bool = True) -> None:
+        t_enter = time.perf_counter()
         torch = self.torch
         b = self.i % 2
         cs, ks, ms = self.copy_stream, self.compute_stream, self.comm_stream
+        if self.i >= self.max_ahead:
+            self.compute_done[(self.i - self.max_ahead) % 2].synchronize()
         # H2D into buffer b once window i-2 (the last user of b) finished computing
         cs.wait_event(self.compute_done[b])
         if w.pod_table is not None:
@@ -204,13 +214,23 @@ class WindowPipeline:
                 self.drain()
                 self.engine.set_pod_table(w.pod_table)
                 self.pod_key = key
+        tr = [time.perf_counter()] if _HOST_TRACE else None
         with torch.cuda.stream(cs):
             nb = w.n_events * w.wire
             self.ev_dev[b][:nb].copy_(w.ev[:nb], non_blocking=True)
+            if tr: tr.append(time.perf_counter())
             self.sp_dev[b][: w.n_spans * 64].copy_(w.sp[: w.n_spans * 64], non_blocking=True)
+            if tr: tr.append(time.perf_counter())
             self.counts_dev[b].copy_(w.counts, non_blocking=True)
+            if tr: tr.append(time.perf_counter())
             self.labels_dev[b].copy_(w.labels, non_blocking=True)
+            if tr: tr.append(time.perf_counter())
             self.h2d_done[b].record(cs)
+        if tr:
+            tr.append(time.perf_counter())
+            print("[host-trace] pre %.1f ev %.1f sp %.1f counts %.1f labels %.1f record %.1f us" % (
+                1e6 * (tr[0] - t_enter), *(1e6 * (tr[j + 1] - tr[j]) for j in range(5))), flush=True)
+        t_copy = time.perf_counter()
         ks.wait_event(self.h2d_done[b])
         ks.wait_event(self.comm_done[b])  # packet[b] no longer being reduced / read
         with torch.cuda.stream(ks):
@@ -240,6 +260,7 @@ class WindowPipeline:
             with torch.cuda.stream(ks):
                 self._run_window(b, w, with_labels)
                 self.compute_done[b].record(ks)
+        t_compute = time.perf_counter()
         ms.wait_event(self.compute_done[b])
         with torch.cuda.stream(ms):
             if self.pg is not None:
@@ -247,6 +268,12 @@ class WindowPipeline:
             self.totals.add_(self.packet_dev[b])
             self.packet_host[b].copy_(self.packet_dev[b], non_blocking=True)
             self.comm_done[b].record(ms)
+        t_exit = time.perf_counter()
+        hs = self.host_s  # host time spent issuing: copies / compute / comm
+        hs[0] += t_copy - t_enter
+        hs[1] += t_compute - t_copy
+        hs[2] += t_exit - t_compute
+        hs[3] += 1
         self.i += 1
         # fold window i-2 (this call's predecessor's predecessor is certainly far along;
         # folding i-1 would stall the host on the window just queued)
@@ -303,6 +330,13 @@ class WindowPipeline:
     def reset_totals(self) -> None:
         self.drain()
         self.totals.zero_()
+        self.host_s = [0.0, 0.0, 0.0, 0]
+
+    def host_issue_us(self) -> Dict[str, float]:
+        """Mean host time per submitted window spent issuing each stream's work (us)."""
+        n = max(self.host_s[3], 1)
+        return {"copy": 1e6 * self.host_s[0] / n, "compute": 1e6 * self.host_s[1] / n,
+                "comm": 1e6 * self.host_s[2] / n}
 
     def summary(self) -> Dict[str, object]:
         self.drain()

@@ -78,6 +78,17 @@ def main():
     res["total_ms"] = tot
     res["events_per_s_compute"] = a.events / (tot / 1e3)
     res["debug"] = eng.outputs().debug
+    if os.environ.get("MISLO_HIP_DEFINES", "").find("MISLO_PROBE_PROFILE") >= 0:
+        # probe cycle counters (diagnostic build): per key type, summed over every run
+        pw = e.probe_work.cpu().numpy()
+        pr = pw[4 + 4 * 1024 * 16:].view(np.uint64).reshape(4, 8).astype(np.float64)
+        runs = a.iters + 3
+        res["probe_profile"] = {
+            name: {"items": pr[k, 0] / runs, "signals": pr[k, 1] / runs, "chunks": pr[k, 2] / runs,
+                   "stage_kcyc_per_item": pr[k, 3] / max(pr[k, 0], 1) / 1e3,
+                   "signal_kcyc_per_item": pr[k, 4] / max(pr[k, 0], 1) / 1e3,
+                   "flush_kcyc_per_item": pr[k, 5] / max(pr[k, 0], 1) / 1e3}
+            for k, name in enumerate(["trace", "pod_pid", "pod_conn", "svc_node"])}
     print(json.dumps(res, indent=1))
 
 
