@@ -51,8 +51,9 @@ def parse():
                     help="windows the host may run ahead of the GPU (host back-pressure)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", type=int, default=32, choices=(32, 64),
-                    help="event record bytes on PCIe: 32 = compact (interned ids), 64 = full")
+    ap.add_argument("--wire", type=int, default=20, choices=(20, 32, 64),
+                    help="event record bytes on PCIe: 20 = EVENT20 (window-relative ts, interned contexts), "
+                         "32 = compact (interned ids), 64 = full")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -93,10 +94,10 @@ def main() -> int:
                        n_services=a.services, seed=a.seed, shard=rank)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
-    from llm_slo_ebpf_toolkit_amd.collector.records import ConnInterner
-    interner = ConnInterner()
+    from llm_slo_ebpf_toolkit_amd.collector.records import ConnInterner, CtxInterner
+    interner, ctx_interner = ConnInterner(), CtxInterner()
     staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, a.services, w.group_domains,
-                           wire=a.wire, interner=interner) for w in wins]
+                           wire=a.wire, interner=interner, ctx_interner=ctx_interner) for w in wins]
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
@@ -177,7 +178,7 @@ def main() -> int:
         for name, model in (("bayes_ref", NaiveBayes.ref()), (a.model, pipe.host_model())):
             eng.set_model(model)
             eng.eng.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
-            eng.eng.counts.copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
+            eng.eng.counts[:4].copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
             eng.eng.bind_io(eng.eng.counts, eng.eng.labels, eng.eng.packet)
             eng.eng.posterior(False)
             pred = eng.eng.pred[: len(samples)].cpu().numpy()

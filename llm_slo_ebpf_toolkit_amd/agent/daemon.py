@@ -162,7 +162,7 @@ class AgentOptions:
     device: int = 0
     model: str = "bayes"
     min_confidence: float = 0.5
-    wire: int = 32
+    wire: int = 20
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -359,15 +359,15 @@ class Agent:
             # measures the agent, not the synthetic trace generator.
             import torch
 
-            from ..collector.records import ConnInterner
+            from ..collector.records import ConnInterner, CtxInterner
             from ..pipeline.window import stage_window
 
-            it = ConnInterner()
+            it, xi = ConnInterner(), CtxInterner()
             pool = []
             for _ in range(4):
                 w = gen.next_window()
                 pool.append(stage_window(torch, w.events, w.spans, min(w.n_groups, o.window_groups), None,
-                                         o.window_groups, None, wire=o.wire, interner=it))
+                                         o.window_groups, None, wire=o.wire, interner=it, ctx_interner=xi))
             names = [f"svc-{g + 1}" for g in range(o.window_groups)]
             i = 0
             while True:

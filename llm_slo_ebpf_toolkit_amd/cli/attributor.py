@@ -56,7 +56,7 @@ def gpu_attributions(samples: List[FaultSample], mode: str):
     eng.set_model(model)
     e = eng.eng
     e.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
-    e.counts.copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
+    e.counts[:4].copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
     e.bind_io(e.counts, e.labels, e.packet)
     e.posterior(False)
     post = e.post[: len(samples)].cpu().numpy()

@@ -56,6 +56,15 @@ EVENT32 = np.dtype([
 ])
 assert EVENT32.itemsize == 32
 
+# 20-byte wire record: the window's base timestamp travels once per window (counts[4..5]),
+# pod / pid / connection / svc|node travel once per distinct context (the device context
+# table, CtxInterner); only the trace hash stays per event. 5/8 of EVENT32's PCIe bytes.
+EVENT20 = np.dtype({"names": ["ts_off", "ctx_type", "value_milli", "trace_h"],
+                    "formats": ["<u4", "<u4", "<u4", "<u8"],
+                    "offsets": [0, 4, 8, 12], "itemsize": 20})
+TS_ZERO = 0xFFFFFFFF  # ts_off of a zero timestamp (never joins)
+assert EVENT20.itemsize == 20
+
 SPAN = np.dtype([
     ("ts_ns", "<i8"),        # 0
     ("trace_h", "<u8"),      # 8
@@ -217,25 +226,55 @@ class ConnInterner:
         return out[inv]
 
 
-def to_compact(events: np.ndarray, interner: "ConnInterner") -> np.ndarray:
-    """EVENT (64 B) -> EVENT32 (32 B): milli-unit fixed point values, interned conn ids."""
-    out = np.zeros(events.shape[0], dtype=EVENT32)
-    out["ts_ns"] = events["ts_ns"]
-    out["trace_h"] = events["trace_h"]
+def _milli_values(events: np.ndarray) -> np.ndarray:
     scale = np.ones(65536, dtype=np.float64)
     for s in catalog.SIGNALS:
         scale[s.kernel_type] = s.decode_scale
     st = events["signal_type"].astype(np.int64)
     milli = np.rint(events["value"].astype(np.float64) * scale[st] * 1000.0)
-    out["value_milli"] = np.clip(milli, 0, 0xFFFFFFFF).astype(np.uint32)
-    out["pid"] = events["pid"]
-    out["pod_id"] = events["pod_id"]
+    return np.clip(milli, 0, 0xFFFFFFFF).astype(np.uint32)
+
+
+def _conn_keys(events: np.ndarray) -> np.ndarray:
     conn = events["conn_h"].copy()
     derived = conn_hash_np(events["src_port"], events["dst_port"], events["dst_ip"])
-    conn = np.where(conn == 0, derived, conn)
-    cid = interner.ids(conn)
-    out["type_conn"] = (st.astype(np.uint32) & np.uint32(0xFF)) | (cid << np.uint32(8))
+    return np.where(conn == 0, derived, conn)
+
+
+def to_compact(events: np.ndarray, interner: "ConnInterner") -> np.ndarray:
+    """EVENT (64 B) -> EVENT32 (32 B): milli-unit fixed point values, interned conn ids."""
+    out = np.zeros(events.shape[0], dtype=EVENT32)
+    out["ts_ns"] = events["ts_ns"]
+    out["trace_h"] = events["trace_h"]
+    out["value_milli"] = _milli_values(events)
+    out["pid"] = events["pid"]
+    out["pod_id"] = events["pod_id"]
+    cid = interner.ids(_conn_keys(events))
+    st = events["signal_type"].astype(np.uint32)
+    out["type_conn"] = (st & np.uint32(0xFF)) | (cid << np.uint32(8))
     return out
+
+
+def to_wire20(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner"):
+    """EVENT (64 B) -> (EVENT20 (20 B), t_base): timestamps relative to the window's
+    earliest non-zero timestamp, interned (pod, pid, conn, svc|node) contexts. Raises
+    ValueError when the window spans 2^32 - 1 ns or more (use EVENT32 then)."""
+    out = np.zeros(events.shape[0], dtype=EVENT20)
+    ts = events["ts_ns"].astype(np.int64)
+    nz = ts != 0
+    t_base = int(ts[nz].min()) if nz.any() else 0
+    off = ts - t_base
+    if nz.any() and int(off[nz].max()) >= TS_ZERO:
+        raise ValueError("window spans >= 2^32 ns: not representable in EVENT20")
+    out["ts_off"] = np.where(nz, off, TS_ZERO).astype(np.uint32)
+    out["value_milli"] = _milli_values(events)
+    out["trace_h"] = events["trace_h"]
+    cid = conns.ids(_conn_keys(events))
+    sn = (events["svc_id"].astype(np.uint32) << np.uint32(16)) | events["node_id"].astype(np.uint32)
+    ctx = ctxs.ids(events["pod_id"], events["pid"], cid, sn)
+    st = events["signal_type"].astype(np.uint32)
+    out["ctx_type"] = (st & np.uint32(0xFF)) | (ctx << np.uint32(8))
+    return out, t_base
 
 
 def compact_spans(spans: np.ndarray, interner: "ConnInterner") -> np.ndarray:
@@ -243,6 +282,51 @@ def compact_spans(spans: np.ndarray, interner: "ConnInterner") -> np.ndarray:
     out = spans.copy()
     out["conn_h"] = interner.ids(spans["conn_h"]).astype(np.uint64)
     return out
+
+
+class CtxInterner:
+    """(pod, pid, conn id, svc<<16|node) -> dense 24-bit context id; id 0 is the all-zero
+    context. ``table()`` is the device context table (int32 [n, 4]) indexed by id. Ids are
+    stable for the agent's lifetime, so the table only grows (and is re-uploaded then)."""
+
+    MAX_IDS = 1 << 24
+
+    def __init__(self):
+        self._ids = {(0, 0, 0, 0): 0}
+        self._rows = [(0, 0, 0, 0)]
+        self._table = None
+
+    def __len__(self) -> int:
+        return len(self._rows)
+
+    def ids(self, pod, pid, cid, sn) -> np.ndarray:
+        rows = np.stack([np.asarray(x).astype(np.uint32) for x in (pod, pid, cid, sn)], axis=1)
+        if rows.shape[0] == 0:
+            return np.zeros(0, dtype=np.uint32)
+        r64 = rows.astype(np.uint64)
+        key = (r64[:, 0] * np.uint64(0x9E3779B97F4A7C15)) ^ (r64[:, 1] * np.uint64(0xC2B2AE3D27D4EB4F)) ^ \
+              (r64[:, 2] * np.uint64(0x165667B19E3779F9)) ^ (r64[:, 3] * np.uint64(0xD6E8FEB86659FD93))
+        _, first, inv = np.unique(key, return_index=True, return_inverse=True)
+        uniq_rows = rows[first]
+        if not np.array_equal(uniq_rows[inv], rows):  # 64-bit key collision: exact path
+            uniq_rows, inv = np.unique(rows, axis=0, return_inverse=True)
+        out = np.empty(uniq_rows.shape[0], dtype=np.uint32)
+        for j, r in enumerate(map(tuple, uniq_rows.tolist())):
+            v = self._ids.get(r)
+            if v is None:
+                v = len(self._rows)
+                if v >= self.MAX_IDS:
+                    raise OverflowError("more than 2^24 interned contexts")
+                self._ids[r] = v
+                self._rows.append(r)
+                self._table = None
+            out[j] = v
+        return out[np.asarray(inv).reshape(-1)]
+
+    def table(self) -> np.ndarray:
+        if self._table is None:
+            self._table = np.array(self._rows, dtype=np.uint32).reshape(-1, 4).view(np.int32)
+        return self._table
 
 
 def string_hash64(s: str) -> int:

@@ -105,7 +105,7 @@ class Engine {
     const int64_t N = sig_cap_, S = span_cap_, G = group_cap_;
     nblk_sig_ = decode_grid(sig_cap_);
     nblk_span_ = decode_grid(span_cap_);
-    counts = torch::zeros({4}, i32);
+    counts = torch::zeros({8}, i32);  // n_ev, n_spans, n_groups, n_local, t_base lo/hi, n_ctx (wire 20)
     // signal columns
     g_ts = torch::empty({N}, i64); g_val = torch::empty({N}, f32); g_slot = torch::empty({N}, u8);
     g_status = torch::empty({N}, u8); g_pod = torch::empty({N}, i32); g_pid = torch::empty({N}, i32);
@@ -142,6 +142,7 @@ class Engine {
     stats = torch::empty({32, 32}, f64); stats_count = torch::empty({kMaxDomains}, f64);
     packet = torch::empty({kPacketLen}, f64);
     pod_table = torch::zeros({1}, i32);
+    ctx_table = torch::zeros({1, 4}, i32);
     model = torch::zeros({(int64_t)sizeof(PosteriorModel)}, u8);
     join_defaults();
   }
@@ -266,6 +267,36 @@ class Engine {
                      dptr<uint32_t>(g_items), cur_stream());
   }
 
+  // context id -> {pod, pid, conn id, svc<<16|node} (int32 [n, 4]) for 20-byte records
+  void set_ctx_table(torch::Tensor table) {
+    check_cuda(table, "ctx_table");
+    if (table.scalar_type() != torch::kInt32 || table.dim() != 2 || table.size(1) != 4 || !table.is_contiguous())
+      throw std::invalid_argument("ctx_table must be contiguous int32 [n, 4]");
+    ctx_table = table;
+  }
+
+  // events: device buffer of 20-byte records (>= sig_cap * 20 bytes); counts[4..5] = t_base,
+  // counts[6] = valid context-table rows (0 = all)
+  void decode_w20(torch::Tensor events) {
+    check_cuda(events, "events");
+    if (events.nbytes() < (size_t)sig_cap_ * 20)
+      throw std::invalid_argument("events buffer must hold sig_cap 20-byte records");
+    if (counts.numel() < 7) throw std::invalid_argument("wire 20 needs counts int32[>= 7] (t_base, n_ctx)");
+    launch_decode_w20(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
+                      (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
+                      dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
+    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
+                     dptr<uint32_t>(g_items), cur_stream());
+  }
+
+  void decode_wire(torch::Tensor events, int64_t wire) {
+    if (wire == 32) decode_compact(events);
+    else if (wire == 20) decode_w20(events);
+    else if (wire == 64) decode(events);
+    else throw std::invalid_argument("wire must be 64, 32 or 20");
+  }
+
   void decode_ref(torch::Tensor events, int64_t pod, int64_t svcnode, int64_t trace_h) {
     check_cuda(events, "events");
     if (events.nbytes() < (size_t)sig_cap_ * 40)
@@ -334,11 +365,11 @@ class Engine {
   }
 
   // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0].
-  // wire: 64 = Event records, 32 = compact EventC32 records
+  // wire: 64 = Event records, 32 = compact EventC32 records, 20 = EventC20 records
   void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn,
                   int64_t wire) {
     reset_window();
-    if (wire == 32) decode_compact(events); else decode(events);
+    decode_wire(events, wire);
     join(spans, n_groups, c10::nullopt);
     posterior(with_labels);
     if (learn) accumulate_stats(c10::nullopt);
@@ -349,7 +380,7 @@ class Engine {
   //   run_window_pre -> all_reduce(gsum), all_reduce(gcnt) -> run_window_post
   void run_window_pre(torch::Tensor events, torch::Tensor spans, int64_t n_groups, int64_t wire) {
     reset_window();
-    if (wire == 32) decode_compact(events); else decode(events);
+    decode_wire(events, wire);
     join(spans, n_groups, c10::nullopt);
   }
 
@@ -386,7 +417,7 @@ class Engine {
   torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, probe_work;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
   torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
-  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, pod_table;
+  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, pod_table, ctx_table;
 
  private:
   int sig_cap_, span_cap_, group_cap_;
@@ -490,6 +521,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("decode_ref", &Engine::decode_ref)
       .def("decode_compact", &Engine::decode_compact)
       .def("set_pod_table", &Engine::set_pod_table)
+      .def("set_ctx_table", &Engine::set_ctx_table)
+      .def("decode_w20", &Engine::decode_w20)
+      .def("decode_wire", &Engine::decode_wire)
       .def("join", &Engine::join, py::arg("spans"), py::arg("n_groups"), py::arg("base_attrs") = py::none())
       .def("posterior", &Engine::posterior)
       .def("accumulate_stats", &Engine::accumulate_stats, py::arg("weights") = py::none())

@@ -196,6 +196,58 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
   }
 }
 
+// 20-byte records: 5/8 of the compact record's PCIe bytes. The window base timestamp is
+// counts[4] | counts[5] << 32; context ids resolve through the device context table
+// (counts[6] valid rows).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_decode_w20(const EventC20* __restrict__ ev, const int* __restrict__ n_ptr,
+                                                   int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
+                                                   DecodeOut o) {
+  __shared__ uint32_t s_hist[kSlots * kBuckets];
+  __shared__ uint32_t s_status[kSlots * 3];
+  __shared__ uint32_t s_part[kKeyTypes * kParts];
+  __shared__ unsigned long long s_sum[kSlots];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
+  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
+  __syncthreads();
+
+  const int n = min(*n_ptr, cap);
+  const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
+  const int64_t t_base = (int64_t)(((uint64_t)(uint32_t)n_ptr[5] << 32) | (uint32_t)n_ptr[4]);
+  // counts[6] = rows of the (fixed-capacity, append-only) context table valid this window
+  if (n_ptr[6] > 0) n_ctx = min(n_ptr[6], n_ctx);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  int unsupported = 0, zero_ts = 0;
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const EventC20 e = ev[i];
+    const int st = (int)(e.ctx_type & 0xFFu);
+    const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
+    const float val = (float)((double)e.value_milli * 1e-3);
+    const uint32_t cid = e.ctx_type >> 8;
+    const uint4 cx = cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
+    const int64_t ts = e.ts_off == kTsZero ? 0 : t_base + (int64_t)e.ts_off;
+    const uint64_t tr = ((uint64_t)e.tr_hi << 32) | e.tr_lo;
+    decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, s_hist, s_status, s_part, s_sum,
+               unsupported, zero_ts, i < n_local);
+  }
+  __syncthreads();
+  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
+  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
+  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
+  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
+  for (int off = 32; off > 0; off >>= 1) {
+    unsupported += __shfl_xor(unsupported, off);
+    zero_ts += __shfl_xor(zero_ts, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
+    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
+  }
+}
+
 // REF 40-byte records: REF units (count stays count, cpu_steal raw ns, else ns/1e6) and
 // workload identity supplied by the consumer (REF EventMetadata, ringbuf.go:19-26).
 template <int NT>
@@ -313,6 +365,15 @@ void launch_decode_compact(const void* ev, const int* n_dev, int cap, const uint
   constexpr int NT = 256;
   hipLaunchKernelGGL((k_decode_compact<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, (const EventC32*)ev, n_dev,
                      cap, pod_svcnode, n_pods, o);
+}
+
+void launch_decode_w20(const void* ev, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
+                       const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                       unsigned long long* misc, hipStream_t stream) {
+  DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
+  constexpr int NT = 256;
+  hipLaunchKernelGGL((k_decode_w20<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, (const EventC20*)ev, n_dev,
+                     cap, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, o);
 }
 
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,

@@ -49,6 +49,18 @@ struct alignas(32) EventC32 {
 };
 static_assert(sizeof(EventC32) == 32, "EventC32 must be 32 bytes");
 
+// 20-byte wire record (collector/records.py EVENT20): timestamp as an offset from the
+// window base (counts[4..5]), workload identity as an interned context id that indexes
+// the device context table {pod, pid, conn id, svc<<16|node}; trace hash kept whole.
+struct EventC20 {
+  uint32_t ts_off;       // ts - t_base; kTsZero = zero timestamp (never joins)
+  uint32_t ctx_type;     // bits 0-7 signal type, bits 8-31 context id
+  uint32_t value_milli;  // value in 1/1000 of the signal's output unit
+  uint32_t tr_lo, tr_hi;
+};
+static_assert(sizeof(EventC20) == 20, "EventC20 must be 20 bytes");
+constexpr uint32_t kTsZero = 0xFFFFFFFFu;
+
 // REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).
 struct __attribute__((packed)) RefEvent {
   uint32_t pid, tid;

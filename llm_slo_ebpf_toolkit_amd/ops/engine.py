@@ -105,7 +105,7 @@ class GpuEngine:
             self.sp_dev = torch.zeros(span_cap * 64, dtype=torch.uint8, device=self.device)
             self.ev_host = torch.empty(sig_cap * 64, dtype=torch.uint8, pin_memory=True)
             self.sp_host = torch.empty(span_cap * 64, dtype=torch.uint8, pin_memory=True)
-            self.cnt_host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+            self.cnt_host = torch.zeros(8, dtype=torch.int32, pin_memory=True)
             self.lab_host = torch.full((group_cap,), -1, dtype=torch.int32, pin_memory=True)
             self.copy_stream = torch.cuda.Stream(self.device)
         self.sig_cap, self.span_cap, self.group_cap = sig_cap, span_cap, group_cap
@@ -128,19 +128,29 @@ class GpuEngine:
             self.eng.set_pod_table(t)
             self.torch.cuda.synchronize(self.device)
 
-    def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None):
+    def set_ctx_table(self, table: np.ndarray) -> None:
+        """context id -> {pod, pid, conn id, svc<<16|node} table used by 20-byte EVENT20 records."""
+        with self.torch.cuda.device(self.device):
+            t = self.torch.from_numpy(np.ascontiguousarray(table, dtype=np.int32).reshape(-1, 4)).to(self.device)
+            self.eng.set_ctx_table(t)
+            self.torch.cuda.synchronize(self.device)
+
+    def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None,
+              t_base: int = 0):
         """Copy records into pinned staging (host memcpy, no GPU work). ``events`` may be
-        64-byte EVENT or 32-byte EVENT32 records (the latter needs ``set_pod_table``)."""
+        64-byte EVENT, 32-byte EVENT32 (needs ``set_pod_table``) or 20-byte EVENT20 records
+        (needs ``set_ctx_table`` and the window base ``t_base``)."""
         n, s = events.shape[0], spans.shape[0]
         if n > self.sig_cap or s > self.span_cap or n_groups > self.group_cap:
             raise ValueError("window exceeds engine capacity")
-        if events.dtype not in (records.EVENT, records.EVENT32) or spans.dtype != records.SPAN:
-            raise TypeError("events/spans must use the EVENT|EVENT32/SPAN record dtypes")
+        if events.dtype not in (records.EVENT, records.EVENT32, records.EVENT20) or spans.dtype != records.SPAN:
+            raise TypeError("events/spans must use the EVENT|EVENT32|EVENT20/SPAN record dtypes")
         self.wire = events.dtype.itemsize
         self.ev_host.numpy()[: n * self.wire] = events.view(np.uint8).reshape(-1)
         self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)
         c = self.cnt_host.numpy()
-        c[:] = (n, s, n_groups, 0)
+        tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
+        c[:] = np.array([n, s, n_groups, 0, tb & 0xFFFFFFFF, tb >> 32, 0, 0], dtype=np.uint32).view(np.int32)
         lab = self.lab_host.numpy()
         lab[:] = -1
         if labels is not None:

@@ -84,6 +84,31 @@ def decode_compact(ev: np.ndarray, pod_svcnode: np.ndarray) -> Decoded:
                    (tc >> np.uint32(8)).astype(np.uint64))
 
 
+def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
+    """k_decode_w20: EVENT20 records with the window base and the context table."""
+    type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
+    for s in catalog.SIGNALS:
+        if s.kernel_type < 256:
+            type_slot[s.kernel_type] = s.slot
+    ct = ev["ctx_type"].astype(np.uint32)
+    st = (ct & np.uint32(0xFF)).astype(np.int64)
+    slot = type_slot[st]
+    val = (ev["value_milli"].astype(np.float64) * 1e-3).astype(np.float32)
+    warn = np.array([s.warn for s in catalog.SIGNALS], dtype=np.float32)
+    err = np.array([s.error for s in catalog.SIGNALS], dtype=np.float32)
+    ok = slot != NO_SLOT
+    sl = np.where(ok, slot, 0)
+    status = np.where(ok, np.where(val >= err[sl], 2, np.where(val >= warn[sl], 1, 0)), 0).astype(np.uint8)
+    tab = np.asarray(ctx_table).view(np.uint32).reshape(-1, 4)
+    cid = (ct >> np.uint32(8)).astype(np.int64)
+    inb = cid < tab.shape[0]
+    row = np.where(inb[:, None], tab[np.minimum(cid, tab.shape[0] - 1)], 0).astype(np.uint32)
+    off = ev["ts_off"].astype(np.int64)
+    ts = np.where(off == 0xFFFFFFFF, 0, np.int64(t_base) + off)
+    return Decoded(ts, val, slot, status, row[:, 0], row[:, 1], row[:, 3], ev["trace_h"].astype(np.uint64),
+                   row[:, 2].astype(np.uint64))
+
+
 def histograms(d: Decoded) -> np.ndarray:
     edges = np.array([list(s.buckets) for s in catalog.SIGNALS], dtype=np.float32)
     h = np.zeros((16, 16), dtype=np.int64)

@@ -65,44 +65,59 @@ class StagedWindow:
     """A window's records in pinned host memory, ready for DMA."""
     ev: "object"        # torch uint8 pinned [>= n_events*wire]
     sp: "object"        # torch uint8 pinned [>= n_spans*64]
-    counts: "object"    # torch int32 pinned [4]
+    counts: "object"    # torch int32 pinned [8]: n_ev, n_spans, n_groups, n_local, t_base lo/hi, n_ctx
     labels: "object"    # torch int32 pinned [group_cap]
     n_events: int
     n_spans: int
     n_groups: int
     group_domains: List[List[str]] = field(default_factory=list)
-    wire: int = 64                      # event record bytes: 64 (EVENT) or 32 (EVENT32)
+    wire: int = 64                      # event record bytes: 64 (EVENT), 32 (EVENT32), 20 (EVENT20)
     pod_table: Optional[np.ndarray] = None  # int32 pod id -> svc<<16|node (wire 32)
+    ctx_rows: "object" = None           # torch int32 pinned [n_ctx, 4] context table snapshot (wire 20)
+    n_ctx: int = 0
 
 
 def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
                  group_cap: int, group_domains=None, wire: int = 64, interner=None,
-                 n_local: Optional[int] = None) -> StagedWindow:
+                 n_local: Optional[int] = None, ctx_interner=None) -> StagedWindow:
     """Pin a window for DMA. ``wire=32`` converts 64-byte events to the compact 32-byte
     record (interned conn ids, milli-unit values; collector/records.py EVENT32), halving
-    the PCIe bytes that bound the pipeline; spans get the same interned conn ids."""
+    the PCIe bytes that bound the pipeline; ``wire=20`` goes further (EVENT20: window-relative
+    timestamps, interned (pod, pid, conn, svc|node) contexts; the context table rows travel
+    once, appended to a device table). Spans get the same interned conn ids."""
     pod_tab = None
-    if wire == 32:
+    ctx_rows, n_ctx, t_base = None, 0, 0
+    if wire in (32, 20):
         if interner is None:
             interner = records.ConnInterner()
-        if events.dtype == records.EVENT:
+        if wire == 32 and events.dtype == records.EVENT:
             pod_tab = records.pod_table(events, spans)
             events = records.to_compact(events, interner)
+        elif wire == 20:
+            if ctx_interner is None:
+                ctx_interner = records.CtxInterner()
+            events, t_base = records.to_wire20(events, interner, ctx_interner)
+            tab = ctx_interner.table()
+            n_ctx = int(tab.shape[0])
+            ctx_rows = torch.from_numpy(tab.copy()).pin_memory()
         spans = records.compact_spans(spans, interner)
     elif wire != 64:
-        raise ValueError("wire must be 64 or 32")
+        raise ValueError("wire must be 64, 32 or 20")
     ev = torch.from_numpy(events.view(np.uint8).reshape(-1).copy()).pin_memory()
     sp = torch.from_numpy(spans.view(np.uint8).reshape(-1).copy()).pin_memory()
     # counts[3] = node-local events; events[n_local:] are imported halo / remote-trace
     # records that join but are not counted (decode kernels, parallel/exchange.py)
     nl = 0 if n_local is None or n_local >= events.shape[0] else int(n_local)
-    counts = torch.tensor([events.shape[0], spans.shape[0], n_groups, nl], dtype=torch.int32).pin_memory()
+    tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
+    cnt = np.array([events.shape[0], spans.shape[0], n_groups, nl, tb & 0xFFFFFFFF, tb >> 32, n_ctx, 0],
+                   dtype=np.uint64).astype(np.uint32).view(np.int32)
+    counts = torch.from_numpy(cnt.copy()).pin_memory()
     lab = np.full(group_cap, -1, dtype=np.int32)
     if labels is not None:
         lab[: len(labels)] = labels
     labels_t = torch.from_numpy(lab).pin_memory()
     return StagedWindow(ev, sp, counts, labels_t, int(events.shape[0]), int(spans.shape[0]), n_groups,
-                        list(group_domains or []), wire, pod_tab)
+                        list(group_domains or []), wire, pod_tab, ctx_rows, n_ctx)
 
 
 class WindowPipeline:
@@ -145,7 +160,13 @@ class WindowPipeline:
             z8 = lambda n: torch.zeros(n, dtype=torch.uint8, device=self.dev)  # noqa: E731
             self.ev_dev = [z8(sig_cap * 64), z8(sig_cap * 64)]
             self.sp_dev = [z8(span_cap * 64), z8(span_cap * 64)]
-            self.counts_dev = [torch.zeros(4, dtype=torch.int32, device=self.dev) for _ in range(2)]
+            self.counts_dev = [torch.zeros(8, dtype=torch.int32, device=self.dev) for _ in range(2)]
+            # append-only context table for 20-byte records: rows are copied once, stream
+            # ordered before the first window that references them; the buffer address stays
+            # fixed (captured graphs keep pointing at it) until it has to grow
+            self.ctx_dev = torch.zeros((1 << 16, 4), dtype=torch.int32, device=self.dev)
+            self.ctx_uploaded = 1  # row 0 = the all-zero context
+            self.eng.set_ctx_table(self.ctx_dev)
             self.labels_dev = [torch.full((group_cap,), -1, dtype=torch.int32, device=self.dev) for _ in range(2)]
             self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(2)]
             self.totals = torch.zeros(L, dtype=torch.float64, device=self.dev)
@@ -214,8 +235,21 @@ class WindowPipeline:
                 self.drain()
                 self.engine.set_pod_table(w.pod_table)
                 self.pod_key = key
+                self.graphs = {}  # captured launches hold the old table's address
+        if w.n_ctx > self.ctx_dev.shape[0]:  # grow the context table (rare): re-capture
+            self.drain()
+            cap = 1 << int(np.ceil(np.log2(w.n_ctx)))
+            grown = torch.zeros((cap, 4), dtype=torch.int32, device=self.dev)
+            grown[: self.ctx_uploaded].copy_(self.ctx_dev[: self.ctx_uploaded])
+            self.ctx_dev = grown
+            self.eng.set_ctx_table(self.ctx_dev)
+            self.graphs = {}
         tr = [time.perf_counter()] if _HOST_TRACE else None
         with torch.cuda.stream(cs):
+            if w.n_ctx > self.ctx_uploaded:  # new context rows (append-only ids)
+                self.ctx_dev[self.ctx_uploaded: w.n_ctx].copy_(w.ctx_rows[self.ctx_uploaded: w.n_ctx],
+                                                               non_blocking=True)
+                self.ctx_uploaded = w.n_ctx
             nb = w.n_events * w.wire
             self.ev_dev[b][:nb].copy_(w.ev[:nb], non_blocking=True)
             if tr: tr.append(time.perf_counter())

@@ -113,7 +113,7 @@ def test_ref_record_decode(engine):
     buf = np.frombuffer(b"".join(recs), dtype=np.uint8)
     dev = torch.zeros(engine.sig_cap * 40, dtype=torch.uint8, device="cuda")
     dev[: buf.size] = torch.from_numpy(buf.copy()).cuda()
-    engine.eng.counts.copy_(torch.tensor([5, 0, 0, 0], dtype=torch.int32))
+    engine.eng.counts[:4].copy_(torch.tensor([5, 0, 0, 0], dtype=torch.int32))
     engine.eng.reset_window()
     engine.eng.decode_ref(dev, 3, (1 << 16) | 2, 0)
     torch.cuda.synchronize()
@@ -154,6 +154,41 @@ def test_compact_wire_matches_oracle(engine):
     np.testing.assert_array_equal(out.feat, ref.feat)
 
 
+def test_wire20_matches_oracle(engine):
+    from llm_slo_ebpf_toolkit_amd.collector import records
+
+    win = small_window(seed=17)
+    engine.set_join_params(2000.0, 0.7, 3, 1)
+    engine.set_model(NaiveBayes.ref())
+    conns, ctxs = records.ConnInterner(), records.CtxInterner()
+    ev = win.events.copy()
+    ev["ts_ns"][3] = 0
+    ev20, t_base = records.to_wire20(ev, conns, ctxs)
+    sp = records.compact_spans(win.spans, conns)
+    engine.set_ctx_table(ctxs.table())
+    engine.stage(ev20, sp, win.n_groups, win.group_labels, t_base=t_base)
+    engine.upload()
+    engine.run(True, False)
+    out = engine.outputs()
+    e = engine.eng
+    d = oracle.decode_w20(ev20, t_base, ctxs.table())
+    N, S = win.n_events, win.n_spans
+    np.testing.assert_array_equal(e.g_ts[:N].cpu().numpy(), d.ts)
+    np.testing.assert_array_equal(e.g_slot[:N].cpu().numpy(), d.slot)
+    np.testing.assert_array_equal(e.g_val[:N].cpu().numpy(), d.val)
+    np.testing.assert_array_equal(e.g_pid[:N].cpu().numpy().view(np.uint32), d.pid)
+    np.testing.assert_array_equal(e.g_svcnode[:N].cpu().numpy().view(np.uint32), d.svcnode)
+    ref = oracle.join(d, sp, win.n_groups)
+    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
+    np.testing.assert_array_equal(top3, ref.top3)
+    np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
+    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
+        assert out.debug[k] == ref.debug[k], k
+    np.testing.assert_array_equal(e.gsum[: win.n_groups].cpu().numpy(), ref.gsum)
+    np.testing.assert_array_equal(out.feat, ref.feat)
+    assert int(e.misc[1].item()) == 1  # the zero timestamp
+
+
 def test_split_pre_post_equals_run_window(engine):
     """Global-incident-scope split (pre -> [group all-reduce] -> post) == one-shot window;
     and n_local excludes imported records from the counters but not from the join."""
@@ -173,7 +208,7 @@ def test_split_pre_post_equals_run_window(engine):
     np.testing.assert_array_equal(e.packet.cpu().numpy(), pk_a)
     # n_local: count only the first half of the events
     half = win.n_events // 2
-    e.counts.copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, half], dtype=torch.int32))
+    e.counts[:4].copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, half], dtype=torch.int32))
     e.run_window(engine.ev_dev, engine.sp_dev, win.n_groups, True, False, 64)
     torch.cuda.synchronize()
     d = oracle.decode_events(win.events[:half])
@@ -182,7 +217,7 @@ def test_split_pre_post_equals_run_window(engine):
     top3 = e.top3[: 3 * win.n_spans].cpu().numpy().view(np.uint64).reshape(win.n_spans, 3)
     ref = oracle.join(oracle.decode_events(win.events), win.spans, win.n_groups)
     np.testing.assert_array_equal(top3, ref.top3)
-    e.counts.copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, 0], dtype=torch.int32))
+    e.counts[:4].copy_(torch.tensor([win.n_events, win.n_spans, win.n_groups, 0], dtype=torch.int32))
 
 
 def test_device_refit_matches_host_learned_model(engine):
@@ -215,3 +250,28 @@ def test_device_refit_matches_host_learned_model(engine):
     assert np.isneginf(dev["bias"][N_DOMAINS:]).all()
     np.testing.assert_array_equal(dev["dom_mask"], ref["dom_mask"])
     assert dev["table_mask"] == ref["table_mask"] and dev["mode"] == 0
+
+
+def test_pipeline_wire20_equals_wire32():
+    """The pipelined engine gives bit-identical window totals on 20- and 32-byte records
+    (append-only context table uploads, graphs, device refit)."""
+    import torch
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, stage_window
+
+    cfg = ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8, events_per_window=6000,
+                       spans_per_window=300, seed=23)
+    gen = ReplayGenerator(cfg)
+    wins = [gen.next_window() for _ in range(3)]
+    sums = {}
+    for wire in (32, 20):
+        it, xi = records.ConnInterner(), records.CtxInterner()
+        staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 8, w.group_domains, wire=wire,
+                               interner=it, ctx_interner=xi) for w in wins]
+        pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
+        for i in range(6):
+            pipe.submit(staged[i % 3])
+        sums[wire] = pipe.summary()
+    for k in ("confusion", "hist", "status", "dbg", "misc"):
+        np.testing.assert_array_equal(sums[20][k], sums[32][k], err_msg=k)

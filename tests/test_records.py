@@ -1,4 +1,4 @@
-"""Record layouts: REF 40-byte records, 64-byte EVENT/SPAN, 32-byte compact EVENT32."""
+"""Record layouts: REF 40-byte records, 64-byte EVENT/SPAN, 32-byte EVENT32, 20-byte EVENT20."""
 
 import numpy as np
 
@@ -16,6 +16,7 @@ def _win(seed=2):
 def test_layout_sizes():
     assert records.EVENT.itemsize == 64
     assert records.EVENT32.itemsize == 32
+    assert records.EVENT20.itemsize == 20
     assert records.SPAN.itemsize == 64
     assert records.REF_EVENT.itemsize == 40
 
@@ -59,3 +60,44 @@ def test_interner_is_stable_and_zero_preserving():
     assert ids[0] == 0 and ids[4] == 0 and ids[1] == ids[3] and ids[1] != ids[2]
     again = it.ids(np.array([5, 99], dtype=np.uint64))
     assert again[0] == ids[2] and again[1] == ids[1]
+
+
+def test_wire20_preserves_decode_and_join():
+    win = _win(seed=4)
+    ev = win.events.copy()
+    ev["ts_ns"][5] = 0  # zero timestamps survive as the TS_ZERO sentinel (never join)
+    conns, ctxs = records.ConnInterner(), records.CtxInterner()
+    ev20, t_base = records.to_wire20(ev, conns, ctxs)
+    sp = records.compact_spans(win.spans, conns)
+    assert ev20["ts_off"][5] == records.TS_ZERO and t_base == int(ev["ts_ns"][ev["ts_ns"] != 0].min())
+    full = oracle.decode_events(ev)
+    d = oracle.decode_w20(ev20, t_base, ctxs.table())
+    for f in ("ts", "slot", "svcnode", "pod", "pid", "trace"):
+        np.testing.assert_array_equal(getattr(full, f), getattr(d, f), err_msg=f)
+    np.testing.assert_allclose(d.val, full.val, atol=6e-4, rtol=1e-6)
+    # the same interned conn ids as EVENT32, so every join key and tier is identical
+    c32 = oracle.decode_compact(records.to_compact(ev, conns), records.pod_table(ev, win.spans))
+    np.testing.assert_array_equal(c32.conn, d.conn)
+    a = oracle.join(full, win.spans, win.n_groups)
+    b = oracle.join(d, sp, win.n_groups)
+    np.testing.assert_array_equal(a.top3, b.top3)
+    np.testing.assert_array_equal(a.cnt, b.cnt)
+    assert a.debug == b.debug
+
+
+def test_ctx_interner_append_only_and_wide_window_rejected():
+    xi = records.CtxInterner()
+    z = np.zeros(3, dtype=np.uint32)
+    ids = xi.ids(np.array([0, 7, 7]), np.array([0, 100, 101]), z, np.array([0, 65537, 65537]))
+    assert ids[0] == 0 and ids[1] != ids[2] and len(xi) == 3
+    tab = xi.table().view(np.uint32)
+    assert tuple(tab[ids[2]]) == (7, 101, 0, 65537) and tuple(tab[0]) == (0, 0, 0, 0)
+    again = xi.ids(np.array([7, 9]), np.array([101, 1]), np.zeros(2), np.array([65537, 1]))
+    assert again[0] == ids[2] and again[1] == 3 and np.array_equal(xi.table()[:3], tab.view(np.int32))
+    win = _win()
+    ev = win.events.copy()
+    ev["ts_ns"][0] = ev["ts_ns"][1:].min() + (1 << 32)
+    import pytest
+
+    with pytest.raises(ValueError):
+        records.to_wire20(ev, records.ConnInterner(), records.CtxInterner())

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--spans", type=int, default=16384)
     ap.add_argument("--services", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--wire", type=int, default=32, choices=(32, 64))
+    ap.add_argument("--wire", type=int, default=20, choices=(20, 32, 64))
     ap.add_argument("--sort-ts", action="store_true", help="events in timestamp order (ring arrival order)")
     a = ap.parse_args()
     t = time.time()
@@ -40,13 +40,21 @@ def main():
         it = records.ConnInterner()
         eng.set_pod_table(records.pod_table(ev, sp))
         ev, sp = records.to_compact(ev, it), records.compact_spans(sp, it)
-    eng.stage(ev, sp, win.n_groups, win.group_labels)
+    t_base = 0
+    if a.wire == 20:
+        from llm_slo_ebpf_toolkit_amd.collector import records
+
+        it, xi = records.ConnInterner(), records.CtxInterner()
+        ev, t_base = records.to_wire20(ev, it, xi)
+        sp = records.compact_spans(sp, it)
+        eng.set_ctx_table(xi.table())
+    eng.stage(ev, sp, win.n_groups, win.group_labels, t_base=t_base)
     eng.upload()
     torch.cuda.synchronize()
     e = eng.eng
     stages = {
         "reset": lambda: e.reset_window(),
-        "decode": (lambda: e.decode_compact(eng.ev_dev)) if a.wire == 32 else (lambda: e.decode(eng.ev_dev)),
+        "decode": lambda: e.decode_wire(eng.ev_dev, a.wire),
         "join": lambda: e.join(eng.sp_dev, win.n_groups, None),
         "posterior": lambda: e.posterior(True),
         "stats": lambda: e.accumulate_stats(None),
