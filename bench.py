@@ -51,9 +51,10 @@ def parse():
                     help="windows the host may run ahead of the GPU (host back-pressure)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", type=int, default=20, choices=(20, 32, 64),
-                    help="event record bytes on PCIe: 20 = EVENT20 (window-relative ts, interned contexts), "
-                         "32 = compact (interned ids), 64 = full")
+    ap.add_argument("--wire", type=int, default=16, choices=(16, 20, 32, 64),
+                    help="event record bytes on PCIe: 16 = EVENT16 (EVENT20 + interned trace ids), "
+                         "20 = EVENT20 (window-relative ts, interned contexts), 32 = compact (interned ids), "
+                         "64 = full")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -94,10 +95,13 @@ def main() -> int:
                        n_services=a.services, seed=a.seed, shard=rank)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
-    from llm_slo_ebpf_toolkit_amd.collector.records import ConnInterner, CtxInterner
-    interner, ctx_interner = ConnInterner(), CtxInterner()
+    from llm_slo_ebpf_toolkit_amd.collector.records import ConnInterner, native_encoder
+    # one native encoder per record stream (ids stay consistent across windows); its cost
+    # is reported as host_encode_ms_per_window
+    interner, encoder = ConnInterner(), native_encoder()
     staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, a.services, w.group_domains,
-                           wire=a.wire, interner=interner, ctx_interner=ctx_interner) for w in wins]
+                           wire=a.wire, interner=interner, encoder=encoder) for w in wins]
+    encode_ms = 1e3 * float(np.mean([s.encode_s for s in staged]))
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
@@ -221,6 +225,7 @@ def main() -> int:
         "ref55_single_fault_macro_f1": {k: round(v, 4) for k, v in ref_f1.items()},
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
         "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
+        "host_encode_ms_per_window": round(encode_ms, 2),
     }
     if rank == 0:
         line = json.dumps(res)

@@ -65,6 +65,17 @@ EVENT20 = np.dtype({"names": ["ts_off", "ctx_type", "value_milli", "trace_h"],
 TS_ZERO = 0xFFFFFFFF  # ts_off of a zero timestamp (never joins)
 assert EVENT20.itemsize == 20
 
+# 16-byte wire record: EVENT20 with the trace hash interned to a 32-bit id shared with the
+# window's spans (TraceInterner / the native WireEncoder).
+EVENT16 = np.dtype([
+    ("ts_off", "<u4"),       # 0  ns since the window base, TS_ZERO = zero timestamp
+    ("ctx_type", "<u4"),     # 4  bits 0-7 signal type, 8-31 context id
+    ("value_milli", "<u4"),  # 8
+    ("trace_id", "<u4"),     # 12 interned trace id, 0 = none
+])
+assert EVENT16.itemsize == 16
+WIRE_DTYPES = {64: EVENT, 32: EVENT32, 20: EVENT20, 16: EVENT16}
+
 SPAN = np.dtype([
     ("ts_ns", "<i8"),        # 0
     ("trace_h", "<u8"),      # 8
@@ -327,6 +338,64 @@ class CtxInterner:
         if self._table is None:
             self._table = np.array(self._rows, dtype=np.uint32).reshape(-1, 4).view(np.int32)
         return self._table
+
+
+class TraceInterner:
+    """64-bit trace hash -> 32-bit id (0 = none), shared by a window's events and spans
+    (numpy reference of the native encoder's trace table; no expiry)."""
+
+    def __init__(self):
+        self._ids = {}
+
+    def ids(self, trace_h: np.ndarray) -> np.ndarray:
+        uniq, inv = np.unique(np.asarray(trace_h, dtype=np.uint64), return_inverse=True)
+        out = np.zeros(uniq.shape[0], dtype=np.uint32)
+        for j, h in enumerate(uniq.tolist()):
+            if h == 0:
+                continue
+            i = self._ids.get(h)
+            if i is None:
+                i = len(self._ids) + 1
+                if i > 0xFFFFFFFF:
+                    raise OverflowError("trace id space exhausted")
+                self._ids[h] = i
+            out[j] = i
+        return out[np.asarray(inv).reshape(-1)]
+
+
+def to_wire16(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner", traces: "TraceInterner"):
+    """EVENT (64 B) -> (EVENT16 (16 B), t_base); spans must go through ``wire_spans`` with
+    the same interners."""
+    e20, t_base = to_wire20(events, conns, ctxs)
+    out = np.zeros(events.shape[0], dtype=EVENT16)
+    for f in ("ts_off", "ctx_type", "value_milli"):
+        out[f] = e20[f]
+    out["trace_id"] = traces.ids(events["trace_h"])
+    return out, t_base
+
+
+def wire_spans(spans: np.ndarray, conns: "ConnInterner", traces: "TraceInterner" = None) -> np.ndarray:
+    """Spans for the compact wire formats: interned conn ids (and trace ids for EVENT16)."""
+    out = compact_spans(spans, conns)
+    if traces is not None:
+        out["trace_h"] = traces.ids(spans["trace_h"]).astype(np.uint64)
+    return out
+
+
+def signal_scale_table() -> np.ndarray:
+    """decode_scale per kernel signal type < 256 (1.0 for unknown types)."""
+    scale = np.ones(256, dtype=np.float64)
+    for s in catalog.SIGNALS:
+        if s.kernel_type < 256:
+            scale[s.kernel_type] = s.decode_scale
+    return scale
+
+
+def native_encoder():
+    """The native WireEncoder (runtime/csrc/wire.h) configured with the signal catalogue."""
+    from ..runtime import load
+
+    return load().WireEncoder(signal_scale_table())
 
 
 def string_hash64(s: str) -> int:

@@ -36,7 +36,7 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 HIP_SOURCES = ["decode.hip", "join.hip", "posterior.hip", "gatestats.hip", "storm.hip"]
-RT_SOURCES = ["ring.cpp", "replay.cpp", "rt_bindings.cpp"]
+RT_SOURCES = ["ring.cpp", "replay.cpp", "wire.cpp", "rt_bindings.cpp"]
 
 
 def torch_flags():
@@ -117,9 +117,11 @@ def build_runtime(force: bool = False, jobs: int = 4) -> List[str]:
     rt_dir = os.path.join(PKG, "runtime")
     hdrs = _headers(RT_CSRC)
     cxx = shutil.which("g++") or "c++"
-    base = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__=1"]
+    # -ffp-contract=off: the wire encoder's fixed-point values must match numpy bit for bit
+    base = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-ffp-contract=off", f"-I{ROCM}/include",
+            "-D__HIP_PLATFORM_AMD__=1"]
     outs = []
-    core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp")]
+    core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp", "wire.cpp")]
     lib = os.path.join(rt_dir, "libmislo_rt.so")
     if force or _newer(lib, core + hdrs):
         _run([cxx, *base, "-shared", *core, "-o", lib, f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])

@@ -275,14 +275,14 @@ class Engine {
     ctx_table = table;
   }
 
-  // events: device buffer of 20-byte records (>= sig_cap * 20 bytes); counts[4..5] = t_base,
-  // counts[6] = valid context-table rows (0 = all)
-  void decode_w20(torch::Tensor events) {
+  // events: device buffer of 20- or 16-byte records (>= sig_cap * wire bytes); counts[4..5] =
+  // t_base, counts[6] = valid context-table rows (0 = all)
+  void decode_ctx_wire(torch::Tensor events, int64_t wire) {
     check_cuda(events, "events");
-    if (events.nbytes() < (size_t)sig_cap_ * 20)
-      throw std::invalid_argument("events buffer must hold sig_cap 20-byte records");
-    if (counts.numel() < 7) throw std::invalid_argument("wire 20 needs counts int32[>= 7] (t_base, n_ctx)");
-    launch_decode_w20(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
+    if (events.nbytes() < (size_t)sig_cap_ * (size_t)wire)
+      throw std::invalid_argument("events buffer must hold sig_cap wire records");
+    if (counts.numel() < 7) throw std::invalid_argument("wire 20/16 needs counts int32[>= 7] (t_base, n_ctx)");
+    launch_decode_wire(events.data_ptr(), (int)wire, dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
                       (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                       dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
     launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
@@ -292,9 +292,9 @@ class Engine {
 
   void decode_wire(torch::Tensor events, int64_t wire) {
     if (wire == 32) decode_compact(events);
-    else if (wire == 20) decode_w20(events);
+    else if (wire == 20 || wire == 16) decode_ctx_wire(events, wire);
     else if (wire == 64) decode(events);
-    else throw std::invalid_argument("wire must be 64, 32 or 20");
+    else throw std::invalid_argument("wire must be 64, 32, 20 or 16");
   }
 
   void decode_ref(torch::Tensor events, int64_t pod, int64_t svcnode, int64_t trace_h) {
@@ -365,7 +365,7 @@ class Engine {
   }
 
   // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0].
-  // wire: 64 = Event records, 32 = compact EventC32 records, 20 = EventC20 records
+  // wire: 64 = Event records, 32 = compact EventC32 records, 20 = EventC20, 16 = EventC16
   void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn,
                   int64_t wire) {
     reset_window();
@@ -522,7 +522,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("decode_compact", &Engine::decode_compact)
       .def("set_pod_table", &Engine::set_pod_table)
       .def("set_ctx_table", &Engine::set_ctx_table)
-      .def("decode_w20", &Engine::decode_w20)
+      .def("decode_ctx_wire", &Engine::decode_ctx_wire)
       .def("decode_wire", &Engine::decode_wire)
       .def("join", &Engine::join, py::arg("spans"), py::arg("n_groups"), py::arg("base_attrs") = py::none())
       .def("posterior", &Engine::posterior)

@@ -196,13 +196,18 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
   }
 }
 
-// 20-byte records: 5/8 of the compact record's PCIe bytes. The window base timestamp is
+// 20-byte (16-byte) records: 5/8 (1/2) of the compact record's PCIe bytes. The window base timestamp is
 // counts[4] | counts[5] << 32; context ids resolve through the device context table
 // (counts[6] valid rows).
-template <int NT>
-__global__ __launch_bounds__(NT) void k_decode_w20(const EventC20* __restrict__ ev, const int* __restrict__ n_ptr,
-                                                   int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
-                                                   DecodeOut o) {
+__device__ __forceinline__ uint64_t wire_trace(const EventC20& e) { return ((uint64_t)e.tr_hi << 32) | e.tr_lo; }
+__device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)e.trace_id; }
+
+// Rec = EventC20 (20-byte) or EventC16 (16-byte, interned trace ids): identical decoding
+// otherwise.
+template <int NT, class Rec>
+__global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, const int* __restrict__ n_ptr,
+                                                    int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
+                                                    DecodeOut o) {
   __shared__ uint32_t s_hist[kSlots * kBuckets];
   __shared__ uint32_t s_status[kSlots * 3];
   __shared__ uint32_t s_part[kKeyTypes * kParts];
@@ -222,14 +227,14 @@ __global__ __launch_bounds__(NT) void k_decode_w20(const EventC20* __restrict__ 
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0;
   for (int i = beg + threadIdx.x; i < end; i += NT) {
-    const EventC20 e = ev[i];
+    const Rec e = ev[i];
     const int st = (int)(e.ctx_type & 0xFFu);
     const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
     const float val = (float)((double)e.value_milli * 1e-3);
     const uint32_t cid = e.ctx_type >> 8;
     const uint4 cx = cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
     const int64_t ts = e.ts_off == kTsZero ? 0 : t_base + (int64_t)e.ts_off;
-    const uint64_t tr = ((uint64_t)e.tr_hi << 32) | e.tr_lo;
+    const uint64_t tr = wire_trace(e);
     decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, s_hist, s_status, s_part, s_sum,
                unsupported, zero_ts, i < n_local);
   }
@@ -367,13 +372,18 @@ void launch_decode_compact(const void* ev, const int* n_dev, int cap, const uint
                      cap, pod_svcnode, n_pods, o);
 }
 
-void launch_decode_w20(const void* ev, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
-                       const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
-                       unsigned long long* misc, hipStream_t stream) {
+void launch_decode_wire(const void* ev, int wire, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
+                        const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                        unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
   constexpr int NT = 256;
-  hipLaunchKernelGGL((k_decode_w20<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, (const EventC20*)ev, n_dev,
-                     cap, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, o);
+  const uint4* tab = reinterpret_cast<const uint4*>(ctx_tab);
+  if (wire == 16)
+    hipLaunchKernelGGL((k_decode_wire<NT, EventC16>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                       (const EventC16*)ev, n_dev, cap, tab, n_ctx, o);
+  else
+    hipLaunchKernelGGL((k_decode_wire<NT, EventC20>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                       (const EventC20*)ev, n_dev, cap, tab, n_ctx, o);
 }
 
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,

@@ -502,15 +502,8 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
         const SpanTC c0r = s_tc[lo];
         const bool key_ok = s_runok[s_rid[lo]] && p0.pod != 0 && p0.pod == g_pod &&
                             (k == 1 ? (p0.pid != 0 && p0.pid == g_pid) : (c0r.cn != 0 && c0r.cn == g_cn));
-#if defined(MISLO_EXP) && MISLO_EXP == 4
-        if (key_ok) continue;
-#endif
         if (key_ok) {
-#if defined(MISLO_EXP) && MISLO_EXP == 3
-          const int hi = min(lo + 8, m);
-#else
           const int hi = upper_ht(s_kt, lo, m, h, thi);
-#endif
           int a1 = hi, b1 = hi;  // P2 sub-range excluded from the pod+conn tier
           if (k == 2 && p0.pid != 0 && p0.pid == g_pid) {
             a1 = lower_ht(s_kt, lo, hi, h, t - jp.win_ns[1]);
@@ -519,14 +512,10 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
           const int n_acc = (hi - lo) - (b1 - a1);
           if (n_acc > 0) {
             if (cand_tier) {
-#if !defined(MISLO_EXP) || MISLO_EXP != 2
               add_range(lo, a1);
               add_range(b1, hi);
-#endif
               n_cand += (unsigned long long)n_acc;
-#if !defined(MISLO_EXP) || MISLO_EXP != 1
               if (do_groups) add_group(p0.grp, g_slot, g_milli, (uint32_t)n_acc);
-#endif
             } else {
               n_low += (unsigned long long)n_acc;
             }

@@ -59,6 +59,12 @@ struct EventC20 {
   uint32_t tr_lo, tr_hi;
 };
 static_assert(sizeof(EventC20) == 20, "EventC20 must be 20 bytes");
+// 16-byte wire record (EVENT16): EventC20 with the trace hash interned to a 32-bit id that
+// the window's spans carry too (runtime/csrc/wire.h).
+struct alignas(16) EventC16 {
+  uint32_t ts_off, ctx_type, value_milli, trace_id;
+};
+static_assert(sizeof(EventC16) == 16, "EventC16 must be 16 bytes");
 constexpr uint32_t kTsZero = 0xFFFFFFFFu;
 
 // REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).

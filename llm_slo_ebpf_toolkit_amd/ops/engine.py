@@ -138,13 +138,13 @@ class GpuEngine:
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None,
               t_base: int = 0):
         """Copy records into pinned staging (host memcpy, no GPU work). ``events`` may be
-        64-byte EVENT, 32-byte EVENT32 (needs ``set_pod_table``) or 20-byte EVENT20 records
-        (needs ``set_ctx_table`` and the window base ``t_base``)."""
+        64-byte EVENT, 32-byte EVENT32 (needs ``set_pod_table``) or 20/16-byte EVENT20/EVENT16
+        records (need ``set_ctx_table`` and the window base ``t_base``)."""
         n, s = events.shape[0], spans.shape[0]
         if n > self.sig_cap or s > self.span_cap or n_groups > self.group_cap:
             raise ValueError("window exceeds engine capacity")
-        if events.dtype not in (records.EVENT, records.EVENT32, records.EVENT20) or spans.dtype != records.SPAN:
-            raise TypeError("events/spans must use the EVENT|EVENT32|EVENT20/SPAN record dtypes")
+        if events.dtype not in records.WIRE_DTYPES.values() or spans.dtype != records.SPAN:
+            raise TypeError("events/spans must use the EVENT|EVENT32|EVENT20|EVENT16/SPAN record dtypes")
         self.wire = events.dtype.itemsize
         self.ev_host.numpy()[: n * self.wire] = events.view(np.uint8).reshape(-1)
         self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)

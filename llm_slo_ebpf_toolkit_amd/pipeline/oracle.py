@@ -85,7 +85,8 @@ def decode_compact(ev: np.ndarray, pod_svcnode: np.ndarray) -> Decoded:
 
 
 def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
-    """k_decode_w20: EVENT20 records with the window base and the context table."""
+    """k_decode_wire: EVENT20 (trace hash) or EVENT16 (trace id) records with the window
+    base and the context table."""
     type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
     for s in catalog.SIGNALS:
         if s.kernel_type < 256:
@@ -105,8 +106,12 @@ def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
     row = np.where(inb[:, None], tab[np.minimum(cid, tab.shape[0] - 1)], 0).astype(np.uint32)
     off = ev["ts_off"].astype(np.int64)
     ts = np.where(off == 0xFFFFFFFF, 0, np.int64(t_base) + off)
-    return Decoded(ts, val, slot, status, row[:, 0], row[:, 1], row[:, 3], ev["trace_h"].astype(np.uint64),
+    trace = ev["trace_id"] if "trace_id" in ev.dtype.names else ev["trace_h"]
+    return Decoded(ts, val, slot, status, row[:, 0], row[:, 1], row[:, 3], trace.astype(np.uint64),
                    row[:, 2].astype(np.uint64))
+
+
+decode_w16 = decode_w20
 
 
 def histograms(d: Decoded) -> np.ndarray:

@@ -73,51 +73,78 @@ class StagedWindow:
     group_domains: List[List[str]] = field(default_factory=list)
     wire: int = 64                      # event record bytes: 64 (EVENT), 32 (EVENT32), 20 (EVENT20)
     pod_table: Optional[np.ndarray] = None  # int32 pod id -> svc<<16|node (wire 32)
-    ctx_rows: "object" = None           # torch int32 pinned [n_ctx, 4] context table snapshot (wire 20)
+    ctx_rows: "object" = None           # torch int32 pinned [n_ctx, 4] context table snapshot (wire 20/16)
     n_ctx: int = 0
+    encode_s: float = 0.0               # host time spent converting records to the wire format
 
 
 def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
                  group_cap: int, group_domains=None, wire: int = 64, interner=None,
-                 n_local: Optional[int] = None, ctx_interner=None) -> StagedWindow:
+                 n_local: Optional[int] = None, ctx_interner=None, trace_interner=None,
+                 encoder=None) -> StagedWindow:
     """Pin a window for DMA. ``wire=32`` converts 64-byte events to the compact 32-byte
     record (interned conn ids, milli-unit values; collector/records.py EVENT32), halving
-    the PCIe bytes that bound the pipeline; ``wire=20`` goes further (EVENT20: window-relative
-    timestamps, interned (pod, pid, conn, svc|node) contexts; the context table rows travel
-    once, appended to a device table). Spans get the same interned conn ids."""
+    the PCIe bytes that bound the pipeline. ``wire=20`` / ``16`` go further (EVENT20 /
+    EVENT16: window-relative timestamps, interned (pod, pid, conn, svc|node) contexts whose
+    rows travel once, appended to a device table; EVENT16 also interns trace hashes). Spans
+    get the same interned ids. 20/16 use the native ``encoder`` (records.native_encoder(),
+    one per record stream, written straight into pinned memory) unless numpy interners are
+    given (the reference path the tests compare against)."""
+    t_enc = time.perf_counter()
     pod_tab = None
     ctx_rows, n_ctx, t_base = None, 0, 0
-    if wire in (32, 20):
+    if wire in (20, 16) and ctx_interner is None:
+        enc = encoder if encoder is not None else records.native_encoder()
+        ev = torch.empty(max(events.shape[0], 1) * wire, dtype=torch.uint8).pin_memory()
+        sp = torch.empty(max(spans.shape[0], 1) * 64, dtype=torch.uint8).pin_memory()
+        t_enc = time.perf_counter()  # conversion only (the agent reuses its pinned buffers)
+        t_base = enc.encode(np.ascontiguousarray(events), ev.numpy(), wire)
+        enc.encode_spans(np.ascontiguousarray(spans), sp.numpy(), wire == 16)
+        enc.end_window()
+        tab = enc.ctx_table()
+        n_ctx = int(tab.shape[0])
+        ctx_rows = torch.from_numpy(tab).pin_memory()
+        return _finish_stage(torch, ev, sp, events.shape[0], spans.shape[0], n_groups, labels, group_cap,
+                             group_domains, wire, None, ctx_rows, n_ctx, t_base, n_local, t_enc)
+    if wire in (32, 20, 16):
         if interner is None:
             interner = records.ConnInterner()
         if wire == 32 and events.dtype == records.EVENT:
             pod_tab = records.pod_table(events, spans)
             events = records.to_compact(events, interner)
-        elif wire == 20:
-            if ctx_interner is None:
-                ctx_interner = records.CtxInterner()
-            events, t_base = records.to_wire20(events, interner, ctx_interner)
+        elif wire in (20, 16):
+            if wire == 20:
+                events, t_base = records.to_wire20(events, interner, ctx_interner)
+            else:
+                trace_interner = trace_interner if trace_interner is not None else records.TraceInterner()
+                events, t_base = records.to_wire16(events, interner, ctx_interner, trace_interner)
             tab = ctx_interner.table()
             n_ctx = int(tab.shape[0])
             ctx_rows = torch.from_numpy(tab.copy()).pin_memory()
-        spans = records.compact_spans(spans, interner)
+        spans = records.wire_spans(spans, interner, trace_interner if wire == 16 else None)
     elif wire != 64:
-        raise ValueError("wire must be 64, 32 or 20")
+        raise ValueError("wire must be 64, 32, 20 or 16")
     ev = torch.from_numpy(events.view(np.uint8).reshape(-1).copy()).pin_memory()
     sp = torch.from_numpy(spans.view(np.uint8).reshape(-1).copy()).pin_memory()
+    return _finish_stage(torch, ev, sp, events.shape[0], spans.shape[0], n_groups, labels, group_cap,
+                         group_domains, wire, pod_tab, ctx_rows, n_ctx, t_base, n_local, t_enc)
+
+
+def _finish_stage(torch, ev, sp, n_ev: int, n_sp: int, n_groups: int, labels, group_cap: int, group_domains,
+                  wire: int, pod_tab, ctx_rows, n_ctx: int, t_base: int, n_local, t_enc: float) -> StagedWindow:
     # counts[3] = node-local events; events[n_local:] are imported halo / remote-trace
     # records that join but are not counted (decode kernels, parallel/exchange.py)
-    nl = 0 if n_local is None or n_local >= events.shape[0] else int(n_local)
+    nl = 0 if n_local is None or n_local >= n_ev else int(n_local)
     tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
-    cnt = np.array([events.shape[0], spans.shape[0], n_groups, nl, tb & 0xFFFFFFFF, tb >> 32, n_ctx, 0],
+    cnt = np.array([n_ev, n_sp, n_groups, nl, tb & 0xFFFFFFFF, tb >> 32, n_ctx, 0],
                    dtype=np.uint64).astype(np.uint32).view(np.int32)
     counts = torch.from_numpy(cnt.copy()).pin_memory()
     lab = np.full(group_cap, -1, dtype=np.int32)
     if labels is not None:
         lab[: len(labels)] = labels
     labels_t = torch.from_numpy(lab).pin_memory()
-    return StagedWindow(ev, sp, counts, labels_t, int(events.shape[0]), int(spans.shape[0]), n_groups,
-                        list(group_domains or []), wire, pod_tab, ctx_rows, n_ctx)
+    return StagedWindow(ev, sp, counts, labels_t, int(n_ev), int(n_sp), n_groups, list(group_domains or []), wire,
+                        pod_tab, ctx_rows, n_ctx, time.perf_counter() - t_enc)
 
 
 class WindowPipeline:

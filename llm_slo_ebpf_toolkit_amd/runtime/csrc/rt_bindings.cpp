@@ -13,6 +13,7 @@
 
 #include "replay.h"
 #include "ring.h"
+#include "wire.h"
 
 namespace py = pybind11;
 using mislo::Ring;
@@ -145,6 +146,53 @@ class PyReplayer {
   std::unique_ptr<mislo::Replayer> rep_;
 };
 
+// 64-byte EVENT / SPAN records -> 20- or 16-byte wire records (runtime/csrc/wire.h)
+class PyWireEncoder {
+ public:
+  explicit PyWireEncoder(py::array_t<double, py::array::c_style | py::array::forcecast> scale) {
+    if (scale.size() != 256) throw std::invalid_argument("scale must have 256 entries");
+    enc_ = std::make_unique<mislo::WireEncoder>(scale.data());
+  }
+
+  // events: EVENT records (any contiguous buffer, n*64 bytes); out: writable buffer of
+  // >= n*wire bytes (e.g. the pinned staging tensor). Returns t_base.
+  int64_t encode(py::buffer events, py::buffer out, int wire) {
+    py::buffer_info ei = events.request(), oi = out.request(true);
+    const size_t nb = (size_t)ei.size * ei.itemsize;
+    if (nb % sizeof(mislo::EventRec)) throw std::invalid_argument("events: not a whole number of 64-byte records");
+    const size_t n = nb / sizeof(mislo::EventRec);
+    if ((size_t)oi.size * oi.itemsize < n * (size_t)wire) throw std::invalid_argument("out buffer too small");
+    py::gil_scoped_release nogil;
+    return enc_->encode(static_cast<const mislo::EventRec*>(ei.ptr), n, oi.ptr, wire);
+  }
+
+  void encode_spans(py::buffer spans, py::buffer out, bool trace_ids) {
+    py::buffer_info si = spans.request(), oi = out.request(true);
+    const size_t nb = (size_t)si.size * si.itemsize;
+    if (nb % sizeof(mislo::SpanRec64)) throw std::invalid_argument("spans: not a whole number of 64-byte records");
+    if ((size_t)oi.size * oi.itemsize < nb) throw std::invalid_argument("out buffer too small");
+    py::gil_scoped_release nogil;
+    enc_->encode_spans(static_cast<const mislo::SpanRec64*>(si.ptr), nb / sizeof(mislo::SpanRec64),
+                       static_cast<mislo::SpanRec64*>(oi.ptr), trace_ids);
+  }
+
+  void end_window() { enc_->end_window(); }
+
+  // context table (int32 [n, 4]: pod, pid, conn id, svc<<16|node), row i = context id i
+  py::array_t<int32_t> ctx_table() const {
+    const auto& rows = enc_->ctx_rows();
+    py::array_t<int32_t> a({(py::ssize_t)rows.size(), (py::ssize_t)4});
+    std::memcpy(a.mutable_data(), rows.data(), rows.size() * sizeof(rows[0]));
+    return a;
+  }
+  size_t n_ctx() const { return enc_->ctx_rows().size(); }
+  size_t n_conns() const { return enc_->n_conns(); }
+  size_t n_traces() const { return enc_->n_traces(); }
+
+ private:
+  std::unique_ptr<mislo::WireEncoder> enc_;
+};
+
 PYBIND11_MODULE(_mislo_rt, m) {
   m.doc() = "MI355X LLM-SLO native host runtime (rings, replay producers)";
   py::class_<HostRing>(m, "HostRing")
@@ -172,4 +220,14 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def("wait", &PyReplayer::wait)
       .def_property_readonly("pushed", &PyReplayer::pushed)
       .def_property_readonly("dropped", &PyReplayer::dropped);
+  py::class_<PyWireEncoder>(m, "WireEncoder")
+      .def(py::init<py::array_t<double, py::array::c_style | py::array::forcecast>>(), py::arg("scale"))
+      .def("encode", &PyWireEncoder::encode, py::arg("events"), py::arg("out"), py::arg("wire") = 20)
+      .def("encode_spans", &PyWireEncoder::encode_spans, py::arg("spans"), py::arg("out"),
+           py::arg("trace_ids") = false)
+      .def("end_window", &PyWireEncoder::end_window)
+      .def("ctx_table", &PyWireEncoder::ctx_table)
+      .def_property_readonly("n_ctx", &PyWireEncoder::n_ctx)
+      .def_property_readonly("n_conns", &PyWireEncoder::n_conns)
+      .def_property_readonly("n_traces", &PyWireEncoder::n_traces);
 }

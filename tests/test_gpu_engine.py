@@ -189,6 +189,38 @@ def test_wire20_matches_oracle(engine):
     assert int(e.misc[1].item()) == 1  # the zero timestamp
 
 
+def test_wire16_native_matches_oracle(engine):
+    """Native encoder (EVENT16, interned trace ids) -> GPU decode + join == numpy oracle."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+
+    win = small_window(seed=19)
+    engine.set_join_params(2000.0, 0.7, 3, 1)
+    engine.set_model(NaiveBayes.ref())
+    enc = records.native_encoder()
+    buf = np.zeros(win.n_events * 16, dtype=np.uint8)
+    t_base = enc.encode(win.events, buf, 16)
+    sp = np.zeros_like(win.spans)
+    enc.encode_spans(win.spans, sp, True)
+    ev16 = buf.view(records.EVENT16)
+    engine.set_ctx_table(enc.ctx_table())
+    engine.stage(ev16, sp, win.n_groups, win.group_labels, t_base=t_base)
+    engine.upload()
+    engine.run(True, False)
+    out = engine.outputs()
+    e = engine.eng
+    d = oracle.decode_w16(ev16, t_base, enc.ctx_table())
+    S = win.n_spans
+    np.testing.assert_array_equal(e.g_ts[: win.n_events].cpu().numpy(), d.ts)
+    ref = oracle.join(d, sp, win.n_groups)
+    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
+    np.testing.assert_array_equal(top3, ref.top3)
+    np.testing.assert_array_equal(out.feat, ref.feat)
+    # interning is exact: the same join as on the full 64-byte records
+    full = oracle.join(oracle.decode_events(win.events), win.spans, win.n_groups)
+    np.testing.assert_array_equal(ref.top3, full.top3)
+    assert ref.debug == full.debug
+
+
 def test_split_pre_post_equals_run_window(engine):
     """Global-incident-scope split (pre -> [group all-reduce] -> post) == one-shot window;
     and n_local excludes imported records from the counters but not from the join."""
@@ -253,8 +285,8 @@ def test_device_refit_matches_host_learned_model(engine):
 
 
 def test_pipeline_wire20_equals_wire32():
-    """The pipelined engine gives bit-identical window totals on 20- and 32-byte records
-    (append-only context table uploads, graphs, device refit)."""
+    """The pipelined engine gives bit-identical window totals on 32-, 20- and 16-byte records
+    (native encoder, append-only context table uploads, graphs, device refit)."""
     import torch
 
     from llm_slo_ebpf_toolkit_amd.collector import records
@@ -265,13 +297,14 @@ def test_pipeline_wire20_equals_wire32():
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(3)]
     sums = {}
-    for wire in (32, 20):
-        it, xi = records.ConnInterner(), records.CtxInterner()
+    for wire in (32, 20, 16):
+        it, enc = records.ConnInterner(), records.native_encoder()
         staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 8, w.group_domains, wire=wire,
-                               interner=it, ctx_interner=xi) for w in wins]
+                               interner=it, encoder=enc) for w in wins]
         pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
         for i in range(6):
             pipe.submit(staged[i % 3])
         sums[wire] = pipe.summary()
-    for k in ("confusion", "hist", "status", "dbg", "misc"):
-        np.testing.assert_array_equal(sums[20][k], sums[32][k], err_msg=k)
+    for wire in (20, 16):
+        for k in ("confusion", "hist", "status", "dbg", "misc"):
+            np.testing.assert_array_equal(sums[wire][k], sums[32][k], err_msg=f"{wire} {k}")

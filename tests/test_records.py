@@ -101,3 +101,44 @@ def test_ctx_interner_append_only_and_wide_window_rejected():
 
     with pytest.raises(ValueError):
         records.to_wire20(ev, records.ConnInterner(), records.CtxInterner())
+
+
+def test_native_encoder_matches_numpy_reference():
+    """runtime/csrc/wire.cpp == records.to_wire20 / to_wire16 up to id numbering."""
+    pytest = __import__("pytest")
+    try:
+        enc20, enc16 = records.native_encoder(), records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    win = _win(seed=6)
+    ev = win.events.copy()
+    ev["ts_ns"][7] = 0
+    buf = np.zeros(ev.shape[0] * 20, dtype=np.uint8)
+    t_base = enc20.encode(ev, buf, 20)
+    n20 = buf.view(records.EVENT20)
+    conns, ctxs = records.ConnInterner(), records.CtxInterner()
+    r20, tb = records.to_wire20(ev, conns, ctxs)
+    assert t_base == tb
+    for f in ("ts_off", "value_milli", "trace_h"):
+        np.testing.assert_array_equal(n20[f], r20[f], err_msg=f)
+    a = oracle.decode_w20(n20, t_base, enc20.ctx_table())
+    b = oracle.decode_w20(r20, tb, ctxs.table())
+    for f in ("ts", "slot", "pod", "pid", "svcnode", "trace"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    # same connection equivalence classes (ids may be numbered differently)
+    pairs = set(zip(a.conn.tolist(), b.conn.tolist()))
+    assert len(pairs) == len(set(a.conn.tolist())) == len(set(b.conn.tolist()))
+    # EVENT16: trace ids shared with the spans reproduce the 64-byte join exactly
+    buf16 = np.zeros(ev.shape[0] * 16, dtype=np.uint8)
+    tb16 = enc16.encode(ev, buf16, 16)
+    sp16 = np.zeros_like(win.spans)
+    enc16.encode_spans(win.spans, sp16, True)
+    d16 = oracle.decode_w16(buf16.view(records.EVENT16), tb16, enc16.ctx_table())
+    full = oracle.join(oracle.decode_events(ev), win.spans, win.n_groups)
+    j16 = oracle.join(d16, sp16, win.n_groups)
+    np.testing.assert_array_equal(full.top3, j16.top3)
+    np.testing.assert_array_equal(full.cnt, j16.cnt)
+    assert full.debug == j16.debug
+    # numpy EVENT16 reference agrees too
+    r16, _ = records.to_wire16(ev, records.ConnInterner(), records.CtxInterner(), records.TraceInterner())
+    assert r16.dtype == records.EVENT16

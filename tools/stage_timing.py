@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--spans", type=int, default=16384)
     ap.add_argument("--services", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--wire", type=int, default=20, choices=(20, 32, 64))
+    ap.add_argument("--wire", type=int, default=20, choices=(16, 20, 32, 64))
     ap.add_argument("--sort-ts", action="store_true", help="events in timestamp order (ring arrival order)")
     a = ap.parse_args()
     t = time.time()
@@ -41,13 +41,16 @@ def main():
         eng.set_pod_table(records.pod_table(ev, sp))
         ev, sp = records.to_compact(ev, it), records.compact_spans(sp, it)
     t_base = 0
-    if a.wire == 20:
+    if a.wire in (20, 16):
         from llm_slo_ebpf_toolkit_amd.collector import records
 
-        it, xi = records.ConnInterner(), records.CtxInterner()
-        ev, t_base = records.to_wire20(ev, it, xi)
-        sp = records.compact_spans(sp, it)
-        eng.set_ctx_table(xi.table())
+        enc = records.native_encoder()
+        buf = np.zeros(ev.shape[0] * a.wire, dtype=np.uint8)
+        t_base = enc.encode(ev, buf, a.wire)
+        sp2 = np.zeros_like(sp)
+        enc.encode_spans(sp, sp2, a.wire == 16)
+        ev, sp = buf.view(records.WIRE_DTYPES[a.wire]), sp2
+        eng.set_ctx_table(enc.ctx_table())
     eng.stage(ev, sp, win.n_groups, win.group_labels, t_base=t_base)
     eng.upload()
     torch.cuda.synchronize()
