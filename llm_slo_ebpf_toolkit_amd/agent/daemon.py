@@ -162,7 +162,7 @@ class AgentOptions:
     device: int = 0
     model: str = "bayes"
     min_confidence: float = 0.5
-    wire: int = 20
+    wire: int = 16
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -359,15 +359,15 @@ class Agent:
             # measures the agent, not the synthetic trace generator.
             import torch
 
-            from ..collector.records import ConnInterner, CtxInterner
+            from ..collector.records import ConnInterner, native_encoder
             from ..pipeline.window import stage_window
 
-            it, xi = ConnInterner(), CtxInterner()
+            it, enc = ConnInterner(), native_encoder()
             pool = []
             for _ in range(4):
                 w = gen.next_window()
                 pool.append(stage_window(torch, w.events, w.spans, min(w.n_groups, o.window_groups), None,
-                                         o.window_groups, None, wire=o.wire, interner=it, ctx_interner=xi))
+                                         o.window_groups, None, wire=o.wire, interner=it, encoder=enc))
             names = [f"svc-{g + 1}" for g in range(o.window_groups)]
             i = 0
             while True:
@@ -378,9 +378,15 @@ class Agent:
 
             from ..pipeline.window import stage_window
 
+            from ..collector.records import ConnInterner, native_encoder
+
+            # ring records are 64-byte EVENTs; the native encoder converts each window to the
+            # configured wire format (one encoder per stream keeps ids consistent)
+            it, enc = ConnInterner(), native_encoder()
             src = RingSource(o.ring_name, o.window_events, o.window_spans)
             for ev, sp, n_groups, names, t0 in src.windows(o.window_ms, self.stop_event, o.window_groups):
-                yield stage_window(torch, ev, sp, n_groups, None, o.window_groups, None, wire=64), names, t0
+                yield stage_window(torch, ev, sp, n_groups, None, o.window_groups, None, wire=o.wire, interner=it,
+                                   encoder=enc), names, t0
         else:
             raise ValueError(f"unknown window source {o.source!r}")
 

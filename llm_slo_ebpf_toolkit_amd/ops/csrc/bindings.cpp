@@ -107,10 +107,9 @@ class Engine {
     nblk_span_ = decode_grid(span_cap_);
     counts = torch::zeros({8}, i32);  // n_ev, n_spans, n_groups, n_local, t_base lo/hi, n_ctx (wire 20)
     // signal columns
-    g_ts = torch::empty({N}, i64); g_val = torch::empty({N}, f32); g_slot = torch::empty({N}, u8);
-    g_status = torch::empty({N}, u8); g_pod = torch::empty({N}, i32); g_pid = torch::empty({N}, i32);
-    g_svcnode = torch::empty({N}, i32); g_trace = torch::empty({N}, i64); g_conn = torch::empty({N}, i64);
-    g_hash = torch::empty({kKeyTypes * N}, i64);
+    // signals: 64-byte row records, status, partition codes of the 4 join keys
+    g_status = torch::empty({N}, u8);
+    g_part = torch::empty({N, 4}, torch::TensorOptions().dtype(torch::kInt16).device(dev_));
     g_part_blk = torch::empty({(int64_t)nblk_sig_ * kKeyTypes * kParts}, i32);
     g_part_off = torch::empty_like(g_part_blk);
     g_part_tot = torch::empty({kKeyTypes * kParts}, i32);
@@ -118,9 +117,7 @@ class Engine {
     g_items = torch::empty({kKeyTypes * N}, i32);
     g_rec = torch::empty({(int64_t)N * (int64_t)sizeof(SigRec)}, u8);
     // span columns
-    s_ts = torch::empty({S}, i64); s_trace = torch::empty({S}, i64); s_conn = torch::empty({S}, i64);
-    s_pod = torch::empty({S}, i32); s_pid = torch::empty({S}, i32); s_svcnode = torch::empty({S}, i32);
-    s_group = torch::empty({S}, i32); s_hash = torch::empty({kKeyTypes * S}, i64);
+    s_part = torch::empty({S, 4}, torch::TensorOptions().dtype(torch::kInt16).device(dev_));
     s_part_blk = torch::empty({(int64_t)nblk_span_ * kKeyTypes * kParts}, i32);
     s_part_off = torch::empty_like(s_part_blk);
     s_part_tot = torch::empty({kKeyTypes * kParts}, i32);
@@ -224,14 +221,11 @@ class Engine {
   }
 
   SignalCols sig_cols() {
-    return SignalCols{reinterpret_cast<SigRec*>(g_rec.data_ptr()), dptr<int64_t>(g_ts), dptr<float>(g_val), dptr<uint8_t>(g_slot), dptr<uint8_t>(g_status),
-                      dptr<uint32_t>(g_pod), dptr<uint32_t>(g_pid), dptr<uint32_t>(g_svcnode),
-                      dptr<uint64_t>(g_trace), dptr<uint64_t>(g_conn), dptr<uint64_t>(g_hash)};
+    return SignalCols{reinterpret_cast<SigRec*>(g_rec.data_ptr()), dptr<uint8_t>(g_status),
+                      reinterpret_cast<PartCodes*>(g_part.data_ptr())};
   }
   SpanCols span_cols() {
-    return SpanCols{reinterpret_cast<SpanRec*>(s_rec.data_ptr()), dptr<int64_t>(s_ts), dptr<uint64_t>(s_trace), dptr<uint64_t>(s_conn), dptr<uint32_t>(s_pod),
-                    dptr<uint32_t>(s_pid), dptr<uint32_t>(s_svcnode), dptr<uint32_t>(s_group),
-                    dptr<uint64_t>(s_hash)};
+    return SpanCols{reinterpret_cast<SpanRec*>(s_rec.data_ptr()), reinterpret_cast<PartCodes*>(s_part.data_ptr())};
   }
 
   // events: device uint8 tensor of 64-byte records (>= n*64 bytes); counts[0] must hold n.
@@ -242,7 +236,7 @@ class Engine {
     launch_decode_events(events.data_ptr(), dptr<int>(counts), sig_cap_, sig_cols(), dptr<uint32_t>(hist),
                          dptr<uint32_t>(status_cnt), dptr<uint32_t>(g_part_blk),
                          dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
                      dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
                      dptr<uint32_t>(g_items), cur_stream());
   }
@@ -262,7 +256,7 @@ class Engine {
     launch_decode_compact(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(pod_table),
                           (int)pod_table.numel(), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                           dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
                      dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
                      dptr<uint32_t>(g_items), cur_stream());
   }
@@ -285,7 +279,7 @@ class Engine {
     launch_decode_wire(events.data_ptr(), (int)wire, dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
                       (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                       dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
                      dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
                      dptr<uint32_t>(g_items), cur_stream());
   }
@@ -304,7 +298,7 @@ class Engine {
     launch_decode_ref(events.data_ptr(), dptr<int>(counts), sig_cap_, (uint32_t)pod, (uint32_t)svcnode,
                       (uint64_t)trace_h, sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                       dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(dptr<uint64_t>(g_hash), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
                      dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
                      dptr<uint32_t>(g_items), cur_stream());
   }
@@ -317,7 +311,7 @@ class Engine {
     if (n_groups > group_cap_) throw std::invalid_argument("n_groups exceeds group capacity");
     hipStream_t st = cur_stream();
     launch_decode_spans(spans.data_ptr(), dptr<int>(counts) + 1, span_cap_, span_cols(), dptr<uint32_t>(s_part_blk), st);
-    launch_partition(dptr<uint64_t>(s_hash), dptr<int>(counts) + 1, span_cap_, nblk_span_,
+    launch_partition(reinterpret_cast<const PartCodes*>(s_part.data_ptr()), dptr<int>(counts) + 1, span_cap_, nblk_span_,
                      dptr<uint32_t>(s_part_blk), dptr<uint32_t>(s_part_off), dptr<uint32_t>(s_part_tot),
                      dptr<uint32_t>(s_part_base), dptr<uint32_t>(s_items), st);
     // top3 / cnt / gsum / gcnt were reset by reset_window()
@@ -411,9 +405,9 @@ class Engine {
   int64_t packet_len() const { return kPacketLen; }
 
   torch::Tensor counts;
-  torch::Tensor g_ts, g_val, g_slot, g_status, g_pod, g_pid, g_svcnode, g_trace, g_conn, g_hash;
+  torch::Tensor g_status, g_part;
   torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items, g_rec, s_rec;
-  torch::Tensor s_ts, s_trace, s_conn, s_pod, s_pid, s_svcnode, s_group, s_hash;
+  torch::Tensor s_part;
   torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, probe_work;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
   torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
@@ -541,8 +535,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("group_cap", &Engine::group_cap)
       .def_property_readonly("packet_len", &Engine::packet_len)
 #define RO(name) .def_readonly(#name, &Engine::name)
-      RO(counts) RO(g_ts) RO(g_val) RO(g_slot) RO(g_status) RO(g_pod) RO(g_pid) RO(g_svcnode) RO(g_trace)
-      RO(g_conn) RO(g_hash) RO(g_part_base) RO(g_items) RO(s_ts) RO(s_hash) RO(s_part_base) RO(s_items) RO(probe_work)
+      RO(counts) RO(g_rec) RO(g_status) RO(g_part) RO(g_part_base) RO(g_items) RO(s_rec) RO(s_part)
+      RO(s_part_base) RO(s_items) RO(probe_work)
       RO(top3) RO(cnt) RO(attrs) RO(conf) RO(kernel_ms) RO(gsum) RO(gcnt) RO(feat) RO(labels) RO(post)
       RO(pred) RO(gconf) RO(evbits) RO(hist) RO(status_cnt) RO(misc) RO(dbg) RO(confusion) RO(stats)
       RO(stats_count) RO(packet) RO(model) RO(pod_table);

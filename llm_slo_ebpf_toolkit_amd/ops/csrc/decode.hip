@@ -68,15 +68,7 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
   } else if (local) {
     ++unsupported;
   }
-  o.cols.ts[i] = ts;
-  o.cols.val[i] = val;
-  o.cols.slot[i] = slot >= 0 ? (uint8_t)slot : kNoSlot;
   o.cols.status[i] = st;
-  o.cols.pod[i] = pod;
-  o.cols.pid[i] = pid;
-  o.cols.svcnode[i] = svcnode;
-  o.cols.trace_h[i] = trace_h;
-  o.cols.conn_h[i] = conn_h;
   {
     SigRec r;
     r.ts = ts;
@@ -93,12 +85,14 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
   // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
   const bool joinable = slot >= 0 && ts != 0;
   if (ts == 0 && local) ++zero_ts;
+  PartCodes pc;
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
-    uint64_t h = joinable ? key_hash(k, trace_h, pod, pid, conn_h, svcnode) : 0ull;
-    o.cols.hash[(size_t)k * cap + i] = h;
+    const uint64_t h = joinable ? key_hash(k, trace_h, pod, pid, conn_h, svcnode) : 0ull;
+    pc.p[k] = h ? (uint16_t)part_of(h) : kNoPart;
     if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
   }
+  o.cols.part[i] = pc;
 }
 
 template <int NT>
@@ -314,13 +308,6 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     const Span s = sp[i];
     const uint32_t svcnode = ((uint32_t)s.svc_id << 16) | s.node_id;
-    c.ts[i] = s.ts_ns;
-    c.trace_h[i] = s.trace_h;
-    c.conn_h[i] = s.conn_h;
-    c.pod[i] = s.pod_id;
-    c.pid[i] = s.pid;
-    c.svcnode[i] = svcnode;
-    c.group[i] = s.group_id;
     {
       SpanRec r;
       r.ts = s.ts_ns;
@@ -332,12 +319,14 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp
       r.grp = s.group_id;
       c.rec[i] = r;
     }
+    PartCodes pc;
 #pragma unroll
     for (int k = 0; k < kKeyTypes; ++k) {
-      uint64_t h = s.ts_ns != 0 ? key_hash(k, s.trace_h, s.pod_id, s.pid, s.conn_h, svcnode) : 0ull;
-      c.hash[(size_t)k * cap + i] = h;
+      const uint64_t h = s.ts_ns != 0 ? key_hash(k, s.trace_h, s.pod_id, s.pid, s.conn_h, svcnode) : 0ull;
+      pc.p[k] = h ? (uint16_t)part_of(h) : kNoPart;
       if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
     }
+    c.part[i] = pc;
   }
   __syncthreads();
   store_counts<NT>(s_part, part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);

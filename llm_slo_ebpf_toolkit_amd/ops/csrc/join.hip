@@ -98,7 +98,7 @@ __global__ __launch_bounds__(1024) void k_base_scan(const uint32_t* __restrict__
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_scatter(const uint64_t* __restrict__ hash, const int* __restrict__ n_ptr,
+__global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ codes, const int* __restrict__ n_ptr,
                                                 int cap, const uint32_t* __restrict__ part_off,
                                                 const uint32_t* __restrict__ base, uint32_t* __restrict__ items) {
   __shared__ uint32_t s_cnt[kKeyTypes * kParts];
@@ -109,11 +109,11 @@ __global__ __launch_bounds__(NT) void k_scatter(const uint64_t* __restrict__ has
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
   for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const PartCodes pc = codes[i];
 #pragma unroll
     for (int k = 0; k < kKeyTypes; ++k) {
-      const uint64_t h = hash[(size_t)k * cap + i];
-      if (!h) continue;
-      const int c = k * kParts + part_of(h);
+      if (pc.p[k] == kNoPart) continue;
+      const int c = k * kParts + pc.p[k];
       const uint32_t r = atomicAdd(&s_cnt[c], 1u);
       items[base[c] + my_off[c] + r] = (uint32_t)i;
     }
@@ -726,8 +726,9 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
       if (key == kEmpty || j >= keep) continue;
       const int tier = (int)(key >> 62);
       const uint32_t g = (uint32_t)(key & ((1ull << kSigBits) - 1));
-      const int slot = gc.slot[g];
-      const float v = gc.val[g];
+      const SigRec& r = gc.rec[g];
+      const int slot = (int)r.slot;
+      const float v = r.val;
       // REF merge: attr = value if absent or value > existing
       float cur = a[0];
 #pragma unroll
@@ -749,7 +750,7 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
     kernel_ms[s] = km > 0.f ? km : __builtin_nanf("");
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) attrs[(size_t)s * kSlots + j] = a[j];
-    const uint32_t grp = sc.group[s];
+    const uint32_t grp = sc.rec[s].grp;
     if (jp.group_mode == 0 && n_groups > 0 && grp < (uint32_t)n_groups) {
 #pragma unroll
       for (int j = 0; j < kSlots; ++j) {
@@ -800,13 +801,13 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 // host launchers
 // ---------------------------------------------------------------------------------------
 
-void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
+void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream) {
   hipLaunchKernelGGL(k_part_scan, dim3((kKeyTypes * kParts + 255) / 256), dim3(256), 0, stream, part_blk, nblk,
                      part_off, part_tot);
   hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(1024), 0, stream, part_tot, part_base);
-  hipLaunchKernelGGL((k_scatter<256>), dim3(nblk), dim3(256), 0, stream, hash, n_dev, cap, part_off, part_base,
+  hipLaunchKernelGGL((k_scatter<256>), dim3(nblk), dim3(256), 0, stream, codes, n_dev, cap, part_off, part_base,
                      items);
 }
 

@@ -112,30 +112,23 @@ struct alignas(64) SpanRec {
 };
 static_assert(sizeof(SigRec) == 64 && sizeof(SpanRec) == 64, "row records are one cache line");
 
+// Per-record partition codes of the 4 join keys (trace, pod+pid, pod+conn, svc+node):
+// the key hash's partition (top kPartBits bits) or kNoPart when the key is invalid. The
+// probe recomputes full hashes from the row records, so only 8 bytes per record are stored.
+constexpr uint16_t kNoPart = 0xFFFF;
+struct alignas(8) PartCodes {
+  uint16_t p[4];
+};
+
 struct SignalCols {
   SigRec* rec;
-  int64_t* ts;
-  float* val;
-  uint8_t* slot;      // kNoSlot = unsupported / unknown type
   uint8_t* status;    // 0 ok, 1 warning, 2 error
-  uint32_t* pod;
-  uint32_t* pid;
-  uint32_t* svcnode;  // (svc << 16) | node
-  uint64_t* trace_h;
-  uint64_t* conn_h;
-  uint64_t* hash;     // [kKeyTypes][n] partition hashes, 0 = key invalid
+  PartCodes* part;
 };
 
 struct SpanCols {
   SpanRec* rec;
-  int64_t* ts;
-  uint64_t* trace_h;
-  uint64_t* conn_h;
-  uint32_t* pod;
-  uint32_t* pid;
-  uint32_t* svcnode;
-  uint32_t* group;
-  uint64_t* hash;     // [kKeyTypes][n]
+  PartCodes* part;
 };
 
 // Correlation tiers (REF pkg/correlation/dns.go:50-76).

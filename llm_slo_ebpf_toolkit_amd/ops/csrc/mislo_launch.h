@@ -40,7 +40,7 @@ void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCo
                          hipStream_t stream);
 
 // join.hip
-void launch_partition(const uint64_t* hash, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
+void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream);
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,

@@ -76,6 +76,19 @@ def decode_debug(dbg: np.ndarray, misc: np.ndarray, n_spans: int, n_events: int)
     }
 
 
+# device row records (ops/csrc/mislo_common.h SigRec / SpanRec), for inspection and tests
+SIG_ROW = np.dtype([("ts", "<i8"), ("trace", "<u8"), ("conn", "<u8"), ("pod", "<u4"), ("pid", "<u4"),
+                    ("svcnode", "<u4"), ("val", "<f4"), ("slot", "<u4"), ("pad", "V20")])
+SPAN_ROW = np.dtype([("ts", "<i8"), ("trace", "<u8"), ("conn", "<u8"), ("pod", "<u4"), ("pid", "<u4"),
+                     ("svcnode", "<u4"), ("group", "<u4"), ("pad", "V24")])
+assert SIG_ROW.itemsize == 64 and SPAN_ROW.itemsize == 64
+
+
+def signal_rows(eng, n: int) -> np.ndarray:
+    """The first n decoded signal row records of an Engine (host copy)."""
+    return eng.g_rec[: n * 64].cpu().numpy().view(SIG_ROW)
+
+
 @dataclass
 class WindowOutputs:
     hist: np.ndarray

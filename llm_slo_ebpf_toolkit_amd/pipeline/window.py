@@ -93,19 +93,25 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
     t_enc = time.perf_counter()
     pod_tab = None
     ctx_rows, n_ctx, t_base = None, 0, 0
-    if wire in (20, 16) and ctx_interner is None:
+    if wire in (20, 16) and ctx_interner is None and events.dtype == records.EVENT:
         enc = encoder if encoder is not None else records.native_encoder()
         ev = torch.empty(max(events.shape[0], 1) * wire, dtype=torch.uint8).pin_memory()
         sp = torch.empty(max(spans.shape[0], 1) * 64, dtype=torch.uint8).pin_memory()
         t_enc = time.perf_counter()  # conversion only (the agent reuses its pinned buffers)
-        t_base = enc.encode(np.ascontiguousarray(events), ev.numpy(), wire)
-        enc.encode_spans(np.ascontiguousarray(spans), sp.numpy(), wire == 16)
-        enc.end_window()
-        tab = enc.ctx_table()
-        n_ctx = int(tab.shape[0])
-        ctx_rows = torch.from_numpy(tab).pin_memory()
-        return _finish_stage(torch, ev, sp, events.shape[0], spans.shape[0], n_groups, labels, group_cap,
-                             group_domains, wire, None, ctx_rows, n_ctx, t_base, n_local, t_enc)
+        try:
+            t_base = enc.encode(np.ascontiguousarray(events), ev.numpy(), wire)
+        except ValueError:
+            # the window's timestamps span >= 2^32 ns (late / skewed producers): this window
+            # travels as 32-byte records, which carry absolute timestamps
+            wire = 32
+        else:
+            enc.encode_spans(np.ascontiguousarray(spans), sp.numpy(), wire == 16)
+            enc.end_window()
+            tab = enc.ctx_table()
+            n_ctx = int(tab.shape[0])
+            ctx_rows = torch.from_numpy(tab).pin_memory()
+            return _finish_stage(torch, ev, sp, events.shape[0], spans.shape[0], n_groups, labels, group_cap,
+                                 group_domains, wire, None, ctx_rows, n_ctx, t_base, n_local, t_enc)
     if wire in (32, 20, 16):
         if interner is None:
             interner = records.ConnInterner()

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, SufficientStats
+from llm_slo_ebpf_toolkit_amd.ops.engine import signal_rows as rows
 from llm_slo_ebpf_toolkit_amd.pipeline import oracle
 from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
 
@@ -39,8 +40,8 @@ def test_decode_join_matches_oracle(engine, group_mode):
     e = engine.eng
     d = oracle.decode_events(win.events)
     N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(e.g_slot[:N].cpu().numpy(), d.slot)
-    np.testing.assert_array_equal(e.g_val[:N].cpu().numpy(), d.val)
+    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
+    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
     np.testing.assert_array_equal(out.hist, oracle.histograms(d))
     np.testing.assert_array_equal(e.misc[2:18].cpu().numpy(), oracle.value_sums_milli(d))
     ref = oracle.join(d, win.spans, win.n_groups, group_mode=group_mode)
@@ -117,8 +118,8 @@ def test_ref_record_decode(engine):
     engine.eng.reset_window()
     engine.eng.decode_ref(dev, 3, (1 << 16) | 2, 0)
     torch.cuda.synchronize()
-    val = engine.eng.g_val[:5].cpu().numpy()
-    slot = engine.eng.g_slot[:5].cpu().numpy()
+    val = rows(engine.eng, 5)["val"]
+    slot = rows(engine.eng, 5)["slot"]
     # REF convertValue (ringbuf.go:229-238): unknown types fall into the ns -> ms default
     np.testing.assert_allclose(val, [220.0, 3.0, 1500.0, 51.0, 1e-6], rtol=1e-6)
     assert list(slot) == [0, 1, 7, 11, 255]
@@ -140,9 +141,9 @@ def test_compact_wire_matches_oracle(engine):
     e = engine.eng
     d = oracle.decode_compact(ev32, table)
     N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(e.g_slot[:N].cpu().numpy(), d.slot)
-    np.testing.assert_array_equal(e.g_val[:N].cpu().numpy(), d.val)
-    np.testing.assert_array_equal(e.g_svcnode[:N].cpu().numpy().view(np.uint32), d.svcnode)
+    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
+    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
+    np.testing.assert_array_equal(rows(e, N)["svcnode"], d.svcnode)
     ref = oracle.join(d, sp, win.n_groups)
     top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
     np.testing.assert_array_equal(top3, ref.top3)
@@ -173,11 +174,11 @@ def test_wire20_matches_oracle(engine):
     e = engine.eng
     d = oracle.decode_w20(ev20, t_base, ctxs.table())
     N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(e.g_ts[:N].cpu().numpy(), d.ts)
-    np.testing.assert_array_equal(e.g_slot[:N].cpu().numpy(), d.slot)
-    np.testing.assert_array_equal(e.g_val[:N].cpu().numpy(), d.val)
-    np.testing.assert_array_equal(e.g_pid[:N].cpu().numpy().view(np.uint32), d.pid)
-    np.testing.assert_array_equal(e.g_svcnode[:N].cpu().numpy().view(np.uint32), d.svcnode)
+    np.testing.assert_array_equal(rows(e, N)["ts"], d.ts)
+    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
+    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
+    np.testing.assert_array_equal(rows(e, N)["pid"], d.pid)
+    np.testing.assert_array_equal(rows(e, N)["svcnode"], d.svcnode)
     ref = oracle.join(d, sp, win.n_groups)
     top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
     np.testing.assert_array_equal(top3, ref.top3)
@@ -210,7 +211,7 @@ def test_wire16_native_matches_oracle(engine):
     e = engine.eng
     d = oracle.decode_w16(ev16, t_base, enc.ctx_table())
     S = win.n_spans
-    np.testing.assert_array_equal(e.g_ts[: win.n_events].cpu().numpy(), d.ts)
+    np.testing.assert_array_equal(rows(e, win.n_events)["ts"], d.ts)
     ref = oracle.join(d, sp, win.n_groups)
     top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
     np.testing.assert_array_equal(top3, ref.top3)
