@@ -5,7 +5,9 @@ Metric (BASELINE.json): "attribution macro-F1 on fault-replay confusion matrix; 
 overhead %", reported on config 5 ("full 9 CPU + 4 GPU signals, safety governor <= 3 %
 overhead, full confusion matrix across all fault domains") plus the events/s scaling
 curve the north star asks for. One step = one 1-second collection window per GPU:
-H2D of the window's 64-byte event/span records -> decode + histograms -> LDS hash join
+the 64-byte probe records of the window (as the probes write them into the agent's ring) ->
+host wire encoding (native, worker pool; skipped only with --wire 64, which DMAs the pinned
+ring records as-is) -> H2D -> decode + histograms -> LDS hash join
 -> MFMA posteriors + confusion -> MFMA sufficient statistics -> RCCL all-reduce of the
 packed window statistics -> online model refit. ``value`` = node-wide events/s (weak
 scaling: every GPU owns one node's shard of pods, 1M events per window).
@@ -51,10 +53,13 @@ def parse():
                     help="windows the host may run ahead of the GPU (host back-pressure)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", type=int, default=16, choices=(16, 20, 32, 64),
-                    help="event record bytes on PCIe: 16 = EVENT16 (EVENT20 + interned trace ids), "
-                         "20 = EVENT20 (window-relative ts, interned contexts), 32 = compact (interned ids), "
-                         "64 = full")
+    ap.add_argument("--wire", type=int, default=64, choices=(16, 20, 64),
+                    help="event record bytes on PCIe: 64 = the probe records DMA'd from the pinned ring "
+                         "as-is (default: no per-event host work); 16 = EVENT16 / 20 = EVENT20, encoded on "
+                         "the host inside every step (interned contexts and trace ids, 1/4 of the PCIe "
+                         "bytes, but the encoder reads the same 64 B per event the DMA would)")
+    ap.add_argument("--encode-threads", type=int, default=0,
+                    help="host encoder worker threads (0 = OMP_NUM_THREADS, else 8; at most 16)")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -69,7 +74,7 @@ def main() -> int:
     from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, samples_to_arrays
     from llm_slo_ebpf_toolkit_amd.ops import require_gpu_extension
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, stage_window
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, WireStager
     from llm_slo_ebpf_toolkit_amd.safety import CPUMeter, OverheadGuard, read_rss_mb
     from llm_slo_ebpf_toolkit_amd.signals import catalog
 
@@ -90,26 +95,33 @@ def main() -> int:
             print("[bench]", *x, file=sys.stderr, flush=True)
 
     # ---- data: this rank's shard of the node (its own pods/services) ------------------
+    # The windows are the 64-byte records the probes write into the agent's ring; converting
+    # them to the wire format (native encoder on a worker pool) is part of every timed step.
     t = time.time()
     cfg = ReplayConfig(scenario=a.scenario, events_per_window=a.events, spans_per_window=a.spans,
                        n_services=a.services, seed=a.seed, shard=rank)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
-    from llm_slo_ebpf_toolkit_amd.collector.records import ConnInterner, native_encoder
-    # one native encoder per record stream (ids stay consistent across windows); its cost
-    # is reported as host_encode_ms_per_window
-    interner, encoder = ConnInterner(), native_encoder()
-    staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, a.services, w.group_domains,
-                           wire=a.wire, interner=interner, encoder=encoder) for w in wins]
-    encode_ms = 1e3 * float(np.mean([s.encode_s for s in staged]))
+    ring = None
+    if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
+        ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
+                 torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
                           group_scope=a.group_scope, use_graphs=not a.no_graphs, max_ahead=a.max_ahead)
+    threads = a.encode_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 8)
+    stager = WireStager(torch, pipe, a.events, a.spans, a.services, wire=a.wire, threads=threads)
+
+    def stage(j):
+        w = wins[j % len(wins)]
+        evp, spp = ring[j % len(wins)] if ring else (None, None)
+        return stager.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
+                            ev_pinned=evp, sp_pinned=spp)
 
     def run(n, start):
         for i in range(n):
-            pipe.submit(staged[(start + i) % len(staged)])
+            pipe.submit(stage(start + i))
 
     # ---- warmup (also the model's first training windows) ------------------------------
     run(a.warmup, 0)
@@ -117,6 +129,7 @@ def main() -> int:
     if pg is not None:
         dist.barrier()
     pipe.reset_totals()
+    enc0, nstage0 = stager.encode_s, stager.k
 
     # ---- timed region -------------------------------------------------------------------
     meter = CPUMeter()
@@ -134,6 +147,7 @@ def main() -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     host_us = pipe.host_issue_us()
+    encode_ms = 1e3 * (stager.encode_s - enc0) / max(stager.k - nstage0, 1)
     busy_cpu_pct, _, _ = meter.stop()
     if pg is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -155,7 +169,7 @@ def main() -> int:
         nxt = time.perf_counter()
         for i in range(a.paced_windows):
             ts = time.perf_counter()
-            pipe.submit(staged[i % len(staged)])
+            pipe.submit(stage(i))
             ev = torch.cuda.Event()
             ev.record(pipe.comm_stream)
             nxt += period
@@ -225,7 +239,8 @@ def main() -> int:
         "ref55_single_fault_macro_f1": {k: round(v, 4) for k, v in ref_f1.items()},
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
         "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
-        "host_encode_ms_per_window": round(encode_ms, 2),
+        "host_encode_ms_per_window": round(encode_ms, 3),
+        "host_encode_threads": threads if a.wire != 64 else 0,
     }
     if rank == 0:
         line = json.dumps(res)

@@ -153,6 +153,78 @@ def _finish_stage(torch, ev, sp, n_ev: int, n_sp: int, n_groups: int, labels, gr
                         pod_tab, ctx_rows, n_ctx, time.perf_counter() - t_enc)
 
 
+class WireStager:
+    """The agent's per-window host stage: 64-byte probe records (as the probes write them into
+    the ring) -> 16/20-byte wire records in one of two reusable pinned slots, on the native
+    encoder's worker pool (runtime/csrc/wire.h ``encode_window``). Window k writes slot k % 2,
+    the buffer the pipeline's H2D of window k reads, after the H2D of window k - 2 (the slot's
+    previous reader) has completed, so encoding window k+1 overlaps the GPU work of window k.
+
+    ``wire=64`` ships the ring records unchanged: ``events``/``spans`` must then already sit in
+    pinned memory (the probe ring is pinned), and staging only fills the counts and labels."""
+
+    def __init__(self, torch, pipe: "WindowPipeline", sig_cap: int, span_cap: int, group_cap: int, wire: int = 16,
+                 threads: int = 8):
+        if wire not in (16, 20, 64):
+            raise ValueError("WireStager: wire must be 16, 20 or 64")
+        self.torch, self.pipe, self.wire, self.threads = torch, pipe, wire, max(1, int(threads))
+        self.group_cap = group_cap
+        pin = lambda n, dt=torch.uint8: torch.empty(n, dtype=dt).pin_memory()  # noqa: E731
+        self.enc = records.native_encoder() if wire != 64 else None
+        self.ev = [pin(max(sig_cap, 1) * wire) for _ in range(2)] if wire != 64 else None
+        self.sp = [pin(max(span_cap, 1) * 64) for _ in range(2)] if wire != 64 else None
+        self.counts = [pin(8, torch.int32) for _ in range(2)]
+        self.labels = [pin(group_cap, torch.int32) for _ in range(2)]
+        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire != 64 else None
+        self.n_ctx = 1
+        self.k = 0
+        self.encode_s = 0.0
+
+    def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
+              group_domains=None, n_local: Optional[int] = None, ev_pinned=None, sp_pinned=None) -> StagedWindow:
+        torch = self.torch
+        slot = self.k % 2
+        if self.k >= 2:  # slot's previous reader: the H2D of window k - 2
+            self.pipe.h2d_done[slot].synchronize()
+        t0 = time.perf_counter()
+        n_ev, n_sp = int(events.shape[0]), int(spans.shape[0])
+        t_base = 0
+        if self.wire == 64:
+            ev, sp = ev_pinned, sp_pinned
+            if ev is None or sp is None:
+                raise ValueError("wire 64 stages the pinned ring records: pass ev_pinned / sp_pinned")
+        else:
+            ev, sp = self.ev[slot], self.sp[slot]
+            if n_ev * self.wire > ev.numel() or n_sp * 64 > sp.numel():
+                raise ValueError("window exceeds the stager's capacity")
+            t_base = self.enc.encode_window(events, ev.numpy(), self.wire, spans, sp.numpy(), self.threads)
+            self.enc.end_window()
+            n_ctx = int(self.enc.n_ctx)
+            if n_ctx > self.n_ctx:  # new context rows (append-only: rows < n_ctx never change)
+                if n_ctx > self.ctx.shape[0]:
+                    cap = 1 << int(np.ceil(np.log2(n_ctx)))
+                    grown = torch.empty(cap * 4, dtype=torch.int32).pin_memory().view(-1, 4)
+                    grown[: self.n_ctx].copy_(self.ctx[: self.n_ctx])
+                    self.ctx = grown
+                self.ctx.numpy()[self.n_ctx:n_ctx] = self.enc.ctx_table()[self.n_ctx:n_ctx]
+                self.n_ctx = n_ctx
+        nl = 0 if n_local is None or n_local >= n_ev else int(n_local)
+        tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
+        c = self.counts[slot].numpy()
+        c[:] = np.array([n_ev, n_sp, n_groups, nl, tb & 0xFFFFFFFF, tb >> 32, self.n_ctx if self.ctx is not None else 0,
+                         0], dtype=np.uint64).astype(np.uint32).view(np.int32)
+        lab = self.labels[slot].numpy()
+        lab[:] = -1
+        if labels is not None:
+            lab[: len(labels)] = labels
+        self.k += 1
+        dt = time.perf_counter() - t0
+        self.encode_s += dt
+        return StagedWindow(ev, sp, self.counts[slot], self.labels[slot], n_ev, n_sp, n_groups,
+                            list(group_domains or []), self.wire, None, self.ctx if self.wire != 64 else None,
+                            self.n_ctx if self.wire != 64 else 0, dt)
+
+
 class WindowPipeline:
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, process_group=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,

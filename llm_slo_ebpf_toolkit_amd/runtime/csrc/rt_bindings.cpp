@@ -176,6 +176,22 @@ class PyWireEncoder {
                        static_cast<mislo::SpanRec64*>(oi.ptr), trace_ids);
   }
 
+  // one window on the worker pool (wire.h encode_window): events -> ev_out, spans -> sp_out
+  int64_t encode_window(py::buffer events, py::buffer ev_out, int wire, py::buffer spans, py::buffer sp_out,
+                        int threads, size_t min_chunk) {
+    py::buffer_info ei = events.request(), eo = ev_out.request(true), si = spans.request(), so = sp_out.request(true);
+    const size_t nb = (size_t)ei.size * ei.itemsize, sb = (size_t)si.size * si.itemsize;
+    if (nb % sizeof(mislo::EventRec)) throw std::invalid_argument("events: not a whole number of 64-byte records");
+    if (sb % sizeof(mislo::SpanRec64)) throw std::invalid_argument("spans: not a whole number of 64-byte records");
+    const size_t n = nb / sizeof(mislo::EventRec), ns = sb / sizeof(mislo::SpanRec64);
+    if ((size_t)eo.size * eo.itemsize < n * (size_t)wire) throw std::invalid_argument("ev_out buffer too small");
+    if ((size_t)so.size * so.itemsize < sb) throw std::invalid_argument("sp_out buffer too small");
+    py::gil_scoped_release nogil;
+    return enc_->encode_window(static_cast<const mislo::EventRec*>(ei.ptr), n, eo.ptr, wire,
+                               static_cast<const mislo::SpanRec64*>(si.ptr), ns,
+                               static_cast<mislo::SpanRec64*>(so.ptr), threads, min_chunk);
+  }
+
   void end_window() { enc_->end_window(); }
 
   // context table (int32 [n, 4]: pod, pid, conn id, svc<<16|node), row i = context id i
@@ -225,6 +241,9 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def("encode", &PyWireEncoder::encode, py::arg("events"), py::arg("out"), py::arg("wire") = 20)
       .def("encode_spans", &PyWireEncoder::encode_spans, py::arg("spans"), py::arg("out"),
            py::arg("trace_ids") = false)
+      .def("encode_window", &PyWireEncoder::encode_window, py::arg("events"), py::arg("ev_out"), py::arg("wire"),
+           py::arg("spans"), py::arg("sp_out"), py::arg("threads") = 8,
+           py::arg("min_chunk") = 16384)
       .def("end_window", &PyWireEncoder::end_window)
       .def("ctx_table", &PyWireEncoder::ctx_table)
       .def_property_readonly("n_ctx", &PyWireEncoder::n_ctx)

@@ -9,11 +9,27 @@
 //   * EVENT16 only: 64-bit trace hash -> 32-bit id, shared with the spans of the same
 //     window so trace equality is exact; ids of traces unseen for two windows are dropped.
 // Hash maps are flat open-addressing tables (power-of-two, linear probing, load <= 1/2).
+//
+// encode_window() is the agent's hot path: one window's events and spans in three phases on a
+// worker pool, byte-identical to encode() + encode_spans() run sequentially:
+//   1. parallel over contiguous chunks: fixed-point values and provisional timestamps; every
+//      key is looked up in the (read-only) global tables; keys not there yet go to a chunk-
+//      local first-seen list and the record holds the local index, noted in a fix-up list;
+//   2. serial: the chunks' new-key lists are merged in chunk order, which is global first-
+//      occurrence order, so ids come out exactly as the sequential encoder assigns them;
+//   3. parallel: fix-up records get their global ids (and timestamps are rebased in the rare
+//      window whose first event is not its earliest).
 #pragma once
 
 #include <array>
+#include <atomic>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace mislo {
@@ -90,15 +106,77 @@ class TraceTable {
  public:
   TraceTable();
   uint32_t id(uint64_t tr, uint32_t gen);
+  // read-only lookup for concurrent readers: id or 0 if absent; marks the entry used in `gen`
+  // (a relaxed store, only when it changes)
+  uint32_t find_touch(uint64_t tr, uint32_t gen);
   void expire(uint32_t min_gen);
   size_t size() const { return size_; }
 
  private:
   void rehash(size_t cap, uint32_t min_gen);
-  std::vector<uint64_t> keys_;
-  std::vector<uint32_t> ids_, gens_;
+  struct Slot {  // one cache access per probe
+    uint64_t key;
+    uint32_t id, gen;
+  };
+  std::vector<Slot> slots_;
   size_t mask_ = 0, size_ = 0;
   uint32_t next_ = 1;
+};
+
+// (pod<<32|pid, conn key, svc<<16|node) -> id with the key stored in the slot (one cache
+// access per probe; no side table to compare against). id kEmpty marks a free slot.
+class CtxMap {
+ public:
+  static constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+  explicit CtxMap(size_t cap = 64);
+  uint32_t find(uint64_t h, uint64_t ppid, uint64_t ck, uint32_t sn) const;  // kEmpty if absent
+  void insert(uint64_t h, uint64_t ppid, uint64_t ck, uint32_t sn, uint32_t id);
+  size_t size() const { return size_; }
+  void clear();
+
+ private:
+  struct Slot {
+    uint64_t ppid, ck, h;
+    uint32_t sn, id;
+  };
+  std::vector<Slot> slots_;
+  size_t mask_ = 0, size_ = 0;
+};
+
+// Fixed pool of worker threads; run(n, fn) executes fn(0..n-1) on the workers and the calling
+// thread and returns when all are done. Idle workers block on a condition variable (no
+// spinning: the agent's CPU budget is measured).
+class WorkerPool {
+ public:
+  explicit WorkerPool(int threads);
+  ~WorkerPool();
+  void run(int ntasks, const std::function<void(int)>& fn);
+  int threads() const { return (int)workers_.size() + 1; }
+
+ private:
+  void loop();
+  void drain_tasks();
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int ntasks_ = 0;
+  std::atomic<int> next_{0};
+  int pending_ = 0;  // tasks not finished (guarded by mu_)
+  uint64_t epoch_ = 0;
+  bool stop_ = false;
+};
+
+// Per-chunk scratch of encode_window (reused across windows).
+struct ChunkScratch {
+  int64_t tmin, tmax;
+  FlatMap conn_map{64}, trace_map{256};
+  CtxMap ctx_map{64};
+  std::vector<uint64_t> new_conns, new_traces;
+  std::vector<std::array<uint64_t, 3>> new_ctx;  // pod<<32|pid, conn key, svc<<16|node
+  std::vector<uint64_t> fix;                     // record index << 2 | (1: ctx / conn, 2: trace)
+  std::vector<uint32_t> conn_remap, ctx_remap, trace_remap;
+  void reset();
 };
 
 class WireEncoder {
@@ -113,6 +191,11 @@ class WireEncoder {
   void encode_spans(const SpanRec64* in, size_t n, SpanRec64* out, bool trace_ids);
   // Trace-id generation boundary (call once per window after events and spans).
   void end_window();
+  // events -> ev_out (wire 20/16) and spans -> sp_out in one pass on `threads` threads; the
+  // same bytes and ids as encode() then encode_spans(ev_out, trace_ids = wire == 16). Does not
+  // call end_window(). Throws std::range_error (tables untouched) like encode().
+  int64_t encode_window(const EventRec* ev, size_t n, void* ev_out, int wire, const SpanRec64* sp, size_t n_sp,
+                        SpanRec64* sp_out, int threads, size_t min_chunk = 16384);
 
   const std::vector<std::array<uint32_t, 4>>& ctx_rows() const { return ctx_rows_; }
   size_t n_conns() const { return n_conns_; }
@@ -121,13 +204,22 @@ class WireEncoder {
 
  private:
   uint32_t conn_id(uint64_t key);
-  uint32_t ctx_id(uint32_t pod, uint32_t pid, uint32_t cid, uint32_t sn);
+  uint32_t conn_find(uint64_t key);  // read-only: 0 if absent (key != 0)
+  // contexts are keyed by the connection KEY (a bijection with its id), so chunks can test a
+  // context for novelty before new connections have ids
+  uint32_t ctx_id(uint32_t pod, uint32_t pid, uint64_t ckey, uint32_t sn);
+  uint32_t ctx_find(uint32_t pod, uint32_t pid, uint64_t ckey, uint32_t sn);  // read-only: kAbsent
+  static constexpr uint32_t kAbsent = CtxMap::kEmpty;
+  void encode_chunk(const EventRec* ev, size_t lo, size_t hi, int64_t base, void* out, int wire, ChunkScratch& cs);
+  void spans_chunk(const SpanRec64* sp, size_t lo, size_t hi, SpanRec64* out, bool trace_ids, ChunkScratch& cs);
 
   double scale_[256];
   FlatMap conns_{1 << 12};
   size_t n_conns_ = 0;
-  FlatMap ctx_{1 << 12};
+  CtxMap ctx_{1 << 12};
   std::vector<std::array<uint32_t, 4>> ctx_rows_;
+  std::unique_ptr<WorkerPool> pool_;
+  std::vector<ChunkScratch> chunks_;
   TraceTable traces_;
   uint32_t gen_ = 1;
 };

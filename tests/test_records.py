@@ -142,3 +142,43 @@ def test_native_encoder_matches_numpy_reference():
     # numpy EVENT16 reference agrees too
     r16, _ = records.to_wire16(ev, records.ConnInterner(), records.CtxInterner(), records.TraceInterner())
     assert r16.dtype == records.EVENT16
+
+
+def test_pooled_encode_window_is_byte_identical_to_sequential():
+    """wire.cpp encode_window (3-phase worker pool) == encode() + encode_spans(), ids included,
+    across windows (ids persist), thread counts, a window whose first event is not its
+    earliest (timestamp rebase), zero timestamps, and connections first seen in spans."""
+    pytest = __import__("pytest")
+    try:
+        seq, par = records.native_encoder(), records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    for wire in (16, 20):
+        seq, par = records.native_encoder(), records.native_encoder()
+        for k, threads in enumerate((1, 3, 8, 5)):
+            win = _win(seed=11 + k)
+            ev, sp = win.events.copy(), win.spans.copy()
+            if k == 1:
+                ev = ev[::-1].copy()  # first record is the latest
+            if k == 2:
+                ev["ts_ns"][::97] = 0
+                sp["conn_h"][::5] = np.arange(sp.shape[0])[::5].astype(np.uint64) * 7919 + 1  # span-only conns
+            oa, ob = np.zeros(ev.shape[0] * wire, np.uint8), np.zeros(ev.shape[0] * wire, np.uint8)
+            sa, sb = np.zeros_like(sp), np.zeros_like(sp)
+            ta = seq.encode(ev, oa, wire)
+            seq.encode_spans(sp, sa, wire == 16)
+            tb = par.encode_window(ev, ob, wire, sp, sb, threads, 256)  # ~12 event + 6 span chunks
+            seq.end_window()
+            par.end_window()
+            assert ta == tb
+            np.testing.assert_array_equal(oa, ob, err_msg=f"wire {wire} window {k}")
+            np.testing.assert_array_equal(sa.view(np.uint8), sb.view(np.uint8))
+            np.testing.assert_array_equal(seq.ctx_table(), par.ctx_table())
+            assert (seq.n_conns, seq.n_traces) == (par.n_conns, par.n_traces)
+    # a window too wide for 32-bit offsets is refused before any table changes
+    ev = _win(seed=3).events.copy()
+    ev["ts_ns"][5] = ev["ts_ns"].max() + (1 << 33)
+    n0 = par.n_ctx
+    with pytest.raises(ValueError):
+        par.encode_window(ev, np.zeros(ev.shape[0] * 16, np.uint8), 16, sp, np.zeros_like(sp), 4, 256)
+    assert par.n_ctx == n0
