@@ -84,10 +84,19 @@ def main() -> int:
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     require_gpu_extension()
+    # MISLO_BENCH_GPU_OF_RANK=0 pins every rank to cuda:0 and MISLO_DIST_BACKEND=gloo swaps
+    # RCCL for gloo: a multi-rank rehearsal of the distributed path on a one-GPU box (RCCL
+    # refuses two ranks on one device). Real runs use neither.
+    if os.environ.get("MISLO_BENCH_GPU_OF_RANK") is not None:
+        local = int(os.environ["MISLO_BENCH_GPU_OF_RANK"])
     torch.cuda.set_device(local)
     pg = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("MISLO_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
 
     def log(*x):
