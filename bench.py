@@ -4,10 +4,10 @@ quality/overhead metrics measured in the same run.
 Metric (BASELINE.json): "attribution macro-F1 on fault-replay confusion matrix; agent CPU
 overhead %", reported on config 5 ("full 9 CPU + 4 GPU signals, safety governor <= 3 %
 overhead, full confusion matrix across all fault domains") plus the events/s scaling
-curve the north star asks for. One step = one 1-second collection window per GPU:
-the 64-byte probe records of the window (as the probes write them into the agent's ring) ->
-host wire encoding (native, worker pool; skipped only with --wire 64, which DMAs the pinned
-ring records as-is) -> H2D -> decode + histograms -> LDS hash join
+curve the north star asks for. One step = one 1-second collection window per GPU, from
+the records the probes wrote into the agent's pinned ring (32-byte EVENT32 by default) ->
+host work (spans mapped onto the kernel's connection ids; with --wire 16/20, wire encoding
+of 64-byte records on a native worker pool) -> H2D -> decode + histograms -> LDS hash join
 -> MFMA posteriors + confusion -> MFMA sufficient statistics -> RCCL all-reduce of the
 packed window statistics -> online model refit. ``value`` = node-wide events/s (weak
 scaling: every GPU owns one node's shard of pods, 1M events per window).
@@ -53,11 +53,13 @@ def parse():
                     help="windows the host may run ahead of the GPU (host back-pressure)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", type=int, default=64, choices=(16, 20, 64),
-                    help="event record bytes on PCIe: 64 = the probe records DMA'd from the pinned ring "
-                         "as-is (default: no per-event host work); 16 = EVENT16 / 20 = EVENT20, encoded on "
-                         "the host inside every step (interned contexts and trace ids, 1/4 of the PCIe "
-                         "bytes, but the encoder reads the same 64 B per event the DMA would)")
+    ap.add_argument("--wire", type=int, default=32, choices=(16, 20, 32, 64),
+                    help="event record bytes on PCIe. 32 (default) / 64: the probes' 32-byte EVENT32 "
+                         "(kernel-interned connections, fixed-point values) / 64-byte EVENT records, DMA'd "
+                         "from the pinned ring as-is (no per-event host work; spans are mapped onto the "
+                         "connection ids for 32); 16 = EVENT16 / 20 = EVENT20, encoded from 64-byte records "
+                         "on the host inside every step (interned contexts and trace ids; the encoder reads "
+                         "the same 64 B per event the DMA would)")
     ap.add_argument("--encode-threads", type=int, default=0,
                     help="host encoder worker threads (0 = OMP_NUM_THREADS, else 8; at most 16)")
     ap.add_argument("--out", default="")
@@ -74,6 +76,7 @@ def main() -> int:
     from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, samples_to_arrays
     from llm_slo_ebpf_toolkit_amd.ops import require_gpu_extension
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+    from llm_slo_ebpf_toolkit_amd.collector import records
     from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, WireStager
     from llm_slo_ebpf_toolkit_amd.safety import CPUMeter, OverheadGuard, read_rss_mb
     from llm_slo_ebpf_toolkit_amd.signals import catalog
@@ -111,22 +114,25 @@ def main() -> int:
                        n_services=a.services, seed=a.seed, shard=rank)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
-    ring = None
-    if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
-        ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
-                 torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-    log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
-
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
                           group_scope=a.group_scope, use_graphs=not a.no_graphs, max_ahead=a.max_ahead)
     threads = a.encode_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 8)
     stager = WireStager(torch, pipe, a.events, a.spans, a.services, wire=a.wire, threads=threads)
+    ring, pods = None, None
+    if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
+        ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
+                 torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
+    elif a.wire == 32:  # the probes' own 32-byte records (kernel-interned connections)
+        ring = [(stager.probe_records32(w.events), None) for w in wins]
+        # pod id -> svc|node: agent metadata (kubelet / CRI), static over the run
+        pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
+    log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
 
     def stage(j):
         w = wins[j % len(wins)]
         evp, spp = ring[j % len(wins)] if ring else (None, None)
         return stager.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
-                            ev_pinned=evp, sp_pinned=spp)
+                            ev_pinned=evp, sp_pinned=spp, pod_table=pods)
 
     def run(n, start):
         for i in range(n):
@@ -249,7 +255,7 @@ def main() -> int:
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
         "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
         "host_encode_ms_per_window": round(encode_ms, 3),
-        "host_encode_threads": threads if a.wire != 64 else 0,
+        "host_encode_threads": threads if a.wire in (16, 20) else 0,
     }
     if rank == 0:
         line = json.dumps(res)

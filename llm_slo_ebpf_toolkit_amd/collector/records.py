@@ -237,13 +237,54 @@ class ConnInterner:
         return out[inv]
 
 
-def _milli_values(events: np.ndarray) -> np.ndarray:
-    scale = np.ones(65536, dtype=np.float64)
+def milli_shift_table() -> np.ndarray:
+    """Per kernel signal type (< 256): the power of ten d with value_milli = raw * 10**d, i.e.
+    log10(decode_scale * 1000). Every catalogue scale is a power of ten (ns -> ms: -3,
+    counts: +3, milli-percent / ns -> us: 0), so the fixed-point conversion is integer-only
+    and the BPF probes compute it in the kernel (probes/ebpf/mislo_record.h mislo_milli)."""
+    shift = np.full(256, 3, dtype=np.int8)  # unknown types: scale 1
     for s in catalog.SIGNALS:
-        scale[s.kernel_type] = s.decode_scale
+        if s.kernel_type < 256:
+            d = float(np.log10(s.decode_scale * 1000.0))
+            if abs(d - round(d)) > 1e-9 or not -9 <= round(d) <= 9:
+                raise ValueError(f"{s.name}: decode_scale {s.decode_scale} is not a power of ten")
+            shift[s.kernel_type] = int(round(d))
+    return shift
+
+
+def milli_int(raw: np.ndarray, shift: np.ndarray) -> np.ndarray:
+    """raw * 10**shift rounded half-to-even, saturated to u32 (integer arithmetic only)."""
+    v = raw.astype(np.uint64)
+    d = shift.astype(np.int64)
+    out = np.zeros(v.shape, dtype=np.uint64)
+    lim = np.uint64(0xFFFFFFFF)
+    for k in np.unique(d).tolist():
+        m = d == k
+        x = v[m]
+        if k >= 0:
+            p = np.uint64(10 ** k)
+            big = x > lim // p if k else np.zeros(x.shape, bool)
+            out[m] = np.where(big, lim, np.minimum(x * p, lim))
+        else:
+            p = np.uint64(10 ** (-k))
+            q, r = x // p, x % p
+            half = p // np.uint64(2)
+            up = (r > half) | ((r == half) & ((q & np.uint64(1)) == np.uint64(1)))
+            out[m] = np.minimum(q + up.astype(np.uint64), lim)
+    return out.astype(np.uint32)
+
+
+_SHIFT = None
+
+
+def _milli_values(events: np.ndarray) -> np.ndarray:
+    """Raw record values -> u32 thousandths of the signal's output unit (milli_int rule)."""
+    global _SHIFT
+    if _SHIFT is None:
+        _SHIFT = milli_shift_table()
     st = events["signal_type"].astype(np.int64)
-    milli = np.rint(events["value"].astype(np.float64) * scale[st] * 1000.0)
-    return np.clip(milli, 0, 0xFFFFFFFF).astype(np.uint32)
+    shift = np.where(st < 256, _SHIFT[np.minimum(st, 255)], np.int8(3))
+    return milli_int(events["value"], shift)
 
 
 def _conn_keys(events: np.ndarray) -> np.ndarray:
@@ -395,7 +436,7 @@ def native_encoder():
     """The native WireEncoder (runtime/csrc/wire.h) configured with the signal catalogue."""
     from ..runtime import load
 
-    return load().WireEncoder(signal_scale_table())
+    return load().WireEncoder(milli_shift_table())
 
 
 def string_hash64(s: str) -> int:

@@ -161,27 +161,42 @@ class WireStager:
     previous reader) has completed, so encoding window k+1 overlaps the GPU work of window k.
 
     ``wire=64`` ships the ring records unchanged: ``events``/``spans`` must then already sit in
-    pinned memory (the probe ring is pinned), and staging only fills the counts and labels."""
+    pinned memory (the probe ring is pinned), and staging only fills the counts and labels.
+
+    ``wire=32`` is the probes' own compact record (EVENT32 = probes/ebpf/mislo_record.h
+    ``mislo_event32``: the kernel interns connections and converts values to fixed point), so
+    events also DMA straight from the pinned ring; the host maps the window's spans onto the
+    same connection ids (``self.enc`` mirrors the kernel's connection map; ``conn_encoder``
+    writes the ring's records, see ``probe_records32``) and the pod table travels when it
+    changes."""
 
     def __init__(self, torch, pipe: "WindowPipeline", sig_cap: int, span_cap: int, group_cap: int, wire: int = 16,
                  threads: int = 8):
-        if wire not in (16, 20, 64):
-            raise ValueError("WireStager: wire must be 16, 20 or 64")
+        if wire not in (16, 20, 32, 64):
+            raise ValueError("WireStager: wire must be 16, 20, 32 or 64")
         self.torch, self.pipe, self.wire, self.threads = torch, pipe, wire, max(1, int(threads))
         self.group_cap = group_cap
         pin = lambda n, dt=torch.uint8: torch.empty(n, dtype=dt).pin_memory()  # noqa: E731
         self.enc = records.native_encoder() if wire != 64 else None
-        self.ev = [pin(max(sig_cap, 1) * wire) for _ in range(2)] if wire != 64 else None
+        self.ev = [pin(max(sig_cap, 1) * wire) for _ in range(2)] if wire in (16, 20) else None
         self.sp = [pin(max(span_cap, 1) * 64) for _ in range(2)] if wire != 64 else None
         self.counts = [pin(8, torch.int32) for _ in range(2)]
         self.labels = [pin(group_cap, torch.int32) for _ in range(2)]
-        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire != 64 else None
+        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire in (16, 20) else None
         self.n_ctx = 1
         self.k = 0
         self.encode_s = 0.0
 
+    def probe_records32(self, events: np.ndarray):
+        """EVENT32 records for 64-byte ``events`` as the probes emit them (kernel-side connection
+        interning, integer fixed point), written into pinned memory: a replayed ring."""
+        out = self.torch.empty(max(events.shape[0], 1) * 32, dtype=self.torch.uint8).pin_memory()
+        self.enc.encode(np.ascontiguousarray(events), out.numpy(), 32)
+        return out
+
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
-              group_domains=None, n_local: Optional[int] = None, ev_pinned=None, sp_pinned=None) -> StagedWindow:
+              group_domains=None, n_local: Optional[int] = None, ev_pinned=None, sp_pinned=None,
+              pod_table: Optional[np.ndarray] = None) -> StagedWindow:
         torch = self.torch
         slot = self.k % 2
         if self.k >= 2:  # slot's previous reader: the H2D of window k - 2
@@ -193,6 +208,13 @@ class WireStager:
             ev, sp = ev_pinned, sp_pinned
             if ev is None or sp is None:
                 raise ValueError("wire 64 stages the pinned ring records: pass ev_pinned / sp_pinned")
+        elif self.wire == 32:
+            ev, sp = ev_pinned, self.sp[slot]
+            if ev is None or pod_table is None:
+                raise ValueError("wire 32 stages the pinned EVENT32 ring: pass ev_pinned and pod_table")
+            if n_sp * 64 > sp.numel():
+                raise ValueError("window exceeds the stager's capacity")
+            self.enc.encode_spans(spans, sp.numpy(), False)
         else:
             ev, sp = self.ev[slot], self.sp[slot]
             if n_ev * self.wire > ev.numel() or n_sp * 64 > sp.numel():
@@ -220,9 +242,10 @@ class WireStager:
         self.k += 1
         dt = time.perf_counter() - t0
         self.encode_s += dt
+        ctx = self.ctx is not None
         return StagedWindow(ev, sp, self.counts[slot], self.labels[slot], n_ev, n_sp, n_groups,
-                            list(group_domains or []), self.wire, None, self.ctx if self.wire != 64 else None,
-                            self.n_ctx if self.wire != 64 else 0, dt)
+                            list(group_domains or []), self.wire, pod_table if self.wire == 32 else None,
+                            self.ctx if ctx else None, self.n_ctx if ctx else 0, dt)
 
 
 class WindowPipeline:

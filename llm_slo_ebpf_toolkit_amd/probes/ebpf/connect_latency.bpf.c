@@ -44,7 +44,7 @@ static __always_inline int on_exit(int ret)
 			e->dst_port = dport;
 			e->dst_ip = daddr;
 			e->err = ret < 0 ? -ret : 0;
-			bpf_ringbuf_submit(e, 0);
+			mislo_submit(e);
 		}
 	}
 	if (ret < 0 && ret != -115 /* EINPROGRESS: non-blocking connect in flight */) {
@@ -54,7 +54,7 @@ static __always_inline int on_exit(int ret)
 			e->dst_port = dport;
 			e->dst_ip = daddr;
 			e->err = -ret;
-			bpf_ringbuf_submit(e, 0);
+			mislo_submit(e);
 		}
 	}
 	return 0;

@@ -46,6 +46,6 @@ int rq_complete(struct trace_event_raw_block_rq_completion *ctx)
 		return 0;
 	struct mislo_event *e = mislo_reserve(MISLO_DISK_IO_LATENCY, dt, pt >> 32, (__u32)pt);
 	if (e)
-		bpf_ringbuf_submit(e, 0);
+		mislo_submit(e);
 	return 0;
 }

@@ -53,7 +53,7 @@ int BPF_KRETPROBE(dns_recv_ret, int ret)
 			e->src_port = q->sport;
 			e->dst_port = q->dport;
 			e->dst_ip = q->daddr;
-			bpf_ringbuf_submit(e, 0);
+			mislo_submit(e);
 		}
 	}
 	bpf_map_delete_elem(&dns_inflight, &key);

@@ -48,7 +48,7 @@ int run_job(struct trace_event_raw_drm_sched_job *ctx)
 	struct mislo_event *e = mislo_reserve(MISLO_GPU_QUEUE_DELAY, dt, pt >> 32, (__u32)pt);
 	if (e) {
 		e->flags = MISLO_FLAG_HAS_GPU;
-		bpf_ringbuf_submit(e, 0);
+		mislo_submit(e);
 	}
 	return 0;
 }
@@ -73,7 +73,7 @@ static __always_inline int coll_exit(void)
 	struct mislo_event *e = mislo_reserve(MISLO_RCCL_COLLECTIVE, dt, pt >> 32, (__u32)pt);
 	if (e) {
 		e->flags = MISLO_FLAG_HAS_GPU;
-		bpf_ringbuf_submit(e, 0);
+		mislo_submit(e);
 	}
 	return 0;
 }

@@ -1,14 +1,19 @@
 /* Common BPF-side plumbing for the agent's probes.
  *
- * Every probe object shares three maps, pinned by name under /sys/fs/bpf so the agent's
+ * Every probe object shares these maps, pinned by name under /sys/fs/bpf so the agent's
  * loader opens them once:
- *   mislo_events  BPF ring buffer the agent drains into the GPU window ring (16 MiB);
+ *   mislo_events  BPF ring buffer of 32-byte mislo_event32 records that the agent drains into
+ *                 the GPU window ring (16 MiB);
  *   mislo_cfg     array: [0] realtime - monotonic offset (ns), [1] node id,
  *                 [2 + type] per-signal emit floor (raw units; the overhead guard raises
- *                 floors before it detaches probes);
- *   mislo_pods    cgroup id -> pod id (agent-populated from the kubelet / CRI).
- * Records are stamped with wall-clock ns in the kernel, so the consumer copies ring bytes
- * straight into pinned memory without touching individual records.
+ *                 floors before it detaches probes), [127] connection id counter;
+ *   mislo_pods    cgroup id -> pod id (agent-populated from the kubelet / CRI);
+ *   mislo_conns   connection key -> 24-bit connection id, assigned here on first sight; the
+ *                 agent reads it (batch lookup, per window) to put spans on the same ids;
+ *   mislo_scratch per-CPU 64-byte mislo_event the probe fills before mislo_submit() packs it.
+ * Records are stamped with wall-clock ns, their connections interned and their values
+ * converted to fixed point in the kernel, so the consumer copies ring bytes straight into
+ * pinned memory and DMAs them to the GPU without touching individual records.
  */
 #ifndef MISLO_PROBE_H
 #define MISLO_PROBE_H
@@ -25,6 +30,8 @@
 #define MISLO_CFG_NODE 1
 #define MISLO_CFG_FLOOR(t) (2 + (t))
 #define MISLO_CFG_SLOTS 128
+#define MISLO_CFG_CONN_NEXT 127
+#define MISLO_CONN_ID_LIMIT (1u << 24)
 
 struct {
 	__uint(type, BPF_MAP_TYPE_RINGBUF);
@@ -48,6 +55,21 @@ struct {
 	__uint(pinning, LIBBPF_PIN_BY_NAME);
 } mislo_pods SEC(".maps");
 
+struct {
+	__uint(type, BPF_MAP_TYPE_HASH);
+	__uint(max_entries, 1 << 20);
+	__type(key, __u64);   /* connection key (records.py conn keys) */
+	__type(value, __u32); /* connection id, 1 .. 2^24 - 1 */
+	__uint(pinning, LIBBPF_PIN_BY_NAME);
+} mislo_conns SEC(".maps");
+
+struct {
+	__uint(type, BPF_MAP_TYPE_PERCPU_ARRAY);
+	__uint(max_entries, 1);
+	__type(key, __u32);
+	__type(value, struct mislo_event);
+} mislo_scratch SEC(".maps");
+
 static __always_inline __u64 mislo_cfg_get(__u32 idx)
 {
 	__u64 *v = bpf_map_lookup_elem(&mislo_cfg, &idx);
@@ -60,9 +82,11 @@ static __always_inline int mislo_below_floor(__u16 type, __u64 value)
 	return value < mislo_cfg_get(MISLO_CFG_FLOOR(type));
 }
 
+/* The probe's working record (per-CPU scratch, not ring memory): fill, then mislo_submit(). */
 static __always_inline struct mislo_event *mislo_reserve(__u16 type, __u64 value, __u32 tgid, __u32 tid)
 {
-	struct mislo_event *e = bpf_ringbuf_reserve(&mislo_events, sizeof(*e), 0);
+	__u32 zero = 0;
+	struct mislo_event *e = bpf_map_lookup_elem(&mislo_scratch, &zero);
 	if (!e)
 		return 0;
 	__u64 cg = bpf_get_current_cgroup_id();
@@ -85,6 +109,57 @@ static __always_inline struct mislo_event *mislo_reserve(__u16 type, __u64 value
 	return e;
 }
 
+/* records.py conn_hash_np: splitmix64 of (src port, dst port, dst ip); 0 = no connection */
+static __always_inline __u64 mislo_conn_key(const struct mislo_event *e)
+{
+	if (e->conn_h)
+		return e->conn_h;
+	if (!e->src_port && !e->dst_port)
+		return 0;
+	__u64 z = (((__u64)e->src_port << 48) | ((__u64)e->dst_port << 32) | e->dst_ip) + 0x9E3779B97F4A7C15ull;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	z ^= z >> 31;
+	return z ? z : 1;
+}
+
+/* Connection key -> id, assigned on first sight from the shared counter. Two CPUs racing on
+ * a new key both draw ids; BPF_NOEXIST lets one win and the other re-reads the winner. An
+ * exhausted id space yields 0 (no connection) until the agent resets the map. */
+static __always_inline __u32 mislo_conn_id(__u64 key)
+{
+	if (!key)
+		return 0;
+	__u32 *id = bpf_map_lookup_elem(&mislo_conns, &key);
+	if (id)
+		return *id;
+	__u32 idx = MISLO_CFG_CONN_NEXT;
+	__u64 *next = bpf_map_lookup_elem(&mislo_cfg, &idx);
+	if (!next)
+		return 0;
+	__u64 fresh = __sync_fetch_and_add(next, 1) + 1;
+	if (fresh >= MISLO_CONN_ID_LIMIT)
+		return 0;
+	__u32 v = (__u32)fresh;
+	if (bpf_map_update_elem(&mislo_conns, &key, &v, BPF_NOEXIST) == 0)
+		return v;
+	id = bpf_map_lookup_elem(&mislo_conns, &key);
+	return id ? *id : 0;
+}
+
+/* Pack the working record into the 32-byte ring record and publish it. */
+static __always_inline void mislo_submit(struct mislo_event *e)
+{
+	struct mislo_event32 r;
+	r.ts_ns = e->ts_ns;
+	r.trace_h = e->trace_h;
+	r.value_milli = mislo_milli(e->signal_type, e->value);
+	r.pid = e->pid;
+	r.pod_id = e->pod_id;
+	r.type_conn = (e->signal_type & 0xFFu) | (mislo_conn_id(mislo_conn_key(e)) << 8);
+	bpf_ringbuf_output(&mislo_events, &r, sizeof(r), 0);
+}
+
 /* Emit a record attributed to the current task. */
 static __always_inline void mislo_emit(__u16 type, __u64 value)
 {
@@ -93,7 +168,7 @@ static __always_inline void mislo_emit(__u16 type, __u64 value)
 	__u64 pt = bpf_get_current_pid_tgid();
 	struct mislo_event *e = mislo_reserve(type, value, pt >> 32, (__u32)pt);
 	if (e)
-		bpf_ringbuf_submit(e, 0);
+		mislo_submit(e);
 }
 
 #endif /* MISLO_PROBE_H */

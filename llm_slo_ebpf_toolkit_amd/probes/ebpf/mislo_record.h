@@ -1,10 +1,21 @@
-/* 64-byte event record shared by every probe, the rocprofiler tool, the native ring and
- * the GPU decode kernel (collector/records.py EVENT, ops/csrc/mislo_common.h Event).
- * Only fixed-width types, so it compiles for the BPF target and for the host layout test. */
+/* Event records shared by the probes, the rocprofiler tool, the native ring and the GPU
+ * decode kernels. Only fixed-width types, so it compiles for the BPF target and for the host
+ * layout test.
+ *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record and
+ *                        the user-space producers' ring record;
+ *   struct mislo_event32 (32 B, records.py EVENT32): what the probes put on the BPF ring. The
+ *                        kernel interns the connection (mislo_probe.h mislo_conn_id) and
+ *                        converts the value to fixed point (mislo_milli), so the agent DMAs
+ *                        ring bytes to the GPU without touching a record: half the PCIe bytes
+ *                        of the 64-byte record. svc / node come from the agent's pod table. */
 #ifndef MISLO_RECORD_H
 #define MISLO_RECORD_H
 
 #include <linux/types.h>
+
+#ifndef __always_inline
+#define __always_inline inline __attribute__((always_inline))
+#endif
 
 enum mislo_signal_type {
 	MISLO_DNS_LATENCY = 1,      /* ns */
@@ -46,5 +57,45 @@ struct mislo_event {
 	__s32 err;
 	__u64 conn_h;      /* 0: derived on the GPU from (ports, ip) */
 };
+
+struct mislo_event32 {
+	__s64 ts_ns;       /* CLOCK_REALTIME ns */
+	__u64 trace_h;     /* trace-id hash (0 = none) */
+	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
+	__u32 pid;         /* tgid */
+	__u32 pod_id;      /* cgroup -> pod id, 0 = unknown */
+	__u32 type_conn;   /* bits 0-7 signal type, bits 8-31 interned connection id (0 = none) */
+};
+
+/* value_milli = raw * 10^shift: the catalogue's decode scales are powers of ten
+ * (signals/catalog.py decode_scale; records.py milli_shift_table is the same table). */
+static __always_inline int mislo_milli_shift(__u16 type)
+{
+	switch (type) {
+	case MISLO_DNS_LATENCY: case MISLO_RUNQUEUE_DELAY: case MISLO_CONNECT_LATENCY:
+	case MISLO_TLS_HANDSHAKE: case MISLO_MEM_RECLAIM: case MISLO_DISK_IO_LATENCY:
+	case MISLO_SYSCALL_LATENCY: case MISLO_CFS_THROTTLE: case MISLO_GPU_QUEUE_DELAY:
+	case MISLO_RCCL_COLLECTIVE:
+		return -3; /* ns -> ms */
+	case MISLO_CPU_STEAL: case MISLO_HBM_PRESSURE: case MISLO_XGMI_LATENCY:
+		return 0;  /* milli-percent -> percent, ns -> us */
+	default:
+		return 3;  /* counts */
+	}
+}
+
+/* records.py milli_int: half-to-even rounding, saturated to u32; integer-only (BPF has no
+ * floating point). */
+static __always_inline __u32 mislo_milli(__u16 type, __u64 v)
+{
+	int d = mislo_milli_shift(type);
+	if (d == 3)
+		return v > 4294967ull ? 0xFFFFFFFFu : (__u32)(v * 1000);
+	if (d == 0)
+		return v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (__u32)v;
+	__u64 q = v / 1000, r = v % 1000;
+	q += (2 * r > 1000) || (2 * r == 1000 && (q & 1));
+	return q > 0xFFFFFFFFull ? 0xFFFFFFFFu : (__u32)q;
+}
 
 #endif /* MISLO_RECORD_H */

@@ -42,6 +42,6 @@ int BPF_PROG(rq_switch, bool preempt, struct task_struct *prev, struct task_stru
 		return 0;
 	struct mislo_event *e = mislo_reserve(MISLO_RUNQUEUE_DELAY, dt, BPF_CORE_READ(next, tgid), tid);
 	if (e)
-		bpf_ringbuf_submit(e, 0);
+		mislo_submit(e);
 	return 0;
 }

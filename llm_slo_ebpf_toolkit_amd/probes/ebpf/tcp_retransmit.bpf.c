@@ -17,6 +17,6 @@ int retransmit(struct trace_event_raw_tcp_event_sk_skb *ctx)
 	e->src_port = ctx->sport;
 	e->dst_port = ctx->dport;
 	__builtin_memcpy(&e->dst_ip, ctx->daddr, 4);
-	bpf_ringbuf_submit(e, 0);
+	mislo_submit(e);
 	return 0;
 }

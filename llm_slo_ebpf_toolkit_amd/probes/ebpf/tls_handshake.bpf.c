@@ -51,7 +51,7 @@ int BPF_KRETPROBE(tls_exit, int ret)
 			struct mislo_event *e = mislo_reserve(MISLO_TLS_HANDSHAKE, dt, pt >> 32, (__u32)pt);
 			if (e) {
 				e->dst_port = 443;
-				bpf_ringbuf_submit(e, 0);
+				mislo_submit(e);
 			}
 		}
 	} else {
@@ -59,7 +59,7 @@ int BPF_KRETPROBE(tls_exit, int ret)
 		if (e) {
 			e->dst_port = 443;
 			e->err = 1;
-			bpf_ringbuf_submit(e, 0);
+			mislo_submit(e);
 		}
 	}
 	return 0;

@@ -149,9 +149,9 @@ class PyReplayer {
 // 64-byte EVENT / SPAN records -> 20- or 16-byte wire records (runtime/csrc/wire.h)
 class PyWireEncoder {
  public:
-  explicit PyWireEncoder(py::array_t<double, py::array::c_style | py::array::forcecast> scale) {
-    if (scale.size() != 256) throw std::invalid_argument("scale must have 256 entries");
-    enc_ = std::make_unique<mislo::WireEncoder>(scale.data());
+  explicit PyWireEncoder(py::array_t<int8_t, py::array::c_style | py::array::forcecast> shift) {
+    if (shift.size() != 256) throw std::invalid_argument("shift must have 256 entries");
+    enc_ = std::make_unique<mislo::WireEncoder>(shift.data());
   }
 
   // events: EVENT records (any contiguous buffer, n*64 bytes); out: writable buffer of
@@ -237,7 +237,7 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def_property_readonly("pushed", &PyReplayer::pushed)
       .def_property_readonly("dropped", &PyReplayer::dropped);
   py::class_<PyWireEncoder>(m, "WireEncoder")
-      .def(py::init<py::array_t<double, py::array::c_style | py::array::forcecast>>(), py::arg("scale"))
+      .def(py::init<py::array_t<int8_t, py::array::c_style | py::array::forcecast>>(), py::arg("shift"))
       .def("encode", &PyWireEncoder::encode, py::arg("events"), py::arg("out"), py::arg("wire") = 20)
       .def("encode_spans", &PyWireEncoder::encode_spans, py::arg("spans"), py::arg("out"),
            py::arg("trace_ids") = false)

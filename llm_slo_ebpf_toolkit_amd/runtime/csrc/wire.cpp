@@ -170,8 +170,11 @@ void CtxMap::clear() {
 
 // ---- WireEncoder --------------------------------------------------------------------------
 
-WireEncoder::WireEncoder(const double* scale256) {
-  for (int t = 0; t < 256; ++t) scale_[t] = scale256[t];
+WireEncoder::WireEncoder(const int8_t* shift256) {
+  for (int t = 0; t < 256; ++t) {
+    if (shift256[t] < -9 || shift256[t] > 9) throw std::invalid_argument("milli shift out of range");
+    shift_[t] = shift256[t];
+  }
   ctx_rows_.push_back({0u, 0u, 0u, 0u});
   ctx_.insert(ctx_hash(0, 0, 0, 0), 0, 0, 0, 0);  // the all-zero context
 }
@@ -207,17 +210,20 @@ uint32_t WireEncoder::ctx_id(uint32_t pod, uint32_t pid, uint64_t ckey, uint32_t
   return id;
 }
 
-// rint(x) clipped to [0, 2^32 - 1]; adding and subtracting 2^52 rounds half-to-even in the
-// default rounding mode for 0 <= x < 2^52 (not folded away without -ffast-math)
-static inline double to_milli(double x) {
-  if (!(x > 0.0)) return 0.0;
-  if (x >= 4294967295.0) return 4294967295.0;
-  const double r = x + 4503599627370496.0;
-  return r - 4503599627370496.0;
-}
-
 int64_t WireEncoder::encode(const EventRec* ev, size_t n, void* out, int wire) {
-  if (wire != 20 && wire != 16) throw std::invalid_argument("wire must be 20 or 16");
+  if (wire == 32) {
+    Event32* o = static_cast<Event32*>(out);
+    for (size_t i = 0; i < n; ++i) {
+      const EventRec& e = ev[i];
+      const uint32_t st = e.signal_type;
+      const uint64_t ck = conn_key(e);
+      const uint32_t cid = ck ? conn_id(ck) : 0;
+      o[i] = Event32{e.ts_ns, e.trace_h, milli_int(e.value, st < 256 ? shift_[st] : 3), e.pid, e.pod_id,
+                     (st & 0xFFu) | (cid << 8)};
+    }
+    return 0;
+  }
+  if (wire != 20 && wire != 16) throw std::invalid_argument("wire must be 32, 20 or 16");
   int64_t t_base = std::numeric_limits<int64_t>::max(), t_max = std::numeric_limits<int64_t>::min();
   for (size_t i = 0; i < n; ++i) {
     const int64_t t = ev[i].ts_ns;
@@ -234,21 +240,16 @@ int64_t WireEncoder::encode(const EventRec* ev, size_t n, void* out, int wire) {
     const EventRec& e = ev[i];
     const uint32_t ts_off = e.ts_ns == 0 ? kWireTsZero : (uint32_t)(e.ts_ns - t_base);
     const uint32_t st = e.signal_type;
-    const double sc = st < 256 ? scale_[st] : 1.0;
-    // records.py _milli_values: rint(value * scale * 1000) clipped to u32 (no FMA:
-    // -ffp-contract=off). Adding and subtracting 2^52 rounds half-to-even in the default
-    // rounding mode for 0 <= x < 2^52 without a libm call.
-    const double x = (double)e.value * sc * 1000.0;
-    const double milli = to_milli(x);
+    const uint32_t milli = milli_int(e.value, st < 256 ? shift_[st] : 3);
     const uint64_t ck = conn_key(e);
     if (ck) conn_id(ck);  // ids in event order (the context row refers to it)
     const uint32_t sn = ((uint32_t)e.svc_id << 16) | e.node_id;
     const uint32_t ctx = ctx_id(e.pod_id, e.pid, ck, sn);
     const uint32_t ct = (st & 0xFFu) | (ctx << 8);
     if (wire == 20) {
-      o20[i] = Wire20{ts_off, ct, (uint32_t)milli, (uint32_t)e.trace_h, (uint32_t)(e.trace_h >> 32)};
+      o20[i] = Wire20{ts_off, ct, milli, (uint32_t)e.trace_h, (uint32_t)(e.trace_h >> 32)};
     } else {
-      o16[i] = Wire16{ts_off, ct, (uint32_t)milli, traces_.id(e.trace_h, gen_)};
+      o16[i] = Wire16{ts_off, ct, milli, traces_.id(e.trace_h, gen_)};
     }
   }
   return t_base;
@@ -372,7 +373,7 @@ void WireEncoder::encode_chunk(const EventRec* ev, size_t lo, size_t hi, int64_t
       ts_off = (uint32_t)(uint64_t)(t - base);  // rebased in phase 3 if base is not the minimum
     }
     const uint32_t st = e.signal_type;
-    const double milli = to_milli((double)e.value * (st < 256 ? scale_[st] : 1.0) * 1000.0);
+    const uint32_t milli = milli_int(e.value, st < 256 ? shift_[st] : 3);
     const uint64_t ck = conn_key(e);
     const uint64_t ppid = (uint64_t)e.pod_id << 32 | e.pid;
     const uint32_t sn = ((uint32_t)e.svc_id << 16) | e.node_id;
@@ -399,7 +400,7 @@ void WireEncoder::encode_chunk(const EventRec* ev, size_t lo, size_t hi, int64_t
     fixbits |= last_ctx_fix;
     const uint32_t ct = (st & 0xFFu) | (last_ctx << 8);
     if (wire == 20) {
-      o20[i] = Wire20{ts_off, ct, (uint32_t)milli, (uint32_t)e.trace_h, (uint32_t)(e.trace_h >> 32)};
+      o20[i] = Wire20{ts_off, ct, milli, (uint32_t)e.trace_h, (uint32_t)(e.trace_h >> 32)};
     } else {
       const uint64_t tr = e.trace_h;
       if (tr != last_tr || i == lo) {
@@ -412,7 +413,7 @@ void WireEncoder::encode_chunk(const EventRec* ev, size_t lo, size_t hi, int64_t
         last_tr = tr;
       }
       fixbits |= last_tr_fix;
-      o16[i] = Wire16{ts_off, ct, (uint32_t)milli, last_tid};
+      o16[i] = Wire16{ts_off, ct, milli, last_tid};
     }
     if (fixbits) cs.fix.push_back((uint64_t)i << 2 | fixbits);
   }

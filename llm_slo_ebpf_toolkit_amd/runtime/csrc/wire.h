@@ -63,7 +63,33 @@ struct Wire20 {
 struct Wire16 {
   uint32_t ts_off, ctx_type, value_milli, trace_id;
 };
-static_assert(sizeof(Wire20) == 20 && sizeof(Wire16) == 16, "wire record sizes");
+struct Event32 {  // collector/records.py EVENT32 = probes/ebpf/mislo_record.h mislo_event32
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli, pid, pod_id, type_conn;
+};
+static_assert(sizeof(Wire20) == 20 && sizeof(Wire16) == 16 && sizeof(Event32) == 32, "wire record sizes");
+
+// records.py milli_int: v * 10^d rounded half-to-even, saturated to u32 (integer-only, the
+// same rule the BPF probes apply in the kernel)
+inline uint32_t milli_int(uint64_t v, int d) {
+  static constexpr uint64_t kP10[10] = {1ull,      10ull,      100ull,      1000ull,      10000ull,
+                                        100000ull, 1000000ull, 10000000ull, 100000000ull, 1000000000ull};
+  constexpr uint64_t kLim = 0xFFFFFFFFull;
+  if (d >= 0) {
+    const uint64_t p = kP10[d];
+    if (v > kLim / p) return (uint32_t)kLim;
+    return (uint32_t)(v * p);
+  }
+  uint64_t q, r, p;
+  if (d == -3) {  // ns -> ms: the common case, constant divisor
+    q = v / 1000, r = v % 1000, p = 1000;
+  } else {
+    p = kP10[-d], q = v / p, r = v % p;
+  }
+  q += (2 * r > p) || (2 * r == p && (q & 1));
+  return q > kLim ? (uint32_t)kLim : (uint32_t)q;
+}
 
 constexpr uint32_t kWireTsZero = 0xFFFFFFFFu;
 
@@ -181,11 +207,13 @@ struct ChunkScratch {
 
 class WireEncoder {
  public:
-  // scale[t]: raw kernel value -> output unit for signal type t < 256 (catalog.decode_scale)
-  explicit WireEncoder(const double* scale256);
+  // shift[t]: value_milli = raw * 10^shift[t] for signal type t < 256 (records.py
+  // milli_shift_table; types >= 256 use 3)
+  explicit WireEncoder(const int8_t* shift256);
 
   // Encodes n events into `out` (wire 20 or 16). Returns t_base (earliest non-zero ts).
-  // Throws std::range_error if the window spans >= 2^32 - 1 ns.
+  // Throws std::range_error if the window spans >= 2^32 - 1 ns. wire 32 writes Event32 (the
+  // record the probes emit: absolute ts, interned connection ids) and returns 0.
   int64_t encode(const EventRec* ev, size_t n, void* out, int wire);
   // Spans keep the 64-byte layout: conn hash -> conn id; with trace_ids, trace -> id.
   void encode_spans(const SpanRec64* in, size_t n, SpanRec64* out, bool trace_ids);
@@ -213,7 +241,7 @@ class WireEncoder {
   void encode_chunk(const EventRec* ev, size_t lo, size_t hi, int64_t base, void* out, int wire, ChunkScratch& cs);
   void spans_chunk(const SpanRec64* sp, size_t lo, size_t hi, SpanRec64* out, bool trace_ids, ChunkScratch& cs);
 
-  double scale_[256];
+  int8_t shift_[256];
   FlatMap conns_{1 << 12};
   size_t n_conns_ = 0;
   CtxMap ctx_{1 << 12};

@@ -162,7 +162,7 @@ def test_sloctl(capsys, http_recorder):
 def test_agent_synthetic_count(tmp_path):
     out = tmp_path / "agent.jsonl"
     assert agent.main(["--count", "3", "--event-kind", "both", "--output", "jsonl", "--output-path", str(out),
-                       "--metrics-bind", "", "--scenario", "dns_latency", "--config",
+                       "--metrics-bind", "", "--scenario", "dns_latency", "--disable-overhead-guard", "--config",
                        os.path.join(ROOT, "config", "toolkit.yaml")]) == 0
     rows = read_jsonl(out)
     slo = [r for r in rows if "sli_name" in r]

@@ -309,3 +309,55 @@ def test_pipeline_wire20_equals_wire32():
     for wire in (20, 16):
         for k in ("confusion", "hist", "status", "dbg", "misc"):
             np.testing.assert_array_equal(sums[wire][k], sums[32][k], err_msg=f"{wire} {k}")
+
+
+@pytest.mark.gpu
+def test_wire_stager_matches_prestaged_windows():
+    """bench.py's per-step staging (WireStager: probe-native EVENT32 ring + span mapping,
+    pooled 16/20-byte encoding, pinned 64-byte ring) reproduces the totals of windows staged
+    up front with stage_window."""
+    import torch
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, WireStager, stage_window
+
+    cfg = ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8, events_per_window=6000,
+                       spans_per_window=300, seed=29)
+    gen = ReplayGenerator(cfg)
+    wins = [gen.next_window() for _ in range(3)]
+    pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
+
+    def totals_prestaged(wire):
+        it, enc = records.ConnInterner(), records.native_encoder()
+        staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 8, w.group_domains, wire=wire,
+                               interner=it, encoder=enc) for w in wins]
+        pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
+        for i in range(7):
+            pipe.submit(staged[i % 3])
+        return pipe.summary()
+
+    def totals_stager(wire):
+        pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
+        st = WireStager(torch, pipe, 8192, 512, 8, wire=wire, threads=4)
+        if wire == 64:
+            ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
+                     torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
+        elif wire == 32:
+            ring = [(st.probe_records32(w.events), None) for w in wins]
+        else:
+            ring = [(None, None)] * 3
+        for i in range(7):
+            w = wins[i % 3]
+            pipe.submit(st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
+                                 ev_pinned=ring[i % 3][0], sp_pinned=ring[i % 3][1], pod_table=pods))
+        return pipe.summary()
+
+    keys = ("confusion", "hist", "status", "dbg", "misc")
+    ref32 = totals_prestaged(32)
+    for wire in (32, 20, 16):
+        got = totals_stager(wire)
+        for k in keys:
+            np.testing.assert_array_equal(got[k], ref32[k], err_msg=f"stager {wire} {k}")
+    ref64, got64 = totals_prestaged(64), totals_stager(64)
+    for k in keys:
+        np.testing.assert_array_equal(got64[k], ref64[k], err_msg=f"stager 64 {k}")

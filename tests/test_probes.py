@@ -19,6 +19,16 @@ def test_bpf_record_layout_matches_event_dtype(tmp_path):
                    check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
+    # the in-kernel fixed-point rule (mislo_milli) == records.milli_int
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+
+    rows = [tuple(int(x) for x in ln.split()[1:]) for ln in out.stdout.splitlines() if ln.startswith("milli ")]
+    assert len(rows) == 52
+    t, v, m = (np.array(c, dtype=np.uint64) for c in zip(*rows))
+    shift = records.milli_shift_table()[t.astype(np.int64)]
+    np.testing.assert_array_equal(records.milli_int(v, shift), m.astype(np.uint32))
 
 
 def test_record_enum_matches_catalogue():

@@ -182,3 +182,49 @@ def test_pooled_encode_window_is_byte_identical_to_sequential():
     with pytest.raises(ValueError):
         par.encode_window(ev, np.zeros(ev.shape[0] * 16, np.uint8), 16, sp, np.zeros_like(sp), 4, 256)
     assert par.n_ctx == n0
+
+
+def test_integer_milli_rule():
+    """records.milli_int (and the probes' in-kernel mislo_milli): half-to-even, saturating;
+    equal to the float rule rint(v * scale * 1000) away from exact halves."""
+    shift = records.milli_shift_table()
+    assert shift[1] == -3 and shift[2] == 3 and shift[6] == 0 and shift[200] == 3
+    v = np.array([0, 499, 500, 501, 1500, 2500, 2501, 10 ** 15, 7], dtype=np.uint64)
+    np.testing.assert_array_equal(records.milli_int(v, np.full(v.shape, -3)),
+                                  [0, 0, 0, 1, 2, 2, 3, 10 ** 12 if 10 ** 12 < 2 ** 32 else 2 ** 32 - 1, 0])
+    np.testing.assert_array_equal(records.milli_int(v[:4], np.full(4, 3)), [0, 499000, 500000, 501000])
+    np.testing.assert_array_equal(records.milli_int(np.array([2 ** 40], np.uint64), np.array([0])), [2 ** 32 - 1])
+    rng = np.random.default_rng(0)
+    raw = rng.integers(0, 5 * 10 ** 9, 20000, dtype=np.uint64)
+    raw = raw[raw % 1000 != 500]
+    np.testing.assert_array_equal(records.milli_int(raw, np.full(raw.shape, -3)),
+                                  np.clip(np.rint(raw.astype(np.float64) * 1e-6 * 1000.0), 0, 2 ** 32 - 1))
+
+
+def test_native_event32_matches_numpy_compact():
+    """Native EVENT32 (what the probes emit; bench --wire 32) == records.to_compact up to
+    connection id numbering; spans mapped by the same encoder share the ids."""
+    pytest = __import__("pytest")
+    try:
+        enc = records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    win = _win(seed=9)
+    ev = win.events
+    buf = np.zeros(ev.shape[0] * 32, np.uint8)
+    assert enc.encode(ev, buf, 32) == 0
+    n32 = buf.view(records.EVENT32)
+    r32 = records.to_compact(ev, records.ConnInterner())
+    for f in ("ts_ns", "trace_h", "value_milli", "pid", "pod_id"):
+        np.testing.assert_array_equal(n32[f], r32[f], err_msg=f)
+    np.testing.assert_array_equal(n32["type_conn"] & 0xFF, r32["type_conn"] & 0xFF)
+    a, b = (n32["type_conn"] >> 8).tolist(), (r32["type_conn"] >> 8).tolist()
+    assert len(set(zip(a, b))) == len(set(a)) == len(set(b))
+    assert (np.array(a) == 0).tolist() == (np.array(b) == 0).tolist()
+    sp = np.zeros_like(win.spans)
+    enc.encode_spans(win.spans, sp, False)
+    ev_ids = dict(zip(records._conn_keys(ev).tolist(), a))
+    for h, cid in zip(win.spans["conn_h"].tolist(), sp["conn_h"].tolist()):
+        if h in ev_ids:
+            assert cid == ev_ids[h]
+    np.testing.assert_array_equal(sp["trace_h"], win.spans["trace_h"])
