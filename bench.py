@@ -5,7 +5,7 @@ Metric (BASELINE.json): "attribution macro-F1 on fault-replay confusion matrix; 
 overhead %", reported on config 5 ("full 9 CPU + 4 GPU signals, safety governor <= 3 %
 overhead, full confusion matrix across all fault domains") plus the events/s scaling
 curve the north star asks for. One step = one 1-second collection window per GPU, from
-the records the probes wrote into the agent's pinned ring (32-byte EVENT32 by default) ->
+the records the probes wrote into the agent's pinned ring (24-byte EVENT24 by default) ->
 host work (spans mapped onto the kernel's connection ids; with --wire 16/20, wire encoding
 of 64-byte records on a native worker pool) -> H2D -> decode + histograms -> LDS hash join
 -> MFMA posteriors + confusion -> MFMA sufficient statistics -> RCCL all-reduce of the
@@ -53,13 +53,13 @@ def parse():
                     help="windows the host may run ahead of the GPU (host back-pressure)")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", type=int, default=32, choices=(16, 20, 32, 64),
-                    help="event record bytes on PCIe. 32 (default) / 64: the probes' 32-byte EVENT32 "
-                         "(kernel-interned connections, fixed-point values) / 64-byte EVENT records, DMA'd "
-                         "from the pinned ring as-is (no per-event host work; spans are mapped onto the "
-                         "connection ids for 32); 16 = EVENT16 / 20 = EVENT20, encoded from 64-byte records "
-                         "on the host inside every step (interned contexts and trace ids; the encoder reads "
-                         "the same 64 B per event the DMA would)")
+    ap.add_argument("--wire", type=int, default=24, choices=(16, 20, 24, 32, 64),
+                    help="event record bytes on PCIe. 24 (default) / 32 / 64: the probes' ring records "
+                         "(EVENT24: kernel-interned contexts; EVENT32: kernel-interned connections; EVENT: "
+                         "64 bytes), DMA'd from the pinned ring as-is (no per-event host work; spans are "
+                         "mapped onto the kernel's connection ids for 24/32); 16 = EVENT16 / 20 = EVENT20, "
+                         "encoded from 64-byte records on the host inside every step (interned contexts and "
+                         "trace ids; the encoder reads the same 64 B per event the DMA would)")
     ap.add_argument("--encode-threads", type=int, default=0,
                     help="host encoder worker threads (0 = OMP_NUM_THREADS, else 8; at most 16)")
     ap.add_argument("--out", default="")
@@ -122,8 +122,8 @@ def main() -> int:
     if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
         ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
                  torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-    elif a.wire == 32:  # the probes' own 32-byte records (kernel-interned connections)
-        ring = [(stager.probe_records32(w.events), None) for w in wins]
+    elif a.wire in (24, 32):  # the probes' own 24/32-byte records (kernel-interned contexts / connections)
+        ring = [(stager.probe_records(w.events), None) for w in wins]
         # pod id -> svc|node: agent metadata (kubelet / CRI), static over the run
         pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")

@@ -74,7 +74,17 @@ EVENT16 = np.dtype([
     ("trace_id", "<u4"),     # 12 interned trace id, 0 = none
 ])
 assert EVENT16.itemsize == 16
-WIRE_DTYPES = {64: EVENT, 32: EVENT32, 20: EVENT20, 16: EVENT16}
+# 24-byte record (= probes/ebpf/mislo_record.h mislo_event24): what the probes put on the
+# ring when the kernel interns the workload context too: absolute timestamp (no window base
+# at the source), trace hash, fixed-point value, context id into the device context table.
+EVENT24 = np.dtype([
+    ("ts_ns", "<i8"),        # 0
+    ("trace_h", "<u8"),      # 8
+    ("value_milli", "<u4"),  # 16
+    ("ctx_type", "<u4"),     # 20 bits 0-7 signal type, 8-31 context id
+])
+assert EVENT24.itemsize == 24
+WIRE_DTYPES = {64: EVENT, 32: EVENT32, 24: EVENT24, 20: EVENT20, 16: EVENT16}
 
 SPAN = np.dtype([
     ("ts_ns", "<i8"),        # 0
@@ -327,6 +337,21 @@ def to_wire20(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner"):
     st = events["signal_type"].astype(np.uint32)
     out["ctx_type"] = (st & np.uint32(0xFF)) | (ctx << np.uint32(8))
     return out, t_base
+
+
+def to_wire24(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner") -> np.ndarray:
+    """EVENT (64 B) -> EVENT24 (24 B), the probes' context-interned ring record: absolute
+    timestamps, trace hash, fixed-point value, interned (pod, pid, conn, svc|node) context."""
+    out = np.zeros(events.shape[0], dtype=EVENT24)
+    out["ts_ns"] = events["ts_ns"]
+    out["trace_h"] = events["trace_h"]
+    out["value_milli"] = _milli_values(events)
+    cid = conns.ids(_conn_keys(events))
+    sn = (events["svc_id"].astype(np.uint32) << np.uint32(16)) | events["node_id"].astype(np.uint32)
+    ctx = ctxs.ids(events["pod_id"], events["pid"], cid, sn)
+    st = events["signal_type"].astype(np.uint32)
+    out["ctx_type"] = (st & np.uint32(0xFF)) | (ctx << np.uint32(8))
+    return out
 
 
 def compact_spans(spans: np.ndarray, interner: "ConnInterner") -> np.ndarray:

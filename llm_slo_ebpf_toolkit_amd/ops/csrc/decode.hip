@@ -195,9 +195,15 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
 // (counts[6] valid rows).
 __device__ __forceinline__ uint64_t wire_trace(const EventC20& e) { return ((uint64_t)e.tr_hi << 32) | e.tr_lo; }
 __device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)e.trace_id; }
+__device__ __forceinline__ uint64_t wire_trace(const EventC24& e) { return e.trace_h; }
+template <class Rec>
+__device__ __forceinline__ int64_t wire_ts(const Rec& e, int64_t t_base) {
+  return e.ts_off == kTsZero ? 0 : t_base + (int64_t)e.ts_off;
+}
+__device__ __forceinline__ int64_t wire_ts(const EventC24& e, int64_t) { return e.ts_ns; }
 
-// Rec = EventC20 (20-byte) or EventC16 (16-byte, interned trace ids): identical decoding
-// otherwise.
+// Rec = EventC20 (20-byte), EventC16 (16-byte, interned trace ids) or EventC24 (24-byte,
+// absolute timestamps: the probes' context-interned ring record): identical decoding otherwise.
 template <int NT, class Rec>
 __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, const int* __restrict__ n_ptr,
                                                     int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
     const float val = (float)((double)e.value_milli * 1e-3);
     const uint32_t cid = e.ctx_type >> 8;
     const uint4 cx = cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
-    const int64_t ts = e.ts_off == kTsZero ? 0 : t_base + (int64_t)e.ts_off;
+    const int64_t ts = wire_ts(e, t_base);
     const uint64_t tr = wire_trace(e);
     decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, s_hist, s_status, s_part, s_sum,
                unsupported, zero_ts, i < n_local);
@@ -370,6 +376,9 @@ void launch_decode_wire(const void* ev, int wire, const int* n_dev, int cap, con
   if (wire == 16)
     hipLaunchKernelGGL((k_decode_wire<NT, EventC16>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                        (const EventC16*)ev, n_dev, cap, tab, n_ctx, o);
+  else if (wire == 24)
+    hipLaunchKernelGGL((k_decode_wire<NT, EventC24>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                       (const EventC24*)ev, n_dev, cap, tab, n_ctx, o);
   else
     hipLaunchKernelGGL((k_decode_wire<NT, EventC20>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                        (const EventC20*)ev, n_dev, cap, tab, n_ctx, o);

@@ -66,6 +66,16 @@ struct alignas(16) EventC16 {
 };
 static_assert(sizeof(EventC16) == 16, "EventC16 must be 16 bytes");
 constexpr uint32_t kTsZero = 0xFFFFFFFFu;
+// 24-byte record (EVENT24 = probes/ebpf/mislo_record.h mislo_event24): what the probes put
+// on the ring when they also intern the workload context in the kernel; absolute timestamp
+// (no window base needed at the source), context id into the device context table.
+struct alignas(8) EventC24 {
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli;
+  uint32_t ctx_type;  // bits 0-7 signal type, bits 8-31 context id
+};
+static_assert(sizeof(EventC24) == 24, "EventC24 must be 24 bytes");
 
 // REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).
 struct __attribute__((packed)) RefEvent {

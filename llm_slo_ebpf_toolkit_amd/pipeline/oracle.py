@@ -84,9 +84,14 @@ def decode_compact(ev: np.ndarray, pod_svcnode: np.ndarray) -> Decoded:
                    (tc >> np.uint32(8)).astype(np.uint64))
 
 
+def decode_w24(ev: np.ndarray, ctx_table: np.ndarray) -> Decoded:
+    """k_decode_wire<EventC24>: the probes' context-interned 24-byte records."""
+    return decode_w20(ev, 0, ctx_table)
+
+
 def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
     """k_decode_wire: EVENT20 (trace hash) or EVENT16 (trace id) records with the window
-    base and the context table."""
+    base, or EVENT24 (absolute timestamps, trace hash), and the context table."""
     type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
     for s in catalog.SIGNALS:
         if s.kernel_type < 256:
@@ -104,8 +109,11 @@ def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
     cid = (ct >> np.uint32(8)).astype(np.int64)
     inb = cid < tab.shape[0]
     row = np.where(inb[:, None], tab[np.minimum(cid, tab.shape[0] - 1)], 0).astype(np.uint32)
-    off = ev["ts_off"].astype(np.int64)
-    ts = np.where(off == 0xFFFFFFFF, 0, np.int64(t_base) + off)
+    if "ts_ns" in ev.dtype.names:
+        ts = ev["ts_ns"].astype(np.int64)
+    else:
+        off = ev["ts_off"].astype(np.int64)
+        ts = np.where(off == 0xFFFFFFFF, 0, np.int64(t_base) + off)
     trace = ev["trace_id"] if "trace_id" in ev.dtype.names else ev["trace_h"]
     return Decoded(ts, val, slot, status, row[:, 0], row[:, 1], row[:, 3], trace.astype(np.uint64),
                    row[:, 2].astype(np.uint64))

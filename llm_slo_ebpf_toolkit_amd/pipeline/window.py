@@ -163,17 +163,17 @@ class WireStager:
     ``wire=64`` ships the ring records unchanged: ``events``/``spans`` must then already sit in
     pinned memory (the probe ring is pinned), and staging only fills the counts and labels.
 
-    ``wire=32`` is the probes' own compact record (EVENT32 = probes/ebpf/mislo_record.h
-    ``mislo_event32``: the kernel interns connections and converts values to fixed point), so
-    events also DMA straight from the pinned ring; the host maps the window's spans onto the
-    same connection ids (``self.enc`` mirrors the kernel's connection map; ``conn_encoder``
-    writes the ring's records, see ``probe_records32``) and the pod table travels when it
-    changes."""
+    ``wire=32`` / ``24`` are the probes' own compact records (probes/ebpf/mislo_record.h
+    ``mislo_event32``: the kernel interns connections and converts values to fixed point;
+    ``mislo_event24``: it also interns the (pod, pid, conn, svc|node) context), so events also
+    DMA straight from the pinned ring. The host maps the window's spans onto the same
+    connection ids (``self.enc`` mirrors the kernel's maps; ``probe_records`` writes a replayed
+    ring with it) and ships the pod table (32) or the new context rows (24) when they change."""
 
     def __init__(self, torch, pipe: "WindowPipeline", sig_cap: int, span_cap: int, group_cap: int, wire: int = 16,
                  threads: int = 8):
-        if wire not in (16, 20, 32, 64):
-            raise ValueError("WireStager: wire must be 16, 20, 32 or 64")
+        if wire not in (16, 20, 24, 32, 64):
+            raise ValueError("WireStager: wire must be 16, 20, 24, 32 or 64")
         self.torch, self.pipe, self.wire, self.threads = torch, pipe, wire, max(1, int(threads))
         self.group_cap = group_cap
         pin = lambda n, dt=torch.uint8: torch.empty(n, dtype=dt).pin_memory()  # noqa: E731
@@ -182,16 +182,19 @@ class WireStager:
         self.sp = [pin(max(span_cap, 1) * 64) for _ in range(2)] if wire != 64 else None
         self.counts = [pin(8, torch.int32) for _ in range(2)]
         self.labels = [pin(group_cap, torch.int32) for _ in range(2)]
-        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire in (16, 20) else None
+        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire in (16, 20, 24) else None
         self.n_ctx = 1
         self.k = 0
         self.encode_s = 0.0
 
-    def probe_records32(self, events: np.ndarray):
-        """EVENT32 records for 64-byte ``events`` as the probes emit them (kernel-side connection
-        interning, integer fixed point), written into pinned memory: a replayed ring."""
-        out = self.torch.empty(max(events.shape[0], 1) * 32, dtype=self.torch.uint8).pin_memory()
-        self.enc.encode(np.ascontiguousarray(events), out.numpy(), 32)
+    def probe_records(self, events: np.ndarray):
+        """EVENT32 / EVENT24 records (``self.wire``) for 64-byte ``events`` as the probes emit
+        them (kernel-side connection / context interning, integer fixed point), written into
+        pinned memory: a replayed ring."""
+        if self.wire not in (24, 32):
+            raise ValueError("probe_records: wire 24 or 32")
+        out = self.torch.empty(max(events.shape[0], 1) * self.wire, dtype=self.torch.uint8).pin_memory()
+        self.enc.encode(np.ascontiguousarray(events), out.numpy(), self.wire)
         return out
 
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
@@ -208,10 +211,10 @@ class WireStager:
             ev, sp = ev_pinned, sp_pinned
             if ev is None or sp is None:
                 raise ValueError("wire 64 stages the pinned ring records: pass ev_pinned / sp_pinned")
-        elif self.wire == 32:
+        elif self.wire in (24, 32):
             ev, sp = ev_pinned, self.sp[slot]
-            if ev is None or pod_table is None:
-                raise ValueError("wire 32 stages the pinned EVENT32 ring: pass ev_pinned and pod_table")
+            if ev is None or (self.wire == 32 and pod_table is None):
+                raise ValueError("wire 32/24 stage the pinned probe ring: pass ev_pinned (and pod_table for 32)")
             if n_sp * 64 > sp.numel():
                 raise ValueError("window exceeds the stager's capacity")
             self.enc.encode_spans(spans, sp.numpy(), False)
@@ -221,6 +224,7 @@ class WireStager:
                 raise ValueError("window exceeds the stager's capacity")
             t_base = self.enc.encode_window(events, ev.numpy(), self.wire, spans, sp.numpy(), self.threads)
             self.enc.end_window()
+        if self.ctx is not None:
             n_ctx = int(self.enc.n_ctx)
             if n_ctx > self.n_ctx:  # new context rows (append-only: rows < n_ctx never change)
                 if n_ctx > self.ctx.shape[0]:

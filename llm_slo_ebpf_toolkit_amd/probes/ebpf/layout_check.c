@@ -36,7 +36,13 @@ int main(void)
 	} while (0)
 	CHECK32(ts_ns, 0); CHECK32(trace_h, 8); CHECK32(value_milli, 16); CHECK32(pid, 20);
 	CHECK32(pod_id, 24); CHECK32(type_conn, 28);
-	printf("mislo_event layout ok (64 bytes), mislo_event32 layout ok (32 bytes)\n");
+	if (sizeof(struct mislo_event24) != 24 || offsetof(struct mislo_event24, ts_ns) != 0 ||
+	    offsetof(struct mislo_event24, trace_h) != 8 || offsetof(struct mislo_event24, value_milli) != 16 ||
+	    offsetof(struct mislo_event24, ctx_type) != 20) {
+		printf("bad mislo_event24 layout\n");
+		return 1;
+	}
+	printf("mislo_event layout ok (64 bytes), mislo_event32 ok (32 bytes), mislo_event24 ok (24 bytes)\n");
 	/* fixed-point rule: print "type value milli" lines for the Python side to compare */
 	static const unsigned long long vals[] = {0, 499, 500, 501, 1500, 2500, 2501, 4294967, 4294968,
 						   4294967295ull, 4294967296ull, 4294967295500ull, 4294967296500ull};

@@ -2,14 +2,22 @@
  *
  * Every probe object shares these maps, pinned by name under /sys/fs/bpf so the agent's
  * loader opens them once:
- *   mislo_events  BPF ring buffer of 32-byte mislo_event32 records that the agent drains into
- *                 the GPU window ring (16 MiB);
+ *   mislo_events  BPF ring buffer of 24-byte mislo_event24 records (32-byte mislo_event32
+ *                 with -DMISLO_RING_EVENT32) that the agent drains into the GPU window ring
+ *                 (16 MiB);
  *   mislo_cfg     array: [0] realtime - monotonic offset (ns), [1] node id,
  *                 [2 + type] per-signal emit floor (raw units; the overhead guard raises
- *                 floors before it detaches probes), [127] connection id counter;
+ *                 floors before it detaches probes), [126] context id counter,
+ *                 [127] connection id counter;
  *   mislo_pods    cgroup id -> pod id (agent-populated from the kubelet / CRI);
  *   mislo_conns   connection key -> 24-bit connection id, assigned here on first sight; the
  *                 agent reads it (batch lookup, per window) to put spans on the same ids;
+ *   mislo_ctxs    (pod, pid, connection id) -> 24-bit context id, assigned here on first
+ *                 sight. When counter [126] has moved since the last window, the agent
+ *                 batch-reads the map after snapshotting the ring (every id a snapshotted
+ *                 record carries was inserted before the record was written) and appends
+ *                 the new rows (pod, pid, conn, svc|node from pod metadata) to the device
+ *                 context table before the window's DMA;
  *   mislo_scratch per-CPU 64-byte mislo_event the probe fills before mislo_submit() packs it.
  * Records are stamped with wall-clock ns, their connections interned and their values
  * converted to fixed point in the kernel, so the consumer copies ring bytes straight into
@@ -30,8 +38,13 @@
 #define MISLO_CFG_NODE 1
 #define MISLO_CFG_FLOOR(t) (2 + (t))
 #define MISLO_CFG_SLOTS 128
+#define MISLO_CFG_CTX_NEXT 126
 #define MISLO_CFG_CONN_NEXT 127
 #define MISLO_CONN_ID_LIMIT (1u << 24)
+
+struct mislo_ctx_key {
+	__u32 pod_id, pid, conn_id, pad;
+};
 
 struct {
 	__uint(type, BPF_MAP_TYPE_RINGBUF);
@@ -62,6 +75,14 @@ struct {
 	__type(value, __u32); /* connection id, 1 .. 2^24 - 1 */
 	__uint(pinning, LIBBPF_PIN_BY_NAME);
 } mislo_conns SEC(".maps");
+
+struct {
+	__uint(type, BPF_MAP_TYPE_HASH);
+	__uint(max_entries, 1 << 20);
+	__type(key, struct mislo_ctx_key);
+	__type(value, __u32); /* context id, 1 .. 2^24 - 1 (0 = the all-zero context) */
+	__uint(pinning, LIBBPF_PIN_BY_NAME);
+} mislo_ctxs SEC(".maps");
 
 struct {
 	__uint(type, BPF_MAP_TYPE_PERCPU_ARRAY);
@@ -123,40 +144,67 @@ static __always_inline __u64 mislo_conn_key(const struct mislo_event *e)
 	return z ? z : 1;
 }
 
-/* Connection key -> id, assigned on first sight from the shared counter. Two CPUs racing on
- * a new key both draw ids; BPF_NOEXIST lets one win and the other re-reads the winner. An
- * exhausted id space yields 0 (no connection) until the agent resets the map. */
+/* key -> id from map `m`, assigned on first sight from counter cfg[`ctr`]. Two CPUs racing on
+ * a new key both draw ids; BPF_NOEXIST lets one win and the other re-reads the winner (the
+ * loser's id is never used). An exhausted id space yields 0 until the agent resets the map. */
+#define MISLO_INTERN(m, keyp, ctr)                                                         \
+	({                                                                                  \
+		__u32 _r = 0;                                                               \
+		__u32 *_id = bpf_map_lookup_elem(&(m), (keyp));                             \
+		if (_id) {                                                                  \
+			_r = *_id;                                                          \
+		} else {                                                                    \
+			__u32 _idx = (ctr);                                                 \
+			__u64 *_next = bpf_map_lookup_elem(&mislo_cfg, &_idx);              \
+			if (_next) {                                                        \
+				__u64 _fresh = __sync_fetch_and_add(_next, 1) + 1;          \
+				if (_fresh < MISLO_CONN_ID_LIMIT) {                         \
+					__u32 _v = (__u32)_fresh;                           \
+					if (bpf_map_update_elem(&(m), (keyp), &_v, BPF_NOEXIST) == 0) \
+						_r = _v;                                    \
+					else if ((_id = bpf_map_lookup_elem(&(m), (keyp))))  \
+						_r = *_id;                                  \
+				}                                                           \
+			}                                                                   \
+		}                                                                           \
+		_r;                                                                         \
+	})
+
 static __always_inline __u32 mislo_conn_id(__u64 key)
 {
 	if (!key)
 		return 0;
-	__u32 *id = bpf_map_lookup_elem(&mislo_conns, &key);
-	if (id)
-		return *id;
-	__u32 idx = MISLO_CFG_CONN_NEXT;
-	__u64 *next = bpf_map_lookup_elem(&mislo_cfg, &idx);
-	if (!next)
-		return 0;
-	__u64 fresh = __sync_fetch_and_add(next, 1) + 1;
-	if (fresh >= MISLO_CONN_ID_LIMIT)
-		return 0;
-	__u32 v = (__u32)fresh;
-	if (bpf_map_update_elem(&mislo_conns, &key, &v, BPF_NOEXIST) == 0)
-		return v;
-	id = bpf_map_lookup_elem(&mislo_conns, &key);
-	return id ? *id : 0;
+	return MISLO_INTERN(mislo_conns, &key, MISLO_CFG_CONN_NEXT);
 }
 
-/* Pack the working record into the 32-byte ring record and publish it. */
+/* (pod, pid, connection) -> context id; the all-zero context is id 0 without a map entry */
+static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 conn_id)
+{
+	if (!pod_id && !pid && !conn_id)
+		return 0;
+	struct mislo_ctx_key k = {.pod_id = pod_id, .pid = pid, .conn_id = conn_id, .pad = 0};
+	return MISLO_INTERN(mislo_ctxs, &k, MISLO_CFG_CTX_NEXT);
+}
+
+/* Pack the working record into the ring record and publish it. */
 static __always_inline void mislo_submit(struct mislo_event *e)
 {
+	__u32 cid = mislo_conn_id(mislo_conn_key(e));
+#ifdef MISLO_RING_EVENT32
 	struct mislo_event32 r;
 	r.ts_ns = e->ts_ns;
 	r.trace_h = e->trace_h;
 	r.value_milli = mislo_milli(e->signal_type, e->value);
 	r.pid = e->pid;
 	r.pod_id = e->pod_id;
-	r.type_conn = (e->signal_type & 0xFFu) | (mislo_conn_id(mislo_conn_key(e)) << 8);
+	r.type_conn = (e->signal_type & 0xFFu) | (cid << 8);
+#else
+	struct mislo_event24 r;
+	r.ts_ns = e->ts_ns;
+	r.trace_h = e->trace_h;
+	r.value_milli = mislo_milli(e->signal_type, e->value);
+	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
+#endif
 	bpf_ringbuf_output(&mislo_events, &r, sizeof(r), 0);
 }
 

@@ -3,11 +3,16 @@
  * layout test.
  *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record and
  *                        the user-space producers' ring record;
- *   struct mislo_event32 (32 B, records.py EVENT32): what the probes put on the BPF ring. The
- *                        kernel interns the connection (mislo_probe.h mislo_conn_id) and
- *                        converts the value to fixed point (mislo_milli), so the agent DMAs
- *                        ring bytes to the GPU without touching a record: half the PCIe bytes
- *                        of the 64-byte record. svc / node come from the agent's pod table. */
+ *   struct mislo_event24 (24 B, records.py EVENT24): what the probes put on the BPF ring
+ *                        (default). The kernel converts the value to fixed point
+ *                        (mislo_milli) and interns the connection and the (pod, pid, conn)
+ *                        context (mislo_probe.h mislo_conn_id / mislo_ctx_id), so the agent
+ *                        DMAs ring bytes to the GPU without touching a record: 3/8 of the PCIe
+ *                        bytes of the 64-byte record. The agent turns new context ids into
+ *                        device context-table rows (adding svc / node from pod metadata);
+ *   struct mislo_event32 (32 B, records.py EVENT32): the ring record with -DMISLO_RING_EVENT32
+ *                        (connections interned, pod and pid inline; svc / node from the
+ *                        agent's pod table). */
 #ifndef MISLO_RECORD_H
 #define MISLO_RECORD_H
 
@@ -65,6 +70,13 @@ struct mislo_event32 {
 	__u32 pid;         /* tgid */
 	__u32 pod_id;      /* cgroup -> pod id, 0 = unknown */
 	__u32 type_conn;   /* bits 0-7 signal type, bits 8-31 interned connection id (0 = none) */
+};
+
+struct mislo_event24 {
+	__s64 ts_ns;       /* CLOCK_REALTIME ns */
+	__u64 trace_h;     /* trace-id hash (0 = none) */
+	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
+	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
 };
 
 /* value_milli = raw * 10^shift: the catalogue's decode scales are powers of ten

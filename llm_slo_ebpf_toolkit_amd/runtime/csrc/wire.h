@@ -63,6 +63,13 @@ struct Wire20 {
 struct Wire16 {
   uint32_t ts_off, ctx_type, value_milli, trace_id;
 };
+struct Event24 {  // collector/records.py EVENT24 = probes/ebpf/mislo_record.h mislo_event24
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli, ctx_type;
+};
+static_assert(sizeof(Event24) == 24, "Event24 is 24 bytes");
+
 struct Event32 {  // collector/records.py EVENT32 = probes/ebpf/mislo_record.h mislo_event32
   int64_t ts_ns;
   uint64_t trace_h;
@@ -212,8 +219,9 @@ class WireEncoder {
   explicit WireEncoder(const int8_t* shift256);
 
   // Encodes n events into `out` (wire 20 or 16). Returns t_base (earliest non-zero ts).
-  // Throws std::range_error if the window spans >= 2^32 - 1 ns. wire 32 writes Event32 (the
-  // record the probes emit: absolute ts, interned connection ids) and returns 0.
+  // Throws std::range_error if the window spans >= 2^32 - 1 ns. wire 32 / 24 write Event32 /
+  // Event24 (the records the probes emit: absolute ts; interned connection / context ids) and
+  // return 0.
   int64_t encode(const EventRec* ev, size_t n, void* out, int wire);
   // Spans keep the 64-byte layout: conn hash -> conn id; with trace_ids, trace -> id.
   void encode_spans(const SpanRec64* in, size_t n, SpanRec64* out, bool trace_ids);

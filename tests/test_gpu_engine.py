@@ -313,7 +313,7 @@ def test_pipeline_wire20_equals_wire32():
 
 @pytest.mark.gpu
 def test_wire_stager_matches_prestaged_windows():
-    """bench.py's per-step staging (WireStager: probe-native EVENT32 ring + span mapping,
+    """bench.py's per-step staging (WireStager: probe-native EVENT32 / EVENT24 rings + span mapping,
     pooled 16/20-byte encoding, pinned 64-byte ring) reproduces the totals of windows staged
     up front with stage_window."""
     import torch
@@ -342,8 +342,8 @@ def test_wire_stager_matches_prestaged_windows():
         if wire == 64:
             ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
                      torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-        elif wire == 32:
-            ring = [(st.probe_records32(w.events), None) for w in wins]
+        elif wire in (24, 32):
+            ring = [(st.probe_records(w.events), None) for w in wins]
         else:
             ring = [(None, None)] * 3
         for i in range(7):
@@ -354,7 +354,7 @@ def test_wire_stager_matches_prestaged_windows():
 
     keys = ("confusion", "hist", "status", "dbg", "misc")
     ref32 = totals_prestaged(32)
-    for wire in (32, 20, 16):
+    for wire in (32, 24, 20, 16):
         got = totals_stager(wire)
         for k in keys:
             np.testing.assert_array_equal(got[k], ref32[k], err_msg=f"stager {wire} {k}")

@@ -228,3 +228,33 @@ def test_native_event32_matches_numpy_compact():
         if h in ev_ids:
             assert cid == ev_ids[h]
     np.testing.assert_array_equal(sp["trace_h"], win.spans["trace_h"])
+
+
+def test_event24_native_numpy_and_join():
+    """EVENT24 (the probes' context-interned ring record): native == records.to_wire24 up to id
+    numbering, and its decode joins exactly like the 64-byte records."""
+    pytest = __import__("pytest")
+    try:
+        enc = records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    win = _win(seed=12)
+    ev = win.events
+    buf = np.zeros(ev.shape[0] * 24, np.uint8)
+    assert enc.encode(ev, buf, 24) == 0
+    n24 = buf.view(records.EVENT24)
+    ctxs = records.CtxInterner()
+    r24 = records.to_wire24(ev, records.ConnInterner(), ctxs)
+    for f in ("ts_ns", "trace_h", "value_milli"):
+        np.testing.assert_array_equal(n24[f], r24[f], err_msg=f)
+    a = oracle.decode_w24(n24, enc.ctx_table())
+    b = oracle.decode_w24(r24, ctxs.table())
+    for f in ("ts", "slot", "pod", "pid", "svcnode", "trace"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    sp = np.zeros_like(win.spans)
+    enc.encode_spans(win.spans, sp, False)
+    full = oracle.join(oracle.decode_events(ev), win.spans, win.n_groups)
+    j24 = oracle.join(a, sp, win.n_groups)
+    np.testing.assert_array_equal(full.top3, j24.top3)
+    np.testing.assert_array_equal(full.cnt, j24.cnt)
+    assert full.debug == j24.debug
