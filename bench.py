@@ -93,6 +93,9 @@ def main() -> int:
     if os.environ.get("MISLO_BENCH_GPU_OF_RANK") is not None:
         local = int(os.environ["MISLO_BENCH_GPU_OF_RANK"])
     torch.cuda.set_device(local)
+    # keep this rank's pinned ring and host threads on its GPU's socket (before any pinning)
+    from llm_slo_ebpf_toolkit_amd.parallel.numa import bind_to_device_numa
+    numa_cpus = bind_to_device_numa(local)
     pg = None
     if world > 1:
         backend = os.environ.get("MISLO_DIST_BACKEND", "nccl")
@@ -256,6 +259,7 @@ def main() -> int:
         "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
         "host_encode_ms_per_window": round(encode_ms, 3),
         "host_encode_threads": threads if a.wire in (16, 20) else 0,
+        "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
     }
     if rank == 0:
         line = json.dumps(res)

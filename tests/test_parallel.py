@@ -121,3 +121,22 @@ def oracle_layout():
     from llm_slo_ebpf_toolkit_amd.pipeline.window import PACKET_LAYOUT
 
     return PACKET_LAYOUT
+
+
+def test_numa_cpulist_and_affinity_choice(tmp_path):
+    from llm_slo_ebpf_toolkit_amd.parallel import numa
+
+    assert numa.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert numa.pci_bdf(0, 0x75, 0) == "0000:75:00.0"
+    dev = tmp_path / "0000:75:00.0"
+    dev.mkdir()
+    (dev / "numa_node").write_text("1\n")
+    (dev / "local_cpulist").write_text("48-95\n")
+    local = numa.local_cpus_of_pci("0000:75:00.0", str(tmp_path))
+    assert local == set(range(48, 96))
+    assert numa.choose_affinity(range(96), local) == set(range(48, 96))
+    assert numa.choose_affinity(range(48), local) is None          # cpuset excludes the GPU's socket
+    assert numa.choose_affinity(range(48, 96), local) is None      # already local: nothing to do
+    (dev / "numa_node").write_text("-1\n")                         # VMs: topology unknown
+    assert numa.local_cpus_of_pci("0000:75:00.0", str(tmp_path)) is None
+    assert numa.local_cpus_of_pci("0000:00:99.0", str(tmp_path)) is None
