@@ -5,7 +5,7 @@ Metric (BASELINE.json): "attribution macro-F1 on fault-replay confusion matrix; 
 overhead %", reported on config 5 ("full 9 CPU + 4 GPU signals, safety governor <= 3 %
 overhead, full confusion matrix across all fault domains") plus the events/s scaling
 curve the north star asks for. One step = one 1-second collection window per GPU, from
-the records the probes wrote into the agent's pinned ring (24-byte EVENT24 by default) ->
+the records the probes wrote into the agent's pinned ring (20-byte EVENT20T by default) ->
 host work (spans mapped onto the kernel's connection ids; with --wire 16/20, wire encoding
 of 64-byte records on a native worker pool) -> H2D -> decode + histograms -> LDS hash join
 -> MFMA posteriors + confusion -> MFMA sufficient statistics -> RCCL all-reduce of the
@@ -49,21 +49,29 @@ def parse():
                     help="windows replayed at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
-    ap.add_argument("--max-ahead", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--max-ahead", type=int, default=3, choices=(1, 2, 3),
                     help="windows the host may run ahead of the GPU (host back-pressure)")
+    ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4),
+                    help="device input buffers (window i uses i %% buffers): copies of window i wait for "
+                         "the kernels of window i - buffers")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", type=int, default=24, choices=(16, 20, 24, 32, 64),
-                    help="event record bytes on PCIe. 24 (default) / 32 / 64: the probes' ring records "
-                         "(EVENT24: kernel-interned contexts; EVENT32: kernel-interned connections; EVENT: "
-                         "64 bytes), DMA'd from the pinned ring as-is (no per-event host work; spans are "
-                         "mapped onto the kernel's connection ids for 24/32); 16 = EVENT16 / 20 = EVENT20, "
-                         "encoded from 64-byte records on the host inside every step (interned contexts and "
-                         "trace ids; the encoder reads the same 64 B per event the DMA would)")
+    ap.add_argument("--wire", default="20t", choices=("16", "20", "20t", "24", "32", "64"),
+                    help="event record format on PCIe. 20t (default) / 24 / 32 / 64: the probes' ring records "
+                         "(EVENT20T: 20 bytes, kernel-interned contexts and trace ids; EVENT24: interned "
+                         "contexts; EVENT32: interned connections; EVENT: 64 bytes), DMA'd from the pinned "
+                         "ring as-is (no per-event host work; spans are mapped onto the kernel's connection "
+                         "(and trace) ids); 16 = EVENT16 / 20 = EVENT20, encoded from 64-byte records on the "
+                         "host inside every step (interned contexts and trace ids; the encoder reads the same "
+                         "64 B per event the DMA would)")
     ap.add_argument("--encode-threads", type=int, default=0,
                     help="host encoder worker threads (0 = OMP_NUM_THREADS, else 8; at most 16)")
     ap.add_argument("--out", default="")
-    return ap.parse_args()
+    a = ap.parse_args()
+    from llm_slo_ebpf_toolkit_amd.collector.records import WIRE_NAMES
+
+    a.wire_name, a.wire = a.wire, WIRE_NAMES[a.wire]
+    return a
 
 
 def main() -> int:
@@ -118,14 +126,15 @@ def main() -> int:
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
     pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
-                          group_scope=a.group_scope, use_graphs=not a.no_graphs, max_ahead=a.max_ahead)
+                          group_scope=a.group_scope, use_graphs=not a.no_graphs,
+                          max_ahead=min(a.max_ahead, a.buffers), n_buffers=a.buffers)
     threads = a.encode_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 8)
     stager = WireStager(torch, pipe, a.events, a.spans, a.services, wire=a.wire, threads=threads)
     ring, pods = None, None
     if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
         ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
                  torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-    elif a.wire in (24, 32):  # the probes' own 24/32-byte records (kernel-interned contexts / connections)
+    elif a.wire in (21, 24, 32):  # the probes' own 20/24/32-byte records (kernel-interned ids)
         ring = [(stager.probe_records(w.events), None) for w in wins]
         # pod id -> svc|node: agent metadata (kubelet / CRI), static over the run
         pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
@@ -244,7 +253,10 @@ def main() -> int:
             "spans_per_window_per_gpu": a.spans,
             "incidents_per_window_per_gpu": a.services,
             "scenario": a.scenario,
-            "wire_bytes_per_event": a.wire,
+            "wire_bytes_per_event": records.wire_bytes(a.wire),
+            "wire_record": {"20t": "EVENT20T", "24": "EVENT24", "32": "EVENT32", "64": "EVENT", "20": "EVENT20",
+                            "16": "EVENT16"}[a.wire_name],
+            "device_buffers": a.buffers,
         },
         "macro_f1": round(summ["macro_f1"], 4),
         "vs_baseline_macro_f1": round(summ["macro_f1"] / BASELINE_MACRO_F1, 4),

@@ -54,7 +54,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("device", d.device, "HIP device ordinal"),
         ("model", d.model, "attribution model: bayes|bayes_learned|lda"),
         ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
-        ("wire", d.wire, "event record bytes on PCIe: 16 (EVENT16) | 20 (EVENT20) | 32 (compact) | 64"),
+        ("wire", d.wire, "event record format on PCIe: 16 (EVENT16) | 20 (EVENT20) | 21 (EVENT20T, 20 bytes) | 24 | 32 (compact) | 64"),
     ]:
         p.flag(name, default, help_)
     a = p.parse_args(argv)

@@ -84,7 +84,31 @@ EVENT24 = np.dtype([
     ("ctx_type", "<u4"),     # 20 bits 0-7 signal type, 8-31 context id
 ])
 assert EVENT24.itemsize == 24
-WIRE_DTYPES = {64: EVENT, 32: EVENT32, 24: EVENT24, 20: EVENT20, 16: EVENT16}
+# 20-byte record (= probes/ebpf/mislo_record.h mislo_event20t, the probes' default ring
+# record): EVENT24 with the trace hash interned in the kernel to a 32-bit id (mislo_traces);
+# the agent puts the window's spans on the same ids. Records sit at 20-byte strides. Its wire
+# code is 21 (20 is EVENT20, the window-relative host encoding): see wire_bytes().
+EVENT20T = np.dtype({"names": ["ts_ns", "value_milli", "ctx_type", "trace_id"],
+                     "formats": ["<i8", "<u4", "<u4", "<u4"],
+                     "offsets": [0, 8, 12, 16], "itemsize": 20})
+assert EVENT20T.itemsize == 20
+WIRE_20T = 21
+WIRE_DTYPES = {64: EVENT, 32: EVENT32, 24: EVENT24, WIRE_20T: EVENT20T, 20: EVENT20, 16: EVENT16}
+# bench / agent spelling of the wire codes
+WIRE_NAMES = {"64": 64, "32": 32, "24": 24, "20t": WIRE_20T, "20": 20, "16": 16}
+
+
+def wire_bytes(wire: int) -> int:
+    """PCIe bytes per event of wire code ``wire`` (21 = EVENT20T is 20 bytes)."""
+    return 20 if wire == WIRE_20T else int(wire)
+
+
+def wire_code(dtype: np.dtype) -> int:
+    """Wire code of a record dtype (itemsize, except EVENT20T -> 21)."""
+    for code, dt in WIRE_DTYPES.items():
+        if dt == dtype:
+            return code
+    raise TypeError(f"not a wire record dtype: {dtype}")
 
 SPAN = np.dtype([
     ("ts_ns", "<i8"),        # 0
@@ -351,6 +375,18 @@ def to_wire24(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner") ->
     ctx = ctxs.ids(events["pod_id"], events["pid"], cid, sn)
     st = events["signal_type"].astype(np.uint32)
     out["ctx_type"] = (st & np.uint32(0xFF)) | (ctx << np.uint32(8))
+    return out
+
+
+def to_wire20t(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner",
+               traces: "TraceInterner") -> np.ndarray:
+    """EVENT (64 B) -> EVENT20T (20 B), the probes' default ring record: EVENT24 with the
+    trace hash interned (spans must go through ``wire_spans`` with the same interners)."""
+    e24 = to_wire24(events, conns, ctxs)
+    out = np.zeros(events.shape[0], dtype=EVENT20T)
+    for f in ("ts_ns", "value_milli", "ctx_type"):
+        out[f] = e24[f]
+    out["trace_id"] = traces.ids(events["trace_h"])
     return out
 
 

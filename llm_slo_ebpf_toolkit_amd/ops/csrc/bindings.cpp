@@ -273,7 +273,7 @@ class Engine {
   // t_base, counts[6] = valid context-table rows (0 = all)
   void decode_ctx_wire(torch::Tensor events, int64_t wire) {
     check_cuda(events, "events");
-    if (events.nbytes() < (size_t)sig_cap_ * (size_t)wire)
+    if (events.nbytes() < (size_t)sig_cap_ * (size_t)wire_bytes((int)wire))
       throw std::invalid_argument("events buffer must hold sig_cap wire records");
     if (counts.numel() < 7) throw std::invalid_argument("wire 24/20/16 needs counts int32[>= 7] (t_base, n_ctx)");
     launch_decode_wire(events.data_ptr(), (int)wire, dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
@@ -286,9 +286,9 @@ class Engine {
 
   void decode_wire(torch::Tensor events, int64_t wire) {
     if (wire == 32) decode_compact(events);
-    else if (wire == 24 || wire == 20 || wire == 16) decode_ctx_wire(events, wire);
+    else if (wire == 24 || wire == kWire20T || wire == 20 || wire == 16) decode_ctx_wire(events, wire);
     else if (wire == 64) decode(events);
-    else throw std::invalid_argument("wire must be 64, 32, 24, 20 or 16");
+    else throw std::invalid_argument("wire must be 64, 32, 24, 21 (EVENT20T), 20 or 16");
   }
 
   void decode_ref(torch::Tensor events, int64_t pod, int64_t svcnode, int64_t trace_h) {
@@ -359,7 +359,8 @@ class Engine {
   }
 
   // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0].
-  // wire: 64 = Event records, 32 = compact EventC32 records, 24 = EventC24, 20 = EventC20, 16 = EventC16
+  // wire: 64 = Event records, 32 = compact EventC32 records, 24 = EventC24, 21 = EventC20T (20 bytes),
+  // 20 = EventC20, 16 = EventC16
   void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn,
                   int64_t wire) {
     reset_window();

@@ -30,14 +30,6 @@ struct DecodeOut {
 
 constexpr int kMiscSums = 2;  // offset of the per-slot value sums in misc
 
-template <int NT>
-__device__ __forceinline__ void flush_counts(uint32_t* lds, uint32_t* global, int n) {
-  for (int i = threadIdx.x; i < n; i += NT) {
-    uint32_t v = lds[i];
-    if (v) atomicAdd(global + i, v);
-  }
-}
-
 // Per-block partition histogram, stored (not atomically merged): the scan kernel turns
 // the [blocks][4][1024] matrix into per-block scatter offsets, so the scatter pass needs
 // no global atomics and places each block's events contiguously.
@@ -46,10 +38,87 @@ __device__ __forceinline__ void store_counts(const uint32_t* lds, uint32_t* dst)
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) dst[i] = lds[i];
 }
 
+// LDS counters of one decode workgroup. The small hot arrays (16 x 16 histogram bins, 16 x 3
+// status bins, 16 value sums) take an atomic from EVERY event, and a wave's 64 events land on
+// a handful of bins: same-address LDS atomics serialise (PMC: 64 % extra LDS cycles with one
+// copy). Each lane adds into copy (lane & 7) and the copies are summed at the flush; the odd
+// copy strides put the copies of a bin on different banks. The partition histogram (4 x 1024
+// hashed bins) keeps one copy: a wave's keys are nearly all distinct, so its conflicts are
+// random bank collisions that copies do not remove.
+struct DecodeLds {
+  static constexpr int kRep = 8, kPartRep = 1;
+  static constexpr int kHS = kSlots * kBuckets + 1, kSS = kSlots * 3 + 1, kUS = kSlots + 1;
+  static constexpr int kPS = kKeyTypes * kParts + 1;
+  uint32_t hist[kRep * kHS];
+  uint32_t status[kRep * kSS];
+  uint32_t part[kPartRep * kPS];
+  unsigned long long sum[kRep * kUS];
+};
+
+template <int NT>
+__device__ __forceinline__ void lds_init(DecodeLds& L) {
+  for (int i = threadIdx.x; i < DecodeLds::kPartRep * DecodeLds::kPS; i += NT) L.part[i] = 0;
+  for (int i = threadIdx.x; i < DecodeLds::kRep * DecodeLds::kUS; i += NT) L.sum[i] = 0;
+  for (int i = threadIdx.x; i < DecodeLds::kRep * DecodeLds::kHS; i += NT) L.hist[i] = 0;
+  for (int i = threadIdx.x; i < DecodeLds::kRep * DecodeLds::kSS; i += NT) L.status[i] = 0;
+  __syncthreads();
+}
+
+// this lane's copies
+struct LdsLane {
+  uint32_t *hist, *status, *part;
+  unsigned long long* sum;
+};
+__device__ __forceinline__ LdsLane lds_lane(DecodeLds& L) {
+  const int r = threadIdx.x & (DecodeLds::kRep - 1), q = threadIdx.x & (DecodeLds::kPartRep - 1);
+  return LdsLane{L.hist + r * DecodeLds::kHS, L.status + r * DecodeLds::kSS, L.part + q * DecodeLds::kPS,
+                 L.sum + r * DecodeLds::kUS};
+}
+
+// sum the copies: signal / status bins and value sums merge with one global atomic per
+// non-zero bin; the partition counts are stored per workgroup (atomic-free scatter)
+template <int NT>
+__device__ __forceinline__ void lds_flush(DecodeLds& L, const DecodeOut& o, int unsupported, int zero_ts) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int r = 0; r < DecodeLds::kRep; ++r) v += L.hist[r * DecodeLds::kHS + i];
+    if (v) atomicAdd(o.hist + i, v);
+  }
+  for (int i = threadIdx.x; i < kSlots * 3; i += NT) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int r = 0; r < DecodeLds::kRep; ++r) v += L.status[r * DecodeLds::kSS + i];
+    if (v) atomicAdd(o.status_cnt + i, v);
+  }
+  if (threadIdx.x < kSlots) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int r = 0; r < DecodeLds::kRep; ++r) v += L.sum[r * DecodeLds::kUS + threadIdx.x];
+    if (v) atomicAdd(&o.misc[kMiscSums + threadIdx.x], v);
+  }
+  uint32_t* dst = o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts;
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < DecodeLds::kPartRep; ++q) v += L.part[q * DecodeLds::kPS + i];
+    dst[i] = v;
+  }
+  // wave-level reduction of the scalar counters, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    unsupported += __shfl_xor(unsupported, off);
+    zero_ts += __shfl_xor(zero_ts, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
+    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
+  }
+}
+
 __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val, int slot,
                                            uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
-                                           uint64_t conn_h, const DecodeOut& o, uint32_t* s_hist,
-                                           uint32_t* s_status, uint32_t* s_part, unsigned long long* s_sum,
+                                           uint64_t conn_h, const DecodeOut& o, const LdsLane& l,
                                            int& unsupported, int& zero_ts, bool local) {
   uint8_t st = 0;
   if (slot >= 0 && local) {
@@ -58,11 +127,11 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
     int b = 0;
 #pragma unroll
     for (int e = 0; e < kBuckets - 1; ++e) b += (val > c_tab.edges[slot][e]) ? 1 : 0;
-    atomicAdd(&s_hist[slot * kBuckets + b], 1u);
-    atomicAdd(&s_status[slot * 3 + st], 1u);
+    atomicAdd(&l.hist[slot * kBuckets + b], 1u);
+    atomicAdd(&l.status[slot * 3 + st], 1u);
     // exact, order-independent integer sum (values are >= 0 by construction)
     const double milli = rint((double)val * 1000.0);
-    if (milli > 0.0) atomicAdd(&s_sum[slot], (unsigned long long)milli);
+    if (milli > 0.0) atomicAdd(&l.sum[slot], (unsigned long long)milli);
   } else if (slot >= 0) {
     st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
   } else if (local) {
@@ -90,7 +159,7 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
   for (int k = 0; k < kKeyTypes; ++k) {
     const uint64_t h = joinable ? key_hash(k, trace_h, pod, pid, conn_h, svcnode) : 0ull;
     pc.p[k] = h ? (uint16_t)part_of(h) : kNoPart;
-    if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
+    if (h) atomicAdd(&l.part[k * kParts + part_of(h)], 1u);
   }
   o.cols.part[i] = pc;
 }
@@ -98,15 +167,9 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
 template <int NT>
 __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ ev, const int* __restrict__ n_ptr,
                                                       int cap, DecodeOut o) {
-  __shared__ uint32_t s_hist[kSlots * kBuckets];
-  __shared__ uint32_t s_status[kSlots * 3];
-  __shared__ uint32_t s_part[kKeyTypes * kParts];
-  __shared__ unsigned long long s_sum[kSlots];
-  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
-  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
-  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
-  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
-  __syncthreads();
+  __shared__ DecodeLds L;
+  lds_init<NT>(L);
+  const LdsLane l = lds_lane(L);
 
   const int n = min(*n_ptr, cap);
   // counts[3] = number of node-local events; events past it are imported halo / remote
@@ -122,23 +185,9 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
     const float val = slot >= 0 ? (float)((double)e.value * (double)c_tab.scale[slot]) : (float)e.value;
     const uint64_t ch = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
     const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
-    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status,
-               s_part, s_sum, unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
   }
-  __syncthreads();
-  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
-  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
-  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
-  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
-  // wave-level reduction of the scalar counters, one atomic per wave
-  for (int off = 32; off > 0; off >>= 1) {
-    unsupported += __shfl_xor(unsupported, off);
-    zero_ts += __shfl_xor(zero_ts, off);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
-    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
-  }
+  lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
 // 32-byte compact records: half the PCIe bytes of Event; service|node come from the
@@ -148,15 +197,9 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
                                                        const int* __restrict__ n_ptr, int cap,
                                                        const uint32_t* __restrict__ pod_svcnode, int n_pods,
                                                        DecodeOut o) {
-  __shared__ uint32_t s_hist[kSlots * kBuckets];
-  __shared__ uint32_t s_status[kSlots * 3];
-  __shared__ uint32_t s_part[kKeyTypes * kParts];
-  __shared__ unsigned long long s_sum[kSlots];
-  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
-  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
-  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
-  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
-  __syncthreads();
+  __shared__ DecodeLds L;
+  lds_init<NT>(L);
+  const LdsLane l = lds_lane(L);
 
   const int n = min(*n_ptr, cap);
   // counts[3] = number of node-local events; events past it are imported halo / remote
@@ -172,22 +215,9 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
     const float val = (float)((double)e.value_milli * 1e-3);
     const uint64_t ch = (uint64_t)(e.type_conn >> 8);
     const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
-    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, s_hist, s_status, s_part,
-               s_sum, unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
   }
-  __syncthreads();
-  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
-  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
-  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
-  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
-  for (int off = 32; off > 0; off >>= 1) {
-    unsupported += __shfl_xor(unsupported, off);
-    zero_ts += __shfl_xor(zero_ts, off);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
-    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
-  }
+  lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
 // 20-byte (16-byte) records: 5/8 (1/2) of the compact record's PCIe bytes. The window base timestamp is
@@ -196,27 +226,24 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
 __device__ __forceinline__ uint64_t wire_trace(const EventC20& e) { return ((uint64_t)e.tr_hi << 32) | e.tr_lo; }
 __device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)e.trace_id; }
 __device__ __forceinline__ uint64_t wire_trace(const EventC24& e) { return e.trace_h; }
+__device__ __forceinline__ uint64_t wire_trace(const EventC20T& e) { return (uint64_t)e.trace_id; }
 template <class Rec>
 __device__ __forceinline__ int64_t wire_ts(const Rec& e, int64_t t_base) {
   return e.ts_off == kTsZero ? 0 : t_base + (int64_t)e.ts_off;
 }
 __device__ __forceinline__ int64_t wire_ts(const EventC24& e, int64_t) { return e.ts_ns; }
+__device__ __forceinline__ int64_t wire_ts(const EventC20T& e, int64_t) { return e.ts_ns; }
 
-// Rec = EventC20 (20-byte), EventC16 (16-byte, interned trace ids) or EventC24 (24-byte,
-// absolute timestamps: the probes' context-interned ring record): identical decoding otherwise.
+// Rec = EventC20 (20-byte), EventC16 (16-byte, interned trace ids), EventC24 (24-byte,
+// absolute timestamps: the probes' context-interned ring record) or EventC20T (20-byte,
+// absolute timestamps, kernel-interned trace ids): identical decoding otherwise.
 template <int NT, class Rec>
 __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, const int* __restrict__ n_ptr,
                                                     int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
                                                     DecodeOut o) {
-  __shared__ uint32_t s_hist[kSlots * kBuckets];
-  __shared__ uint32_t s_status[kSlots * 3];
-  __shared__ uint32_t s_part[kKeyTypes * kParts];
-  __shared__ unsigned long long s_sum[kSlots];
-  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
-  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
-  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
-  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
-  __syncthreads();
+  __shared__ DecodeLds L;
+  lds_init<NT>(L);
+  const LdsLane l = lds_lane(L);
 
   const int n = min(*n_ptr, cap);
   const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
@@ -226,31 +253,34 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0;
-  for (int i = beg + threadIdx.x; i < end; i += NT) {
-    const Rec e = ev[i];
+  // software pipeline: the next record and its context row are loaded while this one is
+  // decoded (one workgroup per CU at this grid: the loads must overlap the LDS work)
+  auto ctx_of = [&](const Rec& r) {
+    const uint32_t cid = r.ctx_type >> 8;
+    return cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
+  };
+  int i = beg + threadIdx.x;
+  Rec e_nx{};
+  uint4 cx_nx = make_uint4(0u, 0u, 0u, 0u);
+  if (i < end) {
+    e_nx = ev[i];
+    cx_nx = ctx_of(e_nx);
+  }
+  for (; i < end; i += NT) {
+    const Rec e = e_nx;
+    const uint4 cx = cx_nx;
+    if (i + NT < end) {
+      e_nx = ev[i + NT];
+      cx_nx = ctx_of(e_nx);
+    }
     const int st = (int)(e.ctx_type & 0xFFu);
     const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
     const float val = (float)((double)e.value_milli * 1e-3);
-    const uint32_t cid = e.ctx_type >> 8;
-    const uint4 cx = cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
     const int64_t ts = wire_ts(e, t_base);
     const uint64_t tr = wire_trace(e);
-    decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, s_hist, s_status, s_part, s_sum,
-               unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, i < n_local);
   }
-  __syncthreads();
-  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
-  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
-  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
-  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
-  for (int off = 32; off > 0; off >>= 1) {
-    unsupported += __shfl_xor(unsupported, off);
-    zero_ts += __shfl_xor(zero_ts, off);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
-    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
-  }
+  lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
 // REF 40-byte records: REF units (count stays count, cpu_steal raw ns, else ns/1e6) and
@@ -259,15 +289,9 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ ev, const int* __restrict__ n_ptr,
                                                    int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,
                                                    DecodeOut o) {
-  __shared__ uint32_t s_hist[kSlots * kBuckets];
-  __shared__ uint32_t s_status[kSlots * 3];
-  __shared__ uint32_t s_part[kKeyTypes * kParts];
-  __shared__ unsigned long long s_sum[kSlots];
-  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
-  if (threadIdx.x < kSlots) s_sum[threadIdx.x] = 0;
-  for (int i = threadIdx.x; i < kSlots * kBuckets; i += NT) s_hist[i] = 0;
-  for (int i = threadIdx.x; i < kSlots * 3; i += NT) s_status[i] = 0;
-  __syncthreads();
+  __shared__ DecodeLds L;
+  lds_init<NT>(L);
+  const LdsLane l = lds_lane(L);
   const int n = min(*n_ptr, cap);
   // counts[3] = number of node-local events; events past it are imported halo / remote
   // trace-tagged copies that take part in the join but not in the window's counters.
@@ -283,22 +307,9 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
     if (st == 2 || st == 6) val = (float)e.value_ns;           // tcp count, cpu_steal raw ns
     else val = (float)((double)e.value_ns / 1e6);               // ns -> ms
     const uint64_t ch = conn_hash(e.conn_src_port, e.conn_dst_port, e.conn_dst_ip);
-    decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, s_hist,
-               s_status, s_part, s_sum, unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
   }
-  __syncthreads();
-  flush_counts<NT>(s_hist, o.hist, kSlots * kBuckets);
-  flush_counts<NT>(s_status, o.status_cnt, kSlots * 3);
-  if (threadIdx.x < kSlots && s_sum[threadIdx.x]) atomicAdd(&o.misc[kMiscSums + threadIdx.x], s_sum[threadIdx.x]);
-  store_counts<NT>(s_part, o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
-  for (int off = 32; off > 0; off >>= 1) {
-    unsupported += __shfl_xor(unsupported, off);
-    zero_ts += __shfl_xor(zero_ts, off);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (unsupported) atomicAdd(&o.misc[0], (unsigned long long)unsupported);
-    if (zero_ts) atomicAdd(&o.misc[1], (unsigned long long)zero_ts);
-  }
+  lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
 // Span records -> span columns + span partition counts.
@@ -338,6 +349,11 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp
   store_counts<NT>(s_part, part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
 }
 
+// Event decoders run 1024 threads per workgroup: the grid is capped at kPartBlocks (the
+// per-block partition matrix the scan consumes), so a fixed grid of 256 workgroups x 4 waves
+// left one wave per SIMD, latency-bound on the record loads; 16 waves per CU hide them.
+constexpr int kDecodeNT = 1024;
+
 int decode_grid(int cap) {
   // Fixed per-capacity grid (graph-replayable): ~4 events per thread, capped at kPartBlocks.
   long long g = ((long long)cap + 1023) / 1024;
@@ -353,7 +369,7 @@ void set_tables(const Tables* host_tables) {
 void launch_decode_events(const void* ev, const int* n_dev, int cap, const SignalCols& cols, uint32_t* hist,
                           uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
-  constexpr int NT = 256;
+  constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_events<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                      (const Event*)ev, n_dev, cap, o);
 }
@@ -362,7 +378,7 @@ void launch_decode_compact(const void* ev, const int* n_dev, int cap, const uint
                            const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                            unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
-  constexpr int NT = 256;
+  constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_compact<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, (const EventC32*)ev, n_dev,
                      cap, pod_svcnode, n_pods, o);
 }
@@ -371,7 +387,7 @@ void launch_decode_wire(const void* ev, int wire, const int* n_dev, int cap, con
                         const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                         unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
-  constexpr int NT = 256;
+  constexpr int NT = kDecodeNT;
   const uint4* tab = reinterpret_cast<const uint4*>(ctx_tab);
   if (wire == 16)
     hipLaunchKernelGGL((k_decode_wire<NT, EventC16>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
@@ -379,6 +395,9 @@ void launch_decode_wire(const void* ev, int wire, const int* n_dev, int cap, con
   else if (wire == 24)
     hipLaunchKernelGGL((k_decode_wire<NT, EventC24>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                        (const EventC24*)ev, n_dev, cap, tab, n_ctx, o);
+  else if (wire == kWire20T)
+    hipLaunchKernelGGL((k_decode_wire<NT, EventC20T>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                       (const EventC20T*)ev, n_dev, cap, tab, n_ctx, o);
   else
     hipLaunchKernelGGL((k_decode_wire<NT, EventC20>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                        (const EventC20*)ev, n_dev, cap, tab, n_ctx, o);
@@ -388,7 +407,7 @@ void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, 
                        const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                        unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
-  constexpr int NT = 256;
+  constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_ref<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
                      (const RefEvent*)ev, n_dev, cap, pod, svcnode, trace_h, o);
 }

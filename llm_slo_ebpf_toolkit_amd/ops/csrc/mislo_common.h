@@ -76,6 +76,18 @@ struct alignas(8) EventC24 {
   uint32_t ctx_type;  // bits 0-7 signal type, bits 8-31 context id
 };
 static_assert(sizeof(EventC24) == 24, "EventC24 must be 24 bytes");
+// 20-byte record (EVENT20T = probes/ebpf/mislo_record.h mislo_event20t, the probes' default
+// ring record): EventC24 with the trace hash interned in the kernel to a 32-bit id that the
+// window's spans carry too. Packed at 20-byte strides (4-byte aligned). Wire code 21.
+struct __attribute__((packed, aligned(4))) EventC20T {
+  int64_t ts_ns;
+  uint32_t value_milli;
+  uint32_t ctx_type;  // bits 0-7 signal type, bits 8-31 context id
+  uint32_t trace_id;
+};
+static_assert(sizeof(EventC20T) == 20, "EventC20T must be 20 bytes");
+constexpr int kWire20T = 21;  // wire code of EventC20T (20 bytes; 20 is the window-based EventC20)
+inline constexpr int wire_bytes(int wire) { return wire == kWire20T ? 20 : wire; }
 
 // REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).
 struct __attribute__((packed)) RefEvent {

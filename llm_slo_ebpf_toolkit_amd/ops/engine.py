@@ -158,8 +158,8 @@ class GpuEngine:
             raise ValueError("window exceeds engine capacity")
         if events.dtype not in records.WIRE_DTYPES.values() or spans.dtype != records.SPAN:
             raise TypeError("events/spans must use the EVENT|EVENT32|EVENT20|EVENT16/SPAN record dtypes")
-        self.wire = events.dtype.itemsize
-        self.ev_host.numpy()[: n * self.wire] = events.view(np.uint8).reshape(-1)
+        self.wire = records.wire_code(events.dtype)
+        self.ev_host.numpy()[: n * records.wire_bytes(self.wire)] = events.view(np.uint8).reshape(-1)
         self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)
         c = self.cnt_host.numpy()
         tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
@@ -175,7 +175,7 @@ class GpuEngine:
         torch = self.torch
         cs = self.copy_stream
         with torch.cuda.stream(cs):
-            nb = self.n_events * self.wire
+            nb = self.n_events * records.wire_bytes(self.wire)
             self.ev_dev[:nb].copy_(self.ev_host[:nb], non_blocking=True)
             self.sp_dev[: self.n_spans * 64].copy_(self.sp_host[: self.n_spans * 64], non_blocking=True)
             self.eng.counts.copy_(self.cnt_host, non_blocking=True)

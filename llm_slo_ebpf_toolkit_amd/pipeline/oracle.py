@@ -248,3 +248,4 @@ def join(d: Decoded, spans: np.ndarray, n_groups: int, window_ms: float = 2000.0
         "spans_enriched": int((conf > 0).sum()),
     }
     return JoinResult(top3, cnt, attrs, conf, gsum, gcnt, feat, debug)
+decode_w20t = decode_w24  # EVENT20T: absolute timestamps, interned trace ids

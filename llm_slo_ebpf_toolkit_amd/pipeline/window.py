@@ -1,8 +1,8 @@
 """Per-GPU window pipeline: copy stream || compute stream || RCCL side stream.
 
-One process drives one MI355X. For window i (double-buffered device I/O, b = i % 2):
+One process drives one MI355X. For window i (nb-buffered device I/O, b = i % nb, nb = 3):
 
-    copy stream    : H2D records(i) -> ev[b], sp[b], counts[b], labels[b]      (PCIe DMA)
+    copy stream    : H2D records(i) -> ev[b]; [counts|labels|spans](i) -> aux[b] (PCIe DMA)
     compute stream : wait H2D(i); decode -> partition -> LDS join -> finalize ->
                      MFMA posterior + confusion -> MFMA sufficient stats -> pack(packet[b])
     comm stream    : wait compute(i); all_reduce(packet[b]) over RCCL/xGMI;
@@ -60,6 +60,12 @@ def stats_from_packet(p: Dict[str, np.ndarray]) -> SufficientStats:
                            x_sum=st[16:, :D].copy(), xx=st[16:, 16:].copy())
 
 
+def aux_head(group_cap: int) -> int:
+    """Bytes ahead of the spans in a packed input block: counts int32[8], labels int32[G],
+    padded to 64 so the span records stay 64-byte aligned."""
+    return (32 + 4 * max(int(group_cap), 1) + 63) // 64 * 64
+
+
 @dataclass
 class StagedWindow:
     """A window's records in pinned host memory, ready for DMA."""
@@ -76,6 +82,9 @@ class StagedWindow:
     ctx_rows: "object" = None           # torch int32 pinned [n_ctx, 4] context table snapshot (wire 20/16)
     n_ctx: int = 0
     encode_s: float = 0.0               # host time spent converting records to the wire format
+    # pinned [counts | labels | pad | spans] block when counts / labels / sp are views of it
+    # (WireStager): the three small inputs then cross PCIe as ONE copy (aux_head(group_cap))
+    aux: "object" = None
 
 
 def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
@@ -93,9 +102,9 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
     t_enc = time.perf_counter()
     pod_tab = None
     ctx_rows, n_ctx, t_base = None, 0, 0
-    if wire in (20, 16) and ctx_interner is None and events.dtype == records.EVENT:
+    if wire in (20, 16, records.WIRE_20T) and ctx_interner is None and events.dtype == records.EVENT:
         enc = encoder if encoder is not None else records.native_encoder()
-        ev = torch.empty(max(events.shape[0], 1) * wire, dtype=torch.uint8).pin_memory()
+        ev = torch.empty(max(events.shape[0], 1) * records.wire_bytes(wire), dtype=torch.uint8).pin_memory()
         sp = torch.empty(max(spans.shape[0], 1) * 64, dtype=torch.uint8).pin_memory()
         t_enc = time.perf_counter()  # conversion only (the agent reuses its pinned buffers)
         try:
@@ -105,31 +114,35 @@ def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, la
             # travels as 32-byte records, which carry absolute timestamps
             wire = 32
         else:
-            enc.encode_spans(np.ascontiguousarray(spans), sp.numpy(), wire == 16)
-            enc.end_window()
+            enc.encode_spans(np.ascontiguousarray(spans), sp.numpy(), wire in (16, records.WIRE_20T))
+            if wire != records.WIRE_20T:  # kernel-interned trace ids live as long as the LRU keeps them
+                enc.end_window()
             tab = enc.ctx_table()
             n_ctx = int(tab.shape[0])
             ctx_rows = torch.from_numpy(tab).pin_memory()
             return _finish_stage(torch, ev, sp, events.shape[0], spans.shape[0], n_groups, labels, group_cap,
                                  group_domains, wire, None, ctx_rows, n_ctx, t_base, n_local, t_enc)
-    if wire in (32, 20, 16):
+    if wire in (32, 20, 16, records.WIRE_20T):
         if interner is None:
             interner = records.ConnInterner()
         if wire == 32 and events.dtype == records.EVENT:
             pod_tab = records.pod_table(events, spans)
             events = records.to_compact(events, interner)
-        elif wire in (20, 16):
+        elif wire in (20, 16, records.WIRE_20T):
             if wire == 20:
                 events, t_base = records.to_wire20(events, interner, ctx_interner)
+            elif wire == records.WIRE_20T:
+                trace_interner = trace_interner if trace_interner is not None else records.TraceInterner()
+                events = records.to_wire20t(events, interner, ctx_interner, trace_interner)
             else:
                 trace_interner = trace_interner if trace_interner is not None else records.TraceInterner()
                 events, t_base = records.to_wire16(events, interner, ctx_interner, trace_interner)
             tab = ctx_interner.table()
             n_ctx = int(tab.shape[0])
             ctx_rows = torch.from_numpy(tab.copy()).pin_memory()
-        spans = records.wire_spans(spans, interner, trace_interner if wire == 16 else None)
+        spans = records.wire_spans(spans, interner, trace_interner if wire in (16, records.WIRE_20T) else None)
     elif wire != 64:
-        raise ValueError("wire must be 64, 32, 20 or 16")
+        raise ValueError("wire must be 64, 32, 21 (EVENT20T), 20 or 16")
     ev = torch.from_numpy(events.view(np.uint8).reshape(-1).copy()).pin_memory()
     sp = torch.from_numpy(spans.view(np.uint8).reshape(-1).copy()).pin_memory()
     return _finish_stage(torch, ev, sp, events.shape[0], spans.shape[0], n_groups, labels, group_cap,
@@ -156,8 +169,8 @@ def _finish_stage(torch, ev, sp, n_ev: int, n_sp: int, n_groups: int, labels, gr
 class WireStager:
     """The agent's per-window host stage: 64-byte probe records (as the probes write them into
     the ring) -> 16/20-byte wire records in one of two reusable pinned slots, on the native
-    encoder's worker pool (runtime/csrc/wire.h ``encode_window``). Window k writes slot k % 2,
-    the buffer the pipeline's H2D of window k reads, after the H2D of window k - 2 (the slot's
+    encoder's worker pool (runtime/csrc/wire.h ``encode_window``). Window k writes slot k % nb,
+    the buffer the pipeline's H2D of window k reads, after the H2D of window k - nb (the slot's
     previous reader) has completed, so encoding window k+1 overlaps the GPU work of window k.
 
     ``wire=64`` ships the ring records unchanged: ``events``/``spans`` must then already sit in
@@ -172,17 +185,25 @@ class WireStager:
 
     def __init__(self, torch, pipe: "WindowPipeline", sig_cap: int, span_cap: int, group_cap: int, wire: int = 16,
                  threads: int = 8):
-        if wire not in (16, 20, 24, 32, 64):
-            raise ValueError("WireStager: wire must be 16, 20, 24, 32 or 64")
+        if wire not in (16, 20, records.WIRE_20T, 24, 32, 64):
+            raise ValueError("WireStager: wire must be 16, 20, 21 (EVENT20T), 24, 32 or 64")
         self.torch, self.pipe, self.wire, self.threads = torch, pipe, wire, max(1, int(threads))
         self.group_cap = group_cap
         pin = lambda n, dt=torch.uint8: torch.empty(n, dtype=dt).pin_memory()  # noqa: E731
         self.enc = records.native_encoder() if wire != 64 else None
-        self.ev = [pin(max(sig_cap, 1) * wire) for _ in range(2)] if wire in (16, 20) else None
-        self.sp = [pin(max(span_cap, 1) * 64) for _ in range(2)] if wire != 64 else None
-        self.counts = [pin(8, torch.int32) for _ in range(2)]
-        self.labels = [pin(group_cap, torch.int32) for _ in range(2)]
-        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire in (16, 20, 24) else None
+        self.nb = pipe.nb  # one pinned slot per device buffer of the pipeline
+        self.ev = [pin(max(sig_cap, 1) * wire) for _ in range(self.nb)] if wire in (16, 20) else None
+        # [counts | labels | pad | spans] per slot: one H2D for the window's small inputs
+        head = aux_head(group_cap)
+        self.aux = [pin(head + max(span_cap, 1) * 64) for _ in range(self.nb)] if wire != 64 else None
+        self.sp = [a[head:] for a in self.aux] if wire != 64 else None
+        if self.aux is not None:
+            self.counts = [a[:32].view(torch.int32) for a in self.aux]
+            self.labels = [a[32:32 + 4 * max(group_cap, 1)].view(torch.int32) for a in self.aux]
+        else:
+            self.counts = [pin(8, torch.int32) for _ in range(self.nb)]
+            self.labels = [pin(group_cap, torch.int32) for _ in range(self.nb)]
+        self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire in (16, 20, records.WIRE_20T, 24) else None
         self.n_ctx = 1
         self.k = 0
         self.encode_s = 0.0
@@ -191,9 +212,10 @@ class WireStager:
         """EVENT32 / EVENT24 records (``self.wire``) for 64-byte ``events`` as the probes emit
         them (kernel-side connection / context interning, integer fixed point), written into
         pinned memory: a replayed ring."""
-        if self.wire not in (24, 32):
-            raise ValueError("probe_records: wire 24 or 32")
-        out = self.torch.empty(max(events.shape[0], 1) * self.wire, dtype=self.torch.uint8).pin_memory()
+        if self.wire not in (records.WIRE_20T, 24, 32):
+            raise ValueError("probe_records: wire 21 (EVENT20T), 24 or 32")
+        out = self.torch.empty(max(events.shape[0], 1) * records.wire_bytes(self.wire),
+                               dtype=self.torch.uint8).pin_memory()
         self.enc.encode(np.ascontiguousarray(events), out.numpy(), self.wire)
         return out
 
@@ -201,8 +223,8 @@ class WireStager:
               group_domains=None, n_local: Optional[int] = None, ev_pinned=None, sp_pinned=None,
               pod_table: Optional[np.ndarray] = None) -> StagedWindow:
         torch = self.torch
-        slot = self.k % 2
-        if self.k >= 2:  # slot's previous reader: the H2D of window k - 2
+        slot = self.k % self.nb
+        if self.k >= self.nb:  # slot's previous reader: the H2D of window k - nb
             self.pipe.h2d_done[slot].synchronize()
         t0 = time.perf_counter()
         n_ev, n_sp = int(events.shape[0]), int(spans.shape[0])
@@ -211,13 +233,14 @@ class WireStager:
             ev, sp = ev_pinned, sp_pinned
             if ev is None or sp is None:
                 raise ValueError("wire 64 stages the pinned ring records: pass ev_pinned / sp_pinned")
-        elif self.wire in (24, 32):
+        elif self.wire in (records.WIRE_20T, 24, 32):
             ev, sp = ev_pinned, self.sp[slot]
             if ev is None or (self.wire == 32 and pod_table is None):
-                raise ValueError("wire 32/24 stage the pinned probe ring: pass ev_pinned (and pod_table for 32)")
+                raise ValueError("wire 32/24/21 stage the pinned probe ring: pass ev_pinned (and pod_table for 32)")
             if n_sp * 64 > sp.numel():
                 raise ValueError("window exceeds the stager's capacity")
-            self.enc.encode_spans(spans, sp.numpy(), False)
+            # spans onto the kernel's connection ids (and, for EVENT20T, its trace ids)
+            self.enc.encode_spans(spans, sp.numpy(), self.wire == records.WIRE_20T)
         else:
             ev, sp = self.ev[slot], self.sp[slot]
             if n_ev * self.wire > ev.numel() or n_sp * 64 > sp.numel():
@@ -249,14 +272,15 @@ class WireStager:
         ctx = self.ctx is not None
         return StagedWindow(ev, sp, self.counts[slot], self.labels[slot], n_ev, n_sp, n_groups,
                             list(group_domains or []), self.wire, pod_table if self.wire == 32 else None,
-                            self.ctx if ctx else None, self.n_ctx if ctx else 0, dt)
+                            self.ctx if ctx else None, self.n_ctx if ctx else 0, dt,
+                            self.aux[slot] if self.aux is not None else None)
 
 
 class WindowPipeline:
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, process_group=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, group_scope: str = "rank",
-                 use_graphs: bool = True, max_ahead: int = 2):
+                 use_graphs: bool = True, max_ahead: int = 3, n_buffers: int = 3):
         import torch
 
         self.torch = torch
@@ -281,7 +305,12 @@ class WindowPipeline:
         # host back-pressure: submit(i) first waits until window i - max_ahead has computed.
         # Stream-ordered waits alone let the host run arbitrarily far ahead; the runtime then
         # stalls the host for milliseconds at a time once its command queues fill
-        self.max_ahead = min(2, max(1, int(max_ahead)))  # events exist for the last 2 windows
+        # device input buffers: window i uses b = i % nb. With two, the H2D of window i waits
+        # for window i-2's kernels, and the host (back-pressured on the same event) issues it
+        # only after waking from that wait: the copy engine idled ~50 us per window. With three,
+        # the H2D of window i depends on window i-3 and is queued before the engine frees up.
+        self.nb = max(2, int(n_buffers))
+        self.max_ahead = min(self.nb, max(1, int(max_ahead)))  # events exist for the last nb windows
         self.engine = GpuEngine(sig_cap, span_cap, group_cap, device, window_ms, threshold, fanout, group_mode)
         self.eng = self.engine.eng
         L = int(self.engine.mod.PACKET_LEN)
@@ -290,17 +319,23 @@ class WindowPipeline:
         self.packet_len = L
         with torch.cuda.device(self.dev):
             z8 = lambda n: torch.zeros(n, dtype=torch.uint8, device=self.dev)  # noqa: E731
-            self.ev_dev = [z8(sig_cap * 64), z8(sig_cap * 64)]
-            self.sp_dev = [z8(span_cap * 64), z8(span_cap * 64)]
-            self.counts_dev = [torch.zeros(8, dtype=torch.int32, device=self.dev) for _ in range(2)]
+            self.ev_dev = [z8(sig_cap * 64) for _ in range(self.nb)]
+            # per buffer one [counts | labels | pad | spans] block (aux_head): a packed staged
+            # window lands with a single H2D; the views keep fixed addresses for the graphs
+            self.aux_head = aux_head(group_cap)
+            self.aux_dev = [z8(self.aux_head + span_cap * 64) for _ in range(self.nb)]
+            self.sp_dev = [a[self.aux_head:] for a in self.aux_dev]
+            self.counts_dev = [a[:32].view(torch.int32) for a in self.aux_dev]
             # append-only context table for 20-byte records: rows are copied once, stream
             # ordered before the first window that references them; the buffer address stays
             # fixed (captured graphs keep pointing at it) until it has to grow
             self.ctx_dev = torch.zeros((1 << 16, 4), dtype=torch.int32, device=self.dev)
             self.ctx_uploaded = 1  # row 0 = the all-zero context
             self.eng.set_ctx_table(self.ctx_dev)
-            self.labels_dev = [torch.full((group_cap,), -1, dtype=torch.int32, device=self.dev) for _ in range(2)]
-            self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(2)]
+            self.labels_dev = [a[32:32 + 4 * max(group_cap, 1)].view(torch.int32) for a in self.aux_dev]
+            for lab in self.labels_dev:
+                lab.fill_(-1)
+            self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(self.nb)]
             self.totals = torch.zeros(L, dtype=torch.float64, device=self.dev)
             self.host_s = [0.0, 0.0, 0.0, 0]
             self.stats_off = sum(PACKET_LAYOUT[:5])
@@ -308,15 +343,17 @@ class WindowPipeline:
             p0 = np.zeros((16, 16), dtype=np.float64)
             p0[:, :N_DOMAINS] = NaiveBayes.random_init_table(seed)
             self.p0_dev = torch.from_numpy(p0.ravel()).to(self.dev)
-            self.packet_host = [torch.zeros(L, dtype=torch.float64).pin_memory() for _ in range(2)]
-            self.model_host = [torch.zeros(2568, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            self.packet_host = [torch.zeros(L, dtype=torch.float64).pin_memory() for _ in range(self.nb)]
+            # a model upload issued in submit(j) completes before window j+1 computes; the host
+            # waits for window i - max_ahead, so max_ahead + 2 slots are never overwritten early
+            self.model_host = [torch.zeros(2568, dtype=torch.uint8).pin_memory() for _ in range(self.max_ahead + 2)]
             self.copy_stream = torch.cuda.Stream(self.dev)
             self.comm_stream = torch.cuda.Stream(self.dev)
             self.compute_stream = torch.cuda.Stream(self.dev)
             ev = lambda: torch.cuda.Event()  # noqa: E731
-            self.h2d_done = [ev(), ev()]
-            self.compute_done = [ev(), ev()]
-            self.comm_done = [ev(), ev()]
+            self.h2d_done = [ev() for _ in range(self.nb)]
+            self.compute_done = [ev() for _ in range(self.nb)]
+            self.comm_done = [ev() for _ in range(self.nb)]
             self.join_done, self.groups_done = ev(), ev()
         self.pod_key = None
         self.i = 0
@@ -336,7 +373,7 @@ class WindowPipeline:
 
     def _upload_model(self, model) -> None:
         torch = self.torch
-        slot = self.i % 2
+        slot = self.i % len(self.model_host)
         host = self.model_host[slot]
         host.numpy()[:] = model_bytes(model)
         with torch.cuda.stream(self.compute_stream):
@@ -355,11 +392,11 @@ class WindowPipeline:
     def submit(self, w: StagedWindow, with_labels: bool = True) -> None:
         t_enter = time.perf_counter()
         torch = self.torch
-        b = self.i % 2
+        b = self.i % self.nb
         cs, ks, ms = self.copy_stream, self.compute_stream, self.comm_stream
         if self.i >= self.max_ahead:
-            self.compute_done[(self.i - self.max_ahead) % 2].synchronize()
-        # H2D into buffer b once window i-2 (the last user of b) finished computing
+            self.compute_done[(self.i - self.max_ahead) % self.nb].synchronize()
+        # H2D into buffer b once window i-nb (the last user of b) finished computing
         cs.wait_event(self.compute_done[b])
         if w.pod_table is not None:
             key = (w.pod_table.shape[0], hash(w.pod_table.tobytes()))
@@ -382,15 +419,23 @@ class WindowPipeline:
                 self.ctx_dev[self.ctx_uploaded: w.n_ctx].copy_(w.ctx_rows[self.ctx_uploaded: w.n_ctx],
                                                                non_blocking=True)
                 self.ctx_uploaded = w.n_ctx
-            nb = w.n_events * w.wire
+            nb = w.n_events * records.wire_bytes(w.wire)
             self.ev_dev[b][:nb].copy_(w.ev[:nb], non_blocking=True)
             if tr: tr.append(time.perf_counter())
-            self.sp_dev[b][: w.n_spans * 64].copy_(w.sp[: w.n_spans * 64], non_blocking=True)
-            if tr: tr.append(time.perf_counter())
-            self.counts_dev[b].copy_(w.counts, non_blocking=True)
-            if tr: tr.append(time.perf_counter())
-            self.labels_dev[b].copy_(w.labels, non_blocking=True)
-            if tr: tr.append(time.perf_counter())
+            if w.aux is not None and w.aux.numel() >= self.aux_head and \
+                    w.counts.data_ptr() == w.aux.data_ptr() and w.sp.data_ptr() == w.aux.data_ptr() + self.aux_head:
+                # packed block: counts, labels and spans in one DMA (a copy has a fixed
+                # ~10 us cost on the copy engine, paid per window on the critical path)
+                na = self.aux_head + w.n_spans * 64
+                self.aux_dev[b][:na].copy_(w.aux[:na], non_blocking=True)
+                if tr: tr.extend([time.perf_counter()] * 3)
+            else:
+                self.sp_dev[b][: w.n_spans * 64].copy_(w.sp[: w.n_spans * 64], non_blocking=True)
+                if tr: tr.append(time.perf_counter())
+                self.counts_dev[b].copy_(w.counts, non_blocking=True)
+                if tr: tr.append(time.perf_counter())
+                self.labels_dev[b].copy_(w.labels, non_blocking=True)
+                if tr: tr.append(time.perf_counter())
             self.h2d_done[b].record(cs)
         if tr:
             tr.append(time.perf_counter())
@@ -400,9 +445,9 @@ class WindowPipeline:
         ks.wait_event(self.h2d_done[b])
         ks.wait_event(self.comm_done[b])  # packet[b] no longer being reduced / read
         with torch.cuda.stream(ks):
-            if self.device_refit and self.i >= 2:
-                # fold window i-2's all-reduced statistics (packet[b], complete per the wait
-                # above) and refit before window i: deterministic prequential lag of 2
+            if self.device_refit and self.i >= self.nb:
+                # fold window i-nb's all-reduced statistics (packet[b], complete per the wait
+                # above) and refit before window i: deterministic prequential lag of nb
                 n = self.stats_acc.numel()
                 self.stats_acc.add_(self.packet_dev[b][self.stats_off:self.stats_off + n])
                 self.eng.refit_nb(self.stats_acc, self.p0_dev, 2.0, 1.0, N_DOMAINS)
@@ -444,7 +489,7 @@ class WindowPipeline:
         # fold window i-2 (this call's predecessor's predecessor is certainly far along;
         # folding i-1 would stall the host on the window just queued)
         if self.i >= 2 and self.learn and not self.device_refit:
-            pb = (self.i - 2) % 2
+            pb = (self.i - 2) % self.nb
             self.comm_done[pb].synchronize()
             pk = unpack_packet(self.packet_host[pb].numpy())
             self.cum_stats = self.cum_stats.merge(stats_from_packet(pk))
@@ -486,7 +531,7 @@ class WindowPipeline:
 
     def last_packet(self) -> Dict[str, np.ndarray]:
         """Unpacked (all-reduced) packet of the most recently submitted window (after drain)."""
-        b = (self.i - 1) % 2
+        b = (self.i - 1) % self.nb
         self.comm_done[b].synchronize()
         return unpack_packet(self.packet_host[b].numpy().copy())
 

@@ -1,5 +1,5 @@
-/* Host-side check that struct mislo_event / mislo_event32 match collector/records.py EVENT /
- * EVENT32, and that mislo_milli agrees with records.py milli_int on boundary values. */
+/* Host-side check that struct mislo_event / mislo_event32 / mislo_event24 / mislo_event20t match
+ * collector/records.py EVENT / EVENT32 / EVENT24 / EVENT20T, and that mislo_milli agrees with records.py milli_int on boundary values. */
 #include <stddef.h>
 #include <stdio.h>
 
@@ -42,7 +42,14 @@ int main(void)
 		printf("bad mislo_event24 layout\n");
 		return 1;
 	}
-	printf("mislo_event layout ok (64 bytes), mislo_event32 ok (32 bytes), mislo_event24 ok (24 bytes)\n");
+	if (sizeof(struct mislo_event20t) != 20 || offsetof(struct mislo_event20t, ts_ns) != 0 ||
+	    offsetof(struct mislo_event20t, value_milli) != 8 || offsetof(struct mislo_event20t, ctx_type) != 12 ||
+	    offsetof(struct mislo_event20t, trace_id) != 16 || _Alignof(struct mislo_event20t) != 4) {
+		printf("bad mislo_event20t layout\n");
+		return 1;
+	}
+	printf("mislo_event layout ok (64 bytes), mislo_event32 ok (32 bytes), mislo_event24 ok (24 bytes), "
+	       "mislo_event20t ok (20 bytes)\n");
 	/* fixed-point rule: print "type value milli" lines for the Python side to compare */
 	static const unsigned long long vals[] = {0, 499, 500, 501, 1500, 2500, 2501, 4294967, 4294968,
 						   4294967295ull, 4294967296ull, 4294967295500ull, 4294967296500ull};

@@ -2,13 +2,18 @@
  *
  * Every probe object shares these maps, pinned by name under /sys/fs/bpf so the agent's
  * loader opens them once:
- *   mislo_events  BPF ring buffer of 24-byte mislo_event24 records (32-byte mislo_event32
- *                 with -DMISLO_RING_EVENT32) that the agent drains into the GPU window ring
- *                 (16 MiB);
+ *   mislo_events  BPF ring buffer of 20-byte mislo_event20t records (24-byte mislo_event24
+ *                 with -DMISLO_RING_EVENT24, 32-byte mislo_event32 with -DMISLO_RING_EVENT32)
+ *                 that the agent drains into the GPU window ring (16 MiB);
  *   mislo_cfg     array: [0] realtime - monotonic offset (ns), [1] node id,
  *                 [2 + type] per-signal emit floor (raw units; the overhead guard raises
- *                 floors before it detaches probes), [126] context id counter,
- *                 [127] connection id counter;
+ *                 floors before it detaches probes), [125] trace id counter,
+ *                 [126] context id counter, [127] connection id counter;
+ *   mislo_traces  LRU trace hash -> 32-bit trace id (event20t rings). Trace ids are per request
+ *                 and never reused within 2^32 - 1 assignments; LRU eviction only drops traces
+ *                 idle for far longer than the 2 s correlation window. The agent looks up the
+ *                 window's span trace hashes here (spans of traces no probe saw get ids from
+ *                 a disjoint range and match nothing, as they should);
  *   mislo_pods    cgroup id -> pod id (agent-populated from the kubelet / CRI);
  *   mislo_conns   connection key -> 24-bit connection id, assigned here on first sight; the
  *                 agent reads it (batch lookup, per window) to put spans on the same ids;
@@ -38,6 +43,7 @@
 #define MISLO_CFG_NODE 1
 #define MISLO_CFG_FLOOR(t) (2 + (t))
 #define MISLO_CFG_SLOTS 128
+#define MISLO_CFG_TRACE_NEXT 125
 #define MISLO_CFG_CTX_NEXT 126
 #define MISLO_CFG_CONN_NEXT 127
 #define MISLO_CONN_ID_LIMIT (1u << 24)
@@ -45,6 +51,14 @@
 struct mislo_ctx_key {
 	__u32 pod_id, pid, conn_id, pad;
 };
+
+struct {
+	__uint(type, BPF_MAP_TYPE_LRU_HASH);
+	__uint(max_entries, 1 << 20);
+	__type(key, __u64);
+	__type(value, __u32);
+	__uint(pinning, LIBBPF_PIN_BY_NAME);
+} mislo_traces SEC(".maps");
 
 struct {
 	__uint(type, BPF_MAP_TYPE_RINGBUF);
@@ -186,6 +200,27 @@ static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 conn_id
 	return MISLO_INTERN(mislo_ctxs, &k, MISLO_CFG_CTX_NEXT);
 }
 
+/* trace hash -> 32-bit id in [1, 2^32 - 1] (wrapping), assigned on first sight like
+ * MISLO_INTERN; 0 for untraced events */
+static __always_inline __u32 mislo_trace_id(__u64 h)
+{
+	if (!h)
+		return 0;
+	__u32 *id = bpf_map_lookup_elem(&mislo_traces, &h);
+	if (id)
+		return *id;
+	__u32 idx = MISLO_CFG_TRACE_NEXT;
+	__u64 *next = bpf_map_lookup_elem(&mislo_cfg, &idx);
+	if (!next)
+		return 0;
+	__u64 fresh = __sync_fetch_and_add(next, 1);
+	__u32 v = (__u32)(fresh % 0xFFFFFFFFull) + 1;
+	if (bpf_map_update_elem(&mislo_traces, &h, &v, BPF_NOEXIST) == 0)
+		return v;
+	id = bpf_map_lookup_elem(&mislo_traces, &h);
+	return id ? *id : 0;
+}
+
 /* Pack the working record into the ring record and publish it. */
 static __always_inline void mislo_submit(struct mislo_event *e)
 {
@@ -198,12 +233,18 @@ static __always_inline void mislo_submit(struct mislo_event *e)
 	r.pid = e->pid;
 	r.pod_id = e->pod_id;
 	r.type_conn = (e->signal_type & 0xFFu) | (cid << 8);
-#else
+#elif defined(MISLO_RING_EVENT24)
 	struct mislo_event24 r;
 	r.ts_ns = e->ts_ns;
 	r.trace_h = e->trace_h;
 	r.value_milli = mislo_milli(e->signal_type, e->value);
 	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
+#else
+	struct mislo_event20t r;
+	r.ts_ns = e->ts_ns;
+	r.value_milli = mislo_milli(e->signal_type, e->value);
+	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
+	r.trace_id = mislo_trace_id(e->trace_h);
 #endif
 	bpf_ringbuf_output(&mislo_events, &r, sizeof(r), 0);
 }

@@ -3,8 +3,12 @@
  * layout test.
  *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record and
  *                        the user-space producers' ring record;
- *   struct mislo_event24 (24 B, records.py EVENT24): what the probes put on the BPF ring
- *                        (default). The kernel converts the value to fixed point
+ *   struct mislo_event20t (20 B, records.py EVENT20T): what the probes put on the BPF ring
+ *                        (default): mislo_event24 with the trace hash interned in the kernel
+ *                        too (mislo_probe.h mislo_trace_id; the agent maps span trace ids
+ *                        through the same map), 5/16 of the 64-byte record's PCIe bytes;
+ *   struct mislo_event24 (24 B, records.py EVENT24): the ring record with -DMISLO_RING_EVENT24.
+ *                        The kernel converts the value to fixed point
  *                        (mislo_milli) and interns the connection and the (pod, pid, conn)
  *                        context (mislo_probe.h mislo_conn_id / mislo_ctx_id), so the agent
  *                        DMAs ring bytes to the GPU without touching a record: 3/8 of the PCIe
@@ -78,6 +82,14 @@ struct mislo_event24 {
 	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
 	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
 };
+
+/* 4-byte aligned: ring records are packed back to back at 20-byte strides */
+struct mislo_event20t {
+	__s64 ts_ns;       /* CLOCK_REALTIME ns */
+	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
+	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
+	__u32 trace_id;    /* interned trace id (mislo_trace_id), 0 = none */
+} __attribute__((packed, aligned(4)));
 
 /* value_milli = raw * 10^shift: the catalogue's decode scales are powers of ten
  * (signals/catalog.py decode_scale; records.py milli_shift_table is the same table). */

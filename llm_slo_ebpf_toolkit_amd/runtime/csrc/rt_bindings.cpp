@@ -161,7 +161,8 @@ class PyWireEncoder {
     const size_t nb = (size_t)ei.size * ei.itemsize;
     if (nb % sizeof(mislo::EventRec)) throw std::invalid_argument("events: not a whole number of 64-byte records");
     const size_t n = nb / sizeof(mislo::EventRec);
-    if ((size_t)oi.size * oi.itemsize < n * (size_t)wire) throw std::invalid_argument("out buffer too small");
+    if ((size_t)oi.size * oi.itemsize < n * (size_t)mislo::wire_bytes(wire))
+      throw std::invalid_argument("out buffer too small");
     py::gil_scoped_release nogil;
     return enc_->encode(static_cast<const mislo::EventRec*>(ei.ptr), n, oi.ptr, wire);
   }

@@ -235,7 +235,20 @@ int64_t WireEncoder::encode(const EventRec* ev, size_t n, void* out, int wire) {
     }
     return 0;
   }
-  if (wire != 20 && wire != 16) throw std::invalid_argument("wire must be 32, 24, 20 or 16");
+  if (wire == kWire20T) {
+    Event20T* o = static_cast<Event20T*>(out);
+    for (size_t i = 0; i < n; ++i) {
+      const EventRec& e = ev[i];
+      const uint32_t st = e.signal_type;
+      const uint64_t ck = conn_key(e);
+      if (ck) conn_id(ck);
+      const uint32_t ctx = ctx_id(e.pod_id, e.pid, ck, ((uint32_t)e.svc_id << 16) | e.node_id);
+      o[i] = Event20T{e.ts_ns, milli_int(e.value, st < 256 ? shift_[st] : 3), (st & 0xFFu) | (ctx << 8),
+                      traces_.id(e.trace_h, gen_)};
+    }
+    return 0;
+  }
+  if (wire != 20 && wire != 16) throw std::invalid_argument("wire must be 32, 24, 21, 20 or 16");
   int64_t t_base = std::numeric_limits<int64_t>::max(), t_max = std::numeric_limits<int64_t>::min();
   for (size_t i = 0; i < n; ++i) {
     const int64_t t = ev[i].ts_ns;

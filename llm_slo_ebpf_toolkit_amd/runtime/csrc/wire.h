@@ -70,6 +70,16 @@ struct Event24 {  // collector/records.py EVENT24 = probes/ebpf/mislo_record.h m
 };
 static_assert(sizeof(Event24) == 24, "Event24 is 24 bytes");
 
+#pragma pack(push, 4)
+struct Event20T {  // collector/records.py EVENT20T = probes/ebpf/mislo_record.h mislo_event20t (wire code 21)
+  int64_t ts_ns;
+  uint32_t value_milli, ctx_type, trace_id;
+};
+#pragma pack(pop)
+static_assert(sizeof(Event20T) == 20, "Event20T is 20 bytes");
+constexpr int kWire20T = 21;
+inline int wire_bytes(int wire) { return wire == kWire20T ? 20 : wire; }
+
 struct Event32 {  // collector/records.py EVENT32 = probes/ebpf/mislo_record.h mislo_event32
   int64_t ts_ns;
   uint64_t trace_h;
@@ -219,8 +229,9 @@ class WireEncoder {
   explicit WireEncoder(const int8_t* shift256);
 
   // Encodes n events into `out` (wire 20 or 16). Returns t_base (earliest non-zero ts).
-  // Throws std::range_error if the window spans >= 2^32 - 1 ns. wire 32 / 24 write Event32 /
-  // Event24 (the records the probes emit: absolute ts; interned connection / context ids) and
+  // Throws std::range_error if the window spans >= 2^32 - 1 ns. wire 32 / 24 / 21 write Event32 /
+  // Event24 / Event20T (the records the probes emit: absolute ts; interned connection / context
+  // ids; Event20T also interned trace ids, shared with encode_spans(trace_ids = true)) and
   // return 0.
   int64_t encode(const EventRec* ev, size_t n, void* out, int wire);
   // Spans keep the 64-byte layout: conn hash -> conn id; with trace_ids, trace -> id.

@@ -190,6 +190,43 @@ def test_wire20_matches_oracle(engine):
     assert int(e.misc[1].item()) == 1  # the zero timestamp
 
 
+def test_wire20t_matches_oracle(engine):
+    """EVENT20T (the probes' default 20-byte ring record, interned trace ids, 4-byte aligned at
+    20-byte strides) -> GPU decode + join == numpy oracle, zero timestamp included."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+
+    win = small_window(seed=21)
+    engine.set_join_params(2000.0, 0.7, 3, 1)
+    engine.set_model(NaiveBayes.ref())
+    conns, ctxs, traces = records.ConnInterner(), records.CtxInterner(), records.TraceInterner()
+    ev = win.events.copy()
+    ev["ts_ns"][5] = 0
+    e20 = records.to_wire20t(ev, conns, ctxs, traces)
+    sp = records.wire_spans(win.spans, conns, traces)
+    engine.set_ctx_table(ctxs.table())
+    engine.stage(e20, sp, win.n_groups, win.group_labels)
+    assert engine.wire == records.WIRE_20T
+    engine.upload()
+    engine.run(True, False)
+    out = engine.outputs()
+    e = engine.eng
+    d = oracle.decode_w20t(e20, ctxs.table())
+    N, S = win.n_events, win.n_spans
+    np.testing.assert_array_equal(rows(e, N)["ts"], d.ts)
+    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
+    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
+    np.testing.assert_array_equal(rows(e, N)["pid"], d.pid)
+    np.testing.assert_array_equal(rows(e, N)["svcnode"], d.svcnode)
+    ref = oracle.join(d, sp, win.n_groups)
+    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
+    np.testing.assert_array_equal(top3, ref.top3)
+    np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
+    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
+        assert out.debug[k] == ref.debug[k], k
+    np.testing.assert_array_equal(out.feat, ref.feat)
+    assert int(e.misc[1].item()) == 1  # the zero timestamp
+
+
 def test_wire16_native_matches_oracle(engine):
     """Native encoder (EVENT16, interned trace ids) -> GPU decode + join == numpy oracle."""
     from llm_slo_ebpf_toolkit_amd.collector import records
@@ -298,7 +335,7 @@ def test_pipeline_wire20_equals_wire32():
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(3)]
     sums = {}
-    for wire in (32, 20, 16):
+    for wire in (32, 21, 20, 16):
         it, enc = records.ConnInterner(), records.native_encoder()
         staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 8, w.group_domains, wire=wire,
                                interner=it, encoder=enc) for w in wins]
@@ -306,14 +343,14 @@ def test_pipeline_wire20_equals_wire32():
         for i in range(6):
             pipe.submit(staged[i % 3])
         sums[wire] = pipe.summary()
-    for wire in (20, 16):
+    for wire in (21, 20, 16):
         for k in ("confusion", "hist", "status", "dbg", "misc"):
             np.testing.assert_array_equal(sums[wire][k], sums[32][k], err_msg=f"{wire} {k}")
 
 
 @pytest.mark.gpu
 def test_wire_stager_matches_prestaged_windows():
-    """bench.py's per-step staging (WireStager: probe-native EVENT32 / EVENT24 rings + span mapping,
+    """bench.py's per-step staging (WireStager: probe-native EVENT32 / EVENT24 / EVENT20T rings + span mapping,
     pooled 16/20-byte encoding, pinned 64-byte ring) reproduces the totals of windows staged
     up front with stage_window."""
     import torch
@@ -342,7 +379,7 @@ def test_wire_stager_matches_prestaged_windows():
         if wire == 64:
             ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
                      torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-        elif wire in (24, 32):
+        elif wire in (21, 24, 32):
             ring = [(st.probe_records(w.events), None) for w in wins]
         else:
             ring = [(None, None)] * 3
@@ -354,7 +391,7 @@ def test_wire_stager_matches_prestaged_windows():
 
     keys = ("confusion", "hist", "status", "dbg", "misc")
     ref32 = totals_prestaged(32)
-    for wire in (32, 24, 20, 16):
+    for wire in (32, 24, 21, 20, 16):
         got = totals_stager(wire)
         for k in keys:
             np.testing.assert_array_equal(got[k], ref32[k], err_msg=f"stager {wire} {k}")

@@ -258,3 +258,47 @@ def test_event24_native_numpy_and_join():
     np.testing.assert_array_equal(full.top3, j24.top3)
     np.testing.assert_array_equal(full.cnt, j24.cnt)
     assert full.debug == j24.debug
+
+
+def test_event20t_native_numpy_and_join():
+    """EVENT20T (the probes' default ring record: kernel-interned contexts and trace ids, 20 bytes
+    at 20-byte strides): native == records.to_wire20t up to id numbering, spans carry the same
+    trace ids, and its decode joins exactly like the 64-byte records."""
+    pytest = __import__("pytest")
+    try:
+        enc = records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    assert records.EVENT20T.itemsize == 20 and records.wire_bytes(records.WIRE_20T) == 20
+    assert records.wire_code(records.EVENT20T) == records.WIRE_20T and records.wire_code(records.EVENT20) == 20
+    win = _win(seed=13)
+    ev = win.events
+    buf = np.zeros(ev.shape[0] * 20, np.uint8)
+    assert enc.encode(ev, buf, records.WIRE_20T) == 0
+    n20 = buf.view(records.EVENT20T)
+    conns, ctxs, traces = records.ConnInterner(), records.CtxInterner(), records.TraceInterner()
+    r20 = records.to_wire20t(ev, conns, ctxs, traces)
+    for f in ("ts_ns", "value_milli"):
+        np.testing.assert_array_equal(n20[f], r20[f], err_msg=f)
+    # trace ids: same partition of the events (0 exactly for untraced ones)
+    np.testing.assert_array_equal(n20["trace_id"] == 0, ev["trace_h"] == 0)
+    pairs = set(zip(n20["trace_id"].tolist(), ev["trace_h"].tolist()))
+    assert len(pairs) == len(set(ev["trace_h"].tolist()))
+    a = oracle.decode_w20t(n20, enc.ctx_table())
+    b = oracle.decode_w20t(r20, ctxs.table())
+    for f in ("ts", "slot", "pod", "pid", "svcnode"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    sp = np.zeros_like(win.spans)
+    enc.encode_spans(win.spans, sp, True)
+    ids = dict(zip(ev["trace_h"].tolist(), n20["trace_id"].tolist()))
+    for h, t in zip(win.spans["trace_h"].tolist(), sp["trace_h"].tolist()):
+        if h in ids:
+            assert t == ids[h]
+    full = oracle.join(oracle.decode_events(ev), win.spans, win.n_groups)
+    j20 = oracle.join(a, sp, win.n_groups)
+    np.testing.assert_array_equal(full.top3, j20.top3)
+    np.testing.assert_array_equal(full.cnt, j20.cnt)
+    assert full.debug == j20.debug
+    jr = oracle.join(b, records.wire_spans(win.spans, conns, traces), win.n_groups)
+    np.testing.assert_array_equal(full.top3, jr.top3)
+    assert full.debug == jr.debug
