@@ -389,14 +389,24 @@ class Engine {
 
   // On-device learned-NB refit from accumulated stats ([32*32 + 16] f64) and the
   // random-init prior table p0 ([16*16] f64); rewrites the model in place (stream order).
-  void refit_nb(torch::Tensor stats_acc, torch::Tensor p0, double alpha, double prior_pseudo, int64_t n_dom) {
+  // add (optional, f64[1040]): statistics folded into stats_acc first, in the same launch.
+  void refit_nb(torch::Tensor stats_acc, torch::Tensor p0, double alpha, double prior_pseudo, int64_t n_dom,
+                c10::optional<torch::Tensor> add) {
     check_cuda(stats_acc, "stats_acc");
     check_cuda(p0, "p0");
-    if (stats_acc.scalar_type() != torch::kFloat64 || stats_acc.numel() < 32 * 32 + kMaxDomains)
-      throw std::invalid_argument("stats_acc must be f64[1040]");
+    if (stats_acc.scalar_type() != torch::kFloat64 || stats_acc.numel() < 32 * 32 + kMaxDomains ||
+        !stats_acc.is_contiguous())
+      throw std::invalid_argument("stats_acc must be contiguous f64[1040]");
     if (p0.scalar_type() != torch::kFloat64 || p0.numel() < kSlots * 16) throw std::invalid_argument("p0: f64[256]");
     if (n_dom < 1 || n_dom > kMaxDomains) throw std::invalid_argument("n_dom out of range");
-    launch_refit_nb(stats_acc.data_ptr<double>(), p0.data_ptr<double>(), alpha, prior_pseudo, (int)n_dom,
+    const double* addp = nullptr;
+    if (add && add->defined()) {
+      check_cuda(*add, "add");
+      if (add->scalar_type() != torch::kFloat64 || add->numel() < 32 * 32 + kMaxDomains || !add->is_contiguous())
+        throw std::invalid_argument("add must be contiguous f64[1040]");
+      addp = add->data_ptr<double>();
+    }
+    launch_refit_nb(stats_acc.data_ptr<double>(), addp, p0.data_ptr<double>(), alpha, prior_pseudo, (int)n_dom,
                     reinterpret_cast<PosteriorModel*>(model.data_ptr()), cur_stream());
   }
 
@@ -526,7 +536,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("run_window", &Engine::run_window, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
            py::arg("with_labels") = true, py::arg("learn") = false, py::arg("wire") = 64)
       .def("refit_nb", &Engine::refit_nb, py::arg("stats_acc"), py::arg("p0"), py::arg("alpha") = 2.0,
-           py::arg("prior_pseudo") = 1.0, py::arg("n_dom") = 10)
+           py::arg("prior_pseudo") = 1.0, py::arg("n_dom") = 10, py::arg("add") = py::none())
       .def("run_window_pre", &Engine::run_window_pre, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
            py::arg("wire") = 64)
       .def("run_window_post", &Engine::run_window_post, py::arg("n_groups"), py::arg("with_labels") = true,

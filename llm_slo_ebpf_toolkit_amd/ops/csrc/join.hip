@@ -42,31 +42,39 @@ constexpr int kChunk = 256;   // spans staged in LDS per pass
 // partition scan + scatter
 // ---------------------------------------------------------------------------------------
 
-// part_blk[b][c] counts -> part_off[b][c] exclusive prefix over blocks, part_tot[c]
-__global__ __launch_bounds__(256) void k_part_scan(const uint32_t* __restrict__ part_blk, int nblk,
-                                                   uint32_t* __restrict__ part_off, uint32_t* __restrict__ part_tot) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= kKeyTypes * kParts) return;
-  uint32_t run = 0;
-  constexpr int U = 8;  // independent loads in flight per thread
-  int b = 0;
-  for (; b + U <= nblk; b += U) {
-    uint32_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = part_blk[(size_t)(b + u) * kKeyTypes * kParts + c];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      part_off[(size_t)(b + u) * kKeyTypes * kParts + c] = run;
-      run += v[u];
-    }
+// part_blk[b][c] counts -> part_off[b][c] exclusive prefix over blocks, part_tot[c].
+// A column scan over the [nblk][4096] matrix. One thread per column left 64 waves on the
+// whole chip, each walking 256 dependent rows; here a workgroup owns kScanCols columns and
+// splits the rows into kScanRG groups: pass 1 sums each group (independent loads, 32 rows
+// of a wave read 128 contiguous bytes each), the group prefixes go through LDS, pass 2
+// rewrites the group's rows as running offsets.
+constexpr int kScanCols = 32, kScanRG = 32;
+__global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_t* __restrict__ part_blk, int nblk,
+                                                                  uint32_t* __restrict__ part_off,
+                                                                  uint32_t* __restrict__ part_tot) {
+  __shared__ uint32_t s_sum[kScanRG][kScanCols];
+  const int cl = threadIdx.x % kScanCols, r = threadIdx.x / kScanCols;
+  const int c = blockIdx.x * kScanCols + cl;
+  const int per = (nblk + kScanRG - 1) / kScanRG;
+  const int b0 = min(nblk, r * per), b1 = min(nblk, b0 + per);
+  constexpr size_t W = (size_t)kKeyTypes * kParts;
+  uint32_t sum = 0;
+  for (int b = b0; b < b1; ++b) sum += part_blk[(size_t)b * W + c];
+  s_sum[r][cl] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (int q = 0; q < kScanRG; ++q) {
+    const uint32_t v = s_sum[q][cl];
+    run += q < r ? v : 0u;
+    tot += v;
   }
-  for (; b < nblk; ++b) {
-    const size_t idx = (size_t)b * kKeyTypes * kParts + c;
+  for (int b = b0; b < b1; ++b) {
+    const size_t idx = (size_t)b * W + c;
     const uint32_t v = part_blk[idx];
     part_off[idx] = run;
     run += v;
   }
-  part_tot[c] = run;
+  if (r == 0) part_tot[c] = tot;
 }
 
 // exclusive scan of the 4096 partition totals (one workgroup of 1024 threads, 4 each)
@@ -175,20 +183,35 @@ struct alignas(16) SpanPP {
 };
 
 constexpr int kLdsGroups = 64;
-constexpr int kSigPerItem = 2048;  // signals per work item (a partition's list is sliced)
+constexpr int kSigPerItem = 4096;  // signals per work item (a partition's list is sliced); sweep: 256 498 us of compute, 1024 389, 2048 352, 4096 330, 8192 368 (staging repeats per item vs load balance)
 
 // Work list for the two probe phases, rebuilt every window on the device (no host sync,
 // graph-capturable). One workgroup of 1024 threads, one partition per thread:
 //   work[0] / work[1]: item counts of phase 1 (trace) / phase 2 (pod+pid, pod+conn, svc+node)
 //   work[2] / work[3]: dequeue counters (zeroed here)
 //   items: code = key type << 28 | partition << 16 | slice << 8 | n slices.
-// Empty partitions get no item, so probe workgroups never wake for them; phase-2 items are
-// ordered by key type (enumerating tiers first, the count-only tier last).
+// Empty partitions get no item, so probe workgroups never wake for them. Phase-2 items are
+// placed longest first (LPT): a counting sort on an estimated cost class. The phase is a few
+// thousand items of very different sizes (a staging cost per item, then up to kSigPerItem
+// signals at a per-key-type rate) dequeued by 1024 workgroups, so its makespan is set by the
+// big items that start last; in key-type order the pod+conn items (the most expensive per
+// signal) came after every pod+pid item and the phase ran ~2x its average load (probe
+// profile). Results do not depend on item order: top-3 insertion is an atomic-min cascade
+// and every count / sum is an integer atomic.
+__device__ __forceinline__ uint32_t probe_item_class(int k, uint32_t n_sig, uint32_t n_span) {
+  // cycles, fitted to the MISLO_PROBE_PROFILE counters (stage ~30 k, per-signal 40-90)
+  constexpr uint32_t kPerSig[kKeyTypes] = {90, 40, 85, 60};
+  const uint32_t cost = 24000u + 64u * min(n_span, 256u) + n_sig * kPerSig[k];
+  return min(cost >> 13, 63u);
+}
+
 __global__ __launch_bounds__(1024) void k_probe_work(const uint32_t* __restrict__ span_base,
                                                      const uint32_t* __restrict__ sig_base, int sig_per_item,
                                                      uint32_t* __restrict__ work) {
   __shared__ unsigned long long s[1024];
+  __shared__ uint32_t s_cls[64];
   const int p = threadIdx.x;
+  if (p < 64) s_cls[p] = 0u;
   uint32_t n[kKeyTypes];
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
@@ -217,13 +240,38 @@ __global__ __launch_bounds__(1024) void k_probe_work(const uint32_t* __restrict_
   uint32_t* items1 = work + 4;
   uint32_t* items2 = work + 4 + kParts * kProbeMaxSplit;
   for (uint32_t j = 0; j < n[0]; ++j) items1[e[0] + j] = (0u << 28) | ((uint32_t)p << 16) | (j << 8) | n[0];
-  uint32_t base = 0;
+  // phase 2: count items per cost class (slot 0 = most expensive), scan, place
+  uint32_t ns[kKeyTypes], ng[kKeyTypes];
 #pragma unroll
   for (int k = 1; k < kKeyTypes; ++k) {
-    for (uint32_t j = 0; j < n[k]; ++j)
-      items2[base + e[k] + j] = ((uint32_t)k << 28) | ((uint32_t)p << 16) | (j << 8) | n[k];
-    base += t[k];
+    const int c = k * kParts + p;
+    ns[k] = span_base[c + 1] - span_base[c];
+    ng[k] = sig_base[c + 1] - sig_base[c];
   }
+  auto slice = [&](int k, uint32_t j) {  // signals of slice j (k_probe's split rule)
+    const uint32_t per = (ng[k] + n[k] - 1) / n[k];
+    const uint32_t a = j * per;
+    return a >= ng[k] ? 0u : min(ng[k], a + per) - a;
+  };
+#pragma unroll
+  for (int k = 1; k < kKeyTypes; ++k)
+    for (uint32_t j = 0; j < n[k]; ++j) atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, j), ns[k])], 1u);
+  __syncthreads();
+  if (p == 0) {
+    uint32_t run = 0;
+    for (int q = 0; q < 64; ++q) {
+      const uint32_t v = s_cls[q];
+      s_cls[q] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 1; k < kKeyTypes; ++k)
+    for (uint32_t j = 0; j < n[k]; ++j) {
+      const uint32_t pos = atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, j), ns[k])], 1u);
+      items2[pos] = ((uint32_t)k << 28) | ((uint32_t)p << 16) | (j << 8) | n[k];
+    }
   if (p == 0) {
     work[0] = t[0];
     work[1] = t[1] + t[2] + t[3];
@@ -771,9 +819,17 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
   }
 }
 
-// Sum the incident-sum stripes into stripe 0 (exact integers: order-free).
+__device__ __forceinline__ float group_feature(unsigned long long sum, uint32_t c) {
+  // exact integer sums of milli-unit values: deterministic under any atomic order and
+  // associative across ranks (the group-sum all-reduce); oracle.join computes the same
+  return c ? (float)(((double)sum * 1e-3) / (double)c) : __builtin_nanf("");
+}
+
+// Sum the incident-sum stripes into stripe 0 (exact integers: order-free) and write the
+// rank-local incident features in the same pass (global scope recomputes them from the
+// all-reduced sums with k_group_features).
 __global__ __launch_bounds__(256) void k_fold_groups(int n, unsigned long long* __restrict__ gsum,
-                                                     uint32_t* __restrict__ gcnt) {
+                                                     uint32_t* __restrict__ gcnt, float* __restrict__ feat) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   unsigned long long s = gsum[i];
@@ -785,16 +841,14 @@ __global__ __launch_bounds__(256) void k_fold_groups(int n, unsigned long long* 
   }
   gsum[i] = s;
   gcnt[i] = c;
+  feat[i] = group_feature(s, c);
 }
 
 __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned long long* __restrict__ gsum,
                                                         const uint32_t* __restrict__ gcnt, float* __restrict__ feat) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const uint32_t c = gcnt[i];
-  // exact integer sums of milli-unit values: deterministic under any atomic order and
-  // associative across ranks (the group-sum all-reduce); oracle.join computes the same
-  feat[i] = c ? (float)(((double)gsum[i] * 1e-3) / (double)c) : __builtin_nanf("");
+  feat[i] = group_feature(gsum[i], gcnt[i]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -804,10 +858,13 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream) {
-  hipLaunchKernelGGL(k_part_scan, dim3((kKeyTypes * kParts + 255) / 256), dim3(256), 0, stream, part_blk, nblk,
-                     part_off, part_tot);
+  static_assert((kKeyTypes * kParts) % kScanCols == 0, "scan columns tile the partition matrix");
+  hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
+                     part_blk, nblk, part_off, part_tot);
   hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(1024), 0, stream, part_tot, part_base);
-  hipLaunchKernelGGL((k_scatter<256>), dim3(nblk), dim3(256), 0, stream, codes, n_dev, cap, part_off, part_base,
+  // 1024 threads per workgroup: the grid is one workgroup per decode block (<= 256), so 256
+  // threads left 4 waves per CU to hide the scattered stores and LDS atomics
+  hipLaunchKernelGGL((k_scatter<1024>), dim3(nblk), dim3(1024), 0, stream, codes, n_dev, cap, part_off, part_base,
                      items);
 }
 
@@ -842,8 +899,7 @@ void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* 
                      cnt, gc, sc, jp, base_attrs, attrs, conf, kernel_ms, n_groups, gsum, gcnt, dbg);
   if (n_groups > 0) {
     const int n = n_groups * kSlots;
-    hipLaunchKernelGGL(k_fold_groups, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt);
-    hipLaunchKernelGGL(k_group_features, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt, feat);
+    hipLaunchKernelGGL(k_fold_groups, dim3((n + 255) / 256), dim3(256), 0, stream, n, gsum, gcnt, feat);
   }
 }
 

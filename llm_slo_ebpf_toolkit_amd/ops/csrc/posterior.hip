@@ -156,13 +156,17 @@ __global__ __launch_bounds__(NT) void k_stats(const float* __restrict__ feat, co
 // turned into the linear-logit model in place (w, bias, evidence masks). Runs on the
 // compute stream between windows, so online learning needs no host round trip.
 // stats: [32 x 32] f64 (rows 0-15 = E^T Y) followed by count[16]; p0: [16 x 16] f64.
-__global__ __launch_bounds__(256) void k_refit_nb(const double* __restrict__ stats, const double* __restrict__ p0,
-                                                  double alpha, double prior_pseudo, int n_dom,
-                                                  PosteriorModel* __restrict__ pm) {
+// add (optional, same layout): a window's all-reduced statistics, folded into stats first
+// (one launch instead of an elementwise add plus the refit on the compute stream).
+__global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, const double* __restrict__ add,
+                                                  const double* __restrict__ p0, double alpha, double prior_pseudo,
+                                                  int n_dom, PosteriorModel* __restrict__ pm) {
   __shared__ double s_logpn[kSlots][kMaxDomains];
   __shared__ uint32_t s_mask[kMaxDomains];
   const double* count = stats + 32 * 32;
   const int t = threadIdx.x;
+  if (add)
+    for (int i = t; i < 32 * 32 + kMaxDomains; i += 256) stats[i] += add[i];
   if (t < kMaxDomains) s_mask[t] = 0u;
   __syncthreads();
   {
@@ -200,9 +204,9 @@ __global__ __launch_bounds__(256) void k_refit_nb(const double* __restrict__ sta
   }
 }
 
-void launch_refit_nb(const double* stats, const double* p0, double alpha, double prior_pseudo, int n_dom,
+void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
                      PosteriorModel* pm, hipStream_t stream) {
-  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, p0, alpha, prior_pseudo, n_dom, pm);
+  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, alpha, prior_pseudo, n_dom, pm);
 }
 
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,

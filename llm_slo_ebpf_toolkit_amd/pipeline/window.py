@@ -449,8 +449,8 @@ class WindowPipeline:
                 # fold window i-nb's all-reduced statistics (packet[b], complete per the wait
                 # above) and refit before window i: deterministic prequential lag of nb
                 n = self.stats_acc.numel()
-                self.stats_acc.add_(self.packet_dev[b][self.stats_off:self.stats_off + n])
-                self.eng.refit_nb(self.stats_acc, self.p0_dev, 2.0, 1.0, N_DOMAINS)
+                self.eng.refit_nb(self.stats_acc, self.p0_dev, 2.0, 1.0, N_DOMAINS,
+                                  self.packet_dev[b][self.stats_off:self.stats_off + n])
                 self.windows_folded += 1
             self.eng.bind_io(self.counts_dev[b], self.labels_dev[b], self.packet_dev[b])
             if self.group_scope == "global" and self.pg is not None:
