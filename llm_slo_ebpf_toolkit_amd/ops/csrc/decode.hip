@@ -46,6 +46,10 @@ __device__ __forceinline__ void store_counts(const uint32_t* lds, uint32_t* dst)
 // hashed bins) keeps one copy: a wave's keys are nearly all distinct, so its conflicts are
 // random bank collisions that copies do not remove.
 struct DecodeLds {
+  // the signal tables, copied from constant memory once per workgroup: per-event lookups use
+  // a lane-varying slot, which constant memory serves as one vector load per element (15 bucket
+  // edges + thresholds + type map per event); from LDS a slot's edges are 4 ds_read_b128
+  alignas(16) Tables tab;
   static constexpr int kRep = 8, kPartRep = 1;
   static constexpr int kHS = kSlots * kBuckets + 1, kSS = kSlots * 3 + 1, kUS = kSlots + 1;
   static constexpr int kPS = kKeyTypes * kParts + 1;
@@ -57,6 +61,12 @@ struct DecodeLds {
 
 template <int NT>
 __device__ __forceinline__ void lds_init(DecodeLds& L) {
+  static_assert(sizeof(Tables) % 4 == 0 && offsetof(Tables, edges) % 16 == 0, "table layout");
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&c_tab);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&L.tab);
+    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 4); i += NT) dst[i] = src[i];
+  }
   for (int i = threadIdx.x; i < DecodeLds::kPartRep * DecodeLds::kPS; i += NT) L.part[i] = 0;
   for (int i = threadIdx.x; i < DecodeLds::kRep * DecodeLds::kUS; i += NT) L.sum[i] = 0;
   for (int i = threadIdx.x; i < DecodeLds::kRep * DecodeLds::kHS; i += NT) L.hist[i] = 0;
@@ -68,11 +78,12 @@ __device__ __forceinline__ void lds_init(DecodeLds& L) {
 struct LdsLane {
   uint32_t *hist, *status, *part;
   unsigned long long* sum;
+  const Tables* tab;
 };
 __device__ __forceinline__ LdsLane lds_lane(DecodeLds& L) {
   const int r = threadIdx.x & (DecodeLds::kRep - 1), q = threadIdx.x & (DecodeLds::kPartRep - 1);
   return LdsLane{L.hist + r * DecodeLds::kHS, L.status + r * DecodeLds::kSS, L.part + q * DecodeLds::kPS,
-                 L.sum + r * DecodeLds::kUS};
+                 L.sum + r * DecodeLds::kUS, &L.tab};
 }
 
 // sum the copies: signal / status bins and value sums merge with one global atomic per
@@ -122,18 +133,21 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
                                            int& unsupported, int& zero_ts, bool local) {
   uint8_t st = 0;
   if (slot >= 0 && local) {
-    st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
+    const Tables& t = *l.tab;
+    st = val >= t.err[slot] ? 2 : (val >= t.warn[slot] ? 1 : 0);
     // bucket = number of finite edges strictly below val ("le" semantics: val <= edge[b])
-    int b = 0;
-#pragma unroll
-    for (int e = 0; e < kBuckets - 1; ++e) b += (val > c_tab.edges[slot][e]) ? 1 : 0;
+    const float4* row = reinterpret_cast<const float4*>(t.edges[slot]);
+    const float4 r0 = row[0], r1 = row[1], r2 = row[2], r3 = row[3];
+    const int b = (val > r0.x) + (val > r0.y) + (val > r0.z) + (val > r0.w) + (val > r1.x) + (val > r1.y) +
+                  (val > r1.z) + (val > r1.w) + (val > r2.x) + (val > r2.y) + (val > r2.z) + (val > r2.w) +
+                  (val > r3.x) + (val > r3.y) + (val > r3.z);  // r3.w is the +inf overflow edge
     atomicAdd(&l.hist[slot * kBuckets + b], 1u);
     atomicAdd(&l.status[slot * 3 + st], 1u);
     // exact, order-independent integer sum (values are >= 0 by construction)
     const double milli = rint((double)val * 1000.0);
     if (milli > 0.0) atomicAdd(&l.sum[slot], (unsigned long long)milli);
   } else if (slot >= 0) {
-    st = val >= c_tab.err[slot] ? 2 : (val >= c_tab.warn[slot] ? 1 : 0);
+    st = val >= l.tab->err[slot] ? 2 : (val >= l.tab->warn[slot] ? 1 : 0);
   } else if (local) {
     ++unsupported;
   }
@@ -181,8 +195,8 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     const Event e = ev[i];
     const int st = e.signal_type;
-    const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
-    const float val = slot >= 0 ? (float)((double)e.value * (double)c_tab.scale[slot]) : (float)e.value;
+    const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
+    const float val = slot >= 0 ? (float)((double)e.value * (double)L.tab.scale[slot]) : (float)e.value;
     const uint64_t ch = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
     const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
     decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
@@ -211,7 +225,7 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     const EventC32 e = ev[i];
     const int st = (int)(e.type_conn & 0xFFu);
-    const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
+    const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
     const float val = (float)((double)e.value_milli * 1e-3);
     const uint64_t ch = (uint64_t)(e.type_conn >> 8);
     const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
@@ -274,7 +288,7 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
       cx_nx = ctx_of(e_nx);
     }
     const int st = (int)(e.ctx_type & 0xFFu);
-    const int slot = st < kMaxTypes ? (int)c_tab.type_slot[st] : -1;
+    const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
     const float val = (float)((double)e.value_milli * 1e-3);
     const int64_t ts = wire_ts(e, t_base);
     const uint64_t tr = wire_trace(e);
@@ -302,7 +316,7 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     const RefEvent e = ev[i];
     const uint32_t st = e.signal_type;
-    int slot = (st >= 1 && st <= 9) ? (int)c_tab.type_slot[st] : -1;
+    int slot = (st >= 1 && st <= 9) ? (int)L.tab.type_slot[st] : -1;
     float val;
     if (st == 2 || st == 6) val = (float)e.value_ns;           // tcp count, cpu_steal raw ns
     else val = (float)((double)e.value_ns / 1e6);               // ns -> ms
