@@ -5,7 +5,7 @@ Metric (BASELINE.json): "attribution macro-F1 on fault-replay confusion matrix; 
 overhead %", reported on config 5 ("full 9 CPU + 4 GPU signals, safety governor <= 3 %
 overhead, full confusion matrix across all fault domains") plus the events/s scaling
 curve the north star asks for. One step = one 1-second collection window per GPU, from
-the records the probes wrote into the agent's pinned ring (20-byte EVENT20T by default) ->
+the records the probes wrote into the agent's pinned ring (16-byte epoch-tagged EVENT16 by default) ->
 host work (spans mapped onto the kernel's connection ids; with --wire 16/20, wire encoding
 of 64-byte records on a native worker pool) -> H2D -> decode + histograms -> LDS hash join
 -> MFMA posteriors + confusion -> MFMA sufficient statistics -> RCCL all-reduce of the
@@ -56,9 +56,11 @@ def parse():
                          "the kernels of window i - buffers")
     ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
                     help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", default="20t", choices=("16", "20", "20t", "24", "32", "64"),
-                    help="event record format on PCIe. 20t (default) / 24 / 32 / 64: the probes' ring records "
-                         "(EVENT20T: 20 bytes, kernel-interned contexts and trace ids; EVENT24: interned "
+    ap.add_argument("--wire", default="16t", choices=("16", "16t", "20", "20t", "24", "32", "64"),
+                    help="event record format on PCIe. 16t (default) / 20t / 24 / 32 / 64: the probes' ring records "
+                         "(EVENT20T: 20 bytes, kernel-interned contexts and trace ids; 16t = EVENT16: "
+                         "16 bytes, also epoch-relative timestamps with 2-bit epoch tags, 4 epochs per "
+                         "window; EVENT24: interned "
                          "contexts; EVENT32: interned connections; EVENT: 64 bytes), DMA'd from the pinned "
                          "ring as-is (no per-event host work; spans are mapped onto the kernel's connection "
                          "(and trace) ids); 16 = EVENT16 / 20 = EVENT20, encoded from 64-byte records on the "
@@ -130,12 +132,16 @@ def main() -> int:
                           max_ahead=min(a.max_ahead, a.buffers), n_buffers=a.buffers)
     threads = a.encode_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 8)
     stager = WireStager(torch, pipe, a.events, a.spans, a.services, wire=a.wire, threads=threads)
-    ring, pods = None, None
+    ring, pods, ring_bases = None, None, None
     if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
         ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
                  torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
     elif a.wire in (21, 24, 32):  # the probes' own 20/24/32-byte records (kernel-interned ids)
         ring = [(stager.probe_records(w.events), None) for w in wins]
+    elif a.wire_name == "16t":  # EVENT16 ring: epoch published every 256 ms (tags 0-3 per window)
+        r16 = [stager.probe_ring16(w.events, epoch_ns=256_000_000) for w in wins]
+        ring = [(t, None) for t, _ in r16]
+        ring_bases = [b for _, b in r16]
         # pod id -> svc|node: agent metadata (kubelet / CRI), static over the run
         pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
     log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
@@ -144,7 +150,8 @@ def main() -> int:
         w = wins[j % len(wins)]
         evp, spp = ring[j % len(wins)] if ring else (None, None)
         return stager.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
-                            ev_pinned=evp, sp_pinned=spp, pod_table=pods)
+                            ev_pinned=evp, sp_pinned=spp, pod_table=pods,
+                            bases=ring_bases[j % len(wins)] if a.wire_name == "16t" else None)
 
     def run(n, start):
         for i in range(n):
@@ -255,7 +262,7 @@ def main() -> int:
             "scenario": a.scenario,
             "wire_bytes_per_event": records.wire_bytes(a.wire),
             "wire_record": {"20t": "EVENT20T", "24": "EVENT24", "32": "EVENT32", "64": "EVENT", "20": "EVENT20",
-                            "16": "EVENT16"}[a.wire_name],
+                            "16": "EVENT16 (host-encoded)", "16t": "EVENT16 (probe ring, epoch-tagged)"}[a.wire_name],
             "device_buffers": a.buffers,
         },
         "macro_f1": round(summ["macro_f1"], 4),
@@ -270,7 +277,7 @@ def main() -> int:
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
         "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
         "host_encode_ms_per_window": round(encode_ms, 3),
-        "host_encode_threads": threads if a.wire in (16, 20) else 0,
+        "host_encode_threads": threads if a.wire_name in ("16", "20") else 0,
         "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
     }
     if rank == 0:

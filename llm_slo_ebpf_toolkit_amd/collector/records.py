@@ -65,14 +65,80 @@ EVENT20 = np.dtype({"names": ["ts_off", "ctx_type", "value_milli", "trace_h"],
 TS_ZERO = 0xFFFFFFFF  # ts_off of a zero timestamp (never joins)
 assert EVENT20.itemsize == 20
 
-# 16-byte wire record: EVENT20 with the trace hash interned to a 32-bit id shared with the
-# window's spans (TraceInterner / the native WireEncoder).
+# 16-byte record (= probes/ebpf/mislo_record.h mislo_event16 with -DMISLO_RING_EVENT16, or the
+# host encoding): EVENT20 with the trace hash interned to a 30-bit id shared with the window's
+# spans (TraceInterner / the native WireEncoder / the kernel's mislo_traces), and a 2-bit epoch
+# tag: ts = base[tag] + ts_off, the window carrying its last 4 epoch bases (counts[4..5],
+# counts[8..13]). The host encoder writes tag 0 (one base per window).
 EVENT16 = np.dtype([
-    ("ts_off", "<u4"),       # 0  ns since the window base, TS_ZERO = zero timestamp
+    ("ts_off", "<u4"),       # 0  ns since the tagged epoch base, TS_ZERO = zero timestamp
     ("ctx_type", "<u4"),     # 4  bits 0-7 signal type, 8-31 context id
     ("value_milli", "<u4"),  # 8
-    ("trace_id", "<u4"),     # 12 interned trace id, 0 = none
+    ("trace_id", "<u4"),     # 12 bits 0-29 interned trace id (0 = none), 30-31 epoch tag
 ])
+EPOCH_TAG_SHIFT = 30
+TRACE_ID_MASK = (1 << EPOCH_TAG_SHIFT) - 1
+COUNTS_LEN = 16  # per-window counts int32[16]: sizes, epoch bases, context rows (ops/csrc)
+
+
+class EpochClock:
+    """The agent's half of the EVENT16 epoch protocol (probes/ebpf/mislo_probe.h). At each window
+    cut the agent publishes epoch k into mislo_cfg[MISLO_CFG_EPOCH] as ``base | (k & 3)`` (base =
+    realtime ns rounded down to a multiple of 4) and remembers the base under tag k & 3. A probe
+    stamps ``ts - base`` with the tag of the epoch it read, so a record written across a cut
+    still names its own base; the window ships the last 4 bases (``counts_row(bases=...)``),
+    indexed by tag, and decodes records stamped up to 3 cuts late exactly."""
+
+    def __init__(self):
+        self.k = -1
+        self._bases = [0, 0, 0, 0]
+
+    def publish(self, now_ns: int) -> int:
+        """Start epoch k+1 at ``now_ns``; returns the mislo_cfg value to write."""
+        self.k += 1
+        base = int(now_ns) & ~3
+        self._bases[self.k & 3] = base
+        return base | (self.k & 3)
+
+    def bases(self) -> tuple:
+        """Epoch bases indexed by tag (counts[4..5], [8..13])."""
+        return tuple(self._bases)
+
+    @staticmethod
+    def stamp(ts_ns: int, cfg_value: int) -> tuple:
+        """(ts_off, tag) exactly as mislo_submit computes them from a cfg value it read."""
+        base, tag = int(cfg_value) & ~3, int(cfg_value) & 3
+        if ts_ns == 0:
+            return TS_ZERO, tag
+        if ts_ns < base:
+            return 0, tag
+        d = ts_ns - base
+        return (TS_ZERO - 1 if d >= TS_ZERO else d), tag
+
+
+def retag_epochs(ev16: np.ndarray, t_base: int, period_ns: int):
+    """Re-express EVENT16 records (tag 0, offsets from ``t_base``) the way probes stamp them when
+    the agent publishes a new epoch every ``period_ns`` inside the window: epoch j = t_base +
+    j * period_ns (j <= 3), each record offset from the latest epoch at or before it, with tag j.
+    Returns (records, bases); decoding with ``bases`` gives back the same timestamps."""
+    out = ev16.copy()
+    off = ev16["ts_off"].astype(np.int64)
+    live = off != TS_ZERO
+    j = np.where(live, np.minimum(off // int(period_ns), 3), 0).astype(np.int64)
+    out["ts_off"] = np.where(live, off - j * int(period_ns), TS_ZERO).astype(np.uint32)
+    out["trace_id"] = (ev16["trace_id"].astype(np.uint32) & np.uint32(TRACE_ID_MASK)) | \
+        (j.astype(np.uint32) << np.uint32(EPOCH_TAG_SHIFT))
+    return out, tuple(int(t_base) + k * int(period_ns) for k in range(4))
+
+
+def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,), n_ctx: int = 0) -> np.ndarray:
+    """The window's counts int32[16] as the decode kernels read them: [0] events, [1] spans,
+    [2] incident groups, [3] node-local events (0 = all), [4..5] epoch base 0 (the window base),
+    [6] valid context rows, [8..9] / [10..11] / [12..13] epoch bases 1-3 (EVENT16 tags)."""
+    b = [int(x) & 0xFFFFFFFFFFFFFFFF for x in (list(bases) + [0, 0, 0, 0])[:4]]
+    v = [n_ev, n_sp, n_groups, n_local, b[0] & 0xFFFFFFFF, b[0] >> 32, n_ctx, 0,
+         b[1] & 0xFFFFFFFF, b[1] >> 32, b[2] & 0xFFFFFFFF, b[2] >> 32, b[3] & 0xFFFFFFFF, b[3] >> 32, 0, 0]
+    return np.array(v, dtype=np.uint64).astype(np.uint32).view(np.int32)
 assert EVENT16.itemsize == 16
 # 24-byte record (= probes/ebpf/mislo_record.h mislo_event24): what the probes put on the
 # ring when the kernel interns the workload context too: absolute timestamp (no window base
@@ -95,7 +161,7 @@ assert EVENT20T.itemsize == 20
 WIRE_20T = 21
 WIRE_DTYPES = {64: EVENT, 32: EVENT32, 24: EVENT24, WIRE_20T: EVENT20T, 20: EVENT20, 16: EVENT16}
 # bench / agent spelling of the wire codes
-WIRE_NAMES = {"64": 64, "32": 32, "24": 24, "20t": WIRE_20T, "20": 20, "16": 16}
+WIRE_NAMES = {"64": 64, "32": 32, "24": 24, "20t": WIRE_20T, "20": 20, "16": 16, "16t": 16}  # 16t: EVENT16 ring
 
 
 def wire_bytes(wire: int) -> int:
@@ -458,7 +524,7 @@ class TraceInterner:
             i = self._ids.get(h)
             if i is None:
                 i = len(self._ids) + 1
-                if i > 0xFFFFFFFF:
+                if i > TRACE_ID_MASK:  # 30-bit ids (EVENT16 keeps 2 bits for the epoch tag)
                     raise OverflowError("trace id space exhausted")
                 self._ids[h] = i
             out[j] = i

@@ -105,7 +105,7 @@ class Engine {
     const int64_t N = sig_cap_, S = span_cap_, G = group_cap_;
     nblk_sig_ = decode_grid(sig_cap_);
     nblk_span_ = decode_grid(span_cap_);
-    counts = torch::zeros({8}, i32);  // n_ev, n_spans, n_groups, n_local, t_base lo/hi, n_ctx (wire 20)
+    counts = torch::zeros({kCountsLen}, i32);  // n_ev, n_spans, n_groups, n_local, base0 lo/hi, n_ctx, -, bases 1-3
     // signal columns
     // signals: 64-byte row records, status, partition codes of the 4 join keys
     g_status = torch::empty({N}, u8);
@@ -275,7 +275,8 @@ class Engine {
     check_cuda(events, "events");
     if (events.nbytes() < (size_t)sig_cap_ * (size_t)wire_bytes((int)wire))
       throw std::invalid_argument("events buffer must hold sig_cap wire records");
-    if (counts.numel() < 7) throw std::invalid_argument("wire 24/20/16 needs counts int32[>= 7] (t_base, n_ctx)");
+    if (counts.numel() < (wire == 16 ? 14 : 7))
+      throw std::invalid_argument("wire 24/21/20 need counts int32[>= 7] (t_base, n_ctx), wire 16 int32[>= 14] (epoch bases)");
     launch_decode_wire(events.data_ptr(), (int)wire, dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
                       (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                       dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());

@@ -12,6 +12,8 @@
 //
 // The REF-compat variant decodes REF's packed 40-byte record with REF's exact unit
 // rules (pkg/collector/ringbuf.go:199-238) for replaying REF ring-buffer captures.
+#include <type_traits>
+
 #include "mislo_common.h"
 #include "mislo_launch.h"
 
@@ -238,15 +240,17 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
 // counts[4] | counts[5] << 32; context ids resolve through the device context table
 // (counts[6] valid rows).
 __device__ __forceinline__ uint64_t wire_trace(const EventC20& e) { return ((uint64_t)e.tr_hi << 32) | e.tr_lo; }
-__device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)e.trace_id; }
+__device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)(e.trace_id & kTraceIdMask); }
 __device__ __forceinline__ uint64_t wire_trace(const EventC24& e) { return e.trace_h; }
 __device__ __forceinline__ uint64_t wire_trace(const EventC20T& e) { return (uint64_t)e.trace_id; }
-template <class Rec>
-__device__ __forceinline__ int64_t wire_ts(const Rec& e, int64_t t_base) {
-  return e.ts_off == kTsZero ? 0 : t_base + (int64_t)e.ts_off;
+__device__ __forceinline__ int64_t wire_ts(const EventC20& e, const int64_t* base) {
+  return e.ts_off == kTsZero ? 0 : base[0] + (int64_t)e.ts_off;
 }
-__device__ __forceinline__ int64_t wire_ts(const EventC24& e, int64_t) { return e.ts_ns; }
-__device__ __forceinline__ int64_t wire_ts(const EventC20T& e, int64_t) { return e.ts_ns; }
+__device__ __forceinline__ int64_t wire_ts(const EventC16& e, const int64_t* base) {
+  return e.ts_off == kTsZero ? 0 : base[e.trace_id >> kEpochTagShift] + (int64_t)e.ts_off;
+}
+__device__ __forceinline__ int64_t wire_ts(const EventC24& e, const int64_t*) { return e.ts_ns; }
+__device__ __forceinline__ int64_t wire_ts(const EventC20T& e, const int64_t*) { return e.ts_ns; }
 
 // Rec = EventC20 (20-byte), EventC16 (16-byte, interned trace ids), EventC24 (24-byte,
 // absolute timestamps: the probes' context-interned ring record) or EventC20T (20-byte,
@@ -261,7 +265,14 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
 
   const int n = min(*n_ptr, cap);
   const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
-  const int64_t t_base = (int64_t)(((uint64_t)(uint32_t)n_ptr[5] << 32) | (uint32_t)n_ptr[4]);
+  // epoch bases: [0] = counts[4..5] (the window base), [1..3] = counts[8..13]
+  auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
+  int64_t t_base[4] = {base_at(4), 0, 0, 0};
+  if constexpr (std::is_same<Rec, EventC16>::value) {  // only tagged records read bases 1-3
+    t_base[1] = base_at(8);
+    t_base[2] = base_at(10);
+    t_base[3] = base_at(12);
+  }
   // counts[6] = rows of the (fixed-capacity, append-only) context table valid this window
   if (n_ptr[6] > 0) n_ctx = min(n_ptr[6], n_ctx);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;

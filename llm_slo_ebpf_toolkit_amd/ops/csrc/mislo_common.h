@@ -59,11 +59,17 @@ struct EventC20 {
   uint32_t tr_lo, tr_hi;
 };
 static_assert(sizeof(EventC20) == 20, "EventC20 must be 20 bytes");
-// 16-byte wire record (EVENT16): EventC20 with the trace hash interned to a 32-bit id that
-// the window's spans carry too (runtime/csrc/wire.h).
+// 16-byte wire record (EVENT16): EventC20 with the trace hash interned to a 30-bit id that
+// the window's spans carry too (runtime/csrc/wire.h), and a 2-bit epoch tag in the top bits of
+// trace_id: ts = base[tag] + ts_off. The probes (mislo_event16) stamp offsets from the epoch the
+// agent last published and tag them with it, so a record emitted across a window cut still
+// decodes exactly; the window carries its last 4 epoch bases (counts[4..5], [8..13]).
 struct alignas(16) EventC16 {
   uint32_t ts_off, ctx_type, value_milli, trace_id;
 };
+constexpr int kEpochTagShift = 30;
+constexpr uint32_t kTraceIdMask = (1u << kEpochTagShift) - 1u;
+constexpr int kCountsLen = 16;  // counts int32[16] (window sizes, epoch bases, context rows)
 static_assert(sizeof(EventC16) == 16, "EventC16 must be 16 bytes");
 constexpr uint32_t kTsZero = 0xFFFFFFFFu;
 // 24-byte record (EVENT24 = probes/ebpf/mislo_record.h mislo_event24): what the probes put

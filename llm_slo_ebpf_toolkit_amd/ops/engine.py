@@ -118,7 +118,7 @@ class GpuEngine:
             self.sp_dev = torch.zeros(span_cap * 64, dtype=torch.uint8, device=self.device)
             self.ev_host = torch.empty(sig_cap * 64, dtype=torch.uint8, pin_memory=True)
             self.sp_host = torch.empty(span_cap * 64, dtype=torch.uint8, pin_memory=True)
-            self.cnt_host = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+            self.cnt_host = torch.zeros(records.COUNTS_LEN, dtype=torch.int32, pin_memory=True)
             self.lab_host = torch.full((group_cap,), -1, dtype=torch.int32, pin_memory=True)
             self.copy_stream = torch.cuda.Stream(self.device)
         self.sig_cap, self.span_cap, self.group_cap = sig_cap, span_cap, group_cap
@@ -149,7 +149,7 @@ class GpuEngine:
             self.torch.cuda.synchronize(self.device)
 
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None,
-              t_base: int = 0):
+              t_base: int = 0, bases=None):
         """Copy records into pinned staging (host memcpy, no GPU work). ``events`` may be
         64-byte EVENT, 32-byte EVENT32 (needs ``set_pod_table``) or 20/16-byte EVENT20/EVENT16
         records (need ``set_ctx_table`` and the window base ``t_base``)."""
@@ -162,8 +162,7 @@ class GpuEngine:
         self.ev_host.numpy()[: n * records.wire_bytes(self.wire)] = events.view(np.uint8).reshape(-1)
         self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)
         c = self.cnt_host.numpy()
-        tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
-        c[:] = np.array([n, s, n_groups, 0, tb & 0xFFFFFFFF, tb >> 32, 0, 0], dtype=np.uint32).view(np.int32)
+        c[:] = records.counts_row(n, s, n_groups, 0, bases if bases is not None else (t_base,))
         lab = self.lab_host.numpy()
         lab[:] = -1
         if labels is not None:

@@ -89,7 +89,7 @@ def decode_w24(ev: np.ndarray, ctx_table: np.ndarray) -> Decoded:
     return decode_w20(ev, 0, ctx_table)
 
 
-def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
+def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray, bases=None) -> Decoded:
     """k_decode_wire: EVENT20 (trace hash) or EVENT16 (trace id) records with the window
     base, or EVENT24 (absolute timestamps, trace hash), and the context table."""
     type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
@@ -109,12 +109,21 @@ def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray) -> Decoded:
     cid = (ct >> np.uint32(8)).astype(np.int64)
     inb = cid < tab.shape[0]
     row = np.where(inb[:, None], tab[np.minimum(cid, tab.shape[0] - 1)], 0).astype(np.uint32)
+    tagged = "ts_off" in ev.dtype.names and "trace_id" in ev.dtype.names  # EVENT16
     if "ts_ns" in ev.dtype.names:
         ts = ev["ts_ns"].astype(np.int64)
     else:
         off = ev["ts_off"].astype(np.int64)
-        ts = np.where(off == 0xFFFFFFFF, 0, np.int64(t_base) + off)
+        if tagged:  # ts = base[tag] + off; bases[0] is the window base
+            b = np.array(list(bases) if bases is not None else [t_base, 0, 0, 0], dtype=np.int64)
+            tag = (ev["trace_id"].astype(np.uint32) >> np.uint32(30)).astype(np.int64)
+            base = b[tag]
+        else:
+            base = np.int64(t_base)
+        ts = np.where(off == 0xFFFFFFFF, 0, base + off)
     trace = ev["trace_id"] if "trace_id" in ev.dtype.names else ev["trace_h"]
+    if tagged:
+        trace = trace.astype(np.uint32) & np.uint32((1 << 30) - 1)
     return Decoded(ts, val, slot, status, row[:, 0], row[:, 1], row[:, 3], trace.astype(np.uint64),
                    row[:, 2].astype(np.uint64))
 

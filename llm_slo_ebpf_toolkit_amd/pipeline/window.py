@@ -61,9 +61,9 @@ def stats_from_packet(p: Dict[str, np.ndarray]) -> SufficientStats:
 
 
 def aux_head(group_cap: int) -> int:
-    """Bytes ahead of the spans in a packed input block: counts int32[8], labels int32[G],
+    """Bytes ahead of the spans in a packed input block: counts int32[16], labels int32[G],
     padded to 64 so the span records stay 64-byte aligned."""
-    return (32 + 4 * max(int(group_cap), 1) + 63) // 64 * 64
+    return (4 * records.COUNTS_LEN + 4 * max(int(group_cap), 1) + 63) // 64 * 64
 
 
 @dataclass
@@ -154,10 +154,7 @@ def _finish_stage(torch, ev, sp, n_ev: int, n_sp: int, n_groups: int, labels, gr
     # counts[3] = node-local events; events[n_local:] are imported halo / remote-trace
     # records that join but are not counted (decode kernels, parallel/exchange.py)
     nl = 0 if n_local is None or n_local >= n_ev else int(n_local)
-    tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
-    cnt = np.array([n_ev, n_sp, n_groups, nl, tb & 0xFFFFFFFF, tb >> 32, n_ctx, 0],
-                   dtype=np.uint64).astype(np.uint32).view(np.int32)
-    counts = torch.from_numpy(cnt.copy()).pin_memory()
+    counts = torch.from_numpy(records.counts_row(n_ev, n_sp, n_groups, nl, (t_base,), n_ctx).copy()).pin_memory()
     lab = np.full(group_cap, -1, dtype=np.int32)
     if labels is not None:
         lab[: len(labels)] = labels
@@ -198,10 +195,11 @@ class WireStager:
         self.aux = [pin(head + max(span_cap, 1) * 64) for _ in range(self.nb)] if wire != 64 else None
         self.sp = [a[head:] for a in self.aux] if wire != 64 else None
         if self.aux is not None:
-            self.counts = [a[:32].view(torch.int32) for a in self.aux]
-            self.labels = [a[32:32 + 4 * max(group_cap, 1)].view(torch.int32) for a in self.aux]
+            cb = 4 * records.COUNTS_LEN
+            self.counts = [a[:cb].view(torch.int32) for a in self.aux]
+            self.labels = [a[cb:cb + 4 * max(group_cap, 1)].view(torch.int32) for a in self.aux]
         else:
-            self.counts = [pin(8, torch.int32) for _ in range(self.nb)]
+            self.counts = [pin(records.COUNTS_LEN, torch.int32) for _ in range(self.nb)]
             self.labels = [pin(group_cap, torch.int32) for _ in range(self.nb)]
         self.ctx = pin((1 << 16) * 4, torch.int32).view(-1, 4) if wire in (16, 20, records.WIRE_20T, 24) else None
         self.n_ctx = 1
@@ -219,9 +217,27 @@ class WireStager:
         self.enc.encode(np.ascontiguousarray(events), out.numpy(), self.wire)
         return out
 
+    def probe_ring16(self, events: np.ndarray, epoch_ns: int = 0):
+        """EVENT16 records for 64-byte ``events`` as the probes write them with
+        -DMISLO_RING_EVENT16 (kernel-interned contexts and trace ids, offsets from the epoch the
+        agent last published, tagged with it), in pinned memory, plus the window's epoch bases.
+        ``epoch_ns`` > 0 publishes a new epoch every ``epoch_ns`` inside the window (tags 0-3)."""
+        if self.wire != 16:
+            raise ValueError("probe_ring16: wire 16")
+        ev = np.zeros(events.shape[0], dtype=records.EVENT16)
+        t_base = int(self.enc.encode(np.ascontiguousarray(events), ev.view(np.uint8).reshape(-1), 16))
+        bases = (t_base,)
+        if epoch_ns > 0:
+            ev, bases = records.retag_epochs(ev, t_base, epoch_ns)
+        out = self.torch.from_numpy(ev.view(np.uint8).reshape(-1).copy()).pin_memory()
+        return out, bases
+
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
               group_domains=None, n_local: Optional[int] = None, ev_pinned=None, sp_pinned=None,
-              pod_table: Optional[np.ndarray] = None) -> StagedWindow:
+              pod_table: Optional[np.ndarray] = None, bases=None) -> StagedWindow:
+        """One window into slot k % nb. ``ev_pinned``: the pinned probe ring segment for wire
+        64/32/24/21, and for wire 16 when the probes write EVENT16 (then ``bases`` = the window's
+        epoch bases); without it wire 16/20 encode the 64-byte records here."""
         torch = self.torch
         slot = self.k % self.nb
         if self.k >= self.nb:  # slot's previous reader: the H2D of window k - nb
@@ -229,7 +245,13 @@ class WireStager:
         t0 = time.perf_counter()
         n_ev, n_sp = int(events.shape[0]), int(spans.shape[0])
         t_base = 0
-        if self.wire == 64:
+        if self.wire == 16 and ev_pinned is not None:  # probe-native EVENT16 ring
+            ev, sp = ev_pinned, self.sp[slot]
+            if n_sp * 64 > sp.numel():
+                raise ValueError("window exceeds the stager's capacity")
+            self.enc.encode_spans(spans, sp.numpy(), True)  # spans onto the kernel's trace ids
+            bases = tuple(bases) if bases is not None else (0,)
+        elif self.wire == 64:
             ev, sp = ev_pinned, sp_pinned
             if ev is None or sp is None:
                 raise ValueError("wire 64 stages the pinned ring records: pass ev_pinned / sp_pinned")
@@ -258,10 +280,9 @@ class WireStager:
                 self.ctx.numpy()[self.n_ctx:n_ctx] = self.enc.ctx_table()[self.n_ctx:n_ctx]
                 self.n_ctx = n_ctx
         nl = 0 if n_local is None or n_local >= n_ev else int(n_local)
-        tb = int(t_base) & 0xFFFFFFFFFFFFFFFF
         c = self.counts[slot].numpy()
-        c[:] = np.array([n_ev, n_sp, n_groups, nl, tb & 0xFFFFFFFF, tb >> 32, self.n_ctx if self.ctx is not None else 0,
-                         0], dtype=np.uint64).astype(np.uint32).view(np.int32)
+        c[:] = records.counts_row(n_ev, n_sp, n_groups, nl, bases if self.wire == 16 and ev_pinned is not None
+                                  else (t_base,), self.n_ctx if self.ctx is not None else 0)
         lab = self.labels[slot].numpy()
         lab[:] = -1
         if labels is not None:
@@ -325,14 +346,15 @@ class WindowPipeline:
             self.aux_head = aux_head(group_cap)
             self.aux_dev = [z8(self.aux_head + span_cap * 64) for _ in range(self.nb)]
             self.sp_dev = [a[self.aux_head:] for a in self.aux_dev]
-            self.counts_dev = [a[:32].view(torch.int32) for a in self.aux_dev]
+            cb = 4 * records.COUNTS_LEN
+            self.counts_dev = [a[:cb].view(torch.int32) for a in self.aux_dev]
             # append-only context table for 20-byte records: rows are copied once, stream
             # ordered before the first window that references them; the buffer address stays
             # fixed (captured graphs keep pointing at it) until it has to grow
             self.ctx_dev = torch.zeros((1 << 16, 4), dtype=torch.int32, device=self.dev)
             self.ctx_uploaded = 1  # row 0 = the all-zero context
             self.eng.set_ctx_table(self.ctx_dev)
-            self.labels_dev = [a[32:32 + 4 * max(group_cap, 1)].view(torch.int32) for a in self.aux_dev]
+            self.labels_dev = [a[cb:cb + 4 * max(group_cap, 1)].view(torch.int32) for a in self.aux_dev]
             for lab in self.labels_dev:
                 lab.fill_(-1)
             self.packet_dev = [torch.zeros(L, dtype=torch.float64, device=self.dev) for _ in range(self.nb)]

@@ -48,8 +48,14 @@ int main(void)
 		printf("bad mislo_event20t layout\n");
 		return 1;
 	}
+	if (sizeof(struct mislo_event16) != 16 || offsetof(struct mislo_event16, ts_off) != 0 ||
+	    offsetof(struct mislo_event16, ctx_type) != 4 || offsetof(struct mislo_event16, value_milli) != 8 ||
+	    offsetof(struct mislo_event16, trace_tag) != 12) {
+		printf("bad mislo_event16 layout\n");
+		return 1;
+	}
 	printf("mislo_event layout ok (64 bytes), mislo_event32 ok (32 bytes), mislo_event24 ok (24 bytes), "
-	       "mislo_event20t ok (20 bytes)\n");
+	       "mislo_event20t ok (20 bytes), mislo_event16 ok (16 bytes)\n");
 	/* fixed-point rule: print "type value milli" lines for the Python side to compare */
 	static const unsigned long long vals[] = {0, 499, 500, 501, 1500, 2500, 2501, 4294967, 4294968,
 						   4294967295ull, 4294967296ull, 4294967295500ull, 4294967296500ull};

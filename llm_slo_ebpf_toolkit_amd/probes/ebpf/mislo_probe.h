@@ -2,12 +2,15 @@
  *
  * Every probe object shares these maps, pinned by name under /sys/fs/bpf so the agent's
  * loader opens them once:
- *   mislo_events  BPF ring buffer of 20-byte mislo_event20t records (24-byte mislo_event24
- *                 with -DMISLO_RING_EVENT24, 32-byte mislo_event32 with -DMISLO_RING_EVENT32)
- *                 that the agent drains into the GPU window ring (16 MiB);
+ *   mislo_events  BPF ring buffer of 16-byte mislo_event16 records (20-byte mislo_event20t
+ *                 with -DMISLO_RING_EVENT20T, 24-byte mislo_event24 with -DMISLO_RING_EVENT24,
+ *                 32-byte mislo_event32 with -DMISLO_RING_EVENT32) that the agent drains into
+ *                 the GPU window ring (16 MiB);
  *   mislo_cfg     array: [0] realtime - monotonic offset (ns), [1] node id,
  *                 [2 + type] per-signal emit floor (raw units; the overhead guard raises
- *                 floors before it detaches probes), [125] trace id counter,
+ *                 floors before it detaches probes), [124] current epoch (event16 rings:
+ *                 realtime ns with the low 2 bits replaced by the epoch tag; the agent
+ *                 publishes one per window cut and keeps the last 4 bases), [125] trace id counter,
  *                 [126] context id counter, [127] connection id counter;
  *   mislo_traces  LRU trace hash -> 32-bit trace id (event20t rings). Trace ids are per request
  *                 and never reused within 2^32 - 1 assignments; LRU eviction only drops traces
@@ -43,6 +46,7 @@
 #define MISLO_CFG_NODE 1
 #define MISLO_CFG_FLOOR(t) (2 + (t))
 #define MISLO_CFG_SLOTS 128
+#define MISLO_CFG_EPOCH 124
 #define MISLO_CFG_TRACE_NEXT 125
 #define MISLO_CFG_CTX_NEXT 126
 #define MISLO_CFG_CONN_NEXT 127
@@ -214,7 +218,7 @@ static __always_inline __u32 mislo_trace_id(__u64 h)
 	if (!next)
 		return 0;
 	__u64 fresh = __sync_fetch_and_add(next, 1);
-	__u32 v = (__u32)(fresh % 0xFFFFFFFFull) + 1;
+	__u32 v = (__u32)(fresh % MISLO_TRACE_ID_MASK) + 1; /* [1, 2^30 - 1]: event16 keeps 2 tag bits */
 	if (bpf_map_update_elem(&mislo_traces, &h, &v, BPF_NOEXIST) == 0)
 		return v;
 	id = bpf_map_lookup_elem(&mislo_traces, &h);
@@ -233,6 +237,12 @@ static __always_inline void mislo_submit(struct mislo_event *e)
 	r.pid = e->pid;
 	r.pod_id = e->pod_id;
 	r.type_conn = (e->signal_type & 0xFFu) | (cid << 8);
+#elif defined(MISLO_RING_EVENT20T)
+	struct mislo_event20t r;
+	r.ts_ns = e->ts_ns;
+	r.value_milli = mislo_milli(e->signal_type, e->value);
+	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
+	r.trace_id = mislo_trace_id(e->trace_h);
 #elif defined(MISLO_RING_EVENT24)
 	struct mislo_event24 r;
 	r.ts_ns = e->ts_ns;
@@ -240,11 +250,21 @@ static __always_inline void mislo_submit(struct mislo_event *e)
 	r.value_milli = mislo_milli(e->signal_type, e->value);
 	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
 #else
-	struct mislo_event20t r;
-	r.ts_ns = e->ts_ns;
-	r.value_milli = mislo_milli(e->signal_type, e->value);
+	/* default: 16-byte record, timestamp offset from the published epoch, tagged with it */
+	struct mislo_event16 r;
+	__u32 eidx = MISLO_CFG_EPOCH;
+	__u64 *ep = bpf_map_lookup_elem(&mislo_cfg, &eidx);
+	__u64 epoch = ep ? *ep : 0;
+	__u64 base = epoch & ~3ull;
+	if (e->ts_ns == 0)
+		r.ts_off = MISLO_TS_ZERO;
+	else if ((__u64)e->ts_ns < base)
+		r.ts_off = 0; /* stamped before the epoch it read (clock step): clamp */
+	else
+		r.ts_off = (__u64)e->ts_ns - base >= MISLO_TS_ZERO ? MISLO_TS_ZERO - 1 : (__u32)((__u64)e->ts_ns - base);
 	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
-	r.trace_id = mislo_trace_id(e->trace_h);
+	r.value_milli = mislo_milli(e->signal_type, e->value);
+	r.trace_tag = (mislo_trace_id(e->trace_h) & MISLO_TRACE_ID_MASK) | ((__u32)(epoch & 3) << MISLO_EPOCH_TAG_SHIFT);
 #endif
 	bpf_ringbuf_output(&mislo_events, &r, sizeof(r), 0);
 }

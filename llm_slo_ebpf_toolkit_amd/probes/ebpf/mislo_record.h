@@ -3,10 +3,15 @@
  * layout test.
  *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record and
  *                        the user-space producers' ring record;
- *   struct mislo_event20t (20 B, records.py EVENT20T): what the probes put on the BPF ring
- *                        (default): mislo_event24 with the trace hash interned in the kernel
+ *   struct mislo_event20t (20 B, records.py EVENT20T): the ring record with
+ *                        -DMISLO_RING_EVENT20T: mislo_event24 with the trace hash interned in the kernel
  *                        too (mislo_probe.h mislo_trace_id; the agent maps span trace ids
  *                        through the same map), 5/16 of the 64-byte record's PCIe bytes;
+ *   struct mislo_event16 (16 B, records.py EVENT16): what the probes put on the BPF ring
+ *                        (default): mislo_event20t with the timestamp as a 32-bit offset from the epoch the
+ *                        agent last published (mislo_cfg[MISLO_CFG_EPOCH]) and that epoch's 2-bit
+ *                        tag in the top of trace_id, so records emitted across a window cut
+ *                        decode exactly (the window carries its last 4 epoch bases);
  *   struct mislo_event24 (24 B, records.py EVENT24): the ring record with -DMISLO_RING_EVENT24.
  *                        The kernel converts the value to fixed point
  *                        (mislo_milli) and interns the connection and the (pod, pid, conn)
@@ -81,6 +86,17 @@ struct mislo_event24 {
 	__u64 trace_h;     /* trace-id hash (0 = none) */
 	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
 	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
+};
+
+#define MISLO_EPOCH_TAG_SHIFT 30
+#define MISLO_TRACE_ID_MASK ((1u << MISLO_EPOCH_TAG_SHIFT) - 1u)
+#define MISLO_TS_ZERO 0xFFFFFFFFu
+
+struct mislo_event16 {
+	__u32 ts_off;      /* ns since the tagged epoch; MISLO_TS_ZERO = no timestamp */
+	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
+	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
+	__u32 trace_tag;   /* bits 0-29 interned trace id (0 = none), bits 30-31 epoch tag */
 };
 
 /* 4-byte aligned: ring records are packed back to back at 20-byte strides */

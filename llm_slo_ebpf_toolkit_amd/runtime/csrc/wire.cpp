@@ -96,10 +96,10 @@ uint32_t TraceTable::id(uint64_t tr, uint32_t gen) {
     }
     if (slots_[i].key == 0) break;
   }
-  // new trace: ids wrap at 2^32 (skipping 0); a live trace would have to outlast 2^32 newer
-  // ones to collide
+  // new trace: ids wrap at 2^30 (skipping 0; EVENT16 keeps the top 2 bits for the epoch tag);
+  // a live trace would have to outlast 2^30 newer ones to collide
   const uint32_t v = next_;
-  next_ = next_ == 0xFFFFFFFFu ? 1u : next_ + 1;
+  next_ = next_ == kTraceIdMask ? 1u : next_ + 1;
   slots_[i] = Slot{tr, v, gen};
   if (2 * ++size_ > slots_.size()) rehash(slots_.size() * 2, 0);
   return v;

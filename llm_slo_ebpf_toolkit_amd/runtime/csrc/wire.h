@@ -109,6 +109,10 @@ inline uint32_t milli_int(uint64_t v, int d) {
 }
 
 constexpr uint32_t kWireTsZero = 0xFFFFFFFFu;
+// EVENT16 trace_id: bits 0-29 interned trace id, bits 30-31 the epoch tag (which of the
+// window's 4 timestamp bases ts_off counts from; the host encoder writes tag 0)
+constexpr int kEpochTagShift = 30;
+constexpr uint32_t kTraceIdMask = (1u << kEpochTagShift) - 1u;
 
 inline uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;

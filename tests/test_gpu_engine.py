@@ -227,6 +227,40 @@ def test_wire20t_matches_oracle(engine):
     assert int(e.misc[1].item()) == 1  # the zero timestamp
 
 
+def test_wire16_epoch_tags_match_oracle(engine):
+    """EVENT16 with 2-bit epoch tags (the probes' -DMISLO_RING_EVENT16 record): the decode kernel
+    picks each record's base from counts[4..5] / [8..13]; decode + join == numpy oracle."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+
+    win = small_window(seed=25)
+    engine.set_join_params(2000.0, 0.7, 3, 1)
+    engine.set_model(NaiveBayes.ref())
+    conns, ctxs, traces = records.ConnInterner(), records.CtxInterner(), records.TraceInterner()
+    ev = win.events.copy()
+    ev["ts_ns"][2] = 0
+    e16, t_base = records.to_wire16(ev, conns, ctxs, traces)
+    e16, bases = records.retag_epochs(e16, t_base, 200_000_000)
+    assert len(set((e16["trace_id"] >> np.uint32(30)).tolist())) > 1
+    sp = records.wire_spans(win.spans, conns, traces)
+    engine.set_ctx_table(ctxs.table())
+    engine.stage(e16, sp, win.n_groups, win.group_labels, bases=bases)
+    engine.upload()
+    engine.run(True, False)
+    out = engine.outputs()
+    e = engine.eng
+    d = oracle.decode_w16(e16, t_base, ctxs.table(), bases=bases)
+    N, S = win.n_events, win.n_spans
+    np.testing.assert_array_equal(rows(e, N)["ts"], d.ts)
+    np.testing.assert_array_equal(d.ts, ev["ts_ns"])
+    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
+    ref = oracle.join(d, sp, win.n_groups)
+    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
+    np.testing.assert_array_equal(top3, ref.top3)
+    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
+        assert out.debug[k] == ref.debug[k], k
+    np.testing.assert_array_equal(out.feat, ref.feat)
+
+
 def test_wire16_native_matches_oracle(engine):
     """Native encoder (EVENT16, interned trace ids) -> GPU decode + join == numpy oracle."""
     from llm_slo_ebpf_toolkit_amd.collector import records
@@ -375,23 +409,30 @@ def test_wire_stager_matches_prestaged_windows():
 
     def totals_stager(wire):
         pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
-        st = WireStager(torch, pipe, 8192, 512, 8, wire=wire, threads=4)
+        st = WireStager(torch, pipe, 8192, 512, 8, wire=16 if wire == "16t" else wire, threads=4)
         if wire == 64:
             ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
                      torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
         elif wire in (21, 24, 32):
             ring = [(st.probe_records(w.events), None) for w in wins]
+        elif wire == "16t":  # EVENT16 probe ring, epoch-tagged
+            r16 = [st.probe_ring16(w.events, epoch_ns=300_000_000) for w in wins]
+            ring = [(t, b) for t, b in r16]
         else:
             ring = [(None, None)] * 3
         for i in range(7):
             w = wins[i % 3]
-            pipe.submit(st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
-                                 ev_pinned=ring[i % 3][0], sp_pinned=ring[i % 3][1], pod_table=pods))
+            if wire == "16t":
+                pipe.submit(st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
+                                     ev_pinned=ring[i % 3][0], bases=ring[i % 3][1]))
+            else:
+                pipe.submit(st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
+                                     ev_pinned=ring[i % 3][0], sp_pinned=ring[i % 3][1], pod_table=pods))
         return pipe.summary()
 
     keys = ("confusion", "hist", "status", "dbg", "misc")
     ref32 = totals_prestaged(32)
-    for wire in (32, 24, 21, 20, 16):
+    for wire in (32, 24, 21, 20, 16, "16t"):
         got = totals_stager(wire)
         for k in keys:
             np.testing.assert_array_equal(got[k], ref32[k], err_msg=f"stager {wire} {k}")

@@ -302,3 +302,54 @@ def test_event20t_native_numpy_and_join():
     jr = oracle.join(b, records.wire_spans(win.spans, conns, traces), win.n_groups)
     np.testing.assert_array_equal(full.top3, jr.top3)
     assert full.debug == jr.debug
+
+
+def test_event16_epoch_tags_decode_like_one_base():
+    """EVENT16 as the probes write it with -DMISLO_RING_EVENT16: offsets from the epoch the agent
+    last published, tagged with it (4 bases per window). Decoding with the window's bases gives
+    the timestamps and trace ids of the single-base encoding, and joins identically."""
+    pytest = __import__("pytest")
+    try:
+        enc = records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    win = _win(seed=14)
+    ev = win.events.copy()
+    ev["ts_ns"][7] = 0
+    buf = np.zeros(ev.shape[0], dtype=records.EVENT16)
+    t_base = enc.encode(ev, buf.view(np.uint8).reshape(-1), 16)
+    assert int((buf["trace_id"] >> np.uint32(30)).max()) == 0  # host encoding: tag 0
+    tagged, bases = records.retag_epochs(buf, t_base, 256_000_000)
+    tags = tagged["trace_id"] >> np.uint32(30)
+    assert set(np.unique(tags).tolist()) == {0, 1, 2, 3}
+    assert int(tagged["ts_off"][7]) == records.TS_ZERO
+    one = oracle.decode_w16(buf, t_base, enc.ctx_table())
+    four = oracle.decode_w16(tagged, t_base, enc.ctx_table(), bases=bases)
+    for f in ("ts", "slot", "pod", "pid", "svcnode", "trace", "val"):
+        np.testing.assert_array_equal(getattr(one, f), getattr(four, f), err_msg=f)
+    np.testing.assert_array_equal(four.ts, np.where(ev["ts_ns"] == 0, 0, ev["ts_ns"]))
+    c = records.counts_row(10, 2, 1, 0, bases, 5)
+    assert c.shape == (records.COUNTS_LEN,) and int(c[6]) == 5
+    got = [int(np.uint64(c[lo].astype(np.uint32)) | (np.uint64(c[lo + 1].astype(np.uint32)) << np.uint64(32)))
+           for lo in (4, 8, 10, 12)]
+    assert got == list(bases)
+
+
+def test_epoch_clock_protocol_across_cuts():
+    """Agent/probe epoch protocol: records stamped against any of the last 4 published epochs
+    (a probe that read the epoch before a cut writes after it) decode to their exact timestamps
+    with the bases the window ships."""
+    clk = records.EpochClock()
+    t0 = 1_700_000_000_123_456_789
+    cfgs = [clk.publish(t0 + k * 1_000_000_007) for k in range(6)]  # 6 cuts: tags wrap
+    bases = clk.bases()
+    rng = np.random.default_rng(3)
+    for k in range(2, 6):  # records stamped against epochs k, k-1, k-2 (late writers)
+        for lag in range(3):
+            cfg = cfgs[k - lag]
+            ts = (cfg & ~3) + int(rng.integers(0, 2_500_000_000))
+            off, tag = records.EpochClock.stamp(ts, cfg)
+            assert tag == (k - lag) & 3
+            if k == 5:  # the window after the last cut carries bases of epochs 2..5
+                assert bases[tag] + off == ts
+    assert records.EpochClock.stamp(0, cfgs[0]) == (records.TS_ZERO, cfgs[0] & 3)
