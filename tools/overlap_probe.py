@@ -25,7 +25,8 @@ from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, WireStager 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=1 << 20)
-    ap.add_argument("--wire", type=int, default=21, choices=(21, 24, 32))
+    ap.add_argument("--wire", type=int, default=16, choices=(16, 21, 24, 32),
+                    help="16 = the epoch-tagged EVENT16 probe ring (4 epochs per window)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--buffers", type=int, default=3)
     a = ap.parse_args()
@@ -34,13 +35,17 @@ def main():
     wins = [gen.next_window() for _ in range(2)]
     pipe = WindowPipeline(a.events, 16384, 64, 0, None, max_ahead=a.buffers, n_buffers=a.buffers)
     st = WireStager(torch, pipe, a.events, 16384, 64, wire=a.wire)
-    ring = [st.probe_records(w.events) for w in wins]
+    if a.wire == 16:
+        r16 = [st.probe_ring16(w.events, epoch_ns=256_000_000) for w in wins]
+        ring, bases = [t for t, _ in r16], [b for _, b in r16]
+    else:
+        ring, bases = [st.probe_records(w.events) for w in wins], [None, None]
     pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
 
     def stage(j):
         w = wins[j % 2]
         return st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains, ev_pinned=ring[j % 2],
-                        pod_table=pods)
+                        pod_table=pods, bases=bases[j % 2])
 
     for j in range(8):  # warm: graphs captured for both buffers
         pipe.submit(stage(j))
