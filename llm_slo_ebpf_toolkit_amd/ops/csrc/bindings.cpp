@@ -352,6 +352,16 @@ class Engine {
                  dptr<double>(stats), dptr<double>(stats_count), cur_stream());
   }
 
+  // posterior(with_labels) + accumulate_stats() of a learning window as one launch
+  void posterior_and_stats(bool with_labels) {
+    launch_posterior_stats(dptr<float>(feat), dptr<int>(counts) + 2, group_cap_,
+                           reinterpret_cast<const PosteriorModel*>(model.data_ptr()),
+                           with_labels ? dptr<int32_t>(labels) : nullptr, dptr<double>(post), dptr<int32_t>(pred),
+                           dptr<double>(gconf), dptr<uint32_t>(evbits), dptr<uint32_t>(confusion),
+                           dptr<int32_t>(labels), nullptr, dptr<double>(stats), dptr<double>(stats_count),
+                           cur_stream());
+  }
+
   void pack() {
     hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, cur_stream(), dptr<uint32_t>(hist),
                        dptr<uint32_t>(status_cnt), dptr<unsigned long long>(misc), dptr<unsigned long long>(dbg),
@@ -367,8 +377,8 @@ class Engine {
     reset_window();
     decode_wire(events, wire);
     join(spans, n_groups, c10::nullopt);
-    posterior(with_labels);
-    if (learn) accumulate_stats(c10::nullopt);
+    if (learn) posterior_and_stats(with_labels);
+    else posterior(with_labels);
     pack();
   }
 
@@ -383,8 +393,8 @@ class Engine {
   void run_window_post(int64_t n_groups, bool with_labels, bool learn) {
     if (n_groups > group_cap_) throw std::invalid_argument("n_groups exceeds group capacity");
     launch_group_features((int)n_groups, dptr<unsigned long long>(gsum), dptr<uint32_t>(gcnt), dptr<float>(feat), cur_stream());
-    posterior(with_labels);
-    if (learn) accumulate_stats(c10::nullopt);
+    if (learn) posterior_and_stats(with_labels);
+    else posterior(with_labels);
     pack();
   }
 

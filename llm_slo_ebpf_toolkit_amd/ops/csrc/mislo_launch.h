@@ -65,6 +65,10 @@ void launch_posterior(const float* feat, const int* ng_dev, int cap, const Poste
 void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                   const float* weights, double* out, double* count, hipStream_t stream);
 
+void launch_posterior_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm,
+                            const int32_t* labels, double* post, int32_t* pred, double* conf, uint32_t* evbits,
+                            uint32_t* confusion, const int32_t* stat_labels, const float* weights, double* out,
+                            double* count, hipStream_t stream);
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
                      PosteriorModel* pm, hipStream_t stream);
 

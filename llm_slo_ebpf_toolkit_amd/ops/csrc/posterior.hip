@@ -42,18 +42,40 @@ __device__ __forceinline__ uint32_t elevated_bits(const float* __restrict__ row,
   return b & pm.table_mask;
 }
 
+struct PosteriorArgs {
+  const float* feat;
+  const int* ng_ptr;
+  int cap;
+  const PosteriorModel* pm;
+  const int32_t* labels;
+  double *post, *conf;
+  int32_t* pred;
+  uint32_t *evbits, *confusion;
+};
+struct StatsArgs {
+  const float* feat;
+  const int* ng_ptr;
+  int cap;
+  const PosteriorModel* pm;
+  const int32_t* labels;
+  const float* weights;
+  double *out, *count;
+};
+
 template <int NT>
-__global__ __launch_bounds__(NT) void k_posterior(const float* __restrict__ feat, const int* __restrict__ ng_ptr,
-                                                  int cap, const PosteriorModel* __restrict__ pmp,
-                                                  const int32_t* __restrict__ labels,
-                                                  double* __restrict__ post, int32_t* __restrict__ pred,
-                                                  double* __restrict__ conf, uint32_t* __restrict__ evbits,
-                                                  uint32_t* __restrict__ confusion) {
-  const int G = min(*ng_ptr, cap);
-  const PosteriorModel& pm = *pmp;
+__device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_) {
+  const float* __restrict__ feat = a_.feat;
+  const int32_t* __restrict__ labels = a_.labels;
+  double* __restrict__ post = a_.post;
+  int32_t* __restrict__ pred = a_.pred;
+  double* __restrict__ conf = a_.conf;
+  uint32_t* __restrict__ evbits = a_.evbits;
+  uint32_t* __restrict__ confusion = a_.confusion;
+  const int G = min(*a_.ng_ptr, a_.cap);
+  const PosteriorModel& pm = *a_.pm;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int row0 = (blockIdx.x * (NT / 64) + wave) * 16;
+  const int row0 = (blk * (NT / 64) + wave) * 16;
   if (row0 >= G) return;  // whole wave exits together
   const int i = lane & 15;
   const int kq = lane >> 4;
@@ -104,17 +126,24 @@ __global__ __launch_bounds__(NT) void k_posterior(const float* __restrict__ feat
   }
 }
 
+template <int NT>
+__global__ __launch_bounds__(NT) void k_posterior(PosteriorArgs a) {
+  posterior_body<NT>(blockIdx.x, a);
+}
+
 // U^T V over labelled incidents; out[32][32] f64, count[16] f64.
 template <int NT, int ROWS_PER_WAVE>
-__global__ __launch_bounds__(NT) void k_stats(const float* __restrict__ feat, const int* __restrict__ ng_ptr, int cap,
-                                              const PosteriorModel* __restrict__ pmp, const int32_t* __restrict__ labels,
-                                              const float* __restrict__ weights, double* __restrict__ out,
-                                              double* __restrict__ count) {
-  const int G = min(*ng_ptr, cap);
-  const PosteriorModel& pm = *pmp;
+__device__ __forceinline__ void stats_body(int blk, const StatsArgs& a_) {
+  const float* __restrict__ feat = a_.feat;
+  const int32_t* __restrict__ labels = a_.labels;
+  const float* __restrict__ weights = a_.weights;
+  double* __restrict__ out = a_.out;
+  double* __restrict__ count = a_.count;
+  const int G = min(*a_.ng_ptr, a_.cap);
+  const PosteriorModel& pm = *a_.pm;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int base = (blockIdx.x * (NT / 64) + wave) * ROWS_PER_WAVE;
+  const int base = (blk * (NT / 64) + wave) * ROWS_PER_WAVE;
   if (base >= G) return;
   const int i = lane & 15;
   const int kq = lane >> 4;
@@ -148,6 +177,20 @@ __global__ __launch_bounds__(NT) void k_stats(const float* __restrict__ feat, co
     atomicAdd(out + (size_t)(16 + rr) * 32 + i, t10[reg]);
     atomicAdd(out + (size_t)(16 + rr) * 32 + 16 + i, t11[reg]);
   }
+}
+
+template <int NT, int ROWS_PER_WAVE>
+__global__ __launch_bounds__(NT) void k_stats(StatsArgs a) {
+  stats_body<NT, ROWS_PER_WAVE>(blockIdx.x, a);
+}
+
+// Posterior + sufficient statistics of a learning window in ONE launch: the two read the same
+// features and model and write disjoint outputs, and each is a single latency-bound
+// workgroup at the default 64 incidents; back to back they cost two serial launches.
+template <int NT, int ROWS_PER_WAVE>
+__global__ __launch_bounds__(NT) void k_posterior_stats(PosteriorArgs p, StatsArgs st, int n_post_blocks) {
+  if ((int)blockIdx.x < n_post_blocks) posterior_body<NT>(blockIdx.x, p);
+  else stats_body<NT, ROWS_PER_WAVE>(blockIdx.x - n_post_blocks, st);
 }
 
 // On-device refit of the learned naive Bayes (models/bayes.py NaiveBayes.learned) from
@@ -209,23 +252,40 @@ void launch_refit_nb(double* stats, const double* add, const double* p0, double 
   hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, alpha, prior_pseudo, n_dom, pm);
 }
 
+constexpr int kPostNT = 256, kStatsRPW = 256;
+static int posterior_grid(int cap) {
+  const int rows_per_block = (kPostNT / 64) * 16;
+  const int g = (cap + rows_per_block - 1) / rows_per_block;
+  return g > 0 ? g : 1;
+}
+static int stats_grid(int cap) {
+  const int rows_per_block = (kPostNT / 64) * kStatsRPW;
+  const int g = (cap + rows_per_block - 1) / rows_per_block;
+  return g > 0 ? g : 1;
+}
+
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                       double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
                       hipStream_t stream) {
-  constexpr int NT = 256;
-  const int rows_per_block = (NT / 64) * 16;
-  const int grid = (cap + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL((k_posterior<NT>), dim3(grid > 0 ? grid : 1), dim3(NT), 0, stream, feat, ng_dev, cap, pm, labels,
-                     post, pred, conf, evbits, confusion);
+  const PosteriorArgs a{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion};
+  hipLaunchKernelGGL((k_posterior<kPostNT>), dim3(posterior_grid(cap)), dim3(kPostNT), 0, stream, a);
 }
 
 void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                   const float* weights, double* out, double* count, hipStream_t stream) {
-  constexpr int NT = 256, RPW = 256;
-  const int rows_per_block = (NT / 64) * RPW;
-  const int grid = (cap + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL((k_stats<NT, RPW>), dim3(grid > 0 ? grid : 1), dim3(NT), 0, stream, feat, ng_dev, cap, pm,
-                     labels, weights, out, count);
+  const StatsArgs a{feat, ng_dev, cap, pm, labels, weights, out, count};
+  hipLaunchKernelGGL((k_stats<kPostNT, kStatsRPW>), dim3(stats_grid(cap)), dim3(kPostNT), 0, stream, a);
+}
+
+void launch_posterior_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm,
+                            const int32_t* labels, double* post, int32_t* pred, double* conf, uint32_t* evbits,
+                            uint32_t* confusion, const int32_t* stat_labels, const float* weights, double* out,
+                            double* count, hipStream_t stream) {
+  const PosteriorArgs p{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion};
+  const StatsArgs st{feat, ng_dev, cap, pm, stat_labels, weights, out, count};
+  const int gp = posterior_grid(cap);
+  hipLaunchKernelGGL((k_posterior_stats<kPostNT, kStatsRPW>), dim3(gp + stats_grid(cap)), dim3(kPostNT), 0, stream, p,
+                     st, gp);
 }
 
 }  // namespace mislo
