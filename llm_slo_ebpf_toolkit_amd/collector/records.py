@@ -131,12 +131,14 @@ def retag_epochs(ev16: np.ndarray, t_base: int, period_ns: int):
     return out, tuple(int(t_base) + k * int(period_ns) for k in range(4))
 
 
-def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,), n_ctx: int = 0) -> np.ndarray:
+def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,), n_ctx: int = 0,
+               span_bytes: int = 64) -> np.ndarray:
     """The window's counts int32[16] as the decode kernels read them: [0] events, [1] spans,
     [2] incident groups, [3] node-local events (0 = all), [4..5] epoch base 0 (the window base),
-    [6] valid context rows, [8..9] / [10..11] / [12..13] epoch bases 1-3 (EVENT16 tags)."""
+    [6] valid context rows, [7] span record bytes (20 = SPAN20, else 64-byte SPAN),
+    [8..9] / [10..11] / [12..13] epoch bases 1-3 (EVENT16 tags)."""
     b = [int(x) & 0xFFFFFFFFFFFFFFFF for x in (list(bases) + [0, 0, 0, 0])[:4]]
-    v = [n_ev, n_sp, n_groups, n_local, b[0] & 0xFFFFFFFF, b[0] >> 32, n_ctx, 0,
+    v = [n_ev, n_sp, n_groups, n_local, b[0] & 0xFFFFFFFF, b[0] >> 32, n_ctx, 20 if span_bytes == 20 else 0,
          b[1] & 0xFFFFFFFF, b[1] >> 32, b[2] & 0xFFFFFFFF, b[2] >> 32, b[3] & 0xFFFFFFFF, b[3] >> 32, 0, 0]
     return np.array(v, dtype=np.uint64).astype(np.uint32).view(np.int32)
 assert EVENT16.itemsize == 16
@@ -453,6 +455,25 @@ def to_wire20t(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner",
     for f in ("ts_ns", "value_milli", "ctx_type"):
         out[f] = e24[f]
     out["trace_id"] = traces.ids(events["trace_h"])
+    return out
+
+
+# 20-byte span record (ops/csrc SpanC20, runtime/csrc/wire.h Span20): what the GPU join reads of
+# a span, with (pod, pid, conn, svc|node) as a context id and an interned trace id; used with the
+# trace-interning event rings (EVENT16 / EVENT20T), 5/16 of the 64-byte SPAN's PCIe bytes.
+SPAN20 = np.dtype({"names": ["ts_ns", "trace_id", "ctx_id", "group_id"],
+                   "formats": ["<i8", "<u4", "<u4", "<u4"], "offsets": [0, 8, 12, 16], "itemsize": 20})
+
+
+def to_span20(spans: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner", traces: "TraceInterner") -> np.ndarray:
+    """SPAN (64 B) -> SPAN20 with the event interners (numpy reference of encode_spans20)."""
+    out = np.zeros(spans.shape[0], dtype=SPAN20)
+    out["ts_ns"] = spans["ts_ns"]
+    out["trace_id"] = traces.ids(spans["trace_h"])
+    cid = conns.ids(spans["conn_h"])
+    sn = (spans["svc_id"].astype(np.uint32) << np.uint32(16)) | spans["node_id"].astype(np.uint32)
+    out["ctx_id"] = ctxs.ids(spans["pod_id"], spans["pid"], cid, sn)
+    out["group_id"] = spans["group_id"]
     return out
 
 

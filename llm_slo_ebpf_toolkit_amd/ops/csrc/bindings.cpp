@@ -311,7 +311,9 @@ class Engine {
       throw std::invalid_argument("spans buffer must hold span_cap 64-byte records");
     if (n_groups > group_cap_) throw std::invalid_argument("n_groups exceeds group capacity");
     hipStream_t st = cur_stream();
-    launch_decode_spans(spans.data_ptr(), dptr<int>(counts) + 1, span_cap_, span_cols(), dptr<uint32_t>(s_part_blk), st);
+    if (counts.numel() < 8) throw std::invalid_argument("counts must hold int32[>= 8] (counts[7] = span record bytes)");
+    launch_decode_spans(spans.data_ptr(), dptr<int>(counts) + 1, span_cap_, span_cols(), dptr<uint32_t>(s_part_blk),
+                        dptr<uint32_t>(ctx_table), (int)ctx_table.size(0), st);
     launch_partition(reinterpret_cast<const PartCodes*>(s_part.data_ptr()), dptr<int>(counts) + 1, span_cap_, nblk_span_,
                      dptr<uint32_t>(s_part_blk), dptr<uint32_t>(s_part_off), dptr<uint32_t>(s_part_tot),
                      dptr<uint32_t>(s_part_base), dptr<uint32_t>(s_items), st);

@@ -337,10 +337,16 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
-// Span records -> span columns + span partition counts.
+// Span records -> span columns + span partition counts. n_ptr = counts + 1: n_ptr[0] spans,
+// n_ptr[5] valid context rows, n_ptr[6] span record bytes (20 = SpanC20 via the context table).
 template <int NT>
-__global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp, const int* __restrict__ n_ptr,
-                                                     int cap, SpanCols c, uint32_t* part_cnt) {
+__global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp_raw, const int* __restrict__ n_ptr,
+                                                     int cap, SpanCols c, uint32_t* part_cnt,
+                                                     const uint4* __restrict__ ctx_tab, int n_ctx) {
+  const Span* __restrict__ sp = static_cast<const Span*>(sp_raw);
+  const SpanC20* __restrict__ sp20 = static_cast<const SpanC20*>(sp_raw);
+  const bool compact = n_ptr[6] == 20;
+  if (n_ptr[5] > 0) n_ctx = min(n_ptr[5], n_ctx);
   __shared__ uint32_t s_part[kKeyTypes * kParts];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
   __syncthreads();
@@ -348,23 +354,32 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const Span* __restrict__ sp
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   for (int i = beg + threadIdx.x; i < end; i += NT) {
-    const Span s = sp[i];
-    const uint32_t svcnode = ((uint32_t)s.svc_id << 16) | s.node_id;
-    {
-      SpanRec r;
+    SpanRec r;
+    if (compact) {
+      const SpanC20 s = sp20[i];
+      const uint4 cx = s.ctx_id < (uint32_t)n_ctx ? ctx_tab[s.ctx_id] : make_uint4(0u, 0u, 0u, 0u);
+      r.ts = s.ts_ns;
+      r.tr = s.trace_id;
+      r.cn = cx.z;
+      r.pod = cx.x;
+      r.pid = cx.y;
+      r.sn = cx.w;
+      r.grp = s.group_id;
+    } else {
+      const Span s = sp[i];
       r.ts = s.ts_ns;
       r.tr = s.trace_h;
       r.cn = s.conn_h;
       r.pod = s.pod_id;
       r.pid = s.pid;
-      r.sn = svcnode;
+      r.sn = ((uint32_t)s.svc_id << 16) | s.node_id;
       r.grp = s.group_id;
-      c.rec[i] = r;
     }
+    c.rec[i] = r;
     PartCodes pc;
 #pragma unroll
     for (int k = 0; k < kKeyTypes; ++k) {
-      const uint64_t h = s.ts_ns != 0 ? key_hash(k, s.trace_h, s.pod_id, s.pid, s.conn_h, svcnode) : 0ull;
+      const uint64_t h = r.ts != 0 ? key_hash(k, r.tr, r.pod, r.pid, r.cn, r.sn) : 0ull;
       pc.p[k] = h ? (uint16_t)part_of(h) : kNoPart;
       if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
     }
@@ -438,10 +453,10 @@ void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, 
 }
 
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
-                         hipStream_t stream) {
+                         const uint32_t* ctx_tab, int n_ctx, hipStream_t stream) {
   constexpr int NT = 256;
-  hipLaunchKernelGGL((k_decode_spans<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
-                     (const Span*)sp, n_dev, cap, cols, part_cnt);
+  hipLaunchKernelGGL((k_decode_spans<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, sp, n_dev, cap, cols,
+                     part_cnt, reinterpret_cast<const uint4*>(ctx_tab), n_ctx);
 }
 
 }  // namespace mislo

@@ -118,6 +118,14 @@ struct alignas(64) Span {
   uint64_t span_h, reserved;
 };
 static_assert(sizeof(Span) == 64, "Span must be 64 bytes");
+// 20-byte span record (collector/records.py SPAN20, runtime/csrc/wire.h Span20): the fields the
+// join reads, with (pod, pid, conn, svc|node) as a context id into the device context table and
+// an interned trace id. A window uses it when counts[7] == 20 (else 64-byte Span records).
+struct __attribute__((packed, aligned(4))) SpanC20 {
+  int64_t ts_ns;
+  uint32_t trace_id, ctx_id, group_id;
+};
+static_assert(sizeof(SpanC20) == 20, "SpanC20 must be 20 bytes");
 
 // Decoded signal columns (structure of arrays, one entry per event).
 // Row records of the fields the join reads per (signal, key type) visit: one 64-byte line

@@ -37,7 +37,7 @@ void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, 
                        const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                        unsigned long long* misc, hipStream_t stream);
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
-                         hipStream_t stream);
+                         const uint32_t* ctx_tab, int n_ctx, hipStream_t stream);
 
 // join.hip
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,

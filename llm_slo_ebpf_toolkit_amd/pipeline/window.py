@@ -85,6 +85,7 @@ class StagedWindow:
     # pinned [counts | labels | pad | spans] block when counts / labels / sp are views of it
     # (WireStager): the three small inputs then cross PCIe as ONE copy (aux_head(group_cap))
     aux: "object" = None
+    span_bytes: int = 64                # 20 = SPAN20 records (counts[7]), else 64-byte SPAN
 
 
 def stage_window(torch, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray],
@@ -245,11 +246,14 @@ class WireStager:
         t0 = time.perf_counter()
         n_ev, n_sp = int(events.shape[0]), int(spans.shape[0])
         t_base = 0
+        span_bytes = 64
         if self.wire == 16 and ev_pinned is not None:  # probe-native EVENT16 ring
             ev, sp = ev_pinned, self.sp[slot]
-            if n_sp * 64 > sp.numel():
+            if n_sp * 20 > sp.numel():
                 raise ValueError("window exceeds the stager's capacity")
-            self.enc.encode_spans(spans, sp.numpy(), True)  # spans onto the kernel's trace ids
+            # spans as 20-byte SPAN20 on the kernel's trace ids and context ids
+            self.enc.encode_spans20(spans, sp.numpy()[: n_sp * 20])
+            span_bytes = 20
             bases = tuple(bases) if bases is not None else (0,)
         elif self.wire == 64:
             ev, sp = ev_pinned, sp_pinned
@@ -261,8 +265,13 @@ class WireStager:
                 raise ValueError("wire 32/24/21 stage the pinned probe ring: pass ev_pinned (and pod_table for 32)")
             if n_sp * 64 > sp.numel():
                 raise ValueError("window exceeds the stager's capacity")
-            # spans onto the kernel's connection ids (and, for EVENT20T, its trace ids)
-            self.enc.encode_spans(spans, sp.numpy(), self.wire == records.WIRE_20T)
+            # spans onto the kernel's connection ids (EVENT20T: 20-byte SPAN20 on its trace and
+            # context ids)
+            if self.wire == records.WIRE_20T:
+                self.enc.encode_spans20(spans, sp.numpy()[: n_sp * 20])
+                span_bytes = 20
+            else:
+                self.enc.encode_spans(spans, sp.numpy(), False)
         else:
             ev, sp = self.ev[slot], self.sp[slot]
             if n_ev * self.wire > ev.numel() or n_sp * 64 > sp.numel():
@@ -282,7 +291,7 @@ class WireStager:
         nl = 0 if n_local is None or n_local >= n_ev else int(n_local)
         c = self.counts[slot].numpy()
         c[:] = records.counts_row(n_ev, n_sp, n_groups, nl, bases if self.wire == 16 and ev_pinned is not None
-                                  else (t_base,), self.n_ctx if self.ctx is not None else 0)
+                                  else (t_base,), self.n_ctx if self.ctx is not None else 0, span_bytes)
         lab = self.labels[slot].numpy()
         lab[:] = -1
         if labels is not None:
@@ -294,7 +303,7 @@ class WireStager:
         return StagedWindow(ev, sp, self.counts[slot], self.labels[slot], n_ev, n_sp, n_groups,
                             list(group_domains or []), self.wire, pod_table if self.wire == 32 else None,
                             self.ctx if ctx else None, self.n_ctx if ctx else 0, dt,
-                            self.aux[slot] if self.aux is not None else None)
+                            self.aux[slot] if self.aux is not None else None, span_bytes)
 
 
 class WindowPipeline:
@@ -448,11 +457,11 @@ class WindowPipeline:
                     w.counts.data_ptr() == w.aux.data_ptr() and w.sp.data_ptr() == w.aux.data_ptr() + self.aux_head:
                 # packed block: counts, labels and spans in one DMA (a copy has a fixed
                 # ~10 us cost on the copy engine, paid per window on the critical path)
-                na = self.aux_head + w.n_spans * 64
+                na = self.aux_head + w.n_spans * w.span_bytes
                 self.aux_dev[b][:na].copy_(w.aux[:na], non_blocking=True)
                 if tr: tr.extend([time.perf_counter()] * 3)
             else:
-                self.sp_dev[b][: w.n_spans * 64].copy_(w.sp[: w.n_spans * 64], non_blocking=True)
+                self.sp_dev[b][: w.n_spans * w.span_bytes].copy_(w.sp[: w.n_spans * w.span_bytes], non_blocking=True)
                 if tr: tr.append(time.perf_counter())
                 self.counts_dev[b].copy_(w.counts, non_blocking=True)
                 if tr: tr.append(time.perf_counter())

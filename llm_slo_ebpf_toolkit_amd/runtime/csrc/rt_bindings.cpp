@@ -167,6 +167,17 @@ class PyWireEncoder {
     return enc_->encode(static_cast<const mislo::EventRec*>(ei.ptr), n, oi.ptr, wire);
   }
 
+  // spans -> 20-byte SPAN20 records (out >= n*20 bytes)
+  void encode_spans20(py::buffer spans, py::buffer out) {
+    py::buffer_info si = spans.request(), oi = out.request(true);
+    const size_t nb = (size_t)si.size * si.itemsize;
+    if (nb % sizeof(mislo::SpanRec64)) throw std::invalid_argument("spans: not a whole number of 64-byte records");
+    const size_t n = nb / sizeof(mislo::SpanRec64);
+    if ((size_t)oi.size * oi.itemsize < n * sizeof(mislo::Span20)) throw std::invalid_argument("out buffer too small");
+    py::gil_scoped_release nogil;
+    enc_->encode_spans20(static_cast<const mislo::SpanRec64*>(si.ptr), n, static_cast<mislo::Span20*>(oi.ptr));
+  }
+
   void encode_spans(py::buffer spans, py::buffer out, bool trace_ids) {
     py::buffer_info si = spans.request(), oi = out.request(true);
     const size_t nb = (size_t)si.size * si.itemsize;
@@ -240,6 +251,7 @@ PYBIND11_MODULE(_mislo_rt, m) {
   py::class_<PyWireEncoder>(m, "WireEncoder")
       .def(py::init<py::array_t<int8_t, py::array::c_style | py::array::forcecast>>(), py::arg("shift"))
       .def("encode", &PyWireEncoder::encode, py::arg("events"), py::arg("out"), py::arg("wire") = 20)
+      .def("encode_spans20", &PyWireEncoder::encode_spans20, py::arg("spans"), py::arg("out"))
       .def("encode_spans", &PyWireEncoder::encode_spans, py::arg("spans"), py::arg("out"),
            py::arg("trace_ids") = false)
       .def("encode_window", &PyWireEncoder::encode_window, py::arg("events"), py::arg("ev_out"), py::arg("wire"),

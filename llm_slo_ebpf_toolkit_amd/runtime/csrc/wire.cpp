@@ -289,6 +289,14 @@ void WireEncoder::encode_spans(const SpanRec64* in, size_t n, SpanRec64* out, bo
   }
 }
 
+void WireEncoder::encode_spans20(const SpanRec64* in, size_t n, Span20* out) {
+  for (size_t i = 0; i < n; ++i) {
+    const SpanRec64& s = in[i];
+    const uint32_t ctx = ctx_id(s.pod_id, s.pid, s.conn_h, ((uint32_t)s.svc_id << 16) | s.node_id);
+    out[i] = Span20{s.ts_ns, traces_.id(s.trace_h, gen_), ctx, s.group_id};
+  }
+}
+
 void WireEncoder::end_window() {
   ++gen_;
   if (gen_ > 2) traces_.expire(gen_ - 2);

@@ -71,12 +71,19 @@ struct Event24 {  // collector/records.py EVENT24 = probes/ebpf/mislo_record.h m
 static_assert(sizeof(Event24) == 24, "Event24 is 24 bytes");
 
 #pragma pack(push, 4)
+// records.py SPAN20: a span as the GPU join needs it (20 B instead of 64): absolute timestamp,
+// interned trace id, (pod, pid, conn, svc|node) context id into the device context table,
+// incident group
+struct Span20 {
+  int64_t ts_ns;
+  uint32_t trace_id, ctx_id, group_id;
+};
 struct Event20T {  // collector/records.py EVENT20T = probes/ebpf/mislo_record.h mislo_event20t (wire code 21)
   int64_t ts_ns;
   uint32_t value_milli, ctx_type, trace_id;
 };
 #pragma pack(pop)
-static_assert(sizeof(Event20T) == 20, "Event20T is 20 bytes");
+static_assert(sizeof(Event20T) == 20 && sizeof(Span20) == 20, "Event20T / Span20 are 20 bytes");
 constexpr int kWire20T = 21;
 inline int wire_bytes(int wire) { return wire == kWire20T ? 20 : wire; }
 
@@ -240,6 +247,9 @@ class WireEncoder {
   int64_t encode(const EventRec* ev, size_t n, void* out, int wire);
   // Spans keep the 64-byte layout: conn hash -> conn id; with trace_ids, trace -> id.
   void encode_spans(const SpanRec64* in, size_t n, SpanRec64* out, bool trace_ids);
+  // Spans -> Span20 (trace ids and contexts on the same tables as the events; new contexts
+  // append ctx rows like events do)
+  void encode_spans20(const SpanRec64* in, size_t n, Span20* out);
   // Trace-id generation boundary (call once per window after events and spans).
   void end_window();
   // events -> ev_out (wire 20/16) and spans -> sp_out in one pass on `threads` threads; the

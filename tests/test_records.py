@@ -353,3 +353,44 @@ def test_epoch_clock_protocol_across_cuts():
             if k == 5:  # the window after the last cut carries bases of epochs 2..5
                 assert bases[tag] + off == ts
     assert records.EpochClock.stamp(0, cfgs[0]) == (records.TS_ZERO, cfgs[0] & 3)
+
+
+def test_span20_native_matches_numpy_reference():
+    """SPAN20 (20-byte spans on the event interners): native encode_spans20 == records.to_span20
+    field for field once context ids are resolved through each side's context table, and trace
+    ids agree with the events' EVENT20T trace ids."""
+    pytest = __import__("pytest")
+    try:
+        enc = records.native_encoder()
+    except RuntimeError:
+        pytest.skip("native runtime not built")
+    win = _win(seed=15)
+    ev, sp = win.events, win.spans
+    buf = np.zeros(ev.shape[0] * 20, np.uint8)
+    enc.encode(ev, buf, records.WIRE_20T)
+    n20 = buf.view(records.EVENT20T)
+    s_nat = np.zeros(sp.shape[0], dtype=records.SPAN20)
+    enc.encode_spans20(sp, s_nat.view(np.uint8).reshape(-1))
+    conns, ctxs, traces = records.ConnInterner(), records.CtxInterner(), records.TraceInterner()
+    records.to_wire20t(ev, conns, ctxs, traces)
+    s_ref = records.to_span20(sp, conns, ctxs, traces)
+    np.testing.assert_array_equal(s_nat["ts_ns"], sp["ts_ns"])
+    np.testing.assert_array_equal(s_nat["group_id"], sp["group_id"])
+    np.testing.assert_array_equal(s_nat["ts_ns"], s_ref["ts_ns"])
+    tn, tr = enc.ctx_table().view(np.uint32), ctxs.table().view(np.uint32)
+    rows_n, rows_r = tn[s_nat["ctx_id"]], tr[s_ref["ctx_id"]]
+    for col in (0, 1, 3):  # pod, pid, svc|node (col 2 = conn id: numbering differs, checked below)
+        np.testing.assert_array_equal(rows_n[:, col], rows_r[:, col])
+    np.testing.assert_array_equal(rows_n[:, 0], sp["pod_id"])
+    # same trace -> same id as the events carry; same conn hash -> same conn id as events
+    ev_trace = dict(zip(ev["trace_h"].tolist(), n20["trace_id"].tolist()))
+    for h, t in zip(sp["trace_h"].tolist(), s_nat["trace_id"].tolist()):
+        assert (t == 0) == (h == 0)
+        if h in ev_trace:
+            assert t == ev_trace[h]
+    ev_conn = dict(zip(records._conn_keys(ev).tolist(), tn[n20["ctx_type"] >> np.uint32(8)][:, 2].tolist()))
+    for h, cid in zip(sp["conn_h"].tolist(), rows_n[:, 2].tolist()):
+        if h in ev_conn and h:
+            assert cid == ev_conn[h]
+    c = records.counts_row(1, 1, 1, span_bytes=20)
+    assert int(c[7]) == 20 and int(records.counts_row(1, 1, 1)[7]) == 0
