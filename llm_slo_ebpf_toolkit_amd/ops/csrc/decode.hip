@@ -132,7 +132,7 @@ __device__ __forceinline__ void lds_flush(DecodeLds& L, const DecodeOut& o, int 
 __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val, int slot,
                                            uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
                                            uint64_t conn_h, const DecodeOut& o, const LdsLane& l,
-                                           int& unsupported, int& zero_ts, bool local) {
+                                           int& unsupported, int& zero_ts, bool local, SigRec* rec_dst) {
   uint8_t st = 0;
   if (slot >= 0 && local) {
     const Tables& t = *l.tab;
@@ -164,7 +164,7 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
     r.sn = svcnode;
     r.val = val;
     r.slot = slot >= 0 ? (uint32_t)slot : kNoSlot;
-    o.cols.rec[i] = r;
+    *rec_dst = r;
   }
   // Unsupported signal types never reach Match (REF correlator.go:73-77), and a zero
   // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
     const float val = slot >= 0 ? (float)((double)e.value * (double)L.tab.scale[slot]) : (float)e.value;
     const uint64_t ch = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
     const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
-    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local, o.cols.rec + i);
   }
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restric
     const float val = (float)((double)e.value_milli * 1e-3);
     const uint64_t ch = (uint64_t)(e.type_conn >> 8);
     const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
-    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local, o.cols.rec + i);
   }
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
@@ -284,6 +284,13 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
     const uint32_t cid = r.ctx_type >> 8;
     return cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
   };
+  // Row records leave through LDS: a lane's 64-byte SigRec stored straight to global memory
+  // makes every store instruction touch 64 cache lines; staged, each wave writes its 64
+  // consecutive records (4 KiB) as 4 fully coalesced 1 KiB stores. Trip counts are uniform
+  // across the workgroup (the staging needs barriers).
+  __shared__ SigRec s_stage[NT];
+  const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
+  const int trips = end > beg ? (end - beg + NT - 1) / NT : 0;
   int i = beg + threadIdx.x;
   Rec e_nx{};
   uint4 cx_nx = make_uint4(0u, 0u, 0u, 0u);
@@ -291,19 +298,35 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
     e_nx = ev[i];
     cx_nx = ctx_of(e_nx);
   }
-  for (; i < end; i += NT) {
+  for (int it = 0; it < trips; ++it, i += NT) {
     const Rec e = e_nx;
     const uint4 cx = cx_nx;
     if (i + NT < end) {
       e_nx = ev[i + NT];
       cx_nx = ctx_of(e_nx);
     }
-    const int st = (int)(e.ctx_type & 0xFFu);
-    const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
-    const float val = (float)((double)e.value_milli * 1e-3);
-    const int64_t ts = wire_ts(e, t_base);
-    const uint64_t tr = wire_trace(e);
-    decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, i < n_local);
+    if (i < end) {
+      const int st = (int)(e.ctx_type & 0xFFu);
+      const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
+      const float val = (float)((double)e.value_milli * 1e-3);
+      const int64_t ts = wire_ts(e, t_base);
+      const uint64_t tr = wire_trace(e);
+      decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts,
+                 i < n_local, &s_stage[threadIdx.x]);
+    }
+    __syncthreads();
+    const int first = i - lane;  // this wave's first record
+    const int nv = min(64, end - first);
+    if (nv > 0) {
+      const uint4* src = reinterpret_cast<const uint4*>(&s_stage[wbase]);
+      uint4* dst = reinterpret_cast<uint4*>(o.cols.rec + first);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = lane + 64 * j;  // 16-byte chunk q of the wave's 4 KiB
+        if ((q >> 2) < nv) dst[q] = src[q];
+      }
+    }
+    __syncthreads();
   }
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
@@ -332,7 +355,7 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
     if (st == 2 || st == 6) val = (float)e.value_ns;           // tcp count, cpu_steal raw ns
     else val = (float)((double)e.value_ns / 1e6);               // ns -> ms
     const uint64_t ch = conn_hash(e.conn_src_port, e.conn_dst_port, e.conn_dst_ip);
-    decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local);
+    decode_one(i, cap, (int64_t)e.timestamp_ns, val, slot, trace_h, pod, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local, o.cols.rec + i);
   }
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
