@@ -132,7 +132,7 @@ __device__ __forceinline__ void lds_flush(DecodeLds& L, const DecodeOut& o, int 
 __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val, int slot,
                                            uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
                                            uint64_t conn_h, const DecodeOut& o, const LdsLane& l,
-                                           int& unsupported, int& zero_ts, bool local, SigRec* rec_dst) {
+                                           int& unsupported, int& zero_ts, bool local, void* rec_dst) {
   uint8_t st = 0;
   if (slot >= 0 && local) {
     const Tables& t = *l.tab;
@@ -164,7 +164,11 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
     r.sn = svcnode;
     r.val = val;
     r.slot = slot >= 0 ? (uint32_t)slot : kNoSlot;
-    *rec_dst = r;
+    // 4 x 16 B: rec_dst is a 64-byte-aligned global row or a 16-byte-aligned LDS staging slot
+    const uint4* rs = reinterpret_cast<const uint4*>(&r);
+    uint4* rd = static_cast<uint4*>(rec_dst);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rd[q] = rs[q];
   }
   // Unsupported signal types never reach Match (REF correlator.go:73-77), and a zero
   // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
@@ -288,7 +292,9 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
   // makes every store instruction touch 64 cache lines; staged, each wave writes its 64
   // consecutive records (4 KiB) as 4 fully coalesced 1 KiB stores. Trip counts are uniform
   // across the workgroup (the staging needs barriers).
-  __shared__ SigRec s_stage[NT];
+  // padded to 5 x 16 B per record: at a 64-byte stride the 16-byte stores of a lane group hit
+  // the same banks
+  __shared__ uint4 s_stage[NT * 5];
   const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
   const int trips = end > beg ? (end - beg + NT - 1) / NT : 0;
   int i = beg + threadIdx.x;
@@ -312,18 +318,18 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
       const int64_t ts = wire_ts(e, t_base);
       const uint64_t tr = wire_trace(e);
       decode_one(i, cap, ts, val, slot, tr, cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts,
-                 i < n_local, &s_stage[threadIdx.x]);
+                 i < n_local, &s_stage[threadIdx.x * 5]);
     }
     __syncthreads();
     const int first = i - lane;  // this wave's first record
     const int nv = min(64, end - first);
     if (nv > 0) {
-      const uint4* src = reinterpret_cast<const uint4*>(&s_stage[wbase]);
+      const uint4* src = &s_stage[wbase * 5];
       uint4* dst = reinterpret_cast<uint4*>(o.cols.rec + first);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = lane + 64 * j;  // 16-byte chunk q of the wave's 4 KiB
-        if ((q >> 2) < nv) dst[q] = src[q];
+        if ((q >> 2) < nv) dst[q] = src[(q >> 2) * 5 + (q & 3)];
       }
     }
     __syncthreads();
