@@ -1,19 +1,26 @@
-"""Headline benchmark: fault-replay attribution throughput on MI355X, with the north-star
-quality/overhead metrics measured in the same run.
+"""Headline benchmark: node-wide fault-replay attribution throughput on MI355X through the
+agent's shipped path, with the north-star attribution quality and agent overhead measured in
+the same run.
 
-Metric (BASELINE.json): "attribution macro-F1 on fault-replay confusion matrix; agent CPU
-overhead %", reported on config 5 ("full 9 CPU + 4 GPU signals, safety governor <= 3 %
-overhead, full confusion matrix across all fault domains") plus the events/s scaling
-curve the north star asks for. One step = one 1-second collection window per GPU, from
-the records the probes wrote into the agent's pinned ring (16-byte epoch-tagged EVENT16 by default) ->
-host work (spans mapped onto the kernel's connection ids; with --wire 16/20, wire encoding
-of 64-byte records on a native worker pool) -> H2D -> decode + histograms -> LDS hash join
--> MFMA posteriors + confusion -> MFMA sufficient statistics -> RCCL all-reduce of the
-packed window statistics -> online model refit. ``value`` = node-wide events/s (weak
-scaling: every GPU owns one node's shard of pods, 1M events per window).
+BASELINE.json metric: "attribution macro-F1 on fault-replay confusion matrix; agent CPU
+overhead %". ``value`` is the events/s the GPU window path sustains node-wide (the scaling
+curve the north star asks for; weak scaling: every GPU owns one node shard, 1M events per
+window); the macro-F1 (held out: windows no model update saw), the REF-55 macro-F1 and the
+agent CPU % / RSS are reported alongside.
 
-Synthetic data: seeded fault-replay traces (pipeline/replay.py) shaped by REF's fault
-profiles; the attribution model starts from random-init priors and learns online.
+One step = one collection window per GPU, exactly as the agent runs it:
+
+  producer process (stands in for the kernel: the probes' records, already framed as the BPF
+  ring buffer holds them, plus the rocprofiler tool's GPU-signal records and the spans)
+    -> emulated BPF ring buffer (kernel user-visible layout) / user-space rings (shared memory)
+  agent (timed):  window cut -> native assembly (parallel compaction of the ring's EVENT16
+    records, id definitions, host encoding of user-space records and spans, context-row patch)
+    -> one H2D DMA -> HIP graph: decode + histograms -> LDS hash join -> MFMA posterior +
+    confusion -> MFMA sufficient statistics -> pack -> RCCL all-reduce of the packet over
+    xGMI (N > 1) -> on-device model refit (prequential, random-init priors).
+
+Synthetic data: seeded fault-replay traces (pipeline/replay.py, REF fault profiles), random-init
+attribution priors; the kernel's record path is the native probe model (runtime/csrc/probesim.h).
 
     python bench.py --gpus N --steps K --warmup W
 """
@@ -22,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import multiprocessing as mp
 import os
 import sys
 import time
@@ -29,9 +37,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BASELINE_EVENTS_PER_S = 900.0      # REF pkg/benchmark/harness.go:77 (hard-coded constant)
 BASELINE_MACRO_F1 = 0.9818         # BASELINE.md §2 (REF Bayes on REF's 30 single-fault rows)
-BASELINE_CPU_PCT = 2.2             # REF harness.go:75 (hard-coded constant)
+BASELINE_CPU_PCT = 2.2             # REF harness.go:75 (a hard-coded constant; the gate is <= 3 %)
 
 
 def parse():
@@ -42,130 +49,187 @@ def parse():
     ap.add_argument("--events", type=int, default=1 << 20, help="events per window per GPU")
     ap.add_argument("--spans", type=int, default=16384, help="spans per window per GPU")
     ap.add_argument("--services", type=int, default=64, help="incident groups per window per GPU")
-    ap.add_argument("--windows", type=int, default=4, help="distinct pre-generated windows per GPU")
+    ap.add_argument("--windows", type=int, default=4, help="distinct replay windows the producer cycles")
+    ap.add_argument("--heldout", type=int, default=4, help="held-out windows scored with the frozen model")
     ap.add_argument("--model", default="bayes_learned", choices=("bayes", "bayes_learned", "lda"))
     ap.add_argument("--scenario", default="full")
     ap.add_argument("--paced-windows", type=int, default=3,
-                    help="windows replayed at 1M events/s for the CPU-overhead measurement (0 = skip)")
+                    help="windows produced at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--threads", type=int, default=0, help="agent host threads (0 = min(OMP_NUM_THREADS, 8))")
+    ap.add_argument("--ring-mib", type=int, default=1024, help="emulated BPF ring buffer size (MiB, power of 2)")
     ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
-    ap.add_argument("--max-ahead", type=int, default=3, choices=(1, 2, 3),
-                    help="windows the host may run ahead of the GPU (host back-pressure)")
-    ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4),
-                    help="device input buffers (window i uses i %% buffers): copies of window i wait for "
-                         "the kernels of window i - buffers")
-    ap.add_argument("--group-scope", default="rank", choices=("rank", "global"),
-                    help="incident groups per GPU (rank) or node-wide with a group-sum all-reduce (global)")
-    ap.add_argument("--wire", default="16t", choices=("16", "16t", "20", "20t", "24", "32", "64"),
-                    help="event record format on PCIe. 16t (default) / 20t / 24 / 32 / 64: the probes' ring records "
-                         "(EVENT20T: 20 bytes, kernel-interned contexts and trace ids; 16t = EVENT16: "
-                         "16 bytes, also epoch-relative timestamps with 2-bit epoch tags, 4 epochs per "
-                         "window; EVENT24: interned "
-                         "contexts; EVENT32: interned connections; EVENT: 64 bytes), DMA'd from the pinned "
-                         "ring as-is (no per-event host work; spans are mapped onto the kernel's connection "
-                         "(and trace) ids); 16 = EVENT16 / 20 = EVENT20, encoded from 64-byte records on the "
-                         "host inside every step (interned contexts and trace ids; the encoder reads the same "
-                         "64 B per event the DMA would)")
-    ap.add_argument("--encode-threads", type=int, default=0,
-                    help="host encoder worker threads (0 = OMP_NUM_THREADS, else 8; at most 16)")
+    ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4))
     ap.add_argument("--out", default="")
-    a = ap.parse_args()
-    from llm_slo_ebpf_toolkit_amd.collector.records import WIRE_NAMES
+    return ap.parse_args()
 
-    a.wire_name, a.wire = a.wire, WIRE_NAMES[a.wire]
-    return a
+
+# ---------------------------------------------------------------------------------------
+# producer process: the kernel and the user-space producers
+# ---------------------------------------------------------------------------------------
+
+def producer_main(names, imgs, heldout, plan, conn) -> None:
+    """Writes windows into the rings the way the probes would have (framed records appended as
+    committed, user-space records and spans pushed), then a cut record per window. ``plan`` =
+    (flat-out windows, paced windows, period s). Never touches the GPU."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    cpus = conn.recv()
+    if cpus:
+        try:
+            os.sched_setaffinity(0, cpus)
+        except OSError:
+            pass
+    rt = load()
+    rb = rt.Ringbuf.attach_shm(names["ring"])
+    user = rt.HostRing(0, 64, names["user"], True)
+    spans = rt.HostRing(0, 64, names["spans"], True)
+    cuts = rt.HostRing(0, 64, names["cuts"], True)
+    n_flat, n_paced, period = plan
+    seq = [(imgs[j % len(imgs)], None) for j in range(n_flat)] + \
+          [(imgs[j % len(imgs)], "paced") for j in range(n_paced)] + [(h, None) for h in heldout]
+    nxt = time.perf_counter()
+    for j, (img, mode) in enumerate(seq):
+        if mode == "paced":
+            nxt += period
+            time.sleep(max(0.0, nxt - time.perf_counter()))
+        while not rb.append_framed(img.framed, 4):
+            time.sleep(50e-6)
+        while len(img.user) and user.push(img.user, 4) == 0:
+            time.sleep(50e-6)
+        while spans.push(img.spans) == 0:
+            time.sleep(50e-6)
+        c = np.zeros(8, dtype=np.uint64)
+        c[:3] = (rb.producer_pos, user.head, spans.head)
+        c[3:7] = np.array(img.bases, dtype=np.int64).astype(np.uint64)
+        c[7] = j
+        while cuts.push(c.view(np.uint8)) == 0:
+            time.sleep(50e-6)
+    conn.send("done")
 
 
 def main() -> int:
     a = parse()
     import numpy as np
-    import torch
-    import torch.distributed as dist
 
-    from llm_slo_ebpf_toolkit_amd.models import load_samples_jsonl, macro_f1
-    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, samples_to_arrays
-    from llm_slo_ebpf_toolkit_amd.ops import require_gpu_extension
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
-    from llm_slo_ebpf_toolkit_amd.collector import records
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, WireStager
-    from llm_slo_ebpf_toolkit_amd.safety import CPUMeter, OverheadGuard, read_rss_mb
-    from llm_slo_ebpf_toolkit_amd.signals import catalog
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, build_replay_images
+    from llm_slo_ebpf_toolkit_amd.runtime import load
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    require_gpu_extension()
-    # MISLO_BENCH_GPU_OF_RANK=0 pins every rank to cuda:0 and MISLO_DIST_BACKEND=gloo swaps
-    # RCCL for gloo: a multi-rank rehearsal of the distributed path on a one-GPU box (RCCL
-    # refuses two ranks on one device). Real runs use neither.
-    if os.environ.get("MISLO_BENCH_GPU_OF_RANK") is not None:
-        local = int(os.environ["MISLO_BENCH_GPU_OF_RANK"])
-    torch.cuda.set_device(local)
-    # keep this rank's pinned ring and host threads on its GPU's socket (before any pinning)
-    from llm_slo_ebpf_toolkit_amd.parallel.numa import bind_to_device_numa
-    numa_cpus = bind_to_device_numa(local)
-    pg = None
-    if world > 1:
-        backend = os.environ.get("MISLO_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-        pg = dist.group.WORLD
+    threads = a.threads or max(1, min(8, int(os.environ.get("OMP_NUM_THREADS", "0") or 8)))
 
     def log(*x):
         if rank == 0:
             print("[bench]", *x, file=sys.stderr, flush=True)
 
-    # ---- data: this rank's shard of the node (its own pods/services) ------------------
-    # The windows are the 64-byte records the probes write into the agent's ring; converting
-    # them to the wire format (native encoder on a worker pool) is part of every timed step.
+    # ---- data: this rank's node shard, run through the probe model (CPU, before the GPU) ----
     t = time.time()
     cfg = ReplayConfig(scenario=a.scenario, events_per_window=a.events, spans_per_window=a.spans,
                        n_services=a.services, seed=a.seed, shard=rank)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
-    pipe = WindowPipeline(a.events, a.spans, a.services, local, pg, model=a.model, seed=a.seed,
-                          group_scope=a.group_scope, use_graphs=not a.no_graphs,
-                          max_ahead=min(a.max_ahead, a.buffers), n_buffers=a.buffers)
-    threads = a.encode_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 8)
-    stager = WireStager(torch, pipe, a.events, a.spans, a.services, wire=a.wire, threads=threads)
-    ring, pods, ring_bases = None, None, None
-    if a.wire == 64:  # the probe ring is pinned: 64-byte records DMA straight from it
-        ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
-                 torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-    elif a.wire in (21, 24, 32):  # the probes' own 20/24/32-byte records (kernel-interned ids)
-        ring = [(stager.probe_records(w.events), None) for w in wins]
-    elif a.wire_name == "16t":  # EVENT16 ring: epoch published every 256 ms (tags 0-3 per window)
-        r16 = [stager.probe_ring16(w.events, epoch_ns=256_000_000) for w in wins]
-        ring = [(t, None) for t, _ in r16]
-        ring_bases = [b for _, b in r16]
-        # pod id -> svc|node: agent metadata (kubelet / CRI), static over the run
-        pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
-    log(f"generated {len(wins)} windows x {a.events} events in {time.time() - t:.1f}s")
+    # held out: a different seed (never trained on), REF's label set and the full set
+    held = []
+    for j in range(a.heldout):
+        hcfg = ReplayConfig(scenario="mixed" if j % 2 else a.scenario, events_per_window=a.events,
+                            spans_per_window=a.spans, n_services=a.services, seed=a.seed + 7919, shard=rank)
+        hg = ReplayGenerator(hcfg)
+        hg.window = 1000 + j  # later in time than the training windows
+        held.append(hg.next_window())
+    images = build_replay_images(wins + held)
+    imgs, himgs = images[: len(wins)], images[len(wins):]
+    pods = np.unique(np.concatenate([w.events["pod_id"] for w in wins + held]))
+    pod_sn = {}
+    for w in wins + held:
+        sn = (w.events["svc_id"].astype(np.uint32) << np.uint32(16)) | w.events["node_id"].astype(np.uint32)
+        pod_sn.update(zip(w.events["pod_id"].tolist(), sn.tolist()))
+    log(f"generated {len(wins)}+{len(held)} windows x {a.events} events, probe-model encoded in {time.time() - t:.1f}s "
+        f"({imgs[0].n_kernel} kernel-ring + {len(imgs[0].user)} user-space records per window)")
 
-    def stage(j):
-        w = wins[j % len(wins)]
-        evp, spp = ring[j % len(wins)] if ring else (None, None)
-        return stager.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
-                            ev_pinned=evp, sp_pinned=spp, pod_table=pods,
-                            bases=ring_bases[j % len(wins)] if a.wire_name == "16t" else None)
+    # ---- rings (shared memory) and the producer process, forked before any GPU work ----------
+    rt = load()
+    tag = f"/mislo-bench-{os.getpid()}"
+    names = {"ring": tag + "-ev", "user": tag + "-user", "spans": tag + "-sp", "cuts": tag + "-cut"}
+    rb = rt.Ringbuf.create_shm(names["ring"], a.ring_mib << 20)
+    user_cap = 1 << max(12, int(np.ceil(np.log2(max(1, len(imgs[0].user)) * 24))))
+    user = rt.HostRing(user_cap, 64, names["user"])
+    spans = rt.HostRing(1 << max(12, int(np.ceil(np.log2(a.spans * 24)))), 64, names["spans"])
+    cuts = rt.HostRing(1 << 12, 64, names["cuts"])
+    n_flat = a.warmup + a.steps
+    period = a.events / 1e6  # 1M events/s per node agent (config 5)
+    ctx = mp.get_context("fork")
+    conn_parent, conn_child = ctx.Pipe()
+    prod = ctx.Process(target=producer_main, args=(names, imgs, himgs, (n_flat, a.paced_windows, period), conn_child),
+                       daemon=True)
+    prod.start()
 
-    def run(n, start):
-        for i in range(n):
-            pipe.submit(stage(start + i))
+    # ---- GPU ------------------------------------------------------------------------------
+    import torch
+    import torch.distributed as dist
 
-    # ---- warmup (also the model's first training windows) ------------------------------
-    run(a.warmup, 0)
+    from llm_slo_ebpf_toolkit_amd.ops import require_gpu_extension
+    from llm_slo_ebpf_toolkit_amd.parallel.numa import bind_to_device_numa
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline
+    from llm_slo_ebpf_toolkit_amd.safety import CPUMeter, OverheadGuard, read_rss_mb
+
+    require_gpu_extension()
+    torch.cuda.set_device(local)
+    numa_cpus = bind_to_device_numa(local)
+    conn_parent.send(sorted(numa_cpus) if numa_cpus else None)
+    pg = None
+    comm = None
+    if world > 1:
+        # control plane over gloo (barriers, the RCCL id, timing max); the data plane -- the
+        # per-window packet all-reduce -- is the engine's own RCCL communicator over xGMI
+        dist.init_process_group("gloo")
+        pg = dist.group.WORLD
+        uid = [rt_uid() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = (uid[0], rank, world)
+    pipe = WindowPipeline(a.events, a.spans, a.services, local, comm, model=a.model, seed=a.seed,
+                          use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers)
+    src = RingWindowSource(pipe, rb, user, spans, threads=threads, cfg_set=lambda i, v: None)
+    keys = np.array(sorted(pod_sn), dtype=np.uint32)
+    src.tables.set_pods(keys, np.array([pod_sn[k] for k in keys.tolist()], dtype=np.uint32))
+    wait_s = [0.0]
+
+    def next_cut(sleep=20e-6) -> Cut:
+        t0 = time.perf_counter()
+        while cuts.size == 0:
+            if not prod.is_alive():
+                raise RuntimeError("producer exited early")
+            time.sleep(sleep)
+        seg = cuts.peek(1)[0]
+        rec = cuts.records_view()[seg[1] * 64:(seg[1] + 1) * 64].view(np.uint64).copy()
+        cuts.release(1)
+        wait_s[0] += time.perf_counter() - t0
+        return Cut(kernel=int(rec[0]), user=int(rec[1]), spans=int(rec[2]),
+                   bases=tuple(int(x) for x in rec[3:7].astype(np.int64)))
+
+    def step(j, with_labels=True, learn=None, sleep=20e-6):
+        img = imgs[j % len(imgs)]
+        c = next_cut(sleep)
+        r = src.stage(c, img.n_groups, img.labels)
+        return pipe.submit(r["dma_bytes"], img.n_groups, with_labels=with_labels, learn=learn), r
+
+    # ---- warmup (also the model's first training windows) ---------------------------------
+    for j in range(a.warmup):
+        step(j)
     pipe.drain()
     if pg is not None:
         dist.barrier()
     pipe.reset_totals()
-    enc0, nstage0 = stager.encode_s, stager.k
+    host0, n0 = src.host_s, src.n
+    wait_s[0] = 0.0
 
-    # ---- timed region -------------------------------------------------------------------
+    # ---- timed region ----------------------------------------------------------------------
     meter = CPUMeter()
     torch.cuda.synchronize()
     if pg is not None:
@@ -173,18 +237,23 @@ def main() -> int:
     torch.cuda.synchronize()
     meter.start()
     t0 = time.perf_counter()
-    run(a.steps, a.warmup)
+    last = None
+    kernel_recs = 0
+    for j in range(a.warmup, a.warmup + a.steps):
+        last, r = step(j)
+        kernel_recs += r["n_kernel"]
     pipe.drain()
     torch.cuda.synchronize()
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    host_us = pipe.host_issue_us()
-    encode_ms = 1e3 * (stager.encode_s - enc0) / max(stager.k - nstage0, 1)
     busy_cpu_pct, _, _ = meter.stop()
+    dev_ms = [pipe.window_ms(k) for k in range(max(0, last - pipe.nb + 1), last + 1)]
+    host_us = 1e6 * (src.host_s - host0) / max(src.n - n0, 1)
+    producer_wait_ms = 1e3 * wait_s[0]
     if pg is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     summ = pipe.summary()
@@ -192,55 +261,60 @@ def main() -> int:
     value = events_total / elapsed
     ms_per_step = 1e3 * elapsed / a.steps
 
-    # ---- CPU overhead at the config-5 rate (1M events/s per node agent), REF formula -----
-    cpu_pct = None
+    # ---- agent CPU overhead at config 5's rate (1M events/s), REF formula -----------------
+    cpu_pct = ref_pct = None
     lat_ms = []
     if a.paced_windows > 0:
         guard = OverheadGuard(3.0)
-        guard.evaluate()  # prime (REF: first call only primes)
+        guard.evaluate()  # REF: the first call only primes
         meter.start()
-        period = a.events / 1e6  # seconds per window at 1M events/s
-        nxt = time.perf_counter()
-        for i in range(a.paced_windows):
-            ts = time.perf_counter()
-            pipe.submit(stage(i))
-            ev = torch.cuda.Event()
-            ev.record(pipe.comm_stream)
-            nxt += period
-            while not ev.query():
-                time.sleep(0.0005)
-            lat_ms.append(1e3 * (time.perf_counter() - ts))
-            time.sleep(max(0.0, nxt - time.perf_counter()))
-        cpu_pct, cpu_s, wall_s = meter.stop()
+        for j in range(a.paced_windows):
+            k, _ = step(j, sleep=2e-3)
+            pipe.wait(k)
+            lat_ms.append(pipe.window_ms(k)[0])
+        cpu_pct, _, _ = meter.stop()
         ref_pct, _ = guard.evaluate()
-        log(f"paced: cpu {cpu_pct:.3f}% of one core (REF tick formula {ref_pct:.2f}%), "
-            f"window latency p50 {np.median(lat_ms):.2f} ms")
+        log(f"paced: cpu {cpu_pct:.3f}% of one core (REF tick formula {ref_pct:.2f}%)")
         if pg is not None:
-            ct = torch.tensor([cpu_pct], dtype=torch.float64, device="cuda")
+            ct = torch.tensor([cpu_pct], dtype=torch.float64)
             dist.all_reduce(ct, op=dist.ReduceOp.MAX)
             cpu_pct = float(ct.item())
 
-    # ---- REF 55-row dataset through the GPU posterior kernel -----------------------------
+    # ---- held-out attribution: frozen model, windows of another seed ------------------------
+    from llm_slo_ebpf_toolkit_amd.models.metrics import macro_f1_from_confusion
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    held_conf = {"full": np.zeros((16, 16)), "mixed": np.zeros((16, 16))}
+    for j, h in enumerate(himgs):
+        c = next_cut(2e-3)
+        r = src.stage(c, h.n_groups, h.labels)
+        k = pipe.submit(r["dma_bytes"], h.n_groups, with_labels=True, learn=False)
+        held_conf["mixed" if j % 2 else "full"] += pipe.packet(k)["confusion"]
+    D = len(catalog.ALL_DOMAINS)
+    heldout = {}
+    for name, cm in held_conf.items():
+        if pg is not None:
+            t_ = torch.from_numpy(cm.copy())
+            dist.all_reduce(t_)
+            cm = t_.numpy()
+        cm = cm[:D, :D].astype(np.int64)
+        if cm.sum():
+            heldout[name] = {"macro_f1": round(macro_f1_from_confusion(cm), 4),
+                             "accuracy": round(float(np.trace(cm) / cm.sum()), 4), "incidents": int(cm.sum()),
+                             "confusion": cm.tolist()}
+
+    # ---- REF 55-row dataset through the GPU posterior kernel --------------------------------
     ref_f1 = {}
     fx = os.path.join(ROOT, "tests", "fixtures", "ref_multi_fault_samples.jsonl")
     if rank == 0 and os.path.exists(fx):
-        samples = [s for s in load_samples_jsonl(fx) if s.expected_domain]
-        vals, labels = samples_to_arrays(samples)
-        eng = pipe.engine
-        for name, model in (("bayes_ref", NaiveBayes.ref()), (a.model, pipe.host_model())):
-            eng.set_model(model)
-            eng.eng.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
-            eng.eng.counts[:4].copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
-            eng.eng.bind_io(eng.eng.counts, eng.eng.labels, eng.eng.packet)
-            eng.eng.posterior(False)
-            pred = eng.eng.pred[: len(samples)].cpu().numpy()
-            ref_f1[name] = macro_f1([catalog.ALL_DOMAINS[i] for i in labels], [catalog.ALL_DOMAINS[i] for i in pred])
+        ref_f1 = ref55_gpu(fx, pipe.host_model(), a.model)
+    prod.join(timeout=30)
 
     conf = summ["confusion"]
     dbg = summ["dbg"]
     res = {
-        "metric": "fault-replay attribution throughput (events/s), node-wide; attribution macro-F1 on the "
-                  "fault-replay confusion matrix and agent CPU overhead % reported alongside",
+        "metric": "fault-replay attribution throughput through the agent's BPF-ring -> GPU path (events/s, "
+                  "node-wide); held-out attribution macro-F1 and agent CPU overhead % reported alongside",
         "value": round(value, 1),
         "unit": "events/s",
         "n_gpus": world,
@@ -249,9 +323,10 @@ def main() -> int:
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_EVENTS_PER_S, 1),
+        "vs_baseline": None,  # REF publishes no measured throughput (its 900 events/s is a constant)
         "dtype": "fp64 posteriors / fp32 features (exact-int64 time joins)",
-        "data": "synthetic fault-replay traces (seeded, REF fault profiles), random-init attribution priors",
+        "data": "synthetic fault-replay traces (seeded, REF fault profiles) through the native probe model into an "
+                "emulated BPF ring buffer; random-init attribution priors",
         "config": {
             "model": f"config5: 16 signals (12 kernel + 4 GPU) x 10 fault domains, {a.model}, 4-tier LDS join",
             "global_batch": world * a.events,
@@ -260,24 +335,31 @@ def main() -> int:
             "spans_per_window_per_gpu": a.spans,
             "incidents_per_window_per_gpu": a.services,
             "scenario": a.scenario,
-            "wire_bytes_per_event": records.wire_bytes(a.wire),
-            "wire_record": {"20t": "EVENT20T", "24": "EVENT24", "32": "EVENT32", "64": "EVENT", "20": "EVENT20",
-                            "16": "EVENT16 (host-encoded)", "16t": "EVENT16 (probe ring, epoch-tagged)"}[a.wire_name],
+            "source": "BPF ring buffer (kernel layout, emulated in shm) + rocprof/user-space ring + span ring",
+            "wire_bytes_per_event": 16,
+            "ring_bytes_per_kernel_event": 24,
             "device_buffers": a.buffers,
         },
-        "macro_f1": round(summ["macro_f1"], 4),
-        "vs_baseline_macro_f1": round(summ["macro_f1"] / BASELINE_MACRO_F1, 4),
-        "attribution_accuracy": round(summ["accuracy"], 4),
-        "incidents_scored": int(conf.sum()),
-        "agent_cpu_overhead_pct": None if cpu_pct is None else round(cpu_pct, 4),
-        "agent_cpu_overhead_pct_busy_loop": round(busy_cpu_pct, 2),
-        "agent_rss_mb": round(read_rss_mb(os.getpid()), 1),
-        "window_latency_ms_p50": round(float(np.median(lat_ms)), 3) if lat_ms else None,
+        "macro_f1_heldout": heldout,
+        "vs_baseline_macro_f1_heldout": round(heldout["mixed"]["macro_f1"] / BASELINE_MACRO_F1, 4)
+        if "mixed" in heldout else None,
         "ref55_single_fault_macro_f1": {k: round(v, 4) for k, v in ref_f1.items()},
+        "vs_baseline_ref55_macro_f1": round(ref_f1[a.model] / BASELINE_MACRO_F1, 4) if a.model in ref_f1 else None,
+        "macro_f1_prequential": round(summ["macro_f1"], 4),
+        "incidents_scored_prequential": int(conf.sum()),
+        "agent_cpu_overhead_pct": None if cpu_pct is None else round(cpu_pct, 4),
+        "agent_cpu_overhead_pct_ref_ticks": None if ref_pct is None else round(ref_pct, 3),
+        "agent_cpu_overhead_pct_flat_out": round(busy_cpu_pct, 2),
+        "bench_process_rss_mb": round(read_rss_mb(os.getpid()), 1),
+        "window_device_ms_dma_to_results": round(float(np.median([d[0] for d in dev_ms])), 3) if dev_ms else None,
+        "window_device_ms_compute": round(float(np.median([d[1] for d in dev_ms])), 3) if dev_ms else None,
+        "paced_window_latency_ms": round(float(np.median(lat_ms)), 3) if lat_ms else None,
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
-        "host_issue_us_per_window": {k: round(v, 1) for k, v in host_us.items()},
-        "host_encode_ms_per_window": round(encode_ms, 3),
-        "host_encode_threads": threads if a.wire_name in ("16", "20") else 0,
+        "kernel_ring_records_per_step": int(kernel_recs // max(a.steps, 1)),
+        "host_assemble_us_per_window": round(host_us, 1),
+        "host_issue_us_per_window": round(pipe.eng.host_issue_us, 1),
+        "producer_wait_ms_total": round(producer_wait_ms, 2),
+        "host_threads": threads,
         "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
     }
     if rank == 0:
@@ -290,6 +372,37 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def rt_uid() -> bytes:
+    from llm_slo_ebpf_toolkit_amd.ops import load_agent
+
+    return load_agent().unique_id()
+
+
+def ref55_gpu(fx: str, learned, model_name: str):
+    """REF's 55-row attribution set through the GPU posterior kernel (torch test engine), with
+    REF's model and with the learned model; macro-F1 over the 30 single-fault rows."""
+    import numpy as np
+    import torch
+
+    from llm_slo_ebpf_toolkit_amd.models import load_samples_jsonl, macro_f1
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, samples_to_arrays
+    from llm_slo_ebpf_toolkit_amd.ops.engine import GpuEngine
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    samples = [s for s in load_samples_jsonl(fx) if s.expected_domain]
+    vals, labels = samples_to_arrays(samples)
+    eng = GpuEngine(64, 64, 64)
+    out = {}
+    for name, model in (("bayes_ref", NaiveBayes.ref()), (model_name, learned)):
+        eng.set_model(model)
+        eng.eng.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
+        eng.eng.counts[:4].copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
+        eng.eng.posterior(False)
+        pred = eng.eng.pred[: len(samples)].cpu().numpy()
+        out[name] = macro_f1([catalog.ALL_DOMAINS[i] for i in labels], [catalog.ALL_DOMAINS[i] for i in pred])
+    return out
 
 
 if __name__ == "__main__":

@@ -9,14 +9,15 @@ Two engines share one process, one Prometheus registry and one set of outputs:
   rate-limited), attributes the sample with naive Bayes when a webhook is configured, and
   evaluates the overhead guard, shedding the highest-cost signal when over budget
   (REF cmd/agent/main.go:515-604).
-* ``gpu`` (``run_windows``): records from probe producers (native shared-memory rings
-  fed by the BPF loader / the rocprofiler-sdk tool library, or the seeded replay
-  generator) are cut into windows and pushed through ``WindowPipeline`` on this node's
-  MI355X: K1 decode -> K2 LDS join -> K3 MFMA posterior (+ RCCL packet all-reduce when
-  several GPUs share the node). Per window the agent folds the kernel histograms into the
-  Prometheus histograms (no per-event Python work), and emits one IncidentAttribution per
-  incident group whose top posterior clears ``min_confidence``, over the same outputs and
-  webhook. Everything per-event stays on the device; the host does O(groups) work.
+* ``gpu`` (``run_windows``): the probes' BPF ring buffer (pinned ``mislo_events``; or the
+  shared-memory emulation), the rocprofiler-sdk tool's / services' user-space event ring and
+  the span ring are cut into windows (epoch published into ``mislo_cfg`` at each cut) and
+  assembled natively into the native window engine's pinned blocks on this node's MI355X:
+  K1 decode -> K2 LDS join -> K3 MFMA posterior (+ RCCL packet all-reduce when several GPUs
+  share the node). Per window the agent folds the kernel histograms into the Prometheus
+  histograms and emits one IncidentAttribution per incident group whose top posterior clears
+  ``min_confidence``, over the same outputs and webhook. No per-event Python work and no
+  PyTorch in the process; the host does O(groups) work per window.
 """
 
 from __future__ import annotations
@@ -26,7 +27,7 @@ import sys
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Callable, Iterator, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
@@ -153,8 +154,9 @@ class AgentOptions:
     metrics_bind: str = ":2112"
     # GPU window engine (additive)
     engine: str = "synthetic"            # synthetic | gpu
-    source: str = "replay"               # replay | ring
+    source: str = "replay"               # bpf | shm | replay
     ring_name: str = "/mislo-agent"
+    pin_dir: str = "/sys/fs/bpf/mislo"
     window_ms: int = 1000
     window_events: int = 1 << 20
     window_spans: int = 16384
@@ -162,7 +164,8 @@ class AgentOptions:
     device: int = 0
     model: str = "bayes"
     min_confidence: float = 0.5
-    wire: int = 16
+    host_threads: int = 2
+    slo_target: float = 0.99             # TTFT SLO objective (burn rate = breach fraction / (1 - target))
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -344,169 +347,139 @@ class Agent:
         return 0
 
     # ---- GPU window engine ----------------------------------------------------------------
-    def _window_source(self) -> Iterator:
-        """Yields (StagedWindow, group_names, t0_ns) per window."""
+    def _open_source(self):
+        """Rings + maps for the configured source. ``bpf``: the probes' pinned maps (root);
+        ``shm``: emulated rings another process produces into (tests, CI); ``replay``: a forked
+        replay producer writing seeded fault-replay windows at window_events per window_ms
+        (stands in for the kernel probes and the rocprofiler tool: its CPU is not the agent's).
+        Returns (maps, ring, user ring, span ring, pod metadata or None)."""
+        from ..collector import bpf
+        from ..runtime import load
+
         o = self.o
+        rt = load()
+        names = bpf.RingNames.of(o.ring_name)
+        if o.source == "bpf":
+            maps = bpf.BpfMaps(o.pin_dir)
+            user = rt.HostRing(1 << 20, 64, names.user)   # rocprofiler tool / services attach and push
+            spans = rt.HostRing(1 << 18, 64, names.spans)  # OTLP receiver / services
+            return maps, maps.ring, user, spans, None
+        if o.source == "shm":
+            ring = rt.Ringbuf.attach_shm(names.ring)
+            return (bpf.EmulatedMaps(ring), ring, rt.HostRing(0, 64, names.user, True),
+                    rt.HostRing(0, 64, names.spans, True), None)
         if o.source == "replay":
-            from ..pipeline.replay import ReplayConfig, ReplayGenerator
+            kw = dict(scenario=o.scenario if o.scenario not in ("baseline",) else "full",
+                      events_per_window=o.window_events, spans_per_window=o.window_spans,
+                      n_services=o.window_groups)
+            ring, user, spans = bpf.create_rings(names, 4 * 24 * o.window_events, 4 * o.window_events,
+                                                 4 * o.window_spans)
+            self._producer = bpf.start_replay_producer(names, kw, o.window_events * 1000.0 / o.window_ms,
+                                                       o.window_ms, max_windows=0)
+            return bpf.EmulatedMaps(ring), ring, user, spans, bpf.pod_metadata(kw)
+        raise ValueError(f"unknown window source {o.source!r} (bpf | shm | replay)")
 
-            gen = ReplayGenerator(ReplayConfig(scenario=o.scenario if o.scenario != "baseline" else "full",
-                                               events_per_window=o.window_events, spans_per_window=o.window_spans,
-                                               n_services=o.window_groups, window_ms=o.window_ms))
-            # The replay producer stands in for the BPF / rocprofiler producers, which run
-            # outside the agent and write records in the wire format: pre-generate and
-            # pre-stage a few windows and cycle them, so the agent's overhead guard
-            # measures the agent, not the synthetic trace generator.
-            import torch
-
-            from ..collector.records import ConnInterner, native_encoder
-            from ..pipeline.window import stage_window
-
-            it, enc = ConnInterner(), native_encoder()
-            pool = []
-            for _ in range(4):
-                w = gen.next_window()
-                pool.append(stage_window(torch, w.events, w.spans, min(w.n_groups, o.window_groups), None,
-                                         o.window_groups, None, wire=o.wire, interner=it, encoder=enc))
-            names = [f"svc-{g + 1}" for g in range(o.window_groups)]
-            i = 0
-            while True:
-                yield pool[i % len(pool)], names, now_ns()
-                i += 1
-        elif o.source == "ring":
-            import torch
-
-            from ..pipeline.window import stage_window
-
-            from ..collector.records import ConnInterner, native_encoder
-
-            # ring records are 64-byte EVENTs; the native encoder converts each window to the
-            # configured wire format (one encoder per stream keeps ids consistent)
-            it, enc = ConnInterner(), native_encoder()
-            src = RingSource(o.ring_name, o.window_events, o.window_spans)
-            for ev, sp, n_groups, names, t0 in src.windows(o.window_ms, self.stop_event, o.window_groups):
-                yield stage_window(torch, ev, sp, n_groups, None, o.window_groups, None, wire=o.wire, interner=it,
-                                   encoder=enc), names, t0
-        else:
-            raise ValueError(f"unknown window source {o.source!r}")
-
-    def _attributions(self, G: int, names: Sequence[str], post: np.ndarray, pred: np.ndarray,
-                      bits: np.ndarray, t_ns: int, model) -> List[IncidentAttribution]:
+    def _attributions(self, G: int, names: Sequence[str], res: dict, sli: Optional[np.ndarray], t_ns: int,
+                      model) -> List[IncidentAttribution]:
+        """One IncidentAttribution per incident group whose top posterior clears min_confidence.
+        Evidence carries the group's measured signal values (mean over joined kernel signals);
+        SLO impact comes from the group's spans in the window (TTFT SLO breach fraction over the
+        error budget = burn rate), not from constants."""
         out = []
         D = model.weights.shape[1]
+        post, bits, feat = res["post"], res["evbits"].view(np.uint32), res["feat"]
         for g in range(G):
             ranked = model.ranked(post[g, :D], bits[g, :D])
             if not ranked or ranked[0].posterior < self.o.min_confidence:
                 continue
             top = ranked[0]
+            ev = []
+            for sname in top.evidence:
+                spec = catalog.BY_NAME[sname]
+                v = float(feat[g, spec.slot])
+                ev.append(Evidence(spec.semconv or sname, round(v, 3) if np.isfinite(v) else "elevated", "ebpf"))
+            if not ev:
+                ev = [Evidence("llm.ebpf.correlation_confidence", float(top.posterior), "ebpf")]
+            n, breach = (sli[g, 0], sli[g, 1]) if sli is not None and g < sli.shape[0] else (0.0, 0.0)
+            budget = max(1e-6, 1.0 - self.o.slo_target)
+            burn = float(breach / n / budget) if n else 0.0
             out.append(IncidentAttribution(
                 incident_id=f"gpu-{t_ns}-{g:03d}", timestamp=t_ns, cluster=self.o.cluster,
                 namespace=self.o.namespace, service=names[g] if g < len(names) else f"group-{g}",
-                predicted_fault_domain=top.domain, confidence=float(top.posterior),
-                evidence=[Evidence(catalog.BY_NAME[s].semconv or s, "elevated", "ebpf") for s in top.evidence] or
-                [Evidence("llm.ebpf.correlation_confidence", float(top.posterior), "ebpf")],
-                slo_impact=SLOImpact("ttft_ms", 2.0, 5),
+                predicted_fault_domain=top.domain, confidence=float(top.posterior), evidence=ev,
+                slo_impact=SLOImpact("ttft_ms", round(burn, 4), max(1, int(round(self.o.window_ms / 60000.0)) or 1)),
                 fault_hypotheses=[FaultHypothesis(p.domain, p.posterior, p.evidence) for p in ranked
                                   if p.posterior >= 0.01]))
         return out
 
-    def run_windows(self, max_windows: int = 0, process_group=None) -> int:
-        """GPU engine main loop (one process per MI355X; ``process_group`` = RCCL node group)."""
-        import torch
+    def _emit_window(self, pipe, k: int, t_ns: int, G: int, names, n_events: int, sli) -> None:
+        pk = pipe.packet(k)
+        lat_ms = pipe.window_ms(k)[0]
+        self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], n_events, lat_ms, self.o.node, self.o.pod,
+                                    self.o.namespace)
+        res = pipe.results(k, G)
+        for attr in self._attributions(G, names, res, sli, t_ns, pipe.model):
+            self.metrics.observe_attribution(attr.predicted_fault_domain)
+            self.writers.emit_attribution(attr)
+            self.attributions_emitted += 1
+            if self.webhook is not None:
+                try:
+                    self.webhook.send(attr)
+                except Exception as exc:  # noqa: BLE001
+                    self.metrics.inc_dropped("emit")
+                    print(f"webhook send failed: {exc}", file=sys.stderr)
 
-        from ..pipeline.window import WindowPipeline
+    def run_windows(self, max_windows: int = 0, comm=None) -> int:
+        """GPU engine main loop (one process per MI355X; ``comm`` = (RCCL unique id, rank, world)).
+
+        Every window_ms: cut (publish epoch k, snapshot the rings) -> native assembly into the
+        engine's pinned block -> submit (DMA + captured graph + packet all-reduce), with no
+        drain: window k-1's results, complete by now, are turned into metrics and attributions
+        while window k computes."""
+        from ..pipeline.window import RingWindowSource, WindowPipeline
 
         o = self.o
-        torch.cuda.set_device(o.device)
-        pipe = WindowPipeline(o.window_events, o.window_spans, o.window_groups, o.device, process_group,
-                              model=o.model, learn=False)
-        source = self._window_source()
-        first = next(source)  # producer warm-up happens before the guard's first sample
+        maps, ring, user, spans, pods = self._open_source()  # a replay producer forks here, before the GPU
+        node_id = (abs(hash(o.node)) % 0xFFFE) + 1
+        maps.init(node_id)
+        pipe = WindowPipeline(o.window_events, o.window_spans, o.window_groups, o.device, comm, model=o.model,
+                              learn=False, window_ms=2000.0)
+        src = RingWindowSource(pipe, ring, user, spans, threads=o.host_threads, cfg_set=maps.cfg_set)
+        if pods is not None:
+            src.tables.set_pods(*pods)
+        names = [f"svc-{g + 1}" for g in range(o.window_groups)]
+        G = o.window_groups
         if self.guard is not None:
             self.guard.evaluate()
         self.ready = True
         period = o.window_ms / 1000.0
-        nxt = time.monotonic()
-        import itertools
-
-        for w, names, t0 in itertools.chain([first], source):
+        nxt = time.monotonic() + period
+        pending = None
+        while not self.stop_event.is_set():
+            self.stop_event.wait(max(0.0, nxt - time.monotonic()))
             if self.stop_event.is_set():
                 break
-            t_start = time.perf_counter()
-            pipe.submit(w, with_labels=False)
-            pipe.drain()
-            e = pipe.eng
-            pk = pipe.last_packet()
-            lat_ms = 1e3 * (time.perf_counter() - t_start)
-            self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], w.n_events, lat_ms, o.node, o.pod,
-                                        o.namespace)
-            G = w.n_groups
-            post = e.post[:G].cpu().numpy()
-            pred = e.pred[:G].cpu().numpy()
-            bits = e.evbits[:G].cpu().numpy().view(np.uint32)
-            for attr in self._attributions(G, names, post, pred, bits, t0 or now_ns(), pipe.model):
-                self.metrics.observe_attribution(attr.predicted_fault_domain)
-                self.writers.emit_attribution(attr)
-                self.attributions_emitted += 1
-                if self.webhook is not None:
-                    try:
-                        self.webhook.send(attr)
-                    except Exception as exc:  # noqa: BLE001
-                        self.metrics.inc_dropped("emit")
-                        print(f"webhook send failed: {exc}", file=sys.stderr)
+            nxt += period
+            cut = src.cut()
+            r = src.stage(cut, G)
+            k = pipe.submit(r["dma_bytes"], G, with_labels=False, learn=False)
+            if pending is not None:
+                self._emit_window(pipe, *pending)
+            pending = (k, cut.t_ns, G, names, int(r["n_events"]), src.group_sli())
+            self.metrics.set_ring(ring.stats() if hasattr(ring, "stats") else {}, r)
             self._guard_tick()
             self.metrics.set_heartbeat()
             self.windows_done += 1
             if max_windows and self.windows_done >= max_windows:
                 break
-            nxt += period
-            if o.source == "replay":
-                self.stop_event.wait(max(0.0, nxt - time.monotonic()))
+            if maps.ctx_ids_used() > (7 << 20) and hasattr(maps, "reset_ctx_ids"):
+                maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
+        if pending is not None:
+            self._emit_window(pipe, *pending)
+        pipe.drain()
+        self.last_pipe = pipe
         self.writers.flush()
         return 0
-
-
-class RingSource:
-    """Windows cut from the native shared-memory rings that probe producers write into
-    (``/<name>-events`` 64-byte EVENT records, ``/<name>-spans`` SPAN records).
-
-    The C ABI (runtime/csrc/ring.h) lets the BPF ring-buffer reader and the
-    rocprofiler-sdk tool library (``tools/rocprof_tool``) push without Python; the agent
-    drains whatever arrived each window (O(1) per window, two segments at most)."""
-
-    def __init__(self, name: str, max_events: int, max_spans: int):
-        from ..collector import records
-        from ..runtime import load
-
-        rt = load()
-        cap_e = 1 << max(1, (max_events * 4 - 1).bit_length())
-        cap_s = 1 << max(1, (max_spans * 4 - 1).bit_length())
-        self.events = rt.HostRing(cap_e, 64, name + "-events")
-        self.spans = rt.HostRing(cap_s, 64, name + "-spans")
-        self.max_events, self.max_spans = max_events, max_spans
-        self._ev_dtype, self._sp_dtype = records.EVENT, records.SPAN
-
-    @staticmethod
-    def _drain(ring, limit: int, dtype) -> np.ndarray:
-        segs = ring.peek(limit)
-        view = ring.records_view()
-        parts = []
-        n = 0
-        for _pos, idx, cnt in segs:
-            parts.append(np.frombuffer(view[idx * 64:(idx + cnt) * 64].tobytes(), dtype=dtype))
-            n += cnt
-        ring.release(n)
-        return np.concatenate(parts) if parts else np.zeros(0, dtype=dtype)
-
-    def windows(self, window_ms: int, stop: threading.Event, n_groups: int) -> Iterator:
-        period = window_ms / 1000.0
-        nxt = time.monotonic() + period
-        while not stop.is_set():
-            stop.wait(max(0.0, nxt - time.monotonic()))
-            nxt += period
-            ev = self._drain(self.events, self.max_events, self._ev_dtype)
-            sp = self._drain(self.spans, self.max_spans, self._sp_dtype)
-            yield ev, sp, n_groups, [f"group-{g}" for g in range(n_groups)], now_ns()
 
 
 def run_forever(agent: Agent, fn: Callable[[], int]) -> int:

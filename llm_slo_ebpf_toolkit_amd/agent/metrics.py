@@ -56,6 +56,12 @@ class AgentMetrics:
         self.corr = r.counter("llm_slo_agent_correlation_pairs_total",
                               "Span/signal correlation outcomes (REF DebugStats) from the join kernel.", ("outcome",))
         self.ring_dropped = r.gauge("llm_slo_agent_ring_dropped_events", "Events dropped by full producer rings.")
+        self.ring_defs = r.counter("llm_slo_agent_ring_definitions_total",
+                                   "Context / trace id definition records consumed from the BPF ring.")
+        self.ring_busy = r.counter("llm_slo_agent_ring_busy_stops_total",
+                                   "Windows whose ring consumption stopped at a record still being written.")
+        self.ring_backlog = r.gauge("llm_slo_agent_ring_backlog_bytes", "Unconsumed bytes in the BPF ring buffer.")
+        self.host_us = r.gauge("llm_slo_agent_window_host_us", "Host time to assemble the last window (us).")
         self.up.set(1)
         for k in EVENT_KINDS:
             self.kind.set(1 if k == event_kind else 0, k)
@@ -113,6 +119,17 @@ class AgentMetrics:
         self.corr.inc(float(max(0, low - overlap)), "low_confidence")
         self.corr.inc(float(dropped), "fanout_dropped")
         self.corr.inc(float(enriched), "span_enriched")
+
+    def set_ring(self, ring_stats: dict, assembled: dict) -> None:
+        """Per-window ring accounting: definitions consumed, busy stops, backlog, drops
+        (the emulated ring counts failed reservations; the kernel's are invisible to user space)."""
+        self.ring_defs.inc(float(assembled.get("n_defs", 0)))
+        if assembled.get("busy_stop"):
+            self.ring_busy.inc()
+        if ring_stats:
+            self.ring_backlog.set(float(ring_stats.get("producer_pos", 0) - ring_stats.get("consumer_pos", 0)))
+            self.ring_dropped.set(float(ring_stats.get("dropped", 0)))
+        self.host_us.set(float(assembled.get("host_us", 0.0)))
 
     def observe_attribution(self, domain: str) -> None:
         self.attr.inc(1, domain)

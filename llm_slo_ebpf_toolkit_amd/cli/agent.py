@@ -1,8 +1,9 @@
 """`agent`: node DaemonSet process (REF cmd/agent/main.go:269-633; flags :334-373).
 
 REF flags are all accepted with REF defaults. Additive flags select the MI355X window
-engine: ``--engine gpu --source replay|ring --window-ms --window-events --device
---model --min-confidence --wire``; ``--count`` bounds the number of windows in GPU mode.
+engine: ``--engine gpu --source bpf|shm|replay --pin-dir --window-ms --window-events --device
+--model --min-confidence --host-threads --slo-target``; ``--count`` bounds the number of
+windows in GPU mode.
 """
 
 from __future__ import annotations
@@ -45,8 +46,9 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("metrics-bind", d.metrics_bind, "metrics and health bind address"),
         ("probe-smoke", False, "run eBPF smoke check and exit"),
         ("engine", d.engine, "attribution engine: synthetic (REF tick loop) | gpu (MI355X window engine)"),
-        ("source", d.source, "gpu engine record source: replay | ring"),
-        ("ring-name", d.ring_name, "shared-memory ring name prefix for --source ring"),
+        ("source", d.source, "gpu engine record source: bpf (pinned probe maps) | shm (emulated rings) | replay"),
+        ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
+        ("pin-dir", d.pin_dir, "bpffs directory the probe loader pinned the maps in (--source bpf)"),
         ("window-ms", d.window_ms, "gpu engine window length"),
         ("window-events", d.window_events, "gpu engine events per window (capacity)"),
         ("window-spans", d.window_spans, "gpu engine spans per window (capacity)"),
@@ -54,7 +56,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("device", d.device, "HIP device ordinal"),
         ("model", d.model, "attribution model: bayes|bayes_learned|lda"),
         ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
-        ("wire", d.wire, "event record format on PCIe: 16 (EVENT16) | 20 (EVENT20) | 21 (EVENT20T, 20 bytes) | 24 | 32 (compact) | 64"),
+        ("host-threads", d.host_threads, "host threads compacting the ring per window"),
+        ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),
     ]:
         p.flag(name, default, help_)
     a = p.parse_args(argv)
@@ -67,9 +70,10 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         capability_mode=a.capability_mode, disable_signals=split_csv(a.disable_signals),
         disable_overhead_guard=a.disable_overhead_guard, config=a.config, enable_hello_tracer=a.enable_hello_tracer,
         hello_target_comm=split_csv(a.hello_target_comm), enable_real_probe_metrics=a.enable_real_probe_metrics,
-        metrics_bind=a.metrics_bind, engine=a.engine, source=a.source, ring_name=a.ring_name,
+        metrics_bind=a.metrics_bind, engine=a.engine, source=a.source, ring_name=a.ring_name, pin_dir=a.pin_dir,
         window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
-        window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence, wire=a.wire)
+        window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
+        host_threads=a.host_threads, slo_target=a.slo_target)
     return o, a.probe_smoke
 
 
@@ -94,9 +98,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     agent.start_server()
     agent.start_hello_tracer()
     if opts.engine == "gpu":
-        from ..ops import require_gpu_extension
+        from ..ops import load_agent
 
-        require_gpu_extension()
+        load_agent()  # the native engine must be built: fail loudly, never fall back
         return run_forever(agent, lambda: agent.run_windows(max_windows=opts.count))
     try:
         return run_forever(agent, agent.run_synthetic)

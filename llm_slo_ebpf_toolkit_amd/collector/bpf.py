@@ -1,0 +1,270 @@
+"""The agent's side of the probes' maps, and the producers that stand in for the kernel.
+
+REF designs a kernel -> user path (pkg/collector/ringbuf.go:56-150, probe_manager.go:25-185)
+that no binary constructs. NEW's agent opens the maps the loader pinned (``make ebpf-gen`` +
+``bpftool prog loadall ... pinmaps /sys/fs/bpf/mislo``; probes/ebpf/Makefile) with raw bpf(2):
+
+* ``mislo_events`` -- the BPF ring buffer the window source consumes (runtime/csrc/bpfring.h);
+* ``mislo_cfg``   -- the agent writes the realtime-monotonic clock offset, the node id, the
+  per-signal emit floors (the overhead guard raises floors before it detaches probes) and the
+  epoch it publishes at every window cut;
+* ``mislo_pods``  -- cgroup id -> pod id, filled from the node's cgroup tree (pods discovered
+  the way REF's ProcMetadataEnricher derives them, pkg/signals/metadata.go:95-118);
+* ``mislo_ctxs`` / ``mislo_traces`` -- the kernel's interning maps. The agent never reads them
+  per window: every new id reaches it as a definition record ahead of its first use in the
+  ring (mislo_probe.h MISLO_INTERN_DEF). It resets them when the context id space runs low.
+
+``EmulatedMaps`` gives the same interface over the emulated ring (tests, CI, the benchmark,
+``--source shm``); ``ReplayProducer`` is a separate process that writes seeded fault-replay
+windows into emulated rings exactly as the probes and the rocprofiler tool would.
+"""
+
+from __future__ import annotations
+
+import os
+import struct
+import time
+from dataclasses import dataclass
+from typing import Dict, Iterable, Optional, Tuple
+
+import numpy as np
+
+from . import records
+
+CFG_CLOCK, CFG_NODE, CFG_EPOCH, CFG_TRACE_NEXT, CFG_CTX_NEXT = 0, 1, 124, 125, 126
+PIN_DIR = "/sys/fs/bpf/mislo"
+
+
+def cfg_floor(signal_type: int) -> int:
+    return 2 + int(signal_type)
+
+
+def clock_offset_ns() -> int:
+    """CLOCK_REALTIME - CLOCK_MONOTONIC: what the probes add to bpf_ktime_get_ns()."""
+    return time.clock_gettime_ns(time.CLOCK_REALTIME) - time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+
+
+class MapSet:
+    """Common agent-side operations over the probes' maps."""
+
+    ring = None
+
+    def cfg_set(self, idx: int, value: int) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def cfg_get(self, idx: int) -> int:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def set_pod(self, cgroup_id: int, pod_id: int) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+    def init(self, node_id: int) -> None:
+        self.cfg_set(CFG_CLOCK, clock_offset_ns() & 0xFFFFFFFFFFFFFFFF)
+        self.cfg_set(CFG_NODE, int(node_id) & 0xFFFF)
+
+    def set_floor(self, signal_type: int, raw_value: int) -> None:
+        self.cfg_set(cfg_floor(signal_type), int(raw_value))
+
+    def ctx_ids_used(self) -> int:
+        return int(self.cfg_get(CFG_CTX_NEXT))
+
+
+class EmulatedMaps(MapSet):
+    """mislo_cfg lives in the emulated ring's meta page; pods in a dict."""
+
+    def __init__(self, ring):
+        self.ring = ring
+        self.pods: Dict[int, int] = {}
+
+    def cfg_set(self, idx: int, value: int) -> None:
+        self.ring.cfg_set(int(idx), int(value) & 0xFFFFFFFFFFFFFFFF)
+
+    def cfg_get(self, idx: int) -> int:
+        return int(self.ring.cfg_get(int(idx)))
+
+    def set_pod(self, cgroup_id: int, pod_id: int) -> None:
+        self.pods[int(cgroup_id)] = int(pod_id)
+
+
+class BpfMaps(MapSet):
+    """The maps the loader pinned under ``pin_dir`` (needs CAP_BPF / root)."""
+
+    def __init__(self, pin_dir: str = PIN_DIR):
+        from ..runtime import load
+
+        rt = load()
+        self.pin_dir = pin_dir
+        self.ring = rt.Ringbuf.open_pinned(os.path.join(pin_dir, "mislo_events"))
+        self.cfg = rt.BpfMap(os.path.join(pin_dir, "mislo_cfg"))
+        self.pods = rt.BpfMap(os.path.join(pin_dir, "mislo_pods"))
+        self._ctxs = os.path.join(pin_dir, "mislo_ctxs")
+
+    def cfg_set(self, idx: int, value: int) -> None:
+        self.cfg.update(struct.pack("<I", int(idx)), struct.pack("<Q", int(value) & 0xFFFFFFFFFFFFFFFF))
+
+    def cfg_get(self, idx: int) -> int:
+        v = self.cfg.lookup(struct.pack("<I", int(idx)))
+        return 0 if v is None else struct.unpack("<Q", v)[0]
+
+    def set_pod(self, cgroup_id: int, pod_id: int) -> None:
+        self.pods.update(struct.pack("<Q", int(cgroup_id)), struct.pack("<I", int(pod_id)))
+
+    def reset_ctx_ids(self) -> int:
+        """Clear mislo_ctxs and restart its id counter (the agent does this at a window cut when
+        the kernel's 2^23 context ids run low; rows are redefined as contexts reappear)."""
+        from ..runtime import load
+
+        m = load().BpfMap(self._ctxs)
+        keys, _ = m.items()
+        ks = m.info()["key_size"]
+        n = 0
+        for i in range(0, len(keys), ks):
+            n += bool(m.delete(keys[i:i + ks]))
+        self.cfg_set(CFG_CTX_NEXT, 0)
+        return n
+
+
+def discover_pods(cgroup_root: str = "/sys/fs/cgroup", interner=None) -> Dict[int, Tuple[int, str]]:
+    """cgroup id (the directory inode bpf_get_current_cgroup_id() returns on cgroup v2) -> (pod
+    id, pod uid) for every kubepods cgroup on the node; pod ids come from ``interner`` (a
+    signals.metadata.Interner over pod uids) so they stay stable across scans."""
+    from ..signals.metadata import Interner
+
+    interner = interner if interner is not None else Interner()
+    out: Dict[int, Tuple[int, str]] = {}
+    for dirpath, _dirs, _files in os.walk(cgroup_root):
+        base = os.path.basename(dirpath)
+        if "pod" not in base:
+            continue
+        uid = _pod_uid(base)
+        if not uid:
+            continue
+        try:
+            ino = os.stat(dirpath).st_ino
+        except OSError:
+            continue
+        out[ino] = (interner.id(uid), uid)
+    return out
+
+
+def _pod_uid(name: str) -> str:
+    """kubepods-burstable-pod<uid with _>.slice | pod<uid> -> uid (REF metadata.go:95-118)."""
+    i = name.find("pod")
+    if i < 0:
+        return ""
+    s = name[i + 3:]
+    for suffix in (".slice", ".scope"):
+        if s.endswith(suffix):
+            s = s[: -len(suffix)]
+    s = s.replace("_", "-")
+    return s if len(s) >= 32 and all(c in "0123456789abcdef-" for c in s.lower()) else ""
+
+
+# ---------------------------------------------------------------------------------------
+# replay producer (stands in for the kernel probes + the rocprofiler tool + instrumented services)
+# ---------------------------------------------------------------------------------------
+
+@dataclass
+class RingNames:
+    ring: str
+    user: str
+    spans: str
+
+    @staticmethod
+    def of(prefix: str) -> "RingNames":
+        return RingNames(prefix + "-bpf", prefix + "-events", prefix + "-spans")
+
+
+def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int):
+    """Create the emulated BPF ring and the two user-space rings (the agent owns them)."""
+    from ..runtime import load
+
+    rt = load()
+    pow2 = lambda n: 1 << max(12, int(np.ceil(np.log2(max(1, n)))))  # noqa: E731
+    return (rt.Ringbuf.create_shm(names.ring, pow2(ring_bytes)), rt.HostRing(pow2(user_records), 64, names.user),
+            rt.HostRing(pow2(span_records), 64, names.spans))
+
+
+def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, window_ms: int, max_windows: int,
+                         n_images: int, ready=None) -> None:
+    """Process body: generates ``n_images`` replay windows, then writes one window per
+    ``window_ms`` at ``rate_eps``: the kernel-signal records through the probe model (using
+    the epoch the agent published, read from the emulated mislo_cfg at write time), the GPU-
+    signal records and the spans into the user-space rings. Stops after ``max_windows`` (0 =
+    forever). Never touches the GPU."""
+    from ..pipeline.replay import ReplayConfig, ReplayGenerator
+    from ..pipeline.window import kernel_event_mask
+    from ..runtime import load
+
+    rt = load()
+    rb = rt.Ringbuf.attach_shm(names.ring)
+    user = rt.HostRing(0, 64, names.user, True)
+    spans = rt.HostRing(0, 64, names.spans, True)
+    cfg = ReplayConfig(window_ms=window_ms, **cfg_kwargs)
+    gen = ReplayGenerator(cfg)
+    wins = [gen.next_window() for _ in range(max(1, n_images))]
+    sim = rt.ProbeSim(rb, records.milli_shift_table())
+    parts = []
+    for w in wins:
+        km = kernel_event_mask(w.events)
+        parts.append((np.ascontiguousarray(w.events[km]), np.ascontiguousarray(w.events[~km]),
+                      np.ascontiguousarray(w.spans)))
+    if ready is not None:
+        ready.send(True)
+    period = window_ms / 1000.0
+    # the replay's timestamps are re-based onto wall-clock time, one window per period
+    t_start = time.time_ns()
+    nxt = time.perf_counter()
+    j = 0
+    while not max_windows or j < max_windows:
+        kev, uev, sp = parts[j % len(parts)]
+        shift = t_start + j * int(period * 1e9) - int(wins[j % len(wins)].t0_ns)
+        kev, uev, sp = kev.copy(), uev.copy(), sp.copy()
+        for a in (kev, uev, sp):
+            nz = a["ts_ns"] != 0
+            a["ts_ns"][nz] += shift
+        # pace: the window's records go out in 10 slices across its period
+        n_sl = 10
+        for s in range(n_sl):
+            lo_k, hi_k = len(kev) * s // n_sl, len(kev) * (s + 1) // n_sl
+            sim.submit(kev[lo_k:hi_k])
+            lo_u, hi_u = len(uev) * s // n_sl, len(uev) * (s + 1) // n_sl
+            if hi_u > lo_u:
+                user.push(uev[lo_u:hi_u])
+            lo_s, hi_s = len(sp) * s // n_sl, len(sp) * (s + 1) // n_sl
+            if hi_s > lo_s:
+                spans.push(sp[lo_s:hi_s])
+            nxt += period / n_sl
+            time.sleep(max(0.0, nxt - time.perf_counter()))
+        j += 1
+
+
+def pod_metadata(cfg_kwargs: dict) -> Tuple[np.ndarray, np.ndarray]:
+    """pod id -> svc<<16|node of the replay world (what kubelet metadata gives a live agent)."""
+    from ..pipeline.replay import ReplayConfig, ReplayGenerator
+
+    g = ReplayGenerator(ReplayConfig(**cfg_kwargs))
+    sn = (g.pod_svc.astype(np.uint32) << np.uint32(16)) | g.pod_node.astype(np.uint32)
+    return g.pod_ids.astype(np.uint32), sn
+
+
+def start_replay_producer(names: RingNames, cfg_kwargs: dict, rate_eps: float, window_ms: int,
+                          max_windows: int = 0, n_images: int = 2):
+    """Fork the replay producer (before this process touches the GPU) and wait until it has
+    generated its windows."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("fork")
+    a, b = ctx.Pipe()
+    p = ctx.Process(target=replay_producer_main, args=(names, cfg_kwargs, rate_eps, window_ms, max_windows, n_images, b),
+                    daemon=True)
+    p.start()
+    if not a.poll(600):
+        raise RuntimeError("replay producer did not start")
+    a.recv()
+    return p
+
+
+def iter_chunks(a: np.ndarray, n: int) -> Iterable[np.ndarray]:
+    for i in range(0, len(a), n):
+        yield a[i:i + n]

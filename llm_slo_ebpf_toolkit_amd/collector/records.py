@@ -1,16 +1,26 @@
-"""Binary event/span record formats shared by the BPF probes, the native ring and the GPU.
+"""Binary event/span record formats shared by the BPF probes, the native runtime and the GPU.
 
 * ``REF_EVENT`` -- REF's packed 40-byte ``struct llm_slo_event``
   (ebpf/c/llm_slo_event.h:32-42). Accepted for replay compatibility; decoded with REF's
   exact rules (pkg/collector/ringbuf.go:152-243): type->(name, unit), count stays a count,
   cpu_steal stays raw ns, everything else ns/1e6 -> ms, conn tuple only if a port != 0
   (src_ip "0.0.0.0", protocol "tcp"), errno only if != 0, IPv4 little-endian bytes.
-* ``EVENT`` -- NEW 64-byte, 64-byte-aligned record (one cache line per event, 16-B
-  aligned fields for dwordx4 loads on gfx950). It keeps every REF field and adds
-  interned workload ids (pod/node/service), a 64-bit trace-id hash, a 64-bit
-  connection hash, a GPU id and flags. Layout is mirrored in
-  ``ops/csrc/mislo_records.h`` and ``ebpf/c/mislo_event.h``.
-* ``SPAN`` -- 64-byte span record for the correlation join.
+* ``EVENT`` -- 64-byte record: the probes' working record (probes/ebpf/mislo_record.h
+  ``mislo_event``) and what user-space producers (the rocprofiler-sdk tool library,
+  instrumented services, replay) push into the shared-memory rings. Every REF field plus
+  interned workload ids (pod/node/service), a 64-bit trace-id hash, a 64-bit connection hash,
+  a GPU id and flags.
+* ``EVENT16`` -- the 16-byte record on the wire: the payload of every record the probes put on
+  the BPF ring (``mislo_event16``), and what the agent's host encoder makes of user-space
+  records. Timestamp as an epoch offset with a 2-bit epoch tag, workload identity as a context
+  id into the device context table, fixed-point value, 30-bit trace id.
+* ``DEF16`` -- the probes' id definition records on the same ring (same 16 bytes, type byte
+  0xFE: a context row; 0xFD: a trace id), which the agent's consumer diverts to its tables.
+* ``SPAN`` (64 B) / ``SPAN20`` -- spans as the span ring carries them / as the GPU join reads them.
+
+``ProbeModel`` / ``HostEncoderModel`` are the numpy references of the in-kernel record path
+(mislo_probe.h mislo_submit) and of the agent's host encoder (runtime/csrc/tables.h); the
+native implementations are tested byte for byte against them.
 """
 
 from __future__ import annotations
@@ -46,30 +56,12 @@ EVENT = np.dtype([
 ])
 assert EVENT.itemsize == 64
 
-EVENT32 = np.dtype([
-    ("ts_ns", "<i8"),        # 0
-    ("trace_h", "<u8"),      # 8
-    ("value_milli", "<u4"),  # 16 value in 1/1000 of the signal's output unit
-    ("pid", "<u4"),          # 20
-    ("pod_id", "<u4"),       # 24 interned pod id (svc/node via the device pod table)
-    ("type_conn", "<u4"),    # 28 bits 0-7 signal_type, bits 8-31 interned connection id
-])
-assert EVENT32.itemsize == 32
-
-# 20-byte wire record: the window's base timestamp travels once per window (counts[4..5]),
-# pod / pid / connection / svc|node travel once per distinct context (the device context
-# table, CtxInterner); only the trace hash stays per event. 5/8 of EVENT32's PCIe bytes.
-EVENT20 = np.dtype({"names": ["ts_off", "ctx_type", "value_milli", "trace_h"],
-                    "formats": ["<u4", "<u4", "<u4", "<u8"],
-                    "offsets": [0, 4, 8, 12], "itemsize": 20})
 TS_ZERO = 0xFFFFFFFF  # ts_off of a zero timestamp (never joins)
-assert EVENT20.itemsize == 20
 
-# 16-byte record (= probes/ebpf/mislo_record.h mislo_event16 with -DMISLO_RING_EVENT16, or the
-# host encoding): EVENT20 with the trace hash interned to a 30-bit id shared with the window's
-# spans (TraceInterner / the native WireEncoder / the kernel's mislo_traces), and a 2-bit epoch
-# tag: ts = base[tag] + ts_off, the window carrying its last 4 epoch bases (counts[4..5],
-# counts[8..13]). The host encoder writes tag 0 (one base per window).
+# 16-byte record (= probes/ebpf/mislo_record.h mislo_event16): ts = base[tag] + ts_off, the
+# window carrying its last 4 epoch bases (counts[4..5], counts[8..13]); context id into the
+# device context table; trace id shared with the window's spans (kernel ids < 2^29, ids the
+# agent assigns >= 2^29).
 EVENT16 = np.dtype([
     ("ts_off", "<u4"),       # 0  ns since the tagged epoch base, TS_ZERO = zero timestamp
     ("ctx_type", "<u4"),     # 4  bits 0-7 signal type, 8-31 context id
@@ -116,21 +108,6 @@ class EpochClock:
         return (TS_ZERO - 1 if d >= TS_ZERO else d), tag
 
 
-def retag_epochs(ev16: np.ndarray, t_base: int, period_ns: int):
-    """Re-express EVENT16 records (tag 0, offsets from ``t_base``) the way probes stamp them when
-    the agent publishes a new epoch every ``period_ns`` inside the window: epoch j = t_base +
-    j * period_ns (j <= 3), each record offset from the latest epoch at or before it, with tag j.
-    Returns (records, bases); decoding with ``bases`` gives back the same timestamps."""
-    out = ev16.copy()
-    off = ev16["ts_off"].astype(np.int64)
-    live = off != TS_ZERO
-    j = np.where(live, np.minimum(off // int(period_ns), 3), 0).astype(np.int64)
-    out["ts_off"] = np.where(live, off - j * int(period_ns), TS_ZERO).astype(np.uint32)
-    out["trace_id"] = (ev16["trace_id"].astype(np.uint32) & np.uint32(TRACE_ID_MASK)) | \
-        (j.astype(np.uint32) << np.uint32(EPOCH_TAG_SHIFT))
-    return out, tuple(int(t_base) + k * int(period_ns) for k in range(4))
-
-
 def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,), n_ctx: int = 0,
                span_bytes: int = 64) -> np.ndarray:
     """The window's counts int32[16] as the decode kernels read them: [0] events, [1] spans,
@@ -142,41 +119,28 @@ def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,)
          b[1] & 0xFFFFFFFF, b[1] >> 32, b[2] & 0xFFFFFFFF, b[2] >> 32, b[3] & 0xFFFFFFFF, b[3] >> 32, 0, 0]
     return np.array(v, dtype=np.uint64).astype(np.uint32).view(np.int32)
 assert EVENT16.itemsize == 16
-# 24-byte record (= probes/ebpf/mislo_record.h mislo_event24): what the probes put on the
-# ring when the kernel interns the workload context too: absolute timestamp (no window base
-# at the source), trace hash, fixed-point value, context id into the device context table.
-EVENT24 = np.dtype([
-    ("ts_ns", "<i8"),        # 0
-    ("trace_h", "<u8"),      # 8
-    ("value_milli", "<u4"),  # 16
-    ("ctx_type", "<u4"),     # 20 bits 0-7 signal type, 8-31 context id
-])
-assert EVENT24.itemsize == 24
-# 20-byte record (= probes/ebpf/mislo_record.h mislo_event20t, the probes' default ring
-# record): EVENT24 with the trace hash interned in the kernel to a 32-bit id (mislo_traces);
-# the agent puts the window's spans on the same ids. Records sit at 20-byte strides. Its wire
-# code is 21 (20 is EVENT20, the window-relative host encoding): see wire_bytes().
-EVENT20T = np.dtype({"names": ["ts_ns", "value_milli", "ctx_type", "trace_id"],
-                     "formats": ["<i8", "<u4", "<u4", "<u4"],
-                     "offsets": [0, 8, 12, 16], "itemsize": 20})
-assert EVENT20T.itemsize == 20
-WIRE_20T = 21
-WIRE_DTYPES = {64: EVENT, 32: EVENT32, 24: EVENT24, WIRE_20T: EVENT20T, 20: EVENT20, 16: EVENT16}
-# bench / agent spelling of the wire codes
-WIRE_NAMES = {"64": 64, "32": 32, "24": 24, "20t": WIRE_20T, "20": 20, "16": 16, "16t": 16}  # 16t: EVENT16 ring
+DEF_TRACE, DEF_CTX, DEF_FIRST = 0xFD, 0xFE, 0xF0  # definition record types (low byte of ctx_type)
+KERNEL_CTX_LIMIT = 1 << 23     # kernel context ids 1 .. 2^23 - 1, host ids above
+KERNEL_TRACE_LIMIT = 1 << 29   # kernel trace ids 1 .. 2^29 - 1, host ids above
+CTX_IDS = 1 << 24
+WIRE_DTYPES = {64: EVENT, 16: EVENT16}
+RB_BUSY, RB_DISCARD, RB_HDR = 1 << 31, 1 << 30, 8   # BPF ring buffer record header bits
+REC_STRIDE = RB_HDR + 16                          # ring bytes per 16-byte record
 
 
 def wire_bytes(wire: int) -> int:
-    """PCIe bytes per event of wire code ``wire`` (21 = EVENT20T is 20 bytes)."""
-    return 20 if wire == WIRE_20T else int(wire)
+    """PCIe bytes per event of wire code ``wire`` (64 = EVENT, 16 = EVENT16)."""
+    if wire not in WIRE_DTYPES:
+        raise ValueError(f"unknown wire code {wire}")
+    return int(wire)
 
 
 def wire_code(dtype: np.dtype) -> int:
-    """Wire code of a record dtype (itemsize, except EVENT20T -> 21)."""
     for code, dt in WIRE_DTYPES.items():
         if dt == dtype:
             return code
     raise TypeError(f"not a wire record dtype: {dtype}")
+
 
 SPAN = np.dtype([
     ("ts_ns", "<i8"),        # 0
@@ -302,43 +266,6 @@ def conn_hash_np(src_port: np.ndarray, dst_port: np.ndarray, dst_ip: np.ndarray)
     return np.where((sp == 0) & (dp == 0), np.uint64(0), h)
 
 
-def pod_table(events: np.ndarray, spans: np.ndarray = None) -> np.ndarray:
-    """pod_id -> (svc << 16 | node) lookup table (int32) from records that carry both."""
-    pods = [events["pod_id"]]
-    sn = [(events["svc_id"].astype(np.uint32) << np.uint32(16)) | events["node_id"].astype(np.uint32)]
-    if spans is not None and len(spans):
-        pods.append(spans["pod_id"])
-        sn.append((spans["svc_id"].astype(np.uint32) << np.uint32(16)) | spans["node_id"].astype(np.uint32))
-    p = np.concatenate(pods).astype(np.int64)
-    v = np.concatenate(sn)
-    table = np.zeros(int(p.max()) + 1 if p.size else 1, dtype=np.uint32)
-    table[p] = v
-    return table.view(np.int32)
-
-
-class ConnInterner:
-    """64-bit connection hash -> dense 24-bit connection id (0 = no connection); the
-    user-space side of the BPF probes' 5-tuple -> id map."""
-
-    def __init__(self):
-        self._ids = {}
-
-    def ids(self, conn_h: np.ndarray) -> np.ndarray:
-        uniq, inv = np.unique(conn_h, return_inverse=True)
-        out = np.zeros(uniq.shape[0], dtype=np.uint32)
-        for j, h in enumerate(uniq.tolist()):
-            if h == 0:
-                continue
-            i = self._ids.get(h)
-            if i is None:
-                i = len(self._ids) + 1
-                if i >= (1 << 24):
-                    raise OverflowError("connection id space exhausted")
-                self._ids[h] = i
-            out[j] = i
-        return out[inv]
-
-
 def milli_shift_table() -> np.ndarray:
     """Per kernel signal type (< 256): the power of ten d with value_milli = raw * 10**d, i.e.
     log10(decode_scale * 1000). Every catalogue scale is a power of ten (ns -> ms: -3,
@@ -395,196 +322,220 @@ def _conn_keys(events: np.ndarray) -> np.ndarray:
     return np.where(conn == 0, derived, conn)
 
 
-def to_compact(events: np.ndarray, interner: "ConnInterner") -> np.ndarray:
-    """EVENT (64 B) -> EVENT32 (32 B): milli-unit fixed point values, interned conn ids."""
-    out = np.zeros(events.shape[0], dtype=EVENT32)
-    out["ts_ns"] = events["ts_ns"]
-    out["trace_h"] = events["trace_h"]
-    out["value_milli"] = _milli_values(events)
-    out["pid"] = events["pid"]
-    out["pod_id"] = events["pod_id"]
-    cid = interner.ids(_conn_keys(events))
-    st = events["signal_type"].astype(np.uint32)
-    out["type_conn"] = (st & np.uint32(0xFF)) | (cid << np.uint32(8))
-    return out
 
 
-def to_wire20(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner"):
-    """EVENT (64 B) -> (EVENT20 (20 B), t_base): timestamps relative to the window's
-    earliest non-zero timestamp, interned (pod, pid, conn, svc|node) contexts. Raises
-    ValueError when the window spans 2^32 - 1 ns or more (use EVENT32 then)."""
-    out = np.zeros(events.shape[0], dtype=EVENT20)
-    ts = events["ts_ns"].astype(np.int64)
-    nz = ts != 0
-    t_base = int(ts[nz].min()) if nz.any() else 0
-    off = ts - t_base
-    if nz.any() and int(off[nz].max()) >= TS_ZERO:
-        raise ValueError("window spans >= 2^32 ns: not representable in EVENT20")
-    out["ts_off"] = np.where(nz, off, TS_ZERO).astype(np.uint32)
-    out["value_milli"] = _milli_values(events)
-    out["trace_h"] = events["trace_h"]
-    cid = conns.ids(_conn_keys(events))
-    sn = (events["svc_id"].astype(np.uint32) << np.uint32(16)) | events["node_id"].astype(np.uint32)
-    ctx = ctxs.ids(events["pod_id"], events["pid"], cid, sn)
-    st = events["signal_type"].astype(np.uint32)
-    out["ctx_type"] = (st & np.uint32(0xFF)) | (ctx << np.uint32(8))
-    return out, t_base
+def conn32_np(keys: np.ndarray) -> np.ndarray:
+    """The 32-bit connection identity of context rows (runtime/csrc/records.h conn32, the
+    kernel's mislo_conn32): fold of the 64-bit connection key, forced odd; 0 = no connection."""
+    k = np.asarray(keys, dtype=np.uint64)
+    f = ((k ^ (k >> np.uint64(32))) & np.uint64(0xFFFFFFFF)) | np.uint64(1)
+    return np.where(k == 0, np.uint64(0), f).astype(np.uint32)
 
 
-def to_wire24(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner") -> np.ndarray:
-    """EVENT (64 B) -> EVENT24 (24 B), the probes' context-interned ring record: absolute
-    timestamps, trace hash, fixed-point value, interned (pod, pid, conn, svc|node) context."""
-    out = np.zeros(events.shape[0], dtype=EVENT24)
-    out["ts_ns"] = events["ts_ns"]
-    out["trace_h"] = events["trace_h"]
-    out["value_milli"] = _milli_values(events)
-    cid = conns.ids(_conn_keys(events))
-    sn = (events["svc_id"].astype(np.uint32) << np.uint32(16)) | events["node_id"].astype(np.uint32)
-    ctx = ctxs.ids(events["pod_id"], events["pid"], cid, sn)
-    st = events["signal_type"].astype(np.uint32)
-    out["ctx_type"] = (st & np.uint32(0xFF)) | (ctx << np.uint32(8))
-    return out
+def conn32(key: int) -> int:
+    key = int(key)
+    return 0 if key == 0 else (((key ^ (key >> 32)) & 0xFFFFFFFF) | 1)
 
 
-def to_wire20t(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner",
-               traces: "TraceInterner") -> np.ndarray:
-    """EVENT (64 B) -> EVENT20T (20 B), the probes' default ring record: EVENT24 with the
-    trace hash interned (spans must go through ``wire_spans`` with the same interners)."""
-    e24 = to_wire24(events, conns, ctxs)
-    out = np.zeros(events.shape[0], dtype=EVENT20T)
-    for f in ("ts_ns", "value_milli", "ctx_type"):
-        out[f] = e24[f]
-    out["trace_id"] = traces.ids(events["trace_h"])
-    return out
-
-
-# 20-byte span record (ops/csrc SpanC20, runtime/csrc/wire.h Span20): what the GPU join reads of
-# a span, with (pod, pid, conn, svc|node) as a context id and an interned trace id; used with the
-# trace-interning event rings (EVENT16 / EVENT20T), 5/16 of the 64-byte SPAN's PCIe bytes.
+# 20-byte span record (ops/csrc SpanC20, runtime/csrc/records.h Span20): what the GPU join reads of
+# a span, with (pod, pid, conn32, svc|node) as a context id and a trace id from the events' id space.
 SPAN20 = np.dtype({"names": ["ts_ns", "trace_id", "ctx_id", "group_id"],
                    "formats": ["<i8", "<u4", "<u4", "<u4"], "offsets": [0, 8, 12, 16], "itemsize": 20})
 
 
-def to_span20(spans: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner", traces: "TraceInterner") -> np.ndarray:
-    """SPAN (64 B) -> SPAN20 with the event interners (numpy reference of encode_spans20)."""
-    out = np.zeros(spans.shape[0], dtype=SPAN20)
-    out["ts_ns"] = spans["ts_ns"]
-    out["trace_id"] = traces.ids(spans["trace_h"])
-    cid = conns.ids(spans["conn_h"])
-    sn = (spans["svc_id"].astype(np.uint32) << np.uint32(16)) | spans["node_id"].astype(np.uint32)
-    out["ctx_id"] = ctxs.ids(spans["pod_id"], spans["pid"], cid, sn)
-    out["group_id"] = spans["group_id"]
-    return out
+def epoch_offset(ts: int, base: int) -> int:
+    """mislo_submit / EpochClock.stamp: offset of ts from an epoch base (clamped)."""
+    if ts == 0:
+        return TS_ZERO
+    if ts < base:
+        return 0
+    return min(ts - base, TS_ZERO - 1)
 
 
-def compact_spans(spans: np.ndarray, interner: "ConnInterner") -> np.ndarray:
-    """Spans keep the 64-byte layout; their conn key is rewritten to the same interned id."""
-    out = spans.copy()
-    out["conn_h"] = interner.ids(spans["conn_h"]).astype(np.uint64)
-    return out
+class ProbeModel:
+    """numpy/Python reference of the probes' in-kernel record path (probes/ebpf/mislo_probe.h
+    mislo_emit -> mislo_submit; runtime/csrc/probesim.h is the native model tested against it):
+    floors, context and trace interning with the definition record emitted ahead of the first
+    use, epoch-relative timestamps with the published epoch's tag. ``cfg`` is the mislo_cfg
+    array (uint64[128])."""
 
+    CFG_EPOCH, CFG_TRACE_NEXT, CFG_CTX_NEXT = 124, 125, 126
 
-class CtxInterner:
-    """(pod, pid, conn id, svc<<16|node) -> dense 24-bit context id; id 0 is the all-zero
-    context. ``table()`` is the device context table (int32 [n, 4]) indexed by id. Ids are
-    stable for the agent's lifetime, so the table only grows (and is re-uploaded then)."""
+    def __init__(self, cfg: np.ndarray = None):
+        self.cfg = cfg if cfg is not None else np.zeros(128, dtype=np.uint64)
+        self.ctx = {}
+        self.traces = {}
 
-    MAX_IDS = 1 << 24
-
-    def __init__(self):
-        self._ids = {(0, 0, 0, 0): 0}
-        self._rows = [(0, 0, 0, 0)]
-        self._table = None
-
-    def __len__(self) -> int:
-        return len(self._rows)
-
-    def ids(self, pod, pid, cid, sn) -> np.ndarray:
-        rows = np.stack([np.asarray(x).astype(np.uint32) for x in (pod, pid, cid, sn)], axis=1)
-        if rows.shape[0] == 0:
-            return np.zeros(0, dtype=np.uint32)
-        r64 = rows.astype(np.uint64)
-        key = (r64[:, 0] * np.uint64(0x9E3779B97F4A7C15)) ^ (r64[:, 1] * np.uint64(0xC2B2AE3D27D4EB4F)) ^ \
-              (r64[:, 2] * np.uint64(0x165667B19E3779F9)) ^ (r64[:, 3] * np.uint64(0xD6E8FEB86659FD93))
-        _, first, inv = np.unique(key, return_index=True, return_inverse=True)
-        uniq_rows = rows[first]
-        if not np.array_equal(uniq_rows[inv], rows):  # 64-bit key collision: exact path
-            uniq_rows, inv = np.unique(rows, axis=0, return_inverse=True)
-        out = np.empty(uniq_rows.shape[0], dtype=np.uint32)
-        for j, r in enumerate(map(tuple, uniq_rows.tolist())):
-            v = self._ids.get(r)
-            if v is None:
-                v = len(self._rows)
-                if v >= self.MAX_IDS:
-                    raise OverflowError("more than 2^24 interned contexts")
-                self._ids[r] = v
-                self._rows.append(r)
-                self._table = None
-            out[j] = v
-        return out[np.asarray(inv).reshape(-1)]
-
-    def table(self) -> np.ndarray:
-        if self._table is None:
-            self._table = np.array(self._rows, dtype=np.uint32).reshape(-1, 4).view(np.int32)
-        return self._table
-
-
-class TraceInterner:
-    """64-bit trace hash -> 32-bit id (0 = none), shared by a window's events and spans
-    (numpy reference of the native encoder's trace table; no expiry)."""
-
-    def __init__(self):
-        self._ids = {}
-
-    def ids(self, trace_h: np.ndarray) -> np.ndarray:
-        uniq, inv = np.unique(np.asarray(trace_h, dtype=np.uint64), return_inverse=True)
-        out = np.zeros(uniq.shape[0], dtype=np.uint32)
-        for j, h in enumerate(uniq.tolist()):
-            if h == 0:
+    def encode(self, events: np.ndarray) -> np.ndarray:
+        """Ring payloads (EVENT16 layout, definitions included, ring order) for ``events``."""
+        out = []
+        shift = milli_shift_table()
+        for e in events:
+            st = int(e["signal_type"])
+            if st < 122 and int(e["value"]) < int(self.cfg[2 + st]):
                 continue
-            i = self._ids.get(h)
-            if i is None:
-                i = len(self._ids) + 1
-                if i > TRACE_ID_MASK:  # 30-bit ids (EVENT16 keeps 2 bits for the epoch tag)
-                    raise OverflowError("trace id space exhausted")
-                self._ids[h] = i
-            out[j] = i
-        return out[np.asarray(inv).reshape(-1)]
+            ck = int(e["conn_h"]) or conn_hash(int(e["src_port"]), int(e["dst_port"]), int(e["dst_ip"]))
+            c = conn32(ck)
+            pod, pid = int(e["pod_id"]), int(e["pid"])
+            ctx = 0
+            if pod or pid or c:
+                ctx = self.ctx.get((pod, pid, c), 0)
+                if not ctx:
+                    fresh = int(self.cfg[self.CFG_CTX_NEXT]) + 1
+                    self.cfg[self.CFG_CTX_NEXT] = fresh
+                    if fresh < KERNEL_CTX_LIMIT:
+                        out.append((c, DEF_CTX | (fresh << 8), pod, pid))
+                        self.ctx[(pod, pid, c)] = fresh
+                        ctx = fresh
+            tid = 0
+            th = int(e["trace_h"])
+            if th:
+                tid = self.traces.get(th, 0)
+                if not tid:
+                    fresh = int(self.cfg[self.CFG_TRACE_NEXT])
+                    self.cfg[self.CFG_TRACE_NEXT] = fresh + 1
+                    tid = fresh % (KERNEL_TRACE_LIMIT - 1) + 1
+                    out.append((tid, DEF_TRACE, th & 0xFFFFFFFF, th >> 32))
+                    self.traces[th] = tid
+            epoch = int(self.cfg[self.CFG_EPOCH])
+            milli = int(milli_int(np.array([int(e["value"])], dtype=np.uint64),
+                                  np.array([shift[st] if st < 256 else 3], dtype=np.int8))[0])
+            out.append((epoch_offset(int(e["ts_ns"]), epoch & ~3), (st & 0xFF) | (ctx << 8), milli,
+                        (tid & TRACE_ID_MASK) | ((epoch & 3) << EPOCH_TAG_SHIFT)))
+        return np.array(out, dtype=np.uint32).reshape(-1, 4).view(EVENT16).reshape(-1) if out else \
+            np.zeros(0, dtype=EVENT16)
 
 
-def to_wire16(events: np.ndarray, conns: "ConnInterner", ctxs: "CtxInterner", traces: "TraceInterner"):
-    """EVENT (64 B) -> (EVENT16 (16 B), t_base); spans must go through ``wire_spans`` with
-    the same interners."""
-    e20, t_base = to_wire20(events, conns, ctxs)
-    out = np.zeros(events.shape[0], dtype=EVENT16)
-    for f in ("ts_off", "ctx_type", "value_milli"):
-        out[f] = e20[f]
-    out["trace_id"] = traces.ids(events["trace_h"])
-    return out, t_base
+def frame(payloads: np.ndarray) -> np.ndarray:
+    """Committed BPF ring records (8-byte header {len = 16, pg_off = 0} + payload) for EVENT16 payloads."""
+    p = np.ascontiguousarray(payloads).view(np.uint32).reshape(-1, 4)
+    out = np.zeros((p.shape[0], 6), dtype=np.uint32)
+    out[:, 0] = 16
+    out[:, 2:] = p
+    return out.view(np.uint8).reshape(-1)
 
 
-def wire_spans(spans: np.ndarray, conns: "ConnInterner", traces: "TraceInterner" = None) -> np.ndarray:
-    """Spans for the compact wire formats: interned conn ids (and trace ids for EVENT16)."""
-    out = compact_spans(spans, conns)
-    if traces is not None:
-        out["trace_h"] = traces.ids(spans["trace_h"]).astype(np.uint64)
-    return out
+def unframe(image: np.ndarray):
+    """libbpf ring_buffer__consume semantics over a byte image of consecutive records starting at a
+    record boundary: (EVENT16 event payloads, definition payloads, n_discarded, stopped_at_busy)."""
+    b = np.ascontiguousarray(image).view(np.uint8)
+    off, ev, defs, disc = 0, [], [], 0
+    while off + RB_HDR <= b.size:
+        ln = int(b[off:off + 4].view(np.uint32)[0])
+        if ln & RB_BUSY:
+            return _as16(ev), _as16(defs), disc, True
+        plen = ln & ~(RB_BUSY | RB_DISCARD)
+        if ln & RB_DISCARD:
+            disc += 1
+        elif plen == 16:
+            rec = tuple(int(x) for x in b[off + 8:off + 24].view(np.uint32))
+            (defs if (rec[1] & 0xFF) >= DEF_FIRST else ev).append(rec)
+        off += (plen + RB_HDR + 7) & ~7
+    return _as16(ev), _as16(defs), disc, False
 
 
-def signal_scale_table() -> np.ndarray:
-    """decode_scale per kernel signal type < 256 (1.0 for unknown types)."""
-    scale = np.ones(256, dtype=np.float64)
-    for s in catalog.SIGNALS:
-        if s.kernel_type < 256:
-            scale[s.kernel_type] = s.decode_scale
-    return scale
+def _as16(rows):
+    return np.array(rows, dtype=np.uint32).reshape(-1, 4).view(EVENT16).reshape(-1) if rows else \
+        np.zeros(0, dtype=EVENT16)
 
 
-def native_encoder():
-    """The native WireEncoder (runtime/csrc/wire.h) configured with the signal catalogue."""
+class HostEncoderModel:
+    """Python reference of the agent's id tables and host encoder (runtime/csrc/tables.h
+    AgentTables): kernel context rows from definitions (svc|node from pod metadata), host context
+    ids from 2^23, trace ids shared with the kernel's definitions (host ids from 2^29), EVENT16
+    with per-record epoch choice, SPAN20, and the row patch in queue order."""
+
+    def __init__(self):
+        self.pod_sn = {}
+        self.kernel_rows = {}
+        self.host = {}
+        self.host_next = KERNEL_CTX_LIMIT
+        self.traces = {}
+        self.trace_next = KERNEL_TRACE_LIMIT
+        self.pending = []
+
+    def set_pod(self, pod: int, sn: int) -> None:
+        if self.pod_sn.get(pod, 0) == sn:
+            return
+        self.pod_sn[pod] = sn
+        for cid in sorted(self.kernel_rows):
+            r = self.kernel_rows[cid]
+            if r[0] == pod and (r[0] | r[1] | r[2]):
+                r = (r[0], r[1], r[2], sn)
+                self.kernel_rows[cid] = r
+                self.pending.append((cid, r))
+
+    def apply_defs(self, defs: np.ndarray) -> None:
+        for d in np.ascontiguousarray(defs).view(np.uint32).reshape(-1, 4).tolist():
+            t = d[1] & 0xFF
+            if t == DEF_CTX:
+                cid = d[1] >> 8
+                if 0 < cid < KERNEL_CTX_LIMIT:
+                    r = (d[2], d[3], d[0], self.pod_sn.get(d[2], 0))
+                    self.kernel_rows[cid] = r
+                    self.pending.append((cid, r))
+            elif t == DEF_TRACE and 0 < d[0] < KERNEL_TRACE_LIMIT:
+                self.traces[d[2] | (d[3] << 32)] = d[0]
+
+    def trace_id(self, h: int) -> int:
+        h = int(h)
+        if not h:
+            return 0
+        if h not in self.traces:
+            self.traces[h] = self.trace_next
+            self.trace_next = KERNEL_TRACE_LIMIT if self.trace_next == TRACE_ID_MASK else self.trace_next + 1
+        return self.traces[h]
+
+    def host_ctx(self, pod, pid, c, sn) -> int:
+        key = (int(pod), int(pid), int(c), int(sn))
+        if key == (0, 0, 0, 0):
+            return 0
+        if key not in self.host:
+            self.host[key] = self.host_next
+            self.pending.append((self.host_next, key))
+            self.host_next += 1
+        return self.host[key]
+
+    def encode_events(self, events: np.ndarray, bases) -> np.ndarray:
+        b = (list(bases) + [0, 0, 0, 0])[:4]
+        shift = milli_shift_table()
+        live = [j for j in range(4) if b[j] != 0]
+        oldest = min(live, key=lambda j: (b[j], j)) if live else 0
+        out = np.zeros(events.shape[0], dtype=EVENT16)
+        for i, e in enumerate(events):
+            ts = int(e["ts_ns"])
+            cands = [j for j in live if ts >= b[j]]
+            tag = max(cands, key=lambda j: (b[j], j)) if cands else oldest
+            st = int(e["signal_type"])
+            ck = int(e["conn_h"]) or conn_hash(int(e["src_port"]), int(e["dst_port"]), int(e["dst_ip"]))
+            sn = (int(e["svc_id"]) << 16) | int(e["node_id"])
+            ctx = self.host_ctx(e["pod_id"], e["pid"], conn32(ck), sn)
+            milli = int(milli_int(np.array([int(e["value"])], dtype=np.uint64),
+                                  np.array([shift[st] if st < 256 else 3], dtype=np.int8))[0])
+            out[i] = (epoch_offset(ts, b[tag]), (st & 0xFF) | (ctx << 8), milli,
+                      (self.trace_id(e["trace_h"]) & TRACE_ID_MASK) | (tag << EPOCH_TAG_SHIFT))
+        return out
+
+    def encode_spans(self, spans: np.ndarray) -> np.ndarray:
+        out = np.zeros(spans.shape[0], dtype=SPAN20)
+        for i, s in enumerate(spans):
+            sn = (int(s["svc_id"]) << 16) | int(s["node_id"])
+            out[i] = (int(s["ts_ns"]), self.trace_id(s["trace_h"]),
+                      self.host_ctx(s["pod_id"], s["pid"], conn32(int(s["conn_h"])), sn), int(s["group_id"]))
+        return out
+
+    def take_rows(self):
+        ids = np.array([p[0] for p in self.pending], dtype=np.uint32)
+        rows = np.array([p[1] for p in self.pending], dtype=np.uint32).reshape(-1, 4)
+        self.pending = []
+        return ids, rows
+
+
+def native_tables():
+    """The agent's native id tables / host encoder (runtime/csrc/tables.h)."""
     from ..runtime import load
 
-    return load().WireEncoder(milli_shift_table())
+    return load().AgentTables(milli_shift_table())
 
 
 def string_hash64(s: str) -> int:

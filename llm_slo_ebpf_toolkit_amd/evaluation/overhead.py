@@ -6,8 +6,8 @@ pkg/safety/overhead_guard.go:103) over a paced run:
 
 * ``agent``: the host agent emit loop at its configured cadence -- synthetic sample ->
   4 SLO events + up to 16 probe events -> compiled-schema validation -> JSONL encode.
-* ``gpu``: the MI355X window pipeline paced at ``rate_eps`` events/s (default 1M/s,
-  BASELINE config 5): H2D + kernels + packet all-reduce + online refit per window.
+* ``gpu``: the agent's MI355X window path paced at ``rate_eps`` events/s (default 1M/s,
+  BASELINE config 5): ring compaction + host encoding + one DMA + the window graph.
 """
 
 from __future__ import annotations
@@ -63,39 +63,47 @@ def _agent_loop(duration_s: float, ticks_per_s: float) -> Dict[str, float]:
 
 
 def _gpu_loop(duration_s: float, rate_eps: float, window_s: float) -> Dict[str, float]:
-    import torch
-
-    from ..pipeline.replay import ReplayConfig, ReplayGenerator
-    from ..pipeline.window import WindowPipeline, stage_window
+    """The agent's GPU window path at ``rate_eps``: a forked replay producer (the kernel's
+    stand-in, not measured) writes into emulated rings; this process cuts a window every
+    ``window_s``, assembles it natively and submits it to the native engine."""
+    from ..collector import bpf
+    from ..pipeline.window import RingWindowSource, WindowPipeline
 
     n = max(1024, int(rate_eps * window_s))
-    cfg = ReplayConfig(events_per_window=n, spans_per_window=max(64, n // 64), n_services=32)
-    gen = ReplayGenerator(cfg)
-    wins = [gen.next_window() for _ in range(2)]
-    staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 32) for w in wins]
-    pipe = WindowPipeline(n, cfg.spans_per_window, 32, torch.cuda.current_device())
-    pipe.submit(staged[0])
-    pipe.drain()
-    c0, w0 = time.process_time(), time.perf_counter()
-    nxt = w0
-    k = 0
-    while time.perf_counter() - w0 < duration_s:
-        pipe.submit(staged[k % 2])
-        k += 1
-        nxt += window_s
-        time.sleep(max(0.0, nxt - time.perf_counter()))
-    pipe.drain()
-    cpu, wall = time.process_time() - c0, time.perf_counter() - w0
-    return {"cpu_pct": 100.0 * cpu / wall, "events_per_second": k * n / wall, "dropped": 0}
+    groups = 32
+    names = bpf.RingNames.of(f"/mislo-ovh-{os.getpid()}")
+    kw = dict(events_per_window=n, spans_per_window=max(64, n // 64), n_services=groups)
+    ring, user, spans = bpf.create_rings(names, 4 * 24 * n, 4 * n, 4 * kw["spans_per_window"])
+    prod = bpf.start_replay_producer(names, kw, rate_eps, int(window_s * 1000), n_images=2)
+    try:
+        pipe = WindowPipeline(n, kw["spans_per_window"], groups, 0, None, model="bayes", learn=False)
+        src = RingWindowSource(pipe, ring, user, spans, threads=2)
+        src.tables.set_pods(*bpf.pod_metadata(kw))
+        src.step(groups, with_labels=False)
+        pipe.drain()
+        c0, w0 = time.process_time(), time.perf_counter()
+        nxt = w0
+        k = events = 0
+        while time.perf_counter() - w0 < duration_s:
+            nxt += window_s
+            time.sleep(max(0.0, nxt - time.perf_counter()))
+            src.step(groups, with_labels=False)
+            events += int(src.last["n_events"])
+            k += 1
+        pipe.drain()
+        cpu, wall = time.process_time() - c0, time.perf_counter() - w0
+    finally:
+        prod.terminate()
+    return {"cpu_pct": 100.0 * cpu / wall, "events_per_second": events / wall, "dropped": 0}
 
 
 def measure(duration_s: float = 1.0, mode: Optional[str] = None, rate_eps: float = 1e6, window_s: float = 1.0,
             ticks_per_s: float = 10.0) -> Dict[str, float]:
     if mode is None:
         try:
-            import torch
+            from ..ops import load_agent
 
-            mode = "gpu" if torch.cuda.is_available() else "agent"
+            mode = "gpu" if load_agent().device_count() > 0 else "agent"
         except Exception:  # pragma: no cover
             mode = "agent"
     if mode == "gpu":

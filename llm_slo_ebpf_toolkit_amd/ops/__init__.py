@@ -64,6 +64,26 @@ def load(device: Optional[int] = None):
     return _MOD
 
 
+_AGENT = None
+
+
+def load_agent():
+    """The native window engine module (``_mislo_agent``: HIP + RCCL, no PyTorch) with the
+    signal-catalogue constant tables uploaded. Raises ExtensionMissing without a build."""
+    global _AGENT
+    with _LOCK:
+        if _AGENT is None:
+            try:
+                mod = importlib.import_module(__name__ + "._mislo_agent")
+            except ImportError as exc:
+                raise ExtensionMissing("native engine _mislo_agent is not built; run "
+                                       "`python -m llm_slo_ebpf_toolkit_amd.ops.build`") from exc
+            if mod.device_count() > 0:
+                mod.set_tables(*tables_arrays())
+            _AGENT = mod
+    return _AGENT
+
+
 def available() -> bool:
     try:
         _import()

@@ -4,6 +4,8 @@ Produces, next to the sources (so the .so travels with the repo snapshot to the 
 
 * ``ops/_mislo_hip<EXT_SUFFIX>``    -- torch extension: decode / join / posterior kernels
   and the ``Engine`` bindings (hipcc, --offload-arch=gfx950).
+* ``ops/_mislo_agent<EXT_SUFFIX>``  -- the native window engine (HIP + RCCL, pybind11, no
+  torch): what the agent daemon and the benchmark run.
 * ``probes/rocprof/libmislo_rocprof.so`` -- rocprofiler-sdk tool library (GPU signals
   from inside LLM workloads into the agent's shared-memory ring).
 * ``runtime/_mislo_rt<EXT_SUFFIX>`` -- native runtime (pinned MPSC ring, replay generator,
@@ -36,7 +38,8 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 HIP_SOURCES = ["decode.hip", "join.hip", "posterior.hip", "gatestats.hip", "storm.hip"]
-RT_SOURCES = ["ring.cpp", "replay.cpp", "wire.cpp", "rt_bindings.cpp"]
+RT_SOURCES = ["ring.cpp", "replay.cpp", "pool.cpp", "bpfring.cpp", "probesim.cpp", "tables.cpp", "assemble.cpp",
+              "bpfsys.cpp", "rt_bindings.cpp"]
 
 
 def torch_flags():
@@ -112,6 +115,38 @@ def build_hip_ext(force: bool = False, jobs: int = 4) -> str:
     return out
 
 
+AGENT_KERNELS = ["decode.hip", "join.hip", "posterior.hip"]
+
+
+def build_agent_ext(force: bool = False, jobs: int = 4) -> str:
+    """``_mislo_agent``: the native window engine (engine.hip) + the window kernels, bound with
+    pybind11 and linked against the HIP runtime and RCCL only (no PyTorch)."""
+    os.makedirs(BUILD, exist_ok=True)
+    out = os.path.join(HERE, "_mislo_agent" + EXT_SUFFIX)
+    hdrs = _headers(CSRC) + [os.path.join(RT_CSRC, "slot.h")]
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", f"-I{RT_CSRC}"]
+    common += os.environ.get("MISLO_HIP_DEFINES", "").split()
+    jobs_list, objs = [], []
+    for src in AGENT_KERNELS:  # shared with the torch extension (same flags, same objects)
+        objs.append(os.path.join(BUILD, src + ".o"))
+    eng = os.path.join(CSRC, "engine.hip")
+    eobj = os.path.join(BUILD, "engine.hip.o")
+    objs.append(eobj)
+    if force or _newer(eobj, [eng] + hdrs):
+        jobs_list.append([HIPCC, *common, "-c", eng, "-o", eobj])
+    bind = os.path.join(CSRC, "agent_bindings.cpp")
+    bobj = os.path.join(BUILD, "agent_bindings.o")
+    objs.append(bobj)
+    if force or _newer(bobj, [bind] + hdrs):
+        jobs_list.append([HIPCC, *common, "-x", "hip", *pybind_flags(), "-c", bind, "-o", bobj])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(_run, jobs_list))
+    if force or jobs_list or _newer(out, objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out, f"-L{ROCM}/lib", "-lamdhip64",
+              "-lrccl", f"-Wl,-rpath,{ROCM}/lib"])
+    return out
+
+
 def build_runtime(force: bool = False, jobs: int = 4) -> List[str]:
     os.makedirs(BUILD, exist_ok=True)
     rt_dir = os.path.join(PKG, "runtime")
@@ -121,13 +156,13 @@ def build_runtime(force: bool = False, jobs: int = 4) -> List[str]:
     base = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-ffp-contract=off", f"-I{ROCM}/include",
             "-D__HIP_PLATFORM_AMD__=1"]
     outs = []
-    core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp", "wire.cpp")]
+    core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp")]
     lib = os.path.join(rt_dir, "libmislo_rt.so")
     if force or _newer(lib, core + hdrs):
         _run([cxx, *base, "-shared", *core, "-o", lib, f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
     outs.append(lib)
     mod = os.path.join(rt_dir, "_mislo_rt" + EXT_SUFFIX)
-    srcs = core + [os.path.join(RT_CSRC, "rt_bindings.cpp")]
+    srcs = [os.path.join(RT_CSRC, s) for s in RT_SOURCES]
     if force or _newer(mod, srcs + hdrs):
         _run([cxx, *base, *pybind_flags(), "-shared", *srcs, "-o", mod, f"-L{ROCM}/lib", "-lamdhip64",
               f"-Wl,-rpath,{ROCM}/lib"])
@@ -152,6 +187,7 @@ def build_rocprof_tool(force: bool = False) -> str:
 def build_all(force: bool = False, jobs: int = 4) -> List[str]:
     outs = build_runtime(force, jobs)
     outs.append(build_hip_ext(force, jobs))
+    outs.append(build_agent_ext(force, jobs))
     outs.append(build_rocprof_tool(force))
     return outs
 
@@ -160,10 +196,12 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
-    ap.add_argument("--only", choices=("hip", "runtime", "all"), default="all")
+    ap.add_argument("--only", choices=("hip", "agent", "runtime", "all"), default="all")
     a = ap.parse_args(argv)
     if a.only == "hip":
         outs = [build_hip_ext(a.force, a.jobs)]
+    elif a.only == "agent":
+        outs = [build_hip_ext(a.force, a.jobs), build_agent_ext(a.force, a.jobs)]
     elif a.only == "runtime":
         outs = build_runtime(a.force, a.jobs)
     else:

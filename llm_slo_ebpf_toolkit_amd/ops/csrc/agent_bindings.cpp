@@ -1,0 +1,234 @@
+// pybind11 module `_mislo_agent`: the native window engine (engine.h) for the agent daemon and
+// the benchmark. No PyTorch: the agent process links the HIP runtime, RCCL and these kernels
+// only (its resident set is part of the overhead budget, REF docs/benchmarks targets <= 250 MB).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+
+#include "engine.h"
+
+namespace py = pybind11;
+using namespace mislo;
+
+namespace {
+
+template <class T>
+py::array_t<T> copy_array(const T* p, std::vector<py::ssize_t> shape) {
+  py::array_t<T> a(shape);
+  size_t n = 1;
+  for (auto s : shape) n *= (size_t)s;
+  if (n) std::memcpy(a.mutable_data(), p, n * sizeof(T));
+  return a;
+}
+
+void set_tables_np(py::array_t<int8_t, py::array::c_style | py::array::forcecast> type_slot,
+                   py::array_t<float, py::array::c_style | py::array::forcecast> scale,
+                   py::array_t<float, py::array::c_style | py::array::forcecast> warn,
+                   py::array_t<float, py::array::c_style | py::array::forcecast> err,
+                   py::array_t<float, py::array::c_style | py::array::forcecast> edges) {
+  Tables t;
+  std::memset(&t, 0, sizeof(t));
+  if (type_slot.size() != kMaxTypes || scale.size() != kSlots || warn.size() != kSlots || err.size() != kSlots ||
+      edges.size() != kSlots * kBuckets)
+    throw std::invalid_argument("table shapes");
+  std::memcpy(t.type_slot, type_slot.data(), sizeof(t.type_slot));
+  std::memcpy(t.scale, scale.data(), sizeof(t.scale));
+  std::memcpy(t.warn, warn.data(), sizeof(t.warn));
+  std::memcpy(t.err, err.data(), sizeof(t.err));
+  std::memcpy(t.edges, edges.data(), sizeof(t.edges));
+  engine_set_tables(t);
+}
+
+}  // namespace
+
+class PyEngine {
+ public:
+  PyEngine(int device, int sig_cap, int span_cap, int group_cap, int row_cap, int n_buffers, int max_ahead,
+           double window_ms, double threshold, int fanout, int group_mode, bool use_graphs, bool device_refit,
+           int n_dom) {
+    EngineConfig c;
+    c.device = device;
+    c.sig_cap = sig_cap;
+    c.span_cap = span_cap;
+    c.group_cap = group_cap;
+    c.row_cap = row_cap;
+    c.n_buffers = n_buffers;
+    c.max_ahead = max_ahead;
+    c.window_ms = window_ms;
+    c.threshold = threshold;
+    c.fanout = fanout;
+    c.group_mode = group_mode;
+    c.use_graphs = use_graphs;
+    c.device_refit = device_refit;
+    c.n_dom = n_dom;
+    e_ = std::make_unique<WindowEngine>(c);
+  }
+  uintptr_t host_slot(int64_t k) const { return reinterpret_cast<uintptr_t>(e_->host_slot(k)); }
+  py::array slot_view(int64_t k) {
+    return py::array(py::dtype("uint8"), {(py::ssize_t)e_->layout().bytes}, {(py::ssize_t)1}, e_->host_slot(k),
+                     py::cast(this, py::return_value_policy::reference));
+  }
+  void wait_slot(int64_t k) {
+    py::gil_scoped_release nogil;
+    e_->wait_slot(k);
+  }
+  void submit(int64_t k, size_t dma_bytes, int n_groups, bool with_labels, bool learn) {
+    py::gil_scoped_release nogil;
+    e_->submit(k, dma_bytes, n_groups, with_labels, learn);
+  }
+  bool query(int64_t k) { return e_->query(k); }
+  void wait(int64_t k) {
+    py::gil_scoped_release nogil;
+    e_->wait(k);
+  }
+  py::array_t<double> packet(int64_t k) { return copy_array(e_->packet(k), {kPacketLen}); }
+  py::dict results(int64_t k, int n_groups) {
+    if (n_groups < 0 || n_groups > e_->config().group_cap) throw std::invalid_argument("n_groups");
+    const ResultView r = e_->results(k);
+    const py::ssize_t G = n_groups;
+    py::dict d;
+    d["post"] = copy_array(r.post, {G, 16});
+    d["conf"] = copy_array(r.gconf, {G});
+    d["feat"] = copy_array(r.feat, {G, 16});
+    d["pred"] = copy_array(r.pred, {G});
+    d["evbits"] = copy_array(r.evbits, {G, 16});
+    return d;
+  }
+  py::tuple window_ms(int64_t k) {
+    std::pair<float, float> t;
+    {
+      py::gil_scoped_release nogil;
+      t = e_->window_ms(k);
+    }
+    return py::make_tuple(t.first, t.second);
+  }
+  void set_model_bytes(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
+    e_->set_model_bytes(b.data(), (size_t)b.size());
+  }
+  void set_p0(py::array_t<double, py::array::c_style | py::array::forcecast> p0) {
+    if (p0.size() != kSlots * 16) throw std::invalid_argument("p0 must be f64[256]");
+    e_->set_p0(p0.data());
+  }
+  void set_join_params(double window_ms, double threshold, int fanout, int group_mode) {
+    e_->set_join_params(window_ms, threshold, fanout, group_mode);
+  }
+  void init_comm(py::bytes id, int rank, int world) {
+    std::string s = id;
+    if (s.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("unique id size");
+    ncclUniqueId u;
+    std::memcpy(&u, s.data(), sizeof(u));
+    py::gil_scoped_release nogil;
+    e_->init_comm(u, rank, world);
+  }
+  py::array_t<double> totals() {
+    std::vector<double> t(kPacketLen);
+    {
+      py::gil_scoped_release nogil;
+      e_->totals(t.data());
+    }
+    return copy_array(t.data(), {kPacketLen});
+  }
+  void reset_totals() {
+    py::gil_scoped_release nogil;
+    e_->reset_totals();
+  }
+  py::array_t<double> stats_acc() {
+    std::vector<double> t(kStatsLen);
+    {
+      py::gil_scoped_release nogil;
+      e_->stats_acc(t.data());
+    }
+    return copy_array(t.data(), {kStatsLen});
+  }
+  py::array_t<uint8_t> model_bytes() {
+    std::vector<uint8_t> t(sizeof(PosteriorModel));
+    {
+      py::gil_scoped_release nogil;
+      e_->model_bytes(t.data());
+    }
+    return copy_array(t.data(), {(py::ssize_t)t.size()});
+  }
+  void sync() {
+    py::gil_scoped_release nogil;
+    e_->sync();
+  }
+  py::dict layout() const {
+    const SlotLayout& L = e_->layout();
+    py::dict d;
+    d["group_cap"] = L.group_cap;
+    d["span_cap"] = L.span_cap;
+    d["sig_cap"] = L.sig_cap;
+    d["row_cap"] = L.row_cap;
+    d["sp_off"] = L.sp_off;
+    d["ev_off"] = L.ev_off;
+    d["bytes"] = L.bytes;
+    return d;
+  }
+  int buffers() const { return e_->buffers(); }
+  int64_t folded() const { return e_->windows_folded(); }
+  size_t graphs() const { return e_->graphs(); }
+  double host_issue_us() const { return e_->host_issue_us(); }
+  bool has_comm() const { return e_->has_comm(); }
+
+ private:
+  std::unique_ptr<WindowEngine> e_;
+};
+
+py::bytes unique_id() {
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) throw std::runtime_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  return py::bytes(reinterpret_cast<const char*>(&u), sizeof(u));
+}
+
+PYBIND11_MODULE(_mislo_agent, m) {
+  m.doc() = "MI355X LLM-SLO native window engine (HIP + RCCL, no PyTorch)";
+  m.def("set_tables", &set_tables_np);
+  m.def("unique_id", &unique_id);
+  m.def("device_count", []() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+  });
+  m.attr("PACKET_LEN") = kPacketLen;
+  m.attr("PACKET_LAYOUT") = py::make_tuple(kPacketHist, kPacketStatus, kPacketMisc, kPacketDbg, kPacketConf,
+                                           kPacketStats, kPacketCount);
+  m.attr("STATS_OFF") = kStatsOff;
+  m.attr("STATS_LEN") = kStatsLen;
+  m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
+  m.attr("CTX_ROWS") = kCtxRows;
+  py::class_<PyEngine>(m, "WindowEngine")
+      .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int>(),
+           py::arg("device") = 0, py::arg("sig_cap") = 1 << 20, py::arg("span_cap") = 16384, py::arg("group_cap") = 64,
+           py::arg("row_cap") = 1 << 17, py::arg("n_buffers") = 3, py::arg("max_ahead") = 3,
+           py::arg("window_ms") = 2000.0, py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1,
+           py::arg("use_graphs") = true, py::arg("device_refit") = true, py::arg("n_dom") = 10)
+      .def("host_slot", &PyEngine::host_slot)
+      .def("slot_view", &PyEngine::slot_view)
+      .def("wait_slot", &PyEngine::wait_slot)
+      .def("submit", &PyEngine::submit, py::arg("k"), py::arg("dma_bytes"), py::arg("n_groups"),
+           py::arg("with_labels") = true, py::arg("learn") = false)
+      .def("query", &PyEngine::query)
+      .def("wait", &PyEngine::wait)
+      .def("packet", &PyEngine::packet)
+      .def("results", &PyEngine::results)
+      .def("window_ms", &PyEngine::window_ms)
+      .def("set_model_bytes", &PyEngine::set_model_bytes)
+      .def("set_p0", &PyEngine::set_p0)
+      .def("set_join_params", &PyEngine::set_join_params)
+      .def("init_comm", &PyEngine::init_comm)
+      .def("totals", &PyEngine::totals)
+      .def("reset_totals", &PyEngine::reset_totals)
+      .def("stats_acc", &PyEngine::stats_acc)
+      .def("model_bytes", &PyEngine::model_bytes)
+      .def("sync", &PyEngine::sync)
+      .def_property_readonly("layout", &PyEngine::layout)
+      .def_property_readonly("buffers", &PyEngine::buffers)
+      .def_property_readonly("windows_folded", &PyEngine::folded)
+      .def_property_readonly("graphs", &PyEngine::graphs)
+      .def_property_readonly("host_issue_us", &PyEngine::host_issue_us)
+      .def_property_readonly("has_comm", &PyEngine::has_comm);
+}

@@ -138,7 +138,6 @@ class Engine {
     confusion = torch::empty({kMaxDomains, kMaxDomains}, i32);
     stats = torch::empty({32, 32}, f64); stats_count = torch::empty({kMaxDomains}, f64);
     packet = torch::empty({kPacketLen}, f64);
-    pod_table = torch::zeros({1}, i32);
     ctx_table = torch::zeros({1, 4}, i32);
     model = torch::zeros({(int64_t)sizeof(PosteriorModel)}, u8);
     join_defaults();
@@ -241,27 +240,7 @@ class Engine {
                      dptr<uint32_t>(g_items), cur_stream());
   }
 
-  // pod id -> (svc << 16 | node) table for compact records (interned by the agent)
-  void set_pod_table(torch::Tensor table) {
-    check_cuda(table, "pod_table");
-    if (table.scalar_type() != torch::kInt32) throw std::invalid_argument("pod_table must be int32");
-    pod_table = table;
-  }
-
-  // events: device buffer of 32-byte compact records (>= sig_cap * 32 bytes)
-  void decode_compact(torch::Tensor events) {
-    check_cuda(events, "events");
-    if (events.nbytes() < (size_t)sig_cap_ * 32)
-      throw std::invalid_argument("events buffer must hold sig_cap 32-byte records");
-    launch_decode_compact(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(pod_table),
-                          (int)pod_table.numel(), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
-                          dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
-                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
-                     dptr<uint32_t>(g_items), cur_stream());
-  }
-
-  // context id -> {pod, pid, conn id, svc<<16|node} (int32 [n, 4]) for 20-byte records
+  // context id -> {pod, pid, conn32, svc<<16|node} (int32 [n, 4]) for EVENT16 records and SPAN20 spans
   void set_ctx_table(torch::Tensor table) {
     check_cuda(table, "ctx_table");
     if (table.scalar_type() != torch::kInt32 || table.dim() != 2 || table.size(1) != 4 || !table.is_contiguous())
@@ -269,27 +248,24 @@ class Engine {
     ctx_table = table;
   }
 
-  // events: device buffer of 24-, 20- or 16-byte records (>= sig_cap * wire bytes); counts[4..5] =
-  // t_base, counts[6] = valid context-table rows (0 = all)
-  void decode_ctx_wire(torch::Tensor events, int64_t wire) {
+  // events: device buffer of 16-byte EVENT16 records (>= sig_cap * 16 bytes); counts[4..5], [8..13] =
+  // epoch bases, counts[6] = valid context-table rows (0 = all)
+  void decode_ctx_wire(torch::Tensor events) {
     check_cuda(events, "events");
-    if (events.nbytes() < (size_t)sig_cap_ * (size_t)wire_bytes((int)wire))
-      throw std::invalid_argument("events buffer must hold sig_cap wire records");
-    if (counts.numel() < (wire == 16 ? 14 : 7))
-      throw std::invalid_argument("wire 24/21/20 need counts int32[>= 7] (t_base, n_ctx), wire 16 int32[>= 14] (epoch bases)");
-    launch_decode_wire(events.data_ptr(), (int)wire, dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
-                      (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
-                      dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
+    if (events.nbytes() < (size_t)sig_cap_ * 16) throw std::invalid_argument("events buffer must hold sig_cap EVENT16 records");
+    if (counts.numel() < 14) throw std::invalid_argument("EVENT16 windows need counts int32[>= 14] (epoch bases)");
+    launch_decode_wire(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
+                       (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
+                       dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
     launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
                      dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
                      dptr<uint32_t>(g_items), cur_stream());
   }
 
   void decode_wire(torch::Tensor events, int64_t wire) {
-    if (wire == 32) decode_compact(events);
-    else if (wire == 24 || wire == kWire20T || wire == 20 || wire == 16) decode_ctx_wire(events, wire);
+    if (wire == 16) decode_ctx_wire(events);
     else if (wire == 64) decode(events);
-    else throw std::invalid_argument("wire must be 64, 32, 24, 21 (EVENT20T), 20 or 16");
+    else throw std::invalid_argument("wire must be 64 (EVENT) or 16 (EVENT16)");
   }
 
   void decode_ref(torch::Tensor events, int64_t pod, int64_t svcnode, int64_t trace_h) {
@@ -371,9 +347,8 @@ class Engine {
                        dptr<double>(packet));
   }
 
-  // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0].
-  // wire: 64 = Event records, 32 = compact EventC32 records, 24 = EventC24, 21 = EventC20T (20 bytes),
-  // 20 = EventC20, 16 = EventC16
+  // Full window: expects events/spans already resident and counts = [n_ev, n_spans, n_groups, 0, ...].
+  // wire: 64 = Event records, 16 = EVENT16
   void run_window(torch::Tensor events, torch::Tensor spans, int64_t n_groups, bool with_labels, bool learn,
                   int64_t wire) {
     reset_window();
@@ -435,7 +410,7 @@ class Engine {
   torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, probe_work;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
   torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
-  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, pod_table, ctx_table;
+  torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, ctx_table;
 
  private:
   int sig_cap_, span_cap_, group_cap_;
@@ -537,8 +512,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("reset_window", &Engine::reset_window)
       .def("decode", &Engine::decode)
       .def("decode_ref", &Engine::decode_ref)
-      .def("decode_compact", &Engine::decode_compact)
-      .def("set_pod_table", &Engine::set_pod_table)
       .def("set_ctx_table", &Engine::set_ctx_table)
       .def("decode_ctx_wire", &Engine::decode_ctx_wire)
       .def("decode_wire", &Engine::decode_wire)
@@ -563,6 +536,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       RO(s_part_base) RO(s_items) RO(probe_work)
       RO(top3) RO(cnt) RO(attrs) RO(conf) RO(kernel_ms) RO(gsum) RO(gcnt) RO(feat) RO(labels) RO(post)
       RO(pred) RO(gconf) RO(evbits) RO(hist) RO(status_cnt) RO(misc) RO(dbg) RO(confusion) RO(stats)
-      RO(stats_count) RO(packet) RO(model) RO(pod_table);
+      RO(stats_count) RO(packet) RO(model) RO(ctx_table);
 #undef RO
 }

@@ -12,8 +12,6 @@
 //
 // The REF-compat variant decodes REF's packed 40-byte record with REF's exact unit
 // rules (pkg/collector/ringbuf.go:199-238) for replaying REF ring-buffer captures.
-#include <type_traits>
-
 #include "mislo_common.h"
 #include "mislo_launch.h"
 
@@ -210,55 +208,14 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
-// 32-byte compact records: half the PCIe bytes of Event; service|node come from the
-// per-agent pod table (device resident), the connection id is already an exact key.
-template <int NT>
-__global__ __launch_bounds__(NT) void k_decode_compact(const EventC32* __restrict__ ev,
-                                                       const int* __restrict__ n_ptr, int cap,
-                                                       const uint32_t* __restrict__ pod_svcnode, int n_pods,
-                                                       DecodeOut o) {
-  __shared__ DecodeLds L;
-  lds_init<NT>(L);
-  const LdsLane l = lds_lane(L);
-
-  const int n = min(*n_ptr, cap);
-  // counts[3] = number of node-local events; events past it are imported halo / remote
-  // trace-tagged copies that take part in the join but not in the window's counters.
-  const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
-  const int chunk = (n + gridDim.x - 1) / gridDim.x;
-  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
-  int unsupported = 0, zero_ts = 0;
-  for (int i = beg + threadIdx.x; i < end; i += NT) {
-    const EventC32 e = ev[i];
-    const int st = (int)(e.type_conn & 0xFFu);
-    const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
-    const float val = (float)((double)e.value_milli * 1e-3);
-    const uint64_t ch = (uint64_t)(e.type_conn >> 8);
-    const uint32_t svcnode = e.pod_id < (uint32_t)n_pods ? pod_svcnode[e.pod_id] : 0u;
-    decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, ch, o, l, unsupported, zero_ts, i < n_local, o.cols.rec + i);
-  }
-  lds_flush<NT>(L, o, unsupported, zero_ts);
-}
-
-// 20-byte (16-byte) records: 5/8 (1/2) of the compact record's PCIe bytes. The window base timestamp is
-// counts[4] | counts[5] << 32; context ids resolve through the device context table
-// (counts[6] valid rows).
-__device__ __forceinline__ uint64_t wire_trace(const EventC20& e) { return ((uint64_t)e.tr_hi << 32) | e.tr_lo; }
+// EVENT16 field accessors: the trace id without its epoch tag; ts = base[tag] + ts_off
 __device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)(e.trace_id & kTraceIdMask); }
-__device__ __forceinline__ uint64_t wire_trace(const EventC24& e) { return e.trace_h; }
-__device__ __forceinline__ uint64_t wire_trace(const EventC20T& e) { return (uint64_t)e.trace_id; }
-__device__ __forceinline__ int64_t wire_ts(const EventC20& e, const int64_t* base) {
-  return e.ts_off == kTsZero ? 0 : base[0] + (int64_t)e.ts_off;
-}
 __device__ __forceinline__ int64_t wire_ts(const EventC16& e, const int64_t* base) {
   return e.ts_off == kTsZero ? 0 : base[e.trace_id >> kEpochTagShift] + (int64_t)e.ts_off;
 }
-__device__ __forceinline__ int64_t wire_ts(const EventC24& e, const int64_t*) { return e.ts_ns; }
-__device__ __forceinline__ int64_t wire_ts(const EventC20T& e, const int64_t*) { return e.ts_ns; }
 
-// Rec = EventC20 (20-byte), EventC16 (16-byte, interned trace ids), EventC24 (24-byte,
-// absolute timestamps: the probes' context-interned ring record) or EventC20T (20-byte,
-// absolute timestamps, kernel-interned trace ids): identical decoding otherwise.
+// EVENT16 records (the BPF ring's payloads, compacted by the agent's consumer, plus host-encoded
+// user-space records). Context rows resolve through the device context table.
 template <int NT, class Rec>
 __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, const int* __restrict__ n_ptr,
                                                     int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
@@ -271,12 +228,7 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
   const int n_local = n_ptr[3] > 0 ? min(n_ptr[3], n) : n;
   // epoch bases: [0] = counts[4..5] (the window base), [1..3] = counts[8..13]
   auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
-  int64_t t_base[4] = {base_at(4), 0, 0, 0};
-  if constexpr (std::is_same<Rec, EventC16>::value) {  // only tagged records read bases 1-3
-    t_base[1] = base_at(8);
-    t_base[2] = base_at(10);
-    t_base[3] = base_at(12);
-  }
+  const int64_t t_base[4] = {base_at(4), base_at(8), base_at(10), base_at(12)};
   // counts[6] = rows of the (fixed-capacity, append-only) context table valid this window
   if (n_ptr[6] > 0) n_ctx = min(n_ptr[6], n_ctx);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -443,33 +395,13 @@ void launch_decode_events(const void* ev, const int* n_dev, int cap, const Signa
                      (const Event*)ev, n_dev, cap, o);
 }
 
-void launch_decode_compact(const void* ev, const int* n_dev, int cap, const uint32_t* pod_svcnode, int n_pods,
-                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
-                           unsigned long long* misc, hipStream_t stream) {
-  DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
-  constexpr int NT = kDecodeNT;
-  hipLaunchKernelGGL((k_decode_compact<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, (const EventC32*)ev, n_dev,
-                     cap, pod_svcnode, n_pods, o);
-}
-
-void launch_decode_wire(const void* ev, int wire, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
+void launch_decode_wire(const void* ev, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
                         const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                         unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
   constexpr int NT = kDecodeNT;
-  const uint4* tab = reinterpret_cast<const uint4*>(ctx_tab);
-  if (wire == 16)
-    hipLaunchKernelGGL((k_decode_wire<NT, EventC16>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
-                       (const EventC16*)ev, n_dev, cap, tab, n_ctx, o);
-  else if (wire == 24)
-    hipLaunchKernelGGL((k_decode_wire<NT, EventC24>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
-                       (const EventC24*)ev, n_dev, cap, tab, n_ctx, o);
-  else if (wire == kWire20T)
-    hipLaunchKernelGGL((k_decode_wire<NT, EventC20T>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
-                       (const EventC20T*)ev, n_dev, cap, tab, n_ctx, o);
-  else
-    hipLaunchKernelGGL((k_decode_wire<NT, EventC20>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
-                       (const EventC20*)ev, n_dev, cap, tab, n_ctx, o);
+  hipLaunchKernelGGL((k_decode_wire<NT, EventC16>), dim3(decode_grid(cap)), dim3(NT), 0, stream,
+                     (const EventC16*)ev, n_dev, cap, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, o);
 }
 
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,

@@ -1,0 +1,162 @@
+// Native per-GPU window engine: the agent's executor, with no Python or PyTorch on the
+// per-window path. One process drives one MI355X; window k uses buffer b = k % nb (nb = 3):
+//
+//   host           : WindowAssembler fills pinned input block b (slot.h) after the H2D of
+//                    window k - nb (its previous reader) completed (wait_slot)
+//   copy stream    : ONE DMA of the block's used prefix -> device block b
+//   compute stream : [device refit from window k - nb's all-reduced statistics]
+//                    graph(b): reset accumulators -> context-row patch -> K1 decode ->
+//                    partition -> spans -> K2 LDS join -> finalize -> K3 MFMA posterior
+//                    (+ confusion, + MFMA sufficient statistics when learning) -> pack(packet b)
+//                    -> D2H of the window's per-incident results into pinned results b
+//   comm stream    : RCCL all-reduce(packet b) over xGMI when the node has several GPUs ->
+//                    totals += packet b -> D2H(packet b)
+//
+// so the DMA of window k+1 and the node-wide all-reduce of window k run under the kernels of
+// window k+1. The whole compute chain of a buffer is captured once into a HIP graph and
+// replayed (one launch per window). Host waits use blocking-sync events (no spin: the
+// agent's CPU budget, REF pkg/safety/overhead_guard.go:77-107, counts this process).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <tuple>
+#include <vector>
+
+#include "mislo_launch.h"
+#include "slot.h"
+
+namespace mislo {
+
+constexpr int kPacketHist = kSlots * kBuckets;          // 256
+constexpr int kPacketStatus = kSlots * 3;               // 48
+constexpr int kPacketMisc = 2 + kSlots;                 // unsupported, zero-ts, per-slot value sums (milli)
+constexpr int kPacketDbg = 8;
+constexpr int kPacketConf = kMaxDomains * kMaxDomains;  // 256
+constexpr int kPacketStats = 32 * 32;                   // 1024
+constexpr int kPacketCount = kMaxDomains;               // 16
+constexpr int kPacketLen = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf + kPacketStats + kPacketCount;
+constexpr int kStatsOff = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf;
+constexpr int kStatsLen = kPacketStats + kPacketCount;  // accumulated-statistics vector (f64[1040])
+constexpr uint32_t kCtxRows = 1u << 24;                 // device context table rows (256 MiB)
+
+struct EngineConfig {
+  int device = 0;
+  int sig_cap = 1 << 20, span_cap = 16384, group_cap = 64, row_cap = 1 << 17;
+  int n_buffers = 3, max_ahead = 3;
+  double window_ms = 2000.0, threshold = 0.7;
+  int fanout = 3, group_mode = 1;
+  bool use_graphs = true;
+  bool device_refit = true;  // learned naive Bayes refit on the device from accumulated statistics
+  double alpha = 2.0, prior_pseudo = 1.0;
+  int n_dom = 10;
+};
+
+// per-incident results of a window, in one pinned block (one D2H)
+struct ResultView {
+  const double* post;     // [G][16]
+  const double* gconf;    // [G]
+  const float* feat;      // [G][16]
+  const int32_t* pred;    // [G]
+  const uint32_t* evbits; // [G][16]
+};
+
+class WindowEngine {
+ public:
+  explicit WindowEngine(const EngineConfig& cfg);
+  ~WindowEngine();
+  WindowEngine(const WindowEngine&) = delete;
+  WindowEngine& operator=(const WindowEngine&) = delete;
+
+  const SlotLayout& layout() const { return L_; }
+  const EngineConfig& config() const { return cfg_; }
+  int buffers() const { return nb_; }
+
+  uint8_t* host_slot(int64_t k) const { return slot_host_[k % nb_]; }
+  void wait_slot(int64_t k);  // the H2D of window k - nb (the slot's previous reader) is done
+  void submit(int64_t k, size_t dma_bytes, int n_groups, bool with_labels, bool learn);
+  bool query(int64_t k);      // window k's results are in host memory
+  void wait(int64_t k);
+  const double* packet(int64_t k) const { return packet_host_[k % nb_]; }
+  ResultView results(int64_t k) const;
+  // device time of window k (ms): DMA start -> results in host memory, and the compute stream's share
+  std::pair<float, float> window_ms(int64_t k);
+
+  void set_model_bytes(const void* bytes, size_t n);  // stream-ordered before the next window
+  void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
+  void set_join_params(double window_ms, double threshold, int fanout, int group_mode);
+  void init_comm(const ncclUniqueId& id, int rank, int world);
+  bool has_comm() const { return comm_ != nullptr; }
+
+  void totals(double* out);           // accumulated (all-reduced) packets (synchronous)
+  void reset_totals();
+  void stats_acc(double* out);        // the device refit's accumulated statistics (synchronous)
+  void model_bytes(void* out);        // the model currently on the device (synchronous)
+  void sync();
+  int64_t windows_folded() const { return folded_; }
+  size_t graphs() const { return graphs_.size(); }
+  double host_issue_us() const { return issue_n_ ? issue_us_ / issue_n_ : 0.0; }
+
+ private:
+  void alloc();
+  void run_chain(int b, int n_groups, bool with_labels, bool learn, hipStream_t st);
+  SignalCols sig_cols() const;
+  SpanCols span_cols() const;
+
+  EngineConfig cfg_;
+  SlotLayout L_;
+  int nb_, max_ahead_;
+  JoinParams jp_{};
+  int nblk_sig_ = 1, nblk_span_ = 1;
+  hipStream_t copy_ = nullptr, compute_ = nullptr, comm_stream_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  // device buffers
+  std::vector<uint8_t*> slot_dev_;
+  std::vector<uint8_t*> slot_host_;
+  std::vector<double*> packet_dev_;
+  std::vector<double*> packet_host_;
+  std::vector<uint8_t*> res_dev_, res_host_;
+  size_t res_bytes_ = 0;
+  uint32_t* ctx_tab_ = nullptr;
+  double *totals_ = nullptr, *stats_acc_ = nullptr, *p0_ = nullptr;
+  uint8_t* model_dev_ = nullptr;
+  std::vector<uint8_t*> model_host_;
+  int model_slot_ = 0;
+  uint8_t* g_status_ = nullptr;
+  PartCodes* g_part_ = nullptr;
+  uint32_t *g_part_blk_ = nullptr, *g_part_off_ = nullptr, *g_part_tot_ = nullptr, *g_part_base_ = nullptr,
+           *g_items_ = nullptr;
+  SigRec* g_rec_ = nullptr;
+  PartCodes* s_part_ = nullptr;
+  uint32_t *s_part_blk_ = nullptr, *s_part_off_ = nullptr, *s_part_tot_ = nullptr, *s_part_base_ = nullptr,
+           *s_items_ = nullptr, *probe_work_ = nullptr;
+  SpanRec* s_rec_ = nullptr;
+  unsigned long long* top3_ = nullptr;
+  uint32_t* cnt_ = nullptr;
+  float *attrs_ = nullptr, *conf_ = nullptr, *kernel_ms_ = nullptr;
+  unsigned long long* gsum_ = nullptr;
+  uint32_t* gcnt_ = nullptr;
+  uint32_t *hist_ = nullptr, *status_ = nullptr, *confusion_ = nullptr;
+  unsigned long long *misc_ = nullptr, *dbg_ = nullptr;
+  double *stats_ = nullptr, *stats_count_ = nullptr;
+  // results block views (device)
+  double *post_ = nullptr, *gconf_ = nullptr;
+  float* feat_ = nullptr;
+  int32_t* pred_ = nullptr;
+  uint32_t* evbits_ = nullptr;
+  // events
+  std::vector<hipEvent_t> h2d_done_, compute_done_, comm_done_;
+  std::vector<hipEvent_t> t_start_, t_comp0_, t_comp1_, t_end_;
+  std::map<std::tuple<int, int, bool, bool>, hipGraphExec_t> graphs_;
+  std::vector<bool> warm_;
+  std::vector<hipGraph_t> graph_defs_;
+  int64_t submitted_ = 0, folded_ = 0;
+  double issue_us_ = 0;
+  int64_t issue_n_ = 0;
+};
+
+void engine_set_tables(const Tables& t);
+
+}  // namespace mislo

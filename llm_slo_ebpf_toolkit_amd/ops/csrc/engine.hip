@@ -1,0 +1,447 @@
+// Native per-GPU window engine (engine.h) and its small glue kernels.
+#include "engine.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace mislo {
+
+namespace {
+
+#define HIPCHECK(x)                                                                                  \
+  do {                                                                                               \
+    hipError_t _e = (x);                                                                             \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
+                                                   " at " #x);                                       \
+  } while (0)
+
+#define NCCLCHECK(x)                                                                                        \
+  do {                                                                                                      \
+    ncclResult_t _r = (x);                                                                                  \
+    if (_r != ncclSuccess) throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(_r) + \
+                                                    " at " #x);                                             \
+  } while (0)
+
+// One launch that zero/poison-fills every per-window accumulator.
+struct FillSeg {
+  uint32_t* ptr;
+  uint32_t n;  // 32-bit words
+  uint32_t value;
+};
+constexpr int kMaxFill = 12;
+struct FillList {
+  FillSeg seg[kMaxFill];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void k_fill(FillList fl) {
+  for (int q = 0; q < fl.count; ++q) {
+    const FillSeg sg = fl.seg[q];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sg.n; i += gridDim.x * 256) sg.ptr[i] = sg.value;
+  }
+}
+
+// The window's context-row patch (slot.h: behind the events, ids then uint4 rows) scattered
+// into the device context table before the decode reads it. Sizes come from the block's
+// counts, so one captured launch serves every window.
+__global__ __launch_bounds__(256) void k_apply_rows(const uint8_t* __restrict__ slot, size_t ev_off,
+                                                    uint4* __restrict__ table, uint32_t table_rows) {
+  const int32_t* c = reinterpret_cast<const int32_t*>(slot);
+  const uint32_t n_ev = (uint32_t)c[0], n_rows = (uint32_t)c[14];
+  const uint8_t* patch = slot + ev_off + 16 * (size_t)n_ev;
+  const uint32_t* ids = reinterpret_cast<const uint32_t*>(patch);
+  const uint4* rows = reinterpret_cast<const uint4*>(patch + ((4 * (size_t)n_rows + 15) & ~size_t(15)));
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_rows; i += gridDim.x * 256) {
+    const uint32_t id = ids[i];
+    if (id < table_rows) table[id] = rows[i];
+  }
+}
+
+// accumulators -> packet (f64), one element per thread
+__global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsigned long long* misc,
+                       const unsigned long long* dbg, const uint32_t* confusion, const double* stats,
+                       const double* count, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int o = 0;
+  if (i < kPacketHist) { out[i] = hist[i]; return; }
+  o += kPacketHist;
+  if (i < o + kPacketStatus) { out[i] = status[i - o]; return; }
+  o += kPacketStatus;
+  if (i < o + kPacketMisc) { out[i] = (double)misc[i - o]; return; }
+  o += kPacketMisc;
+  if (i < o + kPacketDbg) { out[i] = (double)dbg[i - o]; return; }
+  o += kPacketDbg;
+  if (i < o + kPacketConf) { out[i] = confusion[i - o]; return; }
+  o += kPacketConf;
+  if (i < o + kPacketStats) { out[i] = stats[i - o]; return; }
+  o += kPacketStats;
+  if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
+}
+
+__global__ void k_accumulate(const double* __restrict__ packet, double* __restrict__ totals, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) totals[i] += packet[i];
+}
+
+template <class T>
+T* dalloc(size_t n) {
+  void* p = nullptr;
+  HIPCHECK(hipMalloc(&p, n * sizeof(T) + 64));
+  return static_cast<T*>(p);
+}
+
+hipEvent_t mk_event(bool timing) {
+  hipEvent_t e;
+  HIPCHECK(hipEventCreateWithFlags(&e, timing ? hipEventDefault : (hipEventDisableTiming | hipEventBlockingSync)));
+  return e;
+}
+
+}  // namespace
+
+void engine_set_tables(const Tables& t) { set_tables(&t); }
+
+WindowEngine::WindowEngine(const EngineConfig& cfg) : cfg_(cfg) {
+  if (cfg.sig_cap <= 0 || cfg.span_cap <= 0 || cfg.group_cap <= 0 || cfg.group_cap > 4096)
+    throw std::invalid_argument("capacities out of range");
+  if (cfg.sig_cap >= (1 << 27)) throw std::invalid_argument("sig_cap must be < 2^27 (top-3 key packing)");
+  nb_ = std::max(2, cfg.n_buffers);
+  max_ahead_ = std::min(nb_, std::max(1, cfg.max_ahead));
+  L_ = slot_layout((uint32_t)cfg.group_cap, (uint32_t)cfg.span_cap, (uint32_t)cfg.sig_cap, (uint32_t)cfg.row_cap);
+  HIPCHECK(hipSetDevice(cfg.device));
+  set_join_params(cfg.window_ms, cfg.threshold, cfg.fanout, cfg.group_mode);
+  alloc();
+}
+
+void WindowEngine::set_join_params(double window_ms, double threshold, int fanout, int group_mode) {
+  const int64_t ms = 1000000;
+  int64_t outer = (int64_t)llround(window_ms * ms);
+  if (outer <= 0) outer = 2000 * ms;
+  if (outer >= (1LL << 35)) throw std::invalid_argument("window too large for top-3 key packing (< 34 s)");
+  jp_.outer_ns = outer;
+  const int64_t tw[4] = {outer, 100 * ms, 250 * ms, 500 * ms};
+  for (int k = 0; k < 4; ++k) jp_.win_ns[k] = std::min(outer, tw[k]);
+  const float cf[4] = {1.0f, 0.9f, 0.8f, 0.65f};
+  for (int k = 0; k < 4; ++k) jp_.conf[k] = cf[k];
+  jp_.threshold = threshold > 0 ? (float)threshold : 0.7f;
+  if (fanout <= 0) fanout = 3;
+  if (fanout > 3) throw std::invalid_argument("GPU join keeps at most 3 candidates per span");
+  jp_.fanout = fanout;
+  jp_.group_mode = group_mode;
+  graphs_.clear();  // captured launches hold the old parameters
+}
+
+void WindowEngine::alloc() {
+  const int64_t N = cfg_.sig_cap, S = cfg_.span_cap, G = cfg_.group_cap;
+  nblk_sig_ = decode_grid((int)N);
+  nblk_span_ = decode_grid((int)S);
+  HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  HIPCHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  for (int b = 0; b < nb_; ++b) {
+    slot_dev_.push_back(dalloc<uint8_t>(L_.bytes));
+    HIPCHECK(hipMemset(slot_dev_.back(), 0, L_.bytes));
+    void* h = nullptr;
+    HIPCHECK(hipHostMalloc(&h, L_.bytes, hipHostMallocDefault));
+    std::memset(h, 0, L_.bytes);
+    slot_host_.push_back(static_cast<uint8_t*>(h));
+    packet_dev_.push_back(dalloc<double>(kPacketLen));
+    HIPCHECK(hipMemset(packet_dev_.back(), 0, kPacketLen * sizeof(double)));
+    HIPCHECK(hipHostMalloc(&h, kPacketLen * sizeof(double), hipHostMallocDefault));
+    std::memset(h, 0, kPacketLen * sizeof(double));
+    packet_host_.push_back(static_cast<double*>(h));
+    h2d_done_.push_back(mk_event(false));
+    compute_done_.push_back(mk_event(false));
+    comm_done_.push_back(mk_event(false));
+    t_start_.push_back(mk_event(true));
+    t_comp0_.push_back(mk_event(true));
+    t_comp1_.push_back(mk_event(true));
+    t_end_.push_back(mk_event(true));
+  }
+  warm_.assign(nb_, false);
+  // per-incident results block: [post G*16 f64][gconf G f64][feat G*16 f32][pred G i32][evbits G*16 u32]
+  const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
+  res_bytes_ = o_ev + 16 * G * 4;
+  for (int b = 0; b < nb_; ++b) {
+    void* h = nullptr;
+    HIPCHECK(hipHostMalloc(&h, res_bytes_, hipHostMallocDefault));
+    std::memset(h, 0, res_bytes_);
+    res_host_.push_back(static_cast<uint8_t*>(h));
+  }
+  res_dev_.push_back(dalloc<uint8_t>(res_bytes_));
+  uint8_t* r = res_dev_[0];
+  post_ = reinterpret_cast<double*>(r);
+  gconf_ = reinterpret_cast<double*>(r + o_gconf);
+  feat_ = reinterpret_cast<float*>(r + o_feat);
+  pred_ = reinterpret_cast<int32_t*>(r + o_pred);
+  evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
+  HIPCHECK(hipMemset(r, 0, res_bytes_));
+  // context table: every id the kernel or the host encoder can assign, HBM-resident
+  ctx_tab_ = dalloc<uint32_t>((size_t)kCtxRows * 4);
+  HIPCHECK(hipMemset(ctx_tab_, 0, (size_t)kCtxRows * 16));
+  totals_ = dalloc<double>(kPacketLen);
+  HIPCHECK(hipMemset(totals_, 0, kPacketLen * sizeof(double)));
+  stats_acc_ = dalloc<double>(kStatsLen);
+  HIPCHECK(hipMemset(stats_acc_, 0, kStatsLen * sizeof(double)));
+  p0_ = dalloc<double>(kSlots * 16);
+  HIPCHECK(hipMemset(p0_, 0, kSlots * 16 * sizeof(double)));
+  model_dev_ = dalloc<uint8_t>(sizeof(PosteriorModel));
+  HIPCHECK(hipMemset(model_dev_, 0, sizeof(PosteriorModel)));
+  for (int i = 0; i < max_ahead_ + 2; ++i) {
+    void* h = nullptr;
+    HIPCHECK(hipHostMalloc(&h, sizeof(PosteriorModel), hipHostMallocDefault));
+    model_host_.push_back(static_cast<uint8_t*>(h));
+  }
+  g_status_ = dalloc<uint8_t>(N);
+  g_part_ = dalloc<PartCodes>(N);
+  g_part_blk_ = dalloc<uint32_t>((size_t)nblk_sig_ * kKeyTypes * kParts);
+  g_part_off_ = dalloc<uint32_t>((size_t)nblk_sig_ * kKeyTypes * kParts);
+  g_part_tot_ = dalloc<uint32_t>(kKeyTypes * kParts);
+  g_part_base_ = dalloc<uint32_t>(kKeyTypes * kParts + 1);
+  g_items_ = dalloc<uint32_t>(kKeyTypes * N);
+  g_rec_ = dalloc<SigRec>(N);
+  s_part_ = dalloc<PartCodes>(S);
+  s_part_blk_ = dalloc<uint32_t>((size_t)nblk_span_ * kKeyTypes * kParts);
+  s_part_off_ = dalloc<uint32_t>((size_t)nblk_span_ * kKeyTypes * kParts);
+  s_part_tot_ = dalloc<uint32_t>(kKeyTypes * kParts);
+  s_part_base_ = dalloc<uint32_t>(kKeyTypes * kParts + 1);
+  s_items_ = dalloc<uint32_t>(kKeyTypes * S);
+  s_rec_ = dalloc<SpanRec>(S);
+  probe_work_ = dalloc<uint32_t>(kProbeWorkLen);
+  HIPCHECK(hipMemset(probe_work_, 0, kProbeWorkLen * 4));
+  top3_ = dalloc<unsigned long long>(3 * S);
+  cnt_ = dalloc<uint32_t>(S);
+  attrs_ = dalloc<float>(S * kSlots);
+  conf_ = dalloc<float>(S);
+  kernel_ms_ = dalloc<float>(S);
+  gsum_ = dalloc<unsigned long long>((size_t)kGroupStripes * G * kSlots);
+  gcnt_ = dalloc<uint32_t>((size_t)kGroupStripes * G * kSlots);
+  hist_ = dalloc<uint32_t>(kSlots * kBuckets);
+  status_ = dalloc<uint32_t>(kSlots * 3);
+  misc_ = dalloc<unsigned long long>(kPacketMisc);
+  dbg_ = dalloc<unsigned long long>(kPacketDbg);
+  confusion_ = dalloc<uint32_t>(kMaxDomains * kMaxDomains);
+  stats_ = dalloc<double>(32 * 32);
+  stats_count_ = dalloc<double>(kMaxDomains);
+  HIPCHECK(hipDeviceSynchronize());
+}
+
+WindowEngine::~WindowEngine() {
+  hipDeviceSynchronize();
+  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  for (auto g : graph_defs_) hipGraphDestroy(g);
+  if (comm_) ncclCommDestroy(comm_);
+  auto evs = {&h2d_done_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
+  for (auto* v : evs)
+    for (auto e : *v) hipEventDestroy(e);
+  for (auto p : slot_host_) hipHostFree(p);
+  for (auto p : packet_host_) hipHostFree(p);
+  for (auto p : res_host_) hipHostFree(p);
+  for (auto p : model_host_) hipHostFree(p);
+  for (auto p : slot_dev_) hipFree(p);
+  for (auto p : packet_dev_) hipFree(p);
+  for (auto p : res_dev_) hipFree(p);
+  void* bufs[] = {ctx_tab_, totals_, stats_acc_, p0_, model_dev_, g_status_, g_part_, g_part_blk_, g_part_off_,
+                  g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
+                  s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
+                  hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (copy_) hipStreamDestroy(copy_);
+  if (compute_) hipStreamDestroy(compute_);
+  if (comm_stream_) hipStreamDestroy(comm_stream_);
+}
+
+SignalCols WindowEngine::sig_cols() const { return SignalCols{g_rec_, g_status_, g_part_}; }
+SpanCols WindowEngine::span_cols() const { return SpanCols{s_rec_, s_part_}; }
+
+void WindowEngine::wait_slot(int64_t k) {
+  if (k >= nb_) HIPCHECK(hipEventSynchronize(h2d_done_[k % nb_]));
+}
+
+// The captured part of a window: everything between the DMA and the packet.
+void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, hipStream_t st) {
+  uint8_t* slot = slot_dev_[b];
+  const int* counts = reinterpret_cast<const int*>(slot);
+  const int32_t* labels = reinterpret_cast<const int32_t*>(slot + 64);
+  const int N = cfg_.sig_cap, S = cfg_.span_cap, G = cfg_.group_cap;
+  FillList fl{};
+  auto add = [&](void* p, size_t bytes, uint32_t v) { fl.seg[fl.count++] = FillSeg{(uint32_t*)p, (uint32_t)(bytes / 4), v}; };
+  add(hist_, kSlots * kBuckets * 4, 0);
+  add(status_, kSlots * 3 * 4, 0);
+  add(misc_, kPacketMisc * 8, 0);
+  add(dbg_, kPacketDbg * 8, 0);
+  add(confusion_, kMaxDomains * kMaxDomains * 4, 0);
+  add(stats_, 32 * 32 * 8, 0);
+  add(stats_count_, kMaxDomains * 8, 0);
+  add(top3_, 3 * (size_t)S * 8, 0xFFFFFFFFu);
+  add(cnt_, (size_t)S * 4, 0);
+  add(gsum_, (size_t)kGroupStripes * G * kSlots * 8, 0);
+  add(gcnt_, (size_t)kGroupStripes * G * kSlots * 4, 0);
+  hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, st, fl);
+  hipLaunchKernelGGL(k_apply_rows, dim3(64), dim3(256), 0, st, slot, L_.ev_off, reinterpret_cast<uint4*>(ctx_tab_),
+                     kCtxRows);
+  launch_decode_wire(slot + L_.ev_off, counts, N, ctx_tab_, (int)kCtxRows, sig_cols(), hist_, status_, g_part_blk_,
+                     misc_, st);
+  launch_partition(g_part_, counts, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
+  launch_decode_spans(slot + L_.sp_off, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st);
+  launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
+                   st);
+  launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), g_items_, g_part_base_, N, S, jp_, top3_, cnt_,
+               n_groups, gsum_, gcnt_, dbg_, probe_work_, st);
+  launch_finalize(counts + 1, S, top3_, cnt_, sig_cols(), span_cols(), jp_, nullptr, attrs_, conf_, kernel_ms_,
+                  n_groups, gsum_, gcnt_, feat_, dbg_, st);
+  const PosteriorModel* pm = reinterpret_cast<const PosteriorModel*>(model_dev_);
+  if (learn)
+    launch_posterior_stats(feat_, counts + 2, G, pm, with_labels ? labels : nullptr, post_, pred_, gconf_, evbits_,
+                           confusion_, labels, nullptr, stats_, stats_count_, st);
+  else
+    launch_posterior(feat_, counts + 2, G, pm, with_labels ? labels : nullptr, post_, pred_, gconf_, evbits_,
+                     confusion_, st);
+  hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
+                     stats_, stats_count_, packet_dev_[b]);
+}
+
+void WindowEngine::submit(int64_t k, size_t dma_bytes, int n_groups, bool with_labels, bool learn) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (k != submitted_) throw std::invalid_argument("windows must be submitted in order");
+  if (n_groups < 0 || n_groups > cfg_.group_cap) throw std::invalid_argument("n_groups exceeds group capacity");
+  if (dma_bytes < L_.ev_off || dma_bytes > L_.bytes) throw std::invalid_argument("dma_bytes outside the slot");
+  // the host checks what the kernels will assume before launching them
+  const int32_t* c = reinterpret_cast<const int32_t*>(slot_host_[k % nb_]);
+  if (c[0] < 0 || c[0] > cfg_.sig_cap || c[1] < 0 || c[1] > cfg_.span_cap || c[2] != n_groups || c[14] < 0 ||
+      slot_dma_bytes(L_, (uint32_t)c[0], (uint32_t)c[14]) > dma_bytes)
+    throw std::invalid_argument("slot counts inconsistent with the window (events/spans/groups/rows/dma bytes)");
+  const int b = (int)(k % nb_);
+  // host back-pressure: at most max_ahead windows queued beyond the one computing
+  if (k >= max_ahead_) HIPCHECK(hipEventSynchronize(compute_done_[(k - max_ahead_) % nb_]));
+  // DMA of the input block once window k - nb (the device block's previous reader) computed
+  HIPCHECK(hipStreamWaitEvent(copy_, compute_done_[b], 0));
+  HIPCHECK(hipEventRecord(t_start_[b], copy_));
+  HIPCHECK(hipMemcpyAsync(slot_dev_[b], slot_host_[b], dma_bytes, hipMemcpyHostToDevice, copy_));
+  HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
+  HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
+  HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
+  HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
+  if (cfg_.device_refit && k >= nb_) {
+    // fold window k - nb's all-reduced statistics (packet b) and refit before window k: a
+    // deterministic prequential lag of nb, identical on every rank
+    launch_refit_nb(stats_acc_, packet_dev_[b] + kStatsOff, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
+                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_);
+    ++folded_;
+  }
+  if (!cfg_.use_graphs) {
+    run_chain(b, n_groups, with_labels, learn, compute_);
+  } else {
+    auto key = std::make_tuple(b, n_groups, with_labels, learn);
+    auto it = graphs_.find(key);
+    if (it == graphs_.end() && !warm_[b]) {  // first use of the buffers: run eagerly once
+      run_chain(b, n_groups, with_labels, learn, compute_);
+      warm_[b] = true;
+    } else {
+      if (it == graphs_.end()) {
+        hipGraph_t g;
+        HIPCHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+        run_chain(b, n_groups, with_labels, learn, compute_);
+        HIPCHECK(hipStreamEndCapture(compute_, &g));
+        hipGraphExec_t ex;
+        HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+        graph_defs_.push_back(g);
+        it = graphs_.emplace(key, ex).first;
+      }
+      HIPCHECK(hipGraphLaunch(it->second, compute_));
+    }
+  }
+  // per-incident results of this window (the buffers are reused by the next window)
+  HIPCHECK(hipMemcpyAsync(res_host_[b], res_dev_[0], res_bytes_, hipMemcpyDeviceToHost, compute_));
+  HIPCHECK(hipEventRecord(t_comp1_[b], compute_));
+  HIPCHECK(hipEventRecord(compute_done_[b], compute_));
+  HIPCHECK(hipStreamWaitEvent(comm_stream_, compute_done_[b], 0));
+  if (comm_) NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen, ncclFloat64, ncclSum, comm_, comm_stream_));
+  hipLaunchKernelGGL(k_accumulate, dim3((kPacketLen + 255) / 256), dim3(256), 0, comm_stream_, packet_dev_[b], totals_,
+                     kPacketLen);
+  HIPCHECK(hipMemcpyAsync(packet_host_[b], packet_dev_[b], kPacketLen * sizeof(double), hipMemcpyDeviceToHost,
+                          comm_stream_));
+  HIPCHECK(hipEventRecord(t_end_[b], comm_stream_));
+  HIPCHECK(hipEventRecord(comm_done_[b], comm_stream_));
+  ++submitted_;
+  issue_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  ++issue_n_;
+}
+
+bool WindowEngine::query(int64_t k) {
+  const hipError_t e = hipEventQuery(comm_done_[k % nb_]);
+  if (e == hipSuccess) return true;
+  if (e == hipErrorNotReady) return false;
+  HIPCHECK(e);
+  return false;
+}
+
+void WindowEngine::wait(int64_t k) { HIPCHECK(hipEventSynchronize(comm_done_[k % nb_])); }
+
+ResultView WindowEngine::results(int64_t k) const {
+  const uint8_t* r = res_host_[k % nb_];
+  const size_t G = cfg_.group_cap;
+  const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
+  return ResultView{reinterpret_cast<const double*>(r), reinterpret_cast<const double*>(r + o_gconf),
+                    reinterpret_cast<const float*>(r + o_feat), reinterpret_cast<const int32_t*>(r + o_pred),
+                    reinterpret_cast<const uint32_t*>(r + o_ev)};
+}
+
+std::pair<float, float> WindowEngine::window_ms(int64_t k) {
+  const int b = (int)(k % nb_);
+  float total = 0.f, comp = 0.f;
+  HIPCHECK(hipEventSynchronize(t_end_[b]));
+  HIPCHECK(hipEventElapsedTime(&total, t_start_[b], t_end_[b]));
+  HIPCHECK(hipEventElapsedTime(&comp, t_comp0_[b], t_comp1_[b]));
+  return {total, comp};
+}
+
+void WindowEngine::set_model_bytes(const void* bytes, size_t n) {
+  if (n != sizeof(PosteriorModel)) throw std::invalid_argument("model image must be POSTERIOR_MODEL_BYTES bytes");
+  // a pinned staging slot not read by any queued copy: at most max_ahead windows are queued
+  uint8_t* h = model_host_[model_slot_++ % model_host_.size()];
+  std::memcpy(h, bytes, n);
+  HIPCHECK(hipMemcpyAsync(model_dev_, h, n, hipMemcpyHostToDevice, compute_));
+}
+
+void WindowEngine::set_p0(const double* p0) {
+  HIPCHECK(hipMemcpy(p0_, p0, kSlots * 16 * sizeof(double), hipMemcpyHostToDevice));
+}
+
+void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
+  if (comm_) throw std::logic_error("communicator already initialised");
+  if (world <= 1) return;
+  HIPCHECK(hipSetDevice(cfg_.device));
+  NCCLCHECK(ncclCommInitRank(&comm_, world, id, rank));
+}
+
+void WindowEngine::totals(double* out) {
+  sync();
+  HIPCHECK(hipMemcpy(out, totals_, kPacketLen * sizeof(double), hipMemcpyDeviceToHost));
+}
+
+void WindowEngine::reset_totals() {
+  sync();
+  HIPCHECK(hipMemset(totals_, 0, kPacketLen * sizeof(double)));
+}
+
+void WindowEngine::stats_acc(double* out) {
+  sync();
+  HIPCHECK(hipMemcpy(out, stats_acc_, kStatsLen * sizeof(double), hipMemcpyDeviceToHost));
+}
+
+void WindowEngine::model_bytes(void* out) {
+  sync();
+  HIPCHECK(hipMemcpy(out, model_dev_, sizeof(PosteriorModel), hipMemcpyDeviceToHost));
+}
+
+void WindowEngine::sync() {
+  HIPCHECK(hipStreamSynchronize(copy_));
+  HIPCHECK(hipStreamSynchronize(compute_));
+  HIPCHECK(hipStreamSynchronize(comm_stream_));
+}
+
+}  // namespace mislo

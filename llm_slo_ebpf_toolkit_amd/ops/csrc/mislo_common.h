@@ -34,36 +34,14 @@ struct alignas(64) Event {
 };
 static_assert(sizeof(Event) == 64, "Event must be 64 bytes");
 
-// 32-byte compact wire record (collector/records.py EVENT32): what producers write into
-// the ring when PCIe bytes matter. Workload identity is interned at the source (the BPF
-// probes map cgroup -> pod id and the 5-tuple -> connection id in kernel maps that the
-// agent owns), service/node are looked up on the device from the pod id, and the value
-// is fixed-point in 1/1000 of the signal's output unit (1 us for ms latencies).
-struct alignas(32) EventC32 {
-  int64_t ts_ns;
-  uint64_t trace_h;
-  uint32_t value_milli;
-  uint32_t pid;
-  uint32_t pod_id;
-  uint32_t type_conn;  // bits 0-7 signal_type, bits 8-31 interned connection id (0 = none)
-};
-static_assert(sizeof(EventC32) == 32, "EventC32 must be 32 bytes");
-
-// 20-byte wire record (collector/records.py EVENT20): timestamp as an offset from the
-// window base (counts[4..5]), workload identity as an interned context id that indexes
-// the device context table {pod, pid, conn id, svc<<16|node}; trace hash kept whole.
-struct EventC20 {
-  uint32_t ts_off;       // ts - t_base; kTsZero = zero timestamp (never joins)
-  uint32_t ctx_type;     // bits 0-7 signal type, bits 8-31 context id
-  uint32_t value_milli;  // value in 1/1000 of the signal's output unit
-  uint32_t tr_lo, tr_hi;
-};
-static_assert(sizeof(EventC20) == 20, "EventC20 must be 20 bytes");
-// 16-byte wire record (EVENT16): EventC20 with the trace hash interned to a 30-bit id that
-// the window's spans carry too (runtime/csrc/wire.h), and a 2-bit epoch tag in the top bits of
-// trace_id: ts = base[tag] + ts_off. The probes (mislo_event16) stamp offsets from the epoch the
-// agent last published and tag them with it, so a record emitted across a window cut still
-// decodes exactly; the window carries its last 4 epoch bases (counts[4..5], [8..13]).
+// 16-byte wire record (EVENT16 = probes/ebpf/mislo_record.h mislo_event16, the payload of the
+// BPF ring's records): timestamp as an offset from one of the window's 4 epoch bases, selected
+// by the 2-bit tag in the top of trace_id (ts = base[tag] + ts_off; counts[4..5], [8..13]);
+// workload identity as a context id into the device context table {pod, pid, conn32,
+// svc<<16|node}; the value in fixed point (1/1000 of the signal's output unit); a 30-bit trace
+// id shared with the window's spans (kernel ids < 2^29, host-assigned above). The probes stamp
+// offsets from the epoch the agent last published, so a record written across a window cut
+// still decodes exactly.
 struct alignas(16) EventC16 {
   uint32_t ts_off, ctx_type, value_milli, trace_id;
 };
@@ -72,29 +50,6 @@ constexpr uint32_t kTraceIdMask = (1u << kEpochTagShift) - 1u;
 constexpr int kCountsLen = 16;  // counts int32[16] (window sizes, epoch bases, context rows)
 static_assert(sizeof(EventC16) == 16, "EventC16 must be 16 bytes");
 constexpr uint32_t kTsZero = 0xFFFFFFFFu;
-// 24-byte record (EVENT24 = probes/ebpf/mislo_record.h mislo_event24): what the probes put
-// on the ring when they also intern the workload context in the kernel; absolute timestamp
-// (no window base needed at the source), context id into the device context table.
-struct alignas(8) EventC24 {
-  int64_t ts_ns;
-  uint64_t trace_h;
-  uint32_t value_milli;
-  uint32_t ctx_type;  // bits 0-7 signal type, bits 8-31 context id
-};
-static_assert(sizeof(EventC24) == 24, "EventC24 must be 24 bytes");
-// 20-byte record (EVENT20T = probes/ebpf/mislo_record.h mislo_event20t, the probes' default
-// ring record): EventC24 with the trace hash interned in the kernel to a 32-bit id that the
-// window's spans carry too. Packed at 20-byte strides (4-byte aligned). Wire code 21.
-struct __attribute__((packed, aligned(4))) EventC20T {
-  int64_t ts_ns;
-  uint32_t value_milli;
-  uint32_t ctx_type;  // bits 0-7 signal type, bits 8-31 context id
-  uint32_t trace_id;
-};
-static_assert(sizeof(EventC20T) == 20, "EventC20T must be 20 bytes");
-constexpr int kWire20T = 21;  // wire code of EventC20T (20 bytes; 20 is the window-based EventC20)
-inline constexpr int wire_bytes(int wire) { return wire == kWire20T ? 20 : wire; }
-
 // REF packed 40-byte record (ebpf/c/llm_slo_event.h:32-42).
 struct __attribute__((packed)) RefEvent {
   uint32_t pid, tid;
@@ -118,9 +73,9 @@ struct alignas(64) Span {
   uint64_t span_h, reserved;
 };
 static_assert(sizeof(Span) == 64, "Span must be 64 bytes");
-// 20-byte span record (collector/records.py SPAN20, runtime/csrc/wire.h Span20): the fields the
-// join reads, with (pod, pid, conn, svc|node) as a context id into the device context table and
-// an interned trace id. A window uses it when counts[7] == 20 (else 64-byte Span records).
+// 20-byte span record (collector/records.py SPAN20, runtime/csrc/records.h Span20): the fields the
+// join reads, with (pod, pid, conn32, svc|node) as a context id into the device context table and
+// a trace id. A window uses it when counts[7] == 20 (else 64-byte Span records).
 struct __attribute__((packed, aligned(4))) SpanC20 {
   int64_t ts_ns;
   uint32_t trace_id, ctx_id, group_id;

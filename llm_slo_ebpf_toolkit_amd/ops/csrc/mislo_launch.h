@@ -27,10 +27,8 @@ void set_tables(const Tables* host_tables);
 int decode_grid(int cap);
 void launch_decode_events(const void* ev, const int* n_dev, int cap, const SignalCols& cols, uint32_t* hist,
                           uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream);
-void launch_decode_compact(const void* ev, const int* n_dev, int cap, const uint32_t* pod_svcnode, int n_pods,
-                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
-                           unsigned long long* misc, hipStream_t stream);
-void launch_decode_wire(const void* ev, int wire, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
+// EVENT16 records; ctx_tab = device context table (n_ctx rows of uint4)
+void launch_decode_wire(const void* ev, const int* n_dev, int cap, const uint32_t* ctx_tab, int n_ctx,
                         const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                         unsigned long long* misc, hipStream_t stream);
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,

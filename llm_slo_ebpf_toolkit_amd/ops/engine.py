@@ -22,9 +22,8 @@ from . import load
 N_DOMAINS_PAD = 16
 
 
-def model_arrays(model: LinearPosteriorModel):
-    import torch
-
+def model_arrays_np(model: LinearPosteriorModel):
+    """The PosteriorModel fields (numpy) of a host LinearPosteriorModel."""
     D = model.weights.shape[1]
     w = np.zeros((16, N_DOMAINS_PAD), dtype=np.float64)
     w[:, :D] = model.weights
@@ -36,9 +35,17 @@ def model_arrays(model: LinearPosteriorModel):
         dom_mask[d] = int(sum(1 << s for s in range(16) if model.evidence_mask[s, d]))
     table_mask = 0xFFFF if model.table_mask is None else int(sum(1 << s for s in range(16) if model.table_mask[s] > 0))
     mode = 0 if model.feature_mode == "binary" else 1
+    return (w, bias, np.asarray(mean, dtype=np.float64), np.asarray(NOMINAL, dtype=np.float64),
+            np.asarray(model.thresholds, dtype=np.float32), dom_mask, table_mask, mode)
+
+
+def model_arrays(model: LinearPosteriorModel):
+    import torch
+
+    w, bias, mean, nominal, thr, dom_mask, table_mask, mode = model_arrays_np(model)
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
-    return (t(w, np.float64), t(bias, np.float64), t(mean, np.float64), t(NOMINAL, np.float64),
-            t(model.thresholds, np.float32), t(dom_mask, np.int64), table_mask, mode)
+    return (t(w, np.float64), t(bias, np.float64), t(mean, np.float64), t(nominal, np.float64),
+            t(thr, np.float32), t(dom_mask, np.int64), table_mask, mode)
 
 
 MODEL_DTYPE = np.dtype([
@@ -50,14 +57,14 @@ assert MODEL_DTYPE.itemsize == 2568  # == sizeof(mislo::PosteriorModel)
 
 def model_bytes(model: LinearPosteriorModel) -> np.ndarray:
     """Byte image of ``mislo::PosteriorModel`` (ops/csrc/mislo_launch.h) for stream-ordered upload."""
-    w, bias, mean, nominal, thr, dom_mask, table_mask, mode = model_arrays(model)
+    w, bias, mean, nominal, thr, dom_mask, table_mask, mode = model_arrays_np(model)
     rec = np.zeros(1, dtype=MODEL_DTYPE)
-    rec["w"][0] = w.numpy()
-    rec["bias"][0] = bias.numpy()
-    rec["mean"][0] = mean.numpy()
-    rec["nominal"][0] = nominal.numpy()
-    rec["thr"][0] = thr.numpy()
-    rec["dom_mask"][0] = dom_mask.numpy().astype(np.uint32)
+    rec["w"][0] = w
+    rec["bias"][0] = bias
+    rec["mean"][0] = mean
+    rec["nominal"][0] = nominal
+    rec["thr"][0] = thr
+    rec["dom_mask"][0] = dom_mask.astype(np.uint32)
     rec["table_mask"][0] = table_mask
     rec["mode"][0] = mode
     return rec.view(np.uint8)
@@ -123,8 +130,8 @@ class GpuEngine:
             self.copy_stream = torch.cuda.Stream(self.device)
         self.sig_cap, self.span_cap, self.group_cap = sig_cap, span_cap, group_cap
         self.n_events = self.n_spans = self.n_groups = 0
-        self.wire = 64
-        self.graph = None
+        self.wire, self.span_bytes = 64, 64
+        self.ctx_dev = None
 
     # ---------------------------------------------------------------------------------
     def set_model(self, model: LinearPosteriorModel) -> None:
@@ -134,35 +141,36 @@ class GpuEngine:
     def set_join_params(self, window_ms=2000.0, threshold=0.7, fanout=3, group_mode=1):
         self.eng.set_join_params(window_ms, threshold, fanout, group_mode)
 
-    def set_pod_table(self, table: np.ndarray) -> None:
-        """pod id -> (svc<<16|node) table used by 32-byte compact records."""
-        with self.torch.cuda.device(self.device):
-            t = self.torch.from_numpy(np.ascontiguousarray(table, dtype=np.int32)).to(self.device)
-            self.eng.set_pod_table(t)
-            self.torch.cuda.synchronize(self.device)
-
-    def set_ctx_table(self, table: np.ndarray) -> None:
-        """context id -> {pod, pid, conn id, svc<<16|node} table used by 20-byte EVENT20 records."""
-        with self.torch.cuda.device(self.device):
-            t = self.torch.from_numpy(np.ascontiguousarray(table, dtype=np.int32).reshape(-1, 4)).to(self.device)
-            self.eng.set_ctx_table(t)
-            self.torch.cuda.synchronize(self.device)
+    def set_ctx_rows(self, ids: np.ndarray, rows: np.ndarray) -> None:
+        """Write context rows (id -> {pod, pid, conn32, svc<<16|node}) into the device context
+        table the EVENT16 / SPAN20 decoders read (full 2^24-row id space, HBM-resident)."""
+        torch = self.torch
+        with torch.cuda.device(self.device):
+            if self.ctx_dev is None:
+                self.ctx_dev = torch.zeros((records.CTX_IDS, 4), dtype=torch.int32, device=self.device)
+                self.eng.set_ctx_table(self.ctx_dev)
+            if len(ids):
+                idx = torch.from_numpy(np.asarray(ids, dtype=np.int64)).to(self.device)
+                val = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.uint32).view(np.int32).reshape(-1, 4))
+                self.ctx_dev[idx] = val.to(self.device)
+            torch.cuda.synchronize(self.device)
 
     def stage(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels: Optional[np.ndarray] = None,
-              t_base: int = 0, bases=None):
-        """Copy records into pinned staging (host memcpy, no GPU work). ``events`` may be
-        64-byte EVENT, 32-byte EVENT32 (needs ``set_pod_table``) or 20/16-byte EVENT20/EVENT16
-        records (need ``set_ctx_table`` and the window base ``t_base``)."""
+              bases=None):
+        """Copy records into pinned staging (host memcpy, no GPU work). ``events``: 64-byte EVENT
+        or EVENT16 records (EVENT16 needs ``set_ctx_rows`` and the window's epoch ``bases``);
+        ``spans``: 64-byte SPAN or SPAN20 records."""
         n, s = events.shape[0], spans.shape[0]
         if n > self.sig_cap or s > self.span_cap or n_groups > self.group_cap:
             raise ValueError("window exceeds engine capacity")
-        if events.dtype not in records.WIRE_DTYPES.values() or spans.dtype != records.SPAN:
-            raise TypeError("events/spans must use the EVENT|EVENT32|EVENT20|EVENT16/SPAN record dtypes")
+        if events.dtype not in records.WIRE_DTYPES.values() or spans.dtype not in (records.SPAN, records.SPAN20):
+            raise TypeError("events/spans must use the EVENT|EVENT16 / SPAN|SPAN20 record dtypes")
         self.wire = records.wire_code(events.dtype)
-        self.ev_host.numpy()[: n * records.wire_bytes(self.wire)] = events.view(np.uint8).reshape(-1)
-        self.sp_host.numpy()[: s * 64] = spans.view(np.uint8).reshape(-1)
+        self.span_bytes = spans.dtype.itemsize
+        self.ev_host.numpy()[: n * self.wire] = events.view(np.uint8).reshape(-1)
+        self.sp_host.numpy()[: s * self.span_bytes] = spans.view(np.uint8).reshape(-1)
         c = self.cnt_host.numpy()
-        c[:] = records.counts_row(n, s, n_groups, 0, bases if bases is not None else (t_base,))
+        c[:] = records.counts_row(n, s, n_groups, 0, bases if bases is not None else (0,), 0, self.span_bytes)
         lab = self.lab_host.numpy()
         lab[:] = -1
         if labels is not None:
@@ -174,9 +182,10 @@ class GpuEngine:
         torch = self.torch
         cs = self.copy_stream
         with torch.cuda.stream(cs):
-            nb = self.n_events * records.wire_bytes(self.wire)
+            nb = self.n_events * self.wire
             self.ev_dev[:nb].copy_(self.ev_host[:nb], non_blocking=True)
-            self.sp_dev[: self.n_spans * 64].copy_(self.sp_host[: self.n_spans * 64], non_blocking=True)
+            sb = self.n_spans * self.span_bytes
+            self.sp_dev[:sb].copy_(self.sp_host[:sb], non_blocking=True)
             self.eng.counts.copy_(self.cnt_host, non_blocking=True)
             self.eng.labels.copy_(self.lab_host, non_blocking=True)
         (stream or torch.cuda.current_stream(self.device)).wait_stream(cs)

@@ -62,36 +62,31 @@ def decode_events(ev: np.ndarray) -> Decoded:
                    ev["pid"].astype(np.uint32), svcnode, ev["trace_h"].astype(np.uint64), conn.astype(np.uint64))
 
 
-def decode_compact(ev: np.ndarray, pod_svcnode: np.ndarray) -> Decoded:
-    type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
-    for s in catalog.SIGNALS:
-        if s.kernel_type < 256:
-            type_slot[s.kernel_type] = s.slot
-    tc = ev["type_conn"].astype(np.uint32)
-    st = (tc & np.uint32(0xFF)).astype(np.int64)
-    slot = type_slot[st]
-    val = (ev["value_milli"].astype(np.float64) * 1e-3).astype(np.float32)
-    warn = np.array([s.warn for s in catalog.SIGNALS], dtype=np.float32)
-    err = np.array([s.error for s in catalog.SIGNALS], dtype=np.float32)
-    ok = slot != NO_SLOT
-    sl = np.where(ok, slot, 0)
-    status = np.where(ok, np.where(val >= err[sl], 2, np.where(val >= warn[sl], 1, 0)), 0).astype(np.uint8)
-    pods = ev["pod_id"].astype(np.int64)
-    table = pod_svcnode.view(np.uint32)
-    svcnode = np.where(pods < table.shape[0], table[np.minimum(pods, table.shape[0] - 1)], 0).astype(np.uint32)
-    return Decoded(ev["ts_ns"].astype(np.int64), val, slot, status, ev["pod_id"].astype(np.uint32),
-                   ev["pid"].astype(np.uint32), svcnode, ev["trace_h"].astype(np.uint64),
-                   (tc >> np.uint32(8)).astype(np.uint64))
+class CtxTable:
+    """Sparse view of the device context table: (ids, rows) pairs, later pairs win (the patch
+    order of the window engine); absent ids read the all-zero row."""
+
+    def __init__(self, ids=None, rows=None):
+        self.map = {}
+        if ids is not None:
+            self.add(ids, rows)
+
+    def add(self, ids, rows) -> "CtxTable":
+        for i, r in zip(np.asarray(ids).tolist(), np.asarray(rows, dtype=np.uint32).reshape(-1, 4).tolist()):
+            self.map[int(i)] = tuple(r)
+        return self
+
+    def rows(self, cid: np.ndarray) -> np.ndarray:
+        out = np.zeros((cid.shape[0], 4), dtype=np.uint32)
+        for j, c in enumerate(cid.tolist()):
+            r = self.map.get(int(c))
+            if r is not None:
+                out[j] = r
+        return out
 
 
-def decode_w24(ev: np.ndarray, ctx_table: np.ndarray) -> Decoded:
-    """k_decode_wire<EventC24>: the probes' context-interned 24-byte records."""
-    return decode_w20(ev, 0, ctx_table)
-
-
-def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray, bases=None) -> Decoded:
-    """k_decode_wire: EVENT20 (trace hash) or EVENT16 (trace id) records with the window
-    base, or EVENT24 (absolute timestamps, trace hash), and the context table."""
+def decode_w16(ev: np.ndarray, table: CtxTable, bases) -> Decoded:
+    """k_decode_wire on EVENT16 records: ts = bases[tag] + ts_off, context rows from the table."""
     type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
     for s in catalog.SIGNALS:
         if s.kernel_type < 256:
@@ -105,30 +100,29 @@ def decode_w20(ev: np.ndarray, t_base: int, ctx_table: np.ndarray, bases=None) -
     ok = slot != NO_SLOT
     sl = np.where(ok, slot, 0)
     status = np.where(ok, np.where(val >= err[sl], 2, np.where(val >= warn[sl], 1, 0)), 0).astype(np.uint8)
-    tab = np.asarray(ctx_table).view(np.uint32).reshape(-1, 4)
-    cid = (ct >> np.uint32(8)).astype(np.int64)
-    inb = cid < tab.shape[0]
-    row = np.where(inb[:, None], tab[np.minimum(cid, tab.shape[0] - 1)], 0).astype(np.uint32)
-    tagged = "ts_off" in ev.dtype.names and "trace_id" in ev.dtype.names  # EVENT16
-    if "ts_ns" in ev.dtype.names:
-        ts = ev["ts_ns"].astype(np.int64)
-    else:
-        off = ev["ts_off"].astype(np.int64)
-        if tagged:  # ts = base[tag] + off; bases[0] is the window base
-            b = np.array(list(bases) if bases is not None else [t_base, 0, 0, 0], dtype=np.int64)
-            tag = (ev["trace_id"].astype(np.uint32) >> np.uint32(30)).astype(np.int64)
-            base = b[tag]
-        else:
-            base = np.int64(t_base)
-        ts = np.where(off == 0xFFFFFFFF, 0, base + off)
-    trace = ev["trace_id"] if "trace_id" in ev.dtype.names else ev["trace_h"]
-    if tagged:
-        trace = trace.astype(np.uint32) & np.uint32((1 << 30) - 1)
+    row = table.rows((ct >> np.uint32(8)).astype(np.int64))
+    off = ev["ts_off"].astype(np.int64)
+    b = np.array((list(bases) + [0, 0, 0, 0])[:4], dtype=np.int64)
+    tag = (ev["trace_id"].astype(np.uint32) >> np.uint32(30)).astype(np.int64)
+    ts = np.where(off == 0xFFFFFFFF, 0, b[tag] + off)
+    trace = ev["trace_id"].astype(np.uint32) & np.uint32((1 << 30) - 1)
     return Decoded(ts, val, slot, status, row[:, 0], row[:, 1], row[:, 3], trace.astype(np.uint64),
                    row[:, 2].astype(np.uint64))
 
 
-decode_w16 = decode_w20
+def decode_span20(sp: np.ndarray, table: CtxTable) -> np.ndarray:
+    """k_decode_spans on SPAN20 records, as 64-byte SPAN records for ``join``."""
+    row = table.rows(sp["ctx_id"].astype(np.int64))
+    out = np.zeros(sp.shape[0], dtype=records.SPAN)
+    out["ts_ns"] = sp["ts_ns"]
+    out["trace_h"] = sp["trace_id"]
+    out["conn_h"] = row[:, 2]
+    out["pod_id"] = row[:, 0]
+    out["pid"] = row[:, 1]
+    out["svc_id"] = (row[:, 3] >> np.uint32(16)).astype(np.uint16)
+    out["node_id"] = (row[:, 3] & np.uint32(0xFFFF)).astype(np.uint16)
+    out["group_id"] = sp["group_id"]
+    return out
 
 
 def histograms(d: Decoded) -> np.ndarray:
@@ -257,4 +251,3 @@ def join(d: Decoded, spans: np.ndarray, n_groups: int, window_ms: float = 2000.0
         "spans_enriched": int((conf > 0).sum()),
     }
     return JoinResult(top3, cnt, attrs, conf, gsum, gcnt, feat, debug)
-decode_w20t = decode_w24  # EVENT20T: absolute timestamps, interned trace ids

@@ -117,6 +117,16 @@ def _profile(labels: Sequence[str]) -> Dict[str, float]:
     return prof
 
 
+def _sli(labels: Sequence[str]):
+    from ..collector.pipeline import BASE_SLI, SLI_PROFILE
+
+    if not labels:
+        return BASE_SLI
+    if len(labels) > 1:
+        return SLI_PROFILE.get("mixed_multi", BASE_SLI)
+    return SLI_PROFILE.get(labels[0], BASE_SLI)
+
+
 def expected_domains(labels: Sequence[str]) -> List[str]:
     out: List[str] = []
     for lab in labels:
@@ -197,6 +207,13 @@ class ReplayGenerator:
         sp["svc_id"] = self.pod_svc[sp_pod]
         sp["group_id"] = self.pod_svc_idx[sp_pod].astype(np.uint32)
         sp["span_h"] = rng.integers(1, np.iinfo(np.int64).max, size=S, dtype=np.int64).astype(np.uint64)
+        # request SLIs from REF's per-fault SLI profiles (pkg/collector/synthetic.go:80-132), jittered
+        grp_sp = self.pod_svc_idx[sp_pod]
+        ttft = np.array([_sli(faults[g])[0] for g in range(G)], dtype=np.float64)[grp_sp]
+        lat = np.array([_sli(faults[g])[1] for g in range(G)], dtype=np.float64)[grp_sp]
+        jit = np.exp(self.rng.normal(0.0, 0.25, size=S))
+        sp["ttft_ms"] = (ttft * jit).astype(np.float32)
+        sp["latency_ms"] = (lat * jit).astype(np.float32)
 
         # --- events ---
         N = cfg.events_per_window

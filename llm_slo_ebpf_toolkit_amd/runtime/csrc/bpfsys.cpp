@@ -1,0 +1,107 @@
+#include "bpfsys.h"
+
+#include <errno.h>
+#include <linux/bpf.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cstring>
+
+namespace mislo {
+
+namespace {
+inline int sys_bpf(int cmd, union bpf_attr* attr) {
+  const long r = syscall(__NR_bpf, cmd, attr, sizeof(*attr));
+  return r < 0 ? -errno : (int)r;
+}
+inline uint64_t ptr(const void* p) { return (uint64_t)(uintptr_t)p; }
+}  // namespace
+
+int bpf_obj_get(const std::string& path) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.pathname = ptr(path.c_str());
+  return sys_bpf(BPF_OBJ_GET, &a);
+}
+
+int bpf_map_info(int fd, BpfMapInfo* out) {
+  struct bpf_map_info info;
+  std::memset(&info, 0, sizeof(info));
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.info.bpf_fd = (uint32_t)fd;
+  a.info.info_len = sizeof(info);
+  a.info.info = ptr(&info);
+  const int r = sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a);
+  if (r < 0) return r;
+  out->type = info.type;
+  out->id = info.id;
+  out->key_size = info.key_size;
+  out->value_size = info.value_size;
+  out->max_entries = info.max_entries;
+  out->map_flags = info.map_flags;
+  out->name.assign(info.name, strnlen(info.name, sizeof(info.name)));
+  return 0;
+}
+
+int bpf_map_lookup(int fd, const void* key, void* value) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)fd;
+  a.key = ptr(key);
+  a.value = ptr(value);
+  return sys_bpf(BPF_MAP_LOOKUP_ELEM, &a);
+}
+
+int bpf_map_update(int fd, const void* key, const void* value, uint64_t flags) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)fd;
+  a.key = ptr(key);
+  a.value = ptr(value);
+  a.flags = flags;
+  return sys_bpf(BPF_MAP_UPDATE_ELEM, &a);
+}
+
+int bpf_map_delete(int fd, const void* key) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)fd;
+  a.key = ptr(key);
+  return sys_bpf(BPF_MAP_DELETE_ELEM, &a);
+}
+
+int bpf_map_next_key(int fd, const void* key, void* next) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)fd;
+  a.key = ptr(key);
+  a.next_key = ptr(next);
+  return sys_bpf(BPF_MAP_GET_NEXT_KEY, &a);
+}
+
+int bpf_map_lookup_batch(int fd, void* in_batch, void* out_batch, void* keys, void* values, uint32_t* count) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.batch.in_batch = ptr(in_batch);
+  a.batch.out_batch = ptr(out_batch);
+  a.batch.keys = ptr(keys);
+  a.batch.values = ptr(values);
+  a.batch.count = *count;
+  a.batch.map_fd = (uint32_t)fd;
+  const int r = sys_bpf(BPF_MAP_LOOKUP_BATCH, &a);
+  *count = a.batch.count;
+  return r;
+}
+
+bool bpf_syscall_available() {
+  // BPF_PROG_LOAD-free probe: an invalid OBJ_GET answers -EPERM without privilege and
+  // -ENOENT / -EINVAL with it
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.pathname = ptr("/sys/fs/bpf/.mislo-probe-nonexistent");
+  const int r = sys_bpf(BPF_OBJ_GET, &a);
+  return r != -EPERM && r != -ENOSYS;
+}
+
+}  // namespace mislo

@@ -1,0 +1,31 @@
+// bpf(2) without libbpf: the handful of commands the agent needs to work with the maps the
+// probes pinned under /sys/fs/bpf (REF pkg/collector/probe_manager.go:25-185 holds cilium/ebpf
+// collections; NEW's loader pins, the agent only opens what is pinned):
+//   BPF_OBJ_GET (open a pinned map), BPF_OBJ_GET_INFO_BY_FD (type / sizes / max_entries),
+//   BPF_MAP_LOOKUP_ELEM / UPDATE_ELEM / DELETE_ELEM (mislo_cfg epochs and floors, mislo_pods),
+//   BPF_MAP_LOOKUP_BATCH (bulk reads of the interning maps), BPF_MAP_GET_NEXT_KEY (fallback).
+// Each call returns 0 / an fd, or -errno.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+namespace mislo {
+
+struct BpfMapInfo {
+  uint32_t type, id, key_size, value_size, max_entries, map_flags;
+  std::string name;
+};
+
+int bpf_obj_get(const std::string& path);
+int bpf_map_info(int fd, BpfMapInfo* out);
+int bpf_map_lookup(int fd, const void* key, void* value);
+int bpf_map_update(int fd, const void* key, const void* value, uint64_t flags);
+int bpf_map_delete(int fd, const void* key);
+int bpf_map_next_key(int fd, const void* key, void* next);
+// one batch step: *count in = capacity, out = entries read; in_batch null = from the start;
+// returns 0, or -ENOENT at the end (entries of the last step are still valid)
+int bpf_map_lookup_batch(int fd, void* in_batch, void* out_batch, void* keys, void* values, uint32_t* count);
+bool bpf_syscall_available();  // probe: is bpf(2) permitted at all (root / CAP_BPF)
+
+}  // namespace mislo

@@ -1,6 +1,10 @@
 #include "ring.h"
 
+#include "pool.h"
+
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -33,6 +37,7 @@ Ring* Ring::format(void* mem, uint64_t capacity, uint32_t rec_size) {
   h->dropped.store(0, std::memory_order_relaxed);
   h->high_water.store(0, std::memory_order_relaxed);
   h->batches.store(0, std::memory_order_relaxed);
+  h->stolen.store(0, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   h->magic = kRingMagic;
   return attach(mem);
@@ -47,14 +52,27 @@ Ring* Ring::attach(void* mem) {
   return r;
 }
 
-uint64_t Ring::push_batch(const void* recs, uint64_t n) {
+uint64_t Ring::push_batch(const void* recs, uint64_t n, int threads) {
   if (n == 0) return 0;
   RingHeader* h = hdr_;
   const uint64_t cap = h->capacity;
-  // producer lock (test-and-test-and-set)
-  for (;;) {
-    if (h->lock.exchange(1, std::memory_order_acquire) == 0) break;
-    while (h->lock.load(std::memory_order_relaxed)) std::this_thread::yield();
+  // producer lock: holds the owner's pid, so a producer process that died holding it (the
+  // ring lives in shared memory) is detected and the lock taken over. Safe because the
+  // release store of `head` is the commit point: a dead owner either published its batch
+  // or left `head` where it was (its partial copy is overwritten).
+  const uint32_t me = (uint32_t)getpid();
+  for (uint32_t spins = 0;;) {
+    uint32_t cur = 0;
+    if (h->lock.compare_exchange_weak(cur, me, std::memory_order_acquire, std::memory_order_relaxed)) break;
+    if (cur != 0 && cur != me && ++spins >= 4096) {
+      spins = 0;
+      if (kill((pid_t)cur, 0) != 0 && errno == ESRCH &&
+          h->lock.compare_exchange_strong(cur, me, std::memory_order_acquire, std::memory_order_relaxed)) {
+        h->stolen.fetch_add(1, std::memory_order_relaxed);
+        break;
+      }
+    }
+    std::this_thread::yield();
   }
   const uint64_t head = h->head.load(std::memory_order_relaxed);
   const uint64_t tail = h->tail.load(std::memory_order_acquire);
@@ -66,8 +84,8 @@ uint64_t Ring::push_batch(const void* recs, uint64_t n) {
   const uint32_t rs = h->rec_size;
   const uint64_t idx = head & (cap - 1);
   const uint64_t first = (idx + n <= cap) ? n : cap - idx;
-  std::memcpy(recs_ + idx * rs, recs, first * rs);
-  if (first < n) std::memcpy(recs_, reinterpret_cast<const uint8_t*>(recs) + first * rs, (n - first) * rs);
+  parallel_memcpy(recs_ + idx * rs, recs, first * rs, threads);
+  if (first < n) parallel_memcpy(recs_, reinterpret_cast<const uint8_t*>(recs) + first * rs, (n - first) * rs, threads);
   h->head.store(head + n, std::memory_order_release);
   h->lock.store(0, std::memory_order_release);
   h->pushed.fetch_add(n, std::memory_order_relaxed);

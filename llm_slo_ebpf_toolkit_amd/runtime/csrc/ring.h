@@ -5,10 +5,11 @@
 // event store.
 //
 // Design (chosen so the consumer's per-window CPU cost is O(1), not O(records)):
-//   * producers serialise on a tiny test-and-set lock (uncontended in the intended
-//     deployment of one ring per producer source / CPU), copy records in, and publish
-//     with a single release store of `head`; a full ring DROPS the batch and counts it
-//     (bpf_ringbuf_reserve semantics) -- producers never block;
+//   * producers serialise on a tiny lock word holding the owner's pid (uncontended in the
+//     intended deployment of one ring per producer source; a lock left by a producer process
+//     that died is taken over), copy records in, and publish with a single release store of
+//     `head`; a full ring DROPS the batch and counts it (bpf_ringbuf_reserve semantics) --
+//     producers never block;
 //   * the single consumer reads `head` (acquire), hands out at most two contiguous
 //     segments (wrap-around) for DMA, and release()s them after the copy completed.
 // head/tail are monotonic 64-bit counters; capacity is a power of two.
@@ -28,11 +29,12 @@ struct alignas(64) RingHeader {
   uint64_t total_bytes;  // header + records
   alignas(64) std::atomic<uint64_t> head;     // producer publish position
   alignas(64) std::atomic<uint64_t> tail;     // consumer release position
-  alignas(64) std::atomic<uint32_t> lock;     // producer lock
+  alignas(64) std::atomic<uint32_t> lock;     // producer lock: owner pid, 0 = free
   std::atomic<uint64_t> pushed;
   std::atomic<uint64_t> dropped;
   std::atomic<uint64_t> high_water;
   std::atomic<uint64_t> batches;
+  std::atomic<uint64_t> stolen;  // locks taken over from dead producers
 };
 
 constexpr uint64_t kRingMagic = 0x4d49534c4f52494eull;  // "MISLORIN"
@@ -53,7 +55,8 @@ class Ring {
   static Ring* attach(void* mem);
 
   bool push(const void* rec) { return push_batch(rec, 1) == 1; }
-  uint64_t push_batch(const void* recs, uint64_t n);  // all-or-nothing; returns accepted count
+  // all-or-nothing; returns accepted count (large batches copy on `threads` threads)
+  uint64_t push_batch(const void* recs, uint64_t n, int threads = 1);
 
   int peek(uint64_t max_records, Segment out[2]) const;  // consumer: 0..2 segments
   void release(uint64_t n);                               // consumer

@@ -1,9 +1,13 @@
-// pybind11 module `_mislo_rt`: the host runtime (ring, shared-memory rings, pinning for
-// direct DMA, paced replay producers) for the Python agent / benchmark.
+// pybind11 module `_mislo_rt`: the agent's host runtime. Shared-memory MPSC rings for
+// user-space producers, the BPF ring buffer view / consumer / kernel-probe model, the agent's
+// id tables and window assembler, bpf(2) map access, paced replay producers.
 #include <hip/hip_runtime_api.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+
+#include <errno.h>
+#include <unistd.h>
 
 #include <cstdlib>
 #include <cstring>
@@ -11,16 +15,62 @@
 #include <stdexcept>
 #include <string>
 
+#include "assemble.h"
+#include "bpfring.h"
+#include "bpfsys.h"
+#include "probesim.h"
 #include "replay.h"
 #include "ring.h"
-#include "wire.h"
+#include "tables.h"
 
 namespace py = pybind11;
-using mislo::Ring;
+using namespace mislo;
+
+namespace {
+
+template <class T>
+std::pair<const T*, size_t> records_of(const py::buffer& b, const char* what) {
+  py::buffer_info info = b.request();
+  const size_t nb = (size_t)info.size * info.itemsize;
+  if (nb % sizeof(T)) throw std::invalid_argument(std::string(what) + ": not a whole number of records");
+  return {static_cast<const T*>(info.ptr), nb / sizeof(T)};
+}
+
+py::array_t<uint32_t> rec16_array(const Rec16* r, size_t n) {
+  py::array_t<uint32_t> a({(py::ssize_t)n, (py::ssize_t)4});
+  if (n) std::memcpy(a.mutable_data(), r, n * sizeof(Rec16));
+  return a;
+}
+
+const int8_t* shift_of(const py::array_t<int8_t, py::array::c_style | py::array::forcecast>& shift) {
+  if (shift.size() != 256) throw std::invalid_argument("shift must have 256 entries");
+  return shift.data();
+}
+
+py::dict layout_dict(const SlotLayout& L) {
+  py::dict d;
+  d["group_cap"] = L.group_cap;
+  d["span_cap"] = L.span_cap;
+  d["sig_cap"] = L.sig_cap;
+  d["row_cap"] = L.row_cap;
+  d["sp_off"] = L.sp_off;
+  d["ev_off"] = L.ev_off;
+  d["bytes"] = L.bytes;
+  return d;
+}
+
+}  // namespace
 
 class HostRing {
  public:
-  HostRing(uint64_t capacity, uint32_t rec_size, const std::string& shm_name) : shm_name_(shm_name) {
+  HostRing(uint64_t capacity, uint32_t rec_size, const std::string& shm_name, bool attach) : shm_name_(shm_name) {
+    if (attach) {
+      shm_ = mislo_ring_open_shm(shm_name.c_str());
+      if (!shm_) throw std::runtime_error("cannot attach shared-memory ring " + shm_name);
+      ring_ = static_cast<Ring*>(mislo_ring_handle_ring(shm_));
+      owner_ = false;
+      return;
+    }
     if (capacity == 0 || (capacity & (capacity - 1))) throw std::invalid_argument("capacity must be a power of two");
     if (!shm_name.empty()) {
       shm_ = mislo_ring_create_shm(shm_name.c_str(), capacity, rec_size);
@@ -38,14 +88,13 @@ class HostRing {
     unpin();
     if (shm_) {
       mislo_ring_close(shm_);
-      mislo_ring_unlink_shm(shm_name_.c_str());
+      if (owner_) mislo_ring_unlink_shm(shm_name_.c_str());
     } else {
       delete ring_;
       free(mem_);
     }
   }
 
-  // Page-lock the record array so hipMemcpyAsync DMAs straight from the ring.
   bool pin() {
     if (pinned_) return true;
     const size_t n = ring_->capacity() * ring_->rec_size();
@@ -57,17 +106,17 @@ class HostRing {
     pinned_ = false;
   }
 
-  uint64_t push(py::buffer b) {
+  uint64_t push(py::buffer b, int threads) {
     py::buffer_info info = b.request();
     const uint64_t nbytes = (uint64_t)info.size * info.itemsize;
     if (nbytes % ring_->rec_size()) throw std::invalid_argument("buffer is not a whole number of records");
     const uint64_t n = nbytes / ring_->rec_size();
     py::gil_scoped_release nogil;
-    return ring_->push_batch(info.ptr, n);
+    return ring_->push_batch(info.ptr, n, threads);
   }
 
   py::list peek(uint64_t max_records) {
-    mislo::Segment seg[2];
+    Segment seg[2];
     int ns = ring_->peek(max_records, seg);
     py::list out;
     for (int i = 0; i < ns; ++i) out.append(py::make_tuple(seg[i].pos, seg[i].index, seg[i].count));
@@ -78,21 +127,14 @@ class HostRing {
   uint64_t size() const { return ring_->size(); }
   uint64_t capacity() const { return ring_->capacity(); }
   uint32_t rec_size() const { return ring_->rec_size(); }
+  uint64_t head() const { return ring_->header()->head.load(std::memory_order_acquire); }
+  uint64_t tail() const { return ring_->header()->tail.load(std::memory_order_acquire); }
   uintptr_t address() const { return reinterpret_cast<uintptr_t>(ring_->records()); }
   bool pinned() const { return pinned_; }
 
   py::array records_view() {
-    return py::array(py::dtype("uint8"), {(py::ssize_t)(ring_->capacity() * ring_->rec_size())},
-                     {(py::ssize_t)1}, ring_->records(), py::cast(this, py::return_value_policy::reference));
-  }
-
-  // Async H2D of `count` records starting at slot `index` to device address `dst` on `stream`.
-  void copy_to_device(uintptr_t dst, uint64_t index, uint64_t count, uintptr_t stream) {
-    if (index + count > ring_->capacity()) throw std::out_of_range("segment past ring end");
-    const size_t rs = ring_->rec_size();
-    hipError_t e = hipMemcpyAsync(reinterpret_cast<void*>(dst), ring_->records() + index * rs, count * rs,
-                                  hipMemcpyHostToDevice, reinterpret_cast<hipStream_t>(stream));
-    if (e != hipSuccess) throw std::runtime_error(std::string("hipMemcpyAsync: ") + hipGetErrorString(e));
+    return py::array(py::dtype("uint8"), {(py::ssize_t)(ring_->capacity() * ring_->rec_size())}, {(py::ssize_t)1},
+                     ring_->records(), py::cast(this, py::return_value_policy::reference));
   }
 
   py::dict stats() const {
@@ -102,6 +144,7 @@ class HostRing {
     d["dropped"] = h->dropped.load();
     d["high_water"] = h->high_water.load();
     d["batches"] = h->batches.load();
+    d["stolen"] = h->stolen.load();
     d["size"] = ring_->size();
     d["capacity"] = ring_->capacity();
     return d;
@@ -116,6 +159,7 @@ class HostRing {
   size_t bytes_ = 0;
   Ring* ring_ = nullptr;
   bool pinned_ = false;
+  bool owner_ = true;
 };
 
 class PyReplayer {
@@ -125,8 +169,7 @@ class PyReplayer {
     const uint64_t nbytes = (uint64_t)info.size * info.itemsize;
     const uint32_t rs = ring.rec_size();
     if (nbytes % rs || nbytes == 0) throw std::invalid_argument("trace is not a whole number of records");
-    rep_ = std::make_unique<mislo::Replayer>(ring.ring(), reinterpret_cast<const uint8_t*>(info.ptr), nbytes / rs, rs,
-                                             lap_ns);
+    rep_ = std::make_unique<Replayer>(ring.ring(), reinterpret_cast<const uint8_t*>(info.ptr), nbytes / rs, rs, lap_ns);
   }
   void start(int threads, double rate_eps, uint64_t batch, uint64_t max_records) {
     rep_->start(threads, rate_eps, batch, max_records);
@@ -143,123 +186,460 @@ class PyReplayer {
   uint64_t dropped() const { return rep_->dropped(); }
 
  private:
-  std::unique_ptr<mislo::Replayer> rep_;
+  std::unique_ptr<Replayer> rep_;
 };
 
-// 64-byte EVENT / SPAN records -> 20- or 16-byte wire records (runtime/csrc/wire.h)
-class PyWireEncoder {
+// ---- BPF ring buffer ----------------------------------------------------------------------
+
+class PyRingbuf {
  public:
-  explicit PyWireEncoder(py::array_t<int8_t, py::array::c_style | py::array::forcecast> shift) {
-    if (shift.size() != 256) throw std::invalid_argument("shift must have 256 entries");
-    enc_ = std::make_unique<mislo::WireEncoder>(shift.data());
+  explicit PyRingbuf(std::unique_ptr<Ringbuf> rb, int fd = -1) : rb_(std::move(rb)), fd_(fd) {}
+  ~PyRingbuf() {
+    rb_.reset();
+    if (fd_ >= 0) ::close(fd_);
   }
-
-  // events: EVENT records (any contiguous buffer, n*64 bytes); out: writable buffer of
-  // >= n*wire bytes (e.g. the pinned staging tensor). Returns t_base.
-  int64_t encode(py::buffer events, py::buffer out, int wire) {
-    py::buffer_info ei = events.request(), oi = out.request(true);
-    const size_t nb = (size_t)ei.size * ei.itemsize;
-    if (nb % sizeof(mislo::EventRec)) throw std::invalid_argument("events: not a whole number of 64-byte records");
-    const size_t n = nb / sizeof(mislo::EventRec);
-    if ((size_t)oi.size * oi.itemsize < n * (size_t)mislo::wire_bytes(wire))
-      throw std::invalid_argument("out buffer too small");
+  static std::unique_ptr<PyRingbuf> create_shm(const std::string& name, uint64_t size) {
+    return std::make_unique<PyRingbuf>(Ringbuf::create_shm(name, size));
+  }
+  static std::unique_ptr<PyRingbuf> attach_shm(const std::string& name) {
+    return std::make_unique<PyRingbuf>(Ringbuf::attach_shm(name));
+  }
+  // a pinned BPF ringbuf map (/sys/fs/bpf/.../mislo_events)
+  static std::unique_ptr<PyRingbuf> open_pinned(const std::string& path) {
+    const int fd = bpf_obj_get(path);
+    if (fd < 0) throw std::runtime_error("BPF_OBJ_GET " + path + ": " + std::strerror(-fd));
+    BpfMapInfo info;
+    const int r = bpf_map_info(fd, &info);
+    if (r < 0) {
+      ::close(fd);
+      throw std::runtime_error("BPF_OBJ_GET_INFO_BY_FD: " + std::string(std::strerror(-r)));
+    }
+    if (info.type != 27 /* BPF_MAP_TYPE_RINGBUF */) {
+      ::close(fd);
+      throw std::runtime_error(path + " is not a BPF ring buffer map");
+    }
+    return std::make_unique<PyRingbuf>(Ringbuf::open_map_fd(fd, info.max_entries), fd);
+  }
+  Ringbuf* rb() { return rb_.get(); }
+  uint64_t cfg_get(int i) const {
+    check_cfg(i);
+    return __atomic_load_n(&rb_->cfg()[i], __ATOMIC_ACQUIRE);
+  }
+  void cfg_set(int i, uint64_t v) {
+    check_cfg(i);
+    __atomic_store_n(&rb_->cfg()[i], v, __ATOMIC_RELEASE);
+  }
+  bool output(py::buffer b) {
+    py::buffer_info info = b.request();
+    return rb_->output(info.ptr, (uint32_t)(info.size * info.itemsize));
+  }
+  uintptr_t reserve(uint32_t size) { return reinterpret_cast<uintptr_t>(rb_->reserve(size)); }
+  void write(uintptr_t at, py::buffer b) {
+    py::buffer_info info = b.request();
+    std::memcpy(reinterpret_cast<void*>(at), info.ptr, (size_t)(info.size * info.itemsize));
+  }
+  void commit(uintptr_t at, bool discard) { rb_->commit(reinterpret_cast<void*>(at), discard); }
+  bool append_framed(py::buffer b, int threads) {
+    py::buffer_info info = b.request();
+    const uint8_t* p = static_cast<const uint8_t*>(info.ptr);
+    const uint64_t n = (uint64_t)(info.size * info.itemsize);
     py::gil_scoped_release nogil;
-    return enc_->encode(static_cast<const mislo::EventRec*>(ei.ptr), n, oi.ptr, wire);
+    return rb_->append_framed(p, n, threads);
   }
-
-  // spans -> 20-byte SPAN20 records (out >= n*20 bytes)
-  void encode_spans20(py::buffer spans, py::buffer out) {
-    py::buffer_info si = spans.request(), oi = out.request(true);
-    const size_t nb = (size_t)si.size * si.itemsize;
-    if (nb % sizeof(mislo::SpanRec64)) throw std::invalid_argument("spans: not a whole number of 64-byte records");
-    const size_t n = nb / sizeof(mislo::SpanRec64);
-    if ((size_t)oi.size * oi.itemsize < n * sizeof(mislo::Span20)) throw std::invalid_argument("out buffer too small");
-    py::gil_scoped_release nogil;
-    enc_->encode_spans20(static_cast<const mislo::SpanRec64*>(si.ptr), n, static_cast<mislo::Span20*>(oi.ptr));
+  py::array data_view() {
+    return py::array(py::dtype("uint8"), {(py::ssize_t)(2 * rb_->size())}, {(py::ssize_t)1}, rb_->data(),
+                     py::cast(this, py::return_value_policy::reference));
   }
-
-  void encode_spans(py::buffer spans, py::buffer out, bool trace_ids) {
-    py::buffer_info si = spans.request(), oi = out.request(true);
-    const size_t nb = (size_t)si.size * si.itemsize;
-    if (nb % sizeof(mislo::SpanRec64)) throw std::invalid_argument("spans: not a whole number of 64-byte records");
-    if ((size_t)oi.size * oi.itemsize < nb) throw std::invalid_argument("out buffer too small");
-    py::gil_scoped_release nogil;
-    enc_->encode_spans(static_cast<const mislo::SpanRec64*>(si.ptr), nb / sizeof(mislo::SpanRec64),
-                       static_cast<mislo::SpanRec64*>(oi.ptr), trace_ids);
+  void set_consumer_pos(uint64_t p) { rb_->set_consumer_pos(p); }
+  py::dict stats() const {
+    py::dict d;
+    d["size"] = rb_->size();
+    d["consumer_pos"] = rb_->consumer_pos();
+    d["producer_pos"] = rb_->producer_pos();
+    if (rb_->meta()) {
+      d["dropped"] = rb_->meta()->dropped.load();
+      d["reserved"] = rb_->meta()->reserved.load();
+    }
+    return d;
   }
-
-  // one window on the worker pool (wire.h encode_window): events -> ev_out, spans -> sp_out
-  int64_t encode_window(py::buffer events, py::buffer ev_out, int wire, py::buffer spans, py::buffer sp_out,
-                        int threads, size_t min_chunk) {
-    py::buffer_info ei = events.request(), eo = ev_out.request(true), si = spans.request(), so = sp_out.request(true);
-    const size_t nb = (size_t)ei.size * ei.itemsize, sb = (size_t)si.size * si.itemsize;
-    if (nb % sizeof(mislo::EventRec)) throw std::invalid_argument("events: not a whole number of 64-byte records");
-    if (sb % sizeof(mislo::SpanRec64)) throw std::invalid_argument("spans: not a whole number of 64-byte records");
-    const size_t n = nb / sizeof(mislo::EventRec), ns = sb / sizeof(mislo::SpanRec64);
-    if ((size_t)eo.size * eo.itemsize < n * (size_t)wire) throw std::invalid_argument("ev_out buffer too small");
-    if ((size_t)so.size * so.itemsize < sb) throw std::invalid_argument("sp_out buffer too small");
-    py::gil_scoped_release nogil;
-    return enc_->encode_window(static_cast<const mislo::EventRec*>(ei.ptr), n, eo.ptr, wire,
-                               static_cast<const mislo::SpanRec64*>(si.ptr), ns,
-                               static_cast<mislo::SpanRec64*>(so.ptr), threads, min_chunk);
-  }
-
-  void end_window() { enc_->end_window(); }
-
-  // context table (int32 [n, 4]: pod, pid, conn id, svc<<16|node), row i = context id i
-  py::array_t<int32_t> ctx_table() const {
-    const auto& rows = enc_->ctx_rows();
-    py::array_t<int32_t> a({(py::ssize_t)rows.size(), (py::ssize_t)4});
-    std::memcpy(a.mutable_data(), rows.data(), rows.size() * sizeof(rows[0]));
-    return a;
-  }
-  size_t n_ctx() const { return enc_->ctx_rows().size(); }
-  size_t n_conns() const { return enc_->n_conns(); }
-  size_t n_traces() const { return enc_->n_traces(); }
 
  private:
-  std::unique_ptr<mislo::WireEncoder> enc_;
+  void check_cfg(int i) const {
+    if (!rb_->cfg()) throw std::logic_error("mislo_cfg of a real ring lives in its own BPF map (BpfMap)");
+    if (i < 0 || i >= kCfgSlots) throw std::out_of_range("cfg index");
+  }
+  std::unique_ptr<Ringbuf> rb_;
+  int fd_;
+};
+
+class PyConsumer {
+ public:
+  PyConsumer(PyRingbuf& rb, int threads) : c_(rb.rb(), threads) {}
+  py::tuple consume(py::buffer out, uint64_t cap, uint64_t limit) {
+    py::buffer_info oi = out.request(true);
+    if ((uint64_t)(oi.size * oi.itemsize) < cap * sizeof(Rec16)) throw std::invalid_argument("out buffer too small");
+    std::vector<Rec16> defs;
+    ConsumeStats st;
+    {
+      py::gil_scoped_release nogil;
+      st = c_.consume(static_cast<Rec16*>(oi.ptr), cap, defs, limit);
+    }
+    py::dict d;
+    d["events"] = st.events;
+    d["defs"] = st.defs;
+    d["discarded"] = st.discarded;
+    d["foreign"] = st.foreign;
+    d["begin_pos"] = st.begin_pos;
+    d["end_pos"] = st.end_pos;
+    d["busy_stop"] = st.busy_stop;
+    d["serial"] = st.serial;
+    return py::make_tuple(d, rec16_array(defs.data(), defs.size()));
+  }
+  RingbufConsumer* get() { return &c_; }
+  int threads() const { return c_.threads(); }
+
+ private:
+  RingbufConsumer c_;
+};
+
+class PyProbeSim {
+ public:
+  PyProbeSim(PyRingbuf& rb, py::array_t<int8_t, py::array::c_style | py::array::forcecast> shift, size_t trace_lru)
+      : rb_(rb), sim_(rb.rb()->cfg(), shift_of(shift), trace_lru) {}
+  uint64_t submit(py::buffer events) {
+    auto [ev, n] = records_of<EventRec>(events, "events");
+    py::gil_scoped_release nogil;
+    return sim_.submit(*rb_.rb(), ev, n);
+  }
+  py::array_t<uint32_t> encode(py::buffer events) {
+    auto [ev, n] = records_of<EventRec>(events, "events");
+    std::vector<Rec16> out;
+    {
+      py::gil_scoped_release nogil;
+      sim_.encode(ev, n, out);
+    }
+    return rec16_array(out.data(), out.size());
+  }
+  void reset_maps() { sim_.reset_maps(); }
+  size_t n_ctx() const { return sim_.n_ctx(); }
+  size_t n_traces() const { return sim_.n_traces(); }
+  uint64_t dropped() const { return sim_.dropped(); }
+
+ private:
+  PyRingbuf& rb_;
+  ProbeSim sim_;
+};
+
+py::array_t<uint8_t> frame_records_py(py::buffer recs) {
+  auto [r, n] = records_of<Rec16>(recs, "records");
+  py::array_t<uint8_t> out((py::ssize_t)(n * kRecStride));
+  frame_records(r, n, out.mutable_data());
+  return out;
+}
+
+class PyTables {
+ public:
+  explicit PyTables(py::array_t<int8_t, py::array::c_style | py::array::forcecast> shift) : t_(shift_of(shift)) {}
+  void set_pod(uint32_t pod, uint32_t sn) { t_.set_pod(pod, sn); }
+  void set_pods(py::array_t<uint32_t, py::array::c_style | py::array::forcecast> pods,
+                py::array_t<uint32_t, py::array::c_style | py::array::forcecast> sn) {
+    if (pods.size() != sn.size()) throw std::invalid_argument("pods / svcnode size mismatch");
+    for (py::ssize_t i = 0; i < pods.size(); ++i) t_.set_pod(pods.data()[i], sn.data()[i]);
+  }
+  uint32_t pod_svcnode(uint32_t pod) const { return t_.pod_svcnode(pod); }
+  void apply_defs(py::buffer defs) {
+    auto [d, n] = records_of<Rec16>(defs, "defs");
+    t_.apply_defs(d, n);
+  }
+  py::array_t<uint32_t> encode_events(py::buffer events, std::vector<int64_t> bases) {
+    auto [ev, n] = records_of<EventRec>(events, "events");
+    if (bases.size() > 4) throw std::invalid_argument("at most 4 epoch bases");
+    bases.resize(4, 0);
+    std::vector<Rec16> out(n);
+    t_.encode_events(ev, n, out.data(), bases.data());
+    return rec16_array(out.data(), n);
+  }
+  py::array_t<uint8_t> encode_spans(py::buffer spans) {
+    auto [sp, n] = records_of<SpanRec64>(spans, "spans");
+    py::array_t<uint8_t> out((py::ssize_t)(n * sizeof(Span20)));
+    t_.encode_spans(sp, n, reinterpret_cast<Span20*>(out.mutable_data()));
+    return out;
+  }
+  uint32_t trace_id(uint64_t h) { return t_.trace_id(h); }
+  void set_sli_threshold(float ms) { t_.set_sli_threshold(ms); }
+  py::array_t<uint32_t> take_group_sli(size_t groups) {
+    py::array_t<uint32_t> a({(py::ssize_t)groups, (py::ssize_t)2});
+    std::vector<uint32_t> n(groups), b(groups);
+    t_.take_group_sli(n.data(), b.data(), groups);
+    auto m = a.mutable_unchecked<2>();
+    for (size_t g = 0; g < groups; ++g) {
+      m(g, 0) = n[g];
+      m(g, 1) = b[g];
+    }
+    return a;
+  }
+  py::tuple take_rows(size_t cap) {
+    std::vector<uint32_t> ids(cap);
+    std::vector<AgentTables::Row> rows(cap);
+    const size_t k = t_.take_rows(ids.data(), rows.data(), cap);
+    py::array_t<uint32_t> a((py::ssize_t)k), b({(py::ssize_t)k, (py::ssize_t)4});
+    if (k) {
+      std::memcpy(a.mutable_data(), ids.data(), 4 * k);
+      std::memcpy(b.mutable_data(), rows.data(), 16 * k);
+    }
+    return py::make_tuple(a, b);
+  }
+  void end_window() { t_.end_window(); }
+  AgentTables* get() { return &t_; }
+  py::dict stats() const {
+    py::dict d;
+    d["kernel_ctx"] = t_.n_kernel_ctx();
+    d["host_ctx"] = t_.n_host_ctx();
+    d["traces"] = t_.n_traces();
+    d["pending_rows"] = t_.pending_rows();
+    d["host_ctx_wraps"] = t_.host_ctx_wraps();
+    d["bad_defs"] = t_.bad_defs();
+    return d;
+  }
+
+ private:
+  AgentTables t_;
+};
+
+class PyAssembler {
+ public:
+  PyAssembler(uint32_t group_cap, uint32_t span_cap, uint32_t sig_cap, uint32_t row_cap, PyTables& tables,
+              PyConsumer* kernel, HostRing* user, HostRing* spans)
+      : a_(slot_layout(group_cap, span_cap, sig_cap, row_cap), tables.get(), kernel ? kernel->get() : nullptr,
+           user ? user->ring() : nullptr, spans ? spans->ring() : nullptr) {}
+  py::dict assemble(uintptr_t slot, std::vector<int64_t> bases, int n_groups, py::object labels, uint64_t kernel_limit,
+                    uint64_t user_limit, uint64_t span_limit) {
+    bases.resize(4, 0);
+    std::vector<int32_t> lab;
+    if (!labels.is_none()) {
+      auto arr = labels.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
+      lab.assign(arr.data(), arr.data() + arr.size());
+      if ((int)lab.size() < n_groups) lab.resize(n_groups, -1);
+    }
+    AssembleResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = a_.assemble(reinterpret_cast<uint8_t*>(slot), bases.data(), n_groups, lab.empty() ? nullptr : lab.data(),
+                      kernel_limit, user_limit, span_limit);
+    }
+    py::dict d;
+    d["n_events"] = r.n_events;
+    d["n_kernel"] = r.n_kernel;
+    d["n_user"] = r.n_user;
+    d["n_spans"] = r.n_spans;
+    d["n_rows"] = r.n_rows;
+    d["n_defs"] = r.n_defs;
+    d["rows_deferred"] = r.rows_deferred;
+    d["discarded"] = r.discarded;
+    d["foreign"] = r.foreign;
+    d["busy_stop"] = r.busy_stop;
+    d["ring_begin"] = r.ring_begin;
+    d["ring_end"] = r.ring_end;
+    d["user_dropped"] = r.user_dropped;
+    d["dma_bytes"] = r.dma_bytes;
+    d["host_us"] = r.host_us;
+    return d;
+  }
+  py::dict layout() const { return layout_dict(a_.layout()); }
+
+ private:
+  WindowAssembler a_;
+};
+
+class PyBpfMap {
+ public:
+  explicit PyBpfMap(const std::string& path) {
+    fd_ = bpf_obj_get(path);
+    if (fd_ < 0) throw std::runtime_error("BPF_OBJ_GET " + path + ": " + std::strerror(-fd_));
+    const int r = bpf_map_info(fd_, &info_);
+    if (r < 0) throw std::runtime_error("BPF_OBJ_GET_INFO_BY_FD: " + std::string(std::strerror(-r)));
+  }
+  ~PyBpfMap() {
+    if (fd_ >= 0) ::close(fd_);
+  }
+  py::object lookup(py::bytes key) {
+    std::string k = key;
+    if (k.size() != info_.key_size) throw std::invalid_argument("key size");
+    std::string v(info_.value_size, '\0');
+    const int r = bpf_map_lookup(fd_, k.data(), v.data());
+    if (r == -ENOENT) return py::none();
+    if (r < 0) throw std::runtime_error(std::string("lookup: ") + std::strerror(-r));
+    return py::bytes(v);
+  }
+  void update(py::bytes key, py::bytes value, uint64_t flags) {
+    std::string k = key, v = value;
+    if (k.size() != info_.key_size || v.size() != info_.value_size) throw std::invalid_argument("key/value size");
+    const int r = bpf_map_update(fd_, k.data(), v.data(), flags);
+    if (r < 0) throw std::runtime_error(std::string("update: ") + std::strerror(-r));
+  }
+  bool remove(py::bytes key) {
+    std::string k = key;
+    const int r = bpf_map_delete(fd_, k.data());
+    if (r == -ENOENT) return false;
+    if (r < 0) throw std::runtime_error(std::string("delete: ") + std::strerror(-r));
+    return true;
+  }
+  // all entries, by BPF_MAP_LOOKUP_BATCH (next_key walk where batching is unsupported)
+  py::tuple items() {
+    const uint32_t ks = info_.key_size, vs = info_.value_size;
+    std::string keys, vals;
+    uint32_t chunk = 4096;
+    std::string kb(ks * (size_t)chunk, '\0'), vb(vs * (size_t)chunk, '\0');
+    std::string in(ks, '\0'), out(ks, '\0');
+    bool first = true, batch_ok = true;
+    for (;;) {
+      uint32_t cnt = chunk;
+      const int r = bpf_map_lookup_batch(fd_, first ? nullptr : in.data(), out.data(), kb.data(), vb.data(), &cnt);
+      if (r < 0 && r != -ENOENT) {
+        if (first && (r == -EINVAL || r == -ENOTSUPP_ || r == -EOPNOTSUPP)) batch_ok = false;
+        else throw std::runtime_error(std::string("lookup_batch: ") + std::strerror(-r));
+        break;
+      }
+      keys.append(kb.data(), (size_t)cnt * ks);
+      vals.append(vb.data(), (size_t)cnt * vs);
+      if (r == -ENOENT) break;
+      in = out;
+      first = false;
+    }
+    if (!batch_ok) {
+      std::string cur(ks, '\0'), nxt(ks, '\0'), v(vs, '\0');
+      const void* prev = nullptr;
+      while (bpf_map_next_key(fd_, prev, nxt.data()) == 0) {
+        if (bpf_map_lookup(fd_, nxt.data(), v.data()) == 0) {
+          keys.append(nxt);
+          vals.append(v);
+        }
+        cur = nxt;
+        prev = cur.data();
+      }
+    }
+    return py::make_tuple(py::bytes(keys), py::bytes(vals));
+  }
+  py::dict info() const {
+    py::dict d;
+    d["type"] = info_.type;
+    d["id"] = info_.id;
+    d["key_size"] = info_.key_size;
+    d["value_size"] = info_.value_size;
+    d["max_entries"] = info_.max_entries;
+    d["name"] = info_.name;
+    return d;
+  }
+
+ private:
+  static constexpr int ENOTSUPP_ = 524;  // kernel-internal ENOTSUPP
+  int fd_ = -1;
+  BpfMapInfo info_{};
 };
 
 PYBIND11_MODULE(_mislo_rt, m) {
-  m.doc() = "MI355X LLM-SLO native host runtime (rings, replay producers)";
+  m.doc() = "MI355X LLM-SLO agent host runtime (rings, BPF ringbuf consumer, id tables, window assembly)";
   py::class_<HostRing>(m, "HostRing")
-      .def(py::init<uint64_t, uint32_t, const std::string&>(), py::arg("capacity"), py::arg("rec_size") = 64,
-           py::arg("shm_name") = "")
+      .def(py::init<uint64_t, uint32_t, const std::string&, bool>(), py::arg("capacity") = 1, py::arg("rec_size") = 64,
+           py::arg("shm_name") = "", py::arg("attach") = false)
       .def("pin", &HostRing::pin)
       .def("unpin", &HostRing::unpin)
-      .def("push", &HostRing::push)
+      .def("push", &HostRing::push, py::arg("records"), py::arg("threads") = 1)
       .def("peek", &HostRing::peek)
       .def("release", &HostRing::release)
       .def("records_view", &HostRing::records_view)
-      .def("copy_to_device", &HostRing::copy_to_device)
       .def("stats", &HostRing::stats)
       .def_property_readonly("size", &HostRing::size)
       .def_property_readonly("capacity", &HostRing::capacity)
       .def_property_readonly("rec_size", &HostRing::rec_size)
+      .def_property_readonly("head", &HostRing::head)
+      .def_property_readonly("tail", &HostRing::tail)
       .def_property_readonly("address", &HostRing::address)
       .def_property_readonly("pinned", &HostRing::pinned);
   py::class_<PyReplayer>(m, "Replayer")
       .def(py::init<HostRing&, py::buffer, int64_t>(), py::arg("ring"), py::arg("trace"), py::arg("lap_ns"),
            py::keep_alive<1, 2>())
-      .def("start", &PyReplayer::start, py::arg("threads") = 1, py::arg("rate_eps") = 0.0,
-           py::arg("batch") = 256, py::arg("max_records") = 0)
+      .def("start", &PyReplayer::start, py::arg("threads") = 1, py::arg("rate_eps") = 0.0, py::arg("batch") = 256,
+           py::arg("max_records") = 0)
       .def("stop", &PyReplayer::stop)
       .def("wait", &PyReplayer::wait)
       .def_property_readonly("pushed", &PyReplayer::pushed)
       .def_property_readonly("dropped", &PyReplayer::dropped);
-  py::class_<PyWireEncoder>(m, "WireEncoder")
+  py::class_<PyRingbuf>(m, "Ringbuf")
+      .def_static("create_shm", &PyRingbuf::create_shm, py::arg("name"), py::arg("size"))
+      .def_static("attach_shm", &PyRingbuf::attach_shm, py::arg("name"))
+      .def_static("open_pinned", &PyRingbuf::open_pinned, py::arg("path"))
+      .def("cfg_get", &PyRingbuf::cfg_get)
+      .def("cfg_set", &PyRingbuf::cfg_set)
+      .def("output", &PyRingbuf::output)
+      .def("reserve", &PyRingbuf::reserve)
+      .def("write", &PyRingbuf::write)
+      .def("commit", &PyRingbuf::commit, py::arg("at"), py::arg("discard") = false)
+      .def("append_framed", &PyRingbuf::append_framed, py::arg("image"), py::arg("threads") = 1)
+      .def("data_view", &PyRingbuf::data_view)
+      .def("set_consumer_pos", &PyRingbuf::set_consumer_pos)
+      .def("stats", &PyRingbuf::stats)
+      .def_property_readonly("size", [](PyRingbuf& r) { return r.rb()->size(); })
+      .def_property_readonly("page", [](PyRingbuf& r) { return r.rb()->page(); })
+      .def_property_readonly("emulated", [](PyRingbuf& r) { return r.rb()->emulated(); })
+      .def_property_readonly("consumer_pos", [](PyRingbuf& r) { return r.rb()->consumer_pos(); })
+      .def_property_readonly("producer_pos", [](PyRingbuf& r) { return r.rb()->producer_pos(); })
+      .def_property_readonly("available", [](PyRingbuf& r) { return r.rb()->available(); });
+  py::class_<PyConsumer>(m, "RingbufConsumer")
+      .def(py::init<PyRingbuf&, int>(), py::arg("ring"), py::arg("threads") = 1, py::keep_alive<1, 2>())
+      .def("consume", &PyConsumer::consume, py::arg("out"), py::arg("cap"), py::arg("limit") = ~0ull)
+      .def_property_readonly("threads", &PyConsumer::threads);
+  py::class_<PyProbeSim>(m, "ProbeSim")
+      .def(py::init<PyRingbuf&, py::array_t<int8_t, py::array::c_style | py::array::forcecast>, size_t>(),
+           py::arg("ring"), py::arg("shift"), py::arg("trace_lru") = 1u << 20, py::keep_alive<1, 2>())
+      .def("submit", &PyProbeSim::submit)
+      .def("encode", &PyProbeSim::encode)
+      .def("reset_maps", &PyProbeSim::reset_maps)
+      .def_property_readonly("n_ctx", &PyProbeSim::n_ctx)
+      .def_property_readonly("n_traces", &PyProbeSim::n_traces)
+      .def_property_readonly("dropped", &PyProbeSim::dropped);
+  m.def("frame_records", &frame_records_py, py::arg("records"));
+  py::class_<PyTables>(m, "AgentTables")
       .def(py::init<py::array_t<int8_t, py::array::c_style | py::array::forcecast>>(), py::arg("shift"))
-      .def("encode", &PyWireEncoder::encode, py::arg("events"), py::arg("out"), py::arg("wire") = 20)
-      .def("encode_spans20", &PyWireEncoder::encode_spans20, py::arg("spans"), py::arg("out"))
-      .def("encode_spans", &PyWireEncoder::encode_spans, py::arg("spans"), py::arg("out"),
-           py::arg("trace_ids") = false)
-      .def("encode_window", &PyWireEncoder::encode_window, py::arg("events"), py::arg("ev_out"), py::arg("wire"),
-           py::arg("spans"), py::arg("sp_out"), py::arg("threads") = 8,
-           py::arg("min_chunk") = 16384)
-      .def("end_window", &PyWireEncoder::end_window)
-      .def("ctx_table", &PyWireEncoder::ctx_table)
-      .def_property_readonly("n_ctx", &PyWireEncoder::n_ctx)
-      .def_property_readonly("n_conns", &PyWireEncoder::n_conns)
-      .def_property_readonly("n_traces", &PyWireEncoder::n_traces);
+      .def("set_pod", &PyTables::set_pod)
+      .def("set_pods", &PyTables::set_pods)
+      .def("pod_svcnode", &PyTables::pod_svcnode)
+      .def("apply_defs", &PyTables::apply_defs)
+      .def("encode_events", &PyTables::encode_events, py::arg("events"), py::arg("bases"))
+      .def("encode_spans", &PyTables::encode_spans)
+      .def("trace_id", &PyTables::trace_id)
+      .def("set_sli_threshold", &PyTables::set_sli_threshold)
+      .def("take_group_sli", &PyTables::take_group_sli)
+      .def("take_rows", &PyTables::take_rows, py::arg("cap") = 1u << 20)
+      .def("end_window", &PyTables::end_window)
+      .def("stats", &PyTables::stats);
+  py::class_<PyAssembler>(m, "WindowAssembler")
+      .def(py::init<uint32_t, uint32_t, uint32_t, uint32_t, PyTables&, PyConsumer*, HostRing*, HostRing*>(),
+           py::arg("group_cap"), py::arg("span_cap"), py::arg("sig_cap"), py::arg("row_cap"), py::arg("tables"),
+           py::arg("kernel") = nullptr, py::arg("user") = nullptr, py::arg("spans") = nullptr, py::keep_alive<1, 6>(),
+           py::keep_alive<1, 7>(), py::keep_alive<1, 8>(), py::keep_alive<1, 9>())
+      .def("assemble", &PyAssembler::assemble, py::arg("slot"), py::arg("bases"), py::arg("n_groups"),
+           py::arg("labels") = py::none(), py::arg("kernel_limit") = ~0ull, py::arg("user_limit") = ~0ull,
+           py::arg("span_limit") = ~0ull)
+      .def_property_readonly("layout", &PyAssembler::layout);
+  m.def("slot_layout", [](uint32_t g, uint32_t s, uint32_t n, uint32_t r) { return layout_dict(slot_layout(g, s, n, r)); },
+        py::arg("group_cap"), py::arg("span_cap"), py::arg("sig_cap"), py::arg("row_cap"));
+  py::class_<PyBpfMap>(m, "BpfMap")
+      .def(py::init<const std::string&>(), py::arg("path"))
+      .def("lookup", &PyBpfMap::lookup)
+      .def("update", &PyBpfMap::update, py::arg("key"), py::arg("value"), py::arg("flags") = 0)
+      .def("delete", &PyBpfMap::remove)
+      .def("items", &PyBpfMap::items)
+      .def("info", &PyBpfMap::info);
+  m.def("bpf_available", &bpf_syscall_available);
+  m.attr("REC_STRIDE") = kRecStride;
+  m.attr("DEF_TRACE") = kDefTrace;
+  m.attr("DEF_CTX") = kDefCtx;
+  m.attr("KERNEL_CTX_LIMIT") = kKernelCtxLimit;
+  m.attr("KERNEL_TRACE_LIMIT") = kKernelTraceLimit;
+  m.attr("CFG_EPOCH") = kCfgEpoch;
+  m.attr("CFG_TRACE_NEXT") = kCfgTraceNext;
+  m.attr("CFG_CTX_NEXT") = kCfgCtxNext;
+  m.attr("CFG_CLOCK") = kCfgClock;
+  m.attr("CFG_NODE") = kCfgNode;
 }

@@ -5,6 +5,8 @@ import pytest
 
 from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes, SufficientStats
 from llm_slo_ebpf_toolkit_amd.ops.engine import signal_rows as rows
+
+rows_ = rows
 from llm_slo_ebpf_toolkit_amd.pipeline import oracle
 from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
 
@@ -126,171 +128,58 @@ def test_ref_record_decode(engine):
     assert int(engine.eng.misc[0].item()) == 1
 
 
-def test_compact_wire_matches_oracle(engine):
-    from llm_slo_ebpf_toolkit_amd.collector import records
-
-    win = small_window(seed=11)
-    engine.set_join_params(2000.0, 0.7, 3, 1)
-    engine.set_model(NaiveBayes.ref())
-    interner = records.ConnInterner()
-    table = records.pod_table(win.events, win.spans)
-    ev32 = records.to_compact(win.events, interner)
-    sp = records.compact_spans(win.spans, interner)
-    engine.set_pod_table(table)
-    out = engine.process(ev32, sp, win.n_groups, win.group_labels)
-    e = engine.eng
-    d = oracle.decode_compact(ev32, table)
-    N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
-    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
-    np.testing.assert_array_equal(rows(e, N)["svcnode"], d.svcnode)
-    ref = oracle.join(d, sp, win.n_groups)
-    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
-    np.testing.assert_array_equal(top3, ref.top3)
-    np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
-    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
-        assert out.debug[k] == ref.debug[k], k
-    np.testing.assert_array_equal(e.gsum[: win.n_groups].cpu().numpy(), ref.gsum)
-    np.testing.assert_array_equal(e.gcnt[: win.n_groups].cpu().numpy(), ref.gcnt)
-    np.testing.assert_array_equal(out.feat, ref.feat)
-
-
-def test_wire20_matches_oracle(engine):
-    from llm_slo_ebpf_toolkit_amd.collector import records
-
-    win = small_window(seed=17)
-    engine.set_join_params(2000.0, 0.7, 3, 1)
-    engine.set_model(NaiveBayes.ref())
-    conns, ctxs = records.ConnInterner(), records.CtxInterner()
-    ev = win.events.copy()
-    ev["ts_ns"][3] = 0
-    ev20, t_base = records.to_wire20(ev, conns, ctxs)
-    sp = records.compact_spans(win.spans, conns)
-    engine.set_ctx_table(ctxs.table())
-    engine.stage(ev20, sp, win.n_groups, win.group_labels, t_base=t_base)
-    engine.upload()
-    engine.run(True, False)
-    out = engine.outputs()
-    e = engine.eng
-    d = oracle.decode_w20(ev20, t_base, ctxs.table())
-    N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(rows(e, N)["ts"], d.ts)
-    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
-    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
-    np.testing.assert_array_equal(rows(e, N)["pid"], d.pid)
-    np.testing.assert_array_equal(rows(e, N)["svcnode"], d.svcnode)
-    ref = oracle.join(d, sp, win.n_groups)
-    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
-    np.testing.assert_array_equal(top3, ref.top3)
-    np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
-    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
-        assert out.debug[k] == ref.debug[k], k
-    np.testing.assert_array_equal(e.gsum[: win.n_groups].cpu().numpy(), ref.gsum)
-    np.testing.assert_array_equal(out.feat, ref.feat)
-    assert int(e.misc[1].item()) == 1  # the zero timestamp
-
-
-def test_wire20t_matches_oracle(engine):
-    """EVENT20T (the probes' default 20-byte ring record, interned trace ids, 4-byte aligned at
-    20-byte strides) -> GPU decode + join == numpy oracle, zero timestamp included."""
-    from llm_slo_ebpf_toolkit_amd.collector import records
-
-    win = small_window(seed=21)
-    engine.set_join_params(2000.0, 0.7, 3, 1)
-    engine.set_model(NaiveBayes.ref())
-    conns, ctxs, traces = records.ConnInterner(), records.CtxInterner(), records.TraceInterner()
-    ev = win.events.copy()
-    ev["ts_ns"][5] = 0
-    e20 = records.to_wire20t(ev, conns, ctxs, traces)
-    sp = records.wire_spans(win.spans, conns, traces)
-    engine.set_ctx_table(ctxs.table())
-    engine.stage(e20, sp, win.n_groups, win.group_labels)
-    assert engine.wire == records.WIRE_20T
-    engine.upload()
-    engine.run(True, False)
-    out = engine.outputs()
-    e = engine.eng
-    d = oracle.decode_w20t(e20, ctxs.table())
-    N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(rows(e, N)["ts"], d.ts)
-    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
-    np.testing.assert_array_equal(rows(e, N)["val"], d.val)
-    np.testing.assert_array_equal(rows(e, N)["pid"], d.pid)
-    np.testing.assert_array_equal(rows(e, N)["svcnode"], d.svcnode)
-    ref = oracle.join(d, sp, win.n_groups)
-    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
-    np.testing.assert_array_equal(top3, ref.top3)
-    np.testing.assert_array_equal(e.attrs[:S].cpu().numpy(), ref.attrs)
-    for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
-        assert out.debug[k] == ref.debug[k], k
-    np.testing.assert_array_equal(out.feat, ref.feat)
-    assert int(e.misc[1].item()) == 1  # the zero timestamp
-
-
 def test_wire16_epoch_tags_match_oracle(engine):
-    """EVENT16 with 2-bit epoch tags (the probes' -DMISLO_RING_EVENT16 record): the decode kernel
-    picks each record's base from counts[4..5] / [8..13]; decode + join == numpy oracle."""
+    """EVENT16 as the probes write it (probe model: epoch published at each of 4 cuts, records
+    stamped with the epoch in force) + host-encoded spans: decode picks each record's base by its
+    tag; decode + join == numpy oracle, and == the join of the 64-byte originals."""
     from llm_slo_ebpf_toolkit_amd.collector import records
 
     win = small_window(seed=25)
     engine.set_join_params(2000.0, 0.7, 3, 1)
     engine.set_model(NaiveBayes.ref())
-    conns, ctxs, traces = records.ConnInterner(), records.CtxInterner(), records.TraceInterner()
-    ev = win.events.copy()
+    ev = win.events[np.argsort(win.events["ts_ns"], kind="stable")].copy()
     ev["ts_ns"][2] = 0
-    e16, t_base = records.to_wire16(ev, conns, ctxs, traces)
-    e16, bases = records.retag_epochs(e16, t_base, 200_000_000)
+    cfg = np.zeros(128, dtype=np.uint64)
+    clock, model = records.EpochClock(), records.ProbeModel(cfg)
+    first = int(ev["ts_ns"][ev["ts_ns"] > 0].min())
+    cfg[124] = clock.publish(first)  # epoch 0 (tag 0), then one epoch per 250 ms cut
+    bounds = [first + j * 250_000_000 for j in (1, 2, 3)]
+    parts = [model.encode(ev[ev["ts_ns"] < bounds[0]])]
+    for j, c in enumerate(bounds):
+        cfg[124] = clock.publish(c)
+        hi = bounds[j + 1] if j + 1 < len(bounds) else 1 << 62
+        parts.append(model.encode(ev[(ev["ts_ns"] >= c) & (ev["ts_ns"] < hi)]))
+    enc = np.concatenate(parts)
+    e16 = enc[(enc["ctx_type"] & 0xFF) < 0xF0]
     assert len(set((e16["trace_id"] >> np.uint32(30)).tolist())) > 1
-    sp = records.wire_spans(win.spans, conns, traces)
-    engine.set_ctx_table(ctxs.table())
-    engine.stage(e16, sp, win.n_groups, win.group_labels, bases=bases)
+    tab = records.HostEncoderModel()
+    for p, sn in zip(ev["pod_id"], (ev["svc_id"].astype(np.uint32) << 16) | ev["node_id"]):
+        tab.set_pod(int(p), int(sn))
+    tab.apply_defs(enc[(enc["ctx_type"] & 0xFF) >= 0xF0])
+    sp20 = tab.encode_spans(win.spans)
+    ids, rows = tab.take_rows()
+    engine.set_ctx_rows(ids, rows)
+    engine.stage(e16, sp20, win.n_groups, win.group_labels, bases=clock.bases())
     engine.upload()
     engine.run(True, False)
     out = engine.outputs()
     e = engine.eng
-    d = oracle.decode_w16(e16, t_base, ctxs.table(), bases=bases)
-    N, S = win.n_events, win.n_spans
-    np.testing.assert_array_equal(rows(e, N)["ts"], d.ts)
+    table = oracle.CtxTable(ids, rows)
+    d = oracle.decode_w16(e16, table, clock.bases())
+    N, S = len(e16), win.n_spans
+    np.testing.assert_array_equal(rows_(e, N)["ts"], d.ts)
     np.testing.assert_array_equal(d.ts, ev["ts_ns"])
-    np.testing.assert_array_equal(rows(e, N)["slot"], d.slot.astype(np.uint32))
-    ref = oracle.join(d, sp, win.n_groups)
+    np.testing.assert_array_equal(rows_(e, N)["slot"], d.slot.astype(np.uint32))
+    np.testing.assert_array_equal(rows_(e, N)["svcnode"], d.svcnode)
+    ref = oracle.join(d, oracle.decode_span20(sp20, table), win.n_groups)
     top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
     np.testing.assert_array_equal(top3, ref.top3)
     for k in ("candidates", "low_confidence", "fanout_dropped", "unmatched", "unsupported_type", "spans_enriched"):
         assert out.debug[k] == ref.debug[k], k
     np.testing.assert_array_equal(out.feat, ref.feat)
-
-
-def test_wire16_native_matches_oracle(engine):
-    """Native encoder (EVENT16, interned trace ids) -> GPU decode + join == numpy oracle."""
-    from llm_slo_ebpf_toolkit_amd.collector import records
-
-    win = small_window(seed=19)
-    engine.set_join_params(2000.0, 0.7, 3, 1)
-    engine.set_model(NaiveBayes.ref())
-    enc = records.native_encoder()
-    buf = np.zeros(win.n_events * 16, dtype=np.uint8)
-    t_base = enc.encode(win.events, buf, 16)
-    sp = np.zeros_like(win.spans)
-    enc.encode_spans(win.spans, sp, True)
-    ev16 = buf.view(records.EVENT16)
-    engine.set_ctx_table(enc.ctx_table())
-    engine.stage(ev16, sp, win.n_groups, win.group_labels, t_base=t_base)
-    engine.upload()
-    engine.run(True, False)
-    out = engine.outputs()
-    e = engine.eng
-    d = oracle.decode_w16(ev16, t_base, enc.ctx_table())
-    S = win.n_spans
-    np.testing.assert_array_equal(rows(e, win.n_events)["ts"], d.ts)
-    ref = oracle.join(d, sp, win.n_groups)
-    top3 = e.top3[: 3 * S].cpu().numpy().view(np.uint64).reshape(S, 3)
-    np.testing.assert_array_equal(top3, ref.top3)
-    np.testing.assert_array_equal(out.feat, ref.feat)
-    # interning is exact: the same join as on the full 64-byte records
-    full = oracle.join(oracle.decode_events(win.events), win.spans, win.n_groups)
-    np.testing.assert_array_equal(ref.top3, full.top3)
-    assert ref.debug == full.debug
+    full = oracle.join(oracle.decode_events(ev), win.spans, win.n_groups)
+    assert full.debug["candidates"] == ref.debug["candidates"]
+    assert int(e.misc[1].item()) == 1  # the zero timestamp
 
 
 def test_split_pre_post_equals_run_window(engine):
@@ -356,86 +245,3 @@ def test_device_refit_matches_host_learned_model(engine):
     assert dev["table_mask"] == ref["table_mask"] and dev["mode"] == 0
 
 
-def test_pipeline_wire20_equals_wire32():
-    """The pipelined engine gives bit-identical window totals on 32-, 20- and 16-byte records
-    (native encoder, append-only context table uploads, graphs, device refit)."""
-    import torch
-
-    from llm_slo_ebpf_toolkit_amd.collector import records
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, stage_window
-
-    cfg = ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8, events_per_window=6000,
-                       spans_per_window=300, seed=23)
-    gen = ReplayGenerator(cfg)
-    wins = [gen.next_window() for _ in range(3)]
-    sums = {}
-    for wire in (32, 21, 20, 16):
-        it, enc = records.ConnInterner(), records.native_encoder()
-        staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 8, w.group_domains, wire=wire,
-                               interner=it, encoder=enc) for w in wins]
-        pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
-        for i in range(6):
-            pipe.submit(staged[i % 3])
-        sums[wire] = pipe.summary()
-    for wire in (21, 20, 16):
-        for k in ("confusion", "hist", "status", "dbg", "misc"):
-            np.testing.assert_array_equal(sums[wire][k], sums[32][k], err_msg=f"{wire} {k}")
-
-
-@pytest.mark.gpu
-def test_wire_stager_matches_prestaged_windows():
-    """bench.py's per-step staging (WireStager: probe-native EVENT32 / EVENT24 / EVENT20T rings + span mapping,
-    pooled 16/20-byte encoding, pinned 64-byte ring) reproduces the totals of windows staged
-    up front with stage_window."""
-    import torch
-
-    from llm_slo_ebpf_toolkit_amd.collector import records
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, WireStager, stage_window
-
-    cfg = ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8, events_per_window=6000,
-                       spans_per_window=300, seed=29)
-    gen = ReplayGenerator(cfg)
-    wins = [gen.next_window() for _ in range(3)]
-    pods = records.pod_table(np.concatenate([w.events for w in wins]), np.concatenate([w.spans for w in wins]))
-
-    def totals_prestaged(wire):
-        it, enc = records.ConnInterner(), records.native_encoder()
-        staged = [stage_window(torch, w.events, w.spans, w.n_groups, w.group_labels, 8, w.group_domains, wire=wire,
-                               interner=it, encoder=enc) for w in wins]
-        pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
-        for i in range(7):
-            pipe.submit(staged[i % 3])
-        return pipe.summary()
-
-    def totals_stager(wire):
-        pipe = WindowPipeline(8192, 512, 8, 0, None, model="bayes_learned")
-        st = WireStager(torch, pipe, 8192, 512, 8, wire=16 if wire == "16t" else wire, threads=4)
-        if wire == 64:
-            ring = [(torch.from_numpy(w.events.view(np.uint8).reshape(-1)).pin_memory(),
-                     torch.from_numpy(w.spans.view(np.uint8).reshape(-1)).pin_memory()) for w in wins]
-        elif wire in (21, 24, 32):
-            ring = [(st.probe_records(w.events), None) for w in wins]
-        elif wire == "16t":  # EVENT16 probe ring, epoch-tagged
-            r16 = [st.probe_ring16(w.events, epoch_ns=300_000_000) for w in wins]
-            ring = [(t, b) for t, b in r16]
-        else:
-            ring = [(None, None)] * 3
-        for i in range(7):
-            w = wins[i % 3]
-            if wire == "16t":
-                pipe.submit(st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
-                                     ev_pinned=ring[i % 3][0], bases=ring[i % 3][1]))
-            else:
-                pipe.submit(st.stage(w.events, w.spans, w.n_groups, w.group_labels, w.group_domains,
-                                     ev_pinned=ring[i % 3][0], sp_pinned=ring[i % 3][1], pod_table=pods))
-        return pipe.summary()
-
-    keys = ("confusion", "hist", "status", "dbg", "misc")
-    ref32 = totals_prestaged(32)
-    for wire in (32, 24, 21, 20, 16, "16t"):
-        got = totals_stager(wire)
-        for k in keys:
-            np.testing.assert_array_equal(got[k], ref32[k], err_msg=f"stager {wire} {k}")
-    ref64, got64 = totals_prestaged(64), totals_stager(64)
-    for k in keys:
-        np.testing.assert_array_equal(got64[k], ref64[k], err_msg=f"stager 64 {k}")
