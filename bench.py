@@ -13,11 +13,12 @@ One step = one collection window per GPU, exactly as the agent runs it:
   producer process (stands in for the kernel: the probes' records, already framed as the BPF
   ring buffer holds them, plus the rocprofiler tool's GPU-signal records and the spans)
     -> emulated BPF ring buffer (kernel user-visible layout) / user-space rings (shared memory)
-  agent (timed):  window cut -> native assembly (parallel compaction of the ring's EVENT16
-    records, id definitions, host encoding of user-space records and spans, context-row patch)
-    -> one H2D DMA -> HIP graph: decode + histograms -> LDS hash join -> MFMA posterior +
-    confusion -> MFMA sufficient statistics -> pack -> RCCL all-reduce of the packet over
-    xGMI (N > 1) -> on-device model refit (prequential, random-init priors).
+  agent (timed):  window cut -> DMA of the window's ring bytes straight from the page-locked
+    rings (the host touches no record) -> HIP graph: the probes' id definitions applied on the
+    device (context rows, trace map) -> decode of framed + user-space records + histograms ->
+    LDS hash join -> MFMA posterior + confusion -> MFMA sufficient statistics -> pack -> RCCL
+    all-reduce of the packet over xGMI (N > 1) -> on-device model refit (prequential,
+    random-init priors).
 
 Synthetic data: seeded fault-replay traces (pipeline/replay.py, REF fault profiles), random-init
 attribution priors; the kernel's record path is the native probe model (runtime/csrc/probesim.h).
@@ -56,7 +57,6 @@ def parse():
     ap.add_argument("--paced-windows", type=int, default=3,
                     help="windows produced at 1M events/s for the CPU-overhead measurement (0 = skip)")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--threads", type=int, default=0, help="agent host threads (0 = min(OMP_NUM_THREADS, 8))")
     ap.add_argument("--ring-mib", type=int, default=1024, help="emulated BPF ring buffer size (MiB, power of 2)")
     ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
     ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4))
@@ -112,6 +112,9 @@ def producer_main(names, imgs, heldout, plan, conn) -> None:
 
 def main() -> int:
     a = parse()
+    # PyTorch first: it brings its own HIP runtime, which the native engine module then shares
+    # (one HIP runtime per process). Importing it initialises no GPU, so the fork below is safe.
+    import torch  # noqa: F401
     import numpy as np
 
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
@@ -123,7 +126,6 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    threads = a.threads or max(1, min(8, int(os.environ.get("OMP_NUM_THREADS", "0") or 8)))
 
     def log(*x):
         if rank == 0:
@@ -193,11 +195,14 @@ def main() -> int:
         uid = [rt_uid() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = (uid[0], rank, world)
+    user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
     pipe = WindowPipeline(a.events, a.spans, a.services, local, comm, model=a.model, seed=a.seed,
-                          use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers)
-    src = RingWindowSource(pipe, rb, user, spans, threads=threads, cfg_set=lambda i, v: None)
+                          use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,
+                          user_cap=min(user_cap, a.events))
+    # the producer publishes the epochs here (it runs ahead of the cuts): no cfg writes
+    src = RingWindowSource(pipe, rb, user, spans, cfg_set=lambda i, v: None)
     keys = np.array(sorted(pod_sn), dtype=np.uint32)
-    src.tables.set_pods(keys, np.array([pod_sn[k] for k in keys.tolist()], dtype=np.uint32))
+    pipe.eng.set_pods(keys, np.array([pod_sn[k] for k in keys.tolist()], dtype=np.uint32))
     wait_s = [0.0]
 
     def next_cut(sleep=20e-6) -> Cut:
@@ -216,13 +221,13 @@ def main() -> int:
     def step(j, with_labels=True, learn=None, sleep=20e-6):
         img = imgs[j % len(imgs)]
         c = next_cut(sleep)
-        r = src.stage(c, img.n_groups, img.labels)
-        return pipe.submit(r["dma_bytes"], img.n_groups, with_labels=with_labels, learn=learn), r
+        r = src.stage(c, img.n_groups, img.labels, with_labels=with_labels, learn=learn)
+        return r["k"], r
 
     # ---- warmup (also the model's first training windows) ---------------------------------
     for j in range(a.warmup):
         step(j)
-    pipe.drain()
+    src.drain()
     if pg is not None:
         dist.barrier()
     pipe.reset_totals()
@@ -242,7 +247,7 @@ def main() -> int:
     for j in range(a.warmup, a.warmup + a.steps):
         last, r = step(j)
         kernel_recs += r["n_kernel"]
-    pipe.drain()
+    src.drain()
     torch.cuda.synchronize()
     if pg is not None:
         dist.barrier()
@@ -287,8 +292,7 @@ def main() -> int:
     held_conf = {"full": np.zeros((16, 16)), "mixed": np.zeros((16, 16))}
     for j, h in enumerate(himgs):
         c = next_cut(2e-3)
-        r = src.stage(c, h.n_groups, h.labels)
-        k = pipe.submit(r["dma_bytes"], h.n_groups, with_labels=True, learn=False)
+        k = src.stage(c, h.n_groups, h.labels, with_labels=True, learn=False)["k"]
         held_conf["mixed" if j % 2 else "full"] += pipe.packet(k)["confusion"]
     D = len(catalog.ALL_DOMAINS)
     heldout = {}
@@ -309,6 +313,7 @@ def main() -> int:
     if rank == 0 and os.path.exists(fx):
         ref_f1 = ref55_gpu(fx, pipe.host_model(), a.model)
     prod.join(timeout=30)
+    src.drain()
 
     conf = summ["confusion"]
     dbg = summ["dbg"]
@@ -356,10 +361,10 @@ def main() -> int:
         "paced_window_latency_ms": round(float(np.median(lat_ms)), 3) if lat_ms else None,
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
         "kernel_ring_records_per_step": int(kernel_recs // max(a.steps, 1)),
-        "host_assemble_us_per_window": round(host_us, 1),
+        "host_us_per_window": round(host_us, 1),
         "host_issue_us_per_window": round(pipe.eng.host_issue_us, 1),
+        "direct_dma_fraction": round(pipe.eng.direct_bytes / max(1, pipe.eng.direct_bytes + pipe.eng.staged_bytes), 4),
         "producer_wait_ms_total": round(producer_wait_ms, 2),
-        "host_threads": threads,
         "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
     }
     if rank == 0:
@@ -368,6 +373,7 @@ def main() -> int:
         if a.out:
             with open(a.out, "w") as fh:
                 fh.write(line + "\n")
+    pipe.eng.close()  # release the engine's device memory before interpreter teardown
     if pg is not None:
         dist.barrier()
         dist.destroy_process_group()

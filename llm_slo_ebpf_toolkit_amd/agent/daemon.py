@@ -164,7 +164,7 @@ class AgentOptions:
     device: int = 0
     model: str = "bayes"
     min_confidence: float = 0.5
-    host_threads: int = 2
+    ttft_slo_ms: float = 800.0           # per-incident SLO: a span breaches when its TTFT exceeds this
     slo_target: float = 0.99             # TTFT SLO objective (burn rate = breach fraction / (1 - target))
 
 
@@ -379,8 +379,7 @@ class Agent:
             return bpf.EmulatedMaps(ring), ring, user, spans, bpf.pod_metadata(kw)
         raise ValueError(f"unknown window source {o.source!r} (bpf | shm | replay)")
 
-    def _attributions(self, G: int, names: Sequence[str], res: dict, sli: Optional[np.ndarray], t_ns: int,
-                      model) -> List[IncidentAttribution]:
+    def _attributions(self, G: int, names: Sequence[str], res: dict, t_ns: int, model) -> List[IncidentAttribution]:
         """One IncidentAttribution per incident group whose top posterior clears min_confidence.
         Evidence carries the group's measured signal values (mean over joined kernel signals);
         SLO impact comes from the group's spans in the window (TTFT SLO breach fraction over the
@@ -388,6 +387,7 @@ class Agent:
         out = []
         D = model.weights.shape[1]
         post, bits, feat = res["post"], res["evbits"].view(np.uint32), res["feat"]
+        sli = res.get("sli")
         for g in range(G):
             ranked = model.ranked(post[g, :D], bits[g, :D])
             if not ranked or ranked[0].posterior < self.o.min_confidence:
@@ -412,13 +412,15 @@ class Agent:
                                   if p.posterior >= 0.01]))
         return out
 
-    def _emit_window(self, pipe, k: int, t_ns: int, G: int, names, n_events: int, sli) -> None:
+    def _emit_window(self, pipe, k: int, t_ns: int, G: int, names, ring, host_us: float) -> None:
         pk = pipe.packet(k)
         lat_ms = pipe.window_ms(k)[0]
-        self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], n_events, lat_ms, self.o.node, self.o.pod,
+        rs = pk["ring_state"]
+        self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], rs["events"], lat_ms, self.o.node, self.o.pod,
                                     self.o.namespace)
+        self.metrics.set_ring(ring.stats() if ring is not None else {}, rs, host_us)
         res = pipe.results(k, G)
-        for attr in self._attributions(G, names, res, sli, t_ns, pipe.model):
+        for attr in self._attributions(G, names, res, t_ns, pipe.model):
             self.metrics.observe_attribution(attr.predicted_fault_domain)
             self.writers.emit_attribution(attr)
             self.attributions_emitted += 1
@@ -443,10 +445,11 @@ class Agent:
         node_id = (abs(hash(o.node)) % 0xFFFE) + 1
         maps.init(node_id)
         pipe = WindowPipeline(o.window_events, o.window_spans, o.window_groups, o.device, comm, model=o.model,
-                              learn=False, window_ms=2000.0)
-        src = RingWindowSource(pipe, ring, user, spans, threads=o.host_threads, cfg_set=maps.cfg_set)
+                              learn=False, window_ms=2000.0, user_cap=max(1024, o.window_events // 4),
+                              ttft_slo_ms=o.ttft_slo_ms)
+        src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
         if pods is not None:
-            src.tables.set_pods(*pods)
+            pipe.eng.set_pods(*pods)
         names = [f"svc-{g + 1}" for g in range(o.window_groups)]
         G = o.window_groups
         if self.guard is not None:
@@ -461,12 +464,14 @@ class Agent:
                 break
             nxt += period
             cut = src.cut()
-            r = src.stage(cut, G)
-            k = pipe.submit(r["dma_bytes"], G, with_labels=False, learn=False)
+            t_h = time.perf_counter()
+            k = src.stage(cut, G, with_labels=False, learn=False)["k"]
+            host_us = 1e6 * (time.perf_counter() - t_h)
             if pending is not None:
                 self._emit_window(pipe, *pending)
-            pending = (k, cut.t_ns, G, names, int(r["n_events"]), src.group_sli())
-            self.metrics.set_ring(ring.stats() if hasattr(ring, "stats") else {}, r)
+            pending = (k, cut.t_ns, G, names, ring, host_us)
+            if self.windows_done and self.windows_done % 64 == 0:
+                pipe.eng.rotate_traces()  # trace-id mappings live 64-128 windows
             self._guard_tick()
             self.metrics.set_heartbeat()
             self.windows_done += 1
@@ -476,7 +481,7 @@ class Agent:
                 maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
         if pending is not None:
             self._emit_window(pipe, *pending)
-        pipe.drain()
+        src.drain()
         self.last_pipe = pipe
         self.writers.flush()
         return 0

@@ -120,16 +120,17 @@ class AgentMetrics:
         self.corr.inc(float(dropped), "fanout_dropped")
         self.corr.inc(float(enriched), "span_enriched")
 
-    def set_ring(self, ring_stats: dict, assembled: dict) -> None:
-        """Per-window ring accounting: definitions consumed, busy stops, backlog, drops
-        (the emulated ring counts failed reservations; the kernel's are invisible to user space)."""
-        self.ring_defs.inc(float(assembled.get("n_defs", 0)))
-        if assembled.get("busy_stop"):
+    def set_ring(self, ring_stats: dict, ring_state: dict, host_us: float) -> None:
+        """Per-window ring accounting (counted on the device): id definitions applied, windows
+        that met a record still being written, backlog, drops (the emulated ring counts failed
+        reservations; the kernel's are invisible to user space), host time per window."""
+        self.ring_defs.inc(float(ring_state.get("def_ctx", 0) + ring_state.get("def_trace", 0)))
+        if ring_state.get("first_busy", -1) >= 0:
             self.ring_busy.inc()
         if ring_stats:
             self.ring_backlog.set(float(ring_stats.get("producer_pos", 0) - ring_stats.get("consumer_pos", 0)))
             self.ring_dropped.set(float(ring_stats.get("dropped", 0)))
-        self.host_us.set(float(assembled.get("host_us", 0.0)))
+        self.host_us.set(float(host_us))
 
     def observe_attribution(self, domain: str) -> None:
         self.attr.inc(1, domain)

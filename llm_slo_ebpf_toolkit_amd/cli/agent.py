@@ -2,7 +2,7 @@
 
 REF flags are all accepted with REF defaults. Additive flags select the MI355X window
 engine: ``--engine gpu --source bpf|shm|replay --pin-dir --window-ms --window-events --device
---model --min-confidence --host-threads --slo-target``; ``--count`` bounds the number of
+--model --min-confidence --ttft-slo-ms --slo-target``; ``--count`` bounds the number of
 windows in GPU mode.
 """
 
@@ -56,7 +56,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("device", d.device, "HIP device ordinal"),
         ("model", d.model, "attribution model: bayes|bayes_learned|lda"),
         ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
-        ("host-threads", d.host_threads, "host threads compacting the ring per window"),
+        ("ttft-slo-ms", d.ttft_slo_ms, "per-incident TTFT SLO (ms) for burn rates"),
         ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),
     ]:
         p.flag(name, default, help_)
@@ -73,7 +73,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         metrics_bind=a.metrics_bind, engine=a.engine, source=a.source, ring_name=a.ring_name, pin_dir=a.pin_dir,
         window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
-        host_threads=a.host_threads, slo_target=a.slo_target)
+        ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target)
     return o, a.probe_smoke
 
 

@@ -76,11 +76,12 @@ def _gpu_loop(duration_s: float, rate_eps: float, window_s: float) -> Dict[str, 
     ring, user, spans = bpf.create_rings(names, 4 * 24 * n, 4 * n, 4 * kw["spans_per_window"])
     prod = bpf.start_replay_producer(names, kw, rate_eps, int(window_s * 1000), n_images=2)
     try:
-        pipe = WindowPipeline(n, kw["spans_per_window"], groups, 0, None, model="bayes", learn=False)
-        src = RingWindowSource(pipe, ring, user, spans, threads=2)
-        src.tables.set_pods(*bpf.pod_metadata(kw))
+        pipe = WindowPipeline(n, kw["spans_per_window"], groups, 0, None, model="bayes", learn=False,
+                              user_cap=max(1024, n // 2))
+        src = RingWindowSource(pipe, ring, user, spans)
+        pipe.eng.set_pods(*bpf.pod_metadata(kw))
         src.step(groups, with_labels=False)
-        pipe.drain()
+        src.drain()
         c0, w0 = time.process_time(), time.perf_counter()
         nxt = w0
         k = events = 0
@@ -90,10 +91,12 @@ def _gpu_loop(duration_s: float, rate_eps: float, window_s: float) -> Dict[str, 
             src.step(groups, with_labels=False)
             events += int(src.last["n_events"])
             k += 1
-        pipe.drain()
+        src.drain()
         cpu, wall = time.process_time() - c0, time.perf_counter() - w0
     finally:
         prod.terminate()
+        if "pipe" in locals():
+            pipe.eng.close()
     return {"cpu_pct": 100.0 * cpu / wall, "events_per_second": events / wall, "dropped": 0}
 
 

@@ -123,8 +123,8 @@ def build_agent_ext(force: bool = False, jobs: int = 4) -> str:
     pybind11 and linked against the HIP runtime and RCCL only (no PyTorch)."""
     os.makedirs(BUILD, exist_ok=True)
     out = os.path.join(HERE, "_mislo_agent" + EXT_SUFFIX)
-    hdrs = _headers(CSRC) + [os.path.join(RT_CSRC, "slot.h")]
-    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", f"-I{RT_CSRC}"]
+    hdrs = _headers(CSRC)
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
     common += os.environ.get("MISLO_HIP_DEFINES", "").split()
     jobs_list, objs = [], []
     for src in AGENT_KERNELS:  # shared with the torch extension (same flags, same objects)
@@ -159,13 +159,12 @@ def build_runtime(force: bool = False, jobs: int = 4) -> List[str]:
     core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp")]
     lib = os.path.join(rt_dir, "libmislo_rt.so")
     if force or _newer(lib, core + hdrs):
-        _run([cxx, *base, "-shared", *core, "-o", lib, f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+        _run([cxx, *base, "-shared", *core, "-o", lib])
     outs.append(lib)
     mod = os.path.join(rt_dir, "_mislo_rt" + EXT_SUFFIX)
     srcs = [os.path.join(RT_CSRC, s) for s in RT_SOURCES]
-    if force or _newer(mod, srcs + hdrs):
-        _run([cxx, *base, *pybind_flags(), "-shared", *srcs, "-o", mod, f"-L{ROCM}/lib", "-lamdhip64",
-              f"-Wl,-rpath,{ROCM}/lib"])
+    if force or _newer(mod, srcs + hdrs):  # CPU only: no HIP runtime dependency
+        _run([cxx, *base, *pybind_flags(), "-shared", *srcs, "-o", mod])
     outs.append(mod)
     return outs
 

@@ -47,15 +47,15 @@ void set_tables_np(py::array_t<int8_t, py::array::c_style | py::array::forcecast
 
 class PyEngine {
  public:
-  PyEngine(int device, int sig_cap, int span_cap, int group_cap, int row_cap, int n_buffers, int max_ahead,
+  PyEngine(int device, int sig_cap, int span_cap, int group_cap, int user_cap, int n_buffers, int max_ahead,
            double window_ms, double threshold, int fanout, int group_mode, bool use_graphs, bool device_refit,
-           int n_dom) {
+           int n_dom, float ttft_slo_ms) {
     EngineConfig c;
     c.device = device;
     c.sig_cap = sig_cap;
     c.span_cap = span_cap;
     c.group_cap = group_cap;
-    c.row_cap = row_cap;
+    c.user_cap = user_cap;
     c.n_buffers = n_buffers;
     c.max_ahead = max_ahead;
     c.window_ms = window_ms;
@@ -65,20 +65,41 @@ class PyEngine {
     c.use_graphs = use_graphs;
     c.device_refit = device_refit;
     c.n_dom = n_dom;
+    c.ttft_slo_ms = ttft_slo_ms;
     e_ = std::make_unique<WindowEngine>(c);
   }
-  uintptr_t host_slot(int64_t k) const { return reinterpret_cast<uintptr_t>(e_->host_slot(k)); }
-  py::array slot_view(int64_t k) {
-    return py::array(py::dtype("uint8"), {(py::ssize_t)e_->layout().bytes}, {(py::ssize_t)1}, e_->host_slot(k),
-                     py::cast(this, py::return_value_policy::reference));
+  bool register_host(uintptr_t addr, size_t bytes) {
+    return e_->register_host(reinterpret_cast<const void*>(addr), bytes);
   }
-  void wait_slot(int64_t k) {
+  // segments: lists of (host address, bytes) in ring order
+  void submit(int64_t k, const std::vector<std::pair<uintptr_t, size_t>>& kernel,
+              const std::vector<std::pair<uintptr_t, size_t>>& user,
+              const std::vector<std::pair<uintptr_t, size_t>>& spans, int n_groups, py::object labels,
+              std::vector<int64_t> bases, bool with_labels, bool learn) {
+    WindowInput in;
+    auto conv = [](const std::vector<std::pair<uintptr_t, size_t>>& v, std::vector<Seg>& out) {
+      for (auto& p : v) out.push_back(Seg{reinterpret_cast<const void*>(p.first), p.second});
+    };
+    conv(kernel, in.kernel);
+    conv(user, in.user);
+    conv(spans, in.spans);
+    in.n_groups = n_groups;
+    std::vector<int32_t> lab;
+    if (!labels.is_none()) {
+      auto arr = labels.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
+      lab.assign(arr.data(), arr.data() + arr.size());
+      lab.resize(std::max<size_t>(lab.size(), (size_t)std::max(0, n_groups)), -1);
+      in.labels = lab.data();
+    }
+    bases.resize(4, 0);
+    for (int q = 0; q < 4; ++q) in.bases[q] = bases[q];
     py::gil_scoped_release nogil;
-    e_->wait_slot(k);
+    e_->submit(k, in, with_labels, learn);
   }
-  void submit(int64_t k, size_t dma_bytes, int n_groups, bool with_labels, bool learn) {
+  bool h2d_done(int64_t k) { return e_->h2d_done(k); }
+  void wait_h2d(int64_t k) {
     py::gil_scoped_release nogil;
-    e_->submit(k, dma_bytes, n_groups, with_labels, learn);
+    e_->wait_h2d(k);
   }
   bool query(int64_t k) { return e_->query(k); }
   void wait(int64_t k) {
@@ -96,6 +117,7 @@ class PyEngine {
     d["feat"] = copy_array(r.feat, {G, 16});
     d["pred"] = copy_array(r.pred, {G});
     d["evbits"] = copy_array(r.evbits, {G, 16});
+    d["sli"] = copy_array(r.sli, {G, 2});
     return d;
   }
   py::tuple window_ms(int64_t k) {
@@ -113,6 +135,12 @@ class PyEngine {
     if (p0.size() != kSlots * 16) throw std::invalid_argument("p0 must be f64[256]");
     e_->set_p0(p0.data());
   }
+  void set_pods(py::array_t<uint32_t, py::array::c_style | py::array::forcecast> pods,
+                py::array_t<uint32_t, py::array::c_style | py::array::forcecast> sn) {
+    if (pods.size() != sn.size()) throw std::invalid_argument("pods / svcnode size mismatch");
+    e_->set_pods(pods.data(), sn.data(), (size_t)pods.size());
+  }
+  void rotate_traces() { e_->rotate_traces(); }
   void set_join_params(double window_ms, double threshold, int fanout, int group_mode) {
     e_->set_join_params(window_ms, threshold, fanout, group_mode);
   }
@@ -156,23 +184,24 @@ class PyEngine {
     py::gil_scoped_release nogil;
     e_->sync();
   }
-  py::dict layout() const {
-    const SlotLayout& L = e_->layout();
-    py::dict d;
-    d["group_cap"] = L.group_cap;
-    d["span_cap"] = L.span_cap;
-    d["sig_cap"] = L.sig_cap;
-    d["row_cap"] = L.row_cap;
-    d["sp_off"] = L.sp_off;
-    d["ev_off"] = L.ev_off;
-    d["bytes"] = L.bytes;
-    return d;
+  void close() {
+    if (e_) {
+      py::gil_scoped_release nogil;
+      e_->sync();
+      e_.reset();
+    }
   }
-  int buffers() const { return e_->buffers(); }
-  int64_t folded() const { return e_->windows_folded(); }
-  size_t graphs() const { return e_->graphs(); }
-  double host_issue_us() const { return e_->host_issue_us(); }
-  bool has_comm() const { return e_->has_comm(); }
+  WindowEngine& eng() {
+    if (!e_) throw std::logic_error("engine closed");
+    return *e_;
+  }
+  int buffers() { return eng().buffers(); }
+  int64_t folded() { return eng().windows_folded(); }
+  size_t graphs() { return eng().graphs(); }
+  double host_issue_us() { return eng().host_issue_us(); }
+  bool has_comm() { return eng().has_comm(); }
+  size_t staged_bytes() { return eng().staged_bytes(); }
+  size_t direct_bytes() { return eng().direct_bytes(); }
 
  private:
   std::unique_ptr<WindowEngine> e_;
@@ -200,17 +229,21 @@ PYBIND11_MODULE(_mislo_agent, m) {
   m.attr("STATS_LEN") = kStatsLen;
   m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
   m.attr("CTX_ROWS") = kCtxRows;
+  m.attr("REC_STRIDE") = kRecStride;
+  m.attr("RING_STATE") = py::make_tuple("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events");
   py::class_<PyEngine>(m, "WindowEngine")
-      .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int>(),
+      .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int, float>(),
            py::arg("device") = 0, py::arg("sig_cap") = 1 << 20, py::arg("span_cap") = 16384, py::arg("group_cap") = 64,
-           py::arg("row_cap") = 1 << 17, py::arg("n_buffers") = 3, py::arg("max_ahead") = 3,
+           py::arg("user_cap") = 1 << 18, py::arg("n_buffers") = 3, py::arg("max_ahead") = 3,
            py::arg("window_ms") = 2000.0, py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1,
-           py::arg("use_graphs") = true, py::arg("device_refit") = true, py::arg("n_dom") = 10)
-      .def("host_slot", &PyEngine::host_slot)
-      .def("slot_view", &PyEngine::slot_view)
-      .def("wait_slot", &PyEngine::wait_slot)
-      .def("submit", &PyEngine::submit, py::arg("k"), py::arg("dma_bytes"), py::arg("n_groups"),
+           py::arg("use_graphs") = true, py::arg("device_refit") = true, py::arg("n_dom") = 10,
+           py::arg("ttft_slo_ms") = 800.0f)
+      .def("register_host", &PyEngine::register_host)
+      .def("submit", &PyEngine::submit, py::arg("k"), py::arg("kernel"), py::arg("user"), py::arg("spans"),
+           py::arg("n_groups"), py::arg("labels") = py::none(), py::arg("bases") = std::vector<int64_t>{},
            py::arg("with_labels") = true, py::arg("learn") = false)
+      .def("h2d_done", &PyEngine::h2d_done)
+      .def("wait_h2d", &PyEngine::wait_h2d)
       .def("query", &PyEngine::query)
       .def("wait", &PyEngine::wait)
       .def("packet", &PyEngine::packet)
@@ -218,6 +251,8 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("window_ms", &PyEngine::window_ms)
       .def("set_model_bytes", &PyEngine::set_model_bytes)
       .def("set_p0", &PyEngine::set_p0)
+      .def("set_pods", &PyEngine::set_pods)
+      .def("rotate_traces", &PyEngine::rotate_traces)
       .def("set_join_params", &PyEngine::set_join_params)
       .def("init_comm", &PyEngine::init_comm)
       .def("totals", &PyEngine::totals)
@@ -225,10 +260,12 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("stats_acc", &PyEngine::stats_acc)
       .def("model_bytes", &PyEngine::model_bytes)
       .def("sync", &PyEngine::sync)
-      .def_property_readonly("layout", &PyEngine::layout)
+      .def("close", &PyEngine::close)
       .def_property_readonly("buffers", &PyEngine::buffers)
       .def_property_readonly("windows_folded", &PyEngine::folded)
       .def_property_readonly("graphs", &PyEngine::graphs)
       .def_property_readonly("host_issue_us", &PyEngine::host_issue_us)
-      .def_property_readonly("has_comm", &PyEngine::has_comm);
+      .def_property_readonly("has_comm", &PyEngine::has_comm)
+      .def_property_readonly("staged_bytes", &PyEngine::staged_bytes)
+      .def_property_readonly("direct_bytes", &PyEngine::direct_bytes);
 }

@@ -1,14 +1,17 @@
 // Native per-GPU window engine: the agent's executor, with no Python or PyTorch on the
 // per-window path. One process drives one MI355X; window k uses buffer b = k % nb (nb = 3):
 //
-//   host           : WindowAssembler fills pinned input block b (slot.h) after the H2D of
-//                    window k - nb (its previous reader) completed (wait_slot)
-//   copy stream    : ONE DMA of the block's used prefix -> device block b
+//   host           : cut the window (ring positions) and hand the engine the byte ranges; the
+//                    host never reads or rewrites a record
+//   copy stream    : DMA of the window's ring bytes straight from the (registered) rings into
+//                    device block b: the BPF ring's framed records as the kernel wrote them,
+//                    the user-space producers' 64-byte records, the spans, the counts
 //   compute stream : [device refit from window k - nb's all-reduced statistics]
-//                    graph(b): reset accumulators -> context-row patch -> K1 decode ->
-//                    partition -> spans -> K2 LDS join -> finalize -> K3 MFMA posterior
-//                    (+ confusion, + MFMA sufficient statistics when learning) -> pack(packet b)
-//                    -> D2H of the window's per-incident results into pinned results b
+//                    graph(b): reset accumulators -> ring definitions (context rows, trace
+//                    map) -> K1 decode (framed + user records) -> partition -> spans -> K2 LDS
+//                    join -> finalize -> K3 MFMA posterior (+ confusion, + MFMA sufficient
+//                    statistics when learning) -> pack(packet b) -> D2H of the per-incident
+//                    results into pinned results b
 //   comm stream    : RCCL all-reduce(packet b) over xGMI when the node has several GPUs ->
 //                    totals += packet b -> D2H(packet b)
 //
@@ -26,7 +29,6 @@
 #include <vector>
 
 #include "mislo_launch.h"
-#include "slot.h"
 
 namespace mislo {
 
@@ -37,14 +39,27 @@ constexpr int kPacketDbg = 8;
 constexpr int kPacketConf = kMaxDomains * kMaxDomains;  // 256
 constexpr int kPacketStats = 32 * 32;                   // 1024
 constexpr int kPacketCount = kMaxDomains;               // 16
-constexpr int kPacketLen = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf + kPacketStats + kPacketCount;
+constexpr int kPacketRing = kRsLen;                     // ring accounting (RingState)
+constexpr int kPacketLen =
+    kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf + kPacketStats + kPacketCount + kPacketRing;
 constexpr int kStatsOff = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf;
 constexpr int kStatsLen = kPacketStats + kPacketCount;  // accumulated-statistics vector (f64[1040])
 constexpr uint32_t kCtxRows = 1u << 24;                 // device context table rows (256 MiB)
+constexpr uint32_t kPodRows = 1u << 20;                 // device pod table: pod id -> svc<<16|node
+constexpr uint32_t kTraceSlots = 1u << 21;              // device trace map slots per generation
+constexpr int kHeadBytes = 64;                          // counts int32[16] (labels follow)
+
+// A host byte range to DMA (a ring segment): registered memory goes straight to the device,
+// anything else through the engine's pinned staging.
+struct Seg {
+  const void* ptr;
+  size_t bytes;
+};
 
 struct EngineConfig {
   int device = 0;
-  int sig_cap = 1 << 20, span_cap = 16384, group_cap = 64, row_cap = 1 << 17;
+  int sig_cap = 1 << 20, span_cap = 16384, group_cap = 64;
+  int user_cap = 1 << 18;  // user-space (64-byte) records per window; sig_cap bounds framed + user
   int n_buffers = 3, max_ahead = 3;
   double window_ms = 2000.0, threshold = 0.7;
   int fanout = 3, group_mode = 1;
@@ -52,6 +67,7 @@ struct EngineConfig {
   bool device_refit = true;  // learned naive Bayes refit on the device from accumulated statistics
   double alpha = 2.0, prior_pseudo = 1.0;
   int n_dom = 10;
+  float ttft_slo_ms = 800.0f;  // per-incident SLO impact: spans with TTFT above this breach
 };
 
 // per-incident results of a window, in one pinned block (one D2H)
@@ -61,6 +77,17 @@ struct ResultView {
   const float* feat;      // [G][16]
   const int32_t* pred;    // [G]
   const uint32_t* evbits; // [G][16]
+  const uint32_t* sli;    // [G][2]: spans, TTFT-SLO breaches
+};
+
+// The window's inputs: ring byte ranges (as the rings hold them) and the window metadata.
+struct WindowInput {
+  std::vector<Seg> kernel;  // framed BPF ring records (24-byte stride), in ring order
+  std::vector<Seg> user;    // 64-byte EVENT records (user-space producers)
+  std::vector<Seg> spans;   // 64-byte SPAN records
+  int n_groups = 0;
+  const int32_t* labels = nullptr;  // [n_groups] ground-truth domain (replay / evaluation) or null
+  int64_t bases[4] = {0, 0, 0, 0};  // epoch bases by tag
 };
 
 class WindowEngine {
@@ -70,13 +97,17 @@ class WindowEngine {
   WindowEngine(const WindowEngine&) = delete;
   WindowEngine& operator=(const WindowEngine&) = delete;
 
-  const SlotLayout& layout() const { return L_; }
   const EngineConfig& config() const { return cfg_; }
   int buffers() const { return nb_; }
 
-  uint8_t* host_slot(int64_t k) const { return slot_host_[k % nb_]; }
-  void wait_slot(int64_t k);  // the H2D of window k - nb (the slot's previous reader) is done
-  void submit(int64_t k, size_t dma_bytes, int n_groups, bool with_labels, bool learn);
+  // Page-lock a host range (a ring's mapping) so its bytes DMA straight to the device; false if
+  // the driver refuses (those ranges then go through pinned staging).
+  bool register_host(const void* ptr, size_t bytes);
+  // Queue window k (in order). Returns when its DMAs and kernels are queued; the ring bytes
+  // must stay untouched until h2d_done(k).
+  void submit(int64_t k, const WindowInput& in, bool with_labels, bool learn);
+  bool h2d_done(int64_t k);   // window k's input DMAs completed (its ring space may be freed)
+  void wait_h2d(int64_t k);
   bool query(int64_t k);      // window k's results are in host memory
   void wait(int64_t k);
   const double* packet(int64_t k) const { return packet_host_[k % nb_]; }
@@ -86,6 +117,8 @@ class WindowEngine {
 
   void set_model_bytes(const void* bytes, size_t n);  // stream-ordered before the next window
   void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
+  void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
+  void rotate_traces();                               // retire the older trace-map generation
   void set_join_params(double window_ms, double threshold, int fanout, int group_mode);
   void init_comm(const ncclUniqueId& id, int rank, int world);
   bool has_comm() const { return comm_ != nullptr; }
@@ -96,6 +129,8 @@ class WindowEngine {
   void model_bytes(void* out);        // the model currently on the device (synchronous)
   void sync();
   int64_t windows_folded() const { return folded_; }
+  size_t staged_bytes() const { return staged_bytes_; }
+  size_t direct_bytes() const { return direct_bytes_; }
   size_t graphs() const { return graphs_.size(); }
   double host_issue_us() const { return issue_n_ ? issue_us_ / issue_n_ : 0.0; }
 
@@ -104,17 +139,27 @@ class WindowEngine {
   void run_chain(int b, int n_groups, bool with_labels, bool learn, hipStream_t st);
   SignalCols sig_cols() const;
   SpanCols span_cols() const;
+  bool registered(const void* p, size_t n) const;
+  size_t dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap, uint8_t*& staging, size_t& st_off);
 
   EngineConfig cfg_;
-  SlotLayout L_;
   int nb_, max_ahead_;
+  size_t off_kern_ = 0, off_user_ = 0, off_span_ = 0, in_bytes_ = 0;  // device input block layout
+  std::vector<std::pair<const uint8_t*, size_t>> registered_;
+  size_t staged_bytes_ = 0, direct_bytes_ = 0;
+  uint32_t *pod_sn_ = nullptr, *pod_host_ = nullptr, *ring_state_ = nullptr, *trace_cur_ = nullptr,
+           *trace_cur_host_ = nullptr;
+  unsigned long long* trace_key_[2] = {nullptr, nullptr};
+  uint32_t* trace_val_[2] = {nullptr, nullptr};
+  uint32_t* sli_ = nullptr;
   JoinParams jp_{};
   int nblk_sig_ = 1, nblk_span_ = 1;
   hipStream_t copy_ = nullptr, compute_ = nullptr, comm_stream_ = nullptr;
   ncclComm_t comm_ = nullptr;
   // device buffers
-  std::vector<uint8_t*> slot_dev_;
-  std::vector<uint8_t*> slot_host_;
+  std::vector<uint8_t*> in_dev_;     // per buffer: [head | framed | user | spans]
+  std::vector<uint8_t*> head_host_;  // per buffer: counts + labels (pinned)
+  std::vector<uint8_t*> staging_;    // per buffer: pinned staging for unregistered ranges
   std::vector<double*> packet_dev_;
   std::vector<double*> packet_host_;
   std::vector<uint8_t*> res_dev_, res_host_;

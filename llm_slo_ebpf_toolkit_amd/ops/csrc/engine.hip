@@ -44,26 +44,10 @@ __global__ __launch_bounds__(256) void k_fill(FillList fl) {
   }
 }
 
-// The window's context-row patch (slot.h: behind the events, ids then uint4 rows) scattered
-// into the device context table before the decode reads it. Sizes come from the block's
-// counts, so one captured launch serves every window.
-__global__ __launch_bounds__(256) void k_apply_rows(const uint8_t* __restrict__ slot, size_t ev_off,
-                                                    uint4* __restrict__ table, uint32_t table_rows) {
-  const int32_t* c = reinterpret_cast<const int32_t*>(slot);
-  const uint32_t n_ev = (uint32_t)c[0], n_rows = (uint32_t)c[14];
-  const uint8_t* patch = slot + ev_off + 16 * (size_t)n_ev;
-  const uint32_t* ids = reinterpret_cast<const uint32_t*>(patch);
-  const uint4* rows = reinterpret_cast<const uint4*>(patch + ((4 * (size_t)n_rows + 15) & ~size_t(15)));
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n_rows; i += gridDim.x * 256) {
-    const uint32_t id = ids[i];
-    if (id < table_rows) table[id] = rows[i];
-  }
-}
-
 // accumulators -> packet (f64), one element per thread
 __global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsigned long long* misc,
                        const unsigned long long* dbg, const uint32_t* confusion, const double* stats,
-                       const double* count, double* out) {
+                       const double* count, const uint32_t* ring, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   int o = 0;
   if (i < kPacketHist) { out[i] = hist[i]; return; }
@@ -79,6 +63,12 @@ __global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsig
   if (i < o + kPacketStats) { out[i] = stats[i - o]; return; }
   o += kPacketStats;
   if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
+  o += kPacketCount;
+  if (i < o + kPacketRing) {
+    const uint32_t v = ring[i - o];
+    out[i] = (i - o == kRsFirstBusy && v == 0xFFFFFFFFu) ? -1.0 : (double)v;  // -1: no busy record
+    return;
+  }
 }
 
 __global__ void k_accumulate(const double* __restrict__ packet, double* __restrict__ totals, int n) {
@@ -109,7 +99,7 @@ WindowEngine::WindowEngine(const EngineConfig& cfg) : cfg_(cfg) {
   if (cfg.sig_cap >= (1 << 27)) throw std::invalid_argument("sig_cap must be < 2^27 (top-3 key packing)");
   nb_ = std::max(2, cfg.n_buffers);
   max_ahead_ = std::min(nb_, std::max(1, cfg.max_ahead));
-  L_ = slot_layout((uint32_t)cfg.group_cap, (uint32_t)cfg.span_cap, (uint32_t)cfg.sig_cap, (uint32_t)cfg.row_cap);
+  if (cfg.user_cap <= 0 || cfg.user_cap > cfg.sig_cap) throw std::invalid_argument("user_cap must be in [1, sig_cap]");
   HIPCHECK(hipSetDevice(cfg.device));
   set_join_params(cfg.window_ms, cfg.threshold, cfg.fanout, cfg.group_mode);
   alloc();
@@ -140,13 +130,20 @@ void WindowEngine::alloc() {
   HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   HIPCHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  // device input block per buffer: [head (counts + labels) | framed ring records | user records | spans]
+  const size_t head = (kHeadBytes + 4 * (size_t)G + 63) & ~size_t(63);
+  off_kern_ = head;
+  off_user_ = (off_kern_ + (size_t)kRecStride * N + 63) & ~size_t(63);
+  off_span_ = off_user_ + 64 * (size_t)cfg_.user_cap;
+  in_bytes_ = off_span_ + 64 * (size_t)S;
   for (int b = 0; b < nb_; ++b) {
-    slot_dev_.push_back(dalloc<uint8_t>(L_.bytes));
-    HIPCHECK(hipMemset(slot_dev_.back(), 0, L_.bytes));
+    in_dev_.push_back(dalloc<uint8_t>(in_bytes_));
+    HIPCHECK(hipMemset(in_dev_.back(), 0, in_bytes_));
     void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, L_.bytes, hipHostMallocDefault));
-    std::memset(h, 0, L_.bytes);
-    slot_host_.push_back(static_cast<uint8_t*>(h));
+    HIPCHECK(hipHostMalloc(&h, head, hipHostMallocDefault));
+    std::memset(h, 0, head);
+    head_host_.push_back(static_cast<uint8_t*>(h));
+    staging_.push_back(nullptr);  // pinned staging is allocated on first use (unregistered rings only)
     packet_dev_.push_back(dalloc<double>(kPacketLen));
     HIPCHECK(hipMemset(packet_dev_.back(), 0, kPacketLen * sizeof(double)));
     HIPCHECK(hipHostMalloc(&h, kPacketLen * sizeof(double), hipHostMallocDefault));
@@ -162,8 +159,10 @@ void WindowEngine::alloc() {
   }
   warm_.assign(nb_, false);
   // per-incident results block: [post G*16 f64][gconf G f64][feat G*16 f32][pred G i32][evbits G*16 u32]
+  // [sli G*2 u32]
   const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
-  res_bytes_ = o_ev + 16 * G * 4;
+  const size_t o_sli = o_ev + 16 * G * 4;
+  res_bytes_ = o_sli + 2 * G * 4;
   for (int b = 0; b < nb_; ++b) {
     void* h = nullptr;
     HIPCHECK(hipHostMalloc(&h, res_bytes_, hipHostMallocDefault));
@@ -177,7 +176,28 @@ void WindowEngine::alloc() {
   feat_ = reinterpret_cast<float*>(r + o_feat);
   pred_ = reinterpret_cast<int32_t*>(r + o_pred);
   evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
+  sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
   HIPCHECK(hipMemset(r, 0, res_bytes_));
+  // pod metadata, ring accounting, the two-generation trace map
+  pod_sn_ = dalloc<uint32_t>(kPodRows);
+  HIPCHECK(hipMemset(pod_sn_, 0, kPodRows * 4));
+  {
+    void* h = nullptr;
+    HIPCHECK(hipHostMalloc(&h, kPodRows * 4, hipHostMallocDefault));
+    std::memset(h, 0, kPodRows * 4);
+    pod_host_ = static_cast<uint32_t*>(h);
+    HIPCHECK(hipHostMalloc(&h, 64, hipHostMallocDefault));
+    std::memset(h, 0, 64);
+    trace_cur_host_ = static_cast<uint32_t*>(h);
+  }
+  ring_state_ = dalloc<uint32_t>(kRsLen);
+  trace_cur_ = dalloc<uint32_t>(16);
+  HIPCHECK(hipMemset(trace_cur_, 0, 64));
+  for (int g = 0; g < 2; ++g) {
+    trace_key_[g] = dalloc<unsigned long long>(kTraceSlots);
+    trace_val_[g] = dalloc<uint32_t>(kTraceSlots);
+    HIPCHECK(hipMemset(trace_key_[g], 0, kTraceSlots * 8));
+  }
   // context table: every id the kernel or the host encoder can assign, HBM-resident
   ctx_tab_ = dalloc<uint32_t>((size_t)kCtxRows * 4);
   HIPCHECK(hipMemset(ctx_tab_, 0, (size_t)kCtxRows * 16));
@@ -236,17 +256,23 @@ WindowEngine::~WindowEngine() {
   auto evs = {&h2d_done_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
   for (auto* v : evs)
     for (auto e : *v) hipEventDestroy(e);
-  for (auto p : slot_host_) hipHostFree(p);
+  for (auto& r : registered_) hipHostUnregister(const_cast<uint8_t*>(r.first));
+  for (auto p : head_host_) hipHostFree(p);
+  for (auto p : staging_)
+    if (p) hipHostFree(p);
+  if (pod_host_) hipHostFree(pod_host_);
+  if (trace_cur_host_) hipHostFree(trace_cur_host_);
   for (auto p : packet_host_) hipHostFree(p);
   for (auto p : res_host_) hipHostFree(p);
   for (auto p : model_host_) hipHostFree(p);
-  for (auto p : slot_dev_) hipFree(p);
+  for (auto p : in_dev_) hipFree(p);
   for (auto p : packet_dev_) hipFree(p);
   for (auto p : res_dev_) hipFree(p);
   void* bufs[] = {ctx_tab_, totals_, stats_acc_, p0_, model_dev_, g_status_, g_part_, g_part_blk_, g_part_off_,
                   g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
                   s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
-                  hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_};
+                  hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_cur_,
+                  trace_key_[0], trace_key_[1], trace_val_[0], trace_val_[1]};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_) hipStreamDestroy(copy_);
@@ -257,15 +283,66 @@ WindowEngine::~WindowEngine() {
 SignalCols WindowEngine::sig_cols() const { return SignalCols{g_rec_, g_status_, g_part_}; }
 SpanCols WindowEngine::span_cols() const { return SpanCols{s_rec_, s_part_}; }
 
-void WindowEngine::wait_slot(int64_t k) {
-  if (k >= nb_) HIPCHECK(hipEventSynchronize(h2d_done_[k % nb_]));
+bool WindowEngine::register_host(const void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return false;
+  if (registered(ptr, bytes)) return true;
+  if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  registered_.emplace_back(static_cast<const uint8_t*>(ptr), bytes);
+  return true;
 }
+
+bool WindowEngine::registered(const void* p, size_t n) const {
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  for (const auto& r : registered_)
+    if (q >= r.first && q + n <= r.first + r.second) return true;
+  return false;
+}
+
+// DMA a window's segments of one kind back to back into dst (device); unregistered segments go
+// through pinned staging (one host memcpy, then the DMA). Returns the bytes placed.
+size_t WindowEngine::dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap, uint8_t*& staging, size_t& st_off) {
+  size_t off = 0;
+  for (const Seg& s : segs) {
+    if (!s.bytes) continue;
+    if (off + s.bytes > cap) throw std::invalid_argument("window input exceeds the engine's capacity");
+    const void* src = s.ptr;
+    if (!registered(s.ptr, s.bytes)) {
+      if (!staging) {
+        void* h = nullptr;
+        HIPCHECK(hipHostMalloc(&h, in_bytes_ - off_kern_, hipHostMallocDefault));
+        staging = static_cast<uint8_t*>(h);
+      }
+      std::memcpy(staging + st_off, s.ptr, s.bytes);
+      src = staging + st_off;
+      st_off += s.bytes;
+      staged_bytes_ += s.bytes;
+    } else {
+      direct_bytes_ += s.bytes;
+    }
+    HIPCHECK(hipMemcpyAsync(dst + off, src, s.bytes, hipMemcpyHostToDevice, copy_));
+    off += s.bytes;
+  }
+  return off;
+}
+
+bool WindowEngine::h2d_done(int64_t k) {
+  const hipError_t e = hipEventQuery(h2d_done_[k % nb_]);
+  if (e == hipSuccess) return true;
+  if (e == hipErrorNotReady) return false;
+  HIPCHECK(e);
+  return false;
+}
+
+void WindowEngine::wait_h2d(int64_t k) { HIPCHECK(hipEventSynchronize(h2d_done_[k % nb_])); }
 
 // The captured part of a window: everything between the DMA and the packet.
 void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, hipStream_t st) {
-  uint8_t* slot = slot_dev_[b];
-  const int* counts = reinterpret_cast<const int*>(slot);
-  const int32_t* labels = reinterpret_cast<const int32_t*>(slot + 64);
+  uint8_t* in = in_dev_[b];
+  const int* counts = reinterpret_cast<const int*>(in);
+  const int32_t* labels = reinterpret_cast<const int32_t*>(in + kHeadBytes);
   const int N = cfg_.sig_cap, S = cfg_.span_cap, G = cfg_.group_cap;
   FillList fl{};
   auto add = [&](void* p, size_t bytes, uint32_t v) { fl.seg[fl.count++] = FillSeg{(uint32_t*)p, (uint32_t)(bytes / 4), v}; };
@@ -280,13 +357,20 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
   add(cnt_, (size_t)S * 4, 0);
   add(gsum_, (size_t)kGroupStripes * G * kSlots * 8, 0);
   add(gcnt_, (size_t)kGroupStripes * G * kSlots * 4, 0);
+  add(sli_, (size_t)G * 2 * 4, 0);
   hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, st, fl);
-  hipLaunchKernelGGL(k_apply_rows, dim3(64), dim3(256), 0, st, slot, L_.ev_off, reinterpret_cast<uint4*>(ctx_tab_),
-                     kCtxRows);
-  launch_decode_wire(slot + L_.ev_off, counts, N, ctx_tab_, (int)kCtxRows, sig_cols(), hist_, status_, g_part_blk_,
-                     misc_, st);
+  FillList rs{};
+  rs.seg[0] = FillSeg{ring_state_, 1, 0xFFFFFFFFu};  // first busy record: none
+  rs.seg[1] = FillSeg{ring_state_ + 1, kRsLen - 1, 0};
+  rs.count = 2;
+  hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, rs);
+  const TraceTab tt{{trace_key_[0], trace_key_[1]}, {trace_val_[0], trace_val_[1]}, trace_cur_, kTraceSlots - 1};
+  launch_ring_defs(in + off_kern_, counts, N, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
+  launch_decode_window(in + off_kern_, in + off_user_, counts, N, ctx_tab_, (int)kCtxRows, tt, ring_state_, sig_cols(),
+                       hist_, status_, g_part_blk_, misc_, st);
   launch_partition(g_part_, counts, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
-  launch_decode_spans(slot + L_.sp_off, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st);
+  const SpanMap sm{tt, sli_, G, cfg_.ttft_slo_ms};
+  launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
   launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), g_items_, g_part_base_, N, S, jp_, top3_, cnt_,
@@ -301,26 +385,52 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
     launch_posterior(feat_, counts + 2, G, pm, with_labels ? labels : nullptr, post_, pred_, gconf_, evbits_,
                      confusion_, st);
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
-                     stats_, stats_count_, packet_dev_[b]);
+                     stats_, stats_count_, ring_state_, packet_dev_[b]);
 }
 
-void WindowEngine::submit(int64_t k, size_t dma_bytes, int n_groups, bool with_labels, bool learn) {
+void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bool learn) {
   const auto t0 = std::chrono::steady_clock::now();
   if (k != submitted_) throw std::invalid_argument("windows must be submitted in order");
+  const int n_groups = in.n_groups;
   if (n_groups < 0 || n_groups > cfg_.group_cap) throw std::invalid_argument("n_groups exceeds group capacity");
-  if (dma_bytes < L_.ev_off || dma_bytes > L_.bytes) throw std::invalid_argument("dma_bytes outside the slot");
-  // the host checks what the kernels will assume before launching them
-  const int32_t* c = reinterpret_cast<const int32_t*>(slot_host_[k % nb_]);
-  if (c[0] < 0 || c[0] > cfg_.sig_cap || c[1] < 0 || c[1] > cfg_.span_cap || c[2] != n_groups || c[14] < 0 ||
-      slot_dma_bytes(L_, (uint32_t)c[0], (uint32_t)c[14]) > dma_bytes)
-    throw std::invalid_argument("slot counts inconsistent with the window (events/spans/groups/rows/dma bytes)");
+  size_t kb = 0, ub = 0, sb = 0;
+  for (const Seg& s : in.kernel) kb += s.bytes;
+  for (const Seg& s : in.user) ub += s.bytes;
+  for (const Seg& s : in.spans) sb += s.bytes;
+  // what the kernels will assume, checked on the host before anything is queued
+  if (kb % kRecStride || ub % 64 || sb % 64) throw std::invalid_argument("segments must hold whole records");
+  const size_t n_k = kb / kRecStride, n_u = ub / 64, n_s = sb / 64;
+  if (n_k + n_u > (size_t)cfg_.sig_cap || n_u > (size_t)cfg_.user_cap || n_s > (size_t)cfg_.span_cap)
+    throw std::invalid_argument("window exceeds the engine's capacity (events / user records / spans)");
   const int b = (int)(k % nb_);
   // host back-pressure: at most max_ahead windows queued beyond the one computing
   if (k >= max_ahead_) HIPCHECK(hipEventSynchronize(compute_done_[(k - max_ahead_) % nb_]));
-  // DMA of the input block once window k - nb (the device block's previous reader) computed
+  // the pinned head / staging of buffer b were last read by the DMAs of window k - nb
+  if (k >= nb_) HIPCHECK(hipEventSynchronize(h2d_done_[b]));
+  int32_t* c = reinterpret_cast<int32_t*>(head_host_[b]);
+  std::memset(c, 0, kHeadBytes);
+  c[0] = (int32_t)(n_k + n_u);
+  c[1] = (int32_t)n_s;
+  c[2] = n_groups;
+  c[4] = (int32_t)(uint32_t)(uint64_t)in.bases[0];
+  c[5] = (int32_t)(uint32_t)((uint64_t)in.bases[0] >> 32);
+  c[7] = 64;  // 64-byte spans
+  for (int q = 1; q < 4; ++q) {
+    c[8 + 2 * (q - 1)] = (int32_t)(uint32_t)(uint64_t)in.bases[q];
+    c[9 + 2 * (q - 1)] = (int32_t)(uint32_t)((uint64_t)in.bases[q] >> 32);
+  }
+  c[15] = (int32_t)n_k;
+  int32_t* lab = reinterpret_cast<int32_t*>(head_host_[b] + kHeadBytes);
+  for (int g = 0; g < cfg_.group_cap; ++g) lab[g] = (in.labels && g < n_groups) ? in.labels[g] : -1;
+  // DMAs once window k - nb (the device block's previous reader) computed
   HIPCHECK(hipStreamWaitEvent(copy_, compute_done_[b], 0));
   HIPCHECK(hipEventRecord(t_start_[b], copy_));
-  HIPCHECK(hipMemcpyAsync(slot_dev_[b], slot_host_[b], dma_bytes, hipMemcpyHostToDevice, copy_));
+  uint8_t* dst = in_dev_[b];
+  HIPCHECK(hipMemcpyAsync(dst, head_host_[b], off_kern_, hipMemcpyHostToDevice, copy_));
+  size_t st_off = 0;
+  dma(in.kernel, dst + off_kern_, (size_t)kRecStride * cfg_.sig_cap, staging_[b], st_off);
+  dma(in.user, dst + off_user_, 64 * (size_t)cfg_.user_cap, staging_[b], st_off);
+  dma(in.spans, dst + off_span_, 64 * (size_t)cfg_.span_cap, staging_[b], st_off);
   HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
@@ -385,9 +495,10 @@ ResultView WindowEngine::results(int64_t k) const {
   const uint8_t* r = res_host_[k % nb_];
   const size_t G = cfg_.group_cap;
   const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
+  const size_t o_sli = o_ev + 16 * G * 4;
   return ResultView{reinterpret_cast<const double*>(r), reinterpret_cast<const double*>(r + o_gconf),
                     reinterpret_cast<const float*>(r + o_feat), reinterpret_cast<const int32_t*>(r + o_pred),
-                    reinterpret_cast<const uint32_t*>(r + o_ev)};
+                    reinterpret_cast<const uint32_t*>(r + o_ev), reinterpret_cast<const uint32_t*>(r + o_sli)};
 }
 
 std::pair<float, float> WindowEngine::window_ms(int64_t k) {
@@ -409,6 +520,25 @@ void WindowEngine::set_model_bytes(const void* bytes, size_t n) {
 
 void WindowEngine::set_p0(const double* p0) {
   HIPCHECK(hipMemcpy(p0_, p0, kSlots * 16 * sizeof(double), hipMemcpyHostToDevice));
+}
+
+void WindowEngine::set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n) {
+  // the host mirror is only written between the previous upload's completion (compute stream
+  // order: the upload precedes later windows) and this call; uploads are rare (pod churn)
+  HIPCHECK(hipStreamSynchronize(compute_));
+  for (size_t i = 0; i < n; ++i)
+    if (pods[i] < kPodRows) pod_host_[pods[i]] = svcnode[i];
+  HIPCHECK(hipMemcpyAsync(pod_sn_, pod_host_, kPodRows * 4, hipMemcpyHostToDevice, compute_));
+}
+
+void WindowEngine::rotate_traces() {
+  // the older generation is cleared and becomes current (stream-ordered between windows);
+  // mappings live for one to two rotation periods
+  HIPCHECK(hipStreamSynchronize(compute_));
+  const uint32_t next = trace_cur_host_[0] ^ 1u;
+  HIPCHECK(hipMemsetAsync(trace_key_[next], 0, kTraceSlots * 8, compute_));
+  trace_cur_host_[0] = next;
+  HIPCHECK(hipMemcpyAsync(trace_cur_, trace_cur_host_, 4, hipMemcpyHostToDevice, compute_));
 }
 
 void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {

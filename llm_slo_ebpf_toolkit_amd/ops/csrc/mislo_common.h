@@ -193,4 +193,46 @@ __host__ __device__ inline unsigned long long milli_units(float v) {
 
 __host__ __device__ inline int part_of(uint64_t h) { return (int)(h >> (64 - kPartBits)); }
 
+// ---- BPF ring records on the device ---------------------------------------------------------
+// The native engine DMAs the BPF ring's bytes as they are: 8-byte header {len | busy | discard,
+// pg_off} + 16-byte payload per record (runtime/csrc/bpfring.h), i.e. a 24-byte stride.
+constexpr uint32_t kRbBusy = 1u << 31, kRbDiscard = 1u << 30;
+constexpr int kRecStride = 24;
+constexpr uint32_t kDefTrace = 0xFD, kDefCtx = 0xFE, kDefFirst = 0xF0;
+// per-window ring accounting (device, packed into the packet): first busy record (min), records
+// of another size, context / trace definitions applied, discarded records, user-space records
+enum RingState { kRsFirstBusy = 0, kRsForeign, kRsDefCtx, kRsDefTrace, kRsDiscard, kRsEvents, kRsLen = 8 };
+
+// the 32-bit connection identity of context rows (runtime/csrc/records.h conn32)
+__host__ __device__ inline uint32_t conn32(uint64_t key) {
+  return key ? ((uint32_t)(key ^ (key >> 32)) | 1u) : 0u;
+}
+
+// Device trace map: trace hash -> the kernel's trace id (from the probes' TRACE definitions),
+// two generations (lookups try both; inserts go to the current one; the host retires the
+// older one). User-space records and spans carry trace HASHES: a hash the kernel named maps
+// to its id, so they join the kernel's records exactly; any other hash keeps its own value
+// with bit 63 set, disjoint from the kernel's 30-bit ids.
+struct TraceTab {
+  unsigned long long* key[2];  // 0 = empty slot
+  uint32_t* val[2];
+  const uint32_t* cur;         // device word: current generation (0 / 1)
+  uint32_t mask;               // slots per generation - 1
+};
+
+__device__ inline uint64_t trace_key(const TraceTab& t, uint64_t h) {
+  if (!h) return 0;
+  const uint32_t c = *t.cur & 1u;
+  for (int q = 0; q < 2; ++q) {
+    const uint32_t g = q ? c ^ 1u : c;
+    uint32_t i = (uint32_t)splitmix64(h) & t.mask;
+    for (int probe = 0; probe < 64; ++probe, i = (i + 1) & t.mask) {
+      const unsigned long long k = t.key[g][i];
+      if (k == h) return t.val[g][i];
+      if (k == 0) break;
+    }
+  }
+  return h | (1ull << 63);
+}
+
 }  // namespace mislo

@@ -34,8 +34,24 @@ void launch_decode_wire(const void* ev, const int* n_dev, int cap, const uint32_
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,
                        const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                        unsigned long long* misc, hipStream_t stream);
+// spans: SPAN20 (counts[7] == 20) or 64-byte SPAN; sm (optional, native engine): translate
+// trace hashes through the device trace map, fold connections to conn32, count per-group TTFT
+// SLO breaches
+struct SpanMap {
+  TraceTab tt;           // tt.key[0] == nullptr: no translation
+  uint32_t* grp_sli;     // [n_groups][2]: spans, TTFT > slo
+  int n_groups;
+  float ttft_slo_ms;
+};
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
-                         const uint32_t* ctx_tab, int n_ctx, hipStream_t stream);
+                         const uint32_t* ctx_tab, int n_ctx, hipStream_t stream, const SpanMap* sm = nullptr);
+// native engine window: framed BPF ring records (counts[15] of them) + 64-byte user records
+void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t* ctx_tab, uint32_t ctx_rows,
+                      const uint32_t* pod_sn, uint32_t n_pods, const TraceTab& tt, uint32_t* ring_state,
+                      hipStream_t stream);
+void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, int cap, const uint32_t* ctx_tab,
+                          int n_ctx, const TraceTab& tt, uint32_t* ring_state, const SignalCols& cols, uint32_t* hist,
+                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream);
 
 // join.hip
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,

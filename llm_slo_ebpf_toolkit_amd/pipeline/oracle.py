@@ -110,6 +110,65 @@ def decode_w16(ev: np.ndarray, table: CtxTable, bases) -> Decoded:
                    row[:, 2].astype(np.uint64))
 
 
+class TraceMap:
+    """Host mirror of the engine's device trace map (mislo_common.h TraceTab): the probes' TRACE
+    definitions name hashes; any other hash keeps its value with bit 63 set."""
+
+    def __init__(self):
+        self.m: Dict[int, int] = {}
+
+    def key(self, h: int) -> int:
+        h = int(h)
+        return 0 if h == 0 else self.m.get(h, h | (1 << 63))
+
+    def keys(self, hs: np.ndarray) -> np.ndarray:
+        return np.array([self.key(h) for h in np.asarray(hs).tolist()], dtype=np.uint64)
+
+
+def apply_ring_defs(framed: np.ndarray, table: CtxTable, tmap: TraceMap, pod_sn: Dict[int, int]) -> None:
+    """k_ring_defs: context rows (svc|node from pod metadata) and trace ids of a framed window."""
+    r = np.ascontiguousarray(framed).view(np.uint32).reshape(-1, 6)
+    ok = r[:, 0] == 16
+    p = r[ok, 2:6]
+    t = p[:, 1] & 0xFF
+    for c32, ct, pod, pid in p[t == records.DEF_CTX].tolist():
+        table.map[ct >> 8] = (pod, pid, c32, pod_sn.get(pod, 0))
+    for tid, _ct, lo, hi in p[t == records.DEF_TRACE].tolist():
+        tmap.m[lo | (hi << 32)] = tid
+
+
+def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases) -> Decoded:
+    """k_decode_window: rows [0, n framed) from the framed ring records (definitions, discarded
+    and busy records are holes: ts 0, no slot), then the user-space 64-byte records with
+    translated trace ids and conn32 connections."""
+    r = np.ascontiguousarray(framed).view(np.uint32).reshape(-1, 6)
+    n_k = r.shape[0]
+    ev = r[:, 2:6].copy().view(records.EVENT16).reshape(-1)
+    valid = (r[:, 0] == 16) & ((ev["ctx_type"] & np.uint32(0xFF)) < records.DEF_FIRST)
+    d = decode_w16(ev, table, bases)
+    hole = ~valid
+    for f, z in (("ts", 0), ("val", 0), ("slot", NO_SLOT), ("status", 0), ("pod", 0), ("pid", 0), ("svcnode", 0),
+                 ("trace", 0), ("conn", 0)):
+        getattr(d, f)[hole] = z
+    u = decode_events(user) if len(user) else None
+    if u is None:
+        return d
+    u.trace = tmap.keys(user["trace_h"])
+    u.conn = records.conn32_np(u.conn).astype(np.uint64)
+    cat = lambda a, b: np.concatenate([a, b])  # noqa: E731
+    assert n_k == len(d.ts)
+    return Decoded(cat(d.ts, u.ts), cat(d.val, u.val), cat(d.slot, u.slot), cat(d.status, u.status), cat(d.pod, u.pod),
+                   cat(d.pid, u.pid), cat(d.svcnode, u.svcnode), cat(d.trace, u.trace), cat(d.conn, u.conn))
+
+
+def spans_native(spans: np.ndarray, tmap: TraceMap) -> np.ndarray:
+    """k_decode_spans in the native engine: trace hashes through the trace map, conn32."""
+    out = spans.copy()
+    out["trace_h"] = tmap.keys(spans["trace_h"])
+    out["conn_h"] = records.conn32_np(spans["conn_h"])
+    return out
+
+
 def decode_span20(sp: np.ndarray, table: CtxTable) -> np.ndarray:
     """k_decode_spans on SPAN20 records, as 64-byte SPAN records for ``join``."""
     row = table.rows(sp["ctx_id"].astype(np.int64))

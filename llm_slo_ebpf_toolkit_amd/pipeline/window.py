@@ -1,21 +1,24 @@
-"""Per-GPU window pipeline: the agent's window sources feeding the native window engine.
+"""Per-GPU window pipeline: the agent's rings feeding the native window engine, zero-copy.
 
-The per-window path has no Python per event and no PyTorch at all:
+The agent's CPU never reads, rewrites or re-encodes a record:
 
-* a window SOURCE closes the window (publishes the next epoch into ``mislo_cfg``, snapshots the
-  ring positions: the cut) and its native ``WindowAssembler`` (runtime/csrc/assemble.h)
-  compacts the BPF ring's EVENT16 records up to the cut into the pinned input block of the
-  window's engine buffer, applies the probes' id definitions, encodes user-space producers'
-  64-byte records and the window's spans, and writes the context-row patch and the counts;
-* the native ``WindowEngine`` (ops/csrc/engine.h) DMAs the block in one copy and replays the
-  buffer's captured HIP graph (decode -> LDS join -> MFMA posterior/statistics -> pack) on the
-  compute stream, while the RCCL all-reduce of the previous window's packed statistics runs on
-  the comm stream; the learned model refits on the device (prequential, lag = buffers).
+* the window SOURCE closes a window (publishes the next epoch into ``mislo_cfg``, then
+  snapshots the rings' producer positions: the cut) and hands the engine byte RANGES: the BPF
+  ring buffer's framed records since the last cut (one contiguous range thanks to the ring's
+  double mapping), the user-space producers' 64-byte records and the spans (<= 2 ranges each);
+* the native ``WindowEngine`` (ops/csrc/engine.h) DMAs those ranges straight from the
+  page-locked rings into HBM and replays the buffer's captured HIP graph: ring definitions
+  (context rows, trace map) -> decode of framed + user records -> LDS join -> MFMA
+  posterior/statistics -> pack, while the RCCL all-reduce of the previous window's packed
+  statistics runs on the comm stream; the learned model refits on the device (prequential);
+* ring space is freed once the DMA that read it has completed (user / span rings) or once
+  the window's results say no record in it was still being written (the BPF ring: a record
+  the GPU found busy is re-submitted with the next window, exactly once).
 
 ``WindowPipeline`` is the Python handle on the engine (model upload, totals, results);
-``RingWindowSource`` is the kernel-ring source (a pinned BPF ring buffer map, or the
-shared-memory emulation tests and the benchmark use); ``build_replay_images`` turns seeded
-fault-replay windows into the bytes the probes would have written (native probe model).
+``RingWindowSource`` the ring source (a pinned BPF ring buffer map, or the shared-memory
+emulation tests and the benchmark use); ``build_replay_images`` turns seeded fault-replay
+windows into the bytes the probes would have written (native probe model).
 """
 
 from __future__ import annotations
@@ -31,14 +34,16 @@ from ..collector import records
 from ..models.bayes import LDA, N_DOMAINS, NaiveBayes, SufficientStats
 from ..models.metrics import macro_f1_from_confusion
 
-PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16)  # hist, status, misc(+16 value sums), dbg, confusion, stats, count
-ROW_CAP = 1 << 17
+# hist, status, misc(+16 value sums), dbg, confusion, stats, count, ring accounting
+PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16, 8)
+RING_FIELDS = ("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events")
+USER_CAP = 1 << 18
 
 
 def unpack_packet(p: np.ndarray) -> Dict[str, np.ndarray]:
     o = 0
     out = {}
-    for name, n in zip(("hist", "status", "misc", "dbg", "confusion", "stats", "count"), PACKET_LAYOUT):
+    for name, n in zip(("hist", "status", "misc", "dbg", "confusion", "stats", "count", "ring"), PACKET_LAYOUT):
         out[name] = p[o:o + n]
         o += n
     out["hist"] = out["hist"].reshape(16, 16)
@@ -46,6 +51,7 @@ def unpack_packet(p: np.ndarray) -> Dict[str, np.ndarray]:
     out["confusion"] = out["confusion"].reshape(16, 16)
     out["stats"] = out["stats"].reshape(32, 32)
     out["value_sum"] = out["misc"][2:18] * 1e-3  # per-slot sums of decoded values (output units)
+    out["ring_state"] = {k: int(v) for k, v in zip(RING_FIELDS, out["ring"][:len(RING_FIELDS)])}
     return out
 
 
@@ -67,6 +73,7 @@ def summarize(p: np.ndarray) -> Dict[str, object]:
         "status": u["status"].astype(np.int64),
         "dbg": u["dbg"].astype(np.int64),
         "misc": u["misc"].astype(np.int64),
+        "ring": u["ring"].astype(np.int64),
         "stats": stats_from_packet(u),
     }
 
@@ -78,7 +85,7 @@ class WindowPipeline:
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, comm=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, use_graphs: bool = True,
-                 max_ahead: int = 3, n_buffers: int = 3, row_cap: int = ROW_CAP):
+                 max_ahead: int = 3, n_buffers: int = 3, user_cap: int = USER_CAP, ttft_slo_ms: float = 800.0):
         from ..ops import load_agent
         from ..ops.engine import model_bytes
 
@@ -88,14 +95,14 @@ class WindowPipeline:
         self.model_name, self.seed, self.learn = model, seed, learn
         self.device_refit = learn and model == "bayes_learned"
         self._model_bytes = model_bytes
+        user_cap = max(1, min(int(user_cap), int(sig_cap)))
         self.eng = self.mod.WindowEngine(device=device, sig_cap=sig_cap, span_cap=span_cap, group_cap=group_cap,
-                                         row_cap=row_cap, n_buffers=n_buffers, max_ahead=max_ahead,
+                                         user_cap=user_cap, n_buffers=n_buffers, max_ahead=max_ahead,
                                          window_ms=window_ms, threshold=threshold, fanout=fanout,
                                          group_mode=group_mode, use_graphs=use_graphs,
-                                         device_refit=self.device_refit, n_dom=N_DOMAINS)
+                                         device_refit=self.device_refit, n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms)
         self.nb = self.eng.buffers
-        self.layout = self.eng.layout
-        self.sig_cap, self.span_cap, self.group_cap, self.row_cap = sig_cap, span_cap, group_cap, row_cap
+        self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
         if comm is not None and comm[2] > 1:
             self.eng.init_comm(comm[0], comm[1], comm[2])
         p0 = np.zeros((16, 16), dtype=np.float64)
@@ -113,17 +120,15 @@ class WindowPipeline:
         return NaiveBayes.learned(SufficientStats(), seed=self.seed)
 
     # ---- per window -----------------------------------------------------------------------
-    def slot(self, k: Optional[int] = None) -> int:
-        """Address of the pinned input block of window ``k`` (default: the next one), after
-        waiting until its previous reader's DMA is done."""
-        k = self.k if k is None else k
-        self.eng.wait_slot(k)
-        return self.eng.host_slot(k)
-
-    def submit(self, dma_bytes: int, n_groups: int, with_labels: bool = True, learn: Optional[bool] = None) -> int:
+    def submit(self, kernel, user, spans, n_groups: int, labels=None, bases=(0, 0, 0, 0), with_labels: bool = True,
+               learn: Optional[bool] = None) -> int:
+        """Queue the next window: ``kernel`` / ``user`` / ``spans`` = [(host address, bytes)] ranges
+        of framed ring records / 64-byte records / 64-byte spans. Returns its index."""
         k = self.k
         learn = (self.learn and with_labels) if learn is None else learn
-        self.eng.submit(k, int(dma_bytes), int(n_groups), bool(with_labels), bool(learn))
+        lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.int32)
+        self.eng.submit(k, list(kernel), list(user), list(spans), int(n_groups), lab, [int(b) for b in bases],
+                        bool(with_labels), bool(learn))
         self.k += 1
         if self.learn and not self.device_refit and k >= 2:
             self._host_refit(k - 2)  # window k-2 is done or nearly (k-1 would stall the host)
@@ -200,35 +205,44 @@ class Cut:
 
 
 class RingWindowSource:
-    """Kernel-ring window source: consumes the BPF ring buffer (``ring``: a pinned map opened
-    with Ringbuf.open_pinned, or an emulated one), optional user-space event and span rings,
-    through the native tables and assembler into a WindowPipeline's input blocks.
+    """Ring window source: the BPF ring buffer (``ring``: a pinned map opened with
+    Ringbuf.open_pinned, or an emulated one) plus the optional user-space event and span rings,
+    handed to a WindowPipeline as DMA ranges.
 
     ``cut()`` is the live protocol (the agent is the clock): publish epoch k into mislo_cfg
     (``cfg_set``: the emulated array, or the real map's BpfMap update), then snapshot every
     ring's producer position; records a probe stamps from then on carry the new tag, records
     stamped before it keep theirs and decode against the bases the window ships."""
 
-    def __init__(self, pipe: WindowPipeline, ring=None, user_ring=None, span_ring=None, threads: int = 8,
-                 cfg_set=None, tables=None):
+    def __init__(self, pipe: WindowPipeline, ring=None, user_ring=None, span_ring=None, cfg_set=None):
         from ..runtime import load
 
         self.rt = load()
         self.pipe = pipe
         self.ring, self.user_ring, self.span_ring = ring, user_ring, span_ring
-        self.tables = tables if tables is not None else records.native_tables()
-        self.consumer = self.rt.RingbufConsumer(ring, threads) if ring is not None else None
-        L = pipe.layout
-        self.asm = self.rt.WindowAssembler(pipe.group_cap, pipe.span_cap, pipe.sig_cap, pipe.row_cap, self.tables,
-                                           self.consumer, user_ring, span_ring)
-        self.clock = records.EpochClock()
         if cfg_set is None and ring is not None and getattr(ring, "emulated", False):
             cfg_set = lambda i, v: ring.cfg_set(i, v)  # noqa: E731
         self.cfg_set = cfg_set
-        self.last: Dict[str, object] = {}
+        self.clock = records.EpochClock()
+        # page-lock the rings so windows DMA straight from them (the double-mapped BPF ring data
+        # is registered whole: a window that wraps is still one range)
+        self.direct = {}
+        if ring is not None:
+            self.direct["ring"] = pipe.eng.register_host(ring.data_address, 2 * ring.size)
+            self.kpos = ring.consumer_pos
+            self.kmask = ring.size - 1
+        if user_ring is not None:
+            self.direct["user"] = pipe.eng.register_host(user_ring.address, user_ring.capacity * 64)
+            self.upos = user_ring.tail
+        if span_ring is not None:
+            self.direct["spans"] = pipe.eng.register_host(span_ring.address, span_ring.capacity * 64)
+            self.spos = span_ring.tail
+        self.pending: List[tuple] = []   # (k, kernel ranges [(pos, n)], user n, span n, h2d released)
+        self.late: List[tuple] = []      # kernel ranges a window found still being written
+        self.last: Dict[str, int] = {}
         self.host_s = 0.0
         self.n = 0
-        assert L["ev_off"] > 0
+        self.resubmitted = 0
 
     def publish_epoch(self, now_ns: Optional[int] = None) -> int:
         v = self.clock.publish(int(now_ns if now_ns is not None else time.time_ns()))
@@ -245,26 +259,113 @@ class RingWindowSource:
                    spans=self.span_ring.head if self.span_ring is not None else 0,
                    bases=self.clock.bases(), t_ns=t)
 
-    def stage(self, cut: Cut, n_groups: int, labels: Optional[np.ndarray] = None) -> Dict[str, object]:
-        """Assemble the window up to ``cut`` into the pipeline's next input block."""
+    # ---- ring space --------------------------------------------------------------------------
+    def reap(self, keep: Optional[int] = None) -> None:
+        """Free ring space of windows whose DMAs (user / span rings) or results (BPF ring) are in;
+        with ``keep``, first wait until at most ``keep`` windows are outstanding (a window's
+        packet is read before a later window's results overwrite its host buffer)."""
+        eng = self.pipe.eng
+        while self.pending and (eng.query(self.pending[0][0]) or (keep is not None and len(self.pending) > keep)):
+            k, ranges, nu, ns, released = self.pending.pop(0)
+            eng.wait(k)
+            if not released:
+                self._release_user(nu, ns)
+            fb = int(eng.packet(k)[sum(PACKET_LAYOUT[:7])])  # ring state: first busy record (-1 = none)
+            if fb >= 0:  # records from fb on were still being written: re-submit them
+                skip = fb
+                for pos, n in ranges:
+                    if skip >= n:
+                        skip -= n
+                        continue
+                    self.late.append((pos + 24 * skip, n - skip))
+                    self.resubmitted += n - skip
+                    skip = 0
+            if self.ring is not None and ranges:
+                done = max(self.ring.consumer_pos, max(p + 24 * n for p, n in ranges))
+                hold = min([p for p, _ in self.late], default=None)
+                self.ring.set_consumer_pos(min(hold, done) if hold is not None else done)
+        for e in self.pending:  # user / span ring space is free once the DMA that read it is done
+            if not e[4] and eng.h2d_done(e[0]):
+                self._release_user(e[2], e[3])
+                e[4] = True
+
+    def _release_user(self, nu: int, ns: int) -> None:
+        if self.user_ring is not None and nu:
+            self.user_ring.release(nu)
+        if self.span_ring is not None and ns:
+            self.span_ring.release(ns)
+
+    def _ring_ranges(self, start: int, stop: int, rec: int, base: int, cap_pos: int, max_n: int):
+        """[(address, bytes)] of records [start, stop) of a ring of ``cap_pos`` record slots."""
+        n = max(0, min(stop - start, max_n))
+        out, pos, left = [], start, n
+        while left:
+            idx = pos & (cap_pos - 1)
+            take = min(left, cap_pos - idx)
+            out.append((base + idx * rec, take * rec))
+            pos += take
+            left -= take
+        return out, n
+
+    def stage(self, cut: Cut, n_groups: int, labels: Optional[np.ndarray] = None, with_labels: Optional[bool] = None,
+              learn: Optional[bool] = None) -> Dict[str, int]:
+        """Submit the window up to ``cut``; returns what went in."""
         t0 = time.perf_counter()
-        slot = self.pipe.slot()
-        r = self.asm.assemble(slot, list(cut.bases), n_groups, labels, cut.kernel, cut.user, cut.spans)
+        pipe = self.pipe
+        self.reap(keep=pipe.nb - 1)
+        budget = pipe.sig_cap
+        k_ranges, kern = [], []
+        n_k = 0
+        if self.ring is not None:
+            late, self.late = self.late, []
+            for pos, n in late:
+                take = min(n, budget - n_k)
+                if take < n:
+                    self.late.append((pos + 24 * take, n - take))
+                if take:
+                    k_ranges.append((pos, take))
+                    kern.append((self.ring.data_address + (pos & self.kmask), 24 * take))
+                    n_k += take
+            span_b = cut.kernel - self.kpos
+            if span_b % 24:
+                raise RuntimeError("BPF ring holds records of another size (the probes emit 16-byte records only)")
+            take = min(span_b // 24, budget - n_k)
+            if take:  # one range: the data pages are mapped twice back to back
+                k_ranges.append((self.kpos, take))
+                kern.append((self.ring.data_address + (self.kpos & self.kmask), 24 * take))
+                n_k += take
+                self.kpos += 24 * take
+        user, n_u = [], 0
+        if self.user_ring is not None:
+            cap = self.user_ring.capacity
+            user, n_u = self._ring_ranges(self.upos, cut.user, 64, self.user_ring.address, cap,
+                                          min(pipe.user_cap, budget - n_k))
+            self.upos += n_u
+        spans, n_s = [], 0
+        if self.span_ring is not None:
+            spans, n_s = self._ring_ranges(self.spos, cut.spans, 64, self.span_ring.address, self.span_ring.capacity,
+                                           pipe.span_cap)
+            self.spos += n_s
+        wl = labels is not None if with_labels is None else with_labels
+        k = pipe.submit(kern, user, spans, n_groups, labels, cut.bases, with_labels=wl, learn=learn)
+        self.pending.append([k, k_ranges, n_u, n_s, False])
         self.host_s += time.perf_counter() - t0
         self.n += 1
-        self.last = r
-        return r
-
-    def group_sli(self) -> np.ndarray:
-        """[group_cap, 2] spans and TTFT-SLO breaches per incident group since the last call."""
-        return self.tables.take_group_sli(self.pipe.group_cap).astype(np.float64)
+        self.last = {"k": k, "n_kernel": n_k, "n_user": n_u, "n_spans": n_s, "n_events": n_k + n_u}
+        return self.last
 
     def step(self, n_groups: int, labels=None, cut: Optional[Cut] = None, with_labels: Optional[bool] = None) -> int:
-        """cut (live, unless given) -> assemble -> submit; returns the window index."""
+        """cut (live, unless given) -> submit; returns the window index."""
         c = cut if cut is not None else self.cut()
-        r = self.stage(c, n_groups, labels)
-        wl = labels is not None if with_labels is None else with_labels
-        return self.pipe.submit(r["dma_bytes"], n_groups, with_labels=wl)
+        return self.stage(c, n_groups, labels, with_labels)["k"]
+
+    def group_sli(self, k: int) -> np.ndarray:
+        """[groups, 2] spans and TTFT-SLO breaches per incident group of window k (device-counted)."""
+        return self.pipe.results(k, self.pipe.group_cap)["sli"].astype(np.float64)
+
+    def drain(self) -> None:
+        self.pipe.drain()
+        self.reap(keep=0)
 
 
 @dataclass

@@ -1,7 +1,7 @@
-// pybind11 module `_mislo_rt`: the agent's host runtime. Shared-memory MPSC rings for
+// pybind11 module `_mislo_rt`: the agent's host runtime (CPU only: no HIP runtime in this
+// module, so a process loads exactly one HIP runtime -- the engine's, or PyTorch's). Shared-memory MPSC rings for
 // user-space producers, the BPF ring buffer view / consumer / kernel-probe model, the agent's
 // id tables and window assembler, bpf(2) map access, paced replay producers.
-#include <hip/hip_runtime_api.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -85,7 +85,6 @@ class HostRing {
     if (!ring_) throw std::runtime_error("ring format failed");
   }
   ~HostRing() {
-    unpin();
     if (shm_) {
       mislo_ring_close(shm_);
       if (owner_) mislo_ring_unlink_shm(shm_name_.c_str());
@@ -93,17 +92,6 @@ class HostRing {
       delete ring_;
       free(mem_);
     }
-  }
-
-  bool pin() {
-    if (pinned_) return true;
-    const size_t n = ring_->capacity() * ring_->rec_size();
-    pinned_ = hipHostRegister(ring_->records(), n, hipHostRegisterPortable) == hipSuccess;
-    return pinned_;
-  }
-  void unpin() {
-    if (pinned_) (void)hipHostUnregister(ring_->records());
-    pinned_ = false;
   }
 
   uint64_t push(py::buffer b, int threads) {
@@ -130,7 +118,6 @@ class HostRing {
   uint64_t head() const { return ring_->header()->head.load(std::memory_order_acquire); }
   uint64_t tail() const { return ring_->header()->tail.load(std::memory_order_acquire); }
   uintptr_t address() const { return reinterpret_cast<uintptr_t>(ring_->records()); }
-  bool pinned() const { return pinned_; }
 
   py::array records_view() {
     return py::array(py::dtype("uint8"), {(py::ssize_t)(ring_->capacity() * ring_->rec_size())}, {(py::ssize_t)1},
@@ -158,7 +145,6 @@ class HostRing {
   void* mem_ = nullptr;
   size_t bytes_ = 0;
   Ring* ring_ = nullptr;
-  bool pinned_ = false;
   bool owner_ = true;
 };
 
@@ -542,8 +528,6 @@ PYBIND11_MODULE(_mislo_rt, m) {
   py::class_<HostRing>(m, "HostRing")
       .def(py::init<uint64_t, uint32_t, const std::string&, bool>(), py::arg("capacity") = 1, py::arg("rec_size") = 64,
            py::arg("shm_name") = "", py::arg("attach") = false)
-      .def("pin", &HostRing::pin)
-      .def("unpin", &HostRing::unpin)
       .def("push", &HostRing::push, py::arg("records"), py::arg("threads") = 1)
       .def("peek", &HostRing::peek)
       .def("release", &HostRing::release)
@@ -554,8 +538,7 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def_property_readonly("rec_size", &HostRing::rec_size)
       .def_property_readonly("head", &HostRing::head)
       .def_property_readonly("tail", &HostRing::tail)
-      .def_property_readonly("address", &HostRing::address)
-      .def_property_readonly("pinned", &HostRing::pinned);
+      .def_property_readonly("address", &HostRing::address);
   py::class_<PyReplayer>(m, "Replayer")
       .def(py::init<HostRing&, py::buffer, int64_t>(), py::arg("ring"), py::arg("trace"), py::arg("lap_ns"),
            py::keep_alive<1, 2>())
@@ -580,6 +563,7 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def("set_consumer_pos", &PyRingbuf::set_consumer_pos)
       .def("stats", &PyRingbuf::stats)
       .def_property_readonly("size", [](PyRingbuf& r) { return r.rb()->size(); })
+      .def_property_readonly("data_address", [](PyRingbuf& r) { return reinterpret_cast<uintptr_t>(r.rb()->data()); })
       .def_property_readonly("page", [](PyRingbuf& r) { return r.rb()->page(); })
       .def_property_readonly("emulated", [](PyRingbuf& r) { return r.rb()->emulated(); })
       .def_property_readonly("consumer_pos", [](PyRingbuf& r) { return r.rb()->consumer_pos(); })

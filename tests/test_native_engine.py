@@ -1,8 +1,8 @@
-"""Native window engine (ops/csrc/engine.hip, no PyTorch) fed by the kernel-ring path:
-probe model -> framed BPF ring records -> compacting consumer + id tables + window assembler ->
-one DMA -> captured HIP graph of decode / LDS join / MFMA posterior. Every window is checked
-against the numpy oracle run on exactly the bytes that crossed PCIe, and the join against the
-64-byte originals."""
+"""Native window engine (ops/csrc/engine.hip, no PyTorch) fed zero-copy from the rings: probe
+model -> framed BPF ring records -> page-locked ring -> DMA -> on-device definitions (context
+rows, trace map) -> decode of framed + user-space records -> LDS join -> MFMA posterior.
+Every window is checked against the numpy oracle run on exactly the ring bytes, and the join
+against the 64-byte originals; a record left busy in the ring is re-submitted exactly once."""
 
 import os
 
@@ -21,18 +21,15 @@ def windows(n_win=3, seed=31, n=6000, s=300, services=8):
     cfg = ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=services, events_per_window=n,
                        spans_per_window=s, seed=seed)
     g = ReplayGenerator(cfg)
-    return [g.next_window() for _ in range(n_win)]
+    return [g.next_window() for _ in range(n_win)], g
 
 
-def setup_source(pipe, tag, threads=4):
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource
+def rings(tag):
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    rb = rt.Ringbuf.create_shm(f"/mislo-gt-{os.getpid()}-{tag}", 1 << 22)
-    user = rt.HostRing(1 << 14, 64)
-    spans = rt.HostRing(1 << 12, 64)
-    return RingWindowSource(pipe, rb, user, spans, threads=threads), rb, user, spans
+    return (rt.Ringbuf.create_shm(f"/mislo-gt-{os.getpid()}-{tag}", 1 << 22), rt.HostRing(1 << 14, 64),
+            rt.HostRing(1 << 12, 64))
 
 
 def feed(img, rb, user, spans):
@@ -44,6 +41,11 @@ def feed(img, rb, user, spans):
     return Cut(kernel=rb.producer_pos, user=user.head, spans=spans.head, bases=img.bases)
 
 
+def pod_meta(gen):
+    sn = (gen.pod_svc.astype(np.uint32) << np.uint32(16)) | gen.pod_node.astype(np.uint32)
+    return gen.pod_ids.astype(np.uint32), sn
+
+
 def test_extension_is_native():
     from llm_slo_ebpf_toolkit_amd.ops import load_agent
 
@@ -52,41 +54,39 @@ def test_extension_is_native():
 
 
 def test_ring_windows_match_oracle():
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, build_replay_images
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
-    wins = windows()
+    wins, gen = windows()
     imgs = build_replay_images(wins)
-    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, row_cap=4096)
-    src, rb, user, spans = setup_source(pipe, "oracle")
-    for w in wins:
-        sn = (w.events["svc_id"].astype(np.uint32) << np.uint32(16)) | w.events["node_id"].astype(np.uint32)
-        src.tables.set_pods(w.events["pod_id"], sn)
-    table = oracle.CtxTable()
+    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096)
+    rb, user, spans = rings("oracle")
+    src = RingWindowSource(pipe, rb, user, spans)
+    assert all(src.direct.values())  # the rings are page-locked: DMA straight from them
+    pods, sn = pod_meta(gen)
+    pipe.eng.set_pods(pods, sn)
+    pod_sn = dict(zip(pods.tolist(), sn.tolist()))
+    table, tmap = oracle.CtxTable(), oracle.TraceMap()
     model = NaiveBayes.ref()
-    L = pipe.layout
     for w, img in zip(wins, imgs):
         cut = feed(img, rb, user, spans)
         r = src.stage(cut, w.n_groups, img.labels)
-        slot = pipe.eng.slot_view(pipe.k).copy()  # exactly what the DMA carries
-        k = pipe.submit(r["dma_bytes"], w.n_groups, with_labels=True, learn=False)
-        n, nr = r["n_events"], r["n_rows"]
-        ev = slot[L["ev_off"]:L["ev_off"] + 16 * n].view(R.EVENT16)
-        p = L["ev_off"] + 16 * n
-        ids = slot[p:p + 4 * nr].view(np.uint32)
-        q = p + (4 * nr + 15) // 16 * 16
-        table.add(ids, slot[q:q + 16 * nr].view(np.uint32).reshape(-1, 4))
-        d = oracle.decode_w16(ev, table, img.bases)
-        sp = oracle.decode_span20(slot[L["sp_off"]:L["sp_off"] + 20 * r["n_spans"]].view(R.SPAN20), table)
-        ref = oracle.join(d, sp, w.n_groups)
+        k = r["k"]
+        assert r["n_kernel"] * 24 == len(img.framed) and r["n_user"] == len(img.user)
+        oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
+        d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases)
+        ref = oracle.join(d, oracle.spans_native(img.spans, tmap), w.n_groups)
         pk = pipe.packet(k)
         res = pipe.results(k, w.n_groups)
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d))
         np.testing.assert_array_equal(pk["misc"][2:18].astype(np.int64), oracle.value_sums_milli(d))
-        dbg = {key: v for key, v in zip(("candidates", "low_raw", "overlap", "fanout_dropped", "spans_enriched"),
-                                          pk["dbg"][:5].astype(np.int64))}
-        assert dbg["candidates"] == ref.debug["candidates"]
-        assert dbg["fanout_dropped"] == ref.debug["fanout_dropped"]
-        assert dbg["spans_enriched"] == ref.debug["spans_enriched"]
+        assert pk["ring_state"]["first_busy"] == -1
+        fr = img.framed.view(np.uint32).reshape(-1, 6)
+        n_ev = int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
+        assert pk["ring_state"]["events"] == n_ev
+        dbg = dict(zip(("candidates", "low_raw", "overlap", "fanout_dropped", "spans_enriched"),
+                       pk["dbg"][:5].astype(np.int64).tolist()))
+        for key in ("candidates", "fanout_dropped", "spans_enriched"):
+            assert dbg[key] == ref.debug[key], key
         np.testing.assert_array_equal(res["feat"], ref.feat)
         feat = res["feat"].astype(np.float64)
         np.testing.assert_allclose(res["post"][:, :10], model.posteriors(feat), rtol=1e-9, atol=1e-12)
@@ -94,38 +94,82 @@ def test_ring_windows_match_oracle():
         conf = np.zeros((16, 16), dtype=np.int64)
         np.add.at(conf, (img.labels, res["pred"]), 1)
         np.testing.assert_array_equal(pk["confusion"].astype(np.int64), conf)
+        # per-incident TTFT SLO accounting (device-counted) == the spans
+        exp = np.zeros((w.n_groups, 2), dtype=np.int64)
+        np.add.at(exp[:, 0], w.spans["group_id"], 1)
+        np.add.at(exp[:, 1], w.spans["group_id"], (w.spans["ttft_ms"] > 800.0).astype(np.int64))
+        np.testing.assert_array_equal(res["sli"].astype(np.int64), exp)
         # the join on the 64-byte originals sees the same candidates
         full = oracle.join(oracle.decode_events(w.events), w.spans, w.n_groups)
         assert full.debug["candidates"] == ref.debug["candidates"]
         assert full.debug["spans_enriched"] == ref.debug["spans_enriched"]
         total, comp = pipe.window_ms(k)
         assert total > 0 and comp > 0
+    src.drain()
+    assert rb.consumer_pos == rb.producer_pos and user.size == 0 and spans.size == 0
+    assert pipe.eng.staged_bytes == 0 and pipe.eng.direct_bytes > 0
+
+
+def test_busy_record_is_resubmitted_exactly_once():
+    """A record still being written at the cut (busy bit) stops the GPU's decode of that window
+    there; the rest of the range is re-submitted with the next window and counted once."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, RingWindowSource, WindowPipeline
+
+    rb, user, spans = rings("busy")
+    pipe = WindowPipeline(4096, 64, 4, model="bayes", learn=False, user_cap=64)
+    src = RingWindowSource(pipe, rb, user, spans)
+    base = 1_700_000_000_000_000_000
+    rb.cfg_set(124, base)
+    ev = np.zeros(300, dtype=R.EVENT)
+    ev["signal_type"] = 1          # dns_latency_ms
+    ev["value"] = 5_000_000        # 5 ms
+    ev["ts_ns"] = base + np.arange(300) * 1000
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    sim = load().ProbeSim(rb, R.milli_shift_table())
+    sim.submit(ev[:100])
+    at = rb.reserve(16)            # a probe still writing record 100
+    sim.submit(ev[101:200])
+    k0 = src.stage(Cut(kernel=rb.producer_pos, user=0, spans=0, bases=(base, 0, 0, 0)), 4)["k"]
+    src.reap(keep=0)
+    assert pipe.packet(k0)["ring_state"]["first_busy"] == 100
+    assert pipe.packet(k0)["hist"].sum() == 100
+    assert rb.consumer_pos == 100 * 24 and src.resubmitted == 100
+    rb.write(at, sim.encode(ev[100:101]).reshape(-1))
+    rb.commit(at)
+    sim.submit(ev[200:300])
+    k1 = src.stage(Cut(kernel=rb.producer_pos, user=0, spans=0, bases=(base, 0, 0, 0)), 4)["k"]
+    src.drain()
+    assert pipe.packet(k1)["ring_state"]["first_busy"] == -1
+    assert pipe.packet(k1)["hist"].sum() == 200  # the 100 re-submitted + 100 new, each once
+    tot = pipe.summary()["hist"].sum()
+    assert tot == 300
+    assert rb.consumer_pos == rb.producer_pos
 
 
 def test_pipelined_learning_with_graphs_and_device_refit():
     """bayes_learned: graphs captured per buffer, the device refit folds window k-nb before
-    window k; totals equal the per-window packets; eager and graph runs agree."""
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline, build_replay_images
+    window k; eager and graph runs agree bit for bit."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
-    wins = windows(n_win=3, seed=37)
+    wins, gen = windows(n_win=3, seed=37)
     imgs = build_replay_images(wins)
     sums = []
     for graphs in (False, True):
-        pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", use_graphs=graphs, row_cap=4096)
-        src, rb, user, spans = setup_source(pipe, f"learn{graphs}")
-        packets = []
+        pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", use_graphs=graphs, user_cap=4096)
+        rb, user, spans = rings(f"learn{graphs}")
+        src = RingWindowSource(pipe, rb, user, spans)
+        pipe.eng.set_pods(*pod_meta(gen))
         for i in range(8):
             img = imgs[i % 3]
-            cut = feed(img, rb, user, spans)
-            r = src.stage(cut, img.n_groups, img.labels)
-            packets.append(pipe.submit(r["dma_bytes"], img.n_groups, with_labels=True))
+            src.stage(feed(img, rb, user, spans), img.n_groups, img.labels)
+        src.drain()
         summ = pipe.summary()
         assert summ["confusion"].sum() == 8 * imgs[0].n_groups
         assert pipe.windows_folded == 8 - pipe.nb
-        tot = sum(pipe.packet(k)["confusion"] for k in packets[-3:])  # last nb packets still resident
-        assert tot.sum() == 3 * imgs[0].n_groups
         if graphs:
             assert pipe.eng.graphs >= 3
         sums.append(summ)
+        pipe.eng.close()
     for key in ("confusion", "hist", "status", "dbg", "misc"):
         np.testing.assert_array_equal(sums[0][key], sums[1][key], err_msg=key)
