@@ -224,7 +224,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
   });
   m.attr("PACKET_LEN") = kPacketLen;
   m.attr("PACKET_LAYOUT") = py::make_tuple(kPacketHist, kPacketStatus, kPacketMisc, kPacketDbg, kPacketConf,
-                                           kPacketStats, kPacketCount);
+                                           kPacketStats, kPacketCount, kPacketRing);
   m.attr("STATS_OFF") = kStatsOff;
   m.attr("STATS_LEN") = kStatsLen;
   m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
