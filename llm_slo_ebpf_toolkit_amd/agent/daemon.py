@@ -479,10 +479,18 @@ class Agent:
                 break
             if maps.ctx_ids_used() > (7 << 20) and hasattr(maps, "reset_ctx_ids"):
                 maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
-        if pending is not None:
-            self._emit_window(pipe, *pending)
-        src.drain()
-        self.last_pipe = pipe
+        try:
+            if pending is not None:
+                self._emit_window(pipe, *pending)
+            src.drain()
+            self.last_summary = pipe.summary()
+        finally:
+            # unregister the rings from the GPU and free device memory while the ring mappings
+            # still exist (interpreter teardown order is arbitrary)
+            pipe.eng.close()
+            if getattr(self, "_producer", None) is not None:
+                self._producer.terminate()
+                self._producer.join(5)
         self.writers.flush()
         return 0
 
