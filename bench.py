@@ -195,10 +195,13 @@ def main() -> int:
         uid = [rt_uid() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = (uid[0], rank, world)
+    # a window's record budget covers its framed ring records (events AND the definitions the
+    # probes commit ahead of them) plus its user-space records: nothing may spill into the next window
+    sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs + himgs)
     user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
-    pipe = WindowPipeline(a.events, a.spans, a.services, local, comm, model=a.model, seed=a.seed,
+    pipe = WindowPipeline(sig_cap, a.spans, a.services, local, comm, model=a.model, seed=a.seed,
                           use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,
-                          user_cap=min(user_cap, a.events))
+                          user_cap=min(user_cap, sig_cap))
     # the producer publishes the epochs here (it runs ahead of the cuts): no cfg writes
     src = RingWindowSource(pipe, rb, user, spans, cfg_set=lambda i, v: None)
     keys = np.array(sorted(pod_sn), dtype=np.uint32)
@@ -363,6 +366,7 @@ def main() -> int:
         "kernel_ring_records_per_step": int(kernel_recs // max(a.steps, 1)),
         "host_us_per_window": round(host_us, 1),
         "host_issue_us_per_window": round(pipe.eng.host_issue_us, 1),
+        "records_over_window_budget": int(src.carried),
         "direct_dma_fraction": round(pipe.eng.direct_bytes / max(1, pipe.eng.direct_bytes + pipe.eng.staged_bytes), 4),
         "producer_wait_ms_total": round(producer_wait_ms, 2),
         "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,

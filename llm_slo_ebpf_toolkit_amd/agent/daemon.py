@@ -444,9 +444,9 @@ class Agent:
         maps, ring, user, spans, pods = self._open_source()  # a replay producer forks here, before the GPU
         node_id = (abs(hash(o.node)) % 0xFFFE) + 1
         maps.init(node_id)
-        pipe = WindowPipeline(o.window_events, o.window_spans, o.window_groups, o.device, comm, model=o.model,
-                              learn=False, window_ms=2000.0, user_cap=max(1024, o.window_events // 4),
-                              ttft_slo_ms=o.ttft_slo_ms)
+        budget = o.window_events + o.window_events // 4  # events plus the definitions ahead of them
+        pipe = WindowPipeline(budget, o.window_spans, o.window_groups, o.device, comm, model=o.model, learn=False,
+                              window_ms=2000.0, user_cap=max(1024, o.window_events // 4), ttft_slo_ms=o.ttft_slo_ms)
         src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
         if pods is not None:
             pipe.eng.set_pods(*pods)
@@ -491,6 +491,9 @@ class Agent:
             if getattr(self, "_producer", None) is not None:
                 self._producer.terminate()
                 self._producer.join(5)
+                if self._producer.is_alive():
+                    self._producer.kill()
+                    self._producer.join(5)
         self.writers.flush()
         return 0
 

@@ -8,7 +8,9 @@ windows in GPU mode.
 
 from __future__ import annotations
 
+import faulthandler
 import os
+import signal
 import sys
 from typing import List, Optional
 
@@ -79,6 +81,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
 
 def main(argv: Optional[List[str]] = None) -> int:
     argv = sys.argv[1:] if argv is None else argv
+    if hasattr(signal, "SIGUSR1"):  # operators: `kill -USR1 <pid>` dumps every thread's stack
+        faulthandler.register(signal.SIGUSR1, all_threads=True)
     if is_version_request(argv):
         return print_version()
     opts, smoke = parse(argv)
@@ -100,7 +104,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     if opts.engine == "gpu":
         from ..ops import load_agent
 
-        load_agent()  # the native engine must be built: fail loudly, never fall back
+        # the native engine must be built: fail loudly, never fall back (import only: the replay
+        # source forks its producer before the engine initialises the HIP runtime)
+        load_agent(init=False)
         return run_forever(agent, lambda: agent.run_windows(max_windows=opts.count))
     try:
         return run_forever(agent, agent.run_synthetic)

@@ -76,7 +76,7 @@ def _gpu_loop(duration_s: float, rate_eps: float, window_s: float) -> Dict[str, 
     ring, user, spans = bpf.create_rings(names, 4 * 24 * n, 4 * n, 4 * kw["spans_per_window"])
     prod = bpf.start_replay_producer(names, kw, rate_eps, int(window_s * 1000), n_images=2)
     try:
-        pipe = WindowPipeline(n, kw["spans_per_window"], groups, 0, None, model="bayes", learn=False,
+        pipe = WindowPipeline(n + n // 4, kw["spans_per_window"], groups, 0, None, model="bayes", learn=False,
                               user_cap=max(1024, n // 2))
         src = RingWindowSource(pipe, ring, user, spans)
         pipe.eng.set_pods(*bpf.pod_metadata(kw))
@@ -106,7 +106,9 @@ def measure(duration_s: float = 1.0, mode: Optional[str] = None, rate_eps: float
         try:
             from ..ops import load_agent
 
-            mode = "gpu" if load_agent().device_count() > 0 else "agent"
+            # import only (no HIP call): the GPU loop forks its producer before the runtime starts
+            load_agent(init=False)
+            mode = "gpu" if os.path.exists("/dev/kfd") else "agent"
         except Exception:  # pragma: no cover
             mode = "agent"
     if mode == "gpu":

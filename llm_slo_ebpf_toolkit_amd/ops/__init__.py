@@ -67,10 +67,20 @@ def load(device: Optional[int] = None):
 _AGENT = None
 
 
-def load_agent():
+def load_agent(init: bool = True):
     """The native window engine module (``_mislo_agent``: HIP + RCCL, no PyTorch) with the
-    signal-catalogue constant tables uploaded. Raises ExtensionMissing without a build."""
+    signal-catalogue constant tables uploaded. Raises ExtensionMissing without a build.
+    ``init=False`` only imports it (no HIP call): for a process that still has to fork workers,
+    which must happen before the HIP runtime initialises."""
     global _AGENT
+    if not init:
+        if _AGENT is not None:
+            return _AGENT
+        try:
+            return importlib.import_module(__name__ + "._mislo_agent")
+        except ImportError as exc:
+            raise ExtensionMissing("native engine _mislo_agent is not built; run "
+                                   "`python -m llm_slo_ebpf_toolkit_amd.ops.build`") from exc
     with _LOCK:
         if _AGENT is None:
             try:

@@ -243,6 +243,7 @@ class RingWindowSource:
         self.host_s = 0.0
         self.n = 0
         self.resubmitted = 0
+        self.carried = 0   # records past a window's budget, summed over windows (should stay 0)
 
     def publish_epoch(self, now_ns: Optional[int] = None) -> int:
         v = self.clock.publish(int(now_ns if now_ns is not None else time.time_ns()))
@@ -330,6 +331,7 @@ class RingWindowSource:
             if span_b % 24:
                 raise RuntimeError("BPF ring holds records of another size (the probes emit 16-byte records only)")
             take = min(span_b // 24, budget - n_k)
+            self.carried += span_b // 24 - take
             if take:  # one range: the data pages are mapped twice back to back
                 k_ranges.append((self.kpos, take))
                 kern.append((self.ring.data_address + (self.kpos & self.kmask), 24 * take))
@@ -340,11 +342,13 @@ class RingWindowSource:
             cap = self.user_ring.capacity
             user, n_u = self._ring_ranges(self.upos, cut.user, 64, self.user_ring.address, cap,
                                           min(pipe.user_cap, budget - n_k))
+            self.carried += max(0, cut.user - self.upos) - n_u
             self.upos += n_u
         spans, n_s = [], 0
         if self.span_ring is not None:
             spans, n_s = self._ring_ranges(self.spos, cut.spans, 64, self.span_ring.address, self.span_ring.capacity,
                                            pipe.span_cap)
+            self.carried += max(0, cut.spans - self.spos) - n_s
             self.spos += n_s
         wl = labels is not None if with_labels is None else with_labels
         k = pipe.submit(kern, user, spans, n_groups, labels, cut.bases, with_labels=wl, learn=learn)

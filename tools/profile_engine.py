@@ -38,7 +38,8 @@ def main() -> int:
     rb = rt.Ringbuf.create_shm(tag, 1 << 28)
     user = rt.HostRing(1 << int(np.ceil(np.log2(n_user * 4))), 64)
     spans = rt.HostRing(1 << int(np.ceil(np.log2(a.spans * 4))), 64)
-    pipe = WindowPipeline(a.events, a.spans, a.services, 0, None, model="bayes_learned",
+    budget = max(len(i.framed) // 24 + len(i.user) for i in imgs)  # framed (events + definitions) + user
+    pipe = WindowPipeline(budget, a.spans, a.services, 0, None, model="bayes_learned",
                           use_graphs=not a.no_graphs, user_cap=1 << int(np.ceil(np.log2(n_user))))
     pipe.eng.set_pods(gen.pod_ids.astype(np.uint32),
                       (gen.pod_svc.astype(np.uint32) << np.uint32(16)) | gen.pod_node.astype(np.uint32))
@@ -56,7 +57,7 @@ def main() -> int:
     dt = time.perf_counter() - t0
     s = pipe.summary()
     print(f"{a.windows} windows in {dt * 1e3:.1f} ms (ring refill in-process included); macro-F1 "
-          f"{s['macro_f1']:.4f}; direct DMA {pipe.eng.direct_bytes / 1e6:.1f} MB, staged {pipe.eng.staged_bytes}",
+          f"{s['macro_f1']:.4f}; over budget {src.carried}; direct DMA {pipe.eng.direct_bytes / 1e6:.1f} MB, staged {pipe.eng.staged_bytes}",
           flush=True)
     pipe.eng.close()
     return 0
