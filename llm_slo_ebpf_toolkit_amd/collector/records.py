@@ -372,7 +372,7 @@ class ProbeModel:
         shift = milli_shift_table()
         for e in events:
             st = int(e["signal_type"])
-            if st < 122 and int(e["value"]) < int(self.cfg[2 + st]):
+            if st < 120 and int(e["value"]) < int(self.cfg[2 + st]):
                 continue
             ck = int(e["conn_h"]) or conn_hash(int(e["src_port"]), int(e["dst_port"]), int(e["dst_ip"]))
             c = conn32(ck)

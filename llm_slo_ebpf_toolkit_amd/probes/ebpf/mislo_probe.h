@@ -1,35 +1,33 @@
-/* Common BPF-side plumbing for the agent's probes.
+/* Common BPF-side plumbing for the agent's probes (REF ebpf/c/ probes emit through one
+ * ring too, REF pkg/collector/ringbuf.go:56-150 drains it).
  *
  * Every probe object shares these maps, pinned by name under /sys/fs/bpf so the agent's
  * loader opens them once:
- *   mislo_events  BPF ring buffer of 16-byte mislo_event16 records (20-byte mislo_event20t
- *                 with -DMISLO_RING_EVENT20T, 24-byte mislo_event24 with -DMISLO_RING_EVENT24,
- *                 32-byte mislo_event32 with -DMISLO_RING_EVENT32) that the agent drains into
- *                 the GPU window ring (16 MiB);
+ *   mislo_events  BPF ring buffer (256 MiB) of 16-byte records: mislo_event16 events and the
+ *                 mislo_def16 definitions of newly interned ids (mislo_record.h). The agent
+ *                 never copies it: at each window cut it DMAs the framed bytes [consumer_pos,
+ *                 producer_pos) from the page-locked mapping straight into GPU memory, where
+ *                 the definitions are applied and the events decoded (ops/csrc/decode.hip);
  *   mislo_cfg     array: [0] realtime - monotonic offset (ns), [1] node id,
  *                 [2 + type] per-signal emit floor (raw units; the overhead guard raises
- *                 floors before it detaches probes), [124] current epoch (event16 rings:
- *                 realtime ns with the low 2 bits replaced by the epoch tag; the agent
- *                 publishes one per window cut and keeps the last 4 bases), [125] trace id counter,
- *                 [126] context id counter, [127] connection id counter;
- *   mislo_traces  LRU trace hash -> 32-bit trace id (event20t rings). Trace ids are per request
- *                 and never reused within 2^32 - 1 assignments; LRU eviction only drops traces
- *                 idle for far longer than the 2 s correlation window. The agent looks up the
- *                 window's span trace hashes here (spans of traces no probe saw get ids from
- *                 a disjoint range and match nothing, as they should);
+ *                 floors before it detaches probes), [124] current epoch (realtime ns with
+ *                 the low 2 bits replaced by the epoch tag; the agent publishes one per window
+ *                 cut and ships the last 4 bases with the window), [125] trace id counter,
+ *                 [126] context id counter;
+ *   mislo_traces  LRU trace hash -> trace id in 1 .. 2^29 - 1 (wrapping). LRU eviction only drops
+ *                 traces idle far longer than the 2 s correlation window; a re-seen hash gets a
+ *                 fresh id with a fresh definition;
  *   mislo_pods    cgroup id -> pod id (agent-populated from the kubelet / CRI);
- *   mislo_conns   connection key -> 24-bit connection id, assigned here on first sight; the
- *                 agent reads it (batch lookup, per window) to put spans on the same ids;
- *   mislo_ctxs    (pod, pid, connection id) -> 24-bit context id, assigned here on first
- *                 sight. When counter [126] has moved since the last window, the agent
- *                 batch-reads the map after snapshotting the ring (every id a snapshotted
- *                 record carries was inserted before the record was written) and appends
- *                 the new rows (pod, pid, conn, svc|node from pod metadata) to the device
- *                 context table before the window's DMA;
+ *   mislo_ctxs    (pod, pid, conn32) -> context id in 1 .. 2^23 - 1, assigned on first sight.
+ *                 When the counter nears the limit the agent clears the map and the counter
+ *                 (collector/bpf.py reset_ctx_ids) and ids are defined afresh;
  *   mislo_scratch per-CPU 64-byte mislo_event the probe fills before mislo_submit() packs it.
- * Records are stamped with wall-clock ns, their connections interned and their values
- * converted to fixed point in the kernel, so the consumer copies ring bytes straight into
- * pinned memory and DMAs them to the GPU without touching individual records.
+ * Interning emits the definition record first and inserts the map entry only once the
+ * definition is on the ring: any record that carries the id is written after its definition,
+ * so ring order is enough for the GPU to resolve it (no map reads on the agent's window path).
+ * A definition the ring drops (full) leaves the id unassigned; the event then carries id 0.
+ * The userspace model of exactly this logic is runtime/csrc/probesim.cpp (ProbeSim), which
+ * the tests and the replay producer drive.
  */
 #ifndef MISLO_PROBE_H
 #define MISLO_PROBE_H
@@ -49,11 +47,9 @@
 #define MISLO_CFG_EPOCH 124
 #define MISLO_CFG_TRACE_NEXT 125
 #define MISLO_CFG_CTX_NEXT 126
-#define MISLO_CFG_CONN_NEXT 127
-#define MISLO_CONN_ID_LIMIT (1u << 24)
 
 struct mislo_ctx_key {
-	__u32 pod_id, pid, conn_id, pad;
+	__u32 pod_id, pid, conn32, pad;
 };
 
 struct {
@@ -66,7 +62,7 @@ struct {
 
 struct {
 	__uint(type, BPF_MAP_TYPE_RINGBUF);
-	__uint(max_entries, 16 * 1024 * 1024);
+	__uint(max_entries, 256 * 1024 * 1024); /* ~11M framed records: several windows of slack */
 	__uint(pinning, LIBBPF_PIN_BY_NAME);
 } mislo_events SEC(".maps");
 
@@ -89,16 +85,8 @@ struct {
 struct {
 	__uint(type, BPF_MAP_TYPE_HASH);
 	__uint(max_entries, 1 << 20);
-	__type(key, __u64);   /* connection key (records.py conn keys) */
-	__type(value, __u32); /* connection id, 1 .. 2^24 - 1 */
-	__uint(pinning, LIBBPF_PIN_BY_NAME);
-} mislo_conns SEC(".maps");
-
-struct {
-	__uint(type, BPF_MAP_TYPE_HASH);
-	__uint(max_entries, 1 << 20);
 	__type(key, struct mislo_ctx_key);
-	__type(value, __u32); /* context id, 1 .. 2^24 - 1 (0 = the all-zero context) */
+	__type(value, __u32); /* context id, 1 .. 2^23 - 1 (0 = the all-zero context) */
 	__uint(pinning, LIBBPF_PIN_BY_NAME);
 } mislo_ctxs SEC(".maps");
 
@@ -118,7 +106,8 @@ static __always_inline __u64 mislo_cfg_get(__u32 idx)
 /* True when `value` is below the signal's current emit floor. */
 static __always_inline int mislo_below_floor(__u16 type, __u64 value)
 {
-	return value < mislo_cfg_get(MISLO_CFG_FLOOR(type));
+	/* floors exist for types 0-119; the slots above hold the epoch and the id counters */
+	return type < 120 && value < mislo_cfg_get(MISLO_CFG_FLOOR(type));
 }
 
 /* The probe's working record (per-CPU scratch, not ring memory): fill, then mislo_submit(). */
@@ -162,50 +151,45 @@ static __always_inline __u64 mislo_conn_key(const struct mislo_event *e)
 	return z ? z : 1;
 }
 
-/* key -> id from map `m`, assigned on first sight from counter cfg[`ctr`]. Two CPUs racing on
- * a new key both draw ids; BPF_NOEXIST lets one win and the other re-reads the winner (the
- * loser's id is never used). An exhausted id space yields 0 until the agent resets the map. */
-#define MISLO_INTERN(m, keyp, ctr)                                                         \
-	({                                                                                  \
-		__u32 _r = 0;                                                               \
-		__u32 *_id = bpf_map_lookup_elem(&(m), (keyp));                             \
-		if (_id) {                                                                  \
-			_r = *_id;                                                          \
-		} else {                                                                    \
-			__u32 _idx = (ctr);                                                 \
-			__u64 *_next = bpf_map_lookup_elem(&mislo_cfg, &_idx);              \
-			if (_next) {                                                        \
-				__u64 _fresh = __sync_fetch_and_add(_next, 1) + 1;          \
-				if (_fresh < MISLO_CONN_ID_LIMIT) {                         \
-					__u32 _v = (__u32)_fresh;                           \
-					if (bpf_map_update_elem(&(m), (keyp), &_v, BPF_NOEXIST) == 0) \
-						_r = _v;                                    \
-					else if ((_id = bpf_map_lookup_elem(&(m), (keyp))))  \
-						_r = *_id;                                  \
-				}                                                           \
-			}                                                                   \
-		}                                                                           \
-		_r;                                                                         \
-	})
-
-static __always_inline __u32 mislo_conn_id(__u64 key)
+/* Put a 16-byte record on the ring. No wakeup: the agent reads the ring at its window cuts,
+ * never from epoll, so a per-record consumer wakeup would be pure overhead. 0 = written. */
+static __always_inline long mislo_out(const void *r)
 {
-	if (!key)
-		return 0;
-	return MISLO_INTERN(mislo_conns, &key, MISLO_CFG_CONN_NEXT);
+	return bpf_ringbuf_output(&mislo_events, (void *)r, 16, BPF_RB_NO_WAKEUP);
 }
 
-/* (pod, pid, connection) -> context id; the all-zero context is id 0 without a map entry */
-static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 conn_id)
+/* (pod, pid, connection) -> context id, assigned on first sight from counter [126]: the
+ * definition goes on the ring first, then the map entry. Two CPUs racing on a new key both
+ * define an id; BPF_NOEXIST lets one win and the other re-reads the winner (the loser's
+ * definition names an id nothing uses). An exhausted id space yields 0 until the agent
+ * resets the map; the all-zero context is id 0 without a map entry. */
+static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32)
 {
-	if (!pod_id && !pid && !conn_id)
+	if (!pod_id && !pid && !c32)
 		return 0;
-	struct mislo_ctx_key k = {.pod_id = pod_id, .pid = pid, .conn_id = conn_id, .pad = 0};
-	return MISLO_INTERN(mislo_ctxs, &k, MISLO_CFG_CTX_NEXT);
+	struct mislo_ctx_key k = {.pod_id = pod_id, .pid = pid, .conn32 = c32, .pad = 0};
+	__u32 *id = bpf_map_lookup_elem(&mislo_ctxs, &k);
+	if (id)
+		return *id;
+	__u32 idx = MISLO_CFG_CTX_NEXT;
+	__u64 *next = bpf_map_lookup_elem(&mislo_cfg, &idx);
+	if (!next)
+		return 0;
+	__u64 fresh = __sync_fetch_and_add(next, 1) + 1;
+	if (fresh >= MISLO_KERNEL_CTX_LIMIT)
+		return 0;
+	__u32 v = (__u32)fresh;
+	struct mislo_def16 d = {.a = c32, .tag_id = MISLO_DEF_CTX | (v << 8), .b = pod_id, .c = pid};
+	if (mislo_out(&d))
+		return 0; /* ring full: leave the context unnamed */
+	if (bpf_map_update_elem(&mislo_ctxs, &k, &v, BPF_NOEXIST) == 0)
+		return v;
+	id = bpf_map_lookup_elem(&mislo_ctxs, &k);
+	return id ? *id : 0;
 }
 
-/* trace hash -> 32-bit id in [1, 2^32 - 1] (wrapping), assigned on first sight like
- * MISLO_INTERN; 0 for untraced events */
+/* trace hash -> trace id in 1 .. 2^29 - 1 (wrapping), definition first like mislo_ctx_id;
+ * 0 for untraced events */
 static __always_inline __u32 mislo_trace_id(__u64 h)
 {
 	if (!h)
@@ -217,41 +201,23 @@ static __always_inline __u32 mislo_trace_id(__u64 h)
 	__u64 *next = bpf_map_lookup_elem(&mislo_cfg, &idx);
 	if (!next)
 		return 0;
-	__u64 fresh = __sync_fetch_and_add(next, 1);
-	__u32 v = (__u32)(fresh % MISLO_TRACE_ID_MASK) + 1; /* [1, 2^30 - 1]: event16 keeps 2 tag bits */
+	__u32 v = mislo_trace_slot(__sync_fetch_and_add(next, 1));
+	struct mislo_def16 d = {.a = v, .tag_id = MISLO_DEF_TRACE, .b = (__u32)h, .c = (__u32)(h >> 32)};
+	if (mislo_out(&d))
+		return 0;
 	if (bpf_map_update_elem(&mislo_traces, &h, &v, BPF_NOEXIST) == 0)
 		return v;
 	id = bpf_map_lookup_elem(&mislo_traces, &h);
 	return id ? *id : 0;
 }
 
-/* Pack the working record into the ring record and publish it. */
+/* Pack the working record into the 16-byte ring record (timestamp as an offset from the
+ * published epoch, tagged with it) and publish it. */
 static __always_inline void mislo_submit(struct mislo_event *e)
 {
-	__u32 cid = mislo_conn_id(mislo_conn_key(e));
-#ifdef MISLO_RING_EVENT32
-	struct mislo_event32 r;
-	r.ts_ns = e->ts_ns;
-	r.trace_h = e->trace_h;
-	r.value_milli = mislo_milli(e->signal_type, e->value);
-	r.pid = e->pid;
-	r.pod_id = e->pod_id;
-	r.type_conn = (e->signal_type & 0xFFu) | (cid << 8);
-#elif defined(MISLO_RING_EVENT20T)
-	struct mislo_event20t r;
-	r.ts_ns = e->ts_ns;
-	r.value_milli = mislo_milli(e->signal_type, e->value);
-	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
-	r.trace_id = mislo_trace_id(e->trace_h);
-#elif defined(MISLO_RING_EVENT24)
-	struct mislo_event24 r;
-	r.ts_ns = e->ts_ns;
-	r.trace_h = e->trace_h;
-	r.value_milli = mislo_milli(e->signal_type, e->value);
-	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
-#else
-	/* default: 16-byte record, timestamp offset from the published epoch, tagged with it */
 	struct mislo_event16 r;
+	__u32 ctx = mislo_ctx_id(e->pod_id, e->pid, mislo_conn32(mislo_conn_key(e)));
+	__u32 tid = mislo_trace_id(e->trace_h);
 	__u32 eidx = MISLO_CFG_EPOCH;
 	__u64 *ep = bpf_map_lookup_elem(&mislo_cfg, &eidx);
 	__u64 epoch = ep ? *ep : 0;
@@ -262,11 +228,10 @@ static __always_inline void mislo_submit(struct mislo_event *e)
 		r.ts_off = 0; /* stamped before the epoch it read (clock step): clamp */
 	else
 		r.ts_off = (__u64)e->ts_ns - base >= MISLO_TS_ZERO ? MISLO_TS_ZERO - 1 : (__u32)((__u64)e->ts_ns - base);
-	r.ctx_type = (e->signal_type & 0xFFu) | (mislo_ctx_id(e->pod_id, e->pid, cid) << 8);
+	r.ctx_type = (e->signal_type & 0xFFu) | (ctx << 8);
 	r.value_milli = mislo_milli(e->signal_type, e->value);
-	r.trace_tag = (mislo_trace_id(e->trace_h) & MISLO_TRACE_ID_MASK) | ((__u32)(epoch & 3) << MISLO_EPOCH_TAG_SHIFT);
-#endif
-	bpf_ringbuf_output(&mislo_events, &r, sizeof(r), 0);
+	r.trace_tag = (tid & MISLO_TRACE_ID_MASK) | ((__u32)(epoch & 3) << MISLO_EPOCH_TAG_SHIFT);
+	mislo_out(&r);
 }
 
 /* Emit a record attributed to the current task. */

@@ -1,27 +1,23 @@
 /* Event records shared by the probes, the rocprofiler tool, the native ring and the GPU
  * decode kernels. Only fixed-width types, so it compiles for the BPF target and for the host
  * layout test.
- *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record and
- *                        the user-space producers' ring record;
- *   struct mislo_event20t (20 B, records.py EVENT20T): the ring record with
- *                        -DMISLO_RING_EVENT20T: mislo_event24 with the trace hash interned in the kernel
- *                        too (mislo_probe.h mislo_trace_id; the agent maps span trace ids
- *                        through the same map), 5/16 of the 64-byte record's PCIe bytes;
- *   struct mislo_event16 (16 B, records.py EVENT16): what the probes put on the BPF ring
- *                        (default): mislo_event20t with the timestamp as a 32-bit offset from the epoch the
- *                        agent last published (mislo_cfg[MISLO_CFG_EPOCH]) and that epoch's 2-bit
- *                        tag in the top of trace_id, so records emitted across a window cut
- *                        decode exactly (the window carries its last 4 epoch bases);
- *   struct mislo_event24 (24 B, records.py EVENT24): the ring record with -DMISLO_RING_EVENT24.
- *                        The kernel converts the value to fixed point
- *                        (mislo_milli) and interns the connection and the (pod, pid, conn)
- *                        context (mislo_probe.h mislo_conn_id / mislo_ctx_id), so the agent
- *                        DMAs ring bytes to the GPU without touching a record: 3/8 of the PCIe
- *                        bytes of the 64-byte record. The agent turns new context ids into
- *                        device context-table rows (adding svc / node from pod metadata);
- *   struct mislo_event32 (32 B, records.py EVENT32): the ring record with -DMISLO_RING_EVENT32
- *                        (connections interned, pod and pid inline; svc / node from the
- *                        agent's pod table). */
+ *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record (per-CPU
+ *                        scratch) and the user-space producers' ring record (rocprofiler tool);
+ *   struct mislo_event16 (16 B, records.py EVENT16): the one record the probes put on the BPF
+ *                        ring. The timestamp is a 32-bit offset from the epoch the agent last
+ *                        published (mislo_cfg[MISLO_CFG_EPOCH]) and that epoch's 2-bit tag sits
+ *                        in the top of trace_tag, so records written across a window cut decode
+ *                        exactly (a window carries its last 4 epoch bases). The value is fixed
+ *                        point (mislo_milli); the (pod, pid, connection) context and the trace
+ *                        hash are interned in the kernel (mislo_probe.h), so the agent DMAs the
+ *                        ring bytes to the GPU without reading a record;
+ *   definition records   (16 B, same stride, signal-type byte >= MISLO_DEF_FIRST): an interned
+ *                        id's meaning, committed to the ring BEFORE the id enters its map, so in
+ *                        ring order every definition precedes any record that uses the id:
+ *                          MISLO_DEF_CTX   {conn32, 0xFE | ctx id << 8, pod id, pid}
+ *                          MISLO_DEF_TRACE {trace id, 0xFD, trace hash lo, trace hash hi}
+ *                        The GPU applies them to its context table / trace map in ring order
+ *                        (ops/csrc/decode.hip k_ring_defs). */
 #ifndef MISLO_RECORD_H
 #define MISLO_RECORD_H
 
@@ -72,22 +68,6 @@ struct mislo_event {
 	__u64 conn_h;      /* 0: derived on the GPU from (ports, ip) */
 };
 
-struct mislo_event32 {
-	__s64 ts_ns;       /* CLOCK_REALTIME ns */
-	__u64 trace_h;     /* trace-id hash (0 = none) */
-	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
-	__u32 pid;         /* tgid */
-	__u32 pod_id;      /* cgroup -> pod id, 0 = unknown */
-	__u32 type_conn;   /* bits 0-7 signal type, bits 8-31 interned connection id (0 = none) */
-};
-
-struct mislo_event24 {
-	__s64 ts_ns;       /* CLOCK_REALTIME ns */
-	__u64 trace_h;     /* trace-id hash (0 = none) */
-	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
-	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
-};
-
 #define MISLO_EPOCH_TAG_SHIFT 30
 #define MISLO_TRACE_ID_MASK ((1u << MISLO_EPOCH_TAG_SHIFT) - 1u)
 #define MISLO_TS_ZERO 0xFFFFFFFFu
@@ -99,13 +79,33 @@ struct mislo_event16 {
 	__u32 trace_tag;   /* bits 0-29 interned trace id (0 = none), bits 30-31 epoch tag */
 };
 
-/* 4-byte aligned: ring records are packed back to back at 20-byte strides */
-struct mislo_event20t {
-	__s64 ts_ns;       /* CLOCK_REALTIME ns */
-	__u32 value_milli; /* value in 1/1000 of the signal's output unit (mislo_milli) */
-	__u32 ctx_type;    /* bits 0-7 signal type, bits 8-31 interned context id (0 = none) */
-	__u32 trace_id;    /* interned trace id (mislo_trace_id), 0 = none */
-} __attribute__((packed, aligned(4)));
+/* definition records (same 16-byte stride as mislo_event16) */
+#define MISLO_DEF_FIRST 0xF0u
+#define MISLO_DEF_TRACE 0xFDu
+#define MISLO_DEF_CTX 0xFEu
+struct mislo_def16 {
+	__u32 a;       /* ctx: conn32; trace: trace id */
+	__u32 tag_id;  /* bits 0-7 MISLO_DEF_*, bits 8-31 ctx id (ctx definitions) */
+	__u32 b;       /* ctx: pod id; trace: hash bits 0-31 */
+	__u32 c;       /* ctx: pid; trace: hash bits 32-63 */
+};
+
+/* id spaces: the kernel assigns the low part, the agent's host-side encoders the rest, so both
+ * kinds of producer share one device context table (2^24 rows) and one trace-id space */
+#define MISLO_KERNEL_CTX_LIMIT (1u << 23)   /* kernel context ids 1 .. 2^23 - 1 */
+#define MISLO_KERNEL_TRACE_LIMIT (1u << 29) /* kernel trace ids 1 .. 2^29 - 1 */
+
+/* records.py conn32: the 32-bit connection identity in context keys and rows; 0 = none */
+static __always_inline __u32 mislo_conn32(__u64 key)
+{
+	return key ? ((__u32)(key ^ (key >> 32)) | 1u) : 0u;
+}
+
+/* the trace id the kernel assigns for its `fresh`-th new trace hash (wraps in 1 .. 2^29 - 1) */
+static __always_inline __u32 mislo_trace_slot(__u64 fresh)
+{
+	return (__u32)(fresh % (MISLO_KERNEL_TRACE_LIMIT - 1)) + 1;
+}
 
 /* value_milli = raw * 10^shift: the catalogue's decode scales are powers of ten
  * (signals/catalog.py decode_scale; records.py milli_shift_table is the same table). */

@@ -29,6 +29,140 @@ def test_bpf_record_layout_matches_event_dtype(tmp_path):
     t, v, m = (np.array(c, dtype=np.uint64) for c in zip(*rows))
     shift = records.milli_shift_table()[t.astype(np.int64)]
     np.testing.assert_array_equal(records.milli_int(v, shift), m.astype(np.uint32))
+    lines = out.stdout.splitlines()
+    const = [int(x) for x in next(ln for ln in lines if ln.startswith("const ")).split()[1:]]
+    assert const == [records.DEF_FIRST, records.DEF_TRACE, records.DEF_CTX, records.KERNEL_CTX_LIMIT,
+                     records.KERNEL_TRACE_LIMIT]
+    for ln in lines:
+        if ln.startswith("conn32 "):
+            k, c = (int(x) for x in ln.split()[1:])
+            assert records.conn32(k) == c, ln
+        if ln.startswith("trace "):
+            f, v = (int(x) for x in ln.split()[1:])
+            assert v == f % (records.KERNEL_TRACE_LIMIT - 1) + 1, ln
+
+
+HOST_DIR = os.path.join(EBPF_DIR, "host")
+
+
+@pytest.fixture(scope="module")
+def probe_host(tmp_path_factory):
+    """mislo_probe.h compiled for the host against in-process maps (probes/ebpf/host)."""
+    if shutil.which("gcc") is None:
+        pytest.skip("needs a host C compiler")
+    exe = tmp_path_factory.mktemp("probe_host") / "probe_host"
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", HOST_DIR, "-I", EBPF_DIR, "-o", str(exe),
+                    os.path.join(HOST_DIR, "probe_host.c")], check=True)
+    return str(exe)
+
+
+def _run_host(exe, tmp_path, events, *args):
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    events.tofile(fin)
+    r = subprocess.run([exe, str(fin), str(fout), *map(str, args)], capture_output=True, text=True, check=True)
+    import numpy as np
+
+    stats = dict(zip(r.stdout.split()[::2], (int(x) for x in r.stdout.split()[1::2])))
+    return np.fromfile(fout, dtype=np.uint32).reshape(-1, 4), stats
+
+
+def _probe_events(n=3000, seed=5):
+    """Replay events plus hand-made ones: explicit connection hashes, port-derived
+    connections, traces shared across pods, zero timestamps, values under a floor."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+
+    w = ReplayGenerator(ReplayConfig(scenario="full", events_per_window=n, spans_per_window=64, n_services=8,
+                                     seed=seed)).next_window()
+    ev = np.ascontiguousarray(w.events)
+    extra = np.zeros(64, dtype=records.EVENT)
+    rng = np.random.default_rng(seed)
+    extra["ts_ns"] = int(w.t0_ns) + rng.integers(0, 10**9, 64)
+    extra["ts_ns"][::9] = 0
+    extra["signal_type"] = rng.choice([1, 2, 4, 9], 64)
+    extra["value"] = rng.integers(0, 5_000_000, 64)
+    extra["pod_id"] = rng.integers(0, 4, 64)
+    extra["pid"] = rng.integers(0, 3, 64)
+    extra["src_port"] = rng.integers(0, 3, 64) * 40000
+    extra["dst_port"] = 443
+    extra["dst_ip"] = 0x0A000001
+    extra["conn_h"][::5] = 0xDEADBEEF00000001
+    extra["trace_h"][::2] = rng.choice(np.array([0x1111, 0x2222, 0xFFFFFFFFFFFFFFFF], dtype=np.uint64), 32)
+    return np.concatenate([ev, extra])
+
+
+def _probesim_records(events, cuts, cfg):
+    """ProbeSim.encode over ``events`` with the epoch published at each (index, value) cut."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    rb = rt.Ringbuf.create_shm(f"/mislo-ph-{os.getpid()}-{len(events)}", 1 << 16)
+    for i, v in cfg.items():
+        rb.cfg_set(i, v)
+    sim = rt.ProbeSim(rb, records.milli_shift_table(), 1 << 20)
+    out, lo = [], 0
+    for idx, val in list(cuts) + [(len(events), None)]:
+        if idx > lo:
+            out.append(sim.encode(np.ascontiguousarray(events[lo:idx])).reshape(-1, 4))
+            lo = idx
+        if val is not None:
+            rb.cfg_set(124, val)
+    return np.concatenate(out), rb
+
+
+def test_probe_c_plumbing_matches_probesim(probe_host, tmp_path):
+    """The BPF C that runs in the kernel (mislo_probe.h mislo_emit -> mislo_submit, compiled
+    for the host) writes the same ring records as ProbeSim (the producer model the replay,
+    the bench and the GPU tests drive): definitions ahead of first uses, context / trace ids,
+    epoch offsets and tags across cuts, floors, and both id spaces' wrap / exhaustion."""
+    import numpy as np
+
+    ev = _probe_events()
+    t0 = int(ev["ts_ns"][ev["ts_ns"] > 0].min())
+    cuts = [(0, (t0 - 10**6) & ~3 | 1), (1000, (t0 + 3 * 10**8) & ~3 | 2), (2500, (t0 + 6 * 10**8) & ~3 | 3)]
+    floors = {2 + 9: 2_000_000}  # syscall_latency below 2 ms stays in the kernel
+    for trace_next, ctx_next in ((0, 0), ((1 << 29) - 40, (1 << 23) - 30)):
+        args = ["--trace-next", trace_next, "--ctx-next", ctx_next, "--floor", "9:2000000"]
+        for idx, val in cuts:
+            args += ["--epoch-at", f"{idx}:{val}"]
+        got, stats = _run_host(probe_host, tmp_path, ev, *args)
+        ref, rb = _probesim_records(ev, cuts, {125: trace_next, 126: ctx_next, **floors})
+        np.testing.assert_array_equal(got, ref)
+        assert stats["trace_next"] == rb.cfg_get(125) and stats["ctx_next"] == rb.cfg_get(126)
+        types = got[:, 1] & 0xFF
+        assert (types == 0xFE).any() and (types == 0xFD).any()
+        if ctx_next:  # the context space ran out: later new contexts carry id 0
+            assert stats["ctx_next"] > (1 << 23) and ((got[:, 1] >> 8)[types < 0xF0] == 0).any()
+            assert ((got[:, 0][types == 0xFD]) < 100).any()  # trace ids wrapped to the bottom
+
+
+def test_probe_c_full_ring_matches_probesim(probe_host, tmp_path):
+    """Ring full: bpf_ringbuf_output fails from the same record on in the C and in ProbeSim
+    (a definition that does not fit leaves its id unassigned; the counters still advance)."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    ev = _probe_events(n=600, seed=9)
+    epoch = int(ev["ts_ns"][ev["ts_ns"] > 0].min()) & ~3
+    rt = load()
+    rb = rt.Ringbuf.create_shm(f"/mislo-phf-{os.getpid()}", 1 << 12)
+    rb.cfg_set(124, epoch)
+    cap = rb.size // 24
+    got, stats = _run_host(probe_host, tmp_path, ev, "--epoch-at", f"0:{epoch}", "--ring-cap", cap)
+    sim = rt.ProbeSim(rb, records.milli_shift_table(), 1 << 20)
+    sim.submit(ev)
+    n = rb.producer_pos // 24
+    assert n == cap == len(got) and sim.dropped > 0
+    ring = rb.data_view()[: n * 24].view(np.uint32).reshape(-1, 6)
+    np.testing.assert_array_equal(ring[:, 2:], got)
+    assert stats["trace_next"] == rb.cfg_get(125) and stats["ctx_next"] == rb.cfg_get(126)
 
 
 def test_record_enum_matches_catalogue():
