@@ -81,8 +81,10 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
 
 def main(argv: Optional[List[str]] = None) -> int:
     argv = sys.argv[1:] if argv is None else argv
-    if hasattr(signal, "SIGUSR1"):  # operators: `kill -USR1 <pid>` dumps every thread's stack
+    try:  # operators: `kill -USR1 <pid>` dumps every thread's stack to stderr
         faulthandler.register(signal.SIGUSR1, all_threads=True)
+    except (AttributeError, ValueError, OSError):  # no SIGUSR1, or stderr is not a real file
+        pass
     if is_version_request(argv):
         return print_version()
     opts, smoke = parse(argv)
