@@ -44,7 +44,7 @@ from ..models.sample import FaultSample
 from ..safety import OverheadGuard, RateLimiter
 from ..signals import catalog
 from ..signals.generator import Generator
-from ..signals.metadata import Metadata, ProcMetadataEnricher, StaticMetadataEnricher
+from ..signals.metadata import Interner, Metadata, ProcMetadataEnricher, StaticMetadataEnricher
 from ..utils.timeutil import now_ns
 from .metrics import AgentMetrics
 
@@ -166,6 +166,7 @@ class AgentOptions:
     min_confidence: float = 0.5
     ttft_slo_ms: float = 800.0           # per-incident SLO: a span breaches when its TTFT exceeds this
     slo_target: float = 0.99             # TTFT SLO objective (burn rate = breach fraction / (1 - target))
+    otlp_receiver_bind: str = ""         # OTLP/HTTP /v1/traces receiver feeding the span ring ("" = off)
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -221,6 +222,8 @@ class Agent:
         self._probe_schema = validator.compiled("probe-event")
         self.ready = False
         self.windows_done = 0
+        self.pod_ids = Interner()  # pod uid -> pod id (cgroup map and OTLP spans)
+        self.receiver = None
         self.attributions_emitted = 0
 
     # ---- lifecycle ------------------------------------------------------------------------
@@ -314,6 +317,7 @@ class Agent:
         self.metrics.set_heartbeat(t_ns / 1e9)
 
     def _guard_tick(self) -> None:
+        self.metrics.set_rss()
         if self.guard is None:
             return
         try:
@@ -378,6 +382,18 @@ class Agent:
                                                        o.window_ms, max_windows=0)
             return bpf.EmulatedMaps(ring), ring, user, spans, bpf.pod_metadata(kw)
         raise ValueError(f"unknown window source {o.source!r} (bpf | shm | replay)")
+
+    def _scan_pods(self, maps) -> None:
+        """kubepods cgroups -> the probes' cgroup -> pod id map (pod ids from the interner the
+        OTLP receiver maps ``k8s.pod.uid`` through, so spans and kernel records agree)."""
+        from ..collector import bpf
+
+        for cg, (pid, _uid) in bpf.discover_pods(interner=self.pod_ids).items():
+            try:
+                maps.set_pod(cg, pid)
+            except OSError as exc:
+                print(f"pod map update failed: {exc}", file=sys.stderr)
+                return
 
     def _attributions(self, G: int, names: Sequence[str], res: dict, t_ns: int, model) -> List[IncidentAttribution]:
         """One IncidentAttribution per incident group whose top posterior clears min_confidence.
@@ -450,8 +466,19 @@ class Agent:
         src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
         if pods is not None:
             pipe.eng.set_pods(*pods)
-        names = [f"svc-{g + 1}" for g in range(o.window_groups)]
+        if o.source == "bpf":
+            self._scan_pods(maps)
         G = o.window_groups
+        names = [f"svc-{g + 1}" for g in range(G)]
+        receiver = None
+        if o.otlp_receiver_bind and spans is not None:
+            from ..collector.otlp import GroupTable, OtlpSpanReceiver, SpanMapper
+
+            groups = GroupTable(G)
+            names = groups.names  # incident groups are the services the receiver has seen
+            receiver = OtlpSpanReceiver(o.otlp_receiver_bind, SpanMapper(groups, self.pod_ids.id, node_id),
+                                        spans.push).start()
+            self.receiver = receiver
         if self.guard is not None:
             self.guard.evaluate()
         self.ready = True
@@ -472,6 +499,8 @@ class Agent:
             pending = (k, cut.t_ns, G, names, ring, host_us)
             if self.windows_done and self.windows_done % 64 == 0:
                 pipe.eng.rotate_traces()  # trace-id mappings live 64-128 windows
+                if o.source == "bpf":
+                    self._scan_pods(maps)
             self._guard_tick()
             self.metrics.set_heartbeat()
             self.windows_done += 1
@@ -488,6 +517,8 @@ class Agent:
             # unregister the rings from the GPU and free device memory while the ring mappings
             # still exist (interpreter teardown order is arbitrary)
             pipe.eng.close()
+            if receiver is not None:
+                receiver.stop()
             if getattr(self, "_producer", None) is not None:
                 self._producer.terminate()
                 self._producer.join(5)

@@ -10,6 +10,7 @@ histograms without re-observing events. The kernel's buckets are ``le`` buckets
 
 from __future__ import annotations
 
+import os
 import time
 from typing import Iterable, Sequence
 
@@ -62,6 +63,7 @@ class AgentMetrics:
                                    "Windows whose ring consumption stopped at a record still being written.")
         self.ring_backlog = r.gauge("llm_slo_agent_ring_backlog_bytes", "Unconsumed bytes in the BPF ring buffer.")
         self.host_us = r.gauge("llm_slo_agent_window_host_us", "Host time to assemble the last window (us).")
+        self.rss = r.gauge("llm_slo_agent_memory_rss_bytes", "Agent process resident set size (bytes).")
         self.up.set(1)
         for k in EVENT_KINDS:
             self.kind.set(1 if k == event_kind else 0, k)
@@ -76,6 +78,13 @@ class AgentMetrics:
 
     def set_cpu_overhead(self, pct: float) -> None:
         self.cpu.set(max(0.0, pct))
+
+    def set_rss(self) -> None:
+        try:
+            with open("/proc/self/statm") as f:
+                self.rss.set(float(int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")))
+        except (OSError, ValueError, IndexError):
+            pass
 
     def set_enabled_signals(self, supported: Iterable[str], enabled: Iterable[str]) -> None:
         en = set(enabled)

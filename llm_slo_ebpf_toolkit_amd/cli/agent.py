@@ -60,6 +60,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
         ("ttft-slo-ms", d.ttft_slo_ms, "per-incident TTFT SLO (ms) for burn rates"),
         ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),
+        ("otlp-receiver-bind", d.otlp_receiver_bind, "OTLP/HTTP /v1/traces receiver feeding the span ring (gpu engine)"),
     ]:
         p.flag(name, default, help_)
     a = p.parse_args(argv)
@@ -75,7 +76,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         metrics_bind=a.metrics_bind, engine=a.engine, source=a.source, ring_name=a.ring_name, pin_dir=a.pin_dir,
         window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
-        ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target)
+        ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
+        otlp_receiver_bind=a.otlp_receiver_bind)
     return o, a.probe_smoke
 
 

@@ -1,0 +1,389 @@
+"""OTLP/HTTP trace receiver feeding the agent's span ring (VERDICT r1 missing #2).
+
+REF enriches spans inside the OpenTelemetry collector: the `ebpfcorrelator` processor
+(REF pkg/otel/processor/ebpfcorrelator/processor.go:29-49) sees every span of the RAG
+service's request path (REF demo/rag-service/main.go:408-441) and joins it with eBPF signals
+on the host. Here the join runs on the GPU, so the agent itself accepts the services' spans:
+
+    POST /v1/traces   application/json (OTLP/JSON) or application/x-protobuf (OTLP/proto)
+
+Each request's server span (a root span, or any span carrying the TTFT SLI attribute) becomes
+one 64-byte SPAN record (collector/records.py SPAN) pushed into the span ring the window
+engine DMAs from, with its identities mapped onto the ids the kernel side uses:
+
+* trace id  -> ``trace_hash`` (low 64 bits of the W3C trace id; the GPU translates it through
+  the kernel's trace definitions, ops/csrc/decode.hip k_decode_spans);
+* pod       -> the agent's pod id for ``k8s.pod.uid`` (the same interner that fills the
+  probes' cgroup -> pod map, collector/bpf.py discover_pods), else ``k8s.pod.name``;
+* pid       -> ``process.pid``; connection -> (client port, server port, server IPv4) hashed
+  like the probes' connection key (records.conn_hash);
+* incident group -> ``service.name`` (one group per service, ``GroupTable``);
+* SLI       -> ``llm.slo.ttft_ms`` (contracts/semconv.py) and the span duration.
+
+The protobuf decoder is a minimal wire-format walker over the OTLP trace messages
+(ExportTraceServiceRequest / ResourceSpans / ScopeSpans / Span / KeyValue / AnyValue): no
+generated code, no protobuf runtime.
+"""
+
+from __future__ import annotations
+
+import http.server
+import ipaddress
+import json
+import struct
+import threading
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Iterator, List, Optional, Tuple
+
+import numpy as np
+
+from ..contracts import semconv
+from . import records
+
+TTFT_KEYS = (semconv.ATTR_SLO_TTFT_MS, "gen_ai.server.time_to_first_token", "llm.ttft_ms")
+
+
+def trace_hash(trace_id) -> int:
+    """Low 64 bits of a W3C trace id (hex string or 16 bytes); never 0 for a present id."""
+    if not trace_id:
+        return 0
+    if isinstance(trace_id, (bytes, bytearray)):
+        b = bytes(trace_id)[-8:]
+        h = int.from_bytes(b, "big")
+    else:
+        s = str(trace_id).strip().lower()
+        h = int(s[-16:], 16) if s else 0
+    return h or 1
+
+
+def span_hash(span_id) -> int:
+    if not span_id:
+        return 0
+    if isinstance(span_id, (bytes, bytearray)):
+        return int.from_bytes(bytes(span_id)[-8:], "big") or 1
+    return int(str(span_id)[-16:], 16) or 1
+
+
+# ---------------------------------------------------------------------------------------
+# OTLP/proto wire walker
+# ---------------------------------------------------------------------------------------
+
+def _varint(b: bytes, i: int) -> Tuple[int, int]:
+    v, shift = 0, 0
+    while True:
+        if i >= len(b):
+            raise ValueError("truncated varint")
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << shift
+        if not c & 0x80:
+            return v, i
+        shift += 7
+        if shift > 63:
+            raise ValueError("varint too long")
+
+
+def _fields(b: bytes) -> Iterator[Tuple[int, int, object]]:
+    """(field number, wire type, value) over one message's bytes."""
+    i, n = 0, len(b)
+    while i < n:
+        key, i = _varint(b, i)
+        fn, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _varint(b, i)
+        elif wt == 1:
+            if i + 8 > n:
+                raise ValueError("truncated fixed64")
+            v = struct.unpack_from("<Q", b, i)[0]
+            i += 8
+        elif wt == 2:
+            ln, i = _varint(b, i)
+            if i + ln > n:
+                raise ValueError("truncated bytes")
+            v = b[i:i + ln]
+            i += ln
+        elif wt == 5:
+            if i + 4 > n:
+                raise ValueError("truncated fixed32")
+            v = struct.unpack_from("<I", b, i)[0]
+            i += 4
+        else:
+            raise ValueError(f"unsupported wire type {wt}")
+        yield fn, wt, v
+
+
+def _any_value(b: bytes):
+    for fn, wt, v in _fields(b):
+        if fn == 1:
+            return bytes(v).decode("utf-8", "replace")
+        if fn == 2:
+            return bool(v)
+        if fn == 3:
+            return v - (1 << 64) if v >= 1 << 63 else v
+        if fn == 4:
+            return struct.unpack("<d", struct.pack("<Q", v))[0]
+        if fn == 7:
+            return bytes(v)
+    return None
+
+
+def _attrs_pb(items: List[bytes]) -> Dict[str, object]:
+    out = {}
+    for kv in items:
+        k, val = "", None
+        for fn, _wt, v in _fields(kv):
+            if fn == 1:
+                k = bytes(v).decode("utf-8", "replace")
+            elif fn == 2:
+                val = _any_value(v)
+        if k:
+            out[k] = val
+    return out
+
+
+def parse_proto(body: bytes) -> List[Tuple[Dict[str, object], dict]]:
+    """ExportTraceServiceRequest bytes -> [(resource attributes, span dict)]."""
+    out = []
+    for fn, _wt, rs in _fields(body):
+        if fn != 1:
+            continue
+        res_attrs: Dict[str, object] = {}
+        scopes = []
+        for f2, _w2, v2 in _fields(rs):
+            if f2 == 1:  # Resource
+                res_attrs = _attrs_pb([v for f3, _w3, v in _fields(v2) if f3 == 1])
+            elif f2 == 2:  # ScopeSpans
+                scopes.append(v2)
+        for ss in scopes:
+            for f3, _w3, sp in _fields(ss):
+                if f3 != 2:
+                    continue
+                d: dict = {"attributes": []}
+                attrs = []
+                for f4, _w4, v4 in _fields(sp):
+                    if f4 == 1:
+                        d["traceId"] = bytes(v4)
+                    elif f4 == 2:
+                        d["spanId"] = bytes(v4)
+                    elif f4 == 4:
+                        d["parentSpanId"] = bytes(v4)
+                    elif f4 == 5:
+                        d["name"] = bytes(v4).decode("utf-8", "replace")
+                    elif f4 == 6:
+                        d["kind"] = v4
+                    elif f4 == 7:
+                        d["startTimeUnixNano"] = v4
+                    elif f4 == 8:
+                        d["endTimeUnixNano"] = v4
+                    elif f4 == 9:
+                        attrs.append(v4)
+                d["attrs"] = _attrs_pb(attrs)
+                out.append((res_attrs, d))
+    return out
+
+
+def _json_value(v: dict):
+    if not isinstance(v, dict):
+        return v
+    for k in ("stringValue", "boolValue", "doubleValue"):
+        if k in v:
+            return v[k]
+    if "intValue" in v:
+        return int(v["intValue"])
+    if "bytesValue" in v:
+        return v["bytesValue"]
+    return None
+
+
+def _attrs_json(items) -> Dict[str, object]:
+    return {a.get("key", ""): _json_value(a.get("value", {})) for a in (items or []) if a.get("key")}
+
+
+def parse_json(body: bytes) -> List[Tuple[Dict[str, object], dict]]:
+    """OTLP/JSON ExportTraceServiceRequest -> [(resource attributes, span dict)]."""
+    doc = json.loads(body or b"{}")
+    out = []
+    for rs in doc.get("resourceSpans", []) or []:
+        res_attrs = _attrs_json((rs.get("resource") or {}).get("attributes"))
+        for ss in rs.get("scopeSpans", rs.get("instrumentationLibrarySpans", [])) or []:
+            for sp in ss.get("spans", []) or []:
+                d = dict(sp)
+                d["attrs"] = _attrs_json(sp.get("attributes"))
+                out.append((res_attrs, d))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# span -> SPAN record mapping
+# ---------------------------------------------------------------------------------------
+
+@dataclass
+class GroupTable:
+    """service.name -> incident group id (first seen first); the last group collects overflow."""
+    cap: int
+    names: List[str] = field(default_factory=list)
+    ids: Dict[str, int] = field(default_factory=dict)
+    lock: threading.Lock = field(default_factory=threading.Lock)
+
+    def id(self, service: str) -> int:
+        with self.lock:
+            g = self.ids.get(service)
+            if g is None:
+                if len(self.names) < self.cap:
+                    g = len(self.names)
+                    self.names.append(service)
+                else:
+                    g = self.cap - 1
+                self.ids[service] = g
+            return g
+
+
+def _ipv4(v) -> int:
+    try:
+        a = ipaddress.ip_address(str(v))
+    except ValueError:
+        return 0
+    return int(a) if a.version == 4 else 0
+
+
+def _first(attrs: Dict[str, object], keys) -> object:
+    for k in keys:
+        if k in attrs and attrs[k] is not None:
+            return attrs[k]
+    return None
+
+
+class SpanMapper:
+    """OTLP spans -> SPAN records on the agent's ids."""
+
+    def __init__(self, groups: GroupTable, pod_id: Callable[[str], int], node_id: int = 0):
+        self.groups, self.pod_id, self.node_id = groups, pod_id, node_id
+
+    @staticmethod
+    def is_request_span(d: dict) -> bool:
+        attrs = d.get("attrs", {})
+        return not d.get("parentSpanId") or any(k in attrs for k in TTFT_KEYS)
+
+    def records(self, spans: List[Tuple[Dict[str, object], dict]]) -> np.ndarray:
+        sel = [(r, d) for r, d in spans if self.is_request_span(d)]
+        out = np.zeros(len(sel), dtype=records.SPAN)
+        for i, (res, d) in enumerate(sel):
+            a = d["attrs"]
+            t0 = int(d.get("startTimeUnixNano") or 0)
+            t1 = int(d.get("endTimeUnixNano") or t0)
+            svc = str(_first(res, ("service.name",)) or _first(a, ("service.name",)) or "unknown")
+            pod = _first(res, ("k8s.pod.uid",)) or _first(res, ("k8s.pod.name",)) or ""
+            pid = _first(res, ("process.pid",)) or _first(a, ("process.pid", "thread.id")) or 0
+            ttft = _first(a, TTFT_KEYS)
+            sport = _first(a, ("client.port", "net.host.port", "net.sock.host.port")) or 0
+            dport = _first(a, ("server.port", "net.peer.port", "net.sock.peer.port")) or 0
+            dip = _ipv4(_first(a, ("server.address", "net.peer.ip", "net.sock.peer.addr")) or "")
+            g = self.groups.id(svc)
+            out[i]["ts_ns"] = t0
+            out[i]["trace_h"] = trace_hash(d.get("traceId"))
+            out[i]["span_h"] = span_hash(d.get("spanId"))
+            out[i]["pid"] = int(pid)
+            out[i]["pod_id"] = self.pod_id(str(pod)) if pod else 0
+            out[i]["node_id"] = self.node_id
+            out[i]["svc_id"] = g + 1
+            out[i]["group_id"] = g
+            out[i]["ttft_ms"] = float(ttft) if ttft is not None else np.nan
+            out[i]["latency_ms"] = (t1 - t0) / 1e6
+            if int(sport) or int(dport):
+                out[i]["conn_h"] = records.conn_hash(int(sport), int(dport), dip)
+        return out
+
+
+class OtlpSpanReceiver:
+    """POST /v1/traces -> span ring. ``push(records) -> n accepted`` is the ring's push (the
+    span ring is multi-producer: services may also push records directly)."""
+
+    def __init__(self, bind: str, mapper: SpanMapper, push: Callable[[np.ndarray], int]):
+        self.mapper, self.push = mapper, push
+        host, _, port = bind.rpartition(":")
+        self.addr = (host or "127.0.0.1", int(port))
+        self.accepted = self.rejected = self.dropped = self.requests = 0
+        self._lock = threading.Lock()
+        self._srv: Optional[http.server.ThreadingHTTPServer] = None
+        self._thr: Optional[threading.Thread] = None
+
+    def ingest(self, body: bytes, content_type: str) -> Tuple[int, int]:
+        """Parse one export request and push its request spans; (pushed, dropped)."""
+        ct = (content_type or "").split(";")[0].strip().lower()
+        spans = parse_proto(body) if ct in ("application/x-protobuf", "application/protobuf") else parse_json(body)
+        recs = self.mapper.records(spans)
+        n = int(self.push(recs)) if len(recs) else 0
+        with self._lock:
+            self.requests += 1
+            self.accepted += n
+            self.dropped += len(recs) - n
+        return n, len(recs) - n
+
+    def start(self) -> "OtlpSpanReceiver":
+        rx = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *a):  # noqa: D401 - quiet
+                pass
+
+            def _reply(self, code: int, body: bytes, ctype: str) -> None:
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def do_POST(self):
+                if not self.path.startswith("/v1/traces"):
+                    self._reply(404, b"not found", "text/plain")
+                    return
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(n) if n > 0 else b""
+                ctype = self.headers.get("Content-Type", "application/json")
+                try:
+                    _, dropped = rx.ingest(body, ctype)
+                except (ValueError, KeyError, TypeError) as exc:
+                    with rx._lock:
+                        rx.rejected += 1
+                    self._reply(400, json.dumps({"error": str(exc)}).encode(), "application/json")
+                    return
+                if ctype.startswith("application/x-protobuf"):
+                    # ExportTraceServiceResponse{partial_success{rejected_spans}}: empty when none
+                    inner = b"\x08" + _enc_varint(dropped)
+                    msg = b"" if not dropped else b"\x0a" + _enc_varint(len(inner)) + inner
+                    self._reply(200, msg, "application/x-protobuf")
+                else:
+                    body = {} if not dropped else {"partialSuccess": {"rejectedSpans": str(dropped),
+                                                                      "errorMessage": "span ring full"}}
+                    self._reply(200, json.dumps(body).encode(), "application/json")
+
+        self._srv = http.server.ThreadingHTTPServer(self.addr, H)
+        self._srv.daemon_threads = True
+        self.addr = self._srv.server_address[:2]
+        self._thr = threading.Thread(target=self._srv.serve_forever, name="otlp-receiver", daemon=True)
+        self._thr.start()
+        return self
+
+    @property
+    def endpoint(self) -> str:
+        return f"http://{self.addr[0]}:{self.addr[1]}/v1/traces"
+
+    def stop(self) -> None:
+        if self._srv is not None:
+            self._srv.shutdown()
+            self._srv.server_close()
+            self._srv = None
+
+
+def _enc_varint(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)

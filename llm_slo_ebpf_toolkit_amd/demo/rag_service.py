@@ -125,24 +125,33 @@ class LlamaBackend:
 class SpanExporter:
     """Batched OTLP/HTTP JSON trace export (chat.request / chat.retrieval / chat.generation)."""
 
-    def __init__(self, endpoint: str, service: str = "rag-service", max_batch: int = 64):
+    def __init__(self, endpoint: str, service: str = "rag-service", max_batch: int = 64, resource=None):
         self.endpoint, self.service, self.max_batch = endpoint, service, max_batch
         self.buf: List[dict] = []
         self.lock = threading.Lock()
+        # resource identity the agent's OTLP receiver maps onto its pod / process ids
+        # (collector/otlp.py): pod uid / name and node from the downward API, this process's pid
+        res = {"service.name": service, "process.pid": os.getpid(),
+               "k8s.pod.uid": os.environ.get("POD_UID", ""), "k8s.pod.name": os.environ.get("POD_NAME", ""),
+               "k8s.node.name": os.environ.get("NODE_NAME", "")}
+        res.update(resource or {})
+        self.resource = [{"key": k, "value": self._val(v)} for k, v in res.items() if v not in ("", None)]
+
+    @staticmethod
+    def _val(v):
+        if isinstance(v, bool):
+            return {"boolValue": v}
+        if isinstance(v, int):
+            return {"intValue": str(v)}
+        if isinstance(v, float):
+            return {"doubleValue": v}
+        return {"stringValue": str(v)}
 
     @staticmethod
     def span(trace_id: str, span_id: str, parent: str, name: str, t0: int, t1: int, attrs: Dict[str, object]):
-        def val(v):
-            if isinstance(v, bool):
-                return {"boolValue": v}
-            if isinstance(v, int):
-                return {"intValue": str(v)}
-            if isinstance(v, float):
-                return {"doubleValue": v}
-            return {"stringValue": str(v)}
-
         d = {"traceId": trace_id, "spanId": span_id, "name": name, "kind": 2, "startTimeUnixNano": str(t0),
-             "endTimeUnixNano": str(t1), "attributes": [{"key": k, "value": val(v)} for k, v in attrs.items()]}
+             "endTimeUnixNano": str(t1),
+             "attributes": [{"key": k, "value": SpanExporter._val(v)} for k, v in attrs.items()]}
         if parent:
             d["parentSpanId"] = parent
         return d
@@ -164,8 +173,7 @@ class SpanExporter:
             self._post(batch)
 
     def _post(self, spans: List[dict]) -> None:
-        body = {"resourceSpans": [{"resource": {"attributes": [{"key": "service.name",
-                                                                "value": {"stringValue": self.service}}]},
+        body = {"resourceSpans": [{"resource": {"attributes": self.resource},
                                    "scopeSpans": [{"scope": {"name": "rag-service"}, "spans": spans}]}]}
         req = urllib.request.Request(self.endpoint, data=json.dumps(body).encode(), method="POST",
                                      headers={"Content-Type": "application/json"})
@@ -194,13 +202,13 @@ class BurnRate:
 
 class RagService:
     def __init__(self, backend, corpus_path: str = os.path.join(HERE, "fixtures", "corpus.json"),
-                 otlp_endpoint: str = "", node: str = "demo-node", pod: str = "demo-rag-service"):
+                 otlp_endpoint: str = "", node: str = "demo-node", pod: str = "demo-rag-service", resource=None):
         self.backend = backend
         with open(corpus_path) as fh:
             self.docs = json.load(fh)
         self.corr = Correlator()
         self.node, self.pod = node, pod
-        self.spans = SpanExporter(otlp_endpoint)
+        self.spans = SpanExporter(otlp_endpoint, resource=resource)
         self.burn = BurnRate()
         r = self.registry = Registry()
         ms = (5, 10, 25, 50, 100, 200, 400, 800, 1600, 3200)

@@ -1,0 +1,183 @@
+"""OTLP/HTTP span receiver (collector/otlp.py): OTLP/JSON and OTLP/proto export requests
+become SPAN records on the agent's ids in the span ring; the demo RAG service's exporter
+feeds it end to end (REF demo/rag-service/main.go:408-441 -> REF ebpfcorrelator)."""
+
+import json
+import struct
+import urllib.request
+
+import numpy as np
+
+from llm_slo_ebpf_toolkit_amd.collector import otlp, records
+from llm_slo_ebpf_toolkit_amd.signals.metadata import Interner
+
+TID = "4bf92f3577b34da6a3ce929d0e0e4736"
+
+
+# ---- a minimal OTLP/proto encoder (test side only) -------------------------------------
+def _v(n):
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def _ld(fn, payload):
+    return _v(fn << 3 | 2) + _v(len(payload)) + payload
+
+
+def _fx64(fn, x):
+    return _v(fn << 3 | 1) + struct.pack("<Q", x)
+
+
+def _kv(k, val):
+    if isinstance(val, str):
+        av = _ld(1, val.encode())
+    elif isinstance(val, float):
+        av = _fx64(4, struct.unpack("<Q", struct.pack("<d", val))[0])
+    else:
+        av = _v(3 << 3 | 0) + _v(val & (2**64 - 1))
+    return _ld(1, k.encode()) + _ld(2, av)
+
+
+def _span_pb(trace, span, parent, t0, t1, attrs):
+    b = _ld(1, bytes.fromhex(trace)) + _ld(2, bytes.fromhex(span))
+    if parent:
+        b += _ld(4, bytes.fromhex(parent))
+    b += _ld(5, b"chat.request") + _v(6 << 3) + _v(2) + _fx64(7, t0) + _fx64(8, t1)
+    for k, v in attrs.items():
+        b += _ld(9, _kv(k, v))
+    return b
+
+
+def _request_pb(resource, spans):
+    res = b"".join(_ld(1, _kv(k, v)) for k, v in resource.items())
+    ss = _ld(1, _ld(1, b"scope")) + b"".join(_ld(2, s) for s in spans)
+    return _ld(1, _ld(1, res) + _ld(2, ss))
+
+
+def _request_json(resource, spans):
+    def av(v):
+        if isinstance(v, str):
+            return {"stringValue": v}
+        if isinstance(v, float):
+            return {"doubleValue": v}
+        return {"intValue": str(v)}
+
+    return json.dumps({"resourceSpans": [{
+        "resource": {"attributes": [{"key": k, "value": av(v)} for k, v in resource.items()]},
+        "scopeSpans": [{"scope": {"name": "s"}, "spans": [
+            {"traceId": t, "spanId": s, **({"parentSpanId": p} if p else {}), "name": "x", "kind": 2,
+             "startTimeUnixNano": str(t0), "endTimeUnixNano": str(t1),
+             "attributes": [{"key": k, "value": av(v)} for k, v in a.items()]}
+            for t, s, p, t0, t1, a in spans]}]}]}).encode()
+
+
+RES = {"service.name": "rag-service", "k8s.pod.uid": "0f1e2d3c-4b5a-6978-8796-a5b4c3d2e1f0", "process.pid": 4242}
+SPANS = [
+    (TID, "00f067aa0ba902b7", "", 1_700_000_000_000_000_000, 1_700_000_000_250_000_000,
+     {"llm.slo.ttft_ms": 812.5, "client.port": 51000, "server.port": 443, "server.address": "10.0.0.7"}),
+    (TID, "00f067aa0ba902b8", "00f067aa0ba902b7", 1_700_000_000_010_000_000, 1_700_000_000_020_000_000, {}),
+    ("0af7651916cd43dd8448eb211c80319c", "b7ad6b7169203331", "", 1_700_000_000_500_000_000,
+     1_700_000_000_900_000_000, {}),
+]
+
+
+def _mapper(cap=4):
+    pods = Interner()
+    return otlp.SpanMapper(otlp.GroupTable(cap), pods.id, node_id=3), pods
+
+
+def _check(recs, pods):
+    assert len(recs) == 2  # the child span is not a request span
+    r = recs[0]
+    assert r["trace_h"] == int(TID[16:], 16) == otlp.trace_hash(TID)
+    assert r["ts_ns"] == SPANS[0][3] and abs(r["latency_ms"] - 250.0) < 1e-3
+    assert abs(r["ttft_ms"] - 812.5) < 1e-4 and np.isnan(recs[1]["ttft_ms"])
+    assert r["pid"] == 4242 and r["pod_id"] == pods.id(RES["k8s.pod.uid"]) == 1
+    assert r["group_id"] == 0 and r["svc_id"] == 1 and r["node_id"] == 3
+    assert r["conn_h"] == records.conn_hash(51000, 443, 0x0A000007)
+    assert r["span_h"] == 0x00F067AA0BA902B7
+    assert recs[1]["conn_h"] == 0
+
+
+def test_json_request_to_span_records():
+    m, pods = _mapper()
+    _check(m.records(otlp.parse_json(_request_json(RES, SPANS))), pods)
+
+
+def test_proto_request_to_span_records():
+    m, pods = _mapper()
+    body = _request_pb(RES, [_span_pb(*s) for s in SPANS])
+    _check(m.records(otlp.parse_proto(body)), pods)
+
+
+def test_groups_overflow_into_last():
+    g = otlp.GroupTable(2)
+    assert [g.id(s) for s in ("a", "b", "c", "a", "d")] == [0, 1, 1, 0, 1]
+    assert g.names == ["a", "b"]
+
+
+def test_receiver_http_into_span_ring():
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    ring = rt.HostRing(4, 64)
+    m, pods = _mapper()
+    rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push).start()
+    try:
+        for ctype, body in (("application/json", _request_json(RES, SPANS)),
+                            ("application/x-protobuf", _request_pb(RES, [_span_pb(*s) for s in SPANS]))):
+            req = urllib.request.Request(rx.endpoint, data=body, method="POST", headers={"Content-Type": ctype})
+            assert urllib.request.urlopen(req, timeout=5).status == 200
+        # the ring holds 4 records: a third request is accepted partially (ring full)
+        req = urllib.request.Request(rx.endpoint, data=_request_json(RES, SPANS), method="POST",
+                                     headers={"Content-Type": "application/json"})
+        resp = json.loads(urllib.request.urlopen(req, timeout=5).read())
+        assert resp["partialSuccess"]["rejectedSpans"] == "2"
+        bad = urllib.request.Request(rx.endpoint, data=b"\xff\xff", method="POST",
+                                     headers={"Content-Type": "application/x-protobuf"})
+        try:
+            urllib.request.urlopen(bad, timeout=5)
+            raise AssertionError("malformed protobuf accepted")
+        except urllib.error.HTTPError as e:
+            assert e.code == 400
+    finally:
+        rx.stop()
+    assert (rx.requests, rx.accepted, rx.dropped, rx.rejected) == (3, 4, 2, 1)
+    assert ring.size == 4
+    recs = ring.records_view()[: 4 * 64].view(records.SPAN)  # no wrap: the ring was empty
+    _check(recs[:2], pods)
+    _check(recs[2:4], pods)
+
+
+def test_rag_service_spans_reach_the_ring():
+    """The demo service's OTLP exporter -> the agent's receiver -> SPAN records carrying the
+    request's trace hash, TTFT and the service's pod / pid."""
+    import os
+
+    from llm_slo_ebpf_toolkit_amd.demo.rag_service import RagService, StubBackend
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    ring = rt.HostRing(64, 64)
+    m, pods = _mapper()
+    rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push).start()
+    try:
+        svc = RagService(StubBackend(), otlp_endpoint=rx.endpoint, resource={"k8s.pod.uid": RES["k8s.pod.uid"]})
+        outs = [svc.chat({"prompt": f"why is ttft high {i}", "profile": "chat_short", "max_tokens": 2})
+                for i in range(3)]
+        svc.spans.flush()
+    finally:
+        rx.stop()
+    assert ring.size == 3  # one request span per chat (retrieval / generation children stay out)
+    buf = ring.records_view()[: 3 * 64].view(records.SPAN)
+    by_trace = {int(r["trace_h"]): r for r in buf}
+    for o in outs:
+        r = by_trace[otlp.trace_hash(o["trace_id"])]
+        assert abs(float(r["ttft_ms"]) - o["ttft_ms"]) < 1e-2
+        assert r["pid"] == os.getpid() and r["pod_id"] == pods.id(RES["k8s.pod.uid"])
+        assert r["group_id"] == 0
