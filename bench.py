@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--ring-mib", type=int, default=1024, help="emulated BPF ring buffer size (MiB, power of 2)")
     ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
     ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4))
+    ap.add_argument("--halo-ms", type=float, default=0.0,
+                    help="carry rows within this distance of a window's latest record into the next window")
+    ap.add_argument("--xchg-cap", type=int, default=-1,
+                    help="trace-tagged rows each GPU exchanges per window over RCCL (-1: events/8 when N > 1)")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -199,9 +203,11 @@ def main() -> int:
     # probes commit ahead of them) plus its user-space records: nothing may spill into the next window
     sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs + himgs)
     user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
+    xchg = (a.events // 8 if world > 1 else 0) if a.xchg_cap < 0 else a.xchg_cap
+    import_cap = (sig_cap if a.halo_ms > 0 else 0) + (world - 1) * xchg
     pipe = WindowPipeline(sig_cap, a.spans, a.services, local, comm, model=a.model, seed=a.seed,
                           use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,
-                          user_cap=min(user_cap, sig_cap))
+                          user_cap=min(user_cap, sig_cap), halo_ms=a.halo_ms, import_cap=import_cap, xchg_cap=xchg)
     # the producer publishes the epochs here (it runs ahead of the cuts): no cfg writes
     src = RingWindowSource(pipe, rb, user, spans, cfg_set=lambda i, v: None)
     keys = np.array(sorted(pod_sn), dtype=np.uint32)
@@ -339,7 +345,10 @@ def main() -> int:
             "model": f"config5: 16 signals (12 kernel + 4 GPU) x 10 fault domains, {a.model}, 4-tier LDS join",
             "global_batch": world * a.events,
             "seq_len": 1000,
-            "parallelism": f"dp{world} (node-sharded event streams, RCCL packet all-reduce)",
+            "parallelism": f"dp{world} (node-sharded event streams; RCCL per window: packet all-reduce, incident "
+                           f"all-gather{', trace-row exchange' if world > 1 and xchg else ''})",
+            "halo_ms": a.halo_ms,
+            "xchg_rows_per_gpu": xchg,
             "spans_per_window_per_gpu": a.spans,
             "incidents_per_window_per_gpu": a.services,
             "scenario": a.scenario,

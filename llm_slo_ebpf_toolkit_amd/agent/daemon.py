@@ -167,6 +167,7 @@ class AgentOptions:
     ttft_slo_ms: float = 800.0           # per-incident SLO: a span breaches when its TTFT exceeds this
     slo_target: float = 0.99             # TTFT SLO objective (burn rate = breach fraction / (1 - target))
     otlp_receiver_bind: str = ""         # OTLP/HTTP /v1/traces receiver feeding the span ring ("" = off)
+    halo_ms: float = 2000.0              # carry records this close to a window's end into the next window
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -461,8 +462,13 @@ class Agent:
         node_id = (abs(hash(o.node)) % 0xFFFE) + 1
         maps.init(node_id)
         budget = o.window_events + o.window_events // 4  # events plus the definitions ahead of them
+        multi = comm is not None and comm[2] > 1
+        # joins reach across the window cut (halo) and, on a multi-GPU node, across GPUs
+        # (trace-tagged rows exchanged over RCCL); imports are bounded by one window's records
         pipe = WindowPipeline(budget, o.window_spans, o.window_groups, o.device, comm, model=o.model, learn=False,
-                              window_ms=2000.0, user_cap=max(1024, o.window_events // 4), ttft_slo_ms=o.ttft_slo_ms)
+                              window_ms=2000.0, user_cap=max(1024, o.window_events // 4), ttft_slo_ms=o.ttft_slo_ms,
+                              halo_ms=o.halo_ms, import_cap=budget if o.halo_ms > 0 or multi else 0,
+                              xchg_cap=budget // 8 if multi else 0)
         src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
         if pods is not None:
             pipe.eng.set_pods(*pods)
@@ -497,10 +503,8 @@ class Agent:
             if pending is not None:
                 self._emit_window(pipe, *pending)
             pending = (k, cut.t_ns, G, names, ring, host_us)
-            if self.windows_done and self.windows_done % 64 == 0:
-                pipe.eng.rotate_traces()  # trace-id mappings live 64-128 windows
-                if o.source == "bpf":
-                    self._scan_pods(maps)
+            if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
+                self._scan_pods(maps)  # pod churn
             self._guard_tick()
             self.metrics.set_heartbeat()
             self.windows_done += 1

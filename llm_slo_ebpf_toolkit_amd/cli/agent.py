@@ -61,6 +61,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("ttft-slo-ms", d.ttft_slo_ms, "per-incident TTFT SLO (ms) for burn rates"),
         ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),
         ("otlp-receiver-bind", d.otlp_receiver_bind, "OTLP/HTTP /v1/traces receiver feeding the span ring (gpu engine)"),
+        ("halo-ms", d.halo_ms, "gpu engine: records this close to a window's end also join the next window (0 = off)"),
     ]:
         p.flag(name, default, help_)
     a = p.parse_args(argv)
@@ -77,7 +78,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
-        otlp_receiver_bind=a.otlp_receiver_bind)
+        otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms))
     return o, a.probe_smoke
 
 

@@ -60,8 +60,8 @@ TS_ZERO = 0xFFFFFFFF  # ts_off of a zero timestamp (never joins)
 
 # 16-byte record (= probes/ebpf/mislo_record.h mislo_event16): ts = base[tag] + ts_off, the
 # window carrying its last 4 epoch bases (counts[4..5], counts[8..13]); context id into the
-# device context table; trace id shared with the window's spans (kernel ids < 2^29, ids the
-# agent assigns >= 2^29).
+# device context table; trace id shared with the window's spans (kernel ids < 2^24, ids the
+# agent assigns >= 2^24).
 EVENT16 = np.dtype([
     ("ts_off", "<u4"),       # 0  ns since the tagged epoch base, TS_ZERO = zero timestamp
     ("ctx_type", "<u4"),     # 4  bits 0-7 signal type, 8-31 context id
@@ -121,7 +121,7 @@ def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,)
 assert EVENT16.itemsize == 16
 DEF_TRACE, DEF_CTX, DEF_FIRST = 0xFD, 0xFE, 0xF0  # definition record types (low byte of ctx_type)
 KERNEL_CTX_LIMIT = 1 << 23     # kernel context ids 1 .. 2^23 - 1, host ids above
-KERNEL_TRACE_LIMIT = 1 << 29   # kernel trace ids 1 .. 2^29 - 1, host ids above
+KERNEL_TRACE_LIMIT = 1 << 24   # kernel trace ids 1 .. 2^24 - 1, host ids above
 CTX_IDS = 1 << 24
 WIRE_DTYPES = {64: EVENT, 16: EVENT16}
 RB_BUSY, RB_DISCARD, RB_HDR = 1 << 31, 1 << 30, 8   # BPF ring buffer record header bits
@@ -442,7 +442,7 @@ def _as16(rows):
 class HostEncoderModel:
     """Python reference of the agent's id tables and host encoder (runtime/csrc/tables.h
     AgentTables): kernel context rows from definitions (svc|node from pod metadata), host context
-    ids from 2^23, trace ids shared with the kernel's definitions (host ids from 2^29), EVENT16
+    ids from 2^23, trace ids shared with the kernel's definitions (host ids from 2^24), EVENT16
     with per-record epoch choice, SPAN20, and the row patch in queue order."""
 
     def __init__(self):

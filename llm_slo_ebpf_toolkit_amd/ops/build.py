@@ -37,7 +37,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
-HIP_SOURCES = ["decode.hip", "join.hip", "posterior.hip", "gatestats.hip", "storm.hip"]
+HIP_SOURCES = ["decode.hip", "join.hip", "posterior.hip", "gatestats.hip", "storm.hip", "exchange.hip"]
 RT_SOURCES = ["ring.cpp", "replay.cpp", "pool.cpp", "bpfring.cpp", "probesim.cpp", "tables.cpp", "assemble.cpp",
               "bpfsys.cpp", "rt_bindings.cpp"]
 
@@ -115,7 +115,7 @@ def build_hip_ext(force: bool = False, jobs: int = 4) -> str:
     return out
 
 
-AGENT_KERNELS = ["decode.hip", "join.hip", "posterior.hip"]
+AGENT_KERNELS = ["decode.hip", "join.hip", "posterior.hip", "exchange.hip"]
 
 
 def build_agent_ext(force: bool = False, jobs: int = 4) -> str:

@@ -49,7 +49,7 @@ class PyEngine {
  public:
   PyEngine(int device, int sig_cap, int span_cap, int group_cap, int user_cap, int n_buffers, int max_ahead,
            double window_ms, double threshold, int fanout, int group_mode, bool use_graphs, bool device_refit,
-           int n_dom, float ttft_slo_ms) {
+           int n_dom, float ttft_slo_ms, double halo_ms, int import_cap, int xchg_cap) {
     EngineConfig c;
     c.device = device;
     c.sig_cap = sig_cap;
@@ -66,6 +66,9 @@ class PyEngine {
     c.device_refit = device_refit;
     c.n_dom = n_dom;
     c.ttft_slo_ms = ttft_slo_ms;
+    c.halo_ms = halo_ms;
+    c.import_cap = import_cap;
+    c.xchg_cap = xchg_cap;
     e_ = std::make_unique<WindowEngine>(c);
   }
   bool register_host(uintptr_t addr, size_t bytes) {
@@ -108,8 +111,31 @@ class PyEngine {
   }
   py::array_t<double> packet(int64_t k) { return copy_array(e_->packet(k), {kPacketLen}); }
   py::dict results(int64_t k, int n_groups) {
-    if (n_groups < 0 || n_groups > e_->config().group_cap) throw std::invalid_argument("n_groups");
-    const ResultView r = e_->results(k);
+    if (n_groups < 0 || n_groups > eng().config().group_cap) throw std::invalid_argument("n_groups");
+    return result_dict(e_->results(k), n_groups);
+  }
+  // every rank's results of window k (the node-wide incident list, all-gathered over RCCL)
+  py::list results_all(int64_t k, int n_groups) {
+    WindowEngine& e = eng();
+    if (n_groups < 0 || n_groups > e.config().group_cap) throw std::invalid_argument("n_groups");
+    const size_t G = e.config().group_cap, bytes = e.result_bytes();
+    const uint8_t* base = e.results_all(k);
+    const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
+    const size_t o_sli = o_ev + 16 * G * 4;
+    py::list out;
+    const int w = e.has_comm() ? e.world() : 1;
+    for (int r = 0; r < w; ++r) {
+      const uint8_t* p = base + (size_t)r * bytes;
+      out.append(result_dict(ResultView{reinterpret_cast<const double*>(p), reinterpret_cast<const double*>(p + o_gconf),
+                                        reinterpret_cast<const float*>(p + o_feat),
+                                        reinterpret_cast<const int32_t*>(p + o_pred),
+                                        reinterpret_cast<const uint32_t*>(p + o_ev),
+                                        reinterpret_cast<const uint32_t*>(p + o_sli)},
+                             n_groups));
+    }
+    return out;
+  }
+  static py::dict result_dict(const ResultView& r, int n_groups) {
     const py::ssize_t G = n_groups;
     py::dict d;
     d["post"] = copy_array(r.post, {G, 16});
@@ -140,7 +166,12 @@ class PyEngine {
     if (pods.size() != sn.size()) throw std::invalid_argument("pods / svcnode size mismatch");
     e_->set_pods(pods.data(), sn.data(), (size_t)pods.size());
   }
-  void rotate_traces() { e_->rotate_traces(); }
+  void inject_remote(py::buffer blocks, size_t stride, int world, int me) {
+    py::buffer_info bi = blocks.request();
+    if ((size_t)(bi.size * bi.itemsize) < stride * (size_t)std::max(world, 0)) throw std::invalid_argument("blocks too small");
+    py::gil_scoped_release nogil;
+    eng().inject_remote(bi.ptr, stride, world, me);
+  }
   void set_join_params(double window_ms, double threshold, int fanout, int group_mode) {
     e_->set_join_params(window_ms, threshold, fanout, group_mode);
   }
@@ -230,14 +261,17 @@ PYBIND11_MODULE(_mislo_agent, m) {
   m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
   m.attr("CTX_ROWS") = kCtxRows;
   m.attr("REC_STRIDE") = kRecStride;
+  m.attr("SIGREC_BYTES") = (int)sizeof(SigRec);
   m.attr("RING_STATE") = py::make_tuple("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events");
   py::class_<PyEngine>(m, "WindowEngine")
-      .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int, float>(),
+      .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int, float, double, int,
+                    int>(),
            py::arg("device") = 0, py::arg("sig_cap") = 1 << 20, py::arg("span_cap") = 16384, py::arg("group_cap") = 64,
            py::arg("user_cap") = 1 << 18, py::arg("n_buffers") = 3, py::arg("max_ahead") = 3,
            py::arg("window_ms") = 2000.0, py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1,
            py::arg("use_graphs") = true, py::arg("device_refit") = true, py::arg("n_dom") = 10,
-           py::arg("ttft_slo_ms") = 800.0f)
+           py::arg("ttft_slo_ms") = 800.0f, py::arg("halo_ms") = 0.0, py::arg("import_cap") = 0,
+           py::arg("xchg_cap") = 0)
       .def("register_host", &PyEngine::register_host)
       .def("submit", &PyEngine::submit, py::arg("k"), py::arg("kernel"), py::arg("user"), py::arg("spans"),
            py::arg("n_groups"), py::arg("labels") = py::none(), py::arg("bases") = std::vector<int64_t>{},
@@ -252,7 +286,8 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("set_model_bytes", &PyEngine::set_model_bytes)
       .def("set_p0", &PyEngine::set_p0)
       .def("set_pods", &PyEngine::set_pods)
-      .def("rotate_traces", &PyEngine::rotate_traces)
+      .def("inject_remote", &PyEngine::inject_remote)
+      .def("results_all", &PyEngine::results_all)
       .def("set_join_params", &PyEngine::set_join_params)
       .def("init_comm", &PyEngine::init_comm)
       .def("totals", &PyEngine::totals)
@@ -266,6 +301,8 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def_property_readonly("graphs", &PyEngine::graphs)
       .def_property_readonly("host_issue_us", &PyEngine::host_issue_us)
       .def_property_readonly("has_comm", &PyEngine::has_comm)
+      .def_property_readonly("rank", [](PyEngine& p) { return p.eng().rank(); })
+      .def_property_readonly("world", [](PyEngine& p) { return p.eng().world(); })
       .def_property_readonly("staged_bytes", &PyEngine::staged_bytes)
       .def_property_readonly("direct_bytes", &PyEngine::direct_bytes);
 }

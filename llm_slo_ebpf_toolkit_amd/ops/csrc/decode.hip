@@ -293,15 +293,16 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
 
 // One pass over the window's framed ring records (24-byte stride) before the decode: applies
 // the probes' id definitions -- context rows into the device context table (svc|node from the
-// device pod table), trace hash -> id into the device trace map -- and finds the first record
-// still being written (a consumer must stop there; the host re-submits the rest later).
+// device pod table), trace id -> hash into the device trace-id table -- and finds the first
+// record still being written (a consumer must stop there; the host re-submits the rest later).
+// A window holds at most one definition per id (ids are reused only after 2^24 new traces or
+// an agent-side context reset), so the stores need no ordering among themselves.
 __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ framed, const int* __restrict__ n_ptr,
                                                    uint4* __restrict__ ctx_tab, uint32_t ctx_rows,
-                                                   const uint32_t* __restrict__ pod_sn, uint32_t n_pods, TraceTab tt,
+                                                   const uint32_t* __restrict__ pod_sn, uint32_t n_pods, TraceIds tt,
                                                    uint32_t* __restrict__ rs) {
   const int n = n_ptr[15];  // framed records in this window
   uint32_t foreign = 0, dctx = 0, dtr = 0, disc = 0, busy = 0xFFFFFFFFu;
-  const uint32_t cur = *tt.cur & 1u;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const uint8_t* r = framed + (size_t)i * kRecStride;
     const uint2 h = *reinterpret_cast<const uint2*>(r);
@@ -327,15 +328,8 @@ __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ f
       }
     } else if (type == kDefTrace) {  // {id, type, hash lo, hash hi}
       const unsigned long long hash = (unsigned long long)b.x | ((unsigned long long)b.y << 32);
-      if (hash && a.x) {
-        uint32_t j = (uint32_t)splitmix64(hash) & tt.mask;
-        for (int probe = 0; probe <= (int)tt.mask; ++probe, j = (j + 1) & tt.mask) {
-          const unsigned long long prev = atomicCAS(&tt.key[cur][j], 0ull, hash);
-          if (prev == 0ull || prev == hash) {
-            tt.val[cur][j] = a.x;
-            break;
-          }
-        }
+      if (hash && a.x && a.x < tt.n) {
+        tt.hash[a.x] = hash;
         ++dtr;
       }
     }
@@ -359,31 +353,42 @@ __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ f
 // Rows [0, counts[15]) come from the framed ring records (EVENT16 payloads; definitions,
 // discarded, foreign and not-yet-committed records become holes: no counters, no join keys),
 // rows [counts[15], counts[0]) from the user-space producers' 64-byte EVENT records, whose
-// trace hashes are translated through the device trace map and whose connection keys fold to
-// the conn32 of the context rows, so both kinds of record join the same spans identically.
+// connection keys fold to the conn32 of the context rows (kernel records' trace ids become
+// their hashes through the trace-id table; user records carry hashes), so both kinds of record
+// join the same spans identically; rows [counts[0], rows[0]) are imported SigRecs (the halo of
+// the previous window, other GPUs' trace-tagged records): decoded for the join only.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict__ framed,
                                                       const Event* __restrict__ user, const int* __restrict__ n_ptr,
-                                                      int cap, const uint4* __restrict__ ctx_tab, int n_ctx,
-                                                      TraceTab tt, uint32_t* __restrict__ rs, DecodeOut o) {
+                                                      const int* __restrict__ rows, int cap,
+                                                      const SigRec* __restrict__ imp,
+                                                      const uint4* __restrict__ ctx_tab, int n_ctx, TraceIds tt,
+                                                      uint32_t* __restrict__ rs, unsigned long long* __restrict__ tmax,
+                                                      DecodeOut o) {
   __shared__ DecodeLds L;
   lds_init<NT>(L);
   const LdsLane l = lds_lane(L);
-  const int n = min(n_ptr[0], cap);
-  const int n_k = min(n_ptr[15], n);
+  const int n = min(rows[0], cap);
+  const int n_loc = min(n_ptr[0], n);
+  const int n_k = min(n_ptr[15], n_loc);
   const int valid_k = min((int)min((uint32_t)n_k, rs[kRsFirstBusy]), n_k);
   auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
   const int64_t t_base[4] = {base_at(4), base_at(8), base_at(10), base_at(12)};
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0, events = 0;
+  unsigned long long t_hi = 0;
   __shared__ uint4 s_stage[NT * 5];
   const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
   const int trips = end > beg ? (end - beg + NT - 1) / NT : 0;
   int i = beg + threadIdx.x;
   for (int it = 0; it < trips; ++it, i += NT) {
     if (i < end) {
-      if (i < n_k) {
+      if (i >= n_loc) {  // imported row: joins, never counted
+        const SigRec& m = imp[i - n_loc];
+        decode_one(i, cap, m.ts, m.val, m.slot == kNoSlot ? -1 : (int)m.slot, m.tr, m.pod, m.pid, m.sn, m.cn, o, l,
+                   unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+      } else if (i < n_k) {
         const uint8_t* r = framed + (size_t)i * kRecStride;
         const uint2 h = *reinterpret_cast<const uint2*>(r);
         const uint2 a = *reinterpret_cast<const uint2*>(r + 8), b = *reinterpret_cast<const uint2*>(r + 16);
@@ -394,8 +399,10 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
           const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
           const uint32_t cid = e.ctx_type >> 8;
           const uint4 cx = cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
-          decode_one(i, cap, wire_ts(e, t_base), (float)((double)e.value_milli * 1e-3), slot, wire_trace(e), cx.x,
-                     cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+          const int64_t ts = wire_ts(e, t_base);
+          decode_one(i, cap, ts, (float)((double)e.value_milli * 1e-3), slot, trace_of(tt, (uint32_t)wire_trace(e)),
+                     cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+          if (slot >= 0 && ts > 0) t_hi = max(t_hi, (unsigned long long)ts);
           ++events;
         } else {  // a hole: never counted, never joined
           decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
@@ -407,8 +414,9 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const float val = slot >= 0 ? (float)((double)e.value * (double)L.tab.scale[slot]) : (float)e.value;
         const uint64_t ck = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
         const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
-        decode_one(i, cap, e.ts_ns, val, slot, trace_key(tt, e.trace_h), e.pod_id, e.pid, svcnode, conn32(ck), o, l,
-                   unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+        decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, conn32(ck), o, l, unsupported,
+                   zero_ts, true, &s_stage[threadIdx.x * 5]);
+        if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
         ++events;
       }
     }
@@ -426,8 +434,14 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
     }
     __syncthreads();
   }
-  for (int off = 32; off > 0; off >>= 1) events += __shfl_xor(events, off);
-  if ((threadIdx.x & 63) == 0 && events) atomicAdd(&rs[kRsEvents], (uint32_t)events);
+  for (int off = 32; off > 0; off >>= 1) {
+    events += __shfl_xor(events, off);
+    t_hi = max(t_hi, (unsigned long long)__shfl_xor((long long)t_hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (events) atomicAdd(&rs[kRsEvents], (uint32_t)events);
+    if (t_hi) atomicMax(tmax, t_hi);
+  }
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
@@ -491,9 +505,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
     } else {
       const Span s = sp[i];
       r.ts = s.ts_ns;
-      // native engine: trace hashes through the device trace map, connections as conn32
-      r.tr = sm.tt.key[0] ? trace_key(sm.tt, s.trace_h) : s.trace_h;
-      r.cn = sm.tt.key[0] ? (uint64_t)conn32(s.conn_h) : s.conn_h;
+      // native engine: connections as conn32 (the context rows' identity); trace hashes as is
+      r.tr = s.trace_h;
+      r.cn = sm.native ? (uint64_t)conn32(s.conn_h) : s.conn_h;
       if (sm.grp_sli && s.group_id < (uint32_t)sm.n_groups) {  // per-incident TTFT SLO accounting
         atomicAdd(&sm.grp_sli[2 * s.group_id], 1u);
         if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sm.grp_sli[2 * s.group_id + 1], 1u);
@@ -570,7 +584,7 @@ void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCo
 }
 
 void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t* ctx_tab, uint32_t ctx_rows,
-                      const uint32_t* pod_sn, uint32_t n_pods, const TraceTab& tt, uint32_t* ring_state,
+                      const uint32_t* pod_sn, uint32_t n_pods, const TraceIds& tt, uint32_t* ring_state,
                       hipStream_t stream) {
   int g = (cap + 2047) / 2048;
   g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
@@ -578,13 +592,15 @@ void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t
                      ctx_rows, pod_sn, n_pods, tt, ring_state);
 }
 
-void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, int cap, const uint32_t* ctx_tab,
-                          int n_ctx, const TraceTab& tt, uint32_t* ring_state, const SignalCols& cols, uint32_t* hist,
+void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, const int* rows, int cap,
+                          const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
+                          uint32_t* ring_state, unsigned long long* tmax, const SignalCols& cols, uint32_t* hist,
                           uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
   constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_window<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, framed,
-                     (const Event*)user, n_dev, cap, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, tt, ring_state, o);
+                     (const Event*)user, n_dev, rows, cap, imp, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, tt,
+                     ring_state, tmax, o);
 }
 
 }  // namespace mislo

@@ -12,8 +12,14 @@
 //                    join -> finalize -> K3 MFMA posterior (+ confusion, + MFMA sufficient
 //                    statistics when learning) -> pack(packet b) -> D2H of the per-incident
 //                    results into pinned results b
-//   comm stream    : RCCL all-reduce(packet b) over xGMI when the node has several GPUs ->
-//                    totals += packet b -> D2H(packet b)
+//   comm stream    : one RCCL group over xGMI when the node has several GPUs: all-reduce(packet
+//                    b), all-gather of the window's incident results (node-wide incident list),
+//                    all-gather of the trace-tagged rows (merged into window k+1's imports) ->
+//                    totals += packet b -> D2H(packet b, all ranks' results)
+//
+// Imported rows: window k+1 also joins (never counts) the rows of window k within the join
+// window of its latest record (the halo, halo_ms) and the other GPUs' trace-tagged rows of
+// window k (exchange.hip), so joins across window and GPU boundaries match.
 //
 // so the DMA of window k+1 and the node-wide all-reduce of window k run under the kernels of
 // window k+1. The whole compute chain of a buffer is captured once into a HIP graph and
@@ -46,7 +52,7 @@ constexpr int kStatsOff = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg
 constexpr int kStatsLen = kPacketStats + kPacketCount;  // accumulated-statistics vector (f64[1040])
 constexpr uint32_t kCtxRows = 1u << 24;                 // device context table rows (256 MiB)
 constexpr uint32_t kPodRows = 1u << 20;                 // device pod table: pod id -> svc<<16|node
-constexpr uint32_t kTraceSlots = 1u << 21;              // device trace map slots per generation
+constexpr uint32_t kTraceIdRows = 1u << 24;             // device trace id -> hash table (128 MiB)
 constexpr int kHeadBytes = 64;                          // counts int32[16] (labels follow)
 
 // A host byte range to DMA (a ring segment): registered memory goes straight to the device,
@@ -68,6 +74,9 @@ struct EngineConfig {
   double alpha = 2.0, prior_pseudo = 1.0;
   int n_dom = 10;
   float ttft_slo_ms = 800.0f;  // per-incident SLO impact: spans with TTFT above this breach
+  double halo_ms = 0.0;        // carry rows this close to the window's latest record into the next window
+  int import_cap = 0;          // imported rows per window (halo + other GPUs' trace rows); 0 = none
+  int xchg_cap = 0;            // trace-tagged rows each GPU exchanges per window (RCCL); 0 = none
 };
 
 // per-incident results of a window, in one pinned block (one D2H)
@@ -118,10 +127,18 @@ class WindowEngine {
   void set_model_bytes(const void* bytes, size_t n);  // stream-ordered before the next window
   void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
   void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
-  void rotate_traces();                               // retire the older trace-map generation
+  // rows to import into the next window, as other GPUs' exchange blocks would deliver them
+  // (world blocks of [64-byte header: uint32 row count | rows], this rank's block skipped)
+  void inject_remote(const void* blocks, size_t stride, int world, int me);
   void set_join_params(double window_ms, double threshold, int fanout, int group_mode);
   void init_comm(const ncclUniqueId& id, int rank, int world);
   bool has_comm() const { return comm_ != nullptr; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  // all ranks' per-incident results of window k ([world] blocks of result_bytes(); this rank's
+  // alone without a communicator)
+  const uint8_t* results_all(int64_t k) const { return comm_ ? res_all_host_[k % nb_] : res_host_[k % nb_]; }
+  size_t result_bytes() const { return res_bytes_; }
 
   void totals(double* out);           // accumulated (all-reduced) packets (synchronous)
   void reset_totals();
@@ -147,11 +164,21 @@ class WindowEngine {
   size_t off_kern_ = 0, off_user_ = 0, off_span_ = 0, in_bytes_ = 0;  // device input block layout
   std::vector<std::pair<const uint8_t*, size_t>> registered_;
   size_t staged_bytes_ = 0, direct_bytes_ = 0;
-  uint32_t *pod_sn_ = nullptr, *pod_host_ = nullptr, *ring_state_ = nullptr, *trace_cur_ = nullptr,
-           *trace_cur_host_ = nullptr;
-  unsigned long long* trace_key_[2] = {nullptr, nullptr};
-  uint32_t* trace_val_[2] = {nullptr, nullptr};
+  uint32_t *pod_sn_ = nullptr, *pod_host_ = nullptr, *ring_state_ = nullptr;
+  unsigned long long* trace_hash_ = nullptr;  // kernel trace id -> hash
   uint32_t* sli_ = nullptr;
+  // imported rows: per buffer, [halo rows | remote rows]; counts per buffer
+  int n_rows_ = 0;                 // row capacity of the join = sig_cap + import_cap
+  int* rows_ = nullptr;            // device: rows of the current window
+  unsigned long long* tmax_ = nullptr;
+  std::vector<SigRec*> imp_;
+  uint32_t *halo_n_ = nullptr, *remote_n_ = nullptr, *sel_cnt_ = nullptr, *sel_off_ = nullptr;
+  uint8_t *xsend_ = nullptr, *xrecv_ = nullptr;
+  size_t xstride_ = 0;
+  int rank_ = 0, world_ = 1;
+  std::vector<uint8_t*> res_all_dev_, res_all_host_;
+  std::vector<hipEvent_t> xchg_done_;
+  bool exchange() const { return comm_ && cfg_.xchg_cap > 0 && cfg_.import_cap > 0; }
   JoinParams jp_{};
   int nblk_sig_ = 1, nblk_span_ = 1;
   hipStream_t copy_ = nullptr, compute_ = nullptr, comm_stream_ = nullptr;
@@ -162,7 +189,7 @@ class WindowEngine {
   std::vector<uint8_t*> staging_;    // per buffer: pinned staging for unregistered ranges
   std::vector<double*> packet_dev_;
   std::vector<double*> packet_host_;
-  std::vector<uint8_t*> res_dev_, res_host_;
+  std::vector<uint8_t*> res_dev_, res_host_;  // per buffer
   size_t res_bytes_ = 0;
   uint32_t* ctx_tab_ = nullptr;
   double *totals_ = nullptr, *stats_acc_ = nullptr, *p0_ = nullptr;

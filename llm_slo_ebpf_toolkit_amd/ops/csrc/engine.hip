@@ -31,7 +31,7 @@ struct FillSeg {
   uint32_t n;  // 32-bit words
   uint32_t value;
 };
-constexpr int kMaxFill = 12;
+constexpr int kMaxFill = 14;
 struct FillList {
   FillSeg seg[kMaxFill];
   int count;
@@ -100,6 +100,9 @@ WindowEngine::WindowEngine(const EngineConfig& cfg) : cfg_(cfg) {
   nb_ = std::max(2, cfg.n_buffers);
   max_ahead_ = std::min(nb_, std::max(1, cfg.max_ahead));
   if (cfg.user_cap <= 0 || cfg.user_cap > cfg.sig_cap) throw std::invalid_argument("user_cap must be in [1, sig_cap]");
+  if (cfg.import_cap < 0 || cfg.xchg_cap < 0 || cfg.halo_ms < 0) throw std::invalid_argument("negative import sizes");
+  if ((long long)cfg.sig_cap + cfg.import_cap >= (1LL << 27))
+    throw std::invalid_argument("sig_cap + import_cap must be < 2^27 (top-3 key packing)");
   HIPCHECK(hipSetDevice(cfg.device));
   set_join_params(cfg.window_ms, cfg.threshold, cfg.fanout, cfg.group_mode);
   alloc();
@@ -124,7 +127,9 @@ void WindowEngine::set_join_params(double window_ms, double threshold, int fanou
 }
 
 void WindowEngine::alloc() {
-  const int64_t N = cfg_.sig_cap, S = cfg_.span_cap, G = cfg_.group_cap;
+  const int64_t S = cfg_.span_cap, G = cfg_.group_cap;
+  n_rows_ = cfg_.sig_cap + cfg_.import_cap;  // the join's rows: the window's records + imported rows
+  const int64_t N = n_rows_;
   nblk_sig_ = decode_grid((int)N);
   nblk_span_ = decode_grid((int)S);
   HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
@@ -133,7 +138,7 @@ void WindowEngine::alloc() {
   // device input block per buffer: [head (counts + labels) | framed ring records | user records | spans]
   const size_t head = (kHeadBytes + 4 * (size_t)G + 63) & ~size_t(63);
   off_kern_ = head;
-  off_user_ = (off_kern_ + (size_t)kRecStride * N + 63) & ~size_t(63);
+  off_user_ = (off_kern_ + (size_t)kRecStride * cfg_.sig_cap + 63) & ~size_t(63);
   off_span_ = off_user_ + 64 * (size_t)cfg_.user_cap;
   in_bytes_ = off_span_ + 64 * (size_t)S;
   for (int b = 0; b < nb_; ++b) {
@@ -169,16 +174,11 @@ void WindowEngine::alloc() {
     std::memset(h, 0, res_bytes_);
     res_host_.push_back(static_cast<uint8_t*>(h));
   }
-  res_dev_.push_back(dalloc<uint8_t>(res_bytes_));
-  uint8_t* r = res_dev_[0];
-  post_ = reinterpret_cast<double*>(r);
-  gconf_ = reinterpret_cast<double*>(r + o_gconf);
-  feat_ = reinterpret_cast<float*>(r + o_feat);
-  pred_ = reinterpret_cast<int32_t*>(r + o_pred);
-  evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
-  sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
-  HIPCHECK(hipMemset(r, 0, res_bytes_));
-  // pod metadata, ring accounting, the two-generation trace map
+  for (int b = 0; b < nb_; ++b) {  // per buffer: the comm stream gathers window k's while k+1 computes
+    res_dev_.push_back(dalloc<uint8_t>(res_bytes_));
+    HIPCHECK(hipMemset(res_dev_.back(), 0, res_bytes_));
+  }
+  // pod metadata, ring accounting, the trace id -> hash table
   pod_sn_ = dalloc<uint32_t>(kPodRows);
   HIPCHECK(hipMemset(pod_sn_, 0, kPodRows * 4));
   {
@@ -186,17 +186,24 @@ void WindowEngine::alloc() {
     HIPCHECK(hipHostMalloc(&h, kPodRows * 4, hipHostMallocDefault));
     std::memset(h, 0, kPodRows * 4);
     pod_host_ = static_cast<uint32_t*>(h);
-    HIPCHECK(hipHostMalloc(&h, 64, hipHostMallocDefault));
-    std::memset(h, 0, 64);
-    trace_cur_host_ = static_cast<uint32_t*>(h);
   }
   ring_state_ = dalloc<uint32_t>(kRsLen);
-  trace_cur_ = dalloc<uint32_t>(16);
-  HIPCHECK(hipMemset(trace_cur_, 0, 64));
-  for (int g = 0; g < 2; ++g) {
-    trace_key_[g] = dalloc<unsigned long long>(kTraceSlots);
-    trace_val_[g] = dalloc<uint32_t>(kTraceSlots);
-    HIPCHECK(hipMemset(trace_key_[g], 0, kTraceSlots * 8));
+  trace_hash_ = dalloc<unsigned long long>(kTraceIdRows);
+  HIPCHECK(hipMemset(trace_hash_, 0, (size_t)kTraceIdRows * 8));
+  // imported rows (halo + other GPUs' trace rows) and the selections that produce them
+  rows_ = dalloc<int>(16);
+  tmax_ = dalloc<unsigned long long>(1);
+  halo_n_ = dalloc<uint32_t>(nb_);
+  remote_n_ = dalloc<uint32_t>(nb_);
+  HIPCHECK(hipMemset(halo_n_, 0, nb_ * 4));
+  HIPCHECK(hipMemset(remote_n_, 0, nb_ * 4));
+  sel_cnt_ = dalloc<uint32_t>(1024);
+  sel_off_ = dalloc<uint32_t>(1024);
+  for (int b = 0; b < nb_; ++b) imp_.push_back(cfg_.import_cap ? dalloc<SigRec>(cfg_.import_cap) : nullptr);
+  xstride_ = sizeof(SigRec) * (1 + (size_t)cfg_.xchg_cap);  // [header: row count | rows]
+  if (cfg_.xchg_cap) {
+    xsend_ = dalloc<uint8_t>(xstride_);
+    HIPCHECK(hipMemset(xsend_, 0, xstride_));
   }
   // context table: every id the kernel or the host encoder can assign, HBM-resident
   ctx_tab_ = dalloc<uint32_t>((size_t)kCtxRows * 4);
@@ -261,7 +268,11 @@ WindowEngine::~WindowEngine() {
   for (auto p : staging_)
     if (p) hipHostFree(p);
   if (pod_host_) hipHostFree(pod_host_);
-  if (trace_cur_host_) hipHostFree(trace_cur_host_);
+  for (auto p : res_all_host_) hipHostFree(p);
+  for (auto p : res_all_dev_) hipFree(p);
+  for (auto p : imp_)
+    if (p) hipFree(p);
+  for (auto e : xchg_done_) hipEventDestroy(e);
   for (auto p : packet_host_) hipHostFree(p);
   for (auto p : res_host_) hipHostFree(p);
   for (auto p : model_host_) hipHostFree(p);
@@ -271,8 +282,8 @@ WindowEngine::~WindowEngine() {
   void* bufs[] = {ctx_tab_, totals_, stats_acc_, p0_, model_dev_, g_status_, g_part_, g_part_blk_, g_part_off_,
                   g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
                   s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
-                  hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_cur_,
-                  trace_key_[0], trace_key_[1], trace_val_[0], trace_val_[1]};
+                  hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_hash_,
+                  rows_, tmax_, halo_n_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_) hipStreamDestroy(copy_);
@@ -343,7 +354,18 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
   uint8_t* in = in_dev_[b];
   const int* counts = reinterpret_cast<const int*>(in);
   const int32_t* labels = reinterpret_cast<const int32_t*>(in + kHeadBytes);
-  const int N = cfg_.sig_cap, S = cfg_.span_cap, G = cfg_.group_cap;
+  const int N = n_rows_, S = cfg_.span_cap, G = cfg_.group_cap;
+  const int bn = (b + 1) % nb_;  // the next window's buffer (its imports are produced here)
+  // this buffer's per-incident results block
+  uint8_t* r = res_dev_[b];
+  const size_t o_gconf = 16 * (size_t)G * 8, o_feat = o_gconf + (size_t)G * 8, o_pred = o_feat + 16 * (size_t)G * 4;
+  const size_t o_ev = o_pred + (size_t)G * 4, o_sli = o_ev + 16 * (size_t)G * 4;
+  post_ = reinterpret_cast<double*>(r);
+  gconf_ = reinterpret_cast<double*>(r + o_gconf);
+  feat_ = reinterpret_cast<float*>(r + o_feat);
+  pred_ = reinterpret_cast<int32_t*>(r + o_pred);
+  evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
+  sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
   FillList fl{};
   auto add = [&](void* p, size_t bytes, uint32_t v) { fl.seg[fl.count++] = FillSeg{(uint32_t*)p, (uint32_t)(bytes / 4), v}; };
   add(hist_, kSlots * kBuckets * 4, 0);
@@ -358,18 +380,27 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
   add(gsum_, (size_t)kGroupStripes * G * kSlots * 8, 0);
   add(gcnt_, (size_t)kGroupStripes * G * kSlots * 4, 0);
   add(sli_, (size_t)G * 2 * 4, 0);
+  add(tmax_, 8, 0);
   hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, st, fl);
   FillList rs{};
   rs.seg[0] = FillSeg{ring_state_, 1, 0xFFFFFFFFu};  // first busy record: none
   rs.seg[1] = FillSeg{ring_state_ + 1, kRsLen - 1, 0};
   rs.count = 2;
   hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, rs);
-  const TraceTab tt{{trace_key_[0], trace_key_[1]}, {trace_val_[0], trace_val_[1]}, trace_cur_, kTraceSlots - 1};
-  launch_ring_defs(in + off_kern_, counts, N, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
-  launch_decode_window(in + off_kern_, in + off_user_, counts, N, ctx_tab_, (int)kCtxRows, tt, ring_state_, sig_cols(),
-                       hist_, status_, g_part_blk_, misc_, st);
-  launch_partition(g_part_, counts, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
-  const SpanMap sm{tt, sli_, G, cfg_.ttft_slo_ms};
+  launch_window_rows(counts, halo_n_ + b, remote_n_ + b, N, rows_, st);
+  const TraceIds tt{trace_hash_, kTraceIdRows};
+  launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
+  launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
+                       ring_state_, tmax_, sig_cols(), hist_, status_, g_part_blk_, misc_, st);
+  {  // this buffer's imports are consumed: the next producer rewrites both counts
+    FillList z{};
+    z.seg[0] = FillSeg{halo_n_ + b, 1, 0};
+    z.seg[1] = FillSeg{remote_n_ + b, 1, 0};
+    z.count = 2;
+    hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, z);
+  }
+  launch_partition(g_part_, rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
+  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms};
   launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
@@ -386,6 +417,15 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
                      confusion_, st);
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
                      stats_, stats_count_, ring_state_, packet_dev_[b]);
+  // the next window's imports: this window's rows within the join window of its latest record
+  if (cfg_.halo_ms > 0 && cfg_.import_cap > 0)
+    launch_select(g_rec_, rows_, counts, N, kSelHalo, tmax_, (long long)llround(cfg_.halo_ms * 1e6), sel_cnt_,
+                  sel_off_, imp_[bn], halo_n_ + bn, (uint32_t)cfg_.import_cap, false, st);
+  // this window's trace-tagged local rows for the other GPUs (gathered on the comm stream)
+  if (exchange())
+    launch_select(g_rec_, rows_, counts, N, kSelTrace, tmax_, 0, sel_cnt_, sel_off_,
+                  reinterpret_cast<SigRec*>(xsend_ + sizeof(SigRec)), reinterpret_cast<uint32_t*>(xsend_),
+                  (uint32_t)cfg_.xchg_cap, true, st);
 }
 
 void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bool learn) {
@@ -434,6 +474,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
+  // window k's imports include the other GPUs' rows of window k - 1 (merged on the comm stream)
+  if (exchange() && k >= 1) HIPCHECK(hipStreamWaitEvent(compute_, xchg_done_[(k - 1) % nb_], 0));
   HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
   if (cfg_.device_refit && k >= nb_) {
     // fold window k - nb's all-reduced statistics (packet b) and refit before window k: a
@@ -465,11 +507,26 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     }
   }
   // per-incident results of this window (the buffers are reused by the next window)
-  HIPCHECK(hipMemcpyAsync(res_host_[b], res_dev_[0], res_bytes_, hipMemcpyDeviceToHost, compute_));
+  HIPCHECK(hipMemcpyAsync(res_host_[b], res_dev_[b], res_bytes_, hipMemcpyDeviceToHost, compute_));
   HIPCHECK(hipEventRecord(t_comp1_[b], compute_));
   HIPCHECK(hipEventRecord(compute_done_[b], compute_));
   HIPCHECK(hipStreamWaitEvent(comm_stream_, compute_done_[b], 0));
-  if (comm_) NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen, ncclFloat64, ncclSum, comm_, comm_stream_));
+  if (comm_) {
+    // one group: node-wide packet, node-wide incident list, the trace-row exchange
+    NCCLCHECK(ncclGroupStart());
+    NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen, ncclFloat64, ncclSum, comm_, comm_stream_));
+    NCCLCHECK(ncclAllGather(res_dev_[b], res_all_dev_[b], res_bytes_, ncclUint8, comm_, comm_stream_));
+    if (exchange()) NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, comm_, comm_stream_));
+    NCCLCHECK(ncclGroupEnd());
+    if (exchange()) {
+      const int bn = (b + 1) % nb_;
+      launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[bn], halo_n_ + bn, remote_n_ + bn,
+                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, comm_stream_);
+      HIPCHECK(hipEventRecord(xchg_done_[b], comm_stream_));
+    }
+    HIPCHECK(hipMemcpyAsync(res_all_host_[b], res_all_dev_[b], res_bytes_ * world_, hipMemcpyDeviceToHost,
+                            comm_stream_));
+  }
   hipLaunchKernelGGL(k_accumulate, dim3((kPacketLen + 255) / 256), dim3(256), 0, comm_stream_, packet_dev_[b], totals_,
                      kPacketLen);
   HIPCHECK(hipMemcpyAsync(packet_host_[b], packet_dev_[b], kPacketLen * sizeof(double), hipMemcpyDeviceToHost,
@@ -531,21 +588,47 @@ void WindowEngine::set_pods(const uint32_t* pods, const uint32_t* svcnode, size_
   HIPCHECK(hipMemcpyAsync(pod_sn_, pod_host_, kPodRows * 4, hipMemcpyHostToDevice, compute_));
 }
 
-void WindowEngine::rotate_traces() {
-  // the older generation is cleared and becomes current (stream-ordered between windows);
-  // mappings live for one to two rotation periods
+void WindowEngine::inject_remote(const void* blocks, size_t stride, int world, int me) {
+  if (!cfg_.import_cap) throw std::logic_error("inject_remote needs import_cap > 0");
+  if (world < 1 || me < 0 || me >= world || stride < sizeof(SigRec)) throw std::invalid_argument("bad exchange blocks");
+  const uint8_t* h = static_cast<const uint8_t*>(blocks);
+  int max_rows = 0;
+  for (int r = 0; r < world; ++r) {  // the kernel trusts each block's header: check it here
+    uint32_t c;
+    std::memcpy(&c, h + (size_t)r * stride, 4);
+    if ((size_t)c * sizeof(SigRec) + sizeof(SigRec) > stride) throw std::invalid_argument("block row count exceeds stride");
+    max_rows = std::max(max_rows, (int)c);
+  }
+  const int bn = (int)(submitted_ % nb_);  // the next window's buffer
+  uint8_t* d = nullptr;
+  HIPCHECK(hipMalloc(&d, stride * world));
+  HIPCHECK(hipMemcpyAsync(d, blocks, stride * world, hipMemcpyHostToDevice, compute_));
+  launch_remote_merge(d, stride, world, me, imp_[bn], halo_n_ + bn, remote_n_ + bn, (uint32_t)cfg_.import_cap,
+                      max_rows, compute_);
   HIPCHECK(hipStreamSynchronize(compute_));
-  const uint32_t next = trace_cur_host_[0] ^ 1u;
-  HIPCHECK(hipMemsetAsync(trace_key_[next], 0, kTraceSlots * 8, compute_));
-  trace_cur_host_[0] = next;
-  HIPCHECK(hipMemcpyAsync(trace_cur_, trace_cur_host_, 4, hipMemcpyHostToDevice, compute_));
+  HIPCHECK(hipFree(d));
 }
 
 void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
   if (comm_) throw std::logic_error("communicator already initialised");
   if (world <= 1) return;
+  if (submitted_) throw std::logic_error("init_comm before the first window");
   HIPCHECK(hipSetDevice(cfg_.device));
   NCCLCHECK(ncclCommInitRank(&comm_, world, id, rank));
+  rank_ = rank;
+  world_ = world;
+  for (int b = 0; b < nb_; ++b) {
+    res_all_dev_.push_back(dalloc<uint8_t>(res_bytes_ * world));
+    void* h = nullptr;
+    HIPCHECK(hipHostMalloc(&h, res_bytes_ * world, hipHostMallocDefault));
+    std::memset(h, 0, res_bytes_ * world);
+    res_all_host_.push_back(static_cast<uint8_t*>(h));
+    xchg_done_.push_back(mk_event(false));
+  }
+  if (cfg_.xchg_cap) {
+    xrecv_ = dalloc<uint8_t>(xstride_ * world);
+    HIPCHECK(hipMemset(xrecv_, 0, xstride_ * world));
+  }
 }
 
 void WindowEngine::totals(double* out) {

@@ -38,8 +38,8 @@ static_assert(sizeof(Event) == 64, "Event must be 64 bytes");
 // BPF ring's records): timestamp as an offset from one of the window's 4 epoch bases, selected
 // by the 2-bit tag in the top of trace_id (ts = base[tag] + ts_off; counts[4..5], [8..13]);
 // workload identity as a context id into the device context table {pod, pid, conn32,
-// svc<<16|node}; the value in fixed point (1/1000 of the signal's output unit); a 30-bit trace
-// id shared with the window's spans (kernel ids < 2^29, host-assigned above). The probes stamp
+// svc<<16|node}; the value in fixed point (1/1000 of the signal's output unit); the kernel's
+// trace id (< 2^24, translated to its hash on decode, TraceIds). The probes stamp
 // offsets from the epoch the agent last published, so a record written across a window cut
 // still decodes exactly.
 struct alignas(16) EventC16 {
@@ -208,31 +208,17 @@ __host__ __device__ inline uint32_t conn32(uint64_t key) {
   return key ? ((uint32_t)(key ^ (key >> 32)) | 1u) : 0u;
 }
 
-// Device trace map: trace hash -> the kernel's trace id (from the probes' TRACE definitions),
-// two generations (lookups try both; inserts go to the current one; the host retires the
-// older one). User-space records and spans carry trace HASHES: a hash the kernel named maps
-// to its id, so they join the kernel's records exactly; any other hash keeps its own value
-// with bit 63 set, disjoint from the kernel's 30-bit ids.
-struct TraceTab {
-  unsigned long long* key[2];  // 0 = empty slot
-  uint32_t* val[2];
-  const uint32_t* cur;         // device word: current generation (0 / 1)
-  uint32_t mask;               // slots per generation - 1
+// Device trace-id table: the kernel's trace id -> the 64-bit trace hash it names (the probes'
+// TRACE definitions, applied in ring order before any record that uses the id). Kernel records
+// are translated to hashes on decode; user-space records and spans carry hashes already. Every
+// row of the join therefore keys on the hash, an identity that is the same on every node, so
+// records exchanged between GPUs join without any id translation. Ids wrap at 2^24 (records.h
+// kKernelTraceLimit): 128 MiB of HBM, written once per definition, read once per traced event.
+struct TraceIds {
+  unsigned long long* hash;  // [n], 0 = unknown id
+  uint32_t n;
 };
 
-__device__ inline uint64_t trace_key(const TraceTab& t, uint64_t h) {
-  if (!h) return 0;
-  const uint32_t c = *t.cur & 1u;
-  for (int q = 0; q < 2; ++q) {
-    const uint32_t g = q ? c ^ 1u : c;
-    uint32_t i = (uint32_t)splitmix64(h) & t.mask;
-    for (int probe = 0; probe < 64; ++probe, i = (i + 1) & t.mask) {
-      const unsigned long long k = t.key[g][i];
-      if (k == h) return t.val[g][i];
-      if (k == 0) break;
-    }
-  }
-  return h | (1ull << 63);
-}
+__device__ inline uint64_t trace_of(const TraceIds& t, uint32_t id) { return id && id < t.n ? t.hash[id] : 0ull; }
 
 }  // namespace mislo

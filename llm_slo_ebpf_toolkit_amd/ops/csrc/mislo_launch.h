@@ -34,11 +34,11 @@ void launch_decode_wire(const void* ev, const int* n_dev, int cap, const uint32_
 void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, uint32_t svcnode, uint64_t trace_h,
                        const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                        unsigned long long* misc, hipStream_t stream);
-// spans: SPAN20 (counts[7] == 20) or 64-byte SPAN; sm (optional, native engine): translate
-// trace hashes through the device trace map, fold connections to conn32, count per-group TTFT
-// SLO breaches
+// spans: SPAN20 (counts[7] == 20) or 64-byte SPAN; sm (optional, native engine): fold
+// connections to conn32 (the context rows' connection identity), count per-group TTFT SLO
+// breaches
 struct SpanMap {
-  TraceTab tt;           // tt.key[0] == nullptr: no translation
+  int native;            // 1: native engine spans (conn32 connections)
   uint32_t* grp_sli;     // [n_groups][2]: spans, TTFT > slo
   int n_groups;
   float ttft_slo_ms;
@@ -47,11 +47,26 @@ void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCo
                          const uint32_t* ctx_tab, int n_ctx, hipStream_t stream, const SpanMap* sm = nullptr);
 // native engine window: framed BPF ring records (counts[15] of them) + 64-byte user records
 void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t* ctx_tab, uint32_t ctx_rows,
-                      const uint32_t* pod_sn, uint32_t n_pods, const TraceTab& tt, uint32_t* ring_state,
+                      const uint32_t* pod_sn, uint32_t n_pods, const TraceIds& tt, uint32_t* ring_state,
                       hipStream_t stream);
-void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, int cap, const uint32_t* ctx_tab,
-                          int n_ctx, const TraceTab& tt, uint32_t* ring_state, const SignalCols& cols, uint32_t* hist,
+// rows [0, counts[15]) framed, [counts[15], counts[0]) user records, then rows[0] - counts[0]
+// imported rows (SigRec: the previous window's halo and other GPUs' trace-tagged records) that
+// join but are not counted; tmax (u64) receives the window's latest local timestamp
+void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, const int* rows, int cap,
+                          const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
+                          uint32_t* ring_state, unsigned long long* tmax, const SignalCols& cols, uint32_t* hist,
                           uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream);
+
+// exchange.hip: stable row selections (halo carry, trace-tagged rows for the GPU exchange)
+constexpr int kSelHalo = 0, kSelTrace = 1;
+int select_grid(int cap);
+void launch_select(const SigRec* rec, const int* rows, const int* counts, int cap, int mode,
+                   const unsigned long long* tmax, long long halo_ns, uint32_t* blk_cnt, uint32_t* blk_off,
+                   SigRec* out, uint32_t* n_out, uint32_t out_cap, bool clear_identity, hipStream_t stream);
+void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, const uint32_t* halo_n,
+                         uint32_t* remote_n, uint32_t imp_cap, int max_rows, hipStream_t stream);
+void launch_window_rows(const int* counts, const uint32_t* halo_n, const uint32_t* remote_n, int cap, int* rows,
+                        hipStream_t stream);
 
 // join.hip
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,

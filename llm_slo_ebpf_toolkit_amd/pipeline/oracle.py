@@ -111,18 +111,15 @@ def decode_w16(ev: np.ndarray, table: CtxTable, bases) -> Decoded:
 
 
 class TraceMap:
-    """Host mirror of the engine's device trace map (mislo_common.h TraceTab): the probes' TRACE
-    definitions name hashes; any other hash keeps its value with bit 63 set."""
+    """Host mirror of the engine's trace-id table (mislo_common.h TraceIds): the probes' TRACE
+    definitions name the hash behind each kernel trace id; kernel records decode to the hash,
+    user-space records and spans carry hashes already."""
 
     def __init__(self):
-        self.m: Dict[int, int] = {}
+        self.m: Dict[int, int] = {}  # kernel trace id -> hash
 
-    def key(self, h: int) -> int:
-        h = int(h)
-        return 0 if h == 0 else self.m.get(h, h | (1 << 63))
-
-    def keys(self, hs: np.ndarray) -> np.ndarray:
-        return np.array([self.key(h) for h in np.asarray(hs).tolist()], dtype=np.uint64)
+    def hashes(self, ids: np.ndarray) -> np.ndarray:
+        return np.array([self.m.get(int(i), 0) if i else 0 for i in np.asarray(ids).tolist()], dtype=np.uint64)
 
 
 def apply_ring_defs(framed: np.ndarray, table: CtxTable, tmap: TraceMap, pod_sn: Dict[int, int]) -> None:
@@ -134,18 +131,20 @@ def apply_ring_defs(framed: np.ndarray, table: CtxTable, tmap: TraceMap, pod_sn:
     for c32, ct, pod, pid in p[t == records.DEF_CTX].tolist():
         table.map[ct >> 8] = (pod, pid, c32, pod_sn.get(pod, 0))
     for tid, _ct, lo, hi in p[t == records.DEF_TRACE].tolist():
-        tmap.m[lo | (hi << 32)] = tid
+        if 0 < tid < records.KERNEL_TRACE_LIMIT:
+            tmap.m[tid] = lo | (hi << 32)
 
 
 def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases) -> Decoded:
     """k_decode_window: rows [0, n framed) from the framed ring records (definitions, discarded
-    and busy records are holes: ts 0, no slot), then the user-space 64-byte records with
-    translated trace ids and conn32 connections."""
+    and busy records are holes: ts 0, no slot; kernel trace ids become their hashes), then the
+    user-space 64-byte records (trace hashes as is, conn32 connections)."""
     r = np.ascontiguousarray(framed).view(np.uint32).reshape(-1, 6)
     n_k = r.shape[0]
     ev = r[:, 2:6].copy().view(records.EVENT16).reshape(-1)
     valid = (r[:, 0] == 16) & ((ev["ctx_type"] & np.uint32(0xFF)) < records.DEF_FIRST)
     d = decode_w16(ev, table, bases)
+    d.trace = tmap.hashes(d.trace)
     hole = ~valid
     for f, z in (("ts", 0), ("val", 0), ("slot", NO_SLOT), ("status", 0), ("pod", 0), ("pid", 0), ("svcnode", 0),
                  ("trace", 0), ("conn", 0)):
@@ -153,7 +152,6 @@ def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: T
     u = decode_events(user) if len(user) else None
     if u is None:
         return d
-    u.trace = tmap.keys(user["trace_h"])
     u.conn = records.conn32_np(u.conn).astype(np.uint64)
     cat = lambda a, b: np.concatenate([a, b])  # noqa: E731
     assert n_k == len(d.ts)
@@ -161,11 +159,97 @@ def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: T
                    cat(d.pid, u.pid), cat(d.svcnode, u.svcnode), cat(d.trace, u.trace), cat(d.conn, u.conn))
 
 
-def spans_native(spans: np.ndarray, tmap: TraceMap) -> np.ndarray:
-    """k_decode_spans in the native engine: trace hashes through the trace map, conn32."""
+def spans_native(spans: np.ndarray, tmap: TraceMap = None) -> np.ndarray:
+    """k_decode_spans in the native engine: trace hashes as is, connections as conn32."""
     out = spans.copy()
-    out["trace_h"] = tmap.keys(spans["trace_h"])
     out["conn_h"] = records.conn32_np(spans["conn_h"])
+    return out
+
+
+# ---- imported rows (ops/csrc/exchange.hip) ----------------------------------------------
+
+def concat(a: Decoded, b: Decoded) -> Decoded:
+    return Decoded(*(np.concatenate([getattr(a, f), getattr(b, f)]) for f in Decoded.__dataclass_fields__))
+
+
+def take(d: Decoded, m: np.ndarray) -> Decoded:
+    return Decoded(*(getattr(d, f)[m] for f in Decoded.__dataclass_fields__))
+
+
+def empty_rows() -> Decoded:
+    return Decoded(np.zeros(0, np.int64), np.zeros(0, np.float32), np.zeros(0, np.uint8), np.zeros(0, np.uint8),
+                   np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint64),
+                   np.zeros(0, np.uint64))
+
+
+def window_tmax(d: Decoded, n_local: int) -> int:
+    """Latest timestamp of the window's own joinable records (k_decode_window's tmax)."""
+    ts = d.ts[:n_local]
+    ok = (d.slot[:n_local] != NO_SLOT) & (ts > 0)
+    return int(ts[ok].max()) if ok.any() else 0
+
+
+def halo_rows(d: Decoded, n_local: int, halo_ns: int) -> Decoded:
+    """k_sel (halo): the window's rows (imports included) within halo_ns of its latest local
+    record, in row order."""
+    tmax = window_tmax(d, n_local)
+    if tmax == 0:
+        return empty_rows()
+    m = (d.slot != NO_SLOT) & (d.ts != 0) & (d.ts >= tmax - halo_ns)
+    return take(d, m)
+
+
+def trace_rows(d: Decoded, n_local: int) -> Decoded:
+    """k_sel (trace): the window's own trace-tagged joinable rows, identity cleared (a remote
+    GPU joins them by trace hash only), in row order."""
+    loc = take(d, np.arange(len(d.ts)) < n_local)
+    m = (loc.slot != NO_SLOT) & (loc.ts != 0) & (loc.trace != 0)
+    out = take(loc, m)
+    for f in ("pod", "pid", "svcnode"):
+        setattr(out, f, np.zeros_like(getattr(out, f)))
+    out.conn = np.zeros_like(out.conn)
+    return out
+
+
+def status_of(val: np.ndarray, slot: np.ndarray) -> np.ndarray:
+    warn = np.array([s.warn for s in catalog.SIGNALS] + [np.inf] * (16 - len(catalog.SIGNALS)), dtype=np.float32)
+    err = np.array([s.error for s in catalog.SIGNALS] + [np.inf] * (16 - len(catalog.SIGNALS)), dtype=np.float32)
+    ok = slot != NO_SLOT
+    sl = np.where(ok, slot, 0)
+    return np.where(ok, np.where(val >= err[sl], 2, np.where(val >= warn[sl], 1, 0)), 0).astype(np.uint8)
+
+
+SIGREC = np.dtype([("ts", "<i8"), ("tr", "<u8"), ("cn", "<u8"), ("pod", "<u4"), ("pid", "<u4"), ("sn", "<u4"),
+                   ("val", "<f4"), ("slot", "<u4"), ("pad", "<u4", (5,))])
+assert SIGREC.itemsize == 64
+
+
+def to_sigrec(d: Decoded) -> np.ndarray:
+    """Decoded rows as the engine's 64-byte SigRec rows (mislo_common.h)."""
+    out = np.zeros(len(d.ts), dtype=SIGREC)
+    out["ts"], out["tr"], out["cn"] = d.ts, d.trace, d.conn
+    out["pod"], out["pid"], out["sn"] = d.pod, d.pid, d.svcnode
+    out["val"] = d.val
+    out["slot"] = np.where(d.slot == NO_SLOT, 0xFF, d.slot).astype(np.uint32)
+    return out
+
+
+def from_sigrec(r: np.ndarray) -> Decoded:
+    slot = np.where(r["slot"] == 0xFF, NO_SLOT, r["slot"]).astype(np.uint8)
+    return Decoded(r["ts"].astype(np.int64), r["val"].astype(np.float32), slot, status_of(r["val"], slot),
+                   r["pod"].astype(np.uint32), r["pid"].astype(np.uint32), r["sn"].astype(np.uint32),
+                   r["tr"].astype(np.uint64), r["cn"].astype(np.uint64))
+
+
+def exchange_blocks(parts, cap: int) -> np.ndarray:
+    """Per-rank exchange blocks as the GPUs all-gather them: [64-byte header: row count | rows]."""
+    stride = 64 * (1 + cap)
+    out = np.zeros(len(parts) * stride, dtype=np.uint8)
+    for r, p in enumerate(parts):
+        rows = to_sigrec(p)[:cap]
+        blk = out[r * stride:(r + 1) * stride]
+        blk[:4] = np.frombuffer(np.uint32(len(rows)).tobytes(), dtype=np.uint8)
+        blk[64:64 + rows.nbytes] = rows.view(np.uint8)
     return out
 
 

@@ -80,12 +80,17 @@ def summarize(p: np.ndarray) -> Dict[str, object]:
 
 class WindowPipeline:
     """Python handle on one native WindowEngine (one MI355X). ``comm`` = (unique_id bytes,
-    rank, world) joins the node's RCCL communicator for the per-window packet all-reduce."""
+    rank, world) joins the node's RCCL communicator: per window, the packet all-reduce, the
+    all-gather of every GPU's incident results and (``xchg_cap``) of the trace-tagged rows
+    each GPU imports into its next window. ``halo_ms`` carries a window's rows within that
+    distance of its latest record into the next window (joins across the cut); ``import_cap``
+    bounds the imported rows (halo + remote) per window."""
 
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, comm=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, use_graphs: bool = True,
-                 max_ahead: int = 3, n_buffers: int = 3, user_cap: int = USER_CAP, ttft_slo_ms: float = 800.0):
+                 max_ahead: int = 3, n_buffers: int = 3, user_cap: int = USER_CAP, ttft_slo_ms: float = 800.0,
+                 halo_ms: float = 0.0, import_cap: int = 0, xchg_cap: int = 0):
         from ..ops import load_agent
         from ..ops.engine import model_bytes
 
@@ -100,7 +105,9 @@ class WindowPipeline:
                                          user_cap=user_cap, n_buffers=n_buffers, max_ahead=max_ahead,
                                          window_ms=window_ms, threshold=threshold, fanout=fanout,
                                          group_mode=group_mode, use_graphs=use_graphs,
-                                         device_refit=self.device_refit, n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms)
+                                         device_refit=self.device_refit, n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms,
+                                         halo_ms=halo_ms, import_cap=import_cap, xchg_cap=xchg_cap)
+        self.halo_ms, self.import_cap, self.xchg_cap = halo_ms, import_cap, xchg_cap
         self.nb = self.eng.buffers
         self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
         if comm is not None and comm[2] > 1:
@@ -156,6 +163,16 @@ class WindowPipeline:
     def results(self, k: int, n_groups: int) -> Dict[str, np.ndarray]:
         self.eng.wait(k)
         return self.eng.results(k, n_groups)
+
+    def results_all(self, k: int, n_groups: int) -> List[Dict[str, np.ndarray]]:
+        """Every GPU's incident results of window k (RCCL all-gather; this GPU's alone when the
+        node has one): the node-wide incident list."""
+        self.eng.wait(k)
+        return self.eng.results_all(k, n_groups)
+
+    def inject_remote(self, blocks: np.ndarray, world: int, me: int) -> None:
+        """Rows for the next window as other GPUs' exchange blocks deliver them (oracle.exchange_blocks)."""
+        self.eng.inject_remote(np.ascontiguousarray(blocks, dtype=np.uint8), len(blocks) // world, world, me)
 
     def window_ms(self, k: int):
         return self.eng.window_ms(k)

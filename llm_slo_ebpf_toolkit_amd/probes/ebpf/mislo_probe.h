@@ -14,7 +14,7 @@
  *                 the low 2 bits replaced by the epoch tag; the agent publishes one per window
  *                 cut and ships the last 4 bases with the window), [125] trace id counter,
  *                 [126] context id counter;
- *   mislo_traces  LRU trace hash -> trace id in 1 .. 2^29 - 1 (wrapping). LRU eviction only drops
+ *   mislo_traces  LRU trace hash -> trace id in 1 .. 2^24 - 1 (wrapping). LRU eviction only drops
  *                 traces idle far longer than the 2 s correlation window; a re-seen hash gets a
  *                 fresh id with a fresh definition;
  *   mislo_pods    cgroup id -> pod id (agent-populated from the kubelet / CRI);
@@ -188,7 +188,7 @@ static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32)
 	return id ? *id : 0;
 }
 
-/* trace hash -> trace id in 1 .. 2^29 - 1 (wrapping), definition first like mislo_ctx_id;
+/* trace hash -> trace id in 1 .. 2^24 - 1 (wrapping), definition first like mislo_ctx_id;
  * 0 for untraced events */
 static __always_inline __u32 mislo_trace_id(__u64 h)
 {

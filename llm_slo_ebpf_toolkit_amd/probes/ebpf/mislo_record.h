@@ -93,7 +93,7 @@ struct mislo_def16 {
 /* id spaces: the kernel assigns the low part, the agent's host-side encoders the rest, so both
  * kinds of producer share one device context table (2^24 rows) and one trace-id space */
 #define MISLO_KERNEL_CTX_LIMIT (1u << 23)   /* kernel context ids 1 .. 2^23 - 1 */
-#define MISLO_KERNEL_TRACE_LIMIT (1u << 29) /* kernel trace ids 1 .. 2^29 - 1 */
+#define MISLO_KERNEL_TRACE_LIMIT (1u << 24) /* kernel trace ids 1 .. 2^24 - 1 (mislo_traces holds 2^20) */
 
 /* records.py conn32: the 32-bit connection identity in context keys and rows; 0 = none */
 static __always_inline __u32 mislo_conn32(__u64 key)
@@ -101,7 +101,7 @@ static __always_inline __u32 mislo_conn32(__u64 key)
 	return key ? ((__u32)(key ^ (key >> 32)) | 1u) : 0u;
 }
 
-/* the trace id the kernel assigns for its `fresh`-th new trace hash (wraps in 1 .. 2^29 - 1) */
+/* the trace id the kernel assigns for its `fresh`-th new trace hash (wraps in 1 .. 2^24 - 1) */
 static __always_inline __u32 mislo_trace_slot(__u64 fresh)
 {
 	return (__u32)(fresh % (MISLO_KERNEL_TRACE_LIMIT - 1)) + 1;

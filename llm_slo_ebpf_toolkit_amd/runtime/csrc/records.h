@@ -46,7 +46,9 @@ constexpr uint32_t kTraceIdMask = (1u << kEpochTagShift) - 1u;
 // records from both kinds of producer share one device context table and one trace-id space
 constexpr uint32_t kCtxIds = 1u << 24;
 constexpr uint32_t kKernelCtxLimit = 1u << 23;   // kernel context ids 1 .. 2^23 - 1
-constexpr uint32_t kKernelTraceLimit = 1u << 29; // kernel trace ids 1 .. 2^29 - 1
+// kernel trace ids 1 .. 2^24 - 1: the probes' LRU trace map (2^20 entries) evicts an idle hash long
+// before its id comes round again, and the GPU's id -> hash table stays 128 MiB
+constexpr uint32_t kKernelTraceLimit = 1u << 24;
 
 inline uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;

@@ -5,8 +5,8 @@
 //     in the ring, svc|node filled in from the agent's pod metadata), rows 2^23 .. 2^24 - 1 the
 //     host encoder's (user-space producers' records and spans). New rows of a window are handed
 //     out as an (id, row) patch the window's kernels scatter into the table before decoding;
-//   * trace map: trace hash -> trace id, fed by the kernel's TRACE definitions (ids < 2^29) and
-//     extended by the host encoder for hashes the kernel has not seen (ids >= 2^29), so spans
+//   * trace map: trace hash -> trace id, fed by the kernel's TRACE definitions (ids < 2^24) and
+//     extended by the host encoder for hashes the kernel has not seen (ids >= 2^24), so spans
 //     and events share one id space. Entries unused for two windows expire;
 //   * the host encoder: 64-byte EVENT records from user-space producers (the rocprofiler-sdk
 //     tool library, instrumented services) -> EVENT16 against the window's epoch bases, and

@@ -173,3 +173,55 @@ def test_pipelined_learning_with_graphs_and_device_refit():
         pipe.eng.close()
     for key in ("confusion", "hist", "status", "dbg", "misc"):
         np.testing.assert_array_equal(sums[0][key], sums[1][key], err_msg=key)
+
+
+def test_halo_and_remote_rows_join_like_the_oracle():
+    """Imported rows: window k+1 joins (never counts) window k's rows within the halo of its
+    latest record, plus rows other GPUs exchanged (injected here as RCCL would deliver them:
+    trace-tagged, identity cleared). Features, candidates and counters match the oracle run
+    over [window rows | imports] with the same stable selections."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+
+    wins, gen = windows(n_win=3, seed=43)
+    imgs = build_replay_images(wins)
+    halo_ms, icap = 2000.0, 16384
+    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096, halo_ms=halo_ms, import_cap=icap)
+    rb, user, spans = rings("halo")
+    src = RingWindowSource(pipe, rb, user, spans)
+    pods, sn = pod_meta(gen)
+    pipe.eng.set_pods(pods, sn)
+    pod_sn = dict(zip(pods.tolist(), sn.tolist()))
+    table, tmap = oracle.CtxTable(), oracle.TraceMap()
+    imports = oracle.empty_rows()
+    n_imported = []
+    for j, (w, img) in enumerate(zip(wins, imgs)):
+        if j == 2:  # another GPU saw slow DNS lookups on the first 40 traced requests of this window
+            sp = w.spans[w.spans["trace_h"] != 0][:40]
+            remote = oracle.Decoded(sp["ts_ns"].astype(np.int64) + 1_000_000, np.full(len(sp), 150.0, np.float32),
+                                    np.zeros(len(sp), np.uint8), np.full(len(sp), 2, np.uint8),
+                                    np.zeros(len(sp), np.uint32), np.zeros(len(sp), np.uint32),
+                                    np.zeros(len(sp), np.uint32), sp["trace_h"].astype(np.uint64),
+                                    np.zeros(len(sp), np.uint64))
+            pipe.inject_remote(oracle.exchange_blocks([remote, oracle.empty_rows()], 64), world=2, me=1)
+            imports = oracle.concat(imports, remote)
+        r = src.stage(feed(img, rb, user, spans), w.n_groups, img.labels)
+        k = r["k"]
+        oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
+        d_loc = oracle.decode_window(img.framed, img.user, table, tmap, img.bases)
+        n_loc = len(d_loc.ts)
+        d = oracle.concat(d_loc, imports)
+        ref = oracle.join(d, oracle.spans_native(img.spans), w.n_groups)
+        pk = pipe.packet(k)
+        res = pipe.results(k, w.n_groups)
+        np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d_loc))  # imports never count
+        fr = img.framed.view(np.uint32).reshape(-1, 6)
+        assert pk["ring_state"]["events"] == int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
+        np.testing.assert_array_equal(res["feat"], ref.feat)
+        dbg = pk["dbg"][:5].astype(np.int64).tolist()
+        assert dbg[0] == ref.debug["candidates"] and dbg[4] == ref.debug["spans_enriched"]
+        n_imported.append(len(imports.ts))
+        halo = oracle.halo_rows(d, n_loc, int(halo_ms * 1e6))
+        imports = oracle.take(halo, np.arange(len(halo.ts)) < icap)
+    assert n_imported[0] == 0 and n_imported[1] > 0 and n_imported[2] > n_imported[1] - 1
+    src.drain()
+    pipe.eng.close()

@@ -126,7 +126,7 @@ def test_probe_c_plumbing_matches_probesim(probe_host, tmp_path):
     t0 = int(ev["ts_ns"][ev["ts_ns"] > 0].min())
     cuts = [(0, (t0 - 10**6) & ~3 | 1), (1000, (t0 + 3 * 10**8) & ~3 | 2), (2500, (t0 + 6 * 10**8) & ~3 | 3)]
     floors = {2 + 9: 2_000_000}  # syscall_latency below 2 ms stays in the kernel
-    for trace_next, ctx_next in ((0, 0), ((1 << 29) - 40, (1 << 23) - 30)):
+    for trace_next, ctx_next in ((0, 0), ((1 << 24) - 40, (1 << 23) - 30)):
         args = ["--trace-next", trace_next, "--ctx-next", ctx_next, "--floor", "9:2000000"]
         for idx, val in cuts:
             args += ["--epoch-at", f"{idx}:{val}"]

@@ -57,6 +57,34 @@ def _ready(port: int) -> bool:
         return False
 
 
+def _smaps_top(pid: int, top: int = 14) -> list:
+    """[(mapping, rss MB, private MB)] largest first, from /proc/<pid>/smaps."""
+    agg = {}
+    name = "?"
+    try:
+        with open(f"/proc/{pid}/smaps") as f:
+            for ln in f:
+                parts = ln.split()
+                if not parts:
+                    continue
+                if not parts[0].endswith(":") or "-" in parts[0]:
+                    name = parts[5] if len(parts) > 5 else "[anon]"
+                    if name.startswith("/dev/shm/") or name.startswith("/memfd:"):
+                        name = name.split("(")[0]
+                    continue
+                if parts[0] in ("Rss:", "Private_Clean:", "Private_Dirty:"):
+                    r = agg.setdefault(name, [0, 0])
+                    kb = int(parts[1])
+                    if parts[0] == "Rss:":
+                        r[0] += kb
+                    else:
+                        r[1] += kb
+    except OSError:
+        return []
+    rows = sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]
+    return [(k, round(v[0] / 1024, 1), round(v[1] / 1024, 1)) for k, v in rows]
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rate", type=float, default=1e6, help="events/s the producer writes")
@@ -103,6 +131,7 @@ def main() -> int:
         k1 = [k.cpu_times() for k in kids]
         m1 = _scrape(port)
         full = proc.memory_full_info()
+        smaps = _smaps_top(agent.pid)
         wall = w1 - w0
         agent_cpu = (c1.user + c1.system - c0.user - c0.system) / wall * 100.0
         prod_cpu = sum(b.user + b.system - x.user - x.system for x, b in zip(k0, k1)) / wall * 100.0
@@ -119,6 +148,7 @@ def main() -> int:
             "agent_uss_mb": round(full.uss / 2**20, 1),
             "agent_pss_mb": round(getattr(full, "pss", 0) / 2**20, 1),
             "windows_in_interval": win,
+            "rss_by_mapping_mb": smaps,
             "metrics": {k: v for k, v in m1.items() if k.startswith("llm_slo_agent_")},
         }
     finally:
