@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--halo-ms", type=float, default=0.0,
                     help="carry rows within this distance of a window's latest record into the next window")
     ap.add_argument("--xchg-cap", type=int, default=-1,
-                    help="trace-tagged rows each GPU exchanges per window over RCCL (-1: events/8 when N > 1)")
+                    help="warn-level trace-tagged rows each GPU exchanges per window over RCCL (-1: 65536 when N > 1)")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -203,7 +203,7 @@ def main() -> int:
     # probes commit ahead of them) plus its user-space records: nothing may spill into the next window
     sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs + himgs)
     user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
-    xchg = (a.events // 8 if world > 1 else 0) if a.xchg_cap < 0 else a.xchg_cap
+    xchg = (min(65536, a.events) if world > 1 else 0) if a.xchg_cap < 0 else a.xchg_cap
     import_cap = (sig_cap if a.halo_ms > 0 else 0) + (world - 1) * xchg
     pipe = WindowPipeline(sig_cap, a.spans, a.services, local, comm, model=a.model, seed=a.seed,
                           use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,

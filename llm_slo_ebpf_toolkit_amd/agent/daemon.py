@@ -465,10 +465,11 @@ class Agent:
         multi = comm is not None and comm[2] > 1
         # joins reach across the window cut (halo) and, on a multi-GPU node, across GPUs
         # (trace-tagged rows exchanged over RCCL); imports are bounded by one window's records
+        xchg = min(65536, budget) if multi else 0
+        icap = (budget if o.halo_ms > 0 else 0) + 7 * xchg
         pipe = WindowPipeline(budget, o.window_spans, o.window_groups, o.device, comm, model=o.model, learn=False,
                               window_ms=2000.0, user_cap=max(1024, o.window_events // 4), ttft_slo_ms=o.ttft_slo_ms,
-                              halo_ms=o.halo_ms, import_cap=budget if o.halo_ms > 0 or multi else 0,
-                              xchg_cap=budget // 8 if multi else 0)
+                              halo_ms=o.halo_ms, import_cap=icap, xchg_cap=xchg)
         src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
         if pods is not None:
             pipe.eng.set_pods(*pods)

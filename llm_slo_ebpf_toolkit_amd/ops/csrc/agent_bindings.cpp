@@ -215,6 +215,10 @@ class PyEngine {
     py::gil_scoped_release nogil;
     e_->sync();
   }
+  std::vector<int64_t> import_state() {
+    py::gil_scoped_release nogil;
+    return eng().import_state();
+  }
   void close() {
     if (e_) {
       py::gil_scoped_release nogil;
@@ -295,6 +299,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("stats_acc", &PyEngine::stats_acc)
       .def("model_bytes", &PyEngine::model_bytes)
       .def("sync", &PyEngine::sync)
+      .def("import_state", &PyEngine::import_state)
       .def("close", &PyEngine::close)
       .def_property_readonly("buffers", &PyEngine::buffers)
       .def_property_readonly("windows_folded", &PyEngine::folded)

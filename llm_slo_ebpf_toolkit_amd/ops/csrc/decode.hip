@@ -26,6 +26,7 @@ struct DecodeOut {
   uint32_t* part_cnt;    // [gridDim.x][kKeyTypes * kParts] per-block partition counts
   unsigned long long* misc;  // [0] unsupported events, [1] zero-timestamp events,
                              // [2 + slot] per-signal value sum in 1/1000 units (Prometheus _sum)
+  int blk_base = 0;      // this launch's first row in part_cnt (a second row segment's decode)
 };
 
 constexpr int kMiscSums = 2;  // offset of the per-slot value sums in misc
@@ -109,7 +110,7 @@ __device__ __forceinline__ void lds_flush(DecodeLds& L, const DecodeOut& o, int 
     for (int r = 0; r < DecodeLds::kRep; ++r) v += L.sum[r * DecodeLds::kUS + threadIdx.x];
     if (v) atomicAdd(&o.misc[kMiscSums + threadIdx.x], v);
   }
-  uint32_t* dst = o.part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts;
+  uint32_t* dst = o.part_cnt + (size_t)(o.blk_base + blockIdx.x) * kKeyTypes * kParts;
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) {
     uint32_t v = 0;
 #pragma unroll
@@ -364,18 +365,22 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
                                                       const SigRec* __restrict__ imp,
                                                       const uint4* __restrict__ ctx_tab, int n_ctx, TraceIds tt,
                                                       uint32_t* __restrict__ rs, unsigned long long* __restrict__ tmax,
-                                                      DecodeOut o) {
+                                                      int seg, DecodeOut o) {
   __shared__ DecodeLds L;
   lds_init<NT>(L);
   const LdsLane l = lds_lane(L);
-  const int n = min(rows[0], cap);
-  const int n_loc = min(n_ptr[0], n);
+  // segment 0: rows [0, rows[0]) (the window's records and its halo); segment 1: rows
+  // [rows[0], rows[1]) (other GPUs' rows, decoded once they have been all-gathered)
+  const int r0 = min(rows[0], cap);
+  const int seg_beg = seg ? r0 : 0;
+  const int n = seg ? max(r0, min(rows[1], cap)) : r0;
+  const int n_loc = min(n_ptr[0], r0);
   const int n_k = min(n_ptr[15], n_loc);
   const int valid_k = min((int)min((uint32_t)n_k, rs[kRsFirstBusy]), n_k);
   auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
   const int64_t t_base[4] = {base_at(4), base_at(8), base_at(10), base_at(12)};
-  const int chunk = (n + gridDim.x - 1) / gridDim.x;
-  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  const int chunk = (n - seg_beg + gridDim.x - 1) / gridDim.x;
+  const int beg = seg_beg + blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0, events = 0;
   unsigned long long t_hi = 0;
   __shared__ uint4 s_stage[NT * 5];
@@ -595,12 +600,13 @@ void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t
 void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, const int* rows, int cap,
                           const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
                           uint32_t* ring_state, unsigned long long* tmax, const SignalCols& cols, uint32_t* hist,
-                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream) {
-  DecodeOut o{cols, hist, status_cnt, part_cnt, misc};
+                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream,
+                          int seg, int grid, int blk_base) {
+  DecodeOut o{cols, hist, status_cnt, part_cnt, misc, blk_base};
   constexpr int NT = kDecodeNT;
-  hipLaunchKernelGGL((k_decode_window<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, framed,
+  hipLaunchKernelGGL((k_decode_window<NT>), dim3(grid > 0 ? grid : decode_grid(cap)), dim3(NT), 0, stream, framed,
                      (const Event*)user, n_dev, rows, cap, imp, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, tt,
-                     ring_state, tmax, o);
+                     ring_state, tmax, seg, o);
 }
 
 }  // namespace mislo

@@ -127,8 +127,10 @@ class WindowEngine {
   void set_model_bytes(const void* bytes, size_t n);  // stream-ordered before the next window
   void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
   void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
-  // rows to import into the next window, as other GPUs' exchange blocks would deliver them
-  // (world blocks of [64-byte header: uint32 row count | rows], this rank's block skipped)
+  // other GPUs' rows for the next window, as their exchange blocks would arrive over RCCL (world
+  // blocks of [32-byte header: uint32 row count | XRec rows], this rank's block skipped); the
+  // next submit runs the exchange path (decode part 1, merge, part 2) with them
+
   void inject_remote(const void* blocks, size_t stride, int world, int me);
   void set_join_params(double window_ms, double threshold, int fanout, int group_mode);
   void init_comm(const ncclUniqueId& id, int rank, int world);
@@ -145,6 +147,9 @@ class WindowEngine {
   void stats_acc(double* out);        // the device refit's accumulated statistics (synchronous)
   void model_bytes(void* out);        // the model currently on the device (synchronous)
   void sync();
+  // device-side import state (synchronous; diagnostics and tests): rows[0..1], tmax, and per
+  // buffer the halo / other-GPU row counts
+  std::vector<int64_t> import_state();
   int64_t windows_folded() const { return folded_; }
   size_t staged_bytes() const { return staged_bytes_; }
   size_t direct_bytes() const { return direct_bytes_; }
@@ -153,7 +158,9 @@ class WindowEngine {
 
  private:
   void alloc();
-  void run_chain(int b, int n_groups, bool with_labels, bool learn, hipStream_t st);
+  void run_part1(int b, hipStream_t st, bool xchg);
+  void run_part2(int b, int n_groups, bool with_labels, bool learn, hipStream_t st, bool xchg);
+  void launch_part(int part, int b, int n_groups, bool with_labels, bool learn, bool xchg);
   SignalCols sig_cols() const;
   SpanCols span_cols() const;
   bool registered(const void* p, size_t n) const;
@@ -174,7 +181,11 @@ class WindowEngine {
   std::vector<SigRec*> imp_;
   uint32_t *halo_n_ = nullptr, *remote_n_ = nullptr, *sel_cnt_ = nullptr, *sel_off_ = nullptr;
   uint8_t *xsend_ = nullptr, *xrecv_ = nullptr;
-  size_t xstride_ = 0;
+  size_t xstride_ = 0, xrecv_bytes_ = 0;
+  int nblk_imp_ = 0;                    // decode blocks of the other GPUs' rows
+  std::vector<uint8_t> inject_;         // exchange blocks for the next window (inject_remote)
+  size_t inject_stride_ = 0;
+  int inject_world_ = 0, inject_me_ = 0;
   int rank_ = 0, world_ = 1;
   std::vector<uint8_t*> res_all_dev_, res_all_host_;
   std::vector<hipEvent_t> xchg_done_;

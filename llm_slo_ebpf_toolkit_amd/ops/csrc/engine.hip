@@ -162,7 +162,7 @@ void WindowEngine::alloc() {
     t_comp1_.push_back(mk_event(true));
     t_end_.push_back(mk_event(true));
   }
-  warm_.assign(nb_, false);
+  warm_.assign(4 * nb_, false);
   // per-incident results block: [post G*16 f64][gconf G f64][feat G*16 f32][pred G i32][evbits G*16 u32]
   // [sli G*2 u32]
   const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
@@ -200,7 +200,7 @@ void WindowEngine::alloc() {
   sel_cnt_ = dalloc<uint32_t>(1024);
   sel_off_ = dalloc<uint32_t>(1024);
   for (int b = 0; b < nb_; ++b) imp_.push_back(cfg_.import_cap ? dalloc<SigRec>(cfg_.import_cap) : nullptr);
-  xstride_ = sizeof(SigRec) * (1 + (size_t)cfg_.xchg_cap);  // [header: row count | rows]
+  xstride_ = sizeof(XRec) * (1 + (size_t)cfg_.xchg_cap);  // [32-byte header: row count | XRec rows]
   if (cfg_.xchg_cap) {
     xsend_ = dalloc<uint8_t>(xstride_);
     HIPCHECK(hipMemset(xsend_, 0, xstride_));
@@ -223,8 +223,11 @@ void WindowEngine::alloc() {
   }
   g_status_ = dalloc<uint8_t>(N);
   g_part_ = dalloc<PartCodes>(N);
-  g_part_blk_ = dalloc<uint32_t>((size_t)nblk_sig_ * kKeyTypes * kParts);
-  g_part_off_ = dalloc<uint32_t>((size_t)nblk_sig_ * kKeyTypes * kParts);
+  // other GPUs' rows decode in blocks of their own (<= 7 peers' exchange blocks)
+  nblk_imp_ = cfg_.xchg_cap ? decode_grid(7 * cfg_.xchg_cap) : 0;
+  g_part_blk_ = dalloc<uint32_t>((size_t)(nblk_sig_ + nblk_imp_) * kKeyTypes * kParts);
+  g_part_off_ = dalloc<uint32_t>((size_t)(nblk_sig_ + nblk_imp_) * kKeyTypes * kParts);
+  for (int b = 0; b < nb_; ++b) xchg_done_.push_back(mk_event(false));
   g_part_tot_ = dalloc<uint32_t>(kKeyTypes * kParts);
   g_part_base_ = dalloc<uint32_t>(kKeyTypes * kParts + 1);
   g_items_ = dalloc<uint32_t>(kKeyTypes * N);
@@ -350,14 +353,13 @@ bool WindowEngine::h2d_done(int64_t k) {
 void WindowEngine::wait_h2d(int64_t k) { HIPCHECK(hipEventSynchronize(h2d_done_[k % nb_])); }
 
 // The captured part of a window: everything between the DMA and the packet.
-void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, hipStream_t st) {
+// Part 1 of a window: accumulators, definitions, the decode of the window's records and the
+// halo it imported; with the GPU exchange, this window's trace-tagged rows for the others.
+void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   uint8_t* in = in_dev_[b];
   const int* counts = reinterpret_cast<const int*>(in);
-  const int32_t* labels = reinterpret_cast<const int32_t*>(in + kHeadBytes);
   const int N = n_rows_, S = cfg_.span_cap, G = cfg_.group_cap;
-  const int bn = (b + 1) % nb_;  // the next window's buffer (its imports are produced here)
-  // this buffer's per-incident results block
-  uint8_t* r = res_dev_[b];
+  uint8_t* r = res_dev_[b];  // this buffer's per-incident results block
   const size_t o_gconf = 16 * (size_t)G * 8, o_feat = o_gconf + (size_t)G * 8, o_pred = o_feat + 16 * (size_t)G * 4;
   const size_t o_ev = o_pred + (size_t)G * 4, o_sli = o_ev + 16 * (size_t)G * 4;
   post_ = reinterpret_cast<double*>(r);
@@ -385,21 +387,44 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
   FillList rs{};
   rs.seg[0] = FillSeg{ring_state_, 1, 0xFFFFFFFFu};  // first busy record: none
   rs.seg[1] = FillSeg{ring_state_ + 1, kRsLen - 1, 0};
-  rs.count = 2;
+  rs.seg[2] = FillSeg{remote_n_ + b, 1, 0};        // other GPUs' rows: none until merged
+  rs.count = 3;
   hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, rs);
   launch_window_rows(counts, halo_n_ + b, remote_n_ + b, N, rows_, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                        ring_state_, tmax_, sig_cols(), hist_, status_, g_part_blk_, misc_, st);
-  {  // this buffer's imports are consumed: the next producer rewrites both counts
+  if (xchg)  // this window's warn-level trace-tagged rows, as the other GPUs will import them
+    launch_select(g_rec_, g_status_, rows_, counts, N, kSelTrace, tmax_, 0, sel_cnt_, sel_off_, xsend_ + sizeof(XRec),
+                  reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, true, st);
+}
+
+// Part 2: [the other GPUs' rows] -> partition -> spans -> join -> posterior -> packet, and the
+// next window's halo.
+void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, hipStream_t st, bool xchg) {
+  uint8_t* in = in_dev_[b];
+  const int* counts = reinterpret_cast<const int*>(in);
+  const int32_t* labels = reinterpret_cast<const int32_t*>(in + kHeadBytes);
+  const int N = n_rows_, S = cfg_.span_cap, G = cfg_.group_cap;
+  const int bn = (b + 1) % nb_;
+  if (xchg) {
+    const TraceIds tt{trace_hash_, kTraceIdRows};
+    launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
+                         ring_state_, tmax_, sig_cols(), hist_, status_, g_part_blk_, misc_, st, 1, nblk_imp_,
+                         nblk_sig_);
+  }
+  {  // this buffer's imports are consumed
     FillList z{};
     z.seg[0] = FillSeg{halo_n_ + b, 1, 0};
-    z.seg[1] = FillSeg{remote_n_ + b, 1, 0};
-    z.count = 2;
+    z.count = 1;
     hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, z);
   }
-  launch_partition(g_part_, rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
+  if (xchg)
+    launch_partition(g_part_, rows_, N, nblk_sig_ + nblk_imp_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_,
+                     g_items_, st, nblk_sig_);
+  else
+    launch_partition(g_part_, rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
   const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms};
   launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
@@ -417,15 +442,45 @@ void WindowEngine::run_chain(int b, int n_groups, bool with_labels, bool learn, 
                      confusion_, st);
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
                      stats_, stats_count_, ring_state_, packet_dev_[b]);
-  // the next window's imports: this window's rows within the join window of its latest record
+  // the next window's halo: this window's rows (all of them: records, halo, other GPUs' rows)
+  // within the join window of its latest local record
   if (cfg_.halo_ms > 0 && cfg_.import_cap > 0)
-    launch_select(g_rec_, rows_, counts, N, kSelHalo, tmax_, (long long)llround(cfg_.halo_ms * 1e6), sel_cnt_,
-                  sel_off_, imp_[bn], halo_n_ + bn, (uint32_t)cfg_.import_cap, false, st);
-  // this window's trace-tagged local rows for the other GPUs (gathered on the comm stream)
-  if (exchange())
-    launch_select(g_rec_, rows_, counts, N, kSelTrace, tmax_, 0, sel_cnt_, sel_off_,
-                  reinterpret_cast<SigRec*>(xsend_ + sizeof(SigRec)), reinterpret_cast<uint32_t*>(xsend_),
-                  (uint32_t)cfg_.xchg_cap, true, st);
+    launch_select(g_rec_, g_status_, rows_ + 1, counts, N, kSelHalo, tmax_, (long long)llround(cfg_.halo_ms * 1e6),
+                  sel_cnt_, sel_off_, imp_[bn], halo_n_ + bn, (uint32_t)cfg_.import_cap, false, st);
+}
+
+// Launch a chain part eagerly, or through its captured graph (captured on the buffer's second
+// use; the first use runs eagerly so lazily initialised state is out of the capture).
+void WindowEngine::launch_part(int part, int b, int n_groups, bool with_labels, bool learn, bool xchg) {
+  auto run = [&] {
+    if (part == 0) {  // the whole window in one graph (no exchange)
+      run_part1(b, compute_, false);
+      run_part2(b, n_groups, with_labels, learn, compute_, false);
+    } else if (part == 1) {
+      run_part1(b, compute_, xchg);
+    } else {
+      run_part2(b, n_groups, with_labels, learn, compute_, xchg);
+    }
+  };
+  if (!cfg_.use_graphs) return run();
+  auto key = std::make_tuple(b * 4 + part, n_groups, with_labels, learn);
+  auto it = graphs_.find(key);
+  if (it == graphs_.end() && !warm_[b * 4 + part]) {
+    run();
+    warm_[b * 4 + part] = true;
+    return;
+  }
+  if (it == graphs_.end()) {
+    hipGraph_t g;
+    HIPCHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+    run();
+    HIPCHECK(hipStreamEndCapture(compute_, &g));
+    hipGraphExec_t ex;
+    HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    graph_defs_.push_back(g);
+    it = graphs_.emplace(key, ex).first;
+  }
+  HIPCHECK(hipGraphLaunch(it->second, compute_));
 }
 
 void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bool learn) {
@@ -474,8 +529,6 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
-  // window k's imports include the other GPUs' rows of window k - 1 (merged on the comm stream)
-  if (exchange() && k >= 1) HIPCHECK(hipStreamWaitEvent(compute_, xchg_done_[(k - 1) % nb_], 0));
   HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
   if (cfg_.device_refit && k >= nb_) {
     // fold window k - nb's all-reduced statistics (packet b) and refit before window k: a
@@ -484,27 +537,35 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
                     reinterpret_cast<PosteriorModel*>(model_dev_), compute_);
     ++folded_;
   }
-  if (!cfg_.use_graphs) {
-    run_chain(b, n_groups, with_labels, learn, compute_);
+  const bool injected = !inject_.empty();
+  const bool xchg = exchange() || injected;
+  if (!xchg) {
+    launch_part(0, b, n_groups, with_labels, learn, false);
   } else {
-    auto key = std::make_tuple(b, n_groups, with_labels, learn);
-    auto it = graphs_.find(key);
-    if (it == graphs_.end() && !warm_[b]) {  // first use of the buffers: run eagerly once
-      run_chain(b, n_groups, with_labels, learn, compute_);
-      warm_[b] = true;
+    launch_part(1, b, n_groups, with_labels, learn, true);
+    // the exchange sits between the window's two halves: every GPU's trace rows of THIS window
+    if (injected) {  // rows as the other GPUs would have delivered them (tests, replays)
+      HIPCHECK(hipMemcpyAsync(xrecv_, inject_.data(), inject_.size(), hipMemcpyHostToDevice, compute_));
+      HIPCHECK(hipStreamSynchronize(compute_));  // the host copy is released below
+      launch_remote_merge(xrecv_, inject_stride_, inject_world_, inject_me_, imp_[b], halo_n_ + b, remote_n_ + b,
+                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, compute_);
+      inject_.clear();
+      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), halo_n_ + b, remote_n_ + b, n_rows_, rows_,
+                         compute_);
     } else {
-      if (it == graphs_.end()) {
-        hipGraph_t g;
-        HIPCHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
-        run_chain(b, n_groups, with_labels, learn, compute_);
-        HIPCHECK(hipStreamEndCapture(compute_, &g));
-        hipGraphExec_t ex;
-        HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-        graph_defs_.push_back(g);
-        it = graphs_.emplace(key, ex).first;
-      }
-      HIPCHECK(hipGraphLaunch(it->second, compute_));
+      // every use of the communicator stays on the comm stream (one stream, one issue order on
+      // every rank): the compute stream hands over after part 1 and waits for the merge
+      HIPCHECK(hipEventRecord(xchg_done_[b], compute_));
+      HIPCHECK(hipStreamWaitEvent(comm_stream_, xchg_done_[b], 0));
+      NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, comm_, comm_stream_));
+      launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[b], halo_n_ + b, remote_n_ + b,
+                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, comm_stream_);
+      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), halo_n_ + b, remote_n_ + b, n_rows_, rows_,
+                         comm_stream_);
+      HIPCHECK(hipEventRecord(xchg_done_[b], comm_stream_));
+      HIPCHECK(hipStreamWaitEvent(compute_, xchg_done_[b], 0));
     }
+    launch_part(2, b, n_groups, with_labels, learn, true);
   }
   // per-incident results of this window (the buffers are reused by the next window)
   HIPCHECK(hipMemcpyAsync(res_host_[b], res_dev_[b], res_bytes_, hipMemcpyDeviceToHost, compute_));
@@ -512,18 +573,11 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   HIPCHECK(hipEventRecord(compute_done_[b], compute_));
   HIPCHECK(hipStreamWaitEvent(comm_stream_, compute_done_[b], 0));
   if (comm_) {
-    // one group: node-wide packet, node-wide incident list, the trace-row exchange
+    // one group: the node-wide packet and the node-wide incident list
     NCCLCHECK(ncclGroupStart());
     NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen, ncclFloat64, ncclSum, comm_, comm_stream_));
     NCCLCHECK(ncclAllGather(res_dev_[b], res_all_dev_[b], res_bytes_, ncclUint8, comm_, comm_stream_));
-    if (exchange()) NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, comm_, comm_stream_));
     NCCLCHECK(ncclGroupEnd());
-    if (exchange()) {
-      const int bn = (b + 1) % nb_;
-      launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[bn], halo_n_ + bn, remote_n_ + bn,
-                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, comm_stream_);
-      HIPCHECK(hipEventRecord(xchg_done_[b], comm_stream_));
-    }
     HIPCHECK(hipMemcpyAsync(res_all_host_[b], res_all_dev_[b], res_bytes_ * world_, hipMemcpyDeviceToHost,
                             comm_stream_));
   }
@@ -588,25 +642,41 @@ void WindowEngine::set_pods(const uint32_t* pods, const uint32_t* svcnode, size_
   HIPCHECK(hipMemcpyAsync(pod_sn_, pod_host_, kPodRows * 4, hipMemcpyHostToDevice, compute_));
 }
 
+std::vector<int64_t> WindowEngine::import_state() {
+  sync();
+  int rows[2];
+  unsigned long long tmax = 0;
+  std::vector<uint32_t> h(nb_), r(nb_);
+  HIPCHECK(hipMemcpy(rows, rows_, sizeof(rows), hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(&tmax, tmax_, 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(h.data(), halo_n_, 4 * nb_, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(r.data(), remote_n_, 4 * nb_, hipMemcpyDeviceToHost));
+  std::vector<int64_t> out{rows[0], rows[1], (int64_t)tmax};
+  for (int b = 0; b < nb_; ++b) out.push_back(h[b]);
+  for (int b = 0; b < nb_; ++b) out.push_back(r[b]);
+  return out;
+}
+
 void WindowEngine::inject_remote(const void* blocks, size_t stride, int world, int me) {
-  if (!cfg_.import_cap) throw std::logic_error("inject_remote needs import_cap > 0");
-  if (world < 1 || me < 0 || me >= world || stride < sizeof(SigRec)) throw std::invalid_argument("bad exchange blocks");
+  if (!cfg_.import_cap || !cfg_.xchg_cap) throw std::logic_error("inject_remote needs import_cap and xchg_cap > 0");
+  if (world < 1 || me < 0 || me >= world || stride < sizeof(XRec)) throw std::invalid_argument("bad exchange blocks");
   const uint8_t* h = static_cast<const uint8_t*>(blocks);
-  int max_rows = 0;
-  for (int r = 0; r < world; ++r) {  // the kernel trusts each block's header: check it here
+  for (int r = 0; r < world; ++r) {  // the merge kernel trusts each block's header: check it here
     uint32_t c;
     std::memcpy(&c, h + (size_t)r * stride, 4);
-    if ((size_t)c * sizeof(SigRec) + sizeof(SigRec) > stride) throw std::invalid_argument("block row count exceeds stride");
-    max_rows = std::max(max_rows, (int)c);
+    if ((size_t)c * sizeof(XRec) + sizeof(XRec) > stride) throw std::invalid_argument("block row count exceeds stride");
+    if (r != me && c > (uint32_t)cfg_.xchg_cap) throw std::invalid_argument("block holds more rows than xchg_cap");
   }
-  const int bn = (int)(submitted_ % nb_);  // the next window's buffer
-  uint8_t* d = nullptr;
-  HIPCHECK(hipMalloc(&d, stride * world));
-  HIPCHECK(hipMemcpyAsync(d, blocks, stride * world, hipMemcpyHostToDevice, compute_));
-  launch_remote_merge(d, stride, world, me, imp_[bn], halo_n_ + bn, remote_n_ + bn, (uint32_t)cfg_.import_cap,
-                      max_rows, compute_);
-  HIPCHECK(hipStreamSynchronize(compute_));
-  HIPCHECK(hipFree(d));
+  if (stride * world > xrecv_bytes_) {
+    sync();
+    if (xrecv_) HIPCHECK(hipFree(xrecv_));
+    xrecv_ = dalloc<uint8_t>(stride * world);
+    xrecv_bytes_ = stride * world;
+  }
+  inject_.assign(h, h + stride * world);  // consumed by the next submit, between its two halves
+  inject_stride_ = stride;
+  inject_world_ = world;
+  inject_me_ = me;
 }
 
 void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
@@ -623,11 +693,13 @@ void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
     HIPCHECK(hipHostMalloc(&h, res_bytes_ * world, hipHostMallocDefault));
     std::memset(h, 0, res_bytes_ * world);
     res_all_host_.push_back(static_cast<uint8_t*>(h));
-    xchg_done_.push_back(mk_event(false));
   }
   if (cfg_.xchg_cap) {
+    if (world > 8) throw std::invalid_argument("the exchange is sized for <= 8 GPUs per node");
+    if (xrecv_) HIPCHECK(hipFree(xrecv_));
     xrecv_ = dalloc<uint8_t>(xstride_ * world);
-    HIPCHECK(hipMemset(xrecv_, 0, xstride_ * world));
+    xrecv_bytes_ = xstride_ * world;
+    HIPCHECK(hipMemset(xrecv_, 0, xrecv_bytes_));
   }
 }
 

@@ -108,13 +108,22 @@ __global__ __launch_bounds__(1024) void k_base_scan(const uint32_t* __restrict__
 template <int NT>
 __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ codes, const int* __restrict__ n_ptr,
                                                 int cap, const uint32_t* __restrict__ part_off,
-                                                const uint32_t* __restrict__ base, uint32_t* __restrict__ items) {
+                                                const uint32_t* __restrict__ base, uint32_t* __restrict__ items,
+                                                int nblk_a) {
   __shared__ uint32_t s_cnt[kKeyTypes * kParts];
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_cnt[i] = 0;
   __syncthreads();
-  const int n = min(*n_ptr, cap);
-  const int chunk = (n + gridDim.x - 1) / gridDim.x;
-  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  // the same row ranges the decode blocks had: one segment, or two (nblk_a blocks over
+  // [0, n_ptr[0]), the rest over [n_ptr[0], n_ptr[1]))
+  const int n0 = min(n_ptr[0], cap);
+  const bool two = nblk_a < (int)gridDim.x;
+  const bool second = two && (int)blockIdx.x >= nblk_a;
+  const int s_beg = second ? n0 : 0;
+  const int s_end = second ? max(n0, min(n_ptr[1], cap)) : n0;
+  const int g = two ? (second ? (int)gridDim.x - nblk_a : nblk_a) : (int)gridDim.x;
+  const int bi = second ? (int)blockIdx.x - nblk_a : (int)blockIdx.x;
+  const int chunk = (s_end - s_beg + g - 1) / g;
+  const int beg = s_beg + bi * chunk, end = min(s_end, beg + chunk);
   const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     const PartCodes pc = codes[i];
@@ -857,7 +866,7 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
-                      hipStream_t stream) {
+                      hipStream_t stream, int nblk_a) {
   static_assert((kKeyTypes * kParts) % kScanCols == 0, "scan columns tile the partition matrix");
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
                      part_blk, nblk, part_off, part_tot);
@@ -865,7 +874,7 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
   // 1024 threads per workgroup: the grid is one workgroup per decode block (<= 256), so 256
   // threads left 4 waves per CU to hide the scattered stores and LDS atomics
   hipLaunchKernelGGL((k_scatter<1024>), dim3(nblk), dim3(1024), 0, stream, codes, n_dev, cap, part_off, part_base,
-                     items);
+                     items, nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk);
 }
 
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,

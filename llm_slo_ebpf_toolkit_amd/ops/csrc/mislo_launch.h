@@ -49,29 +49,43 @@ void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCo
 void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t* ctx_tab, uint32_t ctx_rows,
                       const uint32_t* pod_sn, uint32_t n_pods, const TraceIds& tt, uint32_t* ring_state,
                       hipStream_t stream);
-// rows [0, counts[15]) framed, [counts[15], counts[0]) user records, then rows[0] - counts[0]
-// imported rows (SigRec: the previous window's halo and other GPUs' trace-tagged records) that
-// join but are not counted; tmax (u64) receives the window's latest local timestamp
+// rows [0, counts[15]) framed, [counts[15], counts[0]) user records, then imported rows (SigRec,
+// imp[i - counts[0]]) that join but are not counted: segment 0 decodes rows [0, rows[0]) (the
+// records + the previous window's halo), segment 1 rows [rows[0], rows[1]) (other GPUs' rows)
+// with `grid` blocks whose partition counts start at block row `blk_base`; tmax (u64) receives
+// the window's latest local timestamp
 void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, const int* rows, int cap,
                           const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
                           uint32_t* ring_state, unsigned long long* tmax, const SignalCols& cols, uint32_t* hist,
-                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream);
+                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream,
+                          int seg = 0, int grid = 0, int blk_base = 0);
 
 // exchange.hip: stable row selections (halo carry, trace-tagged rows for the GPU exchange)
 constexpr int kSelHalo = 0, kSelTrace = 1;
 int select_grid(int cap);
-void launch_select(const SigRec* rec, const int* rows, const int* counts, int cap, int mode,
-                   const unsigned long long* tmax, long long halo_ns, uint32_t* blk_cnt, uint32_t* blk_off,
-                   SigRec* out, uint32_t* n_out, uint32_t out_cap, bool clear_identity, hipStream_t stream);
+// 32-byte exchange row: what another GPU needs to join a row by its trace hash
+struct XRec {
+  int64_t ts;
+  uint64_t tr;
+  float val;
+  uint32_t slot;
+  uint32_t pad[2];
+};
+static_assert(sizeof(XRec) == 32, "exchange rows are 32 bytes");
+void launch_select(const SigRec* rec, const uint8_t* status, const int* rows, const int* counts, int cap, int mode,
+                   const unsigned long long* tmax, long long halo_ns, uint32_t* blk_cnt, uint32_t* blk_off, void* out,
+                   uint32_t* n_out, uint32_t out_cap, bool xrec, hipStream_t stream);
 void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, const uint32_t* halo_n,
                          uint32_t* remote_n, uint32_t imp_cap, int max_rows, hipStream_t stream);
 void launch_window_rows(const int* counts, const uint32_t* halo_n, const uint32_t* remote_n, int cap, int* rows,
                         hipStream_t stream);
 
 // join.hip
+// rows [0, n_dev[0]) decoded by nblk blocks; with split (nblk_a < nblk) the first nblk_a blocks
+// decoded rows [0, n_dev[0]) and the rest rows [n_dev[0], n_dev[1])
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
-                      hipStream_t stream);
+                      hipStream_t stream, int nblk_a = 0);
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
                   const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,

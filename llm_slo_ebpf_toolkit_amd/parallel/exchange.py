@@ -1,77 +1,98 @@
-"""Cross-shard record exchange for exact distributed joins (trace all-gather, P2 halo)."""
+"""CPU model of the engine's per-window import protocol (ops/csrc/exchange.hip, engine.hip).
+
+Per rank and window k, the device does:
+
+1. part 1: decode the window's records plus the halo it imported from window k-1 (rows
+   [counts[0], rows[0]): joined, never counted), and select this rank's trace-tagged local rows
+   at warn level or above as 32-byte XRecs (time, trace hash, value, signal: no pod / pid /
+   connection, so another GPU can only join them through the trace tier), capped at xchg_cap;
+2. RCCL all-gather of every rank's fixed-size block [header: row count | XRecs] (comm stream);
+3. part 2: decode the other ranks' rows (rows [rows[0], rows[1])), join everything, and select
+   the next window's halo: rows (all of them) with a signal, a timestamp and
+   ts >= tmax - halo, tmax = the window's latest local record, in row order, capped at
+   import_cap; the next window's other-GPU rows are appended after it up to the same cap.
+
+``ExchangeModel`` runs exactly that over the numpy oracle with a pluggable all-gather (a gloo
+process group in the tests, so the same bytes cross a real process boundary), making the
+multi-GPU semantics testable on CPU; the GPU test (test_native_engine) checks the device's
+selections and merge against the same oracle functions.
+"""
 
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import Callable, List, Optional
 
 import numpy as np
 
-from ..signals import catalog
-from .shard import trace_tagged
+from ..pipeline import oracle
+
+XREC = oracle.XREC
 
 
-def allgather_records(local: np.ndarray, group=None, device=None) -> List[np.ndarray]:
-    """All-gather variable-length structured record arrays (one collective for the sizes,
-    one for the padded payload). Works on nccl (device tensors) and gloo (CPU tensors)."""
-    import torch
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    dt = local.dtype
-    dev = device if device is not None else torch.device("cpu")
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    cap = max(sizes) if sizes else 0
-    if cap == 0:
-        return [np.zeros(0, dtype=dt) for _ in range(world)]
-    buf = np.zeros(cap, dtype=dt)
-    buf[: local.shape[0]] = local
-    t = torch.from_numpy(buf.view(np.uint8).copy()).to(dev)
-    outs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(outs, t, group=group)
-    return [o.cpu().numpy().view(dt)[:s].copy() for o, s in zip(outs, sizes)]
+def parse_block(block: np.ndarray) -> oracle.Decoded:
+    """One rank's exchange block -> imported rows (oracle.remote_rows of its XRecs)."""
+    b = np.ascontiguousarray(block, dtype=np.uint8)
+    n = int(b[:4].view(np.uint32)[0])
+    cap = b.size // 32 - 1
+    n = min(n, cap)
+    rows = b[32:32 + 32 * n].view(XREC)
+    slot = np.where(rows["slot"] == 0xFF, oracle.NO_SLOT, rows["slot"]).astype(np.uint8)
+    d = oracle.Decoded(rows["ts"].astype(np.int64), rows["val"].astype(np.float32), slot,
+                       np.zeros(n, np.uint8), np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(n, np.uint32),
+                       rows["tr"].astype(np.uint64), np.zeros(n, np.uint64))
+    return oracle.remote_rows(d)
 
 
-def with_remote_trace_events(local: np.ndarray, group=None, device=None) -> Tuple[np.ndarray, int]:
-    """[local events..., trace-tagged events of every other rank...], n_local."""
-    import torch.distributed as dist
+def torch_allgather(group=None) -> Callable[[np.ndarray], List[np.ndarray]]:
+    """All-gather of equal-size uint8 blocks over a torch.distributed group (gloo on CPU)."""
 
-    sup = [s.kernel_type for s in catalog.SIGNALS]
-    mine = local[trace_tagged(local, sup)]
-    parts = allgather_records(mine, group, device)
-    me = dist.get_rank(group)
-    remote = [p for r, p in enumerate(parts) if r != me and p.shape[0]]
-    if not remote:
-        return local, local.shape[0]
-    return np.concatenate([local] + remote), local.shape[0]
+    def gather(block: np.ndarray) -> List[np.ndarray]:
+        import torch
+        import torch.distributed as dist
+
+        t = torch.from_numpy(np.ascontiguousarray(block, dtype=np.uint8).copy())
+        outs = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(outs, t, group=group)
+        return [o.numpy() for o in outs]
+
+    return gather
 
 
-class Halo:
-    """P2 time halo for streaming windows: events of earlier windows whose timestamps lie
-    within ``outer_ns`` of the current window's first span stay joinable. Imported halo
-    events follow the window's own events (counted once, in their own window)."""
+class ExchangeModel:
+    """One rank's window chain with imports (halo + other ranks' trace rows)."""
 
-    def __init__(self, outer_ns: int, max_events: Optional[int] = None):
-        self.outer_ns = int(outer_ns)
-        self.max_events = max_events
-        self._tail: Optional[np.ndarray] = None
+    def __init__(self, rank: int, world: int, halo_ms: float, import_cap: int, xchg_cap: int,
+                 allgather: Optional[Callable[[np.ndarray], List[np.ndarray]]] = None):
+        self.rank, self.world = rank, world
+        self.halo_ns = int(round(halo_ms * 1e6))
+        self.import_cap, self.xchg_cap = import_cap, xchg_cap
+        self.allgather = allgather
+        self.imports = oracle.empty_rows()
+        self.sent = 0
 
-    def extend(self, events: np.ndarray, spans: np.ndarray) -> Tuple[np.ndarray, int]:
-        n_local = events.shape[0]
-        merged = events
-        if self._tail is not None and self._tail.shape[0] and spans.shape[0]:
-            t0 = int(spans["ts_ns"][spans["ts_ns"] != 0].min()) if (spans["ts_ns"] != 0).any() else 0
-            keep = self._tail[self._tail["ts_ns"] >= t0 - self.outer_ns]
-            if keep.shape[0]:
-                merged = np.concatenate([events, keep])
-        # remember this window's tail (plus still-relevant older tail) for the next window
-        if events.shape[0]:
-            t_end = int(events["ts_ns"].max())
-            pool = events if self._tail is None else np.concatenate([self._tail, events])
-            tail = pool[pool["ts_ns"] >= t_end - self.outer_ns]
-            if self.max_events is not None and tail.shape[0] > self.max_events:
-                tail = tail[np.argsort(tail["ts_ns"], kind="stable")[-self.max_events:]]
-            self._tail = tail
-        return merged, n_local
+    def block(self, d_loc: oracle.Decoded) -> Optional[np.ndarray]:
+        """Part 1: this rank's exchange block for the window (what the GPU all-gathers)."""
+        if self.world <= 1 or self.xchg_cap <= 0:
+            return None
+        mine = oracle.trace_rows(d_loc, len(d_loc.ts))
+        self.sent = min(len(mine.ts), self.xchg_cap)
+        return oracle.exchange_blocks([mine], self.xchg_cap)
+
+    def join(self, d_loc: oracle.Decoded, spans: np.ndarray, n_groups: int, blocks=None, **join_kw):
+        """Part 2: join [window rows | halo of k-1 | other ranks' rows], keep the next halo."""
+        imp = self.imports
+        for r, blk in enumerate(blocks or []):
+            if r != self.rank:
+                imp = oracle.concat(imp, parse_block(blk))
+        imp = oracle.take(imp, np.arange(len(imp.ts)) < self.import_cap)
+        d = oracle.concat(d_loc, imp)
+        res = oracle.join(d, spans, n_groups, **join_kw)
+        res.n_rows = len(d.ts)
+        halo = oracle.halo_rows(d, len(d_loc.ts), self.halo_ns) if self.halo_ns > 0 else oracle.empty_rows()
+        self.imports = oracle.take(halo, np.arange(len(halo.ts)) < self.import_cap)
+        return res
+
+    def window(self, d_loc: oracle.Decoded, spans: np.ndarray, n_groups: int, **join_kw):
+        blk = self.block(d_loc)
+        blocks = self.allgather(blk) if blk is not None and self.allgather is not None else None
+        return self.join(d_loc, spans, n_groups, blocks, **join_kw)

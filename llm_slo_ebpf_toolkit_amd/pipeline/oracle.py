@@ -200,10 +200,10 @@ def halo_rows(d: Decoded, n_local: int, halo_ns: int) -> Decoded:
 
 
 def trace_rows(d: Decoded, n_local: int) -> Decoded:
-    """k_sel (trace): the window's own trace-tagged joinable rows, identity cleared (a remote
-    GPU joins them by trace hash only), in row order."""
+    """k_sel (trace): the window's own trace-tagged joinable rows at warn level or above,
+    identity cleared (a remote GPU joins them by trace hash only), in row order."""
     loc = take(d, np.arange(len(d.ts)) < n_local)
-    m = (loc.slot != NO_SLOT) & (loc.ts != 0) & (loc.trace != 0)
+    m = (loc.slot != NO_SLOT) & (loc.ts != 0) & (loc.trace != 0) & (loc.status >= 1)
     out = take(loc, m)
     for f in ("pod", "pid", "svcnode"):
         setattr(out, f, np.zeros_like(getattr(out, f)))
@@ -241,16 +241,31 @@ def from_sigrec(r: np.ndarray) -> Decoded:
                    r["tr"].astype(np.uint64), r["cn"].astype(np.uint64))
 
 
+XREC = np.dtype([("ts", "<i8"), ("tr", "<u8"), ("val", "<f4"), ("slot", "<u4"), ("pad", "<u4", (2,))])
+assert XREC.itemsize == 32
+
+
 def exchange_blocks(parts, cap: int) -> np.ndarray:
-    """Per-rank exchange blocks as the GPUs all-gather them: [64-byte header: row count | rows]."""
-    stride = 64 * (1 + cap)
+    """Per-rank exchange blocks as the GPUs all-gather them (mislo_launch.h XRec):
+    [32-byte header: row count | 32-byte rows]."""
+    stride = 32 * (1 + cap)
     out = np.zeros(len(parts) * stride, dtype=np.uint8)
     for r, p in enumerate(parts):
-        rows = to_sigrec(p)[:cap]
+        n = min(len(p.ts), cap)
+        rows = np.zeros(n, dtype=XREC)
+        rows["ts"], rows["tr"], rows["val"] = p.ts[:n], p.trace[:n], p.val[:n]
+        rows["slot"] = np.where(p.slot[:n] == NO_SLOT, 0xFF, p.slot[:n])
         blk = out[r * stride:(r + 1) * stride]
-        blk[:4] = np.frombuffer(np.uint32(len(rows)).tobytes(), dtype=np.uint8)
-        blk[64:64 + rows.nbytes] = rows.view(np.uint8)
+        blk[:4] = np.frombuffer(np.uint32(n).tobytes(), dtype=np.uint8)
+        blk[32:32 + rows.nbytes] = rows.view(np.uint8)
     return out
+
+
+def remote_rows(p: Decoded) -> Decoded:
+    """What a GPU imports from an exchanged row: time, trace hash, value, signal; no identity."""
+    z32 = np.zeros(len(p.ts), np.uint32)
+    return Decoded(p.ts.copy(), p.val.copy(), p.slot.copy(), status_of(p.val, p.slot), z32, z32.copy(), z32.copy(),
+                   p.trace.copy(), np.zeros(len(p.ts), np.uint64))
 
 
 def decode_span20(sp: np.ndarray, table: CtxTable) -> np.ndarray:

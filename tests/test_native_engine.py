@@ -177,15 +177,17 @@ def test_pipelined_learning_with_graphs_and_device_refit():
 
 def test_halo_and_remote_rows_join_like_the_oracle():
     """Imported rows: window k+1 joins (never counts) window k's rows within the halo of its
-    latest record, plus rows other GPUs exchanged (injected here as RCCL would deliver them:
-    trace-tagged, identity cleared). Features, candidates and counters match the oracle run
-    over [window rows | imports] with the same stable selections."""
+    latest record; a window also joins the rows the other GPUs exchanged in the same window
+    (injected here as the all-gather would deliver them: XRec blocks, no identity), through the
+    engine's two-part chain. Features, candidates and counters match the oracle run over
+    [window rows | halo | other GPUs' rows] with the same stable selections."""
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
     wins, gen = windows(n_win=3, seed=43)
     imgs = build_replay_images(wins)
     halo_ms, icap = 2000.0, 16384
-    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096, halo_ms=halo_ms, import_cap=icap)
+    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096, halo_ms=halo_ms, import_cap=icap,
+                          xchg_cap=64)
     rb, user, spans = rings("halo")
     src = RingWindowSource(pipe, rb, user, spans)
     pods, sn = pod_meta(gen)
@@ -216,9 +218,12 @@ def test_halo_and_remote_rows_join_like_the_oracle():
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d_loc))  # imports never count
         fr = img.framed.view(np.uint32).reshape(-1, 6)
         assert pk["ring_state"]["events"] == int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
-        np.testing.assert_array_equal(res["feat"], ref.feat)
         dbg = pk["dbg"][:5].astype(np.int64).tolist()
-        assert dbg[0] == ref.debug["candidates"] and dbg[4] == ref.debug["spans_enriched"]
+        st = pipe.eng.import_state()  # rows[0], rows[1], tmax, halo_n[nb], remote_n[nb]
+        assert st[0] == n_loc + len(imports.ts) - (40 if j == 2 else 0) and st[1] == n_loc + len(imports.ts), (j, st)
+        assert st[2] == oracle.window_tmax(d_loc, n_loc), (j, st)
+        assert (dbg[0], dbg[4]) == (ref.debug["candidates"], ref.debug["spans_enriched"]), (j, len(imports.ts), dbg)
+        np.testing.assert_array_equal(res["feat"], ref.feat, err_msg=f"window {j}")
         n_imported.append(len(imports.ts))
         halo = oracle.halo_rows(d, n_loc, int(halo_ms * 1e6))
         imports = oracle.take(halo, np.arange(len(halo.ts)) < icap)

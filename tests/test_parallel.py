@@ -1,5 +1,7 @@
-"""Distributed path on CPU (gloo, world_size 2, 127.0.0.1): node sharding + trace-event
-all-gather + packet all-reduce must reproduce the single-process window exactly."""
+"""Distributed path on CPU (gloo, world_size 2, 127.0.0.1): the engine's multi-GPU window
+protocol (parallel/exchange.py, the CPU model of ops/csrc/exchange.hip) over a real process
+group -- node-sharded streams, the halo carried across window cuts, warn-level trace rows
+exchanged as 32-byte XRec blocks and imported one window later, the packet all-reduce."""
 
 import os
 import socket
@@ -7,30 +9,32 @@ import socket
 import numpy as np
 import pytest
 
-from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
 from llm_slo_ebpf_toolkit_amd.parallel import exchange, shard
 from llm_slo_ebpf_toolkit_amd.pipeline import oracle
-from llm_slo_ebpf_toolkit_amd.pipeline.cpu import CpuWindowEngine
 from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
 
 WORLD = 2
+HALO_MS, ICAP, XCAP = 2000.0, 20000, 4000
 
 
-def global_window(seed=3):
+def global_windows(n_win=3, seed=3):
+    """Consecutive windows of a 4-node cluster; a third of the trace-tagged events moved to
+    pods on other nodes, so traces cross the node shards."""
     cfg = ReplayConfig(scenario="full", n_nodes=4, pods_per_node=4, n_services=8, events_per_window=6000,
                        spans_per_window=400, seed=seed)
-    w = ReplayGenerator(cfg).next_window()
-    ev = w.events.copy()
+    g = ReplayGenerator(cfg)
     rng = np.random.default_rng(seed)
-    # move a third of the trace-tagged events to pods on other nodes: cross-node traces
-    idx = np.nonzero(ev["trace_h"] != 0)[0]
-    mv = rng.choice(idx, size=len(idx) // 3, replace=False)
-    donors = rng.integers(0, len(ev), size=len(mv))
-    for f in ("pod_id", "node_id", "svc_id", "pid"):
-        ev[f][mv] = ev[f][donors]
-    # unique timestamps so top-3 tie-breaks never depend on array order
-    ev["ts_ns"] = ev["ts_ns"] + np.arange(len(ev), dtype=np.int64) % 7 * 0 + rng.permutation(len(ev)) * 3
-    return ev, w.spans.copy(), w.n_groups, w.group_labels.copy()
+    out = []
+    for _ in range(n_win):
+        w = g.next_window()
+        ev = w.events.copy()
+        idx = np.nonzero(ev["trace_h"] != 0)[0]
+        mv = rng.choice(idx, size=len(idx) // 3, replace=False)
+        donors = rng.integers(0, len(ev), size=len(mv))
+        for f in ("pod_id", "node_id", "svc_id", "pid"):
+            ev[f][mv] = ev[f][donors]
+        out.append((ev, w.spans.copy(), w.n_groups))
+    return out
 
 
 def _free_port():
@@ -41,6 +45,18 @@ def _free_port():
     return p
 
 
+def _run_rank(rank, wins, allgather, xchg=XCAP):
+    m = exchange.ExchangeModel(rank, WORLD, HALO_MS, ICAP, xchg, allgather)
+    out = []
+    for ev, sp, G in wins:
+        ev_l, sp_l = shard.shard(ev, sp, rank, WORLD)
+        d = oracle.decode_events(ev_l)
+        res = m.window(d, sp_l, G)
+        out.append(dict(feat=res.feat, cnt=res.cnt, gsum=res.gsum, gcnt=res.gcnt, hist=oracle.histograms(d),
+                        n_rows=res.n_rows, n_loc=len(d.ts), sent=m.sent))
+    return out
+
+
 def _worker(rank, world, port, outdir):
     import torch
     import torch.distributed as dist
@@ -48,79 +64,82 @@ def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        ev, sp, G, labels = global_window()
-        ev_l, sp_l = shard.shard(ev, sp, rank, world)
-        merged, n_local = exchange.with_remote_trace_events(ev_l)
-        eng = CpuWindowEngine(NaiveBayes.ref())
-
-        def reduce_groups(gsum, gcnt):
-            gs, gc = torch.from_numpy(gsum.copy()), torch.from_numpy(gcnt.copy())
-            dist.all_reduce(gs)
-            dist.all_reduce(gc)
-            return gs.numpy(), gc.numpy()
-
-        owned = labels.copy()
-        owned[np.arange(G) % world != rank] = -1  # each incident group is scored once node-wide
-        res = eng.run(merged, sp_l, G, owned, n_local=n_local, learn=True, reduce_groups=reduce_groups)
-        pk = torch.from_numpy(res.packet.copy())
-        dist.all_reduce(pk)
-        gs, gc = reduce_groups(res.join.gsum, res.join.gcnt)
-        np.savez(os.path.join(outdir, f"r{rank}.npz"), span_h=sp_l["span_h"], attrs=res.join.attrs,
-                 conf=res.join.conf, cnt=res.join.cnt, packet=pk.numpy(), gsum=gs, gcnt=gc,
-                 n_local=n_local, n_merged=merged.shape[0])
+        res = _run_rank(rank, global_windows(), exchange.torch_allgather())
+        hist = torch.from_numpy(np.stack([r["hist"] for r in res]))
+        dist.all_reduce(hist)  # the packet all-reduce: node-wide counters
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), hist=hist.numpy(),
+                 **{f"{k}{j}": r[k] for j, r in enumerate(res) for k in ("feat", "cnt", "gsum", "gcnt")},
+                 n_rows=[r["n_rows"] for r in res], n_loc=[r["n_loc"] for r in res], sent=[r["sent"] for r in res])
     finally:
         dist.destroy_process_group()
 
 
+def _in_memory(wins, xchg=XCAP):
+    """Both ranks in one process, the all-gather done by hand (same blocks)."""
+    ms = [exchange.ExchangeModel(r, WORLD, HALO_MS, ICAP, xchg) for r in range(WORLD)]
+    out = [[] for _ in range(WORLD)]
+    for ev, sp, G in wins:
+        loc = [shard.shard(ev, sp, r, WORLD) for r in range(WORLD)]
+        ds = [oracle.decode_events(e) for e, _ in loc]
+        blocks = [m.block(d) for m, d in zip(ms, ds)]
+        for r, m in enumerate(ms):
+            out[r].append(m.join(ds[r], loc[r][1], G, blocks if xchg else None))
+    return out
+
+
 def test_sharding_covers_every_record_once():
-    ev, sp, _, _ = global_window()
+    ev, sp, _ = global_windows(1)[0]
     parts = [shard.shard(ev, sp, r, 3) for r in range(3)]
     assert sum(p[0].shape[0] for p in parts) == ev.shape[0]
     assert sum(p[1].shape[0] for p in parts) == sp.shape[0]
 
 
-def test_halo_carries_recent_events():
-    ev, sp, G, _ = global_window()
-    order = np.argsort(ev["ts_ns"])
-    first, second = ev[order[: len(ev) // 2]], ev[order[len(ev) // 2:]]
-    h = exchange.Halo(outer_ns=2_000_000_000)
-    m1, n1 = h.extend(first, sp)
-    assert n1 == m1.shape[0] == first.shape[0]
-    m2, n2 = h.extend(second, sp)
-    assert n2 == second.shape[0] and m2.shape[0] > n2
-    assert (m2["ts_ns"][n2:] >= int(sp["ts_ns"].min()) - 2_000_000_000).all()
+def test_halo_carries_the_previous_windows_tail():
+    wins = global_windows()
+    m = exchange.ExchangeModel(0, 1, HALO_MS, ICAP, 0)
+    n_imp = []
+    for ev, sp, G in wins:
+        d = oracle.decode_events(ev)
+        res = m.window(d, sp, G)
+        n_imp.append(res.n_rows - len(d.ts))
+        tmax = oracle.window_tmax(d, len(d.ts))
+        assert (m.imports.ts >= tmax - int(HALO_MS * 1e6)).all()
+    assert n_imp[0] == 0 and all(n > 0 for n in n_imp[1:])
+
+
+def test_exchange_block_roundtrip():
+    d = oracle.decode_events(global_windows(1)[0][0])
+    rows = oracle.trace_rows(d, len(d.ts))
+    back = exchange.parse_block(oracle.exchange_blocks([rows], 100000))
+    np.testing.assert_array_equal(back.ts, rows.ts)
+    np.testing.assert_array_equal(back.trace, rows.trace)
+    np.testing.assert_array_equal(back.val, rows.val)
+    assert (back.pod == 0).all() and (back.conn == 0).all() and (rows.status >= 1).all()
 
 
 @pytest.mark.timeout(300)
-def test_gloo_two_ranks_match_single_process(tmp_path):
+def test_gloo_two_ranks_run_the_device_protocol(tmp_path):
     import torch.multiprocessing as mp
 
     mp.spawn(_worker, args=(WORLD, _free_port(), str(tmp_path)), nprocs=WORLD, join=True)
-    ev, sp, G, labels = global_window()
-    ref = CpuWindowEngine(NaiveBayes.ref()).run(ev, sp, G, labels, learn=True)
-    r = [np.load(tmp_path / f"r{k}.npz") for k in range(WORLD)]
-    # per-span enrichment identical to the global batch (trace tier crosses the shards)
-    pos = {int(h): i for i, h in enumerate(sp["span_h"])}
-    for part in r:
-        for j, h in enumerate(part["span_h"]):
-            i = pos[int(h)]
-            np.testing.assert_array_equal(part["attrs"][j], ref.join.attrs[i])
-            assert part["conf"][j] == ref.join.conf[i] and part["cnt"][j] == ref.join.cnt[i]
-    assert any(p["n_merged"] > p["n_local"] for p in r)  # remote trace events were imported
-    # incident features and the packed window statistics all-reduce to the global values
-    np.testing.assert_array_equal(r[0]["gcnt"], ref.join.gcnt)
-    np.testing.assert_allclose(r[0]["gsum"], ref.join.gsum, rtol=1e-12)
-    pk, gp = r[0]["packet"], ref.packet
-    lay = np.cumsum((0,) + tuple(oracle_layout()))
-    for k, name in enumerate(("hist", "status", "misc", "dbg", "confusion")):
-        np.testing.assert_array_equal(pk[lay[k]:lay[k + 1]], gp[lay[k]:lay[k + 1]], err_msg=name)
-    np.testing.assert_allclose(pk[lay[5]:], gp[lay[5]:], rtol=1e-9, atol=1e-9)
-
-
-def oracle_layout():
-    from llm_slo_ebpf_toolkit_amd.pipeline.window import PACKET_LAYOUT
-
-    return PACKET_LAYOUT
+    wins = global_windows()
+    ref = _in_memory(wins)
+    solo = _in_memory(wins, xchg=0)  # the same ranks without the exchange
+    got = [np.load(tmp_path / f"r{k}.npz") for k in range(WORLD)]
+    for r in range(WORLD):
+        for j in range(len(wins)):
+            np.testing.assert_array_equal(got[r][f"feat{j}"], ref[r][j].feat)
+            np.testing.assert_array_equal(got[r][f"cnt{j}"], ref[r][j].cnt)
+            np.testing.assert_array_equal(got[r][f"gcnt{j}"], ref[r][j].gcnt)
+        assert (got[r]["sent"] > 0).all() and (got[r]["n_rows"] > got[r]["n_loc"]).all()
+    # cross-node traces: the exchange adds the other shard's elevated signals to the spans'
+    # candidates in the same window
+    for j in range(len(wins)):
+        extra = sum(int(ref[r][j].cnt.sum() - solo[r][j].cnt.sum()) for r in range(WORLD))
+        assert extra > 0, j
+    # node-wide counters: the all-reduced per-rank histograms are the global histograms
+    for j, (ev, _, _) in enumerate(wins):
+        np.testing.assert_array_equal(got[0]["hist"][j], oracle.histograms(oracle.decode_events(ev)))
 
 
 def test_numa_cpulist_and_affinity_choice(tmp_path):
