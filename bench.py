@@ -375,6 +375,11 @@ def main() -> int:
         "kernel_ring_records_per_step": int(kernel_recs // max(a.steps, 1)),
         "host_us_per_window": round(host_us, 1),
         "host_issue_us_per_window": round(pipe.eng.host_issue_us, 1),
+        "host_issue_wait_us_per_window": round(pipe.eng.host_wait_us, 1),
+        "host_issue_dma_us_per_window": round(pipe.eng.host_dma_issue_us, 1),
+        "host_issue_launch_us_per_window": round(pipe.eng.host_launch_us, 1),
+        "host_issue_pre_us_per_window": round(pipe.eng.host_pre_us, 1),
+        "host_issue_tail_us_per_window": round(pipe.eng.host_tail_us, 1),
         "records_over_window_budget": int(src.carried),
         "direct_dma_fraction": round(pipe.eng.direct_bytes / max(1, pipe.eng.direct_bytes + pipe.eng.staged_bytes), 4),
         "producer_wait_ms_total": round(producer_wait_ms, 2),

@@ -234,6 +234,9 @@ class PyEngine {
   int64_t folded() { return eng().windows_folded(); }
   size_t graphs() { return eng().graphs(); }
   double host_issue_us() { return eng().host_issue_us(); }
+  double host_wait_us() { return eng().host_wait_us(); }
+  double host_dma_issue_us() { return eng().host_dma_issue_us(); }
+  double host_launch_us() { return eng().host_launch_us(); }
   bool has_comm() { return eng().has_comm(); }
   size_t staged_bytes() { return eng().staged_bytes(); }
   size_t direct_bytes() { return eng().direct_bytes(); }
@@ -305,6 +308,11 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def_property_readonly("windows_folded", &PyEngine::folded)
       .def_property_readonly("graphs", &PyEngine::graphs)
       .def_property_readonly("host_issue_us", &PyEngine::host_issue_us)
+      .def_property_readonly("host_wait_us", &PyEngine::host_wait_us)
+      .def_property_readonly("host_dma_issue_us", &PyEngine::host_dma_issue_us)
+      .def_property_readonly("host_launch_us", &PyEngine::host_launch_us)
+      .def_property_readonly("host_pre_us", [](PyEngine& p) { return p.eng().host_pre_us(); })
+      .def_property_readonly("host_tail_us", [](PyEngine& p) { return p.eng().host_tail_us(); })
       .def_property_readonly("has_comm", &PyEngine::has_comm)
       .def_property_readonly("rank", [](PyEngine& p) { return p.eng().rank(); })
       .def_property_readonly("world", [](PyEngine& p) { return p.eng().world(); })

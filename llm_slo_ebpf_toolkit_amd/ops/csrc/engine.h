@@ -155,6 +155,12 @@ class WindowEngine {
   size_t direct_bytes() const { return direct_bytes_; }
   size_t graphs() const { return graphs_.size(); }
   double host_issue_us() const { return issue_n_ ? issue_us_ / issue_n_ : 0.0; }
+  // of which: blocked on back-pressure events, and issuing the window's DMAs
+  double host_wait_us() const { return issue_n_ ? wait_us_ / issue_n_ : 0.0; }
+  double host_dma_issue_us() const { return issue_n_ ? dma_us_ / issue_n_ : 0.0; }
+  double host_launch_us() const { return issue_n_ ? launch_us_ / issue_n_ : 0.0; }  // the chain's launch
+  double host_pre_us() const { return issue_n_ ? pre_us_ / issue_n_ : 0.0; }     // stream waits + refit
+  double host_tail_us() const { return issue_n_ ? tail_us_ / issue_n_ : 0.0; }   // results D2H + comm stream
 
  private:
   void alloc();
@@ -236,7 +242,7 @@ class WindowEngine {
   std::vector<bool> warm_;
   std::vector<hipGraph_t> graph_defs_;
   int64_t submitted_ = 0, folded_ = 0;
-  double issue_us_ = 0;
+  double issue_us_ = 0, wait_us_ = 0, dma_us_ = 0, launch_us_ = 0, pre_us_ = 0, tail_us_ = 0;
   int64_t issue_n_ = 0;
 };
 

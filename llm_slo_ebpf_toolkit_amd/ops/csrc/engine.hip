@@ -71,9 +71,39 @@ __global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsig
   }
 }
 
-__global__ void k_accumulate(const double* __restrict__ packet, double* __restrict__ totals, int n) {
+// totals += packet, and the packet stored straight into its pinned host block
+__global__ void k_accumulate(const double* __restrict__ packet, double* __restrict__ totals, int n,
+                             double* __restrict__ host) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) totals[i] += packet[i];
+  if (i < n) {
+    const double v = packet[i];
+    totals[i] += v;
+    host[i] = v;
+  }
+}
+
+// Device -> pinned host results: the kernel stores over PCIe itself. A small hipMemcpyAsync
+// D2H is served by a host-side read of device memory, which blocks the issuing thread until
+// the stream reaches the copy -- the whole window's compute (measured: ~480 us per window of
+// host time in submit) -- where a kernel store is queued like any other launch.
+__global__ void k_to_host(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+void to_host(const void* src, void* dst, size_t bytes, hipStream_t st) {
+  const size_t n16 = (bytes + 15) / 16;
+  const int g = (int)std::min<size_t>(64, (n16 + 255) / 256);
+  hipLaunchKernelGGL(k_to_host, dim3(g > 0 ? g : 1), dim3(256), 0, st, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(dst), n16);
+}
+
+// pinned, device-visible host memory the kernels store into (uncached on the device side)
+void* host_block(size_t bytes) {
+  void* h = nullptr;
+  HIPCHECK(hipHostMalloc(&h, (bytes + 15) & ~size_t(15), hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(h, 0, bytes);
+  return h;
 }
 
 template <class T>
@@ -151,9 +181,7 @@ void WindowEngine::alloc() {
     staging_.push_back(nullptr);  // pinned staging is allocated on first use (unregistered rings only)
     packet_dev_.push_back(dalloc<double>(kPacketLen));
     HIPCHECK(hipMemset(packet_dev_.back(), 0, kPacketLen * sizeof(double)));
-    HIPCHECK(hipHostMalloc(&h, kPacketLen * sizeof(double), hipHostMallocDefault));
-    std::memset(h, 0, kPacketLen * sizeof(double));
-    packet_host_.push_back(static_cast<double*>(h));
+    packet_host_.push_back(static_cast<double*>(host_block(kPacketLen * sizeof(double))));
     h2d_done_.push_back(mk_event(false));
     compute_done_.push_back(mk_event(false));
     comm_done_.push_back(mk_event(false));
@@ -169,10 +197,7 @@ void WindowEngine::alloc() {
   const size_t o_sli = o_ev + 16 * G * 4;
   res_bytes_ = o_sli + 2 * G * 4;
   for (int b = 0; b < nb_; ++b) {
-    void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, res_bytes_, hipHostMallocDefault));
-    std::memset(h, 0, res_bytes_);
-    res_host_.push_back(static_cast<uint8_t*>(h));
+    res_host_.push_back(static_cast<uint8_t*>(host_block(res_bytes_)));
   }
   for (int b = 0; b < nb_; ++b) {  // per buffer: the comm stream gathers window k's while k+1 computes
     res_dev_.push_back(dalloc<uint8_t>(res_bytes_));
@@ -499,9 +524,12 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     throw std::invalid_argument("window exceeds the engine's capacity (events / user records / spans)");
   const int b = (int)(k % nb_);
   // host back-pressure: at most max_ahead windows queued beyond the one computing
+  const auto tw = std::chrono::steady_clock::now();
   if (k >= max_ahead_) HIPCHECK(hipEventSynchronize(compute_done_[(k - max_ahead_) % nb_]));
   // the pinned head / staging of buffer b were last read by the DMAs of window k - nb
   if (k >= nb_) HIPCHECK(hipEventSynchronize(h2d_done_[b]));
+  wait_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
+  const auto td = std::chrono::steady_clock::now();
   int32_t* c = reinterpret_cast<int32_t*>(head_host_[b]);
   std::memset(c, 0, kHeadBytes);
   c[0] = (int32_t)(n_k + n_u);
@@ -527,6 +555,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   dma(in.user, dst + off_user_, 64 * (size_t)cfg_.user_cap, staging_[b], st_off);
   dma(in.spans, dst + off_span_, 64 * (size_t)cfg_.span_cap, staging_[b], st_off);
   HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
+  const auto te = std::chrono::steady_clock::now();
+  dma_us_ += std::chrono::duration<double, std::micro>(te - td).count();
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
   HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
@@ -539,6 +569,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   }
   const bool injected = !inject_.empty();
   const bool xchg = exchange() || injected;
+  const auto tl = std::chrono::steady_clock::now();
+  pre_us_ += std::chrono::duration<double, std::micro>(tl - te).count();
   if (!xchg) {
     launch_part(0, b, n_groups, with_labels, learn, false);
   } else {
@@ -567,8 +599,10 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     }
     launch_part(2, b, n_groups, with_labels, learn, true);
   }
+  const auto tt = std::chrono::steady_clock::now();
+  launch_us_ += std::chrono::duration<double, std::micro>(tt - tl).count();
   // per-incident results of this window (the buffers are reused by the next window)
-  HIPCHECK(hipMemcpyAsync(res_host_[b], res_dev_[b], res_bytes_, hipMemcpyDeviceToHost, compute_));
+  to_host(res_dev_[b], res_host_[b], res_bytes_, compute_);
   HIPCHECK(hipEventRecord(t_comp1_[b], compute_));
   HIPCHECK(hipEventRecord(compute_done_[b], compute_));
   HIPCHECK(hipStreamWaitEvent(comm_stream_, compute_done_[b], 0));
@@ -578,17 +612,16 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen, ncclFloat64, ncclSum, comm_, comm_stream_));
     NCCLCHECK(ncclAllGather(res_dev_[b], res_all_dev_[b], res_bytes_, ncclUint8, comm_, comm_stream_));
     NCCLCHECK(ncclGroupEnd());
-    HIPCHECK(hipMemcpyAsync(res_all_host_[b], res_all_dev_[b], res_bytes_ * world_, hipMemcpyDeviceToHost,
-                            comm_stream_));
+    to_host(res_all_dev_[b], res_all_host_[b], res_bytes_ * world_, comm_stream_);
   }
   hipLaunchKernelGGL(k_accumulate, dim3((kPacketLen + 255) / 256), dim3(256), 0, comm_stream_, packet_dev_[b], totals_,
-                     kPacketLen);
-  HIPCHECK(hipMemcpyAsync(packet_host_[b], packet_dev_[b], kPacketLen * sizeof(double), hipMemcpyDeviceToHost,
-                          comm_stream_));
+                     kPacketLen, packet_host_[b]);
   HIPCHECK(hipEventRecord(t_end_[b], comm_stream_));
   HIPCHECK(hipEventRecord(comm_done_[b], comm_stream_));
   ++submitted_;
-  issue_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  const auto t1 = std::chrono::steady_clock::now();
+  tail_us_ += std::chrono::duration<double, std::micro>(t1 - tt).count();
+  issue_us_ += std::chrono::duration<double, std::micro>(t1 - t0).count();
   ++issue_n_;
 }
 
@@ -689,10 +722,7 @@ void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
   world_ = world;
   for (int b = 0; b < nb_; ++b) {
     res_all_dev_.push_back(dalloc<uint8_t>(res_bytes_ * world));
-    void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, res_bytes_ * world, hipHostMallocDefault));
-    std::memset(h, 0, res_bytes_ * world);
-    res_all_host_.push_back(static_cast<uint8_t*>(h));
+    res_all_host_.push_back(static_cast<uint8_t*>(host_block(res_bytes_ * world)));
   }
   if (cfg_.xchg_cap) {
     if (world > 8) throw std::invalid_argument("the exchange is sized for <= 8 GPUs per node");
