@@ -240,7 +240,7 @@ def main() -> int:
     if pg is not None:
         dist.barrier()
     pipe.reset_totals()
-    host0, n0 = src.host_s, src.n
+    host0, n0, reap0, sub0 = src.host_s, src.n, src.reap_s, src.submit_s
     wait_s[0] = 0.0
 
     # ---- timed region ----------------------------------------------------------------------
@@ -265,6 +265,8 @@ def main() -> int:
     busy_cpu_pct, _, _ = meter.stop()
     dev_ms = [pipe.window_ms(k) for k in range(max(0, last - pipe.nb + 1), last + 1)]
     host_us = 1e6 * (src.host_s - host0) / max(src.n - n0, 1)
+    reap_us = 1e6 * (src.reap_s - reap0) / max(src.n - n0, 1)
+    submit_us = 1e6 * (src.submit_s - sub0) / max(src.n - n0, 1)
     producer_wait_ms = 1e3 * wait_s[0]
     if pg is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -374,11 +376,14 @@ def main() -> int:
         "join_pairs_per_step": int(dbg[0] // max(a.steps, 1)),
         "kernel_ring_records_per_step": int(kernel_recs // max(a.steps, 1)),
         "host_us_per_window": round(host_us, 1),
+        "host_reap_us_per_window": round(reap_us, 1),
+        "host_submit_us_per_window": round(submit_us, 1),
         "host_issue_us_per_window": round(pipe.eng.host_issue_us, 1),
         "host_issue_wait_us_per_window": round(pipe.eng.host_wait_us, 1),
         "host_issue_dma_us_per_window": round(pipe.eng.host_dma_issue_us, 1),
         "host_issue_launch_us_per_window": round(pipe.eng.host_launch_us, 1),
         "host_issue_pre_us_per_window": round(pipe.eng.host_pre_us, 1),
+        "host_issue_dma_split_us": [round(x, 1) for x in pipe.eng.host_dma_split_us],
         "host_issue_tail_us_per_window": round(pipe.eng.host_tail_us, 1),
         "records_over_window_budget": int(src.carried),
         "direct_dma_fraction": round(pipe.eng.direct_bytes / max(1, pipe.eng.direct_bytes + pipe.eng.staged_bytes), 4),

@@ -312,6 +312,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def_property_readonly("host_dma_issue_us", &PyEngine::host_dma_issue_us)
       .def_property_readonly("host_launch_us", &PyEngine::host_launch_us)
       .def_property_readonly("host_pre_us", [](PyEngine& p) { return p.eng().host_pre_us(); })
+      .def_property_readonly("host_dma_split_us", [](PyEngine& p) { return p.eng().host_dma_split_us(); })
       .def_property_readonly("host_tail_us", [](PyEngine& p) { return p.eng().host_tail_us(); })
       .def_property_readonly("has_comm", &PyEngine::has_comm)
       .def_property_readonly("rank", [](PyEngine& p) { return p.eng().rank(); })

@@ -170,7 +170,8 @@ class WindowEngine {
   SignalCols sig_cols() const;
   SpanCols span_cols() const;
   bool registered(const void* p, size_t n) const;
-  size_t dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap, uint8_t*& staging, size_t& st_off);
+  size_t dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap, uint8_t*& staging, size_t& st_off,
+             hipStream_t st);
 
   EngineConfig cfg_;
   int nb_, max_ahead_;
@@ -198,7 +199,7 @@ class WindowEngine {
   bool exchange() const { return comm_ && cfg_.xchg_cap > 0 && cfg_.import_cap > 0; }
   JoinParams jp_{};
   int nblk_sig_ = 1, nblk_span_ = 1;
-  hipStream_t copy_ = nullptr, compute_ = nullptr, comm_stream_ = nullptr;
+  hipStream_t copy_ = nullptr, copy2_ = nullptr, compute_ = nullptr, comm_stream_ = nullptr;
   ncclComm_t comm_ = nullptr;
   // device buffers
   std::vector<uint8_t*> in_dev_;     // per buffer: [head | framed | user | spans]
@@ -236,13 +237,23 @@ class WindowEngine {
   int32_t* pred_ = nullptr;
   uint32_t* evbits_ = nullptr;
   // events
-  std::vector<hipEvent_t> h2d_done_, compute_done_, comm_done_;
+  std::vector<hipEvent_t> h2d_done_, h2d_part_, compute_done_, comm_done_;
   std::vector<hipEvent_t> t_start_, t_comp0_, t_comp1_, t_end_;
   std::map<std::tuple<int, int, bool, bool>, hipGraphExec_t> graphs_;
   std::vector<bool> warm_;
   std::vector<hipGraph_t> graph_defs_;
   int64_t submitted_ = 0, folded_ = 0;
   double issue_us_ = 0, wait_us_ = 0, dma_us_ = 0, launch_us_ = 0, pre_us_ = 0, tail_us_ = 0;
+  double split_us_[4] = {0, 0, 0, 0};  // DMA issue: ring bytes, head, user records, spans
+
+ public:
+  std::vector<double> host_dma_split_us() const {
+    std::vector<double> v;
+    for (double x : split_us_) v.push_back(issue_n_ ? x / issue_n_ : 0.0);
+    return v;
+  }
+
+ private:
   int64_t issue_n_ = 0;
 };
 

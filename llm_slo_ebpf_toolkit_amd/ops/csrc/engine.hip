@@ -2,6 +2,7 @@
 #include "engine.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -82,10 +83,11 @@ __global__ void k_accumulate(const double* __restrict__ packet, double* __restri
   }
 }
 
-// Device -> pinned host results: the kernel stores over PCIe itself. A small hipMemcpyAsync
-// D2H is served by a host-side read of device memory, which blocks the issuing thread until
-// the stream reaches the copy -- the whole window's compute (measured: ~480 us per window of
-// host time in submit) -- where a kernel store is queued like any other launch.
+// Small copies between device memory and pinned host memory, by a kernel (loads or stores over
+// PCIe). A small hipMemcpyAsync is served by the host through the BAR, which blocks the issuing
+// thread until the stream reaches the copy -- for the results D2H the whole window's compute
+// (measured: ~480 us per window of host time in submit) -- where a kernel is queued like any
+// other launch.
 __global__ void k_to_host(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = src[i];
@@ -163,6 +165,11 @@ void WindowEngine::alloc() {
   nblk_sig_ = decode_grid((int)N);
   nblk_span_ = decode_grid((int)S);
   HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  {  // diagnostic knob: MISLO_COPY_STREAMS=1 puts the whole window's DMA on one stream
+    const char* v = getenv("MISLO_COPY_STREAMS");
+    if (v && atoi(v) == 1) copy2_ = copy_;
+    else HIPCHECK(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking));
+  }
   HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   HIPCHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   // device input block per buffer: [head (counts + labels) | framed ring records | user records | spans]
@@ -175,14 +182,13 @@ void WindowEngine::alloc() {
     in_dev_.push_back(dalloc<uint8_t>(in_bytes_));
     HIPCHECK(hipMemset(in_dev_.back(), 0, in_bytes_));
     void* h = nullptr;
-    HIPCHECK(hipHostMalloc(&h, head, hipHostMallocDefault));
-    std::memset(h, 0, head);
-    head_host_.push_back(static_cast<uint8_t*>(h));
+    head_host_.push_back(static_cast<uint8_t*>(host_block(head)));
     staging_.push_back(nullptr);  // pinned staging is allocated on first use (unregistered rings only)
     packet_dev_.push_back(dalloc<double>(kPacketLen));
     HIPCHECK(hipMemset(packet_dev_.back(), 0, kPacketLen * sizeof(double)));
     packet_host_.push_back(static_cast<double*>(host_block(kPacketLen * sizeof(double))));
     h2d_done_.push_back(mk_event(false));
+    h2d_part_.push_back(mk_event(false));
     compute_done_.push_back(mk_event(false));
     comm_done_.push_back(mk_event(false));
     t_start_.push_back(mk_event(true));
@@ -288,7 +294,7 @@ WindowEngine::~WindowEngine() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   for (auto g : graph_defs_) hipGraphDestroy(g);
   if (comm_) ncclCommDestroy(comm_);
-  auto evs = {&h2d_done_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
+  auto evs = {&h2d_done_, &h2d_part_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
   for (auto* v : evs)
     for (auto e : *v) hipEventDestroy(e);
   for (auto& r : registered_) hipHostUnregister(const_cast<uint8_t*>(r.first));
@@ -315,6 +321,7 @@ WindowEngine::~WindowEngine() {
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_) hipStreamDestroy(copy_);
+  if (copy2_ && copy2_ != copy_) hipStreamDestroy(copy2_);
   if (compute_) hipStreamDestroy(compute_);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
@@ -342,7 +349,8 @@ bool WindowEngine::registered(const void* p, size_t n) const {
 
 // DMA a window's segments of one kind back to back into dst (device); unregistered segments go
 // through pinned staging (one host memcpy, then the DMA). Returns the bytes placed.
-size_t WindowEngine::dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap, uint8_t*& staging, size_t& st_off) {
+size_t WindowEngine::dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap, uint8_t*& staging, size_t& st_off,
+                         hipStream_t st) {
   size_t off = 0;
   for (const Seg& s : segs) {
     if (!s.bytes) continue;
@@ -361,21 +369,25 @@ size_t WindowEngine::dma(const std::vector<Seg>& segs, uint8_t* dst, size_t cap,
     } else {
       direct_bytes_ += s.bytes;
     }
-    HIPCHECK(hipMemcpyAsync(dst + off, src, s.bytes, hipMemcpyHostToDevice, copy_));
+    HIPCHECK(hipMemcpyAsync(dst + off, src, s.bytes, hipMemcpyHostToDevice, st));
     off += s.bytes;
   }
   return off;
 }
 
 bool WindowEngine::h2d_done(int64_t k) {
-  const hipError_t e = hipEventQuery(h2d_done_[k % nb_]);
-  if (e == hipSuccess) return true;
-  if (e == hipErrorNotReady) return false;
-  HIPCHECK(e);
-  return false;
+  for (hipEvent_t ev : {h2d_done_[k % nb_], h2d_part_[k % nb_]}) {  // both copy streams
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipErrorNotReady) return false;
+    HIPCHECK(e);
+  }
+  return true;
 }
 
-void WindowEngine::wait_h2d(int64_t k) { HIPCHECK(hipEventSynchronize(h2d_done_[k % nb_])); }
+void WindowEngine::wait_h2d(int64_t k) {
+  HIPCHECK(hipEventSynchronize(h2d_done_[k % nb_]));
+  HIPCHECK(hipEventSynchronize(h2d_part_[k % nb_]));
+}
 
 // The captured part of a window: everything between the DMA and the packet.
 // Part 1 of a window: accumulators, definitions, the decode of the window's records and the
@@ -527,7 +539,10 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   const auto tw = std::chrono::steady_clock::now();
   if (k >= max_ahead_) HIPCHECK(hipEventSynchronize(compute_done_[(k - max_ahead_) % nb_]));
   // the pinned head / staging of buffer b were last read by the DMAs of window k - nb
-  if (k >= nb_) HIPCHECK(hipEventSynchronize(h2d_done_[b]));
+  if (k >= nb_) {
+    HIPCHECK(hipEventSynchronize(h2d_done_[b]));
+    HIPCHECK(hipEventSynchronize(h2d_part_[b]));
+  }
   wait_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
   const auto td = std::chrono::steady_clock::now();
   int32_t* c = reinterpret_cast<int32_t*>(head_host_[b]);
@@ -545,19 +560,38 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   c[15] = (int32_t)n_k;
   int32_t* lab = reinterpret_cast<int32_t*>(head_host_[b] + kHeadBytes);
   for (int g = 0; g < cfg_.group_cap; ++g) lab[g] = (in.labels && g < n_groups) ? in.labels[g] : -1;
-  // DMAs once window k - nb (the device block's previous reader) computed
+  // DMAs once window k - nb (the device block's previous reader) computed, on two copy
+  // streams: the BPF ring's bytes on one, the head, user-space records and spans on the other.
+  // Back to back on one stream, the second SDMA transfer of a window started hundreds of us
+  // after the first ended whenever kernels were running (rocprofv3 memory-copy trace).
   HIPCHECK(hipStreamWaitEvent(copy_, compute_done_[b], 0));
+  HIPCHECK(hipStreamWaitEvent(copy2_, compute_done_[b], 0));
   HIPCHECK(hipEventRecord(t_start_[b], copy_));
   uint8_t* dst = in_dev_[b];
-  HIPCHECK(hipMemcpyAsync(dst, head_host_[b], off_kern_, hipMemcpyHostToDevice, copy_));
   size_t st_off = 0;
-  dma(in.kernel, dst + off_kern_, (size_t)kRecStride * cfg_.sig_cap, staging_[b], st_off);
-  dma(in.user, dst + off_user_, 64 * (size_t)cfg_.user_cap, staging_[b], st_off);
-  dma(in.spans, dst + off_span_, 64 * (size_t)cfg_.span_cap, staging_[b], st_off);
+  auto lap = [](std::chrono::steady_clock::time_point& t, double& acc) {
+    const auto n = std::chrono::steady_clock::now();
+    acc += std::chrono::duration<double, std::micro>(n - t).count();
+    t = n;
+  };
+  auto tq = std::chrono::steady_clock::now();
+  dma(in.kernel, dst + off_kern_, (size_t)kRecStride * cfg_.sig_cap, staging_[b], st_off, copy_);
+  lap(tq, split_us_[0]);
+  // the head (counts, epoch bases, labels: < 1 KiB) by a kernel load from pinned host memory:
+  // a small hipMemcpyAsync H2D is written by the host through the BAR once the stream reaches
+  // it, blocking this thread behind the stream's wait (window k - nb's compute)
+  to_host(head_host_[b], dst, off_kern_, copy2_);
+  lap(tq, split_us_[1]);
+  dma(in.user, dst + off_user_, 64 * (size_t)cfg_.user_cap, staging_[b], st_off, copy2_);
+  lap(tq, split_us_[2]);
+  dma(in.spans, dst + off_span_, 64 * (size_t)cfg_.span_cap, staging_[b], st_off, copy2_);
+  lap(tq, split_us_[3]);
+  HIPCHECK(hipEventRecord(h2d_part_[b], copy2_));
   HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
   const auto te = std::chrono::steady_clock::now();
   dma_us_ += std::chrono::duration<double, std::micro>(te - td).count();
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
+  HIPCHECK(hipStreamWaitEvent(compute_, h2d_part_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
   HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
   if (cfg_.device_refit && k >= nb_) {
@@ -755,6 +789,7 @@ void WindowEngine::model_bytes(void* out) {
 
 void WindowEngine::sync() {
   HIPCHECK(hipStreamSynchronize(copy_));
+  if (copy2_ != copy_) HIPCHECK(hipStreamSynchronize(copy2_));
   HIPCHECK(hipStreamSynchronize(compute_));
   HIPCHECK(hipStreamSynchronize(comm_stream_));
 }

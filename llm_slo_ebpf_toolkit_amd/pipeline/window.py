@@ -261,6 +261,7 @@ class RingWindowSource:
         self.n = 0
         self.resubmitted = 0
         self.carried = 0   # records past a window's budget, summed over windows (should stay 0)
+        self.reap_s = self.submit_s = 0.0  # host time: waiting for / reading back finished windows, submitting
 
     def publish_epoch(self, now_ns: Optional[int] = None) -> int:
         v = self.clock.publish(int(now_ns if now_ns is not None else time.time_ns()))
@@ -331,6 +332,8 @@ class RingWindowSource:
         t0 = time.perf_counter()
         pipe = self.pipe
         self.reap(keep=pipe.nb - 1)
+        t1 = time.perf_counter()
+        self.reap_s += t1 - t0
         budget = pipe.sig_cap
         k_ranges, kern = [], []
         n_k = 0
@@ -368,7 +371,9 @@ class RingWindowSource:
             self.carried += max(0, cut.spans - self.spos) - n_s
             self.spos += n_s
         wl = labels is not None if with_labels is None else with_labels
+        t2 = time.perf_counter()
         k = pipe.submit(kern, user, spans, n_groups, labels, cut.bases, with_labels=wl, learn=learn)
+        self.submit_s += time.perf_counter() - t2
         self.pending.append([k, k_ranges, n_u, n_s, False])
         self.host_s += time.perf_counter() - t0
         self.n += 1
