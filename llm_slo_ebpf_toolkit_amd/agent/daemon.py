@@ -168,6 +168,8 @@ class AgentOptions:
     slo_target: float = 0.99             # TTFT SLO objective (burn rate = breach fraction / (1 - target))
     otlp_receiver_bind: str = ""         # OTLP/HTTP /v1/traces receiver feeding the span ring ("" = off)
     halo_ms: float = 2000.0              # carry records this close to a window's end into the next window
+    state_dir: str = ""                  # checkpoint of the learned state ("" = none; resumed on start)
+    checkpoint_every: int = 60           # windows between checkpoints
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -384,6 +386,12 @@ class Agent:
             return bpf.EmulatedMaps(ring), ring, user, spans, bpf.pod_metadata(kw)
         raise ValueError(f"unknown window source {o.source!r} (bpf | shm | replay)")
 
+    def _checkpoint(self, pipe, path: str) -> None:
+        try:
+            pipe.save_checkpoint(path, {"agent_windows": self.windows_done, "node": self.o.node})
+        except OSError as exc:
+            print(f"checkpoint {path} failed: {exc}", file=sys.stderr)
+
     def _scan_pods(self, maps) -> None:
         """kubepods cgroups -> the probes' cgroup -> pod id map (pod ids from the interner the
         OTLP receiver maps ``k8s.pod.uid`` through, so spans and kernel records agree)."""
@@ -471,6 +479,15 @@ class Agent:
                               window_ms=2000.0, user_cap=max(1024, o.window_events // 4), ttft_slo_ms=o.ttft_slo_ms,
                               halo_ms=o.halo_ms, import_cap=icap, xchg_cap=xchg)
         src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
+        ckpt = os.path.join(o.state_dir, f"agent-{o.node}-gpu{o.device}.safetensors") if o.state_dir else ""
+        if ckpt and os.path.exists(ckpt):
+            try:
+                meta = pipe.load_checkpoint(ckpt)
+                self.windows_done = int(meta.get("agent_windows", 0))
+                print(f"resumed learned state from {ckpt} ({meta.get('windows_folded_device', 0)} windows folded)",
+                      file=sys.stderr)
+            except (ValueError, OSError, KeyError) as exc:
+                print(f"checkpoint {ckpt} not usable ({exc}); starting fresh", file=sys.stderr)
         if pods is not None:
             pipe.eng.set_pods(*pods)
         if o.source == "bpf":
@@ -506,6 +523,8 @@ class Agent:
             pending = (k, cut.t_ns, G, names, ring, host_us)
             if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
                 self._scan_pods(maps)  # pod churn
+            if ckpt and o.checkpoint_every > 0 and self.windows_done % o.checkpoint_every == 0:
+                self._checkpoint(pipe, ckpt)
             self._guard_tick()
             self.metrics.set_heartbeat()
             self.windows_done += 1
@@ -518,6 +537,8 @@ class Agent:
                 self._emit_window(pipe, *pending)
             src.drain()
             self.last_summary = pipe.summary()
+            if ckpt:
+                self._checkpoint(pipe, ckpt)
         finally:
             # unregister the rings from the GPU and free device memory while the ring mappings
             # still exist (interpreter teardown order is arbitrary)

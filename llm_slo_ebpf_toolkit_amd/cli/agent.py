@@ -62,6 +62,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),
         ("otlp-receiver-bind", d.otlp_receiver_bind, "OTLP/HTTP /v1/traces receiver feeding the span ring (gpu engine)"),
         ("halo-ms", d.halo_ms, "gpu engine: records this close to a window's end also join the next window (0 = off)"),
+        ("state-dir", d.state_dir, "gpu engine: checkpoint directory for the learned state (resumed on start)"),
+        ("checkpoint-every", d.checkpoint_every, "gpu engine: windows between checkpoints"),
     ]:
         p.flag(name, default, help_)
     a = p.parse_args(argv)
@@ -78,7 +80,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
-        otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms))
+        otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
+        checkpoint_every=int(a.checkpoint_every))
     return o, a.probe_smoke
 
 

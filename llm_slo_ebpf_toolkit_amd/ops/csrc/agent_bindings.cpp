@@ -203,6 +203,11 @@ class PyEngine {
     }
     return copy_array(t.data(), {kStatsLen});
   }
+  void restore(py::array_t<double, py::array::c_style | py::array::forcecast> stats,
+               py::array_t<uint8_t, py::array::c_style | py::array::forcecast> model, int64_t folded) {
+    if (stats.size() != kStatsLen) throw std::invalid_argument("stats must be f64[STATS_LEN]");
+    eng().restore(stats.data(), model.data(), (size_t)model.size(), folded);
+  }
   py::array_t<uint8_t> model_bytes() {
     std::vector<uint8_t> t(sizeof(PosteriorModel));
     {
@@ -290,6 +295,10 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("packet", &PyEngine::packet)
       .def("results", &PyEngine::results)
       .def("window_ms", &PyEngine::window_ms)
+      .def("copy_ms", [](PyEngine& p, int64_t k) {
+        py::gil_scoped_release nogil;
+        return p.eng().copy_ms(k);
+      })
       .def("set_model_bytes", &PyEngine::set_model_bytes)
       .def("set_p0", &PyEngine::set_p0)
       .def("set_pods", &PyEngine::set_pods)
@@ -301,6 +310,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("reset_totals", &PyEngine::reset_totals)
       .def("stats_acc", &PyEngine::stats_acc)
       .def("model_bytes", &PyEngine::model_bytes)
+      .def("restore", &PyEngine::restore)
       .def("sync", &PyEngine::sync)
       .def("import_state", &PyEngine::import_state)
       .def("close", &PyEngine::close)

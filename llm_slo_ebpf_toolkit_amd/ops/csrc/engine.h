@@ -123,6 +123,7 @@ class WindowEngine {
   ResultView results(int64_t k) const;
   // device time of window k (ms): DMA start -> results in host memory, and the compute stream's share
   std::pair<float, float> window_ms(int64_t k);
+  std::vector<float> copy_ms(int64_t k);  // window k's DMA time and the copy stream's idle gap before it
 
   void set_model_bytes(const void* bytes, size_t n);  // stream-ordered before the next window
   void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
@@ -145,6 +146,9 @@ class WindowEngine {
   void totals(double* out);           // accumulated (all-reduced) packets (synchronous)
   void reset_totals();
   void stats_acc(double* out);        // the device refit's accumulated statistics (synchronous)
+  // restore a checkpoint: accumulated statistics, the model image (model_bytes = 0: refit it
+  // on the device from the statistics) and the folded-window count
+  void restore(const double* stats, const void* model, size_t model_bytes, int64_t folded);
   void model_bytes(void* out);        // the model currently on the device (synchronous)
   void sync();
   // device-side import state (synchronous; diagnostics and tests): rows[0..1], tmax, and per
@@ -190,6 +194,7 @@ class WindowEngine {
   uint8_t *xsend_ = nullptr, *xrecv_ = nullptr;
   size_t xstride_ = 0, xrecv_bytes_ = 0;
   int nblk_imp_ = 0;                    // decode blocks of the other GPUs' rows
+  bool spin_ = false;
   std::vector<uint8_t> inject_;         // exchange blocks for the next window (inject_remote)
   size_t inject_stride_ = 0;
   int inject_world_ = 0, inject_me_ = 0;
@@ -238,7 +243,7 @@ class WindowEngine {
   uint32_t* evbits_ = nullptr;
   // events
   std::vector<hipEvent_t> h2d_done_, h2d_part_, compute_done_, comm_done_;
-  std::vector<hipEvent_t> t_start_, t_comp0_, t_comp1_, t_end_;
+  std::vector<hipEvent_t> t_start_, t_copy_end_, t_comp0_, t_comp1_, t_end_;
   std::map<std::tuple<int, int, bool, bool>, hipGraphExec_t> graphs_;
   std::vector<bool> warm_;
   std::vector<hipGraph_t> graph_defs_;

@@ -165,10 +165,15 @@ void WindowEngine::alloc() {
   nblk_sig_ = decode_grid((int)N);
   nblk_span_ = decode_grid((int)S);
   HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  {  // diagnostic knob: MISLO_COPY_STREAMS=1 puts the whole window's DMA on one stream
+  {  // MISLO_SPIN_WAIT=1: wait() polls its event instead of sleeping on it
+    const char* v = getenv("MISLO_SPIN_WAIT");
+    spin_ = v && atoi(v) == 1;
+  }
+  {  // MISLO_COPY_STREAMS=2 splits a window's DMA over two streams (measured slower: the
+     // second stream's large copy blocks the issuing thread ~0.2 ms per window)
     const char* v = getenv("MISLO_COPY_STREAMS");
-    if (v && atoi(v) == 1) copy2_ = copy_;
-    else HIPCHECK(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking));
+    if (v && atoi(v) == 2) HIPCHECK(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking));
+    else copy2_ = copy_;
   }
   HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   HIPCHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
@@ -192,6 +197,7 @@ void WindowEngine::alloc() {
     compute_done_.push_back(mk_event(false));
     comm_done_.push_back(mk_event(false));
     t_start_.push_back(mk_event(true));
+    t_copy_end_.push_back(mk_event(true));
     t_comp0_.push_back(mk_event(true));
     t_comp1_.push_back(mk_event(true));
     t_end_.push_back(mk_event(true));
@@ -294,7 +300,7 @@ WindowEngine::~WindowEngine() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   for (auto g : graph_defs_) hipGraphDestroy(g);
   if (comm_) ncclCommDestroy(comm_);
-  auto evs = {&h2d_done_, &h2d_part_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
+  auto evs = {&t_copy_end_, &h2d_done_, &h2d_part_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
   for (auto* v : evs)
     for (auto e : *v) hipEventDestroy(e);
   for (auto& r : registered_) hipHostUnregister(const_cast<uint8_t*>(r.first));
@@ -560,10 +566,9 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   c[15] = (int32_t)n_k;
   int32_t* lab = reinterpret_cast<int32_t*>(head_host_[b] + kHeadBytes);
   for (int g = 0; g < cfg_.group_cap; ++g) lab[g] = (in.labels && g < n_groups) ? in.labels[g] : -1;
-  // DMAs once window k - nb (the device block's previous reader) computed, on two copy
-  // streams: the BPF ring's bytes on one, the head, user-space records and spans on the other.
-  // Back to back on one stream, the second SDMA transfer of a window started hundreds of us
-  // after the first ended whenever kernels were running (rocprofv3 memory-copy trace).
+  // DMAs once window k - nb (the device block's previous reader) computed: the head, the BPF
+  // ring's bytes, the user-space records and the spans, back to back on the copy stream (or
+  // over two streams with MISLO_COPY_STREAMS=2).
   HIPCHECK(hipStreamWaitEvent(copy_, compute_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(copy2_, compute_done_[b], 0));
   HIPCHECK(hipEventRecord(t_start_[b], copy_));
@@ -588,6 +593,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   lap(tq, split_us_[3]);
   HIPCHECK(hipEventRecord(h2d_part_[b], copy2_));
   HIPCHECK(hipEventRecord(h2d_done_[b], copy_));
+  HIPCHECK(hipEventRecord(t_copy_end_[b], copy2_));
   const auto te = std::chrono::steady_clock::now();
   dma_us_ += std::chrono::duration<double, std::micro>(te - td).count();
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
@@ -667,7 +673,16 @@ bool WindowEngine::query(int64_t k) {
   return false;
 }
 
-void WindowEngine::wait(int64_t k) { HIPCHECK(hipEventSynchronize(comm_done_[k % nb_])); }
+void WindowEngine::wait(int64_t k) {
+  if (spin_) {  // poll: no interrupt wake-up latency (flat-out benchmarking; costs a core)
+    for (;;) {
+      const hipError_t e = hipEventQuery(comm_done_[k % nb_]);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIPCHECK(e);
+    }
+  }
+  HIPCHECK(hipEventSynchronize(comm_done_[k % nb_]));
+}
 
 ResultView WindowEngine::results(int64_t k) const {
   const uint8_t* r = res_host_[k % nb_];
@@ -677,6 +692,16 @@ ResultView WindowEngine::results(int64_t k) const {
   return ResultView{reinterpret_cast<const double*>(r), reinterpret_cast<const double*>(r + o_gconf),
                     reinterpret_cast<const float*>(r + o_feat), reinterpret_cast<const int32_t*>(r + o_pred),
                     reinterpret_cast<const uint32_t*>(r + o_ev), reinterpret_cast<const uint32_t*>(r + o_sli)};
+}
+
+std::vector<float> WindowEngine::copy_ms(int64_t k) {
+  // [copy duration of window k, copy-engine idle time between window k-1's DMAs and k's]
+  const int b = (int)(k % nb_);
+  float dur = 0.f, gap = -1.f;
+  HIPCHECK(hipEventSynchronize(t_copy_end_[b]));
+  HIPCHECK(hipEventElapsedTime(&dur, t_start_[b], t_copy_end_[b]));
+  if (k >= 1 && nb_ > 1) HIPCHECK(hipEventElapsedTime(&gap, t_copy_end_[(k - 1) % nb_], t_start_[b]));
+  return {dur, gap};
 }
 
 std::pair<float, float> WindowEngine::window_ms(int64_t k) {
@@ -780,6 +805,20 @@ void WindowEngine::reset_totals() {
 void WindowEngine::stats_acc(double* out) {
   sync();
   HIPCHECK(hipMemcpy(out, stats_acc_, kStatsLen * sizeof(double), hipMemcpyDeviceToHost));
+}
+
+void WindowEngine::restore(const double* stats, const void* model, size_t n, int64_t folded) {
+  if (n && n != sizeof(PosteriorModel)) throw std::invalid_argument("model image must be POSTERIOR_MODEL_BYTES bytes");
+  sync();
+  HIPCHECK(hipMemcpy(stats_acc_, stats, kStatsLen * sizeof(double), hipMemcpyHostToDevice));
+  if (n) {
+    HIPCHECK(hipMemcpy(model_dev_, model, n, hipMemcpyHostToDevice));
+  } else {  // the learned model from the restored statistics, by the device refit itself
+    launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
+                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_);
+    HIPCHECK(hipStreamSynchronize(compute_));
+  }
+  folded_ = folded;
 }
 
 void WindowEngine::model_bytes(void* out) {

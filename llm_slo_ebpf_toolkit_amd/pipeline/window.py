@@ -26,7 +26,7 @@ from __future__ import annotations
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -194,6 +194,62 @@ class WindowPipeline:
 
     def summary(self) -> Dict[str, object]:
         return summarize(self.eng.totals())
+
+    # ---- checkpoint / resume (utils/checkpoint.py) ------------------------------------------
+    def state(self) -> Tuple[Dict[str, np.ndarray], Dict[str, object]]:
+        """Everything the learned model depends on (arrays, metadata); drains the engine. The
+        device refit runs nb windows behind: the statistics of the windows it has not folded
+        yet (their all-reduced packets) are added, so the checkpoint holds every finished
+        window (the restored engine refits from them)."""
+        self.drain()
+        c = self.cum_stats
+        stats = np.asarray(self.eng.stats_acc(), dtype=np.float64).copy()
+        off, n = int(self.mod.STATS_OFF), int(self.mod.STATS_LEN)
+        pending = range(max(0, self.k - self.nb), self.k) if self.device_refit else range(0)
+        for j in pending:
+            stats += np.asarray(self.eng.packet(j), dtype=np.float64)[off:off + n]
+        arrays = {"stats_acc": stats,
+                  "model": np.asarray(self.eng.model_bytes(), dtype=np.uint8),
+                  "host_count": c.count, "host_elevated_sum": c.elevated_sum, "host_x_sum": c.x_sum,
+                  "host_xx": c.xx}
+        meta = {"model": self.model_name, "seed": self.seed, "learn": self.learn, "windows": self.k,
+                "windows_folded_device": int(self.eng.windows_folded) + len(pending),
+                "windows_folded_host": self.windows_folded_host, "n_domains": N_DOMAINS}
+        return arrays, meta
+
+    def restore(self, arrays: Dict[str, np.ndarray], meta: Dict[str, object]) -> None:
+        """Resume from ``state()``: the same model family is required; statistics, the model on
+        the device and the fold counters continue where the checkpoint left them."""
+        if meta.get("model") != self.model_name or int(meta.get("n_domains", N_DOMAINS)) != N_DOMAINS:
+            raise ValueError(f"checkpoint of model {meta.get('model')!r} cannot resume {self.model_name!r}")
+        # the learned Bayes is refit on the device from the statistics; other models keep the image
+        model = np.zeros(0, np.uint8) if self.device_refit else np.asarray(arrays["model"], dtype=np.uint8)
+        self.eng.restore(np.asarray(arrays["stats_acc"], dtype=np.float64), model,
+                         int(meta.get("windows_folded_device", 0)))
+        self.cum_stats = SufficientStats(count=np.array(arrays["host_count"], dtype=np.float64),
+                                         elevated_sum=np.array(arrays["host_elevated_sum"], dtype=np.float64),
+                                         x_sum=np.array(arrays["host_x_sum"], dtype=np.float64),
+                                         xx=np.array(arrays["host_xx"], dtype=np.float64))
+        self.windows_folded_host = int(meta.get("windows_folded_host", 0))
+        if not self.device_refit and self.learn and self.cum_stats.count.sum() > 0:
+            if self.model_name == "lda" and self.cum_stats.count.sum() > 32:
+                self.model = LDA.fit(self.cum_stats)
+            else:
+                self.model = NaiveBayes.learned(self.cum_stats, seed=self.seed)
+
+    def save_checkpoint(self, path: str, extra_meta: Optional[Dict[str, object]] = None) -> None:
+        from ..utils import checkpoint
+
+        arrays, meta = self.state()
+        meta.update(extra_meta or {})
+        checkpoint.save(path, arrays, meta)
+
+    def load_checkpoint(self, path: str) -> Dict[str, object]:
+        from ..utils import checkpoint
+
+        arrays, meta = checkpoint.load(path)
+        self.restore(arrays, meta)
+        return meta
 
     def host_model(self):
         """The model currently on the device, as a host LinearPosteriorModel (reporting)."""

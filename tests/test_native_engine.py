@@ -230,3 +230,50 @@ def test_halo_and_remote_rows_join_like_the_oracle():
     assert n_imported[0] == 0 and n_imported[1] > 0 and n_imported[2] > n_imported[1] - 1
     src.drain()
     pipe.eng.close()
+
+
+def test_checkpoint_resume_restores_every_finished_window(tmp_path):
+    """Checkpoint / resume: after 6 learned windows (the device refit folds nb behind), the
+    checkpoint holds the statistics of all 6; a fresh pipeline restored from it refits on the
+    device and scores the next window with exactly that model (= NaiveBayes.learned of the
+    same statistics), and the fold counter continues."""
+    from llm_slo_ebpf_toolkit_amd.models.bayes import SufficientStats
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+
+    wins, gen = windows(n_win=4, seed=47)
+    imgs = build_replay_images(wins)
+    pods = pod_meta(gen)
+
+    def make(tag):
+        pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", user_cap=4096)
+        rb, user, spans = rings(tag)
+        src = RingWindowSource(pipe, rb, user, spans)
+        pipe.eng.set_pods(*pods)
+        return pipe, src, (rb, user, spans)
+
+    a, src_a, ra = make("ckpt-a")
+    total = np.zeros(int(a.mod.STATS_LEN))
+    for i in range(6):
+        img = imgs[i % 3]
+        k = src_a.stage(feed(img, ra[0], ra[1], ra[2]), img.n_groups, img.labels)["k"]
+        a.wait(k)
+        total += a.eng.packet(k)[int(a.mod.STATS_OFF):int(a.mod.STATS_OFF) + int(a.mod.STATS_LEN)]
+    src_a.drain()
+    path = str(tmp_path / "state.safetensors")
+    a.save_checkpoint(path, {"agent_windows": 6})
+    b, src_b, rb_ = make("ckpt-b")
+    meta = b.load_checkpoint(path)
+    assert meta["agent_windows"] == 6 and meta["windows_folded_device"] == 6
+    np.testing.assert_allclose(b.eng.stats_acc(), total, rtol=1e-12, atol=1e-9)
+    img = imgs[3]
+    kb = src_b.stage(feed(img, rb_[0], rb_[1], rb_[2]), img.n_groups, img.labels, learn=False)["k"]
+    res = b.results(kb, img.n_groups)
+    s = SufficientStats(count=total[1024:1024 + 10].copy(), elevated_sum=total[:1024].reshape(32, 32)[:16, :10].copy(),
+                        x_sum=total[:1024].reshape(32, 32)[16:, :10].copy(), xx=total[:1024].reshape(32, 32)[16:, 16:].copy())
+    model = NaiveBayes.learned(s, seed=42)
+    np.testing.assert_allclose(res["post"][:, :10], model.posteriors(res["feat"].astype(np.float64)), rtol=1e-9,
+                               atol=1e-12)
+    src_b.drain()
+    assert b.windows_folded == 6
+    a.eng.close()
+    b.eng.close()
