@@ -13,6 +13,20 @@ test:             ## CPU test suite (no GPU needed)
 test-gpu:         ## GPU tests (MI355X)
 	$(PY) -m pytest tests -q -m gpu
 
+RT := llm_slo_ebpf_toolkit_amd/runtime/csrc
+RT_STRESS := tests/native/ring_stress.cpp $(RT)/ring.cpp $(RT)/bpfring.cpp $(RT)/pool.cpp
+
+sanitize-asan:    ## host ring code under AddressSanitizer + UBSan (multi-producer stress)
+	@mkdir -p build
+	g++ -std=c++17 -O1 -g -pthread -fsanitize=address,undefined -fno-omit-frame-pointer -I$(RT) $(RT_STRESS) \
+	    -o build/ring_stress_asan -lrt
+	build/ring_stress_asan
+
+sanitize-tsan:    ## host ring code under ThreadSanitizer (multi-producer stress)
+	@mkdir -p build
+	g++ -std=c++17 -O1 -g -pthread -fsanitize=thread -I$(RT) $(RT_STRESS) -o build/ring_stress_tsan -lrt
+	build/ring_stress_tsan
+
 lint:
 	$(PY) -m compileall -q llm_slo_ebpf_toolkit_amd tests tools
 
