@@ -7,7 +7,9 @@
 //
 //   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue            (ns)
 //   type 14 hbm_pressure_pct     live device allocations / HBM capacity     (milli-pct)
-//   type 15 xgmi_link_latency_us device<->device copy duration               (ns)
+//   type 15 xgmi_link_latency_us peer GPU copy time beyond its bytes at the
+//                                link's nominal rate (the latency component,
+//                                not a size-dependent duration)             (ns)
 //   type 16 rccl_collective_ms   RCCL API call duration                      (ns)
 //
 // Timestamps are rocprofiler's monotonic clock, shifted to CLOCK_REALTIME once at init
@@ -18,7 +20,8 @@
 //
 // Environment: MISLO_RING (default /mislo-agent-events), MISLO_POD_ID, MISLO_NODE_ID,
 // MISLO_SVC_ID, MISLO_HBM_BYTES (default 288 GiB), MISLO_MAX_EPS (default 200000),
-// MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_ROCPROF_VERBOSE.
+// MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_XGMI_GBPS (nominal peer-copy rate, default
+// 64 GB/s: one xGMI link direction), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/buffer_tracing.h>
 #include <rocprofiler-sdk/callback_tracing.h>
@@ -70,6 +73,7 @@ struct State {
   uint64_t hbm_bytes = 288ull << 30;
   uint64_t max_eps = 200000;
   uint64_t queue_floor_ns = 100000;
+  double xgmi_bytes_per_ns = 64.0;
   bool verbose = false;
   std::mutex mu;
   std::unordered_map<uint64_t, uint64_t> enqueue_ts;  // correlation id -> enqueue time
@@ -160,8 +164,13 @@ void buffer_callback(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofi
     if (h->kind == ROCPROFILER_BUFFER_TRACING_MEMORY_COPY) {
       auto* r = static_cast<rocprofiler_buffer_tracing_memory_copy_record_t*>(h->payload);
       if (r->operation == ROCPROFILER_MEMORY_COPY_DEVICE_TO_DEVICE && r->src_agent_id.handle != r->dst_agent_id.handle &&
-          r->end_timestamp > r->start_timestamp)
-        emit(kXgmiLatency, r->start_timestamp, r->end_timestamp - r->start_timestamp, (uint32_t)r->thread_id);
+          r->end_timestamp > r->start_timestamp) {
+        // latency = duration - bytes / nominal link rate: a healthy link moves a large copy
+        // in ~its transfer time (latency ~ setup cost), a degraded or congested link does not
+        const uint64_t dur = r->end_timestamp - r->start_timestamp;
+        const uint64_t xfer = (uint64_t)((double)r->bytes / g.xgmi_bytes_per_ns);
+        emit(kXgmiLatency, r->start_timestamp, dur > xfer ? dur - xfer : 0, (uint32_t)r->thread_id);
+      }
     } else if (h->kind == ROCPROFILER_BUFFER_TRACING_MEMORY_ALLOCATION) {
       auto* r = static_cast<rocprofiler_buffer_tracing_memory_allocation_record_t*>(h->payload);
       std::lock_guard<std::mutex> lk(g.mu);
@@ -206,6 +215,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.hbm_bytes = env_u64("MISLO_HBM_BYTES", 288ull << 30);
   g.max_eps = env_u64("MISLO_MAX_EPS", 200000);
   g.queue_floor_ns = env_u64("MISLO_QUEUE_FLOOR_NS", 100000);
+  g.xgmi_bytes_per_ns = (double)env_u64("MISLO_XGMI_GBPS", 64);  // GB/s == bytes/ns
   g.verbose = env_u64("MISLO_ROCPROF_VERBOSE", 0) != 0;
   timespec rt{};
   clock_gettime(CLOCK_REALTIME, &rt);

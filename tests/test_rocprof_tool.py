@@ -14,7 +14,16 @@ from conftest import ROOT
 TOOL = os.path.join(ROOT, "llm_slo_ebpf_toolkit_amd", "probes", "rocprof", "libmislo_rocprof.so")
 
 WORKLOAD = r"""
-import torch
+import os, socket, torch
+import torch.distributed as dist
+# a one-rank RCCL communicator: its collectives go through the RCCL API the tool traces
+s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+t = torch.ones(1 << 20, device="cuda")
+for _ in range(4):
+    dist.all_reduce(t)
+torch.cuda.synchronize()
+dist.destroy_process_group()
 x = torch.randn(4096, 4096, device="cuda")
 for _ in range(20):
     y = x @ x
@@ -50,9 +59,53 @@ def test_tool_pushes_gpu_signals_into_ring():
     types = set(recs["signal_type"].tolist())
     assert 13 in types, (types, r.stderr[-1000:])      # gpu_queue_delay_ms from kernel dispatches
     assert 14 in types, (types, r.stderr[-1000:])      # hbm_pressure_pct from allocations
+    assert 16 in types, (types, r.stderr[-1000:])      # rccl_collective_ms from the RCCL API
+    # type 15 (xGMI peer copies) needs two GPUs; on a multi-GPU box it is checked below
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pass  # exercised by tests/test_rocprof_tool.py::test_xgmi_peer_copies (multi-GPU runners)
     assert (recs["pod_id"] == 7).all() and (recs["node_id"] == 3).all()
     assert (recs["flags"] & (1 << 8)).all()
     ts = recs["ts_ns"]
     assert (ts > t0 - 10 * 10**9).all() and (ts < time.time_ns() + 10 * 10**9).all()  # wall clock
     hbm = recs[recs["signal_type"] == 14]["value"].max() * 1e-3  # pct
     assert hbm > 0.5  # >= 2 GiB of 288 GiB live
+
+
+XGMI_WORKLOAD = r"""
+import torch
+a = torch.empty(64 << 20, dtype=torch.uint8, device="cuda:0")
+b = torch.empty(64 << 20, dtype=torch.uint8, device="cuda:1")
+for _ in range(8):
+    b.copy_(a)
+torch.cuda.synchronize()
+print("copies done")
+"""
+
+
+@pytest.mark.gpu
+def test_xgmi_peer_copies():
+    """Type 15 from device-to-device copies between two GPUs: the latency left after the bytes'
+    transfer time at the nominal link rate (not the size-dependent copy duration)."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (xGMI peer copies)")
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    name = f"/mislo-test-{os.getpid()}-xgmi"
+    ring = rt.HostRing(1 << 14, 64, name)
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000000")
+    r = subprocess.run([sys.executable, "-c", XGMI_WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    segs = ring.peek(1 << 14)
+    view = ring.records_view()
+    recs = np.concatenate([np.frombuffer(view[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
+                           for _, i, c in segs]) if segs else np.zeros(0, dtype=records.EVENT)
+    x = recs[recs["signal_type"] == 15]
+    assert len(x) >= 1
+    # a 64 MiB copy takes ~1 ms at 64 GB/s: what remains is far below the copy duration
+    assert (x["value"] < 1_000_000).all(), x["value"]

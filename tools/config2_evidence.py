@@ -1,0 +1,194 @@
+"""Config-2 evidence on one MI355X (REF demo/llama-cpp/k8s/deployment.yaml:29-63 +
+scripts/chaos/run_fault_matrix.sh:46-94; VERDICT r1 "do this" #7).
+
+On one GPU, in one run:
+
+* the LLM workload: the demo RAG service with the Llama backend (models/llama.py, bf16) and the
+  rocprofiler-sdk tool (libmislo_rocprof.so) loaded into it. The tool's GPU signals go to the
+  agent's user-space ring; the service's request spans go over OTLP/HTTP to the agent;
+* the agent: ``--engine gpu`` on the same GPU, joining the tool's signals with the spans;
+* a baseline phase, then a fault phase. In the fault phase a GPU burner process (back-to-back
+  large GEMMs on the same GPU) contends with the LLM, then the fault is lifted;
+* out: per-phase TTFT (p50 / p95, from the service's own responses) and the agent's
+  IncidentAttributions for the service, with the fault phase's predicted domain and evidence.
+
+    python tools/config2_evidence.py --out gpurun_out/config2
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+TOOL = os.path.join(ROOT, "llm_slo_ebpf_toolkit_amd", "probes", "rocprof", "libmislo_rocprof.so")
+POD_UID = "c0nf1g2-0000-4000-8000-000000000001"
+
+BURNER = r"""
+import sys, time, torch
+a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+b = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+end = time.time() + float(sys.argv[1])
+print("burner on", flush=True)
+while time.time() < end:
+    for _ in range(8):
+        a = (a @ b).clamp_(-1, 1)
+    torch.cuda.synchronize()
+print("burner off", flush=True)
+"""
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def wait_http(url: str, proc, timeout: float) -> None:
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if proc.poll() is not None:
+            raise RuntimeError(f"{url}: process exited with {proc.returncode}")
+        try:
+            if urllib.request.urlopen(url, timeout=1).status == 200:
+                return
+        except OSError:
+            pass
+        time.sleep(0.5)
+    raise RuntimeError(f"{url} not ready after {timeout}s")
+
+
+def chat(port: int, i: int, phase: str) -> dict:
+    body = json.dumps({"prompt": f"why did the {phase} request {i} slow down on the gpu", "profile": "chat_short",
+                       "max_tokens": 16, "request_id": f"{phase}-{i}"}).encode()
+    req = urllib.request.Request(f"http://127.0.0.1:{port}/chat", data=body, method="POST",
+                                 headers={"Content-Type": "application/json"})
+    t = time.time_ns()
+    out = json.loads(urllib.request.urlopen(req, timeout=120).read())
+    return {"phase": phase, "t_ns": t, "ttft_ms": out["ttft_ms"], "trace_id": out["trace_id"]}
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))] if xs else None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/config2")
+    ap.add_argument("--requests", type=int, default=24, help="requests per phase")
+    ap.add_argument("--preset", default="1b")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    from llm_slo_ebpf_toolkit_amd.collector import bpf
+
+    prefix = f"/mislo-cfg2-{os.getpid()}"
+    names = bpf.RingNames.of(prefix)
+    rings = bpf.create_rings(names, 1 << 24, 1 << 18, 1 << 14)  # noqa: F841 - kept alive for the children
+    rx, mport, hport = free_port(), free_port(), free_port()
+    attr_path = os.path.join(a.out, "attributions.jsonl")
+    log = open(os.path.join(a.out, "run.log"), "w")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
+    agent = subprocess.Popen(
+        [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "shm",
+         "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
+         "--window-ms", "1000", "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
+         "--model", "bayes", "--min-confidence", "0.3", "--halo-ms", "0", "--output", "jsonl",
+         "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
+    llm_env = dict(env, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1",
+                   MISLO_QUEUE_FLOOR_NS="200000", OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces",
+                   POD_UID=POD_UID, POD_NAME="llm-server-config2")
+    llm = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.rag_service", "--backend", "llama",
+                            "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", ""],
+                           cwd=ROOT, env=llm_env, stdout=log, stderr=subprocess.STDOUT)
+    burner = None
+    rows = []
+    try:
+        wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 180)
+        wait_http(f"http://127.0.0.1:{hport}/healthz", llm, 300)
+        print("[config2] agent and llm ready", flush=True)
+        for i in range(4):  # warm the model (first-request compilation / allocation)
+            chat(hport, i, "warmup")
+        phases = [("baseline", False), ("fault_gpu_contention", True), ("recovery", False)]
+        for phase, fault in phases:
+            if fault:
+                burner = subprocess.Popen([sys.executable, "-c", BURNER, "600"], cwd=ROOT, env=env, stdout=log,
+                                          stderr=subprocess.STDOUT)
+                time.sleep(3.0)
+            t_phase = time.time_ns()
+            for i in range(a.requests):
+                rows.append(chat(hport, i, phase))
+                time.sleep(0.1)
+            if burner is not None:
+                burner.send_signal(signal.SIGTERM)
+                burner.wait(30)
+                burner = None
+            rs = [r["ttft_ms"] for r in rows if r["phase"] == phase]
+            print(f"[config2] {phase}: {len(rs)} requests, TTFT p50 {pct(rs, .5):.1f} ms p95 {pct(rs, .95):.1f} ms "
+                  f"(from {t_phase})", flush=True)
+            time.sleep(2.5)  # let the phase's last window close
+    finally:
+        for p in (burner, llm):
+            if p is not None and p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+                try:
+                    p.wait(30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+        if agent.poll() is None:
+            agent.send_signal(signal.SIGTERM)
+            try:
+                agent.wait(60)
+            except subprocess.TimeoutExpired:
+                agent.kill()
+        log.close()
+    with open(os.path.join(a.out, "ttft.jsonl"), "w") as f:
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
+    attrs = [json.loads(x) for x in open(attr_path)] if os.path.exists(attr_path) else []
+    mine = [x for x in attrs if x["service"] == "rag-service"]
+
+    def phase_of(ts_iso_ns: int) -> str:
+        best = "other"
+        for r in rows:
+            if r["t_ns"] <= ts_iso_ns:
+                best = r["phase"]
+        return best
+
+    by_phase = {}
+    for x in mine:
+        t = int(x["incident_id"].split("-")[1])
+        p = phase_of(t)
+        d = by_phase.setdefault(p, {"windows": 0, "domains": {}, "evidence": []})
+        d["windows"] += 1
+        d["domains"][x["predicted_fault_domain"]] = d["domains"].get(x["predicted_fault_domain"], 0) + 1
+        if x["predicted_fault_domain"] != "unknown":
+            d["evidence"].append({"domain": x["predicted_fault_domain"], "confidence": round(x["confidence"], 3),
+                                  "evidence": x["evidence"], "burn_rate": x["slo_impact"]["burn_rate"]})
+    summary = {
+        "ttft_ms": {p: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
+                    for p in ("baseline", "fault_gpu_contention", "recovery")
+                    for v in [[r["ttft_ms"] for r in rows if r["phase"] == p]]},
+        "attributions_total": len(attrs),
+        "rag_service_by_phase": {p: {"windows": d["windows"], "domains": d["domains"], "evidence": d["evidence"][:3]}
+                                 for p, d in by_phase.items()},
+        "agent_exit": agent.returncode, "llm_exit": llm.returncode,
+    }
+    with open(os.path.join(a.out, "summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary, indent=1), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
