@@ -156,7 +156,7 @@ def build_runtime(force: bool = False, jobs: int = 4) -> List[str]:
     base = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-ffp-contract=off", f"-I{ROCM}/include",
             "-D__HIP_PLATFORM_AMD__=1"]
     outs = []
-    core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp")]
+    core = [os.path.join(RT_CSRC, s) for s in ("ring.cpp", "replay.cpp", "pool.cpp")]
     lib = os.path.join(rt_dir, "libmislo_rt.so")
     if force or _newer(lib, core + hdrs):
         _run([cxx, *base, "-shared", *core, "-o", lib])

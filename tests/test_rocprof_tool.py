@@ -38,6 +38,19 @@ def test_tool_library_built():
     assert os.path.exists(TOOL), "run python -m llm_slo_ebpf_toolkit_amd.ops.build"
 
 
+def test_runtime_c_abi_library_is_self_contained():
+    """libmislo_rt.so (the C ABI the tool library loads into GPU workloads) defines every
+    toolkit symbol it uses: an undefined one only fails at the first push, inside the workload."""
+    import shutil
+
+    if shutil.which("nm") is None:
+        pytest.skip("needs nm")
+    lib = os.path.join(ROOT, "llm_slo_ebpf_toolkit_amd", "runtime", "libmislo_rt.so")
+    out = subprocess.run(["nm", "-D", lib], capture_output=True, text=True, check=True).stdout
+    undefined = [ln.split()[-1] for ln in out.splitlines() if " U " in ln and "mislo" in ln]
+    assert not undefined, undefined
+
+
 @pytest.mark.gpu
 def test_tool_pushes_gpu_signals_into_ring():
     from llm_slo_ebpf_toolkit_amd.collector import records
