@@ -64,6 +64,8 @@ def parse():
                     help="carry rows within this distance of a window's latest record into the next window")
     ap.add_argument("--xchg-cap", type=int, default=-1,
                     help="warn-level trace-tagged rows each GPU exchanges per window over RCCL (-1: 65536 when N > 1)")
+    ap.add_argument("--user-rec", type=int, default=32, choices=(32, 64),
+                    help="user-space ring record size: 32 = USER32 (the rocprof tool's compact record), 64 = EVENT")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 
@@ -149,7 +151,7 @@ def main() -> int:
         hg = ReplayGenerator(hcfg)
         hg.window = 1000 + j  # later in time than the training windows
         held.append(hg.next_window())
-    images = build_replay_images(wins + held)
+    images = build_replay_images(wins + held, user_rec=a.user_rec)
     imgs, himgs = images[: len(wins)], images[len(wins):]
     pods = np.unique(np.concatenate([w.events["pod_id"] for w in wins + held]))
     pod_sn = {}
@@ -165,7 +167,7 @@ def main() -> int:
     names = {"ring": tag + "-ev", "user": tag + "-user", "spans": tag + "-sp", "cuts": tag + "-cut"}
     rb = rt.Ringbuf.create_shm(names["ring"], a.ring_mib << 20)
     user_cap = 1 << max(12, int(np.ceil(np.log2(max(1, len(imgs[0].user)) * 24))))
-    user = rt.HostRing(user_cap, 64, names["user"])
+    user = rt.HostRing(user_cap, a.user_rec, names["user"])
     spans = rt.HostRing(1 << max(12, int(np.ceil(np.log2(a.spans * 24)))), 64, names["spans"])
     cuts = rt.HostRing(1 << 12, 64, names["cuts"])
     n_flat = a.warmup + a.steps
@@ -374,6 +376,7 @@ def main() -> int:
             "source": "BPF ring buffer (kernel layout, emulated in shm) + rocprof/user-space ring + span ring",
             "wire_bytes_per_event": 16,
             "ring_bytes_per_kernel_event": 24,
+            "ring_bytes_per_user_record": a.user_rec,
             "device_buffers": a.buffers,
         },
         "macro_f1_heldout": heldout,

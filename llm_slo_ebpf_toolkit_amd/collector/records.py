@@ -123,6 +123,22 @@ DEF_TRACE, DEF_CTX, DEF_FIRST = 0xFD, 0xFE, 0xF0  # definition record types (low
 KERNEL_CTX_LIMIT = 1 << 23     # kernel context ids 1 .. 2^23 - 1, host ids above
 KERNEL_TRACE_LIMIT = 1 << 24   # kernel trace ids 1 .. 2^24 - 1, host ids above
 CTX_IDS = 1 << 24
+# 32-byte user-space record (probes/rocprof/mislo_rocprof.cpp, rings created with 32-byte
+# records): what the GPU join needs of a user-space producer's event -- no connection, the
+# value already in fixed point like the kernel's records, svc|node from the pod table. Half the
+# PCIe bytes of EVENT; the agent takes either, per ring.
+USER32 = np.dtype([
+    ("ts_ns", "<i8"),        # 0  CLOCK_REALTIME ns
+    ("trace_h", "<u8"),      # 8  trace hash (0 = none)
+    ("value_milli", "<u4"),  # 16 value in 1/1000 of the signal's output unit (milli_int)
+    ("pod_id", "<u4"),       # 20
+    ("pid", "<u4"),          # 24
+    ("signal_type", "u1"),   # 28
+    ("flags", "u1"),         # 29 bit 0: has_gpu
+    ("node_id", "<u2"),      # 30
+])
+assert USER32.itemsize == 32
+
 WIRE_DTYPES = {64: EVENT, 16: EVENT16}
 RB_BUSY, RB_DISCARD, RB_HDR = 1 << 31, 1 << 30, 8   # BPF ring buffer record header bits
 REC_STRIDE = RB_HDR + 16                          # ring bytes per 16-byte record
@@ -279,6 +295,21 @@ def milli_shift_table() -> np.ndarray:
                 raise ValueError(f"{s.name}: decode_scale {s.decode_scale} is not a power of ten")
             shift[s.kernel_type] = int(round(d))
     return shift
+
+
+def to_user32(events: np.ndarray) -> np.ndarray:
+    """64-byte EVENT records -> USER32 (mislo_rocprof.cpp emit with a 32-byte ring)."""
+    out = np.zeros(len(events), dtype=USER32)
+    st = events["signal_type"].astype(np.int64)
+    out["ts_ns"] = events["ts_ns"]
+    out["trace_h"] = events["trace_h"]
+    out["value_milli"] = milli_int(events["value"], milli_shift_table()[np.clip(st, 0, 255)])
+    out["pod_id"] = events["pod_id"]
+    out["pid"] = events["pid"]
+    out["signal_type"] = np.clip(st, 0, 255).astype(np.uint8)
+    out["flags"] = ((events["flags"] >> 8) & 1).astype(np.uint8)
+    out["node_id"] = events["node_id"]
+    return out
 
 
 def milli_int(raw: np.ndarray, shift: np.ndarray) -> np.ndarray:

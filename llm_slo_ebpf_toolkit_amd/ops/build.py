@@ -174,10 +174,11 @@ def build_rocprof_tool(force: bool = False) -> str:
     src = os.path.join(PKG, "probes", "rocprof", "mislo_rocprof.cpp")
     out = os.path.join(PKG, "probes", "rocprof", "libmislo_rocprof.so")
     rt_dir = os.path.join(PKG, "runtime")
-    if force or _newer(out, [src, os.path.join(rt_dir, "libmislo_rt.so")]):
+    if force or _newer(out, [src, os.path.join(rt_dir, "libmislo_rt.so"),
+                             os.path.join(PKG, "probes", "ebpf", "mislo_record.h")]):
         cxx = shutil.which("g++") or "c++"
         _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", f"-I{ROCM}/include",
-              "-D__HIP_PLATFORM_AMD__=1", src, "-o", out,
+              f"-I{os.path.join(PKG, 'probes', 'ebpf')}", "-D__HIP_PLATFORM_AMD__=1", src, "-o", out,
               f"-L{rt_dir}", "-lmislo_rt", "-Wl,-rpath,$ORIGIN/../../runtime", f"-L{ROCM}/lib", "-lrocprofiler-sdk",
               f"-Wl,-rpath,{ROCM}/lib"])
     return out

@@ -78,7 +78,7 @@ class PyEngine {
   void submit(int64_t k, const std::vector<std::pair<uintptr_t, size_t>>& kernel,
               const std::vector<std::pair<uintptr_t, size_t>>& user,
               const std::vector<std::pair<uintptr_t, size_t>>& spans, int n_groups, py::object labels,
-              std::vector<int64_t> bases, bool with_labels, bool learn) {
+              std::vector<int64_t> bases, bool with_labels, bool learn, int user_rec) {
     WindowInput in;
     auto conv = [](const std::vector<std::pair<uintptr_t, size_t>>& v, std::vector<Seg>& out) {
       for (auto& p : v) out.push_back(Seg{reinterpret_cast<const void*>(p.first), p.second});
@@ -87,6 +87,7 @@ class PyEngine {
     conv(user, in.user);
     conv(spans, in.spans);
     in.n_groups = n_groups;
+    in.user_rec = user_rec;
     std::vector<int32_t> lab;
     if (!labels.is_none()) {
       auto arr = labels.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
@@ -287,7 +288,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("register_host", &PyEngine::register_host)
       .def("submit", &PyEngine::submit, py::arg("k"), py::arg("kernel"), py::arg("user"), py::arg("spans"),
            py::arg("n_groups"), py::arg("labels") = py::none(), py::arg("bases") = std::vector<int64_t>{},
-           py::arg("with_labels") = true, py::arg("learn") = false)
+           py::arg("with_labels") = true, py::arg("learn") = false, py::arg("user_rec") = 64)
       .def("h2d_done", &PyEngine::h2d_done)
       .def("wait_h2d", &PyEngine::wait_h2d)
       .def("query", &PyEngine::query)

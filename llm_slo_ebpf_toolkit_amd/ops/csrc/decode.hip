@@ -365,7 +365,8 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
                                                       const SigRec* __restrict__ imp,
                                                       const uint4* __restrict__ ctx_tab, int n_ctx, TraceIds tt,
                                                       uint32_t* __restrict__ rs, unsigned long long* __restrict__ tmax,
-                                                      int seg, DecodeOut o) {
+                                                      const uint32_t* __restrict__ pod_sn, uint32_t n_pods, int seg,
+                                                      DecodeOut o) {
   __shared__ DecodeLds L;
   lds_init<NT>(L);
   const LdsLane l = lds_lane(L);
@@ -376,6 +377,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   const int n = seg ? max(r0, min(rows[1], cap)) : r0;
   const int n_loc = min(n_ptr[0], r0);
   const int n_k = min(n_ptr[15], n_loc);
+  const bool user32 = n_ptr[6] == 32;  // counts[6]: user-space record bytes (64 = EVENT, 32 = User32)
   const int valid_k = min((int)min((uint32_t)n_k, rs[kRsFirstBusy]), n_k);
   auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
   const int64_t t_base[4] = {base_at(4), base_at(8), base_at(10), base_at(12)};
@@ -412,6 +414,15 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         } else {  // a hole: never counted, never joined
           decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
         }
+      } else if (user32) {
+        const User32 e = reinterpret_cast<const User32*>(user)[i - n_k];
+        const int st = e.signal_type;
+        const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
+        const uint32_t sn = e.pod_id < n_pods ? pod_sn[e.pod_id] : 0u;
+        decode_one(i, cap, e.ts_ns, (float)((double)e.value_milli * 1e-3), slot, e.trace_h, e.pod_id, e.pid, sn, 0ull,
+                   o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+        if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
+        ++events;
       } else {
         const Event e = user[i - n_k];
         const int st = e.signal_type;
@@ -599,14 +610,14 @@ void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t
 
 void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, const int* rows, int cap,
                           const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
-                          uint32_t* ring_state, unsigned long long* tmax, const SignalCols& cols, uint32_t* hist,
-                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream,
-                          int seg, int grid, int blk_base) {
+                          uint32_t* ring_state, unsigned long long* tmax, const uint32_t* pod_sn, uint32_t n_pods,
+                          const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                          unsigned long long* misc, hipStream_t stream, int seg, int grid, int blk_base) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc, blk_base};
   constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_window<NT>), dim3(grid > 0 ? grid : decode_grid(cap)), dim3(NT), 0, stream, framed,
                      (const Event*)user, n_dev, rows, cap, imp, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, tt,
-                     ring_state, tmax, seg, o);
+                     ring_state, tmax, pod_sn, n_pods, seg, o);
 }
 
 }  // namespace mislo

@@ -92,7 +92,8 @@ struct ResultView {
 // The window's inputs: ring byte ranges (as the rings hold them) and the window metadata.
 struct WindowInput {
   std::vector<Seg> kernel;  // framed BPF ring records (24-byte stride), in ring order
-  std::vector<Seg> user;    // 64-byte EVENT records (user-space producers)
+  std::vector<Seg> user;    // user-space producers' records: 64-byte EVENT or 32-byte User32
+  int user_rec = 64;        // their size
   std::vector<Seg> spans;   // 64-byte SPAN records
   int n_groups = 0;
   const int32_t* labels = nullptr;  // [n_groups] ground-truth domain (replay / evaluation) or null

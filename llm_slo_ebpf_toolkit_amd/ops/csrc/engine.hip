@@ -437,7 +437,7 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
-                       ring_state_, tmax_, sig_cols(), hist_, status_, g_part_blk_, misc_, st);
+                       ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st);
   if (xchg)  // this window's warn-level trace-tagged rows, as the other GPUs will import them
     launch_select(g_rec_, g_status_, rows_, counts, N, kSelTrace, tmax_, 0, sel_cnt_, sel_off_, xsend_ + sizeof(XRec),
                   reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, true, st);
@@ -454,8 +454,8 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   if (xchg) {
     const TraceIds tt{trace_hash_, kTraceIdRows};
     launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
-                         ring_state_, tmax_, sig_cols(), hist_, status_, g_part_blk_, misc_, st, 1, nblk_imp_,
-                         nblk_sig_);
+                         ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st,
+                         1, nblk_imp_, nblk_sig_);
   }
   {  // this buffer's imports are consumed
     FillList z{};
@@ -536,8 +536,9 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   for (const Seg& s : in.user) ub += s.bytes;
   for (const Seg& s : in.spans) sb += s.bytes;
   // what the kernels will assume, checked on the host before anything is queued
-  if (kb % kRecStride || ub % 64 || sb % 64) throw std::invalid_argument("segments must hold whole records");
-  const size_t n_k = kb / kRecStride, n_u = ub / 64, n_s = sb / 64;
+  if (in.user_rec != 64 && in.user_rec != 32) throw std::invalid_argument("user records are 64 or 32 bytes");
+  if (kb % kRecStride || ub % in.user_rec || sb % 64) throw std::invalid_argument("segments must hold whole records");
+  const size_t n_k = kb / kRecStride, n_u = ub / in.user_rec, n_s = sb / 64;
   if (n_k + n_u > (size_t)cfg_.sig_cap || n_u > (size_t)cfg_.user_cap || n_s > (size_t)cfg_.span_cap)
     throw std::invalid_argument("window exceeds the engine's capacity (events / user records / spans)");
   const int b = (int)(k % nb_);
@@ -558,7 +559,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   c[2] = n_groups;
   c[4] = (int32_t)(uint32_t)(uint64_t)in.bases[0];
   c[5] = (int32_t)(uint32_t)((uint64_t)in.bases[0] >> 32);
-  c[7] = 64;  // 64-byte spans
+  c[6] = in.user_rec;  // user-space record bytes
+  c[7] = 64;           // 64-byte spans
   for (int q = 1; q < 4; ++q) {
     c[8 + 2 * (q - 1)] = (int32_t)(uint32_t)(uint64_t)in.bases[q];
     c[9 + 2 * (q - 1)] = (int32_t)(uint32_t)((uint64_t)in.bases[q] >> 32);

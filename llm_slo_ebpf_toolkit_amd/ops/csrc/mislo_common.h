@@ -34,6 +34,18 @@ struct alignas(64) Event {
 };
 static_assert(sizeof(Event) == 64, "Event must be 64 bytes");
 
+// 32-byte user-space record (collector/records.py USER32; the rocprofiler tool writes it into
+// rings created with 32-byte records): fixed-point value, no connection, svc|node from the
+// device pod table
+struct alignas(32) User32 {
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli, pod_id, pid;
+  uint8_t signal_type, flags;
+  uint16_t node_id;
+};
+static_assert(sizeof(User32) == 32, "User32 must be 32 bytes");
+
 // 16-byte wire record (EVENT16 = probes/ebpf/mislo_record.h mislo_event16, the payload of the
 // BPF ring's records): timestamp as an offset from one of the window's 4 epoch bases, selected
 // by the 2-bit tag in the top of trace_id (ts = base[tag] + ts_off; counts[4..5], [8..13]);

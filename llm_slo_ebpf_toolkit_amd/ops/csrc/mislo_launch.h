@@ -53,12 +53,13 @@ void launch_ring_defs(const uint8_t* framed, const int* n_dev, int cap, uint32_t
 // imp[i - counts[0]]) that join but are not counted: segment 0 decodes rows [0, rows[0]) (the
 // records + the previous window's halo), segment 1 rows [rows[0], rows[1]) (other GPUs' rows)
 // with `grid` blocks whose partition counts start at block row `blk_base`; tmax (u64) receives
-// the window's latest local timestamp
+// the window's latest local timestamp; user-space rows are 64-byte EVENTs or, with counts[6]
+// == 32, User32 records whose svc|node comes from the pod table
 void launch_decode_window(const uint8_t* framed, const void* user, const int* n_dev, const int* rows, int cap,
                           const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
-                          uint32_t* ring_state, unsigned long long* tmax, const SignalCols& cols, uint32_t* hist,
-                          uint32_t* status_cnt, uint32_t* part_cnt, unsigned long long* misc, hipStream_t stream,
-                          int seg = 0, int grid = 0, int blk_base = 0);
+                          uint32_t* ring_state, unsigned long long* tmax, const uint32_t* pod_sn, uint32_t n_pods,
+                          const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
+                          unsigned long long* misc, hipStream_t stream, int seg = 0, int grid = 0, int blk_base = 0);
 
 // exchange.hip: stable row selections (halo carry, trace-tagged rows for the GPU exchange)
 constexpr int kSelHalo = 0, kSelTrace = 1;

@@ -135,7 +135,22 @@ def apply_ring_defs(framed: np.ndarray, table: CtxTable, tmap: TraceMap, pod_sn:
             tmap.m[tid] = lo | (hi << 32)
 
 
-def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases) -> Decoded:
+def decode_user32(u: np.ndarray, pod_sn: Dict[int, int]) -> Decoded:
+    """k_decode_window on USER32 rows: fixed-point value, svc|node from the pod table, no connection."""
+    type_slot = np.full(256, NO_SLOT, dtype=np.uint8)
+    for s in catalog.SIGNALS:
+        if s.kernel_type < 256:
+            type_slot[s.kernel_type] = s.slot
+    slot = type_slot[u["signal_type"].astype(np.int64)]
+    val = (u["value_milli"].astype(np.float64) * 1e-3).astype(np.float32)
+    sn = np.array([pod_sn.get(int(p), 0) for p in u["pod_id"].tolist()], dtype=np.uint32)
+    n = len(u)
+    return Decoded(u["ts_ns"].astype(np.int64), val, slot, status_of(val, slot), u["pod_id"].astype(np.uint32),
+                   u["pid"].astype(np.uint32), sn, u["trace_h"].astype(np.uint64), np.zeros(n, np.uint64))
+
+
+def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases,
+                  pod_sn: Dict[int, int] = None) -> Decoded:
     """k_decode_window: rows [0, n framed) from the framed ring records (definitions, discarded
     and busy records are holes: ts 0, no slot; kernel trace ids become their hashes), then the
     user-space 64-byte records (trace hashes as is, conn32 connections)."""
@@ -149,10 +164,13 @@ def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: T
     for f, z in (("ts", 0), ("val", 0), ("slot", NO_SLOT), ("status", 0), ("pod", 0), ("pid", 0), ("svcnode", 0),
                  ("trace", 0), ("conn", 0)):
         getattr(d, f)[hole] = z
-    u = decode_events(user) if len(user) else None
-    if u is None:
+    if not len(user):
         return d
-    u.conn = records.conn32_np(u.conn).astype(np.uint64)
+    if user.dtype == records.USER32:
+        u = decode_user32(user, pod_sn or {})
+    else:
+        u = decode_events(user)
+        u.conn = records.conn32_np(u.conn).astype(np.uint64)
     cat = lambda a, b: np.concatenate([a, b])  # noqa: E731
     assert n_k == len(d.ts)
     return Decoded(cat(d.ts, u.ts), cat(d.val, u.val), cat(d.slot, u.slot), cat(d.status, u.status), cat(d.pod, u.pod),

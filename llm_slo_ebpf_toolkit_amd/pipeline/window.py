@@ -128,14 +128,14 @@ class WindowPipeline:
 
     # ---- per window -----------------------------------------------------------------------
     def submit(self, kernel, user, spans, n_groups: int, labels=None, bases=(0, 0, 0, 0), with_labels: bool = True,
-               learn: Optional[bool] = None) -> int:
+               learn: Optional[bool] = None, user_rec: int = 64) -> int:
         """Queue the next window: ``kernel`` / ``user`` / ``spans`` = [(host address, bytes)] ranges
         of framed ring records / 64-byte records / 64-byte spans. Returns its index."""
         k = self.k
         learn = (self.learn and with_labels) if learn is None else learn
         lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.int32)
         self.eng.submit(k, list(kernel), list(user), list(spans), int(n_groups), lab, [int(b) for b in bases],
-                        bool(with_labels), bool(learn))
+                        bool(with_labels), bool(learn), int(user_rec))
         self.k += 1
         if self.learn and not self.device_refit and k >= 2:
             self._host_refit(k - 2)  # window k-2 is done or nearly (k-1 would stall the host)
@@ -304,8 +304,12 @@ class RingWindowSource:
             self.direct["ring"] = pipe.eng.register_host(ring.data_address, 2 * ring.size)
             self.kpos = ring.consumer_pos
             self.kmask = ring.size - 1
+        # user-space producers' records: 64-byte EVENT or 32-byte USER32, per ring
+        self.user_rec = int(user_ring.rec_size) if user_ring is not None else 64
+        if self.user_rec not in (32, 64):
+            raise ValueError(f"user ring holds {self.user_rec}-byte records (EVENT = 64, USER32 = 32)")
         if user_ring is not None:
-            self.direct["user"] = pipe.eng.register_host(user_ring.address, user_ring.capacity * 64)
+            self.direct["user"] = pipe.eng.register_host(user_ring.address, user_ring.capacity * self.user_rec)
             self.upos = user_ring.tail
         if span_ring is not None:
             self.direct["spans"] = pipe.eng.register_host(span_ring.address, span_ring.capacity * 64)
@@ -416,7 +420,7 @@ class RingWindowSource:
         user, n_u = [], 0
         if self.user_ring is not None:
             cap = self.user_ring.capacity
-            user, n_u = self._ring_ranges(self.upos, cut.user, 64, self.user_ring.address, cap,
+            user, n_u = self._ring_ranges(self.upos, cut.user, self.user_rec, self.user_ring.address, cap,
                                           min(pipe.user_cap, budget - n_k))
             self.carried += max(0, cut.user - self.upos) - n_u
             self.upos += n_u
@@ -428,7 +432,8 @@ class RingWindowSource:
             self.spos += n_s
         wl = labels is not None if with_labels is None else with_labels
         t2 = time.perf_counter()
-        k = pipe.submit(kern, user, spans, n_groups, labels, cut.bases, with_labels=wl, learn=learn)
+        k = pipe.submit(kern, user, spans, n_groups, labels, cut.bases, with_labels=wl, learn=learn,
+                        user_rec=self.user_rec)
         self.submit_s += time.perf_counter() - t2
         self.pending.append([k, k_ranges, n_u, n_s, False])
         self.host_s += time.perf_counter() - t0
@@ -473,7 +478,8 @@ def kernel_event_mask(events: np.ndarray) -> np.ndarray:
     return ~np.isin(events["signal_type"], gpu_types)
 
 
-def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim_ring=None) -> List[ReplayImage]:
+def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim_ring=None,
+                        user_rec: int = 64) -> List[ReplayImage]:
     """Run replay windows through the native probe model (one epoch per window cut, published
     at the window start): kernel-signal events become framed EVENT16 ring bytes, GPU-signal
     events stay 64-byte user-space records, spans stay 64-byte span records."""
@@ -499,8 +505,10 @@ def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim
         sim_ring.cfg_set(rt.CFG_EPOCH, clock.publish(int(w.t0_ns)))
         parts.append(sim.encode(np.ascontiguousarray(kev[~early])))
         payload = np.concatenate(parts)
+        uev = np.ascontiguousarray(w.events[~km])
         out.append(ReplayImage(framed=rt.frame_records(payload), spans=np.ascontiguousarray(w.spans),
-                               user=np.ascontiguousarray(w.events[~km]), bases=clock.bases(), n_groups=w.n_groups,
+                               user=records.to_user32(uev) if user_rec == 32 else uev, bases=clock.bases(),
+                               n_groups=w.n_groups,
                                labels=np.asarray(w.group_labels, dtype=np.int32), domains=list(w.group_domains),
                                n_kernel=int(km.sum())))
     return out

@@ -1,9 +1,10 @@
 // rocprofiler-sdk tool library: the user-space GPU signal source of the MI355X agent.
 //
 // Loaded into an LLM workload (ROCP_TOOL_LIBRARIES=libmislo_rocprof.so, no root needed),
-// it turns runtime activity into the four GPU signals of the catalogue and pushes them,
-// as 64-byte EVENT records (collector/records.py), into the agent's shared-memory ring
-// (runtime/csrc/ring.h C ABI) -- the same hand-off the BPF probes use:
+// it turns runtime activity into the four GPU signals of the catalogue and pushes them into
+// the agent's shared-memory ring (runtime/csrc/ring.h C ABI) as the ring's record type: 64-byte
+// EVENT or, in rings created with 32-byte records, USER32 (collector/records.py; the value in
+// fixed point by the probes' own rule, mislo_record.h mislo_milli -- half the PCIe bytes):
 //
 //   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue            (ns)
 //   type 14 hbm_pressure_pct     live device allocations / HBM capacity     (milli-pct)
@@ -41,8 +42,11 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "mislo_record.h"
+
 extern "C" {
 void* mislo_ring_open_shm(const char* name);
+uint32_t mislo_ring_rec_size(void* ring);
 void mislo_ring_close(void* ring);
 uint64_t mislo_ring_push_batch(void* ring, const void* recs, uint64_t n);
 }
@@ -60,6 +64,15 @@ struct alignas(64) EventRec {  // collector/records.py EVENT
 };
 static_assert(sizeof(EventRec) == 64, "EVENT layout");
 
+struct User32Rec {  // collector/records.py USER32
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli, pod_id, pid;
+  uint8_t signal_type, flags;
+  uint16_t node_id;
+};
+static_assert(sizeof(User32Rec) == 32, "USER32 layout");
+
 constexpr uint16_t kQueueDelay = 13, kHbmPressure = 14, kXgmiLatency = 15, kRcclCollective = 16;
 
 struct State {
@@ -74,6 +87,7 @@ struct State {
   uint64_t max_eps = 200000;
   uint64_t queue_floor_ns = 100000;
   double xgmi_bytes_per_ns = 64.0;
+  bool rec32 = false;  // the ring holds 32-byte USER32 records
   bool verbose = false;
   std::mutex mu;
   std::unordered_map<uint64_t, uint64_t> enqueue_ts;  // correlation id -> enqueue time
@@ -102,6 +116,20 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread) {
   }
   if (g.window_count.fetch_add(1, std::memory_order_relaxed) >= g.max_eps) {
     g.dropped.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
+  bool ok;
+  if (g.rec32) {
+    User32Rec u{};
+    u.ts_ns = wall;
+    u.value_milli = mislo_milli(type, value);
+    u.pod_id = g.pod;
+    u.pid = (uint32_t)getpid();
+    u.signal_type = (uint8_t)type;
+    u.flags = 1;  // has_gpu
+    u.node_id = g.node;
+    ok = mislo_ring_push_batch(g.ring, &u, 1) == 1;
+    (ok ? g.pushed : g.dropped).fetch_add(1, std::memory_order_relaxed);
     return;
   }
   EventRec e;
@@ -209,6 +237,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   bool ok = true;
   const char* name = std::getenv("MISLO_RING");
   g.ring = mislo_ring_open_shm(name && *name ? name : "/mislo-agent-events");
+  g.rec32 = g.ring && mislo_ring_rec_size(g.ring) == 32;
   g.pod = (uint32_t)env_u64("MISLO_POD_ID", 0);
   g.node = (uint16_t)env_u64("MISLO_NODE_ID", 0);
   g.svc = (uint16_t)env_u64("MISLO_SVC_ID", 0);

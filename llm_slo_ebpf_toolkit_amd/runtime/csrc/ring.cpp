@@ -197,6 +197,8 @@ void* mislo_ring_handle_ring(void* ring) { return ring ? reinterpret_cast<ShmRin
 
 uint64_t mislo_ring_size(void* ring) { return reinterpret_cast<ShmRing*>(ring)->ring->size(); }
 
+uint32_t mislo_ring_rec_size(void* ring) { return reinterpret_cast<ShmRing*>(ring)->ring->rec_size(); }
+
 uint64_t mislo_ring_dropped(void* ring) {
   return reinterpret_cast<ShmRing*>(ring)->ring->header()->dropped.load(std::memory_order_relaxed);
 }

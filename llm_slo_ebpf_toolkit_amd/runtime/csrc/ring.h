@@ -83,6 +83,7 @@ int mislo_ring_unlink_shm(const char* name);
 int mislo_ring_push(void* ring, const void* rec);
 uint64_t mislo_ring_push_batch(void* ring, const void* recs, uint64_t n);
 uint64_t mislo_ring_size(void* ring);
+uint32_t mislo_ring_rec_size(void* ring);  // 64 (EVENT) or 32 (USER32)
 // The mislo::Ring* behind a handle from mislo_ring_create_shm / mislo_ring_open_shm.
 void* mislo_ring_handle_ring(void* ring);
 uint64_t mislo_ring_dropped(void* ring);

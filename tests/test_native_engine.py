@@ -24,11 +24,11 @@ def windows(n_win=3, seed=31, n=6000, s=300, services=8):
     return [g.next_window() for _ in range(n_win)], g
 
 
-def rings(tag):
+def rings(tag, user_rec=64):
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    return (rt.Ringbuf.create_shm(f"/mislo-gt-{os.getpid()}-{tag}", 1 << 22), rt.HostRing(1 << 14, 64),
+    return (rt.Ringbuf.create_shm(f"/mislo-gt-{os.getpid()}-{tag}", 1 << 22), rt.HostRing(1 << 14, user_rec),
             rt.HostRing(1 << 12, 64))
 
 
@@ -53,13 +53,16 @@ def test_extension_is_native():
     assert mod.__file__.endswith(".so") and mod.device_count() >= 1
 
 
-def test_ring_windows_match_oracle():
+@pytest.mark.parametrize("user_rec", [64, 32])
+def test_ring_windows_match_oracle(user_rec):
+    """user_rec 32: the user-space ring holds USER32 records (the rocprof tool's compact form,
+    svc|node from the device pod table)."""
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
     wins, gen = windows()
-    imgs = build_replay_images(wins)
+    imgs = build_replay_images(wins, user_rec=user_rec)
     pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096)
-    rb, user, spans = rings("oracle")
+    rb, user, spans = rings(f"oracle{user_rec}", user_rec)
     src = RingWindowSource(pipe, rb, user, spans)
     assert all(src.direct.values())  # the rings are page-locked: DMA straight from them
     pods, sn = pod_meta(gen)
@@ -73,7 +76,7 @@ def test_ring_windows_match_oracle():
         k = r["k"]
         assert r["n_kernel"] * 24 == len(img.framed) and r["n_user"] == len(img.user)
         oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
-        d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases)
+        d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases, pod_sn=pod_sn)
         ref = oracle.join(d, oracle.spans_native(img.spans, tmap), w.n_groups)
         pk = pipe.packet(k)
         res = pipe.results(k, w.n_groups)

@@ -52,13 +52,16 @@ def test_runtime_c_abi_library_is_self_contained():
 
 
 @pytest.mark.gpu
-def test_tool_pushes_gpu_signals_into_ring():
+@pytest.mark.parametrize("rec", [64, 32])
+def test_tool_pushes_gpu_signals_into_ring(rec):
+    """rec 32: the ring was created with 32-byte records, so the tool writes USER32."""
     from llm_slo_ebpf_toolkit_amd.collector import records
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    name = f"/mislo-test-{os.getpid()}-events"
-    ring = rt.HostRing(1 << 16, 64, name)
+    dt = records.EVENT if rec == 64 else records.USER32
+    name = f"/mislo-test-{os.getpid()}-events{rec}"
+    ring = rt.HostRing(1 << 16, rec, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0",
                MISLO_POD_ID="7", MISLO_NODE_ID="3", MISLO_SVC_ID="2", MISLO_ROCPROF_VERBOSE="1")
     t0 = time.time_ns()
@@ -67,8 +70,8 @@ def test_tool_pushes_gpu_signals_into_ring():
     assert "[mislo-rocprof] started" in r.stderr, r.stderr[-2000:]
     segs = ring.peek(1 << 16)
     view = ring.records_view()
-    recs = np.concatenate([np.frombuffer(view[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
-                           for _, i, c in segs]) if segs else np.zeros(0, dtype=records.EVENT)
+    recs = np.concatenate([np.frombuffer(view[i * rec:(i + c) * rec].tobytes(), dtype=dt)
+                           for _, i, c in segs]) if segs else np.zeros(0, dtype=dt)
     types = set(recs["signal_type"].tolist())
     assert 13 in types, (types, r.stderr[-1000:])      # gpu_queue_delay_ms from kernel dispatches
     assert 14 in types, (types, r.stderr[-1000:])      # hbm_pressure_pct from allocations
@@ -79,10 +82,10 @@ def test_tool_pushes_gpu_signals_into_ring():
     if torch.cuda.device_count() >= 2:
         pass  # exercised by tests/test_rocprof_tool.py::test_xgmi_peer_copies (multi-GPU runners)
     assert (recs["pod_id"] == 7).all() and (recs["node_id"] == 3).all()
-    assert (recs["flags"] & (1 << 8)).all()
+    assert (recs["flags"] & (1 << 8 if rec == 64 else 1)).all()
     ts = recs["ts_ns"]
     assert (ts > t0 - 10 * 10**9).all() and (ts < time.time_ns() + 10 * 10**9).all()  # wall clock
-    hbm = recs[recs["signal_type"] == 14]["value"].max() * 1e-3  # pct
+    hbm = recs[recs["signal_type"] == 14]["value" if rec == 64 else "value_milli"].max() * 1e-3  # pct
     assert hbm > 0.5  # >= 2 GiB of 288 GiB live
 
 
