@@ -414,6 +414,8 @@ class Agent:
         post, bits, feat = res["post"], res["evbits"].view(np.uint32), res["feat"]
         sli = res.get("sli")
         for g in range(G):
+            if sli is not None and g < sli.shape[0] and sli[g, 0] == 0:
+                continue  # no request of this group in the window: no incident to attribute
             ranked = model.ranked(post[g, :D], bits[g, :D])
             if not ranked or ranked[0].posterior < self.o.min_confidence:
                 continue

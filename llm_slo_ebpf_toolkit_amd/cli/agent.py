@@ -56,7 +56,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("window-spans", d.window_spans, "gpu engine spans per window (capacity)"),
         ("window-groups", d.window_groups, "gpu engine incident groups per window"),
         ("device", d.device, "HIP device ordinal"),
-        ("model", d.model, "attribution model: bayes|bayes_learned|lda"),
+        ("model", d.model, "attribution model: bayes (REF table) | bayes_gpu (REF table + GPU signals/domains) | bayes_learned | lda"),
         ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
         ("ttft-slo-ms", d.ttft_slo_ms, "per-incident TTFT SLO (ms) for burn rates"),
         ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),

@@ -173,7 +173,7 @@ def toolkit_config_schema() -> Dict[str, Any]:
         "gpu": _obj({"enabled": _bool(default=True), "window_ms": _int(1, default=1000),
                      "max_events_per_window": _int(1, default=1 << 20),
                      "world_size": _int(1, default=1),
-                     "attribution_model": _enum(("bayes", "bayes_learned", "lda", "rule"),
+                     "attribution_model": _enum(("bayes", "bayes_gpu", "bayes_learned", "lda", "rule"),
                                                 default="bayes")}),
     }
     req = ["signal_set", "sampling", "correlation", "otlp", "safety"]

@@ -196,6 +196,17 @@ class NaiveBayes:
         return NaiveBayes.from_tables(priors, catalog.ref_likelihoods(), doms, "bayes")
 
     @staticmethod
+    def gpu() -> LinearPosteriorModel:
+        """REF's table extended to the 16 signals x 10 domains (catalog.extended_likelihood_matrix:
+        REF rows and columns unchanged, plus the 4 GPU signals and the 2 GPU domains), uniform
+        priors: an expert model that can name gpu_contention / gpu_interconnect without labels
+        (the agent never learns online, REF's table cannot see GPU signals)."""
+        doms = catalog.ALL_DOMAINS
+        m = catalog.extended_likelihood_matrix()
+        lik = {catalog.SIGNAL_NAMES[s]: dict(zip(doms, m[s])) for s in range(N_SLOTS)}
+        return NaiveBayes.from_tables({d: 1.0 / len(doms) for d in doms}, lik, doms, "bayes_gpu")
+
+    @staticmethod
     def random_init_table(seed: int = 42, domains: Sequence[str] = catalog.ALL_DOMAINS) -> np.ndarray:
         rng = np.random.default_rng(seed)
         return rng.uniform(0.05, 0.95, size=(N_SLOTS, len(domains)))
@@ -320,6 +331,8 @@ def samples_to_arrays(samples: Sequence[FaultSample]) -> Tuple[np.ndarray, np.nd
 def get_model(name: str, stats: Optional[SufficientStats] = None, seed: int = 42) -> LinearPosteriorModel:
     if name in ("bayes", "", None):
         return NaiveBayes.ref()
+    if name == "bayes_gpu":
+        return NaiveBayes.gpu()
     if name == "bayes_learned":
         if stats is None:
             raise ValueError("bayes_learned needs sufficient statistics")

@@ -19,7 +19,7 @@ from .sample import FaultSample, build_attribution
 
 MODE_BAYES = "bayes"
 MODE_RULE = "rule"
-MODES = ("bayes", "bayes_learned", "lda", "rule")
+MODES = ("bayes", "bayes_gpu", "bayes_learned", "lda", "rule")
 
 
 def normalize_mode(mode: str) -> str:

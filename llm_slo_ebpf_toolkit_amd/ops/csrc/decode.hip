@@ -304,34 +304,55 @@ __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ f
                                                    uint32_t* __restrict__ rs) {
   const int n = n_ptr[15];  // framed records in this window
   uint32_t foreign = 0, dctx = 0, dtr = 0, disc = 0, busy = 0xFFFFFFFFu;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint8_t* r = framed + (size_t)i * kRecStride;
-    const uint2 h = *reinterpret_cast<const uint2*>(r);
-    if (h.x & kRbBusy) {
-      busy = min(busy, (uint32_t)i);
-      continue;
-    }
-    if ((h.x & ~(kRbBusy | kRbDiscard)) != 16u) {
-      ++foreign;
-      continue;
-    }
-    if (h.x & kRbDiscard) {
-      ++disc;
-      continue;
-    }
-    const uint2 a = *reinterpret_cast<const uint2*>(r + 8), b = *reinterpret_cast<const uint2*>(r + 16);
-    const uint32_t type = a.y & 0xFFu;
-    if (type == kDefCtx) {  // {conn32, type | id << 8, pod, pid}
-      const uint32_t id = a.y >> 8;
-      if (id && id < ctx_rows) {
-        ctx_tab[id] = make_uint4(b.x, b.y, a.x, b.x < n_pods ? pod_sn[b.x] : 0u);
-        ++dctx;
+  // kU records per thread per trip, all 3 x kU loads issued before any is used: the pass is
+  // bound by memory latency, not bytes (a header load followed by a dependent payload load
+  // per record ran at ~0.6 TB/s)
+  constexpr int kU = 4;
+  const int stride = gridDim.x * 256;
+  for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += stride * kU) {
+    uint2 h[kU], a[kU], b[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * stride;
+      if (i < n) {
+        const uint2* r = reinterpret_cast<const uint2*>(framed + (size_t)i * kRecStride);
+        h[u] = r[0];
+        a[u] = r[1];
+        b[u] = r[2];
+      } else {
+        h[u] = make_uint2(16u, 0u);
+        a[u] = b[u] = make_uint2(0u, 0u);
       }
-    } else if (type == kDefTrace) {  // {id, type, hash lo, hash hi}
-      const unsigned long long hash = (unsigned long long)b.x | ((unsigned long long)b.y << 32);
-      if (hash && a.x && a.x < tt.n) {
-        tt.hash[a.x] = hash;
-        ++dtr;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * stride;
+      if (i >= n) continue;
+      if (h[u].x & kRbBusy) {
+        busy = min(busy, (uint32_t)i);
+        continue;
+      }
+      if ((h[u].x & ~(kRbBusy | kRbDiscard)) != 16u) {
+        ++foreign;
+        continue;
+      }
+      if (h[u].x & kRbDiscard) {
+        ++disc;
+        continue;
+      }
+      const uint32_t type = a[u].y & 0xFFu;
+      if (type == kDefCtx) {  // {conn32, type | id << 8, pod, pid}
+        const uint32_t id = a[u].y >> 8;
+        if (id && id < ctx_rows) {
+          ctx_tab[id] = make_uint4(b[u].x, b[u].y, a[u].x, b[u].x < n_pods ? pod_sn[b[u].x] : 0u);
+          ++dctx;
+        }
+      } else if (type == kDefTrace) {  // {id, type, hash lo, hash hi}
+        const unsigned long long hash = (unsigned long long)b[u].x | ((unsigned long long)b[u].y << 32);
+        if (hash && a[u].x && a[u].x < tt.n) {
+          tt.hash[a[u].x] = hash;
+          ++dtr;
+        }
       }
     }
   }
@@ -492,6 +513,8 @@ __global__ __launch_bounds__(NT) void k_decode_ref(const RefEvent* __restrict__ 
 
 // Span records -> span columns + span partition counts. n_ptr = counts + 1: n_ptr[0] spans,
 // n_ptr[5] valid context rows, n_ptr[6] span record bytes (20 = SpanC20 via the context table).
+constexpr int kSliLds = 1024;  // groups whose SLO counts k_decode_spans keeps in LDS
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp_raw, const int* __restrict__ n_ptr,
                                                      int cap, SpanCols c, uint32_t* part_cnt,
@@ -501,7 +524,13 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   const bool compact = n_ptr[6] == 20;
   if (n_ptr[5] > 0) n_ctx = min(n_ptr[5], n_ctx);
   __shared__ uint32_t s_part[kKeyTypes * kParts];
+  // per-incident SLO counts privatised in LDS: a window's spans all land on its few groups, so
+  // global atomics serialised on a handful of L2 addresses (33 us per 16K-span window)
+  __shared__ uint32_t s_sli[2 * kSliLds];
+  const bool sli_lds = sm.grp_sli && sm.n_groups <= kSliLds;
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
+  if (sli_lds)
+    for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT) s_sli[i] = 0;
   __syncthreads();
   const int n = min(*n_ptr, cap);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -525,8 +554,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
       r.tr = s.trace_h;
       r.cn = sm.native ? (uint64_t)conn32(s.conn_h) : s.conn_h;
       if (sm.grp_sli && s.group_id < (uint32_t)sm.n_groups) {  // per-incident TTFT SLO accounting
-        atomicAdd(&sm.grp_sli[2 * s.group_id], 1u);
-        if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sm.grp_sli[2 * s.group_id + 1], 1u);
+        uint32_t* sli = sli_lds ? s_sli : sm.grp_sli;
+        atomicAdd(&sli[2 * s.group_id], 1u);
+        if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sli[2 * s.group_id + 1], 1u);
       }
       r.pod = s.pod_id;
       r.pid = s.pid;
@@ -545,6 +575,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   }
   __syncthreads();
   store_counts<NT>(s_part, part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);
+  if (sli_lds)
+    for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT)
+      if (s_sli[i]) atomicAdd(&sm.grp_sli[i], s_sli[i]);
 }
 
 // Event decoders run 1024 threads per workgroup: the grid is capped at kPartBlocks (the
@@ -592,7 +625,7 @@ void launch_decode_ref(const void* ev, const int* n_dev, int cap, uint32_t pod, 
 
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
                          const uint32_t* ctx_tab, int n_ctx, hipStream_t stream, const SpanMap* sm) {
-  constexpr int NT = 256;
+  constexpr int NT = 1024;  // the grid is decode_grid(cap) (the span partition matrix): ~1 span per thread
   SpanMap m{};
   if (sm) m = *sm;
   hipLaunchKernelGGL((k_decode_spans<NT>), dim3(decode_grid(cap)), dim3(NT), 0, stream, sp, n_dev, cap, cols,

@@ -124,6 +124,8 @@ class WindowPipeline:
     def _initial_model(self):
         if self.model_name == "bayes":
             return NaiveBayes.ref()
+        if self.model_name == "bayes_gpu":
+            return NaiveBayes.gpu()
         return NaiveBayes.learned(SufficientStats(), seed=self.seed)
 
     # ---- per window -----------------------------------------------------------------------

@@ -78,6 +78,26 @@ def chat(port: int, i: int, phase: str) -> dict:
     return {"phase": phase, "t_ns": t, "ttft_ms": out["ttft_ms"], "trace_id": out["trace_id"]}
 
 
+def scrape(port: int) -> dict:
+    """The agent's /metrics counters this run reads: GPU-signal events by status, join outcomes."""
+    out = {}
+    try:
+        text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    except OSError:
+        return out
+    for ln in text.splitlines():
+        if ln.startswith(("llm_ebpf_probe_events_total{", "llm_slo_agent_correlation_pairs_total{")):
+            key, val = ln.rsplit(" ", 1)
+            if "llm_ebpf_probe_events_total" in key and not any(s in key for s in ("gpu_", "hbm_", "xgmi_", "rccl_")):
+                continue
+            out[key] = float(val)
+    return out
+
+
+def delta(a: dict, b: dict) -> dict:
+    return {k: b[k] - a.get(k, 0.0) for k in b if b[k] - a.get(k, 0.0)}
+
+
 def pct(xs, q):
     xs = sorted(xs)
     return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))] if xs else None
@@ -88,6 +108,7 @@ def main() -> int:
     ap.add_argument("--out", default="gpurun_out/config2")
     ap.add_argument("--requests", type=int, default=24, help="requests per phase")
     ap.add_argument("--preset", default="1b")
+    ap.add_argument("--ttft-slo-ms", type=float, default=100.0, help="the agent's TTFT SLO (burn rate per incident)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     from llm_slo_ebpf_toolkit_amd.collector import bpf
@@ -103,7 +124,8 @@ def main() -> int:
         [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "shm",
          "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
          "--window-ms", "1000", "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
-         "--model", "bayes", "--min-confidence", "0.3", "--halo-ms", "0", "--output", "jsonl",
+         "--model", "bayes_gpu", "--min-confidence", "0.3", "--halo-ms", "0", "--ttft-slo-ms", str(a.ttft_slo_ms),
+         "--output", "jsonl",
          "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
     llm_env = dict(env, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1",
                    MISLO_QUEUE_FLOOR_NS="200000", OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces",
@@ -113,6 +135,7 @@ def main() -> int:
                            cwd=ROOT, env=llm_env, stdout=log, stderr=subprocess.STDOUT)
     burner = None
     rows = []
+    counters = {}
     try:
         wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 180)
         wait_http(f"http://127.0.0.1:{hport}/healthz", llm, 300)
@@ -126,6 +149,7 @@ def main() -> int:
                                           stderr=subprocess.STDOUT)
                 time.sleep(3.0)
             t_phase = time.time_ns()
+            m0 = scrape(mport)
             for i in range(a.requests):
                 rows.append(chat(hport, i, phase))
                 time.sleep(0.1)
@@ -137,6 +161,7 @@ def main() -> int:
             print(f"[config2] {phase}: {len(rs)} requests, TTFT p50 {pct(rs, .5):.1f} ms p95 {pct(rs, .95):.1f} ms "
                   f"(from {t_phase})", flush=True)
             time.sleep(2.5)  # let the phase's last window close
+            counters[phase] = delta(m0, scrape(mport))
     finally:
         for p in (burner, llm):
             if p is not None and p.poll() is None:
@@ -180,6 +205,7 @@ def main() -> int:
                     for p in ("baseline", "fault_gpu_contention", "recovery")
                     for v in [[r["ttft_ms"] for r in rows if r["phase"] == p]]},
         "attributions_total": len(attrs),
+        "agent_counters_by_phase": counters,
         "rag_service_by_phase": {p: {"windows": d["windows"], "domains": d["domains"], "evidence": d["evidence"][:3]}
                                  for p, d in by_phase.items()},
         "agent_exit": agent.returncode, "llm_exit": llm.returncode,
