@@ -444,7 +444,7 @@ class Agent:
         lat_ms = pipe.window_ms(k)[0]
         rs = pk["ring_state"]
         self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], rs["events"], lat_ms, self.o.node, self.o.pod,
-                                    self.o.namespace)
+                                    self.o.namespace, value_sums_milli=pk["misc"][2:18])
         self.metrics.set_ring(ring.stats() if ring is not None else {}, rs, host_us)
         res = pipe.results(k, G)
         for attr in self._attributions(G, names, res, t_ns, pipe.model):

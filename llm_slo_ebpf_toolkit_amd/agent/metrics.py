@@ -64,6 +64,10 @@ class AgentMetrics:
         self.ring_backlog = r.gauge("llm_slo_agent_ring_backlog_bytes", "Unconsumed bytes in the BPF ring buffer.")
         self.host_us = r.gauge("llm_slo_agent_window_host_us", "Host time to assemble the last window (us).")
         self.rss = r.gauge("llm_slo_agent_memory_rss_bytes", "Agent process resident set size (bytes).")
+        # GPU signals' value distributions (the window histograms the decode kernel builds)
+        self.gpu_hist = {s.slot: r.histogram(f"llm_ebpf_{s.name}", f"{s.name} values observed from GPU signal records.",
+                                             s.buckets)
+                         for s in catalog.SIGNALS if s.gpu and s.buckets}
         self.up.set(1)
         for k in EVENT_KINDS:
             self.kind.set(1 if k == event_kind else 0, k)
@@ -106,8 +110,9 @@ class AgentMetrics:
 
     # ---- GPU window outputs -------------------------------------------------------------
     def observe_window(self, hist: np.ndarray, status: np.ndarray, dbg, n_events: int, latency_ms: float,
-                       node: str, pod: str, namespace: str) -> None:
-        """hist [16 slots x 16 buckets], status [16 x 3] from the window packet."""
+                       node: str, pod: str, namespace: str, value_sums_milli=None) -> None:
+        """hist [16 slots x 16 buckets], status [16 x 3], value sums (1/1000 unit) per slot from the
+        window packet."""
         self.win_total.inc()
         self.win_events.inc(float(n_events))
         self.win_latency.observe(latency_ms)
@@ -117,6 +122,12 @@ class AgentMetrics:
         ref_counts = list(h[:nref]) + [float(h[nref:].sum())]  # buckets above 800 -> +Inf
         self.dns.add_counts(ref_counts, 0.0, _nz(node, "unknown-node"), _nz(pod, "unknown-pod"),
                             _nz(namespace, "default"))
+        for slot, hm in self.gpu_hist.items():
+            row = np.asarray(hist[slot], dtype=np.float64)
+            nb = len(hm.buckets)
+            if row[: nb + 1].sum():
+                total = float(value_sums_milli[slot]) * 1e-3 if value_sums_milli is not None else 0.0
+                hm.add_counts(list(row[:nb - 1]) + [float(row[nb - 1:].sum())], total)
         names = ("ok", "warning", "error")
         for s in catalog.SIGNALS:
             row = status[s.slot]

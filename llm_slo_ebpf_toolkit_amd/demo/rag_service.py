@@ -122,13 +122,61 @@ class LlamaBackend:
         return {"ttft_s": r["ttft_ms"] / 1e3, "total_s": r["total_ms"] / 1e3, "tokens": r["new_tokens"]}
 
 
-class SpanExporter:
-    """Batched OTLP/HTTP JSON trace export (chat.request / chat.retrieval / chat.generation)."""
+class GpuTraceTag:
+    """Tags the GPU work of a request with its trace: when the rocprofiler-sdk tool
+    (probes/rocprof, libmislo_rocprof.so) is loaded into this process, the kernels the calling
+    thread enqueues carry the request's trace hash (the OTLP receiver's rule: low 64 bits of the
+    W3C id), so the agent joins them to the request's spans through the trace tier. A no-op
+    without the tool."""
 
-    def __init__(self, endpoint: str, service: str = "rag-service", max_batch: int = 64, resource=None):
+    def __init__(self):
+        self._set = None
+        self._resolved = False
+
+    def _resolve(self) -> None:
+        # the tool is loaded when the HIP runtime starts (first GPU use), so resolve lazily
+        self._resolved = True
+        try:
+            with open("/proc/self/maps") as f:
+                path = next((ln.split()[-1] for ln in f if ln.rstrip().endswith("libmislo_rocprof.so")), None)
+            if path:
+                import ctypes
+
+                fn = ctypes.CDLL(path, mode=os.RTLD_NOLOAD | os.RTLD_NOW).mislo_rocprof_set_trace
+                fn.argtypes, fn.restype = [ctypes.c_uint64], None
+                self._set = fn
+        except (OSError, AttributeError):
+            self._set = None
+
+    @property
+    def active(self) -> bool:
+        if not self._resolved:
+            self._resolve()
+        return self._set is not None
+
+    def set(self, trace_id: str) -> None:
+        if not self._resolved:
+            self._resolve()
+        if self._set is not None:
+            from ..collector.otlp import trace_hash
+
+            self._set(trace_hash(trace_id) if trace_id else 0)
+
+
+class SpanExporter:
+    """Batched OTLP/HTTP JSON trace export (chat.request / chat.retrieval / chat.generation):
+    a batch goes out when it holds ``max_batch`` spans or its oldest span is ``max_delay_s`` old
+    (the OTel batch processor's schedule delay), so spans reach the agent's windows promptly."""
+
+    def __init__(self, endpoint: str, service: str = "rag-service", max_batch: int = 64, resource=None,
+                 max_delay_s: float = 0.2):
         self.endpoint, self.service, self.max_batch = endpoint, service, max_batch
+        self.max_delay_s = max_delay_s
         self.buf: List[dict] = []
         self.lock = threading.Lock()
+        self._wake = threading.Event()
+        if endpoint and max_delay_s > 0:
+            threading.Thread(target=self._flusher, name="span-flush", daemon=True).start()
         # resource identity the agent's OTLP receiver maps onto its pod / process ids
         # (collector/otlp.py): pod uid / name and node from the downward API, this process's pid
         res = {"service.name": service, "process.pid": os.getpid(),
@@ -172,6 +220,12 @@ class SpanExporter:
         if batch:
             self._post(batch)
 
+    def _flusher(self) -> None:
+        while True:
+            self._wake.wait(self.max_delay_s)
+            self._wake.clear()
+            self.flush()
+
     def _post(self, spans: List[dict]) -> None:
         body = {"resourceSpans": [{"resource": {"attributes": self.resource},
                                    "scopeSpans": [{"scope": {"name": "rag-service"}, "spans": spans}]}]}
@@ -209,6 +263,7 @@ class RagService:
         self.corr = Correlator()
         self.node, self.pod = node, pod
         self.spans = SpanExporter(otlp_endpoint, resource=resource)
+        self.gpu_tag = GpuTraceTag()
         self.burn = BurnRate()
         r = self.registry = Registry()
         ms = (5, 10, 25, 50, 100, 200, 400, 800, 1600, 3200)
@@ -262,11 +317,14 @@ class RagService:
             if emit:
                 emit({"token": t, "index": len(tokens) - 1})
 
+        self.gpu_tag.set(trace_id)  # this request's kernels carry its trace
         try:
             g = self.backend.generate(prompt, max_tokens, seed, plan, on_tok)
         except Exception:
             self._fail(profile)
             raise
+        finally:
+            self.gpu_tag.set("")
         t_end = time.time_ns()
         ret_ms = (t_r1 - t_r0) / MS
         ttft_ms = (t_r1 - t_req) / MS + g["ttft_s"] * 1e3

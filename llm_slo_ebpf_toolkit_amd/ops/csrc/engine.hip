@@ -176,7 +176,11 @@ void WindowEngine::alloc() {
     else copy2_ = copy_;
   }
   HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
-  HIPCHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+  // one GPU: the window's tail (packet accumulate, timing) runs on the compute stream; a comm
+  // stream of its own exists only with a communicator (init_comm). Every stream backs a
+  // hardware queue, and each MI355X queue pins ~173 MB of host memory (its context save area,
+  // measured: tools/rss_probe.py), so a single-GPU agent does without it.
+  comm_stream_ = compute_;
   // device input block per buffer: [head (counts + labels) | framed ring records | user records | spans]
   const size_t head = (kHeadBytes + 4 * (size_t)G + 63) & ~size_t(63);
   off_kern_ = head;
@@ -329,7 +333,7 @@ WindowEngine::~WindowEngine() {
   if (copy_) hipStreamDestroy(copy_);
   if (copy2_ && copy2_ != copy_) hipStreamDestroy(copy2_);
   if (compute_) hipStreamDestroy(compute_);
-  if (comm_stream_) hipStreamDestroy(comm_stream_);
+  if (comm_stream_ && comm_stream_ != compute_) hipStreamDestroy(comm_stream_);
 }
 
 SignalCols WindowEngine::sig_cols() const { return SignalCols{g_rec_, g_status_, g_part_}; }
@@ -779,6 +783,7 @@ void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
   if (submitted_) throw std::logic_error("init_comm before the first window");
   HIPCHECK(hipSetDevice(cfg_.device));
   NCCLCHECK(ncclCommInitRank(&comm_, world, id, rank));
+  HIPCHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   rank_ = rank;
   world_ = world;
   for (int b = 0; b < nb_; ++b) {

@@ -19,6 +19,12 @@
 // and a per-second budget caps the producer so a pathological workload cannot flood the
 // ring (full rings drop, never block).
 //
+// Request tagging: a serving process calls mislo_rocprof_set_trace(hash) (C ABI, e.g. through
+// ctypes on the already-loaded library) on the thread that runs a request; kernels that thread
+// enqueues carry the hash (trace_h: the low 64 bits of the request's W3C trace id, the OTLP
+// receiver's rule), so the agent joins them to the request's spans through the trace tier
+// instead of the coarser pod+pid window.
+//
 // Environment: MISLO_RING (default /mislo-agent-events), MISLO_POD_ID, MISLO_NODE_ID,
 // MISLO_SVC_ID, MISLO_HBM_BYTES (default 288 GiB), MISLO_MAX_EPS (default 200000),
 // MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_XGMI_GBPS (nominal peer-copy rate, default
@@ -90,7 +96,10 @@ struct State {
   bool rec32 = false;  // the ring holds 32-byte USER32 records
   bool verbose = false;
   std::mutex mu;
-  std::unordered_map<uint64_t, uint64_t> enqueue_ts;  // correlation id -> enqueue time
+  struct Enq {
+    uint64_t ts, trace_h;
+  };
+  std::unordered_map<uint64_t, Enq> enqueue_ts;  // correlation id -> enqueue time, request trace
   std::unordered_map<uint64_t, uint64_t> live_alloc;  // address -> bytes
   uint64_t live_bytes = 0;
   uint64_t last_hbm_milli = ~0ull;
@@ -98,6 +107,7 @@ struct State {
 };
 
 State g;
+thread_local uint64_t t_trace = 0;  // the calling thread's current request (mislo_rocprof_set_trace)
 
 uint64_t env_u64(const char* k, uint64_t d) {
   const char* v = std::getenv(k);
@@ -106,7 +116,7 @@ uint64_t env_u64(const char* k, uint64_t d) {
 
 uint32_t tid() { return (uint32_t)syscall(SYS_gettid); }
 
-void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread) {
+void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t trace_h = 0) {
   if (!g.ring) return;
   const int64_t wall = (int64_t)ts + g.clock_offset;
   const uint64_t sec = (uint64_t)wall / 1000000000ull;
@@ -122,6 +132,7 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread) {
   if (g.rec32) {
     User32Rec u{};
     u.ts_ns = wall;
+    u.trace_h = trace_h;
     u.value_milli = mislo_milli(type, value);
     u.pod_id = g.pod;
     u.pid = (uint32_t)getpid();
@@ -136,6 +147,7 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread) {
   std::memset(&e, 0, sizeof(e));
   e.ts_ns = wall;
   e.value = value;
+  e.trace_h = trace_h;
   e.pid = (uint32_t)getpid();
   e.tid = thread ? thread : tid();
   e.pod_id = g.pod;
@@ -165,10 +177,10 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
     std::lock_guard<std::mutex> lk(g.mu);
-    g.enqueue_ts[rec.correlation_id.internal] = now;
+    g.enqueue_ts[rec.correlation_id.internal] = State::Enq{now, t_trace};  // the enqueuing thread's request
   } else if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_COMPLETE) {
     auto* d = static_cast<rocprofiler_callback_tracing_kernel_dispatch_data_t*>(rec.payload);
-    uint64_t enq = 0;
+    State::Enq enq{0, 0};
     {
       std::lock_guard<std::mutex> lk(g.mu);
       auto it = g.enqueue_ts.find(rec.correlation_id.internal);
@@ -177,9 +189,10 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
         g.enqueue_ts.erase(it);
       }
     }
-    if (enq && d && d->start_timestamp > enq) {
-      const uint64_t delay = d->start_timestamp - enq;
-      if (delay >= g.queue_floor_ns) emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id);
+    if (enq.ts && d && d->start_timestamp > enq.ts) {
+      const uint64_t delay = d->start_timestamp - enq.ts;
+      if (delay >= g.queue_floor_ns)
+        emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id, enq.trace_h);
     }
   }
 }
@@ -299,6 +312,9 @@ extern "C" {
 // Counters for tests / the agent's ring statistics.
 uint64_t mislo_rocprof_pushed() { return g.pushed.load(); }
 uint64_t mislo_rocprof_dropped() { return g.dropped.load(); }
+
+// The calling thread's current request trace (0 = none): kernels it enqueues from now on carry it.
+void mislo_rocprof_set_trace(uint64_t trace_h) { t_trace = trace_h; }
 
 rocprofiler_tool_configure_result_t* rocprofiler_configure(uint32_t, const char*, uint32_t,
                                                            rocprofiler_client_id_t* id) {

@@ -89,6 +89,49 @@ def test_tool_pushes_gpu_signals_into_ring(rec):
     assert hbm > 0.5  # >= 2 GiB of 288 GiB live
 
 
+TAG_WORKLOAD = r"""
+import torch
+from llm_slo_ebpf_toolkit_amd.demo.rag_service import GpuTraceTag
+x = torch.randn(2048, 2048, device="cuda")
+torch.cuda.synchronize()
+tag = GpuTraceTag()
+assert tag.active, "tool not found in /proc/self/maps"
+tag.set("0af7651916cd43dd8448eb211c80319c")   # W3C id; low 64 bits 0x8448eb211c80319c
+for _ in range(50):
+    x = torch.tanh(x @ x) * 0.5
+torch.cuda.synchronize()
+tag.set("")
+for _ in range(50):
+    x = torch.tanh(x @ x) * 0.5
+torch.cuda.synchronize()
+print("tag workload done")
+"""
+
+
+@pytest.mark.gpu
+def test_request_trace_tags_gpu_records():
+    """A serving thread's mislo_rocprof_set_trace: the kernels it enqueues carry the request's
+    trace hash (trace-tier joins with the request's spans); after clearing, none do."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    name = f"/mislo-test-{os.getpid()}-tag"
+    ring = rt.HostRing(1 << 16, 32, name)
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", TAG_WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    segs = ring.peek(1 << 16)
+    view = ring.records_view()
+    recs = np.concatenate([np.frombuffer(view[i * 32:(i + c) * 32].tobytes(), dtype=records.USER32)
+                           for _, i, c in segs])
+    q = recs[recs["signal_type"] == 13]
+    tagged = q[q["trace_h"] == 0x8448EB211C80319C]
+    assert len(tagged) >= 50, (len(q), len(tagged))
+    assert set(q["trace_h"].tolist()) <= {0, 0x8448EB211C80319C}
+    assert (q["trace_h"] == 0).sum() >= 50  # the untagged half
+
+
 XGMI_WORKLOAD = r"""
 import torch
 a = torch.empty(64 << 20, dtype=torch.uint8, device="cuda:0")

@@ -86,7 +86,8 @@ def scrape(port: int) -> dict:
     except OSError:
         return out
     for ln in text.splitlines():
-        if ln.startswith(("llm_ebpf_probe_events_total{", "llm_slo_agent_correlation_pairs_total{")):
+        if ln.startswith(("llm_ebpf_probe_events_total{", "llm_slo_agent_correlation_pairs_total{",
+                          "llm_ebpf_gpu_queue_delay_ms_")):
             key, val = ln.rsplit(" ", 1)
             if "llm_ebpf_probe_events_total" in key and not any(s in key for s in ("gpu_", "hbm_", "xgmi_", "rccl_")):
                 continue
@@ -124,7 +125,7 @@ def main() -> int:
         [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "shm",
          "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
          "--window-ms", "1000", "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
-         "--model", "bayes_gpu", "--min-confidence", "0.3", "--halo-ms", "0", "--ttft-slo-ms", str(a.ttft_slo_ms),
+         "--model", "bayes_gpu", "--min-confidence", "0.3", "--halo-ms", "1500", "--ttft-slo-ms", str(a.ttft_slo_ms),
          "--output", "jsonl",
          "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
     llm_env = dict(env, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1",

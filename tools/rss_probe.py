@@ -25,6 +25,22 @@ def rss_mb() -> float:
         return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2**20
 
 
+def big_anon(min_mb: float = 8.0):
+    """Anonymous mappings with >= min_mb resident: (size MB, rss MB, flags)."""
+    out, cur = [], None
+    with open("/proc/self/smaps") as f:
+        for ln in f:
+            p = ln.split()
+            if p and "-" in p[0] and not p[0].endswith(":"):
+                a, b = (int(x, 16) for x in p[0].split("-"))
+                cur = [(b - a) / 2**20, 0.0, p[1]] if len(p) <= 5 else None
+                if cur is not None:
+                    out.append(cur)
+            elif p and p[0] == "Rss:" and cur is not None:
+                cur[1] = int(p[1]) / 1024
+    return sorted([m for m in out if m[1] >= min_mb], key=lambda m: -m[1])
+
+
 def step(name):
     print(f"{name:40s} rss {rss_mb():8.1f} MB  anon {anon_mb():8.1f} MB", flush=True)
 
@@ -42,8 +58,15 @@ def main():
     step("set_tables")
     from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline
 
+    small = WindowPipeline(65536, 4096, 64, 0, None, model="bayes", learn=False, user_cap=16384)
+    step("WindowPipeline(sig_cap=65536)")
+    small.eng.close()
+    del small
+    step("  closed")
     pipe = WindowPipeline(n, 16384, 64, 0, None, model="bayes", learn=False, user_cap=n // 4)
     step(f"WindowPipeline(sig_cap={n})")
+    for m in big_anon():
+        print(f"    anon mapping {m[0]:9.1f} MB  rss {m[1]:8.1f} MB  {m[2]}", flush=True)
     from llm_slo_ebpf_toolkit_amd.collector import bpf
 
     names = bpf.RingNames.of(f"/mislo-rss-{os.getpid()}")
