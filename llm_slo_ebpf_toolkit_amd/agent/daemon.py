@@ -368,7 +368,7 @@ class Agent:
         names = bpf.RingNames.of(o.ring_name)
         if o.source == "bpf":
             maps = bpf.BpfMaps(o.pin_dir)
-            user = rt.HostRing(1 << 20, 64, names.user)   # rocprofiler tool / services attach and push
+            user = rt.HostRing(1 << 20, 32, names.user)   # the rocprofiler tool attaches, pushes USER32
             spans = rt.HostRing(1 << 18, 64, names.spans)  # OTLP receiver / services
             return maps, maps.ring, user, spans, None
         if o.source == "shm":
@@ -379,7 +379,9 @@ class Agent:
             kw = dict(scenario=o.scenario if o.scenario not in ("baseline",) else "full",
                       events_per_window=o.window_events, spans_per_window=o.window_spans,
                       n_services=o.window_groups)
-            ring, user, spans = bpf.create_rings(names, 4 * 24 * o.window_events, 4 * o.window_events,
+            # the replay writes ~1/4 of a window's events as GPU-signal records: rings of 2+
+            # windows each (the shared pages count in the agent's RSS once registered for DMA)
+            ring, user, spans = bpf.create_rings(names, 2 * 24 * o.window_events, o.window_events,
                                                  4 * o.window_spans)
             self._producer = bpf.start_replay_producer(names, kw, o.window_events * 1000.0 / o.window_ms,
                                                        o.window_ms, max_windows=0)

@@ -175,13 +175,16 @@ class RingNames:
         return RingNames(prefix + "-bpf", prefix + "-events", prefix + "-spans")
 
 
-def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int):
-    """Create the emulated BPF ring and the two user-space rings (the agent owns them)."""
+def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int, user_rec: int = 32):
+    """Create the emulated BPF ring and the two user-space rings (the agent owns them). The
+    user-space ring holds ``user_rec``-byte records: 32 = USER32 (what the rocprofiler tool
+    writes into such a ring, half the PCIe bytes of a 64-byte EVENT)."""
     from ..runtime import load
 
     rt = load()
     pow2 = lambda n: 1 << max(12, int(np.ceil(np.log2(max(1, n)))))  # noqa: E731
-    return (rt.Ringbuf.create_shm(names.ring, pow2(ring_bytes)), rt.HostRing(pow2(user_records), 64, names.user),
+    return (rt.Ringbuf.create_shm(names.ring, pow2(ring_bytes)),
+            rt.HostRing(pow2(user_records), int(user_rec), names.user),
             rt.HostRing(pow2(span_records), 64, names.spans))
 
 
@@ -207,8 +210,10 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
     parts = []
     for w in wins:
         km = kernel_event_mask(w.events)
-        parts.append((np.ascontiguousarray(w.events[km]), np.ascontiguousarray(w.events[~km]),
-                      np.ascontiguousarray(w.spans)))
+        uev = np.ascontiguousarray(w.events[~km])
+        if user.rec_size == 32:  # the agent created a USER32 ring: write what the rocprof tool would
+            uev = records.to_user32(uev)
+        parts.append((np.ascontiguousarray(w.events[km]), uev, np.ascontiguousarray(w.spans)))
     if ready is not None:
         ready.send(True)
     period = window_ms / 1000.0
