@@ -64,8 +64,9 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("halo-ms", d.halo_ms, "gpu engine: records this close to a window's end also join the next window (0 = off)"),
         ("state-dir", d.state_dir, "gpu engine: checkpoint directory for the learned state (resumed on start)"),
         ("checkpoint-every", d.checkpoint_every, "gpu engine: windows between checkpoints"),
-        ("gpu-hw-queues", 0, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; each MI355X queue pins "
-                             "~173 MB of host memory; 0 = runtime default)"),
+        ("gpu-hw-queues", 2, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; each MI355X queue pins "
+                             "~173 MB of host memory; 2 serialises copy and compute, ample at node event rates; "
+                             "0 = runtime default)"),
     ]:
         p.flag(name, default, help_)
     a = p.parse_args(argv)

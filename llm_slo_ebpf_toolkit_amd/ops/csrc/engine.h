@@ -243,7 +243,7 @@ class WindowEngine {
   int32_t* pred_ = nullptr;
   uint32_t* evbits_ = nullptr;
   // events
-  std::vector<hipEvent_t> h2d_done_, h2d_part_, compute_done_, comm_done_;
+  std::vector<hipEvent_t> h2d_done_, h2d_part_, head_done_, compute_done_, comm_done_;
   std::vector<hipEvent_t> t_start_, t_copy_end_, t_comp0_, t_comp1_, t_end_;
   std::map<std::tuple<int, int, bool, bool>, hipGraphExec_t> graphs_;
   std::vector<bool> warm_;

@@ -198,6 +198,7 @@ void WindowEngine::alloc() {
     packet_host_.push_back(static_cast<double*>(host_block(kPacketLen * sizeof(double))));
     h2d_done_.push_back(mk_event(false));
     h2d_part_.push_back(mk_event(false));
+    head_done_.push_back(mk_event(false));
     compute_done_.push_back(mk_event(false));
     comm_done_.push_back(mk_event(false));
     t_start_.push_back(mk_event(true));
@@ -304,7 +305,7 @@ WindowEngine::~WindowEngine() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   for (auto g : graph_defs_) hipGraphDestroy(g);
   if (comm_) ncclCommDestroy(comm_);
-  auto evs = {&t_copy_end_, &h2d_done_, &h2d_part_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
+  auto evs = {&t_copy_end_, &h2d_done_, &h2d_part_, &head_done_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
   for (auto* v : evs)
     for (auto e : *v) hipEventDestroy(e);
   for (auto& r : registered_) hipHostUnregister(const_cast<uint8_t*>(r.first));
@@ -553,6 +554,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   if (k >= nb_) {
     HIPCHECK(hipEventSynchronize(h2d_done_[b]));
     HIPCHECK(hipEventSynchronize(h2d_part_[b]));
+    HIPCHECK(hipEventSynchronize(head_done_[b]));
   }
   wait_us_ += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
   const auto td = std::chrono::steady_clock::now();
@@ -572,9 +574,9 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   c[15] = (int32_t)n_k;
   int32_t* lab = reinterpret_cast<int32_t*>(head_host_[b] + kHeadBytes);
   for (int g = 0; g < cfg_.group_cap; ++g) lab[g] = (in.labels && g < n_groups) ? in.labels[g] : -1;
-  // DMAs once window k - nb (the device block's previous reader) computed: the head, the BPF
-  // ring's bytes, the user-space records and the spans, back to back on the copy stream (or
-  // over two streams with MISLO_COPY_STREAMS=2).
+  // DMAs once window k - nb (the device block's previous reader) computed: the BPF ring's
+  // bytes, the user-space records and the spans, back to back on the copy stream (or over two
+  // streams with MISLO_COPY_STREAMS=2); the head is loaded on the compute stream (below).
   HIPCHECK(hipStreamWaitEvent(copy_, compute_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(copy2_, compute_done_[b], 0));
   HIPCHECK(hipEventRecord(t_start_[b], copy_));
@@ -588,10 +590,6 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   auto tq = std::chrono::steady_clock::now();
   dma(in.kernel, dst + off_kern_, (size_t)kRecStride * cfg_.sig_cap, staging_[b], st_off, copy_);
   lap(tq, split_us_[0]);
-  // the head (counts, epoch bases, labels: < 1 KiB) by a kernel load from pinned host memory:
-  // a small hipMemcpyAsync H2D is written by the host through the BAR once the stream reaches
-  // it, blocking this thread behind the stream's wait (window k - nb's compute)
-  to_host(head_host_[b], dst, off_kern_, copy2_);
   lap(tq, split_us_[1]);
   dma(in.user, dst + off_user_, 64 * (size_t)cfg_.user_cap, staging_[b], st_off, copy2_);
   lap(tq, split_us_[2]);
@@ -606,6 +604,12 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_part_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
   HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
+  // the head (counts, epoch bases, labels: < 1 KiB) by a kernel load from pinned host memory on
+  // the compute stream: a small hipMemcpyAsync H2D is written by the host through the BAR and
+  // blocks this thread, and a kernel on the copy stream put ~25 us of queue hand-offs between
+  // the window's DMAs (measured); the compute stream has the slack
+  to_host(head_host_[b], dst, off_kern_, compute_);
+  HIPCHECK(hipEventRecord(head_done_[b], compute_));
   if (cfg_.device_refit && k >= nb_) {
     // fold window k - nb's all-reduced statistics (packet b) and refit before window k: a
     // deterministic prequential lag of nb, identical on every rank
