@@ -171,9 +171,26 @@ def main() -> int:
     rt = load()
     tag = f"/mislo-bench-{os.getpid()}"
     names = {"ring": tag + "-ev", "user": tag + "-user", "spans": tag + "-sp", "cuts": tag + "-cut"}
-    rb = rt.Ringbuf.create_shm(names["ring"], a.ring_mib << 20)
-    user_cap = 1 << max(12, int(np.ceil(np.log2(max(1, len(imgs[0].user)) * 24))))
-    user = rt.HostRing(user_cap, a.user_rec, names["user"])
+    def shrinking(make, size, floor):
+        # /dev/shm may be smaller than the rings asked for (e.g. 8 ranks on a node): halve down
+        # to two windows' worth; the producer then runs less far ahead of the timed region
+        while True:
+            try:
+                return make(size), size
+            except RuntimeError:
+                if size // 2 < floor:
+                    raise
+                size //= 2
+
+    win_bytes = max(len(i.framed) for i in imgs + himgs)
+    rb, ring_bytes = shrinking(lambda s: rt.Ringbuf.create_shm(names["ring"], s), a.ring_mib << 20,
+                               1 << int(np.ceil(np.log2(2 * win_bytes))))
+    if ring_bytes != a.ring_mib << 20:
+        log(f"note: BPF ring reduced to {ring_bytes >> 20} MiB (shared memory)")
+    n_user = max(1, max(len(i.user) for i in imgs + himgs))
+    user_cap = 1 << max(12, int(np.ceil(np.log2(n_user * 24))))
+    user, _ = shrinking(lambda c: rt.HostRing(c, a.user_rec, names["user"]), user_cap,
+                        1 << int(np.ceil(np.log2(2 * n_user))))
     spans = rt.HostRing(1 << max(12, int(np.ceil(np.log2(a.spans * 24)))), 64, names["spans"])
     cuts = rt.HostRing(1 << 12, 64, names["cuts"])
     n_flat = a.warmup + a.steps

@@ -3,6 +3,7 @@
 // record on a goroutine, decoded on the CPU); here a window's records move as one compaction
 // into DMA-able memory and are decoded on the GPU (ops/csrc/decode.hip k_decode_wire).
 #include "bpfring.h"
+#include "ring.h"
 
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -79,10 +80,11 @@ std::unique_ptr<Ringbuf> Ringbuf::create_shm(const std::string& name, uint64_t s
   if (!pow2(size) || size % page) throw std::invalid_argument("ringbuf size must be a power-of-two page multiple");
   int fd = shm_open(name.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600);
   if (fd < 0) throw std::runtime_error("shm_open " + name + " failed");
-  if (ftruncate(fd, (off_t)(3 * page + size)) != 0) {
+  if (ftruncate(fd, (off_t)(3 * page + size)) != 0 || !mislo_shm_reserve(fd, 3 * page + size)) {
     close(fd);
     shm_unlink(name.c_str());
-    throw std::runtime_error("ftruncate " + name + " failed");
+    throw std::runtime_error("cannot reserve " + std::to_string(3 * page + size) + " bytes of shared memory for " +
+                             name + " (/dev/shm too small?)");
   }
   uint8_t* b = map_double(fd, page, size, true);
   if (!b) {

@@ -137,12 +137,20 @@ struct ShmRing {
 
 extern "C" {
 
+bool mislo_shm_reserve(int fd, size_t bytes) {
+  const int e = posix_fallocate(fd, 0, (off_t)bytes);
+  return e == 0 || e == EOPNOTSUPP || e == EINVAL;  // filesystems without fallocate: as before
+}
+
 void* mislo_ring_create_shm(const char* name, uint64_t capacity, uint32_t rec_size) {
   const size_t bytes = Ring::bytes_for(capacity, rec_size);
   int fd = shm_open(name, O_CREAT | O_RDWR | O_TRUNC, 0600);
   if (fd < 0) return nullptr;
-  if (ftruncate(fd, (off_t)bytes) != 0) {
+  // reserve the pages now: a tmpfs (/dev/shm) too small for a sparse ftruncate'd ring fails
+  // here with ENOSPC instead of SIGBUS-ing the first producer that touches a missing page
+  if (ftruncate(fd, (off_t)bytes) != 0 || !mislo_shm_reserve(fd, bytes)) {
     close(fd);
+    shm_unlink(name);
     return nullptr;
   }
   void* base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
