@@ -376,10 +376,10 @@ def main() -> int:
                              "incidents": int(cm.sum()), "confusion": cm.tolist()}
 
     # ---- REF 55-row dataset through the GPU posterior kernel --------------------------------
-    ref_f1 = {}
+    ref_f1, ref_multi = {}, {}
     fx = os.path.join(ROOT, "tests", "fixtures", "ref_multi_fault_samples.jsonl")
     if rank == 0 and os.path.exists(fx):
-        ref_f1 = ref55_gpu(fx, pipe.host_model(), a.model)
+        ref_f1, ref_multi = ref55_gpu(fx, pipe.host_model(), a.model)
     prod.join(timeout=30)
     src.drain()
 
@@ -421,6 +421,7 @@ def main() -> int:
         "vs_baseline_macro_f1_heldout": round(heldout["mixed"]["macro_f1"] / BASELINE_MACRO_F1, 4)
         if "mixed" in heldout else None,
         "ref55_single_fault_macro_f1": {k: round(v, 4) for k, v in ref_f1.items()},
+        "ref55_multi_fault": ref_multi,
         "vs_baseline_ref55_macro_f1": round(ref_f1[a.model] / BASELINE_MACRO_F1, 4) if a.model in ref_f1 else None,
         "macro_f1_prequential": round(summ["macro_f1"], 4),
         "incidents_scored_prequential": int(conf.sum()),
@@ -472,7 +473,8 @@ def rt_uid() -> bytes:
 
 def ref55_gpu(fx: str, learned, model_name: str):
     """REF's 55-row attribution set through the GPU posterior kernel (torch test engine), with
-    REF's model and with the learned model; macro-F1 over the 30 single-fault rows."""
+    REF's model and with the learned model: macro-F1 over the 30 single-fault rows, and REF's
+    partial / coverage@0.10 accuracy over the 25 multi-fault rows (1.000 / 0.667)."""
     import numpy as np
     import torch
 
@@ -481,18 +483,35 @@ def ref55_gpu(fx: str, learned, model_name: str):
     from llm_slo_ebpf_toolkit_amd.ops.engine import GpuEngine
     from llm_slo_ebpf_toolkit_amd.signals import catalog
 
-    samples = [s for s in load_samples_jsonl(fx) if s.expected_domain]
-    vals, labels = samples_to_arrays(samples)
+    rows = load_samples_jsonl(fx)
+    samples = [s for s in rows if s.expected_domain]
+    multi = [s for s in rows if not s.expected_domain and s.expected_domains]
     eng = GpuEngine(64, 64, 64)
-    out = {}
-    for name, model in (("bayes_ref", NaiveBayes.ref()), (model_name, learned)):
+    out, multi_out = {}, {}
+    D = len(catalog.ALL_DOMAINS)
+
+    def run(model, group):
+        vals, labels = samples_to_arrays(group)
         eng.set_model(model)
-        eng.eng.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
-        eng.eng.counts[:4].copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
+        eng.eng.feat[: len(group)].copy_(torch.from_numpy(vals.astype(np.float32)))
+        eng.eng.counts[:4].copy_(torch.tensor([0, 0, len(group), 0], dtype=torch.int32))
         eng.eng.posterior(False)
-        pred = eng.eng.pred[: len(samples)].cpu().numpy()
+        return labels, eng.eng.pred[: len(group)].cpu().numpy(), eng.eng.post[: len(group), :D].cpu().numpy()
+
+    for name, model in (("bayes_ref", NaiveBayes.ref()), (model_name, learned)):
+        labels, pred, _ = run(model, samples)
         out[name] = macro_f1([catalog.ALL_DOMAINS[i] for i in labels], [catalog.ALL_DOMAINS[i] for i in pred])
-    return out
+        if multi:
+            _, pred, post = run(model, multi)
+            part = cov = 0.0
+            for s, p, row in zip(multi, pred, post):
+                exp = set(s.expected_set())
+                hyp = {catalog.ALL_DOMAINS[d] for d in np.flatnonzero(row >= 0.10)} | {catalog.ALL_DOMAINS[p]}
+                part += catalog.ALL_DOMAINS[p] in exp
+                cov += len(exp & hyp) / len(exp)
+            multi_out[name] = {"partial_accuracy": round(part / len(multi), 4),
+                               "coverage_accuracy": round(cov / len(multi), 4), "rows": len(multi)}
+    return out, multi_out
 
 
 if __name__ == "__main__":
