@@ -182,16 +182,20 @@ def main() -> int:
                     raise
                 size //= 2
 
+    # the rings hold every window of the run (the producer writes them all before the timed
+    # region, so any --steps measures the consume path, not the replay harness), up to 64 GiB
+    pow2 = lambda n: 1 << max(12, int(np.ceil(np.log2(max(1, n)))))  # noqa: E731
+    n_win = a.warmup + a.steps + a.paced_windows + a.heldout + 2
     win_bytes = max(len(i.framed) for i in imgs + himgs)
-    rb, ring_bytes = shrinking(lambda s: rt.Ringbuf.create_shm(names["ring"], s), a.ring_mib << 20,
-                               1 << int(np.ceil(np.log2(2 * win_bytes))))
-    if ring_bytes != a.ring_mib << 20:
+    want = max(a.ring_mib << 20, min(64 << 30, pow2(n_win * win_bytes)))
+    rb, ring_bytes = shrinking(lambda s: rt.Ringbuf.create_shm(names["ring"], s), want, pow2(2 * win_bytes))
+    if ring_bytes != want:
         log(f"note: BPF ring reduced to {ring_bytes >> 20} MiB (shared memory)")
     n_user = max(1, max(len(i.user) for i in imgs + himgs))
-    user_cap = 1 << max(12, int(np.ceil(np.log2(n_user * 24))))
-    user, _ = shrinking(lambda c: rt.HostRing(c, a.user_rec, names["user"]), user_cap,
-                        1 << int(np.ceil(np.log2(2 * n_user))))
-    spans = rt.HostRing(1 << max(12, int(np.ceil(np.log2(a.spans * 24)))), 64, names["spans"])
+    user, _ = shrinking(lambda c: rt.HostRing(c, a.user_rec, names["user"]), pow2(max(24, n_win) * n_user),
+                        pow2(2 * n_user))
+    spans, _ = shrinking(lambda c: rt.HostRing(c, 64, names["spans"]), pow2(max(24, n_win) * a.spans),
+                         pow2(2 * a.spans))
     cuts = rt.HostRing(1 << 12, 64, names["cuts"])
     n_flat = a.warmup + a.steps
     period = a.events / 1e6  # 1M events/s per node agent (config 5)
@@ -269,11 +273,11 @@ def main() -> int:
     wait_s[0] = 0.0
 
     # ---- timed region ----------------------------------------------------------------------
-    # The replay producer stands in for the probes writing the rings; it copies ~34 MB per
+    # The replay producer stands in for the probes writing the rings; it copies ~28 MB per
     # window with a few CPU threads, which on a busy host is slower than the GPU path. Let it
-    # run ahead first (rings hold 20+ windows) so the timed region measures the agent's
-    # consume path -- DMA, decode, join, posterior -- not the replay harness; any wait for it
-    # that remains is reported as producer_wait_ms_total.
+    # run ahead first (the rings are sized for every window of the run) so the timed region
+    # measures the agent's consume path -- DMA, decode, join, posterior -- not the replay
+    # harness; any wait for it that remains is reported as producer_wait_ms_total.
     t_fill = time.perf_counter()
     last, last_t = -1, time.perf_counter()
     while cuts.size < a.steps and time.perf_counter() - t_fill < 60:
