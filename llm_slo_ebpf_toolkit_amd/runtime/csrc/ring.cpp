@@ -7,6 +7,7 @@
 #include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/statvfs.h>
 #include <unistd.h>
 
 #include <cstring>
@@ -138,16 +139,19 @@ struct ShmRing {
 extern "C" {
 
 bool mislo_shm_reserve(int fd, size_t bytes) {
-  const int e = posix_fallocate(fd, 0, (off_t)bytes);
-  return e == 0 || e == EOPNOTSUPP || e == EINVAL;  // filesystems without fallocate: as before
+  // a capacity check, not an allocation: the pages stay unallocated so that the first process
+  // to touch them -- the producer, bound to its GPU's NUMA node -- places them (first touch)
+  struct statvfs sv;
+  if (fstatvfs(fd, &sv) != 0) return true;  // cannot tell: as before
+  return (unsigned long long)sv.f_bavail * sv.f_frsize >= bytes;
 }
 
 void* mislo_ring_create_shm(const char* name, uint64_t capacity, uint32_t rec_size) {
   const size_t bytes = Ring::bytes_for(capacity, rec_size);
   int fd = shm_open(name, O_CREAT | O_RDWR | O_TRUNC, 0600);
   if (fd < 0) return nullptr;
-  // reserve the pages now: a tmpfs (/dev/shm) too small for a sparse ftruncate'd ring fails
-  // here with ENOSPC instead of SIGBUS-ing the first producer that touches a missing page
+  // a tmpfs (/dev/shm) too small for a sparse ftruncate'd ring fails here, instead of SIGBUS-ing
+  // the first producer that touches a page it cannot back
   if (ftruncate(fd, (off_t)bytes) != 0 || !mislo_shm_reserve(fd, bytes)) {
     close(fd);
     shm_unlink(name);

@@ -76,7 +76,7 @@ class Ring {
 
 extern "C" {
 // C ABI for external producers (BPF loader, rocprofiler-sdk tool library) and tests.
-// Reserves a shared-memory file's pages (posix_fallocate): false when the tmpfs is too small.
+// Whether a shared-memory file's filesystem has room for `bytes` (false: a tmpfs too small).
 bool mislo_shm_reserve(int fd, size_t bytes);
 void* mislo_ring_create_shm(const char* name, uint64_t capacity, uint32_t rec_size);
 void* mislo_ring_open_shm(const char* name);
