@@ -141,3 +141,25 @@ def test_confusion_and_macro_f1_helpers():
     assert conf.tolist() == [[1, 1, 0], [0, 1, 0], [0, 0, 1]]
     assert models.macro_f1_from_confusion(conf) == pytest.approx(models.macro_f1(["a", "a", "b", "c"],
                                                                                   ["a", "b", "b", "c"]))
+
+
+def test_bayes_gpu_names_gpu_domains_and_keeps_ref_rows():
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    m = NaiveBayes.gpu()
+    v = np.full((1, catalog.N_SLOTS), np.nan)
+    v[0, catalog.BY_NAME["gpu_queue_delay_ms"].slot] = 5.0
+    top = m.attribute({"gpu_queue_delay_ms": 5.0})[0]
+    assert top.domain == "gpu_contention" and "gpu_queue_delay_ms" in top.evidence
+    assert m.attribute({"rccl_collective_ms": 30.0, "xgmi_link_latency_us": 60.0})[0].domain == "gpu_interconnect"
+    assert m.attribute({"dns_latency_ms": 300.0})[0].domain == "network_dns"
+    # REF's rows over REF's domains are REF's table
+    ref = NaiveBayes.ref()
+    for s in catalog.REF_DOMAINS:
+        d = catalog.DOMAIN_INDEX[s]
+        for name in catalog.SIGNAL_NAMES[:12]:
+            slot = catalog.BY_NAME[name].slot
+            assert m.weights[slot, d] == ref.weights[slot, d]

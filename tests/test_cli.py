@@ -169,3 +169,22 @@ def test_agent_synthetic_count(tmp_path):
     probe = [r for r in rows if "signal" in r]
     assert len(slo) == 12 and len(probe) == 3 * 9
     assert agent.main(["--event-kind", "weird", "--metrics-bind", ""]) == 1
+
+
+def test_agent_metrics_export_gpu_signal_histograms():
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.agent.metrics import AgentMetrics
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    m = AgentMetrics("both", "gpu", catalog.SIGNAL_NAMES, catalog.SIGNAL_NAMES)
+    hist = np.zeros((16, 16), dtype=np.uint32)
+    slot = catalog.BY_NAME["gpu_queue_delay_ms"].slot
+    hist[slot, 2] = 7  # le 5 ms
+    sums = np.zeros(16, dtype=np.int64)
+    sums[slot] = 7 * 4000  # 7 x 4 ms, in 1/1000 ms
+    m.observe_window(hist, np.zeros((16, 3), dtype=np.uint32), np.zeros(8, dtype=np.int64), 7, 1.0, "n", "p", "ns",
+                     value_sums_milli=sums)
+    text = m.registry.exposition() if hasattr(m, "registry") else m.r.exposition()
+    assert 'llm_ebpf_gpu_queue_delay_ms_bucket{le="5"} 7' in text
+    assert "llm_ebpf_gpu_queue_delay_ms_sum 28" in text

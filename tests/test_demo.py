@@ -76,3 +76,40 @@ def test_burn_rate_window():
         b.observe(True, now=i * 0.01)
     assert b.observe(False, now=1.0) == pytest.approx(1.0)
     assert b.observe(True, now=100.0) == 0.0  # old events aged out
+
+
+def test_span_exporter_flushes_on_its_schedule():
+    """A partial batch goes out after max_delay_s (spans must reach the agent's windows promptly)."""
+    import http.server
+    import threading
+    import time
+
+    got = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_POST(self):  # noqa: N802
+            got.append(json.loads(self.rfile.read(int(self.headers["Content-Length"]))))
+            self.send_response(200)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        ex = rs.SpanExporter(f"http://127.0.0.1:{srv.server_port}/v1/traces", max_batch=64, max_delay_s=0.05)
+        ex.add([rs.SpanExporter.span("0af7651916cd43dd8448eb211c80319c", "b7ad6b7169203331", "", "chat.request",
+                                     1, 2, {})])
+        deadline = time.time() + 5
+        while not got and time.time() < deadline:
+            time.sleep(0.02)
+        assert got and got[0]["resourceSpans"][0]["scopeSpans"][0]["spans"][0]["name"] == "chat.request"
+    finally:
+        srv.shutdown()
+
+
+def test_gpu_trace_tag_is_a_noop_without_the_tool():
+    tag = rs.GpuTraceTag()
+    assert not tag.active
+    tag.set("0af7651916cd43dd8448eb211c80319c")  # must not raise
