@@ -183,11 +183,11 @@ def main() -> int:
                 size //= 2
 
     # the rings hold every window of the run (the producer writes them all before the timed
-    # region, so any --steps measures the consume path, not the replay harness), up to 64 GiB
+    # region, so any --steps measures the consume path, not the replay harness), up to 8 GiB
     pow2 = lambda n: 1 << max(12, int(np.ceil(np.log2(max(1, n)))))  # noqa: E731
     n_win = a.warmup + a.steps + a.paced_windows + a.heldout + 2
     win_bytes = max(len(i.framed) for i in imgs + himgs)
-    want = max(a.ring_mib << 20, min(64 << 30, pow2(n_win * win_bytes)))
+    want = max(a.ring_mib << 20, min(8 << 30, pow2(n_win * win_bytes)))
     rb, ring_bytes = shrinking(lambda s: rt.Ringbuf.create_shm(names["ring"], s), want, pow2(2 * win_bytes))
     if ring_bytes != want:
         log(f"note: BPF ring reduced to {ring_bytes >> 20} MiB (shared memory)")
