@@ -157,6 +157,7 @@ class AgentOptions:
     source: str = "replay"               # bpf | shm | replay
     ring_name: str = "/mislo-agent"
     pin_dir: str = "/sys/fs/bpf/mislo"
+    probe_objs: str = ""  # --source bpf: compiled probes to load + attach (empty: loaded externally)
     window_ms: int = 1000
     window_events: int = 1 << 20
     window_spans: int = 16384
@@ -330,7 +331,12 @@ class Agent:
             return
         self.metrics.set_cpu_overhead(pct)
         if exceeded:
-            sig = self.generator.disable_highest_cost()
+            pm = getattr(self, "probe_manager", None)
+            sig = pm.shed_next() if pm is not None else None  # really detach a kernel probe
+            if pm is not None and sig:
+                self.generator.disable(sig)
+            else:
+                sig = self.generator.disable_highest_cost()
             if sig:
                 print(f"overhead budget exceeded: disabled signal {sig}", file=sys.stderr)
                 self.metrics.set_enabled_signals(self.supported, self.generator.enabled_signals())
@@ -367,6 +373,15 @@ class Agent:
         rt = load()
         names = bpf.RingNames.of(o.ring_name)
         if o.source == "bpf":
+            if o.probe_objs:  # load + attach the compiled probes; their shared maps get pinned
+                from ..collector.loader import BpfProbeLoader, probe_specs
+                from ..collector.probes import ProbeManager
+
+                self.probe_manager = ProbeManager(self.mode, self.generator.enabled_signals())
+                for spec in probe_specs(BpfProbeLoader(o.probe_objs, o.pin_dir), self.generator.enabled_signals()):
+                    self.probe_manager.register(spec)
+                attached = self.probe_manager.attach_all()
+                print(f"attached probes for {len(attached)} signals from {o.probe_objs}", file=sys.stderr)
             maps = bpf.BpfMaps(o.pin_dir)
             user = rt.HostRing(1 << 20, 32, names.user)   # the rocprofiler tool attaches, pushes USER32
             spans = rt.HostRing(1 << 18, 64, names.spans)  # OTLP receiver / services
@@ -549,6 +564,8 @@ class Agent:
             pipe.eng.close()
             if receiver is not None:
                 receiver.stop()
+            if getattr(self, "probe_manager", None) is not None:
+                self.probe_manager.detach_all()
             if getattr(self, "_producer", None) is not None:
                 self._producer.terminate()
                 self._producer.join(5)

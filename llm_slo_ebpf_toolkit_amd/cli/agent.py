@@ -51,6 +51,9 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("source", d.source, "gpu engine record source: bpf (pinned probe maps) | shm (emulated rings) | replay"),
         ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
         ("pin-dir", d.pin_dir, "bpffs directory the probe loader pinned the maps in (--source bpf)"),
+        ("probe-objs", d.probe_objs, "--source bpf: directory of compiled probes (*.bpf.o) the agent loads and "
+                                     "attaches with bpftool, pinning their shared maps in --pin-dir "
+                                     "(empty: an external loader did)"),
         ("window-ms", d.window_ms, "gpu engine window length"),
         ("window-events", d.window_events, "gpu engine events per window (capacity)"),
         ("window-spans", d.window_spans, "gpu engine spans per window (capacity)"),
@@ -80,6 +83,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         disable_overhead_guard=a.disable_overhead_guard, config=a.config, enable_hello_tracer=a.enable_hello_tracer,
         hello_target_comm=split_csv(a.hello_target_comm), enable_real_probe_metrics=a.enable_real_probe_metrics,
         metrics_bind=a.metrics_bind, engine=a.engine, source=a.source, ring_name=a.ring_name, pin_dir=a.pin_dir,
+        probe_objs=a.probe_objs,
         window_ms=a.window_ms, window_events=a.window_events, window_spans=a.window_spans,
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,

@@ -108,6 +108,10 @@ class ProbeManager:
         if not exceeded:
             return None
         log.warning("overhead %.2f%% exceeds budget, disabling highest-cost probe", pct)
+        return self.shed_next()
+
+    def shed_next(self) -> Optional[str]:
+        """Detach the next enabled probe in disable order (REF disableHighestCostProbe)."""
         with self._lock:
             for sig in self.disable_order:
                 spec = self._probes.pop(sig, None)
