@@ -227,6 +227,11 @@ class Agent:
         self.ready = False
         self.windows_done = 0
         self.pod_ids = Interner()  # pod uid -> pod id (cgroup map and OTLP spans)
+        # per-group SLO burn forecast over the next 5 minutes of windows, scored as it matures
+        from ..evaluation.slo import BurnRateForecaster
+
+        self.burn = BurnRateForecaster(opts.slo_target, horizon=max(1, int(round(300_000 / max(opts.window_ms, 1)))),
+                                       short=max(1, int(round(30_000 / max(opts.window_ms, 1)))))
         self.receiver = None
         self.attributions_emitted = 0
 
@@ -424,12 +429,19 @@ class Agent:
     def _attributions(self, G: int, names: Sequence[str], res: dict, t_ns: int, model) -> List[IncidentAttribution]:
         """One IncidentAttribution per incident group whose top posterior clears min_confidence.
         Evidence carries the group's measured signal values (mean over joined kernel signals);
-        SLO impact comes from the group's spans in the window (TTFT SLO breach fraction over the
-        error budget = burn rate), not from constants."""
+        SLO impact comes from the group's spans (TTFT SLO breach fraction over the error budget =
+        burn rate, forecast over the next 5 minutes from the recent windows), not from constants."""
         out = []
         D = model.weights.shape[1]
         post, bits, feat = res["post"], res["evbits"].view(np.uint32), res["feat"]
         sli = res.get("sli")
+        forecast = {}
+        if sli is not None:
+            for g in range(min(G, sli.shape[0])):
+                forecast[g] = self.burn.observe(names[g] if g < len(names) else g, float(sli[g, 0]), float(sli[g, 1]))
+            err = self.burn.error()
+            if err is not None:
+                self.metrics.burn_err.set(err)
         for g in range(G):
             if sli is not None and g < sli.shape[0] and sli[g, 0] == 0:
                 continue  # no request of this group in the window: no incident to attribute
@@ -444,9 +456,7 @@ class Agent:
                 ev.append(Evidence(spec.semconv or sname, round(v, 3) if np.isfinite(v) else "elevated", "ebpf"))
             if not ev:
                 ev = [Evidence("llm.ebpf.correlation_confidence", float(top.posterior), "ebpf")]
-            n, breach = (sli[g, 0], sli[g, 1]) if sli is not None and g < sli.shape[0] else (0.0, 0.0)
-            budget = max(1e-6, 1.0 - self.o.slo_target)
-            burn = float(breach / n / budget) if n else 0.0
+            burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
             out.append(IncidentAttribution(
                 incident_id=f"gpu-{t_ns}-{g:03d}", timestamp=t_ns, cluster=self.o.cluster,
                 namespace=self.o.namespace, service=names[g] if g < len(names) else f"group-{g}",

@@ -64,6 +64,8 @@ class AgentMetrics:
         self.ring_backlog = r.gauge("llm_slo_agent_ring_backlog_bytes", "Unconsumed bytes in the BPF ring buffer.")
         self.host_us = r.gauge("llm_slo_agent_window_host_us", "Host time to assemble the last window (us).")
         self.rss = r.gauge("llm_slo_agent_memory_rss_bytes", "Agent process resident set size (bytes).")
+        self.burn_err = r.gauge("llm_slo_agent_burn_rate_prediction_error",
+                                "Mean relative error of the scored SLO burn-rate forecasts.")
         # GPU signals' value distributions (the window histograms the decode kernel builds)
         self.gpu_hist = {s.slot: r.histogram(f"llm_ebpf_{s.name}", f"{s.name} values observed from GPU signal records.",
                                              s.buckets)

@@ -101,3 +101,35 @@ def test_kfd_topology_parse(tmp_path):
     (tmp_path / "0").mkdir()
     (tmp_path / "0" / "properties").write_text("cpu_cores_count 64\ngfx_target_version 0\n")
     assert prereq.kfd_gfx_targets(str(tmp_path)) == ["gfx950"]
+
+
+def test_burn_rate_forecaster_scores_matured_forecasts():
+    fc = slo.BurnRateForecaster(target=0.99, horizon=3, short=2, min_requests=100)
+    # steady 2 % breaches = burn 2.0: every forecast matches what is realised
+    for _ in range(10):
+        f = fc.observe("svc", 100, 2)
+    assert f == pytest.approx(2.0)
+    assert fc.alert("svc") == pytest.approx(2.0)
+    assert fc.error() == pytest.approx(0.0)
+    # a step to 4 %: the forecasts made before the step miss by the realised burn's change
+    fc2 = slo.BurnRateForecaster(target=0.99, horizon=2, short=1, min_requests=1)
+    for b in (1, 1, 3, 3, 3):
+        fc2.observe("a", 100, b)
+    # forecast at t=0 (1.0) vs realised over t=1..2 (2/200/.01 = 2.0): 0.5; at t=1 (1.0) vs
+    # t=2..3 (3.0): 2/3; at t=2 (3.0) vs t=3..4 (3.0): 0
+    assert fc2.error() == pytest.approx((0.5 + 2 / 3 + 0.0) / 3)
+    with pytest.raises(ValueError):
+        slo.BurnRateForecaster(target=1.0)
+
+
+def test_burn_rate_forecaster_bounded_history():
+    fc = slo.BurnRateForecaster(target=0.99, horizon=5, short=3, min_requests=10)
+    for _ in range(2000):
+        fc.observe("k", 10, 0, forecast=False)
+    assert len(fc._hist["k"]) < 100
+
+
+def test_simulated_burn_prediction_error_is_measured():
+    e = slo.simulate_burn_prediction_error([2.0] * 4, horizon=60, short=10, seed=1)
+    assert 0.0 < e < 0.5
+    assert slo.simulate_burn_prediction_error([2.0] * 4, horizon=60, short=10, seed=1) == e  # seeded
