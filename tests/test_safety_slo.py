@@ -133,3 +133,32 @@ def test_simulated_burn_prediction_error_is_measured():
     e = slo.simulate_burn_prediction_error([2.0] * 4, horizon=60, short=10, seed=1)
     assert 0.0 < e < 0.5
     assert slo.simulate_burn_prediction_error([2.0] * 4, horizon=60, short=10, seed=1) == e  # seeded
+
+
+def test_agent_attributions_carry_the_burn_forecast(tmp_path):
+    """The GPU engine's per-group results -> IncidentAttributions: the SLO impact is the
+    forecaster's burn from the group's measured request / breach counts, and groups with no
+    requests in the window are skipped."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    o = AgentOptions(output="jsonl", output_path=str(tmp_path / "a.jsonl"), window_ms=1000, slo_target=0.99,
+                     min_confidence=0.0)
+    agent = Agent(o)
+    model = NaiveBayes.ref()
+    D = model.weights.shape[1]
+    G = 3
+    post = np.zeros((G, 16))
+    post[:, 0] = 0.9
+    post[:, 1:D] = 0.1 / (D - 1)
+    res = {"post": post, "evbits": np.zeros((G, 16), dtype=np.uint32), "feat": np.zeros((G, 16), dtype=np.float32),
+           "sli": np.array([[100, 4], [0, 0], [200, 2]], dtype=np.uint32)}
+    out = agent._attributions(G, ["a", "b", "c"], res, 1, model)
+    assert [x.service for x in out] == ["a", "c"]
+    assert out[0].predicted_fault_domain == catalog.ALL_DOMAINS[0]
+    assert out[0].slo_impact.burn_rate == pytest.approx(4.0)  # 4 % breaches / 1 % budget
+    assert out[1].slo_impact.burn_rate == pytest.approx(1.0)
+    assert agent.burn.error() is None  # no forecast has matured yet (5-minute horizon)
