@@ -1,14 +1,14 @@
-"""Two-rank RCCL probe of the window engine's data plane on ONE GPU.
+"""Two-rank RCCL probe of the window engine's data plane.
 
-Both ranks place their engine on device 0 and build one RCCL communicator (the engine's own,
-``WindowEngine::init_comm``). Each rank runs its node shard of the same replay windows through
+Rank r places its engine on device r mod #GPUs and the two build one RCCL communicator (the
+engine's own, ``WindowEngine::init_comm``). Each rank runs its node shard of the same replay windows through
 the BPF-ring path with the in-window trace-row all-gather enabled, then checks what RCCL
 delivered:
 * the packet all-reduce: both ranks hold identical node-wide totals, and the confusion matrix
   counts every incident of both shards;
 * the incident all-gather: rank r's slice of the gathered results equals rank r's own results.
-RCCL may refuse two ranks on one device (``ncclInvalidUsage``); the probe then reports that
-and exits 3, so the result says which it was. The multi-GPU scaling run itself belongs to
+On a one-GPU box RCCL refuses two ranks on one device (``ncclInvalidUsage``, measured:
+profiles/r2_rccl_pair_one_gpu.log); the probe then reports that and exits 3. The multi-GPU scaling run itself belongs to
 the driver (bench.py under torch.distributed.run).
 
 usage: python tools/rccl_pair_probe.py [--windows 4]
@@ -51,7 +51,10 @@ def rank_main(rank, world, uq, n_win, q):
         sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs)
         user_cap = 1 << int(np.ceil(np.log2(max(len(i.user) for i in imgs))))
         xchg = 4096
-        pipe = WindowPipeline(sig_cap, 2048, 16, 0, (uid, rank, world), model="bayes_learned",
+        import torch
+
+        dev = rank % max(1, torch.cuda.device_count())  # one GPU per rank where there are enough
+        pipe = WindowPipeline(sig_cap, 2048, 16, dev, (uid, rank, world), model="bayes_learned",
                               user_cap=min(user_cap, sig_cap), import_cap=(world - 1) * xchg, xchg_cap=xchg)
         pods = np.unique(np.concatenate([w.events["pod_id"] for w in wins]))
         sn = {}
@@ -86,6 +89,7 @@ def rank_main(rank, world, uq, n_win, q):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", type=int, default=4)
+    ap.add_argument("--wait", type=float, default=90.0, help="seconds to wait for each rank")
     a = ap.parse_args()
     world = 2
     ctx = mp.get_context("spawn")  # no GPU state in the parent: each rank initialises its own
@@ -95,7 +99,7 @@ def main():
         p.start()
     out = {}
     for _ in range(world):
-        m = q.get(timeout=240)
+        m = q.get(timeout=a.wait)
         out[m["rank"]] = m
     for p in procs:
         p.join(60)
