@@ -70,8 +70,9 @@ def parse():
                     help="carry rows within this distance of a window's latest record into the next window")
     ap.add_argument("--xchg-cap", type=int, default=-1,
                     help="warn-level trace-tagged rows each GPU exchanges per window over RCCL (-1: 65536 when N > 1)")
-    ap.add_argument("--user-rec", type=int, default=32, choices=(32, 64),
-                    help="user-space ring record size: 32 = USER32 (the rocprof tool's compact record), 64 = EVENT")
+    ap.add_argument("--user-rec", type=int, default=24, choices=(24, 32, 64),
+                    help="user-space ring record size: 24 = USER24 (the rocprof tool's compact record), 32 = USER32, "
+                         "64 = EVENT")
     ap.add_argument("--out", default="")
     return ap.parse_args()
 

@@ -388,7 +388,7 @@ class Agent:
                 attached = self.probe_manager.attach_all()
                 print(f"attached probes for {len(attached)} signals from {o.probe_objs}", file=sys.stderr)
             maps = bpf.BpfMaps(o.pin_dir)
-            user = rt.HostRing(1 << 20, 32, names.user)   # the rocprofiler tool attaches, pushes USER32
+            user = rt.HostRing(1 << 20, 24, names.user)   # the rocprofiler tool attaches, pushes USER24
             spans = rt.HostRing(1 << 18, 64, names.spans)  # OTLP receiver / services
             return maps, maps.ring, user, spans, None
         if o.source == "shm":

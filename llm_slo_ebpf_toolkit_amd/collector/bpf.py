@@ -175,10 +175,10 @@ class RingNames:
         return RingNames(prefix + "-bpf", prefix + "-events", prefix + "-spans")
 
 
-def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int, user_rec: int = 32):
+def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int, user_rec: int = 24):
     """Create the emulated BPF ring and the two user-space rings (the agent owns them). The
-    user-space ring holds ``user_rec``-byte records: 32 = USER32 (what the rocprofiler tool
-    writes into such a ring, half the PCIe bytes of a 64-byte EVENT)."""
+    user-space ring holds ``user_rec``-byte records: 24 = USER24 (what the rocprofiler tool
+    writes into such a ring, 3/8 of the PCIe bytes of a 64-byte EVENT), 32 = USER32."""
     from ..runtime import load
 
     rt = load()
@@ -211,8 +211,6 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
     for w in wins:
         km = kernel_event_mask(w.events)
         uev = np.ascontiguousarray(w.events[~km])
-        if user.rec_size == 32:  # the agent created a USER32 ring: write what the rocprof tool would
-            uev = records.to_user32(uev)
         parts.append((np.ascontiguousarray(w.events[km]), uev, np.ascontiguousarray(w.spans)))
     if ready is not None:
         ready.send(True)
@@ -234,8 +232,8 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
             lo_k, hi_k = len(kev) * s // n_sl, len(kev) * (s + 1) // n_sl
             sim.submit(kev[lo_k:hi_k])
             lo_u, hi_u = len(uev) * s // n_sl, len(uev) * (s + 1) // n_sl
-            if hi_u > lo_u:
-                user.push(uev[lo_u:hi_u])
+            if hi_u > lo_u:  # in the ring's record: what the rocprof tool would write
+                user.push(records.to_user(uev[lo_u:hi_u], int(user.rec_size)))
             lo_s, hi_s = len(sp) * s // n_sl, len(sp) * (s + 1) // n_sl
             if hi_s > lo_s:
                 spans.push(sp[lo_s:hi_s])

@@ -138,6 +138,20 @@ USER32 = np.dtype([
     ("node_id", "<u2"),      # 30
 ])
 assert USER32.itemsize == 32
+# 24-byte user-space record (rings created with 24-byte records; ops/csrc/mislo_common.h
+# User24): USER32 without the node id and flags the decode never reads, the timestamp as its
+# low 44 bits (decoded to the value nearest the window's newest epoch base, +-2.4 h), pid < 2^22
+# (Linux pid_max), pod id < 2^20 (the device pod table), signal type < 128. 25 % fewer PCIe
+# bytes than USER32.
+USER24 = np.dtype([
+    ("trace_h", "<u8"),      # 0
+    ("value_milli", "<u4"),  # 8
+    ("ts_lo", "<u4"),        # 12 ts bits 0..31
+    ("pid_sig", "<u4"),      # 16 pid | signal_type << 22 | ts_zero << 29 | has_gpu << 30
+    ("pod_ts", "<u4"),       # 20 pod_id | (ts bits 32..43) << 20
+])
+assert USER24.itemsize == 24
+USER24_TS_BITS = 44
 
 WIRE_DTYPES = {64: EVENT, 16: EVENT16}
 RB_BUSY, RB_DISCARD, RB_HDR = 1 << 31, 1 << 30, 8   # BPF ring buffer record header bits
@@ -310,6 +324,65 @@ def to_user32(events: np.ndarray) -> np.ndarray:
     out["flags"] = ((events["flags"] >> 8) & 1).astype(np.uint8)
     out["node_id"] = events["node_id"]
     return out
+
+
+def to_user24(events: np.ndarray) -> np.ndarray:
+    """64-byte EVENT records -> USER24 (mislo_rocprof.cpp emit with a 24-byte ring). Raises on
+    a pid, pod id or signal type that does not fit the record."""
+    st = events["signal_type"].astype(np.int64)
+    pid = events["pid"].astype(np.uint64)
+    pod = events["pod_id"].astype(np.uint64)
+    if len(events) and (pid.max() >= 1 << 22 or pod.max() >= 1 << 20 or st.max() >= 128 or st.min() < 0):
+        raise ValueError("USER24 holds pid < 2^22, pod id < 2^20, signal type < 128")
+    ts = events["ts_ns"].astype(np.int64)
+    t = ts.astype(np.uint64)
+    out = np.zeros(len(events), dtype=USER24)
+    out["trace_h"] = events["trace_h"]
+    out["value_milli"] = milli_int(events["value"], milli_shift_table()[np.clip(st, 0, 255)])
+    out["ts_lo"] = (t & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    zero = (ts == 0).astype(np.uint64)
+    gpu = ((events["flags"].astype(np.uint64) >> np.uint64(8)) & np.uint64(1))
+    out["pid_sig"] = (pid | (st.astype(np.uint64) << np.uint64(22)) | (zero << np.uint64(29))
+                      | (gpu << np.uint64(30))).astype(np.uint32)
+    out["pod_ts"] = (pod | (((t >> np.uint64(32)) & np.uint64(0xFFF)) << np.uint64(20))).astype(np.uint32)
+    return out
+
+
+def user24_ts(u: np.ndarray, base: int) -> np.ndarray:
+    """USER24 timestamps: the value nearest ``base`` with the record's low 44 bits (0 when the
+    record says it has none); ops/csrc/mislo_common.h user24_ts."""
+    t44 = ((u["pod_ts"].astype(np.uint64) >> np.uint64(20)) << np.uint64(32)) | u["ts_lo"].astype(np.uint64)
+    mask = np.uint64((1 << USER24_TS_BITS) - 1)
+    d = (t44 - np.uint64(base & 0xFFFFFFFFFFFFFFFF)) & mask
+    sh = np.uint64(64 - USER24_TS_BITS)
+    sd = ((d << sh).view(np.int64) >> np.int64(64 - USER24_TS_BITS))
+    ts = np.int64(base) + sd
+    return np.where((u["pid_sig"] >> np.uint32(29)) & np.uint32(1), np.int64(0), ts).astype(np.int64)
+
+
+def user24_to_user32(u: np.ndarray, base: int) -> np.ndarray:
+    """USER24 -> USER32 (timestamps nearest ``base``; node id 0: USER24 does not carry it)."""
+    pid_sig, pod_ts = u["pid_sig"].astype(np.uint32), u["pod_ts"].astype(np.uint32)
+    v = np.zeros(len(u), dtype=USER32)
+    v["ts_ns"] = user24_ts(u, int(base))
+    v["trace_h"] = u["trace_h"]
+    v["value_milli"] = u["value_milli"]
+    v["pod_id"] = pod_ts & np.uint32(0xFFFFF)
+    v["pid"] = pid_sig & np.uint32(0x3FFFFF)
+    v["signal_type"] = ((pid_sig >> np.uint32(22)) & np.uint32(0x7F)).astype(np.uint8)
+    v["flags"] = ((pid_sig >> np.uint32(30)) & np.uint32(1)).astype(np.uint8)
+    return v
+
+
+def to_user(events: np.ndarray, rec: int) -> np.ndarray:
+    """EVENT records -> what a user-space producer writes into a ``rec``-byte ring."""
+    if rec == 64:
+        return events
+    if rec == 32:
+        return to_user32(events)
+    if rec == 24:
+        return to_user24(events)
+    raise ValueError(f"user-space records are 64, 32 or 24 bytes, not {rec}")
 
 
 def milli_int(raw: np.ndarray, shift: np.ndarray) -> np.ndarray:

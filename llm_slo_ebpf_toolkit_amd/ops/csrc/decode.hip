@@ -412,10 +412,12 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   const int n = seg ? max(r0, min(rows[1], cap)) : r0;
   const int n_loc = min(n_ptr[0], r0);
   const int n_k = min(n_ptr[15], n_loc);
-  const bool user32 = n_ptr[6] == 32;  // counts[6]: user-space record bytes (64 = EVENT, 32 = User32)
+  const int user_rec = n_ptr[6];  // counts[6]: user-space record bytes (64 = EVENT, 32 = User32, 24 = User24)
   const int valid_k = min((int)min((uint32_t)n_k, rs[kRsFirstBusy]), n_k);
   auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
   const int64_t t_base[4] = {base_at(4), base_at(8), base_at(10), base_at(12)};
+  // USER24 timestamps resolve against the newest epoch base (tags rotate; unset bases are 0)
+  const int64_t u_base = max(max(t_base[0], t_base[1]), max(t_base[2], t_base[3]));
   const int chunk = (n - seg_beg + gridDim.x - 1) / gridDim.x;
   const int beg = seg_beg + blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0, events = 0;
@@ -449,7 +451,19 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         } else {  // a hole: never counted, never joined
           decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
         }
-      } else if (user32) {
+      } else if (user_rec == 24) {
+        const uint2* u = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(user) + (size_t)(i - n_k) * 24);
+        const uint2 a = u[0], b = u[1], c = u[2];  // {trace lo, hi}, {value, ts_lo}, {pid_sig, pod_ts}
+        const int st = (int)((c.x >> 22) & 0x7Fu);
+        const int slot = (int)L.tab.type_slot[st];
+        const uint32_t pod = c.y & 0xFFFFFu;
+        const uint32_t sn = pod < n_pods ? pod_sn[pod] : 0u;
+        const int64_t ts = user24_ts(b.y, c.y, c.x, u_base);
+        decode_one(i, cap, ts, (float)((double)b.x * 1e-3), slot, ((uint64_t)a.y << 32) | a.x, pod, c.x & 0x3FFFFFu, sn,
+                   0ull, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+        if (slot >= 0 && ts > 0) t_hi = max(t_hi, (unsigned long long)ts);
+        ++events;
+      } else if (user_rec == 32) {
         const User32 e = reinterpret_cast<const User32*>(user)[i - n_k];
         const int st = e.signal_type;
         const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;

@@ -149,6 +149,12 @@ def decode_user32(u: np.ndarray, pod_sn: Dict[int, int]) -> Decoded:
                    u["pid"].astype(np.uint32), sn, u["trace_h"].astype(np.uint64), np.zeros(n, np.uint64))
 
 
+def decode_user24(u: np.ndarray, pod_sn: Dict[int, int], base: int) -> Decoded:
+    """k_decode_window on USER24 rows: USER32's decode with the packed pid / type / pod id and the
+    timestamp nearest ``base`` (the window's newest epoch base)."""
+    return decode_user32(records.user24_to_user32(u, base), pod_sn)
+
+
 def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases,
                   pod_sn: Dict[int, int] = None) -> Decoded:
     """k_decode_window: rows [0, n framed) from the framed ring records (definitions, discarded
@@ -168,6 +174,8 @@ def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: T
         return d
     if user.dtype == records.USER32:
         u = decode_user32(user, pod_sn or {})
+    elif user.dtype == records.USER24:
+        u = decode_user24(user, pod_sn or {}, max(int(b) for b in bases))
     else:
         u = decode_events(user)
         u.conn = records.conn32_np(u.conn).astype(np.uint64)

@@ -306,10 +306,10 @@ class RingWindowSource:
             self.direct["ring"] = pipe.eng.register_host(ring.data_address, 2 * ring.size)
             self.kpos = ring.consumer_pos
             self.kmask = ring.size - 1
-        # user-space producers' records: 64-byte EVENT or 32-byte USER32, per ring
+        # user-space producers' records: 64-byte EVENT, 32-byte USER32 or 24-byte USER24, per ring
         self.user_rec = int(user_ring.rec_size) if user_ring is not None else 64
-        if self.user_rec not in (32, 64):
-            raise ValueError(f"user ring holds {self.user_rec}-byte records (EVENT = 64, USER32 = 32)")
+        if self.user_rec not in (24, 32, 64):
+            raise ValueError(f"user ring holds {self.user_rec}-byte records (EVENT = 64, USER32 = 32, USER24 = 24)")
         if user_ring is not None:
             self.direct["user"] = pipe.eng.register_host(user_ring.address, user_ring.capacity * self.user_rec)
             self.upos = user_ring.tail
@@ -509,7 +509,7 @@ def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim
         payload = np.concatenate(parts)
         uev = np.ascontiguousarray(w.events[~km])
         out.append(ReplayImage(framed=rt.frame_records(payload), spans=np.ascontiguousarray(w.spans),
-                               user=records.to_user32(uev) if user_rec == 32 else uev, bases=clock.bases(),
+                               user=records.to_user(uev, user_rec), bases=clock.bases(),
                                n_groups=w.n_groups,
                                labels=np.asarray(w.group_labels, dtype=np.int32), domains=list(w.group_domains),
                                n_kernel=int(km.sum())))

@@ -3,8 +3,9 @@
 // Loaded into an LLM workload (ROCP_TOOL_LIBRARIES=libmislo_rocprof.so, no root needed),
 // it turns runtime activity into the four GPU signals of the catalogue and pushes them into
 // the agent's shared-memory ring (runtime/csrc/ring.h C ABI) as the ring's record type: 64-byte
-// EVENT or, in rings created with 32-byte records, USER32 (collector/records.py; the value in
-// fixed point by the probes' own rule, mislo_record.h mislo_milli -- half the PCIe bytes):
+// EVENT or, in rings created with 32- or 24-byte records, USER32 / USER24 (collector/records.py;
+// the value in fixed point by the probes' own rule, mislo_record.h mislo_milli; USER24 packs
+// pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
 //   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue            (ns)
 //   type 14 hbm_pressure_pct     live device allocations / HBM capacity     (milli-pct)
@@ -79,6 +80,14 @@ struct User32Rec {  // collector/records.py USER32
 };
 static_assert(sizeof(User32Rec) == 32, "USER32 layout");
 
+struct User24Rec {  // collector/records.py USER24 (ops/csrc/mislo_common.h User24)
+  uint64_t trace_h;
+  uint32_t value_milli, ts_lo;
+  uint32_t pid_sig;  // pid | signal_type << 22 | ts_zero << 29 | has_gpu << 30
+  uint32_t pod_ts;   // pod_id | (ts bits 32..43) << 20
+};
+static_assert(sizeof(User24Rec) == 24, "USER24 layout");
+
 constexpr uint16_t kQueueDelay = 13, kHbmPressure = 14, kXgmiLatency = 15, kRcclCollective = 16;
 
 struct State {
@@ -94,6 +103,7 @@ struct State {
   uint64_t queue_floor_ns = 100000;
   double xgmi_bytes_per_ns = 64.0;
   bool rec32 = false;  // the ring holds 32-byte USER32 records
+  bool rec24 = false;  // the ring holds 24-byte USER24 records
   bool verbose = false;
   std::mutex mu;
   struct Enq {
@@ -129,6 +139,19 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t 
     return;
   }
   bool ok;
+  if (g.rec24) {
+    User24Rec u{};
+    const uint64_t t = (uint64_t)wall;
+    u.trace_h = trace_h;
+    u.value_milli = mislo_milli(type, value);
+    u.ts_lo = (uint32_t)t;
+    u.pid_sig = ((uint32_t)getpid() & 0x3FFFFFu) | ((uint32_t)(type & 0x7F) << 22) | (wall == 0 ? 1u << 29 : 0u) |
+                (1u << 30);
+    u.pod_ts = (g.pod & 0xFFFFFu) | (uint32_t)(((t >> 32) & 0xFFFu) << 20);
+    ok = mislo_ring_push_batch(g.ring, &u, 1) == 1;
+    (ok ? g.pushed : g.dropped).fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
   if (g.rec32) {
     User32Rec u{};
     u.ts_ns = wall;
@@ -251,6 +274,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   const char* name = std::getenv("MISLO_RING");
   g.ring = mislo_ring_open_shm(name && *name ? name : "/mislo-agent-events");
   g.rec32 = g.ring && mislo_ring_rec_size(g.ring) == 32;
+  g.rec24 = g.ring && mislo_ring_rec_size(g.ring) == 24;
   g.pod = (uint32_t)env_u64("MISLO_POD_ID", 0);
   g.node = (uint16_t)env_u64("MISLO_NODE_ID", 0);
   g.svc = (uint16_t)env_u64("MISLO_SVC_ID", 0);

@@ -53,9 +53,9 @@ def test_extension_is_native():
     assert mod.__file__.endswith(".so") and mod.device_count() >= 1
 
 
-@pytest.mark.parametrize("user_rec", [64, 32])
+@pytest.mark.parametrize("user_rec", [64, 32, 24])
 def test_ring_windows_match_oracle(user_rec):
-    """user_rec 32: the user-space ring holds USER32 records (the rocprof tool's compact form,
+    """user_rec 32 / 24: the user-space ring holds USER32 / USER24 records (the rocprof tool's compact forms,
     svc|node from the device pod table)."""
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 

@@ -2,6 +2,7 @@
 carries (framed as 24-byte ring records), SPAN20; the integer fixed-point rule and the epoch
 protocol (the ring path itself: tests/test_bpfring.py)."""
 
+import pytest
 import numpy as np
 
 from llm_slo_ebpf_toolkit_amd.collector import records
@@ -71,3 +72,55 @@ def test_epoch_clock_protocol_across_cuts():
             if k == 5:  # the window after the last cut carries bases of epochs 2..5
                 assert bases[tag] + off == ts
     assert records.EpochClock.stamp(0, cfgs[0]) == (records.TS_ZERO, cfgs[0] & 3)
+
+
+def test_user24_roundtrip_against_user32():
+    """USER24 keeps everything the decode reads of USER32: timestamps within +-2.4 h of the
+    window's base come back exact (0 stays 0), pid / pod / type / value / trace unchanged."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+
+    w = ReplayGenerator(ReplayConfig(scenario="full", events_per_window=4096, spans_per_window=64, seed=5)).next_window()
+    ev = w.events.copy()
+    ev["ts_ns"][:3] = 0
+    ev["ts_ns"][3] = int(w.t0_ns) + 2 * 3600 * 10**9      # 2 h after the base
+    ev["ts_ns"][4] = int(w.t0_ns) - 2 * 3600 * 10**9      # 2 h before
+    u24 = records.to_user24(ev)
+    assert u24.itemsize == 24
+    back = records.user24_to_user32(u24, int(w.t0_ns))
+    u32 = records.to_user32(ev)
+    for f in ("ts_ns", "trace_h", "value_milli", "pod_id", "pid", "signal_type"):
+        assert np.array_equal(back[f], u32[f]), f
+    assert (back["flags"] == u32["flags"]).all()  # has_gpu
+    assert records.to_user(ev, 24).tobytes() == u24.tobytes()
+    bad = ev[:1].copy()
+    bad["pid"] = 1 << 22
+    with pytest.raises(ValueError):
+        records.to_user24(bad)
+
+
+def test_user24_windows_decode_like_user32():
+    """The probe-model images of the same replay windows with USER24 and USER32 user rings decode
+    (pipeline/oracle.py, the GPU decode's reference) to identical rows: USER24 loses nothing the
+    window decode reads, with timestamps resolved against the window's newest epoch base."""
+    from llm_slo_ebpf_toolkit_amd.pipeline import oracle
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
+
+    def decoded(rec):
+        g = ReplayGenerator(ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8,
+                                         events_per_window=3000, spans_per_window=100, seed=9))
+        wins = [g.next_window() for _ in range(3)]
+        imgs = build_replay_images(wins, user_rec=rec)
+        sn = (g.pod_svc.astype(np.uint32) << np.uint32(16)) | g.pod_node.astype(np.uint32)
+        pod_sn = dict(zip(g.pod_ids.tolist(), sn.tolist()))
+        table, tmap = oracle.CtxTable(), oracle.TraceMap()
+        out = []
+        for img in imgs:
+            assert img.user.dtype.itemsize == rec and len(img.user)
+            oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
+            out.append(oracle.decode_window(img.framed, img.user, table, tmap, img.bases, pod_sn=pod_sn))
+        return out
+
+    for a, b in zip(decoded(24), decoded(32)):
+        for f in a.__dataclass_fields__:
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f

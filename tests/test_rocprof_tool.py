@@ -52,14 +52,15 @@ def test_runtime_c_abi_library_is_self_contained():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rec", [64, 32])
+@pytest.mark.parametrize("rec", [64, 32, 24])
 def test_tool_pushes_gpu_signals_into_ring(rec):
-    """rec 32: the ring was created with 32-byte records, so the tool writes USER32."""
+    """rec 32 / 24: the ring was created with 32- / 24-byte records, so the tool writes USER32 /
+    USER24 (read back through USER32's fields; USER24 carries no node id)."""
     from llm_slo_ebpf_toolkit_amd.collector import records
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    dt = records.EVENT if rec == 64 else records.USER32
+    dt = {64: records.EVENT, 32: records.USER32, 24: records.USER24}[rec]
     name = f"/mislo-test-{os.getpid()}-events{rec}"
     ring = rt.HostRing(1 << 16, rec, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0",
@@ -72,6 +73,8 @@ def test_tool_pushes_gpu_signals_into_ring(rec):
     view = ring.records_view()
     recs = np.concatenate([np.frombuffer(view[i * rec:(i + c) * rec].tobytes(), dtype=dt)
                            for _, i, c in segs]) if segs else np.zeros(0, dtype=dt)
+    if rec == 24:
+        recs = records.user24_to_user32(recs, t0)
     types = set(recs["signal_type"].tolist())
     assert 13 in types, (types, r.stderr[-1000:])      # gpu_queue_delay_ms from kernel dispatches
     assert 14 in types, (types, r.stderr[-1000:])      # hbm_pressure_pct from allocations
@@ -81,7 +84,7 @@ def test_tool_pushes_gpu_signals_into_ring(rec):
 
     if torch.cuda.device_count() >= 2:
         pass  # exercised by tests/test_rocprof_tool.py::test_xgmi_peer_copies (multi-GPU runners)
-    assert (recs["pod_id"] == 7).all() and (recs["node_id"] == 3).all()
+    assert (recs["pod_id"] == 7).all() and (rec == 24 or (recs["node_id"] == 3).all())
     assert (recs["flags"] & (1 << 8 if rec == 64 else 1)).all()
     ts = recs["ts_ns"]
     assert (ts > t0 - 10 * 10**9).all() and (ts < time.time_ns() + 10 * 10**9).all()  # wall clock

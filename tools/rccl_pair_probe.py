@@ -47,7 +47,7 @@ def rank_main(rank, world, uq, n_win, q):
                            shard=rank)
         gen = ReplayGenerator(cfg)
         wins = [gen.next_window() for _ in range(n_win)]
-        imgs = build_replay_images(wins, user_rec=32)
+        imgs = build_replay_images(wins, user_rec=24)
         sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs)
         user_cap = 1 << int(np.ceil(np.log2(max(len(i.user) for i in imgs))))
         xchg = 4096
@@ -64,7 +64,7 @@ def rank_main(rank, world, uq, n_win, q):
         pipe.eng.set_pods(pods.astype(np.uint32), np.array([sn[p] for p in pods.tolist()], dtype=np.uint32))
         rt = load()
         rb = rt.Ringbuf.create_shm(f"/mislo-rpp-{os.getpid()}", 1 << 24)
-        user, spans = rt.HostRing(1 << 16, 32), rt.HostRing(1 << 14, 64)
+        user, spans = rt.HostRing(1 << 16, 24), rt.HostRing(1 << 14, 64)
         src = RingWindowSource(pipe, rb, user, spans)
         groups, own, gathered = 0, [], []
         for i, img in enumerate(imgs):
