@@ -226,14 +226,15 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
         for a in (kev, uev, sp):
             nz = a["ts_ns"] != 0
             a["ts_ns"][nz] += shift
+        uev = records.to_user(uev, int(user.rec_size))  # what the rocprof tool writes into this ring
         # pace: the window's records go out in 10 slices across its period
         n_sl = 10
         for s in range(n_sl):
             lo_k, hi_k = len(kev) * s // n_sl, len(kev) * (s + 1) // n_sl
             sim.submit(kev[lo_k:hi_k])
             lo_u, hi_u = len(uev) * s // n_sl, len(uev) * (s + 1) // n_sl
-            if hi_u > lo_u:  # in the ring's record: what the rocprof tool would write
-                user.push(records.to_user(uev[lo_u:hi_u], int(user.rec_size)))
+            if hi_u > lo_u:
+                user.push(uev[lo_u:hi_u])
             lo_s, hi_s = len(sp) * s // n_sl, len(sp) * (s + 1) // n_sl
             if hi_s > lo_s:
                 spans.push(sp[lo_s:hi_s])
