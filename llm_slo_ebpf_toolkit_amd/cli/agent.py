@@ -67,7 +67,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("halo-ms", d.halo_ms, "gpu engine: records this close to a window's end also join the next window (0 = off)"),
         ("state-dir", d.state_dir, "gpu engine: checkpoint directory for the learned state (resumed on start)"),
         ("checkpoint-every", d.checkpoint_every, "gpu engine: windows between checkpoints"),
-        ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES, an explicit env wins; "
+        ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; the flag given on the "
+                             "command line wins over the env, the default does not; "
                              "each MI355X queue pins ~173 MB of host memory; 1 serialises copy and compute, ample "
                              "at node event rates; 0 = runtime default)"),
     ]:
@@ -89,8 +90,12 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
         otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
         checkpoint_every=int(a.checkpoint_every))
-    if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime; an explicit env wins
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(int(a.gpu_hw_queues)))
+    if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
+        given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])
+        if given:  # an operator's flag wins over a node-wide GPU_MAX_HW_QUEUES
+            os.environ["GPU_MAX_HW_QUEUES"] = str(int(a.gpu_hw_queues))
+        else:
+            os.environ.setdefault("GPU_MAX_HW_QUEUES", str(int(a.gpu_hw_queues)))
     return o, a.probe_smoke
 
 

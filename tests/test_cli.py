@@ -188,3 +188,19 @@ def test_agent_metrics_export_gpu_signal_histograms():
     text = m.registry.exposition() if hasattr(m, "registry") else m.r.exposition()
     assert 'llm_ebpf_gpu_queue_delay_ms_bucket{le="5"} 7' in text
     assert "llm_ebpf_gpu_queue_delay_ms_sum 28" in text
+
+
+def test_agent_gpu_hw_queues_flag_wins_over_env_default_does_not(monkeypatch):
+    from llm_slo_ebpf_toolkit_amd.cli import agent as agent_cli
+
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")  # a node-wide setting
+    agent_cli.parse(["--engine", "gpu"])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    agent_cli.parse(["--engine", "gpu", "--gpu-hw-queues", "1"])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    agent_cli.parse(["-gpu-hw-queues=2"])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "2"
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    agent_cli.parse([])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
