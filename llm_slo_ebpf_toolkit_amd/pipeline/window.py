@@ -132,7 +132,11 @@ class WindowPipeline:
     def submit(self, kernel, user, spans, n_groups: int, labels=None, bases=(0, 0, 0, 0), with_labels: bool = True,
                learn: Optional[bool] = None, user_rec: int = 64) -> int:
         """Queue the next window: ``kernel`` / ``user`` / ``spans`` = [(host address, bytes)] ranges
-        of framed ring records / 64-byte records / 64-byte spans. Returns its index."""
+        of framed ring records / ``user_rec``-byte records / 64-byte spans. Returns its index.
+        USER24 records (``user_rec`` 24) keep 44 timestamp bits, resolved against the newest of
+        ``bases``: a window of them needs a published epoch."""
+        if user_rec == 24 and not any(int(b) for b in bases) and any(int(n) for _, n in user):
+            raise ValueError("USER24 records need the window's epoch bases (all are 0)")
         k = self.k
         learn = (self.learn and with_labels) if learn is None else learn
         lab = None if labels is None else np.ascontiguousarray(labels, dtype=np.int32)

@@ -124,3 +124,13 @@ def test_user24_windows_decode_like_user32():
     for a, b in zip(decoded(24), decoded(32)):
         for f in a.__dataclass_fields__:
             assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_user24_window_without_epoch_is_refused():
+    """WindowPipeline.submit refuses USER24 records with no epoch base to resolve them against
+    (checked before the engine is touched, so this runs without a GPU)."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline
+
+    pipe = WindowPipeline.__new__(WindowPipeline)  # no engine: the check comes first
+    with pytest.raises(ValueError):
+        pipe.submit([], [(0x1000, 24)], [], 1, bases=(0, 0, 0, 0), user_rec=24)
