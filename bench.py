@@ -344,7 +344,7 @@ def main() -> int:
             cpu_pct = float(ct.item())
 
     # ---- held-out attribution: frozen model, windows of another seed ------------------------
-    from llm_slo_ebpf_toolkit_amd.models.metrics import macro_f1_from_confusion
+    from llm_slo_ebpf_toolkit_amd.models.metrics import confusion_report, macro_f1_from_confusion
     from llm_slo_ebpf_toolkit_amd.signals import catalog
 
     # per scenario: the device's confusion (primary label x prediction) plus REF's partial
@@ -378,7 +378,8 @@ def main() -> int:
                              "accuracy": round(float(np.trace(cm) / cm.sum()), 4),
                              "partial_accuracy": round(float(pc[0] / max(pc[2], 1)), 4),
                              "coverage_accuracy": round(float(pc[1] / max(pc[2], 1)), 4),
-                             "incidents": int(cm.sum()), "confusion": cm.tolist()}
+                             "incidents": int(cm.sum()), "confusion": cm.tolist(),
+                             **confusion_report(cm, catalog.ALL_DOMAINS)}
 
     # ---- REF 55-row dataset through the GPU posterior kernel --------------------------------
     ref_f1, ref_multi = {}, {}

@@ -121,6 +121,39 @@ def confusion_from_arrays(actual_idx, pred_idx, n_classes: int):
     return m
 
 
+def confusion_report(conf, labels: Sequence[str], abstain_label: str = "unknown") -> dict:
+    """conf[actual, predicted] -> per-class precision / recall / F1 / support (classes with
+    support or predictions), the one-vs-rest false-positive and false-negative rates averaged
+    over those classes (REF harness definitions, evaluation/benchmark.py), and the abstain rate
+    (share of incidents predicted ``abstain_label``; REF target <= 15 %)."""
+    import numpy as np
+
+    conf = np.asarray(conf, dtype=np.float64)
+    n = conf.sum()
+    tp = np.diag(conf)
+    sup, npred = conf.sum(axis=1), conf.sum(axis=0)
+    per, fprs, fnrs = [], [], []
+    for i, lab in enumerate(labels):
+        if sup[i] == 0 and npred[i] == 0:
+            continue
+        prec = tp[i] / npred[i] if npred[i] else 0.0
+        rec = tp[i] / sup[i] if sup[i] else 0.0
+        f1 = 2 * prec * rec / (prec + rec) if prec + rec > 0 else 0.0
+        per.append({"label": lab, "precision": round(float(prec), 4), "recall": round(float(rec), 4),
+                    "f1": round(float(f1), 4), "support": int(sup[i])})
+        fp, fn = npred[i] - tp[i], sup[i] - tp[i]
+        tn = n - tp[i] - fp - fn
+        if tp[i] + fn:
+            fnrs.append(fn / (tp[i] + fn))
+        if fp + tn:
+            fprs.append(fp / (fp + tn))
+    ab = list(labels).index(abstain_label) if abstain_label in labels else -1
+    return {"per_class": per,
+            "false_positive_rate": round(float(np.mean(fprs)), 4) if fprs else 0.0,
+            "false_negative_rate": round(float(np.mean(fnrs)), 4) if fnrs else 0.0,
+            "abstain_rate": round(float(npred[ab] / n), 4) if ab >= 0 and n else 0.0}
+
+
 def macro_f1_from_confusion(conf, present_only: bool = True) -> float:
     """conf[actual, predicted]; macro over classes with support (ground-truth classes)."""
     import numpy as np

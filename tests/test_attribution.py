@@ -163,3 +163,29 @@ def test_bayes_gpu_names_gpu_domains_and_keeps_ref_rows():
         for name in catalog.SIGNAL_NAMES[:12]:
             slot = catalog.BY_NAME[name].slot
             assert m.weights[slot, d] == ref.weights[slot, d]
+
+
+def test_confusion_report_matches_list_metrics():
+    """confusion_report (the bench's held-out report) agrees with the list-based per-class
+    report and REF's one-vs-rest rates on the same predictions."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.evaluation.benchmark import one_vs_rest_rates
+    from llm_slo_ebpf_toolkit_amd.models.metrics import confusion_report, per_class_report
+
+    labels = ["a", "b", "unknown", "c"]
+    actual = ["a", "a", "b", "b", "b", "c", "c", "a"]
+    pred = ["a", "b", "b", "unknown", "b", "c", "a", "a"]
+    cm = np.zeros((4, 4))
+    for x, y in zip(actual, pred):
+        cm[labels.index(x), labels.index(y)] += 1
+    rep = confusion_report(cm, labels)
+    ref = {r.label: r for r in per_class_report(actual, pred, labels)}
+    for r in rep["per_class"]:
+        assert r["precision"] == pytest.approx(ref[r["label"]].precision, abs=1e-4)
+        assert r["recall"] == pytest.approx(ref[r["label"]].recall, abs=1e-4)
+        assert r["f1"] == pytest.approx(ref[r["label"]].f1, abs=1e-4)
+    rates = one_vs_rest_rates(actual, pred)
+    assert rep["false_positive_rate"] == pytest.approx(rates["false_positive_rate"], abs=1e-4)
+    assert rep["false_negative_rate"] == pytest.approx(rates["false_negative_rate"], abs=1e-4)
+    assert rep["abstain_rate"] == pytest.approx(1 / 8)
