@@ -124,8 +124,10 @@ def confusion_from_arrays(actual_idx, pred_idx, n_classes: int):
 def confusion_report(conf, labels: Sequence[str], abstain_label: str = "unknown") -> dict:
     """conf[actual, predicted] -> per-class precision / recall / F1 / support (classes with
     support or predictions), the one-vs-rest false-positive and false-negative rates averaged
-    over those classes (REF harness definitions, evaluation/benchmark.py), and the abstain rate
-    (share of incidents predicted ``abstain_label``; REF target <= 15 %)."""
+    over those classes (REF harness definitions, evaluation/benchmark.py), and the abstain rate:
+    the share of faulted incidents (ground truth other than ``abstain_label``) predicted
+    ``abstain_label`` (REF target <= 15 %; a no-fault incident predicted so is correct, not an
+    abstention)."""
     import numpy as np
 
     conf = np.asarray(conf, dtype=np.float64)
@@ -151,7 +153,8 @@ def confusion_report(conf, labels: Sequence[str], abstain_label: str = "unknown"
     return {"per_class": per,
             "false_positive_rate": round(float(np.mean(fprs)), 4) if fprs else 0.0,
             "false_negative_rate": round(float(np.mean(fnrs)), 4) if fnrs else 0.0,
-            "abstain_rate": round(float(npred[ab] / n), 4) if ab >= 0 and n else 0.0}
+            "abstain_rate": round(float((conf[:, ab].sum() - conf[ab, ab]) / (n - sup[ab])), 4)
+            if ab >= 0 and n > sup[ab] else 0.0}
 
 
 def macro_f1_from_confusion(conf, present_only: bool = True) -> float:

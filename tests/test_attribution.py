@@ -188,4 +188,7 @@ def test_confusion_report_matches_list_metrics():
     rates = one_vs_rest_rates(actual, pred)
     assert rep["false_positive_rate"] == pytest.approx(rates["false_positive_rate"], abs=1e-4)
     assert rep["false_negative_rate"] == pytest.approx(rates["false_negative_rate"], abs=1e-4)
-    assert rep["abstain_rate"] == pytest.approx(1 / 8)
+    assert rep["abstain_rate"] == pytest.approx(1 / 8)  # b -> unknown, of 8 faulted incidents
+    cm2 = cm.copy()
+    cm2[labels.index("unknown"), labels.index("unknown")] += 4  # correct no-fault incidents
+    assert confusion_report(cm2, labels)["abstain_rate"] == pytest.approx(1 / 8)
