@@ -169,8 +169,11 @@ class AgentOptions:
     slo_target: float = 0.99             # TTFT SLO objective (burn rate = breach fraction / (1 - target))
     otlp_receiver_bind: str = ""         # OTLP/HTTP /v1/traces receiver feeding the span ring ("" = off)
     halo_ms: float = 2000.0              # carry records this close to a window's end into the next window
-    state_dir: str = ""                  # checkpoint of the learned state ("" = none; resumed on start)
+    state_dir: str = ""                  # agent state checkpoint directory ("" = none; resumed on start)
     checkpoint_every: int = 60           # windows between checkpoints
+    gpus: int = 1                        # window workers (one per GPU); 0 = every GPU visible to the agent
+    model_path: str = ""                 # trained model file (attributor --train); overrides --model
+    otlp_receiver_allow: str = ""        # CIDRs allowed to export spans to the receiver ("" = any)
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -217,8 +220,9 @@ class Agent:
         self.metrics = AgentMetrics(opts.event_kind, self.mode, self.supported, self.generator.enabled_signals())
         self.server: Optional[MetricsServer] = None
         self.limiter = RateLimiter(self.cfg.sampling.events_per_second_limit)
+        # the window engine evaluates the guard every window: REF's formula over a 30 s horizon
         self.guard = None if opts.disable_overhead_guard or not sys.platform.startswith("linux") else \
-            OverheadGuard(self.cfg.safety.max_overhead_pct)
+            OverheadGuard(self.cfg.safety.max_overhead_pct, horizon_s=30.0 if opts.engine in ("gpu", "cpu") else 0.0)
         self.stop_event = threading.Event()
         self.meta = SampleMeta(cluster=opts.cluster, namespace=opts.namespace, workload=opts.workload,
                                service=opts.service, node=opts.node)
@@ -364,7 +368,7 @@ class Agent:
         self.writers.flush()
         return 0
 
-    # ---- GPU window engine ----------------------------------------------------------------
+    # ---- window engine (GPU, or the CPU oracle engine) ---------------------------------------
     def _open_source(self):
         """Rings + maps for the configured source. ``bpf``: the probes' pinned maps (root);
         ``shm``: emulated rings another process produces into (tests, CI); ``replay``: a forked
@@ -408,11 +412,78 @@ class Agent:
             return bpf.EmulatedMaps(ring), ring, user, spans, bpf.pod_metadata(kw)
         raise ValueError(f"unknown window source {o.source!r} (bpf | shm | replay)")
 
-    def _checkpoint(self, pipe, path: str) -> None:
+    def _load_model(self):
+        """(host model, PosteriorModel image, metadata): the file ``--model-path`` names (written by
+        ``attributor --train``), else the built-in expert tables."""
+        from ..ops.engine import model_bytes
+
+        o = self.o
+        if o.model_path:
+            from ..models.train import load_model
+
+            return load_model(o.model_path)
+        if o.model in ("bayes", ""):
+            m = NaiveBayes.ref()
+        elif o.model == "bayes_gpu":
+            m = NaiveBayes.gpu()
+        else:
+            raise ValueError(f"--model {o.model} is learned: give --model-path (a file `attributor --train` wrote)")
+        return m, model_bytes(m), {"name": m.name}
+
+    def n_gpus(self) -> int:
+        """Window workers: --gpus, or every GPU visible to the agent (--gpus 0; counted without
+        initialising HIP, which the controller never does)."""
+        if self.o.gpus > 0:
+            return int(self.o.gpus)
+        if self.o.engine == "cpu":
+            return 1
+        from ..parallel.numa import visible_gpu_count
+
+        return max(1, visible_gpu_count())
+
+    # ---- agent state (checkpoint / resume) ----------------------------------------------------
+    def _state_path(self) -> str:
+        if not self.o.state_dir:
+            return ""
+        safe = "".join(c if c.isalnum() or c in "-_." else "_" for c in self.o.node)
+        return os.path.join(self.o.state_dir, f"agent-{safe}.state.json")
+
+    def save_state(self, path: str) -> None:
+        """What the agent has learned at run time: the window counter, every incident group's
+        burn-rate history and pending forecasts (the SLO-impact forecaster), the pod-uid -> pod-id
+        interning (ids the probes' cgroup map and the engine's pod table carry) and the model in
+        use. Written to a temporary file and renamed."""
+        import json
+
+        st = {"format": "mislo-agent-state/2", "node": self.o.node, "windows": self.windows_done,
+              "model": getattr(self, "model_meta", {}).get("name", ""),
+              "burn": self.burn.state(), "pods": self.pod_ids.names()}
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        tmp = f"{path}.tmp.{os.getpid()}"
         try:
-            pipe.save_checkpoint(path, {"agent_windows": self.windows_done, "node": self.o.node})
+            with open(tmp, "w", encoding="utf-8") as fh:
+                json.dump(st, fh)
+            os.replace(tmp, path)
         except OSError as exc:
-            print(f"checkpoint {path} failed: {exc}", file=sys.stderr)
+            print(f"state checkpoint {path} failed: {exc}", file=sys.stderr)
+
+    def load_state(self, path: str) -> bool:
+        import json
+
+        try:
+            with open(path, encoding="utf-8") as fh:
+                st = json.load(fh)
+            if st.get("format") != "mislo-agent-state/2":
+                raise ValueError("unknown state format")
+            self.windows_done = int(st.get("windows", 0))
+            self.burn.restore(st.get("burn", {}))
+            for name in st.get("pods", [])[1:]:
+                self.pod_ids.id(name)
+        except (OSError, ValueError, KeyError, TypeError) as exc:
+            print(f"state {path} not usable ({exc}); starting fresh", file=sys.stderr)
+            return False
+        print(f"resumed agent state from {path} ({self.windows_done} windows)", file=sys.stderr)
+        return True
 
     def _scan_pods(self, maps) -> None:
         """kubepods cgroups -> the probes' cgroup -> pod id map (pod ids from the interner the
@@ -438,10 +509,13 @@ class Agent:
         forecast = {}
         if sli is not None:
             for g in range(min(G, sli.shape[0])):
-                forecast[g] = self.burn.observe(names[g] if g < len(names) else g, float(sli[g, 0]), float(sli[g, 1]))
+                key = names[g] if g < len(names) else f"group-{g}"
+                forecast[g] = self.burn.observe(key, float(sli[g, 0]), float(sli[g, 1]))
             err = self.burn.error()
             if err is not None:
                 self.metrics.burn_err.set(err)
+        # the SLO-impact window is the forecast horizon the burn rate is quoted over (5 minutes)
+        impact_min = max(1, int(round(self.burn.horizon * self.o.window_ms / 60000.0)))
         for g in range(G):
             if sli is not None and g < sli.shape[0] and sli[g, 0] == 0:
                 continue  # no request of this group in the window: no incident to attribute
@@ -461,20 +535,32 @@ class Agent:
                 incident_id=f"gpu-{t_ns}-{g:03d}", timestamp=t_ns, cluster=self.o.cluster,
                 namespace=self.o.namespace, service=names[g] if g < len(names) else f"group-{g}",
                 predicted_fault_domain=top.domain, confidence=float(top.posterior), evidence=ev,
-                slo_impact=SLOImpact("ttft_ms", round(burn, 4), max(1, int(round(self.o.window_ms / 60000.0)) or 1)),
+                slo_impact=SLOImpact("ttft_ms", round(burn, 4), impact_min),
                 fault_hypotheses=[FaultHypothesis(p.domain, p.posterior, p.evidence) for p in ranked
                                   if p.posterior >= 0.01]))
         return out
 
-    def _emit_window(self, pipe, k: int, t_ns: int, G: int, names, ring, host_us: float) -> None:
-        pk = pipe.packet(k)
-        lat_ms = pipe.window_ms(k)[0]
-        rs = pk["ring_state"]
-        self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], rs["events"], lat_ms, self.o.node, self.o.pod,
-                                    self.o.namespace, value_sums_milli=pk["misc"][2:18])
-        self.metrics.set_ring(ring.stats() if ring is not None else {}, rs, host_us)
-        res = pipe.results(k, G)
-        for attr in self._attributions(G, names, res, t_ns, pipe.model):
+    def _emit_window(self, replies: List[dict], t_ns: int, G: int, names, ring, model) -> None:
+        """Window k-1 of every worker: worker 0 carries the node-wide packet (RCCL all-reduce)
+        and every worker's incidents (all-gather); each worker its own ring accounting."""
+        from ..pipeline.window import RING_FIELDS, unpack_packet
+        from .worker import merge_results
+
+        prevs = [r["prev"] for r in replies if r.get("prev") is not None]
+        if not prevs or "packet" not in prevs[0]:
+            return
+        head = prevs[0]
+        pk = unpack_packet(head["packet"])
+        rings = [dict(zip(RING_FIELDS, (int(x) for x in p["ring"]))) for p in prevs]
+        events = sum(r["events"] for r in rings)
+        rs = dict(rings[0])
+        rs["first_busy"] = max(r["first_busy"] for r in rings)
+        self.metrics.observe_window(pk["hist"], pk["status"], pk["dbg"], events, max(p["latency_ms"] for p in prevs),
+                                    self.o.node, self.o.pod, self.o.namespace, value_sums_milli=pk["misc"][2:18])
+        self.metrics.set_ring(ring.stats() if ring is not None else {}, rs, max(p["host_us"] for p in prevs))
+        res = merge_results(head["results"], G)
+        self.last_results = res
+        for attr in self._attributions(G, names, res, t_ns, model):
             self.metrics.observe_attribution(attr.predicted_fault_domain)
             self.writers.emit_attribution(attr)
             self.attributions_emitted += 1
@@ -485,93 +571,115 @@ class Agent:
                     self.metrics.inc_dropped("emit")
                     print(f"webhook send failed: {exc}", file=sys.stderr)
 
-    def run_windows(self, max_windows: int = 0, comm=None) -> int:
-        """GPU engine main loop (one process per MI355X; ``comm`` = (RCCL unique id, rank, world)).
-
-        Every window_ms: cut (publish epoch k, snapshot the rings) -> native assembly into the
-        engine's pinned block -> submit (DMA + captured graph + packet all-reduce), with no
-        drain: window k-1's results, complete by now, are turned into metrics and attributions
-        while window k computes."""
-        from ..pipeline.window import RingWindowSource, WindowPipeline
+    def run_windows(self, max_windows: int = 0) -> int:
+        """Window engine main loop. This process is the controller: every window_ms it cuts
+        the node's rings (publishes epoch k into mislo_cfg -- the only writer -- then snapshots
+        the producer positions) and hands the cut to the window workers, one per GPU
+        (agent/worker.py; in this process when the node uses one). Each worker DMAs the window
+        straight from the rings into its GPU, decodes it, keeps the services it owns (group
+        sharding) and joins / scores them; the RCCL all-reduce and all-gather leave the
+        node-wide packet and incident list on worker 0. Window k-1's results, complete by the
+        time window k is staged, become metrics and attributions while window k computes."""
+        from ..collector import bpf
+        from ..collector.records import EpochClock
+        from ..pipeline.window import Cut
+        from ..safety import TreeCPUSampler
+        from .worker import WorkerPool, WorkerSpec, groups_of
 
         o = self.o
-        maps, ring, user, spans, pods = self._open_source()  # a replay producer forks here, before the GPU
-        node_id = (abs(hash(o.node)) % 0xFFFE) + 1
+        maps, ring, user, spans, pods = self._open_source()  # a replay producer forks here, before any GPU work
+        node_id = bpf.stable_node_id(o.node)
         maps.init(node_id)
+        model, image, self.model_meta = self._load_model()
+        self.model = model
+        N = self.n_gpus()
+        G = o.window_groups
         budget = o.window_events + o.window_events // 4  # events plus the definitions ahead of them
-        multi = comm is not None and comm[2] > 1
         # joins reach across the window cut (halo) and, on a multi-GPU node, across GPUs
         # (trace-tagged rows exchanged over RCCL); imports are bounded by one window's records
-        xchg = min(65536, budget) if multi else 0
-        icap = (budget if o.halo_ms > 0 else 0) + 7 * xchg
-        pipe = WindowPipeline(budget, o.window_spans, o.window_groups, o.device, comm, model=o.model, learn=False,
-                              window_ms=2000.0, user_cap=max(1024, o.window_events // 4), ttft_slo_ms=o.ttft_slo_ms,
-                              halo_ms=o.halo_ms, import_cap=icap, xchg_cap=xchg)
-        src = RingWindowSource(pipe, ring, user, spans, cfg_set=maps.cfg_set)
-        ckpt = os.path.join(o.state_dir, f"agent-{o.node}-gpu{o.device}.safetensors") if o.state_dir else ""
-        if ckpt and os.path.exists(ckpt):
-            try:
-                meta = pipe.load_checkpoint(ckpt)
-                self.windows_done = int(meta.get("agent_windows", 0))
-                print(f"resumed learned state from {ckpt} ({meta.get('windows_folded_device', 0)} windows folded)",
-                      file=sys.stderr)
-            except (ValueError, OSError, KeyError) as exc:
-                print(f"checkpoint {ckpt} not usable ({exc}); starting fresh", file=sys.stderr)
-        if pods is not None:
-            pipe.eng.set_pods(*pods)
+        xchg = min(65536, budget) if N > 1 else 0
+        icap = (budget if o.halo_ms > 0 else 0) + (N - 1) * xchg
+        port = 0
+        if o.engine == "cpu" and N > 1:
+            import socket
+
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+            sk.close()
+        specs = [WorkerSpec(rank=r, world=N, device=r if o.engine == "gpu" and N > 1 else o.device, engine=o.engine,
+                            source="bpf" if o.source == "bpf" else "shm", ring_name=o.ring_name, pin_dir=o.pin_dir,
+                            user_rec=int(user.rec_size), sig_cap=budget, span_cap=o.window_spans,
+                            group_cap=max(1, groups_of(0, N, G)), user_cap=max(1024, o.window_events // 4),
+                            window_ms=float(o.window_ms), ttft_slo_ms=o.ttft_slo_ms, halo_ms=o.halo_ms,
+                            import_cap=icap, xchg_cap=xchg, model_image=np.asarray(image, np.uint8).tobytes(),
+                            pods=pods, master=("127.0.0.1", port)) for r in range(N)]
+        state = self._state_path()
+        if state and os.path.exists(state):
+            self.load_state(state)
+        pool = WorkerPool(specs, (ring, user, spans), in_process=N == 1)
+        self.pool = pool
+        print(f"window engine: {o.engine} x {N} worker(s), model {self.model_meta.get('name')}"
+              f"{' T=%.3g' % self.model_meta['temperature'] if 'temperature' in self.model_meta else ''}",
+              file=sys.stderr)
         if o.source == "bpf":
             self._scan_pods(maps)
-        G = o.window_groups
         names = [f"svc-{g + 1}" for g in range(G)]
         receiver = None
+        mapper = None
         if o.otlp_receiver_bind and spans is not None:
             from ..collector.otlp import GroupTable, OtlpSpanReceiver, SpanMapper
 
             groups = GroupTable(G)
             names = groups.names  # incident groups are the services the receiver has seen
-            receiver = OtlpSpanReceiver(o.otlp_receiver_bind, SpanMapper(groups, self.pod_ids.id, node_id),
-                                        spans.push).start()
+            mapper = SpanMapper(groups, self.pod_ids.id, node_id)
+            receiver = OtlpSpanReceiver(o.otlp_receiver_bind, mapper, spans.push, allow=o.otlp_receiver_allow).start()
             self.receiver = receiver
         if self.guard is not None:
+            self.guard.source = TreeCPUSampler(lambda: [os.getpid()] + pool.pids())
             self.guard.evaluate()
+        clock = EpochClock()
         self.ready = True
         period = o.window_ms / 1000.0
         nxt = time.monotonic() + period
-        pending = None
-        while not self.stop_event.is_set():
-            self.stop_event.wait(max(0.0, nxt - time.monotonic()))
-            if self.stop_event.is_set():
-                break
-            nxt += period
-            cut = src.cut()
-            t_h = time.perf_counter()
-            k = src.stage(cut, G, with_labels=False, learn=False)["k"]
-            host_us = 1e6 * (time.perf_counter() - t_h)
-            if pending is not None:
-                self._emit_window(pipe, *pending)
-            pending = (k, cut.t_ns, G, names, ring, host_us)
-            if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
-                self._scan_pods(maps)  # pod churn
-            if ckpt and o.checkpoint_every > 0 and self.windows_done % o.checkpoint_every == 0:
-                self._checkpoint(pipe, ckpt)
-            self._guard_tick()
-            self.metrics.set_heartbeat()
-            self.windows_done += 1
-            if max_windows and self.windows_done >= max_windows:
-                break
-            if maps.ctx_ids_used() > (7 << 20) and hasattr(maps, "reset_ctx_ids"):
-                maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
+        cut_t = {}
+        windows = 0
         try:
-            if pending is not None:
-                self._emit_window(pipe, *pending)
-            src.drain()
-            self.last_summary = pipe.summary()
-            if ckpt:
-                self._checkpoint(pipe, ckpt)
+            while not self.stop_event.is_set():
+                self.stop_event.wait(max(0.0, nxt - time.monotonic()))
+                if self.stop_event.is_set():
+                    break
+                nxt += period
+                t = time.time_ns()
+                maps.cfg_set(bpf.CFG_EPOCH, clock.publish(t))  # epoch first, then the ring snapshots
+                cut = Cut(kernel=ring.producer_pos, user=user.head, spans=spans.head, bases=clock.bases(), t_ns=t)
+                replies = pool.window(cut, G, mapper.take_pod_updates() if mapper is not None else None)
+                cut_t[replies[0]["k"]] = t
+                prev = replies[0].get("prev")
+                if prev is not None:
+                    self._emit_window(replies, cut_t.pop(prev["k"], t), G, names, ring, model)
+                if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
+                    self._scan_pods(maps)  # pod churn
+                self.windows_done += 1
+                windows += 1
+                if state and o.checkpoint_every > 0 and self.windows_done % o.checkpoint_every == 0:
+                    self.save_state(state)
+                self._guard_tick()
+                self.metrics.set_heartbeat()
+                if max_windows and windows >= max_windows:
+                    break
+                if maps.ctx_ids_used() > (7 << 20) and hasattr(maps, "reset_ctx_ids"):
+                    maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
+            final = pool.stop()
+            if final and final[0].get("prev") is not None:
+                self._emit_window(final, cut_t.pop(final[0]["prev"]["k"], time.time_ns()), G, names, ring, model)
+            self.last_summary = final[0].get("summary") if final else None
+            if state:
+                self.save_state(state)
         finally:
-            # unregister the rings from the GPU and free device memory while the ring mappings
-            # still exist (interpreter teardown order is arbitrary)
-            pipe.eng.close()
+            # workers unregister the rings from their GPUs and free device memory while the
+            # ring mappings still exist (interpreter teardown order is arbitrary)
+            pool.close()
             if receiver is not None:
                 receiver.stop()
             if getattr(self, "probe_manager", None) is not None:

@@ -1,0 +1,355 @@
+"""Window workers of the node agent: one per GPU (``agent --gpus N``).
+
+REF runs one agent per node and fans its per-probe readers into one stream
+(/root/reference/deploy/k8s/daemonset.yaml:1-20, pkg/collector/ringbuf.go:97-112). On an MI355X
+node the agent's window engine can use every GPU of the node, so the agent splits into:
+
+* the **controller** (the agent process, agent/daemon.py): the window clock and the node's only
+  ``mislo_cfg`` writer (epochs, node id, emit floors), the cuts of the node's rings, pod
+  discovery and the OTLP receiver (the pod -> service table), metrics, outputs, webhook, the
+  overhead guard over the whole process tree. It never initialises HIP;
+* one **worker per GPU** (a spawned process; ``LocalWorker`` runs the same core in-process when
+  the node uses one GPU): a WindowPipeline on its GPU over the SAME rings, consuming every cut.
+  Group sharding splits the stream on the device (decode.hip ``shard_owns``): worker r counts and
+  joins only the records and spans of the services it owns (service s -> worker (s - 1) % N), so
+  an incident is scored entirely on one GPU; cross-service trace joins go through the engine's
+  trace-row exchange, node-wide histograms through its packet all-reduce, and worker 0 receives
+  every worker's incident results through the all-gather (RCCL over xGMI; gloo for the CPU
+  engine). Workers never move ring consumer positions: each reports how far it is done and the
+  controller frees ring space up to the slowest worker.
+
+Protocol (multiprocessing pipes, pickled, O(groups) bytes per window): controller -> worker
+``("window", cut, n_groups, pods)`` every window, ``("stop",)``; worker -> controller one reply per
+window with its release positions, its ring accounting and -- worker 0 only -- the previous
+window's node-wide packet and all workers' incident results.
+"""
+
+from __future__ import annotations
+
+import os
+import time
+import traceback
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+RING_TAIL = 8  # ring accounting slots at the packet's tail (pipeline/window.py PACKET_LAYOUT[-1])
+
+
+@dataclass
+class WorkerSpec:
+    rank: int
+    world: int
+    device: int
+    engine: str                 # gpu | cpu
+    source: str                 # bpf | shm (replay rings are shm rings)
+    ring_name: str              # RingNames prefix
+    pin_dir: str
+    user_rec: int
+    sig_cap: int
+    span_cap: int
+    group_cap: int              # incident groups per worker: ceil(G / world) on every worker (the all-gather
+                                # of the results needs equal blocks)
+    user_cap: int
+    window_ms: float
+    ttft_slo_ms: float
+    halo_ms: float
+    import_cap: int
+    xchg_cap: int
+    model_image: bytes
+    pods: Optional[Tuple[np.ndarray, np.ndarray]] = None
+    master: Tuple[str, int] = ("127.0.0.1", 0)   # gloo rendezvous (cpu engine)
+    env: Dict[str, str] = field(default_factory=dict)
+
+
+def groups_of(rank: int, world: int, n_groups: int) -> int:
+    """Incident groups g < n_groups with g % world == rank (local index g // world)."""
+    return len(range(rank, n_groups, world))
+
+
+def merge_results(parts: List[dict], n_groups: int) -> dict:
+    """Every worker's local incident results -> the node's, in global group order
+    (group g = local g // world of worker g % world)."""
+    world = len(parts)
+    out = {}
+    for key in ("post", "conf", "feat", "pred", "evbits", "sli"):
+        ref = np.asarray(parts[0][key])
+        arr = np.zeros((n_groups,) + ref.shape[1:], dtype=ref.dtype)
+        for r, p in enumerate(parts):
+            n = groups_of(r, world, n_groups)
+            arr[r::world][:n] = np.asarray(p[key])[:n]
+        out[key] = arr
+    return out
+
+
+class WorkerCore:
+    """One GPU's share of the node's windows (the body of a worker process, or of LocalWorker)."""
+
+    def __init__(self, spec: WorkerSpec, comm=None, group=None, shared: bool = True, rings=None):
+        """``rings``: the controller's own ring objects (in-process worker); a worker process maps
+        the rings itself (the pinned BPF ring, the named shared-memory rings)."""
+        from ..collector import bpf
+        from ..pipeline.window import RingWindowSource, WindowPipeline
+        from ..runtime import load
+
+        self.spec = spec
+        if rings is None:
+            rt = load()
+            names = bpf.RingNames.of(spec.ring_name)
+            if spec.source == "bpf":
+                ring = rt.Ringbuf.open_pinned(os.path.join(spec.pin_dir, "mislo_events"))
+            else:
+                ring = rt.Ringbuf.attach_shm(names.ring)
+            rings = (ring, rt.HostRing(0, spec.user_rec, names.user, True), rt.HostRing(0, 64, names.spans, True))
+        ring, user, spans = rings
+        self.rings = rings
+        self.pipe = WindowPipeline(spec.sig_cap, spec.span_cap, spec.group_cap, spec.device, comm, model="bayes",
+                                   learn=False, window_ms=2000.0, user_cap=spec.user_cap,
+                                   ttft_slo_ms=spec.ttft_slo_ms, halo_ms=spec.halo_ms, import_cap=spec.import_cap,
+                                   xchg_cap=spec.xchg_cap, shard=(spec.rank, spec.world), engine=spec.engine,
+                                   group=group, model_image=np.frombuffer(spec.model_image, dtype=np.uint8))
+        # the controller publishes the epochs: this source never writes mislo_cfg
+        self.src = RingWindowSource(self.pipe, ring, user, spans, cfg_set=lambda i, v: None, shared=shared)
+        if spec.pods is not None:
+            self.pipe.eng.set_pods(*spec.pods)
+        self.pending: Optional[Tuple[int, float]] = None
+        self.windows = 0
+
+    def window(self, cut, n_groups: int, pods=None) -> dict:
+        """Stage window k; return what the controller needs of window k-1 (finished by now or
+        nearly: the engine runs nb windows deep)."""
+        if pods is not None and len(pods[0]):
+            self.pipe.eng.set_pods(*pods)
+        t0 = time.perf_counter()
+        r = self.src.stage(cut, n_groups, with_labels=False, learn=False)
+        host_us = 1e6 * (time.perf_counter() - t0)
+        out = {"rank": self.spec.rank, "k": r["k"], "staged": r, "done": self.src.done()}
+        prev, self.pending = self.pending, (r["k"], host_us, n_groups)
+        if prev is not None:
+            out["prev"] = self._collect(*prev)
+        self.windows += 1
+        return out
+
+    def _collect(self, k: int, host_us: float, n_groups: int) -> dict:
+        pipe = self.pipe
+        pipe.wait(k)
+        pk = np.asarray(pipe.eng.packet(k), dtype=np.float64)
+        d = {"k": k, "ring": pk[-RING_TAIL:].copy(), "host_us": host_us, "latency_ms": float(pipe.window_ms(k)[0])}
+        if self.spec.rank == 0:  # the node-wide packet and every worker's incidents (all-gathered)
+            d["packet"] = pk
+            d["results"] = pipe.results_all(k, n_groups) if self.spec.world > 1 else [pipe.results(k, n_groups)]
+        return d
+
+    def stop(self) -> dict:
+        out = {"rank": self.spec.rank, "done": None}
+        if self.pending is not None:
+            out["prev"] = self._collect(*self.pending)
+            self.pending = None
+        self.src.drain()
+        out["done"] = self.src.done()
+        out["summary"] = self.pipe.summary() if self.spec.rank == 0 else None
+        return out
+
+    def close(self) -> None:
+        self.pipe.eng.close()
+
+
+# ---------------------------------------------------------------------------------------
+# process plumbing
+# ---------------------------------------------------------------------------------------
+
+def worker_main(spec: WorkerSpec, conn) -> None:
+    """Spawned worker process: comm bring-up, then one reply per window until "stop"."""
+    os.environ.update(spec.env)
+    core = None
+    group = None
+    try:
+        comm = None
+        if spec.world > 1 and spec.engine == "gpu":
+            from ..ops import load_agent
+
+            mod = load_agent()
+            if spec.rank == 0:  # the communicator's id travels through the controller
+                uid = mod.unique_id()
+                conn.send(("uid", uid))
+            else:
+                uid = conn.recv()[1]
+            comm = (uid, spec.rank, spec.world)
+        elif spec.world > 1:
+            import torch.distributed as dist
+
+            os.environ.update(MASTER_ADDR=spec.master[0], MASTER_PORT=str(spec.master[1]))
+            dist.init_process_group("gloo", rank=spec.rank, world_size=spec.world)
+            group = dist.group.WORLD
+        core = WorkerCore(spec, comm=comm, group=group, shared=True)
+        conn.send(("ready", {"rank": spec.rank, "pid": os.getpid(), "device": spec.device}))
+        while True:
+            msg = conn.recv()
+            if msg[0] == "window":
+                conn.send(("window", core.window(*msg[1:])))
+            elif msg[0] == "stop":
+                conn.send(("stopped", core.stop()))
+                break
+            else:
+                raise ValueError(f"unknown worker message {msg[0]!r}")
+    except (EOFError, KeyboardInterrupt):
+        pass
+    except Exception:  # noqa: BLE001 - reported to the controller, then fatal
+        try:
+            conn.send(("error", traceback.format_exc()))
+        except (OSError, BrokenPipeError):
+            pass
+        raise
+    finally:
+        if core is not None:
+            core.close()
+        if group is not None:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+
+
+class WorkerError(RuntimeError):
+    pass
+
+
+class RemoteWorker:
+    """Controller-side handle of a spawned worker process."""
+
+    def __init__(self, spec: WorkerSpec, ctx):
+        self.spec = spec
+        self.conn, child = ctx.Pipe()
+        self.proc = ctx.Process(target=worker_main, args=(spec, child), name=f"mislo-worker-{spec.rank}", daemon=True)
+        self.proc.start()
+        child.close()
+
+    @property
+    def pid(self) -> int:
+        return int(self.proc.pid or 0)
+
+    def recv(self, timeout: float = 600.0):
+        if not self.conn.poll(timeout):
+            raise WorkerError(f"worker {self.spec.rank} did not answer in {timeout:.0f} s")
+        try:
+            msg = self.conn.recv()
+        except EOFError as exc:
+            raise WorkerError(f"worker {self.spec.rank} exited (code {self.proc.exitcode})") from exc
+        if msg[0] == "error":
+            raise WorkerError(f"worker {self.spec.rank} failed:\n{msg[1]}")
+        return msg
+
+    def send(self, msg) -> None:
+        self.conn.send(msg)
+
+    def close(self, timeout: float = 30.0) -> None:
+        self.proc.join(timeout)
+        if self.proc.is_alive():
+            self.proc.terminate()
+            self.proc.join(10)
+        if self.proc.is_alive():
+            self.proc.kill()
+            self.proc.join(5)
+
+
+class LocalWorker:
+    """The same core in the controller's process (a node agent on one GPU: no extra process)."""
+
+    def __init__(self, spec: WorkerSpec, rings=None):
+        self.spec = spec
+        self.core = WorkerCore(spec, shared=False, rings=rings)
+        self._reply = None
+
+    @property
+    def pid(self) -> int:
+        return os.getpid()
+
+    def send(self, msg) -> None:
+        if msg[0] == "window":
+            self._reply = ("window", self.core.window(*msg[1:]))
+        elif msg[0] == "stop":
+            self._reply = ("stopped", self.core.stop())
+
+    def recv(self, timeout: float = 600.0):
+        r, self._reply = self._reply, None
+        return r
+
+    def close(self, timeout: float = 30.0) -> None:
+        self.core.close()
+
+
+class WorkerPool:
+    """The node's workers: bring-up (RCCL id relay), per-window fan-out / fan-in, and the ring
+    space release up to the slowest worker."""
+
+    def __init__(self, specs: List[WorkerSpec], rings, in_process: bool = False):
+        import multiprocessing as mp
+
+        self.rings = rings  # the controller's own mappings: (BPF ring, user ring, span ring)
+        self.world = len(specs)
+        if in_process:
+            if self.world != 1:
+                raise ValueError("in-process workers: exactly one")
+            self.workers = [LocalWorker(specs[0], rings)]
+        else:
+            ctx = mp.get_context("spawn")
+            self.workers = [RemoteWorker(s, ctx) for s in specs]
+            try:
+                if self.world > 1 and specs[0].engine == "gpu":
+                    uid = self.workers[0].recv()[1]
+                    for w in self.workers[1:]:
+                        w.send(("uid", uid))
+                for w in self.workers:
+                    w.recv()  # ("ready", info)
+            except BaseException:
+                self.close()
+                raise
+        self.in_process = in_process
+        r = rings
+        self._rel_user = r[1].tail if r[1] is not None else 0
+        self._rel_spans = r[2].tail if r[2] is not None else 0
+
+    def pids(self) -> List[int]:
+        return [w.pid for w in self.workers]
+
+    def window(self, cut, n_groups: int, pods=None) -> List[dict]:
+        for w in self.workers:
+            w.send(("window", cut, groups_of(w.spec.rank, self.world, n_groups), pods))
+        replies = [w.recv()[1] for w in self.workers]
+        self._release(replies)
+        return replies
+
+    def _release(self, replies: List[dict]) -> None:
+        if self.in_process:
+            return  # the single source frees its rings itself
+        ring, user, spans = self.rings
+        dones = [r["done"] for r in replies if r.get("done") is not None]
+        if not dones:
+            return
+        k = min(d[0] for d in dones)
+        if ring is not None and k > ring.consumer_pos:
+            ring.set_consumer_pos(k)
+        u = min(d[1] for d in dones)
+        if user is not None and u > self._rel_user:
+            user.release(u - self._rel_user)
+            self._rel_user = u
+        s = min(d[2] for d in dones)
+        if spans is not None and s > self._rel_spans:
+            spans.release(s - self._rel_spans)
+            self._rel_spans = s
+
+    def stop(self) -> List[dict]:
+        for w in self.workers:
+            w.send(("stop",))
+        replies = []
+        for w in self.workers:
+            try:
+                replies.append(w.recv(120)[1])
+            except WorkerError:
+                replies.append({"rank": w.spec.rank, "done": None})
+        self._release(replies)
+        return replies
+
+    def close(self) -> None:
+        for w in self.workers:
+            w.close()

@@ -1,9 +1,9 @@
 """`agent`: node DaemonSet process (REF cmd/agent/main.go:269-633; flags :334-373).
 
 REF flags are all accepted with REF defaults. Additive flags select the MI355X window
-engine: ``--engine gpu --source bpf|shm|replay --pin-dir --window-ms --window-events --device
---model --min-confidence --ttft-slo-ms --slo-target``; ``--count`` bounds the number of
-windows in GPU mode.
+engine: ``--engine gpu|cpu --source bpf|shm|replay --gpus --pin-dir --window-ms --window-events
+--device --model --model-path --min-confidence --ttft-slo-ms --slo-target``; ``--count`` bounds the
+number of windows in window-engine mode.
 """
 
 from __future__ import annotations
@@ -19,9 +19,17 @@ from ..collector.probes import probe_smoke_check
 from ._common import GoFlags, eprint, is_version_request, print_version, split_csv
 
 
+ENGINES = ("synthetic", "gpu", "cpu")
+SOURCES = ("bpf", "shm", "replay")
+MODELS = ("bayes", "bayes_gpu", "bayes_learned", "lda")
+
+
 def parse(argv: List[str]) -> (AgentOptions, bool):
     d = AgentOptions()
     p = GoFlags("agent", "LLM SLO node agent (MI355X window engine)")
+    # the additive flags are checked at parse time; REF's own flags keep REF's post-parse
+    # validation (exit 1, cmd/agent/main.go)
+    choices = {"engine": ENGINES, "source": SOURCES, "model": MODELS}
     for name, default, help_ in [
         ("cluster", d.cluster, "cluster name"), ("namespace", d.namespace, "namespace"),
         ("workload", d.workload, "workload"), ("service", d.service, "service"),
@@ -47,8 +55,15 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("enable-real-probe-metrics", True, "enable probe-derived metrics on /metrics"),
         ("metrics-bind", d.metrics_bind, "metrics and health bind address"),
         ("probe-smoke", False, "run eBPF smoke check and exit"),
-        ("engine", d.engine, "attribution engine: synthetic (REF tick loop) | gpu (MI355X window engine)"),
-        ("source", d.source, "gpu engine record source: bpf (pinned probe maps) | shm (emulated rings) | replay"),
+        ("engine", d.engine, "attribution engine: synthetic (REF tick loop) | gpu (MI355X window engine) | cpu "
+                             "(the window engine's contract on the host: the numpy oracle; hosts without a GPU)"),
+        ("source", d.source, "window engine record source: bpf (pinned probe maps) | shm (emulated rings) | replay"),
+        ("gpus", d.gpus, "window workers, one per GPU (0 = every GPU visible to the agent); each owns a share of "
+                         "the node's services, node-wide results over RCCL"),
+        ("model-path", d.model_path, "trained attribution model (safetensors) written by `attributor --train`; "
+                                     "overrides --model"),
+        ("otlp-receiver-allow", d.otlp_receiver_allow, "comma-separated CIDRs allowed to export spans to the "
+                                                       "receiver (empty = any)"),
         ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
         ("pin-dir", d.pin_dir, "bpffs directory the probe loader pinned the maps in (--source bpf)"),
         ("probe-objs", d.probe_objs, "--source bpf: directory of compiled probes (*.bpf.o) the agent loads and "
@@ -72,7 +87,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                              "each MI355X queue pins ~173 MB of host memory; 1 serialises copy and compute, ample "
                              "at node event rates; 0 = runtime default)"),
     ]:
-        p.flag(name, default, help_)
+        p.flag(name, default, help_, choices=choices.get(name))
     a = p.parse_args(argv)
     o = AgentOptions(
         cluster=a.cluster, namespace=a.namespace, workload=a.workload, service=a.service, node=a.k8s_node,
@@ -89,7 +104,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
         otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
-        checkpoint_every=int(a.checkpoint_every))
+        checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), model_path=a.model_path,
+        otlp_receiver_allow=a.otlp_receiver_allow)
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])
         if given:  # an operator's flag wins over a node-wide GPU_MAX_HW_QUEUES
@@ -123,13 +139,18 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 1
     agent.start_server()
     agent.start_hello_tracer()
-    if opts.engine == "gpu":
-        from ..ops import load_agent
+    if opts.engine in ("gpu", "cpu"):
+        if opts.engine == "gpu":
+            from ..ops import load_agent
 
-        # the native engine must be built: fail loudly, never fall back (import only: the replay
-        # source forks its producer before the engine initialises the HIP runtime)
-        load_agent(init=False)
-        return run_forever(agent, lambda: agent.run_windows(max_windows=opts.count))
+            # the native engine must be built: fail loudly, never fall back (import only: this
+            # process forks the replay producer and spawns the GPU workers; it never initialises HIP)
+            load_agent(init=False)
+        try:
+            return run_forever(agent, lambda: agent.run_windows(max_windows=opts.count))
+        except Exception as exc:  # noqa: BLE001 - a worker or source failure ends the agent (k8s restarts it)
+            eprint(f"window engine failed: {exc}")
+            return 1
     try:
         return run_forever(agent, agent.run_synthetic)
     except Exception as exc:  # noqa: BLE001 - REF: emit failures are fatal (exit 1)

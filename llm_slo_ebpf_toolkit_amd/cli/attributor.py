@@ -2,10 +2,19 @@
 (REF cmd/attributor/main.go:37-327).
 
 Flags match REF (--input --out --summary-out --confusion-out --schema --config
---attribution-mode --webhook-*). Additive: ``--attribution-mode`` also accepts
-``bayes_learned`` / ``lda`` (models/bayes.py), and ``--device gpu`` scores the batch with
-the MFMA posterior kernel (ops/csrc/posterior.hip) instead of numpy; the summary gains
-macro-F1 and per-class P/R/F1, which REF's report template asks for.
+--attribution-mode --webhook-*). Additive:
+
+* ``--device gpu`` scores the batch with the window engine's MFMA posterior kernel
+  (ops/csrc/posterior.hip through WindowEngine.score) instead of numpy;
+* ``--model-path FILE`` scores with a trained model file (models/train.py), the file the agent
+  loads with the same flag;
+* ``--train --out FILE`` trains that file: from ``--input`` (labelled FaultSamples with signals;
+  a multi-fault row's mass spread over its expected domains) or, without it, from the fixed
+  fault-replay training set (single and compound faults of REF's profiles) whose incident
+  features the window engine's CPU oracle computes from the records; calibrated by a held-out
+  temperature. ``--summary-out`` then reports the fit and REF's 55-row scores of the new model.
+
+The summary gains macro-F1, per-class P/R/F1, partial and coverage accuracy.
 """
 
 from __future__ import annotations
@@ -42,26 +51,62 @@ def write_confusion_csv(path: str, samples, predictions) -> None:
             w.writerow([act, pred, m[(act, pred)]])
 
 
-def gpu_attributions(samples: List[FaultSample], mode: str):
-    """Score the batch with the HIP posterior kernel; returns IncidentAttributions."""
+def gpu_attributions(samples: List[FaultSample], model):
+    """Score the batch with the window engine's posterior kernel (WindowEngine.score, the
+    agent's engine); returns IncidentAttributions."""
     import numpy as np
-    import torch
 
-    from ..models.bayes import get_model, samples_to_arrays
-    from ..ops.engine import GpuEngine
+    from ..models.bayes import samples_to_arrays
+    from ..ops import load_agent
+    from ..ops.engine import model_bytes
 
-    model = get_model(metrics.normalize_mode(mode))
     vals, _ = samples_to_arrays(samples)
-    eng = GpuEngine(8, 8, max(1, len(samples)))
-    eng.set_model(model)
-    e = eng.eng
-    e.feat[: len(samples)].copy_(torch.from_numpy(vals.astype(np.float32)))
-    e.counts[:4].copy_(torch.tensor([0, 0, len(samples), 0], dtype=torch.int32))
-    e.bind_io(e.counts, e.labels, e.packet)
-    e.posterior(False)
-    post = e.post[: len(samples)].cpu().numpy()
-    bits = e.evbits[: len(samples)].cpu().numpy().view(np.uint32)
+    eng = load_agent().WindowEngine(sig_cap=1024, span_cap=64, group_cap=64, user_cap=64, n_buffers=2,
+                                    max_ahead=2, use_graphs=False, device_refit=False)
+    try:
+        eng.set_model_bytes(model_bytes(model))
+        r = eng.score(np.ascontiguousarray(vals, dtype=np.float32), None)
+    finally:
+        eng.close()
+    post, bits = r["post"], r["evbits"].view(np.uint32)
     return [model.attribution_from_posterior(s, post[i], bits[i]) for i, s in enumerate(samples)]
+
+
+def train_main(a) -> int:
+    """attributor --train: fit, calibrate and write a model file (agent --model-path)."""
+    import numpy as np
+
+    from ..models import train as mtrain
+    from ..models.bayes import label_code
+    from ..signals import catalog
+
+    cfg = mtrain.TrainConfig(windows=a.train_windows, events_per_window=a.train_events,
+                             spans_per_window=a.train_spans, seed=a.seed)
+    if a.input:
+        rows = [s for s in load_samples_jsonl(a.input) if s.signals and s.expected_set()]
+        if not rows:
+            eprint(f"{a.input}: no labelled rows with signals")
+            return 1
+        feats = np.array([catalog.feature_vector(s.signals) for s in rows], dtype=np.float32)
+        codes = np.array([label_code(catalog.DOMAIN_INDEX[s.expected_set()[0]],
+                                     [catalog.DOMAIN_INDEX[d] for d in s.expected_set()]) for s in rows], np.int32)
+        tm = mtrain.fit(feats, codes, np.arange(len(rows)), cfg)
+        tm.meta.update({"engine": "labelled-samples", "input": a.input, "config": cfg.__dict__})
+    else:
+        tm = mtrain.train_cpu(cfg)
+    fx = a.ref55 if a.ref55 and os.path.exists(a.ref55) else ""
+    if fx:
+        tm.meta["ref55"] = mtrain.ref55_report(fx, mtrain.host_scorer(tm.model))
+    if a.out in ("", "-"):
+        eprint("--train needs --out FILE")
+        return 2
+    mtrain.save_model(a.out, tm)
+    if a.summary_out:
+        ensure_parent(a.summary_out)
+        with open(a.summary_out, "w", encoding="utf-8") as fh:
+            json.dump({"model": a.out, **tm.meta}, fh, indent=2, default=str)
+    eprint(f"trained {a.out}: T = {tm.temperature:.3f}, active domains {tm.meta.get('active_domains')}")
+    return 0
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -90,7 +135,17 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.flag("webhook-timeout-ms", int(cfg.webhook.timeout_ms), "webhook timeout in milliseconds")
     p.flag("webhook-strict", False, "fail command when webhook delivery fails")
     p.flag("device", "cpu", "posterior device: cpu|gpu (MFMA posterior kernel)", choices=("cpu", "gpu"))
+    p.flag("model-path", "", "score with a trained model file (attributor --train / the agent's --model-path)")
+    p.flag("train", False, "train a model file (--out) from --input labelled samples or the fault-replay set")
+    p.flag("train-windows", 32, "--train without --input: fault-replay training windows")
+    p.flag("train-events", 16384, "--train: events per training window")
+    p.flag("train-spans", 1024, "--train: spans per training window")
+    p.flag("seed", 42, "--train: replay and random-init seed")
+    p.flag("ref55", os.path.join("tests", "fixtures", "ref_multi_fault_samples.jsonl"),
+           "--train: REF's 55 labelled rows to score the new model on (skipped if absent)")
     a = p.parse_args(argv)
+    if a.train:
+        return train_main(a)
     if a.config.strip() != cfg_path.strip():
         try:
             cfg = toolkitcfg.load(a.config)
@@ -103,8 +158,27 @@ def main(argv: Optional[List[str]] = None) -> int:
         eprint(f"failed to load samples: {exc}")
         return 1
     mode = a.attribution_mode
-    if a.device == "gpu" and metrics.normalize_mode(mode) != metrics.MODE_RULE:
-        preds = gpu_attributions(samples, mode)
+    model = None
+    if a.model_path:
+        from ..models.train import load_model
+
+        try:
+            model = load_model(a.model_path)[0]
+        except (OSError, ValueError) as exc:
+            eprint(f"failed to load model: {exc}")
+            return 1
+        mode = f"model:{os.path.basename(a.model_path)}"
+    elif metrics.normalize_mode(mode) != metrics.MODE_RULE:
+        from ..models.bayes import get_model
+
+        if metrics.normalize_mode(mode) in ("bayes_learned", "lda"):
+            eprint(f"attribution-mode {mode} is learned: give --model-path (attributor --train writes one)")
+            return 1
+        model = get_model(metrics.normalize_mode(mode))
+    if model is not None and a.device == "gpu":
+        preds = gpu_attributions(samples, model)
+    elif model is not None:
+        preds = [model.attribute_sample(s) for s in samples]
     else:
         preds = metrics.build_attributions(samples, mode)
     schema = a.schema if os.path.exists(a.schema) else "incident-attribution"

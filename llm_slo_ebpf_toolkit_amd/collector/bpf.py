@@ -35,6 +35,16 @@ CFG_CLOCK, CFG_NODE, CFG_EPOCH, CFG_TRACE_NEXT, CFG_CTX_NEXT = 0, 1, 124, 125, 1
 PIN_DIR = "/sys/fs/bpf/mislo"
 
 
+def stable_node_id(name: str) -> int:
+    """The node's 16-bit id in [1, 0xFFFE] (mislo_cfg[1], the svc|node join key): the first two
+    bytes of the BLAKE2b digest of the node name -- the same in every process and across
+    restarts (Python's str hash is salted per process)."""
+    import hashlib
+
+    v = int.from_bytes(hashlib.blake2b(str(name).encode("utf-8"), digest_size=2).digest(), "little")
+    return min(max(v, 1), 0xFFFE)
+
+
 def cfg_floor(signal_type: int) -> int:
     return 2 + int(signal_type)
 

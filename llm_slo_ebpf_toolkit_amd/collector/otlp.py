@@ -258,6 +258,21 @@ class SpanMapper:
 
     def __init__(self, groups: GroupTable, pod_id: Callable[[str], int], node_id: int = 0):
         self.groups, self.pod_id, self.node_id = groups, pod_id, node_id
+        # pod id -> svc << 16 | node as the spans reveal it: the window engine's pod table, so the
+        # kernel's and the rocprof tool's records of a pod carry its service (the service+node join
+        # tier, and the service that decides which GPU owns them, agent --gpus N)
+        self._pods: Dict[int, int] = {}
+        self._new: Dict[int, int] = {}
+        self._plock = threading.Lock()
+
+    def take_pod_updates(self) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+        """(pod ids, svc|node) learned since the last call, or None."""
+        with self._plock:
+            if not self._new:
+                return None
+            new, self._new = self._new, {}
+        ids = np.array(list(new), dtype=np.uint32)
+        return ids, np.array([new[int(i)] for i in ids.tolist()], dtype=np.uint32)
 
     @staticmethod
     def is_request_span(d: dict) -> bool:
@@ -283,9 +298,16 @@ class SpanMapper:
             out[i]["trace_h"] = trace_hash(d.get("traceId"))
             out[i]["span_h"] = span_hash(d.get("spanId"))
             out[i]["pid"] = int(pid)
-            out[i]["pod_id"] = self.pod_id(str(pod)) if pod else 0
+            pid_ = self.pod_id(str(pod)) if pod else 0
+            out[i]["pod_id"] = pid_
             out[i]["node_id"] = self.node_id
             out[i]["svc_id"] = g + 1
+            if pid_:
+                sn = ((g + 1) << 16) | (self.node_id & 0xFFFF)
+                if self._pods.get(pid_) != sn:
+                    with self._plock:
+                        self._pods[pid_] = sn
+                        self._new[pid_] = sn
             out[i]["group_id"] = g
             out[i]["ttft_ms"] = float(ttft) if ttft is not None else np.nan
             out[i]["latency_ms"] = (t1 - t0) / 1e6
@@ -298,11 +320,19 @@ class OtlpSpanReceiver:
     """POST /v1/traces -> span ring. ``push(records) -> n accepted`` is the ring's push (the
     span ring is multi-producer: services may also push records directly)."""
 
-    def __init__(self, bind: str, mapper: SpanMapper, push: Callable[[np.ndarray], int]):
+    MAX_BODY = 4 << 20  # bytes per export request (OTLP exporters batch well below this)
+
+    def __init__(self, bind: str, mapper: SpanMapper, push: Callable[[np.ndarray], int], allow: str = "",
+                 max_body: int = MAX_BODY):
+        """``allow``: comma-separated CIDRs of peers that may export (empty = any): the agent binds
+        on the host network, so without it any node that reaches the port could inject spans."""
         self.mapper, self.push = mapper, push
         host, _, port = bind.rpartition(":")
         self.addr = (host or "127.0.0.1", int(port))
+        self.max_body = int(max_body)
+        self.allow = [ipaddress.ip_network(c.strip(), strict=False) for c in allow.split(",") if c.strip()]
         self.accepted = self.rejected = self.dropped = self.requests = 0
+        self.refused = 0  # peers outside the allow-list, oversized or unframed bodies
         self._lock = threading.Lock()
         self._srv: Optional[http.server.ThreadingHTTPServer] = None
         self._thr: Optional[threading.Thread] = None
@@ -335,11 +365,32 @@ class OtlpSpanReceiver:
                 self.end_headers()
                 self.wfile.write(body)
 
+            def _refuse(self, code: int, msg: bytes) -> None:
+                with rx._lock:
+                    rx.refused += 1
+                self.close_connection = True
+                self._reply(code, msg, "text/plain")
+
             def do_POST(self):
+                if rx.allow:
+                    try:
+                        peer = ipaddress.ip_address(self.client_address[0])
+                    except ValueError:
+                        peer = None
+                    if peer is None or not any(peer in net for net in rx.allow):
+                        self._refuse(403, b"forbidden")
+                        return
                 if not self.path.startswith("/v1/traces"):
                     self._reply(404, b"not found", "text/plain")
                     return
-                n = int(self.headers.get("Content-Length") or 0)
+                try:
+                    n = int(self.headers.get("Content-Length", ""))
+                except ValueError:  # chunked or missing: the body size must be known up front
+                    self._refuse(411, b"length required")
+                    return
+                if n < 0 or n > rx.max_body:  # refused before a byte of it is read
+                    self._refuse(413, b"request body too large")
+                    return
                 body = self.rfile.read(n) if n > 0 else b""
                 ctype = self.headers.get("Content-Type", "application/json")
                 try:

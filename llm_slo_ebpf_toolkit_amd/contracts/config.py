@@ -172,7 +172,7 @@ def normalize(cfg: ToolkitConfig) -> ToolkitConfig:
         cfg.gpu.window_ms = d.gpu.window_ms
     if cfg.gpu.max_events_per_window <= 0:
         cfg.gpu.max_events_per_window = d.gpu.max_events_per_window
-    if cfg.gpu.world_size <= 0:
+    if cfg.gpu.world_size < 0:  # 0 = every GPU visible to the agent (agent --gpus 0)
         cfg.gpu.world_size = d.gpu.world_size
     return cfg
 

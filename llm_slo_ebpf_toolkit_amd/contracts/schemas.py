@@ -172,7 +172,7 @@ def toolkit_config_schema() -> Dict[str, Any]:
         # NEW additive block: GPU engine knobs.
         "gpu": _obj({"enabled": _bool(default=True), "window_ms": _int(1, default=1000),
                      "max_events_per_window": _int(1, default=1 << 20),
-                     "world_size": _int(1, default=1),
+                     "world_size": _int(0, default=1),  # 0 = every GPU visible to the agent
                      "attribution_model": _enum(("bayes", "bayes_gpu", "bayes_learned", "lda", "rule"),
                                                 default="bayes")}),
     }

@@ -204,6 +204,17 @@ class BurnRateForecaster:
     def error(self) -> Optional[float]:
         return float(sum(self.scored) / len(self.scored)) if self.scored else None
 
+    def state(self) -> dict:
+        """JSON-able state (agent checkpoint): per-key window history and pending forecasts."""
+        return {"hist": {str(k): v for k, v in self._hist.items()},
+                "pending": {str(k): v for k, v in self._pending.items()},
+                "scored": self.scored[-10000:]}
+
+    def restore(self, st: dict) -> None:
+        self._hist = {k: [tuple(x) for x in v] for k, v in (st.get("hist") or {}).items()}
+        self._pending = {k: [tuple(x) for x in v] for k, v in (st.get("pending") or {}).items()}
+        self.scored = [float(x) for x in st.get("scored") or []]
+
 
 def simulate_burn_prediction_error(burn_rates: Sequence[float], target: float = 0.99, horizon: int = 300,
                                    short: int = 30, requests_per_window: float = 50.0, seed: int = 42) -> float:

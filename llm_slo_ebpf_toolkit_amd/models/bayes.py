@@ -214,9 +214,12 @@ class NaiveBayes:
     @staticmethod
     def learned(stats: "SufficientStats", alpha: float = 2.0, seed: int = 42,
                 init: Optional[np.ndarray] = None, domains: Sequence[str] = catalog.ALL_DOMAINS,
-                prior_pseudo: float = 1.0) -> LinearPosteriorModel:
+                prior_pseudo: float = 1.0, temperature: float = 1.0, min_count: float = 0.0) -> LinearPosteriorModel:
         """Posterior-mean estimates: p_sd = (c_sd + alpha*p0_sd) / (n_d + alpha), with p0 a
-        seeded random-init table (north star: random-init priors); pi_d ~ Dirichlet(1)."""
+        seeded random-init table (north star: random-init priors); pi_d ~ Dirichlet(1).
+        ``temperature`` T divides every logit (calibration: same argmax, flatter posteriors for
+        T > 1); a domain with less than ``min_count`` labelled mass is inactive. The device refit
+        (ops/csrc/posterior.hip k_refit_nb) computes exactly this."""
         p0 = init if init is not None else NaiveBayes.random_init_table(seed, domains)
         idx = [catalog.DOMAIN_INDEX[d] for d in domains]
         n = stats.count[idx]
@@ -226,7 +229,50 @@ class NaiveBayes:
         priors = {d: float(priors_arr[i]) for i, d in enumerate(domains)}
         lik = {catalog.SIGNAL_NAMES[s]: {d: float(p[s, i]) for i, d in enumerate(domains)}
                for s in range(N_SLOTS)}
-        return NaiveBayes.from_tables(priors, lik, domains, "bayes_learned")
+        m = NaiveBayes.from_tables(priors, lik, domains, "bayes_learned")
+        for i, d in enumerate(domains):
+            if n[i] < min_count:
+                m.bias[catalog.DOMAIN_INDEX[d]] = NEG_INF
+        return with_temperature(m, temperature)
+
+
+def with_temperature(m: LinearPosteriorModel, temperature: float) -> LinearPosteriorModel:
+    """The model with every logit divided by ``temperature`` (inactive domains stay -inf)."""
+    if temperature == 1.0:
+        return m
+    if not temperature > 0:
+        raise ValueError("temperature must be > 0")
+    inv = 1.0 / float(temperature)
+    bias = np.where(np.isfinite(m.bias), m.bias * inv, m.bias)
+    return LinearPosteriorModel(m.name, m.weights * inv, bias, m.evidence_mask.copy(), m.feature_mode,
+                                m.thresholds.copy(), None if m.mean is None else m.mean.copy(),
+                                None if m.table_mask is None else m.table_mask.copy())
+
+
+def label_code(primary: int, domains: Sequence[int] = ()) -> int:
+    """int32 incident label the engine takes (posterior.hip): bits 0-7 the primary domain,
+    bits 8-23 the domain set of a multi-fault incident (its statistics spread evenly over the
+    set; the confusion matrix counts the primary)."""
+    ds = sorted(set(int(d) for d in domains) | {int(primary)})
+    if len(ds) <= 1:
+        return int(primary)
+    return int(primary) | (sum(1 << d for d in ds) << 8)
+
+
+def soft_labels(codes: np.ndarray, n_domains: int = N_DOMAINS) -> np.ndarray:
+    """label codes [B] -> soft label rows [B, n_domains] (0 rows for codes < 0)."""
+    codes = np.asarray(codes, dtype=np.int64)
+    Y = np.zeros((len(codes), n_domains))
+    for b, c in enumerate(codes.tolist()):
+        if c < 0:
+            continue
+        dset = (c >> 8) & 0xFFFF
+        if dset:
+            ds = [d for d in range(16) if dset >> d & 1 and d < n_domains]
+            Y[b, ds] = 1.0 / len(ds)
+        elif (c & 0xFF) < n_domains:
+            Y[b, c & 0xFF] = 1.0
+    return Y
 
 
 class LDA:

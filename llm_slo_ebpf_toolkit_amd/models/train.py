@@ -1,0 +1,276 @@
+"""Deployable learned attribution model: train on labelled fault-replay windows, calibrate, export.
+
+REF attributes with one fixed expert table (/root/reference/pkg/attribution/bayesian.go:67-190)
+through one pipeline (/root/reference/pkg/attribution/pipeline.go:44-51, cmd/attributor/main.go
+:81-152). NEW learns the same naive-Bayes form from data, starting from a seeded random-init
+likelihood table (the north star's "random-init priors"), and ships the result as a file the
+agent loads (``agent --model-path``):
+
+1. **training set** -- a fixed, seeded set of fault-replay windows (pipeline/replay.py): single
+   faults of every domain (scenario ``full``) alternating with compound incidents (scenario
+   ``compound``: every pair and triple of REF's five fault labels -- REF's faultreplay
+   mixed_multi pairs, generator.go:61-66, and its incident-lab compound scenario,
+   test/incident-lab/scenarios/mixed_multi.yaml, which injects three at once);
+2. **features** -- each incident group's features as the window engine computes them from the
+   records (decode -> 4-tier join -> per-group means): the GPU engine in the benchmark, the CPU
+   oracle engine here (identical by the GPU tests);
+3. **fit** -- sufficient statistics with *soft* labels (a multi-fault incident's mass is spread
+   over its domain set: label_code), posterior-mean likelihoods towards the random-init table,
+   domains without labelled mass left inactive (a classifier never shown a domain must not
+   predict it from random likelihoods);
+4. **calibration** -- one temperature T dividing every logit, fitted on held-out windows by the
+   soft-label negative log-likelihood. Naive Bayes multiplies 16 signals' evidence as if
+   independent, so its raw posteriors are far too sharp; T restores probabilities that spread
+   over a compound incident's domains (REF's coverage metric counts hypotheses with posterior
+   >= 0.10, pipeline.go:140-185) without changing any argmax.
+
+The device refit (posterior.hip k_refit_nb) evaluates exactly ``NaiveBayes.learned`` with the
+same T and minimum mass, so a model trained on the GPU and one trained here are the same
+function of the same statistics.
+"""
+
+from __future__ import annotations
+
+import itertools
+import json
+import math
+from dataclasses import asdict, dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..signals import catalog
+from .bayes import (N_DOMAINS, LinearPosteriorModel, NaiveBayes, SufficientStats, label_code, soft_labels,
+                    with_temperature)
+
+REF_FAULTS = ("provider_throttle", "dns_latency", "cpu_throttle", "memory_pressure", "network_partition")
+COMPOUND = [c for k in (2, 3) for c in itertools.combinations(REF_FAULTS, k)]
+TRAIN_SCENARIOS = ("full", "compound")
+MODEL_FORMAT = "mislo-model/1"
+
+
+@dataclass
+class TrainConfig:
+    windows: int = 32                 # labelled training windows (cycling TRAIN_SCENARIOS)
+    events_per_window: int = 16384
+    spans_per_window: int = 1024
+    services: int = 64                # incident groups per window
+    seed: int = 42                    # replay seed and random-init table seed
+    alpha: float = 2.0                # pseudo-count towards the random-init table
+    prior_pseudo: float = 1.0
+    min_count: float = 1.0            # labelled mass below which a domain stays inactive
+    holdout_every: int = 4            # every 4th window is held out for the temperature fit
+    t_grid: Tuple[float, float, int] = (1.0, 20.0, 64)
+
+
+@dataclass
+class TrainedModel:
+    model: LinearPosteriorModel
+    stats: SufficientStats
+    temperature: float
+    meta: Dict[str, object] = field(default_factory=dict)
+
+    def image(self) -> np.ndarray:
+        from ..ops.engine import model_bytes
+
+        return model_bytes(self.model)
+
+
+# ---------------------------------------------------------------------------------------
+# training data
+# ---------------------------------------------------------------------------------------
+
+def ensure_scenarios() -> None:
+    from ..pipeline import replay
+
+    replay.SCENARIOS.setdefault("compound", list(COMPOUND))
+
+
+def training_windows(cfg: TrainConfig):
+    """The fixed training set: windows alternating over TRAIN_SCENARIOS (seeded, deterministic)."""
+    from ..pipeline.replay import ReplayConfig, ReplayGenerator
+
+    ensure_scenarios()
+    gens = [ReplayGenerator(ReplayConfig(scenario=s, n_services=cfg.services, events_per_window=cfg.events_per_window,
+                                         spans_per_window=cfg.spans_per_window, seed=cfg.seed + 101 * i))
+            for i, s in enumerate(TRAIN_SCENARIOS)]
+    return [gens[j % len(gens)].next_window() for j in range(cfg.windows)]
+
+
+def window_codes(win) -> np.ndarray:
+    """Label codes of a replay window's incident groups (primary + domain set)."""
+    out = np.zeros(win.n_groups, dtype=np.int32)
+    for g, doms in enumerate(win.group_domains):
+        ds = [catalog.DOMAIN_INDEX[d] for d in doms]
+        out[g] = label_code(ds[0], ds)
+    return out
+
+
+def cpu_features(windows) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(features [B, 16], label codes [B], window index [B]) of every window's incident groups,
+    by the CPU oracle engine on the window's records."""
+    from ..pipeline.cpu import CpuWindowEngine
+
+    eng = CpuWindowEngine(NaiveBayes.ref())
+    feats, codes, wid = [], [], []
+    for j, w in enumerate(windows):
+        r = eng.run(w.events, w.spans, w.n_groups)
+        feats.append(r.feat.astype(np.float32))
+        codes.append(window_codes(w))
+        wid.append(np.full(w.n_groups, j))
+    return np.concatenate(feats), np.concatenate(codes), np.concatenate(wid)
+
+
+# ---------------------------------------------------------------------------------------
+# fit + calibration
+# ---------------------------------------------------------------------------------------
+
+def soft_nll(model: LinearPosteriorModel, feats: np.ndarray, Y: np.ndarray, temperature: float) -> float:
+    lg = model.logits(np.asarray(feats, dtype=np.float64)) / temperature
+    finite = np.isfinite(lg)
+    m = np.max(np.where(finite, lg, -np.inf), axis=1, keepdims=True)
+    ex = np.where(finite, np.exp(lg - m), 0.0)
+    logp = lg - m - np.log(ex.sum(axis=1, keepdims=True))
+    return float(-(Y * np.where(finite, logp, 0.0)).sum() / max(len(Y), 1))
+
+
+def fit_temperature(model: LinearPosteriorModel, feats: np.ndarray, Y: np.ndarray,
+                    grid: Tuple[float, float, int] = (1.0, 20.0, 64)) -> Tuple[float, float]:
+    """T minimising the soft-label NLL on held-out incidents (log-spaced grid); (T, NLL)."""
+    lo, hi, n = grid
+    best = (float("inf"), 1.0)
+    for t in np.exp(np.linspace(math.log(lo), math.log(hi), int(n))):
+        nll = soft_nll(model, feats, Y, float(t))
+        if nll < best[0]:
+            best = (nll, float(t))
+    return best[1], best[0]
+
+
+def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: TrainConfig) -> TrainedModel:
+    """Statistics on the training windows, temperature on the held-out ones."""
+    feats = np.asarray(feats, dtype=np.float64)
+    Y = soft_labels(codes)
+    hold = (np.asarray(window_ids) % cfg.holdout_every) == cfg.holdout_every - 1
+    tr = ~hold & (np.asarray(codes) >= 0)
+    st = SufficientStats()
+    st.add(feats[tr], Y[tr])
+    base = NaiveBayes.learned(st, alpha=cfg.alpha, seed=cfg.seed, prior_pseudo=cfg.prior_pseudo,
+                              min_count=cfg.min_count)
+    hv = hold & (np.asarray(codes) >= 0)
+    t, nll = fit_temperature(base, feats[hv], Y[hv], cfg.t_grid) if hv.any() else (1.0, float("nan"))
+    model = with_temperature(base, t)
+    model.name = "bayes_learned"
+    meta = {"temperature": t, "holdout_nll": nll, "holdout_nll_t1": soft_nll(base, feats[hv], Y[hv], 1.0)
+            if hv.any() else float("nan"), "train_incidents": int(tr.sum()), "holdout_incidents": int(hv.sum()),
+            "domain_mass": {catalog.ALL_DOMAINS[d]: round(float(st.count[d]), 3) for d in range(N_DOMAINS)},
+            "active_domains": [catalog.ALL_DOMAINS[d] for d in range(N_DOMAINS) if np.isfinite(model.bias[d])]}
+    return TrainedModel(model, st, t, meta)
+
+
+def train_cpu(cfg: Optional[TrainConfig] = None) -> TrainedModel:
+    cfg = cfg or TrainConfig()
+    wins = training_windows(cfg)
+    feats, codes, wid = cpu_features(wins)
+    tm = fit(feats, codes, wid, cfg)
+    tm.meta.update({"engine": "cpu-oracle", "config": asdict(cfg), "scenarios": list(TRAIN_SCENARIOS)})
+    return tm
+
+
+# ---------------------------------------------------------------------------------------
+# REF's 55 labelled rows (pkg/attribution/testdata/multi_fault_samples.jsonl)
+# ---------------------------------------------------------------------------------------
+
+Scorer = Callable[[np.ndarray], Tuple[np.ndarray, np.ndarray]]  # feat [n,16] f32 -> (post [n,D], pred [n])
+
+
+def host_scorer(model: LinearPosteriorModel) -> Scorer:
+    def score(feat):
+        f = np.asarray(feat, dtype=np.float64)
+        return model.posteriors(f), np.argmax(model.logits(f), axis=1)
+
+    return score
+
+
+def ref55_report(path: str, score: Scorer) -> Dict[str, object]:
+    """Single-fault macro-F1 over the ground-truth classes and accuracy on REF's 30 single-fault
+    rows; REF's partial accuracy (top-1 in the expected set) and coverage@0.10 (share of the
+    expected set among the hypotheses with posterior >= 0.10 plus the top-1) on its 25
+    multi-fault rows (0.9818 / 0.9667 / 1.000 / 0.667 for REF's own table)."""
+    from . import load_samples_jsonl, macro_f1
+
+    rows = load_samples_jsonl(path)
+    single = [s for s in rows if s.expected_domain]
+    multi = [s for s in rows if not s.expected_domain and s.expected_domains]
+    D = N_DOMAINS
+    out: Dict[str, object] = {}
+    if single:
+        v = np.array([catalog.feature_vector(s.signals) for s in single], dtype=np.float32)
+        _, pred = score(v)
+        names = [catalog.ALL_DOMAINS[int(p)] for p in pred]
+        truth = [s.expected_domain for s in single]
+        out["single_fault_macro_f1"] = round(macro_f1(truth, names), 4)
+        out["single_fault_accuracy"] = round(float(np.mean([a == b for a, b in zip(truth, names)])), 4)
+        out["single_fault_rows"] = len(single)
+        out["single_fault_misses"] = [f"{s.incident_id}:{a}->{b}" for s, a, b in zip(single, truth, names) if a != b]
+    if multi:
+        v = np.array([catalog.feature_vector(s.signals) for s in multi], dtype=np.float32)
+        post, pred = score(v)
+        part = cov = 0.0
+        for s, p, row in zip(multi, pred, np.asarray(post)[:, :D]):
+            exp = set(s.expected_set())
+            top = catalog.ALL_DOMAINS[int(p)]
+            hyp = {catalog.ALL_DOMAINS[d] for d in np.flatnonzero(row >= 0.10)} | {top}
+            part += top in exp
+            cov += len(exp & hyp) / len(exp)
+        out["multi_fault_partial_accuracy"] = round(part / len(multi), 4)
+        out["multi_fault_coverage_accuracy"] = round(cov / len(multi), 4)
+        out["multi_fault_rows"] = len(multi)
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# model files (safetensors tensors + JSON metadata; loading executes nothing from the file)
+# ---------------------------------------------------------------------------------------
+
+def save_model(path: str, tm: TrainedModel, extra: Optional[Dict[str, object]] = None) -> None:
+    import os
+
+    from safetensors.numpy import save_file
+
+    m = tm.model
+    st = tm.stats
+    arrays = {"image": tm.image(), "weights": m.weights, "bias": m.bias, "evidence_mask": m.evidence_mask.astype(np.uint8),
+              "thresholds": m.thresholds, "stats_count": st.count, "stats_elevated_sum": st.elevated_sum,
+              "stats_x_sum": st.x_sum, "stats_xx": st.xx}
+    meta = dict(tm.meta)
+    meta.update(extra or {})
+    meta.update({"name": m.name, "temperature": tm.temperature, "domains": list(catalog.ALL_DOMAINS),
+                 "signals": list(catalog.SIGNAL_NAMES)})
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    tmp = f"{path}.tmp.{os.getpid()}"
+    save_file({k: np.ascontiguousarray(v) for k, v in arrays.items()}, tmp,
+              metadata={"format": MODEL_FORMAT, "meta": json.dumps(meta, sort_keys=True, default=float)})
+    os.chmod(tmp, 0o644)  # read by the agent's container user
+    os.replace(tmp, path)
+
+
+def load_model(path: str) -> Tuple[LinearPosteriorModel, np.ndarray, Dict[str, object]]:
+    """(host model, PosteriorModel image for the engine, metadata)."""
+    from safetensors import safe_open
+
+    from ..ops.engine import MODEL_DTYPE, model_from_bytes
+
+    with safe_open(path, framework="numpy") as f:
+        md = f.metadata() or {}
+        if md.get("format") != MODEL_FORMAT:
+            raise ValueError(f"{path}: not a {MODEL_FORMAT} model file")
+        image = np.asarray(f.get_tensor("image"), dtype=np.uint8)
+    if image.size != MODEL_DTYPE.itemsize:
+        raise ValueError(f"{path}: model image of {image.size} bytes (expected {MODEL_DTYPE.itemsize})")
+    meta = json.loads(md.get("meta", "{}"))
+    if list(meta.get("domains", catalog.ALL_DOMAINS)) != list(catalog.ALL_DOMAINS):
+        raise ValueError(f"{path}: trained for another domain set")
+    model = model_from_bytes(image)
+    model.name = str(meta.get("name", "bayes_learned"))
+    return model, image, meta

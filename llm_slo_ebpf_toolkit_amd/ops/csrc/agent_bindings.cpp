@@ -49,7 +49,9 @@ class PyEngine {
  public:
   PyEngine(int device, int sig_cap, int span_cap, int group_cap, int user_cap, int n_buffers, int max_ahead,
            double window_ms, double threshold, int fanout, int group_mode, bool use_graphs, bool device_refit,
-           int n_dom, float ttft_slo_ms, double halo_ms, int import_cap, int xchg_cap) {
+           int n_dom, float ttft_slo_ms, double halo_ms, int import_cap, int xchg_cap, int shard_rank,
+           int shard_world) {
+    if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank / world");
     EngineConfig c;
     c.device = device;
     c.sig_cap = sig_cap;
@@ -69,6 +71,8 @@ class PyEngine {
     c.halo_ms = halo_ms;
     c.import_cap = import_cap;
     c.xchg_cap = xchg_cap;
+    c.shard_rank = shard_rank;
+    c.shard_world = shard_world;
     e_ = std::make_unique<WindowEngine>(c);
   }
   bool register_host(uintptr_t addr, size_t bytes) {
@@ -157,6 +161,36 @@ class PyEngine {
   }
   void set_model_bytes(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
     e_->set_model_bytes(b.data(), (size_t)b.size());
+  }
+  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count) {
+    eng().set_refit(alpha, prior_pseudo, inv_temp, min_count);
+  }
+  void refit_now() { eng().refit_now(); }
+  // K3 on given features (REF's 55 rows, offline evaluation) with the model on the device
+  py::dict score(py::array_t<float, py::array::c_style | py::array::forcecast> feat, py::object labels) {
+    if (feat.ndim() != 2 || feat.shape(1) != 16) throw std::invalid_argument("feat must be float32 [n, 16]");
+    const int n = (int)feat.shape(0);
+    std::vector<int32_t> lab;
+    if (!labels.is_none()) {
+      auto a = labels.cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
+      if (a.size() != n) throw std::invalid_argument("labels must have n entries");
+      lab.assign(a.data(), a.data() + n);
+    }
+    std::vector<double> post((size_t)n * 16), conf(n);
+    std::vector<int32_t> pred(n);
+    std::vector<uint32_t> ev((size_t)n * 16), cm(256);
+    {
+      py::gil_scoped_release nogil;
+      eng().score_features(feat.data(), n, lab.empty() ? nullptr : lab.data(), post.data(), pred.data(), conf.data(),
+                           ev.data(), cm.data());
+    }
+    py::dict d;
+    d["post"] = copy_array(post.data(), {n, 16});
+    d["pred"] = copy_array(pred.data(), {n});
+    d["conf"] = copy_array(conf.data(), {n});
+    d["evbits"] = copy_array(ev.data(), {n, 16});
+    d["confusion"] = copy_array(cm.data(), {16, 16});
+    return d;
   }
   void set_p0(py::array_t<double, py::array::c_style | py::array::forcecast> p0) {
     if (p0.size() != kSlots * 16) throw std::invalid_argument("p0 must be f64[256]");
@@ -275,16 +309,17 @@ PYBIND11_MODULE(_mislo_agent, m) {
   m.attr("CTX_ROWS") = kCtxRows;
   m.attr("REC_STRIDE") = kRecStride;
   m.attr("SIGREC_BYTES") = (int)sizeof(SigRec);
-  m.attr("RING_STATE") = py::make_tuple("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events");
+  m.attr("RING_STATE") =
+      py::make_tuple("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events", "other_shard");
   py::class_<PyEngine>(m, "WindowEngine")
       .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int, float, double, int,
-                    int>(),
+                    int, int, int>(),
            py::arg("device") = 0, py::arg("sig_cap") = 1 << 20, py::arg("span_cap") = 16384, py::arg("group_cap") = 64,
            py::arg("user_cap") = 1 << 18, py::arg("n_buffers") = 3, py::arg("max_ahead") = 3,
            py::arg("window_ms") = 2000.0, py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1,
            py::arg("use_graphs") = true, py::arg("device_refit") = true, py::arg("n_dom") = 10,
            py::arg("ttft_slo_ms") = 800.0f, py::arg("halo_ms") = 0.0, py::arg("import_cap") = 0,
-           py::arg("xchg_cap") = 0)
+           py::arg("xchg_cap") = 0, py::arg("shard_rank") = 0, py::arg("shard_world") = 1)
       .def("register_host", &PyEngine::register_host)
       .def("submit", &PyEngine::submit, py::arg("k"), py::arg("kernel"), py::arg("user"), py::arg("spans"),
            py::arg("n_groups"), py::arg("labels") = py::none(), py::arg("bases") = std::vector<int64_t>{},
@@ -302,6 +337,11 @@ PYBIND11_MODULE(_mislo_agent, m) {
       })
       .def("set_model_bytes", &PyEngine::set_model_bytes)
       .def("set_p0", &PyEngine::set_p0)
+      .def("set_refit", &PyEngine::set_refit, py::arg("alpha") = 2.0, py::arg("prior_pseudo") = 1.0,
+           py::arg("inv_temp") = 1.0, py::arg("min_count") = 0.0)
+      .def("refit_now", &PyEngine::refit_now)
+      .def("set_device_refit", [](PyEngine& p, bool on) { p.eng().set_device_refit(on); })
+      .def("score", &PyEngine::score, py::arg("feat"), py::arg("labels") = py::none())
       .def("set_pods", &PyEngine::set_pods)
       .def("inject_remote", &PyEngine::inject_remote)
       .def("results_all", &PyEngine::results_all)

@@ -209,6 +209,16 @@ __global__ __launch_bounds__(NT) void k_decode_events(const Event* __restrict__ 
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
 
+// Group sharding (one node's stream split across the node's GPUs, ``agent --gpus N``): every
+// GPU decodes the whole window, but only the records of the services it owns (service s >= 1
+// -> GPU (s - 1) % world; records of no service -> GPU 0) are counted and joined; the rest
+// become holes. Incident group g (service g + 1) lives on GPU g % world as local group g / world.
+__device__ __forceinline__ bool shard_owns(uint32_t svcnode, int rank, int world) {
+  if (world <= 1) return true;
+  const uint32_t svc = svcnode >> 16;
+  return (svc ? (int)((svc - 1u) % (uint32_t)world) : 0) == rank;
+}
+
 // EVENT16 field accessors: the trace id without its epoch tag; ts = base[tag] + ts_off
 __device__ __forceinline__ uint64_t wire_trace(const EventC16& e) { return (uint64_t)(e.trace_id & kTraceIdMask); }
 __device__ __forceinline__ int64_t wire_ts(const EventC16& e, const int64_t* base) {
@@ -401,7 +411,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
                                                       const uint4* __restrict__ ctx_tab, int n_ctx, TraceIds tt,
                                                       uint32_t* __restrict__ rs, unsigned long long* __restrict__ tmax,
                                                       const uint32_t* __restrict__ pod_sn, uint32_t n_pods, int seg,
-                                                      DecodeOut o) {
+                                                      int sh_rank, int sh_world, DecodeOut o) {
   __shared__ DecodeLds L;
   lds_init<NT>(L);
   const LdsLane l = lds_lane(L);
@@ -420,7 +430,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   const int64_t u_base = max(max(t_base[0], t_base[1]), max(t_base[2], t_base[3]));
   const int chunk = (n - seg_beg + gridDim.x - 1) / gridDim.x;
   const int beg = seg_beg + blockIdx.x * chunk, end = min(n, beg + chunk);
-  int unsupported = 0, zero_ts = 0, events = 0;
+  int unsupported = 0, zero_ts = 0, events = 0, other = 0;
   unsigned long long t_hi = 0;
   __shared__ uint4 s_stage[NT * 5];
   const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
@@ -437,12 +447,16 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const uint2 h = *reinterpret_cast<const uint2*>(r);
         const uint2 a = *reinterpret_cast<const uint2*>(r + 8), b = *reinterpret_cast<const uint2*>(r + 16);
         const EventC16 e{a.x, a.y, b.x, b.y};
-        const bool ok = i < valid_k && h.x == 16u && (e.ctx_type & 0xFFu) < kDefFirst;
+        bool ok = i < valid_k && h.x == 16u && (e.ctx_type & 0xFFu) < kDefFirst;
+        const uint32_t cid = e.ctx_type >> 8;
+        const uint4 cx = ok && cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
+        if (ok && !shard_owns(cx.w, sh_rank, sh_world)) {
+          ok = false;
+          ++other;
+        }
         if (ok) {
           const int st = (int)(e.ctx_type & 0xFFu);
           const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
-          const uint32_t cid = e.ctx_type >> 8;
-          const uint4 cx = cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
           const int64_t ts = wire_ts(e, t_base);
           decode_one(i, cap, ts, (float)((double)e.value_milli * 1e-3), slot, trace_of(tt, (uint32_t)wire_trace(e)),
                      cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
@@ -459,19 +473,29 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const uint32_t pod = c.y & 0xFFFFFu;
         const uint32_t sn = pod < n_pods ? pod_sn[pod] : 0u;
         const int64_t ts = user24_ts(b.y, c.y, c.x, u_base);
+        if (!shard_owns(sn, sh_rank, sh_world)) {
+          ++other;
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+        } else {
         decode_one(i, cap, ts, (float)((double)b.x * 1e-3), slot, ((uint64_t)a.y << 32) | a.x, pod, c.x & 0x3FFFFFu, sn,
                    0ull, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
         if (slot >= 0 && ts > 0) t_hi = max(t_hi, (unsigned long long)ts);
         ++events;
+        }
       } else if (user_rec == 32) {
         const User32 e = reinterpret_cast<const User32*>(user)[i - n_k];
         const int st = e.signal_type;
         const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
         const uint32_t sn = e.pod_id < n_pods ? pod_sn[e.pod_id] : 0u;
+        if (!shard_owns(sn, sh_rank, sh_world)) {
+          ++other;
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+        } else {
         decode_one(i, cap, e.ts_ns, (float)((double)e.value_milli * 1e-3), slot, e.trace_h, e.pod_id, e.pid, sn, 0ull,
                    o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
         if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
         ++events;
+        }
       } else {
         const Event e = user[i - n_k];
         const int st = e.signal_type;
@@ -479,10 +503,15 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const float val = slot >= 0 ? (float)((double)e.value * (double)L.tab.scale[slot]) : (float)e.value;
         const uint64_t ck = e.conn_h ? e.conn_h : conn_hash(e.src_port, e.dst_port, e.dst_ip);
         const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
-        decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, conn32(ck), o, l, unsupported,
-                   zero_ts, true, &s_stage[threadIdx.x * 5]);
-        if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
-        ++events;
+        if (!shard_owns(svcnode, sh_rank, sh_world)) {
+          ++other;
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+        } else {
+          decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, conn32(ck), o, l, unsupported,
+                     zero_ts, true, &s_stage[threadIdx.x * 5]);
+          if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
+          ++events;
+        }
       }
     }
     __syncthreads();
@@ -501,10 +530,12 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   }
   for (int off = 32; off > 0; off >>= 1) {
     events += __shfl_xor(events, off);
+    other += __shfl_xor(other, off);
     t_hi = max(t_hi, (unsigned long long)__shfl_xor((long long)t_hi, off));
   }
   if ((threadIdx.x & 63) == 0) {
     if (events) atomicAdd(&rs[kRsEvents], (uint32_t)events);
+    if (other) atomicAdd(&rs[kRsOtherShard], (uint32_t)other);
     if (t_hi) atomicMax(tmax, t_hi);
   }
   lds_flush<NT>(L, o, unsupported, zero_ts);
@@ -575,21 +606,32 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
       r.pid = cx.y;
       r.sn = cx.w;
       r.grp = s.group_id;
+      if (sm.sh_world > 1) {  // another GPU's incident group: a span row that never joins
+        if (r.grp % (uint32_t)sm.sh_world != (uint32_t)sm.sh_rank) r.ts = 0;
+        r.grp /= (uint32_t)sm.sh_world;
+      }
     } else {
       const Span s = sp[i];
       r.ts = s.ts_ns;
       // native engine: connections as conn32 (the context rows' identity); trace hashes as is
       r.tr = s.trace_h;
       r.cn = sm.native ? (uint64_t)conn32(s.conn_h) : s.conn_h;
-      if (sm.grp_sli && s.group_id < (uint32_t)sm.n_groups) {  // per-incident TTFT SLO accounting
+      uint32_t grp = s.group_id;
+      bool mine = true;
+      if (sm.sh_world > 1) {
+        mine = grp % (uint32_t)sm.sh_world == (uint32_t)sm.sh_rank;
+        grp /= (uint32_t)sm.sh_world;
+        if (!mine) r.ts = 0;  // another GPU's incident group: never joins, never counted here
+      }
+      if (mine && sm.grp_sli && grp < (uint32_t)sm.n_groups) {  // per-incident TTFT SLO accounting
         uint32_t* sli = sli_lds ? s_sli : sm.grp_sli;
-        atomicAdd(&sli[2 * s.group_id], 1u);
-        if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sli[2 * s.group_id + 1], 1u);
+        atomicAdd(&sli[2 * grp], 1u);
+        if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sli[2 * grp + 1], 1u);
       }
       r.pod = s.pod_id;
       r.pid = s.pid;
       r.sn = ((uint32_t)s.svc_id << 16) | s.node_id;
-      r.grp = s.group_id;
+      r.grp = grp;
     }
     c.rec[i] = r;
     PartCodes pc;
@@ -675,12 +717,13 @@ void launch_decode_window(const uint8_t* framed, const void* user, const int* n_
                           const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
                           uint32_t* ring_state, unsigned long long* tmax, const uint32_t* pod_sn, uint32_t n_pods,
                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
-                          unsigned long long* misc, hipStream_t stream, int seg, int grid, int blk_base) {
+                          unsigned long long* misc, hipStream_t stream, int seg, int grid, int blk_base, int sh_rank,
+                          int sh_world) {
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc, blk_base};
   constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_window<NT>), dim3(grid > 0 ? grid : decode_grid(cap)), dim3(NT), 0, stream, framed,
                      (const Event*)user, n_dev, rows, cap, imp, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, tt,
-                     ring_state, tmax, pod_sn, n_pods, seg, o);
+                     ring_state, tmax, pod_sn, n_pods, seg, sh_rank, sh_world, o);
 }
 
 }  // namespace mislo

@@ -72,11 +72,15 @@ struct EngineConfig {
   bool use_graphs = true;
   bool device_refit = true;  // learned naive Bayes refit on the device from accumulated statistics
   double alpha = 2.0, prior_pseudo = 1.0;
+  double inv_temp = 1.0, min_count = 0.0;  // refit calibration (posterior.hip k_refit_nb)
   int n_dom = 10;
   float ttft_slo_ms = 800.0f;  // per-incident SLO impact: spans with TTFT above this breach
   double halo_ms = 0.0;        // carry rows this close to the window's latest record into the next window
   int import_cap = 0;          // imported rows per window (halo + other GPUs' trace rows); 0 = none
   int xchg_cap = 0;            // trace-tagged rows each GPU exchanges per window (RCCL); 0 = none
+  // group sharding of one node's stream over the node's GPUs (agent --gpus N): this GPU counts and
+  // joins only its services' records and incident groups (decode.hip shard_owns); 1 = whole stream
+  int shard_rank = 0, shard_world = 1;
 };
 
 // per-incident results of a window, in one pinned block (one D2H)
@@ -127,6 +131,18 @@ class WindowEngine {
   std::vector<float> copy_ms(int64_t k);  // window k's DMA time and the copy stream's idle gap before it
 
   void set_model_bytes(const void* bytes, size_t n);  // stream-ordered before the next window
+  // device refit parameters (smoothing, prior pseudo-count, 1 / temperature, minimum labelled mass
+  // of an active domain), and a refit of the model from the accumulated statistics now
+  // (stream-ordered before the next window)
+  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count);
+  void refit_now();
+  // stop (or resume) the per-window prequential refit: the model on the device stays frozen
+  void set_device_refit(bool on) { cfg_.device_refit = on; }
+  // Score n incidents' features [n][16] with the model on the device (the K3 posterior kernel;
+  // synchronous, drains the engine first): post [n][16], pred [n], conf [n], evbits [n][16], and
+  // the confusion of labels (label_code, may be null) x predictions [16][16].
+  void score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred, double* conf,
+                      uint32_t* evbits, uint32_t* confusion);
   void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
   void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
   // other GPUs' rows for the next window, as their exchange blocks would arrive over RCCL (world

@@ -442,7 +442,8 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
-                       ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st);
+                       ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st, 0, 0, 0,
+                       cfg_.shard_rank, cfg_.shard_world);
   if (xchg)  // this window's warn-level trace-tagged rows, as the other GPUs will import them
     launch_select(g_rec_, g_status_, rows_, counts, N, kSelTrace, tmax_, 0, sel_cnt_, sel_off_, xsend_ + sizeof(XRec),
                   reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, true, st);
@@ -460,7 +461,7 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
     const TraceIds tt{trace_hash_, kTraceIdRows};
     launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                          ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st,
-                         1, nblk_imp_, nblk_sig_);
+                         1, nblk_imp_, nblk_sig_, cfg_.shard_rank, cfg_.shard_world);
   }
   {  // this buffer's imports are consumed
     FillList z{};
@@ -473,7 +474,7 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
                      g_items_, st, nblk_sig_);
   else
     launch_partition(g_part_, rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
-  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms};
+  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world};
   launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
@@ -615,7 +616,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     // fold window k - nb's all-reduced statistics (packet b) and refit before window k: a
     // deterministic prequential lag of nb, identical on every rank
     launch_refit_nb(stats_acc_, packet_dev_[b] + kStatsOff, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
-                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_);
+                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count);
     ++folded_;
   }
   const bool injected = !inject_.empty();
@@ -658,9 +659,12 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   HIPCHECK(hipEventRecord(compute_done_[b], compute_));
   HIPCHECK(hipStreamWaitEvent(comm_stream_, compute_done_[b], 0));
   if (comm_) {
-    // one group: the node-wide packet and the node-wide incident list
+    // one group: the node-wide packet and the node-wide incident list. The ring accounting at
+    // the packet's tail stays this GPU's own (each GPU is a consumer of its rings: its first busy
+    // record, its records), so it is left out of the sum.
     NCCLCHECK(ncclGroupStart());
-    NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen, ncclFloat64, ncclSum, comm_, comm_stream_));
+    NCCLCHECK(ncclAllReduce(packet_dev_[b], packet_dev_[b], kPacketLen - kPacketRing, ncclFloat64, ncclSum, comm_,
+                            comm_stream_));
     NCCLCHECK(ncclAllGather(res_dev_[b], res_all_dev_[b], res_bytes_, ncclUint8, comm_, comm_stream_));
     NCCLCHECK(ncclGroupEnd());
     to_host(res_all_dev_[b], res_all_host_[b], res_bytes_ * world_, comm_stream_);
@@ -734,6 +738,48 @@ void WindowEngine::set_model_bytes(const void* bytes, size_t n) {
 
 void WindowEngine::set_p0(const double* p0) {
   HIPCHECK(hipMemcpy(p0_, p0, kSlots * 16 * sizeof(double), hipMemcpyHostToDevice));
+}
+
+void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count) {
+  if (!(alpha > 0.0) || !(prior_pseudo >= 0.0) || !(inv_temp > 0.0) || !(min_count >= 0.0))
+    throw std::invalid_argument("refit parameters");
+  cfg_.alpha = alpha;
+  cfg_.prior_pseudo = prior_pseudo;
+  cfg_.inv_temp = inv_temp;
+  cfg_.min_count = min_count;
+}
+
+void WindowEngine::refit_now() {
+  launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
+                  reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count);
+}
+
+void WindowEngine::score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred,
+                                  double* conf, uint32_t* evbits, uint32_t* confusion) {
+  if (n < 0) throw std::invalid_argument("n");
+  sync();
+  if (n == 0) return;
+  // one scratch block: [n][16] f32 features | n | labels | post | pred | conf | evbits | confusion
+  const size_t o_n = (size_t)n * 16 * 4, o_lab = o_n + 64, o_post = (o_lab + (size_t)n * 4 + 63) & ~size_t(63);
+  const size_t o_pred = o_post + (size_t)n * 16 * 8, o_conf = (o_pred + (size_t)n * 4 + 63) & ~size_t(63);
+  const size_t o_ev = o_conf + (size_t)n * 8, o_cm = o_ev + (size_t)n * 16 * 4, bytes = o_cm + 16 * 16 * 4;
+  uint8_t* d = dalloc<uint8_t>(bytes);
+  HIPCHECK(hipMemset(d, 0, bytes));
+  HIPCHECK(hipMemcpy(d, feat, o_n, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(d + o_n, &n, sizeof(int), hipMemcpyHostToDevice));
+  if (labels) HIPCHECK(hipMemcpy(d + o_lab, labels, (size_t)n * 4, hipMemcpyHostToDevice));
+  launch_posterior(reinterpret_cast<const float*>(d), reinterpret_cast<const int*>(d + o_n), n,
+                   reinterpret_cast<const PosteriorModel*>(model_dev_),
+                   labels ? reinterpret_cast<const int32_t*>(d + o_lab) : nullptr, reinterpret_cast<double*>(d + o_post),
+                   reinterpret_cast<int32_t*>(d + o_pred), reinterpret_cast<double*>(d + o_conf),
+                   reinterpret_cast<uint32_t*>(d + o_ev), reinterpret_cast<uint32_t*>(d + o_cm), compute_);
+  HIPCHECK(hipStreamSynchronize(compute_));
+  HIPCHECK(hipMemcpy(post, d + o_post, (size_t)n * 16 * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(pred, d + o_pred, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(conf, d + o_conf, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(evbits, d + o_ev, (size_t)n * 16 * 4, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(confusion, d + o_cm, 16 * 16 * 4, hipMemcpyDeviceToHost));
+  HIPCHECK(hipFree(d));
 }
 
 void WindowEngine::set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n) {
@@ -827,7 +873,7 @@ void WindowEngine::restore(const double* stats, const void* model, size_t n, int
     HIPCHECK(hipMemcpy(model_dev_, model, n, hipMemcpyHostToDevice));
   } else {  // the learned model from the restored statistics, by the device refit itself
     launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
-                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_);
+                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count);
     HIPCHECK(hipStreamSynchronize(compute_));
   }
   folded_ = folded;

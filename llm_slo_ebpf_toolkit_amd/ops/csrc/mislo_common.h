@@ -235,7 +235,7 @@ constexpr int kRecStride = 24;
 constexpr uint32_t kDefTrace = 0xFD, kDefCtx = 0xFE, kDefFirst = 0xF0;
 // per-window ring accounting (device, packed into the packet): first busy record (min), records
 // of another size, context / trace definitions applied, discarded records, user-space records
-enum RingState { kRsFirstBusy = 0, kRsForeign, kRsDefCtx, kRsDefTrace, kRsDiscard, kRsEvents, kRsLen = 8 };
+enum RingState { kRsFirstBusy = 0, kRsForeign, kRsDefCtx, kRsDefTrace, kRsDiscard, kRsEvents, kRsOtherShard, kRsLen = 8 };
 
 // the 32-bit connection identity of context rows (runtime/csrc/records.h conn32)
 __host__ __device__ inline uint32_t conn32(uint64_t key) {

@@ -42,6 +42,7 @@ struct SpanMap {
   uint32_t* grp_sli;     // [n_groups][2]: spans, TTFT > slo
   int n_groups;
   float ttft_slo_ms;
+  int sh_rank = 0, sh_world = 1;  // group sharding: this GPU keeps groups g % sh_world == sh_rank as g / sh_world
 };
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
                          const uint32_t* ctx_tab, int n_ctx, hipStream_t stream, const SpanMap* sm = nullptr);
@@ -59,7 +60,8 @@ void launch_decode_window(const uint8_t* framed, const void* user, const int* n_
                           const SigRec* imp, const uint32_t* ctx_tab, int n_ctx, const TraceIds& tt,
                           uint32_t* ring_state, unsigned long long* tmax, const uint32_t* pod_sn, uint32_t n_pods,
                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
-                          unsigned long long* misc, hipStream_t stream, int seg = 0, int grid = 0, int blk_base = 0);
+                          unsigned long long* misc, hipStream_t stream, int seg = 0, int grid = 0, int blk_base = 0,
+                          int sh_rank = 0, int sh_world = 1);
 
 // exchange.hip: stable row selections (halo carry, trace-tagged rows for the GPU exchange)
 constexpr int kSelHalo = 0, kSelTrace = 1;
@@ -114,7 +116,7 @@ void launch_posterior_stats(const float* feat, const int* ng_dev, int cap, const
                             uint32_t* confusion, const int32_t* stat_labels, const float* weights, double* out,
                             double* count, hipStream_t stream);
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
-                     PosteriorModel* pm, hipStream_t stream);
+                     PosteriorModel* pm, hipStream_t stream, double inv_temp = 1.0, double min_count = 0.0);
 
 // gatestats.hip (K5)
 int boot_max_n();

@@ -118,8 +118,8 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
         pred[r] = am;
         conf[r] = exp(m - logz);
         if (labels != nullptr) {
-          const int y = labels[r];
-          if (y >= 0 && y < kMaxDomains) atomicAdd(confusion + y * kMaxDomains + am, 1u);
+          const int y = labels[r];  // primary domain in bits 0-7 (label_code: a domain set above)
+          if (y >= 0 && (y & 0xFF) < kMaxDomains) atomicAdd(confusion + (y & 0xFF) * kMaxDomains + am, 1u);
         }
       }
     }
@@ -159,8 +159,11 @@ __device__ __forceinline__ void stats_body(int blk, const StatsArgs& a_) {
         e = ((v == v) && v >= pm.thr[i]) ? 1.0 : 0.0;
         const double vv = (v == v) ? (double)v : pm.nominal[i];
         x = log1p(vv > 0.0 ? vv : 0.0);
-        y = (lab == i) ? wgt : 0.0;
-        if (i == 0) atomicAdd(count + (lab < kMaxDomains ? lab : 0), wgt);
+        // label_code: bits 0-7 the primary domain, bits 8-23 the incident's domain set (a
+        // multi-fault incident): a soft label spread evenly over the set
+        const uint32_t set = ((uint32_t)lab >> 8) & 0xFFFFu;
+        y = set ? (((set >> i) & 1u) ? wgt / (double)__popc(set) : 0.0) : ((lab & 0xFF) == i ? wgt : 0.0);
+        if (y != 0.0) atomicAdd(count + i, y);
       }
     }
     // A = U^T (rows = U columns, k = incident), B = V (k = incident, cols = V columns)
@@ -201,9 +204,15 @@ __global__ __launch_bounds__(NT) void k_posterior_stats(PosteriorArgs p, StatsAr
 // stats: [32 x 32] f64 (rows 0-15 = E^T Y) followed by count[16]; p0: [16 x 16] f64.
 // add (optional, same layout): a window's all-reduced statistics, folded into stats first
 // (one launch instead of an elementwise add plus the refit on the compute stream).
+// inv_temp scales every logit (w and bias; the calibration temperature T = 1 / inv_temp fitted on
+// held-out windows, models/train.py): argmax and evidence are unchanged, the posteriors are
+// flatter for T > 1 (REF's coverage metric counts hypotheses >= 0.10). A domain with less than
+// min_count labelled mass is inactive (bias -inf): its likelihoods would be the random-init
+// table, not data.
 __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, const double* __restrict__ add,
                                                   const double* __restrict__ p0, double alpha, double prior_pseudo,
-                                                  int n_dom, PosteriorModel* __restrict__ pm) {
+                                                  int n_dom, double inv_temp, double min_count,
+                                                  PosteriorModel* __restrict__ pm) {
   __shared__ double s_logpn[kSlots][kMaxDomains];
   __shared__ uint32_t s_mask[kMaxDomains];
   const double* count = stats + 32 * 32;
@@ -219,7 +228,7 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
       const double c = stats[sl * 32 + d];
       const double p = (c + alpha * p0[sl * 16 + d]) / (n + alpha);
       const double pe = fmin(fmax(p, 0.01), 0.99), pn = fmin(fmax(1.0 - p, 0.01), 0.99);
-      pm->w[sl][d] = log(pe) - log(pn);
+      pm->w[sl][d] = (log(pe) - log(pn)) * inv_temp;
       s_logpn[sl][d] = log(pn);
       if (p >= 0.5) atomicOr(&s_mask[d], 1u << sl);
     } else {
@@ -229,12 +238,12 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
   }
   __syncthreads();
   if (t < kMaxDomains) {
-    if (t < n_dom) {
+    if (t < n_dom && count[t] >= min_count) {
       double N = 0.0;
       for (int d = 0; d < n_dom; ++d) N += count[d];
       double b = log((count[t] + prior_pseudo) / (N + prior_pseudo * (double)n_dom));
       for (int sl = 0; sl < kSlots; ++sl) b += s_logpn[sl][t];
-      pm->bias[t] = b;
+      pm->bias[t] = b * inv_temp;
       pm->dom_mask[t] = s_mask[t];
     } else {
       pm->bias[t] = -__builtin_inf();
@@ -248,8 +257,9 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
 }
 
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
-                     PosteriorModel* pm, hipStream_t stream) {
-  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, alpha, prior_pseudo, n_dom, pm);
+                     PosteriorModel* pm, hipStream_t stream, double inv_temp, double min_count) {
+  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, alpha, prior_pseudo, n_dom, inv_temp,
+                     min_count, pm);
 }
 
 constexpr int kPostNT = 256, kStatsRPW = 256;

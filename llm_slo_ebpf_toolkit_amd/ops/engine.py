@@ -15,7 +15,7 @@ from typing import Dict, Optional
 import numpy as np
 
 from ..collector import records
-from ..models.bayes import NOMINAL, LinearPosteriorModel
+from ..models.bayes import N_DOMAINS, NOMINAL, LinearPosteriorModel
 from ..signals import catalog
 from . import load
 
@@ -68,6 +68,23 @@ def model_bytes(model: LinearPosteriorModel) -> np.ndarray:
     rec["table_mask"][0] = table_mask
     rec["mode"][0] = mode
     return rec.view(np.uint8)
+
+
+def model_from_bytes(b: np.ndarray) -> LinearPosteriorModel:
+    """Inverse of ``model_bytes``: the host model a ``mislo::PosteriorModel`` image evaluates
+    (the CPU window engine scores with it; exported model files hold the image)."""
+    rec = np.frombuffer(np.ascontiguousarray(b, dtype=np.uint8).tobytes(), dtype=MODEL_DTYPE)[0]
+    w = np.array(rec["w"], dtype=np.float64)
+    bias = np.array(rec["bias"], dtype=np.float64)
+    dom = np.array(rec["dom_mask"], dtype=np.uint32)
+    D = N_DOMAINS
+    mask = np.array([[(int(dom[d]) >> s) & 1 for d in range(D)] for s in range(16)], dtype=bool)
+    tm = int(rec["table_mask"])
+    mode = "binary" if int(rec["mode"]) == 0 else "continuous"
+    mean = np.array(rec["mean"], dtype=np.float64) if mode == "continuous" else None
+    table = np.array([(tm >> s) & 1 for s in range(16)], dtype=np.float64) if mode == "binary" else None
+    return LinearPosteriorModel("image", w[:, :D].copy(), bias[:D].copy(), mask, mode,
+                                np.array(rec["thr"], dtype=np.float64), mean, table)
 
 
 def decode_debug(dbg: np.ndarray, misc: np.ndarray, n_spans: int, n_events: int) -> Dict[str, int]:

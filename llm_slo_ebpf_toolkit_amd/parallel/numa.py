@@ -78,3 +78,24 @@ def bind_to_device_numa(device_index: int, sysfs: str = "/sys/bus/pci/devices") 
     except OSError:
         return None
     return pick
+
+
+def visible_gpu_count(topology: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this process may use, WITHOUT initialising the HIP runtime (a process that forks or
+    spawns GPU workers must not): the device-visibility env if set, else the KFD topology's GPU
+    nodes (gpu_id != 0; readable without root)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    n = 0
+    try:
+        for node in os.listdir(topology):
+            try:
+                with open(os.path.join(topology, node, "gpu_id")) as fh:
+                    n += int(fh.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    return n

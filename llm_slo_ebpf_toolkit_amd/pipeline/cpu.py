@@ -1,24 +1,26 @@
-"""CPU window engine: the numpy oracle of one window (pipeline/oracle.py) packaged with the
-exact packet layout the GPU engine all-reduces (ops/csrc/bindings.cpp k_pack).
+"""CPU window engines: the numpy oracle of one window (pipeline/oracle.py) packaged with the
+exact packet layout the GPU engine all-reduces (ops/csrc/engine.hip k_pack).
 
-Two uses:
-
-* the reference side of the multi-process tests -- ``gloo`` ranks run this engine on
-  their shard, all-reduce the packets, and must reproduce the single-process window
-  (parallel/ correctness by construction, no GPU needed);
-* an explicit, loudly-selected CPU engine (``--device cpu``) for hosts without an MI355X
-  (REF's deployment class, "config 1"). It is never a silent fallback: GPU hosts fail if
-  the HIP extension is missing (ops.require_gpu_extension).
+* ``CpuWindowEngine`` -- one window of 64-byte EVENT/SPAN records: the reference side of the
+  record-level tests;
+* ``CpuRingEngine`` -- the native ``WindowEngine``'s contract (ring byte ranges in, packet and
+  per-incident results out, halo, group sharding, the collectives over a gloo group). It is the
+  engine of ``agent --engine cpu`` (hosts without an MI355X, REF's deployment class, "config 1")
+  and of the multi-process agent tests, where ``gloo`` ranks must reproduce the single-process
+  window. It is never a silent fallback: GPU hosts fail if the HIP extension is missing
+  (ops.require_gpu_extension).
 """
 
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 from typing import Dict, Optional
 
 import numpy as np
 
-from ..models.bayes import N_DOMAINS, LinearPosteriorModel, SufficientStats
+from ..collector import records
+from ..models.bayes import N_DOMAINS, LinearPosteriorModel, SufficientStats, soft_labels
 from . import oracle
 from .window import PACKET_LAYOUT
 
@@ -110,3 +112,277 @@ class CpuWindowEngine:
         from .window import unpack_packet
 
         return unpack_packet(packet)
+
+
+# ---------------------------------------------------------------------------------------
+# the native engine's window contract on the CPU (agent --engine cpu, multi-process tests)
+# ---------------------------------------------------------------------------------------
+
+def _read(addr: int, n: int) -> np.ndarray:
+    import ctypes
+
+    if n <= 0:
+        return np.zeros(0, dtype=np.uint8)
+    return np.ctypeslib.as_array((ctypes.c_uint8 * int(n)).from_address(int(addr))).copy()
+
+
+def _gather(segs) -> np.ndarray:
+    parts = [_read(a, n) for a, n in segs]
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+
+
+def shard_owner(svcnode: np.ndarray, world: int) -> np.ndarray:
+    """decode.hip shard_owns: service s >= 1 -> GPU (s - 1) % world, no service -> GPU 0."""
+    svc = (np.asarray(svcnode, dtype=np.uint32) >> np.uint32(16)).astype(np.int64)
+    return np.where(svc > 0, (svc - 1) % max(1, world), 0)
+
+
+class CpuRingEngine:
+    """The native ``WindowEngine``'s window contract (ops/csrc/engine.h) evaluated by the numpy
+    oracle on the host: the same ring byte ranges in (framed BPF ring records, user-space
+    records, spans), the same packet, per-incident results, busy-record stop, halo, group
+    sharding and -- with a ``torch.distributed`` group (gloo) -- the same collectives: the
+    packet all-reduce (ring accounting excluded), the all-gather of every rank's incident
+    results and of the trace-tagged exchange blocks.
+
+    Selected explicitly (``agent --engine cpu``; the multi-process tests), never as a silent
+    fallback. The oracle join is O(spans x rows): a reference engine for small windows, not a
+    production path at node event rates."""
+
+    def __init__(self, device: int = 0, sig_cap: int = 1 << 20, span_cap: int = 16384, group_cap: int = 64, user_cap: int = 1 << 18,
+                 n_buffers: int = 3, window_ms: float = 2000.0, threshold: float = 0.7, fanout: int = 3,
+                 group_mode: int = 1, n_dom: int = N_DOMAINS, ttft_slo_ms: float = 800.0, halo_ms: float = 0.0,
+                 import_cap: int = 0, xchg_cap: int = 0, shard_rank: int = 0, shard_world: int = 1, group=None,
+                 **_native_only):
+        from ..parallel.exchange import ExchangeModel, torch_allgather
+
+        self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
+        self.buffers = int(n_buffers)
+        self.window_ms_, self.threshold, self.fanout, self.group_mode = window_ms, threshold, fanout, group_mode
+        self.n_dom, self.ttft_slo_ms = n_dom, float(ttft_slo_ms)
+        self.shard_rank, self.shard_world = int(shard_rank), int(shard_world)
+        self.group = group
+        if group is not None:
+            import torch.distributed as dist
+
+            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+        self.xm = ExchangeModel(self.rank, self.world, halo_ms, import_cap, xchg_cap if self.world > 1 else 0,
+                                torch_allgather(group) if group is not None else None)
+        self.table, self.tmap = oracle.CtxTable(), oracle.TraceMap()
+        self.pod_sn: Dict[int, int] = {}
+        self.model = None
+        self.win: Dict[int, dict] = {}
+        self._totals = np.zeros(PACKET_LEN)
+        self.windows_folded = 0
+        self.graphs = 0
+        self.staged_bytes = self.direct_bytes = 0
+        self.host_issue_us = self.host_wait_us = self.host_dma_issue_us = self.host_launch_us = 0.0
+        self.host_pre_us = self.host_tail_us = 0.0
+        self.host_dma_split_us = [0.0, 0.0, 0.0, 0.0]
+
+    @property
+    def has_comm(self) -> bool:
+        return self.group is not None and self.world > 1
+
+    # ---- setup ------------------------------------------------------------------------------
+    def register_host(self, addr: int, n: int) -> bool:
+        return True
+
+    def set_model_bytes(self, b) -> None:
+        from ..ops.engine import model_from_bytes
+
+        self.model_image = np.ascontiguousarray(b, dtype=np.uint8).copy()
+        self.model = model_from_bytes(self.model_image)
+
+    def model_bytes(self) -> np.ndarray:
+        return self.model_image.copy()
+
+    def set_p0(self, p0) -> None:
+        pass
+
+    def set_pods(self, pods, sn) -> None:
+        self.pod_sn.update(zip(np.asarray(pods).tolist(), np.asarray(sn).tolist()))
+
+    def init_comm(self, *a) -> None:
+        raise RuntimeError("the CPU engine communicates over its torch.distributed group (gloo)")
+
+    # ---- per window -------------------------------------------------------------------------
+    def submit(self, k: int, kernel, user, spans, n_groups: int, labels, bases, with_labels: bool, learn: bool,
+               user_rec: int) -> None:
+        t0 = time.perf_counter()
+        framed = _gather(kernel)
+        fr = framed.view(np.uint32).reshape(-1, 6) if len(framed) else np.zeros((0, 6), np.uint32)
+        busy = np.nonzero(fr[:, 0] & np.uint32(records.RB_BUSY))[0] if len(fr) else np.zeros(0, np.int64)
+        first_busy = int(busy[0]) if len(busy) else -1
+        oracle.apply_ring_defs(framed, self.table, self.tmap, self.pod_sn)
+        if first_busy >= 0:  # the engine stops at the first record still being written
+            fr = fr.copy()
+            fr[first_busy:, 0] = np.uint32(records.RB_BUSY | 16)
+            framed = fr.view(np.uint8).reshape(-1)
+        ub = _gather(user)
+        udt = {64: records.EVENT, 32: records.USER32, 24: records.USER24}[int(user_rec)]
+        u = ub.view(udt) if len(ub) else np.zeros(0, dtype=udt)
+        d = oracle.decode_window(framed, u, self.table, self.tmap, bases, pod_sn=self.pod_sn)
+        n_k = len(fr)
+        valid_k = ((fr[:, 0] == 16) & ((fr[:, 3] & np.uint32(0xFF)) < records.DEF_FIRST)) if n_k else np.zeros(0, bool)
+        other = 0
+        is_rec = np.concatenate([valid_k, np.ones(len(u), bool)])
+        if self.shard_world > 1:
+            mine = shard_owner(d.svcnode, self.shard_world) == self.shard_rank
+            drop = is_rec & ~mine
+            other = int(drop.sum())
+            d = _holes(d, drop)
+            is_rec = is_rec & ~drop
+        events = int(valid_k.sum()) + len(u) - other
+        sp = _gather(spans)
+        spr = oracle.spans_native(sp.view(records.SPAN) if len(sp) else np.zeros(0, records.SPAN))
+        G = int(n_groups)
+        grp_local = spr["group_id"].astype(np.int64)
+        if self.shard_world > 1:
+            mine_sp = grp_local % self.shard_world == self.shard_rank
+            spr["ts_ns"] = np.where(mine_sp, spr["ts_ns"], 0)
+            grp_local = grp_local // self.shard_world
+            spr["group_id"] = grp_local.astype(spr["group_id"].dtype)
+        else:
+            mine_sp = np.ones(len(spr), bool)
+        n_loc = len(d.ts)
+        res = self.xm.window(d, spr, G, window_ms=self.window_ms_, threshold=self.threshold, fanout=self.fanout,
+                             group_mode=self.group_mode)
+        hist = oracle.histograms(d)
+        status = np.zeros((16, 3), dtype=np.int64)
+        ok = d.slot != oracle.NO_SLOT
+        np.add.at(status, (d.slot[ok].astype(np.int64), d.status[ok].astype(np.int64)), 1)
+        misc = np.zeros(PACKET_LAYOUT[2], dtype=np.int64)
+        misc[0] = int(((~ok) & is_rec).sum())
+        misc[1] = int(((d.ts == 0) & is_rec).sum())
+        misc[2:18] = oracle.value_sums_milli(d)
+        dbg = np.zeros(PACKET_LAYOUT[3], dtype=np.int64)
+        dbg[0] = res.debug["candidates"]
+        dbg[1] = res.debug["low_confidence"]
+        dbg[3] = res.debug["fanout_dropped"]
+        dbg[4] = res.debug["spans_enriched"]
+        feat = res.feat.astype(np.float32)
+        f64 = feat.astype(np.float64)
+        D = self.n_dom
+        post = np.zeros((G, 16))
+        pred = np.zeros(G, np.int32)
+        gconf = np.zeros(G)
+        evbits = np.zeros((G, 16), np.uint32)
+        if G and self.model is not None:
+            post[:, :D] = self.model.posteriors(f64)
+            lg = self.model.logits(f64)
+            pred = np.argmax(lg, axis=1).astype(np.int32)
+            gconf = post[np.arange(G), pred]
+            evbits[:, :D] = self.model.evidence_bits(f64)
+        conf = np.zeros((16, 16), dtype=np.int64)
+        stats = SufficientStats()
+        if labels is not None and G:
+            lab = np.asarray(labels, dtype=np.int64)[:G]
+            m = lab >= 0
+            if with_labels:
+                np.add.at(conf, (lab[m] & 0xFF, pred[m]), 1)
+            if learn and m.any():
+                stats.add(f64[m], soft_labels(lab[m]))
+        sli = np.zeros((G, 2), np.uint32)
+        okg = mine_sp & (grp_local >= 0) & (grp_local < G)
+        np.add.at(sli[:, 0], grp_local[okg], 1)
+        np.add.at(sli[:, 1], grp_local[okg & (spr["ttft_ms"] > np.float32(self.ttft_slo_ms))], 1)
+        ring = np.zeros(PACKET_LAYOUT[7])
+        ring[:7] = (first_busy, 0, 0, 0, 0, events, other)
+        pk = build_packet(hist, status, misc, dbg, conf, stats)
+        pk[PACKET_LEN - PACKET_LAYOUT[7]:] = ring
+        out = {"post": post, "conf": gconf, "feat": feat, "pred": pred, "evbits": evbits, "sli": sli}
+        outs = [out]
+        if self.has_comm:
+            import torch
+            import torch.distributed as dist
+
+            t = torch.from_numpy(pk[:PACKET_LEN - PACKET_LAYOUT[7]].copy())
+            dist.all_reduce(t, group=self.group)
+            pk[:PACKET_LEN - PACKET_LAYOUT[7]] = t.numpy()
+            outs = [None] * self.world
+            dist.all_gather_object(outs, out, group=self.group)
+        self._totals += pk
+        ms = 1e3 * (time.perf_counter() - t0)
+        self.win[k % max(1, self.buffers)] = {"k": k, "packet": pk, "res": out, "all": outs, "ms": ms,
+                                             "rows": (n_loc, res.n_rows)}
+
+    def _w(self, k: int) -> dict:
+        w = self.win.get(k % max(1, self.buffers))
+        if w is None or w["k"] != k:
+            raise KeyError(f"window {k} is not held (only the last {self.buffers})")
+        return w
+
+    def h2d_done(self, k: int) -> bool:
+        return True
+
+    def wait_h2d(self, k: int) -> None:
+        pass
+
+    def query(self, k: int) -> bool:
+        return True
+
+    def wait(self, k: int) -> None:
+        self._w(k)
+
+    def packet(self, k: int) -> np.ndarray:
+        return self._w(k)["packet"].copy()
+
+    @staticmethod
+    def _cut(r: dict, G: int) -> dict:
+        return {key: np.asarray(v)[:G].copy() for key, v in r.items()}
+
+    def results(self, k: int, n_groups: int) -> dict:
+        return self._cut(self._w(k)["res"], n_groups)
+
+    def results_all(self, k: int, n_groups: int) -> list:
+        return [self._cut(r, n_groups) for r in self._w(k)["all"]]
+
+    def window_ms(self, k: int):
+        ms = self._w(k)["ms"]
+        return ms, ms
+
+    def copy_ms(self, k: int):
+        return [0.0, 0.0]
+
+    def inject_remote(self, blocks, stride, world, me) -> None:
+        from ..parallel.exchange import parse_block
+
+        b = np.ascontiguousarray(blocks, dtype=np.uint8)
+        for r in range(world):
+            if r != me:
+                self.xm.imports = oracle.concat(self.xm.imports, parse_block(b[r * stride:(r + 1) * stride]))
+
+    def import_state(self):
+        return []
+
+    # ---- totals / state -----------------------------------------------------------------------
+    def totals(self) -> np.ndarray:
+        return self._totals.copy()
+
+    def reset_totals(self) -> None:
+        self._totals[:] = 0
+
+    def stats_acc(self) -> np.ndarray:
+        return np.zeros(1040)
+
+    def restore(self, stats, model, folded) -> None:
+        if len(model):
+            self.set_model_bytes(model)
+
+    def sync(self) -> None:
+        pass
+
+    def close(self) -> None:
+        self.win.clear()
+
+
+def _holes(d: oracle.Decoded, m: np.ndarray) -> oracle.Decoded:
+    """Rows ``m`` become holes: no timestamp, no signal, no identity (decode.hip hole rows)."""
+    out = oracle.Decoded(*(getattr(d, f).copy() for f in oracle.Decoded.__dataclass_fields__))
+    for f, z in (("ts", 0), ("val", 0), ("slot", oracle.NO_SLOT), ("status", 0), ("pod", 0), ("pid", 0),
+                 ("svcnode", 0), ("trace", 0), ("conn", 0)):
+        getattr(out, f)[m] = z
+    return out

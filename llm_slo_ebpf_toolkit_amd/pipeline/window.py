@@ -36,7 +36,7 @@ from ..models.metrics import macro_f1_from_confusion
 
 # hist, status, misc(+16 value sums), dbg, confusion, stats, count, ring accounting
 PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16, 8)
-RING_FIELDS = ("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events")
+RING_FIELDS = ("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events", "other_shard")
 USER_CAP = 1 << 18
 
 
@@ -90,24 +90,44 @@ class WindowPipeline:
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, use_graphs: bool = True,
                  max_ahead: int = 3, n_buffers: int = 3, user_cap: int = USER_CAP, ttft_slo_ms: float = 800.0,
-                 halo_ms: float = 0.0, import_cap: int = 0, xchg_cap: int = 0):
-        from ..ops import load_agent
+                 halo_ms: float = 0.0, import_cap: int = 0, xchg_cap: int = 0, shard: Tuple[int, int] = (0, 1),
+                 engine: str = "gpu", group=None, model_image: Optional[np.ndarray] = None):
+        """``engine``: "gpu" = the native WindowEngine on HIP device ``device`` (``comm`` = its RCCL
+        communicator); "cpu" = pipeline.cpu.CpuRingEngine, the same contract on the host, with
+        ``group`` (a torch.distributed gloo group) as its communicator. ``shard`` = (rank, world):
+        this engine's share of one node's stream (group sharding, decode.hip shard_owns).
+        ``model_image``: a PosteriorModel image to score with (models/export.py) instead of ``model``'s
+        built-in initial model."""
         from ..ops.engine import model_bytes
 
-        self.mod = load_agent()
-        if tuple(self.mod.PACKET_LAYOUT) != PACKET_LAYOUT:
-            raise RuntimeError("stale _mislo_agent build: packet layout mismatch (rebuild with ops.build)")
         self.model_name, self.seed, self.learn = model, seed, learn
-        self.device_refit = learn and model == "bayes_learned"
+        self.device_refit = learn and model == "bayes_learned" and engine == "gpu" and model_image is None
         self._model_bytes = model_bytes
         user_cap = max(1, min(int(user_cap), int(sig_cap)))
-        self.eng = self.mod.WindowEngine(device=device, sig_cap=sig_cap, span_cap=span_cap, group_cap=group_cap,
-                                         user_cap=user_cap, n_buffers=n_buffers, max_ahead=max_ahead,
-                                         window_ms=window_ms, threshold=threshold, fanout=fanout,
-                                         group_mode=group_mode, use_graphs=use_graphs,
-                                         device_refit=self.device_refit, n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms,
-                                         halo_ms=halo_ms, import_cap=import_cap, xchg_cap=xchg_cap)
+        kw = dict(device=device, sig_cap=sig_cap, span_cap=span_cap, group_cap=group_cap, user_cap=user_cap,
+                  n_buffers=n_buffers, window_ms=window_ms, threshold=threshold, fanout=fanout, group_mode=group_mode,
+                  n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms, halo_ms=halo_ms, import_cap=import_cap, xchg_cap=xchg_cap,
+                  shard_rank=int(shard[0]), shard_world=int(shard[1]))
+        self.engine_kind = engine
+        if engine == "cpu":
+            from .cpu import CpuRingEngine
+
+            self.mod = None
+            self.stats_off, self.stats_len = sum(PACKET_LAYOUT[:5]), PACKET_LAYOUT[5] + PACKET_LAYOUT[6]
+            self.eng = CpuRingEngine(group=group, **kw)
+        elif engine == "gpu":
+            from ..ops import load_agent
+
+            self.mod = load_agent()
+            if tuple(self.mod.PACKET_LAYOUT) != PACKET_LAYOUT:
+                raise RuntimeError("stale _mislo_agent build: packet layout mismatch (rebuild with ops.build)")
+            self.stats_off, self.stats_len = int(self.mod.STATS_OFF), int(self.mod.STATS_LEN)
+            self.eng = self.mod.WindowEngine(max_ahead=max_ahead, use_graphs=use_graphs,
+                                             device_refit=self.device_refit, **kw)
+        else:
+            raise ValueError(f"unknown window engine {engine!r} (gpu | cpu)")
         self.halo_ms, self.import_cap, self.xchg_cap = halo_ms, import_cap, xchg_cap
+        self.shard = (int(shard[0]), int(shard[1]))
         self.nb = self.eng.buffers
         self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
         if comm is not None and comm[2] > 1:
@@ -116,8 +136,14 @@ class WindowPipeline:
         p0[:, :N_DOMAINS] = NaiveBayes.random_init_table(seed)
         self.eng.set_p0(p0.ravel())
         self.cum_stats = SufficientStats()
-        self.model = self._initial_model()
-        self.eng.set_model_bytes(model_bytes(self.model))
+        if model_image is not None:
+            from ..ops.engine import model_from_bytes
+
+            self.model = model_from_bytes(model_image)
+            self.eng.set_model_bytes(np.ascontiguousarray(model_image, dtype=np.uint8))
+        else:
+            self.model = self._initial_model()
+            self.eng.set_model_bytes(model_bytes(self.model))
         self.k = 0
         self.windows_folded_host = 0
 
@@ -210,7 +236,7 @@ class WindowPipeline:
         self.drain()
         c = self.cum_stats
         stats = np.asarray(self.eng.stats_acc(), dtype=np.float64).copy()
-        off, n = int(self.mod.STATS_OFF), int(self.mod.STATS_LEN)
+        off, n = self.stats_off, self.stats_len
         pending = range(max(0, self.k - self.nb), self.k) if self.device_refit else range(0)
         for j in pending:
             stats += np.asarray(self.eng.packet(j), dtype=np.float64)[off:off + n]
@@ -293,7 +319,11 @@ class RingWindowSource:
     ring's producer position; records a probe stamps from then on carry the new tag, records
     stamped before it keep theirs and decode against the bases the window ships."""
 
-    def __init__(self, pipe: WindowPipeline, ring=None, user_ring=None, span_ring=None, cfg_set=None):
+    def __init__(self, pipe: WindowPipeline, ring=None, user_ring=None, span_ring=None, cfg_set=None,
+                 shared: bool = False):
+        """``shared``: the rings have other consumers too (the node's other GPU workers, agent
+        --gpus N): this source never moves a ring's consumer position, it only reports how far
+        it is done (``done()``); the agent's controller frees ring space up to the slowest."""
         from ..runtime import load
 
         self.rt = load()
@@ -320,6 +350,10 @@ class RingWindowSource:
         if span_ring is not None:
             self.direct["spans"] = pipe.eng.register_host(span_ring.address, span_ring.capacity * 64)
             self.spos = span_ring.tail
+        self.shared = shared
+        self.kernel_done = self.kpos if ring is not None else 0
+        self.user_done = self.upos if user_ring is not None else 0
+        self.span_done = self.spos if span_ring is not None else 0
         self.pending: List[tuple] = []   # (k, kernel ranges [(pos, n)], user n, span n, h2d released)
         self.late: List[tuple] = []      # kernel ranges a window found still being written
         self.last: Dict[str, int] = {}
@@ -366,19 +400,29 @@ class RingWindowSource:
                     self.resubmitted += n - skip
                     skip = 0
             if self.ring is not None and ranges:
-                done = max(self.ring.consumer_pos, max(p + 24 * n for p, n in ranges))
+                done = max(self.kernel_done, max(p + 24 * n for p, n in ranges))
                 hold = min([p for p, _ in self.late], default=None)
-                self.ring.set_consumer_pos(min(hold, done) if hold is not None else done)
+                self.kernel_done = min(hold, done) if hold is not None else done
+                if not self.shared:
+                    self.ring.set_consumer_pos(max(self.ring.consumer_pos, self.kernel_done))
         for e in self.pending:  # user / span ring space is free once the DMA that read it is done
             if not e[4] and eng.h2d_done(e[0]):
                 self._release_user(e[2], e[3])
                 e[4] = True
 
     def _release_user(self, nu: int, ns: int) -> None:
+        self.user_done += nu
+        self.span_done += ns
+        if self.shared:
+            return
         if self.user_ring is not None and nu:
             self.user_ring.release(nu)
         if self.span_ring is not None and ns:
             self.span_ring.release(ns)
+
+    def done(self) -> Tuple[int, int, int]:
+        """(BPF ring byte position, user-space records, spans) this source no longer needs."""
+        return int(self.kernel_done), int(self.user_done), int(self.span_done)
 
     def _ring_ranges(self, start: int, stop: int, rec: int, base: int, cap_pos: int, max_n: int):
         """[(address, bytes)] of records [start, stop) of a ring of ``cap_pos`` record slots."""

@@ -16,8 +16,9 @@ import os
 import sys
 import threading
 import time
+from collections import deque
 from dataclasses import dataclass
-from typing import Optional, Protocol, Tuple
+from typing import Callable, Iterable, Optional, Protocol, Tuple
 
 
 @dataclass
@@ -70,20 +71,55 @@ class ProcCPUSampler:
         return CPUSample(read_process_ticks(self.pid, self.proc_root), read_total_ticks(self.proc_root))
 
 
+class TreeCPUSampler:
+    """The agent's process tree: the controller plus its window workers (agent --gpus N). Ticks
+    of processes that have exited drop out (their last reading is kept, so the sum never goes
+    backwards)."""
+
+    def __init__(self, pids: Callable[[], Iterable[int]], proc_root: str = "/proc"):
+        self.pids, self.proc_root = pids, proc_root
+        self._last: dict = {}
+
+    def sample(self) -> CPUSample:
+        if not sys.platform.startswith("linux"):
+            raise OSError("cpu sampler requires linux")
+        for pid in set(int(p) for p in self.pids()):
+            try:
+                self._last[pid] = read_process_ticks(pid, self.proc_root)
+            except (OSError, ValueError):
+                continue
+        return CPUSample(sum(self._last.values()), read_total_ticks(self.proc_root))
+
+
 class OverheadGuard:
-    def __init__(self, max_pct: float, sampler: Optional[CPUSampler] = None, ncpu: Optional[int] = None):
+    """REF's formula; with ``horizon_s`` > 0 the percentage is taken over the samples of the
+    last ``horizon_s`` seconds instead of since the previous call: at 1 s evaluations 10 ms
+    clock ticks quantise a sub-1 % agent to 0 or >= 1 % (a gauge reading 0.0 while the agent
+    works, and shedding decisions on noise); over 30 s the resolution is 0.03 %."""
+
+    def __init__(self, max_pct: float, sampler: Optional[CPUSampler] = None, ncpu: Optional[int] = None,
+                 horizon_s: float = 0.0):
         self.max_pct = max_pct
         self.source = sampler if sampler is not None else ProcCPUSampler()
         self.ncpu = ncpu if ncpu is not None else (os.cpu_count() or 1)
+        self.horizon_s = float(horizon_s)
         self._prev: Optional[CPUSample] = None
+        self._hist: deque = deque()
 
     def evaluate(self) -> Tuple[float, bool]:
         """Returns (pct, exceeded). Raises on sampler error (REF returns err)."""
         s = self.source.sample()
         if self._prev is None:
             self._prev = s
+            self._hist.append((time.monotonic(), s))
             return 0.0, False
         prev, self._prev = self._prev, s
+        if self.horizon_s > 0:
+            now = time.monotonic()
+            self._hist.append((now, s))
+            while len(self._hist) > 2 and now - self._hist[1][0] >= self.horizon_s:
+                self._hist.popleft()
+            prev = self._hist[0][1]
         if s.total_ticks <= prev.total_ticks:
             return 0.0, False
         d_proc = s.process_ticks - prev.process_ticks

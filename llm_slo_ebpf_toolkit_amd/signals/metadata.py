@@ -164,5 +164,10 @@ class Interner:
     def name(self, i: int) -> str:
         return self._names[i] if 0 <= i < len(self._names) else ""
 
+    def names(self) -> list:
+        """Every interned string in id order (id 0 = "")."""
+        with self._lock:
+            return list(self._names)
+
     def __len__(self) -> int:
         return len(self._names)

@@ -1,0 +1,125 @@
+"""The shipped deployments start: the Helm chart's and the kustomize
+DaemonSet's agent arguments, rendered with their own values / ConfigMap, parse with the agent's
+CLI into options the window engine accepts; the learned model they point at is the one
+`attributor --train` produces; the helm test pod is well formed."""
+
+import os
+import re
+
+import numpy as np
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIPPED_MODEL = "config/models/mislo-learned.safetensors"
+
+
+def _get(values, dotted):
+    v = values
+    for part in dotted.split("."):
+        v = v[part]
+    return v
+
+
+def render_chart_args():
+    """The chart's container args with `{{ .Values.* }}` substituted from values.yaml (the chart
+    uses no other construct in its args; `range .Values.agent.extraArgs` expands the list)."""
+    with open(os.path.join(ROOT, "charts/llm-slo-agent/values.yaml")) as fh:
+        values = yaml.safe_load(fh)
+    with open(os.path.join(ROOT, "charts/llm-slo-agent/templates/daemonset.yaml")) as fh:
+        text = fh.read()
+    block = text[text.index("          args:\n"):text.index("          env:")]
+    args = []
+    in_range = False
+    for ln in block.splitlines()[1:]:
+        s = ln.strip()
+        if s.startswith("{{- range .Values.agent.extraArgs"):
+            in_range = True
+            args += [str(x) for x in values["agent"]["extraArgs"]]
+            continue
+        if s.startswith("{{- end"):
+            in_range = False
+            continue
+        if in_range or not s.startswith("- "):
+            continue
+        arg = re.sub(r"\{\{\s*\.Values\.([\w.]+)\s*\}\}", lambda m: str(_get(values, m.group(1))), s[2:])
+        assert "{{" not in arg, arg
+        args.append(arg)
+    return args, values
+
+
+def render_kustomize_args():
+    """The kustomize DaemonSet's args with $(VAR) expanded from the ConfigMap and the pod env."""
+    docs = {}
+    for rel in ("deploy/k8s/daemonset.yaml", "deploy/k8s/configmap.yaml"):
+        with open(os.path.join(ROOT, rel)) as fh:
+            for d in yaml.safe_load_all(fh):
+                if d:
+                    docs[d["kind"]] = d
+    c = docs["DaemonSet"]["spec"]["template"]["spec"]["containers"][0]
+    env = {k: str(v) for k, v in docs["ConfigMap"]["data"].items() if k.isupper()}
+    for e in c.get("env", []):
+        env[e["name"]] = str(e.get("value", f"<{e['name']}>"))
+    out = []
+    for a in c["args"]:
+        a2 = re.sub(r"\$\((\w+)\)", lambda m: env[m.group(1)], a)
+        out.append(a2)
+    return out, c
+
+
+def _check(args):
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+    from llm_slo_ebpf_toolkit_amd.cli import agent as cli
+
+    opts, smoke = cli.parse(args)
+    assert not smoke
+    assert isinstance(opts, AgentOptions)
+    assert opts.engine == "gpu" and opts.source == "bpf", (opts.engine, opts.source)
+    assert opts.gpus == 0  # every GPU of the node
+    assert opts.model_path.endswith(SHIPPED_MODEL.split("/", 1)[1])
+    assert opts.otlp_receiver_bind.endswith(":4318") and opts.otlp_receiver_allow
+    a = Agent(AgentOptions(**{**opts.__dict__, "config": os.path.join(ROOT, "config", "toolkit.yaml"),
+                              "metrics_bind": "", "output": "stdout"}))
+    a.o.model_path = os.path.join(ROOT, SHIPPED_MODEL)
+    model, image, meta = a._load_model()  # the model file the image ships loads
+    assert meta["name"] == "bayes_learned" and image.size == 2568
+    a.close()
+
+
+def test_helm_chart_args_start_the_agent():
+    args, values = render_chart_args()
+    assert values["agent"]["source"] == "bpf"
+    _check(args)
+
+
+def test_kustomize_daemonset_args_start_the_agent():
+    args, c = render_kustomize_args()
+    _check(args)
+    names = {e["name"] for e in c.get("env", [])}
+    assert "HIP_VISIBLE_DEVICES" not in names  # the agent uses every GPU of the node
+
+
+def test_helm_test_pod_checks_the_agent_endpoints():
+    with open(os.path.join(ROOT, "charts/llm-slo-agent/templates/tests/test-connection.yaml")) as fh:
+        text = fh.read()
+    assert '"helm.sh/hook": test' in text
+    for path in ("/healthz", "/readyz", "/metrics"):
+        assert path in text
+    for name in re.findall(r"\^(llm_slo_agent_\w+)", text):
+        from llm_slo_ebpf_toolkit_amd.agent.metrics import AgentMetrics
+
+        m = AgentMetrics("probe", "core_full", [], [])
+        assert name in m.registry.exposition(), name
+
+
+def test_shipped_model_is_what_attributor_train_produces():
+    """config/models/mislo-learned.safetensors is `attributor --train` with its defaults: the
+    deterministic training set and fit reproduce it, and on REF's 55 rows it beats REF's table
+    on all three of REF's quality numbers."""
+    from llm_slo_ebpf_toolkit_amd.models import train
+
+    model, image, meta = train.load_model(os.path.join(ROOT, SHIPPED_MODEL))
+    tm = train.train_cpu(train.TrainConfig())
+    np.testing.assert_array_equal(image, tm.image())
+    r = meta["ref55"]
+    assert r["single_fault_macro_f1"] >= 0.9818 and r["multi_fault_partial_accuracy"] >= 1.0
+    assert r["multi_fault_coverage_accuracy"] >= 0.667

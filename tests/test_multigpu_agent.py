@@ -1,0 +1,171 @@
+"""Multi-GPU node agent on CPU: the benchmark self-launches its ranks, the agent
+splits one node's stream over N window workers (group sharding, agent/worker.py) and two
+spawned workers running the CPU engine over gloo reproduce the single-process window exactly;
+the node id is stable across processes."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_self_launches_its_ranks():
+    """`bench.py --gpus 2` with no launcher env starts 2 ranks itself (fresh interpreters, the
+    parent never touches the GPU) and rank 0's JSON reports the world the ranks formed."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-probe"],
+                         capture_output=True, text=True, env=env, timeout=240, check=True).stdout
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["gpus_requested"] == 2
+    assert sorted(r[0] for r in d["ranks"]) == [0, 1] and sorted(r[1] for r in d["ranks"]) == [0, 1]
+    assert len({r[2] for r in d["ranks"]}) == 2  # two processes
+
+
+def test_node_id_is_stable_across_processes():
+    code = ("from llm_slo_ebpf_toolkit_amd.collector.bpf import stable_node_id; "
+            "print(stable_node_id('mi355x-node-07'))")
+    ids = set()
+    for seed in ("1", "2", "3"):
+        env = dict(os.environ, PYTHONHASHSEED=seed)
+        ids.add(subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=ROOT,
+                               check=True).stdout.strip())
+    assert len(ids) == 1
+    v = int(ids.pop())
+    assert 1 <= v <= 0xFFFE
+
+
+def test_merge_results_places_every_group_once():
+    from llm_slo_ebpf_toolkit_amd.agent.worker import groups_of, merge_results
+
+    G, W = 11, 3
+    parts = []
+    for r in range(W):
+        n = groups_of(r, W, G)
+        g = np.arange(r, G, W)
+        parts.append({"post": np.tile(g[:, None], (1, 16)).astype(float), "conf": g.astype(float),
+                      "feat": np.tile(g[:, None], (1, 16)).astype(np.float32), "pred": g.astype(np.int32),
+                      "evbits": np.zeros((n, 16), np.uint32), "sli": np.tile(g[:, None], (1, 2)).astype(np.uint32)})
+    m = merge_results(parts, G)
+    np.testing.assert_array_equal(m["pred"], np.arange(G))
+    np.testing.assert_array_equal(m["sli"][:, 0], np.arange(G))
+
+
+def _windows(n_win=3, seed=11):
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
+
+    cfg = ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8, events_per_window=3000,
+                       spans_per_window=160, seed=seed)
+    g = ReplayGenerator(cfg)
+    wins = [g.next_window() for _ in range(n_win)]
+    sn = (g.pod_svc.astype(np.uint32) << np.uint32(16)) | g.pod_node.astype(np.uint32)
+    return wins, build_replay_images(wins, user_rec=24), (g.pod_ids.astype(np.uint32), sn)
+
+
+def _spec(r, world, tag, pods, port=0, engine="cpu"):
+    from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerSpec, groups_of
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+    from llm_slo_ebpf_toolkit_amd.ops.engine import model_bytes
+
+    return WorkerSpec(rank=r, world=world, device=0, engine=engine, source="shm", ring_name=tag, pin_dir="",
+                      user_rec=24, sig_cap=8192, span_cap=512, group_cap=groups_of(0, world, 8), user_cap=4096,
+                      window_ms=1000.0, ttft_slo_ms=800.0, halo_ms=2000.0, import_cap=16384,
+                      xchg_cap=512 if world > 1 else 0, model_image=model_bytes(NaiveBayes.ref()).tobytes(),
+                      pods=pods, master=("127.0.0.1", port))
+
+
+def _run_pool(world, imgs, pods, tag):
+    import socket
+
+    from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerPool, merge_results
+    from llm_slo_ebpf_toolkit_amd.collector import bpf
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut
+
+    names = bpf.RingNames.of(tag)
+    ring, user, spans = bpf.create_rings(names, 1 << 22, 1 << 14, 1 << 12, user_rec=24)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    pool = WorkerPool([_spec(r, world, tag, pods, port) for r in range(world)], (ring, user, spans),
+                      in_process=world == 1)
+    out = []
+    try:
+        replies = []
+        for img in imgs:
+            assert ring.append_framed(img.framed)
+            assert user.push(img.user) == len(img.user) and spans.push(img.spans) == len(img.spans)
+            replies.append(pool.window(Cut(ring.producer_pos, user.head, spans.head, img.bases), 8))
+        replies.append(pool.stop())
+        for rep in replies[1:]:
+            prev = [r["prev"] for r in rep]
+            out.append({"packet": prev[0]["packet"], "res": merge_results(prev[0]["results"], 8),
+                        "events": sum(int(p["ring"][5]) for p in prev)})
+        # every worker is done with every record: the controller freed the rings completely
+        assert ring.consumer_pos == ring.producer_pos and user.size == 0 and spans.size == 0
+    finally:
+        pool.close()
+    return out
+
+
+@pytest.mark.timeout(300)
+def test_two_cpu_workers_reproduce_the_single_process_window():
+    """The same windows through one in-process worker and through two spawned workers (CPU
+    engine, gloo): node-wide packet (histograms, status, value sums, join counters: all-reduced),
+    every incident's features / posteriors / predictions / SLO counts, and the node's event
+    count are identical -- group sharding loses and duplicates nothing, the halo included."""
+    wins, imgs, pods = _windows()
+    tag = f"/mislo-mg-{os.getpid()}"
+    one = _run_pool(1, imgs, pods, tag + "-a")
+    two = _run_pool(2, imgs, pods, tag + "-b")
+    assert len(one) == len(two) == len(imgs)
+    for j, (a, b) in enumerate(zip(one, two)):
+        n = 256 + 48 + 18 + 8  # hist, status, misc, dbg
+        np.testing.assert_array_equal(a["packet"][:n], b["packet"][:n], err_msg=f"window {j}")
+        for key in ("feat", "pred", "sli", "evbits"):
+            np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
+        np.testing.assert_allclose(a["res"]["post"], b["res"]["post"], rtol=1e-12, atol=1e-15)
+        assert a["events"] == b["events"] > 0
+        assert (a["res"]["sli"][:, 0] > 0).all()
+
+
+@pytest.mark.timeout(300)
+def test_agent_cpu_engine_with_two_workers_end_to_end(tmp_path):
+    """`agent --engine cpu --gpus 2 --source replay`: the controller spawns two workers, emits
+    schema-valid attributions for the node's incidents, and checkpoints / resumes its state."""
+    code = f"""
+import io, json, os, sys
+sys.path.insert(0, {ROOT!r})
+from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+from llm_slo_ebpf_toolkit_amd.contracts import validator
+if __name__ == "__main__":
+    out = io.StringIO()
+    o = AgentOptions(engine="cpu", source="replay", gpus=2, window_events=4096, window_spans=256, window_groups=8,
+                     window_ms=400, count=5, metrics_bind="", output="stdout", ring_name="/mislo-e2e-%d" % os.getpid(),
+                     config="", min_confidence=0.0, state_dir={str(tmp_path)!r})
+    a = Agent(o, out_stream=out)
+    rc = a.run_windows(max_windows=5)
+    recs = [json.loads(x) for x in out.getvalue().splitlines()]
+    schema = validator.compiled("incident-attribution")
+    assert all(schema.is_valid(r) for r in recs), recs[:1]
+    print(json.dumps({{"rc": rc, "n": len(recs), "services": sorted({{r["service"] for r in recs}}),
+                      "windows": a.windows_done, "workers": len(a.pool.workers)}}))
+    a.close()
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["rc"] == 0 and d["workers"] == 2 and d["windows"] == 5
+    assert d["n"] > 0 and len(d["services"]) >= 4
+    st = [f for f in os.listdir(tmp_path) if f.endswith(".state.json")]
+    assert st, os.listdir(tmp_path)
+    with open(tmp_path / st[0]) as fh:
+        state = json.load(fh)
+    assert state["windows"] == 5 and state["burn"]["hist"]

@@ -280,3 +280,87 @@ def test_checkpoint_resume_restores_every_finished_window(tmp_path):
     assert b.windows_folded == 6
     a.eng.close()
     b.eng.close()
+
+
+def test_group_sharding_on_device_matches_the_whole_stream():
+    """agent --gpus N on one GPU's worth of checks: engines configured as shard 0/2 and 1/2 decode
+    the same ring bytes, each keeps only its services' records and incident groups (decode.hip
+    shard_owns); their histograms add up to the whole-stream engine's and their local groups'
+    features, SLO counts and posteriors are the whole-stream engine's, group for group."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+
+    wins, gen = windows(n_win=2, seed=53)
+    imgs = build_replay_images(wins, user_rec=24)
+    pods = pod_meta(gen)
+    out = {}
+    for shard in ((0, 1), (0, 2), (1, 2)):
+        G = len(range(shard[0], 8, shard[1]))
+        pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096, shard=shard, halo_ms=2000.0,
+                              import_cap=8192)
+        rb, user, spans = rings(f"shard{shard[0]}{shard[1]}", 24)
+        src = RingWindowSource(pipe, rb, user, spans)
+        pipe.eng.set_pods(*pods)
+        res = []
+        for img in imgs:
+            k = src.stage(feed(img, rb, user, spans), G, None)["k"]
+            res.append((pipe.packet(k), pipe.results(k, G)))
+        src.drain()
+        pipe.eng.close()
+        out[shard] = res
+    for j in range(len(imgs)):
+        whole, a, b = out[(0, 1)][j], out[(0, 2)][j], out[(1, 2)][j]
+        np.testing.assert_array_equal(whole[0]["hist"], a[0]["hist"] + b[0]["hist"])
+        assert whole[0]["ring_state"]["events"] == a[0]["ring_state"]["events"] + b[0]["ring_state"]["events"]
+        assert a[0]["ring_state"]["other_shard"] == b[0]["ring_state"]["events"]
+        for r, part in ((0, a), (1, b)):
+            np.testing.assert_array_equal(part[1]["feat"], whole[1]["feat"][r::2], err_msg=f"window {j} shard {r}")
+            np.testing.assert_array_equal(part[1]["sli"], whole[1]["sli"][r::2])
+            np.testing.assert_allclose(part[1]["post"], whole[1]["post"][r::2], rtol=1e-12, atol=1e-15)
+
+
+def test_soft_label_statistics_temperature_refit_and_scoring():
+    """Learning on the device with soft labels (a multi-fault incident's mass spread over its
+    domain set, label_code) gives the host's SufficientStats; the refit with a temperature and a
+    minimum domain mass is NaiveBayes.learned(..., temperature, min_count); scoring REF's 55
+    rows through the engine's posterior kernel matches the host model."""
+    from llm_slo_ebpf_toolkit_amd.models.bayes import SufficientStats, label_code, soft_labels
+    from llm_slo_ebpf_toolkit_amd.models.train import ref55_report, host_scorer
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+
+    wins, gen = windows(n_win=3, seed=59)
+    imgs = build_replay_images(wins)
+    pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", user_cap=4096)
+    rb, user, spans = rings("softlab")
+    src = RingWindowSource(pipe, rb, user, spans)
+    pipe.eng.set_pods(*pod_meta(gen))
+    host = SufficientStats()
+    rng = np.random.default_rng(5)
+    for img in imgs:
+        codes = np.array([label_code(int(l), [int(l), int(rng.integers(0, 5))] if rng.random() < 0.5 else [])
+                          for l in img.labels], dtype=np.int32)
+        k = src.stage(feed(img, rb, user, spans), img.n_groups, codes)["k"]
+        res = pipe.results(k, img.n_groups)
+        host.add(res["feat"].astype(np.float64), soft_labels(codes))
+    src.drain()
+    # the device has folded the windows the prequential refit reached; the last nb are in their packets
+    arrays, meta = pipe.state()
+    st = arrays["stats_acc"]
+    np.testing.assert_allclose(st[1024:1024 + 10], host.count, rtol=1e-12)
+    np.testing.assert_allclose(st[:1024].reshape(32, 32)[:16, :10], host.elevated_sum, rtol=1e-12, atol=1e-12)
+    # refit from exactly these statistics with a temperature and a minimum domain mass
+    pipe.eng.restore(st, np.zeros(0, np.uint8), len(imgs))
+    pipe.eng.set_refit(2.0, 1.0, 1.0 / 2.5, 1.0)
+    pipe.eng.refit_now()
+    model = NaiveBayes.learned(host, seed=42, temperature=2.5, min_count=1.0)
+    fx = os.path.join(os.path.dirname(__file__), "fixtures", "ref_multi_fault_samples.jsonl")
+
+    def dev(feat):
+        r = pipe.eng.score(np.ascontiguousarray(feat, dtype=np.float32), None)
+        return r["post"][:, :10], r["pred"]
+
+    f = np.random.default_rng(3).uniform(0, 300, (40, 16)).astype(np.float32)
+    p_dev, pred_dev = dev(f)
+    np.testing.assert_allclose(p_dev, model.posteriors(f.astype(np.float64)), rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(pred_dev, np.argmax(model.logits(f.astype(np.float64)), axis=1))
+    assert ref55_report(fx, dev) == ref55_report(fx, host_scorer(model))
+    pipe.eng.close()
