@@ -244,8 +244,10 @@ def main() -> int:
 
     # ---- data: this rank's node shard, run through the probe model (CPU, before the GPU) ----
     t = time.time()
+    # the cycled windows share one fault assignment: the halo joins each window's start with
+    # the previous window's end, and a fault persists across consecutive windows
     cfg = ReplayConfig(scenario=a.scenario, events_per_window=a.events, spans_per_window=a.spans,
-                       n_services=a.services, seed=a.seed, shard=rank)
+                       n_services=a.services, seed=a.seed, shard=rank, fault_hold=max(1, a.windows))
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
     # held out: a different seed (never trained on), REF's label set and the full set
@@ -254,7 +256,7 @@ def main() -> int:
         hcfg = ReplayConfig(scenario=HELDOUT_SCENARIOS[j % len(HELDOUT_SCENARIOS)], events_per_window=a.events,
                             spans_per_window=a.spans, n_services=a.services, seed=a.seed + 7919, shard=rank)
         hg = ReplayGenerator(hcfg)
-        hg.window = 1000 + j  # later in time than the training windows
+        hg.window = 1000 + 10 * j  # later than the timed windows, 10 s apart: no halo reaches across scenarios
         held.append(hg.next_window())
     images = build_replay_images(wins + held, user_rec=a.user_rec)
     imgs, himgs = images[: len(wins)], images[len(wins):]
@@ -270,7 +272,10 @@ def main() -> int:
                                               seed=a.seed + 1000 + 101 * i, shard=rank,
                                               start_ns=cfg.start_ns - 3600 * 10 ** 9))
                  for i, sc in enumerate(mtrain.TRAIN_SCENARIOS)]
-        train_wins = [tgens[j % len(tgens)].next_window() for j in range(a.train_windows)]
+        for j in range(a.train_windows):  # 10 s apart: the halo never joins two training incidents
+            tg = tgens[j % len(tgens)]
+            tg.window = 10 * j
+            train_wins.append(tg.next_window())
     train_imgs = build_replay_images(train_wins, user_rec=a.user_rec) if train_wins else []
     train_codes = [mtrain.window_codes(w) for w in train_wins]
     pods = np.unique(np.concatenate([w.events["pod_id"] for w in wins + held]))

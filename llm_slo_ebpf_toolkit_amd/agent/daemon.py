@@ -387,7 +387,8 @@ class Agent:
                 from ..collector.probes import ProbeManager
 
                 self.probe_manager = ProbeManager(self.mode, self.generator.enabled_signals())
-                for spec in probe_specs(BpfProbeLoader(o.probe_objs, o.pin_dir), self.generator.enabled_signals()):
+                self.bpf_loader = BpfProbeLoader(o.probe_objs, o.pin_dir)
+                for spec in probe_specs(self.bpf_loader, self.generator.enabled_signals()):
                     self.probe_manager.register(spec)
                 attached = self.probe_manager.attach_all()
                 print(f"attached probes for {len(attached)} signals from {o.probe_objs}", file=sys.stderr)
@@ -660,6 +661,8 @@ class Agent:
                     self._emit_window(replies, cut_t.pop(prev["k"], t), G, names, ring, model)
                 if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
                     self._scan_pods(maps)  # pod churn
+                    if getattr(self, "bpf_loader", None) is not None:
+                        self.bpf_loader.rescan_uprobes()  # libssl / librccl of new workloads
                 self.windows_done += 1
                 windows += 1
                 if state and o.checkpoint_every > 0 and self.windows_done % o.checkpoint_every == 0:

@@ -213,7 +213,8 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
     rb = rt.Ringbuf.attach_shm(names.ring)
     user = rt.HostRing(0, 64, names.user, True)
     spans = rt.HostRing(0, 64, names.spans, True)
-    cfg = ReplayConfig(window_ms=window_ms, **cfg_kwargs)
+    # the cycled images keep one fault assignment (window k's halo joins window k+1)
+    cfg = ReplayConfig(window_ms=window_ms, fault_hold=max(1, n_images), **cfg_kwargs)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, n_images))]
     sim = rt.ProbeSim(rb, records.milli_shift_table())

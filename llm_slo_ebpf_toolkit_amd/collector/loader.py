@@ -15,8 +15,12 @@ BTF loader:
 * every later object loads with ``map name <m> pinned <pin_dir>/<m>`` for each shared map,
   reusing them;
 * ``autoattach`` attaches each program by its section (kprobe/kretprobe, fentry/fexit,
-  tracepoints, uprobes) and pins the links under ``<pin_dir>/progs/<object>``; unloading a
-  probe removes that directory, which detaches it.
+  tracepoints) and pins the links under ``<pin_dir>/progs/<object>``; unloading a probe
+  removes that directory, which detaches it;
+* uprobe programs (``SEC("uprobe")``: no binary in the section) are only pinned by bpftool; the
+  loader attaches them to every mapped instance of their library (collector/uprobes.py:
+  /proc/<pid>/maps, ELF symbol offsets, perf_event_open + BPF_LINK_CREATE) and ``rescan_uprobes``
+  attaches the libraries of workloads started since.
 
 ``probe_specs`` turns the objects into ``ProbeManager`` specs (one per signal; signals of one
 object share a reference-counted load), so the overhead guard's shedding really detaches
@@ -57,11 +61,29 @@ class LoaderError(RuntimeError):
 
 class BpfProbeLoader:
     def __init__(self, obj_dir: str, pin_dir: str = "/sys/fs/bpf/mislo", bpftool: str = "bpftool",
-                 run: Optional[Callable[[List[str]], None]] = None):
+                 run: Optional[Callable[[List[str]], None]] = None, uprobes=None):
         self.obj_dir, self.pin_dir, self.bpftool = obj_dir, pin_dir, bpftool
         self._run = run or self._subprocess
         self._lock = threading.Lock()
         self._refs: Dict[str, int] = {}
+        self._uprobes = uprobes  # collector.uprobes.UprobeAttacher (created on first use)
+
+    @property
+    def uprobes(self):
+        if self._uprobes is None:
+            from .uprobes import UprobeAttacher
+
+            self._uprobes = UprobeAttacher(self.pin_dir)
+        return self._uprobes
+
+    def rescan_uprobes(self) -> int:
+        """Attach the loaded probes' uprobe programs to libraries mapped since the last scan."""
+        from .uprobes import UPROBE_PROBES
+
+        with self._lock:
+            if not any(p in UPROBE_PROBES for p in self._refs):
+                return 0
+        return self.uprobes.rescan()
 
     # ---- plumbing ------------------------------------------------------------------------
     @staticmethod
@@ -104,6 +126,10 @@ class BpfProbeLoader:
                 if os.path.exists(self.prog_dir(probe)):  # a previous agent's pins
                     shutil.rmtree(self.prog_dir(probe), ignore_errors=True)
                 self._run(self.load_cmd(probe))
+                from .uprobes import UPROBE_PROBES
+
+                if probe in UPROBE_PROBES:
+                    self.uprobes.attach(probe)
             self._refs[probe] = n + 1
 
     def unload(self, probe: str) -> None:
@@ -113,6 +139,10 @@ class BpfProbeLoader:
             if n <= 0:
                 return
             if n == 1:
+                from .uprobes import UPROBE_PROBES
+
+                if probe in UPROBE_PROBES and self._uprobes is not None:
+                    self._uprobes.detach(probe)  # close the uprobe links first
                 shutil.rmtree(self.prog_dir(probe), ignore_errors=True)
                 del self._refs[probe]
             else:

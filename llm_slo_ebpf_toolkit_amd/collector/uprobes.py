@@ -1,0 +1,258 @@
+"""Uprobe attachment to the binaries the node's workloads actually map.
+
+REF's TLS probe leaves the libssl path to its loader (/root/reference/ebpf/c/tls_handshake.bpf.c
+:12-14), and no REF binary ever attaches it. A libbpf ``SEC("uprobe/<func>")`` names no binary,
+so no loader can auto-attach it either. NEW's uprobe programs are declared ``SEC("uprobe")`` /
+``SEC("uretprobe")``: ``bpftool prog loadall ... autoattach`` attaches the kprobes and
+tracepoints of an object and merely pins its uprobe programs, and the agent attaches those
+itself:
+
+1. **resolve** -- every process's ``/proc/<pid>/maps`` names the shared objects it mapped; a
+   library matching the target (``libssl.so*``, ``librccl.so*``) is addressed through
+   ``/proc/<pid>/root/<path>`` (the container's mount namespace, seen from the host-PID agent),
+   de-duplicated by (device, inode): one attachment per distinct file, however many processes
+   and containers map it;
+2. **locate** -- the function's file offset from the ELF itself (.dynsym / .symtab value mapped
+   through the PT_LOAD segment that holds it), cached per file;
+3. **attach** -- ``perf_event_open`` on the uprobe PMU (type and retprobe bit read from
+   /sys/bus/event_source/devices/uprobe) with the path and offset, then ``BPF_LINK_CREATE`` of
+   the pinned program onto that perf event (runtime/csrc/bpfsys.cpp); closing the link detaches.
+
+``UprobeAttacher.rescan()`` (the agent calls it with its pod rescans) attaches newly started
+workloads' libraries. The syscalls go through an injectable object so the argument flow is
+unit-tested without privileges.
+"""
+
+from __future__ import annotations
+
+import os
+import re
+import struct
+import threading
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Tuple
+
+
+@dataclass(frozen=True)
+class UprobeTarget:
+    probe: str        # probe object (probes/ebpf/<probe>.bpf.o)
+    program: str      # program name in it (pinned as progs/<probe>/<program>)
+    library: str      # regex on the mapped file's basename
+    symbol: str
+    retprobe: bool
+
+
+UPROBE_TARGETS: Tuple[UprobeTarget, ...] = (
+    UprobeTarget("tls_handshake", "tls_enter", r"^libssl\.so", "SSL_do_handshake", False),
+    UprobeTarget("tls_handshake", "tls_exit", r"^libssl\.so", "SSL_do_handshake", True),
+    UprobeTarget("gpu_kfd", "allreduce_enter", r"^librccl\.so", "ncclAllReduce", False),
+    UprobeTarget("gpu_kfd", "allreduce_exit", r"^librccl\.so", "ncclAllReduce", True),
+    UprobeTarget("gpu_kfd", "allgather_enter", r"^librccl\.so", "ncclAllGather", False),
+    UprobeTarget("gpu_kfd", "allgather_exit", r"^librccl\.so", "ncclAllGather", True),
+    UprobeTarget("gpu_kfd", "reducescatter_enter", r"^librccl\.so", "ncclReduceScatter", False),
+    UprobeTarget("gpu_kfd", "reducescatter_exit", r"^librccl\.so", "ncclReduceScatter", True),
+)
+UPROBE_PROBES = frozenset(t.probe for t in UPROBE_TARGETS)
+
+
+# ---------------------------------------------------------------------------------------
+# ELF: function name -> file offset
+# ---------------------------------------------------------------------------------------
+
+def elf_symbol_offset(path: str, symbol: str) -> Optional[int]:
+    """File offset of ``symbol`` (a defined function) in a 64-bit little-endian ELF, or None."""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    if len(data) < 64 or data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        return None
+    e_phoff, e_shoff = struct.unpack_from("<QQ", data, 0x20)
+    e_phentsize, e_phnum, e_shentsize, e_shnum = struct.unpack_from("<HHHH", data, 0x36)
+    segs = []
+    for i in range(e_phnum):
+        p_type, _flags, p_offset, p_vaddr, _paddr, p_filesz = struct.unpack_from("<IIQQQQ", data,
+                                                                                 e_phoff + i * e_phentsize)
+        if p_type == 1:  # PT_LOAD
+            segs.append((p_vaddr, p_filesz, p_offset))
+    secs = []
+    for i in range(e_shnum):
+        o = e_shoff + i * e_shentsize
+        if o + 64 > len(data):
+            break
+        _name, sh_type, _flags, _addr, sh_offset, sh_size, sh_link, _info, _align, sh_entsize = \
+            struct.unpack_from("<IIQQQQIIQQ", data, o)
+        secs.append((sh_type, sh_offset, sh_size, sh_link, sh_entsize))
+    want = symbol.encode()
+    for sh_type, off, size, link, ent in secs:
+        if sh_type not in (2, 11) or ent != 24 or link >= len(secs):  # SHT_SYMTAB, SHT_DYNSYM
+            continue
+        str_off = secs[link][1]
+        for j in range(size // ent):
+            st_name, st_info, _other, st_shndx, st_value, _size = struct.unpack_from("<IBBHQQ", data, off + j * ent)
+            if st_value == 0 or st_shndx == 0 or (st_info & 0xF) != 2:  # defined STT_FUNC
+                continue
+            end = data.find(b"\x00", str_off + st_name)
+            name = data[str_off + st_name:end]
+            if name == want or name.split(b"@")[0] == want:
+                for vaddr, filesz, poff in segs:
+                    if vaddr <= st_value < vaddr + filesz:
+                        return st_value - vaddr + poff
+                return st_value
+    return None
+
+
+# ---------------------------------------------------------------------------------------
+# /proc: which processes map which library
+# ---------------------------------------------------------------------------------------
+
+_MAPS = re.compile(r"^[0-9a-f]+-[0-9a-f]+ \S+ [0-9a-f]+ ([0-9a-f]+:[0-9a-f]+) (\d+)\s+(/\S.*)$")
+
+
+def mapped_libraries(pattern: str, proc_root: str = "/proc", pids: Optional[Iterable[int]] = None
+                     ) -> Dict[Tuple[str, int], str]:
+    """(device, inode) -> a path to that file usable from here (/proc/<pid>/root/<path>) for every
+    mapped file whose basename matches ``pattern``."""
+    rx = re.compile(pattern)
+    out: Dict[Tuple[str, int], str] = {}
+    if pids is None:
+        try:
+            pids = [int(p) for p in os.listdir(proc_root) if p.isdigit()]
+        except OSError:
+            return out
+    for pid in pids:
+        try:
+            with open(os.path.join(proc_root, str(pid), "maps")) as fh:
+                lines = fh.readlines()
+        except OSError:
+            continue
+        for ln in lines:
+            m = _MAPS.match(ln.rstrip("\n"))
+            if not m:
+                continue
+            dev, ino, path = m.group(1), int(m.group(2)), m.group(3)
+            if ino == 0 or path.endswith(" (deleted)") or not rx.search(os.path.basename(path)):
+                continue
+            out.setdefault((dev, ino), os.path.join(proc_root, str(pid), "root", path.lstrip("/")))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# attach
+# ---------------------------------------------------------------------------------------
+
+class NativeSys:
+    """The real syscalls (runtime/csrc/bpfsys.cpp); every call returns an fd or -errno."""
+
+    def __init__(self, sysfs: str = "/sys/bus/event_source/devices/uprobe"):
+        from ..runtime import load
+
+        self.rt = load()
+        self.sysfs = sysfs
+
+    def pmu(self) -> Tuple[int, int]:
+        with open(os.path.join(self.sysfs, "type")) as fh:
+            typ = int(fh.read().strip())
+        bit = 0
+        try:
+            with open(os.path.join(self.sysfs, "format", "retprobe")) as fh:
+                bit = int(fh.read().strip().split(":")[1])
+        except (OSError, IndexError, ValueError):
+            pass
+        return typ, bit
+
+    def obj_get(self, path: str) -> int:
+        return self.rt.bpf_obj_get(path)
+
+    def perf_uprobe_open(self, pmu_type: int, retprobe_bit: int, retprobe: bool, path: str, offset: int,
+                         pid: int = -1) -> int:
+        return self.rt.perf_uprobe_open(pmu_type, retprobe_bit, retprobe, path, offset, pid)
+
+    def link_create(self, prog_fd: int, perf_fd: int) -> int:
+        return self.rt.bpf_link_create_perf(prog_fd, perf_fd)
+
+    def close(self, fd: int) -> None:
+        self.rt.close_fd(fd)
+
+
+@dataclass
+class _Probe:
+    progs: Dict[str, int] = field(default_factory=dict)                 # program -> prog fd
+    links: Dict[Tuple[str, Tuple[str, int]], int] = field(default_factory=dict)  # (program, file) -> link fd
+
+
+class UprobeAttacher:
+    """Attaches the pinned uprobe programs of loaded probe objects to every mapped instance of
+    their libraries; ``rescan()`` picks up new ones, ``detach(probe)`` closes the links."""
+
+    def __init__(self, pin_dir: str, sys_=None, proc_root: str = "/proc"):
+        self.pin_dir, self.proc_root = pin_dir, proc_root
+        self.sys = sys_ if sys_ is not None else NativeSys()
+        self._pmu: Optional[Tuple[int, int]] = None
+        self._probes: Dict[str, _Probe] = {}
+        self._offsets: Dict[Tuple[Tuple[str, int], str], Optional[int]] = {}
+        self._lock = threading.Lock()
+        self.errors: List[str] = []
+
+    def attach(self, probe: str) -> int:
+        """Open the probe's pinned uprobe programs and attach them; returns links created."""
+        with self._lock:
+            st = self._probes.setdefault(probe, _Probe())
+            for t in UPROBE_TARGETS:
+                if t.probe == probe and t.program not in st.progs:
+                    fd = self.sys.obj_get(os.path.join(self.pin_dir, "progs", probe, t.program))
+                    if fd < 0:
+                        self.errors.append(f"{probe}/{t.program}: pinned program not found ({fd})")
+                        continue
+                    st.progs[t.program] = fd
+        return self.rescan(probe)
+
+    def rescan(self, probe: Optional[str] = None) -> int:
+        with self._lock:
+            if self._pmu is None:
+                self._pmu = self.sys.pmu()
+            pmu_type, bit = self._pmu
+            made = 0
+            libs_cache: Dict[str, Dict[Tuple[str, int], str]] = {}
+            for name, st in self._probes.items():
+                if probe is not None and name != probe:
+                    continue
+                for t in UPROBE_TARGETS:
+                    if t.probe != name or t.program not in st.progs:
+                        continue
+                    if t.library not in libs_cache:
+                        libs_cache[t.library] = mapped_libraries(t.library, self.proc_root)
+                    for key, path in libs_cache[t.library].items():
+                        if (t.program, key) in st.links:
+                            continue
+                        ck = (key, t.symbol)
+                        if ck not in self._offsets:
+                            self._offsets[ck] = elf_symbol_offset(path, t.symbol)
+                        off = self._offsets[ck]
+                        if off is None:
+                            continue  # this build of the library does not export the function
+                        pfd = self.sys.perf_uprobe_open(pmu_type, bit, t.retprobe, path, off, -1)
+                        if pfd < 0:
+                            self.errors.append(f"{t.program} -> {path}+{off:#x}: perf_event_open {pfd}")
+                            continue
+                        lfd = self.sys.link_create(st.progs[t.program], pfd)
+                        self.sys.close(pfd)  # the link holds the perf event
+                        if lfd < 0:
+                            self.errors.append(f"{t.program} -> {path}+{off:#x}: link_create {lfd}")
+                            continue
+                        st.links[(t.program, key)] = lfd
+                        made += 1
+            return made
+
+    def detach(self, probe: str) -> None:
+        with self._lock:
+            st = self._probes.pop(probe, None)
+            if st is None:
+                return
+            for fd in list(st.links.values()) + list(st.progs.values()):
+                self.sys.close(fd)
+
+    def links(self, probe: Optional[str] = None) -> int:
+        with self._lock:
+            return sum(len(st.links) for n, st in self._probes.items() if probe is None or n == probe)

@@ -12,6 +12,7 @@
 #include <stdexcept>
 
 #include "mislo_launch.h"
+#include "mislo_packet_kernels.h"
 
 namespace py = pybind11;
 using namespace mislo;
@@ -35,56 +36,6 @@ T* dptr(const torch::Tensor& t) {
 void check_cuda(const torch::Tensor& t, const char* name) {
   if (!t.is_cuda()) throw std::invalid_argument(std::string(name) + " must be a device tensor");
   if (!t.is_contiguous()) throw std::invalid_argument(std::string(name) + " must be contiguous");
-}
-
-constexpr int kPacketHist = kSlots * kBuckets;            // 256
-constexpr int kPacketStatus = kSlots * 3;                 // 48
-constexpr int kPacketMisc = 2 + kSlots;             // unsupported, zero-ts, per-slot value sums (milli)
-constexpr int kPacketDbg = 8;
-constexpr int kPacketConf = kMaxDomains * kMaxDomains;    // 256
-constexpr int kPacketStats = 32 * 32;                     // 1024
-constexpr int kPacketCount = kMaxDomains;                 // 16
-constexpr int kPacketLen = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf + kPacketStats +
-                           kPacketCount;
-
-__global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsigned long long* misc,
-                       const unsigned long long* dbg, const uint32_t* confusion, const double* stats,
-                       const double* count, double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int o = 0;
-  if (i < kPacketHist) { out[i] = hist[i]; return; }
-  o += kPacketHist;
-  if (i < o + kPacketStatus) { out[i] = status[i - o]; return; }
-  o += kPacketStatus;
-  if (i < o + kPacketMisc) { out[i] = (double)misc[i - o]; return; }
-  o += kPacketMisc;
-  if (i < o + kPacketDbg) { out[i] = (double)dbg[i - o]; return; }
-  o += kPacketDbg;
-  if (i < o + kPacketConf) { out[i] = confusion[i - o]; return; }
-  o += kPacketConf;
-  if (i < o + kPacketStats) { out[i] = stats[i - o]; return; }
-  o += kPacketStats;
-  if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
-}
-
-// One launch that zero/poison-fills every per-window accumulator (replaces eleven
-// hipMemsetAsync calls, each ~5 us of fill-kernel + launch overhead on gfx950).
-struct FillSeg {
-  uint32_t* ptr;
-  uint32_t n;      // 32-bit words
-  uint32_t value;
-};
-constexpr int kMaxFill = 12;
-struct FillList {
-  FillSeg seg[kMaxFill];
-  int count;
-};
-
-__global__ __launch_bounds__(256) void k_fill_multi(FillList fl) {
-  for (int q = 0; q < fl.count; ++q) {
-    const FillSeg sg = fl.seg[q];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sg.n; i += gridDim.x * 256) sg.ptr[i] = sg.value;
-  }
 }
 
 }  // namespace
@@ -216,7 +167,7 @@ class Engine {
     };
     add(hist, 0); add(status_cnt, 0); add(misc, 0); add(dbg, 0); add(confusion, 0); add(stats, 0);
     add(stats_count, 0); add(top3, 0xFFFFFFFFu); add(cnt, 0); add(gsum, 0); add(gcnt, 0);
-    hipLaunchKernelGGL(k_fill_multi, dim3(256), dim3(256), 0, cur_stream(), fl);
+    hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, cur_stream(), fl);
   }
 
   SignalCols sig_cols() {
@@ -343,7 +294,7 @@ class Engine {
   void pack() {
     hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, cur_stream(), dptr<uint32_t>(hist),
                        dptr<uint32_t>(status_cnt), dptr<unsigned long long>(misc), dptr<unsigned long long>(dbg),
-                       dptr<uint32_t>(confusion), dptr<double>(stats), dptr<double>(stats_count),
+                       dptr<uint32_t>(confusion), dptr<double>(stats), dptr<double>(stats_count), nullptr,
                        dptr<double>(packet));
   }
 

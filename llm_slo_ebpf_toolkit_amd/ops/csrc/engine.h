@@ -35,21 +35,10 @@
 #include <vector>
 
 #include "mislo_launch.h"
+#include "mislo_packet.h"
 
 namespace mislo {
 
-constexpr int kPacketHist = kSlots * kBuckets;          // 256
-constexpr int kPacketStatus = kSlots * 3;               // 48
-constexpr int kPacketMisc = 2 + kSlots;                 // unsupported, zero-ts, per-slot value sums (milli)
-constexpr int kPacketDbg = 8;
-constexpr int kPacketConf = kMaxDomains * kMaxDomains;  // 256
-constexpr int kPacketStats = 32 * 32;                   // 1024
-constexpr int kPacketCount = kMaxDomains;               // 16
-constexpr int kPacketRing = kRsLen;                     // ring accounting (RingState)
-constexpr int kPacketLen =
-    kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf + kPacketStats + kPacketCount + kPacketRing;
-constexpr int kStatsOff = kPacketHist + kPacketStatus + kPacketMisc + kPacketDbg + kPacketConf;
-constexpr int kStatsLen = kPacketStats + kPacketCount;  // accumulated-statistics vector (f64[1040])
 constexpr uint32_t kCtxRows = 1u << 24;                 // device context table rows (256 MiB)
 constexpr uint32_t kPodRows = 1u << 20;                 // device pod table: pod id -> svc<<16|node
 constexpr uint32_t kTraceIdRows = 1u << 24;             // device trace id -> hash table (128 MiB)

@@ -1,5 +1,6 @@
 // Native per-GPU window engine (engine.h) and its small glue kernels.
 #include "engine.h"
+#include "mislo_packet_kernels.h"
 
 #include <chrono>
 #include <cstdlib>
@@ -25,52 +26,6 @@ namespace {
     if (_r != ncclSuccess) throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(_r) + \
                                                     " at " #x);                                             \
   } while (0)
-
-// One launch that zero/poison-fills every per-window accumulator.
-struct FillSeg {
-  uint32_t* ptr;
-  uint32_t n;  // 32-bit words
-  uint32_t value;
-};
-constexpr int kMaxFill = 14;
-struct FillList {
-  FillSeg seg[kMaxFill];
-  int count;
-};
-
-__global__ __launch_bounds__(256) void k_fill(FillList fl) {
-  for (int q = 0; q < fl.count; ++q) {
-    const FillSeg sg = fl.seg[q];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sg.n; i += gridDim.x * 256) sg.ptr[i] = sg.value;
-  }
-}
-
-// accumulators -> packet (f64), one element per thread
-__global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsigned long long* misc,
-                       const unsigned long long* dbg, const uint32_t* confusion, const double* stats,
-                       const double* count, const uint32_t* ring, double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int o = 0;
-  if (i < kPacketHist) { out[i] = hist[i]; return; }
-  o += kPacketHist;
-  if (i < o + kPacketStatus) { out[i] = status[i - o]; return; }
-  o += kPacketStatus;
-  if (i < o + kPacketMisc) { out[i] = (double)misc[i - o]; return; }
-  o += kPacketMisc;
-  if (i < o + kPacketDbg) { out[i] = (double)dbg[i - o]; return; }
-  o += kPacketDbg;
-  if (i < o + kPacketConf) { out[i] = confusion[i - o]; return; }
-  o += kPacketConf;
-  if (i < o + kPacketStats) { out[i] = stats[i - o]; return; }
-  o += kPacketStats;
-  if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
-  o += kPacketCount;
-  if (i < o + kPacketRing) {
-    const uint32_t v = ring[i - o];
-    out[i] = (i - o == kRsFirstBusy && v == 0xFFFFFFFFu) ? -1.0 : (double)v;  // -1: no busy record
-    return;
-  }
-}
 
 // totals += packet, and the packet stored straight into its pinned host block
 __global__ void k_accumulate(const double* __restrict__ packet, double* __restrict__ totals, int n,

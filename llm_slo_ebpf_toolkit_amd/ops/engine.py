@@ -1,10 +1,16 @@
-"""Python driver of the device-resident window ``Engine`` (ops/csrc/bindings.cpp).
+"""Model images, record-level drivers and debug decoding around the window engine.
 
-``GpuEngine`` owns pinned host staging + device record buffers sized for the window
-capacity, uploads a window's records with async H2D copies on a copy stream, runs the
-whole kernel chain on the compute stream (optionally captured once into a HIP graph and
-replayed), and exposes the outputs. Debug-counter decoding reproduces REF's DebugStats
-from the kernel's pair counts (join.hip header).
+* ``GpuEngine`` -- a window of 64-byte EVENT / SPAN records (pipeline/replay.py, the incident
+  lab) through the SHIPPED engine: the records go into page-locked user-space / span rings and
+  the native ``WindowEngine`` (ops/csrc/engine.h, the agent's executor) DMAs, decodes, joins and
+  scores them exactly as it does the agent's rings;
+* ``KernelHarness`` -- the kernel unit-test harness (ops/csrc/bindings.cpp, a PyTorch extension):
+  the same kernels launched one by one on torch tensors, with their intermediate buffers
+  exposed (REF 40-byte record decode, EVENT16 wire decode, split chains, the refit kernel). It
+  shares the engine's packet layout and packet kernels (mislo_packet.h); the agent, the
+  benchmark and smoke() never use it.
+
+Debug-counter decoding reproduces REF's DebugStats from the kernel's pair counts (join.hip).
 """
 
 from __future__ import annotations
@@ -128,6 +134,56 @@ class WindowOutputs:
 
 
 class GpuEngine:
+    """One window of 64-byte EVENT / SPAN records through the shipped WindowEngine."""
+
+    def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, window_ms: float = 2000.0,
+                 threshold: float = 0.7, fanout: int = 3, group_mode: int = 1):
+        from ..pipeline.window import RingWindowSource, WindowPipeline
+        from ..runtime import load as load_rt
+
+        rt = load_rt()
+        pow2 = lambda n: 1 << max(4, int(np.ceil(np.log2(max(1, n)))))  # noqa: E731
+        self.pipe = WindowPipeline(sig_cap, span_cap, group_cap, device, None, model="bayes", learn=False,
+                                   window_ms=window_ms, threshold=threshold, fanout=fanout, group_mode=group_mode,
+                                   user_cap=sig_cap, n_buffers=2, max_ahead=2)
+        self.user, self.spans = rt.HostRing(pow2(2 * sig_cap), 64), rt.HostRing(pow2(2 * span_cap), 64)
+        self.src = RingWindowSource(self.pipe, None, self.user, self.spans)
+        self.sig_cap, self.span_cap, self.group_cap = sig_cap, span_cap, group_cap
+
+    def set_model(self, model: LinearPosteriorModel) -> None:
+        self.pipe.set_model(model)
+
+    def process(self, events: np.ndarray, spans: np.ndarray, n_groups: int, labels=None,
+                learn: bool = False) -> "WindowOutputs":
+        from ..pipeline.window import Cut
+
+        if events.dtype != records.EVENT or spans.dtype != records.SPAN:
+            raise TypeError("events / spans must be 64-byte EVENT / SPAN records")
+        if len(events) > self.sig_cap or len(spans) > self.span_cap or n_groups > self.group_cap:
+            raise ValueError("window exceeds engine capacity")
+        if len(events) and self.user.push(np.ascontiguousarray(events)) != len(events):
+            raise RuntimeError("event ring full")
+        if len(spans) and self.spans.push(np.ascontiguousarray(spans)) != len(spans):
+            raise RuntimeError("span ring full")
+        k = self.src.stage(Cut(kernel=0, user=self.user.head, spans=self.spans.head), n_groups, labels,
+                           with_labels=labels is not None, learn=learn)["k"]
+        pk = self.pipe.packet(k)
+        r = self.pipe.results(k, n_groups)
+        self.src.reap()
+        return WindowOutputs(
+            hist=pk["hist"].astype(np.int64), status=pk["status"].astype(np.int64),
+            debug=decode_debug(pk["dbg"], pk["misc"], len(spans), len(events)), feat=r["feat"], post=r["post"],
+            pred=r["pred"], conf=r["conf"], evbits=r["evbits"].view(np.uint32),
+            confusion=pk["confusion"].astype(np.int64), value_sum=pk["misc"][2:18].astype(np.float64) * 1e-3)
+
+    def close(self) -> None:
+        self.src.drain()
+        self.pipe.eng.close()
+
+
+class KernelHarness:
+    """Kernel unit-test harness over the PyTorch extension (see the module docstring)."""
+
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, window_ms: float = 2000.0,
                  threshold: float = 0.7, fanout: int = 3, group_mode: int = 1):
         import torch

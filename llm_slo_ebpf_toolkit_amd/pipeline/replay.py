@@ -82,6 +82,10 @@ class ReplayConfig:
     seed: int = 42
     shard: int = 0
     start_ns: int = 1_760_000_000 * 1_000_000_000
+    # windows a drawn fault assignment persists (faults last minutes in REF's incident-lab
+    # phases, test/incident-lab/scenarios/*.yaml): with a halo, a window joins the previous
+    # window's boundary rows, which must carry the same faults
+    fault_hold: int = 1
 
     @property
     def n_pods(self) -> int:
@@ -188,7 +192,9 @@ class ReplayGenerator:
         self.window += 1
         W = cfg.window_ms * 1_000_000
         t0 = cfg.start_ns + w * W
-        faults = self._labels()
+        if w % max(1, cfg.fault_hold) == 0 or getattr(self, "_faults", None) is None:
+            self._faults = self._labels()
+        faults = self._faults
         profiles = [_profile(f) for f in faults]
         G = cfg.n_services
         P = cfg.n_pods

@@ -5,7 +5,8 @@
  *                        (gpu_scheduler:drm_sched_job -> drm_run_job, per fence)
  *   rccl_collective_ms   uprobe/uretprobe on librccl's ncclAllReduce / ncclAllGather /
  *                        ncclReduceScatter (host-side enqueue + completion of blocking
- *                        calls; the loader attaches to the workload's librccl.so)
+ *                        calls; the agent attaches these pinned programs to every librccl
+ *                        the node's processes map, collector/uprobes.py)
  * Records carry the has_gpu flag. */
 #include "mislo_probe.h"
 
@@ -78,15 +79,15 @@ static __always_inline int coll_exit(void)
 	return 0;
 }
 
-SEC("uprobe/ncclAllReduce")
+SEC("uprobe")
 int BPF_KPROBE(allreduce_enter) { return coll_enter(); }
-SEC("uretprobe/ncclAllReduce")
+SEC("uretprobe")
 int BPF_KRETPROBE(allreduce_exit) { return coll_exit(); }
-SEC("uprobe/ncclAllGather")
+SEC("uprobe")
 int BPF_KPROBE(allgather_enter) { return coll_enter(); }
-SEC("uretprobe/ncclAllGather")
+SEC("uretprobe")
 int BPF_KRETPROBE(allgather_exit) { return coll_exit(); }
-SEC("uprobe/ncclReduceScatter")
+SEC("uprobe")
 int BPF_KPROBE(reducescatter_enter) { return coll_enter(); }
-SEC("uretprobe/ncclReduceScatter")
+SEC("uretprobe")
 int BPF_KRETPROBE(reducescatter_exit) { return coll_exit(); }

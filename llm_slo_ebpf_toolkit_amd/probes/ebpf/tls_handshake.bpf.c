@@ -1,5 +1,7 @@
-/* tls_handshake_ms + tls_handshake_fail_total: uprobes on the workload's libssl
- * SSL_do_handshake (path supplied by the loader). Non-blocking handshakes return -1 with
+/* tls_handshake_ms + tls_handshake_fail_total: uprobes on the workloads' libssl
+ * SSL_do_handshake. The sections name no binary: the loader pins these programs and the agent
+ * attaches them to every libssl the node's processes map, resolved through /proc/<pid>/maps
+ * (collector/uprobes.py: ELF symbol offset, perf_event_open + BPF_LINK_CREATE). Non-blocking handshakes return -1 with
  * WANT_READ/WANT_WRITE several times; the handshake time runs from the first call to the
  * call that returns 1, and a final failure (ret <= 0 after which the SSL* is not retried
  * within the window) is counted by the agent from the ret == 0 case reported here. */
@@ -21,7 +23,7 @@ struct {
 	__type(value, __u64); /* SSL* of the call in flight */
 } tls_call SEC(".maps");
 
-SEC("uprobe/SSL_do_handshake")
+SEC("uprobe")
 int BPF_KPROBE(tls_enter, void *ssl)
 {
 	__u64 s = (__u64)ssl, now = bpf_ktime_get_ns(), pt = bpf_get_current_pid_tgid();
@@ -30,7 +32,7 @@ int BPF_KPROBE(tls_enter, void *ssl)
 	return 0;
 }
 
-SEC("uretprobe/SSL_do_handshake")
+SEC("uretprobe")
 int BPF_KRETPROBE(tls_exit, int ret)
 {
 	__u64 pt = bpf_get_current_pid_tgid();

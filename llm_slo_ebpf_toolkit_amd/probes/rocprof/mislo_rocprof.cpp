@@ -8,10 +8,14 @@
 // pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
 //   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue            (ns)
-//   type 14 hbm_pressure_pct     live device allocations / HBM capacity     (milli-pct)
-//   type 15 xgmi_link_latency_us peer GPU copy time beyond its bytes at the
-//                                link's nominal rate (the latency component,
-//                                not a size-dependent duration)             (ns)
+//   type 14 hbm_pressure_pct     the GPU's node-wide HBM use: amdgpu sysfs mem_info_vram_used /
+//                                mem_info_vram_total of the PCI device the process allocates on
+//                                (every process's allocations, not this one's), sampled on
+//                                allocations and every MISLO_HBM_SAMPLE_MS (milli-pct)
+//   type 15 xgmi_link_latency_us peer GPU copy latency, calibrated per (src, dst) GPU pair: a
+//                                small copy (<= 64 KiB) is all latency; a larger one's latency is
+//                                its time beyond its bytes at the best rate that pair has shown
+//                                (its calibrated bandwidth, large copies only)             (ns)
 //   type 16 rccl_collective_ms   RCCL API call duration                      (ns)
 //
 // Timestamps are rocprofiler's monotonic clock, shifted to CLOCK_REALTIME once at init
@@ -27,9 +31,11 @@
 // instead of the coarser pod+pid window.
 //
 // Environment: MISLO_RING (default /mislo-agent-events), MISLO_POD_ID, MISLO_NODE_ID,
-// MISLO_SVC_ID, MISLO_HBM_BYTES (default 288 GiB), MISLO_MAX_EPS (default 200000),
-// MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_XGMI_GBPS (nominal peer-copy rate, default
-// 64 GB/s: one xGMI link direction), MISLO_ROCPROF_VERBOSE.
+// MISLO_SVC_ID, MISLO_HBM_BYTES (fallback capacity when sysfs is unreadable, default 288 GiB),
+// MISLO_PCI_SYSFS (default /sys/bus/pci/devices), MISLO_HBM_SAMPLE_MS (default 1000),
+// MISLO_MAX_EPS (default 200000), MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_XGMI_GBPS (a
+// pair's starting rate before it has shown a large copy, default 64 GB/s: one xGMI link
+// direction), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/buffer_tracing.h>
 #include <rocprofiler-sdk/callback_tracing.h>
@@ -37,11 +43,17 @@
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <fcntl.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <string>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -112,7 +124,27 @@ struct State {
   std::unordered_map<uint64_t, Enq> enqueue_ts;  // correlation id -> enqueue time, request trace
   std::unordered_map<uint64_t, uint64_t> live_alloc;  // address -> bytes
   uint64_t live_bytes = 0;
-  uint64_t last_hbm_milli = ~0ull;
+  // node-wide HBM of the GPUs this process uses: agent handle -> the PCI device's VRAM counters
+  struct Vram {
+    int used_fd = -1, total_fd = -1;
+    uint64_t last_milli = ~0ull;
+  };
+  std::map<uint64_t, Vram> vram;
+  std::string pci_sysfs = "/sys/bus/pci/devices";
+  uint64_t hbm_sample_ms = 1000;
+  uint64_t last_hbm_milli = ~0ull;  // fallback (no sysfs): this process's live allocations
+  // per (src, dst) agent pair: calibrated bandwidth (bytes/ns, best large copy) and the smallest
+  // small-copy latency seen
+  struct Link {
+    double bytes_per_ns = 0.0;
+    uint64_t min_small_ns = ~0ull;
+    uint64_t copies = 0;
+  };
+  std::map<std::pair<uint64_t, uint64_t>, Link> links;
+  std::thread sampler;
+  std::mutex smu;
+  std::condition_variable scv;
+  bool stop = false;
   std::atomic<uint64_t> window_sec{0}, window_count{0}, pushed{0}, dropped{0};
 };
 
@@ -184,13 +216,81 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t 
     g.dropped.fetch_add(1, std::memory_order_relaxed);
 }
 
-void emit_hbm(uint64_t ts) {
-  // value in milli-percent of HBM capacity; emitted when it moves by >= 0.1 pct-point
-  const uint64_t milli = g.hbm_bytes ? (uint64_t)((double)g.live_bytes * 100000.0 / (double)g.hbm_bytes) : 0;
-  if (g.last_hbm_milli != ~0ull && (milli > g.last_hbm_milli ? milli - g.last_hbm_milli : g.last_hbm_milli - milli) < 100)
-    return;
-  g.last_hbm_milli = milli;
+uint64_t read_u64_fd(int fd) {
+  char buf[32];
+  const ssize_t n = pread(fd, buf, sizeof(buf) - 1, 0);
+  if (n <= 0) return 0;
+  buf[n] = 0;
+  return std::strtoull(buf, nullptr, 10);
+}
+
+// HBM pressure of one GPU in milli-percent: node-wide VRAM use from the amdgpu driver (every
+// process on the GPU), or -- without sysfs -- this process's live allocations over the capacity.
+bool hbm_milli(uint64_t agent, uint64_t* out, uint64_t** last) {
+  auto it = g.vram.find(agent);
+  if (it != g.vram.end() && it->second.used_fd >= 0 && it->second.total_fd >= 0) {
+    const uint64_t used = read_u64_fd(it->second.used_fd), total = read_u64_fd(it->second.total_fd);
+    if (total) {
+      *out = (uint64_t)((double)used * 100000.0 / (double)total);
+      *last = &it->second.last_milli;
+      return true;
+    }
+  }
+  *out = g.hbm_bytes ? (uint64_t)((double)g.live_bytes * 100000.0 / (double)g.hbm_bytes) : 0;
+  *last = &g.last_hbm_milli;
+  return true;
+}
+
+// emitted when the GPU's pressure moved by >= 0.1 pct-point since its last record
+void emit_hbm(uint64_t ts, uint64_t agent) {
+  uint64_t milli = 0, *last = nullptr;
+  if (!hbm_milli(agent, &milli, &last)) return;
+  if (*last != ~0ull && (milli > *last ? milli - *last : *last - milli) < 100) return;
+  *last = milli;
   emit(kHbmPressure, ts, milli, 0);
+}
+
+// A peer copy's xGMI latency on its (src, dst) pair, calibrating the pair as it goes.
+uint64_t xgmi_latency(uint64_t src, uint64_t dst, uint64_t bytes, uint64_t dur) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  State::Link& l = g.links[{src, dst}];
+  ++l.copies;
+  if (bytes <= (64u << 10)) {  // small copy: the duration is the link's latency
+    if (dur < l.min_small_ns) l.min_small_ns = dur;
+    return dur;
+  }
+  const double rate = (double)bytes / (double)dur;
+  if (bytes >= (1u << 20) && rate > l.bytes_per_ns) l.bytes_per_ns = rate;  // calibrated bandwidth
+  const double bw = l.bytes_per_ns > 0.0 ? l.bytes_per_ns : g.xgmi_bytes_per_ns;
+  const uint64_t xfer = (uint64_t)((double)bytes / bw);
+  return dur > xfer ? dur - xfer : 0;
+}
+
+void sampler_main() {
+  std::unique_lock<std::mutex> lk(g.smu);
+  while (!g.scv.wait_for(lk, std::chrono::milliseconds(g.hbm_sample_ms), [] { return g.stop; })) {
+    rocprofiler_timestamp_t now = 0;
+    rocprofiler_get_timestamp(&now);
+    for (auto& kv : g.vram)
+      if (kv.second.last_milli != ~0ull) emit_hbm(now, kv.first);  // the GPUs this process has used
+  }
+}
+
+rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents, size_t n, void*) {
+  for (size_t i = 0; i < n; ++i) {
+    const auto* a = static_cast<const rocprofiler_agent_v0_t*>(agents[i]);
+    if (a->type != ROCPROFILER_AGENT_TYPE_GPU) continue;
+    char bdf[32];
+    std::snprintf(bdf, sizeof(bdf), "%04x:%02x:%02x.%x", a->domain & 0xFFFF, (a->location_id >> 8) & 0xFF,
+                  (a->location_id >> 3) & 0x1F, a->location_id & 7);
+    State::Vram v;
+    v.used_fd = open((g.pci_sysfs + "/" + bdf + "/mem_info_vram_used").c_str(), O_RDONLY | O_CLOEXEC);
+    v.total_fd = open((g.pci_sysfs + "/" + bdf + "/mem_info_vram_total").c_str(), O_RDONLY | O_CLOEXEC);
+    if (g.verbose)
+      std::fprintf(stderr, "[mislo-rocprof] GPU %s: vram sysfs %s\n", bdf, v.used_fd >= 0 ? "ok" : "unreadable");
+    g.vram[a->id.handle] = v;
+  }
+  return ROCPROFILER_STATUS_SUCCESS;
 }
 
 // Kernel dispatch ENQUEUE (host side) and COMPLETE (with device start/end timestamps).
@@ -229,15 +329,15 @@ void buffer_callback(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofi
       auto* r = static_cast<rocprofiler_buffer_tracing_memory_copy_record_t*>(h->payload);
       if (r->operation == ROCPROFILER_MEMORY_COPY_DEVICE_TO_DEVICE && r->src_agent_id.handle != r->dst_agent_id.handle &&
           r->end_timestamp > r->start_timestamp) {
-        // latency = duration - bytes / nominal link rate: a healthy link moves a large copy
-        // in ~its transfer time (latency ~ setup cost), a degraded or congested link does not
+        // a healthy link moves a copy in its latency plus its bytes at the pair's calibrated
+        // rate; a degraded or congested link does not
         const uint64_t dur = r->end_timestamp - r->start_timestamp;
-        const uint64_t xfer = (uint64_t)((double)r->bytes / g.xgmi_bytes_per_ns);
-        emit(kXgmiLatency, r->start_timestamp, dur > xfer ? dur - xfer : 0, (uint32_t)r->thread_id);
+        emit(kXgmiLatency, r->start_timestamp, xgmi_latency(r->src_agent_id.handle, r->dst_agent_id.handle, r->bytes, dur),
+             (uint32_t)r->thread_id);
       }
     } else if (h->kind == ROCPROFILER_BUFFER_TRACING_MEMORY_ALLOCATION) {
       auto* r = static_cast<rocprofiler_buffer_tracing_memory_allocation_record_t*>(h->payload);
-      std::lock_guard<std::mutex> lk(g.mu);
+      std::unique_lock<std::mutex> lk(g.mu);
       const uint64_t addr = r->address.handle;
       if (r->operation == ROCPROFILER_MEMORY_ALLOCATION_ALLOCATE ||
           r->operation == ROCPROFILER_MEMORY_ALLOCATION_VMEM_ALLOCATE) {
@@ -251,7 +351,8 @@ void buffer_callback(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofi
           g.live_alloc.erase(it);
         }
       }
-      emit_hbm(r->end_timestamp ? r->end_timestamp : r->start_timestamp);
+      lk.unlock();
+      emit_hbm(r->end_timestamp ? r->end_timestamp : r->start_timestamp, r->agent_id.handle);
     } else if (h->kind == ROCPROFILER_BUFFER_TRACING_RCCL_API) {
       auto* r = static_cast<rocprofiler_buffer_tracing_rccl_api_record_t*>(h->payload);
       if (r->end_timestamp > r->start_timestamp)
@@ -283,6 +384,10 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.queue_floor_ns = env_u64("MISLO_QUEUE_FLOOR_NS", 100000);
   g.xgmi_bytes_per_ns = (double)env_u64("MISLO_XGMI_GBPS", 64);  // GB/s == bytes/ns
   g.verbose = env_u64("MISLO_ROCPROF_VERBOSE", 0) != 0;
+  if (const char* ps = std::getenv("MISLO_PCI_SYSFS")) g.pci_sysfs = ps;
+  g.hbm_sample_ms = env_u64("MISLO_HBM_SAMPLE_MS", 1000);
+  rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, agents_cb, sizeof(rocprofiler_agent_v0_t),
+                                     nullptr);
   timespec rt{};
   clock_gettime(CLOCK_REALTIME, &rt);
   rocprofiler_timestamp_t now = 0;
@@ -314,6 +419,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   CHECK(rocprofiler_context_is_valid(g.ctx, &valid));
   if (!ok || !valid) return -1;
   CHECK(rocprofiler_start_context(g.ctx));
+  if (g.hbm_sample_ms) g.sampler = std::thread(sampler_main);
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] started (ring=%s attached=%d)\n", name ? name : "/mislo-agent-events",
                  g.ring != nullptr);
@@ -321,6 +427,12 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
 }
 
 void tool_fini(void*) {
+  {
+    std::lock_guard<std::mutex> lk(g.smu);
+    g.stop = true;
+  }
+  g.scv.notify_all();
+  if (g.sampler.joinable()) g.sampler.join();
   rocprofiler_flush_buffer(g.buffer);
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] pushed=%llu dropped=%llu\n", (unsigned long long)g.pushed.load(),
@@ -339,6 +451,34 @@ uint64_t mislo_rocprof_dropped() { return g.dropped.load(); }
 
 // The calling thread's current request trace (0 = none): kernels it enqueues from now on carry it.
 void mislo_rocprof_set_trace(uint64_t trace_h) { t_trace = trace_h; }
+
+// Node-wide HBM pressure (milli-pct) of the GPU agent with the given index among the GPUs
+// (-1 if its sysfs counters are unreadable), for tests and the agent's checks.
+int64_t mislo_rocprof_hbm_milli(int gpu_index) {
+  int i = 0;
+  for (auto& kv : g.vram) {
+    if (i++ != gpu_index) continue;
+    if (kv.second.used_fd < 0 || kv.second.total_fd < 0) return -1;
+    const uint64_t total = read_u64_fd(kv.second.total_fd);
+    return total ? (int64_t)((double)read_u64_fd(kv.second.used_fd) * 100000.0 / (double)total) : -1;
+  }
+  return -1;
+}
+
+// A GPU pair's calibration (xGMI): copies seen, calibrated bytes/ns (0 = no large copy yet) and
+// the smallest small-copy latency (ns; ~0 = none). Returns the number of calibrated pairs.
+int mislo_rocprof_links(int i, uint64_t* copies, double* bytes_per_ns, uint64_t* min_small_ns) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  int j = 0;
+  for (auto& kv : g.links) {
+    if (j++ == i) {
+      *copies = kv.second.copies;
+      *bytes_per_ns = kv.second.bytes_per_ns;
+      *min_small_ns = kv.second.min_small_ns;
+    }
+  }
+  return (int)g.links.size();
+}
 
 rocprofiler_tool_configure_result_t* rocprofiler_configure(uint32_t, const char*, uint32_t,
                                                            rocprofiler_client_id_t* id) {

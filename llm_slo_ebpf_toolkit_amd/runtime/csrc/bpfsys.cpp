@@ -2,6 +2,7 @@
 
 #include <errno.h>
 #include <linux/bpf.h>
+#include <linux/perf_event.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -93,6 +94,30 @@ int bpf_map_lookup_batch(int fd, void* in_batch, void* out_batch, void* keys, vo
   *count = a.batch.count;
   return r;
 }
+
+int perf_uprobe_open(const UprobeAttr& u) {
+  struct perf_event_attr attr;
+  std::memset(&attr, 0, sizeof(attr));
+  attr.size = sizeof(attr);
+  attr.type = u.pmu_type;
+  attr.config = u.retprobe ? (1ull << u.retprobe_bit) : 0ull;
+  attr.config1 = ptr(u.path.c_str());  // uprobe_path
+  attr.config2 = u.offset;             // probe_offset
+  // a system-wide uprobe is opened on one CPU: it fires for the binary on every CPU
+  const long fd = syscall(__NR_perf_event_open, &attr, u.pid, u.pid == -1 ? 0 : -1, -1, PERF_FLAG_FD_CLOEXEC);
+  return fd < 0 ? -errno : (int)fd;
+}
+
+int bpf_link_create_perf(int prog_fd, int perf_fd) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.link_create.prog_fd = (uint32_t)prog_fd;
+  a.link_create.target_fd = (uint32_t)perf_fd;
+  a.link_create.attach_type = BPF_PERF_EVENT;
+  return sys_bpf(BPF_LINK_CREATE, &a);
+}
+
+int close_fd(int fd) { return close(fd) < 0 ? -errno : 0; }
 
 bool bpf_syscall_available() {
   // BPF_PROG_LOAD-free probe: an invalid OBJ_GET answers -EPERM without privilege and

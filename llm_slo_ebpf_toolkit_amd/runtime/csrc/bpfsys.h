@@ -28,4 +28,21 @@ int bpf_map_next_key(int fd, const void* key, void* next);
 int bpf_map_lookup_batch(int fd, void* in_batch, void* out_batch, void* keys, void* values, uint32_t* count);
 bool bpf_syscall_available();  // probe: is bpf(2) permitted at all (root / CAP_BPF)
 
+// Uprobe attachment without libbpf (the probes' uprobe programs are pinned by the loader; the
+// agent attaches them to the binaries it resolves per process, collector/uprobes.py):
+//   perf_event_open(PERF_TYPE = the uprobe PMU's dynamic type, config = retprobe bit,
+//   config1 = binary path, config2 = file offset of the function, pid = -1, cpu = 0) -> fd,
+//   then BPF_LINK_CREATE(prog fd, perf fd, BPF_PERF_EVENT) -> link fd (closing it detaches).
+struct UprobeAttr {
+  uint32_t pmu_type;      // /sys/bus/event_source/devices/uprobe/type
+  uint32_t retprobe_bit;  // /sys/bus/event_source/devices/uprobe/format/retprobe ("config:N")
+  bool retprobe;
+  std::string path;       // the binary, as the agent sees it (/proc/<pid>/root/...)
+  uint64_t offset;        // file offset of the probed instruction
+  int pid;                // -1: every process mapping the binary
+};
+int perf_uprobe_open(const UprobeAttr& a);
+int bpf_link_create_perf(int prog_fd, int perf_fd);
+int close_fd(int fd);
+
 }  // namespace mislo

@@ -616,6 +616,17 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def("items", &PyBpfMap::items)
       .def("info", &PyBpfMap::info);
   m.def("bpf_available", &bpf_syscall_available);
+  m.def(
+      "perf_uprobe_open",
+      [](uint32_t pmu_type, uint32_t retprobe_bit, bool retprobe, const std::string& path, uint64_t offset, int pid) {
+        return perf_uprobe_open(UprobeAttr{pmu_type, retprobe_bit, retprobe, path, offset, pid});
+      },
+      py::arg("pmu_type"), py::arg("retprobe_bit"), py::arg("retprobe"), py::arg("path"), py::arg("offset"),
+      py::arg("pid") = -1, "perf_event_open of a uprobe; an fd or -errno");
+  m.def("bpf_link_create_perf", &bpf_link_create_perf, py::arg("prog_fd"), py::arg("perf_fd"),
+        "BPF_LINK_CREATE(prog, perf event); a link fd or -errno");
+  m.def("bpf_obj_get", &bpf_obj_get, py::arg("path"), "BPF_OBJ_GET of a pinned object; an fd or -errno");
+  m.def("close_fd", &close_fd);
   m.attr("REC_STRIDE") = kRecStride;
   m.attr("DEF_TRACE") = kDefTrace;
   m.attr("DEF_CTX") = kDefCtx;

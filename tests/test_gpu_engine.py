@@ -21,9 +21,9 @@ def small_window(seed=1, n=4096, s=256, services=8, scenario="full"):
 
 @pytest.fixture(scope="module")
 def engine():
-    from llm_slo_ebpf_toolkit_amd.ops.engine import GpuEngine
+    from llm_slo_ebpf_toolkit_amd.ops.engine import KernelHarness
 
-    return GpuEngine(sig_cap=8192, span_cap=512, group_cap=64)
+    return KernelHarness(sig_cap=8192, span_cap=512, group_cap=64)
 
 
 def test_extension_is_native(engine):
@@ -245,3 +245,27 @@ def test_device_refit_matches_host_learned_model(engine):
     assert dev["table_mask"] == ref["table_mask"] and dev["mode"] == 0
 
 
+
+
+def test_record_window_through_the_shipped_engine():
+    """ops.engine.GpuEngine: a window of 64-byte EVENT / SPAN records through the agent's
+    WindowEngine (page-locked rings -> DMA -> decode -> LDS join -> MFMA posterior) matches the
+    oracle on the same records (connections folded to conn32 as the native engine does)."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.ops.engine import GpuEngine
+
+    w = small_window(seed=9)
+    eng = GpuEngine(8192, 512, 8)
+    model = NaiveBayes.ref()
+    eng.set_model(model)
+    for _ in range(2):  # the rings and buffers are reused window after window
+        out = eng.process(w.events, w.spans, w.n_groups, w.group_labels)
+        d = oracle.decode_events(w.events)
+        d.conn = records.conn32_np(d.conn).astype(np.uint64)
+        ref = oracle.join(d, oracle.spans_native(w.spans), w.n_groups)
+        np.testing.assert_array_equal(out.feat, ref.feat)
+        np.testing.assert_array_equal(out.hist, oracle.histograms(d))
+        assert out.debug["candidates"] == ref.debug["candidates"]
+        np.testing.assert_array_equal(out.pred, np.argmax(model.logits(ref.feat.astype(np.float64)), axis=1))
+        assert out.confusion.sum() == w.n_groups
+    eng.close()

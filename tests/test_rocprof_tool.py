@@ -171,3 +171,58 @@ def test_xgmi_peer_copies():
     assert len(x) >= 1
     # a 64 MiB copy takes ~1 ms at 64 GB/s: what remains is far below the copy duration
     assert (x["value"] < 1_000_000).all(), x["value"]
+
+
+HBM_WORKLOAD = r"""
+import ctypes, time, torch
+keep = [torch.empty(1 << 30, dtype=torch.uint8, device="cuda") for _ in range(8)]  # 8 GiB live
+torch.cuda.synchronize()
+time.sleep(1.5)  # the tool's sampler re-reads the GPU's VRAM counters every 1 s
+tool = [ln.split()[-1] for ln in open("/proc/self/maps") if "libmislo_rocprof" in ln][0]
+lib = ctypes.CDLL(tool)
+lib.mislo_rocprof_hbm_milli.restype = ctypes.c_int64
+print("tool_hbm_milli", lib.mislo_rocprof_hbm_milli(0), flush=True)
+"""
+
+
+def _vram_sysfs(dev=0):
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    for fn in range(8):
+        d = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.{fn}"
+        if os.path.exists(os.path.join(d, "mem_info_vram_used")):
+            return d
+    return None
+
+
+@pytest.mark.gpu
+def test_hbm_pressure_is_the_gpus_node_wide_vram_use():
+    """hbm_pressure_pct is the GPU's node-wide HBM use (amdgpu mem_info_vram_used / _total, every
+    process on the GPU), not the workload's own allocations over 288 GiB: the tool's reading and
+    its last record agree with the driver's counters read by this test."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    sysfs = _vram_sysfs(0)
+    if sysfs is None:
+        pytest.skip("amdgpu VRAM counters not exposed in this container's sysfs")
+    rt = load()
+    name = f"/mislo-test-{os.getpid()}-hbm"
+    ring = rt.HostRing(1 << 14, 32, name)
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000000",
+               MISLO_ROCPROF_VERBOSE="1")
+    r = subprocess.run([sys.executable, "-c", HBM_WORKLOAD], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    read = lambda f: int(open(os.path.join(sysfs, f)).read())  # noqa: E731
+    node_milli = read("mem_info_vram_used") * 100000 // read("mem_info_vram_total")  # after the workload exit
+    tool = int([ln for ln in r.stdout.splitlines() if ln.startswith("tool_hbm_milli")][0].split()[1])
+    assert tool > 0, r.stderr[-2000:]
+    own = 8 * 100000 // 288  # the workload's 8 GiB over 288 GiB: what round 2 reported
+    recs = np.concatenate([np.frombuffer(ring.records_view()[i * 32:(i + c) * 32].tobytes(), dtype=records.USER32)
+                           for _, i, c in ring.peek(1 << 14)])
+    hbm = recs[recs["signal_type"] == 14]["value_milli"].astype(np.int64)
+    assert len(hbm), r.stderr[-1000:]
+    # the tool read the driver's node-wide counter while 8 GiB were live: at least the workload's
+    # share, and within 2 pct-points of the last record it emitted
+    assert tool >= own - 200 and abs(int(hbm[-1]) - tool) <= 2000, (tool, hbm[-5:].tolist(), own, node_milli)
