@@ -174,6 +174,9 @@ class AgentOptions:
     gpus: int = 1                        # window workers (one per GPU); 0 = every GPU visible to the agent
     model_path: str = ""                 # trained model file (attributor --train); overrides --model
     otlp_receiver_allow: str = ""        # CIDRs allowed to export spans to the receiver ("" = any)
+    procfs_sampler: bool = False         # runqueue_delay_ms from /proc schedstat (no BPF needed)
+    procfs_pods: str = ""                # pid:pod-uid,... to watch ("" = the node's kubepods cgroups)
+    procfs_interval_ms: int = 100
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -242,7 +245,9 @@ class Agent:
     # ---- lifecycle ------------------------------------------------------------------------
     def start_server(self) -> Optional[MetricsServer]:
         if self.o.metrics_bind:
-            self.server = MetricsServer(self.metrics.registry, self.o.metrics_bind, ready=lambda: self.ready).start()
+            pods = lambda: {n: i for i, n in enumerate(self.pod_ids.names()) if n}  # noqa: E731
+            self.server = MetricsServer(self.metrics.registry, self.o.metrics_bind, ready=lambda: self.ready,
+                                        debug={"pods": pods}).start()
         return self.server
 
     def close(self) -> None:
@@ -636,6 +641,24 @@ class Agent:
             mapper = SpanMapper(groups, self.pod_ids.id, node_id)
             receiver = OtlpSpanReceiver(o.otlp_receiver_bind, mapper, spans.push, allow=o.otlp_receiver_allow).start()
             self.receiver = receiver
+        sampler = None
+        if o.procfs_sampler:
+            from ..collector import procfs
+
+            static = procfs.parse_pod_list(o.procfs_pods)
+            cache = {"t": 0.0, "m": {}}
+
+            def targets():
+                if static:
+                    return {pid: self.pod_ids.id(uid) for pid, uid in static.items()}
+                if time.monotonic() - cache["t"] > 10.0:  # pod churn: re-walk the cgroups every 10 s
+                    cache["m"] = {pid: self.pod_ids.id(uid) for pid, uid in procfs.pod_processes().items()}
+                    cache["t"] = time.monotonic()
+                return cache["m"]
+
+            sampler = procfs.SchedstatSampler(targets, user.push, rec=int(user.rec_size), node_id=node_id)
+            sampler.start(o.procfs_interval_ms / 1000.0)
+            self.procfs = sampler
         if self.guard is not None:
             self.guard.source = TreeCPUSampler(lambda: [os.getpid()] + pool.pids())
             self.guard.evaluate()
@@ -683,6 +706,8 @@ class Agent:
             # workers unregister the rings from their GPUs and free device memory while the
             # ring mappings still exist (interpreter teardown order is arbitrary)
             pool.close()
+            if sampler is not None:
+                sampler.stop()
             if receiver is not None:
                 receiver.stop()
             if getattr(self, "probe_manager", None) is not None:

@@ -64,6 +64,10 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                      "overrides --model"),
         ("otlp-receiver-allow", d.otlp_receiver_allow, "comma-separated CIDRs allowed to export spans to the "
                                                        "receiver (empty = any)"),
+        ("procfs-sampler", False, "window engine: runqueue_delay_ms of pod processes from /proc schedstat "
+                                  "(unprivileged; min-capability mode)"),
+        ("procfs-pods", d.procfs_pods, "pid:pod-uid,... for the procfs sampler (empty: the kubepods cgroups)"),
+        ("procfs-interval-ms", d.procfs_interval_ms, "procfs sampler interval"),
         ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
         ("pin-dir", d.pin_dir, "bpffs directory the probe loader pinned the maps in (--source bpf)"),
         ("probe-objs", d.probe_objs, "--source bpf: directory of compiled probes (*.bpf.o) the agent loads and "
@@ -105,7 +109,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
         otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
         checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), model_path=a.model_path,
-        otlp_receiver_allow=a.otlp_receiver_allow)
+        otlp_receiver_allow=a.otlp_receiver_allow, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
+        procfs_interval_ms=int(a.procfs_interval_ms))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])
         if given:  # an operator's flag wins over a node-wide GPU_MAX_HW_QUEUES

@@ -159,7 +159,7 @@ def discover_pods(cgroup_root: str = "/sys/fs/cgroup", interner=None) -> Dict[in
 
 def _pod_uid(name: str) -> str:
     """kubepods-burstable-pod<uid with _>.slice | pod<uid> -> uid (REF metadata.go:95-118)."""
-    i = name.find("pod")
+    i = name.rfind("pod")  # the last one: "kubepods-...-pod<uid>" holds two
     if i < 0:
         return ""
     s = name[i + 3:]

@@ -239,11 +239,15 @@ class GroupTable:
 
 
 def _ipv4(v) -> int:
+    """An IPv4 address as the probes hold it: the 4 network-order bytes the kernel stores
+    (skc_daddr, the tcp tracepoint's daddr) read as a little-endian u32 -- REF's ipFromU32
+    formats that value byte-wise (pkg/collector/ringbuf.go:240-243) -- so a span's connection
+    hashes like the kernel records of the same connection."""
     try:
         a = ipaddress.ip_address(str(v))
     except ValueError:
         return 0
-    return int(a) if a.version == 4 else 0
+    return struct.unpack("<I", a.packed)[0] if a.version == 4 else 0
 
 
 def _first(attrs: Dict[str, object], keys) -> object:

@@ -1,0 +1,150 @@
+"""Unprivileged kernel signals from /proc: the agent's own producer where BPF is not allowed.
+
+REF's min-capability mode keeps two signals (dns, tcp) and drops the scheduler ones with the BPF
+programs (/root/reference/docs/security/agent-min-capability-mode.md:1-35). The scheduler already
+accounts what ``runqueue_delay.bpf.c`` measures: ``/proc/<pid>/task/<tid>/schedstat`` holds each
+thread's on-CPU time, run-queue wait time and timeslice count, readable without privilege. The
+``SchedstatSampler`` turns their per-interval deltas into ``runqueue_delay_ms`` records -- the mean
+wait per timeslice of every thread that ran (the probe's per-switch delay averaged over the
+interval), above the probe's 100 us floor -- tagged with the process's pid and pod, and pushes
+them into the agent's user-space ring like the rocprofiler tool's records. The GPU window engine
+joins them to the pod's spans (pod + pid tier).
+
+Watched processes: a static ``pid -> pod uid`` list (``agent --procfs-pods``), or every process in
+the node's kubepods cgroups (``pod_processes``).
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Callable, Dict, Iterable, Optional, Tuple
+
+import numpy as np
+
+from . import records
+
+RUNQUEUE_TYPE = 3          # catalogue kernel type of runqueue_delay_ms (ns in the record)
+FLOOR_NS = 100_000         # runqueue_delay.bpf.c's emit floor
+
+
+def read_schedstat(path: str) -> Optional[Tuple[int, int, int]]:
+    try:
+        with open(path) as fh:
+            f = fh.read().split()
+        return int(f[0]), int(f[1]), int(f[2])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+class SchedstatSampler:
+    def __init__(self, targets: Callable[[], Dict[int, int]], push: Callable[[np.ndarray], int], rec: int = 24,
+                 proc_root: str = "/proc", floor_ns: int = FLOOR_NS, node_id: int = 0):
+        """``targets()`` -> {pid: pod id}; ``push(records)`` -> records accepted (the user ring)."""
+        self.targets, self.push, self.rec = targets, push, int(rec)
+        self.proc_root, self.floor_ns, self.node_id = proc_root, int(floor_ns), int(node_id)
+        self._prev: Dict[Tuple[int, int], Tuple[int, int]] = {}
+        self.samples = self.emitted = self.dropped = 0
+        self._stop = threading.Event()
+        self._thr: Optional[threading.Thread] = None
+
+    def sample(self, now_ns: Optional[int] = None) -> np.ndarray:
+        """One interval: EVENT records of the threads whose mean wait per timeslice crossed the floor."""
+        now = int(now_ns if now_ns is not None else time.time_ns())
+        rows, seen = [], set()
+        for pid, pod in self.targets().items():
+            task = os.path.join(self.proc_root, str(pid), "task")
+            try:
+                tids = [int(t) for t in os.listdir(task) if t.isdigit()]
+            except OSError:
+                continue
+            for tid in tids:
+                st = read_schedstat(os.path.join(task, str(tid), "schedstat"))
+                if st is None:
+                    continue
+                key = (pid, tid)
+                seen.add(key)
+                prev = self._prev.get(key)
+                self._prev[key] = (st[1], st[2])
+                if prev is None:
+                    continue
+                dw, ds = st[1] - prev[0], st[2] - prev[1]
+                if ds > 0 and dw > 0 and dw // ds >= self.floor_ns:
+                    rows.append((pid, tid, pod, dw // ds))
+        for key in list(self._prev):
+            if key not in seen:
+                del self._prev[key]
+        self.samples += 1
+        ev = np.zeros(len(rows), dtype=records.EVENT)
+        if rows:
+            a = np.array(rows, dtype=np.int64)
+            ev["ts_ns"] = now
+            ev["signal_type"] = RUNQUEUE_TYPE
+            ev["value"] = a[:, 3].astype(np.uint64)
+            ev["pid"] = a[:, 0].astype(np.uint32)
+            ev["tid"] = a[:, 1].astype(np.uint32)
+            ev["pod_id"] = a[:, 2].astype(np.uint32)
+            ev["node_id"] = self.node_id
+        return ev
+
+    def tick(self, now_ns: Optional[int] = None) -> int:
+        ev = self.sample(now_ns)
+        if not len(ev):
+            return 0
+        n = int(self.push(records.to_user(ev, self.rec)))
+        self.emitted += n
+        self.dropped += len(ev) - n
+        return n
+
+    def start(self, interval_s: float = 0.1) -> "SchedstatSampler":
+        def run():
+            while not self._stop.wait(interval_s):
+                try:
+                    self.tick()
+                except Exception:  # noqa: BLE001 - a sampler hiccup must not stop the agent
+                    self.dropped += 1
+
+        self._thr = threading.Thread(target=run, name="procfs-sampler", daemon=True)
+        self._thr.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thr is not None:
+            self._thr.join(5)
+
+
+def parse_pod_list(spec: str) -> Dict[int, str]:
+    """'pid:uid,pid:uid' -> {pid: uid}."""
+    out: Dict[int, str] = {}
+    for item in (spec or "").split(","):
+        if ":" in item:
+            pid, uid = item.split(":", 1)
+            out[int(pid)] = uid.strip()
+    return out
+
+
+def pod_processes(cgroup_root: str = "/sys/fs/cgroup") -> Dict[int, str]:
+    """{pid: pod uid} of every process in the node's kubepods cgroups."""
+    from .bpf import _pod_uid
+
+    out: Dict[int, str] = {}
+    for dirpath, _dirs, files in os.walk(cgroup_root):
+        if "cgroup.procs" not in files or "pod" not in dirpath:
+            continue
+        uid = ""
+        for part in reversed(dirpath.split(os.sep)):
+            uid = _pod_uid(part)
+            if uid:
+                break
+        if not uid:
+            continue
+        try:
+            with open(os.path.join(dirpath, "cgroup.procs")) as fh:
+                for ln in fh:
+                    if ln.strip().isdigit():
+                        out[int(ln)] = uid
+        except OSError:
+            continue
+    return out

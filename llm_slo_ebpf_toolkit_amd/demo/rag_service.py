@@ -33,7 +33,7 @@ import threading
 import time
 import urllib.request
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 from ..contracts import semconv
 from ..correlation.correlator import Correlator
@@ -254,10 +254,54 @@ class BurnRate:
         return (errs / n) / (1.0 - self.objective) if n else 0.0
 
 
+class VectorDBClient:
+    """Keep-alive HTTP client of the vector-DB stub (demo/vectordb.py), one TCP connection per
+    worker thread: a request's span carries its connection's tuple, so TCP-level kernel signals
+    of that connection join the request (pod + connection tier)."""
+
+    def __init__(self, url: str, timeout_s: float = 10.0):
+        from urllib.parse import urlparse
+
+        u = urlparse(url)
+        self.host, self.port, self.timeout = u.hostname or "127.0.0.1", int(u.port or 80), timeout_s
+        self._tls = threading.local()
+
+    def _conn(self):
+        import http.client
+
+        c = getattr(self._tls, "conn", None)
+        if c is None:
+            c = http.client.HTTPConnection(self.host, self.port, timeout=self.timeout)
+            c.connect()
+            self._tls.conn = c
+        return c
+
+    def search(self, query: str, k: int) -> Tuple[List[str], Dict[str, object]]:
+        """(titles, connection attributes: client.port / server.port / server.address)."""
+        for attempt in (0, 1):
+            c = self._conn()
+            try:
+                body = json.dumps({"query": query, "k": k}).encode()
+                c.request("POST", "/search", body=body, headers={"Content-Type": "application/json"})
+                out = json.loads(c.getresponse().read())
+                lip, lport = c.sock.getsockname()[:2]
+                rip, rport = c.sock.getpeername()[:2]
+                return [h["title"] for h in out["hits"]], {"client.port": int(lport), "server.port": int(rport),
+                                                           "server.address": rip}
+            except (OSError, ValueError):
+                c.close()
+                self._tls.conn = None
+                if attempt:
+                    raise
+        return [], {}
+
+
 class RagService:
     def __init__(self, backend, corpus_path: str = os.path.join(HERE, "fixtures", "corpus.json"),
-                 otlp_endpoint: str = "", node: str = "demo-node", pod: str = "demo-rag-service", resource=None):
+                 otlp_endpoint: str = "", node: str = "demo-node", pod: str = "demo-rag-service", resource=None,
+                 vectordb_url: str = ""):
         self.backend = backend
+        self.vdb = VectorDBClient(vectordb_url) if vectordb_url else None
         with open(corpus_path) as fh:
             self.docs = json.load(fh)
         self.corr = Correlator()
@@ -299,8 +343,17 @@ class RagService:
         rnd = random.Random(seed + prompt_hash(prompt))
         docs = sorted(d["title"] for d in rnd.sample(self.docs, min(plan.docs, len(self.docs))))
         t_r0 = time.time_ns()
-        for wait in (plan.dns_ms, plan.network_ms, plan.vectordb_ms):
-            time.sleep(wait / 1000.0)
+        conn_attrs: Dict[str, object] = {}
+        if self.vdb is not None:  # a real vector-DB hop; DNS and network stay the plan's
+            for wait in (plan.dns_ms, plan.network_ms):
+                time.sleep(wait / 1000.0)
+            t_v = time.time_ns()
+            docs, conn_attrs = self.vdb.search(prompt, plan.docs)
+            vdb_ms = (time.time_ns() - t_v) / MS
+        else:
+            for wait in (plan.dns_ms, plan.network_ms, plan.vectordb_ms):
+                time.sleep(wait / 1000.0)
+            vdb_ms = plan.vectordb_ms
         t_r1 = time.time_ns()
         span = SpanRef(trace_id=trace_id, service="rag-service", node=self.node, pod=self.pod, pid=os.getpid(),
                        timestamp=t_req)
@@ -332,7 +385,7 @@ class RagService:
         tps = (g["tokens"] - 1) / dec_s if g["tokens"] > 1 else float(g["tokens"])
         self.m_ttft.observe(ttft_ms)
         self.m_tps.observe(tps)
-        self.m_vdb.observe(plan.vectordb_ms)
+        self.m_vdb.observe(vdb_ms)
         self.m_net.observe(plan.network_ms)
         self.m_dns.observe(plan.dns_ms)
         self.m_req.inc(1, "ok", profile)
@@ -340,12 +393,13 @@ class RagService:
         root_attrs = {"request.id": rid, "llm.profile": profile, "llm.seed": seed, "llm.backend": self.backend.name,
                       semconv.ATTR_SLO_TTFT_MS: ttft_ms, semconv.ATTR_SLO_TOKENS_PER_SEC: tps}
         root_attrs.update({k: float(v) for k, v in (attrs or {}).items()})
+        root_attrs.update(conn_attrs)
         if decision.tier:
             root_attrs["llm.ebpf.correlation_tier"] = decision.tier
         self.spans.add([
             SpanExporter.span(trace_id, root, "", "chat.request", t_req, t_end, root_attrs),
             SpanExporter.span(trace_id, rsp, root, "chat.retrieval", t_r0, t_r1, {
-                semconv.ATTR_RETRIEVAL_VECTORDB: float(plan.vectordb_ms),
+                semconv.ATTR_RETRIEVAL_VECTORDB: float(vdb_ms),
                 semconv.ATTR_RETRIEVAL_NETWORK_MS: float(plan.network_ms),
                 semconv.ATTR_RETRIEVAL_DNS_MS: float(plan.dns_ms), "retrieval.selected_docs": len(docs)}),
             SpanExporter.span(trace_id, gsp, root, "chat.generation", t_r1, t_end, {"llm.tokens.count": g["tokens"]}),
@@ -435,9 +489,11 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default=os.environ.get("LLM_BACKEND", "stub"), choices=("stub", "llama"))
     ap.add_argument("--llama-preset", default="1b")
     ap.add_argument("--otlp-endpoint", default=os.environ.get("OTEL_EXPORTER_OTLP_TRACES_ENDPOINT", ""))
+    ap.add_argument("--vectordb-url", default=os.environ.get("VECTORDB_URL", ""),
+                    help="vector-DB stub (demo/vectordb.py) to search over a keep-alive connection")
     a = ap.parse_args(argv)
     backend = LlamaBackend(a.llama_preset) if a.backend == "llama" else StubBackend()
-    svc = RagService(backend, otlp_endpoint=a.otlp_endpoint)
+    svc = RagService(backend, otlp_endpoint=a.otlp_endpoint, vectordb_url=a.vectordb_url)
     httpd, _ = svc.serve(a.bind, a.metrics_bind)
     print(f"rag-service listening on {a.bind} (backend={backend.name})", flush=True)
     try:

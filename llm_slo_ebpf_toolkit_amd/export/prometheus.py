@@ -197,12 +197,17 @@ def parse_exposition(text: str) -> Dict[str, float]:
 class MetricsServer:
     """/metrics, /healthz ("ok"), /readyz ("ready") -- REF cmd/agent/main.go:304-326."""
 
-    def __init__(self, registry: Registry, bind: str = ":2112", ready=lambda: True):
+    def __init__(self, registry: Registry, bind: str = ":2112", ready=lambda: True, debug=None):
+        """``debug``: name -> callable returning a JSON-able object, served as /debug/<name>
+        (the agent's pod-uid -> pod-id table, for fault injectors and operators)."""
+        import json
+
         host, _, port = bind.rpartition(":")
         self.registry = registry
         self.ready = ready
         reg = registry
         is_ready = ready
+        routes = dict(debug or {})
 
         class H(BaseHTTPRequestHandler):
             def log_message(self, *a):  # quiet
@@ -218,6 +223,9 @@ class MetricsServer:
                 elif self.path.startswith("/readyz"):
                     ok = is_ready()
                     body, ctype, code = (b"ready", "text/plain", 200) if ok else (b"not ready", "text/plain", 503)
+                elif self.path.startswith("/debug/") and self.path[7:].split("?")[0] in routes:
+                    body = json.dumps(routes[self.path[7:].split("?")[0]]()).encode()
+                    ctype, code = "application/json", 200
                 else:
                     body, ctype, code = b"not found", "text/plain", 404
                 self.send_response(code)

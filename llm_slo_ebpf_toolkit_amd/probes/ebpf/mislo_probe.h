@@ -110,14 +110,14 @@ static __always_inline int mislo_below_floor(__u16 type, __u64 value)
 	return type < 120 && value < mislo_cfg_get(MISLO_CFG_FLOOR(type));
 }
 
-/* The probe's working record (per-CPU scratch, not ring memory): fill, then mislo_submit(). */
-static __always_inline struct mislo_event *mislo_reserve(__u16 type, __u64 value, __u32 tgid, __u32 tid)
+/* The probe's working record (per-CPU scratch, not ring memory) of a task or socket in cgroup
+ * ``cg``: fill, then mislo_submit(). */
+static __always_inline struct mislo_event *mislo_reserve_cg(__u16 type, __u64 value, __u32 tgid, __u32 tid, __u64 cg)
 {
 	__u32 zero = 0;
 	struct mislo_event *e = bpf_map_lookup_elem(&mislo_scratch, &zero);
 	if (!e)
 		return 0;
-	__u64 cg = bpf_get_current_cgroup_id();
 	__u32 *pod = bpf_map_lookup_elem(&mislo_pods, &cg);
 	e->ts_ns = (__s64)(bpf_ktime_get_ns() + mislo_cfg_get(MISLO_CFG_CLOCK));
 	e->value = value;
@@ -135,6 +135,12 @@ static __always_inline struct mislo_event *mislo_reserve(__u16 type, __u64 value
 	e->err = 0;
 	e->conn_h = 0;
 	return e;
+}
+
+/* ... attributed to the current task's cgroup */
+static __always_inline struct mislo_event *mislo_reserve(__u16 type, __u64 value, __u32 tgid, __u32 tid)
+{
+	return mislo_reserve_cg(type, value, tgid, tid, bpf_get_current_cgroup_id());
 }
 
 /* records.py conn_hash_np: splitmix64 of (src port, dst port, dst ip); 0 = no connection */

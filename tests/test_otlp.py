@@ -99,7 +99,9 @@ def _check(recs, pods):
     assert abs(r["ttft_ms"] - 812.5) < 1e-4 and np.isnan(recs[1]["ttft_ms"])
     assert r["pid"] == 4242 and r["pod_id"] == pods.id(RES["k8s.pod.uid"]) == 1
     assert r["group_id"] == 0 and r["svc_id"] == 1 and r["node_id"] == 3
-    assert r["conn_h"] == records.conn_hash(51000, 443, 0x0A000007)
+    # the address as the probes hold it (network-order bytes read little-endian, REF ipFromU32)
+    assert records.ipv4_from_u32(0x0700000A) == "10.0.0.7"
+    assert r["conn_h"] == records.conn_hash(51000, 443, 0x0700000A)
     assert r["span_h"] == 0x00F067AA0BA902B7
     assert recs[1]["conn_h"] == 0
 

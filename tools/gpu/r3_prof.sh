@@ -13,4 +13,9 @@ bash tools/gpu_steps.sh \
   "150|r3_pmc1|$P SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES -d gpurun_out/r3_pmc1 -- $B" \
   "150|r3_pmc2|$P SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d gpurun_out/r3_pmc2 -- $B" \
   "150|r3_pmc3|$P FETCH_SIZE -d gpurun_out/r3_pmc3 -- $B" \
-  "150|r3_pmc4|$P WRITE_SIZE TCC_HIT_sum TCC_MISS_sum -d gpurun_out/r3_pmc4 -- $B"
+  "150|r3_pmc4|$P WRITE_SIZE TCC_HIT_sum TCC_MISS_sum -d gpurun_out/r3_pmc4 -- $B" \
+"120|rss_q1|GPU_MAX_HW_QUEUES=1 python tools/rss_probe.py" \
+  "120|rss_q1_devq|GPU_MAX_HW_QUEUES=1 HSA_ALLOCATE_QUEUE_DEV_MEM=1 python tools/rss_probe.py" \
+  "120|rss_q1_nosdma|GPU_MAX_HW_QUEUES=1 HSA_ENABLE_SDMA=0 python tools/rss_probe.py" \
+  "120|rss_q1_devq_nosdma|GPU_MAX_HW_QUEUES=1 HSA_ALLOCATE_QUEUE_DEV_MEM=1 HSA_ENABLE_SDMA=0 python tools/rss_probe.py" \
+  "120|rss_q2_devq|GPU_MAX_HW_QUEUES=2 HSA_ALLOCATE_QUEUE_DEV_MEM=1 python tools/rss_probe.py"

@@ -41,12 +41,35 @@ def big_anon(min_mb: float = 8.0):
     return sorted([m for m in out if m[1] >= min_mb], key=lambda m: -m[1])
 
 
-def step(name):
+def top_mappings(n: int = 6, min_mb: float = 4.0):
+    """The largest resident mappings (RSS >= min_mb): (rss MB, kind, name)."""
+    out, cur = [], None
+    with open("/proc/self/smaps") as f:
+        for ln in f:
+            p = ln.split()
+            if p and "-" in p[0] and not p[0].endswith(":"):
+                name = " ".join(p[5:]) if len(p) > 5 else "[anon]"
+                cur = [0.0, p[1], name]
+                out.append(cur)
+            elif p and p[0] == "Rss:" and cur is not None:
+                cur[0] = int(p[1]) / 1024
+    agg = {}
+    for rss, flags, name in out:
+        key = (os.path.basename(name) if name.startswith("/") else name)
+        agg[key] = agg.get(key, 0.0) + rss
+    return sorted([(v, k) for k, v in agg.items() if v >= min_mb], reverse=True)[:n]
+
+
+def step(name, detail=False):
     print(f"{name:40s} rss {rss_mb():8.1f} MB  anon {anon_mb():8.1f} MB", flush=True)
+    if detail:
+        for rss, key in top_mappings():
+            print(f"      {rss:8.1f} MB  {key}", flush=True)
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_250_000
+    print("env:", {k: v for k, v in os.environ.items() if k.startswith(("GPU_", "HSA_", "HIP_", "ROC_"))}, flush=True)
     step("start")
     from llm_slo_ebpf_toolkit_amd.ops import load_agent
 
@@ -55,7 +78,7 @@ def main():
     mod.device_count()
     step("hip runtime init (device_count)")
     load_agent()
-    step("set_tables")
+    step("set_tables", detail=True)
     from llm_slo_ebpf_toolkit_amd.pipeline.window import WindowPipeline
 
     small = WindowPipeline(65536, 4096, 64, 0, None, model="bayes", learn=False, user_cap=16384)
@@ -70,7 +93,8 @@ def main():
     from llm_slo_ebpf_toolkit_amd.collector import bpf
 
     names = bpf.RingNames.of(f"/mislo-rss-{os.getpid()}")
-    ring, user, spans = bpf.create_rings(names, 4 * 24 * 1_000_000, 4_000_000, 4 * 16384)
+    # the agent's replay-source sizes: two windows of framed records, a window of USER24 records
+    ring, user, spans = bpf.create_rings(names, 2 * 24 * 1_000_000, 1_000_000, 4 * 16384)
     step("create_rings")
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource
 
@@ -79,7 +103,7 @@ def main():
     for _ in range(4):
         src.step(64)
     src.drain()
-    step("4 empty windows")
+    step("4 empty windows", detail=True)
     pipe.eng.close()
     step("engine closed")
 
