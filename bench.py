@@ -389,8 +389,8 @@ def main() -> int:
     trained = None
     train_info = {}
     if train_imgs:
-        from llm_slo_ebpf_toolkit_amd.models.bayes import SufficientStats, soft_labels
-        from llm_slo_ebpf_toolkit_amd.pipeline.window import stats_from_packet, unpack_packet
+        from llm_slo_ebpf_toolkit_amd.models.bayes import SufficientStats, soft_labels, with_pairs
+        from llm_slo_ebpf_toolkit_amd.ops.engine import model_bytes
 
         t_tr = time.perf_counter()
         hold_f, hold_c = [], []
@@ -414,20 +414,30 @@ def main() -> int:
             dist.all_gather_object(gath, (hf, hc))
             hf, hc = np.concatenate([g[0] for g in gath]), np.concatenate([g[1] for g in gath])
         T, nll = mtrain.fit_temperature(base, hf, soft_labels(hc), tcfg.t_grid)
-        pipe.eng.restore(st, np.zeros(0, np.uint8), int(pipe.windows_folded))
+        # 2-fault hypotheses: prior mass = the labelled share of multi-fault training incidents
+        trc = np.concatenate([c for j, c in enumerate(train_codes) if j % 4 != 3])
+        if pg is not None:
+            gath = [None] * world
+            dist.all_gather_object(gath, trc)
+            trc = np.concatenate(gath)
+        rho = mtrain.pair_prior(trc)
+        model = with_pairs(NaiveBayes_learned(stats, tcfg, T), rho, T)
+        # the image carries the pair structure (members, rho); the device refit rebuilds every
+        # table from the all-reduced statistics with the fitted temperature
+        pipe.eng.restore(st, model_bytes(model), int(pipe.windows_folded))
         pipe.eng.set_refit(tcfg.alpha, tcfg.prior_pseudo, 1.0 / T, tcfg.min_count)
         pipe.eng.refit_now()
         pipe.eng.set_device_refit(False)  # frozen from here on: the timed region scores, as the agent does
         pipe.device_refit = False
         pipe.learn = False
-        model = NaiveBayes_learned(stats, tcfg, T)
         pipe.model = model
         trained = mtrain.TrainedModel(model, stats, T, {
-            "engine": "gpu-window-engine", "temperature": T, "holdout_nll": nll,
+            "engine": "gpu-window-engine", "temperature": T, "pair_rho": rho, "holdout_nll": nll,
             "holdout_nll_t1": mtrain.soft_nll(base, hf, soft_labels(hc), 1.0), "train_windows": len(train_imgs),
             "events_per_window": a.train_events, "scenarios": list(mtrain.TRAIN_SCENARIOS), "seed": a.seed,
             "active_domains": [d for i, d in enumerate(catalog_domains()) if np.isfinite(model.bias[i])]})
         train_info = {"windows": len(train_imgs), "held_out": len(hold_f), "temperature": round(T, 4),
+                      "pair_rho": round(rho, 4),
                       "holdout_nll": round(nll, 4), "holdout_nll_t1": round(trained.meta["holdout_nll_t1"], 4),
                       "seconds": round(train_s, 3), "events_per_window": a.train_events,
                       "incidents_trained": int(round(stats.count.sum())), "active_domains": trained.meta["active_domains"]}

@@ -177,6 +177,8 @@ class AgentOptions:
     procfs_sampler: bool = False         # runqueue_delay_ms from /proc schedstat (no BPF needed)
     procfs_pods: str = ""                # pid:pod-uid,... to watch ("" = the node's kubepods cgroups)
     procfs_interval_ms: int = 100
+    model_signals: str = ""              # signals the node's sources produce (others marginalised; "" = all)
+    pair_prior: float = 0.0              # 2-fault prior mass added to a table model without pairs (0 = none)
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -423,18 +425,31 @@ class Agent:
         ``attributor --train``), else the built-in expert tables."""
         from ..ops.engine import model_bytes
 
+        from ..models.bayes import marginalize, with_pairs
+
         o = self.o
         if o.model_path:
             from ..models.train import load_model
 
-            return load_model(o.model_path)
-        if o.model in ("bayes", ""):
-            m = NaiveBayes.ref()
-        elif o.model == "bayes_gpu":
-            m = NaiveBayes.gpu()
+            m, image, meta = load_model(o.model_path)
+        elif o.model in ("bayes", "bayes_gpu", ""):
+            m = NaiveBayes.gpu() if o.model == "bayes_gpu" else NaiveBayes.ref()
+            image, meta = model_bytes(m), {"name": m.name}
         else:
             raise ValueError(f"--model {o.model} is learned: give --model-path (a file `attributor --train` wrote)")
-        return m, model_bytes(m), {"name": m.name}
+        T = float(meta.get("temperature", 1.0))
+        if o.pair_prior > 0 and m.pairs is None:
+            m = with_pairs(m, o.pair_prior, T)
+            meta = dict(meta, pair_rho=o.pair_prior)
+        if o.model_signals:
+            # signals no source on this node produces are summed out of the likelihood: their
+            # absence says nothing about the domains they would indicate
+            obs = [x.strip() for x in o.model_signals.split(",") if x.strip()]
+            m = marginalize(m, obs, T)
+            meta = dict(meta, observable_signals=obs)
+        if o.pair_prior > 0 or o.model_signals:
+            image = model_bytes(m)
+        return m, image, meta
 
     def n_gpus(self) -> int:
         """Window workers: --gpus, or every GPU visible to the agent (--gpus 0; counted without
@@ -566,7 +581,8 @@ class Agent:
         self.metrics.set_ring(ring.stats() if ring is not None else {}, rs, max(p["host_us"] for p in prevs))
         res = merge_results(head["results"], G)
         self.last_results = res
-        for attr in self._attributions(G, names, res, t_ns, model):
+        attrs = self._attributions(G, names, res, t_ns, model)
+        for attr in attrs:
             self.metrics.observe_attribution(attr.predicted_fault_domain)
             self.writers.emit_attribution(attr)
             self.attributions_emitted += 1
@@ -576,6 +592,8 @@ class Agent:
                 except Exception as exc:  # noqa: BLE001
                     self.metrics.inc_dropped("emit")
                     print(f"webhook send failed: {exc}", file=sys.stderr)
+        if attrs:
+            self.writers.flush()  # a window's incidents leave with the window (detection delay)
 
     def run_windows(self, max_windows: int = 0) -> int:
         """Window engine main loop. This process is the controller: every window_ms it cuts

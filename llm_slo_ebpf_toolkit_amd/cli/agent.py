@@ -68,6 +68,11 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                   "(unprivileged; min-capability mode)"),
         ("procfs-pods", d.procfs_pods, "pid:pod-uid,... for the procfs sampler (empty: the kubepods cgroups)"),
         ("procfs-interval-ms", d.procfs_interval_ms, "procfs sampler interval"),
+        ("model-signals", d.model_signals, "window engine: comma-separated signals this node's sources produce; "
+                                           "the model sums the others out instead of reading their absence as "
+                                           "'not elevated' (empty = every signal)"),
+        ("pair-prior", d.pair_prior, "window engine: add 2-fault hypotheses with this prior mass to a table model "
+                                     "(--model bayes | bayes_gpu; trained files carry their own)"),
         ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
         ("pin-dir", d.pin_dir, "bpffs directory the probe loader pinned the maps in (--source bpf)"),
         ("probe-objs", d.probe_objs, "--source bpf: directory of compiled probes (*.bpf.o) the agent loads and "
@@ -110,7 +115,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
         checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), model_path=a.model_path,
         otlp_receiver_allow=a.otlp_receiver_allow, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
-        procfs_interval_ms=int(a.procfs_interval_ms))
+        procfs_interval_ms=int(a.procfs_interval_ms), model_signals=a.model_signals,
+        pair_prior=float(a.pair_prior))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])
         if given:  # an operator's flag wins over a node-wide GPU_MAX_HW_QUEUES

@@ -5,11 +5,17 @@ Additive: ``--emit-ring PREFIX`` injects a fault at the record level into a runn
 probes' own record path (ProbeSim: definitions, trace ids, the epochs the agent publishes):
 
     faultinject --emit-ring /mislo-agent --signal tcp_retransmits_total --pod-uid UID \\
-        --agent http://127.0.0.1:2112 --conn 51234:6333:127.0.0.1 --rate 40 --duration 30
+        --agent http://127.0.0.1:2112 --conn 51234:6333:127.0.0.1,51236:6333:127.0.0.1 --rate 40 --duration 30
 
 The pod id is the agent's own for that pod uid (``/debug/pods``), so the records join the pod's
 spans on the connection (pod + connection tier). A ``tcp_retransmits_total`` record carries the
 connection's retransmits so far, as tcp_retransmit.bpf.c does.
+
+``--fault LABEL`` injects a whole fault instead of one signal: every kernel signal of REF's
+per-fault profile (pkg/signals/generator.go:244-289; the profile REF's own faultinject samples
+carry), jittered like the replay (lognormal sigma 0.3, Poisson counts), one record of each per
+tick -- e.g. ``network_partition``: retransmits, connect latency and errors, DNS latency, TLS
+handshake failures on the victim's connections.
 """
 
 from __future__ import annotations
@@ -44,43 +50,63 @@ def emit_ring(a) -> int:
     import numpy as np
 
     from ..collector import bpf, records
+    from ..collector.otlp import _ipv4
     from ..runtime import load
     from ..signals import catalog
+    from ..signals.generator import _TUPLE_SIGNALS, FAULT_OVERRIDES
 
-    spec = catalog.BY_NAME.get(a.signal)
-    if spec is None or spec.kernel_type >= 128:
-        eprint(f"--signal {a.signal!r} is not a kernel-probe signal")
-        return 2
+    if a.fault:
+        if a.fault not in FAULT_OVERRIDES:
+            eprint(f"--fault {a.fault!r}: one of {sorted(FAULT_OVERRIDES)}")
+            return 2
+        profile = [(catalog.BY_NAME[n], v) for n, v in FAULT_OVERRIDES[a.fault].items()
+                   if catalog.BY_NAME[n].kernel_type < 128]
+    else:
+        spec = catalog.BY_NAME.get(a.signal)
+        if spec is None or spec.kernel_type >= 128:
+            eprint(f"--signal {a.signal!r} is not a kernel-probe signal")
+            return 2
+        profile = [(spec, None)]
     pod = int(a.pod_id) if a.pod_id >= 0 else agent_pod_id(a.agent, a.pod_uid)
-    sport = dport = dip = 0
-    if a.conn:
-        sp, dp, ip = a.conn.split(":", 2)
-        sport, dport = int(sp), int(dp)
-        from ..collector.otlp import _ipv4
-
-        dip = _ipv4(ip)
+    conns = []
+    for c in (x for x in a.conn.split(",") if x.strip()):
+        sp, dp, ip = c.strip().split(":", 2)
+        conns.append((int(sp), int(dp), _ipv4(ip)))
+    conns = conns or [(0, 0, 0)]
+    counts = [0] * len(conns)
     rt = load()
     ring = rt.Ringbuf.attach_shm(bpf.RingNames.of(a.emit_ring).ring)
     sim = rt.ProbeSim(ring, records.milli_shift_table())
     period = 1.0 / max(a.rate, 1e-3)
     n_total = int(round(a.duration * a.rate))
-    count = 0
+    rng = np.random.default_rng(a.seed)
     nxt = time.perf_counter()
+    n_rec = 0
     for i in range(n_total):
-        ev = np.zeros(1, dtype=records.EVENT)
+        j = i % len(conns)  # connections in turn, each with its own running count
+        counts[j] += 1
+        ev = np.zeros(len(profile), dtype=records.EVENT)
+        for r, (spec, level) in enumerate(profile):
+            if level is None:  # --signal: a counter's running total, else --value
+                v = counts[j] if spec.unit == "count" else a.value
+            elif spec.unit == "count":
+                v = max(1, int(rng.poisson(level)))
+            else:
+                v = level * float(np.exp(rng.normal(0.0, 0.3)))
+            sport, dport, dip = conns[j] if spec.name in _TUPLE_SIGNALS or level is None else (0, 0, 0)
+            ev["signal_type"][r] = spec.kernel_type
+            ev["value"][r] = int(v) if spec.unit == "count" else int(round(v / spec.decode_scale))
+            ev["src_port"][r], ev["dst_port"][r], ev["dst_ip"][r] = sport, dport, dip
         ev["ts_ns"] = time.time_ns()
-        ev["signal_type"] = spec.kernel_type
-        count += 1
-        raw = count if spec.unit == "count" else int(round(a.value / spec.decode_scale))
-        ev["value"] = raw
         ev["pid"] = a.pid
         ev["tid"] = a.pid
         ev["pod_id"] = pod
-        ev["src_port"], ev["dst_port"], ev["dst_ip"] = sport, dport, dip
         sim.submit(ev)
+        n_rec += len(ev)
         nxt += period
         time.sleep(max(0.0, nxt - time.perf_counter()))
-    print(f"injected {n_total} {a.signal} records for pod {pod} into {a.emit_ring}", flush=True)
+    what = f"{a.fault} fault" if a.fault else a.signal
+    print(f"injected {n_rec} {what} records for pod {pod} into {a.emit_ring}", flush=True)
     return 0
 
 
@@ -103,10 +129,12 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.flag("pod-id", -1, "--emit-ring: the agent's pod id, if known (skips the lookup)")
     p.flag("agent", "http://127.0.0.1:2112", "--emit-ring: the agent's metrics address")
     p.flag("pid", 0, "--emit-ring: pid on the records (0: none, e.g. softirq-context retransmits)")
-    p.flag("conn", "", "--emit-ring: sport:dport:dst-ip of the victim connection")
+    p.flag("conn", "", "--emit-ring: sport:dport:dst-ip[,...] of the victim connection(s)")
     p.flag("rate", 20.0, "--emit-ring: records per second")
     p.flag("duration", 10.0, "--emit-ring: seconds")
     p.flag("value", 0.0, "--emit-ring: value of non-count signals (output unit, e.g. ms)")
+    p.flag("fault", "", "--emit-ring: inject every kernel signal of this fault's profile (e.g. network_partition)")
+    p.flag("seed", 42, "--emit-ring --fault: jitter seed")
     a = p.parse_args(argv)
     if a.emit_ring:
         try:

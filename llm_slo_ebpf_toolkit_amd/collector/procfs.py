@@ -10,6 +10,12 @@ interval), above the probe's 100 us floor -- tagged with the process's pid and p
 them into the agent's user-space ring like the rocprofiler tool's records. The GPU window engine
 joins them to the pod's spans (pod + pid tier).
 
+Memory: the pressure-stall accounting (PSI, ``memory.pressure`` of the process's cgroup v2, else
+the node's ``/proc/pressure/memory``) says how long tasks stalled on memory -- reclaim, refaults,
+swap-in -- in every interval. Its per-interval growth becomes ``mem_reclaim_latency_ms`` records
+(the reclaim probe's signal) for the watched processes, so memory pressure is observed, not
+assumed absent, by an agent without BPF.
+
 Watched processes: a static ``pid -> pod uid`` list (``agent --procfs-pods``), or every process in
 the node's kubepods cgroups (``pod_processes``).
 """
@@ -26,7 +32,39 @@ import numpy as np
 from . import records
 
 RUNQUEUE_TYPE = 3          # catalogue kernel type of runqueue_delay_ms (ns in the record)
+MEM_RECLAIM_TYPE = 7       # catalogue kernel type of mem_reclaim_latency_ms (ns in the record)
 FLOOR_NS = 100_000         # runqueue_delay.bpf.c's emit floor
+
+
+def psi_path(pid: int, proc_root: str = "/proc", cgroup_root: str = "/sys/fs/cgroup") -> Optional[str]:
+    """The memory.pressure file covering ``pid``: its cgroup v2 group's, else the node's."""
+    try:
+        with open(os.path.join(proc_root, str(pid), "cgroup")) as fh:
+            for ln in fh:
+                if ln.startswith("0::"):
+                    p = os.path.join(cgroup_root, ln[3:].strip().lstrip("/"), "memory.pressure")
+                    if os.access(p, os.R_OK):
+                        return p
+    except OSError:
+        pass
+    p = os.path.join(proc_root, "pressure", "memory")
+    return p if os.access(p, os.R_OK) else None
+
+
+def read_psi_total_us(path: str) -> Optional[int]:
+    """``some ... total=<us>`` of a PSI file."""
+    try:
+        with open(path) as fh:
+            for ln in fh:
+                if ln.startswith("some"):
+                    return int(ln.rsplit("total=", 1)[1])
+    except (OSError, ValueError, IndexError):
+        return None
+    return None
+
+
+def psi_available(proc_root: str = "/proc") -> bool:
+    return read_psi_total_us(os.path.join(proc_root, "pressure", "memory")) is not None
 
 
 def read_schedstat(path: str) -> Optional[Tuple[int, int, int]]:
@@ -45,6 +83,7 @@ class SchedstatSampler:
         self.targets, self.push, self.rec = targets, push, int(rec)
         self.proc_root, self.floor_ns, self.node_id = proc_root, int(floor_ns), int(node_id)
         self._prev: Dict[Tuple[int, int], Tuple[int, int]] = {}
+        self._psi: Dict[int, Tuple[Optional[str], Optional[int]]] = {}   # pid -> (PSI file, last total us)
         self.samples = self.emitted = self.dropped = 0
         self._stop = threading.Event()
         self._thr: Optional[threading.Thread] = None
@@ -75,18 +114,46 @@ class SchedstatSampler:
         for key in list(self._prev):
             if key not in seen:
                 del self._prev[key]
+        mem = self._memory_rows()
         self.samples += 1
-        ev = np.zeros(len(rows), dtype=records.EVENT)
-        if rows:
-            a = np.array(rows, dtype=np.int64)
+        ev = np.zeros(len(rows) + len(mem), dtype=records.EVENT)
+        if len(ev):
+            a = np.array(rows + mem, dtype=np.int64)
             ev["ts_ns"] = now
-            ev["signal_type"] = RUNQUEUE_TYPE
+            ev["signal_type"] = np.where(np.arange(len(ev)) < len(rows), RUNQUEUE_TYPE, MEM_RECLAIM_TYPE)
             ev["value"] = a[:, 3].astype(np.uint64)
             ev["pid"] = a[:, 0].astype(np.uint32)
             ev["tid"] = a[:, 1].astype(np.uint32)
             ev["pod_id"] = a[:, 2].astype(np.uint32)
             ev["node_id"] = self.node_id
         return ev
+
+    def _memory_rows(self):
+        """(pid, pid, pod, stall ns) of the watched processes whose PSI memory stall grew by at
+        least the floor since the last interval."""
+        rows = []
+        live = set()
+        totals: Dict[str, Optional[int]] = {}
+        for pid, pod in self.targets().items():
+            live.add(pid)
+            path, last = self._psi.get(pid, (None, None))
+            if path is None:
+                path = psi_path(pid, self.proc_root)
+                if path is None:
+                    continue
+            if path not in totals:
+                totals[path] = read_psi_total_us(path)
+            tot = totals[path]
+            self._psi[pid] = (path, tot)
+            if tot is None or last is None:
+                continue
+            d_ns = (tot - last) * 1000
+            if d_ns >= self.floor_ns:
+                rows.append((pid, pid, pod, d_ns))
+        for pid in list(self._psi):
+            if pid not in live:
+                del self._psi[pid]
+        return rows
 
     def tick(self, now_ns: Optional[int] = None) -> int:
         ev = self.sample(now_ns)

@@ -407,7 +407,7 @@ class RagService:
         return {"request_id": rid, "trace_id": trace_id, "profile": profile, "tokens": tokens, "documents": docs,
                 "ttft_ms": round(ttft_ms, 3), "tokens_per_sec": round(tps, 3), "retrieval_ms": round(ret_ms, 3),
                 "correlation": {"tier": decision.tier, "confidence": decision.confidence},
-                "attributes": attrs or {}}
+                "attributes": attrs or {}, "retrieval_conn": conn_attrs}
 
     def handler(self):
         svc = self

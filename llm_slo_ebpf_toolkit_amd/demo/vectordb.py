@@ -9,6 +9,10 @@ per worker thread, so its request spans carry that connection's tuple (client po
 port, server address) and the node agent joins TCP-level kernel signals of the connection to
 the requests (the pod+connection tier).
 
+``POST /fault {"delay_ms": D}`` stalls every response by D ms until reset with 0: the latency a
+lossy path adds to the connection (retransmission timeouts), for fault-injection runs on hosts
+where ``tc netem`` needs privileges the harness does not have.
+
     python -m llm_slo_ebpf_toolkit_amd.demo.vectordb --bind 127.0.0.1:6333
 """
 
@@ -51,6 +55,7 @@ class VectorDB:
         noise = rng.normal(0, 0.05, size=(len(docs), replicas, DIM)).astype(np.float32)
         self.matrix = (base[:, None, :] + noise).reshape(-1, DIM)
         self.searches = 0
+        self.delay_ms = 0.0
         self._lock = threading.Lock()
 
     def search(self, query: str, k: int = 4):
@@ -83,6 +88,15 @@ class VectorDB:
                 self._json(200 if self.path == "/healthz" else 404, {"status": "ok", "searches": db.searches})
 
             def do_POST(self):
+                if self.path == "/fault":
+                    n = int(self.headers.get("Content-Length") or 0)
+                    try:
+                        db.delay_ms = max(0.0, float(json.loads(self.rfile.read(n) or b"{}").get("delay_ms", 0)))
+                    except (ValueError, TypeError, AttributeError):
+                        self._json(400, {"error": "delay_ms must be a number"})
+                        return
+                    self._json(200, {"delay_ms": db.delay_ms})
+                    return
                 if self.path != "/search":
                     self._json(404, {"error": "not found"})
                     return
@@ -94,6 +108,8 @@ class VectorDB:
                     return
                 t0 = time.perf_counter()
                 hits = db.search(str(req.get("query", "")), int(req.get("k", 4)))
+                if db.delay_ms:
+                    time.sleep(db.delay_ms / 1000.0)
                 self._json(200, {"hits": hits, "took_ms": round(1e3 * (time.perf_counter() - t0), 3)})
 
         return H

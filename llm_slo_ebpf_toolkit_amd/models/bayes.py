@@ -18,11 +18,20 @@ evaluates for a whole batch of incidents at once:
   class conditionals on log1p(signal) features; W = S^-1 mu_d,
   b = -1/2 mu_d^T S^-1 mu_d + log pi_d. Its scatter matrix is the MFMA covariance step.
 
+* ``with_pairs(model, rho)`` -- the 2-fault posterior: the hypothesis space grows from the
+  single domains to every pair of fault domains, each pair a noisy-OR of its members'
+  likelihoods (P(e_s | {a, b}) = 1 - (1 - p_sa)(1 - p_sb)) with prior mass ``rho`` shared over
+  the pairs in proportion to pi_a pi_b. A pair is one more linear-logit column, so the MFMA
+  kernel scores all 10 + 36 hypotheses in the same product; the output per domain is its
+  *marginal* P(d in the incident | evidence) = P({d}) + sum of the pairs holding d (REF's
+  single-label posterior, pipeline.go:140-185, has no way to say "both").
+
 All CPU math is float64 numpy (the oracle); the GPU path evaluates the same W/b.
 """
 
 from __future__ import annotations
 
+import itertools
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -41,6 +50,11 @@ THRESHOLDS = np.array([s.elevated for s in catalog.SIGNALS], dtype=np.float64)
 # REF base signal profile (pkg/signals/generator.go:244-259) + GPU nominals.
 NOMINAL = np.array([12, 0.2, 4, 18, 0, 22, 0, 0.6, 5, 0.5, 2, 5, 0.5, 40, 3, 1.0], dtype=np.float64)
 NEG_INF = -np.inf
+MAX_PAIRS = 48                             # ops/csrc/mislo_launch.h kMaxPairs (3 MFMA column tiles)
+# 2-fault hypotheses: every pair of fault domains ("unknown" is the no-fault hypothesis)
+PAIR_LIST: Tuple[Tuple[int, int], ...] = tuple(itertools.combinations(
+    [d for d, n in enumerate(catalog.ALL_DOMAINS) if n != "unknown"], 2))
+assert len(PAIR_LIST) <= MAX_PAIRS
 
 
 def clamp_likelihood(p):
@@ -65,6 +79,11 @@ class LinearPosteriorModel:
     thresholds: np.ndarray = field(default_factory=lambda: THRESHOLDS.copy())
     mean: Optional[np.ndarray] = None   # continuous: feature centring
     table_mask: Optional[np.ndarray] = None  # binary: which slots the model knows
+    # 2-fault hypotheses (with_pairs): [16, P] weights, [P] bias (-inf = inactive), [P, 2] members
+    pair_w: Optional[np.ndarray] = None
+    pair_b: Optional[np.ndarray] = None
+    pairs: Optional[np.ndarray] = None
+    pair_rho: float = 0.0
 
     def features(self, values: np.ndarray) -> np.ndarray:
         """values: [B, 16] with NaN for absent signals -> model features X [B, 16]."""
@@ -93,13 +112,41 @@ class LinearPosteriorModel:
     def logits(self, values: np.ndarray) -> np.ndarray:
         return self.features(values) @ self.weights + self.bias[None, :]
 
-    def posteriors(self, values: np.ndarray) -> np.ndarray:
-        lg = self.logits(values)
-        m = np.max(lg, axis=1, keepdims=True)
+    def hypothesis_posteriors(self, values: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """(P(single d) [B, D], P(pair h) [B, P]) -- the normalised hypothesis distribution (no
+        pairs: [B, 0])."""
+        x = self.features(values)
+        lg = x @ self.weights + self.bias[None, :]
+        l2 = (x @ self.pair_w + self.pair_b[None, :]) if self.pairs is not None else np.zeros((lg.shape[0], 0))
+        allv = np.concatenate([lg, l2], axis=1)
+        m = np.max(allv, axis=1, keepdims=True)
         with np.errstate(invalid="ignore"):
-            ex = np.exp(lg - m)
-        z = m + np.log(np.sum(ex, axis=1, keepdims=True))
-        return np.exp(lg - z)
+            z = m + np.log(np.sum(np.exp(allv - m), axis=1, keepdims=True))
+        return np.exp(lg - z), np.exp(l2 - z)
+
+    def posteriors(self, values: np.ndarray) -> np.ndarray:
+        """Per domain: the posterior (single-fault model) or the marginal P(d in the incident)
+        (2-fault model)."""
+        if self.pairs is None:
+            lg = self.logits(values)
+            m = np.max(lg, axis=1, keepdims=True)
+            with np.errstate(invalid="ignore"):
+                ex = np.exp(lg - m)
+            z = m + np.log(np.sum(ex, axis=1, keepdims=True))
+            return np.exp(lg - z)
+        p1, p2 = self.hypothesis_posteriors(values)
+        marg = p1.copy()
+        for h, (a, b) in enumerate(self.pairs.tolist()):
+            marg[:, a] += p2[:, h]
+            marg[:, b] += p2[:, h]
+        return marg
+
+    def predict(self, values: np.ndarray) -> np.ndarray:
+        """Top-1 domain: argmax of the logits (single-fault) or of the marginals (2-fault);
+        ties -> the lowest domain index, as the kernel."""
+        if self.pairs is None:
+            return np.argmax(self.logits(values), axis=1)
+        return np.argmax(self.posteriors(values), axis=1)
 
     def evidence_bits(self, values: np.ndarray) -> np.ndarray:
         """[B, D] uint32 bitmask over slots: elevated & P(elevated|d) >= 0.5."""
@@ -244,9 +291,102 @@ def with_temperature(m: LinearPosteriorModel, temperature: float) -> LinearPoste
         raise ValueError("temperature must be > 0")
     inv = 1.0 / float(temperature)
     bias = np.where(np.isfinite(m.bias), m.bias * inv, m.bias)
-    return LinearPosteriorModel(m.name, m.weights * inv, bias, m.evidence_mask.copy(), m.feature_mode,
-                                m.thresholds.copy(), None if m.mean is None else m.mean.copy(),
-                                None if m.table_mask is None else m.table_mask.copy())
+    out = LinearPosteriorModel(m.name, m.weights * inv, bias, m.evidence_mask.copy(), m.feature_mode,
+                               m.thresholds.copy(), None if m.mean is None else m.mean.copy(),
+                               None if m.table_mask is None else m.table_mask.copy())
+    if m.pairs is not None:
+        out.pair_w, out.pairs, out.pair_rho = m.pair_w * inv, m.pairs.copy(), m.pair_rho
+        out.pair_b = np.where(np.isfinite(m.pair_b), m.pair_b * inv, m.pair_b)
+    return out
+
+
+def _raw_tables(m: LinearPosteriorModel, temperature: float):
+    """(P(e | d) [16, D], log prior [D] (-inf inactive), table slots [16] bool) of a binary naive
+    Bayes in linear-logit form at ``temperature``: W = logit(p) and pe + pn = 1 after REF's
+    clamp, so p = sigmoid(T W) and log pi_d = T b_d - sum_s log(1 - p_sd)."""
+    T = float(temperature)
+    table = (m.table_mask if m.table_mask is not None else np.ones(N_SLOTS)).astype(bool)
+    raw = m.weights * T
+    p = 1.0 / (1.0 + np.exp(-raw))
+    logpn = -np.logaddexp(0.0, raw)
+    with np.errstate(invalid="ignore"):
+        logpi = np.where(np.isfinite(m.bias), m.bias * T - (logpn * table[:, None]).sum(axis=0), NEG_INF)
+    return p, logpi, table
+
+
+def with_pairs(m: LinearPosteriorModel, rho: float, temperature: float = 1.0) -> LinearPosteriorModel:
+    """The 2-fault model of a binary naive Bayes (see the module docstring): single hypotheses
+    keep their likelihoods with prior (1 - rho) pi_d; pair {a, b} gets the noisy-OR likelihood
+    and prior rho pi_a pi_b / sum over active pairs. ``temperature`` is the one the model's
+    weights are already divided by (the pair columns get the same). The device refit
+    (posterior.hip k_refit_nb) builds the identical tables."""
+    if m.feature_mode != "binary":
+        raise ValueError("the 2-fault model is defined for binary naive Bayes")
+    if not 0.0 < rho < 1.0:
+        raise ValueError("rho must be in (0, 1)")
+    T = float(temperature)
+    p, logpi, table = _raw_tables(m, T)
+    fin = np.isfinite(logpi)
+    logpi = np.where(fin, logpi - np.log(np.exp(logpi[fin]).sum()), NEG_INF)
+    P = len(PAIR_LIST)
+    pw = np.zeros((N_SLOTS, P))
+    pb = np.full(P, NEG_INF)
+    pr = np.array([logpi[a] + logpi[b] for a, b in PAIR_LIST])
+    act = np.isfinite(pr)
+    pnorm = math.log(np.exp(pr[act]).sum()) if act.any() else 0.0
+    for h, (a, b) in enumerate(PAIR_LIST):
+        if not act[h]:
+            continue
+        q = clamp_likelihood(1.0 - (1.0 - p[:, a]) * (1.0 - p[:, b]))
+        qn = clamp_likelihood(1.0 - q)
+        pw[:, h] = np.where(table, np.log(q) - np.log(qn), 0.0) / T
+        pb[h] = (math.log(rho) + pr[h] - pnorm + float(np.log(qn)[table].sum())) / T
+    bias = np.where(np.isfinite(m.bias), m.bias + math.log1p(-rho) / T, m.bias)
+    out = LinearPosteriorModel(m.name, m.weights.copy(), bias, m.evidence_mask.copy(), m.feature_mode,
+                               m.thresholds.copy(), None, None if m.table_mask is None else m.table_mask.copy())
+    out.pair_w, out.pair_b, out.pairs, out.pair_rho = pw, pb, np.array(PAIR_LIST, dtype=np.int64), float(rho)
+    return out
+
+
+def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature: float = 1.0) -> LinearPosteriorModel:
+    """The binary naive-Bayes model scoring only the ``observable`` signals: every other table
+    signal is summed out of the likelihood (its factor P(e_s | d) marginalises to 1) instead of
+    being read as "not elevated". An agent whose sources cannot produce a signal at all (no
+    probe for it on this node, a degraded capability mode, no GPU tool) must not count its
+    absence as evidence against the domains it would indicate.
+
+    In the linear-logit form a table signal contributes ``e * W[s, d]`` plus ``log P(not e | d)``
+    folded into the bias, with ``W = logit(P(e | d))``; so summing it out is ``W[s, :] = 0`` and
+    ``bias[d] += softplus(W[s, d])``, both at the model's ``temperature`` (stored weights and bias
+    are divided by it)."""
+    if m.feature_mode != "binary":
+        raise ValueError("only binary naive-Bayes models marginalise signal by signal")
+    keep = {catalog.BY_NAME[s].slot for s in observable if s in catalog.BY_NAME}
+    unknown = [s for s in observable if s not in catalog.BY_NAME]
+    if unknown:
+        raise ValueError(f"unknown signals {unknown}")
+    T = float(temperature)
+    W, b = m.weights.copy(), m.bias.copy()
+    table = m.table_mask.copy() if m.table_mask is not None else np.ones(N_SLOTS)
+    mask = m.evidence_mask.copy()
+    fin = np.isfinite(b)
+    pw = m.pair_w.copy() if m.pairs is not None else None
+    pb = m.pair_b.copy() if m.pairs is not None else None
+    pfin = np.isfinite(pb) if pb is not None else None
+    for s in range(N_SLOTS):
+        if s in keep or not table[s]:
+            continue
+        b[fin] += (np.logaddexp(0.0, W[s] * T) / T)[fin]
+        W[s] = 0.0
+        if pw is not None:  # the pair columns are naive-Bayes columns too
+            pb[pfin] += (np.logaddexp(0.0, pw[s] * T) / T)[pfin]
+            pw[s] = 0.0
+        mask[s] = False
+        table[s] = 0.0
+    out = LinearPosteriorModel(m.name, W, b, mask, m.feature_mode, m.thresholds.copy(), None, table)
+    if pw is not None:
+        out.pair_w, out.pair_b, out.pairs, out.pair_rho = pw, pb, m.pairs.copy(), m.pair_rho
+    return out
 
 
 def label_code(primary: int, domains: Sequence[int] = ()) -> int:

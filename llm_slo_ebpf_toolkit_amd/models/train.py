@@ -22,7 +22,11 @@ agent loads (``agent --model-path``):
    soft-label negative log-likelihood. Naive Bayes multiplies 16 signals' evidence as if
    independent, so its raw posteriors are far too sharp; T restores probabilities that spread
    over a compound incident's domains (REF's coverage metric counts hypotheses with posterior
-   >= 0.10, pipeline.go:140-185) without changing any argmax.
+   >= 0.10, pipeline.go:140-185) without changing any argmax;
+5. **2-fault posterior** -- the hypothesis space grows to every pair of fault domains
+   (bayes.with_pairs: noisy-OR likelihoods), the pairs' prior mass rho being the labelled share
+   of multi-fault incidents; the model then reports each domain's marginal probability of
+   being part of the incident.
 
 The device refit (posterior.hip k_refit_nb) evaluates exactly ``NaiveBayes.learned`` with the
 same T and minimum mass, so a model trained on the GPU and one trained here are the same
@@ -40,8 +44,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from ..signals import catalog
-from .bayes import (N_DOMAINS, LinearPosteriorModel, NaiveBayes, SufficientStats, label_code, soft_labels,
-                    with_temperature)
+from .bayes import (N_DOMAINS, PAIR_LIST, LinearPosteriorModel, NaiveBayes, SufficientStats, label_code,
+                    soft_labels, with_pairs, with_temperature)
 
 REF_FAULTS = ("provider_throttle", "dns_latency", "cpu_throttle", "memory_pressure", "network_partition")
 COMPOUND = [c for k in (2, 3) for c in itertools.combinations(REF_FAULTS, k)]
@@ -61,6 +65,7 @@ class TrainConfig:
     min_count: float = 1.0            # labelled mass below which a domain stays inactive
     holdout_every: int = 4            # every 4th window is held out for the temperature fit
     t_grid: Tuple[float, float, int] = (1.0, 20.0, 64)
+    pairs: bool = True                # 2-fault posterior (bayes.with_pairs)
 
 
 @dataclass
@@ -146,6 +151,42 @@ def fit_temperature(model: LinearPosteriorModel, feats: np.ndarray, Y: np.ndarra
     return best[1], best[0]
 
 
+def hypothesis_targets(codes: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Label codes -> target rows over the 2-fault hypothesis space: a single fault (or no
+    fault: "unknown") is its single hypothesis, a pair its pair, a larger set its pairs evenly."""
+    codes = np.asarray(codes, dtype=np.int64)
+    index = {pr: h for h, pr in enumerate(PAIR_LIST)}
+    Y1 = np.zeros((len(codes), N_DOMAINS))
+    Y2 = np.zeros((len(codes), len(PAIR_LIST)))
+    for b, c in enumerate(codes.tolist()):
+        if c < 0:
+            continue
+        dset = [d for d in range(16) if (c >> 8) >> d & 1]
+        if len(dset) <= 1:
+            Y1[b, (dset[0] if dset else c & 0xFF)] = 1.0
+            continue
+        hs = [index[pr] for pr in itertools.combinations(sorted(dset), 2) if pr in index]
+        for h in hs:
+            Y2[b, h] = 1.0 / len(hs)
+    return Y1, Y2
+
+
+def hypothesis_nll(model: LinearPosteriorModel, feats: np.ndarray, Y1: np.ndarray, Y2: np.ndarray) -> float:
+    p1, p2 = model.hypothesis_posteriors(np.asarray(feats, dtype=np.float64))
+    with np.errstate(divide="ignore"):
+        l1, l2 = np.log(np.maximum(p1, 1e-300)), np.log(np.maximum(p2, 1e-300))
+    return float(-((Y1 * l1).sum() + (Y2 * l2).sum()) / max(len(Y1), 1))
+
+
+def pair_prior(codes: np.ndarray) -> float:
+    """rho: the labelled share of multi-fault incidents (Laplace-smoothed), the 2-fault
+    hypotheses' prior mass -- estimated from counts like the single-domain priors."""
+    c = np.asarray(codes, dtype=np.int64)
+    c = c[c >= 0]
+    multi = int((((c >> 8) & 0xFFFF) != 0).sum())
+    return (multi + 1.0) / (len(c) + 2.0)
+
+
 def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: TrainConfig) -> TrainedModel:
     """Statistics on the training windows, temperature on the held-out ones."""
     feats = np.asarray(feats, dtype=np.float64)
@@ -159,8 +200,14 @@ def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: Train
     hv = hold & (np.asarray(codes) >= 0)
     t, nll = fit_temperature(base, feats[hv], Y[hv], cfg.t_grid) if hv.any() else (1.0, float("nan"))
     model = with_temperature(base, t)
+    rho, hnll = 0.0, float("nan")
+    if cfg.pairs:
+        rho = pair_prior(np.asarray(codes)[tr])
+        model = with_pairs(model, rho, t)
+        if hv.any():
+            hnll = hypothesis_nll(model, feats[hv], *hypothesis_targets(np.asarray(codes)[hv]))
     model.name = "bayes_learned"
-    meta = {"temperature": t, "holdout_nll": nll, "holdout_nll_t1": soft_nll(base, feats[hv], Y[hv], 1.0)
+    meta = {"temperature": t, "pair_rho": rho, "holdout_hypothesis_nll": hnll, "holdout_nll": nll, "holdout_nll_t1": soft_nll(base, feats[hv], Y[hv], 1.0)
             if hv.any() else float("nan"), "train_incidents": int(tr.sum()), "holdout_incidents": int(hv.sum()),
             "domain_mass": {catalog.ALL_DOMAINS[d]: round(float(st.count[d]), 3) for d in range(N_DOMAINS)},
             "active_domains": [catalog.ALL_DOMAINS[d] for d in range(N_DOMAINS) if np.isfinite(model.bias[d])]}
@@ -186,7 +233,7 @@ Scorer = Callable[[np.ndarray], Tuple[np.ndarray, np.ndarray]]  # feat [n,16] f3
 def host_scorer(model: LinearPosteriorModel) -> Scorer:
     def score(feat):
         f = np.asarray(feat, dtype=np.float64)
-        return model.posteriors(f), np.argmax(model.logits(f), axis=1)
+        return model.posteriors(f), model.predict(f)
 
     return score
 

@@ -113,30 +113,6 @@ class Engine {
     jp_.group_mode = (int)group_mode;
   }
 
-  // model: w[16,16] f64, bias[16], mean[16], nominal[16], thr[16] f32, dom_mask[16] i32
-  void set_model(torch::Tensor w, torch::Tensor bias, torch::Tensor mean, torch::Tensor nominal, torch::Tensor thr,
-                 torch::Tensor dom_mask, int64_t table_mask, int64_t mode) {
-    PosteriorModel pm;
-    std::memset(&pm, 0, sizeof(pm));
-    auto wc = w.to(torch::kCPU, torch::kFloat64).contiguous();
-    auto bc = bias.to(torch::kCPU, torch::kFloat64).contiguous();
-    auto mc = mean.to(torch::kCPU, torch::kFloat64).contiguous();
-    auto nc = nominal.to(torch::kCPU, torch::kFloat64).contiguous();
-    auto tc = thr.to(torch::kCPU, torch::kFloat32).contiguous();
-    auto dc = dom_mask.to(torch::kCPU, torch::kInt64).contiguous();
-    if (wc.numel() != kSlots * kMaxDomains || bc.numel() != kMaxDomains) throw std::invalid_argument("model shape");
-    std::memcpy(pm.w, wc.data_ptr<double>(), sizeof(pm.w));
-    std::memcpy(pm.bias, bc.data_ptr<double>(), sizeof(pm.bias));
-    std::memcpy(pm.mean, mc.data_ptr<double>(), sizeof(pm.mean));
-    std::memcpy(pm.nominal, nc.data_ptr<double>(), sizeof(pm.nominal));
-    std::memcpy(pm.thr, tc.data_ptr<float>(), sizeof(pm.thr));
-    for (int d = 0; d < kMaxDomains; ++d) pm.dom_mask[d] = (uint32_t)dc.data_ptr<int64_t>()[d];
-    pm.table_mask = (uint32_t)table_mask;
-    pm.mode = (int32_t)mode;
-    auto host = torch::from_blob(&pm, {(int64_t)sizeof(pm)}, torch::kUInt8).clone();
-    model.copy_(host, /*non_blocking=*/false);
-  }
-
   // Retarget the per-window I/O buffers (counts int32[4], labels int32[group_cap],
   // packet f64[PACKET_LEN]) so the caller can double-buffer them: the H2D of window i+1
   // and the RCCL all-reduce of window i's packet then never race window i's kernels.
@@ -457,7 +433,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("group_cap"), py::arg("device") = 0)
       .def("set_join_params", &Engine::set_join_params, py::arg("window_ms") = 2000.0,
            py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1)
-      .def("set_model", &Engine::set_model)
       .def("set_model_bytes", &Engine::set_model_bytes)
       .def("bind_io", &Engine::bind_io)
       .def("reset_window", &Engine::reset_window)

@@ -17,6 +17,7 @@ constexpr int kPartBits = 10;       // 1024 hash partitions per key type
 constexpr int kParts = 1 << kPartBits;
 constexpr int kPartBlocks = 256;    // max decode/scatter workgroups (per-block partition counts)
 constexpr int kMaxDomains = 16;     // posterior columns (10 used, padded to the MFMA tile)
+constexpr int kMaxPairs = 48;       // 2-fault hypothesis columns (36 used: pairs of the 9 fault domains)
 constexpr int kGroupStripes = 16;   // incident-sum copies (join atomics spread, folded after)
 constexpr int kMaxTypes = 128;      // signal_type lookup table size
 constexpr uint64_t kEmpty = ~0ull;  // empty top-3 slot

@@ -20,6 +20,14 @@ struct PosteriorModel {
   uint32_t dom_mask[kMaxDomains]; // per domain: slots with P(elevated|d) >= 0.5
   uint32_t table_mask;            // slots known to the model (binary mode)
   int32_t mode;                   // 0 binary evidence, 1 continuous (log1p) features
+  // 2-fault hypotheses (models/bayes.py with_pairs): pair h = {pair_a[h], pair_b[h]} is one
+  // more logit column; post[] then holds each domain's marginal P(d in the incident)
+  int32_t n_pairs;                // 0 = single-fault posterior
+  double pair_rho;                // prior mass of the pairs (the device refit rebuilds them)
+  double w2[kSlots][kMaxPairs];
+  double bias2[kMaxPairs];        // -inf = inactive pair
+  uint8_t pair_a[kMaxPairs];
+  uint8_t pair_b[kMaxPairs];
 };
 
 // decode.hip

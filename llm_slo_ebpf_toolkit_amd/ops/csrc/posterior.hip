@@ -14,6 +14,12 @@
 // sums) and X^T X (scatter) in one 32x32 f64 product, reduced across waves with f64
 // atomics. These are the sufficient statistics the learned models are refit from.
 //
+// 2-fault models (models/bayes.py with_pairs) add up to kMaxPairs hypothesis columns -- every
+// pair of fault domains, a noisy-OR of its members -- as up to three more 16-column MFMA tiles
+// of the same K = 16 product. The log-sum-exp then runs over singles and pairs together, and
+// each domain lane sums its marginal P(d in incident) = P({d}) + sum_h P(pair h holds d) with
+// one 16-lane shuffle per pair; argmax / confidence are taken over the marginals.
+//
 // f64 MFMA C/D layout on gfx950: col = lane & 15, row = (lane >> 4) + 4 * reg
 // (cdna_hip_programming.md section 3 -- NOT the f32 row map).
 #include "mislo_common.h"
@@ -80,7 +86,10 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
   const int i = lane & 15;
   const int kq = lane >> 4;
 
+  const int n_pairs = pm.n_pairs;
+  const int n_pt = (n_pairs + 15) >> 4;  // pair tiles (uniform over the wave)
   f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  f64x4 acc2[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     const int s = 4 * kk + kq;
@@ -88,9 +97,66 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
     const double a = r < G ? feature_x(feat[(size_t)r * kSlots + s], s, pm) : 0.0;
     const double b = pm.w[s][i];
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      if (t < n_pt) acc2[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, pm.w2[s][16 * t + i], acc2[t], 0, 0, 0);
   }
 
   const double bias = pm.bias[i];
+  if (n_pt > 0) {
+    double b2[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) b2[t] = (16 * t + i < n_pairs) ? pm.bias2[16 * t + i] : -INFINITY;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int r = row0 + kq + 4 * reg;
+      const double lg = acc[reg] + bias;
+      double l2[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) l2[t] = (t < n_pt) ? acc2[t][reg] + b2[t] : -INFINITY;
+      double m = fmax(lg, fmax(l2[0], fmax(l2[1], l2[2])));
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) m = fmax(m, __shfl_xor(m, off, 16));
+      double sum = (lg == -INFINITY) ? 0.0 : exp(lg - m);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) sum += (l2[t] == -INFINITY) ? 0.0 : exp(l2[t] - m);
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
+      const double logz = m + log(sum);
+      double pp[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) pp[t] = (l2[t] == -INFINITY) ? 0.0 : exp(l2[t] - logz);
+      double marg = (lg == -INFINITY) ? 0.0 : exp(lg - logz);
+      for (int h = 0; h < n_pairs; ++h) {  // pair h lives in tile h >> 4, lane h & 15
+        const int t = h >> 4;
+        const double v = t == 0 ? pp[0] : (t == 1 ? pp[1] : pp[2]);
+        const double ph = __shfl(v, h & 15, 16);
+        if (pm.pair_a[h] == i || pm.pair_b[h] == i) marg += ph;
+      }
+      double mm = marg;
+      int am = i;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        const double om = __shfl_xor(mm, off, 16);
+        const int oa = __shfl_xor(am, off, 16);
+        if (om > mm || (om == mm && oa < am)) { mm = om; am = oa; }
+      }
+      if (r < G) {
+        post[(size_t)r * kMaxDomains + i] = marg;
+        const uint32_t eb = elevated_bits(feat + (size_t)r * kSlots, pm);
+        evbits[(size_t)r * kMaxDomains + i] = eb & pm.dom_mask[i];
+        if (i == 0) {
+          pred[r] = am;
+          conf[r] = mm;
+          if (labels != nullptr) {
+            const int y = labels[r];
+            if (y >= 0 && (y & 0xFF) < kMaxDomains) atomicAdd(confusion + (y & 0xFF) * kMaxDomains + am, 1u);
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int reg = 0; reg < 4; ++reg) {
     const int r = row0 + kq + 4 * reg;
@@ -214,6 +280,9 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
                                                   int n_dom, double inv_temp, double min_count,
                                                   PosteriorModel* __restrict__ pm) {
   __shared__ double s_logpn[kSlots][kMaxDomains];
+  __shared__ double s_pe[kSlots][kMaxDomains];
+  __shared__ double s_logpi[kMaxDomains];
+  __shared__ double s_pnorm;
   __shared__ uint32_t s_mask[kMaxDomains];
   const double* count = stats + 32 * 32;
   const int t = threadIdx.x;
@@ -230,29 +299,67 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
       const double pe = fmin(fmax(p, 0.01), 0.99), pn = fmin(fmax(1.0 - p, 0.01), 0.99);
       pm->w[sl][d] = (log(pe) - log(pn)) * inv_temp;
       s_logpn[sl][d] = log(pn);
+      s_pe[sl][d] = pe;
       if (p >= 0.5) atomicOr(&s_mask[d], 1u << sl);
     } else {
       pm->w[sl][d] = 0.0;
       s_logpn[sl][d] = 0.0;
+      s_pe[sl][d] = 0.0;
     }
   }
   __syncthreads();
+  const int n_pairs = pm->n_pairs;
+  const double rho = pm->pair_rho;
   if (t < kMaxDomains) {
     if (t < n_dom && count[t] >= min_count) {
       double N = 0.0;
       for (int d = 0; d < n_dom; ++d) N += count[d];
-      double b = log((count[t] + prior_pseudo) / (N + prior_pseudo * (double)n_dom));
+      const double logpi = log((count[t] + prior_pseudo) / (N + prior_pseudo * (double)n_dom));
+      double b = logpi;
       for (int sl = 0; sl < kSlots; ++sl) b += s_logpn[sl][t];
+      if (n_pairs > 0) b += log1p(-rho);  // singles keep 1 - rho of the prior
       pm->bias[t] = b * inv_temp;
       pm->dom_mask[t] = s_mask[t];
+      s_logpi[t] = logpi;
     } else {
       pm->bias[t] = -__builtin_inf();
       pm->dom_mask[t] = 0u;
+      s_logpi[t] = -__builtin_inf();
     }
   }
   if (t == 0) {
     pm->table_mask = 0xFFFFu;
     pm->mode = 0;
+  }
+  if (n_pairs <= 0) return;
+  // 2-fault columns (models/bayes.py with_pairs): noisy-OR likelihoods q = 1 - (1-p_a)(1-p_b),
+  // prior rho * pi_a pi_b / sum over the active pairs
+  __syncthreads();
+  if (t == 0) {
+    double z = 0.0;
+    for (int h = 0; h < n_pairs; ++h) {
+      const double pr = s_logpi[pm->pair_a[h]] + s_logpi[pm->pair_b[h]];
+      if (pr > -__builtin_inf()) z += exp(pr);
+    }
+    s_pnorm = log(z);
+  }
+  __syncthreads();
+  for (int h = t; h < n_pairs; h += 256) {
+    const int a = pm->pair_a[h], b = pm->pair_b[h];
+    const double pr = s_logpi[a] + s_logpi[b];
+    if (!(pr > -__builtin_inf())) {
+      for (int sl = 0; sl < kSlots; ++sl) pm->w2[sl][h] = 0.0;
+      pm->bias2[h] = -__builtin_inf();
+      continue;
+    }
+    double bb = log(rho) + pr - s_pnorm;
+    for (int sl = 0; sl < kSlots; ++sl) {
+      const double q0 = 1.0 - (1.0 - s_pe[sl][a]) * (1.0 - s_pe[sl][b]);
+      const double q = fmin(fmax(q0, 0.01), 0.99), qn = fmin(fmax(1.0 - q, 0.01), 0.99);
+      pm->w2[sl][h] = (log(q) - log(qn)) * inv_temp;
+      bb += log(qn);
+    }
+    pm->bias2[h] = bb * inv_temp;
   }
 }
 

@@ -21,7 +21,7 @@ from typing import Dict, Optional
 import numpy as np
 
 from ..collector import records
-from ..models.bayes import N_DOMAINS, NOMINAL, LinearPosteriorModel
+from ..models.bayes import MAX_PAIRS, N_DOMAINS, NOMINAL, LinearPosteriorModel
 from ..signals import catalog
 from . import load
 
@@ -45,20 +45,13 @@ def model_arrays_np(model: LinearPosteriorModel):
             np.asarray(model.thresholds, dtype=np.float32), dom_mask, table_mask, mode)
 
 
-def model_arrays(model: LinearPosteriorModel):
-    import torch
-
-    w, bias, mean, nominal, thr, dom_mask, table_mask, mode = model_arrays_np(model)
-    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))  # noqa: E731
-    return (t(w, np.float64), t(bias, np.float64), t(mean, np.float64), t(nominal, np.float64),
-            t(thr, np.float32), t(dom_mask, np.int64), table_mask, mode)
-
-
 MODEL_DTYPE = np.dtype([
     ("w", "<f8", (16, 16)), ("bias", "<f8", (16,)), ("mean", "<f8", (16,)), ("nominal", "<f8", (16,)),
     ("thr", "<f4", (16,)), ("dom_mask", "<u4", (16,)), ("table_mask", "<u4"), ("mode", "<i4"),
+    ("n_pairs", "<i4"), ("_pad", "<i4"), ("pair_rho", "<f8"), ("w2", "<f8", (16, MAX_PAIRS)),
+    ("bias2", "<f8", (MAX_PAIRS,)), ("pair_a", "u1", (MAX_PAIRS,)), ("pair_b", "u1", (MAX_PAIRS,)),
 ])
-assert MODEL_DTYPE.itemsize == 2568  # == sizeof(mislo::PosteriorModel)
+assert MODEL_DTYPE.itemsize == 9208  # == sizeof(mislo::PosteriorModel)
 
 
 def model_bytes(model: LinearPosteriorModel) -> np.ndarray:
@@ -73,6 +66,15 @@ def model_bytes(model: LinearPosteriorModel) -> np.ndarray:
     rec["dom_mask"][0] = dom_mask.astype(np.uint32)
     rec["table_mask"][0] = table_mask
     rec["mode"][0] = mode
+    rec["bias2"][0] = -np.inf
+    if model.pairs is not None:
+        P = len(model.pairs)
+        rec["n_pairs"][0] = P
+        rec["pair_rho"][0] = model.pair_rho
+        rec["w2"][0][:, :P] = model.pair_w
+        rec["bias2"][0][:P] = model.pair_b
+        rec["pair_a"][0][:P] = model.pairs[:, 0]
+        rec["pair_b"][0][:P] = model.pairs[:, 1]
     return rec.view(np.uint8)
 
 
@@ -89,8 +91,15 @@ def model_from_bytes(b: np.ndarray) -> LinearPosteriorModel:
     mode = "binary" if int(rec["mode"]) == 0 else "continuous"
     mean = np.array(rec["mean"], dtype=np.float64) if mode == "continuous" else None
     table = np.array([(tm >> s) & 1 for s in range(16)], dtype=np.float64) if mode == "binary" else None
-    return LinearPosteriorModel("image", w[:, :D].copy(), bias[:D].copy(), mask, mode,
-                                np.array(rec["thr"], dtype=np.float64), mean, table)
+    m = LinearPosteriorModel("image", w[:, :D].copy(), bias[:D].copy(), mask, mode,
+                             np.array(rec["thr"], dtype=np.float64), mean, table)
+    P = int(rec["n_pairs"])
+    if P:
+        m.pair_w = np.array(rec["w2"], dtype=np.float64)[:, :P].copy()
+        m.pair_b = np.array(rec["bias2"], dtype=np.float64)[:P].copy()
+        m.pairs = np.stack([np.array(rec["pair_a"][:P]), np.array(rec["pair_b"][:P])], axis=1).astype(np.int64)
+        m.pair_rho = float(rec["pair_rho"])
+    return m
 
 
 def decode_debug(dbg: np.ndarray, misc: np.ndarray, n_spans: int, n_events: int) -> Dict[str, int]:
@@ -209,7 +218,7 @@ class KernelHarness:
     # ---------------------------------------------------------------------------------
     def set_model(self, model: LinearPosteriorModel) -> None:
         with self.torch.cuda.device(self.device):
-            self.eng.set_model(*model_arrays(model))
+            self.eng.set_model_bytes(self.torch.from_numpy(model_bytes(model).copy()))
 
     def set_join_params(self, window_ms=2000.0, threshold=0.7, fanout=3, group_mode=1):
         self.eng.set_join_params(window_ms, threshold, fanout, group_mode)

@@ -95,7 +95,7 @@ class CpuWindowEngine:
             gsum, gcnt = reduce_groups(gsum, gcnt)
         feat = oracle.group_features(gsum, gcnt).astype(np.float64)
         post = self.model.posteriors(feat)
-        pred = np.argmax(self.model.logits(feat), axis=1) if n_groups else np.zeros(0, dtype=np.int64)
+        pred = self.model.predict(feat) if n_groups else np.zeros(0, dtype=np.int64)
         conf = np.zeros((16, 16), dtype=np.int64)
         stats = SufficientStats()
         if labels is not None and n_groups:
@@ -272,8 +272,7 @@ class CpuRingEngine:
         evbits = np.zeros((G, 16), np.uint32)
         if G and self.model is not None:
             post[:, :D] = self.model.posteriors(f64)
-            lg = self.model.logits(f64)
-            pred = np.argmax(lg, axis=1).astype(np.int32)
+            pred = self.model.predict(f64).astype(np.int32)
             gconf = post[np.arange(G), pred]
             evbits[:, :D] = self.model.evidence_bits(f64)
         conf = np.zeros((16, 16), dtype=np.int64)

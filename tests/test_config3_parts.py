@@ -122,3 +122,48 @@ def test_faultinject_emit_ring_writes_probe_records_for_the_connection():
 
 def test_faultinject_rejects_non_kernel_signal(capsys):
     assert faultinject.main(["--emit-ring", "/x", "--signal", "not_a_signal"]) == 2
+
+
+def test_psi_memory_stall_becomes_reclaim_records(tmp_path):
+    """Memory stall time (PSI) growth per interval -> mem_reclaim_latency_ms records of the
+    watched processes; the pod's cgroup v2 file wins over the node's."""
+    (tmp_path / "pressure").mkdir()
+    node = tmp_path / "pressure" / "memory"
+    node.write_text("some avg10=0.00 avg60=0.00 avg300=0.00 total=1000\nfull avg10=0.00 avg60=0.00 avg300=0.00 total=0\n")
+    write_schedstat(tmp_path, 100, 100, 1, 1, 1)
+    (tmp_path / "100" / "cgroup").write_text("0::/\n")
+    s = procfs.SchedstatSampler(lambda: {100: 4}, lambda u: len(u), proc_root=str(tmp_path))
+    assert procfs.psi_available(str(tmp_path))
+    assert len(s.sample()) == 0
+    node.write_text("some avg10=1.00 avg60=0.00 avg300=0.00 total=6000\nfull avg10=0.00 avg60=0.00 avg300=0.00 total=0\n")
+    ev = s.sample()
+    assert len(ev) == 1 and int(ev[0]["signal_type"]) == procfs.MEM_RECLAIM_TYPE
+    assert (int(ev[0]["value"]), int(ev[0]["pid"]), int(ev[0]["pod_id"])) == (5_000_000, 100, 4)
+    assert len(s.sample()) == 0  # no growth, no record
+    cg = tmp_path / "cg" / "kubepods" / "podx"
+    cg.mkdir(parents=True)
+    (cg / "memory.pressure").write_text("some avg10=0.00 avg60=0.00 avg300=0.00 total=7\n")
+    (tmp_path / "100" / "cgroup").write_text("0::/kubepods/podx\n")
+    assert procfs.psi_path(100, str(tmp_path), str(tmp_path / "cg")) == str(cg / "memory.pressure")
+    assert procfs.read_psi_total_us(str(cg / "memory.pressure")) == 7
+
+
+def test_faultinject_fault_profile_emits_every_kernel_signal_of_the_fault():
+    from llm_slo_ebpf_toolkit_amd.collector import bpf
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+    from llm_slo_ebpf_toolkit_amd.signals.generator import FAULT_OVERRIDES
+
+    rt = load()
+    prefix = f"/mislo-fp-{os.getpid()}"
+    ring, _u, _s = bpf.create_rings(bpf.RingNames.of(prefix), 1 << 16, 1024, 1024)
+    ring.cfg_set(rt.CFG_EPOCH, (1_700_000_000_000_000_000) & ~3)
+    assert faultinject.main(["--emit-ring", prefix, "--fault", "network_partition", "--pod-id", "3", "--conn",
+                             "51000:6333:127.0.0.1,51002:6333:127.0.0.1", "--rate", "1000", "--duration", "0.01"]) == 0
+    ev, defs, _d, _b = R.unframe(ring.data_view()[:ring.producer_pos].copy())
+    types = ev.view(np.uint32).reshape(-1, 4)[:, 1] & 0xFF
+    want = {catalog.BY_NAME[n].kernel_type for n in FAULT_OVERRIDES["network_partition"]}
+    assert set(types.tolist()) == want and len(ev) == 10 * len(want)
+    ctx = [r for r in defs.view(np.uint32).reshape(-1, 4) if (r[1] & 0xFF) == R.DEF_CTX]
+    assert {int(r[0]) for r in ctx} == {R.conn32(R.conn_hash(p, 6333, _ipv4("127.0.0.1"))) for p in (51000, 51002)}
+    assert faultinject.main(["--emit-ring", prefix, "--fault", "no_such_fault"]) == 2

@@ -81,7 +81,7 @@ def _check(args):
                               "metrics_bind": "", "output": "stdout"}))
     a.o.model_path = os.path.join(ROOT, SHIPPED_MODEL)
     model, image, meta = a._load_model()  # the model file the image ships loads
-    assert meta["name"] == "bayes_learned" and image.size == 2568
+    assert meta["name"] == "bayes_learned" and image.size == 9208
     a.close()
 
 

@@ -364,3 +364,53 @@ def test_soft_label_statistics_temperature_refit_and_scoring():
     np.testing.assert_array_equal(pred_dev, np.argmax(model.logits(f.astype(np.float64)), axis=1))
     assert ref55_report(fx, dev) == ref55_report(fx, host_scorer(model))
     pipe.eng.close()
+
+
+@pytest.mark.gpu
+def test_two_fault_refit_and_marginals_match_the_host_model():
+    """2-fault posterior on the device: the image carries the pair structure, k_refit_nb
+    rebuilds the noisy-OR pair columns from the statistics (bayes.with_pairs), and the posterior
+    kernel's per-domain marginals / argmax equal the host model's; REF's 55 rows score the same."""
+    from llm_slo_ebpf_toolkit_amd.models.bayes import SufficientStats, label_code, soft_labels, with_pairs
+    from llm_slo_ebpf_toolkit_amd.models.train import ref55_report, host_scorer
+    from llm_slo_ebpf_toolkit_amd.ops.engine import MODEL_DTYPE, model_bytes
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+
+    wins, gen = windows(n_win=3, seed=61)
+    imgs = build_replay_images(wins)
+    pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", user_cap=4096)
+    rb, user, spans = rings("pairs")
+    src = RingWindowSource(pipe, rb, user, spans)
+    pipe.eng.set_pods(*pod_meta(gen))
+    host = SufficientStats()
+    rng = np.random.default_rng(7)
+    for img in imgs:
+        codes = np.array([label_code(int(l), [int(l), int(rng.integers(0, 5))] if rng.random() < 0.5 else [])
+                          for l in img.labels], dtype=np.int32)
+        k = src.stage(feed(img, rb, user, spans), img.n_groups, codes)["k"]
+        host.add(pipe.results(k, img.n_groups)["feat"].astype(np.float64), soft_labels(codes))
+    src.drain()
+    st = pipe.state()[0]["stats_acc"]
+    T, rho = 2.5, 0.3
+    model = with_pairs(NaiveBayes.learned(host, seed=42, temperature=T, min_count=1.0), rho, T)
+    pipe.eng.restore(st, model_bytes(model), len(imgs))
+    pipe.eng.set_refit(2.0, 1.0, 1.0 / T, 1.0)
+    pipe.eng.refit_now()
+    dev_img = np.frombuffer(np.asarray(pipe.eng.model_bytes(), dtype=np.uint8).tobytes(), dtype=MODEL_DTYPE)[0]
+    ref_img = np.frombuffer(model_bytes(model).tobytes(), dtype=MODEL_DTYPE)[0]
+    assert int(dev_img["n_pairs"]) == len(model.pairs)
+    np.testing.assert_allclose(dev_img["w2"], ref_img["w2"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(dev_img["bias2"], ref_img["bias2"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(dev_img["bias"], ref_img["bias"], rtol=1e-9, atol=1e-12)
+
+    def dev(feat):
+        r = pipe.eng.score(np.ascontiguousarray(feat, dtype=np.float32), None)
+        return r["post"][:, :10], r["pred"]
+
+    f = np.random.default_rng(4).uniform(0, 300, (48, 16)).astype(np.float32)
+    p_dev, pred_dev = dev(f)
+    np.testing.assert_allclose(p_dev, model.posteriors(f.astype(np.float64)), rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(pred_dev, model.predict(f.astype(np.float64)))
+    fx = os.path.join(os.path.dirname(__file__), "fixtures", "ref_multi_fault_samples.jsonl")
+    assert ref55_report(fx, dev) == ref55_report(fx, host_scorer(model))
+    pipe.eng.close()

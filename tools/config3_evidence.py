@@ -1,0 +1,402 @@
+"""Config-3 evidence (BASELINE.json config 3: "demo/rag-service + vectordb on 1 GPU, cmd/faultinject
+TCP-retransmit + runqueue-delay, Bayesian 2-fault attribution"; REF scripts/chaos/
+run_fault_matrix.sh:46-94 runs the same scenarios against a kind cluster with netem / stress-ng).
+
+One box, one run:
+
+* workload: the demo RAG service (Llama backend on the GPU, demo/rag_service.py) pinned to two
+  CPUs, searching the vector-DB stub (demo/vectordb.py) over keep-alive TCP connections; its spans
+  go over OTLP/HTTP to the agent; closed-loop clients on keep-alive connections drive it;
+* agent: ``--engine gpu --source shm`` on the same GPU with the shipped learned 2-fault model
+  (config/models/mislo-learned.safetensors) and the unprivileged sampler on the RAG service's
+  process (collector/procfs.py: REAL run-queue delay from schedstat, REAL memory stall from PSI);
+  the rocprofiler tool in the RAG service for the GPU signals (llama backend). ``--model-signals``
+  names what these sources produce; the model sums the rest out;
+* faults, one phase each, with recovery phases between them:
+  - ``network_egress``: the vector DB stalls every response (the latency a lossy path adds) and
+    ``faultinject --emit-ring --fault network_partition`` writes the records the network probes
+    would emit for it -- REF's network-partition signal profile: retransmits, connect latency and
+    errors, DNS latency, TLS failures -- on the RAG service's vector-DB connections into the
+    agent's ring (no tc netem / BPF privileges on the box: the kernel's view of the fault is
+    injected at the record level, through the probes' own record path);
+  - ``cpu_throttle``: CPU burners pinned to the RAG service's CPUs (a real noisy neighbour; the
+    run-queue delay the agent sees is measured, not injected);
+  - ``compound``: both at once (REF's 2-fault case);
+* out: per phase, the agent's top-1 domain of the RAG service's incident group per window,
+  single-fault accuracy / macro-F1, compound partial accuracy and coverage@0.10 (REF's
+  definitions, pipeline.go:140-185), detection delay (fault onset -> arrival of the first correct
+  attribution in the agent's output, wall clock), TTFT p50 / p95 and the agent's CPU overhead.
+
+    python tools/config3_evidence.py --out gpurun_out/config3
+    python tools/config3_evidence.py --engine cpu --backend stub --phase-s 6 --recover-s 4  # CPU rehearsal
+"""
+
+from __future__ import annotations
+
+import argparse
+import http.client
+import json
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from config2_evidence import free_port, pct, wait_http  # noqa: E402
+
+POD_UID = "c0f13000-0000-4000-8000-000000000003"
+TOOL = os.path.join(ROOT, "llm_slo_ebpf_toolkit_amd", "probes", "rocprof", "libmislo_rocprof.so")
+NET_SIGNALS = ("dns_latency_ms", "tcp_retransmits_total", "connect_latency_ms", "connect_errors_total",
+               "tls_handshake_ms", "tls_handshake_fail_total")
+GPU_SIGNALS = ("gpu_queue_delay_ms", "hbm_pressure_pct", "xgmi_link_latency_us", "rccl_collective_ms")
+MODEL = os.path.join(ROOT, "config", "models", "mislo-learned.safetensors")
+BURN = "import os, sys\nos.sched_setaffinity(0, {int(sys.argv[1])})\nwhile True:\n    pass\n"
+EXPECT = {"baseline": set(), "fault_network": {"network_egress"}, "recovery_1": set(),
+          "fault_cpu": {"cpu_throttle"}, "recovery_2": set(), "fault_compound": {"network_egress", "cpu_throttle"},
+          "recovery_3": set()}
+
+
+class Client(threading.Thread):
+    """Closed-loop client on one keep-alive connection (one RAG-service handler thread, so one
+    vector-DB connection behind it)."""
+
+    def __init__(self, port: int, idx: int, phase, stop: threading.Event, rows: list, gap_s: float):
+        super().__init__(daemon=True)
+        self.port, self.idx, self.phase, self.stop, self.rows, self.gap = port, idx, phase, stop, rows, gap_s
+        self.conn_tuple = None
+
+    def run(self):
+        c = http.client.HTTPConnection("127.0.0.1", self.port, timeout=120)
+        i = 0
+        while not self.stop.is_set():
+            ph = self.phase()
+            body = json.dumps({"prompt": f"how does retrieval {i} of client {self.idx} use the vector index",
+                               "profile": "rag_medium", "max_tokens": 16, "request_id": f"c{self.idx}-{i}"})
+            t = time.time_ns()
+            try:
+                c.request("POST", "/chat", body=body, headers={"Content-Type": "application/json"})
+                out = json.loads(c.getresponse().read())
+            except (OSError, ValueError, http.client.HTTPException):
+                c.close()
+                c = http.client.HTTPConnection("127.0.0.1", self.port, timeout=120)
+                time.sleep(0.2)
+                continue
+            rc = out.get("retrieval_conn") or {}
+            if rc.get("client.port"):
+                self.conn_tuple = f"{rc['client.port']}:{rc['server.port']}:{rc['server.address']}"
+            self.rows.append({"phase": ph, "t_ns": t, "ttft_ms": out.get("ttft_ms"), "client": self.idx})
+            i += 1
+            time.sleep(self.gap)
+        c.close()
+
+
+class Tailer(threading.Thread):
+    """Reads the agent's attribution JSONL as it grows: (arrival wall-clock ns, row)."""
+
+    def __init__(self, path: str, stop: threading.Event):
+        super().__init__(daemon=True)
+        self.path, self.stop, self.rows = path, stop, []
+
+    def run(self):
+        buf, pos = "", 0
+        while True:
+            try:
+                with open(self.path) as fh:
+                    fh.seek(pos)
+                    data = fh.read()
+                    pos = fh.tell()
+            except OSError:
+                data = ""
+            now = time.time_ns()
+            buf += data
+            *lines, buf = buf.split("\n")
+            for ln in lines:
+                if ln.strip():
+                    try:
+                        self.rows.append((now, json.loads(ln)))
+                    except ValueError:
+                        pass
+            if self.stop.is_set() and not data:
+                return
+            time.sleep(0.1)
+
+
+def post(url: str, obj: dict) -> dict:
+    req = urllib.request.Request(url, data=json.dumps(obj).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    return json.loads(urllib.request.urlopen(req, timeout=10).read())
+
+
+def scrape_overhead(port: int) -> dict:
+    out = {}
+    try:
+        text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    except OSError:
+        return out
+    for ln in text.splitlines():
+        if ln.startswith(("llm_slo_agent_cpu", "llm_slo_agent_overhead", "llm_ebpf_agent_cpu")) and " " in ln:
+            k, v = ln.rsplit(" ", 1)
+            try:
+                out[k] = float(v)
+            except ValueError:
+                pass
+    return out
+
+
+COUNTERS = ("llm_ebpf_probe_events_total{", "llm_slo_agent_correlation_pairs_total{", "llm_slo_agent_gpu_window_events_total",
+            "llm_slo_agent_dropped_events_total{")
+
+
+def scrape_counters(port: int) -> dict:
+    """Probe events by signal and status, join outcomes, drops: diffed per phase."""
+    out = {}
+    try:
+        text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    except OSError:
+        return out
+    for ln in text.splitlines():
+        if ln.startswith(COUNTERS) and " " in ln:
+            k, v = ln.rsplit(" ", 1)
+            try:
+                out[k] = float(v)
+            except ValueError:
+                pass
+    return out
+
+
+def score(phases, attrs, window_ms: float, service: str = "rag-service") -> dict:
+    """Per-phase top-1 per window of the service's incident group (windows without an attribution
+    count as ``none``), accuracy, macro-F1 over the single-fault + healthy phases, compound
+    partial / coverage@0.10, detection delay."""
+    win = window_ms * 1e6
+    mine = [(arr, r) for arr, r in attrs if r.get("service") == service]
+
+    def t_of(r):
+        return int(r["incident_id"].split("-")[1])
+
+    out = {"phases": {}}
+    truth, pred = [], []
+    for name, t0, t1 in phases:
+        exp = EXPECT[name]
+        # windows wholly inside the phase: cut time t with (t - window, t] inside [t0, t1]
+        rows = [r for _a, r in mine if t0 + win <= t_of(r) <= t1]
+        n_win = max(1, int((t1 - t0 - win) // win) + 1)
+        tops = {}
+        for r in rows:
+            tops[r["predicted_fault_domain"]] = tops.get(r["predicted_fault_domain"], 0) + 1
+        tops["none"] = max(0, n_win - len(rows))
+        d = {"windows": n_win, "attributed": len(rows), "top1": tops}
+        if len(exp) == 1:
+            (e,) = exp
+            d["accuracy"] = round(sum(r["predicted_fault_domain"] == e for r in rows) / n_win, 4)
+        elif not exp:
+            d["false_positive_rate"] = round(sum(r["predicted_fault_domain"] not in ("unknown",) for r in rows) / n_win, 4)
+        else:
+            part = cov = 0.0
+            for r in rows:
+                hyp = {h["domain"] for h in r.get("fault_hypotheses", []) if h["posterior"] >= 0.10}
+                hyp.add(r["predicted_fault_domain"])
+                part += r["predicted_fault_domain"] in exp
+                cov += len(exp & hyp) / len(exp)
+            d["partial_accuracy"] = round(part / n_win, 4)
+            d["coverage_at_0.10"] = round(cov / n_win, 4)
+        if len(exp) <= 1:
+            label = next(iter(exp)) if exp else "unknown"
+            got = {t_of(r): r["predicted_fault_domain"] for r in rows}
+            for k in range(n_win):
+                truth.append(label)
+                # a healthy window without an incident is a correct "unknown"
+                pred.append(next((v for t, v in got.items() if t0 + win * (k + 1) <= t < t0 + win * (k + 2)),
+                                 "unknown" if not exp else "none"))
+        if exp:
+            hits = [(arr, t_of(r)) for arr, r in mine if t_of(r) > t0 and r["predicted_fault_domain"] in exp
+                    and t_of(r) <= t1 + 2 * win]
+            if hits:
+                arr, tw = min(hits, key=lambda x: x[0])
+                d["detection_delay_s"] = round((arr - t0) / 1e9, 3)
+                d["first_correct_window_end_s"] = round((tw - t0) / 1e9, 3)
+        out["phases"][name] = d
+    labels = sorted(set(truth))
+    f1s = {}
+    for lab in labels:
+        tp = sum(t == lab and p == lab for t, p in zip(truth, pred))
+        fp = sum(t != lab and p == lab for t, p in zip(truth, pred))
+        fn = sum(t == lab and p != lab for t, p in zip(truth, pred))
+        f1s[lab] = round(2 * tp / (2 * tp + fp + fn), 4) if tp else 0.0
+    out["single_fault_f1"] = f1s
+    out["single_fault_macro_f1"] = round(sum(f1s.values()) / len(f1s), 4) if f1s else None
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/config3")
+    ap.add_argument("--engine", default="gpu", choices=("gpu", "cpu"))
+    ap.add_argument("--backend", default="llama", choices=("llama", "stub"))
+    ap.add_argument("--preset", default="1b")
+    ap.add_argument("--phase-s", type=float, default=15.0)
+    ap.add_argument("--recover-s", type=float, default=8.0)
+    ap.add_argument("--clients", type=int, default=2)
+    ap.add_argument("--burners-per-cpu", type=int, default=4)
+    ap.add_argument("--delay-ms", type=float, default=150.0, help="vector-DB stall per response in network faults")
+    ap.add_argument("--retrans-rate", type=float, default=20.0, help="fault-profile record sets per second")
+    ap.add_argument("--ttft-slo-ms", type=float, default=400.0)
+    ap.add_argument("--window-ms", type=int, default=1000)
+    ap.add_argument("--model-path", default=MODEL)
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    from llm_slo_ebpf_toolkit_amd.collector import bpf
+
+    cpus = sorted(os.sched_getaffinity(0))
+    victim = cpus[:2]
+    rest = cpus[2:] or cpus
+    prefix = f"/mislo-cfg3-{os.getpid()}"
+    names = bpf.RingNames.of(prefix)
+    rings = bpf.create_rings(names, 1 << 24, 1 << 18, 1 << 14)  # noqa: F841 - kept alive for the children
+    rx, mport, hport, vport = free_port(), free_port(), free_port(), free_port()
+    attr_path = os.path.join(a.out, "attributions.jsonl")
+    if os.path.exists(attr_path):
+        os.remove(attr_path)
+    log = open(os.path.join(a.out, "run.log"), "w")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
+
+    def pinned(cset):
+        return lambda: os.sched_setaffinity(0, set(cset))
+
+    vdb = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.vectordb", "--bind",
+                            f"127.0.0.1:{vport}"], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT,
+                           preexec_fn=pinned(rest))
+    rag_env = dict(env, OMP_NUM_THREADS=str(len(victim)), POD_UID=POD_UID, POD_NAME="rag-service-config3",
+                   OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces")
+    from llm_slo_ebpf_toolkit_amd.collector import procfs
+
+    observable = list(NET_SIGNALS) + ["runqueue_delay_ms"]
+    if procfs.psi_available():
+        observable.append("mem_reclaim_latency_ms")
+    gpu_tool = a.backend == "llama" and os.path.exists(TOOL)
+    if gpu_tool:  # GPU signals of the RAG service's own kernels (the agent's pod id 1: its first pod)
+        rag_env.update(ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1",
+                       MISLO_QUEUE_FLOOR_NS="200000")
+        observable += list(GPU_SIGNALS)
+    rag = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.rag_service", "--backend",
+                            a.backend, "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", "",
+                            "--vectordb-url", f"http://127.0.0.1:{vport}"], cwd=ROOT, env=rag_env, stdout=log,
+                           stderr=subprocess.STDOUT, preexec_fn=pinned(victim))
+    agent = subprocess.Popen(
+        [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", a.engine, "--source", "shm",
+         "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
+         "--window-ms", str(a.window_ms), "--window-events", "65536", "--window-spans", "4096", "--window-groups", "8",
+         "--model-path", a.model_path, "--min-confidence", "0.3", "--halo-ms", "1500",
+         "--ttft-slo-ms", str(a.ttft_slo_ms), "--procfs-sampler", "--procfs-pods", f"{rag.pid}:{POD_UID}",
+         "--procfs-interval-ms", "100", "--model-signals", ",".join(observable),
+         "--output", "jsonl", "--output-path", attr_path],
+        cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
+    stop, tstop = threading.Event(), threading.Event()
+    rows: list = []
+    cur = {"phase": "warmup"}
+    clients = []
+    burners: list = []
+    inj = None
+    tailer = Tailer(attr_path, tstop)
+    phases = []
+    overhead = {}
+    counters: dict = {}
+    try:
+        wait_http(f"http://127.0.0.1:{vport}/healthz", vdb, 120)
+        wait_http(f"http://127.0.0.1:{hport}/healthz", rag, 300)
+        wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 240)
+        tailer.start()
+        clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05) for i in range(a.clients)]
+        for c in clients:
+            c.start()
+        t_w = time.time()
+        while time.time() - t_w < 60 and (sum(r["phase"] == "warmup" for r in rows) < 4 * a.clients
+                                         or any(c.conn_tuple is None for c in clients)):
+            time.sleep(0.2)
+        conns = ",".join(sorted({c.conn_tuple for c in clients if c.conn_tuple}))
+        print(f"[config3] ready; rag-service pid {rag.pid} on cpus {victim}; vector-DB connections {conns}", flush=True)
+        plan = [("baseline", a.phase_s), ("fault_network", a.phase_s), ("recovery_1", a.recover_s),
+                ("fault_cpu", a.phase_s), ("recovery_2", a.recover_s), ("fault_compound", a.phase_s),
+                ("recovery_3", a.recover_s)]
+        for name, dur in plan:
+            exp = EXPECT[name]
+            t0 = time.time_ns()
+            cur["phase"] = name
+            m0 = scrape_counters(mport)
+            if "network_egress" in exp:
+                post(f"http://127.0.0.1:{vport}/fault", {"delay_ms": a.delay_ms})
+                inj = subprocess.Popen(
+                    [sys.executable, "-m", "llm_slo_ebpf_toolkit_amd.cli.faultinject", "--emit-ring", prefix,
+                     "--fault", "network_partition", "--pod-uid", POD_UID, "--agent", f"http://127.0.0.1:{mport}",
+                     "--conn", conns, "--rate", str(a.retrans_rate), "--duration", str(dur)],
+                    cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
+            if "cpu_throttle" in exp:
+                burners = [subprocess.Popen([sys.executable, "-c", BURN, str(c)], cwd=ROOT, env=env,
+                                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                           for c in victim for _ in range(a.burners_per_cpu)]
+            time.sleep(dur)
+            if inj is not None:
+                inj.wait(30)
+                inj = None
+            if "network_egress" in exp:
+                post(f"http://127.0.0.1:{vport}/fault", {"delay_ms": 0})
+            for b in burners:
+                b.kill()
+                b.wait(10)
+            burners = []
+            t1 = time.time_ns()
+            phases.append((name, t0, t1))
+            m1 = scrape_counters(mport)
+            counters[name] = {k: v - m0.get(k, 0.0) for k, v in m1.items() if v - m0.get(k, 0.0)}
+            ph = [r["ttft_ms"] for r in rows if r["phase"] == name and r["ttft_ms"] is not None]
+            print(f"[config3] {name}: {len(ph)} requests, TTFT p50 {pct(ph, .5)} ms p95 {pct(ph, .95)} ms", flush=True)
+        time.sleep(3 * a.window_ms / 1000.0)  # the last windows' attributions
+        overhead = scrape_overhead(mport)
+    finally:
+        stop.set()
+        for b in burners + ([inj] if inj is not None else []):
+            if b.poll() is None:
+                b.kill()
+        for c in clients:
+            c.join(30)
+        for p in (rag, vdb, agent):
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+                try:
+                    p.wait(60)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+        tstop.set()
+        if tailer.is_alive():
+            tailer.join(10)
+        log.close()
+    with open(os.path.join(a.out, "requests.jsonl"), "w") as f:
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
+    res = score(phases, tailer.rows, a.window_ms)
+    res["ttft_ms"] = {n: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
+                      for n, _t0, _t1 in phases for v in [[r["ttft_ms"] for r in rows if r["phase"] == n]]}
+    res["agent_overhead_metrics"] = overhead
+    res["agent_counters_by_phase"] = counters
+    res["setup"] = {"engine": a.engine, "backend": a.backend, "preset": a.preset, "model": os.path.relpath(a.model_path, ROOT),
+                    "victim_cpus": victim, "burners_per_cpu": a.burners_per_cpu, "vectordb_delay_ms": a.delay_ms,
+                    "network_record_sets_per_s": a.retrans_rate, "observable_signals": observable,
+                    "rocprof_tool": gpu_tool, "window_ms": a.window_ms, "phase_s": a.phase_s,
+                    "recover_s": a.recover_s, "clients": a.clients,
+                    "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "
+                                     "injected on its connections via faultinject --emit-ring --fault",
+                    "cpu_fault": "pinned CPU burners; run-queue delay measured by the schedstat sampler"}
+    res["exit"] = {"agent": agent.returncode, "rag": rag.returncode, "vectordb": vdb.returncode}
+    with open(os.path.join(a.out, "summary.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
