@@ -81,6 +81,14 @@ def load_samples(scenario: str, input_path: str = "") -> List[FaultSample]:
     return [build_sample(scenario, expected, i, base) for i in range(12)]
 
 
+def detected_accelerator() -> str:
+    """What this host has, without initialising HIP: the GPUs the amdgpu driver exposes."""
+    from ..parallel.numa import visible_gpu_count
+
+    n = visible_gpu_count()
+    return f"{n} x AMD Instinct GPU (amdgpu)" if n else "none (CPU only)"
+
+
 def one_vs_rest_rates(actual: Sequence[str], predicted: Sequence[str]) -> Dict[str, float]:
     labels = sorted(set(actual) | set(predicted))
     fprs, fnrs = [], []
@@ -178,7 +186,7 @@ def generate_artifacts(out_dir: str, scenario: str = "provider_throttle", worklo
                "workload_profile": workload, "attribution_mode": mode,
                "environment": {"kubernetes_version": os.environ.get("K8S_VERSION", "n/a"),
                                "kernel_version": os.uname().release, "node_count": 1,
-                               "accelerator": os.environ.get("MISLO_ACCELERATOR", "AMD Instinct MI355X (gfx950)")},
+                               "accelerator": os.environ.get("MISLO_ACCELERATOR") or detected_accelerator()},
                "metrics": metrics}
     with open(os.path.join(out_dir, "attribution_summary.json"), "w") as fh:
         json.dump(summary, fh, indent=2)

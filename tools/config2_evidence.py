@@ -10,9 +10,11 @@ On one GPU, in one run:
 * a baseline phase, then a fault phase. In the fault phase a GPU burner process (back-to-back
   large GEMMs on the same GPU) contends with the LLM, then the fault is lifted;
 * out: per-phase TTFT (p50 / p95, from the service's own responses) and the agent's
-  IncidentAttributions for the service, with the fault phase's predicted domain and evidence.
+  IncidentAttributions for the service, with the fault phase's predicted domain and evidence,
+  and the measured detection delay: the burner's first GEMM on the GPU (fault onset) -> the
+  arrival of the first gpu_contention attribution of the service in the agent's output.
 
-    python tools/config2_evidence.py --out gpurun_out/config2
+    python tools/config2_evidence.py --out gpurun_out/config2     # 7B preset, TTFT SLO 800 ms
 """
 
 from __future__ import annotations
@@ -24,6 +26,7 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 import urllib.request
 
@@ -37,13 +40,45 @@ import sys, time, torch
 a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
 b = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
 end = time.time() + float(sys.argv[1])
-print("burner on", flush=True)
+(a @ b).sum().item()  # first GEMM done: the contention starts now
+print("burner on", time.time_ns(), flush=True)
 while time.time() < end:
     for _ in range(8):
         a = (a @ b).clamp_(-1, 1)
     torch.cuda.synchronize()
 print("burner off", flush=True)
 """
+
+
+class Tailer(threading.Thread):
+    """Reads the agent's attribution JSONL as it grows: (arrival wall-clock ns, row)."""
+
+    def __init__(self, path: str, stop: threading.Event):
+        super().__init__(daemon=True)
+        self.path, self.stop, self.rows = path, stop, []
+
+    def run(self):
+        buf, pos = "", 0
+        while True:
+            try:
+                with open(self.path) as fh:
+                    fh.seek(pos)
+                    data = fh.read()
+                    pos = fh.tell()
+            except OSError:
+                data = ""
+            now = time.time_ns()
+            buf += data
+            *lines, buf = buf.split("\n")
+            for ln in lines:
+                if ln.strip():
+                    try:
+                        self.rows.append((now, json.loads(ln)))
+                    except ValueError:
+                        pass
+            if self.stop.is_set() and not data:
+                return
+            time.sleep(0.1)
 
 
 def free_port() -> int:
@@ -108,8 +143,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/config2")
     ap.add_argument("--requests", type=int, default=24, help="requests per phase")
-    ap.add_argument("--preset", default="1b")
-    ap.add_argument("--ttft-slo-ms", type=float, default=100.0, help="the agent's TTFT SLO (burn rate per incident)")
+    ap.add_argument("--preset", default="7b", help="Llama preset of the workload (BASELINE config 2: 7B)")
+    ap.add_argument("--ttft-slo-ms", type=float, default=800.0, help="the agent's TTFT SLO (BASELINE config 2: 800 ms)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     from llm_slo_ebpf_toolkit_amd.collector import bpf
@@ -137,18 +172,23 @@ def main() -> int:
     burner = None
     rows = []
     counters = {}
+    onset_ns = None
+    tstop = threading.Event()
+    tailer = Tailer(attr_path, tstop)
     try:
         wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 180)
         wait_http(f"http://127.0.0.1:{hport}/healthz", llm, 300)
         print("[config2] agent and llm ready", flush=True)
+        tailer.start()
         for i in range(4):  # warm the model (first-request compilation / allocation)
             chat(hport, i, "warmup")
         phases = [("baseline", False), ("fault_gpu_contention", True), ("recovery", False)]
         for phase, fault in phases:
             if fault:
-                burner = subprocess.Popen([sys.executable, "-c", BURNER, "600"], cwd=ROOT, env=env, stdout=log,
-                                          stderr=subprocess.STDOUT)
-                time.sleep(3.0)
+                burner = subprocess.Popen([sys.executable, "-c", BURNER, "600"], cwd=ROOT, env=env,
+                                          stdout=subprocess.PIPE, stderr=log, text=True)
+                ln = burner.stdout.readline()  # "burner on <ns>" once its first GEMM finished
+                onset_ns = int(ln.split()[-1]) if ln.startswith("burner on") else time.time_ns()
             t_phase = time.time_ns()
             m0 = scrape(mport)
             for i in range(a.requests):
@@ -177,6 +217,9 @@ def main() -> int:
                 agent.wait(60)
             except subprocess.TimeoutExpired:
                 agent.kill()
+        tstop.set()
+        if tailer.is_alive():
+            tailer.join(10)
         log.close()
     with open(os.path.join(a.out, "ttft.jsonl"), "w") as f:
         for r in rows:
@@ -201,7 +244,15 @@ def main() -> int:
         if x["predicted_fault_domain"] != "unknown":
             d["evidence"].append({"domain": x["predicted_fault_domain"], "confidence": round(x["confidence"], 3),
                                   "evidence": x["evidence"], "burn_rate": x["slo_impact"]["burn_rate"]})
+    # detection delay: fault onset -> arrival of the first gpu_contention attribution of the service
+    det = None
+    if onset_ns is not None:
+        hits = [arr for arr, x in tailer.rows if x.get("service") == "rag-service"
+                and x.get("predicted_fault_domain") == "gpu_contention" and int(x["incident_id"].split("-")[1]) > onset_ns]
+        det = {"onset_ns": onset_ns, "first_attribution_arrival_ns": min(hits) if hits else None,
+               "detection_delay_s": round((min(hits) - onset_ns) / 1e9, 3) if hits else None}
     summary = {
+        "preset": a.preset, "ttft_slo_ms": a.ttft_slo_ms, "detection": det,
         "ttft_ms": {p: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
                     for p in ("baseline", "fault_gpu_contention", "recovery")
                     for v in [[r["ttft_ms"] for r in rows if r["phase"] == p]]},

@@ -47,7 +47,7 @@ import urllib.request
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-from config2_evidence import free_port, pct, wait_http  # noqa: E402
+from config2_evidence import Tailer, free_port, pct, wait_http  # noqa: E402
 
 POD_UID = "c0f13000-0000-4000-8000-000000000003"
 TOOL = os.path.join(ROOT, "llm_slo_ebpf_toolkit_amd", "probes", "rocprof", "libmislo_rocprof.so")
@@ -93,37 +93,6 @@ class Client(threading.Thread):
             i += 1
             time.sleep(self.gap)
         c.close()
-
-
-class Tailer(threading.Thread):
-    """Reads the agent's attribution JSONL as it grows: (arrival wall-clock ns, row)."""
-
-    def __init__(self, path: str, stop: threading.Event):
-        super().__init__(daemon=True)
-        self.path, self.stop, self.rows = path, stop, []
-
-    def run(self):
-        buf, pos = "", 0
-        while True:
-            try:
-                with open(self.path) as fh:
-                    fh.seek(pos)
-                    data = fh.read()
-                    pos = fh.tell()
-            except OSError:
-                data = ""
-            now = time.time_ns()
-            buf += data
-            *lines, buf = buf.split("\n")
-            for ln in lines:
-                if ln.strip():
-                    try:
-                        self.rows.append((now, json.loads(ln)))
-                    except ValueError:
-                        pass
-            if self.stop.is_set() and not data:
-                return
-            time.sleep(0.1)
 
 
 def post(url: str, obj: dict) -> dict:
