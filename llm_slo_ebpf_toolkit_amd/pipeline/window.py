@@ -333,11 +333,13 @@ class RingWindowSource:
             cfg_set = lambda i, v: ring.cfg_set(i, v)  # noqa: E731
         self.cfg_set = cfg_set
         self.clock = records.EpochClock()
-        # page-lock the rings so windows DMA straight from them (the double-mapped BPF ring data
-        # is registered whole: a window that wraps is still one range)
+        # page-lock the rings so windows DMA straight from them. Only the first mapping of the
+        # double-mapped BPF ring data is registered (page-locking the second copy would count the
+        # same pages twice in the agent's RSS): a window that wraps is two DMA segments, placed
+        # back to back on the device, so a record split by the wrap is whole again there
         self.direct = {}
         if ring is not None:
-            self.direct["ring"] = pipe.eng.register_host(ring.data_address, 2 * ring.size)
+            self.direct["ring"] = pipe.eng.register_host(ring.data_address, ring.size)
             self.kpos = ring.consumer_pos
             self.kmask = ring.size - 1
         # user-space producers' records: 64-byte EVENT, 32-byte USER32 or 24-byte USER24, per ring
@@ -424,6 +426,15 @@ class RingWindowSource:
         """(BPF ring byte position, user-space records, spans) this source no longer needs."""
         return int(self.kernel_done), int(self.user_done), int(self.span_done)
 
+    def _kernel_segments(self, pos: int, nbytes: int) -> List[Tuple[int, int]]:
+        """[(address, bytes)] of BPF ring bytes [pos, pos + nbytes) in the first data mapping."""
+        idx = pos & self.kmask
+        first = min(nbytes, self.ring.size - idx)
+        out = [(self.ring.data_address + idx, first)]
+        if nbytes > first:
+            out.append((self.ring.data_address, nbytes - first))
+        return out
+
     def _ring_ranges(self, start: int, stop: int, rec: int, base: int, cap_pos: int, max_n: int):
         """[(address, bytes)] of records [start, stop) of a ring of ``cap_pos`` record slots."""
         n = max(0, min(stop - start, max_n))
@@ -455,16 +466,16 @@ class RingWindowSource:
                     self.late.append((pos + 24 * take, n - take))
                 if take:
                     k_ranges.append((pos, take))
-                    kern.append((self.ring.data_address + (pos & self.kmask), 24 * take))
+                    kern += self._kernel_segments(pos, 24 * take)
                     n_k += take
             span_b = cut.kernel - self.kpos
             if span_b % 24:
                 raise RuntimeError("BPF ring holds records of another size (the probes emit 16-byte records only)")
             take = min(span_b // 24, budget - n_k)
             self.carried += span_b // 24 - take
-            if take:  # one range: the data pages are mapped twice back to back
+            if take:
                 k_ranges.append((self.kpos, take))
-                kern.append((self.ring.data_address + (self.kpos & self.kmask), 24 * take))
+                kern += self._kernel_segments(self.kpos, 24 * take)
                 n_k += take
                 self.kpos += 24 * take
         user, n_u = [], 0

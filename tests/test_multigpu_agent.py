@@ -81,7 +81,7 @@ def _spec(r, world, tag, pods, port=0, engine="cpu"):
                       pods=pods, master=("127.0.0.1", port))
 
 
-def _run_pool(world, imgs, pods, tag):
+def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22):
     import socket
 
     from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerPool, merge_results
@@ -89,7 +89,7 @@ def _run_pool(world, imgs, pods, tag):
     from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut
 
     names = bpf.RingNames.of(tag)
-    ring, user, spans = bpf.create_rings(names, 1 << 22, 1 << 14, 1 << 12, user_rec=24)
+    ring, user, spans = bpf.create_rings(names, ring_bytes, 1 << 14, 1 << 12, user_rec=24)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -169,3 +169,18 @@ if __name__ == "__main__":
     with open(tmp_path / st[0]) as fh:
         state = json.load(fh)
     assert state["windows"] == 5 and state["burn"]["hist"]
+
+
+def test_windows_that_wrap_the_bpf_ring_equal_unwrapped_windows():
+    """Only the first mapping of the double-mapped BPF ring is page-locked: a window that wraps
+    goes as two DMA segments placed back to back, records split by the wrap included, and the
+    results equal those of the same windows in a ring that never wraps."""
+    wins, imgs, pods = _windows()
+    tag = f"/mislo-wr-{os.getpid()}"
+    big = _run_pool(1, imgs, pods, tag + "-a")
+    small = _run_pool(1, imgs, pods, tag + "-b", ring_bytes=1 << 17)  # the third window wraps
+    assert sum(im.framed.size for im in imgs) > (1 << 17)
+    for j, (a, b) in enumerate(zip(big, small)):
+        np.testing.assert_array_equal(a["packet"], b["packet"], err_msg=f"window {j}")
+        for key in ("feat", "pred", "sli", "evbits"):
+            np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
