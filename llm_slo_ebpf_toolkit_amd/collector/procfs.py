@@ -4,9 +4,10 @@ REF's min-capability mode keeps two signals (dns, tcp) and drops the scheduler o
 programs (/root/reference/docs/security/agent-min-capability-mode.md:1-35). The scheduler already
 accounts what ``runqueue_delay.bpf.c`` measures: ``/proc/<pid>/task/<tid>/schedstat`` holds each
 thread's on-CPU time, run-queue wait time and timeslice count, readable without privilege. The
-``SchedstatSampler`` turns their per-interval deltas into ``runqueue_delay_ms`` records -- the mean
-wait per timeslice of every thread that ran (the probe's per-switch delay averaged over the
-interval), above the probe's 100 us floor -- tagged with the process's pid and pod, and pushes
+``SchedstatSampler`` turns their per-interval deltas into ``runqueue_delay_ms`` records -- per
+process, its threads' run-queue wait over their timeslices in the interval (each timeslice is one
+wakeup-to-run the BPF probe would have timed, so this is the mean of the probe's per-switch
+delays for the process), above the probe's 100 us floor -- tagged with the pid and pod, and pushes
 them into the agent's user-space ring like the rocprofiler tool's records. The GPU window engine
 joins them to the pod's spans (pod + pid tier).
 
@@ -89,7 +90,7 @@ class SchedstatSampler:
         self._thr: Optional[threading.Thread] = None
 
     def sample(self, now_ns: Optional[int] = None) -> np.ndarray:
-        """One interval: EVENT records of the threads whose mean wait per timeslice crossed the floor."""
+        """One interval: EVENT records of the processes whose mean wait per timeslice crossed the floor."""
         now = int(now_ns if now_ns is not None else time.time_ns())
         rows, seen = [], set()
         for pid, pod in self.targets().items():
@@ -98,6 +99,7 @@ class SchedstatSampler:
                 tids = [int(t) for t in os.listdir(task) if t.isdigit()]
             except OSError:
                 continue
+            w_sum = s_sum = 0
             for tid in tids:
                 st = read_schedstat(os.path.join(task, str(tid), "schedstat"))
                 if st is None:
@@ -109,8 +111,11 @@ class SchedstatSampler:
                 if prev is None:
                     continue
                 dw, ds = st[1] - prev[0], st[2] - prev[1]
-                if ds > 0 and dw > 0 and dw // ds >= self.floor_ns:
-                    rows.append((pid, tid, pod, dw // ds))
+                if ds > 0 and dw >= 0:
+                    w_sum += dw
+                    s_sum += ds
+            if s_sum and w_sum // s_sum >= self.floor_ns:
+                rows.append((pid, pid, pod, w_sum // s_sum))
         for key in list(self._prev):
             if key not in seen:
                 del self._prev[key]

@@ -1,0 +1,156 @@
+"""Tensor-parallel LLM server for config 4 (BASELINE.json: "8xMI355X TP inference under
+RCCL-latency + CPU-steal injection").
+
+One process per GPU (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT from the launcher,
+torch.distributed over RCCL): every rank holds its tensor-parallel shard of the Llama model
+(parallel/tensor.py: two RCCL all-reduces per layer over xGMI). Rank 0 serves ``POST /chat`` and
+``GET /healthz``; each request's prompt goes to every rank with one broadcast, all ranks decode in
+lock step, rank 0 answers with the TTFT and exports the request's spans over OTLP (the same
+exporter and resource identity as the RAG demo, so the node agent joins the ranks' GPU signals --
+kernel queue delay, RCCL collective time, xGMI latency from the rocprofiler tool each rank loads --
+to the requests).
+
+    python -m llm_slo_ebpf_toolkit_amd.demo.tp_server --preset 7b --bind 127.0.0.1:8090  # under a launcher
+"""
+
+from __future__ import annotations
+
+import argparse
+import hashlib
+import http.server
+import json
+import os
+import sys
+import threading
+import time
+
+STOP = -1
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="tensor-parallel LLM server (config 4)")
+    ap.add_argument("--preset", default="7b")
+    ap.add_argument("--bind", default="127.0.0.1:8090")
+    ap.add_argument("--otlp-endpoint", default=os.environ.get("OTEL_EXPORTER_OTLP_TRACES_ENDPOINT", ""))
+    ap.add_argument("--max-new", type=int, default=16)
+    a = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    from ..contracts import semconv
+    from ..parallel.tensor import build_tp
+    from .rag_service import VOCAB, GpuTraceTag, SpanExporter, prompt_hash
+
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    model = build_tp(a.preset, rank, world, device=dev)
+    hdr = torch.zeros(2, dtype=torch.int64, device=dev)   # [prompt length | STOP, max_new]
+    buf = torch.zeros(256, dtype=torch.int64, device=dev)
+
+    def step(ids, max_new):
+        """One request on every rank (rank 0 calls it with the ids, the others get them)."""
+        if world > 1:
+            dist.broadcast(hdr, 0)
+            n = int(hdr[0].item())
+            if n == STOP:
+                return None
+            dist.broadcast(buf[:n], 0)
+            x = buf[:n].view(1, n).clone()
+            max_new = int(hdr[1].item())
+        else:
+            x = ids
+        return model.generate(x, max_new)
+
+    if rank != 0:
+        while step(None, 0) is not None:
+            pass
+        dist.destroy_process_group()
+        return 0
+
+    spans = SpanExporter(a.otlp_endpoint, service="llm-tp", resource={"llm.tp.world_size": world})
+    tag = GpuTraceTag()
+    lock = threading.Lock()
+    stats = {"requests": 0}
+
+    def chat(req):
+        prompt = (req.get("prompt") or "").strip() or "hello"
+        rid = req.get("request_id") or f"req-{time.time_ns()}"
+        max_new = max(1, min(int(req.get("max_tokens") or a.max_new), 128))
+        toks = [prompt_hash(w) % model.cfg.vocab for w in prompt.split()][:256] or [1]
+        trace = hashlib.blake2b(rid.encode(), digest_size=16).hexdigest()
+        root = hashlib.blake2b(f"{rid}/r".encode(), digest_size=8).hexdigest()
+        t0 = time.time_ns()
+        with lock:  # requests are serialised: every rank runs the same one
+            ids = torch.tensor([toks], dtype=torch.int64, device=dev)
+            if world > 1:
+                hdr[0], hdr[1] = len(toks), max_new
+                buf[:len(toks)] = ids[0]
+            tag.set(trace)
+            try:
+                r = step(ids, max_new)
+            finally:
+                tag.set("")
+        t1 = time.time_ns()
+        stats["requests"] += 1
+        spans.add([SpanExporter.span(trace, root, "", "chat.request", t0, t1, {
+            "request.id": rid, "llm.tp.world_size": world, semconv.ATTR_SLO_TTFT_MS: r["ttft_ms"],
+            semconv.ATTR_SLO_TOKENS_PER_SEC: r["tokens_per_s"]})])
+        return {"request_id": rid, "trace_id": trace, "ttft_ms": round(r["ttft_ms"], 3),
+                "tokens_per_sec": round(r["tokens_per_s"], 3), "tokens": [VOCAB[i % len(VOCAB)] for i in range(max_new)]}
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *x):
+            pass
+
+        def _json(self, code, obj):
+            b = json.dumps(obj).encode()
+            self.send_response(code)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(b)))
+            self.end_headers()
+            self.wfile.write(b)
+
+        def do_GET(self):
+            self._json(200 if self.path == "/healthz" else 404, {"status": "ok", "world": world, **stats})
+
+        def do_POST(self):
+            if self.path != "/chat":
+                self._json(404, {"error": "not found"})
+                return
+            n = int(self.headers.get("Content-Length") or 0)
+            try:
+                self._json(200, chat(json.loads(self.rfile.read(n) or b"{}")))
+            except (ValueError, KeyError) as exc:
+                self._json(400, {"error": str(exc)})
+
+    host, port = a.bind.rsplit(":", 1)
+    httpd = http.server.ThreadingHTTPServer((host, int(port)), H)
+    httpd.daemon_threads = True
+    th = threading.Thread(target=httpd.serve_forever, daemon=True)
+    th.start()
+    print(f"tp-server rank 0 of {world} listening on {a.bind}", flush=True)
+    import signal as _signal
+
+    done = threading.Event()
+    for s in (_signal.SIGTERM, _signal.SIGINT):
+        _signal.signal(s, lambda *_: done.set())
+    done.wait()
+    httpd.shutdown()
+    spans.flush()
+    if world > 1:
+        with lock:
+            hdr[0] = STOP
+            dist.broadcast(hdr, 0)
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -7,7 +7,7 @@
 // the value in fixed point by the probes' own rule, mislo_record.h mislo_milli; USER24 packs
 // pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
-//   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue            (ns)
+//   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue return     (ns)
 //   type 14 hbm_pressure_pct     the GPU's node-wide HBM use: amdgpu sysfs mem_info_vram_used /
 //                                mem_info_vram_total of the PCI device the process allocates on
 //                                (every process's allocations, not this one's), sampled on
@@ -293,10 +293,15 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
   return ROCPROFILER_STATUS_SUCCESS;
 }
 
-// Kernel dispatch ENQUEUE (host side) and COMPLETE (with device start/end timestamps).
+// Kernel dispatch ENQUEUE (host side) and COMPLETE (with device start/end timestamps). The
+// enqueue time is taken when the enqueue RETURNS (packet written, doorbell rung): from the
+// entry, a host thread preempted inside the enqueue (CPU contention on the launching thread)
+// counted as GPU queue delay (config-3 run: 926 "warning" queue delays while only the CPUs were
+// contended). From the exit the delay is the time the dispatch waited on the device: behind
+// earlier work of the queue or for compute units held by other work.
 void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
   if (rec.kind != ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH) return;
-  if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_ENTER) {
+  if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
     std::lock_guard<std::mutex> lk(g.mu);

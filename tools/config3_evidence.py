@@ -138,10 +138,11 @@ def scrape_counters(port: int) -> dict:
     return out
 
 
-def score(phases, attrs, window_ms: float, service: str = "rag-service") -> dict:
+def score(phases, attrs, window_ms: float, service: str = "rag-service", expect=None) -> dict:
     """Per-phase top-1 per window of the service's incident group (windows without an attribution
     count as ``none``), accuracy, macro-F1 over the single-fault + healthy phases, compound
     partial / coverage@0.10, detection delay."""
+    expect = EXPECT if expect is None else expect
     win = window_ms * 1e6
     mine = [(arr, r) for arr, r in attrs if r.get("service") == service]
 
@@ -151,7 +152,7 @@ def score(phases, attrs, window_ms: float, service: str = "rag-service") -> dict
     out = {"phases": {}}
     truth, pred = [], []
     for name, t0, t1 in phases:
-        exp = EXPECT[name]
+        exp = expect[name]
         # windows wholly inside the phase: cut time t with (t - window, t] inside [t0, t1]
         rows = [r for _a, r in mine if t0 + win <= t_of(r) <= t1]
         n_win = max(1, int((t1 - t0 - win) // win) + 1)
@@ -163,6 +164,9 @@ def score(phases, attrs, window_ms: float, service: str = "rag-service") -> dict
         if len(exp) == 1:
             (e,) = exp
             d["accuracy"] = round(sum(r["predicted_fault_domain"] == e for r in rows) / n_win, 4)
+            # over the windows that had an incident at all (a window in which no request of
+            # the service completed has no spans, so no incident to attribute)
+            d["accuracy_attributed"] = round(sum(r["predicted_fault_domain"] == e for r in rows) / max(1, len(rows)), 4)
         elif not exp:
             d["false_positive_rate"] = round(sum(r["predicted_fault_domain"] not in ("unknown",) for r in rows) / n_win, 4)
         else:
@@ -174,6 +178,8 @@ def score(phases, attrs, window_ms: float, service: str = "rag-service") -> dict
                 cov += len(exp & hyp) / len(exp)
             d["partial_accuracy"] = round(part / n_win, 4)
             d["coverage_at_0.10"] = round(cov / n_win, 4)
+            d["partial_accuracy_attributed"] = round(part / max(1, len(rows)), 4)
+            d["coverage_at_0.10_attributed"] = round(cov / max(1, len(rows)), 4)
         if len(exp) <= 1:
             label = next(iter(exp)) if exp else "unknown"
             got = {t_of(r): r["predicted_fault_domain"] for r in rows}
