@@ -155,12 +155,17 @@ class GpuTraceTag:
         return self._set is not None
 
     def set(self, trace_id: str) -> None:
+        from ..collector.otlp import trace_hash
+
+        self.set_hash(trace_hash(trace_id) if trace_id else 0)
+
+    def set_hash(self, h: int) -> None:
+        """The trace hash itself (another process computed it: a TP rank tags its shard's kernels
+        with the request rank 0 received)."""
         if not self._resolved:
             self._resolve()
         if self._set is not None:
-            from ..collector.otlp import trace_hash
-
-            self._set(trace_hash(trace_id) if trace_id else 0)
+            self._set(int(h) & 0xFFFFFFFFFFFFFFFF)
 
 
 class SpanExporter:

@@ -33,6 +33,7 @@ def main(argv=None) -> int:
     ap.add_argument("--bind", default="127.0.0.1:8090")
     ap.add_argument("--otlp-endpoint", default=os.environ.get("OTEL_EXPORTER_OTLP_TRACES_ENDPOINT", ""))
     ap.add_argument("--max-new", type=int, default=16)
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"), help="cpu: the gloo rehearsal (tests)")
     a = ap.parse_args(argv)
 
     import torch
@@ -44,16 +45,26 @@ def main(argv=None) -> int:
 
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if a.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    model = build_tp(a.preset, rank, world, device=dev)
-    hdr = torch.zeros(2, dtype=torch.int64, device=dev)   # [prompt length | STOP, max_new]
+        if a.device == "cuda":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    model = build_tp(a.preset, rank, world, device=dev, dtype=torch.bfloat16 if a.device == "cuda" else torch.float32)
+    hdr = torch.zeros(3, dtype=torch.int64, device=dev)   # [prompt length | STOP, max_new, trace hash]
     buf = torch.zeros(256, dtype=torch.int64, device=dev)
 
+    tag = GpuTraceTag()
+
     def step(ids, max_new):
-        """One request on every rank (rank 0 calls it with the ids, the others get them)."""
+        """One request on every rank (rank 0 calls it with the ids, the others get them). Every
+        rank tags its kernels with the request's trace, so the agent joins all shards' GPU
+        signals to the request."""
         if world > 1:
             dist.broadcast(hdr, 0)
             n = int(hdr[0].item())
@@ -62,9 +73,15 @@ def main(argv=None) -> int:
             dist.broadcast(buf[:n], 0)
             x = buf[:n].view(1, n).clone()
             max_new = int(hdr[1].item())
+            if rank:
+                tag.set_hash(int(hdr[2].item()))
         else:
             x = ids
-        return model.generate(x, max_new)
+        try:
+            return model.generate(x, max_new)
+        finally:
+            if rank:
+                tag.set_hash(0)
 
     if rank != 0:
         while step(None, 0) is not None:
@@ -72,8 +89,9 @@ def main(argv=None) -> int:
         dist.destroy_process_group()
         return 0
 
+    from ..collector.otlp import trace_hash
+
     spans = SpanExporter(a.otlp_endpoint, service="llm-tp", resource={"llm.tp.world_size": world})
-    tag = GpuTraceTag()
     lock = threading.Lock()
     stats = {"requests": 0}
 
@@ -88,7 +106,8 @@ def main(argv=None) -> int:
         with lock:  # requests are serialised: every rank runs the same one
             ids = torch.tensor([toks], dtype=torch.int64, device=dev)
             if world > 1:
-                hdr[0], hdr[1] = len(toks), max_new
+                th = trace_hash(trace)
+                hdr[0], hdr[1], hdr[2] = len(toks), max_new, th - (1 << 64) if th >= 1 << 63 else th
                 buf[:len(toks)] = ids[0]
             tag.set(trace)
             try:
