@@ -7,7 +7,7 @@
 // the value in fixed point by the probes' own rule, mislo_record.h mislo_milli; USER24 packs
 // pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
-//   type 13 gpu_queue_delay_ms   kernel dispatch: start - enqueue return     (ns)
+//   type 13 gpu_queue_delay_ms   kernel dispatch: start - max(enqueue return, queue predecessor end) (ns)
 //   type 14 hbm_pressure_pct     the GPU's node-wide HBM use: amdgpu sysfs mem_info_vram_used /
 //                                mem_info_vram_total of the PCI device the process allocates on
 //                                (every process's allocations, not this one's), sampled on
@@ -122,6 +122,7 @@ struct State {
     uint64_t ts, trace_h;
   };
   std::unordered_map<uint64_t, Enq> enqueue_ts;  // correlation id -> enqueue time, request trace
+  std::unordered_map<uint64_t, uint64_t> queue_end;  // HW queue -> latest end of a completed dispatch
   std::unordered_map<uint64_t, uint64_t> live_alloc;  // address -> bytes
   uint64_t live_bytes = 0;
   // node-wide HBM of the GPUs this process uses: agent handle -> the PCI device's VRAM counters
@@ -293,12 +294,17 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
   return ROCPROFILER_STATUS_SUCCESS;
 }
 
-// Kernel dispatch ENQUEUE (host side) and COMPLETE (with device start/end timestamps). The
-// enqueue time is taken when the enqueue RETURNS (packet written, doorbell rung): from the
-// entry, a host thread preempted inside the enqueue (CPU contention on the launching thread)
-// counted as GPU queue delay (config-3 run: 926 "warning" queue delays while only the CPUs were
-// contended). From the exit the delay is the time the dispatch waited on the device: behind
-// earlier work of the queue or for compute units held by other work.
+// Kernel dispatch ENQUEUE (host side) and COMPLETE (with device start/end timestamps).
+// gpu_queue_delay is the time a dispatch that COULD run waited for the device:
+//   start - max(enqueue return, end of the previous dispatch on the same HW queue).
+// * The enqueue time is taken when the enqueue returns (packet written, doorbell rung): from its
+//   entry, a launching thread preempted inside the enqueue counted as GPU delay.
+// * Waiting behind the process's own earlier dispatches on an in-order queue is not contention:
+//   a CPU-starved launcher enqueues in bursts, and each kernel of a burst then queues behind the
+//   previous one (config-3 run: 700-900 "warning" queue delays per phase while only the CPUs
+//   were contended). What remains is the wait for compute units other work holds.
+// Completions of one queue normally arrive in order; one that arrives after a later dispatch of
+// its queue is ignored for the other's readiness (the delay is then an upper bound).
 void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
   if (rec.kind != ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH) return;
   if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
@@ -317,8 +323,16 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
         g.enqueue_ts.erase(it);
       }
     }
-    if (enq.ts && d && d->start_timestamp > enq.ts) {
-      const uint64_t delay = d->start_timestamp - enq.ts;
+    if (!d) return;
+    uint64_t ready = enq.ts;
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      uint64_t& last = g.queue_end[d->dispatch_info.queue_id.handle];
+      if (last <= d->start_timestamp && last > ready) ready = last;
+      if (d->end_timestamp > last) last = d->end_timestamp;
+    }
+    if (enq.ts && d->start_timestamp > ready) {
+      const uint64_t delay = d->start_timestamp - ready;
       if (delay >= g.queue_floor_ns)
         emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id, enq.trace_h);
     }

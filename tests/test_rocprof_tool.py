@@ -226,3 +226,37 @@ def test_hbm_pressure_is_the_gpus_node_wide_vram_use():
     # the tool read the driver's node-wide counter while 8 GiB were live: at least the workload's
     # share, and within 2 pct-points of the last record it emitted
     assert tool >= own - 200 and abs(int(hbm[-1]) - tool) <= 2000, (tool, hbm[-5:].tolist(), own, node_milli)
+
+
+BURST_WORKLOAD = r"""
+import torch
+x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+torch.cuda.synchronize()
+for _ in range(3):  # a burst: 24 ~1 ms GEMMs enqueued back to back on one stream
+    ys = [x @ x for _ in range(24)]
+    torch.cuda.synchronize()
+"""
+
+
+@pytest.mark.gpu
+def test_queue_delay_excludes_waiting_behind_own_queue():
+    """A burst of GEMMs on one in-order stream: each kernel waits behind the previous one, which
+    is the process's own queued work, not contention for the GPU. gpu_queue_delay counts from
+    max(enqueue return, the queue predecessor's end), so it stays far below the burst's ~24 ms
+    of self-queueing (timed from the enqueue alone, the last GEMMs of a burst read ~20 ms)."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    name = f"/mislo-test-{os.getpid()}-burst"
+    ring = rt.HostRing(1 << 16, 64, name)
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0")
+    r = subprocess.run([sys.executable, "-c", BURST_WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    segs = ring.peek(1 << 16)
+    view = ring.records_view()
+    recs = np.concatenate([np.frombuffer(view[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
+                           for _, i, c in segs]) if segs else np.zeros(0, dtype=records.EVENT)
+    q = recs[recs["signal_type"] == 13]["value"].astype(np.float64) * 1e-6  # ms
+    assert len(q) >= 72, len(q)
+    assert q.max() < 5.0, np.sort(q)[-10:]

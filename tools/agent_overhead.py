@@ -70,7 +70,7 @@ def _smaps_top(pid: int, top: int = 14) -> list:
                 if not parts[0].endswith(":") or "-" in parts[0]:
                     name = parts[5] if len(parts) > 5 else "[anon]"
                     if name.startswith("/dev/shm/") or name.startswith("/memfd:"):
-                        name = name.split("(")[0]
+                        name = name.replace("(anonymous namespace)::", "").split("(")[0]
                     continue
                 if parts[0] in ("Rss:", "Private_Clean:", "Private_Dirty:"):
                     r = agg.setdefault(name, [0, 0])

@@ -65,9 +65,10 @@ class Client(threading.Thread):
     """Closed-loop client on one keep-alive connection (one RAG-service handler thread, so one
     vector-DB connection behind it)."""
 
-    def __init__(self, port: int, idx: int, phase, stop: threading.Event, rows: list, gap_s: float):
+    def __init__(self, port: int, idx: int, phase, stop: threading.Event, rows: list, gap_s: float, max_tokens: int = 16):
         super().__init__(daemon=True)
         self.port, self.idx, self.phase, self.stop, self.rows, self.gap = port, idx, phase, stop, rows, gap_s
+        self.max_tokens = max_tokens
         self.conn_tuple = None
 
     def run(self):
@@ -76,7 +77,7 @@ class Client(threading.Thread):
         while not self.stop.is_set():
             ph = self.phase()
             body = json.dumps({"prompt": f"how does retrieval {i} of client {self.idx} use the vector index",
-                               "profile": "rag_medium", "max_tokens": 16, "request_id": f"c{self.idx}-{i}"})
+                               "profile": "rag_medium", "max_tokens": self.max_tokens, "request_id": f"c{self.idx}-{i}"})
             t = time.time_ns()
             try:
                 c.request("POST", "/chat", body=body, headers={"Content-Type": "application/json"})
@@ -217,7 +218,8 @@ def main() -> int:
     ap.add_argument("--phase-s", type=float, default=15.0)
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--clients", type=int, default=2)
-    ap.add_argument("--burners-per-cpu", type=int, default=4)
+    ap.add_argument("--burners-per-cpu", type=int, default=6)
+    ap.add_argument("--max-tokens", type=int, default=8, help="tokens per request (short requests keep completing under contention)")
     ap.add_argument("--delay-ms", type=float, default=150.0, help="vector-DB stall per response in network faults")
     ap.add_argument("--retrans-rate", type=float, default=20.0, help="fault-profile record sets per second")
     ap.add_argument("--ttft-slo-ms", type=float, default=400.0)
@@ -286,7 +288,7 @@ def main() -> int:
         wait_http(f"http://127.0.0.1:{hport}/healthz", rag, 300)
         wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 240)
         tailer.start()
-        clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05) for i in range(a.clients)]
+        clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05, a.max_tokens) for i in range(a.clients)]
         for c in clients:
             c.start()
         t_w = time.time()
@@ -362,7 +364,7 @@ def main() -> int:
                     "victim_cpus": victim, "burners_per_cpu": a.burners_per_cpu, "vectordb_delay_ms": a.delay_ms,
                     "network_record_sets_per_s": a.retrans_rate, "observable_signals": observable,
                     "rocprof_tool": gpu_tool, "window_ms": a.window_ms, "phase_s": a.phase_s,
-                    "recover_s": a.recover_s, "clients": a.clients,
+                    "recover_s": a.recover_s, "clients": a.clients, "max_tokens": a.max_tokens,
                     "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "
                                      "injected on its connections via faultinject --emit-ring --fault",
                     "cpu_fault": "pinned CPU burners; run-queue delay measured by the schedstat sampler"}

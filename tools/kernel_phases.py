@@ -21,7 +21,7 @@ def load(d):
     for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         with open(path) as fh:
             for r in csv.DictReader(fh):
-                name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                 shape = f"{r.get('Grid_Size', r.get('Grid_Size_X', '?'))}/{r.get('Workgroup_Size', r.get('Workgroup_Size_X', '?'))}"
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, shape))
     rows.sort()

@@ -39,7 +39,7 @@ def load(dirs):
             disp = {}
             with open(path) as fh:
                 for row in csv.DictReader(fh):
-                    k = row["Kernel_Name"].split("(")[0].replace("void ", "")
+                    k = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                     shape = (row["Grid_Size"], row["Workgroup_Size"], row["LDS_Block_Size"], row["VGPR_Count"],
                              row["SGPR_Count"])
                     key = (path, row["Dispatch_Id"])

@@ -18,7 +18,7 @@ def summarise(db: str, top: int = 25) -> str:
     out = ["| kernel | calls | total us | avg us | min us | max us | % | grid | wg | vgpr | agpr | sgpr | lds B |",
            "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows[:top]:
-        name = r[0].split("(")[0].replace("void ", "")
+        name = r[0].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         out.append(f"| `{name}` | {r[1]} | {r[2] * unit:.1f} | {r[3] * unit:.2f} | {r[4] * unit:.2f} | "
                    f"{r[5] * unit:.2f} | {100 * r[2] / total:.1f} | {r[6]}x{r[7]} | {r[8]} | {r[9]} | {r[10]} | "
                    f"{r[11]} | {r[12]} |")
