@@ -43,15 +43,15 @@ __device__ __forceinline__ void store_counts(const uint32_t* lds, uint32_t* dst)
 // status bins, 16 value sums) take an atomic from EVERY event, and a wave's 64 events land on
 // a handful of bins: same-address LDS atomics serialise (PMC: 64 % extra LDS cycles with one
 // copy). Each lane adds into copy (lane & 7) and the copies are summed at the flush; the odd
-// copy strides put the copies of a bin on different banks. The partition histogram (4 x 1024
-// hashed bins) keeps one copy: a wave's keys are nearly all distinct, so its conflicts are
-// random bank collisions that copies do not remove.
+// copy strides put the copies of a bin on different banks. The partition histogram (4 x kParts
+// hashed bins) gets kPartRep copies too: the pod / service keys of a wave's events repeat (a
+// few hundred pods, tens of services), and with kParts = 128 trace keys collide as well.
 struct DecodeLds {
   // the signal tables, copied from constant memory once per workgroup: per-event lookups use
   // a lane-varying slot, which constant memory serves as one vector load per element (15 bucket
   // edges + thresholds + type map per event); from LDS a slot's edges are 4 ds_read_b128
   alignas(16) Tables tab;
-  static constexpr int kRep = 8, kPartRep = 1;
+  static constexpr int kRep = 8, kPartRep = 4;
   static constexpr int kHS = kSlots * kBuckets + 1, kSS = kSlots * 3 + 1, kUS = kSlots + 1;
   static constexpr int kPS = kKeyTypes * kParts + 1;
   uint32_t hist[kRep * kHS];

@@ -10,8 +10,8 @@
 // pairs are counted (DebugStats).
 //
 // GPU design (MI355X):
-//   1. decode (decode.hip) hashes every record's 4 join keys; the top 10 hash bits pick
-//      one of 1024 partitions per key type, counted per workgroup;
+//   1. decode (decode.hip) hashes every record's 4 join keys; the top kPartBits hash bits
+//      pick one of kParts partitions per key type, counted per workgroup;
 //   2. k_part_scan / k_base_scan turn per-workgroup counts into scatter offsets;
 //   3. k_scatter writes record indices into partition lists (no global atomics);
 //   4. k_probe: one workgroup per (key type, partition) stages the partition's SPANS in
@@ -77,9 +77,10 @@ __global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_
   if (r == 0) part_tot[c] = tot;
 }
 
-// exclusive scan of the 4096 partition totals (one workgroup of 1024 threads, 4 each)
-__global__ __launch_bounds__(1024) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base) {
-  __shared__ uint32_t s[1024];
+// exclusive scan of the kKeyTypes x kParts partition totals (one workgroup, 4 per thread)
+constexpr int kBaseNT = kKeyTypes * kParts / 4;
+__global__ __launch_bounds__(kBaseNT) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base) {
+  __shared__ uint32_t s[kBaseNT];
   const int t = threadIdx.x;
   uint32_t v[4];
   uint32_t sum = 0;
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(1024) void k_base_scan(const uint32_t* __restrict__
   }
   s[t] = sum;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
+  for (int off = 1; off < kBaseNT; off <<= 1) {
     uint32_t x = t >= off ? s[t - off] : 0;
     __syncthreads();
     s[t] += x;
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(1024) void k_base_scan(const uint32_t* __restrict__
     base[t * 4 + j] = run;
     run += v[j];
   }
-  if (t == 1023) base[kKeyTypes * kParts] = s[1023];
+  if (t == kBaseNT - 1) base[kKeyTypes * kParts] = s[kBaseNT - 1];
 }
 
 template <int NT>
@@ -161,7 +162,7 @@ __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
 
 // Work decomposition: two launches (the trace tier first, then pod+pid / pod+conn /
 // svc+node) of a fixed grid that dequeues items from a device-built work list (see
-// k_probe_work). Keys of the pod and service tiers are few and skewed: most of the 1024
+// k_probe_work). Keys of the pod and service tiers are few and skewed: most of the
 // partitions are empty and a handful carry thousands of signals. Empty partitions get no
 // item; a big signal list is sliced into items of kSigPerItem signals.
 //
@@ -195,7 +196,7 @@ constexpr int kLdsGroups = 64;
 constexpr int kSigPerItem = 4096;  // signals per work item (a partition's list is sliced); sweep: 256 498 us of compute, 1024 389, 2048 352, 4096 330, 8192 368 (staging repeats per item vs load balance)
 
 // Work list for the two probe phases, rebuilt every window on the device (no host sync,
-// graph-capturable). One workgroup of 1024 threads, one partition per thread:
+// graph-capturable). One workgroup of kParts threads, one partition per thread:
 //   work[0] / work[1]: item counts of phase 1 (trace) / phase 2 (pod+pid, pod+conn, svc+node)
 //   work[2] / work[3]: dequeue counters (zeroed here)
 //   items: code = key type << 28 | partition << 16 | slice << 8 | n slices.
@@ -214,10 +215,10 @@ __device__ __forceinline__ uint32_t probe_item_class(int k, uint32_t n_sig, uint
   return min(cost >> 13, 63u);
 }
 
-__global__ __launch_bounds__(1024) void k_probe_work(const uint32_t* __restrict__ span_base,
-                                                     const uint32_t* __restrict__ sig_base, int sig_per_item,
-                                                     uint32_t* __restrict__ work) {
-  __shared__ unsigned long long s[1024];
+__global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restrict__ span_base,
+                                                       const uint32_t* __restrict__ sig_base, int sig_per_item,
+                                                       uint32_t* __restrict__ work) {
+  __shared__ unsigned long long s[kParts];
   __shared__ uint32_t s_cls[64];
   const int p = threadIdx.x;
   if (p < 64) s_cls[p] = 0u;
@@ -233,13 +234,13 @@ __global__ __launch_bounds__(1024) void k_probe_work(const uint32_t* __restrict_
                                   ((unsigned long long)n[2] << 32) | ((unsigned long long)n[3] << 48);
   s[p] = mine;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
+  for (int off = 1; off < kParts; off <<= 1) {
     const unsigned long long x = p >= off ? s[p - off] : 0ull;
     __syncthreads();
     s[p] += x;
     __syncthreads();
   }
-  const unsigned long long tot = s[1023], excl = s[p] - mine;
+  const unsigned long long tot = s[kParts - 1], excl = s[p] - mine;
   uint32_t t[kKeyTypes], e[kKeyTypes];
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
@@ -870,7 +871,7 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
   static_assert((kKeyTypes * kParts) % kScanCols == 0, "scan columns tile the partition matrix");
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
                      part_blk, nblk, part_off, part_tot);
-  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(1024), 0, stream, part_tot, part_base);
+  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, part_base);
   // 1024 threads per workgroup: the grid is one workgroup per decode block (<= 256), so 256
   // threads left 4 waves per CU to hide the scattered stores and LDS atomics
   hipLaunchKernelGGL((k_scatter<1024>), dim3(nblk), dim3(1024), 0, stream, codes, n_dev, cap, part_off, part_base,
@@ -894,7 +895,7 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
     const int x = v ? atoi(v) : kSigPerItem;
     return x >= 1 ? x : kSigPerItem;
   }();
-  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(1024), 0, stream, span_base, sig_base, per_item, work);
+  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, sig_base, per_item, work);
   for (int phase = 0; phase < 2; ++phase)
     hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, sc, span_items, span_base, gc, sig_items,
                        sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);

@@ -13,8 +13,15 @@ namespace mislo {
 constexpr int kSlots = 16;          // feature slots (12 REF + 4 GPU signals)
 constexpr int kBuckets = 16;        // histogram buckets per slot (15 edges + overflow)
 constexpr int kKeyTypes = 4;        // trace, pod+pid, pod+conn, svc+node
-constexpr int kPartBits = 10;       // 1024 hash partitions per key type
+// Hash partitions per key type. Fewer, larger partitions make the scatter's per-(workgroup,
+// partition) runs long enough to fill cache lines and cut the probe's per-item staging; more make
+// each staged span chunk smaller. 2^7 measured best on MI355X (profiles/r3_prof).
+#ifndef MISLO_PART_BITS
+#define MISLO_PART_BITS 7
+#endif
+constexpr int kPartBits = MISLO_PART_BITS;
 constexpr int kParts = 1 << kPartBits;
+static_assert(kPartBits >= 6 && kPartBits <= 10, "partition table sizes assume 64..1024 partitions");
 constexpr int kPartBlocks = 256;    // max decode/scatter workgroups (per-block partition counts)
 constexpr int kMaxDomains = 16;     // posterior columns (10 used, padded to the MFMA tile)
 constexpr int kMaxPairs = 48;       // 2-fault hypothesis columns (36 used: pairs of the 9 fault domains)

@@ -102,8 +102,8 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
                   const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
                   uint32_t* gcnt, unsigned long long* dbg, uint32_t* work, hipStream_t stream);
 // probe work list: 4 header words + one word per (key type, partition, signal slice)
-constexpr int kProbeMaxSplit = 16;
-constexpr int kProbeProfOff = 4 + 4 * 1024 * kProbeMaxSplit;  // MISLO_PROBE_PROFILE counters (u64 [4][8])
+constexpr int kProbeMaxSplit = 64;  // signal slices per (key type, partition); the item code holds 8 bits
+constexpr int kProbeProfOff = 4 + 4 * kParts * kProbeMaxSplit;  // MISLO_PROBE_PROFILE counters (u64 [4][8])
 constexpr int kProbeWorkLen = kProbeProfOff + 64;
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
                      const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,
