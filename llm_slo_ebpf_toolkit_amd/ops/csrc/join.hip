@@ -160,6 +160,30 @@ __device__ __forceinline__ void top3_insert(unsigned long long* slot3, unsigned 
 
 __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
 
+// The first 48 bytes of a SigRec (every field the probe reads; the padding is never loaded):
+// three 16-byte loads per gathered signal.
+struct SigHot {
+  int64_t ts;
+  uint64_t tr, cn;
+  uint32_t pod, pid, sn;
+  float val;
+  uint32_t slot;
+};
+__device__ __forceinline__ SigHot load_hot(const SigRec* p) {
+  const uint4* v = reinterpret_cast<const uint4*>(p);
+  const uint4 a = v[0], b = v[1], c = v[2];
+  SigHot h;
+  h.ts = (int64_t)(((uint64_t)a.y << 32) | a.x);
+  h.tr = ((uint64_t)a.w << 32) | a.z;
+  h.cn = ((uint64_t)b.y << 32) | b.x;
+  h.pod = b.z;
+  h.pid = b.w;
+  h.sn = c.x;
+  h.val = __uint_as_float(c.y);
+  h.slot = c.z;
+  return h;
+}
+
 // Work decomposition: two launches (the trace tier first, then pod+pid / pod+conn /
 // svc+node) of a fixed grid that dequeues items from a device-built work list (see
 // k_probe_work). Keys of the pod and service tiers are few and skewed: most of the
@@ -340,7 +364,7 @@ __device__ __forceinline__ int lower_u16(const uint16_t* v, int n, int x) {
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
+__global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
                                               const uint32_t* __restrict__ span_base, SignalCols gc,
                                               const uint32_t* __restrict__ sig_items,
                                               const uint32_t* __restrict__ sig_base, int sig_cap, int span_cap,
@@ -526,19 +550,29 @@ __global__ __launch_bounds__(NT) void k_probe(SpanCols sc, const uint32_t* __res
     { const unsigned long long t = clock64(); p_stage += t - pt; pt = t; }
 #endif
 
-    // signal records are prefetched one iteration ahead (their indices two ahead): each
-    // iteration's random 64-byte load overlaps the previous signal's LDS work
+    // Signal records are random 64-byte gathers (from the Infinity Cache at best), so the loop
+    // keeps kDepth of them in flight per lane -- records kDepth iterations ahead, their indices
+    // one further -- and each iteration's LDS work overlaps the next ones' loads. The workgroup's
+    // LDS already caps the CU at 4 waves per SIMD, which leaves registers for the deeper queue
+    // (one record ahead: 2.2 TB/s of gathers, 72 % of wave time waiting; r3 PMC). Two fit in 128
+    // VGPRs (4 waves per SIMD, the LDS limit); three spill.
+    constexpr int kDepth = 2;
     uint32_t q = sg0 + threadIdx.x;
-    uint32_t g_nx = q < sg1 ? sig_items[q] : 0u;
-    uint32_t g_nx2 = q + NT < sg1 ? sig_items[q + NT] : 0u;
-    SigRec r_nx{};
-    if (q < sg1) r_nx = gc.rec[g_nx];
+    uint32_t gi[kDepth + 1];
+    SigHot rq[kDepth];
+#pragma unroll
+    for (int d = 0; d <= kDepth; ++d) gi[d] = q + d * NT < sg1 ? sig_items[q + d * NT] : 0u;
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) rq[d] = q + d * NT < sg1 ? load_hot(gc.rec + gi[d]) : SigHot{};
     for (; q < sg1; q += NT) {
-      const uint32_t g = g_nx;
-      const SigRec r = r_nx;
-      g_nx = g_nx2;
-      if (q + NT < sg1) r_nx = gc.rec[g_nx];
-      g_nx2 = q + 2 * NT < sg1 ? sig_items[q + 2 * NT] : 0u;
+      const uint32_t g = gi[0];
+      const SigHot r = rq[0];
+#pragma unroll
+      for (int d = 0; d < kDepth; ++d) gi[d] = gi[d + 1];
+#pragma unroll
+      for (int d = 0; d + 1 < kDepth; ++d) rq[d] = rq[d + 1];
+      if (q + kDepth * NT < sg1) rq[kDepth - 1] = load_hot(gc.rec + gi[kDepth - 1]);
+      gi[kDepth] = q + (kDepth + 1) * NT < sg1 ? sig_items[q + (kDepth + 1) * NT] : 0u;
       const uint64_t h = key_hash(k, r.tr, r.pod, r.pid, r.cn, r.sn);
       const int64_t t = r.ts;
       const int lo = lower_ht(s_kt, 0, m, h, t - w);

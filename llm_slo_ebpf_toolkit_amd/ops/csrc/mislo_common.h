@@ -14,10 +14,11 @@ constexpr int kSlots = 16;          // feature slots (12 REF + 4 GPU signals)
 constexpr int kBuckets = 16;        // histogram buckets per slot (15 edges + overflow)
 constexpr int kKeyTypes = 4;        // trace, pod+pid, pod+conn, svc+node
 // Hash partitions per key type. Fewer, larger partitions make the scatter's per-(workgroup,
-// partition) runs long enough to fill cache lines and cut the probe's per-item staging; more make
-// each staged span chunk smaller. 2^7 measured best on MI355X (profiles/r3_prof).
+// partition) runs longer (2^7: scatter 71 -> 41 us per halo-on window) but every probe item
+// stages and searches a bigger span chunk (2^7: probe 217 -> 258 us); 2^10 is the better total
+// on MI355X (profiles/r3_prof/kernel_phases_parts128.md).
 #ifndef MISLO_PART_BITS
-#define MISLO_PART_BITS 7
+#define MISLO_PART_BITS 10
 #endif
 constexpr int kPartBits = MISLO_PART_BITS;
 constexpr int kParts = 1 << kPartBits;

@@ -258,5 +258,6 @@ def test_queue_delay_excludes_waiting_behind_own_queue():
     recs = np.concatenate([np.frombuffer(view[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
                            for _, i, c in segs]) if segs else np.zeros(0, dtype=records.EVENT)
     q = recs[recs["signal_type"] == 13]["value"].astype(np.float64) * 1e-6  # ms
-    assert len(q) >= 72, len(q)
-    assert q.max() < 5.0, np.sort(q)[-10:]
+    # a GEMM that started the moment its predecessor ended waited for nothing: no record at all
+    # (r3 box: 5 records for 72 GEMMs + the setup kernels, none above 1 ms)
+    assert len(q) >= 1 and q.max() < 5.0, np.sort(q)[-10:]
