@@ -5,9 +5,12 @@ programs (/root/reference/docs/security/agent-min-capability-mode.md:1-35). The 
 accounts what ``runqueue_delay.bpf.c`` measures: ``/proc/<pid>/task/<tid>/schedstat`` holds each
 thread's on-CPU time, run-queue wait time and timeslice count, readable without privilege. The
 ``SchedstatSampler`` turns their per-interval deltas into ``runqueue_delay_ms`` records -- per
-process, its threads' run-queue wait over their timeslices in the interval (each timeslice is one
-wakeup-to-run the BPF probe would have timed, so this is the mean of the probe's per-switch
-delays for the process), above the probe's 100 us floor -- tagged with the pid and pod, and pushes
+process, the run-queue wait over the timeslices of its threads whose mean wait per timeslice
+reached the probe's 100 us floor (each timeslice is one wakeup-to-run the BPF probe times, and
+the probe emits only waits above its floor, so this is the mean of the waits the probe would
+have emitted for the process; without the filter the many near-zero waits of a runtime's
+helper threads hid a starved main thread: config-3 run, profiles/r3_config3_*) -- tagged with
+the pid and pod, and pushes
 them into the agent's user-space ring like the rocprofiler tool's records. The GPU window engine
 joins them to the pod's spans (pod + pid tier).
 
@@ -111,7 +114,7 @@ class SchedstatSampler:
                 if prev is None:
                     continue
                 dw, ds = st[1] - prev[0], st[2] - prev[1]
-                if ds > 0 and dw >= 0:
+                if ds > 0 and dw >= self.floor_ns * ds:  # this thread's waits reach the floor
                     w_sum += dw
                     s_sum += ds
             if s_sum and w_sum // s_sum >= self.floor_ns:

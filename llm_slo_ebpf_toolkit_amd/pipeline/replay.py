@@ -52,6 +52,9 @@ SCENARIOS: Dict[str, List[Tuple[str, ...]]] = {
 }
 
 COUNT_SIGNALS = {"tcp_retransmits_total", "connect_errors_total", "tls_handshake_fail_total"}
+# Level gauges of a shared resource (a GPU's HBM in use): every reader sees nearly the same value,
+# bounded by 100 %, not a per-event latency with a heavy tail
+GAUGE_SIGMA = {"hbm_pressure_pct": 0.03}
 CTX_SIGNALS = {"dns_latency_ms": .22, "connect_latency_ms": .2, "connect_errors_total": .06,
                "tls_handshake_ms": .18, "tls_handshake_fail_total": .05, "syscall_latency_ms": .17,
                "tcp_retransmits_total": .12}
@@ -112,10 +115,22 @@ class ReplayWindow:
         return int(self.spans.shape[0])
 
 
+# Replay services are GPU-served LLMs: a fault that starves the serving process's CPUs also
+# delays its GPU dispatches (the launching thread submits in bursts between its timeslices; live
+# config-3 runs with the CPUs contended: GPU queue delay p50 6-9 ms, 700-900 dispatches per
+# 15-s phase above the 2-ms warning level, profiles/r3_config3_*). REF's profiles describe
+# CPU-only services, so the coupling is added here, on top of them.
+GPU_SERVED_COUPLING: Dict[str, Dict[str, float]] = {
+    "cpu_throttle": {"gpu_queue_delay_ms": 6.0},
+}
+
+
 def _profile(labels: Sequence[str]) -> Dict[str, float]:
     prof = dict(BASE_PROFILE)
     for lab in labels:
-        for k, v in FAULT_OVERRIDES.get(lab, {}).items():
+        over = dict(FAULT_OVERRIDES.get(lab, {}))
+        over.update(GPU_SERVED_COUPLING.get(lab, {}))
+        for k, v in over.items():
             # multi-fault: the more severe symptom wins (latency up / tps down are both "up" here)
             prof[k] = max(prof[k], v) if k in prof else v
     return prof
@@ -181,6 +196,8 @@ class ReplayGenerator:
             prof = np.array([profiles[g][name] for g in range(G)], dtype=np.float64)[grp[m]]
             if name in COUNT_SIGNALS:
                 out[m] = self.rng.poisson(prof)
+            elif name in GAUGE_SIGMA:
+                out[m] = np.minimum(100.0, prof * np.exp(self.rng.normal(0.0, GAUGE_SIGMA[name], size=int(m.sum()))))
             else:
                 out[m] = prof * np.exp(self.rng.normal(0.0, self.cfg.jitter_sigma, size=int(m.sum())))
         return out

@@ -31,13 +31,13 @@ def test_schedstat_sampler_emits_mean_wait_per_slice_above_the_floor(tmp_path):
                                 proc_root=str(tmp_path), node_id=3)
     assert len(s.sample(10**18)) == 0  # first look: no deltas yet
     write_schedstat(tmp_path, 100, 100, 9_000_000, 1_000_000 + 4 * 2_000_000, 14)  # 2 ms per slice
-    write_schedstat(tmp_path, 100, 101, 9_000_000, 1_000_000 + 4 * 50_000, 14)     # 50 us per slice
+    write_schedstat(tmp_path, 100, 101, 9_000_000, 1_000_000 + 4 * 50_000, 14)     # 50 us per slice: below
     write_schedstat(tmp_path, 200, 200, 2, 1, 2)                                     # ran, never waited
     ev = s.sample(10**18 + 100_000_000)
-    assert len(ev) == 1  # per process: its threads' wait over their 8 timeslices
+    assert len(ev) == 1  # per process: the wait over the timeslices of its threads above the floor
     e = ev[0]
     assert (int(e["signal_type"]), int(e["value"]), int(e["pid"]), int(e["tid"]), int(e["pod_id"]),
-            int(e["node_id"])) == (procfs.RUNQUEUE_TYPE, (8_000_000 + 200_000) // 8, 100, 100, 7, 3)
+            int(e["node_id"])) == (procfs.RUNQUEUE_TYPE, 2_000_000, 100, 100, 7, 3)
     write_schedstat(tmp_path, 100, 100, 9_500_000, 9_000_000 + 3_000_000, 15)
     assert s.tick(10**18 + 200_000_000) == 1 and s.emitted == 1 and pushed[0].dtype.itemsize == 24
     # an exited thread is forgotten
