@@ -219,6 +219,9 @@ def main() -> int:
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--clients", type=int, default=2)
     ap.add_argument("--burners-per-cpu", type=int, default=6)
+    ap.add_argument("--procfs-ms", type=int, default=25,
+                    help="schedstat sampling interval: run-queue records join a request's span only within 100 ms "
+                         "of its start (REF's pod+pid tier), so they must come faster than that")
     ap.add_argument("--max-tokens", type=int, default=8, help="tokens per request (short requests keep completing under contention)")
     ap.add_argument("--delay-ms", type=float, default=150.0, help="vector-DB stall per response in network faults")
     ap.add_argument("--retrans-rate", type=float, default=20.0, help="fault-profile record sets per second")
@@ -270,7 +273,7 @@ def main() -> int:
          "--window-ms", str(a.window_ms), "--window-events", "65536", "--window-spans", "4096", "--window-groups", "8",
          "--model-path", a.model_path, "--min-confidence", "0.3", "--halo-ms", "1500",
          "--ttft-slo-ms", str(a.ttft_slo_ms), "--procfs-sampler", "--procfs-pods", f"{rag.pid}:{POD_UID}",
-         "--procfs-interval-ms", "100", "--model-signals", ",".join(observable),
+         "--procfs-interval-ms", str(a.procfs_ms), "--model-signals", ",".join(observable),
          "--output", "jsonl", "--output-path", attr_path],
         cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
     stop, tstop = threading.Event(), threading.Event()
@@ -365,6 +368,7 @@ def main() -> int:
                     "network_record_sets_per_s": a.retrans_rate, "observable_signals": observable,
                     "rocprof_tool": gpu_tool, "window_ms": a.window_ms, "phase_s": a.phase_s,
                     "recover_s": a.recover_s, "clients": a.clients, "max_tokens": a.max_tokens,
+                    "procfs_interval_ms": a.procfs_ms,
                     "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "
                                      "injected on its connections via faultinject --emit-ring --fault",
                     "cpu_fault": "pinned CPU burners; run-queue delay measured by the schedstat sampler"}
