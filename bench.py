@@ -352,7 +352,7 @@ def main() -> int:
     sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs + himgs)
     user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
     xchg = (min(65536, a.events) if world > 1 else 0) if a.xchg_cap < 0 else a.xchg_cap
-    import_cap = (sig_cap if a.halo_ms > 0 else 0) + (world - 1) * xchg
+    import_cap = (world - 1) * xchg  # other GPUs' rows (the halo's rows stay resident)
     pipe = WindowPipeline(sig_cap, max(a.spans, a.train_spans if train_imgs else 0), a.services, local, comm,
                           model=a.model, seed=a.seed, learn=bool(train_imgs),
                           use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,

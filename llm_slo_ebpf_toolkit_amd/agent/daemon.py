@@ -22,6 +22,7 @@ Two engines share one process, one Prometheus registry and one set of outputs:
 
 from __future__ import annotations
 
+import math
 import os
 import sys
 import threading
@@ -619,10 +620,12 @@ class Agent:
         N = self.n_gpus()
         G = o.window_groups
         budget = o.window_events + o.window_events // 4  # events plus the definitions ahead of them
-        # joins reach across the window cut (halo) and, on a multi-GPU node, across GPUs
-        # (trace-tagged rows exchanged over RCCL); imports are bounded by one window's records
+        # joins reach across the window cut (halo: the rows of the earlier windows it spans stay
+        # resident on the device) and, on a multi-GPU node, across GPUs (trace-tagged rows
+        # exchanged over RCCL, bounded per peer)
         xchg = min(65536, budget) if N > 1 else 0
-        icap = (budget if o.halo_ms > 0 else 0) + (N - 1) * xchg
+        icap = (N - 1) * xchg
+        halo_windows = int(min(3, max(1, math.ceil(o.halo_ms / max(o.window_ms, 1)) + 1)))
         port = 0
         if o.engine == "cpu" and N > 1:
             import socket
@@ -637,7 +640,7 @@ class Agent:
                             group_cap=max(1, groups_of(0, N, G)), user_cap=max(1024, o.window_events // 4),
                             window_ms=float(o.window_ms), ttft_slo_ms=o.ttft_slo_ms, halo_ms=o.halo_ms,
                             import_cap=icap, xchg_cap=xchg, model_image=np.asarray(image, np.uint8).tobytes(),
-                            pods=pods, master=("127.0.0.1", port)) for r in range(N)]
+                            pods=pods, master=("127.0.0.1", port), halo_windows=halo_windows) for r in range(N)]
         state = self._state_path()
         if state and os.path.exists(state):
             self.load_state(state)

@@ -61,6 +61,7 @@ class WorkerSpec:
     pods: Optional[Tuple[np.ndarray, np.ndarray]] = None
     master: Tuple[str, int] = ("127.0.0.1", 0)   # gloo rendezvous (cpu engine)
     env: Dict[str, str] = field(default_factory=dict)
+    halo_windows: int = 3       # earlier windows resident on the device for the halo
 
 
 def groups_of(rank: int, world: int, n_groups: int) -> int:
@@ -106,7 +107,8 @@ class WorkerCore:
         self.rings = rings
         self.pipe = WindowPipeline(spec.sig_cap, spec.span_cap, spec.group_cap, spec.device, comm, model="bayes",
                                    learn=False, window_ms=2000.0, user_cap=spec.user_cap,
-                                   ttft_slo_ms=spec.ttft_slo_ms, halo_ms=spec.halo_ms, import_cap=spec.import_cap,
+                                   ttft_slo_ms=spec.ttft_slo_ms, halo_ms=spec.halo_ms, halo_windows=spec.halo_windows,
+                                   import_cap=spec.import_cap,
                                    xchg_cap=spec.xchg_cap, shard=(spec.rank, spec.world), engine=spec.engine,
                                    group=group, model_image=np.frombuffer(spec.model_image, dtype=np.uint8))
         # the controller publishes the epochs: this source never writes mislo_cfg

@@ -21,7 +21,10 @@ swap-in -- in every interval. Its per-interval growth becomes ``mem_reclaim_late
 assumed absent, by an agent without BPF.
 
 Watched processes: a static ``pid -> pod uid`` list (``agent --procfs-pods``), or every process in
-the node's kubepods cgroups (``pod_processes``).
+the node's kubepods cgroups (``pod_processes``). They are named by the agent's (host) pids; the
+records carry each process's pid in its own innermost pid namespace (``/proc/<pid>/status``
+NSpid), the pid its spans and its rocprofiler records carry, as the BPF probes do
+(mislo_probe.h mislo_ns_tgid).
 """
 
 from __future__ import annotations
@@ -71,6 +74,20 @@ def psi_available(proc_root: str = "/proc") -> bool:
     return read_psi_total_us(os.path.join(proc_root, "pressure", "memory")) is not None
 
 
+def ns_pid(pid: int, proc_root: str = "/proc") -> int:
+    """``pid``'s pid in its innermost pid namespace (the last NSpid field; ``pid`` itself for a
+    process in the reader's namespace or when the field is unavailable)."""
+    try:
+        with open(os.path.join(proc_root, str(pid), "status")) as fh:
+            for ln in fh:
+                if ln.startswith("NSpid:"):
+                    f = ln.split()
+                    return int(f[-1]) if len(f) > 1 else pid
+    except (OSError, ValueError):
+        pass
+    return pid
+
+
 def read_schedstat(path: str) -> Optional[Tuple[int, int, int]]:
     try:
         with open(path) as fh:
@@ -88,6 +105,7 @@ class SchedstatSampler:
         self.proc_root, self.floor_ns, self.node_id = proc_root, int(floor_ns), int(node_id)
         self._prev: Dict[Tuple[int, int], Tuple[int, int]] = {}
         self._psi: Dict[int, Tuple[Optional[str], Optional[int]]] = {}   # pid -> (PSI file, last total us)
+        self._ns: Dict[int, int] = {}      # host pid -> pid in its own namespace
         self.samples = self.emitted = self.dropped = 0
         self._stop = threading.Event()
         self._thr: Optional[threading.Thread] = None
@@ -118,10 +136,14 @@ class SchedstatSampler:
                     w_sum += dw
                     s_sum += ds
             if s_sum and w_sum // s_sum >= self.floor_ns:
-                rows.append((pid, pid, pod, w_sum // s_sum))
+                rows.append((self.pod_pid(pid), pid, pod, w_sum // s_sum))
         for key in list(self._prev):
             if key not in seen:
                 del self._prev[key]
+        alive = {k[0] for k in seen}
+        for pid in list(self._ns):
+            if pid not in alive:
+                del self._ns[pid]
         mem = self._memory_rows()
         self.samples += 1
         ev = np.zeros(len(rows) + len(mem), dtype=records.EVENT)
@@ -135,6 +157,13 @@ class SchedstatSampler:
             ev["pod_id"] = a[:, 2].astype(np.uint32)
             ev["node_id"] = self.node_id
         return ev
+
+    def pod_pid(self, pid: int) -> int:
+        """The record's pid: ``pid`` as its own pod sees it (cached while it lives)."""
+        v = self._ns.get(pid)
+        if v is None:
+            v = self._ns[pid] = ns_pid(pid, self.proc_root)
+        return v
 
     def _memory_rows(self):
         """(pid, pid, pod, stall ns) of the watched processes whose PSI memory stall grew by at
@@ -157,7 +186,7 @@ class SchedstatSampler:
                 continue
             d_ns = (tot - last) * 1000
             if d_ns >= self.floor_ns:
-                rows.append((pid, pid, pod, d_ns))
+                rows.append((self.pod_pid(pid), pid, pod, d_ns))
         for pid in list(self._psi):
             if pid not in live:
                 del self._psi[pid]

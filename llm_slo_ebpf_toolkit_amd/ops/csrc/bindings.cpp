@@ -66,6 +66,7 @@ class Engine {
     g_part_tot = torch::empty({kKeyTypes * kParts}, i32);
     g_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
     g_items = torch::empty({kKeyTypes * N}, i32);
+    g_keys = torch::empty({kKeyTypes * N * (int64_t)sizeof(KeyTs)}, u8);
     g_rec = torch::empty({(int64_t)N * (int64_t)sizeof(SigRec)}, u8);
     // span columns
     s_part = torch::empty({S, 4}, torch::TensorOptions().dtype(torch::kInt16).device(dev_));
@@ -146,9 +147,16 @@ class Engine {
     hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, cur_stream(), fl);
   }
 
+  // one generation (no halo): slot 0, every row local
   SignalCols sig_cols() {
     return SignalCols{reinterpret_cast<SigRec*>(g_rec.data_ptr()), dptr<uint8_t>(g_status),
-                      reinterpret_cast<PartCodes*>(g_part.data_ptr())};
+                      reinterpret_cast<PartCodes*>(g_part.data_ptr()), dptr<uint32_t>(g_items),
+                      reinterpret_cast<KeyTs*>(g_keys.data_ptr()), dptr<uint32_t>(g_part_base), nullptr,
+                      (int64_t)sig_cap_, 1};
+  }
+  void partition_signals() {
+    launch_partition_sig(sig_cols(), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
+                         dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), cur_stream());
   }
   SpanCols span_cols() {
     return SpanCols{reinterpret_cast<SpanRec*>(s_rec.data_ptr()), reinterpret_cast<PartCodes*>(s_part.data_ptr())};
@@ -162,9 +170,7 @@ class Engine {
     launch_decode_events(events.data_ptr(), dptr<int>(counts), sig_cap_, sig_cols(), dptr<uint32_t>(hist),
                          dptr<uint32_t>(status_cnt), dptr<uint32_t>(g_part_blk),
                          dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
-                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
-                     dptr<uint32_t>(g_items), cur_stream());
+    partition_signals();
   }
 
   // context id -> {pod, pid, conn32, svc<<16|node} (int32 [n, 4]) for EVENT16 records and SPAN20 spans
@@ -184,9 +190,7 @@ class Engine {
     launch_decode_wire(events.data_ptr(), dptr<int>(counts), sig_cap_, dptr<uint32_t>(ctx_table),
                        (int)ctx_table.size(0), sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                        dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
-                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
-                     dptr<uint32_t>(g_items), cur_stream());
+    partition_signals();
   }
 
   void decode_wire(torch::Tensor events, int64_t wire) {
@@ -202,9 +206,7 @@ class Engine {
     launch_decode_ref(events.data_ptr(), dptr<int>(counts), sig_cap_, (uint32_t)pod, (uint32_t)svcnode,
                       (uint64_t)trace_h, sig_cols(), dptr<uint32_t>(hist), dptr<uint32_t>(status_cnt),
                       dptr<uint32_t>(g_part_blk), dptr<unsigned long long>(misc), cur_stream());
-    launch_partition(reinterpret_cast<const PartCodes*>(g_part.data_ptr()), dptr<int>(counts), sig_cap_, nblk_sig_, dptr<uint32_t>(g_part_blk),
-                     dptr<uint32_t>(g_part_off), dptr<uint32_t>(g_part_tot), dptr<uint32_t>(g_part_base),
-                     dptr<uint32_t>(g_items), cur_stream());
+    partition_signals();
   }
 
   // spans: device uint8 tensor of 64-byte span records; counts[1] = n spans, counts[2] = n groups
@@ -221,8 +223,7 @@ class Engine {
                      dptr<uint32_t>(s_part_blk), dptr<uint32_t>(s_part_off), dptr<uint32_t>(s_part_tot),
                      dptr<uint32_t>(s_part_base), dptr<uint32_t>(s_items), st);
     // top3 / cnt / gsum / gcnt were reset by reset_window()
-    launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(),
-                 dptr<uint32_t>(g_items), dptr<uint32_t>(g_part_base), sig_cap_, span_cap_, jp_,
+    launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(), span_cap_, jp_,
                  dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<unsigned long long>(gsum),
                  dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), dptr<uint32_t>(probe_work), st);
     const float* base = nullptr;
@@ -332,7 +333,7 @@ class Engine {
 
   torch::Tensor counts;
   torch::Tensor g_status, g_part;
-  torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items, g_rec, s_rec;
+  torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items, g_keys, g_rec, s_rec;
   torch::Tensor s_part;
   torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, probe_work;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
@@ -428,6 +429,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                            kPacketStats, kPacketCount);
   m.attr("PARTS") = kParts;
   m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
+  m.attr("PROBE_PROF_OFF") = kProbeProfOff;
   py::class_<Engine>(m, "Engine")
       .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("sig_cap"), py::arg("span_cap"),
            py::arg("group_cap"), py::arg("device") = 0)

@@ -131,7 +131,8 @@ __device__ __forceinline__ void lds_flush(DecodeLds& L, const DecodeOut& o, int 
 __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val, int slot,
                                            uint64_t trace_h, uint32_t pod, uint32_t pid, uint32_t svcnode,
                                            uint64_t conn_h, const DecodeOut& o, const LdsLane& l,
-                                           int& unsupported, int& zero_ts, bool local, void* rec_dst) {
+                                           int& unsupported, int& zero_ts, bool local, void* rec_dst,
+                                           uint64_t* t_range = nullptr) {
   uint8_t st = 0;
   if (slot >= 0 && local) {
     const Tables& t = *l.tab;
@@ -173,6 +174,10 @@ __device__ __forceinline__ void decode_one(int i, int cap, int64_t ts, float val
   // timestamp never satisfies a window (REF dns.go:107-113): no join keys for either.
   const bool joinable = slot >= 0 && ts != 0;
   if (ts == 0 && local) ++zero_ts;
+  if (t_range && joinable) {  // the generation's joinable time range (probe pruning)
+    t_range[0] = min(t_range[0], ts_image(ts));
+    t_range[1] = max(t_range[1], ts_image(ts));
+  }
   PartCodes pc;
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
@@ -432,6 +437,10 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   const int beg = seg_beg + blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0, events = 0, other = 0;
   unsigned long long t_hi = 0;
+  uint64_t tr[2] = {~0ull, 0ull};  // joinable rows' time range (u64 images)
+  // rows land in the current generation's slot (resident for the halo)
+  const uint32_t cur = cur_slot(o.cols);
+  SigRec* const rec_out = o.cols.rec + (size_t)cur * (size_t)o.cols.stride;
   __shared__ uint4 s_stage[NT * 5];
   const int lane = threadIdx.x & 63, wbase = threadIdx.x & ~63;
   const int trips = end > beg ? (end - beg + NT - 1) / NT : 0;
@@ -441,7 +450,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
       if (i >= n_loc) {  // imported row: joins, never counted
         const SigRec& m = imp[i - n_loc];
         decode_one(i, cap, m.ts, m.val, m.slot == kNoSlot ? -1 : (int)m.slot, m.tr, m.pod, m.pid, m.sn, m.cn, o, l,
-                   unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+                   unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
       } else if (i < n_k) {
         const uint8_t* r = framed + (size_t)i * kRecStride;
         const uint2 h = *reinterpret_cast<const uint2*>(r);
@@ -459,11 +468,11 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
           const int slot = st < kMaxTypes ? (int)L.tab.type_slot[st] : -1;
           const int64_t ts = wire_ts(e, t_base);
           decode_one(i, cap, ts, (float)((double)e.value_milli * 1e-3), slot, trace_of(tt, (uint32_t)wire_trace(e)),
-                     cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+                     cx.x, cx.y, cx.w, (uint64_t)cx.z, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5], tr);
           if (slot >= 0 && ts > 0) t_hi = max(t_hi, (unsigned long long)ts);
           ++events;
         } else {  // a hole: never counted, never joined
-          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
         }
       } else if (user_rec == 24) {
         const uint2* u = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(user) + (size_t)(i - n_k) * 24);
@@ -475,10 +484,10 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const int64_t ts = user24_ts(b.y, c.y, c.x, u_base);
         if (!shard_owns(sn, sh_rank, sh_world)) {
           ++other;
-          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
         } else {
         decode_one(i, cap, ts, (float)((double)b.x * 1e-3), slot, ((uint64_t)a.y << 32) | a.x, pod, c.x & 0x3FFFFFu, sn,
-                   0ull, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+                   0ull, o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5], tr);
         if (slot >= 0 && ts > 0) t_hi = max(t_hi, (unsigned long long)ts);
         ++events;
         }
@@ -489,10 +498,10 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const uint32_t sn = e.pod_id < n_pods ? pod_sn[e.pod_id] : 0u;
         if (!shard_owns(sn, sh_rank, sh_world)) {
           ++other;
-          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
         } else {
         decode_one(i, cap, e.ts_ns, (float)((double)e.value_milli * 1e-3), slot, e.trace_h, e.pod_id, e.pid, sn, 0ull,
-                   o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5]);
+                   o, l, unsupported, zero_ts, true, &s_stage[threadIdx.x * 5], tr);
         if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
         ++events;
         }
@@ -505,10 +514,10 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const uint32_t svcnode = ((uint32_t)e.svc_id << 16) | e.node_id;
         if (!shard_owns(svcnode, sh_rank, sh_world)) {
           ++other;
-          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5]);
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
         } else {
           decode_one(i, cap, e.ts_ns, val, slot, e.trace_h, e.pod_id, e.pid, svcnode, conn32(ck), o, l, unsupported,
-                     zero_ts, true, &s_stage[threadIdx.x * 5]);
+                     zero_ts, true, &s_stage[threadIdx.x * 5], tr);
           if (slot >= 0 && e.ts_ns > 0) t_hi = max(t_hi, (unsigned long long)e.ts_ns);
           ++events;
         }
@@ -519,7 +528,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
     const int nv = min(64, end - first);
     if (nv > 0) {
       const uint4* src = &s_stage[wbase * 5];
-      uint4* dst = reinterpret_cast<uint4*>(o.cols.rec + first);
+      uint4* dst = reinterpret_cast<uint4*>(rec_out + first);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = lane + 64 * j;
@@ -532,11 +541,17 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
     events += __shfl_xor(events, off);
     other += __shfl_xor(other, off);
     t_hi = max(t_hi, (unsigned long long)__shfl_xor((long long)t_hi, off));
+    tr[0] = min(tr[0], (uint64_t)__shfl_xor((long long)tr[0], off));
+    tr[1] = max(tr[1], (uint64_t)__shfl_xor((long long)tr[1], off));
   }
   if ((threadIdx.x & 63) == 0) {
     if (events) atomicAdd(&rs[kRsEvents], (uint32_t)events);
     if (other) atomicAdd(&rs[kRsOtherShard], (uint32_t)other);
     if (t_hi) atomicMax(tmax, t_hi);
+    if (o.cols.gen && tr[0] <= tr[1]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(&o.cols.gen->tlo[cur]), (unsigned long long)tr[0]);
+      atomicMax(reinterpret_cast<unsigned long long*>(&o.cols.gen->thi[cur]), (unsigned long long)tr[1]);
+    }
   }
   lds_flush<NT>(L, o, unsupported, zero_ts);
 }
@@ -594,6 +609,7 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   const int n = min(*n_ptr, cap);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  uint64_t t_lo = ~0ull, t_hi = 0ull;  // joinable spans' time range (u64 images)
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     SpanRec r;
     if (compact) {
@@ -634,6 +650,10 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
       r.grp = grp;
     }
     c.rec[i] = r;
+    if (r.ts != 0) {
+      t_lo = min(t_lo, ts_image(r.ts));
+      t_hi = max(t_hi, ts_image(r.ts));
+    }
     PartCodes pc;
 #pragma unroll
     for (int k = 0; k < kKeyTypes; ++k) {
@@ -642,6 +662,16 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
       if (h) atomicAdd(&s_part[k * kParts + part_of(h)], 1u);
     }
     c.part[i] = pc;
+  }
+  if (sm.gen) {
+    for (int off = 32; off > 0; off >>= 1) {
+      t_lo = min(t_lo, (uint64_t)__shfl_xor((long long)t_lo, off));
+      t_hi = max(t_hi, (uint64_t)__shfl_xor((long long)t_hi, off));
+    }
+    if ((threadIdx.x & 63) == 0 && t_lo <= t_hi) {
+      atomicMin(reinterpret_cast<unsigned long long*>(&sm.gen->span_lo), (unsigned long long)t_lo);
+      atomicMax(reinterpret_cast<unsigned long long*>(&sm.gen->span_hi), (unsigned long long)t_hi);
+    }
   }
   __syncthreads();
   store_counts<NT>(s_part, part_cnt + (size_t)blockIdx.x * kKeyTypes * kParts);

@@ -17,8 +17,9 @@
 //                    all-gather of the trace-tagged rows (merged into window k+1's imports) ->
 //                    totals += packet b -> D2H(packet b, all ranks' results)
 //
-// Imported rows: window k+1 also joins (never counts) the rows of window k within the join
-// window of its latest record (the halo, halo_ms) and the other GPUs' trace-tagged rows of
+// Halo and imported rows: window k also joins (never counts) the rows of up to halo_windows
+// earlier windows that lie within halo_ms of each later window's latest record -- kept resident
+// where their own window decoded and partitioned them -- and the other GPUs' trace-tagged rows of
 // window k (exchange.hip), so joins across window and GPU boundaries match.
 //
 // so the DMA of window k+1 and the node-wide all-reduce of window k run under the kernels of
@@ -64,8 +65,9 @@ struct EngineConfig {
   double inv_temp = 1.0, min_count = 0.0;  // refit calibration (posterior.hip k_refit_nb)
   int n_dom = 10;
   float ttft_slo_ms = 800.0f;  // per-incident SLO impact: spans with TTFT above this breach
-  double halo_ms = 0.0;        // carry rows this close to the window's latest record into the next window
-  int import_cap = 0;          // imported rows per window (halo + other GPUs' trace rows); 0 = none
+  double halo_ms = 0.0;        // later windows also join rows this close to every later window's latest record
+  int halo_windows = 3;        // earlier windows whose rows stay resident for the halo (1..3)
+  int import_cap = 0;          // other GPUs' trace rows per window; 0 = none
   int xchg_cap = 0;            // trace-tagged rows each GPU exchanges per window (RCCL); 0 = none
   // group sharding of one node's stream over the node's GPUs (agent --gpus N): this GPU counts and
   // joins only its services' records and incident groups (decode.hip shard_owns); 1 = whole stream
@@ -157,8 +159,9 @@ class WindowEngine {
   void restore(const double* stats, const void* model, size_t model_bytes, int64_t folded);
   void model_bytes(void* out);        // the model currently on the device (synchronous)
   void sync();
-  // device-side import state (synchronous; diagnostics and tests): rows[0..1], tmax, and per
-  // buffer the halo / other-GPU row counts
+  // device-side import state (synchronous; diagnostics and tests): rows[0..1], tmax, the
+  // generations (count, current slot, windows held, per-age cut-offs and rows), per buffer the
+  // other-GPU row counts
   std::vector<int64_t> import_state();
   int64_t windows_folded() const { return folded_; }
   size_t staged_bytes() const { return staged_bytes_; }
@@ -191,12 +194,15 @@ class WindowEngine {
   uint32_t *pod_sn_ = nullptr, *pod_host_ = nullptr, *ring_state_ = nullptr;
   unsigned long long* trace_hash_ = nullptr;  // kernel trace id -> hash
   uint32_t* sli_ = nullptr;
-  // imported rows: per buffer, [halo rows | remote rows]; counts per buffer
-  int n_rows_ = 0;                 // row capacity of the join = sig_cap + import_cap
+  // other GPUs' rows: per buffer, imported after this window's records; counts per buffer
+  int n_rows_ = 0;                 // rows per generation = sig_cap + import_cap
+  int gens_ = 1;                   // resident generations (1 + halo_windows with a halo)
   int* rows_ = nullptr;            // device: rows of the current window
   unsigned long long* tmax_ = nullptr;
+  GenMeta* gen_ = nullptr;         // device: generation slots, halo cut-offs, time ranges
+  KeyTs* g_keys_ = nullptr;        // [gens][kKeyTypes * n_rows] partition list keys
   std::vector<SigRec*> imp_;
-  uint32_t *halo_n_ = nullptr, *remote_n_ = nullptr, *sel_cnt_ = nullptr, *sel_off_ = nullptr;
+  uint32_t *remote_n_ = nullptr, *sel_cnt_ = nullptr, *sel_off_ = nullptr;
   uint8_t *xsend_ = nullptr, *xrecv_ = nullptr;
   size_t xstride_ = 0, xrecv_bytes_ = 0;
   int nblk_imp_ = 0;                    // decode blocks of the other GPUs' rows

@@ -88,8 +88,11 @@ WindowEngine::WindowEngine(const EngineConfig& cfg) : cfg_(cfg) {
   max_ahead_ = std::min(nb_, std::max(1, cfg.max_ahead));
   if (cfg.user_cap <= 0 || cfg.user_cap > cfg.sig_cap) throw std::invalid_argument("user_cap must be in [1, sig_cap]");
   if (cfg.import_cap < 0 || cfg.xchg_cap < 0 || cfg.halo_ms < 0) throw std::invalid_argument("negative import sizes");
-  if ((long long)cfg.sig_cap + cfg.import_cap >= (1LL << 27))
-    throw std::invalid_argument("sig_cap + import_cap must be < 2^27 (top-3 key packing)");
+  if (cfg.halo_windows < 1 || cfg.halo_windows >= kMaxGens)
+    throw std::invalid_argument("halo_windows must be in [1, 3] (resident generations)");
+  gens_ = cfg.halo_ms > 0 ? 1 + cfg.halo_windows : 1;
+  if (2LL * gens_ * ((long long)cfg.sig_cap + cfg.import_cap) >= (1LL << 27))
+    throw std::invalid_argument("2 x generations x (sig_cap + import_cap) must be < 2^27 (top-3 key packing)");
   HIPCHECK(hipSetDevice(cfg.device));
   set_join_params(cfg.window_ms, cfg.threshold, cfg.fanout, cfg.group_mode);
   alloc();
@@ -187,13 +190,19 @@ void WindowEngine::alloc() {
   ring_state_ = dalloc<uint32_t>(kRsLen);
   trace_hash_ = dalloc<unsigned long long>(kTraceIdRows);
   HIPCHECK(hipMemset(trace_hash_, 0, (size_t)kTraceIdRows * 8));
-  // imported rows (halo + other GPUs' trace rows) and the selections that produce them
+  // other GPUs' trace rows and the selection of this GPU's; the generations' state
   rows_ = dalloc<int>(16);
   tmax_ = dalloc<unsigned long long>(1);
-  halo_n_ = dalloc<uint32_t>(nb_);
+  HIPCHECK(hipMemset(tmax_, 0, 8));
   remote_n_ = dalloc<uint32_t>(nb_);
-  HIPCHECK(hipMemset(halo_n_, 0, nb_ * 4));
   HIPCHECK(hipMemset(remote_n_, 0, nb_ * 4));
+  gen_ = dalloc<GenMeta>(1);
+  {
+    GenMeta g{};
+    g.cur = (uint32_t)gens_ - 1;  // the first window's k_gen_begin moves to slot 0
+    for (int a = 0; a < kMaxGens; ++a) g.cut[a] = INT64_MAX;
+    HIPCHECK(hipMemcpy(gen_, &g, sizeof(g), hipMemcpyHostToDevice));
+  }
   sel_cnt_ = dalloc<uint32_t>(1024);
   sel_off_ = dalloc<uint32_t>(1024);
   for (int b = 0; b < nb_; ++b) imp_.push_back(cfg_.import_cap ? dalloc<SigRec>(cfg_.import_cap) : nullptr);
@@ -226,9 +235,11 @@ void WindowEngine::alloc() {
   g_part_off_ = dalloc<uint32_t>((size_t)(nblk_sig_ + nblk_imp_) * kKeyTypes * kParts);
   for (int b = 0; b < nb_; ++b) xchg_done_.push_back(mk_event(false));
   g_part_tot_ = dalloc<uint32_t>(kKeyTypes * kParts);
-  g_part_base_ = dalloc<uint32_t>(kKeyTypes * kParts + 1);
-  g_items_ = dalloc<uint32_t>(kKeyTypes * N);
-  g_rec_ = dalloc<SigRec>(N);
+  g_part_base_ = dalloc<uint32_t>((size_t)gens_ * kBaseLen);
+  // resident generations: rows, partition lists, list keys and offsets of the last gens_ windows
+  g_items_ = dalloc<uint32_t>((size_t)gens_ * kKeyTypes * N);
+  g_keys_ = dalloc<KeyTs>((size_t)gens_ * kKeyTypes * N);
+  g_rec_ = dalloc<SigRec>((size_t)gens_ * N);
   s_part_ = dalloc<PartCodes>(S);
   s_part_blk_ = dalloc<uint32_t>((size_t)nblk_span_ * kKeyTypes * kParts);
   s_part_off_ = dalloc<uint32_t>((size_t)nblk_span_ * kKeyTypes * kParts);
@@ -283,7 +294,7 @@ WindowEngine::~WindowEngine() {
                   g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
                   s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
                   hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_hash_,
-                  rows_, tmax_, halo_n_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_};
+                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_, g_keys_, gen_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_) hipStreamDestroy(copy_);
@@ -292,7 +303,9 @@ WindowEngine::~WindowEngine() {
   if (comm_stream_ && comm_stream_ != compute_) hipStreamDestroy(comm_stream_);
 }
 
-SignalCols WindowEngine::sig_cols() const { return SignalCols{g_rec_, g_status_, g_part_}; }
+SignalCols WindowEngine::sig_cols() const {
+  return SignalCols{g_rec_, g_status_, g_part_, g_items_, g_keys_, g_part_base_, gen_, (int64_t)n_rows_, gens_};
+}
 SpanCols WindowEngine::span_cols() const { return SpanCols{s_rec_, s_part_}; }
 
 bool WindowEngine::register_host(const void* ptr, size_t bytes) {
@@ -371,6 +384,8 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   pred_ = reinterpret_cast<int32_t*>(r + o_pred);
   evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
   sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
+  // the next generation slot and the halo cut-offs (reads the finished window's tmax: first)
+  launch_gen_begin(gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), st);
   FillList fl{};
   auto add = [&](void* p, size_t bytes, uint32_t v) { fl.seg[fl.count++] = FillSeg{(uint32_t*)p, (uint32_t)(bytes / 4), v}; };
   add(hist_, kSlots * kBuckets * 4, 0);
@@ -393,48 +408,41 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   rs.seg[2] = FillSeg{remote_n_ + b, 1, 0};        // other GPUs' rows: none until merged
   rs.count = 3;
   hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, rs);
-  launch_window_rows(counts, halo_n_ + b, remote_n_ + b, N, rows_, st);
+  launch_window_rows(counts, remote_n_ + b, N, rows_, gen_, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                        ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st, 0, 0, 0,
                        cfg_.shard_rank, cfg_.shard_world);
   if (xchg)  // this window's warn-level trace-tagged rows, as the other GPUs will import them
-    launch_select(g_rec_, g_status_, rows_, counts, N, kSelTrace, tmax_, 0, sel_cnt_, sel_off_, xsend_ + sizeof(XRec),
-                  reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, true, st);
+    launch_select(sig_cols(), rows_, counts, N, sel_cnt_, sel_off_, reinterpret_cast<XRec*>(xsend_ + sizeof(XRec)),
+                  reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, st);
 }
 
-// Part 2: [the other GPUs' rows] -> partition -> spans -> join -> posterior -> packet, and the
-// next window's halo.
+// Part 2: [the other GPUs' rows] -> partition -> spans -> join (this window's spans x every
+// generation's visible rows) -> posterior -> packet.
 void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, hipStream_t st, bool xchg) {
   uint8_t* in = in_dev_[b];
   const int* counts = reinterpret_cast<const int*>(in);
   const int32_t* labels = reinterpret_cast<const int32_t*>(in + kHeadBytes);
   const int N = n_rows_, S = cfg_.span_cap, G = cfg_.group_cap;
-  const int bn = (b + 1) % nb_;
   if (xchg) {
     const TraceIds tt{trace_hash_, kTraceIdRows};
     launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                          ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st,
                          1, nblk_imp_, nblk_sig_, cfg_.shard_rank, cfg_.shard_world);
   }
-  {  // this buffer's imports are consumed
-    FillList z{};
-    z.seg[0] = FillSeg{halo_n_ + b, 1, 0};
-    z.count = 1;
-    hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, z);
-  }
   if (xchg)
-    launch_partition(g_part_, rows_, N, nblk_sig_ + nblk_imp_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_,
-                     g_items_, st, nblk_sig_);
+    launch_partition_sig(sig_cols(), rows_, N, nblk_sig_ + nblk_imp_, g_part_blk_, g_part_off_, g_part_tot_, st,
+                         nblk_sig_);
   else
-    launch_partition(g_part_, rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, g_part_base_, g_items_, st);
-  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world};
+    launch_partition_sig(sig_cols(), rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, st);
+  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_};
   launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
-  launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), g_items_, g_part_base_, N, S, jp_, top3_, cnt_,
-               n_groups, gsum_, gcnt_, dbg_, probe_work_, st);
+  launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), S, jp_, top3_, cnt_, n_groups, gsum_, gcnt_, dbg_,
+               probe_work_, st);
   launch_finalize(counts + 1, S, top3_, cnt_, sig_cols(), span_cols(), jp_, nullptr, attrs_, conf_, kernel_ms_,
                   n_groups, gsum_, gcnt_, feat_, dbg_, st);
   const PosteriorModel* pm = reinterpret_cast<const PosteriorModel*>(model_dev_);
@@ -446,11 +454,6 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
                      confusion_, st);
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
                      stats_, stats_count_, ring_state_, packet_dev_[b]);
-  // the next window's halo: this window's rows (all of them: records, halo, other GPUs' rows)
-  // within the join window of its latest local record
-  if (cfg_.halo_ms > 0 && cfg_.import_cap > 0)
-    launch_select(g_rec_, g_status_, rows_ + 1, counts, N, kSelHalo, tmax_, (long long)llround(cfg_.halo_ms * 1e6),
-                  sel_cnt_, sel_off_, imp_[bn], halo_n_ + bn, (uint32_t)cfg_.import_cap, false, st);
 }
 
 // Launch a chain part eagerly, or through its captured graph (captured on the buffer's second
@@ -586,21 +589,19 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     if (injected) {  // rows as the other GPUs would have delivered them (tests, replays)
       HIPCHECK(hipMemcpyAsync(xrecv_, inject_.data(), inject_.size(), hipMemcpyHostToDevice, compute_));
       HIPCHECK(hipStreamSynchronize(compute_));  // the host copy is released below
-      launch_remote_merge(xrecv_, inject_stride_, inject_world_, inject_me_, imp_[b], halo_n_ + b, remote_n_ + b,
+      launch_remote_merge(xrecv_, inject_stride_, inject_world_, inject_me_, imp_[b], remote_n_ + b,
                           (uint32_t)cfg_.import_cap, cfg_.xchg_cap, compute_);
       inject_.clear();
-      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), halo_n_ + b, remote_n_ + b, n_rows_, rows_,
-                         compute_);
+      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, compute_);
     } else {
       // every use of the communicator stays on the comm stream (one stream, one issue order on
       // every rank): the compute stream hands over after part 1 and waits for the merge
       HIPCHECK(hipEventRecord(xchg_done_[b], compute_));
       HIPCHECK(hipStreamWaitEvent(comm_stream_, xchg_done_[b], 0));
       NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, comm_, comm_stream_));
-      launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[b], halo_n_ + b, remote_n_ + b,
-                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, comm_stream_);
-      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), halo_n_ + b, remote_n_ + b, n_rows_, rows_,
-                         comm_stream_);
+      launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[b], remote_n_ + b, (uint32_t)cfg_.import_cap,
+                          cfg_.xchg_cap, comm_stream_);
+      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, comm_stream_);
       HIPCHECK(hipEventRecord(xchg_done_[b], comm_stream_));
       HIPCHECK(hipStreamWaitEvent(compute_, xchg_done_[b], 0));
     }
@@ -750,13 +751,17 @@ std::vector<int64_t> WindowEngine::import_state() {
   sync();
   int rows[2];
   unsigned long long tmax = 0;
-  std::vector<uint32_t> h(nb_), r(nb_);
+  GenMeta g{};
+  std::vector<uint32_t> r(nb_);
   HIPCHECK(hipMemcpy(rows, rows_, sizeof(rows), hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(&tmax, tmax_, 8, hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(h.data(), halo_n_, 4 * nb_, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(&g, gen_, sizeof(g), hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(r.data(), remote_n_, 4 * nb_, hipMemcpyDeviceToHost));
-  std::vector<int64_t> out{rows[0], rows[1], (int64_t)tmax};
-  for (int b = 0; b < nb_; ++b) out.push_back(h[b]);
+  // rows[0..1], tmax, generations, current slot, windows held, per age: cut-off and rows, per
+  // buffer: other GPUs' rows
+  std::vector<int64_t> out{rows[0], rows[1], (int64_t)tmax, gens_, g.cur, g.filled};
+  for (int a = 0; a < kMaxGens; ++a) out.push_back(g.cut[a]);
+  for (int a = 0; a < kMaxGens; ++a) out.push_back(a < gens_ ? g.n_rows[(g.cur + gens_ - a) % gens_] : 0);
   for (int b = 0; b < nb_; ++b) out.push_back(r[b]);
   return out;
 }

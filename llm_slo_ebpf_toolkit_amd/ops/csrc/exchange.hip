@@ -1,17 +1,22 @@
-// Window-to-window and GPU-to-GPU record exchange of the native engine.
+// Window-to-window and GPU-to-GPU rows of the native engine.
 //
-//   halo   : the decoded rows of window k whose timestamps lie within the join window of the
-//            window's latest local record are carried into window k+1 as imported rows, so a
-//            span early in window k+1 still finds the signals recorded just before the cut
-//            (REF correlates against a continuous 2 s buffer, pkg/correlation/dns.go:12).
+//   halo   : window k+1 also joins the decoded rows of earlier windows whose timestamps lie within
+//            halo_ms of the latest local record of every window since (REF correlates against a
+//            continuous 2 s buffer, pkg/correlation/dns.go:12), so a span early in window k+1
+//            still finds the signals recorded just before the cut. The rows stay where their own
+//            window decoded them: the engine keeps up to kMaxGens generations of rows, partition
+//            lists and list keys resident, and k_gen_begin turns the generations' anchors into
+//            per-age visibility cut-offs that the probe applies while it streams the lists (the
+//            rows a chain of per-window halo selections would carry forward, with no copy, no
+//            re-decode and no re-partition of them).
 //   remote : each GPU's trace-tagged local rows of window k at warn level or above (the
 //            evidence; identity dropped: only their trace hash can join) are all-gathered over
-//            RCCL on the comm stream as 32-byte XRecs and imported into window k+1 on every other
-//            GPU, so a request traced across nodes joins the elevated signals of every node that
-//            saw it.
+//            RCCL on the comm stream as 32-byte XRecs and appended to the same window's rows on
+//            every other GPU, so a request traced across nodes joins the elevated signals of
+//            every node that saw it.
 //
-// Both are stable stream compactions (count -> exclusive scan -> ordered scatter), so the
-// imported rows, and with them the join's tie-breaks by row index, are deterministic.
+// The trace-row selection is a stable stream compaction (count -> exclusive scan -> ordered
+// scatter), so the exchanged rows, and with them the join's tie-breaks by row, are deterministic.
 #include "mislo_common.h"
 #include "mislo_launch.h"
 
@@ -22,35 +27,32 @@ namespace {
 constexpr int kSelNT = 256;
 
 struct SelArgs {
-  const SigRec* rec;
-  const uint8_t* status;  // per row: 0 ok, 1 warn, 2 error
-  const int* rows;      // rows[0] = rows of the window (local + imported)
+  SignalCols gc;        // the current generation's rows
+  const int* rows;      // rows[0] = local rows of the window
   const int* counts;    // counts[0] = local rows
   int cap;
-  int mode;             // kSelHalo | kSelTrace
-  const unsigned long long* tmax;
-  long long halo_ns;
 };
 
-__device__ __forceinline__ int sel_end(const SelArgs& a) {
-  const int n = min(a.rows[0], a.cap);
-  return a.mode == kSelTrace ? min(a.counts[0], n) : n;
+__device__ __forceinline__ int sel_end(const SelArgs& a) { return min(a.counts[0], min(a.rows[0], a.cap)); }
+
+__device__ __forceinline__ const SigRec* sel_rows(const SelArgs& a) {
+  return a.gc.rec + (size_t)cur_slot(a.gc) * (size_t)a.gc.stride;
 }
 
-__device__ __forceinline__ bool selected(const SelArgs& a, const SigRec& r, int i, unsigned long long tmax) {
+// a warn-level (or worse) trace-tagged joinable local row
+__device__ __forceinline__ bool selected(const SelArgs& a, const SigRec& r, int i) {
   if (r.slot == kNoSlot || r.ts == 0) return false;
-  if (a.mode == kSelTrace) return r.tr != 0 && a.status[i] >= 1;
-  return tmax != 0 && r.ts >= (long long)tmax - a.halo_ns;
+  return r.tr != 0 && a.gc.status[i] >= 1;
 }
 
 // per-block counts of selected rows (fixed grid; block b owns a contiguous chunk)
 __global__ __launch_bounds__(kSelNT) void k_sel_count(SelArgs a, uint32_t* __restrict__ blk_cnt) {
   const int n = sel_end(a);
-  const unsigned long long tmax = *a.tmax;
+  const SigRec* rec = sel_rows(a);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   uint32_t c = 0;
-  for (int i = beg + threadIdx.x; i < end; i += kSelNT) c += selected(a, a.rec[i], i, tmax) ? 1u : 0u;
+  for (int i = beg + threadIdx.x; i < end; i += kSelNT) c += selected(a, rec[i], i) ? 1u : 0u;
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
   __shared__ uint32_t s_w[kSelNT / 64];
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
@@ -81,12 +83,12 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
   if (t == 1023) *n_out = min(s[1023], out_cap);
 }
 
-// ordered scatter: block offset + wave offsets + in-wave ballot rank; full SigRec rows (halo)
-// or 32-byte exchange rows (XRec: no identity)
+// ordered scatter: block offset + wave offsets + in-wave ballot rank; 32-byte exchange rows
+// (XRec: no identity)
 __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_t* __restrict__ blk_off,
-                                                        void* __restrict__ out, uint32_t out_cap, int xrec) {
+                                                        XRec* __restrict__ out, uint32_t out_cap) {
   const int n = sel_end(a);
-  const unsigned long long tmax = *a.tmax;
+  const SigRec* rec = sel_rows(a);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
   const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
   __shared__ uint32_t s_w[kSelNT / 64];
@@ -99,8 +101,8 @@ __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_
     SigRec r{};
     bool s = false;
     if (i < end) {
-      r = a.rec[i];
-      s = selected(a, r, i, tmax);
+      r = rec[i];
+      s = selected(a, r, i);
     }
     const unsigned long long m = __ballot(s);
     const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
@@ -111,12 +113,7 @@ __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_
     for (int q = 0; q < w; ++q) wo += s_w[q];
     if (s) {
       const uint32_t dst = wo + rank;
-      if (dst < out_cap) {
-        if (xrec)  // a remote row joins through its trace hash only
-          static_cast<XRec*>(out)[dst] = XRec{r.ts, r.tr, r.val, r.slot, 0, 0};
-        else
-          static_cast<SigRec*>(out)[dst] = r;
-      }
+      if (dst < out_cap) out[dst] = XRec{r.ts, r.tr, r.val, r.slot, 0, 0};  // joins by its trace hash only
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -128,13 +125,11 @@ __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_
 }
 
 // other GPUs' exchanged rows (each rank's block: a 32-byte header holding its row count, then
-// XRec rows) appended after this window's halo rows as identity-free SigRecs, in rank order
+// XRec rows) as identity-free SigRecs, in rank order: appended to the window's own rows
 __global__ __launch_bounds__(256) void k_remote_merge(const uint8_t* __restrict__ xrecv, size_t stride, int world,
                                                       int me, SigRec* __restrict__ imp,
-                                                      const uint32_t* __restrict__ halo_n,
                                                       uint32_t* __restrict__ remote_n, uint32_t imp_cap) {
-  const uint32_t h = *halo_n;
-  uint32_t off = h;
+  uint32_t off = 0;
   for (int r = 0; r < world; ++r) {
     if (r == me) continue;
     const uint8_t* blk = xrecv + (size_t)r * stride;
@@ -152,19 +147,56 @@ __global__ __launch_bounds__(256) void k_remote_merge(const uint8_t* __restrict_
       }
     off += c;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *remote_n = (off < imp_cap ? off : imp_cap) - h;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *remote_n = off < imp_cap ? off : imp_cap;
 }
 
-// rows of the window: rows[0] = local records + the imported halo (decode segment 0),
-// rows[1] = rows[0] + other GPUs' rows (segment 1)
-__global__ void k_window_rows(const int* __restrict__ counts, const uint32_t* __restrict__ halo_n,
-                              const uint32_t* __restrict__ remote_n, int cap, int* __restrict__ rows) {
+// rows of the window: rows[0] = local records (decode segment 0), rows[1] = rows[0] + other
+// GPUs' rows (segment 1); the generation keeps both counts (the join's row classes)
+__global__ void k_window_rows(const int* __restrict__ counts, const uint32_t* __restrict__ remote_n, int cap,
+                              int* __restrict__ rows, GenMeta* __restrict__ gen) {
   if (threadIdx.x == 0) {
-    const long long a = (long long)counts[0] + *halo_n;
-    const long long r0 = a < cap ? a : cap;
+    const long long r0 = counts[0] < cap ? counts[0] : cap;
     const long long b = r0 + *remote_n;
     rows[0] = (int)r0;
     rows[1] = (int)(b < cap ? b : cap);
+    if (gen) {
+      gen->n_local[gen->cur] = (uint32_t)rows[0];
+      gen->n_rows[gen->cur] = (uint32_t)rows[1];
+    }
+  }
+}
+
+// Start of a window: the finished window's halo anchor (its latest local record), the next
+// slot (its old rows, kMaxGens windows back, drop out), and the visibility cut-off of every
+// age: a row of window k - a stays visible in window k while ts >= tmax_i - halo for every
+// window i in [k - a, k - 1] (a window without local records ends the chain, as an empty
+// selection would). Runs first in the window's graph, before tmax is reset.
+__global__ void k_gen_begin(GenMeta* __restrict__ g, const unsigned long long* __restrict__ tmax_prev, int gens,
+                            long long halo_ns) {
+  if (threadIdx.x != 0) return;
+  if (g->filled > 0) g->tmax_local[g->cur] = (int64_t)*tmax_prev;
+  const uint32_t cur = (g->cur + 1) % (uint32_t)gens;
+  g->cur = cur;
+  g->filled = min(g->filled + 1, (uint32_t)gens);
+  g->n_local[cur] = 0;
+  g->n_rows[cur] = 0;
+  g->tmax_local[cur] = 0;
+  g->tlo[cur] = ~0ull;
+  g->thi[cur] = 0ull;
+  g->span_lo = ~0ull;
+  g->span_hi = 0ull;
+  g->cut[0] = INT64_MIN;
+  bool ok = halo_ns > 0;
+  int64_t c = INT64_MIN;
+  for (int a = 1; a < kMaxGens; ++a) {
+    if (ok && a < gens && (uint32_t)a < g->filled) {
+      const int64_t tm = g->tmax_local[(cur + (uint32_t)(gens - a)) % (uint32_t)gens];
+      if (tm == 0) ok = false;
+      else c = max(c, tm - (int64_t)halo_ns);
+    } else {
+      ok = false;
+    }
+    g->cut[a] = ok ? c : INT64_MAX;
   }
 }
 
@@ -175,27 +207,30 @@ int select_grid(int cap) {
   return g < 1 ? 1 : (g > 1024 ? 1024 : g);
 }
 
-void launch_select(const SigRec* rec, const uint8_t* status, const int* rows, const int* counts, int cap, int mode,
-                   const unsigned long long* tmax, long long halo_ns, uint32_t* blk_cnt, uint32_t* blk_off, void* out,
-                   uint32_t* n_out, uint32_t out_cap, bool xrec, hipStream_t stream) {
-  const SelArgs a{rec, status, rows, counts, cap, mode, tmax, halo_ns};
+void launch_select(const SignalCols& gc, const int* rows, const int* counts, int cap, uint32_t* blk_cnt,
+                   uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream) {
+  const SelArgs a{gc, rows, counts, cap};
   const int g = select_grid(cap);
   hipLaunchKernelGGL(k_sel_count, dim3(g), dim3(kSelNT), 0, stream, a, blk_cnt);
   hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap);
-  hipLaunchKernelGGL(k_sel_scatter, dim3(g), dim3(kSelNT), 0, stream, a, blk_off, out, out_cap, xrec ? 1 : 0);
+  hipLaunchKernelGGL(k_sel_scatter, dim3(g), dim3(kSelNT), 0, stream, a, blk_off, out, out_cap);
 }
 
-void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, const uint32_t* halo_n,
-                         uint32_t* remote_n, uint32_t imp_cap, int max_rows, hipStream_t stream) {
+void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, uint32_t* remote_n,
+                         uint32_t imp_cap, int max_rows, hipStream_t stream) {
   int g = (max_rows + 255) / 256;
   g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
-  hipLaunchKernelGGL(k_remote_merge, dim3(g), dim3(256), 0, stream, xrecv, stride, world, me, imp, halo_n, remote_n,
-                     imp_cap);
+  hipLaunchKernelGGL(k_remote_merge, dim3(g), dim3(256), 0, stream, xrecv, stride, world, me, imp, remote_n, imp_cap);
 }
 
-void launch_window_rows(const int* counts, const uint32_t* halo_n, const uint32_t* remote_n, int cap, int* rows,
+void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, int* rows, GenMeta* gen,
                         hipStream_t stream) {
-  hipLaunchKernelGGL(k_window_rows, dim3(1), dim3(64), 0, stream, counts, halo_n, remote_n, cap, rows);
+  hipLaunchKernelGGL(k_window_rows, dim3(1), dim3(64), 0, stream, counts, remote_n, cap, rows, gen);
+}
+
+void launch_gen_begin(GenMeta* gen, const unsigned long long* tmax_prev, int gens, long long halo_ns,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(k_gen_begin, dim3(1), dim3(64), 0, stream, gen, tmax_prev, gens, halo_ns);
 }
 
 }  // namespace mislo

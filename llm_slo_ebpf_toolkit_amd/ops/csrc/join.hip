@@ -78,8 +78,11 @@ __global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_
 }
 
 // exclusive scan of the kKeyTypes x kParts partition totals (one workgroup, 4 per thread)
+// (signals: into the current generation's offsets)
 constexpr int kBaseNT = kKeyTypes * kParts / 4;
-__global__ __launch_bounds__(kBaseNT) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base) {
+__global__ __launch_bounds__(kBaseNT) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base,
+                                                      const GenMeta* __restrict__ gen) {
+  if (gen) base += (size_t)gen->cur * kBaseLen;
   __shared__ uint32_t s[kBaseNT];
   const int t = threadIdx.x;
   uint32_t v[4];
@@ -134,6 +137,50 @@ __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ co
       const int c = k * kParts + pc.p[k];
       const uint32_t r = atomicAdd(&s_cnt[c], 1u);
       items[base[c] + my_off[c] + r] = (uint32_t)i;
+    }
+  }
+}
+
+// Signal scatter: the current generation's partition lists, each entry a row index plus the
+// row's (key hash, ts) for the list's key type, written once and streamed by the probe of this
+// window and of the later windows the rows stay in the halo for. The hashes are recomputed from
+// the row records (the decode kept only their partitions); the rows are read in order.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __restrict__ n_ptr, int cap,
+                                                    const uint32_t* __restrict__ part_off, int nblk_a) {
+  __shared__ uint32_t s_cnt[kKeyTypes * kParts];
+  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_cnt[i] = 0;
+  __syncthreads();
+  const uint32_t cur = cur_slot(gc);
+  const SigRec* rec = gc.rec + (size_t)cur * (size_t)gc.stride;
+  const uint32_t* base = gc.base + (size_t)cur * kBaseLen;
+  uint32_t* items = gc.items + (size_t)cur * kKeyTypes * (size_t)gc.stride;
+  KeyTs* keys = gc.keys + (size_t)cur * kKeyTypes * (size_t)gc.stride;
+  // the row ranges of the decode blocks (see k_scatter)
+  const int n0 = min(n_ptr[0], cap);
+  const bool two = nblk_a < (int)gridDim.x;
+  const bool second = two && (int)blockIdx.x >= nblk_a;
+  const int s_beg = second ? n0 : 0;
+  const int s_end = second ? max(n0, min(n_ptr[1], cap)) : n0;
+  const int g = two ? (second ? (int)gridDim.x - nblk_a : nblk_a) : (int)gridDim.x;
+  const int bi = second ? (int)blockIdx.x - nblk_a : (int)blockIdx.x;
+  const int chunk = (s_end - s_beg + g - 1) / g;
+  const int beg = s_beg + bi * chunk, end = min(s_end, beg + chunk);
+  const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
+  for (int i = beg + threadIdx.x; i < end; i += NT) {
+    const PartCodes pc = gc.part[i];
+    if ((pc.p[0] & pc.p[1] & pc.p[2] & pc.p[3]) == kNoPart) continue;  // not joinable
+    const uint4* v = reinterpret_cast<const uint4*>(rec + i);
+    const uint4 a = v[0], b = v[1], c4 = v[2];
+    const int64_t ts = (int64_t)(((uint64_t)a.y << 32) | a.x);
+    const uint64_t tr = ((uint64_t)a.w << 32) | a.z, cn = ((uint64_t)b.y << 32) | b.x;
+#pragma unroll
+    for (int k = 0; k < kKeyTypes; ++k) {
+      if (pc.p[k] == kNoPart) continue;
+      const int c = k * kParts + pc.p[k];
+      const uint32_t pos = base[c] + my_off[c] + atomicAdd(&s_cnt[c], 1u);
+      items[pos] = (uint32_t)i;
+      keys[pos] = KeyTs{key_hash(k, tr, b.z, b.w, cn, c4.x), ts};
     }
   }
 }
@@ -223,8 +270,11 @@ constexpr int kSigPerItem = 4096;  // signals per work item (a partition's list 
 // graph-capturable). One workgroup of kParts threads, one partition per thread:
 //   work[0] / work[1]: item counts of phase 1 (trace) / phase 2 (pod+pid, pod+conn, svc+node)
 //   work[2] / work[3]: dequeue counters (zeroed here)
-//   items: code = key type << 28 | partition << 16 | slice << 8 | n slices.
-// Empty partitions get no item, so probe workgroups never wake for them. Phase-2 items are
+//   items: code = key type << 30 | generation age << 28 | sole << 26 | partition << 16 | slice << 8 |
+//          n slices (sole: the partition's only trace-phase item).
+// Empty partitions get no item, so probe workgroups never wake for them; nor does a generation
+// whose visible rows (ts >= its age's halo cut-off) all lie farther than the tier's window from
+// every span of the window (typically the oldest generation at the pod tiers). Phase-2 items are
 // placed longest first (LPT): a counting sort on an estimated cost class. The phase is a few
 // thousand items of very different sizes (a staging cost per item, then up to kSigPerItem
 // signals at a per-key-type rate) dequeued by 1024 workgroups, so its makespan is set by the
@@ -239,57 +289,78 @@ __device__ __forceinline__ uint32_t probe_item_class(int k, uint32_t n_sig, uint
   return min(cost >> 13, 63u);
 }
 
-__global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restrict__ span_base,
-                                                       const uint32_t* __restrict__ sig_base, int sig_per_item,
-                                                       uint32_t* __restrict__ work) {
-  __shared__ unsigned long long s[kParts];
+__global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restrict__ span_base, SignalCols gc,
+                                                       JoinParams jp, int sig_per_item, uint32_t* __restrict__ work) {
+  __shared__ unsigned long long s[kParts], s2[kParts];
   __shared__ uint32_t s_cls[64];
   const int p = threadIdx.x;
   if (p < 64) s_cls[p] = 0u;
-  uint32_t n[kKeyTypes];
+  const uint32_t cur = cur_slot(gc);
+  const GenMeta* gm = gc.gen;
+  // the window's span time range (without generations: no pruning)
+  const int64_t s_lo = gm ? ts_of_image(gm->span_lo) : INT64_MIN, s_hi = gm ? ts_of_image(gm->span_hi) : INT64_MAX;
+  uint32_t ns[kKeyTypes], ng[kKeyTypes][kMaxGens], n[kKeyTypes][kMaxGens], nk[kKeyTypes];
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
-    const int c = k * kParts + p;
-    const uint32_t ns = span_base[c + 1] - span_base[c], ng = sig_base[c + 1] - sig_base[c];
-    n[k] = (ns == 0 || ng == 0) ? 0u : min((ng + sig_per_item - 1) / (uint32_t)sig_per_item, (uint32_t)kProbeMaxSplit);
-  }
-  // packed inclusive scan: trace | pod+pid | pod+conn | svc+node counts, 16 bits each
-  const unsigned long long mine = (unsigned long long)n[0] | ((unsigned long long)n[1] << 16) |
-                                  ((unsigned long long)n[2] << 32) | ((unsigned long long)n[3] << 48);
-  s[p] = mine;
-  __syncthreads();
-  for (int off = 1; off < kParts; off <<= 1) {
-    const unsigned long long x = p >= off ? s[p - off] : 0ull;
-    __syncthreads();
-    s[p] += x;
-    __syncthreads();
-  }
-  const unsigned long long tot = s[kParts - 1], excl = s[p] - mine;
-  uint32_t t[kKeyTypes], e[kKeyTypes];
-#pragma unroll
-  for (int k = 0; k < kKeyTypes; ++k) {
-    t[k] = (uint32_t)((tot >> (16 * k)) & 0xFFFF);
-    e[k] = (uint32_t)((excl >> (16 * k)) & 0xFFFF);
-  }
-  uint32_t* items1 = work + 4;
-  uint32_t* items2 = work + 4 + kParts * kProbeMaxSplit;
-  for (uint32_t j = 0; j < n[0]; ++j) items1[e[0] + j] = (0u << 28) | ((uint32_t)p << 16) | (j << 8) | n[0];
-  // phase 2: count items per cost class (slot 0 = most expensive), scan, place
-  uint32_t ns[kKeyTypes], ng[kKeyTypes];
-#pragma unroll
-  for (int k = 1; k < kKeyTypes; ++k) {
     const int c = k * kParts + p;
     ns[k] = span_base[c + 1] - span_base[c];
-    ng[k] = sig_base[c + 1] - sig_base[c];
+    nk[k] = 0;
+    const int64_t w = jp.win_ns[k];
+#pragma unroll
+    for (int a = 0; a < kMaxGens; ++a) {
+      ng[k][a] = 0;
+      n[k][a] = 0;
+      if (a >= gc.gens || ns[k] == 0) continue;
+      const uint32_t slot = age_slot(gc, cur, a);
+      if (gm) {
+        if ((uint32_t)a >= gm->filled || gm->tlo[slot] > gm->thi[slot]) continue;
+        const int64_t lo = max(ts_of_image(gm->tlo[slot]), gm->cut[a]), hi = ts_of_image(gm->thi[slot]);
+        if (lo > hi || hi < s_lo - w || lo > s_hi + w) continue;  // nothing visible can pair
+      }
+      const uint32_t* b = gc.base + (size_t)slot * kBaseLen;
+      ng[k][a] = b[c + 1] - b[c];
+      n[k][a] = ng[k][a] == 0 ? 0u : min((ng[k][a] + sig_per_item - 1) / (uint32_t)sig_per_item, (uint32_t)kProbeMaxSplit);
+      nk[k] += n[k][a];
+    }
   }
-  auto slice = [&](int k, uint32_t j) {  // signals of slice j (k_probe's split rule)
-    const uint32_t per = (ng[k] + n[k] - 1) / n[k];
-    const uint32_t a = j * per;
-    return a >= ng[k] ? 0u : min(ng[k], a + per) - a;
+  // packed inclusive scans: trace | pod+pid and pod+conn | svc+node item counts, 32 bits each
+  const unsigned long long mine = (unsigned long long)nk[0] | ((unsigned long long)nk[1] << 32);
+  const unsigned long long mine2 = (unsigned long long)nk[2] | ((unsigned long long)nk[3] << 32);
+  s[p] = mine;
+  s2[p] = mine2;
+  __syncthreads();
+  for (int off = 1; off < kParts; off <<= 1) {
+    const unsigned long long x = p >= off ? s[p - off] : 0ull, x2 = p >= off ? s2[p - off] : 0ull;
+    __syncthreads();
+    s[p] += x;
+    s2[p] += x2;
+    __syncthreads();
+  }
+  const unsigned long long tot = s[kParts - 1], tot2 = s2[kParts - 1], excl = s[p] - mine;
+  const uint32_t t[kKeyTypes] = {(uint32_t)tot, (uint32_t)(tot >> 32), (uint32_t)tot2, (uint32_t)(tot2 >> 32)};
+  uint32_t* items1 = work + 4;
+  uint32_t* items2 = work + 4 + kProbePhaseItems;
+  auto code = [&](int k, int a, uint32_t j) {
+    return ((uint32_t)k << 30) | ((uint32_t)a << 28) | ((uint32_t)p << 16) | (j << 8) | n[k][a];
+  };
+  {
+    uint32_t pos = (uint32_t)excl;
+    const uint32_t sole = nk[0] == 1 ? 1u << 26 : 0u;
+#pragma unroll
+    for (int a = 0; a < kMaxGens; ++a)
+      for (uint32_t j = 0; j < n[0][a]; ++j) items1[pos++] = code(0, a, j) | sole;
+  }
+  // phase 2: count items per cost class (slot 0 = most expensive), scan, place
+  auto slice = [&](int k, int a, uint32_t j) {  // signals of slice j (k_probe's split rule)
+    const uint32_t per = (ng[k][a] + n[k][a] - 1) / n[k][a];
+    const uint32_t lo = j * per;
+    return lo >= ng[k][a] ? 0u : min(ng[k][a], lo + per) - lo;
   };
 #pragma unroll
   for (int k = 1; k < kKeyTypes; ++k)
-    for (uint32_t j = 0; j < n[k]; ++j) atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, j), ns[k])], 1u);
+#pragma unroll
+    for (int a = 0; a < kMaxGens; ++a)
+      for (uint32_t j = 0; j < n[k][a]; ++j) atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, a, j), ns[k])], 1u);
   __syncthreads();
   if (p == 0) {
     uint32_t run = 0;
@@ -302,10 +373,12 @@ __global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restric
   __syncthreads();
 #pragma unroll
   for (int k = 1; k < kKeyTypes; ++k)
-    for (uint32_t j = 0; j < n[k]; ++j) {
-      const uint32_t pos = atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, j), ns[k])], 1u);
-      items2[pos] = ((uint32_t)k << 28) | ((uint32_t)p << 16) | (j << 8) | n[k];
-    }
+#pragma unroll
+    for (int a = 0; a < kMaxGens; ++a)
+      for (uint32_t j = 0; j < n[k][a]; ++j) {
+        const uint32_t pos = atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, a, j), ns[k])], 1u);
+        items2[pos] = code(k, a, j);
+      }
   if (p == 0) {
     work[0] = t[0];
     work[1] = t[1] + t[2] + t[3];
@@ -365,9 +438,7 @@ __device__ __forceinline__ int lower_u16(const uint16_t* v, int n, int x) {
 
 template <int NT>
 __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
-                                              const uint32_t* __restrict__ span_base, SignalCols gc,
-                                              const uint32_t* __restrict__ sig_items,
-                                              const uint32_t* __restrict__ sig_base, int sig_cap, int span_cap,
+                                              const uint32_t* __restrict__ span_base, SignalCols gc, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups,
                                               unsigned long long* __restrict__ gsum, uint32_t* __restrict__ gcnt,
@@ -410,7 +481,8 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
   const bool cand1 = jp.conf[1] >= jp.threshold, cand2 = jp.conf[2] >= jp.threshold;
   unsigned long long n_cand = 0, n_low = 0, n_overlap = 0;
   const uint32_t n_work = work[phase];
-  const uint32_t* items = work + 4 + (phase ? kParts * kProbeMaxSplit : 0);
+  const uint32_t* items = work + 4 + (phase ? kProbePhaseItems : 0);
+  const uint32_t cur = cur_slot(gc);
 
   // dynamic work queue: one item = (key type, partition, signal slice)
   for (;;) {
@@ -423,11 +495,24 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
     unsigned long long pt = clock64(), p_stage = 0, p_sig = 0, p_flush = 0;
 #endif
     const uint32_t code = items[it];
-    const int k = (int)(code >> 28);
+    const int k = (int)(code >> 30);
+    const int age = (int)((code >> 28) & 3u);
     const int part = (int)((code >> 16) & 0x3FF);
     const uint32_t si = (code >> 8) & 0xFF, nsplit = code & 0xFF;
     const int c = k * kParts + part;
     const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
+    // the item's generation: its rows, lists and keys, its halo cut-off, and the row classes of
+    // the top-3 key (this window's local rows, then older windows' local rows, then the other
+    // GPUs' rows oldest first: the order of [rows | halo | remote] under nested halo selections)
+    const uint32_t gslot = age_slot(gc, cur, age);
+    const uint32_t* sig_base = gc.base + (size_t)gslot * kBaseLen;
+    const uint32_t* sig_items = gc.items + (size_t)gslot * kKeyTypes * (size_t)gc.stride;
+    const KeyTs* sig_keys = gc.keys + (size_t)gslot * kKeyTypes * (size_t)gc.stride;
+    const SigRec* grec = gc.rec + (size_t)gslot * (size_t)gc.stride;
+    const int64_t cut = gc.gen ? gc.gen->cut[age] : INT64_MIN;
+    const uint32_t n_loc = gc.gen ? gc.gen->n_local[gslot] : 0xFFFFFFFFu;
+    const uint32_t cls_loc = (uint32_t)age * (uint32_t)gc.stride;
+    const uint32_t cls_rem = (uint32_t)(2 * gc.gens - 1 - age) * (uint32_t)gc.stride;
     const uint32_t gb0 = sig_base[c], gb1 = sig_base[c + 1];
     const uint32_t per = (gb1 - gb0 + nsplit - 1) / nsplit;
     const uint32_t sg0 = gb0 + si * per;
@@ -550,38 +635,70 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
     { const unsigned long long t = clock64(); p_stage += t - pt; pt = t; }
 #endif
 
-    // Signal records are random 64-byte gathers (from the Infinity Cache at best), so the loop
-    // keeps kDepth of them in flight per lane -- records kDepth iterations ahead, their indices
-    // one further -- and each iteration's LDS work overlaps the next ones' loads. The workgroup's
-    // LDS already caps the CU at 4 waves per SIMD, which leaves registers for the deeper queue
-    // (one record ahead: 2.2 TB/s of gathers, 72 % of wave time waiting; r3 PMC). Two fit in 128
-    // VGPRs (4 waves per SIMD, the LDS limit); three spill.
-    constexpr int kDepth = 2;
+    // The item's list entries -- (key hash, ts) and the row index, 20 coalesced bytes per lane --
+    // stream kDepth iterations ahead. A signal's 48-byte row record (a random gather) is needed
+    // only when its key run holds a span within the tier's window: the broad tier counts from
+    // the keys alone, older generations' rows outside the halo and rows with no span in reach
+    // cost no gather. A matching signal's search and gather are issued one iteration ahead of
+    // its accounting, so the gather overlaps the previous signal's LDS work.
+    constexpr int kDepth = 1;
     uint32_t q = sg0 + threadIdx.x;
-    uint32_t gi[kDepth + 1];
-    SigHot rq[kDepth];
+    KeyTs kq[kDepth];
+    uint32_t iq[kDepth];
 #pragma unroll
-    for (int d = 0; d <= kDepth; ++d) gi[d] = q + d * NT < sg1 ? sig_items[q + d * NT] : 0u;
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d) rq[d] = q + d * NT < sg1 ? load_hot(gc.rec + gi[d]) : SigHot{};
+    for (int d = 0; d < kDepth; ++d) {
+      const bool ok = q + (d + 1) * NT < sg1;
+      kq[d] = ok ? sig_keys[q + (d + 1) * NT] : KeyTs{0ull, INT64_MIN};
+      iq[d] = ok ? sig_items[q + (d + 1) * NT] : 0u;
+    }
+    // stage 1 of an element: halo visibility, the span-run search, the record gather on a hit
+    auto stage1 = [&](const KeyTs& e, uint32_t idx, bool valid, int& lo, bool& vis, bool& hit, SigHot& r) {
+      vis = valid && e.t >= cut;
+      hit = false;
+      lo = 0;
+      if (!vis) return;
+      lo = lower_ht(s_kt, 0, m, e.h, e.t - w);
+      if (count_only) return;
+      hit = lo < m && s_kt[lo].h == e.h && s_kt[lo].t <= e.t + w;
+      if (hit) r = load_hot(grec + idx);
+    };
+    KeyTs e0 = q < sg1 ? sig_keys[q] : KeyTs{0ull, INT64_MIN};
+    uint32_t i0 = q < sg1 ? sig_items[q] : 0u;
+    int lo0;
+    bool vis0, hit0;
+    SigHot r0{};
+    stage1(e0, i0, q < sg1, lo0, vis0, hit0, r0);
     for (; q < sg1; q += NT) {
-      const uint32_t g = gi[0];
-      const SigHot r = rq[0];
+      const KeyTs e1 = kq[0];
+      const uint32_t i1 = iq[0];
 #pragma unroll
-      for (int d = 0; d < kDepth; ++d) gi[d] = gi[d + 1];
-#pragma unroll
-      for (int d = 0; d + 1 < kDepth; ++d) rq[d] = rq[d + 1];
-      if (q + kDepth * NT < sg1) rq[kDepth - 1] = load_hot(gc.rec + gi[kDepth - 1]);
-      gi[kDepth] = q + (kDepth + 1) * NT < sg1 ? sig_items[q + (kDepth + 1) * NT] : 0u;
-      const uint64_t h = key_hash(k, r.tr, r.pod, r.pid, r.cn, r.sn);
-      const int64_t t = r.ts;
-      const int lo = lower_ht(s_kt, 0, m, h, t - w);
+      for (int d = 0; d + 1 < kDepth; ++d) {
+        kq[d] = kq[d + 1];
+        iq[d] = iq[d + 1];
+      }
+      {
+        const bool ok = q + (kDepth + 1) * NT < sg1;
+        kq[kDepth - 1] = ok ? sig_keys[q + (kDepth + 1) * NT] : KeyTs{0ull, INT64_MIN};
+        iq[kDepth - 1] = ok ? sig_items[q + (kDepth + 1) * NT] : 0u;
+      }
+      int lo1;
+      bool vis1, hit1;
+      SigHot r1{};
+      stage1(e1, i1, q + NT < sg1, lo1, vis1, hit1, r1);
+      // stage 2: this element's accounting
+      do {
+      if (!vis0) break;
+      const uint64_t h = e0.h;
+      const int64_t t = e0.t;
+      const int lo = lo0;
       const int64_t thi = t + w;
       if (count_only) {
         n_low += (unsigned long long)(upper_ht(s_kt, lo, m, h, thi) - lo);
-        continue;
+        break;
       }
-      if (lo >= m || s_kt[lo].h != h || s_kt[lo].t > thi) continue;
+      if (!hit0) break;
+      const SigHot r = r0;
+      const uint32_t g = (i0 < n_loc ? cls_loc : cls_rem) + i0;  // top-3 key row id
       const uint32_t g_pod = r.pod, g_pid = r.pid, g_sn = r.sn;
       const uint64_t g_tr = r.tr, g_cn = r.cn;
       const int g_slot = (int)r.slot;
@@ -635,7 +752,7 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
               }
             }
           }
-          continue;
+          break;
         }
       }
 
@@ -714,6 +831,13 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
         }
       }
       add_group(run_grp, g_slot, g_milli, run_n);
+      } while (0);
+      e0 = e1;
+      i0 = i1;
+      lo0 = lo1;
+      vis0 = vis1;
+      hit0 = hit1;
+      r0 = r1;
     }
     // flush this chunk's per-span candidates to the global top-3 / counts
     __syncthreads();
@@ -722,9 +846,9 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
 #endif
     if (!count_only) {
       block_inclusive_scan<NT>(s_diff, m, s_wsum);  // difference array -> per-span counts
-      // phase 1, sole item of its partition: the only writer of these spans so far (a span
-      // has one trace key), so plain stores replace the atomic cascade
-      const bool sole = phase == 0 && nsplit == 1;
+      // phase 1, sole item of its partition (one slice of one generation): the only writer of
+      // these spans so far (a span has one trace key), so plain stores replace the atomic cascade
+      const bool sole = phase == 0 && ((code >> 26) & 1u);
       for (int i = threadIdx.x; i < m; i += NT) {
         const int nc = s_diff[i];
         const uint32_t s = s_i[i];
@@ -806,6 +930,7 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
     gcnt += stripe;
   }
   unsigned long long dropped = 0, enriched = 0;
+  const uint32_t cur = cur_slot(gc);
   if (s < ns) {
     float a[kSlots];
 #pragma unroll
@@ -817,8 +942,12 @@ __global__ __launch_bounds__(NT) void k_finalize(const int* __restrict__ ns_ptr,
       const unsigned long long key = top3[3ull * s + j];
       if (key == kEmpty || j >= keep) continue;
       const int tier = (int)(key >> 62);
+      // the key's row id: class * stride + row, class = generation age for local rows and
+      // 2 * gens - 1 - age for the other GPUs' rows (k_probe)
       const uint32_t g = (uint32_t)(key & ((1ull << kSigBits) - 1));
-      const SigRec& r = gc.rec[g];
+      const uint32_t cls = g / (uint32_t)gc.stride, row = g - cls * (uint32_t)gc.stride;
+      const int age = (int)cls < gc.gens ? (int)cls : 2 * gc.gens - 1 - (int)cls;
+      const SigRec& r = gc.rec[(size_t)age_slot(gc, cur, age) * (size_t)gc.stride + row];
       const int slot = (int)r.slot;
       const float v = r.val;
       // REF merge: attr = value if absent or value > existing
@@ -899,13 +1028,22 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 // host launchers
 // ---------------------------------------------------------------------------------------
 
+void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
+                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a) {
+  hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
+                     part_blk, nblk, part_off, part_tot);
+  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, gc.base, gc.gen);
+  hipLaunchKernelGGL((k_scatter_sig<1024>), dim3(nblk), dim3(1024), 0, stream, gc, n_dev, cap, part_off,
+                     nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk);
+}
+
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream, int nblk_a) {
   static_assert((kKeyTypes * kParts) % kScanCols == 0, "scan columns tile the partition matrix");
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
                      part_blk, nblk, part_off, part_tot);
-  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, part_base);
+  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, part_base, nullptr);
   // 1024 threads per workgroup: the grid is one workgroup per decode block (<= 256), so 256
   // threads left 4 waves per CU to hide the scattered stores and LDS atomics
   hipLaunchKernelGGL((k_scatter<1024>), dim3(nblk), dim3(1024), 0, stream, codes, n_dev, cap, part_off, part_base,
@@ -913,9 +1051,9 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
 }
 
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
-                  const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
-                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
-                  uint32_t* gcnt, unsigned long long* dbg, uint32_t* work, hipStream_t stream) {
+                  int span_cap, const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups,
+                  unsigned long long* gsum, uint32_t* gcnt, unsigned long long* dbg, uint32_t* work,
+                  hipStream_t stream) {
   // phase 1: trace tier; phase 2: pod+pid, pod+conn, svc+node seeded with phase 1's top-3.
   // Both phases pull items from the device-built work list. Diagnostic knobs (read once):
   // MISLO_PROBE_GRID workgroups per phase, MISLO_PROBE_ITEM signals per work item.
@@ -929,10 +1067,10 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
     const int x = v ? atoi(v) : kSigPerItem;
     return x >= 1 ? x : kSigPerItem;
   }();
-  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, sig_base, per_item, work);
+  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, per_item, work);
   for (int phase = 0; phase < 2; ++phase)
-    hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, sc, span_items, span_base, gc, sig_items,
-                       sig_base, sig_cap, span_cap, jp, top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);
+    hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, sc, span_items, span_base, gc, span_cap, jp,
+                       top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);
 }
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,

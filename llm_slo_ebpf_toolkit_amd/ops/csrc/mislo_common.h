@@ -148,17 +148,58 @@ static_assert(sizeof(SigRec) == 64 && sizeof(SpanRec) == 64, "row records are on
 
 // Per-record partition codes of the 4 join keys (trace, pod+pid, pod+conn, svc+node):
 // the key hash's partition (top kPartBits bits) or kNoPart when the key is invalid. The
-// probe recomputes full hashes from the row records, so only 8 bytes per record are stored.
+// signal scatter recomputes full hashes from the row records (into the lists' KeyTs), so only
+// 8 bytes per record are stored.
 constexpr uint16_t kNoPart = 0xFFFF;
 struct alignas(8) PartCodes {
   uint16_t p[4];
 };
 
-struct SignalCols {
-  SigRec* rec;
-  uint8_t* status;    // 0 ok, 1 warning, 2 error
-  PartCodes* part;
+// One entry of a signal partition list: the row's key hash for the list's key type and its
+// timestamp, so the probe streams (hash, ts) in list order and gathers a row record only when
+// the key run holds a span within the tier's window.
+struct alignas(16) KeyTs {
+  uint64_t h;
+  int64_t t;
 };
+
+// Resident signal generations (the halo). The engine keeps the decoded rows, partition lists and
+// list keys of the last kMaxGens windows in place: window k joins the rows of windows k-1.. that
+// lie within halo_ms of every later window's latest local record -- the rows a chain of
+// per-window halo selections would have carried forward -- without re-copying, re-decoding or
+// re-partitioning them (engine.hip k_gen_begin). Generation slots rotate; everything here is
+// device state, so a captured window graph replays against whichever slot is current.
+constexpr int kMaxGens = 4;  // this window + up to 3 earlier ones (the top-3 key holds the age in 2 bits)
+struct GenMeta {
+  uint32_t cur;                    // slot of the window being processed
+  uint32_t filled;                 // windows held, this one included (<= gens)
+  uint32_t n_local[kMaxGens];      // per slot: node-local rows (the other GPUs' rows follow them)
+  uint32_t n_rows[kMaxGens];       // per slot: rows
+  int64_t tmax_local[kMaxGens];    // per slot: latest local joinable timestamp (the halo anchor; 0 = none)
+  uint64_t tlo[kMaxGens], thi[kMaxGens];  // per slot: joinable row time range (order-preserving u64 image)
+  int64_t cut[kMaxGens];           // per age: visible rows have ts >= cut (INT64_MAX: none visible)
+  uint64_t span_lo, span_hi;       // this window's joinable spans (u64 image)
+};
+// order-preserving unsigned image of a signed timestamp (atomicMin / atomicMax on u64)
+__host__ __device__ inline uint64_t ts_image(int64_t t) { return (uint64_t)t ^ 0x8000000000000000ull; }
+__host__ __device__ inline int64_t ts_of_image(uint64_t u) { return (int64_t)(u ^ 0x8000000000000000ull); }
+
+struct SignalCols {
+  SigRec* rec;          // [gens][stride] row records
+  uint8_t* status;      // this window's rows: 0 ok, 1 warning, 2 error
+  PartCodes* part;      // this window's rows
+  uint32_t* items = nullptr;  // [gens][kKeyTypes * stride] partition lists (row indices)
+  KeyTs* keys = nullptr;      // [gens][kKeyTypes * stride] the lists' (key hash, ts)
+  uint32_t* base = nullptr;   // [gens][kKeyTypes * kParts + 1] list offsets
+  GenMeta* gen = nullptr;     // nullptr: one generation (slot 0)
+  int64_t stride = 0;         // rows per generation
+  int gens = 1;
+};
+constexpr int kBaseLen = kKeyTypes * kParts + 1;  // list offsets per generation
+__device__ __forceinline__ uint32_t cur_slot(const SignalCols& c) { return c.gen ? c.gen->cur : 0u; }
+__device__ __forceinline__ uint32_t age_slot(const SignalCols& c, uint32_t cur, int age) {
+  return (cur + (uint32_t)(c.gens - age)) % (uint32_t)c.gens;
+}
 
 struct SpanCols {
   SpanRec* rec;

@@ -51,6 +51,7 @@ struct SpanMap {
   int n_groups;
   float ttft_slo_ms;
   int sh_rank = 0, sh_world = 1;  // group sharding: this GPU keeps groups g % sh_world == sh_rank as g / sh_world
+  GenMeta* gen = nullptr;         // receives the spans' time range (probe pruning of older generations)
 };
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
                          const uint32_t* ctx_tab, int n_ctx, hipStream_t stream, const SpanMap* sm = nullptr);
@@ -71,8 +72,7 @@ void launch_decode_window(const uint8_t* framed, const void* user, const int* n_
                           unsigned long long* misc, hipStream_t stream, int seg = 0, int grid = 0, int blk_base = 0,
                           int sh_rank = 0, int sh_world = 1);
 
-// exchange.hip: stable row selections (halo carry, trace-tagged rows for the GPU exchange)
-constexpr int kSelHalo = 0, kSelTrace = 1;
+// exchange.hip: the trace-tagged rows of the GPU exchange, the other GPUs' rows, the generations
 int select_grid(int cap);
 // 32-byte exchange row: what another GPU needs to join a row by its trace hash
 struct XRec {
@@ -83,13 +83,16 @@ struct XRec {
   uint32_t pad[2];
 };
 static_assert(sizeof(XRec) == 32, "exchange rows are 32 bytes");
-void launch_select(const SigRec* rec, const uint8_t* status, const int* rows, const int* counts, int cap, int mode,
-                   const unsigned long long* tmax, long long halo_ns, uint32_t* blk_cnt, uint32_t* blk_off, void* out,
-                   uint32_t* n_out, uint32_t out_cap, bool xrec, hipStream_t stream);
-void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, const uint32_t* halo_n,
-                         uint32_t* remote_n, uint32_t imp_cap, int max_rows, hipStream_t stream);
-void launch_window_rows(const int* counts, const uint32_t* halo_n, const uint32_t* remote_n, int cap, int* rows,
+// the current generation's warn-level trace-tagged local rows -> out (stable order), count -> n_out
+void launch_select(const SignalCols& gc, const int* rows, const int* counts, int cap, uint32_t* blk_cnt,
+                   uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream);
+void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, uint32_t* remote_n,
+                         uint32_t imp_cap, int max_rows, hipStream_t stream);
+void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, int* rows, GenMeta* gen,
                         hipStream_t stream);
+// next generation slot and the halo's per-age visibility cut-offs (see exchange.hip)
+void launch_gen_begin(GenMeta* gen, const unsigned long long* tmax_prev, int gens, long long halo_ns,
+                      hipStream_t stream);
 
 // join.hip
 // rows [0, n_dev[0]) decoded by nblk blocks; with split (nblk_a < nblk) the first nblk_a blocks
@@ -97,13 +100,20 @@ void launch_window_rows(const int* counts, const uint32_t* halo_n, const uint32_
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream, int nblk_a = 0);
+// signals: the current generation's lists (gc.items / gc.keys / gc.base) from gc.part and gc.rec
+void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
+                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a = 0);
+// spans of this window x every visible generation's signals
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
-                  const uint32_t* sig_items, const uint32_t* sig_base, int sig_cap, int span_cap,
-                  const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups, unsigned long long* gsum,
-                  uint32_t* gcnt, unsigned long long* dbg, uint32_t* work, hipStream_t stream);
-// probe work list: 4 header words + one word per (key type, partition, signal slice)
-constexpr int kProbeMaxSplit = 64;  // signal slices per (key type, partition); the item code holds 8 bits
-constexpr int kProbeProfOff = 4 + 4 * kParts * kProbeMaxSplit;  // MISLO_PROBE_PROFILE counters (u64 [4][8])
+                  int span_cap, const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups,
+                  unsigned long long* gsum, uint32_t* gcnt, unsigned long long* dbg, uint32_t* work,
+                  hipStream_t stream);
+// probe work list: 4 header words + per phase one word per (key type, generation, partition,
+// signal slice)
+constexpr int kProbeMaxSplit = 64;  // signal slices per (key type, generation, partition); 8 bits of the item code
+constexpr int kProbePhaseItems = kMaxGens * kParts * kProbeMaxSplit;  // per key type
+// phase 1 (trace) holds one key type's items, phase 2 three
+constexpr int kProbeProfOff = 4 + 4 * kProbePhaseItems;  // MISLO_PROBE_PROFILE counters (u64 [4][8])
 constexpr int kProbeWorkLen = kProbeProfOff + 64;
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,
                      const SignalCols& gc, const SpanCols& sc, const JoinParams& jp, const float* base_attrs,

@@ -1,21 +1,25 @@
-"""CPU model of the engine's per-window import protocol (ops/csrc/exchange.hip, engine.hip).
+"""CPU model of the engine's per-window row protocol (ops/csrc/exchange.hip, engine.hip).
 
 Per rank and window k, the device does:
 
-1. part 1: decode the window's records plus the halo it imported from window k-1 (rows
-   [counts[0], rows[0]): joined, never counted), and select this rank's trace-tagged local rows
-   at warn level or above as 32-byte XRecs (time, trace hash, value, signal: no pod / pid /
-   connection, so another GPU can only join them through the trace tier), capped at xchg_cap;
+1. part 1: decode the window's records (rows [0, counts[0])) into the current generation slot,
+   and select this rank's trace-tagged local rows at warn level or above as 32-byte XRecs (time,
+   trace hash, value, signal: no pod / pid / connection, so another GPU can only join them
+   through the trace tier), capped at xchg_cap;
 2. RCCL all-gather of every rank's fixed-size block [header: row count | XRecs] (comm stream);
-3. part 2: decode the other ranks' rows (rows [rows[0], rows[1])), join everything, and select
-   the next window's halo: rows (all of them) with a signal, a timestamp and
-   ts >= tmax - halo, tmax = the window's latest local record, in row order, capped at
-   import_cap; the next window's other-GPU rows are appended after it up to the same cap.
+3. part 2: decode the other ranks' rows after the window's own (capped at import_cap), partition
+   the generation, and join this window's spans against every resident generation: the window's
+   rows, and the rows of up to ``halo_windows`` earlier windows (their own records and the other
+   ranks' rows they imported) that carry a signal and a timestamp with ts >= tmax_i - halo for
+   every window i since theirs (tmax_i = window i's latest local record; a window without one
+   ends the chain).
 
-``ExchangeModel`` runs exactly that over the numpy oracle with a pluggable all-gather (a gloo
-process group in the tests, so the same bytes cross a real process boundary), making the
-multi-GPU semantics testable on CPU; the GPU test (test_native_engine) checks the device's
-selections and merge against the same oracle functions.
+The join's row order -- which breaks ties between equally close candidates -- is [this window's
+records | earlier windows' records, newest first | other ranks' rows, oldest window first], the
+order nested per-window halo selections would produce. ``ExchangeModel`` runs exactly that over
+the numpy oracle with a pluggable all-gather (a gloo process group in the tests, so the same
+bytes cross a real process boundary), making the multi-GPU semantics testable on CPU; the GPU
+test (test_native_engine) checks the device against the same oracle functions.
 """
 
 from __future__ import annotations
@@ -59,15 +63,17 @@ def torch_allgather(group=None) -> Callable[[np.ndarray], List[np.ndarray]]:
 
 
 class ExchangeModel:
-    """One rank's window chain with imports (halo + other ranks' trace rows)."""
+    """One rank's window chain: resident generations (the halo) + other ranks' trace rows."""
 
     def __init__(self, rank: int, world: int, halo_ms: float, import_cap: int, xchg_cap: int,
-                 allgather: Optional[Callable[[np.ndarray], List[np.ndarray]]] = None):
+                 allgather: Optional[Callable[[np.ndarray], List[np.ndarray]]] = None, halo_windows: int = 3):
         self.rank, self.world = rank, world
         self.halo_ns = int(round(halo_ms * 1e6))
         self.import_cap, self.xchg_cap = import_cap, xchg_cap
+        self.halo_windows = halo_windows
         self.allgather = allgather
-        self.imports = oracle.empty_rows()
+        self.gens: list = []                   # newest first: (local rows, other ranks' rows, tmax)
+        self.injected = oracle.empty_rows()    # other ranks' rows for the next window (tests)
         self.sent = 0
 
     def block(self, d_loc: oracle.Decoded) -> Optional[np.ndarray]:
@@ -78,18 +84,33 @@ class ExchangeModel:
         self.sent = min(len(mine.ts), self.xchg_cap)
         return oracle.exchange_blocks([mine], self.xchg_cap)
 
+    def halo(self) -> oracle.Decoded:
+        """The earlier generations' visible rows, in the join's row order (k_gen_begin cut-offs)."""
+        if self.halo_ns <= 0:
+            return oracle.empty_rows()
+        locs, rems, cut = [], [], None
+        for loc, rem, tmax in self.gens[:self.halo_windows]:
+            if tmax == 0:
+                break
+            cut = tmax - self.halo_ns if cut is None else max(cut, tmax - self.halo_ns)
+            locs.append(oracle.take(loc, (loc.slot != oracle.NO_SLOT) & (loc.ts != 0) & (loc.ts >= cut)))
+            rems.append(oracle.take(rem, (rem.slot != oracle.NO_SLOT) & (rem.ts != 0) & (rem.ts >= cut)))
+        out = oracle.empty_rows()
+        for d in locs + rems[::-1]:
+            out = oracle.concat(out, d)
+        return out
+
     def join(self, d_loc: oracle.Decoded, spans: np.ndarray, n_groups: int, blocks=None, **join_kw):
-        """Part 2: join [window rows | halo of k-1 | other ranks' rows], keep the next halo."""
-        imp = self.imports
+        """Part 2: join [window rows | halo | other ranks' rows]; the window becomes a generation."""
+        imp, self.injected = self.injected, oracle.empty_rows()
         for r, blk in enumerate(blocks or []):
             if r != self.rank:
                 imp = oracle.concat(imp, parse_block(blk))
         imp = oracle.take(imp, np.arange(len(imp.ts)) < self.import_cap)
-        d = oracle.concat(d_loc, imp)
+        d = oracle.concat(oracle.concat(d_loc, self.halo()), imp)
         res = oracle.join(d, spans, n_groups, **join_kw)
         res.n_rows = len(d.ts)
-        halo = oracle.halo_rows(d, len(d_loc.ts), self.halo_ns) if self.halo_ns > 0 else oracle.empty_rows()
-        self.imports = oracle.take(halo, np.arange(len(halo.ts)) < self.import_cap)
+        self.gens = [(d_loc, imp, oracle.window_tmax(d_loc, len(d_loc.ts)))] + self.gens[:self.halo_windows - 1]
         return res
 
     def window(self, d_loc: oracle.Decoded, spans: np.ndarray, n_groups: int, **join_kw):

@@ -153,7 +153,7 @@ class CpuRingEngine:
                  n_buffers: int = 3, window_ms: float = 2000.0, threshold: float = 0.7, fanout: int = 3,
                  group_mode: int = 1, n_dom: int = N_DOMAINS, ttft_slo_ms: float = 800.0, halo_ms: float = 0.0,
                  import_cap: int = 0, xchg_cap: int = 0, shard_rank: int = 0, shard_world: int = 1, group=None,
-                 **_native_only):
+                 halo_windows: int = 3, **_native_only):
         from ..parallel.exchange import ExchangeModel, torch_allgather
 
         self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
@@ -169,7 +169,7 @@ class CpuRingEngine:
         else:
             self.rank, self.world = 0, 1
         self.xm = ExchangeModel(self.rank, self.world, halo_ms, import_cap, xchg_cap if self.world > 1 else 0,
-                                torch_allgather(group) if group is not None else None)
+                                torch_allgather(group) if group is not None else None, halo_windows=halo_windows)
         self.table, self.tmap = oracle.CtxTable(), oracle.TraceMap()
         self.pod_sn: Dict[int, int] = {}
         self.model = None
@@ -352,7 +352,7 @@ class CpuRingEngine:
         b = np.ascontiguousarray(blocks, dtype=np.uint8)
         for r in range(world):
             if r != me:
-                self.xm.imports = oracle.concat(self.xm.imports, parse_block(b[r * stride:(r + 1) * stride]))
+                self.xm.injected = oracle.concat(self.xm.injected, parse_block(b[r * stride:(r + 1) * stride]))
 
     def import_state(self):
         return []

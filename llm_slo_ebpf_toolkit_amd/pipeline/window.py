@@ -82,16 +82,17 @@ class WindowPipeline:
     """Python handle on one native WindowEngine (one MI355X). ``comm`` = (unique_id bytes,
     rank, world) joins the node's RCCL communicator: per window, the packet all-reduce, the
     all-gather of every GPU's incident results and (``xchg_cap``) of the trace-tagged rows
-    each GPU imports into its next window. ``halo_ms`` carries a window's rows within that
-    distance of its latest record into the next window (joins across the cut); ``import_cap``
-    bounds the imported rows (halo + remote) per window."""
+    each GPU imports into its window. ``halo_ms``: later windows also join a window's rows within
+    that distance of every later window's latest record (joins across the cut); the rows of
+    ``halo_windows`` earlier windows stay resident on the device for it. ``import_cap`` bounds
+    the other GPUs' rows per window."""
 
     def __init__(self, sig_cap: int, span_cap: int, group_cap: int, device: int = 0, comm=None,
                  model: str = "bayes_learned", seed: int = 42, window_ms: float = 2000.0, threshold: float = 0.7,
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, use_graphs: bool = True,
                  max_ahead: int = 3, n_buffers: int = 3, user_cap: int = USER_CAP, ttft_slo_ms: float = 800.0,
                  halo_ms: float = 0.0, import_cap: int = 0, xchg_cap: int = 0, shard: Tuple[int, int] = (0, 1),
-                 engine: str = "gpu", group=None, model_image: Optional[np.ndarray] = None):
+                 engine: str = "gpu", group=None, model_image: Optional[np.ndarray] = None, halo_windows: int = 3):
         """``engine``: "gpu" = the native WindowEngine on HIP device ``device`` (``comm`` = its RCCL
         communicator); "cpu" = pipeline.cpu.CpuRingEngine, the same contract on the host, with
         ``group`` (a torch.distributed gloo group) as its communicator. ``shard`` = (rank, world):
@@ -107,7 +108,7 @@ class WindowPipeline:
         kw = dict(device=device, sig_cap=sig_cap, span_cap=span_cap, group_cap=group_cap, user_cap=user_cap,
                   n_buffers=n_buffers, window_ms=window_ms, threshold=threshold, fanout=fanout, group_mode=group_mode,
                   n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms, halo_ms=halo_ms, import_cap=import_cap, xchg_cap=xchg_cap,
-                  shard_rank=int(shard[0]), shard_world=int(shard[1]))
+                  shard_rank=int(shard[0]), shard_world=int(shard[1]), halo_windows=int(halo_windows))
         self.engine_kind = engine
         if engine == "cpu":
             from .cpu import CpuRingEngine

@@ -112,8 +112,29 @@ static __always_inline int mislo_below_floor(__u16 type, __u64 value)
 	return type < 120 && value < mislo_cfg_get(MISLO_CFG_FLOOR(type));
 }
 
+/* Process ids in the pod's own pid namespace. A pod's spans (process.pid) and its rocprofiler
+ * records (getpid()) carry the pid the process sees inside its container; the kernel hands the
+ * probes host pids. Records are therefore stamped with the thread group's pid in the task's
+ * innermost pid namespace (the level its struct pid was allocated at) -- the host pid for a task
+ * on the host -- so the pod + pid join tier keys every producer the same way. */
+#if defined(__bpf__)
+static __always_inline __u32 mislo_ns_tgid(struct task_struct *t)
+{
+	struct pid *p = BPF_CORE_READ(t, group_leader, thread_pid);
+	unsigned int lvl = BPF_CORE_READ(p, level);
+	return BPF_CORE_READ(p, numbers[lvl].nr);
+}
+static __always_inline __u32 mislo_cur_ns_tgid(__u32 tgid)
+{
+	(void)tgid;
+	return mislo_ns_tgid((struct task_struct *)bpf_get_current_task());
+}
+#else /* host build (probes/ebpf/host): no task structs, pids are taken as given */
+static __always_inline __u32 mislo_cur_ns_tgid(__u32 tgid) { return tgid; }
+#endif
+
 /* The probe's working record (per-CPU scratch, not ring memory) of a task or socket in cgroup
- * ``cg``: fill, then mislo_submit(). */
+ * ``cg``: fill, then mislo_submit(). ``tgid`` is already in the pod's pid namespace. */
 static __always_inline struct mislo_event *mislo_reserve_cg(__u16 type, __u64 value, __u32 tgid, __u32 tid, __u64 cg)
 {
 	__u32 zero = 0;
@@ -139,11 +160,22 @@ static __always_inline struct mislo_event *mislo_reserve_cg(__u16 type, __u64 va
 	return e;
 }
 
-/* ... attributed to the current task's cgroup */
+/* ... attributed to the current task (its cgroup, its pid in its own namespace; ``tgid`` is the
+ * host tgid of bpf_get_current_pid_tgid()) */
 static __always_inline struct mislo_event *mislo_reserve(__u16 type, __u64 value, __u32 tgid, __u32 tid)
 {
-	return mislo_reserve_cg(type, value, tgid, tid, bpf_get_current_cgroup_id());
+	return mislo_reserve_cg(type, value, mislo_cur_ns_tgid(tgid), tid, bpf_get_current_cgroup_id());
 }
+
+#if defined(__bpf__)
+/* ... attributed to task ``t``, which need not be the current one (the scheduler probes: at
+ * sched_switch the current task is the one leaving the CPU): its cgroup v2 group, its pid */
+static __always_inline struct mislo_event *mislo_reserve_task(__u16 type, __u64 value, struct task_struct *t)
+{
+	return mislo_reserve_cg(type, value, mislo_ns_tgid(t), BPF_CORE_READ(t, pid),
+				BPF_CORE_READ(t, cgroups, dfl_cgrp, kn, id));
+}
+#endif
 
 /* records.py conn_hash_np: splitmix64 of (src port, dst port, dst ip); 0 = no connection */
 static __always_inline __u64 mislo_conn_key(const struct mislo_event *e)

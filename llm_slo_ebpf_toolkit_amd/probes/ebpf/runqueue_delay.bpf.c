@@ -1,6 +1,7 @@
 /* runqueue_delay_ms: wakeup -> actually running on a CPU, per task (BTF tracepoints).
- * Attributed to the task that waited (next), emitted only above the floor (default set
- * by the agent to 100 us). */
+ * Attributed to the task that waited (next: its cgroup and its pid in its own namespace, not
+ * the outgoing current task's), emitted only above the floor (default set by the agent to
+ * 100 us). */
 #include "mislo_probe.h"
 
 char LICENSE[] SEC("license") = "GPL";
@@ -40,7 +41,8 @@ int BPF_PROG(rq_switch, bool preempt, struct task_struct *prev, struct task_stru
 	bpf_map_delete_elem(&runq_enq, &tid);
 	if (mislo_below_floor(MISLO_RUNQUEUE_DELAY, dt))
 		return 0;
-	struct mislo_event *e = mislo_reserve(MISLO_RUNQUEUE_DELAY, dt, BPF_CORE_READ(next, tgid), tid);
+	/* the waiter's own pod and pid: at sched_switch the current task (and cgroup) is prev's */
+	struct mislo_event *e = mislo_reserve_task(MISLO_RUNQUEUE_DELAY, dt, next);
 	if (e)
 		mislo_submit(e);
 	return 0;

@@ -46,6 +46,25 @@ def test_schedstat_sampler_emits_mean_wait_per_slice_above_the_floor(tmp_path):
     assert (100, 101) not in s._prev
 
 
+def test_sampler_records_carry_the_pid_the_pod_sees(tmp_path):
+    """A containerised process: the agent watches it as host pid 4242, the pod's spans and its
+    rocprofiler records say pid 17 (NSpid's innermost field). The run-queue record joins them on
+    the pod + pid tier only if it carries 17 -- as the BPF probes do (mislo_ns_tgid). A process
+    in the agent's own namespace keeps its pid."""
+    for pid in (4242, 500):
+        write_schedstat(tmp_path, pid, pid, 1, 1, 1)
+    (tmp_path / "4242" / "status").write_text("Name:\tpython\nTgid:\t4242\nNSpid:\t4242\t17\n")
+    (tmp_path / "500" / "status").write_text("Name:\tsh\nNSpid:\t500\n")
+    s = procfs.SchedstatSampler(lambda: {4242: 7, 500: 8}, lambda u: len(u), proc_root=str(tmp_path))
+    s.sample(10**18)
+    for pid in (4242, 500):
+        write_schedstat(tmp_path, pid, pid, 2, 1 + 3_000_000, 2)
+    ev = s.sample(10**18 + 10**8)
+    got = sorted((int(e["pod_id"]), int(e["pid"]), int(e["tid"])) for e in ev)
+    assert got == [(7, 17, 4242), (8, 500, 500)]
+    assert procfs.ns_pid(999, str(tmp_path)) == 999  # gone / unreadable: as given
+
+
 def test_schedstat_sampler_reads_this_process():
     me = os.getpid()
     s = procfs.SchedstatSampler(lambda: {me: 1}, lambda u: len(u), floor_ns=0)

@@ -179,11 +179,14 @@ def test_pipelined_learning_with_graphs_and_device_refit():
 
 
 def test_halo_and_remote_rows_join_like_the_oracle():
-    """Imported rows: window k+1 joins (never counts) window k's rows within the halo of its
-    latest record; a window also joins the rows the other GPUs exchanged in the same window
+    """Halo and imported rows: window k also joins (never counts) the rows of earlier windows --
+    resident on the device in their generation slots -- that lie within the halo of every later
+    window's latest local record, and the rows the other GPUs exchanged in the same window
     (injected here as the all-gather would deliver them: XRec blocks, no identity), through the
     engine's two-part chain. Features, candidates and counters match the oracle run over
-    [window rows | halo | other GPUs' rows] with the same stable selections."""
+    [window rows | halo | other GPUs' rows] in the same row order (parallel/exchange.py
+    ExchangeModel), and the device's generation state (rows, anchors, cut-offs) is the oracle's."""
+    from llm_slo_ebpf_toolkit_amd.parallel.exchange import ExchangeModel
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
     wins, gen = windows(n_win=3, seed=43)
@@ -197,9 +200,10 @@ def test_halo_and_remote_rows_join_like_the_oracle():
     pipe.eng.set_pods(pods, sn)
     pod_sn = dict(zip(pods.tolist(), sn.tolist()))
     table, tmap = oracle.CtxTable(), oracle.TraceMap()
-    imports = oracle.empty_rows()
-    n_imported = []
+    xm = ExchangeModel(0, 1, halo_ms, icap, 0, halo_windows=3)
+    n_halo, tmaxes = [], []
     for j, (w, img) in enumerate(zip(wins, imgs)):
+        n_remote = 0
         if j == 2:  # another GPU saw slow DNS lookups on the first 40 traced requests of this window
             sp = w.spans[w.spans["trace_h"] != 0][:40]
             remote = oracle.Decoded(sp["ts_ns"].astype(np.int64) + 1_000_000, np.full(len(sp), 150.0, np.float32),
@@ -208,29 +212,33 @@ def test_halo_and_remote_rows_join_like_the_oracle():
                                     np.zeros(len(sp), np.uint32), sp["trace_h"].astype(np.uint64),
                                     np.zeros(len(sp), np.uint64))
             pipe.inject_remote(oracle.exchange_blocks([remote, oracle.empty_rows()], 64), world=2, me=1)
-            imports = oracle.concat(imports, remote)
+            xm.injected = remote
+            n_remote = len(remote.ts)
         r = src.stage(feed(img, rb, user, spans), w.n_groups, img.labels)
         k = r["k"]
         oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
         d_loc = oracle.decode_window(img.framed, img.user, table, tmap, img.bases)
         n_loc = len(d_loc.ts)
-        d = oracle.concat(d_loc, imports)
-        ref = oracle.join(d, oracle.spans_native(img.spans), w.n_groups)
+        n_halo.append(len(xm.halo().ts))
+        ref = xm.join(d_loc, oracle.spans_native(img.spans), w.n_groups)
         pk = pipe.packet(k)
         res = pipe.results(k, w.n_groups)
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d_loc))  # imports never count
         fr = img.framed.view(np.uint32).reshape(-1, 6)
         assert pk["ring_state"]["events"] == int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
         dbg = pk["dbg"][:5].astype(np.int64).tolist()
-        st = pipe.eng.import_state()  # rows[0], rows[1], tmax, halo_n[nb], remote_n[nb]
-        assert st[0] == n_loc + len(imports.ts) - (40 if j == 2 else 0) and st[1] == n_loc + len(imports.ts), (j, st)
-        assert st[2] == oracle.window_tmax(d_loc, n_loc), (j, st)
-        assert (dbg[0], dbg[4]) == (ref.debug["candidates"], ref.debug["spans_enriched"]), (j, len(imports.ts), dbg)
+        # rows[0..1], tmax, gens, cur, filled, cut[4], rows per age[4], remote per buffer
+        st = pipe.eng.import_state()
+        tmaxes.append(oracle.window_tmax(d_loc, n_loc))
+        assert st[0] == n_loc and st[1] == n_loc + n_remote, (j, st)
+        assert st[2] == tmaxes[-1], (j, st)
+        assert st[3] == 4 and st[4] == j % 4 and st[5] == j + 1, (j, st)
+        cuts = [max(tmaxes[j - i] for i in range(1, a + 1)) - int(halo_ms * 1e6) for a in range(1, j + 1)]
+        assert st[7:7 + j] == cuts and st[6] == -(1 << 63), (j, st, cuts)
+        assert st[10] == n_loc + n_remote, (j, st)
+        assert (dbg[0], dbg[4]) == (ref.debug["candidates"], ref.debug["spans_enriched"]), (j, n_halo, dbg)
         np.testing.assert_array_equal(res["feat"], ref.feat, err_msg=f"window {j}")
-        n_imported.append(len(imports.ts))
-        halo = oracle.halo_rows(d, n_loc, int(halo_ms * 1e6))
-        imports = oracle.take(halo, np.arange(len(halo.ts)) < icap)
-    assert n_imported[0] == 0 and n_imported[1] > 0 and n_imported[2] > n_imported[1] - 1
+    assert n_halo[0] == 0 and n_halo[1] > 0 and n_halo[2] > 0, n_halo
     src.drain()
     pipe.eng.close()
 

@@ -103,8 +103,33 @@ def test_halo_carries_the_previous_windows_tail():
         res = m.window(d, sp, G)
         n_imp.append(res.n_rows - len(d.ts))
         tmax = oracle.window_tmax(d, len(d.ts))
-        assert (m.imports.ts >= tmax - int(HALO_MS * 1e6)).all()
+        assert (m.halo().ts >= tmax - int(HALO_MS * 1e6)).all()
     assert n_imp[0] == 0 and all(n > 0 for n in n_imp[1:])
+
+
+def test_resident_generations_are_the_nested_halo_selections():
+    """The engine keeps earlier windows' rows resident and filters them by per-age cut-offs
+    (exchange.hip k_gen_begin); that is row for row, in the same order, what selecting each
+    window's halo from [its rows | the halo it joined] (oracle.halo_rows) and carrying it forward
+    would import -- so the join's tie-breaks by row order are unchanged too."""
+    wins = global_windows()
+    m = exchange.ExchangeModel(0, 1, HALO_MS, ICAP, 0, halo_windows=3)
+    nested = oracle.empty_rows()
+    seen = remote_seen = 0
+    for j, (ev, sp, G) in enumerate(wins):
+        d = oracle.decode_events(ev)
+        # other GPUs' rows of this window (identity-free), joined after the halo
+        tr = oracle.trace_rows(d, len(d.ts))
+        remote = oracle.take(oracle.remote_rows(tr), np.arange(len(tr.ts)) % 7 == j % 7)
+        h = m.halo()
+        for f in oracle.Decoded.__dataclass_fields__:
+            np.testing.assert_array_equal(getattr(h, f), getattr(nested, f), err_msg=f"window {j}: {f}")
+        seen += len(h.ts)
+        remote_seen += int((h.pod == 0).sum())
+        m.injected = remote
+        m.window(d, sp, G)
+        nested = oracle.halo_rows(oracle.concat(oracle.concat(d, nested), remote), len(d.ts), int(HALO_MS * 1e6))
+    assert seen > 0 and remote_seen > 0
 
 
 def test_exchange_block_roundtrip():

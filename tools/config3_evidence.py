@@ -219,7 +219,7 @@ def main() -> int:
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--clients", type=int, default=2)
     ap.add_argument("--burners-per-cpu", type=int, default=6)
-    ap.add_argument("--procfs-ms", type=int, default=25,
+    ap.add_argument("--procfs-ms", type=int, default=100,
                     help="schedstat sampling interval: run-queue records join a request's span only within 100 ms "
                          "of its start (REF's pod+pid tier), so they must come faster than that")
     ap.add_argument("--max-tokens", type=int, default=8, help="tokens per request (short requests keep completing under contention)")
