@@ -355,10 +355,12 @@ class RingWindowSource:
             self.spos = span_ring.tail
         self.shared = shared
         self.kernel_done = self.kpos if ring is not None else 0
+        self.kernel_seen = self.kernel_done  # end of the kernel ranges of every reaped window
         self.user_done = self.upos if user_ring is not None else 0
         self.span_done = self.spos if span_ring is not None else 0
-        self.pending: List[tuple] = []   # (k, kernel ranges [(pos, n)], user n, span n, h2d released)
-        self.late: List[tuple] = []      # kernel ranges a window found still being written
+        self.pending: List[tuple] = []   # (k, kernel ranges [(pos, n, window cut)], user n, span n, h2d released)
+        self.late: List[tuple] = []      # kernel ranges a window found still being written: (pos, n, window)
+        self.late_dropped = 0            # late records too old for the 4 epoch bases of a later window
         self.last: Dict[str, int] = {}
         self.host_s = 0.0
         self.n = 0
@@ -395,19 +397,23 @@ class RingWindowSource:
             fb = int(eng.packet(k)[sum(PACKET_LAYOUT[:7])])  # ring state: first busy record (-1 = none)
             if fb >= 0:  # records from fb on were still being written: re-submit them
                 skip = fb
-                for pos, n in ranges:
+                for pos, n, k0 in ranges:  # k0: the window whose cut first took the range
                     if skip >= n:
                         skip -= n
                         continue
-                    self.late.append((pos + 24 * skip, n - skip))
+                    self.late.append((pos + 24 * skip, n - skip, k0))
                     self.resubmitted += n - skip
                     skip = 0
-            if self.ring is not None and ranges:
-                done = max(self.kernel_done, max(p + 24 * n for p, n in ranges))
-                hold = min([p for p, _ in self.late], default=None)
-                self.kernel_done = min(hold, done) if hold is not None else done
-                if not self.shared:
-                    self.ring.set_consumer_pos(max(self.ring.consumer_pos, self.kernel_done))
+            if ranges:
+                self.kernel_seen = max(self.kernel_seen, max(p + 24 * n for p, n, _ in ranges))
+        if self.ring is not None:
+            # ring space is free up to the decoded records, short of the first range still needed:
+            # a late range, or one a window in flight holds (a re-submitted range lies behind
+            # ranges already decoded)
+            hold = min([p for p, _, _ in self.late] + [p for e in self.pending for p, _, _ in e[1]], default=None)
+            self.kernel_done = max(self.kernel_done, min(hold, self.kernel_seen) if hold is not None else self.kernel_seen)
+            if not self.shared:
+                self.ring.set_consumer_pos(max(self.ring.consumer_pos, self.kernel_done))
         for e in self.pending:  # user / span ring space is free once the DMA that read it is done
             if not e[4] and eng.h2d_done(e[0]):
                 self._release_user(e[2], e[3])
@@ -461,12 +467,19 @@ class RingWindowSource:
         n_k = 0
         if self.ring is not None:
             late, self.late = self.late, []
-            for pos, n in late:
+            for pos, n, k0 in late:
+                # A record of window k0 carries the epoch tag of window k0 or k0 - 1; window
+                # pipe.k decodes tags against the bases of windows pipe.k - 3 .. pipe.k, so from
+                # pipe.k - k0 = 3 on the tag would name a newer epoch (a timestamp shifted by whole
+                # windows): such records are dropped and counted instead.
+                if pipe.k - k0 >= 3:
+                    self.late_dropped += n
+                    continue
                 take = min(n, budget - n_k)
                 if take < n:
-                    self.late.append((pos + 24 * take, n - take))
+                    self.late.append((pos + 24 * take, n - take, k0))
                 if take:
-                    k_ranges.append((pos, take))
+                    k_ranges.append((pos, take, k0))
                     kern += self._kernel_segments(pos, 24 * take)
                     n_k += take
             span_b = cut.kernel - self.kpos
@@ -475,7 +488,7 @@ class RingWindowSource:
             take = min(span_b // 24, budget - n_k)
             self.carried += span_b // 24 - take
             if take:
-                k_ranges.append((self.kpos, take))
+                k_ranges.append((self.kpos, take, pipe.k))
                 kern += self._kernel_segments(self.kpos, 24 * take)
                 n_k += take
                 self.kpos += 24 * take
