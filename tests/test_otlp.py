@@ -183,3 +183,53 @@ def test_rag_service_spans_reach_the_ring():
         assert abs(float(r["ttft_ms"]) - o["ttft_ms"]) < 1e-2
         assert r["pid"] == os.getpid() and r["pod_id"] == pods.id(RES["k8s.pod.uid"])
         assert r["group_id"] == 0
+
+
+def test_receiver_refuses_oversized_bodies_and_unlisted_peers():
+    """The agent binds its receiver on the host network: a body over the cap is refused (413)
+    before it is read, and with an allow-list a peer outside it gets 403."""
+    import http.client
+
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    ring = rt.HostRing(16, 64)
+    m, _ = _mapper()
+    body = _request_json(RES, SPANS)
+    rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push, max_body=len(body) - 1).start()
+    try:
+        c = http.client.HTTPConnection(rx.addr[0], rx.addr[1], timeout=5)
+        # the header announces 1 GiB; nothing past the headers is sent
+        c.putrequest("POST", "/v1/traces")
+        c.putheader("Content-Type", "application/json")
+        c.putheader("Content-Length", str(1 << 30))
+        c.endheaders()
+        assert c.getresponse().status == 413
+        c.close()
+        req = urllib.request.Request(rx.endpoint, data=body, method="POST", headers={"Content-Type": "application/json"})
+        try:
+            urllib.request.urlopen(req, timeout=5)
+            raise AssertionError("body over the cap accepted")
+        except urllib.error.HTTPError as e:
+            assert e.code == 413
+    finally:
+        rx.stop()
+    assert ring.size == 0 and rx.refused == 2 and rx.requests == 0
+    rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push, allow="10.0.0.0/8").start()
+    try:
+        req = urllib.request.Request(rx.endpoint, data=body, method="POST", headers={"Content-Type": "application/json"})
+        try:
+            urllib.request.urlopen(req, timeout=5)
+            raise AssertionError("peer outside the allow-list accepted")
+        except urllib.error.HTTPError as e:
+            assert e.code == 403
+    finally:
+        rx.stop()
+    assert ring.size == 0 and rx.refused == 1
+    rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push, allow="127.0.0.0/8").start()
+    try:
+        req = urllib.request.Request(rx.endpoint, data=body, method="POST", headers={"Content-Type": "application/json"})
+        assert urllib.request.urlopen(req, timeout=5).status == 200
+    finally:
+        rx.stop()
+    assert ring.size == 2
