@@ -75,6 +75,7 @@ class Engine {
     s_part_tot = torch::empty({kKeyTypes * kParts}, i32);
     s_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
     s_items = torch::empty({kKeyTypes * S}, i32);
+    s_pre = torch::empty({kKeyTypes * S * (int64_t)sizeof(PreSpan)}, u8);
     s_rec = torch::empty({(int64_t)S * (int64_t)sizeof(SpanRec)}, u8);
     probe_work = torch::zeros({kProbeWorkLen}, i32);
     top3 = torch::empty({3 * S}, i64); cnt = torch::empty({S}, i32);
@@ -225,7 +226,8 @@ class Engine {
     // top3 / cnt / gsum / gcnt were reset by reset_window()
     launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(), span_cap_, jp_,
                  dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<unsigned long long>(gsum),
-                 dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), dptr<uint32_t>(probe_work), st);
+                 dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), dptr<uint32_t>(probe_work),
+                 reinterpret_cast<PreSpan*>(s_pre.data_ptr()), st);
     const float* base = nullptr;
     if (base_attrs.has_value()) {
       check_cuda(*base_attrs, "base_attrs");
@@ -335,7 +337,7 @@ class Engine {
   torch::Tensor g_status, g_part;
   torch::Tensor g_part_blk, g_part_off, g_part_tot, g_part_base, g_items, g_keys, g_rec, s_rec;
   torch::Tensor s_part;
-  torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, probe_work;
+  torch::Tensor s_part_blk, s_part_off, s_part_tot, s_part_base, s_items, s_pre, probe_work;
   torch::Tensor top3, cnt, attrs, conf, kernel_ms;
   torch::Tensor gsum, gcnt, feat, labels, post, pred, gconf, evbits;
   torch::Tensor hist, status_cnt, misc, dbg, confusion, stats, stats_count, packet, model, ctx_table;

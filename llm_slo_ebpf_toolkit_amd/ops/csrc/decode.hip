@@ -418,6 +418,16 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ pod_sn, uint32_t n_pods, int seg,
                                                       int sh_rank, int sh_world, DecodeOut o) {
   __shared__ DecodeLds L;
+  // the workgroup's scalar results, merged in LDS first: one global atomic per workgroup and
+  // counter (per-wave atomics put 4096 waves x 5 updates per window on the same few L2 lines)
+  __shared__ uint32_t s_cnt2[2];
+  __shared__ unsigned long long s_t[3];
+  if (threadIdx.x == 0) {
+    s_cnt2[0] = s_cnt2[1] = 0u;
+    s_t[0] = 0ull;
+    s_t[1] = ~0ull;
+    s_t[2] = 0ull;
+  }
   lds_init<NT>(L);
   const LdsLane l = lds_lane(L);
   // segment 0: rows [0, rows[0]) (the window's records and its halo); segment 1: rows
@@ -545,15 +555,24 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
     tr[1] = max(tr[1], (uint64_t)__shfl_xor((long long)tr[1], off));
   }
   if ((threadIdx.x & 63) == 0) {
-    if (events) atomicAdd(&rs[kRsEvents], (uint32_t)events);
-    if (other) atomicAdd(&rs[kRsOtherShard], (uint32_t)other);
-    if (t_hi) atomicMax(tmax, t_hi);
-    if (o.cols.gen && tr[0] <= tr[1]) {
-      atomicMin(reinterpret_cast<unsigned long long*>(&o.cols.gen->tlo[cur]), (unsigned long long)tr[0]);
-      atomicMax(reinterpret_cast<unsigned long long*>(&o.cols.gen->thi[cur]), (unsigned long long)tr[1]);
+    if (events) atomicAdd(&s_cnt2[0], (uint32_t)events);
+    if (other) atomicAdd(&s_cnt2[1], (uint32_t)other);
+    if (t_hi) atomicMax(&s_t[0], t_hi);
+    if (tr[0] <= tr[1]) {
+      atomicMin(&s_t[1], (unsigned long long)tr[0]);
+      atomicMax(&s_t[2], (unsigned long long)tr[1]);
     }
   }
-  lds_flush<NT>(L, o, unsupported, zero_ts);
+  lds_flush<NT>(L, o, unsupported, zero_ts);  // starts with a barrier: s_cnt2 / s_t are final
+  if (threadIdx.x == 0) {
+    if (s_cnt2[0]) atomicAdd(&rs[kRsEvents], s_cnt2[0]);
+    if (s_cnt2[1]) atomicAdd(&rs[kRsOtherShard], s_cnt2[1]);
+    if (s_t[0]) atomicMax(tmax, s_t[0]);
+    if (o.cols.gen && s_t[1] <= s_t[2]) {
+      atomicMin(reinterpret_cast<unsigned long long*>(&o.cols.gen->tlo[cur]), s_t[1]);
+      atomicMax(reinterpret_cast<unsigned long long*>(&o.cols.gen->thi[cur]), s_t[2]);
+    }
+  }
 }
 
 // REF 40-byte records: REF units (count stays count, cpu_steal raw ns, else ns/1e6) and

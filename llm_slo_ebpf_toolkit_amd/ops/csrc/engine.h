@@ -239,6 +239,7 @@ class WindowEngine {
   PartCodes* s_part_ = nullptr;
   uint32_t *s_part_blk_ = nullptr, *s_part_off_ = nullptr, *s_part_tot_ = nullptr, *s_part_base_ = nullptr,
            *s_items_ = nullptr, *probe_work_ = nullptr;
+  PreSpan* s_pre_ = nullptr;  // the probe's per-window sorted span lists (k_span_sort)
   SpanRec* s_rec_ = nullptr;
   unsigned long long* top3_ = nullptr;
   uint32_t* cnt_ = nullptr;

@@ -38,6 +38,27 @@ __global__ void k_accumulate(const double* __restrict__ packet, double* __restri
   }
 }
 
+// The tail of a single-GPU window in one dispatch (it was three: pack, results copy, accumulate):
+// the packet from the accumulators -- kept on the device for the prequential refit --, added to
+// the run's totals and stored into its pinned host block; the per-incident results block copied
+// to its pinned host block.
+__global__ __launch_bounds__(256) void k_window_end(const uint32_t* hist, const uint32_t* status,
+                                                    const unsigned long long* misc, const unsigned long long* dbg,
+                                                    const uint32_t* confusion, const double* stats, const double* count,
+                                                    const uint32_t* ring, double* __restrict__ packet,
+                                                    double* __restrict__ totals, double* __restrict__ packet_host,
+                                                    const uint4* __restrict__ res, uint4* __restrict__ res_host,
+                                                    size_t res16) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  if (t < (size_t)kPacketLen) {
+    const double v = packet_value((int)t, hist, status, misc, dbg, confusion, stats, count, ring);
+    packet[t] = v;
+    totals[t] += v;
+    packet_host[t] = v;
+  }
+  for (size_t i = t; i < res16; i += stride) res_host[i] = res[i];
+}
+
 // Small copies between device memory and pinned host memory, by a kernel (loads or stores over
 // PCIe). A small hipMemcpyAsync is served by the host through the BAR, which blocks the issuing
 // thread until the stream reaches the copy -- for the results D2H the whole window's compute
@@ -246,6 +267,7 @@ void WindowEngine::alloc() {
   s_part_tot_ = dalloc<uint32_t>(kKeyTypes * kParts);
   s_part_base_ = dalloc<uint32_t>(kKeyTypes * kParts + 1);
   s_items_ = dalloc<uint32_t>(kKeyTypes * S);
+  s_pre_ = dalloc<PreSpan>((size_t)kKeyTypes * S);
   s_rec_ = dalloc<SpanRec>(S);
   probe_work_ = dalloc<uint32_t>(kProbeWorkLen);
   HIPCHECK(hipMemset(probe_work_, 0, kProbeWorkLen * 4));
@@ -294,7 +316,7 @@ WindowEngine::~WindowEngine() {
                   g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
                   s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
                   hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_hash_,
-                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_, g_keys_, gen_};
+                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_, g_keys_, gen_, s_pre_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_) hipStreamDestroy(copy_);
@@ -384,8 +406,6 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   pred_ = reinterpret_cast<int32_t*>(r + o_pred);
   evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
   sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
-  // the next generation slot and the halo cut-offs (reads the finished window's tmax: first)
-  launch_gen_begin(gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), st);
   FillList fl{};
   auto add = [&](void* p, size_t bytes, uint32_t v) { fl.seg[fl.count++] = FillSeg{(uint32_t*)p, (uint32_t)(bytes / 4), v}; };
   add(hist_, kSlots * kBuckets * 4, 0);
@@ -400,15 +420,10 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   add(gsum_, (size_t)kGroupStripes * G * kSlots * 8, 0);
   add(gcnt_, (size_t)kGroupStripes * G * kSlots * 4, 0);
   add(sli_, (size_t)G * 2 * 4, 0);
-  add(tmax_, 8, 0);
-  hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, st, fl);
-  FillList rs{};
-  rs.seg[0] = FillSeg{ring_state_, 1, 0xFFFFFFFFu};  // first busy record: none
-  rs.seg[1] = FillSeg{ring_state_ + 1, kRsLen - 1, 0};
-  rs.seg[2] = FillSeg{remote_n_ + b, 1, 0};        // other GPUs' rows: none until merged
-  rs.count = 3;
-  hipLaunchKernelGGL(k_fill, dim3(1), dim3(64), 0, st, rs);
-  launch_window_rows(counts, remote_n_ + b, N, rows_, gen_, st);
+  // + the next generation slot and the halo cut-offs (the finished window's tmax is read before
+  // its reset), the ring state, no other GPUs' rows until merged, the window's rows
+  launch_window_begin(fl, gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), ring_state_, remote_n_ + b,
+                      counts, N, rows_, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
@@ -442,7 +457,7 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
   launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), S, jp_, top3_, cnt_, n_groups, gsum_, gcnt_, dbg_,
-               probe_work_, st);
+               probe_work_, s_pre_, st);
   launch_finalize(counts + 1, S, top3_, cnt_, sig_cols(), span_cols(), jp_, nullptr, attrs_, conf_, kernel_ms_,
                   n_groups, gsum_, gcnt_, feat_, dbg_, st);
   const PosteriorModel* pm = reinterpret_cast<const PosteriorModel*>(model_dev_);
@@ -452,6 +467,15 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   else
     launch_posterior(feat_, counts + 2, G, pm, with_labels ? labels : nullptr, post_, pred_, gconf_, evbits_,
                      confusion_, st);
+  if (!comm_) {  // one GPU: the whole tail here (see k_window_end)
+    const size_t res16 = (res_bytes_ + 15) / 16;
+    const int g = (int)std::max<size_t>((kPacketLen + 255) / 256, std::min<size_t>(64, (res16 + 255) / 256));
+    hipLaunchKernelGGL(k_window_end, dim3(g), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_, stats_,
+                       stats_count_, ring_state_, packet_dev_[b], totals_, packet_host_[b],
+                       static_cast<const uint4*>(static_cast<const void*>(res_dev_[b])),
+                       static_cast<uint4*>(res_host_[b]), res16);
+    return;
+  }
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
                      stats_, stats_count_, ring_state_, packet_dev_[b]);
 }
@@ -609,8 +633,9 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   }
   const auto tt = std::chrono::steady_clock::now();
   launch_us_ += std::chrono::duration<double, std::micro>(tt - tl).count();
-  // per-incident results of this window (the buffers are reused by the next window)
-  to_host(res_dev_[b], res_host_[b], res_bytes_, compute_);
+  // per-incident results of this window (the buffers are reused by the next window); one GPU:
+  // copied by the graph's k_window_end
+  if (comm_) to_host(res_dev_[b], res_host_[b], res_bytes_, compute_);
   HIPCHECK(hipEventRecord(t_comp1_[b], compute_));
   HIPCHECK(hipEventRecord(compute_done_[b], compute_));
   HIPCHECK(hipStreamWaitEvent(comm_stream_, compute_done_[b], 0));
@@ -625,8 +650,9 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     NCCLCHECK(ncclGroupEnd());
     to_host(res_all_dev_[b], res_all_host_[b], res_bytes_ * world_, comm_stream_);
   }
-  hipLaunchKernelGGL(k_accumulate, dim3((kPacketLen + 255) / 256), dim3(256), 0, comm_stream_, packet_dev_[b], totals_,
-                     kPacketLen, packet_host_[b]);
+  if (comm_)
+    hipLaunchKernelGGL(k_accumulate, dim3((kPacketLen + 255) / 256), dim3(256), 0, comm_stream_, packet_dev_[b],
+                       totals_, kPacketLen, packet_host_[b]);
   HIPCHECK(hipEventRecord(t_end_[b], comm_stream_));
   HIPCHECK(hipEventRecord(comm_done_[b], comm_stream_));
   ++submitted_;

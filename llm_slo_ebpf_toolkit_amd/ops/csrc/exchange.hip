@@ -19,6 +19,7 @@
 // scatter), so the exchanged rows, and with them the join's tie-breaks by row, are deterministic.
 #include "mislo_common.h"
 #include "mislo_launch.h"
+#include "mislo_packet.h"
 
 namespace mislo {
 
@@ -152,29 +153,31 @@ __global__ __launch_bounds__(256) void k_remote_merge(const uint8_t* __restrict_
 
 // rows of the window: rows[0] = local records (decode segment 0), rows[1] = rows[0] + other
 // GPUs' rows (segment 1); the generation keeps both counts (the join's row classes)
+__device__ __forceinline__ void window_rows_body(const int* __restrict__ counts, uint32_t remote_n, int cap,
+                                                 int* __restrict__ rows, GenMeta* __restrict__ gen) {
+  const long long r0 = counts[0] < cap ? counts[0] : cap;
+  const long long b = r0 + remote_n;
+  rows[0] = (int)r0;
+  rows[1] = (int)(b < cap ? b : cap);
+  if (gen) {
+    gen->n_local[gen->cur] = (uint32_t)rows[0];
+    gen->n_rows[gen->cur] = (uint32_t)rows[1];
+  }
+}
+
 __global__ void k_window_rows(const int* __restrict__ counts, const uint32_t* __restrict__ remote_n, int cap,
                               int* __restrict__ rows, GenMeta* __restrict__ gen) {
-  if (threadIdx.x == 0) {
-    const long long r0 = counts[0] < cap ? counts[0] : cap;
-    const long long b = r0 + *remote_n;
-    rows[0] = (int)r0;
-    rows[1] = (int)(b < cap ? b : cap);
-    if (gen) {
-      gen->n_local[gen->cur] = (uint32_t)rows[0];
-      gen->n_rows[gen->cur] = (uint32_t)rows[1];
-    }
-  }
+  if (threadIdx.x == 0) window_rows_body(counts, *remote_n, cap, rows, gen);
 }
 
 // Start of a window: the finished window's halo anchor (its latest local record), the next
 // slot (its old rows, kMaxGens windows back, drop out), and the visibility cut-off of every
 // age: a row of window k - a stays visible in window k while ts >= tmax_i - halo for every
 // window i in [k - a, k - 1] (a window without local records ends the chain, as an empty
-// selection would). Runs first in the window's graph, before tmax is reset.
-__global__ void k_gen_begin(GenMeta* __restrict__ g, const unsigned long long* __restrict__ tmax_prev, int gens,
-                            long long halo_ns) {
-  if (threadIdx.x != 0) return;
-  if (g->filled > 0) g->tmax_local[g->cur] = (int64_t)*tmax_prev;
+// selection would).
+__device__ __forceinline__ void gen_begin_body(GenMeta* __restrict__ g, unsigned long long tmax_prev, int gens,
+                                               long long halo_ns) {
+  if (g->filled > 0) g->tmax_local[g->cur] = (int64_t)tmax_prev;
   const uint32_t cur = (g->cur + 1) % (uint32_t)gens;
   g->cur = cur;
   g->filled = min(g->filled + 1, (uint32_t)gens);
@@ -197,6 +200,29 @@ __global__ void k_gen_begin(GenMeta* __restrict__ g, const unsigned long long* _
       ok = false;
     }
     g->cut[a] = ok ? c : INT64_MAX;
+  }
+}
+
+// The head of a window's graph in ONE dispatch (it was four latency-bound ones: generation
+// step, accumulator fill, ring-state fill, row counts -- ~19 us per window): every thread zeroes
+// the accumulators while thread 0 of block 0 runs the ordered scalar part -- the finished
+// window's tmax into its generation, then tmax reset; the ring state (first busy record: none);
+// no other GPUs' rows yet; the window's row counts.
+__global__ __launch_bounds__(256) void k_window_begin(FillList fl, GenMeta* __restrict__ gen,
+                                                      unsigned long long* __restrict__ tmax, int gens, long long halo_ns,
+                                                      uint32_t* __restrict__ ring_state, uint32_t* __restrict__ remote_n,
+                                                      const int* __restrict__ counts, int cap, int* __restrict__ rows) {
+  for (int q = 0; q < fl.count; ++q) {
+    const FillSeg sg = fl.seg[q];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < sg.n; i += gridDim.x * 256) sg.ptr[i] = sg.value;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (gen) gen_begin_body(gen, *tmax, gens, halo_ns);
+    *tmax = 0ull;
+    ring_state[kRsFirstBusy] = 0xFFFFFFFFu;
+    for (int j = 1; j < kRsLen; ++j) ring_state[j] = 0u;
+    *remote_n = 0u;
+    window_rows_body(counts, 0u, cap, rows, gen);
   }
 }
 
@@ -228,9 +254,11 @@ void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, in
   hipLaunchKernelGGL(k_window_rows, dim3(1), dim3(64), 0, stream, counts, remote_n, cap, rows, gen);
 }
 
-void launch_gen_begin(GenMeta* gen, const unsigned long long* tmax_prev, int gens, long long halo_ns,
-                      hipStream_t stream) {
-  hipLaunchKernelGGL(k_gen_begin, dim3(1), dim3(64), 0, stream, gen, tmax_prev, gens, halo_ns);
+void launch_window_begin(const FillList& fl, GenMeta* gen, unsigned long long* tmax, int gens, long long halo_ns,
+                         uint32_t* ring_state, uint32_t* remote_n, const int* counts, int cap, int* rows,
+                         hipStream_t stream) {
+  hipLaunchKernelGGL(k_window_begin, dim3(256), dim3(256), 0, stream, fl, gen, tmax, gens, halo_ns, ring_state,
+                     remote_n, counts, cap, rows);
 }
 
 }  // namespace mislo

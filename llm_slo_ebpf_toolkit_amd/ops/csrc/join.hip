@@ -12,7 +12,7 @@
 // GPU design (MI355X):
 //   1. decode (decode.hip) hashes every record's 4 join keys; the top kPartBits hash bits
 //      pick one of kParts partitions per key type, counted per workgroup;
-//   2. k_part_scan / k_base_scan turn per-workgroup counts into scatter offsets;
+//   2. k_part_scan turns per-workgroup counts into scatter offsets and list bases;
 //   3. k_scatter writes record indices into partition lists (no global atomics);
 //   4. k_probe: one workgroup per (key type, partition) stages the partition's SPANS in
 //      LDS (bitonic-sorted by (key hash, ts)), then streams the partition's SIGNALS
@@ -49,10 +49,62 @@ constexpr int kChunk = 256;   // spans staged in LDS per pass
 // of a wave read 128 contiguous bytes each), the group prefixes go through LDS, pass 2
 // rewrites the group's rows as running offsets.
 constexpr int kScanCols = 32, kScanRG = 32;
+constexpr int kBaseNT = kScanCols * kScanRG;  // the last column-scan workgroup runs the base scan
+constexpr int kBasePer = (kKeyTypes * kParts + kBaseNT - 1) / kBaseNT;  // totals per thread
+
+// Workgroups of the running k_part_scan that have finished, per scan (0 signals, 1 spans); the
+// last one re-arms its counter, so graph replays find it at zero.
+__device__ uint32_t g_scan_done[2];
+
+// exclusive scan of the kKeyTypes x kParts partition totals (one workgroup, 4 per thread)
+// (signals: into the current generation's offsets). The totals were stored by other workgroups
+// of the same dispatch: read at device scope, past this CU's L1.
+__device__ __forceinline__ void base_scan_body(const uint32_t* tot, uint32_t* base, const GenMeta* gen) {
+  if (gen) base += (size_t)gen->cur * kBaseLen;
+  constexpr int W = kKeyTypes * kParts;
+  __shared__ uint32_t s[kBaseNT];
+  const int t = threadIdx.x;
+  uint32_t v[kBasePer];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kBasePer; ++j) {
+    const int q = t * kBasePer + j;
+    v[j] = q < W ? __hip_atomic_load(tot + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    sum += v[j];
+  }
+  s[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < kBaseNT; off <<= 1) {
+    uint32_t x = t >= off ? s[t - off] : 0;
+    __syncthreads();
+    s[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = s[t] - sum;
+#pragma unroll
+  for (int j = 0; j < kBasePer; ++j) {
+    const int q = t * kBasePer + j;
+    if (q < W) base[q] = run;
+    run += v[j];
+  }
+  if (t == kBaseNT - 1) base[W] = s[kBaseNT - 1];
+}
+
+// part_blk[b][c] counts -> part_off[b][c] exclusive prefix over blocks, part_tot[c], and -- in
+// the last workgroup to finish -- the list offsets `base` (the base scan used to be a launch of
+// its own: ~6 us of a one-workgroup dispatch per scan, two scans per window).
+// A column scan over the [nblk][4096] matrix. One thread per column left 64 waves on the
+// whole chip, each walking 256 dependent rows; here a workgroup owns kScanCols columns and
+// splits the rows into kScanRG groups: pass 1 sums each group (independent loads, 32 rows
+// of a wave read 128 contiguous bytes each), the group prefixes go through LDS, pass 2
+// rewrites the group's rows as running offsets.
 __global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_t* __restrict__ part_blk, int nblk,
                                                                   uint32_t* __restrict__ part_off,
-                                                                  uint32_t* __restrict__ part_tot) {
+                                                                  uint32_t* __restrict__ part_tot,
+                                                                  uint32_t* __restrict__ base,
+                                                                  const GenMeta* __restrict__ gen, int which) {
   __shared__ uint32_t s_sum[kScanRG][kScanCols];
+  __shared__ int s_last;
   const int cl = threadIdx.x % kScanCols, r = threadIdx.x / kScanCols;
   const int c = blockIdx.x * kScanCols + cl;
   const int per = (nblk + kScanRG - 1) / kScanRG;
@@ -75,38 +127,15 @@ __global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_
     run += v;
   }
   if (r == 0) part_tot[c] = tot;
-}
-
-// exclusive scan of the kKeyTypes x kParts partition totals (one workgroup, 4 per thread)
-// (signals: into the current generation's offsets)
-constexpr int kBaseNT = kKeyTypes * kParts / 4;
-__global__ __launch_bounds__(kBaseNT) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base,
-                                                      const GenMeta* __restrict__ gen) {
-  if (gen) base += (size_t)gen->cur * kBaseLen;
-  __shared__ uint32_t s[kBaseNT];
-  const int t = threadIdx.x;
-  uint32_t v[4];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = tot[t * 4 + j];
-    sum += v[j];
-  }
-  s[t] = sum;
+  __threadfence();  // this workgroup's totals are visible before it arrives
   __syncthreads();
-  for (int off = 1; off < kBaseNT; off <<= 1) {
-    uint32_t x = t >= off ? s[t - off] : 0;
-    __syncthreads();
-    s[t] += x;
-    __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&g_scan_done[which], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (s_last) {
+    __threadfence();
+    base_scan_body(part_tot, base, gen);
+    if (threadIdx.x == 0) g_scan_done[which] = 0u;
   }
-  uint32_t run = s[t] - sum;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    base[t * 4 + j] = run;
-    run += v[j];
-  }
-  if (t == kBaseNT - 1) base[kKeyTypes * kParts] = s[kBaseNT - 1];
 }
 
 template <int NT>
@@ -114,8 +143,13 @@ __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ co
                                                 int cap, const uint32_t* __restrict__ part_off,
                                                 const uint32_t* __restrict__ base, uint32_t* __restrict__ items,
                                                 int nblk_a) {
-  __shared__ uint32_t s_cnt[kKeyTypes * kParts];
-  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_cnt[i] = 0;
+  // this workgroup's next slot in every list (list base + the workgroup's offset), bumped by an
+  // LDS atomic per entry: two dependent global loads per entry less
+  __shared__ uint32_t s_pos[kKeyTypes * kParts];
+  {
+    const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
+    for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_pos[i] = base[i] + my_off[i];
+  }
   __syncthreads();
   // the same row ranges the decode blocks had: one segment, or two (nblk_a blocks over
   // [0, n_ptr[0]), the rest over [n_ptr[0], n_ptr[1]))
@@ -128,15 +162,12 @@ __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ co
   const int bi = second ? (int)blockIdx.x - nblk_a : (int)blockIdx.x;
   const int chunk = (s_end - s_beg + g - 1) / g;
   const int beg = s_beg + bi * chunk, end = min(s_end, beg + chunk);
-  const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
   for (int i = beg + threadIdx.x; i < end; i += NT) {
     const PartCodes pc = codes[i];
 #pragma unroll
     for (int k = 0; k < kKeyTypes; ++k) {
       if (pc.p[k] == kNoPart) continue;
-      const int c = k * kParts + pc.p[k];
-      const uint32_t r = atomicAdd(&s_cnt[c], 1u);
-      items[base[c] + my_off[c] + r] = (uint32_t)i;
+      items[atomicAdd(&s_pos[k * kParts + pc.p[k]], 1u)] = (uint32_t)i;
     }
   }
 }
@@ -148,14 +179,18 @@ __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ co
 template <int NT>
 __global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __restrict__ n_ptr, int cap,
                                                     const uint32_t* __restrict__ part_off, int nblk_a) {
-  __shared__ uint32_t s_cnt[kKeyTypes * kParts];
-  for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_cnt[i] = 0;
-  __syncthreads();
   const uint32_t cur = cur_slot(gc);
   const SigRec* rec = gc.rec + (size_t)cur * (size_t)gc.stride;
   const uint32_t* base = gc.base + (size_t)cur * kBaseLen;
   uint32_t* items = gc.items + (size_t)cur * kKeyTypes * (size_t)gc.stride;
   KeyTs* keys = gc.keys + (size_t)cur * kKeyTypes * (size_t)gc.stride;
+  // next slot per list (see k_scatter)
+  __shared__ uint32_t s_pos[kKeyTypes * kParts];
+  {
+    const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
+    for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_pos[i] = base[i] + my_off[i];
+  }
+  __syncthreads();
   // the row ranges of the decode blocks (see k_scatter)
   const int n0 = min(n_ptr[0], cap);
   const bool two = nblk_a < (int)gridDim.x;
@@ -166,21 +201,39 @@ __global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __
   const int bi = second ? (int)blockIdx.x - nblk_a : (int)blockIdx.x;
   const int chunk = (s_end - s_beg + g - 1) / g;
   const int beg = s_beg + bi * chunk, end = min(s_end, beg + chunk);
-  const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
-  for (int i = beg + threadIdx.x; i < end; i += NT) {
-    const PartCodes pc = gc.part[i];
-    if ((pc.p[0] & pc.p[1] & pc.p[2] & pc.p[3]) == kNoPart) continue;  // not joinable
-    const uint4* v = reinterpret_cast<const uint4*>(rec + i);
-    const uint4 a = v[0], b = v[1], c4 = v[2];
-    const int64_t ts = (int64_t)(((uint64_t)a.y << 32) | a.x);
-    const uint64_t tr = ((uint64_t)a.w << 32) | a.z, cn = ((uint64_t)b.y << 32) | b.x;
+  // kU rows per thread per trip, every load of the trip issued before the first is used: the
+  // list stores of a row may alias the next row's loads for the compiler, so a row-at-a-time loop
+  // waited out one memory latency per row
+  constexpr int kU = 4;
+  const PartCodes* __restrict__ part = gc.part;
+  for (int i0 = beg + threadIdx.x; i0 < end; i0 += NT * kU) {
+    PartCodes pc[kU];
+    uint4 a[kU], b[kU], c4[kU];
 #pragma unroll
-    for (int k = 0; k < kKeyTypes; ++k) {
-      if (pc.p[k] == kNoPart) continue;
-      const int c = k * kParts + pc.p[k];
-      const uint32_t pos = base[c] + my_off[c] + atomicAdd(&s_cnt[c], 1u);
-      items[pos] = (uint32_t)i;
-      keys[pos] = KeyTs{key_hash(k, tr, b.z, b.w, cn, c4.x), ts};
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * NT;
+      if (i < end) {
+        pc[u] = part[i];
+        const uint4* v = reinterpret_cast<const uint4*>(rec + i);
+        a[u] = v[0];
+        b[u] = v[1];
+        c4[u] = v[2];
+      } else {
+        pc[u].p[0] = pc[u].p[1] = pc[u].p[2] = pc[u].p[3] = kNoPart;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if ((pc[u].p[0] & pc[u].p[1] & pc[u].p[2] & pc[u].p[3]) == kNoPart) continue;  // not joinable
+      const int64_t ts = (int64_t)(((uint64_t)a[u].y << 32) | a[u].x);
+      const uint64_t tr = ((uint64_t)a[u].w << 32) | a[u].z, cn = ((uint64_t)b[u].y << 32) | b[u].x;
+#pragma unroll
+      for (int k = 0; k < kKeyTypes; ++k) {
+        if (pc[u].p[k] == kNoPart) continue;
+        const uint32_t pos = atomicAdd(&s_pos[k * kParts + pc[u].p[k]], 1u);
+        items[pos] = (uint32_t)(i0 + u * NT);
+        keys[pos] = KeyTs{key_hash(k, tr, b[u].z, b[u].w, cn, c4[u].x), ts};
+      }
     }
   }
 }
@@ -436,8 +489,195 @@ __device__ __forceinline__ int lower_u16(const uint16_t* v, int n, int x) {
   return lo;
 }
 
+// Span staging, once per window: every (key type, partition) list of spans, in chunks of kChunk
+// list positions, sorted by (key hash, ts) with its hash runs marked. The probe stages a list once
+// per work item -- per generation and signal slice, 3-9 times a window -- and did this sort, the
+// span gathers and the run scans each time; now it loads the chunk's PreSpans (coalesced).
+//
+// A workgroup owns kListsPerWg consecutive lists. Most lists hold a few dozen spans (16,384 spans
+// over 1024 partitions per key type): a list of <= 64 spans is sorted by one wave in registers
+// (bitonic network over lane shuffles, no barriers); longer lists take the workgroup's LDS path.
+constexpr int kListsPerWg = 4;
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void store_prespan(PreSpan* dst_p, uint64_t h, int64_t t, const SpanRec& rr, uint32_t idx,
+                                              uint32_t run) {
+  PreSpan ps;
+  ps.h = h;
+  ps.t = t;
+  ps.tr = rr.tr;
+  ps.cn = rr.cn;
+  ps.pod = rr.pod;
+  ps.pid = rr.pid;
+  ps.sn = rr.sn;
+  ps.grp = rr.grp;
+  ps.idx = idx;
+  ps.run = run;
+  ps.pad[0] = ps.pad[1] = 0u;
+  const uint4* src = reinterpret_cast<const uint4*>(&ps);
+  uint4* dst = reinterpret_cast<uint4*>(dst_p);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dst[q] = src[q];
+}
+
 template <int NT>
-__global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __restrict__ span_items,
+__global__ __launch_bounds__(NT) void k_span_sort(SpanCols sc, const uint32_t* __restrict__ span_items,
+                                                  const uint32_t* __restrict__ span_base, PreSpan* __restrict__ out) {
+  static_assert(kChunk == NT && NT / 64 == kListsPerWg, "one span per thread, one list per wave");
+  __shared__ SpanKT s_kt[kChunk];
+  __shared__ SpanTC s_tc[kChunk];
+  __shared__ SpanPP s_pp[kChunk];
+  __shared__ uint16_t s_pos[kChunk];
+  __shared__ uint16_t s_inv[kChunk];
+  __shared__ int s_aux[kChunk];
+  __shared__ uint32_t s_ok[kChunk];
+  __shared__ int s_wsum[NT / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // ---- wave path: this wave's list, if it holds 1..64 spans ----
+  {
+    const int c = blockIdx.x * kListsPerWg + wave, k = c / kParts;
+    const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
+    const int m = (int)(sp1 - sp0);
+    if (m > 0 && m <= 64) {
+      SpanRec rr{};
+      uint32_t my_s = 0;
+      uint64_t h = ~0ull;
+      int64_t t = INT64_MAX;
+      int pos = lane;  // pre-sort position; padding lanes sort last
+      if (lane < m) {
+        my_s = span_items[sp0 + lane];
+        rr = sc.rec[my_s];
+        h = key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn);
+        t = rr.ts;
+      }
+      int M = 1;
+      while (M < m) M <<= 1;
+      // bitonic sort of (h, t, pos) over lanes [0, M): the pair (lane, lane ^ j) keeps the smaller
+      // on the lower lane of an ascending block, the larger on a descending one
+      for (int size = 2; size <= M; size <<= 1) {
+        for (int j = size >> 1; j > 0; j >>= 1) {
+          const int partner = lane ^ j;
+          const uint64_t oh = shfl_u64(h, partner);
+          const int64_t ot = (int64_t)shfl_u64((uint64_t)t, partner);
+          const int op = __shfl(pos, partner);
+          const bool lower = (lane & j) == 0, up = (lane & size) == 0;
+          const bool other_less = less_ht(oh, ot, h, t) || (oh == h && ot == t && op < pos);
+          const bool take = lane < M && (lower == up ? other_less : !other_less);
+          if (take) {
+            h = oh;
+            t = ot;
+            pos = op;
+          }
+        }
+      }
+      // this lane now holds sorted position `lane`; its record is the one pre-sort lane `pos` loaded
+      const uint64_t s_tr = shfl_u64(rr.tr, pos), s_cn = shfl_u64(rr.cn, pos);
+      const uint32_t s_pod = (uint32_t)__shfl((int)rr.pod, pos), s_pid = (uint32_t)__shfl((int)rr.pid, pos);
+      const uint32_t s_sn = (uint32_t)__shfl((int)rr.sn, pos), s_grp = (uint32_t)__shfl((int)rr.grp, pos);
+      const uint32_t s_idx = (uint32_t)__shfl((int)my_s, pos);
+      // hash runs: heads, run ids, and whether every member's key fields agree with its predecessor
+      const uint64_t ph = shfl_u64(h, lane ? lane - 1 : 0);
+      const uint64_t pcn = shfl_u64(s_cn, lane ? lane - 1 : 0);
+      const uint32_t ppod = (uint32_t)__shfl((int)s_pod, lane ? lane - 1 : 0);
+      const uint32_t ppid = (uint32_t)__shfl((int)s_pid, lane ? lane - 1 : 0);
+      const uint32_t psn = (uint32_t)__shfl((int)s_sn, lane ? lane - 1 : 0);
+      const uint32_t pgrp = (uint32_t)__shfl((int)s_grp, lane ? lane - 1 : 0);
+      const bool in_list = lane < m;
+      const bool head = in_list && (lane == 0 || ph != h);
+      const bool brk = in_list && !head &&
+                       (ppod != s_pod || ppid != s_pid || psn != s_sn || pgrp != s_grp || (k == 2 && pcn != s_cn));
+      const uint64_t hm = __ballot(head), bm = __ballot(brk);
+      const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
+      const int rid = __popcll(hm & below) - 1;
+      const int rs = 63 - __clzll(hm & below);                            // this run's head lane
+      const uint64_t after = lane == 63 ? 0ull : (hm >> (lane + 1));
+      const int re = after ? lane + 1 + __ffsll((long long)after) - 1 : m;  // next run's head (or m)
+      const uint64_t span = (re >= 64 ? ~0ull : ((1ull << re) - 1)) & ~((2ull << rs) - 1);  // (rs, re)
+      const uint32_t ok = (bm & span) ? 0u : 1u;
+      if (in_list) {
+        SpanRec sr{};
+        sr.tr = s_tr;
+        sr.cn = s_cn;
+        sr.pod = s_pod;
+        sr.pid = s_pid;
+        sr.sn = s_sn;
+        sr.grp = s_grp;
+        store_prespan(out + sp0 + lane, h, t, sr, s_idx, (uint32_t)rid | (ok << 16));
+      }
+    }
+  }
+  // ---- workgroup path: this workgroup's lists of more than 64 spans, chunk by chunk ----
+  const int ti = threadIdx.x;
+  for (int w = 0; w < kListsPerWg; ++w) {
+    const int c = blockIdx.x * kListsPerWg + w, k = c / kParts;
+    const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
+    if (sp1 - sp0 <= 64) continue;  // workgroup-uniform
+    for (uint32_t c0 = sp0; c0 < sp1; c0 += kChunk) {
+      const int m = (int)min((uint32_t)kChunk, sp1 - c0);
+      int M = 1;
+      while (M < m) M <<= 1;
+      __syncthreads();
+      SpanRec rr{};
+      uint32_t my_s = 0xFFFFFFFFu;
+      if (ti < m) {
+        my_s = span_items[c0 + ti];
+        rr = sc.rec[my_s];
+      }
+      if (ti < M) {
+        s_kt[ti] = ti < m ? SpanKT{key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn), rr.ts} : SpanKT{~0ull, INT64_MAX};
+        s_pos[ti] = (uint16_t)ti;  // pre-sort position, carried through the sort
+      }
+      __syncthreads();
+      // bitonic sort of (hash, ts, position) ascending
+      for (int size = 2; size <= M; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int t = threadIdx.x; t < (M >> 1); t += NT) {
+            const int i = 2 * t - (t & (stride - 1));
+            const int j = i + stride;
+            const bool up = (i & size) == 0;
+            const SpanKT ei = s_kt[i], ej = s_kt[j];
+            const bool gt = less_ht(ej.h, ej.t, ei.h, ei.t);
+            if (gt == up) {
+              s_kt[i] = ej; s_kt[j] = ei;
+              const uint16_t tp = s_pos[i]; s_pos[i] = s_pos[j]; s_pos[j] = tp;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      if (ti < m) s_inv[s_pos[ti]] = (uint16_t)ti;
+      __syncthreads();
+      int i = 0;  // this thread's span, sorted position
+      if (ti < m) {
+        i = s_inv[ti];
+        s_tc[i] = SpanTC{rr.tr, rr.cn};
+        s_pp[i] = SpanPP{rr.pod, rr.pid, rr.sn, rr.grp};
+        s_ok[i] = 1u;
+        s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;  // hash-run heads
+      }
+      __syncthreads();
+      block_inclusive_scan<NT>(s_aux, m, s_wsum);  // run id = #heads up to i, minus one
+      if (ti < m && i > 0 && s_kt[i].h == s_kt[i - 1].h) {  // a run is uniform when its key fields agree
+        const SpanPP a = s_pp[i], b = s_pp[i - 1];
+        const SpanTC x = s_tc[i], y = s_tc[i - 1];
+        if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || (k == 2 && x.cn != y.cn))
+          atomicAnd(&s_ok[s_aux[i] - 1], 0u);
+      }
+      __syncthreads();
+      if (ti < m) {
+        const uint32_t rid = (uint32_t)(s_aux[i] - 1);
+        store_prespan(out + c0 + i, s_kt[i].h, s_kt[i].t, rr, my_s, rid | (s_ok[rid] << 16));
+      }
+    }
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT, 4) void k_probe(const PreSpan* __restrict__ pre,
                                               const uint32_t* __restrict__ span_base, SignalCols gc, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups,
@@ -544,77 +784,31 @@ __global__ __launch_bounds__(NT, 4) void k_probe(SpanCols sc, const uint32_t* __
 
   for (uint32_t c0 = sp0; c0 < sp1; c0 += kChunk) {
     const int m = (int)min((uint32_t)kChunk, sp1 - c0);
-    int M = 1;
-    while (M < m) M <<= 1;
     __syncthreads();
-    // one span per thread (kChunk == NT): every global load of the chunk is issued up
-    // front and kept in registers across the sort, then written to its sorted slot
+    // the chunk, sorted by k_span_sort: one span per thread at its sorted position
     const int ti = threadIdx.x;
-    SpanRec rr{};
-    uint32_t my_s = 0xFFFFFFFFu;
-    unsigned long long my_seed = kEmpty;
     if (ti < m) {
-      my_s = span_items[c0 + ti];
-      rr = sc.rec[my_s];
-      if (k > 0 && !count_only) my_seed = top3[3ull * my_s + 2];
-    }
-    if (ti < M) {
-      s_kt[ti] = ti < m ? SpanKT{key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn), rr.ts}
-                        : SpanKT{~0ull, INT64_MAX};
-      s_rid[ti] = (uint16_t)ti;  // pre-sort position, carried through the sort
-    }
-    __syncthreads();
-    // bitonic sort of (hash, ts, position) ascending
-    for (int size = 2; size <= M; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int t = threadIdx.x; t < (M >> 1); t += NT) {
-          const int i = 2 * t - (t & (stride - 1));
-          const int j = i + stride;
-          const bool up = (i & size) == 0;
-          const SpanKT ei = s_kt[i], ej = s_kt[j];
-          const bool gt = less_ht(ej.h, ej.t, ei.h, ei.t);
-          if (gt == up) {
-            s_kt[i] = ej; s_kt[j] = ei;
-            const uint16_t tp = s_rid[i]; s_rid[i] = s_rid[j]; s_rid[j] = tp;
-          }
-        }
-        __syncthreads();
-      }
-    }
-    if (ti < m) s_needy[s_rid[ti]] = (uint16_t)ti;  // inverse permutation (scratch)
-    __syncthreads();
-    if (ti < m) {
-      const int i = s_needy[ti];  // this thread's span, sorted position
-      s_i[i] = my_s;
+      const uint4* src = reinterpret_cast<const uint4*>(pre + c0 + ti);
+      const uint4 a = src[0], b = src[1], cc = src[2], d = src[3];
+      const uint32_t my_s = d.x;
+      s_kt[ti] = SpanKT{((uint64_t)a.y << 32) | a.x, (int64_t)(((uint64_t)a.w << 32) | a.z)};
+      s_i[ti] = my_s;
       if (!count_only) {
-        s_tc[i] = SpanTC{rr.tr, rr.cn};
-        s_pp[i] = SpanPP{rr.pod, rr.pid, rr.sn, rr.grp};
-        s_top[3 * i] = kEmpty;
-        s_top[3 * i + 1] = kEmpty;
-        s_top[3 * i + 2] = kEmpty;
-        s_seed3[i] = my_seed;
-        s_diff[i] = 0;
-        s_runok[i] = 1u;
+        s_tc[ti] = SpanTC{((uint64_t)b.y << 32) | b.x, ((uint64_t)b.w << 32) | b.z};
+        s_pp[ti] = SpanPP{cc.x, cc.y, cc.z, cc.w};
+        s_top[3 * ti] = kEmpty;
+        s_top[3 * ti + 1] = kEmpty;
+        s_top[3 * ti + 2] = kEmpty;
+        s_seed3[ti] = k > 0 ? top3[3ull * my_s + 2] : kEmpty;
+        s_diff[ti] = 0;
+        s_rid[ti] = (uint16_t)(d.y & 0xFFFFu);
+        s_runok[d.y & 0xFFFFu] = d.y >> 16;  // every member of a run writes the same flag
       }
     }
+    if (threadIdx.x == 0 && !count_only) s_diff[m] = 0;
+    __syncthreads();  // the staged chunk is complete
     if (!count_only) {
-      __syncthreads();
-      for (int i = threadIdx.x; i < m; i += NT)  // hash-run heads
-        s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;
-      if (threadIdx.x == 0) s_diff[m] = 0;
-      __syncthreads();
       if (ranged) {
-        block_inclusive_scan<NT>(s_aux, m, s_wsum);  // run id = #heads up to i, minus one
-        for (int i = threadIdx.x; i < m; i += NT) {
-          s_rid[i] = (uint16_t)(s_aux[i] - 1);
-          if (i > 0 && s_kt[i].h == s_kt[i - 1].h) {
-            const SpanPP a = s_pp[i], b = s_pp[i - 1];
-            const SpanTC x = s_tc[i], y = s_tc[i - 1];
-            if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || (k == 2 && x.cn != y.cn))
-              atomicAnd(&s_runok[s_aux[i] - 1], 0u);
-          }
-        }
-        __syncthreads();
         // compact list of needy spans (sorted positions)
         for (int i = threadIdx.x; i < m; i += NT) {
           const unsigned long long seed = s_seed3[i];
@@ -1031,8 +1225,7 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                           uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a) {
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
-                     part_blk, nblk, part_off, part_tot);
-  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, gc.base, gc.gen);
+                     part_blk, nblk, part_off, part_tot, gc.base, gc.gen, 0);
   hipLaunchKernelGGL((k_scatter_sig<1024>), dim3(nblk), dim3(1024), 0, stream, gc, n_dev, cap, part_off,
                      nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk);
 }
@@ -1042,8 +1235,7 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
                       hipStream_t stream, int nblk_a) {
   static_assert((kKeyTypes * kParts) % kScanCols == 0, "scan columns tile the partition matrix");
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
-                     part_blk, nblk, part_off, part_tot);
-  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, part_base, nullptr);
+                     part_blk, nblk, part_off, part_tot, part_base, nullptr, 1);
   // 1024 threads per workgroup: the grid is one workgroup per decode block (<= 256), so 256
   // threads left 4 waves per CU to hide the scattered stores and LDS atomics
   hipLaunchKernelGGL((k_scatter<1024>), dim3(nblk), dim3(1024), 0, stream, codes, n_dev, cap, part_off, part_base,
@@ -1053,7 +1245,7 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   int span_cap, const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups,
                   unsigned long long* gsum, uint32_t* gcnt, unsigned long long* dbg, uint32_t* work,
-                  hipStream_t stream) {
+                  PreSpan* span_pre, hipStream_t stream) {
   // phase 1: trace tier; phase 2: pod+pid, pod+conn, svc+node seeded with phase 1's top-3.
   // Both phases pull items from the device-built work list. Diagnostic knobs (read once):
   // MISLO_PROBE_GRID workgroups per phase, MISLO_PROBE_ITEM signals per work item.
@@ -1067,10 +1259,13 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
     const int x = v ? atoi(v) : kSigPerItem;
     return x >= 1 ? x : kSigPerItem;
   }();
+  static_assert((kKeyTypes * kParts) % kListsPerWg == 0, "workgroups tile the lists");
+  hipLaunchKernelGGL((k_span_sort<kChunk>), dim3(kKeyTypes * kParts / kListsPerWg), dim3(kChunk), 0, stream, sc,
+                     span_items, span_base, span_pre);
   hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, per_item, work);
   for (int phase = 0; phase < 2; ++phase)
-    hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, sc, span_items, span_base, gc, span_cap, jp,
-                       top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);
+    hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, span_pre, span_base, gc, span_cap, jp, top3,
+                       cnt, n_groups, gsum, gcnt, dbg, work, phase);
 }
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "mislo_common.h"
+#include "mislo_packet.h"
 
 namespace mislo {
 
@@ -90,9 +91,12 @@ void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me,
                          uint32_t imp_cap, int max_rows, hipStream_t stream);
 void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, int* rows, GenMeta* gen,
                         hipStream_t stream);
-// next generation slot and the halo's per-age visibility cut-offs (see exchange.hip)
-void launch_gen_begin(GenMeta* gen, const unsigned long long* tmax_prev, int gens, long long halo_ns,
-                      hipStream_t stream);
+// head of a window's graph: the next generation slot and the halo's per-age visibility cut-offs,
+// tmax / ring state / other GPUs' row count reset, the window's row counts, and the fills of
+// `fl` (see exchange.hip)
+void launch_window_begin(const FillList& fl, GenMeta* gen, unsigned long long* tmax, int gens, long long halo_ns,
+                         uint32_t* ring_state, uint32_t* remote_n, const int* counts, int cap, int* rows,
+                         hipStream_t stream);
 
 // join.hip
 // rows [0, n_dev[0]) decoded by nblk blocks; with split (nblk_a < nblk) the first nblk_a blocks
@@ -103,11 +107,24 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
 // signals: the current generation's lists (gc.items / gc.keys / gc.base) from gc.part and gc.rec
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                           uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a = 0);
-// spans of this window x every visible generation's signals
+// A span at its position in a (key type, partition) list, the list sorted by (key hash, ts) in
+// chunks of the probe's staging size: what the probe stages, written once per window
+// (k_span_sort). run = the position's hash-run id in its chunk | run uniform << 16.
+struct alignas(64) PreSpan {
+  uint64_t h;
+  int64_t t;
+  uint64_t tr, cn;
+  uint32_t pod, pid, sn, grp;
+  uint32_t idx, run;
+  uint32_t pad[2];
+};
+static_assert(sizeof(PreSpan) == 64, "one cache line per staged span");
+// spans of this window x every visible generation's signals; span_pre: kKeyTypes * span_cap
+// PreSpan of scratch
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   int span_cap, const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups,
                   unsigned long long* gsum, uint32_t* gcnt, unsigned long long* dbg, uint32_t* work,
-                  hipStream_t stream);
+                  PreSpan* span_pre, hipStream_t stream);
 // probe work list: 4 header words + per phase one word per (key type, generation, partition,
 // signal slice)
 constexpr int kProbeMaxSplit = 64;  // signal slices per (key type, generation, partition); 8 bits of the item code

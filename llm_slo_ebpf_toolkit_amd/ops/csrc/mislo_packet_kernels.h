@@ -13,31 +13,36 @@ __global__ __launch_bounds__(256) void k_fill(FillList fl) {
   }
 }
 
-// accumulators -> packet (f64), one element per thread; ring (RingState) may be null
+// packet element i (< kPacketLen) from the window's accumulators; ring (RingState) may be null
+__device__ __forceinline__ double packet_value(int i, const uint32_t* hist, const uint32_t* status,
+                                               const unsigned long long* misc, const unsigned long long* dbg,
+                                               const uint32_t* confusion, const double* stats, const double* count,
+                                               const uint32_t* ring) {
+  int o = 0;
+  if (i < kPacketHist) return hist[i];
+  o += kPacketHist;
+  if (i < o + kPacketStatus) return status[i - o];
+  o += kPacketStatus;
+  if (i < o + kPacketMisc) return (double)misc[i - o];
+  o += kPacketMisc;
+  if (i < o + kPacketDbg) return (double)dbg[i - o];
+  o += kPacketDbg;
+  if (i < o + kPacketConf) return confusion[i - o];
+  o += kPacketConf;
+  if (i < o + kPacketStats) return stats[i - o];
+  o += kPacketStats;
+  if (i < o + kPacketCount) return count[i - o];
+  o += kPacketCount;
+  const uint32_t v = ring ? ring[i - o] : (i - o == kRsFirstBusy ? 0xFFFFFFFFu : 0u);
+  return (i - o == kRsFirstBusy && v == 0xFFFFFFFFu) ? -1.0 : (double)v;  // -1: no busy record
+}
+
+// accumulators -> packet (f64), one element per thread
 __global__ void k_pack(const uint32_t* hist, const uint32_t* status, const unsigned long long* misc,
                        const unsigned long long* dbg, const uint32_t* confusion, const double* stats,
                        const double* count, const uint32_t* ring, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  int o = 0;
-  if (i < kPacketHist) { out[i] = hist[i]; return; }
-  o += kPacketHist;
-  if (i < o + kPacketStatus) { out[i] = status[i - o]; return; }
-  o += kPacketStatus;
-  if (i < o + kPacketMisc) { out[i] = (double)misc[i - o]; return; }
-  o += kPacketMisc;
-  if (i < o + kPacketDbg) { out[i] = (double)dbg[i - o]; return; }
-  o += kPacketDbg;
-  if (i < o + kPacketConf) { out[i] = confusion[i - o]; return; }
-  o += kPacketConf;
-  if (i < o + kPacketStats) { out[i] = stats[i - o]; return; }
-  o += kPacketStats;
-  if (i < o + kPacketCount) { out[i] = count[i - o]; return; }
-  o += kPacketCount;
-  if (i < o + kPacketRing) {
-    const uint32_t v = ring ? ring[i - o] : (i - o == kRsFirstBusy ? 0xFFFFFFFFu : 0u);
-    out[i] = (i - o == kRsFirstBusy && v == 0xFFFFFFFFu) ? -1.0 : (double)v;  // -1: no busy record
-    return;
-  }
+  if (i < kPacketLen) out[i] = packet_value(i, hist, status, misc, dbg, confusion, stats, count, ring);
 }
 
 }  // namespace

@@ -29,6 +29,11 @@ namespace mislo {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// element `j` (wave-uniform, not a compile-time constant) of an accumulator, as selects
+__device__ __forceinline__ double pick(const f64x4& v, int j) {
+  return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3]));
+}
+
 __device__ __forceinline__ double feature_x(float v, int s, const PosteriorModel& pm) {
   if (pm.mode == 0) {
     const bool e = (v == v) && v >= pm.thr[s] && ((pm.table_mask >> s) & 1u);
@@ -68,7 +73,11 @@ struct StatsArgs {
   double *out, *count;
 };
 
-template <int NT>
+// WPG waves per 16-row group: each computes the group's logit tile (four MFMAs, cheap to repeat)
+// and then the softmax / marginal / argmax of 4 / WPG of its accumulator rows. The normalisation
+// is a chain of f64 exp / shuffles per row quad: with one wave per group a window's 64
+// incidents ran as 4 waves of 4 serial quads (~30 us); 4 waves per group cut the chain to one.
+template <int NT, int WPG = 1>
 __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_) {
   const float* __restrict__ feat = a_.feat;
   const int32_t* __restrict__ labels = a_.labels;
@@ -77,16 +86,39 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
   double* __restrict__ conf = a_.conf;
   uint32_t* __restrict__ evbits = a_.evbits;
   uint32_t* __restrict__ confusion = a_.confusion;
+  // The model (~9 KB) is copied into LDS once, with every load in flight together: read from
+  // global memory, its fields were dependent round trips to a cold L2 (a window's join evicts
+  // it), several per row group since the result stores may alias the model (49 us per dispatch
+  // with the 2-fault columns, most of it waiting)
+  __shared__ alignas(16) PosteriorModel s_pm;
+  {
+    constexpr int n16 = (int)(sizeof(PosteriorModel) / 16), tail = (int)(sizeof(PosteriorModel) % 16);
+    const uint4* src = reinterpret_cast<const uint4*>(a_.pm);
+    uint4* dst = reinterpret_cast<uint4*>(&s_pm);
+    for (int q = threadIdx.x; q < n16; q += NT) dst[q] = src[q];
+    if (tail && threadIdx.x < tail)
+      reinterpret_cast<uint8_t*>(&s_pm)[16 * n16 + threadIdx.x] =
+          reinterpret_cast<const uint8_t*>(a_.pm)[16 * n16 + threadIdx.x];
+  }
+  __syncthreads();
+  const PosteriorModel& pm = s_pm;
   const int G = min(*a_.ng_ptr, a_.cap);
-  const PosteriorModel& pm = *a_.pm;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int row0 = (blk * (NT / 64) + wave) * 16;
-  if (row0 >= G) return;  // whole wave exits together
+  static_assert(WPG == 1 || WPG == 2 || WPG == 4, "waves per row group divide the 4 accumulator rows");
+  constexpr int kRegs = 4 / WPG;
+  const int row0 = (blk * (NT / 64 / WPG) + wave / WPG) * 16;
+  const int reg0 = (wave % WPG) * kRegs;
   const int i = lane & 15;
   const int kq = lane >> 4;
-
   const int n_pairs = pm.n_pairs;
+  // the pairs holding this lane's domain, as a bitmask
+  static_assert(kMaxPairs <= 64, "pair masks are 64-bit");
+  unsigned long long pmask = 0ull;
+  for (int h = 0; h < n_pairs; ++h)
+    if (pm.pair_a[h] == i || pm.pair_b[h] == i) pmask |= 1ull << h;
+  if (row0 >= G) return;  // whole wave exits together
+
   const int n_pt = (n_pairs + 15) >> 4;  // pair tiles (uniform over the wave)
   f64x4 acc = {0.0, 0.0, 0.0, 0.0};
   f64x4 acc2[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
@@ -108,30 +140,34 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
 #pragma unroll
     for (int t = 0; t < 3; ++t) b2[t] = (16 * t + i < n_pairs) ? pm.bias2[16 * t + i] : -INFINITY;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
+    for (int rr = 0; rr < kRegs; ++rr) {
+      const int reg = reg0 + rr;
       const int r = row0 + kq + 4 * reg;
-      const double lg = acc[reg] + bias;
+      const double lg = pick(acc, reg) + bias;
       double l2[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t) l2[t] = (t < n_pt) ? acc2[t][reg] + b2[t] : -INFINITY;
+      for (int t = 0; t < 3; ++t) l2[t] = (t < n_pt) ? pick(acc2[t], reg) + b2[t] : -INFINITY;
       double m = fmax(lg, fmax(l2[0], fmax(l2[1], l2[2])));
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1) m = fmax(m, __shfl_xor(m, off, 16));
-      double sum = (lg == -INFINITY) ? 0.0 : exp(lg - m);
+      // normalised by one reciprocal: each hypothesis' exp is taken once (not again against logz)
+      const double e1 = (lg == -INFINITY) ? 0.0 : exp(lg - m);
+      double e2[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t) sum += (l2[t] == -INFINITY) ? 0.0 : exp(l2[t] - m);
+      for (int t = 0; t < 3; ++t) e2[t] = (l2[t] == -INFINITY) ? 0.0 : exp(l2[t] - m);
+      double sum = e1 + e2[0] + e2[1] + e2[2];
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
-      const double logz = m + log(sum);
+      const double inv = 1.0 / sum;
       double pp[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t) pp[t] = (l2[t] == -INFINITY) ? 0.0 : exp(l2[t] - logz);
-      double marg = (lg == -INFINITY) ? 0.0 : exp(lg - logz);
+      for (int t = 0; t < 3; ++t) pp[t] = e2[t] * inv;
+      double marg = e1 * inv;
       for (int h = 0; h < n_pairs; ++h) {  // pair h lives in tile h >> 4, lane h & 15
         const int t = h >> 4;
         const double v = t == 0 ? pp[0] : (t == 1 ? pp[1] : pp[2]);
         const double ph = __shfl(v, h & 15, 16);
-        if (pm.pair_a[h] == i || pm.pair_b[h] == i) marg += ph;
+        if ((pmask >> h) & 1ull) marg += ph;
       }
       double mm = marg;
       int am = i;
@@ -158,9 +194,10 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
     return;
   }
 #pragma unroll
-  for (int reg = 0; reg < 4; ++reg) {
+  for (int rr = 0; rr < kRegs; ++rr) {
+    const int reg = reg0 + rr;
     const int r = row0 + kq + 4 * reg;
-    const double lg = acc[reg] + bias;  // -inf for inactive domains
+    const double lg = pick(acc, reg) + bias;  // -inf for inactive domains
     // max + argmax over the 16 domain lanes (ties -> lowest index)
     double m = lg;
     int am = i;
@@ -174,15 +211,15 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
     double sum = ex;
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 16);
-    const double logz = m + log(sum);
-    const double p = (lg == -INFINITY) ? 0.0 : exp(lg - logz);
+    const double inv = 1.0 / sum;  // the argmax's own term is exp(0) = 1: its posterior is inv
+    const double p = ex * inv;
     if (r < G) {
       post[(size_t)r * kMaxDomains + i] = p;
       const uint32_t eb = elevated_bits(feat + (size_t)r * kSlots, pm);
       evbits[(size_t)r * kMaxDomains + i] = eb & pm.dom_mask[i];
       if (i == 0) {
         pred[r] = am;
-        conf[r] = exp(m - logz);
+        conf[r] = inv;
         if (labels != nullptr) {
           const int y = labels[r];  // primary domain in bits 0-7 (label_code: a domain set above)
           if (y >= 0 && (y & 0xFF) < kMaxDomains) atomicAdd(confusion + (y & 0xFF) * kMaxDomains + am, 1u);
@@ -192,9 +229,9 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
   }
 }
 
-template <int NT>
+template <int NT, int WPG>
 __global__ __launch_bounds__(NT) void k_posterior(PosteriorArgs a) {
-  posterior_body<NT>(blockIdx.x, a);
+  posterior_body<NT, WPG>(blockIdx.x, a);
 }
 
 // U^T V over labelled incidents; out[32][32] f64, count[16] f64.
@@ -385,7 +422,10 @@ void launch_posterior(const float* feat, const int* ng_dev, int cap, const Poste
                       double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
                       hipStream_t stream) {
   const PosteriorArgs a{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion};
-  hipLaunchKernelGGL((k_posterior<kPostNT>), dim3(posterior_grid(cap)), dim3(kPostNT), 0, stream, a);
+  // 16 waves per workgroup, 4 per 16-row group: a window's 64 incidents in one workgroup
+  constexpr int kWPG = 4, kNT = 1024, kRowsPerBlock = kNT / 64 / kWPG * 16;
+  hipLaunchKernelGGL((k_posterior<kNT, kWPG>), dim3(cap > 0 ? (cap + kRowsPerBlock - 1) / kRowsPerBlock : 1), dim3(kNT),
+                     0, stream, a);
 }
 
 void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,

@@ -69,19 +69,19 @@ def _windows(n_win=3, seed=11):
     return wins, build_replay_images(wins, user_rec=24), (g.pod_ids.astype(np.uint32), sn)
 
 
-def _spec(r, world, tag, pods, port=0, engine="cpu"):
+def _spec(r, world, tag, pods, port=0, engine="cpu", device=0):
     from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerSpec, groups_of
     from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
     from llm_slo_ebpf_toolkit_amd.ops.engine import model_bytes
 
-    return WorkerSpec(rank=r, world=world, device=0, engine=engine, source="shm", ring_name=tag, pin_dir="",
+    return WorkerSpec(rank=r, world=world, device=device, engine=engine, source="shm", ring_name=tag, pin_dir="",
                       user_rec=24, sig_cap=8192, span_cap=512, group_cap=groups_of(0, world, 8), user_cap=4096,
                       window_ms=1000.0, ttft_slo_ms=800.0, halo_ms=2000.0, import_cap=16384,
                       xchg_cap=512 if world > 1 else 0, model_image=model_bytes(NaiveBayes.ref()).tobytes(),
                       pods=pods, master=("127.0.0.1", port))
 
 
-def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22):
+def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22, engine="cpu"):
     import socket
 
     from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerPool, merge_results
@@ -94,8 +94,8 @@ def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    pool = WorkerPool([_spec(r, world, tag, pods, port) for r in range(world)], (ring, user, spans),
-                      in_process=world == 1)
+    pool = WorkerPool([_spec(r, world, tag, pods, port, engine, r if engine == "gpu" else 0) for r in range(world)],
+                      (ring, user, spans), in_process=world == 1 and engine == "cpu")
     out = []
     try:
         replies = []
@@ -134,6 +134,43 @@ def test_two_cpu_workers_reproduce_the_single_process_window():
         np.testing.assert_allclose(a["res"]["post"], b["res"]["post"], rtol=1e-12, atol=1e-15)
         assert a["events"] == b["events"] > 0
         assert (a["res"]["sli"][:, 0] > 0).all()
+
+
+def _assert_same_windows(ref, got):
+    assert len(ref) == len(got)
+    for j, (a, b) in enumerate(zip(ref, got)):
+        n = 256 + 48 + 18 + 8  # hist, status, misc, dbg
+        np.testing.assert_array_equal(a["packet"][:n], b["packet"][:n], err_msg=f"window {j}")
+        for key in ("feat", "pred", "sli", "evbits"):
+            np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
+        np.testing.assert_allclose(a["res"]["post"], b["res"]["post"], rtol=1e-9, atol=1e-12)
+        assert a["events"] == b["events"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_worker_reproduces_the_cpu_oracle():
+    """The agent's spawned GPU window worker (the shipped WindowEngine on the BPF-layout rings)
+    against the single-process CPU engine on the same windows, halo included."""
+    wins, imgs, pods = _windows()
+    tag = f"/mislo-mg1-{os.getpid()}"
+    _assert_same_windows(_run_pool(1, imgs, pods, tag + "-c"), _run_pool(1, imgs, pods, tag + "-g", engine="gpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_gpu_workers_over_rccl_reproduce_the_cpu_oracle():
+    """Two GPU window workers (one per GPU, joined by the engine's RCCL communicator: packet
+    all-reduce, incident all-gather, in-window trace-row all-gather) against the single-process
+    CPU engine on the same windows: node-wide packet and every incident identical, posteriors to
+    f64 rounding. Needs two GPUs: RCCL refuses two ranks on one device."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+    wins, imgs, pods = _windows()
+    tag = f"/mislo-mg-{os.getpid()}"
+    _assert_same_windows(_run_pool(1, imgs, pods, tag + "-c"), _run_pool(2, imgs, pods, tag + "-g", engine="gpu"))
 
 
 @pytest.mark.timeout(300)
