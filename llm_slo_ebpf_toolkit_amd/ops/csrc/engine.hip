@@ -472,8 +472,7 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
     const int g = (int)std::max<size_t>((kPacketLen + 255) / 256, std::min<size_t>(64, (res16 + 255) / 256));
     hipLaunchKernelGGL(k_window_end, dim3(g), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_, stats_,
                        stats_count_, ring_state_, packet_dev_[b], totals_, packet_host_[b],
-                       static_cast<const uint4*>(static_cast<const void*>(res_dev_[b])),
-                       static_cast<uint4*>(res_host_[b]), res16);
+                       reinterpret_cast<const uint4*>(res_dev_[b]), reinterpret_cast<uint4*>(res_host_[b]), res16);
     return;
   }
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,

@@ -12,7 +12,7 @@
 // GPU design (MI355X):
 //   1. decode (decode.hip) hashes every record's 4 join keys; the top kPartBits hash bits
 //      pick one of kParts partitions per key type, counted per workgroup;
-//   2. k_part_scan turns per-workgroup counts into scatter offsets and list bases;
+//   2. k_part_scan / k_base_scan turn per-workgroup counts into scatter offsets;
 //   3. k_scatter writes record indices into partition lists (no global atomics);
 //   4. k_probe: one workgroup per (key type, partition) stages the partition's SPANS in
 //      LDS (bitonic-sorted by (key hash, ts)), then streams the partition's SIGNALS
@@ -49,62 +49,10 @@ constexpr int kChunk = 256;   // spans staged in LDS per pass
 // of a wave read 128 contiguous bytes each), the group prefixes go through LDS, pass 2
 // rewrites the group's rows as running offsets.
 constexpr int kScanCols = 32, kScanRG = 32;
-constexpr int kBaseNT = kScanCols * kScanRG;  // the last column-scan workgroup runs the base scan
-constexpr int kBasePer = (kKeyTypes * kParts + kBaseNT - 1) / kBaseNT;  // totals per thread
-
-// Workgroups of the running k_part_scan that have finished, per scan (0 signals, 1 spans); the
-// last one re-arms its counter, so graph replays find it at zero.
-__device__ uint32_t g_scan_done[2];
-
-// exclusive scan of the kKeyTypes x kParts partition totals (one workgroup, 4 per thread)
-// (signals: into the current generation's offsets). The totals were stored by other workgroups
-// of the same dispatch: read at device scope, past this CU's L1.
-__device__ __forceinline__ void base_scan_body(const uint32_t* tot, uint32_t* base, const GenMeta* gen) {
-  if (gen) base += (size_t)gen->cur * kBaseLen;
-  constexpr int W = kKeyTypes * kParts;
-  __shared__ uint32_t s[kBaseNT];
-  const int t = threadIdx.x;
-  uint32_t v[kBasePer];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < kBasePer; ++j) {
-    const int q = t * kBasePer + j;
-    v[j] = q < W ? __hip_atomic_load(tot + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    sum += v[j];
-  }
-  s[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < kBaseNT; off <<= 1) {
-    uint32_t x = t >= off ? s[t - off] : 0;
-    __syncthreads();
-    s[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = s[t] - sum;
-#pragma unroll
-  for (int j = 0; j < kBasePer; ++j) {
-    const int q = t * kBasePer + j;
-    if (q < W) base[q] = run;
-    run += v[j];
-  }
-  if (t == kBaseNT - 1) base[W] = s[kBaseNT - 1];
-}
-
-// part_blk[b][c] counts -> part_off[b][c] exclusive prefix over blocks, part_tot[c], and -- in
-// the last workgroup to finish -- the list offsets `base` (the base scan used to be a launch of
-// its own: ~6 us of a one-workgroup dispatch per scan, two scans per window).
-// A column scan over the [nblk][4096] matrix. One thread per column left 64 waves on the
-// whole chip, each walking 256 dependent rows; here a workgroup owns kScanCols columns and
-// splits the rows into kScanRG groups: pass 1 sums each group (independent loads, 32 rows
-// of a wave read 128 contiguous bytes each), the group prefixes go through LDS, pass 2
-// rewrites the group's rows as running offsets.
 __global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_t* __restrict__ part_blk, int nblk,
                                                                   uint32_t* __restrict__ part_off,
-                                                                  uint32_t* __restrict__ part_tot,
-                                                                  uint32_t* __restrict__ base,
-                                                                  const GenMeta* __restrict__ gen, int which) {
+                                                                  uint32_t* __restrict__ part_tot) {
   __shared__ uint32_t s_sum[kScanRG][kScanCols];
-  __shared__ int s_last;
   const int cl = threadIdx.x % kScanCols, r = threadIdx.x / kScanCols;
   const int c = blockIdx.x * kScanCols + cl;
   const int per = (nblk + kScanRG - 1) / kScanRG;
@@ -127,15 +75,41 @@ __global__ __launch_bounds__(kScanCols * kScanRG) void k_part_scan(const uint32_
     run += v;
   }
   if (r == 0) part_tot[c] = tot;
-  __threadfence();  // this workgroup's totals are visible before it arrives
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&g_scan_done[which], 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (s_last) {
-    __threadfence();
-    base_scan_body(part_tot, base, gen);
-    if (threadIdx.x == 0) g_scan_done[which] = 0u;
+}
+
+// exclusive scan of the kKeyTypes x kParts partition totals (one workgroup, 4 per thread)
+// (signals: into the current generation's offsets). A launch of its own: folding it into the
+// last k_part_scan workgroup needs a device-scope release per workgroup, which on this GPU
+// writes back the XCD's L2 -- measured 89 us for the two fused scans against 25 us unfused
+// (profiles/r3_kernels/step4_tried.md).
+constexpr int kBaseNT = kKeyTypes * kParts / 4;
+__global__ __launch_bounds__(kBaseNT) void k_base_scan(const uint32_t* __restrict__ tot, uint32_t* __restrict__ base,
+                                                      const GenMeta* __restrict__ gen) {
+  if (gen) base += (size_t)gen->cur * kBaseLen;
+  __shared__ uint32_t s[kBaseNT];
+  const int t = threadIdx.x;
+  uint32_t v[4];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = tot[t * 4 + j];
+    sum += v[j];
   }
+  s[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < kBaseNT; off <<= 1) {
+    uint32_t x = t >= off ? s[t - off] : 0;
+    __syncthreads();
+    s[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = s[t] - sum;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    base[t * 4 + j] = run;
+    run += v[j];
+  }
+  if (t == kBaseNT - 1) base[kKeyTypes * kParts] = s[kBaseNT - 1];
 }
 
 template <int NT>
@@ -409,11 +383,41 @@ __global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restric
     const uint32_t lo = j * per;
     return lo >= ng[k][a] ? 0u : min(ng[k][a], lo + per) - lo;
   };
+  // Items of a wave cluster into a few cost classes, and same-address LDS atomics serialise (a
+  // wave's 64 lanes on one class counter take 64 LDS cycles): each (key type, generation, slice)
+  // round adds once per distinct class of the wave (ballot over the lanes of the leader's class).
+  const int lane = p & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;  // lanes below this one
+  auto wave_add = [&](bool active, uint32_t cls, bool place, uint32_t code_v) {
+    unsigned long long todo = __ballot(active);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const uint32_t lc = (uint32_t)__shfl((int)cls, leader);
+      const unsigned long long same = __ballot(active && cls == lc) & todo;
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&s_cls[lc], (uint32_t)__popcll(same));
+      base = (uint32_t)__shfl((int)base, leader);
+      if (place && ((same >> lane) & 1ull)) items2[base + (uint32_t)__popcll(same & lt)] = code_v;
+      todo &= ~same;
+    }
+  };
+  uint32_t jmax[kKeyTypes][kMaxGens];  // the wave's largest slice count per (key type, generation)
+#pragma unroll
+  for (int k = 1; k < kKeyTypes; ++k)
+#pragma unroll
+    for (int a = 0; a < kMaxGens; ++a) {
+      uint32_t m = n[k][a];
+      for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+      jmax[k][a] = m;
+    }
 #pragma unroll
   for (int k = 1; k < kKeyTypes; ++k)
 #pragma unroll
     for (int a = 0; a < kMaxGens; ++a)
-      for (uint32_t j = 0; j < n[k][a]; ++j) atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, a, j), ns[k])], 1u);
+      for (uint32_t j = 0; j < jmax[k][a]; ++j) {
+        const bool act = j < n[k][a];
+        wave_add(act, act ? 63u - probe_item_class(k, slice(k, a, j), ns[k]) : 0u, false, 0u);
+      }
   __syncthreads();
   if (p == 0) {
     uint32_t run = 0;
@@ -428,9 +432,9 @@ __global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restric
   for (int k = 1; k < kKeyTypes; ++k)
 #pragma unroll
     for (int a = 0; a < kMaxGens; ++a)
-      for (uint32_t j = 0; j < n[k][a]; ++j) {
-        const uint32_t pos = atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, a, j), ns[k])], 1u);
-        items2[pos] = code(k, a, j);
+      for (uint32_t j = 0; j < jmax[k][a]; ++j) {
+        const bool act = j < n[k][a];
+        wave_add(act, act ? 63u - probe_item_class(k, slice(k, a, j), ns[k]) : 0u, true, act ? code(k, a, j) : 0u);
       }
   if (p == 0) {
     work[0] = t[0];
@@ -493,17 +497,9 @@ __device__ __forceinline__ int lower_u16(const uint16_t* v, int n, int x) {
 // list positions, sorted by (key hash, ts) with its hash runs marked. The probe stages a list once
 // per work item -- per generation and signal slice, 3-9 times a window -- and did this sort, the
 // span gathers and the run scans each time; now it loads the chunk's PreSpans (coalesced).
-//
-// A workgroup owns kListsPerWg consecutive lists. Most lists hold a few dozen spans (16,384 spans
-// over 1024 partitions per key type): a list of <= 64 spans is sorted by one wave in registers
-// (bitonic network over lane shuffles, no barriers); longer lists take the workgroup's LDS path.
-constexpr int kListsPerWg = 4;
-
-__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
-  return ((uint64_t)hi << 32) | lo;
-}
-
+// One workgroup per list: the kernel's time is its longest list's (the few service keys hold
+// thousands of spans), so a workgroup owning several lists -- with a wave-level sort for the
+// short ones -- ran slower (30.7 against 17.2 us, profiles/r3_kernels/step4_tried.md).
 __device__ __forceinline__ void store_prespan(PreSpan* dst_p, uint64_t h, int64_t t, const SpanRec& rr, uint32_t idx,
                                               uint32_t run) {
   PreSpan ps;
@@ -527,7 +523,7 @@ __device__ __forceinline__ void store_prespan(PreSpan* dst_p, uint64_t h, int64_
 template <int NT>
 __global__ __launch_bounds__(NT) void k_span_sort(SpanCols sc, const uint32_t* __restrict__ span_items,
                                                   const uint32_t* __restrict__ span_base, PreSpan* __restrict__ out) {
-  static_assert(kChunk == NT && NT / 64 == kListsPerWg, "one span per thread, one list per wave");
+  static_assert(kChunk == NT, "one span per thread");
   __shared__ SpanKT s_kt[kChunk];
   __shared__ SpanTC s_tc[kChunk];
   __shared__ SpanPP s_pp[kChunk];
@@ -536,142 +532,64 @@ __global__ __launch_bounds__(NT) void k_span_sort(SpanCols sc, const uint32_t* _
   __shared__ int s_aux[kChunk];
   __shared__ uint32_t s_ok[kChunk];
   __shared__ int s_wsum[NT / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // ---- wave path: this wave's list, if it holds 1..64 spans ----
-  {
-    const int c = blockIdx.x * kListsPerWg + wave, k = c / kParts;
-    const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
-    const int m = (int)(sp1 - sp0);
-    if (m > 0 && m <= 64) {
-      SpanRec rr{};
-      uint32_t my_s = 0;
-      uint64_t h = ~0ull;
-      int64_t t = INT64_MAX;
-      int pos = lane;  // pre-sort position; padding lanes sort last
-      if (lane < m) {
-        my_s = span_items[sp0 + lane];
-        rr = sc.rec[my_s];
-        h = key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn);
-        t = rr.ts;
-      }
-      int M = 1;
-      while (M < m) M <<= 1;
-      // bitonic sort of (h, t, pos) over lanes [0, M): the pair (lane, lane ^ j) keeps the smaller
-      // on the lower lane of an ascending block, the larger on a descending one
-      for (int size = 2; size <= M; size <<= 1) {
-        for (int j = size >> 1; j > 0; j >>= 1) {
-          const int partner = lane ^ j;
-          const uint64_t oh = shfl_u64(h, partner);
-          const int64_t ot = (int64_t)shfl_u64((uint64_t)t, partner);
-          const int op = __shfl(pos, partner);
-          const bool lower = (lane & j) == 0, up = (lane & size) == 0;
-          const bool other_less = less_ht(oh, ot, h, t) || (oh == h && ot == t && op < pos);
-          const bool take = lane < M && (lower == up ? other_less : !other_less);
-          if (take) {
-            h = oh;
-            t = ot;
-            pos = op;
+  const int c = blockIdx.x, k = c / kParts;
+  const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
+  const int ti = threadIdx.x;
+  for (uint32_t c0 = sp0; c0 < sp1; c0 += kChunk) {
+    const int m = (int)min((uint32_t)kChunk, sp1 - c0);
+    int M = 1;
+    while (M < m) M <<= 1;
+    __syncthreads();
+    SpanRec rr{};
+    uint32_t my_s = 0xFFFFFFFFu;
+    if (ti < m) {
+      my_s = span_items[c0 + ti];
+      rr = sc.rec[my_s];
+    }
+    if (ti < M) {
+      s_kt[ti] = ti < m ? SpanKT{key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn), rr.ts} : SpanKT{~0ull, INT64_MAX};
+      s_pos[ti] = (uint16_t)ti;  // pre-sort position, carried through the sort
+    }
+    __syncthreads();
+    // bitonic sort of (hash, ts, position) ascending
+    for (int size = 2; size <= M; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int t = threadIdx.x; t < (M >> 1); t += NT) {
+          const int i = 2 * t - (t & (stride - 1));
+          const int j = i + stride;
+          const bool up = (i & size) == 0;
+          const SpanKT ei = s_kt[i], ej = s_kt[j];
+          const bool gt = less_ht(ej.h, ej.t, ei.h, ei.t);
+          if (gt == up) {
+            s_kt[i] = ej; s_kt[j] = ei;
+            const uint16_t tp = s_pos[i]; s_pos[i] = s_pos[j]; s_pos[j] = tp;
           }
         }
-      }
-      // this lane now holds sorted position `lane`; its record is the one pre-sort lane `pos` loaded
-      const uint64_t s_tr = shfl_u64(rr.tr, pos), s_cn = shfl_u64(rr.cn, pos);
-      const uint32_t s_pod = (uint32_t)__shfl((int)rr.pod, pos), s_pid = (uint32_t)__shfl((int)rr.pid, pos);
-      const uint32_t s_sn = (uint32_t)__shfl((int)rr.sn, pos), s_grp = (uint32_t)__shfl((int)rr.grp, pos);
-      const uint32_t s_idx = (uint32_t)__shfl((int)my_s, pos);
-      // hash runs: heads, run ids, and whether every member's key fields agree with its predecessor
-      const uint64_t ph = shfl_u64(h, lane ? lane - 1 : 0);
-      const uint64_t pcn = shfl_u64(s_cn, lane ? lane - 1 : 0);
-      const uint32_t ppod = (uint32_t)__shfl((int)s_pod, lane ? lane - 1 : 0);
-      const uint32_t ppid = (uint32_t)__shfl((int)s_pid, lane ? lane - 1 : 0);
-      const uint32_t psn = (uint32_t)__shfl((int)s_sn, lane ? lane - 1 : 0);
-      const uint32_t pgrp = (uint32_t)__shfl((int)s_grp, lane ? lane - 1 : 0);
-      const bool in_list = lane < m;
-      const bool head = in_list && (lane == 0 || ph != h);
-      const bool brk = in_list && !head &&
-                       (ppod != s_pod || ppid != s_pid || psn != s_sn || pgrp != s_grp || (k == 2 && pcn != s_cn));
-      const uint64_t hm = __ballot(head), bm = __ballot(brk);
-      const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
-      const int rid = __popcll(hm & below) - 1;
-      const int rs = 63 - __clzll(hm & below);                            // this run's head lane
-      const uint64_t after = lane == 63 ? 0ull : (hm >> (lane + 1));
-      const int re = after ? lane + 1 + __ffsll((long long)after) - 1 : m;  // next run's head (or m)
-      const uint64_t span = (re >= 64 ? ~0ull : ((1ull << re) - 1)) & ~((2ull << rs) - 1);  // (rs, re)
-      const uint32_t ok = (bm & span) ? 0u : 1u;
-      if (in_list) {
-        SpanRec sr{};
-        sr.tr = s_tr;
-        sr.cn = s_cn;
-        sr.pod = s_pod;
-        sr.pid = s_pid;
-        sr.sn = s_sn;
-        sr.grp = s_grp;
-        store_prespan(out + sp0 + lane, h, t, sr, s_idx, (uint32_t)rid | (ok << 16));
+        __syncthreads();
       }
     }
-  }
-  // ---- workgroup path: this workgroup's lists of more than 64 spans, chunk by chunk ----
-  const int ti = threadIdx.x;
-  for (int w = 0; w < kListsPerWg; ++w) {
-    const int c = blockIdx.x * kListsPerWg + w, k = c / kParts;
-    const uint32_t sp0 = span_base[c], sp1 = span_base[c + 1];
-    if (sp1 - sp0 <= 64) continue;  // workgroup-uniform
-    for (uint32_t c0 = sp0; c0 < sp1; c0 += kChunk) {
-      const int m = (int)min((uint32_t)kChunk, sp1 - c0);
-      int M = 1;
-      while (M < m) M <<= 1;
-      __syncthreads();
-      SpanRec rr{};
-      uint32_t my_s = 0xFFFFFFFFu;
-      if (ti < m) {
-        my_s = span_items[c0 + ti];
-        rr = sc.rec[my_s];
-      }
-      if (ti < M) {
-        s_kt[ti] = ti < m ? SpanKT{key_hash(k, rr.tr, rr.pod, rr.pid, rr.cn, rr.sn), rr.ts} : SpanKT{~0ull, INT64_MAX};
-        s_pos[ti] = (uint16_t)ti;  // pre-sort position, carried through the sort
-      }
-      __syncthreads();
-      // bitonic sort of (hash, ts, position) ascending
-      for (int size = 2; size <= M; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int t = threadIdx.x; t < (M >> 1); t += NT) {
-            const int i = 2 * t - (t & (stride - 1));
-            const int j = i + stride;
-            const bool up = (i & size) == 0;
-            const SpanKT ei = s_kt[i], ej = s_kt[j];
-            const bool gt = less_ht(ej.h, ej.t, ei.h, ei.t);
-            if (gt == up) {
-              s_kt[i] = ej; s_kt[j] = ei;
-              const uint16_t tp = s_pos[i]; s_pos[i] = s_pos[j]; s_pos[j] = tp;
-            }
-          }
-          __syncthreads();
-        }
-      }
-      if (ti < m) s_inv[s_pos[ti]] = (uint16_t)ti;
-      __syncthreads();
-      int i = 0;  // this thread's span, sorted position
-      if (ti < m) {
-        i = s_inv[ti];
-        s_tc[i] = SpanTC{rr.tr, rr.cn};
-        s_pp[i] = SpanPP{rr.pod, rr.pid, rr.sn, rr.grp};
-        s_ok[i] = 1u;
-        s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;  // hash-run heads
-      }
-      __syncthreads();
-      block_inclusive_scan<NT>(s_aux, m, s_wsum);  // run id = #heads up to i, minus one
-      if (ti < m && i > 0 && s_kt[i].h == s_kt[i - 1].h) {  // a run is uniform when its key fields agree
-        const SpanPP a = s_pp[i], b = s_pp[i - 1];
-        const SpanTC x = s_tc[i], y = s_tc[i - 1];
-        if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || (k == 2 && x.cn != y.cn))
-          atomicAnd(&s_ok[s_aux[i] - 1], 0u);
-      }
-      __syncthreads();
-      if (ti < m) {
-        const uint32_t rid = (uint32_t)(s_aux[i] - 1);
-        store_prespan(out + c0 + i, s_kt[i].h, s_kt[i].t, rr, my_s, rid | (s_ok[rid] << 16));
-      }
+    if (ti < m) s_inv[s_pos[ti]] = (uint16_t)ti;
+    __syncthreads();
+    int i = 0;  // this thread's span, sorted position
+    if (ti < m) {
+      i = s_inv[ti];
+      s_tc[i] = SpanTC{rr.tr, rr.cn};
+      s_pp[i] = SpanPP{rr.pod, rr.pid, rr.sn, rr.grp};
+      s_ok[i] = 1u;
+      s_aux[i] = (i == 0 || s_kt[i].h != s_kt[i - 1].h) ? 1 : 0;  // hash-run heads
+    }
+    __syncthreads();
+    block_inclusive_scan<NT>(s_aux, m, s_wsum);  // run id = #heads up to i, minus one
+    if (ti < m && i > 0 && s_kt[i].h == s_kt[i - 1].h) {  // a run is uniform when its key fields agree
+      const SpanPP a = s_pp[i], b = s_pp[i - 1];
+      const SpanTC x = s_tc[i], y = s_tc[i - 1];
+      if (a.pod != b.pod || a.pid != b.pid || a.sn != b.sn || a.grp != b.grp || (k == 2 && x.cn != y.cn))
+        atomicAnd(&s_ok[s_aux[i] - 1], 0u);
+    }
+    __syncthreads();
+    if (ti < m) {
+      const uint32_t rid = (uint32_t)(s_aux[i] - 1);
+      store_prespan(out + c0 + i, s_kt[i].h, s_kt[i].t, rr, my_s, rid | (s_ok[rid] << 16));
     }
   }
 }
@@ -1225,7 +1143,8 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                           uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a) {
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
-                     part_blk, nblk, part_off, part_tot, gc.base, gc.gen, 0);
+                     part_blk, nblk, part_off, part_tot);
+  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, gc.base, gc.gen);
   hipLaunchKernelGGL((k_scatter_sig<1024>), dim3(nblk), dim3(1024), 0, stream, gc, n_dev, cap, part_off,
                      nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk);
 }
@@ -1235,7 +1154,8 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
                       hipStream_t stream, int nblk_a) {
   static_assert((kKeyTypes * kParts) % kScanCols == 0, "scan columns tile the partition matrix");
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
-                     part_blk, nblk, part_off, part_tot, part_base, nullptr, 1);
+                     part_blk, nblk, part_off, part_tot);
+  hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, part_base, nullptr);
   // 1024 threads per workgroup: the grid is one workgroup per decode block (<= 256), so 256
   // threads left 4 waves per CU to hide the scattered stores and LDS atomics
   hipLaunchKernelGGL((k_scatter<1024>), dim3(nblk), dim3(1024), 0, stream, codes, n_dev, cap, part_off, part_base,
@@ -1259,9 +1179,8 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
     const int x = v ? atoi(v) : kSigPerItem;
     return x >= 1 ? x : kSigPerItem;
   }();
-  static_assert((kKeyTypes * kParts) % kListsPerWg == 0, "workgroups tile the lists");
-  hipLaunchKernelGGL((k_span_sort<kChunk>), dim3(kKeyTypes * kParts / kListsPerWg), dim3(kChunk), 0, stream, sc,
-                     span_items, span_base, span_pre);
+  hipLaunchKernelGGL((k_span_sort<kChunk>), dim3(kKeyTypes * kParts), dim3(kChunk), 0, stream, sc, span_items,
+                     span_base, span_pre);
   hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, per_item, work);
   for (int phase = 0; phase < 2; ++phase)
     hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, span_pre, span_base, gc, span_cap, jp, top3,

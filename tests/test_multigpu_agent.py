@@ -140,7 +140,9 @@ def _assert_same_windows(ref, got):
     assert len(ref) == len(got)
     for j, (a, b) in enumerate(zip(ref, got)):
         n = 256 + 48 + 18 + 8  # hist, status, misc, dbg
-        np.testing.assert_array_equal(a["packet"][:n], b["packet"][:n], err_msg=f"window {j}")
+        bad = np.nonzero(np.asarray(a["packet"][:n]) != np.asarray(b["packet"][:n]))[0]
+        assert not len(bad), (f"window {j}: packet elements {bad.tolist()} differ: "
+                              f"{np.asarray(a['packet'])[bad].tolist()} vs {np.asarray(b['packet'])[bad].tolist()}")
         for key in ("feat", "pred", "sli", "evbits"):
             np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
         np.testing.assert_allclose(a["res"]["post"], b["res"]["post"], rtol=1e-9, atol=1e-12)
