@@ -383,41 +383,11 @@ __global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restric
     const uint32_t lo = j * per;
     return lo >= ng[k][a] ? 0u : min(ng[k][a], lo + per) - lo;
   };
-  // Items of a wave cluster into a few cost classes, and same-address LDS atomics serialise (a
-  // wave's 64 lanes on one class counter take 64 LDS cycles): each (key type, generation, slice)
-  // round adds once per distinct class of the wave (ballot over the lanes of the leader's class).
-  const int lane = p & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;  // lanes below this one
-  auto wave_add = [&](bool active, uint32_t cls, bool place, uint32_t code_v) {
-    unsigned long long todo = __ballot(active);
-    while (todo) {
-      const int leader = __ffsll((long long)todo) - 1;
-      const uint32_t lc = (uint32_t)__shfl((int)cls, leader);
-      const unsigned long long same = __ballot(active && cls == lc) & todo;
-      uint32_t base = 0;
-      if (lane == leader) base = atomicAdd(&s_cls[lc], (uint32_t)__popcll(same));
-      base = (uint32_t)__shfl((int)base, leader);
-      if (place && ((same >> lane) & 1ull)) items2[base + (uint32_t)__popcll(same & lt)] = code_v;
-      todo &= ~same;
-    }
-  };
-  uint32_t jmax[kKeyTypes][kMaxGens];  // the wave's largest slice count per (key type, generation)
-#pragma unroll
-  for (int k = 1; k < kKeyTypes; ++k)
-#pragma unroll
-    for (int a = 0; a < kMaxGens; ++a) {
-      uint32_t m = n[k][a];
-      for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
-      jmax[k][a] = m;
-    }
 #pragma unroll
   for (int k = 1; k < kKeyTypes; ++k)
 #pragma unroll
     for (int a = 0; a < kMaxGens; ++a)
-      for (uint32_t j = 0; j < jmax[k][a]; ++j) {
-        const bool act = j < n[k][a];
-        wave_add(act, act ? 63u - probe_item_class(k, slice(k, a, j), ns[k]) : 0u, false, 0u);
-      }
+      for (uint32_t j = 0; j < n[k][a]; ++j) atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, a, j), ns[k])], 1u);
   __syncthreads();
   if (p == 0) {
     uint32_t run = 0;
@@ -432,9 +402,9 @@ __global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restric
   for (int k = 1; k < kKeyTypes; ++k)
 #pragma unroll
     for (int a = 0; a < kMaxGens; ++a)
-      for (uint32_t j = 0; j < jmax[k][a]; ++j) {
-        const bool act = j < n[k][a];
-        wave_add(act, act ? 63u - probe_item_class(k, slice(k, a, j), ns[k]) : 0u, true, act ? code(k, a, j) : 0u);
+      for (uint32_t j = 0; j < n[k][a]; ++j) {
+        const uint32_t pos = atomicAdd(&s_cls[63u - probe_item_class(k, slice(k, a, j), ns[k])], 1u);
+        items2[pos] = code(k, a, j);
       }
   if (p == 0) {
     work[0] = t[0];

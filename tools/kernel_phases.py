@@ -1,6 +1,7 @@
 """Per-window kernel time breakdown from a rocprofv3 ``--kernel-trace --output-format csv`` run.
 
-Windows are delimited by the engine's one ``k_pack`` dispatch per window (ops/csrc/engine.hip);
+Windows are delimited by the engine's one ``k_pack`` (multi-GPU) or ``k_window_end`` (one GPU)
+dispatch per window (ops/csrc/engine.hip);
 the dispatches of each window are grouped by kernel and launch shape (grid / workgroup), and the
 table reports, per group, the median over the last ``--windows`` windows of its summed duration
 per window and of its dispatch count -- the unprofiled (no PMC) device time each phase costs.
@@ -28,11 +29,11 @@ def load(d):
     return rows
 
 
-def windows(rows, marker="k_pack"):
+def windows(rows, markers=("k_pack", "k_window_end")):
     out, cur = [], []
     for r in rows:
         cur.append(r)
-        if marker in r[2]:
+        if any(m in r[2] for m in markers):
             out.append(cur)
             cur = []
     return out
@@ -55,7 +56,7 @@ def summarise(d, n_last, title, prefix="mislo::"):
         rows.append((name, shape, statistics.median(cnt), statistics.median(tot)))
     rows.sort(key=lambda r: -r[3])
     total = sum(r[3] for r in rows)
-    out = [f"# {title}", "", f"{len(wins)} windows (delimited by k_pack); median per window.", "",
+    out = [f"# {title}", "", f"{len(wins)} windows (delimited by k_pack / k_window_end); median per window.", "",
            "| kernel | grid/wg | dispatches / window | us / window | share % |", "|---|---|---|---|---|"]
     for r in rows:
         out.append(f"| `{r[0]}` | {r[1]} | {r[2]:.0f} | {r[3]:.1f} | {100 * r[3] / total:.1f} |")
