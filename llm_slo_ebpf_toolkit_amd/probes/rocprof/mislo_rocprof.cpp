@@ -119,10 +119,11 @@ struct State {
   bool verbose = false;
   std::mutex mu;
   struct Enq {
-    uint64_t ts, trace_h;
+    uint64_t ts, trace_h, pred;  // pred: dispatch id of the same queue's previous dispatch (0: none)
   };
   std::unordered_map<uint64_t, Enq> enqueue_ts;  // correlation id -> enqueue time, request trace
-  std::unordered_map<uint64_t, uint64_t> queue_end;  // HW queue -> latest end of a completed dispatch
+  std::unordered_map<uint64_t, uint64_t> queue_last;  // HW queue -> its latest enqueued dispatch id
+  std::unordered_map<uint64_t, uint64_t> disp_end;    // dispatch id -> end, until its successor completes
   std::unordered_map<uint64_t, uint64_t> live_alloc;  // address -> bytes
   uint64_t live_bytes = 0;
   // node-wide HBM of the GPUs this process uses: agent handle -> the PCI device's VRAM counters
@@ -303,18 +304,28 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
 //   a CPU-starved launcher enqueues in bursts, and each kernel of a burst then queues behind the
 //   previous one (config-3 run: 700-900 "warning" queue delays per phase while only the CPUs
 //   were contended). What remains is the wait for compute units other work holds.
-// Completions of one queue normally arrive in order; one that arrives after a later dispatch of
-// its queue is ignored for the other's readiness (the delay is then an upper bound).
+// The predecessor is the dispatch enqueued on the same queue just before (recorded at enqueue), not
+// the latest completion seen: completion callbacks can arrive out of order, and a later
+// dispatch's end taken for an earlier one's predecessor made the whole self-queued burst read as
+// delay (a one-stream GEMM burst: 27 records up to 19 ms on one box). When the predecessor's
+// completion has not been delivered yet, the dispatch emits nothing: on an in-order queue it
+// started after that end, at an unknown point, so the wait behind its own queue is not separable.
 void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
   if (rec.kind != ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH) return;
+  auto* d = static_cast<rocprofiler_callback_tracing_kernel_dispatch_data_t*>(rec.payload);
   if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
     std::lock_guard<std::mutex> lk(g.mu);
-    g.enqueue_ts[rec.correlation_id.internal] = State::Enq{now, t_trace};  // the enqueuing thread's request
+    uint64_t pred = 0;
+    if (d) {
+      uint64_t& last = g.queue_last[d->dispatch_info.queue_id.handle];
+      pred = last;
+      last = d->dispatch_info.dispatch_id;
+    }
+    g.enqueue_ts[rec.correlation_id.internal] = State::Enq{now, t_trace, pred};  // the enqueuing thread's request
   } else if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_COMPLETE) {
-    auto* d = static_cast<rocprofiler_callback_tracing_kernel_dispatch_data_t*>(rec.payload);
-    State::Enq enq{0, 0};
+    State::Enq enq{0, 0, 0};
     {
       std::lock_guard<std::mutex> lk(g.mu);
       auto it = g.enqueue_ts.find(rec.correlation_id.internal);
@@ -325,13 +336,22 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     }
     if (!d) return;
     uint64_t ready = enq.ts;
+    bool known = true;
     {
       std::lock_guard<std::mutex> lk(g.mu);
-      uint64_t& last = g.queue_end[d->dispatch_info.queue_id.handle];
-      if (last <= d->start_timestamp && last > ready) ready = last;
-      if (d->end_timestamp > last) last = d->end_timestamp;
+      if (g.disp_end.size() > 65536) g.disp_end.clear();  // ends whose successor never completed
+      g.disp_end[d->dispatch_info.dispatch_id] = d->end_timestamp;
+      if (enq.pred) {
+        auto pe = g.disp_end.find(enq.pred);
+        if (pe == g.disp_end.end()) {
+          known = false;
+        } else {
+          if (pe->second > ready) ready = pe->second;
+          g.disp_end.erase(pe);  // its successor is done with it
+        }
+      }
     }
-    if (enq.ts && d->start_timestamp > ready) {
+    if (known && enq.ts && d->start_timestamp > ready) {
       const uint64_t delay = d->start_timestamp - ready;
       if (delay >= g.queue_floor_ns)
         emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id, enq.trace_h);
