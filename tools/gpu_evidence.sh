@@ -1,0 +1,42 @@
+#!/usr/bin/env bash
+# The GPU evidence suites behind profiles/ and docs/BENCHMARKS.md, one gpurun call per suite:
+#
+#   gpurun --timeout 1100 -- 'bash tools/gpu_evidence.sh reentry'
+#
+# Suites:
+#   reentry   GPU tests, smoke(), the default bench, a kernel + copy trace of the bench
+#   pmc       rocprofv3 counter passes over a short bench (one pass per counter block budget)
+#   config2   BASELINE config 2: Llama 7B preset, 800 ms TTFT SLO, onset -> first attribution
+#   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
+#   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
+#   rss       the HIP runtime's resident floor under queue / SDMA knobs
+#
+# Every step runs under its own time limit (tools/gpu_steps.sh); a timeout or crash ends the call.
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+S="bash tools/gpu_steps.sh"
+B="python3 bench.py --steps 5 --warmup 2 --paced-windows 0"
+P="timeout -s KILL 120 rocprofv3 --output-format csv --kernel-trace --pmc"
+case "${1:-reentry}" in
+  reentry)
+    $S "400|gputests|python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread" \
+       "200|smoke|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
+       "300|bench|python -u bench.py" \
+       "300|trace|rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/trace -- python3 bench.py --steps 20 --warmup 3 --paced-windows 0" ;;
+  pmc)
+    $S "150|pmc1|$P SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES -d gpurun_out/pmc1 -- $B" \
+       "150|pmc2|$P SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d gpurun_out/pmc2 -- $B" \
+       "150|pmc3|$P FETCH_SIZE -d gpurun_out/pmc3 -- $B" \
+       "150|pmc4|$P WRITE_SIZE TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc4 -- $B" ;;
+  config2)
+    $S "600|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r3_config2_7b" ;;
+  overhead)
+    $S "200|agent_oh|python -u tools/agent_overhead.py --rate 1e6 --seconds 20 --out gpurun_out/r3_agent_overhead_1Mevs.json" ;;
+  config3)
+    $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r3_config3 ${2:-}" ;;
+  rss)
+    $S "120|rss_q1|GPU_MAX_HW_QUEUES=1 python tools/rss_probe.py" \
+       "120|rss_q1_devq|GPU_MAX_HW_QUEUES=1 HSA_ALLOCATE_QUEUE_DEV_MEM=1 python tools/rss_probe.py" \
+       "120|rss_q1_nosdma|GPU_MAX_HW_QUEUES=1 HSA_ENABLE_SDMA=0 python tools/rss_probe.py" ;;
+  *) echo "unknown suite: $1" >&2; exit 2 ;;
+esac
