@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--ring-mib", type=int, default=1024, help="emulated BPF ring buffer size (MiB, power of 2)")
     ap.add_argument("--no-graphs", action="store_true", help="launch the window kernels eagerly (no HIP graph)")
-    ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4))
+    ap.add_argument("--buffers", type=int, default=3, choices=(2, 3, 4, 5, 6))
     ap.add_argument("--halo-ms", type=float, default=2000.0,
                     help="carry rows within this distance of a window's latest record into the next window "
                          "(the agent's default)")

@@ -6,6 +6,7 @@
 # Suites:
 #   reentry   GPU tests, smoke(), the default bench, a kernel + copy trace of the bench
 #   pmc       rocprofv3 counter passes over a short bench (one pass per counter block budget)
+#   rptests   the rocprofiler tool's GPU tests (request GPU wait under contention included)
 #   config2   BASELINE config 2: Llama 7B preset, 800 ms TTFT SLO, onset -> first attribution
 #   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
@@ -28,12 +29,19 @@ case "${1:-reentry}" in
        "150|pmc2|$P SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d gpurun_out/pmc2 -- $B" \
        "150|pmc3|$P FETCH_SIZE -d gpurun_out/pmc3 -- $B" \
        "150|pmc4|$P WRITE_SIZE TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc4 -- $B" ;;
+  rptests)
+    $S "240|rp_tests|python -u -m pytest tests/test_rocprof_tool.py -m gpu -x -v -s --timeout 150 --timeout-method thread" ;;
   config2)
     $S "600|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r3_config2_7b" ;;
   overhead)
     $S "200|agent_oh|python -u tools/agent_overhead.py --rate 1e6 --seconds 20 --out gpurun_out/r3_agent_overhead_1Mevs.json" ;;
   config3)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r3_config3 ${2:-}" ;;
+  buffers)  # windows in flight: the copy of window k waits for window k - buffers + 1's results
+    for b in 3 4 5 4 3; do
+      $S "200|buf_$b|python3 bench.py --steps 100 --warmup 10 --buffers $b" || exit 1
+      tail -n 1 gpurun_out/buf_$b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('buffers', $b, d['ms_per_step'], d['value'], d['window_copy_ms'], d['window_device_ms_compute'])"
+    done ;;
   rss)
     $S "120|rss_q1|GPU_MAX_HW_QUEUES=1 python tools/rss_probe.py" \
        "120|rss_q1_devq|GPU_MAX_HW_QUEUES=1 HSA_ALLOCATE_QUEUE_DEV_MEM=1 python tools/rss_probe.py" \
