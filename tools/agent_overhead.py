@@ -105,7 +105,12 @@ def main() -> int:
            "--window-groups", str(a.groups), "--scenario", "full", "--output", "jsonl", "--output-path", out_path,
            "--metrics-bind", f"127.0.0.1:{port}"]
     t_start = time.time()
-    agent = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    # the agent as the DaemonSet starts it: the pod env has no GPU_MAX_HW_QUEUES, so the agent's own
+    # cap (--gpu-hw-queues, default 1) applies; a box-wide value (4 on the GPU pool) would win over it
+    # and map three more 173 MB queue save areas into the agent
+    env = dict(os.environ)
+    box_queues = env.pop("GPU_MAX_HW_QUEUES", None)
+    agent = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
     proc = psutil.Process(agent.pid)
     try:
         deadline = time.time() + 300
@@ -141,6 +146,7 @@ def main() -> int:
             "window_ms": a.window_ms,
             "measured_s": round(wall, 2),
             "agent_cpu_pct_of_one_core": round(agent_cpu, 3),
+            "box_gpu_max_hw_queues_removed_from_agent_env": box_queues,
             "agent_cpu_pct_gauge_ref_formula": m1.get("llm_slo_agent_cpu_overhead_pct"),
             "producer_cpu_pct_of_one_core": round(prod_cpu, 3),
             "agent_rss_mb": round(full.rss / 2**20, 1),
