@@ -7,12 +7,7 @@
 // the value in fixed point by the probes' own rule, mislo_record.h mislo_milli; USER24 packs
 // pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
-//   type 13 gpu_queue_delay_ms   the time kernels waited for the device (ns): per tagged request, the
-//                                sum over its dispatches of the queue wait (start - max(enqueue
-//                                return, queue predecessor end)) and the stretch (duration beyond
-//                                the kernel's uncontended duration at that launch shape), one record
-//                                once the request's dispatches go idle; untagged dispatches: the
-//                                queue wait, one record per dispatch
+//   type 13 gpu_queue_delay_ms   kernel dispatch: start - max(enqueue return, queue predecessor end) (ns)
 //   type 14 hbm_pressure_pct     the GPU's node-wide HBM use: amdgpu sysfs mem_info_vram_used /
 //                                mem_info_vram_total of the PCI device the process allocates on
 //                                (every process's allocations, not this one's), sampled on
@@ -38,8 +33,7 @@
 // Environment: MISLO_RING (default /mislo-agent-events), MISLO_POD_ID, MISLO_NODE_ID,
 // MISLO_SVC_ID, MISLO_HBM_BYTES (fallback capacity when sysfs is unreadable, default 288 GiB),
 // MISLO_PCI_SYSFS (default /sys/bus/pci/devices), MISLO_HBM_SAMPLE_MS (default 1000),
-// MISLO_MAX_EPS (default 200000), MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_REQUEST_IDLE_MS
-// (default 50), MISLO_XGMI_GBPS (a
+// MISLO_MAX_EPS (default 200000), MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_XGMI_GBPS (a
 // pair's starting rate before it has shown a large copy, default 64 GB/s: one xGMI link
 // direction), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
@@ -119,7 +113,6 @@ struct State {
   uint64_t hbm_bytes = 288ull << 30;
   uint64_t max_eps = 200000;
   uint64_t queue_floor_ns = 100000;
-  uint64_t request_idle_ns = 50000000;  // a request's accumulated wait is emitted after this idle gap
   double xgmi_bytes_per_ns = 64.0;
   bool rec32 = false;  // the ring holds 32-byte USER32 records
   bool rec24 = false;  // the ring holds 24-byte USER24 records
@@ -131,14 +124,6 @@ struct State {
   std::unordered_map<uint64_t, Enq> enqueue_ts;  // correlation id -> enqueue time, request trace
   std::unordered_map<uint64_t, uint64_t> queue_last;  // HW queue -> its latest enqueued dispatch id
   std::unordered_map<uint64_t, uint64_t> disp_end;    // dispatch id -> end, until its successor completes
-  // uncontended duration per launch shape (kernel, grid, workgroup): a low-tracking average that
-  // follows a faster run at once and a slower one by 1/1024 per dispatch
-  std::unordered_map<uint64_t, double> base_dur;
-  struct Req {
-    uint64_t wait = 0, last_end = 0;
-    uint32_t thread = 0;
-  };
-  std::unordered_map<uint64_t, Req> req;  // tagged request -> its dispatches' accumulated wait
   std::unordered_map<uint64_t, uint64_t> live_alloc;  // address -> bytes
   uint64_t live_bytes = 0;
   // node-wide HBM of the GPUs this process uses: agent handle -> the PCI device's VRAM counters
@@ -283,8 +268,6 @@ uint64_t xgmi_latency(uint64_t src, uint64_t dst, uint64_t bytes, uint64_t dur) 
   return dur > xfer ? dur - xfer : 0;
 }
 
-void flush_requests(uint64_t now, uint64_t idle);
-
 void sampler_main() {
   std::unique_lock<std::mutex> lk(g.smu);
   while (!g.scv.wait_for(lk, std::chrono::milliseconds(g.hbm_sample_ms), [] { return g.stop; })) {
@@ -292,8 +275,6 @@ void sampler_main() {
     rocprofiler_get_timestamp(&now);
     for (auto& kv : g.vram)
       if (kv.second.last_milli != ~0ull) emit_hbm(now, kv.first);  // the GPUs this process has used
-    std::lock_guard<std::mutex> rl(g.mu);
-    flush_requests(now, g.request_idle_ns);  // requests whose last kernel ended a while ago
   }
 }
 
@@ -312,40 +293,6 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
     g.vram[a->id.handle] = v;
   }
   return ROCPROFILER_STATUS_SUCCESS;
-}
-
-// Emit (and forget) the tagged requests idle since before `now` - idle (all of them: idle = 0,
-// now = ~0). Caller holds g.mu.
-void flush_requests(uint64_t now, uint64_t idle) {
-  for (auto it = g.req.begin(); it != g.req.end();) {
-    if (it->second.last_end + idle < now) {
-      if (it->second.wait >= g.queue_floor_ns && it->second.wait > 0)
-        emit(kQueueDelay, it->second.last_end, it->second.wait, it->second.thread, it->first);
-      it = g.req.erase(it);
-    } else {
-      ++it;
-    }
-  }
-}
-
-// The part of a dispatch's duration beyond its launch shape's uncontended duration (0 within a
-// 25 % + 5 us jitter allowance). Caller holds g.mu.
-uint64_t stretch_ns(const rocprofiler_kernel_dispatch_info_t& di, uint64_t dur) {
-  uint64_t h = di.kernel_id * 0x9E3779B97F4A7C15ull;
-  for (uint64_t v : {(uint64_t)di.grid_size.x, (uint64_t)di.grid_size.y, (uint64_t)di.grid_size.z,
-                     (uint64_t)di.workgroup_size.x, (uint64_t)di.workgroup_size.y, (uint64_t)di.workgroup_size.z})
-    h = (h ^ v) * 0x100000001B3ull;
-  auto it = g.base_dur.find(h);
-  if (it == g.base_dur.end()) {
-    if (g.base_dur.size() > 65536) g.base_dur.clear();
-    g.base_dur.emplace(h, (double)dur);
-    return 0;
-  }
-  double& b = it->second;
-  const double slack = 1.25 * b + 5000.0;
-  const uint64_t out = (double)dur > slack ? (uint64_t)((double)dur - b) : 0;
-  b += ((double)dur - b) * ((double)dur < b ? 1.0 : 1.0 / 1024.0);
-  return out;
 }
 
 // Kernel dispatch ENQUEUE (host side) and COMPLETE (with device start/end timestamps).
@@ -404,18 +351,10 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
         }
       }
     }
-    const uint64_t wait = known && enq.ts && d->start_timestamp > ready ? d->start_timestamp - ready : 0;
-    if (enq.trace_h) {
-      // a request's kernels: their waits add up to what the device cost the request
-      std::lock_guard<std::mutex> lk(g.mu);
-      const uint64_t dur = d->end_timestamp > d->start_timestamp ? d->end_timestamp - d->start_timestamp : 0;
-      State::Req& r = g.req[enq.trace_h];
-      r.wait += wait + stretch_ns(d->dispatch_info, dur);
-      r.last_end = std::max(r.last_end, d->end_timestamp);
-      r.thread = (uint32_t)rec.thread_id;
-      flush_requests(d->end_timestamp, g.request_idle_ns);
-    } else if (wait && wait >= g.queue_floor_ns) {
-      emit(kQueueDelay, d->start_timestamp, wait, (uint32_t)rec.thread_id, 0);
+    if (known && enq.ts && d->start_timestamp > ready) {
+      const uint64_t delay = d->start_timestamp - ready;
+      if (delay >= g.queue_floor_ns)
+        emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id, enq.trace_h);
     }
   }
 }
@@ -482,7 +421,6 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.hbm_bytes = env_u64("MISLO_HBM_BYTES", 288ull << 30);
   g.max_eps = env_u64("MISLO_MAX_EPS", 200000);
   g.queue_floor_ns = env_u64("MISLO_QUEUE_FLOOR_NS", 100000);
-  g.request_idle_ns = env_u64("MISLO_REQUEST_IDLE_MS", 50) * 1000000ull;
   g.xgmi_bytes_per_ns = (double)env_u64("MISLO_XGMI_GBPS", 64);  // GB/s == bytes/ns
   g.verbose = env_u64("MISLO_ROCPROF_VERBOSE", 0) != 0;
   if (const char* ps = std::getenv("MISLO_PCI_SYSFS")) g.pci_sysfs = ps;
@@ -535,10 +473,6 @@ void tool_fini(void*) {
   g.scv.notify_all();
   if (g.sampler.joinable()) g.sampler.join();
   rocprofiler_flush_buffer(g.buffer);
-  {
-    std::lock_guard<std::mutex> lk(g.mu);
-    flush_requests(~0ull, 0);
-  }
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] pushed=%llu dropped=%llu\n", (unsigned long long)g.pushed.load(),
                  (unsigned long long)g.dropped.load());
