@@ -10,6 +10,7 @@
 #   config2   BASELINE config 2: Llama 7B preset, 800 ms TTFT SLO, onset -> first attribution
 #   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
+#   spread    the headline bench at K = 20 and K = 200, repeated on one box
 #   rss       the HIP runtime's resident floor under queue / SDMA knobs
 #
 # Every step runs under its own time limit (tools/gpu_steps.sh); a timeout or crash ends the call.
@@ -41,6 +42,15 @@ case "${1:-reentry}" in
     for b in 3 4 5 4 3; do
       $S "200|buf_$b|python3 bench.py --steps 100 --warmup 10 --buffers $b" || exit 1
       tail -n 1 gpurun_out/buf_$b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('buffers', $b, d['ms_per_step'], d['value'], d['window_copy_ms'], d['window_device_ms_compute'])"
+    done ;;
+  spread)  # the headline's spread on one box: K = 20 (the driver's default) and K = 200
+    for i in 1 2 3; do
+      $S "200|k20_$i|python3 bench.py --steps 20 --warmup 5" || exit 1
+      tail -n 1 gpurun_out/k20_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('K20', d['ms_per_step'], d['value'])"
+    done
+    for i in 1 2; do
+      $S "300|k200_$i|python3 bench.py --steps 200 --warmup 10" || exit 1
+      tail -n 1 gpurun_out/k200_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('K200', d['ms_per_step'], d['value'])"
     done ;;
   rss)
     $S "120|rss_q1|GPU_MAX_HW_QUEUES=1 python tools/rss_probe.py" \
