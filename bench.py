@@ -396,7 +396,10 @@ def main() -> int:
         hold_f, hold_c = [], []
         for j, img in enumerate(train_imgs):
             held = j % 4 == 3
-            k = src.stage(next_cut(), img.n_groups, train_codes[j], with_labels=True, learn=not held)["k"]
+            # learning windows: the likelihood statistics see single-fault incidents only (compound
+            # ones unlabelled, models/train.py likelihood_codes); held-out ones keep every label
+            codes = train_codes[j] if held else mtrain.likelihood_codes(train_codes[j])
+            k = src.stage(next_cut(), img.n_groups, codes, with_labels=True, learn=not held)["k"]
             if held:  # read before a later window reuses its results buffer
                 hold_f.append(pipe.results(k, img.n_groups)["feat"].astype(np.float64))
                 hold_c.append(train_codes[j])

@@ -178,6 +178,7 @@ class AgentOptions:
     procfs_sampler: bool = False         # runqueue_delay_ms from /proc schedstat (no BPF needed)
     procfs_pods: str = ""                # pid:pod-uid,... to watch ("" = the node's kubepods cgroups)
     procfs_interval_ms: int = 100
+    procfs_cpu_psi: bool = False         # cpu_steal_pct also from the pod group's cpu.pressure (pod-private cgroups)
     model_signals: str = ""              # signals the node's sources produce (others marginalised; "" = all)
     pair_prior: float = 0.0              # 2-fault prior mass added to a table model without pairs (0 = none)
 
@@ -348,6 +349,15 @@ class Agent:
             return
         self.metrics.set_cpu_overhead(pct)
         if exceeded:
+            ladder = getattr(self, "ladder", None)
+            if ladder is not None:  # window engine: floors -> sampler -> GPU producers -> probes
+                what = ladder.step()
+                if what:
+                    print(f"overhead budget exceeded: shed {what}", file=sys.stderr)
+                    gone = ladder.disabled()
+                    self.metrics.set_enabled_signals(
+                        self.supported, [x for x in self.generator.enabled_signals() if x not in gone])
+                return
             pm = getattr(self, "probe_manager", None)
             sig = pm.shed_next() if pm is not None else None  # really detach a kernel probe
             if pm is not None and sig:
@@ -677,9 +687,15 @@ class Agent:
                     cache["t"] = time.monotonic()
                 return cache["m"]
 
-            sampler = procfs.SchedstatSampler(targets, user.push, rec=int(user.rec_size), node_id=node_id)
+            # native: a C++ thread reads schedstat / cgroup / PSI and pushes into the user ring
+            sampler = procfs.NativeSampler(user, targets, node_id=node_id, cpu_psi=o.procfs_cpu_psi,
+                                           refresh_s=10.0 if not static else 3600.0)
             sampler.start(o.procfs_interval_ms / 1000.0)
             self.procfs = sampler
+        from ..safety import ShedLadder
+
+        self.ladder = ShedLadder(catalog.DISABLE_ORDER, maps=maps, sampler=sampler, user_ring=user,
+                                 probe_manager=getattr(self, "probe_manager", None), generator=self.generator)
         if self.guard is not None:
             self.guard.source = TreeCPUSampler(lambda: [os.getpid()] + pool.pids())
             self.guard.evaluate()

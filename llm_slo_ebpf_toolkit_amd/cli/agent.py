@@ -64,10 +64,13 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                      "overrides --model"),
         ("otlp-receiver-allow", d.otlp_receiver_allow, "comma-separated CIDRs allowed to export spans to the "
                                                        "receiver (empty = any)"),
-        ("procfs-sampler", False, "window engine: runqueue_delay_ms of pod processes from /proc schedstat "
+        ("procfs-sampler", False, "window engine: run-queue delay, CPU wait share (cpu_steal_pct), CFS throttling "
+                                  "and memory stall of pod processes from /proc schedstat and their cgroups "
                                   "(unprivileged; min-capability mode)"),
         ("procfs-pods", d.procfs_pods, "pid:pod-uid,... for the procfs sampler (empty: the kubepods cgroups)"),
         ("procfs-interval-ms", d.procfs_interval_ms, "procfs sampler interval"),
+        ("procfs-cpu-psi", False, "procfs sampler: cpu_steal_pct is also the pod cgroup's cpu.pressure 'some' share "
+                                  "(pod-private cgroups only)"),
         ("model-signals", d.model_signals, "window engine: comma-separated signals this node's sources produce; "
                                            "the model sums the others out instead of reading their absence as "
                                            "'not elevated' (empty = every signal)"),
@@ -115,7 +118,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
         checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), model_path=a.model_path,
         otlp_receiver_allow=a.otlp_receiver_allow, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
-        procfs_interval_ms=int(a.procfs_interval_ms), model_signals=a.model_signals,
+        procfs_interval_ms=int(a.procfs_interval_ms), procfs_cpu_psi=bool(a.procfs_cpu_psi),
+        model_signals=a.model_signals,
         pair_prior=float(a.pair_prior))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])

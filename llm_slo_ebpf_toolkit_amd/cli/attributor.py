@@ -137,7 +137,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.flag("device", "cpu", "posterior device: cpu|gpu (MFMA posterior kernel)", choices=("cpu", "gpu"))
     p.flag("model-path", "", "score with a trained model file (attributor --train / the agent's --model-path)")
     p.flag("train", False, "train a model file (--out) from --input labelled samples or the fault-replay set")
-    p.flag("train-windows", 32, "--train without --input: fault-replay training windows")
+    p.flag("train-windows", 48, "--train without --input: fault-replay training windows")
     p.flag("train-events", 16384, "--train: events per training window")
     p.flag("train-spans", 1024, "--train: spans per training window")
     p.flag("seed", 42, "--train: replay and random-init seed")

@@ -6,7 +6,8 @@ that no binary constructs. NEW's agent opens the maps the loader pinned (``make 
 
 * ``mislo_events`` -- the BPF ring buffer the window source consumes (runtime/csrc/bpfring.h);
 * ``mislo_cfg``   -- the agent writes the realtime-monotonic clock offset, the node id, the
-  per-signal emit floors (the overhead guard raises floors before it detaches probes) and the
+  per-signal emit floors (the overhead guard raises them to the evidence thresholds before it detaches
+  probes: safety.ShedLadder) and the
   epoch it publishes at every window cut;
 * ``mislo_pods``  -- cgroup id -> pod id, filled from the node's cgroup tree (pods discovered
   the way REF's ProcMetadataEnricher derives them, pkg/signals/metadata.go:95-118);

@@ -97,103 +97,202 @@ def read_schedstat(path: str) -> Optional[Tuple[int, int, int]]:
         return None
 
 
+STEAL_TYPE = 6             # catalogue kernel type of cpu_steal_pct (milli-percent in the record)
+CFS_TYPE = 12              # catalogue kernel type of cfs_throttled_ms (ns in the record)
+STEAL_FLOOR_MILLI = 1000   # 1 % of one CPU over the interval
+SIGNAL_TYPES = {"runqueue_delay_ms": RUNQUEUE_TYPE, "cpu_steal_pct": STEAL_TYPE,
+                "mem_reclaim_latency_ms": MEM_RECLAIM_TYPE, "cfs_throttled_ms": CFS_TYPE}
+ALL_MASK = sum(1 << t for t in SIGNAL_TYPES.values())
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as fh:
+            return fh.read()
+    except OSError:
+        return None
+
+
+def cgroup_files(pid: int, proc_root: str = "/proc", cgroup_root: str = "/sys/fs/cgroup",
+                 cpu_psi: bool = False) -> Tuple[str, str, str]:
+    """(quota group's cpu.stat, memory PSI file, cpu PSI file) of ``pid`` ("" = none):
+    runtime/csrc/procsampler.cpp ProcSampler::resolve. The CFS throttling of a process is its
+    nearest ancestor group with a CPU quota (cgroup v2 cpu.max, v1 cpu.cfs_quota_us)."""
+    cfs = mem = cpu = ""
+    text = _read(os.path.join(proc_root, str(pid), "cgroup"))
+    root = cgroup_root.rstrip("/")
+    for ln in (text or "").splitlines():
+        parts = ln.split(":", 2)
+        if len(parts) != 3:
+            continue
+        hid, ctrls, path = parts
+        if hid == "0" and not ctrls:  # v2
+            base = os.path.join(root, path.lstrip("/")).rstrip("/") or "/"
+            d = base
+            while True:
+                mx = _read(os.path.join(d, "cpu.max"))
+                if mx and not mx.startswith("max"):
+                    cfs = os.path.join(d, "cpu.stat")
+                    break
+                if len(d) <= len(root) or d == "/":
+                    break
+                d = os.path.dirname(d)
+            if os.access(os.path.join(base, "memory.pressure"), os.R_OK):
+                mem = os.path.join(base, "memory.pressure")
+            if cpu_psi and os.access(os.path.join(base, "cpu.pressure"), os.R_OK):
+                cpu = os.path.join(base, "cpu.pressure")
+        elif not cfs and "cpu" in ctrls.split(","):  # v1
+            mnt = os.path.join(root, ctrls)
+            d = os.path.join(mnt, path.lstrip("/")).rstrip("/")
+            while True:
+                q = _read(os.path.join(d, "cpu.cfs_quota_us"))
+                try:
+                    if q is not None and int(q.strip()) > 0:
+                        cfs = os.path.join(d, "cpu.stat")
+                        break
+                except ValueError:
+                    pass
+                if len(d) <= len(mnt) or d == "/":
+                    break
+                d = os.path.dirname(d)
+    if not mem and os.access(os.path.join(proc_root, "pressure", "memory"), os.R_OK):
+        mem = os.path.join(proc_root, "pressure", "memory")
+    return cfs, mem, cpu
+
+
+def read_throttled_ns(path: str) -> Optional[int]:
+    """cpu.stat throttled_usec (v2, -> ns) or throttled_time (v1, ns)."""
+    text = _read(path)
+    if text is None:
+        return None
+    kv = dict(ln.split(" ", 1) for ln in text.splitlines() if " " in ln)
+    try:
+        if "throttled_usec" in kv:
+            return int(kv["throttled_usec"]) * 1000
+        if "throttled_time" in kv:
+            return int(kv["throttled_time"])
+    except ValueError:
+        return None
+    return None
+
+
 class SchedstatSampler:
+    """The Python model of the native sampler (runtime/csrc/procsampler.cpp, ``NativeSampler``):
+    per watched process and interval, in this order,
+
+    * ``runqueue_delay_ms``: the mean run-queue wait per timeslice over its threads whose mean
+      reached the probe's 100 us floor;
+    * ``cpu_steal_pct``: its threads' summed run-queue wait over the interval, in percent of one
+      CPU (milli-percent in the record) -- CPU the process wanted and did not get; with
+      ``cpu_psi`` the larger of that and its (pod-private) group's cpu.pressure "some" share;
+    * ``cfs_throttled_ms``: the growth of its quota group's throttled time (CFS bandwidth);
+    * ``mem_reclaim_latency_ms``: the growth of its group's PSI memory stall (else the node's).
+
+    The agent runs the native sampler; this class is its oracle in the tests and the fallback
+    where the native runtime is not built."""
+
     def __init__(self, targets: Callable[[], Dict[int, int]], push: Callable[[np.ndarray], int], rec: int = 24,
-                 proc_root: str = "/proc", floor_ns: int = FLOOR_NS, node_id: int = 0):
+                 proc_root: str = "/proc", floor_ns: int = FLOOR_NS, node_id: int = 0,
+                 cgroup_root: str = "/sys/fs/cgroup", cpu_psi: bool = False,
+                 steal_floor_milli: int = STEAL_FLOOR_MILLI):
         """``targets()`` -> {pid: pod id}; ``push(records)`` -> records accepted (the user ring)."""
         self.targets, self.push, self.rec = targets, push, int(rec)
         self.proc_root, self.floor_ns, self.node_id = proc_root, int(floor_ns), int(node_id)
+        self.cgroup_root, self.cpu_psi, self.steal_floor = cgroup_root, bool(cpu_psi), int(steal_floor_milli)
+        self.mask = ALL_MASK
+        self.paused = False
         self._prev: Dict[Tuple[int, int], Tuple[int, int]] = {}
-        self._psi: Dict[int, Tuple[Optional[str], Optional[int]]] = {}   # pid -> (PSI file, last total us)
-        self._ns: Dict[int, int] = {}      # host pid -> pid in its own namespace
+        self._procs: Dict[int, Tuple[int, str, str, str]] = {}  # pid -> (ns pid, cfs, mem, cpu psi files)
+        self._groups: Dict[str, int] = {}                      # file -> last reading (ns)
+        self._prev_mono: Optional[int] = None
         self.samples = self.emitted = self.dropped = 0
         self._stop = threading.Event()
         self._thr: Optional[threading.Thread] = None
 
-    def sample(self, now_ns: Optional[int] = None) -> np.ndarray:
-        """One interval: EVENT records of the processes whose mean wait per timeslice crossed the floor."""
+    def _group_delta(self, path: str, kind: int, cache: Dict[str, int]) -> int:
+        if path in cache:
+            return cache[path]
+        v = read_throttled_ns(path) if kind == 0 else read_psi_total_us(path)
+        d = 0
+        if v is not None:
+            v = v if kind == 0 else v * 1000
+            last = self._groups.get(path)
+            if last is not None and v >= last:
+                d = v - last
+            self._groups[path] = v
+        cache[path] = d
+        return d
+
+    def sample(self, now_ns: Optional[int] = None, mono_ns: Optional[int] = None) -> np.ndarray:
+        """One interval: EVENT records of the watched processes (see the class docstring)."""
         now = int(now_ns if now_ns is not None else time.time_ns())
-        rows, seen = [], set()
+        # an interval given only as wall-clock times (tests) is measured on that clock
+        mono = int(mono_ns if mono_ns is not None else (now if now_ns is not None else time.monotonic_ns()))
+        dt = mono - self._prev_mono if self._prev_mono is not None and mono > self._prev_mono else 0
+        self._prev_mono = mono
+        rows = []
+        nxt: Dict[Tuple[int, int], Tuple[int, int]] = {}
+        live: Dict[int, Tuple[int, str, str, str]] = {}
+        cache: Dict[str, int] = {}
         for pid, pod in self.targets().items():
             task = os.path.join(self.proc_root, str(pid), "task")
             try:
-                tids = [int(t) for t in os.listdir(task) if t.isdigit()]
+                tids = sorted(int(t) for t in os.listdir(task) if t.isdigit())
             except OSError:
                 continue
-            w_sum = s_sum = 0
+            w_sum = s_sum = w_all = 0
             for tid in tids:
                 st = read_schedstat(os.path.join(task, str(tid), "schedstat"))
                 if st is None:
                     continue
                 key = (pid, tid)
-                seen.add(key)
+                nxt[key] = (st[1], st[2])
                 prev = self._prev.get(key)
-                self._prev[key] = (st[1], st[2])
                 if prev is None:
                     continue
-                dw, ds = st[1] - prev[0], st[2] - prev[1]
+                dw, ds = max(0, st[1] - prev[0]), max(0, st[2] - prev[1])
+                w_all += dw
                 if ds > 0 and dw >= self.floor_ns * ds:  # this thread's waits reach the floor
                     w_sum += dw
                     s_sum += ds
-            if s_sum and w_sum // s_sum >= self.floor_ns:
-                rows.append((self.pod_pid(pid), pid, pod, w_sum // s_sum))
-        for key in list(self._prev):
-            if key not in seen:
-                del self._prev[key]
-        alive = {k[0] for k in seen}
-        for pid in list(self._ns):
-            if pid not in alive:
-                del self._ns[pid]
-        mem = self._memory_rows()
+            info = self._procs.get(pid)
+            if info is None:
+                info = (ns_pid(pid, self.proc_root),) + cgroup_files(pid, self.proc_root, self.cgroup_root, self.cpu_psi)
+            live[pid] = info
+            npid, cfs, mem, cpu = info
+            if self.mask >> RUNQUEUE_TYPE & 1 and s_sum and w_sum // s_sum >= self.floor_ns:
+                rows.append((RUNQUEUE_TYPE, npid, pid, pod, w_sum // s_sum))
+            psi_d = self._group_delta(cpu, 1, cache) if cpu else 0  # read every tick
+            if self.mask >> STEAL_TYPE & 1 and dt:
+                milli = max(int(float(w_all) * 100000.0 / float(dt)), int(float(psi_d) * 100000.0 / float(dt)))
+                if milli >= self.steal_floor:
+                    rows.append((STEAL_TYPE, npid, pid, pod, milli))
+            if cfs:
+                d = self._group_delta(cfs, 0, cache)
+                if self.mask >> CFS_TYPE & 1 and d >= self.floor_ns:
+                    rows.append((CFS_TYPE, npid, pid, pod, d))
+            if mem:
+                d = self._group_delta(mem, 1, cache)
+                if self.mask >> MEM_RECLAIM_TYPE & 1 and d >= self.floor_ns:
+                    rows.append((MEM_RECLAIM_TYPE, npid, pid, pod, d))
+        self._prev = nxt
+        self._procs = live
+        self._groups = {k: v for k, v in self._groups.items() if k in cache}
         self.samples += 1
-        ev = np.zeros(len(rows) + len(mem), dtype=records.EVENT)
-        if len(ev):
-            a = np.array(rows + mem, dtype=np.int64)
+        ev = np.zeros(len(rows), dtype=records.EVENT)
+        if rows:
+            a = np.array(rows, dtype=np.int64)
             ev["ts_ns"] = now
-            ev["signal_type"] = np.where(np.arange(len(ev)) < len(rows), RUNQUEUE_TYPE, MEM_RECLAIM_TYPE)
-            ev["value"] = a[:, 3].astype(np.uint64)
-            ev["pid"] = a[:, 0].astype(np.uint32)
-            ev["tid"] = a[:, 1].astype(np.uint32)
-            ev["pod_id"] = a[:, 2].astype(np.uint32)
+            ev["signal_type"] = a[:, 0].astype(np.uint16)
+            ev["value"] = a[:, 4].astype(np.uint64)
+            ev["pid"] = a[:, 1].astype(np.uint32)
+            ev["tid"] = a[:, 2].astype(np.uint32)
+            ev["pod_id"] = a[:, 3].astype(np.uint32)
             ev["node_id"] = self.node_id
         return ev
 
-    def pod_pid(self, pid: int) -> int:
-        """The record's pid: ``pid`` as its own pod sees it (cached while it lives)."""
-        v = self._ns.get(pid)
-        if v is None:
-            v = self._ns[pid] = ns_pid(pid, self.proc_root)
-        return v
-
-    def _memory_rows(self):
-        """(pid, pid, pod, stall ns) of the watched processes whose PSI memory stall grew by at
-        least the floor since the last interval."""
-        rows = []
-        live = set()
-        totals: Dict[str, Optional[int]] = {}
-        for pid, pod in self.targets().items():
-            live.add(pid)
-            path, last = self._psi.get(pid, (None, None))
-            if path is None:
-                path = psi_path(pid, self.proc_root)
-                if path is None:
-                    continue
-            if path not in totals:
-                totals[path] = read_psi_total_us(path)
-            tot = totals[path]
-            self._psi[pid] = (path, tot)
-            if tot is None or last is None:
-                continue
-            d_ns = (tot - last) * 1000
-            if d_ns >= self.floor_ns:
-                rows.append((self.pod_pid(pid), pid, pod, d_ns))
-        for pid in list(self._psi):
-            if pid not in live:
-                del self._psi[pid]
-        return rows
-
-    def tick(self, now_ns: Optional[int] = None) -> int:
-        ev = self.sample(now_ns)
+    def tick(self, now_ns: Optional[int] = None, mono_ns: Optional[int] = None) -> int:
+        ev = self.sample(now_ns, mono_ns)
         if not len(ev):
             return 0
         n = int(self.push(records.to_user(ev, self.rec)))
@@ -204,6 +303,8 @@ class SchedstatSampler:
     def start(self, interval_s: float = 0.1) -> "SchedstatSampler":
         def run():
             while not self._stop.wait(interval_s):
+                if self.paused:
+                    continue
                 try:
                     self.tick()
                 except Exception:  # noqa: BLE001 - a sampler hiccup must not stop the agent
@@ -217,6 +318,74 @@ class SchedstatSampler:
         self._stop.set()
         if self._thr is not None:
             self._thr.join(5)
+
+    def stats(self) -> Dict[str, int]:
+        return {"ticks": self.samples, "emitted": self.emitted, "dropped": self.dropped}
+
+
+class NativeSampler:
+    """The agent's sampler: runtime/csrc/procsampler.cpp on its own thread, pushing straight into
+    the user ring (no Python per record or per file). ``targets`` is re-read every
+    ``refresh_s`` by a light Python timer (pod churn); everything per interval is native."""
+
+    def __init__(self, ring, targets: Callable[[], Dict[int, int]], node_id: int = 0, proc_root: str = "/proc",
+                 cgroup_root: str = "/sys/fs/cgroup", cpu_psi: bool = False, floor_ns: int = FLOOR_NS,
+                 steal_floor_milli: int = STEAL_FLOOR_MILLI, refresh_s: float = 10.0):
+        from ..runtime import load
+
+        rt = load()
+        self.targets, self.refresh_s = targets, float(refresh_s)
+        self.native = rt.ProcSampler(ring, node_id, proc_root, cgroup_root, bool(cpu_psi), int(floor_ns),
+                                     int(steal_floor_milli), int(floor_ns), int(floor_ns))
+        self._stop = threading.Event()
+        self._thr: Optional[threading.Thread] = None
+
+    @property
+    def mask(self) -> int:
+        return int(self.native.mask)
+
+    @mask.setter
+    def mask(self, m: int) -> None:
+        self.native.mask = int(m)
+
+    @property
+    def paused(self) -> bool:
+        return bool(self.native.paused)
+
+    @paused.setter
+    def paused(self, p: bool) -> None:
+        self.native.paused = bool(p)
+
+    def refresh(self) -> None:
+        self.native.set_target_list(sorted((int(p), int(v)) for p, v in self.targets().items()))
+
+    def sample(self, now_ns: int, mono_ns: int) -> np.ndarray:
+        """One interval by hand (tests): the EVENT records it produced (also pushed)."""
+        return np.frombuffer(self.native.tick(int(now_ns), int(mono_ns)), dtype=records.EVENT)
+
+    def start(self, interval_s: float = 0.1) -> "NativeSampler":
+        self.refresh()
+        self.native.start(float(interval_s))
+
+        def run():
+            while not self._stop.wait(self.refresh_s):
+                try:
+                    self.refresh()
+                except Exception:  # noqa: BLE001 - keep the last target list
+                    pass
+
+        self._thr = threading.Thread(target=run, name="procfs-targets", daemon=True)
+        self._thr.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.native.stop()
+        if self._thr is not None:
+            self._thr.join(5)
+
+    def stats(self) -> Dict[str, int]:
+        return dict(self.native.stats())
 
 
 def parse_pod_list(spec: str) -> Dict[int, str]:

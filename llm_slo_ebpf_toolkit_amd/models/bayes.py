@@ -348,7 +348,8 @@ def with_pairs(m: LinearPosteriorModel, rho: float, temperature: float = 1.0) ->
     return out
 
 
-def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature: float = 1.0) -> LinearPosteriorModel:
+def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature: float = 1.0,
+                drop_unobservable: bool = True) -> LinearPosteriorModel:
     """The binary naive-Bayes model scoring only the ``observable`` signals: every other table
     signal is summed out of the likelihood (its factor P(e_s | d) marginalises to 1) instead of
     being read as "not elevated". An agent whose sources cannot produce a signal at all (no
@@ -358,7 +359,8 @@ def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature:
     In the linear-logit form a table signal contributes ``e * W[s, d]`` plus ``log P(not e | d)``
     folded into the bias, with ``W = logit(P(e | d))``; so summing it out is ``W[s, :] = 0`` and
     ``bias[d] += softplus(W[s, d])``, both at the model's ``temperature`` (stored weights and bias
-    are divided by it)."""
+    are divided by it). With ``drop_unobservable`` a domain none of the observable signals indicates
+    is deactivated (below); without it the result is the exact marginal of the full model."""
     if m.feature_mode != "binary":
         raise ValueError("only binary naive-Bayes models marginalise signal by signal")
     keep = {catalog.BY_NAME[s].slot for s in observable if s in catalog.BY_NAME}
@@ -383,6 +385,21 @@ def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature:
             pw[s] = 0.0
         mask[s] = False
         table[s] = 0.0
+    # a fault domain that no observable signal indicates (P(e | d) >= 0.5 and at least twice
+    # P(e | unknown)) cannot be told apart from "unknown" on this node: with its evidence summed
+    # out it would win on its prior alone whenever nothing is elevated. It is not attributed.
+    if drop_unobservable and "unknown" in catalog.DOMAIN_INDEX and keep:
+        u = catalog.DOMAIN_INDEX["unknown"]
+        raw = m.weights * T
+        p = 1.0 / (1.0 + np.exp(-raw))
+        obs = np.array(sorted(keep))
+        for d in range(W.shape[1]):
+            if d == u or not fin[d]:
+                continue
+            if not np.any((p[obs, d] >= 0.5) & (p[obs, d] >= 2.0 * p[obs, u])):
+                b[d] = NEG_INF
+                if pb is not None:
+                    pb[(m.pairs[:, 0] == d) | (m.pairs[:, 1] == d)] = NEG_INF
     out = LinearPosteriorModel(m.name, W, b, mask, m.feature_mode, m.thresholds.copy(), None, table)
     if pw is not None:
         out.pair_w, out.pair_b, out.pairs, out.pair_rho = pw, pb, m.pairs.copy(), m.pair_rho

@@ -24,7 +24,9 @@ LABEL_TO_DOMAIN = {
     "retrieval_slowdown": "retrieval_backend",
     # NEW (MI355X) fault labels
     "gpu_contention": "gpu_contention",
+    "gpu_compute_contention": "gpu_contention",
     "hbm_pressure": "gpu_contention",
+    "cpu_contention": "cpu_throttle",
     "rccl_latency": "gpu_interconnect",
     "xgmi_degraded": "gpu_interconnect",
 }

@@ -10,7 +10,11 @@ agent loads (``agent --model-path``):
    faults of every domain (scenario ``full``) alternating with compound incidents (scenario
    ``compound``: every pair and triple of REF's five fault labels -- REF's faultreplay
    mixed_multi pairs, generator.go:61-66, and its incident-lab compound scenario,
-   test/incident-lab/scenarios/mixed_multi.yaml, which injects three at once);
+   test/incident-lab/scenarios/mixed_multi.yaml, which injects three at once), and windows of
+   the shapes the CPU and GPU contention domains take on a live node (scenario ``live``:
+   signals/generator.py cpu_contention -- a noisy neighbour on a pod without a CPU limit --
+   and gpu_compute_contention -- another process's kernels without an HBM fill -- next to REF's
+   cpu_throttle and the HBM-filling gpu_contention, alone and with a network fault);
 2. **features** -- each incident group's features as the window engine computes them from the
    records (decode -> 4-tier join -> per-group means): the GPU engine in the benchmark, the CPU
    oracle engine here (identical by the GPU tests);
@@ -49,13 +53,13 @@ from .bayes import (N_DOMAINS, PAIR_LIST, LinearPosteriorModel, NaiveBayes, Suff
 
 REF_FAULTS = ("provider_throttle", "dns_latency", "cpu_throttle", "memory_pressure", "network_partition")
 COMPOUND = [c for k in (2, 3) for c in itertools.combinations(REF_FAULTS, k)]
-TRAIN_SCENARIOS = ("full", "compound")
+TRAIN_SCENARIOS = ("full", "compound", "live")
 MODEL_FORMAT = "mislo-model/1"
 
 
 @dataclass
 class TrainConfig:
-    windows: int = 32                 # labelled training windows (cycling TRAIN_SCENARIOS)
+    windows: int = 48                 # labelled training windows (cycling TRAIN_SCENARIOS)
     events_per_window: int = 16384
     spans_per_window: int = 1024
     services: int = 64                # incident groups per window
@@ -66,6 +70,11 @@ class TrainConfig:
     holdout_every: int = 4            # every 4th window is held out for the temperature fit
     t_grid: Tuple[float, float, int] = (1.0, 20.0, 64)
     pairs: bool = True                # 2-fault posterior (bayes.with_pairs)
+    # the single domains' likelihoods from single-fault (and healthy) incidents only: a compound
+    # incident's evidence is the pair hypothesis's (noisy-OR of its members), and spread over its
+    # members as soft labels it taught every member the other's symptoms (P(dns elevated |
+    # cpu_throttle) ~ 0.3), which then counted against a lone CPU fault
+    single_fault_likelihoods: bool = True
 
 
 @dataclass
@@ -187,6 +196,16 @@ def pair_prior(codes: np.ndarray) -> float:
     return (multi + 1.0) / (len(c) + 2.0)
 
 
+def likelihood_codes(codes: np.ndarray, cfg: Optional[TrainConfig] = None) -> np.ndarray:
+    """The label codes the likelihood statistics learn from: compound incidents unlabelled (-1)
+    under ``single_fault_likelihoods`` -- the rule the host fit and the device statistics kernel
+    (bench.py's training windows) share."""
+    c = np.asarray(codes, dtype=np.int32)
+    if cfg is not None and not cfg.single_fault_likelihoods:
+        return c
+    return np.where(((c.astype(np.int64) >> 8) & 0xFFFF) != 0, np.int32(-1), c).astype(np.int32)
+
+
 def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: TrainConfig) -> TrainedModel:
     """Statistics on the training windows, temperature on the held-out ones."""
     feats = np.asarray(feats, dtype=np.float64)
@@ -194,7 +213,8 @@ def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: Train
     hold = (np.asarray(window_ids) % cfg.holdout_every) == cfg.holdout_every - 1
     tr = ~hold & (np.asarray(codes) >= 0)
     st = SufficientStats()
-    st.add(feats[tr], Y[tr])
+    single = likelihood_codes(codes, cfg) >= 0
+    st.add(feats[tr & single], Y[tr & single])
     base = NaiveBayes.learned(st, alpha=cfg.alpha, seed=cfg.seed, prior_pseudo=cfg.prior_pseudo,
                               min_count=cfg.min_count)
     hv = hold & (np.asarray(codes) >= 0)
@@ -208,7 +228,7 @@ def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: Train
             hnll = hypothesis_nll(model, feats[hv], *hypothesis_targets(np.asarray(codes)[hv]))
     model.name = "bayes_learned"
     meta = {"temperature": t, "pair_rho": rho, "holdout_hypothesis_nll": hnll, "holdout_nll": nll, "holdout_nll_t1": soft_nll(base, feats[hv], Y[hv], 1.0)
-            if hv.any() else float("nan"), "train_incidents": int(tr.sum()), "holdout_incidents": int(hv.sum()),
+            if hv.any() else float("nan"), "train_incidents": int(tr.sum()), "likelihood_incidents": int((tr & single).sum()), "holdout_incidents": int(hv.sum()),
             "domain_mass": {catalog.ALL_DOMAINS[d]: round(float(st.count[d]), 3) for d in range(N_DOMAINS)},
             "active_domains": [catalog.ALL_DOMAINS[d] for d in range(N_DOMAINS) if np.isfinite(model.bias[d])]}
     return TrainedModel(model, st, t, meta)

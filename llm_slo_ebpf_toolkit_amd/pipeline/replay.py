@@ -49,6 +49,11 @@ SCENARIOS: Dict[str, List[Tuple[str, ...]]] = {
     # NEW: every single fault incl. the MI355X GPU faults (config 5: all fault domains)
     "full": [("provider_throttle",), ("dns_latency",), ("cpu_throttle",), ("memory_pressure",),
              ("network_partition",), ("gpu_contention",), ("rccl_latency",)],
+    # NEW: the live-node shapes of the CPU and GPU contention domains (signals/generator.py
+    # cpu_contention, gpu_compute_contention) next to REF's, alone and with a network fault
+    "live": [("cpu_contention",), ("gpu_compute_contention",), ("cpu_throttle",), ("gpu_contention",),
+             ("cpu_contention", "network_partition"), ("gpu_compute_contention", "network_partition"),
+             ("network_partition",), ("dns_latency",)],
 }
 
 COUNT_SIGNALS = {"tcp_retransmits_total", "connect_errors_total", "tls_handshake_fail_total"}
@@ -120,6 +125,9 @@ class ReplayWindow:
 # config-3 runs with the CPUs contended: GPU queue delay p50 6-9 ms, 700-900 dispatches per
 # 15-s phase above the 2-ms warning level, profiles/r3_config3_*). REF's profiles describe
 # CPU-only services, so the coupling is added here, on top of them.
+# The live shape (cpu_contention) has no coupling: the rocprofiler tool's queue delay no longer
+# counts a starved launcher's waits behind its own queue, and its foreign-GPU-time records need
+# another process on the device (tests/test_rocprof_tool.py).
 GPU_SERVED_COUPLING: Dict[str, Dict[str, float]] = {
     "cpu_throttle": {"gpu_queue_delay_ms": 6.0},
 }

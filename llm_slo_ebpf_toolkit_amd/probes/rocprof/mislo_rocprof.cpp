@@ -7,7 +7,14 @@
 // the value in fixed point by the probes' own rule, mislo_record.h mislo_milli; USER24 packs
 // pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
-//   type 13 gpu_queue_delay_ms   kernel dispatch: start - max(enqueue return, queue predecessor end) (ns)
+//   type 13 gpu_queue_delay_ms   (a) kernel dispatch: start - max(enqueue return, queue predecessor end) (ns);
+//                                (b) foreign GPU time: every MISLO_FOREIGN_MS (default 100) while this
+//                                process runs kernels, the GPU time other processes held over the
+//                                interval -- the device's GFX activity (amdgpu gpu_metrics
+//                                gfx_activity_acc, an exact integral; else gpu_busy_percent) minus
+//                                this process's own kernel time (the union of its dispatches'
+//                                [start, end]) -- emitted when it reaches MISLO_FOREIGN_FLOOR_PCT
+//                                (default 10) of the interval, as ns of the interval (ns)
 //   type 14 hbm_pressure_pct     the GPU's node-wide HBM use: amdgpu sysfs mem_info_vram_used /
 //                                mem_info_vram_total of the PCI device the process allocates on
 //                                (every process's allocations, not this one's), sampled on
@@ -30,12 +37,20 @@
 // receiver's rule), so the agent joins them to the request's spans through the trace tier
 // instead of the coarser pod+pid window.
 //
+// Shedding: the agent's overhead guard sets bits in the ring header's drop mask (runtime/csrc/ring.h);
+// a record whose signal type's bit is set is not emitted (counted as dropped).
+//
 // Environment: MISLO_RING (default /mislo-agent-events), MISLO_POD_ID, MISLO_NODE_ID,
 // MISLO_SVC_ID, MISLO_HBM_BYTES (fallback capacity when sysfs is unreadable, default 288 GiB),
 // MISLO_PCI_SYSFS (default /sys/bus/pci/devices), MISLO_HBM_SAMPLE_MS (default 1000),
-// MISLO_MAX_EPS (default 200000), MISLO_QUEUE_FLOOR_NS (default 100000), MISLO_XGMI_GBPS (a
+// MISLO_MAX_EPS (default 200000), MISLO_QUEUE_FLOOR_NS (default 10 ms: below that a dispatch's wait
+// on an otherwise idle GPU is clock / power-state ramp, not another process -- config-2 baselines
+// read 2-5 ms waits there, while contention shows up as foreign GPU time), MISLO_XGMI_GBPS (a
 // pair's starting rate before it has shown a large copy, default 64 GB/s: one xGMI link
-// direction), MISLO_ROCPROF_VERBOSE.
+// direction; a pair's calibration starts there and a measured rate may only raise it, to at most
+// 4x: a link already degraded when the process starts is not its own baseline),
+// MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_FOREIGN_MIN_OWN_PCT (default 1: the process must
+// have run kernels for this share of the interval), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/buffer_tracing.h>
 #include <rocprofiler-sdk/callback_tracing.h>
@@ -68,6 +83,7 @@ void* mislo_ring_open_shm(const char* name);
 uint32_t mislo_ring_rec_size(void* ring);
 void mislo_ring_close(void* ring);
 uint64_t mislo_ring_push_batch(void* ring, const void* recs, uint64_t n);
+uint32_t mislo_ring_drop_mask(void* ring);
 }
 
 namespace {
@@ -112,7 +128,7 @@ struct State {
   uint16_t node = 0, svc = 0;
   uint64_t hbm_bytes = 288ull << 30;
   uint64_t max_eps = 200000;
-  uint64_t queue_floor_ns = 100000;
+  uint64_t queue_floor_ns = 10000000;
   double xgmi_bytes_per_ns = 64.0;
   bool rec32 = false;  // the ring holds 32-byte USER32 records
   bool rec24 = false;  // the ring holds 24-byte USER24 records
@@ -132,6 +148,20 @@ struct State {
     uint64_t last_milli = ~0ull;
   };
   std::map<uint64_t, Vram> vram;
+  std::mutex hbm_mu;  // emit_hbm runs on the sampler thread and the buffer callback thread
+  // foreign GPU time per GPU agent: this process's kernel time (union of dispatch [start, end],
+  // guarded by mu) against the device's activity accumulator (sampler thread only)
+  struct Busy {
+    int metrics_fd = -1, busy_fd = -1;
+    bool acc = false;           // gpu_metrics carries gfx_activity_acc at byte 76 (format 1.7 / 1.8)
+    uint64_t own_ns = 0, own_last_end = 0;
+    uint32_t last_acc = 0;
+    uint64_t last_t = 0;        // rocprofiler ns of the last reading (0: not primed)
+    double dev_pct = 0.0, own_pct = 0.0;  // last interval (tests)
+    uint64_t intervals = 0;
+  };
+  std::map<uint64_t, Busy> busy;
+  uint64_t foreign_ms = 100, foreign_floor_pct = 10, foreign_min_own_pct = 1;
   std::string pci_sysfs = "/sys/bus/pci/devices";
   uint64_t hbm_sample_ms = 1000;
   uint64_t last_hbm_milli = ~0ull;  // fallback (no sysfs): this process's live allocations
@@ -162,6 +192,10 @@ uint32_t tid() { return (uint32_t)syscall(SYS_gettid); }
 
 void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t trace_h = 0) {
   if (!g.ring) return;
+  if (type < 32 && (mislo_ring_drop_mask(g.ring) >> type & 1u)) {  // shed by the agent's overhead guard
+    g.dropped.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
   const int64_t wall = (int64_t)ts + g.clock_offset;
   const uint64_t sec = (uint64_t)wall / 1000000000ull;
   if (g.window_sec.load(std::memory_order_relaxed) != sec) {
@@ -245,6 +279,7 @@ bool hbm_milli(uint64_t agent, uint64_t* out, uint64_t** last) {
 
 // emitted when the GPU's pressure moved by >= 0.1 pct-point since its last record
 void emit_hbm(uint64_t ts, uint64_t agent) {
+  std::lock_guard<std::mutex> lk(g.hbm_mu);
   uint64_t milli = 0, *last = nullptr;
   if (!hbm_milli(agent, &milli, &last)) return;
   if (*last != ~0ull && (milli > *last ? milli - *last : *last - milli) < 100) return;
@@ -256,25 +291,88 @@ void emit_hbm(uint64_t ts, uint64_t agent) {
 uint64_t xgmi_latency(uint64_t src, uint64_t dst, uint64_t bytes, uint64_t dur) {
   std::lock_guard<std::mutex> lk(g.mu);
   State::Link& l = g.links[{src, dst}];
+  if (l.copies == 0) l.bytes_per_ns = g.xgmi_bytes_per_ns;  // nominal: a measured rate only raises it
   ++l.copies;
   if (bytes <= (64u << 10)) {  // small copy: the duration is the link's latency
     if (dur < l.min_small_ns) l.min_small_ns = dur;
     return dur;
   }
   const double rate = (double)bytes / (double)dur;
-  if (bytes >= (1u << 20) && rate > l.bytes_per_ns) l.bytes_per_ns = rate;  // calibrated bandwidth
+  if (bytes >= (1u << 20) && rate > l.bytes_per_ns)  // calibrated bandwidth, at most 4x the nominal rate
+    l.bytes_per_ns = rate < 4.0 * g.xgmi_bytes_per_ns ? rate : 4.0 * g.xgmi_bytes_per_ns;
   const double bw = l.bytes_per_ns > 0.0 ? l.bytes_per_ns : g.xgmi_bytes_per_ns;
   const uint64_t xfer = (uint64_t)((double)bytes / bw);
   return dur > xfer ? dur - xfer : 0;
 }
 
+// The device's GFX activity over (last reading, now] in percent: the gpu_metrics accumulator
+// (percent x ms, exact over any interval) or, without it, the driver's smoothed busy percent.
+bool device_busy_pct(State::Busy& b, uint64_t now, double* pct) {
+  char buf[96];
+  if (b.acc) {
+    if (pread(b.metrics_fd, buf, sizeof(buf), 0) < 80) return false;
+    uint32_t acc;
+    std::memcpy(&acc, buf + 76, 4);
+    const bool primed = b.last_t != 0;
+    const uint64_t dt = now - b.last_t;
+    const uint32_t d = acc - b.last_acc;
+    b.last_acc = acc;
+    if (!primed || dt == 0) return false;
+    *pct = (double)d * 1e6 / (double)dt;  // (percent x ms) per ms
+    return true;
+  }
+  if (b.busy_fd < 0) return false;
+  const ssize_t n = pread(b.busy_fd, buf, sizeof(buf) - 1, 0);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  *pct = std::strtod(buf, nullptr);
+  return b.last_t != 0;
+}
+
+// Every foreign_ms: per GPU this process has run kernels on, the GPU time others held.
+void foreign_tick(uint64_t now) {
+  for (auto& kv : g.busy) {
+    State::Busy& b = kv.second;
+    if (b.metrics_fd < 0 && b.busy_fd < 0) continue;
+    double dev = 0.0;
+    const bool ok = device_busy_pct(b, now, &dev);
+    const uint64_t dt = b.last_t ? now - b.last_t : 0;
+    b.last_t = now;
+    uint64_t own;
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      own = b.own_ns;
+      b.own_ns = 0;
+    }
+    if (!ok || dt == 0) continue;
+    double own_pct = 100.0 * (double)own / (double)dt;
+    if (own_pct > 100.0) own_pct = 100.0;
+    if (dev > 100.0) dev = 100.0;
+    b.dev_pct = dev, b.own_pct = own_pct;
+    ++b.intervals;
+    const double foreign = dev - own_pct;
+    if (own_pct >= (double)g.foreign_min_own_pct && foreign >= (double)g.foreign_floor_pct)
+      emit(kQueueDelay, now - dt / 2, (uint64_t)(foreign / 100.0 * (double)dt), 0);
+  }
+}
+
 void sampler_main() {
   std::unique_lock<std::mutex> lk(g.smu);
-  while (!g.scv.wait_for(lk, std::chrono::milliseconds(g.hbm_sample_ms), [] { return g.stop; })) {
+  const uint64_t tick = g.foreign_ms ? (g.hbm_sample_ms ? std::min(g.foreign_ms, g.hbm_sample_ms) : g.foreign_ms)
+                                     : g.hbm_sample_ms;
+  uint64_t next_hbm = 0, next_foreign = 0;
+  while (!g.scv.wait_for(lk, std::chrono::milliseconds(tick), [] { return g.stop; })) {
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
-    for (auto& kv : g.vram)
-      if (kv.second.last_milli != ~0ull) emit_hbm(now, kv.first);  // the GPUs this process has used
+    if (g.hbm_sample_ms && now >= next_hbm) {
+      next_hbm = now + g.hbm_sample_ms * 1000000ull - 500000ull;
+      for (auto& kv : g.vram)
+        if (kv.second.last_milli != ~0ull) emit_hbm(now, kv.first);  // the GPUs this process has used
+    }
+    if (g.foreign_ms && now >= next_foreign) {
+      next_foreign = now + g.foreign_ms * 1000000ull - 500000ull;
+      foreign_tick(now);
+    }
   }
 }
 
@@ -291,6 +389,19 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
     if (g.verbose)
       std::fprintf(stderr, "[mislo-rocprof] GPU %s: vram sysfs %s\n", bdf, v.used_fd >= 0 ? "ok" : "unreadable");
     g.vram[a->id.handle] = v;
+    State::Busy b;
+    b.metrics_fd = open((g.pci_sysfs + "/" + bdf + "/gpu_metrics").c_str(), O_RDONLY | O_CLOEXEC);
+    b.busy_fd = open((g.pci_sysfs + "/" + bdf + "/gpu_busy_percent").c_str(), O_RDONLY | O_CLOEXEC);
+    if (b.metrics_fd >= 0) {  // metrics_table_header: u16 size, u8 format, u8 content revision
+      uint8_t hdr[4] = {0, 0, 0, 0};
+      const ssize_t n = pread(b.metrics_fd, hdr, 4, 0);
+      const unsigned size = hdr[0] | (unsigned)hdr[1] << 8;
+      b.acc = n == 4 && hdr[2] == 1 && (hdr[3] == 7 || hdr[3] == 8) && size >= 80;
+    }
+    if (g.verbose)
+      std::fprintf(stderr, "[mislo-rocprof] GPU %s: activity %s\n", bdf,
+                   b.acc ? "gpu_metrics accumulator" : b.busy_fd >= 0 ? "gpu_busy_percent" : "unreadable");
+    g.busy[a->id.handle] = b;
   }
   return ROCPROFILER_STATUS_SUCCESS;
 }
@@ -339,6 +450,13 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     bool known = true;
     {
       std::lock_guard<std::mutex> lk(g.mu);
+      // this process's kernel time on the device (union: dispatches complete in order per queue)
+      auto bi = g.busy.find(d->dispatch_info.agent_id.handle);
+      if (bi != g.busy.end() && d->end_timestamp > bi->second.own_last_end) {
+        const uint64_t from = d->start_timestamp > bi->second.own_last_end ? d->start_timestamp : bi->second.own_last_end;
+        bi->second.own_ns += d->end_timestamp - from;
+        bi->second.own_last_end = d->end_timestamp;
+      }
       if (g.disp_end.size() > 65536) g.disp_end.clear();  // ends whose successor never completed
       g.disp_end[d->dispatch_info.dispatch_id] = d->end_timestamp;
       if (enq.pred) {
@@ -420,11 +538,14 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.svc = (uint16_t)env_u64("MISLO_SVC_ID", 0);
   g.hbm_bytes = env_u64("MISLO_HBM_BYTES", 288ull << 30);
   g.max_eps = env_u64("MISLO_MAX_EPS", 200000);
-  g.queue_floor_ns = env_u64("MISLO_QUEUE_FLOOR_NS", 100000);
+  g.queue_floor_ns = env_u64("MISLO_QUEUE_FLOOR_NS", 10000000);
   g.xgmi_bytes_per_ns = (double)env_u64("MISLO_XGMI_GBPS", 64);  // GB/s == bytes/ns
   g.verbose = env_u64("MISLO_ROCPROF_VERBOSE", 0) != 0;
   if (const char* ps = std::getenv("MISLO_PCI_SYSFS")) g.pci_sysfs = ps;
   g.hbm_sample_ms = env_u64("MISLO_HBM_SAMPLE_MS", 1000);
+  g.foreign_ms = env_u64("MISLO_FOREIGN_MS", 100);
+  g.foreign_floor_pct = env_u64("MISLO_FOREIGN_FLOOR_PCT", 10);
+  g.foreign_min_own_pct = env_u64("MISLO_FOREIGN_MIN_OWN_PCT", 1);
   rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, agents_cb, sizeof(rocprofiler_agent_v0_t),
                                      nullptr);
   timespec rt{};
@@ -458,7 +579,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   CHECK(rocprofiler_context_is_valid(g.ctx, &valid));
   if (!ok || !valid) return -1;
   CHECK(rocprofiler_start_context(g.ctx));
-  if (g.hbm_sample_ms) g.sampler = std::thread(sampler_main);
+  if (g.hbm_sample_ms || g.foreign_ms) g.sampler = std::thread(sampler_main);
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] started (ring=%s attached=%d)\n", name ? name : "/mislo-agent-events",
                  g.ring != nullptr);
@@ -490,6 +611,19 @@ uint64_t mislo_rocprof_dropped() { return g.dropped.load(); }
 
 // The calling thread's current request trace (0 = none): kernels it enqueues from now on carry it.
 void mislo_rocprof_set_trace(uint64_t trace_h) { t_trace = trace_h; }
+
+// The last foreign-time interval of the GPU agent with the given index: device activity and this
+// process's own kernel share (percent); returns the intervals measured so far (-1: no such GPU).
+int64_t mislo_rocprof_foreign(int gpu_index, double* dev_pct, double* own_pct) {
+  int i = 0;
+  for (auto& kv : g.busy) {
+    if (i++ != gpu_index) continue;
+    *dev_pct = kv.second.dev_pct;
+    *own_pct = kv.second.own_pct;
+    return (int64_t)kv.second.intervals;
+  }
+  return -1;
+}
 
 // Node-wide HBM pressure (milli-pct) of the GPU agent with the given index among the GPUs
 // (-1 if its sysfs counters are unreadable), for tests and the agent's checks.

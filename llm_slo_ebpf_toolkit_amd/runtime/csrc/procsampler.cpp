@@ -1,0 +1,331 @@
+// Native unprivileged CPU / memory sampler (procsampler.h). collector/procfs.py SchedstatSampler is
+// the Python model of this file, record for record.
+#include "procsampler.h"
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+namespace mislo {
+
+namespace {
+
+// Whole small file into `out` (procfs / cgroupfs files are a page at most). False if unreadable.
+bool read_small(const std::string& path, std::string* out) {
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  char buf[4096];
+  out->clear();
+  for (;;) {
+    const ssize_t n = ::read(fd, buf, sizeof(buf));
+    if (n < 0) {
+      ::close(fd);
+      return false;
+    }
+    if (n == 0) break;
+    out->append(buf, (size_t)n);
+    if (out->size() > (1u << 16)) break;
+  }
+  ::close(fd);
+  return true;
+}
+
+bool readable(const std::string& path) { return ::access(path.c_str(), R_OK) == 0; }
+
+std::string parent(const std::string& d) {
+  const size_t k = d.find_last_of('/');
+  return k == std::string::npos || k == 0 ? std::string("/") : d.substr(0, k);
+}
+
+std::string join(const std::string& a, const std::string& b) {
+  std::string r = a;
+  while (!r.empty() && r.back() == '/') r.pop_back();
+  size_t i = 0;
+  while (i < b.size() && b[i] == '/') ++i;
+  if (i == b.size()) return r.empty() ? std::string("/") : r;
+  return r + "/" + b.substr(i);
+}
+
+// "name value" line of a flat-keyed file (cpu.stat)
+bool keyed_u64(const std::string& text, const char* key, uint64_t* v) {
+  const size_t kl = std::strlen(key);
+  size_t pos = 0;
+  while (pos < text.size()) {
+    size_t e = text.find('\n', pos);
+    if (e == std::string::npos) e = text.size();
+    if (e - pos > kl && text.compare(pos, kl, key) == 0 && text[pos + kl] == ' ') {
+      *v = std::strtoull(text.c_str() + pos + kl + 1, nullptr, 10);
+      return true;
+    }
+    pos = e + 1;
+  }
+  return false;
+}
+
+// PSI "some ... total=<us>"
+bool psi_some_us(const std::string& text, uint64_t* v) {
+  if (text.compare(0, 4, "some") != 0) return false;
+  const size_t e = text.find('\n');
+  const size_t t = text.rfind("total=", e == std::string::npos ? text.size() : e);
+  if (t == std::string::npos) return false;
+  *v = std::strtoull(text.c_str() + t + 6, nullptr, 10);
+  return true;
+}
+
+uint32_t ns_pid_of(const std::string& proc_root, uint32_t pid) {
+  std::string s;
+  if (!read_small(join(proc_root, std::to_string(pid) + "/status"), &s)) return pid;
+  const size_t k = s.find("\nNSpid:");
+  if (k == std::string::npos) return pid;
+  size_t e = s.find('\n', k + 1);
+  if (e == std::string::npos) e = s.size();
+  // last whitespace-separated field of the line
+  size_t end = e;
+  while (end > k && (s[end - 1] == ' ' || s[end - 1] == '\t')) --end;
+  size_t beg = end;
+  while (beg > k && s[beg - 1] != ' ' && s[beg - 1] != '\t' && s[beg - 1] != ':') --beg;
+  if (beg >= end) return pid;
+  return (uint32_t)std::strtoul(s.c_str() + beg, nullptr, 10);
+}
+
+}  // namespace
+
+ProcSampler::ProcSampler(Ring* ring, ProcSamplerConfig cfg) : ring_(ring), cfg_(std::move(cfg)) {}
+
+ProcSampler::~ProcSampler() { stop(); }
+
+void ProcSampler::set_targets(const std::vector<std::pair<uint32_t, uint32_t>>& pid_pod) {
+  std::lock_guard<std::mutex> lk(mu_);
+  targets_ = pid_pod;
+}
+
+// The process's cgroup files: the quota group's cpu.stat (nearest ancestor with a CFS quota),
+// memory.pressure of its group (else the node's), cpu.pressure of its group (opt-in).
+void ProcSampler::resolve(uint32_t pid, Proc& p) {
+  p.resolved = true;
+  p.ns_pid = ns_pid_of(cfg_.proc_root, pid);
+  std::string cg;
+  if (!read_small(join(cfg_.proc_root, std::to_string(pid) + "/cgroup"), &cg)) return;
+  const std::string root = cfg_.cgroup_root;
+  size_t pos = 0;
+  while (pos < cg.size()) {
+    size_t e = cg.find('\n', pos);
+    if (e == std::string::npos) e = cg.size();
+    const std::string ln = cg.substr(pos, e - pos);
+    pos = e + 1;
+    const size_t c1 = ln.find(':');
+    const size_t c2 = c1 == std::string::npos ? std::string::npos : ln.find(':', c1 + 1);
+    if (c2 == std::string::npos) continue;
+    const std::string ctrls = ln.substr(c1 + 1, c2 - c1 - 1), path = ln.substr(c2 + 1);
+    if (ln.compare(0, c1, "0") == 0 && ctrls.empty()) {  // cgroup v2
+      const std::string base = join(root, path);
+      for (std::string d = base;; d = parent(d)) {
+        std::string mx;
+        if (read_small(join(d, "cpu.max"), &mx) && mx.compare(0, 3, "max") != 0 && !mx.empty()) {
+          p.cfs_file = join(d, "cpu.stat");
+          break;
+        }
+        if (d.size() <= root.size() || d == "/") break;
+      }
+      if (readable(join(base, "memory.pressure"))) p.mem_file = join(base, "memory.pressure");
+      if (cfg_.cgroup_cpu_psi && readable(join(base, "cpu.pressure"))) p.cpu_psi_file = join(base, "cpu.pressure");
+    } else if (p.cfs_file.empty()) {  // cgroup v1: the hierarchy holding the cpu controller
+      bool cpu = false;
+      for (size_t a = 0; a <= ctrls.size();) {
+        size_t b = ctrls.find(',', a);
+        if (b == std::string::npos) b = ctrls.size();
+        if (ctrls.compare(a, b - a, "cpu") == 0) cpu = true;
+        a = b + 1;
+      }
+      if (!cpu) continue;
+      const std::string mnt = join(root, ctrls);
+      for (std::string d = join(mnt, path);; d = parent(d)) {
+        std::string q;
+        if (read_small(join(d, "cpu.cfs_quota_us"), &q) && std::strtoll(q.c_str(), nullptr, 10) > 0) {
+          p.cfs_file = join(d, "cpu.stat");
+          break;
+        }
+        if (d.size() <= mnt.size() || d == "/") break;
+      }
+    }
+  }
+  if (p.mem_file.empty() && readable(join(cfg_.proc_root, "pressure/memory")))
+    p.mem_file = join(cfg_.proc_root, "pressure/memory");
+}
+
+// This tick's growth of a group counter in ns: 0 on its first reading (it only primes) and when
+// unreadable; read once per tick however many targets share the group.
+uint64_t ProcSampler::group_delta(const std::string& file, int kind) {
+  Group& g = groups_[file];
+  if (g.seen) return g.delta;
+  g.seen = true;
+  g.delta = 0;
+  std::string s;
+  uint64_t v = 0, us = 0;
+  bool got = false;
+  if (read_small(file, &s)) {
+    if (kind == 0) {
+      if (keyed_u64(s, "throttled_usec", &us)) {
+        v = us * 1000, got = true;
+      } else if (keyed_u64(s, "throttled_time", &v)) {  // cgroup v1: ns
+        got = true;
+      }
+    } else if (psi_some_us(s, &us)) {
+      v = us * 1000, got = true;
+    }
+  }
+  if (!got) return 0;
+  if (g.have && v >= g.last) g.delta = v - g.last;
+  g.have = true;
+  g.last = v;
+  return g.delta;
+}
+
+std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<EventRec> out;
+  std::lock_guard<std::mutex> lk(mu_);
+  const uint32_t mask = mask_.load(std::memory_order_relaxed);
+  const uint64_t dt = prev_mono_ && mono_ns > prev_mono_ ? mono_ns - prev_mono_ : 0;
+  prev_mono_ = mono_ns;
+  for (auto& kv : groups_) kv.second.seen = false;
+  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> next;
+  std::map<uint32_t, Proc> live;
+  uint64_t cfs_groups = 0;
+  auto rec = [&](uint16_t type, uint32_t ns_pid, uint32_t pid, uint32_t pod, uint64_t value) {
+    EventRec e{};
+    e.ts_ns = wall_ns;
+    e.value = value;
+    e.pid = ns_pid;
+    e.tid = pid;
+    e.pod_id = pod;
+    e.node_id = (uint16_t)cfg_.node_id;
+    e.signal_type = type;
+    out.push_back(e);
+  };
+  for (const auto& tp : targets_) {
+    const uint32_t pid = tp.first, pod = tp.second;
+    const std::string task = join(cfg_.proc_root, std::to_string(pid) + "/task");
+    DIR* dir = ::opendir(task.c_str());
+    if (!dir) continue;
+    std::vector<uint32_t> tids;
+    while (dirent* de = ::readdir(dir)) {
+      const char* n = de->d_name;
+      if (*n < '0' || *n > '9') continue;
+      tids.push_back((uint32_t)std::strtoul(n, nullptr, 10));
+    }
+    ::closedir(dir);
+    std::sort(tids.begin(), tids.end());
+    uint64_t w_sum = 0, s_sum = 0, w_all = 0;
+    for (uint32_t tid : tids) {
+      std::string s;
+      if (!read_small(join(task, std::to_string(tid) + "/schedstat"), &s)) continue;
+      char* p = nullptr;
+      std::strtoull(s.c_str(), &p, 10);
+      const uint64_t wait = std::strtoull(p, &p, 10), slices = std::strtoull(p, &p, 10);
+      const auto key = std::make_pair(pid, tid);
+      next[key] = {wait, slices};
+      auto it = prev_.find(key);
+      if (it == prev_.end()) continue;
+      const uint64_t dw = wait >= it->second.first ? wait - it->second.first : 0;
+      const uint64_t ds = slices >= it->second.second ? slices - it->second.second : 0;
+      w_all += dw;
+      if (ds > 0 && dw >= cfg_.runq_floor_ns * ds) {  // this thread's waits reach the probe's floor
+        w_sum += dw;
+        s_sum += ds;
+      }
+    }
+    auto pit = procs_.find(pid);
+    Proc pr = pit != procs_.end() ? pit->second : Proc{};
+    if (!pr.resolved) resolve(pid, pr);
+    live[pid] = pr;
+    if ((mask >> kSigRunq & 1) && s_sum && w_sum / s_sum >= cfg_.runq_floor_ns)
+      rec(kSigRunq, pr.ns_pid, pid, pod, w_sum / s_sum);
+    const uint64_t psi_d = pr.cpu_psi_file.empty() ? 0 : group_delta(pr.cpu_psi_file, 1);  // read every tick
+    if ((mask >> kSigSteal & 1) && dt) {
+      uint64_t milli = (uint64_t)((double)w_all * 100000.0 / (double)dt);  // milli-percent of one CPU
+      const uint64_t m2 = (uint64_t)((double)psi_d * 100000.0 / (double)dt);
+      if (m2 > milli) milli = m2;
+      if (milli >= cfg_.steal_floor_milli) rec(kSigSteal, pr.ns_pid, pid, pod, milli);
+    }
+    if (!pr.cfs_file.empty()) {
+      ++cfs_groups;
+      const uint64_t d = group_delta(pr.cfs_file, 0);
+      if ((mask >> kSigCfs & 1) && d >= cfg_.cfs_floor_ns) rec(kSigCfs, pr.ns_pid, pid, pod, d);
+    }
+    if (!pr.mem_file.empty()) {
+      const uint64_t d = group_delta(pr.mem_file, 1);
+      if ((mask >> kSigMem & 1) && d >= cfg_.mem_floor_ns) rec(kSigMem, pr.ns_pid, pid, pod, d);
+    }
+  }
+  prev_.swap(next);
+  procs_.swap(live);
+  for (auto it = groups_.begin(); it != groups_.end();) it = it->second.seen ? std::next(it) : groups_.erase(it);
+  uint64_t pushed = 0;
+  if (ring_ && !out.empty()) {
+    const uint32_t rs = ring_->rec_size();
+    std::vector<uint8_t> buf(out.size() * rs);
+    size_t n = 0;
+    for (const EventRec& e : out)
+      if (pack_user(e, rs, buf.data() + n * rs)) ++n;
+    pushed = n ? ring_->push_batch(buf.data(), n) : 0;
+  }
+  ++st_.ticks;
+  st_.targets = targets_.size();
+  st_.cfs_groups = cfs_groups;
+  if (ring_) {
+    st_.emitted += pushed;
+    st_.dropped += out.size() - pushed;
+  } else {
+    st_.emitted += out.size();
+  }
+  for (const EventRec& e : out)
+    ++st_.by_type[e.signal_type == kSigRunq ? 0 : e.signal_type == kSigSteal ? 1 : e.signal_type == kSigMem ? 2 : 3];
+  const uint64_t took = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now() - t0).count();
+  st_.last_tick_ns = took;
+  if (took > st_.max_tick_ns) st_.max_tick_ns = took;
+  return out;
+}
+
+void ProcSampler::start(uint64_t interval_ns) {
+  stop();
+  {
+    std::lock_guard<std::mutex> lk(tmu_);
+    stop_ = false;
+  }
+  thr_ = std::thread([this, interval_ns] {
+    std::unique_lock<std::mutex> lk(tmu_);
+    while (!cv_.wait_for(lk, std::chrono::nanoseconds(interval_ns), [this] { return stop_; })) {
+      if (paused_.load(std::memory_order_relaxed)) continue;
+      lk.unlock();
+      timespec rt{}, mo{};
+      clock_gettime(CLOCK_REALTIME, &rt);
+      clock_gettime(CLOCK_MONOTONIC, &mo);
+      tick((int64_t)rt.tv_sec * 1000000000ll + rt.tv_nsec, (uint64_t)mo.tv_sec * 1000000000ull + (uint64_t)mo.tv_nsec);
+      lk.lock();
+    }
+  });
+}
+
+void ProcSampler::stop() {
+  {
+    std::lock_guard<std::mutex> lk(tmu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (thr_.joinable()) thr_.join();
+}
+
+ProcSamplerStats ProcSampler::stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return st_;
+}
+
+}  // namespace mislo

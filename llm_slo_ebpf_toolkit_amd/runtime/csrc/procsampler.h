@@ -1,0 +1,113 @@
+// Native unprivileged CPU / memory signal sampler: the agent's kernel-signal producer where BPF is
+// not allowed (collector/procfs.py is the Python model of exactly this code and the oracle of its
+// tests). A thread of the agent reads, every interval, for each watched process:
+//
+//   /proc/<pid>/task/<tid>/schedstat   on-CPU ns, run-queue wait ns, timeslices of each thread
+//   <cgroup>/cpu.stat                  throttled_usec (v2) / throttled_time (v1) of the nearest
+//                                      ancestor group with a CPU quota (CFS bandwidth throttling)
+//   <cgroup>/memory.pressure           PSI "some" total (v2; else the node's /proc/pressure/memory)
+//   <cgroup>/cpu.pressure              PSI "some" total (opt-in: only meaningful for a pod-private group)
+//
+// and pushes records straight into the agent's user-space ring in its record size (USER24 /
+// USER32 / EVENT), stamped with the process's pid in its own pid namespace and its pod id:
+//
+//   type 3  runqueue_delay_ms  mean run-queue wait per timeslice over the threads whose mean
+//                              reached the floor (runqueue_delay.bpf.c: per-wakeup waits >= 100 us)
+//   type 6  cpu_steal_pct      CPU time the process was runnable but not running over the
+//                              interval, in percent of one CPU (sum over its threads of the
+//                              run-queue wait / interval): the process's view of stolen CPU. Under
+//                              EEVDF a starved thread waits a short time per wakeup but most of the
+//                              interval in total, so this fires where the per-wakeup mean does not
+//   type 7  mem_reclaim_latency_ms  PSI memory stall of the process's group over the interval
+//   type 12 cfs_throttled_ms   CFS bandwidth throttling of the process's quota group over the interval
+//
+// Each signal has an emit floor (the BPF probes' in-kernel filters); the overhead guard sheds by
+// clearing a signal's bit in the mask or pausing the sampler (agent/daemon.py _guard_tick).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "records.h"
+#include "ring.h"
+
+namespace mislo {
+
+struct ProcSamplerConfig {
+  std::string proc_root = "/proc";
+  std::string cgroup_root = "/sys/fs/cgroup";
+  uint32_t node_id = 0;
+  uint64_t runq_floor_ns = 100000;    // runqueue_delay.bpf.c emit floor (100 us per timeslice)
+  uint64_t steal_floor_milli = 1000;  // 1 % of one CPU over the interval
+  uint64_t cfs_floor_ns = 100000;
+  uint64_t mem_floor_ns = 100000;
+  bool cgroup_cpu_psi = false;        // cpu_steal_pct = max(wait share, the group's cpu.pressure share)
+};
+
+constexpr uint16_t kSigRunq = 3, kSigSteal = 6, kSigMem = 7, kSigCfs = 12;
+constexpr uint32_t kProcAllSignals = (1u << kSigRunq) | (1u << kSigSteal) | (1u << kSigMem) | (1u << kSigCfs);
+
+struct ProcSamplerStats {
+  uint64_t ticks = 0, emitted = 0, dropped = 0, targets = 0, last_tick_ns = 0, max_tick_ns = 0;
+  uint64_t by_type[4] = {0, 0, 0, 0};  // runq, steal, mem, cfs
+  uint64_t cfs_groups = 0;             // quota groups found for the targets (0: throttling unobservable)
+};
+
+class ProcSampler {
+ public:
+  // `ring` may be null (tick() then only returns the records); it must outlive the sampler.
+  ProcSampler(Ring* ring, ProcSamplerConfig cfg);
+  ~ProcSampler();
+  ProcSampler(const ProcSampler&) = delete;
+  ProcSampler& operator=(const ProcSampler&) = delete;
+
+  void set_targets(const std::vector<std::pair<uint32_t, uint32_t>>& pid_pod);
+  // One interval at (realtime ns, monotonic ns): the records it produced (pushed when a ring is set).
+  std::vector<EventRec> tick(int64_t wall_ns, uint64_t mono_ns);
+  void start(uint64_t interval_ns);
+  void stop();
+  void set_mask(uint32_t mask) { mask_.store(mask, std::memory_order_relaxed); }
+  uint32_t mask() const { return mask_.load(std::memory_order_relaxed); }
+  void set_paused(bool p) { paused_.store(p, std::memory_order_relaxed); }
+  bool paused() const { return paused_.load(std::memory_order_relaxed); }
+  ProcSamplerStats stats();
+  ProcSamplerConfig& config() { return cfg_; }
+
+ private:
+  struct Group {  // a cgroup file's last reading
+    uint64_t last = 0, delta = 0;
+    bool have = false, seen = false;
+  };
+  struct Proc {
+    uint32_t ns_pid = 0;
+    bool resolved = false;
+    std::string cfs_file, mem_file, cpu_psi_file;  // empty: none
+  };
+  void resolve(uint32_t pid, Proc& p);
+  uint64_t group_delta(const std::string& file, int kind);  // kind 0: cpu.stat throttle ns, 1: PSI some ns
+
+  Ring* ring_;
+  ProcSamplerConfig cfg_;
+  std::mutex mu_;  // targets_, state, stats
+  std::vector<std::pair<uint32_t, uint32_t>> targets_;
+  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> prev_;  // (pid, tid) -> (wait, slices)
+  std::map<uint32_t, Proc> procs_;
+  std::map<std::string, Group> groups_;
+  uint64_t prev_mono_ = 0;
+  ProcSamplerStats st_;
+  std::atomic<uint32_t> mask_{kProcAllSignals};
+  std::atomic<bool> paused_{false};
+  std::thread thr_;
+  std::mutex tmu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+}  // namespace mislo

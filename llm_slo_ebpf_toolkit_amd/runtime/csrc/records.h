@@ -91,6 +91,69 @@ inline uint32_t milli_int(uint64_t v, int d) {
   return q > kLim ? (uint32_t)kLim : (uint32_t)q;
 }
 
+// records.py milli_shift_table / mislo_record.h mislo_milli_shift: value_milli = raw * 10^d
+inline int milli_shift(uint16_t type) {
+  switch (type) {
+    case 1: case 3: case 4: case 5: case 7: case 8: case 9: case 12: case 13: case 16:
+      return -3;  // ns -> ms
+    case 6: case 14: case 15:
+      return 0;   // milli-percent -> percent, ns -> us
+    default:
+      return 3;   // counts
+  }
+}
+
+struct User32Rec {  // records.py USER32
+  int64_t ts_ns;
+  uint64_t trace_h;
+  uint32_t value_milli, pod_id, pid;
+  uint8_t signal_type, flags;
+  uint16_t node_id;
+};
+static_assert(sizeof(User32Rec) == 32, "USER32 is 32 bytes");
+
+struct User24Rec {  // records.py USER24
+  uint64_t trace_h;
+  uint32_t value_milli, ts_lo;
+  uint32_t pid_sig;  // pid | signal_type << 22 | ts_zero << 29 | has_gpu << 30
+  uint32_t pod_ts;   // pod_id | (ts bits 32..43) << 20
+};
+static_assert(sizeof(User24Rec) == 24, "USER24 is 24 bytes");
+
+// records.py to_user: an EVENT as a user-space producer writes it into a `rec`-byte ring (64, 32
+// or 24 bytes at `out`). False when the record does not fit USER24 (pid >= 2^22, pod >= 2^20).
+inline bool pack_user(const EventRec& e, uint32_t rec, void* out) {
+  const uint32_t vm = milli_int(e.value, milli_shift(e.signal_type));
+  const uint32_t gpu = (e.flags >> 8) & 1u;
+  if (rec == 64) {
+    *static_cast<EventRec*>(out) = e;
+    return true;
+  }
+  if (rec == 32) {
+    User32Rec u{};
+    u.ts_ns = e.ts_ns;
+    u.trace_h = e.trace_h;
+    u.value_milli = vm;
+    u.pod_id = e.pod_id;
+    u.pid = e.pid;
+    u.signal_type = (uint8_t)e.signal_type;
+    u.flags = (uint8_t)gpu;
+    u.node_id = e.node_id;
+    *static_cast<User32Rec*>(out) = u;
+    return true;
+  }
+  if (rec != 24 || e.pid >= (1u << 22) || e.pod_id >= (1u << 20) || e.signal_type >= 128) return false;
+  const uint64_t t = (uint64_t)e.ts_ns;
+  User24Rec u{};
+  u.trace_h = e.trace_h;
+  u.value_milli = vm;
+  u.ts_lo = (uint32_t)t;
+  u.pid_sig = e.pid | ((uint32_t)e.signal_type << 22) | (e.ts_ns == 0 ? 1u << 29 : 0u) | (gpu << 30);
+  u.pod_ts = e.pod_id | (uint32_t)(((t >> 32) & 0xFFFull) << 20);
+  *static_cast<User24Rec*>(out) = u;
+  return true;
+}
+
 // EpochClock.stamp (records.py) / mislo_submit: offset of ts from the epoch base
 inline uint32_t epoch_offset(int64_t ts, uint64_t base) {
   if (ts == 0) return kTsZero;

@@ -39,6 +39,7 @@ Ring* Ring::format(void* mem, uint64_t capacity, uint32_t rec_size) {
   h->high_water.store(0, std::memory_order_relaxed);
   h->batches.store(0, std::memory_order_relaxed);
   h->stolen.store(0, std::memory_order_relaxed);
+  h->drop_mask.store(0, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   h->magic = kRingMagic;
   return attach(mem);
@@ -213,5 +214,11 @@ uint32_t mislo_ring_rec_size(void* ring) { return reinterpret_cast<ShmRing*>(rin
 
 uint64_t mislo_ring_dropped(void* ring) {
   return reinterpret_cast<ShmRing*>(ring)->ring->header()->dropped.load(std::memory_order_relaxed);
+}
+uint32_t mislo_ring_drop_mask(void* ring) {
+  return reinterpret_cast<ShmRing*>(ring)->ring->header()->drop_mask.load(std::memory_order_relaxed);
+}
+void mislo_ring_set_drop_mask(void* ring, uint32_t mask) {
+  reinterpret_cast<ShmRing*>(ring)->ring->header()->drop_mask.store(mask, std::memory_order_relaxed);
 }
 }

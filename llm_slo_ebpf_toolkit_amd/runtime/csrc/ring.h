@@ -35,6 +35,10 @@ struct alignas(64) RingHeader {
   std::atomic<uint64_t> high_water;
   std::atomic<uint64_t> batches;
   std::atomic<uint64_t> stolen;  // locks taken over from dead producers
+  // Shedding control (agent -> producers): bit t set = producers stop emitting signal type t
+  // (t < 32). The agent's overhead guard sets it before it detaches probes; producers that
+  // attach (the rocprofiler tool inside workloads) read it per record.
+  alignas(64) std::atomic<uint32_t> drop_mask;
 };
 
 constexpr uint64_t kRingMagic = 0x4d49534c4f52494eull;  // "MISLORIN"
@@ -89,4 +93,7 @@ uint32_t mislo_ring_rec_size(void* ring);  // 64 (EVENT) or 32 (USER32)
 // The mislo::Ring* behind a handle from mislo_ring_create_shm / mislo_ring_open_shm.
 void* mislo_ring_handle_ring(void* ring);
 uint64_t mislo_ring_dropped(void* ring);
+// The ring's shedding mask (bit t: drop signal type t) -- read by producers, set by the agent.
+uint32_t mislo_ring_drop_mask(void* ring);
+void mislo_ring_set_drop_mask(void* ring, uint32_t mask);
 }

@@ -19,6 +19,7 @@
 #include "bpfring.h"
 #include "bpfsys.h"
 #include "probesim.h"
+#include "procsampler.h"
 #include "replay.h"
 #include "ring.h"
 #include "tables.h"
@@ -118,6 +119,8 @@ class HostRing {
   uint64_t head() const { return ring_->header()->head.load(std::memory_order_acquire); }
   uint64_t tail() const { return ring_->header()->tail.load(std::memory_order_acquire); }
   uintptr_t address() const { return reinterpret_cast<uintptr_t>(ring_->records()); }
+  uint32_t drop_mask() const { return ring_->header()->drop_mask.load(std::memory_order_relaxed); }
+  void set_drop_mask(uint32_t m) { ring_->header()->drop_mask.store(m, std::memory_order_relaxed); }
 
   py::array records_view() {
     return py::array(py::dtype("uint8"), {(py::ssize_t)(ring_->capacity() * ring_->rec_size())}, {(py::ssize_t)1},
@@ -437,6 +440,69 @@ class PyAssembler {
   WindowAssembler a_;
 };
 
+// procsampler.h: the agent's native schedstat / cgroup / PSI sampler thread, pushing into a user ring.
+class PyProcSampler {
+ public:
+  PyProcSampler(HostRing* ring, uint32_t node_id, const std::string& proc_root, const std::string& cgroup_root,
+                bool cgroup_cpu_psi, uint64_t runq_floor_ns, uint64_t steal_floor_milli, uint64_t cfs_floor_ns,
+                uint64_t mem_floor_ns) {
+    ProcSamplerConfig c;
+    c.node_id = node_id;
+    c.proc_root = proc_root;
+    c.cgroup_root = cgroup_root;
+    c.cgroup_cpu_psi = cgroup_cpu_psi;
+    c.runq_floor_ns = runq_floor_ns;
+    c.steal_floor_milli = steal_floor_milli;
+    c.cfs_floor_ns = cfs_floor_ns;
+    c.mem_floor_ns = mem_floor_ns;
+    s_ = std::make_unique<ProcSampler>(ring ? ring->ring() : nullptr, c);
+  }
+  void set_targets(const std::map<uint32_t, uint32_t>& pid_pod) {
+    std::vector<std::pair<uint32_t, uint32_t>> v(pid_pod.begin(), pid_pod.end());
+    s_->set_targets(v);
+  }
+  void set_target_list(const std::vector<std::pair<uint32_t, uint32_t>>& v) { s_->set_targets(v); }
+  py::bytes tick(int64_t wall_ns, uint64_t mono_ns) {
+    std::vector<EventRec> r;
+    {
+      py::gil_scoped_release nogil;
+      r = s_->tick(wall_ns, mono_ns);
+    }
+    return py::bytes(reinterpret_cast<const char*>(r.data()), r.size() * sizeof(EventRec));
+  }
+  void start(double interval_s) {
+    if (!(interval_s > 0)) throw std::invalid_argument("interval must be > 0");
+    s_->start((uint64_t)(interval_s * 1e9));
+  }
+  void stop() {
+    py::gil_scoped_release nogil;
+    s_->stop();
+  }
+  uint32_t mask() const { return s_->mask(); }
+  void set_mask(uint32_t m) { s_->set_mask(m); }
+  bool paused() const { return s_->paused(); }
+  void set_paused(bool p) { s_->set_paused(p); }
+  py::dict stats() {
+    ProcSamplerStats st = s_->stats();
+    py::dict d;
+    d["ticks"] = st.ticks;
+    d["emitted"] = st.emitted;
+    d["dropped"] = st.dropped;
+    d["targets"] = st.targets;
+    d["last_tick_ns"] = st.last_tick_ns;
+    d["max_tick_ns"] = st.max_tick_ns;
+    d["runqueue_delay_ms"] = st.by_type[0];
+    d["cpu_steal_pct"] = st.by_type[1];
+    d["mem_reclaim_latency_ms"] = st.by_type[2];
+    d["cfs_throttled_ms"] = st.by_type[3];
+    d["cfs_groups"] = st.cfs_groups;
+    return d;
+  }
+
+ private:
+  std::unique_ptr<ProcSampler> s_;
+};
+
 class PyBpfMap {
  public:
   explicit PyBpfMap(const std::string& path) {
@@ -537,6 +603,7 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def_property_readonly("capacity", &HostRing::capacity)
       .def_property_readonly("rec_size", &HostRing::rec_size)
       .def_property_readonly("head", &HostRing::head)
+      .def_property("drop_mask", &HostRing::drop_mask, &HostRing::set_drop_mask)
       .def_property_readonly("tail", &HostRing::tail)
       .def_property_readonly("address", &HostRing::address);
   py::class_<PyReplayer>(m, "Replayer")
@@ -608,6 +675,21 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def_property_readonly("layout", &PyAssembler::layout);
   m.def("slot_layout", [](uint32_t g, uint32_t s, uint32_t n, uint32_t r) { return layout_dict(slot_layout(g, s, n, r)); },
         py::arg("group_cap"), py::arg("span_cap"), py::arg("sig_cap"), py::arg("row_cap"));
+  py::class_<PyProcSampler>(m, "ProcSampler")
+      .def(py::init<HostRing*, uint32_t, const std::string&, const std::string&, bool, uint64_t, uint64_t, uint64_t,
+                    uint64_t>(),
+           py::arg("ring"), py::arg("node_id") = 0, py::arg("proc_root") = "/proc",
+           py::arg("cgroup_root") = "/sys/fs/cgroup", py::arg("cgroup_cpu_psi") = false,
+           py::arg("runq_floor_ns") = 100000, py::arg("steal_floor_milli") = 1000, py::arg("cfs_floor_ns") = 100000,
+           py::arg("mem_floor_ns") = 100000, py::keep_alive<1, 2>())
+      .def("set_targets", &PyProcSampler::set_targets)
+      .def("set_target_list", &PyProcSampler::set_target_list)
+      .def("tick", &PyProcSampler::tick, py::arg("wall_ns"), py::arg("mono_ns"))
+      .def("start", &PyProcSampler::start, py::arg("interval_s"))
+      .def("stop", &PyProcSampler::stop)
+      .def("stats", &PyProcSampler::stats)
+      .def_property("mask", &PyProcSampler::mask, &PyProcSampler::set_mask)
+      .def_property("paused", &PyProcSampler::paused, &PyProcSampler::set_paused);
   py::class_<PyBpfMap>(m, "BpfMap")
       .def(py::init<const std::string&>(), py::arg("path"))
       .def("lookup", &PyBpfMap::lookup)

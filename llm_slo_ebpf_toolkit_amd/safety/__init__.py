@@ -186,3 +186,108 @@ class TokenBucket:
                 self._tokens -= n
                 return True
             return False
+
+
+class ShedLadder:
+    """What the agent gives up, one step per over-budget evaluation, cheapest loss first (REF sheds
+    one signal per over-budget tick in cost order, cmd/agent/main.go:587-600 with
+    pkg/safety/overhead_guard.go:77-107 and pkg/signals/constants.go:46-59; REF's only lever is
+    detaching a probe). The window engine's sources have cheaper levers, so the ladder is:
+
+    1. **floors** -- every kernel probe's emit floor (``mislo_cfg`` [2 + type], read per record by
+       the probes and the ring producers) rises to the signal's evidence threshold: the records
+       the attribution never reads as elevated stop leaving the kernel, the elevated ones still
+       arrive. One step for all probe signals.
+    2. **sampler** -- the procfs sampler stops one signal per step (shed order), then pauses.
+    3. **GPU producers** -- the user ring's drop mask stops one GPU signal per step (shed order);
+       the rocprofiler tool inside the workloads reads it per record.
+    4. **probes** -- REF's step: detach the next kernel probe (or, without loaded probes, disable
+       the next signal of the synthetic generator).
+
+    ``step()`` returns a label of what it shed, or None once nothing is left."""
+
+    def __init__(self, order, maps=None, sampler=None, user_ring=None, probe_manager=None, generator=None):
+        from ..signals import catalog
+
+        self.order = [s for s in order if s in catalog.BY_NAME]
+        self.maps, self.sampler, self.user_ring = maps, sampler, user_ring
+        self.probe_manager, self.generator = probe_manager, generator
+        self.floors_raised = False
+        self.shed: list = []
+        self._catalog = catalog
+
+    def _floors(self) -> Optional[str]:
+        if self.floors_raised or self.maps is None:
+            return None
+        raised = []
+        for name in self.order:
+            spec = self._catalog.BY_NAME[name]
+            if spec.gpu or not 0 < spec.kernel_type < 120:
+                continue
+            raw = int(round(spec.elevated / spec.decode_scale))
+            if raw > int(self.maps.cfg_get(2 + spec.kernel_type)):
+                self.maps.set_floor(spec.kernel_type, raw)
+                raised.append(name)
+        self.floors_raised = True
+        return f"floors:{','.join(raised)}" if raised else None
+
+    def _sampler(self) -> Optional[str]:
+        s = self.sampler
+        if s is None or s.paused:
+            return None
+        from ..collector.procfs import SIGNAL_TYPES
+
+        for name in self.order:
+            t = SIGNAL_TYPES.get(name)
+            if t is not None and s.mask >> t & 1:
+                s.mask = s.mask & ~(1 << t)
+                if s.mask == 0:
+                    s.paused = True
+                return f"sampler:{name}"
+        s.paused = True
+        return "sampler:paused"
+
+    def _gpu(self) -> Optional[str]:
+        r = self.user_ring
+        if r is None:
+            return None
+        for name in self.order:
+            spec = self._catalog.BY_NAME[name]
+            if spec.gpu and not int(r.drop_mask) >> spec.kernel_type & 1:
+                r.drop_mask = int(r.drop_mask) | (1 << spec.kernel_type)
+                return f"gpu:{name}"
+        return None
+
+    def _probes(self) -> Optional[str]:
+        pm = self.probe_manager
+        sig = pm.shed_next() if pm is not None else None
+        if sig:
+            if self.generator is not None:
+                self.generator.disable(sig)
+            return f"probe:{sig}"
+        if self.generator is not None:
+            sig = self.generator.disable_highest_cost()
+            if sig:
+                return f"signal:{sig}"
+        return None
+
+    def disabled(self) -> set:
+        """Signals no source emits any more (floors only thin a signal out)."""
+        out = set()
+        for what in self.shed:
+            kind, _, name = what.partition(":")
+            if kind in ("sampler", "gpu", "probe", "signal") and name in self._catalog.BY_NAME:
+                out.add(name)
+        if self.sampler is not None and self.sampler.paused:
+            from ..collector.procfs import SIGNAL_TYPES
+
+            out.update(SIGNAL_TYPES)
+        return out
+
+    def step(self) -> Optional[str]:
+        for stage in (self._floors, self._sampler, self._gpu, self._probes):
+            what = stage()
+            if what:
+                self.shed.append(what)
+                return what
+        return None

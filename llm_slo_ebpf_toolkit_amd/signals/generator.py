@@ -40,6 +40,15 @@ FAULT_OVERRIDES: Dict[str, Dict[str, float]] = {
     # under CPU contention)
     "gpu_contention": {"gpu_queue_delay_ms": 35, "hbm_pressure_pct": 93},
     "rccl_latency": {"rccl_collective_ms": 28, "xgmi_link_latency_us": 60},
+    # NEW: the shapes the same two domains take on a live MI355X node (tools/config3_evidence.py,
+    # tools/config2_evidence.py). A noisy neighbour on a pod WITHOUT a CPU limit (REF's
+    # cpu_throttle profile is CFS quota throttling): under EEVDF each wakeup waits little
+    # (run-queue delay per timeslice stays below REF's 10 ms threshold: 546 of 562 samples in
+    # profiles/r3_config3_*), no quota group throttles, but the process waits for CPU most of the
+    # interval (cpu_steal_pct, the sampler's wait share). Another process's kernels on the GPU
+    # without filling its HBM: foreign GPU time, HBM at its usual level.
+    "cpu_contention": {"runqueue_delay_ms": 6, "cpu_steal_pct": 40},
+    "gpu_compute_contention": {"gpu_queue_delay_ms": 35},
 }
 FAULT_ERRNO = {"provider_throttle": 110, "network_partition": 113}
 

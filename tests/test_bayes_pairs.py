@@ -67,7 +67,7 @@ def test_marginalising_a_signal_drops_its_factor():
     base = NaiveBayes.ref()
     obs = ["dns_latency_ms", "tcp_retransmits_total", "runqueue_delay_ms"]
     slots = {catalog.BY_NAME[s].slot for s in obs}
-    m = marginalize(with_pairs(base, 0.2), obs)
+    m = marginalize(with_pairs(base, 0.2), obs, drop_unobservable=False)
     rng = np.random.default_rng(2)
     for _ in range(20):
         v = rng.uniform(0, 400, 16)
@@ -78,6 +78,22 @@ def test_marginalising_a_signal_drops_its_factor():
         w[[s for s in range(16) if s not in slots]] = 0.0
         np.testing.assert_allclose(m.posteriors(v[None, :]), m.posteriors(w[None, :]), rtol=1e-12)
     assert not m.evidence_mask[[s for s in range(16) if s not in slots]].any()
+
+
+def test_domains_no_observable_signal_indicates_are_not_attributed():
+    """A node whose sources produce only the network signals cannot tell CPU, memory, provider or
+    GPU faults from a healthy service: those domains (and their pairs) are inactive, so a window
+    with nothing elevated is "unknown", not the domain with the largest prior."""
+    base = with_pairs(NaiveBayes.gpu(), 0.2)
+    obs = ["dns_latency_ms", "tcp_retransmits_total", "connect_latency_ms"]
+    m = marginalize(base, obs)
+    active = {catalog.ALL_DOMAINS[d] for d in np.flatnonzero(np.isfinite(m.bias))}
+    assert active == {"network_dns", "network_egress", "provider_throttle", "unknown"}, active
+    assert not np.isfinite(m.pair_b[(m.pairs == catalog.DOMAIN_INDEX["cpu_throttle"]).any(axis=1)]).any()
+    v = np.full((1, 16), np.nan)
+    assert catalog.ALL_DOMAINS[int(m.predict(v)[0])] == "unknown"
+    v[0, catalog.BY_NAME["dns_latency_ms"].slot] = 250.0
+    assert catalog.ALL_DOMAINS[int(m.predict(v)[0])] == "network_dns"
 
 
 def test_single_fault_limit_and_temperature_commute():

@@ -34,12 +34,15 @@ def test_schedstat_sampler_emits_mean_wait_per_slice_above_the_floor(tmp_path):
     write_schedstat(tmp_path, 100, 101, 9_000_000, 1_000_000 + 4 * 50_000, 14)     # 50 us per slice: below
     write_schedstat(tmp_path, 200, 200, 2, 1, 2)                                     # ran, never waited
     ev = s.sample(10**18 + 100_000_000)
-    assert len(ev) == 1  # per process: the wait over the timeslices of its threads above the floor
+    # per process: the wait over the timeslices of its threads above the floor, then the CPU it
+    # waited for over the interval (8.2 ms of 100 ms: 8.2 % of one CPU, in milli-percent)
+    assert len(ev) == 2
     e = ev[0]
     assert (int(e["signal_type"]), int(e["value"]), int(e["pid"]), int(e["tid"]), int(e["pod_id"]),
             int(e["node_id"])) == (procfs.RUNQUEUE_TYPE, 2_000_000, 100, 100, 7, 3)
+    assert (int(ev[1]["signal_type"]), int(ev[1]["value"]), int(ev[1]["pod_id"])) == (procfs.STEAL_TYPE, 8200, 7)
     write_schedstat(tmp_path, 100, 100, 9_500_000, 9_000_000 + 3_000_000, 15)
-    assert s.tick(10**18 + 200_000_000) == 1 and s.emitted == 1 and pushed[0].dtype.itemsize == 24
+    assert s.tick(10**18 + 200_000_000) == 2 and s.emitted == 2 and pushed[0].dtype.itemsize == 24
     # an exited thread is forgotten
     os.remove(tmp_path / "100" / "task" / "101" / "schedstat")
     s.sample()
@@ -60,6 +63,7 @@ def test_sampler_records_carry_the_pid_the_pod_sees(tmp_path):
     for pid in (4242, 500):
         write_schedstat(tmp_path, pid, pid, 2, 1 + 3_000_000, 2)
     ev = s.sample(10**18 + 10**8)
+    ev = ev[ev["signal_type"] == procfs.RUNQUEUE_TYPE]
     got = sorted((int(e["pod_id"]), int(e["pid"]), int(e["tid"])) for e in ev)
     assert got == [(7, 17, 4242), (8, 500, 500)]
     assert procfs.ns_pid(999, str(tmp_path)) == 999  # gone / unreadable: as given
@@ -151,7 +155,8 @@ def test_psi_memory_stall_becomes_reclaim_records(tmp_path):
     node.write_text("some avg10=0.00 avg60=0.00 avg300=0.00 total=1000\nfull avg10=0.00 avg60=0.00 avg300=0.00 total=0\n")
     write_schedstat(tmp_path, 100, 100, 1, 1, 1)
     (tmp_path / "100" / "cgroup").write_text("0::/\n")
-    s = procfs.SchedstatSampler(lambda: {100: 4}, lambda u: len(u), proc_root=str(tmp_path))
+    s = procfs.SchedstatSampler(lambda: {100: 4}, lambda u: len(u), proc_root=str(tmp_path),
+                                cgroup_root=str(tmp_path / "cg"))
     assert procfs.psi_available(str(tmp_path))
     assert len(s.sample()) == 0
     node.write_text("some avg10=1.00 avg60=0.00 avg300=0.00 total=6000\nfull avg10=0.00 avg60=0.00 avg300=0.00 total=0\n")

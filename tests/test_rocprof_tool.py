@@ -263,3 +263,108 @@ def test_queue_delay_excludes_waiting_behind_own_queue():
     # a GEMM that started the moment its predecessor ended waited for nothing: no record at all
     # (r3 box: 5 records for 72 GEMMs + the setup kernels, none above 1 ms)
     assert len(q) >= 1 and q.max() < 5.0, np.sort(q)[-10:]
+
+
+FOREIGN_WORKLOAD = r"""
+import ctypes, sys, time, torch
+tool = [ln.split()[-1] for ln in open("/proc/self/maps") if "libmislo_rocprof" in ln][0]
+lib = ctypes.CDLL(tool)
+lib.mislo_rocprof_foreign.restype = ctypes.c_int64
+lib.mislo_rocprof_foreign.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+torch.cuda.synchronize()
+dev, own = ctypes.c_double(), ctypes.c_double()
+
+def serve(seconds, two_streams):
+    # a service's duty cycle: ~6 ms of GEMMs every 15 ms, on one stream or two concurrent ones
+    end = time.time() + seconds
+    while time.time() < end:
+        if two_streams:
+            with torch.cuda.stream(s1):
+                a = [x @ x for _ in range(24)]
+            with torch.cuda.stream(s2):
+                b = [x @ x for _ in range(24)]
+        else:
+            a = [x @ x for _ in range(48)]
+        torch.cuda.synchronize()
+        n = lib.mislo_rocprof_foreign(0, ctypes.byref(dev), ctypes.byref(own))
+        print("foreign", time.time_ns(), n, round(dev.value, 1), round(own.value, 1), flush=True)
+        time.sleep(0.009)
+
+serve(1.5, False)
+serve(1.5, True)
+print("phase_b", time.time_ns(), flush=True)
+sys.stdin.readline()  # the test has started another process's GEMMs
+print("contended", time.time_ns(), flush=True)
+serve(2.0, False)
+print("done", time.time_ns(), flush=True)
+"""
+
+BURNER = r"""
+import time, torch
+a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+torch.cuda.synchronize()
+print("burning", flush=True)
+end = time.time() + 30
+while time.time() < end:
+    for _ in range(8):
+        a = (a @ a).clamp_(-1, 1)
+    torch.cuda.synchronize()
+"""
+
+
+@pytest.mark.gpu
+def test_foreign_gpu_time_separates_another_process_from_the_services_own_concurrency():
+    """gpu_queue_delay_ms (b): the device's activity accumulator minus the process's own kernel
+    time. Alone -- on one stream or two concurrent ones -- the process sees no foreign time and
+    the tool emits no foreign record; with another process's GEMMs on the GPU every interval
+    shows it and the tool emits records of >= 10 % of the interval."""
+    import threading
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    name = f"/mislo-test-{os.getpid()}-foreign"
+    ring = rt.HostRing(1 << 16, 64, name)
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000000",
+               MISLO_ROCPROF_VERBOSE="1")
+    w = subprocess.Popen([sys.executable, "-u", "-c", FOREIGN_WORKLOAD], env=env, stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    burner = None
+    lines = []
+    try:
+        for ln in w.stdout:
+            lines.append(ln.split())
+            if ln.startswith("phase_b"):
+                burner = subprocess.Popen([sys.executable, "-u", "-c", BURNER], stdout=subprocess.PIPE, text=True)
+                assert burner.stdout.readline().startswith("burning")
+                time.sleep(0.3)
+                w.stdin.write("go\n")
+                w.stdin.flush()
+            if ln.startswith("done"):
+                break
+        w.wait(60)
+    finally:
+        for p in (burner, w):
+            if p is not None and p.poll() is None:
+                p.kill()
+                p.wait(10)
+    err = w.stderr.read()
+    assert w.returncode == 0, err[-2000:]
+    t_b = int(next(x[1] for x in lines if x[0] == "contended"))
+    alone = [(float(x[3]), float(x[4])) for x in lines if x[0] == "foreign" and int(x[1]) < t_b and int(x[2]) > 2]
+    shared = [(float(x[3]), float(x[4])) for x in lines if x[0] == "foreign" and int(x[1]) > t_b + 300_000_000]
+    assert alone and shared, lines[-5:]
+    f_alone = np.median([d - o for d, o in alone])
+    f_shared = np.median([d - o for d, o in shared])
+    recs = np.concatenate([np.frombuffer(ring.records_view()[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
+                           for _, i, c in ring.peek(1 << 16)]) if ring.peek(1 << 16) else np.zeros(0, records.EVENT)
+    q = recs[recs["signal_type"] == 13]
+    big = q[q["value"] >= 10_000_000]  # foreign records: >= 10 % of a 100 ms interval
+    before, after = int((big["ts_ns"] < t_b).sum()), int((big["ts_ns"] > t_b).sum())
+    print({"foreign_alone_median": f_alone, "foreign_shared_median": f_shared, "records_alone": before,
+           "records_shared": after, "alone": alone[:6], "shared": shared[:6]})
+    assert f_alone < 10.0 and before <= 1, (f_alone, before, alone[:10])
+    assert f_shared >= 25.0 and after >= 5, (f_shared, after, shared[:10])

@@ -103,9 +103,10 @@ def wait_http(url: str, proc, timeout: float) -> None:
     raise RuntimeError(f"{url} not ready after {timeout}s")
 
 
-def chat(port: int, i: int, phase: str) -> dict:
-    body = json.dumps({"prompt": f"why did the {phase} request {i} slow down on the gpu", "profile": "chat_short",
-                       "max_tokens": 16, "request_id": f"{phase}-{i}"}).encode()
+def chat(port: int, i: int, phase: str, prompt_words: int = 16) -> dict:
+    words = " ".join(f"token{(i * 7 + k) % 997}" for k in range(max(0, prompt_words - 8)))
+    body = json.dumps({"prompt": f"why did the {phase} request {i} slow down on the gpu {words}".strip(),
+                       "profile": "chat_short", "max_tokens": 16, "request_id": f"{phase}-{i}"}).encode()
     req = urllib.request.Request(f"http://127.0.0.1:{port}/chat", data=body, method="POST",
                                  headers={"Content-Type": "application/json"})
     t = time.time_ns()
@@ -139,14 +140,25 @@ def pct(xs, q):
     return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))] if xs else None
 
 
+MODEL = os.path.join(ROOT, "config", "models", "mislo-learned.safetensors")
+GPU_SIGNALS = ("gpu_queue_delay_ms", "hbm_pressure_pct", "xgmi_link_latency_us", "rccl_collective_ms")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/config2")
-    ap.add_argument("--requests", type=int, default=24, help="requests per phase")
     ap.add_argument("--preset", default="7b", help="Llama preset of the workload (BASELINE config 2: 7B)")
     ap.add_argument("--ttft-slo-ms", type=float, default=800.0, help="the agent's TTFT SLO (BASELINE config 2: 800 ms)")
+    ap.add_argument("--phase-s", type=float, default=24.0, help="seconds of the baseline and fault phases")
+    ap.add_argument("--recover-s", type=float, default=12.0)
+    ap.add_argument("--burners", type=int, default=4, help="GEMM burner processes on the GPU in the fault phase")
+    ap.add_argument("--prompt-words", type=int, default=512, help="prompt length (prefill tokens)")
+    ap.add_argument("--gap-s", type=float, default=0.05, help="client think time between requests")
+    ap.add_argument("--window-ms", type=int, default=1000)
+    ap.add_argument("--model-path", default=MODEL, help="the agent's model ('' = the bayes_gpu expert table)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
+    from config3_evidence import score  # noqa: E402 - tools/ sibling (imports this module at load)
     from llm_slo_ebpf_toolkit_amd.collector import bpf
 
     prefix = f"/mislo-cfg2-{os.getpid()}"
@@ -154,25 +166,29 @@ def main() -> int:
     rings = bpf.create_rings(names, 1 << 24, 1 << 18, 1 << 14)  # noqa: F841 - kept alive for the children
     rx, mport, hport = free_port(), free_port(), free_port()
     attr_path = os.path.join(a.out, "attributions.jsonl")
+    if os.path.exists(attr_path):
+        os.remove(attr_path)
     log = open(os.path.join(a.out, "run.log"), "w")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
+    model_args = ["--model-path", a.model_path, "--model-signals", ",".join(GPU_SIGNALS)] if a.model_path else \
+        ["--model", "bayes_gpu"]
     agent = subprocess.Popen(
         [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "shm",
          "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
-         "--window-ms", "1000", "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
-         "--model", "bayes_gpu", "--min-confidence", "0.3", "--halo-ms", "1500", "--ttft-slo-ms", str(a.ttft_slo_ms),
-         "--output", "jsonl",
-         "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
+         "--window-ms", str(a.window_ms), "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
+         *model_args, "--min-confidence", "0.3", "--halo-ms", "1500", "--ttft-slo-ms", str(a.ttft_slo_ms),
+         "--output", "jsonl", "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
     llm_env = dict(env, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1",
-                   MISLO_QUEUE_FLOOR_NS="200000", OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces",
+                   OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces",
                    POD_UID=POD_UID, POD_NAME="llm-server-config2")
     llm = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.rag_service", "--backend", "llama",
                             "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", ""],
                            cwd=ROOT, env=llm_env, stdout=log, stderr=subprocess.STDOUT)
-    burner = None
+    burners = []
     rows = []
     counters = {}
     onset_ns = None
+    phases = []
     tstop = threading.Event()
     tailer = Tailer(attr_path, tstop)
     try:
@@ -181,30 +197,38 @@ def main() -> int:
         print("[config2] agent and llm ready", flush=True)
         tailer.start()
         for i in range(4):  # warm the model (first-request compilation / allocation)
-            chat(hport, i, "warmup")
-        phases = [("baseline", False), ("fault_gpu_contention", True), ("recovery", False)]
-        for phase, fault in phases:
+            chat(hport, i, "warmup", a.prompt_words)
+        plan = [("baseline", a.phase_s, False), ("fault_gpu_contention", a.phase_s, True),
+                ("recovery", a.recover_s, False)]
+        for phase, dur, fault in plan:
             if fault:
-                burner = subprocess.Popen([sys.executable, "-c", BURNER, "600"], cwd=ROOT, env=env,
-                                          stdout=subprocess.PIPE, stderr=log, text=True)
-                ln = burner.stdout.readline()  # "burner on <ns>" once its first GEMM finished
-                onset_ns = int(ln.split()[-1]) if ln.startswith("burner on") else time.time_ns()
-            t_phase = time.time_ns()
+                burners = [subprocess.Popen([sys.executable, "-c", BURNER, "600"], cwd=ROOT, env=env,
+                                            stdout=subprocess.PIPE, stderr=log, text=True) for _ in range(a.burners)]
+                ons = []
+                for b in burners:
+                    ln = b.stdout.readline()  # "burner on <ns>" once its first GEMM finished
+                    ons.append(int(ln.split()[-1]) if ln.startswith("burner on") else time.time_ns())
+                onset_ns = min(ons)
+            t0 = time.time_ns()
             m0 = scrape(mport)
-            for i in range(a.requests):
-                rows.append(chat(hport, i, phase))
-                time.sleep(0.1)
-            if burner is not None:
-                burner.send_signal(signal.SIGTERM)
-                burner.wait(30)
-                burner = None
+            i = 0
+            while time.time_ns() - t0 < dur * 1e9:
+                rows.append(chat(hport, i, phase, a.prompt_words))
+                i += 1
+                time.sleep(a.gap_s)
+            for b in burners:
+                b.send_signal(signal.SIGTERM)
+                b.wait(30)
+            burners = []
+            t1 = time.time_ns()
+            phases.append((phase, t0, t1))
             rs = [r["ttft_ms"] for r in rows if r["phase"] == phase]
-            print(f"[config2] {phase}: {len(rs)} requests, TTFT p50 {pct(rs, .5):.1f} ms p95 {pct(rs, .95):.1f} ms "
-                  f"(from {t_phase})", flush=True)
-            time.sleep(2.5)  # let the phase's last window close
+            print(f"[config2] {phase}: {len(rs)} requests, TTFT p50 {pct(rs, .5):.1f} ms p95 {pct(rs, .95):.1f} ms",
+                  flush=True)
             counters[phase] = delta(m0, scrape(mport))
+        time.sleep(3 * a.window_ms / 1000.0)  # the last windows' attributions
     finally:
-        for p in (burner, llm):
+        for p in burners + [llm]:
             if p is not None and p.poll() is None:
                 p.send_signal(signal.SIGTERM)
                 try:
@@ -224,47 +248,33 @@ def main() -> int:
     with open(os.path.join(a.out, "ttft.jsonl"), "w") as f:
         for r in rows:
             f.write(json.dumps(r) + "\n")
-    attrs = [json.loads(x) for x in open(attr_path)] if os.path.exists(attr_path) else []
-    mine = [x for x in attrs if x["service"] == "rag-service"]
-
-    def phase_of(ts_iso_ns: int) -> str:
-        best = "other"
-        for r in rows:
-            if r["t_ns"] <= ts_iso_ns:
-                best = r["phase"]
-        return best
-
-    by_phase = {}
-    for x in mine:
-        t = int(x["incident_id"].split("-")[1])
-        p = phase_of(t)
-        d = by_phase.setdefault(p, {"windows": 0, "domains": {}, "evidence": []})
-        d["windows"] += 1
-        d["domains"][x["predicted_fault_domain"]] = d["domains"].get(x["predicted_fault_domain"], 0) + 1
-        if x["predicted_fault_domain"] != "unknown":
-            d["evidence"].append({"domain": x["predicted_fault_domain"], "confidence": round(x["confidence"], 3),
-                                  "evidence": x["evidence"], "burn_rate": x["slo_impact"]["burn_rate"]})
-    # detection delay: fault onset -> arrival of the first gpu_contention attribution of the service
-    det = None
-    if onset_ns is not None:
-        hits = [arr for arr, x in tailer.rows if x.get("service") == "rag-service"
-                and x.get("predicted_fault_domain") == "gpu_contention" and int(x["incident_id"].split("-")[1]) > onset_ns]
-        det = {"onset_ns": onset_ns, "first_attribution_arrival_ns": min(hits) if hits else None,
-               "detection_delay_s": round((min(hits) - onset_ns) / 1e9, 3) if hits else None}
-    summary = {
-        "preset": a.preset, "ttft_slo_ms": a.ttft_slo_ms, "detection": det,
-        "ttft_ms": {p: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
-                    for p in ("baseline", "fault_gpu_contention", "recovery")
-                    for v in [[r["ttft_ms"] for r in rows if r["phase"] == p]]},
-        "attributions_total": len(attrs),
-        "agent_counters_by_phase": counters,
-        "rag_service_by_phase": {p: {"windows": d["windows"], "domains": d["domains"], "evidence": d["evidence"][:3]}
-                                 for p, d in by_phase.items()},
-        "agent_exit": agent.returncode, "llm_exit": llm.returncode,
-    }
+    expect = {"baseline": set(), "fault_gpu_contention": {"gpu_contention"}, "recovery": set()}
+    res = score(phases, tailer.rows, a.window_ms, service="rag-service", expect=expect)
+    fault = res["phases"].get("fault_gpu_contention", {})
+    # detection delay: the burners' first GEMM (fault onset) -> arrival of the service's first
+    # gpu_contention attribution
+    hits = [arr for arr, x in tailer.rows if x.get("service") == "rag-service"
+            and x.get("predicted_fault_domain") == "gpu_contention" and onset_ns is not None
+            and int(x["incident_id"].split("-")[1]) > onset_ns]
+    res["detection"] = {"onset_ns": onset_ns, "first_attribution_arrival_ns": min(hits) if hits else None,
+                        "detection_delay_s": round((min(hits) - onset_ns) / 1e9, 3) if hits else None}
+    res["ttft_ms"] = {p: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95),
+                          "slo_breach_fraction": round(sum(x > a.ttft_slo_ms for x in v) / max(1, len(v)), 4)}
+                      for p, _t0, _t1 in phases for v in [[r["ttft_ms"] for r in rows if r["phase"] == p]]}
+    res["gpu_contention_windows"] = f"{fault.get('top1', {}).get('gpu_contention', 0)}/{fault.get('windows', 0)}"
+    res["evidence_samples"] = [{"domain": x["predicted_fault_domain"], "confidence": round(x["confidence"], 3),
+                                "evidence": x["evidence"]} for _arr, x in tailer.rows
+                               if x.get("service") == "rag-service" and x.get("predicted_fault_domain") != "unknown"][:4]
+    res["agent_counters_by_phase"] = counters
+    res["setup"] = {"preset": a.preset, "ttft_slo_ms": a.ttft_slo_ms, "burners": a.burners,
+                    "prompt_words": a.prompt_words, "phase_s": a.phase_s, "recover_s": a.recover_s,
+                    "model": os.path.relpath(a.model_path, ROOT) if a.model_path else "bayes_gpu",
+                    "observable_signals": list(GPU_SIGNALS) if a.model_path else "all",
+                    "fault": f"{a.burners} processes of back-to-back 8192^3 bf16 GEMMs on the service's GPU"}
+    res["exit"] = {"agent": agent.returncode, "llm": llm.returncode}
     with open(os.path.join(a.out, "summary.json"), "w") as f:
-        json.dump(summary, f, indent=1)
-    print(json.dumps(summary, indent=1), flush=True)
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1), flush=True)
     return 0
 
 

@@ -218,7 +218,9 @@ def main() -> int:
     ap.add_argument("--phase-s", type=float, default=15.0)
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--clients", type=int, default=2)
-    ap.add_argument("--burners-per-cpu", type=int, default=6)
+    ap.add_argument("--burners-per-cpu", type=int, default=2,
+                    help="CPU burners per victim CPU: the service keeps ~1/3 of its CPUs, so requests still "
+                         "complete every window (at 6 only 8 requests completed in 15 s, profiles/r3_config3_fourth)")
     ap.add_argument("--procfs-ms", type=int, default=100,
                     help="schedstat sampling interval: run-queue records join a request's span only within 100 ms "
                          "of its start (REF's pod+pid tier), so they must come faster than that")
@@ -255,13 +257,17 @@ def main() -> int:
                    OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces")
     from llm_slo_ebpf_toolkit_amd.collector import procfs
 
-    observable = list(NET_SIGNALS) + ["runqueue_delay_ms"]
+    # CPU: the sampler's run-queue delay and CPU wait share; CFS throttling only where the
+    # service's cgroup has a CPU quota (the box's has none: a signal that cannot fire is not
+    # evidence, so it is summed out rather than read as "not elevated")
+    observable = list(NET_SIGNALS) + ["runqueue_delay_ms", "cpu_steal_pct"]
+    if procfs.cgroup_files(os.getpid())[0]:
+        observable.append("cfs_throttled_ms")
     if procfs.psi_available():
         observable.append("mem_reclaim_latency_ms")
     gpu_tool = a.backend == "llama" and os.path.exists(TOOL)
     if gpu_tool:  # GPU signals of the RAG service's own kernels (the agent's pod id 1: its first pod)
-        rag_env.update(ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1",
-                       MISLO_QUEUE_FLOOR_NS="200000")
+        rag_env.update(ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1")
         observable += list(GPU_SIGNALS)
     rag = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.rag_service", "--backend",
                             a.backend, "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", "",
@@ -371,7 +377,8 @@ def main() -> int:
                     "procfs_interval_ms": a.procfs_ms,
                     "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "
                                      "injected on its connections via faultinject --emit-ring --fault",
-                    "cpu_fault": "pinned CPU burners; run-queue delay measured by the schedstat sampler"}
+                    "cpu_fault": "pinned CPU burners; run-queue delay and CPU wait share measured by the agent's "
+                                 "native schedstat sampler"}
     res["exit"] = {"agent": agent.returncode, "rag": rag.returncode, "vectordb": vdb.returncode}
     with open(os.path.join(a.out, "summary.json"), "w") as f:
         json.dump(res, f, indent=1)
