@@ -173,8 +173,10 @@ class AgentOptions:
     state_dir: str = ""                  # agent state checkpoint directory ("" = none; resumed on start)
     checkpoint_every: int = 60           # windows between checkpoints
     gpus: int = 1                        # window workers (one per GPU); 0 = every GPU visible to the agent
+    split_rings: bool = True             # gpus > 1: one ring set per worker, producers route by owner
     model_path: str = ""                 # trained model file (attributor --train); overrides --model
     otlp_receiver_allow: str = ""        # CIDRs allowed to export spans to the receiver ("" = any)
+    otlp_forwarders: str = ""            # CIDRs of trusted span forwarders (no pod-address check)
     procfs_sampler: bool = False         # runqueue_delay_ms from /proc schedstat (no BPF needed)
     procfs_pods: str = ""                # pid:pod-uid,... to watch ("" = the node's kubepods cgroups)
     procfs_interval_ms: int = 100
@@ -387,18 +389,20 @@ class Agent:
         return 0
 
     # ---- window engine (GPU, or the CPU oracle engine) ---------------------------------------
-    def _open_source(self):
+    def _open_source(self, world: int = 1):
         """Rings + maps for the configured source. ``bpf``: the probes' pinned maps (root);
         ``shm``: emulated rings another process produces into (tests, CI); ``replay``: a forked
         replay producer writing seeded fault-replay windows at window_events per window_ms
         (stands in for the kernel probes and the rocprofiler tool: its CPU is not the agent's).
-        Returns (maps, ring, user ring, span ring, pod metadata or None)."""
+        ``world`` > 1: split rings, one (kernel, user-space, span) ring set per worker, every
+        producer routing each record to its owner's set (collector/bpf.py ShardRouter).
+        Returns (maps, [(ring, user ring, span ring)] per worker, pod metadata or None)."""
         from ..collector import bpf
         from ..runtime import load
 
         o = self.o
         rt = load()
-        names = bpf.RingNames.of(o.ring_name)
+        sets_names = [bpf.RingNames.of(o.ring_name, r) for r in range(max(1, world))]
         if o.source == "bpf":
             if o.probe_objs:  # load + attach the compiled probes; their shared maps get pinned
                 from ..collector.loader import BpfProbeLoader, probe_specs
@@ -411,25 +415,46 @@ class Agent:
                 attached = self.probe_manager.attach_all()
                 print(f"attached probes for {len(attached)} signals from {o.probe_objs}", file=sys.stderr)
             maps = bpf.BpfMaps(o.pin_dir)
-            user = rt.HostRing(1 << 20, 24, names.user)   # the rocprofiler tool attaches, pushes USER24
-            spans = rt.HostRing(1 << 18, 64, names.spans)  # OTLP receiver / services
-            return maps, maps.ring, user, spans, None
+            sets = []
+            for r, names in enumerate(sets_names):
+                ring = maps.ring if r == 0 else rt.Ringbuf.open_pinned(os.path.join(o.pin_dir, f"mislo_events{r}"))
+                sets.append((ring, rt.HostRing(1 << 20, 24, names.user),   # the rocprofiler tool pushes USER24
+                             rt.HostRing(1 << 18, 64, names.spans)))       # OTLP receiver / services
+            return maps, sets, None
         if o.source == "shm":
-            ring = rt.Ringbuf.attach_shm(names.ring)
-            return (bpf.EmulatedMaps(ring), ring, rt.HostRing(0, 64, names.user, True),
-                    rt.HostRing(0, 64, names.spans, True), None)
+            sets = [(rt.Ringbuf.attach_shm(n.ring), rt.HostRing(0, 64, n.user, True), rt.HostRing(0, 64, n.spans, True))
+                    for n in sets_names]
+            return bpf.EmulatedMaps(sets[0][0], [s[0] for s in sets[1:]]), sets, None
         if o.source == "replay":
             kw = dict(scenario=o.scenario if o.scenario not in ("baseline",) else "full",
                       events_per_window=o.window_events, spans_per_window=o.window_spans,
                       n_services=o.window_groups)
             # the replay writes ~1/4 of a window's events as GPU-signal records: rings of 2+
             # windows each (the shared pages count in the agent's RSS once registered for DMA)
-            ring, user, spans = bpf.create_rings(names, 2 * 24 * o.window_events, o.window_events,
-                                                 4 * o.window_spans)
-            self._producer = bpf.start_replay_producer(names, kw, o.window_events * 1000.0 / o.window_ms,
-                                                       o.window_ms, max_windows=0)
-            return bpf.EmulatedMaps(ring), ring, user, spans, bpf.pod_metadata(kw)
+            w = max(1, world)
+            sets = [tuple(bpf.create_rings(n, 2 * 24 * o.window_events // w + (1 << 20), o.window_events // w,
+                                           4 * o.window_spans // w + 1024)) for n in sets_names]
+            self._producer = bpf.start_replay_producer(sets_names[0], kw, o.window_events * 1000.0 / o.window_ms,
+                                                       o.window_ms, max_windows=0,
+                                                       shard_names=sets_names if w > 1 else None)
+            return bpf.EmulatedMaps(sets[0][0], [s[0] for s in sets[1:]]), sets, bpf.pod_metadata(kw)
         raise ValueError(f"unknown window source {o.source!r} (bpf | shm | replay)")
+
+    def _shard_table(self, world: int):
+        """The shared-memory pod id -> shard table the rocprofiler tool in the workloads routes its
+        records by (MISLO_SHARD_TABLE; 2^20 pod ids, one byte each; pods it does not list: 0)."""
+        from ..collector import bpf
+
+        path = "/dev/shm" + bpf.RingNames.shard_table(self.o.ring_name)
+        try:
+            with open(path, "wb") as fh:
+                fh.truncate(1 << 20)
+            os.chmod(path, 0o644)
+            self._shard_table_path = path
+            return np.memmap(path, dtype=np.uint8, mode="r+", shape=(1 << 20,))
+        except OSError as exc:
+            print(f"shard table {path}: {exc}; the GPU tool's records stay on ring 0", file=sys.stderr)
+            return None
 
     def _load_model(self):
         """(host model, PosteriorModel image, metadata): the file ``--model-path`` names (written by
@@ -622,12 +647,21 @@ class Agent:
         from .worker import WorkerPool, WorkerSpec, groups_of
 
         o = self.o
-        maps, ring, user, spans, pods = self._open_source()  # a replay producer forks here, before any GPU work
+        N = self.n_gpus()
+        split = N > 1 and o.split_rings
+        # a replay producer forks here, before any GPU work
+        maps, sets, pods = self._open_source(N if split else 1)
+        ring, user, spans = sets[0]
+        router = None
+        if split:  # producers route every record to its owner's ring set
+            router = bpf.ShardRouter(N, self._shard_table(N))
+            if pods is not None:
+                router.set_pods(*pods)
+        self.router = router
         node_id = bpf.stable_node_id(o.node)
         maps.init(node_id)
         model, image, self.model_meta = self._load_model()
         self.model = model
-        N = self.n_gpus()
         G = o.window_groups
         budget = o.window_events + o.window_events // 4  # events plus the definitions ahead of them
         # joins reach across the window cut (halo: the rows of the earlier windows it spans stay
@@ -650,13 +684,15 @@ class Agent:
                             group_cap=max(1, groups_of(0, N, G)), user_cap=max(1024, o.window_events // 4),
                             window_ms=float(o.window_ms), ttft_slo_ms=o.ttft_slo_ms, halo_ms=o.halo_ms,
                             import_cap=icap, xchg_cap=xchg, model_image=np.asarray(image, np.uint8).tobytes(),
-                            pods=pods, master=("127.0.0.1", port), halo_windows=halo_windows) for r in range(N)]
+                            pods=pods, master=("127.0.0.1", port), halo_windows=halo_windows, split=split)
+                 for r in range(N)]
         state = self._state_path()
         if state and os.path.exists(state):
             self.load_state(state)
         pool = WorkerPool(specs, (ring, user, spans), in_process=N == 1)
         self.pool = pool
-        print(f"window engine: {o.engine} x {N} worker(s), model {self.model_meta.get('name')}"
+        print(f"window engine: {o.engine} x {N} worker(s){' on split rings' if split else ''}, model "
+              f"{self.model_meta.get('name')}"
               f"{' T=%.3g' % self.model_meta['temperature'] if 'temperature' in self.model_meta else ''}",
               file=sys.stderr)
         if o.source == "bpf":
@@ -669,8 +705,25 @@ class Agent:
 
             groups = GroupTable(G)
             names = groups.names  # incident groups are the services the receiver has seen
-            mapper = SpanMapper(groups, self.pod_ids.id, node_id)
-            receiver = OtlpSpanReceiver(o.otlp_receiver_bind, mapper, spans.push, allow=o.otlp_receiver_allow).start()
+            pod_ips = None
+            if o.source == "bpf":  # a span naming a node's pod must come from that pod's address
+                from ..collector import procfs as _procfs
+
+                ipcache = {"t": -1e9, "m": {}}
+
+                def pod_ips():
+                    if time.monotonic() - ipcache["t"] > 10.0:
+                        ipcache["m"] = _procfs.pod_addresses(_procfs.pod_processes())
+                        ipcache["t"] = time.monotonic()
+                    return ipcache["m"]
+            mapper = SpanMapper(groups, self.pod_ids.id, node_id, pod_ips=pod_ips, forwarders=o.otlp_forwarders)
+            if router is not None:  # each span to the ring of the worker owning its incident group
+                def push_spans(recs):
+                    sh = router.span_shard(recs)
+                    return sum(int(sets[r][2].push(part)) for r, part in router.split(recs, sh) if len(part))
+            else:
+                push_spans = spans.push
+            receiver = OtlpSpanReceiver(o.otlp_receiver_bind, mapper, push_spans, allow=o.otlp_receiver_allow).start()
             self.receiver = receiver
         sampler = None
         if o.procfs_sampler:
@@ -688,8 +741,20 @@ class Agent:
                 return cache["m"]
 
             # native: a C++ thread reads schedstat / cgroup / PSI and pushes into the user ring
-            sampler = procfs.NativeSampler(user, targets, node_id=node_id, cpu_psi=o.procfs_cpu_psi,
-                                           refresh_s=10.0 if not static else 3600.0)
+            if router is None:
+                sampler = procfs.NativeSampler(user, targets, node_id=node_id, cpu_psi=o.procfs_cpu_psi,
+                                               refresh_s=10.0 if not static else 3600.0)
+            else:  # split rings: one sampler per worker, over the pods its services own
+                def shard_targets(r):
+                    def f():
+                        t = targets()
+                        owner = router.pod_shard(np.array(list(t.values()), dtype=np.int64)) if t else []
+                        return {pid: pod for (pid, pod), s in zip(t.items(), owner) if int(s) == r}
+                    return f
+
+                sampler = procfs.MultiSampler([procfs.NativeSampler(sets[r][1], shard_targets(r), node_id=node_id,
+                                                                    cpu_psi=o.procfs_cpu_psi, refresh_s=10.0)
+                                               for r in range(N)])
             sampler.start(o.procfs_interval_ms / 1000.0)
             self.procfs = sampler
         from ..safety import ShedLadder
@@ -713,8 +778,15 @@ class Agent:
                 nxt += period
                 t = time.time_ns()
                 maps.cfg_set(bpf.CFG_EPOCH, clock.publish(t))  # epoch first, then the ring snapshots
-                cut = Cut(kernel=ring.producer_pos, user=user.head, spans=spans.head, bases=clock.bases(), t_ns=t)
-                replies = pool.window(cut, G, mapper.take_pod_updates() if mapper is not None else None)
+                bases = clock.bases()
+                cuts = [Cut(kernel=rs[0].producer_pos, user=rs[1].head, spans=rs[2].head, bases=bases, t_ns=t)
+                        for rs in sets]
+                upd = mapper.take_pod_updates() if mapper is not None else None
+                if upd is not None and router is not None:  # later records of these pods go to their owners' rings
+                    router.set_pods(*upd)
+                    if hasattr(maps, "set_shards"):
+                        maps.set_shards(upd[0], router.pod_shard(upd[0]))
+                replies = pool.window(cuts if split else cuts[0], G, upd)
                 cut_t[replies[0]["k"]] = t
                 prev = replies[0].get("prev")
                 if prev is not None:

@@ -9,14 +9,22 @@ node the agent's window engine can use every GPU of the node, so the agent split
   discovery and the OTLP receiver (the pod -> service table), metrics, outputs, webhook, the
   overhead guard over the whole process tree. It never initialises HIP;
 * one **worker per GPU** (a spawned process; ``LocalWorker`` runs the same core in-process when
-  the node uses one GPU): a WindowPipeline on its GPU over the SAME rings, consuming every cut.
-  Group sharding splits the stream on the device (decode.hip ``shard_owns``): worker r counts and
-  joins only the records and spans of the services it owns (service s -> worker (s - 1) % N), so
-  an incident is scored entirely on one GPU; cross-service trace joins go through the engine's
-  trace-row exchange, node-wide histograms through its packet all-reduce, and worker 0 receives
-  every worker's incident results through the all-gather (RCCL over xGMI; gloo for the CPU
-  engine). Workers never move ring consumer positions: each reports how far it is done and the
-  controller frees ring space up to the slowest worker.
+  the node uses one GPU): a WindowPipeline on its GPU. Worker r owns the services s with
+  (s - 1) % N == r, so an incident is scored entirely on one GPU; cross-service trace joins go
+  through the engine's trace-row exchange, node-wide histograms through its packet all-reduce,
+  and worker 0 receives every worker's incident results through the all-gather (RCCL over xGMI;
+  gloo for the CPU engine). Two ways to split the node's stream:
+
+  - **split rings** (``split``, the default with N > 1): every producer writes each record to the
+    ring set of the worker owning it (collector/bpf.py ShardRouter: kernel and user-space records
+    by their pod's service, spans by incident group; the probes through ``mislo_shards``, the
+    rocprofiler tool through the shared pod -> shard table, the OTLP receiver and the procfs
+    sampler in the agent). Worker r DMAs and decodes only its own rings -- 1/N of the node's
+    bytes -- and frees them itself;
+  - **shared rings**: every worker DMAs the whole window and group sharding drops the records of
+    services it does not own on the device (decode.hip ``shard_owns``). Workers never move ring
+    consumer positions: each reports how far it is done and the controller frees ring space up
+    to the slowest worker.
 
 Protocol (multiprocessing pipes, pickled, O(groups) bytes per window): controller -> worker
 ``("window", cut, n_groups, pods)`` every window, ``("stop",)``; worker -> controller one reply per
@@ -62,6 +70,7 @@ class WorkerSpec:
     master: Tuple[str, int] = ("127.0.0.1", 0)   # gloo rendezvous (cpu engine)
     env: Dict[str, str] = field(default_factory=dict)
     halo_windows: int = 3       # earlier windows resident on the device for the halo
+    split: bool = False         # split rings: this worker's own ring set (RingNames.of(ring_name, rank))
 
 
 def groups_of(rank: int, world: int, n_groups: int) -> int:
@@ -95,11 +104,12 @@ class WorkerCore:
         from ..runtime import load
 
         self.spec = spec
+        shard = spec.rank if spec.split else 0
         if rings is None:
             rt = load()
-            names = bpf.RingNames.of(spec.ring_name)
+            names = bpf.RingNames.of(spec.ring_name, shard)
             if spec.source == "bpf":
-                ring = rt.Ringbuf.open_pinned(os.path.join(spec.pin_dir, "mislo_events"))
+                ring = rt.Ringbuf.open_pinned(os.path.join(spec.pin_dir, "mislo_events" + (str(shard) if shard else "")))
             else:
                 ring = rt.Ringbuf.attach_shm(names.ring)
             rings = (ring, rt.HostRing(0, spec.user_rec, names.user, True), rt.HostRing(0, 64, names.spans, True))
@@ -110,9 +120,12 @@ class WorkerCore:
                                    ttft_slo_ms=spec.ttft_slo_ms, halo_ms=spec.halo_ms, halo_windows=spec.halo_windows,
                                    import_cap=spec.import_cap,
                                    xchg_cap=spec.xchg_cap, shard=(spec.rank, spec.world), engine=spec.engine,
-                                   group=group, model_image=np.frombuffer(spec.model_image, dtype=np.uint8))
-        # the controller publishes the epochs: this source never writes mislo_cfg
-        self.src = RingWindowSource(self.pipe, ring, user, spans, cfg_set=lambda i, v: None, shared=shared)
+                                   group=group, model_image=np.frombuffer(spec.model_image, dtype=np.uint8),
+                                   split_rings=spec.split)
+        # the controller publishes the epochs: this source never writes mislo_cfg. Split rings are
+        # this worker's alone: it frees their space itself
+        self.src = RingWindowSource(self.pipe, ring, user, spans, cfg_set=lambda i, v: None,
+                                    shared=shared and not spec.split)
         if spec.pods is not None:
             self.pipe.eng.set_pods(*spec.pods)
         self.pending: Optional[Tuple[int, float]] = None
@@ -307,6 +320,7 @@ class WorkerPool:
                 self.close()
                 raise
         self.in_process = in_process
+        self.split = bool(specs[0].split) and self.world > 1
         r = rings
         self._rel_user = r[1].tail if r[1] is not None else 0
         self._rel_spans = r[2].tail if r[2] is not None else 0
@@ -315,15 +329,17 @@ class WorkerPool:
         return [w.pid for w in self.workers]
 
     def window(self, cut, n_groups: int, pods=None) -> List[dict]:
+        """``cut``: one Cut of the shared rings, or (split rings) a list with each worker's own."""
         for w in self.workers:
-            w.send(("window", cut, groups_of(w.spec.rank, self.world, n_groups), pods))
+            c = cut[w.spec.rank] if isinstance(cut, (list, tuple)) and not hasattr(cut, "kernel") else cut
+            w.send(("window", c, groups_of(w.spec.rank, self.world, n_groups), pods))
         replies = [w.recv()[1] for w in self.workers]
         self._release(replies)
         return replies
 
     def _release(self, replies: List[dict]) -> None:
-        if self.in_process:
-            return  # the single source frees its rings itself
+        if self.in_process or self.split:
+            return  # the single source / every split-ring worker frees its rings itself
         ring, user, spans = self.rings
         dones = [r["done"] for r in replies if r.get("done") is not None]
         if not dones:

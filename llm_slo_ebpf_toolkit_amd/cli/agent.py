@@ -60,10 +60,15 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("source", d.source, "window engine record source: bpf (pinned probe maps) | shm (emulated rings) | replay"),
         ("gpus", d.gpus, "window workers, one per GPU (0 = every GPU visible to the agent); each owns a share of "
                          "the node's services, node-wide results over RCCL"),
+        ("split-rings", True, "with --gpus N > 1: one ring set per worker, every producer routing each record to "
+                              "the worker owning its service (false: every worker reads the whole stream)"),
         ("model-path", d.model_path, "trained attribution model (safetensors) written by `attributor --train`; "
                                      "overrides --model"),
         ("otlp-receiver-allow", d.otlp_receiver_allow, "comma-separated CIDRs allowed to export spans to the "
                                                        "receiver (empty = any)"),
+        ("otlp-forwarders", d.otlp_forwarders, "comma-separated CIDRs of trusted span forwarders (an OTel collector "
+                                               "relaying other pods' spans): exempt from the check that a span "
+                                               "naming a pod comes from that pod's address"),
         ("procfs-sampler", False, "window engine: run-queue delay, CPU wait share (cpu_steal_pct), CFS throttling "
                                   "and memory stall of pod processes from /proc schedstat and their cgroups "
                                   "(unprivileged; min-capability mode)"),
@@ -116,8 +121,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         window_groups=a.window_groups, device=a.device, model=a.model, min_confidence=a.min_confidence,
         ttft_slo_ms=a.ttft_slo_ms, slo_target=a.slo_target,
         otlp_receiver_bind=a.otlp_receiver_bind, halo_ms=float(a.halo_ms), state_dir=a.state_dir,
-        checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), model_path=a.model_path,
-        otlp_receiver_allow=a.otlp_receiver_allow, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
+        checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), split_rings=bool(a.split_rings), model_path=a.model_path,
+        otlp_receiver_allow=a.otlp_receiver_allow, otlp_forwarders=a.otlp_forwarders, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
         procfs_interval_ms=int(a.procfs_interval_ms), procfs_cpu_psi=bool(a.procfs_cpu_psi),
         model_signals=a.model_signals,
         pair_prior=float(a.pair_prior))

@@ -81,14 +81,17 @@ class MapSet:
 
 
 class EmulatedMaps(MapSet):
-    """mislo_cfg lives in the emulated ring's meta page; pods in a dict."""
+    """mislo_cfg lives in the emulated ring's meta page (every shard ring's, with split rings:
+    each ring's producers read the epoch and floors from their own ring); pods in a dict."""
 
-    def __init__(self, ring):
+    def __init__(self, ring, shard_rings=()):
         self.ring = ring
+        self.rings = [ring] + [r for r in shard_rings if r is not None and r is not ring]
         self.pods: Dict[int, int] = {}
 
     def cfg_set(self, idx: int, value: int) -> None:
-        self.ring.cfg_set(int(idx), int(value) & 0xFFFFFFFFFFFFFFFF)
+        for r in self.rings:
+            r.cfg_set(int(idx), int(value) & 0xFFFFFFFFFFFFFFFF)
 
     def cfg_get(self, idx: int) -> int:
         return int(self.ring.cfg_get(int(idx)))
@@ -119,6 +122,20 @@ class BpfMaps(MapSet):
 
     def set_pod(self, cgroup_id: int, pod_id: int) -> None:
         self.pods.update(struct.pack("<Q", int(cgroup_id)), struct.pack("<I", int(pod_id)))
+
+    def set_shards(self, pod_ids, shards) -> None:
+        """mislo_shards: the ring a pod's records go to (split rings, agent --gpus N)."""
+        if getattr(self, "_shards", None) is None:
+            from ..runtime import load
+
+            try:
+                self._shards = load().BpfMap(os.path.join(self.pin_dir, "mislo_shards"))
+            except (OSError, RuntimeError):
+                self._shards = False
+        if not self._shards:
+            return
+        for p, s in zip(np.asarray(pod_ids).tolist(), np.asarray(shards).tolist()):
+            self._shards.update(struct.pack("<I", int(p)), struct.pack("<I", int(s)))
 
     def reset_ctx_ids(self) -> int:
         """Clear mislo_ctxs and restart its id counter (the agent does this at a window cut when
@@ -182,8 +199,60 @@ class RingNames:
     spans: str
 
     @staticmethod
-    def of(prefix: str) -> "RingNames":
-        return RingNames(prefix + "-bpf", prefix + "-events", prefix + "-spans")
+    def of(prefix: str, shard: int = 0) -> "RingNames":
+        """The ring set of one worker (``shard`` > 0: agent --gpus N with split rings, worker
+        ``shard``'s own kernel / user-space / span rings)."""
+        sfx = str(int(shard)) if shard else ""
+        return RingNames(prefix + "-bpf" + sfx, prefix + "-events" + sfx, prefix + "-spans" + sfx)
+
+    @staticmethod
+    def shard_table(prefix: str) -> str:
+        """Shared-memory pod id -> shard byte table the user-space producers route by."""
+        return prefix + "-shards"
+
+
+def shard_of_pod(svcnode: np.ndarray, world: int) -> np.ndarray:
+    """The worker that owns a pod's records: its service's (decode.hip shard_owns: service
+    s >= 1 -> (s - 1) % world; no service yet -> 0)."""
+    svc = (np.asarray(svcnode, dtype=np.uint32) >> np.uint32(16)).astype(np.int64)
+    return np.where(svc > 0, (svc - 1) % max(1, world), 0).astype(np.int64)
+
+
+class ShardRouter:
+    """Split rings (agent --gpus N): one ring set per worker, every record written to the ring of
+    the worker that owns it -- kernel and user-space records by their pod's service (the pod
+    table), spans by their incident group (group g -> worker g % N). Each worker then DMAs and
+    decodes only its own share of the node's stream."""
+
+    def __init__(self, world: int, table=None):
+        self.world = max(1, int(world))
+        self.svc: Dict[int, int] = {}  # pod id -> svc|node
+        self.table = table              # shared-memory pod -> shard bytes (numpy view), for the GPU tool
+
+    def set_pods(self, pods: np.ndarray, sn: np.ndarray) -> None:
+        sh = shard_of_pod(sn, self.world)
+        for p, v, s in zip(np.asarray(pods).tolist(), np.asarray(sn).tolist(), sh.tolist()):
+            self.svc[int(p)] = int(v)
+            if self.table is not None and 0 <= int(p) < len(self.table):
+                self.table[int(p)] = int(s)
+
+    def pod_shard(self, pod_ids: np.ndarray) -> np.ndarray:
+        sn = np.array([self.svc.get(int(p), 0) for p in np.asarray(pod_ids).tolist()], dtype=np.uint32)
+        return shard_of_pod(sn, self.world)
+
+    def span_shard(self, spans: np.ndarray) -> np.ndarray:
+        return (spans["group_id"].astype(np.int64) % self.world).astype(np.int64)
+
+    def split(self, recs: np.ndarray, shard: np.ndarray):
+        """[(shard, records of that shard)] in shard order (stable within a shard)."""
+        return [(r, recs[shard == r]) for r in range(self.world)]
+
+
+def create_shard_rings(prefix: str, world: int, ring_bytes: int, user_records: int, span_records: int,
+                       user_rec: int = 24):
+    """One ring set per worker (split rings), each sized for its share of the node's stream."""
+    return [create_rings(RingNames.of(prefix, r), ring_bytes, user_records, span_records, user_rec)
+            for r in range(max(1, int(world)))]
 
 
 def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int, user_rec: int = 24):
@@ -200,30 +269,38 @@ def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_reco
 
 
 def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, window_ms: int, max_windows: int,
-                         n_images: int, ready=None) -> None:
+                         n_images: int, ready=None, shard_names=None) -> None:
     """Process body: generates ``n_images`` replay windows, then writes one window per
     ``window_ms`` at ``rate_eps``: the kernel-signal records through the probe model (using
     the epoch the agent published, read from the emulated mislo_cfg at write time), the GPU-
     signal records and the spans into the user-space rings. Stops after ``max_windows`` (0 =
-    forever). Never touches the GPU."""
+    forever). Never touches the GPU. ``shard_names``: the workers' ring sets (split rings): every
+    record goes to the ring set of the worker owning its service (ShardRouter), through that
+    ring's own probe model (each kernel ring carries its own id definitions)."""
     from ..pipeline.replay import ReplayConfig, ReplayGenerator
     from ..pipeline.window import kernel_event_mask
     from ..runtime import load
 
     rt = load()
-    rb = rt.Ringbuf.attach_shm(names.ring)
-    user = rt.HostRing(0, 64, names.user, True)
-    spans = rt.HostRing(0, 64, names.spans, True)
+    sets = list(shard_names) if shard_names else [names]
+    world = len(sets)
+    rbs = [rt.Ringbuf.attach_shm(n.ring) for n in sets]
+    users = [rt.HostRing(0, 64, n.user, True) for n in sets]
+    spanss = [rt.HostRing(0, 64, n.spans, True) for n in sets]
     # the cycled images keep one fault assignment (window k's halo joins window k+1)
     cfg = ReplayConfig(window_ms=window_ms, fault_hold=max(1, n_images), **cfg_kwargs)
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, n_images))]
-    sim = rt.ProbeSim(rb, records.milli_shift_table())
+    sims = [rt.ProbeSim(rb, records.milli_shift_table()) for rb in rbs]
+    router = ShardRouter(world)
+    router.set_pods(*pod_metadata(cfg_kwargs))
     parts = []
     for w in wins:
         km = kernel_event_mask(w.events)
-        uev = np.ascontiguousarray(w.events[~km])
-        parts.append((np.ascontiguousarray(w.events[km]), uev, np.ascontiguousarray(w.spans)))
+        kev, uev, sp = w.events[km], w.events[~km], w.spans
+        ks, us, ss = router.pod_shard(kev["pod_id"]), router.pod_shard(uev["pod_id"]), router.span_shard(sp)
+        parts.append([(np.ascontiguousarray(kev[ks == r]), np.ascontiguousarray(uev[us == r]),
+                       np.ascontiguousarray(sp[ss == r])) for r in range(world)])
     if ready is not None:
         ready.send(True)
     period = window_ms / 1000.0
@@ -232,24 +309,27 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
     nxt = time.perf_counter()
     j = 0
     while not max_windows or j < max_windows:
-        kev, uev, sp = parts[j % len(parts)]
         shift = t_start + j * int(period * 1e9) - int(wins[j % len(wins)].t0_ns)
-        kev, uev, sp = kev.copy(), uev.copy(), sp.copy()
-        for a in (kev, uev, sp):
-            nz = a["ts_ns"] != 0
-            a["ts_ns"][nz] += shift
-        uev = records.to_user(uev, int(user.rec_size))  # what the rocprof tool writes into this ring
+        shard_parts = []
+        for r, (kev, uev, sp) in enumerate(parts[j % len(parts)]):
+            kev, uev, sp = kev.copy(), uev.copy(), sp.copy()
+            for a in (kev, uev, sp):
+                nz = a["ts_ns"] != 0
+                a["ts_ns"][nz] += shift
+            # what the rocprof tool writes into this ring
+            shard_parts.append((kev, records.to_user(uev, int(users[r].rec_size)), sp))
         # pace: the window's records go out in 10 slices across its period
         n_sl = 10
         for s in range(n_sl):
-            lo_k, hi_k = len(kev) * s // n_sl, len(kev) * (s + 1) // n_sl
-            sim.submit(kev[lo_k:hi_k])
-            lo_u, hi_u = len(uev) * s // n_sl, len(uev) * (s + 1) // n_sl
-            if hi_u > lo_u:
-                user.push(uev[lo_u:hi_u])
-            lo_s, hi_s = len(sp) * s // n_sl, len(sp) * (s + 1) // n_sl
-            if hi_s > lo_s:
-                spans.push(sp[lo_s:hi_s])
+            for r, (kev, uev, sp) in enumerate(shard_parts):
+                lo_k, hi_k = len(kev) * s // n_sl, len(kev) * (s + 1) // n_sl
+                sims[r].submit(kev[lo_k:hi_k])
+                lo_u, hi_u = len(uev) * s // n_sl, len(uev) * (s + 1) // n_sl
+                if hi_u > lo_u:
+                    users[r].push(uev[lo_u:hi_u])
+                lo_s, hi_s = len(sp) * s // n_sl, len(sp) * (s + 1) // n_sl
+                if hi_s > lo_s:
+                    spanss[r].push(sp[lo_s:hi_s])
             nxt += period / n_sl
             time.sleep(max(0.0, nxt - time.perf_counter()))
         j += 1
@@ -265,15 +345,15 @@ def pod_metadata(cfg_kwargs: dict) -> Tuple[np.ndarray, np.ndarray]:
 
 
 def start_replay_producer(names: RingNames, cfg_kwargs: dict, rate_eps: float, window_ms: int,
-                          max_windows: int = 0, n_images: int = 2):
+                          max_windows: int = 0, n_images: int = 2, shard_names=None):
     """Fork the replay producer (before this process touches the GPU) and wait until it has
     generated its windows."""
     import multiprocessing as mp
 
     ctx = mp.get_context("fork")
     a, b = ctx.Pipe()
-    p = ctx.Process(target=replay_producer_main, args=(names, cfg_kwargs, rate_eps, window_ms, max_windows, n_images, b),
-                    daemon=True)
+    p = ctx.Process(target=replay_producer_main,
+                    args=(names, cfg_kwargs, rate_eps, window_ms, max_windows, n_images, b, shard_names), daemon=True)
     p.start()
     if not a.poll(600):
         raise RuntimeError("replay producer did not start")

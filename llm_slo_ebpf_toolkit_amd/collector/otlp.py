@@ -260,8 +260,17 @@ def _first(attrs: Dict[str, object], keys) -> object:
 class SpanMapper:
     """OTLP spans -> SPAN records on the agent's ids."""
 
-    def __init__(self, groups: GroupTable, pod_id: Callable[[str], int], node_id: int = 0):
+    def __init__(self, groups: GroupTable, pod_id: Callable[[str], int], node_id: int = 0,
+                 pod_ips: Optional[Callable[[], Dict[str, set]]] = None, forwarders: str = ""):
+        """``pod_ips()`` -> {IP: pod uids at that IP} of this node's pods (procfs.pod_addresses):
+        a span that names a pod is kept only when it comes from that pod's address (or from an
+        address the map does not know). ``forwarders``: CIDRs of trusted span forwarders (an
+        OpenTelemetry collector relaying many pods' spans) the address check does not apply to."""
         self.groups, self.pod_id, self.node_id = groups, pod_id, node_id
+        self.pod_ips = pod_ips
+        self.forwarders = [ipaddress.ip_network(c.strip(), strict=False) for c in forwarders.split(",") if c.strip()]
+        self.conflicts = 0  # spans that named a pod already bound to another service (dropped)
+        self.spoofed = 0    # spans from a known pod address naming another pod (dropped)
         # pod id -> svc << 16 | node as the spans reveal it: the window engine's pod table, so the
         # kernel's and the rocprof tool's records of a pod carry its service (the service+node join
         # tier, and the service that decides which GPU owns them, agent --gpus N)
@@ -278,14 +287,32 @@ class SpanMapper:
         ids = np.array(list(new), dtype=np.uint32)
         return ids, np.array([new[int(i)] for i in ids.tolist()], dtype=np.uint32)
 
+    def _forwarder(self, peer: str) -> bool:
+        try:
+            ip = ipaddress.ip_address(peer)
+        except ValueError:
+            return False
+        return any(ip in n for n in self.forwarders)
+
     @staticmethod
     def is_request_span(d: dict) -> bool:
         attrs = d.get("attrs", {})
         return not d.get("parentSpanId") or any(k in attrs for k in TTFT_KEYS)
 
-    def records(self, spans: List[Tuple[Dict[str, object], dict]]) -> np.ndarray:
+    def records(self, spans: List[Tuple[Dict[str, object], dict]], peer: str = "") -> np.ndarray:
+        """Request spans -> SPAN records. A pod's service is bound by the first span that names
+        both; later spans naming that pod with another service are dropped (a pod cannot move
+        another pod's records to its service), and with ``pod_ips`` a span naming a pod must come
+        from that pod's address when the address is one of this node's pods."""
         sel = [(r, d) for r, d in spans if self.is_request_span(d)]
+        at_peer = None
+        if self.pod_ips is not None and peer and not self._forwarder(peer):
+            try:
+                at_peer = self.pod_ips().get(peer)
+            except Exception:  # noqa: BLE001 - an unreadable map checks nothing
+                at_peer = None
         out = np.zeros(len(sel), dtype=records.SPAN)
+        keep = np.ones(len(sel), dtype=bool)
         for i, (res, d) in enumerate(sel):
             a = d["attrs"]
             t0 = int(d.get("startTimeUnixNano") or 0)
@@ -297,6 +324,10 @@ class SpanMapper:
             sport = _first(a, ("client.port", "net.host.port", "net.sock.host.port")) or 0
             dport = _first(a, ("server.port", "net.peer.port", "net.sock.peer.port")) or 0
             dip = _ipv4(_first(a, ("server.address", "net.peer.ip", "net.sock.peer.addr")) or "")
+            if pod and at_peer is not None and str(pod) not in at_peer:
+                self.spoofed += 1
+                keep[i] = False
+                continue
             g = self.groups.id(svc)
             out[i]["ts_ns"] = t0
             out[i]["trace_h"] = trace_hash(d.get("traceId"))
@@ -308,7 +339,12 @@ class SpanMapper:
             out[i]["svc_id"] = g + 1
             if pid_:
                 sn = ((g + 1) << 16) | (self.node_id & 0xFFFF)
-                if self._pods.get(pid_) != sn:
+                bound = self._pods.get(pid_)
+                if bound is not None and bound != sn:
+                    self.conflicts += 1
+                    keep[i] = False
+                    continue
+                if bound is None:
                     with self._plock:
                         self._pods[pid_] = sn
                         self._new[pid_] = sn
@@ -317,7 +353,7 @@ class SpanMapper:
             out[i]["latency_ms"] = (t1 - t0) / 1e6
             if int(sport) or int(dport):
                 out[i]["conn_h"] = records.conn_hash(int(sport), int(dport), dip)
-        return out
+        return out if keep.all() else out[keep]
 
 
 class OtlpSpanReceiver:
@@ -341,11 +377,11 @@ class OtlpSpanReceiver:
         self._srv: Optional[http.server.ThreadingHTTPServer] = None
         self._thr: Optional[threading.Thread] = None
 
-    def ingest(self, body: bytes, content_type: str) -> Tuple[int, int]:
+    def ingest(self, body: bytes, content_type: str, peer: str = "") -> Tuple[int, int]:
         """Parse one export request and push its request spans; (pushed, dropped)."""
         ct = (content_type or "").split(";")[0].strip().lower()
         spans = parse_proto(body) if ct in ("application/x-protobuf", "application/protobuf") else parse_json(body)
-        recs = self.mapper.records(spans)
+        recs = self.mapper.records(spans, peer)
         n = int(self.push(recs)) if len(recs) else 0
         with self._lock:
             self.requests += 1
@@ -398,7 +434,7 @@ class OtlpSpanReceiver:
                 body = self.rfile.read(n) if n > 0 else b""
                 ctype = self.headers.get("Content-Type", "application/json")
                 try:
-                    _, dropped = rx.ingest(body, ctype)
+                    _, dropped = rx.ingest(body, ctype, str(self.client_address[0]))
                 except (ValueError, KeyError, TypeError) as exc:
                     with rx._lock:
                         rx.rejected += 1

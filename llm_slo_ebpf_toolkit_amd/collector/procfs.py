@@ -99,7 +99,10 @@ def read_schedstat(path: str) -> Optional[Tuple[int, int, int]]:
 
 STEAL_TYPE = 6             # catalogue kernel type of cpu_steal_pct (milli-percent in the record)
 CFS_TYPE = 12              # catalogue kernel type of cfs_throttled_ms (ns in the record)
-STEAL_FLOOR_MILLI = 1000   # 1 % of one CPU over the interval
+# 20 % of one CPU over the interval: a healthy multi-threaded service's own threads contend for
+# its CPUs at a few percent (config-3 baseline on MI355X: 27 of ~150 intervals of the RAG service
+# at 2-8 %, 7 above 8 %; under the CPU fault every interval well above 8 %, profiles/r4_config3_first)
+STEAL_FLOOR_MILLI = 20000
 SIGNAL_TYPES = {"runqueue_delay_ms": RUNQUEUE_TYPE, "cpu_steal_pct": STEAL_TYPE,
                 "mem_reclaim_latency_ms": MEM_RECLAIM_TYPE, "cfs_throttled_ms": CFS_TYPE}
 ALL_MASK = sum(1 << t for t in SIGNAL_TYPES.values())
@@ -420,4 +423,74 @@ def pod_processes(cgroup_root: str = "/sys/fs/cgroup") -> Dict[int, str]:
                         out[int(ln)] = uid
         except OSError:
             continue
+    return out
+
+
+class MultiSampler:
+    """Several samplers as one (split rings: one per worker ring set); the shedding ladder sets
+    the mask / pause on all of them."""
+
+    def __init__(self, samplers):
+        self.samplers = list(samplers)
+
+    @property
+    def mask(self) -> int:
+        return self.samplers[0].mask if self.samplers else 0
+
+    @mask.setter
+    def mask(self, m: int) -> None:
+        for s in self.samplers:
+            s.mask = m
+
+    @property
+    def paused(self) -> bool:
+        return all(s.paused for s in self.samplers)
+
+    @paused.setter
+    def paused(self, p: bool) -> None:
+        for s in self.samplers:
+            s.paused = p
+
+    def start(self, interval_s: float = 0.1) -> "MultiSampler":
+        for s in self.samplers:
+            s.start(interval_s)
+        return self
+
+    def stop(self) -> None:
+        for s in self.samplers:
+            s.stop()
+
+    def stats(self) -> Dict[str, int]:
+        out: Dict[str, int] = {}
+        for s in self.samplers:
+            for k, v in s.stats().items():
+                out[k] = max(out.get(k, 0), v) if k in ("max_tick_ns", "last_tick_ns") else out.get(k, 0) + v
+        return out
+
+
+def local_addresses(pid: int, proc_root: str = "/proc") -> set:
+    """The IPv4 addresses local to ``pid``'s network namespace (``/proc/<pid>/net/fib_trie``
+    "/32 host LOCAL" entries), loopback excluded."""
+    text = _read(os.path.join(proc_root, str(pid), "net", "fib_trie")) or ""
+    out, last = set(), ""
+    for ln in text.splitlines():
+        t = ln.strip()
+        if t.startswith("|--"):
+            last = t[3:].strip()
+        elif t.startswith("/32 host LOCAL") and last and not last.startswith("127."):
+            out.add(last)
+    return out
+
+
+def pod_addresses(procs: Dict[int, str], proc_root: str = "/proc") -> Dict[str, set]:
+    """{IP: pod uids} of the node's pods, from one process per pod (``procs``: pid -> pod uid, e.g.
+    ``pod_processes()``): the OTLP receiver keeps a span that names a pod only when it arrives
+    from that pod's address (collector/otlp.py SpanMapper)."""
+    seen: Dict[str, int] = {}
+    for pid, uid in sorted(procs.items()):
+        seen.setdefault(uid, pid)
+    out: Dict[str, set] = {}
+    for uid, pid in seen.items():
+        for ip in local_addresses(pid, proc_root):
+            out.setdefault(ip, set()).add(uid)
     return out

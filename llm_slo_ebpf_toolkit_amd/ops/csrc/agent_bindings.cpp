@@ -50,7 +50,7 @@ class PyEngine {
   PyEngine(int device, int sig_cap, int span_cap, int group_cap, int user_cap, int n_buffers, int max_ahead,
            double window_ms, double threshold, int fanout, int group_mode, bool use_graphs, bool device_refit,
            int n_dom, float ttft_slo_ms, double halo_ms, int import_cap, int xchg_cap, int shard_rank,
-           int shard_world, int halo_windows) {
+           int shard_world, int halo_windows, bool split_rings) {
     if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world) throw std::invalid_argument("shard rank / world");
     EngineConfig c;
     c.device = device;
@@ -74,6 +74,7 @@ class PyEngine {
     c.xchg_cap = xchg_cap;
     c.shard_rank = shard_rank;
     c.shard_world = shard_world;
+    c.split_rings = split_rings;
     e_ = std::make_unique<WindowEngine>(c);
   }
   bool register_host(uintptr_t addr, size_t bytes) {
@@ -314,14 +315,14 @@ PYBIND11_MODULE(_mislo_agent, m) {
       py::make_tuple("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events", "other_shard");
   py::class_<PyEngine>(m, "WindowEngine")
       .def(py::init<int, int, int, int, int, int, int, double, double, int, int, bool, bool, int, float, double, int,
-                    int, int, int, int>(),
+                    int, int, int, int, bool>(),
            py::arg("device") = 0, py::arg("sig_cap") = 1 << 20, py::arg("span_cap") = 16384, py::arg("group_cap") = 64,
            py::arg("user_cap") = 1 << 18, py::arg("n_buffers") = 3, py::arg("max_ahead") = 3,
            py::arg("window_ms") = 2000.0, py::arg("threshold") = 0.7, py::arg("fanout") = 3, py::arg("group_mode") = 1,
            py::arg("use_graphs") = true, py::arg("device_refit") = true, py::arg("n_dom") = 10,
            py::arg("ttft_slo_ms") = 800.0f, py::arg("halo_ms") = 0.0, py::arg("import_cap") = 0,
            py::arg("xchg_cap") = 0, py::arg("shard_rank") = 0, py::arg("shard_world") = 1,
-           py::arg("halo_windows") = 3)
+           py::arg("halo_windows") = 3, py::arg("split_rings") = false)
       .def("register_host", &PyEngine::register_host)
       .def("submit", &PyEngine::submit, py::arg("k"), py::arg("kernel"), py::arg("user"), py::arg("spans"),
            py::arg("n_groups"), py::arg("labels") = py::none(), py::arg("bases") = std::vector<int64_t>{},

@@ -468,7 +468,11 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const EventC16 e{a.x, a.y, b.x, b.y};
         bool ok = i < valid_k && h.x == 16u && (e.ctx_type & 0xFFu) < kDefFirst;
         const uint32_t cid = e.ctx_type >> 8;
-        const uint4 cx = ok && cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
+        uint4 cx = ok && cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
+        // the pod's service as the pod table knows it now: a context defined before the pod's
+        // first span reached the agent stored svc 0, which would keep its records on GPU 0
+        const uint32_t sn_now = cx.x < n_pods ? pod_sn[cx.x] : 0u;
+        if (sn_now) cx.w = sn_now;
         if (ok && !shard_owns(cx.w, sh_rank, sh_world)) {
           ok = false;
           ++other;

@@ -72,6 +72,11 @@ struct EngineConfig {
   // group sharding of one node's stream over the node's GPUs (agent --gpus N): this GPU counts and
   // joins only its services' records and incident groups (decode.hip shard_owns); 1 = whole stream
   int shard_rank = 0, shard_world = 1;
+  // split rings (agent --gpus N with per-worker rings): the producers already routed every record
+  // to the ring of the worker owning its service, so the records are not filtered again here (a
+  // record routed before its pod's service was known is counted where it landed, never twice);
+  // spans keep the ownership filter (it also maps global groups to this GPU's local ones)
+  bool split_rings = false;
 };
 
 // per-incident results of a window, in one pinned block (one D2H)
@@ -176,6 +181,9 @@ class WindowEngine {
   double host_tail_us() const { return issue_n_ ? tail_us_ / issue_n_ : 0.0; }   // results D2H + comm stream
 
  private:
+  // the record ownership filter's (rank, world): none with split rings (EngineConfig::split_rings)
+  int rec_shard_rank() const { return cfg_.split_rings ? 0 : cfg_.shard_rank; }
+  int rec_shard_world() const { return cfg_.split_rings ? 1 : cfg_.shard_world; }
   void alloc();
   void run_part1(int b, hipStream_t st, bool xchg);
   void run_part2(int b, int n_groups, bool with_labels, bool learn, hipStream_t st, bool xchg);

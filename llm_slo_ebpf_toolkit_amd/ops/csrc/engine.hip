@@ -428,7 +428,7 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                        ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st, 0, 0, 0,
-                       cfg_.shard_rank, cfg_.shard_world);
+                       rec_shard_rank(), rec_shard_world());
   if (xchg)  // this window's warn-level trace-tagged rows, as the other GPUs will import them
     launch_select(sig_cols(), rows_, counts, N, sel_cnt_, sel_off_, reinterpret_cast<XRec*>(xsend_ + sizeof(XRec)),
                   reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, st);
@@ -445,7 +445,7 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
     const TraceIds tt{trace_hash_, kTraceIdRows};
     launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                          ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st,
-                         1, nblk_imp_, nblk_sig_, cfg_.shard_rank, cfg_.shard_world);
+                         1, nblk_imp_, nblk_sig_, rec_shard_rank(), rec_shard_world());
   }
   if (xchg)
     launch_partition_sig(sig_cols(), rows_, N, nblk_sig_ + nblk_imp_, g_part_blk_, g_part_off_, g_part_tot_, st,

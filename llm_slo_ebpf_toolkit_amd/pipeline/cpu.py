@@ -153,7 +153,7 @@ class CpuRingEngine:
                  n_buffers: int = 3, window_ms: float = 2000.0, threshold: float = 0.7, fanout: int = 3,
                  group_mode: int = 1, n_dom: int = N_DOMAINS, ttft_slo_ms: float = 800.0, halo_ms: float = 0.0,
                  import_cap: int = 0, xchg_cap: int = 0, shard_rank: int = 0, shard_world: int = 1, group=None,
-                 halo_windows: int = 3, **_native_only):
+                 halo_windows: int = 3, split_rings: bool = False, **_native_only):
         from ..parallel.exchange import ExchangeModel, torch_allgather
 
         self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
@@ -161,6 +161,7 @@ class CpuRingEngine:
         self.window_ms_, self.threshold, self.fanout, self.group_mode = window_ms, threshold, fanout, group_mode
         self.n_dom, self.ttft_slo_ms = n_dom, float(ttft_slo_ms)
         self.shard_rank, self.shard_world = int(shard_rank), int(shard_world)
+        self.split_rings = bool(split_rings)
         self.group = group
         if group is not None:
             import torch.distributed as dist
@@ -229,7 +230,7 @@ class CpuRingEngine:
         valid_k = ((fr[:, 0] == 16) & ((fr[:, 3] & np.uint32(0xFF)) < records.DEF_FIRST)) if n_k else np.zeros(0, bool)
         other = 0
         is_rec = np.concatenate([valid_k, np.ones(len(u), bool)])
-        if self.shard_world > 1:
+        if self.shard_world > 1 and not self.split_rings:  # split rings: routed by the producers
             mine = shard_owner(d.svcnode, self.shard_world) == self.shard_rank
             drop = is_rec & ~mine
             other = int(drop.sum())

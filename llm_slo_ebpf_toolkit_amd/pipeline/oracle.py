@@ -166,6 +166,9 @@ def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: T
     valid = (r[:, 0] == 16) & ((ev["ctx_type"] & np.uint32(0xFF)) < records.DEF_FIRST)
     d = decode_w16(ev, table, bases)
     d.trace = tmap.hashes(d.trace)
+    if pod_sn:  # the pod's service as the pod table knows it now (not when its context was defined)
+        now = np.array([pod_sn.get(int(p), 0) for p in d.pod.tolist()], dtype=np.uint32)
+        d.svcnode = np.where(now != 0, now, d.svcnode).astype(d.svcnode.dtype)
     hole = ~valid
     for f, z in (("ts", 0), ("val", 0), ("slot", NO_SLOT), ("status", 0), ("pod", 0), ("pid", 0), ("svcnode", 0),
                  ("trace", 0), ("conn", 0)):

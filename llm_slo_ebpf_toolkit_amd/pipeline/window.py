@@ -92,11 +92,14 @@ class WindowPipeline:
                  fanout: int = 3, group_mode: int = 1, learn: bool = True, use_graphs: bool = True,
                  max_ahead: int = 3, n_buffers: int = 3, user_cap: int = USER_CAP, ttft_slo_ms: float = 800.0,
                  halo_ms: float = 0.0, import_cap: int = 0, xchg_cap: int = 0, shard: Tuple[int, int] = (0, 1),
-                 engine: str = "gpu", group=None, model_image: Optional[np.ndarray] = None, halo_windows: int = 3):
+                 engine: str = "gpu", group=None, model_image: Optional[np.ndarray] = None, halo_windows: int = 3,
+                 split_rings: bool = False):
         """``engine``: "gpu" = the native WindowEngine on HIP device ``device`` (``comm`` = its RCCL
         communicator); "cpu" = pipeline.cpu.CpuRingEngine, the same contract on the host, with
         ``group`` (a torch.distributed gloo group) as its communicator. ``shard`` = (rank, world):
-        this engine's share of one node's stream (group sharding, decode.hip shard_owns).
+        this engine's share of one node's stream (group sharding, decode.hip shard_owns);
+        ``split_rings``: the records arrive already routed to this worker's own rings (no record
+        ownership filter; spans keep theirs).
         ``model_image``: a PosteriorModel image to score with (models/export.py) instead of ``model``'s
         built-in initial model."""
         from ..ops.engine import model_bytes
@@ -108,7 +111,8 @@ class WindowPipeline:
         kw = dict(device=device, sig_cap=sig_cap, span_cap=span_cap, group_cap=group_cap, user_cap=user_cap,
                   n_buffers=n_buffers, window_ms=window_ms, threshold=threshold, fanout=fanout, group_mode=group_mode,
                   n_dom=N_DOMAINS, ttft_slo_ms=ttft_slo_ms, halo_ms=halo_ms, import_cap=import_cap, xchg_cap=xchg_cap,
-                  shard_rank=int(shard[0]), shard_world=int(shard[1]), halo_windows=int(halo_windows))
+                  shard_rank=int(shard[0]), shard_world=int(shard[1]), halo_windows=int(halo_windows),
+                  split_rings=bool(split_rings))
         self.engine_kind = engine
         if engine == "cpu":
             from .cpu import CpuRingEngine
@@ -587,3 +591,26 @@ def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim
                                labels=np.asarray(w.group_labels, dtype=np.int32), domains=list(w.group_domains),
                                n_kernel=int(km.sum())))
     return out
+
+
+def build_shard_images(windows, world: int, pods, window_ns: int = 1_000_000_000,
+                       user_rec: int = 64) -> List[List[ReplayImage]]:
+    """Split rings: each replay window as the node's producers would have written it into the
+    workers' ring sets -- kernel and user-space records by their pod's owner, spans by incident
+    group (collector/bpf.py ShardRouter), every ring through its own probe model. Returns, per
+    window, one ReplayImage per worker (the same epoch bases in each)."""
+    import dataclasses
+
+    from ..collector.bpf import ShardRouter
+
+    router = ShardRouter(world)
+    router.set_pods(*pods)
+    per_shard = []
+    for r in range(world):
+        ws = []
+        for w in windows:
+            ev = w.events[router.pod_shard(w.events["pod_id"]) == r]
+            sp = w.spans[router.span_shard(w.spans) == r]
+            ws.append(dataclasses.replace(w, events=np.ascontiguousarray(ev), spans=np.ascontiguousarray(sp)))
+        per_shard.append(build_replay_images(ws, window_ns=window_ns, user_rec=user_rec))
+    return [[per_shard[r][j] for r in range(world)] for j in range(len(windows))]

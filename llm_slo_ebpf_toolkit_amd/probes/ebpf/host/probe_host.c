@@ -6,10 +6,11 @@
  * and the numpy ProbeModel (collector/records.py) record for record.
  *
  *   probe_host IN OUT [--epoch-at IDX:VALUE]... [--trace-next N] [--ctx-next N]
- *                     [--floor TYPE:VALUE]... [--ring-cap RECORDS]
+ *                     [--floor TYPE:VALUE]... [--ring-cap RECORDS] [--shard POD:SHARD]...
  *
  * --epoch-at publishes mislo_cfg[124] = VALUE before input record IDX (the agent's window
- * cut); --ring-cap makes bpf_ringbuf_output fail once that many records are out (a full ring). */
+ * cut); --ring-cap makes bpf_ringbuf_output fail once that many records are out (a full ring);
+ * --shard routes a pod's records to split ring SHARD (mislo_shards), written to OUT.SHARD. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -24,10 +25,11 @@ struct hmap {
 	unsigned char *used;
 };
 
-static struct hmap traces_m, ctxs_m, pods_m;
+static struct hmap traces_m, ctxs_m, pods_m, shards_m;
 static __u64 cfg_m[MISLO_CFG_SLOTS];
 static struct mislo_event scratch_m;
-static FILE *ring_out;
+static FILE *ring_out, *shard_out[MISLO_SHARDS];
+static const char *out_path;
 static unsigned long long ring_n, ring_cap = ~0ull;
 
 static void hmap_init(struct hmap *m, unsigned key_size, unsigned cap)
@@ -68,6 +70,8 @@ static struct hmap *hmap_of(void *map)
 		return &ctxs_m;
 	if (map == (void *)&mislo_pods)
 		return &pods_m;
+	if (map == (void *)&mislo_shards)
+		return &shards_m;
 	return 0;
 }
 
@@ -103,14 +107,55 @@ long bpf_map_update_elem(void *map, const void *key, const void *value, __u64 fl
 	return 0;
 }
 
+static int shard_of_ring(void *ringbuf)
+{
+	if (ringbuf == (void *)&mislo_events)
+		return 0;
+#if MISLO_SHARDS > 1
+	if (ringbuf == (void *)&mislo_events1)
+		return 1;
+#endif
+#if MISLO_SHARDS > 2
+	if (ringbuf == (void *)&mislo_events2)
+		return 2;
+#endif
+#if MISLO_SHARDS > 3
+	if (ringbuf == (void *)&mislo_events3)
+		return 3;
+#endif
+#if MISLO_SHARDS > 4
+	if (ringbuf == (void *)&mislo_events4)
+		return 4;
+	if (ringbuf == (void *)&mislo_events5)
+		return 5;
+	if (ringbuf == (void *)&mislo_events6)
+		return 6;
+	if (ringbuf == (void *)&mislo_events7)
+		return 7;
+#endif
+	return -1;
+}
+
 long bpf_ringbuf_output(void *ringbuf, void *data, __u64 size, __u64 flags)
 {
 	(void)flags;
-	if (ringbuf != (void *)&mislo_events || size != 16)
+	int s = shard_of_ring(ringbuf);
+	if (s < 0 || size != 16)
 		return -22;
 	if (ring_n >= ring_cap)
 		return -11; /* -EAGAIN: ring full */
-	if (fwrite(data, 16, 1, ring_out) != 1)
+	FILE *f = ring_out;
+	if (s > 0) {
+		if (!shard_out[s]) {
+			char p[4096];
+			snprintf(p, sizeof(p), "%s.%d", out_path, s);
+			shard_out[s] = fopen(p, "wb");
+			if (!shard_out[s])
+				return -5;
+		}
+		f = shard_out[s];
+	}
+	if (fwrite(data, 16, 1, f) != 1)
 		return -5;
 	++ring_n;
 	return 0;
@@ -146,15 +191,24 @@ int main(int argc, char **argv)
 			cfg_m[MISLO_CFG_FLOOR(a)] = b;
 		else if (!strcmp(argv[i], "--ring-cap"))
 			ring_cap = strtoull(argv[i + 1], 0, 0);
+		else if (!strcmp(argv[i], "--shard") && sscanf(argv[i + 1], "%llu:%llu", &a, &b) == 2) {
+			if (!shards_m.cap)
+				hmap_init(&shards_m, 4, 1u << 16);
+			__u32 pod = (__u32)a, sh = (__u32)b;
+			bpf_map_update_elem(&mislo_shards, &pod, &sh, BPF_ANY);
+		}
 		else {
 			fprintf(stderr, "bad option %s\n", argv[i]);
 			return 2;
 		}
 	}
+	if (!shards_m.cap)
+		hmap_init(&shards_m, 4, 1u << 16);
 	hmap_init(&traces_m, 8, 1u << 22);
 	hmap_init(&ctxs_m, sizeof(struct mislo_ctx_key), 1u << 22);
 	hmap_init(&pods_m, 8, 1u << 16);
 	FILE *in = fopen(argv[1], "rb");
+	out_path = argv[2];
 	ring_out = fopen(argv[2], "wb");
 	if (!in || !ring_out) {
 		perror("open");
@@ -175,6 +229,9 @@ int main(int argc, char **argv)
 	}
 	fclose(in);
 	fclose(ring_out);
+	for (int s = 1; s < MISLO_SHARDS; ++s)
+		if (shard_out[s])
+			fclose(shard_out[s]);
 	printf("events %llu records %llu trace_next %llu ctx_next %llu\n", n, ring_n,
 	       (unsigned long long)cfg_m[MISLO_CFG_TRACE_NEXT], (unsigned long long)cfg_m[MISLO_CFG_CTX_NEXT]);
 	return 0;

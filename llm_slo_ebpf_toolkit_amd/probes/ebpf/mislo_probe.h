@@ -68,6 +68,43 @@ struct {
 	__uint(pinning, LIBBPF_PIN_BY_NAME);
 } mislo_events SEC(".maps");
 
+/* Split rings (agent --gpus N): shard s >= 1 has its own ring buffer, so each window worker DMAs
+ * only its share of the node's records. MISLO_SHARDS rings in all (compile-time: the ring maps
+ * are created when the object loads); a pod's shard is in mislo_shards (agent-written: the
+ * worker owning the pod's service), pods not in it use ring 0. */
+#ifndef MISLO_SHARDS
+#define MISLO_SHARDS 8
+#endif
+#define MISLO_SHARD_RING(n)                                   \
+	struct {                                              \
+		__uint(type, BPF_MAP_TYPE_RINGBUF);           \
+		__uint(max_entries, 16 * 1024 * 1024);        \
+		__uint(pinning, LIBBPF_PIN_BY_NAME);          \
+	} mislo_events##n SEC(".maps");
+#if MISLO_SHARDS > 1
+MISLO_SHARD_RING(1)
+#endif
+#if MISLO_SHARDS > 2
+MISLO_SHARD_RING(2)
+#endif
+#if MISLO_SHARDS > 3
+MISLO_SHARD_RING(3)
+#endif
+#if MISLO_SHARDS > 4
+MISLO_SHARD_RING(4)
+MISLO_SHARD_RING(5)
+MISLO_SHARD_RING(6)
+MISLO_SHARD_RING(7)
+#endif
+
+struct {
+	__uint(type, BPF_MAP_TYPE_HASH);
+	__uint(max_entries, 65536);
+	__type(key, __u32);   /* pod id */
+	__type(value, __u32); /* shard: the ring of the window worker that owns the pod's service */
+	__uint(pinning, LIBBPF_PIN_BY_NAME);
+} mislo_shards SEC(".maps");
+
 struct {
 	__uint(type, BPF_MAP_TYPE_ARRAY);
 	__uint(max_entries, MISLO_CFG_SLOTS);
@@ -193,9 +230,41 @@ static __always_inline __u64 mislo_conn_key(const struct mislo_event *e)
 
 /* Put a 16-byte record on the ring. No wakeup: the agent reads the ring at its window cuts,
  * never from epoll, so a per-record consumer wakeup would be pure overhead. 0 = written. */
-static __always_inline long mislo_out(const void *r)
+static __always_inline long mislo_out(const void *r, __u32 shard)
 {
-	return bpf_ringbuf_output(&mislo_events, (void *)r, 16, BPF_RB_NO_WAKEUP);
+	switch (shard) {
+#if MISLO_SHARDS > 1
+	case 1:
+		return bpf_ringbuf_output(&mislo_events1, (void *)r, 16, BPF_RB_NO_WAKEUP);
+#endif
+#if MISLO_SHARDS > 2
+	case 2:
+		return bpf_ringbuf_output(&mislo_events2, (void *)r, 16, BPF_RB_NO_WAKEUP);
+#endif
+#if MISLO_SHARDS > 3
+	case 3:
+		return bpf_ringbuf_output(&mislo_events3, (void *)r, 16, BPF_RB_NO_WAKEUP);
+#endif
+#if MISLO_SHARDS > 4
+	case 4:
+		return bpf_ringbuf_output(&mislo_events4, (void *)r, 16, BPF_RB_NO_WAKEUP);
+	case 5:
+		return bpf_ringbuf_output(&mislo_events5, (void *)r, 16, BPF_RB_NO_WAKEUP);
+	case 6:
+		return bpf_ringbuf_output(&mislo_events6, (void *)r, 16, BPF_RB_NO_WAKEUP);
+	case 7:
+		return bpf_ringbuf_output(&mislo_events7, (void *)r, 16, BPF_RB_NO_WAKEUP);
+#endif
+	default:
+		return bpf_ringbuf_output(&mislo_events, (void *)r, 16, BPF_RB_NO_WAKEUP);
+	}
+}
+
+/* the shard (ring) of a pod's records: 0 unless the agent routed the pod elsewhere */
+static __always_inline __u32 mislo_shard(__u32 pod_id)
+{
+	__u32 *s = pod_id ? bpf_map_lookup_elem(&mislo_shards, &pod_id) : 0;
+	return s && *s < MISLO_SHARDS ? *s : 0;
 }
 
 /* (pod, pid, connection) -> context id, assigned on first sight from counter [126]: the
@@ -203,11 +272,12 @@ static __always_inline long mislo_out(const void *r)
  * define an id; BPF_NOEXIST lets one win and the other re-reads the winner (the loser's
  * definition names an id nothing uses). An exhausted id space yields 0 until the agent
  * resets the map; the all-zero context is id 0 without a map entry. */
-static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32)
+static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32, __u32 shard)
 {
 	if (!pod_id && !pid && !c32)
 		return 0;
-	struct mislo_ctx_key k = {.pod_id = pod_id, .pid = pid, .conn32 = c32, .pad = 0};
+	/* keyed per shard: a context is defined on every ring its records go to */
+	struct mislo_ctx_key k = {.pod_id = pod_id, .pid = pid, .conn32 = c32, .pad = shard};
 	__u32 *id = bpf_map_lookup_elem(&mislo_ctxs, &k);
 	if (id)
 		return *id;
@@ -220,7 +290,7 @@ static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32)
 		return 0;
 	__u32 v = (__u32)fresh;
 	struct mislo_def16 d = {.a = c32, .tag_id = MISLO_DEF_CTX | (v << 8), .b = pod_id, .c = pid};
-	if (mislo_out(&d))
+	if (mislo_out(&d, shard))
 		return 0; /* ring full: leave the context unnamed */
 	if (bpf_map_update_elem(&mislo_ctxs, &k, &v, BPF_NOEXIST) == 0)
 		return v;
@@ -230,11 +300,14 @@ static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32)
 
 /* trace hash -> trace id in 1 .. 2^24 - 1 (wrapping), definition first like mislo_ctx_id;
  * 0 for untraced events */
-static __always_inline __u32 mislo_trace_id(__u64 h)
+static __always_inline __u32 mislo_trace_id(__u64 h, __u32 shard)
 {
 	if (!h)
 		return 0;
-	__u32 *id = bpf_map_lookup_elem(&mislo_traces, &h);
+	/* keyed per shard too (the shard folded into the hash's top bits): every ring defines the
+	 * trace ids its records use */
+	__u64 key = h ^ ((__u64)shard << 58);
+	__u32 *id = bpf_map_lookup_elem(&mislo_traces, &key);
 	if (id)
 		return *id;
 	__u32 idx = MISLO_CFG_TRACE_NEXT;
@@ -243,11 +316,11 @@ static __always_inline __u32 mislo_trace_id(__u64 h)
 		return 0;
 	__u32 v = mislo_trace_slot(__sync_fetch_and_add(next, 1));
 	struct mislo_def16 d = {.a = v, .tag_id = MISLO_DEF_TRACE, .b = (__u32)h, .c = (__u32)(h >> 32)};
-	if (mislo_out(&d))
+	if (mislo_out(&d, shard))
 		return 0;
-	if (bpf_map_update_elem(&mislo_traces, &h, &v, BPF_NOEXIST) == 0)
+	if (bpf_map_update_elem(&mislo_traces, &key, &v, BPF_NOEXIST) == 0)
 		return v;
-	id = bpf_map_lookup_elem(&mislo_traces, &h);
+	id = bpf_map_lookup_elem(&mislo_traces, &key);
 	return id ? *id : 0;
 }
 
@@ -256,8 +329,9 @@ static __always_inline __u32 mislo_trace_id(__u64 h)
 static __always_inline void mislo_submit(struct mislo_event *e)
 {
 	struct mislo_event16 r;
-	__u32 ctx = mislo_ctx_id(e->pod_id, e->pid, mislo_conn32(mislo_conn_key(e)));
-	__u32 tid = mislo_trace_id(e->trace_h);
+	__u32 shard = mislo_shard(e->pod_id);
+	__u32 ctx = mislo_ctx_id(e->pod_id, e->pid, mislo_conn32(mislo_conn_key(e)), shard);
+	__u32 tid = mislo_trace_id(e->trace_h, shard);
 	__u32 eidx = MISLO_CFG_EPOCH;
 	__u64 *ep = bpf_map_lookup_elem(&mislo_cfg, &eidx);
 	__u64 epoch = ep ? *ep : 0;
@@ -271,7 +345,7 @@ static __always_inline void mislo_submit(struct mislo_event *e)
 	r.ctx_type = (e->signal_type & 0xFFu) | (ctx << 8);
 	r.value_milli = mislo_milli(e->signal_type, e->value);
 	r.trace_tag = (tid & MISLO_TRACE_ID_MASK) | ((__u32)(epoch & 3) << MISLO_EPOCH_TAG_SHIFT);
-	mislo_out(&r);
+	mislo_out(&r, shard);
 }
 
 /* Emit a record attributed to the current task. */

@@ -37,6 +37,11 @@
 // receiver's rule), so the agent joins them to the request's spans through the trace tier
 // instead of the coarser pod+pid window.
 //
+// Split rings (agent --gpus N): MISLO_RING may list one ring per window worker ("a,b,..."); the
+// records go to the ring of the worker that owns this process's pod, read from the agent's
+// shared-memory pod -> shard table (MISLO_SHARD_TABLE, one byte per pod id; re-read every sample
+// tick, so a pod the agent routes later follows). Without a table, the first ring.
+//
 // Shedding: the agent's overhead guard sets bits in the ring header's drop mask (runtime/csrc/ring.h);
 // a record whose signal type's bit is set is not emitted (counted as dropped).
 //
@@ -59,11 +64,14 @@
 #include <rocprofiler-sdk/rocprofiler.h>
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <vector>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -122,7 +130,9 @@ struct State {
   rocprofiler_client_id_t* client = nullptr;
   rocprofiler_context_id_t ctx{};
   rocprofiler_buffer_id_t buffer{};
-  void* ring = nullptr;
+  void* ring = nullptr;                // the ring records go to now (rings[shard])
+  std::vector<void*> rings;            // MISLO_RING's rings, one per window worker
+  const uint8_t* shard_table = nullptr;  // pod id -> shard (MISLO_SHARD_TABLE), 2^20 bytes
   int64_t clock_offset = 0;  // realtime - rocprofiler timestamp
   uint32_t pod = 0;
   uint16_t node = 0, svc = 0;
@@ -154,9 +164,12 @@ struct State {
   struct Busy {
     int metrics_fd = -1, busy_fd = -1;
     bool acc = false;           // gpu_metrics carries gfx_activity_acc at byte 76 (format 1.7 / 1.8)
-    uint64_t own_ns = 0, own_last_end = 0;
-    uint32_t last_acc = 0;
-    uint64_t last_t = 0;        // rocprofiler ns of the last reading (0: not primed)
+    // this process's kernels' [start, end] as their completions arrive (any order: completion
+    // callbacks run on several threads), kept until no later interval can overlap them
+    std::vector<std::pair<uint64_t, uint64_t>> iv;
+    uint64_t t_p = 0, t_pp = 0;   // the last two readings' times (rocprofiler ns; 0 = none)
+    uint32_t acc_p = 0, acc_pp = 0;
+    double busy_p = 0.0;          // gpu_busy_percent at the last reading (no accumulator)
     double dev_pct = 0.0, own_pct = 0.0;  // last interval (tests)
     uint64_t intervals = 0;
   };
@@ -305,46 +318,63 @@ uint64_t xgmi_latency(uint64_t src, uint64_t dst, uint64_t bytes, uint64_t dur) 
   return dur > xfer ? dur - xfer : 0;
 }
 
-// The device's GFX activity over (last reading, now] in percent: the gpu_metrics accumulator
-// (percent x ms, exact over any interval) or, without it, the driver's smoothed busy percent.
-bool device_busy_pct(State::Busy& b, uint64_t now, double* pct) {
+// One reading of the device's GFX activity: the gpu_metrics accumulator (percent x ms, exact
+// over any interval) or, without it, the driver's smoothed busy percent.
+bool read_activity(State::Busy& b, uint32_t* acc, double* busy) {
   char buf[96];
   if (b.acc) {
     if (pread(b.metrics_fd, buf, sizeof(buf), 0) < 80) return false;
-    uint32_t acc;
-    std::memcpy(&acc, buf + 76, 4);
-    const bool primed = b.last_t != 0;
-    const uint64_t dt = now - b.last_t;
-    const uint32_t d = acc - b.last_acc;
-    b.last_acc = acc;
-    if (!primed || dt == 0) return false;
-    *pct = (double)d * 1e6 / (double)dt;  // (percent x ms) per ms
+    std::memcpy(acc, buf + 76, 4);
     return true;
   }
   if (b.busy_fd < 0) return false;
   const ssize_t n = pread(b.busy_fd, buf, sizeof(buf) - 1, 0);
   if (n <= 0) return false;
   buf[n] = 0;
-  *pct = std::strtod(buf, nullptr);
-  return b.last_t != 0;
+  *busy = std::strtod(buf, nullptr);
+  return true;
 }
 
-// Every foreign_ms: per GPU this process has run kernels on, the GPU time others held.
+// Every foreign_ms, per GPU this process has run kernels on: the GPU time others held over the
+// PREVIOUS interval [t_pp, t_p] (one interval of lag: by now every completion callback of a kernel
+// that ended in it has arrived). Own time is the union of this process's kernel intervals clipped
+// to it (overlapping streams count once), device time the accumulator's growth over it.
 void foreign_tick(uint64_t now) {
   for (auto& kv : g.busy) {
     State::Busy& b = kv.second;
-    if (b.metrics_fd < 0 && b.busy_fd < 0) continue;
-    double dev = 0.0;
-    const bool ok = device_busy_pct(b, now, &dev);
-    const uint64_t dt = b.last_t ? now - b.last_t : 0;
-    b.last_t = now;
-    uint64_t own;
+    uint32_t acc = 0;
+    double busy = 0.0;
+    if (!read_activity(b, &acc, &busy)) continue;
+    const uint64_t lo = b.t_pp, hi = b.t_p;
+    const uint32_t dacc = b.acc_p - b.acc_pp;
+    const double busy_w = b.busy_p;
+    b.t_pp = b.t_p, b.acc_pp = b.acc_p;
+    b.t_p = now, b.acc_p = acc, b.busy_p = busy;
+    std::vector<std::pair<uint64_t, uint64_t>> iv;
     {
       std::lock_guard<std::mutex> lk(g.mu);
-      own = b.own_ns;
-      b.own_ns = 0;
+      iv.swap(b.iv);
+      // keep what a later window [hi, ...] can still overlap
+      for (const auto& x : iv)
+        if (x.second > hi) b.iv.push_back(x);
+      if (b.iv.size() > 262144) b.iv.clear();  // no ticks for a long time: start afresh
     }
-    if (!ok || dt == 0) continue;
+    if (!lo || hi <= lo) continue;
+    std::sort(iv.begin(), iv.end());
+    uint64_t own = 0, cur_s = 0, cur_e = 0;
+    for (const auto& x : iv) {
+      const uint64_t s = x.first < lo ? lo : x.first, e = x.second > hi ? hi : x.second;
+      if (e <= s) continue;
+      if (s > cur_e) {
+        own += cur_e - cur_s;
+        cur_s = s, cur_e = e;
+      } else if (e > cur_e) {
+        cur_e = e;
+      }
+    }
+    own += cur_e - cur_s;
+    const uint64_t dt = hi - lo;
+    double dev = b.acc ? (double)dacc * 1e6 / (double)dt : busy_w;  // (percent x ms) per ms
     double own_pct = 100.0 * (double)own / (double)dt;
     if (own_pct > 100.0) own_pct = 100.0;
     if (dev > 100.0) dev = 100.0;
@@ -352,8 +382,16 @@ void foreign_tick(uint64_t now) {
     ++b.intervals;
     const double foreign = dev - own_pct;
     if (own_pct >= (double)g.foreign_min_own_pct && foreign >= (double)g.foreign_floor_pct)
-      emit(kQueueDelay, now - dt / 2, (uint64_t)(foreign / 100.0 * (double)dt), 0);
+      emit(kQueueDelay, lo + dt / 2, (uint64_t)(foreign / 100.0 * (double)dt), 0);
   }
+}
+
+// Follow the agent's routing of this process's pod (split rings).
+void route() {
+  if (!g.shard_table || g.rings.size() < 2) return;
+  const uint8_t s = g.shard_table[g.pod & 0xFFFFFu];
+  void* r = g.rings[s < g.rings.size() ? s : 0];
+  if (r) g.ring = r;
 }
 
 void sampler_main() {
@@ -364,6 +402,7 @@ void sampler_main() {
   while (!g.scv.wait_for(lk, std::chrono::milliseconds(tick), [] { return g.stop; })) {
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
+    route();
     if (g.hbm_sample_ms && now >= next_hbm) {
       next_hbm = now + g.hbm_sample_ms * 1000000ull - 500000ull;
       for (auto& kv : g.vram)
@@ -450,13 +489,10 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     bool known = true;
     {
       std::lock_guard<std::mutex> lk(g.mu);
-      // this process's kernel time on the device (union: dispatches complete in order per queue)
+      // this process's kernel time on the device (merged into a union at the next tick)
       auto bi = g.busy.find(d->dispatch_info.agent_id.handle);
-      if (bi != g.busy.end() && d->end_timestamp > bi->second.own_last_end) {
-        const uint64_t from = d->start_timestamp > bi->second.own_last_end ? d->start_timestamp : bi->second.own_last_end;
-        bi->second.own_ns += d->end_timestamp - from;
-        bi->second.own_last_end = d->end_timestamp;
-      }
+      if (bi != g.busy.end() && d->end_timestamp > d->start_timestamp)
+        bi->second.iv.emplace_back(d->start_timestamp, d->end_timestamp);
       if (g.disp_end.size() > 65536) g.disp_end.clear();  // ends whose successor never completed
       g.disp_end[d->dispatch_info.dispatch_id] = d->end_timestamp;
       if (enq.pred) {
@@ -530,10 +566,29 @@ void buffer_callback(rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofi
 int tool_init(rocprofiler_client_finalize_t, void*) {
   bool ok = true;
   const char* name = std::getenv("MISLO_RING");
-  g.ring = mislo_ring_open_shm(name && *name ? name : "/mislo-agent-events");
+  {
+    const std::string list = name && *name ? name : "/mislo-agent-events";
+    size_t a = 0;
+    while (a <= list.size()) {
+      size_t b = list.find(',', a);
+      if (b == std::string::npos) b = list.size();
+      if (b > a) g.rings.push_back(mislo_ring_open_shm(list.substr(a, b - a).c_str()));
+      a = b + 1;
+    }
+    g.ring = g.rings.empty() ? nullptr : g.rings[0];
+    if (const char* t = std::getenv("MISLO_SHARD_TABLE")) {
+      const int fd = shm_open(t, O_RDONLY, 0);
+      if (fd >= 0) {
+        void* m = mmap(nullptr, 1u << 20, PROT_READ, MAP_SHARED, fd, 0);
+        close(fd);
+        if (m != MAP_FAILED) g.shard_table = static_cast<const uint8_t*>(m);
+      }
+    }
+  }
   g.rec32 = g.ring && mislo_ring_rec_size(g.ring) == 32;
   g.rec24 = g.ring && mislo_ring_rec_size(g.ring) == 24;
   g.pod = (uint32_t)env_u64("MISLO_POD_ID", 0);
+  route();
   g.node = (uint16_t)env_u64("MISLO_NODE_ID", 0);
   g.svc = (uint16_t)env_u64("MISLO_SVC_ID", 0);
   g.hbm_bytes = env_u64("MISLO_HBM_BYTES", 288ull << 30);
@@ -597,7 +652,9 @@ void tool_fini(void*) {
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] pushed=%llu dropped=%llu\n", (unsigned long long)g.pushed.load(),
                  (unsigned long long)g.dropped.load());
-  if (g.ring) mislo_ring_close(g.ring);
+  for (void* r : g.rings)
+    if (r) mislo_ring_close(r);
+  g.rings.clear();
   g.ring = nullptr;
 }
 

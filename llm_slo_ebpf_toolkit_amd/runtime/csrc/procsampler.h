@@ -45,7 +45,7 @@ struct ProcSamplerConfig {
   std::string cgroup_root = "/sys/fs/cgroup";
   uint32_t node_id = 0;
   uint64_t runq_floor_ns = 100000;    // runqueue_delay.bpf.c emit floor (100 us per timeslice)
-  uint64_t steal_floor_milli = 1000;  // 1 % of one CPU over the interval
+  uint64_t steal_floor_milli = 20000; // 20 % of one CPU over the interval (collector/procfs.py STEAL_FLOOR_MILLI)
   uint64_t cfs_floor_ns = 100000;
   uint64_t mem_floor_ns = 100000;
   bool cgroup_cpu_psi = false;        // cpu_steal_pct = max(wait share, the group's cpu.pressure share)

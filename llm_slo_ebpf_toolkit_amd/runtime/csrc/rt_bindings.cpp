@@ -680,7 +680,7 @@ PYBIND11_MODULE(_mislo_rt, m) {
                     uint64_t>(),
            py::arg("ring"), py::arg("node_id") = 0, py::arg("proc_root") = "/proc",
            py::arg("cgroup_root") = "/sys/fs/cgroup", py::arg("cgroup_cpu_psi") = false,
-           py::arg("runq_floor_ns") = 100000, py::arg("steal_floor_milli") = 1000, py::arg("cfs_floor_ns") = 100000,
+           py::arg("runq_floor_ns") = 100000, py::arg("steal_floor_milli") = 20000, py::arg("cfs_floor_ns") = 100000,
            py::arg("mem_floor_ns") = 100000, py::keep_alive<1, 2>())
       .def("set_targets", &PyProcSampler::set_targets)
       .def("set_target_list", &PyProcSampler::set_target_list)

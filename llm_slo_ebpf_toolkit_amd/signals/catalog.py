@@ -66,7 +66,9 @@ SIGNALS: Tuple[SignalSpec, ...] = (
     SignalSpec("tls_handshake_ms", 5, "ms", 5, 1e-6, 60, 160, 60, "llm.ebpf.tls.handshake_ms", 3, True, buckets=_MS_BUCKETS),
     SignalSpec("tls_handshake_fail_total", 6, "count", 11, 1.0, 1, 3, 1, "llm.ebpf.tls.handshake_fail_total", 14, False, buckets=_COUNT_BUCKETS),
     SignalSpec("cpu_steal_pct", 7, "pct", 6, 1e-3, 2, 8, 2, "llm.ebpf.cpu.steal_pct", 9, True, buckets=_PCT_BUCKETS),
-    SignalSpec("cfs_throttled_ms", 8, "ms", 12, 1e-6, 40, 120, 40, "llm.ebpf.cpu.cfs_throttled_ms", 12, False, buckets=_MS_BUCKETS),
+    # in the config enum (NEW, additive: REF's enum omits it although its generator and Bayes
+    # table use it; cfs_throttle.bpf.c and the procfs sampler produce it here)
+    SignalSpec("cfs_throttled_ms", 8, "ms", 12, 1e-6, 40, 120, 40, "llm.ebpf.cpu.cfs_throttled_ms", 12, True, buckets=_MS_BUCKETS),
     SignalSpec("mem_reclaim_latency_ms", 9, "ms", 7, 1e-6, 5, 20, 5, "llm.ebpf.mm.reclaim_latency_ms", 8, True, buckets=_MS_BUCKETS),
     SignalSpec("disk_io_latency_ms", 10, "ms", 8, 1e-6, 10, 50, 10, "llm.ebpf.blk.io_latency_ms", 6, True, buckets=_MS_BUCKETS),
     SignalSpec("syscall_latency_ms", 11, "ms", 9, 1e-6, 50, 200, 50, "llm.ebpf.syscall.latency_ms", 4, True, buckets=_MS_BUCKETS),
@@ -106,6 +108,9 @@ DEFAULT_CONFIG_SIGNALS: Tuple[str, ...] = (
     "tls_handshake_ms", "cpu_steal_pct", "mem_reclaim_latency_ms", "disk_io_latency_ms",
     "syscall_latency_ms",
 )
+# What the shipped DaemonSet / Helm chart enable: REF's nine, CFS throttling (REF's cpu_throttle
+# profile signal) and the four GPU signals (deploy/k8s/configmap.yaml, charts/llm-slo-agent).
+DEPLOY_SIGNALS: Tuple[str, ...] = DEFAULT_CONFIG_SIGNALS + ("cfs_throttled_ms",) + GPU_SIGNALS
 # The REF 12-signal shed order (constants.go:46-59). NEW inserts the GPU probes by cost:
 # per-dispatch uprobes first, polled counters last.
 REF_DISABLE_ORDER: Tuple[str, ...] = (

@@ -74,7 +74,7 @@ def _check(args):
     assert not smoke
     assert isinstance(opts, AgentOptions)
     assert opts.engine == "gpu" and opts.source == "bpf", (opts.engine, opts.source)
-    assert opts.gpus == 0  # every GPU of the node
+    assert opts.gpus == 1  # one worker on one GPU; node-wide multi-GPU fusion is opt-in
     assert opts.model_path.endswith(SHIPPED_MODEL.split("/", 1)[1])
     assert opts.otlp_receiver_bind.endswith(":4318") and opts.otlp_receiver_allow
     a = Agent(AgentOptions(**{**opts.__dict__, "config": os.path.join(ROOT, "config", "toolkit.yaml"),
@@ -95,7 +95,72 @@ def test_kustomize_daemonset_args_start_the_agent():
     args, c = render_kustomize_args()
     _check(args)
     names = {e["name"] for e in c.get("env", [])}
-    assert "HIP_VISIBLE_DEVICES" not in names  # the agent uses every GPU of the node
+    assert "HIP_VISIBLE_DEVICES" not in names  # the worker picks its GPU itself
+
+
+# measured: the agent with one worker at 1M events/s, profiles/r3_agent_overhead_1Mevs.json (787 MB);
+# the HIP runtime's floor per worker process at one hardware queue (docs/BENCHMARKS.md, 465 MB)
+AGENT_ONE_WORKER_MB, WORKER_FLOOR_MB, MI355X_NODE_GPUS = 787, 465, 8
+
+
+def _mib(q: str) -> float:
+    q = str(q)
+    for suf, f in (("Gi", 1024.0), ("Mi", 1.0), ("G", 1000 ** 3 / 2 ** 20), ("M", 1000 ** 2 / 2 ** 20)):
+        if q.endswith(suf):
+            return float(q[: -len(suf)]) * f
+    return float(q) / 2 ** 20
+
+
+def _cores(q: str) -> float:
+    q = str(q)
+    return float(q[:-1]) / 1000 if q.endswith("m") else float(q)
+
+
+def _sized(gpus: int, limits: dict) -> None:
+    workers = gpus if gpus > 0 else MI355X_NODE_GPUS
+    need = AGENT_ONE_WORKER_MB + (workers - 1) * WORKER_FLOOR_MB
+    assert _mib(limits["memory"]) * 1.048576 >= need, (limits, workers, need)  # MiB -> MB
+    assert _cores(limits["cpu"]) >= 0.5 * workers, (limits, workers)
+
+
+def test_shipped_resources_fit_the_workers_they_start():
+    """the memory limit must hold every worker the args start (each carries
+    the HIP runtime's resident floor) and the CPU limit must not be shared by N workers."""
+    args, values = render_chart_args()
+    _sized(int(values["agent"]["gpus"]), values["resources"]["limits"])
+    kargs, c = render_kustomize_args()
+    g = int(next(a.split("=", 1)[1] for a in kargs if a.startswith("--gpus=")))
+    _sized(g, c["resources"]["limits"])
+
+
+def test_shipped_signal_set_loads_the_gpu_and_cfs_probes():
+    """the shipped config enables the GPU signals and CFS throttling, so the
+    loader's probe specs include gpu_kfd.bpf.o (and the HIP uprobes in it) and cfs_throttle.bpf.o."""
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import choose_enabled_signals
+    from llm_slo_ebpf_toolkit_amd.collector import loader
+    from llm_slo_ebpf_toolkit_amd.contracts import config as toolkitcfg
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    docs = {}
+    with open(os.path.join(ROOT, "deploy/k8s/configmap.yaml")) as fh:
+        for d in yaml.safe_load_all(fh):
+            docs[d["kind"]] = d
+    sets = [yaml.safe_load(docs["ConfigMap"]["data"]["toolkit.yaml"])["signal_set"]]
+    with open(os.path.join(ROOT, "charts/llm-slo-agent/values.yaml")) as fh:
+        sets.append(yaml.safe_load(fh)["config"]["signal_set"])
+
+    class AllObjects(loader.BpfProbeLoader):
+        def available(self):
+            return list(loader.PROBE_SIGNALS)
+
+    for sig in sets:
+        assert set(catalog.DEPLOY_SIGNALS) <= set(sig), sig
+        cfg = toolkitcfg.default()
+        cfg.signal_set = sig
+        enabled = choose_enabled_signals(cfg.signal_set, [], catalog.supported_signals_for_mode(catalog.MODE_GPU))
+        specs = loader.probe_specs(AllObjects("/nonexistent"), enabled)
+        loaded = {s.signal for s in specs}
+        assert {"gpu_queue_delay_ms", "rccl_collective_ms", "cfs_throttled_ms"} <= loaded, loaded
 
 
 def test_helm_test_pod_checks_the_agent_endpoints():

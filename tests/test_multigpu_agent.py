@@ -69,19 +69,21 @@ def _windows(n_win=3, seed=11):
     return wins, build_replay_images(wins, user_rec=24), (g.pod_ids.astype(np.uint32), sn)
 
 
-def _spec(r, world, tag, pods, port=0, engine="cpu", device=0):
+def _spec(r, world, tag, pods, port=0, engine="cpu", device=0, halo_ms=2000.0, split=False):
     from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerSpec, groups_of
     from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
     from llm_slo_ebpf_toolkit_amd.ops.engine import model_bytes
 
     return WorkerSpec(rank=r, world=world, device=device, engine=engine, source="shm", ring_name=tag, pin_dir="",
                       user_rec=24, sig_cap=8192, span_cap=512, group_cap=groups_of(0, world, 8), user_cap=4096,
-                      window_ms=1000.0, ttft_slo_ms=800.0, halo_ms=2000.0, import_cap=16384,
+                      window_ms=1000.0, ttft_slo_ms=800.0, halo_ms=halo_ms, import_cap=16384,
                       xchg_cap=512 if world > 1 else 0, model_image=model_bytes(NaiveBayes.ref()).tobytes(),
-                      pods=pods, master=("127.0.0.1", port))
+                      pods=pods, master=("127.0.0.1", port), split=split)
 
 
-def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22, engine="cpu"):
+def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22, engine="cpu", late_pods=None, halo_ms=2000.0):
+    """``late_pods`` (window index, (pod ids, svc|node)): the pod table arrives at that window's
+    cut, as the OTLP receiver's first spans of the pods would deliver it."""
     import socket
 
     from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerPool, merge_results
@@ -94,15 +96,17 @@ def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22, engine="cpu"):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    pool = WorkerPool([_spec(r, world, tag, pods, port, engine, r if engine == "gpu" else 0) for r in range(world)],
+    pool = WorkerPool([_spec(r, world, tag, pods, port, engine, r if engine == "gpu" else 0, halo_ms)
+                       for r in range(world)],
                       (ring, user, spans), in_process=world == 1 and engine == "cpu")
     out = []
     try:
         replies = []
-        for img in imgs:
+        for j, img in enumerate(imgs):
             assert ring.append_framed(img.framed)
             assert user.push(img.user) == len(img.user) and spans.push(img.spans) == len(img.spans)
-            replies.append(pool.window(Cut(ring.producer_pos, user.head, spans.head, img.bases), 8))
+            upd = late_pods[1] if late_pods is not None and late_pods[0] == j else None
+            replies.append(pool.window(Cut(ring.producer_pos, user.head, spans.head, img.bases), 8, upd))
         replies.append(pool.stop())
         for rep in replies[1:]:
             prev = [r["prev"] for r in rep]
@@ -136,6 +140,88 @@ def test_two_cpu_workers_reproduce_the_single_process_window():
         assert (a["res"]["sli"][:, 0] > 0).all()
 
 
+@pytest.mark.timeout(300)
+def test_pods_learned_after_their_contexts_were_defined_shard_like_one_process():
+    """on a bpf source the pod -> service table fills only once the OTLP
+    receiver sees a pod's spans, after the kernel defined the pod's contexts. Sharding must use
+    the service the pod table holds when a record is decoded, not the one stored with its context
+    at definition time (svc 0, which kept every such record on GPU 0 and left the other GPUs'
+    services without them). Pods arrive at window 1's cut; from then on two workers equal one."""
+    wins, imgs, pods = _windows(n_win=4)
+    tag = f"/mislo-late-{os.getpid()}"
+    one = _run_pool(1, imgs, None, tag + "-a", late_pods=(1, pods), halo_ms=0.0)
+    two = _run_pool(2, imgs, None, tag + "-b", late_pods=(1, pods), halo_ms=0.0)
+    for j in range(1, len(imgs)):
+        a, b = one[j], two[j]
+        for key in ("feat", "pred", "sli"):
+            np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
+        assert a["events"] == b["events"] > 0
+
+
+def _run_split(world, shard_imgs, pods, tag, ring_bytes=1 << 22, engine="cpu"):
+    """``agent --gpus N`` on split rings: worker r's own ring set holds only the records and
+    spans of the services it owns (what the node's producers write through ShardRouter)."""
+    import socket
+
+    from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerPool, merge_results
+    from llm_slo_ebpf_toolkit_amd.collector import bpf
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut
+
+    sets = bpf.create_shard_rings(tag, world, ring_bytes, 1 << 14, 1 << 12, user_rec=24)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    pool = WorkerPool([_spec(r, world, tag, pods, port, engine, r if engine == "gpu" else 0, split=True)
+                       for r in range(world)], sets[0])
+    out, direct = [], []
+    try:
+        replies = []
+        for imgs in shard_imgs:
+            cuts = []
+            for (ring, user, spans), img in zip(sets, imgs):
+                assert ring.append_framed(img.framed)
+                assert user.push(img.user) == len(img.user) and spans.push(img.spans) == len(img.spans)
+                cuts.append(Cut(ring.producer_pos, user.head, spans.head, img.bases))
+            direct.append([len(img.framed) + img.user.nbytes for img in imgs])
+            replies.append(pool.window(cuts, 8))
+        replies.append(pool.stop())
+        for rep in replies[1:]:
+            prev = [r["prev"] for r in rep]
+            out.append({"packet": prev[0]["packet"], "res": merge_results(prev[0]["results"], 8),
+                        "events": sum(int(p["ring"][5]) for p in prev)})
+        # every worker freed its own rings completely (nobody else consumes them)
+        for ring, user, spans in sets:
+            assert ring.consumer_pos == ring.producer_pos and user.size == 0 and spans.size == 0
+    finally:
+        pool.close()
+    return out, direct
+
+
+@pytest.mark.timeout(300)
+def test_two_workers_on_split_rings_reproduce_the_single_process_window():
+    """the node's stream split at the source. Each of two workers DMAs and
+    decodes only its own ring set (half of the window's bytes), and the node-wide packet, every
+    incident's results and the node's event count equal one process reading one ring."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import build_shard_images
+
+    wins, imgs, pods = _windows()
+    tag = f"/mislo-split-{os.getpid()}"
+    one = _run_pool(1, imgs, pods, tag + "-a")
+    two, direct = _run_split(2, build_shard_images(wins, 2, pods, user_rec=24), pods, tag + "-b")
+    assert len(one) == len(two) == len(imgs)
+    for j, (a, b) in enumerate(zip(one, two)):
+        n = 256 + 48 + 18 + 8  # hist, status, misc, dbg
+        np.testing.assert_array_equal(a["packet"][:n], b["packet"][:n], err_msg=f"window {j}")
+        for key in ("feat", "pred", "sli", "evbits"):
+            np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
+        np.testing.assert_allclose(a["res"]["post"], b["res"]["post"], rtol=1e-12, atol=1e-15)
+        assert a["events"] == b["events"] > 0
+    whole = [len(i.framed) + i.user.nbytes for i in imgs]
+    for j, per in enumerate(direct):  # each worker's share of the bytes is about half
+        assert sum(per) >= whole[j] and all(0.3 * whole[j] < x < 0.7 * whole[j] for x in per), (per, whole[j])
+
+
 def _net_packet(p, n):
     """The packet's first n elements with the low-confidence count net of the tier-4 overlap: the
     GPU probe reports (raw low, overlap) in dbg[1:3], the CPU engine the net count and 0."""
@@ -167,6 +253,18 @@ def test_gpu_worker_reproduces_the_cpu_oracle():
     wins, imgs, pods = _windows()
     tag = f"/mislo-mg1-{os.getpid()}"
     _assert_same_windows(_run_pool(1, imgs, pods, tag + "-c"), _run_pool(1, imgs, pods, tag + "-g", engine="gpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_worker_with_late_pods_reproduces_the_cpu_oracle():
+    """Pods learned after their contexts were defined: the device decode resolves a record's
+    service through the pod table at decode time (decode.hip), as the oracle does -- the
+    service + node tier joins those records from the window the pods arrive in."""
+    wins, imgs, pods = _windows(n_win=4)
+    tag = f"/mislo-mgl-{os.getpid()}"
+    _assert_same_windows(_run_pool(1, imgs, None, tag + "-c", late_pods=(1, pods)),
+                         _run_pool(1, imgs, None, tag + "-g", engine="gpu", late_pods=(1, pods)))
 
 
 @pytest.mark.gpu

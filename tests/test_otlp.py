@@ -233,3 +233,54 @@ def test_receiver_refuses_oversized_bodies_and_unlisted_peers():
     finally:
         rx.stop()
     assert ring.size == 2
+
+
+def test_a_pods_service_is_bound_by_its_first_span():
+    """the pod -> service table decides the service (and the GPU) a pod's kernel
+    records belong to. A later span naming the same pod with another service is dropped, so a
+    pod cannot move another pod's records to its service."""
+    m, pods = _mapper()
+    first = m.records(otlp.parse_json(_request_json(RES, SPANS)))
+    assert len(first) == 2 and m.conflicts == 0
+    other = dict(RES, **{"service.name": "intruder"})
+    again = m.records(otlp.parse_json(_request_json(other, SPANS)))
+    assert len(again) == 0 and m.conflicts >= 1
+    upd = m.take_pod_updates()
+    assert upd is not None and len(upd[0]) == 1  # one binding, from the first service
+
+
+def test_span_naming_a_pod_must_come_from_its_address():
+    groups = otlp.GroupTable(8)
+    pods = Interner()
+    uid = RES["k8s.pod.uid"]
+    m = otlp.SpanMapper(groups, pods.id, 3, pod_ips=lambda: {"10.244.1.5": {uid}, "10.244.1.9": {"someone-else"}},
+                        forwarders="10.244.7.0/24")
+    body = otlp.parse_json(_request_json(RES, SPANS))
+    assert len(m.records(body, "10.244.1.9")) == 0 and m.spoofed >= 1  # another pod's address
+    assert len(m.records(body, "10.244.1.5")) > 0                      # its own address
+    assert len(m.records(body, "10.244.7.3")) > 0                      # a trusted forwarder
+    assert len(m.records(body, "192.168.9.9")) > 0                     # not a pod of this node
+
+
+def test_local_addresses_from_fib_trie(tmp_path):
+    from llm_slo_ebpf_toolkit_amd.collector import procfs
+
+    d = tmp_path / "55" / "net"
+    d.mkdir(parents=True)
+    (d / "fib_trie").write_text("""Main:
+  +-- 0.0.0.0/0 3 0 5
+     |-- 0.0.0.0
+        /0 universe UNICAST
+     +-- 127.0.0.0/8 2 0 2
+           |-- 127.0.0.1
+              /32 host LOCAL
+     +-- 10.244.1.0/24 2 0 2
+           |-- 10.244.1.0
+              /24 link UNICAST
+           |-- 10.244.1.5
+              /32 host LOCAL
+        |-- 10.244.1.255
+           /32 link BROADCAST
+""")
+    assert procfs.local_addresses(55, str(tmp_path)) == {"10.244.1.5"}
+    assert procfs.pod_addresses({55: "uid-a", 56: "uid-a"}, str(tmp_path)) == {"10.244.1.5": {"uid-a"}}

@@ -183,3 +183,52 @@ def test_every_signal_has_a_producer():
         for p in progs:
             assert re.search(rf"\b{p}\b\s*[(,)]", src), (sig, obj, p)
         assert 'SEC("license")' in src
+
+
+def _resolve(rows):
+    """Ring records -> the events they mean, ids resolved through the definitions ahead of them
+    (what the GPU's k_ring_defs + decode recover): (ts_off, tag, type, value_milli, pod, pid,
+    conn32, trace hash) per event, in ring order."""
+    ctx, tr, out = {}, {}, []
+    for a, tag_id, b, c in rows.tolist():
+        t = tag_id & 0xFF
+        if t == 0xFE:
+            ctx[tag_id >> 8] = (b, c, a)
+        elif t == 0xFD:
+            tr[a] = b | (c << 32)
+        else:
+            pod, pid, c32 = ctx.get(tag_id >> 8, (0, 0, 0))
+            tid = c & ((1 << 30) - 1)
+            out.append((a, c >> 30, t, b, pod, pid, c32, tr.get(tid, 0) if tid else 0))
+    return out
+
+
+def test_probe_c_split_rings_route_every_record_with_its_definitions(probe_host, tmp_path):
+    """Split rings (agent --gpus N): with mislo_shards routing pods to rings 1..3, every record
+    goes to its pod's ring and each ring carries the context and trace definitions its own
+    records use -- the same events, ring by ring, as a ProbeSim per ring fed its shard's records
+    (what the replay producer and the bench drive)."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    ev = _probe_events(n=2000, seed=13)
+    t0 = int(ev["ts_ns"][ev["ts_ns"] > 0].min())
+    epoch = (t0 - 10**6) & ~3 | 1
+    pods = sorted(set(ev["pod_id"].tolist()) - {0})
+    shard = {p: (i % 4) for i, p in enumerate(pods)}  # pod -> ring 0..3 (pod 0: unrouted -> 0)
+    args = ["--epoch-at", f"0:{epoch}"]
+    for p, s in shard.items():
+        args += ["--shard", f"{p}:{s}"]
+    got0, _ = _run_host(probe_host, tmp_path, ev, *args)
+    rt = load()
+    sh = np.array([shard.get(int(p), 0) for p in ev["pod_id"].tolist()])
+    for s in range(4):
+        got = got0 if s == 0 else np.fromfile(tmp_path / f"out.bin.{s}", dtype=np.uint32).reshape(-1, 4)
+        rb = rt.Ringbuf.create_shm(f"/mislo-phs-{os.getpid()}-{s}", 1 << 18)
+        rb.cfg_set(124, epoch)
+        sim = rt.ProbeSim(rb, records.milli_shift_table(), 1 << 20)
+        ref = sim.encode(np.ascontiguousarray(ev[sh == s])).reshape(-1, 4)
+        a, b = _resolve(got), _resolve(ref)
+        assert len(a) == int((sh == s).sum()) > 0 and a == b, s

@@ -272,15 +272,23 @@ lib = ctypes.CDLL(tool)
 lib.mislo_rocprof_foreign.restype = ctypes.c_int64
 lib.mislo_rocprof_foreign.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
 x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+w = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+v = torch.randn(1, 4096, device="cuda", dtype=torch.bfloat16)
 s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 torch.cuda.synchronize()
 dev, own = ctypes.c_double(), ctypes.c_double()
 
-def serve(seconds, two_streams):
-    # a service's duty cycle: ~6 ms of GEMMs every 15 ms, on one stream or two concurrent ones
+def serve(seconds, two_streams, decode=False):
+    # a service's duty cycle: ~6 ms of GEMMs every 15 ms, on one stream or two concurrent ones;
+    # decode: an LLM decode step's shape -- hundreds of microsecond-scale kernels (GEMV + norms)
     end = time.time() + seconds
     while time.time() < end:
-        if two_streams:
+        if decode:
+            h = v
+            for _ in range(64):
+                h = torch.nn.functional.silu(h @ w) * 0.01 + h
+                h = h / (h.float().pow(2).mean().sqrt().to(h.dtype) + 1)
+        elif two_streams:
             with torch.cuda.stream(s1):
                 a = [x @ x for _ in range(24)]
             with torch.cuda.stream(s2):
@@ -294,6 +302,7 @@ def serve(seconds, two_streams):
 
 serve(1.5, False)
 serve(1.5, True)
+serve(1.5, False, decode=True)
 print("phase_b", time.time_ns(), flush=True)
 sys.stdin.readline()  # the test has started another process's GEMMs
 print("contended", time.time_ns(), flush=True)
@@ -357,7 +366,7 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
     alone = [(float(x[3]), float(x[4])) for x in lines if x[0] == "foreign" and int(x[1]) < t_b and int(x[2]) > 2]
     shared = [(float(x[3]), float(x[4])) for x in lines if x[0] == "foreign" and int(x[1]) > t_b + 300_000_000]
     assert alone and shared, lines[-5:]
-    f_alone = np.median([d - o for d, o in alone])
+    f_alone = float(np.percentile([d - o for d, o in alone], 90))  # every alone phase, decode-like included
     f_shared = np.median([d - o for d, o in shared])
     recs = np.concatenate([np.frombuffer(ring.records_view()[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
                            for _, i, c in ring.peek(1 << 16)]) if ring.peek(1 << 16) else np.zeros(0, records.EVENT)
@@ -366,5 +375,29 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
     before, after = int((big["ts_ns"] < t_b).sum()), int((big["ts_ns"] > t_b).sum())
     print({"foreign_alone_median": f_alone, "foreign_shared_median": f_shared, "records_alone": before,
            "records_shared": after, "alone": alone[:6], "shared": shared[:6]})
-    assert f_alone < 10.0 and before <= 1, (f_alone, before, alone[:10])
+    assert f_alone < 10.0 and before <= 1, (f_alone, before, alone[-12:])
     assert f_shared >= 25.0 and after >= 5, (f_shared, after, shared[:10])
+
+
+@pytest.mark.gpu
+def test_split_rings_route_the_tools_records_to_the_pods_worker():
+    """agent --gpus N on split rings: MISLO_RING lists the workers' user rings and the agent's
+    pod -> shard table says which one owns this pod; every record lands there."""
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    names = [f"/mislo-test-{os.getpid()}-sr{r}" for r in range(2)]
+    rings = [rt.HostRing(1 << 14, 24, n) for n in names]
+    table = f"/mislo-test-{os.getpid()}-shards"
+    with open("/dev/shm" + table, "wb") as fh:
+        fh.truncate(1 << 20)
+        fh.seek(7)
+        fh.write(b"\x01")  # pod 7 -> worker 1
+    try:
+        env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=",".join(names), MISLO_SHARD_TABLE=table,
+                   MISLO_POD_ID="7", MISLO_QUEUE_FLOOR_NS="0")
+        r = subprocess.run([sys.executable, "-c", WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert rings[0].size == 0 and rings[1].size > 0, (rings[0].size, rings[1].size)
+    finally:
+        os.remove("/dev/shm" + table)

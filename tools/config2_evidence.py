@@ -103,10 +103,10 @@ def wait_http(url: str, proc, timeout: float) -> None:
     raise RuntimeError(f"{url} not ready after {timeout}s")
 
 
-def chat(port: int, i: int, phase: str, prompt_words: int = 16) -> dict:
+def chat(port: int, i: int, phase: str, prompt_words: int = 16, max_tokens: int = 16) -> dict:
     words = " ".join(f"token{(i * 7 + k) % 997}" for k in range(max(0, prompt_words - 8)))
     body = json.dumps({"prompt": f"why did the {phase} request {i} slow down on the gpu {words}".strip(),
-                       "profile": "chat_short", "max_tokens": 16, "request_id": f"{phase}-{i}"}).encode()
+                       "profile": "chat_short", "max_tokens": max_tokens, "request_id": f"{phase}-{i}"}).encode()
     req = urllib.request.Request(f"http://127.0.0.1:{port}/chat", data=body, method="POST",
                                  headers={"Content-Type": "application/json"})
     t = time.time_ns()
@@ -149,12 +149,18 @@ def main() -> int:
     ap.add_argument("--out", default="gpurun_out/config2")
     ap.add_argument("--preset", default="7b", help="Llama preset of the workload (BASELINE config 2: 7B)")
     ap.add_argument("--ttft-slo-ms", type=float, default=800.0, help="the agent's TTFT SLO (BASELINE config 2: 800 ms)")
-    ap.add_argument("--phase-s", type=float, default=24.0, help="seconds of the baseline and fault phases")
-    ap.add_argument("--recover-s", type=float, default=12.0)
-    ap.add_argument("--burners", type=int, default=4, help="GEMM burner processes on the GPU in the fault phase")
-    ap.add_argument("--prompt-words", type=int, default=512, help="prompt length (prefill tokens)")
+    ap.add_argument("--phase-s", type=float, default=48.0, help="seconds of the baseline and fault phases")
+    ap.add_argument("--recover-s", type=float, default=16.0)
+    ap.add_argument("--burners", type=int, default=3,
+                    help="GEMM burner processes on the GPU in the fault phase (4 left 2 requests in 24 s, "
+                         "profiles/r4_config2_first)")
+    ap.add_argument("--prompt-words", type=int, default=256, help="prompt length (prefill tokens)")
+    ap.add_argument("--max-tokens", type=int, default=2, help="tokens per request: TTFT is the SLO, short "
+                                                              "answers keep requests completing in every window")
+    ap.add_argument("--clients", type=int, default=2, help="concurrent closed-loop clients")
     ap.add_argument("--gap-s", type=float, default=0.05, help="client think time between requests")
-    ap.add_argument("--window-ms", type=int, default=1000)
+    ap.add_argument("--window-ms", type=int, default=2000,
+                    help="agent window: under the fault a request takes over a second, so 2 s windows")
     ap.add_argument("--model-path", default=MODEL, help="the agent's model ('' = the bayes_gpu expert table)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -197,7 +203,7 @@ def main() -> int:
         print("[config2] agent and llm ready", flush=True)
         tailer.start()
         for i in range(4):  # warm the model (first-request compilation / allocation)
-            chat(hport, i, "warmup", a.prompt_words)
+            chat(hport, i, "warmup", a.prompt_words, a.max_tokens)
         plan = [("baseline", a.phase_s, False), ("fault_gpu_contention", a.phase_s, True),
                 ("recovery", a.recover_s, False)]
         for phase, dur, fault in plan:
@@ -211,11 +217,22 @@ def main() -> int:
                 onset_ns = min(ons)
             t0 = time.time_ns()
             m0 = scrape(mport)
-            i = 0
-            while time.time_ns() - t0 < dur * 1e9:
-                rows.append(chat(hport, i, phase, a.prompt_words))
-                i += 1
-                time.sleep(a.gap_s)
+
+            def client(c, phase=phase, t0=t0, dur=dur):
+                i = 0
+                while time.time_ns() - t0 < dur * 1e9:
+                    try:
+                        rows.append(chat(hport, 1000 * c + i, phase, a.prompt_words, a.max_tokens))
+                    except (OSError, ValueError, KeyError):
+                        time.sleep(0.2)
+                    i += 1
+                    time.sleep(a.gap_s)
+
+            cl = [threading.Thread(target=client, args=(c,), daemon=True) for c in range(a.clients)]
+            for t in cl:
+                t.start()
+            for t in cl:
+                t.join(dur + 120)
             for b in burners:
                 b.send_signal(signal.SIGTERM)
                 b.wait(30)
@@ -267,7 +284,8 @@ def main() -> int:
                                if x.get("service") == "rag-service" and x.get("predicted_fault_domain") != "unknown"][:4]
     res["agent_counters_by_phase"] = counters
     res["setup"] = {"preset": a.preset, "ttft_slo_ms": a.ttft_slo_ms, "burners": a.burners,
-                    "prompt_words": a.prompt_words, "phase_s": a.phase_s, "recover_s": a.recover_s,
+                    "prompt_words": a.prompt_words, "max_tokens": a.max_tokens, "clients": a.clients,
+                    "window_ms": a.window_ms, "phase_s": a.phase_s, "recover_s": a.recover_s,
                     "model": os.path.relpath(a.model_path, ROOT) if a.model_path else "bayes_gpu",
                     "observable_signals": list(GPU_SIGNALS) if a.model_path else "all",
                     "fault": f"{a.burners} processes of back-to-back 8192^3 bf16 GEMMs on the service's GPU"}

@@ -261,8 +261,9 @@ def main() -> int:
     # service's cgroup has a CPU quota (the box's has none: a signal that cannot fire is not
     # evidence, so it is summed out rather than read as "not elevated")
     observable = list(NET_SIGNALS) + ["runqueue_delay_ms", "cpu_steal_pct"]
-    if procfs.cgroup_files(os.getpid())[0]:
-        observable.append("cfs_throttled_ms")
+    # (cfs_throttled_ms is not: the box's CPU quota sits on a group every process of this run
+    # shares -- agent, vector DB, clients, burners -- so its throttling is not the service's;
+    # profiles/r4_config3_first read 16 throttled intervals in the healthy baseline)
     if procfs.psi_available():
         observable.append("mem_reclaim_latency_ms")
     gpu_tool = a.backend == "llama" and os.path.exists(TOOL)

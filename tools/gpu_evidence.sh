@@ -7,7 +7,8 @@
 #   reentry   GPU tests, smoke(), the default bench, a kernel + copy trace of the bench
 #   pmc       rocprofv3 counter passes over a short bench (one pass per counter block budget)
 #   rptests   the rocprofiler tool's GPU tests (request GPU wait under contention included)
-#   config2   BASELINE config 2: Llama 7B preset, 800 ms TTFT SLO, onset -> first attribution
+#   config2   BASELINE config 2: Llama 7B preset, 800 ms TTFT SLO, GEMM burners, per-window attribution
+#   live      config3 then config2
 #   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
 #   spread    the headline bench at K = 20 and K = 200, repeated on one box
@@ -33,11 +34,18 @@ case "${1:-reentry}" in
   rptests)
     $S "240|rp_tests|python -u -m pytest tests/test_rocprof_tool.py -m gpu -x -v -s --timeout 150 --timeout-method thread" ;;
   config2)
-    $S "600|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r3_config2_7b" ;;
+    $S "600|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b ${2:-}" ;;
+  live2)    # the rocprof tool's GPU tests, then configs 3 and 2
+    $S "300|rp_tests|python -u -m pytest tests/test_rocprof_tool.py -m gpu -x -v -s --timeout 200 --timeout-method thread" \
+       "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
+       "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
+  live)     # configs 3 and 2 back to back (the live-attribution evidence)
+    $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
+       "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
   overhead)
     $S "200|agent_oh|python -u tools/agent_overhead.py --rate 1e6 --seconds 20 --out gpurun_out/r3_agent_overhead_1Mevs.json" ;;
   config3)
-    $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r3_config3 ${2:-}" ;;
+    $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3 ${2:-}" ;;
   buffers)  # windows in flight: the copy of window k waits for window k - buffers + 1's results
     for b in 3 4 5 4 3; do
       $S "200|buf_$b|python3 bench.py --steps 100 --warmup 10 --buffers $b" || exit 1
