@@ -8,6 +8,13 @@ curve the north star asks for; weak scaling: every GPU owns one node shard, 1M e
 window); the macro-F1 (held out: windows no model update saw), the REF-55 macro-F1 and the
 agent CPU % / RSS are reported alongside.
 
+Topology = the agent's (``agent --gpus N`` on split rings, agent/worker.py): every GPU is one
+window worker reading its own ring set -- the node's producers route each record to the worker
+owning its service, so each GPU DMAs and decodes its share of the node's stream only -- and its
+timed windows run through the agent's worker path (``WorkerCore.window``: stage window k, collect
+window k-1's packet and node-wide incident results) with rank 0 also doing the controller's
+per-window host epilogue (``Agent._emit_window``: metrics, IncidentAttributions, output).
+
 One step = one collection window per GPU, exactly as the agent runs it:
 
   producer process (stands in for the kernel: the probes' records, already framed as the BPF
@@ -50,6 +57,8 @@ HELDOUT_SCENARIOS = ("full", "mixed", "mixed_multi")
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--engine", default="gpu", choices=("gpu", "cpu"),
+                    help="cpu: the window engine's host oracle over gloo (CI rehearsal of the multi-rank path)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--events", type=int, default=1 << 20, help="events per window per GPU")
@@ -250,6 +259,16 @@ def main() -> int:
                        n_services=a.services, seed=a.seed, shard=rank, fault_hold=max(1, a.windows))
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(max(1, a.windows))]
+
+    def globalize(ws):
+        # the node's incident group g of this rank's local group l: g = l * world + rank (worker
+        # r owns the groups g % world == r; agent/worker.py groups_of)
+        if world > 1:
+            for w in ws:
+                w.spans["group_id"] = w.spans["group_id"] * world + rank
+        return ws
+
+    globalize(wins)
     # held out: a different seed (never trained on), REF's label set and the full set
     held = []
     for j in range(a.heldout):
@@ -257,7 +276,7 @@ def main() -> int:
                             spans_per_window=a.spans, n_services=a.services, seed=a.seed + 7919, shard=rank)
         hg = ReplayGenerator(hcfg)
         hg.window = 1000 + 10 * j  # later than the timed windows, 10 s apart: no halo reaches across scenarios
-        held.append(hg.next_window())
+        held.append(globalize([hg.next_window()])[0])
     images = build_replay_images(wins + held, user_rec=a.user_rec)
     imgs, himgs = images[: len(wins)], images[len(wins):]
     # the model's training set (untimed): REF-profile single and compound faults, another seed,
@@ -275,7 +294,7 @@ def main() -> int:
         for j in range(a.train_windows):  # 10 s apart: the halo never joins two training incidents
             tg = tgens[j % len(tgens)]
             tg.window = 10 * j
-            train_wins.append(tg.next_window())
+            train_wins.append(globalize([tg.next_window()])[0])
     train_imgs = build_replay_images(train_wins, user_rec=a.user_rec) if train_wins else []
     train_codes = [mtrain.window_codes(w) for w in train_wins]
     pods = np.unique(np.concatenate([w.events["pod_id"] for w in wins + held]))
@@ -333,10 +352,14 @@ def main() -> int:
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline
     from llm_slo_ebpf_toolkit_amd.safety import CPUMeter, OverheadGuard, read_rss_mb
 
-    require_gpu_extension()
-    torch.cuda.set_device(local)
-    numa_cpus = bind_to_device_numa(local)
+    gpu = a.engine == "gpu"
+    numa_cpus = None
+    if gpu:
+        require_gpu_extension()
+        torch.cuda.set_device(local)
+        numa_cpus = bind_to_device_numa(local)
     conn_parent.send(sorted(numa_cpus) if numa_cpus else None)
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
     pg = None
     comm = None
     if world > 1:
@@ -344,9 +367,10 @@ def main() -> int:
         # per-window packet all-reduce -- is the engine's own RCCL communicator over xGMI
         dist.init_process_group("gloo")
         pg = dist.group.WORLD
-        uid = [rt_uid() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = (uid[0], rank, world)
+        if gpu:
+            uid = [rt_uid() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = (uid[0], rank, world)
     # a window's record budget covers its framed ring records (events AND the definitions the
     # probes commit ahead of them) plus its user-space records: nothing may spill into the next window
     sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs + himgs)
@@ -356,7 +380,10 @@ def main() -> int:
     pipe = WindowPipeline(sig_cap, max(a.spans, a.train_spans if train_imgs else 0), a.services, local, comm,
                           model=a.model, seed=a.seed, learn=bool(train_imgs),
                           use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,
-                          user_cap=min(user_cap, sig_cap), halo_ms=a.halo_ms, import_cap=import_cap, xchg_cap=xchg)
+                          user_cap=min(user_cap, sig_cap), halo_ms=a.halo_ms, import_cap=import_cap, xchg_cap=xchg,
+                          # the agent's worker r on split rings: its own ring set, the node's groups g % N == r
+                          shard=(rank, world), split_rings=world > 1, engine=a.engine,
+                          group=pg if not gpu else None)
     # the producer publishes the epochs here (it runs ahead of the cuts): no cfg writes
     src = RingWindowSource(pipe, rb, user, spans, cfg_set=lambda i, v: None)
     keys = np.array(sorted(pod_sn), dtype=np.uint32)
@@ -473,29 +500,66 @@ def main() -> int:
             break
         time.sleep(1e-3)
     prefilled = int(cuts.size)
+    # the agent's worker path (agent/worker.py WorkerCore.window: stage window k, collect window
+    # k-1's node-wide packet and every worker's incident results) is the timed step. Rank 0 then
+    # runs the controller's per-window host epilogue (agent/daemon.py Agent._emit_window:
+    # Prometheus histograms, IncidentAttributions from the posteriors, JSONL output) over every
+    # collected window, timed on its own: it is O(incident groups), runs once per agent window
+    # (1 s) next to the GPU's next window, and at this benchmark's back-to-back 1M-event windows
+    # it would measure Python, not the window path (host_epilogue_us_per_window)
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+    from llm_slo_ebpf_toolkit_amd.agent.worker import WorkerCore, WorkerSpec
+
+    g_node = a.services * world
+    spec = WorkerSpec(rank=rank, world=world, device=local, engine=a.engine, source="shm", ring_name=tag, pin_dir="",
+                      user_rec=a.user_rec, sig_cap=sig_cap, span_cap=a.spans, group_cap=a.services,
+                      user_cap=min(user_cap, sig_cap), window_ms=1000.0, ttft_slo_ms=800.0, halo_ms=a.halo_ms,
+                      import_cap=import_cap, xchg_cap=xchg, model_image=b"", split=world > 1)
+    core = WorkerCore.adopt(spec, pipe, src)
+    ctl = Agent(AgentOptions(engine=a.engine, metrics_bind="", output="jsonl", output_path=os.devnull, config="",
+                             window_groups=g_node, min_confidence=0.5)) if rank == 0 else None
+    svc_names = [f"svc-{g + 1}" for g in range(g_node)]
+    epi = [0.0, 0]  # host epilogue seconds, windows
+
+    def epilogue(rep):
+        if ctl is not None and rep.get("prev") is not None:
+            te = time.perf_counter()
+            ctl._emit_window([rep], time.time_ns(), g_node, svc_names, rb, pipe.model)
+            epi[0] += time.perf_counter() - te
+            epi[1] += 1
+
     if pg is not None:
         dist.barrier()
     meter = CPUMeter()
-    torch.cuda.synchronize()
+    sync()
     if pg is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     meter.start()
     t0 = time.perf_counter()
     last = None
     kernel_recs = 0
+    collected = []
     for j in range(a.warmup, a.warmup + a.steps):
-        last, r = step(j)
-        kernel_recs += r["n_kernel"]
-    src.drain()
-    torch.cuda.synchronize()
+        rep = core.window(next_cut(), a.services, labels=imgs[j % len(imgs)].labels)
+        if rank == 0 and rep.get("prev") is not None:
+            collected.append(rep)
+        last = rep["k"]
+        kernel_recs += rep["staged"]["n_kernel"]
+    fin = core.stop()  # the last window's results (drains the source)
+    sync()
     if pg is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
+    for rep in collected + ([fin] if rank == 0 else []):
+        epilogue(rep)
+    attributions_emitted = ctl.attributions_emitted if ctl is not None else 0
+    if ctl is not None:
+        ctl.close()
     busy_cpu_pct, _, _ = meter.stop()
     dev_ms = [pipe.window_ms(k) for k in range(max(0, last - pipe.nb + 1), last + 1)]
-    cp = [pipe.eng.copy_ms(k) for k in range(max(1, last - pipe.nb + 1), last + 1)]
+    cp = [pipe.eng.copy_ms(k) for k in range(max(1, last - pipe.nb + 1), last + 1)] if gpu else []
     host_us = 1e6 * (src.host_s - host0) / max(src.n - n0, 1)
     reap_us = 1e6 * (src.reap_s - reap0) / max(src.n - n0, 1)
     submit_us = 1e6 * (src.submit_s - sub0) / max(src.n - n0, 1)
@@ -572,7 +636,13 @@ def main() -> int:
     ref55 = {}
     fx = os.path.join(ROOT, "tests", "fixtures", "ref_multi_fault_samples.jsonl")
     if rank == 0 and os.path.exists(fx):
-        ref55 = ref55_engine(pipe, fx, a.model)
+        if gpu:
+            ref55 = ref55_engine(pipe, fx, a.model)
+        else:  # the host oracle engine scores with the same model on the host
+            from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+            from llm_slo_ebpf_toolkit_amd.models.train import host_scorer, ref55_report
+
+            ref55 = {a.model: ref55_report(fx, host_scorer(pipe.model)), "bayes": ref55_report(fx, host_scorer(NaiveBayes.ref()))}
 
     conf = summ["confusion"]
     dbg = summ["dbg"]
@@ -635,18 +705,27 @@ def main() -> int:
         "host_us_per_window": round(host_us, 1),
         "host_reap_us_per_window": round(reap_us, 1),
         "host_submit_us_per_window": round(submit_us, 1),
-        "host_issue_us_per_window": round(pipe.eng.host_issue_us, 1),
-        "host_issue_wait_us_per_window": round(pipe.eng.host_wait_us, 1),
-        "host_issue_dma_us_per_window": round(pipe.eng.host_dma_issue_us, 1),
-        "host_issue_launch_us_per_window": round(pipe.eng.host_launch_us, 1),
-        "host_issue_pre_us_per_window": round(pipe.eng.host_pre_us, 1),
-        "host_issue_dma_split_us": [round(x, 1) for x in pipe.eng.host_dma_split_us],
-        "host_issue_tail_us_per_window": round(pipe.eng.host_tail_us, 1),
+        "host_issue_us_per_window": round(getattr(pipe.eng, 'host_issue_us', 0.0), 1),
+        "host_issue_wait_us_per_window": round(getattr(pipe.eng, 'host_wait_us', 0.0), 1),
+        "host_issue_dma_us_per_window": round(getattr(pipe.eng, 'host_dma_issue_us', 0.0), 1),
+        "host_issue_launch_us_per_window": round(getattr(pipe.eng, 'host_launch_us', 0.0), 1),
+        "host_issue_pre_us_per_window": round(getattr(pipe.eng, 'host_pre_us', 0.0), 1),
+        "host_issue_dma_split_us": [round(x, 1) for x in getattr(pipe.eng, "host_dma_split_us", [])],
+        "host_issue_tail_us_per_window": round(getattr(pipe.eng, 'host_tail_us', 0.0), 1),
         "records_over_window_budget": int(src.carried),
-        "direct_dma_fraction": round(pipe.eng.direct_bytes / max(1, pipe.eng.direct_bytes + pipe.eng.staged_bytes), 4),
+        "direct_dma_fraction": round(getattr(pipe.eng, "direct_bytes", 0) / max(1, getattr(pipe.eng, "direct_bytes", 0)
+                                                                  + getattr(pipe.eng, "staged_bytes", 0)), 4),
         "windows_prefilled": prefilled,
         "producer_wait_ms_total": round(producer_wait_ms, 2),
         "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
+        # the controller's per-window epilogue on rank 0, inside the timed region (agent/daemon.py
+        # Agent._emit_window over the node-wide results the worker path collected)
+        "host_epilogue_us_per_window": round(1e6 * epi[0] / max(epi[1], 1), 1),
+        "attributions_emitted_timed": int(attributions_emitted),
+        "topology": (f"agent --gpus {world}: one window worker per GPU on split rings (its own kernel / user-space / "
+                     f"span rings, producers routing by service), agent/worker.py WorkerCore.window per step, "
+                     f"controller epilogue on rank 0") if world > 1 else
+                    "agent --gpus 1: one window worker (agent/worker.py WorkerCore.window per step) + the controller epilogue",
     }
     if rank == 0:
         line = json.dumps(res)

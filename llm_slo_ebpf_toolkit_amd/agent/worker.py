@@ -131,13 +131,25 @@ class WorkerCore:
         self.pending: Optional[Tuple[int, float]] = None
         self.windows = 0
 
-    def window(self, cut, n_groups: int, pods=None) -> dict:
+    @classmethod
+    def adopt(cls, spec: WorkerSpec, pipe, src) -> "WorkerCore":
+        """A worker core around a pipeline and ring source built elsewhere (bench.py: trained and
+        warmed up on the same engine before its timed windows run through this worker path)."""
+        core = cls.__new__(cls)
+        core.spec, core.pipe, core.src = spec, pipe, src
+        core.rings = (src.ring, src.user_ring, src.span_ring)
+        core.pending = None
+        core.windows = 0
+        return core
+
+    def window(self, cut, n_groups: int, pods=None, labels=None) -> dict:
         """Stage window k; return what the controller needs of window k-1 (finished by now or
-        nearly: the engine runs nb windows deep)."""
+        nearly: the engine runs nb windows deep). ``labels``: incident labels for the device's
+        confusion matrix (the benchmark's replay windows; the agent has none)."""
         if pods is not None and len(pods[0]):
             self.pipe.eng.set_pods(*pods)
         t0 = time.perf_counter()
-        r = self.src.stage(cut, n_groups, with_labels=False, learn=False)
+        r = self.src.stage(cut, n_groups, labels, with_labels=labels is not None, learn=False)
         host_us = 1e6 * (time.perf_counter() - t0)
         out = {"rank": self.spec.rank, "k": r["k"], "staged": r, "done": self.src.done()}
         prev, self.pending = self.pending, (r["k"], host_us, n_groups)

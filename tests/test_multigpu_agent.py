@@ -331,3 +331,24 @@ def test_windows_that_wrap_the_bpf_ring_equal_unwrapped_windows():
         np.testing.assert_array_equal(a["packet"], b["packet"], err_msg=f"window {j}")
         for key in ("feat", "pred", "sli", "evbits"):
             np.testing.assert_array_equal(a["res"][key], b["res"][key], err_msg=f"window {j} {key}")
+
+
+@pytest.mark.timeout(600)
+def test_bench_runs_the_agents_worker_path_on_two_ranks(tmp_path):
+    """`bench.py --gpus 2` (self-launched ranks, the host oracle engine over
+    gloo) times the agent's topology: each rank is a window worker on its own split ring set
+    (agent/worker.py WorkerCore.window per step) and rank 0 runs the controller's per-window
+    epilogue (Agent._emit_window) inside the timed region."""
+    out = tmp_path / "bench.json"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--engine", "cpu", "--model", "bayes",
+                        "--events", "4096", "--spans", "256", "--services", "8", "--windows", "2", "--heldout", "3",
+                        "--paced-windows", "0", "--steps", "3", "--warmup", "1", "--ring-mib", "16",
+                        "--train-windows", "0", "--out", str(out)],
+                       capture_output=True, text=True, timeout=580, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
+    assert "split rings" in d["topology"] and "WorkerCore.window" in d["topology"]
+    # every node-wide incident of the timed windows became an attribution on the controller
+    assert d["incidents_scored_timed_windows"] == 3 * 2 * 8 == d["attributions_emitted_timed"]
+    assert d["host_epilogue_us_per_window"] > 0
