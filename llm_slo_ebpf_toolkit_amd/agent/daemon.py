@@ -181,6 +181,11 @@ class AgentOptions:
     procfs_pods: str = ""                # pid:pod-uid,... to watch ("" = the node's kubepods cgroups)
     procfs_interval_ms: int = 100
     procfs_cpu_psi: bool = False         # cpu_steal_pct also from the pod group's cpu.pressure (pod-private cgroups)
+    # gpu_queue_delay_ms from the KFD driver's per-process occupancy / eviction files (runtime/csrc/
+    # gpusampler.h): "auto" = when /sys/class/kfd exists and pod processes are watched (bpf source or
+    # the procfs sampler); needs the host pid namespace (hostPID) to match KFD's pids to pods
+    kfd_sampler: str = "auto"
+    kfd_proc: str = "/sys/class/kfd/kfd/proc"
     model_signals: str = ""              # signals the node's sources produce (others marginalised; "" = all)
     pair_prior: float = 0.0              # 2-fault prior mass added to a table model without pairs (0 = none)
 
@@ -726,40 +731,57 @@ class Agent:
             receiver = OtlpSpanReceiver(o.otlp_receiver_bind, mapper, push_spans, allow=o.otlp_receiver_allow).start()
             self.receiver = receiver
         sampler = None
-        if o.procfs_sampler:
-            from ..collector import procfs
+        from ..collector import kfd, procfs
 
-            static = procfs.parse_pod_list(o.procfs_pods)
-            cache = {"t": 0.0, "m": {}}
+        static = procfs.parse_pod_list(o.procfs_pods)
+        cache = {"t": 0.0, "m": {}}
+        tlock = threading.Lock()
 
-            def targets():
-                if static:
-                    return {pid: self.pod_ids.id(uid) for pid, uid in static.items()}
+        def targets():
+            if static:
+                return {pid: self.pod_ids.id(uid) for pid, uid in static.items()}
+            with tlock:
                 if time.monotonic() - cache["t"] > 10.0:  # pod churn: re-walk the cgroups every 10 s
                     cache["m"] = {pid: self.pod_ids.id(uid) for pid, uid in procfs.pod_processes().items()}
                     cache["t"] = time.monotonic()
                 return cache["m"]
 
+        def shard_targets(r):
+            def f():
+                t = targets()
+                owner = router.pod_shard(np.array(list(t.values()), dtype=np.int64)) if t else []
+                return {pid: pod for (pid, pod), s in zip(t.items(), owner) if int(s) == r}
+            return f
+
+        if o.procfs_sampler:
             # native: a C++ thread reads schedstat / cgroup / PSI and pushes into the user ring
             if router is None:
                 sampler = procfs.NativeSampler(user, targets, node_id=node_id, cpu_psi=o.procfs_cpu_psi,
                                                refresh_s=10.0 if not static else 3600.0)
             else:  # split rings: one sampler per worker, over the pods its services own
-                def shard_targets(r):
-                    def f():
-                        t = targets()
-                        owner = router.pod_shard(np.array(list(t.values()), dtype=np.int64)) if t else []
-                        return {pid: pod for (pid, pod), s in zip(t.items(), owner) if int(s) == r}
-                    return f
-
                 sampler = procfs.MultiSampler([procfs.NativeSampler(sets[r][1], shard_targets(r), node_id=node_id,
                                                                     cpu_psi=o.procfs_cpu_psi, refresh_s=10.0)
                                                for r in range(N)])
             sampler.start(o.procfs_interval_ms / 1000.0)
             self.procfs = sampler
+        use_kfd = o.kfd_sampler == "on" or (o.kfd_sampler == "auto" and kfd.available(o.kfd_proc)
+                                             and (o.procfs_sampler or o.source == "bpf"))
+        if use_kfd:
+            loader = getattr(self, "bpf_loader", None)
+            bpf_gpu = loader is not None and "gpu_kfd" in loader.available()
+            finder = kfd.hip_map_finder(lambda: loader.loaded("gpu_kfd")) if bpf_gpu else None
+            kfds = [kfd.KfdSampler(user if router is None else sets[r][1],
+                                   targets if router is None else shard_targets(r), node_id=node_id,
+                                   kfd_proc=o.kfd_proc, refresh_s=10.0 if not static else 3600.0, hip_map=finder,
+                                   evictions=not bpf_gpu)  # the probe's kprobes report evictions
+                    for r in range(1 if router is None else N)]
+            for k in kfds:
+                k.start()
+            self.kfd = kfds
+            sampler = procfs.MultiSampler(([sampler] if sampler is not None else []) + kfds)
         from ..safety import ShedLadder
 
-        self.ladder = ShedLadder(catalog.DISABLE_ORDER, maps=maps, sampler=sampler, user_ring=user,
+        self.ladder = ShedLadder(catalog.DISABLE_ORDER, maps=maps, sampler=sampler, user_ring=[x[1] for x in sets],
                                  probe_manager=getattr(self, "probe_manager", None), generator=self.generator)
         if self.guard is not None:
             self.guard.source = TreeCPUSampler(lambda: [os.getpid()] + pool.pids())
@@ -794,7 +816,7 @@ class Agent:
                 if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
                     self._scan_pods(maps)  # pod churn
                     if getattr(self, "bpf_loader", None) is not None:
-                        self.bpf_loader.rescan_uprobes()  # libssl / librccl of new workloads
+                        self.bpf_loader.rescan_uprobes(background=True)  # libssl / librccl / libamdhip64 of new workloads
                 self.windows_done += 1
                 windows += 1
                 if state and o.checkpoint_every > 0 and self.windows_done % o.checkpoint_every == 0:

@@ -74,6 +74,9 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                   "(unprivileged; min-capability mode)"),
         ("procfs-pods", d.procfs_pods, "pid:pod-uid,... for the procfs sampler (empty: the kubepods cgroups)"),
         ("procfs-interval-ms", d.procfs_interval_ms, "procfs sampler interval"),
+        ("kfd-sampler", d.kfd_sampler, "gpu_queue_delay_ms from the KFD driver's per-process files: other processes' "
+                                       "wave occupancy of a pod's GPU and its queue evictions (auto | on | off; "
+                                       "auto = when /sys/class/kfd exists and pod processes are watched)"),
         ("procfs-cpu-psi", False, "procfs sampler: cpu_steal_pct is also the pod cgroup's cpu.pressure 'some' share "
                                   "(pod-private cgroups only)"),
         ("model-signals", d.model_signals, "window engine: comma-separated signals this node's sources produce; "
@@ -124,6 +127,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         checkpoint_every=int(a.checkpoint_every), gpus=int(a.gpus), split_rings=bool(a.split_rings), model_path=a.model_path,
         otlp_receiver_allow=a.otlp_receiver_allow, otlp_forwarders=a.otlp_forwarders, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
         procfs_interval_ms=int(a.procfs_interval_ms), procfs_cpu_psi=bool(a.procfs_cpu_psi),
+        kfd_sampler=a.kfd_sampler,
         model_signals=a.model_signals,
         pair_prior=float(a.pair_prior))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime

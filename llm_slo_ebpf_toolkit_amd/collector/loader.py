@@ -76,13 +76,21 @@ class BpfProbeLoader:
             self._uprobes = UprobeAttacher(self.pin_dir)
         return self._uprobes
 
-    def rescan_uprobes(self) -> int:
-        """Attach the loaded probes' uprobe programs to libraries mapped since the last scan."""
+    def loaded(self, probe: str) -> bool:
+        with self._lock:
+            return self._refs.get(probe, 0) > 0
+
+    def rescan_uprobes(self, background: bool = False) -> int:
+        """Attach the loaded probes' uprobe programs to libraries mapped since the last scan
+        (``background``: on the attacher's thread; returns 0 and the links appear later)."""
         from .uprobes import UPROBE_PROBES
 
         with self._lock:
             if not any(p in UPROBE_PROBES for p in self._refs):
                 return 0
+        if background:
+            self.uprobes.rescan_async()
+            return 0
         return self.uprobes.rescan()
 
     # ---- plumbing ------------------------------------------------------------------------

@@ -435,7 +435,7 @@ class MultiSampler:
 
     @property
     def mask(self) -> int:
-        return self.samplers[0].mask if self.samplers else 0
+        return max((s.mask for s in self.samplers), default=0)  # (KFD samplers report 0)
 
     @mask.setter
     def mask(self, m: int) -> None:

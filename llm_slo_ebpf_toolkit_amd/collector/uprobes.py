@@ -12,19 +12,21 @@ itself:
    ``/proc/<pid>/root/<path>`` (the container's mount namespace, seen from the host-PID agent),
    de-duplicated by (device, inode): one attachment per distinct file, however many processes
    and containers map it;
-2. **locate** -- the function's file offset from the ELF itself (.dynsym / .symtab value mapped
-   through the PT_LOAD segment that holds it), cached per file;
+2. **locate** -- the function's file offset from the ELF itself (the memory-mapped file's .dynsym
+   value mapped through the PT_LOAD segment that holds it), every target symbol of the library in
+   one pass, cached per (device, inode);
 3. **attach** -- ``perf_event_open`` on the uprobe PMU (type and retprobe bit read from
    /sys/bus/event_source/devices/uprobe) with the path and offset, then ``BPF_LINK_CREATE`` of
    the pinned program onto that perf event (runtime/csrc/bpfsys.cpp); closing the link detaches.
 
-``UprobeAttacher.rescan()`` (the agent calls it with its pod rescans) attaches newly started
-workloads' libraries. The syscalls go through an injectable object so the argument flow is
+``UprobeAttacher.rescan_async()`` (the agent calls it with its pod rescans) attaches newly started
+workloads' libraries on a background thread, off the window loop. The syscalls go through an injectable object so the argument flow is
 unit-tested without privileges.
 """
 
 from __future__ import annotations
 
+import mmap
 import os
 import re
 import struct
@@ -51,6 +53,20 @@ UPROBE_TARGETS: Tuple[UprobeTarget, ...] = (
     UprobeTarget("gpu_kfd", "allgather_exit", r"^librccl\.so", "ncclAllGather", True),
     UprobeTarget("gpu_kfd", "reducescatter_enter", r"^librccl\.so", "ncclReduceScatter", False),
     UprobeTarget("gpu_kfd", "reducescatter_exit", r"^librccl\.so", "ncclReduceScatter", True),
+    # HIP runtime: a process's GPU work submissions and its host-side waits for the GPU, per tgid
+    # (gpu_kfd.bpf.c hip_activity: the agent's KFD sampler weighs other processes' occupancy of a
+    # pod's GPU by them, runtime/csrc/gpusampler.h)
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipLaunchKernel", False),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipModuleLaunchKernel", False),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipExtModuleLaunchKernel", False),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipGraphLaunch", False),
+    UprobeTarget("gpu_kfd", "hip_copy", r"^libamdhip64\.so", "hipMemcpyAsync", False),
+    UprobeTarget("gpu_kfd", "hip_sync_enter", r"^libamdhip64\.so", "hipStreamSynchronize", False),
+    UprobeTarget("gpu_kfd", "hip_sync_exit", r"^libamdhip64\.so", "hipStreamSynchronize", True),
+    UprobeTarget("gpu_kfd", "hip_sync_enter", r"^libamdhip64\.so", "hipDeviceSynchronize", False),
+    UprobeTarget("gpu_kfd", "hip_sync_exit", r"^libamdhip64\.so", "hipDeviceSynchronize", True),
+    UprobeTarget("gpu_kfd", "hip_sync_enter", r"^libamdhip64\.so", "hipEventSynchronize", False),
+    UprobeTarget("gpu_kfd", "hip_sync_exit", r"^libamdhip64\.so", "hipEventSynchronize", True),
 )
 UPROBE_PROBES = frozenset(t.probe for t in UPROBE_TARGETS)
 
@@ -59,48 +75,76 @@ UPROBE_PROBES = frozenset(t.probe for t in UPROBE_TARGETS)
 # ELF: function name -> file offset
 # ---------------------------------------------------------------------------------------
 
-def elf_symbol_offset(path: str, symbol: str) -> Optional[int]:
-    """File offset of ``symbol`` (a defined function) in a 64-bit little-endian ELF, or None."""
+_SYM = struct.Struct("<IBBHQQ")
+
+
+def elf_symbol_offsets(path: str, symbols: Iterable[str]) -> Dict[str, int]:
+    """File offsets of the defined functions among ``symbols`` in a 64-bit little-endian ELF.
+
+    The file is memory-mapped, not read (librccl / libamdhip64 are hundreds of MB), and only the
+    dynamic symbol table is walked: a uprobe target is an exported API function, which .dynsym
+    always holds (.symtab -- often stripped, and 10-100x larger -- only when there is no .dynsym).
+    One pass resolves every wanted name."""
+    want = {w.encode(): w for w in symbols}
+    out: Dict[str, int] = {}
     try:
-        with open(path, "rb") as fh:
-            data = fh.read()
+        fh = open(path, "rb")
     except OSError:
-        return None
-    if len(data) < 64 or data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
-        return None
-    e_phoff, e_shoff = struct.unpack_from("<QQ", data, 0x20)
-    e_phentsize, e_phnum, e_shentsize, e_shnum = struct.unpack_from("<HHHH", data, 0x36)
-    segs = []
-    for i in range(e_phnum):
-        p_type, _flags, p_offset, p_vaddr, _paddr, p_filesz = struct.unpack_from("<IIQQQQ", data,
-                                                                                 e_phoff + i * e_phentsize)
-        if p_type == 1:  # PT_LOAD
-            segs.append((p_vaddr, p_filesz, p_offset))
-    secs = []
-    for i in range(e_shnum):
-        o = e_shoff + i * e_shentsize
-        if o + 64 > len(data):
-            break
-        _name, sh_type, _flags, _addr, sh_offset, sh_size, sh_link, _info, _align, sh_entsize = \
-            struct.unpack_from("<IIQQQQIIQQ", data, o)
-        secs.append((sh_type, sh_offset, sh_size, sh_link, sh_entsize))
-    want = symbol.encode()
-    for sh_type, off, size, link, ent in secs:
-        if sh_type not in (2, 11) or ent != 24 or link >= len(secs):  # SHT_SYMTAB, SHT_DYNSYM
-            continue
-        str_off = secs[link][1]
-        for j in range(size // ent):
-            st_name, st_info, _other, st_shndx, st_value, _size = struct.unpack_from("<IBBHQQ", data, off + j * ent)
-            if st_value == 0 or st_shndx == 0 or (st_info & 0xF) != 2:  # defined STT_FUNC
-                continue
-            end = data.find(b"\x00", str_off + st_name)
-            name = data[str_off + st_name:end]
-            if name == want or name.split(b"@")[0] == want:
-                for vaddr, filesz, poff in segs:
-                    if vaddr <= st_value < vaddr + filesz:
-                        return st_value - vaddr + poff
-                return st_value
-    return None
+        return out
+    with fh:
+        try:
+            mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+        except (OSError, ValueError):
+            return out
+        with mm:
+            n = len(mm)
+            if n < 64 or mm[:4] != b"\x7fELF" or mm[4] != 2 or mm[5] != 1:
+                return out
+            e_phoff, e_shoff = struct.unpack_from("<QQ", mm, 0x20)
+            e_phentsize, e_phnum, e_shentsize, e_shnum = struct.unpack_from("<HHHH", mm, 0x36)
+            segs = []
+            for i in range(e_phnum):
+                o = e_phoff + i * e_phentsize
+                if o + 56 > n:
+                    break
+                p_type, _f, p_offset, p_vaddr, _pa, p_filesz = struct.unpack_from("<IIQQQQ", mm, o)
+                if p_type == 1:  # PT_LOAD
+                    segs.append((p_vaddr, p_filesz, p_offset))
+            secs = []
+            for i in range(e_shnum):
+                o = e_shoff + i * e_shentsize
+                if o + 64 > n:
+                    break
+                _nm, sh_type, _fl, _ad, sh_offset, sh_size, sh_link, _in, _al, sh_entsize = \
+                    struct.unpack_from("<IIQQQQIIQQ", mm, o)
+                secs.append((sh_type, sh_offset, sh_size, sh_link, sh_entsize))
+            tables = [x for x in secs if x[0] == 11] or [x for x in secs if x[0] == 2]  # DYNSYM, else SYMTAB
+            for _t, off, size, link, ent in tables:
+                if ent != 24 or link >= len(secs) or off + size > n:
+                    continue
+                str_off, str_size = secs[link][1], secs[link][2]
+                for st_name, st_info, _o, st_shndx, st_value, _sz in _SYM.iter_unpack(mm[off:off + size - size % 24]):
+                    if st_value == 0 or st_shndx == 0 or (st_info & 0xF) != 2 or st_name >= str_size:
+                        continue  # defined STT_FUNC only
+                    a = str_off + st_name
+                    name = mm[a:mm.find(b"\x00", a, str_off + str_size)]
+                    hit = want.get(name) or want.get(name.split(b"@")[0])
+                    if hit is None or hit in out:
+                        continue
+                    for vaddr, filesz, poff in segs:
+                        if vaddr <= st_value < vaddr + filesz:
+                            out[hit] = st_value - vaddr + poff
+                            break
+                    else:
+                        out[hit] = st_value
+                    if len(out) == len(want):
+                        return out
+    return out
+
+
+def elf_symbol_offset(path: str, symbol: str) -> Optional[int]:
+    """File offset of one defined function (``elf_symbol_offsets`` for a single name), or None."""
+    return elf_symbol_offsets(path, [symbol]).get(symbol)
 
 
 # ---------------------------------------------------------------------------------------
@@ -179,7 +223,8 @@ class NativeSys:
 @dataclass
 class _Probe:
     progs: Dict[str, int] = field(default_factory=dict)                 # program -> prog fd
-    links: Dict[Tuple[str, Tuple[str, int]], int] = field(default_factory=dict)  # (program, file) -> link fd
+    # (program, symbol, file) -> link fd (one program may serve several functions: hip_launch)
+    links: Dict[Tuple[str, str, Tuple[str, int]], int] = field(default_factory=dict)
 
 
 class UprobeAttacher:
@@ -191,8 +236,10 @@ class UprobeAttacher:
         self.sys = sys_ if sys_ is not None else NativeSys()
         self._pmu: Optional[Tuple[int, int]] = None
         self._probes: Dict[str, _Probe] = {}
-        self._offsets: Dict[Tuple[Tuple[str, int], str], Optional[int]] = {}
+        # (dev, inode) -> {symbol: offset} of every target symbol of that library, one ELF pass
+        self._offsets: Dict[Tuple[str, int], Dict[str, int]] = {}
         self._lock = threading.Lock()
+        self._bg: Optional[threading.Thread] = None
         self.errors: List[str] = []
 
     def attach(self, probe: str) -> int:
@@ -209,6 +256,7 @@ class UprobeAttacher:
         return self.rescan(probe)
 
     def rescan(self, probe: Optional[str] = None) -> int:
+        """Attach to libraries mapped since the last scan; returns links created."""
         with self._lock:
             if self._pmu is None:
                 self._pmu = self.sys.pmu()
@@ -224,12 +272,13 @@ class UprobeAttacher:
                     if t.library not in libs_cache:
                         libs_cache[t.library] = mapped_libraries(t.library, self.proc_root)
                     for key, path in libs_cache[t.library].items():
-                        if (t.program, key) in st.links:
+                        if (t.program, t.symbol, key) in st.links:
                             continue
-                        ck = (key, t.symbol)
-                        if ck not in self._offsets:
-                            self._offsets[ck] = elf_symbol_offset(path, t.symbol)
-                        off = self._offsets[ck]
+                        offs = self._offsets.get(key)
+                        if offs is None:
+                            offs = self._offsets[key] = elf_symbol_offsets(
+                                path, {u.symbol for u in UPROBE_TARGETS if u.library == t.library})
+                        off = offs.get(t.symbol)
                         if off is None:
                             continue  # this build of the library does not export the function
                         pfd = self.sys.perf_uprobe_open(pmu_type, bit, t.retprobe, path, off, -1)
@@ -241,9 +290,29 @@ class UprobeAttacher:
                         if lfd < 0:
                             self.errors.append(f"{t.program} -> {path}+{off:#x}: link_create {lfd}")
                             continue
-                        st.links[(t.program, key)] = lfd
+                        st.links[(t.program, t.symbol, key)] = lfd
                         made += 1
             return made
+
+    def rescan_async(self) -> bool:
+        """``rescan()`` on a background thread (the /proc walk and ELF reads stay off the agent's
+        window loop); False while the previous one is still running."""
+        if self._bg is not None and self._bg.is_alive():
+            return False
+
+        def run():
+            try:
+                self.rescan()
+            except Exception as e:  # a vanished process or library must not end the agent
+                self.errors.append(f"rescan: {type(e).__name__}: {e}")
+
+        self._bg = threading.Thread(target=run, name="uprobe-rescan", daemon=True)
+        self._bg.start()
+        return True
+
+    def wait(self, timeout: Optional[float] = None) -> None:
+        if self._bg is not None:
+            self._bg.join(timeout)
 
     def detach(self, probe: str) -> None:
         with self._lock:

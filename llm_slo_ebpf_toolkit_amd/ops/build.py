@@ -39,7 +39,7 @@ EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 HIP_SOURCES = ["decode.hip", "join.hip", "posterior.hip", "gatestats.hip", "storm.hip", "exchange.hip"]
 RT_SOURCES = ["ring.cpp", "replay.cpp", "pool.cpp", "bpfring.cpp", "probesim.cpp", "tables.cpp", "assemble.cpp",
-              "bpfsys.cpp", "procsampler.cpp", "rt_bindings.cpp"]
+              "bpfsys.cpp", "procsampler.cpp", "gpusampler.cpp", "rt_bindings.cpp"]
 
 
 def torch_flags():

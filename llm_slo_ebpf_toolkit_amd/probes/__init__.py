@@ -32,7 +32,7 @@ PROBES = {
     "mem_reclaim_latency_ms": ("bpf", "mem_reclaim", ("reclaim_begin", "reclaim_end")),
     "disk_io_latency_ms": ("bpf", "disk_io_latency", ("rq_issue", "rq_complete")),
     "syscall_latency_ms": ("bpf", "syscall_latency", ("read_enter", "read_exit", "write_enter", "write_exit")),
-    "gpu_queue_delay_ms": ("rocprof+bpf", "gpu_kfd", ("sched_job", "run_job")),
+    "gpu_queue_delay_ms": ("rocprof+bpf", "gpu_kfd", ("kfd_evict", "kfd_restore")),
     "hbm_pressure_pct": ("rocprof", "libmislo_rocprof", ()),
     "xgmi_link_latency_us": ("rocprof", "libmislo_rocprof", ()),
     "rccl_collective_ms": ("rocprof+bpf", "gpu_kfd", ("allreduce_enter", "allreduce_exit", "allgather_enter",

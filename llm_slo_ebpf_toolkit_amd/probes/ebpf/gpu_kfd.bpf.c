@@ -1,23 +1,42 @@
 /* GPU-side kernel signals for MI355X nodes (NEW): complements the rocprofiler-sdk tool
- * (probes/rocprof) for workloads that were not started with it.
+ * (probes/rocprof) for workloads that were not started with it. ROCm compute never reaches the
+ * DRM GPU scheduler -- HIP writes AQL packets into KFD user-mode queues and rings their doorbells
+ * -- so the hooks are where that path is visible to the kernel and to BPF:
  *
- *   gpu_queue_delay_ms   drm GPU scheduler: job queued -> job run on the ring
- *                        (gpu_scheduler:drm_sched_job -> drm_run_job, per fence)
+ *   gpu_queue_delay_ms   KFD queue eviction: kprobe kfd_process_evict_queues -> kprobe
+ *                        kfd_process_restore_queues, per kfd_process. While evicted (VRAM
+ *                        eviction / overcommit, kgd2kfd_quiesce_mm for MMU notifiers and
+ *                        userptr invalidation, which call evict) none of the process's queues
+ *                        run: the whole span is GPU queue delay of that process, attributed to
+ *                        its lead thread's pod (the evicting context is some other task)
  *   rccl_collective_ms   uprobe/uretprobe on librccl's ncclAllReduce / ncclAllGather /
- *                        ncclReduceScatter (host-side enqueue + completion of blocking
- *                        calls; the agent attaches these pinned programs to every librccl
- *                        the node's processes map, collector/uprobes.py)
- * Records carry the has_gpu flag. */
+ *                        ncclReduceScatter (host-side enqueue + completion of blocking calls)
+ *   hip_activity (map)   uprobes on libamdhip64: kernel launches (hipLaunchKernel,
+ *                        hipModuleLaunchKernel, hipExtModuleLaunchKernel, hipGraphLaunch) and
+ *                        hipMemcpyAsync, and the time spent in hipStreamSynchronize /
+ *                        hipDeviceSynchronize / hipEventSynchronize, per tgid. No ring records:
+ *                        the agent's KFD sampler (runtime/csrc/gpusampler.h) reads it to tell a
+ *                        pod that is using its GPU -- and how long it waited on it -- from an
+ *                        idle one, and weighs other processes' wave occupancy of that GPU by it
+ *                        (gpu_queue_delay_ms, foreign occupancy)
+ *
+ * The uprobe programs are attached by the agent to every libamdhip64 / librccl the node's
+ * processes map (collector/uprobes.py). Records carry the has_gpu flag. */
 #include "mislo_probe.h"
 
 char LICENSE[] SEC("license") = "GPL";
 
+/* amdkfd's process (module BTF: CO-RE relocates the field) */
+struct kfd_process {
+	struct task_struct *lead_thread;
+} __attribute__((preserve_access_index));
+
 struct {
 	__uint(type, BPF_MAP_TYPE_LRU_HASH);
-	__uint(max_entries, 65536);
-	__type(key, __u64);   /* scheduler job pointer */
-	__type(value, __u64); /* queued time */
-} job_q SEC(".maps");
+	__uint(max_entries, 4096);
+	__type(key, __u64);   /* struct kfd_process * */
+	__type(value, __u64); /* eviction start */
+} kfd_evicted SEC(".maps");
 
 struct {
 	__uint(type, BPF_MAP_TYPE_HASH);
@@ -26,27 +45,44 @@ struct {
 	__type(value, __u64); /* call start */
 } coll_t0 SEC(".maps");
 
-SEC("tp/gpu_scheduler/drm_sched_job")
-int sched_job(struct trace_event_raw_drm_sched_job *ctx)
+struct {
+	__uint(type, BPF_MAP_TYPE_LRU_HASH);
+	__uint(max_entries, 16384);
+	__type(key, __u32);   /* host tgid */
+	__type(value, struct mislo_hip_act);
+} hip_activity SEC(".maps");
+
+struct {
+	__uint(type, BPF_MAP_TYPE_LRU_HASH);
+	__uint(max_entries, 16384);
+	__type(key, __u64);   /* pid_tgid */
+	__type(value, __u64); /* synchronize entry */
+} hip_sync_t0 SEC(".maps");
+
+SEC("kprobe/kfd_process_evict_queues")
+int BPF_KPROBE(kfd_evict, struct kfd_process *p)
 {
-	__u64 job = (__u64)ctx->sched_job, now = bpf_ktime_get_ns();
-	bpf_map_update_elem(&job_q, &job, &now, BPF_ANY);
+	__u64 key = (__u64)p, now = bpf_ktime_get_ns();
+	/* nested evictions (KFD counts them) keep the first start */
+	bpf_map_update_elem(&kfd_evicted, &key, &now, BPF_NOEXIST);
 	return 0;
 }
 
-SEC("tp/gpu_scheduler/drm_run_job")
-int run_job(struct trace_event_raw_drm_sched_job *ctx)
+SEC("kprobe/kfd_process_restore_queues")
+int BPF_KPROBE(kfd_restore, struct kfd_process *p)
 {
-	__u64 job = (__u64)ctx->sched_job;
-	__u64 *t0 = bpf_map_lookup_elem(&job_q, &job);
+	__u64 key = (__u64)p;
+	__u64 *t0 = bpf_map_lookup_elem(&kfd_evicted, &key);
 	if (!t0)
 		return 0;
 	__u64 dt = bpf_ktime_get_ns() - *t0;
-	bpf_map_delete_elem(&job_q, &job);
+	bpf_map_delete_elem(&kfd_evicted, &key);
 	if (mislo_below_floor(MISLO_GPU_QUEUE_DELAY, dt))
 		return 0;
-	__u64 pt = bpf_get_current_pid_tgid();
-	struct mislo_event *e = mislo_reserve(MISLO_GPU_QUEUE_DELAY, dt, pt >> 32, (__u32)pt);
+	struct task_struct *t = BPF_CORE_READ(p, lead_thread);
+	if (!t)
+		return 0;
+	struct mislo_event *e = mislo_reserve_task(MISLO_GPU_QUEUE_DELAY, dt, t);
 	if (e) {
 		e->flags = MISLO_FLAG_HAS_GPU;
 		mislo_submit(e);
@@ -91,3 +127,60 @@ SEC("uprobe")
 int BPF_KPROBE(reducescatter_enter) { return coll_enter(); }
 SEC("uretprobe")
 int BPF_KRETPROBE(reducescatter_exit) { return coll_exit(); }
+
+static __always_inline struct mislo_hip_act *hip_act(__u32 tgid)
+{
+	struct mislo_hip_act *a = bpf_map_lookup_elem(&hip_activity, &tgid);
+	if (a)
+		return a;
+	struct mislo_hip_act zero = {};
+	bpf_map_update_elem(&hip_activity, &tgid, &zero, BPF_NOEXIST);
+	return bpf_map_lookup_elem(&hip_activity, &tgid);
+}
+
+SEC("uprobe")
+int BPF_KPROBE(hip_launch)
+{
+	struct mislo_hip_act *a = hip_act(bpf_get_current_pid_tgid() >> 32);
+	if (a) {
+		__sync_fetch_and_add(&a->launches, 1);
+		a->last_ns = bpf_ktime_get_ns();
+	}
+	return 0;
+}
+
+SEC("uprobe")
+int BPF_KPROBE(hip_copy)
+{
+	struct mislo_hip_act *a = hip_act(bpf_get_current_pid_tgid() >> 32);
+	if (a) {
+		__sync_fetch_and_add(&a->copies, 1);
+		a->last_ns = bpf_ktime_get_ns();
+	}
+	return 0;
+}
+
+SEC("uprobe")
+int BPF_KPROBE(hip_sync_enter)
+{
+	__u64 pt = bpf_get_current_pid_tgid(), now = bpf_ktime_get_ns();
+	bpf_map_update_elem(&hip_sync_t0, &pt, &now, BPF_ANY);
+	return 0;
+}
+
+SEC("uretprobe")
+int BPF_KRETPROBE(hip_sync_exit)
+{
+	__u64 pt = bpf_get_current_pid_tgid();
+	__u64 *t0 = bpf_map_lookup_elem(&hip_sync_t0, &pt);
+	if (!t0)
+		return 0;
+	__u64 dt = bpf_ktime_get_ns() - *t0;
+	bpf_map_delete_elem(&hip_sync_t0, &pt);
+	struct mislo_hip_act *a = hip_act(pt >> 32);
+	if (a) {
+		__sync_fetch_and_add(&a->sync_ns, dt);
+		__sync_fetch_and_add(&a->syncs, 1);
+	}
+	return 0;
+}

@@ -90,6 +90,16 @@ struct mislo_def16 {
 	__u32 c;       /* ctx: pid; trace: hash bits 32-63 */
 };
 
+/* gpu_kfd.bpf.c hip_activity value, per host tgid: the HIP runtime calls of a process (uprobes on
+ * libamdhip64), read by the agent's KFD sampler (runtime/csrc/gpusampler.h HipActivity) */
+struct mislo_hip_act {
+	__u64 launches;   /* hipLaunchKernel / hipModuleLaunchKernel / hipExtModuleLaunchKernel / hipGraphLaunch */
+	__u64 copies;     /* hipMemcpyAsync */
+	__u64 last_ns;    /* bpf_ktime of the latest submission */
+	__u64 sync_ns;    /* total time in hipStreamSynchronize / hipDeviceSynchronize / hipEventSynchronize */
+	__u64 syncs;
+};
+
 /* id spaces: the kernel assigns the low part, the agent's host-side encoders the rest, so both
  * kinds of producer share one device context table (2^24 rows) and one trace-id space */
 #define MISLO_KERNEL_CTX_LIMIT (1u << 23)   /* kernel context ids 1 .. 2^23 - 1 */

@@ -9,12 +9,21 @@
 //
 //   type 13 gpu_queue_delay_ms   (a) kernel dispatch: start - max(enqueue return, queue predecessor end) (ns);
 //                                (b) foreign GPU time: every MISLO_FOREIGN_MS (default 100) while this
-//                                process runs kernels, the GPU time other processes held over the
-//                                interval -- the device's GFX activity (amdgpu gpu_metrics
-//                                gfx_activity_acc, an exact integral; else gpu_busy_percent) minus
-//                                this process's own kernel time (the union of its dispatches'
-//                                [start, end]) -- emitted when it reaches MISLO_FOREIGN_FLOOR_PCT
-//                                (default 10) of the interval, as ns of the interval (ns)
+//                                process runs kernels, the share of the interval other processes'
+//                                waves held the GPU, as ns of the interval, when it reaches
+//                                MISLO_FOREIGN_FLOOR_PCT (default 10). KFD reports each process's
+//                                wave occupancy per GPU (/sys/class/kfd/kfd/proc/<pid>/stats_<gpu_id>/
+//                                cu_occupancy, readable without root); every MISLO_OCC_MS (default
+//                                10) at which this process has NO kernel in flight, the sum over all
+//                                processes on its GPU is other processes' occupancy alone -- no need
+//                                to know which host pid is this one (a container's pid namespace
+//                                hides it), and immune to the inter-kernel overhead that made
+//                                "device activity minus own kernel time" read 30 % busy for a
+//                                decode loop of microsecond kernels alone on the GPU (r4 box).
+//                                Meanwhile the tool learns its own entry (never holding waves at
+//                                those idle readings, most often while it has kernels in flight);
+//                                from then on every reading counts, minus its own entry -- a
+//                                saturated server has no idle moments at all (ns)
 //   type 14 hbm_pressure_pct     the GPU's node-wide HBM use: amdgpu sysfs mem_info_vram_used /
 //                                mem_info_vram_total of the PCI device the process allocates on
 //                                (every process's allocations, not this one's), sampled on
@@ -54,8 +63,8 @@
 // pair's starting rate before it has shown a large copy, default 64 GB/s: one xGMI link
 // direction; a pair's calibration starts there and a measured rate may only raise it, to at most
 // 4x: a link already degraded when the process starts is not its own baseline),
-// MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_FOREIGN_MIN_OWN_PCT (default 1: the process must
-// have run kernels for this share of the interval), MISLO_ROCPROF_VERBOSE.
+// MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_OCC_MS, MISLO_FOREIGN_MIN_SAMPLES (default 3 idle
+// samples per interval), MISLO_KFD_PROC (default /sys/class/kfd/kfd/proc), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/buffer_tracing.h>
 #include <rocprofiler-sdk/callback_tracing.h>
@@ -63,6 +72,7 @@
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
@@ -159,22 +169,34 @@ struct State {
   };
   std::map<uint64_t, Vram> vram;
   std::mutex hbm_mu;  // emit_hbm runs on the sampler thread and the buffer callback thread
-  // foreign GPU time per GPU agent: this process's kernel time (union of dispatch [start, end],
-  // guarded by mu) against the device's activity accumulator (sampler thread only)
-  struct Busy {
-    int metrics_fd = -1, busy_fd = -1;
-    bool acc = false;           // gpu_metrics carries gfx_activity_acc at byte 76 (format 1.7 / 1.8)
-    // this process's kernels' [start, end] as their completions arrive (any order: completion
-    // callbacks run on several threads), kept until no later interval can overlap them
-    std::vector<std::pair<uint64_t, uint64_t>> iv;
-    uint64_t t_p = 0, t_pp = 0;   // the last two readings' times (rocprofiler ns; 0 = none)
-    uint32_t acc_p = 0, acc_pp = 0;
-    double busy_p = 0.0;          // gpu_busy_percent at the last reading (no accumulator)
-    double dev_pct = 0.0, own_pct = 0.0;  // last interval (tests)
-    uint64_t intervals = 0;
+  // foreign GPU time per GPU agent (KFD gpu_id): this process's kernels in flight (enqueued, not
+  // yet completed; guarded by mu) gate the sampler thread's occupancy readings
+  struct Occ {
+    uint64_t gpu_id = 0;
+    int64_t inflight = 0;          // mu
+    uint64_t enq_seq = 0;          // mu: enqueues so far (a reading that straddles one is dropped)
+    uint64_t disp = 0;             // mu: enqueues in the current interval
+    uint64_t last_read = 0;        // sampler thread: time of the last reading (ns)
+    uint64_t last_done = 0;        // mu: last completion, or the enqueue that ended an idle spell (ns)
+    // sampler thread only: the current interval's idle readings
+    uint64_t t0 = 0, t_first = 0, clean = 0, hot = 0, busy_skips = 0;
+    double occ_sum = 0.0;
+    // last decided interval and the reading cost (tests, overhead accounting)
+    double share = 0.0, occ_mean = 0.0;
+    uint64_t decisions = 0, reads = 0, read_ns = 0, cleans = 0, emitted = 0;
+    // which KFD entry is this process (a container's pid namespace hides its host pid): the entry
+    // that never holds waves while this process has none in flight, and most often does while it
+    // has -- learned from the readings; once known, every reading counts, in flight or not
+    struct Cand {
+      uint64_t idle_hot = 0, busy_hot = 0;
+    };
+    std::map<uint32_t, Cand> cands;
+    uint64_t idle_n = 0, busy_n = 0;
+    uint32_t self_pid = 0;  // 0: not identified yet
   };
-  std::map<uint64_t, Busy> busy;
-  uint64_t foreign_ms = 100, foreign_floor_pct = 10, foreign_min_own_pct = 1;
+  std::map<uint64_t, Occ> occ;
+  uint64_t foreign_ms = 100, foreign_floor_pct = 10, occ_ms = 10, foreign_min_samples = 3;
+  std::string kfd_proc = "/sys/class/kfd/kfd/proc";
   std::string pci_sysfs = "/sys/bus/pci/devices";
   uint64_t hbm_sample_ms = 1000;
   uint64_t last_hbm_milli = ~0ull;  // fallback (no sysfs): this process's live allocations
@@ -190,6 +212,7 @@ struct State {
   std::mutex smu;
   std::condition_variable scv;
   bool stop = false;
+  std::atomic<bool> kick{false};  // a GPU went idle for this process: take an occupancy reading now
   std::atomic<uint64_t> window_sec{0}, window_count{0}, pushed{0}, dropped{0};
 };
 
@@ -318,71 +341,152 @@ uint64_t xgmi_latency(uint64_t src, uint64_t dst, uint64_t bytes, uint64_t dur) 
   return dur > xfer ? dur - xfer : 0;
 }
 
-// One reading of the device's GFX activity: the gpu_metrics accumulator (percent x ms, exact
-// over any interval) or, without it, the driver's smoothed busy percent.
-bool read_activity(State::Busy& b, uint32_t* acc, double* busy) {
-  char buf[96];
-  if (b.acc) {
-    if (pread(b.metrics_fd, buf, sizeof(buf), 0) < 80) return false;
-    std::memcpy(acc, buf + 76, 4);
-    return true;
+// Every KFD process's cu_occupancy on one GPU (CU-equivalents of resident waves): (host pid,
+// occupancy) of the processes with a stats_<gpu_id> directory -- the others are not on this GPU.
+bool kfd_occupancy(uint64_t gpu_id, std::vector<std::pair<uint32_t, uint64_t>>* out) {
+  out->clear();
+  DIR* d = opendir(g.kfd_proc.c_str());
+  if (!d) return false;
+  char path[512], buf[32];
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    std::snprintf(path, sizeof(path), "%s/%s/stats_%llu/cu_occupancy", g.kfd_proc.c_str(), e->d_name,
+                  (unsigned long long)gpu_id);
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) continue;
+    const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (n <= 0) continue;
+    buf[n] = 0;
+    out->emplace_back((uint32_t)std::strtoul(e->d_name, nullptr, 10), std::strtoull(buf, nullptr, 10));
   }
-  if (b.busy_fd < 0) return false;
-  const ssize_t n = pread(b.busy_fd, buf, sizeof(buf) - 1, 0);
-  if (n <= 0) return false;
-  buf[n] = 0;
-  *busy = std::strtod(buf, nullptr);
-  return true;
+  closedir(d);
+  return !out->empty();
 }
 
-// Every foreign_ms, per GPU this process has run kernels on: the GPU time others held over the
-// PREVIOUS interval [t_pp, t_p] (one interval of lag: by now every completion callback of a kernel
-// that ended in it has arrived). Own time is the union of this process's kernel intervals clipped
-// to it (overlapping streams count once), device time the accumulator's growth over it.
-void foreign_tick(uint64_t now) {
-  for (auto& kv : g.busy) {
-    State::Busy& b = kv.second;
-    uint32_t acc = 0;
-    double busy = 0.0;
-    if (!read_activity(b, &acc, &busy)) continue;
-    const uint64_t lo = b.t_pp, hi = b.t_p;
-    const uint32_t dacc = b.acc_p - b.acc_pp;
-    const double busy_w = b.busy_p;
-    b.t_pp = b.t_p, b.acc_pp = b.acc_p;
-    b.t_p = now, b.acc_p = acc, b.busy_p = busy;
-    std::vector<std::pair<uint64_t, uint64_t>> iv;
+// Which entry is this process: never hot at its idle readings (<= 1 %), hot at the most of its
+// busy ones, clearly ahead of the runner-up. Re-checked as readings accrue; a choice that starts
+// holding waves while this process is idle is dropped.
+void identify_self(State::Occ& o) {
+  if (o.self_pid) {
+    const auto it = o.cands.find(o.self_pid);
+    if (it == o.cands.end() || (o.idle_n >= 100 && it->second.idle_hot * 100 > o.idle_n)) o.self_pid = 0;
+    return;
+  }
+  if (o.idle_n < 20 || o.busy_n < 20) return;
+  uint32_t best = 0;
+  uint64_t b1 = 0, b2 = 0;
+  for (const auto& kv : o.cands) {
+    if (kv.second.idle_hot * 100 > o.idle_n) continue;
+    if (kv.second.busy_hot > b1) {
+      b2 = b1, b1 = kv.second.busy_hot, best = kv.first;
+    } else if (kv.second.busy_hot > b2) {
+      b2 = kv.second.busy_hot;
+    }
+  }
+  if (best && b1 >= 5 && 2 * b2 < b1) o.self_pid = best;
+}
+
+// One occupancy reading per GPU this process is using. Idle (no kernel of this process in flight,
+// none enqueued during the reading): every entry's waves are other processes' -- and a lesson for
+// identify_self. In flight: only once this process's own entry is known, other entries' waves.
+void occ_sample(uint64_t now) {
+  static thread_local std::vector<std::pair<uint32_t, uint64_t>> per;
+  for (auto& kv : g.occ) {
+    State::Occ& o = kv.second;
+    if (!o.gpu_id) continue;
+    uint64_t seq = 0;
+    bool idle = false, active = false;
     {
       std::lock_guard<std::mutex> lk(g.mu);
-      iv.swap(b.iv);
-      // keep what a later window [hi, ...] can still overlap
-      for (const auto& x : iv)
-        if (x.second > hi) b.iv.push_back(x);
-      if (b.iv.size() > 262144) b.iv.clear();  // no ticks for a long time: start afresh
+      // in flight with no completion for 5 s: a lost completion, not a kernel still running
+      if (o.inflight > 0 && now > o.last_done + 5000000000ull) o.inflight = 0;
+      idle = o.inflight <= 0;
+      // serving: it enqueued in this interval, or kernels of it are still queued / running (a
+      // contended prefill enqueues in a burst, then waits on them for most of a second)
+      active = o.disp > 0 || !idle;
+      if (!idle) o.disp += o.disp == 0;  // the interval counts as one this process used the GPU in
+      seq = o.enq_seq;
     }
-    if (!lo || hi <= lo) continue;
-    std::sort(iv.begin(), iv.end());
-    uint64_t own = 0, cur_s = 0, cur_e = 0;
-    for (const auto& x : iv) {
-      const uint64_t s = x.first < lo ? lo : x.first, e = x.second > hi ? hi : x.second;
-      if (e <= s) continue;
-      if (s > cur_e) {
-        own += cur_e - cur_s;
-        cur_s = s, cur_e = e;
-      } else if (e > cur_e) {
-        cur_e = e;
+    if (!active) continue;  // not serving: no readings
+    // at most two readings per MISLO_OCC_MS (a reading costs ~70 us of this thread on the r4 box)
+    if (now < o.last_read + g.occ_ms * 500000ull) continue;
+    o.last_read = now;
+    const auto t = std::chrono::steady_clock::now();
+    const bool ok = kfd_occupancy(o.gpu_id, &per);
+    o.read_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count();
+    ++o.reads;
+    if (!ok) continue;
+    bool busy = false;
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      const bool still_idle = o.inflight <= 0 && o.enq_seq == seq;
+      busy = !idle && o.inflight > 0;
+      if (idle && !still_idle) continue;  // this process enqueued meanwhile: neither kind
+    }
+    if (!idle && !busy) continue;
+    uint64_t total = 0, self = 0;
+    for (const auto& e : per) {
+      total += e.second;
+      if (e.first == o.self_pid) self = e.second;
+      if (e.second) {
+        State::Occ::Cand& c = o.cands[e.first];
+        ++(idle ? c.idle_hot : c.busy_hot);
+      } else {
+        o.cands.emplace(e.first, State::Occ::Cand{});
       }
     }
-    own += cur_e - cur_s;
-    const uint64_t dt = hi - lo;
-    double dev = b.acc ? (double)dacc * 1e6 / (double)dt : busy_w;  // (percent x ms) per ms
-    double own_pct = 100.0 * (double)own / (double)dt;
-    if (own_pct > 100.0) own_pct = 100.0;
-    if (dev > 100.0) dev = 100.0;
-    b.dev_pct = dev, b.own_pct = own_pct;
-    ++b.intervals;
-    const double foreign = dev - own_pct;
-    if (own_pct >= (double)g.foreign_min_own_pct && foreign >= (double)g.foreign_floor_pct)
-      emit(kQueueDelay, lo + dt / 2, (uint64_t)(foreign / 100.0 * (double)dt), 0);
+    ++(idle ? o.idle_n : o.busy_n);
+    if (o.cands.size() > 4096) o.cands.clear(), o.idle_n = o.busy_n = 0, o.self_pid = 0;  // pid churn
+    if ((o.idle_n + o.busy_n) % 16 == 0) identify_self(o);
+    if (busy && !o.self_pid) {
+      ++o.busy_skips;
+      continue;
+    }
+    const uint64_t foreign = total - (idle ? 0 : self);
+    if (!o.clean) o.t_first = now;
+    ++o.clean, ++o.cleans;
+    o.occ_sum += (double)foreign;
+    if (foreign > 0) ++o.hot;
+  }
+}
+
+// Every foreign_ms, per GPU this process ran kernels on in the interval: the share of its idle
+// readings at which other processes held waves on the GPU, emitted as that share of the interval.
+// A busy process has few idle moments (a contended decode loop: ~1 per step): an interval with
+// fewer than foreign_min_samples readings is extended, up to 10 x foreign_ms, before it is decided.
+void foreign_tick(uint64_t now) {
+  for (auto& kv : g.occ) {
+    State::Occ& o = kv.second;
+    if (o.t0 && o.clean < g.foreign_min_samples && now < o.t0 + 10 * g.foreign_ms * 1000000ull) continue;
+    uint64_t disp = 0;
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      disp = o.disp;
+      o.disp = 0;
+    }
+    // the interval starts at its first reading (less one reading period): a stretch without any
+    // (the process idle, not serving) is not reported with the share seen after it
+    const uint64_t t0 = o.t0 && o.t_first ? std::max(o.t0, o.t_first - std::min<uint64_t>(o.t_first, g.occ_ms * 1000000ull)) : o.t0;
+    const uint64_t clean = o.clean, hot = o.hot;
+    const double occ_sum = o.occ_sum;
+    o.t0 = now, o.t_first = 0, o.clean = 0, o.hot = 0, o.occ_sum = 0.0;
+    if (!t0 || now <= t0 || !disp || clean < g.foreign_min_samples) continue;
+    const uint64_t dt = now - t0;
+    o.share = (double)hot / (double)clean;
+    o.occ_mean = occ_sum / (double)clean;
+    ++o.decisions;
+    if (o.share * 100.0 >= (double)g.foreign_floor_pct) {
+      // an extended interval is reported as foreign_ms pieces, so the records keep the time
+      // resolution the agent's join tiers need (pod + pid: 100 ms of the request span)
+      const uint64_t step = g.foreign_ms * 1000000ull;
+      const uint64_t k = std::max<uint64_t>(1, (dt + step / 2) / step);
+      for (uint64_t j = 0; j < k; ++j) {
+        const uint64_t a = t0 + dt * j / k, b = t0 + dt * (j + 1) / k;
+        emit(kQueueDelay, a + (b - a) / 2, (uint64_t)(o.share * (double)(b - a)), 0);
+      }
+      ++o.emitted;
+    }
   }
 }
 
@@ -396,21 +500,49 @@ void route() {
 
 void sampler_main() {
   std::unique_lock<std::mutex> lk(g.smu);
-  const uint64_t tick = g.foreign_ms ? (g.hbm_sample_ms ? std::min(g.foreign_ms, g.hbm_sample_ms) : g.foreign_ms)
+  const uint64_t tick = g.foreign_ms ? (g.hbm_sample_ms ? std::min(g.occ_ms, g.hbm_sample_ms) : g.occ_ms)
                                      : g.hbm_sample_ms;
-  uint64_t next_hbm = 0, next_foreign = 0;
-  while (!g.scv.wait_for(lk, std::chrono::milliseconds(tick), [] { return g.stop; })) {
+  uint64_t next_hbm = 0, next_foreign = 0, next_tick = 0, next_report = 0;
+  for (;;) {
+    g.scv.wait_for(lk, std::chrono::milliseconds(tick), [] { return g.stop || g.kick.load(); });
+    if (g.stop) break;
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
+    if (g.kick.exchange(false) && now < next_tick) {  // woken by an idle GPU between ticks
+      occ_sample(now);
+      continue;
+    }
+    next_tick = now + tick * 1000000ull - 500000ull;
     route();
     if (g.hbm_sample_ms && now >= next_hbm) {
       next_hbm = now + g.hbm_sample_ms * 1000000ull - 500000ull;
       for (auto& kv : g.vram)
         if (kv.second.last_milli != ~0ull) emit_hbm(now, kv.first);  // the GPUs this process has used
     }
-    if (g.foreign_ms && now >= next_foreign) {
-      next_foreign = now + g.foreign_ms * 1000000ull - 500000ull;
-      foreign_tick(now);
+    if (g.foreign_ms) {
+      occ_sample(now);
+      if (now >= next_foreign) {
+        next_foreign = now + g.foreign_ms * 1000000ull - 500000ull;
+        foreign_tick(now);
+      }
+      if (g.verbose && now >= next_report) {
+        next_report = now + 10000000000ull;
+        for (auto& kv : g.occ) {
+          int64_t inflight = 0;
+          {
+            std::lock_guard<std::mutex> lk2(g.mu);
+            inflight = kv.second.inflight;
+          }
+          std::fprintf(stderr,
+                       "[mislo-rocprof] occupancy gpu_id %llu: reads=%llu counted=%llu busy_skips=%llu decisions=%llu "
+                       "emitted=%llu last_share=%.3f inflight=%lld read_us=%.1f self=%u (idle %llu busy %llu)\n",
+                       (unsigned long long)kv.second.gpu_id, (unsigned long long)kv.second.reads,
+                       (unsigned long long)kv.second.cleans, (unsigned long long)kv.second.busy_skips,
+                       (unsigned long long)kv.second.decisions, (unsigned long long)kv.second.emitted, kv.second.share,
+                       (long long)inflight, kv.second.reads ? kv.second.read_ns / 1e3 / kv.second.reads : 0.0,
+                       kv.second.self_pid, (unsigned long long)kv.second.idle_n, (unsigned long long)kv.second.busy_n);
+        }
+      }
     }
   }
 }
@@ -428,19 +560,13 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
     if (g.verbose)
       std::fprintf(stderr, "[mislo-rocprof] GPU %s: vram sysfs %s\n", bdf, v.used_fd >= 0 ? "ok" : "unreadable");
     g.vram[a->id.handle] = v;
-    State::Busy b;
-    b.metrics_fd = open((g.pci_sysfs + "/" + bdf + "/gpu_metrics").c_str(), O_RDONLY | O_CLOEXEC);
-    b.busy_fd = open((g.pci_sysfs + "/" + bdf + "/gpu_busy_percent").c_str(), O_RDONLY | O_CLOEXEC);
-    if (b.metrics_fd >= 0) {  // metrics_table_header: u16 size, u8 format, u8 content revision
-      uint8_t hdr[4] = {0, 0, 0, 0};
-      const ssize_t n = pread(b.metrics_fd, hdr, 4, 0);
-      const unsigned size = hdr[0] | (unsigned)hdr[1] << 8;
-      b.acc = n == 4 && hdr[2] == 1 && (hdr[3] == 7 || hdr[3] == 8) && size >= 80;
+    State::Occ& o = g.occ[a->id.handle];
+    o.gpu_id = a->gpu_id;
+    if (g.verbose) {
+      std::vector<std::pair<uint32_t, uint64_t>> per;
+      std::fprintf(stderr, "[mislo-rocprof] GPU %s: kfd gpu_id %llu occupancy %s\n", bdf, (unsigned long long)a->gpu_id,
+                   kfd_occupancy(a->gpu_id, &per) ? "readable" : "unreadable (no foreign-time signal)");
     }
-    if (g.verbose)
-      std::fprintf(stderr, "[mislo-rocprof] GPU %s: activity %s\n", bdf,
-                   b.acc ? "gpu_metrics accumulator" : b.busy_fd >= 0 ? "gpu_busy_percent" : "unreadable");
-    g.busy[a->id.handle] = b;
   }
   return ROCPROFILER_STATUS_SUCCESS;
 }
@@ -463,7 +589,18 @@ rocprofiler_status_t agents_cb(rocprofiler_agent_version_t, const void** agents,
 void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_user_data_t*, void*) {
   if (rec.kind != ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH) return;
   auto* d = static_cast<rocprofiler_callback_tracing_kernel_dispatch_data_t*>(rec.payload);
-  if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
+  if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_ENTER && d) {
+    // in flight from before the packet is submitted: its completion can only come after this
+    // (counted at the enqueue's exit, a fast kernel's completion could overtake the count)
+    rocprofiler_timestamp_t now = 0;
+    rocprofiler_get_timestamp(&now);
+    std::lock_guard<std::mutex> lk(g.mu);
+    auto oi = g.occ.find(d->dispatch_info.agent_id.handle);
+    if (oi != g.occ.end()) {
+      if (oi->second.inflight++ <= 0) oi->second.last_done = now;
+      ++oi->second.enq_seq, ++oi->second.disp;
+    }
+  } else if (rec.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE && rec.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) {
     rocprofiler_timestamp_t now = 0;
     rocprofiler_get_timestamp(&now);
     std::lock_guard<std::mutex> lk(g.mu);
@@ -483,16 +620,24 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
         enq = it->second;
         g.enqueue_ts.erase(it);
       }
+      if (d) {  // no longer in flight
+        auto oi = g.occ.find(d->dispatch_info.agent_id.handle);
+        if (oi != g.occ.end()) {
+          if (oi->second.inflight > 0 && --oi->second.inflight == 0 && g.foreign_ms) {
+            g.kick.store(true);  // idle now: the sampler reads other processes' occupancy
+            g.scv.notify_one();
+          }
+          rocprofiler_timestamp_t now = 0;
+          rocprofiler_get_timestamp(&now);
+          oi->second.last_done = now;
+        }
+      }
     }
     if (!d) return;
     uint64_t ready = enq.ts;
     bool known = true;
     {
       std::lock_guard<std::mutex> lk(g.mu);
-      // this process's kernel time on the device (merged into a union at the next tick)
-      auto bi = g.busy.find(d->dispatch_info.agent_id.handle);
-      if (bi != g.busy.end() && d->end_timestamp > d->start_timestamp)
-        bi->second.iv.emplace_back(d->start_timestamp, d->end_timestamp);
       if (g.disp_end.size() > 65536) g.disp_end.clear();  // ends whose successor never completed
       g.disp_end[d->dispatch_info.dispatch_id] = d->end_timestamp;
       if (enq.pred) {
@@ -600,7 +745,9 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.hbm_sample_ms = env_u64("MISLO_HBM_SAMPLE_MS", 1000);
   g.foreign_ms = env_u64("MISLO_FOREIGN_MS", 100);
   g.foreign_floor_pct = env_u64("MISLO_FOREIGN_FLOOR_PCT", 10);
-  g.foreign_min_own_pct = env_u64("MISLO_FOREIGN_MIN_OWN_PCT", 1);
+  g.occ_ms = std::max<uint64_t>(1, env_u64("MISLO_OCC_MS", 10));
+  g.foreign_min_samples = env_u64("MISLO_FOREIGN_MIN_SAMPLES", 3);
+  if (const char* kp = std::getenv("MISLO_KFD_PROC")) g.kfd_proc = kp;
   rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, agents_cb, sizeof(rocprofiler_agent_v0_t),
                                      nullptr);
   timespec rt{};
@@ -669,15 +816,44 @@ uint64_t mislo_rocprof_dropped() { return g.dropped.load(); }
 // The calling thread's current request trace (0 = none): kernels it enqueues from now on carry it.
 void mislo_rocprof_set_trace(uint64_t trace_h) { t_trace = trace_h; }
 
-// The last foreign-time interval of the GPU agent with the given index: device activity and this
-// process's own kernel share (percent); returns the intervals measured so far (-1: no such GPU).
-int64_t mislo_rocprof_foreign(int gpu_index, double* dev_pct, double* own_pct) {
+// The last decided foreign-time interval of the GPU agent with the given index: the share of idle
+// readings with other processes' waves on the GPU and their mean occupancy (CUs); returns the
+// intervals decided so far (-1: no such GPU).
+int64_t mislo_rocprof_foreign(int gpu_index, double* share, double* occ_mean) {
   int i = 0;
-  for (auto& kv : g.busy) {
+  for (auto& kv : g.occ) {
     if (i++ != gpu_index) continue;
-    *dev_pct = kv.second.dev_pct;
-    *own_pct = kv.second.own_pct;
-    return (int64_t)kv.second.intervals;
+    *share = kv.second.share;
+    *occ_mean = kv.second.occ_mean;
+    return (int64_t)kv.second.decisions;
+  }
+  return -1;
+}
+
+// This process's own KFD entry (host pid; 0 = not identified yet) on the GPU agent with the given
+// index, and the idle / in-flight readings it was learned from.
+int64_t mislo_rocprof_self(int gpu_index, uint64_t* idle_n, uint64_t* busy_n) {
+  int i = 0;
+  for (auto& kv : g.occ) {
+    if (i++ != gpu_index) continue;
+    *idle_n = kv.second.idle_n;
+    *busy_n = kv.second.busy_n;
+    return kv.second.self_pid;
+  }
+  return -1;
+}
+
+// The occupancy readings' cost on the GPU agent with the given index: readings, their total time
+// (ns) and the readings not counted because a kernel of this process was in flight (before its
+// own entry was identified).
+int64_t mislo_rocprof_occ_cost(int gpu_index, uint64_t* reads, uint64_t* read_ns, uint64_t* busy_skips) {
+  int i = 0;
+  for (auto& kv : g.occ) {
+    if (i++ != gpu_index) continue;
+    *reads = kv.second.reads;
+    *read_ns = kv.second.read_ns;
+    *busy_skips = kv.second.busy_skips;
+    return 0;
   }
   return -1;
 }

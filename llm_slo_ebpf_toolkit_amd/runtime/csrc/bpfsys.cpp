@@ -45,6 +45,26 @@ int bpf_map_info(int fd, BpfMapInfo* out) {
   return 0;
 }
 
+int bpf_map_find(const std::string& name, uint32_t value_size) {
+  uint32_t id = 0;
+  for (;;) {
+    union bpf_attr a;
+    std::memset(&a, 0, sizeof(a));
+    a.start_id = id;
+    if (sys_bpf(BPF_MAP_GET_NEXT_ID, &a) < 0) return -ENOENT;
+    id = a.next_id;
+    union bpf_attr b;
+    std::memset(&b, 0, sizeof(b));
+    b.map_id = id;
+    const int fd = sys_bpf(BPF_MAP_GET_FD_BY_ID, &b);
+    if (fd < 0) continue;  // gone meanwhile, or not permitted
+    BpfMapInfo info;
+    if (bpf_map_info(fd, &info) == 0 && info.name == name && (!value_size || info.value_size == value_size))
+      return fd;
+    close(fd);
+  }
+}
+
 int bpf_map_lookup(int fd, const void* key, void* value) {
   union bpf_attr a;
   std::memset(&a, 0, sizeof(a));

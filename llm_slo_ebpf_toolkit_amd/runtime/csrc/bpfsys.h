@@ -19,6 +19,10 @@ struct BpfMapInfo {
 
 int bpf_obj_get(const std::string& path);
 int bpf_map_info(int fd, BpfMapInfo* out);
+// The first loaded map named `name` (BPF object names: <= 15 chars) whose values are
+// `value_size` bytes (0: any): an fd, or -ENOENT. Needs CAP_SYS_ADMIN (map ids). For maps
+// a probe object keeps private (not pinned by the loader): gpu_kfd.bpf.c hip_activity.
+int bpf_map_find(const std::string& name, uint32_t value_size);
 int bpf_map_lookup(int fd, const void* key, void* value);
 int bpf_map_update(int fd, const void* key, const void* value, uint64_t flags);
 int bpf_map_delete(int fd, const void* key);

@@ -2,6 +2,8 @@
 // the Python model of this file, record for record.
 #include "procsampler.h"
 
+#include "fsread.h"
+
 #include <dirent.h>
 #include <fcntl.h>
 #include <time.h>
@@ -16,40 +18,11 @@ namespace mislo {
 
 namespace {
 
-// Whole small file into `out` (procfs / cgroupfs files are a page at most). False if unreadable.
-bool read_small(const std::string& path, std::string* out) {
-  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return false;
-  char buf[4096];
-  out->clear();
-  for (;;) {
-    const ssize_t n = ::read(fd, buf, sizeof(buf));
-    if (n < 0) {
-      ::close(fd);
-      return false;
-    }
-    if (n == 0) break;
-    out->append(buf, (size_t)n);
-    if (out->size() > (1u << 16)) break;
-  }
-  ::close(fd);
-  return true;
-}
-
 bool readable(const std::string& path) { return ::access(path.c_str(), R_OK) == 0; }
 
 std::string parent(const std::string& d) {
   const size_t k = d.find_last_of('/');
   return k == std::string::npos || k == 0 ? std::string("/") : d.substr(0, k);
-}
-
-std::string join(const std::string& a, const std::string& b) {
-  std::string r = a;
-  while (!r.empty() && r.back() == '/') r.pop_back();
-  size_t i = 0;
-  while (i < b.size() && b[i] == '/') ++i;
-  if (i == b.size()) return r.empty() ? std::string("/") : r;
-  return r + "/" + b.substr(i);
 }
 
 // "name value" line of a flat-keyed file (cpu.stat)
@@ -76,22 +49,6 @@ bool psi_some_us(const std::string& text, uint64_t* v) {
   if (t == std::string::npos) return false;
   *v = std::strtoull(text.c_str() + t + 6, nullptr, 10);
   return true;
-}
-
-uint32_t ns_pid_of(const std::string& proc_root, uint32_t pid) {
-  std::string s;
-  if (!read_small(join(proc_root, std::to_string(pid) + "/status"), &s)) return pid;
-  const size_t k = s.find("\nNSpid:");
-  if (k == std::string::npos) return pid;
-  size_t e = s.find('\n', k + 1);
-  if (e == std::string::npos) e = s.size();
-  // last whitespace-separated field of the line
-  size_t end = e;
-  while (end > k && (s[end - 1] == ' ' || s[end - 1] == '\t')) --end;
-  size_t beg = end;
-  while (beg > k && s[beg - 1] != ' ' && s[beg - 1] != '\t' && s[beg - 1] != ':') --beg;
-  if (beg >= end) return pid;
-  return (uint32_t)std::strtoul(s.c_str() + beg, nullptr, 10);
 }
 
 }  // namespace

@@ -19,6 +19,7 @@
 #include "bpfring.h"
 #include "bpfsys.h"
 #include "probesim.h"
+#include "gpusampler.h"
 #include "procsampler.h"
 #include "replay.h"
 #include "ring.h"
@@ -503,6 +504,90 @@ class PyProcSampler {
   std::unique_ptr<ProcSampler> s_;
 };
 
+// gpusampler.h: the agent's KFD occupancy / eviction sampler thread, pushing into a user ring.
+class PyGpuSampler {
+ public:
+  PyGpuSampler(HostRing* ring, uint32_t node_id, const std::string& kfd_proc, const std::string& proc_root,
+               uint64_t floor_pct, uint64_t min_samples, uint64_t evict_floor_ns, bool evictions) {
+    GpuSamplerConfig c;
+    c.node_id = node_id;
+    c.kfd_proc = kfd_proc;
+    c.proc_root = proc_root;
+    c.floor_pct = floor_pct;
+    c.min_samples = min_samples;
+    c.evict_floor_ns = evict_floor_ns;
+    c.evictions = evictions;
+    s_ = std::make_unique<GpuSampler>(ring ? ring->ring() : nullptr, c);
+  }
+  void set_target_list(const std::vector<std::pair<uint32_t, uint32_t>>& v) {
+    py::gil_scoped_release nogil;
+    s_->set_targets(v);
+  }
+  void set_hip_map(int fd) { s_->set_hip_map(fd); }
+  void set_hip_activity(uint32_t pid, uint64_t launches, uint64_t copies, uint64_t sync_ns, uint64_t syncs) {
+    HipActivity a;
+    a.launches = launches, a.copies = copies, a.sync_ns = sync_ns, a.syncs = syncs;
+    s_->set_hip_activity(pid, a);
+  }
+  void sample() {
+    py::gil_scoped_release nogil;
+    s_->sample();
+  }
+  py::bytes decide(int64_t wall_ns, uint64_t mono_ns) {
+    std::vector<EventRec> r;
+    {
+      py::gil_scoped_release nogil;
+      r = s_->decide(wall_ns, mono_ns);
+    }
+    return py::bytes(reinterpret_cast<const char*>(r.data()), r.size() * sizeof(EventRec));
+  }
+  void start(double sample_s, double decide_s) {
+    if (!(sample_s > 0) || !(decide_s >= sample_s)) throw std::invalid_argument("need 0 < sample_s <= decide_s");
+    s_->start((uint64_t)(sample_s * 1e9), (uint64_t)(decide_s * 1e9));
+  }
+  void stop() {
+    py::gil_scoped_release nogil;
+    s_->stop();
+  }
+  uint32_t mask() const { return s_->mask(); }
+  void set_mask(uint32_t m) { s_->set_mask(m); }
+  bool paused() const { return s_->paused(); }
+  void set_paused(bool p) { s_->set_paused(p); }
+  py::dict stats() {
+    GpuSamplerStats st = s_->stats();
+    py::dict d;
+    d["samples"] = st.samples;
+    d["reads"] = st.reads;
+    d["sample_ns"] = st.read_ns;
+    d["max_sample_ns"] = st.max_sample_ns;
+    d["decisions"] = st.decisions;
+    d["emitted"] = st.emitted;
+    d["dropped"] = st.dropped;
+    d["evictions"] = st.evictions;
+    d["pairs"] = st.pairs;
+    return d;
+  }
+  py::list shares() {
+    py::list out;
+    for (const GpuShare& g : s_->shares()) {
+      py::dict d;
+      d["pod"] = g.pod;
+      d["gpu_id"] = g.gpu_id;
+      d["samples"] = g.samples;
+      d["hot"] = g.hot;
+      d["own_hot"] = g.own_hot;
+      d["share"] = g.share;
+      d["foreign_mean"] = g.foreign_mean;
+      d["active"] = g.active;
+      out.append(d);
+    }
+    return out;
+  }
+
+ private:
+  std::unique_ptr<GpuSampler> s_;
+};
+
 class PyBpfMap {
  public:
   explicit PyBpfMap(const std::string& path) {
@@ -675,6 +760,23 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def_property_readonly("layout", &PyAssembler::layout);
   m.def("slot_layout", [](uint32_t g, uint32_t s, uint32_t n, uint32_t r) { return layout_dict(slot_layout(g, s, n, r)); },
         py::arg("group_cap"), py::arg("span_cap"), py::arg("sig_cap"), py::arg("row_cap"));
+  py::class_<PyGpuSampler>(m, "GpuSampler")
+      .def(py::init<HostRing*, uint32_t, const std::string&, const std::string&, uint64_t, uint64_t, uint64_t, bool>(),
+           py::arg("ring"), py::arg("node_id") = 0, py::arg("kfd_proc") = "/sys/class/kfd/kfd/proc",
+           py::arg("proc_root") = "/proc", py::arg("floor_pct") = 10, py::arg("min_samples") = 3,
+           py::arg("evict_floor_ns") = 1000000, py::arg("evictions") = true, py::keep_alive<1, 2>())
+      .def("set_target_list", &PyGpuSampler::set_target_list)
+      .def("set_hip_map", &PyGpuSampler::set_hip_map)
+      .def("set_hip_activity", &PyGpuSampler::set_hip_activity, py::arg("pid"), py::arg("launches"),
+           py::arg("copies") = 0, py::arg("sync_ns") = 0, py::arg("syncs") = 0)
+      .def("sample", &PyGpuSampler::sample)
+      .def("decide", &PyGpuSampler::decide, py::arg("wall_ns"), py::arg("mono_ns"))
+      .def("start", &PyGpuSampler::start, py::arg("sample_s"), py::arg("decide_s"))
+      .def("stop", &PyGpuSampler::stop)
+      .def("stats", &PyGpuSampler::stats)
+      .def("shares", &PyGpuSampler::shares)
+      .def_property("mask", &PyGpuSampler::mask, &PyGpuSampler::set_mask)
+      .def_property("paused", &PyGpuSampler::paused, &PyGpuSampler::set_paused);
   py::class_<PyProcSampler>(m, "ProcSampler")
       .def(py::init<HostRing*, uint32_t, const std::string&, const std::string&, bool, uint64_t, uint64_t, uint64_t,
                     uint64_t>(),
@@ -707,6 +809,8 @@ PYBIND11_MODULE(_mislo_rt, m) {
       py::arg("pid") = -1, "perf_event_open of a uprobe; an fd or -errno");
   m.def("bpf_link_create_perf", &bpf_link_create_perf, py::arg("prog_fd"), py::arg("perf_fd"),
         "BPF_LINK_CREATE(prog, perf event); a link fd or -errno");
+  m.def("bpf_map_find", &bpf_map_find, py::arg("name"), py::arg("value_size") = 0,
+        "fd of the first loaded BPF map of that name (and value size), or -errno");
   m.def("bpf_obj_get", &bpf_obj_get, py::arg("path"), "BPF_OBJ_GET of a pinned object; an fd or -errno");
   m.def("close_fd", &close_fd);
   m.attr("REC_STRIDE") = kRecStride;

@@ -248,13 +248,16 @@ class ShedLadder:
         return "sampler:paused"
 
     def _gpu(self) -> Optional[str]:
-        r = self.user_ring
-        if r is None:
+        # every worker's user ring (split rings): each GPU producer obeys the ring it writes to
+        rings = self.user_ring if isinstance(self.user_ring, (list, tuple)) else [self.user_ring]
+        rings = [r for r in rings if r is not None]
+        if not rings:
             return None
         for name in self.order:
             spec = self._catalog.BY_NAME[name]
-            if spec.gpu and not int(r.drop_mask) >> spec.kernel_type & 1:
-                r.drop_mask = int(r.drop_mask) | (1 << spec.kernel_type)
+            if spec.gpu and not int(rings[0].drop_mask) >> spec.kernel_type & 1:
+                for r in rings:
+                    r.drop_mask = int(r.drop_mask) | (1 << spec.kernel_type)
                 return f"gpu:{name}"
         return None
 

@@ -276,7 +276,8 @@ w = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
 v = torch.randn(1, 4096, device="cuda", dtype=torch.bfloat16)
 s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 torch.cuda.synchronize()
-dev, own = ctypes.c_double(), ctypes.c_double()
+lib.mislo_rocprof_occ_cost.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint64)] * 3
+share, occ = ctypes.c_double(), ctypes.c_double()
 
 def serve(seconds, two_streams, decode=False):
     # a service's duty cycle: ~6 ms of GEMMs every 15 ms, on one stream or two concurrent ones;
@@ -296,8 +297,8 @@ def serve(seconds, two_streams, decode=False):
         else:
             a = [x @ x for _ in range(48)]
         torch.cuda.synchronize()
-        n = lib.mislo_rocprof_foreign(0, ctypes.byref(dev), ctypes.byref(own))
-        print("foreign", time.time_ns(), n, round(dev.value, 1), round(own.value, 1), flush=True)
+        n = lib.mislo_rocprof_foreign(0, ctypes.byref(share), ctypes.byref(occ))
+        print("foreign", time.time_ns(), n, round(share.value, 3), round(occ.value, 1), int(decode), flush=True)
         time.sleep(0.009)
 
 serve(1.5, False)
@@ -307,6 +308,22 @@ print("phase_b", time.time_ns(), flush=True)
 sys.stdin.readline()  # the test has started another process's GEMMs
 print("contended", time.time_ns(), flush=True)
 serve(2.0, False)
+print("decode", time.time_ns(), flush=True)
+serve(2.0, False, decode=True)
+print("saturated", time.time_ns(), flush=True)
+end = time.time() + 2.5
+while time.time() < end:  # a saturated server: its kernels are always in flight
+    a = [x @ x for _ in range(200)]
+    torch.cuda.synchronize()
+    n = lib.mislo_rocprof_foreign(0, ctypes.byref(share), ctypes.byref(occ))
+    print("foreign", time.time_ns(), n, round(share.value, 3), round(occ.value, 1), 2, flush=True)
+lib.mislo_rocprof_self.restype = ctypes.c_int64
+lib.mislo_rocprof_self.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+i_n, b_n = ctypes.c_uint64(), ctypes.c_uint64()
+print("self", lib.mislo_rocprof_self(0, ctypes.byref(i_n), ctypes.byref(b_n)), i_n.value, b_n.value, flush=True)
+r, ns, sk = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+lib.mislo_rocprof_occ_cost(0, ctypes.byref(r), ctypes.byref(ns), ctypes.byref(sk))
+print("cost", r.value, ns.value, sk.value, flush=True)
 print("done", time.time_ns(), flush=True)
 """
 
@@ -325,12 +342,12 @@ while time.time() < end:
 
 @pytest.mark.gpu
 def test_foreign_gpu_time_separates_another_process_from_the_services_own_concurrency():
-    """gpu_queue_delay_ms (b): the device's activity accumulator minus the process's own kernel
-    time. Alone -- on one stream or two concurrent ones -- the process sees no foreign time and
-    the tool emits no foreign record; with another process's GEMMs on the GPU every interval
-    shows it and the tool emits records of >= 10 % of the interval."""
-    import threading
-
+    """gpu_queue_delay_ms (b): other processes' wave occupancy (KFD per-process cu_occupancy) read
+    while this process has no kernel in flight -- and, once the tool has learned which KFD entry is
+    its own, at any time. Alone -- one stream, two concurrent ones, or a decode loop of microsecond
+    kernels -- the share is ~0 and the tool emits no foreign record; with another process's GEMMs
+    on the GPU it is high for a GEMM service, a decode loop AND a saturated server that never
+    idles, and the tool emits records of >= 10 % of the interval."""
     from llm_slo_ebpf_toolkit_amd.collector import records
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
@@ -343,12 +360,14 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     burner = None
     lines = []
+    t_burn = 0
     try:
         for ln in w.stdout:
             lines.append(ln.split())
             if ln.startswith("phase_b"):
                 burner = subprocess.Popen([sys.executable, "-u", "-c", BURNER], stdout=subprocess.PIPE, text=True)
                 assert burner.stdout.readline().startswith("burning")
+                t_burn = time.time_ns()
                 time.sleep(0.3)
                 w.stdin.write("go\n")
                 w.stdin.flush()
@@ -363,20 +382,35 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
     err = w.stderr.read()
     assert w.returncode == 0, err[-2000:]
     t_b = int(next(x[1] for x in lines if x[0] == "contended"))
-    alone = [(float(x[3]), float(x[4])) for x in lines if x[0] == "foreign" and int(x[1]) < t_b and int(x[2]) > 2]
-    shared = [(float(x[3]), float(x[4])) for x in lines if x[0] == "foreign" and int(x[1]) > t_b + 300_000_000]
-    assert alone and shared, lines[-5:]
-    f_alone = float(np.percentile([d - o for d, o in alone], 90))  # every alone phase, decode-like included
-    f_shared = np.median([d - o for d, o in shared])
+    t_d = int(next(x[1] for x in lines if x[0] == "decode"))
+    t_s = int(next(x[1] for x in lines if x[0] == "saturated"))
+    self_pid, idle_n, busy_n = (int(v) for v in next(x[1:] for x in lines if x[0] == "self"))
+    reads, read_ns, skips = (int(v) for v in next(x[1:] for x in lines if x[0] == "cost"))
+    fl = [x for x in lines if x[0] == "foreign"]
+    alone = [float(x[3]) for x in fl if int(x[1]) < t_b and int(x[2]) > 2]
+    gemm = [float(x[3]) for x in fl if t_b + 300_000_000 < int(x[1]) < t_d]
+    decode = [float(x[3]) for x in fl if t_d + 300_000_000 < int(x[1]) < t_s]
+    sat = [float(x[3]) for x in fl if int(x[1]) > t_s + 1_200_000_000]
+    assert alone and gemm and decode, lines[-5:]
     recs = np.concatenate([np.frombuffer(ring.records_view()[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
                            for _, i, c in ring.peek(1 << 16)]) if ring.peek(1 << 16) else np.zeros(0, records.EVENT)
     q = recs[recs["signal_type"] == 13]
     big = q[q["value"] >= 10_000_000]  # foreign records: >= 10 % of a 100 ms interval
-    before, after = int((big["ts_ns"] < t_b).sum()), int((big["ts_ns"] > t_b).sum())
-    print({"foreign_alone_median": f_alone, "foreign_shared_median": f_shared, "records_alone": before,
-           "records_shared": after, "alone": alone[:6], "shared": shared[:6]})
-    assert f_alone < 10.0 and before <= 1, (f_alone, before, alone[-12:])
-    assert f_shared >= 25.0 and after >= 5, (f_shared, after, shared[:10])
+    ts = big["ts_ns"]
+    before = int((ts < t_burn - 100_000_000).sum())  # (a record's interval may straddle the burner's start)
+    in_gemm, in_decode = int(((ts > t_b) & (ts < t_d)).sum()), int(((ts > t_d) & (ts < t_s)).sum())
+    in_sat = int((ts > t_s).sum())
+    res = {"share_alone_p90": float(np.percentile(alone, 90)), "share_gemm_median": float(np.median(gemm)),
+           "share_decode_median": float(np.median(decode)), "records_alone": before, "records_gemm": in_gemm,
+           "records_decode": in_decode, "occ_reads": reads, "occ_read_us_mean": read_ns / max(reads, 1) / 1e3,
+           "busy_skips": skips, "self_pid": self_pid, "idle_readings": idle_n, "busy_readings": busy_n,
+           "share_saturated_median": float(np.median(sat)) if sat else None, "records_saturated": in_sat}
+    print(res)
+    assert res["share_alone_p90"] < 0.10 and before <= 1, (res, alone[-12:])
+    assert res["share_gemm_median"] >= 0.5 and in_gemm >= 5, (res, gemm[:10])
+    assert res["share_decode_median"] >= 0.5 and in_decode >= 5, (res, decode[:10])
+    # a saturated server never idles: its own KFD entry, learned earlier, is left out of every reading
+    assert self_pid > 0 and res["share_saturated_median"] >= 0.5 and in_sat >= 5, res
 
 
 @pytest.mark.gpu

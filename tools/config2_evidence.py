@@ -159,6 +159,9 @@ def main() -> int:
                                                               "answers keep requests completing in every window")
     ap.add_argument("--clients", type=int, default=2, help="concurrent closed-loop clients")
     ap.add_argument("--gap-s", type=float, default=0.05, help="client think time between requests")
+    ap.add_argument("--halo-ms", type=int, default=3000,
+                    help="agent halo: a contended request's span arrives ~1-2 s after its start (its TTFT plus "
+                         "the exporter's batch delay), and its records are joined around that start")
     ap.add_argument("--window-ms", type=int, default=2000,
                     help="agent window: under the fault a request takes over a second, so 2 s windows")
     ap.add_argument("--model-path", default=MODEL, help="the agent's model ('' = the bayes_gpu expert table)")
@@ -182,7 +185,7 @@ def main() -> int:
         [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "shm",
          "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
          "--window-ms", str(a.window_ms), "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
-         *model_args, "--min-confidence", "0.3", "--halo-ms", "1500", "--ttft-slo-ms", str(a.ttft_slo_ms),
+         *model_args, "--min-confidence", "0.3", "--halo-ms", str(a.halo_ms), "--ttft-slo-ms", str(a.ttft_slo_ms),
          "--output", "jsonl", "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
     llm_env = dict(env, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1",
                    OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces",
@@ -285,7 +288,7 @@ def main() -> int:
     res["agent_counters_by_phase"] = counters
     res["setup"] = {"preset": a.preset, "ttft_slo_ms": a.ttft_slo_ms, "burners": a.burners,
                     "prompt_words": a.prompt_words, "max_tokens": a.max_tokens, "clients": a.clients,
-                    "window_ms": a.window_ms, "phase_s": a.phase_s, "recover_s": a.recover_s,
+                    "window_ms": a.window_ms, "halo_ms": a.halo_ms, "phase_s": a.phase_s, "recover_s": a.recover_s,
                     "model": os.path.relpath(a.model_path, ROOT) if a.model_path else "bayes_gpu",
                     "observable_signals": list(GPU_SIGNALS) if a.model_path else "all",
                     "fault": f"{a.burners} processes of back-to-back 8192^3 bf16 GEMMs on the service's GPU"}
