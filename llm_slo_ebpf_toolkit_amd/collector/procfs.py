@@ -103,6 +103,10 @@ CFS_TYPE = 12              # catalogue kernel type of cfs_throttled_ms (ns in th
 # its CPUs at a few percent (config-3 baseline on MI355X: 27 of ~150 intervals of the RAG service
 # at 2-8 %, 7 above 8 %; under the CPU fault every interval well above 8 %, profiles/r4_config3_first)
 STEAL_FLOOR_MILLI = 20000
+# ... held for this many consecutive intervals: the healthy service's threads still crossed 20 % in
+# ~1 of 30 intervals, one at a time (5 cpu_throttle false positives in 15 baseline windows,
+# profiles/r4_config3_gated), while a starved service stays above it in every interval
+STEAL_SUSTAIN = 3
 SIGNAL_TYPES = {"runqueue_delay_ms": RUNQUEUE_TYPE, "cpu_steal_pct": STEAL_TYPE,
                 "mem_reclaim_latency_ms": MEM_RECLAIM_TYPE, "cfs_throttled_ms": CFS_TYPE}
 ALL_MASK = sum(1 << t for t in SIGNAL_TYPES.values())
@@ -197,11 +201,13 @@ class SchedstatSampler:
     def __init__(self, targets: Callable[[], Dict[int, int]], push: Callable[[np.ndarray], int], rec: int = 24,
                  proc_root: str = "/proc", floor_ns: int = FLOOR_NS, node_id: int = 0,
                  cgroup_root: str = "/sys/fs/cgroup", cpu_psi: bool = False,
-                 steal_floor_milli: int = STEAL_FLOOR_MILLI):
+                 steal_floor_milli: int = STEAL_FLOOR_MILLI, steal_sustain: int = STEAL_SUSTAIN):
         """``targets()`` -> {pid: pod id}; ``push(records)`` -> records accepted (the user ring)."""
         self.targets, self.push, self.rec = targets, push, int(rec)
         self.proc_root, self.floor_ns, self.node_id = proc_root, int(floor_ns), int(node_id)
         self.cgroup_root, self.cpu_psi, self.steal_floor = cgroup_root, bool(cpu_psi), int(steal_floor_milli)
+        self.steal_sustain = max(1, int(steal_sustain))
+        self._steal_run: Dict[int, int] = {}  # pid -> consecutive intervals at the floor
         self.mask = ALL_MASK
         self.paused = False
         self._prev: Dict[Tuple[int, int], Tuple[int, int]] = {}
@@ -268,7 +274,9 @@ class SchedstatSampler:
             psi_d = self._group_delta(cpu, 1, cache) if cpu else 0  # read every tick
             if self.mask >> STEAL_TYPE & 1 and dt:
                 milli = max(int(float(w_all) * 100000.0 / float(dt)), int(float(psi_d) * 100000.0 / float(dt)))
-                if milli >= self.steal_floor:
+                run = self._steal_run.get(pid, 0) + 1 if milli >= self.steal_floor else 0
+                self._steal_run[pid] = run
+                if run >= self.steal_sustain:
                     rows.append((STEAL_TYPE, npid, pid, pod, milli))
             if cfs:
                 d = self._group_delta(cfs, 0, cache)
@@ -280,6 +288,7 @@ class SchedstatSampler:
                     rows.append((MEM_RECLAIM_TYPE, npid, pid, pod, d))
         self._prev = nxt
         self._procs = live
+        self._steal_run = {p: r for p, r in self._steal_run.items() if p in live}
         self._groups = {k: v for k, v in self._groups.items() if k in cache}
         self.samples += 1
         ev = np.zeros(len(rows), dtype=records.EVENT)
@@ -333,13 +342,14 @@ class NativeSampler:
 
     def __init__(self, ring, targets: Callable[[], Dict[int, int]], node_id: int = 0, proc_root: str = "/proc",
                  cgroup_root: str = "/sys/fs/cgroup", cpu_psi: bool = False, floor_ns: int = FLOOR_NS,
-                 steal_floor_milli: int = STEAL_FLOOR_MILLI, refresh_s: float = 10.0):
+                 steal_floor_milli: int = STEAL_FLOOR_MILLI, refresh_s: float = 10.0,
+                 steal_sustain: int = STEAL_SUSTAIN):
         from ..runtime import load
 
         rt = load()
         self.targets, self.refresh_s = targets, float(refresh_s)
         self.native = rt.ProcSampler(ring, node_id, proc_root, cgroup_root, bool(cpu_psi), int(floor_ns),
-                                     int(steal_floor_milli), int(floor_ns), int(floor_ns))
+                                     int(steal_floor_milli), int(floor_ns), int(floor_ns), int(steal_sustain))
         self._stop = threading.Event()
         self._thr: Optional[threading.Thread] = None
 

@@ -7,7 +7,8 @@
 // the value in fixed point by the probes' own rule, mislo_record.h mislo_milli; USER24 packs
 // pid / type / pod id and keeps the timestamp's low 44 bits -- 3/8 of the PCIe bytes of EVENT):
 //
-//   type 13 gpu_queue_delay_ms   (a) kernel dispatch: start - max(enqueue return, queue predecessor end) (ns);
+//   type 13 gpu_queue_delay_ms   (a) kernel dispatch: start - max(enqueue return, queue predecessor end),
+//                                when another process's waves were on the GPU during the wait (ns);
 //                                (b) foreign GPU time: every MISLO_FOREIGN_MS (default 100) while this
 //                                process runs kernels, the share of the interval other processes'
 //                                waves held the GPU, as ns of the interval, when it reaches
@@ -64,7 +65,10 @@
 // direction; a pair's calibration starts there and a measured rate may only raise it, to at most
 // 4x: a link already degraded when the process starts is not its own baseline),
 // MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_OCC_MS, MISLO_FOREIGN_MIN_SAMPLES (default 3 idle
-// samples per interval), MISLO_KFD_PROC (default /sys/class/kfd/kfd/proc), MISLO_ROCPROF_VERBOSE.
+// samples per interval), MISLO_KFD_PROC (default /sys/class/kfd/kfd/proc), MISLO_WAIT_NEEDS_FOREIGN
+// (default 1: with KFD occupancy readable, a dispatch wait is emitted only if another process held
+// waves on the GPU during it -- a CPU-starved process's kernels wait behind its own host-staged
+// copies and barriers too; 0 = every wait above the floor), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/buffer_tracing.h>
 #include <rocprofiler-sdk/callback_tracing.h>
@@ -184,6 +188,13 @@ struct State {
     // last decided interval and the reading cost (tests, overhead accounting)
     double share = 0.0, occ_mean = 0.0;
     uint64_t decisions = 0, reads = 0, read_ns = 0, cleans = 0, emitted = 0;
+    // mu: the latest counted reading with other processes' waves on the GPU (ns; 0 = never) and
+    // whether readings work at all -- a dispatch wait counts as contention only when foreign waves
+    // were seen during it (a host-starved process's kernels also wait, behind its own staged
+    // copies and host-signalled barriers: profiles/r4_config3 read that as gpu_contention)
+    uint64_t last_foreign = 0;
+    bool readable = false;
+    uint64_t waits_emitted = 0, waits_unconfirmed = 0;
     // which KFD entry is this process (a container's pid namespace hides its host pid): the entry
     // that never holds waves while this process has none in flight, and most often does while it
     // has -- learned from the readings; once known, every reading counts, in flight or not
@@ -196,6 +207,7 @@ struct State {
   };
   std::map<uint64_t, Occ> occ;
   uint64_t foreign_ms = 100, foreign_floor_pct = 10, occ_ms = 10, foreign_min_samples = 3;
+  bool wait_needs_foreign = true;
   std::string kfd_proc = "/sys/class/kfd/kfd/proc";
   std::string pci_sysfs = "/sys/bus/pci/devices";
   uint64_t hbm_sample_ms = 1000;
@@ -444,6 +456,11 @@ void occ_sample(uint64_t now) {
       continue;
     }
     const uint64_t foreign = total - (idle ? 0 : self);
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      o.readable = true;
+      if (foreign > 0) o.last_foreign = now;
+    }
     if (!o.clean) o.t_first = now;
     ++o.clean, ++o.cleans;
     o.occ_sum += (double)foreign;
@@ -529,10 +546,15 @@ void sampler_main() {
         next_report = now + 10000000000ull;
         for (auto& kv : g.occ) {
           int64_t inflight = 0;
+          uint64_t w_ok = 0, w_no = 0;
           {
             std::lock_guard<std::mutex> lk2(g.mu);
             inflight = kv.second.inflight;
+            w_ok = kv.second.waits_emitted, w_no = kv.second.waits_unconfirmed;
           }
+          std::fprintf(stderr,
+                       "[mislo-rocprof] occupancy gpu_id %llu: dispatch waits emitted=%llu unconfirmed=%llu\n",
+                       (unsigned long long)kv.second.gpu_id, (unsigned long long)w_ok, (unsigned long long)w_no);
           std::fprintf(stderr,
                        "[mislo-rocprof] occupancy gpu_id %llu: reads=%llu counted=%llu busy_skips=%llu decisions=%llu "
                        "emitted=%llu last_share=%.3f inflight=%lld read_us=%.1f self=%u (idle %llu busy %llu)\n",
@@ -636,8 +658,17 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     if (!d) return;
     uint64_t ready = enq.ts;
     bool known = true;
+    uint64_t last_foreign = 0;
+    bool gated = false;
+    State::Occ* occ = nullptr;
     {
       std::lock_guard<std::mutex> lk(g.mu);
+      auto oi = g.occ.find(d->dispatch_info.agent_id.handle);
+      if (oi != g.occ.end() && g.foreign_ms && g.wait_needs_foreign && oi->second.readable) {
+        occ = &oi->second;
+        gated = true;
+        last_foreign = occ->last_foreign;
+      }
       if (g.disp_end.size() > 65536) g.disp_end.clear();  // ends whose successor never completed
       g.disp_end[d->dispatch_info.dispatch_id] = d->end_timestamp;
       if (enq.pred) {
@@ -652,8 +683,15 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     }
     if (known && enq.ts && d->start_timestamp > ready) {
       const uint64_t delay = d->start_timestamp - ready;
-      if (delay >= g.queue_floor_ns)
-        emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id, enq.trace_h);
+      // with occupancy readable: only a wait during which another process held waves (one
+      // reading period of slack: readings are MISLO_OCC_MS apart)
+      const bool confirmed = !gated || last_foreign + g.occ_ms * 1000000ull >= ready;
+      if (delay >= g.queue_floor_ns) {
+        if (confirmed)
+          emit(kQueueDelay, d->start_timestamp, delay, (uint32_t)rec.thread_id, enq.trace_h);
+        std::lock_guard<std::mutex> lk(g.mu);
+        if (occ) ++(confirmed ? occ->waits_emitted : occ->waits_unconfirmed);
+      }
     }
   }
 }
@@ -747,6 +785,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.foreign_floor_pct = env_u64("MISLO_FOREIGN_FLOOR_PCT", 10);
   g.occ_ms = std::max<uint64_t>(1, env_u64("MISLO_OCC_MS", 10));
   g.foreign_min_samples = env_u64("MISLO_FOREIGN_MIN_SAMPLES", 3);
+  g.wait_needs_foreign = env_u64("MISLO_WAIT_NEEDS_FOREIGN", 1) != 0;
   if (const char* kp = std::getenv("MISLO_KFD_PROC")) g.kfd_proc = kp;
   rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, agents_cb, sizeof(rocprofiler_agent_v0_t),
                                      nullptr);
@@ -826,6 +865,20 @@ int64_t mislo_rocprof_foreign(int gpu_index, double* share, double* occ_mean) {
     *share = kv.second.share;
     *occ_mean = kv.second.occ_mean;
     return (int64_t)kv.second.decisions;
+  }
+  return -1;
+}
+
+// Dispatch waits (>= the queue floor) on the GPU agent with the given index: emitted (foreign waves
+// seen during the wait, or occupancy unreadable) and withheld; -1 for an unknown index.
+int64_t mislo_rocprof_waits(int gpu_index, uint64_t* emitted, uint64_t* unconfirmed) {
+  int i = 0;
+  std::lock_guard<std::mutex> lk(g.mu);
+  for (auto& kv : g.occ) {
+    if (i++ != gpu_index) continue;
+    *emitted = kv.second.waits_emitted;
+    *unconfirmed = kv.second.waits_unconfirmed;
+    return 0;
   }
   return -1;
 }

@@ -201,7 +201,6 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
     auto pit = procs_.find(pid);
     Proc pr = pit != procs_.end() ? pit->second : Proc{};
     if (!pr.resolved) resolve(pid, pr);
-    live[pid] = pr;
     if ((mask >> kSigRunq & 1) && s_sum && w_sum / s_sum >= cfg_.runq_floor_ns)
       rec(kSigRunq, pr.ns_pid, pid, pod, w_sum / s_sum);
     const uint64_t psi_d = pr.cpu_psi_file.empty() ? 0 : group_delta(pr.cpu_psi_file, 1);  // read every tick
@@ -209,8 +208,10 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
       uint64_t milli = (uint64_t)((double)w_all * 100000.0 / (double)dt);  // milli-percent of one CPU
       const uint64_t m2 = (uint64_t)((double)psi_d * 100000.0 / (double)dt);
       if (m2 > milli) milli = m2;
-      if (milli >= cfg_.steal_floor_milli) rec(kSigSteal, pr.ns_pid, pid, pod, milli);
+      pr.steal_run = milli >= cfg_.steal_floor_milli ? pr.steal_run + 1 : 0;
+      if (pr.steal_run >= std::max<uint32_t>(1, cfg_.steal_sustain)) rec(kSigSteal, pr.ns_pid, pid, pod, milli);
     }
+    live[pid] = pr;
     if (!pr.cfs_file.empty()) {
       ++cfs_groups;
       const uint64_t d = group_delta(pr.cfs_file, 0);

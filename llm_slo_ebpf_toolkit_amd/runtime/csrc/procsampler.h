@@ -17,7 +17,9 @@
 //                              interval, in percent of one CPU (sum over its threads of the
 //                              run-queue wait / interval): the process's view of stolen CPU. Under
 //                              EEVDF a starved thread waits a short time per wakeup but most of the
-//                              interval in total, so this fires where the per-wakeup mean does not
+//                              interval in total, so this fires where the per-wakeup mean does not.
+//                              Emitted once the share has stayed at the floor for steal_sustain
+//                              intervals in a row: a service's own threads spike past it now and then
 //   type 7  mem_reclaim_latency_ms  PSI memory stall of the process's group over the interval
 //   type 12 cfs_throttled_ms   CFS bandwidth throttling of the process's quota group over the interval
 //
@@ -46,6 +48,7 @@ struct ProcSamplerConfig {
   uint32_t node_id = 0;
   uint64_t runq_floor_ns = 100000;    // runqueue_delay.bpf.c emit floor (100 us per timeslice)
   uint64_t steal_floor_milli = 20000; // 20 % of one CPU over the interval (collector/procfs.py STEAL_FLOOR_MILLI)
+  uint32_t steal_sustain = 3;         // ... in this many consecutive intervals (procfs.py STEAL_SUSTAIN)
   uint64_t cfs_floor_ns = 100000;
   uint64_t mem_floor_ns = 100000;
   bool cgroup_cpu_psi = false;        // cpu_steal_pct = max(wait share, the group's cpu.pressure share)
@@ -87,6 +90,7 @@ class ProcSampler {
   };
   struct Proc {
     uint32_t ns_pid = 0;
+    uint32_t steal_run = 0;  // consecutive intervals with the wait share at the floor
     bool resolved = false;
     std::string cfs_file, mem_file, cpu_psi_file;  // empty: none
   };

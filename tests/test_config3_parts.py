@@ -28,7 +28,8 @@ def test_schedstat_sampler_emits_mean_wait_per_slice_above_the_floor(tmp_path):
     write_schedstat(tmp_path, 200, 200, 1, 1, 1)
     pushed = []
     s = procfs.SchedstatSampler(lambda: {100: 7, 200: 9}, lambda u: pushed.append(u) or len(u), rec=24,
-                                proc_root=str(tmp_path), node_id=3, steal_floor_milli=1000)  # 1 %: see the steal record
+                                proc_root=str(tmp_path), node_id=3, steal_floor_milli=1000,  # 1 %: see the steal record
+                                steal_sustain=1)
     assert len(s.sample(10**18)) == 0  # first look: no deltas yet
     write_schedstat(tmp_path, 100, 100, 9_000_000, 1_000_000 + 4 * 2_000_000, 14)  # 2 ms per slice
     write_schedstat(tmp_path, 100, 101, 9_000_000, 1_000_000 + 4 * 50_000, 14)     # 50 us per slice: below

@@ -77,3 +77,43 @@ def test_replay_window_shapes():
     assert win.n_events == 5000 and win.n_spans == 100
     assert np.all(np.diff(win.events["ts_ns"]) >= 0)
     assert win.group_labels.shape == (win.n_groups,)
+
+
+def _same_join(a, b):
+    np.testing.assert_array_equal(a.top3, b.top3)
+    np.testing.assert_array_equal(a.cnt, b.cnt)
+    np.testing.assert_array_equal(a.attrs, b.attrs)
+    np.testing.assert_array_equal(a.conf, b.conf)
+    np.testing.assert_array_equal(a.gsum, b.gsum)
+    np.testing.assert_array_equal(a.gcnt, b.gcnt)
+    np.testing.assert_array_equal(a.feat, b.feat)
+    assert a.debug == b.debug
+
+
+def test_indexed_join_is_the_bruteforce_join():
+    """oracle.join (per-key time-sorted indexes: each span looks only at rows that share one of
+    its tier keys within the tier's reach) gives the brute-force all-pairs join bit for bit --
+    top-3 keys, counts, attributes, confidences, group sums, features and every debug counter --
+    across scenarios, both group modes, the 100 ms / 2 s windows and imported halo rows."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
+
+    for seed, scen in ((11, "full"), (12, "mixed"), (13, "baseline")):
+        cfg = ReplayConfig(scenario=scen, n_nodes=2, pods_per_node=8, n_services=8, events_per_window=4000,
+                           spans_per_window=200, seed=seed)
+        g = ReplayGenerator(cfg)
+        wins = [g.next_window() for _ in range(2)]
+        for w in wins:
+            d = oracle.decode_events(w.events)
+            for kw in ({}, {"window_ms": 100.0}, {"group_mode": 0}, {"threshold": 0.6, "fanout": 2}):
+                _same_join(oracle.join(d, w.spans, w.n_groups, **kw), oracle.join_bruteforce(d, w.spans, w.n_groups, **kw))
+        # the ring path: framed records + user rows, then the previous window's rows as imports
+        imgs = build_replay_images(wins, user_rec=24)
+        table, tmap = oracle.CtxTable(), oracle.TraceMap()
+        prev = oracle.empty_rows()
+        for w, img in zip(wins, imgs):
+            oracle.apply_ring_defs(img.framed, table, tmap, {})
+            d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases)
+            dd = oracle.concat(d, prev)
+            sp = oracle.spans_native(img.spans, tmap)
+            _same_join(oracle.join(dd, sp, w.n_groups), oracle.join_bruteforce(dd, sp, w.n_groups))
+            prev = d

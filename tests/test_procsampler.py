@@ -75,14 +75,14 @@ def advance(proc, q, v1=False):
     psi(proc / "pressure" / "memory", 900)
 
 
-def model(proc, cg, targets, **kw):
+def model(proc, cg, targets, steal_sustain=1, **kw):
     return procfs.SchedstatSampler(lambda: dict(targets), lambda u: len(u), proc_root=str(proc), cgroup_root=str(cg),
-                                   node_id=5, **kw)
+                                   node_id=5, steal_sustain=steal_sustain, **kw)
 
 
-def native(proc, cg, targets, ring=None, cpu_psi=False):
+def native(proc, cg, targets, ring=None, cpu_psi=False, steal_sustain=1):
     rt = load()
-    s = rt.ProcSampler(ring, 5, str(proc), str(cg), cpu_psi)
+    s = rt.ProcSampler(ring, 5, str(proc), str(cg), cpu_psi, steal_sustain=steal_sustain)
     s.set_targets(dict(targets))
     return s
 
@@ -134,6 +134,26 @@ def test_pod_cpu_pressure_raises_steal_when_enabled(tmp_path):
     assert a.tobytes() == b.tobytes()
     steal = a[a["signal_type"] == procfs.STEAL_TYPE]
     assert int(steal["value"][0]) == 60_000  # the group stalled 60 ms of 100: above the process's own 30 %
+
+
+def test_steal_needs_a_sustained_wait_share(tmp_path):
+    """cpu_steal_pct comes out only once the wait share has held the floor for steal_sustain
+    intervals in a row (a healthy service's threads cross it now and then, one interval at a
+    time); an interval below the floor starts the count again. Model and native agree."""
+    proc, cg, q = world(tmp_path)
+    targets = {100: 7}
+    m, n = model(proc, cg, targets, steal_sustain=3), native(proc, cg, targets, steal_sustain=3)
+    m.sample(T0, M0), nat_sample(n, T0, M0)
+    wait = [1_000]
+    got = []
+    for i, waited_ms in enumerate([30, 30, 0, 30, 30, 30, 40], start=1):
+        wait[0] += waited_ms * 1_000_000
+        schedstat(proc, 100, 100, 20, wait[0], 11 + i)
+        t, mo = T0 + i * 10**8, M0 + i * 10**8
+        a, b = m.sample(t, mo), nat_sample(n, t, mo)
+        assert a.tobytes() == b.tobytes(), i
+        got.append([int(e["value"]) for e in a if int(e["signal_type"]) == procfs.STEAL_TYPE])
+    assert got == [[], [], [], [], [], [30_000], [40_000]], got
 
 
 def test_shedding_mask_and_pause(tmp_path):

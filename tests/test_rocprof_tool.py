@@ -63,7 +63,7 @@ def test_tool_pushes_gpu_signals_into_ring(rec):
     dt = {64: records.EVENT, 32: records.USER32, 24: records.USER24}[rec]
     name = f"/mislo-test-{os.getpid()}-events{rec}"
     ring = rt.HostRing(1 << 16, rec, name)
-    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0",
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", MISLO_WAIT_NEEDS_FOREIGN="0",
                MISLO_POD_ID="7", MISLO_NODE_ID="3", MISLO_SVC_ID="2", MISLO_ROCPROF_VERBOSE="1")
     t0 = time.time_ns()
     r = subprocess.run([sys.executable, "-c", WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
@@ -121,7 +121,7 @@ def test_request_trace_tags_gpu_records():
     rt = load()
     name = f"/mislo-test-{os.getpid()}-tag"
     ring = rt.HostRing(1 << 16, 32, name)
-    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", PYTHONPATH=ROOT)
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", MISLO_WAIT_NEEDS_FOREIGN="0", PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-c", TAG_WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     segs = ring.peek(1 << 16)
@@ -252,7 +252,7 @@ def test_queue_delay_excludes_waiting_behind_own_queue():
     rt = load()
     name = f"/mislo-test-{os.getpid()}-burst"
     ring = rt.HostRing(1 << 16, 64, name)
-    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0")
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", MISLO_WAIT_NEEDS_FOREIGN="0")
     r = subprocess.run([sys.executable, "-c", BURST_WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     segs = ring.peek(1 << 16)
@@ -263,6 +263,76 @@ def test_queue_delay_excludes_waiting_behind_own_queue():
     # a GEMM that started the moment its predecessor ended waited for nothing: no record at all
     # (r3 box: 5 records for 72 GEMMs + the setup kernels, none above 1 ms)
     assert len(q) >= 1 and q.max() < 5.0, np.sort(q)[-10:]
+
+
+STARVED_WORKLOAD = r"""
+import ctypes, os, sys, time
+import numpy as np
+import torch
+os.sched_setaffinity(0, {int(sys.argv[1])})
+tool = [ln.split()[-1] for ln in open("/proc/self/maps") if "libmislo_rocprof" in ln][0]
+lib = ctypes.CDLL(tool)
+lib.mislo_rocprof_waits.restype = ctypes.c_int64
+lib.mislo_rocprof_waits.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+x = torch.randn(2048, 2048, device="cuda")
+host = np.random.rand(8 << 20).astype(np.float32)  # 32 MB pageable: staged through the host CPU
+torch.cuda.synchronize()
+print("ready", flush=True)
+sys.stdin.readline()  # the burners share this process's CPU now
+end = time.time() + 4.0
+while time.time() < end:
+    d = torch.from_numpy(host).to("cuda", non_blocking=True)
+    for _ in range(8):
+        x = torch.tanh(x @ x) * 0.5
+    y = d[:16].sum() + x[0, 0]
+    torch.cuda.synchronize()
+ok, no = ctypes.c_uint64(), ctypes.c_uint64()
+lib.mislo_rocprof_waits(0, ctypes.byref(ok), ctypes.byref(no))
+print("waits", ok.value, no.value, flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_cpu_starved_process_waits_are_not_gpu_contention():
+    """A service starved of CPU (burners on its CPU) alone on the GPU: its kernels can start late
+    behind its own host-staged copies and barriers, but no other process holds waves, so no
+    gpu_queue_delay record may come out (profiles/r4_config3: before the occupancy gate, a CPU
+    fault read as gpu_contention in 13 of 15 windows)."""
+    from llm_slo_ebpf_toolkit_amd.collector import records
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    name = f"/mislo-test-{os.getpid()}-starved"
+    ring = rt.HostRing(1 << 16, 64, name)
+    cpu = sorted(os.sched_getaffinity(0))[0]
+    env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000",
+               MISLO_ROCPROF_VERBOSE="1")
+    p = subprocess.Popen([sys.executable, "-c", STARVED_WORKLOAD, str(cpu)], env=env, stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    burn = "import os, sys\nos.sched_setaffinity(0, {int(sys.argv[1])})\nwhile True:\n    pass\n"
+    burners = []
+    try:
+        assert p.stdout.readline().strip() == "ready", p.stderr.read()[-2000:]
+        burners = [subprocess.Popen([sys.executable, "-c", burn, str(cpu)]) for _ in range(3)]
+        time.sleep(0.5)
+        p.stdin.write("go\n")
+        p.stdin.flush()
+        out, err = p.communicate(timeout=180)
+    finally:
+        for b in burners:
+            b.kill()
+            b.wait(10)
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode == 0, err[-2000:]
+    waits = [ln for ln in out.splitlines() if ln.startswith("waits")]
+    print(waits, [ln for ln in err.splitlines() if "occupancy" in ln][-2:])
+    segs = ring.peek(1 << 16)
+    view = ring.records_view()
+    recs = np.concatenate([np.frombuffer(view[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
+                           for _, i, c in segs]) if segs else np.zeros(0, dtype=records.EVENT)
+    q = recs[recs["signal_type"] == 13]
+    assert len(q) == 0, (waits, np.sort(q["value"])[-10:])
 
 
 FOREIGN_WORKLOAD = r"""
@@ -429,7 +499,7 @@ def test_split_rings_route_the_tools_records_to_the_pods_worker():
         fh.write(b"\x01")  # pod 7 -> worker 1
     try:
         env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=",".join(names), MISLO_SHARD_TABLE=table,
-                   MISLO_POD_ID="7", MISLO_QUEUE_FLOOR_NS="0")
+                   MISLO_POD_ID="7", MISLO_QUEUE_FLOOR_NS="0", MISLO_WAIT_NEEDS_FOREIGN="0")
         r = subprocess.run([sys.executable, "-c", WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         assert rings[0].size == 0 and rings[1].size > 0, (rings[0].size, rings[1].size)

@@ -268,7 +268,7 @@ def main() -> int:
         observable.append("mem_reclaim_latency_ms")
     gpu_tool = a.backend == "llama" and os.path.exists(TOOL)
     if gpu_tool:  # GPU signals of the RAG service's own kernels (the agent's pod id 1: its first pod)
-        rag_env.update(ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1")
+        rag_env.update(ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1")
         observable += list(GPU_SIGNALS)
     rag = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.rag_service", "--backend",
                             a.backend, "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", "",

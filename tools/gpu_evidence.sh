@@ -9,6 +9,8 @@
 #   rptests   the rocprofiler tool's GPU tests (request GPU wait under contention included)
 #   config2   BASELINE config 2: Llama 7B preset, 800 ms TTFT SLO, GEMM burners, per-window attribution
 #   live      config3 then config2
+#   live3     the rocprof tool's GPU tests, then config3
+#   live34    config3, then config4 (TP = visible GPUs)
 #   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
 #   spread    the headline bench at K = 20 and K = 200, repeated on one box
@@ -39,6 +41,12 @@ case "${1:-reentry}" in
     $S "300|rp_tests|python -u -m pytest tests/test_rocprof_tool.py -m gpu -x -v -s --timeout 200 --timeout-method thread" \
        "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
        "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
+  live3)    # the rocprof tool's GPU tests, then config 3
+    $S "300|rp_tests|python -u -m pytest tests/test_rocprof_tool.py -m gpu -x -v -s --timeout 200 --timeout-method thread" \
+       "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" ;;
+  live34)   # configs 3 and 4 (config 4 at TP = the box's GPU count)
+    $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
+       "700|c4|python -u tools/config4_evidence.py --out gpurun_out/r4_config4" ;;
   live)     # configs 3 and 2 back to back (the live-attribution evidence)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
        "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
