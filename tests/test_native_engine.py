@@ -422,3 +422,73 @@ def test_two_fault_refit_and_marginals_match_the_host_model():
     fx = os.path.join(os.path.dirname(__file__), "fixtures", "ref_multi_fault_samples.jsonl")
     assert ref55_report(fx, dev) == ref55_report(fx, host_scorer(model))
     pipe.eng.close()
+
+
+def test_headline_shape_windows_match_the_oracle():
+    """The bench's window shape (BASELINE config 5): 1,048,576 events with the probes' framed
+    definitions + USER24 rows, 16,384 spans, 64 incident groups, the agent's 2000 ms halo, over
+    two consecutive windows (the second joins the first's resident rows). This is the shape that
+    runs the multi-block part scans, the long-list span sort and full LDS partitions, which the
+    8192-event tests never reach. Histograms, value sums, ring accounting, join counters,
+    features, SLI counts, confusion are exact; posteriors within 1e-9."""
+    import time
+
+    from llm_slo_ebpf_toolkit_amd.parallel.exchange import ExchangeModel
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    t0 = time.time()
+    cfg = ReplayConfig(scenario="full", events_per_window=1 << 20, spans_per_window=16384, n_services=64, seed=42,
+                       fault_hold=2)
+    gen = ReplayGenerator(cfg)
+    wins = [gen.next_window() for _ in range(2)]
+    imgs = build_replay_images(wins, user_rec=24)
+    sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs)
+    halo_ms = 2000.0
+    pipe = WindowPipeline(sig_cap, 16384, 64, model="bayes", learn=False, user_cap=1 << 18, halo_ms=halo_ms)
+    rt = load()
+    rb = rt.Ringbuf.create_shm(f"/mislo-gt-{os.getpid()}-headline", 1 << 26)
+    user, spans = rt.HostRing(1 << 19, 24), rt.HostRing(1 << 16, 64)  # two windows in flight
+    src = RingWindowSource(pipe, rb, user, spans)
+    pods, sn = pod_meta(gen)
+    pipe.eng.set_pods(pods, sn)
+    pod_sn = dict(zip(pods.tolist(), sn.tolist()))
+    table, tmap = oracle.CtxTable(), oracle.TraceMap()
+    xm = ExchangeModel(0, 1, halo_ms, 0, 0, halo_windows=3)
+    model = NaiveBayes.ref()
+    print(f"generated in {time.time() - t0:.1f} s; sig_cap {sig_cap}", flush=True)
+    for j, (w, img) in enumerate(zip(wins, imgs)):
+        r = src.stage(feed(img, rb, user, spans), w.n_groups, img.labels)
+        k = r["k"]
+        assert r["n_kernel"] * 24 == len(img.framed) and r["n_user"] == len(img.user)
+        pk = pipe.packet(k)
+        res = pipe.results(k, w.n_groups)
+        t1 = time.time()
+        oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
+        d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases, pod_sn=pod_sn)
+        ref = xm.join(d, oracle.spans_native(img.spans, tmap), w.n_groups)
+        print(f"window {j}: {len(d.ts)} rows, oracle in {time.time() - t1:.1f} s, {ref.debug}", flush=True)
+        np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d))
+        np.testing.assert_array_equal(pk["misc"][2:18].astype(np.int64), oracle.value_sums_milli(d))
+        assert pk["ring_state"]["first_busy"] == -1
+        fr = img.framed.view(np.uint32).reshape(-1, 6)
+        assert pk["ring_state"]["events"] == int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
+        dbg = dict(zip(("candidates", "low_raw", "overlap", "fanout_dropped", "spans_enriched"),
+                       pk["dbg"][:5].astype(np.int64).tolist()))
+        for key in ("candidates", "fanout_dropped", "spans_enriched"):
+            assert dbg[key] == ref.debug[key], (j, key, dbg, ref.debug)
+        np.testing.assert_array_equal(res["feat"], ref.feat, err_msg=f"window {j}")
+        feat = res["feat"].astype(np.float64)
+        np.testing.assert_allclose(res["post"][:, :10], model.posteriors(feat), rtol=1e-9, atol=1e-12)
+        np.testing.assert_array_equal(res["pred"], np.argmax(model.logits(feat), axis=1))
+        conf = np.zeros((16, 16), dtype=np.int64)
+        np.add.at(conf, (img.labels, res["pred"]), 1)
+        np.testing.assert_array_equal(pk["confusion"].astype(np.int64), conf)
+        exp = np.zeros((w.n_groups, 2), dtype=np.int64)
+        np.add.at(exp[:, 0], w.spans["group_id"], 1)
+        np.add.at(exp[:, 1], w.spans["group_id"], (w.spans["ttft_ms"] > 800.0).astype(np.int64))
+        np.testing.assert_array_equal(res["sli"].astype(np.int64), exp)
+        if j == 1:  # the second window joined the first's rows through the halo
+            assert pipe.eng.import_state()[5] == 2
+    src.drain()
+    pipe.eng.close()

@@ -11,6 +11,7 @@
 #   live      config3 then config2
 #   live3     the rocprof tool's GPU tests, then config3
 #   live34    config3, then config4 (TP = visible GPUs)
+#   headline  the headline-shape oracle test, then config4
 #   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
 #   spread    the headline bench at K = 20 and K = 200, repeated on one box
@@ -47,6 +48,9 @@ case "${1:-reentry}" in
   live34)   # configs 3 and 4 (config 4 at TP = the box's GPU count)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
        "700|c4|python -u tools/config4_evidence.py --out gpurun_out/r4_config4" ;;
+  headline) # the bench-shape oracle test, then config 4 with lighter burners
+    $S "400|headline|python -u -m pytest tests/test_native_engine.py -m gpu -x -v -s --timeout 360 --timeout-method thread -k headline" \
+       "700|c4|python -u tools/config4_evidence.py --out gpurun_out/r4_config4 --burners-per-cpu 2 ${2:-}" ;;
   live)     # configs 3 and 2 back to back (the live-attribution evidence)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
        "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
