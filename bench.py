@@ -239,6 +239,7 @@ def main() -> int:
 
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
     from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, build_replay_images
+    from llm_slo_ebpf_toolkit_amd.collector.records import framed_rows
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -373,7 +374,7 @@ def main() -> int:
             comm = (uid[0], rank, world)
     # a window's record budget covers its framed ring records (events AND the definitions the
     # probes commit ahead of them) plus its user-space records: nothing may spill into the next window
-    sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs + himgs)
+    sig_cap = max(framed_rows(i.framed) + len(i.user) for i in imgs + himgs)
     user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
     xchg = (min(65536, a.events) if world > 1 else 0) if a.xchg_cap < 0 else a.xchg_cap
     import_cap = (world - 1) * xchg  # other GPUs' rows (the halo's rows stay resident)
@@ -674,7 +675,8 @@ def main() -> int:
             "scenario": a.scenario,
             "source": "BPF ring buffer (kernel layout, emulated in shm) + rocprof/user-space ring + span ring",
             "wire_bytes_per_event": 16,
-            "ring_bytes_per_kernel_event": 24,
+            # batch records: 8 slots (events, definitions, pads) per 136 ring bytes
+            "ring_bytes_per_kernel_event": round(sum(len(i.framed) for i in imgs) / max(1, sum(i.n_kernel for i in imgs)), 2),
             "ring_bytes_per_user_record": a.user_rec,
             "device_buffers": a.buffers,
             "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default"),

@@ -636,6 +636,55 @@ class Agent:
         if attrs:
             self.writers.flush()  # a window's incidents leave with the window (detection delay)
 
+    def _restart_workers(self, exc, rings, sets, maps, G: int):
+        """A worker died or stopped answering: its communicator is broken for every worker. Stop
+        them all and start fresh processes for the surviving GPUs -- a new communicator (RCCL id,
+        or a new gloo port for the CPU engine), world N - 1, the services re-sharded over them
+        (split rings: the producers' routing follows at once; the lost worker's ring set is left
+        behind). The new workers resume from the ring positions already released, so the windows
+        that were in flight are read again. Returns (pool, split)."""
+        from dataclasses import replace
+
+        from .worker import WorkerPool, groups_of
+
+        old = self.pool
+        dead = set(old.dead_ranks())
+        if exc.rank is not None:
+            dead.add(int(exc.rank))
+        old.close(timeout=2.0)
+        survivors = [s for s in self.specs if s.rank not in dead]
+        print(f"window worker(s) {sorted(dead)} lost ({str(exc).splitlines()[0]}); restarting on "
+              f"{len(survivors)} worker(s)", file=sys.stderr)
+        if not survivors:
+            raise exc
+        N = len(survivors)
+        split = bool(self.specs[0].split) and N > 1
+        port = self.specs[0].master[1]
+        if self.o.engine == "cpu" and N > 1:
+            import socket
+
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+            sk.close()
+        xchg = self.specs[0].xchg_cap if N > 1 else 0
+        specs = [replace(s, rank=r, world=N, group_cap=max(1, groups_of(0, N, G)), xchg_cap=xchg,
+                         import_cap=(N - 1) * xchg, master=(s.master[0], port), split=split)
+                 for r, s in enumerate(survivors)]
+        if self.router is not None:  # producers route to the surviving workers' ring sets
+            pods, sh = self.router.resize(N if split else 1)
+            if hasattr(maps, "set_shards") and len(pods):
+                maps.set_shards(pods, sh)
+        if self.pod_table:  # every new worker starts with the pods' services known so far
+            keys = np.array(sorted(self.pod_table), dtype=np.uint32)
+            specs = [replace(s, pods=(keys, np.array([self.pod_table[k] for k in keys.tolist()], dtype=np.uint32)))
+                     for s in specs]
+        self.pool = WorkerPool(specs, rings, in_process=False)
+        self.specs = specs
+        self.metrics.worker_restarts.inc()
+        self.metrics.workers.set(N)
+        return self.pool, split
+
     def run_windows(self, max_windows: int = 0) -> int:
         """Window engine main loop. This process is the controller: every window_ms it cuts
         the node's rings (publishes epoch k into mislo_cfg -- the only writer -- then snapshots
@@ -649,7 +698,7 @@ class Agent:
         from ..collector.records import EpochClock
         from ..pipeline.window import Cut
         from ..safety import TreeCPUSampler
-        from .worker import WorkerPool, WorkerSpec, groups_of
+        from .worker import WorkerError, WorkerPool, WorkerSpec, groups_of
 
         o = self.o
         N = self.n_gpus()
@@ -663,12 +712,18 @@ class Agent:
             if pods is not None:
                 router.set_pods(*pods)
         self.router = router
+        # pod id -> svc|node as the workers know it (fresh workers after a restart start from it)
+        self.pod_table = {}
+        if pods is not None:
+            self.pod_table.update(zip(np.asarray(pods[0]).tolist(), np.asarray(pods[1]).tolist()))
         node_id = bpf.stable_node_id(o.node)
         maps.init(node_id)
         model, image, self.model_meta = self._load_model()
         self.model = model
         G = o.window_groups
-        budget = o.window_events + o.window_events // 4  # events plus the definitions ahead of them
+        # rows: events plus the definitions ahead of them and the pad slots of batches a
+        # definition or a cut flushed part-full
+        budget = o.window_events + o.window_events // 2
         # joins reach across the window cut (halo: the rows of the earlier windows it spans stay
         # resident on the device) and, on a multi-GPU node, across GPUs (trace-tagged rows
         # exchanged over RCCL, bounded per peer)
@@ -696,6 +751,8 @@ class Agent:
             self.load_state(state)
         pool = WorkerPool(specs, (ring, user, spans), in_process=N == 1)
         self.pool = pool
+        self.specs = specs
+        self.metrics.workers.set(N)
         print(f"window engine: {o.engine} x {N} worker(s){' on split rings' if split else ''}, model "
               f"{self.model_meta.get('name')}"
               f"{' T=%.3g' % self.model_meta['temperature'] if 'temperature' in self.model_meta else ''}",
@@ -784,7 +841,7 @@ class Agent:
         self.ladder = ShedLadder(catalog.DISABLE_ORDER, maps=maps, sampler=sampler, user_ring=[x[1] for x in sets],
                                  probe_manager=getattr(self, "probe_manager", None), generator=self.generator)
         if self.guard is not None:
-            self.guard.source = TreeCPUSampler(lambda: [os.getpid()] + pool.pids())
+            self.guard.source = TreeCPUSampler(lambda: [os.getpid()] + self.pool.pids())
             self.guard.evaluate()
         clock = EpochClock()
         self.ready = True
@@ -800,15 +857,23 @@ class Agent:
                 nxt += period
                 t = time.time_ns()
                 maps.cfg_set(bpf.CFG_EPOCH, clock.publish(t))  # epoch first, then the ring snapshots
+                maps.flush_cpus()  # every CPU's staged batches onto the rings before the snapshots
                 bases = clock.bases()
                 cuts = [Cut(kernel=rs[0].producer_pos, user=rs[1].head, spans=rs[2].head, bases=bases, t_ns=t)
                         for rs in sets]
                 upd = mapper.take_pod_updates() if mapper is not None else None
+                if upd is not None and len(upd[0]):
+                    self.pod_table.update(zip(np.asarray(upd[0]).tolist(), np.asarray(upd[1]).tolist()))
                 if upd is not None and router is not None:  # later records of these pods go to their owners' rings
                     router.set_pods(*upd)
                     if hasattr(maps, "set_shards"):
                         maps.set_shards(upd[0], router.pod_shard(upd[0]))
-                replies = pool.window(cuts if split else cuts[0], G, upd)
+                try:
+                    replies = pool.window(cuts if split else cuts[0], G, upd, timeout=max(30.0, 20 * period))
+                except WorkerError as exc:
+                    pool, split = self._restart_workers(exc, (ring, user, spans), sets, maps, G)
+                    cut_t.clear()  # the lost windows' records are read again by the new workers
+                    continue
                 cut_t[replies[0]["k"]] = t
                 prev = replies[0].get("prev")
                 if prev is not None:
@@ -827,6 +892,7 @@ class Agent:
                     break
                 if maps.ctx_ids_used() > (7 << 20) and hasattr(maps, "reset_ctx_ids"):
                     maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
+            pool = self.pool
             final = pool.stop()
             if final and final[0].get("prev") is not None:
                 self._emit_window(final, cut_t.pop(final[0]["prev"]["k"], time.time_ns()), G, names, ring, model)
@@ -836,7 +902,7 @@ class Agent:
         finally:
             # workers unregister the rings from their GPUs and free device memory while the
             # ring mappings still exist (interpreter teardown order is arbitrary)
-            pool.close()
+            self.pool.close()
             if sampler is not None:
                 sampler.stop()
             if receiver is not None:

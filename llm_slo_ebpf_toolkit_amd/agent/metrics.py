@@ -63,6 +63,9 @@ class AgentMetrics:
                                    "Windows whose ring consumption stopped at a record still being written.")
         self.ring_backlog = r.gauge("llm_slo_agent_ring_backlog_bytes", "Unconsumed bytes in the BPF ring buffer.")
         self.host_us = r.gauge("llm_slo_agent_window_host_us", "Host time to assemble the last window (us).")
+        self.workers = r.gauge("llm_slo_agent_window_workers", "Window workers (GPUs) the agent is running.")
+        self.worker_restarts = r.counter("llm_slo_agent_worker_restarts_total",
+                                         "Worker pool restarts after a worker died (the survivors' GPUs go on).")
         self.rss = r.gauge("llm_slo_agent_memory_rss_bytes", "Agent process resident set size (bytes).")
         self.burn_err = r.gauge("llm_slo_agent_burn_rate_prediction_error",
                                 "Mean relative error of the scored SLO burn-rate forecasts.")

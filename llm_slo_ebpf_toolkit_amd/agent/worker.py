@@ -30,6 +30,12 @@ Protocol (multiprocessing pipes, pickled, O(groups) bytes per window): controlle
 ``("window", cut, n_groups, pods)`` every window, ``("stop",)``; worker -> controller one reply per
 window with its release positions, its ring accounting and -- worker 0 only -- the previous
 window's node-wide packet and all workers' incident results.
+
+Failure: a worker that dies (or stops answering) breaks the communicator for all of them. The
+controller (agent/daemon.py Agent._restart_workers) then stops every worker and starts fresh
+processes for the surviving GPUs -- a new communicator (RCCL id / gloo port), world N - 1, the
+services re-sharded over them -- which resume from the ring positions already released; the
+windows that were in flight are read again (at least once).
 """
 
 from __future__ import annotations
@@ -238,7 +244,9 @@ def worker_main(spec: WorkerSpec, conn) -> None:
 
 
 class WorkerError(RuntimeError):
-    pass
+    def __init__(self, msg: str, rank: Optional[int] = None):
+        super().__init__(msg)
+        self.rank = rank
 
 
 class RemoteWorker:
@@ -257,14 +265,21 @@ class RemoteWorker:
 
     def recv(self, timeout: float = 600.0):
         if not self.conn.poll(timeout):
-            raise WorkerError(f"worker {self.spec.rank} did not answer in {timeout:.0f} s")
+            raise WorkerError(f"worker {self.spec.rank} did not answer in {timeout:.0f} s", self.spec.rank)
         try:
             msg = self.conn.recv()
-        except EOFError as exc:
-            raise WorkerError(f"worker {self.spec.rank} exited (code {self.proc.exitcode})") from exc
+        except (EOFError, OSError) as exc:
+            raise WorkerError(f"worker {self.spec.rank} exited (code {self.proc.exitcode})", self.spec.rank) from exc
         if msg[0] == "error":
-            raise WorkerError(f"worker {self.spec.rank} failed:\n{msg[1]}")
+            raise WorkerError(f"worker {self.spec.rank} failed:\n{msg[1]}", self.spec.rank)
         return msg
+
+    def ready(self) -> bool:
+        return self.conn.poll(0)
+
+    @property
+    def alive(self) -> bool:
+        return self.proc.is_alive()
 
     def send(self, msg) -> None:
         self.conn.send(msg)
@@ -300,6 +315,11 @@ class LocalWorker:
     def recv(self, timeout: float = 600.0):
         r, self._reply = self._reply, None
         return r
+
+    def ready(self) -> bool:
+        return True
+
+    alive = True
 
     def close(self, timeout: float = 30.0) -> None:
         self.core.close()
@@ -340,14 +360,39 @@ class WorkerPool:
     def pids(self) -> List[int]:
         return [w.pid for w in self.workers]
 
-    def window(self, cut, n_groups: int, pods=None) -> List[dict]:
-        """``cut``: one Cut of the shared rings, or (split rings) a list with each worker's own."""
+    def window(self, cut, n_groups: int, pods=None, timeout: float = 600.0) -> List[dict]:
+        """``cut``: one Cut of the shared rings, or (split rings) a list with each worker's own.
+        Raises WorkerError naming the first worker found dead (the others may be blocked in a
+        collective with it, so the replies are gathered while watching every process), or the
+        first one silent for ``timeout`` s."""
         for w in self.workers:
             c = cut[w.spec.rank] if isinstance(cut, (list, tuple)) and not hasattr(cut, "kernel") else cut
-            w.send(("window", c, groups_of(w.spec.rank, self.world, n_groups), pods))
-        replies = [w.recv()[1] for w in self.workers]
+            try:
+                w.send(("window", c, groups_of(w.spec.rank, self.world, n_groups), pods))
+            except (OSError, BrokenPipeError) as exc:
+                raise WorkerError(f"worker {w.spec.rank} is gone ({exc})", w.spec.rank) from exc
+        replies: List[Optional[dict]] = [None] * self.world
+        deadline = time.monotonic() + timeout
+        while any(r is None for r in replies):
+            got = False
+            for i, w in enumerate(self.workers):
+                if replies[i] is None and w.ready():
+                    replies[i] = w.recv()[1]
+                    got = True
+            if got:
+                continue
+            dead = self.dead_ranks()
+            if dead:
+                raise WorkerError(f"worker {dead[0]} exited", dead[0])
+            if time.monotonic() > deadline:
+                late = next(i for i, r in enumerate(replies) if r is None)
+                raise WorkerError(f"worker {late} did not answer in {timeout:.0f} s", late)
+            time.sleep(0.0005)
         self._release(replies)
         return replies
+
+    def dead_ranks(self) -> List[int]:
+        return [w.spec.rank for w in self.workers if not w.alive]
 
     def _release(self, replies: List[dict]) -> None:
         if self.in_process or self.split:
@@ -380,6 +425,6 @@ class WorkerPool:
         self._release(replies)
         return replies
 
-    def close(self) -> None:
+    def close(self, timeout: float = 30.0) -> None:
         for w in self.workers:
-            w.close()
+            w.close(timeout)

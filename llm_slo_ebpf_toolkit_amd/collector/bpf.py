@@ -79,6 +79,12 @@ class MapSet:
     def ctx_ids_used(self) -> int:
         return int(self.cfg_get(CFG_CTX_NEXT))
 
+    def flush_cpus(self) -> int:
+        """The window cut's flush of every CPU's staging batches (after the new epoch is
+        published, before the ring positions are read); CPUs flushed. The emulated rings'
+        producers flush their own batches."""
+        return 0
+
 
 class EmulatedMaps(MapSet):
     """mislo_cfg lives in the emulated ring's meta page (every shard ring's, with split rings:
@@ -112,6 +118,26 @@ class BpfMaps(MapSet):
         self.cfg = rt.BpfMap(os.path.join(pin_dir, "mislo_cfg"))
         self.pods = rt.BpfMap(os.path.join(pin_dir, "mislo_pods"))
         self._ctxs = os.path.join(pin_dir, "mislo_ctxs")
+        # probes/ebpf/mislo_flush.bpf.c, pinned by the loader (no attachment): run on each CPU at
+        # every cut. Without it a quiet CPU's partial batch waits for that CPU's next event.
+        self.flush_fd = rt.bpf_obj_get(os.path.join(pin_dir, "progs", "mislo_flush", "mislo_flush"))
+        self.cpus = list(range(os.cpu_count() or 1))
+        self.flush_errors = 0
+
+    def flush_cpus(self) -> int:
+        if self.flush_fd < 0:
+            return 0
+        from ..runtime import load
+
+        rt = load()
+        n = 0
+        for c in self.cpus:
+            r = rt.bpf_prog_run_on_cpu(self.flush_fd, c)
+            if r >= 0:
+                n += 1
+            elif r != -6:  # -ENXIO: an offline CPU
+                self.flush_errors += 1
+        return n
 
     def cfg_set(self, idx: int, value: int) -> None:
         self.cfg.update(struct.pack("<I", int(idx)), struct.pack("<Q", int(value) & 0xFFFFFFFFFFFFFFFF))
@@ -240,6 +266,18 @@ class ShardRouter:
         sn = np.array([self.svc.get(int(p), 0) for p in np.asarray(pod_ids).tolist()], dtype=np.uint32)
         return shard_of_pod(sn, self.world)
 
+    def resize(self, world: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Re-shard every known pod over ``world`` workers (a worker was lost): the shared table
+        follows at once; returns (pods, shards) for the probes' mislo_shards map."""
+        self.world = max(1, int(world))
+        pods = np.array(sorted(self.svc), dtype=np.int64)
+        sh = self.pod_shard(pods) if len(pods) else np.zeros(0, np.int64)
+        if self.table is not None:
+            for p, s in zip(pods.tolist(), sh.tolist()):
+                if 0 <= p < len(self.table):
+                    self.table[p] = int(s)
+        return pods, sh
+
     def span_shard(self, spans: np.ndarray) -> np.ndarray:
         return (spans["group_id"].astype(np.int64) % self.world).astype(np.int64)
 
@@ -323,7 +361,9 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
         for s in range(n_sl):
             for r, (kev, uev, sp) in enumerate(shard_parts):
                 lo_k, hi_k = len(kev) * s // n_sl, len(kev) * (s + 1) // n_sl
-                sims[r].submit(kev[lo_k:hi_k])
+                # staged per CPU as the probes do (a batch goes out when full, with a
+                # definition, or at the first record after the agent's next epoch)
+                sims[r].submit(kev[lo_k:hi_k], flush=False)
                 lo_u, hi_u = len(uev) * s // n_sl, len(uev) * (s + 1) // n_sl
                 if hi_u > lo_u:
                     users[r].push(uev[lo_u:hi_u])
@@ -332,6 +372,8 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
                     spanss[r].push(sp[lo_s:hi_s])
             nxt += period / n_sl
             time.sleep(max(0.0, nxt - time.perf_counter()))
+        for sim in sims:  # what the agent's cut flush does to a quiet CPU's batch
+            sim.flush()
         j += 1
 
 

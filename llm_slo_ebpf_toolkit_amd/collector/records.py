@@ -119,7 +119,8 @@ def counts_row(n_ev: int, n_sp: int, n_groups: int, n_local: int = 0, bases=(0,)
          b[1] & 0xFFFFFFFF, b[1] >> 32, b[2] & 0xFFFFFFFF, b[2] >> 32, b[3] & 0xFFFFFFFF, b[3] >> 32, 0, 0]
     return np.array(v, dtype=np.uint64).astype(np.uint32).view(np.int32)
 assert EVENT16.itemsize == 16
-DEF_TRACE, DEF_CTX, DEF_FIRST = 0xFD, 0xFE, 0xF0  # definition record types (low byte of ctx_type)
+DEF_TRACE, DEF_CTX, DEF_FIRST = 0xFD, 0xFE, 0xF0  # definition slot types (low byte of ctx_type)
+DEF_PAD = 0xFC  # an unused slot of a batch flushed before it filled
 KERNEL_CTX_LIMIT = 1 << 23     # kernel context ids 1 .. 2^23 - 1, host ids above
 KERNEL_TRACE_LIMIT = 1 << 24   # kernel trace ids 1 .. 2^24 - 1, host ids above
 CTX_IDS = 1 << 24
@@ -155,7 +156,30 @@ USER24_TS_BITS = 44
 
 WIRE_DTYPES = {64: EVENT, 16: EVENT16}
 RB_BUSY, RB_DISCARD, RB_HDR = 1 << 31, 1 << 30, 8   # BPF ring buffer record header bits
-REC_STRIDE = RB_HDR + 16                          # ring bytes per 16-byte record
+# A BPF ring record is a batch of BATCH_SLOTS 16-byte slots a CPU staged (probes/ebpf/mislo_probe.h
+# mislo_stage_put): row r of a window is slot r % 8 of record r // 8
+BATCH_SLOTS = 8
+REC_PAYLOAD = 16 * BATCH_SLOTS                    # 128
+REC_STRIDE = RB_HDR + REC_PAYLOAD                 # 136 ring bytes per record
+PROBE_CPUS = 16                                   # the probe models' CPUs (a task runs on tid % 16)
+
+
+def framed_rows(framed) -> int:
+    """Rows (slots) of a framed image of whole batch records."""
+    return len(framed) // REC_STRIDE * BATCH_SLOTS
+
+
+def framed_slots(framed: np.ndarray):
+    """(header len words per row [rows], slots as uint32 [rows, 4]) of a framed image."""
+    r = np.ascontiguousarray(framed).view(np.uint32).reshape(-1, REC_STRIDE // 4)
+    hdr = np.repeat(r[:, 0], BATCH_SLOTS)
+    return hdr, r[:, 2:].reshape(-1, 4)
+
+
+def framed_event_count(framed: np.ndarray) -> int:
+    """Events in a framed image: event slots of committed (not busy / discarded) batch records."""
+    hdr, sl = framed_slots(framed)
+    return int(((hdr == REC_PAYLOAD) & ((sl[:, 1] & 0xFF) < DEF_FIRST)).sum())
 
 
 def wire_bytes(wire: int) -> int:
@@ -465,16 +489,49 @@ class ProbeModel:
 
     CFG_EPOCH, CFG_TRACE_NEXT, CFG_CTX_NEXT = 124, 125, 126
 
-    def __init__(self, cfg: np.ndarray = None):
+    def __init__(self, cfg: np.ndarray = None, cpus: int = PROBE_CPUS):
         self.cfg = cfg if cfg is not None else np.zeros(128, dtype=np.uint64)
         self.ctx = {}
         self.traces = {}
+        self.stages = [([], 0) for _ in range(max(1, cpus))]  # per CPU: (slots, epoch)
 
-    def encode(self, events: np.ndarray) -> np.ndarray:
-        """Ring payloads (EVENT16 layout, definitions included, ring order) for ``events``."""
+    def _flush(self, cpu: int, out: list) -> None:
+        sl, _ = self.stages[cpu]
+        if sl:
+            out.extend(sl + [(0, DEF_PAD, 0, 0)] * (BATCH_SLOTS - len(sl)))
+        self.stages[cpu] = ([], 0)
+
+    def _put(self, cpu: int, slot: tuple, flush_now: bool, out: list) -> None:
+        """mislo_stage_put: into the CPU's batch; the batch goes out when full, with a definition,
+        or before a slot of a newer epoch."""
+        epoch = int(self.cfg[self.CFG_EPOCH])
+        sl, ep = self.stages[cpu]
+        if sl and ep != epoch:
+            self._flush(cpu, out)
+        sl = self.stages[cpu][0] + [slot]
+        self.stages[cpu] = (sl, epoch)
+        if len(sl) == BATCH_SLOTS or flush_now:
+            self._flush(cpu, out)
+
+    def flush(self) -> np.ndarray:
+        """The agent's cut: every CPU's partial batch, CPU 0 first."""
+        out = []
+        for c in range(len(self.stages)):
+            self._flush(c, out)
+        return self._as_slots(out)
+
+    @staticmethod
+    def _as_slots(out):
+        return np.array(out, dtype=np.uint32).reshape(-1, 4).view(EVENT16).reshape(-1) if out else \
+            np.zeros(0, dtype=EVENT16)
+
+    def encode(self, events: np.ndarray, flush: bool = True) -> np.ndarray:
+        """Ring payloads (whole batches of EVENT16 slots, definitions and pads included, ring
+        order) for ``events``; with ``flush`` the partial batches too."""
         out = []
         shift = milli_shift_table()
         for e in events:
+            cpu = int(e["tid"]) % len(self.stages)
             st = int(e["signal_type"])
             if st < 120 and int(e["value"]) < int(self.cfg[2 + st]):
                 continue
@@ -488,7 +545,7 @@ class ProbeModel:
                     fresh = int(self.cfg[self.CFG_CTX_NEXT]) + 1
                     self.cfg[self.CFG_CTX_NEXT] = fresh
                     if fresh < KERNEL_CTX_LIMIT:
-                        out.append((c, DEF_CTX | (fresh << 8), pod, pid))
+                        self._put(cpu, (c, DEF_CTX | (fresh << 8), pod, pid), True, out)
                         self.ctx[(pod, pid, c)] = fresh
                         ctx = fresh
             tid = 0
@@ -499,29 +556,35 @@ class ProbeModel:
                     fresh = int(self.cfg[self.CFG_TRACE_NEXT])
                     self.cfg[self.CFG_TRACE_NEXT] = fresh + 1
                     tid = fresh % (KERNEL_TRACE_LIMIT - 1) + 1
-                    out.append((tid, DEF_TRACE, th & 0xFFFFFFFF, th >> 32))
+                    self._put(cpu, (tid, DEF_TRACE, th & 0xFFFFFFFF, th >> 32), True, out)
                     self.traces[th] = tid
             epoch = int(self.cfg[self.CFG_EPOCH])
             milli = int(milli_int(np.array([int(e["value"])], dtype=np.uint64),
                                   np.array([shift[st] if st < 256 else 3], dtype=np.int8))[0])
-            out.append((epoch_offset(int(e["ts_ns"]), epoch & ~3), (st & 0xFF) | (ctx << 8), milli,
-                        (tid & TRACE_ID_MASK) | ((epoch & 3) << EPOCH_TAG_SHIFT)))
-        return np.array(out, dtype=np.uint32).reshape(-1, 4).view(EVENT16).reshape(-1) if out else \
-            np.zeros(0, dtype=EVENT16)
+            self._put(cpu, (epoch_offset(int(e["ts_ns"]), epoch & ~3), (st & 0xFF) | (ctx << 8), milli,
+                            (tid & TRACE_ID_MASK) | ((epoch & 3) << EPOCH_TAG_SHIFT)), False, out)
+        if flush:
+            for c in range(len(self.stages)):
+                self._flush(c, out)
+        return self._as_slots(out)
 
 
 def frame(payloads: np.ndarray) -> np.ndarray:
-    """Committed BPF ring records (8-byte header {len = 16, pg_off = 0} + payload) for EVENT16 payloads."""
+    """Committed BPF ring records (8-byte header {len = 128, pg_off = 0} + a batch of 8 EVENT16
+    slots) for whole batches of slots."""
     p = np.ascontiguousarray(payloads).view(np.uint32).reshape(-1, 4)
-    out = np.zeros((p.shape[0], 6), dtype=np.uint32)
-    out[:, 0] = 16
-    out[:, 2:] = p
+    if p.shape[0] % BATCH_SLOTS:
+        raise ValueError("frame: whole batches of 8 slots only")
+    out = np.zeros((p.shape[0] // BATCH_SLOTS, REC_STRIDE // 4), dtype=np.uint32)
+    out[:, 0] = REC_PAYLOAD
+    out[:, 2:] = p.reshape(-1, REC_PAYLOAD // 4)
     return out.view(np.uint8).reshape(-1)
 
 
 def unframe(image: np.ndarray):
     """libbpf ring_buffer__consume semantics over a byte image of consecutive records starting at a
-    record boundary: (EVENT16 event payloads, definition payloads, n_discarded, stopped_at_busy)."""
+    record boundary: (EVENT16 event slots, definition slots, n_discarded, stopped_at_busy); pads
+    are dropped."""
     b = np.ascontiguousarray(image).view(np.uint8)
     off, ev, defs, disc = 0, [], [], 0
     while off + RB_HDR <= b.size:
@@ -531,9 +594,12 @@ def unframe(image: np.ndarray):
         plen = ln & ~(RB_BUSY | RB_DISCARD)
         if ln & RB_DISCARD:
             disc += 1
-        elif plen == 16:
-            rec = tuple(int(x) for x in b[off + 8:off + 24].view(np.uint32))
-            (defs if (rec[1] & 0xFF) >= DEF_FIRST else ev).append(rec)
+        elif plen == REC_PAYLOAD:
+            for j in range(BATCH_SLOTS):
+                rec = tuple(int(x) for x in b[off + 8 + 16 * j:off + 24 + 16 * j].view(np.uint32))
+                t = rec[1] & 0xFF
+                if t != DEF_PAD:
+                    (defs if t >= DEF_FIRST else ev).append(rec)
         off += (plen + RB_HDR + 7) & ~7
     return _as16(ev), _as16(defs), disc, False
 

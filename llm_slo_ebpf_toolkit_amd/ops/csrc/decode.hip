@@ -307,17 +307,18 @@ __global__ __launch_bounds__(NT) void k_decode_wire(const Rec* __restrict__ ev, 
 
 // ---- the native engine's window: BPF ring bytes + user-space records, decoded on the GPU ----
 
-// One pass over the window's framed ring records (24-byte stride) before the decode: applies
-// the probes' id definitions -- context rows into the device context table (svc|node from the
-// device pod table), trace id -> hash into the device trace-id table -- and finds the first
-// record still being written (a consumer must stop there; the host re-submits the rest later).
-// A window holds at most one definition per id (ids are reused only after 2^24 new traces or
-// an agent-side context reset), so the stores need no ordering among themselves.
+// One pass over the slots of the window's framed batch records (136-byte stride, 8 slots each:
+// one thread per slot, the 8 threads of a record share its header line) before the decode:
+// applies the probes' id definitions -- context rows into the device context table (svc|node
+// from the device pod table), trace id -> hash into the device trace-id table -- and finds the
+// first record still being written (a consumer must stop there; the host re-submits the rest
+// later). A window holds at most one definition per id (ids are reused only after 2^24 new
+// traces or an agent-side context reset), so the stores need no ordering among themselves.
 __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ framed, const int* __restrict__ n_ptr,
                                                    uint4* __restrict__ ctx_tab, uint32_t ctx_rows,
                                                    const uint32_t* __restrict__ pod_sn, uint32_t n_pods, TraceIds tt,
                                                    uint32_t* __restrict__ rs) {
-  const int n = n_ptr[15];  // framed records in this window
+  const int n = n_ptr[15];  // framed rows (slots) in this window
   uint32_t foreign = 0, dctx = 0, dtr = 0, disc = 0, busy = 0xFFFFFFFFu;
   // kU records per thread per trip, all 3 x kU loads issued before any is used: the pass is
   // bound by memory latency, not bytes (a header load followed by a dependent payload load
@@ -330,12 +331,13 @@ __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ f
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * stride;
       if (i < n) {
-        const uint2* r = reinterpret_cast<const uint2*>(framed + (size_t)i * kRecStride);
-        h[u] = r[0];
-        a[u] = r[1];
-        b[u] = r[2];
+        // 8-byte loads: records are 136 bytes apart, so slots are 8- but not 16-byte aligned
+        const uint2* sl = reinterpret_cast<const uint2*>(framed + slot_off(i));
+        h[u] = *reinterpret_cast<const uint2*>(framed + rec_off(i));
+        a[u] = sl[0];
+        b[u] = sl[1];
       } else {
-        h[u] = make_uint2(16u, 0u);
+        h[u] = make_uint2(kRecPayload, 0u);
         a[u] = b[u] = make_uint2(0u, 0u);
       }
     }
@@ -347,12 +349,12 @@ __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ f
         busy = min(busy, (uint32_t)i);
         continue;
       }
-      if ((h[u].x & ~(kRbBusy | kRbDiscard)) != 16u) {
-        ++foreign;
+      if ((h[u].x & ~(kRbBusy | kRbDiscard)) != kRecPayload) {
+        foreign += (i & 7) == 0;  // once per record
         continue;
       }
       if (h[u].x & kRbDiscard) {
-        ++disc;
+        disc += (i & 7) == 0;
         continue;
       }
       const uint32_t type = a[u].y & 0xFFu;
@@ -401,8 +403,9 @@ __global__ __launch_bounds__(256) void k_ring_defs(const uint8_t* __restrict__ f
   }
 }
 
-// Rows [0, counts[15]) come from the framed ring records (EVENT16 payloads; definitions,
-// discarded, foreign and not-yet-committed records become holes: no counters, no join keys),
+// Rows [0, counts[15]) come from the slots of the framed batch records (row i = slot i % 8 of
+// record i / 8; definitions, pads, discarded, foreign and not-yet-committed records become
+// holes: no counters, no join keys),
 // rows [counts[15], counts[0]) from the user-space producers' 64-byte EVENT records, whose
 // connection keys fold to the conn32 of the context rows (kernel records' trace ids become
 // their hashes through the trace-id table; user records carry hashes), so both kinds of record
@@ -461,12 +464,12 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
         const SigRec& m = imp[i - n_loc];
         decode_one(i, cap, m.ts, m.val, m.slot == kNoSlot ? -1 : (int)m.slot, m.tr, m.pod, m.pid, m.sn, m.cn, o, l,
                    unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
-      } else if (i < n_k) {
-        const uint8_t* r = framed + (size_t)i * kRecStride;
-        const uint2 h = *reinterpret_cast<const uint2*>(r);
-        const uint2 a = *reinterpret_cast<const uint2*>(r + 8), b = *reinterpret_cast<const uint2*>(r + 16);
+      } else if (i < n_k) {  // slot i & 7 of batch record i >> 3
+        const uint2 h = *reinterpret_cast<const uint2*>(framed + rec_off(i));
+        const uint2* sl = reinterpret_cast<const uint2*>(framed + slot_off(i));
+        const uint2 a = sl[0], b = sl[1];
         const EventC16 e{a.x, a.y, b.x, b.y};
-        bool ok = i < valid_k && h.x == 16u && (e.ctx_type & 0xFFu) < kDefFirst;
+        bool ok = i < valid_k && h.x == kRecPayload && (e.ctx_type & 0xFFu) < kDefFirst;
         const uint32_t cid = e.ctx_type >> 8;
         uint4 cx = ok && cid < (uint32_t)n_ctx ? ctx_tab[cid] : make_uint4(0u, 0u, 0u, 0u);
         // the pod's service as the pod table knows it now: a context defined before the pod's

@@ -91,7 +91,7 @@ struct ResultView {
 
 // The window's inputs: ring byte ranges (as the rings hold them) and the window metadata.
 struct WindowInput {
-  std::vector<Seg> kernel;  // framed BPF ring records (24-byte stride), in ring order
+  std::vector<Seg> kernel;  // framed BPF ring batch records (136-byte stride), in ring order
   std::vector<Seg> user;    // user-space producers' records: 64-byte EVENT or 32-byte User32
   int user_rec = 64;        // their size
   std::vector<Seg> spans;   // 64-byte SPAN records
@@ -197,6 +197,8 @@ class WindowEngine {
   EngineConfig cfg_;
   int nb_, max_ahead_;
   size_t off_kern_ = 0, off_user_ = 0, off_span_ = 0, in_bytes_ = 0;  // device input block layout
+  // the BPF ring bytes a window of sig_cap rows can hold: whole batch records
+  size_t kern_bytes() const { return (size_t)kRecStride * (((size_t)cfg_.sig_cap + kBatchSlots - 1) / kBatchSlots); }
   std::vector<std::pair<const uint8_t*, size_t>> registered_;
   size_t staged_bytes_ = 0, direct_bytes_ = 0;
   uint32_t *pod_sn_ = nullptr, *pod_host_ = nullptr, *ring_state_ = nullptr;

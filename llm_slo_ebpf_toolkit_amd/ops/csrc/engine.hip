@@ -163,7 +163,7 @@ void WindowEngine::alloc() {
   // device input block per buffer: [head (counts + labels) | framed ring records | user records | spans]
   const size_t head = (kHeadBytes + 4 * (size_t)G + 63) & ~size_t(63);
   off_kern_ = head;
-  off_user_ = (off_kern_ + (size_t)kRecStride * cfg_.sig_cap + 63) & ~size_t(63);
+  off_user_ = (off_kern_ + kern_bytes() + 63) & ~size_t(63);
   off_span_ = off_user_ + 64 * (size_t)cfg_.user_cap;
   in_bytes_ = off_span_ + 64 * (size_t)S;
   for (int b = 0; b < nb_; ++b) {
@@ -526,7 +526,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   if (in.user_rec != 64 && in.user_rec != 32 && in.user_rec != 24)
     throw std::invalid_argument("user records are 64, 32 or 24 bytes");
   if (kb % kRecStride || ub % in.user_rec || sb % 64) throw std::invalid_argument("segments must hold whole records");
-  const size_t n_k = kb / kRecStride, n_u = ub / in.user_rec, n_s = sb / 64;
+  // kernel rows: every slot of every batch record (definitions and pads become holes)
+  const size_t n_k = kb / kRecStride * kBatchSlots, n_u = ub / in.user_rec, n_s = sb / 64;
   if (n_k + n_u > (size_t)cfg_.sig_cap || n_u > (size_t)cfg_.user_cap || n_s > (size_t)cfg_.span_cap)
     throw std::invalid_argument("window exceeds the engine's capacity (events / user records / spans)");
   const int b = (int)(k % nb_);
@@ -571,7 +572,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     t = n;
   };
   auto tq = std::chrono::steady_clock::now();
-  dma(in.kernel, dst + off_kern_, (size_t)kRecStride * cfg_.sig_cap, staging_[b], st_off, copy_);
+  dma(in.kernel, dst + off_kern_, kern_bytes(), staging_[b], st_off, copy_);
   lap(tq, split_us_[0]);
   lap(tq, split_us_[1]);
   dma(in.user, dst + off_user_, 64 * (size_t)cfg_.user_cap, staging_[b], st_off, copy2_);

@@ -279,12 +279,19 @@ __host__ __device__ inline int part_of(uint64_t h) { return (int)(h >> (64 - kPa
 
 // ---- BPF ring records on the device ---------------------------------------------------------
 // The native engine DMAs the BPF ring's bytes as they are: 8-byte header {len | busy | discard,
-// pg_off} + 16-byte payload per record (runtime/csrc/bpfring.h), i.e. a 24-byte stride.
+// pg_off} + a batch of 8 16-byte slots per record (runtime/csrc/bpfring.h), i.e. a 136-byte
+// stride; row r of the window is slot r % 8 of record r / 8.
 constexpr uint32_t kRbBusy = 1u << 31, kRbDiscard = 1u << 30;
-constexpr int kRecStride = 24;
+constexpr int kBatchSlots = 8;
+constexpr uint32_t kRecPayload = 16 * kBatchSlots;
+constexpr int kRecStride = 8 + kRecPayload;
 constexpr uint32_t kDefTrace = 0xFD, kDefCtx = 0xFE, kDefFirst = 0xF0;
-// per-window ring accounting (device, packed into the packet): first busy record (min), records
-// of another size, context / trace definitions applied, discarded records, user-space records
+// the ring bytes of row i's record header and of its slot
+__host__ __device__ inline size_t rec_off(int i) { return (size_t)(i >> 3) * kRecStride; }
+__host__ __device__ inline size_t slot_off(int i) { return rec_off(i) + 8 + (size_t)(i & 7) * 16; }
+// per-window ring accounting (device, packed into the packet): first busy row (min; a batch
+// record's first slot), records of another size, context / trace definitions applied, discarded
+// records, user-space records
 enum RingState { kRsFirstBusy = 0, kRsForeign, kRsDefCtx, kRsDefTrace, kRsDiscard, kRsEvents, kRsOtherShard, kRsLen = 8 };
 
 // the 32-bit connection identity of context rows (runtime/csrc/records.h conn32)

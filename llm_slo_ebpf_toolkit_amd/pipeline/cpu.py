@@ -214,20 +214,22 @@ class CpuRingEngine:
                user_rec: int) -> None:
         t0 = time.perf_counter()
         framed = _gather(kernel)
-        fr = framed.view(np.uint32).reshape(-1, 6) if len(framed) else np.zeros((0, 6), np.uint32)
+        words = records.REC_STRIDE // 4
+        fr = framed.view(np.uint32).reshape(-1, words) if len(framed) else np.zeros((0, words), np.uint32)
         busy = np.nonzero(fr[:, 0] & np.uint32(records.RB_BUSY))[0] if len(fr) else np.zeros(0, np.int64)
-        first_busy = int(busy[0]) if len(busy) else -1
+        # in rows, like the device: the busy batch's first slot
+        first_busy = int(busy[0]) * records.BATCH_SLOTS if len(busy) else -1
         oracle.apply_ring_defs(framed, self.table, self.tmap, self.pod_sn)
         if first_busy >= 0:  # the engine stops at the first record still being written
             fr = fr.copy()
-            fr[first_busy:, 0] = np.uint32(records.RB_BUSY | 16)
+            fr[int(busy[0]):, 0] = np.uint32(records.RB_BUSY | records.REC_PAYLOAD)
             framed = fr.view(np.uint8).reshape(-1)
         ub = _gather(user)
         udt = {64: records.EVENT, 32: records.USER32, 24: records.USER24}[int(user_rec)]
         u = ub.view(udt) if len(ub) else np.zeros(0, dtype=udt)
         d = oracle.decode_window(framed, u, self.table, self.tmap, bases, pod_sn=self.pod_sn)
-        n_k = len(fr)
-        valid_k = ((fr[:, 0] == 16) & ((fr[:, 3] & np.uint32(0xFF)) < records.DEF_FIRST)) if n_k else np.zeros(0, bool)
+        hdr, sl = records.framed_slots(framed) if len(fr) else (np.zeros(0, np.uint32), np.zeros((0, 4), np.uint32))
+        valid_k = (hdr == records.REC_PAYLOAD) & ((sl[:, 1] & np.uint32(0xFF)) < records.DEF_FIRST)
         other = 0
         is_rec = np.concatenate([valid_k, np.ones(len(u), bool)])
         if self.shard_world > 1 and not self.split_rings:  # split rings: routed by the producers

@@ -124,9 +124,8 @@ class TraceMap:
 
 def apply_ring_defs(framed: np.ndarray, table: CtxTable, tmap: TraceMap, pod_sn: Dict[int, int]) -> None:
     """k_ring_defs: context rows (svc|node from pod metadata) and trace ids of a framed window."""
-    r = np.ascontiguousarray(framed).view(np.uint32).reshape(-1, 6)
-    ok = r[:, 0] == 16
-    p = r[ok, 2:6]
+    hdr, sl = records.framed_slots(framed)
+    p = sl[hdr == records.REC_PAYLOAD]
     t = p[:, 1] & 0xFF
     for c32, ct, pod, pid in p[t == records.DEF_CTX].tolist():
         table.map[ct >> 8] = (pod, pid, c32, pod_sn.get(pod, 0))
@@ -157,13 +156,14 @@ def decode_user24(u: np.ndarray, pod_sn: Dict[int, int], base: int) -> Decoded:
 
 def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases,
                   pod_sn: Dict[int, int] = None) -> Decoded:
-    """k_decode_window: rows [0, n framed) from the framed ring records (definitions, discarded
-    and busy records are holes: ts 0, no slot; kernel trace ids become their hashes), then the
-    user-space 64-byte records (trace hashes as is, conn32 connections)."""
-    r = np.ascontiguousarray(framed).view(np.uint32).reshape(-1, 6)
-    n_k = r.shape[0]
-    ev = r[:, 2:6].copy().view(records.EVENT16).reshape(-1)
-    valid = (r[:, 0] == 16) & ((ev["ctx_type"] & np.uint32(0xFF)) < records.DEF_FIRST)
+    """k_decode_window: rows [0, n framed) from the slots of the framed batch records (row r =
+    slot r % 8 of record r // 8; definitions, pads, discarded and busy records are holes: ts 0,
+    no slot; kernel trace ids become their hashes), then the user-space records (trace hashes
+    as is, conn32 connections)."""
+    hdr, sl = records.framed_slots(framed)
+    n_k = sl.shape[0]
+    ev = sl.copy().view(records.EVENT16).reshape(-1)
+    valid = (hdr == records.REC_PAYLOAD) & ((ev["ctx_type"] & np.uint32(0xFF)) < records.DEF_FIRST)
     d = decode_w16(ev, table, bases)
     d.trace = tmap.hashes(d.trace)
     if pod_sn:  # the pod's service as the pod table knows it now (not when its context was defined)

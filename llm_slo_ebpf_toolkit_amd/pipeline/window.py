@@ -36,6 +36,7 @@ from ..models.metrics import macro_f1_from_confusion
 
 # hist, status, misc(+16 value sums), dbg, confusion, stats, count, ring accounting
 PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16, 8)
+RS, BS = records.REC_STRIDE, records.BATCH_SLOTS  # BPF ring: bytes per batch record, rows (slots) per record
 RING_FIELDS = ("first_busy", "foreign", "def_ctx", "def_trace", "discarded", "events", "other_shard")
 USER_CAP = 1 << 18
 
@@ -325,7 +326,7 @@ class RingWindowSource:
     stamped before it keep theirs and decode against the bases the window ships."""
 
     def __init__(self, pipe: WindowPipeline, ring=None, user_ring=None, span_ring=None, cfg_set=None,
-                 shared: bool = False):
+                 shared: bool = False, flush=None):
         """``shared``: the rings have other consumers too (the node's other GPU workers, agent
         --gpus N): this source never moves a ring's consumer position, it only reports how far
         it is done (``done()``); the agent's controller frees ring space up to the slowest."""
@@ -337,6 +338,7 @@ class RingWindowSource:
         if cfg_set is None and ring is not None and getattr(ring, "emulated", False):
             cfg_set = lambda i, v: ring.cfg_set(i, v)  # noqa: E731
         self.cfg_set = cfg_set
+        self.flush = flush  # the cut's flush of the probes' per-CPU staging batches (BPF rings)
         self.clock = records.EpochClock()
         # page-lock the rings so windows DMA straight from them. Only the first mapping of the
         # double-mapped BPF ring data is registered (page-locking the second copy would count the
@@ -362,6 +364,7 @@ class RingWindowSource:
         self.kernel_seen = self.kernel_done  # end of the kernel ranges of every reaped window
         self.user_done = self.upos if user_ring is not None else 0
         self.span_done = self.spos if span_ring is not None else 0
+        # kernel ranges count batch records (RS ring bytes, BS rows each)
         self.pending: List[tuple] = []   # (k, kernel ranges [(pos, n, window cut)], user n, span n, h2d released)
         self.late: List[tuple] = []      # kernel ranges a window found still being written: (pos, n, window)
         self.late_dropped = 0            # late records too old for the 4 epoch bases of a later window
@@ -379,9 +382,12 @@ class RingWindowSource:
         return v
 
     def cut(self, now_ns: Optional[int] = None) -> Cut:
-        """Close the window at ``now_ns``: new epoch first, then the ring snapshots."""
+        """Close the window at ``now_ns``: new epoch first, then every CPU's staging batches onto
+        the ring (``flush``: collector/bpf.py BpfMaps.flush_cpus), then the ring snapshots."""
         t = int(now_ns if now_ns is not None else time.time_ns())
         self.publish_epoch(t)
+        if self.flush is not None:
+            self.flush()
         return Cut(kernel=self.ring.producer_pos if self.ring is not None else 0,
                    user=self.user_ring.head if self.user_ring is not None else 0,
                    spans=self.span_ring.head if self.span_ring is not None else 0,
@@ -398,18 +404,18 @@ class RingWindowSource:
             eng.wait(k)
             if not released:
                 self._release_user(nu, ns)
-            fb = int(eng.packet(k)[sum(PACKET_LAYOUT[:7])])  # ring state: first busy record (-1 = none)
-            if fb >= 0:  # records from fb on were still being written: re-submit them
-                skip = fb
+            fb = int(eng.packet(k)[sum(PACKET_LAYOUT[:7])])  # ring state: first busy row (-1 = none)
+            if fb >= 0:  # batch records from fb's on were still being written: re-submit them
+                skip = fb // BS
                 for pos, n, k0 in ranges:  # k0: the window whose cut first took the range
                     if skip >= n:
                         skip -= n
                         continue
-                    self.late.append((pos + 24 * skip, n - skip, k0))
-                    self.resubmitted += n - skip
+                    self.late.append((pos + RS * skip, n - skip, k0))
+                    self.resubmitted += BS * (n - skip)
                     skip = 0
             if ranges:
-                self.kernel_seen = max(self.kernel_seen, max(p + 24 * n for p, n, _ in ranges))
+                self.kernel_seen = max(self.kernel_seen, max(p + RS * n for p, n, _ in ranges))
         if self.ring is not None:
             # ring space is free up to the decoded records, short of the first range still needed:
             # a late range, or one a window in flight holds (a re-submitted range lies behind
@@ -477,25 +483,25 @@ class RingWindowSource:
                 # pipe.k - k0 = 3 on the tag would name a newer epoch (a timestamp shifted by whole
                 # windows): such records are dropped and counted instead.
                 if pipe.k - k0 >= 3:
-                    self.late_dropped += n
+                    self.late_dropped += BS * n
                     continue
-                take = min(n, budget - n_k)
+                take = min(n, (budget - n_k) // BS)
                 if take < n:
-                    self.late.append((pos + 24 * take, n - take, k0))
+                    self.late.append((pos + RS * take, n - take, k0))
                 if take:
                     k_ranges.append((pos, take, k0))
-                    kern += self._kernel_segments(pos, 24 * take)
-                    n_k += take
+                    kern += self._kernel_segments(pos, RS * take)
+                    n_k += BS * take
             span_b = cut.kernel - self.kpos
-            if span_b % 24:
-                raise RuntimeError("BPF ring holds records of another size (the probes emit 16-byte records only)")
-            take = min(span_b // 24, budget - n_k)
-            self.carried += span_b // 24 - take
+            if span_b % RS:
+                raise RuntimeError("BPF ring holds records of another size (the probes emit 8-slot batches only)")
+            take = min(span_b // RS, (budget - n_k) // BS)
+            self.carried += BS * (span_b // RS - take)
             if take:
                 k_ranges.append((self.kpos, take, pipe.k))
-                kern += self._kernel_segments(self.kpos, 24 * take)
-                n_k += take
-                self.kpos += 24 * take
+                kern += self._kernel_segments(self.kpos, RS * take)
+                n_k += BS * take
+                self.kpos += RS * take
         user, n_u = [], 0
         if self.user_ring is not None:
             cap = self.user_ring.capacity
@@ -560,7 +566,7 @@ def kernel_event_mask(events: np.ndarray) -> np.ndarray:
 def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim_ring=None,
                         user_rec: int = 64) -> List[ReplayImage]:
     """Run replay windows through the native probe model (one epoch per window cut, published
-    at the window start): kernel-signal events become framed EVENT16 ring bytes, GPU-signal
+    at the window start): kernel-signal events become framed batch records of EVENT16 slots, GPU-signal
     events stay 64-byte user-space records, spans stay 64-byte span records."""
     from ..runtime import load
 
@@ -580,9 +586,10 @@ def build_replay_images(windows, shift=None, window_ns: int = 1_000_000_000, sim
         # records stamped before the cut carry the previous epoch's tag (late writers across the
         # cut), the rest the epoch the agent published at the window start
         early = (kev["ts_ns"] < int(w.t0_ns)) & (kev["ts_ns"] != 0)
-        parts = [sim.encode(np.ascontiguousarray(kev[early]))]
+        parts = [sim.encode(np.ascontiguousarray(kev[early]), flush=False)]
         sim_ring.cfg_set(rt.CFG_EPOCH, clock.publish(int(w.t0_ns)))
-        parts.append(sim.encode(np.ascontiguousarray(kev[~early])))
+        # the window ends at the next cut: every CPU's staged batch is flushed into it
+        parts.append(sim.encode(np.ascontiguousarray(kev[~early]), flush=True))
         payload = np.concatenate(parts)
         uev = np.ascontiguousarray(w.events[~km])
         out.append(ReplayImage(framed=rt.frame_records(payload), spans=np.ascontiguousarray(w.spans),

@@ -1,15 +1,17 @@
 /* Host build of the probes' shared BPF plumbing: compiles mislo_probe.h as written (the
- * interning with definitions ahead of map inserts, the epoch-offset packing, the emit floors)
- * against in-process maps, and runs mislo_emit's logic over a file of 64-byte mislo_event
- * records. The records it "puts on the ring" go to the output file, 16 bytes each, so the
- * tests compare the C the kernel runs with the runtime's ProbeSim (runtime/csrc/probesim.cpp)
- * and the numpy ProbeModel (collector/records.py) record for record.
+ * interning with definitions ahead of map inserts, the epoch-offset packing, the emit floors,
+ * the per-CPU staging batches) against in-process maps, and runs mislo_emit's logic over a file
+ * of 64-byte mislo_event records. The batches it "puts on the ring" go to the output file, 128
+ * bytes each (8 slots), so the tests compare the C the kernel runs with the runtime's ProbeSim
+ * (runtime/csrc/probesim.cpp) and the numpy ProbeModel (collector/records.py) batch for batch.
+ * A record's CPU is its tid % HOST_CPUS (ProbeSim's model of the task's CPU).
  *
  *   probe_host IN OUT [--epoch-at IDX:VALUE]... [--trace-next N] [--ctx-next N]
- *                     [--floor TYPE:VALUE]... [--ring-cap RECORDS] [--shard POD:SHARD]...
+ *                     [--floor TYPE:VALUE]... [--ring-cap BATCHES] [--shard POD:SHARD]...
  *
- * --epoch-at publishes mislo_cfg[124] = VALUE before input record IDX (the agent's window
- * cut); --ring-cap makes bpf_ringbuf_output fail once that many records are out (a full ring);
+ * --epoch-at is the agent's window cut before input record IDX: mislo_cfg[124] = VALUE, then
+ * mislo_flush.bpf.c on every CPU in turn; the end of the input is a last cut (flush only);
+ * --ring-cap makes bpf_ringbuf_output fail once that many batches are out (a full ring);
  * --shard routes a pod's records to split ring SHARD (mislo_shards), written to OUT.SHARD. */
 #include <stdio.h>
 #include <stdlib.h>
@@ -25,9 +27,12 @@ struct hmap {
 	unsigned char *used;
 };
 
+#define HOST_CPUS 16
 static struct hmap traces_m, ctxs_m, pods_m, shards_m;
 static __u64 cfg_m[MISLO_CFG_SLOTS];
 static struct mislo_event scratch_m;
+static struct mislo_stage stages_m[HOST_CPUS][MISLO_SHARDS];
+static unsigned cur_cpu;
 static FILE *ring_out, *shard_out[MISLO_SHARDS];
 static const char *out_path;
 static unsigned long long ring_n, ring_cap = ~0ull;
@@ -82,6 +87,8 @@ void *bpf_map_lookup_elem(void *map, const void *key)
 		return idx < MISLO_CFG_SLOTS ? &cfg_m[idx] : 0;
 	if (map == (void *)&mislo_scratch)
 		return idx == 0 ? &scratch_m : 0;
+	if (map == (void *)&mislo_stages)
+		return idx < MISLO_SHARDS ? &stages_m[cur_cpu][idx] : 0;
 	struct hmap *m = hmap_of(map);
 	if (!m)
 		return 0;
@@ -140,7 +147,7 @@ long bpf_ringbuf_output(void *ringbuf, void *data, __u64 size, __u64 flags)
 {
 	(void)flags;
 	int s = shard_of_ring(ringbuf);
-	if (s < 0 || size != 16)
+	if (s < 0 || size != MISLO_BATCH_BYTES)
 		return -22;
 	if (ring_n >= ring_cap)
 		return -11; /* -EAGAIN: ring full */
@@ -155,7 +162,7 @@ long bpf_ringbuf_output(void *ringbuf, void *data, __u64 size, __u64 flags)
 		}
 		f = shard_out[s];
 	}
-	if (fwrite(data, 16, 1, f) != 1)
+	if (fwrite(data, MISLO_BATCH_BYTES, 1, f) != 1)
 		return -5;
 	++ring_n;
 	return 0;
@@ -214,25 +221,34 @@ int main(int argc, char **argv)
 		perror("open");
 		return 2;
 	}
+	for (unsigned c = 0; c < HOST_CPUS; ++c)
+		for (unsigned sh = 0; sh < MISLO_SHARDS; ++sh)
+			mislo_pad_batch(&stages_m[c][sh].b);
 	struct mislo_event ev;
 	unsigned long long n = 0;
 	unsigned e = 0;
 	while (fread(&ev, sizeof(ev), 1, in) == 1) {
-		while (e < n_ep && ep[e].idx <= n)
+		while (e < n_ep && ep[e].idx <= n) { /* the agent's cut: epoch, then every CPU's flush */
 			cfg_m[MISLO_CFG_EPOCH] = ep[e++].value;
-		/* mislo_emit with the record's own task / pod: the floor, then the working record */
+			for (cur_cpu = 0; cur_cpu < HOST_CPUS; ++cur_cpu)
+				mislo_flush_cpu();
+		}
+		/* mislo_emit with the record's own task / pod on its CPU: the floor, then the working record */
+		cur_cpu = ev.tid % HOST_CPUS;
 		if (!mislo_below_floor(ev.signal_type, ev.value)) {
 			scratch_m = ev;
 			mislo_submit(&scratch_m);
 		}
 		++n;
 	}
+	for (cur_cpu = 0; cur_cpu < HOST_CPUS; ++cur_cpu)
+		mislo_flush_cpu();
 	fclose(in);
 	fclose(ring_out);
 	for (int s = 1; s < MISLO_SHARDS; ++s)
 		if (shard_out[s])
 			fclose(shard_out[s]);
-	printf("events %llu records %llu trace_next %llu ctx_next %llu\n", n, ring_n,
+	printf("events %llu batches %llu trace_next %llu ctx_next %llu\n", n, ring_n,
 	       (unsigned long long)cfg_m[MISLO_CFG_TRACE_NEXT], (unsigned long long)cfg_m[MISLO_CFG_CTX_NEXT]);
 	return 0;
 }

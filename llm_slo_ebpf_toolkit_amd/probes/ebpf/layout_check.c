@@ -35,6 +35,10 @@ int main(void)
 		printf("bad mislo_def16 layout\n");
 		return 1;
 	}
+	if (sizeof(struct mislo_batch) != 16 * MISLO_BATCH_SLOTS || MISLO_BATCH_SLOTS != 8) {
+		printf("bad mislo_batch layout\n");
+		return 1;
+	}
 	printf("mislo_event layout ok (64 bytes), mislo_event16 ok (16 bytes), mislo_def16 ok (16 bytes)\n");
 	printf("const %u %u %u %u %u\n", MISLO_DEF_FIRST, MISLO_DEF_TRACE, MISLO_DEF_CTX, MISLO_KERNEL_CTX_LIMIT,
 	       MISLO_KERNEL_TRACE_LIMIT);

@@ -21,10 +21,16 @@
  *   mislo_ctxs    (pod, pid, conn32) -> context id in 1 .. 2^23 - 1, assigned on first sight.
  *                 When the counter nears the limit the agent clears the map and the counter
  *                 (collector/bpf.py reset_ctx_ids) and ids are defined afresh;
- *   mislo_scratch per-CPU 64-byte mislo_event the probe fills before mislo_submit() packs it.
- * Interning emits the definition record first and inserts the map entry only once the
- * definition is on the ring: any record that carries the id is written after its definition,
- * so ring order is enough for the GPU to resolve it (no map reads on the agent's window path).
+ *   mislo_scratch per-CPU 64-byte mislo_event the probe fills before mislo_submit() packs it;
+ *   mislo_stages  per-CPU staging batch per ring: slots go on the ring 8 to a record (struct
+ *                 mislo_batch, 136 ring bytes) -- when the batch is full, when a definition joins
+ *                 it, before a slot of a newer epoch joins it, and at the agent's window cut,
+ *                 which runs mislo_flush.bpf.c on every CPU (BPF_PROG_TEST_RUN on that CPU)
+ *                 after publishing the new epoch. Unused slots of a flushed batch are pads.
+ * Interning puts the definition on the ring first (its batch is flushed at once) and inserts the
+ * map entry only then: any record that carries the id, on any CPU, is written after its
+ * definition, so ring order is enough for the GPU to resolve it (no map reads on the agent's
+ * window path).
  * A definition the ring drops (full) leaves the id unassigned; the event then carries id 0.
  * The userspace model of exactly this logic is runtime/csrc/probesim.cpp (ProbeSim), which
  * the tests and the replay producer drive.
@@ -39,6 +45,12 @@
 #include <bpf/bpf_tracing.h>
 
 #include "mislo_record.h"
+
+#if defined(__clang__)
+#define MISLO_UNROLL _Pragma("unroll")
+#else
+#define MISLO_UNROLL
+#endif
 
 #define MISLO_CFG_CLOCK 0
 #define MISLO_CFG_NODE 1
@@ -136,6 +148,23 @@ struct {
 	__type(value, struct mislo_event);
 } mislo_scratch SEC(".maps");
 
+/* A CPU's staging batch for one ring (mislo_stage_put). */
+struct mislo_stage {
+	__u32 n;     /* slots filled */
+	__u32 busy;  /* a program of this CPU is inside mislo_stage_put: one that interrupts it (the
+	                cut's flush, an NMI-context probe) leaves the batch alone */
+	__u64 epoch; /* the epoch the slots were written in (mislo_cfg[MISLO_CFG_EPOCH]) */
+	struct mislo_batch b;
+};
+
+struct {
+	__uint(type, BPF_MAP_TYPE_PERCPU_ARRAY);
+	__uint(max_entries, MISLO_SHARDS);
+	__type(key, __u32); /* ring (shard) */
+	__type(value, struct mislo_stage);
+	__uint(pinning, LIBBPF_PIN_BY_NAME);
+} mislo_stages SEC(".maps");
+
 static __always_inline __u64 mislo_cfg_get(__u32 idx)
 {
 	__u64 *v = bpf_map_lookup_elem(&mislo_cfg, &idx);
@@ -228,35 +257,100 @@ static __always_inline __u64 mislo_conn_key(const struct mislo_event *e)
 	return z ? z : 1;
 }
 
-/* Put a 16-byte record on the ring. No wakeup: the agent reads the ring at its window cuts,
- * never from epoll, so a per-record consumer wakeup would be pure overhead. 0 = written. */
-static __always_inline long mislo_out(const void *r, __u32 shard)
+/* Put a batch on a ring. No wakeup: the agent reads the ring at its window cuts, never from
+ * epoll, so a per-record consumer wakeup would be pure overhead. 0 = written. */
+#define MISLO_BATCH_BYTES (16 * MISLO_BATCH_SLOTS)
+static __always_inline long mislo_ring_out(void *b, __u32 shard)
 {
 	switch (shard) {
 #if MISLO_SHARDS > 1
 	case 1:
-		return bpf_ringbuf_output(&mislo_events1, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events1, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 #endif
 #if MISLO_SHARDS > 2
 	case 2:
-		return bpf_ringbuf_output(&mislo_events2, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events2, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 #endif
 #if MISLO_SHARDS > 3
 	case 3:
-		return bpf_ringbuf_output(&mislo_events3, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events3, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 #endif
 #if MISLO_SHARDS > 4
 	case 4:
-		return bpf_ringbuf_output(&mislo_events4, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events4, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 	case 5:
-		return bpf_ringbuf_output(&mislo_events5, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events5, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 	case 6:
-		return bpf_ringbuf_output(&mislo_events6, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events6, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 	case 7:
-		return bpf_ringbuf_output(&mislo_events7, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events7, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
 #endif
 	default:
-		return bpf_ringbuf_output(&mislo_events, (void *)r, 16, BPF_RB_NO_WAKEUP);
+		return bpf_ringbuf_output(&mislo_events, b, MISLO_BATCH_BYTES, BPF_RB_NO_WAKEUP);
+	}
+}
+
+static __always_inline void mislo_pad_batch(struct mislo_batch *b)
+{
+MISLO_UNROLL
+	for (int j = 0; j < MISLO_BATCH_SLOTS; ++j) {
+		b->slot[j].ts_off = 0;
+		b->slot[j].ctx_type = MISLO_DEF_PAD;
+		b->slot[j].value_milli = 0;
+		b->slot[j].trace_tag = 0;
+	}
+}
+
+/* The batch goes on its ring (a full ring drops it whole); the stage starts over, all pads. */
+static __always_inline long mislo_stage_flush(struct mislo_stage *st, __u32 shard)
+{
+	long rc = mislo_ring_out(&st->b, shard);
+	mislo_pad_batch(&st->b);
+	st->n = 0;
+	return rc;
+}
+
+/* A 16-byte slot into this CPU's batch for `shard` (flush_now: a definition -- its batch goes on
+ * the ring before the caller publishes the id in a map). 0 = staged / written. */
+static __always_inline long mislo_stage_put(const void *slot, __u32 shard, int flush_now)
+{
+	__u32 key = shard;
+	struct mislo_stage *st = bpf_map_lookup_elem(&mislo_stages, &key);
+	if (!st)
+		return -1;
+	__u64 epoch = mislo_cfg_get(MISLO_CFG_EPOCH);
+	if (st->busy) { /* this CPU's batch is mid-update below us: a batch of its own */
+		struct mislo_batch one;
+		mislo_pad_batch(&one);
+		__builtin_memcpy(&one.slot[0], slot, 16);
+		return mislo_ring_out(&one, shard);
+	}
+	st->busy = 1;
+	if (st->n && st->epoch != epoch) /* a batch holds one epoch's slots */
+		mislo_stage_flush(st, shard);
+	__u32 n = st->n & (MISLO_BATCH_SLOTS - 1);
+	__builtin_memcpy(&st->b.slot[n], slot, 16);
+	st->n = n + 1;
+	st->epoch = epoch;
+	long rc = 0;
+	if (st->n >= MISLO_BATCH_SLOTS || flush_now)
+		rc = mislo_stage_flush(st, shard);
+	st->busy = 0;
+	return rc;
+}
+
+/* The window cut's flush of this CPU's batches (mislo_flush.bpf.c, run on each CPU in turn). */
+static __always_inline void mislo_flush_cpu(void)
+{
+MISLO_UNROLL
+	for (__u32 s = 0; s < MISLO_SHARDS; ++s) {
+		__u32 key = s;
+		struct mislo_stage *st = bpf_map_lookup_elem(&mislo_stages, &key);
+		if (!st || !st->n || st->busy)
+			continue;
+		st->busy = 1;
+		mislo_stage_flush(st, s);
+		st->busy = 0;
 	}
 }
 
@@ -290,7 +384,7 @@ static __always_inline __u32 mislo_ctx_id(__u32 pod_id, __u32 pid, __u32 c32, __
 		return 0;
 	__u32 v = (__u32)fresh;
 	struct mislo_def16 d = {.a = c32, .tag_id = MISLO_DEF_CTX | (v << 8), .b = pod_id, .c = pid};
-	if (mislo_out(&d, shard))
+	if (mislo_stage_put(&d, shard, 1))
 		return 0; /* ring full: leave the context unnamed */
 	if (bpf_map_update_elem(&mislo_ctxs, &k, &v, BPF_NOEXIST) == 0)
 		return v;
@@ -316,7 +410,7 @@ static __always_inline __u32 mislo_trace_id(__u64 h, __u32 shard)
 		return 0;
 	__u32 v = mislo_trace_slot(__sync_fetch_and_add(next, 1));
 	struct mislo_def16 d = {.a = v, .tag_id = MISLO_DEF_TRACE, .b = (__u32)h, .c = (__u32)(h >> 32)};
-	if (mislo_out(&d, shard))
+	if (mislo_stage_put(&d, shard, 1))
 		return 0;
 	if (bpf_map_update_elem(&mislo_traces, &key, &v, BPF_NOEXIST) == 0)
 		return v;
@@ -324,8 +418,8 @@ static __always_inline __u32 mislo_trace_id(__u64 h, __u32 shard)
 	return id ? *id : 0;
 }
 
-/* Pack the working record into the 16-byte ring record (timestamp as an offset from the
- * published epoch, tagged with it) and publish it. */
+/* Pack the working record into its 16-byte slot (timestamp as an offset from the published
+ * epoch, tagged with it) and stage it in this CPU's batch. */
 static __always_inline void mislo_submit(struct mislo_event *e)
 {
 	struct mislo_event16 r;
@@ -345,7 +439,7 @@ static __always_inline void mislo_submit(struct mislo_event *e)
 	r.ctx_type = (e->signal_type & 0xFFu) | (ctx << 8);
 	r.value_milli = mislo_milli(e->signal_type, e->value);
 	r.trace_tag = (tid & MISLO_TRACE_ID_MASK) | ((__u32)(epoch & 3) << MISLO_EPOCH_TAG_SHIFT);
-	mislo_out(&r, shard);
+	mislo_stage_put(&r, shard, 0);
 }
 
 /* Emit a record attributed to the current task. */

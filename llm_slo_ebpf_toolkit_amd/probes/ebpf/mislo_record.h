@@ -3,8 +3,8 @@
  * layout test.
  *   struct mislo_event   (64 B, collector/records.py EVENT): the probes' working record (per-CPU
  *                        scratch) and the user-space producers' ring record (rocprofiler tool);
- *   struct mislo_event16 (16 B, records.py EVENT16): the one record the probes put on the BPF
- *                        ring. The timestamp is a 32-bit offset from the epoch the agent last
+ *   struct mislo_event16 (16 B, records.py EVENT16): the slot the probes put on the BPF ring,
+ *                        8 to a ring record (struct mislo_batch). The timestamp is a 32-bit offset from the epoch the agent last
  *                        published (mislo_cfg[MISLO_CFG_EPOCH]) and that epoch's 2-bit tag sits
  *                        in the top of trace_tag, so records written across a window cut decode
  *                        exactly (a window carries its last 4 epoch bases). The value is fixed
@@ -79,10 +79,18 @@ struct mislo_event16 {
 	__u32 trace_tag;   /* bits 0-29 interned trace id (0 = none), bits 30-31 epoch tag */
 };
 
-/* definition records (same 16-byte stride as mislo_event16) */
+/* definition slots (same 16 bytes as mislo_event16) */
 #define MISLO_DEF_FIRST 0xF0u
+#define MISLO_DEF_PAD 0xFCu   /* an unused slot of a batch flushed before it filled: {0, 0xFC, 0, 0} */
 #define MISLO_DEF_TRACE 0xFDu
 #define MISLO_DEF_CTX 0xFEu
+
+/* The ring record: a batch of 16-byte slots a CPU staged (mislo_probe.h mislo_stage_put), one
+ * 8-byte ring header per MISLO_BATCH_SLOTS slots -- 17 ring bytes per event instead of 24. */
+#define MISLO_BATCH_SLOTS 8
+struct mislo_batch {
+	struct mislo_event16 slot[MISLO_BATCH_SLOTS];
+};
 struct mislo_def16 {
 	__u32 a;       /* ctx: conn32; trace: trace id */
 	__u32 tag_id;  /* bits 0-7 MISLO_DEF_*, bits 8-31 ctx id (ctx definitions) */

@@ -239,12 +239,36 @@ bool Ringbuf::append_framed(const uint8_t* bytes, uint64_t n, int threads) {
 }
 
 void frame_records(const Rec16* recs, uint64_t n, uint8_t* out) {
-  for (uint64_t i = 0; i < n; ++i) {
+  if (n % kBatchSlots) throw std::invalid_argument("frame_records: whole batches of 8 slots only");
+  for (uint64_t i = 0; i < n / kBatchSlots; ++i) {
     RbHeader h{kRecPayload, 0};
     std::memcpy(out + i * kRecStride, &h, sizeof(h));
-    std::memcpy(out + i * kRecStride + kRbHdrSz, &recs[i], kRecPayload);
+    std::memcpy(out + i * kRecStride + kRbHdrSz, &recs[i * kBatchSlots], kRecPayload);
   }
 }
+
+namespace {
+// One batch record's slots: events to `out` (while there is room; returns false when full),
+// definitions to `defs`, pads counted.
+template <class Def>
+bool take_slots(const uint8_t* payload, Rec16* out, uint64_t cap, uint64_t* k, Def&& def, uint64_t* pads) {
+  Rec16 r[kBatchSlots];
+  std::memcpy(r, payload, sizeof(r));
+  uint64_t ev = 0;
+  for (uint32_t j = 0; j < kBatchSlots; ++j) ev += (r[j].ctx_type & 0xFFu) < kDefFirst;
+  if (*k + ev > cap) return false;  // the whole batch waits for the next window
+  for (uint32_t j = 0; j < kBatchSlots; ++j) {
+    const uint32_t t = r[j].ctx_type & 0xFFu;
+    if (t < kDefFirst)
+      out[(*k)++] = r[j];
+    else if (t == kPad)
+      ++*pads;
+    else
+      def(r[j]);
+  }
+  return true;
+}
+}  // namespace
 
 // ---- RingbufConsumer --------------------------------------------------------------------
 
@@ -275,15 +299,10 @@ ConsumeStats RingbufConsumer::consume_serial(Rec16* out, uint64_t cap, std::vect
     }
     const uint32_t plen = len & ~(kRbBusyBit | kRbDiscardBit);
     if (!(len & kRbDiscardBit) && plen == kRecPayload) {
-      Rec16 r;
-      std::memcpy(&r, hdr + kRbHdrSz, sizeof(r));
-      if ((r.ctx_type & 0xFFu) >= kDefFirst) {
-        defs.push_back(r);
-        ++st.defs;
-      } else {
-        if (st.events >= cap) break;  // window full: the record stays for the next window
-        out[st.events++] = r;
-      }
+      // window full: the record stays for the next window
+      if (!take_slots(hdr + kRbHdrSz, out, cap, &st.events, [&](const Rec16& d) { defs.push_back(d), ++st.defs; },
+                      &st.pads))
+        break;
     } else if (len & kRbDiscardBit) {
       ++st.discarded;
     } else {
@@ -306,12 +325,13 @@ ConsumeStats RingbufConsumer::consume(Rec16* out, uint64_t cap, std::vector<Rec1
     return st;
   }
   const uint64_t span = prod - cons;
-  // fast path: every record in range is a 16-byte payload (24 ring bytes), so record i sits
-  // at cons + 24 i and chunks can be compacted independently; a foreign size anywhere sends
-  // the window down the serial walk
+  // fast path: every record in range is a batch (136 ring bytes), so record i sits at
+  // cons + 136 i and chunks can be compacted independently; a foreign size anywhere sends the
+  // window down the serial walk
   if (span % kRecStride) return consume_serial(out, cap, defs, cons, prod);
   const uint64_t n = span / kRecStride;
-  const uint64_t n_scan = std::min<uint64_t>(n, cap);  // defs/discards only shrink the output
+  // defs / pads / discards only shrink the output: scanning cap / 8 batches always fits
+  const uint64_t n_scan = std::min<uint64_t>(n, cap / kBatchSlots);
   const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads() * 2, n_scan / 8192 + 1));
   if ((int)tasks_.size() < nt) tasks_.resize(nt);
   const uint8_t* data = rb_->data();
@@ -320,11 +340,11 @@ ConsumeStats RingbufConsumer::consume(Rec16* out, uint64_t cap, std::vector<Rec1
     Task& tk = tasks_[t];
     tk.lo = n_scan * t / nt;
     tk.hi = n_scan * (t + 1) / nt;
-    tk.k = tk.discards = 0;
+    tk.k = tk.discards = tk.pads = 0;
     tk.busy = -1;
     tk.foreign = false;
     tk.defs.clear();
-    Rec16* dst = out + tk.lo;
+    Rec16* dst = out + tk.lo * kBatchSlots;
     for (uint64_t i = tk.lo; i < tk.hi; ++i) {
       const uint8_t* hdr = data + ((cons + i * kRecStride) & mask);
       const uint32_t len = load_len(hdr);
@@ -340,13 +360,7 @@ ConsumeStats RingbufConsumer::consume(Rec16* out, uint64_t cap, std::vector<Rec1
         ++tk.discards;
         continue;
       }
-      Rec16 r;
-      std::memcpy(&r, hdr + kRbHdrSz, sizeof(r));
-      if ((r.ctx_type & 0xFFu) >= kDefFirst) {
-        tk.defs.emplace_back(i, r);
-        continue;
-      }
-      dst[tk.k++] = r;
+      take_slots(hdr + kRbHdrSz, dst, ~0ull, &tk.k, [&](const Rec16& d) { tk.defs.emplace_back(i, d); }, &tk.pads);
     }
   });
   for (int t = 0; t < nt; ++t)
@@ -367,9 +381,10 @@ ConsumeStats RingbufConsumer::consume(Rec16* out, uint64_t cap, std::vector<Rec1
   uint64_t w = 0;
   for (int t = 0; t <= last; ++t) {
     Task& tk = tasks_[t];
-    if (w != tk.lo && tk.k) std::memmove(out + w, out + tk.lo, tk.k * sizeof(Rec16));
+    if (w != tk.lo * kBatchSlots && tk.k) std::memmove(out + w, out + tk.lo * kBatchSlots, tk.k * sizeof(Rec16));
     w += tk.k;
     st.discarded += tk.discards;
+    st.pads += tk.pads;
     for (auto& d : tk.defs) defs.push_back(d.second);
     st.defs += tk.defs.size();
   }

@@ -13,11 +13,12 @@
 // may only pass records whose header is not busy, and frees space by storing consumer_pos.
 //
 // The agent's consumer (RingbufConsumer) does not hand records to a callback one by one, as
-// libbpf's ring_buffer__consume does: it compacts a window's committed 16-byte EVENT16
-// payloads (probes/ebpf/mislo_record.h mislo_event16; 24 ring bytes each) straight into the
+// libbpf's ring_buffer__consume does: it compacts a window's committed EVENT16 slots
+// (probes/ebpf/mislo_record.h mislo_event16; batches of 8 per 136-byte record) straight into the
 // pinned buffer the window is DMA'd from, on a worker pool, diverting the probes' id
-// definition records (mislo_def16: context rows, trace ids) to a side list, skipping discarded
-// records and stopping at the first busy one (libbpf semantics: nothing past it is consumed).
+// definition slots (mislo_def16: context rows, trace ids) to a side list, skipping pads and
+// discarded records and stopping at the first busy one (libbpf semantics: nothing past it is
+// consumed).
 //
 // For tests, the benchmark and the CPU-only CI, `Ringbuf::create_shm` builds the identical
 // user-visible layout over shared memory (double-mapped data, a meta page holding the
@@ -40,14 +41,21 @@ class WorkerPool;
 constexpr uint32_t kRbBusyBit = 1u << 31;
 constexpr uint32_t kRbDiscardBit = 1u << 30;
 constexpr uint32_t kRbHdrSz = 8;
-constexpr uint32_t kRecPayload = 16;                 // mislo_event16 / mislo_def16
-constexpr uint32_t kRecStride = kRbHdrSz + kRecPayload;  // 24 ring bytes per record
-constexpr int kCfgSlots = 128;                        // mislo_cfg entries (u64)
+// A ring record is a batch: the probes stage 16-byte slots per CPU (mislo_probe.h mislo_stage)
+// and put kBatchSlots of them on the ring in one record, so the 8-byte header is paid once per
+// batch instead of once per event (17 ring bytes per event instead of 24). Row r of a window is
+// slot r % kBatchSlots of record r / kBatchSlots.
+constexpr uint32_t kSlotBytes = 16;                      // mislo_event16 / mislo_def16 / pad
+constexpr uint32_t kBatchSlots = 8;
+constexpr uint32_t kRecPayload = kSlotBytes * kBatchSlots;  // 128
+constexpr uint32_t kRecStride = kRbHdrSz + kRecPayload;     // 136 ring bytes per record
+constexpr int kCfgSlots = 128;                              // mislo_cfg entries (u64)
 
-// definition records (mislo_record.h): low byte of ctx_type
+// non-event slots (mislo_record.h): low byte of ctx_type
 constexpr uint32_t kDefTrace = 0xFD;  // {ts_off = trace id, ctx_type, value_milli = hash lo, trace_tag = hash hi}
 constexpr uint32_t kDefCtx = 0xFE;    // {ts_off = conn32, ctx_type = type | id << 8, value_milli = pod, trace_tag = pid}
-constexpr uint32_t kDefFirst = 0xF0;  // types >= this never reach the GPU
+constexpr uint32_t kPad = 0xFC;       // an unused slot of a batch flushed before it filled
+constexpr uint32_t kDefFirst = 0xF0;  // types >= this never reach the GPU as events
 
 struct Rec16 {
   uint32_t ts_off, ctx_type, value_milli, trace_tag;
@@ -126,8 +134,9 @@ class Ringbuf {
 };
 
 struct ConsumeStats {
-  uint64_t events = 0;     // EVENT16 records written to the output
-  uint64_t defs = 0;       // definition records diverted
+  uint64_t events = 0;     // EVENT16 slots written to the output
+  uint64_t defs = 0;       // definition slots diverted
+  uint64_t pads = 0;       // unused slots of partial batches
   uint64_t discarded = 0;  // records committed with the discard bit
   uint64_t foreign = 0;    // records of another payload size (skipped, counted)
   uint64_t begin_pos = 0, end_pos = 0;  // consumed ring range [begin, end)
@@ -151,7 +160,7 @@ class RingbufConsumer {
   Ringbuf* rb_;
   std::unique_ptr<WorkerPool> pool_;
   struct Task {
-    uint64_t lo, hi, k, discards;
+    uint64_t lo, hi, k, discards, pads;
     int64_t busy;  // first busy index or -1
     bool foreign;
     std::vector<std::pair<uint64_t, Rec16>> defs;
@@ -159,8 +168,10 @@ class RingbufConsumer {
   std::vector<Task> tasks_;
 };
 
-// Frames 16-byte payloads as committed ring records (header + payload, 24 bytes each, pg_off
-// left 0): the byte image Ringbuf::append_framed publishes.
+// Frames batches of kBatchSlots slots as committed ring records (header + 128-byte payload,
+// pg_off left 0): the byte image Ringbuf::append_framed publishes. `n` is a multiple of kBatchSlots.
 void frame_records(const Rec16* recs, uint64_t n, uint8_t* out);
+
+inline Rec16 pad_slot() { return Rec16{0, kPad, 0, 0}; }
 
 }  // namespace mislo

@@ -137,6 +137,16 @@ int bpf_link_create_perf(int prog_fd, int perf_fd) {
   return sys_bpf(BPF_LINK_CREATE, &a);
 }
 
+int bpf_prog_run_on_cpu(int prog_fd, uint32_t cpu) {
+  union bpf_attr a;
+  std::memset(&a, 0, sizeof(a));
+  a.test.prog_fd = (uint32_t)prog_fd;
+  a.test.flags = BPF_F_TEST_RUN_ON_CPU;
+  a.test.cpu = cpu;
+  const int r = sys_bpf(BPF_PROG_TEST_RUN, &a);
+  return r < 0 ? r : (int)a.test.retval;
+}
+
 int close_fd(int fd) { return close(fd) < 0 ? -errno : 0; }
 
 bool bpf_syscall_available() {

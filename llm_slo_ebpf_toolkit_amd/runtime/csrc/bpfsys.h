@@ -49,4 +49,9 @@ int perf_uprobe_open(const UprobeAttr& a);
 int bpf_link_create_perf(int prog_fd, int perf_fd);
 int close_fd(int fd);
 
+// BPF_PROG_TEST_RUN of a raw_tp program on one CPU (BPF_F_TEST_RUN_ON_CPU: the kernel runs it
+// there, in an IPI): the agent's window-cut flush of that CPU's staging batches
+// (probes/ebpf/mislo_flush.bpf.c). The program's return value, or -errno.
+int bpf_prog_run_on_cpu(int prog_fd, uint32_t cpu);
+
 }  // namespace mislo

@@ -11,8 +11,12 @@
 //     ahead of it in ring order;
 //   * trace hash -> id from the mislo_traces LRU map, same protocol (TRACE definitions);
 //   * timestamp as an offset from the epoch the agent published in mislo_cfg[124], tagged;
-//   * bpf_ringbuf_output of the 16-byte record.
-// Thread-safe (the maps sit behind a mutex; the ring's own lock orders reservations).
+//   * the 16-byte slot into the CPU's staging batch (mislo_stage_put): a batch goes on the ring
+//     as one 136-byte record when its 8 slots are full, when a definition joins it (a definition
+//     is on the ring before its id is in the map), before a slot of a newer epoch joins it, and
+//     at the agent's window cut (flush(): every CPU's batch, CPU 0 first; unused slots are pads).
+// A task's CPU is modelled as tid % cpus. Thread-safe (maps and batches behind a mutex; the
+// ring's own lock orders reservations).
 #pragma once
 
 #include <cstdint>
@@ -32,24 +36,43 @@ class ProbeSim {
  public:
   // cfg: the emulated mislo_cfg array (kCfgSlots u64, e.g. Ringbuf::cfg()); shift256: records.py
   // milli_shift_table
-  ProbeSim(uint64_t* cfg, const int8_t* shift256, size_t trace_lru = 1u << 20);
-  // every record through mislo_emit: floors checked, defs + event output into `rb`; returns the
-  // number of event records committed (a full ring drops, as bpf_ringbuf_output does)
-  uint64_t submit(Ringbuf& rb, const EventRec* ev, size_t n);
-  // the same records as ring payloads, appended to `out` (an image for append_framed)
-  void encode(const EventRec* ev, size_t n, std::vector<Rec16>& out);
-  uint64_t dropped() const { return dropped_; }
+  ProbeSim(uint64_t* cfg, const int8_t* shift256, size_t trace_lru = 1u << 20, uint32_t cpus = 16);
+  // every record through mislo_emit: floors checked, defs + event slots staged, full batches
+  // output into `rb`, and with `flush` the partial batches too (the agent's cut); returns the
+  // number of events committed to the ring by this call (a full ring drops a whole batch, as
+  // bpf_ringbuf_output does)
+  uint64_t submit(Ringbuf& rb, const EventRec* ev, size_t n, bool flush = true);
+  uint64_t flush(Ringbuf& rb);
+  // the same records as ring payloads (whole batches of 8 slots), appended to `out` (an image for
+  // append_framed); encode_flush appends the partial batches
+  void encode(const EventRec* ev, size_t n, std::vector<Rec16>& out, bool flush = true);
+  void encode_flush(std::vector<Rec16>& out);
+  uint64_t dropped() const { return dropped_; }  // events lost to a full ring
+  uint64_t batches() const { return batches_; }  // batches output (ring records)
   size_t n_ctx() const { return ctx_.size(); }
   size_t n_traces() const { return traces_.size(); }
   // what the agent does when the id space runs low: clear the maps and counters
   void reset_maps();
 
  private:
-  template <class Emit>
-  void one(const EventRec& e, Emit&& emit);
+  struct Stage {
+    uint32_t n = 0;
+    uint64_t epoch = 0;
+    Rec16 slot[kBatchSlots];
+  };
+  // mislo_stage_put: returns false when the batch carrying `r` could not go on the ring (only
+  // meaningful for definitions, which flush at once)
+  template <class Out>
+  bool put(uint32_t cpu, const Rec16& r, bool def, Out&& out);
+  template <class Out>
+  bool flush_stage(Stage& st, Out&& out);
+  template <class Out>
+  void one(const EventRec& e, Out&& out);
   uint64_t* cfg_;
   int8_t shift_[256];
   size_t trace_lru_;
+  std::vector<Stage> stages_;
+  uint64_t batches_ = 0;
   std::mutex mu_;
   std::unordered_map<uint64_t, uint32_t> traces_;
   struct CtxKey {

@@ -277,6 +277,7 @@ class PyConsumer {
     py::dict d;
     d["events"] = st.events;
     d["defs"] = st.defs;
+    d["pads"] = st.pads;
     d["discarded"] = st.discarded;
     d["foreign"] = st.foreign;
     d["begin_pos"] = st.begin_pos;
@@ -294,22 +295,33 @@ class PyConsumer {
 
 class PyProbeSim {
  public:
-  PyProbeSim(PyRingbuf& rb, py::array_t<int8_t, py::array::c_style | py::array::forcecast> shift, size_t trace_lru)
-      : rb_(rb), sim_(rb.rb()->cfg(), shift_of(shift), trace_lru) {}
-  uint64_t submit(py::buffer events) {
+  PyProbeSim(PyRingbuf& rb, py::array_t<int8_t, py::array::c_style | py::array::forcecast> shift, size_t trace_lru,
+             uint32_t cpus)
+      : rb_(rb), sim_(rb.rb()->cfg(), shift_of(shift), trace_lru, cpus) {}
+  uint64_t submit(py::buffer events, bool flush) {
     auto [ev, n] = records_of<EventRec>(events, "events");
     py::gil_scoped_release nogil;
-    return sim_.submit(*rb_.rb(), ev, n);
+    return sim_.submit(*rb_.rb(), ev, n, flush);
   }
-  py::array_t<uint32_t> encode(py::buffer events) {
+  uint64_t flush() {
+    py::gil_scoped_release nogil;
+    return sim_.flush(*rb_.rb());
+  }
+  py::array_t<uint32_t> encode(py::buffer events, bool flush) {
     auto [ev, n] = records_of<EventRec>(events, "events");
     std::vector<Rec16> out;
     {
       py::gil_scoped_release nogil;
-      sim_.encode(ev, n, out);
+      sim_.encode(ev, n, out, flush);
     }
     return rec16_array(out.data(), out.size());
   }
+  py::array_t<uint32_t> encode_flush() {
+    std::vector<Rec16> out;
+    sim_.encode_flush(out);
+    return rec16_array(out.data(), out.size());
+  }
+  uint64_t batches() const { return sim_.batches(); }
   void reset_maps() { sim_.reset_maps(); }
   size_t n_ctx() const { return sim_.n_ctx(); }
   size_t n_traces() const { return sim_.n_traces(); }
@@ -322,7 +334,8 @@ class PyProbeSim {
 
 py::array_t<uint8_t> frame_records_py(py::buffer recs) {
   auto [r, n] = records_of<Rec16>(recs, "records");
-  py::array_t<uint8_t> out((py::ssize_t)(n * kRecStride));
+  if (n % kBatchSlots) throw std::invalid_argument("frame_records: whole batches of 8 slots only");
+  py::array_t<uint8_t> out((py::ssize_t)(n / kBatchSlots * kRecStride));
   frame_records(r, n, out.mutable_data());
   return out;
 }
@@ -727,10 +740,14 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def("consume", &PyConsumer::consume, py::arg("out"), py::arg("cap"), py::arg("limit") = ~0ull)
       .def_property_readonly("threads", &PyConsumer::threads);
   py::class_<PyProbeSim>(m, "ProbeSim")
-      .def(py::init<PyRingbuf&, py::array_t<int8_t, py::array::c_style | py::array::forcecast>, size_t>(),
-           py::arg("ring"), py::arg("shift"), py::arg("trace_lru") = 1u << 20, py::keep_alive<1, 2>())
-      .def("submit", &PyProbeSim::submit)
-      .def("encode", &PyProbeSim::encode)
+      .def(py::init<PyRingbuf&, py::array_t<int8_t, py::array::c_style | py::array::forcecast>, size_t, uint32_t>(),
+           py::arg("ring"), py::arg("shift"), py::arg("trace_lru") = 1u << 20, py::arg("cpus") = 16,
+           py::keep_alive<1, 2>())
+      .def("submit", &PyProbeSim::submit, py::arg("events"), py::arg("flush") = true)
+      .def("flush", &PyProbeSim::flush)
+      .def("encode", &PyProbeSim::encode, py::arg("events"), py::arg("flush") = true)
+      .def("encode_flush", &PyProbeSim::encode_flush)
+      .def_property_readonly("batches", &PyProbeSim::batches)
       .def("reset_maps", &PyProbeSim::reset_maps)
       .def_property_readonly("n_ctx", &PyProbeSim::n_ctx)
       .def_property_readonly("n_traces", &PyProbeSim::n_traces)
@@ -814,7 +831,12 @@ PYBIND11_MODULE(_mislo_rt, m) {
         "fd of the first loaded BPF map of that name (and value size), or -errno");
   m.def("bpf_obj_get", &bpf_obj_get, py::arg("path"), "BPF_OBJ_GET of a pinned object; an fd or -errno");
   m.def("close_fd", &close_fd);
+  m.def("bpf_obj_get", [](const std::string& path) { return bpf_obj_get(path); }, py::arg("path"));
+  m.def("bpf_prog_run_on_cpu", &bpf_prog_run_on_cpu, py::arg("prog_fd"), py::arg("cpu"),
+        py::call_guard<py::gil_scoped_release>());
   m.attr("REC_STRIDE") = kRecStride;
+  m.attr("BATCH_SLOTS") = kBatchSlots;
+  m.attr("DEF_PAD") = kPad;
   m.attr("DEF_TRACE") = kDefTrace;
   m.attr("DEF_CTX") = kDefCtx;
   m.attr("KERNEL_CTX_LIMIT") = kKernelCtxLimit;

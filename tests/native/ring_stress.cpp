@@ -101,15 +101,19 @@ static int bpf_ring(int producers, int per_producer) {
   std::vector<std::thread> ps;
   for (int p = 0; p < producers; ++p)
     ps.emplace_back([&, p] {
-      for (int i = 0; i < per_producer; ++i) {
-        Rec16 rec{(uint32_t)i, (uint32_t)(p + 1), (uint32_t)(i * 3), 0};
-        if (i % 3 == 0) {
-          while (!rb->output(&rec, sizeof(rec))) std::this_thread::yield();
+      // batch records of kBatchSlots events: per_producer events per producer
+      for (int i = 0; i < per_producer; i += (int)kBatchSlots) {
+        Rec16 rec[kBatchSlots];
+        for (uint32_t j = 0; j < kBatchSlots; ++j)
+          rec[j] = Rec16{(uint32_t)(i + (int)j), (uint32_t)(p + 1), (uint32_t)((i + (int)j) * 3), 0};
+        const int b = i / (int)kBatchSlots;
+        if (b % 3 == 0) {
+          while (!rb->output(rec, sizeof(rec))) std::this_thread::yield();
         } else {
           void* s = nullptr;
           while (!(s = rb->reserve(sizeof(rec)))) std::this_thread::yield();
-          std::memcpy(s, &rec, sizeof(rec));
-          rb->commit(s, i % 7 == 0);  // some discarded
+          std::memcpy(s, rec, sizeof(rec));
+          rb->commit(s, b % 7 == 0);  // some discarded
         }
       }
       done.fetch_add(1);
@@ -128,15 +132,15 @@ static int bpf_ring(int producers, int per_producer) {
       last[p] = (int)out[i].ts_off;
     }
     events += st.events;
-    discarded += st.discarded;
+    discarded += st.discarded * kBatchSlots;
     if (!st.events && !st.discarded) std::this_thread::yield();
   }
   for (auto& t : ps) t.join();
   CHECK(events + discarded == (uint64_t)producers * per_producer);
   // pre-framed appends from a multi-threaded copy, read back by a parallel consumer
-  std::vector<Rec16> recs(2000);  // 48 KiB of a 64 KiB ring
+  std::vector<Rec16> recs(2000);  // 250 batch records: 34 KiB of a 64 KiB ring
   for (size_t i = 0; i < recs.size(); ++i) recs[i] = Rec16{(uint32_t)i, 9, (uint32_t)i * 3, 0};
-  std::vector<uint8_t> img(recs.size() * kRecStride);
+  std::vector<uint8_t> img(recs.size() / kBatchSlots * kRecStride);
   frame_records(recs.data(), recs.size(), img.data());
   CHECK(rb->append_framed(img.data(), img.size(), 4));
   RingbufConsumer par(rb.get(), 4);

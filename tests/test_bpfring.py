@@ -32,30 +32,38 @@ def payload16(k: int, i: int):
     return np.array([i, 7 | ((i % 50) << 8), i * 3, k], dtype=np.uint32)
 
 
+def batch(k: int, i: int):
+    """Batch record i's 8 event slots (slot j carries event 8 i + j)."""
+    return np.concatenate([payload16(k, 8 * i + j) for j in range(R.BATCH_SLOTS)])
+
+
+RS = R.REC_STRIDE
+
+
 def test_producer_writes_kernel_exact_framing():
     """reserve/commit/output lay records out exactly as kernel/bpf/ringbuf.c does: 8-byte
     header {len | busy, pg_off}, payload, 8-byte rounding; commit clears busy, discard sets it."""
     rb = shm("frame", 4 * PAGE)
-    a = rb.reserve(16)
-    rb.write(a, payload16(1, 0))
+    a = rb.reserve(R.REC_PAYLOAD)
+    rb.write(a, batch(1, 0))
     b = rb.reserve(5)                   # 5 bytes -> 16-byte record (8 + 5 rounded up)
     rb.write(b, np.frombuffer(b"hello", dtype=np.uint8))
-    c = rb.reserve(16)
+    c = rb.reserve(R.REC_PAYLOAD)
     data = rb.data_view()
     hdr = lambda off: data[off:off + 8].view(np.uint32)  # noqa: E731
-    assert tuple(hdr(0)) == (16 | R.RB_BUSY, 3)          # data page 3 of the kernel's rb struct
-    assert tuple(hdr(24)) == (5 | R.RB_BUSY, 3)
-    assert rb.producer_pos == 24 + 16 + 24
+    assert tuple(hdr(0)) == (R.REC_PAYLOAD | R.RB_BUSY, 3)  # data page 3 of the kernel's rb struct
+    assert tuple(hdr(RS)) == (5 | R.RB_BUSY, 3)
+    assert rb.producer_pos == RS + 16 + RS
     rb.commit(a)
     rb.commit(b, discard=True)
-    assert tuple(hdr(0)) == (16, 3)
-    assert tuple(hdr(24)) == (5 | R.RB_DISCARD, 3)
-    # numpy model of the same bytes (the record the test wrote) == the ring bytes
-    exp = R.frame(payload16(1, 0).view(R.EVENT16))
+    assert tuple(hdr(0)) == (R.REC_PAYLOAD, 3)
+    assert tuple(hdr(RS)) == (5 | R.RB_DISCARD, 3)
+    # numpy model of the same bytes (the batch the test wrote) == the ring bytes
+    exp = R.frame(batch(1, 0).view(R.EVENT16))
     exp[4:8] = np.array([3], dtype=np.uint32).view(np.uint8)
-    np.testing.assert_array_equal(data[:24], exp)
+    np.testing.assert_array_equal(data[:RS], exp)
     ev, defs, disc, busy = R.unframe(data[:rb.producer_pos])
-    assert len(ev) == 1 and disc == 1 and busy  # c is still being written
+    assert len(ev) == R.BATCH_SLOTS and disc == 1 and busy  # c is still being written
     rb.commit(c)
     assert not R.unframe(data[:rb.producer_pos])[3]
 
@@ -63,18 +71,18 @@ def test_producer_writes_kernel_exact_framing():
 def test_consumer_wraps_skips_discards_and_stops_at_busy():
     """Small ring, many laps: the consumer returns every committed 16-byte record once, in
     order, skips discards, never passes a busy record, and frees space as it goes."""
-    rb = shm("wrap", 4 * PAGE)                # 16 KiB: 682 records per lap
+    rb = shm("wrap", 4 * PAGE)                # 16 KiB: 120 batch records per lap
     con = rt.RingbufConsumer(rb, 4)
     out = np.zeros((4096, 4), dtype=np.uint32)
     rng = np.random.default_rng(3)
     expect, got, seq = [], [], 0
     pending = []
     for lap in range(12):
-        for _ in range(int(rng.integers(200, 600))):
-            at = rb.reserve(16)
+        for _ in range(int(rng.integers(30, 90))):
+            at = rb.reserve(R.REC_PAYLOAD)
             if at == 0:
                 break
-            p = payload16(lap, seq)
+            p = batch(lap, seq)
             seq += 1
             rb.write(at, p)
             pending.append((at, p, rng.random() < 0.05))
@@ -82,7 +90,7 @@ def test_consumer_wraps_skips_discards_and_stops_at_busy():
         for at, p, disc in pending[:len(pending) - keep]:
             rb.commit(at, disc)
             if not disc:
-                expect.append(tuple(p))
+                expect += [tuple(r) for r in p.reshape(-1, 4)]
         pending = pending[len(pending) - keep:]
         st, defs = con.consume(out, out.shape[0])
         got += [tuple(r) for r in out[:st["events"]]]
@@ -92,7 +100,7 @@ def test_consumer_wraps_skips_discards_and_stops_at_busy():
     for at, p, disc in pending:
         rb.commit(at, disc)
         if not disc:
-            expect.append(tuple(p))
+            expect += [tuple(r) for r in p.reshape(-1, 4)]
     st, _ = con.consume(out, out.shape[0])
     got += [tuple(r) for r in out[:st["events"]]]
     assert got == expect
@@ -103,9 +111,9 @@ def test_consumer_wraps_skips_discards_and_stops_at_busy():
 def test_full_ring_drops_like_the_kernel():
     rb = shm("full", 4 * PAGE)
     n = 0
-    while rb.output(payload16(0, n)):
+    while rb.output(batch(0, n)):
         n += 1
-    assert n == (4 * PAGE - 1) // 24  # producer may run at most size - 1 bytes ahead
+    assert n == (4 * PAGE - 1) // RS  # producer may run at most size - 1 bytes ahead
     assert rb.stats()["dropped"] == 1
 
 
@@ -121,8 +129,9 @@ def test_parallel_compaction_equals_serial_and_model():
     for threads in (1, 8):
         rb = shm(f"par{threads}", 1 << 20)
         assert rb.append_framed(img)
-        out = np.zeros((8000, 4), dtype=np.uint32)
-        st, defs = rt.RingbufConsumer(rb, threads).consume(out, 8000)
+        out = np.zeros((16000, 4), dtype=np.uint32)
+        st, defs = rt.RingbufConsumer(rb, threads).consume(out, 16000)
+        assert st["pads"] > 0
         assert not st["serial"]
         np.testing.assert_array_equal(out[:st["events"]].view(R.EVENT16).reshape(-1), ev_ref)
         np.testing.assert_array_equal(defs.view(R.EVENT16).reshape(-1), defs_ref)
@@ -131,28 +140,29 @@ def test_parallel_compaction_equals_serial_and_model():
 def test_foreign_record_size_takes_the_serial_walk():
     rb = shm("foreign", 1 << 16)
     for i in range(100):
-        assert rb.output(payload16(0, i))
+        assert rb.output(batch(0, i))
     assert rb.output(np.zeros(32, dtype=np.uint8))  # another program's 32-byte record
     for i in range(100, 150):
-        assert rb.output(payload16(0, i))
-    out = np.zeros((512, 4), dtype=np.uint32)
-    st, _ = rt.RingbufConsumer(rb, 8).consume(out, 512)
-    assert st["serial"] and st["foreign"] == 1 and st["events"] == 150
-    assert out[149, 0] == 149
+        assert rb.output(batch(0, i))
+    out = np.zeros((2048, 4), dtype=np.uint32)
+    st, _ = rt.RingbufConsumer(rb, 8).consume(out, 2048)
+    assert st["serial"] and st["foreign"] == 1 and st["events"] == 1200
+    assert out[1199, 0] == 1199
 
 
 def test_window_capacity_and_limit_leave_the_rest_queued():
+    """Whole batches only: a window of 100 rows takes 12 batch records (96 events)."""
     rb = shm("cap", 1 << 16)
-    for i in range(300):
-        rb.output(payload16(0, i))
+    for i in range(40):
+        rb.output(batch(0, i))
     out = np.zeros((1000, 4), dtype=np.uint32)
     con = rt.RingbufConsumer(rb, 4)
     st, _ = con.consume(out, 100)                        # window capacity
-    assert st["events"] == 100 and st["end_pos"] == 100 * 24
-    st, _ = con.consume(out, 1000, limit=150 * 24)       # window cut
-    assert st["events"] == 50 and out[0, 0] == 100
+    assert st["events"] == 96 and st["end_pos"] == 12 * RS
+    st, _ = con.consume(out, 1000, limit=20 * RS)        # window cut
+    assert st["events"] == 64 and out[0, 0] == 96
     st, _ = con.consume(out, 1000)
-    assert st["events"] == 150 and out[149, 0] == 299
+    assert st["events"] == 160 and out[159, 0] == 319
 
 
 def test_native_probe_model_matches_numpy_model_and_floors():
@@ -182,8 +192,8 @@ def test_probe_submit_through_ring_equals_encode():
     n = a.producer_pos
     data = a.data_view()[:n].copy()
     # pg_off differs by position; everything else is byte-identical
-    hdr = data.view(np.uint32).reshape(-1, 6)
-    assert (hdr[:, 1] == 3 + (np.arange(hdr.shape[0]) * 24) // PAGE).all()
+    hdr = data.view(np.uint32).reshape(-1, RS // 4)
+    assert (hdr[:, 1] == 3 + (np.arange(hdr.shape[0]) * RS) // PAGE).all()
     hdr[:, 1] = 0
     np.testing.assert_array_equal(data, img)
 
@@ -193,7 +203,7 @@ def test_epoch_tags_decode_records_written_across_cuts():
     w = window(seed=11, n=2000)
     clock = R.EpochClock()
     cfg = np.zeros(128, dtype=np.uint64)
-    model = R.ProbeModel(cfg)
+    model = R.ProbeModel(cfg, cpus=1)  # one CPU: the slots keep the input order
     ev = w.events.copy()
     ev = ev[np.argsort(ev["ts_ns"])]
     cuts = [int(ev["ts_ns"][0]) + j * 200_000_000 for j in range(5)]
@@ -258,7 +268,7 @@ def test_event16_path_preserves_the_join_of_the_64_byte_originals():
     cfg = np.zeros(128, dtype=np.uint64)
     clock = R.EpochClock()
     cfg[124] = clock.publish(int(w.events["ts_ns"].min()) - 10)
-    enc = R.ProbeModel(cfg).encode(w.events[km])
+    enc = R.ProbeModel(cfg, cpus=1).encode(w.events[km])  # one CPU: row order = event order
     tab = R.HostEncoderModel()
     for p, sn in zip(w.events["pod_id"], (w.events["svc_id"].astype(np.uint32) << 16) | w.events["node_id"]):
         tab.set_pod(int(p), int(sn))
@@ -327,9 +337,9 @@ def test_assembler_fills_the_slot_layout():
 def _producer(name: str, k: int, n: int) -> None:
     r = load().Ringbuf.attach_shm(name)
     i = 0
-    while i < n:
-        if r.output(np.array([i, 7, k, 0xC0FFEE], dtype=np.uint32)):
-            i += 1
+    while i < n:  # batch records of 8 events
+        if r.output(np.array([[i + j, 7, k, 0xC0FFEE] for j in range(8)], dtype=np.uint32)):
+            i += 8
 
 
 def test_multiprocess_producers_exactly_once():

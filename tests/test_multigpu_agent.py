@@ -318,15 +318,62 @@ if __name__ == "__main__":
     assert state["windows"] == 5 and state["burn"]["hist"]
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("split", [False, True])
+def test_agent_survives_a_worker_killed_mid_run(tmp_path, split):
+    """`agent --engine cpu --gpus 3 --source replay`: one of the three worker processes is
+    SIGKILLed after a few windows. The controller notices (the survivors may be blocked in a
+    collective with it), stops them, starts fresh workers for the 2 surviving GPUs with a new
+    communicator, and keeps emitting schema-valid attributions for every service."""
+    code = f"""
+import io, json, os, signal, sys, threading, time
+sys.path.insert(0, {ROOT!r})
+from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+from llm_slo_ebpf_toolkit_amd.contracts import validator
+if __name__ == "__main__":
+    out = io.StringIO()
+    o = AgentOptions(engine="cpu", source="replay", gpus=3, window_events=4096, window_spans=256, window_groups=8,
+                     window_ms=400, metrics_bind="", output="stdout", ring_name="/mislo-kill-%d" % os.getpid(),
+                     config="", min_confidence=0.0, split_rings={split!r})
+    a = Agent(o, out_stream=out)
+    killed = {{}}
+
+    def killer():
+        while a.windows_done < 3:
+            time.sleep(0.05)
+        victim = a.pool.workers[1].pid
+        killed["pid"], killed["at"] = victim, a.windows_done
+        os.kill(victim, signal.SIGKILL)
+
+    threading.Thread(target=killer, daemon=True).start()
+    rc = a.run_windows(max_windows=10)
+    recs = [json.loads(x) for x in out.getvalue().splitlines()]
+    schema = validator.compiled("incident-attribution")
+    assert all(schema.is_valid(r) for r in recs), recs[:1]
+    after = [r for r in recs if int(r["incident_id"].split("-")[1]) > 0]
+    print(json.dumps({{"rc": rc, "n": len(recs), "services": sorted({{r["service"] for r in recs}}),
+                      "windows": a.windows_done, "workers": len(a.pool.workers), "killed": killed,
+                      "restarts": a.metrics.worker_restarts.value(), "gauge": a.metrics.workers.value()}}))
+    a.close()
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["killed"] and d["killed"]["at"] >= 3
+    assert d["rc"] == 0 and d["restarts"] == 1 and d["workers"] == 2 and d["gauge"] == 2
+    assert d["windows"] == 10 and d["n"] > 0 and len(d["services"]) >= 4
+    assert "restarting on 2 worker(s)" in p.stderr
+
+
 def test_windows_that_wrap_the_bpf_ring_equal_unwrapped_windows():
     """Only the first mapping of the double-mapped BPF ring is page-locked: a window that wraps
     goes as two DMA segments placed back to back, records split by the wrap included, and the
     results equal those of the same windows in a ring that never wraps."""
-    wins, imgs, pods = _windows()
+    wins, imgs, pods = _windows(n_win=5)
     tag = f"/mislo-wr-{os.getpid()}"
     big = _run_pool(1, imgs, pods, tag + "-a")
-    small = _run_pool(1, imgs, pods, tag + "-b", ring_bytes=1 << 17)  # the third window wraps
-    assert sum(im.framed.size for im in imgs) > (1 << 17)
+    small = _run_pool(1, imgs, pods, tag + "-b", ring_bytes=1 << 18)  # a later window wraps
+    assert sum(im.framed.size for im in imgs) > (1 << 18)
     for j, (a, b) in enumerate(zip(big, small)):
         np.testing.assert_array_equal(a["packet"], b["packet"], err_msg=f"window {j}")
         for key in ("feat", "pred", "sli", "evbits"):

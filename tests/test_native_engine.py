@@ -61,7 +61,7 @@ def test_ring_windows_match_oracle(user_rec):
 
     wins, gen = windows()
     imgs = build_replay_images(wins, user_rec=user_rec)
-    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096)
+    pipe = WindowPipeline(16384, 512, 8, model="bayes", learn=False, user_cap=4096)
     rb, user, spans = rings(f"oracle{user_rec}", user_rec)
     src = RingWindowSource(pipe, rb, user, spans)
     assert all(src.direct.values())  # the rings are page-locked: DMA straight from them
@@ -74,7 +74,7 @@ def test_ring_windows_match_oracle(user_rec):
         cut = feed(img, rb, user, spans)
         r = src.stage(cut, w.n_groups, img.labels)
         k = r["k"]
-        assert r["n_kernel"] * 24 == len(img.framed) and r["n_user"] == len(img.user)
+        assert r["n_kernel"] == R.framed_rows(img.framed) and r["n_user"] == len(img.user)
         oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
         d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases, pod_sn=pod_sn)
         ref = oracle.join(d, oracle.spans_native(img.spans, tmap), w.n_groups)
@@ -83,9 +83,7 @@ def test_ring_windows_match_oracle(user_rec):
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d))
         np.testing.assert_array_equal(pk["misc"][2:18].astype(np.int64), oracle.value_sums_milli(d))
         assert pk["ring_state"]["first_busy"] == -1
-        fr = img.framed.view(np.uint32).reshape(-1, 6)
-        n_ev = int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
-        assert pk["ring_state"]["events"] == n_ev
+        assert pk["ring_state"]["events"] == R.framed_event_count(img.framed) + len(img.user)
         dbg = dict(zip(("candidates", "low_raw", "overlap", "fanout_dropped", "spans_enriched"),
                        pk["dbg"][:5].astype(np.int64).tolist()))
         for key in ("candidates", "fanout_dropped", "spans_enriched"):
@@ -114,8 +112,8 @@ def test_ring_windows_match_oracle(user_rec):
 
 
 def test_busy_record_is_resubmitted_exactly_once():
-    """A record still being written at the cut (busy bit) stops the GPU's decode of that window
-    there; the rest of the range is re-submitted with the next window and counted once."""
+    """A batch record still being written at the cut (busy bit) stops the GPU's decode of that
+    window there; the rest of the range is re-submitted with the next window and counted once."""
     from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, RingWindowSource, WindowPipeline
 
     rb, user, spans = rings("busy")
@@ -130,21 +128,21 @@ def test_busy_record_is_resubmitted_exactly_once():
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     sim = load().ProbeSim(rb, R.milli_shift_table())
-    sim.submit(ev[:100])
-    at = rb.reserve(16)            # a probe still writing record 100
-    sim.submit(ev[101:200])
+    sim.submit(ev[:96])            # 12 full batch records (all on CPU 0)
+    at = rb.reserve(R.REC_PAYLOAD)  # a CPU still writing batch 12 (events 96..103)
+    sim.submit(ev[104:200])        # 12 more batches
     k0 = src.stage(Cut(kernel=rb.producer_pos, user=0, spans=0, bases=(base, 0, 0, 0)), 4)["k"]
     src.reap(keep=0)
-    assert pipe.packet(k0)["ring_state"]["first_busy"] == 100
-    assert pipe.packet(k0)["hist"].sum() == 100
-    assert rb.consumer_pos == 100 * 24 and src.resubmitted == 100
-    rb.write(at, sim.encode(ev[100:101]).reshape(-1))
+    assert pipe.packet(k0)["ring_state"]["first_busy"] == 96  # the busy batch's first row
+    assert pipe.packet(k0)["hist"].sum() == 96
+    assert rb.consumer_pos == 12 * R.REC_STRIDE and src.resubmitted == 13 * R.BATCH_SLOTS
+    rb.write(at, sim.encode(ev[96:104]).reshape(-1))
     rb.commit(at)
     sim.submit(ev[200:300])
     k1 = src.stage(Cut(kernel=rb.producer_pos, user=0, spans=0, bases=(base, 0, 0, 0)), 4)["k"]
     src.drain()
     assert pipe.packet(k1)["ring_state"]["first_busy"] == -1
-    assert pipe.packet(k1)["hist"].sum() == 200  # the 100 re-submitted + 100 new, each once
+    assert pipe.packet(k1)["hist"].sum() == 204  # the 104 re-submitted + 100 new, each once
     tot = pipe.summary()["hist"].sum()
     assert tot == 300
     assert rb.consumer_pos == rb.producer_pos
@@ -159,7 +157,7 @@ def test_pipelined_learning_with_graphs_and_device_refit():
     imgs = build_replay_images(wins)
     sums = []
     for graphs in (False, True):
-        pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", use_graphs=graphs, user_cap=4096)
+        pipe = WindowPipeline(16384, 512, 8, model="bayes_learned", use_graphs=graphs, user_cap=4096)
         rb, user, spans = rings(f"learn{graphs}")
         src = RingWindowSource(pipe, rb, user, spans)
         pipe.eng.set_pods(*pod_meta(gen))
@@ -192,7 +190,7 @@ def test_halo_and_remote_rows_join_like_the_oracle():
     wins, gen = windows(n_win=3, seed=43)
     imgs = build_replay_images(wins)
     halo_ms, icap = 2000.0, 16384
-    pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096, halo_ms=halo_ms, import_cap=icap,
+    pipe = WindowPipeline(16384, 512, 8, model="bayes", learn=False, user_cap=4096, halo_ms=halo_ms, import_cap=icap,
                           xchg_cap=64)
     rb, user, spans = rings("halo")
     src = RingWindowSource(pipe, rb, user, spans)
@@ -224,8 +222,7 @@ def test_halo_and_remote_rows_join_like_the_oracle():
         pk = pipe.packet(k)
         res = pipe.results(k, w.n_groups)
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d_loc))  # imports never count
-        fr = img.framed.view(np.uint32).reshape(-1, 6)
-        assert pk["ring_state"]["events"] == int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
+        assert pk["ring_state"]["events"] == R.framed_event_count(img.framed) + len(img.user)
         dbg = pk["dbg"][:5].astype(np.int64).tolist()
         # rows[0..1], tmax, gens, cur, filled, cut[4], rows per age[4], remote per buffer
         st = pipe.eng.import_state()
@@ -256,7 +253,7 @@ def test_checkpoint_resume_restores_every_finished_window(tmp_path):
     pods = pod_meta(gen)
 
     def make(tag):
-        pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", user_cap=4096)
+        pipe = WindowPipeline(16384, 512, 8, model="bayes_learned", user_cap=4096)
         rb, user, spans = rings(tag)
         src = RingWindowSource(pipe, rb, user, spans)
         pipe.eng.set_pods(*pods)
@@ -303,7 +300,7 @@ def test_group_sharding_on_device_matches_the_whole_stream():
     out = {}
     for shard in ((0, 1), (0, 2), (1, 2)):
         G = len(range(shard[0], 8, shard[1]))
-        pipe = WindowPipeline(8192, 512, 8, model="bayes", learn=False, user_cap=4096, shard=shard, halo_ms=2000.0,
+        pipe = WindowPipeline(16384, 512, 8, model="bayes", learn=False, user_cap=4096, shard=shard, halo_ms=2000.0,
                               import_cap=8192)
         rb, user, spans = rings(f"shard{shard[0]}{shard[1]}", 24)
         src = RingWindowSource(pipe, rb, user, spans)
@@ -337,7 +334,7 @@ def test_soft_label_statistics_temperature_refit_and_scoring():
 
     wins, gen = windows(n_win=3, seed=59)
     imgs = build_replay_images(wins)
-    pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", user_cap=4096)
+    pipe = WindowPipeline(16384, 512, 8, model="bayes_learned", user_cap=4096)
     rb, user, spans = rings("softlab")
     src = RingWindowSource(pipe, rb, user, spans)
     pipe.eng.set_pods(*pod_meta(gen))
@@ -386,7 +383,7 @@ def test_two_fault_refit_and_marginals_match_the_host_model():
 
     wins, gen = windows(n_win=3, seed=61)
     imgs = build_replay_images(wins)
-    pipe = WindowPipeline(8192, 512, 8, model="bayes_learned", user_cap=4096)
+    pipe = WindowPipeline(16384, 512, 8, model="bayes_learned", user_cap=4096)
     rb, user, spans = rings("pairs")
     src = RingWindowSource(pipe, rb, user, spans)
     pipe.eng.set_pods(*pod_meta(gen))
@@ -460,7 +457,7 @@ def test_headline_shape_windows_match_the_oracle():
     for j, (w, img) in enumerate(zip(wins, imgs)):
         r = src.stage(feed(img, rb, user, spans), w.n_groups, img.labels)
         k = r["k"]
-        assert r["n_kernel"] * 24 == len(img.framed) and r["n_user"] == len(img.user)
+        assert r["n_kernel"] == R.framed_rows(img.framed) and r["n_user"] == len(img.user)
         pk = pipe.packet(k)
         res = pipe.results(k, w.n_groups)
         t1 = time.time()
@@ -471,8 +468,7 @@ def test_headline_shape_windows_match_the_oracle():
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d))
         np.testing.assert_array_equal(pk["misc"][2:18].astype(np.int64), oracle.value_sums_milli(d))
         assert pk["ring_state"]["first_busy"] == -1
-        fr = img.framed.view(np.uint32).reshape(-1, 6)
-        assert pk["ring_state"]["events"] == int(((fr[:, 0] == 16) & ((fr[:, 3] & 0xFF) < 0xF0)).sum()) + len(img.user)
+        assert pk["ring_state"]["events"] == R.framed_event_count(img.framed) + len(img.user)
         dbg = dict(zip(("candidates", "low_raw", "overlap", "fanout_dropped", "spans_enriched"),
                        pk["dbg"][:5].astype(np.int64).tolist()))
         for key in ("candidates", "fanout_dropped", "spans_enriched"):

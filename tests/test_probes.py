@@ -154,14 +154,15 @@ def test_probe_c_full_ring_matches_probesim(probe_host, tmp_path):
     rt = load()
     rb = rt.Ringbuf.create_shm(f"/mislo-phf-{os.getpid()}", 1 << 12)
     rb.cfg_set(124, epoch)
-    cap = rb.size // 24
+    RS = records.REC_STRIDE
+    cap = rb.size // RS  # batch records
     got, stats = _run_host(probe_host, tmp_path, ev, "--epoch-at", f"0:{epoch}", "--ring-cap", cap)
     sim = rt.ProbeSim(rb, records.milli_shift_table(), 1 << 20)
     sim.submit(ev)
-    n = rb.producer_pos // 24
-    assert n == cap == len(got) and sim.dropped > 0
-    ring = rb.data_view()[: n * 24].view(np.uint32).reshape(-1, 6)
-    np.testing.assert_array_equal(ring[:, 2:], got)
+    n = rb.producer_pos // RS
+    assert n == cap == len(got) // records.BATCH_SLOTS and sim.dropped > 0
+    ring = rb.data_view()[: n * RS].view(np.uint32).reshape(-1, RS // 4)
+    np.testing.assert_array_equal(ring[:, 2:].reshape(-1, 4), got)
     assert stats["trace_next"] == rb.cfg_get(125) and stats["ctx_next"] == rb.cfg_get(126)
 
 
@@ -196,6 +197,8 @@ def _resolve(rows):
             ctx[tag_id >> 8] = (b, c, a)
         elif t == 0xFD:
             tr[a] = b | (c << 32)
+        elif t == 0xFC:  # a pad: the unused slot of a batch flushed before it filled
+            continue
         else:
             pod, pid, c32 = ctx.get(tag_id >> 8, (0, 0, 0))
             tid = c & ((1 << 30) - 1)

@@ -1,5 +1,5 @@
 """Record layouts: REF 40-byte records, 64-byte EVENT/SPAN, the 16-byte EVENT16 the BPF ring
-carries (framed as 24-byte ring records), SPAN20; the integer fixed-point rule and the epoch
+carries (8 to a 136-byte ring record), SPAN20; the integer fixed-point rule and the epoch
 protocol (the ring path itself: tests/test_bpfring.py)."""
 
 import pytest
@@ -14,7 +14,7 @@ def test_layout_sizes():
     assert records.SPAN.itemsize == 64
     assert records.SPAN20.itemsize == 20
     assert records.REF_EVENT.itemsize == 40
-    assert records.REC_STRIDE == 24
+    assert records.REC_STRIDE == 136 and records.BATCH_SLOTS == 8  # 8-slot batch records
     assert records.WIRE_DTYPES == {64: records.EVENT, 16: records.EVENT16}
 
 

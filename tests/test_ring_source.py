@@ -29,7 +29,7 @@ def test_late_records_past_three_cuts_are_dropped_not_mis_stamped():
     ev["ts_ns"] = base + np.arange(300) * 1000
     sim = rt.ProbeSim(rb, R.milli_shift_table())
     sim.submit(ev[:100])
-    rb.reserve(16)                 # a probe that never finishes record 100
+    rb.reserve(R.REC_PAYLOAD)      # a CPU's batch that is never finished (after 13 batches: 100 events)
     sim.submit(ev[101:200])
     hist = []
     for _ in range(5):
@@ -37,8 +37,9 @@ def test_late_records_past_three_cuts_are_dropped_not_mis_stamped():
         src.reap(keep=0)
         hist.append(int(pipe.packet(k)["hist"].sum()))
     src.drain()
-    # window 0 decodes the 100 records ahead of the busy one; windows 1 and 2 re-submit the tail
-    # (and stop at the busy record again); window 3 would decode it 3 cuts late: dropped
+    # window 0 decodes the 100 events ahead of the busy batch; windows 1 and 2 re-submit the tail
+    # (and stop at the busy batch again); window 3 would decode it 3 cuts late: dropped -- the
+    # busy batch and the 13 batches behind it (99 events + 5 pads), in rows
     assert hist == [100, 0, 0, 0, 0], hist
-    assert src.late_dropped == 100 and not src.late
+    assert src.late_dropped == R.BATCH_SLOTS * (1 + 13) and not src.late
     assert rb.consumer_pos == rb.producer_pos

@@ -92,5 +92,7 @@ def test_forced_over_budget_raises_floors_and_the_next_windows_carry_fewer_event
     a.close()
     assert rc == 0 and len(seen) >= 6, seen
     assert a.ladder.shed and a.ladder.shed[0].startswith("floors:")
-    before, after = seen[0], np.mean(seen[-3:])
+    # (the first window may be partial: the producer's staged batches of the window it was cut
+    # in flush at the producer's own window end, into the agent's next window)
+    before, after = max(seen[:2]), np.mean(seen[-3:])
     assert after < 0.6 * before, seen

@@ -26,6 +26,7 @@ def main() -> int:
     a = ap.parse_args()
     import numpy as np
 
+    from llm_slo_ebpf_toolkit_amd.collector.records import framed_rows
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
     from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, RingWindowSource, WindowPipeline, build_replay_images
     from llm_slo_ebpf_toolkit_amd.runtime import load
@@ -38,7 +39,7 @@ def main() -> int:
     rb = rt.Ringbuf.create_shm(tag, 1 << 28)
     user = rt.HostRing(1 << int(np.ceil(np.log2(n_user * 4))), 64)
     spans = rt.HostRing(1 << int(np.ceil(np.log2(a.spans * 4))), 64)
-    budget = max(len(i.framed) // 24 + len(i.user) for i in imgs)  # framed (events + definitions) + user
+    budget = max(framed_rows(i.framed) + len(i.user) for i in imgs)  # framed (events + definitions) + user
     pipe = WindowPipeline(budget, a.spans, a.services, 0, None, model="bayes_learned",
                           use_graphs=not a.no_graphs, user_cap=1 << int(np.ceil(np.log2(n_user))))
     pipe.eng.set_pods(gen.pod_ids.astype(np.uint32),

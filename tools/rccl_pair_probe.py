@@ -39,6 +39,7 @@ def rank_main(rank, world, uq, n_win, q):
         else:
             uid = uq.get(timeout=120)
 
+        from llm_slo_ebpf_toolkit_amd.collector.records import framed_rows
         from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
         from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, RingWindowSource, WindowPipeline, build_replay_images
         from llm_slo_ebpf_toolkit_amd.runtime import load
@@ -48,7 +49,7 @@ def rank_main(rank, world, uq, n_win, q):
         gen = ReplayGenerator(cfg)
         wins = [gen.next_window() for _ in range(n_win)]
         imgs = build_replay_images(wins, user_rec=24)
-        sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs)
+        sig_cap = max(framed_rows(i.framed) + len(i.user) for i in imgs)
         user_cap = 1 << int(np.ceil(np.log2(max(len(i.user) for i in imgs))))
         xchg = 4096
         import torch
