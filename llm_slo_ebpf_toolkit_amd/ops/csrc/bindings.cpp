@@ -224,6 +224,9 @@ class Engine {
                      dptr<uint32_t>(s_part_blk), dptr<uint32_t>(s_part_off), dptr<uint32_t>(s_part_tot),
                      dptr<uint32_t>(s_part_base), dptr<uint32_t>(s_items), st);
     // top3 / cnt / gsum / gcnt were reset by reset_window()
+    launch_span_sort(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base),
+                     reinterpret_cast<PreSpan*>(s_pre.data_ptr()), st);
+    launch_probe_work(dptr<uint32_t>(s_part_base), sig_cols(), jp_, dptr<uint32_t>(probe_work), st);
     launch_probe(span_cols(), dptr<uint32_t>(s_items), dptr<uint32_t>(s_part_base), sig_cols(), span_cap_, jp_,
                  dptr<unsigned long long>(top3), dptr<uint32_t>(cnt), (int)n_groups, dptr<unsigned long long>(gsum),
                  dptr<uint32_t>(gcnt), dptr<unsigned long long>(dbg), dptr<uint32_t>(probe_work),

@@ -187,6 +187,10 @@ class WindowEngine {
   void alloc();
   void run_part1(int b, hipStream_t st, bool xchg);
   void run_part2(int b, int n_groups, bool with_labels, bool learn, hipStream_t st, bool xchg);
+  // the window's span side (decode, partition, probe work list, span sort) on side_, forked
+  // from `st` after the accumulators are reset and joined before the probe (one-GPU chain)
+  void run_span_branch(int b, hipStream_t st);
+  void run_spans(int b, hipStream_t st);
   void launch_part(int part, int b, int n_groups, bool with_labels, bool learn, bool xchg);
   SignalCols sig_cols() const;
   SpanCols span_cols() const;
@@ -223,6 +227,14 @@ class WindowEngine {
   int rank_ = 0, world_ = 1;
   std::vector<uint8_t*> res_all_dev_, res_all_host_;
   std::vector<hipEvent_t> xchg_done_;
+  // span branch: a second compute stream, overlapping the span side of the chain (~50 us of
+  // small kernels, plus the one-workgroup probe work list) with the signal side's decode and
+  // scatter; with one hardware queue (the agent's GPU_MAX_HW_QUEUES=1) it simply serialises.
+  // Opt-in (MISLO_SPAN_STREAM=1): at the default stream priority the branch shortened the chain
+  // by 40 us but delayed the next window's DMA by as much (profiles/r4_span_branch.md).
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_sigbase_ = nullptr, ev_spans_ = nullptr;
+  bool branch_ = false;
   bool exchange() const { return comm_ && cfg_.xchg_cap > 0 && cfg_.import_cap > 0; }
   JoinParams jp_{};
   int nblk_sig_ = 1, nblk_span_ = 1;

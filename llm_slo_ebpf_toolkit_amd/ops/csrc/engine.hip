@@ -155,6 +155,24 @@ void WindowEngine::alloc() {
     else copy2_ = copy_;
   }
   HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  {
+    const char* v = getenv("MISLO_SPAN_STREAM");
+    branch_ = v && atoi(v) == 1;
+    if (branch_) {
+      // its own priority: streams of one priority share that priority's hardware queues, and a
+      // side stream landing on the copy stream's queue held the next window's DMA behind the
+      // branch's kernels (measured: copy 0.434 -> 0.477 ms per window at the default priority)
+      int lo = 0, hi = 0;
+      HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      const char* pv = getenv("MISLO_SPAN_STREAM_PRIO");  // 0 = the default priority
+      if (pv && atoi(pv) == 0)
+        HIPCHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+      else
+        HIPCHECK(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
+      for (hipEvent_t* e : {&ev_fork_, &ev_sigbase_, &ev_spans_})
+        HIPCHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+  }
   // one GPU: the window's tail (packet accumulate, timing) runs on the compute stream; a comm
   // stream of its own exists only with a communicator (init_comm). Every stream backs a
   // hardware queue, and each MI355X queue pins ~173 MB of host memory (its context save area,
@@ -322,6 +340,9 @@ WindowEngine::~WindowEngine() {
   if (copy_) hipStreamDestroy(copy_);
   if (copy2_ && copy2_ != copy_) hipStreamDestroy(copy2_);
   if (compute_) hipStreamDestroy(compute_);
+  if (side_) hipStreamDestroy(side_);
+  for (hipEvent_t e : {ev_fork_, ev_sigbase_, ev_spans_})
+    if (e) hipEventDestroy(e);
   if (comm_stream_ && comm_stream_ != compute_) hipStreamDestroy(comm_stream_);
 }
 
@@ -424,6 +445,7 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   // its reset), the ring state, no other GPUs' rows until merged, the window's rows
   launch_window_begin(fl, gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), ring_state_, remote_n_ + b,
                       counts, N, rows_, st);
+  if (branch_ && !xchg) run_span_branch(b, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
@@ -447,15 +469,23 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
                          ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st,
                          1, nblk_imp_, nblk_sig_, rec_shard_rank(), rec_shard_world());
   }
+  const bool branched = branch_ && !xchg;
+  // with the span branch: the signal bases are what the branch's probe work list waits for
+  hipEvent_t sig_base = branched ? ev_sigbase_ : nullptr;
   if (xchg)
     launch_partition_sig(sig_cols(), rows_, N, nblk_sig_ + nblk_imp_, g_part_blk_, g_part_off_, g_part_tot_, st,
-                         nblk_sig_);
+                         nblk_sig_, sig_base);
   else
-    launch_partition_sig(sig_cols(), rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, st);
-  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_};
-  launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
-  launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
-                   st);
+    launch_partition_sig(sig_cols(), rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, st, 0, sig_base);
+  if (branched) {  // the work list needs the signal bases just recorded; then join
+    HIPCHECK(hipStreamWaitEvent(side_, ev_sigbase_, 0));
+    launch_probe_work(s_part_base_, sig_cols(), jp_, probe_work_, side_);
+    HIPCHECK(hipEventRecord(ev_spans_, side_));
+    HIPCHECK(hipStreamWaitEvent(st, ev_spans_, 0));  // spans sorted, work list built
+  } else {
+    run_spans(b, st);
+    launch_probe_work(s_part_base_, sig_cols(), jp_, probe_work_, st);
+  }
   launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), S, jp_, top3_, cnt_, n_groups, gsum_, gcnt_, dbg_,
                probe_work_, s_pre_, st);
   launch_finalize(counts + 1, S, top3_, cnt_, sig_cols(), span_cols(), jp_, nullptr, attrs_, conf_, kernel_ms_,
@@ -477,6 +507,29 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   }
   hipLaunchKernelGGL(k_pack, dim3((kPacketLen + 255) / 256), dim3(256), 0, st, hist_, status_, misc_, dbg_, confusion_,
                      stats_, stats_count_, ring_state_, packet_dev_[b]);
+}
+
+// The span side of the chain: decode, partition, span sort (inputs: the span DMA and the reset
+// accumulators only).
+void WindowEngine::run_spans(int b, hipStream_t st) {
+  uint8_t* in = in_dev_[b];
+  const int* counts = reinterpret_cast<const int*>(in);
+  const int S = cfg_.span_cap, G = cfg_.group_cap;
+  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_};
+  launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
+  launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
+                   st);
+  launch_span_sort(span_cols(), s_items_, s_part_base_, s_pre_, st);
+}
+
+// Fork from `st` (after k_window_begin): the span side on side_. run_part2 continues the branch
+// once the signal side's partition bases exist -- the probe work list reads both sides' bases
+// and time ranges -- and joins it before the probe (ev_spans_). Native 64-byte spans never read
+// the context table, so the branch does not wait for k_ring_defs.
+void WindowEngine::run_span_branch(int b, hipStream_t st) {
+  HIPCHECK(hipEventRecord(ev_fork_, st));
+  HIPCHECK(hipStreamWaitEvent(side_, ev_fork_, 0));
+  run_spans(b, side_);
 }
 
 // Launch a chain part eagerly, or through its captured graph (captured on the buffer's second

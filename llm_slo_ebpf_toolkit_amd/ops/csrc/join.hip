@@ -1111,10 +1111,11 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 // ---------------------------------------------------------------------------------------
 
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
-                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a) {
+                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a, hipEvent_t bases_done) {
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
                      part_blk, nblk, part_off, part_tot);
   hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, gc.base, gc.gen);
+  if (bases_done) (void)hipEventRecord(bases_done, stream);  // the span branch's probe work list may start
   hipLaunchKernelGGL((k_scatter_sig<1024>), dim3(nblk), dim3(1024), 0, stream, gc, n_dev, cap, part_off,
                      nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk);
 }
@@ -1149,12 +1150,26 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
     const int x = v ? atoi(v) : kSigPerItem;
     return x >= 1 ? x : kSigPerItem;
   }();
-  hipLaunchKernelGGL((k_span_sort<kChunk>), dim3(kKeyTypes * kParts), dim3(kChunk), 0, stream, sc, span_items,
-                     span_base, span_pre);
-  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, per_item, work);
+  (void)sc, (void)span_items, (void)per_item;
   for (int phase = 0; phase < 2; ++phase)
     hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, span_pre, span_base, gc, span_cap, jp, top3,
                        cnt, n_groups, gsum, gcnt, dbg, work, phase);
+}
+
+void launch_span_sort(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, PreSpan* span_pre,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL((k_span_sort<kChunk>), dim3(kKeyTypes * kParts), dim3(kChunk), 0, stream, sc, span_items,
+                     span_base, span_pre);
+}
+
+void launch_probe_work(const uint32_t* span_base, const SignalCols& gc, const JoinParams& jp, uint32_t* work,
+                       hipStream_t stream) {
+  static const int per_item = [] {  // MISLO_PROBE_ITEM: signals per work item (diagnostic)
+    const char* v = getenv("MISLO_PROBE_ITEM");
+    const int x = v ? atoi(v) : kSigPerItem;
+    return x >= 1 ? x : kSigPerItem;
+  }();
+  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, per_item, work);
 }
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,

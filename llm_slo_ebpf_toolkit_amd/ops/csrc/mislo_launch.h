@@ -105,8 +105,10 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream, int nblk_a = 0);
 // signals: the current generation's lists (gc.items / gc.keys / gc.base) from gc.part and gc.rec
+// (bases_done: recorded after the partition bases, before the scatter -- the span branch's cue)
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
-                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a = 0);
+                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a = 0,
+                          hipEvent_t bases_done = nullptr);
 // A span at its position in a (key type, partition) list, the list sorted by (key hash, ts) in
 // chunks of the probe's staging size: what the probe stages, written once per window
 // (k_span_sort). run = the position's hash-run id in its chunk | run uniform << 16.
@@ -121,10 +123,17 @@ struct alignas(64) PreSpan {
 static_assert(sizeof(PreSpan) == 64, "one cache line per staged span");
 // spans of this window x every visible generation's signals; span_pre: kKeyTypes * span_cap
 // PreSpan of scratch
+// (after launch_span_sort and launch_probe_work)
 void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, const SignalCols& gc,
                   int span_cap, const JoinParams& jp, unsigned long long* top3, uint32_t* cnt, int n_groups,
                   unsigned long long* gsum, uint32_t* gcnt, unsigned long long* dbg, uint32_t* work,
                   PreSpan* span_pre, hipStream_t stream);
+// every (key type, partition) span list sorted by (key hash, ts) into span_pre (k_span_sort)
+void launch_span_sort(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, PreSpan* span_pre,
+                      hipStream_t stream);
+// the probe's work list from both sides' partition bases (k_probe_work, one workgroup)
+void launch_probe_work(const uint32_t* span_base, const SignalCols& gc, const JoinParams& jp, uint32_t* work,
+                       hipStream_t stream);
 // probe work list: 4 header words + per phase one word per (key type, generation, partition,
 // signal slice)
 constexpr int kProbeMaxSplit = 64;  // signal slices per (key type, generation, partition); 8 bits of the item code

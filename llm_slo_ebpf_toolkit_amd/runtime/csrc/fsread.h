@@ -43,6 +43,17 @@ inline bool read_u64_file(const char* path, uint64_t* v) {
   return true;
 }
 
+// The same from a file kept open: one pread at offset 0 (sysfs regenerates the attribute on
+// every read from the start), no open / close per reading.
+inline bool pread_u64(int fd, uint64_t* v) {
+  char buf[32];
+  const ssize_t n = ::pread(fd, buf, sizeof(buf) - 1, 0);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  *v = std::strtoull(buf, nullptr, 10);
+  return true;
+}
+
 inline std::string join(const std::string& a, const std::string& b) {
   std::string r = a;
   while (!r.empty() && r.back() == '/') r.pop_back();

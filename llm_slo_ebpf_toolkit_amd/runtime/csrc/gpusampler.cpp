@@ -2,7 +2,9 @@
 #include "gpusampler.h"
 
 #include <dirent.h>
+#include <fcntl.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -17,7 +19,10 @@ namespace mislo {
 
 GpuSampler::GpuSampler(Ring* ring, GpuSamplerConfig cfg) : ring_(ring), cfg_(std::move(cfg)) {}
 
-GpuSampler::~GpuSampler() { stop(); }
+GpuSampler::~GpuSampler() {
+  stop();
+  for (auto& kv : occ_fd_) ::close(kv.second);
+}
 
 void GpuSampler::set_targets(const std::vector<std::pair<uint32_t, uint32_t>>& pid_pod) {
   std::lock_guard<std::mutex> lk(mu_);
@@ -59,36 +64,69 @@ void GpuSampler::refresh_locked() {
   std::sort(gpus.begin(), gpus.end());
   gpus.erase(std::unique(gpus.begin(), gpus.end()), gpus.end());
   procs_.swap(live);
+  if (gpus != gpus_) last_scan_ns_ = 0;  // other GPUs watched: re-open the files at the next reading
   gpus_.swap(gpus);
+}
+
+void GpuSampler::rescan_locked() {
+  std::map<std::pair<uint32_t, uint64_t>, int> next;
+  if (DIR* d = ::opendir(cfg_.kfd_proc.c_str())) {
+    char path[512];
+    while (dirent* e = ::readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      const uint32_t pid = (uint32_t)std::strtoul(e->d_name, nullptr, 10);
+      for (uint64_t g : gpus_) {
+        const auto key = std::make_pair(pid, g);
+        const auto it = occ_fd_.find(key);
+        if (it != occ_fd_.end()) {  // still listed: keep its open file
+          next[key] = it->second;
+          occ_fd_.erase(it);
+          continue;
+        }
+        std::snprintf(path, sizeof(path), "%s/%s/stats_%llu/cu_occupancy", cfg_.kfd_proc.c_str(), e->d_name,
+                      (unsigned long long)g);
+        const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        if (fd >= 0) next[key] = fd;
+      }
+    }
+    ::closedir(d);
+  }
+  for (auto& kv : occ_fd_) ::close(kv.second);  // processes gone, GPUs no longer watched
+  occ_fd_.swap(next);
+  ++st_.scans;
 }
 
 void GpuSampler::sample() {
   const auto t0 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> lk(mu_);
   if (gpus_.empty() || !enabled()) return;
+  const uint64_t now = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           t0.time_since_epoch()).count();
+  if (!last_scan_ns_ || now - last_scan_ns_ >= rescan_ns_) {
+    rescan_locked();
+    last_scan_ns_ = now;
+  }
   std::map<uint32_t, uint32_t> pod_of;
   for (const auto& tp : targets_) pod_of[tp.first] = tp.second;
   // every KFD process's occupancy of the watched GPUs
   std::vector<uint64_t> total(gpus_.size(), 0);
   std::map<std::pair<uint32_t, uint64_t>, uint64_t> own;  // (pod, gpu) -> its processes' occupancy
-  DIR* d = ::opendir(cfg_.kfd_proc.c_str());
-  if (!d) return;
-  char path[512];
-  while (dirent* e = ::readdir(d)) {
-    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
-    const uint32_t pid = (uint32_t)std::strtoul(e->d_name, nullptr, 10);
-    const auto pp = pod_of.find(pid);
-    for (size_t i = 0; i < gpus_.size(); ++i) {
-      std::snprintf(path, sizeof(path), "%s/%s/stats_%llu/cu_occupancy", cfg_.kfd_proc.c_str(), e->d_name,
-                    (unsigned long long)gpus_[i]);
-      uint64_t occ = 0;
-      if (!read_u64_file(path, &occ)) continue;
-      ++st_.reads;
+  for (auto it = occ_fd_.begin(); it != occ_fd_.end();) {
+    uint64_t occ = 0;
+    if (!pread_u64(it->second, &occ)) {  // the process is gone
+      ::close(it->second);
+      it = occ_fd_.erase(it);
+      continue;
+    }
+    ++st_.reads;
+    const size_t i = (size_t)(std::lower_bound(gpus_.begin(), gpus_.end(), it->first.second) - gpus_.begin());
+    if (i < gpus_.size() && gpus_[i] == it->first.second) {
       total[i] += occ;
+      const auto pp = pod_of.find(it->first.first);
       if (pp != pod_of.end()) own[{pp->second, gpus_[i]}] += occ;
     }
+    ++it;
   }
-  ::closedir(d);
   // each (pod, GPU) the pod's processes have opened: one reading
   std::set<std::pair<uint32_t, uint64_t>> pairs;
   for (const auto& tp : targets_) {

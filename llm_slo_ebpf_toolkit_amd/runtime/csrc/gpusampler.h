@@ -60,7 +60,7 @@ static_assert(sizeof(HipActivity) == 40, "mislo_hip_act layout");
 constexpr uint16_t kSigGpuQueue = 13;
 
 struct GpuSamplerStats {
-  uint64_t samples = 0, reads = 0, read_ns = 0, decisions = 0, emitted = 0, dropped = 0, evictions = 0;
+  uint64_t samples = 0, reads = 0, read_ns = 0, decisions = 0, emitted = 0, dropped = 0, evictions = 0, scans = 0;
   uint64_t max_sample_ns = 0;
   uint64_t pairs = 0;  // (pod, GPU) pairs seen at the last decision
 };
@@ -113,6 +113,7 @@ class GpuSampler {
     bool resolved = false;
   };
   void refresh_locked();  // target processes' GPUs (each decision)
+  void rescan_locked();   // the KFD process tree: open the watched GPUs' cu_occupancy files
   bool hip_locked(uint32_t pid, HipActivity* a);
   bool enabled() const;
 
@@ -122,6 +123,12 @@ class GpuSampler {
   std::vector<std::pair<uint32_t, uint32_t>> targets_;
   std::map<uint32_t, Proc> procs_;                         // target pid -> state
   std::vector<uint64_t> gpus_;                             // gpu_ids any target uses
+  // (KFD pid, gpu_id) -> its cu_occupancy file, kept open between readings (one pread each:
+  // opening every process's file per reading cost ~100 us at 50 readings/s); the tree is
+  // re-listed every rescan_ns for processes that came and went
+  std::map<std::pair<uint32_t, uint64_t>, int> occ_fd_;
+  uint64_t last_scan_ns_ = 0;
+  uint64_t rescan_ns_ = 500000000;
   std::map<std::pair<uint32_t, uint64_t>, Acc> acc_;       // (pod, gpu) -> readings
   std::map<uint32_t, HipActivity> hip_prev_, hip_override_;
   std::vector<GpuShare> last_;

@@ -572,6 +572,7 @@ class PyGpuSampler {
     py::dict d;
     d["samples"] = st.samples;
     d["reads"] = st.reads;
+    d["scans"] = st.scans;
     d["sample_ns"] = st.read_ns;
     d["max_sample_ns"] = st.max_sample_ns;
     d["decisions"] = st.decisions;

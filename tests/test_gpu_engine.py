@@ -140,7 +140,7 @@ def test_wire16_epoch_tags_match_oracle(engine):
     ev = win.events[np.argsort(win.events["ts_ns"], kind="stable")].copy()
     ev["ts_ns"][2] = 0
     cfg = np.zeros(128, dtype=np.uint64)
-    clock, model = records.EpochClock(), records.ProbeModel(cfg)
+    clock, model = records.EpochClock(), records.ProbeModel(cfg, cpus=1)  # one CPU: slots keep the event order
     first = int(ev["ts_ns"][ev["ts_ns"] > 0].min())
     cfg[124] = clock.publish(first)  # epoch 0 (tag 0), then one epoch per 250 ms cut
     bounds = [first + j * 250_000_000 for j in (1, 2, 3)]

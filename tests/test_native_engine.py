@@ -440,7 +440,7 @@ def test_headline_shape_windows_match_the_oracle():
     gen = ReplayGenerator(cfg)
     wins = [gen.next_window() for _ in range(2)]
     imgs = build_replay_images(wins, user_rec=24)
-    sig_cap = max(len(i.framed) // 24 + len(i.user) for i in imgs)
+    sig_cap = max(R.framed_rows(i.framed) + len(i.user) for i in imgs)
     halo_ms = 2000.0
     pipe = WindowPipeline(sig_cap, 16384, 64, model="bayes", learn=False, user_cap=1 << 18, halo_ms=halo_ms)
     rt = load()

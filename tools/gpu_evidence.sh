@@ -12,6 +12,7 @@
 #   live3     the rocprof tool's GPU tests, then config3
 #   live34    config3, then config4 (TP = visible GPUs)
 #   headline  the headline-shape oracle test, then config4
+#   branch    GPU tests, smoke, the bench with / without the span branch stream, a kernel trace
 #   overhead  the shipped agent's CPU / RSS at 1M events/s (its defaults: one hardware queue)
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
 #   spread    the headline bench at K = 20 and K = 200, repeated on one box
@@ -51,6 +52,13 @@ case "${1:-reentry}" in
   headline) # the bench-shape oracle test, then config 4 with lighter burners
     $S "400|headline|python -u -m pytest tests/test_native_engine.py -m gpu -x -v -s --timeout 360 --timeout-method thread -k headline" \
        "700|c4|python -u tools/config4_evidence.py --out gpurun_out/r4_config4 --burners-per-cpu 2 ${2:-}" ;;
+  branch)   # GPU tests, then the bench with and without the span branch stream, and a kernel trace
+    $S "400|gputests|python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread" \
+       "200|smoke|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
+       "300|bench|python -u bench.py" \
+       "300|bench_nobranch|MISLO_SPAN_STREAM=0 python -u bench.py" \
+       "300|bench_branch_defprio|MISLO_SPAN_STREAM_PRIO=0 python -u bench.py" \
+       "300|trace|rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/trace -- python3 bench.py --steps 20 --warmup 3 --paced-windows 0" ;;
   live)     # configs 3 and 2 back to back (the live-attribution evidence)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
        "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
