@@ -355,24 +355,62 @@ uint64_t xgmi_latency(uint64_t src, uint64_t dst, uint64_t bytes, uint64_t dur) 
 
 // Every KFD process's cu_occupancy on one GPU (CU-equivalents of resident waves): (host pid,
 // occupancy) of the processes with a stats_<gpu_id> directory -- the others are not on this GPU.
-bool kfd_occupancy(uint64_t gpu_id, std::vector<std::pair<uint32_t, uint64_t>>* out) {
-  out->clear();
-  DIR* d = opendir(g.kfd_proc.c_str());
-  if (!d) return false;
-  char path[512], buf[32];
-  while (dirent* e = readdir(d)) {
-    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
-    std::snprintf(path, sizeof(path), "%s/%s/stats_%llu/cu_occupancy", g.kfd_proc.c_str(), e->d_name,
-                  (unsigned long long)gpu_id);
-    const int fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) continue;
-    const ssize_t n = read(fd, buf, sizeof(buf) - 1);
-    close(fd);
-    if (n <= 0) continue;
-    buf[n] = 0;
-    out->emplace_back((uint32_t)std::strtoul(e->d_name, nullptr, 10), std::strtoull(buf, nullptr, 10));
+// The files stay open between readings (one pread each); the process tree is re-listed every
+// 500 ms for processes that came and went -- an opendir plus an open / read / close per process
+// cost ~130 us a reading (profiles/r4_config3_gated/rocprof_tool.log, read_us).
+struct OccFiles {
+  std::vector<std::pair<uint32_t, int>> fds;  // (host pid, cu_occupancy fd)
+  std::chrono::steady_clock::time_point listed{};
+  bool have = false;
+};
+
+void occ_list(uint64_t gpu_id, OccFiles& f) {
+  std::map<uint32_t, int> old;
+  for (const auto& e : f.fds) old[e.first] = e.second;
+  std::vector<std::pair<uint32_t, int>> next;
+  if (DIR* d = opendir(g.kfd_proc.c_str())) {
+    char path[512];
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      const uint32_t pid = (uint32_t)std::strtoul(e->d_name, nullptr, 10);
+      const auto it = old.find(pid);
+      if (it != old.end()) {
+        next.emplace_back(pid, it->second);
+        old.erase(it);
+        continue;
+      }
+      std::snprintf(path, sizeof(path), "%s/%s/stats_%llu/cu_occupancy", g.kfd_proc.c_str(), e->d_name,
+                    (unsigned long long)gpu_id);
+      const int fd = open(path, O_RDONLY | O_CLOEXEC);
+      if (fd >= 0) next.emplace_back(pid, fd);
+    }
+    closedir(d);
   }
-  closedir(d);
+  for (const auto& kv : old) close(kv.second);
+  f.fds.swap(next);
+  f.listed = std::chrono::steady_clock::now();
+  f.have = true;
+}
+
+bool kfd_occupancy(uint64_t gpu_id, std::vector<std::pair<uint32_t, uint64_t>>* out) {
+  static std::mutex mu;  // the sampler thread, and init's readability check
+  static std::map<uint64_t, OccFiles> files;
+  std::lock_guard<std::mutex> lk(mu);
+  out->clear();
+  OccFiles& f = files[gpu_id];
+  if (!f.have || std::chrono::steady_clock::now() - f.listed > std::chrono::milliseconds(500)) occ_list(gpu_id, f);
+  char buf[32];
+  for (size_t i = 0; i < f.fds.size();) {
+    const ssize_t n = pread(f.fds[i].second, buf, sizeof(buf) - 1, 0);
+    if (n <= 0) {  // the process is gone
+      close(f.fds[i].second);
+      f.fds.erase(f.fds.begin() + (std::ptrdiff_t)i);
+      continue;
+    }
+    buf[n] = 0;
+    out->emplace_back(f.fds[i].first, std::strtoull(buf, nullptr, 10));
+    ++i;
+  }
   return !out->empty();
 }
 

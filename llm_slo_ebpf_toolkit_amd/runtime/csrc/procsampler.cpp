@@ -55,7 +55,46 @@ bool psi_some_us(const std::string& text, uint64_t* v) {
 
 ProcSampler::ProcSampler(Ring* ring, ProcSamplerConfig cfg) : ring_(ring), cfg_(std::move(cfg)) {}
 
-ProcSampler::~ProcSampler() { stop(); }
+ProcSampler::~ProcSampler() {
+  stop();
+  for (auto& kv : procs_) close_tasks(kv.second);
+}
+
+void ProcSampler::close_tasks(Proc& p) {
+  for (auto& t : p.task_fds) ::close(t.second);
+  p.task_fds.clear();
+  p.listed = false;
+}
+
+// (Re-)list the process's threads: keep the open files of threads still there, open the new ones.
+void ProcSampler::list_tasks(uint32_t pid, Proc& p, uint64_t mono_ns) {
+  const std::string task = join(cfg_.proc_root, std::to_string(pid) + "/task");
+  std::vector<uint32_t> tids;
+  if (DIR* dir = ::opendir(task.c_str())) {
+    while (dirent* de = ::readdir(dir)) {
+      const char* n = de->d_name;
+      if (*n < '0' || *n > '9') continue;
+      tids.push_back((uint32_t)std::strtoul(n, nullptr, 10));
+    }
+    ::closedir(dir);
+  }
+  std::sort(tids.begin(), tids.end());
+  std::vector<std::pair<uint32_t, int>> next;
+  size_t j = 0;
+  for (uint32_t tid : tids) {
+    while (j < p.task_fds.size() && p.task_fds[j].first < tid) ::close(p.task_fds[j++].second);  // gone
+    if (j < p.task_fds.size() && p.task_fds[j].first == tid) {
+      next.push_back(p.task_fds[j++]);
+      continue;
+    }
+    const int fd = ::open(join(task, std::to_string(tid) + "/schedstat").c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd >= 0) next.emplace_back(tid, fd);
+  }
+  for (; j < p.task_fds.size(); ++j) ::close(p.task_fds[j].second);
+  p.task_fds.swap(next);
+  p.listed_ns = mono_ns;
+  p.listed = true;
+}
 
 void ProcSampler::set_targets(const std::vector<std::pair<uint32_t, uint32_t>>& pid_pod) {
   std::lock_guard<std::mutex> lk(mu_);
@@ -168,23 +207,25 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
   };
   for (const auto& tp : targets_) {
     const uint32_t pid = tp.first, pod = tp.second;
-    const std::string task = join(cfg_.proc_root, std::to_string(pid) + "/task");
-    DIR* dir = ::opendir(task.c_str());
-    if (!dir) continue;
-    std::vector<uint32_t> tids;
-    while (dirent* de = ::readdir(dir)) {
-      const char* n = de->d_name;
-      if (*n < '0' || *n > '9') continue;
-      tids.push_back((uint32_t)std::strtoul(n, nullptr, 10));
+    if (live.count(pid)) continue;  // listed twice
+    auto pit = procs_.find(pid);
+    Proc pr = pit != procs_.end() ? pit->second : Proc{};
+    if (pit != procs_.end()) pit->second.task_fds.clear();  // moved into pr
+    if (!pr.listed || mono_ns < pr.listed_ns || mono_ns - pr.listed_ns >= task_rescan_ns_)
+      list_tasks(pid, pr, mono_ns);
+    if (pr.task_fds.empty()) {  // the process is gone (or unreadable)
+      close_tasks(pr);
+      continue;
     }
-    ::closedir(dir);
-    std::sort(tids.begin(), tids.end());
     uint64_t w_sum = 0, s_sum = 0, w_all = 0;
-    for (uint32_t tid : tids) {
-      std::string s;
-      if (!read_small(join(task, std::to_string(tid) + "/schedstat"), &s)) continue;
+    for (const auto& tf : pr.task_fds) {
+      const uint32_t tid = tf.first;
+      char buf[128];
+      const ssize_t nr = ::pread(tf.second, buf, sizeof(buf) - 1, 0);
+      if (nr <= 0) continue;  // the thread exited (dropped at the next listing)
+      buf[nr] = 0;
       char* p = nullptr;
-      std::strtoull(s.c_str(), &p, 10);
+      std::strtoull(buf, &p, 10);
       const uint64_t wait = std::strtoull(p, &p, 10), slices = std::strtoull(p, &p, 10);
       const auto key = std::make_pair(pid, tid);
       next[key] = {wait, slices};
@@ -198,8 +239,6 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
         s_sum += ds;
       }
     }
-    auto pit = procs_.find(pid);
-    Proc pr = pit != procs_.end() ? pit->second : Proc{};
     if (!pr.resolved) resolve(pid, pr);
     if ((mask >> kSigRunq & 1) && s_sum && w_sum / s_sum >= cfg_.runq_floor_ns)
       rec(kSigRunq, pr.ns_pid, pid, pod, w_sum / s_sum);
@@ -223,6 +262,7 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
     }
   }
   prev_.swap(next);
+  for (auto& kv : procs_) close_tasks(kv.second);  // processes no longer watched (the rest moved)
   procs_.swap(live);
   for (auto it = groups_.begin(); it != groups_.end();) it = it->second.seen ? std::next(it) : groups_.erase(it);
   uint64_t pushed = 0;

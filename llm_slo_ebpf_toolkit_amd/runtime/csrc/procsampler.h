@@ -92,9 +92,17 @@ class ProcSampler {
     uint32_t ns_pid = 0;
     uint32_t steal_run = 0;  // consecutive intervals with the wait share at the floor
     bool resolved = false;
+    // its threads' schedstat files, kept open (one pread per thread and tick instead of an
+    // open / read / close); the task directory is re-listed every task_rescan_ns
+    std::vector<std::pair<uint32_t, int>> task_fds;  // (tid, fd), tid order
+    uint64_t listed_ns = 0;
+    bool listed = false;
     std::string cfs_file, mem_file, cpu_psi_file;  // empty: none
   };
   void resolve(uint32_t pid, Proc& p);
+  void list_tasks(uint32_t pid, Proc& p, uint64_t mono_ns);
+  static void close_tasks(Proc& p);
+  uint64_t task_rescan_ns_ = 1000000000;
   uint64_t group_delta(const std::string& file, int kind);  // kind 0: cpu.stat throttle ns, 1: PSI some ns
 
   Ring* ring_;
