@@ -564,8 +564,10 @@ __global__ __launch_bounds__(NT) void k_span_sort(SpanCols sc, const uint32_t* _
   }
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT, 4) void k_probe(const PreSpan* __restrict__ pre,
+// LG: incident sums privatised in LDS (12 KB of the workgroup's 38 KB: 4 workgroups per CU);
+// without, they go straight to the striped global copies and the probe fits 6 workgroups per CU.
+template <int NT, bool LG>
+__global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restrict__ pre,
                                               const uint32_t* __restrict__ span_base, SignalCols gc, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups,
@@ -588,8 +590,9 @@ __global__ __launch_bounds__(NT, 4) void k_probe(const PreSpan* __restrict__ pre
   __shared__ int s_wsum[NT / 64];
   __shared__ int s_nneedy;
   __shared__ uint32_t s_item;
-  __shared__ unsigned long long s_gsum[kLdsGroups * kSlots];
-  __shared__ uint32_t s_gcnt[kLdsGroups * kSlots];
+  constexpr int kLg = LG ? kLdsGroups * kSlots : 1;
+  __shared__ unsigned long long s_gsum[kLg];
+  __shared__ uint32_t s_gcnt[kLg];
 
   // incident sums go to one of kGroupStripes copies (folded after the join): thousands of
   // workgroups adding into the same G x 16 words would otherwise serialise in L2 atomics
@@ -598,7 +601,7 @@ __global__ __launch_bounds__(NT, 4) void k_probe(const PreSpan* __restrict__ pre
     gsum += stripe;
     gcnt += stripe;
   }
-  const bool grp_lds = n_groups <= kLdsGroups;
+  const bool grp_lds = LG && n_groups <= kLdsGroups;
   const bool any_groups = jp.group_mode == 1 && n_groups > 0;
   if (grp_lds && any_groups) {
     for (int i = threadIdx.x; i < kLdsGroups * kSlots; i += NT) {
@@ -1151,9 +1154,18 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
     return x >= 1 ? x : kSigPerItem;
   }();
   (void)sc, (void)span_items, (void)per_item;
-  for (int phase = 0; phase < 2; ++phase)
-    hipLaunchKernelGGL((k_probe<256>), dim3(grid), dim3(256), 0, stream, span_pre, span_base, gc, span_cap, jp, top3,
-                       cnt, n_groups, gsum, gcnt, dbg, work, phase);
+  static const bool lds_groups = [] {  // MISLO_PROBE_LDS_GROUPS=0: sums to global memory, 6 WG/CU
+    const char* v = getenv("MISLO_PROBE_LDS_GROUPS");
+    return !(v && atoi(v) == 0);
+  }();
+  for (int phase = 0; phase < 2; ++phase) {
+    if (lds_groups)
+      hipLaunchKernelGGL((k_probe<256, true>), dim3(grid), dim3(256), 0, stream, span_pre, span_base, gc, span_cap, jp,
+                         top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);
+    else
+      hipLaunchKernelGGL((k_probe<256, false>), dim3(grid), dim3(256), 0, stream, span_pre, span_base, gc, span_cap, jp,
+                         top3, cnt, n_groups, gsum, gcnt, dbg, work, phase);
+  }
 }
 
 void launch_span_sort(const SpanCols& sc, const uint32_t* span_items, const uint32_t* span_base, PreSpan* span_pre,
