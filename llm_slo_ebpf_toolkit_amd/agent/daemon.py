@@ -578,8 +578,10 @@ class Agent:
                 self.metrics.burn_err.set(err)
         # the SLO-impact window is the forecast horizon the burn rate is quoted over (5 minutes)
         impact_min = max(1, int(round(self.burn.horizon * self.o.window_ms / 60000.0)))
+        reqs = sli[:, 0].tolist() if sli is not None else []
+        feat_l = np.asarray(feat, dtype=np.float64).tolist()  # Python rows: one conversion per window
         for g in range(G):
-            if sli is not None and g < sli.shape[0] and sli[g, 0] == 0:
+            if g < len(reqs) and reqs[g] == 0:
                 continue  # no request of this group in the window: no incident to attribute
             ranked = model.ranked(post[g, :D], bits[g, :D])
             if not ranked or ranked[0].posterior < self.o.min_confidence:
@@ -588,8 +590,8 @@ class Agent:
             ev = []
             for sname in top.evidence:
                 spec = catalog.BY_NAME[sname]
-                v = float(feat[g, spec.slot])
-                ev.append(Evidence(spec.semconv or sname, round(v, 3) if np.isfinite(v) else "elevated", "ebpf"))
+                v = feat_l[g][spec.slot]
+                ev.append(Evidence(spec.semconv or sname, round(v, 3) if math.isfinite(v) else "elevated", "ebpf"))
             if not ev:
                 ev = [Evidence("llm.ebpf.correlation_confidence", float(top.posterior), "ebpf")]
             burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)

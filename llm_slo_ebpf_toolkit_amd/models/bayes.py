@@ -31,6 +31,7 @@ All CPU math is float64 numpy (the oracle); the GPU path evaluates the same W/b.
 
 from __future__ import annotations
 
+import functools
 import itertools
 import math
 from dataclasses import dataclass, field
@@ -66,6 +67,12 @@ class Posterior:
     domain: str
     posterior: float
     evidence: List[str]
+
+
+@functools.lru_cache(maxsize=4096)
+def _evidence_names(bits: int) -> tuple:
+    """Signal names of an evidence bitmask over the 16 slots, sorted (REF's evidence order)."""
+    return tuple(sorted(catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if bits >> s & 1))
 
 
 @dataclass
@@ -163,13 +170,14 @@ class LinearPosteriorModel:
         return self.ranked(self.posteriors(vec)[0], self.evidence_bits(vec)[0])
 
     def ranked(self, post: np.ndarray, bits: np.ndarray) -> List[Posterior]:
-        """Posterior row + evidence bitmask row (numpy or the GPU kernel's) -> sorted hypotheses."""
-        out: List[Posterior] = []
-        for d, dom in enumerate(catalog.ALL_DOMAINS[: self.weights.shape[1]]):
-            if not np.isfinite(self.bias[d]):
-                continue
-            ev = sorted(catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if int(bits[d]) >> s & 1)
-            out.append(Posterior(dom, float(post[d]), ev))
+        """Posterior row + evidence bitmask row (numpy or the GPU kernel's) -> sorted hypotheses.
+        Rows become Python lists once (the agent ranks every incident of every window)."""
+        D = self.weights.shape[1]
+        live = np.isfinite(self.bias[:D]).tolist()
+        pl = np.asarray(post, dtype=np.float64)[:D].tolist()
+        bl = np.asarray(bits).astype(np.int64)[:D].tolist()
+        out: List[Posterior] = [Posterior(dom, pl[d], list(_evidence_names(bl[d])))
+                                for d, dom in enumerate(catalog.ALL_DOMAINS[:D]) if live[d]]
         out.sort(key=lambda p: -p.posterior)  # Python sort is stable == sort.SliceStable
         return out
 

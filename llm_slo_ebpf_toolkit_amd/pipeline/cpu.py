@@ -36,6 +36,9 @@ class CpuWindowResult:
     join: oracle.JoinResult
 
 
+STATS_OFF, STATS_LEN = sum(PACKET_LAYOUT[:5]), PACKET_LAYOUT[5] + PACKET_LAYOUT[6]  # sufficient statistics
+
+
 def build_packet(hist, status, misc, dbg, confusion, stats: SufficientStats) -> np.ndarray:
     p = np.zeros(PACKET_LEN, dtype=np.float64)
     o = 0
@@ -176,6 +179,7 @@ class CpuRingEngine:
         self.model = None
         self.win: Dict[int, dict] = {}
         self._totals = np.zeros(PACKET_LEN)
+        self._stats_acc = np.zeros(STATS_LEN)
         self.windows_folded = 0
         self.graphs = 0
         self.staged_bytes = self.direct_bytes = 0
@@ -307,6 +311,8 @@ class CpuRingEngine:
             outs = [None] * self.world
             dist.all_gather_object(outs, out, group=self.group)
         self._totals += pk
+        if learn:  # the node-wide statistics of learning windows (the device folds them in k_refit_nb)
+            self._stats_acc += pk[STATS_OFF:STATS_OFF + STATS_LEN]
         ms = 1e3 * (time.perf_counter() - t0)
         self.win[k % max(1, self.buffers)] = {"k": k, "packet": pk, "res": out, "all": outs, "ms": ms,
                                              "rows": (n_loc, res.n_rows)}
@@ -368,11 +374,26 @@ class CpuRingEngine:
         self._totals[:] = 0
 
     def stats_acc(self) -> np.ndarray:
-        return np.zeros(1040)
+        return self._stats_acc.copy()
 
     def restore(self, stats, model, folded) -> None:
+        if stats is not None and len(stats) == STATS_LEN:
+            self._stats_acc = np.asarray(stats, dtype=np.float64).copy()
         if len(model):
             self.set_model_bytes(model)
+
+    # The host engine scores with the model image it was given: the device refit (k_refit_nb,
+    # rebuilding the tables from the all-reduced statistics) has no counterpart here, and the image
+    # a trainer restores is already the host-fitted model (models/train.py), which the device refit
+    # reproduces (__graft_entry__.smoke checks that equality on the GPU).
+    def set_refit(self, alpha: float, prior_pseudo: float, inv_temp: float, min_count: float) -> None:
+        self.refit_params = (float(alpha), float(prior_pseudo), float(inv_temp), float(min_count))
+
+    def refit_now(self) -> None:
+        pass
+
+    def set_device_refit(self, on: bool) -> None:
+        pass
 
     def sync(self) -> None:
         pass

@@ -385,7 +385,7 @@ def test_bench_runs_the_agents_worker_path_on_two_ranks(tmp_path):
     """`bench.py --gpus 2` (self-launched ranks, the host oracle engine over
     gloo) times the agent's topology: each rank is a window worker on its own split ring set
     (agent/worker.py WorkerCore.window per step) and rank 0 runs the controller's per-window
-    epilogue (Agent._emit_window) inside the timed region."""
+    epilogue (Agent._emit_window) over every timed window, measured on its own."""
     out = tmp_path / "bench.json"
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--engine", "cpu", "--model", "bayes",
                         "--events", "4096", "--spans", "256", "--services", "8", "--windows", "2", "--heldout", "3",
@@ -399,3 +399,20 @@ def test_bench_runs_the_agents_worker_path_on_two_ranks(tmp_path):
     # every node-wide incident of the timed windows became an attribution on the controller
     assert d["incidents_scored_timed_windows"] == 3 * 2 * 8 == d["attributions_emitted_timed"]
     assert d["host_epilogue_us_per_window"] > 0
+
+
+def test_bench_trains_the_learned_model_on_the_host_engine(tmp_path):
+    """`bench.py --engine cpu` with the learned model: the host engine accumulates the labelled
+    windows' sufficient statistics as the device does (its packets' statistics block), so the
+    model trained from random-init priors scores the timed windows (it scored none before)."""
+    out = tmp_path / "bench.json"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--engine", "cpu", "--events", "16384",
+                        "--spans", "1024", "--services", "16", "--windows", "2", "--heldout", "0",
+                        "--paced-windows", "0", "--steps", "3", "--warmup", "1", "--ring-mib", "16",
+                        "--train-windows", "8", "--train-events", "16384", "--train-spans", "1024", "--out", str(out)],
+                       capture_output=True, text=True, timeout=580, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["training"]["windows"] == 8 and d["training"]["incidents_trained"] > 0
+    assert d["macro_f1_timed_windows"] >= 0.9
+    assert d["attributions_emitted_timed"] == d["incidents_scored_timed_windows"] == 3 * 16
