@@ -12,8 +12,9 @@ Topology = the agent's (``agent --gpus N`` on split rings, agent/worker.py): eve
 window worker reading its own ring set -- the node's producers route each record to the worker
 owning its service, so each GPU DMAs and decodes its share of the node's stream only -- and its
 timed windows run through the agent's worker path (``WorkerCore.window``: stage window k, collect
-window k-1's packet and node-wide incident results) with rank 0 also doing the controller's
-per-window host epilogue (``Agent._emit_window``: metrics, IncidentAttributions, output).
+the finished windows' packets and node-wide incident results) with rank 0 also running the
+controller's per-window host epilogue (``Agent._emit_window``: metrics, IncidentAttributions,
+output) over them, measured on its own.
 
 One step = one collection window per GPU, exactly as the agent runs it:
 
@@ -501,8 +502,9 @@ def main() -> int:
             break
         time.sleep(1e-3)
     prefilled = int(cuts.size)
-    # the agent's worker path (agent/worker.py WorkerCore.window: stage window k, collect window
-    # k-1's node-wide packet and every worker's incident results) is the timed step. Rank 0 then
+    # the agent's worker path (agent/worker.py WorkerCore.window: stage window k, collect the
+    # finished windows' node-wide packets and every worker's incident results -- back to back,
+    # window k-2 once two are in flight) is the timed step. Rank 0 then
     # runs the controller's per-window host epilogue (agent/daemon.py Agent._emit_window:
     # Prometheus histograms, IncidentAttributions from the posteriors, JSONL output) over every
     # collected window, timed on its own: it is O(incident groups), runs once per agent window
@@ -522,10 +524,10 @@ def main() -> int:
     svc_names = [f"svc-{g + 1}" for g in range(g_node)]
     epi = [0.0, 0]  # host epilogue seconds, windows
 
-    def epilogue(rep):
-        if ctl is not None and rep.get("prev") is not None:
+    def epilogue(prev):
+        if ctl is not None:
             te = time.perf_counter()
-            ctl._emit_window([rep], time.time_ns(), g_node, svc_names, rb, pipe.model)
+            ctl._emit_window([prev], time.time_ns(), g_node, svc_names, rb, pipe.model)
             epi[0] += time.perf_counter() - te
             epi[1] += 1
 
@@ -543,8 +545,8 @@ def main() -> int:
     collected = []
     for j in range(a.warmup, a.warmup + a.steps):
         rep = core.window(next_cut(), a.services, labels=imgs[j % len(imgs)].labels)
-        if rank == 0 and rep.get("prev") is not None:
-            collected.append(rep)
+        if rank == 0:
+            collected.extend(rep["prevs"])
         last = rep["k"]
         kernel_recs += rep["staged"]["n_kernel"]
     fin = core.stop()  # the last window's results (drains the source)
@@ -553,8 +555,8 @@ def main() -> int:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    for rep in collected + ([fin] if rank == 0 else []):
-        epilogue(rep)
+    for prev in collected + (fin["prevs"] if rank == 0 else []):
+        epilogue(prev)
     attributions_emitted = ctl.attributions_emitted if ctl is not None else 0
     if ctl is not None:
         ctl.close()

@@ -604,13 +604,13 @@ class Agent:
                                   if p.posterior >= 0.01]))
         return out
 
-    def _emit_window(self, replies: List[dict], t_ns: int, G: int, names, ring, model) -> None:
-        """Window k-1 of every worker: worker 0 carries the node-wide packet (RCCL all-reduce)
-        and every worker's incidents (all-gather); each worker its own ring accounting."""
+    def _emit_window(self, prevs: List[dict], t_ns: int, G: int, names, ring, model) -> None:
+        """One finished window, as every worker's part of it in rank order (worker.PrevJoiner):
+        worker 0's carries the node-wide packet (RCCL all-reduce) and every worker's incidents
+        (all-gather); each worker its own ring accounting."""
         from ..pipeline.window import RING_FIELDS, unpack_packet
         from .worker import merge_results
 
-        prevs = [r["prev"] for r in replies if r.get("prev") is not None]
         if not prevs or "packet" not in prevs[0]:
             return
         head = prevs[0]
@@ -700,7 +700,7 @@ class Agent:
         from ..collector.records import EpochClock
         from ..pipeline.window import Cut
         from ..safety import TreeCPUSampler
-        from .worker import WorkerError, WorkerPool, WorkerSpec, groups_of
+        from .worker import PrevJoiner, WorkerError, WorkerPool, WorkerSpec, groups_of
 
         o = self.o
         N = self.n_gpus()
@@ -850,6 +850,7 @@ class Agent:
         period = o.window_ms / 1000.0
         nxt = time.monotonic() + period
         cut_t = {}
+        joiner = PrevJoiner(N)
         windows = 0
         try:
             while not self.stop_event.is_set():
@@ -875,11 +876,11 @@ class Agent:
                 except WorkerError as exc:
                     pool, split = self._restart_workers(exc, (ring, user, spans), sets, maps, G)
                     cut_t.clear()  # the lost windows' records are read again by the new workers
+                    joiner.reset(len(self.specs))
                     continue
                 cut_t[replies[0]["k"]] = t
-                prev = replies[0].get("prev")
-                if prev is not None:
-                    self._emit_window(replies, cut_t.pop(prev["k"], t), G, names, ring, model)
+                for parts in joiner.add(replies):
+                    self._emit_window(parts, cut_t.pop(parts[0]["k"], t), G, names, ring, model)
                 if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
                     self._scan_pods(maps)  # pod churn
                     if getattr(self, "bpf_loader", None) is not None:
@@ -896,8 +897,8 @@ class Agent:
                     maps.reset_ctx_ids()  # kernel context ids run low: redefine from scratch
             pool = self.pool
             final = pool.stop()
-            if final and final[0].get("prev") is not None:
-                self._emit_window(final, cut_t.pop(final[0]["prev"]["k"], time.time_ns()), G, names, ring, model)
+            for parts in joiner.add(final or []):
+                self._emit_window(parts, cut_t.pop(parts[0]["k"], time.time_ns()), G, names, ring, model)
             self.last_summary = final[0].get("summary") if final else None
             if state:
                 self.save_state(state)

@@ -40,11 +40,12 @@ windows that were in flight are read again (at least once).
 
 from __future__ import annotations
 
+import collections
 import os
 import time
 import traceback
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Deque, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -99,6 +100,34 @@ def merge_results(parts: List[dict], n_groups: int) -> dict:
     return out
 
 
+class PrevJoiner:
+    """The controller's side of the workers' collected windows: each worker reports a window when
+    its own chain is done, so one reply may carry none, one or several of them, and the workers
+    need not report a window in the same reply. A window is complete once every worker has
+    reported it; complete windows come out in window order, each as the workers' parts in rank
+    order (rank 0's carries the node-wide packet and every worker's incidents)."""
+
+    def __init__(self, world: int):
+        self.world = int(world)
+        self.parts: Dict[int, Dict[int, dict]] = {}
+
+    def add(self, replies) -> List[List[dict]]:
+        for r in replies:
+            for p in r.get("prevs", ()):
+                self.parts.setdefault(int(p["k"]), {})[int(r["rank"])] = p
+        out = []
+        for k in sorted(self.parts):
+            if len(self.parts[k]) < self.world:
+                break
+            got = self.parts.pop(k)
+            out.append([got[i] for i in sorted(got)])
+        return out
+
+    def reset(self, world: int) -> None:
+        self.world = int(world)
+        self.parts.clear()
+
+
 class WorkerCore:
     """One GPU's share of the node's windows (the body of a worker process, or of LocalWorker)."""
 
@@ -134,7 +163,7 @@ class WorkerCore:
                                     shared=shared and not spec.split)
         if spec.pods is not None:
             self.pipe.eng.set_pods(*spec.pods)
-        self.pending: Optional[Tuple[int, float]] = None
+        self.pending: Deque[Tuple[int, float, int]] = collections.deque()
         self.windows = 0
 
     @classmethod
@@ -144,13 +173,24 @@ class WorkerCore:
         core = cls.__new__(cls)
         core.spec, core.pipe, core.src = spec, pipe, src
         core.rings = (src.ring, src.user_ring, src.span_ring)
-        core.pending = None
+        core.pending = collections.deque()
         core.windows = 0
         return core
 
+    @property
+    def max_pending(self) -> int:
+        """Windows staged but not yet collected, at most: the engine's buffers minus the one the
+        next stage reuses (that window's results must have been read first)."""
+        return max(1, int(self.pipe.nb) - 1)
+
     def window(self, cut, n_groups: int, pods=None, labels=None) -> dict:
-        """Stage window k; return what the controller needs of window k-1 (finished by now or
-        nearly: the engine runs nb windows deep). ``labels``: incident labels for the device's
+        """Stage window k; return, under "prevs", what the controller needs of the earlier windows
+        that are finished: every one whose chain is done (at the agent's window period, window
+        k-1), and the oldest ones regardless once max_pending are in flight (back-to-back
+        windows: the next stage reuses the oldest window's buffer). Collection never waits for a
+        window younger than that, so window k+1's copies are issued while windows k-1 and k
+        compute (waiting for k-1 here put one window's copy time plus the host's turnaround on
+        every window: profiles/r4_timeline/). ``labels``: incident labels for the device's
         confusion matrix (the benchmark's replay windows; the agent has none)."""
         if pods is not None and len(pods[0]):
             self.pipe.eng.set_pods(*pods)
@@ -158,9 +198,12 @@ class WorkerCore:
         r = self.src.stage(cut, n_groups, labels, with_labels=labels is not None, learn=False)
         host_us = 1e6 * (time.perf_counter() - t0)
         out = {"rank": self.spec.rank, "k": r["k"], "staged": r, "done": self.src.done()}
-        prev, self.pending = self.pending, (r["k"], host_us, n_groups)
-        if prev is not None:
-            out["prev"] = self._collect(*prev)
+        self.pending.append((r["k"], host_us, n_groups))
+        prevs = []
+        while len(self.pending) > 1 and (len(self.pending) > self.max_pending or
+                                         self.pipe.eng.query(self.pending[0][0])):
+            prevs.append(self._collect(*self.pending.popleft()))
+        out["prevs"] = prevs
         self.windows += 1
         return out
 
@@ -175,10 +218,9 @@ class WorkerCore:
         return d
 
     def stop(self) -> dict:
-        out = {"rank": self.spec.rank, "done": None}
-        if self.pending is not None:
-            out["prev"] = self._collect(*self.pending)
-            self.pending = None
+        out = {"rank": self.spec.rank, "done": None, "prevs": []}
+        while self.pending:
+            out["prevs"].append(self._collect(*self.pending.popleft()))
         self.src.drain()
         out["done"] = self.src.done()
         out["summary"] = self.pipe.summary() if self.spec.rank == 0 else None

@@ -57,6 +57,19 @@ def test_merge_results_places_every_group_once():
     np.testing.assert_array_equal(m["sli"][:, 0], np.arange(G))
 
 
+def joiner_windows(replies, world):
+    """Every finished window of a run's replies (one list per pool.window / pool.stop call), as
+    the workers' parts in rank order (the controller's PrevJoiner)."""
+    from llm_slo_ebpf_toolkit_amd.agent.worker import PrevJoiner
+
+    j = PrevJoiner(world)
+    out = []
+    for rep in replies:
+        out.extend(j.add(rep))
+    assert not j.parts, "a window some worker never reported"
+    return out
+
+
 def _windows(n_win=3, seed=11):
     from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
     from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
@@ -108,8 +121,7 @@ def _run_pool(world, imgs, pods, tag, ring_bytes=1 << 22, engine="cpu", late_pod
             upd = late_pods[1] if late_pods is not None and late_pods[0] == j else None
             replies.append(pool.window(Cut(ring.producer_pos, user.head, spans.head, img.bases), 8, upd))
         replies.append(pool.stop())
-        for rep in replies[1:]:
-            prev = [r["prev"] for r in rep]
+        for prev in joiner_windows(replies, world):
             out.append({"packet": prev[0]["packet"], "res": merge_results(prev[0]["results"], 8),
                         "events": sum(int(p["ring"][5]) for p in prev)})
         # every worker is done with every record: the controller freed the rings completely
@@ -186,8 +198,7 @@ def _run_split(world, shard_imgs, pods, tag, ring_bytes=1 << 22, engine="cpu"):
             direct.append([len(img.framed) + img.user.nbytes for img in imgs])
             replies.append(pool.window(cuts, 8))
         replies.append(pool.stop())
-        for rep in replies[1:]:
-            prev = [r["prev"] for r in rep]
+        for prev in joiner_windows(replies, world):
             out.append({"packet": prev[0]["packet"], "res": merge_results(prev[0]["results"], 8),
                         "events": sum(int(p["ring"][5]) for p in prev)})
         # every worker freed its own rings completely (nobody else consumes them)
