@@ -427,3 +427,21 @@ def test_bench_trains_the_learned_model_on_the_host_engine(tmp_path):
     assert d["training"]["windows"] == 8 and d["training"]["incidents_trained"] > 0
     assert d["macro_f1_timed_windows"] >= 0.9
     assert d["attributions_emitted_timed"] == d["incidents_scored_timed_windows"] == 3 * 16
+
+
+def test_prev_joiner_emits_windows_once_every_worker_reported_them():
+    """Workers report a window when their own chain is done (agent/worker.py WorkerCore.window):
+    worker 1 may still be computing window 3 when worker 0 reports it. The controller emits a
+    window once both reported it, in window order, with rank 0's part first."""
+    from llm_slo_ebpf_toolkit_amd.agent.worker import PrevJoiner
+
+    j = PrevJoiner(2)
+    p = lambda r, k: {"k": k, "rank_tag": r}  # noqa: E731
+    assert j.add([{"rank": 1, "prevs": [p(1, 3)]}, {"rank": 0, "prevs": []}]) == []
+    out = j.add([{"rank": 0, "prevs": [p(0, 3), p(0, 4)]}, {"rank": 1, "prevs": []}])
+    assert [[x["rank_tag"] for x in w] for w in out] == [[0, 1]] and out[0][0]["k"] == 3
+    out = j.add([{"rank": 1, "prevs": [p(1, 4), p(1, 5)]}, {"rank": 0, "prevs": [p(0, 5)]}])
+    assert [w[0]["k"] for w in out] == [4, 5] and not j.parts
+    j.add([{"rank": 0, "prevs": [p(0, 6)]}])
+    j.reset(1)  # a worker was lost: the pool restarts with one worker and re-reads those windows
+    assert j.add([{"rank": 0, "prevs": [p(0, 6)]}])[0][0]["k"] == 6
