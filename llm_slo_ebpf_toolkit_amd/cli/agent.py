@@ -97,7 +97,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("model", d.model, "attribution model: bayes (REF table) | bayes_gpu (REF table + GPU signals/domains) | bayes_learned | lda"),
         ("min-confidence", d.min_confidence, "emit incidents whose top posterior is at least this"),
         ("ttft-slo-ms", d.ttft_slo_ms, "per-incident TTFT SLO (ms) for burn rates"),
-        ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1% error budget)"),
+        ("slo-target", d.slo_target, "TTFT SLO objective for burn rates (0.99 = 1%% error budget)"),
         ("otlp-receiver-bind", d.otlp_receiver_bind, "OTLP/HTTP /v1/traces receiver feeding the span ring (gpu engine)"),
         ("halo-ms", d.halo_ms, "gpu engine: records this close to a window's end also join the next window (0 = off)"),
         ("state-dir", d.state_dir, "gpu engine: checkpoint directory for the learned state (resumed on start)"),

@@ -204,3 +204,35 @@ def test_agent_gpu_hw_queues_flag_wins_over_env_default_does_not(monkeypatch):
     monkeypatch.delenv("GPU_MAX_HW_QUEUES")
     agent_cli.parse([])
     assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
+
+
+# REF's flag surface per binary (cmd/agent/main.go:334-373, cmd/collector/main.go:25-41,
+# cmd/attributor/main.go:53-69, cmd/m5gate/main.go:22-39): every flag is accepted and documented
+REF_FLAGS = {
+    agent: "--cluster --namespace --workload --service --k8s-node --pod --container --scenario --count --interval-ms "
+           "--event-kind --output --output-path --otlp-endpoint --otlp-timeout-ms --webhook-url --webhook-secret "
+           "--webhook-format --webhook-timeout-ms --capability-mode --disable-signals --disable-overhead-guard "
+           "--config --enable-hello-tracer --hello-target-comm --enable-real-probe-metrics --metrics-bind --probe-smoke",
+    collector: "--input --output --output-path --otlp-endpoint --otlp-timeout-ms --cluster --namespace --workload "
+               "--service --k8s-node --scenario --count --interval-ms",
+    attributor: "--input --out --summary-out --confusion-out --schema --config --attribution-mode --webhook-enabled "
+                "--webhook-url --webhook-secret --webhook-format --webhook-timeout-ms --webhook-strict",
+    benchgen: "--out --scenario --workload --input --attribution-mode",
+    faultreplay: "--scenario --count --out",
+    faultinject: "--scenario --count --out --cluster --namespace --workload --service --node",
+    correlationeval: "--input --out --predictions-out --window-ms --threshold --min-precision --min-recall",
+    m5gate: "--candidate-root --baseline-root --baseline-manifest --candidate-ref --candidate-commit "
+            "--require-baseline-manifest --scenarios --max-overhead-pct --max-variance-pct --min-runs "
+            "--ttft-regression-pct --alpha --bootstrap-iters --seed --min-samples --min-cliffs-delta --out-json --out-md",
+    loadgen: "--profile --duration-sec --rps --seed --out",
+}
+
+
+@pytest.mark.parametrize("mod", list(REF_FLAGS), ids=lambda m: m.__name__.rsplit(".", 1)[-1])
+def test_help_lists_refs_flags(mod, capsys):
+    """`--help` renders (a '%' in a help string once broke the agent's) and names REF's flags."""
+    with pytest.raises(SystemExit) as e:
+        mod.main(["--help"])
+    assert e.value.code == 0
+    out = capsys.readouterr().out
+    assert [f for f in REF_FLAGS[mod].split() if f not in out] == []
