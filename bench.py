@@ -543,12 +543,15 @@ def main() -> int:
     last = None
     kernel_recs = 0
     collected = []
+    c0, cw0 = core.collect_s, core.collect_wait_s
     for j in range(a.warmup, a.warmup + a.steps):
         rep = core.window(next_cut(), a.services, labels=imgs[j % len(imgs)].labels)
         if rank == 0:
             collected.extend(rep["prevs"])
         last = rep["k"]
         kernel_recs += rep["staged"]["n_kernel"]
+    loop_s = time.perf_counter() - t0  # the timed steps' host loop, before the final drain
+    coll_s, coll_wait_s = core.collect_s - c0, core.collect_wait_s - cw0
     fin = core.stop()  # the last window's results (drains the source)
     sync()
     if pg is not None:
@@ -725,6 +728,11 @@ def main() -> int:
         # the controller's per-window epilogue on rank 0, inside the timed region (agent/daemon.py
         # Agent._emit_window over the node-wide results the worker path collected)
         "host_epilogue_us_per_window": round(1e6 * epi[0] / max(epi[1], 1), 1),
+        # the worker's host loop per timed step: all of it, collecting finished windows (packet and
+        # results reads), and of that the time blocked waiting for a window's chain to finish
+        "host_loop_us_per_step": round(1e6 * loop_s / max(a.steps, 1), 1),
+        "host_collect_us_per_step": round(1e6 * coll_s / max(a.steps, 1), 1),
+        "host_collect_wait_us_per_step": round(1e6 * coll_wait_s / max(a.steps, 1), 1),
         "attributions_emitted_timed": int(attributions_emitted),
         "topology": (f"agent --gpus {world}: one window worker per GPU on split rings (its own kernel / user-space / "
                      f"span rings, producers routing by service), agent/worker.py WorkerCore.window per step, "

@@ -165,6 +165,7 @@ class WorkerCore:
             self.pipe.eng.set_pods(*spec.pods)
         self.pending: Deque[Tuple[int, float, int]] = collections.deque()
         self.windows = 0
+        self.collect_s = self.collect_wait_s = 0.0  # host time collecting finished windows / waiting for them
 
     @classmethod
     def adopt(cls, spec: WorkerSpec, pipe, src) -> "WorkerCore":
@@ -175,6 +176,7 @@ class WorkerCore:
         core.rings = (src.ring, src.user_ring, src.span_ring)
         core.pending = collections.deque()
         core.windows = 0
+        core.collect_s = core.collect_wait_s = 0.0
         return core
 
     @property
@@ -209,7 +211,17 @@ class WorkerCore:
 
     def _collect(self, k: int, host_us: float, n_groups: int) -> dict:
         pipe = self.pipe
+        t0 = time.perf_counter()
         pipe.wait(k)
+        t1 = time.perf_counter()
+        self.collect_wait_s += t1 - t0
+        try:
+            return self._read(k, host_us, n_groups)
+        finally:
+            self.collect_s += time.perf_counter() - t0
+
+    def _read(self, k: int, host_us: float, n_groups: int) -> dict:
+        pipe = self.pipe
         pk = np.asarray(pipe.eng.packet(k), dtype=np.float64)
         d = {"k": k, "ring": pk[-RING_TAIL:].copy(), "host_us": host_us, "latency_ms": float(pipe.window_ms(k)[0])}
         if self.spec.rank == 0:  # the node-wide packet and every worker's incidents (all-gathered)
