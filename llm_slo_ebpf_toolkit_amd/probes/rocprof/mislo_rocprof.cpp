@@ -66,9 +66,10 @@
 // 4x: a link already degraded when the process starts is not its own baseline),
 // MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_OCC_MS, MISLO_FOREIGN_MIN_SAMPLES (default 3 idle
 // samples per interval), MISLO_KFD_PROC (default /sys/class/kfd/kfd/proc), MISLO_WAIT_NEEDS_FOREIGN
-// (default 1: with KFD occupancy readable, a dispatch wait is emitted only if another process held
-// waves on the GPU during it -- a CPU-starved process's kernels wait behind its own host-staged
-// copies and barriers too; 0 = every wait above the floor), MISLO_ROCPROF_VERBOSE.
+// (default 1: where KFD's process directory exists, a dispatch wait is emitted only if a reading
+// saw another process hold waves on the GPU during it, none before the first reading -- a
+// CPU-starved process's kernels wait behind its own host-staged copies and barriers too; 0 =
+// every wait above the floor), MISLO_ROCPROF_VERBOSE.
 #include <rocprofiler-sdk/buffer.h>
 #include <rocprofiler-sdk/buffer_tracing.h>
 #include <rocprofiler-sdk/callback_tracing.h>
@@ -208,6 +209,7 @@ struct State {
   std::map<uint64_t, Occ> occ;
   uint64_t foreign_ms = 100, foreign_floor_pct = 10, occ_ms = 10, foreign_min_samples = 3;
   bool wait_needs_foreign = true;
+  bool kfd_dir = false;  // the KFD process directory is there: occupancy can confirm waits
   std::string kfd_proc = "/sys/class/kfd/kfd/proc";
   std::string pci_sysfs = "/sys/bus/pci/devices";
   uint64_t hbm_sample_ms = 1000;
@@ -702,7 +704,10 @@ void dispatch_callback(rocprofiler_callback_tracing_record_t rec, rocprofiler_us
     {
       std::lock_guard<std::mutex> lk(g.mu);
       auto oi = g.occ.find(d->dispatch_info.agent_id.handle);
-      if (oi != g.occ.end() && g.foreign_ms && g.wait_needs_foreign && oi->second.readable) {
+      // gated as soon as KFD's process directory exists, before the first reading: a wait with no
+      // reading of foreign waves behind it is not emitted (a CPU-starved process's sampler thread
+      // may not have read once yet -- it shares the starved CPU)
+      if (oi != g.occ.end() && g.foreign_ms && g.wait_needs_foreign && (oi->second.readable || g.kfd_dir)) {
         occ = &oi->second;
         gated = true;
         last_foreign = occ->last_foreign;
@@ -825,6 +830,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.foreign_min_samples = env_u64("MISLO_FOREIGN_MIN_SAMPLES", 3);
   g.wait_needs_foreign = env_u64("MISLO_WAIT_NEEDS_FOREIGN", 1) != 0;
   if (const char* kp = std::getenv("MISLO_KFD_PROC")) g.kfd_proc = kp;
+  g.kfd_dir = access(g.kfd_proc.c_str(), R_OK | X_OK) == 0;
   rocprofiler_query_available_agents(ROCPROFILER_AGENT_INFO_VERSION_0, agents_cb, sizeof(rocprofiler_agent_v0_t),
                                      nullptr);
   timespec rt{};

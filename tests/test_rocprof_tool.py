@@ -293,6 +293,40 @@ print("waits", ok.value, no.value, flush=True)
 
 
 @pytest.mark.gpu
+def _kfd_waves():
+    """{KFD process entry: waves it holds on the GPUs} over /sys/class/kfd (every process)."""
+    import glob
+
+    out = {}
+    for f in glob.glob("/sys/class/kfd/kfd/proc/*/stats_*/cu_occupancy"):
+        try:
+            with open(f) as fh:
+                v = int(fh.read().strip() or 0)
+        except (OSError, ValueError):
+            continue
+        pid = f.split("/")[5]
+        out[pid] = out.get(pid, 0) + v
+    return out
+
+
+def _wait_gpu_quiet(timeout=20.0, settle=1.0):
+    """Until no process holds waves on the GPU for `settle` s (an earlier test's workload may still
+    be draining): this test is about the process alone on the GPU. Returns the last reading."""
+    t_end = time.monotonic() + timeout
+    quiet_since = None
+    w = _kfd_waves()
+    while time.monotonic() < t_end:
+        w = _kfd_waves()
+        if sum(w.values()) == 0:
+            quiet_since = quiet_since or time.monotonic()
+            if time.monotonic() - quiet_since >= settle:
+                return w
+        else:
+            quiet_since = None
+        time.sleep(0.05)
+    return w
+
+
 def test_cpu_starved_process_waits_are_not_gpu_contention():
     """A service starved of CPU (burners on its CPU) alone on the GPU: its kernels can start late
     behind its own host-staged copies and barriers, but no other process holds waves, so no
@@ -302,6 +336,8 @@ def test_cpu_starved_process_waits_are_not_gpu_contention():
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
+    quiet = _wait_gpu_quiet()
+    assert sum(quiet.values()) == 0, f"other processes keep waves on the GPU: {quiet}"
     name = f"/mislo-test-{os.getpid()}-starved"
     ring = rt.HostRing(1 << 16, 64, name)
     cpu = sorted(os.sched_getaffinity(0))[0]
@@ -332,7 +368,8 @@ def test_cpu_starved_process_waits_are_not_gpu_contention():
     recs = np.concatenate([np.frombuffer(view[i * 64:(i + c) * 64].tobytes(), dtype=records.EVENT)
                            for _, i, c in segs]) if segs else np.zeros(0, dtype=records.EVENT)
     q = recs[recs["signal_type"] == 13]
-    assert len(q) == 0, (waits, np.sort(q["value"])[-10:])
+    assert len(q) == 0, (waits, np.sort(q["value"])[-10:], [ln for ln in err.splitlines() if "occupancy" in ln],
+                         _kfd_waves())
 
 
 FOREIGN_WORKLOAD = r"""
