@@ -63,7 +63,7 @@ case "${1:-reentry}" in
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
        "700|c2_7b|python -u tools/config2_evidence.py --out gpurun_out/r4_config2_7b" ;;
   overhead)
-    $S "200|agent_oh|python -u tools/agent_overhead.py --rate 1e6 --seconds 20 --out gpurun_out/r3_agent_overhead_1Mevs.json" ;;
+    $S "200|agent_oh|python -u tools/agent_overhead.py --rate 1e6 --seconds 20 --out gpurun_out/r4_agent_overhead_1Mevs.json" ;;
   config3)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3 ${2:-}" ;;
   buffers)  # windows in flight: the copy of window k waits for window k - buffers + 1's results
