@@ -32,7 +32,7 @@ from __future__ import annotations
 import os
 import threading
 import time
-from typing import Callable, Dict, Iterable, Optional, Tuple
+from typing import Callable, Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
 
@@ -107,6 +107,12 @@ STEAL_FLOOR_MILLI = 20000
 # ~1 of 30 intervals, one at a time (5 cpu_throttle false positives in 15 baseline windows,
 # profiles/r4_config3_gated), while a starved service stays above it in every interval
 STEAL_SUSTAIN = 3
+# ... and, for a pod on a small CPU set (at most STEAL_FOREIGN_MAX_CPUS), only while other processes
+# kept at least this share of those CPUs busy: after a CPU fault a pod working off its backlog waits
+# behind its own threads (6 of 8 recovery windows read cpu_throttle in one config-3 run,
+# profiles/r4_config3_rerun)
+STEAL_FOREIGN_MILLI = 25000
+STEAL_FOREIGN_MAX_CPUS = 32
 SIGNAL_TYPES = {"runqueue_delay_ms": RUNQUEUE_TYPE, "cpu_steal_pct": STEAL_TYPE,
                 "mem_reclaim_latency_ms": MEM_RECLAIM_TYPE, "cfs_throttled_ms": CFS_TYPE}
 ALL_MASK = sum(1 << t for t in SIGNAL_TYPES.values())
@@ -118,6 +124,45 @@ def _read(path: str) -> Optional[str]:
             return fh.read()
     except OSError:
         return None
+
+
+def cpu_list(text: str) -> List[int]:
+    """"0-3,8,10-11" -> [0, 1, 2, 3, 8, 10, 11]."""
+    out: List[int] = []
+    for part in text.replace(" ", "").split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        try:
+            lo = int(a)
+            hi = int(b) if b else lo
+        except ValueError:
+            break
+        out.extend(range(lo, min(hi, 65535) + 1))
+    return out
+
+
+def allowed_cpus(pid: int, proc_root: str = "/proc") -> List[int]:
+    """Cpus_allowed_list of /proc/<pid>/status ([] = unreadable)."""
+    text = _read(os.path.join(proc_root, str(pid), "status")) or ""
+    for ln in text.splitlines():
+        if ln.startswith("Cpus_allowed_list:"):
+            return cpu_list(ln.split(":", 1)[1].strip())
+    return []
+
+
+def cpu_busy_jiffies(proc_root: str = "/proc") -> Dict[int, int]:
+    """Busy jiffies per CPU from /proc/stat: every field but idle and iowait."""
+    out: Dict[int, int] = {}
+    for ln in (_read(os.path.join(proc_root, "stat")) or "").splitlines():
+        if ln.startswith("cpu") and len(ln) > 3 and ln[3].isdigit():
+            f = ln.split()
+            try:
+                v = [int(x) for x in f[1:9]] + [0] * 8
+            except ValueError:
+                continue
+            out[int(f[0][3:])] = v[0] + v[1] + v[2] + v[5] + v[6] + v[7]
+    return out
 
 
 def cgroup_files(pid: int, proc_root: str = "/proc", cgroup_root: str = "/sys/fs/cgroup",
@@ -201,17 +246,21 @@ class SchedstatSampler:
     def __init__(self, targets: Callable[[], Dict[int, int]], push: Callable[[np.ndarray], int], rec: int = 24,
                  proc_root: str = "/proc", floor_ns: int = FLOOR_NS, node_id: int = 0,
                  cgroup_root: str = "/sys/fs/cgroup", cpu_psi: bool = False,
-                 steal_floor_milli: int = STEAL_FLOOR_MILLI, steal_sustain: int = STEAL_SUSTAIN):
+                 steal_floor_milli: int = STEAL_FLOOR_MILLI, steal_sustain: int = STEAL_SUSTAIN,
+                 steal_foreign_milli: int = STEAL_FOREIGN_MILLI, steal_foreign_max_cpus: int = STEAL_FOREIGN_MAX_CPUS):
         """``targets()`` -> {pid: pod id}; ``push(records)`` -> records accepted (the user ring)."""
         self.targets, self.push, self.rec = targets, push, int(rec)
         self.proc_root, self.floor_ns, self.node_id = proc_root, int(floor_ns), int(node_id)
         self.cgroup_root, self.cpu_psi, self.steal_floor = cgroup_root, bool(cpu_psi), int(steal_floor_milli)
         self.steal_sustain = max(1, int(steal_sustain))
+        self.steal_foreign, self.steal_foreign_max_cpus = int(steal_foreign_milli), int(steal_foreign_max_cpus)
+        self._cpu_busy: Optional[Dict[int, int]] = None
+        self.steal_gated = 0
         self._steal_run: Dict[int, int] = {}  # pid -> consecutive intervals at the floor
         self.mask = ALL_MASK
         self.paused = False
-        self._prev: Dict[Tuple[int, int], Tuple[int, int]] = {}
-        self._procs: Dict[int, Tuple[int, str, str, str]] = {}  # pid -> (ns pid, cfs, mem, cpu psi files)
+        self._prev: Dict[Tuple[int, int], Tuple[int, int, int]] = {}  # (pid, tid) -> (run, wait, slices)
+        self._procs: Dict[int, tuple] = {}  # pid -> (ns pid, cfs, mem, cpu psi files, allowed CPUs)
         self._groups: Dict[str, int] = {}                      # file -> last reading (ns)
         self._prev_mono: Optional[int] = None
         self.samples = self.emitted = self.dropped = 0
@@ -240,41 +289,76 @@ class SchedstatSampler:
         dt = mono - self._prev_mono if self._prev_mono is not None and mono > self._prev_mono else 0
         self._prev_mono = mono
         rows = []
-        nxt: Dict[Tuple[int, int], Tuple[int, int]] = {}
-        live: Dict[int, Tuple[int, str, str, str]] = {}
+        nxt: Dict[Tuple[int, int], Tuple[int, int, int]] = {}
+        live: Dict[int, tuple] = {}
         cache: Dict[str, int] = {}
+        obs = []  # pass 1: (pid, pod, w_sum, s_sum, w_all, r_all)
         for pid, pod in self.targets().items():
             task = os.path.join(self.proc_root, str(pid), "task")
             try:
                 tids = sorted(int(t) for t in os.listdir(task) if t.isdigit())
             except OSError:
                 continue
-            w_sum = s_sum = w_all = 0
+            w_sum = s_sum = w_all = r_all = 0
             for tid in tids:
                 st = read_schedstat(os.path.join(task, str(tid), "schedstat"))
                 if st is None:
                     continue
                 key = (pid, tid)
-                nxt[key] = (st[1], st[2])
+                nxt[key] = (st[0], st[1], st[2])
                 prev = self._prev.get(key)
                 if prev is None:
                     continue
-                dw, ds = max(0, st[1] - prev[0]), max(0, st[2] - prev[1])
+                dr, dw, ds = max(0, st[0] - prev[0]), max(0, st[1] - prev[1]), max(0, st[2] - prev[2])
+                r_all += dr
                 w_all += dw
                 if ds > 0 and dw >= self.floor_ns * ds:  # this thread's waits reach the floor
                     w_sum += dw
                     s_sum += ds
             info = self._procs.get(pid)
             if info is None:
-                info = (ns_pid(pid, self.proc_root),) + cgroup_files(pid, self.proc_root, self.cgroup_root, self.cpu_psi)
+                info = ((ns_pid(pid, self.proc_root),) + cgroup_files(pid, self.proc_root, self.cgroup_root, self.cpu_psi)
+                        + (allowed_cpus(pid, self.proc_root),))
             live[pid] = info
-            npid, cfs, mem, cpu = info
+            obs.append((pid, pod, w_sum, s_sum, w_all, r_all))
+        # neighbours' load on each pod's CPUs (runtime/csrc/procsampler.cpp tick): busy time of the
+        # pod's CPU set less its own on-CPU time, milli-percent of the set's capacity; -1 = not gated
+        busy = cpu_busy_jiffies(self.proc_root)
+        foreign: Dict[int, int] = {}
+        if self.steal_foreign and self.mask >> STEAL_TYPE & 1:
+            sets: Dict[int, set] = {}
+            own: Dict[int, int] = {}
+            unknown = set()
+            for pid, pod, _, _, _, r_all in obs:
+                cpus = live[pid][4]
+                if not cpus:
+                    unknown.add(pod)
+                sets.setdefault(pod, set()).update(cpus)
+                own[pod] = own.get(pod, 0) + r_all
+            ns_per_jiffy = 1e9 / float(max(1, os.sysconf("SC_CLK_TCK")))
+            for pod, cs in sets.items():
+                ok = bool(busy) and self._cpu_busy is not None and dt > 0 and pod not in unknown
+                ok = ok and all(c in busy and c in self._cpu_busy for c in cs)
+                if not ok or not cs or len(cs) > self.steal_foreign_max_cpus:
+                    foreign[pod] = -1
+                    continue
+                jif = sum(max(0, busy[c] - self._cpu_busy[c]) for c in cs)
+                f = max(0.0, float(jif) * ns_per_jiffy - float(own[pod]))
+                foreign[pod] = int(f * 100000.0 / (float(dt) * float(len(cs))))
+        if busy:
+            self._cpu_busy = busy
+        for pid, pod, w_sum, s_sum, w_all, _ in obs:  # pass 2: the records, in watch order
+            npid, cfs, mem, cpu, _ = live[pid]
             if self.mask >> RUNQUEUE_TYPE & 1 and s_sum and w_sum // s_sum >= self.floor_ns:
                 rows.append((RUNQUEUE_TYPE, npid, pid, pod, w_sum // s_sum))
             psi_d = self._group_delta(cpu, 1, cache) if cpu else 0  # read every tick
             if self.mask >> STEAL_TYPE & 1 and dt:
                 milli = max(int(float(w_all) * 100000.0 / float(dt)), int(float(psi_d) * 100000.0 / float(dt)))
-                run = self._steal_run.get(pid, 0) + 1 if milli >= self.steal_floor else 0
+                at_floor = milli >= self.steal_floor
+                if at_floor and 0 <= foreign.get(pod, -1) < self.steal_foreign:
+                    at_floor = False  # the pod waited behind its own threads: no neighbour held its CPUs
+                    self.steal_gated += 1
+                run = self._steal_run.get(pid, 0) + 1 if at_floor else 0
                 self._steal_run[pid] = run
                 if run >= self.steal_sustain:
                     rows.append((STEAL_TYPE, npid, pid, pod, milli))
@@ -343,13 +427,15 @@ class NativeSampler:
     def __init__(self, ring, targets: Callable[[], Dict[int, int]], node_id: int = 0, proc_root: str = "/proc",
                  cgroup_root: str = "/sys/fs/cgroup", cpu_psi: bool = False, floor_ns: int = FLOOR_NS,
                  steal_floor_milli: int = STEAL_FLOOR_MILLI, refresh_s: float = 10.0,
-                 steal_sustain: int = STEAL_SUSTAIN):
+                 steal_sustain: int = STEAL_SUSTAIN, steal_foreign_milli: int = STEAL_FOREIGN_MILLI,
+                 steal_foreign_max_cpus: int = STEAL_FOREIGN_MAX_CPUS):
         from ..runtime import load
 
         rt = load()
         self.targets, self.refresh_s = targets, float(refresh_s)
         self.native = rt.ProcSampler(ring, node_id, proc_root, cgroup_root, bool(cpu_psi), int(floor_ns),
-                                     int(steal_floor_milli), int(floor_ns), int(floor_ns), int(steal_sustain))
+                                     int(steal_floor_milli), int(floor_ns), int(floor_ns), int(steal_sustain),
+                                     int(steal_foreign_milli), int(steal_foreign_max_cpus))
         self._stop = threading.Event()
         self._thr: Optional[threading.Thread] = None
 

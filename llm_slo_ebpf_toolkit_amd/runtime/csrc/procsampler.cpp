@@ -51,7 +51,59 @@ bool psi_some_us(const std::string& text, uint64_t* v) {
   return true;
 }
 
+// "0-3,8,10-11" -> {0, 1, 2, 3, 8, 10, 11}
+std::vector<uint32_t> cpu_list(const std::string& s) {
+  std::vector<uint32_t> out;
+  const char* p = s.c_str();
+  while (*p) {
+    while (*p == ' ' || *p == ',' || *p == '\t') ++p;
+    if (*p < '0' || *p > '9') break;
+    char* e = nullptr;
+    const unsigned long a = std::strtoul(p, &e, 10);
+    unsigned long b = a;
+    p = e;
+    if (*p == '-') b = std::strtoul(p + 1, &e, 10), p = e;
+    for (unsigned long c = a; c <= b && c < 65536; ++c) out.push_back((uint32_t)c);
+  }
+  return out;
+}
+
+// Cpus_allowed_list of /proc/<pid>/status (empty: unreadable)
+std::vector<uint32_t> allowed_cpus(const std::string& proc_root, uint32_t pid) {
+  std::string st;
+  if (!read_small(join(proc_root, std::to_string(pid) + "/status"), &st)) return {};
+  const size_t k = st.find("Cpus_allowed_list:");
+  if (k == std::string::npos) return {};
+  const size_t e = st.find('\n', k);
+  return cpu_list(st.substr(k + 18, (e == std::string::npos ? st.size() : e) - k - 18));
+}
+
 }  // namespace
+
+// Busy jiffies per CPU from /proc/stat (user nice system idle iowait irq softirq steal ...: all
+// but idle and iowait).
+bool ProcSampler::read_cpu_busy(std::vector<uint64_t>* out) {
+  out->clear();
+  std::string st;
+  if (!read_small(join(cfg_.proc_root, "stat"), &st)) return false;
+  size_t pos = 0;
+  while (pos < st.size()) {
+    size_t e = st.find('\n', pos);
+    if (e == std::string::npos) e = st.size();
+    if (e - pos > 4 && st.compare(pos, 3, "cpu") == 0 && st[pos + 3] >= '0' && st[pos + 3] <= '9') {
+      char* p = nullptr;
+      const unsigned long cpu = std::strtoul(st.c_str() + pos + 3, &p, 10);
+      uint64_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int i = 0; i < 8 && p < st.c_str() + e; ++i) f[i] = std::strtoull(p, &p, 10);
+      if (cpu < 65536) {
+        if (out->size() <= cpu) out->resize(cpu + 1, 0);
+        (*out)[cpu] = f[0] + f[1] + f[2] + f[5] + f[6] + f[7];
+      }
+    }
+    pos = e + 1;
+  }
+  return !out->empty();
+}
 
 ProcSampler::ProcSampler(Ring* ring, ProcSamplerConfig cfg) : ring_(ring), cfg_(std::move(cfg)) {}
 
@@ -106,6 +158,7 @@ void ProcSampler::set_targets(const std::vector<std::pair<uint32_t, uint32_t>>& 
 void ProcSampler::resolve(uint32_t pid, Proc& p) {
   p.resolved = true;
   p.ns_pid = ns_pid_of(cfg_.proc_root, pid);
+  p.cpus = allowed_cpus(cfg_.proc_root, pid);
   std::string cg;
   if (!read_small(join(cfg_.proc_root, std::to_string(pid) + "/cgroup"), &cg)) return;
   const std::string root = cfg_.cgroup_root;
@@ -191,7 +244,7 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
   const uint64_t dt = prev_mono_ && mono_ns > prev_mono_ ? mono_ns - prev_mono_ : 0;
   prev_mono_ = mono_ns;
   for (auto& kv : groups_) kv.second.seen = false;
-  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> next;
+  std::map<std::pair<uint32_t, uint32_t>, Tid> next;
   std::map<uint32_t, Proc> live;
   uint64_t cfs_groups = 0;
   auto rec = [&](uint16_t type, uint32_t ns_pid, uint32_t pid, uint32_t pod, uint64_t value) {
@@ -205,6 +258,12 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
     e.signal_type = type;
     out.push_back(e);
   };
+  // pass 1: every watched process's threads (run-queue wait, on-CPU time)
+  struct Obs {
+    uint32_t pid, pod;
+    uint64_t w_sum, s_sum, w_all, r_all;
+  };
+  std::vector<Obs> obs;
   for (const auto& tp : targets_) {
     const uint32_t pid = tp.first, pod = tp.second;
     if (live.count(pid)) continue;  // listed twice
@@ -217,7 +276,7 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
       close_tasks(pr);
       continue;
     }
-    uint64_t w_sum = 0, s_sum = 0, w_all = 0;
+    uint64_t w_sum = 0, s_sum = 0, w_all = 0, r_all = 0;
     for (const auto& tf : pr.task_fds) {
       const uint32_t tid = tf.first;
       char buf[128];
@@ -225,14 +284,15 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
       if (nr <= 0) continue;  // the thread exited (dropped at the next listing)
       buf[nr] = 0;
       char* p = nullptr;
-      std::strtoull(buf, &p, 10);
+      const uint64_t run = std::strtoull(buf, &p, 10);
       const uint64_t wait = std::strtoull(p, &p, 10), slices = std::strtoull(p, &p, 10);
       const auto key = std::make_pair(pid, tid);
-      next[key] = {wait, slices};
+      next[key] = Tid{run, wait, slices};
       auto it = prev_.find(key);
       if (it == prev_.end()) continue;
-      const uint64_t dw = wait >= it->second.first ? wait - it->second.first : 0;
-      const uint64_t ds = slices >= it->second.second ? slices - it->second.second : 0;
+      const uint64_t dw = wait >= it->second.wait ? wait - it->second.wait : 0;
+      const uint64_t ds = slices >= it->second.slices ? slices - it->second.slices : 0;
+      r_all += run >= it->second.run ? run - it->second.run : 0;
       w_all += dw;
       if (ds > 0 && dw >= cfg_.runq_floor_ns * ds) {  // this thread's waits reach the probe's floor
         w_sum += dw;
@@ -240,17 +300,74 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
       }
     }
     if (!pr.resolved) resolve(pid, pr);
-    if ((mask >> kSigRunq & 1) && s_sum && w_sum / s_sum >= cfg_.runq_floor_ns)
-      rec(kSigRunq, pr.ns_pid, pid, pod, w_sum / s_sum);
+    live[pid] = pr;
+    obs.push_back(Obs{pid, pod, w_sum, s_sum, w_all, r_all});
+  }
+  // neighbours' load on each pod's CPUs: /proc/stat busy time of the pod's CPU set less the pod's
+  // own on-CPU time, as a share of the set's capacity (milli-percent); -1: not gated
+  std::vector<uint64_t> busy;
+  const bool have_busy = read_cpu_busy(&busy);
+  const bool busy_delta = have_busy && cpu_busy_have_ && dt;
+  std::map<uint32_t, int64_t> foreign;  // pod -> milli-percent or -1
+  if (cfg_.steal_foreign_milli && (mask >> kSigSteal & 1)) {
+    std::map<uint32_t, std::pair<std::vector<bool>, uint64_t>> pods;  // pod -> (CPU set, on-CPU ns)
+    std::map<uint32_t, bool> unknown;
+    for (const Obs& o : obs) {
+      const Proc& pr = live[o.pid];
+      auto& e = pods[o.pod];
+      if (pr.cpus.empty()) unknown[o.pod] = true;
+      for (uint32_t c : pr.cpus) {
+        if (e.first.size() <= c) e.first.resize(c + 1, false);
+        e.first[c] = true;
+      }
+      e.second += o.r_all;
+    }
+    const double ns_per_jiffy = 1e9 / (double)std::max(1L, ::sysconf(_SC_CLK_TCK));
+    for (const auto& kv : pods) {
+      uint64_t n = 0, jif = 0;
+      bool ok = busy_delta && !unknown.count(kv.first);
+      for (size_t c = 0; ok && c < kv.second.first.size(); ++c) {
+        if (!kv.second.first[c]) continue;
+        ++n;
+        if (c >= busy.size() || c >= cpu_busy_.size()) {
+          ok = false;
+          break;
+        }
+        jif += busy[c] >= cpu_busy_[c] ? busy[c] - cpu_busy_[c] : 0;
+      }
+      if (!ok || n == 0 || n > cfg_.steal_foreign_max_cpus) {
+        foreign[kv.first] = -1;
+        continue;
+      }
+      const double busy_ns = (double)jif * ns_per_jiffy, own = (double)kv.second.second;
+      const double f = busy_ns > own ? busy_ns - own : 0.0;
+      foreign[kv.first] = (int64_t)(f * 100000.0 / ((double)dt * (double)n));
+    }
+  }
+  if (have_busy) {
+    cpu_busy_.swap(busy);
+    cpu_busy_have_ = true;
+  }
+  // pass 2: the records, per process in watch order
+  for (const Obs& o : obs) {
+    const uint32_t pid = o.pid, pod = o.pod;
+    Proc& pr = live[pid];
+    if ((mask >> kSigRunq & 1) && o.s_sum && o.w_sum / o.s_sum >= cfg_.runq_floor_ns)
+      rec(kSigRunq, pr.ns_pid, pid, pod, o.w_sum / o.s_sum);
     const uint64_t psi_d = pr.cpu_psi_file.empty() ? 0 : group_delta(pr.cpu_psi_file, 1);  // read every tick
     if ((mask >> kSigSteal & 1) && dt) {
-      uint64_t milli = (uint64_t)((double)w_all * 100000.0 / (double)dt);  // milli-percent of one CPU
+      uint64_t milli = (uint64_t)((double)o.w_all * 100000.0 / (double)dt);  // milli-percent of one CPU
       const uint64_t m2 = (uint64_t)((double)psi_d * 100000.0 / (double)dt);
       if (m2 > milli) milli = m2;
-      pr.steal_run = milli >= cfg_.steal_floor_milli ? pr.steal_run + 1 : 0;
+      bool at_floor = milli >= cfg_.steal_floor_milli;
+      const auto fit = foreign.find(pod);
+      if (at_floor && fit != foreign.end() && fit->second >= 0 && (uint64_t)fit->second < cfg_.steal_foreign_milli) {
+        at_floor = false;  // the pod waited behind its own threads: no neighbour held its CPUs
+        ++st_.steal_gated;
+      }
+      pr.steal_run = at_floor ? pr.steal_run + 1 : 0;
       if (pr.steal_run >= std::max<uint32_t>(1, cfg_.steal_sustain)) rec(kSigSteal, pr.ns_pid, pid, pod, milli);
     }
-    live[pid] = pr;
     if (!pr.cfs_file.empty()) {
       ++cfs_groups;
       const uint64_t d = group_delta(pr.cfs_file, 0);

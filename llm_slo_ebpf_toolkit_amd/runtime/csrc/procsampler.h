@@ -19,7 +19,12 @@
 //                              EEVDF a starved thread waits a short time per wakeup but most of the
 //                              interval in total, so this fires where the per-wakeup mean does not.
 //                              Emitted once the share has stayed at the floor for steal_sustain
-//                              intervals in a row: a service's own threads spike past it now and then
+//                              intervals in a row: a service's own threads spike past it now and then.
+//                              Where the pod runs on a small CPU set (Cpus_allowed_list of at most
+//                              steal_foreign_max_cpus), the wait counts only while other processes
+//                              kept those CPUs busy (/proc/stat busy time minus the pod's own on-CPU
+//                              time, at least steal_foreign_milli of their capacity): a pod catching
+//                              up on its own backlog waits behind its own threads, not a neighbour
 //   type 7  mem_reclaim_latency_ms  PSI memory stall of the process's group over the interval
 //   type 12 cfs_throttled_ms   CFS bandwidth throttling of the process's quota group over the interval
 //
@@ -52,6 +57,8 @@ struct ProcSamplerConfig {
   uint64_t cfs_floor_ns = 100000;
   uint64_t mem_floor_ns = 100000;
   bool cgroup_cpu_psi = false;        // cpu_steal_pct = max(wait share, the group's cpu.pressure share)
+  uint64_t steal_foreign_milli = 25000;  // neighbours' share of the pod's CPUs a wait needs (0: no gate)
+  uint32_t steal_foreign_max_cpus = 32;  // pods on larger CPU sets are not gated (node-wide load says little)
 };
 
 constexpr uint16_t kSigRunq = 3, kSigSteal = 6, kSigMem = 7, kSigCfs = 12;
@@ -61,6 +68,7 @@ struct ProcSamplerStats {
   uint64_t ticks = 0, emitted = 0, dropped = 0, targets = 0, last_tick_ns = 0, max_tick_ns = 0;
   uint64_t by_type[4] = {0, 0, 0, 0};  // runq, steal, mem, cfs
   uint64_t cfs_groups = 0;             // quota groups found for the targets (0: throttling unobservable)
+  uint64_t steal_gated = 0;            // intervals a wait share at the floor was not counted (no neighbour load)
 };
 
 class ProcSampler {
@@ -98,6 +106,10 @@ class ProcSampler {
     uint64_t listed_ns = 0;
     bool listed = false;
     std::string cfs_file, mem_file, cpu_psi_file;  // empty: none
+    std::vector<uint32_t> cpus;  // Cpus_allowed_list (empty: unknown)
+  };
+  struct Tid {  // a thread's last schedstat reading
+    uint64_t run = 0, wait = 0, slices = 0;
   };
   void resolve(uint32_t pid, Proc& p);
   void list_tasks(uint32_t pid, Proc& p, uint64_t mono_ns);
@@ -109,7 +121,10 @@ class ProcSampler {
   ProcSamplerConfig cfg_;
   std::mutex mu_;  // targets_, state, stats
   std::vector<std::pair<uint32_t, uint32_t>> targets_;
-  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint64_t, uint64_t>> prev_;  // (pid, tid) -> (wait, slices)
+  std::map<std::pair<uint32_t, uint32_t>, Tid> prev_;  // (pid, tid) -> last reading
+  std::vector<uint64_t> cpu_busy_;                   // /proc/stat busy jiffies per CPU, last tick
+  bool cpu_busy_have_ = false;
+  bool read_cpu_busy(std::vector<uint64_t>* out);
   std::map<uint32_t, Proc> procs_;
   std::map<std::string, Group> groups_;
   uint64_t prev_mono_ = 0;

@@ -459,7 +459,8 @@ class PyProcSampler {
  public:
   PyProcSampler(HostRing* ring, uint32_t node_id, const std::string& proc_root, const std::string& cgroup_root,
                 bool cgroup_cpu_psi, uint64_t runq_floor_ns, uint64_t steal_floor_milli, uint64_t cfs_floor_ns,
-                uint64_t mem_floor_ns, uint32_t steal_sustain) {
+                uint64_t mem_floor_ns, uint32_t steal_sustain, uint64_t steal_foreign_milli,
+                uint32_t steal_foreign_max_cpus) {
     ProcSamplerConfig c;
     c.node_id = node_id;
     c.proc_root = proc_root;
@@ -470,6 +471,8 @@ class PyProcSampler {
     c.cfs_floor_ns = cfs_floor_ns;
     c.mem_floor_ns = mem_floor_ns;
     c.steal_sustain = steal_sustain;
+    c.steal_foreign_milli = steal_foreign_milli;
+    c.steal_foreign_max_cpus = steal_foreign_max_cpus;
     s_ = std::make_unique<ProcSampler>(ring ? ring->ring() : nullptr, c);
   }
   void set_targets(const std::map<uint32_t, uint32_t>& pid_pod) {
@@ -511,6 +514,7 @@ class PyProcSampler {
     d["mem_reclaim_latency_ms"] = st.by_type[2];
     d["cfs_throttled_ms"] = st.by_type[3];
     d["cfs_groups"] = st.cfs_groups;
+    d["steal_gated"] = st.steal_gated;
     return d;
   }
 
@@ -798,11 +802,12 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def_property("paused", &PyGpuSampler::paused, &PyGpuSampler::set_paused);
   py::class_<PyProcSampler>(m, "ProcSampler")
       .def(py::init<HostRing*, uint32_t, const std::string&, const std::string&, bool, uint64_t, uint64_t, uint64_t,
-                    uint64_t, uint32_t>(),
+                    uint64_t, uint32_t, uint64_t, uint32_t>(),
            py::arg("ring"), py::arg("node_id") = 0, py::arg("proc_root") = "/proc",
            py::arg("cgroup_root") = "/sys/fs/cgroup", py::arg("cgroup_cpu_psi") = false,
            py::arg("runq_floor_ns") = 100000, py::arg("steal_floor_milli") = 20000, py::arg("cfs_floor_ns") = 100000,
-           py::arg("mem_floor_ns") = 100000, py::arg("steal_sustain") = 3, py::keep_alive<1, 2>())
+           py::arg("mem_floor_ns") = 100000, py::arg("steal_sustain") = 3, py::arg("steal_foreign_milli") = 25000,
+           py::arg("steal_foreign_max_cpus") = 32, py::keep_alive<1, 2>())
       .def("set_targets", &PyProcSampler::set_targets)
       .def("set_target_list", &PyProcSampler::set_target_list)
       .def("tick", &PyProcSampler::tick, py::arg("wall_ns"), py::arg("mono_ns"))

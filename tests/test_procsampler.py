@@ -220,3 +220,44 @@ def test_ring_drop_mask_is_shared_with_attached_producers():
         assert peer.drop_mask == 1 << 13
     finally:
         del owner
+
+
+def test_steal_counts_only_while_neighbours_hold_the_pods_cpus(tmp_path):
+    """A pod pinned to CPUs 0-1: a wait share at the floor counts only while other processes kept
+    those CPUs busy (/proc/stat busy time less the pod's own on-CPU time, schedstat field 1): after
+    a CPU fault, a pod working off its backlog waits behind its own threads (profiles/r4_config3_rerun:
+    6 of 8 recovery windows read cpu_throttle). A pod on a large CPU set is not gated. Model and
+    native agree record for record."""
+    proc, cg, q = world(tmp_path)
+    tck = os.sysconf("SC_CLK_TCK")
+    (proc / "100" / "status").write_text("Name:\tpython\nNSpid:\t100\t17\nCpus_allowed_list:\t0-1\n")
+    (proc / "200" / "status").write_text("Name:\tsh\nNSpid:\t200\nCpus_allowed_list:\t0-63\n")
+    busy = [0] * 64
+
+    def stat():
+        lines = ["cpu  0 0 0 0 0 0 0 0 0 0"] + [f"cpu{c} {busy[c]} 0 0 1000 0 0 0 0 0 0" for c in range(64)]
+        (proc / "stat").write_text("\n".join(lines) + "\nintr 0\n")
+
+    stat()
+    targets = {100: 7, 200: 9}
+    m, n = model(proc, cg, targets), native(proc, cg, targets)
+    m.sample(T0, M0), nat_sample(n, T0, M0)
+    run, wait, run2, wait2 = 10, 1_000, 10, 0
+    got = []
+    # (pod 7's own on-CPU ms, CPU 0-1 busy ms each): neighbours held 70 %; then the pod alone
+    for i, (own_ms, cpu_ms) in enumerate([(60, 100), (60, 100), (190, 100), (195, 100)], start=1):
+        run += own_ms * 1_000_000
+        wait += 30_000_000  # 30 % of one CPU waited every interval
+        run2 += 1_000_000
+        wait2 += 50_000_000  # pod 9 (64 CPUs): never gated
+        schedstat(proc, 100, 100, run, wait, 10 * i + 1)
+        schedstat(proc, 200, 200, run2, wait2, 10 * i + 1)
+        for c in (0, 1):
+            busy[c] += cpu_ms * tck // 1000
+        stat()
+        t, mo = T0 + i * 10**8, M0 + i * 10**8
+        a, b = m.sample(t, mo), nat_sample(n, t, mo)
+        assert a.tobytes() == b.tobytes(), i
+        got.append({int(e["pod_id"]): int(e["value"]) for e in a if int(e["signal_type"]) == procfs.STEAL_TYPE})
+    assert got == [{7: 30_000, 9: 50_000}, {7: 30_000, 9: 50_000}, {9: 50_000}, {9: 50_000}], got
+    assert m.steal_gated == n.stats()["steal_gated"] == 2

@@ -292,7 +292,6 @@ print("waits", ok.value, no.value, flush=True)
 """
 
 
-@pytest.mark.gpu
 def _kfd_waves():
     """{KFD process entry: waves it holds on the GPUs} over /sys/class/kfd (every process)."""
     import glob
@@ -327,6 +326,7 @@ def _wait_gpu_quiet(timeout=20.0, settle=1.0):
     return w
 
 
+@pytest.mark.gpu
 def test_cpu_starved_process_waits_are_not_gpu_contention():
     """A service starved of CPU (burners on its CPU) alone on the GPU: its kernels can start late
     behind its own host-staged copies and barriers, but no other process holds waves, so no
