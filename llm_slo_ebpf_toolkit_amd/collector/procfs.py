@@ -255,6 +255,7 @@ class SchedstatSampler:
         self.steal_sustain = max(1, int(steal_sustain))
         self.steal_foreign, self.steal_foreign_max_cpus = int(steal_foreign_milli), int(steal_foreign_max_cpus)
         self._cpu_busy: Optional[Dict[int, int]] = None
+        self._cpu_busy_tick = -1
         self.steal_gated = 0
         self._steal_run: Dict[int, int] = {}  # pid -> consecutive intervals at the floor
         self.mask = ALL_MASK
@@ -321,9 +322,16 @@ class SchedstatSampler:
                         + (allowed_cpus(pid, self.proc_root),))
             live[pid] = info
             obs.append((pid, pod, w_sum, s_sum, w_all, r_all))
-        # neighbours' load on each pod's CPUs (runtime/csrc/procsampler.cpp tick): busy time of the
-        # pod's CPU set less its own on-CPU time, milli-percent of the set's capacity; -1 = not gated
-        busy = cpu_busy_jiffies(self.proc_root)
+        milli = []  # each process's wait share (milli-percent of one CPU; its cpu.pressure share if larger)
+        for pid, pod, _, _, w_all, _ in obs:
+            cpu = live[pid][3]
+            psi_d = self._group_delta(cpu, 1, cache) if cpu else 0  # read every tick
+            milli.append(max(int(float(w_all) * 100000.0 / float(dt)), int(float(psi_d) * 100000.0 / float(dt)))
+                         if dt else 0)
+        # neighbours' load on the CPUs of each pod pinned to a small set (runtime/csrc/procsampler.cpp
+        # tick): /proc/stat busy time of the set less the pod's own on-CPU time, milli-percent of the
+        # set's capacity; read only while such a pod waits at the floor (-2: no delta yet, unconfirmed;
+        # -1: not gated)
         foreign: Dict[int, int] = {}
         if self.steal_foreign and self.mask >> STEAL_TYPE & 1:
             sets: Dict[int, set] = {}
@@ -335,33 +343,38 @@ class SchedstatSampler:
                     unknown.add(pod)
                 sets.setdefault(pod, set()).update(cpus)
                 own[pod] = own.get(pod, 0) + r_all
-            ns_per_jiffy = 1e9 / float(max(1, os.sysconf("SC_CLK_TCK")))
             for pod, cs in sets.items():
-                ok = bool(busy) and self._cpu_busy is not None and dt > 0 and pod not in unknown
-                ok = ok and all(c in busy and c in self._cpu_busy for c in cs)
-                if not ok or not cs or len(cs) > self.steal_foreign_max_cpus:
-                    foreign[pod] = -1
-                    continue
-                jif = sum(max(0, busy[c] - self._cpu_busy[c]) for c in cs)
-                f = max(0.0, float(jif) * ns_per_jiffy - float(own[pod]))
-                foreign[pod] = int(f * 100000.0 / (float(dt) * float(len(cs))))
-        if busy:
-            self._cpu_busy = busy
-        for pid, pod, w_sum, s_sum, w_all, _ in obs:  # pass 2: the records, in watch order
+                foreign[pod] = -1 if pod in unknown or not cs or len(cs) > self.steal_foreign_max_cpus else -2
+            need = any(m >= self.steal_floor and foreign[o[1]] == -2 for m, o in zip(milli, obs))
+            if need:
+                busy = cpu_busy_jiffies(self.proc_root)
+                valid = bool(busy) and self._cpu_busy is not None and self._cpu_busy_tick + 1 == self.samples and dt > 0
+                ns_per_jiffy = 1e9 / float(max(1, os.sysconf("SC_CLK_TCK")))
+                for pod, cs in sets.items():
+                    if foreign[pod] != -2 or not valid or not all(c in busy and c in self._cpu_busy for c in cs):
+                        continue
+                    jif = sum(max(0, busy[c] - self._cpu_busy[c]) for c in cs)
+                    f = max(0.0, float(jif) * ns_per_jiffy - float(own[pod]))
+                    foreign[pod] = int(f * 100000.0 / (float(dt) * float(len(cs))))
+                self._cpu_busy = busy or None
+                self._cpu_busy_tick = self.samples
+            else:
+                self._cpu_busy = None
+        for i, (pid, pod, w_sum, s_sum, w_all, _) in enumerate(obs):  # pass 2: the records, in watch order
             npid, cfs, mem, cpu, _ = live[pid]
             if self.mask >> RUNQUEUE_TYPE & 1 and s_sum and w_sum // s_sum >= self.floor_ns:
                 rows.append((RUNQUEUE_TYPE, npid, pid, pod, w_sum // s_sum))
-            psi_d = self._group_delta(cpu, 1, cache) if cpu else 0  # read every tick
             if self.mask >> STEAL_TYPE & 1 and dt:
-                milli = max(int(float(w_all) * 100000.0 / float(dt)), int(float(psi_d) * 100000.0 / float(dt)))
-                at_floor = milli >= self.steal_floor
-                if at_floor and 0 <= foreign.get(pod, -1) < self.steal_foreign:
+                m = milli[i]
+                at_floor = m >= self.steal_floor
+                fg = foreign.get(pod, -1)
+                if at_floor and fg != -1 and (fg == -2 or fg < self.steal_foreign):
                     at_floor = False  # the pod waited behind its own threads: no neighbour held its CPUs
                     self.steal_gated += 1
                 run = self._steal_run.get(pid, 0) + 1 if at_floor else 0
                 self._steal_run[pid] = run
                 if run >= self.steal_sustain:
-                    rows.append((STEAL_TYPE, npid, pid, pod, milli))
+                    rows.append((STEAL_TYPE, npid, pid, pod, m))
             if cfs:
                 d = self._group_delta(cfs, 0, cache)
                 if self.mask >> CFS_TYPE & 1 and d >= self.floor_ns:

@@ -303,12 +303,22 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
     live[pid] = pr;
     obs.push_back(Obs{pid, pod, w_sum, s_sum, w_all, r_all});
   }
-  // neighbours' load on each pod's CPUs: /proc/stat busy time of the pod's CPU set less the pod's
-  // own on-CPU time, as a share of the set's capacity (milli-percent); -1: not gated
-  std::vector<uint64_t> busy;
-  const bool have_busy = read_cpu_busy(&busy);
-  const bool busy_delta = have_busy && cpu_busy_have_ && dt;
-  std::map<uint32_t, int64_t> foreign;  // pod -> milli-percent or -1
+  // each process's wait share this interval (milli-percent of one CPU; its group's cpu.pressure
+  // share where that is larger)
+  std::vector<uint64_t> milli(obs.size(), 0);
+  for (size_t i = 0; i < obs.size(); ++i) {
+    const Proc& pr = live[obs[i].pid];
+    const uint64_t psi_d = pr.cpu_psi_file.empty() ? 0 : group_delta(pr.cpu_psi_file, 1);  // read every tick
+    if (!dt) continue;
+    milli[i] = (uint64_t)((double)obs[i].w_all * 100000.0 / (double)dt);
+    const uint64_t m2 = (uint64_t)((double)psi_d * 100000.0 / (double)dt);
+    if (m2 > milli[i]) milli[i] = m2;
+  }
+  // neighbours' load on the CPUs of each pod pinned to a small set: /proc/stat busy time of the set
+  // less the pod's own on-CPU time, milli-percent of the set's capacity. Read only while such a pod
+  // waits at the floor (on a large host /proc/stat costs ~1 ms of kernel time per read), so the
+  // first interval at the floor has no delta yet and counts as unconfirmed (-2); -1: not gated.
+  std::map<uint32_t, int64_t> foreign;
   if (cfg_.steal_foreign_milli && (mask >> kSigSteal & 1)) {
     std::map<uint32_t, std::pair<std::vector<bool>, uint64_t>> pods;  // pod -> (CPU set, on-CPU ns)
     std::map<uint32_t, bool> unknown;
@@ -322,31 +332,42 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
       }
       e.second += o.r_all;
     }
-    const double ns_per_jiffy = 1e9 / (double)std::max(1L, ::sysconf(_SC_CLK_TCK));
+    bool need = false;
     for (const auto& kv : pods) {
-      uint64_t n = 0, jif = 0;
-      bool ok = busy_delta && !unknown.count(kv.first);
-      for (size_t c = 0; ok && c < kv.second.first.size(); ++c) {
-        if (!kv.second.first[c]) continue;
-        ++n;
-        if (c >= busy.size() || c >= cpu_busy_.size()) {
-          ok = false;
-          break;
-        }
-        jif += busy[c] >= cpu_busy_[c] ? busy[c] - cpu_busy_[c] : 0;
-      }
-      if (!ok || n == 0 || n > cfg_.steal_foreign_max_cpus) {
-        foreign[kv.first] = -1;
-        continue;
-      }
-      const double busy_ns = (double)jif * ns_per_jiffy, own = (double)kv.second.second;
-      const double f = busy_ns > own ? busy_ns - own : 0.0;
-      foreign[kv.first] = (int64_t)(f * 100000.0 / ((double)dt * (double)n));
+      const uint64_t n = (uint64_t)std::count(kv.second.first.begin(), kv.second.first.end(), true);
+      foreign[kv.first] = (unknown.count(kv.first) || n == 0 || n > cfg_.steal_foreign_max_cpus) ? -1 : -2;
     }
-  }
-  if (have_busy) {
-    cpu_busy_.swap(busy);
-    cpu_busy_have_ = true;
+    for (size_t i = 0; i < obs.size(); ++i)
+      if (milli[i] >= cfg_.steal_floor_milli && foreign[obs[i].pod] == -2) need = true;
+    if (need) {
+      std::vector<uint64_t> busy;
+      const bool have = read_cpu_busy(&busy);
+      const bool valid = have && cpu_busy_have_ && cpu_busy_tick_ + 1 == st_.ticks && dt;
+      const double ns_per_jiffy = 1e9 / (double)std::max(1L, ::sysconf(_SC_CLK_TCK));
+      for (const auto& kv : pods) {
+        if (foreign[kv.first] != -2 || !valid) continue;
+        uint64_t n = 0, jif = 0;
+        bool ok = true;
+        for (size_t c = 0; c < kv.second.first.size(); ++c) {
+          if (!kv.second.first[c]) continue;
+          ++n;
+          if (c >= busy.size() || c >= cpu_busy_.size()) {
+            ok = false;
+            break;
+          }
+          jif += busy[c] >= cpu_busy_[c] ? busy[c] - cpu_busy_[c] : 0;
+        }
+        if (!ok) continue;  // a CPU missing from /proc/stat: unconfirmed
+        const double busy_ns = (double)jif * ns_per_jiffy, own = (double)kv.second.second;
+        const double f = busy_ns > own ? busy_ns - own : 0.0;
+        foreign[kv.first] = (int64_t)(f * 100000.0 / ((double)dt * (double)n));
+      }
+      cpu_busy_.swap(busy);
+      cpu_busy_have_ = have;
+      cpu_busy_tick_ = st_.ticks;
+    } else {
+      cpu_busy_have_ = false;
+    }
   }
   // pass 2: the records, per process in watch order
   for (const Obs& o : obs) {
@@ -354,19 +375,17 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
     Proc& pr = live[pid];
     if ((mask >> kSigRunq & 1) && o.s_sum && o.w_sum / o.s_sum >= cfg_.runq_floor_ns)
       rec(kSigRunq, pr.ns_pid, pid, pod, o.w_sum / o.s_sum);
-    const uint64_t psi_d = pr.cpu_psi_file.empty() ? 0 : group_delta(pr.cpu_psi_file, 1);  // read every tick
     if ((mask >> kSigSteal & 1) && dt) {
-      uint64_t milli = (uint64_t)((double)o.w_all * 100000.0 / (double)dt);  // milli-percent of one CPU
-      const uint64_t m2 = (uint64_t)((double)psi_d * 100000.0 / (double)dt);
-      if (m2 > milli) milli = m2;
-      bool at_floor = milli >= cfg_.steal_floor_milli;
+      const uint64_t m = milli[&o - obs.data()];
+      bool at_floor = m >= cfg_.steal_floor_milli;
       const auto fit = foreign.find(pod);
-      if (at_floor && fit != foreign.end() && fit->second >= 0 && (uint64_t)fit->second < cfg_.steal_foreign_milli) {
+      if (at_floor && fit != foreign.end() && fit->second != -1 &&
+          (fit->second == -2 || (uint64_t)fit->second < cfg_.steal_foreign_milli)) {
         at_floor = false;  // the pod waited behind its own threads: no neighbour held its CPUs
         ++st_.steal_gated;
       }
       pr.steal_run = at_floor ? pr.steal_run + 1 : 0;
-      if (pr.steal_run >= std::max<uint32_t>(1, cfg_.steal_sustain)) rec(kSigSteal, pr.ns_pid, pid, pod, milli);
+      if (pr.steal_run >= std::max<uint32_t>(1, cfg_.steal_sustain)) rec(kSigSteal, pr.ns_pid, pid, pod, m);
     }
     if (!pr.cfs_file.empty()) {
       ++cfs_groups;

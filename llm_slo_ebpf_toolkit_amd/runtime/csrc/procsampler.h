@@ -124,6 +124,7 @@ class ProcSampler {
   std::map<std::pair<uint32_t, uint32_t>, Tid> prev_;  // (pid, tid) -> last reading
   std::vector<uint64_t> cpu_busy_;                   // /proc/stat busy jiffies per CPU, last tick
   bool cpu_busy_have_ = false;
+  uint64_t cpu_busy_tick_ = 0;                       // the tick that read cpu_busy_
   bool read_cpu_busy(std::vector<uint64_t>* out);
   std::map<uint32_t, Proc> procs_;
   std::map<std::string, Group> groups_;
