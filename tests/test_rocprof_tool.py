@@ -459,6 +459,8 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
+    quiet = _wait_gpu_quiet()  # the previous test's workload may still hold waves
+    assert sum(quiet.values()) == 0, f"other processes keep waves on the GPU: {quiet}"
     name = f"/mislo-test-{os.getpid()}-foreign"
     ring = rt.HostRing(1 << 16, 64, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000000",
@@ -513,7 +515,8 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
            "busy_skips": skips, "self_pid": self_pid, "idle_readings": idle_n, "busy_readings": busy_n,
            "share_saturated_median": float(np.median(sat)) if sat else None, "records_saturated": in_sat}
     print(res)
-    assert res["share_alone_p90"] < 0.10 and before <= 1, (res, alone[-12:])
+    early = [(round((int(t) - t_burn) / 1e6, 1), int(v) // 1_000_000) for t, v in zip(ts, big["value"]) if t < t_burn - 100_000_000]
+    assert res["share_alone_p90"] < 0.10 and before <= 1, (res, alone[-12:], early)
     assert res["share_gemm_median"] >= 0.5 and in_gemm >= 5, (res, gemm[:10])
     assert res["share_decode_median"] >= 0.5 and in_decode >= 5, (res, decode[:10])
     # a saturated server never idles: its own KFD entry, learned earlier, is left out of every reading
