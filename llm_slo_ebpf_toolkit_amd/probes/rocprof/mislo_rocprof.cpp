@@ -64,7 +64,8 @@
 // pair's starting rate before it has shown a large copy, default 64 GB/s: one xGMI link
 // direction; a pair's calibration starts there and a measured rate may only raise it, to at most
 // 4x: a link already degraded when the process starts is not its own baseline),
-// MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_OCC_MS, MISLO_FOREIGN_MIN_SAMPLES (default 3 idle
+// MISLO_FOREIGN_MS, MISLO_FOREIGN_FLOOR_PCT, MISLO_FOREIGN_MIN_HOT (default 2 readings with foreign waves
+// per interval), MISLO_OCC_MS, MISLO_FOREIGN_MIN_SAMPLES (default 3 idle
 // samples per interval), MISLO_KFD_PROC (default /sys/class/kfd/kfd/proc), MISLO_WAIT_NEEDS_FOREIGN
 // (default 1: where KFD's process directory exists, a dispatch wait is emitted only if a reading
 // saw another process hold waves on the GPU during it, none before the first reading -- a
@@ -207,7 +208,7 @@ struct State {
     uint32_t self_pid = 0;  // 0: not identified yet
   };
   std::map<uint64_t, Occ> occ;
-  uint64_t foreign_ms = 100, foreign_floor_pct = 10, occ_ms = 10, foreign_min_samples = 3;
+  uint64_t foreign_ms = 100, foreign_floor_pct = 10, occ_ms = 10, foreign_min_samples = 3, foreign_min_hot = 2;
   bool wait_needs_foreign = true;
   bool kfd_dir = false;  // the KFD process directory is there: occupancy can confirm waits
   std::string kfd_proc = "/sys/class/kfd/kfd/proc";
@@ -533,7 +534,9 @@ void foreign_tick(uint64_t now) {
     o.share = (double)hot / (double)clean;
     o.occ_mean = occ_sum / (double)clean;
     ++o.decisions;
-    if (o.share * 100.0 >= (double)g.foreign_floor_pct) {
+    // one hot reading is not evidence: a process alone on the GPU reads a few of its own waves as
+    // another's when they race its idle check (2 such intervals in ~60 of the foreign test's alone phase)
+    if (hot >= g.foreign_min_hot && o.share * 100.0 >= (double)g.foreign_floor_pct) {
       // an extended interval is reported as foreign_ms pieces, so the records keep the time
       // resolution the agent's join tiers need (pod + pid: 100 ms of the request span)
       const uint64_t step = g.foreign_ms * 1000000ull;
@@ -826,6 +829,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   g.hbm_sample_ms = env_u64("MISLO_HBM_SAMPLE_MS", 1000);
   g.foreign_ms = env_u64("MISLO_FOREIGN_MS", 100);
   g.foreign_floor_pct = env_u64("MISLO_FOREIGN_FLOOR_PCT", 10);
+  g.foreign_min_hot = env_u64("MISLO_FOREIGN_MIN_HOT", 2);
   g.occ_ms = std::max<uint64_t>(1, env_u64("MISLO_OCC_MS", 10));
   g.foreign_min_samples = env_u64("MISLO_FOREIGN_MIN_SAMPLES", 3);
   g.wait_needs_foreign = env_u64("MISLO_WAIT_NEEDS_FOREIGN", 1) != 0;
