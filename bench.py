@@ -25,11 +25,12 @@ One step = one collection window per GPU, exactly as the agent runs it:
     rings (the host touches no record) -> HIP graph: the probes' id definitions applied on the
     device (context rows, trace map) -> decode of framed + user-space records + histograms ->
     LDS hash join -> MFMA posterior + confusion -> MFMA sufficient statistics -> pack -> RCCL
-    all-reduce of the packet over xGMI (N > 1) -> on-device model refit (prequential,
-    random-init priors).
+    all-reduce of the packet over xGMI (N > 1). The attribution model is trained first (untimed,
+    on the device: MFMA sufficient statistics of labelled windows -> k_refit_nb) with REF's expert
+    likelihood table as its Beta prior, then frozen.
 
-Synthetic data: seeded fault-replay traces (pipeline/replay.py, REF fault profiles), random-init
-attribution priors; the kernel's record path is the native probe model (runtime/csrc/probesim.h).
+Synthetic data: seeded fault-replay traces (pipeline/replay.py, REF fault profiles plus the two
+REF domains REF's generator has no profile for); the kernel's record path is the native probe model (runtime/csrc/probesim.h).
 
     python bench.py --gpus N --steps K --warmup W
 """
@@ -69,12 +70,15 @@ def parse():
     ap.add_argument("--heldout", type=int, default=6,
                     help="held-out windows scored with the frozen model, cycling over " + ", ".join(HELDOUT_SCENARIOS))
     ap.add_argument("--model", default="bayes_learned", choices=("bayes", "bayes_learned"),
-                    help="bayes_learned: trained on the device (untimed) from random-init priors, then frozen; "
+                    help="bayes_learned: trained on the device (untimed) from labelled replay windows, then frozen; "
                          "bayes: REF's expert table")
     ap.add_argument("--train-windows", type=int, default=24,
                     help="labelled training windows (models/train.py TRAIN_SCENARIOS), every 4th held out for the "
                          "temperature fit")
     ap.add_argument("--train-events", type=int, default=65536, help="events per training window")
+    ap.add_argument("--prior", default="expert", choices=("expert", "random"),
+                    help="the learned likelihoods' Beta prior: REF's expert table (the shipped model's) or the seeded "
+                         "random-init table (both are scored on REF's 55 rows)")
     ap.add_argument("--train-spans", type=int, default=4096, help="spans per training window")
     ap.add_argument("--export-model", default="", help="write the trained model file (agent --model-path)")
     ap.add_argument("--hw-queues", type=int, default=0,
@@ -411,7 +415,7 @@ def main() -> int:
         r = src.stage(c, img.n_groups, img.labels, with_labels=with_labels, learn=learn)
         return r["k"], r
 
-    # ---- training (untimed): the learned model from random-init priors on the device --------
+    # ---- training (untimed): the learned model on the device -------------------------------
     # labelled windows through the same path (MFMA sufficient statistics with soft multi-fault
     # labels), every 4th held out; the temperature is fitted on the held-out incidents, then the
     # device refits the model with it (k_refit_nb) and the model is frozen for everything below
@@ -438,7 +442,7 @@ def main() -> int:
         st = arrays["stats_acc"]  # node-wide already: every window's packet is all-reduced
         stats = SufficientStats(count=st[1024:1024 + 10].copy(), elevated_sum=st[:1024].reshape(32, 32)[:16, :10].copy(),
                                 x_sum=st[:1024].reshape(32, 32)[16:, :10].copy(), xx=st[:1024].reshape(32, 32)[16:, 16:].copy())
-        tcfg = mtrain.TrainConfig(seed=a.seed)
+        tcfg = mtrain.TrainConfig(seed=a.seed, init=a.prior)
         base = NaiveBayes_learned(stats, tcfg)
         hf, hc = np.concatenate(hold_f), np.concatenate(hold_c)
         if pg is not None:  # the held-out incidents of every rank: one temperature node-wide
@@ -457,7 +461,9 @@ def main() -> int:
         # the image carries the pair structure (members, rho); the device refit rebuilds every
         # table from the all-reduced statistics with the fitted temperature
         pipe.eng.restore(st, model_bytes(model), int(pipe.windows_folded))
-        pipe.eng.set_refit(tcfg.alpha, tcfg.prior_pseudo, 1.0 / T, tcfg.min_count)
+        kw = mtrain.learned_kwargs(tcfg)
+        pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"])
+        pipe.eng.set_refit(tcfg.alpha, tcfg.prior_pseudo, 1.0 / T, tcfg.min_count, pipe.cap_dom())
         pipe.eng.refit_now()
         pipe.eng.set_device_refit(False)  # frozen from here on: the timed region scores, as the agent does
         pipe.device_refit = False
@@ -469,10 +475,15 @@ def main() -> int:
             "events_per_window": a.train_events, "scenarios": list(mtrain.TRAIN_SCENARIOS), "seed": a.seed,
             "active_domains": [d for i, d in enumerate(catalog_domains()) if np.isfinite(model.bias[i])]})
         train_info = {"windows": len(train_imgs), "held_out": len(hold_f), "temperature": round(T, 4),
+                      "likelihood_prior": tcfg.init, "alpha": tcfg.alpha, "unknown_calibrated": tcfg.calibrate_unknown,
                       "pair_rho": round(rho, 4),
                       "holdout_nll": round(nll, 4), "holdout_nll_t1": round(trained.meta["holdout_nll_t1"], 4),
                       "seconds": round(train_s, 3), "events_per_window": a.train_events,
                       "incidents_trained": int(round(stats.count.sum())), "active_domains": trained.meta["active_domains"]}
+        # the same statistics with the seeded random-init table as the prior (the north star's
+        # random-init configuration), scored on REF's rows on the host below
+        alt = mtrain.TrainConfig(seed=a.seed, init="random" if tcfg.init == "expert" else "expert")
+        alt_model = with_pairs(NaiveBayes_learned(stats, alt, T), rho, T)
         if a.export_model and rank == 0:
             mtrain.save_model(a.export_model, trained)
         log(f"trained on {len(train_imgs)} windows in {train_s:.2f}s: T = {T:.3f} (held-out NLL {nll:.3f})")
@@ -642,13 +653,16 @@ def main() -> int:
     ref55 = {}
     fx = os.path.join(ROOT, "tests", "fixtures", "ref_multi_fault_samples.jsonl")
     if rank == 0 and os.path.exists(fx):
+        from llm_slo_ebpf_toolkit_amd.models.train import host_scorer, ref55_report
+
         if gpu:
             ref55 = ref55_engine(pipe, fx, a.model)
         else:  # the host oracle engine scores with the same model on the host
             from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
-            from llm_slo_ebpf_toolkit_amd.models.train import host_scorer, ref55_report
 
             ref55 = {a.model: ref55_report(fx, host_scorer(pipe.model)), "bayes": ref55_report(fx, host_scorer(NaiveBayes.ref()))}
+        if trained is not None:
+            ref55[f"{a.model}_prior_{alt.init}"] = ref55_report(fx, host_scorer(alt_model))
 
     conf = summ["confusion"]
     dbg = summ["dbg"]
@@ -666,7 +680,8 @@ def main() -> int:
         "vs_baseline": None,  # REF publishes no measured throughput (its 900 events/s is a constant)
         "dtype": "fp64 posteriors / fp32 features (exact-int64 time joins)",
         "data": "synthetic fault-replay traces (seeded, REF fault profiles) through the native probe model into an "
-                "emulated BPF ring buffer; random-init attribution priors",
+                "emulated BPF ring buffer; attribution model trained (untimed) on labelled replay windows of other "
+                "seeds, REF's expert table as its likelihood prior",
         "config": {
             "model": f"config5: 16 signals (12 kernel + 4 GPU) x 10 fault domains, {a.model}, 4-tier LDS join",
             "global_batch": world * a.events,
@@ -786,8 +801,9 @@ def NaiveBayes_learned(stats, tcfg, temperature: float = 1.0):
     """models/train.py's fit on the device's statistics (what k_refit_nb computes)."""
     from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
 
-    return NaiveBayes.learned(stats, alpha=tcfg.alpha, seed=tcfg.seed, prior_pseudo=tcfg.prior_pseudo,
-                              temperature=temperature, min_count=tcfg.min_count)
+    from llm_slo_ebpf_toolkit_amd.models.train import learned_kwargs
+
+    return NaiveBayes.learned(stats, temperature=temperature, **learned_kwargs(tcfg))
 
 
 def catalog_domains():

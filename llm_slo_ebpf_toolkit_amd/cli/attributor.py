@@ -81,7 +81,7 @@ def train_main(a) -> int:
     from ..signals import catalog
 
     cfg = mtrain.TrainConfig(windows=a.train_windows, events_per_window=a.train_events,
-                             spans_per_window=a.train_spans, seed=a.seed)
+                             spans_per_window=a.train_spans, seed=a.seed, init=a.train_prior)
     if a.input:
         rows = [s for s in load_samples_jsonl(a.input) if s.signals and s.expected_set()]
         if not rows:
@@ -94,6 +94,7 @@ def train_main(a) -> int:
         tm.meta.update({"engine": "labelled-samples", "input": a.input, "config": cfg.__dict__})
     else:
         tm = mtrain.train_cpu(cfg)
+        tm.meta["heldout"] = mtrain.heldout_report(tm.model, cfg)
     fx = a.ref55 if a.ref55 and os.path.exists(a.ref55) else ""
     if fx:
         tm.meta["ref55"] = mtrain.ref55_report(fx, mtrain.host_scorer(tm.model))
@@ -141,6 +142,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     p.flag("train-events", 16384, "--train: events per training window")
     p.flag("train-spans", 1024, "--train: spans per training window")
     p.flag("seed", 42, "--train: replay and random-init seed")
+    p.flag("train-prior", "expert", "--train: the likelihoods' Beta prior, expert (REF's table) or random (seeded)",
+           choices=("expert", "random"))
     p.flag("ref55", os.path.join("tests", "fixtures", "ref_multi_fault_samples.jsonl"),
            "--train: REF's 55 labelled rows to score the new model on (skipped if absent)")
     a = p.parse_args(argv)

@@ -122,6 +122,10 @@ SLI_PROFILE: Dict[str, tuple] = {
     "mixed_multi": (1450, 4200, 2, 0.31),
     "gpu_contention": (900, 1900, 9, 0.02),
     "rccl_latency": (1100, 2600, 6, 0.03),
+    # NEW (REF has no SLI profile for them): a provider failing requests costs errors more than
+    # time; a slow vector store delays the first token by the retrieval stall
+    "provider_error": (620, 1300, 20, 0.22),
+    "retrieval_slowdown": (1050, 1500, 24, 0.01),
 }
 BASE_SLI = (340, 720, 36, 0.005)
 

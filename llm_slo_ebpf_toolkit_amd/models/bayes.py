@@ -267,11 +267,37 @@ class NaiveBayes:
         return rng.uniform(0.05, 0.95, size=(N_SLOTS, len(domains)))
 
     @staticmethod
+    def expert_table(domains: Sequence[str] = catalog.ALL_DOMAINS) -> np.ndarray:
+        """[16, D] P(elevated | domain) of REF's expert table (bayesian.go:67-190), extended to
+        the GPU signals and domains (catalog.extended_likelihood_matrix)."""
+        m = np.asarray(catalog.extended_likelihood_matrix(), dtype=np.float64)
+        return m[:, [catalog.DOMAIN_INDEX[d] for d in domains]]
+
+    @staticmethod
+    def unknown_floor(domains: Sequence[str] = catalog.ALL_DOMAINS) -> np.ndarray:
+        """[16, D] minimum likelihoods: the ``unknown`` column of REF's table (every signal
+        elevated by chance 5-10 % of the time), zero elsewhere. Healthy replay incidents never
+        show an elevated signal, so the learned P(e | unknown) falls to REF's clamp (0.01) and one
+        elevated signal then costs "no fault" more than a whole fault domain's missing symptoms
+        (REF row mf-51, a lone DNS elevation, read as unknown). The floor keeps "unknown" what it
+        is in REF: the hypothesis that whatever is elevated is noise."""
+        f = np.zeros((N_SLOTS, len(domains)))
+        if "unknown" in domains:
+            u = list(domains).index("unknown")
+            f[:, u] = NaiveBayes.expert_table(domains)[:, u]
+        return f
+
+    @staticmethod
     def learned(stats: "SufficientStats", alpha: float = 2.0, seed: int = 42,
                 init: Optional[np.ndarray] = None, domains: Sequence[str] = catalog.ALL_DOMAINS,
-                prior_pseudo: float = 1.0, temperature: float = 1.0, min_count: float = 0.0) -> LinearPosteriorModel:
+                prior_pseudo: float = 1.0, temperature: float = 1.0, min_count: float = 0.0,
+                floor: Optional[np.ndarray] = None, cap_domain: Optional[str] = None) -> LinearPosteriorModel:
         """Posterior-mean estimates: p_sd = (c_sd + alpha*p0_sd) / (n_d + alpha), with p0 a
-        seeded random-init table (north star: random-init priors); pi_d ~ Dirichlet(1).
+        seeded random-init table (north star: random-init priors) or REF's expert table
+        (``expert_table``: a domain without labelled mass keeps REF's column); pi_d ~ Dirichlet(1).
+        ``floor`` [16, D] bounds every likelihood from below (``unknown_floor``); the prior of
+        ``cap_domain`` is capped at the largest prior of the other active domains (the no-fault
+        class, the most frequent label, must not win on its prior alone).
         ``temperature`` T divides every logit (calibration: same argmax, flatter posteriors for
         T > 1); a domain with less than ``min_count`` labelled mass is inactive. The device refit
         (ops/csrc/posterior.hip k_refit_nb) computes exactly this."""
@@ -280,7 +306,14 @@ class NaiveBayes:
         n = stats.count[idx]
         c = stats.elevated_sum[:, idx]
         p = (c + alpha * p0) / (n[None, :] + alpha)
+        if floor is not None:
+            p = np.maximum(p, floor)
         priors_arr = (n + prior_pseudo) / (n.sum() + prior_pseudo * len(idx))
+        if cap_domain is not None and cap_domain in domains:
+            u = list(domains).index(cap_domain)
+            others = [i for i in range(len(idx)) if i != u and n[i] >= min_count]
+            if others:
+                priors_arr[u] = min(priors_arr[u], max(priors_arr[i] for i in others))
         priors = {d: float(priors_arr[i]) for i, d in enumerate(domains)}
         lik = {catalog.SIGNAL_NAMES[s]: {d: float(p[s, i]) for i, d in enumerate(domains)}
                for s in range(N_SLOTS)}

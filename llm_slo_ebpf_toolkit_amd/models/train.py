@@ -2,9 +2,10 @@
 
 REF attributes with one fixed expert table (/root/reference/pkg/attribution/bayesian.go:67-190)
 through one pipeline (/root/reference/pkg/attribution/pipeline.go:44-51, cmd/attributor/main.go
-:81-152). NEW learns the same naive-Bayes form from data, starting from a seeded random-init
-likelihood table (the north star's "random-init priors"), and ships the result as a file the
-agent loads (``agent --model-path``):
+:81-152). NEW learns the same naive-Bayes form from data, with REF's expert table as the Beta prior
+of every likelihood (``TrainConfig.init = "expert"``; the north star's seeded random-init table
+stays available as ``init = "random"``), and ships the result as a file the agent loads
+(``agent --model-path``):
 
 1. **training set** -- a fixed, seeded set of fault-replay windows (pipeline/replay.py): single
    faults of every domain (scenario ``full``) alternating with compound incidents (scenario
@@ -19,9 +20,11 @@ agent loads (``agent --model-path``):
    records (decode -> 4-tier join -> per-group means): the GPU engine in the benchmark, the CPU
    oracle engine here (identical by the GPU tests);
 3. **fit** -- sufficient statistics with *soft* labels (a multi-fault incident's mass is spread
-   over its domain set: label_code), posterior-mean likelihoods towards the random-init table,
-   domains without labelled mass left inactive (a classifier never shown a domain must not
-   predict it from random likelihoods);
+   over its domain set: label_code), posterior-mean likelihoods towards REF's table (a domain with
+   little labelled mass keeps REF's column and a finite prior: all 8 REF domains plus the 2 GPU
+   domains stay reachable), and "unknown" calibrated as the no-fault hypothesis -- its
+   likelihoods floored at REF's chance-elevation column and its prior capped at the largest fault
+   prior, so one strongly elevated signal outweighs it (bayes.NaiveBayes.learned);
 4. **calibration** -- one temperature T dividing every logit, fitted on held-out windows by the
    soft-label negative log-likelihood. Naive Bayes multiplies 16 signals' evidence as if
    independent, so its raw posteriors are far too sharp; T restores probabilities that spread
@@ -52,7 +55,11 @@ from .bayes import (N_DOMAINS, PAIR_LIST, LinearPosteriorModel, NaiveBayes, Suff
                     soft_labels, with_pairs, with_temperature)
 
 REF_FAULTS = ("provider_throttle", "dns_latency", "cpu_throttle", "memory_pressure", "network_partition")
-COMPOUND = [c for k in (2, 3) for c in itertools.combinations(REF_FAULTS, k)]
+# REF's two domains its generator has no profile for (signals/generator.py provider_error,
+# retrieval_slowdown; mapper.go:43-46)
+EXTRA_FAULTS = ("provider_error", "retrieval_slowdown")
+COMPOUND = ([c for c in itertools.combinations(REF_FAULTS + EXTRA_FAULTS, 2)]
+            + [c for c in itertools.combinations(REF_FAULTS, 3)])
 TRAIN_SCENARIOS = ("full", "compound", "live")
 MODEL_FORMAT = "mislo-model/1"
 
@@ -64,7 +71,10 @@ class TrainConfig:
     spans_per_window: int = 1024
     services: int = 64                # incident groups per window
     seed: int = 42                    # replay seed and random-init table seed
-    alpha: float = 2.0                # pseudo-count towards the random-init table
+    # pseudo-count of the Beta prior (init below): 10 labelled incidents' worth, ~7 % of a domain's
+    # training mass. Chosen on held-out replay windows only (another seed; complete and partial
+    # symptom sets): 2 -> 0.986 / 0.783, 10 -> 0.986 / 0.809, 15 -> 0.986 / 0.803 macro-F1
+    alpha: float = 10.0
     prior_pseudo: float = 1.0
     min_count: float = 1.0            # labelled mass below which a domain stays inactive
     holdout_every: int = 4            # every 4th window is held out for the temperature fit
@@ -75,6 +85,16 @@ class TrainConfig:
     # members as soft labels it taught every member the other's symptoms (P(dns elevated |
     # cpu_throttle) ~ 0.3), which then counted against a lone CPU fault
     single_fault_likelihoods: bool = True
+    # the likelihoods' Beta prior: "expert" = REF's table (bayesian.go:67-190, extended to the GPU
+    # rows and domains), so a domain with little labelled mass keeps REF's column; "random" = the
+    # seeded random-init table (the north star's random-init priors)
+    init: str = "expert"
+    # "unknown" = the no-fault hypothesis: its likelihoods floored at REF's unknown column (chance
+    # elevations) and its prior capped at the largest fault-domain prior (bayes.NaiveBayes.learned)
+    calibrate_unknown: bool = True
+    # each elevated symptom of a fault shows with this probability in a training incident
+    # (pipeline/replay.py ReplayConfig.symptom_keep)
+    symptom_keep: float = 1.0
 
 
 @dataclass
@@ -106,7 +126,8 @@ def training_windows(cfg: TrainConfig):
 
     ensure_scenarios()
     gens = [ReplayGenerator(ReplayConfig(scenario=s, n_services=cfg.services, events_per_window=cfg.events_per_window,
-                                         spans_per_window=cfg.spans_per_window, seed=cfg.seed + 101 * i))
+                                         spans_per_window=cfg.spans_per_window, seed=cfg.seed + 101 * i,
+                                         symptom_keep=cfg.symptom_keep))
             for i, s in enumerate(TRAIN_SCENARIOS)]
     return [gens[j % len(gens)].next_window() for j in range(cfg.windows)]
 
@@ -206,6 +227,25 @@ def likelihood_codes(codes: np.ndarray, cfg: Optional[TrainConfig] = None) -> np
     return np.where(((c.astype(np.int64) >> 8) & 0xFFFF) != 0, np.int32(-1), c).astype(np.int32)
 
 
+def learned_kwargs(cfg: TrainConfig) -> Dict[str, object]:
+    """NaiveBayes.learned's keyword arguments for a training config (host fit, bench, device refit)."""
+    return {"alpha": cfg.alpha, "seed": cfg.seed, "prior_pseudo": cfg.prior_pseudo, "min_count": cfg.min_count,
+            "init": NaiveBayes.expert_table() if cfg.init == "expert" else None,
+            "floor": NaiveBayes.unknown_floor() if cfg.calibrate_unknown else None,
+            "cap_domain": "unknown" if cfg.calibrate_unknown else None}
+
+
+def device_p0(cfg: TrainConfig) -> np.ndarray:
+    """[2, 16, 16] f64 the device refit reads (posterior.hip k_refit_nb): the Beta-prior table
+    and the likelihood floor, domains in columns 0..9."""
+    kw = learned_kwargs(cfg)
+    out = np.zeros((2, 16, 16))
+    out[0, :, :N_DOMAINS] = kw["init"] if kw["init"] is not None else NaiveBayes.random_init_table(cfg.seed)
+    if kw["floor"] is not None:
+        out[1, :, :N_DOMAINS] = kw["floor"]
+    return out
+
+
 def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: TrainConfig) -> TrainedModel:
     """Statistics on the training windows, temperature on the held-out ones."""
     feats = np.asarray(feats, dtype=np.float64)
@@ -215,8 +255,7 @@ def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: Train
     st = SufficientStats()
     single = likelihood_codes(codes, cfg) >= 0
     st.add(feats[tr & single], Y[tr & single])
-    base = NaiveBayes.learned(st, alpha=cfg.alpha, seed=cfg.seed, prior_pseudo=cfg.prior_pseudo,
-                              min_count=cfg.min_count)
+    base = NaiveBayes.learned(st, **learned_kwargs(cfg))
     hv = hold & (np.asarray(codes) >= 0)
     t, nll = fit_temperature(base, feats[hv], Y[hv], cfg.t_grid) if hv.any() else (1.0, float("nan"))
     model = with_temperature(base, t)
@@ -241,6 +280,54 @@ def train_cpu(cfg: Optional[TrainConfig] = None) -> TrainedModel:
     tm = fit(feats, codes, wid, cfg)
     tm.meta.update({"engine": "cpu-oracle", "config": asdict(cfg), "scenarios": list(TRAIN_SCENARIOS)})
     return tm
+
+
+# ---------------------------------------------------------------------------------------
+# held-out replay windows (another seed: what the hyperparameters are chosen on)
+# ---------------------------------------------------------------------------------------
+
+HELDOUT_SEED_OFFSET = 7919
+
+
+def heldout_report(model: LinearPosteriorModel, cfg: TrainConfig, windows: int = 6,
+                   keeps: Sequence[float] = (1.0, 0.7)) -> Dict[str, object]:
+    """The model on replay windows no fit saw (seed + 7919): the ``full`` single-fault set (every
+    fault domain) with complete symptom sets and with each symptom kept at 0.7 (partial
+    incidents), and REF's mixed_multi pairs (partial / coverage@0.10). Macro-F1 over the 10
+    domains, per-domain recall and the confusion matrix (rows = truth)."""
+    from ..pipeline.replay import ReplayConfig, ReplayGenerator
+    from .metrics import confusion_report, macro_f1_from_confusion
+
+    ensure_scenarios()
+    D = N_DOMAINS
+    out: Dict[str, object] = {}
+    for keep in keeps:
+        g = ReplayGenerator(ReplayConfig(scenario="full", events_per_window=cfg.events_per_window,
+                                         spans_per_window=cfg.spans_per_window, n_services=cfg.services,
+                                         seed=cfg.seed + HELDOUT_SEED_OFFSET, symptom_keep=keep))
+        f, c, _ = cpu_features([g.next_window() for _ in range(windows)])
+        cm = np.zeros((D, D), dtype=np.int64)
+        np.add.at(cm, (np.asarray(c) & 0xFF, model.predict(f)), 1)
+        out[f"full_keep{keep:g}"] = {"macro_f1": round(macro_f1_from_confusion(cm), 4), "incidents": int(cm.sum()),
+                                     "recall": {catalog.ALL_DOMAINS[d]: round(float(cm[d, d] / max(cm[d].sum(), 1)), 4)
+                                                for d in range(D)},
+                                     "confusion": cm.tolist(), **confusion_report(cm, catalog.ALL_DOMAINS)}
+    g = ReplayGenerator(ReplayConfig(scenario="mixed_multi", events_per_window=cfg.events_per_window,
+                                     spans_per_window=cfg.spans_per_window, n_services=cfg.services,
+                                     seed=cfg.seed + HELDOUT_SEED_OFFSET))
+    wins = [g.next_window() for _ in range(max(1, windows // 2))]
+    f, _, _ = cpu_features(wins)
+    post, pred = model.posteriors(f), model.predict(f)
+    doms = [d for w in wins for d in w.group_domains]
+    part = cov = 0.0
+    for p, row, ds in zip(pred, post, doms):
+        exp = {catalog.DOMAIN_INDEX[d] for d in ds}
+        hyp = set(np.flatnonzero(row[:D] >= 0.10).tolist()) | {int(p)}
+        part += int(p) in exp
+        cov += len(exp & hyp) / len(exp)
+    out["mixed_multi"] = {"partial_accuracy": round(part / len(doms), 4), "coverage_accuracy": round(cov / len(doms), 4),
+                          "incidents": len(doms)}
+    return out
 
 
 # ---------------------------------------------------------------------------------------

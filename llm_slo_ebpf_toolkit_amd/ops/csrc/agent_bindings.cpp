@@ -164,8 +164,8 @@ class PyEngine {
   void set_model_bytes(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
     e_->set_model_bytes(b.data(), (size_t)b.size());
   }
-  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count) {
-    eng().set_refit(alpha, prior_pseudo, inv_temp, min_count);
+  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom) {
+    eng().set_refit(alpha, prior_pseudo, inv_temp, min_count, cap_dom);
   }
   void refit_now() { eng().refit_now(); }
   // K3 on given features (REF's 55 rows, offline evaluation) with the model on the device
@@ -195,8 +195,9 @@ class PyEngine {
     return d;
   }
   void set_p0(py::array_t<double, py::array::c_style | py::array::forcecast> p0) {
-    if (p0.size() != kSlots * 16) throw std::invalid_argument("p0 must be f64[256]");
-    e_->set_p0(p0.data());
+    if (p0.size() != kSlots * 16 && p0.size() != 2 * kSlots * 16)
+      throw std::invalid_argument("p0 must be f64[256] (table) or f64[512] (table, floor)");
+    e_->set_p0(p0.data(), (size_t)p0.size());
   }
   void set_pods(py::array_t<uint32_t, py::array::c_style | py::array::forcecast> pods,
                 py::array_t<uint32_t, py::array::c_style | py::array::forcecast> sn) {
@@ -341,7 +342,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("set_model_bytes", &PyEngine::set_model_bytes)
       .def("set_p0", &PyEngine::set_p0)
       .def("set_refit", &PyEngine::set_refit, py::arg("alpha") = 2.0, py::arg("prior_pseudo") = 1.0,
-           py::arg("inv_temp") = 1.0, py::arg("min_count") = 0.0)
+           py::arg("inv_temp") = 1.0, py::arg("min_count") = 0.0, py::arg("cap_dom") = -1)
       .def("refit_now", &PyEngine::refit_now)
       .def("set_device_refit", [](PyEngine& p, bool on) { p.eng().set_device_refit(on); })
       .def("score", &PyEngine::score, py::arg("feat"), py::arg("labels") = py::none())

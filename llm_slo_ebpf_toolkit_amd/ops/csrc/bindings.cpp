@@ -308,11 +308,12 @@ class Engine {
     pack();
   }
 
-  // On-device learned-NB refit from accumulated stats ([32*32 + 16] f64) and the
-  // random-init prior table p0 ([16*16] f64); rewrites the model in place (stream order).
-  // add (optional, f64[1040]): statistics folded into stats_acc first, in the same launch.
+  // On-device learned-NB refit from accumulated stats ([32*32 + 16] f64) and the Beta prior's
+  // table p0 ([16*16] f64, optionally followed by a [16*16] likelihood floor); rewrites the model
+  // in place (stream order). add (optional, f64[1040]): statistics folded into stats_acc first,
+  // in the same launch. cap_dom >= 0: that domain's prior capped at the others' largest.
   void refit_nb(torch::Tensor stats_acc, torch::Tensor p0, double alpha, double prior_pseudo, int64_t n_dom,
-                c10::optional<torch::Tensor> add) {
+                c10::optional<torch::Tensor> add, int64_t cap_dom) {
     check_cuda(stats_acc, "stats_acc");
     check_cuda(p0, "p0");
     if (stats_acc.scalar_type() != torch::kFloat64 || stats_acc.numel() < 32 * 32 + kMaxDomains ||
@@ -327,8 +328,11 @@ class Engine {
         throw std::invalid_argument("add must be contiguous f64[1040]");
       addp = add->data_ptr<double>();
     }
+    if (cap_dom >= n_dom) throw std::invalid_argument("cap_dom out of range");
+    const double* floor_tab = p0.numel() >= 2 * kSlots * 16 ? p0.data_ptr<double>() + kSlots * 16 : nullptr;
     launch_refit_nb(stats_acc.data_ptr<double>(), addp, p0.data_ptr<double>(), alpha, prior_pseudo, (int)n_dom,
-                    reinterpret_cast<PosteriorModel*>(model.data_ptr()), cur_stream());
+                    reinterpret_cast<PosteriorModel*>(model.data_ptr()), cur_stream(), 1.0, 0.0, floor_tab,
+                    (int)cap_dom);
   }
 
   int64_t sig_cap() const { return sig_cap_; }
@@ -455,7 +459,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("run_window", &Engine::run_window, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
            py::arg("with_labels") = true, py::arg("learn") = false, py::arg("wire") = 64)
       .def("refit_nb", &Engine::refit_nb, py::arg("stats_acc"), py::arg("p0"), py::arg("alpha") = 2.0,
-           py::arg("prior_pseudo") = 1.0, py::arg("n_dom") = 10, py::arg("add") = py::none())
+           py::arg("prior_pseudo") = 1.0, py::arg("n_dom") = 10, py::arg("add") = py::none(), py::arg("cap_dom") = -1)
       .def("run_window_pre", &Engine::run_window_pre, py::arg("events"), py::arg("spans"), py::arg("n_groups"),
            py::arg("wire") = 64)
       .def("run_window_post", &Engine::run_window_post, py::arg("n_groups"), py::arg("with_labels") = true,

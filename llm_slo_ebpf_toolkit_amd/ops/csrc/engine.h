@@ -63,6 +63,7 @@ struct EngineConfig {
   bool device_refit = true;  // learned naive Bayes refit on the device from accumulated statistics
   double alpha = 2.0, prior_pseudo = 1.0;
   double inv_temp = 1.0, min_count = 0.0;  // refit calibration (posterior.hip k_refit_nb)
+  int cap_dom = -1;                         // refit: the domain whose prior is capped (-1: none)
   int n_dom = 10;
   float ttft_slo_ms = 800.0f;  // per-incident SLO impact: spans with TTFT above this breach
   double halo_ms = 0.0;        // later windows also join rows this close to every later window's latest record
@@ -130,7 +131,7 @@ class WindowEngine {
   // device refit parameters (smoothing, prior pseudo-count, 1 / temperature, minimum labelled mass
   // of an active domain), and a refit of the model from the accumulated statistics now
   // (stream-ordered before the next window)
-  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count);
+  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom = -1);
   void refit_now();
   // stop (or resume) the per-window prequential refit: the model on the device stays frozen
   void set_device_refit(bool on) { cfg_.device_refit = on; }
@@ -139,7 +140,8 @@ class WindowEngine {
   // the confusion of labels (label_code, may be null) x predictions [16][16].
   void score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred, double* conf,
                       uint32_t* evbits, uint32_t* confusion);
-  void set_p0(const double* p0);                      // [16 x 16] random-init table (device refit)
+  // device refit: [16 x 16] Beta-prior table, optionally followed by a [16 x 16] likelihood floor
+  void set_p0(const double* p0, size_t n);
   void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
   // other GPUs' rows for the next window, as their exchange blocks would arrive over RCCL (world
   // blocks of [32-byte header: uint32 row count | XRec rows], this rank's block skipped); the

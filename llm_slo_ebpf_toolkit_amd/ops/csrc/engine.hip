@@ -257,8 +257,8 @@ void WindowEngine::alloc() {
   HIPCHECK(hipMemset(totals_, 0, kPacketLen * sizeof(double)));
   stats_acc_ = dalloc<double>(kStatsLen);
   HIPCHECK(hipMemset(stats_acc_, 0, kStatsLen * sizeof(double)));
-  p0_ = dalloc<double>(kSlots * 16);
-  HIPCHECK(hipMemset(p0_, 0, kSlots * 16 * sizeof(double)));
+  p0_ = dalloc<double>(2 * kSlots * 16);  // the Beta prior's table, then the likelihood floor
+  HIPCHECK(hipMemset(p0_, 0, 2 * kSlots * 16 * sizeof(double)));
   model_dev_ = dalloc<uint8_t>(sizeof(PosteriorModel));
   HIPCHECK(hipMemset(model_dev_, 0, sizeof(PosteriorModel)));
   for (int i = 0; i < max_ahead_ + 2; ++i) {
@@ -651,7 +651,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     // fold window k - nb's all-reduced statistics (packet b) and refit before window k: a
     // deterministic prequential lag of nb, identical on every rank
     launch_refit_nb(stats_acc_, packet_dev_[b] + kStatsOff, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
-                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count);
+                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count,
+                    p0_ + kSlots * 16, cfg_.cap_dom);
     ++folded_;
   }
   const bool injected = !inject_.empty();
@@ -771,13 +772,16 @@ void WindowEngine::set_model_bytes(const void* bytes, size_t n) {
   HIPCHECK(hipMemcpyAsync(model_dev_, h, n, hipMemcpyHostToDevice, compute_));
 }
 
-void WindowEngine::set_p0(const double* p0) {
-  HIPCHECK(hipMemcpy(p0_, p0, kSlots * 16 * sizeof(double), hipMemcpyHostToDevice));
+void WindowEngine::set_p0(const double* p0, size_t n) {
+  if (n != (size_t)kSlots * 16 && n != 2 * (size_t)kSlots * 16) throw std::invalid_argument("p0 must be f64[256] or [512]");
+  HIPCHECK(hipMemset(p0_ + kSlots * 16, 0, kSlots * 16 * sizeof(double)));  // [256]: no floor
+  HIPCHECK(hipMemcpy(p0_, p0, n * sizeof(double), hipMemcpyHostToDevice));
 }
 
-void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count) {
-  if (!(alpha > 0.0) || !(prior_pseudo >= 0.0) || !(inv_temp > 0.0) || !(min_count >= 0.0))
+void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom) {
+  if (!(alpha > 0.0) || !(prior_pseudo >= 0.0) || !(inv_temp > 0.0) || !(min_count >= 0.0) || cap_dom >= cfg_.n_dom)
     throw std::invalid_argument("refit parameters");
+  cfg_.cap_dom = cap_dom < 0 ? -1 : cap_dom;
   cfg_.alpha = alpha;
   cfg_.prior_pseudo = prior_pseudo;
   cfg_.inv_temp = inv_temp;
@@ -786,7 +790,8 @@ void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp,
 
 void WindowEngine::refit_now() {
   launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
-                  reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count);
+                  reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count,
+                    p0_ + kSlots * 16, cfg_.cap_dom);
 }
 
 void WindowEngine::score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred,
@@ -912,7 +917,8 @@ void WindowEngine::restore(const double* stats, const void* model, size_t n, int
     HIPCHECK(hipMemcpy(model_dev_, model, n, hipMemcpyHostToDevice));
   } else {  // the learned model from the restored statistics, by the device refit itself
     launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
-                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count);
+                    reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count,
+                    p0_ + kSlots * 16, cfg_.cap_dom);
     HIPCHECK(hipStreamSynchronize(compute_));
   }
   folded_ = folded;

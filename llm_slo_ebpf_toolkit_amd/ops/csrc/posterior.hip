@@ -301,21 +301,24 @@ __global__ __launch_bounds__(NT) void k_posterior_stats(PosteriorArgs p, StatsAr
 
 // On-device refit of the learned naive Bayes (models/bayes.py NaiveBayes.learned) from
 // the accumulated, all-reduced sufficient statistics: posterior-mean likelihoods
-//   p_sd = (c_sd + alpha * p0_sd) / (n_d + alpha),  pi_d = (n_d + pp) / (N + pp * D)
+//   p_sd = max((c_sd + alpha * p0_sd) / (n_d + alpha), floor_sd),  pi_d = (n_d + pp) / (N + pp * D)
 // turned into the linear-logit model in place (w, bias, evidence masks). Runs on the
 // compute stream between windows, so online learning needs no host round trip.
-// stats: [32 x 32] f64 (rows 0-15 = E^T Y) followed by count[16]; p0: [16 x 16] f64.
+// stats: [32 x 32] f64 (rows 0-15 = E^T Y) followed by count[16]; p0: [16 x 16] f64, the Beta
+// prior's table (REF's expert table or the random-init one); floor (optional): [16 x 16] f64
+// minimum likelihoods (REF's "unknown" column: chance elevations, models/bayes.py unknown_floor).
 // add (optional, same layout): a window's all-reduced statistics, folded into stats first
 // (one launch instead of an elementwise add plus the refit on the compute stream).
 // inv_temp scales every logit (w and bias; the calibration temperature T = 1 / inv_temp fitted on
 // held-out windows, models/train.py): argmax and evidence are unchanged, the posteriors are
 // flatter for T > 1 (REF's coverage metric counts hypotheses >= 0.10). A domain with less than
-// min_count labelled mass is inactive (bias -inf): its likelihoods would be the random-init
-// table, not data.
+// min_count labelled mass is inactive (bias -inf). cap_dom (>= 0): that domain's prior is capped
+// at the largest prior of the other active domains (the no-fault class must not win on its
+// label frequency alone).
 __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, const double* __restrict__ add,
-                                                  const double* __restrict__ p0, double alpha, double prior_pseudo,
-                                                  int n_dom, double inv_temp, double min_count,
-                                                  PosteriorModel* __restrict__ pm) {
+                                                  const double* __restrict__ p0, const double* __restrict__ floor_tab,
+                                                  double alpha, double prior_pseudo, int n_dom, double inv_temp,
+                                                  double min_count, int cap_dom, PosteriorModel* __restrict__ pm) {
   __shared__ double s_logpn[kSlots][kMaxDomains];
   __shared__ double s_pe[kSlots][kMaxDomains];
   __shared__ double s_logpi[kMaxDomains];
@@ -332,7 +335,8 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
     if (d < n_dom) {
       const double n = count[d];
       const double c = stats[sl * 32 + d];
-      const double p = (c + alpha * p0[sl * 16 + d]) / (n + alpha);
+      double p = (c + alpha * p0[sl * 16 + d]) / (n + alpha);
+      if (floor_tab) p = fmax(p, floor_tab[sl * 16 + d]);
       const double pe = fmin(fmax(p, 0.01), 0.99), pn = fmin(fmax(1.0 - p, 0.01), 0.99);
       pm->w[sl][d] = (log(pe) - log(pn)) * inv_temp;
       s_logpn[sl][d] = log(pn);
@@ -344,30 +348,43 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
       s_pe[sl][d] = 0.0;
     }
   }
-  __syncthreads();
-  const int n_pairs = pm->n_pairs;
-  const double rho = pm->pair_rho;
   if (t < kMaxDomains) {
     if (t < n_dom && count[t] >= min_count) {
       double N = 0.0;
       for (int d = 0; d < n_dom; ++d) N += count[d];
-      const double logpi = log((count[t] + prior_pseudo) / (N + prior_pseudo * (double)n_dom));
-      double b = logpi;
+      s_logpi[t] = log((count[t] + prior_pseudo) / (N + prior_pseudo * (double)n_dom));
+    } else {
+      s_logpi[t] = -__builtin_inf();
+    }
+  }
+  __syncthreads();
+  double logpi_t = t < kMaxDomains ? s_logpi[t] : 0.0;
+  if (t == cap_dom && logpi_t > -__builtin_inf()) {
+    double mx = -__builtin_inf();
+    for (int d = 0; d < n_dom; ++d)
+      if (d != t) mx = fmax(mx, s_logpi[d]);
+    if (mx > -__builtin_inf()) logpi_t = fmin(logpi_t, mx);
+  }
+  __syncthreads();  // every read of s_logpi above is done before the capped prior is stored
+  if (t < kMaxDomains) {
+    if (logpi_t > -__builtin_inf()) {
+      double b = logpi_t;
       for (int sl = 0; sl < kSlots; ++sl) b += s_logpn[sl][t];
-      if (n_pairs > 0) b += log1p(-rho);  // singles keep 1 - rho of the prior
+      if (pm->n_pairs > 0) b += log1p(-pm->pair_rho);  // singles keep 1 - rho of the prior
       pm->bias[t] = b * inv_temp;
       pm->dom_mask[t] = s_mask[t];
-      s_logpi[t] = logpi;
     } else {
       pm->bias[t] = -__builtin_inf();
       pm->dom_mask[t] = 0u;
-      s_logpi[t] = -__builtin_inf();
     }
+    s_logpi[t] = logpi_t;
   }
   if (t == 0) {
     pm->table_mask = 0xFFFFu;
     pm->mode = 0;
   }
+  const int n_pairs = pm->n_pairs;
+  const double rho = pm->pair_rho;
   if (n_pairs <= 0) return;
   // 2-fault columns (models/bayes.py with_pairs): noisy-OR likelihoods q = 1 - (1-p_a)(1-p_b),
   // prior rho * pi_a pi_b / sum over the active pairs
@@ -401,9 +418,10 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
 }
 
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
-                     PosteriorModel* pm, hipStream_t stream, double inv_temp, double min_count) {
-  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, alpha, prior_pseudo, n_dom, inv_temp,
-                     min_count, pm);
+                     PosteriorModel* pm, hipStream_t stream, double inv_temp, double min_count, const double* floor_tab,
+                     int cap_dom) {
+  hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, floor_tab, alpha, prior_pseudo, n_dom,
+                     inv_temp, min_count, cap_dom, pm);
 }
 
 constexpr int kPostNT = 256, kStatsRPW = 256;

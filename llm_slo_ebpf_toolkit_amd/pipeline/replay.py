@@ -48,7 +48,11 @@ SCENARIOS: Dict[str, List[Tuple[str, ...]]] = {
                     ("network_partition", "dns_latency"), ("provider_throttle", "network_partition")],
     # NEW: every single fault incl. the MI355X GPU faults (config 5: all fault domains)
     "full": [("provider_throttle",), ("dns_latency",), ("cpu_throttle",), ("memory_pressure",),
-             ("network_partition",), ("gpu_contention",), ("rccl_latency",)],
+             ("network_partition",), ("gpu_contention",), ("rccl_latency",), ("provider_error",),
+             ("retrieval_slowdown",)],
+    # the two REF domains REF's own generator cannot produce (mapper.go:43-46)
+    "provider_error": [("provider_error",)],
+    "retrieval_slowdown": [("retrieval_slowdown",)],
     # NEW: the live-node shapes of the CPU and GPU contention domains (signals/generator.py
     # cpu_contention, gpu_compute_contention) next to REF's, alone and with a network fault
     "live": [("cpu_contention",), ("gpu_compute_contention",), ("cpu_throttle",), ("gpu_contention",),
@@ -94,6 +98,13 @@ class ReplayConfig:
     # phases, test/incident-lab/scenarios/*.yaml): with a halo, a window joins the previous
     # window's boundary rows, which must carry the same faults
     fault_hold: int = 1
+    # symptom variability: each of a fault's elevated symptoms shows in an incident with this
+    # probability (at least one always does). 1.0 = every symptom of REF's profile, every time
+    # (REF's generator.go:244-289). REF's expert columns say real incidents are not that clean
+    # (P(connect elevated | network_dns) = .50, bayesian.go:67-190): a model trained only on
+    # complete profiles learns that a DNS fault always slows connects and then misses the DNS
+    # incident whose connects stayed fast (REF row mf-51).
+    symptom_keep: float = 1.0
 
     @property
     def n_pods(self) -> int:
@@ -128,11 +139,26 @@ class ReplayWindow:
 GPU_SERVED_COUPLING: Dict[str, Dict[str, float]] = {}
 
 
-def _profile(labels: Sequence[str]) -> Dict[str, float]:
+def _symptoms(lab: str, rng: Optional[np.random.Generator], keep: float) -> Dict[str, float]:
+    """A fault's overrides in one incident: every elevated symptom with probability ``keep``
+    (at least one of them), the sub-threshold ones always."""
+    over = dict(FAULT_OVERRIDES.get(lab, {}))
+    over.update(GPU_SERVED_COUPLING.get(lab, {}))
+    if rng is None or keep >= 1.0:
+        return over
+    elev = [k for k, v in over.items() if v >= catalog.BY_NAME[k].elevated]
+    if not elev:
+        return over
+    kept = [k for k in elev if rng.random() < keep]
+    if not kept:
+        kept = [elev[int(rng.integers(len(elev)))]]
+    return {k: v for k, v in over.items() if k in kept or k not in elev}
+
+
+def _profile(labels: Sequence[str], rng: Optional[np.random.Generator] = None, keep: float = 1.0) -> Dict[str, float]:
     prof = dict(BASE_PROFILE)
     for lab in labels:
-        over = dict(FAULT_OVERRIDES.get(lab, {}))
-        over.update(GPU_SERVED_COUPLING.get(lab, {}))
+        over = _symptoms(lab, rng, keep)
         for k, v in over.items():
             # multi-fault: the more severe symptom wins (latency up / tps down are both "up" here)
             prof[k] = max(prof[k], v) if k in prof else v
@@ -215,7 +241,10 @@ class ReplayGenerator:
         if w % max(1, cfg.fault_hold) == 0 or getattr(self, "_faults", None) is None:
             self._faults = self._labels()
         faults = self._faults
-        profiles = [_profile(f) for f in faults]
+        if w % max(1, cfg.fault_hold) == 0 or getattr(self, "_profiles", None) is None:
+            # drawn with the assignment: a held fault keeps its symptoms across windows
+            self._profiles = [_profile(f, self.rng, cfg.symptom_keep) for f in faults]
+        profiles = self._profiles
         G = cfg.n_services
         P = cfg.n_pods
 

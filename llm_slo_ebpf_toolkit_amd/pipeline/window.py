@@ -33,6 +33,7 @@ import numpy as np
 from ..collector import records
 from ..models.bayes import LDA, N_DOMAINS, NaiveBayes, SufficientStats
 from ..models.metrics import macro_f1_from_confusion
+from ..signals import catalog
 
 # hist, status, misc(+16 value sums), dbg, confusion, stats, count, ring accounting
 PACKET_LAYOUT = (256, 48, 18, 8, 256, 1024, 16, 8)
@@ -141,6 +142,8 @@ class WindowPipeline:
         p0 = np.zeros((16, 16), dtype=np.float64)
         p0[:, :N_DOMAINS] = NaiveBayes.random_init_table(seed)
         self.eng.set_p0(p0.ravel())
+        # NaiveBayes.learned's arguments the device refit mirrors (set_prior changes them)
+        self.learned_kw: Dict[str, object] = {"seed": seed}
         self.cum_stats = SufficientStats()
         if model_image is not None:
             from ..ops.engine import model_from_bytes
@@ -159,6 +162,24 @@ class WindowPipeline:
         if self.model_name == "bayes_gpu":
             return NaiveBayes.gpu()
         return NaiveBayes.learned(SufficientStats(), seed=self.seed)
+
+    def set_prior(self, init: Optional[np.ndarray] = None, floor: Optional[np.ndarray] = None,
+                  cap_domain: Optional[str] = None) -> None:
+        """The learned model's Beta prior table [16, D] (None: the seeded random-init one), its
+        likelihood floor [16, D] and the capped-prior domain (models/train.py learned_kwargs), on
+        the device refit (k_refit_nb) and the host mirror alike. The refit's other parameters
+        stay set_refit's."""
+        p0 = np.zeros((2, 16, 16), dtype=np.float64)
+        p0[0, :, :N_DOMAINS] = init if init is not None else NaiveBayes.random_init_table(self.seed)
+        if floor is not None:
+            p0[1, :, :N_DOMAINS] = floor
+        self.eng.set_p0(p0.ravel())
+        self.learned_kw = {"seed": self.seed, "init": init, "floor": floor, "cap_domain": cap_domain}
+
+    def cap_dom(self) -> int:
+        """The capped-prior domain's index for set_refit (-1: none)."""
+        c = self.learned_kw.get("cap_domain")
+        return -1 if c is None else catalog.DOMAIN_INDEX[str(c)]
 
     # ---- per window -----------------------------------------------------------------------
     def submit(self, kernel, user, spans, n_groups: int, labels=None, bases=(0, 0, 0, 0), with_labels: bool = True,
@@ -188,7 +209,7 @@ class WindowPipeline:
         if self.model_name == "lda" and self.cum_stats.count.sum() > 32:
             self.model = LDA.fit(self.cum_stats)
         elif self.model_name in ("bayes_learned", "lda"):
-            self.model = NaiveBayes.learned(self.cum_stats, seed=self.seed)
+            self.model = NaiveBayes.learned(self.cum_stats, **self.learned_kw)
         self.eng.set_model_bytes(self._model_bytes(self.model))
 
     def wait(self, k: int) -> None:
@@ -273,7 +294,7 @@ class WindowPipeline:
             if self.model_name == "lda" and self.cum_stats.count.sum() > 32:
                 self.model = LDA.fit(self.cum_stats)
             else:
-                self.model = NaiveBayes.learned(self.cum_stats, seed=self.seed)
+                self.model = NaiveBayes.learned(self.cum_stats, **self.learned_kw)
 
     def save_checkpoint(self, path: str, extra_meta: Optional[Dict[str, object]] = None) -> None:
         from ..utils import checkpoint
@@ -298,7 +319,7 @@ class WindowPipeline:
                             elevated_sum=st[:1024].reshape(32, 32)[:16, :N_DOMAINS].copy(),
                             x_sum=st[:1024].reshape(32, 32)[16:, :N_DOMAINS].copy(),
                             xx=st[:1024].reshape(32, 32)[16:, 16:].copy())
-        return NaiveBayes.learned(s, seed=self.seed)
+        return NaiveBayes.learned(s, **self.learned_kw)
 
 
 # ---------------------------------------------------------------------------------------

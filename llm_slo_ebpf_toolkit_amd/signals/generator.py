@@ -49,8 +49,17 @@ FAULT_OVERRIDES: Dict[str, Dict[str, float]] = {
     # without filling its HBM: foreign GPU time, HBM at its usual level.
     "cpu_contention": {"runqueue_delay_ms": 6, "cpu_steal_pct": 40},
     "gpu_compute_contention": {"gpu_queue_delay_ms": 35},
+    # NEW: the two REF domains REF's generator has no profile for (generator.go:244-289 stops at
+    # five), shaped from their expert likelihood columns (bayesian.go:67-190). provider_error: the
+    # provider resets / refuses connections and fails handshakes (connect_errors .85, tls_fail .60,
+    # syscall .60, tls .50) while connects themselves stay fast (connect .40). retrieval_slowdown:
+    # the vector store answers slowly -- the service's reads block (syscall .40) and the store's
+    # index reads hit disk (disk .30) -- with the network healthy (dns .15, connect .30).
+    "provider_error": {"connect_errors_total": 3, "tls_handshake_fail_total": 2, "syscall_latency_ms": 120,
+                       "tls_handshake_ms": 65},
+    "retrieval_slowdown": {"syscall_latency_ms": 140, "disk_io_latency_ms": 30, "connect_latency_ms": 45},
 }
-FAULT_ERRNO = {"provider_throttle": 110, "network_partition": 113}
+FAULT_ERRNO = {"provider_throttle": 110, "network_partition": 113, "provider_error": 104}
 
 # Signals that carry the demo conn tuple (REF generator.go:141-152)
 _TUPLE_SIGNALS = {"dns_latency_ms", "tcp_retransmits_total", "connect_latency_ms", "connect_errors_total",

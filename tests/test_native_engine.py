@@ -488,3 +488,57 @@ def test_headline_shape_windows_match_the_oracle():
             assert pipe.eng.import_state()[5] == 2
     src.drain()
     pipe.eng.close()
+
+
+def test_expert_prior_floor_and_capped_unknown_refit_matches_the_host_model():
+    """The shipped training configuration on the device: REF's expert table as the Beta prior
+    (alpha 10), the likelihood floor of the "unknown" column and its capped prior
+    (models/train.py learned_kwargs), with the 2-fault columns -- k_refit_nb builds the same image
+    as NaiveBayes.learned(..., init, floor, cap_domain) + with_pairs, and scores the same."""
+    from llm_slo_ebpf_toolkit_amd.models import train as mtrain
+    from llm_slo_ebpf_toolkit_amd.models.bayes import SufficientStats, label_code, soft_labels, with_pairs
+    from llm_slo_ebpf_toolkit_amd.ops.engine import MODEL_DTYPE, model_bytes
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
+
+    wins, gen = windows(n_win=3, seed=67)
+    imgs = build_replay_images(wins)
+    pipe = WindowPipeline(16384, 512, 8, model="bayes_learned", user_cap=4096)
+    rb, user, spans = rings("expert")
+    src = RingWindowSource(pipe, rb, user, spans)
+    pipe.eng.set_pods(*pod_meta(gen))
+    host = SufficientStats()
+    for img in imgs:
+        codes = np.asarray(img.labels, dtype=np.int32)
+        k = src.stage(feed(img, rb, user, spans), img.n_groups, codes)["k"]
+        host.add(pipe.results(k, img.n_groups)["feat"].astype(np.float64), soft_labels(codes))
+    src.drain()
+    st = pipe.state()[0]["stats_acc"]
+    cfg = mtrain.TrainConfig()
+    kw = mtrain.learned_kwargs(cfg)
+    T, rho = 2.5, 0.3
+    model = with_pairs(NaiveBayes.learned(host, temperature=T, **kw), rho, T)
+    uncapped = NaiveBayes.learned(host, temperature=T, **dict(kw, cap_domain=None))
+    pipe.eng.restore(st, model_bytes(model), len(imgs))
+    pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"])
+    pipe.eng.set_refit(cfg.alpha, cfg.prior_pseudo, 1.0 / T, cfg.min_count, pipe.cap_dom())
+    pipe.eng.refit_now()
+    dev_img = np.frombuffer(np.asarray(pipe.eng.model_bytes(), dtype=np.uint8).tobytes(), dtype=MODEL_DTYPE)[0]
+    ref_img = np.frombuffer(model_bytes(model).tobytes(), dtype=MODEL_DTYPE)[0]
+    for f in ("w", "bias", "w2", "bias2"):
+        np.testing.assert_allclose(dev_img[f], ref_img[f], rtol=1e-9, atol=1e-12, err_msg=f)
+    np.testing.assert_array_equal(dev_img["dom_mask"], ref_img["dom_mask"])
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    u = catalog.DOMAIN_INDEX["unknown"]
+    capped = NaiveBayes.learned(host, temperature=T, **kw)
+    assert capped.bias[u] < uncapped.bias[u]  # the windows' many healthy groups: the cap bites
+
+    def dev(feat):
+        r = pipe.eng.score(np.ascontiguousarray(feat, dtype=np.float32), None)
+        return r["post"][:, :10], r["pred"]
+
+    f = np.random.default_rng(8).uniform(0, 300, (48, 16)).astype(np.float32)
+    p_dev, pred_dev = dev(f)
+    np.testing.assert_allclose(p_dev, model.posteriors(f.astype(np.float64)), rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(pred_dev, model.predict(f.astype(np.float64)))
+    pipe.eng.close()
