@@ -137,7 +137,7 @@ class WindowPipeline:
         self.shard = (int(shard[0]), int(shard[1]))
         self.nb = self.eng.buffers
         self.sig_cap, self.span_cap, self.group_cap, self.user_cap = sig_cap, span_cap, group_cap, user_cap
-        if comm is not None and comm[2] > 1:
+        if comm is not None and comm[2] >= 1:  # (uid, rank, world); world 1 = a one-rank communicator
             self.eng.init_comm(comm[0], comm[1], comm[2])
         p0 = np.zeros((16, 16), dtype=np.float64)
         p0[:, :N_DOMAINS] = NaiveBayes.random_init_table(seed)

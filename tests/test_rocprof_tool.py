@@ -1,6 +1,7 @@
 """rocprofiler-sdk tool library (probes/rocprof): a GPU workload with the tool loaded pushes
 GPU signal records into the agent's shared-memory ring (no root, no BPF)."""
 
+import functools
 import os
 import subprocess
 import sys
@@ -292,18 +293,33 @@ print("waits", ok.value, no.value, flush=True)
 """
 
 
+@functools.lru_cache(maxsize=1)
+def _my_gpu_ids():
+    """KFD gpu_ids of the GPUs this process opened (its own /sys/class/kfd/kfd/proc/<pid>/stats_<id>):
+    the box's other GPUs -- and other tenants' processes on them -- are not this test's GPU."""
+    import torch
+
+    torch.zeros(1, device="cuda")  # the process's KFD entry exists once the runtime opened the GPU
+    d = f"/sys/class/kfd/kfd/proc/{os.getpid()}"
+    return {e[len("stats_"):] for e in os.listdir(d) if e.startswith("stats_")} if os.path.isdir(d) else set()
+
+
 def _kfd_waves():
-    """{KFD process entry: waves it holds on the GPUs} over /sys/class/kfd (every process)."""
+    """{KFD process entry: waves it holds on this process's GPUs} over /sys/class/kfd (every
+    process on the node; only the stats_<gpu_id> of our own GPUs count)."""
     import glob
 
+    mine = _my_gpu_ids()
     out = {}
     for f in glob.glob("/sys/class/kfd/kfd/proc/*/stats_*/cu_occupancy"):
+        if mine and f.split("/")[7][len("stats_"):] not in mine:
+            continue
         try:
             with open(f) as fh:
                 v = int(fh.read().strip() or 0)
         except (OSError, ValueError):
             continue
-        pid = f.split("/")[5]
+        pid = f.split("/")[6]
         out[pid] = out.get(pid, 0) + v
     return out
 
@@ -337,7 +353,7 @@ def test_cpu_starved_process_waits_are_not_gpu_contention():
 
     rt = load()
     quiet = _wait_gpu_quiet()
-    assert sum(quiet.values()) == 0, f"other processes keep waves on the GPU: {quiet}"
+    assert sum(quiet.values()) == 0, f"processes keep waves on the GPU: {quiet} (this test: {os.getpid()})"
     name = f"/mislo-test-{os.getpid()}-starved"
     ring = rt.HostRing(1 << 16, 64, name)
     cpu = sorted(os.sched_getaffinity(0))[0]
@@ -460,7 +476,7 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
 
     rt = load()
     quiet = _wait_gpu_quiet()  # the previous test's workload may still hold waves
-    assert sum(quiet.values()) == 0, f"other processes keep waves on the GPU: {quiet}"
+    assert sum(quiet.values()) == 0, f"processes keep waves on the GPU: {quiet} (this test: {os.getpid()})"
     name = f"/mislo-test-{os.getpid()}-foreign"
     ring = rt.HostRing(1 << 16, 64, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000000",
