@@ -22,6 +22,7 @@ Two engines share one process, one Prometheus registry and one set of outputs:
 
 from __future__ import annotations
 
+import collections
 import math
 import os
 import sys
@@ -39,7 +40,7 @@ from ..contracts import validator
 from ..contracts.types import Evidence, FaultHypothesis, IncidentAttribution, ProbeEventV1, SLOImpact
 from ..export.otel import OTLPLogExporter
 from ..export.prometheus import MetricsServer
-from ..export.webhook import WebhookExporter
+from ..export.webhook import AsyncWebhook, WebhookExporter
 from ..models.bayes import NaiveBayes
 from ..models.sample import FaultSample
 from ..safety import OverheadGuard, RateLimiter
@@ -145,6 +146,10 @@ class AgentOptions:
     webhook_secret: str = ""
     webhook_format: str = "generic"
     webhook_timeout_ms: int = 5000
+    webhook_queue: int = 256             # attributions waiting for delivery; more are dropped (reason "emit")
+    emit_min_burn: float = 1.0           # attribute a group only while its SLO burns at least this (x budget rate)
+    emit_wait_ms: int = 250              # after a cut, wait up to this long for the window's results (0 = emit
+                                         # window k at cut k+1)
     capability_mode: str = "auto"
     disable_signals: List[str] = field(default_factory=list)
     disable_overhead_guard: bool = False
@@ -232,6 +237,10 @@ class Agent:
         self.webhook = WebhookExporter(wh_url, wh_secret, wh_fmt, wh_to) if wh_url else None
         self.bayes = NaiveBayes.ref() if self.webhook is not None else None
         self.metrics = AgentMetrics(opts.event_kind, self.mode, self.supported, self.generator.enabled_signals())
+        # deliveries leave on their own thread: the window clock never waits on the endpoint
+        self.webhook_q = AsyncWebhook(self.webhook, maxsize=opts.webhook_queue,
+                                      on_drop=lambda reason: self.metrics.inc_dropped("emit"),
+                                      log=lambda m: print(m, file=sys.stderr)) if self.webhook is not None else None
         self.server: Optional[MetricsServer] = None
         self.limiter = RateLimiter(self.cfg.sampling.events_per_second_limit)
         # the window engine evaluates the guard every window: REF's formula over a 30 s horizon
@@ -252,6 +261,9 @@ class Agent:
                                        short=max(1, int(round(30_000 / max(opts.window_ms, 1)))))
         self.receiver = None
         self.attributions_emitted = 0
+        # cut -> emission time of every window (ms): the agent's own share of detection delay
+        self.emit_lag_ms: "collections.deque" = collections.deque(maxlen=4096)
+        self.cut_skew_ms: "collections.deque" = collections.deque(maxlen=4096)
 
     # ---- lifecycle ------------------------------------------------------------------------
     def start_server(self) -> Optional[MetricsServer]:
@@ -265,6 +277,8 @@ class Agent:
         self.stop_event.set()
         try:
             self.writers.close()
+            if self.webhook_q is not None:
+                self.webhook_q.close()
         finally:
             if self.server is not None:
                 self.server.stop()
@@ -338,10 +352,7 @@ class Agent:
                              namespace=self.o.namespace, service=self.o.service, fault_label=sample.fault_label,
                              confidence=0.9, burn_rate=2.0, window_minutes=5, request_id=sample.request_id,
                              trace_id=sample.trace_id)
-            try:
-                self.webhook.send(self.bayes.attribute_sample(fs))
-            except Exception as exc:  # noqa: BLE001
-                print(f"webhook send failed: {exc}", file=sys.stderr)
+            self.webhook_q.send(self.bayes.attribute_sample(fs))
         self._guard_tick()
         self.metrics.set_heartbeat(t_ns / 1e9)
 
@@ -560,10 +571,19 @@ class Agent:
                 return
 
     def _attributions(self, G: int, names: Sequence[str], res: dict, t_ns: int, model) -> List[IncidentAttribution]:
-        """One IncidentAttribution per incident group whose top posterior clears min_confidence.
-        Evidence carries the group's measured signal values (mean over joined kernel signals);
-        SLO impact comes from the group's spans (TTFT SLO breach fraction over the error budget =
-        burn rate, forecast over the next 5 minutes from the recent windows), not from constants."""
+        """One IncidentAttribution per incident group with SLO impact whose top posterior clears
+        min_confidence. Evidence carries the group's measured signal values (mean over joined
+        kernel signals); SLO impact comes from the group's spans (TTFT SLO breach fraction over the
+        error budget = burn rate, forecast over the next 5 minutes from the recent windows), not
+        from constants.
+
+        Emission is gated on SLO impact: a group is attributed only while its SLO burns its error
+        budget at least ``emit_min_burn`` times the sustainable rate (the forecast burn over the
+        recent windows, >= 1 by default: SRE burn-rate alerting), so "unknown" never leaves at zero
+        burn and one slow request among a few does not page. Every scored group still counts in
+        ``llm_slo_agent_incidents_scored_total{domain, emitted}``; a healthy node emits nothing (REF
+        posts every tick, cmd/agent/main.go:567-585 -- with a webhook configured that pages on
+        every healthy window)."""
         out = []
         D = model.weights.shape[1]
         post, bits, feat = res["post"], res["evbits"].view(np.uint32), res["feat"]
@@ -587,6 +607,12 @@ class Agent:
             if not ranked or ranked[0].posterior < self.o.min_confidence:
                 continue
             top = ranked[0]
+            burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
+            # (1 - 1e-9: the budget 1 - target is not exact in binary, a burn of exactly 1 lands a hair under)
+            emit = sli is None or (burn > 0 and burn >= self.o.emit_min_burn * (1.0 - 1e-9))
+            self.metrics.observe_incident(top.domain, emit)
+            if not emit:
+                continue
             ev = []
             for sname in top.evidence:
                 spec = catalog.BY_NAME[sname]
@@ -594,7 +620,6 @@ class Agent:
                 ev.append(Evidence(spec.semconv or sname, round(v, 3) if math.isfinite(v) else "elevated", "ebpf"))
             if not ev:
                 ev = [Evidence("llm.ebpf.correlation_confidence", float(top.posterior), "ebpf")]
-            burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
             out.append(IncidentAttribution(
                 incident_id=f"gpu-{t_ns}-{g:03d}", timestamp=t_ns, cluster=self.o.cluster,
                 namespace=self.o.namespace, service=names[g] if g < len(names) else f"group-{g}",
@@ -629,14 +654,11 @@ class Agent:
             self.metrics.observe_attribution(attr.predicted_fault_domain)
             self.writers.emit_attribution(attr)
             self.attributions_emitted += 1
-            if self.webhook is not None:
-                try:
-                    self.webhook.send(attr)
-                except Exception as exc:  # noqa: BLE001
-                    self.metrics.inc_dropped("emit")
-                    print(f"webhook send failed: {exc}", file=sys.stderr)
+            if self.webhook_q is not None:
+                self.webhook_q.send(attr)  # enqueued; delivered on the webhook thread
         if attrs:
             self.writers.flush()  # a window's incidents leave with the window (detection delay)
+        self.emit_lag_ms.append(1e-6 * (time.time_ns() - t_ns))
 
     def _restart_workers(self, exc, rings, sets, maps, G: int):
         """A worker died or stopped answering: its communicator is broken for every worker. Stop
@@ -857,6 +879,7 @@ class Agent:
                 self.stop_event.wait(max(0.0, nxt - time.monotonic()))
                 if self.stop_event.is_set():
                     break
+                self.cut_skew_ms.append(1e3 * (time.monotonic() - nxt))  # how late the cut is on its schedule
                 nxt += period
                 t = time.time_ns()
                 maps.cfg_set(bpf.CFG_EPOCH, clock.publish(t))  # epoch first, then the ring snapshots
@@ -881,6 +904,19 @@ class Agent:
                 cut_t[replies[0]["k"]] = t
                 for parts in joiner.add(replies):
                     self._emit_window(parts, cut_t.pop(parts[0]["k"], t), G, names, ring, model)
+                if o.emit_wait_ms > 0:
+                    # window k leaves as soon as every worker's chain is done (~ms after the cut),
+                    # not with the next cut: one window period less detection delay
+                    wait = min(o.emit_wait_ms / 1000.0, max(0.0, nxt - time.monotonic() - 0.01))
+                    try:
+                        got = pool.collect(wait)
+                    except WorkerError as exc:
+                        pool, split = self._restart_workers(exc, (ring, user, spans), sets, maps, G)
+                        cut_t.clear()
+                        joiner.reset(len(self.specs))
+                        continue
+                    for parts in joiner.add(got):
+                        self._emit_window(parts, cut_t.pop(parts[0]["k"], t), G, names, ring, model)
                 if self.windows_done and self.windows_done % 64 == 0 and o.source == "bpf":
                     self._scan_pods(maps)  # pod churn
                     if getattr(self, "bpf_loader", None) is not None:

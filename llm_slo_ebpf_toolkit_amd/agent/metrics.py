@@ -54,6 +54,9 @@ class AgentMetrics:
                                        (0.5, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000))
         self.attr = r.counter("llm_slo_agent_attributions_total", "Incident attributions by predicted domain.",
                               ("domain",))
+        self.scored = r.counter("llm_slo_agent_incidents_scored_total",
+                                "Incident groups scored per window by top domain, and whether an attribution was "
+                                "emitted (only groups with SLO impact are).", ("domain", "emitted"))
         self.corr = r.counter("llm_slo_agent_correlation_pairs_total",
                               "Span/signal correlation outcomes (REF DebugStats) from the join kernel.", ("outcome",))
         self.ring_dropped = r.gauge("llm_slo_agent_ring_dropped_events", "Events dropped by full producer rings.")
@@ -159,3 +162,6 @@ class AgentMetrics:
 
     def observe_attribution(self, domain: str) -> None:
         self.attr.inc(1, domain)
+
+    def observe_incident(self, domain: str, emitted: bool) -> None:
+        self.scored.inc(1, domain, "true" if emitted else "false")

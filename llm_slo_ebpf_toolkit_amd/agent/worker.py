@@ -209,6 +209,22 @@ class WorkerCore:
         self.windows += 1
         return out
 
+    def collect(self, timeout_s: float) -> dict:
+        """Every staged window whose chain finishes within ``timeout_s`` (oldest first), polled --
+        the controller's early emission: window k leaves as soon as the device is done with it,
+        not at the next cut. A window still computing at the deadline stays pending (the next
+        ``window`` or ``collect`` takes it)."""
+        deadline = time.perf_counter() + max(0.0, float(timeout_s))
+        prevs = []
+        while self.pending:
+            k = self.pending[0][0]
+            while not self.pipe.eng.query(k):
+                if time.perf_counter() >= deadline:
+                    return {"rank": self.spec.rank, "prevs": prevs}
+                time.sleep(2e-4)
+            prevs.append(self._collect(*self.pending.popleft()))
+        return {"rank": self.spec.rank, "prevs": prevs}
+
     def _collect(self, k: int, host_us: float, n_groups: int) -> dict:
         pipe = self.pipe
         t0 = time.perf_counter()
@@ -275,6 +291,8 @@ def worker_main(spec: WorkerSpec, conn) -> None:
             msg = conn.recv()
             if msg[0] == "window":
                 conn.send(("window", core.window(*msg[1:])))
+            elif msg[0] == "collect":
+                conn.send(("collect", core.collect(*msg[1:])))
             elif msg[0] == "stop":
                 conn.send(("stopped", core.stop()))
                 break
@@ -363,6 +381,8 @@ class LocalWorker:
     def send(self, msg) -> None:
         if msg[0] == "window":
             self._reply = ("window", self.core.window(*msg[1:]))
+        elif msg[0] == "collect":
+            self._reply = ("collect", self.core.collect(*msg[1:]))
         elif msg[0] == "stop":
             self._reply = ("stopped", self.core.stop())
 
@@ -425,6 +445,21 @@ class WorkerPool:
                 w.send(("window", c, groups_of(w.spec.rank, self.world, n_groups), pods))
             except (OSError, BrokenPipeError) as exc:
                 raise WorkerError(f"worker {w.spec.rank} is gone ({exc})", w.spec.rank) from exc
+        replies = self._gather(timeout)
+        self._release(replies)
+        return replies
+
+    def collect(self, wait_s: float, timeout: float = 600.0) -> List[dict]:
+        """Every worker's windows that finish within ``wait_s`` (WorkerCore.collect): the
+        controller emits window k as soon as every worker is done with it."""
+        for w in self.workers:
+            try:
+                w.send(("collect", float(wait_s)))
+            except (OSError, BrokenPipeError) as exc:
+                raise WorkerError(f"worker {w.spec.rank} is gone ({exc})", w.spec.rank) from exc
+        return self._gather(max(timeout, wait_s + 30.0))
+
+    def _gather(self, timeout: float) -> List[dict]:
         replies: List[Optional[dict]] = [None] * self.world
         deadline = time.monotonic() + timeout
         while any(r is None for r in replies):
@@ -442,7 +477,6 @@ class WorkerPool:
                 late = next(i for i, r in enumerate(replies) if r is None)
                 raise WorkerError(f"worker {late} did not answer in {timeout:.0f} s", late)
             time.sleep(0.0005)
-        self._release(replies)
         return replies
 
     def dead_ranks(self) -> List[int]:

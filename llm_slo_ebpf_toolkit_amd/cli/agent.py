@@ -102,6 +102,11 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("halo-ms", d.halo_ms, "gpu engine: records this close to a window's end also join the next window (0 = off)"),
         ("state-dir", d.state_dir, "gpu engine: checkpoint directory for the learned state (resumed on start)"),
         ("checkpoint-every", d.checkpoint_every, "gpu engine: windows between checkpoints"),
+        ("emit-wait-ms", d.emit_wait_ms, "gpu engine: after a cut, wait up to this long for the window's results "
+                                         "and emit them at once (0 = with the next cut)"),
+        ("webhook-queue", d.webhook_queue, "attributions queued for webhook delivery (more are dropped)"),
+        ("emit-min-burn", d.emit_min_burn, "gpu engine: attribute an incident group only while its SLO burn rate "
+                                           "(error-budget multiples) is at least this"),
         ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; the flag given on the "
                              "command line wins over the env, the default does not; "
                              "each MI355X queue pins ~173 MB of host memory; 1 serialises copy and compute, ample "
@@ -129,7 +134,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         procfs_interval_ms=int(a.procfs_interval_ms), procfs_cpu_psi=bool(a.procfs_cpu_psi),
         kfd_sampler=a.kfd_sampler,
         model_signals=a.model_signals,
-        pair_prior=float(a.pair_prior))
+        pair_prior=float(a.pair_prior), emit_wait_ms=int(a.emit_wait_ms), webhook_queue=int(a.webhook_queue),
+        emit_min_burn=float(a.emit_min_burn))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])
         if given:  # an operator's flag wins over a node-wide GPU_MAX_HW_QUEUES

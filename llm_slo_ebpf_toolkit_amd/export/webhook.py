@@ -142,3 +142,67 @@ class WebhookExporter:
             except ConnectionError as exc:
                 last = exc
         raise ConnectionError(f"webhook delivery failed after {self.max_retry} attempts: {last}")
+
+
+class AsyncWebhook:
+    """Webhook delivery off the caller's thread: a bounded queue and one sender thread.
+
+    REF's agent posts inside its tick (cmd/agent/main.go:567-585), so one hung endpoint -- 5 s
+    timeout x 3 attempts plus 1 s + 2 s backoff (exporter.go:63-85) -- stalls the tick by ~18 s per
+    attribution. The window agent's clock must not wait on a pager: ``send`` only enqueues; a full
+    queue drops the attribution and calls ``on_drop`` (the agent counts it as
+    ``llm_slo_agent_dropped_events_total{reason="emit"}``, as REF counts a failed delivery), and so
+    does a delivery that fails after the exporter's retries."""
+
+    def __init__(self, exporter: WebhookExporter, maxsize: int = 256,
+                 on_drop: Optional[Callable[[str], None]] = None, log: Optional[Callable[[str], None]] = None):
+        import queue
+        import threading
+
+        self.exporter = exporter
+        self.q: "queue.Queue" = queue.Queue(maxsize=max(1, int(maxsize)))
+        self.on_drop = on_drop or (lambda reason: None)
+        self.log = log or (lambda msg: None)
+        self.sent = self.failed = self.dropped = 0
+        self._t = threading.Thread(target=self._run, name="mislo-webhook", daemon=True)
+        self._t.start()
+
+    def send(self, attr: IncidentAttribution) -> bool:
+        import queue
+
+        try:
+            self.q.put_nowait(attr)
+            return True
+        except queue.Full:
+            self.dropped += 1
+            self.on_drop("queue_full")
+            return False
+
+    def _run(self) -> None:
+        while True:
+            attr = self.q.get()
+            if attr is None:
+                return
+            try:
+                self.exporter.send(attr)
+                self.sent += 1
+            except Exception as exc:  # noqa: BLE001 - a delivery failure never reaches the caller
+                self.failed += 1
+                self.on_drop("failed")
+                self.log(f"webhook send failed: {exc}")
+            finally:
+                self.q.task_done()
+
+    def pending(self) -> int:
+        return self.q.unfinished_tasks
+
+    def close(self, timeout: float = 5.0) -> None:
+        """Stop after the queued deliveries (at most ``timeout`` s; the thread is a daemon)."""
+        deadline = time.monotonic() + timeout
+        while True:
+            try:
+                self.q.put(None, timeout=max(0.0, deadline - time.monotonic()))
+                break
+            except Exception:  # noqa: BLE001 - queue full past the deadline
+                break
+        self._t.join(max(0.0, deadline - time.monotonic()))

@@ -33,6 +33,9 @@ from ..signals.generator import BASE_PROFILE, FAULT_OVERRIDES, FAULT_ERRNO
 
 SCENARIOS: Dict[str, List[Tuple[str, ...]]] = {
     "baseline": [()],
+    # the same fault-free node under another name: the agent's replay source reads its REF-default
+    # --scenario "baseline" as "full" (a replay with nothing to attribute is no demo)
+    "healthy": [()],
     "dns_latency": [("dns_latency",)],
     "cpu_throttle": [("cpu_throttle",)],
     "memory_pressure": [("memory_pressure",)],
@@ -209,7 +212,7 @@ class ReplayGenerator:
         choices = SCENARIOS[cfg.scenario]
         out: List[Tuple[str, ...]] = []
         for _ in range(cfg.n_services):
-            if cfg.scenario != "baseline" and self.rng.random() < cfg.p_fault:
+            if choices != [()] and self.rng.random() < cfg.p_fault:
                 out.append(choices[int(self.rng.integers(len(choices)))])
             else:
                 out.append(())

@@ -407,8 +407,10 @@ def test_bench_runs_the_agents_worker_path_on_two_ranks(tmp_path):
     d = json.loads(out.read_text())
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
     assert "split rings" in d["topology"] and "WorkerCore.window" in d["topology"]
-    # every node-wide incident of the timed windows became an attribution on the controller
-    assert d["incidents_scored_timed_windows"] == 3 * 2 * 8 == d["attributions_emitted_timed"]
+    # every node-wide incident of the timed windows was scored; those with SLO impact (the replay's
+    # faulted groups breach the TTFT SLO) became attributions on the controller
+    assert d["incidents_scored_timed_windows"] == 3 * 2 * 8
+    assert 0 < d["attributions_emitted_timed"] <= d["incidents_scored_timed_windows"]
     assert d["host_epilogue_us_per_window"] > 0
 
 
@@ -426,7 +428,8 @@ def test_bench_trains_the_learned_model_on_the_host_engine(tmp_path):
     d = json.loads(out.read_text())
     assert d["training"]["windows"] == 8 and d["training"]["incidents_trained"] > 0
     assert d["macro_f1_timed_windows"] >= 0.9
-    assert d["attributions_emitted_timed"] == d["incidents_scored_timed_windows"] == 3 * 16
+    assert d["incidents_scored_timed_windows"] == 3 * 16
+    assert 0 < d["attributions_emitted_timed"] <= d["incidents_scored_timed_windows"]
 
 
 def test_prev_joiner_emits_windows_once_every_worker_reported_them():
