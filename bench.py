@@ -16,7 +16,9 @@ the finished windows' packets and node-wide incident results) with rank 0 also r
 controller's per-window host epilogue (``Agent._emit_window``: metrics, IncidentAttributions,
 output) over them, measured on its own.
 
-One step = one collection window per GPU, exactly as the agent runs it:
+One step = one collection window per GPU, exactly as the agent's workers run it (the controller's
+per-window epilogue -- metrics, attributions, outputs -- is run over the same windows after the
+timed region and reported as host_epilogue_us_per_window):
 
   producer process (stands in for the kernel: the probes' records, already framed as the BPF
   ring buffer holds them, plus the rocprofiler tool's GPU-signal records and the spans)
@@ -740,8 +742,9 @@ def main() -> int:
         "windows_prefilled": prefilled,
         "producer_wait_ms_total": round(producer_wait_ms, 2),
         "host_numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
-        # the controller's per-window epilogue on rank 0, inside the timed region (agent/daemon.py
-        # Agent._emit_window over the node-wide results the worker path collected)
+        # the controller's per-window epilogue on rank 0 (agent/daemon.py Agent._emit_window over the
+        # node-wide results the timed steps collected), run and timed AFTER the timed region: it is
+        # not part of ms_per_step
         "host_epilogue_us_per_window": round(1e6 * epi[0] / max(epi[1], 1), 1),
         # the worker's host loop per timed step: all of it, collecting finished windows (packet and
         # results reads), and of that the time blocked waiting for a window's chain to finish
@@ -751,8 +754,10 @@ def main() -> int:
         "attributions_emitted_timed": int(attributions_emitted),
         "topology": (f"agent --gpus {world}: one window worker per GPU on split rings (its own kernel / user-space / "
                      f"span rings, producers routing by service), agent/worker.py WorkerCore.window per step, "
-                     f"controller epilogue on rank 0") if world > 1 else
-                    "agent --gpus 1: one window worker (agent/worker.py WorkerCore.window per step) + the controller epilogue",
+                     f"controller epilogue on rank 0 timed separately (host_epilogue_us_per_window, not in ms_per_step)")
+        if world > 1 else
+                    "agent --gpus 1: one window worker (agent/worker.py WorkerCore.window per step); the controller "
+                    "epilogue timed separately (host_epilogue_us_per_window, not in ms_per_step)",
     }
     if rank == 0:
         line = json.dumps(res)

@@ -29,7 +29,7 @@ import sys
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -193,6 +193,42 @@ class AgentOptions:
     kfd_proc: str = "/sys/class/kfd/kfd/proc"
     model_signals: str = ""              # signals the node's sources produce (others marginalised; "" = all)
     pair_prior: float = 0.0              # 2-fault prior mass added to a table model without pairs (0 = none)
+    explicit_flags: Tuple[str, ...] = ()  # flags given on the command line (they win over the config's gpu: block)
+
+
+# the config file's gpu: block -> the agent option it sets (flag name, option field)
+GPU_CONFIG_FLAGS = (("window_ms", "window-ms", "window_ms"),
+                    ("max_events_per_window", "window-events", "window_events"),
+                    ("world_size", "gpus", "gpus"),
+                    ("attribution_model", "model", "model"))
+
+
+def apply_gpu_config(opts: "AgentOptions", gpu) -> "AgentOptions":
+    """The toolkit config's ``gpu:`` block (window_ms, max_events_per_window, world_size,
+    attribution_model, enabled) as the window engine's settings; a flag given on the command line
+    wins, with a warning when it disagrees (REF: CLI overrides config, cmd/agent/main.go:426-440).
+    ``enabled: false`` runs REF's tick loop (engine synthetic) unless --engine was given. A learned
+    ``attribution_model`` needs --model-path, so with none the config's model is not taken."""
+    from dataclasses import replace
+
+    given = set(opts.explicit_flags)
+    upd = {}
+    for key, flag, field_ in GPU_CONFIG_FLAGS:
+        v = getattr(gpu, key)
+        if key == "attribution_model" and (opts.model_path or v not in ("bayes", "bayes_gpu")):
+            continue
+        if flag in given:
+            if v != getattr(opts, field_):
+                print(f"config gpu.{key}={v!r} overridden by --{flag}={getattr(opts, field_)!r}", file=sys.stderr)
+            continue
+        upd[field_] = type(getattr(opts, field_))(v)
+    if not gpu.enabled:
+        if "engine" in given:
+            if opts.engine in ("gpu", "cpu"):
+                print(f"config gpu.enabled=false overridden by --engine={opts.engine}", file=sys.stderr)
+        else:
+            upd["engine"] = "synthetic"
+    return replace(opts, **upd) if upd else opts
 
 
 def choose_enabled_signals(config_signals: Sequence[str], disabled: Sequence[str],
@@ -217,6 +253,7 @@ class Agent:
         if opts.config:
             try:
                 self.cfg = toolkitcfg.load(opts.config)
+                opts = self.o = apply_gpu_config(opts, self.cfg.gpu)
             except Exception as exc:  # noqa: BLE001 - REF: log and use defaults
                 print(f"config load warning ({opts.config}): {exc}; using defaults", file=sys.stderr)
         self.mode = catalog.parse_capability_mode(opts.capability_mode)
@@ -430,7 +467,15 @@ class Agent:
                     self.probe_manager.register(spec)
                 attached = self.probe_manager.attach_all()
                 print(f"attached probes for {len(attached)} signals from {o.probe_objs}", file=sys.stderr)
+                try:
+                    self.bpf_loader.load_flush()
+                except Exception as exc:  # noqa: BLE001 - reported below through flush_fd < 0
+                    print(f"WARNING: flush program not loaded: {exc}", file=sys.stderr)
             maps = bpf.BpfMaps(o.pin_dir)
+            if maps.flush_fd < 0:
+                print(f"WARNING: no flush program pinned at {o.pin_dir}/progs/mislo_flush: partial per-CPU "
+                      f"batches of quiet CPUs reach the ring only with that CPU's next events", file=sys.stderr)
+            self.metrics.flush_loaded.set(1 if maps.flush_fd >= 0 else 0)
             sets = []
             for r, names in enumerate(sets_names):
                 ring = maps.ring if r == 0 else rt.Ringbuf.open_pinned(os.path.join(o.pin_dir, f"mislo_events{r}"))
@@ -660,6 +705,26 @@ class Agent:
             self.writers.flush()  # a window's incidents leave with the window (detection delay)
         self.emit_lag_ms.append(1e-6 * (time.time_ns() - t_ns))
 
+    def _start_fresh(self, pool, maps, sets, split: bool) -> None:
+        """Spawned workers start at the rings' current positions: what the producers wrote while
+        the workers started (seconds) is skipped. Those records would be a backlog the windows
+        never work off in shared-ring mode, and once more than 3 cuts old their 2-bit epoch tags
+        decode against the wrong bases (timestamps off by whole windows). The interning maps are
+        reset first, so every id is defined again after the start point."""
+        if hasattr(maps, "reset_definitions"):
+            try:
+                maps.reset_definitions(len(pool.workers) if split else 1)
+            except OSError as exc:
+                print(f"id redefinition at the workers' start failed: {exc}", file=sys.stderr)
+        maps.flush_cpus()
+        pos = [(int(rs[0].producer_pos) if rs[0] is not None else 0, int(rs[1].head) if rs[1] is not None else 0,
+                int(rs[2].head) if rs[2] is not None else 0) for rs in sets]
+        skipped = sum(p[0] - int(rs[0].consumer_pos) for p, rs in zip(pos, sets) if rs[0] is not None)
+        pool.start_at(pos[:len(pool.workers)] if split else pos[0])
+        if skipped > 0:
+            print(f"window workers start at the rings' current positions ({skipped} kernel-ring bytes written "
+                  f"while they started are skipped)", file=sys.stderr)
+
     def _restart_workers(self, exc, rings, sets, maps, G: int):
         """A worker died or stopped answering: its communicator is broken for every worker. Stop
         them all and start fresh processes for the surviving GPUs -- a new communicator (RCCL id,
@@ -699,12 +764,18 @@ class Agent:
             pods, sh = self.router.resize(N if split else 1)
             if hasattr(maps, "set_shards") and len(pods):
                 maps.set_shards(pods, sh)
+
         if self.pod_table:  # every new worker starts with the pods' services known so far
             keys = np.array(sorted(self.pod_table), dtype=np.uint32)
             specs = [replace(s, pods=(keys, np.array([self.pod_table[k] for k in keys.tolist()], dtype=np.uint32)))
                      for s in specs]
         self.pool = WorkerPool(specs, rings, in_process=False)
         self.specs = specs
+        # the new workers' context / trace tables start empty: the interning maps are reset (the
+        # replay producer re-interns and re-routes) and the workers start at the rings' current
+        # positions -- the windows in flight when the worker died are lost, not re-read with ids
+        # the new workers never saw defined
+        self._start_fresh(self.pool, maps, sets, split)
         self.metrics.worker_restarts.inc()
         self.metrics.workers.set(N)
         return self.pool, split
@@ -776,6 +847,8 @@ class Agent:
         pool = WorkerPool(specs, (ring, user, spans), in_process=N == 1)
         self.pool = pool
         self.specs = specs
+        if N > 1:  # spawned workers: the records written while they started are skipped
+            self._start_fresh(pool, maps, sets, split)
         self.metrics.workers.set(N)
         print(f"window engine: {o.engine} x {N} worker(s){' on split rings' if split else ''}, model "
               f"{self.model_meta.get('name')}"
@@ -850,7 +923,7 @@ class Agent:
         if use_kfd:
             loader = getattr(self, "bpf_loader", None)
             bpf_gpu = loader is not None and "gpu_kfd" in loader.available()
-            finder = kfd.hip_map_finder(lambda: loader.loaded("gpu_kfd")) if bpf_gpu else None
+            finder = kfd.hip_map_finder(lambda: loader.is_loaded("gpu_kfd")) if bpf_gpu else None
             kfds = [kfd.KfdSampler(user if router is None else sets[r][1],
                                    targets if router is None else shard_targets(r), node_id=node_id,
                                    kfd_proc=o.kfd_proc, refresh_s=10.0 if not static else 3600.0, hip_map=finder,
@@ -879,11 +952,20 @@ class Agent:
                 self.stop_event.wait(max(0.0, nxt - time.monotonic()))
                 if self.stop_event.is_set():
                     break
-                self.cut_skew_ms.append(1e3 * (time.monotonic() - nxt))  # how late the cut is on its schedule
+                now = time.monotonic()
+                self.cut_skew_ms.append(1e3 * (now - nxt))  # how late the cut is on its schedule
                 nxt += period
+                if now > nxt:
+                    # a stall of more than a period (a worker restart, a paused process): the missed
+                    # cuts are not made up back to back -- windows of a fraction of a period each --
+                    # the schedule restarts from now
+                    missed = int((now - nxt) // period) + 1
+                    nxt += missed * period
+                    self.metrics.windows_skipped.inc(missed)
                 t = time.time_ns()
                 maps.cfg_set(bpf.CFG_EPOCH, clock.publish(t))  # epoch first, then the ring snapshots
                 maps.flush_cpus()  # every CPU's staged batches onto the rings before the snapshots
+                self.metrics.flush_errors.set(float(getattr(maps, "flush_errors", 0)))
                 bases = clock.bases()
                 cuts = [Cut(kernel=rs[0].producer_pos, user=rs[1].head, spans=rs[2].head, bases=bases, t_ns=t)
                         for rs in sets]

@@ -65,7 +65,13 @@ class AgentMetrics:
         self.ring_busy = r.counter("llm_slo_agent_ring_busy_stops_total",
                                    "Windows whose ring consumption stopped at a record still being written.")
         self.ring_backlog = r.gauge("llm_slo_agent_ring_backlog_bytes", "Unconsumed bytes in the BPF ring buffer.")
+        self.flush_loaded = r.gauge("llm_slo_agent_flush_program_loaded",
+                                    "1 when the cut's per-CPU flush program (mislo_flush) is pinned and run.")
+        self.flush_errors = r.gauge("llm_slo_agent_flush_errors",
+                                    "Per-CPU flush runs that failed (other than offline CPUs), since start.")
         self.host_us = r.gauge("llm_slo_agent_window_host_us", "Host time to assemble the last window (us).")
+        self.windows_skipped = r.counter("llm_slo_agent_windows_skipped_total",
+                                         "Window cuts skipped after the loop stalled for more than a window period.")
         self.workers = r.gauge("llm_slo_agent_window_workers", "Window workers (GPUs) the agent is running.")
         self.worker_restarts = r.counter("llm_slo_agent_worker_restarts_total",
                                          "Worker pool restarts after a worker died (the survivors' GPUs go on).")

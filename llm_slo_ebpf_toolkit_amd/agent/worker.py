@@ -209,6 +209,27 @@ class WorkerCore:
         self.windows += 1
         return out
 
+    def start_at(self, kernel: int, user: int, spans: int) -> dict:
+        """Start reading the rings at these positions (the controller's fresh start: records
+        produced while this process spawned are skipped -- older than 3 cuts, their epoch tags
+        would decode against the wrong bases -- and the ids they defined were reset). A split
+        ring set is this worker's alone: its skipped space is freed here."""
+        src = self.src
+        if src.ring is not None:
+            kernel = max(int(kernel), src.kpos)
+            src.kpos = src.kernel_done = src.kernel_seen = kernel
+            if not src.shared:
+                src.ring.set_consumer_pos(max(src.ring.consumer_pos, kernel))
+        if src.user_ring is not None:
+            du = max(0, int(user) - src.upos)
+            src.upos += du
+            src._release_user(du, 0)
+        if src.span_ring is not None:
+            ds = max(0, int(spans) - src.spos)
+            src.spos += ds
+            src._release_user(0, ds)
+        return {"rank": self.spec.rank, "done": src.done()}
+
     def collect(self, timeout_s: float) -> dict:
         """Every staged window whose chain finishes within ``timeout_s`` (oldest first), polled --
         the controller's early emission: window k leaves as soon as the device is done with it,
@@ -293,6 +314,8 @@ def worker_main(spec: WorkerSpec, conn) -> None:
                 conn.send(("window", core.window(*msg[1:])))
             elif msg[0] == "collect":
                 conn.send(("collect", core.collect(*msg[1:])))
+            elif msg[0] == "start_at":
+                conn.send(("start_at", core.start_at(*msg[1:])))
             elif msg[0] == "stop":
                 conn.send(("stopped", core.stop()))
                 break
@@ -383,6 +406,8 @@ class LocalWorker:
             self._reply = ("window", self.core.window(*msg[1:]))
         elif msg[0] == "collect":
             self._reply = ("collect", self.core.collect(*msg[1:]))
+        elif msg[0] == "start_at":
+            self._reply = ("start_at", self.core.start_at(*msg[1:]))
         elif msg[0] == "stop":
             self._reply = ("stopped", self.core.stop())
 
@@ -458,6 +483,20 @@ class WorkerPool:
             except (OSError, BrokenPipeError) as exc:
                 raise WorkerError(f"worker {w.spec.rank} is gone ({exc})", w.spec.rank) from exc
         return self._gather(max(timeout, wait_s + 30.0))
+
+    def start_at(self, positions, timeout: float = 120.0) -> List[dict]:
+        """Every worker starts reading at ``positions`` -- one (kernel, user, spans) of the shared
+        rings, or (split rings) a list with each worker's own -- and the skipped ring space is
+        freed."""
+        for w in self.workers:
+            pos = positions[w.spec.rank] if isinstance(positions, list) else positions
+            try:
+                w.send(("start_at",) + tuple(int(x) for x in pos))
+            except (OSError, BrokenPipeError) as exc:
+                raise WorkerError(f"worker {w.spec.rank} is gone ({exc})", w.spec.rank) from exc
+        replies = self._gather(timeout)
+        self._release(replies)
+        return replies
 
     def _gather(self, timeout: float) -> List[dict]:
         replies: List[Optional[dict]] = [None] * self.world

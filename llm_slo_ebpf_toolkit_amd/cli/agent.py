@@ -135,7 +135,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         kfd_sampler=a.kfd_sampler,
         model_signals=a.model_signals,
         pair_prior=float(a.pair_prior), emit_wait_ms=int(a.emit_wait_ms), webhook_queue=int(a.webhook_queue),
-        emit_min_burn=float(a.emit_min_burn))
+        emit_min_burn=float(a.emit_min_burn),
+        explicit_flags=tuple(sorted({x.lstrip("-").split("=", 1)[0] for x in (argv if argv is not None else sys.argv[1:]) if x.startswith("-")})))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])
         if given:  # an operator's flag wins over a node-wide GPU_MAX_HW_QUEUES

@@ -33,6 +33,10 @@ import numpy as np
 from . import records
 
 CFG_CLOCK, CFG_NODE, CFG_EPOCH, CFG_TRACE_NEXT, CFG_CTX_NEXT = 0, 1, 124, 125, 126
+# replay producer control (emulated maps only; no probe reads it): (generation << 8) | ring sets in
+# use. A new generation after a worker restart makes the producer re-route over the surviving
+# workers' ring sets and re-intern every id, so the fresh workers see every definition again.
+CFG_REPLAY_CTL = 127
 PIN_DIR = "/sys/fs/bpf/mislo"
 
 
@@ -105,6 +109,12 @@ class EmulatedMaps(MapSet):
     def set_pod(self, cgroup_id: int, pod_id: int) -> None:
         self.pods[int(cgroup_id)] = int(pod_id)
 
+    def reset_definitions(self, world: int) -> None:
+        """After a worker restart: the replay producer re-routes over ``world`` ring sets and
+        re-interns every context / trace id (its next records carry the definitions again)."""
+        gen = (self.cfg_get(CFG_REPLAY_CTL) >> 8) + 1
+        self.cfg_set(CFG_REPLAY_CTL, (gen << 8) | (int(world) & 0xFF))
+
 
 class BpfMaps(MapSet):
     """The maps the loader pinned under ``pin_dir`` (needs CAP_BPF / root)."""
@@ -118,6 +128,7 @@ class BpfMaps(MapSet):
         self.cfg = rt.BpfMap(os.path.join(pin_dir, "mislo_cfg"))
         self.pods = rt.BpfMap(os.path.join(pin_dir, "mislo_pods"))
         self._ctxs = os.path.join(pin_dir, "mislo_ctxs")
+        self._traces = os.path.join(pin_dir, "mislo_traces")
         # probes/ebpf/mislo_flush.bpf.c, pinned by the loader (no attachment): run on each CPU at
         # every cut. Without it a quiet CPU's partial batch waits for that CPU's next event.
         self.flush_fd = rt.bpf_obj_get(os.path.join(pin_dir, "progs", "mislo_flush", "mislo_flush"))
@@ -162,6 +173,21 @@ class BpfMaps(MapSet):
             return
         for p, s in zip(np.asarray(pod_ids).tolist(), np.asarray(shards).tolist()):
             self._shards.update(struct.pack("<I", int(p)), struct.pack("<I", int(s)))
+
+    def reset_definitions(self, world: int) -> None:
+        """After a worker restart the fresh workers' context and trace tables are empty, and the
+        probes define an id only when they first intern it: clear both interning maps and their
+        counters, so every id is defined again -- on every ring that carries it -- by the next
+        records (kernel records would otherwise resolve to context 0, no pod)."""
+        from ..runtime import load
+
+        self.reset_ctx_ids()
+        m = load().BpfMap(self._traces)
+        keys, _ = m.items()
+        ks = m.info()["key_size"]
+        for i in range(0, len(keys), ks):
+            m.delete(keys[i:i + ks])
+        self.cfg_set(CFG_TRACE_NEXT, 0)
 
     def reset_ctx_ids(self) -> int:
         """Clear mislo_ctxs and restart its id counter (the agent does this at a window cut when
@@ -346,7 +372,22 @@ def replay_producer_main(names: RingNames, cfg_kwargs: dict, rate_eps: float, wi
     t_start = time.time_ns()
     nxt = time.perf_counter()
     j = 0
+    ctl = int(rbs[0].cfg_get(CFG_REPLAY_CTL))
     while not max_windows or j < max_windows:
+        c = int(rbs[0].cfg_get(CFG_REPLAY_CTL))
+        if c != ctl:  # a worker restart: fresh id interning, the surviving workers' ring sets
+            ctl = c
+            world = max(1, min(len(sets), c & 0xFF))
+            sims = [rt.ProbeSim(rb, records.milli_shift_table()) for rb in rbs[:world]]
+            router = ShardRouter(world)
+            router.set_pods(*pod_metadata(cfg_kwargs))
+            parts = []
+            for w in wins:
+                km = kernel_event_mask(w.events)
+                kev, uev, sp = w.events[km], w.events[~km], w.spans
+                ks, us, ss = router.pod_shard(kev["pod_id"]), router.pod_shard(uev["pod_id"]), router.span_shard(sp)
+                parts.append([(np.ascontiguousarray(kev[ks == r]), np.ascontiguousarray(uev[us == r]),
+                               np.ascontiguousarray(sp[ss == r])) for r in range(world)])
         shift = t_start + j * int(period * 1e9) - int(wins[j % len(wins)].t0_ns)
         shard_parts = []
         for r, (kev, uev, sp) in enumerate(parts[j % len(parts)]):

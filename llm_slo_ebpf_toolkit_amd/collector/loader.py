@@ -37,7 +37,17 @@ from typing import Callable, Dict, List, Optional, Sequence
 
 from .probes import ProbeSpec
 
-SHARED_MAPS = ("mislo_events", "mislo_cfg", "mislo_pods", "mislo_ctxs", "mislo_traces", "mislo_scratch")
+MISLO_SHARDS = 8  # probes/ebpf/mislo_probe.h: split rings mislo_events, mislo_events1 .. mislo_events7
+# Every map mislo_probe.h pins by name, plus the per-CPU scratch: one set for the node. Later
+# objects reuse them through `map name X pinned <pin_dir>/X`; a map missing here would fall back to
+# libbpf's PIN_BY_NAME default root (/sys/fs/bpf), not pin_dir, and a probe could end up with a
+# private shard table, staging array or split ring the agent never routes, flushes or reads.
+SHARED_MAPS = (("mislo_events", "mislo_cfg", "mislo_pods", "mislo_ctxs", "mislo_traces", "mislo_scratch",
+                "mislo_stages", "mislo_shards")
+               + tuple(f"mislo_events{n}" for n in range(1, MISLO_SHARDS)))
+# the cut's per-CPU flush of the staged batches (probes/ebpf/mislo_flush.bpf.c): loaded and pinned,
+# never attached -- the agent runs it on every CPU at each window cut (collector/bpf.py BpfMaps)
+FLUSH_PROBE = "mislo_flush"
 
 # probe object -> the catalogue signals it emits (probes/ebpf/*.bpf.c)
 PROBE_SIGNALS: Dict[str, Sequence[str]] = {
@@ -76,7 +86,7 @@ class BpfProbeLoader:
             self._uprobes = UprobeAttacher(self.pin_dir)
         return self._uprobes
 
-    def loaded(self, probe: str) -> bool:
+    def is_loaded(self, probe: str) -> bool:
         with self._lock:
             return self._refs.get(probe, 0) > 0
 
@@ -113,14 +123,28 @@ class BpfProbeLoader:
         """Probe objects present in obj_dir, in PROBE_SIGNALS order."""
         return [p for p in PROBE_SIGNALS if os.path.exists(self.obj_path(p))]
 
-    def load_cmd(self, probe: str) -> List[str]:
+    def load_cmd(self, probe: str, attach: bool = True) -> List[str]:
         cmd = [self.bpftool, "prog", "loadall", self.obj_path(probe), self.prog_dir(probe)]
         if self.maps_pinned():  # reuse the node's one set of shared maps
             for m in SHARED_MAPS:
                 cmd += ["map", "name", m, "pinned", os.path.join(self.pin_dir, m)]
         else:  # first object: its shared maps become the node's
             cmd += ["pinmaps", self.pin_dir]
-        return cmd + ["autoattach"]
+        return cmd + (["autoattach"] if attach else [])
+
+    def load_flush(self) -> bool:
+        """Load and pin the cut's flush program (no attachment) after the probes: without it a
+        quiet CPU's partial batch stays staged until 8 slots fill, and slots more than 3 cuts old
+        decode against the wrong epoch base (their 2-bit epoch tag wraps). Returns whether it is
+        pinned where BpfMaps opens it."""
+        if not os.path.exists(self.obj_path(FLUSH_PROBE)):
+            raise LoaderError(f"no flush program {self.obj_path(FLUSH_PROBE)} (make -C probes/ebpf)")
+        with self._lock:
+            os.makedirs(os.path.join(self.pin_dir, "progs"), exist_ok=True)
+            if os.path.exists(self.prog_dir(FLUSH_PROBE)):  # a previous agent's pin
+                shutil.rmtree(self.prog_dir(FLUSH_PROBE), ignore_errors=True)
+            self._run(self.load_cmd(FLUSH_PROBE, attach=False))
+        return os.path.exists(os.path.join(self.prog_dir(FLUSH_PROBE), FLUSH_PROBE))
 
     # ---- lifecycle -------------------------------------------------------------------------
     def load(self, probe: str) -> None:

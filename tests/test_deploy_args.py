@@ -188,3 +188,64 @@ def test_shipped_model_is_what_attributor_train_produces():
     r = meta["ref55"]
     assert r["single_fault_macro_f1"] >= 0.9818 and r["multi_fault_partial_accuracy"] >= 1.0
     assert r["multi_fault_coverage_accuracy"] >= 0.667
+
+
+def _mode_env(*args):
+    import subprocess
+
+    p = subprocess.run(["bash", os.path.join(ROOT, "scripts/chaos/set_agent_mode.sh"), *args],
+                       env=dict(os.environ, DRY_RUN="1"), capture_output=True, text=True)
+    return p, dict(ln.split("=", 1) for ln in p.stdout.split())
+
+
+def test_set_agent_mode_values_start_the_agent():
+    """scripts/chaos/set_agent_mode.sh (REF scripts/chaos/set_agent_mode.sh:1-37) sets the env the
+    DaemonSet's args read; every mode it accepts -- its defaults included -- must parse with the
+    agent's CLI (round 4 defaulted SOURCE=ring, which `agent --source` rejects: crash loop)."""
+    from llm_slo_ebpf_toolkit_amd.cli import agent as cli
+
+    for args in ((), ("gpu", "bpf"), ("cpu", "replay", "jsonl", "both"), ("synthetic", "shm", "stdout", "slo")):
+        p, env = _mode_env(*args)
+        assert p.returncode == 0, p.stderr
+        base, c = render_kustomize_args()
+        rendered = [re.sub(r"--(engine|source|output|event-kind)=\S*", lambda m: f"--{m.group(1)}=" + env[
+            {"engine": "ENGINE", "source": "SOURCE", "output": "OUTPUT", "event-kind": "EVENT_KIND"}[m.group(1)]], a)
+            for a in base]
+        opts, _ = cli.parse(rendered)
+        assert (opts.engine, opts.source, opts.output, opts.event_kind) == (
+            env["ENGINE"], env["SOURCE"], env["OUTPUT"], env["EVENT_KIND"])
+    p, _ = _mode_env("gpu", "ring")
+    assert p.returncode == 2 and "SOURCE must be one of" in p.stderr
+
+
+def test_config_gpu_block_sets_the_window_engine_and_flags_win():
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import AgentOptions, apply_gpu_config
+    from llm_slo_ebpf_toolkit_amd.cli import agent as cli
+    from llm_slo_ebpf_toolkit_amd.contracts.config import GPUConfig
+
+    gpu = GPUConfig(enabled=True, window_ms=500, max_events_per_window=4096, world_size=2, attribution_model="bayes_gpu")
+    o, _ = cli.parse(["--engine=gpu"])
+    o2 = apply_gpu_config(o, gpu)
+    assert (o2.window_ms, o2.window_events, o2.gpus, o2.model) == (500, 4096, 2, "bayes_gpu")
+    o, _ = cli.parse(["--engine=gpu", "--window-ms=1000", "--gpus=1"])
+    o2 = apply_gpu_config(o, gpu)
+    assert (o2.window_ms, o2.gpus, o2.window_events) == (1000, 1, 4096)
+    # a learned model comes from --model-path only
+    o2 = apply_gpu_config(cli.parse(["--model-path=x.safetensors"])[0], gpu)
+    assert o2.model == AgentOptions().model
+    o2 = apply_gpu_config(cli.parse([])[0], GPUConfig(enabled=False))
+    assert o2.engine == "synthetic"
+    assert apply_gpu_config(cli.parse(["--engine=gpu"])[0], GPUConfig(enabled=False)).engine == "gpu"
+
+
+def test_shipped_gpu_block_agrees_with_the_flags_the_deployments_pass():
+    docs = {}
+    with open(os.path.join(ROOT, "deploy/k8s/configmap.yaml")) as fh:
+        cm = yaml.safe_load(fh)
+    cfg = yaml.safe_load(cm["data"]["toolkit.yaml"])
+    assert cfg["gpu"]["world_size"] == int(cm["data"]["GPUS"])
+    with open(os.path.join(ROOT, "charts/llm-slo-agent/values.yaml")) as fh:
+        values = yaml.safe_load(fh)
+    assert values["config"]["gpu"]["world_size"] == values["agent"]["gpus"]
+    assert cfg["gpu"]["attribution_model"] in ("bayes", "bayes_gpu")
+    assert values["config"]["gpu"]["attribution_model"] in ("bayes", "bayes_gpu")

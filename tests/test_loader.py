@@ -17,9 +17,10 @@ class FakeBpftool:
 
     def __call__(self, cmd):
         self.cmds.append(cmd)
-        assert cmd[1:3] == ["prog", "loadall"] and cmd[-1] == "autoattach"
+        assert cmd[1:3] == ["prog", "loadall"]
+        assert cmd[-1] == "autoattach" or cmd[3].endswith("mislo_flush.bpf.o")
         os.makedirs(cmd[4], exist_ok=True)
-        open(os.path.join(cmd[4], "link0"), "w").close()
+        open(os.path.join(cmd[4], "link0" if cmd[-1] == "autoattach" else os.path.basename(cmd[4])), "w").close()
         if "pinmaps" in cmd:
             d = cmd[cmd.index("pinmaps") + 1]
             for m in SHARED_MAPS:
@@ -98,3 +99,37 @@ def test_missing_object_is_an_error(tmp_path):
     with pytest.raises(LoaderError):
         ld.load("dns_latency")
     assert ld.available() == []
+
+
+def test_every_pinned_map_of_the_probe_header_is_shared():
+    """maps pinned by name in mislo_probe.h but missing from SHARED_MAPS fall back to
+    libbpf's default pin root, not pin_dir, and later objects get private copies."""
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "llm_slo_ebpf_toolkit_amd/probes/ebpf/mislo_probe.h")) as fh:
+        text = fh.read()
+    shards = int(re.search(r"#define MISLO_SHARDS (\d+)", text).group(1))
+    pinned = set()
+    for m in re.finditer(r"struct \{(.*?)\}\s*(\w+)\s*SEC\(\"\.maps\"\)", text, re.S):
+        if "LIBBPF_PIN_BY_NAME" in m.group(1):
+            pinned.add(m.group(2))
+    if "MISLO_SHARD_RING" in text:
+        pinned |= {f"mislo_events{n}" for n in range(1, shards)}
+    assert pinned and pinned <= set(SHARED_MAPS), sorted(pinned - set(SHARED_MAPS))
+
+
+def test_the_flush_program_is_loaded_pinned_and_never_attached(tmp_path):
+    from llm_slo_ebpf_toolkit_amd.collector.loader import FLUSH_PROBE
+
+    fake = FakeBpftool()
+    pin = str(tmp_path / "bpf")
+    os.makedirs(pin)
+    ld = BpfProbeLoader(_objs(tmp_path, ["dns_latency", FLUSH_PROBE]), pin, run=fake)
+    ld.load("dns_latency")
+    assert ld.load_flush()
+    cmd = fake.cmds[-1]
+    assert cmd[3].endswith("mislo_flush.bpf.o") and "autoattach" not in cmd
+    assert [cmd[i + 2] for i, a in enumerate(cmd) if a == "map"] == list(SHARED_MAPS)  # the node's maps
+    assert os.path.exists(os.path.join(pin, "progs", FLUSH_PROBE, FLUSH_PROBE))  # where BpfMaps opens it
+    assert FLUSH_PROBE not in ld.available()  # not a signal probe: shedding never detaches it

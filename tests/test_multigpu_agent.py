@@ -338,6 +338,7 @@ def test_agent_survives_a_worker_killed_mid_run(tmp_path, split):
     communicator, and keeps emitting schema-valid attributions for every service."""
     code = f"""
 import io, json, os, signal, sys, threading, time
+import numpy as np
 sys.path.insert(0, {ROOT!r})
 from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
 from llm_slo_ebpf_toolkit_amd.contracts import validator
@@ -357,6 +358,16 @@ if __name__ == "__main__":
         os.kill(victim, signal.SIGKILL)
 
     threading.Thread(target=killer, daemon=True).start()
+    # kernel-ring records (context ids the fresh workers must learn again): per window, the incident
+    # groups whose features hold a DNS value (a kernel-ring signal resolved to its pod's service)
+    kern = []
+    orig = a._attributions
+
+    def spy(G, names, res, t_ns, model):
+        kern.append((a.metrics.worker_restarts.value(), int(np.isfinite(res["feat"][:, 0]).sum())))
+        return orig(G, names, res, t_ns, model)
+
+    a._attributions = spy
     rc = a.run_windows(max_windows=10)
     recs = [json.loads(x) for x in out.getvalue().splitlines()]
     schema = validator.compiled("incident-attribution")
@@ -364,7 +375,8 @@ if __name__ == "__main__":
     after = [r for r in recs if int(r["incident_id"].split("-")[1]) > 0]
     print(json.dumps({{"rc": rc, "n": len(recs), "services": sorted({{r["service"] for r in recs}}),
                       "windows": a.windows_done, "workers": len(a.pool.workers), "killed": killed,
-                      "restarts": a.metrics.worker_restarts.value(), "gauge": a.metrics.workers.value()}}))
+                      "restarts": a.metrics.worker_restarts.value(), "gauge": a.metrics.workers.value(),
+                      "kern": kern}}))
     a.close()
 """
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280, cwd=str(tmp_path))
@@ -374,6 +386,11 @@ if __name__ == "__main__":
     assert d["rc"] == 0 and d["restarts"] == 1 and d["workers"] == 2 and d["gauge"] == 2
     assert d["windows"] == 10 and d["n"] > 0 and len(d["services"]) >= 4
     assert "restarting on 2 worker(s)" in p.stderr
+    # after the restart the ids are defined again, so kernel-ring records keep resolving
+    # to their pods' services (not context 0): past the restart's transition (the producers switch
+    # over at their next window) every window joins DNS records to groups
+    after = [n for r, n in d["kern"] if r >= 1]
+    assert len(after) >= 4 and min(after[2:]) > 0, d["kern"]
 
 
 def test_windows_that_wrap_the_bpf_ring_equal_unwrapped_windows():
