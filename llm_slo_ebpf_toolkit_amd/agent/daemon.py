@@ -932,7 +932,9 @@ class Agent:
             for k in kfds:
                 k.start()
             self.kfd = kfds
-            sampler = procfs.MultiSampler(([sampler] if sampler is not None else []) + kfds)
+        # the ladder's sampler stage sheds the procfs signals only: the KFD samplers emit
+        # gpu_queue_delay_ms into the user rings and obey their drop mask -- the GPU stage, one
+        # signal at a time -- so the procfs stage never pauses them
         from ..safety import ShedLadder
 
         self.ladder = ShedLadder(catalog.DISABLE_ORDER, maps=maps, sampler=sampler, user_ring=[x[1] for x in sets],
@@ -1026,6 +1028,8 @@ class Agent:
             self.pool.close()
             if sampler is not None:
                 sampler.stop()
+            for k in getattr(self, "kfd", None) or []:
+                k.stop()
             if receiver is not None:
                 receiver.stop()
             if getattr(self, "probe_manager", None) is not None:

@@ -146,7 +146,10 @@ struct State {
   rocprofiler_client_id_t* client = nullptr;
   rocprofiler_context_id_t ctx{};
   rocprofiler_buffer_id_t buffer{};
-  void* ring = nullptr;                // the ring records go to now (rings[shard])
+  // the ring records go to now (rings[shard]): route() switches it on the sampler thread while the
+  // callback threads emit, so each emit() loads it once and uses that ring for both the drop-mask
+  // check and the push
+  std::atomic<void*> ring{nullptr};
   std::vector<void*> rings;            // MISLO_RING's rings, one per window worker
   const uint8_t* shard_table = nullptr;  // pod id -> shard (MISLO_SHARD_TABLE), 2^20 bytes
   int64_t clock_offset = 0;  // realtime - rocprofiler timestamp
@@ -242,8 +245,9 @@ uint64_t env_u64(const char* k, uint64_t d) {
 uint32_t tid() { return (uint32_t)syscall(SYS_gettid); }
 
 void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t trace_h = 0) {
-  if (!g.ring) return;
-  if (type < 32 && (mislo_ring_drop_mask(g.ring) >> type & 1u)) {  // shed by the agent's overhead guard
+  void* const ring = g.ring.load(std::memory_order_acquire);
+  if (!ring) return;
+  if (type < 32 && (mislo_ring_drop_mask(ring) >> type & 1u)) {  // shed by the agent's overhead guard
     g.dropped.fetch_add(1, std::memory_order_relaxed);
     return;
   }
@@ -267,7 +271,7 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t 
     u.pid_sig = ((uint32_t)getpid() & 0x3FFFFFu) | ((uint32_t)(type & 0x7F) << 22) | (wall == 0 ? 1u << 29 : 0u) |
                 (1u << 30);
     u.pod_ts = (g.pod & 0xFFFFFu) | (uint32_t)(((t >> 32) & 0xFFFu) << 20);
-    ok = mislo_ring_push_batch(g.ring, &u, 1) == 1;
+    ok = mislo_ring_push_batch(ring, &u, 1) == 1;
     (ok ? g.pushed : g.dropped).fetch_add(1, std::memory_order_relaxed);
     return;
   }
@@ -281,7 +285,7 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t 
     u.signal_type = (uint8_t)type;
     u.flags = 1;  // has_gpu
     u.node_id = g.node;
-    ok = mislo_ring_push_batch(g.ring, &u, 1) == 1;
+    ok = mislo_ring_push_batch(ring, &u, 1) == 1;
     (ok ? g.pushed : g.dropped).fetch_add(1, std::memory_order_relaxed);
     return;
   }
@@ -297,7 +301,7 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t 
   e.svc_id = g.svc;
   e.signal_type = type;
   e.flags = 1u << 8;  // has_gpu
-  if (mislo_ring_push_batch(g.ring, &e, 1) == 1)
+  if (mislo_ring_push_batch(ring, &e, 1) == 1)
     g.pushed.fetch_add(1, std::memory_order_relaxed);
   else
     g.dropped.fetch_add(1, std::memory_order_relaxed);
@@ -555,7 +559,7 @@ void route() {
   if (!g.shard_table || g.rings.size() < 2) return;
   const uint8_t s = g.shard_table[g.pod & 0xFFFFFu];
   void* r = g.rings[s < g.rings.size() ? s : 0];
-  if (r) g.ring = r;
+  if (r) g.ring.store(r, std::memory_order_release);
 }
 
 void sampler_main() {
@@ -804,7 +808,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
       if (b > a) g.rings.push_back(mislo_ring_open_shm(list.substr(a, b - a).c_str()));
       a = b + 1;
     }
-    g.ring = g.rings.empty() ? nullptr : g.rings[0];
+    g.ring.store(g.rings.empty() ? nullptr : g.rings[0], std::memory_order_release);
     if (const char* t = std::getenv("MISLO_SHARD_TABLE")) {
       const int fd = shm_open(t, O_RDONLY, 0);
       if (fd >= 0) {
@@ -814,8 +818,9 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
       }
     }
   }
-  g.rec32 = g.ring && mislo_ring_rec_size(g.ring) == 32;
-  g.rec24 = g.ring && mislo_ring_rec_size(g.ring) == 24;
+  void* const r0 = g.ring.load(std::memory_order_acquire);
+  g.rec32 = r0 && mislo_ring_rec_size(r0) == 32;
+  g.rec24 = r0 && mislo_ring_rec_size(r0) == 24;
   g.pod = (uint32_t)env_u64("MISLO_POD_ID", 0);
   route();
   g.node = (uint16_t)env_u64("MISLO_NODE_ID", 0);
@@ -871,7 +876,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   if (g.hbm_sample_ms || g.foreign_ms) g.sampler = std::thread(sampler_main);
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] started (ring=%s attached=%d)\n", name ? name : "/mislo-agent-events",
-                 g.ring != nullptr);
+                 g.ring.load() != nullptr);
   return ok ? 0 : -1;
 }
 
@@ -886,10 +891,10 @@ void tool_fini(void*) {
   if (g.verbose)
     std::fprintf(stderr, "[mislo-rocprof] pushed=%llu dropped=%llu\n", (unsigned long long)g.pushed.load(),
                  (unsigned long long)g.dropped.load());
+  g.ring.store(nullptr, std::memory_order_release);  // no emit() picks a ring about to close
   for (void* r : g.rings)
     if (r) mislo_ring_close(r);
   g.rings.clear();
-  g.ring = nullptr;
 }
 
 }  // namespace

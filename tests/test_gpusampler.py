@@ -309,3 +309,26 @@ def test_kfd_sampler_on_the_real_driver_sees_another_process_on_the_pods_gpu():
     print(res)
     assert alone <= 1, res
     assert shared.size >= 5 and np.median(shared["value"]) >= 0.5 * 500_000_000, res
+
+
+def test_without_a_procfs_sampler_the_ladder_never_pauses_the_kfd_samplers(tmp_path):
+    """the agent hands the ladder only the procfs sampler (KFD samplers obey the rings'
+    drop mask, the GPU rung). With no procfs sampler the first step must not be
+    "sampler:paused" -- the KFD samplers keep reading until the GPU rung drops their signal."""
+    from llm_slo_ebpf_toolkit_amd.collector import kfd
+    from llm_slo_ebpf_toolkit_amd.safety import ShedLadder
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    k = Kfd(tmp_path)
+    k.proc_on(100, [7])
+    k.proc_on(200, [7])
+    k.occ(100, 7, 1)
+    k.occ(200, 7, 9)
+    ring = rt.HostRing(1 << 10, 24, "")
+    ks = kfd.KfdSampler(ring, lambda: {100: 5}, kfd_proc=k.kfd, proc_root=k.proc)
+    ks.refresh()
+    lad = ShedLadder(catalog.DISABLE_ORDER, sampler=None, user_ring=[ring])
+    first = lad.step()
+    assert first is not None and not first.startswith("sampler"), first
+    ks.native.sample()
+    assert ks.native.stats()["samples"] == (0 if first == "gpu:gpu_queue_delay_ms" else 1)
