@@ -19,7 +19,7 @@ import numpy as np
 from . import records
 
 KFD_PROC = "/sys/class/kfd/kfd/proc"
-HIP_ACT_BYTES = 40  # probes/ebpf/mislo_record.h struct mislo_hip_act
+HIP_ACT_BYTES = 64  # probes/ebpf/mislo_record.h struct mislo_hip_act
 
 
 def available(kfd_proc: str = KFD_PROC) -> bool:

@@ -61,12 +61,20 @@ UPROBE_TARGETS: Tuple[UprobeTarget, ...] = (
     UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipExtModuleLaunchKernel", False),
     UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipGraphLaunch", False),
     UprobeTarget("gpu_kfd", "hip_copy", r"^libamdhip64\.so", "hipMemcpyAsync", False),
+    UprobeTarget("gpu_kfd", "hip_copy_exit", r"^libamdhip64\.so", "hipMemcpyAsync", True),
+    UprobeTarget("gpu_kfd", "hip_copy", r"^libamdhip64\.so", "hipMemcpy", False),
+    UprobeTarget("gpu_kfd", "hip_copy_exit", r"^libamdhip64\.so", "hipMemcpy", True),
     UprobeTarget("gpu_kfd", "hip_sync_enter", r"^libamdhip64\.so", "hipStreamSynchronize", False),
     UprobeTarget("gpu_kfd", "hip_sync_exit", r"^libamdhip64\.so", "hipStreamSynchronize", True),
     UprobeTarget("gpu_kfd", "hip_sync_enter", r"^libamdhip64\.so", "hipDeviceSynchronize", False),
     UprobeTarget("gpu_kfd", "hip_sync_exit", r"^libamdhip64\.so", "hipDeviceSynchronize", True),
     UprobeTarget("gpu_kfd", "hip_sync_enter", r"^libamdhip64\.so", "hipEventSynchronize", False),
     UprobeTarget("gpu_kfd", "hip_sync_exit", r"^libamdhip64\.so", "hipEventSynchronize", True),
+    # ROCr: the waits on GPU completion signals every blocking HIP path ends in
+    UprobeTarget("gpu_kfd", "hsa_wait_enter", r"^libhsa-runtime64\.so", "hsa_signal_wait_scacquire", False),
+    UprobeTarget("gpu_kfd", "hsa_wait_exit", r"^libhsa-runtime64\.so", "hsa_signal_wait_scacquire", True),
+    UprobeTarget("gpu_kfd", "hsa_wait_enter", r"^libhsa-runtime64\.so", "hsa_signal_wait_relaxed", False),
+    UprobeTarget("gpu_kfd", "hsa_wait_exit", r"^libhsa-runtime64\.so", "hsa_signal_wait_relaxed", True),
 )
 UPROBE_PROBES = frozenset(t.probe for t in UPROBE_TARGETS)
 

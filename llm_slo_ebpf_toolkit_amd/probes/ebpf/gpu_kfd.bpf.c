@@ -12,17 +12,21 @@
  *   rccl_collective_ms   uprobe/uretprobe on librccl's ncclAllReduce / ncclAllGather /
  *                        ncclReduceScatter (host-side enqueue + completion of blocking calls)
  *   hip_activity (map)   uprobes on libamdhip64: kernel launches (hipLaunchKernel,
- *                        hipModuleLaunchKernel, hipExtModuleLaunchKernel, hipGraphLaunch) and
- *                        hipMemcpyAsync, and the time spent in hipStreamSynchronize /
- *                        hipDeviceSynchronize / hipEventSynchronize, per tgid. No ring records:
+ *                        hipModuleLaunchKernel, hipExtModuleLaunchKernel, hipGraphLaunch), copies
+ *                        (hipMemcpy, hipMemcpyAsync: entry counts, exit times the call), the time
+ *                        spent in hipStreamSynchronize / hipDeviceSynchronize /
+ *                        hipEventSynchronize; and on libhsa-runtime64 (ROCr) the time its threads
+ *                        wait for GPU completion signals (hsa_signal_wait_scacquire /
+ *                        hsa_signal_wait_relaxed), per tgid (mislo_gpu_act.h). No ring records:
  *                        the agent's KFD sampler (runtime/csrc/gpusampler.h) reads it to tell a
- *                        pod that is using its GPU -- and how long it waited on it -- from an
- *                        idle one, and weighs other processes' wave occupancy of that GPU by it
- *                        (gpu_queue_delay_ms, foreign occupancy)
+ *                        pod that is using its GPU from an idle one, and turns the pod's GPU wait
+ *                        time into gpu_queue_delay_ms: the share of it other processes' waves held
+ *                        that GPU
  *
- * The uprobe programs are attached by the agent to every libamdhip64 / librccl the node's
- * processes map (collector/uprobes.py). Records carry the has_gpu flag. */
+ * The uprobe programs are attached by the agent to every libamdhip64 / libhsa-runtime64 / librccl
+ * the node's processes map (collector/uprobes.py). Records carry the has_gpu flag. */
 #include "mislo_probe.h"
+#include "mislo_gpu_act.h"
 
 char LICENSE[] SEC("license") = "GPL";
 
@@ -55,9 +59,9 @@ struct {
 struct {
 	__uint(type, BPF_MAP_TYPE_LRU_HASH);
 	__uint(max_entries, 16384);
-	__type(key, __u64);   /* pid_tgid */
-	__type(value, __u64); /* synchronize entry */
-} hip_sync_t0 SEC(".maps");
+	__type(key, __u64);   /* mislo_act_key(pid_tgid, kind) */
+	__type(value, __u64); /* call entry */
+} act_t0 SEC(".maps");
 
 SEC("kprobe/kfd_process_evict_queues")
 int BPF_KPROBE(kfd_evict, struct kfd_process *p)
@@ -128,59 +132,53 @@ int BPF_KPROBE(reducescatter_enter) { return coll_enter(); }
 SEC("uretprobe")
 int BPF_KRETPROBE(reducescatter_exit) { return coll_exit(); }
 
-static __always_inline struct mislo_hip_act *hip_act(__u32 tgid)
-{
-	struct mislo_hip_act *a = bpf_map_lookup_elem(&hip_activity, &tgid);
-	if (a)
-		return a;
-	struct mislo_hip_act zero = {};
-	bpf_map_update_elem(&hip_activity, &tgid, &zero, BPF_NOEXIST);
-	return bpf_map_lookup_elem(&hip_activity, &tgid);
-}
-
 SEC("uprobe")
 int BPF_KPROBE(hip_launch)
 {
-	struct mislo_hip_act *a = hip_act(bpf_get_current_pid_tgid() >> 32);
-	if (a) {
-		__sync_fetch_and_add(&a->launches, 1);
-		a->last_ns = bpf_ktime_get_ns();
-	}
+	mislo_act_submit(&hip_activity, bpf_get_current_pid_tgid(), 0, bpf_ktime_get_ns());
 	return 0;
 }
 
 SEC("uprobe")
 int BPF_KPROBE(hip_copy)
 {
-	struct mislo_hip_act *a = hip_act(bpf_get_current_pid_tgid() >> 32);
-	if (a) {
-		__sync_fetch_and_add(&a->copies, 1);
-		a->last_ns = bpf_ktime_get_ns();
-	}
+	__u64 pt = bpf_get_current_pid_tgid(), now = bpf_ktime_get_ns();
+	mislo_act_submit(&hip_activity, pt, 1, now);
+	mislo_act_enter(&act_t0, pt, MISLO_ACT_COPY, now);
+	return 0;
+}
+
+SEC("uretprobe")
+int BPF_KRETPROBE(hip_copy_exit)
+{
+	mislo_act_exit(&act_t0, &hip_activity, bpf_get_current_pid_tgid(), MISLO_ACT_COPY, bpf_ktime_get_ns());
 	return 0;
 }
 
 SEC("uprobe")
 int BPF_KPROBE(hip_sync_enter)
 {
-	__u64 pt = bpf_get_current_pid_tgid(), now = bpf_ktime_get_ns();
-	bpf_map_update_elem(&hip_sync_t0, &pt, &now, BPF_ANY);
+	mislo_act_enter(&act_t0, bpf_get_current_pid_tgid(), MISLO_ACT_SYNC, bpf_ktime_get_ns());
 	return 0;
 }
 
 SEC("uretprobe")
 int BPF_KRETPROBE(hip_sync_exit)
 {
-	__u64 pt = bpf_get_current_pid_tgid();
-	__u64 *t0 = bpf_map_lookup_elem(&hip_sync_t0, &pt);
-	if (!t0)
-		return 0;
-	__u64 dt = bpf_ktime_get_ns() - *t0;
-	bpf_map_delete_elem(&hip_sync_t0, &pt);
-	struct mislo_hip_act *a = hip_act(pt >> 32);
-	if (a) {
-		__sync_fetch_and_add(&a->sync_ns, dt);
-		__sync_fetch_and_add(&a->syncs, 1);
-	}
+	mislo_act_exit(&act_t0, &hip_activity, bpf_get_current_pid_tgid(), MISLO_ACT_SYNC, bpf_ktime_get_ns());
+	return 0;
+}
+
+SEC("uprobe")
+int BPF_KPROBE(hsa_wait_enter)
+{
+	mislo_act_enter(&act_t0, bpf_get_current_pid_tgid(), MISLO_ACT_WAIT, bpf_ktime_get_ns());
+	return 0;
+}
+
+SEC("uretprobe")
+int BPF_KRETPROBE(hsa_wait_exit)
+{
+	mislo_act_exit(&act_t0, &hip_activity, bpf_get_current_pid_tgid(), MISLO_ACT_WAIT, bpf_ktime_get_ns());
 	return 0;
 }

@@ -102,10 +102,13 @@ struct mislo_def16 {
  * libamdhip64), read by the agent's KFD sampler (runtime/csrc/gpusampler.h HipActivity) */
 struct mislo_hip_act {
 	__u64 launches;   /* hipLaunchKernel / hipModuleLaunchKernel / hipExtModuleLaunchKernel / hipGraphLaunch */
-	__u64 copies;     /* hipMemcpyAsync */
+	__u64 copies;     /* hipMemcpy / hipMemcpyAsync calls */
 	__u64 last_ns;    /* bpf_ktime of the latest submission */
 	__u64 sync_ns;    /* total time in hipStreamSynchronize / hipDeviceSynchronize / hipEventSynchronize */
 	__u64 syncs;
+	__u64 copy_ns;    /* total time in hipMemcpy / hipMemcpyAsync calls (mislo_gpu_act.h) */
+	__u64 wait_ns;    /* total time in ROCr hsa_signal_wait_scacquire / hsa_signal_wait_relaxed */
+	__u64 waits;
 };
 
 /* id spaces: the kernel assigns the low part, the agent's host-side encoders the rest, so both

@@ -187,16 +187,24 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
     e.flags = 1u << 8;  // has_gpu
     out.push_back(e);
   };
-  // the pods whose HIP runtime submitted work since the last decision
+  // the pods whose HIP runtime submitted work or waited on the GPU since the last decision, and
+  // how long their threads waited: ROCr's completion-signal waits (every blocking HIP path ends in
+  // one) when those uprobes report, else the HIP synchronize and copy calls
   std::map<uint32_t, bool> hip_active;
+  std::map<uint32_t, uint64_t> pod_wait;
   std::map<uint32_t, HipActivity> hip_now;
   for (const auto& tp : targets_) {
     HipActivity a;
     if (!hip_locked(tp.first, &a)) continue;
     hip_now[tp.first] = a;
     const auto pv = hip_prev_.find(tp.first);
-    if (pv != hip_prev_.end() && (a.launches != pv->second.launches || a.copies != pv->second.copies))
-      hip_active[tp.second] = true;
+    if (pv == hip_prev_.end()) continue;
+    const HipActivity& b = pv->second;
+    const uint64_t wait = a.waits != b.waits || a.wait_ns != b.wait_ns
+                              ? a.wait_ns - b.wait_ns
+                              : (a.sync_ns - b.sync_ns) + (a.copy_ns - b.copy_ns);
+    if (a.launches != b.launches || a.copies != b.copies || wait) hip_active[tp.second] = true;
+    if (wait) pod_wait[tp.second] += wait;
   }
   hip_prev_.swap(hip_now);
   last_.clear();
@@ -210,17 +218,26 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
     s.share = (double)a.hot / (double)a.samples;
     s.foreign_mean = a.foreign_sum / (double)a.samples;
     s.active = a.own_hot > 0 || hip_active.count(s.pod);
-    last_.push_back(s);
+    const auto pw = pod_wait.find(s.pod);
+    s.gpu_wait_ns = pw != pod_wait.end() ? pw->second : 0;
     ++st_.decisions;
-    if (!dt || !s.active || !(mask >> kSigGpuQueue & 1) || s.share * 100.0 < (double)cfg_.floor_pct) continue;
-    // stamped with the pod's first process on that GPU
-    for (const auto& tp : targets_) {
-      if (tp.second != s.pod) continue;
-      const auto pr = procs_.find(tp.first);
-      if (pr == procs_.end() || !std::binary_search(pr->second.gpus.begin(), pr->second.gpus.end(), s.gpu_id)) continue;
-      rec(pr->second.ns_pid, tp.first, s.pod, (uint64_t)(s.share * (double)dt));
-      break;
+    if (dt && s.active && (mask >> kSigGpuQueue & 1) && s.share * 100.0 >= (double)cfg_.floor_pct) {
+      // the pod's measured GPU wait, the share of it other processes held the GPU; without the
+      // uprobes, the share of the interval
+      const uint64_t base = s.gpu_wait_ns ? std::min<uint64_t>(s.gpu_wait_ns, dt) : dt;
+      const uint64_t v = (uint64_t)(s.share * (double)base);
+      // stamped with the pod's first process on that GPU
+      for (const auto& tp : targets_) {
+        if (tp.second != s.pod) continue;
+        const auto pr = procs_.find(tp.first);
+        if (pr == procs_.end() || !std::binary_search(pr->second.gpus.begin(), pr->second.gpus.end(), s.gpu_id))
+          continue;
+        rec(pr->second.ns_pid, tp.first, s.pod, v);
+        s.delay_ns = v;
+        break;
+      }
     }
+    last_.push_back(s);
   }
   // queue evictions: growth of each process's evicted_ms per GPU
   char path[512];

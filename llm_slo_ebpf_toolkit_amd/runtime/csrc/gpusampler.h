@@ -13,8 +13,12 @@
 //   type 13 gpu_queue_delay_ms  the share of readings at which OTHER processes (not the pod's
 //                               own) held waves on that GPU, as ns of the interval, when the pod
 //                               was using the GPU (its own waves were seen, or its HIP runtime
-//                               submitted work: gpu_kfd.bpf.c hip_activity launches / copies) and
-//                               the share reached the floor (default 10 %)
+//                               submitted work or waited on the GPU: gpu_kfd.bpf.c hip_activity)
+//                               and the share reached the floor (default 10 %). Where the HIP /
+//                               ROCr uprobes report how long the pod's threads waited on the GPU
+//                               (ROCr completion-signal waits; else hip*Synchronize + hipMemcpy
+//                               call time), the value is that share of the wait (capped at the
+//                               interval): the delay the pod actually sat through
 //   type 13 gpu_queue_delay_ms  the time the pod's queues were evicted over the interval
 //                               (evicted_ms growth; the BPF probe's kfd_process_evict_queues ->
 //                               restore span, for nodes without BPF) when >= 1 ms
@@ -54,8 +58,9 @@ struct GpuSamplerConfig {
 // gpu_kfd.bpf.c hip_activity value (probes/ebpf/mislo_record.h struct mislo_hip_act)
 struct HipActivity {
   uint64_t launches = 0, copies = 0, last_ns = 0, sync_ns = 0, syncs = 0;
+  uint64_t copy_ns = 0, wait_ns = 0, waits = 0;  // hipMemcpy(Async) call time, ROCr signal waits
 };
-static_assert(sizeof(HipActivity) == 40, "mislo_hip_act layout");
+static_assert(sizeof(HipActivity) == 64, "mislo_hip_act layout");
 
 constexpr uint16_t kSigGpuQueue = 13;
 
@@ -72,6 +77,8 @@ struct GpuShare {
   uint64_t samples = 0, hot = 0, own_hot = 0;
   double share = 0.0, foreign_mean = 0.0;
   bool active = false;
+  uint64_t gpu_wait_ns = 0;  // the pod's host-side GPU wait over the interval (0: no HIP / ROCr uprobes)
+  uint64_t delay_ns = 0;     // the gpu_queue_delay_ms value decided (0: none emitted)
 };
 
 class GpuSampler {

@@ -542,9 +542,11 @@ class PyGpuSampler {
     s_->set_targets(v);
   }
   void set_hip_map(int fd) { s_->set_hip_map(fd); }
-  void set_hip_activity(uint32_t pid, uint64_t launches, uint64_t copies, uint64_t sync_ns, uint64_t syncs) {
+  void set_hip_activity(uint32_t pid, uint64_t launches, uint64_t copies, uint64_t sync_ns, uint64_t syncs,
+                        uint64_t copy_ns, uint64_t wait_ns, uint64_t waits) {
     HipActivity a;
     a.launches = launches, a.copies = copies, a.sync_ns = sync_ns, a.syncs = syncs;
+    a.copy_ns = copy_ns, a.wait_ns = wait_ns, a.waits = waits;
     s_->set_hip_activity(pid, a);
   }
   void sample() {
@@ -596,6 +598,8 @@ class PyGpuSampler {
       d["hot"] = g.hot;
       d["own_hot"] = g.own_hot;
       d["share"] = g.share;
+      d["gpu_wait_ns"] = g.gpu_wait_ns;
+      d["delay_ns"] = g.delay_ns;
       d["foreign_mean"] = g.foreign_mean;
       d["active"] = g.active;
       out.append(d);
@@ -791,7 +795,8 @@ PYBIND11_MODULE(_mislo_rt, m) {
       .def("set_target_list", &PyGpuSampler::set_target_list)
       .def("set_hip_map", &PyGpuSampler::set_hip_map)
       .def("set_hip_activity", &PyGpuSampler::set_hip_activity, py::arg("pid"), py::arg("launches"),
-           py::arg("copies") = 0, py::arg("sync_ns") = 0, py::arg("syncs") = 0)
+           py::arg("copies") = 0, py::arg("sync_ns") = 0, py::arg("syncs") = 0, py::arg("copy_ns") = 0,
+           py::arg("wait_ns") = 0, py::arg("waits") = 0)
       .def("sample", &PyGpuSampler::sample)
       .def("decide", &PyGpuSampler::decide, py::arg("wall_ns"), py::arg("mono_ns"))
       .def("start", &PyGpuSampler::start, py::arg("sample_s"), py::arg("decide_s"))

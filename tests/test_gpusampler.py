@@ -332,3 +332,32 @@ def test_without_a_procfs_sampler_the_ladder_never_pauses_the_kfd_samplers(tmp_p
     assert first is not None and not first.startswith("sampler"), first
     ks.native.sample()
     assert ks.native.stats()["samples"] == (0 if first == "gpu:gpu_queue_delay_ms" else 1)
+
+
+def test_a_pods_measured_gpu_wait_is_the_delay_other_processes_held_it(tmp_path):
+    """the HIP / ROCr uprobes' per-process wait time (gpu_kfd.bpf.c: ROCr
+    hsa_signal_wait_*, else hip*Synchronize + hipMemcpy call time) becomes gpu_queue_delay_ms
+    evidence: the share of the pod's GPU wait other processes held the GPU."""
+    k = Kfd(tmp_path)
+    k.proc_on(100, [7])
+    k.proc_on(200, [7])
+    s = sampler(k)
+    s.set_target_list([(100, 5)])
+    s.set_hip_activity(100, launches=1)
+    s.decide(0, DT)
+    k.occ(200, 7, 64)  # another process holds waves at every reading
+    for _ in range(5):
+        s.sample()
+    # the pod launched nothing new, but its threads waited 0.3 of the interval on ROCr signals
+    s.set_hip_activity(100, launches=1, wait_ns=int(0.3 * DT), waits=40)
+    r = recs(s.decide(0, 2 * DT))
+    sh = s.shares()[0]
+    assert sh["active"] and sh["gpu_wait_ns"] == int(0.3 * DT)
+    assert r.size == 1 and r[0]["value"] == int(0.3 * DT) == sh["delay_ns"]
+    # no ROCr uprobes: the synchronize and copy call time stand in for the wait
+    for _ in range(5):
+        s.sample()
+    s.set_hip_activity(100, launches=1, wait_ns=int(0.3 * DT), waits=40, sync_ns=int(0.1 * DT), syncs=3,
+                       copy_ns=int(0.05 * DT))
+    r = recs(s.decide(0, 3 * DT))
+    assert r.size == 1 and r[0]["value"] == int(0.15 * DT)

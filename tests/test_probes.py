@@ -235,3 +235,54 @@ def test_probe_c_split_rings_route_every_record_with_its_definitions(probe_host,
         ref = sim.encode(np.ascontiguousarray(ev[sh == s])).reshape(-1, 4)
         a, b = _resolve(got), _resolve(ref)
         assert len(a) == int((sh == s).sum()) > 0 and a == b, s
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs a host C compiler")
+def test_hip_and_rocr_wait_accounting_c_matches_its_rules(tmp_path):
+    """gpu_kfd.bpf.c's uprobes on hipMemcpy(Async) (entry + return) and on ROCr's
+    hsa_signal_wait_scacquire / _relaxed time the calls per process (mislo_gpu_act.h, compiled
+    for the host as the kernel runs it): nested calls of different kinds each count, the same
+    kind re-entered on a thread keeps the outer start, a return without an entry is ignored,
+    threads of one process add up."""
+    import random
+
+    exe = tmp_path / "gpu_act_host"
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", EBPF_DIR, "-o", str(exe),
+                    os.path.join(HOST_DIR, "gpu_act_host.c")], check=True)
+    rng = random.Random(3)
+    lines, now = [], 1000
+    model = {}  # tgid -> [launches, copies, last, sync_ns, syncs, copy_ns, wait_ns, waits]
+    open_ = {}  # (tgid, tid, kind) -> start
+    for _ in range(3000):
+        now += rng.randint(1, 5000)
+        tgid, tid = rng.choice([(7, 70), (7, 71), (9, 90)])
+        op = rng.random()
+        m = model.setdefault(tgid, [0] * 8)
+        if op < 0.2:
+            copy = rng.randint(0, 1)
+            lines.append(f"SUBMIT {copy} {tgid} {tid} {now}")
+            m[1 if copy else 0] += 1
+            m[2] = now
+        elif op < 0.6:
+            kind = rng.randint(0, 2)
+            lines.append(f"ENTER {kind} {tgid} {tid} {now}")
+            open_.setdefault((tgid, tid, kind), now)  # BPF_NOEXIST: the outer call's start stays
+        else:
+            kind = rng.randint(0, 2)
+            lines.append(f"EXIT {kind} {tgid} {tid} {now}")
+            t0 = open_.pop((tgid, tid, kind), None)
+            if t0 is None:
+                continue  # no entry seen
+            dt = now - t0
+            if kind == 0:
+                m[3] += dt
+                m[4] += 1
+            elif kind == 1:
+                m[5] += dt
+            else:
+                m[6] += dt
+                m[7] += 1
+    out = subprocess.run([str(exe)], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True).stdout
+    got = {int(r.split()[0]): [int(x) for x in r.split()[1:]] for r in out.strip().splitlines()}
+    want = {t: v for t, v in model.items() if any(v)}
+    assert got == want

@@ -172,3 +172,44 @@ def test_uprobe_sections_name_no_binary():
 def test_real_libssl_offset_is_the_exported_function():
     off = U.elf_symbol_offset("/usr/lib/x86_64-linux-gnu/libssl.so.3", "SSL_do_handshake")
     assert off is not None and off > 0
+
+
+def test_rocr_and_copy_uprobes_attach_to_their_libraries(tmp_path):
+    """hipMemcpy / hipMemcpyAsync get entry and return probes, ROCr's
+    hsa_signal_wait_scacquire / hsa_signal_wait_relaxed (libhsa-runtime64) too."""
+    proc = tmp_path / "proc"
+    fake_proc(proc, 7, [("/opt/rocm/lib/libamdhip64.so.7", "08:01", 5000),
+                        ("/opt/rocm/lib/libhsa-runtime64.so.1", "08:01", 5001)])
+    hip = {"hipLaunchKernel": 0x401100, "hipModuleLaunchKernel": 0x401200, "hipExtModuleLaunchKernel": 0x401300,
+           "hipGraphLaunch": 0x401400, "hipMemcpyAsync": 0x401500, "hipMemcpy": 0x401600,
+           "hipStreamSynchronize": 0x401700, "hipDeviceSynchronize": 0x401800, "hipEventSynchronize": 0x401900}
+    make_elf(str(proc / "7/root/opt/rocm/lib/libamdhip64.so.7"), hip)
+    make_elf(str(proc / "7/root/opt/rocm/lib/libhsa-runtime64.so.1"),
+             {"hsa_signal_wait_scacquire": 0x401a00, "hsa_signal_wait_relaxed": 0x401b00})
+    sys_ = FakeSys()
+    att = U.UprobeAttacher("/sys/fs/bpf/mislo", sys_=sys_, proc_root=str(proc))
+    n = att.attach("gpu_kfd")
+    perfs = [c for c in sys_.calls if c[0] == "perf"]
+    by = {(p[4].rsplit("/", 1)[1], p[5], p[3]) for p in perfs}
+    # file offsets: address - 0x401000 (the PT_LOAD's vaddr) + 0x1000 (its file offset)
+    for addr in (hip["hipMemcpyAsync"], hip["hipMemcpy"]):  # the copies: entry and return
+        off = addr - 0x400000
+        assert ("libamdhip64.so.7", off, False) in by and ("libamdhip64.so.7", off, True) in by
+    for addr in (0x401a00, 0x401b00):  # ROCr signal waits: entry and return
+        off = addr - 0x400000
+        assert ("libhsa-runtime64.so.1", off, False) in by and ("libhsa-runtime64.so.1", off, True) in by
+    gets = {c[1].rsplit("/", 1)[1] for c in sys_.calls if c[0] == "obj_get"}
+    assert {"hip_copy", "hip_copy_exit", "hsa_wait_enter", "hsa_wait_exit"} <= gets
+    assert n == len(perfs) and not att.errors
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhsa-runtime64.so"), reason="no ROCm")
+def test_real_rocm_wait_and_copy_symbols_resolve():
+    import glob
+
+    hsa = sorted(glob.glob("/opt/rocm/lib/libhsa-runtime64.so.*"))[-1]
+    hip = sorted(glob.glob("/opt/rocm/lib/libamdhip64.so.*"))[-1]
+    offs = U.elf_symbol_offsets(hsa, ["hsa_signal_wait_scacquire", "hsa_signal_wait_relaxed"])
+    assert all(v > 0 for v in offs.values()) and len(offs) == 2
+    offs = U.elf_symbol_offsets(hip, ["hipMemcpy", "hipMemcpyAsync"])
+    assert all(v > 0 for v in offs.values()) and len(offs) == 2
