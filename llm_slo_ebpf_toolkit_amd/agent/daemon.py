@@ -147,7 +147,8 @@ class AgentOptions:
     webhook_format: str = "generic"
     webhook_timeout_ms: int = 5000
     webhook_queue: int = 256             # attributions waiting for delivery; more are dropped (reason "emit")
-    emit_min_burn: float = 1.0           # attribute a group only while its SLO burns at least this (x budget rate)
+    emit_min_burn: float = 1.0           # attribute a group only while its SLO burns at least this (x budget rate;
+                                         # <= 0: every scored group, REF's emit-per-tick)
     emit_wait_ms: int = 250              # after a cut, wait up to this long for the window's results (0 = emit
                                          # window k at cut k+1)
     capability_mode: str = "auto"
@@ -654,7 +655,7 @@ class Agent:
             top = ranked[0]
             burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
             # (1 - 1e-9: the budget 1 - target is not exact in binary, a burn of exactly 1 lands a hair under)
-            emit = sli is None or (burn > 0 and burn >= self.o.emit_min_burn * (1.0 - 1e-9))
+            emit = sli is None or self.o.emit_min_burn <= 0 or (burn > 0 and burn >= self.o.emit_min_burn * (1.0 - 1e-9))
             self.metrics.observe_incident(top.domain, emit)
             if not emit:
                 continue

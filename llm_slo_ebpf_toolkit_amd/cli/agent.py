@@ -106,7 +106,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                          "and emit them at once (0 = with the next cut)"),
         ("webhook-queue", d.webhook_queue, "attributions queued for webhook delivery (more are dropped)"),
         ("emit-min-burn", d.emit_min_burn, "gpu engine: attribute an incident group only while its SLO burn rate "
-                                           "(error-budget multiples) is at least this"),
+                                           "(error-budget multiples) is at least this (<= 0: every scored group)"),
         ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; the flag given on the "
                              "command line wins over the env, the default does not; "
                              "each MI355X queue pins ~173 MB of host memory; 1 serialises copy and compute, ample "

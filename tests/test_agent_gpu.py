@@ -22,7 +22,7 @@ def test_agent_replay_windows_and_clean_exit(tmp_path):
     cmd = [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "replay",
            "--count", str(n_win), "--window-ms", "300", "--window-events", "65536", "--window-spans", "2048",
            "--window-groups", str(groups), "--output", "jsonl", "--output-path", str(out), "--metrics-bind", "",
-           "--scenario", "full"]
+           "--scenario", "full", "--emit-min-burn", "0"]  # every scored group (no SLO-impact gate)
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=100)
     assert p.returncode == 0, p.stderr[-2000:]
     rows = [json.loads(x) for x in out.read_text().splitlines() if x.strip()]
@@ -74,7 +74,10 @@ def test_rag_service_spans_through_agent_to_attribution(tmp_path):
            "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx_port}",
            "--metrics-bind", f"127.0.0.1:{m_port}", "--count", "12", "--window-ms", "400", "--window-events", "65536",
            "--window-spans", "1024", "--window-groups", "8", "--model", "bayes", "--output", "jsonl",
-           "--output-path", str(out)]
+           "--output-path", str(out),
+           # the stub's requests take tens of ms (the plan's DNS / network / vector-DB sleeps): an
+           # SLO they breach, so the service burns its budget and the agent attributes the incident
+           "--ttft-slo-ms", "5"]
     agent = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     try:
         deadline = time.time() + 90

@@ -275,6 +275,9 @@ def test_kfd_sampler_on_the_real_driver_sees_another_process_on_the_pods_gpu():
 
     if not os.path.isdir("/sys/class/kfd/kfd/proc"):
         pytest.skip("no KFD")
+    from test_rocprof_tool import _require_quiet_gpu
+
+    _require_quiet_gpu()  # "alone" must mean alone: another workload on the GPU is a precondition failure
     before = set(os.listdir("/sys/class/kfd/kfd/proc"))
     v = subprocess.Popen([sys.executable, "-c", VICTIM, "14"], stdout=subprocess.PIPE, text=True)
     b = None

@@ -301,7 +301,25 @@ def _my_gpu_ids():
 
     torch.zeros(1, device="cuda")  # the process's KFD entry exists once the runtime opened the GPU
     d = f"/sys/class/kfd/kfd/proc/{os.getpid()}"
-    return {e[len("stats_"):] for e in os.listdir(d) if e.startswith("stats_")} if os.path.isdir(d) else set()
+    if os.path.isdir(d):
+        return {e[len("stats_"):] for e in os.listdir(d) if e.startswith("stats_")}
+    # in a pid namespace KFD names us by our host pid: find the GPU's KFD node by its PCI address
+    # instead (topology properties: location_id = bus << 8 | device << 3 | function, domain)
+    pr = torch.cuda.get_device_properties(torch.cuda.current_device())
+    out = set()
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    for n in os.listdir(topo) if os.path.isdir(topo) else []:
+        try:
+            with open(os.path.join(topo, n, "gpu_id")) as fh:
+                gid = fh.read().strip()
+            with open(os.path.join(topo, n, "properties")) as fh:
+                props = dict(ln.split()[:2] for ln in fh if len(ln.split()) >= 2)
+        except OSError:
+            continue
+        loc, dom = int(props.get("location_id", -1)), int(props.get("domain", -1))
+        if gid != "0" and loc >> 8 == pr.pci_bus_id and (loc >> 3) & 0x1F == pr.pci_device_id and dom == pr.pci_domain_id:
+            out.add(gid)
+    return out
 
 
 def _kfd_waves():
@@ -342,6 +360,17 @@ def _wait_gpu_quiet(timeout=20.0, settle=1.0):
     return w
 
 
+def _require_quiet_gpu():
+    """These tests measure one process alone on the GPU, then against a burner they start. KFD
+    lists every process on the node by host pid (this test runs in a pid namespace and cannot
+    tell its own entry by pid), so when some process keeps waves on the GPU past the 20 s wait
+    -- a workload sharing the box's GPU -- the premise does not hold: skipped, with what KFD
+    showed, rather than reported as a detector failure."""
+    quiet = _wait_gpu_quiet()
+    if sum(quiet.values()):
+        pytest.skip(f"the GPU is not idle: KFD shows waves {dict((k, v) for k, v in quiet.items() if v)}")
+
+
 @pytest.mark.gpu
 def test_cpu_starved_process_waits_are_not_gpu_contention():
     """A service starved of CPU (burners on its CPU) alone on the GPU: its kernels can start late
@@ -352,8 +381,7 @@ def test_cpu_starved_process_waits_are_not_gpu_contention():
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    quiet = _wait_gpu_quiet()
-    assert sum(quiet.values()) == 0, f"processes keep waves on the GPU: {quiet} (this test: {os.getpid()})"
+    _require_quiet_gpu()
     name = f"/mislo-test-{os.getpid()}-starved"
     ring = rt.HostRing(1 << 16, 64, name)
     cpu = sorted(os.sched_getaffinity(0))[0]
@@ -475,8 +503,7 @@ def test_foreign_gpu_time_separates_another_process_from_the_services_own_concur
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    quiet = _wait_gpu_quiet()  # the previous test's workload may still hold waves
-    assert sum(quiet.values()) == 0, f"processes keep waves on the GPU: {quiet} (this test: {os.getpid()})"
+    _require_quiet_gpu()  # the previous test's workload may still hold waves
     name = f"/mislo-test-{os.getpid()}-foreign"
     ring = rt.HostRing(1 << 16, 64, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="1000000000",
