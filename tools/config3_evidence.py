@@ -96,6 +96,18 @@ class Client(threading.Thread):
         c.close()
 
 
+def slo_from_warmup(ttft_ms, factor: float = 1.5, floor_ms: float = 10.0) -> float:
+    """A TTFT SLO from the service's healthy warmup: 1.5x its p95 (SRE practice: an objective the
+    healthy service meets with headroom). REF's incident lab states its SLOs per scenario
+    (test/incident-lab/scenarios/*.yaml); here the workload is whatever the box runs, so the SLO is
+    set from it before the agent starts."""
+    v = sorted(float(x) for x in ttft_ms)
+    if not v:
+        return 800.0
+    p95 = v[min(len(v) - 1, int(0.95 * len(v)))]
+    return round(max(floor_ms, factor * p95), 1)
+
+
 def post(url: str, obj: dict) -> dict:
     req = urllib.request.Request(url, data=json.dumps(obj).encode(), method="POST",
                                  headers={"Content-Type": "application/json"})
@@ -227,7 +239,8 @@ def main() -> int:
     ap.add_argument("--max-tokens", type=int, default=8, help="tokens per request (short requests keep completing under contention)")
     ap.add_argument("--delay-ms", type=float, default=150.0, help="vector-DB stall per response in network faults")
     ap.add_argument("--retrans-rate", type=float, default=20.0, help="fault-profile record sets per second")
-    ap.add_argument("--ttft-slo-ms", type=float, default=400.0)
+    ap.add_argument("--ttft-slo-ms", type=float, default=0.0,
+                    help="the agent's TTFT SLO; 0 = calibrated from the healthy warmup (slo_from_warmup)")
     ap.add_argument("--window-ms", type=int, default=1000)
     ap.add_argument("--model-path", default=MODEL)
     a = ap.parse_args()
@@ -274,15 +287,20 @@ def main() -> int:
                             a.backend, "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", "",
                             "--vectordb-url", f"http://127.0.0.1:{vport}"], cwd=ROOT, env=rag_env, stdout=log,
                            stderr=subprocess.STDOUT, preexec_fn=pinned(victim))
-    agent = subprocess.Popen(
-        [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", a.engine, "--source", "shm",
-         "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
-         "--window-ms", str(a.window_ms), "--window-events", "65536", "--window-spans", "4096", "--window-groups", "8",
-         "--model-path", a.model_path, "--min-confidence", "0.3", "--halo-ms", "1500",
-         "--ttft-slo-ms", str(a.ttft_slo_ms), "--procfs-sampler", "--procfs-pods", f"{rag.pid}:{POD_UID}",
-         "--procfs-interval-ms", str(a.procfs_ms), "--model-signals", ",".join(observable),
-         "--output", "jsonl", "--output-path", attr_path],
-        cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
+
+    def start_agent(slo_ms):
+        return subprocess.Popen(
+            [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", a.engine, "--source", "shm",
+             "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
+             "--window-ms", str(a.window_ms), "--window-events", "65536", "--window-spans", "4096", "--window-groups", "8",
+             "--model-path", a.model_path, "--min-confidence", "0.3", "--halo-ms", "1500",
+             "--ttft-slo-ms", str(slo_ms), "--procfs-sampler", "--procfs-pods", f"{rag.pid}:{POD_UID}",
+             "--procfs-interval-ms", str(a.procfs_ms), "--model-signals", ",".join(observable),
+             "--output", "jsonl", "--output-path", attr_path],
+            cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
+
+    agent = None
+    slo = a.ttft_slo_ms
     stop, tstop = threading.Event(), threading.Event()
     rows: list = []
     cur = {"phase": "warmup"}
@@ -296,15 +314,20 @@ def main() -> int:
     try:
         wait_http(f"http://127.0.0.1:{vport}/healthz", vdb, 120)
         wait_http(f"http://127.0.0.1:{hport}/healthz", rag, 300)
-        wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 240)
-        tailer.start()
         clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05, a.max_tokens) for i in range(a.clients)]
         for c in clients:
             c.start()
         t_w = time.time()
-        while time.time() - t_w < 60 and (sum(r["phase"] == "warmup" for r in rows) < 4 * a.clients
-                                         or any(c.conn_tuple is None for c in clients)):
+        while time.time() - t_w < 120 and (sum(r["phase"] == "warmup" for r in rows) < max(24, 4 * a.clients)
+                                          or any(c.conn_tuple is None for c in clients)):
             time.sleep(0.2)
+        if slo <= 0:  # the service's SLO from its own healthy latency, before the agent watches it
+            slo = slo_from_warmup([r["ttft_ms"] for r in rows if r["phase"] == "warmup" and r["ttft_ms"] is not None])
+        print(f"[config3] TTFT SLO {slo:.1f} ms", flush=True)
+        agent = start_agent(slo)
+        wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 240)
+        tailer.start()
+        time.sleep(3 * a.window_ms / 1000.0)  # a few windows of the agent on the healthy service
         conns = ",".join(sorted({c.conn_tuple for c in clients if c.conn_tuple}))
         print(f"[config3] ready; rag-service pid {rag.pid} on cpus {victim}; vector-DB connections {conns}", flush=True)
         plan = [("baseline", a.phase_s), ("fault_network", a.phase_s), ("recovery_1", a.recover_s),
@@ -352,7 +375,7 @@ def main() -> int:
         for c in clients:
             c.join(30)
         for p in (rag, vdb, agent):
-            if p.poll() is None:
+            if p is not None and p.poll() is None:
                 p.send_signal(signal.SIGTERM)
                 try:
                     p.wait(60)
@@ -375,12 +398,14 @@ def main() -> int:
                     "network_record_sets_per_s": a.retrans_rate, "observable_signals": observable,
                     "rocprof_tool": gpu_tool, "window_ms": a.window_ms, "phase_s": a.phase_s,
                     "recover_s": a.recover_s, "clients": a.clients, "max_tokens": a.max_tokens,
-                    "procfs_interval_ms": a.procfs_ms,
+                    "procfs_interval_ms": a.procfs_ms, "ttft_slo_ms": slo,
+                    "slo_source": "given" if a.ttft_slo_ms > 0 else "1.5 x healthy warmup TTFT p95",
                     "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "
                                      "injected on its connections via faultinject --emit-ring --fault",
                     "cpu_fault": "pinned CPU burners; run-queue delay and CPU wait share measured by the agent's "
                                  "native schedstat sampler"}
-    res["exit"] = {"agent": agent.returncode, "rag": rag.returncode, "vectordb": vdb.returncode}
+    res["exit"] = {"agent": agent.returncode if agent is not None else None, "rag": rag.returncode,
+                   "vectordb": vdb.returncode}
     with open(os.path.join(a.out, "summary.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1), flush=True)

@@ -40,7 +40,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from config2_evidence import Tailer, free_port, pct, wait_http  # noqa: E402
-from config3_evidence import GPU_SIGNALS, MODEL, TOOL, Client, scrape_counters, scrape_overhead, score  # noqa: E402
+from config3_evidence import (GPU_SIGNALS, MODEL, TOOL, Client, scrape_counters, scrape_overhead, score,  # noqa: E402
+                              slo_from_warmup)
 
 POD_UID = "c0f14000-0000-4000-8000-000000000004"
 BURN = "import os, sys\nos.sched_setaffinity(0, {int(sys.argv[1])})\nwhile True:\n    pass\n"
@@ -58,7 +59,11 @@ def main() -> int:
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--burners-per-cpu", type=int, default=4)
     ap.add_argument("--steal-pct", type=float, default=9.0, help="injected cpu_steal_pct (REF's cpu_throttle level)")
-    ap.add_argument("--ttft-slo-ms", type=float, default=800.0)
+    ap.add_argument("--ttft-slo-ms", type=float, default=0.0,
+                    help="the agent's TTFT SLO; 0 = calibrated from the healthy warmup (slo_from_warmup)")
+    ap.add_argument("--clients", type=int, default=3,
+                    help="closed-loop clients: a server slowed by a fault keeps completing requests in every "
+                         "1 s window (one client left windows without a request, so without an incident)")
     ap.add_argument("--model-path", default=MODEL)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -94,15 +99,20 @@ def main() -> int:
                                       stderr=subprocess.STDOUT, preexec_fn=pinned(rank_cpus[r])))
     observable = ["runqueue_delay_ms", "cpu_steal_pct"] + (["mem_reclaim_latency_ms"] if procfs.psi_available() else [])
     observable += [s for s in GPU_SIGNALS if s != "xgmi_link_latency_us"] if os.path.exists(TOOL) else []
-    agent = subprocess.Popen(
-        [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--gpus", str(n),
-         "--source", "shm", "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}",
-         "--metrics-bind", f"127.0.0.1:{mport}", "--window-ms", "1000", "--window-events", "262144",
-         "--window-spans", "4096", "--window-groups", "8", "--model-path", a.model_path, "--min-confidence", "0.3",
-         "--halo-ms", "1500", "--ttft-slo-ms", str(a.ttft_slo_ms), "--procfs-sampler",
-         "--procfs-pods", ",".join(f"{p.pid}:{POD_UID}" for p in ranks), "--procfs-interval-ms", "100",
-         "--model-signals", ",".join(observable), "--output", "jsonl", "--output-path", attr_path],
-        cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
+
+    def start_agent(slo_ms):
+        return subprocess.Popen(
+            [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--gpus", str(n),
+             "--source", "shm", "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}",
+             "--metrics-bind", f"127.0.0.1:{mport}", "--window-ms", "1000", "--window-events", "262144",
+             "--window-spans", "4096", "--window-groups", "8", "--model-path", a.model_path, "--min-confidence", "0.3",
+             "--halo-ms", "1500", "--ttft-slo-ms", str(slo_ms), "--procfs-sampler",
+             "--procfs-pods", ",".join(f"{p.pid}:{POD_UID}" for p in ranks), "--procfs-interval-ms", "100",
+             "--model-signals", ",".join(observable), "--output", "jsonl", "--output-path", attr_path],
+            cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
+
+    agent = None
+    slo = a.ttft_slo_ms
     stop, tstop = threading.Event(), threading.Event()
     rows: list = []
     cur = {"phase": "warmup"}
@@ -111,14 +121,19 @@ def main() -> int:
     phases, counters, overhead = [], {}, {}
     try:
         wait_http(f"http://127.0.0.1:{hport}/healthz", ranks[0], 600)
-        wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 300)
-        tailer.start()
-        clients = [Client(hport, 0, lambda: cur["phase"], stop, rows, 0.05)]
+        clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05) for i in range(a.clients)]
         for c in clients:
             c.start()
         t_w = time.time()
-        while time.time() - t_w < 120 and sum(r["phase"] == "warmup" for r in rows) < 4:
+        while time.time() - t_w < 180 and sum(r["phase"] == "warmup" for r in rows) < 24:
             time.sleep(0.2)
+        if slo <= 0:  # the service's SLO from its own healthy latency, before the agent watches it
+            slo = slo_from_warmup([r["ttft_ms"] for r in rows if r["phase"] == "warmup" and r["ttft_ms"] is not None])
+        print(f"[config4] TTFT SLO {slo:.1f} ms", flush=True)
+        agent = start_agent(slo)
+        wait_http(f"http://127.0.0.1:{mport}/readyz", agent, 300)
+        tailer.start()
+        time.sleep(3.0)  # a few windows of the agent on the healthy server
         print(f"[config4] ready: TP {n}, rank pids {[p.pid for p in ranks]}", flush=True)
         plan = [("baseline", a.phase_s), ("fault_interconnect", a.phase_s), ("recovery_1", a.recover_s),
                 ("fault_cpu", a.phase_s), ("recovery_2", a.recover_s), ("fault_compound", a.phase_s),
@@ -169,7 +184,7 @@ def main() -> int:
                 p.kill()
         for c in clients:
             c.join(60)
-        for p in [ranks[0]] + [agent]:
+        for p in [ranks[0]] + ([agent] if agent is not None else []):
             if p.poll() is None:
                 p.send_signal(signal.SIGTERM)
                 try:
@@ -191,10 +206,12 @@ def main() -> int:
     res["agent_overhead_metrics"] = overhead
     res["agent_counters_by_phase"] = counters
     res["setup"] = {"tp_ranks": n, "preset": a.preset, "model": os.path.relpath(a.model_path, ROOT),
+                    "ttft_slo_ms": slo, "clients": a.clients,
+                    "slo_source": "given" if a.ttft_slo_ms > 0 else "1.5 x healthy warmup TTFT p95",
                     "observable_signals": observable, "rank_cpus": rank_cpus, "burners_per_cpu": a.burners_per_cpu,
                     "interconnect_fault": "tools/xgmi_hog.py peer copies over every GPU pair",
                     "cpu_fault": "pinned burners (measured run-queue delay) + injected cpu_steal_pct records"}
-    res["exit"] = {"agent": agent.returncode, "ranks": [p.returncode for p in ranks]}
+    res["exit"] = {"agent": agent.returncode if agent is not None else None, "ranks": [p.returncode for p in ranks]}
     with open(os.path.join(a.out, "summary.json"), "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1), flush=True)
