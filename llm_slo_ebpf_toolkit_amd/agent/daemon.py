@@ -624,9 +624,11 @@ class Agent:
         from constants.
 
         Emission is gated on SLO impact: a group is attributed only while its SLO burns its error
-        budget at least ``emit_min_burn`` times the sustainable rate (the forecast burn over the
-        recent windows, >= 1 by default: SRE burn-rate alerting), so "unknown" never leaves at zero
-        burn and one slow request among a few does not page. Every scored group still counts in
+        budget at least ``emit_min_burn`` times the sustainable rate NOW (the burn over the last few
+        windows holding >= 20 requests, >= 1 by default: a fast-burn alert), so "unknown" never
+        leaves at zero burn, one slow request among a few does not page, and a recovered service
+        stops paging although its 5-minute forecast still carries the fault. The attribution's
+        SLO impact quotes the forecast burn. Every scored group still counts in
         ``llm_slo_agent_incidents_scored_total{domain, emitted}``; a healthy node emits nothing (REF
         posts every tick, cmd/agent/main.go:567-585 -- with a webhook configured that pages on
         every healthy window)."""
@@ -634,11 +636,12 @@ class Agent:
         D = model.weights.shape[1]
         post, bits, feat = res["post"], res["evbits"].view(np.uint32), res["feat"]
         sli = res.get("sli")
-        forecast = {}
+        forecast, now_burn = {}, {}
         if sli is not None:
             for g in range(min(G, sli.shape[0])):
                 key = names[g] if g < len(names) else f"group-{g}"
                 forecast[g] = self.burn.observe(key, float(sli[g, 0]), float(sli[g, 1]))
+                now_burn[g] = self.burn.current(key)
             err = self.burn.error()
             if err is not None:
                 self.metrics.burn_err.set(err)
@@ -655,7 +658,8 @@ class Agent:
             top = ranked[0]
             burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
             # (1 - 1e-9: the budget 1 - target is not exact in binary, a burn of exactly 1 lands a hair under)
-            emit = sli is None or self.o.emit_min_burn <= 0 or (burn > 0 and burn >= self.o.emit_min_burn * (1.0 - 1e-9))
+            cur = now_burn.get(g, 0.0)
+            emit = sli is None or self.o.emit_min_burn <= 0 or (cur > 0 and cur >= self.o.emit_min_burn * (1.0 - 1e-9))
             self.metrics.observe_incident(top.domain, emit)
             if not emit:
                 continue

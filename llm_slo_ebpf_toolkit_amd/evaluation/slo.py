@@ -197,6 +197,19 @@ class BurnRateForecaster:
             self._pending[key] = [(t0 - drop, f0) for t0, f0 in pend]
         return f
 
+    def current(self, key, windows: int = 3, min_requests: float = 20.0) -> float:
+        """The burn now: over the shortest trailing run of at most ``windows`` windows holding at
+        least ``min_requests`` requests (all of them if fewer). The agent's emission gate -- a
+        fast-burn alert: the forecast (``observe``) keeps a fault's breaches for up to ``short``
+        windows after the service recovered, which would page "unknown" through the recovery."""
+        n_acc = b_acc = 0.0
+        for x in reversed(self._hist.get(key, [])[-int(windows):]):
+            n_acc += x[0]
+            b_acc += x[1]
+            if n_acc >= min_requests:
+                break
+        return self.burn(n_acc, b_acc)
+
     def alert(self, key) -> float:
         recent = self._hist.get(key, [])[-self.short:]
         return self.burn(sum(x[0] for x in recent), sum(x[1] for x in recent))

@@ -162,3 +162,24 @@ def test_agent_attributions_carry_the_burn_forecast(tmp_path):
     assert out[0].slo_impact.burn_rate == pytest.approx(4.0)  # 4 % breaches / 1 % budget
     assert out[1].slo_impact.burn_rate == pytest.approx(1.0)
     assert agent.burn.error() is None  # no forecast has matured yet (5-minute horizon)
+
+
+def test_a_recovered_group_stops_paging_although_its_forecast_still_burns(tmp_path):
+    """The emission gate is the burn NOW (last few windows), the attribution quotes the 5-minute
+    forecast: a fault's windows are attributed, the clean windows after it are not."""
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+
+    agent = Agent(AgentOptions(output="jsonl", output_path=str(tmp_path / "a.jsonl"), window_ms=1000,
+                               min_confidence=0.0))
+    model = NaiveBayes.ref()
+    post = np.zeros((1, 16))
+    post[0, 0] = 0.9
+    res = lambda n, b: {"post": post, "evbits": np.zeros((1, 16), np.uint32),  # noqa: E731
+                        "feat": np.zeros((1, 16), np.float32), "sli": np.array([[n, b]], np.uint32)}
+    emitted = [len(agent._attributions(1, ["svc"], res(20, 10 if w < 3 else 0), w, model)) for w in range(8)]
+    assert emitted[:3] == [1, 1, 1]      # breaching windows page
+    assert emitted[6:] == [0, 0]         # three clean windows later: silent
+    assert agent.burn.observe("svc", 20, 0) > 0  # while the forecast still carries the fault
