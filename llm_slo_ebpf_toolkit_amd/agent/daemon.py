@@ -23,6 +23,7 @@ Two engines share one process, one Prometheus registry and one set of outputs:
 from __future__ import annotations
 
 import collections
+import json
 import math
 import os
 import sys
@@ -149,8 +150,12 @@ class AgentOptions:
     webhook_queue: int = 256             # attributions waiting for delivery; more are dropped (reason "emit")
     emit_min_burn: float = 1.0           # attribute a group only while its SLO burns at least this (x budget rate;
                                          # <= 0: every scored group, REF's emit-per-tick)
+    emit_min_requests: float = 8.0       # the gate's burn "now": the last windows (at most 3) holding this many
+                                         # requests -- one busy window with no breach ends a page
     emit_wait_ms: int = 250              # after a cut, wait up to this long for the window's results (0 = emit
                                          # window k at cut k+1)
+    decision_log: str = ""               # JSONL of every scored group per window, emitted or not, and why
+                                         # ("" = off; the evidence harnesses' per-window audit trail)
     capability_mode: str = "auto"
     disable_signals: List[str] = field(default_factory=list)
     disable_overhead_guard: bool = False
@@ -279,6 +284,10 @@ class Agent:
         self.webhook_q = AsyncWebhook(self.webhook, maxsize=opts.webhook_queue,
                                       on_drop=lambda reason: self.metrics.inc_dropped("emit"),
                                       log=lambda m: print(m, file=sys.stderr)) if self.webhook is not None else None
+        self.decisions = None
+        if opts.decision_log:
+            os.makedirs(os.path.dirname(os.path.abspath(opts.decision_log)), exist_ok=True)
+            self.decisions = open(opts.decision_log, "a", buffering=1)  # line-buffered: tailed while it runs
         self.server: Optional[MetricsServer] = None
         self.limiter = RateLimiter(self.cfg.sampling.events_per_second_limit)
         # the window engine evaluates the guard every window: REF's formula over a 30 s horizon
@@ -317,6 +326,9 @@ class Agent:
             self.writers.close()
             if self.webhook_q is not None:
                 self.webhook_q.close()
+            if self.decisions is not None:
+                self.decisions.close()
+                self.decisions = None
         finally:
             if self.server is not None:
                 self.server.stop()
@@ -624,8 +636,9 @@ class Agent:
         from constants.
 
         Emission is gated on SLO impact: a group is attributed only while its SLO burns its error
-        budget at least ``emit_min_burn`` times the sustainable rate NOW (the burn over the last few
-        windows holding >= 20 requests, >= 1 by default: a fast-burn alert), so "unknown" never
+        budget at least ``emit_min_burn`` times the sustainable rate NOW (the burn over the shortest
+        run of the last <= 3 windows holding ``emit_min_requests`` requests, >= 1 by default: a
+        fast-burn alert), so "unknown" never
         leaves at zero burn, one slow request among a few does not page, and a recovered service
         stops paging although its 5-minute forecast still carries the fault. The attribution's
         SLO impact quotes the forecast burn. Every scored group still counts in
@@ -641,7 +654,7 @@ class Agent:
             for g in range(min(G, sli.shape[0])):
                 key = names[g] if g < len(names) else f"group-{g}"
                 forecast[g] = self.burn.observe(key, float(sli[g, 0]), float(sli[g, 1]))
-                now_burn[g] = self.burn.current(key)
+                now_burn[g] = self.burn.current(key, windows=3, min_requests=self.o.emit_min_requests)
             err = self.burn.error()
             if err is not None:
                 self.metrics.burn_err.set(err)
@@ -649,17 +662,28 @@ class Agent:
         impact_min = max(1, int(round(self.burn.horizon * self.o.window_ms / 60000.0)))
         reqs = sli[:, 0].tolist() if sli is not None else []
         feat_l = np.asarray(feat, dtype=np.float64).tolist()  # Python rows: one conversion per window
+        log = self.decisions
         for g in range(G):
             if g < len(reqs) and reqs[g] == 0:
                 continue  # no request of this group in the window: no incident to attribute
             ranked = model.ranked(post[g, :D], bits[g, :D])
-            if not ranked or ranked[0].posterior < self.o.min_confidence:
-                continue
-            top = ranked[0]
             burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
             # (1 - 1e-9: the budget 1 - target is not exact in binary, a burn of exactly 1 lands a hair under)
             cur = now_burn.get(g, 0.0)
-            emit = sli is None or self.o.emit_min_burn <= 0 or (cur > 0 and cur >= self.o.emit_min_burn * (1.0 - 1e-9))
+            confident = bool(ranked) and ranked[0].posterior >= self.o.min_confidence
+            emit = confident and (sli is None or self.o.emit_min_burn <= 0
+                                  or (cur > 0 and cur >= self.o.emit_min_burn * (1.0 - 1e-9)))
+            if log is not None:
+                log.write(json.dumps({
+                    "t_ns": int(t_ns), "group": g, "service": names[g] if g < len(names) else f"group-{g}",
+                    "requests": float(sli[g, 0]) if sli is not None and g < sli.shape[0] else None,
+                    "breaches": float(sli[g, 1]) if sli is not None and g < sli.shape[0] else None,
+                    "burn_now": round(cur, 4), "burn_forecast": round(burn, 4),
+                    "top": [[p.domain, round(float(p.posterior), 4)] for p in ranked[:3]],
+                    "emitted": emit, "why": "emitted" if emit else ("low_confidence" if not confident else "no_burn")}) + "\n")
+            if not confident:
+                continue
+            top = ranked[0]
             self.metrics.observe_incident(top.domain, emit)
             if not emit:
                 continue

@@ -107,6 +107,10 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("webhook-queue", d.webhook_queue, "attributions queued for webhook delivery (more are dropped)"),
         ("emit-min-burn", d.emit_min_burn, "gpu engine: attribute an incident group only while its SLO burn rate "
                                            "(error-budget multiples) is at least this (<= 0: every scored group)"),
+        ("emit-min-requests", d.emit_min_requests, "gpu engine: the emission gate's burn is over the last windows "
+                                                   "(at most 3) holding this many requests"),
+        ("decision-log", d.decision_log, "gpu engine: JSONL of every scored incident group per window -- "
+                                         "requests, breaches, burn, top posteriors, emitted or why not (\"\" = off)"),
         ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; the flag given on the "
                              "command line wins over the env, the default does not; "
                              "each MI355X queue pins ~173 MB of host memory; 1 serialises copy and compute, ample "
@@ -135,7 +139,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         kfd_sampler=a.kfd_sampler,
         model_signals=a.model_signals,
         pair_prior=float(a.pair_prior), emit_wait_ms=int(a.emit_wait_ms), webhook_queue=int(a.webhook_queue),
-        emit_min_burn=float(a.emit_min_burn),
+        emit_min_burn=float(a.emit_min_burn), emit_min_requests=float(a.emit_min_requests),
+        decision_log=a.decision_log,
         explicit_flags=tuple(sorted({x.lstrip("-").split("=", 1)[0] for x in (argv if argv is not None else sys.argv[1:]) if x.startswith("-")})))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime
         given = any(x.lstrip("-").split("=", 1)[0] == "gpu-hw-queues" for x in argv or [])

@@ -102,8 +102,12 @@ def main(argv=None) -> int:
         toks = [prompt_hash(w) % model.cfg.vocab for w in prompt.split()][:256] or [1]
         trace = hashlib.blake2b(rid.encode(), digest_size=16).hexdigest()
         root = hashlib.blake2b(f"{rid}/r".encode(), digest_size=8).hexdigest()
-        t0 = time.time_ns()
+        t_arrive = time.time_ns()
         with lock:  # requests are serialised: every rank runs the same one
+            # the span is the request's service (what TTFT is measured over), its wait for the
+            # lock an attribute: the agent joins signals near the span's start, and a start
+            # several queued requests back would fall outside the records it still holds
+            t0 = time.time_ns()
             ids = torch.tensor([toks], dtype=torch.int64, device=dev)
             if world > 1:
                 th = trace_hash(trace)
@@ -118,7 +122,7 @@ def main(argv=None) -> int:
         stats["requests"] += 1
         spans.add([SpanExporter.span(trace, root, "", "chat.request", t0, t1, {
             "request.id": rid, "llm.tp.world_size": world, semconv.ATTR_SLO_TTFT_MS: r["ttft_ms"],
-            semconv.ATTR_SLO_TOKENS_PER_SEC: r["tokens_per_s"]})])
+            semconv.ATTR_SLO_TOKENS_PER_SEC: r["tokens_per_s"], "llm.queue_ms": round((t0 - t_arrive) / 1e6, 3)})])
         return {"request_id": rid, "trace_id": trace, "ttft_ms": round(r["ttft_ms"], 3),
                 "tokens_per_sec": round(r["tokens_per_s"], 3), "tokens": [VOCAB[i % len(VOCAB)] for i in range(max_new)]}
 

@@ -183,3 +183,44 @@ def test_a_recovered_group_stops_paging_although_its_forecast_still_burns(tmp_pa
     assert emitted[:3] == [1, 1, 1]      # breaching windows page
     assert emitted[6:] == [0, 0]         # three clean windows later: silent
     assert agent.burn.observe("svc", 20, 0) > 0  # while the forecast still carries the fault
+
+
+def test_decision_log_records_every_scored_group_and_why(tmp_path):
+    """--decision-log: one JSON line per scored group per window, emitted or not (the evidence
+    harnesses' audit trail for windows that left no attribution)."""
+    import json
+
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+
+    path = tmp_path / "d" / "decisions.jsonl"
+    agent = Agent(AgentOptions(output="jsonl", output_path=str(tmp_path / "a.jsonl"), window_ms=1000,
+                               min_confidence=0.5, decision_log=str(path)))
+    model = NaiveBayes.ref()
+    post = np.zeros((3, 16))
+    post[0, 0], post[1, 0], post[2, 1] = 0.9, 0.9, 0.3
+    sli = np.array([[20, 10], [20, 0], [20, 10]], np.uint32)
+    res = {"post": post, "evbits": np.zeros((3, 16), np.uint32), "feat": np.zeros((3, 16), np.float32), "sli": sli}
+    out = agent._attributions(3, ["hot", "calm", "vague"], res, 7, model)
+    agent.close()
+    assert [a.service for a in out] == ["hot"]
+    rows = [json.loads(x) for x in path.read_text().splitlines()]
+    assert [(r["service"], r["emitted"], r["why"]) for r in rows] == [
+        ("hot", True, "emitted"), ("calm", False, "no_burn"), ("vague", False, "low_confidence")]
+    assert rows[0]["requests"] == 20 and rows[0]["breaches"] == 10 and rows[0]["burn_now"] == 50.0
+    assert rows[2]["top"][0][1] == 0.3
+
+
+def test_emission_gate_burn_is_over_the_last_windows_holding_enough_requests():
+    """BurnRateForecaster.current: a busy clean window alone says "not burning now"; sparse
+    windows (a slow LLM server completes 2-3 requests a window) are pooled, up to 3 windows."""
+    fc = slo.BurnRateForecaster(target=0.99, horizon=10, short=5)
+    for n, b in ((2, 1), (2, 1), (3, 0)):
+        fc.observe("sparse", n, b)
+    assert fc.current("sparse", windows=3, min_requests=8) == pytest.approx((2 / 7) / 0.01)
+    for n, b in ((2, 2), (2, 2), (8, 0)):
+        fc.observe("busy", n, b)
+    assert fc.current("busy", windows=3, min_requests=8) == 0.0
+    assert fc.current("busy", windows=3, min_requests=20) == pytest.approx((4 / 12) / 0.01)

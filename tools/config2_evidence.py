@@ -167,7 +167,7 @@ def main() -> int:
     ap.add_argument("--model-path", default=MODEL, help="the agent's model ('' = the bayes_gpu expert table)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    from config3_evidence import score  # noqa: E402 - tools/ sibling (imports this module at load)
+    from config3_evidence import load_cuts, score  # noqa: E402 - tools/ sibling (imports this module at load)
     from llm_slo_ebpf_toolkit_amd.collector import bpf
 
     prefix = f"/mislo-cfg2-{os.getpid()}"
@@ -186,7 +186,8 @@ def main() -> int:
          "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}", "--metrics-bind", f"127.0.0.1:{mport}",
          "--window-ms", str(a.window_ms), "--window-events", "262144", "--window-spans", "4096", "--window-groups", "8",
          *model_args, "--min-confidence", "0.3", "--halo-ms", str(a.halo_ms), "--ttft-slo-ms", str(a.ttft_slo_ms),
-         "--output", "jsonl", "--output-path", attr_path], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
+         "--output", "jsonl", "--output-path", attr_path,
+         "--decision-log", os.path.join(a.out, "decisions.jsonl")], cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
     llm_env = dict(env, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=names.user, MISLO_POD_ID="1", MISLO_ROCPROF_VERBOSE="1",
                    OTEL_EXPORTER_OTLP_TRACES_ENDPOINT=f"http://127.0.0.1:{rx}/v1/traces",
                    POD_UID=POD_UID, POD_NAME="llm-server-config2")
@@ -269,7 +270,8 @@ def main() -> int:
         for r in rows:
             f.write(json.dumps(r) + "\n")
     expect = {"baseline": set(), "fault_gpu_contention": {"gpu_contention"}, "recovery": set()}
-    res = score(phases, tailer.rows, a.window_ms, service="rag-service", expect=expect)
+    res = score(phases, tailer.rows, a.window_ms, service="rag-service", expect=expect,
+                cuts=load_cuts(os.path.join(a.out, "decisions.jsonl")))
     fault = res["phases"].get("fault_gpu_contention", {})
     # detection delay: the burners' first GEMM (fault onset) -> arrival of the service's first
     # gpu_contention attribution

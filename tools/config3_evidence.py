@@ -151,10 +151,36 @@ def scrape_counters(port: int) -> dict:
     return out
 
 
-def score(phases, attrs, window_ms: float, service: str = "rag-service", expect=None) -> dict:
+def load_cuts(path: str) -> list:
+    """The agent's window cut times from its decision log (every scored group of every window)."""
+    cuts = set()
+    if os.path.exists(path):
+        with open(path) as f:
+            for ln in f:
+                try:
+                    cuts.add(int(json.loads(ln)["t_ns"]))
+                except (ValueError, KeyError):
+                    pass
+    return sorted(cuts)
+
+
+def phase_windows(t0: int, t1: int, win: float, cuts=None) -> list:
+    """Cut times of the windows wholly inside [t0, t1] ((t - window, t] inside the phase). With the
+    agent's own cut times (``load_cuts``) the grid is the agent's: a 15 s phase that does not start
+    on a cut holds 14 whole windows, not 15; without them, windows are counted from t0."""
+    if cuts:
+        anchor = min(cuts, key=lambda c: abs(c - t0))
+        k0 = -int((anchor - t0) // win) - 1
+        grid = [anchor + k * win for k in range(k0, k0 + int((t1 - t0) // win) + 3)]
+        return [int(c) for c in grid if t0 + win <= c <= t1]
+    return [int(t0 + win * (k + 1)) for k in range(max(1, int((t1 - t0 - win) // win) + 1))]
+
+
+def score(phases, attrs, window_ms: float, service: str = "rag-service", expect=None, cuts=None) -> dict:
     """Per-phase top-1 per window of the service's incident group (windows without an attribution
     count as ``none``), accuracy, macro-F1 over the single-fault + healthy phases, compound
-    partial / coverage@0.10, detection delay."""
+    partial / coverage@0.10, detection delay. ``cuts``: the agent's window cut times (decision
+    log), so the phase's whole windows are counted on the agent's grid."""
     expect = EXPECT if expect is None else expect
     win = window_ms * 1e6
     mine = [(arr, r) for arr, r in attrs if r.get("service") == service]
@@ -166,9 +192,10 @@ def score(phases, attrs, window_ms: float, service: str = "rag-service", expect=
     truth, pred = [], []
     for name, t0, t1 in phases:
         exp = expect[name]
+        wins = phase_windows(t0, t1, win, cuts)
         # windows wholly inside the phase: cut time t with (t - window, t] inside [t0, t1]
         rows = [r for _a, r in mine if t0 + win <= t_of(r) <= t1]
-        n_win = max(1, int((t1 - t0 - win) // win) + 1)
+        n_win = max(1, len(wins))
         tops = {}
         for r in rows:
             tops[r["predicted_fault_domain"]] = tops.get(r["predicted_fault_domain"], 0) + 1
@@ -196,10 +223,10 @@ def score(phases, attrs, window_ms: float, service: str = "rag-service", expect=
         if len(exp) <= 1:
             label = next(iter(exp)) if exp else "unknown"
             got = {t_of(r): r["predicted_fault_domain"] for r in rows}
-            for k in range(n_win):
+            for c in (wins or [int(t0 + win)]):
                 truth.append(label)
                 # a healthy window without an incident is a correct "unknown"
-                pred.append(next((v for t, v in got.items() if t0 + win * (k + 1) <= t < t0 + win * (k + 2)),
+                pred.append(next((v for t, v in got.items() if abs(t - c) < win / 2),
                                  "unknown" if not exp else "none"))
         if exp:
             hits = [(arr, t_of(r)) for arr, r in mine if t_of(r) > t0 and r["predicted_fault_domain"] in exp
@@ -296,7 +323,8 @@ def main() -> int:
              "--model-path", a.model_path, "--min-confidence", "0.3", "--halo-ms", "1500",
              "--ttft-slo-ms", str(slo_ms), "--procfs-sampler", "--procfs-pods", f"{rag.pid}:{POD_UID}",
              "--procfs-interval-ms", str(a.procfs_ms), "--model-signals", ",".join(observable),
-             "--output", "jsonl", "--output-path", attr_path],
+             "--output", "jsonl", "--output-path", attr_path,
+             "--decision-log", os.path.join(a.out, "decisions.jsonl")],
             cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
 
     agent = None
@@ -388,7 +416,7 @@ def main() -> int:
     with open(os.path.join(a.out, "requests.jsonl"), "w") as f:
         for r in rows:
             f.write(json.dumps(r) + "\n")
-    res = score(phases, tailer.rows, a.window_ms)
+    res = score(phases, tailer.rows, a.window_ms, cuts=load_cuts(os.path.join(a.out, "decisions.jsonl")))
     res["ttft_ms"] = {n: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
                       for n, _t0, _t1 in phases for v in [[r["ttft_ms"] for r in rows if r["phase"] == n]]}
     res["agent_overhead_metrics"] = overhead

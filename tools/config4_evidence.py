@@ -40,7 +40,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from config2_evidence import Tailer, free_port, pct, wait_http  # noqa: E402
-from config3_evidence import (GPU_SIGNALS, MODEL, TOOL, Client, scrape_counters, scrape_overhead, score,  # noqa: E402
+from config3_evidence import (GPU_SIGNALS, MODEL, TOOL, Client, load_cuts, scrape_counters, scrape_overhead, score,  # noqa: E402
                               slo_from_warmup)
 
 POD_UID = "c0f14000-0000-4000-8000-000000000004"
@@ -57,7 +57,8 @@ def main() -> int:
     ap.add_argument("--preset", default="7b")
     ap.add_argument("--phase-s", type=float, default=15.0)
     ap.add_argument("--recover-s", type=float, default=8.0)
-    ap.add_argument("--burners-per-cpu", type=int, default=4)
+    ap.add_argument("--burners-per-cpu", type=int, default=2,
+                    help="busy loops per rank CPU: 2 slows the server ~3x; 4 starves it to a request every few s")
     ap.add_argument("--steal-pct", type=float, default=9.0, help="injected cpu_steal_pct (REF's cpu_throttle level)")
     ap.add_argument("--ttft-slo-ms", type=float, default=0.0,
                     help="the agent's TTFT SLO; 0 = calibrated from the healthy warmup (slo_from_warmup)")
@@ -108,7 +109,8 @@ def main() -> int:
              "--window-spans", "4096", "--window-groups", "8", "--model-path", a.model_path, "--min-confidence", "0.3",
              "--halo-ms", "1500", "--ttft-slo-ms", str(slo_ms), "--procfs-sampler",
              "--procfs-pods", ",".join(f"{p.pid}:{POD_UID}" for p in ranks), "--procfs-interval-ms", "100",
-             "--model-signals", ",".join(observable), "--output", "jsonl", "--output-path", attr_path],
+             "--model-signals", ",".join(observable), "--output", "jsonl", "--output-path", attr_path,
+             "--decision-log", os.path.join(a.out, "decisions.jsonl")],
             cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, preexec_fn=pinned(rest))
 
     agent = None
@@ -200,7 +202,8 @@ def main() -> int:
         if tailer.is_alive():
             tailer.join(10)
         log.close()
-    res = score(phases, tailer.rows, 1000.0, service="llm-tp", expect=EXPECT)
+    res = score(phases, tailer.rows, 1000.0, service="llm-tp", expect=EXPECT,
+                cuts=load_cuts(os.path.join(a.out, "decisions.jsonl")))
     res["ttft_ms"] = {nm: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
                       for nm, _t0, _t1 in phases for v in [[r["ttft_ms"] for r in rows if r["phase"] == nm]]}
     res["agent_overhead_metrics"] = overhead
