@@ -65,6 +65,9 @@ def main() -> int:
     ap.add_argument("--clients", type=int, default=3,
                     help="closed-loop clients: a server slowed by a fault keeps completing requests in every "
                          "1 s window (one client left windows without a request, so without an incident)")
+    ap.add_argument("--max-tokens", type=int, default=8,
+                    help="tokens per completion: short chat turns, so a CPU-starved 7B server still completes "
+                         "a request in most 1 s windows (16 tokens took > 1 s per request under the fault)")
     ap.add_argument("--model-path", default=MODEL)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -123,7 +126,7 @@ def main() -> int:
     phases, counters, overhead = [], {}, {}
     try:
         wait_http(f"http://127.0.0.1:{hport}/healthz", ranks[0], 600)
-        clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05) for i in range(a.clients)]
+        clients = [Client(hport, i, lambda: cur["phase"], stop, rows, 0.05, max_tokens=a.max_tokens) for i in range(a.clients)]
         for c in clients:
             c.start()
         t_w = time.time()
@@ -209,7 +212,7 @@ def main() -> int:
     res["agent_overhead_metrics"] = overhead
     res["agent_counters_by_phase"] = counters
     res["setup"] = {"tp_ranks": n, "preset": a.preset, "model": os.path.relpath(a.model_path, ROOT),
-                    "ttft_slo_ms": slo, "clients": a.clients,
+                    "ttft_slo_ms": slo, "clients": a.clients, "max_tokens": a.max_tokens,
                     "slo_source": "given" if a.ttft_slo_ms > 0 else "1.5 x healthy warmup TTFT p95",
                     "observable_signals": observable, "rank_cpus": rank_cpus, "burners_per_cpu": a.burners_per_cpu,
                     "interconnect_fault": "tools/xgmi_hog.py peer copies over every GPU pair",

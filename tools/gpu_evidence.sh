@@ -17,6 +17,7 @@
 #   config3   BASELINE config 3: rag-service + vector DB, TCP-retransmit and CPU faults, 2-fault Bayes
 #   spread    the headline bench at K = 20 and K = 200, repeated on one box
 #   rss       the HIP runtime's resident floor under queue / SDMA knobs
+#   probe     the join's oracle GPU tests, the default bench, a kernel trace (join kernel work)
 #
 # Every step runs under its own time limit (tools/gpu_steps.sh); a timeout or crash ends the call.
 set -u
@@ -80,6 +81,10 @@ case "${1:-reentry}" in
       $S "300|k200_$i|python3 bench.py --steps 200 --warmup 10" || exit 1
       tail -n 1 gpurun_out/k200_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('K200', d['ms_per_step'], d['value'])"
     done ;;
+  probe)    # the join's oracle tests (headline shape included), the bench, a kernel trace ($2: out tag)
+    $S "420|native|python -u -m pytest tests/test_native_engine.py tests/test_gpu_engine.py -m gpu -x -v --timeout 360 --timeout-method thread" \
+       "300|bench|python -u bench.py" \
+       "300|trace|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/trace_${2:-probe} -- python3 bench.py --steps 20 --warmup 3 --paced-windows 0" ;;
   rss)
     $S "120|rss_q1|GPU_MAX_HW_QUEUES=1 python tools/rss_probe.py" \
        "120|rss_q1_devq|GPU_MAX_HW_QUEUES=1 HSA_ALLOCATE_QUEUE_DEV_MEM=1 python tools/rss_probe.py" \
