@@ -1,9 +1,15 @@
 #!/usr/bin/env bash
 # Fault matrix: for every scenario x rerun, produce the artefacts the M5 gate consumes
 # (raw_samples.jsonl + collector_overhead.csv per run directory), attribute the replayed
-# incidents and write the benchmark bundle. Synthetic by default; REAL_INJECTORS=true also
-# applies tc-netem delay/loss (network scenarios) or a CPU burner in the kind nodes, in
-# which case the agent's measured signals feed the same pipeline.
+# incidents and write the benchmark bundle. The incident artefacts are synthetic (faultinject /
+# faultreplay); REAL_INJECTORS=true additionally applies tc-netem delay/loss (network scenarios)
+# or a CPU burner in the kind nodes while the run's artefacts are produced -- it does not route
+# measured signals into them.
+#
+# collector_overhead.csv (the gate's B5 input) is measured on the agent that ships: the window
+# agent (ENGINE=gpu on the MI355X runner, cpu elsewhere) with the ConfigMap's toolkit.yaml, the
+# shipped model, the native samplers and the OTLP receiver, at OVERHEAD_RATE events/s for
+# OVERHEAD_SECONDS (tools/agent_overhead.py).
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 export PYTHONPATH="$ROOT${PYTHONPATH:+:$PYTHONPATH}"
@@ -13,6 +19,9 @@ SCENARIOS=${SCENARIOS:-"dns_latency cpu_throttle provider_throttle memory_pressu
 RUNS=${RUNS:-3}
 COUNT=${COUNT:-36}
 REAL_INJECTORS=${REAL_INJECTORS:-false}
+if [ -e /dev/kfd ]; then ENGINE=${ENGINE:-gpu}; else ENGINE=${ENGINE:-cpu}; fi
+OVERHEAD_RATE=${OVERHEAD_RATE:-1e6}
+OVERHEAD_SECONDS=${OVERHEAD_SECONDS:-10}
 
 inject_real() {  # $1 scenario, $2 on|off
   local node=${KIND_NODE:-llm-slo-lab-worker}
@@ -35,17 +44,10 @@ for sc in $SCENARIOS; do
     $CLI.faultreplay --scenario "$sc" --count "$COUNT" --with-signals --seed "$run" --out "$dir/fault_samples.jsonl"
     $CLI.attributor --input "$dir/fault_samples.jsonl" --out "$dir/attributions.jsonl" \
       --summary-out "$dir/attribution_summary.json" --confusion-out "$dir/confusion.csv"
-    python3 - "$dir" <<'PY'
-import csv, os, sys
-from llm_slo_ebpf_toolkit_amd.evaluation import overhead
-d = sys.argv[1]
-m = overhead.measure(duration_s=1.0, mode="agent")
-with open(os.path.join(d, "collector_overhead.csv"), "w", newline="") as fh:
-    w = csv.writer(fh)
-    w.writerow(["timestamp", "node", "collector_cpu_pct", "collector_memory_mb", "events_per_second", "dropped_events"])
-    w.writerow([m.get("timestamp", ""), os.environ.get("NODE_NAME", "node-a"), f"{m['cpu_pct']:.4f}",
-                f"{m.get('rss_mb', 0):.1f}", f"{m.get('events_per_second', 0):.1f}", 0])
-PY
+    rm -f "$dir/collector_overhead.csv"
+    python3 "$ROOT/tools/agent_overhead.py" --engine "$ENGINE" --rate "$OVERHEAD_RATE" \
+      --seconds "$OVERHEAD_SECONDS" --warmup 3 --node "${NODE_NAME:-node-a}" \
+      --csv "$dir/collector_overhead.csv" --out "$dir/agent_overhead.json" > "$dir/agent_overhead.log" 2>&1
     [ "$REAL_INJECTORS" = true ] && inject_real "$sc" off
   done
 done

@@ -9,6 +9,16 @@ core over the measured interval, its own REF-formula gauge from /metrics
 windows and attributions done. Then SIGTERM, and a clean exit is required.
 
     python tools/agent_overhead.py --rate 1e6 --seconds 20 --out gpurun_out/agent_overhead.json
+
+Shipped configuration (the default; ``--bare`` measures the agent with its built-in defaults): the
+ConfigMap's toolkit.yaml (deploy/k8s/configmap.yaml: its 14-signal set, sampling limits, gpu block),
+the shipped learned model, the ConfigMap's min confidence, the native schedstat sampler over a set of
+watched workload processes and the KFD sampler (when /sys/class/kfd exists), and the OTLP span
+receiver fed by a sender posting ``--span-rate`` spans/s. RSS is split into the HIP runtime's queue
+save areas (the large equal-size anonymous mappings ROCr allocates per hardware queue for context
+save/restore) and the rest. ``--csv`` appends the release gate's collector_overhead.csv row (REF
+pkg/releasegate/gate.go:303-376 reads timestamp,node,collector_cpu_pct,collector_memory_mb,
+events_per_second,dropped_events) from this measurement of the window agent.
 """
 
 from __future__ import annotations
@@ -85,6 +95,92 @@ def _smaps_top(pid: int, top: int = 14) -> list:
     return [(k, round(v[0] / 1024, 1), round(v[1] / 1024, 1)) for k, v in rows]
 
 
+def rss_split(pid: int, min_queue_area_mb: float = 64.0) -> dict:
+    """RSS of the HIP runtime's per-queue context save areas vs everything else, from smaps: ROCr
+    maps one anonymous area per hardware queue, all of one size (~173 MB on MI355X); they are
+    the unnamed (anonymous) mappings of at least ``min_queue_area_mb`` (the agent's own large host
+    buffers are pinned /dev/zero mappings or smaller)."""
+    maps = []  # (name, size kB, rss kB)
+    cur = None
+    try:
+        with open(f"/proc/{pid}/smaps") as f:
+            for ln in f:
+                parts = ln.split()
+                if not parts:
+                    continue
+                if not parts[0].endswith(":") or "-" in parts[0]:
+                    cur = [parts[5] if len(parts) > 5 else "", 0, 0]
+                    maps.append(cur)
+                elif parts[0] == "Size:" and cur is not None:
+                    cur[1] = int(parts[1])
+                elif parts[0] == "Rss:" and cur is not None:
+                    cur[2] = int(parts[1])
+    except OSError:
+        return {}
+    qa = [m for m in maps if not m[0] and m[1] >= min_queue_area_mb * 1024 and m[2] > 0]
+    q_rss = sum(m[2] for m in qa)
+    total = sum(m[2] for m in maps)
+    shm = sum(m[2] for m in maps if m[0].startswith("/dev/shm/"))
+    return {"total_mb": round(total / 1024, 1), "queue_save_areas_mb": round(q_rss / 1024, 1),
+            "queue_save_areas": len(qa), "queue_save_area_size_mb": sorted({round(m[1] / 1024, 1) for m in qa}),
+            "shared_rings_mb": round(shm / 1024, 1),
+            "rest_mb": round((total - q_rss - shm) / 1024, 1)}
+
+
+def configmap_toolkit(path: str, out: str) -> dict:
+    """The ConfigMap's toolkit.yaml written to ``out``; returns the ConfigMap's data block."""
+    import yaml
+
+    with open(path) as f:
+        cm = yaml.safe_load(f)
+    data = cm["data"]
+    with open(out, "w") as f:
+        f.write(data["toolkit.yaml"])
+    return data
+
+
+class SpanSender:
+    """Posts OTLP/HTTP JSON request spans to the agent's receiver at a fixed rate (batches every
+    100 ms), as the node's instrumented services would."""
+
+    def __init__(self, port: int, rate: float, pids):
+        import threading
+
+        self.port, self.rate, self.pids = port, rate, list(pids)
+        self.stop = threading.Event()
+        self.sent = self.failed = 0
+        self.t = threading.Thread(target=self.run, daemon=True)
+
+    def run(self):
+        import random
+
+        rng = random.Random(7)
+        per = max(1, int(round(self.rate / 10)))
+        i = 0
+        while not self.stop.wait(0.1):
+            now = time.time_ns()
+            spans = []
+            for _ in range(per):
+                i += 1
+                t0 = now - rng.randrange(50_000_000, 400_000_000)
+                spans.append({"traceId": f"{i:032x}", "spanId": f"{i:016x}", "name": "chat.request", "kind": 2,
+                              "startTimeUnixNano": str(t0), "endTimeUnixNano": str(now),
+                              "attributes": [{"key": "llm.slo.ttft_ms",
+                                              "value": {"doubleValue": rng.uniform(40, 900)}}]})
+            pid = self.pids[i % len(self.pids)] if self.pids else 0
+            body = {"resourceSpans": [{"resource": {"attributes": [
+                {"key": "service.name", "value": {"stringValue": f"svc-{i % 8}"}},
+                {"key": "process.pid", "value": {"intValue": str(pid)}}]},
+                "scopeSpans": [{"scope": {"name": "overhead"}, "spans": spans}]}]}
+            req = urllib.request.Request(f"http://127.0.0.1:{self.port}/v1/traces", data=json.dumps(body).encode(),
+                                         method="POST", headers={"Content-Type": "application/json"})
+            try:
+                urllib.request.urlopen(req, timeout=2).read()
+                self.sent += len(spans)
+            except OSError:
+                self.failed += 1
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rate", type=float, default=1e6, help="events/s the producer writes")
@@ -94,16 +190,43 @@ def main() -> int:
     ap.add_argument("--groups", type=int, default=64)
     ap.add_argument("--spans", type=int, default=16384)
     ap.add_argument("--out", default="")
+    ap.add_argument("--engine", default="gpu", choices=("gpu", "cpu"))
+    ap.add_argument("--bare", action="store_true", help="the agent's built-in defaults instead of the shipped config")
+    ap.add_argument("--configmap", default=os.path.join(ROOT, "deploy", "k8s", "configmap.yaml"))
+    ap.add_argument("--model-path", default=os.path.join(ROOT, "config", "models", "mislo-learned.safetensors"))
+    ap.add_argument("--watched", type=int, default=8, help="workload processes the schedstat / KFD samplers watch")
+    ap.add_argument("--span-rate", type=float, default=200.0, help="OTLP spans/s posted to the receiver")
+    ap.add_argument("--csv", default="", help="append the release gate's collector_overhead.csv row here")
+    ap.add_argument("--node", default=os.environ.get("NODE_NAME", "node-a"))
     a = ap.parse_args()
     import psutil
 
     port = _free_port()
     n_win = int(a.rate * a.window_ms / 1000)
     out_path = os.path.join("/tmp", f"agent_overhead_{os.getpid()}.jsonl")
-    cmd = [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--source", "replay",
+    cmd = [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", a.engine, "--source", "replay",
            "--window-ms", str(a.window_ms), "--window-events", str(n_win), "--window-spans", str(a.spans),
            "--window-groups", str(a.groups), "--scenario", "full", "--output", "jsonl", "--output-path", out_path,
            "--metrics-bind", f"127.0.0.1:{port}"]
+    shipped, watched, sender, rx = {}, [], None, 0
+    if not a.bare:
+        cfg_path = os.path.join("/tmp", f"agent_overhead_toolkit_{os.getpid()}.yaml")
+        data = configmap_toolkit(a.configmap, cfg_path)
+        rx = _free_port()
+        # workload stand-ins the samplers watch (idle processes: the samplers' cost is per watched
+        # process and interval, not per unit of the workload's activity)
+        watched = [subprocess.Popen([sys.executable, "-c", "import time\nwhile True: time.sleep(1)"])
+                   for _ in range(max(0, a.watched))]
+        pods = ",".join(f"{p.pid}:c0f14000-0000-4000-8000-{i:012d}" for i, p in enumerate(watched))
+        kfd = "on" if os.path.isdir("/sys/class/kfd") else "off"
+        cmd += ["--config", cfg_path, "--model-path", a.model_path, "--min-confidence", data.get("MIN_CONFIDENCE", "0.6"),
+                "--gpus", data.get("GPUS", "1"), "--otlp-receiver-bind", f"127.0.0.1:{rx}",
+                "--otlp-receiver-allow", "127.0.0.0/8", "--kfd-sampler", kfd]
+        if watched:
+            cmd += ["--procfs-sampler", "--procfs-pods", pods, "--procfs-interval-ms", "100"]
+        shipped = {"config": os.path.relpath(a.configmap, ROOT) + ":toolkit.yaml", "model": os.path.relpath(a.model_path, ROOT),
+                   "min_confidence": data.get("MIN_CONFIDENCE"), "gpus": data.get("GPUS"), "kfd_sampler": kfd,
+                   "schedstat_sampler_pids": len(watched), "otlp_span_rate": a.span_rate}
     t_start = time.time()
     # the agent as the DaemonSet starts it: the pod env has no GPU_MAX_HW_QUEUES, so the agent's own
     # cap (--gpu-hw-queues, default 1) applies; a box-wide value (4 on the GPU pool) would win over it
@@ -119,6 +242,9 @@ def main() -> int:
                 raise RuntimeError(f"agent did not become ready (rc={agent.poll()}): {agent.stdout.read()[-2000:]}")
             time.sleep(0.5)
         t_ready = time.time()
+        if rx and a.span_rate > 0:
+            sender = SpanSender(rx, a.span_rate, [p.pid for p in watched])
+            sender.t.start()
         print(f"[agent_overhead] ready after {t_ready - t_start:.1f}s; warming {a.warmup}s", flush=True)
         time.sleep(a.warmup)
         kids = proc.children()
@@ -137,6 +263,7 @@ def main() -> int:
         m1 = _scrape(port)
         full = proc.memory_full_info()
         smaps = _smaps_top(agent.pid)
+        split = rss_split(agent.pid)
         wall = w1 - w0
         agent_cpu = (c1.user + c1.system - c0.user - c0.system) / wall * 100.0
         prod_cpu = sum(b.user + b.system - x.user - x.system for x, b in zip(k0, k1)) / wall * 100.0
@@ -155,9 +282,19 @@ def main() -> int:
             "agent_pss_mb": round(getattr(full, "pss", 0) / 2**20, 1),
             "windows_in_interval": win,
             "rss_by_mapping_mb": smaps,
+            "rss_split_mb": split,
+            "shipped_config": shipped or None,
+            "spans_posted": sender.sent if sender else 0,
+            "dropped_events": sum(v for k, v in m1.items() if k.startswith("llm_slo_agent_dropped_events_total"))
+                              - sum(v for k, v in m0.items() if k.startswith("llm_slo_agent_dropped_events_total")),
             "metrics": {k: v for k, v in m1.items() if k.startswith("llm_slo_agent_")},
         }
     finally:
+        if sender is not None:
+            sender.stop.set()
+        for p in watched:
+            p.kill()
+            p.wait(5)
         if agent.poll() is None:
             agent.send_signal(signal.SIGTERM)
         try:
@@ -178,6 +315,19 @@ def main() -> int:
     if a.out:
         with open(a.out, "w") as f:
             f.write(s)
+    if a.csv:
+        import csv
+
+        new = not os.path.exists(a.csv)
+        with open(a.csv, "a", newline="") as fh:
+            w = csv.writer(fh)
+            if new:
+                w.writerow(["timestamp", "node", "collector_cpu_pct", "collector_memory_mb", "events_per_second",
+                            "dropped_events"])
+            w.writerow([time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), a.node,
+                        f"{res['agent_cpu_pct_of_one_core']:.4f}", f"{res['agent_rss_mb']:.1f}",
+                        f"{res['windows_in_interval'] * n_win / max(res['measured_s'], 1e-9):.1f}",
+                        int(res.get("dropped_events") or 0)])
     return 0 if rc == 0 else 1
 
 
