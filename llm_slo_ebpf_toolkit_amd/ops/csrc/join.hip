@@ -545,8 +545,14 @@ __global__ __launch_bounds__(NT) void k_span_sort(SpanCols sc, const uint32_t* _
 
 // LG: incident sums privatised in LDS (12 KB of the workgroup's 38 KB: 4 workgroups per CU);
 // without, they go straight to the striped global copies and the probe fits 6 workgroups per CU.
+#ifndef MISLO_PROBE_DEPTH
+#define MISLO_PROBE_DEPTH 1
+#endif
+#ifndef MISLO_PROBE_MINWG
+#define MISLO_PROBE_MINWG 4
+#endif
 template <int NT, bool LG>
-__global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restrict__ pre,
+__global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const PreSpan* __restrict__ pre,
                                               const uint32_t* __restrict__ span_base, SignalCols gc, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups,
@@ -599,10 +605,11 @@ __global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restr
     __syncthreads();  // previous item's LDS reads are done before s_item / staging reuse
     if (threadIdx.x == 0) s_item = atomicAdd(&work[2 + phase], 1u);
     __syncthreads();
-    const uint32_t it = s_item;
+    // wave-uniform from here: the item's fields, list bounds and pointers live in SGPRs
+    const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
     if (it >= n_work) break;
 #ifdef MISLO_PROBE_PROFILE
-    unsigned long long pt = clock64(), p_stage = 0, p_sig = 0, p_flush = 0;
+    unsigned long long pt = clock64(), p_stage = 0, p_sig = 0, p_flush = 0, p_s1 = 0, p_s2 = 0;
 #endif
     const uint32_t code = items[it];
     const int k = (int)(code >> 30);
@@ -703,7 +710,7 @@ __global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restr
     // accounting reads), 48 coalesced bytes per lane; 16 for the broad tier, which counts from the
     // keys alone -- stream kDepth iterations ahead: no row record is gathered on the common path.
     // A signal's span-run search runs one iteration ahead of its accounting.
-    constexpr int kDepth = 1;
+    constexpr int kDepth = MISLO_PROBE_DEPTH;
     uint32_t q = sg0 + threadIdx.x;
     KeyTs kq[kDepth];
     uint4 ha[kDepth], hb[kDepth];
@@ -735,6 +742,9 @@ __global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restr
     bool vis0, hit0;
     stage1(e0, q < sg1, lo0, vis0, hit0);
     for (; q < sg1; q += NT) {
+#ifdef MISLO_PROBE_PROFILE
+      const unsigned long long q0 = clock64();
+#endif
       const KeyTs e1 = kq[0];
       const uint4 a1 = ha[0], b1h = hb[0];
 #pragma unroll
@@ -747,6 +757,10 @@ __global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restr
       int lo1;
       bool vis1, hit1;
       stage1(e1, q + NT < sg1, lo1, vis1, hit1);
+#ifdef MISLO_PROBE_PROFILE
+      const unsigned long long q1 = clock64();
+      p_s1 += q1 - q0;
+#endif
       // stage 2: this element's accounting
       do {
       if (!vis0) break;
@@ -900,6 +914,9 @@ __global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restr
       }
       add_group(run_grp, g_slot, g_milli, run_n);
       } while (0);
+#ifdef MISLO_PROBE_PROFILE
+      p_s2 += clock64() - q1;
+#endif
       e0 = e1;
       a0 = a1;
       b0 = b1h;
@@ -950,6 +967,8 @@ __global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restr
     atomicAdd(pr + 3, p_stage);
     atomicAdd(pr + 4, p_sig);
     atomicAdd(pr + 5, p_flush);
+    atomicAdd(pr + 6, p_s1);  // signal loop: next entry's wait + span-run search
+    atomicAdd(pr + 7, p_s2);  // signal loop: this entry's accounting
   }
 #endif
   }  // work loop

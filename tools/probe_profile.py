@@ -48,11 +48,14 @@ def main() -> int:
         h.eng.probe_work.zero_()
     out = {}
     for k, name in enumerate(KEYS):
-        items, sig, chunks, stage, sigc, flush = (int(x) for x in acc[k, :6])
+        items, sig, chunks, stage, sigc, flush, s1, s2 = (int(x) for x in acc[k, :8])
         out[name] = {"items": items, "signals": sig, "span_chunks": chunks, "stage_Mcycles": round(stage / 1e6, 2),
                      "signal_Mcycles": round(sigc / 1e6, 2), "flush_Mcycles": round(flush / 1e6, 2),
                      "stage_cycles_per_item": round(stage / max(items, 1)),
-                     "signal_cycles_per_signal_per_wg": round(sigc / max(sig, 1), 1)}
+                     "signal_cycles_per_signal_per_wg": round(sigc / max(sig, 1), 1),
+                     # thread 0's share of the signal loop: waiting for the next entry + its search,
+                     # then this entry's accounting (per 256-signal iteration of a workgroup)
+                     "search_Mcycles": round(s1 / 1e6, 2), "account_Mcycles": round(s2 / 1e6, 2)}
     print(json.dumps({"windows": a.windows, "rows_per_window": a.events, "spans": a.spans, "per_key_type": out},
                      indent=1))
     return 0
