@@ -198,6 +198,8 @@ def main() -> int:
     ap.add_argument("--span-rate", type=float, default=200.0, help="OTLP spans/s posted to the receiver")
     ap.add_argument("--csv", default="", help="append the release gate's collector_overhead.csv row here")
     ap.add_argument("--node", default=os.environ.get("NODE_NAME", "node-a"))
+    ap.add_argument("--no-samplers", action="store_true", help="shipped config without the schedstat / KFD samplers")
+    ap.add_argument("--no-otlp", action="store_true", help="shipped config without the OTLP receiver and its spans")
     a = ap.parse_args()
     import psutil
 
@@ -212,21 +214,22 @@ def main() -> int:
     if not a.bare:
         cfg_path = os.path.join("/tmp", f"agent_overhead_toolkit_{os.getpid()}.yaml")
         data = configmap_toolkit(a.configmap, cfg_path)
-        rx = _free_port()
+        rx = 0 if a.no_otlp else _free_port()
         # workload stand-ins the samplers watch (idle processes: the samplers' cost is per watched
         # process and interval, not per unit of the workload's activity)
         watched = [subprocess.Popen([sys.executable, "-c", "import time\nwhile True: time.sleep(1)"])
-                   for _ in range(max(0, a.watched))]
+                   for _ in range(0 if a.no_samplers else max(0, a.watched))]
         pods = ",".join(f"{p.pid}:c0f14000-0000-4000-8000-{i:012d}" for i, p in enumerate(watched))
-        kfd = "on" if os.path.isdir("/sys/class/kfd") else "off"
+        kfd = "on" if os.path.isdir("/sys/class/kfd") and not a.no_samplers else "off"
         cmd += ["--config", cfg_path, "--model-path", a.model_path, "--min-confidence", data.get("MIN_CONFIDENCE", "0.6"),
-                "--gpus", data.get("GPUS", "1"), "--otlp-receiver-bind", f"127.0.0.1:{rx}",
-                "--otlp-receiver-allow", "127.0.0.0/8", "--kfd-sampler", kfd]
+                "--gpus", data.get("GPUS", "1"), "--kfd-sampler", kfd]
+        if rx:
+            cmd += ["--otlp-receiver-bind", f"127.0.0.1:{rx}", "--otlp-receiver-allow", "127.0.0.0/8"]
         if watched:
             cmd += ["--procfs-sampler", "--procfs-pods", pods, "--procfs-interval-ms", "100"]
         shipped = {"config": os.path.relpath(a.configmap, ROOT) + ":toolkit.yaml", "model": os.path.relpath(a.model_path, ROOT),
                    "min_confidence": data.get("MIN_CONFIDENCE"), "gpus": data.get("GPUS"), "kfd_sampler": kfd,
-                   "schedstat_sampler_pids": len(watched), "otlp_span_rate": a.span_rate}
+                   "schedstat_sampler_pids": len(watched), "otlp_span_rate": a.span_rate if rx else 0}
     t_start = time.time()
     # the agent as the DaemonSet starts it: the pod env has no GPU_MAX_HW_QUEUES, so the agent's own
     # cap (--gpu-hw-queues, default 1) applies; a box-wide value (4 on the GPU pool) would win over it

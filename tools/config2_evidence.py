@@ -155,15 +155,17 @@ def main() -> int:
                     help="GEMM burner processes on the GPU in the fault phase (4 left 2 requests in 24 s, "
                          "profiles/r4_config2_first)")
     ap.add_argument("--prompt-words", type=int, default=256, help="prompt length (prefill tokens)")
-    ap.add_argument("--max-tokens", type=int, default=2, help="tokens per request: TTFT is the SLO, short "
-                                                              "answers keep requests completing in every window")
-    ap.add_argument("--clients", type=int, default=2, help="concurrent closed-loop clients")
+    ap.add_argument("--max-tokens", type=int, default=1, help="tokens per request: TTFT is the SLO; under the "
+                                                              "fault each decoded token costs ~1 s more, one token "
+                                                              "keeps requests completing in every 1 s window")
+    ap.add_argument("--clients", type=int, default=3, help="concurrent closed-loop clients")
     ap.add_argument("--gap-s", type=float, default=0.05, help="client think time between requests")
     ap.add_argument("--halo-ms", type=int, default=3000,
                     help="agent halo: a contended request's span arrives ~1-2 s after its start (its TTFT plus "
                          "the exporter's batch delay), and its records are joined around that start")
-    ap.add_argument("--window-ms", type=int, default=2000,
-                    help="agent window: under the fault a request takes over a second, so 2 s windows")
+    ap.add_argument("--window-ms", type=int, default=1000,
+                    help="agent window (1 s: with 1-token requests from 3 clients every window holds a completed "
+                         "request under the fault; 2 s windows put the first attribution ~3.6 s after the onset)")
     ap.add_argument("--model-path", default=MODEL, help="the agent's model ('' = the bayes_gpu expert table)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
