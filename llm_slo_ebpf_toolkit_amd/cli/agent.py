@@ -148,6 +148,14 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
             os.environ["GPU_MAX_HW_QUEUES"] = str(int(a.gpu_hw_queues))
         else:
             os.environ.setdefault("GPU_MAX_HW_QUEUES", str(int(a.gpu_hw_queues)))
+    if os.environ.get("GPU_MAX_HW_QUEUES") == "1":
+        # one hardware queue runs a copy stream's and the compute stream's commands in order
+        # anyway: one HIP stream (its second stream's host state is ~16 MB), and the window's
+        # host->device copies as blit kernels on that queue instead of SDMA -- the first large SDMA
+        # copy maps another 173.4 MB queue save area into the process (tools/native/hip_rss_floor.hip,
+        # profiles/r5_rss/); the agent copies ~20 MB/s at 1M events/s, far below either path's rate
+        os.environ.setdefault("MISLO_ONE_STREAM", "1")
+        os.environ.setdefault("HSA_ENABLE_SDMA", "0")
     return o, a.probe_smoke
 
 

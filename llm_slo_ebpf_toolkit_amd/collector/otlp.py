@@ -311,49 +311,82 @@ class SpanMapper:
                 at_peer = self.pod_ips().get(peer)
             except Exception:  # noqa: BLE001 - an unreadable map checks nothing
                 at_peer = None
-        out = np.zeros(len(sel), dtype=records.SPAN)
-        keep = np.ones(len(sel), dtype=bool)
-        for i, (res, d) in enumerate(sel):
+        # per-field lists, written into the record array column by column at the end: setting the
+        # fields of one structured element at a time cost ~18 us per span (the receiver's CPU)
+        ts, tr, sh, pids, pods, svcs, grps, ttft, lat, conn = ([] for _ in range(10))
+        res_cache: Dict[int, tuple] = {}  # one resource's service / pod / pid per request
+        groups_seen: Dict[str, int] = {}
+        pods_seen: Dict[object, int] = {}
+        for res, d in sel:
             a = d["attrs"]
             t0 = int(d.get("startTimeUnixNano") or 0)
             t1 = int(d.get("endTimeUnixNano") or t0)
-            svc = str(_first(res, ("service.name",)) or _first(a, ("service.name",)) or "unknown")
-            pod = _first(res, ("k8s.pod.uid",)) or _first(res, ("k8s.pod.name",)) or ""
-            pid = _first(res, ("process.pid",)) or _first(a, ("process.pid", "thread.id")) or 0
-            ttft = _first(a, TTFT_KEYS)
-            sport = _first(a, ("client.port", "net.host.port", "net.sock.host.port")) or 0
-            dport = _first(a, ("server.port", "net.peer.port", "net.sock.peer.port")) or 0
-            dip = _ipv4(_first(a, ("server.address", "net.peer.ip", "net.sock.peer.addr")) or "")
+            rk = id(res)
+            rv = res_cache.get(rk)
+            if rv is None:
+                rv = res_cache[rk] = (_first(res, ("service.name",)), _first(res, ("k8s.pod.uid",)) or
+                                      _first(res, ("k8s.pod.name",)) or "", _first(res, ("process.pid",)))
+            svc = str(rv[0] or _first(a, ("service.name",)) or "unknown")
+            pod = rv[1]
+            gk = groups_seen.get(svc)
+            pid = rv[2] or _first(a, ("process.pid", "thread.id")) or 0
             if pod and at_peer is not None and str(pod) not in at_peer:
                 self.spoofed += 1
-                keep[i] = False
                 continue
-            g = self.groups.id(svc)
-            out[i]["ts_ns"] = t0
-            out[i]["trace_h"] = trace_hash(d.get("traceId"))
-            out[i]["span_h"] = span_hash(d.get("spanId"))
-            out[i]["pid"] = int(pid)
-            pid_ = self.pod_id(str(pod)) if pod else 0
-            out[i]["pod_id"] = pid_
-            out[i]["node_id"] = self.node_id
-            out[i]["svc_id"] = g + 1
+            if gk is None:
+                gk = groups_seen[svc] = self.groups.id(svc)
+            g = gk
+            pid_ = pods_seen.get(pod)
+            if pid_ is None:
+                pid_ = pods_seen[pod] = self.pod_id(str(pod)) if pod else 0
             if pid_:
                 sn = ((g + 1) << 16) | (self.node_id & 0xFFFF)
                 bound = self._pods.get(pid_)
                 if bound is not None and bound != sn:
                     self.conflicts += 1
-                    keep[i] = False
                     continue
                 if bound is None:
                     with self._plock:
                         self._pods[pid_] = sn
                         self._new[pid_] = sn
-            out[i]["group_id"] = g
-            out[i]["ttft_ms"] = float(ttft) if ttft is not None else np.nan
-            out[i]["latency_ms"] = (t1 - t0) / 1e6
+            sport = _first(a, ("client.port", "net.host.port", "net.sock.host.port")) or 0
+            dport = _first(a, ("server.port", "net.peer.port", "net.sock.peer.port")) or 0
+            v = _first(a, TTFT_KEYS)
+            ts.append(t0)
+            tr.append(trace_hash(d.get("traceId")))
+            sh.append(span_hash(d.get("spanId")))
+            pids.append(int(pid))
+            pods.append(pid_)
+            svcs.append(g + 1)
+            grps.append(g)
+            ttft.append(float(v) if v is not None else np.nan)
+            lat.append((t1 - t0) / 1e6)
             if int(sport) or int(dport):
-                out[i]["conn_h"] = records.conn_hash(int(sport), int(dport), dip)
-        return out if keep.all() else out[keep]
+                dip = _ipv4(_first(a, ("server.address", "net.peer.ip", "net.sock.peer.addr")) or "")
+                conn.append(records.conn_hash(int(sport), int(dport), dip))
+            else:
+                conn.append(0)
+        out = np.zeros(len(ts), dtype=records.SPAN)
+        if ts:
+            out["ts_ns"] = ts
+            out["trace_h"] = np.array(tr, dtype=np.uint64)
+            out["span_h"] = np.array(sh, dtype=np.uint64)
+            out["pid"] = pids
+            out["pod_id"] = pods
+            out["node_id"] = self.node_id
+            out["svc_id"] = svcs
+            out["group_id"] = grps
+            out["ttft_ms"] = ttft
+            out["latency_ms"] = lat
+            out["conn_h"] = np.array(conn, dtype=np.uint64)
+        return out
+
+
+class _Headers(dict):
+    """Request headers by lower-cased name, with the case-insensitive ``get`` of http.client's."""
+
+    def get(self, key, default=None):
+        return super().get(key.lower(), default)
 
 
 class OtlpSpanReceiver:
@@ -373,6 +406,7 @@ class OtlpSpanReceiver:
         self.allow = [ipaddress.ip_network(c.strip(), strict=False) for c in allow.split(",") if c.strip()]
         self.accepted = self.rejected = self.dropped = self.requests = 0
         self.refused = 0  # peers outside the allow-list, oversized or unframed bodies
+        self._peer_ok: Dict[str, bool] = {}
         self._lock = threading.Lock()
         self._srv: Optional[http.server.ThreadingHTTPServer] = None
         self._thr: Optional[threading.Thread] = None
@@ -398,12 +432,47 @@ class OtlpSpanReceiver:
             def log_message(self, *a):  # noqa: D401 - quiet
                 pass
 
+            def parse_request(self) -> bool:
+                """The request line and headers without the email-package parser
+                (http.client.parse_headers: ~0.3 ms of the receiver's ~1.4 ms per export request):
+                exporters send a handful of plain headers; anything unusual falls back to it."""
+                line = str(self.raw_requestline, "iso-8859-1").rstrip("\r\n")
+                parts = line.split()
+                if len(parts) != 3 or not parts[2].startswith("HTTP/1."):
+                    return super().parse_request()
+                self.command, self.path, self.request_version = parts
+                self.requestline = line
+                hdrs = _Headers()
+                for _ in range(100):
+                    raw = self.rfile.readline(65537)
+                    if len(raw) > 65536:
+                        self.send_error(431, "Line too long")
+                        return False
+                    if raw in (b"\r\n", b"\n", b""):
+                        break
+                    k, sep, v = raw.decode("iso-8859-1").partition(":")
+                    if not sep:
+                        self.send_error(400, "Bad header line")
+                        return False
+                    hdrs[k.strip().lower()] = v.strip()
+                else:
+                    self.send_error(431, "Too many headers")
+                    return False
+                self.headers = hdrs
+                conn = hdrs.get("connection", "").lower()
+                self.close_connection = conn == "close" or (self.request_version == "HTTP/1.0" and conn != "keep-alive")
+                if hdrs.get("expect", "").lower() == "100-continue":
+                    self.send_response_only(100)
+                    self.end_headers()
+                return True
+
             def _reply(self, code: int, body: bytes, ctype: str) -> None:
-                self.send_response(code)
-                self.send_header("Content-Type", ctype)
-                self.send_header("Content-Length", str(len(body)))
-                self.end_headers()
-                self.wfile.write(body)
+                # one write: status line, headers and body (send_response formats a Date header
+                # and buffers per header)
+                head = (f"HTTP/1.1 {code} {self.responses.get(code, ('',))[0]}\r\nContent-Type: {ctype}\r\n"
+                        f"Content-Length: {len(body)}\r\n" + ("Connection: close\r\n" if self.close_connection else "")
+                        + "\r\n")
+                self.wfile.write(head.encode("latin-1") + body)
 
             def _refuse(self, code: int, msg: bytes) -> None:
                 with rx._lock:
@@ -413,11 +482,17 @@ class OtlpSpanReceiver:
 
             def do_POST(self):
                 if rx.allow:
-                    try:
-                        peer = ipaddress.ip_address(self.client_address[0])
-                    except ValueError:
-                        peer = None
-                    if peer is None or not any(peer in net for net in rx.allow):
+                    host = self.client_address[0]
+                    ok = rx._peer_ok.get(host)
+                    if ok is None:  # decided once per peer address (ipaddress parsing is slow)
+                        try:
+                            peer = ipaddress.ip_address(host)
+                        except ValueError:
+                            peer = None
+                        ok = peer is not None and any(peer in net for net in rx.allow)
+                        if len(rx._peer_ok) < 4096:
+                            rx._peer_ok[host] = ok
+                    if not ok:
                         self._refuse(403, b"forbidden")
                         return
                 if not self.path.startswith("/v1/traces"):

@@ -143,7 +143,17 @@ void WindowEngine::alloc() {
   const int64_t N = n_rows_;
   nblk_sig_ = decode_grid((int)N);
   nblk_span_ = decode_grid((int)S);
-  HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  // MISLO_ONE_STREAM=1: the window's copies on the compute stream (one HIP stream). With one
+  // hardware queue (the agent's GPU_MAX_HW_QUEUES=1) the two streams' commands run in order on
+  // that queue anyway, and the copy stream's first use maps another ~173 MB queue save area
+  // (tools/rss_probe.py); the bench keeps the two streams (copy / compute overlap on 4 queues).
+  const bool one_stream = [] {
+    const char* v = getenv("MISLO_ONE_STREAM");
+    return v && atoi(v) == 1;
+  }();
+  HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  if (one_stream) copy_ = compute_;
+  else HIPCHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   {  // MISLO_SPIN_WAIT=1: wait() polls its event instead of sleeping on it
     const char* v = getenv("MISLO_SPIN_WAIT");
     spin_ = v && atoi(v) == 1;
@@ -151,10 +161,9 @@ void WindowEngine::alloc() {
   {  // MISLO_COPY_STREAMS=2 splits a window's DMA over two streams (measured slower: the
      // second stream's large copy blocks the issuing thread ~0.2 ms per window)
     const char* v = getenv("MISLO_COPY_STREAMS");
-    if (v && atoi(v) == 2) HIPCHECK(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking));
+    if (v && atoi(v) == 2 && !one_stream) HIPCHECK(hipStreamCreateWithFlags(&copy2_, hipStreamNonBlocking));
     else copy2_ = copy_;
   }
-  HIPCHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   {
     const char* v = getenv("MISLO_SPAN_STREAM");
     branch_ = v && atoi(v) == 1;
@@ -337,7 +346,7 @@ WindowEngine::~WindowEngine() {
                   rows_, tmax_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_, g_keys_, gen_, s_pre_};
   for (void* p : bufs)
     if (p) hipFree(p);
-  if (copy_) hipStreamDestroy(copy_);
+  if (copy_ && copy_ != compute_) hipStreamDestroy(copy_);
   if (copy2_ && copy2_ != copy_) hipStreamDestroy(copy2_);
   if (compute_) hipStreamDestroy(compute_);
   if (side_) hipStreamDestroy(side_);

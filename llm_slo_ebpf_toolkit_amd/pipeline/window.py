@@ -129,6 +129,8 @@ class WindowPipeline:
             if tuple(self.mod.PACKET_LAYOUT) != PACKET_LAYOUT:
                 raise RuntimeError("stale _mislo_agent build: packet layout mismatch (rebuild with ops.build)")
             self.stats_off, self.stats_len = int(self.mod.STATS_OFF), int(self.mod.STATS_LEN)
+            if os.environ.get("MISLO_GRAPHS", "") == "0":  # diagnostic: plain launches instead of HIP graphs
+                use_graphs = False
             self.eng = self.mod.WindowEngine(max_ahead=max_ahead, use_graphs=use_graphs,
                                              device_refit=self.device_refit, **kw)
         else:

@@ -24,6 +24,7 @@ events_per_second,dropped_events) from this measurement of the window agent.
 from __future__ import annotations
 
 import argparse
+import http.client
 import json
 import os
 import signal
@@ -156,6 +157,7 @@ class SpanSender:
 
         rng = random.Random(7)
         per = max(1, int(round(self.rate / 10)))
+        conn = None
         i = 0
         while not self.stop.wait(0.1):
             now = time.time_ns()
@@ -172,13 +174,18 @@ class SpanSender:
                 {"key": "service.name", "value": {"stringValue": f"svc-{i % 8}"}},
                 {"key": "process.pid", "value": {"intValue": str(pid)}}]},
                 "scopeSpans": [{"scope": {"name": "overhead"}, "spans": spans}]}]}
-            req = urllib.request.Request(f"http://127.0.0.1:{self.port}/v1/traces", data=json.dumps(body).encode(),
-                                         method="POST", headers={"Content-Type": "application/json"})
-            try:
-                urllib.request.urlopen(req, timeout=2).read()
+            try:  # one keep-alive connection, as an OTLP/HTTP exporter holds
+                if conn is None:
+                    conn = http.client.HTTPConnection("127.0.0.1", self.port, timeout=2)
+                conn.request("POST", "/v1/traces", body=json.dumps(body).encode(),
+                             headers={"Content-Type": "application/json"})
+                conn.getresponse().read()
                 self.sent += len(spans)
-            except OSError:
+            except (OSError, http.client.HTTPException):
                 self.failed += 1
+                if conn is not None:
+                    conn.close()
+                conn = None
 
 
 def main() -> int:
@@ -200,6 +207,7 @@ def main() -> int:
     ap.add_argument("--node", default=os.environ.get("NODE_NAME", "node-a"))
     ap.add_argument("--no-samplers", action="store_true", help="shipped config without the schedstat / KFD samplers")
     ap.add_argument("--no-otlp", action="store_true", help="shipped config without the OTLP receiver and its spans")
+    ap.add_argument("--env-hw-queues", type=int, default=0, help="diagnostic: GPU_MAX_HW_QUEUES in the agent's env")
     a = ap.parse_args()
     import psutil
 
@@ -236,6 +244,8 @@ def main() -> int:
     # and map three more 173 MB queue save areas into the agent
     env = dict(os.environ)
     box_queues = env.pop("GPU_MAX_HW_QUEUES", None)
+    if a.env_hw_queues:  # diagnostic: the cap in the agent's environment from the start
+        env["GPU_MAX_HW_QUEUES"] = str(a.env_hw_queues)
     agent = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
     proc = psutil.Process(agent.pid)
     try:

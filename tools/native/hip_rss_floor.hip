@@ -89,5 +89,34 @@ int main() {
   step("hipGraphInstantiate", hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   step("hipGraphLaunch", hipGraphLaunch(ge, s));
   step("hipStreamSynchronize", hipStreamSynchronize(s));
+  // the engine's per-window calls, one at a time: which of them maps a queue save area beyond
+  // the stream's (round 5: the agent holds three 173.4 MB areas at GPU_MAX_HW_QUEUES=1)
+  step("hipMemcpyAsync H2D 16 MB pinned", hipMemcpyAsync(d, pin, 16 << 20, hipMemcpyHostToDevice, s));
+  step("hipStreamSynchronize", hipStreamSynchronize(s));
+  std::vector<char> big(32 << 20, 1);
+  step("hipHostRegister 32 MB", hipHostRegister(big.data(), big.size(), hipHostRegisterDefault));
+  step("hipMemcpyAsync H2D 32 MB registered", hipMemcpyAsync(d, big.data(), 32 << 20, hipMemcpyHostToDevice, s));
+  step("hipStreamSynchronize", hipStreamSynchronize(s));
+  hipEvent_t ev;
+  step("hipEventCreateWithFlags", hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  step("hipEventRecord", hipEventRecord(ev, s));
+  step("hipEventSynchronize", hipEventSynchronize(ev));
+  hipEvent_t evt;
+  step("hipEventCreate (timing)", hipEventCreate(&evt));
+  step("hipEventRecord (timing)", hipEventRecord(evt, s));
+  step("hipEventSynchronize (timing)", hipEventSynchronize(evt));
+  step("hipMemcpy D2H 8 B (null stream)", hipMemcpy(h.data(), d, 8, hipMemcpyDeviceToHost));
+  step("hipMemcpy H2D 8 B (null stream)", hipMemcpy(d, h.data(), 8, hipMemcpyHostToDevice));
+  step("hipMemsetAsync 1 MB", hipMemsetAsync(d, 0, 1 << 20, s));
+  step("hipStreamSynchronize", hipStreamSynchronize(s));
+  k_touch<<<1024, 256>>>(d, 1 << 18);
+  step("kernel on the null stream", hipGetLastError());
+  step("hipDeviceSynchronize", hipDeviceSynchronize());
+  hipStream_t s2;
+  step("second stream (same priority)", hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  k_touch<<<1024, 256, 0, s2>>>(d, 1 << 18);
+  step("kernel on the second stream", hipGetLastError());
+  step("hipStreamWaitEvent (cross-stream)", hipStreamWaitEvent(s, ev, 0));
+  step("hipDeviceSynchronize", hipDeviceSynchronize());
   return 0;
 }

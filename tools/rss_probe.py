@@ -104,6 +104,25 @@ def main():
         src.step(64)
     src.drain()
     step("4 empty windows", detail=True)
+    # real windows (spans only: the join, posterior, refit and result paths run), the queue save
+    # areas counted after each phase: which call maps a hardware queue beyond the first stream's
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+
+    def areas():
+        return len([m for m in big_anon(100.0) if 170 < m[0] < 180])
+
+    w = ReplayGenerator(ReplayConfig(events_per_window=4096, spans_per_window=4096, n_services=64)).next_window()
+    sp = np.ascontiguousarray(w.spans)
+    for k in range(6):
+        j = pipe.submit([], [], [(sp.ctypes.data, sp.nbytes)], 64, labels=np.zeros(64, np.int32))
+        print(f"  window {j} submitted: queue areas {areas()}", flush=True)
+        pipe.wait(j)
+        print(f"  window {j} done:      queue areas {areas()}", flush=True)
+        pipe.results(j, 64)
+        print(f"  window {j} results:   queue areas {areas()}", flush=True)
+    step("6 span windows", detail=True)
     pipe.eng.close()
     step("engine closed")
 
