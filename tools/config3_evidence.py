@@ -22,6 +22,10 @@ One box, one run:
   - ``cpu_throttle``: CPU burners pinned to the RAG service's CPUs (a real noisy neighbour; the
     run-queue delay the agent sees is measured, not injected);
   - ``compound``: both at once (REF's 2-fault case);
+  - ``retrieval_backend`` (``--retrieval-phase``, on by default): the vector DB stalls every response and
+    nothing else is injected -- the fault lives inside the vector DB's process, where only the
+    root-only syscall / disk probes would see it; scored apart from REF's two single faults
+    (``single_fault_macro_f1`` keeps REF's set, ``single_fault_macro_f1_with_retrieval`` adds it);
 * out: per phase, the agent's top-1 domain of the RAG service's incident group per window,
   single-fault accuracy / macro-F1, compound partial accuracy and coverage@0.10 (REF's
   definitions, pipeline.go:140-185), detection delay (fault onset -> arrival of the first correct
@@ -58,7 +62,7 @@ MODEL = os.path.join(ROOT, "config", "models", "mislo-learned.safetensors")
 BURN = "import os, sys\nos.sched_setaffinity(0, {int(sys.argv[1])})\nwhile True:\n    pass\n"
 EXPECT = {"baseline": set(), "fault_network": {"network_egress"}, "recovery_1": set(),
           "fault_cpu": {"cpu_throttle"}, "recovery_2": set(), "fault_compound": {"network_egress", "cpu_throttle"},
-          "recovery_3": set()}
+          "recovery_3": set(), "fault_retrieval": {"retrieval_backend"}, "recovery_4": set()}
 
 
 class Client(threading.Thread):
@@ -268,6 +272,8 @@ def main() -> int:
     ap.add_argument("--max-tokens", type=int, default=8, help="tokens per request (short requests keep completing under contention)")
     ap.add_argument("--delay-ms", type=float, default=150.0, help="vector-DB stall per response in network faults")
     ap.add_argument("--retrans-rate", type=float, default=20.0, help="fault-profile record sets per second")
+    ap.add_argument("--retrieval-phase", type=int, default=1,
+                    help="1: add a vector-DB stall phase with nothing injected (retrieval_backend), then a recovery")
     ap.add_argument("--ttft-slo-ms", type=float, default=0.0,
                     help="the agent's TTFT SLO; 0 = calibrated from the healthy warmup (slo_from_warmup)")
     ap.add_argument("--window-ms", type=int, default=1000)
@@ -363,13 +369,16 @@ def main() -> int:
         plan = [("baseline", a.phase_s), ("fault_network", a.phase_s), ("recovery_1", a.recover_s),
                 ("fault_cpu", a.phase_s), ("recovery_2", a.recover_s), ("fault_compound", a.phase_s),
                 ("recovery_3", a.recover_s)]
+        if a.retrieval_phase:
+            plan += [("fault_retrieval", a.phase_s), ("recovery_4", a.recover_s)]
         for name, dur in plan:
             exp = EXPECT[name]
             t0 = time.time_ns()
             cur["phase"] = name
             m0 = scrape_counters(mport)
-            if "network_egress" in exp:
+            if "network_egress" in exp or "retrieval_backend" in exp:
                 post(f"http://127.0.0.1:{vport}/fault", {"delay_ms": a.delay_ms})
+            if "network_egress" in exp:
                 inj = subprocess.Popen(
                     [sys.executable, "-m", "llm_slo_ebpf_toolkit_amd.cli.faultinject", "--emit-ring", prefix,
                      "--fault", "network_partition", "--pod-uid", POD_UID, "--agent", f"http://127.0.0.1:{mport}",
@@ -383,7 +392,7 @@ def main() -> int:
             if inj is not None:
                 inj.wait(30)
                 inj = None
-            if "network_egress" in exp:
+            if "network_egress" in exp or "retrieval_backend" in exp:
                 post(f"http://127.0.0.1:{vport}/fault", {"delay_ms": 0})
             for b in burners:
                 b.kill()
@@ -418,7 +427,15 @@ def main() -> int:
     with open(os.path.join(a.out, "requests.jsonl"), "w") as f:
         for r in rows:
             f.write(json.dumps(r) + "\n")
-    res = score(phases, tailer.rows, a.window_ms, cuts=load_cuts(os.path.join(a.out, "decisions.jsonl")))
+    cuts = load_cuts(os.path.join(a.out, "decisions.jsonl"))
+    res = score(phases, tailer.rows, a.window_ms, cuts=cuts)
+    ref_set = [p for p in phases if p[0] not in ("fault_retrieval", "recovery_4")]
+    if len(ref_set) < len(phases):  # REF's single faults only (network, CPU) vs with the retrieval stall
+        ref = score(ref_set, tailer.rows, a.window_ms, cuts=cuts)
+        res["single_fault_f1_with_retrieval"] = res["single_fault_f1"]
+        res["single_fault_macro_f1_with_retrieval"] = res["single_fault_macro_f1"]
+        res["single_fault_f1"] = ref["single_fault_f1"]
+        res["single_fault_macro_f1"] = ref["single_fault_macro_f1"]
     res["ttft_ms"] = {n: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
                       for n, _t0, _t1 in phases for v in [[r["ttft_ms"] for r in rows if r["phase"] == n]]}
     res["agent_overhead_metrics"] = overhead
@@ -430,6 +447,7 @@ def main() -> int:
                     "recover_s": a.recover_s, "clients": a.clients, "max_tokens": a.max_tokens,
                     "procfs_interval_ms": a.procfs_ms, "ttft_slo_ms": slo,
                     "slo_source": "given" if a.ttft_slo_ms > 0 else "1.5 x healthy warmup TTFT p95",
+                    "retrieval_fault": "vector-DB response stall only (no records injected)" if a.retrieval_phase else None,
                     "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "
                                      "injected on its connections via faultinject --emit-ring --fault",
                     "cpu_fault": "pinned CPU burners; run-queue delay and CPU wait share measured by the agent's "
