@@ -65,7 +65,7 @@ class Engine {
     g_part_off = torch::empty_like(g_part_blk);
     g_part_tot = torch::empty({kKeyTypes * kParts}, i32);
     g_part_base = torch::empty({kKeyTypes * kParts + 1}, i32);
-    g_items = torch::empty({kKeyTypes * N * (int64_t)sizeof(HotSig)}, u8);
+    g_items = torch::empty({kKeyTypes * N}, i32);
     g_keys = torch::empty({kKeyTypes * N * (int64_t)sizeof(KeyTs)}, u8);
     g_rec = torch::empty({(int64_t)N * (int64_t)sizeof(SigRec)}, u8);
     // span columns
@@ -151,7 +151,7 @@ class Engine {
   // one generation (no halo): slot 0, every row local
   SignalCols sig_cols() {
     return SignalCols{reinterpret_cast<SigRec*>(g_rec.data_ptr()), dptr<uint8_t>(g_status),
-                      reinterpret_cast<PartCodes*>(g_part.data_ptr()), reinterpret_cast<HotSig*>(g_items.data_ptr()),
+                      reinterpret_cast<PartCodes*>(g_part.data_ptr()), dptr<uint32_t>(g_items),
                       reinterpret_cast<KeyTs*>(g_keys.data_ptr()), dptr<uint32_t>(g_part_base), nullptr,
                       (int64_t)sig_cap_, 1};
   }

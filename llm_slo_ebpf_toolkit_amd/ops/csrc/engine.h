@@ -257,8 +257,8 @@ class WindowEngine {
   int model_slot_ = 0;
   uint8_t* g_status_ = nullptr;
   PartCodes* g_part_ = nullptr;
-  uint32_t *g_part_blk_ = nullptr, *g_part_off_ = nullptr, *g_part_tot_ = nullptr, *g_part_base_ = nullptr;
-  HotSig* g_items_ = nullptr;      // [gens][kKeyTypes * n_rows] partition lists (row index + probe fields)
+  uint32_t *g_part_blk_ = nullptr, *g_part_off_ = nullptr, *g_part_tot_ = nullptr, *g_part_base_ = nullptr,
+           *g_items_ = nullptr;
   SigRec* g_rec_ = nullptr;
   PartCodes* s_part_ = nullptr;
   uint32_t *s_part_blk_ = nullptr, *s_part_off_ = nullptr, *s_part_tot_ = nullptr, *s_part_base_ = nullptr,

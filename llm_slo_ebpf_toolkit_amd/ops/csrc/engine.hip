@@ -285,7 +285,7 @@ void WindowEngine::alloc() {
   g_part_tot_ = dalloc<uint32_t>(kKeyTypes * kParts);
   g_part_base_ = dalloc<uint32_t>((size_t)gens_ * kBaseLen);
   // resident generations: rows, partition lists, list keys and offsets of the last gens_ windows
-  g_items_ = dalloc<HotSig>((size_t)gens_ * kKeyTypes * N);
+  g_items_ = dalloc<uint32_t>((size_t)gens_ * kKeyTypes * N);
   g_keys_ = dalloc<KeyTs>((size_t)gens_ * kKeyTypes * N);
   g_rec_ = dalloc<SigRec>((size_t)gens_ * N);
   s_part_ = dalloc<PartCodes>(S);

@@ -146,18 +146,17 @@ __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ co
   }
 }
 
-// Signal scatter: the current generation's partition lists, each entry the row's (key hash, ts)
-// for the list's key type plus its HotSig (row index and the fields the probe reads), written once
-// and streamed by the probe of this window and of the later windows the rows stay in the halo for
-// -- the probe never gathers a row record on its common path. The hashes are recomputed from the
-// row records (the decode kept only their partitions); the rows are read in order.
+// Signal scatter: the current generation's partition lists, each entry a row index plus the
+// row's (key hash, ts) for the list's key type, written once and streamed by the probe of this
+// window and of the later windows the rows stay in the halo for. The hashes are recomputed from
+// the row records (the decode kept only their partitions); the rows are read in order.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __restrict__ n_ptr, int cap,
                                                     const uint32_t* __restrict__ part_off, int nblk_a) {
   const uint32_t cur = cur_slot(gc);
   const SigRec* rec = gc.rec + (size_t)cur * (size_t)gc.stride;
   const uint32_t* base = gc.base + (size_t)cur * kBaseLen;
-  uint4* hot = reinterpret_cast<uint4*>(gc.items + (size_t)cur * kKeyTypes * (size_t)gc.stride);
+  uint32_t* items = gc.items + (size_t)cur * kKeyTypes * (size_t)gc.stride;
   KeyTs* keys = gc.keys + (size_t)cur * kKeyTypes * (size_t)gc.stride;
   // next slot per list (see k_scatter)
   __shared__ uint32_t s_pos[kKeyTypes * kParts];
@@ -206,10 +205,8 @@ __global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __
       for (int k = 0; k < kKeyTypes; ++k) {
         if (pc[u].p[k] == kNoPart) continue;
         const uint32_t pos = atomicAdd(&s_pos[k * kParts + pc[u].p[k]], 1u);
+        items[pos] = (uint32_t)(i0 + u * NT);
         keys[pos] = KeyTs{key_hash(k, tr, b[u].z, b[u].w, cn, c4[u].x), ts};
-        // HotSig: cn | pod | pid (the row's second 16 bytes), then sn | val | row | slot
-        hot[2 * (size_t)pos] = b[u];
-        hot[2 * (size_t)pos + 1] = make_uint4(c4[u].x, c4[u].y, (uint32_t)(i0 + u * NT), c4[u].z);
       }
     }
   }
@@ -236,6 +233,30 @@ __device__ __forceinline__ void top3_insert(unsigned long long* slot3, unsigned 
 }
 
 __device__ __forceinline__ int64_t iabs64(int64_t x) { return x < 0 ? -x : x; }
+
+// The first 48 bytes of a SigRec (every field the probe reads; the padding is never loaded):
+// three 16-byte loads per gathered signal.
+struct SigHot {
+  int64_t ts;
+  uint64_t tr, cn;
+  uint32_t pod, pid, sn;
+  float val;
+  uint32_t slot;
+};
+__device__ __forceinline__ SigHot load_hot(const SigRec* p) {
+  const uint4* v = reinterpret_cast<const uint4*>(p);
+  const uint4 a = v[0], b = v[1], c = v[2];
+  SigHot h;
+  h.ts = (int64_t)(((uint64_t)a.y << 32) | a.x);
+  h.tr = ((uint64_t)a.w << 32) | a.z;
+  h.cn = ((uint64_t)b.y << 32) | b.x;
+  h.pod = b.z;
+  h.pid = b.w;
+  h.sn = c.x;
+  h.val = __uint_as_float(c.y);
+  h.slot = c.z;
+  return h;
+}
 
 // Work decomposition: two launches (the trace tier first, then pod+pid / pod+conn /
 // svc+node) of a fixed grid that dequeues items from a device-built work list (see
@@ -545,14 +566,8 @@ __global__ __launch_bounds__(NT) void k_span_sort(SpanCols sc, const uint32_t* _
 
 // LG: incident sums privatised in LDS (12 KB of the workgroup's 38 KB: 4 workgroups per CU);
 // without, they go straight to the striped global copies and the probe fits 6 workgroups per CU.
-#ifndef MISLO_PROBE_DEPTH
-#define MISLO_PROBE_DEPTH 1
-#endif
-#ifndef MISLO_PROBE_MINWG
-#define MISLO_PROBE_MINWG 4
-#endif
 template <int NT, bool LG>
-__global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const PreSpan* __restrict__ pre,
+__global__ __launch_bounds__(NT, LG ? 4 : 6) void k_probe(const PreSpan* __restrict__ pre,
                                               const uint32_t* __restrict__ span_base, SignalCols gc, int span_cap,
                                               JoinParams jp, unsigned long long* __restrict__ top3,
                                               uint32_t* __restrict__ cnt, int n_groups,
@@ -605,11 +620,10 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
     __syncthreads();  // previous item's LDS reads are done before s_item / staging reuse
     if (threadIdx.x == 0) s_item = atomicAdd(&work[2 + phase], 1u);
     __syncthreads();
-    // wave-uniform from here: the item's fields, list bounds and pointers live in SGPRs
-    const uint32_t it = __builtin_amdgcn_readfirstlane(s_item);
+    const uint32_t it = s_item;
     if (it >= n_work) break;
 #ifdef MISLO_PROBE_PROFILE
-    unsigned long long pt = clock64(), p_stage = 0, p_sig = 0, p_flush = 0, p_s1 = 0, p_s2 = 0;
+    unsigned long long pt = clock64(), p_stage = 0, p_sig = 0, p_flush = 0;
 #endif
     const uint32_t code = items[it];
     const int k = (int)(code >> 30);
@@ -623,7 +637,7 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
     // GPUs' rows oldest first: the order of [rows | halo | remote] under nested halo selections)
     const uint32_t gslot = age_slot(gc, cur, age);
     const uint32_t* sig_base = gc.base + (size_t)gslot * kBaseLen;
-    const uint4* sig_hot = reinterpret_cast<const uint4*>(gc.items + (size_t)gslot * kKeyTypes * (size_t)gc.stride);
+    const uint32_t* sig_items = gc.items + (size_t)gslot * kKeyTypes * (size_t)gc.stride;
     const KeyTs* sig_keys = gc.keys + (size_t)gslot * kKeyTypes * (size_t)gc.stride;
     const SigRec* grec = gc.rec + (size_t)gslot * (size_t)gc.stride;
     const int64_t cut = gc.gen ? gc.gen->cut[age] : INT64_MIN;
@@ -706,27 +720,24 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
     { const unsigned long long t = clock64(); p_stage += t - pt; pt = t; }
 #endif
 
-    // The item's list entries -- (key hash, ts) and the HotSig (row index + the fields the
-    // accounting reads), 48 coalesced bytes per lane; 16 for the broad tier, which counts from the
-    // keys alone -- stream kDepth iterations ahead: no row record is gathered on the common path.
-    // A signal's span-run search runs one iteration ahead of its accounting.
-    constexpr int kDepth = MISLO_PROBE_DEPTH;
+    // The item's list entries -- (key hash, ts) and the row index, 20 coalesced bytes per lane --
+    // stream kDepth iterations ahead. A signal's 48-byte row record (a random gather) is needed
+    // only when its key run holds a span within the tier's window: the broad tier counts from
+    // the keys alone, older generations' rows outside the halo and rows with no span in reach
+    // cost no gather. A matching signal's search and gather are issued one iteration ahead of
+    // its accounting, so the gather overlaps the previous signal's LDS work.
+    constexpr int kDepth = 1;
     uint32_t q = sg0 + threadIdx.x;
     KeyTs kq[kDepth];
-    uint4 ha[kDepth], hb[kDepth];
-    auto load_entry = [&](uint32_t at, bool ok, KeyTs& e, uint4& a, uint4& b) {
-      e = ok ? sig_keys[at] : KeyTs{0ull, INT64_MIN};
-      if (ok && !count_only) {
-        a = sig_hot[2 * (size_t)at];
-        b = sig_hot[2 * (size_t)at + 1];
-      } else {
-        a = b = make_uint4(0u, 0u, 0u, 0u);
-      }
-    };
+    uint32_t iq[kDepth];
 #pragma unroll
-    for (int d = 0; d < kDepth; ++d) load_entry(q + (d + 1) * NT, q + (d + 1) * NT < sg1, kq[d], ha[d], hb[d]);
-    // stage 1 of an element: halo visibility, the span-run search, whether the run holds a span in reach
-    auto stage1 = [&](const KeyTs& e, bool valid, int& lo, bool& vis, bool& hit) {
+    for (int d = 0; d < kDepth; ++d) {
+      const bool ok = q + (d + 1) * NT < sg1;
+      kq[d] = ok ? sig_keys[q + (d + 1) * NT] : KeyTs{0ull, INT64_MIN};
+      iq[d] = ok ? sig_items[q + (d + 1) * NT] : 0u;
+    }
+    // stage 1 of an element: halo visibility, the span-run search, the record gather on a hit
+    auto stage1 = [&](const KeyTs& e, uint32_t idx, bool valid, int& lo, bool& vis, bool& hit, SigHot& r) {
       vis = valid && e.t >= cut;
       hit = false;
       lo = 0;
@@ -734,33 +745,31 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
       lo = lower_ht(s_kt, 0, m, e.h, e.t - w);
       if (count_only) return;
       hit = lo < m && s_kt[lo].h == e.h && s_kt[lo].t <= e.t + w;
+      if (hit) r = load_hot(grec + idx);
     };
-    KeyTs e0;
-    uint4 a0, b0;
-    load_entry(q, q < sg1, e0, a0, b0);
+    KeyTs e0 = q < sg1 ? sig_keys[q] : KeyTs{0ull, INT64_MIN};
+    uint32_t i0 = q < sg1 ? sig_items[q] : 0u;
     int lo0;
     bool vis0, hit0;
-    stage1(e0, q < sg1, lo0, vis0, hit0);
+    SigHot r0{};
+    stage1(e0, i0, q < sg1, lo0, vis0, hit0, r0);
     for (; q < sg1; q += NT) {
-#ifdef MISLO_PROBE_PROFILE
-      const unsigned long long q0 = clock64();
-#endif
       const KeyTs e1 = kq[0];
-      const uint4 a1 = ha[0], b1h = hb[0];
+      const uint32_t i1 = iq[0];
 #pragma unroll
       for (int d = 0; d + 1 < kDepth; ++d) {
         kq[d] = kq[d + 1];
-        ha[d] = ha[d + 1];
-        hb[d] = hb[d + 1];
+        iq[d] = iq[d + 1];
       }
-      load_entry(q + (kDepth + 1) * NT, q + (kDepth + 1) * NT < sg1, kq[kDepth - 1], ha[kDepth - 1], hb[kDepth - 1]);
+      {
+        const bool ok = q + (kDepth + 1) * NT < sg1;
+        kq[kDepth - 1] = ok ? sig_keys[q + (kDepth + 1) * NT] : KeyTs{0ull, INT64_MIN};
+        iq[kDepth - 1] = ok ? sig_items[q + (kDepth + 1) * NT] : 0u;
+      }
       int lo1;
       bool vis1, hit1;
-      stage1(e1, q + NT < sg1, lo1, vis1, hit1);
-#ifdef MISLO_PROBE_PROFILE
-      const unsigned long long q1 = clock64();
-      p_s1 += q1 - q0;
-#endif
+      SigHot r1{};
+      stage1(e1, i1, q + NT < sg1, lo1, vis1, hit1, r1);
       // stage 2: this element's accounting
       do {
       if (!vis0) break;
@@ -772,17 +781,13 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
         n_low += (unsigned long long)(upper_ht(s_kt, lo, m, h, thi) - lo);
         break;
       }
-      if (!hit0) break;  // (a hit has lo < m and s_kt[lo] in the signal's hash run)
-      const uint32_t row = b0.z;
-      const uint32_t g = (row < n_loc ? cls_loc : cls_rem) + row;  // top-3 key row id
-      const uint32_t g_pod = a0.z, g_pid = a0.w, g_sn = b0.x;
-      const uint64_t g_cn = ((uint64_t)a0.y << 32) | a0.x;
-      const int g_slot = (int)b0.w;
-      const unsigned long long g_milli = milli_units(__uint_as_float(b0.y));
-      // the trace hash, off the common path: a trace-tier signal's is its run's (key_hash is a
-      // bijection of the trace id but for the key it maps to 1); the pod / service tiers read it
-      // from the row record on their rare needy-span and exact-walk paths
-      auto row_trace = [&]() -> uint64_t { return grec[row].tr; };
+      if (!hit0) break;
+      const SigHot r = r0;
+      const uint32_t g = (i0 < n_loc ? cls_loc : cls_rem) + i0;  // top-3 key row id
+      const uint32_t g_pod = r.pod, g_pid = r.pid, g_sn = r.sn;
+      const uint64_t g_tr = r.tr, g_cn = r.cn;
+      const int g_slot = (int)r.slot;
+      const unsigned long long g_milli = milli_units(r.val);
       const bool g_sn_ok = (g_sn >> 16) != 0 && (g_sn & 0xFFFF) != 0;
 
       // ---- range accounting (pod tiers, uniform hash run) ----------------------------
@@ -811,7 +816,6 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
             if (track_overlap && g_sn_ok && p0.sn == g_sn && w <= jp.win_ns[3]) n_overlap += (unsigned long long)n_acc;
             // top-3 keys only for needy spans in the accepted ranges
             if (n_needy) {
-              const uint64_t g_tr = row_trace();
               for (int part = 0; part < 2; ++part) {
                 const int ra = part ? b1 : lo, rb = part ? hi : a1;
                 for (int j = lower_u16(s_needy, n_needy, ra); j < n_needy && (int)s_needy[j] < rb; ++j) {
@@ -838,7 +842,6 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
       }
 
       // ---- exact per-pair walk (trace tier, colliding / mixed runs, low threshold) ---
-      const uint64_t g_tr = (k == 0 && h != 1ull) ? s_tc[lo].tr : row_trace();
       uint32_t run_grp = 0xFFFFFFFFu, run_n = 0;
       for (int i = lo; i < m; ++i) {
         const SpanKT e = s_kt[i];
@@ -914,15 +917,12 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
       }
       add_group(run_grp, g_slot, g_milli, run_n);
       } while (0);
-#ifdef MISLO_PROBE_PROFILE
-      p_s2 += clock64() - q1;
-#endif
       e0 = e1;
-      a0 = a1;
-      b0 = b1h;
+      i0 = i1;
       lo0 = lo1;
       vis0 = vis1;
       hit0 = hit1;
+      r0 = r1;
     }
     // flush this chunk's per-span candidates to the global top-3 / counts
     __syncthreads();
@@ -967,8 +967,6 @@ __global__ __launch_bounds__(NT, LG ? MISLO_PROBE_MINWG : 6) void k_probe(const 
     atomicAdd(pr + 3, p_stage);
     atomicAdd(pr + 4, p_sig);
     atomicAdd(pr + 5, p_flush);
-    atomicAdd(pr + 6, p_s1);  // signal loop: next entry's wait + span-run search
-    atomicAdd(pr + 7, p_s2);  // signal loop: this entry's accounting
   }
 #endif
   }  // work loop

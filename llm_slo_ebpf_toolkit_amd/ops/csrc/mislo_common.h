@@ -162,21 +162,6 @@ struct alignas(16) KeyTs {
   uint64_t h;
   int64_t t;
 };
-// The row fields a probe visit reads, written next to the list key by the signal scatter, so the
-// probe streams them with the keys (two coalesced 16-byte loads per entry) instead of gathering
-// the row's 64-byte record from a random line: the first 16 bytes are the SigRec's cn | pod | pid,
-// the second its sn | val | the row index | slot. The trace hash is not carried: a trace-tier
-// entry's is its key's (key_hash is a bijection of the trace id but for the one key it maps to 1),
-// and the other tiers need it only on their rare exact-walk / needy-span paths, which gather it.
-struct alignas(16) HotSig {
-  uint64_t cn;
-  uint32_t pod, pid;
-  uint32_t sn;
-  uint32_t val;  // float bits
-  uint32_t row;  // row index in the generation
-  uint32_t slot;
-};
-static_assert(sizeof(HotSig) == 32, "HotSig is two 16-byte loads");
 
 // Resident signal generations (the halo). The engine keeps the decoded rows, partition lists and
 // list keys of the last kMaxGens windows in place: window k joins the rows of windows k-1.. that
@@ -203,7 +188,7 @@ struct SignalCols {
   SigRec* rec;          // [gens][stride] row records
   uint8_t* status;      // this window's rows: 0 ok, 1 warning, 2 error
   PartCodes* part;      // this window's rows
-  HotSig* items = nullptr;    // [gens][kKeyTypes * stride] partition lists (row index + the probe's fields)
+  uint32_t* items = nullptr;  // [gens][kKeyTypes * stride] partition lists (row indices)
   KeyTs* keys = nullptr;      // [gens][kKeyTypes * stride] the lists' (key hash, ts)
   uint32_t* base = nullptr;   // [gens][kKeyTypes * kParts + 1] list offsets
   GenMeta* gen = nullptr;     // nullptr: one generation (slot 0)

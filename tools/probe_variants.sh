@@ -19,7 +19,13 @@ case "$cmd" in
     cp -r "$ROOT/config" "$V/"
     cp "$ROOT/tests/fixtures/ref_multi_fault_samples.jsonl" "$V/tests/fixtures/"
     (cd "$ROOT" && tar --exclude='__pycache__' --exclude='_build' -cf - llm_slo_ebpf_toolkit_amd) | (cd "$V" && tar -xf -)
-    (cd "$V" && MISLO_HIP_DEFINES="$defines" python3 -m llm_slo_ebpf_toolkit_amd.ops.build --only agent --force)
+    if [ -n "${CSRC_REV:-}" ]; then  # the kernels of another commit (A/B against an earlier tree)
+      for f in $(cd "$ROOT" && git ls-tree --name-only "$CSRC_REV" llm_slo_ebpf_toolkit_amd/ops/csrc/); do
+        (cd "$ROOT" && git show "$CSRC_REV:$f") > "$V/$f"
+      done
+      defines="$defines (csrc from $CSRC_REV)"
+    fi
+    (cd "$V" && MISLO_HIP_DEFINES="${defines%% (csrc*}" python3 -m llm_slo_ebpf_toolkit_amd.ops.build --only agent --force)
     rm -rf "$V/llm_slo_ebpf_toolkit_amd/_build"
     echo "$defines" > "$V/DEFINES" ;;
   bench)
