@@ -91,3 +91,19 @@ def http_recorder():
     yield make
     for r in made:
         r.close()
+
+
+# the agent CLI sets these for the HIP runtime it is about to start (cli/agent.py parse): a test
+# that parses agent flags must not leave them to the tests after it in this process
+_RUNTIME_ENV = ("GPU_MAX_HW_QUEUES", "MISLO_ONE_STREAM", "HSA_ENABLE_SDMA")
+
+
+@pytest.fixture(autouse=True)
+def _restore_runtime_env():
+    saved = {k: os.environ.get(k) for k in _RUNTIME_ENV}
+    yield
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v

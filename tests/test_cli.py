@@ -193,6 +193,8 @@ def test_agent_metrics_export_gpu_signal_histograms():
 def test_agent_gpu_hw_queues_flag_wins_over_env_default_does_not(monkeypatch):
     from llm_slo_ebpf_toolkit_amd.cli import agent as agent_cli
 
+    for k in ("MISLO_ONE_STREAM", "HSA_ENABLE_SDMA"):
+        monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")  # a node-wide setting
     agent_cli.parse(["--engine", "gpu"])
     assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
@@ -202,8 +204,26 @@ def test_agent_gpu_hw_queues_flag_wins_over_env_default_does_not(monkeypatch):
     agent_cli.parse(["-gpu-hw-queues=2"])
     assert os.environ["GPU_MAX_HW_QUEUES"] == "2"
     monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    monkeypatch.delenv("MISLO_ONE_STREAM", raising=False)
+    monkeypatch.delenv("HSA_ENABLE_SDMA", raising=False)
     agent_cli.parse([])
     assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    # one hardware queue: one HIP stream and blit-kernel copies (no SDMA queue save area)
+    assert os.environ["MISLO_ONE_STREAM"] == "1" and os.environ["HSA_ENABLE_SDMA"] == "0"
+
+
+def test_agent_keeps_two_streams_and_sdma_with_more_hardware_queues(monkeypatch):
+    from llm_slo_ebpf_toolkit_amd.cli import agent as agent_cli
+
+    for k in ("GPU_MAX_HW_QUEUES", "MISLO_ONE_STREAM", "HSA_ENABLE_SDMA"):
+        monkeypatch.delenv(k, raising=False)
+    agent_cli.parse(["--gpu-hw-queues", "4"])
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    assert "MISLO_ONE_STREAM" not in os.environ and "HSA_ENABLE_SDMA" not in os.environ
+    monkeypatch.setenv("HSA_ENABLE_SDMA", "1")  # an operator's explicit setting wins
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES")
+    agent_cli.parse([])
+    assert os.environ["HSA_ENABLE_SDMA"] == "1"
 
 
 # REF's flag surface per binary (cmd/agent/main.go:334-373, cmd/collector/main.go:25-41,
