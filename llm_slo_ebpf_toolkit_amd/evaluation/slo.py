@@ -8,8 +8,9 @@ negative values clamped to 0 before aggregation, TTFT truncated to whole ms like
 from __future__ import annotations
 
 import math
+from collections import deque
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import Deque, List, Optional, Sequence, Tuple
 
 from ..utils.timeutil import MS, SECOND
 
@@ -161,40 +162,69 @@ class BurnRateForecaster:
         self.budget = 1.0 - target
         self.horizon, self.short, self.floor = int(horizon), int(short), float(floor)
         self.min_requests = float(min_requests)
-        self._hist: dict = {}     # key -> list of (n, breach) per window
-        self._pending: dict = {}  # key -> list of (window index, forecast)
-        self.scored: List[float] = []
+        # per key: prefix sums of requests / breaches over the kept windows ([0] = 0; window i of
+        # the kept history is cum[i + 1] - cum[i]): every trailing or forecast-horizon sum is one
+        # subtraction (the agent observes every incident group every window)
+        self._cum: dict = {}      # key -> [cum_n list, cum_b list]
+        self._pending: dict = {}  # key -> deque of (window index, forecast)
+        self.scored: Deque[float] = deque(maxlen=10000)  # the latest scored errors (checkpoint state)
+        self._err_sum, self._err_n = 0.0, 0                 # every scored error (error())
 
     def burn(self, n: float, breach: float) -> float:
         return (breach / n) / self.budget if n > 0 else 0.0
 
+    def _trailing(self, cn: List[float], cb: List[float], windows: int, min_requests: float) -> float:
+        """Burn over the shortest trailing run of at most ``windows`` windows holding at least
+        ``min_requests`` requests (all of them if fewer)."""
+        t = len(cn) - 1  # windows kept
+        jmax = min(int(windows), t)
+        if jmax <= 0:
+            return 0.0
+        if cn[t] - cn[t - jmax] < min_requests:
+            j = jmax
+        else:  # the smallest j with the last j windows' requests >= min_requests
+            lo, hi = 1, jmax
+            while lo < hi:
+                mid = (lo + hi) >> 1
+                if cn[t] - cn[t - mid] >= min_requests:
+                    hi = mid
+                else:
+                    lo = mid + 1
+            j = lo
+        return self.burn(cn[t] - cn[t - j], cb[t] - cb[t - j])
+
     def observe(self, key, n: float, breach: float, forecast: bool = True) -> float:
         """Adds one window's request and breach counts; returns the forecast made at it (and
         keeps it for scoring unless ``forecast`` is False)."""
-        h = self._hist.setdefault(key, [])
-        h.append((float(n), float(breach)))
-        t = len(h) - 1
-        pend = self._pending.setdefault(key, [])
+        c = self._cum.get(key)
+        if c is None:
+            c = self._cum[key] = [[0.0], [0.0]]
+        cn, cb = c
+        cn.append(cn[-1] + float(n))
+        cb.append(cb[-1] + float(breach))
+        t = len(cn) - 2  # this window's index in the kept history
+        pend = self._pending.get(key)
+        if pend is None:
+            pend = self._pending[key] = deque()
         while pend and pend[0][0] + self.horizon <= t:  # matured: windows (t0, t0 + horizon]
-            t0, f = pend.pop(0)
-            seg = h[t0 + 1:t0 + 1 + self.horizon]
-            real = self.burn(sum(x[0] for x in seg), sum(x[1] for x in seg))
-            self.scored.append(abs(f - real) / max(real, self.floor))
-        n_acc = b_acc = 0.0
-        for x in reversed(h[-self.short:]):
-            n_acc += x[0]
-            b_acc += x[1]
-            if n_acc >= self.min_requests:
-                break
-        f = self.burn(n_acc, b_acc)
+            t0, f = pend.popleft()
+            a, b = t0 + 1, t0 + 1 + self.horizon
+            real = self.burn(cn[b] - cn[a], cb[b] - cb[a])
+            err = abs(f - real) / max(real, self.floor)
+            self.scored.append(err)
+            self._err_sum += err
+            self._err_n += 1
+        f = self._trailing(cn, cb, self.short, self.min_requests)
         if forecast:
             pend.append((t, f))
         # keep what the short window and the oldest pending forecast still need
         keep = max(self.short, t - pend[0][0] + 1 if pend else 0)
-        if len(h) > 4 * keep + 64:
-            drop = len(h) - keep
-            del h[:drop]
-            self._pending[key] = [(t0 - drop, f0) for t0, f0 in pend]
+        if len(cn) - 1 > 4 * keep + 64:
+            drop = len(cn) - 1 - keep
+            base_n, base_b = cn[drop], cb[drop]
+            c[0] = [x - base_n for x in cn[drop:]]
+            c[1] = [x - base_b for x in cb[drop:]]
+            self._pending[key] = deque((t0 - drop, f0) for t0, f0 in pend)
         return f
 
     def current(self, key, windows: int = 3, min_requests: float = 20.0) -> float:
@@ -202,31 +232,49 @@ class BurnRateForecaster:
         least ``min_requests`` requests (all of them if fewer). The agent's emission gate -- a
         fast-burn alert: the forecast (``observe``) keeps a fault's breaches for up to ``short``
         windows after the service recovered, which would page "unknown" through the recovery."""
-        n_acc = b_acc = 0.0
-        for x in reversed(self._hist.get(key, [])[-int(windows):]):
-            n_acc += x[0]
-            b_acc += x[1]
-            if n_acc >= min_requests:
-                break
-        return self.burn(n_acc, b_acc)
+        c = self._cum.get(key)
+        return self._trailing(c[0], c[1], windows, min_requests) if c is not None else 0.0
 
     def alert(self, key) -> float:
-        recent = self._hist.get(key, [])[-self.short:]
-        return self.burn(sum(x[0] for x in recent), sum(x[1] for x in recent))
+        c = self._cum.get(key)
+        if c is None:
+            return 0.0
+        cn, cb = c
+        j = min(self.short, len(cn) - 1)
+        return self.burn(cn[-1] - cn[-1 - j], cb[-1] - cb[-1 - j])
 
     def error(self) -> Optional[float]:
-        return float(sum(self.scored) / len(self.scored)) if self.scored else None
+        return float(self._err_sum / self._err_n) if self._err_n else None
+
+    def history(self, key) -> List[Tuple[float, float]]:
+        """The kept per-window (requests, breaches) of ``key``."""
+        c = self._cum.get(key)
+        if c is None:
+            return []
+        cn, cb = c
+        return [(cn[i + 1] - cn[i], cb[i + 1] - cb[i]) for i in range(len(cn) - 1)]
 
     def state(self) -> dict:
         """JSON-able state (agent checkpoint): per-key window history and pending forecasts."""
-        return {"hist": {str(k): v for k, v in self._hist.items()},
-                "pending": {str(k): v for k, v in self._pending.items()},
-                "scored": self.scored[-10000:]}
+        return {"hist": {str(k): self.history(k) for k in self._cum},
+                "pending": {str(k): list(v) for k, v in self._pending.items()},
+                "scored": list(self.scored), "err": [self._err_sum, self._err_n]}
 
     def restore(self, st: dict) -> None:
-        self._hist = {k: [tuple(x) for x in v] for k, v in (st.get("hist") or {}).items()}
-        self._pending = {k: [tuple(x) for x in v] for k, v in (st.get("pending") or {}).items()}
-        self.scored = [float(x) for x in st.get("scored") or []]
+        self._cum = {}
+        for k, v in (st.get("hist") or {}).items():
+            cn, cb = [0.0], [0.0]
+            for n, b in v:
+                cn.append(cn[-1] + float(n))
+                cb.append(cb[-1] + float(b))
+            self._cum[k] = [cn, cb]
+        self._pending = {k: deque(tuple(x) for x in v) for k, v in (st.get("pending") or {}).items()}
+        self.scored = deque((float(x) for x in st.get("scored") or []), maxlen=10000)
+        err = st.get("err")
+        if err:
+            self._err_sum, self._err_n = float(err[0]), int(err[1])
+        else:
+            self._err_sum, self._err_n = float(sum(self.scored)), len(self.scored)
 
 
 def simulate_burn_prediction_error(burn_rates: Sequence[float], target: float = 0.99, horizon: int = 300,

@@ -126,7 +126,8 @@ def test_burn_rate_forecaster_bounded_history():
     fc = slo.BurnRateForecaster(target=0.99, horizon=5, short=3, min_requests=10)
     for _ in range(2000):
         fc.observe("k", 10, 0, forecast=False)
-    assert len(fc._hist["k"]) < 100
+    assert len(fc.history("k")) < 100
+    assert fc.history("k")[-1] == (10.0, 0.0)
 
 
 def test_simulated_burn_prediction_error_is_measured():
@@ -224,3 +225,20 @@ def test_emission_gate_burn_is_over_the_last_windows_holding_enough_requests():
         fc.observe("busy", n, b)
     assert fc.current("busy", windows=3, min_requests=8) == 0.0
     assert fc.current("busy", windows=3, min_requests=20) == pytest.approx((4 / 12) / 0.01)
+
+
+def test_burn_rate_forecaster_state_round_trips_and_scores_stay_bounded():
+    fc = slo.BurnRateForecaster(target=0.99, horizon=4, short=3, min_requests=5)
+    for i in range(40):
+        fc.observe("a", 10, i % 3)
+    st = fc.state()
+    fc2 = slo.BurnRateForecaster(target=0.99, horizon=4, short=3, min_requests=5)
+    fc2.restore(st)
+    assert fc2.history("a") == fc.history("a") and fc2.error() == pytest.approx(fc.error())
+    assert fc2.observe("a", 10, 1) == pytest.approx(fc.observe("a", 10, 1))
+    assert fc2.current("a", windows=3, min_requests=8) == pytest.approx(fc.current("a", windows=3, min_requests=8))
+    assert fc2.alert("a") == pytest.approx(fc.alert("a"))
+    big = slo.BurnRateForecaster(target=0.99, horizon=2, short=2, min_requests=1)
+    for _ in range(20000):
+        big.observe("k", 10, 1)
+    assert len(big.scored) <= 10000 and big.error() == pytest.approx(0.0)
