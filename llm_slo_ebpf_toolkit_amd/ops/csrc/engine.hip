@@ -481,19 +481,23 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   const bool branched = branch_ && !xchg;
   // with the span branch: the signal bases are what the branch's probe work list waits for
   hipEvent_t sig_base = branched ? ev_sigbase_ : nullptr;
+  // without the span branch: the span side first, so the signal scatter's launch can build the
+  // probe's work list next to it (it needs both sides' list offsets)
+  if (!branched) run_spans(b, st);
+  const uint32_t* wspan = branched ? nullptr : s_part_base_;
+  const JoinParams* wjp = branched ? nullptr : &jp_;
+  uint32_t* wlist = branched ? nullptr : probe_work_;
   if (xchg)
     launch_partition_sig(sig_cols(), rows_, N, nblk_sig_ + nblk_imp_, g_part_blk_, g_part_off_, g_part_tot_, st,
-                         nblk_sig_, sig_base);
+                         nblk_sig_, sig_base, wspan, wjp, wlist);
   else
-    launch_partition_sig(sig_cols(), rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, st, 0, sig_base);
+    launch_partition_sig(sig_cols(), rows_, N, nblk_sig_, g_part_blk_, g_part_off_, g_part_tot_, st, 0, sig_base,
+                         wspan, wjp, wlist);
   if (branched) {  // the work list needs the signal bases just recorded; then join
     HIPCHECK(hipStreamWaitEvent(side_, ev_sigbase_, 0));
     launch_probe_work(s_part_base_, sig_cols(), jp_, probe_work_, side_);
     HIPCHECK(hipEventRecord(ev_spans_, side_));
     HIPCHECK(hipStreamWaitEvent(st, ev_spans_, 0));  // spans sorted, work list built
-  } else {
-    run_spans(b, st);
-    launch_probe_work(s_part_base_, sig_cols(), jp_, probe_work_, st);
   }
   launch_probe(span_cols(), s_items_, s_part_base_, sig_cols(), S, jp_, top3_, cnt_, n_groups, gsum_, gcnt_, dbg_,
                probe_work_, s_pre_, st);

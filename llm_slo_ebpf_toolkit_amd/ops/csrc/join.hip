@@ -150,29 +150,30 @@ __global__ __launch_bounds__(NT) void k_scatter(const PartCodes* __restrict__ co
 // row's (key hash, ts) for the list's key type, written once and streamed by the probe of this
 // window and of the later windows the rows stay in the halo for. The hashes are recomputed from
 // the row records (the decode kept only their partitions); the rows are read in order.
+// (body: block `bid` of `nblk` scatter blocks; `s_pos` = kKeyTypes * kParts words of LDS)
 template <int NT>
-__global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __restrict__ n_ptr, int cap,
-                                                    const uint32_t* __restrict__ part_off, int nblk_a) {
+__device__ __forceinline__ void scatter_sig_body(const SignalCols& gc, const int* __restrict__ n_ptr, int cap,
+                                                 const uint32_t* __restrict__ part_off, int nblk_a, int bid,
+                                                 int nblk, uint32_t* s_pos) {
   const uint32_t cur = cur_slot(gc);
   const SigRec* rec = gc.rec + (size_t)cur * (size_t)gc.stride;
   const uint32_t* base = gc.base + (size_t)cur * kBaseLen;
   uint32_t* items = gc.items + (size_t)cur * kKeyTypes * (size_t)gc.stride;
   KeyTs* keys = gc.keys + (size_t)cur * kKeyTypes * (size_t)gc.stride;
   // next slot per list (see k_scatter)
-  __shared__ uint32_t s_pos[kKeyTypes * kParts];
   {
-    const uint32_t* my_off = part_off + (size_t)blockIdx.x * kKeyTypes * kParts;
+    const uint32_t* my_off = part_off + (size_t)bid * kKeyTypes * kParts;
     for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_pos[i] = base[i] + my_off[i];
   }
   __syncthreads();
   // the row ranges of the decode blocks (see k_scatter)
   const int n0 = min(n_ptr[0], cap);
-  const bool two = nblk_a < (int)gridDim.x;
-  const bool second = two && (int)blockIdx.x >= nblk_a;
+  const bool two = nblk_a < nblk;
+  const bool second = two && bid >= nblk_a;
   const int s_beg = second ? n0 : 0;
   const int s_end = second ? max(n0, min(n_ptr[1], cap)) : n0;
-  const int g = two ? (second ? (int)gridDim.x - nblk_a : nblk_a) : (int)gridDim.x;
-  const int bi = second ? (int)blockIdx.x - nblk_a : (int)blockIdx.x;
+  const int g = two ? (second ? nblk - nblk_a : nblk_a) : nblk;
+  const int bi = second ? bid - nblk_a : bid;
   const int chunk = (s_end - s_beg + g - 1) / g;
   const int beg = s_beg + bi * chunk, end = min(s_end, beg + chunk);
   // kU rows per thread per trip, every load of the trip issued before the first is used: the
@@ -210,6 +211,13 @@ __global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __
       }
     }
   }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scatter_sig(SignalCols gc, const int* __restrict__ n_ptr, int cap,
+                                                    const uint32_t* __restrict__ part_off, int nblk_a) {
+  __shared__ uint32_t s_pos[kKeyTypes * kParts];
+  scatter_sig_body<NT>(gc, n_ptr, cap, part_off, nblk_a, (int)blockIdx.x, (int)gridDim.x, s_pos);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -316,10 +324,10 @@ __device__ __forceinline__ uint32_t probe_item_class(int k, uint32_t n_sig, uint
   return min(cost >> 13, 63u);
 }
 
-__global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restrict__ span_base, SignalCols gc,
-                                                       JoinParams jp, int sig_per_item, uint32_t* __restrict__ work) {
-  __shared__ unsigned long long s[kParts], s2[kParts];
-  __shared__ uint32_t s_cls[64];
+// (body: one workgroup of kParts threads; s / s2 = kParts words each, s_cls = 64 words of LDS)
+__device__ __forceinline__ void probe_work_body(const uint32_t* __restrict__ span_base, const SignalCols& gc,
+                                                const JoinParams& jp, int sig_per_item, uint32_t* __restrict__ work,
+                                                unsigned long long* s, unsigned long long* s2, uint32_t* s_cls) {
   const int p = threadIdx.x;
   if (p < 64) s_cls[p] = 0u;
   const uint32_t cur = cur_slot(gc);
@@ -412,6 +420,34 @@ __global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restric
     work[2] = 0u;
     work[3] = 0u;
   }
+}
+
+__global__ __launch_bounds__(kParts) void k_probe_work(const uint32_t* __restrict__ span_base, SignalCols gc,
+                                                       JoinParams jp, int sig_per_item, uint32_t* __restrict__ work) {
+  __shared__ unsigned long long s[kParts], s2[kParts];
+  __shared__ uint32_t s_cls[64];
+  probe_work_body(span_base, gc, jp, sig_per_item, work, s, s2, s_cls);
+}
+
+// The signal scatter with the probe's work list built by one more workgroup of the same launch
+// (block 0, dispatched first): the list needs only the span and signal list offsets, so it no
+// longer runs alone between the scatter and the probe (~26 us of one CU, serial, per window).
+// LDS is one buffer, used as either kernel's arrays.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scatter_sig_work(SignalCols gc, const int* __restrict__ n_ptr, int cap,
+                                                         const uint32_t* __restrict__ part_off, int nblk_a,
+                                                         const uint32_t* __restrict__ span_base, JoinParams jp,
+                                                         int sig_per_item, uint32_t* __restrict__ work) {
+  static_assert(NT == kParts, "the work-list block runs one thread per partition");
+  static_assert(2 * kParts * 8 + 64 * 4 >= kKeyTypes * kParts * 4, "one LDS buffer serves both");
+  __shared__ unsigned long long s_buf[2 * kParts + 32];
+  if (blockIdx.x == 0) {
+    probe_work_body(span_base, gc, jp, sig_per_item, work, s_buf, s_buf + kParts,
+                    reinterpret_cast<uint32_t*>(s_buf + 2 * kParts));
+    return;
+  }
+  scatter_sig_body<NT>(gc, n_ptr, cap, part_off, nblk_a, (int)blockIdx.x - 1, (int)gridDim.x - 1,
+                       reinterpret_cast<uint32_t*>(s_buf));
 }
 
 // In-place inclusive scan of v[0..n), n <= 2 * NT (each thread owns two adjacent entries).
@@ -1113,14 +1149,28 @@ __global__ __launch_bounds__(256) void k_group_features(int n, const unsigned lo
 // host launchers
 // ---------------------------------------------------------------------------------------
 
+static int probe_item_signals() {  // MISLO_PROBE_ITEM: signals per work item (diagnostic)
+  static const int per_item = [] {
+    const char* v = getenv("MISLO_PROBE_ITEM");
+    const int x = v ? atoi(v) : kSigPerItem;
+    return x >= 1 ? x : kSigPerItem;
+  }();
+  return per_item;
+}
+
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
-                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a, hipEvent_t bases_done) {
+                          uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a, hipEvent_t bases_done,
+                          const uint32_t* work_span_base, const JoinParams* work_jp, uint32_t* work) {
   hipLaunchKernelGGL(k_part_scan, dim3(kKeyTypes * kParts / kScanCols), dim3(kScanCols * kScanRG), 0, stream,
                      part_blk, nblk, part_off, part_tot);
   hipLaunchKernelGGL(k_base_scan, dim3(1), dim3(kBaseNT), 0, stream, part_tot, gc.base, gc.gen);
   if (bases_done) (void)hipEventRecord(bases_done, stream);  // the span branch's probe work list may start
-  hipLaunchKernelGGL((k_scatter_sig<1024>), dim3(nblk), dim3(1024), 0, stream, gc, n_dev, cap, part_off,
-                     nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk);
+  const int na = nblk_a > 0 && nblk_a < nblk ? nblk_a : nblk;
+  if (work != nullptr && work_jp != nullptr && work_span_base != nullptr)  // + the probe's work list
+    hipLaunchKernelGGL((k_scatter_sig_work<1024>), dim3(nblk + 1), dim3(1024), 0, stream, gc, n_dev, cap, part_off,
+                       na, work_span_base, *work_jp, probe_item_signals(), work);
+  else
+    hipLaunchKernelGGL((k_scatter_sig<1024>), dim3(nblk), dim3(1024), 0, stream, gc, n_dev, cap, part_off, na);
 }
 
 void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
@@ -1176,12 +1226,7 @@ void launch_span_sort(const SpanCols& sc, const uint32_t* span_items, const uint
 
 void launch_probe_work(const uint32_t* span_base, const SignalCols& gc, const JoinParams& jp, uint32_t* work,
                        hipStream_t stream) {
-  static const int per_item = [] {  // MISLO_PROBE_ITEM: signals per work item (diagnostic)
-    const char* v = getenv("MISLO_PROBE_ITEM");
-    const int x = v ? atoi(v) : kSigPerItem;
-    return x >= 1 ? x : kSigPerItem;
-  }();
-  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, per_item, work);
+  hipLaunchKernelGGL(k_probe_work, dim3(1), dim3(kParts), 0, stream, span_base, gc, jp, probe_item_signals(), work);
 }
 
 void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* top3, const uint32_t* cnt,

@@ -105,10 +105,14 @@ void launch_partition(const PartCodes* codes, const int* n_dev, int cap, int nbl
                       uint32_t* part_off, uint32_t* part_tot, uint32_t* part_base, uint32_t* items,
                       hipStream_t stream, int nblk_a = 0);
 // signals: the current generation's lists (gc.items / gc.keys / gc.base) from gc.part and gc.rec
-// (bases_done: recorded after the partition bases, before the scatter -- the span branch's cue)
+// (bases_done: recorded after the partition bases, before the scatter -- the span branch's cue;
+// work_*: the spans' list offsets, the join parameters and the probe's work list -- given, the
+// scatter's launch also builds the work list (one extra workgroup), the spans' lists must exist)
+struct JoinParams;
 void launch_partition_sig(const SignalCols& gc, const int* n_dev, int cap, int nblk, const uint32_t* part_blk,
                           uint32_t* part_off, uint32_t* part_tot, hipStream_t stream, int nblk_a = 0,
-                          hipEvent_t bases_done = nullptr);
+                          hipEvent_t bases_done = nullptr, const uint32_t* work_span_base = nullptr,
+                          const JoinParams* work_jp = nullptr, uint32_t* work = nullptr);
 // A span at its position in a (key type, partition) list, the list sorted by (key hash, ts) in
 // chunks of the probe's staging size: what the probe stages, written once per window
 // (k_span_sort). run = the position's hash-run id in its chunk | run uniform << 16.
