@@ -165,19 +165,22 @@ void WindowEngine::alloc() {
     else copy2_ = copy_;
   }
   {
+    // The span side of the chain (decode, partition, sort, the probe's work list) on a second
+    // stream, overlapping the signal side's decode: on by default where the streams have
+    // hardware queues to overlap on (not with MISLO_ONE_STREAM, the one-queue agent);
+    // MISLO_SPAN_STREAM=0/1 overrides. At the default priority it measured 0.521-0.526 against
+    // 0.539-0.546 ms per window (K = 100, profiles/r5_probe/README.md); a high-priority side
+    // stream (MISLO_SPAN_STREAM_PRIO=1, its own hardware-queue pool) measured 0.65.
     const char* v = getenv("MISLO_SPAN_STREAM");
-    branch_ = v && atoi(v) == 1;
+    branch_ = v ? atoi(v) == 1 : !one_stream;
     if (branch_) {
-      // its own priority: streams of one priority share that priority's hardware queues, and a
-      // side stream landing on the copy stream's queue held the next window's DMA behind the
-      // branch's kernels (measured: copy 0.434 -> 0.477 ms per window at the default priority)
       int lo = 0, hi = 0;
       HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      const char* pv = getenv("MISLO_SPAN_STREAM_PRIO");  // 0 = the default priority
-      if (pv && atoi(pv) == 0)
-        HIPCHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-      else
+      const char* pv = getenv("MISLO_SPAN_STREAM_PRIO");  // 1 = the highest priority
+      if (pv && atoi(pv) == 1)
         HIPCHECK(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
+      else
+        HIPCHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
       for (hipEvent_t* e : {&ev_fork_, &ev_sigbase_, &ev_spans_})
         HIPCHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
