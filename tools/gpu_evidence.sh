@@ -58,7 +58,7 @@ case "${1:-reentry}" in
        "200|smoke|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
        "300|bench|python -u bench.py" \
        "300|bench_nobranch|MISLO_SPAN_STREAM=0 python -u bench.py" \
-       "300|bench_branch_defprio|MISLO_SPAN_STREAM_PRIO=0 python -u bench.py" \
+       "300|bench_branch_hiprio|MISLO_SPAN_STREAM_PRIO=1 python -u bench.py" \
        "300|trace|rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/trace -- python3 bench.py --steps 20 --warmup 3 --paced-windows 0" ;;
   live)     # configs 3 and 2 back to back (the live-attribution evidence)
     $S "480|c3|python -u tools/config3_evidence.py --out gpurun_out/r4_config3" \
