@@ -57,12 +57,26 @@ def test_extension_is_native():
 def test_ring_windows_match_oracle(user_rec):
     """user_rec 32 / 24: the user-space ring holds USER32 / USER24 records (the rocprof tool's compact forms,
     svc|node from the device pod table)."""
+    _check_ring_windows(user_rec, f"oracle{user_rec}")
+
+
+@pytest.mark.parametrize("mode", ["one_chain", "one_stream"])
+def test_stream_layouts_match_oracle(monkeypatch, mode):
+    """The engine's stream layouts compute the same windows: the default (the span side on its own
+    stream), one chain on the compute stream (MISLO_SPAN_STREAM=0: the probe's work list built in the
+    signal scatter's launch) and the one-queue agent's single stream (MISLO_ONE_STREAM=1, copies on
+    the compute stream too)."""
+    monkeypatch.setenv("MISLO_SPAN_STREAM" if mode == "one_chain" else "MISLO_ONE_STREAM", "0" if mode == "one_chain" else "1")
+    _check_ring_windows(24, f"layout-{mode}")
+
+
+def _check_ring_windows(user_rec, tag):
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
     wins, gen = windows()
     imgs = build_replay_images(wins, user_rec=user_rec)
     pipe = WindowPipeline(16384, 512, 8, model="bayes", learn=False, user_cap=4096)
-    rb, user, spans = rings(f"oracle{user_rec}", user_rec)
+    rb, user, spans = rings(tag, user_rec)
     src = RingWindowSource(pipe, rb, user, spans)
     assert all(src.direct.values())  # the rings are page-locked: DMA straight from them
     pods, sn = pod_meta(gen)
