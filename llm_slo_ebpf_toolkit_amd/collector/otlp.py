@@ -454,7 +454,12 @@ class OtlpSpanReceiver:
                     if not sep:
                         self.send_error(400, "Bad header line")
                         return False
-                    hdrs[k.strip().lower()] = v.strip()
+                    name = k.strip().lower()
+                    if name in hdrs and name in ("content-length", "transfer-encoding", "host"):
+                        self.close_connection = True  # conflicting framing: never guess which one
+                        self.send_error(400, "Duplicate header")
+                        return False
+                    hdrs[name] = v.strip()
                 else:
                     self.send_error(431, "Too many headers")
                     return False
@@ -497,6 +502,9 @@ class OtlpSpanReceiver:
                         return
                 if not self.path.startswith("/v1/traces"):
                     self._reply(404, b"not found", "text/plain")
+                    return
+                if self.headers.get("Transfer-Encoding") is not None:  # chunked bodies are not accepted
+                    self._refuse(411, b"length required")
                     return
                 try:
                     n = int(self.headers.get("Content-Length", ""))

@@ -284,3 +284,37 @@ def test_local_addresses_from_fib_trie(tmp_path):
 """)
     assert procfs.local_addresses(55, str(tmp_path)) == {"10.244.1.5"}
     assert procfs.pod_addresses({55: "uid-a", 56: "uid-a"}, str(tmp_path)) == {"10.244.1.5": {"uid-a"}}
+
+
+def test_receiver_refuses_ambiguous_framing_and_keeps_a_connection_alive():
+    """The receiver's header fast path: a duplicate Content-Length or a chunked body is refused
+    (no guessing between framings), and an exporter's keep-alive connection carries request
+    after request."""
+    import http.client
+    import socket
+
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    ring = rt.HostRing(64, 64)
+    m, _ = _mapper()
+    body = _request_json(RES, SPANS)
+    rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push).start()
+    try:
+        for extra in (f"Content-Length: {len(body)}\r\n", "Transfer-Encoding: chunked\r\n"):
+            s = socket.create_connection(rx.addr, timeout=5)
+            s.sendall((f"POST /v1/traces HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                       f"Content-Length: {len(body)}\r\n{extra}\r\n").encode() + body)
+            status = s.recv(4096).split(b"\r\n", 1)[0]
+            s.close()
+            assert status.split()[1] in (b"400", b"411"), status
+        assert ring.size == 0
+        c = http.client.HTTPConnection(rx.addr[0], rx.addr[1], timeout=5)
+        for _ in range(3):
+            c.request("POST", "/v1/traces", body=body, headers={"Content-Type": "application/json"})
+            r = c.getresponse()
+            assert r.status == 200 and r.read() == b"{}"
+        c.close()
+    finally:
+        rx.stop()
+    assert ring.size == 3 * len(m.records(otlp.parse_json(body)))
