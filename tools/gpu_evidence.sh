@@ -18,6 +18,8 @@
 #   spread    the headline bench at K = 20 and K = 200, repeated on one box
 #   rss       the HIP runtime's resident floor under queue / SDMA knobs
 #   probe     the join's oracle GPU tests, the default bench, a kernel trace (join kernel work)
+#   final     every GPU test, smoke, the bench at K = 20 and 100, a kernel + copy trace (profiles/r5_final/)
+#   overhead5 the shipped agent's CPU / RSS with the shipped configuration (profiles/r5_overhead/)
 #
 # Every step runs under its own time limit (tools/gpu_steps.sh); a timeout or crash ends the call.
 set -u
@@ -81,6 +83,16 @@ case "${1:-reentry}" in
       $S "300|k200_$i|python3 bench.py --steps 200 --warmup 10" || exit 1
       tail -n 1 gpurun_out/k200_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('K200', d['ms_per_step'], d['value'])"
     done ;;
+  final)    # round 5's final validation: every GPU test, smoke, the bench at K = 20 and 100, a kernel + copy trace
+    $S "500|gputests|python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread" \
+       "200|smoke|python3 -c 'import __graft_entry__ as g; g.smoke()'" \
+       "300|bench|python -u bench.py" \
+       "300|bench100|python -u bench.py --steps 100 --warmup 10" \
+       "300|trace|rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/trace_final -- python3 bench.py --steps 20 --warmup 3 --paced-windows 0" ;;
+  overhead5) # the shipped agent at 1M events/s, shipped configuration (3 runs) and built-in defaults
+    O="python -u tools/agent_overhead.py --rate 1e6 --seconds 20"
+    $S "200|oh_1|$O --out gpurun_out/r5_oh_1.json" "200|oh_2|$O --out gpurun_out/r5_oh_2.json" \
+       "200|oh_3|$O --out gpurun_out/r5_oh_3.json" "200|oh_bare|$O --bare --out gpurun_out/r5_oh_bare.json" ;;
   probe)    # the join's oracle tests (headline shape included), the bench, a kernel trace ($2: out tag)
     $S "420|native|python -u -m pytest tests/test_native_engine.py tests/test_gpu_engine.py -m gpu -x -v --timeout 360 --timeout-method thread" \
        "300|bench|python -u bench.py" \
