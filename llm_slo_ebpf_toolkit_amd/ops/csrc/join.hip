@@ -299,6 +299,10 @@ struct alignas(16) SpanPP {
 };
 
 constexpr int kLdsGroups = 64;
+// Probe workgroups per phase (3 per CU): ~1,400 phase-2 items pack into two near-full rounds
+// instead of a full round plus a third of one at 1,024, leaving CUs to the span stream.
+// K = 100 A/B, alternating on one box: 0.515 / 0.514 ms per step vs 0.525 / 0.518 at 1,024.
+constexpr int kProbeGrid = 768;
 constexpr int kSigPerItem = 4096;  // signals per work item (a partition's list is sliced); sweep: 256 498 us of compute, 1024 389, 2048 352, 4096 330, 8192 368 (staging repeats per item vs load balance)
 
 // Work list for the two probe phases, rebuilt every window on the device (no host sync,
@@ -312,7 +316,7 @@ constexpr int kSigPerItem = 4096;  // signals per work item (a partition's list 
 // every span of the window (typically the oldest generation at the pod tiers). Phase-2 items are
 // placed longest first (LPT): a counting sort on an estimated cost class. The phase is a few
 // thousand items of very different sizes (a staging cost per item, then up to kSigPerItem
-// signals at a per-key-type rate) dequeued by 1024 workgroups, so its makespan is set by the
+// signals at a per-key-type rate) dequeued by kProbeGrid workgroups, so its makespan is set by the
 // big items that start last; in key-type order the pod+conn items (the most expensive per
 // signal) came after every pod+pid item and the phase ran ~2x its average load (probe
 // profile). Results do not depend on item order: top-3 insertion is an atomic-min cascade
@@ -1195,8 +1199,8 @@ void launch_probe(const SpanCols& sc, const uint32_t* span_items, const uint32_t
   // MISLO_PROBE_GRID workgroups per phase, MISLO_PROBE_ITEM signals per work item.
   static const int grid = [] {
     const char* v = getenv("MISLO_PROBE_GRID");
-    const int x = v ? atoi(v) : 1024;
-    return x >= 1 && x <= 65536 ? x : 1024;
+    const int x = v ? atoi(v) : kProbeGrid;
+    return x >= 1 && x <= 65536 ? x : kProbeGrid;
   }();
   static const int per_item = [] {
     const char* v = getenv("MISLO_PROBE_ITEM");
