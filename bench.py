@@ -97,6 +97,10 @@ def parse():
                          "(the agent's default)")
     ap.add_argument("--xchg-cap", type=int, default=-1,
                     help="warn-level trace-tagged rows each GPU exchanges per window over RCCL (-1: 65536 when N > 1)")
+    ap.add_argument("--rccl-self", action="store_true",
+                    help="one-GPU rehearsal of the multi-GPU chain (diagnostic, not the headline): a one-rank RCCL "
+                         "communicator, the window split around the trace-row exchange (no rows arrive), the packet "
+                         "all-reduce and the incident all-gather")
     ap.add_argument("--user-rec", type=int, default=24, choices=(24, 32, 64),
                     help="user-space ring record size: 24 = USER24 (the rocprof tool's compact record), 32 = USER32, "
                          "64 = EVENT")
@@ -379,12 +383,15 @@ def main() -> int:
             uid = [rt_uid() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             comm = (uid[0], rank, world)
+    elif gpu and a.rccl_self:
+        comm = (rt_uid(), 0, 1)
     # a window's record budget covers its framed ring records (events AND the definitions the
     # probes commit ahead of them) plus its user-space records: nothing may spill into the next window
     sig_cap = max(framed_rows(i.framed) + len(i.user) for i in imgs + himgs)
     user_cap = 1 << int(np.ceil(np.log2(max(1, max(len(i.user) for i in imgs + himgs)))))
-    xchg = (min(65536, a.events) if world > 1 else 0) if a.xchg_cap < 0 else a.xchg_cap
-    import_cap = (world - 1) * xchg  # other GPUs' rows (the halo's rows stay resident)
+    xchg = (min(65536, a.events) if world > 1 or comm else 0) if a.xchg_cap < 0 else a.xchg_cap
+    # other GPUs' rows (the halo's rows stay resident); the one-rank rehearsal sizes for one peer
+    import_cap = (world - 1 if world > 1 else int(comm is not None)) * xchg
     pipe = WindowPipeline(sig_cap, max(a.spans, a.train_spans if train_imgs else 0), a.services, local, comm,
                           model=a.model, seed=a.seed, learn=bool(train_imgs),
                           use_graphs=not a.no_graphs, max_ahead=a.buffers, n_buffers=a.buffers,
@@ -689,7 +696,8 @@ def main() -> int:
             "global_batch": world * a.events,
             "seq_len": 1000,
             "parallelism": f"dp{world} (node-sharded event streams; RCCL per window: packet all-reduce, incident "
-                           f"all-gather{', trace-row exchange' if world > 1 and xchg else ''})",
+                           f"all-gather{', trace-row exchange' if comm and xchg else ''}"
+                           f"{'; one-rank communicator rehearsal' if world == 1 and comm else ''})",
             "halo_ms": a.halo_ms,
             "xchg_rows_per_gpu": xchg,
             "spans_per_window_per_gpu": a.spans,

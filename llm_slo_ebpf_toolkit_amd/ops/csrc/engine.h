@@ -231,9 +231,9 @@ class WindowEngine {
   std::vector<hipEvent_t> xchg_done_;
   // span branch: a second compute stream, overlapping the span side of the chain (~50 us of
   // small kernels, plus the one-workgroup probe work list) with the signal side's decode and
-  // scatter; with one hardware queue (the agent's GPU_MAX_HW_QUEUES=1) it simply serialises.
-  // Opt-in (MISLO_SPAN_STREAM=1): at the default stream priority the branch shortened the chain
-  // by 40 us but delayed the next window's DMA by as much (profiles/r4_span_branch.md).
+  // scatter, joined before the probe: the one-GPU chain only (with the exchange the window runs
+  // as two graphs on the compute stream). On by default, off with MISLO_ONE_STREAM (the
+  // one-queue agent) or MISLO_SPAN_STREAM=0 (profiles/r5_probe/README.md).
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_sigbase_ = nullptr, ev_spans_ = nullptr;
   bool branch_ = false;
@@ -242,6 +242,7 @@ class WindowEngine {
   int nblk_sig_ = 1, nblk_span_ = 1;
   hipStream_t copy_ = nullptr, copy2_ = nullptr, compute_ = nullptr, comm_stream_ = nullptr;
   ncclComm_t comm_ = nullptr;
+  ncclComm_t xcomm_ = nullptr;  // the trace-row exchange's communicator (compute stream; init_comm)
   // device buffers
   std::vector<uint8_t*> in_dev_;     // per buffer: [head | framed | user | spans]
   std::vector<uint8_t*> head_host_;  // per buffer: counts + labels (pinned)

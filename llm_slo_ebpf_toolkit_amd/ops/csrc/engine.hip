@@ -322,6 +322,7 @@ WindowEngine::~WindowEngine() {
   hipDeviceSynchronize();
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   for (auto g : graph_defs_) hipGraphDestroy(g);
+  if (xcomm_) ncclCommDestroy(xcomm_);
   if (comm_) ncclCommDestroy(comm_);
   auto evs = {&t_copy_end_, &h2d_done_, &h2d_part_, &head_done_, &compute_done_, &comm_done_, &t_start_, &t_comp0_, &t_comp1_, &t_end_};
   for (auto* v : evs)
@@ -457,6 +458,8 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   // its reset), the ring state, no other GPUs' rows until merged, the window's rows
   launch_window_begin(fl, gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), ring_state_, remote_n_ + b,
                       counts, N, rows_, st);
+  // the span branch in the one-GPU chain only: forked inside part 1's graph and joined before the
+  // exchange it measured 0.76 against 0.62 ms per window (one-rank rehearsal, bench.py --rccl-self)
   if (branch_ && !xchg) run_span_branch(b, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
@@ -561,6 +564,7 @@ void WindowEngine::launch_part(int part, int b, int n_groups, bool with_labels, 
       run_part2(b, n_groups, with_labels, learn, compute_, xchg);
     }
   };
+  hipStream_t cs = compute_;  // the stream the part is captured on
   if (!cfg_.use_graphs) return run();
   auto key = std::make_tuple(b * 4 + part, n_groups, with_labels, learn);
   auto it = graphs_.find(key);
@@ -571,15 +575,15 @@ void WindowEngine::launch_part(int part, int b, int n_groups, bool with_labels, 
   }
   if (it == graphs_.end()) {
     hipGraph_t g;
-    HIPCHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+    HIPCHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     run();
-    HIPCHECK(hipStreamEndCapture(compute_, &g));
+    HIPCHECK(hipStreamEndCapture(cs, &g));
     hipGraphExec_t ex;
     HIPCHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     graph_defs_.push_back(g);
     it = graphs_.emplace(key, ex).first;
   }
-  HIPCHECK(hipGraphLaunch(it->second, compute_));
+  HIPCHECK(hipGraphLaunch(it->second, cs));
 }
 
 void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bool learn) {
@@ -687,9 +691,18 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
                           (uint32_t)cfg_.import_cap, cfg_.xchg_cap, compute_);
       inject_.clear();
       launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, compute_);
+    } else if (xcomm_) {
+      // on the compute stream, over the exchange's own communicator (each communicator is used
+      // on one stream only, so each keeps one issue order on every rank): part 2 follows the
+      // merge in stream order, with no hand-off between hardware queues on the window's critical
+      // path (each such hop idled the compute queue 20-45 us, profiles/r5_multigpu/)
+      NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, xcomm_, compute_));
+      launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[b], remote_n_ + b, (uint32_t)cfg_.import_cap,
+                          cfg_.xchg_cap, compute_);
+      launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, compute_);
     } else {
-      // every use of the communicator stays on the comm stream (one stream, one issue order on
-      // every rank): the compute stream hands over after part 1 and waits for the merge
+      // MISLO_XCHG_STREAM=comm: the exchange on the comm stream with the window's other
+      // collectives: the compute stream hands over after part 1 and waits for the merge
       HIPCHECK(hipEventRecord(xchg_done_[b], compute_));
       HIPCHECK(hipStreamWaitEvent(comm_stream_, xchg_done_[b], 0));
       NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, comm_, comm_stream_));
@@ -923,6 +936,10 @@ void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
     xrecv_ = dalloc<uint8_t>(xstride_ * world);
     xrecv_bytes_ = xstride_ * world;
     HIPCHECK(hipMemset(xrecv_, 0, xrecv_bytes_));
+    // the exchange's own communicator (a split of comm_: every rank, same color), used on the
+    // compute stream only; MISLO_XCHG_STREAM=comm keeps the exchange on the comm stream instead
+    const char* xv = getenv("MISLO_XCHG_STREAM");
+    if (!(xv && std::strcmp(xv, "comm") == 0)) NCCLCHECK(ncclCommSplit(comm_, 0, rank, &xcomm_, nullptr));
   }
 }
 

@@ -3,7 +3,7 @@
 RCCL refuses two ranks on one device, so the two-rank tests (test_rccl_pair.py,
 test_multigpu_agent.py) skip on the one-GPU box. A communicator of world 1 still runs every
 collective the multi-GPU chain issues (engine.hip: the trace-row all-gather between the window's
-two halves, the packet all-reduce and the incident all-gather on the comm stream, the results
+two halves -- on the compute stream over a split communicator, or on the comm stream --, the packet all-reduce and the incident all-gather on the comm stream, the results
 copied from the all-gathered block, the totals accumulated behind the collectives), so the same
 windows through an engine with and without one must agree bit for bit: packets, incident
 results, features, posteriors and totals. SURVEY §2.4 RCCL table; REF has no collective
@@ -40,10 +40,18 @@ def _run(tag, comm, wins, imgs, gen):
 
 
 @pytest.mark.timeout(120)
-def test_one_rank_rccl_communicator_matches_the_communicator_free_engine():
+@pytest.mark.parametrize("xchg_stream", ["compute", "comm"])
+def test_one_rank_rccl_communicator_matches_the_communicator_free_engine(xchg_stream, monkeypatch):
+    """xchg_stream: the trace-row exchange on the compute stream over its own (split)
+    communicator (the default), or on the comm stream with the window's other collectives
+    (MISLO_XCHG_STREAM=comm)."""
     from llm_slo_ebpf_toolkit_amd.ops import load_agent
     from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
 
+    if xchg_stream == "comm":
+        monkeypatch.setenv("MISLO_XCHG_STREAM", "comm")
+    else:
+        monkeypatch.delenv("MISLO_XCHG_STREAM", raising=False)
     wins, gen = windows(n_win=4, seed=71)
     imgs = build_replay_images(wins)
     solo, solo_info = _run("solo", None, wins, imgs, gen)
