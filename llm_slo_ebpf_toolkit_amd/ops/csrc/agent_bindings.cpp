@@ -262,6 +262,14 @@ class PyEngine {
     py::gil_scoped_release nogil;
     return eng().import_state();
   }
+  py::bytes sent_block() {
+    std::vector<uint8_t> b;
+    {
+      py::gil_scoped_release nogil;
+      b = eng().sent_block();
+    }
+    return py::bytes(reinterpret_cast<const char*>(b.data()), b.size());
+  }
   void close() {
     if (e_) {
       py::gil_scoped_release nogil;
@@ -358,6 +366,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("restore", &PyEngine::restore)
       .def("sync", &PyEngine::sync)
       .def("import_state", &PyEngine::import_state)
+      .def("sent_block", &PyEngine::sent_block)
       .def("close", &PyEngine::close)
       .def_property_readonly("buffers", &PyEngine::buffers)
       .def_property_readonly("windows_folded", &PyEngine::folded)

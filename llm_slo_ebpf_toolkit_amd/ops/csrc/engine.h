@@ -170,6 +170,9 @@ class WindowEngine {
   // generations (count, current slot, windows held, per-age cut-offs and rows), per buffer the
   // other-GPU row counts
   std::vector<int64_t> import_state();
+  // this GPU's exchange block of the last window (header: row count | XRec rows; empty without
+  // the exchange): what the all-gather delivers to the other GPUs (tests)
+  std::vector<uint8_t> sent_block();
   int64_t windows_folded() const { return folded_; }
   size_t staged_bytes() const { return staged_bytes_; }
   size_t direct_bytes() const { return direct_bytes_; }

@@ -860,6 +860,13 @@ void WindowEngine::set_pods(const uint32_t* pods, const uint32_t* svcnode, size_
   HIPCHECK(hipMemcpyAsync(pod_sn_, pod_host_, kPodRows * 4, hipMemcpyHostToDevice, compute_));
 }
 
+std::vector<uint8_t> WindowEngine::sent_block() {
+  sync();
+  std::vector<uint8_t> out(xsend_ ? xstride_ : 0);
+  if (xsend_) HIPCHECK(hipMemcpy(out.data(), xsend_, xstride_, hipMemcpyDeviceToHost));
+  return out;
+}
+
 std::vector<int64_t> WindowEngine::import_state() {
   sync();
   int rows[2];

@@ -25,16 +25,18 @@ def _run(tag, comm, wins, imgs, gen):
     rb, user, spans = rings(tag)
     src = RingWindowSource(pipe, rb, user, spans)
     pipe.eng.set_pods(*pod_meta(gen))
-    out = []
+    out, sent = [], []
     for w, img in zip(wins, imgs):
         k = src.stage(feed(img, rb, user, spans), w.n_groups, img.labels)["k"]
         pk = {key: np.array(v, copy=True) if not isinstance(v, dict) else dict(v) for key, v in pipe.packet(k).items()}
         res = {key: v.copy() for key, v in pipe.results(k, w.n_groups).items()}
         allr = [{key: v.copy() for key, v in r.items()} for r in pipe.results_all(k, w.n_groups)]
         out.append((pk, res, allr))
+        sent.append(bytes(pipe.eng.sent_block()) if comm is not None else b"")
     src.drain()
     info = {"has_comm": bool(pipe.eng.has_comm) if hasattr(pipe.eng, "has_comm") else comm is not None,
-            "world": int(pipe.eng.world), "totals": np.asarray(pipe.eng.totals(), dtype=np.float64).copy()}
+            "world": int(pipe.eng.world), "totals": np.asarray(pipe.eng.totals(), dtype=np.float64).copy(),
+            "sent": sent}
     pipe.eng.close()
     return out, info
 
@@ -72,3 +74,36 @@ def test_one_rank_rccl_communicator_matches_the_communicator_free_engine(xchg_st
             np.testing.assert_array_equal(ab[0][key], rb[key], err_msg=f"window {j} all-gathered {key}")
     assert any(int(r[0]["dbg"][0]) > 0 for r in rccl), "no join candidates: the comparison would be vacuous"
     np.testing.assert_array_equal(solo_info["totals"], rccl_info["totals"])
+
+
+@pytest.mark.timeout(120)
+def test_the_exchange_block_is_the_oracles_trace_row_selection():
+    """What this GPU hands the all-gather each window (k_sel_count / k_sel_scan / k_sel_scatter:
+    its warn-level trace-tagged local rows, identity dropped, in row order, capped at xchg_cap)
+    is byte for byte the oracle's block (oracle.trace_rows -> oracle.exchange_blocks). With one
+    rank nothing is imported, so the comparison above never looks at these bytes."""
+    from llm_slo_ebpf_toolkit_amd.ops import load_agent
+    from llm_slo_ebpf_toolkit_amd.pipeline import oracle
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
+
+    from test_native_engine import pod_meta as _pm
+
+    wins, gen = windows(n_win=4, seed=73)
+    imgs = build_replay_images(wins)
+    _, info = _run("sel", (load_agent().unique_id(), 0, 1), wins, imgs, gen)
+    pods, sn = _pm(gen)
+    pod_sn = dict(zip(pods.tolist(), sn.tolist()))
+    table, tmap = oracle.CtxTable(), oracle.TraceMap()
+    n_sel = []
+    for j, (img, blk) in enumerate(zip(imgs, info["sent"])):
+        oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
+        d_loc = oracle.decode_window(img.framed, img.user, table, tmap, img.bases)
+        mine = oracle.trace_rows(d_loc, len(d_loc.ts))
+        ref = oracle.exchange_blocks([mine], 1024)
+        got = np.frombuffer(blk, dtype=np.uint8)
+        assert got.size == ref.size, (j, got.size, ref.size)
+        n_dev = int(got[:4].view(np.uint32)[0])
+        assert n_dev == min(len(mine.ts), 1024), (j, n_dev, len(mine.ts))
+        np.testing.assert_array_equal(got[32:32 * (1 + n_dev)], ref[32:32 * (1 + n_dev)], err_msg=f"window {j}")
+        n_sel.append(n_dev)
+    assert min(n_sel) > 0, "no trace rows selected: the comparison would be vacuous"
