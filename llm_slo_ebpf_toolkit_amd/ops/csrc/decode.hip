@@ -27,6 +27,12 @@ struct DecodeOut {
   unsigned long long* misc;  // [0] unsupported events, [1] zero-timestamp events,
                              // [2 + slot] per-signal value sum in 1/1000 units (Prometheus _sum)
   int blk_base = 0;      // this launch's first row in part_cnt (a second row segment's decode)
+  // the exchange's trace-row selection, fused (segment 0 with the exchange): per block the
+  // count of selected local rows, per (block, trip, wave) the 64-row ballot mask (exchange.hip
+  // k_sel_scatter_mask reads them in the same geometry)
+  uint32_t* sel_cnt = nullptr;
+  unsigned long long* sel_mask = nullptr;
+  int sel_stride = 0;    // masks per block
 };
 
 constexpr int kMiscSums = 2;  // offset of the per-slot value sums in misc
@@ -423,10 +429,10 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   __shared__ DecodeLds L;
   // the workgroup's scalar results, merged in LDS first: one global atomic per workgroup and
   // counter (per-wave atomics put 4096 waves x 5 updates per window on the same few L2 lines)
-  __shared__ uint32_t s_cnt2[2];
+  __shared__ uint32_t s_cnt2[3];
   __shared__ unsigned long long s_t[3];
   if (threadIdx.x == 0) {
-    s_cnt2[0] = s_cnt2[1] = 0u;
+    s_cnt2[0] = s_cnt2[1] = s_cnt2[2] = 0u;
     s_t[0] = 0ull;
     s_t[1] = ~0ull;
     s_t[2] = 0ull;
@@ -449,6 +455,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   const int chunk = (n - seg_beg + gridDim.x - 1) / gridDim.x;
   const int beg = seg_beg + blockIdx.x * chunk, end = min(n, beg + chunk);
   int unsupported = 0, zero_ts = 0, events = 0, other = 0;
+  uint32_t n_sel = 0;  // lane 0 of each wave: its selected rows
   unsigned long long t_hi = 0;
   uint64_t tr[2] = {~0ull, 0ull};  // joinable rows' time range (u64 images)
   // rows land in the current generation's slot (resident for the halo)
@@ -541,6 +548,18 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
       }
     }
     __syncthreads();
+    if (o.sel_mask) {  // a warn-level (or worse) trace-tagged joinable local row (exchange.hip selected())
+      bool sel = false;
+      if (i < end && i < n_loc) {
+        const SigRec& r = *reinterpret_cast<const SigRec*>(&s_stage[threadIdx.x * 5]);
+        sel = r.slot != kNoSlot && r.ts != 0 && r.tr != 0 && (r.val >= L.tab.err[r.slot] || r.val >= L.tab.warn[r.slot]);
+      }
+      const unsigned long long m = __ballot(sel);
+      if (lane == 0) {
+        o.sel_mask[(size_t)blockIdx.x * o.sel_stride + (size_t)it * (NT / 64) + (threadIdx.x >> 6)] = m;
+        n_sel += (uint32_t)__popcll(m);
+      }
+    }
     const int first = i - lane;
     const int nv = min(64, end - first);
     if (nv > 0) {
@@ -564,6 +583,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   if ((threadIdx.x & 63) == 0) {
     if (events) atomicAdd(&s_cnt2[0], (uint32_t)events);
     if (other) atomicAdd(&s_cnt2[1], (uint32_t)other);
+    if (n_sel) atomicAdd(&s_cnt2[2], n_sel);
     if (t_hi) atomicMax(&s_t[0], t_hi);
     if (tr[0] <= tr[1]) {
       atomicMin(&s_t[1], (unsigned long long)tr[0]);
@@ -574,6 +594,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   if (threadIdx.x == 0) {
     if (s_cnt2[0]) atomicAdd(&rs[kRsEvents], s_cnt2[0]);
     if (s_cnt2[1]) atomicAdd(&rs[kRsOtherShard], s_cnt2[1]);
+    if (o.sel_cnt) o.sel_cnt[blockIdx.x] = s_cnt2[2];  // every block, zero included (the scan reads all)
     if (s_t[0]) atomicMax(tmax, s_t[0]);
     if (o.cols.gen && s_t[1] <= s_t[2]) {
       atomicMin(reinterpret_cast<unsigned long long*>(&o.cols.gen->tlo[cur]), s_t[1]);
@@ -711,6 +732,11 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
 // left one wave per SIMD, latency-bound on the record loads; 16 waves per CU hide them.
 constexpr int kDecodeNT = 1024;
 
+int decode_sel_stride(int cap) {
+  const long long g = decode_grid(cap), chunk = ((long long)cap + g - 1) / g;
+  return (int)((chunk + kDecodeNT - 1) / kDecodeNT) * (kDecodeNT / 64);
+}
+
 int decode_grid(int cap) {
   // Fixed per-capacity grid (graph-replayable): ~4 events per thread, capped at kPartBlocks.
   long long g = ((long long)cap + 1023) / 1024;
@@ -774,8 +800,8 @@ void launch_decode_window(const uint8_t* framed, const void* user, const int* n_
                           uint32_t* ring_state, unsigned long long* tmax, const uint32_t* pod_sn, uint32_t n_pods,
                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                           unsigned long long* misc, hipStream_t stream, int seg, int grid, int blk_base, int sh_rank,
-                          int sh_world) {
-  DecodeOut o{cols, hist, status_cnt, part_cnt, misc, blk_base};
+                          int sh_world, uint32_t* sel_cnt, unsigned long long* sel_mask, int sel_stride) {
+  DecodeOut o{cols, hist, status_cnt, part_cnt, misc, blk_base, sel_cnt, sel_mask, sel_stride};
   constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_window<NT>), dim3(grid > 0 ? grid : decode_grid(cap)), dim3(NT), 0, stream, framed,
                      (const Event*)user, n_dev, rows, cap, imp, reinterpret_cast<const uint4*>(ctx_tab), n_ctx, tt,

@@ -222,6 +222,8 @@ class WindowEngine {
   KeyTs* g_keys_ = nullptr;        // [gens][kKeyTypes * n_rows] partition list keys
   std::vector<SigRec*> imp_;
   uint32_t *remote_n_ = nullptr, *sel_cnt_ = nullptr, *sel_off_ = nullptr;
+  unsigned long long* sel_mask_ = nullptr;  // the fused selection's ballot masks (nullptr: two passes)
+  int sel_stride_ = 0;
   uint8_t *xsend_ = nullptr, *xrecv_ = nullptr;
   size_t xstride_ = 0, xrecv_bytes_ = 0;
   int nblk_imp_ = 0;                    // decode blocks of the other GPUs' rows

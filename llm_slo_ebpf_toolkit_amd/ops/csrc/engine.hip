@@ -261,6 +261,11 @@ void WindowEngine::alloc() {
   if (cfg_.xchg_cap) {
     xsend_ = dalloc<uint8_t>(xstride_);
     HIPCHECK(hipMemset(xsend_, 0, xstride_));
+    const char* tp = getenv("MISLO_SEL_TWO_PASS");
+    if (!(tp && atoi(tp) == 1)) {  // the fused selection's ballot masks (segment 0's decode geometry)
+      sel_stride_ = decode_sel_stride(n_rows_);
+      sel_mask_ = dalloc<unsigned long long>((size_t)decode_grid(n_rows_) * (size_t)sel_stride_);
+    }
   }
   // context table: every id the kernel or the host encoder can assign, HBM-resident
   ctx_tab_ = dalloc<uint32_t>((size_t)kCtxRows * 4);
@@ -347,7 +352,7 @@ WindowEngine::~WindowEngine() {
                   g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
                   s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
                   hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_hash_,
-                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, xsend_, xrecv_, g_keys_, gen_, s_pre_};
+                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, sel_mask_, xsend_, xrecv_, g_keys_, gen_, s_pre_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_ && copy_ != compute_) hipStreamDestroy(copy_);
@@ -463,10 +468,17 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   if (branch_ && !xchg) run_span_branch(b, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
+  const bool fused_sel = xchg && sel_mask_;  // the selection's count and masks left by the decode
   launch_decode_window(in + off_kern_, in + off_user_, counts, rows_, N, imp_[b], ctx_tab_, (int)kCtxRows, tt,
                        ring_state_, tmax_, pod_sn_, kPodRows, sig_cols(), hist_, status_, g_part_blk_, misc_, st, 0, 0, 0,
-                       rec_shard_rank(), rec_shard_world());
-  if (xchg)  // this window's warn-level trace-tagged rows, as the other GPUs will import them
+                       rec_shard_rank(), rec_shard_world(), fused_sel ? sel_cnt_ : nullptr,
+                       fused_sel ? sel_mask_ : nullptr, sel_stride_);
+  // this window's warn-level trace-tagged rows, as the other GPUs will import them
+  if (fused_sel)
+    launch_select_masked(sig_cols(), rows_, N, sel_cnt_, sel_off_, sel_mask_, sel_stride_,
+                         reinterpret_cast<XRec*>(xsend_ + sizeof(XRec)), reinterpret_cast<uint32_t*>(xsend_),
+                         (uint32_t)cfg_.xchg_cap, st);
+  else if (xchg)
     launch_select(sig_cols(), rows_, counts, N, sel_cnt_, sel_off_, reinterpret_cast<XRec*>(xsend_ + sizeof(XRec)),
                   reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, st);
 }

@@ -17,6 +17,9 @@
 //
 // The trace-row selection is a stable stream compaction (count -> exclusive scan -> ordered
 // scatter), so the exchanged rows, and with them the join's tie-breaks by row, are deterministic.
+// By default the count is fused into segment 0's decode (per-block counts and 64-row ballot
+// masks) and the scatter reads only the selected rows (k_sel_scatter_mask); the two full passes
+// (k_sel_count, k_sel_scatter) remain behind MISLO_SEL_TWO_PASS=1.
 #include "mislo_common.h"
 #include "mislo_launch.h"
 #include "mislo_packet.h"
@@ -122,6 +125,44 @@ __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_
       for (int q = 0; q < kSelNT / 64; ++q) t += s_w[q];
       s_base += t;
     }
+  }
+}
+
+// ordered scatter from segment 0's decode (fused selection): the decode's geometry (its grid,
+// kDecodeNT threads, block b owning rows [b * chunk, ...) of [0, min(rows[0], cap))), its ballot
+// mask per (block, trip, wave) and its per-block count (scanned into blk_off). Only the selected
+// rows are read.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_sel_scatter_mask(SignalCols gc, const int* __restrict__ rows, int cap,
+                                                         const unsigned long long* __restrict__ mask, int mask_stride,
+                                                         const uint32_t* __restrict__ blk_off, XRec* __restrict__ out,
+                                                         uint32_t out_cap) {
+  constexpr int NW = NT / 64;
+  const int n = min(rows[0], cap);
+  const int chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int beg = blockIdx.x * chunk, end = min(n, beg + chunk);
+  const int trips = end > beg ? (end - beg + NT - 1) / NT : 0;
+  const SigRec* rec = gc.rec + (size_t)cur_slot(gc) * (size_t)gc.stride;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ uint32_t s_w[NW];
+  uint32_t base = blk_off[blockIdx.x];
+  const unsigned long long* mb = mask + (size_t)blockIdx.x * mask_stride;
+  for (int it = 0; it < trips; ++it) {
+    const unsigned long long m = mb[it * NW + w];
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t wo = base, tot = 0;
+    for (int q = 0; q < NW; ++q) {
+      if (q < w) wo += s_w[q];
+      tot += s_w[q];
+    }
+    if ((m >> lane) & 1ull) {
+      const uint32_t dst = wo + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      const SigRec r = rec[beg + it * NT + threadIdx.x];
+      if (dst < out_cap) out[dst] = XRec{r.ts, r.tr, r.val, r.slot, 0, 0};  // joins by its trace hash only
+    }
+    base += tot;
+    __syncthreads();  // s_w is rewritten by the next trip
   }
 }
 
@@ -240,6 +281,15 @@ void launch_select(const SignalCols& gc, const int* rows, const int* counts, int
   hipLaunchKernelGGL(k_sel_count, dim3(g), dim3(kSelNT), 0, stream, a, blk_cnt);
   hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap);
   hipLaunchKernelGGL(k_sel_scatter, dim3(g), dim3(kSelNT), 0, stream, a, blk_off, out, out_cap);
+}
+
+void launch_select_masked(const SignalCols& gc, const int* rows, int cap, const uint32_t* blk_cnt, uint32_t* blk_off,
+                          const unsigned long long* mask, int mask_stride, XRec* out, uint32_t* n_out,
+                          uint32_t out_cap, hipStream_t stream) {
+  const int g = decode_grid(cap);  // segment 0's decode grid (its counts and masks)
+  hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap);
+  hipLaunchKernelGGL((k_sel_scatter_mask<1024>), dim3(g), dim3(1024), 0, stream, gc, rows, cap, mask, mask_stride,
+                     blk_off, out, out_cap);
 }
 
 void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, uint32_t* remote_n,

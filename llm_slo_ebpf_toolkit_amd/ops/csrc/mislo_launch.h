@@ -71,7 +71,10 @@ void launch_decode_window(const uint8_t* framed, const void* user, const int* n_
                           uint32_t* ring_state, unsigned long long* tmax, const uint32_t* pod_sn, uint32_t n_pods,
                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                           unsigned long long* misc, hipStream_t stream, int seg = 0, int grid = 0, int blk_base = 0,
-                          int sh_rank = 0, int sh_world = 1);
+                          int sh_rank = 0, int sh_world = 1, uint32_t* sel_cnt = nullptr,
+                          unsigned long long* sel_mask = nullptr, int sel_stride = 0);
+// ballot masks per decode block of `cap` rows (the fused selection's mask stride)
+int decode_sel_stride(int cap);
 
 // exchange.hip: the trace-tagged rows of the GPU exchange, the other GPUs' rows, the generations
 int select_grid(int cap);
@@ -87,6 +90,11 @@ static_assert(sizeof(XRec) == 32, "exchange rows are 32 bytes");
 // the current generation's warn-level trace-tagged local rows -> out (stable order), count -> n_out
 void launch_select(const SignalCols& gc, const int* rows, const int* counts, int cap, uint32_t* blk_cnt,
                    uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream);
+// the same selection from the counts and ballot masks segment 0's decode left (sel_cnt /
+// sel_mask): scan, then an ordered scatter that reads only the selected rows
+void launch_select_masked(const SignalCols& gc, const int* rows, int cap, const uint32_t* blk_cnt, uint32_t* blk_off,
+                          const unsigned long long* mask, int mask_stride, XRec* out, uint32_t* n_out,
+                          uint32_t out_cap, hipStream_t stream);
 void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, uint32_t* remote_n,
                          uint32_t imp_cap, int max_rows, hipStream_t stream);
 void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, int* rows, GenMeta* gen,
