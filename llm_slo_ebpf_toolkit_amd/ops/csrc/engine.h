@@ -144,7 +144,7 @@ class WindowEngine {
   void set_p0(const double* p0, size_t n);
   void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
   // other GPUs' rows for the next window, as their exchange blocks would arrive over RCCL (world
-  // blocks of [32-byte header: uint32 row count | XRec rows], this rank's block skipped); the
+  // blocks of [24-byte header: uint32 row count | XRec rows], this rank's block skipped); the
   // next submit runs the exchange path (decode part 1, merge, part 2) with them
 
   void inject_remote(const void* blocks, size_t stride, int world, int me);

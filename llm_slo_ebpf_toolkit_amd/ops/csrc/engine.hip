@@ -257,7 +257,7 @@ void WindowEngine::alloc() {
   sel_cnt_ = dalloc<uint32_t>(1024);
   sel_off_ = dalloc<uint32_t>(1024);
   for (int b = 0; b < nb_; ++b) imp_.push_back(cfg_.import_cap ? dalloc<SigRec>(cfg_.import_cap) : nullptr);
-  xstride_ = sizeof(XRec) * (1 + (size_t)cfg_.xchg_cap);  // [32-byte header: row count | XRec rows]
+  xstride_ = sizeof(XRec) * (1 + (size_t)cfg_.xchg_cap);  // [24-byte header: row count | XRec rows]
   if (cfg_.xchg_cap) {
     xsend_ = dalloc<uint8_t>(xstride_);
     HIPCHECK(hipMemset(xsend_, 0, xstride_));

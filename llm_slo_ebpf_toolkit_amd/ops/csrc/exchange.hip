@@ -11,7 +11,7 @@
 //            re-decode and no re-partition of them).
 //   remote : each GPU's trace-tagged local rows of window k at warn level or above (the
 //            evidence; identity dropped: only their trace hash can join) are all-gathered over
-//            RCCL on the comm stream as 32-byte XRecs and appended to the same window's rows on
+//            RCCL as 24-byte XRecs and appended to the same window's rows on
 //            every other GPU, so a request traced across nodes joins the elevated signals of
 //            every node that saw it.
 //
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
   if (t == 1023) *n_out = min(s[1023], out_cap);
 }
 
-// ordered scatter: block offset + wave offsets + in-wave ballot rank; 32-byte exchange rows
+// ordered scatter: block offset + wave offsets + in-wave ballot rank; 24-byte exchange rows
 // (XRec: no identity)
 __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_t* __restrict__ blk_off,
                                                         XRec* __restrict__ out, uint32_t out_cap) {
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kSelNT) void k_sel_scatter(SelArgs a, const uint32_
     for (int q = 0; q < w; ++q) wo += s_w[q];
     if (s) {
       const uint32_t dst = wo + rank;
-      if (dst < out_cap) out[dst] = XRec{r.ts, r.tr, r.val, r.slot, 0, 0};  // joins by its trace hash only
+      if (dst < out_cap) out[dst] = XRec{r.ts, r.tr, r.val, r.slot};  // joins by its trace hash only
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -159,14 +159,14 @@ __global__ __launch_bounds__(NT) void k_sel_scatter_mask(SignalCols gc, const in
     if ((m >> lane) & 1ull) {
       const uint32_t dst = wo + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
       const SigRec r = rec[beg + it * NT + threadIdx.x];
-      if (dst < out_cap) out[dst] = XRec{r.ts, r.tr, r.val, r.slot, 0, 0};  // joins by its trace hash only
+      if (dst < out_cap) out[dst] = XRec{r.ts, r.tr, r.val, r.slot};  // joins by its trace hash only
     }
     base += tot;
     __syncthreads();  // s_w is rewritten by the next trip
   }
 }
 
-// other GPUs' exchanged rows (each rank's block: a 32-byte header holding its row count, then
+// other GPUs' exchanged rows (each rank's block: a 24-byte header holding its row count, then
 // XRec rows) as identity-free SigRecs, in rank order: appended to the window's own rows
 __global__ __launch_bounds__(256) void k_remote_merge(const uint8_t* __restrict__ xrecv, size_t stride, int world,
                                                       int me, SigRec* __restrict__ imp,

@@ -78,15 +78,15 @@ int decode_sel_stride(int cap);
 
 // exchange.hip: the trace-tagged rows of the GPU exchange, the other GPUs' rows, the generations
 int select_grid(int cap);
-// 32-byte exchange row: what another GPU needs to join a row by its trace hash
+// 24-byte exchange row: what another GPU needs to join a row by its trace hash (no padding:
+// the all-gather moves world x (1 + xchg_cap) of them per window)
 struct XRec {
   int64_t ts;
   uint64_t tr;
   float val;
   uint32_t slot;
-  uint32_t pad[2];
 };
-static_assert(sizeof(XRec) == 32, "exchange rows are 32 bytes");
+static_assert(sizeof(XRec) == 24, "exchange rows are 24 bytes");
 // the current generation's warn-level trace-tagged local rows -> out (stable order), count -> n_out
 void launch_select(const SignalCols& gc, const int* rows, const int* counts, int cap, uint32_t* blk_cnt,
                    uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream);

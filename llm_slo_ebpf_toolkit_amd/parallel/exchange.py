@@ -3,7 +3,7 @@
 Per rank and window k, the device does:
 
 1. part 1: decode the window's records (rows [0, counts[0])) into the current generation slot,
-   and select this rank's trace-tagged local rows at warn level or above as 32-byte XRecs (time,
+   and select this rank's trace-tagged local rows at warn level or above as 24-byte XRecs (time,
    trace hash, value, signal: no pod / pid / connection, so another GPU can only join them
    through the trace tier), capped at xchg_cap;
 2. RCCL all-gather of every rank's fixed-size block [header: row count | XRecs] (comm stream);
@@ -37,9 +37,10 @@ def parse_block(block: np.ndarray) -> oracle.Decoded:
     """One rank's exchange block -> imported rows (oracle.remote_rows of its XRecs)."""
     b = np.ascontiguousarray(block, dtype=np.uint8)
     n = int(b[:4].view(np.uint32)[0])
-    cap = b.size // 32 - 1
+    w = XREC.itemsize
+    cap = b.size // w - 1
     n = min(n, cap)
-    rows = b[32:32 + 32 * n].view(XREC)
+    rows = b[w:w + w * n].view(XREC)
     slot = np.where(rows["slot"] == 0xFF, oracle.NO_SLOT, rows["slot"]).astype(np.uint8)
     d = oracle.Decoded(rows["ts"].astype(np.int64), rows["val"].astype(np.float32), slot,
                        np.zeros(n, np.uint8), np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(n, np.uint32),

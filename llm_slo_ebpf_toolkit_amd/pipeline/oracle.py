@@ -270,14 +270,14 @@ def from_sigrec(r: np.ndarray) -> Decoded:
                    r["tr"].astype(np.uint64), r["cn"].astype(np.uint64))
 
 
-XREC = np.dtype([("ts", "<i8"), ("tr", "<u8"), ("val", "<f4"), ("slot", "<u4"), ("pad", "<u4", (2,))])
-assert XREC.itemsize == 32
+XREC = np.dtype([("ts", "<i8"), ("tr", "<u8"), ("val", "<f4"), ("slot", "<u4")])
+assert XREC.itemsize == 24
 
 
 def exchange_blocks(parts, cap: int) -> np.ndarray:
     """Per-rank exchange blocks as the GPUs all-gather them (mislo_launch.h XRec):
-    [32-byte header: row count | 32-byte rows]."""
-    stride = 32 * (1 + cap)
+    [24-byte header: row count | 24-byte rows]."""
+    stride = XREC.itemsize * (1 + cap)
     out = np.zeros(len(parts) * stride, dtype=np.uint8)
     for r, p in enumerate(parts):
         n = min(len(p.ts), cap)
@@ -286,7 +286,7 @@ def exchange_blocks(parts, cap: int) -> np.ndarray:
         rows["slot"] = np.where(p.slot[:n] == NO_SLOT, 0xFF, p.slot[:n])
         blk = out[r * stride:(r + 1) * stride]
         blk[:4] = np.frombuffer(np.uint32(n).tobytes(), dtype=np.uint8)
-        blk[32:32 + rows.nbytes] = rows.view(np.uint8)
+        blk[XREC.itemsize:XREC.itemsize + rows.nbytes] = rows.view(np.uint8)
     return out
 
 

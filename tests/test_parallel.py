@@ -1,7 +1,7 @@
 """Distributed path on CPU (gloo, world_size 2, 127.0.0.1): the engine's multi-GPU window
 protocol (parallel/exchange.py, the CPU model of ops/csrc/exchange.hip) over a real process
 group -- node-sharded streams, the halo carried across window cuts, warn-level trace rows
-exchanged as 32-byte XRec blocks and imported one window later, the packet all-reduce."""
+exchanged as 24-byte XRec blocks and imported one window later, the packet all-reduce."""
 
 import os
 import socket
