@@ -190,6 +190,8 @@ class WindowEngine {
   int rec_shard_rank() const { return cfg_.split_rings ? 0 : cfg_.shard_rank; }
   int rec_shard_world() const { return cfg_.split_rings ? 1 : cfg_.shard_world; }
   void alloc();
+  void set_buffer(int b);
+  void run_begin(int b, hipStream_t st);
   void run_part1(int b, hipStream_t st, bool xchg);
   void run_part2(int b, int n_groups, bool with_labels, bool learn, hipStream_t st, bool xchg);
   // the window's span side (decode, partition, probe work list, span sort) on side_, forked
@@ -242,6 +244,7 @@ class WindowEngine {
   hipStream_t side_ = nullptr;
   hipEvent_t ev_fork_ = nullptr, ev_sigbase_ = nullptr, ev_spans_ = nullptr;
   bool branch_ = false;
+  bool xspan_ = false;  // with the exchange: window head (part 4) and span side on side_ (part 3)
   bool exchange() const { return comm_ && cfg_.xchg_cap > 0 && cfg_.import_cap > 0; }
   JoinParams jp_{};
   int nblk_sig_ = 1, nblk_span_ = 1;

@@ -183,6 +183,8 @@ void WindowEngine::alloc() {
         HIPCHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
       for (hipEvent_t* e : {&ev_fork_, &ev_sigbase_, &ev_spans_})
         HIPCHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      const char* xv = getenv("MISLO_XCHG_SPAN_SIDE");  // 0: the exchange path's span side in part 2
+      xspan_ = !(xv && atoi(xv) == 0);
     }
   }
   // one GPU: the window's tail (packet accumulate, timing) runs on the compute stream; a comm
@@ -216,7 +218,7 @@ void WindowEngine::alloc() {
     t_comp1_.push_back(mk_event(true));
     t_end_.push_back(mk_event(true));
   }
-  warm_.assign(4 * nb_, false);
+  warm_.assign(8 * nb_, false);
   // per-incident results block: [post G*16 f64][gconf G f64][feat G*16 f32][pred G i32][evbits G*16 u32]
   // [sli G*2 u32]
   const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
@@ -429,13 +431,9 @@ void WindowEngine::wait_h2d(int64_t k) {
   HIPCHECK(hipEventSynchronize(h2d_part_[k % nb_]));
 }
 
-// The captured part of a window: everything between the DMA and the packet.
-// Part 1 of a window: accumulators, definitions, the decode of the window's records and the
-// halo it imported; with the GPU exchange, this window's trace-tagged rows for the others.
-void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
-  uint8_t* in = in_dev_[b];
-  const int* counts = reinterpret_cast<const int*>(in);
-  const int N = n_rows_, S = cfg_.span_cap, G = cfg_.group_cap;
+// This buffer's per-incident result pointers (read by the kernels the parts launch).
+void WindowEngine::set_buffer(int b) {
+  const int G = cfg_.group_cap;
   uint8_t* r = res_dev_[b];  // this buffer's per-incident results block
   const size_t o_gconf = 16 * (size_t)G * 8, o_feat = o_gconf + (size_t)G * 8, o_pred = o_feat + 16 * (size_t)G * 4;
   const size_t o_ev = o_pred + (size_t)G * 4, o_sli = o_ev + 16 * (size_t)G * 4;
@@ -445,6 +443,13 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   pred_ = reinterpret_cast<int32_t*>(r + o_pred);
   evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
   sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
+}
+
+// The head of a window: the accumulators reset, the next generation slot, the window's rows.
+void WindowEngine::run_begin(int b, hipStream_t st) {
+  set_buffer(b);
+  const int* counts = reinterpret_cast<const int*>(in_dev_[b]);
+  const int S = cfg_.span_cap, G = cfg_.group_cap;
   FillList fl{};
   auto add = [&](void* p, size_t bytes, uint32_t v) { fl.seg[fl.count++] = FillSeg{(uint32_t*)p, (uint32_t)(bytes / 4), v}; };
   add(hist_, kSlots * kBuckets * 4, 0);
@@ -462,9 +467,22 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   // + the next generation slot and the halo cut-offs (the finished window's tmax is read before
   // its reset), the ring state, no other GPUs' rows until merged, the window's rows
   launch_window_begin(fl, gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), ring_state_, remote_n_ + b,
-                      counts, N, rows_, st);
-  // the span branch in the one-GPU chain only: forked inside part 1's graph and joined before the
-  // exchange it measured 0.76 against 0.62 ms per window (one-rank rehearsal, bench.py --rccl-self)
+                      counts, n_rows_, rows_, st);
+}
+
+// The captured part of a window: everything between the DMA and the packet.
+// Part 1 of a window: accumulators, definitions, the decode of the window's records and the
+// halo it imported; with the GPU exchange, this window's trace-tagged rows for the others.
+void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
+  uint8_t* in = in_dev_[b];
+  const int* counts = reinterpret_cast<const int*>(in);
+  const int N = n_rows_;
+  if (!(xchg && xspan_)) run_begin(b, st);  // else its own launch (submit: part 4)
+  else set_buffer(b);
+  // the span branch in the one-GPU chain: forked inside the window's graph and joined before the
+  // probe. With the exchange, forked inside part 1's graph and joined before the exchange it
+  // measured 0.76 against 0.62 ms per window (bench.py --rccl-self); there the span side is a
+  // graph of its own on side_ instead (xspan_, submit: parts 4 and 3)
   if (branch_ && !xchg) run_span_branch(b, st);
   const TraceIds tt{trace_hash_, kTraceIdRows};
   launch_ring_defs(in + off_kern_, counts, cfg_.sig_cap, ctx_tab_, kCtxRows, pod_sn_, kPodRows, tt, ring_state_, st);
@@ -500,8 +518,9 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   // with the span branch: the signal bases are what the branch's probe work list waits for
   hipEvent_t sig_base = branched ? ev_sigbase_ : nullptr;
   // without the span branch: the span side first, so the signal scatter's launch can build the
-  // probe's work list next to it (it needs both sides' list offsets)
-  if (!branched) run_spans(b, st);
+  // probe's work list next to it (it needs both sides' list offsets); with the exchange and
+  // xspan_ the span side ran on side_ next to part 1 (submit: part 3)
+  if (!branched && !(xchg && xspan_)) run_spans(b, st);
   const uint32_t* wspan = branched ? nullptr : s_part_base_;
   const JoinParams* wjp = branched ? nullptr : &jp_;
   uint32_t* wlist = branched ? nullptr : probe_work_;
@@ -572,17 +591,21 @@ void WindowEngine::launch_part(int part, int b, int n_groups, bool with_labels, 
       run_part2(b, n_groups, with_labels, learn, compute_, false);
     } else if (part == 1) {
       run_part1(b, compute_, xchg);
-    } else {
+    } else if (part == 2) {
       run_part2(b, n_groups, with_labels, learn, compute_, xchg);
+    } else if (part == 3) {  // the exchange path's span side (xspan_)
+      run_spans(b, side_);
+    } else {  // part 4: the exchange path's window head (xspan_)
+      run_begin(b, compute_);
     }
   };
-  hipStream_t cs = compute_;  // the stream the part is captured on
+  hipStream_t cs = part == 3 ? side_ : compute_;  // the stream the part is captured on
   if (!cfg_.use_graphs) return run();
-  auto key = std::make_tuple(b * 4 + part, n_groups, with_labels, learn);
+  auto key = std::make_tuple(b * 8 + part, n_groups, with_labels, learn);
   auto it = graphs_.find(key);
-  if (it == graphs_.end() && !warm_[b * 4 + part]) {
+  if (it == graphs_.end() && !warm_[b * 8 + part]) {
     run();
-    warm_[b * 4 + part] = true;
+    warm_[b * 8 + part] = true;
     return;
   }
   if (it == graphs_.end()) {
@@ -694,6 +717,15 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   if (!xchg) {
     launch_part(0, b, n_groups, with_labels, learn, false);
   } else {
+    if (xspan_) {
+      // the window head, then the span side (decode, partition, sort: it reads only the span DMA
+      // and the reset accumulators) on side_ while part 1 decodes the records; joined before part 2
+      launch_part(4, b, n_groups, with_labels, learn, true);
+      HIPCHECK(hipEventRecord(ev_fork_, compute_));
+      HIPCHECK(hipStreamWaitEvent(side_, ev_fork_, 0));
+      launch_part(3, b, n_groups, with_labels, learn, true);
+      HIPCHECK(hipEventRecord(ev_spans_, side_));
+    }
     launch_part(1, b, n_groups, with_labels, learn, true);
     // the exchange sits between the window's two halves: every GPU's trace rows of THIS window
     if (injected) {  // rows as the other GPUs would have delivered them (tests, replays)
@@ -724,6 +756,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
       HIPCHECK(hipEventRecord(xchg_done_[b], comm_stream_));
       HIPCHECK(hipStreamWaitEvent(compute_, xchg_done_[b], 0));
     }
+    if (xspan_) HIPCHECK(hipStreamWaitEvent(compute_, ev_spans_, 0));
     launch_part(2, b, n_groups, with_labels, learn, true);
   }
   const auto tt = std::chrono::steady_clock::now();
