@@ -198,6 +198,9 @@ class AgentOptions:
     kfd_sampler: str = "auto"
     kfd_proc: str = "/sys/class/kfd/kfd/proc"
     model_signals: str = ""              # signals the node's sources produce (others marginalised; "" = all)
+    # application evidence (models/bayes.py AppEvidence): a group's retrieval time beyond the
+    # kernel-attributed share at least this long is elevated (<= 0: off)
+    retrieval_residual_ms: float = 100.0
     pair_prior: float = 0.0              # 2-fault prior mass added to a table model without pairs (0 = none)
     explicit_flags: Tuple[str, ...] = ()  # flags given on the command line (they win over the config's gpu: block)
 
@@ -548,6 +551,10 @@ class Agent:
         else:
             raise ValueError(f"--model {o.model} is learned: give --model-path (a file `attributor --train` wrote)")
         T = float(meta.get("temperature", 1.0))
+        if o.retrieval_residual_ms > 0:  # spans' retrieval breakdowns as application evidence
+            from ..models.bayes import AppEvidence
+
+            m.app = AppEvidence.expert(o.retrieval_residual_ms, temperature=T)
         if o.pair_prior > 0 and m.pairs is None:
             m = with_pairs(m, o.pair_prior, T)
             meta = dict(meta, pair_rho=o.pair_prior)
@@ -697,6 +704,9 @@ class Agent:
             top = ranked[0]
             ev = []
             for sname in top.evidence:
+                if sname == catalog.APP_RETRIEVAL_SIGNAL:  # application evidence (AppEvidence)
+                    ev.extend(self._retrieval_evidence(res, g))
+                    continue
                 spec = catalog.BY_NAME[sname]
                 v = feat_l[g][spec.slot]
                 ev.append(Evidence(spec.semconv or sname, round(v, 3) if math.isfinite(v) else "elevated", "ebpf"))
@@ -710,6 +720,23 @@ class Agent:
                 fault_hypotheses=[FaultHypothesis(p.domain, p.posterior, p.evidence) for p in ranked
                                   if p.posterior >= 0.01]))
         return out
+
+    @staticmethod
+    def _retrieval_evidence(res: dict, g: int) -> List[Evidence]:
+        """The application evidence of group g: its retrieval time beyond the kernel-attributed share
+        (source "application", REF incident-attribution.schema.json:41-56) and that share itself,
+        REF's llm.ebpf.retrieval.kernel_attributed_ms (DecomposeRetrieval, source "ebpf")."""
+        from ..contracts import semconv
+        from ..models.bayes import AppEvidence
+
+        app, feat = res.get("app"), res["feat"]
+        if app is None:
+            return [Evidence(catalog.APP_RETRIEVAL_SEMCONV, "elevated", "application")]
+        resid = float(AppEvidence.residual(app[g:g + 1], feat[g:g + 1])[0])
+        f = np.asarray(feat[g], dtype=np.float64)
+        kern = float(sum(f[s] for s in (0, 3, 5) if math.isfinite(f[s])))
+        return [Evidence(catalog.APP_RETRIEVAL_SEMCONV, round(max(resid, 0.0), 3), "application"),
+                Evidence(semconv.ATTR_RETRIEVAL_KERNEL_MS, round(kern, 3), "ebpf")]
 
     def _emit_window(self, prevs: List[dict], t_ns: int, G: int, names, ring, model) -> None:
         """One finished window, as every worker's part of it in rank order (worker.PrevJoiner):
@@ -828,6 +855,7 @@ class Agent:
         time window k is staged, become metrics and attributions while window k computes."""
         from ..collector import bpf
         from ..collector.records import EpochClock
+        from ..ops.engine import app_model_bytes
         from ..pipeline.window import Cut
         from ..safety import TreeCPUSampler
         from .worker import PrevJoiner, WorkerError, WorkerPool, WorkerSpec, groups_of
@@ -876,7 +904,8 @@ class Agent:
                             group_cap=max(1, groups_of(0, N, G)), user_cap=max(1024, o.window_events // 4),
                             window_ms=float(o.window_ms), ttft_slo_ms=o.ttft_slo_ms, halo_ms=o.halo_ms,
                             import_cap=icap, xchg_cap=xchg, model_image=np.asarray(image, np.uint8).tobytes(),
-                            pods=pods, master=("127.0.0.1", port), halo_windows=halo_windows, split=split)
+                            pods=pods, master=("127.0.0.1", port), halo_windows=halo_windows, split=split,
+                            app_image=app_model_bytes(model).tobytes() if model.app is not None else b"")
                  for r in range(N)]
         state = self._state_path()
         if state and os.path.exists(state):

@@ -78,6 +78,7 @@ class WorkerSpec:
     env: Dict[str, str] = field(default_factory=dict)
     halo_windows: int = 3       # earlier windows resident on the device for the halo
     split: bool = False         # split rings: this worker's own ring set (RingNames.of(ring_name, rank))
+    app_image: bytes = b""      # the application evidence model (ops/engine.py app_model_bytes); empty: off
 
 
 def groups_of(rank: int, world: int, n_groups: int) -> int:
@@ -90,7 +91,9 @@ def merge_results(parts: List[dict], n_groups: int) -> dict:
     (group g = local g // world of worker g % world)."""
     world = len(parts)
     out = {}
-    for key in ("post", "conf", "feat", "pred", "evbits", "sli"):
+    for key in ("post", "conf", "feat", "pred", "evbits", "sli", "app"):
+        if key not in parts[0]:
+            continue
         ref = np.asarray(parts[0][key])
         arr = np.zeros((n_groups,) + ref.shape[1:], dtype=ref.dtype)
         for r, p in enumerate(parts):
@@ -163,6 +166,12 @@ class WorkerCore:
                                     shared=shared and not spec.split)
         if spec.pods is not None:
             self.pipe.eng.set_pods(*spec.pods)
+        if spec.app_image:
+            from ..ops.engine import app_from_bytes
+
+            img = np.frombuffer(spec.app_image, dtype=np.uint8)
+            self.pipe.eng.set_app_model(img)
+            self.pipe.app = self.pipe.model.app = app_from_bytes(img)
         self.pending: Deque[Tuple[int, float, int]] = collections.deque()
         self.windows = 0
         self.collect_s = self.collect_wait_s = 0.0  # host time collecting finished windows / waiting for them

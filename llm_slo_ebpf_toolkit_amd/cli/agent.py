@@ -82,6 +82,11 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         ("model-signals", d.model_signals, "window engine: comma-separated signals this node's sources produce; "
                                            "the model sums the others out instead of reading their absence as "
                                            "'not elevated' (empty = every signal)"),
+        ("retrieval-residual-ms", d.retrieval_residual_ms, "window engine: application evidence -- an incident "
+                                                           "group whose spans' retrieval time (llm.slo.retrieval.*) "
+                                                           "exceeds the kernel-attributed share (dns + connect + "
+                                                           "TLS) by at least this is retrieval_backend evidence "
+                                                           "(<= 0 = off)"),
         ("pair-prior", d.pair_prior, "window engine: add 2-fault hypotheses with this prior mass to a table model "
                                      "(--model bayes | bayes_gpu; trained files carry their own)"),
         ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
@@ -137,7 +142,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         otlp_receiver_allow=a.otlp_receiver_allow, otlp_forwarders=a.otlp_forwarders, procfs_sampler=bool(a.procfs_sampler), procfs_pods=a.procfs_pods,
         procfs_interval_ms=int(a.procfs_interval_ms), procfs_cpu_psi=bool(a.procfs_cpu_psi),
         kfd_sampler=a.kfd_sampler,
-        model_signals=a.model_signals,
+        model_signals=a.model_signals, retrieval_residual_ms=float(a.retrieval_residual_ms),
         pair_prior=float(a.pair_prior), emit_wait_ms=int(a.emit_wait_ms), webhook_queue=int(a.webhook_queue),
         emit_min_burn=float(a.emit_min_burn), emit_min_requests=float(a.emit_min_requests),
         decision_log=a.decision_log,

@@ -18,7 +18,15 @@ engine DMAs from, with its identities mapped onto the ids the kernel side uses:
 * pid       -> ``process.pid``; connection -> (client port, server port, server IPv4) hashed
   like the probes' connection key (records.conn_hash);
 * incident group -> ``service.name`` (one group per service, ``GroupTable``);
-* SLI       -> ``llm.slo.ttft_ms`` (contracts/semconv.py) and the span duration.
+* SLI       -> ``llm.slo.ttft_ms`` (contracts/semconv.py) and the span duration;
+* retrieval -> ``retr_ms``: the request's ``llm.slo.retrieval.{vectordb,network,dns}_ms`` summed over
+  the spans of its trace (REF puts them on the ``chat.retrieval`` child span,
+  demo/rag-service/main.go:393-397). The engine turns it into application evidence: the group's
+  retrieval time beyond the kernel-attributed share (REF DecomposeRetrieval,
+  pkg/otel/processor/ebpfcorrelator/correlator.go:179-194; models/bayes.py AppEvidence). A child
+  span that arrives in an earlier export than its request span waits in a bounded table keyed by
+  trace (an OTel SDK exports spans as they end: children first); one that arrives after its
+  request span was pushed is not joined.
 
 The protobuf decoder is a minimal wire-format walker over the OTLP trace messages
 (ExportTraceServiceRequest / ResourceSpans / ScopeSpans / Span / KeyValue / AnyValue): no
@@ -27,6 +35,7 @@ generated code, no protobuf runtime.
 
 from __future__ import annotations
 
+import collections
 import http.server
 import ipaddress
 import json
@@ -41,6 +50,25 @@ from ..contracts import semconv
 from . import records
 
 TTFT_KEYS = (semconv.ATTR_SLO_TTFT_MS, "gen_ai.server.time_to_first_token", "llm.ttft_ms")
+RETRIEVAL_KEYS = (semconv.ATTR_RETRIEVAL_VECTORDB, semconv.ATTR_RETRIEVAL_NETWORK_MS, semconv.ATTR_RETRIEVAL_DNS_MS)
+
+
+def retrieval_ms(attrs: Dict[str, object]) -> Optional[float]:
+    """A span's application-reported retrieval time: its ``llm.slo.retrieval.*`` breakdown summed
+    (None without one). Non-numeric, negative or non-finite parts are ignored."""
+    tot, seen = 0.0, False
+    for k in RETRIEVAL_KEYS:
+        v = attrs.get(k)
+        if v is None or isinstance(v, bool):
+            continue
+        try:
+            f = float(v)
+        except (TypeError, ValueError):
+            continue
+        if f >= 0.0 and f < float("inf"):
+            tot += f
+            seen = True
+    return tot if seen else None
 
 
 def trace_hash(trace_id) -> int:
@@ -277,6 +305,10 @@ class SpanMapper:
         self._pods: Dict[int, int] = {}
         self._new: Dict[int, int] = {}
         self._plock = threading.Lock()
+        # retrieval breakdowns of traces whose request span has not arrived yet (bounded, oldest out)
+        self._retr: "collections.OrderedDict[int, float]" = collections.OrderedDict()
+        self._rlock = threading.Lock()
+        self.retrieval_cap = 8192
 
     def take_pod_updates(self) -> Optional[Tuple[np.ndarray, np.ndarray]]:
         """(pod ids, svc|node) learned since the last call, or None."""
@@ -305,6 +337,22 @@ class SpanMapper:
         another pod's records to its service), and with ``pod_ips`` a span naming a pod must come
         from that pod's address when the address is one of this node's pods."""
         sel = [(r, d) for r, d in spans if self.is_request_span(d)]
+        # the retrieval breakdowns of this export's spans, summed per trace
+        retr: Dict[int, float] = {}
+        for _r, d in spans:
+            v = retrieval_ms(d.get("attrs", {}))
+            if v is not None:
+                th = trace_hash(d.get("traceId"))
+                if th:
+                    retr[th] = retr.get(th, 0.0) + v
+        if retr:
+            req = {trace_hash(d.get("traceId")) for _r, d in sel}
+            with self._rlock:
+                for th, v in retr.items():
+                    if th not in req:  # its request span comes later: wait for it
+                        self._retr[th] = self._retr.pop(th, 0.0) + v
+                while len(self._retr) > self.retrieval_cap:
+                    self._retr.popitem(last=False)
         at_peer = None
         if self.pod_ips is not None and peer and not self._forwarder(peer):
             try:
@@ -313,7 +361,7 @@ class SpanMapper:
                 at_peer = None
         # per-field lists, written into the record array column by column at the end: setting the
         # fields of one structured element at a time cost ~18 us per span (the receiver's CPU)
-        ts, tr, sh, pids, pods, svcs, grps, ttft, lat, conn = ([] for _ in range(10))
+        ts, tr, sh, pids, pods, svcs, grps, ttft, lat, conn, rms = ([] for _ in range(11))
         res_cache: Dict[int, tuple] = {}  # one resource's service / pod / pid per request
         groups_seen: Dict[str, int] = {}
         pods_seen: Dict[object, int] = {}
@@ -352,8 +400,16 @@ class SpanMapper:
             sport = _first(a, ("client.port", "net.host.port", "net.sock.host.port")) or 0
             dport = _first(a, ("server.port", "net.peer.port", "net.sock.peer.port")) or 0
             v = _first(a, TTFT_KEYS)
+            th = trace_hash(d.get("traceId"))
+            rv = retr.get(th)
+            if self._retr and th:
+                with self._rlock:
+                    early = self._retr.pop(th, None)
+                if early is not None:
+                    rv = (rv or 0.0) + early
+            rms.append(rv if rv is not None else 0.0)
             ts.append(t0)
-            tr.append(trace_hash(d.get("traceId")))
+            tr.append(th)
             sh.append(span_hash(d.get("spanId")))
             pids.append(int(pid))
             pods.append(pid_)
@@ -379,6 +435,7 @@ class SpanMapper:
             out["ttft_ms"] = ttft
             out["latency_ms"] = lat
             out["conn_h"] = np.array(conn, dtype=np.uint64)
+            out["retr_ms"] = rms
         return out
 
 

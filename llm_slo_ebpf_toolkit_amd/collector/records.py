@@ -208,7 +208,11 @@ SPAN = np.dtype([
     ("ttft_ms", "<f4"),      # 40
     ("latency_ms", "<f4"),   # 44
     ("span_h", "<u8"),       # 48
-    ("reserved", "<u8"),     # 56
+    # 56 the request's retrieval time as the application reports it: REF's
+    # llm.slo.retrieval.{vectordb,network,dns}_ms summed (demo/rag-service/main.go:393-397);
+    # <= 0 / NaN = no breakdown (the application evidence of ops/csrc/posterior.hip)
+    ("retr_ms", "<f4"),
+    ("reserved", "<u4"),     # 60
 ])
 assert SPAN.itemsize == 64
 

@@ -401,13 +401,14 @@ class RagService:
         root_attrs.update(conn_attrs)
         if decision.tier:
             root_attrs["llm.ebpf.correlation_tier"] = decision.tier
+        # in the order an OTel SDK exports them: as they end, the children before the request
         self.spans.add([
-            SpanExporter.span(trace_id, root, "", "chat.request", t_req, t_end, root_attrs),
             SpanExporter.span(trace_id, rsp, root, "chat.retrieval", t_r0, t_r1, {
                 semconv.ATTR_RETRIEVAL_VECTORDB: float(vdb_ms),
                 semconv.ATTR_RETRIEVAL_NETWORK_MS: float(plan.network_ms),
                 semconv.ATTR_RETRIEVAL_DNS_MS: float(plan.dns_ms), "retrieval.selected_docs": len(docs)}),
             SpanExporter.span(trace_id, gsp, root, "chat.generation", t_r1, t_end, {"llm.tokens.count": g["tokens"]}),
+            SpanExporter.span(trace_id, root, "", "chat.request", t_req, t_end, root_attrs),
         ])
         return {"request_id": rid, "trace_id": trace_id, "profile": profile, "tokens": tokens, "documents": docs,
                 "ttft_ms": round(ttft_ms, 3), "tokens_per_sec": round(tps, 3), "retrieval_ms": round(ret_ms, 3),

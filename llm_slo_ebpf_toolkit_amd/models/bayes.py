@@ -69,10 +69,120 @@ class Posterior:
     evidence: List[str]
 
 
+APP_BIT = 16  # ops/csrc/mislo_launch.h kAppBit: the application evidence's bit in evbits
+
+
 @functools.lru_cache(maxsize=4096)
 def _evidence_names(bits: int) -> tuple:
-    """Signal names of an evidence bitmask over the 16 slots, sorted (REF's evidence order)."""
-    return tuple(sorted(catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if bits >> s & 1))
+    """Signal names of an evidence bitmask over the 16 slots (and the application bit), sorted
+    (REF's evidence order)."""
+    names = [catalog.SIGNAL_NAMES[s] for s in range(N_SLOTS) if bits >> s & 1]
+    if bits >> APP_BIT & 1:
+        names.append(catalog.APP_RETRIEVAL_SIGNAL)
+    return tuple(sorted(names))
+
+
+@dataclass
+class AppEvidence:
+    """Application-source evidence: one binary signal beside the 16 kernel slots (the device twin
+    is ops/csrc/mislo_launch.h ``AppModel``, evaluated inside the K3 posterior kernel).
+
+    The signal is an incident group's retrieval time that the kernel does not account for. It is
+    REF's ``DecomposeRetrieval`` (pkg/otel/processor/ebpfcorrelator/correlator.go:179-194) taken
+    to group level: the mean application-reported retrieval time of the group's spans (REF's
+    ``llm.slo.retrieval.{vectordb,network,dns}_ms``, demo/rag-service/main.go:393-397) minus the
+    kernel-attributed share, the group's mean joined dns + connect + TLS latency. REF's schema
+    lets such evidence come from the application (incident-attribution.schema.json:41-56).
+
+    A group none of whose spans carries a breakdown contributes nothing: the signal is summed out,
+    not read as "not elevated", so REF's rows score exactly as before. Otherwise the domain logit
+    gains ``log P(!e|d) + e * logit P(e|d)`` (at the model's temperature), e = residual >= threshold."""
+    p: Optional[np.ndarray]            # [D] P(residual elevated | domain)
+    threshold_ms: float = catalog.APP_RETRIEVAL_THRESHOLD_MS
+    temperature: float = 1.0
+    # the device image's terms as given (from_image: the CPU engine scores what the GPU would)
+    image_terms: Optional[Tuple[np.ndarray, ...]] = None
+
+    @staticmethod
+    def expert(threshold_ms: float = catalog.APP_RETRIEVAL_THRESHOLD_MS, temperature: float = 1.0) -> "AppEvidence":
+        p = np.array([catalog.APP_RETRIEVAL_LIKELIHOOD[d] for d in catalog.ALL_DOMAINS], dtype=np.float64)
+        return AppEvidence(p, float(threshold_ms), float(temperature))
+
+    @staticmethod
+    def from_image(w: np.ndarray, b: np.ndarray, w2: np.ndarray, b2: np.ndarray, thr_ms: float,
+                   dom_mask: int) -> "AppEvidence":
+        mask = np.array([(int(dom_mask) >> d) & 1 for d in range(len(w))], dtype=bool)
+        return AppEvidence(None, float(thr_ms), 1.0, (np.asarray(w, np.float64), np.asarray(b, np.float64),
+                                                      np.asarray(w2, np.float64), np.asarray(b2, np.float64), mask))
+
+    def evidence_mask(self, D: int) -> np.ndarray:
+        """[D] bool: domains whose evidence the elevated signal is (P(e|d) >= 0.5)."""
+        if self.image_terms is not None:
+            return self.image_terms[4][:D]
+        return self.p[:D] >= 0.5
+
+    def terms(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(w [D], b [D]): logit P(e|d) and log P(!e|d), divided by the temperature."""
+        if self.image_terms is not None:
+            return self.image_terms[0], self.image_terms[1]
+        pe, pn = clamp_likelihood(self.p), clamp_likelihood(1.0 - self.p)
+        return (np.log(pe) - np.log(pn)) / self.temperature, np.log(pn) / self.temperature
+
+    def pair_terms(self, pairs: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """The 2-fault columns' terms: noisy-OR of the members (``with_pairs``)."""
+        if self.image_terms is not None:
+            P = len(pairs)
+            return self.image_terms[2][:P], self.image_terms[3][:P]
+        pe = clamp_likelihood(self.p)
+        a, b = np.asarray(pairs)[:, 0], np.asarray(pairs)[:, 1]
+        q = clamp_likelihood(1.0 - (1.0 - pe[a]) * (1.0 - pe[b]))
+        qn = clamp_likelihood(1.0 - q)
+        return (np.log(q) - np.log(qn)) / self.temperature, np.log(qn) / self.temperature
+
+    @staticmethod
+    def residual(app_cnt: np.ndarray, feat: np.ndarray) -> np.ndarray:
+        """[G] residual ms (NaN: no breakdown) from the groups' [G, 2] counts (spans, sum in 10 us
+        units) and features, in the device's operation order (posterior.hip app_state)."""
+        cnt = np.asarray(app_cnt, dtype=np.uint32).reshape(-1, 2)
+        f = np.asarray(feat, dtype=np.float32).reshape(-1, N_SLOTS)
+        n = cnt[:, 0].astype(np.float64)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            mean = cnt[:, 1].astype(np.float64) / APP_UNITS_PER_MS / n
+        kern = np.zeros(len(n))
+        for s in (0, 3, 5):  # dns + connect + tls, in that order
+            v = f[:, s].astype(np.float64)
+            kern = kern + np.where(np.isnan(v), 0.0, v)
+        return np.where(n > 0, mean - kern, np.nan)
+
+    def state(self, app_cnt: np.ndarray, feat: np.ndarray) -> np.ndarray:
+        """[G] int: -1 absent, 0 present, 1 elevated."""
+        r = self.residual(app_cnt, feat)
+        with np.errstate(invalid="ignore"):
+            return np.where(np.isnan(r), -1, (r >= self.threshold_ms).astype(np.int64))
+
+
+APP_UNITS_PER_MS = 100.0  # ops/csrc/mislo_launch.h kAppUnitsPerMs (10 us fixed point)
+
+
+def app_counts(spans: np.ndarray, n_groups: int, mine: Optional[np.ndarray] = None,
+               groups: Optional[np.ndarray] = None) -> np.ndarray:
+    """[G, 2] uint32 application retrieval counts of a window's SPAN records, as k_decode_spans
+    accumulates them: spans with 0 < retr_ms < 1e7 (spans, rint(retr_ms * 100) summed, u32)."""
+    out = np.zeros((int(n_groups), 2), np.uint32)
+    if len(spans) == 0 or n_groups <= 0:
+        return out
+    r = np.asarray(spans["retr_ms"], dtype=np.float32)
+    g = np.asarray(spans["group_id"] if groups is None else groups, dtype=np.int64)
+    with np.errstate(invalid="ignore"):
+        ok = (r > np.float32(0)) & (r < np.float32(1e7)) & (g >= 0) & (g < n_groups)
+    if mine is not None:
+        ok &= mine
+    units = np.rint(r[ok].astype(np.float64) * APP_UNITS_PER_MS).astype(np.uint64)
+    np.add.at(out[:, 0], g[ok], np.uint32(1))
+    s = np.zeros(int(n_groups), np.uint64)
+    np.add.at(s, g[ok], units)
+    out[:, 1] = (s & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    return out
 
 
 @dataclass
@@ -91,6 +201,23 @@ class LinearPosteriorModel:
     pair_b: Optional[np.ndarray] = None
     pairs: Optional[np.ndarray] = None
     pair_rho: float = 0.0
+    # application evidence (AppEvidence); the methods below take the groups' states (-1/0/1,
+    # AppEvidence.state) as ``app``
+    app: Optional[AppEvidence] = None
+
+    def _app_add(self, app: Optional[np.ndarray], B: int) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
+        """(single [B, D], pair [B, P]) logit terms of the application evidence, or None."""
+        if self.app is None or app is None:
+            return None, None
+        st = np.asarray(app, dtype=np.int64).reshape(-1)[:B]
+        w, b = self.app.terms()
+        pres = (st >= 0)[:, None]
+        add = np.where(pres, b[None, :self.weights.shape[1]] + np.where((st == 1)[:, None], w[None, :self.weights.shape[1]], 0.0), 0.0)
+        add2 = None
+        if self.pairs is not None:
+            w2, b2 = self.app.pair_terms(self.pairs)
+            add2 = np.where(pres, b2[None, :] + np.where((st == 1)[:, None], w2[None, :], 0.0), 0.0)
+        return add, add2
 
     def features(self, values: np.ndarray) -> np.ndarray:
         """values: [B, 16] with NaN for absent signals -> model features X [B, 16]."""
@@ -116,52 +243,65 @@ class LinearPosteriorModel:
             e &= self.table_mask[None, :].astype(bool)
         return e
 
-    def logits(self, values: np.ndarray) -> np.ndarray:
-        return self.features(values) @ self.weights + self.bias[None, :]
+    def logits(self, values: np.ndarray, app: Optional[np.ndarray] = None) -> np.ndarray:
+        lg = self.features(values) @ self.weights + self.bias[None, :]
+        add, _ = self._app_add(app, lg.shape[0])
+        return lg if add is None else lg + add
 
-    def hypothesis_posteriors(self, values: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    def hypothesis_posteriors(self, values: np.ndarray, app: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
         """(P(single d) [B, D], P(pair h) [B, P]) -- the normalised hypothesis distribution (no
         pairs: [B, 0])."""
         x = self.features(values)
         lg = x @ self.weights + self.bias[None, :]
         l2 = (x @ self.pair_w + self.pair_b[None, :]) if self.pairs is not None else np.zeros((lg.shape[0], 0))
+        add, add2 = self._app_add(app, lg.shape[0])
+        if add is not None:
+            lg = lg + add
+            if add2 is not None:
+                l2 = l2 + add2
         allv = np.concatenate([lg, l2], axis=1)
         m = np.max(allv, axis=1, keepdims=True)
         with np.errstate(invalid="ignore"):
             z = m + np.log(np.sum(np.exp(allv - m), axis=1, keepdims=True))
         return np.exp(lg - z), np.exp(l2 - z)
 
-    def posteriors(self, values: np.ndarray) -> np.ndarray:
+    def posteriors(self, values: np.ndarray, app: Optional[np.ndarray] = None) -> np.ndarray:
         """Per domain: the posterior (single-fault model) or the marginal P(d in the incident)
         (2-fault model)."""
         if self.pairs is None:
-            lg = self.logits(values)
+            lg = self.logits(values, app)
             m = np.max(lg, axis=1, keepdims=True)
             with np.errstate(invalid="ignore"):
                 ex = np.exp(lg - m)
             z = m + np.log(np.sum(ex, axis=1, keepdims=True))
             return np.exp(lg - z)
-        p1, p2 = self.hypothesis_posteriors(values)
+        p1, p2 = self.hypothesis_posteriors(values, app)
         marg = p1.copy()
         for h, (a, b) in enumerate(self.pairs.tolist()):
             marg[:, a] += p2[:, h]
             marg[:, b] += p2[:, h]
         return marg
 
-    def predict(self, values: np.ndarray) -> np.ndarray:
+    def predict(self, values: np.ndarray, app: Optional[np.ndarray] = None) -> np.ndarray:
         """Top-1 domain: argmax of the logits (single-fault) or of the marginals (2-fault);
         ties -> the lowest domain index, as the kernel."""
         if self.pairs is None:
-            return np.argmax(self.logits(values), axis=1)
-        return np.argmax(self.posteriors(values), axis=1)
+            return np.argmax(self.logits(values, app), axis=1)
+        return np.argmax(self.posteriors(values, app), axis=1)
 
-    def evidence_bits(self, values: np.ndarray) -> np.ndarray:
-        """[B, D] uint32 bitmask over slots: elevated & P(elevated|d) >= 0.5."""
+    def evidence_bits(self, values: np.ndarray, app: Optional[np.ndarray] = None) -> np.ndarray:
+        """[B, D] uint32 bitmask over slots: elevated & P(elevated|d) >= 0.5; bit APP_BIT: the
+        application evidence elevated & P(e|d) >= 0.5."""
         e = self.elevated(values)
-        bits = np.zeros((e.shape[0], self.weights.shape[1]), dtype=np.uint32)
+        D = self.weights.shape[1]
+        bits = np.zeros((e.shape[0], D), dtype=np.uint32)
         for s in range(N_SLOTS):
             col = e[:, s:s + 1] & self.evidence_mask[s][None, :]
             bits |= (col.astype(np.uint32) << np.uint32(s))
+        if self.app is not None and app is not None:
+            st = np.asarray(app, dtype=np.int64).reshape(-1)[:e.shape[0]]
+            col = (st == 1)[:, None] & self.app.evidence_mask(D)[None, :]
+            bits |= (col.astype(np.uint32) << np.uint32(APP_BIT))
         return bits
 
     def attribute(self, signals: Dict[str, float]) -> List[Posterior]:
@@ -338,6 +478,8 @@ def with_temperature(m: LinearPosteriorModel, temperature: float) -> LinearPoste
     if m.pairs is not None:
         out.pair_w, out.pairs, out.pair_rho = m.pair_w * inv, m.pairs.copy(), m.pair_rho
         out.pair_b = np.where(np.isfinite(m.pair_b), m.pair_b * inv, m.pair_b)
+    if m.app is not None and m.app.p is not None:
+        out.app = AppEvidence(m.app.p.copy(), m.app.threshold_ms, m.app.temperature * float(temperature))
     return out
 
 
@@ -386,6 +528,7 @@ def with_pairs(m: LinearPosteriorModel, rho: float, temperature: float = 1.0) ->
     out = LinearPosteriorModel(m.name, m.weights.copy(), bias, m.evidence_mask.copy(), m.feature_mode,
                                m.thresholds.copy(), None, None if m.table_mask is None else m.table_mask.copy())
     out.pair_w, out.pair_b, out.pairs, out.pair_rho = pw, pb, np.array(PAIR_LIST, dtype=np.int64), float(rho)
+    out.app = m.app
     return out
 
 
@@ -437,6 +580,8 @@ def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature:
         for d in range(W.shape[1]):
             if d == u or not fin[d]:
                 continue
+            if m.app is not None and m.app.p is not None and m.app.p[d] >= 0.5 and m.app.p[d] >= 2.0 * m.app.p[u]:
+                continue  # the application evidence indicates it (AppEvidence)
             if not np.any((p[obs, d] >= 0.5) & (p[obs, d] >= 2.0 * p[obs, u])):
                 b[d] = NEG_INF
                 if pb is not None:
@@ -444,6 +589,7 @@ def marginalize(m: LinearPosteriorModel, observable: Sequence[str], temperature:
     out = LinearPosteriorModel(m.name, W, b, mask, m.feature_mode, m.thresholds.copy(), None, table)
     if pw is not None:
         out.pair_w, out.pair_b, out.pairs, out.pair_rho = pw, pb, m.pairs.copy(), m.pair_rho
+    out.app = m.app
     return out
 
 

@@ -137,7 +137,8 @@ class PyEngine {
                                         reinterpret_cast<const float*>(p + o_feat),
                                         reinterpret_cast<const int32_t*>(p + o_pred),
                                         reinterpret_cast<const uint32_t*>(p + o_ev),
-                                        reinterpret_cast<const uint32_t*>(p + o_sli)},
+                                        reinterpret_cast<const uint32_t*>(p + o_sli),
+                                        reinterpret_cast<const uint32_t*>(p + o_sli) + 2 * G},
                              n_groups));
     }
     return out;
@@ -151,6 +152,7 @@ class PyEngine {
     d["pred"] = copy_array(r.pred, {G});
     d["evbits"] = copy_array(r.evbits, {G, 16});
     d["sli"] = copy_array(r.sli, {G, 2});
+    d["app"] = copy_array(r.app, {G, 2});
     return d;
   }
   py::tuple window_ms(int64_t k) {
@@ -164,12 +166,16 @@ class PyEngine {
   void set_model_bytes(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
     e_->set_model_bytes(b.data(), (size_t)b.size());
   }
+  void set_app_model(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
+    e_->set_app_model(b.data(), (size_t)b.size());
+  }
   void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom) {
     eng().set_refit(alpha, prior_pseudo, inv_temp, min_count, cap_dom);
   }
   void refit_now() { eng().refit_now(); }
   // K3 on given features (REF's 55 rows, offline evaluation) with the model on the device
-  py::dict score(py::array_t<float, py::array::c_style | py::array::forcecast> feat, py::object labels) {
+  py::dict score(py::array_t<float, py::array::c_style | py::array::forcecast> feat, py::object labels,
+                 py::object app) {
     if (feat.ndim() != 2 || feat.shape(1) != 16) throw std::invalid_argument("feat must be float32 [n, 16]");
     const int n = (int)feat.shape(0);
     std::vector<int32_t> lab;
@@ -178,13 +184,19 @@ class PyEngine {
       if (a.size() != n) throw std::invalid_argument("labels must have n entries");
       lab.assign(a.data(), a.data() + n);
     }
+    std::vector<uint32_t> appc;
+    if (!app.is_none()) {
+      auto a = app.cast<py::array_t<uint32_t, py::array::c_style | py::array::forcecast>>();
+      if (a.size() != 2 * (py::ssize_t)n) throw std::invalid_argument("app must be uint32 [n, 2]");
+      appc.assign(a.data(), a.data() + 2 * (size_t)n);
+    }
     std::vector<double> post((size_t)n * 16), conf(n);
     std::vector<int32_t> pred(n);
     std::vector<uint32_t> ev((size_t)n * 16), cm(256);
     {
       py::gil_scoped_release nogil;
       eng().score_features(feat.data(), n, lab.empty() ? nullptr : lab.data(), post.data(), pred.data(), conf.data(),
-                           ev.data(), cm.data());
+                           ev.data(), cm.data(), appc.empty() ? nullptr : appc.data());
     }
     py::dict d;
     d["post"] = copy_array(post.data(), {n, 16});
@@ -317,6 +329,8 @@ PYBIND11_MODULE(_mislo_agent, m) {
   m.attr("STATS_OFF") = kStatsOff;
   m.attr("STATS_LEN") = kStatsLen;
   m.attr("POSTERIOR_MODEL_BYTES") = (int64_t)sizeof(PosteriorModel);
+  m.attr("APP_MODEL_BYTES") = (int64_t)sizeof(AppModel);
+  m.attr("APP_EVIDENCE_BIT") = kAppBit;
   m.attr("CTX_ROWS") = kCtxRows;
   m.attr("REC_STRIDE") = kRecStride;
   m.attr("SIGREC_BYTES") = (int)sizeof(SigRec);
@@ -348,12 +362,13 @@ PYBIND11_MODULE(_mislo_agent, m) {
         return p.eng().copy_ms(k);
       })
       .def("set_model_bytes", &PyEngine::set_model_bytes)
+      .def("set_app_model", &PyEngine::set_app_model)
       .def("set_p0", &PyEngine::set_p0)
       .def("set_refit", &PyEngine::set_refit, py::arg("alpha") = 2.0, py::arg("prior_pseudo") = 1.0,
            py::arg("inv_temp") = 1.0, py::arg("min_count") = 0.0, py::arg("cap_dom") = -1)
       .def("refit_now", &PyEngine::refit_now)
       .def("set_device_refit", [](PyEngine& p, bool on) { p.eng().set_device_refit(on); })
-      .def("score", &PyEngine::score, py::arg("feat"), py::arg("labels") = py::none())
+      .def("score", &PyEngine::score, py::arg("feat"), py::arg("labels") = py::none(), py::arg("app") = py::none())
       .def("set_pods", &PyEngine::set_pods)
       .def("inject_remote", &PyEngine::inject_remote)
       .def("results_all", &PyEngine::results_all)

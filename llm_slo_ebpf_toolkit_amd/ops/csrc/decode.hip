@@ -648,10 +648,14 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   // per-incident SLO counts privatised in LDS: a window's spans all land on its few groups, so
   // global atomics serialised on a handful of L2 addresses (33 us per 16K-span window)
   __shared__ uint32_t s_sli[2 * kSliLds];
+  __shared__ uint32_t s_app[2 * kSliLds];  // application retrieval: spans, sum (10 us units)
   const bool sli_lds = sm.grp_sli && sm.n_groups <= kSliLds;
+  const bool app_lds = sm.grp_app && sm.n_groups <= kSliLds;
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
   if (sli_lds)
     for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT) s_sli[i] = 0;
+  if (app_lds)
+    for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT) s_app[i] = 0;
   __syncthreads();
   const int n = min(*n_ptr, cap);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -691,6 +695,13 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
         atomicAdd(&sli[2 * grp], 1u);
         if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sli[2 * grp + 1], 1u);
       }
+      // the application's retrieval time of the request (REF DecomposeRetrieval's input,
+      // correlator.go:179-194): its group sum, in fixed point like every incident sum
+      if (mine && sm.grp_app && grp < (uint32_t)sm.n_groups && s.retr_ms > 0.f && s.retr_ms < 1e7f) {
+        uint32_t* app = app_lds ? s_app : sm.grp_app;
+        atomicAdd(&app[2 * grp], 1u);
+        atomicAdd(&app[2 * grp + 1], (uint32_t)rint((double)s.retr_ms * kAppUnitsPerMs));
+      }
       r.pod = s.pod_id;
       r.pid = s.pid;
       r.sn = ((uint32_t)s.svc_id << 16) | s.node_id;
@@ -725,6 +736,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   if (sli_lds)
     for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT)
       if (s_sli[i]) atomicAdd(&sm.grp_sli[i], s_sli[i]);
+  if (app_lds)
+    for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT)
+      if (s_app[i]) atomicAdd(&sm.grp_app[i], s_app[i]);
 }
 
 // Event decoders run 1024 threads per workgroup: the grid is capped at kPartBlocks (the

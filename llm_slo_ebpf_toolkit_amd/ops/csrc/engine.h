@@ -88,6 +88,7 @@ struct ResultView {
   const int32_t* pred;    // [G]
   const uint32_t* evbits; // [G][16]
   const uint32_t* sli;    // [G][2]: spans, TTFT-SLO breaches
+  const uint32_t* app;    // [G][2]: spans with an application retrieval time, its sum (10 us units)
 };
 
 // The window's inputs: ring byte ranges (as the rings hold them) and the window metadata.
@@ -138,8 +139,12 @@ class WindowEngine {
   // Score n incidents' features [n][16] with the model on the device (the K3 posterior kernel;
   // synchronous, drains the engine first): post [n][16], pred [n], conf [n], evbits [n][16], and
   // the confusion of labels (label_code, may be null) x predictions [16][16].
+  // app_cnt (optional, [n][2]): the incidents' application retrieval counts for the application
+  // evidence (set_app_model)
   void score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred, double* conf,
-                      uint32_t* evbits, uint32_t* confusion);
+                      uint32_t* evbits, uint32_t* confusion, const uint32_t* app_cnt = nullptr);
+  // the application evidence model (mislo_launch.h AppModel), stream-ordered before the next window
+  void set_app_model(const void* bytes, size_t n);
   // device refit: [16 x 16] Beta-prior table, optionally followed by a [16 x 16] likelihood floor
   void set_p0(const double* p0, size_t n);
   void set_pods(const uint32_t* pods, const uint32_t* svcnode, size_t n);  // pod metadata (stream-ordered)
@@ -215,6 +220,8 @@ class WindowEngine {
   uint32_t *pod_sn_ = nullptr, *pod_host_ = nullptr, *ring_state_ = nullptr;
   unsigned long long* trace_hash_ = nullptr;  // kernel trace id -> hash
   uint32_t* sli_ = nullptr;
+  uint32_t* app_ = nullptr;         // this buffer's [G][2] application retrieval counts (after sli_)
+  AppModel* app_dev_ = nullptr;     // the application evidence model (device)
   // other GPUs' rows: per buffer, imported after this window's records; counts per buffer
   int n_rows_ = 0;                 // rows per generation = sig_cap + import_cap
   int gens_ = 1;                   // resident generations (1 + halo_windows with a halo)

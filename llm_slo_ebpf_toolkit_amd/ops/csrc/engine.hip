@@ -220,10 +220,10 @@ void WindowEngine::alloc() {
   }
   warm_.assign(8 * nb_, false);
   // per-incident results block: [post G*16 f64][gconf G f64][feat G*16 f32][pred G i32][evbits G*16 u32]
-  // [sli G*2 u32]
+  // [sli G*2 u32][app G*2 u32]
   const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
   const size_t o_sli = o_ev + 16 * G * 4;
-  res_bytes_ = o_sli + 2 * G * 4;
+  res_bytes_ = o_sli + 4 * G * 4;
   for (int b = 0; b < nb_; ++b) {
     res_host_.push_back(static_cast<uint8_t*>(host_block(res_bytes_)));
   }
@@ -280,6 +280,8 @@ void WindowEngine::alloc() {
   HIPCHECK(hipMemset(p0_, 0, 2 * kSlots * 16 * sizeof(double)));
   model_dev_ = dalloc<uint8_t>(sizeof(PosteriorModel));
   HIPCHECK(hipMemset(model_dev_, 0, sizeof(PosteriorModel)));
+  app_dev_ = dalloc<AppModel>(1);
+  HIPCHECK(hipMemset(app_dev_, 0, sizeof(AppModel)));  // on = 0: no application evidence until set
   for (int i = 0; i < max_ahead_ + 2; ++i) {
     void* h = nullptr;
     HIPCHECK(hipHostMalloc(&h, sizeof(PosteriorModel), hipHostMallocDefault));
@@ -354,7 +356,7 @@ WindowEngine::~WindowEngine() {
                   g_part_tot_, g_part_base_, g_items_, g_rec_, s_part_, s_part_blk_, s_part_off_, s_part_tot_,
                   s_part_base_, s_items_, s_rec_, probe_work_, top3_, cnt_, attrs_, conf_, kernel_ms_, gsum_, gcnt_,
                   hist_, status_, misc_, dbg_, confusion_, stats_, stats_count_, pod_sn_, ring_state_, trace_hash_,
-                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, sel_mask_, xsend_, xrecv_, g_keys_, gen_, s_pre_};
+                  rows_, tmax_, remote_n_, sel_cnt_, sel_off_, sel_mask_, xsend_, xrecv_, g_keys_, gen_, s_pre_, app_dev_};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (copy_ && copy_ != compute_) hipStreamDestroy(copy_);
@@ -443,6 +445,7 @@ void WindowEngine::set_buffer(int b) {
   pred_ = reinterpret_cast<int32_t*>(r + o_pred);
   evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
   sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
+  app_ = sli_ + 2 * (size_t)G;
 }
 
 // The head of a window: the accumulators reset, the next generation slot, the window's rows.
@@ -463,7 +466,7 @@ void WindowEngine::run_begin(int b, hipStream_t st) {
   add(cnt_, (size_t)S * 4, 0);
   add(gsum_, (size_t)kGroupStripes * G * kSlots * 8, 0);
   add(gcnt_, (size_t)kGroupStripes * G * kSlots * 4, 0);
-  add(sli_, (size_t)G * 2 * 4, 0);
+  add(sli_, (size_t)G * 4 * 4, 0);  // + the application retrieval counts (app_) behind it
   // + the next generation slot and the halo cut-offs (the finished window's tmax is read before
   // its reset), the ring state, no other GPUs' rows until merged, the window's rows
   launch_window_begin(fl, gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), ring_state_, remote_n_ + b,
@@ -543,10 +546,10 @@ void WindowEngine::run_part2(int b, int n_groups, bool with_labels, bool learn, 
   const PosteriorModel* pm = reinterpret_cast<const PosteriorModel*>(model_dev_);
   if (learn)
     launch_posterior_stats(feat_, counts + 2, G, pm, with_labels ? labels : nullptr, post_, pred_, gconf_, evbits_,
-                           confusion_, labels, nullptr, stats_, stats_count_, st);
+                           confusion_, labels, nullptr, stats_, stats_count_, st, app_dev_, app_);
   else
     launch_posterior(feat_, counts + 2, G, pm, with_labels ? labels : nullptr, post_, pred_, gconf_, evbits_,
-                     confusion_, st);
+                     confusion_, st, app_dev_, app_);
   if (!comm_) {  // one GPU: the whole tail here (see k_window_end)
     const size_t res16 = (res_bytes_ + 15) / 16;
     const int g = (int)std::max<size_t>((kPacketLen + 255) / 256, std::min<size_t>(64, (res16 + 255) / 256));
@@ -565,7 +568,7 @@ void WindowEngine::run_spans(int b, hipStream_t st) {
   uint8_t* in = in_dev_[b];
   const int* counts = reinterpret_cast<const int*>(in);
   const int S = cfg_.span_cap, G = cfg_.group_cap;
-  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_};
+  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_, app_};
   launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
@@ -816,7 +819,8 @@ ResultView WindowEngine::results(int64_t k) const {
   const size_t o_sli = o_ev + 16 * G * 4;
   return ResultView{reinterpret_cast<const double*>(r), reinterpret_cast<const double*>(r + o_gconf),
                     reinterpret_cast<const float*>(r + o_feat), reinterpret_cast<const int32_t*>(r + o_pred),
-                    reinterpret_cast<const uint32_t*>(r + o_ev), reinterpret_cast<const uint32_t*>(r + o_sli)};
+                    reinterpret_cast<const uint32_t*>(r + o_ev), reinterpret_cast<const uint32_t*>(r + o_sli),
+                    reinterpret_cast<const uint32_t*>(r + o_sli) + 2 * G};
 }
 
 std::vector<float> WindowEngine::copy_ms(int64_t k) {
@@ -846,6 +850,14 @@ void WindowEngine::set_model_bytes(const void* bytes, size_t n) {
   HIPCHECK(hipMemcpyAsync(model_dev_, h, n, hipMemcpyHostToDevice, compute_));
 }
 
+void WindowEngine::set_app_model(const void* bytes, size_t n) {
+  if (n != sizeof(AppModel)) throw std::invalid_argument("application model must be APP_MODEL_BYTES bytes");
+  uint8_t* h = model_host_[model_slot_++ % model_host_.size()];  // pinned slots hold a PosteriorModel
+  static_assert(sizeof(AppModel) <= sizeof(PosteriorModel), "the staging slots fit the application model");
+  std::memcpy(h, bytes, n);
+  HIPCHECK(hipMemcpyAsync(app_dev_, h, n, hipMemcpyHostToDevice, compute_));
+}
+
 void WindowEngine::set_p0(const double* p0, size_t n) {
   if (n != (size_t)kSlots * 16 && n != 2 * (size_t)kSlots * 16) throw std::invalid_argument("p0 must be f64[256] or [512]");
   HIPCHECK(hipMemset(p0_ + kSlots * 16, 0, kSlots * 16 * sizeof(double)));  // [256]: no floor
@@ -869,24 +881,28 @@ void WindowEngine::refit_now() {
 }
 
 void WindowEngine::score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred,
-                                  double* conf, uint32_t* evbits, uint32_t* confusion) {
+                                  double* conf, uint32_t* evbits, uint32_t* confusion, const uint32_t* app_cnt) {
   if (n < 0) throw std::invalid_argument("n");
   sync();
   if (n == 0) return;
-  // one scratch block: [n][16] f32 features | n | labels | post | pred | conf | evbits | confusion
+  // one scratch block: [n][16] f32 features | n | labels | post | pred | conf | evbits | confusion |
+  // application counts [n][2]
   const size_t o_n = (size_t)n * 16 * 4, o_lab = o_n + 64, o_post = (o_lab + (size_t)n * 4 + 63) & ~size_t(63);
   const size_t o_pred = o_post + (size_t)n * 16 * 8, o_conf = (o_pred + (size_t)n * 4 + 63) & ~size_t(63);
-  const size_t o_ev = o_conf + (size_t)n * 8, o_cm = o_ev + (size_t)n * 16 * 4, bytes = o_cm + 16 * 16 * 4;
+  const size_t o_ev = o_conf + (size_t)n * 8, o_cm = o_ev + (size_t)n * 16 * 4, o_app = o_cm + 16 * 16 * 4;
+  const size_t bytes = o_app + (size_t)n * 2 * 4;
   uint8_t* d = dalloc<uint8_t>(bytes);
   HIPCHECK(hipMemset(d, 0, bytes));
   HIPCHECK(hipMemcpy(d, feat, o_n, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(d + o_n, &n, sizeof(int), hipMemcpyHostToDevice));
   if (labels) HIPCHECK(hipMemcpy(d + o_lab, labels, (size_t)n * 4, hipMemcpyHostToDevice));
+  if (app_cnt) HIPCHECK(hipMemcpy(d + o_app, app_cnt, (size_t)n * 2 * 4, hipMemcpyHostToDevice));
   launch_posterior(reinterpret_cast<const float*>(d), reinterpret_cast<const int*>(d + o_n), n,
                    reinterpret_cast<const PosteriorModel*>(model_dev_),
                    labels ? reinterpret_cast<const int32_t*>(d + o_lab) : nullptr, reinterpret_cast<double*>(d + o_post),
                    reinterpret_cast<int32_t*>(d + o_pred), reinterpret_cast<double*>(d + o_conf),
-                   reinterpret_cast<uint32_t*>(d + o_ev), reinterpret_cast<uint32_t*>(d + o_cm), compute_);
+                   reinterpret_cast<uint32_t*>(d + o_ev), reinterpret_cast<uint32_t*>(d + o_cm), compute_,
+                   app_cnt ? app_dev_ : nullptr, app_cnt ? reinterpret_cast<const uint32_t*>(d + o_app) : nullptr);
   HIPCHECK(hipStreamSynchronize(compute_));
   HIPCHECK(hipMemcpy(post, d + o_post, (size_t)n * 16 * 8, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(pred, d + o_pred, (size_t)n * 4, hipMemcpyDeviceToHost));

@@ -105,7 +105,9 @@ struct __attribute__((packed)) RefEvent {
 };
 static_assert(sizeof(RefEvent) == 40, "RefEvent must be 40 bytes");
 
-// 64-byte span record (collector/records.py SPAN).
+// 64-byte span record (collector/records.py SPAN). retr_ms: the request's retrieval time as the
+// application reports it (REF's llm.slo.retrieval.{vectordb,network,dns}_ms summed,
+// demo/rag-service/main.go:393-397); <= 0 or NaN = no breakdown.
 struct alignas(64) Span {
   int64_t ts_ns;
   uint64_t trace_h, conn_h;
@@ -113,7 +115,9 @@ struct alignas(64) Span {
   uint16_t node_id, svc_id;
   uint32_t group_id;
   float ttft_ms, latency_ms;
-  uint64_t span_h, reserved;
+  uint64_t span_h;
+  float retr_ms;
+  uint32_t reserved;
 };
 static_assert(sizeof(Span) == 64, "Span must be 64 bytes");
 // 20-byte span record (collector/records.py SPAN20, runtime/csrc/records.h Span20): the fields the

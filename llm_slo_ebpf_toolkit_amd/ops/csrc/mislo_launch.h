@@ -31,6 +31,24 @@ struct PosteriorModel {
   uint8_t pair_b[kMaxPairs];
 };
 
+// Application evidence (models/bayes.py AppEvidence): one more binary signal next to the 16 slots,
+// the incident group's retrieval time that the kernel signals do not account for -- REF's
+// DecomposeRetrieval (ebpfcorrelator/correlator.go:179-194) at group level: the mean application
+// retrieval time of the group's spans (SpanMap::grp_app) minus the kernel-attributed share, the
+// group's mean joined dns + connect + TLS latency (feature slots 0, 3, 5). A group without an
+// application breakdown contributes nothing (the signal is summed out, so REF's 55 rows score
+// exactly as before); otherwise elevated = residual >= thr_ms adds w[d] and present adds b[d].
+constexpr int kAppBit = 16;  // its evidence bit in evbits (bits 0-15: the signal slots)
+struct AppModel {
+  double w[kMaxDomains];   // (log P(e|d) - log P(!e|d)) / T
+  double b[kMaxDomains];   // log P(!e|d) / T
+  double w2[kMaxPairs];    // the 2-fault columns' noisy-OR terms
+  double b2[kMaxPairs];
+  double thr_ms;           // elevated threshold of the residual (ms)
+  uint32_t dom_mask;       // domains with P(e|d) >= 0.5 (evidence)
+  int32_t on;              // 0: the channel is off
+};
+
 // decode.hip
 void set_tables(const Tables* host_tables);
 int decode_grid(int cap);
@@ -53,7 +71,11 @@ struct SpanMap {
   float ttft_slo_ms;
   int sh_rank = 0, sh_world = 1;  // group sharding: this GPU keeps groups g % sh_world == sh_rank as g / sh_world
   GenMeta* gen = nullptr;         // receives the spans' time range (probe pruning of older generations)
+  // [n_groups][2]: spans carrying an application retrieval time (Span::retr_ms > 0), and the sum
+  // of those times in kAppUnitsPerMs units (exact integers: order-free, all-reducible)
+  uint32_t* grp_app = nullptr;
 };
+constexpr double kAppUnitsPerMs = 100.0;  // 10 us: a u32 group sum holds 42,949 s of retrieval per window
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,
                          const uint32_t* ctx_tab, int n_ctx, hipStream_t stream, const SpanMap* sm = nullptr);
 // native engine window: framed BPF ring records (counts[15] of them) + 64-byte user records
@@ -161,16 +183,18 @@ void launch_finalize(const int* ns_dev, int span_cap, const unsigned long long* 
 void launch_group_features(int n_groups, const unsigned long long* gsum, const uint32_t* gcnt, float* feat, hipStream_t stream);
 
 // posterior.hip
+// app / app_cnt (optional): the application evidence model and the groups' [G][2] retrieval counts
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                       double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
-                      hipStream_t stream);
+                      hipStream_t stream, const AppModel* app = nullptr, const uint32_t* app_cnt = nullptr);
 void launch_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                   const float* weights, double* out, double* count, hipStream_t stream);
 
 void launch_posterior_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm,
                             const int32_t* labels, double* post, int32_t* pred, double* conf, uint32_t* evbits,
                             uint32_t* confusion, const int32_t* stat_labels, const float* weights, double* out,
-                            double* count, hipStream_t stream);
+                            double* count, hipStream_t stream, const AppModel* app = nullptr,
+                            const uint32_t* app_cnt = nullptr);
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
                      PosteriorModel* pm, hipStream_t stream, double inv_temp = 1.0, double min_count = 0.0,
                      const double* floor_tab = nullptr, int cap_dom = -1);

@@ -62,7 +62,26 @@ struct PosteriorArgs {
   double *post, *conf;
   int32_t* pred;
   uint32_t *evbits, *confusion;
+  const AppModel* app;      // optional application evidence (mislo_launch.h)
+  const uint32_t* app_cnt;  // [G][2] the groups' application retrieval counts
 };
+
+// Application evidence of row r: -1 absent (no span of the group reported a retrieval time), 0
+// present, 1 elevated. The residual is computed in double from the exact group sum and the float
+// features, in the order models/bayes.py AppEvidence.residual uses, so host and device agree
+// bit for bit.
+__device__ __forceinline__ int app_state(const uint32_t* __restrict__ cnt, const float* __restrict__ feat, int r,
+                                         double thr_ms) {
+  const uint32_t n = cnt[2 * r];
+  if (n == 0) return -1;
+  const double mean = (double)cnt[2 * r + 1] / kAppUnitsPerMs / (double)n;
+  const float* f = feat + (size_t)r * kSlots;
+  double kern = 0.0;  // REF DecomposeRetrieval: dns + connect + tls
+  if (f[0] == f[0]) kern += (double)f[0];
+  if (f[3] == f[3]) kern += (double)f[3];
+  if (f[5] == f[5]) kern += (double)f[5];
+  return (mean - kern) >= thr_ms ? 1 : 0;
+}
 struct StatsArgs {
   const float* feat;
   const int* ng_ptr;
@@ -118,6 +137,23 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
   for (int h = 0; h < n_pairs; ++h)
     if (pm.pair_a[h] == i || pm.pair_b[h] == i) pmask |= 1ull << h;
   if (row0 >= G) return;  // whole wave exits together
+  // the application channel's terms of this lane's domain (and pair columns)
+  const bool app_on = a_.app != nullptr && a_.app_cnt != nullptr && a_.app->on != 0;
+  double app_w = 0.0, app_b = 0.0, app_thr = 0.0;
+  double app_w2[3] = {0.0, 0.0, 0.0}, app_b2[3] = {0.0, 0.0, 0.0};
+  uint32_t app_ev = 0u;
+  if (app_on) {
+    app_w = a_.app->w[i];
+    app_b = a_.app->b[i];
+    app_thr = a_.app->thr_ms;
+    app_ev = (a_.app->dom_mask >> i) & 1u;
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      if (16 * t + i < kMaxPairs) {
+        app_w2[t] = a_.app->w2[16 * t + i];
+        app_b2[t] = a_.app->b2[16 * t + i];
+      }
+  }
 
   const int n_pt = (n_pairs + 15) >> 4;  // pair tiles (uniform over the wave)
   f64x4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -143,10 +179,15 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
     for (int rr = 0; rr < kRegs; ++rr) {
       const int reg = reg0 + rr;
       const int r = row0 + kq + 4 * reg;
-      const double lg = pick(acc, reg) + bias;
+      const int as = (app_on && r < G) ? app_state(a_.app_cnt, feat, r, app_thr) : -1;
+      double lg = pick(acc, reg) + bias;
+      if (as >= 0 && lg != -INFINITY) lg += app_b + (as ? app_w : 0.0);
       double l2[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t) l2[t] = (t < n_pt) ? pick(acc2[t], reg) + b2[t] : -INFINITY;
+      for (int t = 0; t < 3; ++t) {
+        l2[t] = (t < n_pt) ? pick(acc2[t], reg) + b2[t] : -INFINITY;
+        if (as >= 0 && l2[t] != -INFINITY) l2[t] += app_b2[t] + (as ? app_w2[t] : 0.0);
+      }
       double m = fmax(lg, fmax(l2[0], fmax(l2[1], l2[2])));
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1) m = fmax(m, __shfl_xor(m, off, 16));
@@ -180,7 +221,7 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
       if (r < G) {
         post[(size_t)r * kMaxDomains + i] = marg;
         const uint32_t eb = elevated_bits(feat + (size_t)r * kSlots, pm);
-        evbits[(size_t)r * kMaxDomains + i] = eb & pm.dom_mask[i];
+        evbits[(size_t)r * kMaxDomains + i] = (eb & pm.dom_mask[i]) | ((as == 1 ? app_ev : 0u) << kAppBit);
         if (i == 0) {
           pred[r] = am;
           conf[r] = mm;
@@ -197,7 +238,9 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
   for (int rr = 0; rr < kRegs; ++rr) {
     const int reg = reg0 + rr;
     const int r = row0 + kq + 4 * reg;
-    const double lg = pick(acc, reg) + bias;  // -inf for inactive domains
+    const int as = (app_on && r < G) ? app_state(a_.app_cnt, feat, r, app_thr) : -1;
+    double lg = pick(acc, reg) + bias;  // -inf for inactive domains
+    if (as >= 0 && lg != -INFINITY) lg += app_b + (as ? app_w : 0.0);
     // max + argmax over the 16 domain lanes (ties -> lowest index)
     double m = lg;
     int am = i;
@@ -216,7 +259,7 @@ __device__ __forceinline__ void posterior_body(int blk, const PosteriorArgs& a_)
     if (r < G) {
       post[(size_t)r * kMaxDomains + i] = p;
       const uint32_t eb = elevated_bits(feat + (size_t)r * kSlots, pm);
-      evbits[(size_t)r * kMaxDomains + i] = eb & pm.dom_mask[i];
+      evbits[(size_t)r * kMaxDomains + i] = (eb & pm.dom_mask[i]) | ((as == 1 ? app_ev : 0u) << kAppBit);
       if (i == 0) {
         pred[r] = am;
         conf[r] = inv;
@@ -438,8 +481,8 @@ static int stats_grid(int cap) {
 
 void launch_posterior(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm, const int32_t* labels,
                       double* post, int32_t* pred, double* conf, uint32_t* evbits, uint32_t* confusion,
-                      hipStream_t stream) {
-  const PosteriorArgs a{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion};
+                      hipStream_t stream, const AppModel* app, const uint32_t* app_cnt) {
+  const PosteriorArgs a{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion, app, app_cnt};
   // 16 waves per workgroup, 4 per 16-row group: a window's 64 incidents in one workgroup
   constexpr int kWPG = 4, kNT = 1024, kRowsPerBlock = kNT / 64 / kWPG * 16;
   hipLaunchKernelGGL((k_posterior<kNT, kWPG>), dim3(cap > 0 ? (cap + kRowsPerBlock - 1) / kRowsPerBlock : 1), dim3(kNT),
@@ -455,8 +498,8 @@ void launch_stats(const float* feat, const int* ng_dev, int cap, const Posterior
 void launch_posterior_stats(const float* feat, const int* ng_dev, int cap, const PosteriorModel* pm,
                             const int32_t* labels, double* post, int32_t* pred, double* conf, uint32_t* evbits,
                             uint32_t* confusion, const int32_t* stat_labels, const float* weights, double* out,
-                            double* count, hipStream_t stream) {
-  const PosteriorArgs p{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion};
+                            double* count, hipStream_t stream, const AppModel* app, const uint32_t* app_cnt) {
+  const PosteriorArgs p{feat, ng_dev, cap, pm, labels, post, conf, pred, evbits, confusion, app, app_cnt};
   const StatsArgs st{feat, ng_dev, cap, pm, stat_labels, weights, out, count};
   const int gp = posterior_grid(cap);
   hipLaunchKernelGGL((k_posterior_stats<kPostNT, kStatsRPW>), dim3(gp + stats_grid(cap)), dim3(kPostNT), 0, stream, p,

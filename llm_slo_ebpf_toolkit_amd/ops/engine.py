@@ -78,6 +78,46 @@ def model_bytes(model: LinearPosteriorModel) -> np.ndarray:
     return rec.view(np.uint8)
 
 
+APP_MODEL_DTYPE = np.dtype([
+    ("w", "<f8", (16,)), ("b", "<f8", (16,)), ("w2", "<f8", (MAX_PAIRS,)), ("b2", "<f8", (MAX_PAIRS,)),
+    ("thr_ms", "<f8"), ("dom_mask", "<u4"), ("on", "<i4"),
+])
+assert APP_MODEL_DTYPE.itemsize == 1040  # == sizeof(mislo::AppModel)
+
+
+def app_model_bytes(model: LinearPosteriorModel) -> np.ndarray:
+    """Byte image of ``mislo::AppModel`` (ops/csrc/mislo_launch.h): the model's application
+    evidence (models/bayes.py AppEvidence) with the 2-fault columns of its pairs; ``on`` = 0
+    without one."""
+    rec = np.zeros(1, dtype=APP_MODEL_DTYPE)
+    app = model.app
+    if app is not None:
+        D = model.weights.shape[1]
+        w, b = app.terms()
+        rec["w"][0][:D] = w[:D]
+        rec["b"][0][:D] = b[:D]
+        if model.pairs is not None:
+            w2, b2 = app.pair_terms(model.pairs)
+            rec["w2"][0][:len(w2)] = w2
+            rec["b2"][0][:len(b2)] = b2
+        rec["thr_ms"][0] = app.threshold_ms
+        rec["dom_mask"][0] = int(sum(1 << d for d in range(D) if app.evidence_mask(D)[d]))
+        rec["on"][0] = 1
+    return rec.view(np.uint8)
+
+
+def app_from_bytes(b: np.ndarray, n_dom: int = N_DOMAINS):
+    """Inverse of ``app_model_bytes``: the AppEvidence an ``AppModel`` image evaluates, or None
+    when the image is off."""
+    from ..models.bayes import AppEvidence
+
+    rec = np.frombuffer(np.ascontiguousarray(b, dtype=np.uint8).tobytes(), dtype=APP_MODEL_DTYPE)[0]
+    if int(rec["on"]) == 0:
+        return None
+    return AppEvidence.from_image(np.array(rec["w"])[:n_dom], np.array(rec["b"])[:n_dom], np.array(rec["w2"]),
+                                  np.array(rec["b2"]), float(rec["thr_ms"]), int(rec["dom_mask"]))
+
+
 def model_from_bytes(b: np.ndarray) -> LinearPosteriorModel:
     """Inverse of ``model_bytes``: the host model a ``mislo::PosteriorModel`` image evaluates
     (the CPU window engine scores with it; exported model files hold the image)."""

@@ -20,7 +20,7 @@ from typing import Dict, Optional
 import numpy as np
 
 from ..collector import records
-from ..models.bayes import N_DOMAINS, LinearPosteriorModel, SufficientStats, soft_labels
+from ..models.bayes import N_DOMAINS, LinearPosteriorModel, SufficientStats, app_counts, soft_labels
 from . import oracle
 from .window import PACKET_LAYOUT
 
@@ -177,6 +177,7 @@ class CpuRingEngine:
         self.table, self.tmap = oracle.CtxTable(), oracle.TraceMap()
         self.pod_sn: Dict[int, int] = {}
         self.model = None
+        self.app = None  # application evidence (set_app_model)
         self.win: Dict[int, dict] = {}
         self._totals = np.zeros(PACKET_LEN)
         self._stats_acc = np.zeros(STATS_LEN)
@@ -203,6 +204,11 @@ class CpuRingEngine:
 
     def model_bytes(self) -> np.ndarray:
         return self.model_image.copy()
+
+    def set_app_model(self, b) -> None:
+        from ..ops.engine import app_from_bytes
+
+        self.app = app_from_bytes(b, self.n_dom)
 
     def set_p0(self, p0) -> None:
         pass
@@ -277,11 +283,15 @@ class CpuRingEngine:
         pred = np.zeros(G, np.int32)
         gconf = np.zeros(G)
         evbits = np.zeros((G, 16), np.uint32)
+        okg = mine_sp & (grp_local >= 0) & (grp_local < G)
+        app = app_counts(spr, G, mine=okg, groups=grp_local)
         if G and self.model is not None:
-            post[:, :D] = self.model.posteriors(f64)
-            pred = self.model.predict(f64).astype(np.int32)
+            self.model.app = self.app
+            st = self.app.state(app, feat) if self.app is not None else None
+            post[:, :D] = self.model.posteriors(f64, st)
+            pred = self.model.predict(f64, st).astype(np.int32)
             gconf = post[np.arange(G), pred]
-            evbits[:, :D] = self.model.evidence_bits(f64)
+            evbits[:, :D] = self.model.evidence_bits(f64, st)
         conf = np.zeros((16, 16), dtype=np.int64)
         stats = SufficientStats()
         if labels is not None and G:
@@ -292,14 +302,13 @@ class CpuRingEngine:
             if learn and m.any():
                 stats.add(f64[m], soft_labels(lab[m]))
         sli = np.zeros((G, 2), np.uint32)
-        okg = mine_sp & (grp_local >= 0) & (grp_local < G)
         np.add.at(sli[:, 0], grp_local[okg], 1)
         np.add.at(sli[:, 1], grp_local[okg & (spr["ttft_ms"] > np.float32(self.ttft_slo_ms))], 1)
         ring = np.zeros(PACKET_LAYOUT[7])
         ring[:7] = (first_busy, 0, 0, 0, 0, events, other)
         pk = build_packet(hist, status, misc, dbg, conf, stats)
         pk[PACKET_LEN - PACKET_LAYOUT[7]:] = ring
-        out = {"post": post, "conf": gconf, "feat": feat, "pred": pred, "evbits": evbits, "sli": sli}
+        out = {"post": post, "conf": gconf, "feat": feat, "pred": pred, "evbits": evbits, "sli": sli, "app": app}
         outs = [out]
         if self.has_comm:
             import torch

@@ -212,6 +212,7 @@ class WindowPipeline:
             self.model = LDA.fit(self.cum_stats)
         elif self.model_name in ("bayes_learned", "lda"):
             self.model = NaiveBayes.learned(self.cum_stats, **self.learned_kw)
+        self.model.app = getattr(self, "app", None)
         self.eng.set_model_bytes(self._model_bytes(self.model))
 
     def wait(self, k: int) -> None:
@@ -241,6 +242,20 @@ class WindowPipeline:
     def set_model(self, model) -> None:
         self.model = model
         self.eng.set_model_bytes(self._model_bytes(model))
+        if getattr(self, "app", None) is not None and model.app is None:
+            model.app = self.app
+        if model.app is not None:
+            self.set_app(model.app)
+
+    def set_app(self, app) -> None:
+        """The application evidence (models/bayes.py AppEvidence; None: off) the posterior kernel
+        adds to every incident group whose spans report a retrieval time. Its 2-fault columns
+        follow the current model's pairs."""
+        from ..ops.engine import app_model_bytes
+
+        self.app = app
+        self.model.app = app
+        self.eng.set_app_model(app_model_bytes(self.model))
 
     # ---- totals / model ---------------------------------------------------------------------
     def drain(self) -> None:

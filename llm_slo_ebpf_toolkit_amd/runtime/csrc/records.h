@@ -25,7 +25,9 @@ struct SpanRec64 {  // records.py SPAN (64 B)
   uint16_t node_id, svc_id;
   uint32_t group_id;
   float ttft_ms, latency_ms;
-  uint64_t span_h, reserved;
+  uint64_t span_h;
+  float retr_ms;  // application-reported retrieval ms (0 = none)
+  uint32_t reserved;
 };
 static_assert(sizeof(SpanRec64) == 64, "SPAN is 64 bytes");
 

@@ -233,6 +233,24 @@ _GPU_COLS_FOR_REF_ROWS = {  # P(REF signal elevated | gpu domain)
 }
 
 
+# Application evidence (NEW, additive; ops/csrc/mislo_launch.h AppModel, models/bayes.py
+# AppEvidence): the incident group's retrieval time the kernel signals do not account for -- the
+# application's llm.slo.retrieval.{vectordb,network,dns}_ms (REF demo/rag-service/main.go:393-397)
+# minus REF's kernel-attributed share, dns + connect + TLS (DecomposeRetrieval,
+# pkg/otel/processor/ebpfcorrelator/correlator.go:179-194). REF's table has no row for it; this is
+# its expert row. A retrieval backend stall (vector DB, search index) is the one fault that lives
+# there alone; a starved or network-slowed service inflates its own measured retrieval time too
+# (CPU / memory / network 0.30-0.35), and a provider or GPU fault does not touch retrieval.
+APP_RETRIEVAL_SIGNAL = "retrieval_residual_ms"
+APP_RETRIEVAL_SEMCONV = "llm.slo.retrieval.residual_ms"
+APP_RETRIEVAL_THRESHOLD_MS = 100.0
+APP_RETRIEVAL_LIKELIHOOD: Dict[str, float] = {
+    "network_dns": .30, "network_egress": .30, "cpu_throttle": .35, "memory_pressure": .30,
+    "provider_throttle": .10, "provider_error": .10, "retrieval_backend": .90, "unknown": .05,
+    "gpu_contention": .10, "gpu_interconnect": .05,
+}
+
+
 def extended_likelihood_matrix() -> List[List[float]]:
     """16 x 10 matrix [slot][domain] of P(elevated | domain)."""
     rows: List[List[float]] = []

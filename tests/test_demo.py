@@ -46,7 +46,8 @@ def test_chat_roundtrip_metrics_and_traces(service):
     assert m['llm_slo_correlation_total{tier="trace_id_exact",enriched="true"}'] == 1
     assert m["llm_slo_ttft_ms_count"] == 1 and m["llm_slo_burn_rate"] == 0
     spans = json.loads(traces.requests[0]["body"])["resourceSpans"][0]["scopeSpans"][0]["spans"]
-    assert [s["name"] for s in spans] == ["chat.request", "chat.retrieval", "chat.generation"]
+    # exported as an OTel SDK ends them: the children before the request
+    assert [s["name"] for s in spans] == ["chat.retrieval", "chat.generation", "chat.request"]
     assert len({s["traceId"] for s in spans}) == 1
 
 

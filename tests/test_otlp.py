@@ -183,6 +183,41 @@ def test_rag_service_spans_reach_the_ring():
         assert abs(float(r["ttft_ms"]) - o["ttft_ms"]) < 1e-2
         assert r["pid"] == os.getpid() and r["pod_id"] == pods.id(RES["k8s.pod.uid"])
         assert r["group_id"] == 0
+        # the retrieval child span's llm.slo.retrieval.* breakdown, folded into the request's record
+        # (the breakdown is the plan's parts; the response's retrieval_ms the wall time around them)
+        assert 0.0 < float(r["retr_ms"]) <= o["retrieval_ms"] + 0.5
+
+
+def test_retrieval_breakdown_folds_into_the_request_span():
+    """REF puts llm.slo.retrieval.{vectordb,network,dns}_ms on the chat.retrieval child span
+    (demo/rag-service/main.go:393-397): the receiver sums them per trace onto the request's SPAN
+    record, in the same export or from an earlier one (children end first); a trace without a
+    breakdown carries 0 (no application evidence)."""
+    m, _ = _mapper()
+    retr = {"llm.slo.retrieval.vectordb_ms": 150.0, "llm.slo.retrieval.network_ms": 12.0,
+            "llm.slo.retrieval.dns_ms": 6.5}
+    child = (TID, "00f067aa0ba902b9", "00f067aa0ba902b7", 1_700_000_000_010_000_000, 1_700_000_000_180_000_000, retr)
+    recs = m.records(otlp.parse_json(_request_json(RES, [child] + SPANS)))
+    assert len(recs) == 2
+    assert recs[0]["retr_ms"] == np.float32(168.5) and recs[1]["retr_ms"] == 0.0
+    # the child in an earlier export than its request span
+    m2, _ = _mapper()
+    assert len(m2.records(otlp.parse_json(_request_json(RES, [child])))) == 0
+    recs = m2.records(otlp.parse_json(_request_json(RES, SPANS)))
+    assert recs[0]["retr_ms"] == np.float32(168.5)
+    assert not m2._retr  # consumed
+    # over protobuf, with junk parts ignored
+    m3, _ = _mapper()
+    bad = dict(retr, **{"llm.slo.retrieval.dns_ms": "n/a"})
+    body = _request_pb(RES, [_span_pb(*(child[:5] + (bad,)))] + [_span_pb(*x) for x in SPANS])
+    assert m3.records(otlp.parse_proto(body))[0]["retr_ms"] == np.float32(162.0)
+    assert otlp.retrieval_ms({}) is None and otlp.retrieval_ms({"llm.slo.retrieval.vectordb_ms": -1.0}) is None
+    # the pending table is bounded
+    m4, _ = _mapper()
+    m4.retrieval_cap = 4
+    for i in range(10):
+        m4.records(otlp.parse_json(_request_json(RES, [(f"{i:032x}",) + child[1:]])))
+    assert len(m4._retr) == 4
 
 
 def test_receiver_refuses_oversized_bodies_and_unlisted_peers():
