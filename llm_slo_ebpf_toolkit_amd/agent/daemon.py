@@ -152,6 +152,8 @@ class AgentOptions:
                                          # <= 0: every scored group, REF's emit-per-tick)
     emit_min_requests: float = 8.0       # the gate's burn "now": the last windows (at most 3) holding this many
                                          # requests -- one busy window with no breach ends a page
+    emit_recovered_requests: int = 4     # a window completing at least this many requests, none breaching in it,
+                                         # is recovered: not attributed (0 = off)
     emit_wait_ms: int = 250              # after a cut, wait up to this long for the window's results (0 = emit
                                          # window k at cut k+1)
     decision_log: str = ""               # JSONL of every scored group per window, emitted or not, and why
@@ -658,9 +660,11 @@ class Agent:
         sli = res.get("sli")
         forecast, now_burn = {}, {}
         if sli is not None:
+            late = res.get("late")
             for g in range(min(G, sli.shape[0])):
                 key = names[g] if g < len(names) else f"group-{g}"
-                forecast[g] = self.burn.observe(key, float(sli[g, 0]), float(sli[g, 1]))
+                lb = float(late[g, 0]) if late is not None and g < late.shape[0] else 0.0
+                forecast[g] = self.burn.observe(key, float(sli[g, 0]), float(sli[g, 1]), late=lb)
                 now_burn[g] = self.burn.current(key, windows=3, min_requests=self.o.emit_min_requests)
             err = self.burn.error()
             if err is not None:
@@ -678,15 +682,23 @@ class Agent:
         top_d = pl.argmax(axis=1).tolist() if G else []
         top_p = pl.max(axis=1).tolist() if G else []
         any_live = bool(live.any())
+        late_l = res["late"][:, 0].tolist() if res.get("late") is not None else []
+        rec_n = int(self.o.emit_recovered_requests)
         for g in range(G):
-            if g < len(reqs) and reqs[g] == 0:
+            if g < len(reqs) and reqs[g] == 0 and not (g < len(late_l) and late_l[g]):
                 continue  # no request of this group in the window: no incident to attribute
             burn = forecast.get(g, 0.0)  # forecast burn over the SLO window (measured counts)
             # (1 - 1e-9: the budget 1 - target is not exact in binary, a burn of exactly 1 lands a hair under)
             cur = now_burn.get(g, 0.0)
             confident = any_live and top_p[g] >= self.o.min_confidence
-            emit = confident and (sli is None or self.o.emit_min_burn <= 0
-                                  or (cur > 0 and cur >= self.o.emit_min_burn * (1.0 - 1e-9)))
+            # recovered: the window itself completed enough requests and none breached in it (a breach
+            # whose deadline passed in an earlier window is that window's, SPAN_LATE); the pooled burn
+            # still holds the fault's windows, but the service no longer burns
+            recovered = (sli is not None and rec_n > 0 and g < sli.shape[0] and sli[g, 0] >= rec_n
+                         and sli[g, 1] == 0)
+            burning = (sli is None or self.o.emit_min_burn <= 0
+                       or (cur > 0 and cur >= self.o.emit_min_burn * (1.0 - 1e-9)))
+            emit = confident and burning and not recovered
             ranked = model.ranked(post[g, :D], bits[g, :D]) if (emit or log is not None) else None
             if log is not None:
                 log.write(json.dumps({
@@ -695,7 +707,9 @@ class Agent:
                     "breaches": float(sli[g, 1]) if sli is not None and g < sli.shape[0] else None,
                     "burn_now": round(cur, 4), "burn_forecast": round(burn, 4),
                     "top": [[p.domain, round(float(p.posterior), 4)] for p in ranked[:3]],
-                    "emitted": emit, "why": "emitted" if emit else ("low_confidence" if not confident else "no_burn")}) + "\n")
+                    "late": late_l[g] if g < len(late_l) else 0, "emitted": emit,
+                    "why": "emitted" if emit else ("low_confidence" if not confident else
+                                                   ("no_burn" if not burning else "recovered"))}) + "\n")
             if not confident:
                 continue
             self.metrics.observe_incident(catalog.ALL_DOMAINS[top_d[g]], emit)
@@ -942,6 +956,7 @@ class Agent:
                         ipcache["t"] = time.monotonic()
                     return ipcache["m"]
             mapper = SpanMapper(groups, self.pod_ids.id, node_id, pod_ips=pod_ips, forwarders=o.otlp_forwarders)
+            mapper.slo_ms = float(o.ttft_slo_ms)
             if router is not None:  # each span to the ring of the worker owning its incident group
                 def push_spans(recs):
                     sh = router.span_shard(recs)
@@ -1037,6 +1052,8 @@ class Agent:
                 bases = clock.bases()
                 cuts = [Cut(kernel=rs[0].producer_pos, user=rs[1].head, spans=rs[2].head, bases=bases, t_ns=t)
                         for rs in sets]
+                if mapper is not None:  # spans after this cut: a deadline before it is an earlier window's
+                    mapper.late_before_ns = t
                 upd = mapper.take_pod_updates() if mapper is not None else None
                 if upd is not None and len(upd[0]):
                     self.pod_table.update(zip(np.asarray(upd[0]).tolist(), np.asarray(upd[1]).tolist()))

@@ -91,7 +91,7 @@ def merge_results(parts: List[dict], n_groups: int) -> dict:
     (group g = local g // world of worker g % world)."""
     world = len(parts)
     out = {}
-    for key in ("post", "conf", "feat", "pred", "evbits", "sli", "app"):
+    for key in ("post", "conf", "feat", "pred", "evbits", "sli", "app", "late"):
         if key not in parts[0]:
             continue
         ref = np.asarray(parts[0][key])

@@ -114,6 +114,9 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                            "(error-budget multiples) is at least this (<= 0: every scored group)"),
         ("emit-min-requests", d.emit_min_requests, "gpu engine: the emission gate's burn is over the last windows "
                                                    "(at most 3) holding this many requests"),
+        ("emit-recovered-requests", d.emit_recovered_requests, "gpu engine: a window that completes at least "
+                                                               "this many requests of a group, none breaching "
+                                                               "its SLO in the window, is not attributed (0 = off)"),
         ("decision-log", d.decision_log, "gpu engine: JSONL of every scored incident group per window -- "
                                          "requests, breaches, burn, top posteriors, emitted or why not (\"\" = off)"),
         ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; the flag given on the "
@@ -145,6 +148,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         model_signals=a.model_signals, retrieval_residual_ms=float(a.retrieval_residual_ms),
         pair_prior=float(a.pair_prior), emit_wait_ms=int(a.emit_wait_ms), webhook_queue=int(a.webhook_queue),
         emit_min_burn=float(a.emit_min_burn), emit_min_requests=float(a.emit_min_requests),
+        emit_recovered_requests=int(a.emit_recovered_requests),
         decision_log=a.decision_log,
         explicit_flags=tuple(sorted({x.lstrip("-").split("=", 1)[0] for x in (argv if argv is not None else sys.argv[1:]) if x.startswith("-")})))
     if int(a.gpu_hw_queues) > 0:  # before anything initialises the HIP runtime

@@ -305,6 +305,11 @@ class SpanMapper:
         self._pods: Dict[int, int] = {}
         self._new: Dict[int, int] = {}
         self._plock = threading.Lock()
+        # late breaches (records.SPAN_LATE): the agent sets slo_ms, and late_before_ns at every window
+        # cut; a span whose TTFT-SLO deadline (start + slo) lies before it is flagged -- if it
+        # breached, the breach belongs to an earlier window than the one it is reported in
+        self.slo_ms = 0.0
+        self.late_before_ns = 0
         # retrieval breakdowns of traces whose request span has not arrived yet (bounded, oldest out)
         self._retr: "collections.OrderedDict[int, float]" = collections.OrderedDict()
         self._rlock = threading.Lock()
@@ -362,6 +367,7 @@ class SpanMapper:
         # per-field lists, written into the record array column by column at the end: setting the
         # fields of one structured element at a time cost ~18 us per span (the receiver's CPU)
         ts, tr, sh, pids, pods, svcs, grps, ttft, lat, conn, rms = ([] for _ in range(11))
+        late_before, slo_ns = int(self.late_before_ns), int(round(float(self.slo_ms) * 1e6))
         res_cache: Dict[int, tuple] = {}  # one resource's service / pod / pid per request
         groups_seen: Dict[str, int] = {}
         pods_seen: Dict[object, int] = {}
@@ -436,6 +442,9 @@ class SpanMapper:
             out["latency_ms"] = lat
             out["conn_h"] = np.array(conn, dtype=np.uint64)
             out["retr_ms"] = rms
+            if late_before > 0 and slo_ns > 0:
+                t0s = np.asarray(ts, dtype=np.int64)
+                out["flags"] = np.where((t0s > 0) & (t0s + slo_ns < late_before), records.SPAN_LATE, 0)
         return out
 
 

@@ -212,8 +212,11 @@ SPAN = np.dtype([
     # llm.slo.retrieval.{vectordb,network,dns}_ms summed (demo/rag-service/main.go:393-397);
     # <= 0 / NaN = no breakdown (the application evidence of ops/csrc/posterior.hip)
     ("retr_ms", "<f4"),
-    ("reserved", "<u4"),     # 60
+    # 60 bit 0 (SPAN_LATE): the request's TTFT-SLO deadline (start + SLO) passed before the agent's
+    # last window cut -- a breach that belongs to an earlier window (collector/otlp.py)
+    ("flags", "<u4"),
 ])
+SPAN_LATE = 1
 assert SPAN.itemsize == 64
 
 FLAG_HAS_GPU = 1 << 8

@@ -233,13 +233,21 @@ class BurnRateForecaster:
             j = lo
         return self.burn(cn[t] - cn[t - j], cb[t] - cb[t - j])
 
-    def observe(self, key, n: float, breach: float, forecast: bool = True) -> float:
+    def observe(self, key, n: float, breach: float, forecast: bool = True, late: float = 0.0) -> float:
         """Adds one window's request and breach counts; returns the forecast made at it (and
-        keeps it for scoring unless ``forecast`` is False)."""
+        keeps it for scoring unless ``forecast`` is False). ``late``: breaching requests reported
+        in this window whose SLO deadline passed in an earlier one (collector/otlp.py SPAN_LATE);
+        they are credited to the previous window, where the breach happened."""
         c = self._cum.get(key)
         if c is None:
             c = self._cum[key] = [[0.0], [0.0]]
         cn, cb = c
+        if late:
+            if len(cn) > 1:
+                cn[-1] += float(late)
+                cb[-1] += float(late)
+            else:
+                n, breach = float(n) + float(late), float(breach) + float(late)
         cn.append(cn[-1] + float(n))
         cb.append(cb[-1] + float(breach))
         t = len(cn) - 2  # this window's index in the kept history

@@ -138,7 +138,8 @@ class PyEngine {
                                         reinterpret_cast<const int32_t*>(p + o_pred),
                                         reinterpret_cast<const uint32_t*>(p + o_ev),
                                         reinterpret_cast<const uint32_t*>(p + o_sli),
-                                        reinterpret_cast<const uint32_t*>(p + o_sli) + 2 * G},
+                                        reinterpret_cast<const uint32_t*>(p + o_sli) + 2 * G,
+                                        reinterpret_cast<const uint32_t*>(p + o_sli) + 4 * G},
                              n_groups));
     }
     return out;
@@ -153,6 +154,7 @@ class PyEngine {
     d["evbits"] = copy_array(r.evbits, {G, 16});
     d["sli"] = copy_array(r.sli, {G, 2});
     d["app"] = copy_array(r.app, {G, 2});
+    d["late"] = copy_array(r.late, {G, 2});
     return d;
   }
   py::tuple window_ms(int64_t k) {

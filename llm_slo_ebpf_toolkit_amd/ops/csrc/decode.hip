@@ -649,6 +649,7 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   // global atomics serialised on a handful of L2 addresses (33 us per 16K-span window)
   __shared__ uint32_t s_sli[2 * kSliLds];
   __shared__ uint32_t s_app[2 * kSliLds];  // application retrieval: spans, sum (10 us units)
+  __shared__ uint32_t s_late[kSliLds];     // late breaches
   const bool sli_lds = sm.grp_sli && sm.n_groups <= kSliLds;
   const bool app_lds = sm.grp_app && sm.n_groups <= kSliLds;
   for (int i = threadIdx.x; i < kKeyTypes * kParts; i += NT) s_part[i] = 0;
@@ -656,6 +657,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
     for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT) s_sli[i] = 0;
   if (app_lds)
     for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT) s_app[i] = 0;
+  const bool late_lds = sm.grp_late && sm.n_groups <= kSliLds;
+  if (late_lds)
+    for (int i = threadIdx.x; i < sm.n_groups; i += NT) s_late[i] = 0;
   __syncthreads();
   const int n = min(*n_ptr, cap);
   const int chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -691,9 +695,15 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
         if (!mine) r.ts = 0;  // another GPU's incident group: never joins, never counted here
       }
       if (mine && sm.grp_sli && grp < (uint32_t)sm.n_groups) {  // per-incident TTFT SLO accounting
-        uint32_t* sli = sli_lds ? s_sli : sm.grp_sli;
-        atomicAdd(&sli[2 * grp], 1u);
-        if (s.ttft_ms > sm.ttft_slo_ms) atomicAdd(&sli[2 * grp + 1], 1u);
+        const bool breach = s.ttft_ms > sm.ttft_slo_ms;
+        if (breach && (s.flags & kSpanLate) && sm.grp_late) {  // an earlier window's breach, reported now
+          if (late_lds) atomicAdd(&s_late[grp], 1u);
+          else atomicAdd(&sm.grp_late[2 * grp], 1u);
+        } else {
+          uint32_t* sli = sli_lds ? s_sli : sm.grp_sli;
+          atomicAdd(&sli[2 * grp], 1u);
+          if (breach) atomicAdd(&sli[2 * grp + 1], 1u);
+        }
       }
       // the application's retrieval time of the request (REF DecomposeRetrieval's input,
       // correlator.go:179-194): its group sum, in fixed point like every incident sum
@@ -739,6 +749,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
   if (app_lds)
     for (int i = threadIdx.x; i < 2 * sm.n_groups; i += NT)
       if (s_app[i]) atomicAdd(&sm.grp_app[i], s_app[i]);
+  if (late_lds)
+    for (int i = threadIdx.x; i < sm.n_groups; i += NT)
+      if (s_late[i]) atomicAdd(&sm.grp_late[2 * i], s_late[i]);
 }
 
 // Event decoders run 1024 threads per workgroup: the grid is capped at kPartBlocks (the

@@ -89,6 +89,7 @@ struct ResultView {
   const uint32_t* evbits; // [G][16]
   const uint32_t* sli;    // [G][2]: spans, TTFT-SLO breaches
   const uint32_t* app;    // [G][2]: spans with an application retrieval time, its sum (10 us units)
+  const uint32_t* late;   // [G][2]: breaches of earlier windows reported in this one (SpanMap::grp_late), spare
 };
 
 // The window's inputs: ring byte ranges (as the rings hold them) and the window metadata.
@@ -221,6 +222,7 @@ class WindowEngine {
   unsigned long long* trace_hash_ = nullptr;  // kernel trace id -> hash
   uint32_t* sli_ = nullptr;
   uint32_t* app_ = nullptr;         // this buffer's [G][2] application retrieval counts (after sli_)
+  uint32_t* late_ = nullptr;        // this buffer's [G][2] late breaches (after app_)
   AppModel* app_dev_ = nullptr;     // the application evidence model (device)
   // other GPUs' rows: per buffer, imported after this window's records; counts per buffer
   int n_rows_ = 0;                 // rows per generation = sig_cap + import_cap

@@ -220,10 +220,10 @@ void WindowEngine::alloc() {
   }
   warm_.assign(8 * nb_, false);
   // per-incident results block: [post G*16 f64][gconf G f64][feat G*16 f32][pred G i32][evbits G*16 u32]
-  // [sli G*2 u32][app G*2 u32]
+  // [sli G*2 u32][app G*2 u32][late G*2 u32]
   const size_t o_gconf = 16 * G * 8, o_feat = o_gconf + G * 8, o_pred = o_feat + 16 * G * 4, o_ev = o_pred + G * 4;
   const size_t o_sli = o_ev + 16 * G * 4;
-  res_bytes_ = o_sli + 4 * G * 4;
+  res_bytes_ = o_sli + 6 * G * 4;
   for (int b = 0; b < nb_; ++b) {
     res_host_.push_back(static_cast<uint8_t*>(host_block(res_bytes_)));
   }
@@ -446,6 +446,7 @@ void WindowEngine::set_buffer(int b) {
   evbits_ = reinterpret_cast<uint32_t*>(r + o_ev);
   sli_ = reinterpret_cast<uint32_t*>(r + o_sli);
   app_ = sli_ + 2 * (size_t)G;
+  late_ = sli_ + 4 * (size_t)G;
 }
 
 // The head of a window: the accumulators reset, the next generation slot, the window's rows.
@@ -466,7 +467,7 @@ void WindowEngine::run_begin(int b, hipStream_t st) {
   add(cnt_, (size_t)S * 4, 0);
   add(gsum_, (size_t)kGroupStripes * G * kSlots * 8, 0);
   add(gcnt_, (size_t)kGroupStripes * G * kSlots * 4, 0);
-  add(sli_, (size_t)G * 4 * 4, 0);  // + the application retrieval counts (app_) behind it
+  add(sli_, (size_t)G * 6 * 4, 0);  // + the application retrieval counts (app_) and late breaches (late_)
   // + the next generation slot and the halo cut-offs (the finished window's tmax is read before
   // its reset), the ring state, no other GPUs' rows until merged, the window's rows
   launch_window_begin(fl, gen_, tmax_, gens_, (long long)llround(cfg_.halo_ms * 1e6), ring_state_, remote_n_ + b,
@@ -568,7 +569,7 @@ void WindowEngine::run_spans(int b, hipStream_t st) {
   uint8_t* in = in_dev_[b];
   const int* counts = reinterpret_cast<const int*>(in);
   const int S = cfg_.span_cap, G = cfg_.group_cap;
-  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_, app_};
+  const SpanMap sm{1, sli_, G, cfg_.ttft_slo_ms, cfg_.shard_rank, cfg_.shard_world, gen_, app_, late_};
   launch_decode_spans(in + off_span_, counts + 1, S, span_cols(), s_part_blk_, ctx_tab_, (int)kCtxRows, st, &sm);
   launch_partition(s_part_, counts + 1, S, nblk_span_, s_part_blk_, s_part_off_, s_part_tot_, s_part_base_, s_items_,
                    st);
@@ -820,7 +821,8 @@ ResultView WindowEngine::results(int64_t k) const {
   return ResultView{reinterpret_cast<const double*>(r), reinterpret_cast<const double*>(r + o_gconf),
                     reinterpret_cast<const float*>(r + o_feat), reinterpret_cast<const int32_t*>(r + o_pred),
                     reinterpret_cast<const uint32_t*>(r + o_ev), reinterpret_cast<const uint32_t*>(r + o_sli),
-                    reinterpret_cast<const uint32_t*>(r + o_sli) + 2 * G};
+                    reinterpret_cast<const uint32_t*>(r + o_sli) + 2 * G,
+                    reinterpret_cast<const uint32_t*>(r + o_sli) + 4 * G};
 }
 
 std::vector<float> WindowEngine::copy_ms(int64_t k) {

@@ -74,6 +74,10 @@ struct SpanMap {
   // [n_groups][2]: spans carrying an application retrieval time (Span::retr_ms > 0), and the sum
   // of those times in kAppUnitsPerMs units (exact integers: order-free, all-reducible)
   uint32_t* grp_app = nullptr;
+  // [n_groups][2]: breaching spans flagged late (Span::flags kSpanLate: the SLO deadline passed before
+  // the agent's previous cut), counted here instead of in grp_sli -- the host credits them to the
+  // earlier window their breach belongs to; [2g + 1] is spare
+  uint32_t* grp_late = nullptr;
 };
 constexpr double kAppUnitsPerMs = 100.0;  // 10 us: a u32 group sum holds 42,949 s of retrieval per window
 void launch_decode_spans(const void* sp, const int* n_dev, int cap, const SpanCols& cols, uint32_t* part_cnt,

@@ -302,13 +302,18 @@ class CpuRingEngine:
             if learn and m.any():
                 stats.add(f64[m], soft_labels(lab[m]))
         sli = np.zeros((G, 2), np.uint32)
-        np.add.at(sli[:, 0], grp_local[okg], 1)
-        np.add.at(sli[:, 1], grp_local[okg & (spr["ttft_ms"] > np.float32(self.ttft_slo_ms))], 1)
+        late = np.zeros((G, 2), np.uint32)
+        breach = spr["ttft_ms"] > np.float32(self.ttft_slo_ms)
+        is_late = breach & ((spr["flags"] & np.uint32(records.SPAN_LATE)) != 0)
+        np.add.at(sli[:, 0], grp_local[okg & ~is_late], 1)
+        np.add.at(sli[:, 1], grp_local[okg & breach & ~is_late], 1)
+        np.add.at(late[:, 0], grp_local[okg & is_late], 1)
         ring = np.zeros(PACKET_LAYOUT[7])
         ring[:7] = (first_busy, 0, 0, 0, 0, events, other)
         pk = build_packet(hist, status, misc, dbg, conf, stats)
         pk[PACKET_LEN - PACKET_LAYOUT[7]:] = ring
-        out = {"post": post, "conf": gconf, "feat": feat, "pred": pred, "evbits": evbits, "sli": sli, "app": app}
+        out = {"post": post, "conf": gconf, "feat": feat, "pred": pred, "evbits": evbits, "sli": sli, "app": app,
+               "late": late}
         outs = [out]
         if self.has_comm:
             import torch

@@ -27,7 +27,7 @@ struct SpanRec64 {  // records.py SPAN (64 B)
   float ttft_ms, latency_ms;
   uint64_t span_h;
   float retr_ms;  // application-reported retrieval ms (0 = none)
-  uint32_t reserved;
+  uint32_t flags;  // bit 0: TTFT-SLO deadline before the agent's last window cut
 };
 static_assert(sizeof(SpanRec64) == 64, "SPAN is 64 bytes");
 

@@ -149,13 +149,17 @@ def test_cpu_ring_engine_scores_the_application_evidence():
 
 
 def _stall_spans(w, stall=(0,), healthy=(1,)):
+    """Retrieval breakdowns on the replay's spans: a stall far above any kernel share (the replay's
+    fault profiles put connect latency at 350 ms) in ``stall``, a healthy time in ``healthy``; every
+    third span flagged late (SPAN_LATE)."""
     sp = w.spans.copy()
     g = sp["group_id"]
     sp["retr_ms"] = 0.0
     for x in stall:
-        sp["retr_ms"][g == x] = np.float32(150.0) + (np.arange((g == x).sum()) % 7).astype(np.float32)
+        sp["retr_ms"][g == x] = np.float32(5000.0) + (np.arange((g == x).sum()) % 7).astype(np.float32)
     for x in healthy:
         sp["retr_ms"][g == x] = np.float32(22.5)
+    sp["flags"][::3] = R.SPAN_LATE
     return sp
 
 
@@ -187,6 +191,16 @@ def test_engine_application_evidence_matches_the_host_model(pairs):
         r = src.stage(feed(img, rb, user, spans), w.n_groups, img.labels)
         res = pipe.results(r["k"], w.n_groups)
         np.testing.assert_array_equal(res["app"], app_counts(w.spans, w.n_groups))
+        # late breaches (SPAN_LATE): counted apart from the window's own requests
+        breach = w.spans["ttft_ms"] > np.float32(800.0)
+        late = breach & (w.spans["flags"] == R.SPAN_LATE)
+        exp = np.zeros((w.n_groups, 2), np.int64)
+        np.add.at(exp[:, 0], w.spans["group_id"][~late], 1)
+        np.add.at(exp[:, 1], w.spans["group_id"][breach & ~late], 1)
+        np.testing.assert_array_equal(res["sli"].astype(np.int64), exp)
+        exp_late = np.zeros(w.n_groups, np.int64)
+        np.add.at(exp_late, w.spans["group_id"][late], 1)
+        np.testing.assert_array_equal(res["late"][:, 0].astype(np.int64), exp_late)
         feat = res["feat"].astype(np.float64)
         st = m.app.state(res["app"], res["feat"])
         seen_elevated |= bool((st == 1).any())

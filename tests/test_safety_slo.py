@@ -1,5 +1,6 @@
 """Safety (REF pkg/safety/*_test.go), SLO math (REF pkg/slo/calculator_test.go), prereq."""
 
+import json
 import os
 
 import pytest
@@ -285,3 +286,66 @@ def test_burn_rate_forecaster_state_round_trips_and_scores_stay_bounded():
     for _ in range(20000):
         big.observe("k", 10, 1)
     assert len(big.scored) <= 10000 and big.error() == pytest.approx(0.0)
+
+
+def test_a_late_breach_is_credited_to_the_window_it_happened_in():
+    """SPAN_LATE breaches (the SLO deadline passed before the previous cut) count in the previous
+    window's burn, not in the window that reported them."""
+    fc = slo.BurnRateForecaster(target=0.99, horizon=10, short=5, method="persistence", min_requests=1)
+    fc.observe("k", 6, 6)
+    fc.observe("k", 7, 0, late=1)
+    assert fc.history("k") == [(7.0, 7.0), (7.0, 0.0)]
+    assert fc.current("k", windows=1, min_requests=1) == 0.0
+    fresh = slo.BurnRateForecaster(target=0.99, horizon=10, short=5)
+    fresh.observe("k", 3, 0, late=2)  # nothing earlier to credit: this window's
+    assert fresh.history("k") == [(5.0, 2.0)]
+
+
+def test_the_first_recovery_window_is_not_attributed_but_sparse_fault_windows_are(tmp_path):
+    """The emission gate's recovery rule (round-5 config 3's two recovery false positives): a window
+    that completes >= 4 requests with none breaching in it is not attributed, although the pooled
+    burn still holds the fault -- the fault's last breaching request arrives in it flagged late. A
+    slow service's fault windows (2-3 requests, some of them clean) keep paging through the pool."""
+    import json
+
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.agent.daemon import Agent, AgentOptions
+    from llm_slo_ebpf_toolkit_amd.models.bayes import NaiveBayes
+
+    path = tmp_path / "d.jsonl"
+    agent = Agent(AgentOptions(output="jsonl", output_path=str(tmp_path / "a.jsonl"), window_ms=1000,
+                               min_confidence=0.0, decision_log=str(path)))
+    model = NaiveBayes.ref()
+    post = np.zeros((1, 16))
+    post[0, 2] = 0.9
+
+    def res(n, b, late=0):
+        return {"post": post, "evbits": np.zeros((1, 16), np.uint32), "feat": np.zeros((1, 16), np.float32),
+                "sli": np.array([[n, b]], np.uint32), "late": np.array([[late, 0]], np.uint32)}
+
+    seq = [(6, 6, 0), (6, 6, 0), (7, 0, 1), (8, 0, 0), (2, 0, 0), (2, 1, 1), (2, 0, 0), (3, 0, 1), (8, 0, 1)]
+    emitted = [len(agent._attributions(1, ["svc"], res(*w), i, model)) for i, w in enumerate(seq)]
+    agent.close()
+    assert emitted == [1, 1, 0, 0, 0, 1, 1, 1, 0]
+    why = [json.loads(x)["why"] for x in path.read_text().splitlines()]
+    assert why[2] == "recovered" and why[3] == "no_burn" and why[8] == "no_burn"
+
+
+def test_receiver_flags_breaches_whose_deadline_passed_before_the_last_cut():
+    from llm_slo_ebpf_toolkit_amd.collector import otlp, records
+    from llm_slo_ebpf_toolkit_amd.signals.metadata import Interner
+
+    m = otlp.SpanMapper(otlp.GroupTable(2), Interner().id)
+    t0 = 1_700_000_000_000_000_000
+    body = {"resourceSpans": [{"resource": {"attributes": [{"key": "service.name", "value": {"stringValue": "s"}}]},
+                               "scopeSpans": [{"spans": [
+                                   {"traceId": f"{i + 1:032x}", "spanId": f"{i + 1:016x}", "name": "r",
+                                    "startTimeUnixNano": str(t0 + i * 50_000_000),
+                                    "endTimeUnixNano": str(t0 + i * 50_000_000 + 900_000_000),
+                                    "attributes": [{"key": "llm.slo.ttft_ms", "value": {"doubleValue": 500.0}}]}
+                                   for i in range(3)]}]}]}
+    spans = otlp.parse_json(json.dumps(body).encode())
+    assert (m.records(spans)["flags"] == 0).all()  # no cut yet, no SLO: nothing is late
+    m.slo_ms, m.late_before_ns = 60.0, t0 + 100_000_000  # deadlines t0+60, +110, +160 ms
+    assert m.records(spans)["flags"].tolist() == [records.SPAN_LATE, 0, 0]
