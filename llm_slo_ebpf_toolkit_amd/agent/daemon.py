@@ -694,8 +694,8 @@ class Agent:
             # recovered: the window itself completed enough requests and none breached in it (a breach
             # whose deadline passed in an earlier window is that window's, SPAN_LATE); the pooled burn
             # still holds the fault's windows, but the service no longer burns
-            recovered = (sli is not None and rec_n > 0 and g < sli.shape[0] and sli[g, 0] >= rec_n
-                         and sli[g, 1] == 0)
+            recovered = (sli is not None and rec_n > 0 and self.o.emit_min_burn > 0 and g < sli.shape[0]
+                         and sli[g, 0] >= rec_n and sli[g, 1] == 0)
             burning = (sli is None or self.o.emit_min_burn <= 0
                        or (cur > 0 and cur >= self.o.emit_min_burn * (1.0 - 1e-9)))
             emit = confident and burning and not recovered

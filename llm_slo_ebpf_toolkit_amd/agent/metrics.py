@@ -21,7 +21,7 @@ from ..export.prometheus import Registry
 from ..signals import catalog
 
 EVENT_KINDS = ("slo", "probe", "both")
-DROP_REASONS = ("rate_limit", "schema", "emit")
+DROP_REASONS = ("rate_limit", "schema", "emit", "xchg_cap", "import_cap")
 
 
 def _nz(v: str, fallback: str) -> str:
@@ -149,6 +149,12 @@ class AgentMetrics:
                 if row[k]:
                     self.probe_events.inc(float(row[k]), s.name, names[k])
         cand, low, overlap, dropped, enriched = (int(x) for x in list(dbg)[:5])
+        d = list(dbg)
+        if len(d) > 6:  # the multi-GPU exchange's losses (mislo_packet.h kDbgXchgDropped / kDbgImportDropped)
+            if d[5]:
+                self.dropped.inc(float(d[5]), "xchg_cap")
+            if d[6]:
+                self.dropped.inc(float(d[6]), "import_cap")
         self.corr.inc(float(cand), "candidate")
         self.corr.inc(float(max(0, low - overlap)), "low_confidence")
         self.corr.inc(float(dropped), "fanout_dropped")

@@ -499,10 +499,10 @@ void WindowEngine::run_part1(int b, hipStream_t st, bool xchg) {
   if (fused_sel)
     launch_select_masked(sig_cols(), rows_, N, sel_cnt_, sel_off_, sel_mask_, sel_stride_,
                          reinterpret_cast<XRec*>(xsend_ + sizeof(XRec)), reinterpret_cast<uint32_t*>(xsend_),
-                         (uint32_t)cfg_.xchg_cap, st);
+                         (uint32_t)cfg_.xchg_cap, st, dbg_ + kDbgXchgDropped);
   else if (xchg)
     launch_select(sig_cols(), rows_, counts, N, sel_cnt_, sel_off_, reinterpret_cast<XRec*>(xsend_ + sizeof(XRec)),
-                  reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, st);
+                  reinterpret_cast<uint32_t*>(xsend_), (uint32_t)cfg_.xchg_cap, st, dbg_ + kDbgXchgDropped);
 }
 
 // Part 2: [the other GPUs' rows] -> partition -> spans -> join (this window's spans x every
@@ -736,7 +736,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
       HIPCHECK(hipMemcpyAsync(xrecv_, inject_.data(), inject_.size(), hipMemcpyHostToDevice, compute_));
       HIPCHECK(hipStreamSynchronize(compute_));  // the host copy is released below
       launch_remote_merge(xrecv_, inject_stride_, inject_world_, inject_me_, imp_[b], remote_n_ + b,
-                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, compute_);
+                          (uint32_t)cfg_.import_cap, cfg_.xchg_cap, compute_, dbg_ + kDbgXchgDropped);
       inject_.clear();
       launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, compute_);
     } else if (xcomm_) {
@@ -746,7 +746,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
       // path (each such hop idled the compute queue 20-45 us, profiles/r5_multigpu/)
       NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, xcomm_, compute_));
       launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[b], remote_n_ + b, (uint32_t)cfg_.import_cap,
-                          cfg_.xchg_cap, compute_);
+                          cfg_.xchg_cap, compute_, dbg_ + kDbgXchgDropped);
       launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, compute_);
     } else {
       // MISLO_XCHG_STREAM=comm: the exchange on the comm stream with the window's other
@@ -755,7 +755,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
       HIPCHECK(hipStreamWaitEvent(comm_stream_, xchg_done_[b], 0));
       NCCLCHECK(ncclAllGather(xsend_, xrecv_, xstride_, ncclUint8, comm_, comm_stream_));
       launch_remote_merge(xrecv_, xstride_, world_, rank_, imp_[b], remote_n_ + b, (uint32_t)cfg_.import_cap,
-                          cfg_.xchg_cap, comm_stream_);
+                          cfg_.xchg_cap, comm_stream_, dbg_ + kDbgXchgDropped);
       launch_window_rows(reinterpret_cast<const int*>(in_dev_[b]), remote_n_ + b, n_rows_, rows_, gen_, comm_stream_);
       HIPCHECK(hipEventRecord(xchg_done_[b], comm_stream_));
       HIPCHECK(hipStreamWaitEvent(compute_, xchg_done_[b], 0));
@@ -1006,10 +1006,22 @@ void WindowEngine::init_comm(const ncclUniqueId& id, int rank, int world) {
     xrecv_ = dalloc<uint8_t>(xstride_ * world);
     xrecv_bytes_ = xstride_ * world;
     HIPCHECK(hipMemset(xrecv_, 0, xrecv_bytes_));
-    // the exchange's own communicator (a split of comm_: every rank, same color), used on the
-    // compute stream only; MISLO_XCHG_STREAM=comm keeps the exchange on the comm stream instead
+    // The exchange runs on the comm stream with the window's other collectives: one communicator,
+    // one stream, one issue order on every rank. MISLO_XCHG_STREAM=compute puts it on the compute
+    // stream over a communicator of its own (ncclCommSplit: 0.60 against 0.62 ms per window in the
+    // one-rank rehearsal, profiles/r5_multigpu/); two communicators then run collectives on two
+    // streams at once, which no run with world >= 2 has exercised yet, so it is opt-in. Rank 0's
+    // choice is broadcast first: ncclCommSplit is collective, and ranks with another env must
+    // neither hang in it nor skip it.
     const char* xv = getenv("MISLO_XCHG_STREAM");
-    if (!(xv && std::strcmp(xv, "comm") == 0)) NCCLCHECK(ncclCommSplit(comm_, 0, rank, &xcomm_, nullptr));
+    int split = (xv && std::strcmp(xv, "compute") == 0) ? 1 : 0;
+    int* d_split = dalloc<int>(1);
+    HIPCHECK(hipMemcpy(d_split, &split, sizeof(int), hipMemcpyHostToDevice));
+    NCCLCHECK(ncclBroadcast(d_split, d_split, 1, ncclInt32, 0, comm_, comm_stream_));
+    HIPCHECK(hipStreamSynchronize(comm_stream_));
+    HIPCHECK(hipMemcpy(&split, d_split, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHECK(hipFree(d_split));
+    if (split) NCCLCHECK(ncclCommSplit(comm_, 0, rank, &xcomm_, nullptr));
   }
 }
 

@@ -68,10 +68,11 @@ __global__ __launch_bounds__(kSelNT) void k_sel_count(SelArgs a, uint32_t* __res
   }
 }
 
-// exclusive scan of <= 1024 block counts; total (clamped to the output capacity) -> *n_out
+// exclusive scan of <= 1024 block counts; total (clamped to the output capacity) -> *n_out, the
+// rows beyond the capacity -> *dropped (the packet's dbg[kDbgXchgDropped]: never silent)
 __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ blk_cnt, int nblk,
                                                   uint32_t* __restrict__ blk_off, uint32_t* __restrict__ n_out,
-                                                  uint32_t out_cap) {
+                                                  uint32_t out_cap, unsigned long long* __restrict__ dropped) {
   __shared__ uint32_t s[1024];
   const int t = threadIdx.x;
   const uint32_t v = t < nblk ? blk_cnt[t] : 0u;
@@ -84,7 +85,10 @@ __global__ __launch_bounds__(1024) void k_sel_scan(const uint32_t* __restrict__ 
     __syncthreads();
   }
   if (t < nblk) blk_off[t] = s[t] - v;
-  if (t == 1023) *n_out = min(s[1023], out_cap);
+  if (t == 1023) {
+    *n_out = min(s[1023], out_cap);
+    if (dropped && s[1023] > out_cap) atomicAdd(dropped, (unsigned long long)(s[1023] - out_cap));
+  }
 }
 
 // ordered scatter: block offset + wave offsets + in-wave ballot rank; 24-byte exchange rows
@@ -168,14 +172,23 @@ __global__ __launch_bounds__(NT) void k_sel_scatter_mask(SignalCols gc, const in
 
 // other GPUs' exchanged rows (each rank's block: a 24-byte header holding its row count, then
 // XRec rows) as identity-free SigRecs, in rank order: appended to the window's own rows
+// Rows that do not fit are counted, never silently lost: a block's rows beyond the all-gathered
+// block size (its sender selected more than was sent) into dropped[0] (dbg[kDbgXchgDropped], by
+// the sender's successor only, so the node-wide sum counts each row once), rows beyond the import
+// capacity into dropped[1] (dbg[kDbgImportDropped]).
 __global__ __launch_bounds__(256) void k_remote_merge(const uint8_t* __restrict__ xrecv, size_t stride, int world,
                                                       int me, SigRec* __restrict__ imp,
-                                                      uint32_t* __restrict__ remote_n, uint32_t imp_cap) {
+                                                      uint32_t* __restrict__ remote_n, uint32_t imp_cap,
+                                                      unsigned long long* __restrict__ dropped) {
   uint32_t off = 0;
+  const uint32_t per_blk = (uint32_t)((stride - sizeof(XRec)) / sizeof(XRec));
   for (int r = 0; r < world; ++r) {
     if (r == me) continue;
     const uint8_t* blk = xrecv + (size_t)r * stride;
-    const uint32_t c = min(*reinterpret_cast<const uint32_t*>(blk), (uint32_t)((stride - sizeof(XRec)) / sizeof(XRec)));
+    const uint32_t hdr = *reinterpret_cast<const uint32_t*>(blk);
+    const uint32_t c = min(hdr, per_blk);
+    if (dropped && hdr > c && (r + 1) % world == me && blockIdx.x == 0 && threadIdx.x == 0)
+      atomicAdd(&dropped[0], (unsigned long long)(hdr - c));
     const XRec* rows = reinterpret_cast<const XRec*>(blk + sizeof(XRec));
     for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < c; j += gridDim.x * 256)
       if (off + j < imp_cap) {
@@ -189,7 +202,10 @@ __global__ __launch_bounds__(256) void k_remote_merge(const uint8_t* __restrict_
       }
     off += c;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *remote_n = off < imp_cap ? off : imp_cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *remote_n = off < imp_cap ? off : imp_cap;
+    if (dropped && off > imp_cap) atomicAdd(&dropped[1], (unsigned long long)(off - imp_cap));
+  }
 }
 
 // rows of the window: rows[0] = local records (decode segment 0), rows[1] = rows[0] + other
@@ -275,28 +291,30 @@ int select_grid(int cap) {
 }
 
 void launch_select(const SignalCols& gc, const int* rows, const int* counts, int cap, uint32_t* blk_cnt,
-                   uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream) {
+                   uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream,
+                   unsigned long long* dropped) {
   const SelArgs a{gc, rows, counts, cap};
   const int g = select_grid(cap);
   hipLaunchKernelGGL(k_sel_count, dim3(g), dim3(kSelNT), 0, stream, a, blk_cnt);
-  hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap);
+  hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap, dropped);
   hipLaunchKernelGGL(k_sel_scatter, dim3(g), dim3(kSelNT), 0, stream, a, blk_off, out, out_cap);
 }
 
 void launch_select_masked(const SignalCols& gc, const int* rows, int cap, const uint32_t* blk_cnt, uint32_t* blk_off,
                           const unsigned long long* mask, int mask_stride, XRec* out, uint32_t* n_out,
-                          uint32_t out_cap, hipStream_t stream) {
+                          uint32_t out_cap, hipStream_t stream, unsigned long long* dropped) {
   const int g = decode_grid(cap);  // segment 0's decode grid (its counts and masks)
-  hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap);
+  hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, stream, blk_cnt, g, blk_off, n_out, out_cap, dropped);
   hipLaunchKernelGGL((k_sel_scatter_mask<1024>), dim3(g), dim3(1024), 0, stream, gc, rows, cap, mask, mask_stride,
                      blk_off, out, out_cap);
 }
 
 void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, uint32_t* remote_n,
-                         uint32_t imp_cap, int max_rows, hipStream_t stream) {
+                         uint32_t imp_cap, int max_rows, hipStream_t stream, unsigned long long* dropped) {
   int g = (max_rows + 255) / 256;
   g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
-  hipLaunchKernelGGL(k_remote_merge, dim3(g), dim3(256), 0, stream, xrecv, stride, world, me, imp, remote_n, imp_cap);
+  hipLaunchKernelGGL(k_remote_merge, dim3(g), dim3(256), 0, stream, xrecv, stride, world, me, imp, remote_n, imp_cap,
+                     dropped);
 }
 
 void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, int* rows, GenMeta* gen,

@@ -114,15 +114,19 @@ struct XRec {
 };
 static_assert(sizeof(XRec) == 24, "exchange rows are 24 bytes");
 // the current generation's warn-level trace-tagged local rows -> out (stable order), count -> n_out
+// dropped (optional): rows over out_cap are added to it (the packet's dbg[kDbgXchgDropped])
 void launch_select(const SignalCols& gc, const int* rows, const int* counts, int cap, uint32_t* blk_cnt,
-                   uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream);
+                   uint32_t* blk_off, XRec* out, uint32_t* n_out, uint32_t out_cap, hipStream_t stream,
+                   unsigned long long* dropped = nullptr);
 // the same selection from the counts and ballot masks segment 0's decode left (sel_cnt /
 // sel_mask): scan, then an ordered scatter that reads only the selected rows
 void launch_select_masked(const SignalCols& gc, const int* rows, int cap, const uint32_t* blk_cnt, uint32_t* blk_off,
                           const unsigned long long* mask, int mask_stride, XRec* out, uint32_t* n_out,
-                          uint32_t out_cap, hipStream_t stream);
+                          uint32_t out_cap, hipStream_t stream, unsigned long long* dropped = nullptr);
+// dropped (optional, [2]): rows beyond a block's sent size / beyond imp_cap (dbg[kDbgXchgDropped],
+// dbg[kDbgImportDropped])
 void launch_remote_merge(const uint8_t* xrecv, size_t stride, int world, int me, SigRec* imp, uint32_t* remote_n,
-                         uint32_t imp_cap, int max_rows, hipStream_t stream);
+                         uint32_t imp_cap, int max_rows, hipStream_t stream, unsigned long long* dropped = nullptr);
 void launch_window_rows(const int* counts, const uint32_t* remote_n, int cap, int* rows, GenMeta* gen,
                         hipStream_t stream);
 // head of a window's graph: the next generation slot and the halo's per-age visibility cut-offs,

@@ -13,6 +13,10 @@ constexpr int kPacketHist = kSlots * kBuckets;          // 256
 constexpr int kPacketStatus = kSlots * 3;               // 48
 constexpr int kPacketMisc = 2 + kSlots;                 // unsupported, zero-ts, per-slot value sums (milli)
 constexpr int kPacketDbg = 8;
+// dbg: [0] candidates [1] low confidence [2] overlap [3] fanout dropped [4] spans enriched, then the
+// multi-GPU exchange's losses: [5] trace rows selected beyond the exchange capacity (or the sent
+// block size), [6] other GPUs' rows beyond the import capacity
+constexpr int kDbgXchgDropped = 5, kDbgImportDropped = 6;
 constexpr int kPacketConf = kMaxDomains * kMaxDomains;  // 256
 constexpr int kPacketStats = 32 * 32;                   // 1024
 constexpr int kPacketCount = kMaxDomains;               // 16

@@ -76,6 +76,8 @@ class ExchangeModel:
         self.gens: list = []                   # newest first: (local rows, other ranks' rows, tmax)
         self.injected = oracle.empty_rows()    # other ranks' rows for the next window (tests)
         self.sent = 0
+        # rows lost to the capacities in the last window (the packet's dbg[5] / dbg[6])
+        self.xchg_dropped = self.import_dropped = 0
 
     def block(self, d_loc: oracle.Decoded) -> Optional[np.ndarray]:
         """Part 1: this rank's exchange block for the window (what the GPU all-gathers)."""
@@ -83,6 +85,7 @@ class ExchangeModel:
             return None
         mine = oracle.trace_rows(d_loc, len(d_loc.ts))
         self.sent = min(len(mine.ts), self.xchg_cap)
+        self.xchg_dropped = len(mine.ts) - self.sent
         return oracle.exchange_blocks([mine], self.xchg_cap)
 
     def halo(self) -> oracle.Decoded:
@@ -107,6 +110,7 @@ class ExchangeModel:
         for r, blk in enumerate(blocks or []):
             if r != self.rank:
                 imp = oracle.concat(imp, parse_block(blk))
+        self.import_dropped = max(0, len(imp.ts) - self.import_cap)
         imp = oracle.take(imp, np.arange(len(imp.ts)) < self.import_cap)
         d = oracle.concat(oracle.concat(d_loc, self.halo()), imp)
         res = oracle.join(d, spans, n_groups, **join_kw)
@@ -115,6 +119,7 @@ class ExchangeModel:
         return res
 
     def window(self, d_loc: oracle.Decoded, spans: np.ndarray, n_groups: int, **join_kw):
+        self.xchg_dropped = self.import_dropped = 0
         blk = self.block(d_loc)
         blocks = self.allgather(blk) if blk is not None and self.allgather is not None else None
         return self.join(d_loc, spans, n_groups, blocks, **join_kw)

@@ -276,6 +276,7 @@ class CpuRingEngine:
         dbg[1] = res.debug["low_confidence"]
         dbg[3] = res.debug["fanout_dropped"]
         dbg[4] = res.debug["spans_enriched"]
+        dbg[5], dbg[6] = self.xm.xchg_dropped, self.xm.import_dropped
         feat = res.feat.astype(np.float32)
         f64 = feat.astype(np.float64)
         D = self.n_dom

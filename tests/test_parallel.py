@@ -1,4 +1,4 @@
-"""Distributed path on CPU (gloo, world_size 2, 127.0.0.1): the engine's multi-GPU window
+"""Distributed path on CPU (gloo, world_size 2 / 4 / 8, 127.0.0.1): the engine's multi-GPU window
 protocol (parallel/exchange.py, the CPU model of ops/csrc/exchange.hip) over a real process
 group -- node-sharded streams, the halo carried across window cuts, warn-level trace rows
 exchanged as 24-byte XRec blocks and imported one window later, the packet all-reduce."""
@@ -17,11 +17,11 @@ WORLD = 2
 HALO_MS, ICAP, XCAP = 2000.0, 20000, 4000
 
 
-def global_windows(n_win=3, seed=3):
-    """Consecutive windows of a 4-node cluster; a third of the trace-tagged events moved to
-    pods on other nodes, so traces cross the node shards."""
-    cfg = ReplayConfig(scenario="full", n_nodes=4, pods_per_node=4, n_services=8, events_per_window=6000,
-                       spans_per_window=400, seed=seed)
+def global_windows(n_win=3, seed=3, n_nodes=4):
+    """Consecutive windows of an ``n_nodes``-node cluster; a third of the trace-tagged events moved
+    to pods on other nodes, so traces cross the node shards."""
+    cfg = ReplayConfig(scenario="full", n_nodes=n_nodes, pods_per_node=4, n_services=8,
+                       events_per_window=1500 * n_nodes, spans_per_window=100 * n_nodes, seed=seed)
     g = ReplayGenerator(cfg)
     rng = np.random.default_rng(seed)
     out = []
@@ -45,11 +45,11 @@ def _free_port():
     return p
 
 
-def _run_rank(rank, wins, allgather, xchg=XCAP):
-    m = exchange.ExchangeModel(rank, WORLD, HALO_MS, ICAP, xchg, allgather)
+def _run_rank(rank, wins, allgather, xchg=XCAP, world=WORLD):
+    m = exchange.ExchangeModel(rank, world, HALO_MS, ICAP, xchg, allgather)
     out = []
     for ev, sp, G in wins:
-        ev_l, sp_l = shard.shard(ev, sp, rank, WORLD)
+        ev_l, sp_l = shard.shard(ev, sp, rank, world)
         d = oracle.decode_events(ev_l)
         res = m.window(d, sp_l, G)
         out.append(dict(feat=res.feat, cnt=res.cnt, gsum=res.gsum, gcnt=res.gcnt, hist=oracle.histograms(d),
@@ -64,7 +64,7 @@ def _worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _run_rank(rank, global_windows(), exchange.torch_allgather())
+        res = _run_rank(rank, global_windows(n_nodes=max(4, 2 * world)), exchange.torch_allgather(), world=world)
         hist = torch.from_numpy(np.stack([r["hist"] for r in res]))
         dist.all_reduce(hist)  # the packet all-reduce: node-wide counters
         np.savez(os.path.join(outdir, f"r{rank}.npz"), hist=hist.numpy(),
@@ -74,12 +74,14 @@ def _worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def _in_memory(wins, xchg=XCAP):
-    """Both ranks in one process, the all-gather done by hand (same blocks)."""
-    ms = [exchange.ExchangeModel(r, WORLD, HALO_MS, ICAP, xchg) for r in range(WORLD)]
-    out = [[] for _ in range(WORLD)]
+def _in_memory(wins, xchg=XCAP, world=WORLD, icap=ICAP, models=None):
+    """Every rank in one process, the all-gather done by hand (same blocks)."""
+    ms = [exchange.ExchangeModel(r, world, HALO_MS, icap, xchg) for r in range(world)]
+    if models is not None:
+        models.extend(ms)
+    out = [[] for _ in range(world)]
     for ev, sp, G in wins:
-        loc = [shard.shard(ev, sp, r, WORLD) for r in range(WORLD)]
+        loc = [shard.shard(ev, sp, r, world) for r in range(world)]
         ds = [oracle.decode_events(e) for e, _ in loc]
         blocks = [m.block(d) for m, d in zip(ms, ds)]
         for r, m in enumerate(ms):
@@ -142,29 +144,53 @@ def test_exchange_block_roundtrip():
     assert (back.pod == 0).all() and (back.conn == 0).all() and (rows.status >= 1).all()
 
 
-@pytest.mark.timeout(300)
-def test_gloo_two_ranks_run_the_device_protocol(tmp_path):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_ranks_run_the_device_protocol(tmp_path, world):
+    """2, 4 and 8 gloo ranks (the node sizes bench.py --gpus runs) reproduce the single-process
+    model of the same ranks exactly: features, candidates and group counts per rank and window."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_worker, args=(WORLD, _free_port(), str(tmp_path)), nprocs=WORLD, join=True)
-    wins = global_windows()
-    ref = _in_memory(wins)
-    solo = _in_memory(wins, xchg=0)  # the same ranks without the exchange
-    got = [np.load(tmp_path / f"r{k}.npz") for k in range(WORLD)]
-    for r in range(WORLD):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    wins = global_windows(n_nodes=max(4, 2 * world))
+    ref = _in_memory(wins, world=world)
+    solo = _in_memory(wins, xchg=0, world=world)  # the same ranks without the exchange
+    got = [np.load(tmp_path / f"r{k}.npz") for k in range(world)]
+    for r in range(world):
         for j in range(len(wins)):
             np.testing.assert_array_equal(got[r][f"feat{j}"], ref[r][j].feat)
             np.testing.assert_array_equal(got[r][f"cnt{j}"], ref[r][j].cnt)
             np.testing.assert_array_equal(got[r][f"gcnt{j}"], ref[r][j].gcnt)
-        assert (got[r]["sent"] > 0).all() and (got[r]["n_rows"] > got[r]["n_loc"]).all()
+        if got[r]["n_loc"].sum():  # a rank the node hash gave no node has nothing to send
+            assert (got[r]["sent"] > 0).all() and (got[r]["n_rows"] > got[r]["n_loc"]).all()
+        else:  # but it still imports the others' rows
+            assert (got[r]["n_rows"] > 0).all()
+    assert sum(int(got[r]["n_loc"].sum() > 0) for r in range(world)) >= world - 1
     # cross-node traces: the exchange adds the other shard's elevated signals to the spans'
     # candidates in the same window
     for j in range(len(wins)):
-        extra = sum(int(ref[r][j].cnt.sum() - solo[r][j].cnt.sum()) for r in range(WORLD))
+        extra = sum(int(ref[r][j].cnt.sum() - solo[r][j].cnt.sum()) for r in range(world))
         assert extra > 0, j
     # node-wide counters: the all-reduced per-rank histograms are the global histograms
     for j, (ev, _, _) in enumerate(wins):
         np.testing.assert_array_equal(got[0]["hist"][j], oracle.histograms(oracle.decode_events(ev)))
+
+
+def test_exchange_losses_are_counted_not_silent():
+    """Rows over the exchange capacity (a rank selected more than its block holds) and over the
+    import capacity (more peer rows than the window imports) are counted -- the packet's dbg[5] /
+    dbg[6], llm_slo_agent_dropped_events_total{reason="xchg_cap"|"import_cap"} -- and the rows kept
+    are the first ones, in rank order."""
+    wins = global_windows(2, n_nodes=8)
+    ms = []
+    _in_memory(wins, xchg=50, world=8, icap=200, models=ms)
+    full = []
+    _in_memory(wins, xchg=100000, world=8, icap=10 ** 7, models=full)
+    for m, f in zip(ms, full):
+        assert m.sent == min(50, f.sent) and m.xchg_dropped == max(0, f.sent - 50)
+        assert m.import_dropped > 0  # 7 peers x up to 50 rows > 200
+    assert sum(m.xchg_dropped for m in ms) > 0
+    assert all(f.xchg_dropped == 0 and f.import_dropped == 0 for f in full)
 
 
 def test_numa_cpulist_and_affinity_choice(tmp_path):

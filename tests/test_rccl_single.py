@@ -44,14 +44,14 @@ def _run(tag, comm, wins, imgs, gen):
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("xchg_stream", ["compute", "comm"])
 def test_one_rank_rccl_communicator_matches_the_communicator_free_engine(xchg_stream, monkeypatch):
-    """xchg_stream: the trace-row exchange on the compute stream over its own (split)
-    communicator (the default), or on the comm stream with the window's other collectives
-    (MISLO_XCHG_STREAM=comm)."""
+    """xchg_stream: the trace-row exchange on the comm stream with the window's other collectives
+    (the default: one communicator, one stream), or on the compute stream over a communicator of
+    its own (MISLO_XCHG_STREAM=compute: a split decided on rank 0 and broadcast)."""
     from llm_slo_ebpf_toolkit_amd.ops import load_agent
     from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images
 
-    if xchg_stream == "comm":
-        monkeypatch.setenv("MISLO_XCHG_STREAM", "comm")
+    if xchg_stream == "compute":
+        monkeypatch.setenv("MISLO_XCHG_STREAM", "compute")
     else:
         monkeypatch.delenv("MISLO_XCHG_STREAM", raising=False)
     wins, gen = windows(n_win=4, seed=71)
@@ -90,7 +90,7 @@ def test_the_exchange_block_is_the_oracles_trace_row_selection():
 
     wins, gen = windows(n_win=4, seed=73)
     imgs = build_replay_images(wins)
-    _, info = _run("sel", (load_agent().unique_id(), 0, 1), wins, imgs, gen)
+    out, info = _run("sel", (load_agent().unique_id(), 0, 1), wins, imgs, gen)
     pods, sn = _pm(gen)
     pod_sn = dict(zip(pods.tolist(), sn.tolist()))
     table, tmap = oracle.CtxTable(), oracle.TraceMap()
@@ -107,4 +107,6 @@ def test_the_exchange_block_is_the_oracles_trace_row_selection():
         w = oracle.XREC.itemsize
         np.testing.assert_array_equal(got[w:w * (1 + n_dev)], ref[w:w * (1 + n_dev)], err_msg=f"window {j}")
         n_sel.append(n_dev)
+        # rows beyond the exchange capacity are counted (dbg[5]), never silently lost
+        assert int(out[j][0]["dbg"][5]) == max(0, len(mine.ts) - 1024), (j, out[j][0]["dbg"][:8])
     assert min(n_sel) > 0, "no trace rows selected: the comparison would be vacuous"
