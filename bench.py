@@ -472,7 +472,8 @@ def main() -> int:
         pipe.eng.restore(st, model_bytes(model), int(pipe.windows_folded))
         kw = mtrain.learned_kwargs(tcfg)
         pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"])
-        pipe.eng.set_refit(tcfg.alpha, tcfg.prior_pseudo, 1.0 / T, tcfg.min_count, pipe.cap_dom())
+        pipe.eng.set_refit(mtrain.learned_kwargs(tcfg)["alpha"], tcfg.prior_pseudo, 1.0 / T, tcfg.min_count,
+                           pipe.cap_dom())
         pipe.eng.refit_now()
         pipe.eng.set_device_refit(False)  # frozen from here on: the timed region scores, as the agent does
         pipe.device_refit = False
@@ -484,7 +485,7 @@ def main() -> int:
             "events_per_window": a.train_events, "scenarios": list(mtrain.TRAIN_SCENARIOS), "seed": a.seed,
             "active_domains": [d for i, d in enumerate(catalog_domains()) if np.isfinite(model.bias[i])]})
         train_info = {"windows": len(train_imgs), "held_out": len(hold_f), "temperature": round(T, 4),
-                      "likelihood_prior": tcfg.init, "alpha": tcfg.alpha, "unknown_calibrated": tcfg.calibrate_unknown,
+                      "likelihood_prior": tcfg.init, "alpha": mtrain.learned_kwargs(tcfg)["alpha"], "unknown_calibrated": tcfg.calibrate_unknown,
                       "pair_rho": round(rho, 4),
                       "holdout_nll": round(nll, 4), "holdout_nll_t1": round(trained.meta["holdout_nll_t1"], 4),
                       "seconds": round(train_s, 3), "events_per_window": a.train_events,

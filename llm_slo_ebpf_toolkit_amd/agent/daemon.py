@@ -152,8 +152,9 @@ class AgentOptions:
                                          # <= 0: every scored group, REF's emit-per-tick)
     emit_min_requests: float = 8.0       # the gate's burn "now": the last windows (at most 3) holding this many
                                          # requests -- one busy window with no breach ends a page
-    emit_recovered_requests: int = 4     # a window completing at least this many requests, none breaching in it,
-                                         # is recovered: not attributed (0 = off)
+    emit_recovered_requests: int = -1    # a window completing at least this many requests, none breaching in it,
+                                         # is recovered: not attributed (0 = off; -1 = 4 per second of window,
+                                         # at least 2)
     emit_wait_ms: int = 250              # after a cut, wait up to this long for the window's results (0 = emit
                                          # window k at cut k+1)
     decision_log: str = ""               # JSONL of every scored group per window, emitted or not, and why
@@ -684,6 +685,8 @@ class Agent:
         any_live = bool(live.any())
         late_l = res["late"][:, 0].tolist() if res.get("late") is not None else []
         rec_n = int(self.o.emit_recovered_requests)
+        if rec_n < 0:  # 4 requests per 1 s window (the first recovery windows of config 3), at least 2
+            rec_n = max(2, int(round(4 * self.o.window_ms / 1000.0)))
         for g in range(G):
             if g < len(reqs) and reqs[g] == 0 and not (g < len(late_l) and late_l[g]):
                 continue  # no request of this group in the window: no incident to attribute

@@ -116,7 +116,8 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                                    "(at most 3) holding this many requests"),
         ("emit-recovered-requests", d.emit_recovered_requests, "gpu engine: a window that completes at least "
                                                                "this many requests of a group, none breaching "
-                                                               "its SLO in the window, is not attributed (0 = off)"),
+                                                               "its SLO in the window, is not attributed (0 = off, "
+                                                               "-1 = 4 per second of window, at least 2)"),
         ("decision-log", d.decision_log, "gpu engine: JSONL of every scored incident group per window -- "
                                          "requests, breaches, burn, top posteriors, emitted or why not (\"\" = off)"),
         ("gpu-hw-queues", 1, "gpu engine: cap on HIP hardware queues (GPU_MAX_HW_QUEUES; the flag given on the "

@@ -75,6 +75,11 @@ class TrainConfig:
     # training mass. Chosen on held-out replay windows only (another seed; complete and partial
     # symptom sets): 2 -> 0.986 / 0.783, 10 -> 0.986 / 0.809, 15 -> 0.986 / 0.803 macro-F1
     alpha: float = 10.0
+    # the pseudo-count with the random-init table (init = "random"): a random table carries no
+    # knowledge, so it weighs one incident. Chosen on held-out replay only: alpha 1 / 2 / 5 / 10 ->
+    # full-set macro-F1 0.9928 / 0.9928 / 0.9928 / 0.985, mixed_multi coverage@0.10 1.0 / 1.0 /
+    # 0.9961 / 0.9961 (round 6, 48 windows)
+    random_alpha: float = 1.0
     prior_pseudo: float = 1.0
     min_count: float = 1.0            # labelled mass below which a domain stays inactive
     holdout_every: int = 4            # every 4th window is held out for the temperature fit
@@ -95,6 +100,9 @@ class TrainConfig:
     # each elevated symptom of a fault shows with this probability in a training incident
     # (pipeline/replay.py ReplayConfig.symptom_keep)
     symptom_keep: float = 1.0
+    # > 0: one more training scenario, the single faults with each symptom kept at this
+    # probability (incidents that show part of their fault's signature, as live ones do)
+    partial_keep: float = 0.0
 
 
 @dataclass
@@ -120,15 +128,36 @@ def ensure_scenarios() -> None:
     replay.SCENARIOS.setdefault("compound", list(COMPOUND))
 
 
+def training_mix(cfg: TrainConfig) -> List[Tuple[str, float]]:
+    """(scenario, symptom keep) of each training generator, in the order windows cycle over them."""
+    mix = [(s, cfg.symptom_keep) for s in TRAIN_SCENARIOS]
+    if cfg.partial_keep > 0:
+        mix.append(("full", cfg.partial_keep))
+    return mix
+
+
+def held_out(window_ids, cfg: TrainConfig) -> np.ndarray:
+    """Which training windows are held out for the temperature fit: every ``holdout_every``-th
+    window, counted so that the windows of every training generator are held out in turn (a plain
+    ``j % holdout_every`` with as many generators as ``holdout_every`` would hold out one
+    generator's windows only -- and never learn from them)."""
+    j = np.asarray(window_ids, dtype=np.int64)
+    n = len(training_mix(cfg))
+    k = cfg.holdout_every
+    if n % k == 0 or k % n == 0:
+        return ((j // n + j % n) % k) == k - 1
+    return (j % k) == k - 1
+
+
 def training_windows(cfg: TrainConfig):
-    """The fixed training set: windows alternating over TRAIN_SCENARIOS (seeded, deterministic)."""
+    """The fixed training set: windows alternating over training_mix (seeded, deterministic)."""
     from ..pipeline.replay import ReplayConfig, ReplayGenerator
 
     ensure_scenarios()
     gens = [ReplayGenerator(ReplayConfig(scenario=s, n_services=cfg.services, events_per_window=cfg.events_per_window,
                                          spans_per_window=cfg.spans_per_window, seed=cfg.seed + 101 * i,
-                                         symptom_keep=cfg.symptom_keep))
-            for i, s in enumerate(TRAIN_SCENARIOS)]
+                                         symptom_keep=keep))
+            for i, (s, keep) in enumerate(training_mix(cfg))]
     return [gens[j % len(gens)].next_window() for j in range(cfg.windows)]
 
 
@@ -229,7 +258,8 @@ def likelihood_codes(codes: np.ndarray, cfg: Optional[TrainConfig] = None) -> np
 
 def learned_kwargs(cfg: TrainConfig) -> Dict[str, object]:
     """NaiveBayes.learned's keyword arguments for a training config (host fit, bench, device refit)."""
-    return {"alpha": cfg.alpha, "seed": cfg.seed, "prior_pseudo": cfg.prior_pseudo, "min_count": cfg.min_count,
+    return {"alpha": cfg.alpha if cfg.init == "expert" else cfg.random_alpha, "seed": cfg.seed,
+            "prior_pseudo": cfg.prior_pseudo, "min_count": cfg.min_count,
             "init": NaiveBayes.expert_table() if cfg.init == "expert" else None,
             "floor": NaiveBayes.unknown_floor() if cfg.calibrate_unknown else None,
             "cap_domain": "unknown" if cfg.calibrate_unknown else None}
@@ -250,7 +280,7 @@ def fit(feats: np.ndarray, codes: np.ndarray, window_ids: np.ndarray, cfg: Train
     """Statistics on the training windows, temperature on the held-out ones."""
     feats = np.asarray(feats, dtype=np.float64)
     Y = soft_labels(codes)
-    hold = (np.asarray(window_ids) % cfg.holdout_every) == cfg.holdout_every - 1
+    hold = held_out(window_ids, cfg)
     tr = ~hold & (np.asarray(codes) >= 0)
     st = SufficientStats()
     single = likelihood_codes(codes, cfg) >= 0
@@ -278,7 +308,7 @@ def train_cpu(cfg: Optional[TrainConfig] = None) -> TrainedModel:
     wins = training_windows(cfg)
     feats, codes, wid = cpu_features(wins)
     tm = fit(feats, codes, wid, cfg)
-    tm.meta.update({"engine": "cpu-oracle", "config": asdict(cfg), "scenarios": list(TRAIN_SCENARIOS)})
+    tm.meta.update({"engine": "cpu-oracle", "config": asdict(cfg), "scenarios": [f"{s}@{k:g}" for s, k in training_mix(cfg)]})
     return tm
 
 

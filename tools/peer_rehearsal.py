@@ -1,0 +1,133 @@
+"""Worker 0 of an 8-GPU node, rehearsed on one MI355X at the headline window:
+the device time of a window when the seven other GPUs' trace-row blocks arrive full.
+
+Three runs over the same bench-shaped windows (config 5: 1M events, 16,384 spans, 64 incident
+groups, 2 s halo):
+
+* ``solo``   -- the one-GPU chain (no exchange);
+* ``empty``  -- the exchange path with seven empty peer blocks (the chain's structure: selection,
+                merge, the second decode segment, two graphs);
+* ``full``   -- seven peer blocks of up to ``--xchg-cap`` rows each (458,752 rows at 65,536):
+                the window's own warn-level trace-tagged rows (oracle.trace_rows), each peer's
+                copy shifted by 1-7 ms, so every imported row reaches spans through the trace tier
+                -- the worst case of a node whose requests all cross every GPU.
+
+Peer blocks are injected where the RCCL all-gather would deliver them (``inject_remote``: a host
+copy and a stream sync per window, outside the device timing). Reported per run: the median and
+mean device compute time per window (events on the compute stream around the chain), imported
+rows, candidates and the import / exchange drop counters. The all-gather itself cannot run with
+one rank on one device; the projection adds the xGMI ring all-gather time of 8 blocks.
+
+    python tools/peer_rehearsal.py --out gpurun_out/r6_multigpu/peers.json
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--windows", type=int, default=16)
+    ap.add_argument("--events", type=int, default=1 << 20)
+    ap.add_argument("--spans", type=int, default=16384)
+    ap.add_argument("--services", type=int, default=64)
+    ap.add_argument("--xchg-cap", type=int, default=65536)
+    ap.add_argument("--peers", type=int, default=7)
+    ap.add_argument("--xgmi-gbs", type=float, default=64.0, help="per-link unidirectional xGMI bandwidth (GB/s) "
+                                                                "for the all-gather projection")
+    ap.add_argument("--out", default="gpurun_out/r6_multigpu/peers.json")
+    a = ap.parse_args()
+    import numpy as np
+
+    from llm_slo_ebpf_toolkit_amd.collector.records import framed_rows
+    from llm_slo_ebpf_toolkit_amd.pipeline import oracle
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import Cut, RingWindowSource, WindowPipeline, build_replay_images
+    from llm_slo_ebpf_toolkit_amd.runtime import load
+
+    rt = load()
+    t0 = time.time()
+    gen = ReplayGenerator(ReplayConfig(events_per_window=a.events, spans_per_window=a.spans, n_services=a.services))
+    wins = [gen.next_window() for _ in range(4)]
+    imgs = build_replay_images(wins)
+    world = a.peers + 1
+    blocks_full, blocks_empty, n_rows = [], [], []
+    for w in wins:
+        tr = oracle.trace_rows(oracle.decode_events(w.events), len(w.events))
+        parts = [oracle.empty_rows()]
+        for p in range(a.peers):
+            d = oracle.take(tr, np.arange(len(tr.ts)) < a.xchg_cap)
+            d.ts = d.ts + (p + 1) * 1_000_000
+            parts.append(d)
+        blocks_full.append(oracle.exchange_blocks(parts, a.xchg_cap))
+        blocks_empty.append(oracle.exchange_blocks([oracle.empty_rows()] * world, a.xchg_cap))
+        n_rows.append(sum(min(len(p.ts), a.xchg_cap) for p in parts))
+    print(f"[peers] {len(wins)} windows built in {time.time() - t0:.1f}s; peer rows per window {n_rows}", flush=True)
+    n_user = max(len(i.user) for i in imgs)
+    budget = max(framed_rows(i.framed) + len(i.user) for i in imgs)
+    out = {"events": a.events, "spans": a.spans, "groups": a.services, "xchg_cap": a.xchg_cap, "peers": a.peers,
+           "peer_rows_per_window": n_rows, "runs": {}}
+    for mode in ("solo", "empty", "full"):
+        tag = f"/mislo-peer-{os.getpid()}-{mode}"
+        rb = rt.Ringbuf.create_shm(tag, 1 << 28)
+        user = rt.HostRing(1 << int(np.ceil(np.log2(n_user * 4))), 64)
+        spans = rt.HostRing(1 << int(np.ceil(np.log2(a.spans * 4))), 64)
+        xc = a.xchg_cap if mode != "solo" else 0
+        pipe = WindowPipeline(budget, a.spans, a.services, 0, None, model="bayes", learn=False,
+                              user_cap=1 << int(np.ceil(np.log2(n_user))), halo_ms=2000.0,
+                              import_cap=a.peers * xc, xchg_cap=xc)
+        pipe.eng.set_pods(gen.pod_ids.astype(np.uint32),
+                          (gen.pod_svc.astype(np.uint32) << np.uint32(16)) | gen.pod_node.astype(np.uint32))
+        src = RingWindowSource(pipe, rb, user, spans)
+        comp, total, dbg = [], [], []
+        for i in range(a.windows):
+            j = i % len(imgs)
+            img = imgs[j]
+            if mode != "solo":
+                pipe.inject_remote(blocks_full[j] if mode == "full" else blocks_empty[j], world=world, me=0)
+            src.reap(keep=1)
+            while not rb.append_framed(img.framed, 8):
+                src.reap(keep=0)
+            user.push(img.user, 4)
+            spans.push(img.spans)
+            k = src.stage(Cut(rb.producer_pos, user.head, spans.head, img.bases), img.n_groups, img.labels)["k"]
+            pk = pipe.packet(k)
+            ms_total, ms_comp = pipe.window_ms(k)
+            if i >= 2:  # the first windows capture the graphs
+                comp.append(ms_comp)
+                total.append(ms_total)
+                dbg.append(pk["dbg"][:8].astype(np.int64).tolist())
+        src.drain()
+        pipe.eng.close()
+        d = np.array(dbg)
+        r = {"compute_ms_median": round(float(np.median(comp)), 4), "compute_ms_mean": round(float(np.mean(comp)), 4),
+             "dma_to_results_ms_median": round(float(np.median(total)), 4),
+             "candidates_mean": int(d[:, 0].mean()), "xchg_dropped": int(d[:, 5].sum()),
+             "import_dropped": int(d[:, 6].sum()), "windows_timed": len(comp)}
+        out["runs"][mode] = r
+        print(f"[peers] {mode}: {r}", flush=True)
+    blk = 24 * (1 + a.xchg_cap)
+    ag_ms = (world - 1) * blk / (a.xgmi_gbs * 1e9) * 1e3  # ring all-gather: (N-1) blocks over one link
+    out["allgather_ms_projected"] = round(ag_ms, 4)
+    out["allgather_bytes_per_gpu"] = world * blk
+    out["projected_ms_per_window_n8"] = round(out["runs"]["full"]["compute_ms_median"] + ag_ms, 4)
+    out["note"] = ("one rank on one GPU: the all-gather is projected from the block bytes at --xgmi-gbs per link "
+                   "(a ring all-gather moves N-1 blocks over each link); the exchange runs on the comm stream "
+                   "between the window's two graphs, so it adds to the window unless another window's chain "
+                   "covers it")
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
