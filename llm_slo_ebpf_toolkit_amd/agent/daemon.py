@@ -408,7 +408,11 @@ class Agent:
                              namespace=self.o.namespace, service=self.o.service, fault_label=sample.fault_label,
                              confidence=0.9, burn_rate=2.0, window_minutes=5, request_id=sample.request_id,
                              trace_id=sample.trace_id)
-            self.webhook_q.send(self.bayes.attribute_sample(fs))
+            try:  # a failed attribution is logged and counted; it never ends the tick loop
+                self.webhook_q.send(self.bayes.attribute_sample(fs))
+            except Exception as exc:  # noqa: BLE001
+                print(f"attribution for the webhook failed: {exc}", file=sys.stderr)
+                self.metrics.inc_dropped("emit")
         self._guard_tick()
         self.metrics.set_heartbeat(t_ns / 1e9)
 

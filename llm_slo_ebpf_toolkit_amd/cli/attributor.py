@@ -34,6 +34,10 @@ from ..models.sample import FaultSample, load_samples_jsonl
 from ..utils.timeutil import format_rfc3339_s, now_ns
 from ._common import GoFlags, eprint, ensure_parent, is_version_request, jsonl_line, open_output, print_version
 
+# the model `attributor --train` shipped with the toolkit (agent --model-path in the DaemonSet)
+SHIPPED_MODEL = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                             "config", "models", "mislo-learned.safetensors")
+
 
 def default_sample() -> FaultSample:
     return FaultSample(incident_id="inc-1", timestamp=now_ns(), cluster="local", namespace="default",
@@ -162,6 +166,9 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 1
     mode = a.attribution_mode
     model = None
+    if not a.model_path and metrics.normalize_mode(mode) == "bayes_learned":
+        # the shipped trained model (config/models/mislo-learned.safetensors) unless another is given
+        a.model_path = SHIPPED_MODEL
     if a.model_path:
         from ..models.train import load_model
 
@@ -174,7 +181,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     elif metrics.normalize_mode(mode) != metrics.MODE_RULE:
         from ..models.bayes import get_model
 
-        if metrics.normalize_mode(mode) in ("bayes_learned", "lda"):
+        if metrics.normalize_mode(mode) == "lda":
             eprint(f"attribution-mode {mode} is learned: give --model-path (attributor --train writes one)")
             return 1
         model = get_model(metrics.normalize_mode(mode))

@@ -14,6 +14,7 @@
 // rules (pkg/collector/ringbuf.go:199-238) for replaying REF ring-buffer captures.
 #include "mislo_common.h"
 #include "mislo_launch.h"
+#include <stdexcept>
 
 namespace mislo {
 
@@ -828,6 +829,11 @@ void launch_decode_window(const uint8_t* framed, const void* user, const int* n_
                           const SignalCols& cols, uint32_t* hist, uint32_t* status_cnt, uint32_t* part_cnt,
                           unsigned long long* misc, hipStream_t stream, int seg, int grid, int blk_base, int sh_rank,
                           int sh_world, uint32_t* sel_cnt, unsigned long long* sel_mask, int sel_stride) {
+  // the fused exchange selection (sel_mask) is scattered by k_sel_scatter_mask with
+  // decode_grid(cap) blocks and decode_sel_stride(cap) masks per block: the decode that writes the
+  // masks must run that very geometry
+  if (sel_mask != nullptr && (grid != 0 || sel_stride != decode_sel_stride(cap)))
+    throw std::invalid_argument("launch_decode_window: the fused selection needs the default decode grid");
   DecodeOut o{cols, hist, status_cnt, part_cnt, misc, blk_base, sel_cnt, sel_mask, sel_stride};
   constexpr int NT = kDecodeNT;
   hipLaunchKernelGGL((k_decode_window<NT>), dim3(grid > 0 ? grid : decode_grid(cap)), dim3(NT), 0, stream, framed,

@@ -699,6 +699,14 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_done_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, h2d_part_[b], 0));
   HIPCHECK(hipStreamWaitEvent(compute_, comm_done_[b], 0));  // packet b no longer reduced / read
+  const bool injected = !inject_.empty();
+  if (injected) {
+    // rows as the other GPUs would have delivered them (tests, replays): on the device before the
+    // window's timed chain (the all-gather they stand for is not the chain's), after window k-1's
+    // merge read the receive buffer (compute stream order); the host copy is released here
+    HIPCHECK(hipMemcpyAsync(xrecv_, inject_.data(), inject_.size(), hipMemcpyHostToDevice, compute_));
+    HIPCHECK(hipStreamSynchronize(compute_));
+  }
   HIPCHECK(hipEventRecord(t_comp0_[b], compute_));
   // the head (counts, epoch bases, labels: < 1 KiB) by a kernel load from pinned host memory on
   // the compute stream: a small hipMemcpyAsync H2D is written by the host through the BAR and
@@ -714,7 +722,6 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
                     p0_ + kSlots * 16, cfg_.cap_dom);
     ++folded_;
   }
-  const bool injected = !inject_.empty();
   const bool xchg = exchange() || injected;
   const auto tl = std::chrono::steady_clock::now();
   pre_us_ += std::chrono::duration<double, std::micro>(tl - te).count();
@@ -732,9 +739,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     }
     launch_part(1, b, n_groups, with_labels, learn, true);
     // the exchange sits between the window's two halves: every GPU's trace rows of THIS window
-    if (injected) {  // rows as the other GPUs would have delivered them (tests, replays)
-      HIPCHECK(hipMemcpyAsync(xrecv_, inject_.data(), inject_.size(), hipMemcpyHostToDevice, compute_));
-      HIPCHECK(hipStreamSynchronize(compute_));  // the host copy is released below
+    if (injected) {  // rows as the other GPUs would have delivered them (copied above)
       launch_remote_merge(xrecv_, inject_stride_, inject_world_, inject_me_, imp_[b], remote_n_ + b,
                           (uint32_t)cfg_.import_cap, cfg_.xchg_cap, compute_, dbg_ + kDbgXchgDropped);
       inject_.clear();

@@ -192,11 +192,14 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
   // one) when those uprobes report, else the HIP synchronize and copy calls
   std::map<uint32_t, bool> hip_active;
   std::map<uint32_t, uint64_t> pod_wait;
+  // pods whose uprobes report: a measured wait of 0 is "did not block", not "no measurement"
+  std::map<uint32_t, bool> pod_reports;
   std::map<uint32_t, HipActivity> hip_now;
   for (const auto& tp : targets_) {
     HipActivity a;
     if (!hip_locked(tp.first, &a)) continue;
     hip_now[tp.first] = a;
+    if (a.waits || a.syncs) pod_reports[tp.second] = true;  // the wait / synchronize uprobes have fired
     const auto pv = hip_prev_.find(tp.first);
     if (pv == hip_prev_.end()) continue;
     const HipActivity& b = pv->second;
@@ -220,11 +223,13 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
     s.active = a.own_hot > 0 || hip_active.count(s.pod);
     const auto pw = pod_wait.find(s.pod);
     s.gpu_wait_ns = pw != pod_wait.end() ? pw->second : 0;
+    s.wait_reported = pod_reports.count(s.pod) > 0;
     ++st_.decisions;
     if (dt && s.active && (mask >> kSigGpuQueue & 1) && s.share * 100.0 >= (double)cfg_.floor_pct) {
-      // the pod's measured GPU wait, the share of it other processes held the GPU; without the
-      // uprobes, the share of the interval
-      const uint64_t base = s.gpu_wait_ns ? std::min<uint64_t>(s.gpu_wait_ns, dt) : dt;
+      // the pod's measured GPU wait, the share of it other processes held the GPU (a pod that did
+      // not block this interval: 0); without the uprobes, the share of the interval (ADVICE r5:
+      // a 0 wait no longer jumps to the whole interval)
+      const uint64_t base = s.wait_reported ? std::min<uint64_t>(s.gpu_wait_ns, dt) : dt;
       const uint64_t v = (uint64_t)(s.share * (double)base);
       // stamped with the pod's first process on that GPU
       for (const auto& tp : targets_) {

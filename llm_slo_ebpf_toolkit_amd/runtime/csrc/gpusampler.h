@@ -77,7 +77,8 @@ struct GpuShare {
   uint64_t samples = 0, hot = 0, own_hot = 0;
   double share = 0.0, foreign_mean = 0.0;
   bool active = false;
-  uint64_t gpu_wait_ns = 0;  // the pod's host-side GPU wait over the interval (0: no HIP / ROCr uprobes)
+  uint64_t gpu_wait_ns = 0;  // the pod's host-side GPU wait over the interval
+  bool wait_reported = false;  // the pod's HIP / ROCr uprobes report (gpu_wait_ns is measured, 0 included)
   uint64_t delay_ns = 0;     // the gpu_queue_delay_ms value decided (0: none emitted)
 };
 

@@ -599,6 +599,7 @@ class PyGpuSampler {
       d["own_hot"] = g.own_hot;
       d["share"] = g.share;
       d["gpu_wait_ns"] = g.gpu_wait_ns;
+      d["wait_reported"] = g.wait_reported;
       d["delay_ns"] = g.delay_ns;
       d["foreign_mean"] = g.foreign_mean;
       d["active"] = g.active;

@@ -52,6 +52,17 @@ def test_attributor_ref_dataset_macro_f1(tmp_path):
     assert s["partial_accuracy"] == pytest.approx(0.9818, abs=1e-4)
 
 
+def test_attributor_bayes_learned_defaults_to_the_shipped_model(tmp_path):
+    """`attributor --attribution-mode bayes_learned` without --model-path scores with the shipped
+    trained model (config/models/mislo-learned.safetensors), as the DaemonSet's agent does."""
+    summ = tmp_path / "s.json"
+    rc = attributor.main(["--attribution-mode", "bayes_learned", "--input", os.path.join(FIXTURES, "ref_multi_fault_samples.jsonl"),
+                          "--out", str(tmp_path / "a.jsonl"), "--summary-out", str(summ)])
+    assert rc == 0
+    s = json.loads(summ.read_text())
+    assert s["attribution_mode"] == "model:mislo-learned.safetensors" and s["single_fault_macro_f1"] == 1.0
+
+
 def test_attributor_default_sample_rule_mode(capsys):
     assert attributor.main(["--attribution-mode", "rule"]) == 0
     row = json.loads(capsys.readouterr().out.strip())

@@ -364,3 +364,38 @@ def test_a_pods_measured_gpu_wait_is_the_delay_other_processes_held_it(tmp_path)
                        copy_ns=int(0.05 * DT))
     r = recs(s.decide(0, 3 * DT))
     assert r.size == 1 and r[0]["value"] == int(0.15 * DT)
+
+
+def test_an_active_pod_that_did_not_wait_gets_no_delay(tmp_path):
+    """with the uprobes reporting, a pod that launched work but never blocked on the GPU
+    this interval has a measured wait of 0 -- its delay is 0 (share x 0), not the whole interval
+    (the fallback for pods without the uprobes)."""
+    k = Kfd(tmp_path)
+    k.proc_on(100, [7])
+    k.proc_on(200, [7])
+    s = sampler(k)
+    s.set_target_list([(100, 5)])
+    s.set_hip_activity(100, launches=1, waits=4, wait_ns=1000)
+    s.decide(0, DT)
+    k.occ(200, 7, 64)
+    for _ in range(5):
+        s.sample()
+    s.set_hip_activity(100, launches=9, waits=4, wait_ns=1000)  # launched more, waited no more
+    r = recs(s.decide(0, 2 * DT))
+    sh = s.shares()[0]
+    assert sh["active"] and sh["wait_reported"] and sh["gpu_wait_ns"] == 0
+    assert r.size == 0 or int(r[0]["value"]) == 0
+    # a pod whose uprobes never fired (no HIP runtime hooks): the interval's share, as before
+    k2 = Kfd(tmp_path / "b")
+    k2.proc_on(100, [7])
+    k2.proc_on(200, [7])
+    s2 = sampler(k2)
+    s2.set_target_list([(100, 5)])
+    s2.decide(0, DT)
+    k2.occ(100, 7, 1)
+    k2.occ(200, 7, 64)
+    for _ in range(5):
+        s2.sample()
+    r2 = recs(s2.decide(0, 2 * DT))
+    assert not s2.shares()[0]["wait_reported"]
+    assert r2.size == 1 and int(r2[0]["value"]) > 0
