@@ -221,6 +221,15 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
     s.share = (double)a.hot / (double)a.samples;
     s.foreign_mean = a.foreign_sum / (double)a.samples;
     s.active = a.own_hot > 0 || hip_active.count(s.pod);
+    uint32_t& hold = hold_[kv.first];
+    if (s.active) {
+      hold = cfg_.starved_hold;
+    } else if (hold && s.share * 100.0 >= (double)cfg_.starved_pct) {
+      s.active = s.starved = true;
+      --hold;
+    } else {
+      hold = 0;
+    }
     const auto pw = pod_wait.find(s.pod);
     s.gpu_wait_ns = pw != pod_wait.end() ? pw->second : 0;
     s.wait_reported = pod_reports.count(s.pod) > 0;
@@ -266,6 +275,8 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
     }
   }
   st_.pairs = acc_.size();
+  for (auto it = hold_.begin(); it != hold_.end();)  // only pairs read this interval keep a hold
+    it = it->second && acc_.count(it->first) ? std::next(it) : hold_.erase(it);
   acc_.clear();
   refresh_locked();
   uint64_t pushed = 0;

@@ -53,6 +53,11 @@ struct GpuSamplerConfig {
   uint64_t min_samples = 3;            // readings of a (pod, GPU) needed to decide an interval
   uint64_t evict_floor_ns = 1000000;   // eviction time per interval to emit
   bool evictions = true;               // evicted_ms records (off when gpu_kfd.bpf.c's kprobes run)
+  // a pod active last interval that shows no occupancy of its own while other processes hold the
+  // GPU in >= starved_pct % of the readings is starved, not idle (its kernels wait for CUs and
+  // cu_occupancy only counts resident waves): it stays active for up to starved_hold intervals
+  uint32_t starved_hold = 2;
+  uint64_t starved_pct = 90;
 };
 
 // gpu_kfd.bpf.c hip_activity value (probes/ebpf/mislo_record.h struct mislo_hip_act)
@@ -77,6 +82,7 @@ struct GpuShare {
   uint64_t samples = 0, hot = 0, own_hot = 0;
   double share = 0.0, foreign_mean = 0.0;
   bool active = false;
+  bool starved = false;      // active by the starvation hold, not by its own readings
   uint64_t gpu_wait_ns = 0;  // the pod's host-side GPU wait over the interval
   bool wait_reported = false;  // the pod's HIP / ROCr uprobes report (gpu_wait_ns is measured, 0 included)
   uint64_t delay_ns = 0;     // the gpu_queue_delay_ms value decided (0: none emitted)
@@ -138,6 +144,7 @@ class GpuSampler {
   uint64_t last_scan_ns_ = 0;
   uint64_t rescan_ns_ = 500000000;
   std::map<std::pair<uint32_t, uint64_t>, Acc> acc_;       // (pod, gpu) -> readings
+  std::map<std::pair<uint32_t, uint64_t>, uint32_t> hold_;  // (pod, gpu) -> starvation hold left
   std::map<uint32_t, HipActivity> hip_prev_, hip_override_;
   std::vector<GpuShare> last_;
   uint64_t prev_mono_ = 0;

@@ -95,6 +95,44 @@ def test_an_idle_pod_is_not_contended_unless_its_hip_runtime_submitted_work(tmp_
     assert r.size == 1 and r[0]["value"] == DT and s.shares()[0]["active"]
 
 
+def test_a_pod_starved_by_a_neighbour_stays_active_for_the_hold(tmp_path):
+    """A pod's kernels queued behind a neighbour that fills every CU hold no waves, so its own
+    cu_occupancy reads 0 exactly while it is delayed most (the MI355X run of the real-driver test
+    below: 3 of 9 contended intervals had a reading of its own). A pod active last interval stays
+    active while the neighbour holds the GPU in >= starved_pct % of the readings, for at most
+    starved_hold intervals; a neighbour below that share does not extend it."""
+    k = Kfd(tmp_path)
+    k.proc_on(100, [7])
+    k.proc_on(200, [7])
+    s = sampler(k, starved_hold=2, starved_pct=90)
+    s.set_target_list([(100, 5)])
+    s.decide(0, DT)
+    k.occ(100, 7, 4)
+    k.occ(200, 7, 64)
+    for _ in range(5):
+        s.sample()
+    assert recs(s.decide(0, 2 * DT)).size == 1 and not s.shares()[0]["starved"]
+    k.occ(100, 7, 0)  # starved from here on
+    got = []
+    for i in range(4):
+        for _ in range(5):
+            s.sample()
+        r = recs(s.decide(0, (3 + i) * DT))
+        sh = s.shares()[0]
+        got.append((r.size, sh["active"], sh["starved"]))
+    assert got == [(1, True, True), (1, True, True), (0, False, False), (0, False, False)]
+    # a neighbour holding the GPU in 60 % of the readings is contention, not starvation
+    k.occ(100, 7, 4)
+    for _ in range(5):
+        s.sample()
+    assert recs(s.decide(0, 7 * DT)).size == 1
+    k.occ(100, 7, 0)
+    for i in range(5):
+        k.occ(200, 7, 64 if i < 3 else 0)
+        s.sample()
+    assert recs(s.decide(0, 8 * DT)).size == 0 and not s.shares()[0]["active"]
+
+
 def test_processes_of_the_same_pod_are_its_own_load_and_other_pods_are_foreign(tmp_path):
     k = Kfd(tmp_path)
     for pid in (100, 101, 200):
