@@ -513,11 +513,15 @@ class Agent:
             kw = dict(scenario=o.scenario if o.scenario not in ("baseline",) else "full",
                       events_per_window=o.window_events, spans_per_window=o.window_spans,
                       n_services=o.window_groups)
-            # the replay writes ~1/4 of a window's events as GPU-signal records: rings of 2+
-            # windows each (the shared pages count in the agent's RSS once registered for DMA)
+            # rings sized by rate: a window's space is freed as soon as its
+            # chain is collected (worker.collect), so each ring holds one window plus a quarter
+            # for late collection -- the kernel records at <= 24 B per event (18.6 measured), the
+            # GPU-signal records (~1/4 of a window's events) and the spans; the shared pages count
+            # in the agent's RSS once registered for DMA
             w = max(1, world)
-            sets = [tuple(bpf.create_rings(n, 2 * 24 * o.window_events // w + (1 << 20), o.window_events // w,
-                                           4 * o.window_spans // w + 1024)) for n in sets_names]
+            ev = o.window_events // w
+            sets = [tuple(bpf.create_rings(n, 5 * 24 * ev // 4 + (1 << 20), 5 * ev // 16 + 1024,
+                                           5 * o.window_spans // (4 * w) + 1024)) for n in sets_names]
             self._producer = bpf.start_replay_producer(sets_names[0], kw, o.window_events * 1000.0 / o.window_ms,
                                                        o.window_ms, max_windows=0,
                                                        shard_names=sets_names if w > 1 else None)

@@ -76,6 +76,9 @@ class AgentMetrics:
         self.worker_restarts = r.counter("llm_slo_agent_worker_restarts_total",
                                          "Worker pool restarts after a worker died (the survivors' GPUs go on).")
         self.rss = r.gauge("llm_slo_agent_memory_rss_bytes", "Agent process resident set size (bytes).")
+        self.cg_mem = r.gauge("llm_slo_agent_memory_cgroup_bytes",
+                              "Memory charged to the agent's cgroup (v2 memory.current, v1 usage_in_bytes): what a "
+                              "pod memory limit is enforced on, next to RSS.")
         self.burn_err = r.gauge("llm_slo_agent_burn_rate_prediction_error",
                                 "Mean relative error of the scored SLO burn-rate forecasts.")
         # GPU signals' value distributions (the window histograms the decode kernel builds)
@@ -103,6 +106,11 @@ class AgentMetrics:
                 self.rss.set(float(int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")))
         except (OSError, ValueError, IndexError):
             pass
+        from ..utils import cgroupmem
+
+        cg = cgroupmem.reading()
+        if cg is not None:
+            self.cg_mem.set(float(cg["charged_bytes"]))
 
     def set_enabled_signals(self, supported: Iterable[str], enabled: Iterable[str]) -> None:
         en = set(enabled)

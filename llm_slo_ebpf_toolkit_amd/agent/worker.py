@@ -253,6 +253,8 @@ class WorkerCore:
                     return {"rank": self.spec.rank, "prevs": prevs}
                 time.sleep(2e-4)
             prevs.append(self._collect(*self.pending.popleft()))
+        if prevs:  # the collected windows' ring space is free now, not at the next cut: the rings
+            self.src.reap()  # need one window of headroom instead of two
         return {"rank": self.spec.rank, "prevs": prevs}
 
     def _collect(self, k: int, host_us: float, n_groups: int) -> dict:

@@ -285,6 +285,10 @@ def _first(attrs: Dict[str, object], keys) -> object:
     return None
 
 
+def _truthy(v: object) -> bool:
+    return v is True or (isinstance(v, str) and v.lower() == "true") or (isinstance(v, (int, float)) and v == 1)
+
+
 class SpanMapper:
     """OTLP spans -> SPAN records on the agent's ids."""
 
@@ -314,6 +318,13 @@ class SpanMapper:
         self._retr: "collections.OrderedDict[int, float]" = collections.OrderedDict()
         self._rlock = threading.Lock()
         self.retrieval_cap = 8192
+        # first-token records (llm.slo.ttft_early): a request's SLI as soon as its first token is
+        # out, not when the request span ends -- the breach reaches the window it happened in. The
+        # traces counted that way (and, for the rare early record that comes second, the traces
+        # whose request span counted already), bounded, oldest out
+        self._early: "collections.OrderedDict[int, bool]" = collections.OrderedDict()
+        self._final: "collections.OrderedDict[int, bool]" = collections.OrderedDict()
+        self.early_dropped = 0  # first-token records after their request span (counted by it)
 
     def take_pod_updates(self) -> Optional[Tuple[np.ndarray, np.ndarray]]:
         """(pod ids, svc|node) learned since the last call, or None."""
@@ -366,7 +377,7 @@ class SpanMapper:
                 at_peer = None
         # per-field lists, written into the record array column by column at the end: setting the
         # fields of one structured element at a time cost ~18 us per span (the receiver's CPU)
-        ts, tr, sh, pids, pods, svcs, grps, ttft, lat, conn, rms = ([] for _ in range(11))
+        ts, tr, sh, pids, pods, svcs, grps, ttft, lat, conn, rms, flags = ([] for _ in range(12))
         late_before, slo_ns = int(self.late_before_ns), int(round(float(self.slo_ms) * 1e6))
         res_cache: Dict[int, tuple] = {}  # one resource's service / pod / pid per request
         groups_seen: Dict[str, int] = {}
@@ -407,8 +418,28 @@ class SpanMapper:
             dport = _first(a, ("server.port", "net.peer.port", "net.sock.peer.port")) or 0
             v = _first(a, TTFT_KEYS)
             th = trace_hash(d.get("traceId"))
-            rv = retr.get(th)
-            if self._retr and th:
+            fl = 0
+            if th and v is not None:
+                if _truthy(a.get(semconv.ATTR_SLO_TTFT_EARLY)):
+                    with self._rlock:
+                        if self._final.pop(th, None) is not None:
+                            self.early_dropped += 1
+                            continue
+                        self._early[th] = True
+                        while len(self._early) > self.retrieval_cap:
+                            self._early.popitem(last=False)
+                    fl = records.SPAN_SLI_ONLY
+                else:
+                    with self._rlock:
+                        if self._early.pop(th, None) is not None:
+                            fl = records.SPAN_NO_SLI
+                        else:
+                            self._final[th] = True
+                            while len(self._final) > self.retrieval_cap:
+                                self._final.popitem(last=False)
+            flags.append(fl)
+            rv = retr.get(th) if fl != records.SPAN_SLI_ONLY else None
+            if self._retr and th and fl != records.SPAN_SLI_ONLY:
                 with self._rlock:
                     early = self._retr.pop(th, None)
                 if early is not None:
@@ -442,9 +473,11 @@ class SpanMapper:
             out["latency_ms"] = lat
             out["conn_h"] = np.array(conn, dtype=np.uint64)
             out["retr_ms"] = rms
+            fl = np.asarray(flags, dtype=np.uint32)
             if late_before > 0 and slo_ns > 0:
                 t0s = np.asarray(ts, dtype=np.int64)
-                out["flags"] = np.where((t0s > 0) & (t0s + slo_ns < late_before), records.SPAN_LATE, 0)
+                fl |= np.where((t0s > 0) & (t0s + slo_ns < late_before), records.SPAN_LATE, 0).astype(np.uint32)
+            out["flags"] = fl
         return out
 
 

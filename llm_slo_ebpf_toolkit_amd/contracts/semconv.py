@@ -15,6 +15,8 @@ ATTR_CONNECT_LATENCY_MS = "llm.ebpf.net.connect_latency_ms"
 ATTR_TLS_HANDSHAKE_MS = "llm.ebpf.tls.handshake_ms"
 ATTR_CORRELATION_CONF = "llm.ebpf.correlation_confidence"
 ATTR_SLO_TTFT_MS = "llm.slo.ttft_ms"
+# true on a record exported when the first token is out (the SLI, ahead of the request span)
+ATTR_SLO_TTFT_EARLY = "llm.slo.ttft_early"
 ATTR_SLO_TOKENS_PER_SEC = "llm.slo.tokens_per_sec"
 ATTR_RETRIEVAL_VECTORDB = "llm.slo.retrieval.vectordb_ms"
 ATTR_RETRIEVAL_NETWORK_MS = "llm.slo.retrieval.network_ms"

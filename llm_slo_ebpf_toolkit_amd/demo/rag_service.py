@@ -209,12 +209,16 @@ class SpanExporter:
             d["parentSpanId"] = parent
         return d
 
-    def add(self, spans: List[dict]) -> None:
+    def add(self, spans: List[dict], urgent: bool = False) -> None:
+        """Queue spans; ``urgent``: the flusher sends them now instead of at the batch delay
+        (without blocking the caller -- the request thread)."""
         if not self.endpoint:
             return
         with self.lock:
             self.buf += spans
             if len(self.buf) < self.max_batch:
+                if urgent:
+                    self._wake.set()
                 return
             batch, self.buf = self.buf, []
         self._post(batch)
@@ -304,8 +308,12 @@ class VectorDBClient:
 class RagService:
     def __init__(self, backend, corpus_path: str = os.path.join(HERE, "fixtures", "corpus.json"),
                  otlp_endpoint: str = "", node: str = "demo-node", pod: str = "demo-rag-service", resource=None,
-                 vectordb_url: str = ""):
+                 vectordb_url: str = "", early_ttft: bool = True):
         self.backend = backend
+        # export the TTFT SLI when the first token is out (a chat.first_token span,
+        # llm.slo.ttft_early), not only on the request span at the end: an SLO breach reaches the
+        # agent's window it happened in (collector/otlp.py counts each request once)
+        self.early_ttft = early_ttft
         self.vdb = VectorDBClient(vectordb_url) if vectordb_url else None
         with open(corpus_path) as fh:
             self.docs = json.load(fh)
@@ -372,6 +380,12 @@ class RagService:
 
         def on_tok(t):
             tokens.append(t)
+            if len(tokens) == 1 and self.early_ttft:
+                t_ft = time.time_ns()
+                self.spans.add([SpanExporter.span(
+                    trace_id, hashlib.blake2b(f"{rid}/f".encode(), digest_size=8).hexdigest(), root, "chat.first_token",
+                    t_req, t_ft, {semconv.ATTR_SLO_TTFT_MS: (t_ft - t_req) / MS, semconv.ATTR_SLO_TTFT_EARLY: True})],
+                    urgent=True)
             if emit:
                 emit({"token": t, "index": len(tokens) - 1})
 
@@ -495,11 +509,13 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default=os.environ.get("LLM_BACKEND", "stub"), choices=("stub", "llama"))
     ap.add_argument("--llama-preset", default="1b")
     ap.add_argument("--otlp-endpoint", default=os.environ.get("OTEL_EXPORTER_OTLP_TRACES_ENDPOINT", ""))
+    ap.add_argument("--early-ttft", type=int, default=1, help="1: export each request's TTFT when its first token "
+                                                                "is out (chat.first_token), not only at its end")
     ap.add_argument("--vectordb-url", default=os.environ.get("VECTORDB_URL", ""),
                     help="vector-DB stub (demo/vectordb.py) to search over a keep-alive connection")
     a = ap.parse_args(argv)
     backend = LlamaBackend(a.llama_preset) if a.backend == "llama" else StubBackend()
-    svc = RagService(backend, otlp_endpoint=a.otlp_endpoint, vectordb_url=a.vectordb_url)
+    svc = RagService(backend, otlp_endpoint=a.otlp_endpoint, vectordb_url=a.vectordb_url, early_ttft=bool(a.early_ttft))
     httpd, _ = svc.serve(a.bind, a.metrics_bind)
     print(f"rag-service listening on {a.bind} (backend={backend.name})", flush=True)
     try:

@@ -33,6 +33,8 @@ def main(argv=None) -> int:
     ap.add_argument("--bind", default="127.0.0.1:8090")
     ap.add_argument("--otlp-endpoint", default=os.environ.get("OTEL_EXPORTER_OTLP_TRACES_ENDPOINT", ""))
     ap.add_argument("--max-new", type=int, default=16)
+    ap.add_argument("--early-ttft", type=int, default=1, help="1: export each request's TTFT when its first token "
+                                                                "is out (chat.first_token), not only at its end")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"), help="cpu: the gloo rehearsal (tests)")
     a = ap.parse_args(argv)
 
@@ -61,7 +63,7 @@ def main(argv=None) -> int:
 
     tag = GpuTraceTag()
 
-    def step(ids, max_new):
+    def step(ids, max_new, on_token=None):
         """One request on every rank (rank 0 calls it with the ids, the others get them). Every
         rank tags its kernels with the request's trace, so the agent joins all shards' GPU
         signals to the request."""
@@ -78,7 +80,7 @@ def main(argv=None) -> int:
         else:
             x = ids
         try:
-            return model.generate(x, max_new)
+            return model.generate(x, max_new, on_token=on_token)
         finally:
             if rank:
                 tag.set_hash(0)
@@ -114,8 +116,19 @@ def main(argv=None) -> int:
                 hdr[0], hdr[1], hdr[2] = len(toks), max_new, th - (1 << 64) if th >= 1 << 63 else th
                 buf[:len(toks)] = ids[0]
             tag.set(trace)
+            first = []
+
+            def on_token(_tok):  # the TTFT SLI as the first token is out (collector/otlp.py counts once)
+                if not first:
+                    first.append(time.time_ns())
+                    spans.add([SpanExporter.span(
+                        trace, hashlib.blake2b(f"{rid}/f".encode(), digest_size=8).hexdigest(), root,
+                        "chat.first_token", t0, first[0],
+                        {semconv.ATTR_SLO_TTFT_MS: (first[0] - t0) / 1e6, semconv.ATTR_SLO_TTFT_EARLY: True})],
+                        urgent=True)
+
             try:
-                r = step(ids, max_new)
+                r = step(ids, max_new, on_token if a.early_ttft else None)
             finally:
                 tag.set("")
         t1 = time.time_ns()

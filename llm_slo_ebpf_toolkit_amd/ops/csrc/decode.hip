@@ -695,7 +695,9 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
         grp /= (uint32_t)sm.sh_world;
         if (!mine) r.ts = 0;  // another GPU's incident group: never joins, never counted here
       }
-      if (mine && sm.grp_sli && grp < (uint32_t)sm.n_groups) {  // per-incident TTFT SLO accounting
+      if (s.flags & kSpanSliOnly) r.ts = 0;  // a first-token record: the SLI, not a join row
+      // per-incident TTFT SLO accounting (a request whose first-token record counted it: once)
+      if (mine && sm.grp_sli && grp < (uint32_t)sm.n_groups && !(s.flags & kSpanNoSli)) {
         const bool breach = s.ttft_ms > sm.ttft_slo_ms;
         if (breach && (s.flags & kSpanLate) && sm.grp_late) {  // an earlier window's breach, reported now
           if (late_lds) atomicAdd(&s_late[grp], 1u);

@@ -251,6 +251,8 @@ class CpuRingEngine:
         events = int(valid_k.sum()) + len(u) - other
         sp = _gather(spans)
         spr = oracle.spans_native(sp.view(records.SPAN) if len(sp) else np.zeros(0, records.SPAN))
+        counted = (spr["flags"] & np.uint32(records.SPAN_NO_SLI)) == 0  # first-token records count once
+        spr["ts_ns"] = np.where((spr["flags"] & np.uint32(records.SPAN_SLI_ONLY)) != 0, 0, spr["ts_ns"])
         G = int(n_groups)
         grp_local = spr["group_id"].astype(np.int64)
         if self.shard_world > 1:
@@ -306,9 +308,10 @@ class CpuRingEngine:
         late = np.zeros((G, 2), np.uint32)
         breach = spr["ttft_ms"] > np.float32(self.ttft_slo_ms)
         is_late = breach & ((spr["flags"] & np.uint32(records.SPAN_LATE)) != 0)
-        np.add.at(sli[:, 0], grp_local[okg & ~is_late], 1)
-        np.add.at(sli[:, 1], grp_local[okg & breach & ~is_late], 1)
-        np.add.at(late[:, 0], grp_local[okg & is_late], 1)
+        ok = okg & counted
+        np.add.at(sli[:, 0], grp_local[ok & ~is_late], 1)
+        np.add.at(sli[:, 1], grp_local[ok & breach & ~is_late], 1)
+        np.add.at(late[:, 0], grp_local[ok & is_late], 1)
         ring = np.zeros(PACKET_LAYOUT[7])
         ring[:7] = (first_busy, 0, 0, 0, 0, events, other)
         pk = build_packet(hist, status, misc, dbg, conf, stats)

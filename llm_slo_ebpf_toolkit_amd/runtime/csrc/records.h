@@ -27,7 +27,8 @@ struct SpanRec64 {  // records.py SPAN (64 B)
   float ttft_ms, latency_ms;
   uint64_t span_h;
   float retr_ms;  // application-reported retrieval ms (0 = none)
-  uint32_t flags;  // bit 0: TTFT-SLO deadline before the agent's last window cut
+  uint32_t flags;  // bit 0: TTFT-SLO deadline before the agent's last window cut; bit 1: SLI counted
+                   // already (first-token record); bit 2: first-token record (SLI only)
 };
 static_assert(sizeof(SpanRec64) == 64, "SPAN is 64 bytes");
 

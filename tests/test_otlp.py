@@ -169,7 +169,8 @@ def test_rag_service_spans_reach_the_ring():
     m, pods = _mapper()
     rx = otlp.OtlpSpanReceiver("127.0.0.1:0", m, ring.push).start()
     try:
-        svc = RagService(StubBackend(), otlp_endpoint=rx.endpoint, resource={"k8s.pod.uid": RES["k8s.pod.uid"]})
+        svc = RagService(StubBackend(), otlp_endpoint=rx.endpoint, resource={"k8s.pod.uid": RES["k8s.pod.uid"]},
+                         early_ttft=False)  # (first-token records: tests/test_first_token.py)
         outs = [svc.chat({"prompt": f"why is ttft high {i}", "profile": "chat_short", "max_tokens": 2})
                 for i in range(3)]
         svc.spans.flush()

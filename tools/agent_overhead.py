@@ -119,12 +119,15 @@ def rss_split(pid: int, min_queue_area_mb: float = 64.0) -> dict:
     except OSError:
         return {}
     qa = [m for m in maps if not m[0] and m[1] >= min_queue_area_mb * 1024 and m[2] > 0]
+    zero = sorted((m for m in maps if m[0] == "/dev/zero" and m[2] >= 1024), key=lambda m: -m[2])
     q_rss = sum(m[2] for m in qa)
     total = sum(m[2] for m in maps)
     shm = sum(m[2] for m in maps if m[0].startswith("/dev/shm/"))
     return {"total_mb": round(total / 1024, 1), "queue_save_areas_mb": round(q_rss / 1024, 1),
             "queue_save_areas": len(qa), "queue_save_area_size_mb": sorted({round(m[1] / 1024, 1) for m in qa}),
             "shared_rings_mb": round(shm / 1024, 1),
+            # MAP_SHARED|MAP_ANONYMOUS mappings (ROCr's host allocations: pinned buffers, pools), >= 1 MB
+            "dev_zero_maps_mb": [[round(m[1] / 1024, 1), round(m[2] / 1024, 1)] for m in zero],
             "rest_mb": round((total - q_rss - shm) / 1024, 1)}
 
 
@@ -246,6 +249,9 @@ def main() -> int:
     box_queues = env.pop("GPU_MAX_HW_QUEUES", None)
     if a.env_hw_queues:  # diagnostic: the cap in the agent's environment from the start
         env["GPU_MAX_HW_QUEUES"] = str(a.env_hw_queues)
+    from llm_slo_ebpf_toolkit_amd.utils import cgroupmem
+
+    cg0 = cgroupmem.reading()  # the cgroup's charge before the agent (and its producer) start
     agent = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
     proc = psutil.Process(agent.pid)
     try:
@@ -275,6 +281,7 @@ def main() -> int:
         k1 = [k.cpu_times() for k in kids]
         m1 = _scrape(port)
         full = proc.memory_full_info()
+        cg1 = cgroupmem.reading()
         smaps = _smaps_top(agent.pid)
         split = rss_split(agent.pid)
         wall = w1 - w0
@@ -296,6 +303,11 @@ def main() -> int:
             "windows_in_interval": win,
             "rss_by_mapping_mb": smaps,
             "rss_split_mb": split,
+            # what the agent's start added to the cgroup's charge (agent + its replay producer + the
+            # watched stand-ins; nothing else in the cgroup runs meanwhile): the number a pod memory
+            # limit is enforced on, next to RSS
+            "cgroup": {"version": cg1["version"], "dir": cg1["dir"]} if cg1 else None,
+            "cgroup_charge_delta_mb": cgroupmem.delta(cg0, cg1),
             "shipped_config": shipped or None,
             "spans_posted": sender.sent if sender else 0,
             "dropped_events": sum(v for k, v in m1.items() if k.startswith("llm_slo_agent_dropped_events_total"))

@@ -277,6 +277,8 @@ def main() -> int:
     ap.add_argument("--ttft-slo-ms", type=float, default=0.0,
                     help="the agent's TTFT SLO; 0 = calibrated from the healthy warmup (slo_from_warmup)")
     ap.add_argument("--window-ms", type=int, default=1000)
+    ap.add_argument("--early-ttft", type=int, default=1,
+                    help="1: the service exports each request's TTFT at its first token (chat.first_token)")
     ap.add_argument("--model-path", default=MODEL)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -320,7 +322,7 @@ def main() -> int:
         observable += list(GPU_SIGNALS)
     rag = subprocess.Popen([sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.demo.rag_service", "--backend",
                             a.backend, "--llama-preset", a.preset, "--bind", f"127.0.0.1:{hport}", "--metrics-bind", "",
-                            "--vectordb-url", f"http://127.0.0.1:{vport}"], cwd=ROOT, env=rag_env, stdout=log,
+                            "--vectordb-url", f"http://127.0.0.1:{vport}", "--early-ttft", str(a.early_ttft)], cwd=ROOT, env=rag_env, stdout=log,
                            stderr=subprocess.STDOUT, preexec_fn=pinned(victim))
 
     def start_agent(slo_ms):
@@ -445,7 +447,7 @@ def main() -> int:
                     "network_record_sets_per_s": a.retrans_rate, "observable_signals": observable,
                     "rocprof_tool": gpu_tool, "window_ms": a.window_ms, "phase_s": a.phase_s,
                     "recover_s": a.recover_s, "clients": a.clients, "max_tokens": a.max_tokens,
-                    "procfs_interval_ms": a.procfs_ms, "ttft_slo_ms": slo,
+                    "procfs_interval_ms": a.procfs_ms, "ttft_slo_ms": slo, "early_ttft": a.early_ttft,
                     "slo_source": "given" if a.ttft_slo_ms > 0 else "1.5 x healthy warmup TTFT p95",
                     "retrieval_fault": "vector-DB response stall only (no records injected)" if a.retrieval_phase else None,
                     "network_fault": "vector-DB response stall + REF's network_partition kernel-signal profile "

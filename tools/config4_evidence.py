@@ -56,6 +56,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=0, help="TP ranks = agent workers (0 = every visible GPU)")
     ap.add_argument("--preset", default="7b")
     ap.add_argument("--phase-s", type=float, default=15.0)
+    ap.add_argument("--window-ms", type=int, default=1000)
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--burners-per-cpu", type=int, default=2,
                     help="busy loops per rank CPU: 2 slows the server ~3x; 4 starves it to a request every few s")
@@ -108,7 +109,7 @@ def main() -> int:
         return subprocess.Popen(
             [sys.executable, "-u", "-m", "llm_slo_ebpf_toolkit_amd.cli.agent", "--engine", "gpu", "--gpus", str(n),
              "--source", "shm", "--ring-name", prefix, "--otlp-receiver-bind", f"127.0.0.1:{rx}",
-             "--metrics-bind", f"127.0.0.1:{mport}", "--window-ms", "1000", "--window-events", "262144",
+             "--metrics-bind", f"127.0.0.1:{mport}", "--window-ms", str(a.window_ms), "--window-events", "262144",
              "--window-spans", "4096", "--window-groups", "8", "--model-path", a.model_path, "--min-confidence", "0.3",
              "--halo-ms", "1500", "--ttft-slo-ms", str(slo_ms), "--procfs-sampler",
              "--procfs-pods", ",".join(f"{p.pid}:{POD_UID}" for p in ranks), "--procfs-interval-ms", "100",
@@ -205,14 +206,14 @@ def main() -> int:
         if tailer.is_alive():
             tailer.join(10)
         log.close()
-    res = score(phases, tailer.rows, 1000.0, service="llm-tp", expect=EXPECT,
+    res = score(phases, tailer.rows, float(a.window_ms), service="llm-tp", expect=EXPECT,
                 cuts=load_cuts(os.path.join(a.out, "decisions.jsonl")))
     res["ttft_ms"] = {nm: {"n": len(v), "p50": pct(v, .5), "p95": pct(v, .95)}
                       for nm, _t0, _t1 in phases for v in [[r["ttft_ms"] for r in rows if r["phase"] == nm]]}
     res["agent_overhead_metrics"] = overhead
     res["agent_counters_by_phase"] = counters
     res["setup"] = {"tp_ranks": n, "preset": a.preset, "model": os.path.relpath(a.model_path, ROOT),
-                    "ttft_slo_ms": slo, "clients": a.clients, "max_tokens": a.max_tokens,
+                    "ttft_slo_ms": slo, "clients": a.clients, "max_tokens": a.max_tokens, "window_ms": a.window_ms,
                     "slo_source": "given" if a.ttft_slo_ms > 0 else "1.5 x healthy warmup TTFT p95",
                     "observable_signals": observable, "rank_cpus": rank_cpus, "burners_per_cpu": a.burners_per_cpu,
                     "interconnect_fault": "tools/xgmi_hog.py peer copies over every GPU pair",
