@@ -1,7 +1,7 @@
 """Is a HIP hardware queue's context save area charged to the process's memory cgroup?
 (the agent's RSS is dominated by ~173 MB per queue on MI355X.)
 
-For 0, 1, 2 and 3 streams, a child process brings up the HIP runtime through ctypes (no torch),
+For 0, 1, 2 and 3 streams (-1: the null stream only), a child process brings up the HIP runtime through ctypes (no torch),
 creates that many streams (each with its own hardware queue: GPU_MAX_HW_QUEUES is set to the
 stream count) and runs one memset on each, then holds still while the parent reads:
 
@@ -35,7 +35,9 @@ hip = ctypes.CDLL("libamdhip64.so")
 assert hip.hipSetDevice(0) == 0
 p = ctypes.c_void_p()
 assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 20)) == 0
-for i in range(n):
+if n < 0:  # the null stream only
+    assert hip.hipMemsetAsync(p, 0, ctypes.c_size_t(1 << 20), None) == 0
+for i in range(max(n, 0)):
     s = ctypes.c_void_p()
     assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0
     assert hip.hipMemsetAsync(p, 0, ctypes.c_size_t(1 << 20), s) == 0
@@ -50,6 +52,7 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--streams", default="0,1,2,3")
     ap.add_argument("--hold-s", type=float, default=6.0)
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for the children (repeatable)")
     ap.add_argument("--out", default="gpurun_out/queue_mem.json")
     a = ap.parse_args()
     from agent_overhead import rss_split
@@ -59,6 +62,7 @@ def main() -> int:
     rows = []
     for n in (int(x) for x in a.streams.split(",")):
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(max(1, n)))
+        env.update(kv.split("=", 1) for kv in a.env)
         time.sleep(1.0)  # the previous child's pages are uncharged
         cg0 = cgroupmem.reading()
         ch = subprocess.Popen([sys.executable, "-c", CHILD, str(n), str(a.hold_s)], stdout=subprocess.PIPE, text=True,
@@ -77,7 +81,7 @@ def main() -> int:
              "cgroup": {"version": cg1["version"], "dir": cg1["dir"]} if cg1 else None}
         rows.append(r)
         print(json.dumps(r), flush=True)
-    out = {"rows": rows}
+    out = {"rows": rows, "env": a.env}
     if len(rows) >= 2 and all(r["cgroup_charge_delta_mb"] for r in rows):
         d_rss = rows[-1]["rss_split_mb"]["total_mb"] - rows[0]["rss_split_mb"]["total_mb"]
         d_q = rows[-1]["rss_split_mb"]["queue_save_areas_mb"] - rows[0]["rss_split_mb"]["queue_save_areas_mb"]
