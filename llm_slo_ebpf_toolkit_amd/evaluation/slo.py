@@ -151,13 +151,16 @@ def _binom_ll(n: float, b: float) -> float:
 
 
 def _binom_ll_np(n, b):
-    """``_binom_ll`` over arrays."""
+    """``_binom_ll`` over arrays (the logs only where 0 < b < n: no floating-point state to switch)."""
     import numpy as np
 
-    with np.errstate(divide="ignore", invalid="ignore"):
-        ok = (b > 0) & (b < n)
-        p = np.where(ok, b / np.where(ok, n, 1.0), 0.5)
-        return np.where(ok, b * np.log(p) + (n - b) * np.log1p(-p), 0.0)
+    ok = (b > 0) & (b < n)
+    out = np.zeros(np.shape(n), dtype=np.float64)
+    if ok.any():
+        nn, bb = n[ok], b[ok]
+        p = bb / nn
+        out[ok] = bb * np.log(p) + (nn - bb) * np.log1p(-p)
+    return out
 
 
 class BurnRateForecaster:
@@ -323,7 +326,9 @@ class BurnRateForecaster:
         while L - s0 > j:
             n_all, b_all = CN[L] - CN[s0], CB[L] - CB[s0]
             nl, bl = CN[s0 + 1:L - j + 1] - CN[s0], CB[s0 + 1:L - j + 1] - CB[s0]
-            llr = _binom_ll_np(nl, bl) + _binom_ll_np(n_all - nl, b_all - bl) - _binom_ll(n_all, b_all)
+            m = len(nl)  # both sides of every split in one pass
+            ll = _binom_ll_np(np.concatenate([nl, n_all - nl]), np.concatenate([bl, b_all - bl]))
+            llr = ll[:m] + ll[m:] - _binom_ll(n_all, b_all)
             k = int(np.argmax(llr))
             if not llr[k] > self.change_llr:
                 break
