@@ -204,6 +204,9 @@ class AgentOptions:
     # application evidence (models/bayes.py AppEvidence): a group's retrieval time beyond the
     # kernel-attributed share at least this long is elevated (<= 0: off)
     retrieval_residual_ms: float = 100.0
+    # per-launch HIP uprobes (hipLaunchKernel & co.): off -- ~39,000 hits/s on an LLM decode loop
+    # (profiles/r6_uprobe/); the KFD sampler's activity decision does without them
+    hip_launch_uprobes: bool = False
     pair_prior: float = 0.0              # 2-fault prior mass added to a table model without pairs (0 = none)
     explicit_flags: Tuple[str, ...] = ()  # flags given on the command line (they win over the config's gpu: block)
 
@@ -485,7 +488,7 @@ class Agent:
                 from ..collector.probes import ProbeManager
 
                 self.probe_manager = ProbeManager(self.mode, self.generator.enabled_signals())
-                self.bpf_loader = BpfProbeLoader(o.probe_objs, o.pin_dir)
+                self.bpf_loader = BpfProbeLoader(o.probe_objs, o.pin_dir, launch_uprobes=o.hip_launch_uprobes)
                 for spec in probe_specs(self.bpf_loader, self.generator.enabled_signals()):
                     self.probe_manager.register(spec)
                 attached = self.probe_manager.attach_all()

@@ -87,6 +87,9 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
                                                            "exceeds the kernel-attributed share (dns + connect + "
                                                            "TLS) by at least this is retrieval_backend evidence "
                                                            "(<= 0 = off)"),
+        ("hip-launch-uprobes", False, "bpf source: also uprobe every HIP kernel launch (hipLaunchKernel & co.) "
+                                      "for the KFD sampler's activity decision; off by default -- an LLM decode "
+                                      "loop launches ~39,000 kernels/s and each uprobe hit traps (1-3 us)"),
         ("pair-prior", d.pair_prior, "window engine: add 2-fault hypotheses with this prior mass to a table model "
                                      "(--model bayes | bayes_gpu; trained files carry their own)"),
         ("ring-name", d.ring_name, "shared-memory ring name prefix (user-space / span rings; emulated BPF ring)"),
@@ -147,6 +150,7 @@ def parse(argv: List[str]) -> (AgentOptions, bool):
         procfs_interval_ms=int(a.procfs_interval_ms), procfs_cpu_psi=bool(a.procfs_cpu_psi),
         kfd_sampler=a.kfd_sampler,
         model_signals=a.model_signals, retrieval_residual_ms=float(a.retrieval_residual_ms),
+        hip_launch_uprobes=bool(a.hip_launch_uprobes),
         pair_prior=float(a.pair_prior), emit_wait_ms=int(a.emit_wait_ms), webhook_queue=int(a.webhook_queue),
         emit_min_burn=float(a.emit_min_burn), emit_min_requests=float(a.emit_min_requests),
         emit_recovered_requests=int(a.emit_recovered_requests),

@@ -71,8 +71,9 @@ class LoaderError(RuntimeError):
 
 class BpfProbeLoader:
     def __init__(self, obj_dir: str, pin_dir: str = "/sys/fs/bpf/mislo", bpftool: str = "bpftool",
-                 run: Optional[Callable[[List[str]], None]] = None, uprobes=None):
+                 run: Optional[Callable[[List[str]], None]] = None, uprobes=None, launch_uprobes: bool = False):
         self.obj_dir, self.pin_dir, self.bpftool = obj_dir, pin_dir, bpftool
+        self.launch_uprobes = launch_uprobes  # per-launch HIP uprobes (collector/uprobes.py per_launch)
         self._run = run or self._subprocess
         self._lock = threading.Lock()
         self._refs: Dict[str, int] = {}
@@ -83,7 +84,7 @@ class BpfProbeLoader:
         if self._uprobes is None:
             from .uprobes import UprobeAttacher
 
-            self._uprobes = UprobeAttacher(self.pin_dir)
+            self._uprobes = UprobeAttacher(self.pin_dir, launches=self.launch_uprobes)
         return self._uprobes
 
     def is_loaded(self, probe: str) -> bool:

@@ -42,6 +42,11 @@ class UprobeTarget:
     library: str      # regex on the mapped file's basename
     symbol: str
     retprobe: bool
+    # fires on every kernel launch of the probed process: opt-in (UprobeAttacher(launches=True)).
+    # Measured on the demo's Llama decode (tools/uprobe_rate.py, profiles/r6_uprobe/): ~39,000
+    # hipLaunchKernel calls/s, where a uprobe trap of 1-3 us each would cost the launching thread
+    # 4-12 % of a core; the waits and copies fire ~13 times/s
+    per_launch: bool = False
 
 
 UPROBE_TARGETS: Tuple[UprobeTarget, ...] = (
@@ -56,10 +61,10 @@ UPROBE_TARGETS: Tuple[UprobeTarget, ...] = (
     # HIP runtime: a process's GPU work submissions and its host-side waits for the GPU, per tgid
     # (gpu_kfd.bpf.c hip_activity: the agent's KFD sampler weighs other processes' occupancy of a
     # pod's GPU by them, runtime/csrc/gpusampler.h)
-    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipLaunchKernel", False),
-    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipModuleLaunchKernel", False),
-    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipExtModuleLaunchKernel", False),
-    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipGraphLaunch", False),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipLaunchKernel", False, per_launch=True),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipModuleLaunchKernel", False, per_launch=True),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipExtModuleLaunchKernel", False, per_launch=True),
+    UprobeTarget("gpu_kfd", "hip_launch", r"^libamdhip64\.so", "hipGraphLaunch", False, per_launch=True),
     UprobeTarget("gpu_kfd", "hip_copy", r"^libamdhip64\.so", "hipMemcpyAsync", False),
     UprobeTarget("gpu_kfd", "hip_copy_exit", r"^libamdhip64\.so", "hipMemcpyAsync", True),
     UprobeTarget("gpu_kfd", "hip_copy", r"^libamdhip64\.so", "hipMemcpy", False),
@@ -239,8 +244,12 @@ class UprobeAttacher:
     """Attaches the pinned uprobe programs of loaded probe objects to every mapped instance of
     their libraries; ``rescan()`` picks up new ones, ``detach(probe)`` closes the links."""
 
-    def __init__(self, pin_dir: str, sys_=None, proc_root: str = "/proc"):
+    def __init__(self, pin_dir: str, sys_=None, proc_root: str = "/proc", launches: bool = False):
+        """``launches``: also attach the per-launch HIP targets (``UprobeTarget.per_launch``); off by
+        default -- the KFD sampler decides a pod's GPU activity from its own wave occupancy, the
+        starvation hold and its waits / copies without them."""
         self.pin_dir, self.proc_root = pin_dir, proc_root
+        self.launches = bool(launches)
         self.sys = sys_ if sys_ is not None else NativeSys()
         self._pmu: Optional[Tuple[int, int]] = None
         self._probes: Dict[str, _Probe] = {}
@@ -254,7 +263,7 @@ class UprobeAttacher:
         """Open the probe's pinned uprobe programs and attach them; returns links created."""
         with self._lock:
             st = self._probes.setdefault(probe, _Probe())
-            for t in UPROBE_TARGETS:
+            for t in self._targets():
                 if t.probe == probe and t.program not in st.progs:
                     fd = self.sys.obj_get(os.path.join(self.pin_dir, "progs", probe, t.program))
                     if fd < 0:
@@ -262,6 +271,9 @@ class UprobeAttacher:
                         continue
                     st.progs[t.program] = fd
         return self.rescan(probe)
+
+    def _targets(self) -> Tuple[UprobeTarget, ...]:
+        return tuple(t for t in UPROBE_TARGETS if self.launches or not t.per_launch)
 
     def rescan(self, probe: Optional[str] = None) -> int:
         """Attach to libraries mapped since the last scan; returns links created."""
@@ -274,7 +286,7 @@ class UprobeAttacher:
             for name, st in self._probes.items():
                 if probe is not None and name != probe:
                     continue
-                for t in UPROBE_TARGETS:
+                for t in self._targets():
                     if t.probe != name or t.program not in st.progs:
                         continue
                     if t.library not in libs_cache:

@@ -201,6 +201,14 @@ def test_rocr_and_copy_uprobes_attach_to_their_libraries(tmp_path):
     gets = {c[1].rsplit("/", 1)[1] for c in sys_.calls if c[0] == "obj_get"}
     assert {"hip_copy", "hip_copy_exit", "hsa_wait_enter", "hsa_wait_exit"} <= gets
     assert n == len(perfs) and not att.errors
+    # the per-launch targets are opt-in (an LLM decode loop launches ~39,000 kernels/s)
+    launch_offs = {a - 0x400000 for a in (hip["hipLaunchKernel"], hip["hipModuleLaunchKernel"],
+                                          hip["hipExtModuleLaunchKernel"], hip["hipGraphLaunch"])}
+    assert "hip_launch" not in gets and not launch_offs & {p[5] for p in perfs}
+    sys2 = FakeSys()
+    att2 = U.UprobeAttacher("/sys/fs/bpf/mislo", sys_=sys2, proc_root=str(proc), launches=True)
+    assert att2.attach("gpu_kfd") == n + 4
+    assert launch_offs <= {c[5] for c in sys2.calls if c[0] == "perf"}
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhsa-runtime64.so"), reason="no ROCm")
