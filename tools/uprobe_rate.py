@@ -84,12 +84,16 @@ def main() -> int:
             line = [ln for ln in fh if ln.startswith("{")][-1]
         r = json.loads(line)
         out["run"] = r
-        waits = sum(v for k, v in calls.items() if k.startswith("hsa_signal_wait") or k.startswith("hipMemcpy"))
-        per_s = waits / max(r["seconds"], 1e-9)
-        out["probed_calls_per_s"] = round(per_s, 1)
-        # a uprobe + uretprobe pair per call, 1-3 us each pair (trap + return trampoline)
-        out["slowdown_pct_of_one_core_at_1us"] = round(per_s * 1e-6 * 100, 3)
-        out["slowdown_pct_of_one_core_at_3us"] = round(per_s * 3e-6 * 100, 3)
+        sec = max(r["seconds"], 1e-9)
+        waits = sum(v for k, v in calls.items() if k.startswith("hsa_signal_wait") or k.startswith("hipMemcpy")
+                    or k.endswith("Synchronize"))
+        launches = sum(v for k, v in calls.items() if "Launch" in k)
+        # a uprobe (+ uretprobe for the waits) per call, 1-3 us per hit (trap + return trampoline)
+        for name, n in (("waits_copies_syncs", waits), ("launches", launches)):
+            per_s = n / sec
+            out[f"{name}_per_s"] = round(per_s, 1)
+            out[f"{name}_pct_of_one_core_at_1us"] = round(per_s * 1e-6 * 100, 3)
+            out[f"{name}_pct_of_one_core_at_3us"] = round(per_s * 3e-6 * 100, 3)
     s = json.dumps(out, indent=1)
     print(s)
     if a.out:
