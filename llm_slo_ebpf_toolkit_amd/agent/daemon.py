@@ -1068,6 +1068,7 @@ class Agent:
                         for rs in sets]
                 if mapper is not None:  # spans after this cut: a deadline before it is an earlier window's
                     mapper.late_before_ns = t
+                    self.metrics.set_otlp(self.receiver, mapper)
                 upd = mapper.take_pod_updates() if mapper is not None else None
                 if upd is not None and len(upd[0]):
                     self.pod_table.update(zip(np.asarray(upd[0]).tolist(), np.asarray(upd[1]).tolist()))

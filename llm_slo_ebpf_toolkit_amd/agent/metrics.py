@@ -76,6 +76,11 @@ class AgentMetrics:
         self.worker_restarts = r.counter("llm_slo_agent_worker_restarts_total",
                                          "Worker pool restarts after a worker died (the survivors' GPUs go on).")
         self.rss = r.gauge("llm_slo_agent_memory_rss_bytes", "Agent process resident set size (bytes).")
+        self.otlp = r.gauge("llm_slo_agent_otlp_spans", "OTLP receiver span records since start by outcome: accepted "
+                            "into the span ring, dropped (ring full), rejected (malformed export), conflict (a pod "
+                            "bound to another service), spoofed (a pod named from another pod's address), "
+                            "first_token_late (a first-token record after its request span, which counted it).",
+                            ("outcome",))
         self.cg_mem = r.gauge("llm_slo_agent_memory_cgroup_bytes",
                               "Memory charged to the agent's cgroup (v2 memory.current, v1 usage_in_bytes): what a "
                               "pod memory limit is enforced on, next to RSS.")
@@ -179,6 +184,14 @@ class AgentMetrics:
             self.ring_backlog.set(float(ring_stats.get("producer_pos", 0) - ring_stats.get("consumer_pos", 0)))
             self.ring_dropped.set(float(ring_stats.get("dropped", 0)))
         self.host_us.set(float(host_us))
+
+    def set_otlp(self, receiver, mapper) -> None:
+        """The OTLP receiver's and span mapper's running counts (collector/otlp.py)."""
+        for outcome, v in (("accepted", getattr(receiver, "accepted", 0)), ("dropped", getattr(receiver, "dropped", 0)),
+                           ("rejected", getattr(receiver, "rejected", 0)), ("conflict", getattr(mapper, "conflicts", 0)),
+                           ("spoofed", getattr(mapper, "spoofed", 0)),
+                           ("first_token_late", getattr(mapper, "early_dropped", 0))):
+            self.otlp.set(float(v), outcome)
 
     def observe_attribution(self, domain: str) -> None:
         self.attr.inc(1, domain)

@@ -201,6 +201,22 @@ def test_agent_metrics_export_gpu_signal_histograms():
     assert "llm_ebpf_gpu_queue_delay_ms_sum 28" in text
 
 
+def test_agent_metrics_export_otlp_outcomes_and_memory_charge():
+    from types import SimpleNamespace
+
+    from llm_slo_ebpf_toolkit_amd.agent.metrics import AgentMetrics
+    from llm_slo_ebpf_toolkit_amd.signals import catalog
+
+    m = AgentMetrics("both", "gpu", catalog.SIGNAL_NAMES, catalog.SIGNAL_NAMES)
+    m.set_otlp(SimpleNamespace(accepted=40, dropped=2, rejected=1),
+               SimpleNamespace(conflicts=3, spoofed=0, early_dropped=5))
+    m.set_rss()
+    text = m.registry.exposition() if hasattr(m, "registry") else m.r.exposition()
+    for outcome, v in (("accepted", 40), ("dropped", 2), ("rejected", 1), ("conflict", 3), ("first_token_late", 5)):
+        assert f'llm_slo_agent_otlp_spans{{outcome="{outcome}"}} {v}' in text, outcome
+    assert "llm_slo_agent_memory_rss_bytes" in text and "llm_slo_agent_memory_cgroup_bytes" in text
+
+
 def test_agent_gpu_hw_queues_flag_wins_over_env_default_does_not(monkeypatch):
     from llm_slo_ebpf_toolkit_amd.cli import agent as agent_cli
 
