@@ -28,15 +28,17 @@ def available(kfd_proc: str = KFD_PROC) -> bool:
 
 class KfdSampler:
     def __init__(self, ring, targets: Callable[[], Dict[int, int]], node_id: int = 0, kfd_proc: str = KFD_PROC,
-                 proc_root: str = "/proc", floor_pct: int = 10, sample_s: float = 0.02, decide_s: float = 0.1,
+                 proc_root: str = "/proc", floor_pct: int = 10, sample_s: float = 0.02, decide_s: float = 0.5,
                  refresh_s: float = 10.0, hip_map: Optional[Callable[[], int]] = None, evictions: bool = True,
-                 starved_hold_s: float = 1.0):
-        """``decide_s``: one gpu_queue_delay_ms record per contended pod and interval, stamped at the
-        interval's middle. 100 ms (round 6; was 500 ms): a request span joins the pod's records
-        within the pod+pid tier's 100 ms of its start, so a record every 100 ms is always in reach
-        while the GPU is contended (config 2's second run read its first burning window `unknown`:
-        no record within reach of its few request starts). ``starved_hold_s``: how long a pod
-        starved of CUs stays active without a reading of its own (runtime/csrc/gpusampler.h)."""
+                 starved_hold_s: float = 1.0, stamps: int = 5):
+        """``decide_s``: the contention decision's interval (its floor gates on the whole interval's
+        share, so a burst of another process's kernels in one short slice does not count).
+        ``stamps``: records per contended interval, the delay split evenly over them at the
+        sub-intervals' middles (round 6; was one at the interval's middle): a request span joins the
+        pod's records within the pod+pid tier's 100 ms of its start, so with 100 ms between records
+        one is in reach wherever the start falls (config 2's second run read its first burning
+        window `unknown`: no record within reach of its few request starts). ``starved_hold_s``: how
+        long a pod starved of CUs stays active without a reading of its own (gpusampler.h)."""
         from ..runtime import load
 
         self.rt = load()
@@ -44,7 +46,8 @@ class KfdSampler:
         self.sample_s, self.decide_s = float(sample_s), float(decide_s)
         self.native = self.rt.GpuSampler(ring, node_id=node_id, kfd_proc=kfd_proc, proc_root=proc_root,
                                          floor_pct=int(floor_pct), evictions=bool(evictions),
-                                         starved_hold=max(1, int(round(starved_hold_s / max(self.decide_s, 1e-3)))))
+                                         starved_hold=max(1, int(round(starved_hold_s / max(self.decide_s, 1e-3)))),
+                                         stamps=max(1, int(stamps)))
         self._hip_map = hip_map
         self._hip_fd = -1
         self._stop = threading.Event()

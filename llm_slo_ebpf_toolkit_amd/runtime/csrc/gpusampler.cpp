@@ -174,18 +174,20 @@ std::vector<EventRec> GpuSampler::decide(int64_t wall_ns, uint64_t mono_ns) {
   const uint32_t mask = enabled() ? 1u << kSigGpuQueue : 0u;
   const uint64_t dt = prev_mono_ && mono_ns > prev_mono_ ? mono_ns - prev_mono_ : 0;
   prev_mono_ = mono_ns;
-  const int64_t mid = wall_ns - (int64_t)(dt / 2);
+  const uint32_t n_st = std::max<uint32_t>(1u, cfg_.stamps);
   auto rec = [&](uint32_t ns_pid, uint32_t pid, uint32_t pod, uint64_t value) {
-    EventRec e{};
-    e.ts_ns = mid;
-    e.value = value;
-    e.pid = ns_pid;
-    e.tid = pid;
-    e.pod_id = pod;
-    e.node_id = (uint16_t)cfg_.node_id;
-    e.signal_type = kSigGpuQueue;
-    e.flags = 1u << 8;  // has_gpu
-    out.push_back(e);
+    for (uint32_t i = 0; i < n_st; ++i) {  // sub-interval i's middle; the value split evenly
+      EventRec e{};
+      e.ts_ns = wall_ns - (int64_t)dt + (int64_t)((2 * (uint64_t)i + 1) * dt / (2 * (uint64_t)n_st));
+      e.value = value / n_st;
+      e.pid = ns_pid;
+      e.tid = pid;
+      e.pod_id = pod;
+      e.node_id = (uint16_t)cfg_.node_id;
+      e.signal_type = kSigGpuQueue;
+      e.flags = 1u << 8;  // has_gpu
+      out.push_back(e);
+    }
   };
   // the pods whose HIP runtime submitted work or waited on the GPU since the last decision, and
   // how long their threads waited: ROCr's completion-signal waits (every blocking HIP path ends in

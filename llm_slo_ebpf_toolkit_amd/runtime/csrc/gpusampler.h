@@ -58,6 +58,10 @@ struct GpuSamplerConfig {
   // cu_occupancy only counts resident waves): it stays active for up to starved_hold intervals
   uint32_t starved_hold = 2;
   uint64_t starved_pct = 90;
+  // records per contended interval: the interval's delay split evenly over this many records
+  // stamped at the sub-intervals' middles, so a request span's pod+pid join (100 ms of its start)
+  // finds one wherever its start falls; the floor still gates on the whole interval's share
+  uint32_t stamps = 1;
 };
 
 // gpu_kfd.bpf.c hip_activity value (probes/ebpf/mislo_record.h struct mislo_hip_act)

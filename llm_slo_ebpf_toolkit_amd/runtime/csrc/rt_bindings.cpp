@@ -527,8 +527,9 @@ class PyGpuSampler {
  public:
   PyGpuSampler(HostRing* ring, uint32_t node_id, const std::string& kfd_proc, const std::string& proc_root,
                uint64_t floor_pct, uint64_t min_samples, uint64_t evict_floor_ns, bool evictions,
-               uint32_t starved_hold, uint64_t starved_pct) {
+               uint32_t starved_hold, uint64_t starved_pct, uint32_t stamps) {
     GpuSamplerConfig c;
+    c.stamps = stamps;
     c.starved_hold = starved_hold;
     c.starved_pct = starved_pct;
     c.node_id = node_id;
@@ -794,11 +795,11 @@ PYBIND11_MODULE(_mislo_rt, m) {
         py::arg("group_cap"), py::arg("span_cap"), py::arg("sig_cap"), py::arg("row_cap"));
   py::class_<PyGpuSampler>(m, "GpuSampler")
       .def(py::init<HostRing*, uint32_t, const std::string&, const std::string&, uint64_t, uint64_t, uint64_t, bool,
-                    uint32_t, uint64_t>(),
+                    uint32_t, uint64_t, uint32_t>(),
            py::arg("ring"), py::arg("node_id") = 0, py::arg("kfd_proc") = "/sys/class/kfd/kfd/proc",
            py::arg("proc_root") = "/proc", py::arg("floor_pct") = 10, py::arg("min_samples") = 3,
            py::arg("evict_floor_ns") = 1000000, py::arg("evictions") = true, py::arg("starved_hold") = 2,
-           py::arg("starved_pct") = 90, py::keep_alive<1, 2>())
+           py::arg("starved_pct") = 90, py::arg("stamps") = 1, py::keep_alive<1, 2>())
       .def("set_target_list", &PyGpuSampler::set_target_list)
       .def("set_hip_map", &PyGpuSampler::set_hip_map)
       .def("set_hip_activity", &PyGpuSampler::set_hip_activity, py::arg("pid"), py::arg("launches"),

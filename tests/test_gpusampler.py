@@ -95,6 +95,30 @@ def test_an_idle_pod_is_not_contended_unless_its_hip_runtime_submitted_work(tmp_
     assert r.size == 1 and r[0]["value"] == DT and s.shares()[0]["active"]
 
 
+def test_an_intervals_delay_is_stamped_over_its_sub_intervals(tmp_path):
+    """``stamps``: the contended interval's delay split evenly over records at the sub-intervals'
+    middles (a span's pod+pid join reaches 100 ms from its start); the floor still gates on the
+    whole interval's share, so a neighbour's short burst adds no record."""
+    k = Kfd(tmp_path)
+    k.proc_on(100, [7])
+    k.proc_on(200, [7])
+    s = sampler(k, stamps=5)
+    s.set_target_list([(100, 5)])
+    s.decide(0, DT)
+    for i in range(10):
+        k.occ(100, 7, 4)
+        k.occ(200, 7, 64 if i < 6 else 0)
+        s.sample()
+    r = recs(s.decide(10 * DT, 2 * DT))
+    assert r.size == 5
+    assert r["ts_ns"].tolist() == [10 * DT - DT + (2 * i + 1) * DT // 10 for i in range(5)]
+    assert (r["value"] == int(0.6 * DT) // 5).all() and int(s.shares()[0]["delay_ns"]) == int(0.6 * DT)
+    for i in range(20):  # 1 of 20 readings hot: 5 % < the 10 % floor, no records
+        k.occ(200, 7, 64 if i == 0 else 0)
+        s.sample()
+    assert recs(s.decide(11 * DT, 3 * DT)).size == 0
+
+
 def test_a_pod_starved_by_a_neighbour_stays_active_for_the_hold(tmp_path):
     """A pod's kernels queued behind a neighbour that fills every CU hold no waves, so its own
     cu_occupancy reads 0 exactly while it is delayed most (the MI355X run of the real-driver test
