@@ -43,6 +43,7 @@ def main() -> int:
     ap.add_argument("--xgmi-gbs", type=float, default=64.0, help="per-link unidirectional xGMI bandwidth (GB/s) "
                                                                 "for the all-gather projection")
     ap.add_argument("--out", default="gpurun_out/r6_multigpu/peers.json")
+    ap.add_argument("--modes", default="solo,empty,full", help="comma-separated subset (one mode per profiled run)")
     a = ap.parse_args()
     import numpy as np
 
@@ -74,7 +75,7 @@ def main() -> int:
     budget = max(framed_rows(i.framed) + len(i.user) for i in imgs)
     out = {"events": a.events, "spans": a.spans, "groups": a.services, "xchg_cap": a.xchg_cap, "peers": a.peers,
            "peer_rows_per_window": n_rows, "runs": {}}
-    for mode in ("solo", "empty", "full"):
+    for mode in [m for m in ("solo", "empty", "full") if m in a.modes.split(",")]:
         tag = f"/mislo-peer-{os.getpid()}-{mode}"
         rb = rt.Ringbuf.create_shm(tag, 1 << 28)
         user = rt.HostRing(1 << int(np.ceil(np.log2(n_user * 4))), 64)
@@ -113,6 +114,12 @@ def main() -> int:
              "import_dropped": int(d[:, 6].sum()), "windows_timed": len(comp)}
         out["runs"][mode] = r
         print(f"[peers] {mode}: {r}", flush=True)
+    if "full" not in out["runs"]:  # a profiled subset: no projection
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps(out), flush=True)
+        return 0
     blk = 24 * (1 + a.xchg_cap)
     ag_ms = (world - 1) * blk / (a.xgmi_gbs * 1e9) * 1e3  # ring all-gather: (N-1) blocks over one link
     out["allgather_ms_projected"] = round(ag_ms, 4)
