@@ -471,9 +471,9 @@ def main() -> int:
         # table from the all-reduced statistics with the fitted temperature
         pipe.eng.restore(st, model_bytes(model), int(pipe.windows_folded))
         kw = mtrain.learned_kwargs(tcfg)
-        pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"])
+        pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"], kw["ceil"])
         pipe.eng.set_refit(mtrain.learned_kwargs(tcfg)["alpha"], tcfg.prior_pseudo, 1.0 / T, tcfg.min_count,
-                           pipe.cap_dom())
+                           pipe.cap_dom(), pipe.lik_ceil())
         pipe.eng.refit_now()
         pipe.eng.set_device_refit(False)  # frozen from here on: the timed region scores, as the agent does
         pipe.device_refit = False

@@ -431,11 +431,14 @@ class NaiveBayes:
     def learned(stats: "SufficientStats", alpha: float = 2.0, seed: int = 42,
                 init: Optional[np.ndarray] = None, domains: Sequence[str] = catalog.ALL_DOMAINS,
                 prior_pseudo: float = 1.0, temperature: float = 1.0, min_count: float = 0.0,
-                floor: Optional[np.ndarray] = None, cap_domain: Optional[str] = None) -> LinearPosteriorModel:
+                floor: Optional[np.ndarray] = None, cap_domain: Optional[str] = None,
+                ceil: Optional[float] = None) -> LinearPosteriorModel:
         """Posterior-mean estimates: p_sd = (c_sd + alpha*p0_sd) / (n_d + alpha), with p0 a
         seeded random-init table (north star: random-init priors) or REF's expert table
         (``expert_table``: a domain without labelled mass keeps REF's column); pi_d ~ Dirichlet(1).
-        ``floor`` [16, D] bounds every likelihood from below (``unknown_floor``); the prior of
+        ``floor`` [16, D] bounds every likelihood from below (``unknown_floor``), ``ceil`` from
+        above (REF's table spans [0.05, 0.95]: no symptom's presence or absence is near-certain
+        evidence); the prior of
         ``cap_domain`` is capped at the largest prior of the other active domains (the no-fault
         class, the most frequent label, must not win on its prior alone).
         ``temperature`` T divides every logit (calibration: same argmax, flatter posteriors for
@@ -448,6 +451,8 @@ class NaiveBayes:
         p = (c + alpha * p0) / (n[None, :] + alpha)
         if floor is not None:
             p = np.maximum(p, floor)
+        if ceil is not None:
+            p = np.minimum(p, float(ceil))
         priors_arr = (n + prior_pseudo) / (n.sum() + prior_pseudo * len(idx))
         if cap_domain is not None and cap_domain in domains:
             u = list(domains).index(cap_domain)

@@ -171,8 +171,8 @@ class PyEngine {
   void set_app_model(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> b) {
     e_->set_app_model(b.data(), (size_t)b.size());
   }
-  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom) {
-    eng().set_refit(alpha, prior_pseudo, inv_temp, min_count, cap_dom);
+  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom, double ceil) {
+    eng().set_refit(alpha, prior_pseudo, inv_temp, min_count, cap_dom, ceil);
   }
   void refit_now() { eng().refit_now(); }
   // K3 on given features (REF's 55 rows, offline evaluation) with the model on the device
@@ -367,7 +367,7 @@ PYBIND11_MODULE(_mislo_agent, m) {
       .def("set_app_model", &PyEngine::set_app_model)
       .def("set_p0", &PyEngine::set_p0)
       .def("set_refit", &PyEngine::set_refit, py::arg("alpha") = 2.0, py::arg("prior_pseudo") = 1.0,
-           py::arg("inv_temp") = 1.0, py::arg("min_count") = 0.0, py::arg("cap_dom") = -1)
+           py::arg("inv_temp") = 1.0, py::arg("min_count") = 0.0, py::arg("cap_dom") = -1, py::arg("ceil") = 1.0)
       .def("refit_now", &PyEngine::refit_now)
       .def("set_device_refit", [](PyEngine& p, bool on) { p.eng().set_device_refit(on); })
       .def("score", &PyEngine::score, py::arg("feat"), py::arg("labels") = py::none(), py::arg("app") = py::none())

@@ -64,6 +64,7 @@ struct EngineConfig {
   double alpha = 2.0, prior_pseudo = 1.0;
   double inv_temp = 1.0, min_count = 0.0;  // refit calibration (posterior.hip k_refit_nb)
   int cap_dom = -1;                         // refit: the domain whose prior is capped (-1: none)
+  double lik_ceil = 1.0;                    // refit: every likelihood capped here (models/train.py lik_ceil)
   int n_dom = 10;
   float ttft_slo_ms = 800.0f;  // per-incident SLO impact: spans with TTFT above this breach
   double halo_ms = 0.0;        // later windows also join rows this close to every later window's latest record
@@ -133,7 +134,8 @@ class WindowEngine {
   // device refit parameters (smoothing, prior pseudo-count, 1 / temperature, minimum labelled mass
   // of an active domain), and a refit of the model from the accumulated statistics now
   // (stream-ordered before the next window)
-  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom = -1);
+  void set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom = -1,
+                 double ceil = 1.0);
   void refit_now();
   // stop (or resume) the per-window prequential refit: the model on the device stays frozen
   void set_device_refit(bool on) { cfg_.device_refit = on; }

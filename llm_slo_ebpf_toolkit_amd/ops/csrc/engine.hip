@@ -719,7 +719,7 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
     // deterministic prequential lag of nb, identical on every rank
     launch_refit_nb(stats_acc_, packet_dev_[b] + kStatsOff, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
                     reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count,
-                    p0_ + kSlots * 16, cfg_.cap_dom);
+                    p0_ + kSlots * 16, cfg_.cap_dom, cfg_.lik_ceil);
     ++folded_;
   }
   const bool xchg = exchange() || injected;
@@ -871,9 +871,12 @@ void WindowEngine::set_p0(const double* p0, size_t n) {
   HIPCHECK(hipMemcpy(p0_, p0, n * sizeof(double), hipMemcpyHostToDevice));
 }
 
-void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom) {
-  if (!(alpha > 0.0) || !(prior_pseudo >= 0.0) || !(inv_temp > 0.0) || !(min_count >= 0.0) || cap_dom >= cfg_.n_dom)
+void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp, double min_count, int cap_dom,
+                             double ceil) {
+  if (!(alpha > 0.0) || !(prior_pseudo >= 0.0) || !(inv_temp > 0.0) || !(min_count >= 0.0) || cap_dom >= cfg_.n_dom ||
+      !(ceil > 0.0 && ceil <= 1.0))
     throw std::invalid_argument("refit parameters");
+  cfg_.lik_ceil = ceil;
   cfg_.cap_dom = cap_dom < 0 ? -1 : cap_dom;
   cfg_.alpha = alpha;
   cfg_.prior_pseudo = prior_pseudo;
@@ -884,7 +887,7 @@ void WindowEngine::set_refit(double alpha, double prior_pseudo, double inv_temp,
 void WindowEngine::refit_now() {
   launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
                   reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count,
-                    p0_ + kSlots * 16, cfg_.cap_dom);
+                    p0_ + kSlots * 16, cfg_.cap_dom, cfg_.lik_ceil);
 }
 
 void WindowEngine::score_features(const float* feat, int n, const int32_t* labels, double* post, int32_t* pred,
@@ -1054,7 +1057,7 @@ void WindowEngine::restore(const double* stats, const void* model, size_t n, int
   } else {  // the learned model from the restored statistics, by the device refit itself
     launch_refit_nb(stats_acc_, nullptr, p0_, cfg_.alpha, cfg_.prior_pseudo, cfg_.n_dom,
                     reinterpret_cast<PosteriorModel*>(model_dev_), compute_, cfg_.inv_temp, cfg_.min_count,
-                    p0_ + kSlots * 16, cfg_.cap_dom);
+                    p0_ + kSlots * 16, cfg_.cap_dom, cfg_.lik_ceil);
     HIPCHECK(hipStreamSynchronize(compute_));
   }
   folded_ = folded;

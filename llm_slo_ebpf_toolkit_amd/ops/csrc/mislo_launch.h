@@ -205,7 +205,7 @@ void launch_posterior_stats(const float* feat, const int* ng_dev, int cap, const
                             const uint32_t* app_cnt = nullptr);
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
                      PosteriorModel* pm, hipStream_t stream, double inv_temp = 1.0, double min_count = 0.0,
-                     const double* floor_tab = nullptr, int cap_dom = -1);
+                     const double* floor_tab = nullptr, int cap_dom = -1, double ceil = 1.0);
 
 // gatestats.hip (K5)
 int boot_max_n();

@@ -361,7 +361,8 @@ __global__ __launch_bounds__(NT) void k_posterior_stats(PosteriorArgs p, StatsAr
 __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, const double* __restrict__ add,
                                                   const double* __restrict__ p0, const double* __restrict__ floor_tab,
                                                   double alpha, double prior_pseudo, int n_dom, double inv_temp,
-                                                  double min_count, int cap_dom, PosteriorModel* __restrict__ pm) {
+                                                  double min_count, int cap_dom, double ceil,
+                                                  PosteriorModel* __restrict__ pm) {
   __shared__ double s_logpn[kSlots][kMaxDomains];
   __shared__ double s_pe[kSlots][kMaxDomains];
   __shared__ double s_logpi[kMaxDomains];
@@ -380,6 +381,7 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
       const double c = stats[sl * 32 + d];
       double p = (c + alpha * p0[sl * 16 + d]) / (n + alpha);
       if (floor_tab) p = fmax(p, floor_tab[sl * 16 + d]);
+      p = fmin(p, ceil);  // the learned likelihood cap (models/bayes.py NaiveBayes.learned ceil)
       const double pe = fmin(fmax(p, 0.01), 0.99), pn = fmin(fmax(1.0 - p, 0.01), 0.99);
       pm->w[sl][d] = (log(pe) - log(pn)) * inv_temp;
       s_logpn[sl][d] = log(pn);
@@ -462,9 +464,9 @@ __global__ __launch_bounds__(256) void k_refit_nb(double* __restrict__ stats, co
 
 void launch_refit_nb(double* stats, const double* add, const double* p0, double alpha, double prior_pseudo, int n_dom,
                      PosteriorModel* pm, hipStream_t stream, double inv_temp, double min_count, const double* floor_tab,
-                     int cap_dom) {
+                     int cap_dom, double ceil) {
   hipLaunchKernelGGL(k_refit_nb, dim3(1), dim3(256), 0, stream, stats, add, p0, floor_tab, alpha, prior_pseudo, n_dom,
-                     inv_temp, min_count, cap_dom, pm);
+                     inv_temp, min_count, cap_dom, ceil, pm);
 }
 
 constexpr int kPostNT = 256, kStatsRPW = 256;

@@ -404,8 +404,10 @@ class CpuRingEngine:
     # rebuilding the tables from the all-reduced statistics) has no counterpart here, and the image
     # a trainer restores is already the host-fitted model (models/train.py), which the device refit
     # reproduces (__graft_entry__.smoke checks that equality on the GPU).
-    def set_refit(self, alpha: float, prior_pseudo: float, inv_temp: float, min_count: float, cap_dom: int = -1) -> None:
-        self.refit_params = (float(alpha), float(prior_pseudo), float(inv_temp), float(min_count), int(cap_dom))
+    def set_refit(self, alpha: float, prior_pseudo: float, inv_temp: float, min_count: float, cap_dom: int = -1,
+                  ceil: float = 1.0) -> None:
+        self.refit_params = (float(alpha), float(prior_pseudo), float(inv_temp), float(min_count), int(cap_dom),
+                             float(ceil))
 
     def refit_now(self) -> None:
         pass

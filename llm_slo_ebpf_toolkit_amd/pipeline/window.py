@@ -166,17 +166,23 @@ class WindowPipeline:
         return NaiveBayes.learned(SufficientStats(), seed=self.seed)
 
     def set_prior(self, init: Optional[np.ndarray] = None, floor: Optional[np.ndarray] = None,
-                  cap_domain: Optional[str] = None) -> None:
+                  cap_domain: Optional[str] = None, ceil: Optional[float] = None) -> None:
         """The learned model's Beta prior table [16, D] (None: the seeded random-init one), its
         likelihood floor [16, D] and the capped-prior domain (models/train.py learned_kwargs), on
-        the device refit (k_refit_nb) and the host mirror alike. The refit's other parameters
-        stay set_refit's."""
+        the device refit (k_refit_nb) and the host mirror alike; ``ceil`` caps every likelihood
+        (the device's through set_refit, ``lik_ceil()``). The refit's other parameters stay
+        set_refit's."""
         p0 = np.zeros((2, 16, 16), dtype=np.float64)
         p0[0, :, :N_DOMAINS] = init if init is not None else NaiveBayes.random_init_table(self.seed)
         if floor is not None:
             p0[1, :, :N_DOMAINS] = floor
         self.eng.set_p0(p0.ravel())
-        self.learned_kw = {"seed": self.seed, "init": init, "floor": floor, "cap_domain": cap_domain}
+        self.learned_kw = {"seed": self.seed, "init": init, "floor": floor, "cap_domain": cap_domain, "ceil": ceil}
+
+    def lik_ceil(self) -> float:
+        """The likelihood cap for set_refit (1.0: none)."""
+        c = self.learned_kw.get("ceil")
+        return 1.0 if c is None else float(c)
 
     def cap_dom(self) -> int:
         """The capped-prior domain's index for set_refit (-1: none)."""

@@ -533,8 +533,8 @@ def test_expert_prior_floor_and_capped_unknown_refit_matches_the_host_model():
     model = with_pairs(NaiveBayes.learned(host, temperature=T, **kw), rho, T)
     uncapped = NaiveBayes.learned(host, temperature=T, **dict(kw, cap_domain=None))
     pipe.eng.restore(st, model_bytes(model), len(imgs))
-    pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"])
-    pipe.eng.set_refit(cfg.alpha, cfg.prior_pseudo, 1.0 / T, cfg.min_count, pipe.cap_dom())
+    pipe.set_prior(kw["init"], kw["floor"], kw["cap_domain"], kw["ceil"])
+    pipe.eng.set_refit(cfg.alpha, cfg.prior_pseudo, 1.0 / T, cfg.min_count, pipe.cap_dom(), pipe.lik_ceil())
     pipe.eng.refit_now()
     dev_img = np.frombuffer(np.asarray(pipe.eng.model_bytes(), dtype=np.uint8).tobytes(), dtype=MODEL_DTYPE)[0]
     ref_img = np.frombuffer(model_bytes(model).tobytes(), dtype=MODEL_DTYPE)[0]
