@@ -486,6 +486,7 @@ def main() -> int:
             "active_domains": [d for i, d in enumerate(catalog_domains()) if np.isfinite(model.bias[i])]})
         train_info = {"windows": len(train_imgs), "held_out": len(hold_f), "temperature": round(T, 4),
                       "likelihood_prior": tcfg.init, "alpha": mtrain.learned_kwargs(tcfg)["alpha"], "unknown_calibrated": tcfg.calibrate_unknown,
+                      "likelihood_cap": tcfg.lik_ceil,
                       "pair_rho": round(rho, 4),
                       "holdout_nll": round(nll, 4), "holdout_nll_t1": round(trained.meta["holdout_nll_t1"], 4),
                       "seconds": round(train_s, 3), "events_per_window": a.train_events,
