@@ -187,7 +187,10 @@ class BurnRateForecaster:
     realised over them. ``error()`` is the mean absolute error of the scored forecasts relative
     to the realised burn. REF reports this metric as the hard-coded 0.07
     (pkg/benchmark/harness.go:103); here it is measured. Keyed per SLO owner (service /
-    incident group)."""
+    incident group).
+
+    On the benchgen episodes the segment forecast is at the data's floor: an estimator told where
+    each fault's plateau starts scores no better (tools/burn_floor.py, profiles/r6_burn/)."""
 
     def __init__(self, target: float = 0.99, horizon: int = 300, short: int = 30, floor: float = 0.05,
                  min_requests: float = 1000.0, method: str = "segment", change_llr: float = 8.0,
