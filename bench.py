@@ -63,7 +63,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--engine", default="gpu", choices=("gpu", "cpu"),
                     help="cpu: the window engine's host oracle over gloo (CI rehearsal of the multi-rank path)")
-    ap.add_argument("--steps", type=int, default=20)
+    # 100 timed windows by default: the timed region holds one window's fill and drain (its copy
+    # before any kernel, its last kernels after the last copy -- the 1.5 ms DMA-to-results latency)
+    # besides K overlapped windows, ~8 % of a 20-window run, ~1.5 % of a 100-window one
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--events", type=int, default=1 << 20, help="events per window per GPU")
     ap.add_argument("--spans", type=int, default=16384, help="spans per window per GPU")
