@@ -428,7 +428,7 @@ class SpanMapper:
                         self._early[th] = True
                         while len(self._early) > self.retrieval_cap:
                             self._early.popitem(last=False)
-                    fl = records.SPAN_SLI_ONLY
+                    fl = records.SPAN_FIRST_TOKEN
                 else:
                     with self._rlock:
                         if self._early.pop(th, None) is not None:
@@ -438,8 +438,8 @@ class SpanMapper:
                             while len(self._final) > self.retrieval_cap:
                                 self._final.popitem(last=False)
             flags.append(fl)
-            rv = retr.get(th) if fl != records.SPAN_SLI_ONLY else None
-            if self._retr and th and fl != records.SPAN_SLI_ONLY:
+            rv = retr.get(th) if fl != records.SPAN_FIRST_TOKEN else None
+            if self._retr and th and fl != records.SPAN_FIRST_TOKEN:
                 with self._rlock:
                     early = self._retr.pop(th, None)
                 if early is not None:

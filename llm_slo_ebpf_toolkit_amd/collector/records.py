@@ -215,11 +215,13 @@ SPAN = np.dtype([
     # 60 bit 0 (SPAN_LATE): the request's TTFT-SLO deadline (start + SLO) passed before the agent's
     # last window cut -- a breach that belongs to an earlier window (collector/otlp.py);
     # bit 1 (SPAN_NO_SLI): the request's SLI was counted by its first-token record already -- the
-    # request span joins but does not count again; bit 2 (SPAN_SLI_ONLY): a first-token record
-    # (exported when the first token is out, llm.slo.ttft_early) -- counted, never joined
+    # request span joins but does not count again; bit 2 (SPAN_FIRST_TOKEN): a first-token record
+    # (exported when the first token is out, llm.slo.ttft_early) -- counted, and joined like the
+    # request span (its keys but the connection: the request span brings the pod+conn tier), so the
+    # request's kernel evidence reaches the window its SLI is counted in
     ("flags", "<u4"),
 ])
-SPAN_LATE, SPAN_NO_SLI, SPAN_SLI_ONLY = 1, 2, 4
+SPAN_LATE, SPAN_NO_SLI, SPAN_FIRST_TOKEN = 1, 2, 4
 assert SPAN.itemsize == 64
 
 FLAG_HAS_GPU = 1 << 8

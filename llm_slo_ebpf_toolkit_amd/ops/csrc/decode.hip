@@ -695,7 +695,8 @@ __global__ __launch_bounds__(NT) void k_decode_spans(const void* __restrict__ sp
         grp /= (uint32_t)sm.sh_world;
         if (!mine) r.ts = 0;  // another GPU's incident group: never joins, never counted here
       }
-      if (s.flags & kSpanSliOnly) r.ts = 0;  // a first-token record: the SLI, not a join row
+      // a first-token record (kSpanFirstToken) joins like its request span: the request's evidence
+      // reaches the window its SLI is counted in, not the one its request span is exported in
       // per-incident TTFT SLO accounting (a request whose first-token record counted it: once)
       if (mine && sm.grp_sli && grp < (uint32_t)sm.n_groups && !(s.flags & kSpanNoSli)) {
         const bool breach = s.ttft_ms > sm.ttft_slo_ms;

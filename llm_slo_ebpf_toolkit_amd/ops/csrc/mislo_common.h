@@ -118,10 +118,10 @@ struct alignas(64) Span {
   uint64_t span_h;
   float retr_ms;
   uint32_t flags;  // bit 0 (kSpanLate): the TTFT-SLO deadline passed before the agent's last cut;
-                   // bit 1 (kSpanNoSli): SLI counted by the first-token record; bit 2 (kSpanSliOnly):
-                   // a first-token record (counted, never joined) -- collector/records.py SPAN
+                   // bit 1 (kSpanNoSli): SLI counted by the first-token record; bit 2 (kSpanFirstToken):
+                   // a first-token record (counted and joined) -- collector/records.py SPAN
 };
-constexpr uint32_t kSpanLate = 1u, kSpanNoSli = 2u, kSpanSliOnly = 4u;
+constexpr uint32_t kSpanLate = 1u, kSpanNoSli = 2u, kSpanFirstToken = 4u;
 static_assert(sizeof(Span) == 64, "Span must be 64 bytes");
 // 20-byte span record (collector/records.py SPAN20, runtime/csrc/records.h Span20): the fields the
 // join reads, with (pod, pid, conn32, svc|node) as a context id into the device context table and

@@ -252,7 +252,6 @@ class CpuRingEngine:
         sp = _gather(spans)
         spr = oracle.spans_native(sp.view(records.SPAN) if len(sp) else np.zeros(0, records.SPAN))
         counted = (spr["flags"] & np.uint32(records.SPAN_NO_SLI)) == 0  # first-token records count once
-        spr["ts_ns"] = np.where((spr["flags"] & np.uint32(records.SPAN_SLI_ONLY)) != 0, 0, spr["ts_ns"])
         G = int(n_groups)
         grp_local = spr["group_id"].astype(np.int64)
         if self.shard_world > 1:

@@ -1,9 +1,12 @@
-"""First-token SLI records (collector/records.py SPAN_SLI_ONLY / SPAN_NO_SLI): a service exports a
+"""First-token SLI records (collector/records.py SPAN_FIRST_TOKEN / SPAN_NO_SLI): a service exports a
 request's TTFT when its first token is out (demo/rag_service.py chat.first_token,
 llm.slo.ttft_early) and the request span at the end; the receiver (collector/otlp.py) flags the
-pair so the request counts once -- the first-token record carries the SLI and never joins, the
-request span joins and does not count again. On both engines a window with the pairs equals the
-same window with the request spans alone (k_decode_spans / pipeline/cpu.py)."""
+pair so the request counts once -- the first-token record carries the SLI, the request span does
+not count again. Both join: the first-token record brings the request's kernel evidence into the
+window its SLI is counted in (a CPU-starved service exports its request spans a window or more
+later), the request span adds the pod+conn tier. On both engines the SLI, late and retrieval
+counts of a window with the pairs equal those with the request spans alone; the GPU engine's
+paired windows equal the host engine's (k_decode_spans / pipeline/cpu.py)."""
 
 import os
 
@@ -56,7 +59,7 @@ def test_receiver_counts_a_request_once_whichever_record_comes_first():
     a, b, c = (f"{i:032x}" for i in (1, 2, 3))
     # a: first token, then the request span (with its retrieval breakdown)
     r1 = m.records(otlp.parse_json(_json([_early(a, 90.0)])))
-    assert len(r1) == 1 and int(r1["flags"][0]) == R.SPAN_SLI_ONLY and float(r1["retr_ms"][0]) == 0.0
+    assert len(r1) == 1 and int(r1["flags"][0]) == R.SPAN_FIRST_TOKEN and float(r1["retr_ms"][0]) == 0.0
     r2 = m.records(otlp.parse_json(_json(_final(a, 91.0, retr=150.0))))
     assert len(r2) == 1 and int(r2["flags"][0]) == R.SPAN_NO_SLI
     assert r2["retr_ms"][0] == np.float32(150.0)  # the retrieval folds into the request span, not the early one
@@ -69,7 +72,7 @@ def test_receiver_counts_a_request_once_whichever_record_comes_first():
     # late flag combines: a first-token record whose deadline passed before the last cut
     m.slo_ms, m.late_before_ns = 10.0, T0 + 50_000_000
     r4 = m.records(otlp.parse_json(_json([_early(f"{4:032x}", 80.0)])))
-    assert int(r4["flags"][0]) == R.SPAN_SLI_ONLY | R.SPAN_LATE
+    assert int(r4["flags"][0]) == R.SPAN_FIRST_TOKEN | R.SPAN_LATE
     # the tables are bounded
     m2 = otlp.SpanMapper(otlp.GroupTable(4), Interner().id)
     m2.retrieval_cap = 3
@@ -96,8 +99,8 @@ def test_rag_service_exports_the_first_token_record():
     assert ring.size == 6
     for o in outs:
         mine = buf[buf["trace_h"] == np.uint64(otlp.trace_hash(o["trace_id"]))]
-        assert sorted(int(f) for f in mine["flags"]) == [R.SPAN_NO_SLI, R.SPAN_SLI_ONLY]
-        early = mine[mine["flags"] == R.SPAN_SLI_ONLY][0]
+        assert sorted(int(f) for f in mine["flags"]) == [R.SPAN_NO_SLI, R.SPAN_FIRST_TOKEN]
+        early = mine[mine["flags"] == R.SPAN_FIRST_TOKEN][0]
         assert abs(float(early["ttft_ms"]) - o["ttft_ms"]) < 2.0  # the request span's definition, known earlier
 
 
@@ -106,7 +109,7 @@ def _with_first_token(sp, every=2):
     sp = sp.copy()
     idx = np.arange(0, len(sp), every)
     early = sp[idx].copy()
-    early["flags"] = R.SPAN_SLI_ONLY
+    early["flags"] = R.SPAN_FIRST_TOKEN
     early["retr_ms"] = 0.0
     early["conn_h"] = 0
     sp["flags"][idx] |= R.SPAN_NO_SLI
@@ -139,7 +142,7 @@ def _run(engine, wins, tag, pair):
 
 
 @pytest.mark.parametrize("engine", ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)])
-def test_first_token_records_change_nothing_but_when_the_sli_arrives(engine):
+def test_first_token_records_count_once_and_join(engine):
     from tests.test_native_engine import windows
 
     wins, gen = windows(n_win=2, seed=7)
@@ -148,9 +151,16 @@ def test_first_token_records_change_nothing_but_when_the_sli_arrives(engine):
     plain = _run(engine, wins, f"{engine}{os.getpid()}p", False)
     paired = _run(engine, wins, f"{engine}{os.getpid()}q", True)
     for j, ((d0, h0, r0), (d1, h1, r1)) in enumerate(zip(plain, paired)):
-        np.testing.assert_array_equal(d0, d1, err_msg=f"window {j} dbg (joins, candidates)")
-        np.testing.assert_array_equal(h0, h1, err_msg=f"window {j} hist")
-        for key in ("sli", "late", "app", "feat", "pred", "evbits"):
+        np.testing.assert_array_equal(h0, h1, err_msg=f"window {j} hist")  # the signals are the same
+        for key in ("sli", "late", "app"):  # each request counted once, retrieval on the request span
             np.testing.assert_array_equal(r0[key], r1[key], err_msg=f"window {j} {key}")
-        np.testing.assert_array_equal(r0["post"], r1["post"])
         assert r0["sli"][:, 0].sum() == len(wins[j].spans0)
+        assert d1[0] > d0[0], f"window {j}: the first-token records join (pairs {d0[0]} -> {d1[0]})"
+    if engine == "gpu":  # the paired windows on the device equal the host engine's
+        host = _run("cpu", wins, f"h{os.getpid()}q", True)
+        for j, ((d1, h1, r1), (dh, hh, rh)) in enumerate(zip(paired, host)):
+            np.testing.assert_array_equal(d1, dh, err_msg=f"window {j} dbg (joins, candidates)")
+            np.testing.assert_array_equal(h1, hh, err_msg=f"window {j} hist")
+            for key in ("sli", "late", "app", "feat", "pred", "evbits"):
+                np.testing.assert_array_equal(r1[key], rh[key], err_msg=f"window {j} {key}")
+            np.testing.assert_allclose(r1["post"], rh["post"], rtol=1e-9, atol=1e-12)
