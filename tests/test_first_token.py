@@ -159,7 +159,10 @@ def test_first_token_records_count_once_and_join(engine):
     if engine == "gpu":  # the paired windows on the device equal the host engine's
         host = _run("cpu", wins, f"h{os.getpid()}q", True)
         for j, ((d1, h1, r1), (dh, hh, rh)) in enumerate(zip(paired, host)):
-            np.testing.assert_array_equal(d1, dh, err_msg=f"window {j} dbg (joins, candidates)")
+            # dbg: candidates, low-confidence (the device reports raw and overlap in [1:3], the host
+            # the net count and 0), fan-out drops, enriched spans
+            net = lambda d: [int(d[0]), int(d[1] - d[2]), int(d[3]), int(d[4])]  # noqa: E731
+            assert net(d1) == net(dh), (j, d1, dh)
             np.testing.assert_array_equal(h1, hh, err_msg=f"window {j} hist")
             for key in ("sli", "late", "app", "feat", "pred", "evbits"):
                 np.testing.assert_array_equal(r1[key], rh[key], err_msg=f"window {j} {key}")
