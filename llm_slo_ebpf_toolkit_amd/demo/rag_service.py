@@ -386,13 +386,15 @@ class RagService:
             tokens.append(t)
             if len(tokens) == 1 and self.early_ttft:
                 # the request span's TTFT definition (retrieval + the backend's time to its first
-                # token, a wait for the backend's lock excluded), known now instead of at the end
+                # token, a wait for the backend's lock excluded), known now instead of at the end;
+                # with the request's connection, so the record joins the pod+conn tier as well
                 t_ft = time.time_ns()
                 ttft_now = (t_r1 - t_req) / MS + (t_ft - t_gen[0]) / MS
+                ft_attrs = {semconv.ATTR_SLO_TTFT_MS: ttft_now, semconv.ATTR_SLO_TTFT_EARLY: True}
+                ft_attrs.update(conn_attrs)
                 self.spans.add([SpanExporter.span(
                     trace_id, hashlib.blake2b(f"{rid}/f".encode(), digest_size=8).hexdigest(), root, "chat.first_token",
-                    t_req, t_ft, {semconv.ATTR_SLO_TTFT_MS: ttft_now, semconv.ATTR_SLO_TTFT_EARLY: True})],
-                    urgent=True)
+                    t_req, t_ft, ft_attrs)], urgent=True)
             if emit:
                 emit({"token": t, "index": len(tokens) - 1})
 

@@ -102,6 +102,8 @@ def test_rag_service_exports_the_first_token_record():
         assert sorted(int(f) for f in mine["flags"]) == [R.SPAN_NO_SLI, R.SPAN_FIRST_TOKEN]
         early = mine[mine["flags"] == R.SPAN_FIRST_TOKEN][0]
         assert abs(float(early["ttft_ms"]) - o["ttft_ms"]) < 2.0  # the request span's definition, known earlier
+        final = mine[mine["flags"] == R.SPAN_NO_SLI][0]
+        assert early["conn_h"] == final["conn_h"]  # the request's connection: both join the pod+conn tier
 
 
 def _with_first_token(sp, every=2):
