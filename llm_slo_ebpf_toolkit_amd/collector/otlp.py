@@ -438,8 +438,10 @@ class SpanMapper:
                             while len(self._final) > self.retrieval_cap:
                                 self._final.popitem(last=False)
             flags.append(fl)
-            rv = retr.get(th) if fl != records.SPAN_FIRST_TOKEN else None
-            if self._retr and th and fl != records.SPAN_FIRST_TOKEN:
+            # the trace's retrieval breakdown goes to its first record (a first-token record when the
+            # service exports one), once: later records of the trace carry only what arrives with them
+            rv = retr.pop(th, None) if th else None
+            if self._retr and th:
                 with self._rlock:
                     early = self._retr.pop(th, None)
                 if early is not None:

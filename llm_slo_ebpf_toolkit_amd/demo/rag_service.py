@@ -372,6 +372,13 @@ class RagService:
                 time.sleep(wait / 1000.0)
             vdb_ms = plan.vectordb_ms
         t_r1 = time.time_ns()
+        # spans leave as an OTel SDK's batch processor sends them, as they end: the retrieval span
+        # now, ahead of the request's first token (its breakdown reaches the agent with the
+        # first-token record instead of at the request's end)
+        self.spans.add([SpanExporter.span(trace_id, rsp, root, "chat.retrieval", t_r0, t_r1, {
+            semconv.ATTR_RETRIEVAL_VECTORDB: float(vdb_ms),
+            semconv.ATTR_RETRIEVAL_NETWORK_MS: float(plan.network_ms),
+            semconv.ATTR_RETRIEVAL_DNS_MS: float(plan.dns_ms), "retrieval.selected_docs": len(docs)})])
         span = SpanRef(trace_id=trace_id, service="rag-service", node=self.node, pod=self.pod, pid=os.getpid(),
                        timestamp=t_req)
         sig = SignalRef(signal="dns_latency_ms", trace_id=trace_id, service="rag-service", node=self.node,
@@ -429,12 +436,8 @@ class RagService:
         root_attrs.update(conn_attrs)
         if decision.tier:
             root_attrs["llm.ebpf.correlation_tier"] = decision.tier
-        # in the order an OTel SDK exports them: as they end, the children before the request
+        # as they end: the generation before the request
         self.spans.add([
-            SpanExporter.span(trace_id, rsp, root, "chat.retrieval", t_r0, t_r1, {
-                semconv.ATTR_RETRIEVAL_VECTORDB: float(vdb_ms),
-                semconv.ATTR_RETRIEVAL_NETWORK_MS: float(plan.network_ms),
-                semconv.ATTR_RETRIEVAL_DNS_MS: float(plan.dns_ms), "retrieval.selected_docs": len(docs)}),
             SpanExporter.span(trace_id, gsp, root, "chat.generation", t_r1, t_end, {"llm.tokens.count": g["tokens"]}),
             SpanExporter.span(trace_id, root, "", "chat.request", t_req, t_end, root_attrs),
         ])

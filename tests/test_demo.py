@@ -47,11 +47,11 @@ def test_chat_roundtrip_metrics_and_traces(service):
     assert m["llm_slo_ttft_ms_count"] == 1 and m["llm_slo_burn_rate"] == 0
     svc.spans.flush()
     spans = [s for r in traces.requests for s in json.loads(r["body"])["resourceSpans"][0]["scopeSpans"][0]["spans"]]
-    # exported as an OTel SDK ends them: the children before the request; the first-token record
-    # (the TTFT SLI when the first token is out, llm.slo.ttft_early) ahead of them all
-    assert [s["name"] for s in spans] == ["chat.first_token", "chat.retrieval", "chat.generation", "chat.request"]
+    # exported as an OTel SDK ends them: the retrieval, then the first-token record (the TTFT SLI
+    # when the first token is out, llm.slo.ttft_early), then the generation and the request
+    assert [s["name"] for s in spans] == ["chat.retrieval", "chat.first_token", "chat.generation", "chat.request"]
     assert len({s["traceId"] for s in spans}) == 1
-    ft = {a["key"]: a["value"] for a in spans[0]["attributes"]}
+    ft = {a["key"]: a["value"] for a in spans[1]["attributes"]}
     assert ft["llm.slo.ttft_early"] == {"boolValue": True} and ft["llm.slo.ttft_ms"]["doubleValue"] > 0
 
 

@@ -63,6 +63,15 @@ def test_receiver_counts_a_request_once_whichever_record_comes_first():
     r2 = m.records(otlp.parse_json(_json(_final(a, 91.0, retr=150.0))))
     assert len(r2) == 1 and int(r2["flags"][0]) == R.SPAN_NO_SLI
     assert r2["retr_ms"][0] == np.float32(150.0)  # the retrieval folds into the request span, not the early one
+    # a2: the retrieval span sent before (or with) the first-token record: the breakdown rides on it
+    a2 = f"{5:032x}"
+    ret = _final(a2, 0.0, retr=120.0)[0]
+    r5 = m.records(otlp.parse_json(_json([ret])))
+    assert len(r5) == 0  # a child span: no record, its breakdown waits for the trace's first record
+    r6 = m.records(otlp.parse_json(_json([_early(a2, 95.0)])))
+    assert r6["retr_ms"][0] == np.float32(120.0)
+    r7 = m.records(otlp.parse_json(_json(_final(a2, 96.0))))
+    assert int(r7["flags"][0]) == R.SPAN_NO_SLI and float(r7["retr_ms"][0]) == 0.0  # counted once
     # b: the request span alone (a service without first-token export)
     r3 = m.records(otlp.parse_json(_json(_final(b, 50.0))))
     assert int(r3["flags"][0]) == 0
@@ -104,6 +113,8 @@ def test_rag_service_exports_the_first_token_record():
         assert abs(float(early["ttft_ms"]) - o["ttft_ms"]) < 2.0  # the request span's definition, known earlier
         final = mine[mine["flags"] == R.SPAN_NO_SLI][0]
         assert early["conn_h"] == final["conn_h"]  # the request's connection: both join the pod+conn tier
+        # the retrieval span leaves when it ends: its breakdown rides on the first-token record, once
+        assert float(early["retr_ms"]) > 0 and float(final["retr_ms"]) == 0.0
 
 
 def _with_first_token(sp, every=2):
