@@ -263,9 +263,12 @@ def main() -> int:
     ap.add_argument("--phase-s", type=float, default=15.0)
     ap.add_argument("--recover-s", type=float, default=8.0)
     ap.add_argument("--clients", type=int, default=2)
-    ap.add_argument("--burners-per-cpu", type=int, default=2,
-                    help="CPU burners per victim CPU: the service keeps ~1/3 of its CPUs, so requests still "
-                         "complete every window (at 6 only 8 requests completed in 15 s, profiles/r3_config3_fourth)")
+    ap.add_argument("--burners-per-cpu", type=int, default=3,
+                    help="CPU burners per victim CPU: at 3 the service keeps ~1/4 of its CPUs, its TTFT p50 doubles "
+                         "(93-115 ms against SLOs of 69-76 ms) and requests still complete every window (at 6 only 8 "
+                         "requests completed in 15 s, profiles/r3_config3_fourth); at 2 the fault's p50 sat at the SLO "
+                         "(1.5 x the healthy p95), so whether a window breached at all was a coin flip per run "
+                         "(profiles/r6_config3_g, _n)")
     ap.add_argument("--procfs-ms", type=int, default=100,
                     help="schedstat sampling interval: run-queue records join a request's span only within 100 ms "
                          "of its start (REF's pod+pid tier), so they must come faster than that")
