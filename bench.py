@@ -104,9 +104,9 @@ def parse():
                     help="one-GPU rehearsal of the multi-GPU chain (diagnostic, not the headline): a one-rank RCCL "
                          "communicator, the window split around the trace-row exchange (no rows arrive), the packet "
                          "all-reduce and the incident all-gather")
-    ap.add_argument("--user-rec", type=int, default=24, choices=(24, 32, 64),
-                    help="user-space ring record size: 24 = USER24 (the rocprof tool's compact record), 32 = USER32, "
-                         "64 = EVENT")
+    ap.add_argument("--user-rec", type=int, default=16, choices=(16, 24, 32, 64),
+                    help="user-space ring record size: 16 = USER16 (the rocprof tool's and samplers' compact slot; "
+                         "a traced record takes two), 24 = USER24, 32 = USER32, 64 = EVENT")
     ap.add_argument("--out", default="")
     ap.add_argument("--launch-probe", action="store_true",
                     help="rank bring-up only: join the process group, print the world JSON line, exit (no GPU)")
@@ -712,7 +712,9 @@ def main() -> int:
             "wire_bytes_per_event": 16,
             # batch records: 8 slots (events, definitions, pads) per 136 ring bytes
             "ring_bytes_per_kernel_event": round(sum(len(i.framed) for i in imgs) / max(1, sum(i.n_kernel for i in imgs)), 2),
-            "ring_bytes_per_user_record": a.user_rec,
+            "ring_bytes_per_user_record": round(sum(i.user.nbytes for i in imgs) / max(1, sum(
+                int((i.user["pid_sig"] != np.uint32(0xFFFFFFFF)).sum()) if a.user_rec == 16 else len(i.user)
+                for i in imgs)), 2),
             "device_buffers": a.buffers,
             "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default"),
             "learning_in_timed_region": False,

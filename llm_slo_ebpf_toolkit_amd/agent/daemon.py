@@ -505,7 +505,7 @@ class Agent:
             sets = []
             for r, names in enumerate(sets_names):
                 ring = maps.ring if r == 0 else rt.Ringbuf.open_pinned(os.path.join(o.pin_dir, f"mislo_events{r}"))
-                sets.append((ring, rt.HostRing(1 << 20, 24, names.user),   # the rocprofiler tool pushes USER24
+                sets.append((ring, rt.HostRing(1 << 20, 16, names.user),   # the rocprofiler tool pushes USER16
                              rt.HostRing(1 << 18, 64, names.spans)))       # OTLP receiver / services
             return maps, sets, None
         if o.source == "shm":

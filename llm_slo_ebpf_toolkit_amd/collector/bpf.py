@@ -313,16 +313,17 @@ class ShardRouter:
 
 
 def create_shard_rings(prefix: str, world: int, ring_bytes: int, user_records: int, span_records: int,
-                       user_rec: int = 24):
+                       user_rec: int = 16):
     """One ring set per worker (split rings), each sized for its share of the node's stream."""
     return [create_rings(RingNames.of(prefix, r), ring_bytes, user_records, span_records, user_rec)
             for r in range(max(1, int(world)))]
 
 
-def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int, user_rec: int = 24):
+def create_rings(names: RingNames, ring_bytes: int, user_records: int, span_records: int, user_rec: int = 16):
     """Create the emulated BPF ring and the two user-space rings (the agent owns them). The
-    user-space ring holds ``user_rec``-byte records: 24 = USER24 (what the rocprofiler tool
-    writes into such a ring, 3/8 of the PCIe bytes of a 64-byte EVENT), 32 = USER32."""
+    user-space ring holds ``user_rec``-byte records: 16 = USER16 slots (what the rocprofiler tool
+    and the samplers write into such a ring: a quarter of the PCIe bytes of a 64-byte EVENT, a
+    traced record two slots), 24 = USER24, 32 = USER32."""
     from ..runtime import load
 
     rt = load()

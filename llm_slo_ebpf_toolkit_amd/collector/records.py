@@ -153,6 +153,21 @@ USER24 = np.dtype([
 ])
 assert USER24.itemsize == 24
 USER24_TS_BITS = 44
+# 16-byte user-space slot (rings created with 16-byte records; ops/csrc/mislo_common.h User16):
+# USER24 without the trace hash. A record with a trace (pid_sig bit 31) is followed by a
+# continuation slot {trace lo, trace hi, USER16_CONT, 0} that decodes as a hole; both are pushed
+# in one batch, so a window never splits them. The GPU signals' records carry no trace unless the
+# workload tagged its kernels (probes/rocprof mislo_rocprof_set_trace), so most take 16 bytes,
+# two thirds of USER24. Signal type < 127 (127 with every other bit set would read as the marker).
+USER16 = np.dtype([
+    ("ts_lo", "<u4"),        # 0  ts bits 0..31
+    ("value_milli", "<u4"),  # 4
+    ("pid_sig", "<u4"),      # 8  pid | signal_type << 22 | ts_zero << 29 | has_gpu << 30 | has_trace << 31
+    ("pod_ts", "<u4"),       # 12 pod_id | (ts bits 32..43) << 20
+])
+assert USER16.itemsize == 16
+USER16_CONT = 0xFFFFFFFF
+USER16_HAS_TRACE = 1 << 31
 
 WIRE_DTYPES = {64: EVENT, 16: EVENT16}
 RB_BUSY, RB_DISCARD, RB_HDR = 1 << 31, 1 << 30, 8   # BPF ring buffer record header bits
@@ -384,6 +399,46 @@ def to_user24(events: np.ndarray) -> np.ndarray:
     return out
 
 
+def to_user16(events: np.ndarray) -> np.ndarray:
+    """64-byte EVENT records -> USER16 slots (a traced record takes two: the record, then its
+    trace in a continuation slot). Raises like ``to_user24`` and on signal type 127."""
+    u24 = to_user24(events)
+    st = events["signal_type"].astype(np.int64)
+    if len(events) and st.max() >= 127:
+        raise ValueError("USER16 holds signal type < 127")
+    traced = u24["trace_h"] != 0
+    n = len(u24) + int(traced.sum())
+    out = np.zeros(n, dtype=USER16)
+    pos = np.arange(len(u24)) + np.concatenate([[0], np.cumsum(traced)[:-1]]).astype(np.int64) if len(u24) else \
+        np.zeros(0, np.int64)
+    out["ts_lo"][pos] = u24["ts_lo"]
+    out["value_milli"][pos] = u24["value_milli"]
+    out["pid_sig"][pos] = u24["pid_sig"] | np.where(traced, np.uint32(USER16_HAS_TRACE), np.uint32(0))
+    out["pod_ts"][pos] = u24["pod_ts"]
+    cont = pos[traced] + 1
+    th = u24["trace_h"][traced].astype(np.uint64)
+    out["ts_lo"][cont] = (th & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    out["value_milli"][cont] = (th >> np.uint64(32)).astype(np.uint32)
+    out["pid_sig"][cont] = np.uint32(USER16_CONT)
+    return out
+
+
+def user16_to_user24(u: np.ndarray):
+    """USER16 slots -> (USER24 rows, one per slot, and the continuation mask: those rows are
+    holes). A record's trace comes from the slot after it."""
+    cont = u["pid_sig"] == np.uint32(USER16_CONT)
+    v = np.zeros(len(u), dtype=USER24)
+    v["ts_lo"], v["value_milli"], v["pod_ts"] = u["ts_lo"], u["value_milli"], u["pod_ts"]
+    v["pid_sig"] = u["pid_sig"] & np.uint32(0x7FFFFFFF)
+    has = ((u["pid_sig"] & np.uint32(USER16_HAS_TRACE)) != 0) & ~cont
+    nxt = np.minimum(np.arange(len(u)) + 1, max(len(u) - 1, 0))
+    ok = has & (np.arange(len(u)) + 1 < len(u))
+    ok &= cont[nxt] if len(u) else ok
+    tr = (u["value_milli"][nxt].astype(np.uint64) << np.uint64(32)) | u["ts_lo"][nxt].astype(np.uint64)
+    v["trace_h"] = np.where(ok, tr, np.uint64(0))
+    return v, cont
+
+
 def user24_ts(u: np.ndarray, base: int) -> np.ndarray:
     """USER24 timestamps: the value nearest ``base`` with the record's low 44 bits (0 when the
     record says it has none); ops/csrc/mislo_common.h user24_ts."""
@@ -418,7 +473,9 @@ def to_user(events: np.ndarray, rec: int) -> np.ndarray:
         return to_user32(events)
     if rec == 24:
         return to_user24(events)
-    raise ValueError(f"user-space records are 64, 32 or 24 bytes, not {rec}")
+    if rec == 16:
+        return to_user16(events)
+    raise ValueError(f"user-space records are 64, 32, 24 or 16 bytes, not {rec}")
 
 
 def milli_int(raw: np.ndarray, shift: np.ndarray) -> np.ndarray:

@@ -447,7 +447,7 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
   const int n = seg ? max(r0, min(rows[1], cap)) : r0;
   const int n_loc = min(n_ptr[0], r0);
   const int n_k = min(n_ptr[15], n_loc);
-  const int user_rec = n_ptr[6];  // counts[6]: user-space record bytes (64 = EVENT, 32 = User32, 24 = User24)
+  const int user_rec = n_ptr[6];  // counts[6]: user-space record bytes (64 = EVENT, 32 = User32, 24 = User24, 16 = User16)
   const int valid_k = min((int)min((uint32_t)n_k, rs[kRsFirstBusy]), n_k);
   auto base_at = [&](int lo) { return (int64_t)(((uint64_t)(uint32_t)n_ptr[lo + 1] << 32) | (uint32_t)n_ptr[lo]); };
   const int64_t t_base[4] = {base_at(4), base_at(8), base_at(10), base_at(12)};
@@ -498,6 +498,31 @@ __global__ __launch_bounds__(NT) void k_decode_window(const uint8_t* __restrict_
           ++events;
         } else {  // a hole: never counted, never joined
           decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
+        }
+      } else if (user_rec == 16) {
+        const int j = i - n_k;
+        const uint4 u = reinterpret_cast<const uint4*>(user)[j];  // {ts_lo, value, pid_sig, pod_ts}
+        const uint32_t pod = u.w & 0xFFFFFu;
+        const uint32_t sn = pod < n_pods ? pod_sn[pod] : 0u;
+        if (u.z == kUser16Cont) {  // a continuation slot: the previous record's trace, not a record
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
+        } else if (!shard_owns(sn, sh_rank, sh_world)) {
+          ++other;
+          decode_one(i, cap, 0, 0.f, -1, 0, 0, 0, 0, 0, o, l, unsupported, zero_ts, false, &s_stage[threadIdx.x * 5], tr);
+        } else {
+          uint64_t trh = 0;
+          if ((u.z & kUser16Trace) && i + 1 < n_loc) {
+            const uint4 c = reinterpret_cast<const uint4*>(user)[j + 1];
+            if (c.z == kUser16Cont) trh = ((uint64_t)c.y << 32) | c.x;
+          }
+          const uint32_t ps = u.z & ~kUser16Trace;
+          const int st = (int)((ps >> 22) & 0x7Fu);
+          const int slot = (int)L.tab.type_slot[st];
+          const int64_t ts = user24_ts(u.x, u.w, ps, u_base);
+          decode_one(i, cap, ts, (float)((double)u.y * 1e-3), slot, trh, pod, ps & 0x3FFFFFu, sn, 0ull, o, l,
+                     unsupported, zero_ts, true, &s_stage[threadIdx.x * 5], tr);
+          if (slot >= 0 && ts > 0) t_hi = max(t_hi, (unsigned long long)ts);
+          ++events;
         }
       } else if (user_rec == 24) {
         const uint2* u = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(user) + (size_t)(i - n_k) * 24);

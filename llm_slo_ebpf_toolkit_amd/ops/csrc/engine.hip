@@ -635,8 +635,8 @@ void WindowEngine::submit(int64_t k, const WindowInput& in, bool with_labels, bo
   for (const Seg& s : in.user) ub += s.bytes;
   for (const Seg& s : in.spans) sb += s.bytes;
   // what the kernels will assume, checked on the host before anything is queued
-  if (in.user_rec != 64 && in.user_rec != 32 && in.user_rec != 24)
-    throw std::invalid_argument("user records are 64, 32 or 24 bytes");
+  if (in.user_rec != 64 && in.user_rec != 32 && in.user_rec != 24 && in.user_rec != 16)
+    throw std::invalid_argument("user records are 64, 32, 24 or 16 bytes");
   if (kb % kRecStride || ub % in.user_rec || sb % 64) throw std::invalid_argument("segments must hold whole records");
   // kernel rows: every slot of every batch record (definitions and pads become holes)
   const size_t n_k = kb / kRecStride * kBatchSlots, n_u = ub / in.user_rec, n_s = sb / 64;

@@ -77,6 +77,13 @@ __host__ __device__ inline int64_t user24_ts(uint32_t ts_lo, uint32_t pod_ts, ui
   return base + sd;
 }
 
+// 16-byte user-space slot (collector/records.py USER16; rings created with 16-byte records):
+// User24 without the trace hash, {ts_lo, value_milli, pid_sig, pod_ts}. A record whose pid_sig
+// has bit 31 set carries a trace: the next slot is its continuation {trace lo, trace hi,
+// kUser16Cont, 0}, a hole (the producers push both in one batch, so no window splits them).
+constexpr uint32_t kUser16Cont = 0xFFFFFFFFu;
+constexpr uint32_t kUser16Trace = 1u << 31;
+
 // 16-byte wire record (EVENT16 = probes/ebpf/mislo_record.h mislo_event16, the payload of the
 // BPF ring's records): timestamp as an offset from one of the window's 4 epoch bases, selected
 // by the 2-bit tag in the top of trace_id (ts = base[tag] + ts_off; counts[4..5], [8..13]);

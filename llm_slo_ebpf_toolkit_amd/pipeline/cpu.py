@@ -235,20 +235,22 @@ class CpuRingEngine:
             fr[int(busy[0]):, 0] = np.uint32(records.RB_BUSY | records.REC_PAYLOAD)
             framed = fr.view(np.uint8).reshape(-1)
         ub = _gather(user)
-        udt = {64: records.EVENT, 32: records.USER32, 24: records.USER24}[int(user_rec)]
+        udt = {64: records.EVENT, 32: records.USER32, 24: records.USER24, 16: records.USER16}[int(user_rec)]
         u = ub.view(udt) if len(ub) else np.zeros(0, dtype=udt)
         d = oracle.decode_window(framed, u, self.table, self.tmap, bases, pod_sn=self.pod_sn)
         hdr, sl = records.framed_slots(framed) if len(fr) else (np.zeros(0, np.uint32), np.zeros((0, 4), np.uint32))
         valid_k = (hdr == records.REC_PAYLOAD) & ((sl[:, 1] & np.uint32(0xFF)) < records.DEF_FIRST)
         other = 0
-        is_rec = np.concatenate([valid_k, np.ones(len(u), bool)])
+        # USER16 continuation slots (a traced record's trace) are rows but not records
+        u_rec = u["pid_sig"] != np.uint32(records.USER16_CONT) if u.dtype == records.USER16 else np.ones(len(u), bool)
+        is_rec = np.concatenate([valid_k, u_rec])
         if self.shard_world > 1 and not self.split_rings:  # split rings: routed by the producers
             mine = shard_owner(d.svcnode, self.shard_world) == self.shard_rank
             drop = is_rec & ~mine
             other = int(drop.sum())
             d = _holes(d, drop)
             is_rec = is_rec & ~drop
-        events = int(valid_k.sum()) + len(u) - other
+        events = int(valid_k.sum()) + int(u_rec.sum()) - other
         sp = _gather(spans)
         spr = oracle.spans_native(sp.view(records.SPAN) if len(sp) else np.zeros(0, records.SPAN))
         counted = (spr["flags"] & np.uint32(records.SPAN_NO_SLI)) == 0  # first-token records count once

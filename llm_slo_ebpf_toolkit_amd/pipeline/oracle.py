@@ -154,6 +154,17 @@ def decode_user24(u: np.ndarray, pod_sn: Dict[int, int], base: int) -> Decoded:
     return decode_user32(records.user24_to_user32(u, base), pod_sn)
 
 
+def decode_user16(u: np.ndarray, pod_sn: Dict[int, int], base: int) -> Decoded:
+    """k_decode_window on USER16 slots: USER24's decode, the trace from a traced record's
+    continuation slot, continuation slots holes (ts 0, no slot, no keys)."""
+    v, cont = records.user16_to_user24(u)
+    d = decode_user24(v, pod_sn, base)
+    for f, z in (("ts", 0), ("val", 0), ("slot", NO_SLOT), ("status", 0), ("pod", 0), ("pid", 0), ("svcnode", 0),
+                 ("trace", 0), ("conn", 0)):
+        getattr(d, f)[cont] = z
+    return d
+
+
 def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: TraceMap, bases,
                   pod_sn: Dict[int, int] = None) -> Decoded:
     """k_decode_window: rows [0, n framed) from the slots of the framed batch records (row r =
@@ -179,6 +190,8 @@ def decode_window(framed: np.ndarray, user: np.ndarray, table: CtxTable, tmap: T
         u = decode_user32(user, pod_sn or {})
     elif user.dtype == records.USER24:
         u = decode_user24(user, pod_sn or {}, max(int(b) for b in bases))
+    elif user.dtype == records.USER16:
+        u = decode_user16(user, pod_sn or {}, max(int(b) for b in bases))
     else:
         u = decode_events(user)
         u.conn = records.conn32_np(u.conn).astype(np.uint64)

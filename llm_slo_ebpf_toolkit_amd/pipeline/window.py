@@ -196,7 +196,7 @@ class WindowPipeline:
         of framed ring records / ``user_rec``-byte records / 64-byte spans. Returns its index.
         USER24 records (``user_rec`` 24) keep 44 timestamp bits, resolved against the newest of
         ``bases``: a window of them needs a published epoch."""
-        if user_rec == 24 and not any(int(b) for b in bases) and any(int(n) for _, n in user):
+        if user_rec in (16, 24) and not any(int(b) for b in bases) and any(int(n) for _, n in user):
             raise ValueError("USER24 records need the window's epoch bases (all are 0)")
         k = self.k
         learn = (self.learn and with_labels) if learn is None else learn
@@ -395,8 +395,9 @@ class RingWindowSource:
             self.kmask = ring.size - 1
         # user-space producers' records: 64-byte EVENT, 32-byte USER32 or 24-byte USER24, per ring
         self.user_rec = int(user_ring.rec_size) if user_ring is not None else 64
-        if self.user_rec not in (24, 32, 64):
-            raise ValueError(f"user ring holds {self.user_rec}-byte records (EVENT = 64, USER32 = 32, USER24 = 24)")
+        if self.user_rec not in (16, 24, 32, 64):
+            raise ValueError(f"user ring holds {self.user_rec}-byte records (EVENT = 64, USER32 = 32, USER24 = 24, "
+                             "USER16 = 16)")
         if user_ring is not None:
             self.direct["user"] = pipe.eng.register_host(user_ring.address, user_ring.capacity * self.user_rec)
             self.upos = user_ring.tail

@@ -161,6 +161,7 @@ struct State {
   double xgmi_bytes_per_ns = 64.0;
   bool rec32 = false;  // the ring holds 32-byte USER32 records
   bool rec24 = false;  // the ring holds 24-byte USER24 records
+  bool rec16 = false;  // the ring holds 16-byte USER16 slots (a traced record takes two)
   bool verbose = false;
   std::mutex mu;
   struct Enq {
@@ -262,6 +263,22 @@ void emit(uint16_t type, uint64_t ts, uint64_t value, uint32_t thread, uint64_t 
     return;
   }
   bool ok;
+  if (g.rec16) {  // collector/records.py USER16: {ts_lo, value, pid_sig, pod_ts} [+ {trace, marker, 0}]
+    const uint64_t t = (uint64_t)wall;
+    uint32_t w[8] = {};
+    w[0] = (uint32_t)t;
+    w[1] = mislo_milli(type, value);
+    w[2] = ((uint32_t)getpid() & 0x3FFFFFu) | ((uint32_t)(type & 0x7F) << 22) | (wall == 0 ? 1u << 29 : 0u) |
+           (1u << 30) | (trace_h ? 1u << 31 : 0u);
+    w[3] = (g.pod & 0xFFFFFu) | (uint32_t)(((t >> 32) & 0xFFFu) << 20);
+    w[4] = (uint32_t)trace_h;
+    w[5] = (uint32_t)(trace_h >> 32);
+    w[6] = 0xFFFFFFFFu;  // continuation marker
+    const uint64_t n = trace_h ? 2 : 1;  // one batch: a window never splits a record from its trace
+    ok = mislo_ring_push_batch(ring, w, n) == n;
+    (ok ? g.pushed : g.dropped).fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
   if (g.rec24) {
     User24Rec u{};
     const uint64_t t = (uint64_t)wall;
@@ -821,6 +838,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   void* const r0 = g.ring.load(std::memory_order_acquire);
   g.rec32 = r0 && mislo_ring_rec_size(r0) == 32;
   g.rec24 = r0 && mislo_ring_rec_size(r0) == 24;
+  g.rec16 = r0 && mislo_ring_rec_size(r0) == 16;
   g.pod = (uint32_t)env_u64("MISLO_POD_ID", 0);
   route();
   g.node = (uint16_t)env_u64("MISLO_NODE_ID", 0);

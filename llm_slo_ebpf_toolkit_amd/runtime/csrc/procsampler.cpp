@@ -404,11 +404,14 @@ std::vector<EventRec> ProcSampler::tick(int64_t wall_ns, uint64_t mono_ns) {
   uint64_t pushed = 0;
   if (ring_ && !out.empty()) {
     const uint32_t rs = ring_->rec_size();
-    std::vector<uint8_t> buf(out.size() * rs);
-    size_t n = 0;
-    for (const EventRec& e : out)
-      if (pack_user(e, rs, buf.data() + n * rs)) ++n;
-    pushed = n ? ring_->push_batch(buf.data(), n) : 0;
+    std::vector<uint8_t> buf(2 * out.size() * rs);  // a traced USER16 record takes two slots
+    size_t n = 0, recs = 0;
+    for (const EventRec& e : out) {
+      const int w = pack_user(e, rs, buf.data() + n * rs);
+      n += (size_t)w;
+      recs += w ? 1u : 0u;
+    }
+    pushed = n && ring_->push_batch(buf.data(), n) == n ? recs : 0;  // all or nothing
   }
   ++st_.ticks;
   st_.targets = targets_.size();

@@ -115,6 +115,9 @@ struct User32Rec {  // records.py USER32
 };
 static_assert(sizeof(User32Rec) == 32, "USER32 is 32 bytes");
 
+constexpr uint32_t kUser16TraceBit = 1u << 31;   // records.py USER16_HAS_TRACE
+constexpr uint32_t kUser16ContWord = 0xFFFFFFFFu;  // records.py USER16_CONT
+
 struct User24Rec {  // records.py USER24
   uint64_t trace_h;
   uint32_t value_milli, ts_lo;
@@ -123,14 +126,16 @@ struct User24Rec {  // records.py USER24
 };
 static_assert(sizeof(User24Rec) == 24, "USER24 is 24 bytes");
 
-// records.py to_user: an EVENT as a user-space producer writes it into a `rec`-byte ring (64, 32
-// or 24 bytes at `out`). False when the record does not fit USER24 (pid >= 2^22, pod >= 2^20).
-inline bool pack_user(const EventRec& e, uint32_t rec, void* out) {
+// records.py to_user: an EVENT as a user-space producer writes it into a `rec`-byte ring (64, 32,
+// 24 or 16 bytes at `out`). Returns the slots written: 1, or 2 for a traced USER16 record (its
+// continuation slot; `out` must hold two), 0 when the record does not fit USER24 / USER16 (pid >=
+// 2^22, pod >= 2^20, signal type >= 128, or 127 in USER16).
+inline int pack_user(const EventRec& e, uint32_t rec, void* out) {
   const uint32_t vm = milli_int(e.value, milli_shift(e.signal_type));
   const uint32_t gpu = (e.flags >> 8) & 1u;
   if (rec == 64) {
     *static_cast<EventRec*>(out) = e;
-    return true;
+    return 1;
   }
   if (rec == 32) {
     User32Rec u{};
@@ -143,9 +148,10 @@ inline bool pack_user(const EventRec& e, uint32_t rec, void* out) {
     u.flags = (uint8_t)gpu;
     u.node_id = e.node_id;
     *static_cast<User32Rec*>(out) = u;
-    return true;
+    return 1;
   }
-  if (rec != 24 || e.pid >= (1u << 22) || e.pod_id >= (1u << 20) || e.signal_type >= 128) return false;
+  if ((rec != 24 && rec != 16) || e.pid >= (1u << 22) || e.pod_id >= (1u << 20) || e.signal_type >= 128) return 0;
+  if (rec == 16 && e.signal_type >= 127) return 0;
   const uint64_t t = (uint64_t)e.ts_ns;
   User24Rec u{};
   u.trace_h = e.trace_h;
@@ -153,8 +159,22 @@ inline bool pack_user(const EventRec& e, uint32_t rec, void* out) {
   u.ts_lo = (uint32_t)t;
   u.pid_sig = e.pid | ((uint32_t)e.signal_type << 22) | (e.ts_ns == 0 ? 1u << 29 : 0u) | (gpu << 30);
   u.pod_ts = e.pod_id | (uint32_t)(((t >> 32) & 0xFFFull) << 20);
-  *static_cast<User24Rec*>(out) = u;
-  return true;
+  if (rec == 24) {
+    *static_cast<User24Rec*>(out) = u;
+    return 1;
+  }
+  // USER16: {ts_lo, value, pid_sig | has_trace, pod_ts} [+ {trace lo, trace hi, marker, 0}]
+  uint32_t* w = static_cast<uint32_t*>(out);
+  w[0] = u.ts_lo;
+  w[1] = u.value_milli;
+  w[2] = u.pid_sig | (e.trace_h ? kUser16TraceBit : 0u);
+  w[3] = u.pod_ts;
+  if (!e.trace_h) return 1;
+  w[4] = (uint32_t)e.trace_h;
+  w[5] = (uint32_t)(e.trace_h >> 32);
+  w[6] = kUser16ContWord;
+  w[7] = 0u;
+  return 2;
 }
 
 // EpochClock.stamp (records.py) / mislo_submit: offset of ts from the epoch base

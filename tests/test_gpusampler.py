@@ -217,11 +217,12 @@ def test_queue_evictions_are_queue_delay_of_the_evicted_process(tmp_path):
     assert recs(s2.decide(0, 2 * DT)).size == 0 and s2.stats()["evictions"] == 1
 
 
-def test_records_reach_the_user_ring_and_the_guard_mask_sheds_them(tmp_path):
+@pytest.mark.parametrize("rec", [24, 16])
+def test_records_reach_the_user_ring_and_the_guard_mask_sheds_them(tmp_path, rec):
     k = Kfd(tmp_path)
     k.proc_on(100, [7])
     k.proc_on(200, [7])
-    ring = rt.HostRing(1 << 10, 24, "")
+    ring = rt.HostRing(1 << 10, rec, "")
     s = sampler(k, ring=ring)
     s.set_target_list([(100, 5)])
     s.set_hip_activity(100, launches=1)
@@ -233,8 +234,9 @@ def test_records_reach_the_user_ring_and_the_guard_mask_sheds_them(tmp_path):
     s.decide(1 << 40, 2 * DT)
     segs = ring.peek(16)
     assert sum(c for _, _, c in segs) == 1
-    u = np.frombuffer(ring.records_view()[:24].tobytes(), dtype=records.USER24)[0]
+    u = np.frombuffer(ring.records_view()[:rec].tobytes(), dtype=records.USER24 if rec == 24 else records.USER16)[0]
     assert (u["pid_sig"] >> 22) & 0x7F == 13 and (u["pod_ts"] & 0xFFFFF) == 5 and (u["pid_sig"] >> 30) & 1
+    assert not (u["pid_sig"] >> 31) & 1  # no trace: one slot
     s.mask = 0  # the overhead guard shed gpu_queue_delay_ms: no readings, no records
     for _ in range(3):
         s.sample()

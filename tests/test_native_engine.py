@@ -53,10 +53,11 @@ def test_extension_is_native():
     assert mod.__file__.endswith(".so") and mod.device_count() >= 1
 
 
-@pytest.mark.parametrize("user_rec", [64, 32, 24])
+@pytest.mark.parametrize("user_rec", [64, 32, 24, 16])
 def test_ring_windows_match_oracle(user_rec):
-    """user_rec 32 / 24: the user-space ring holds USER32 / USER24 records (the rocprof tool's compact forms,
-    svc|node from the device pod table)."""
+    """user_rec 32 / 24 / 16: the user-space ring holds USER32 / USER24 records / USER16 slots (the rocprof
+    tool's compact forms, svc|node from the device pod table; USER16 with traced records, whose trace
+    rides in a continuation slot)."""
     _check_ring_windows(user_rec, f"oracle{user_rec}")
 
 
@@ -74,6 +75,12 @@ def _check_ring_windows(user_rec, tag):
     from llm_slo_ebpf_toolkit_amd.pipeline.window import RingWindowSource, WindowPipeline, build_replay_images
 
     wins, gen = windows()
+    if user_rec == 16:  # a third of the GPU signals' records tagged with a request's trace (two slots each)
+        from llm_slo_ebpf_toolkit_amd.pipeline.window import kernel_event_mask
+
+        for w in wins:
+            gpu = np.nonzero(~kernel_event_mask(w.events))[0][::3]
+            w.events["trace_h"][gpu] = w.spans["trace_h"][np.arange(len(gpu)) % len(w.spans)]
     imgs = build_replay_images(wins, user_rec=user_rec)
     pipe = WindowPipeline(16384, 512, 8, model="bayes", learn=False, user_cap=4096)
     rb, user, spans = rings(tag, user_rec)
@@ -97,7 +104,10 @@ def _check_ring_windows(user_rec, tag):
         np.testing.assert_array_equal(pk["hist"].astype(np.int64), oracle.histograms(d))
         np.testing.assert_array_equal(pk["misc"][2:18].astype(np.int64), oracle.value_sums_milli(d))
         assert pk["ring_state"]["first_busy"] == -1
-        assert pk["ring_state"]["events"] == R.framed_event_count(img.framed) + len(img.user)
+        n_rec = int((img.user["pid_sig"] != R.USER16_CONT).sum()) if user_rec == 16 else len(img.user)
+        if user_rec == 16:
+            assert n_rec < len(img.user)  # continuation slots are rows, not records
+        assert pk["ring_state"]["events"] == R.framed_event_count(img.framed) + n_rec
         dbg = dict(zip(("candidates", "low_raw", "overlap", "fanout_dropped", "spans_enriched"),
                        pk["dbg"][:5].astype(np.int64).tolist()))
         for key in ("candidates", "fanout_dropped", "spans_enriched"):

@@ -126,6 +126,68 @@ def test_user24_windows_decode_like_user32():
             assert np.array_equal(getattr(a, f), getattr(b, f)), f
 
 
+def test_user16_roundtrip_and_continuation_slots():
+    """USER16 is USER24 without the trace hash: an untraced record is one 16-byte slot, a traced one
+    two (the record with pid_sig bit 31, then {trace lo, trace hi, USER16_CONT, 0}); decoded, the
+    records equal USER24's and the continuation slots are holes."""
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+
+    w = ReplayGenerator(ReplayConfig(scenario="full", events_per_window=4096, spans_per_window=64, seed=5)).next_window()
+    ev = w.events[w.events["signal_type"] < 127].copy()
+    ev["trace_h"][::4] = np.arange(len(ev[::4]), dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)
+    ev["trace_h"][1::4] = 0
+    u16 = records.to_user16(ev)
+    traced = ev["trace_h"] != 0
+    assert u16.itemsize == 16 and len(u16) == len(ev) + int(traced.sum())
+    v, cont = records.user16_to_user24(u16)
+    assert int(cont.sum()) == int(traced.sum())
+    u24 = records.to_user24(ev)
+    for f in u24.dtype.names:
+        assert np.array_equal(v[~cont][f], u24[f]), f
+    assert records.to_user(ev, 16).tobytes() == u16.tobytes()
+    bad = ev[:1].copy()
+    bad["signal_type"] = 127
+    with pytest.raises(ValueError):
+        records.to_user16(bad)
+
+
+def test_user16_windows_decode_like_user24():
+    """The oracle decode of the same windows with USER16 and USER24 user rings: identical rows once
+    the continuation slots (holes) are taken out, traced records keeping their traces."""
+    from llm_slo_ebpf_toolkit_amd.pipeline import oracle
+    from llm_slo_ebpf_toolkit_amd.pipeline.replay import ReplayConfig, ReplayGenerator
+    from llm_slo_ebpf_toolkit_amd.pipeline.window import build_replay_images, kernel_event_mask
+
+    def decoded(rec):
+        g = ReplayGenerator(ReplayConfig(scenario="full", n_nodes=2, pods_per_node=8, n_services=8,
+                                         events_per_window=3000, spans_per_window=100, seed=9))
+        wins = [g.next_window() for _ in range(2)]
+        for w in wins:
+            gpu = np.nonzero(~kernel_event_mask(w.events))[0][::2]
+            w.events["trace_h"][gpu] = w.spans["trace_h"][np.arange(len(gpu)) % len(w.spans)]
+        imgs = build_replay_images(wins, user_rec=rec)
+        sn = (g.pod_svc.astype(np.uint32) << np.uint32(16)) | g.pod_node.astype(np.uint32)
+        pod_sn = dict(zip(g.pod_ids.tolist(), sn.tolist()))
+        table, tmap = oracle.CtxTable(), oracle.TraceMap()
+        out = []
+        for img in imgs:
+            oracle.apply_ring_defs(img.framed, table, tmap, pod_sn)
+            d = oracle.decode_window(img.framed, img.user, table, tmap, img.bases, pod_sn=pod_sn)
+            n_k = records.framed_rows(img.framed)
+            keep = np.ones(len(d.ts), bool)
+            if rec == 16:
+                cont = img.user["pid_sig"] == np.uint32(records.USER16_CONT)
+                assert cont.any()
+                keep[n_k:] = ~cont
+                assert (d.slot[n_k:][cont] == oracle.NO_SLOT).all() and (d.ts[n_k:][cont] == 0).all()
+            out.append(oracle.take(d, keep))
+        return out
+
+    for a, b in zip(decoded(16), decoded(24)):
+        for f in a.__dataclass_fields__:
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
 def test_user24_window_without_epoch_is_refused():
     """WindowPipeline.submit refuses USER24 records with no epoch base to resolve them against
     (checked before the engine is touched, so this runs without a GPU)."""
