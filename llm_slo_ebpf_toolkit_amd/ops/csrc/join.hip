@@ -299,11 +299,13 @@ struct alignas(16) SpanPP {
 };
 
 constexpr int kLdsGroups = 64;
-// Probe workgroups per phase (3 per CU): ~1,400 phase-2 items pack into two near-full rounds
-// instead of a full round plus a third of one at 1,024, leaving CUs to the span stream.
-// K = 100 A/B, alternating on one box: 0.515 / 0.514 ms per step vs 0.525 / 0.518 at 1,024.
-constexpr int kProbeGrid = 768;
-constexpr int kSigPerItem = 4096;  // signals per work item (a partition's list is sliced); sweep: 256 498 us of compute, 1024 389, 2048 352, 4096 330, 8192 368 (staging repeats per item vs load balance)
+// Probe workgroups per phase (2 per CU) and signals per work item (a partition's list is sliced:
+// staging repeats per item vs load balance). Round 6 sweep on the USER16 tree, K = 100, one box
+// (profiles/r6_probe_sweep/): 512 x 6144 2.074 / 2.044 / 2.044 G events/s (chain 0.425-0.427 ms),
+// 768 x 4096 (round 5's choice) 2.042 / 2.035 / 2.019 / 2.019 / 2.008 G (0.437-0.441 ms); 512 x
+// 4096 2.02-2.05, 512 x 8192 2.004, 640 x 4096 2.010, 384 x 4096 1.959, x 2048 1.89-1.97.
+constexpr int kProbeGrid = 512;
+constexpr int kSigPerItem = 6144;
 
 // Work list for the two probe phases, rebuilt every window on the device (no host sync,
 // graph-capturable). One workgroup of kParts threads, one partition per thread:
