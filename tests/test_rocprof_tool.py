@@ -53,15 +53,15 @@ def test_runtime_c_abi_library_is_self_contained():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rec", [64, 32, 24])
+@pytest.mark.parametrize("rec", [64, 32, 24, 16])
 def test_tool_pushes_gpu_signals_into_ring(rec):
-    """rec 32 / 24: the ring was created with 32- / 24-byte records, so the tool writes USER32 /
-    USER24 (read back through USER32's fields; USER24 carries no node id)."""
+    """rec 32 / 24 / 16: the ring was created with 32- / 24- / 16-byte records, so the tool writes
+    USER32 / USER24 / USER16 (read back through USER32's fields; USER24 and USER16 carry no node id)."""
     from llm_slo_ebpf_toolkit_amd.collector import records
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    dt = {64: records.EVENT, 32: records.USER32, 24: records.USER24}[rec]
+    dt = {64: records.EVENT, 32: records.USER32, 24: records.USER24, 16: records.USER16}[rec]
     name = f"/mislo-test-{os.getpid()}-events{rec}"
     ring = rt.HostRing(1 << 16, rec, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", MISLO_WAIT_NEEDS_FOREIGN="0",
@@ -74,7 +74,10 @@ def test_tool_pushes_gpu_signals_into_ring(rec):
     view = ring.records_view()
     recs = np.concatenate([np.frombuffer(view[i * rec:(i + c) * rec].tobytes(), dtype=dt)
                            for _, i, c in segs]) if segs else np.zeros(0, dtype=dt)
-    if rec == 24:
+    if rec == 16:
+        v, cont = records.user16_to_user24(recs)
+        recs = v[~cont]
+    if rec in (16, 24):
         recs = records.user24_to_user32(recs, t0)
     types = set(recs["signal_type"].tolist())
     assert 13 in types, (types, r.stderr[-1000:])      # gpu_queue_delay_ms from kernel dispatches
@@ -85,7 +88,7 @@ def test_tool_pushes_gpu_signals_into_ring(rec):
 
     if torch.cuda.device_count() >= 2:
         pass  # exercised by tests/test_rocprof_tool.py::test_xgmi_peer_copies (multi-GPU runners)
-    assert (recs["pod_id"] == 7).all() and (rec == 24 or (recs["node_id"] == 3).all())
+    assert (recs["pod_id"] == 7).all() and (rec in (16, 24) or (recs["node_id"] == 3).all())
     assert (recs["flags"] & (1 << 8 if rec == 64 else 1)).all()
     ts = recs["ts_ns"]
     assert (ts > t0 - 10 * 10**9).all() and (ts < time.time_ns() + 10 * 10**9).all()  # wall clock
@@ -113,22 +116,27 @@ print("tag workload done")
 
 
 @pytest.mark.gpu
-def test_request_trace_tags_gpu_records():
+@pytest.mark.parametrize("rec", [32, 16])
+def test_request_trace_tags_gpu_records(rec):
     """A serving thread's mislo_rocprof_set_trace: the kernels it enqueues carry the request's
-    trace hash (trace-tier joins with the request's spans); after clearing, none do."""
+    trace hash (trace-tier joins with the request's spans); after clearing, none do. In a 16-byte
+    ring a tagged record takes two slots, its trace in the continuation."""
     from llm_slo_ebpf_toolkit_amd.collector import records
     from llm_slo_ebpf_toolkit_amd.runtime import load
 
     rt = load()
-    name = f"/mislo-test-{os.getpid()}-tag"
-    ring = rt.HostRing(1 << 16, 32, name)
+    name = f"/mislo-test-{os.getpid()}-tag{rec}"
+    ring = rt.HostRing(1 << 16, rec, name)
     env = dict(os.environ, ROCP_TOOL_LIBRARIES=TOOL, MISLO_RING=name, MISLO_QUEUE_FLOOR_NS="0", MISLO_WAIT_NEEDS_FOREIGN="0", PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-c", TAG_WORKLOAD], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     segs = ring.peek(1 << 16)
     view = ring.records_view()
-    recs = np.concatenate([np.frombuffer(view[i * 32:(i + c) * 32].tobytes(), dtype=records.USER32)
-                           for _, i, c in segs])
+    recs = np.concatenate([np.frombuffer(view[i * rec:(i + c) * rec].tobytes(),
+                                         dtype=records.USER32 if rec == 32 else records.USER16) for _, i, c in segs])
+    if rec == 16:
+        v, cont = records.user16_to_user24(recs)
+        recs = records.user24_to_user32(v[~cont], time.time_ns())
     q = recs[recs["signal_type"] == 13]
     # queue delays are emitted only for dispatches that waited with their queue free (most of the
     # back-to-back kernels here start as their predecessor ends): some of each half remain
