@@ -341,6 +341,18 @@ __device__ __forceinline__ void probe_work_body(const uint32_t* __restrict__ spa
   // the window's span time range (without generations: no pruning)
   const int64_t s_lo = gm ? ts_of_image(gm->span_lo) : INT64_MIN, s_hi = gm ? ts_of_image(gm->span_hi) : INT64_MAX;
   uint32_t ns[kKeyTypes], ng[kKeyTypes][kMaxGens], n[kKeyTypes][kMaxGens], nk[kKeyTypes];
+  // every list offset this thread may need, loaded up front: independent loads in flight together
+  // instead of one dependent round trip per (key type, generation) behind the pruning tests
+  uint32_t b_lo[kKeyTypes][kMaxGens], b_hi[kKeyTypes][kMaxGens];
+#pragma unroll
+  for (int a = 0; a < kMaxGens; ++a) {
+    const uint32_t* b = gc.base + (size_t)(a < gc.gens ? age_slot(gc, cur, a) : 0u) * kBaseLen;
+#pragma unroll
+    for (int k = 0; k < kKeyTypes; ++k) {
+      b_lo[k][a] = a < gc.gens ? b[k * kParts + p] : 0u;
+      b_hi[k][a] = a < gc.gens ? b[k * kParts + p + 1] : 0u;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kKeyTypes; ++k) {
     const int c = k * kParts + p;
@@ -358,8 +370,7 @@ __device__ __forceinline__ void probe_work_body(const uint32_t* __restrict__ spa
         const int64_t lo = max(ts_of_image(gm->tlo[slot]), gm->cut[a]), hi = ts_of_image(gm->thi[slot]);
         if (lo > hi || hi < s_lo - w || lo > s_hi + w) continue;  // nothing visible can pair
       }
-      const uint32_t* b = gc.base + (size_t)slot * kBaseLen;
-      ng[k][a] = b[c + 1] - b[c];
+      ng[k][a] = b_hi[k][a] - b_lo[k][a];
       n[k][a] = ng[k][a] == 0 ? 0u : min((ng[k][a] + sig_per_item - 1) / (uint32_t)sig_per_item, (uint32_t)kProbeMaxSplit);
       nk[k] += n[k][a];
     }
